@@ -1,0 +1,211 @@
+/*
+ * ORACLE / TEST INFRASTRUCTURE ONLY -- "parity oracle" for the MI355X
+ * admission engine.  A single-threaded C restatement of the reference's
+ * statistics-and-decision hot path (Alibaba Sentinel 1.8.4-SNAPSHOT, the
+ * Gepeng18/Sentinel fork) under a mocked TimeUtil clock: every call takes the
+ * virtual time `now` (ms) that TimeUtil.currentTimeMillis() would return.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library, and only as the checker.  The product (sentinel_amd/)
+ * never links or calls it.
+ *
+ * Path aliases (relative to the reference root):
+ *   CORE = sentinel-core/src/main/java/com/alibaba/csp/sentinel
+ *   PF   = sentinel-extension/sentinel-parameter-flow-control/src/main/java/com/alibaba/csp/sentinel
+ *   CS   = sentinel-cluster/sentinel-cluster-server-default/src/main/java/com/alibaba/csp/sentinel/cluster
+ *   RLS  = sentinel-cluster/sentinel-cluster-server-envoy-rls/src/main/java/com/alibaba/csp/sentinel/cluster/server/envoy/rls
+ *
+ * Parity pinning: the restatement is checked against the known-answer tests
+ * transcribed from the reference's JUnit suites (the JSON fixtures under tests/golden/, see
+ * tests/golden/README.md); Java could not be run in this container (no JDK).
+ */
+#ifndef SENTINEL_ORACLE_H
+#define SENTINEL_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- leap arrays (CORE/slots/statistic/base/LeapArray.java) ---------------- */
+enum orc_leap_kind {
+    ORC_LEAP_BUCKET = 0,     /* BucketLeapArray            CORE/slots/statistic/metric/BucketLeapArray.java */
+    ORC_LEAP_OCCUPIABLE = 1, /* OccupiableBucketLeapArray  CORE/slots/statistic/metric/occupy/OccupiableBucketLeapArray.java */
+    ORC_LEAP_FUTURE = 2,     /* FutureBucketLeapArray      CORE/slots/statistic/metric/occupy/FutureBucketLeapArray.java */
+    ORC_LEAP_CLUSTER = 3,    /* ClusterMetricLeapArray     CS/flow/statistic/metric/ClusterMetricLeapArray.java */
+    ORC_LEAP_UNARY = 4       /* UnaryLeapArray (LongAdder) CORE/slots/statistic/base/UnaryLeapArray.java */
+};
+
+/* MetricEvent ordinals (CORE/slots/statistic/MetricEvent.java:21-39) */
+enum { ORC_EV_PASS = 0, ORC_EV_BLOCK, ORC_EV_EXCEPTION, ORC_EV_SUCCESS, ORC_EV_RT, ORC_EV_OCCUPIED_PASS };
+/* ClusterFlowEvent ordinals (CS/flow/statistic/data/ClusterFlowEvent.java:22-52) */
+enum { ORC_CEV_PASS = 0, ORC_CEV_BLOCK, ORC_CEV_PASS_REQUEST, ORC_CEV_BLOCK_REQUEST, ORC_CEV_OCCUPIED_PASS,
+       ORC_CEV_OCCUPIED_BLOCK, ORC_CEV_WAITING };
+
+typedef struct orc_leap orc_leap;
+
+orc_leap *orc_leap_new(int kind, int sample_count, int interval_ms);
+void orc_leap_free(orc_leap *l);
+/* currentWindow(t): returns window start or INT64_MIN when t < 0 (null). */
+int64_t orc_leap_current_window(orc_leap *l, int64_t t);
+/* currentWindow(t).value().add(ev, n) */
+void orc_leap_add(orc_leap *l, int64_t t, int ev, int64_t n);
+void orc_leap_add_rt(orc_leap *l, int64_t t, int64_t rt);
+/* counter of the bucket that currentWindow(t) returns */
+int64_t orc_leap_current_get(orc_leap *l, int64_t t, int ev);
+/* values(t): sum of ev over valid buckets; *count receives the list size */
+int64_t orc_leap_values_sum(orc_leap *l, int64_t t, int ev, int *count);
+/* getPreviousWindow(t) evaluated at mocked clock `now`; returns 1 if non-null */
+int orc_leap_previous_window(orc_leap *l, int64_t t, int64_t now, int64_t *start, int64_t *pass);
+/* getValidHead(now); returns 1 if non-null */
+int orc_leap_valid_head(orc_leap *l, int64_t now, int64_t *start, int64_t *pass);
+/* occupiable only */
+void orc_leap_add_waiting(orc_leap *l, int64_t t, int n);
+int64_t orc_leap_current_waiting(orc_leap *l, int64_t now);
+/* getWindowValue(t).pass() or -1 when null */
+int64_t orc_leap_window_value_pass(orc_leap *l, int64_t t);
+
+/* ---- StatisticNode (CORE/node/StatisticNode.java) --------------------------- */
+typedef struct orc_node orc_node;
+orc_node *orc_node_new(void);
+void orc_node_free(orc_node *n);
+double orc_node_pass_qps(orc_node *n, int64_t now);
+double orc_node_block_qps(orc_node *n, int64_t now);
+double orc_node_success_qps(orc_node *n, int64_t now);
+double orc_node_exception_qps(orc_node *n, int64_t now);
+double orc_node_previous_pass_qps(orc_node *n, int64_t now);
+double orc_node_avg_rt(orc_node *n, int64_t now);
+double orc_node_min_rt(orc_node *n, int64_t now);
+double orc_node_occupied_pass_qps(orc_node *n, int64_t now);
+int64_t orc_node_total_pass(orc_node *n, int64_t now);
+int64_t orc_node_total_block(orc_node *n, int64_t now);
+int64_t orc_node_total_success(orc_node *n, int64_t now);
+int64_t orc_node_total_exception(orc_node *n, int64_t now);
+int32_t orc_node_cur_thread_num(orc_node *n);
+int64_t orc_node_waiting(orc_node *n, int64_t now);
+void orc_node_add_pass_request(orc_node *n, int64_t now, int count);
+void orc_node_add_rt_and_success(orc_node *n, int64_t now, int64_t rt, int count);
+void orc_node_increase_block_qps(orc_node *n, int64_t now, int count);
+void orc_node_increase_exception_qps(orc_node *n, int64_t now, int count);
+void orc_node_increase_thread_num(orc_node *n);
+void orc_node_decrease_thread_num(orc_node *n);
+int64_t orc_node_try_occupy_next(orc_node *n, int64_t now, int acquire, double threshold);
+void orc_node_add_waiting_request(orc_node *n, int64_t future_time, int acquire);
+void orc_node_add_occupied_pass(orc_node *n, int64_t now, int acquire);
+/* Mock node: passQps/previousPassQps/curThreadNum stubbed (Mockito in the JUnit tests). */
+orc_node *orc_node_new_mock(double pass_qps, double previous_pass_qps, int32_t threads);
+void orc_node_set_mock(orc_node *n, double pass_qps, double previous_pass_qps, int32_t threads);
+
+/* ---- traffic shaping controllers (CORE/slots/block/flow/controller) ------ */
+enum { ORC_CTRL_DEFAULT = 0, ORC_CTRL_WARM_UP = 1, ORC_CTRL_RATE_LIMITER = 2, ORC_CTRL_WARM_UP_RATE_LIMITER = 3 };
+enum { ORC_GRADE_THREAD = 0, ORC_GRADE_QPS = 1 };
+/* decision codes shared with include/sentinel_amd.h */
+enum { ORC_PASS = 0, ORC_BLOCK_FLOW = 1, ORC_BLOCK_PARAM = 2, ORC_BLOCK_DEGRADE = 3, ORC_PASS_WAIT = 4 };
+
+typedef struct orc_ctrl orc_ctrl;
+orc_ctrl *orc_ctrl_new(int behavior, int grade, double count, int warm_up_period_sec, int max_queueing_time_ms,
+                       int cold_factor);
+void orc_ctrl_free(orc_ctrl *c);
+/* rater.canPass(node, acquire, prioritized) at mocked time `now`.  Returns an
+ * ORC_* decision; *wait_ms receives the sleep the reference would perform. */
+int orc_ctrl_can_pass(orc_ctrl *c, orc_node *node, int64_t now, int acquire, int prioritized, int64_t *wait_ms);
+/* state peeks for parity tests */
+int64_t orc_ctrl_latest_passed_time(const orc_ctrl *c);
+int64_t orc_ctrl_stored_tokens(const orc_ctrl *c);
+int64_t orc_ctrl_last_filled_time(const orc_ctrl *c);
+int32_t orc_ctrl_warning_token(const orc_ctrl *c);
+int32_t orc_ctrl_max_token(const orc_ctrl *c);
+double orc_ctrl_slope(const orc_ctrl *c);
+
+/* ---- local flow engine: StatisticSlot + FlowSlot replay (one default ctx) -- */
+typedef struct orc_flow_rule {
+    uint32_t resource;     /* dense resource id (the engine's name table is host side) */
+    int32_t grade;         /* RuleConstant.FLOW_GRADE_* */
+    double count;
+    int32_t control_behavior;
+    int32_t warm_up_period_sec;
+    int32_t max_queueing_time_ms;
+    int32_t strategy;      /* only DIRECT(0) is supported by the engine */
+} orc_flow_rule;
+
+typedef struct orc_flow orc_flow;
+orc_flow *orc_flow_new(uint32_t n_resources, int cold_factor);
+void orc_flow_free(orc_flow *f);
+/* FlowRuleManager.loadRules: validity filter, rater regenerated (controller
+ * state reset), node statistics kept.  Returns #valid rules. */
+int orc_flow_load_rules(orc_flow *f, const orc_flow_rule *rules, size_t n);
+/* SphU.entry(resource, type, acquire) -> decision (ORC_*), wait ms */
+int orc_flow_entry(orc_flow *f, uint32_t resource, int64_t now, int acquire, int prioritized, int64_t *wait_ms);
+/* Entry.exit for a PASSED entry: rt = now - createTimestamp supplied by caller */
+void orc_flow_exit(orc_flow *f, uint32_t resource, int64_t now, int64_t rt, int count, int error);
+orc_node *orc_flow_node(orc_flow *f, uint32_t resource);
+/* batch replay: events in order; kind 0 = entry, 1 = exit */
+void orc_flow_replay(orc_flow *f, size_t n, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
+                     const int32_t *acquire, const uint8_t *flags, const int64_t *rt, int8_t *decision,
+                     int32_t *wait_ms);
+
+/* ---- cluster token server (CS/flow) ---------------------------------------- */
+typedef struct orc_cluster_rule {
+    int64_t flow_id;
+    double count;
+    int32_t threshold_type; /* ClusterRuleConstant.FLOW_THRESHOLD_AVG_LOCAL=0 / GLOBAL=1 */
+    int32_t sample_count;   /* ClusterFlowConfig.sampleCount (default 10) */
+    int32_t window_interval_ms;
+    int32_t grade;          /* must be QPS for token requests */
+    int32_t strategy;       /* ClusterFlowConfig.strategy (NORMAL=0) */
+} orc_cluster_rule;
+
+typedef struct orc_token_result {
+    int32_t status;     /* TokenResultStatus */
+    int32_t remaining;
+    int32_t wait_in_ms;
+} orc_token_result;
+
+typedef struct orc_cluster orc_cluster;
+orc_cluster *orc_cluster_new(double exceed_count, double max_occupy_ratio);
+void orc_cluster_free(orc_cluster *c);
+/* ClusterFlowRuleManager.loadRules(namespace, rules); returns #applied */
+int orc_cluster_load_rules(orc_cluster *c, const char *ns, const orc_cluster_rule *rules, size_t n);
+/* ClusterServerConfigManager namespace QPS limiter (GlobalRequestLimiter.initIfAbsent) */
+void orc_cluster_set_namespace_limit(orc_cluster *c, const char *ns, double max_allowed_qps);
+void orc_cluster_set_connected_count(orc_cluster *c, const char *ns, int32_t n);
+/* DefaultTokenService.requestToken(flowId, acquire, prioritized) at `now` */
+orc_token_result orc_cluster_request_token(orc_cluster *c, int64_t flow_id, int32_t acquire, int prioritized,
+                                           int64_t now);
+/* SimpleClusterFlowChecker (Envoy RLS) on the same metric store */
+orc_token_result orc_cluster_request_token_simple(orc_cluster *c, int64_t flow_id, int32_t acquire, int64_t now);
+void orc_cluster_replay(orc_cluster *c, size_t n, const int64_t *flow_id, const int32_t *acquire,
+                        const uint8_t *prio, const int64_t *ts, orc_token_result *out);
+/* sum of a ClusterFlowEvent over valid buckets of flow's metric at now (ClusterMetric.getSum) */
+int64_t orc_cluster_metric_sum(orc_cluster *c, int64_t flow_id, int ev, int64_t now);
+/* standalone ClusterMetric (CS/flow/statistic/metric/ClusterMetric.java) for KATs */
+typedef struct orc_cmetric orc_cmetric;
+orc_cmetric *orc_cmetric_new(int sample_count, int interval_ms);
+void orc_cmetric_free(orc_cmetric *m);
+void orc_cmetric_add(orc_cmetric *m, int64_t now, int ev, int64_t n);
+int64_t orc_cmetric_sum(orc_cmetric *m, int64_t now, int ev);
+double orc_cmetric_avg(orc_cmetric *m, int64_t now, int ev);
+int32_t orc_cmetric_try_occupy_next(orc_cmetric *m, int64_t now, int ev, int32_t acquire, double threshold);
+/* RequestLimiter (CS/flow/statistic/limit/RequestLimiter.java) */
+typedef struct orc_limiter orc_limiter;
+orc_limiter *orc_limiter_new(double qps_allowed);
+void orc_limiter_free(orc_limiter *l);
+void orc_limiter_add(orc_limiter *l, int64_t now, int x);
+int64_t orc_limiter_sum(orc_limiter *l, int64_t now);
+double orc_limiter_qps(orc_limiter *l, int64_t now);
+int orc_limiter_can_pass(orc_limiter *l, int64_t now);
+int orc_limiter_try_pass(orc_limiter *l, int64_t now);
+
+/* ---- Java numerics exposed for tests ---------------------------------------- */
+int64_t orc_java_round(double d);
+double orc_java_next_up(double d);
+int32_t orc_java_d2i(double d);
+int64_t orc_java_d2l(double d);
+int32_t orc_java_string_hash(const char *utf8);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,327 @@
+"""ctypes binding to the ORACLE (oracle/build/liboracle.so) and the interpreter
+for the transcribed known-answer scenarios in tests/golden/kat_*.json.
+
+Test infrastructure only: the oracle is the checker, never the thing measured
+or shipped.
+"""
+import ctypes as C
+import glob
+import json
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+
+EV = {"PASS": 0, "BLOCK": 1, "EXCEPTION": 2, "SUCCESS": 3, "RT": 4, "OCCUPIED_PASS": 5}
+CEV = {"PASS": 0, "BLOCK": 1, "PASS_REQUEST": 2, "BLOCK_REQUEST": 3, "OCCUPIED_PASS": 4, "OCCUPIED_BLOCK": 5,
+       "WAITING": 6}
+LEAP_KIND = {"bucket": 0, "occupiable": 1, "future": 2, "cluster": 3, "unary": 4}
+DECISION = {"PASS": 0, "BLOCK": 1, "BLOCK_PARAM": 2, "BLOCK_DEGRADE": 3, "PASS_WAIT": 4}
+TOKEN_STATUS = {"BAD_REQUEST": -4, "TOO_MANY_REQUEST": -2, "FAIL": -1, "OK": 0, "BLOCKED": 1, "SHOULD_WAIT": 2,
+                "NO_RULE_EXISTS": 3}
+
+
+class OrcFlowRule(C.Structure):
+    _fields_ = [("resource", C.c_uint32), ("grade", C.c_int32), ("count", C.c_double),
+                ("control_behavior", C.c_int32), ("warm_up_period_sec", C.c_int32),
+                ("max_queueing_time_ms", C.c_int32), ("strategy", C.c_int32)]
+
+
+class OrcClusterRule(C.Structure):
+    _fields_ = [("flow_id", C.c_int64), ("count", C.c_double), ("threshold_type", C.c_int32),
+                ("sample_count", C.c_int32), ("window_interval_ms", C.c_int32), ("grade", C.c_int32),
+                ("strategy", C.c_int32)]
+
+
+class OrcTokenResult(C.Structure):
+    _fields_ = [("status", C.c_int32), ("remaining", C.c_int32), ("wait_in_ms", C.c_int32)]
+
+
+_lib = None
+
+
+def build_oracle():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(ORACLE_SO):
+        build_oracle()
+    L = C.CDLL(ORACLE_SO)
+    P, I64, I32, D, U32 = C.c_void_p, C.c_int64, C.c_int32, C.c_double, C.c_uint32
+    sigs = {
+        "orc_leap_new": (P, [C.c_int, C.c_int, C.c_int]),
+        "orc_leap_free": (None, [P]),
+        "orc_leap_current_window": (I64, [P, I64]),
+        "orc_leap_add": (None, [P, I64, C.c_int, I64]),
+        "orc_leap_current_get": (I64, [P, I64, C.c_int]),
+        "orc_leap_values_sum": (I64, [P, I64, C.c_int, C.POINTER(C.c_int)]),
+        "orc_leap_previous_window": (C.c_int, [P, I64, I64, C.POINTER(I64), C.POINTER(I64)]),
+        "orc_leap_valid_head": (C.c_int, [P, I64, C.POINTER(I64), C.POINTER(I64)]),
+        "orc_leap_add_waiting": (None, [P, I64, C.c_int]),
+        "orc_leap_current_waiting": (I64, [P, I64]),
+        "orc_node_new": (P, []),
+        "orc_node_new_mock": (P, [D, D, I32]),
+        "orc_node_set_mock": (None, [P, D, D, I32]),
+        "orc_node_free": (None, [P]),
+        "orc_node_pass_qps": (D, [P, I64]),
+        "orc_node_total_pass": (I64, [P, I64]),
+        "orc_ctrl_new": (P, [C.c_int, C.c_int, D, C.c_int, C.c_int, C.c_int]),
+        "orc_ctrl_free": (None, [P]),
+        "orc_ctrl_can_pass": (C.c_int, [P, P, I64, C.c_int, C.c_int, C.POINTER(I64)]),
+        "orc_flow_new": (P, [U32, C.c_int]),
+        "orc_flow_free": (None, [P]),
+        "orc_flow_load_rules": (C.c_int, [P, C.POINTER(OrcFlowRule), C.c_size_t]),
+        "orc_flow_entry": (C.c_int, [P, U32, I64, C.c_int, C.c_int, C.POINTER(I64)]),
+        "orc_flow_exit": (None, [P, U32, I64, I64, C.c_int, C.c_int]),
+        "orc_flow_replay": (None, [P, C.c_size_t, P, P, P, P, P, P, P, P]),
+        "orc_flow_node": (P, [P, U32]),
+        "orc_cluster_new": (P, [D, D]),
+        "orc_cluster_free": (None, [P]),
+        "orc_cluster_load_rules": (C.c_int, [P, C.c_char_p, C.POINTER(OrcClusterRule), C.c_size_t]),
+        "orc_cluster_set_namespace_limit": (None, [P, C.c_char_p, D]),
+        "orc_cluster_set_connected_count": (None, [P, C.c_char_p, I32]),
+        "orc_cluster_request_token": (OrcTokenResult, [P, I64, I32, C.c_int, I64]),
+        "orc_cluster_request_token_simple": (OrcTokenResult, [P, I64, I32, I64]),
+        "orc_cluster_replay": (None, [P, C.c_size_t, P, P, P, P, P]),
+        "orc_cluster_metric_sum": (I64, [P, I64, C.c_int, I64]),
+        "orc_cmetric_new": (P, [C.c_int, C.c_int]),
+        "orc_cmetric_free": (None, [P]),
+        "orc_cmetric_add": (None, [P, I64, C.c_int, I64]),
+        "orc_cmetric_sum": (I64, [P, I64, C.c_int]),
+        "orc_cmetric_avg": (D, [P, I64, C.c_int]),
+        "orc_cmetric_try_occupy_next": (I32, [P, I64, C.c_int, I32, D]),
+        "orc_limiter_new": (P, [D]),
+        "orc_limiter_free": (None, [P]),
+        "orc_limiter_add": (None, [P, I64, C.c_int]),
+        "orc_limiter_sum": (I64, [P, I64]),
+        "orc_limiter_qps": (D, [P, I64]),
+        "orc_limiter_can_pass": (C.c_int, [P, I64]),
+        "orc_limiter_try_pass": (C.c_int, [P, I64]),
+        "orc_java_round": (I64, [D]),
+        "orc_java_next_up": (D, [D]),
+        "orc_java_d2i": (I32, [D]),
+        "orc_java_d2l": (I64, [D]),
+        "orc_java_string_hash": (I32, [C.c_char_p]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def flow_rules_array(rules):
+    arr = (OrcFlowRule * max(1, len(rules)))()
+    for i, r in enumerate(rules):
+        arr[i].resource = r["resource"]
+        arr[i].grade = r.get("grade", 1)
+        arr[i].count = r["count"]
+        arr[i].control_behavior = r.get("control_behavior", 0)
+        arr[i].warm_up_period_sec = r.get("warm_up_period_sec", 10)
+        arr[i].max_queueing_time_ms = r.get("max_queueing_time_ms", 500)
+        arr[i].strategy = r.get("strategy", 0)
+    return arr
+
+
+def cluster_rules_array(rules):
+    arr = (OrcClusterRule * max(1, len(rules)))()
+    for i, r in enumerate(rules):
+        arr[i].flow_id = r["flow_id"]
+        arr[i].count = r["count"]
+        arr[i].threshold_type = r.get("threshold_type", 0)
+        arr[i].sample_count = r.get("sample_count", 10)
+        arr[i].window_interval_ms = r.get("window_interval_ms", 1000)
+        arr[i].grade = r.get("grade", 1)
+        arr[i].strategy = r.get("strategy", 0)
+    return arr
+
+
+def load_scenarios():
+    out = []
+    for p in sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "kat_*.json"))):
+        with open(p) as f:
+            out.append(json.load(f))
+    return out
+
+
+class ScenarioFailure(AssertionError):
+    pass
+
+
+def run_scenario(sc, base):
+    """Replays one transcribed scenario against the oracle at virtual base time `base`."""
+    L = lib()
+    objs = {}
+    now = base
+
+    def T(v):
+        if v == "now":
+            return now
+        if isinstance(v, dict):
+            b = base - base % v["window"]
+            return b + v["aligned_plus"]
+        return base + v
+
+    def check(cond, op, got):
+        if not cond:
+            raise ScenarioFailure(f"{sc['name']} @base={base}: op {op} got {got}")
+
+    frees = []
+    try:
+        for op in sc["ops"]:
+            k = op["op"]
+            if k == "set_time":
+                now = base + op["t"]
+            elif k == "sleep":
+                now += op["ms"]
+            elif k == "leap_new":
+                h = L.orc_leap_new(LEAP_KIND[op["kind"]], op["sample_count"], op["interval_ms"])
+                objs[op["id"]] = h
+                frees.append((L.orc_leap_free, h))
+            elif k == "leap_current_window":
+                got = L.orc_leap_current_window(objs[op["id"]], T(op["t"]))
+                if "expect_start" in op:
+                    check(got == T(op["expect_start"]), op, got)
+            elif k == "leap_add":
+                ev = op["event"] if isinstance(op["event"], int) else EV[op["event"]]
+                L.orc_leap_add(objs[op["id"]], T(op["t"]), ev, op["n"])
+            elif k == "leap_current_get":
+                got = L.orc_leap_current_get(objs[op["id"]], T(op["t"]), EV[op["event"]])
+                check(got == op["expect"], op, got)
+            elif k == "leap_values_sum":
+                cnt = C.c_int()
+                got = L.orc_leap_values_sum(objs[op["id"]], T(op["t"]), EV[op["event"]], C.byref(cnt))
+                check(got == op["expect"] and cnt.value == op.get("expect_count", cnt.value), op, (got, cnt.value))
+            elif k == "leap_add_waiting":
+                L.orc_leap_add_waiting(objs[op["id"]], T(op["t"]), op["n"])
+            elif k == "leap_current_waiting":
+                got = L.orc_leap_current_waiting(objs[op["id"]], now)
+                check(got == op["expect"], op, got)
+            elif k == "leap_previous_window":
+                st, ps = C.c_int64(), C.c_int64()
+                ok = L.orc_leap_previous_window(objs[op["id"]], T(op["t"]), now, C.byref(st), C.byref(ps))
+                if op.get("expect_null"):
+                    check(ok == 0, op, ok)
+                else:
+                    check(ok == 1 and st.value == T(op["expect_start"]), op, (ok, st.value))
+            elif k == "leap_valid_head":
+                st, ps = C.c_int64(), C.c_int64()
+                ok = L.orc_leap_valid_head(objs[op["id"]], now, C.byref(st), C.byref(ps))
+                if op.get("expect_null"):
+                    check(ok == 0, op, ok)
+                else:
+                    check(ok == 1 and st.value == T(op["expect_start"]), op, (ok, st.value))
+            elif k == "ctrl_new":
+                h = L.orc_ctrl_new(op["behavior"], op["grade"], float(op["count"]), op.get("warm_up_period_sec", 10),
+                                   op.get("max_queueing_time_ms", 500), op.get("cold_factor", 3))
+                objs[op["id"]] = h
+                frees.append((L.orc_ctrl_free, h))
+            elif k == "node_mock":
+                if op["id"] not in objs:
+                    h = L.orc_node_new_mock(op["pass_qps"], op["prev_pass_qps"], op["threads"])
+                    objs[op["id"]] = h
+                    frees.append((L.orc_node_free, h))
+                else:
+                    L.orc_node_set_mock(objs[op["id"]], op["pass_qps"], op["prev_pass_qps"], op["threads"])
+            elif k == "ctrl_can_pass":
+                w = C.c_int64()
+                d = L.orc_ctrl_can_pass(objs[op["id"]], objs[op["node"]], now, op["acquire"],
+                                        1 if op.get("prio") else 0, C.byref(w))
+                if "expect" in op:
+                    want = DECISION[op["expect"]]
+                    check(d == want, op, d)
+                if "expect_wait" in op:
+                    check(w.value == op["expect_wait"], op, w.value)
+                if op.get("sleep_wait"):
+                    now += w.value
+            elif k == "flow_new":
+                h = L.orc_flow_new(op["n_resources"], op.get("cold_factor", 3))
+                objs[op["id"]] = h
+                frees.append((L.orc_flow_free, h))
+            elif k == "flow_load":
+                arr = flow_rules_array(op["rules"])
+                L.orc_flow_load_rules(objs[op["id"]], arr, len(op["rules"]))
+            elif k == "flow_entry":
+                w = C.c_int64()
+                d = L.orc_flow_entry(objs[op["id"]], op["resource"], now, op["acquire"], 1 if op.get("prio") else 0,
+                                     C.byref(w))
+                check(d == DECISION[op["expect"]], op, d)
+            elif k == "flow_exit":
+                L.orc_flow_exit(objs[op["id"]], op["resource"], now, op["rt"], op["count"], 1 if op.get("error") else 0)
+            elif k == "flow_loop":
+                per_sec = {}
+                t0 = now
+                for ms in range(op["ms"]):
+                    t = t0 + ms
+                    for _ in range(op["per_ms"]):
+                        d = L.orc_flow_entry(objs[op["id"]], op["resource"], t, 1, 0, None)
+                        if d == 0:
+                            sec = (t - t0) // 1000
+                            per_sec[sec] = per_sec.get(sec, 0) + 1
+                            L.orc_flow_exit(objs[op["id"]], op["resource"], t, 0, 1, 0)
+                got = [per_sec.get(s, 0) for s in range(len(op["expect_pass_per_second"]))]
+                check(got == op["expect_pass_per_second"], op, got)
+                now = t0 + op["ms"]
+            elif k == "cm_new":
+                h = L.orc_cmetric_new(op["sample_count"], op["interval_ms"])
+                objs[op["id"]] = h
+                frees.append((L.orc_cmetric_free, h))
+            elif k == "cm_add":
+                L.orc_cmetric_add(objs[op["id"]], now, CEV[op["event"]], op["n"])
+            elif k == "cm_sum":
+                got = L.orc_cmetric_sum(objs[op["id"]], now, CEV[op["event"]])
+                check(got == op["expect"], op, got)
+            elif k == "cm_avg":
+                got = L.orc_cmetric_avg(objs[op["id"]], now, CEV[op["event"]])
+                check(abs(got - op["expect"]) <= op.get("tol", 0), op, got)
+            elif k == "cm_try_occupy_next":
+                got = L.orc_cmetric_try_occupy_next(objs[op["id"]], now, CEV["PASS"], op["acquire"],
+                                                    float(op["threshold"]))
+                check(got == op["expect"], op, got)
+            elif k == "lim_new":
+                h = L.orc_limiter_new(float(op["qps"]))
+                objs[op["id"]] = h
+                frees.append((L.orc_limiter_free, h))
+            elif k == "lim_add":
+                L.orc_limiter_add(objs[op["id"]], now, op["n"])
+            elif k == "lim_can_pass":
+                got = bool(L.orc_limiter_can_pass(objs[op["id"]], now))
+                check(got == op["expect"], op, got)
+            elif k == "lim_try_pass":
+                got = bool(L.orc_limiter_try_pass(objs[op["id"]], now))
+                check(got == op["expect"], op, got)
+            elif k == "lim_sum":
+                got = L.orc_limiter_sum(objs[op["id"]], now)
+                check(got == op["expect"], op, got)
+            elif k == "lim_qps":
+                got = L.orc_limiter_qps(objs[op["id"]], now)
+                check(abs(got - op["expect"]) <= op.get("tol", 0), op, got)
+            elif k == "cl_new":
+                h = L.orc_cluster_new(op.get("exceed_count", 1.0), op.get("max_occupy_ratio", 1.0))
+                objs[op["id"]] = h
+                frees.append((L.orc_cluster_free, h))
+            elif k == "cl_load":
+                arr = cluster_rules_array(op["rules"])
+                L.orc_cluster_load_rules(objs[op["id"]], op["namespace"].encode(), arr, len(op["rules"]))
+            elif k == "cl_request":
+                r = L.orc_cluster_request_token(objs[op["id"]], op["flow_id"], op["acquire"],
+                                                1 if op.get("prio") else 0, now)
+                check(r.status == TOKEN_STATUS[op["expect_status"]], op, (r.status, r.remaining, r.wait_in_ms))
+                if "expect_wait" in op:
+                    check(r.wait_in_ms == op["expect_wait"], op, r.wait_in_ms)
+                if "expect_remaining" in op:
+                    check(r.remaining == op["expect_remaining"], op, r.remaining)
+            else:
+                # ops handled by extension oracles (param flow / degrade) live in their own harnesses
+                from tests import oracle_harness_ext  # noqa: F401
+                oracle_harness_ext.run_op(L, sc, base, op, objs, frees, now, check)
+    finally:
+        for fn, h in reversed(frees):
+            fn(h)
