@@ -1,0 +1,87 @@
+"""ctypes binding of libsentinel_amd.so (include/sentinel_amd.h).
+
+The HIP library is the only implementation: if it is missing or cannot load,
+importing the engine raises -- there is no CPU fallback in the product path.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsentinel_amd.so")
+
+
+class SgaConfig(C.Structure):
+    _fields_ = [("device", C.c_int32), ("max_batch", C.c_uint32), ("max_rules", C.c_uint32),
+                ("cold_factor", C.c_int32), ("statistic_max_rt", C.c_int32), ("reserved0", C.c_int32),
+                ("exceed_count", C.c_double), ("max_occupy_ratio", C.c_double)]
+
+
+class SgaClusterFlowRule(C.Structure):
+    _fields_ = [("flow_id", C.c_int64), ("count", C.c_double), ("threshold_type", C.c_int32),
+                ("sample_count", C.c_int32), ("window_interval_ms", C.c_int32), ("grade", C.c_int32),
+                ("strategy", C.c_int32), ("reserved", C.c_int32)]
+
+
+class SgaTokenResult(C.Structure):
+    _fields_ = [("remaining", C.c_int32), ("wait_in_ms", C.c_int16), ("status", C.c_int8), ("reserved", C.c_int8)]
+
+
+class SgaFlowRule(C.Structure):
+    _fields_ = [("resource", C.c_uint32), ("grade", C.c_int32), ("count", C.c_double),
+                ("control_behavior", C.c_int32), ("warm_up_period_sec", C.c_int32),
+                ("max_queueing_time_ms", C.c_int32), ("strategy", C.c_int32)]
+
+
+# (restype, argtypes) for every exported symbol; tests check this list against include/*.h
+SIGNATURES = {
+    "sga_abi_version": (C.c_int, []),
+    "sga_config_default": (None, [C.POINTER(SgaConfig)]),
+    "sga_create": (C.c_int, [C.POINTER(SgaConfig), C.POINTER(C.c_void_p)]),
+    "sga_destroy": (C.c_int, [C.c_void_p]),
+    "sga_last_error": (C.c_char_p, [C.c_void_p]),
+    "sga_engine_stream": (C.c_void_p, [C.c_void_p]),
+    "sga_load_cluster_flow_rules": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(SgaClusterFlowRule), C.c_size_t]),
+    "sga_set_namespace_limit": (C.c_int, [C.c_void_p, C.c_char_p, C.c_double]),
+    "sga_set_connected_count": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
+    "sga_request_tokens": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                     C.c_void_p]),
+    "sga_request_tokens_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
+                                            C.c_size_t, C.c_void_p, C.c_void_p]),
+    "sga_cluster_metric_sums": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.POINTER(C.c_int64)]),
+    "sga_cluster_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "sga_rls_should_rate_limit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.c_void_p, C.c_void_p]),
+}
+
+_lib = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load():
+    """Loads the HIP engine library; raises if it is absent (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EngineError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                          " (or `make -C sentinel_amd/csrc`)")
+    L = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc, engine=None, what=""):
+    if rc < 0:
+        msg = ""
+        if engine is not None:
+            m = load().sga_last_error(engine)
+            msg = m.decode() if m else ""
+        raise EngineError(f"{what} failed rc={rc} {msg}")
+    return rc

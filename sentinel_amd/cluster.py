@@ -1,0 +1,218 @@
+"""Host-side mirror of the reference's cluster token-server interface.
+
+Same names and argument meaning as the Java API the engine replaces:
+  TokenService.requestToken(Long ruleId, int acquireCount, boolean prioritized)
+      CORE/cluster/TokenService.java:36  -> DefaultTokenService.request_token / request_tokens
+  ClusterFlowRuleManager.loadRules(String namespace, List<FlowRule> rules)
+      CS/flow/rule/ClusterFlowRuleManager.java:254-260 -> ClusterFlowRuleManager.load_rules
+  TokenResult / TokenResultStatus  CORE/cluster/TokenResult.java, CORE/cluster/TokenResultStatus.java:27-60
+Every decision is computed by the HIP engine (libsentinel_amd.so); the mocked
+TimeUtil clock of the reference tests is the explicit `now`/`ts` argument.
+"""
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import SgaClusterFlowRule, SgaConfig, SgaTokenResult, check
+
+
+class TokenResultStatus:
+    BAD_REQUEST = -4
+    TOO_MANY_REQUEST = -2
+    FAIL = -1
+    OK = 0
+    BLOCKED = 1
+    SHOULD_WAIT = 2
+    NO_RULE_EXISTS = 3
+    NO_REF_RULE_EXISTS = 4
+    NOT_AVAILABLE = 5
+    RELEASE_OK = 6
+    ALREADY_RELEASE = 7
+
+
+class ClusterRuleConstant:
+    FLOW_CLUSTER_STRATEGY_NORMAL = 0
+    FLOW_THRESHOLD_AVG_LOCAL = 0
+    FLOW_THRESHOLD_GLOBAL = 1
+    DEFAULT_CLUSTER_SAMPLE_COUNT = 10
+
+
+class ClusterFlowEvent:
+    PASS, BLOCK, PASS_REQUEST, BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK, WAITING = range(7)
+
+
+@dataclass
+class TokenResult:
+    status: int
+    remaining: int = 0
+    wait_in_ms: int = 0
+
+
+@dataclass
+class ClusterFlowConfig:
+    flow_id: Optional[int] = None
+    threshold_type: int = ClusterRuleConstant.FLOW_THRESHOLD_AVG_LOCAL
+    sample_count: int = ClusterRuleConstant.DEFAULT_CLUSTER_SAMPLE_COUNT
+    window_interval_ms: int = 1000
+    strategy: int = ClusterRuleConstant.FLOW_CLUSTER_STRATEGY_NORMAL
+
+
+@dataclass
+class FlowRule:
+    resource: str = ""
+    count: float = 0.0
+    grade: int = 1  # RuleConstant.FLOW_GRADE_QPS
+    cluster_mode: bool = False
+    cluster_config: ClusterFlowConfig = field(default_factory=ClusterFlowConfig)
+
+
+class Engine:
+    """Owns one sga_engine (one GPU / one shard)."""
+
+    def __init__(self, device: int = 0, max_batch: int = 1 << 20, max_rules: int = 1 << 16,
+                 exceed_count: float = 1.0, max_occupy_ratio: float = 1.0):
+        L = _lib.load()
+        cfg = SgaConfig()
+        L.sga_config_default(C.byref(cfg))
+        cfg.device = device
+        cfg.max_batch = max_batch
+        cfg.max_rules = max_rules
+        cfg.exceed_count = exceed_count
+        cfg.max_occupy_ratio = max_occupy_ratio
+        h = C.c_void_p()
+        rc = L.sga_create(C.byref(cfg), C.byref(h))
+        if rc < 0:
+            raise _lib.EngineError(f"sga_create failed rc={rc}")
+        self._h = h
+        self.max_batch = max_batch
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            _lib.load().sga_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def _rules_array(rules: List[FlowRule]):
+    arr = (SgaClusterFlowRule * max(1, len(rules)))()
+    for i, r in enumerate(rules):
+        cc = r.cluster_config
+        arr[i].flow_id = cc.flow_id if cc.flow_id is not None else 0
+        arr[i].count = r.count
+        arr[i].threshold_type = cc.threshold_type
+        arr[i].sample_count = cc.sample_count
+        arr[i].window_interval_ms = cc.window_interval_ms
+        arr[i].grade = r.grade
+        arr[i].strategy = cc.strategy
+    return arr
+
+
+class ClusterFlowRuleManager:
+    """CS/flow/rule/ClusterFlowRuleManager.java mirror bound to one engine."""
+
+    def __init__(self, engine: Engine):
+        self.engine = engine
+
+    def load_rules(self, namespace: str, rules: List[FlowRule]) -> int:
+        rules = [r for r in rules if r.cluster_mode]  # applyClusterFlowRule skips !isClusterMode
+        arr = _rules_array(rules)
+        rc = _lib.load().sga_load_cluster_flow_rules(self.engine.handle, namespace.encode(), arr, len(rules))
+        return check(rc, self.engine.handle, "loadRules")
+
+    def load_rule_arrays(self, namespace: str, flow_id, count, threshold_type=1, sample_count=10,
+                         window_interval_ms=1000) -> int:
+        """Bulk form for large rule sets (numpy arrays)."""
+        n = len(flow_id)
+        dt = np.dtype([("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"), ("sample_count", "<i4"),
+                       ("window_interval_ms", "<i4"), ("grade", "<i4"), ("strategy", "<i4"), ("reserved", "<i4")])
+        a = np.zeros(n, dtype=dt)
+        a["flow_id"] = flow_id
+        a["count"] = count
+        a["threshold_type"] = threshold_type
+        a["sample_count"] = sample_count
+        a["window_interval_ms"] = window_interval_ms
+        a["grade"] = 1
+        ptr = a.ctypes.data_as(C.POINTER(SgaClusterFlowRule))
+        rc = _lib.load().sga_load_cluster_flow_rules(self.engine.handle, namespace.encode(), ptr, n)
+        return check(rc, self.engine.handle, "loadRules")
+
+    def set_connected_count(self, namespace: str, n: int):
+        check(_lib.load().sga_set_connected_count(self.engine.handle, namespace.encode(), n), self.engine.handle)
+
+
+TOKEN_DTYPE = np.dtype([("remaining", "<i4"), ("wait_in_ms", "<i2"), ("status", "i1"), ("reserved", "i1")])
+
+
+class DefaultTokenService:
+    """CS/flow/DefaultTokenService.java mirror: requests are decided in order under a mocked clock."""
+
+    def __init__(self, engine: Engine):
+        self.engine = engine
+
+    def request_tokens(self, flow_id, acquire, prioritized, ts) -> np.ndarray:
+        fid = np.ascontiguousarray(flow_id, dtype=np.int64)
+        acq = np.ascontiguousarray(acquire, dtype=np.int32)
+        pr = np.ascontiguousarray(prioritized, dtype=np.uint8)
+        t = np.ascontiguousarray(ts, dtype=np.int64)
+        n = len(fid)
+        out = np.zeros(n, dtype=TOKEN_DTYPE)
+        rc = _lib.load().sga_request_tokens(self.engine.handle, fid.ctypes.data, acq.ctypes.data, pr.ctypes.data,
+                                            t.ctypes.data, n, out.ctypes.data)
+        check(rc, self.engine.handle, "requestToken")
+        return out
+
+    def request_token(self, rule_id: int, acquire_count: int, prioritized: bool, now: int) -> TokenResult:
+        r = self.request_tokens([rule_id], [acquire_count], [1 if prioritized else 0], [now])[0]
+        return TokenResult(int(r["status"]), int(r["remaining"]), int(r["wait_in_ms"]))
+
+    def metric_sums(self, flow_id: int, now: int) -> List[int]:
+        out = (C.c_int64 * 7)()
+        check(_lib.load().sga_cluster_metric_sums(self.engine.handle, flow_id, now, out), self.engine.handle)
+        return list(out)
+
+
+class EnvoyRlsService:
+    """RLS/SentinelEnvoyRlsServiceImpl.shouldRateLimit mirror over batches of requests."""
+
+    OK = 1
+    OVER_LIMIT = 2
+
+    def __init__(self, engine: Engine):
+        self.engine = engine
+
+    @staticmethod
+    def generate_flow_id(key: str) -> int:
+        # EnvoySentinelRuleConverter.generateFlowId: (long) Integer.MAX_VALUE + key.hashCode()
+        from .javautil import string_hash_code
+        return 2147483647 + string_hash_code(key)
+
+    def should_rate_limit(self, desc_offsets, desc_flow_id, hits_addend, ts):
+        off = np.ascontiguousarray(desc_offsets, dtype=np.uint32)
+        fid = np.ascontiguousarray(desc_flow_id, dtype=np.int64)
+        hits = np.ascontiguousarray(hits_addend, dtype=np.int32)
+        t = np.ascontiguousarray(ts, dtype=np.int64)
+        nreq = len(hits)
+        st = np.zeros(len(fid), dtype=np.int8)
+        code = np.zeros(nreq, dtype=np.int32)
+        rc = _lib.load().sga_rls_should_rate_limit(self.engine.handle, off.ctypes.data, nreq, fid.ctypes.data,
+                                                   hits.ctypes.data, t.ctypes.data, st.ctypes.data, code.ctypes.data)
+        check(rc, self.engine.handle, "shouldRateLimit")
+        return code, st

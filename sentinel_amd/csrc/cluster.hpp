@@ -1,0 +1,82 @@
+// Device-side state and launch interface of the cluster token server path
+// (ClusterFlowChecker + ClusterMetric over ClusterMetricLeapArray).
+#pragma once
+#include "common.hpp"
+#include "radix_sort.hpp"
+
+namespace sga {
+
+// Per rule slot, read-only during a batch (48 bytes).
+struct SlotParam {
+    double thr;         // calcGlobalThreshold(rule) * exceedCount   ClusterFlowChecker.java:38-48,68
+    double thr_simple;  // rule.count * exceedCount                  SimpleClusterFlowChecker.java:43
+    double isec;        // LeapArray.intervalInSecond = intervalInMs / 1000.0  LeapArray.java:68
+    uint32_t boff;      // first bucket of this slot's ClusterMetricLeapArray
+    int32_t S;          // sampleCount of the metric (fixed at metric creation)
+    int32_t W;          // windowLengthInMs = interval / sampleCount
+    int32_t interval;   // intervalInMs
+    int32_t active;     // rule present (FLOW_RULES contains the flowId)
+    int32_t ns;         // namespace index
+};
+
+// Per slot mutable occupy state: ClusterMetricLeapArray.occupyCounter/hasOccupied
+struct SlotOcc {
+    int64_t occ_pass;   // occupyCounter[PASS]
+    int64_t occ_preq;   // occupyCounter[PASS_REQUEST]
+    int32_t has_occ;    // hasOccupied
+    int32_t pad;
+};
+
+// Bucket field ordinals = ClusterFlowEvent ordinals.
+enum : int { CEV_PASS = 0, CEV_BLOCK, CEV_PASS_REQUEST, CEV_BLOCK_REQUEST, CEV_OCCUPIED_PASS, CEV_OCCUPIED_BLOCK,
+             CEV_WAITING, CEV_N };
+
+struct ClusterState {
+    const SlotParam *param;
+    SlotOcc *occ;
+    int64_t *bstart;         // [nbuckets] window start or kAbsent
+    int64_t *cnt[CEV_N];     // [nbuckets] LongAdder sums per ClusterFlowEvent
+    const int64_t *hkeys;    // open-addressing flowId -> slot
+    const uint32_t *hvals;
+    uint32_t hmask;
+    uint32_t nslots;
+    double max_occupy_ratio;
+};
+
+// Per-batch scratch (device), sized for max_batch events.
+struct BatchScratch {
+    uint32_t *keys[2];
+    Payload *pay[2];
+    uint32_t *ev_run;   // run id per sorted event
+    uint32_t *ev_cp;    // prioritized events before this one in its run
+    // run records
+    uint32_t *run_start, *run_end, *run_slot, *run_t0off, *run_cp;
+    int32_t *run_amin, *run_amax;
+    int64_t *run_s0;
+    uint32_t *run_f, *run_cpf, *run_cw;
+    uint8_t *run_mode;
+    uint32_t *flow_first_run;
+    // tile scan
+    void *tile_agg;
+    void *tile_carry;
+    uint32_t *counters;  // [0]=nvalid [1]=nruns [2]=nflows [3]=flags
+    RadixScratch radix;
+    size_t cap = 0;
+};
+
+size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap);
+void batch_scratch_carve(BatchScratch &b, void *base, size_t cap, uint32_t nslots_cap);
+
+// Runs the whole decision pipeline for one batch on `stream` (asynchronous).
+// simple != 0 selects SimpleClusterFlowChecker semantics (Envoy RLS).
+void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
+                          const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, int simple,
+                          void *out /* sga_token_result */, hipStream_t stream);
+
+// ClusterMetric.getSum for all 7 events at `now` (rotates the current window as the reference does).
+void cluster_metric_sums(const ClusterState &st, uint32_t slot, int64_t now, int64_t *d_out7, hipStream_t stream);
+
+// Fills bucket range [b0, b1) with kAbsent / zero counters.
+void cluster_init_buckets(const ClusterState &st, uint32_t b0, uint32_t b1, hipStream_t stream);
+
+}  // namespace sga

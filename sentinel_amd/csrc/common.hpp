@@ -1,0 +1,118 @@
+// Shared helpers for the MI355X admission engine (gfx950, HIP).
+// Java numeric semantics are restated here for device code (independently of
+// the oracle): JLS 5.1.3 narrowing casts, Math.round, Math.nextUp.
+// All translation units are compiled with -ffp-contract=off so double
+// expressions round exactly like the JVM (no FMA contraction).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#define SGA_HD __host__ __device__ __forceinline__
+
+namespace sga {
+
+constexpr int64_t kAbsent = INT64_MIN;  // "array.get(idx) == null" for a window slot
+
+SGA_HD int32_t j_d2i(double d) {
+    if (d != d) return 0;
+    if (d >= 2147483647.0) return INT32_MAX;
+    if (d <= -2147483648.0) return INT32_MIN;
+    return (int32_t)d;
+}
+
+SGA_HD int64_t j_d2l(double d) {
+    if (d != d) return 0;
+    if (d >= 9223372036854775807.0) return INT64_MAX;
+    if (d <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)d;
+}
+
+// Math.round(double): nearest long, ties toward +infinity, NaN -> 0, saturating.
+SGA_HD int64_t j_round(double a) {
+    uint64_t bits = (uint64_t)__builtin_bit_cast(int64_t, a);
+    int64_t biased_exp = (int64_t)((bits & 0x7FF0000000000000ULL) >> 52);
+    int64_t shift = 1074 - biased_exp;
+    if (shift >= 0 && shift < 64) {
+        int64_t r = (int64_t)((bits & 0x000FFFFFFFFFFFFFULL) | 0x0010000000000000ULL);
+        if ((int64_t)bits < 0) r = -r;
+        return ((r >> shift) + 1) >> 1;
+    }
+    if (shift >= 64) return 0;
+    return j_d2l(a);
+}
+
+// Math.nextUp(double)
+SGA_HD double j_next_up(double d) {
+    if (d != d) return d;
+    int64_t b = __builtin_bit_cast(int64_t, d);
+    if (b == 0x7FF0000000000000LL) return d;  // +inf
+    if (d == 0.0) return __builtin_bit_cast(double, (int64_t)1);  // +MIN_VALUE for +0/-0
+    b += (b >= 0) ? 1 : -1;
+    return __builtin_bit_cast(double, b);
+}
+
+SGA_HD uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+SGA_HD uint64_t hash_flow_id(int64_t id) { return splitmix64((uint64_t)id ^ 0x5EB7F00DULL); }
+
+}  // namespace sga
+
+struct sga_error_sink {
+    std::string msg;
+};
+
+#define SGA_HIP_CHECK(expr)                                                                        \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess) {                                                                    \
+            throw sga::HipError(std::string(#expr) + ": " + hipGetErrorString(_e), __FILE__, __LINE__); \
+        }                                                                                          \
+    } while (0)
+
+namespace sga {
+struct HipError {
+    std::string what;
+    HipError(std::string w, const char *f, int l) : what(std::move(w) + " @" + f + ":" + std::to_string(l)) {}
+};
+
+// Minimal owning device buffer.
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void alloc(size_t count) {
+        release();
+        if (count == 0) return;
+        SGA_HIP_CHECK(hipMalloc((void **)&p, count * sizeof(T)));
+        n = count;
+    }
+    // grow preserving contents (stream-ordered copy); fill is done by caller
+    void grow(size_t count, hipStream_t s) {
+        if (count <= n) return;
+        T *q = nullptr;
+        SGA_HIP_CHECK(hipMalloc((void **)&q, count * sizeof(T)));
+        if (p && n) SGA_HIP_CHECK(hipMemcpyAsync(q, p, n * sizeof(T), hipMemcpyDeviceToDevice, s));
+        SGA_HIP_CHECK(hipStreamSynchronize(s));
+        if (p) (void)hipFree(p);
+        p = q;
+        n = count;
+    }
+    size_t bytes() const { return n * sizeof(T); }
+};
+}  // namespace sga

@@ -1,0 +1,520 @@
+// Host side of the admission engine: rule management (the ClusterFlowRuleManager
+// mirror), device state ownership and the extern "C" ABI of include/sentinel_amd.h.
+#include "../../include/sentinel_amd.h"
+#include "cluster.hpp"
+#include "flow.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace sga {
+
+struct SlotHost {
+    int64_t flow_id = 0;
+    bool allocated = false;  // ClusterMetricStatistics holds a metric for flow_id
+    bool active = false;     // FLOW_RULES holds the rule
+    int ns = -1;
+    double count = 0;
+    int threshold_type = 0;
+    int S = 0, interval = 0;  // metric geometry, fixed at metric creation (putMetricIfAbsent)
+    uint32_t boff = 0, bcap = 0;
+};
+
+struct NamespaceHost {
+    std::string name;
+    int32_t connected = 0;
+    bool has_limit = false;
+    double max_qps = 0;
+};
+
+struct Engine {
+    sga_config cfg{};
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::mutex mu;
+
+    // ---- cluster rules (host mirror)
+    std::vector<SlotHost> slots;
+    std::vector<uint32_t> free_slots;
+    std::unordered_map<int64_t, uint32_t> slot_of;  // flowId -> slot (metric exists)
+    std::vector<NamespaceHost> nss;
+    uint32_t bucket_used = 0;
+
+    // ---- device state
+    DevBuf<SlotParam> d_param;
+    DevBuf<SlotOcc> d_occ;
+    DevBuf<int64_t> d_bstart;
+    DevBuf<int64_t> d_cnt[CEV_N];
+    DevBuf<int64_t> d_hkeys;
+    DevBuf<uint32_t> d_hvals;
+    uint32_t hmask = 0;
+    DevBuf<uint8_t> d_scratch;
+    BatchScratch scratch;
+    uint32_t scratch_slots_cap = 0;
+    // host API staging
+    DevBuf<int64_t> d_in_fid;
+    DevBuf<int32_t> d_in_acq;
+    DevBuf<uint8_t> d_in_prio;
+    DevBuf<uint32_t> d_in_ts;
+    DevBuf<uint64_t> d_out;
+    DevBuf<int64_t> d_tmp7;
+
+    // ---- local flow engine
+    FlowEngine flow;
+
+    ClusterState state() const {
+        ClusterState st{};
+        st.param = d_param.p;
+        st.occ = d_occ.p;
+        st.bstart = d_bstart.p;
+        for (int k = 0; k < CEV_N; ++k) st.cnt[k] = d_cnt[k].p;
+        st.hkeys = d_hkeys.p;
+        st.hvals = d_hvals.p;
+        st.hmask = hmask;
+        st.nslots = (uint32_t)slots.size();
+        st.max_occupy_ratio = cfg.max_occupy_ratio;
+        return st;
+    }
+
+    int ns_index(const char *ns, bool create) {
+        for (size_t i = 0; i < nss.size(); ++i)
+            if (nss[i].name == ns) return (int)i;
+        if (!create) return -1;
+        NamespaceHost h;
+        h.name = ns;
+        nss.push_back(h);
+        return (int)nss.size() - 1;
+    }
+
+    void ensure_scratch() {
+        const uint32_t need_slots = std::max<uint32_t>((uint32_t)slots.size(), 1024u);
+        if (d_scratch.p && need_slots <= scratch_slots_cap) return;
+        uint32_t cap_slots = std::max<uint32_t>(need_slots, cfg.max_rules);
+        // round to the next power of two so the radix digit layout fits
+        uint32_t p2 = 1024;
+        while (p2 < cap_slots) p2 <<= 1;
+        const size_t bytes = batch_scratch_bytes(cfg.max_batch, p2);
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+        d_scratch.alloc(bytes);
+        batch_scratch_carve(scratch, d_scratch.p, cfg.max_batch, p2);
+        scratch_slots_cap = p2;
+    }
+
+    uint32_t alloc_slot() {
+        if (!free_slots.empty()) {
+            uint32_t s = free_slots.back();
+            free_slots.pop_back();
+            return s;
+        }
+        slots.emplace_back();
+        return (uint32_t)slots.size() - 1;
+    }
+
+    // Upload param table + hash table; init buckets of new metrics.
+    void sync_device(const std::vector<uint32_t> &fresh) {
+        const size_t ns = slots.size();
+        // capacity growth
+        const size_t slot_cap = std::max<size_t>(ns, 1);
+        if (d_param.n < slot_cap) {
+            size_t c = std::max<size_t>(slot_cap, d_param.n * 2);
+            d_param.grow(c, stream);
+            d_occ.grow(c, stream);
+        }
+        if (d_bstart.n < std::max<uint32_t>(bucket_used, 1)) {
+            size_t c = std::max<size_t>(bucket_used, d_bstart.n * 2);
+            d_bstart.grow(c, stream);
+            for (int k = 0; k < CEV_N; ++k) d_cnt[k].grow(c, stream);
+        }
+        // param table
+        std::vector<SlotParam> hp(ns);
+        for (size_t i = 0; i < ns; ++i) {
+            const SlotHost &h = slots[i];
+            SlotParam &p = hp[i];
+            std::memset(&p, 0, sizeof(p));
+            if (!h.allocated) continue;
+            const int conn = h.ns >= 0 ? nss[h.ns].connected : 0;
+            // ClusterFlowChecker.calcGlobalThreshold(rule) * exceedCount, :38-48,68
+            const double base = h.threshold_type == 1 ? h.count : h.count * (double)conn;
+            p.thr = base * cfg.exceed_count;
+            p.thr_simple = h.count * cfg.exceed_count;  // SimpleClusterFlowChecker.java:43
+            p.isec = h.interval / 1000.0;
+            p.boff = h.boff;
+            p.S = h.S;
+            p.W = h.interval / h.S;
+            p.interval = h.interval;
+            p.active = h.active ? 1 : 0;
+            p.ns = h.ns;
+        }
+        if (ns) SGA_HIP_CHECK(hipMemcpyAsync(d_param.p, hp.data(), ns * sizeof(SlotParam), hipMemcpyHostToDevice, stream));
+        // hash table over active rules
+        size_t nact = 0;
+        for (auto &h : slots) nact += h.active ? 1 : 0;
+        size_t hcap = 1024;
+        while (hcap < 2 * nact + 1) hcap <<= 1;
+        std::vector<int64_t> hk(hcap, 0);
+        std::vector<uint32_t> hv(hcap, 0);
+        for (size_t i = 0; i < ns; ++i) {
+            if (!slots[i].active) continue;
+            uint32_t h = (uint32_t)hash_flow_id(slots[i].flow_id) & (uint32_t)(hcap - 1);
+            while (hk[h] != 0) h = (h + 1) & (uint32_t)(hcap - 1);
+            hk[h] = slots[i].flow_id;
+            hv[h] = (uint32_t)i;
+        }
+        if (d_hkeys.n != hcap) {
+            SGA_HIP_CHECK(hipStreamSynchronize(stream));
+            d_hkeys.alloc(hcap);
+            d_hvals.alloc(hcap);
+        }
+        SGA_HIP_CHECK(hipMemcpyAsync(d_hkeys.p, hk.data(), hcap * 8, hipMemcpyHostToDevice, stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(d_hvals.p, hv.data(), hcap * 4, hipMemcpyHostToDevice, stream));
+        hmask = (uint32_t)(hcap - 1);
+        // fresh metrics: empty windows, no occupy
+        ClusterState st = state();
+        for (uint32_t s : fresh) {
+            cluster_init_buckets(st, slots[s].boff, slots[s].boff + slots[s].bcap, stream);
+            SGA_HIP_CHECK(hipMemsetAsync(d_occ.p + s, 0, sizeof(SlotOcc), stream));
+        }
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+        ensure_scratch();
+    }
+};
+
+}  // namespace sga
+
+struct sga_engine {
+    sga::Engine impl;
+};
+
+using sga::Engine;
+using sga::SlotHost;
+using sga::CEV_N;
+
+template <typename F>
+static int guarded(sga_engine *e, F &&f) {
+    if (!e) return SGA_EINVAL;
+    std::lock_guard<std::mutex> lk(e->impl.mu);
+    try {
+        return f(e->impl);
+    } catch (const sga::HipError &h) {
+        e->impl.err = h.what;
+        return SGA_EIO;
+    } catch (const std::bad_alloc &) {
+        e->impl.err = "out of host memory";
+        return SGA_ENOMEM;
+    }
+}
+
+extern "C" {
+
+int sga_abi_version(void) { return SGA_ABI_VERSION; }
+
+void sga_config_default(sga_config *c) {
+    if (!c) return;
+    std::memset(c, 0, sizeof(*c));
+    c->device = 0;
+    c->max_batch = 1u << 20;
+    c->max_rules = 1u << 16;
+    c->cold_factor = 3;          // SentinelConfig.DEFAULT_COLD_FACTOR
+    c->statistic_max_rt = 5000;  // SentinelConfig.DEFAULT_STATISTIC_MAX_RT
+    c->exceed_count = 1.0;       // ServerFlowConfig.DEFAULT_EXCEED_COUNT
+    c->max_occupy_ratio = 1.0;   // ServerFlowConfig.DEFAULT_MAX_OCCUPY_RATIO
+}
+
+int sga_create(const sga_config *cfg, sga_engine **out) {
+    if (!out) return SGA_EINVAL;
+    *out = nullptr;
+    sga_config c;
+    if (cfg) c = *cfg;
+    else sga_config_default(&c);
+    if (c.max_batch == 0 || c.max_batch > (1u << 30)) return SGA_EINVAL;
+    if (c.cold_factor <= 1) c.cold_factor = 3;  // SentinelConfig.coldFactor() fallback, :224-238
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= c.device || c.device < 0) return SGA_ENODEV;
+    sga_engine *e = new (std::nothrow) sga_engine();
+    if (!e) return SGA_ENOMEM;
+    e->impl.cfg = c;
+    int rc = guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(c.device));
+        hipDeviceProp_t prop;
+        SGA_HIP_CHECK(hipGetDeviceProperties(&prop, c.device));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            g.err = std::string("device is ") + prop.gcnArchName + ", engine is built for gfx950";
+            return SGA_ENODEV;
+        }
+        SGA_HIP_CHECK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
+        g.d_tmp7.alloc(8);
+        g.flow.init(c, g.stream);
+        g.ensure_scratch();
+        return SGA_OK;
+    });
+    if (rc != SGA_OK) {
+        delete e;
+        return rc;
+    }
+    *out = e;
+    return SGA_OK;
+}
+
+int sga_destroy(sga_engine *e) {
+    if (!e) return SGA_EINVAL;
+    {
+        std::lock_guard<std::mutex> lk(e->impl.mu);
+        if (e->impl.stream) {
+            (void)hipStreamSynchronize(e->impl.stream);
+            e->impl.flow.release();
+            (void)hipStreamDestroy(e->impl.stream);
+        }
+    }
+    delete e;
+    return SGA_OK;
+}
+
+const char *sga_last_error(const sga_engine *e) { return e ? e->impl.err.c_str() : "null engine"; }
+
+void *sga_engine_stream(sga_engine *e) { return e ? (void *)e->impl.stream : nullptr; }
+
+// ClusterFlowRuleManager.applyClusterFlowRule, CS/flow/rule/ClusterFlowRuleManager.java:325-374
+int sga_load_cluster_flow_rules(sga_engine *e, const char *ns, const sga_cluster_flow_rule *rules, size_t n) {
+    if (!ns || !*ns || (n && !rules)) return SGA_EINVAL;  // AssertUtil.notEmpty(namespace)
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        const int nsi = g.ns_index(ns, true);
+        std::vector<uint32_t> fresh;
+        if (n == 0) {  // clearAndResetRulesFor: rules dropped, metrics kept (:281-296)
+            for (auto &h : g.slots)
+                if (h.allocated && h.ns == nsi) h.active = false;
+            g.sync_device(fresh);
+            return 0;
+        }
+        std::unordered_map<int64_t, const sga_cluster_flow_rule *> rule_map;
+        std::vector<int64_t> order;
+        for (size_t i = 0; i < n; ++i) {
+            const sga_cluster_flow_rule &r = rules[i];
+            // FlowRuleUtil.isValidRule + checkClusterField (FlowRuleUtil.java:176-231)
+            if (!(r.count >= 0 && r.grade >= 0 && r.strategy >= 0)) continue;
+            if (r.flow_id <= 0) continue;
+            if (!(r.sample_count > 0 && r.window_interval_ms > 0 && r.window_interval_ms % r.sample_count == 0))
+                continue;
+            if (r.strategy != 0) continue;
+            if (!rule_map.count(r.flow_id)) order.push_back(r.flow_id);
+            rule_map[r.flow_id] = &r;  // ruleMap.put: last one wins
+        }
+        // clearAndResetRulesConditional: flowIds of this namespace not in the new map lose rule AND metric
+        for (uint32_t s = 0; s < g.slots.size(); ++s) {
+            SlotHost &h = g.slots[s];
+            if (!h.allocated || h.ns != nsi || !h.active) continue;
+            if (rule_map.count(h.flow_id)) continue;
+            h.active = false;
+            h.allocated = false;
+            g.slot_of.erase(h.flow_id);
+            g.free_slots.push_back(s);
+        }
+        for (int64_t fid : order) {
+            const sga_cluster_flow_rule &r = *rule_map[fid];
+            auto it = g.slot_of.find(fid);
+            uint32_t s;
+            if (it == g.slot_of.end()) {  // putMetricIfAbsent -> new ClusterMetric(sampleCount, windowIntervalMs)
+                s = g.alloc_slot();
+                SlotHost &h = g.slots[s];
+                const uint32_t need = (uint32_t)r.sample_count;
+                if (h.bcap < need) {
+                    h.boff = g.bucket_used;
+                    h.bcap = need;
+                    g.bucket_used += need;
+                }
+                h.flow_id = fid;
+                h.allocated = true;
+                h.S = r.sample_count;
+                h.interval = r.window_interval_ms;
+                g.slot_of[fid] = s;
+                fresh.push_back(s);
+            } else {
+                s = it->second;  // existing metric keeps its geometry and counters
+            }
+            SlotHost &h = g.slots[s];
+            h.active = true;
+            h.ns = nsi;
+            h.count = r.count;
+            h.threshold_type = r.threshold_type;
+        }
+        g.sync_device(fresh);
+        return (int)order.size();
+    });
+}
+
+int sga_set_namespace_limit(sga_engine *e, const char *ns, double max_allowed_qps) {
+    if (!ns || !*ns || !(max_allowed_qps >= 0)) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        (void)g.ns_index(ns, true);
+        g.err = "namespace QPS limiter (GlobalRequestLimiter) is not implemented on the device path yet";
+        return SGA_ENOSYS;
+    });
+}
+
+int sga_set_connected_count(sga_engine *e, const char *ns, int32_t connected) {
+    if (!ns || !*ns || connected < 0) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        const int i = g.ns_index(ns, true);
+        g.nss[i].connected = connected;
+        std::vector<uint32_t> none;
+        g.sync_device(none);
+        return SGA_OK;
+    });
+}
+
+static bool any_limit(const Engine &g) {
+    for (auto &n : g.nss)
+        if (n.has_limit) return true;
+    return false;
+}
+
+int sga_request_tokens_device(sga_engine *e, const int64_t *d_flow_id, const int32_t *d_acquire,
+                              const uint8_t *d_prio, int64_t ts_base, const uint32_t *d_ts_off, size_t n,
+                              sga_token_result *d_out, void *hip_stream) {
+    if (n && (!d_flow_id || !d_acquire || !d_ts_off || !d_out)) return SGA_EINVAL;
+    if (ts_base < 0) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        if (n > g.cfg.max_batch) return SGA_ERANGE;
+        if (any_limit(g)) return SGA_EINVAL;
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        hipStream_t s = hip_stream ? (hipStream_t)hip_stream : g.stream;
+        sga::cluster_decide_batch(g.state(), g.scratch, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off, (uint32_t)n,
+                                  0, d_out, s);
+        SGA_HIP_CHECK(hipGetLastError());
+        return SGA_OK;
+    });
+}
+
+static int run_host_batch(Engine &g, const int64_t *flow_id, const int32_t *acquire, const uint8_t *prio,
+                          const int64_t *ts, size_t n, uint64_t *out, int simple) {
+    SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+    const size_t cap = g.cfg.max_batch;
+    if (g.d_in_fid.n < cap) {
+        g.d_in_fid.alloc(cap);
+        g.d_in_acq.alloc(cap);
+        g.d_in_prio.alloc(cap);
+        g.d_in_ts.alloc(cap);
+        g.d_out.alloc(cap);
+    }
+    std::vector<uint32_t> off;
+    for (size_t b = 0; b < n;) {
+        // chunk: at most cap events and a timestamp span that fits u32 offsets
+        size_t m = std::min(cap, n - b);
+        int64_t lo = ts[b], hi = ts[b];
+        for (size_t i = 0; i < m; ++i) {
+            const int64_t t = ts[b + i];
+            if (t < 0) return SGA_EINVAL;  // LeapArray.currentWindow(t < 0) returns null
+            const int64_t nlo = std::min(lo, t), nhi = std::max(hi, t);
+            if (nhi - nlo > (int64_t)0xFFFFFFFFLL) {
+                m = i;
+                break;
+            }
+            lo = nlo;
+            hi = nhi;
+        }
+        off.resize(m);
+        for (size_t i = 0; i < m; ++i) off[i] = (uint32_t)(ts[b + i] - lo);
+        SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_fid.p, flow_id + b, m * 8, hipMemcpyHostToDevice, g.stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_acq.p, acquire + b, m * 4, hipMemcpyHostToDevice, g.stream));
+        if (prio) SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_prio.p, prio + b, m, hipMemcpyHostToDevice, g.stream));
+        else SGA_HIP_CHECK(hipMemsetAsync(g.d_in_prio.p, 0, m, g.stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_ts.p, off.data(), m * 4, hipMemcpyHostToDevice, g.stream));
+        sga::cluster_decide_batch(g.state(), g.scratch, g.d_in_fid.p, g.d_in_acq.p, g.d_in_prio.p, lo, g.d_in_ts.p,
+                                  (uint32_t)m, simple, g.d_out.p, g.stream);
+        SGA_HIP_CHECK(hipGetLastError());
+        SGA_HIP_CHECK(hipMemcpyAsync(out + b, g.d_out.p, m * 8, hipMemcpyDeviceToHost, g.stream));
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        b += m;
+    }
+    return SGA_OK;
+}
+
+int sga_request_tokens(sga_engine *e, const int64_t *flow_id, const int32_t *acquire, const uint8_t *prio,
+                       const int64_t *ts, size_t n, sga_token_result *out) {
+    if (n && (!flow_id || !acquire || !ts || !out)) return SGA_EINVAL;
+    static_assert(sizeof(sga_token_result) == 8, "token result is 8 bytes");
+    return guarded(e, [&](Engine &g) {
+        if (any_limit(g)) return SGA_EINVAL;
+        return run_host_batch(g, flow_id, acquire, prio, ts, n, (uint64_t *)out, 0);
+    });
+}
+
+int sga_cluster_metric_sums(sga_engine *e, int64_t flow_id, int64_t now, int64_t *out7) {
+    if (!out7 || now < 0) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        auto it = g.slot_of.find(flow_id);
+        if (it == g.slot_of.end()) return SGA_EINVAL;
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        sga::cluster_metric_sums(g.state(), it->second, now, g.d_tmp7.p, g.stream);
+        SGA_HIP_CHECK(hipMemcpyAsync(out7, g.d_tmp7.p, 7 * 8, hipMemcpyDeviceToHost, g.stream));
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        return SGA_OK;
+    });
+}
+
+int sga_cluster_stats(sga_engine *e, uint64_t *n_active, uint64_t *state_bytes) {
+    return guarded(e, [&](Engine &g) {
+        uint64_t a = 0;
+        for (auto &h : g.slots) a += h.active ? 1 : 0;
+        if (n_active) *n_active = a;
+        if (state_bytes)
+            *state_bytes = (uint64_t)g.bucket_used * 8 * (1 + CEV_N) + g.slots.size() * (sizeof(sga::SlotParam) +
+                                                                                      sizeof(sga::SlotOcc));
+        return SGA_OK;
+    });
+}
+
+// SentinelEnvoyRlsServiceImpl.shouldRateLimit, RLS/SentinelEnvoyRlsServiceImpl.java:51-101
+int sga_rls_should_rate_limit(sga_engine *e, const uint32_t *desc_offsets, size_t n_requests,
+                              const int64_t *desc_flow_id, const int32_t *hits_addend, const int64_t *ts,
+                              int8_t *desc_status, int32_t *code) {
+    if (n_requests && (!desc_offsets || !hits_addend || !ts || !code)) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        const size_t nd = desc_offsets[n_requests];
+        std::vector<int64_t> fid;
+        std::vector<int32_t> acq;
+        std::vector<int64_t> t;
+        std::vector<size_t> where;
+        fid.reserve(nd);
+        for (size_t r = 0; r < n_requests; ++r) {
+            int32_t a = hits_addend[r];
+            if (a < 0) continue;  // onError(IllegalArgumentException): no descriptor is checked
+            if (a == 0) a = 1;    // "Not present, use the default 1"
+            for (uint32_t d = desc_offsets[r]; d < desc_offsets[r + 1]; ++d) {
+                fid.push_back(desc_flow_id[d]);
+                acq.push_back(a);
+                t.push_back(ts[r]);
+                where.push_back(d);
+            }
+        }
+        std::vector<uint64_t> res(fid.size());
+        int rc = fid.empty() ? SGA_OK
+                             : run_host_batch(g, fid.data(), acq.data(), nullptr, t.data(), fid.size(), res.data(), 1);
+        if (rc != SGA_OK) return rc;
+        std::vector<int8_t> st(nd, 0);
+        for (size_t k = 0; k < res.size(); ++k) {
+            int8_t s = (int8_t)(res[k] >> 48);
+            if (s == SGA_TOKEN_NO_RULE_EXISTS) s = SGA_TOKEN_OK;  // absent rule passes
+            st[where[k]] = s;
+        }
+        for (size_t r = 0; r < n_requests; ++r) {
+            if (hits_addend[r] < 0) {
+                code[r] = -1;
+                continue;
+            }
+            bool blocked = false;
+            for (uint32_t d = desc_offsets[r]; d < desc_offsets[r + 1]; ++d) blocked |= st[d] != SGA_TOKEN_OK;
+            code[r] = blocked ? 2 : 1;  // Code.OVER_LIMIT : Code.OK
+        }
+        if (desc_status)
+            for (size_t d = 0; d < nd; ++d) desc_status[d] = st[d];
+        return SGA_OK;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,32 @@
+#pragma once
+#include "common.hpp"
+
+namespace sga {
+
+// 12-byte payload carried through the sort: original index, timestamp offset,
+// acquire count with the prioritized flag in bit 31.
+struct Payload {
+    uint32_t idx;
+    uint32_t ts_off;
+    uint32_t acq_prio;
+};
+
+constexpr int kMaxDigitBits = 11;
+
+struct RadixScratch {
+    uint32_t *hist = nullptr;       // radix_hist_entries(n, bits)
+    uint32_t *hist_scan = nullptr;  // same size
+    uint32_t *partial = nullptr;    // scan_partials_needed(hist entries)
+};
+
+size_t radix_tiles(size_t n);
+size_t radix_hist_entries(size_t n, int bits);
+size_t scan_partials_needed(size_t n);
+void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, uint32_t *partial, hipStream_t s);
+
+// Stable sort by the low `bits` bits of keys.  Returns the number of passes;
+// the sorted data is in (keys, pay) when it is even, in the alt buffers when odd.
+int radix_sort_pairs(uint32_t *keys, Payload *pay, uint32_t *keys_alt, Payload *pay_alt, size_t n, int bits,
+                     RadixScratch &sc, hipStream_t s);
+
+}  // namespace sga

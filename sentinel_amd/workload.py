@@ -1,0 +1,149 @@
+"""Synthetic workloads of SURVEY.md §8(d) (C1-C5), shared by tests and bench.py.
+
+Not part of the decision path.  Counter-based randomness so any slice of a
+trace can be generated independently (and identically by the GPU generator in
+csrc/workload.hip, up to libm last-ulp differences in the Zipf sampler):
+  u64(stream, i) = splitmix64(seed + stream * 0xD1B54A32D192ED03 + i * 0x9E3779B97F4A7C15)
+Zipf(s) uses Hormann-Derflinger rejection-inversion (as published; the same
+algorithm as Apache Commons RNG's RejectionInversionZipfSampler); rank -> id
+goes through a seeded permutation so hot ids spread across shards.
+"""
+import numpy as np
+
+MASTER_SEED = 0x53454E54494E454C
+T0 = 1_700_000_000_000
+
+S_ZIPF, S_PRIO, S_COUNT, S_PERM, S_ACQ, S_MIX, S_EXIT = range(1, 8)
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def splitmix64(z):
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def rng_u64(stream, idx, seed=MASTER_SEED):
+    idx = np.asarray(idx, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = np.uint64(seed) + np.uint64(stream) * np.uint64(0xD1B54A32D192ED03) + idx * np.uint64(0x9E3779B97F4A7C15)
+    return splitmix64(x)
+
+
+def rng_unit(stream, idx, seed=MASTER_SEED):
+    return (rng_u64(stream, idx, seed) >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+
+class Zipf:
+    def __init__(self, n, s=1.1):
+        self.n = int(n)
+        self.s = float(s)
+        self.hx1 = self.H(1.5) - 1.0
+        self.hn = self.H(self.n + 0.5)
+        self.sval = 2.0 - self.Hinv(self.H(2.5) - self.h(2.0))
+
+    def h(self, x):
+        return np.exp(-self.s * np.log(x))
+
+    @staticmethod
+    def _helper1(x):
+        x = np.asarray(x, dtype=np.float64)
+        small = np.abs(x) <= 1e-8
+        with np.errstate(divide="ignore", invalid="ignore"):
+            big = np.log1p(x) / x
+        return np.where(small, 1.0 - x * (0.5 - x * (1.0 / 3.0 - 0.25 * x)), big)
+
+    @staticmethod
+    def _helper2(x):
+        x = np.asarray(x, dtype=np.float64)
+        small = np.abs(x) <= 1e-8
+        with np.errstate(divide="ignore", invalid="ignore"):
+            big = np.expm1(x) / x
+        return np.where(small, 1.0 + x * 0.5 * (1.0 + x * (1.0 / 3.0) * (1.0 + 0.25 * x)), big)
+
+    def H(self, x):
+        lx = np.log(x)
+        return self._helper2((1.0 - self.s) * lx) * lx
+
+    def Hinv(self, x):
+        t = np.maximum(x * (1.0 - self.s), -1.0)
+        return np.exp(self._helper1(t) * x)
+
+    def sample(self, stream, idx, seed=MASTER_SEED):
+        """1-based ranks for event indices idx (vectorised, deterministic per index)."""
+        idx = np.asarray(idx, dtype=np.uint64)
+        out = np.zeros(idx.shape, dtype=np.int64)
+        pending = np.arange(idx.size)
+        for attempt in range(64):
+            if pending.size == 0:
+                break
+            with np.errstate(over="ignore"):
+                sub = idx[pending] * np.uint64(64) + np.uint64(attempt)
+            u01 = rng_unit(stream, sub, seed)
+            u = self.hn + u01 * (self.hx1 - self.hn)
+            x = self.Hinv(u)
+            k = np.floor(x + 0.5).astype(np.int64)
+            k = np.clip(k, 1, self.n)
+            ok = (k - x <= self.sval) | (u >= self.H(k + 0.5) - self.h(k.astype(np.float64)))
+            out[pending[ok]] = k[ok]
+            pending = pending[~ok]
+        if pending.size:
+            out[pending] = 1
+        return out
+
+
+def permutation(n, stream=S_PERM, seed=MASTER_SEED):
+    """Seeded permutation of 0..n-1 (sort of random keys)."""
+    keys = rng_u64(stream, np.arange(n, dtype=np.uint64), seed)
+    return np.argsort(keys, kind="stable").astype(np.int64)
+
+
+# ------------------------------------------------------------------ C3
+class ClusterTrace:
+    """C3: n_rules cluster FlowRules (flowId 1..n, GLOBAL, count U{10..10000},
+    sampleCount 10, 1000 ms); requestToken(flowId ~ Zipf(1.1), 1, prio 1 %)
+    at lambda events per virtual second starting at T0."""
+
+    def __init__(self, n_rules=1_000_000, lam=100_000_000, prio_pct=1, seed=MASTER_SEED, s=1.1,
+                 acquire_mix=False, count_lo=10, count_hi=10000):
+        self.n = n_rules
+        self.lam = lam
+        self.prio_pct = prio_pct
+        self.seed = seed
+        self.zipf = Zipf(n_rules, s)
+        self.perm = permutation(n_rules, seed=seed)
+        self.acquire_mix = acquire_mix
+        self.count_lo, self.count_hi = count_lo, count_hi
+
+    def rules(self):
+        fid = np.arange(1, self.n + 1, dtype=np.int64)
+        span = self.count_hi - self.count_lo + 1
+        count = (self.count_lo + (rng_u64(S_COUNT, fid.astype(np.uint64), self.seed) % np.uint64(span))).astype(
+            np.float64)
+        return fid, count
+
+    def events(self, start, m):
+        idx = np.arange(start, start + m, dtype=np.uint64)
+        rank = self.zipf.sample(S_ZIPF, idx, self.seed)
+        fid = self.perm[rank - 1] + 1
+        if self.prio_pct:
+            prio = ((rng_u64(S_PRIO, idx, self.seed) % np.uint64(100)) < np.uint64(self.prio_pct)).astype(np.uint8)
+        else:
+            prio = np.zeros(m, dtype=np.uint8)
+        if self.acquire_mix:  # 95 % acquire 1, 5 % U{2..5}
+            r = rng_u64(S_ACQ, idx, self.seed)
+            acq = np.where((r % np.uint64(100)) < np.uint64(95), 1, 2 + ((r >> np.uint64(8)) % np.uint64(4))).astype(
+                np.int32)
+        else:
+            acq = np.ones(m, dtype=np.int32)
+        ts = (T0 + (idx.astype(np.int64) * 1000) // self.lam).astype(np.int64)
+        return fid.astype(np.int64), acq, prio, ts
+
+
+def shard_of(flow_id, n_shards):
+    """Rules shard by flowId hash across GPUs: splitmix64(flowId) mod G."""
+    return (splitmix64(np.asarray(flow_id, dtype=np.int64).astype(np.uint64)) % np.uint64(n_shards)).astype(np.int64)

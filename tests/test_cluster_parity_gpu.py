@@ -1,0 +1,281 @@
+"""GPU parity: the HIP cluster token-server path (through the C-ABI) against the
+oracle's single-threaded replay of ClusterFlowChecker on the same ordered
+trace under a mocked clock.  Decisions (status, remaining, waitInMs) and every
+ClusterMetric counter must be bit-exact."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from tests import oracle_harness as H
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1_700_000_000_000
+
+
+def oracle_cluster(rules, namespace_conn=None, exceed=1.0, ratio=1.0):
+    L = H.lib()
+    h = L.orc_cluster_new(exceed, ratio)
+    if namespace_conn:
+        for ns, c in namespace_conn.items():
+            L.orc_cluster_set_connected_count(h, ns.encode(), c)
+    for ns, rs in rules.items():
+        arr = H.cluster_rules_array(rs)
+        L.orc_cluster_load_rules(h, ns.encode(), arr, len(rs))
+    return h
+
+
+def oracle_replay(h, fid, acq, prio, ts):
+    L = H.lib()
+    n = len(fid)
+    out = (H.OrcTokenResult * n)()
+    fid = np.ascontiguousarray(fid, np.int64)
+    acq = np.ascontiguousarray(acq, np.int32)
+    prio = np.ascontiguousarray(prio, np.uint8)
+    ts = np.ascontiguousarray(ts, np.int64)
+    L.orc_cluster_replay(h, n, fid.ctypes.data, acq.ctypes.data, prio.ctypes.data, ts.ctypes.data, out)
+    a = np.frombuffer(out, dtype=np.int32).reshape(n, 3)
+    return a[:, 0].copy(), a[:, 1].copy(), a[:, 2].copy()
+
+
+@pytest.fixture(scope="module")
+def eng_mod():
+    from sentinel_amd import cluster
+    return cluster
+
+
+def make_engine(cluster, **kw):
+    kw.setdefault("max_batch", 1 << 20)
+    return cluster.Engine(**kw)
+
+
+def engine_rules(cluster, eng, rules, namespace_conn=None):
+    mgr = cluster.ClusterFlowRuleManager(eng)
+    if namespace_conn:
+        for ns, c in namespace_conn.items():
+            mgr.set_connected_count(ns, c)
+    for ns, rs in rules.items():
+        fr = [cluster.FlowRule(resource=f"r{r['flow_id']}", count=r["count"], cluster_mode=True,
+                               cluster_config=cluster.ClusterFlowConfig(
+                                   flow_id=r["flow_id"], threshold_type=r.get("threshold_type", 0),
+                                   sample_count=r.get("sample_count", 10),
+                                   window_interval_ms=r.get("window_interval_ms", 1000))) for r in rs]
+        mgr.load_rules(ns, fr)
+    return mgr
+
+
+def assert_same(gpu, orc, fid, ts, ctx=""):
+    st, rem, wait = orc
+    bad = np.nonzero((gpu["status"] != st) | (gpu["remaining"] != rem) | (gpu["wait_in_ms"] != wait))[0]
+    if bad.size:
+        i = bad[0]
+        raise AssertionError(f"{ctx}: {bad.size} mismatches; first at {i}: flow={fid[i]} ts={ts[i]} "
+                             f"gpu=({gpu['status'][i]},{gpu['remaining'][i]},{gpu['wait_in_ms'][i]}) "
+                             f"oracle=({st[i]},{rem[i]},{wait[i]})")
+
+
+def assert_metrics(cluster, eng, oh, flow_ids, now):
+    svc = cluster.DefaultTokenService(eng)
+    L = H.lib()
+    for f in flow_ids:
+        g = svc.metric_sums(int(f), now)
+        o = [L.orc_cluster_metric_sum(oh, int(f), ev, now) for ev in range(7)]
+        assert g == o, (f, g, o)
+
+
+def random_rules(rng, n, ids=None, mixed_geometry=False):
+    rs = []
+    ids = ids if ids is not None else range(1, n + 1)
+    for fid in ids:
+        r = {"flow_id": int(fid), "count": float(rng.integers(1, 60)), "threshold_type": 1}
+        if mixed_geometry:
+            sc = int(rng.choice([1, 2, 5, 10, 20]))
+            r["sample_count"] = sc
+            r["window_interval_ms"] = int(sc * rng.choice([10, 50, 100, 200]))
+            if rng.random() < 0.2:
+                r["count"] = float(rng.integers(1, 60)) + 0.5
+        rs.append(r)
+    return rs
+
+
+def test_cluster_flow_checker_kat_sequence(eng_mod):
+    """CST/flow/ClusterFlowCheckerTest.java:37-75 sequence (disabled upstream) on the GPU."""
+    c = eng_mod
+    rule = [{"flow_id": 98765, "count": 5, "threshold_type": 1, "sample_count": 5, "window_interval_ms": 1000}]
+    seq = [(0, 0, "OK"), (0, 0, "OK"), (200, 0, "OK"), (400, 1, "OK"), (400, 0, "OK"), (400, 1, "BLOCKED"),
+           (600, 0, "BLOCKED"), (600, 0, "BLOCKED"), (800, 0, "BLOCKED"), (800, 1, "SHOULD_WAIT"),
+           (800, 0, "BLOCKED"), (1000, 0, "OK")]
+    for base in (T0, T0 + 123, T0 + 199):
+        for one_by_one in (True, False):
+            eng = make_engine(c)
+            engine_rules(c, eng, {"default": rule})
+            svc = c.DefaultTokenService(eng)
+            ts = [base + d for d, _, _ in seq]
+            pr = [p for _, p, _ in seq]
+            if one_by_one:
+                got = [svc.request_token(98765, 1, bool(p), t).status for t, p in zip(ts, pr)]
+            else:
+                got = list(svc.request_tokens([98765] * len(seq), [1] * len(seq), pr, ts)["status"])
+            want = [H.TOKEN_STATUS[s] for _, _, s in seq]
+            assert got == want, (base, one_by_one, got)
+            eng.close()
+
+
+def test_request_validation(eng_mod):
+    c = eng_mod
+    eng = make_engine(c)
+    engine_rules(c, eng, {"default": [{"flow_id": 7, "count": 3, "threshold_type": 1}]})
+    svc = c.DefaultTokenService(eng)
+    r = svc.request_tokens([0, -5, 7, 7, 99, 7], [1, 1, 0, -3, 1, 1], [0] * 6, [T0] * 6)
+    assert list(r["status"]) == [-4, -4, -4, -4, 3, 0]
+    assert r["remaining"][5] == 2
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("mixed", [False, True])
+def test_random_traces_bit_exact(eng_mod, seed, mixed):
+    """Random rules (mixed window geometries, fractional counts), acquire mix,
+    10 % prioritized, bursts: every decision and counter equals the oracle."""
+    c = eng_mod
+    rng = np.random.default_rng(seed)
+    nr = 300
+    rules = random_rules(rng, nr, mixed_geometry=mixed)
+    n = 60_000
+    fid = rng.integers(1, nr + 40, size=n)          # some ids without rules
+    fid[rng.random(n) < 0.002] = 0                  # BAD_REQUEST
+    hot = rng.random(n) < 0.5
+    fid[hot] = rng.integers(1, 6, size=hot.sum())   # hot rules -> long runs
+    acq = np.where(rng.random(n) < 0.9, 1, rng.integers(1, 6, size=n)) if mixed else np.ones(n, np.int64)
+    acq[rng.random(n) < 0.001] = 0                  # BAD_REQUEST
+    prio = (rng.random(n) < 0.1).astype(np.uint8)
+    ts = T0 + np.cumsum(rng.integers(0, 3, size=n))
+    oh = oracle_cluster({"default": rules})
+    eng = make_engine(c, max_batch=1 << 16)
+    engine_rules(c, eng, {"default": rules})
+    svc = c.DefaultTokenService(eng)
+    for lo in range(0, n, 20_000):  # several batches continue the same state
+        sl = slice(lo, lo + 20_000)
+        g = svc.request_tokens(fid[sl], acq[sl], prio[sl], ts[sl])
+        o = oracle_replay(oh, fid[sl], acq[sl], prio[sl], ts[sl])
+        assert_same(g, o, fid[sl], ts[sl], f"seed={seed} batch@{lo}")
+    assert_metrics(c, eng, oh, range(1, nr + 1), int(ts[-1]))
+    H.lib().orc_cluster_free(oh)
+    eng.close()
+
+
+def test_avg_local_threshold_and_reload(eng_mod):
+    """AVG_LOCAL (count * connectedCount) and ClusterFlowRuleManager reload
+    semantics: kept flowIds keep their metric, dropped ones lose it."""
+    c = eng_mod
+    rng = np.random.default_rng(7)
+    rules = [{"flow_id": i, "count": float(rng.integers(1, 20)), "threshold_type": int(i % 2)} for i in range(1, 41)]
+    conn = {"default": 3}
+    oh = oracle_cluster({"default": rules}, namespace_conn=conn)
+    eng = make_engine(c, max_batch=1 << 15)
+    mgr = engine_rules(c, eng, {"default": rules}, namespace_conn=conn)
+    svc = c.DefaultTokenService(eng)
+
+    def batch(t0, n):
+        fid = rng.integers(1, 45, size=n)
+        acq = np.ones(n, np.int64)
+        prio = (rng.random(n) < 0.2).astype(np.uint8)
+        ts = t0 + np.sort(rng.integers(0, 1500, size=n))
+        g = svc.request_tokens(fid, acq, prio, ts)
+        o = oracle_replay(oh, fid, acq, prio, ts)
+        assert_same(g, o, fid, ts)
+        return int(ts[-1])
+
+    t = batch(T0, 5000)
+    # reload: drop 1..10, keep 11..40 (new counts), add 41..50
+    rules2 = [{"flow_id": i, "count": float(rng.integers(1, 20)), "threshold_type": 1} for i in range(11, 51)]
+    arr = H.cluster_rules_array(rules2)
+    H.lib().orc_cluster_load_rules(oh, b"default", arr, len(rules2))
+    mgr.load_rules("default", [c.FlowRule(count=r["count"], cluster_mode=True, cluster_config=c.ClusterFlowConfig(
+        flow_id=r["flow_id"], threshold_type=1)) for r in rules2])
+    t = batch(t + 1, 5000)
+    assert_metrics(c, eng, oh, range(11, 51), t)
+    H.lib().orc_cluster_free(oh)
+    eng.close()
+
+
+def test_time_regression_and_gaps(eng_mod):
+    """Clock going backwards (detached windows) and long idle gaps."""
+    c = eng_mod
+    rules = [{"flow_id": 1, "count": 4, "threshold_type": 1, "sample_count": 5, "window_interval_ms": 500},
+             {"flow_id": 2, "count": 2, "threshold_type": 1}]
+    oh = oracle_cluster({"default": rules})
+    eng = make_engine(c, max_batch=1 << 12)
+    engine_rules(c, eng, {"default": rules})
+    svc = c.DefaultTokenService(eng)
+    ts = np.array([T0, T0 + 10, T0 + 250, T0 + 120, T0 + 130, T0 + 5000, T0 + 4000, T0 + 5001, T0 + 90000,
+                   T0 + 90000, T0 + 90100] * 3, dtype=np.int64)
+    fid = np.where(np.arange(len(ts)) % 3 == 2, 2, 1).astype(np.int64)
+    prio = np.array([0, 1] * (len(ts) // 2) + [1] * (len(ts) % 2), dtype=np.uint8)
+    acq = np.ones(len(ts), np.int64)
+    g = svc.request_tokens(fid, acq, prio, ts)
+    o = oracle_replay(oh, fid, acq, prio, ts)
+    assert_same(g, o, fid, ts)
+    H.lib().orc_cluster_free(oh)
+    eng.close()
+
+
+def test_zipf_c3_slice_bit_exact(eng_mod):
+    """C3 trace slice (100k rules, 2^21 requests, Zipf(1.1), 1 % prioritized)."""
+    from sentinel_amd.workload import ClusterTrace
+    c = eng_mod
+    tr = ClusterTrace(n_rules=100_000, lam=10_000_000)
+    fid_r, cnt = tr.rules()
+    rules = [{"flow_id": int(f), "count": float(x), "threshold_type": 1} for f, x in zip(fid_r, cnt)]
+    oh = oracle_cluster({"default": rules})
+    eng = make_engine(c, max_batch=1 << 20, max_rules=1 << 17)
+    c.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_r, cnt)
+    svc = c.DefaultTokenService(eng)
+    for b in range(2):
+        fid, acq, prio, ts = tr.events(b << 20, 1 << 20)
+        g = svc.request_tokens(fid, acq, prio, ts)
+        o = oracle_replay(oh, fid, acq, prio, ts)
+        assert_same(g, o, fid, ts, f"batch {b}")
+    hot = np.unique(fid)[:200]
+    assert_metrics(c, eng, oh, hot, int(ts[-1]))
+    H.lib().orc_cluster_free(oh)
+    eng.close()
+
+
+def test_rls_descriptors(eng_mod):
+    """Envoy RLS: SimpleClusterFlowChecker per descriptor, NO_RULE -> OK, no short-circuit."""
+    from sentinel_amd.javautil import rls_key
+    c = eng_mod
+    rls = c.EnvoyRlsService
+    keys = [rls_key("d", [("k", f"v{i}")]) for i in range(8)]
+    fids = [rls.generate_flow_id(k) for k in keys]
+    rules = [{"flow_id": f, "count": 3.0, "threshold_type": 1, "sample_count": 1, "window_interval_ms": 1000}
+             for f in fids[:6]]
+    eng = make_engine(c, max_batch=1 << 12)
+    engine_rules(c, eng, {"default": rules})
+    oh = oracle_cluster({"default": rules})
+    svc = rls(eng)
+    rng = np.random.default_rng(3)
+    nreq = 400
+    ndesc = rng.integers(1, 5, size=nreq)
+    off = np.concatenate([[0], np.cumsum(ndesc)]).astype(np.uint32)
+    dfid = np.array([fids[i] for i in rng.integers(0, 8, size=off[-1])], dtype=np.int64)
+    hits = rng.integers(0, 3, size=nreq).astype(np.int32)
+    hits[5] = -1
+    ts = T0 + np.arange(nreq) * 7
+    code, st = svc.should_rate_limit(off, dfid, hits, ts)
+    L = H.lib()
+    for r in range(nreq):
+        if hits[r] < 0:
+            assert code[r] == -1
+            continue
+        a = 1 if hits[r] == 0 else int(hits[r])
+        blocked = False
+        for d in range(off[r], off[r + 1]):
+            res = L.orc_cluster_request_token_simple(oh, int(dfid[d]), a, int(ts[r]))
+            s = 0 if res.status == 3 else res.status
+            assert st[d] == s, (r, d, st[d], s)
+            blocked |= s != 0
+        assert code[r] == (2 if blocked else 1)
+    L.orc_cluster_free(oh)
+    eng.close()
