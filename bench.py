@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""Headline benchmark: admission decisions/s of the cluster token server at 1M
+rules, Zipf(1.1) (BASELINE.json metric).
+
+One process per GPU (torch.distributed.run for N > 1).  Rules shard by
+splitmix64(flowId) mod N; every rank owns its shard's rules and decides the
+requests routed to it (no data-path collective; "weak" scaling: each rank sees
+a global batch of N * 2^24 requests at lambda = N * 1e8 requests per virtual
+second, of which ~2^24 are its own).  A step = one DefaultTokenService batch
+(sga_request_tokens_device) over one pre-generated, HBM-resident batch.
+
+Prints ONE JSON line on rank 0 (the driver's contract) with `roofline` and
+`cpu_baseline` objects.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PER_RANK_BATCH = 1 << 24
+N_RULES = 1_000_000
+LAMBDA_PER_GPU = 100_000_000
+E_IN, E_OUT, S_FLOW = 12, 8, 704  # token request 12 B, token result 8 B, cluster flow 704 B
+HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+class SgawParams(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("t0", C.c_int64), ("lambda_", C.c_int64), ("n_rules", C.c_int64),
+                ("zipf_s", C.c_double), ("prio_pct", C.c_int32), ("n_shards", C.c_int32), ("shard", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=PER_RANK_BATCH, help="requests per rank per step (avg)")
+    ap.add_argument("--rules", type=int, default=N_RULES)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 25, help="oracle replay sample (requests)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    n_gpus = world
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+
+    from sentinel_amd import _lib, cluster
+    from sentinel_amd.workload import MASTER_SEED, T0, ClusterTrace, permutation, shard_of
+
+    wl = C.CDLL(os.path.join(ROOT, "sentinel_amd", "libsga_workload.so"))
+    wl.sgaw_gen_cluster.restype = C.c_int
+    wl.sgaw_gen_cluster.argtypes = [C.POINTER(SgawParams), C.c_uint64, C.c_uint32, C.c_void_p, C.c_int64,
+                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_void_p]
+    wl.sgaw_flow_histogram.restype = C.c_int
+    wl.sgaw_flow_histogram.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64, C.c_void_p]
+
+    lam = LAMBDA_PER_GPU * n_gpus
+    glob_batch = args.batch * n_gpus
+    dev = torch.device("cuda", local)
+
+    # ---- rules of this shard (C3: flowId 1..1M, GLOBAL, count U{10..10000}, 10 x 100 ms)
+    tr = ClusterTrace(n_rules=args.rules, lam=lam)
+    fid_all, cnt_all = tr.rules()
+    mine = shard_of(fid_all, n_gpus) == rank
+    perm = torch.from_numpy(permutation(args.rules)).to(dev)
+
+    # ---- pre-generate warmup+steps batches in HBM (untimed)
+    nb = args.warmup + args.steps
+    params = SgawParams(MASTER_SEED, T0, lam, args.rules, 1.1, 1, n_gpus, rank, 0)
+    tmp = torch.empty(4 * glob_batch + 4096, dtype=torch.int32, device=dev)
+    cnt_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+    hist = torch.zeros(args.rules + 1, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    batches = []
+    touched = []
+    max_n = 0
+    for b in range(nb):
+        start = b * glob_batch
+        ts_base = T0 + (start * 1000) // lam
+        cap = glob_batch  # worst case: every request of the global batch is ours
+        f = torch.empty(cap, dtype=torch.int64, device=dev)
+        a = torch.empty(cap, dtype=torch.int32, device=dev)
+        p = torch.empty(cap, dtype=torch.uint8, device=dev)
+        t = torch.empty(cap, dtype=torch.int32, device=dev)
+        rc = wl.sgaw_gen_cluster(C.byref(params), start, glob_batch, perm.data_ptr(), ts_base, f.data_ptr(),
+                                 a.data_ptr(), p.data_ptr(), t.data_ptr(), cnt_dev.data_ptr(), tmp.data_ptr(),
+                                 C.c_void_p(stream.cuda_stream))
+        assert rc == 0, rc
+        torch.cuda.synchronize(dev)
+        n = int(cnt_dev.item())
+        wl.sgaw_flow_histogram(f.data_ptr(), n, hist.data_ptr(), args.rules, C.c_void_p(stream.cuda_stream))
+        torch.cuda.synchronize(dev)
+        touched.append(int((hist > 0).sum().item()))
+        # shrink to the kept events
+        batches.append((f[:n].clone(), a[:n].clone(), p[:n].clone(), t[:n].clone(), ts_base, n))
+        del f, a, p, t
+        max_n = max(max_n, n)
+    del tmp
+
+    eng = cluster.Engine(device=local, max_batch=max_n + 1024, max_rules=max(1 << 16, int(mine.sum()) + 1))
+    cluster.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_all[mine], cnt_all[mine])
+    out = torch.empty(max_n + 1024, dtype=torch.int64, device=dev)
+    L = _lib.load()
+    estream = L.sga_engine_stream(eng.handle)
+
+    def step(b):
+        f, a, p, t, ts_base, n = batches[b]
+        rc = L.sga_request_tokens_device(eng.handle, f.data_ptr(), a.data_ptr(), p.data_ptr(), ts_base, t.data_ptr(),
+                                         n, out.data_ptr(), None)
+        if rc != 0:
+            raise RuntimeError(f"sga_request_tokens_device rc={rc}: {L.sga_last_error(eng.handle)}")
+
+    for b in range(args.warmup):
+        step(b)
+    torch.cuda.synchronize(dev)
+
+    # HIP events on the engine's stream bracket the timed steps (kernel-side duration)
+    hip = C.CDLL("libamdhip64.so.7")
+    hip.hipEventCreate.argtypes = [C.POINTER(C.c_void_p)]
+    hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
+    hip.hipEventSynchronize.argtypes = [C.c_void_p]
+    hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
+    ev0, ev1 = C.c_void_p(), C.c_void_p()
+    hip.hipEventCreate(C.byref(ev0))
+    hip.hipEventCreate(C.byref(ev1))
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    hip.hipEventRecord(ev0, estream)
+    for b in range(args.warmup, nb):
+        step(b)
+    hip.hipEventRecord(ev1, estream)
+    torch.cuda.synchronize(dev)
+    t_end = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    hip.hipEventSynchronize(ev1)
+    ms_ev = C.c_float()
+    hip.hipEventElapsedTime(C.byref(ms_ev), ev0, ev1)
+
+    wall = t_end - t_start
+    my_events = sum(batches[b][5] for b in range(args.warmup, nb))
+    my_touched = sum(touched[b] for b in range(args.warmup, nb))
+    stats = torch.tensor([wall, ms_ev.value / 1e3, float(my_events), float(my_touched)], dtype=torch.float64)
+    if world > 1:
+        tmax = stats[:2].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = stats[2:].clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        stats = torch.cat([tmax, tsum])
+    wall_max, gpu_max, total_events, total_touched = [float(x) for x in stats]
+
+    # correctness spot-check of the last batch's statuses (cheap invariants)
+    res = out[: batches[-1][5]].cpu().numpy().view(np.uint64)
+    status = ((res >> np.uint64(48)) & np.uint64(0xFF)).astype(np.int8)
+    frac_ok = float((status == 0).mean())
+
+    cpu_baseline = None
+    if rank == 0 and not args.no_cpu:
+        cpu_baseline = run_cpu_baseline(args, n_gpus)
+
+    if rank == 0:
+        value = total_events / wall_max
+        per_gpu_events = total_events / n_gpus
+        per_gpu_touched = total_touched / n_gpus
+        bytes_alg = per_gpu_events * (E_IN + E_OUT) + per_gpu_touched * 2 * S_FLOW  # per GPU, all timed steps
+        achieved = bytes_alg / gpu_max / 1e9
+        line = {
+            "metric": "admission decisions/sec at 1M rules Zipf(1.1), 1/2/4/8 GPU; % HBM peak",
+            "value": value,
+            "unit": "decisions/s",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic C3 trace (Zipf(1.1) flowIds, 1% prioritized, acquire 1), generated on GPU",
+            "config": {"workload": "C3 cluster token server: DefaultTokenService.requestToken batches, "
+                                   "1M cluster FlowRules (GLOBAL, count U{10..10000}, 10x100ms), sharded by flowId",
+                       "rules": args.rules, "requests_per_step_per_gpu": args.batch,
+                       "global_requests_per_step": args.batch * n_gpus, "lambda_per_virtual_s": lam,
+                       "parallelism": f"shard{n_gpus}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "sga_request_tokens_device pipeline (classify+sort+runs+flows+results), "
+                                   "HIP events on the engine stream",
+                         "bytes_alg_per_step_per_gpu": bytes_alg / args.steps,
+                         "touched_rules_per_step_per_gpu": per_gpu_touched / args.steps,
+                         "gpu_ms_per_step": gpu_max / args.steps * 1e3},
+            "cpu_baseline": cpu_baseline,
+            "ok_fraction_last_batch": frac_ok,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_cpu_baseline(args, n_gpus):
+    """Oracle (single-threaded C restatement of ClusterFlowChecker) on a bounded
+    sample of the same workload: the first `cpu_sample` requests of rank 0's
+    shard stream at 1M rules."""
+    try:
+        from tests import oracle_harness as H
+        from sentinel_amd.workload import ClusterTrace, shard_of
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "error": str(e)}
+    L = H.lib()
+    tr = ClusterTrace(n_rules=args.rules, lam=LAMBDA_PER_GPU * n_gpus)
+    fid_all, cnt_all = tr.rules()
+    mine = shard_of(fid_all, n_gpus) == 0
+    rules = np.zeros(int(mine.sum()), dtype=[("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"),
+                                           ("sample_count", "<i4"), ("window_interval_ms", "<i4"), ("grade", "<i4"),
+                                           ("strategy", "<i4")])
+    rules["flow_id"] = fid_all[mine]
+    rules["count"] = cnt_all[mine]
+    rules["threshold_type"] = 1
+    rules["sample_count"] = 10
+    rules["window_interval_ms"] = 1000
+    rules["grade"] = 1
+    oh = L.orc_cluster_new(1.0, 1.0)
+    L.orc_cluster_load_rules(oh, b"default", rules.ctypes.data_as(C.POINTER(H.OrcClusterRule)), len(rules))
+    total, dt = 0, 0.0
+    chunk = 1 << 22
+    g = 0
+    while total < args.cpu_sample:
+        f, a, p, ts = tr.events(g, chunk)
+        g += chunk
+        sel = shard_of(f, n_gpus) == 0
+        f, a, p, ts = [np.ascontiguousarray(x[sel]) for x in (f, a, p, ts)]
+        out = (H.OrcTokenResult * len(f))()
+        t0 = time.perf_counter()
+        L.orc_cluster_replay(oh, len(f), f.ctypes.data, a.ctypes.data, p.ctypes.data, ts.ctypes.data, out)
+        dt += time.perf_counter() - t0
+        total += len(f)
+    L.orc_cluster_free(oh)
+    return {"value": total / dt, "unit": "decisions/s", "cores": 1, "kind": "port",
+            "sample": f"{total} requests of the rank-0 shard stream of the same C3 trace, replayed by the "
+                      f"single-threaded C oracle (oracle/sentinel_oracle.c ClusterFlowChecker restatement); "
+                      f"JMH reference unavailable (no JDK on host)",
+            "seconds": dt}
+
+
+if __name__ == "__main__":
+    main()

@@ -36,14 +36,15 @@ def test_headers_declare_api():
 
 
 def test_library_exports_every_declared_symbol(lib):
-    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    wl = ctypes.CDLL(os.path.join(ROOT, "sentinel_amd", "libsga_workload.so"))
+    missing = [s for s in declared_symbols() if not hasattr(wl if s.startswith("sgaw_") else lib, s)]
     assert not missing, missing
 
 
 def test_python_mirror_binds_every_symbol():
     from sentinel_amd import _lib
     L = _lib.load()
-    decl = set(declared_symbols())
+    decl = {s for s in declared_symbols() if not s.startswith("sgaw_")}
     assert decl <= set(_lib.SIGNATURES), decl - set(_lib.SIGNATURES)
     assert L.sga_abi_version() == 1
 
