@@ -41,23 +41,22 @@ __device__ __forceinline__ uint64_t pack_result(int8_t status, int32_t remaining
            ((uint64_t)(uint8_t)status << 48);
 }
 
-__device__ __forceinline__ int64_t slot_lookup(const ClusterState &st, int64_t fid) {
+__device__ __forceinline__ HashEntry slot_lookup(const ClusterState &st, int64_t fid) {
     uint32_t h = (uint32_t)hash_flow_id(fid) & st.hmask;
     for (uint32_t probe = 0; probe <= st.hmask; ++probe) {
-        const int64_t k = st.hkeys[h];
-        if (k == fid) return st.hvals[h];
-        if (k == 0) return -1;
+        const HashEntry e = st.htab[h];
+        if (e.key == fid || e.key == 0) return e;
         h = (h + 1) & st.hmask;
     }
-    return -1;
+    return HashEntry{0, 0, 0};
 }
 
 // ---------------------------------------------------------------- classify
 __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const int64_t *__restrict__ flow_id,
                                                        const int32_t *__restrict__ acquire,
                                                        const uint8_t *__restrict__ prio,
-                                                       const uint32_t *__restrict__ ts_off, uint32_t n, int simple,
-                                                       uint32_t invalid_key, uint32_t *__restrict__ keys,
+                                                       const uint32_t *__restrict__ ts_off, int64_t ts_base,
+                                                       uint32_t n, int simple, uint32_t invalid_key, uint32_t *__restrict__ keys,
                                                        Payload *__restrict__ pay, uint64_t *__restrict__ out,
                                                        uint32_t *__restrict__ counters) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
@@ -66,30 +65,35 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
         const int64_t fid = flow_id[i];
         const int32_t a = acquire[i];
         int8_t status = TRS_OK;
-        int64_t slot = -1;
+        HashEntry he{0, 0, 0};
         if (!simple && (fid <= 0 || a <= 0)) {
             status = TRS_BAD_REQUEST;  // DefaultTokenService.notValidRequest, :87-89
         } else {
             // ClusterFlowRuleManager.getFlowRuleById: validId(id > 0) && FLOW_RULES.get(id)
-            slot = fid > 0 ? slot_lookup(st, fid) : -1;
-            if (slot < 0 || !st.param[slot].active) status = TRS_NO_RULE_EXISTS;
+            if (fid > 0) he = slot_lookup(st, fid);
+            if (he.key != fid || fid <= 0) status = TRS_NO_RULE_EXISTS;
         }
         if (status != TRS_OK) {
             out[i] = pack_result(status, 0, 0);
             keys[i] = invalid_key;
-            pay[i] = Payload{i, 0u, 0u};
+            pay[i] = Payload{i, 0u, 0u, 0u};
         } else {
             valid = true;
-            keys[i] = (uint32_t)slot;
+            keys[i] = he.slot;
             const uint32_t p = (!simple && prio && prio[i]) ? 0x80000000u : 0u;
-            pay[i] = Payload{i, ts_off[i], (uint32_t)a | p};
+            const uint32_t off = ts_off[i];
+            const int64_t t = ts_base + (int64_t)off;
+            pay[i] = Payload{i, off, (uint32_t)a | p, (uint32_t)(t / (int64_t)he.W)};
         }
     }
-    const uint64_t m = __ballot(valid);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&counters[0], (uint32_t)__popcll(m));
+    (void)valid;
+    (void)counters;  // the valid count is derived after the sort (invalid keys sort last)
 }
 
 // ---------------------------------------------------------------- runs (segmented scan)
+// A run = maximal group of sorted requests with the same (rule, window bucket).
+// Segmented scan value: run/flow head counts (plain sums) and, since the last
+// run head, the number of prioritized requests and the min/max acquire count.
 struct Agg {
     uint32_t nh, nf;  // run heads, flow heads
     uint32_t flag;    // segment (run) head seen
@@ -103,235 +107,324 @@ __device__ __forceinline__ Agg agg_combine(const Agg &a, const Agg &b) {
     Agg r;
     r.nh = a.nh + b.nh;
     r.nf = a.nf + b.nf;
-    if (b.flag) {
-        r.flag = 1;
-        r.cnt = b.cnt;
-        r.mn = b.mn;
-        r.mx = b.mx;
-    } else {
-        r.flag = a.flag;
-        r.cnt = a.cnt + b.cnt;
-        r.mn = min(a.mn, b.mn);
-        r.mx = max(a.mx, b.mx);
-    }
+    r.flag = a.flag | b.flag;
+    r.cnt = b.flag ? b.cnt : a.cnt + b.cnt;
+    r.mn = b.flag ? b.mn : min(a.mn, b.mn);
+    r.mx = b.flag ? b.mx : max(a.mx, b.mx);
     return r;
 }
 
 __device__ __forceinline__ Agg agg_shfl_up(const Agg &v, int o) {
-    Agg r;
-    r.nh = __shfl_up(v.nh, o, 64);
-    r.nf = __shfl_up(v.nf, o, 64);
-    r.flag = __shfl_up(v.flag, o, 64);
-    r.cnt = __shfl_up(v.cnt, o, 64);
-    r.mn = __shfl_up(v.mn, o, 64);
-    r.mx = __shfl_up(v.mx, o, 64);
-    return r;
+    return Agg{(uint32_t)__shfl_up((int)v.nh, o, 64), (uint32_t)__shfl_up((int)v.nf, o, 64),
+               (uint32_t)__shfl_up((int)v.flag, o, 64), (uint32_t)__shfl_up((int)v.cnt, o, 64),
+               __shfl_up(v.mn, o, 64), __shfl_up(v.mx, o, 64)};
 }
 
-// exclusive scan of one Agg per thread over the workgroup (NT threads)
-template <int NT>
-__device__ Agg block_excl_scan(const Agg &v, Agg *total) {
-    constexpr int NW = NT / 64;
-    __shared__ Agg wtot[NW];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    Agg x = v;
+__device__ __forceinline__ Agg agg_shfl(const Agg &v, int src) {
+    return Agg{(uint32_t)__shfl((int)v.nh, src, 64), (uint32_t)__shfl((int)v.nf, src, 64),
+               (uint32_t)__shfl((int)v.flag, src, 64), (uint32_t)__shfl((int)v.cnt, src, 64),
+               __shfl(v.mn, src, 64), __shfl(v.mx, src, 64)};
+}
+
+// inclusive scan over the 64 lanes of a wave (lane order = element order)
+__device__ __forceinline__ Agg wave_incl_scan(Agg x, int lane) {
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        Agg y = agg_shfl_up(x, o);
+        const Agg y = agg_shfl_up(x, o);
         if (lane >= o) x = agg_combine(y, x);
     }
+    return x;
+}
+
+constexpr int kRunThreads = 512;
+constexpr int kRunRounds = 8;                       // rounds of 64 per wave
+constexpr int kRunWaves = kRunThreads / 64;         // 8
+constexpr int kWaveElems = kRunRounds * 64;         // 512
+static_assert(kWaveElems * kRunWaves == kTileElems, "tile geometry");
+
+struct RunIn {
+    uint32_t key;
+    Payload q;
+};
+
+__device__ __forceinline__ RunIn run_load(const uint32_t *keys, const Payload *pay, uint32_t e, uint32_t nlim,
+                                          uint32_t invalid_key) {
+    RunIn x;
+    if (e < nlim) {
+        x.key = keys[e];
+        x.q = pay[e];
+    } else {
+        x.key = invalid_key;
+        x.q = Payload{0, 0, 0, 0};
+    }
+    return x;
+}
+
+__device__ __forceinline__ RunIn run_shfl_up1(const RunIn &x) {
+    RunIn y;
+    y.key = (uint32_t)__shfl_up((int)x.key, 1, 64);
+    y.q.idx = (uint32_t)__shfl_up((int)x.q.idx, 1, 64);
+    y.q.ts_off = (uint32_t)__shfl_up((int)x.q.ts_off, 1, 64);
+    y.q.acq_prio = (uint32_t)__shfl_up((int)x.q.acq_prio, 1, 64);
+    y.q.bucket = (uint32_t)__shfl_up((int)x.q.bucket, 1, 64);
+    return y;
+}
+
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
+
+// Agg contribution of element x with predecessor px (has_prev = x is not element 0)
+__device__ __forceinline__ Agg run_value(const RunIn &x, const RunIn &px, bool has_prev, bool valid) {
+    if (!valid) return agg_identity();
+    const bool fh = !has_prev || x.key != px.key;
+    const bool h = fh || x.q.bucket != px.q.bucket;
+    const int32_t a = (int32_t)(x.q.acq_prio & 0x7FFFFFFFu);
+    return Agg{h ? 1u : 0u, fh ? 1u : 0u, h ? 1u : 0u, x.q.acq_prio >> 31, a, a};
+}
+
+// Per tile: aggregate over its valid elements + count of valid elements.
+__global__ __launch_bounds__(kRunThreads) void k_runs_up(const uint32_t *__restrict__ keys,
+                                                      const Payload *__restrict__ pay, uint32_t n,
+                                                      uint32_t invalid_key, Agg *__restrict__ tile_agg,
+                                                      uint32_t *__restrict__ tile_valid) {
+    __shared__ Agg wagg[kRunWaves];
+    __shared__ uint32_t wval[kRunWaves];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t wb = blockIdx.x * kTileElems + wave * kWaveElems;
+    RunIn last = run_load(keys, pay, wb - 1, wb > 0 ? min(wb, n) : 0, invalid_key);  // element wb-1 (if any)
+    Agg acc = agg_identity();
+    uint32_t nval = 0;
+    for (int r = 0; r < kRunRounds; ++r) {
+        const uint32_t e = wb + r * 64 + lane;
+        const RunIn x = run_load(keys, pay, e, n, invalid_key);
+        const bool valid = x.key != invalid_key;
+        RunIn px = run_shfl_up1(x);
+        if (lane == 0) px = last;
+        Agg v = run_value(x, px, e > 0, valid);
+        // ordered tree reduction: lane 0 ends with lanes 0..63 combined in order
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const Agg y = agg_shfl(v, (lane + o) & 63);
+            if (lane + o < 64 && (lane & (2 * o - 1)) == 0) v = agg_combine(v, y);
+        }
+        acc = agg_combine(acc, agg_shfl(v, 0));
+        nval += (uint32_t)__popcll(__ballot(valid));
+        last.key = shfl_u32(x.key, 63);
+        last.q.bucket = shfl_u32(x.q.bucket, 63);
+    }
+    if (lane == 0) {
+        wagg[wave] = acc;
+        wval[wave] = nval;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Agg t = agg_identity();
+        uint32_t c = 0;
+        for (int w = 0; w < kRunWaves; ++w) {
+            t = agg_combine(t, wagg[w]);
+            c += wval[w];
+        }
+        tile_agg[blockIdx.x] = t;
+        tile_valid[blockIdx.x] = c;
+    }
+}
+
+constexpr int kTileScanThreads = 1024;
+
+// exclusive scan of one Agg per thread over a 1024-thread workgroup
+__device__ Agg block_excl_scan_1024(const Agg &v, Agg *total) {
+    constexpr int NW = kTileScanThreads / 64;
+    __shared__ Agg wtot[NW];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const Agg x = wave_incl_scan(v, lane);
     if (lane == 63) wtot[wave] = x;
     __syncthreads();
     Agg wpre = agg_identity();
     for (int w = 0; w < wave; ++w) wpre = agg_combine(wpre, wtot[w]);
     Agg lane_excl = agg_shfl_up(x, 1);
     if (lane == 0) lane_excl = agg_identity();
-    if (total) {
-        Agg t = agg_identity();
-        for (int w = 0; w < NW; ++w) t = agg_combine(t, wtot[w]);
-        *total = t;
-    }
+    Agg t = agg_identity();
+    for (int w = 0; w < NW; ++w) t = agg_combine(t, wtot[w]);
+    *total = t;
     __syncthreads();
     return agg_combine(wpre, lane_excl);
 }
 
-struct Elem {
-    uint32_t key;
-    uint32_t ts_off;
-    int32_t a;
-    uint32_t p;
-    int64_t bucket;
-};
-
-__device__ __forceinline__ Elem load_elem(const ClusterState &st, const uint32_t *keys, const Payload *pay,
-                                          int64_t ts_base, uint32_t e) {
-    Elem x;
-    x.key = keys[e];
-    const Payload q = pay[e];
-    x.ts_off = q.ts_off;
-    x.a = (int32_t)(q.acq_prio & 0x7FFFFFFFu);
-    x.p = q.acq_prio >> 31;
-    const int64_t t = ts_base + (int64_t)q.ts_off;
-    x.bucket = t / (int64_t)st.param[x.key].W;
-    return x;
-}
-
-__global__ __launch_bounds__(kThreads) void k_runs_up(ClusterState st, const uint32_t *__restrict__ keys,
-                                                      const Payload *__restrict__ pay, int64_t ts_base,
-                                                      const uint32_t *__restrict__ counters, Agg *__restrict__ tile_agg) {
-    const uint32_t nvalid = counters[0];
-    const uint32_t base = blockIdx.x * kTileElems;
-    if (base >= nvalid) return;
-    const uint32_t e0 = base + threadIdx.x * kItems;
-    Agg acc = agg_identity();
-    if (e0 < nvalid) {
-        Elem prev;
-        if (e0 > 0) prev = load_elem(st, keys, pay, ts_base, e0 - 1);
-        for (int i = 0; i < kItems; ++i) {
-            const uint32_t e = e0 + i;
-            if (e >= nvalid) break;
-            const Elem x = load_elem(st, keys, pay, ts_base, e);
-            const bool fh = e == 0 || x.key != prev.key;
-            const bool h = fh || x.bucket != prev.bucket;
-            Agg v{h ? 1u : 0u, fh ? 1u : 0u, h ? 1u : 0u, x.p, x.a, x.a};
-            acc = agg_combine(acc, v);
-            prev = x;
-        }
-    }
-    Agg total;
-    block_excl_scan<kThreads>(acc, &total);
-    if (threadIdx.x == 0) tile_agg[blockIdx.x] = total;
-}
-
-constexpr int kTileScanThreads = 1024;
-
+// Single workgroup: tile carries, nvalid / nruns / nflows.
 __global__ __launch_bounds__(kTileScanThreads) void k_runs_tiles(const Agg *__restrict__ tile_agg,
-                                                                 const uint32_t *__restrict__ counters,
-                                                                 Agg *__restrict__ tile_carry) {
-    const uint32_t nvalid = counters[0];
-    const uint32_t ntiles = (nvalid + kTileElems - 1) / kTileElems;
+                                                                 const uint32_t *__restrict__ tile_valid,
+                                                                 uint32_t ntiles, Agg *__restrict__ tile_carry,
+                                                                 uint32_t *__restrict__ counters) {
     Agg carry = agg_identity();
+    uint32_t nvalid = 0;
     for (uint32_t b = 0; b < ntiles; b += kTileScanThreads) {
         const uint32_t t = b + threadIdx.x;
         const Agg v = t < ntiles ? tile_agg[t] : agg_identity();
+        const uint32_t c = t < ntiles ? tile_valid[t] : 0;
         Agg total;
-        const Agg ex = block_excl_scan<kTileScanThreads>(v, &total);
+        const Agg ex = block_excl_scan_1024(v, &total);
         if (t < ntiles) tile_carry[t] = agg_combine(carry, ex);
         carry = agg_combine(carry, total);
+        // valid counts: plain block sum
+        uint32_t s = c;
+        for (int o = 32; o > 0; o >>= 1) s += (uint32_t)__shfl_down((int)s, o, 64);
+        __shared__ uint32_t ws[kTileScanThreads / 64];
+        if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int w = 0; w < kTileScanThreads / 64; ++w) nvalid += ws[w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        counters[0] = nvalid;
+        counters[1] = carry.nh;
+        counters[2] = carry.nf;
     }
 }
 
-__global__ __launch_bounds__(kThreads) void k_runs_down(ClusterState st, const uint32_t *__restrict__ keys,
-                                                        const Payload *__restrict__ pay, int64_t ts_base,
+// Per tile: per-event run id and prioritized prefix; run and flow records.
+__global__ __launch_bounds__(kRunThreads) void k_runs_down(const uint32_t *__restrict__ keys,
+                                                        const Payload *__restrict__ pay, uint32_t invalid_key,
                                                         const Agg *__restrict__ tile_carry, BatchScratch sc) {
+    __shared__ Agg wagg[kRunWaves];
     const uint32_t nvalid = sc.counters[0];
     const uint32_t base = blockIdx.x * kTileElems;
     if (base >= nvalid) return;
-    const uint32_t e0 = base + threadIdx.x * kItems;
-    // pass 1: thread aggregate
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t wb = base + wave * kWaveElems;
+    RunIn x[kRunRounds];
+    const RunIn first_prev = run_load(keys, pay, wb - 1, wb > 0 ? min(wb, nvalid) : 0, invalid_key);
+    RunIn last = first_prev;
     Agg acc = agg_identity();
-    Elem prev;
-    const bool any = e0 < nvalid;
-    if (any) {
-        if (e0 > 0) prev = load_elem(st, keys, pay, ts_base, e0 - 1);
-        Elem pv = prev;
-        for (int i = 0; i < kItems; ++i) {
-            const uint32_t e = e0 + i;
-            if (e >= nvalid) break;
-            const Elem x = load_elem(st, keys, pay, ts_base, e);
-            const bool fh = e == 0 || x.key != pv.key;
-            const bool h = fh || x.bucket != pv.bucket;
-            acc = agg_combine(acc, Agg{h ? 1u : 0u, fh ? 1u : 0u, h ? 1u : 0u, x.p, x.a, x.a});
-            pv = x;
+    // pass 1: ordered wave reduction per round (elements stay in registers)
+#pragma unroll
+    for (int r = 0; r < kRunRounds; ++r) {
+        const uint32_t e = wb + r * 64 + lane;
+        x[r] = run_load(keys, pay, e, nvalid, invalid_key);
+        RunIn px = run_shfl_up1(x[r]);
+        if (lane == 0) px = last;
+        Agg v = run_value(x[r], px, e > 0, e < nvalid);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const Agg y = agg_shfl(v, (lane + o) & 63);
+            if (lane + o < 64 && (lane & (2 * o - 1)) == 0) v = agg_combine(v, y);
         }
+        acc = agg_combine(acc, agg_shfl(v, 0));
+        last.key = shfl_u32(x[r].key, 63);
+        last.q.bucket = shfl_u32(x[r].q.bucket, 63);
     }
-    const Agg ex = block_excl_scan<kThreads>(acc, nullptr);
-    if (!any) return;
-    Agg run = agg_combine(tile_carry[blockIdx.x], ex);  // everything before e0
-    Elem x = load_elem(st, keys, pay, ts_base, e0);
-    for (int i = 0; i < kItems; ++i) {
-        const uint32_t e = e0 + i;
-        if (e >= nvalid) break;
-        const bool fh = e == 0 || x.key != prev.key;
-        const bool h = fh || x.bucket != prev.bucket;
-        run = agg_combine(run, Agg{h ? 1u : 0u, fh ? 1u : 0u, h ? 1u : 0u, x.p, x.a, x.a});
-        const uint32_t r = run.nh - 1;
-        sc.ev_run[e] = r;
-        sc.ev_cp[e] = run.cnt - x.p;
+    if (lane == 0) wagg[wave] = acc;
+    __syncthreads();
+    Agg carry = tile_carry[blockIdx.x];
+    for (int w = 0; w < wave; ++w) carry = agg_combine(carry, wagg[w]);
+    // element after this wave's sub-tile (for the last element of the last round)
+    const uint32_t enext = wb + kWaveElems;
+    const RunIn after = run_load(keys, pay, enext, nvalid, invalid_key);
+    // pass 2: inclusive scan per round with the running carry
+#pragma unroll
+    for (int r = 0; r < kRunRounds; ++r) {
+        const uint32_t e = wb + r * 64 + lane;
+        // cross-lane reads are done by every lane (a shuffle from an inactive lane is undefined)
+        RunIn px = run_shfl_up1(x[r]);
+        const uint32_t prev_key = r == 0 ? first_prev.key : shfl_u32(x[r > 0 ? r - 1 : 0].key, 63);
+        const uint32_t prev_bucket = r == 0 ? first_prev.q.bucket : shfl_u32(x[r > 0 ? r - 1 : 0].q.bucket, 63);
+        uint32_t nkey = (uint32_t)__shfl_down((int)x[r].key, 1, 64);
+        uint32_t nbucket = (uint32_t)__shfl_down((int)x[r].q.bucket, 1, 64);
+        const uint32_t next_key = r + 1 < kRunRounds ? shfl_u32(x[r + 1 < kRunRounds ? r + 1 : r].key, 0) : after.key;
+        const uint32_t next_bucket =
+            r + 1 < kRunRounds ? shfl_u32(x[r + 1 < kRunRounds ? r + 1 : r].q.bucket, 0) : after.q.bucket;
+        if (lane == 0) {
+            px.key = prev_key;
+            px.q.bucket = prev_bucket;
+        }
+        if (lane == 63) {
+            nkey = next_key;
+            nbucket = next_bucket;
+        }
+        const Agg vr = wave_incl_scan(run_value(x[r], px, e > 0, e < nvalid), lane);
+        const Agg run = agg_combine(carry, vr);  // inclusive up to e
+        carry = agg_combine(carry, agg_shfl(vr, 63));
+        if (e >= nvalid) continue;
+        const uint32_t rid = run.nh - 1;
+        const uint32_t p = x[r].q.acq_prio >> 31;
+        sc.ev_run[e] = rid;
+        sc.ev_cp[e] = run.cnt - p;
+        const bool fh = e == 0 || x[r].key != px.key;
+        const bool h = fh || x[r].q.bucket != px.q.bucket;
         if (h) {
-            sc.run_start[r] = e;
-            sc.run_slot[r] = x.key;
-            sc.run_t0off[r] = x.ts_off;
+            sc.run_start[rid] = e;
+            sc.run_slot[rid] = x[r].key;
+            sc.run_t0off[rid] = x[r].q.ts_off;
         }
-        if (fh) sc.flow_first_run[run.nf - 1] = r;
-        // is e the last event of its run?
-        bool last = (e + 1 >= nvalid);
-        Elem nx;
-        if (!last) {
-            nx = load_elem(st, keys, pay, ts_base, e + 1);
-            last = nx.key != x.key || nx.bucket != x.bucket;
+        if (fh) sc.flow_first_run[run.nf - 1] = rid;
+        const bool last_of_run = (e + 1 >= nvalid) || nkey != x[r].key || nbucket != x[r].q.bucket;
+        if (last_of_run) {
+            sc.run_end[rid] = e + 1;
+            sc.run_cp[rid] = run.cnt;
+            sc.run_amin[rid] = run.mn;
+            sc.run_amax[rid] = run.mx;
         }
-        if (last) {
-            sc.run_end[r] = e + 1;
-            sc.run_cp[r] = run.cnt;
-            sc.run_amin[r] = run.mn;
-            sc.run_amax[r] = run.mx;
-        }
-        if (e + 1 == nvalid) {
-            sc.counters[1] = run.nh;
-            sc.counters[2] = run.nf;
-        }
-        prev = x;
-        if (e + 1 < nvalid) x = nx;
     }
 }
 
 // ---------------------------------------------------------------- exact per-request replay (device)
+// Window state of a rule lives in one contiguous record of 8 fields x S buckets:
+// field 0 = window start (kAbsent = null slot), fields 1..7 = ClusterFlowEvent sums.
+struct Rec {
+    int64_t *r;
+    int S;
+    __device__ __forceinline__ int64_t &start(int j) const { return r[j]; }
+    __device__ __forceinline__ int64_t &cnt(int ev, int j) const { return r[(1 + ev) * S + j]; }
+};
+
+__device__ __forceinline__ Rec rec_of(const ClusterState &st, const SlotParam &P) {
+    return Rec{st.rec + (size_t)P.boff * 8, P.S};
+}
+
 struct WinRef {
-    uint32_t b;
+    int j;
     bool detached;
 };
 
-__device__ __forceinline__ void bucket_zero(const ClusterState &st, uint32_t b) {
+__device__ __forceinline__ void bucket_zero(const Rec &R, int j) {
 #pragma unroll
-    for (int k = 0; k < CEV_N; ++k) st.cnt[k][b] = 0;
+    for (int k = 0; k < CEV_N; ++k) R.cnt(k, j) = 0;
 }
 
 // LeapArray.currentWindow(t) on a ClusterMetricLeapArray (t >= 0)
 __device__ WinRef cur_window(const ClusterState &st, const SlotParam &P, uint32_t s, int64_t t) {
-    const int64_t tid = t / P.W;
-    const uint32_t b = P.boff + (uint32_t)(tid % P.S);
+    const Rec R = rec_of(st, P);
+    const int j = (int)((t / P.W) % P.S);
     const int64_t ws = t - t % P.W;
-    const int64_t old = st.bstart[b];
+    const int64_t old = R.start(j);
     if (old == kAbsent) {  // newEmptyBucket: no occupy transfer
-        st.bstart[b] = ws;
-        bucket_zero(st, b);
-        return WinRef{b, false};
+        R.start(j) = ws;
+        bucket_zero(R, j);
+        return WinRef{j, false};
     }
-    if (ws == old) return WinRef{b, false};
+    if (ws == old) return WinRef{j, false};
     if (ws > old) {  // resetWindowTo + transferOccupyToBucket
-        st.bstart[b] = ws;
-        bucket_zero(st, b);
+        R.start(j) = ws;
+        bucket_zero(R, j);
         SlotOcc &o = st.occ[s];
         if (o.has_occ) {
-            st.cnt[CEV_OCCUPIED_PASS][b] += o.occ_pass;
-            st.cnt[CEV_PASS][b] += o.occ_pass;
+            R.cnt(CEV_OCCUPIED_PASS, j) += o.occ_pass;
+            R.cnt(CEV_PASS, j) += o.occ_pass;
             o.occ_pass = 0;
-            st.cnt[CEV_PASS_REQUEST][b] += o.occ_preq;
+            R.cnt(CEV_PASS_REQUEST, j) += o.occ_preq;
             o.occ_preq = 0;
             o.has_occ = 0;
         }
-        return WinRef{b, false};
+        return WinRef{j, false};
     }
-    return WinRef{b, true};  // time went backwards: detached bucket, adds lost
+    return WinRef{j, true};  // time went backwards: detached bucket, adds lost
 }
 
 __device__ int64_t values_sum(const ClusterState &st, const SlotParam &P, int64_t t, int ev) {
+    const Rec R = rec_of(st, P);
     int64_t s = 0;
     for (int j = 0; j < P.S; ++j) {
-        const uint32_t b = P.boff + j;
-        const int64_t w = st.bstart[b];
-        if (w != kAbsent && !(t - w > (int64_t)P.interval)) s += st.cnt[ev][b];
+        const int64_t w = R.start(j);
+        if (w != kAbsent && !(t - w > (int64_t)P.interval)) s += R.cnt(ev, j);
     }
     return s;
 }
@@ -344,7 +437,15 @@ __device__ __forceinline__ double get_avg(const ClusterState &st, const SlotPara
 __device__ __forceinline__ void metric_add(const ClusterState &st, const SlotParam &P, uint32_t s, int64_t t, int ev,
                                            int64_t n) {
     const WinRef w = cur_window(st, P, s, t);
-    if (!w.detached) st.cnt[ev][w.b] += n;
+    if (!w.detached) rec_of(st, P).cnt(ev, w.j) += n;
+}
+
+// ClusterMetricLeapArray.getFirstCountOfWindow(PASS) = getValidHead(now).value().get(PASS)
+__device__ __forceinline__ int64_t head_pass(const ClusterState &st, const SlotParam &P, int64_t t) {
+    const Rec R = rec_of(st, P);
+    const int j = (int)(((t + P.W) / P.W) % P.S);
+    const int64_t w = R.start(j);
+    return (w != kAbsent && !(t - w > (int64_t)P.interval)) ? R.cnt(CEV_PASS, j) : 0;
 }
 
 // ClusterFlowChecker.acquireClusterToken / SimpleClusterFlowChecker.acquireClusterToken for one request
@@ -364,12 +465,7 @@ __device__ uint64_t request_exact(const ClusterState &st, uint32_t s, int64_t t,
         if (occupy_avg <= st.max_occupy_ratio * thr) {
             // ClusterMetric.tryOccupyNext(PASS, a, thr)
             const double latest2 = get_avg(st, P, s, t, CEV_PASS);
-            int64_t head = 0;
-            {
-                const uint32_t hb = P.boff + (uint32_t)(((t + P.W) / P.W) % P.S);
-                const int64_t w = st.bstart[hb];
-                if (w != kAbsent && !(t - w > (int64_t)P.interval)) head = st.cnt[CEV_PASS][hb];
-            }
+            const int64_t head = head_pass(st, P, t);
             SlotOcc &o = st.occ[s];
             if (latest2 + (double)((int64_t)a + o.occ_pass) - (double)head <= thr) {
                 o.occ_pass += a;
@@ -403,16 +499,18 @@ __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratc
         for (uint32_t r = r0; r < r1; ++r) {
             const uint32_t s = sc.run_slot[r];
             const SlotParam P = st.param[s];
+            const Rec R = rec_of(st, P);
             const uint32_t j0 = sc.run_start[r], j1 = sc.run_end[r];
             const uint32_t n = j1 - j0;
             const int64_t t0 = ts_base + (int64_t)sc.run_t0off[r];
             const uint32_t cp_tot = sc.run_cp[r];
             const int32_t a = sc.run_amin[r];
             const double thr = simple ? P.thr_simple : P.thr;
-            // ---- decide fast path eligibility
+            // ---- fast path eligibility: equal acquire counts, no clock regression,
+            //      prioritized requests only where the occupy path is regular
             const int64_t ws = t0 - t0 % P.W;
-            const uint32_t cb = P.boff + (uint32_t)((t0 / P.W) % P.S);
-            const int64_t old = st.bstart[cb];
+            const int cj = (int)((t0 / P.W) % P.S);
+            const int64_t old = R.start(cj);
             bool fast = (a == sc.run_amax[r]) && !(old != kAbsent && ws < old);
             if (cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) fast = false;
             if (!fast) {
@@ -430,22 +528,16 @@ __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratc
             cur_window(st, P, s, t0);
             int64_t base_pass = 0, base_wait = 0;
             for (int jj = 0; jj < P.S; ++jj) {
-                const uint32_t b = P.boff + jj;
-                if (b == cb) continue;
-                const int64_t w = st.bstart[b];
+                if (jj == cj) continue;
+                const int64_t w = R.start(jj);
                 if (w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
-                    base_pass += st.cnt[CEV_PASS][b];
-                    base_wait += st.cnt[CEV_WAITING][b];
+                    base_pass += R.cnt(CEV_PASS, jj);
+                    base_wait += R.cnt(CEV_WAITING, jj);
                 }
             }
-            int64_t head = 0;
-            {
-                const uint32_t hb = P.boff + (uint32_t)(((t0 + P.W) / P.W) % P.S);
-                const int64_t w = st.bstart[hb];
-                if (w != kAbsent && !(t0 - w > (int64_t)P.interval)) head = st.cnt[CEV_PASS][hb];
-            }
-            const int64_t s0 = base_pass + st.cnt[CEV_PASS][cb];
-            const int64_t w0 = base_wait + st.cnt[CEV_WAITING][cb];
+            const int64_t head = head_pass(st, P, t0);
+            const int64_t s0 = base_pass + R.cnt(CEV_PASS, cj);
+            const int64_t w0 = base_wait + R.cnt(CEV_WAITING, cj);
             // ---- pass prefix: first i with !cond(s0 + i*a, a)   (monotone in i)
             uint32_t lo = 0, hi = n;
             while (lo < hi) {
@@ -477,13 +569,13 @@ __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratc
             const int64_t fa = (int64_t)f * a;
             const int64_t wa = (int64_t)cw * a;
             const uint32_t nblk = n - f - cw;
-            st.cnt[CEV_PASS][cb] += fa;
-            st.cnt[CEV_PASS_REQUEST][cb] += f;
-            st.cnt[CEV_OCCUPIED_PASS][cb] += (int64_t)cpf * a;
-            st.cnt[CEV_WAITING][cb] += wa;
-            st.cnt[CEV_BLOCK][cb] += (int64_t)nblk * a;
-            st.cnt[CEV_BLOCK_REQUEST][cb] += nblk;
-            st.cnt[CEV_OCCUPIED_BLOCK][cb] += (int64_t)(np_after - cw) * a;
+            R.cnt(CEV_PASS, cj) += fa;
+            R.cnt(CEV_PASS_REQUEST, cj) += f;
+            R.cnt(CEV_OCCUPIED_PASS, cj) += (int64_t)cpf * a;
+            R.cnt(CEV_WAITING, cj) += wa;
+            R.cnt(CEV_BLOCK, cj) += (int64_t)nblk * a;
+            R.cnt(CEV_BLOCK_REQUEST, cj) += nblk;
+            R.cnt(CEV_OCCUPIED_BLOCK, cj) += (int64_t)(np_after - cw) * a;
             if (cw > 0) {
                 SlotOcc &o = st.occ[s];
                 o.occ_pass += wa;
@@ -533,12 +625,17 @@ __global__ void k_metric_sums(ClusterState st, uint32_t s, int64_t now, int64_t 
     for (int k = 0; k < CEV_N; ++k) out7[k] = values_sum(st, P, now, k);
 }
 
-__global__ void k_init_buckets(ClusterState st, uint32_t b0, uint32_t b1) {
-    const uint32_t b = b0 + blockIdx.x * kThreads + threadIdx.x;
-    if (b >= b1) return;
-    st.bstart[b] = kAbsent;
-#pragma unroll
-    for (int k = 0; k < CEV_N; ++k) st.cnt[k][b] = 0;
+__global__ void k_init_slots(ClusterState st, const uint32_t *slots, uint32_t n) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = slots[i];
+    const SlotParam P = st.param[s];
+    const Rec R = rec_of(st, P);
+    for (int j = 0; j < P.S; ++j) {
+        R.start(j) = kAbsent;
+        bucket_zero(R, j);
+    }
+    st.occ[s] = SlotOcc{0, 0, 0, 0};
 }
 
 }  // namespace
@@ -565,7 +662,7 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += 3 * align_up(cap * 4);                 // run_f, run_cpf, run_cw
     b += align_up(cap);                         // run_mode
     b += align_up(cap * 4);                     // flow_first_run
-    b += 2 * align_up(ntiles * sizeof(Agg));
+    b += 2 * align_up(ntiles * sizeof(Agg)) + align_up(ntiles * 4);
     b += align_up(64);
     b += 2 * align_up(hist * 4) + align_up(scan_partials_needed(hist) * 4 + 64);
     return b;
@@ -602,6 +699,7 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.flow_first_run = (uint32_t *)take(cap * 4);
     sc.tile_agg = take(ntiles * sizeof(Agg));
     sc.tile_carry = take(ntiles * sizeof(Agg));
+    sc.tile_valid = (uint32_t *)take(ntiles * 4);
     sc.counters = (uint32_t *)take(64);
     sc.radix.hist = (uint32_t *)take(hist * 4);
     sc.radix.hist_scan = (uint32_t *)take(hist * 4);
@@ -619,17 +717,17 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     const uint32_t invalid_key = st.nslots;
     SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, s));
     const uint32_t nb = (n + kThreads - 1) / kThreads;
-    hipLaunchKernelGGL(k_classify, dim3(nb), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, n, simple,
-                       invalid_key, sc.keys[0], sc.pay[0], out, sc.counters);
+    hipLaunchKernelGGL(k_classify, dim3(nb), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n,
+                       simple, invalid_key, sc.keys[0], sc.pay[0], out, sc.counters);
     const int npass = radix_sort_pairs(sc.keys[0], sc.pay[0], sc.keys[1], sc.pay[1], n, bits, sc.radix, s);
     const uint32_t *keys = sc.keys[npass & 1];
     const Payload *pay = sc.pay[npass & 1];
     const uint32_t ntiles = (n + kTileElems - 1) / kTileElems;
-    hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kThreads), 0, s, st, keys, pay, ts_base, sc.counters,
-                       (Agg *)sc.tile_agg);
-    hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.counters,
-                       (Agg *)sc.tile_carry);
-    hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kThreads), 0, s, st, keys, pay, ts_base,
+    hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, keys, pay, n, invalid_key, (Agg *)sc.tile_agg,
+                       sc.tile_valid);
+    hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
+                       ntiles, (Agg *)sc.tile_carry, sc.counters);
+    hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, keys, pay, invalid_key,
                        (const Agg *)sc.tile_carry, sc);
     uint32_t flow_threads = n < st.nslots ? n : st.nslots;
     uint32_t fb = (flow_threads + kThreads - 1) / kThreads;
@@ -642,10 +740,9 @@ void cluster_metric_sums(const ClusterState &st, uint32_t slot, int64_t now, int
     hipLaunchKernelGGL(k_metric_sums, dim3(1), dim3(64), 0, s, st, slot, now, d_out7);
 }
 
-void cluster_init_buckets(const ClusterState &st, uint32_t b0, uint32_t b1, hipStream_t s) {
-    if (b1 <= b0) return;
-    const uint32_t nb = (b1 - b0 + kThreads - 1) / kThreads;
-    hipLaunchKernelGGL(k_init_buckets, dim3(nb), dim3(kThreads), 0, s, st, b0, b1);
+void cluster_init_slots(const ClusterState &st, const uint32_t *d_slots, uint32_t n, hipStream_t s) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_init_slots, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, st, d_slots, n);
 }
 
 }  // namespace sga

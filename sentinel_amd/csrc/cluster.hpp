@@ -11,7 +11,7 @@ struct SlotParam {
     double thr;         // calcGlobalThreshold(rule) * exceedCount   ClusterFlowChecker.java:38-48,68
     double thr_simple;  // rule.count * exceedCount                  SimpleClusterFlowChecker.java:43
     double isec;        // LeapArray.intervalInSecond = intervalInMs / 1000.0  LeapArray.java:68
-    uint32_t boff;      // first bucket of this slot's ClusterMetricLeapArray
+    uint32_t boff;      // bucket offset of this slot's ClusterMetricLeapArray (record at rec[8*boff])
     int32_t S;          // sampleCount of the metric (fixed at metric creation)
     int32_t W;          // windowLengthInMs = interval / sampleCount
     int32_t interval;   // intervalInMs
@@ -31,13 +31,19 @@ struct SlotOcc {
 enum : int { CEV_PASS = 0, CEV_BLOCK, CEV_PASS_REQUEST, CEV_BLOCK_REQUEST, CEV_OCCUPIED_PASS, CEV_OCCUPIED_BLOCK,
              CEV_WAITING, CEV_N };
 
+// flowId -> slot hash entry (16 B, one load per probe); key 0 = empty (flowIds are > 0)
+struct alignas(16) HashEntry {
+    int64_t key;
+    uint32_t slot;
+    uint32_t W;  // windowLengthInMs of the slot's metric
+};
+
 struct ClusterState {
     const SlotParam *param;
     SlotOcc *occ;
-    int64_t *bstart;         // [nbuckets] window start or kAbsent
-    int64_t *cnt[CEV_N];     // [nbuckets] LongAdder sums per ClusterFlowEvent
-    const int64_t *hkeys;    // open-addressing flowId -> slot
-    const uint32_t *hvals;
+    int64_t *rec;            // per slot: 8 fields x S buckets at rec[8*boff]; field 0 = window start
+                             // (kAbsent = null), fields 1..7 = LongAdder sums per ClusterFlowEvent
+    const HashEntry *htab;   // open-addressing flowId -> (slot, windowLengthInMs)
     uint32_t hmask;
     uint32_t nslots;
     double max_occupy_ratio;
@@ -59,6 +65,7 @@ struct BatchScratch {
     // tile scan
     void *tile_agg;
     void *tile_carry;
+    uint32_t *tile_valid;
     uint32_t *counters;  // [0]=nvalid [1]=nruns [2]=nflows [3]=flags
     RadixScratch radix;
     size_t cap = 0;
@@ -76,7 +83,7 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
 // ClusterMetric.getSum for all 7 events at `now` (rotates the current window as the reference does).
 void cluster_metric_sums(const ClusterState &st, uint32_t slot, int64_t now, int64_t *d_out7, hipStream_t stream);
 
-// Fills bucket range [b0, b1) with kAbsent / zero counters.
-void cluster_init_buckets(const ClusterState &st, uint32_t b0, uint32_t b1, hipStream_t stream);
+// Fresh metrics: every bucket of each listed slot absent, occupy counters zero.
+void cluster_init_slots(const ClusterState &st, const uint32_t *d_slots, uint32_t n, hipStream_t stream);
 
 }  // namespace sga

@@ -47,10 +47,9 @@ struct Engine {
     // ---- device state
     DevBuf<SlotParam> d_param;
     DevBuf<SlotOcc> d_occ;
-    DevBuf<int64_t> d_bstart;
-    DevBuf<int64_t> d_cnt[CEV_N];
-    DevBuf<int64_t> d_hkeys;
-    DevBuf<uint32_t> d_hvals;
+    DevBuf<int64_t> d_rec;  // 8 int64 per bucket
+    DevBuf<HashEntry> d_htab;
+    DevBuf<uint32_t> d_fresh;
     uint32_t hmask = 0;
     DevBuf<uint8_t> d_scratch;
     BatchScratch scratch;
@@ -70,10 +69,8 @@ struct Engine {
         ClusterState st{};
         st.param = d_param.p;
         st.occ = d_occ.p;
-        st.bstart = d_bstart.p;
-        for (int k = 0; k < CEV_N; ++k) st.cnt[k] = d_cnt[k].p;
-        st.hkeys = d_hkeys.p;
-        st.hvals = d_hvals.p;
+        st.rec = d_rec.p;
+        st.htab = d_htab.p;
         st.hmask = hmask;
         st.nslots = (uint32_t)slots.size();
         st.max_occupy_ratio = cfg.max_occupy_ratio;
@@ -124,10 +121,9 @@ struct Engine {
             d_param.grow(c, stream);
             d_occ.grow(c, stream);
         }
-        if (d_bstart.n < std::max<uint32_t>(bucket_used, 1)) {
-            size_t c = std::max<size_t>(bucket_used, d_bstart.n * 2);
-            d_bstart.grow(c, stream);
-            for (int k = 0; k < CEV_N; ++k) d_cnt[k].grow(c, stream);
+        if (d_rec.n < 8 * (size_t)std::max<uint32_t>(bucket_used, 1)) {
+            size_t c = std::max<size_t>(8 * (size_t)bucket_used, d_rec.n * 2);
+            d_rec.grow(c, stream);
         }
         // param table
         std::vector<SlotParam> hp(ns);
@@ -155,28 +151,30 @@ struct Engine {
         for (auto &h : slots) nact += h.active ? 1 : 0;
         size_t hcap = 1024;
         while (hcap < 2 * nact + 1) hcap <<= 1;
-        std::vector<int64_t> hk(hcap, 0);
-        std::vector<uint32_t> hv(hcap, 0);
+        std::vector<HashEntry> ht(hcap);
+        std::memset(ht.data(), 0, hcap * sizeof(HashEntry));
         for (size_t i = 0; i < ns; ++i) {
             if (!slots[i].active) continue;
             uint32_t h = (uint32_t)hash_flow_id(slots[i].flow_id) & (uint32_t)(hcap - 1);
-            while (hk[h] != 0) h = (h + 1) & (uint32_t)(hcap - 1);
-            hk[h] = slots[i].flow_id;
-            hv[h] = (uint32_t)i;
+            while (ht[h].key != 0) h = (h + 1) & (uint32_t)(hcap - 1);
+            ht[h].key = slots[i].flow_id;
+            ht[h].slot = (uint32_t)i;
+            ht[h].W = (uint32_t)(slots[i].interval / slots[i].S);
         }
-        if (d_hkeys.n != hcap) {
+        if (d_htab.n != hcap) {
             SGA_HIP_CHECK(hipStreamSynchronize(stream));
-            d_hkeys.alloc(hcap);
-            d_hvals.alloc(hcap);
+            d_htab.alloc(hcap);
         }
-        SGA_HIP_CHECK(hipMemcpyAsync(d_hkeys.p, hk.data(), hcap * 8, hipMemcpyHostToDevice, stream));
-        SGA_HIP_CHECK(hipMemcpyAsync(d_hvals.p, hv.data(), hcap * 4, hipMemcpyHostToDevice, stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(d_htab.p, ht.data(), hcap * sizeof(HashEntry), hipMemcpyHostToDevice, stream));
         hmask = (uint32_t)(hcap - 1);
-        // fresh metrics: empty windows, no occupy
-        ClusterState st = state();
-        for (uint32_t s : fresh) {
-            cluster_init_buckets(st, slots[s].boff, slots[s].boff + slots[s].bcap, stream);
-            SGA_HIP_CHECK(hipMemsetAsync(d_occ.p + s, 0, sizeof(SlotOcc), stream));
+        // fresh metrics: empty windows, no occupy (one kernel for all of them)
+        if (!fresh.empty()) {
+            if (d_fresh.n < fresh.size()) {
+                SGA_HIP_CHECK(hipStreamSynchronize(stream));
+                d_fresh.alloc(fresh.size());
+            }
+            SGA_HIP_CHECK(hipMemcpyAsync(d_fresh.p, fresh.data(), fresh.size() * 4, hipMemcpyHostToDevice, stream));
+            cluster_init_slots(state(), d_fresh.p, (uint32_t)fresh.size(), stream);
         }
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
         ensure_scratch();
@@ -463,7 +461,7 @@ int sga_cluster_stats(sga_engine *e, uint64_t *n_active, uint64_t *state_bytes) 
         for (auto &h : g.slots) a += h.active ? 1 : 0;
         if (n_active) *n_active = a;
         if (state_bytes)
-            *state_bytes = (uint64_t)g.bucket_used * 8 * (1 + CEV_N) + g.slots.size() * (sizeof(sga::SlotParam) +
+            *state_bytes = (uint64_t)g.bucket_used * 64 + g.slots.size() * (sizeof(sga::SlotParam) +
                                                                                       sizeof(sga::SlotOcc));
         return SGA_OK;
     });

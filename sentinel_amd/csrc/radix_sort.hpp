@@ -3,12 +3,14 @@
 
 namespace sga {
 
-// 12-byte payload carried through the sort: original index, timestamp offset,
-// acquire count with the prioritized flag in bit 31.
-struct Payload {
+// 16-byte payload carried through the sort: original index, timestamp offset,
+// acquire count with the prioritized flag in bit 31, and the low 32 bits of the
+// request's window-bucket index (t / windowLengthInMs of its rule).
+struct alignas(16) Payload {
     uint32_t idx;
     uint32_t ts_off;
     uint32_t acq_prio;
+    uint32_t bucket;
 };
 
 constexpr int kMaxDigitBits = 11;
