@@ -1,0 +1,550 @@
+/*
+ * ORACLE / TEST INFRASTRUCTURE ONLY (see sentinel_oracle.h, oracle_ext.h).
+ * ParamFlowChecker / ParameterMetric and DegradeSlot circuit breakers, and the
+ * full local slot chain entry/exit of the engine's local path.
+ *   PF = sentinel-extension/sentinel-parameter-flow-control/src/main/java/com/alibaba/csp/sentinel
+ *   CB = CORE/slots/block/degrade/circuitbreaker
+ */
+#include "oracle_internal.h"
+#include "java_semantics.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------- u64 -> i64 map */
+struct orc_pmap {
+    uint64_t *k;
+    int64_t *v;
+    uint8_t *used;
+    size_t cap, n;
+};
+
+static uint64_t pm_hash(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+static orc_pmap *pm_new(void) {
+    orc_pmap *m = (orc_pmap *)calloc(1, sizeof(orc_pmap));
+    m->cap = 64;
+    m->k = (uint64_t *)calloc(m->cap, 8);
+    m->v = (int64_t *)calloc(m->cap, 8);
+    m->used = (uint8_t *)calloc(m->cap, 1);
+    return m;
+}
+
+static void pm_free(orc_pmap *m) {
+    if (!m) return;
+    free(m->k);
+    free(m->v);
+    free(m->used);
+    free(m);
+}
+
+static int64_t *pm_find(orc_pmap *m, uint64_t key) {
+    size_t h = pm_hash(key) & (m->cap - 1);
+    while (m->used[h]) {
+        if (m->k[h] == key) return &m->v[h];
+        h = (h + 1) & (m->cap - 1);
+    }
+    return NULL;
+}
+
+static void pm_put(orc_pmap *m, uint64_t key, int64_t val) {
+    int64_t *p = pm_find(m, key);
+    if (p) {
+        *p = val;
+        return;
+    }
+    if ((m->n + 1) * 2 > m->cap) {
+        orc_pmap big = {0};
+        big.cap = m->cap * 2;
+        big.k = (uint64_t *)calloc(big.cap, 8);
+        big.v = (int64_t *)calloc(big.cap, 8);
+        big.used = (uint8_t *)calloc(big.cap, 1);
+        for (size_t i = 0; i < m->cap; i++)
+            if (m->used[i]) pm_put(&big, m->k[i], m->v[i]);
+        free(m->k);
+        free(m->v);
+        free(m->used);
+        m->k = big.k;
+        m->v = big.v;
+        m->used = big.used;
+        m->cap = big.cap;
+        m->n = big.n;
+    }
+    size_t h = pm_hash(key) & (m->cap - 1);
+    while (m->used[h]) h = (h + 1) & (m->cap - 1);
+    m->used[h] = 1;
+    m->k[h] = key;
+    m->v[h] = val;
+    m->n++;
+}
+
+static void pm_remove(orc_pmap *m, uint64_t key) {
+    size_t h = pm_hash(key) & (m->cap - 1);
+    while (m->used[h]) {
+        if (m->k[h] == key) break;
+        h = (h + 1) & (m->cap - 1);
+    }
+    if (!m->used[h]) return;
+    m->used[h] = 0;
+    m->n--;
+    /* re-insert the rest of the cluster (linear probing deletion) */
+    size_t j = (h + 1) & (m->cap - 1);
+    while (m->used[j]) {
+        uint64_t k = m->k[j];
+        int64_t v = m->v[j];
+        m->used[j] = 0;
+        m->n--;
+        pm_put(m, k, v);
+        j = (j + 1) & (m->cap - 1);
+    }
+}
+
+/* ---------------------------------------------------------------- param rules */
+struct orc_prule {
+    orc_param_rule r;
+    uint64_t *hot_v;
+    int32_t *hot_t;
+    orc_pmap *time;   /* ParameterMetric.ruleTimeCounters[rule] */
+    orc_pmap *token;  /* ParameterMetric.ruleTokenCounter[rule] */
+};
+
+orc_prule *orc_prule_new(const orc_param_rule *r) {
+    orc_prule *p = (orc_prule *)calloc(1, sizeof(orc_prule));
+    p->r = *r;
+    if (r->n_hot) {
+        p->hot_v = (uint64_t *)malloc(8 * r->n_hot);
+        p->hot_t = (int32_t *)malloc(4 * r->n_hot);
+        memcpy(p->hot_v, r->hot_values, 8 * r->n_hot);
+        memcpy(p->hot_t, r->hot_thresholds, 4 * r->n_hot);
+    }
+    p->r.hot_values = p->hot_v;
+    p->r.hot_thresholds = p->hot_t;
+    p->time = pm_new();
+    p->token = pm_new();
+    return p;
+}
+
+void orc_prule_free(orc_prule *p) {
+    if (!p) return;
+    free(p->hot_v);
+    free(p->hot_t);
+    pm_free(p->time);
+    pm_free(p->token);
+    free(p);
+}
+
+static int hot_lookup(const orc_prule *p, uint64_t value, int64_t *thr) {
+    for (uint32_t i = 0; i < p->r.n_hot; i++)
+        if (p->hot_v[i] == value) {
+            *thr = p->hot_t[i];
+            return 1;
+        }
+    return 0;
+}
+
+static int64_t lwrap_mul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+static int64_t lwrap_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+
+/* ParamFlowChecker.passDefaultLocalCheck, PF/slots/block/flow/param/ParamFlowChecker.java:132-222 */
+static int pass_default(orc_prule *p, uint64_t value, int acquire, int64_t now) {
+    int64_t token_count = j_d2l(p->r.count);
+    int64_t hot;
+    if (hot_lookup(p, value, &hot)) token_count = hot;
+    if (token_count == 0) return 0;
+    const int64_t max_count = lwrap_add(token_count, p->r.burst_count);
+    if ((int64_t)acquire > max_count) return 0;
+    int64_t *last = pm_find(p->time, value);
+    if (!last) {
+        pm_put(p->time, value, now);
+        if (!pm_find(p->token, value)) pm_put(p->token, value, max_count - acquire);
+        return 1;
+    }
+    const int64_t pass_time = now - *last;
+    const int64_t dur_ms = lwrap_mul(p->r.duration_in_sec, 1000);
+    if (pass_time > dur_ms) {
+        int64_t *old = pm_find(p->token, value);
+        if (!old) {
+            pm_put(p->token, value, max_count - acquire);
+            *pm_find(p->time, value) = now;
+            return 1;
+        }
+        const int64_t rest = *old;
+        const int64_t to_add = lwrap_mul(pass_time, token_count) / dur_ms;
+        const int64_t new_qps =
+            lwrap_add(to_add, rest) > max_count ? max_count - acquire : lwrap_add(rest, to_add) - acquire;
+        if (new_qps < 0) return 0;
+        *old = new_qps;
+        *pm_find(p->time, value) = now;
+        return 1;
+    }
+    int64_t *old = pm_find(p->token, value);
+    if (old) {
+        if (*old - acquire >= 0) {
+            *old -= acquire;
+            return 1;
+        }
+        return 0;
+    }
+    /* token evicted but time kept: the reference spins (Thread.yield loop); maps never evict here */
+    return 0;
+}
+
+/* ParamFlowChecker.passThrottleLocalCheck, ParamFlowChecker.java:224-281 */
+static int pass_throttle(orc_prule *p, uint64_t value, int acquire, int64_t now, int64_t *wait_ms) {
+    int64_t token_count = j_d2l(p->r.count);
+    int64_t hot;
+    if (hot_lookup(p, value, &hot)) token_count = hot;
+    if (token_count == 0) return 0;
+    const int64_t cost =
+        j_round(1.0 * 1000 * (double)acquire * (double)p->r.duration_in_sec / (double)token_count);
+    int64_t *rec = pm_find(p->time, value);
+    if (!rec) {
+        pm_put(p->time, value, now);
+        return 1;
+    }
+    const int64_t last = *rec;
+    const int64_t expected = last + cost;
+    if (expected <= now || expected - now < p->r.max_queueing_time_ms) {
+        *rec = now;
+        const int64_t wait = expected - now;
+        if (wait > 0) {
+            *rec = expected;
+            *wait_ms = wait;
+        }
+        return 1;
+    }
+    return 0;
+}
+
+/* ParamFlowChecker.passSingleValueCheck, ParamFlowChecker.java:103-130 */
+int orc_prule_pass_single(orc_prule *p, uint64_t value, int acquire, int64_t now, int64_t thread_count,
+                          int64_t *wait_ms) {
+    int64_t dummy;
+    if (!wait_ms) wait_ms = &dummy;
+    *wait_ms = 0;
+    if (p->r.grade == ORC_GRADE_QPS) {
+        if (p->r.control_behavior == ORC_CTRL_RATE_LIMITER) return pass_throttle(p, value, acquire, now, wait_ms);
+        return pass_default(p, value, acquire, now);
+    }
+    if (p->r.grade == ORC_GRADE_THREAD) {
+        int64_t hot;
+        if (hot_lookup(p, value, &hot)) return ++thread_count <= hot;
+        return ++thread_count <= j_d2l(p->r.count);
+    }
+    return 1;
+}
+
+/* ---------------------------------------------------------------- circuit breakers */
+enum { CB_CLOSED = 0, CB_OPEN = 1, CB_HALF_OPEN = 2 };
+
+struct orc_cb {
+    orc_degrade_rule r;
+    int state;
+    int64_t next_retry;
+    int64_t recovery_ms;      /* timeWindow * 1000, AbstractCircuitBreaker.java:54 */
+    int64_t max_allowed_rt;   /* Math.round(count), ResponseTimeCircuitBreaker.java:52 */
+    orc_leap *stat;           /* LeapArray(1, statIntervalMs) of {err|slow, total} */
+};
+
+static orc_cb *cb_new(const orc_degrade_rule *r) {
+    orc_cb *c = (orc_cb *)calloc(1, sizeof(orc_cb));
+    c->r = *r;
+    c->state = CB_CLOSED;
+    c->recovery_ms = (int64_t)r->time_window * 1000;
+    c->max_allowed_rt = j_round(r->count);
+    c->stat = orc_leap_new(ORC_LEAP_UNARY, 1, r->stat_interval_ms);
+    return c;
+}
+
+static void cb_free(orc_cb *c) {
+    if (!c) return;
+    orc_leap_free(c->stat);
+    free(c);
+}
+
+/* AbstractCircuitBreaker.tryPass, AbstractCircuitBreaker.java:73-87 (+fromOpenToHalfOpen :117-139) */
+static int cb_try_pass(orc_cb *c, int64_t now, int *to_half_open) {
+    *to_half_open = 0;
+    if (c->state == CB_CLOSED) return 1;
+    if (c->state == CB_OPEN) {
+        if (now >= c->next_retry) {
+            c->state = CB_HALF_OPEN;
+            *to_half_open = 1;
+            return 1;
+        }
+        return 0;
+    }
+    return 0;
+}
+
+static void cb_to_open(orc_cb *c, int64_t now) { /* transformToOpen / fromHalfOpenToOpen */
+    if (c->state == CB_CLOSED || c->state == CB_HALF_OPEN) {
+        c->state = CB_OPEN;
+        c->next_retry = now + c->recovery_ms; /* updateNextRetryTimestamp */
+    }
+}
+
+/* onRequestComplete: ExceptionCircuitBreaker.java:69-128 / ResponseTimeCircuitBreaker.java:64-128.
+ * Bucket counter 0 = error or slow count, counter 1 = total count. */
+static void cb_on_complete(orc_cb *c, int64_t now, int64_t rt, int error) {
+    const int is_rt = c->r.grade == 0;
+    const int bad = is_rt ? (rt > c->max_allowed_rt) : error;
+    if (bad) orc_leap_add(c->stat, now, 0, 1);
+    orc_leap_add(c->stat, now, 1, 1);
+    if (c->state == CB_OPEN) return;
+    if (c->state == CB_HALF_OPEN) {
+        if (bad) {
+            cb_to_open(c, now);
+        } else {
+            c->state = CB_CLOSED; /* fromHalfOpenToClose -> resetStat: currentWindow().value().reset() */
+            orc_leap_current_window(c->stat, now);
+            int64_t e = orc_leap_current_get(c->stat, now, 0), t = orc_leap_current_get(c->stat, now, 1);
+            orc_leap_add(c->stat, now, 0, -e);
+            orc_leap_add(c->stat, now, 1, -t);
+        }
+        return;
+    }
+    const int64_t bad_count = orc_leap_values_sum(c->stat, now, 0, NULL);
+    const int64_t total = orc_leap_values_sum(c->stat, now, 1, NULL);
+    if (total < c->r.min_request_amount) return;
+    if (is_rt) {
+        const double ratio = (double)bad_count * 1.0 / (double)total;
+        if (ratio > c->r.slow_ratio_threshold) cb_to_open(c, now);
+        /* Double.compare(ratio, max) == 0 && Double.compare(max, 1.0) == 0 */
+        if (ratio == c->r.slow_ratio_threshold && c->r.slow_ratio_threshold == 1.0) cb_to_open(c, now);
+    } else {
+        double cur = (double)bad_count;
+        if (c->r.grade == 1) cur = (double)bad_count * 1.0 / (double)total;
+        if (cur > c->r.count) cb_to_open(c, now);
+    }
+}
+
+int orc_flow_cb_state(orc_flow *f, uint32_t resource, int k) {
+    if (resource >= f->n || k >= f->res[resource].ncb) return -1;
+    return f->res[resource].cb[k]->state;
+}
+
+/* ---------------------------------------------------------------- rule loading */
+static int param_rule_valid(const orc_param_rule *r) { /* ParamFlowRuleUtil.isValidParamRule, :40-50 */
+    return r->count >= 0 && r->grade >= 0 && r->duration_in_sec > 0 && r->burst_count >= 0 &&
+           r->control_behavior >= 0 && r->max_queueing_time_ms >= 0;
+}
+
+static int param_rule_equal(const orc_param_rule *a, const orc_param_rule *b) {
+    if (a->grade != b->grade || a->count != b->count || a->control_behavior != b->control_behavior ||
+        a->max_queueing_time_ms != b->max_queueing_time_ms || a->burst_count != b->burst_count ||
+        a->param_idx != b->param_idx || a->duration_in_sec != b->duration_in_sec || a->n_hot != b->n_hot)
+        return 0;
+    for (uint32_t i = 0; i < a->n_hot; i++)
+        if (a->hot_values[i] != b->hot_values[i] || a->hot_thresholds[i] != b->hot_thresholds[i]) return 0;
+    return 1;
+}
+
+/* ParamFlowRuleManager.loadRules: rules grouped by resource in list order; the
+ * ParameterMetric maps are keyed by the rule (equal rules keep their maps). */
+int orc_flow_load_param_rules(orc_flow *f, const orc_param_rule *rules, size_t n) {
+    int valid = 0;
+    for (uint32_t i = 0; i < f->n; i++) {
+        flow_res *fr = &f->res[i];
+        orc_prule **old = fr->prule;
+        int nold = fr->nprule;
+        fr->prule = NULL;
+        fr->nprule = 0;
+        for (size_t j = 0; j < n; j++) {
+            if (rules[j].resource != i || !param_rule_valid(&rules[j])) continue;
+            orc_prule *keep = NULL;
+            for (int k = 0; k < nold; k++)
+                if (old[k] && param_rule_equal(&old[k]->r, &rules[j])) {
+                    keep = old[k];
+                    old[k] = NULL;
+                    break;
+                }
+            if (!keep) keep = orc_prule_new(&rules[j]);
+            fr->prule = (orc_prule **)realloc(fr->prule, sizeof(orc_prule *) * (size_t)(fr->nprule + 1));
+            fr->prule[fr->nprule++] = keep;
+            valid++;
+        }
+        for (int k = 0; k < nold; k++) orc_prule_free(old[k]);
+        free(old);
+        if (fr->nprule && !fr->pthreads) fr->pthreads = pm_new();
+    }
+    return valid;
+}
+
+static int degrade_rule_valid(const orc_degrade_rule *r) { /* DegradeRuleManager.isValidRule, :171-203 */
+    if (!(r->count >= 0 && r->time_window > 0)) return 0;
+    if (r->min_request_amount <= 0 || r->stat_interval_ms <= 0) return 0;
+    switch (r->grade) {
+    case 0: return r->slow_ratio_threshold >= 0 && r->slow_ratio_threshold <= 1;
+    case 1: return r->count <= 1;
+    case 2: return 1;
+    default: return 0;
+    }
+}
+
+static int degrade_rule_equal(const orc_degrade_rule *a, const orc_degrade_rule *b) {
+    return a->grade == b->grade && a->count == b->count && a->time_window == b->time_window &&
+           a->min_request_amount == b->min_request_amount && a->slow_ratio_threshold == b->slow_ratio_threshold &&
+           a->stat_interval_ms == b->stat_interval_ms;
+}
+
+/* DegradeRuleManager.loadRules -> buildCircuitBreakers: an unchanged rule keeps its breaker
+ * (getExistingSameCbOrNew, DegradeRuleManager.java:150-163). */
+int orc_flow_load_degrade_rules(orc_flow *f, const orc_degrade_rule *rules, size_t n) {
+    int valid = 0;
+    for (uint32_t i = 0; i < f->n; i++) {
+        flow_res *fr = &f->res[i];
+        orc_cb **old = fr->cb;
+        int nold = fr->ncb;
+        fr->cb = NULL;
+        fr->ncb = 0;
+        for (size_t j = 0; j < n; j++) {
+            if (rules[j].resource != i || !degrade_rule_valid(&rules[j])) continue;
+            orc_cb *keep = NULL;
+            for (int k = 0; k < nold; k++)
+                if (old[k] && degrade_rule_equal(&old[k]->r, &rules[j])) {
+                    keep = old[k];
+                    old[k] = NULL;
+                    break;
+                }
+            if (!keep) keep = cb_new(&rules[j]);
+            fr->cb = (orc_cb **)realloc(fr->cb, sizeof(orc_cb *) * (size_t)(fr->ncb + 1));
+            fr->cb[fr->ncb++] = keep;
+            valid++;
+        }
+        for (int k = 0; k < nold; k++) cb_free(old[k]);
+        free(old);
+    }
+    return valid;
+}
+
+void orc_flow_res_free_ext(flow_res *fr) {
+    for (int k = 0; k < fr->nprule; k++) orc_prule_free(fr->prule[k]);
+    free(fr->prule);
+    pm_free(fr->pthreads);
+    for (int k = 0; k < fr->ncb; k++) cb_free(fr->cb[k]);
+    free(fr->cb);
+}
+
+/* ---------------------------------------------------------------- slot chain */
+static void param_thread_add(flow_res *fr, int has_param, uint64_t param) { /* ParameterMetric.addThreadCount */
+    if (!fr->pthreads || !has_param) return;
+    int64_t *c = pm_find(fr->pthreads, param);
+    if (c) (*c)++;
+    else pm_put(fr->pthreads, param, 1);
+}
+
+static void param_thread_dec(flow_res *fr, int has_param, uint64_t param) { /* ParameterMetric.decreaseThreadCount */
+    if (!fr->pthreads || !has_param) return;
+    int64_t *c = pm_find(fr->pthreads, param);
+    if (!c) {
+        pm_put(fr->pthreads, param, 0); /* putIfAbsent(value, new AtomicInteger()) */
+        return;
+    }
+    if (--(*c) <= 0) pm_remove(fr->pthreads, param);
+}
+
+/* CtSph.entryWithPriority -> StatisticSlot.entry (StatisticSlot.java:64-145) around
+ * ParamFlowSlot.checkFlow (ParamFlowSlot.java:65-92), FlowSlot (FlowSlot.java:161-172)
+ * and DegradeSlot.performChecking (DegradeSlot.java:49-66). */
+int orc_flow_entry_p(orc_flow *f, uint32_t resource, int64_t now, int acquire, int prioritized, int has_param,
+                     uint64_t param, int64_t *wait_ms) {
+    int64_t dummy;
+    if (!wait_ms) wait_ms = &dummy;
+    *wait_ms = 0;
+    if (resource >= f->n) return ORC_PASS;
+    flow_res *fr = &f->res[resource];
+    int64_t total_wait = 0;
+    /* ParamFlowSlot */
+    const int nargs = has_param ? 1 : 0;
+    for (int k = 0; k < fr->nprule; k++) {
+        orc_prule *p = fr->prule[k];
+        int idx = p->r.param_idx;
+        if (idx < 0) idx = (-idx <= nargs) ? nargs + idx : -idx; /* applyRealParamIdx */
+        if (nargs <= idx) continue;                               /* args.length <= paramIdx -> pass */
+        int64_t tc = 0;
+        if (idx == 0 && fr->pthreads) {
+            int64_t *c = pm_find(fr->pthreads, param);
+            tc = c ? *c : 0;
+        }
+        int64_t w = 0;
+        if (!orc_prule_pass_single(p, param, acquire, now, tc, &w)) {
+            orc_node_increase_block_qps(fr->node, now, acquire);
+            return ORC_BLOCK_PARAM;
+        }
+        total_wait += w;
+    }
+    /* FlowSlot */
+    int64_t w = 0;
+    int d = orc_flow_rule_check(f, resource, now, acquire, prioritized, &w);
+    if (d == ORC_BLOCK_FLOW) {
+        orc_node_increase_block_qps(fr->node, now, acquire);
+        return ORC_BLOCK_FLOW;
+    }
+    if (d == ORC_PASS_WAIT) { /* PriorityWaitException: thread++ and entry callbacks only */
+        orc_node_increase_thread_num(fr->node);
+        param_thread_add(fr, has_param, param);
+        *wait_ms = w;
+        return ORC_PASS_WAIT;
+    }
+    total_wait += w;
+    /* DegradeSlot */
+    uint8_t half_open_here[64];
+    for (int k = 0; k < fr->ncb; k++) {
+        int half = 0;
+        const int ok = cb_try_pass(fr->cb[k], now, &half);
+        if (k < 64) half_open_here[k] = (uint8_t)half;
+        if (!ok) {
+            /* DegradeException: CtSph exits the entry; the whenTerminate handlers of the
+             * breakers that turned half-open for THIS entry see the block error and move
+             * HALF_OPEN -> OPEN without touching nextRetryTimestamp (AbstractCircuitBreaker.java:123-134) */
+            for (int q = 0; q < k && q < 64; q++)
+                if (half_open_here[q] && fr->cb[q]->state == CB_HALF_OPEN) fr->cb[q]->state = CB_OPEN;
+            orc_node_increase_block_qps(fr->node, now, acquire);
+            return ORC_BLOCK_DEGRADE;
+        }
+    }
+    orc_node_increase_thread_num(fr->node);
+    orc_node_add_pass_request(fr->node, now, acquire);
+    param_thread_add(fr, has_param, param);
+    *wait_ms = total_wait;
+    return ORC_PASS;
+}
+
+/* Entry.exit of a passed entry: StatisticSlot.exit (:147-175), ParamFlowStatisticExitCallback,
+ * DegradeSlot.exit (DegradeSlot.java:68-89). */
+void orc_flow_exit_p(orc_flow *f, uint32_t resource, int64_t now, int64_t rt, int count, int error, int has_param,
+                     uint64_t param) {
+    if (resource >= f->n) return;
+    flow_res *fr = &f->res[resource];
+    orc_node *n = fr->node;
+    orc_node_add_rt_and_success(n, now, rt, count);
+    orc_node_decrease_thread_num(n);
+    if (error) orc_node_increase_exception_qps(n, now, count);
+    param_thread_dec(fr, has_param, param);
+    for (int k = 0; k < fr->ncb; k++) cb_on_complete(fr->cb[k], now, rt, error);
+}
+
+void orc_flow_replay_p(orc_flow *f, size_t n, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
+                       const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
+                       int8_t *decision, int32_t *wait_ms) {
+    for (size_t i = 0; i < n; i++) {
+        const uint8_t fl = flags ? flags[i] : 0;
+        const int hp = (fl & 4) != 0;
+        const uint64_t pv = param ? param[i] : 0;
+        if (kind && kind[i] == 1) {
+            orc_flow_exit_p(f, resource[i], ts[i], rt ? rt[i] : 0, acquire[i], (fl & 2) != 0, hp, pv);
+            if (decision) decision[i] = ORC_PASS;
+            if (wait_ms) wait_ms[i] = 0;
+            continue;
+        }
+        int64_t w = 0;
+        int d = orc_flow_entry_p(f, resource[i], ts[i], acquire[i], fl & 1, hp, pv, &w);
+        if (decision) decision[i] = (int8_t)d;
+        if (wait_ms) wait_ms[i] = (int32_t)w;
+    }
+}

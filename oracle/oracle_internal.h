@@ -1,0 +1,77 @@
+/* ORACLE / TEST INFRASTRUCTURE ONLY: internal structures shared by the oracle's
+ * translation units (not an interface). */
+#ifndef SENTINEL_ORACLE_INTERNAL_H
+#define SENTINEL_ORACLE_INTERNAL_H
+#include "sentinel_oracle.h"
+#include "oracle_ext.h"
+
+#define ORC_STATISTIC_MAX_RT 5000 /* CORE/config/SentinelConfig.java:69 DEFAULT_STATISTIC_MAX_RT */
+#define ORC_SAMPLE_COUNT 2        /* CORE/node/SampleCountProperty.java:39 */
+#define ORC_INTERVAL 1000         /* CORE/node/IntervalProperty.java:41 */
+#define ORC_OCCUPY_TIMEOUT 500    /* CORE/node/OccupyTimeoutProperty.java:40 */
+#define ORC_NCOUNTERS 7
+
+typedef struct obucket {
+    int64_t start;
+    int64_t c[ORC_NCOUNTERS];
+    int64_t min_rt;
+} obucket;
+
+struct orc_leap {
+    int kind;
+    int sample_count, interval_ms, window_ms;
+    double interval_sec;
+    obucket *b;
+    uint8_t *present;
+    obucket detached;
+    orc_leap *borrow;           /* OccupiableBucketLeapArray.borrowArray */
+    int64_t occ[ORC_NCOUNTERS]; /* ClusterMetricLeapArray.occupyCounter */
+    int has_occ;                /* ClusterMetricLeapArray.hasOccupied */
+};
+
+struct orc_node {
+    orc_leap *second; /* ArrayMetric(SAMPLE_COUNT, INTERVAL): occupiable, StatisticNode.java:99-100 */
+    orc_leap *minute; /* ArrayMetric(60, 60*1000, false), StatisticNode.java:106 */
+    int64_t threads;  /* curThreadNum LongAdder */
+    int mock;
+    double mock_pass_qps, mock_prev_pass_qps;
+    int32_t mock_threads;
+};
+
+struct orc_ctrl {
+    int behavior, grade;
+    double count;
+    int max_queueing_time_ms;
+    int64_t latest_passed_time; /* RateLimiterController.java:33 / WarmUpRateLimiterController.java:30 */
+    /* WarmUpController.java:66-73 */
+    int cold_factor;
+    int32_t warning_token, max_token;
+    double slope;
+    int64_t stored_tokens, last_filled_time;
+};
+
+typedef struct orc_cb orc_cb;        /* circuit breaker (oracle_ext.c) */
+typedef struct orc_pmap orc_pmap;    /* u64 -> i64 map (oracle_ext.c) */
+
+typedef struct flow_res {
+    orc_node *node;  /* ClusterNode of the resource (ClusterBuilderSlot.java:82-110) */
+    orc_ctrl **ctrl; /* rules' raters in FlowRuleComparator order */
+    int nctrl;
+    orc_prule **prule;  /* ParamFlowRuleManager rules of the resource, list order */
+    int nprule;
+    orc_pmap *pthreads; /* ParameterMetric.threadCountMap[0] */
+    orc_cb **cb;        /* DegradeRuleManager circuit breakers, list order */
+    int ncb;
+} flow_res;
+
+struct orc_flow {
+    uint32_t n;
+    int cold_factor;
+    flow_res *res;
+};
+
+/* helpers implemented in sentinel_oracle.c */
+int orc_flow_rule_check(orc_flow *f, uint32_t resource, int64_t now, int acquire, int prioritized, int64_t *wait_ms);
+void orc_flow_res_free_ext(flow_res *fr);
+
+#endif

@@ -5,39 +5,18 @@
  * behaviour collapses to plain integer arithmetic in a single-threaded replay
  * (LongAdder sums are order-independent; every CAS in the path succeeds).
  */
-#include "sentinel_oracle.h"
+#include "oracle_internal.h"
 #include "java_semantics.h"
 
 #include <stdlib.h>
 #include <string.h>
 
-#define ORC_STATISTIC_MAX_RT 5000 /* CORE/config/SentinelConfig.java:69 DEFAULT_STATISTIC_MAX_RT */
-#define ORC_SAMPLE_COUNT 2        /* CORE/node/SampleCountProperty.java:39 */
-#define ORC_INTERVAL 1000         /* CORE/node/IntervalProperty.java:41 */
-#define ORC_OCCUPY_TIMEOUT 500    /* CORE/node/OccupyTimeoutProperty.java:40 */
-#define ORC_NCOUNTERS 7
 
 /* ========================================================================== */
 /* LeapArray family                                                            */
 /* ========================================================================== */
 
-typedef struct obucket {
-    int64_t start;
-    int64_t c[ORC_NCOUNTERS];
-    int64_t min_rt;
-} obucket;
 
-struct orc_leap {
-    int kind;
-    int sample_count, interval_ms, window_ms;
-    double interval_sec;
-    obucket *b;
-    uint8_t *present;
-    obucket detached;
-    orc_leap *borrow;           /* OccupiableBucketLeapArray.borrowArray */
-    int64_t occ[ORC_NCOUNTERS]; /* ClusterMetricLeapArray.occupyCounter */
-    int has_occ;                /* ClusterMetricLeapArray.hasOccupied */
-};
 
 orc_leap *orc_leap_new(int kind, int sample_count, int interval_ms) {
     /* LeapArray.java:61-72 */
@@ -246,14 +225,6 @@ int64_t orc_leap_window_value_pass(orc_leap *l, int64_t t) {
 /* ArrayMetric / StatisticNode                                                  */
 /* ========================================================================== */
 
-struct orc_node {
-    orc_leap *second; /* ArrayMetric(SAMPLE_COUNT, INTERVAL): occupiable, StatisticNode.java:99-100 */
-    orc_leap *minute; /* ArrayMetric(60, 60*1000, false), StatisticNode.java:106 */
-    int64_t threads;  /* curThreadNum LongAdder */
-    int mock;
-    double mock_pass_qps, mock_prev_pass_qps;
-    int32_t mock_threads;
-};
 
 orc_node *orc_node_new(void) {
     orc_node *n = (orc_node *)calloc(1, sizeof(orc_node));
@@ -397,17 +368,6 @@ void orc_node_add_occupied_pass(orc_node *n, int64_t now, int acquire) {
 /* Traffic shaping controllers                                                  */
 /* ========================================================================== */
 
-struct orc_ctrl {
-    int behavior, grade;
-    double count;
-    int max_queueing_time_ms;
-    int64_t latest_passed_time; /* RateLimiterController.java:33 / WarmUpRateLimiterController.java:30 */
-    /* WarmUpController.java:66-73 */
-    int cold_factor;
-    int32_t warning_token, max_token;
-    double slope;
-    int64_t stored_tokens, last_filled_time;
-};
 
 /* WarmUpController.construct, WarmUpController.java:83-106 */
 static void warmup_construct(orc_ctrl *c, double count, int period, int cold_factor) {
@@ -557,17 +517,7 @@ double orc_ctrl_slope(const orc_ctrl *c) { return c->slope; }
 /* Local flow engine: StatisticSlot + FlowSlot (single default context)         */
 /* ========================================================================== */
 
-typedef struct flow_res {
-    orc_node *node;  /* ClusterNode of the resource (ClusterBuilderSlot.java:82-110) */
-    orc_ctrl **ctrl; /* rules' raters in FlowRuleComparator order */
-    int nctrl;
-} flow_res;
 
-struct orc_flow {
-    uint32_t n;
-    int cold_factor;
-    flow_res *res;
-};
 
 orc_flow *orc_flow_new(uint32_t n_resources, int cold_factor) {
     orc_flow *f = (orc_flow *)calloc(1, sizeof(orc_flow));
@@ -584,6 +534,7 @@ void orc_flow_free(orc_flow *f) {
         for (int k = 0; k < f->res[i].nctrl; k++) orc_ctrl_free(f->res[i].ctrl[k]);
         free(f->res[i].ctrl);
         orc_node_free(f->res[i].node);
+        orc_flow_res_free_ext(&f->res[i]);
     }
     free(f->res);
     free(f);
@@ -630,44 +581,34 @@ int orc_flow_load_rules(orc_flow *f, const orc_flow_rule *rules, size_t n) {
 
 orc_node *orc_flow_node(orc_flow *f, uint32_t resource) { return resource < f->n ? f->res[resource].node : NULL; }
 
-/* StatisticSlot.entry (StatisticSlot.java:64-145) around FlowSlot.checkFlow
- * (FlowSlot.java:161-172, FlowRuleChecker.java:44-60; DIRECT + default limitApp
- * selects the ClusterNode, FlowRuleChecker.java:118-166). */
-int orc_flow_entry(orc_flow *f, uint32_t resource, int64_t now, int acquire, int prioritized, int64_t *wait_ms) {
-    int64_t dummy;
-    if (!wait_ms) wait_ms = &dummy;
-    *wait_ms = 0;
-    if (resource >= f->n) return ORC_PASS;
+/* FlowSlot.checkFlow (FlowSlot.java:161-172, FlowRuleChecker.java:44-60; DIRECT +
+ * default limitApp selects the ClusterNode, FlowRuleChecker.java:118-166):
+ * the resource's raters in order; ORC_PASS (with accumulated sleeps),
+ * ORC_BLOCK_FLOW or ORC_PASS_WAIT (PriorityWaitException). No statistics. */
+int orc_flow_rule_check(orc_flow *f, uint32_t resource, int64_t now, int acquire, int prioritized, int64_t *wait_ms) {
     flow_res *fr = &f->res[resource];
     int64_t total_wait = 0;
+    *wait_ms = 0;
     for (int k = 0; k < fr->nctrl; k++) {
         int64_t w = 0;
         int d = orc_ctrl_can_pass(fr->ctrl[k], fr->node, now, acquire, prioritized, &w);
-        if (d == ORC_BLOCK_FLOW) { /* FlowException -> StatisticSlot catch(BlockException) */
-            orc_node_increase_block_qps(fr->node, now, acquire);
-            *wait_ms = 0;
-            return ORC_BLOCK_FLOW;
-        }
-        if (d == ORC_PASS_WAIT) { /* PriorityWaitException: thread++ only, no pass add */
-            orc_node_increase_thread_num(fr->node);
+        if (d == ORC_BLOCK_FLOW) return ORC_BLOCK_FLOW;
+        if (d == ORC_PASS_WAIT) {
             *wait_ms = w;
             return ORC_PASS_WAIT;
         }
         total_wait += w;
     }
-    orc_node_increase_thread_num(fr->node);
-    orc_node_add_pass_request(fr->node, now, acquire);
     *wait_ms = total_wait;
     return ORC_PASS;
 }
 
-/* StatisticSlot.exit + recordCompleteFor, StatisticSlot.java:147-187 (no blockError) */
+int orc_flow_entry(orc_flow *f, uint32_t resource, int64_t now, int acquire, int prioritized, int64_t *wait_ms) {
+    return orc_flow_entry_p(f, resource, now, acquire, prioritized, 0, 0, wait_ms);
+}
+
 void orc_flow_exit(orc_flow *f, uint32_t resource, int64_t now, int64_t rt, int count, int error) {
-    if (resource >= f->n) return;
-    orc_node *n = f->res[resource].node;
-    orc_node_add_rt_and_success(n, now, rt, count);
-    orc_node_decrease_thread_num(n);
-    if (error) orc_node_increase_exception_qps(n, now, count);
+    orc_flow_exit_p(f, resource, now, rt, count, error, 0, 0);
 }
 
 void orc_flow_replay(orc_flow *f, size_t n, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,

@@ -367,13 +367,20 @@ __global__ __launch_bounds__(kRunThreads) void k_runs_down(const uint32_t *__res
 }
 
 // ---------------------------------------------------------------- exact per-request replay (device)
-// Window state of a rule lives in one contiguous record of 8 fields x S buckets:
-// field 0 = window start (kAbsent = null slot), fields 1..7 = ClusterFlowEvent sums.
+// Window state of a rule lives in one contiguous record of 8 x S int64:
+//   [start x S][PASS x S][WAITING x S][per bucket j: BLOCK, PASS_REQUEST, BLOCK_REQUEST,
+//   OCCUPIED_PASS, OCCUPIED_BLOCK]
+// so the window sums read 3 dense vectors and a run's update writes the current bucket's
+// PASS, WAITING and one 40-byte group.
 struct Rec {
     int64_t *r;
     int S;
     __device__ __forceinline__ int64_t &start(int j) const { return r[j]; }
-    __device__ __forceinline__ int64_t &cnt(int ev, int j) const { return r[(1 + ev) * S + j]; }
+    __device__ __forceinline__ int64_t &cnt(int ev, int j) const {
+        if (ev == CEV_PASS) return r[S + j];
+        if (ev == CEV_WAITING) return r[2 * S + j];
+        return r[3 * S + 5 * j + (ev - 1)];  // BLOCK..OCCUPIED_BLOCK = ordinals 1..5
+    }
 };
 
 __device__ __forceinline__ Rec rec_of(const ClusterState &st, const SlotParam &P) {
@@ -489,11 +496,28 @@ __device__ __forceinline__ bool pass_cond(double thr, double isec, int64_t sum, 
     return thr - (double)sum / isec - (double)a >= 0;
 }
 
+// One 16-lane group per rule; lanes load the record's start/PASS/WAITING vectors
+// in parallel, lane 0 of the group resolves the runs.
+constexpr int kGroup = 16;
+
+__device__ __forceinline__ int64_t group_sum(int64_t v) {
+#pragma unroll
+    for (int o = kGroup / 2; o > 0; o >>= 1) {
+        const int lo = __shfl_xor((int)(uint32_t)v, o, kGroup);
+        const int hi = __shfl_xor((int)(uint32_t)((uint64_t)v >> 32), o, kGroup);
+        v += (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+    }
+    return v;
+}
+
 __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratch sc, const Payload *__restrict__ pay,
                                                     int64_t ts_base, int simple, uint64_t *__restrict__ out) {
     const uint32_t nflows = sc.counters[2];
     const uint32_t nruns = sc.counters[1];
-    for (uint32_t fl = blockIdx.x * kThreads + threadIdx.x; fl < nflows; fl += gridDim.x * kThreads) {
+    const int gl = threadIdx.x & (kGroup - 1);
+    const uint32_t groups_per_block = kThreads / kGroup;
+    const uint32_t stride = gridDim.x * groups_per_block;
+    for (uint32_t fl = blockIdx.x * groups_per_block + threadIdx.x / kGroup; fl < nflows; fl += stride) {
         const uint32_t r0 = sc.flow_first_run[fl];
         const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
         for (uint32_t r = r0; r < r1; ++r) {
@@ -514,31 +538,37 @@ __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratc
             bool fast = (a == sc.run_amax[r]) && !(old != kAbsent && ws < old);
             if (cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) fast = false;
             if (!fast) {
-                // exact replay of every request of the run, in order
-                for (uint32_t j = j0; j < j1; ++j) {
-                    const Payload q = pay[j];
-                    const int64_t t = ts_base + (int64_t)q.ts_off;
-                    out[q.idx] = request_exact(st, s, t, (int32_t)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
-                                               simple);
+                if (gl == 0) {  // exact replay of every request of the run, in order
+                    for (uint32_t j = j0; j < j1; ++j) {
+                        const Payload q = pay[j];
+                        const int64_t t = ts_base + (int64_t)q.ts_off;
+                        out[q.idx] = request_exact(st, s, t, (int32_t)(q.acq_prio & 0x7FFFFFFFu),
+                                                   (q.acq_prio >> 31) != 0, simple);
+                    }
+                    sc.run_mode[r] = RUN_DONE;
+                    __threadfence_block();
                 }
-                sc.run_mode[r] = RUN_DONE;
                 continue;
             }
-            // ---- rotate the current window once (LeapArray.currentWindow(t0))
-            cur_window(st, P, s, t0);
-            int64_t base_pass = 0, base_wait = 0;
-            for (int jj = 0; jj < P.S; ++jj) {
-                if (jj == cj) continue;
+            // ---- window sums over the valid buckets other than the current one (rotation of the
+            //      current bucket does not touch them); lanes split the buckets
+            int64_t bp = 0, bw = 0;
+            for (int jj = gl; jj < P.S; jj += kGroup) {
                 const int64_t w = R.start(jj);
-                if (w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
-                    base_pass += R.cnt(CEV_PASS, jj);
-                    base_wait += R.cnt(CEV_WAITING, jj);
+                if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
+                    bp += R.cnt(CEV_PASS, jj);
+                    bw += R.cnt(CEV_WAITING, jj);
                 }
             }
+            const int64_t base_pass = group_sum(bp);
+            const int64_t base_wait = group_sum(bw);
+            if (gl != 0) continue;
+            // ---- lane 0: rotate the current window (LeapArray.currentWindow(t0)), then resolve
+            cur_window(st, P, s, t0);
             const int64_t head = head_pass(st, P, t0);
             const int64_t s0 = base_pass + R.cnt(CEV_PASS, cj);
             const int64_t w0 = base_wait + R.cnt(CEV_WAITING, cj);
-            // ---- pass prefix: first i with !cond(s0 + i*a, a)   (monotone in i)
+            // pass prefix: first i with !cond(s0 + i*a, a)   (monotone in i)
             uint32_t lo = 0, hi = n;
             while (lo < hi) {
                 const uint32_t mid = lo + ((hi - lo) >> 1);
@@ -548,7 +578,7 @@ __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratc
             const uint32_t f = lo;
             const uint32_t cpf = (f >= n) ? cp_tot : (cp_tot ? sc.ev_cp[j0 + f] : 0u);
             const uint32_t np_after = cp_tot - cpf;
-            // ---- occupied prefix among prioritized blocked requests (monotone in count)
+            // occupied prefix among prioritized blocked requests (monotone in the count)
             uint32_t cw = 0;
             if (np_after > 0) {
                 const double latest = (double)(s0 + (int64_t)f * a) / P.isec;
@@ -565,11 +595,10 @@ __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratc
                 }
                 cw = l2;
             }
-            // ---- counters of the current bucket
-            const int64_t fa = (int64_t)f * a;
+            // counters of the current bucket
             const int64_t wa = (int64_t)cw * a;
             const uint32_t nblk = n - f - cw;
-            R.cnt(CEV_PASS, cj) += fa;
+            R.cnt(CEV_PASS, cj) += (int64_t)f * a;
             R.cnt(CEV_PASS_REQUEST, cj) += f;
             R.cnt(CEV_OCCUPIED_PASS, cj) += (int64_t)cpf * a;
             R.cnt(CEV_WAITING, cj) += wa;
@@ -586,7 +615,11 @@ __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratc
             sc.run_f[r] = f;
             sc.run_cpf[r] = cpf;
             sc.run_cw[r] = cw;
+            sc.run_thr[r] = thr;
+            sc.run_isec[r] = P.isec;
+            sc.run_wait[r] = 1000 / P.S;
             sc.run_mode[r] = RUN_FAST;
+            __threadfence_block();  // the group's lanes re-read this record for the rule's next run
         }
     }
 }
@@ -606,12 +639,10 @@ __global__ __launch_bounds__(kThreads) void k_results(ClusterState st, BatchScra
     const int32_t a = (int32_t)(q.acq_prio & 0x7FFFFFFFu);
     uint64_t res;
     if (local < f) {
-        const SlotParam &P = st.param[keys[j]];
-        const double thr = simple ? P.thr_simple : P.thr;
         const int64_t sum = sc.run_s0[r] + (int64_t)local * a;
-        res = pack_result(TRS_OK, j_d2i(thr - (double)sum / P.isec - (double)a), 0);
+        res = pack_result(TRS_OK, j_d2i(sc.run_thr[r] - (double)sum / sc.run_isec[r] - (double)a), 0);
     } else if ((q.acq_prio >> 31) && sc.ev_cp[j] - sc.run_cpf[r] < sc.run_cw[r]) {
-        res = pack_result(TRS_SHOULD_WAIT, 0, 1000 / st.param[keys[j]].S);
+        res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)sc.run_wait[r]);
     } else {
         res = pack_result(TRS_BLOCKED, 0, 0);
     }
@@ -659,7 +690,8 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += 2 * align_up(cap * 4);                 // ev_run, ev_cp
     b += 8 * align_up(cap * 4);                 // run_* u32/i32
     b += align_up(cap * 8);                     // run_s0
-    b += 3 * align_up(cap * 4);                 // run_f, run_cpf, run_cw
+    b += 4 * align_up(cap * 4);                 // run_f, run_cpf, run_cw, run_wait
+    b += 2 * align_up(cap * 8);                 // run_thr, run_isec
     b += align_up(cap);                         // run_mode
     b += align_up(cap * 4);                     // flow_first_run
     b += 2 * align_up(ntiles * sizeof(Agg)) + align_up(ntiles * 4);
@@ -695,6 +727,9 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.run_f = (uint32_t *)take(cap * 4);
     sc.run_cpf = (uint32_t *)take(cap * 4);
     sc.run_cw = (uint32_t *)take(cap * 4);
+    sc.run_wait = (uint32_t *)take(cap * 4);
+    sc.run_thr = (double *)take(cap * 8);
+    sc.run_isec = (double *)take(cap * 8);
     sc.run_mode = (uint8_t *)take(cap);
     sc.flow_first_run = (uint32_t *)take(cap * 4);
     sc.tile_agg = take(ntiles * sizeof(Agg));
@@ -729,8 +764,8 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
                        ntiles, (Agg *)sc.tile_carry, sc.counters);
     hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, keys, pay, invalid_key,
                        (const Agg *)sc.tile_carry, sc);
-    uint32_t flow_threads = n < st.nslots ? n : st.nslots;
-    uint32_t fb = (flow_threads + kThreads - 1) / kThreads;
+    const uint64_t max_flows = n < st.nslots ? n : st.nslots;
+    uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows * kGroup + kThreads - 1) / kThreads, 16384);
     if (fb == 0) fb = 1;
     hipLaunchKernelGGL(k_flows, dim3(fb), dim3(kThreads), 0, s, st, sc, pay, ts_base, simple, out);
     hipLaunchKernelGGL(k_results, dim3(nb), dim3(kThreads), 0, s, st, sc, keys, pay, simple, out);

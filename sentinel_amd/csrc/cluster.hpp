@@ -59,7 +59,8 @@ struct BatchScratch {
     uint32_t *run_start, *run_end, *run_slot, *run_t0off, *run_cp;
     int32_t *run_amin, *run_amax;
     int64_t *run_s0;
-    uint32_t *run_f, *run_cpf, *run_cw;
+    uint32_t *run_f, *run_cpf, *run_cw, *run_wait;
+    double *run_thr, *run_isec;
     uint8_t *run_mode;
     uint32_t *flow_first_run;
     // tile scan

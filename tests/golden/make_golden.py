@@ -300,6 +300,80 @@ scenario("DefaultTokenService request validation",
           {"op": "cl_request", "id": "s", "flow_id": 98765, "acquire": 1, "prio": False, "expect_status": "OK",
            "expect_remaining": 4}], bases=BASES[:1])
 
+# ------------------------------------------------------------ param flow
+def _prule(**kw):
+    r = {"grade": 1, "count": 5, "control_behavior": 0, "max_queueing_time_ms": 0, "burst_count": 0,
+         "param_idx": 0, "duration_in_sec": 1}
+    r.update(kw)
+    return r
+
+
+def _pp(expect, n=1):
+    return [{"op": "prule_pass", "id": "p", "value": 0x76616C756541, "acquire": 1, "expect": expect}] * n
+
+
+_ops = [{"op": "set_time", "t": 0}, {"op": "prule_new", "id": "p", "rule": _prule(count=25000)}]
+_ops += _pp(True, 2) + [{"op": "sleep", "ms": 1000 * 60 * 60 * 24}] + _pp(True, 2) + \
+    [{"op": "sleep", "ms": 1000 * 60 * 60 * 48}] + _pp(True, 2)
+scenario("ParamFlowDefaultCheckerTest.testCheckQpsWithLongIntervalAndHighThreshold",
+         PFT + "/slots/block/flow/param/ParamFlowDefaultCheckerTest.java:46-82", _ops)
+
+_ops = [{"op": "set_time", "t": 0}, {"op": "prule_new", "id": "p", "rule": _prule(count=5)}]
+_ops += _pp(True, 5) + _pp(False) + [{"op": "sleep", "ms": 3000}] + _pp(True, 5) + _pp(False)
+scenario("ParamFlowDefaultCheckerTest.testParamFlowDefaultCheckSingleQps",
+         PFT + "/slots/block/flow/param/ParamFlowDefaultCheckerTest.java:84-116", _ops)
+
+_ops = [{"op": "set_time", "t": 0}, {"op": "prule_new", "id": "p", "rule": _prule(count=5, burst_count=3)}]
+_ops += _pp(True, 8) + _pp(False) + [{"op": "sleep", "ms": 1002}] + _pp(True, 5) + _pp(False) + \
+    [{"op": "sleep", "ms": 1002}] + _pp(True, 5) + _pp(False) + [{"op": "sleep", "ms": 2000}] + _pp(True, 8) + \
+    _pp(False) + [{"op": "sleep", "ms": 1002}] + _pp(True, 5) + _pp(False)
+scenario("ParamFlowDefaultCheckerTest.testParamFlowDefaultCheckSingleQpsWithBurst",
+         PFT + "/slots/block/flow/param/ParamFlowDefaultCheckerTest.java:118-171", _ops)
+
+_ops = [{"op": "set_time", "t": 0}, {"op": "prule_new", "id": "p", "rule": _prule(count=5, duration_in_sec=60)}]
+_ops += _pp(True, 5) + _pp(False) + [{"op": "sleep", "ms": 1000}] + _pp(False) + [{"op": "sleep", "ms": 10000}] + \
+    _pp(False) + [{"op": "sleep", "ms": 30000}] + _pp(False) + [{"op": "sleep", "ms": 30000}] + _pp(True, 5) + \
+    _pp(False)
+scenario("ParamFlowDefaultCheckerTest.testParamFlowDefaultCheckQpsInDifferentDuration",
+         PFT + "/slots/block/flow/param/ParamFlowDefaultCheckerTest.java:173-213", _ops)
+
+# --------------------------------------------------------- circuit breakers
+def _deg(**kw):
+    r = {"resource": 0, "grade": 0, "count": 0, "time_window": 1, "min_request_amount": 5,
+         "slow_ratio_threshold": 1.0, "stat_interval_ms": 1000}
+    r.update(kw)
+    return r
+
+
+def _es(ms, expect):  # AbstractTimeBasedTest.entryAndSleepFor
+    return {"op": "flow_entry_sleep", "id": "f", "resource": 0, "ms": ms, "expect": expect}
+
+
+def _ee(expect, ms=7):  # entryWithErrorIfPresent(res, exception): sleep 5..10 ms (fixed 7 here)
+    return {"op": "flow_entry_error", "id": "f", "resource": 0, "ms": ms, "expect": expect}
+
+
+_ops = [{"op": "set_time", "t": 0}, {"op": "flow_new", "id": "f", "n_resources": 1},
+        {"op": "flow_load_degrade", "id": "f", "rules": [_deg(grade=1, count=0.2, stat_interval_ms=20000,
+                                                              time_window=10, min_request_amount=1)]},
+        _es(10, True), _ee(True), _ee(False), _es(100, False), {"op": "sleep", "ms": 5000}, _es(100, False),
+        {"op": "sleep", "ms": 5000}, _ee(True), _es(100, False), _es(100, False), {"op": "sleep", "ms": 10000}]
+_ops += [_es(100, True)] * 7 + [_ee(True), _es(100, True)]
+scenario("ExceptionCircuitBreakerTest.testRecordErrorOrSuccess",
+         CORET_DEG + "/ExceptionCircuitBreakerTest.java:50-83", _ops)
+
+_ops = [{"op": "set_time", "t": 0}, {"op": "flow_new", "id": "f", "n_resources": 1},
+        {"op": "flow_load_degrade", "id": "f", "rules": [_deg(grade=0, count=10, min_request_amount=3,
+                                                              slow_ratio_threshold=1, stat_interval_ms=5000,
+                                                              time_window=5)]},
+        _es(20, True), _es(20, True), _es(20, True), _es(20, False), {"op": "sleep", "ms": 1000}, _es(20, False),
+        {"op": "sleep", "ms": 4000}, _es(20, True)]
+# the reference test implicitly assumes its first 60 ms do not straddle a 5 s stat-bucket boundary
+# (statIntervalMs 5000, one bucket): bases with t % 5000 > 4940 would roll the bucket between the
+# three slow exits in the reference too, so only non-straddling bases are used.
+scenario("ResponseTimeCircuitBreakerTest.testMaxSlowRatioThreshold",
+         CORET_DEG + "/ResponseTimeCircuitBreakerTest.java:33-55", _ops, bases=BASES[:4])
+
 
 def main():
     for sc in SCENARIOS:

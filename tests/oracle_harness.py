@@ -35,6 +35,19 @@ class OrcClusterRule(C.Structure):
                 ("strategy", C.c_int32)]
 
 
+class OrcParamRule(C.Structure):
+    _fields_ = [("resource", C.c_uint32), ("grade", C.c_int32), ("count", C.c_double),
+                ("control_behavior", C.c_int32), ("max_queueing_time_ms", C.c_int32), ("burst_count", C.c_int32),
+                ("param_idx", C.c_int32), ("duration_in_sec", C.c_int64), ("n_hot", C.c_uint32),
+                ("hot_values", C.POINTER(C.c_uint64)), ("hot_thresholds", C.POINTER(C.c_int32))]
+
+
+class OrcDegradeRule(C.Structure):
+    _fields_ = [("resource", C.c_uint32), ("grade", C.c_int32), ("count", C.c_double), ("time_window", C.c_int32),
+                ("min_request_amount", C.c_int32), ("slow_ratio_threshold", C.c_double),
+                ("stat_interval_ms", C.c_int32)]
+
+
 class OrcTokenResult(C.Structure):
     _fields_ = [("status", C.c_int32), ("remaining", C.c_int32), ("wait_in_ms", C.c_int32)]
 
@@ -103,6 +116,15 @@ def lib():
         "orc_limiter_qps": (D, [P, I64]),
         "orc_limiter_can_pass": (C.c_int, [P, I64]),
         "orc_limiter_try_pass": (C.c_int, [P, I64]),
+        "orc_flow_load_param_rules": (C.c_int, [P, C.POINTER(OrcParamRule), C.c_size_t]),
+        "orc_flow_load_degrade_rules": (C.c_int, [P, C.POINTER(OrcDegradeRule), C.c_size_t]),
+        "orc_flow_entry_p": (C.c_int, [P, U32, I64, C.c_int, C.c_int, C.c_int, C.c_uint64, C.POINTER(I64)]),
+        "orc_flow_exit_p": (None, [P, U32, I64, I64, C.c_int, C.c_int, C.c_int, C.c_uint64]),
+        "orc_flow_cb_state": (C.c_int, [P, U32, C.c_int]),
+        "orc_flow_replay_p": (None, [P, C.c_size_t, P, P, P, P, P, P, P, P, P]),
+        "orc_prule_new": (P, [C.POINTER(OrcParamRule)]),
+        "orc_prule_free": (None, [P]),
+        "orc_prule_pass_single": (C.c_int, [P, C.c_uint64, C.c_int, I64, I64, C.POINTER(I64)]),
         "orc_java_round": (I64, [D]),
         "orc_java_next_up": (D, [D]),
         "orc_java_d2i": (I32, [D]),
@@ -140,6 +162,47 @@ def cluster_rules_array(rules):
         arr[i].window_interval_ms = r.get("window_interval_ms", 1000)
         arr[i].grade = r.get("grade", 1)
         arr[i].strategy = r.get("strategy", 0)
+    return arr
+
+
+def param_rule_struct(r, keep):
+    x = OrcParamRule()
+    x.resource = r.get("resource", 0)
+    x.grade = r.get("grade", 1)
+    x.count = r["count"]
+    x.control_behavior = r.get("control_behavior", 0)
+    x.max_queueing_time_ms = r.get("max_queueing_time_ms", 0)
+    x.burst_count = r.get("burst_count", 0)
+    x.param_idx = r.get("param_idx", 0)
+    x.duration_in_sec = r.get("duration_in_sec", 1)
+    hot = r.get("hot", {})
+    x.n_hot = len(hot)
+    if hot:
+        hv = (C.c_uint64 * len(hot))(*[int(k) for k in hot])
+        ht = (C.c_int32 * len(hot))(*[int(v) for v in hot.values()])
+        keep += [hv, ht]
+        x.hot_values = hv
+        x.hot_thresholds = ht
+    return x
+
+
+def param_rules_array(rules, keep):
+    arr = (OrcParamRule * max(1, len(rules)))()
+    for i, r in enumerate(rules):
+        arr[i] = param_rule_struct(r, keep)
+    return arr
+
+
+def degrade_rules_array(rules):
+    arr = (OrcDegradeRule * max(1, len(rules)))()
+    for i, r in enumerate(rules):
+        arr[i].resource = r.get("resource", 0)
+        arr[i].grade = r.get("grade", 0)
+        arr[i].count = r["count"]
+        arr[i].time_window = r.get("time_window", 1)
+        arr[i].min_request_amount = r.get("min_request_amount", 5)
+        arr[i].slow_ratio_threshold = r.get("slow_ratio_threshold", 1.0)
+        arr[i].stat_interval_ms = r.get("stat_interval_ms", 1000)
     return arr
 
 
@@ -318,10 +381,31 @@ def run_scenario(sc, base):
                     check(r.wait_in_ms == op["expect_wait"], op, r.wait_in_ms)
                 if "expect_remaining" in op:
                     check(r.remaining == op["expect_remaining"], op, r.remaining)
+            elif k == "prule_new":
+                keep = []
+                h = L.orc_prule_new(C.byref(param_rule_struct(op["rule"], keep)))
+                objs[op["id"]] = h
+                frees.append((L.orc_prule_free, h))
+            elif k == "prule_pass":
+                w = C.c_int64()
+                got = bool(L.orc_prule_pass_single(objs[op["id"]], op["value"], op["acquire"], now,
+                                                   op.get("threads", 0), C.byref(w)))
+                check(got == op["expect"], op, got)
+            elif k == "flow_load_degrade":
+                arr = degrade_rules_array(op["rules"])
+                L.orc_flow_load_degrade_rules(objs[op["id"]], arr, len(op["rules"]))
+            elif k in ("flow_entry_sleep", "flow_entry_error"):
+                w = C.c_int64()
+                d = L.orc_flow_entry_p(objs[op["id"]], op["resource"], now, 1, 0, 0, 0, C.byref(w))
+                passed = d in (0, 4)
+                if passed:
+                    t_in = now
+                    now += op["ms"]
+                    L.orc_flow_exit_p(objs[op["id"]], op["resource"], now, now - t_in, 1,
+                                      1 if k == "flow_entry_error" else 0, 0, 0)
+                check(passed == op["expect"], op, d)
             else:
-                # ops handled by extension oracles (param flow / degrade) live in their own harnesses
-                from tests import oracle_harness_ext  # noqa: F401
-                oracle_harness_ext.run_op(L, sc, base, op, objs, frees, now, check)
+                raise ScenarioFailure(f"unknown op {k}")
     finally:
         for fn, h in reversed(frees):
             fn(h)
