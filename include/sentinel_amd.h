@@ -17,8 +17,18 @@
  *   sga_set_connected_count   <- ConnectionManager.getConnectedCount (AVG_LOCAL thresholds)
  *                                CS/flow/rule/ClusterFlowRuleManager.java:333-343
  *   sga_cluster_metric_sums   <- ClusterMetric.getSum(ClusterFlowEvent)  CS/flow/statistic/metric/ClusterMetric.java:53-62
- *   sga_rls_check_descriptors <- SentinelEnvoyRlsServiceImpl.checkToken -> SimpleClusterFlowChecker
- *                                RLS/SentinelEnvoyRlsServiceImpl.java:116-125, RLS/flow/SimpleClusterFlowChecker.java:33-65
+ *   sga_rls_should_rate_limit <- SentinelEnvoyRlsServiceImpl.shouldRateLimit -> SimpleClusterFlowChecker
+ *                                RLS/SentinelEnvoyRlsServiceImpl.java:51-134, RLS/flow/SimpleClusterFlowChecker.java:33-65
+ *   sga_submit_events         <- SphU.entry(String, EntryType, int, Object...) / Entry.exit(int, Object...)
+ *                                CORE/SphU.java:84-208, CORE/Entry.java:86-111 through the slot chain
+ *                                StatisticSlot (CORE/slots/statistic/StatisticSlot.java:64-187) ->
+ *                                ParamFlowSlot (PF/slots/block/flow/param/ParamFlowSlot.java:34-93) ->
+ *                                FlowSlot (CORE/slots/block/flow/FlowSlot.java:161-189) ->
+ *                                DegradeSlot (CORE/slots/block/degrade/DegradeSlot.java:41-89)
+ *   sga_load_flow_rules       <- FlowRuleManager.loadRules(List<FlowRule>)  CORE/slots/block/flow/FlowRuleManager.java:125-127
+ *   sga_load_param_rules      <- ParamFlowRuleManager.loadRules(List<ParamFlowRule>)  PF/slots/block/flow/param/ParamFlowRuleManager.java:52
+ *   sga_load_degrade_rules    <- DegradeRuleManager.loadRules(List<DegradeRule>)  CORE/slots/block/degrade/DegradeRuleManager.java:108
+ *   sga_query_node            <- Node views (ClusterNode) CORE/node/Node.java:40-203, StatisticNode.java:185-250
  */
 #ifndef SENTINEL_AMD_H
 #define SENTINEL_AMD_H
@@ -138,6 +148,89 @@ int sga_cluster_stats(sga_engine *e, uint64_t *n_active_rules, uint64_t *state_b
 int sga_rls_should_rate_limit(sga_engine *e, const uint32_t *desc_offsets, size_t n_requests,
                               const int64_t *desc_flow_id, const int32_t *hits_addend, const int64_t *ts,
                               int8_t *desc_status, int32_t *code);
+
+/* ---------------------------------------------------------------------------
+ * Local path: resources are dense ids 0..n_resources-1 (the host keeps the
+ * name table, like CtSph's chain map keys).  One ClusterNode per resource
+ * (single default context, limitApp "default", strategy DIRECT).
+ * ------------------------------------------------------------------------- */
+
+/* decision codes of sga_submit_events */
+#define SGA_PASS 0
+#define SGA_BLOCK_FLOW 1     /* FlowException */
+#define SGA_BLOCK_PARAM 2    /* ParamFlowException */
+#define SGA_BLOCK_DEGRADE 3  /* DegradeException */
+#define SGA_PASS_WAIT 4      /* PriorityWaitException: passed after wait_ms, not counted as pass */
+
+/* event flags */
+#define SGA_EV_PRIORITIZED 1u
+#define SGA_EV_ERROR 2u      /* exit of an entry that recorded a business error (Tracer.traceEntry) */
+#define SGA_EV_HAS_PARAM 4u  /* args[0] present (param field) */
+
+/* FlowRule, CORE/slots/block/flow/FlowRule.java:52-95 (limitApp default, strategy DIRECT) */
+typedef struct sga_flow_rule {
+    uint32_t resource;
+    int32_t grade;                 /* FLOW_GRADE_THREAD 0 / QPS 1 */
+    double count;
+    int32_t control_behavior;      /* 0 default, 1 warm up, 2 rate limiter, 3 warm up + rate limiter */
+    int32_t warm_up_period_sec;    /* default 10 */
+    int32_t max_queueing_time_ms;  /* default 500 */
+    int32_t strategy;              /* STRATEGY_DIRECT 0 only */
+} sga_flow_rule;
+
+/* ParamFlowRule, PF/slots/block/flow/param/ParamFlowRule.java:45-83 */
+typedef struct sga_param_rule {
+    uint32_t resource;
+    int32_t grade;                 /* QPS 1 / THREAD 0 */
+    double count;
+    int32_t control_behavior;      /* 0 token bucket, 2 throttle (RATE_LIMITER) */
+    int32_t max_queueing_time_ms;  /* default 0 */
+    int32_t burst_count;           /* default 0 */
+    int32_t param_idx;             /* 0 (or -1): the event's single parameter */
+    int64_t duration_in_sec;       /* default 1 */
+    uint32_t n_hot;                /* parsed hot items: value -> threshold */
+    uint32_t reserved;
+    const uint64_t *hot_values;
+    const int32_t *hot_thresholds;
+} sga_param_rule;
+
+/* DegradeRule, CORE/slots/block/degrade/DegradeRule.java:59-84 */
+typedef struct sga_degrade_rule {
+    uint32_t resource;
+    int32_t grade;                 /* RT 0, EXCEPTION_RATIO 1, EXCEPTION_COUNT 2 */
+    double count;
+    int32_t time_window;           /* seconds */
+    int32_t min_request_amount;    /* default 5 */
+    double slow_ratio_threshold;   /* default 1.0 */
+    int32_t stat_interval_ms;      /* default 1000 */
+    int32_t reserved;
+} sga_degrade_rule;
+
+/* Node view at virtual time `now` (StatisticNode getters; reads rotate windows like the reference). */
+typedef struct sga_node_view {
+    double pass_qps, block_qps, success_qps, exception_qps, occupied_pass_qps;
+    double avg_rt, min_rt, previous_pass_qps;
+    int64_t total_pass, total_block, total_success, total_exception;  /* minute window */
+    int64_t cur_thread_num;
+    int64_t waiting;                                                /* borrowed (occupied) tokens */
+} sga_node_view;
+
+int sga_flow_set_resources(sga_engine *e, uint32_t n_resources);
+int sga_load_flow_rules(sga_engine *e, const sga_flow_rule *rules, size_t n);
+int sga_load_param_rules(sga_engine *e, const sga_param_rule *rules, size_t n);
+int sga_load_degrade_rules(sga_engine *e, const sga_degrade_rule *rules, size_t n);
+
+/* A time-ordered stream of entries (kind 0) and exits of passed entries (kind 1),
+ * decided as if SphU.entry / Entry.exit were called one by one under a mocked
+ * TimeUtil returning ts[i].  acquire = batchCount; rt[i] = exit - entry time
+ * (exits); param[i] = args[0] when SGA_EV_HAS_PARAM.  decision[i] / wait_ms[i]
+ * for entries (exits report SGA_PASS).  Host buffers, synchronous. */
+int sga_submit_events(sga_engine *e, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
+                      const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
+                      size_t n, int8_t *decision, int32_t *wait_ms);
+int sga_query_node(sga_engine *e, uint32_t resource, int64_t now, sga_node_view *out);
+/* circuit breaker k of a resource: 0 CLOSED, 1 OPEN, 2 HALF_OPEN (negative = no such breaker) */
+int sga_circuit_breaker_state(sga_engine *e, uint32_t resource, uint32_t k);
 
 /* Optional helper for tools: HIP stream of the engine (hipStream_t as void*). */
 void *sga_engine_stream(sga_engine *e);

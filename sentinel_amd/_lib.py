@@ -32,6 +32,28 @@ class SgaFlowRule(C.Structure):
                 ("max_queueing_time_ms", C.c_int32), ("strategy", C.c_int32)]
 
 
+class SgaParamRule(C.Structure):
+    _fields_ = [("resource", C.c_uint32), ("grade", C.c_int32), ("count", C.c_double),
+                ("control_behavior", C.c_int32), ("max_queueing_time_ms", C.c_int32), ("burst_count", C.c_int32),
+                ("param_idx", C.c_int32), ("duration_in_sec", C.c_int64), ("n_hot", C.c_uint32),
+                ("reserved", C.c_uint32), ("hot_values", C.POINTER(C.c_uint64)),
+                ("hot_thresholds", C.POINTER(C.c_int32))]
+
+
+class SgaDegradeRule(C.Structure):
+    _fields_ = [("resource", C.c_uint32), ("grade", C.c_int32), ("count", C.c_double), ("time_window", C.c_int32),
+                ("min_request_amount", C.c_int32), ("slow_ratio_threshold", C.c_double),
+                ("stat_interval_ms", C.c_int32), ("reserved", C.c_int32)]
+
+
+class SgaNodeView(C.Structure):
+    _fields_ = [("pass_qps", C.c_double), ("block_qps", C.c_double), ("success_qps", C.c_double),
+                ("exception_qps", C.c_double), ("occupied_pass_qps", C.c_double), ("avg_rt", C.c_double),
+                ("min_rt", C.c_double), ("previous_pass_qps", C.c_double), ("total_pass", C.c_int64),
+                ("total_block", C.c_int64), ("total_success", C.c_int64), ("total_exception", C.c_int64),
+                ("cur_thread_num", C.c_int64), ("waiting", C.c_int64)]
+
+
 # (restype, argtypes) for every exported symbol; tests check this list against include/*.h
 SIGNATURES = {
     "sga_abi_version": (C.c_int, []),
@@ -51,6 +73,14 @@ SIGNATURES = {
     "sga_cluster_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "sga_rls_should_rate_limit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p, C.c_void_p]),
+    "sga_flow_set_resources": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "sga_load_flow_rules": (C.c_int, [C.c_void_p, C.POINTER(SgaFlowRule), C.c_size_t]),
+    "sga_load_param_rules": (C.c_int, [C.c_void_p, C.POINTER(SgaParamRule), C.c_size_t]),
+    "sga_load_degrade_rules": (C.c_int, [C.c_void_p, C.POINTER(SgaDegradeRule), C.c_size_t]),
+    "sga_submit_events": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
+    "sga_query_node": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int64, C.POINTER(SgaNodeView)]),
+    "sga_circuit_breaker_state": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
 }
 
 _lib = None

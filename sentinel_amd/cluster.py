@@ -10,13 +10,14 @@ Every decision is computed by the HIP engine (libsentinel_amd.so); the mocked
 TimeUtil clock of the reference tests is the explicit `now`/`ts` argument.
 """
 import ctypes as C
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import List, Optional
 
 import numpy as np
 
 from . import _lib
 from ._lib import SgaClusterFlowRule, SgaConfig, SgaTokenResult, check
+from .rules import ClusterFlowConfig, ClusterRuleConstant, FlowRule  # noqa: F401 (re-exported)
 
 
 class TokenResultStatus:
@@ -33,13 +34,6 @@ class TokenResultStatus:
     ALREADY_RELEASE = 7
 
 
-class ClusterRuleConstant:
-    FLOW_CLUSTER_STRATEGY_NORMAL = 0
-    FLOW_THRESHOLD_AVG_LOCAL = 0
-    FLOW_THRESHOLD_GLOBAL = 1
-    DEFAULT_CLUSTER_SAMPLE_COUNT = 10
-
-
 class ClusterFlowEvent:
     PASS, BLOCK, PASS_REQUEST, BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK, WAITING = range(7)
 
@@ -49,24 +43,6 @@ class TokenResult:
     status: int
     remaining: int = 0
     wait_in_ms: int = 0
-
-
-@dataclass
-class ClusterFlowConfig:
-    flow_id: Optional[int] = None
-    threshold_type: int = ClusterRuleConstant.FLOW_THRESHOLD_AVG_LOCAL
-    sample_count: int = ClusterRuleConstant.DEFAULT_CLUSTER_SAMPLE_COUNT
-    window_interval_ms: int = 1000
-    strategy: int = ClusterRuleConstant.FLOW_CLUSTER_STRATEGY_NORMAL
-
-
-@dataclass
-class FlowRule:
-    resource: str = ""
-    count: float = 0.0
-    grade: int = 1  # RuleConstant.FLOW_GRADE_QPS
-    cluster_mode: bool = False
-    cluster_config: ClusterFlowConfig = field(default_factory=ClusterFlowConfig)
 
 
 class Engine:

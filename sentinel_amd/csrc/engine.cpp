@@ -515,4 +515,61 @@ int sga_rls_should_rate_limit(sga_engine *e, const uint32_t *desc_offsets, size_
     });
 }
 
+// ---------------------------------------------------------------- local path
+int sga_flow_set_resources(sga_engine *e, uint32_t n_resources) {
+    if (n_resources == 0 || n_resources >= (1u << 30)) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        return g.flow.set_resources(n_resources);
+    });
+}
+
+int sga_load_flow_rules(sga_engine *e, const sga_flow_rule *rules, size_t n) {
+    if (n && !rules) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        return g.flow.load_flow_rules(rules, n);
+    });
+}
+
+int sga_load_param_rules(sga_engine *e, const sga_param_rule *rules, size_t n) {
+    if (n && !rules) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        return g.flow.load_param_rules(rules, n);
+    });
+}
+
+int sga_load_degrade_rules(sga_engine *e, const sga_degrade_rule *rules, size_t n) {
+    if (n && !rules) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        return g.flow.load_degrade_rules(rules, n);
+    });
+}
+
+int sga_submit_events(sga_engine *e, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
+                      const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
+                      size_t n, int8_t *decision, int32_t *wait_ms) {
+    if (n && (!kind || !resource || !ts || !acquire || !decision)) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        return g.flow.submit(kind, resource, ts, acquire, flags, rt, param, n, decision, wait_ms);
+    });
+}
+
+int sga_query_node(sga_engine *e, uint32_t resource, int64_t now, sga_node_view *out) {
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        return g.flow.query(resource, now, out);
+    });
+}
+
+int sga_circuit_breaker_state(sga_engine *e, uint32_t resource, uint32_t k) {
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        return g.flow.cb_state(resource, k);
+    });
+}
+
 }  // extern "C"

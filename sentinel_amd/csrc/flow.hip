@@ -1,0 +1,1419 @@
+// Local path on gfx950: StatisticSlot + ParamFlowSlot + FlowSlot + DegradeSlot over batches of
+// entry/exit events (kernels K1-K5, K8 of DESIGN.md).
+//
+// Semantics restated from the reference (aliases as in SURVEY.md):
+//   StatisticNode / ArrayMetric / Occupiable+Future+BucketLeapArray  CORE/node/StatisticNode.java:99-350,
+//       CORE/slots/statistic/metric/ArrayMetric.java:37-350, .../occupy/OccupiableBucketLeapArray.java:33-82
+//   StatisticSlot.entry/exit  CORE/slots/statistic/StatisticSlot.java:64-187
+//   DefaultController / RateLimiterController / WarmUpController / WarmUpRateLimiterController
+//       CORE/slots/block/flow/controller/*.java
+//   ParamFlowChecker / ParameterMetric  PF/slots/block/flow/param/ParamFlowChecker.java:48-281, ParameterMetric.java
+//   Exception/ResponseTimeCircuitBreaker + DegradeSlot  CORE/slots/block/degrade/**
+//
+// Batch algorithm: events are sorted by resource (stable: arrival order kept per resource) and
+// segmented into runs = (resource, 500 ms second-window bucket).  One lane per resource walks its
+// runs in time order.  A run of a resource whose only rule is a QPS DefaultController or
+// WarmUpController, without prioritized entries and with equal acquire counts, is resolved in
+// closed form: the window sums after one rotation, the pass prefix by binary search over the exact
+// Java predicate, all exits of the run applied as one segmented reduction.  Every other run is
+// replayed event by event with a device restatement of the whole slot chain.
+#include "flow.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace sga {
+
+namespace {
+
+constexpr int kT = 256;
+constexpr int kItems = 16;
+constexpr int kTileElems = kT * kItems;  // 4096
+constexpr int kSecW = 500, kSecInterval = 1000;   // SampleCountProperty.SAMPLE_COUNT = 2, INTERVAL = 1000
+constexpr int kMinW = 1000, kMinInterval = 60000;
+constexpr int kOccupyTimeout = 500;               // OccupyTimeoutProperty
+enum : int8_t { D_PASS = 0, D_BLOCK_FLOW = 1, D_BLOCK_PARAM = 2, D_BLOCK_DEGRADE = 3, D_PASS_WAIT = 4 };
+enum : uint32_t { F_EXIT = 1u << 30, F_ERROR = 1u << 29, F_PARAM = 1u << 28, F_IDX = (1u << 28) - 1 };
+enum : uint8_t { RUN_FAST = 0, RUN_DONE = 1 };
+
+struct Ctx {
+    FlowState st;
+    int64_t max_rt;  // csp.sentinel.statistic.max.rt
+};
+
+// ------------------------------------------------------------------ MetricBucket windows
+__device__ __forceinline__ void mb_zero(int64_t *b, int64_t max_rt) {
+#pragma unroll
+    for (int k = 1; k < MB_MINRT; ++k) b[k] = 0;
+    b[MB_MINRT] = max_rt;
+}
+
+// FutureBucketLeapArray (borrow) getWindowValue(t): bucket whose [start, start+500) contains t
+__device__ __forceinline__ int64_t *bor_value(int64_t *node, int64_t t) {
+    if (t < 0) return nullptr;
+    int64_t *b = node + kNodeBor + 2 * (int)((t / kSecW) % 2);
+    if (b[0] == kAbsent || !(b[0] <= t && t < b[0] + kSecW)) return nullptr;
+    return b;
+}
+
+// LeapArray.currentWindow(t) on the borrow array (newEmpty / reset both give an empty bucket)
+__device__ int64_t *bor_current(int64_t *node, int64_t t, bool *detached) {
+    int64_t *b = node + kNodeBor + 2 * (int)((t / kSecW) % 2);
+    const int64_t ws = t - t % kSecW;
+    *detached = false;
+    if (b[0] == kAbsent || ws > b[0]) {
+        b[0] = ws;
+        b[1] = 0;
+        return b;
+    }
+    if (ws == b[0]) return b;
+    *detached = true;
+    return nullptr;
+}
+
+// OccupiableBucketLeapArray.currentWindow(t): new bucket copies the borrowed bucket,
+// a reset bucket takes only its PASS ((int) cast), OccupiableBucketLeapArray.java:40-64
+__device__ int64_t *sec_current(int64_t *node, int64_t t, int64_t max_rt) {
+    int64_t *b = node + kNodeSec + kMB * (int)((t / kSecW) % 2);
+    const int64_t ws = t - t % kSecW;
+    if (b[0] == kAbsent) {
+        mb_zero(b, max_rt);
+        const int64_t *bb = bor_value(node, t);
+        if (bb) b[MB_PASS] = bb[1];  // MetricBucket.reset(borrow): every counter (only PASS is ever borrowed)
+        b[0] = ws;
+        return b;
+    }
+    if (ws == b[0]) return b;
+    if (ws > b[0]) {
+        b[0] = ws;
+        mb_zero(b, max_rt);
+        const int64_t *bb = bor_value(node, ws);
+        if (bb) b[MB_PASS] += (int64_t)(int32_t)bb[1];
+        return b;
+    }
+    return nullptr;  // clock went backwards: detached bucket, adds lost
+}
+
+__device__ int64_t *min_current(int64_t *node, int64_t t, int64_t max_rt) {
+    int64_t *b = node + kNodeMin + kMB * (int)((t / kMinW) % 60);
+    const int64_t ws = t - t % kMinW;
+    if (b[0] == kAbsent || ws > b[0]) {
+        b[0] = ws;
+        mb_zero(b, max_rt);
+        return b;
+    }
+    if (ws == b[0]) return b;
+    return nullptr;
+}
+
+__device__ __forceinline__ int64_t sec_sum(int64_t *node, int64_t t, int f) {
+    int64_t s = 0;
+    for (int j = 0; j < 2; ++j) {
+        const int64_t *b = node + kNodeSec + kMB * j;
+        if (b[0] != kAbsent && !(t - b[0] > kSecInterval)) s += b[f];
+    }
+    return s;
+}
+
+__device__ __forceinline__ int64_t min_sum(int64_t *node, int64_t t, int f) {
+    int64_t s = 0;
+    for (int j = 0; j < 60; ++j) {
+        const int64_t *b = node + kNodeMin + kMB * j;
+        if (b[0] != kAbsent && !(t - b[0] > kMinInterval)) s += b[f];
+    }
+    return s;
+}
+
+// ------------------------------------------------------------------ StatisticNode
+__device__ __forceinline__ double node_pass_qps(const Ctx &c, int64_t *node, int64_t t) {
+    sec_current(node, t, c.max_rt);
+    return (double)sec_sum(node, t, MB_PASS) / 1.0;
+}
+
+// minute.previousWindowPass(): currentWindow(now) then getPreviousWindow(now), LeapArray.java:230-248
+__device__ double node_prev_pass_qps(const Ctx &c, int64_t *node, int64_t t) {
+    min_current(node, t, c.max_rt);
+    const int64_t tp = t - kMinW;
+    if (t < 0) return 0;
+    const int64_t *b = node + kNodeMin + kMB * (int)((tp / kMinW) % 60);
+    if (b[0] == kAbsent || t - b[0] > kMinInterval) return 0;
+    if (b[0] + kMinW < tp) return 0;
+    return (double)b[MB_PASS];
+}
+
+__device__ __forceinline__ void node_add(const Ctx &c, int64_t *node, int64_t t, int f, int64_t n) {
+    int64_t *b = sec_current(node, t, c.max_rt);
+    if (b) b[f] += n;
+    b = min_current(node, t, c.max_rt);
+    if (b) b[f] += n;
+}
+
+__device__ void node_add_rt_success(const Ctx &c, int64_t *node, int64_t t, int64_t rt, int count) {
+    int64_t *b = sec_current(node, t, c.max_rt);
+    if (b) b[MB_SUCC] += count;
+    b = sec_current(node, t, c.max_rt);
+    if (b) {
+        b[MB_RT] += rt;
+        if (rt < b[MB_MINRT]) b[MB_MINRT] = rt;
+    }
+    b = min_current(node, t, c.max_rt);
+    if (b) b[MB_SUCC] += count;
+    b = min_current(node, t, c.max_rt);
+    if (b) {
+        b[MB_RT] += rt;
+        if (rt < b[MB_MINRT]) b[MB_MINRT] = rt;
+    }
+}
+
+__device__ int64_t node_waiting(int64_t *node, int64_t t) {
+    bool det;
+    bor_current(node, t, &det);
+    int64_t s = 0;
+    for (int j = 0; j < 2; ++j) {
+        const int64_t *b = node + kNodeBor + 2 * j;
+        if (b[0] != kAbsent && !(t >= b[0])) s += b[1];  // FutureBucketLeapArray deprecation
+    }
+    return s;
+}
+
+// StatisticNode.tryOccupyNext, StatisticNode.java:302-334
+__device__ int64_t node_try_occupy_next(const Ctx &c, int64_t *node, int64_t t, int acquire, double threshold) {
+    const double max_count = threshold * kSecInterval / 1000;
+    const int64_t current_borrow = node_waiting(node, t);
+    if ((double)current_borrow >= max_count) return kOccupyTimeout;
+    const int window_length = kSecInterval / 2;
+    int64_t earliest = t - t % window_length + window_length - kSecInterval;
+    int idx = 0;
+    sec_current(node, t, c.max_rt);
+    int64_t current_pass = sec_sum(node, t, MB_PASS);
+    while (earliest < t) {
+        const int64_t wait = (int64_t)idx * window_length + window_length - t % window_length;
+        if (wait >= kOccupyTimeout) break;
+        int64_t window_pass = 0;
+        {  // ArrayMetric.getWindowPass(earliest) = data.getWindowValue(earliest)
+            const int64_t *b = node + kNodeSec + kMB * (int)((earliest / kSecW) % 2);
+            if (earliest >= 0 && b[0] != kAbsent && b[0] <= earliest && earliest < b[0] + kSecW) window_pass = b[MB_PASS];
+        }
+        if ((double)(current_pass + current_borrow + acquire - window_pass) <= max_count) return wait;
+        earliest += window_length;
+        current_pass -= window_pass;
+        idx++;
+    }
+    return kOccupyTimeout;
+}
+
+// ------------------------------------------------------------------ controllers
+__device__ void warmup_sync(FlowRuleDev &r, int64_t t, int64_t pass_qps) {  // WarmUpController.java:140-175
+    const int64_t current_time = t - t % 1000;
+    if (current_time <= r.last_filled) return;
+    const int64_t old_value = r.stored_tokens;
+    int64_t new_value = old_value;
+    if (old_value < r.warning_token) {
+        new_value = j_d2l((double)old_value + (double)(current_time - r.last_filled) * r.count / 1000);
+    } else if (old_value > r.warning_token) {
+        if (pass_qps < (int64_t)(j_d2i(r.count) / r.cold_factor))
+            new_value = j_d2l((double)old_value + (double)(current_time - r.last_filled) * r.count / 1000);
+    }
+    if (new_value > (int64_t)r.max_token) new_value = r.max_token;
+    r.stored_tokens = new_value - pass_qps;
+    if (r.stored_tokens < 0) r.stored_tokens = 0;
+    r.last_filled = current_time;
+}
+
+__device__ int8_t pace_tail(FlowRuleDev &r, int64_t t, int64_t cost, int64_t *wait_ms) {
+    const int64_t expected = cost + r.latest_passed;
+    if (expected <= t) {
+        r.latest_passed = t;
+        return D_PASS;
+    }
+    int64_t wait = cost + r.latest_passed - t;
+    if (wait > r.max_queue) return D_BLOCK_FLOW;
+    r.latest_passed += cost;
+    wait = r.latest_passed - t;
+    if (wait > r.max_queue) {
+        r.latest_passed -= cost;
+        return D_BLOCK_FLOW;
+    }
+    *wait_ms = wait > 0 ? wait : 0;
+    return D_PASS;
+}
+
+__device__ int8_t rater_can_pass(const Ctx &c, FlowRuleDev &r, int64_t *node, int64_t t, int acquire, bool prio,
+                                 int64_t *wait_ms) {
+    *wait_ms = 0;
+    switch (r.behavior) {
+    case 2: {  // RateLimiterController.canPass, :46-91
+        if (acquire <= 0) return D_PASS;
+        if (r.count <= 0) return D_BLOCK_FLOW;
+        return pace_tail(r, t, j_round(1.0 * acquire / r.count * 1000), wait_ms);
+    }
+    case 1: {  // WarmUpController.canPass, :113-138
+        const int64_t pass_qps = j_d2l(node_pass_qps(c, node, t));
+        const int64_t previous_qps = j_d2l(node_prev_pass_qps(c, node, t));
+        warmup_sync(r, t, previous_qps);
+        const int64_t rest = r.stored_tokens;
+        if (rest >= r.warning_token) {
+            const int64_t above = rest - r.warning_token;
+            const double warning_qps = j_next_up(1.0 / ((double)above * r.slope + 1.0 / r.count));
+            if ((double)(pass_qps + acquire) <= warning_qps) return D_PASS;
+        } else if ((double)(pass_qps + acquire) <= r.count) {
+            return D_PASS;
+        }
+        return D_BLOCK_FLOW;
+    }
+    case 3: {  // WarmUpRateLimiterController.canPass, :43-87
+        const int64_t previous_qps = j_d2l(node_prev_pass_qps(c, node, t));
+        warmup_sync(r, t, previous_qps);
+        const int64_t rest = r.stored_tokens;
+        int64_t cost;
+        if (rest >= r.warning_token) {
+            const int64_t above = rest - r.warning_token;
+            const double warming_qps = j_next_up(1.0 / ((double)above * r.slope + 1.0 / r.count));
+            cost = j_round(1.0 * acquire / warming_qps * 1000);
+        } else {
+            cost = j_round(1.0 * acquire / r.count * 1000);
+        }
+        return pace_tail(r, t, cost, wait_ms);
+    }
+    default: {  // DefaultController.canPass, DefaultController.java:49-78
+        int32_t cur = r.grade == 0 ? (int32_t)node[kNodeThreads] : j_d2i(node_pass_qps(c, node, t));
+        const int32_t sum = (int32_t)((uint32_t)cur + (uint32_t)acquire);
+        if ((double)sum > r.count) {
+            if (prio && r.grade == 1) {
+                const int64_t wait = node_try_occupy_next(c, node, t, acquire, r.count);
+                if (wait < kOccupyTimeout) {
+                    bool det;
+                    int64_t *bb = bor_current(node, t + wait, &det);  // addWaitingRequest(now + wait)
+                    if (bb) bb[1] += acquire;
+                    int64_t *m = min_current(node, t, c.max_rt);      // addOccupiedPass
+                    if (m) m[MB_OPASS] += acquire;
+                    m = min_current(node, t, c.max_rt);
+                    if (m) m[MB_PASS] += acquire;
+                    *wait_ms = wait;
+                    return D_PASS_WAIT;
+                }
+            }
+            return D_BLOCK_FLOW;
+        }
+        return D_PASS;
+    }
+    }
+}
+
+// ------------------------------------------------------------------ parameter maps
+__device__ PEntry *ptab_get(PEntry *tab, uint32_t mask, uint32_t owner, uint64_t value, bool create,
+                            uint32_t *overflow) {
+    uint32_t h = (uint32_t)splitmix64(value ^ ((uint64_t)owner << 40) ^ 0xA5A5ULL) & mask;
+    for (uint32_t probe = 0; probe <= mask; ++probe) {
+        PEntry *e = &tab[h];
+        uint32_t o = __hip_atomic_load(&e->owner, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (o == 0) {
+            if (!create) return nullptr;
+            // claim: the value is written before the owner becomes visible to other lanes
+            const uint32_t prev = atomicCAS(&e->owner, 0u, 0xFFFFFFFFu);
+            if (prev == 0) {
+                e->value = value;
+                e->a = kPAbsent;
+                e->b = kPAbsent;
+                __threadfence();
+                __hip_atomic_store(&e->owner, owner, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                return e;
+            }
+            o = prev;
+        }
+        while (o == 0xFFFFFFFFu) o = __hip_atomic_load(&e->owner, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (o == owner && e->value == value) return e;
+        h = (h + 1) & mask;
+    }
+    atomicOr(overflow, 1u);
+    return nullptr;
+}
+
+__device__ __forceinline__ int64_t lwrap_mul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+__device__ __forceinline__ int64_t lwrap_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+
+__device__ bool hot_lookup(const Ctx &c, const ParamRuleDev &p, uint64_t v, int64_t *thr) {
+    for (int i = 0; i < p.n_hot; ++i)
+        if (c.st.hot_v[p.hot_off + i] == v) {
+            *thr = c.st.hot_t[p.hot_off + i];
+            return true;
+        }
+    return false;
+}
+
+// ParamFlowChecker.passSingleValueCheck / passDefaultLocalCheck / passThrottleLocalCheck
+__device__ bool param_pass(const Ctx &c, const ParamRuleDev &p, uint64_t v, int acquire, int64_t t,
+                           int64_t thread_count, int64_t *wait_ms) {
+    *wait_ms = 0;
+    int64_t hot;
+    if (p.grade == 1) {
+        int64_t token_count = j_d2l(p.count);
+        if (hot_lookup(c, p, v, &hot)) token_count = hot;
+        if (token_count == 0) return false;
+        PEntry *e = ptab_get(c.st.ptab, c.st.pmask, p.id + 1, v, true, c.st.overflow);
+        if (!e) return false;
+        if (p.behavior == 2) {  // throttle, ParamFlowChecker.java:224-281
+            const int64_t cost = j_round(1.0 * 1000 * (double)acquire * (double)p.duration / (double)token_count);
+            if (e->a == kPAbsent) {
+                e->a = t;
+                return true;
+            }
+            const int64_t expected = e->a + cost;
+            if (expected <= t || expected - t < p.max_queue) {
+                e->a = t;
+                const int64_t wait = expected - t;
+                if (wait > 0) {
+                    e->a = expected;
+                    *wait_ms = wait;
+                }
+                return true;
+            }
+            return false;
+        }
+        // token bucket, ParamFlowChecker.java:132-222
+        const int64_t max_count = lwrap_add(token_count, p.burst);
+        if ((int64_t)acquire > max_count) return false;
+        if (e->a == kPAbsent) {
+            e->a = t;
+            if (e->b == kPAbsent) e->b = max_count - acquire;
+            return true;
+        }
+        const int64_t pass_time = t - e->a;
+        const int64_t dur_ms = lwrap_mul(p.duration, 1000);
+        if (pass_time > dur_ms) {
+            if (e->b == kPAbsent) {
+                e->b = max_count - acquire;
+                e->a = t;
+                return true;
+            }
+            const int64_t rest = e->b;
+            const int64_t to_add = lwrap_mul(pass_time, token_count) / dur_ms;
+            const int64_t nq = lwrap_add(to_add, rest) > max_count ? max_count - acquire
+                                                                   : lwrap_add(rest, to_add) - acquire;
+            if (nq < 0) return false;
+            e->b = nq;
+            e->a = t;
+            return true;
+        }
+        if (e->b != kPAbsent) {
+            if (e->b - acquire >= 0) {
+                e->b -= acquire;
+                return true;
+            }
+            return false;
+        }
+        return false;
+    }
+    if (p.grade == 0) {
+        if (hot_lookup(c, p, v, &hot)) return ++thread_count <= hot;
+        return ++thread_count <= j_d2l(p.count);
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------ circuit breakers
+__device__ void cb_to_open(CbDev &b, int64_t t) {
+    if (b.state == 0 || b.state == 2) {
+        b.state = 1;
+        b.next_retry = t + b.recovery_ms;
+    }
+}
+
+__device__ void cb_stat_current(CbDev &b, int64_t t) {  // LeapArray(1, statIntervalMs).currentWindow(t)
+    const int64_t ws = t - t % b.stat_interval;
+    if (b.st_start == kAbsent || ws > b.st_start) {
+        b.st_start = ws;
+        b.st_bad = 0;
+        b.st_total = 0;
+    }
+}
+
+__device__ void cb_on_complete(CbDev &b, int64_t t, int64_t rt, bool error) {
+    const bool is_rt = b.grade == 0;
+    const bool bad = is_rt ? rt > b.max_allowed_rt : error;
+    const int64_t ws = t - t % b.stat_interval;
+    const bool detached = b.st_start != kAbsent && ws < b.st_start;
+    cb_stat_current(b, t);
+    if (!detached) {
+        if (bad) b.st_bad += 1;
+        b.st_total += 1;
+    }
+    if (b.state == 1) return;
+    if (b.state == 2) {
+        if (bad) cb_to_open(b, t);
+        else {
+            b.state = 0;  // fromHalfOpenToClose -> resetStat on currentWindow()
+            cb_stat_current(b, t);
+            if (!(b.st_start != kAbsent && ws < b.st_start)) {
+                b.st_bad = 0;
+                b.st_total = 0;
+            }
+        }
+        return;
+    }
+    int64_t badc = 0, total = 0;
+    if (b.st_start != kAbsent && !(t - b.st_start > b.stat_interval)) {
+        badc = b.st_bad;
+        total = b.st_total;
+    }
+    if (total < b.min_req) return;
+    if (is_rt) {
+        const double ratio = (double)badc * 1.0 / (double)total;
+        if (ratio > b.slow_ratio) cb_to_open(b, t);
+        if (ratio == b.slow_ratio && b.slow_ratio == 1.0) cb_to_open(b, t);
+    } else {
+        double cur = (double)badc;
+        if (b.grade == 1) cur = (double)badc * 1.0 / (double)total;
+        if (cur > b.count) cb_to_open(b, t);
+    }
+}
+
+// ------------------------------------------------------------------ slot chain (one event)
+__device__ int8_t chain_entry(const Ctx &c, uint32_t r, int64_t t, int acquire, bool prio, bool has_param,
+                              uint64_t param, int64_t *wait_ms) {
+    const ResDev R = c.st.res[r];
+    int64_t *node = c.st.node + (size_t)r * kNodeWords;
+    *wait_ms = 0;
+    int64_t total_wait = 0;
+    // ParamFlowSlot (ParamFlowSlot.java:65-92): args = [param] or []
+    const int nargs = has_param ? 1 : 0;
+    for (uint32_t k = 0; k < R.n_prules; ++k) {
+        const ParamRuleDev &p = c.st.prules[R.prule_off + k];
+        int idx = p.param_idx;
+        if (idx < 0) idx = (-idx <= nargs) ? nargs + idx : -idx;
+        if (nargs <= idx) continue;
+        int64_t tc = 0;
+        if (idx == 0 && (R.fast & 2u)) {
+            PEntry *te = ptab_get(c.st.ttab, c.st.tmask, r + 1, param, false, c.st.overflow);
+            tc = (te && te->a != kPAbsent) ? te->a : 0;
+        }
+        int64_t w = 0;
+        if (!param_pass(c, p, param, acquire, t, tc, &w)) {
+            node_add(c, node, t, MB_BLOCK, acquire);
+            return D_BLOCK_PARAM;
+        }
+        total_wait += w;
+    }
+    // FlowSlot
+    for (uint32_t k = 0; k < R.n_rules; ++k) {
+        int64_t w = 0;
+        const int8_t d = rater_can_pass(c, c.st.rules[R.rule_off + k], node, t, acquire, prio, &w);
+        if (d == D_BLOCK_FLOW) {
+            node_add(c, node, t, MB_BLOCK, acquire);
+            return D_BLOCK_FLOW;
+        }
+        if (d == D_PASS_WAIT) {
+            node[kNodeThreads] += 1;
+            if (has_param && (R.fast & 2u)) {
+                PEntry *te = ptab_get(c.st.ttab, c.st.tmask, r + 1, param, true, c.st.overflow);
+                if (te) te->a = (te->a == kPAbsent ? 0 : te->a) + 1;
+            }
+            *wait_ms = w;
+            return D_PASS_WAIT;
+        }
+        total_wait += w;
+    }
+    // DegradeSlot
+    uint64_t half_mask = 0;
+    for (uint32_t k = 0; k < R.n_cbs; ++k) {
+        CbDev &b = c.st.cbs[R.cb_off + k];
+        bool ok = false;
+        if (b.state == 0) ok = true;
+        else if (b.state == 1 && t >= b.next_retry) {
+            b.state = 2;
+            if (k < 64) half_mask |= 1ULL << k;
+            ok = true;
+        }
+        if (!ok) {
+            for (uint32_t q = 0; q < k && q < 64; ++q) {
+                CbDev &bq = c.st.cbs[R.cb_off + q];
+                if (((half_mask >> q) & 1) && bq.state == 2) bq.state = 1;
+            }
+            node_add(c, node, t, MB_BLOCK, acquire);
+            return D_BLOCK_DEGRADE;
+        }
+    }
+    node[kNodeThreads] += 1;
+    node_add(c, node, t, MB_PASS, acquire);
+    if (has_param && (R.fast & 2u)) {
+        PEntry *te = ptab_get(c.st.ttab, c.st.tmask, r + 1, param, true, c.st.overflow);
+        if (te) te->a = (te->a == kPAbsent ? 0 : te->a) + 1;
+    }
+    *wait_ms = total_wait;
+    return D_PASS;
+}
+
+__device__ void chain_exit(const Ctx &c, uint32_t r, int64_t t, int64_t rt, int count, bool error, bool has_param,
+                           uint64_t param) {
+    const ResDev R = c.st.res[r];
+    int64_t *node = c.st.node + (size_t)r * kNodeWords;
+    node_add_rt_success(c, node, t, rt, count);
+    node[kNodeThreads] -= 1;
+    if (error) node_add(c, node, t, MB_EXC, count);
+    if (has_param && (R.fast & 2u)) {  // ParameterMetric.decreaseThreadCount
+        PEntry *te = ptab_get(c.st.ttab, c.st.tmask, r + 1, param, true, c.st.overflow);
+        if (te) {
+            if (te->a == kPAbsent) te->a = 0;
+            else if (--te->a <= 0) te->a = kPAbsent;  // remove(value)
+        }
+    }
+    for (uint32_t k = 0; k < R.n_cbs; ++k) cb_on_complete(c.st.cbs[R.cb_off + k], t, rt, error);
+}
+
+// ------------------------------------------------------------------ classify
+__global__ __launch_bounds__(kT) void k_lclassify(FlowState st, const uint8_t *__restrict__ kind,
+                                                  const uint32_t *__restrict__ resource,
+                                                  const uint32_t *__restrict__ ts_off, int64_t ts_base,
+                                                  const int32_t *__restrict__ acquire,
+                                                  const uint8_t *__restrict__ flags, uint32_t n, uint32_t *keys,
+                                                  Payload *pay, int8_t *decision, int32_t *wait_ms) {
+    const uint32_t i = blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = resource[i];
+    const uint8_t fl = flags ? flags[i] : 0;
+    const bool ex = kind[i] == 1;
+    decision[i] = D_PASS;
+    wait_ms[i] = 0;
+    if (r >= st.nres) {  // unknown resource: no node, no rules (documented)
+        keys[i] = st.nres;
+        pay[i] = Payload{i, 0, 0, 0};
+        return;
+    }
+    keys[i] = r;
+    const uint32_t off = ts_off[i];
+    const int64_t t = ts_base + (int64_t)off;
+    uint32_t idx = i | (ex ? F_EXIT : 0u) | ((fl & SGA_EV_ERROR) ? F_ERROR : 0u) | ((fl & SGA_EV_HAS_PARAM) ? F_PARAM : 0u);
+    const uint32_t a = (uint32_t)acquire[i] & 0x7FFFFFFFu;
+    pay[i] = Payload{idx, off, a | ((!ex && (fl & SGA_EV_PRIORITIZED)) ? 0x80000000u : 0u), (uint32_t)(t / kSecW)};
+}
+
+// ------------------------------------------------------------------ runs (segmented scan)
+struct LAgg {
+    uint32_t nh, nf, flag;
+    uint32_t nent, nexit, cp;   // entries, exits, prioritized entries since the run head
+    int32_t mn, mx;             // entry acquire min / max
+};
+
+__device__ __forceinline__ LAgg lagg_id() { return LAgg{0, 0, 0, 0, 0, 0, INT32_MAX, INT32_MIN}; }
+
+__device__ __forceinline__ LAgg lagg_combine(const LAgg &a, const LAgg &b) {
+    LAgg r;
+    r.nh = a.nh + b.nh;
+    r.nf = a.nf + b.nf;
+    r.flag = a.flag | b.flag;
+    r.nent = b.flag ? b.nent : a.nent + b.nent;
+    r.nexit = b.flag ? b.nexit : a.nexit + b.nexit;
+    r.cp = b.flag ? b.cp : a.cp + b.cp;
+    r.mn = b.flag ? b.mn : min(a.mn, b.mn);
+    r.mx = b.flag ? b.mx : max(a.mx, b.mx);
+    return r;
+}
+
+__device__ __forceinline__ LAgg lagg_value(uint32_t key, uint32_t pkey, const Payload &q, const Payload &pq,
+                                           bool has_prev, bool valid) {
+    if (!valid) return lagg_id();
+    const bool fh = !has_prev || key != pkey;
+    const bool h = fh || q.bucket != pq.bucket;
+    const bool ex = (q.idx & F_EXIT) != 0;
+    const int32_t a = (int32_t)(q.acq_prio & 0x7FFFFFFFu);
+    return LAgg{h ? 1u : 0u, fh ? 1u : 0u, h ? 1u : 0u, ex ? 0u : 1u, ex ? 1u : 0u,
+                ex ? 0u : (q.acq_prio >> 31), ex ? INT32_MAX : a, ex ? INT32_MIN : a};
+}
+
+// blocked arrangement per thread (kItems consecutive events), block scan of thread aggregates
+template <int NT>
+__device__ LAgg lblock_excl(const LAgg &v, LAgg *total) {
+    __shared__ LAgg sh[NT];
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    // Hillis-Steele in LDS (NT = 256: 8 steps)
+    for (int o = 1; o < NT; o <<= 1) {
+        LAgg x = sh[threadIdx.x];
+        if ((int)threadIdx.x >= o) x = lagg_combine(sh[threadIdx.x - o], x);
+        __syncthreads();
+        sh[threadIdx.x] = x;
+        __syncthreads();
+    }
+    const LAgg incl = sh[threadIdx.x];
+    if (total) *total = sh[NT - 1];
+    const LAgg ex = threadIdx.x ? sh[threadIdx.x - 1] : lagg_id();
+    __syncthreads();
+    (void)incl;
+    return ex;
+}
+
+__global__ __launch_bounds__(kT) void k_lruns_up(const uint32_t *__restrict__ keys, const Payload *__restrict__ pay,
+                                                 uint32_t n, uint32_t invalid, LAgg *tile_agg, uint32_t *tile_valid) {
+    const uint32_t e0 = blockIdx.x * kTileElems + threadIdx.x * kItems;
+    LAgg acc = lagg_id();
+    uint32_t nv = 0;
+    if (e0 < n) {
+        uint32_t pk = e0 > 0 ? keys[e0 - 1] : invalid;
+        Payload pq = e0 > 0 ? pay[e0 - 1] : Payload{0, 0, 0, 0};
+        for (int i = 0; i < kItems && e0 + i < n; ++i) {
+            const uint32_t e = e0 + i;
+            const uint32_t k = keys[e];
+            const Payload q = pay[e];
+            const bool valid = k != invalid;
+            acc = lagg_combine(acc, lagg_value(k, pk, q, pq, e > 0, valid));
+            nv += valid ? 1 : 0;
+            pk = k;
+            pq = q;
+        }
+    }
+    LAgg total;
+    lblock_excl<kT>(acc, &total);
+    __shared__ uint32_t cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    atomicAdd(&cnt, nv);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        tile_agg[blockIdx.x] = total;
+        tile_valid[blockIdx.x] = cnt;
+    }
+}
+
+__global__ __launch_bounds__(kT) void k_lruns_tiles(const LAgg *__restrict__ tile_agg,
+                                                    const uint32_t *__restrict__ tile_valid, uint32_t ntiles,
+                                                    LAgg *tile_carry, uint32_t *counters) {
+    LAgg carry = lagg_id();
+    uint32_t nvalid = 0;
+    for (uint32_t b = 0; b < ntiles; b += kT) {
+        const uint32_t t = b + threadIdx.x;
+        const LAgg v = t < ntiles ? tile_agg[t] : lagg_id();
+        LAgg total;
+        const LAgg ex = lblock_excl<kT>(v, &total);
+        if (t < ntiles) tile_carry[t] = lagg_combine(carry, ex);
+        carry = lagg_combine(carry, total);
+        __shared__ uint32_t s;
+        if (threadIdx.x == 0) s = 0;
+        __syncthreads();
+        if (t < ntiles) atomicAdd(&s, tile_valid[t]);
+        __syncthreads();
+        nvalid += s;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        counters[0] = nvalid;
+        counters[1] = carry.nh;
+        counters[2] = carry.nf;
+    }
+}
+
+__global__ __launch_bounds__(kT) void k_lruns_down(const uint32_t *__restrict__ keys, const Payload *__restrict__ pay,
+                                                   const int64_t *__restrict__ rt_in, uint32_t invalid,
+                                                   const LAgg *__restrict__ tile_carry, FlowScratch sc) {
+    const uint32_t nvalid = sc.counters[0];
+    const uint32_t base = blockIdx.x * kTileElems;
+    if (base >= nvalid) return;
+    const uint32_t e0 = base + threadIdx.x * kItems;
+    LAgg acc = lagg_id();
+    uint32_t pk0 = e0 > 0 && e0 - 1 < nvalid ? keys[e0 - 1] : invalid;
+    Payload pq0 = e0 > 0 && e0 - 1 < nvalid ? pay[e0 - 1] : Payload{0, 0, 0, 0};
+    {
+        uint32_t pk = pk0;
+        Payload pq = pq0;
+        for (int i = 0; i < kItems && e0 + i < nvalid; ++i) {
+            const uint32_t e = e0 + i;
+            const uint32_t k = keys[e];
+            const Payload q = pay[e];
+            acc = lagg_combine(acc, lagg_value(k, pk, q, pq, e > 0, true));
+            pk = k;
+            pq = q;
+        }
+    }
+    const LAgg ex = lblock_excl<kT>(acc, nullptr);
+    if (e0 >= nvalid) return;
+    LAgg run = lagg_combine(tile_carry[blockIdx.x], ex);
+    uint32_t pk = pk0;
+    Payload pq = pq0;
+    for (int i = 0; i < kItems && e0 + i < nvalid; ++i) {
+        const uint32_t e = e0 + i;
+        const uint32_t k = keys[e];
+        const Payload q = pay[e];
+        const LAgg v = lagg_value(k, pk, q, pq, e > 0, true);
+        run = lagg_combine(run, v);
+        const uint32_t rid = run.nh - 1;
+        const bool ex_ev = (q.idx & F_EXIT) != 0;
+        sc.ev_run[e] = rid;
+        sc.ev_eidx[e] = ex_ev ? 0xFFFFFFFFu : run.nent - 1;  // entry index within the run
+        if (v.flag) {
+            sc.run_start[rid] = e;
+            sc.run_slot[rid] = k;
+            sc.run_t0off[rid] = q.ts_off;
+            sc.run_exc[rid] = 0;
+            sc.run_exerr[rid] = 0;
+            sc.run_exrt[rid] = 0;
+            sc.run_exmin[rid] = INT64_MAX;
+        }
+        if (v.nf) sc.flow_first_run[run.nf - 1] = rid;
+        bool last = e + 1 >= nvalid;
+        if (!last) {
+            const uint32_t nk = keys[e + 1];
+            last = nk != k || pay[e + 1].bucket != q.bucket;
+        }
+        if (last) {
+            sc.run_end[rid] = e + 1;
+            sc.run_nent[rid] = run.nent;
+            sc.run_nexit[rid] = run.nexit;
+            sc.run_cp[rid] = run.cp;
+            sc.run_amin[rid] = run.mn;
+            sc.run_amax[rid] = run.mx;
+        }
+        pk = k;
+        pq = q;
+    }
+}
+
+// exit aggregates per run (SUCCESS count, exceptions, RT sum, min RT): atomics per run
+// pre-reduced inside each thread's consecutive events.
+__global__ __launch_bounds__(kT) void k_lexits(const Payload *__restrict__ pay, const int64_t *__restrict__ rt_in,
+                                               FlowScratch sc) {
+    const uint32_t nvalid = sc.counters[0];
+    const uint32_t e0 = (blockIdx.x * kT + threadIdx.x) * kItems;
+    if (e0 >= nvalid) return;
+    uint32_t cur = 0xFFFFFFFFu;
+    uint64_t c = 0, er = 0;
+    int64_t rs = 0, mn = INT64_MAX;
+    auto flush = [&]() {
+        if (cur == 0xFFFFFFFFu || (c == 0 && mn == INT64_MAX)) return;
+        atomicAdd((unsigned long long *)&sc.run_exc[cur], (unsigned long long)c);
+        atomicAdd((unsigned long long *)&sc.run_exerr[cur], (unsigned long long)er);
+        atomicAdd((unsigned long long *)&sc.run_exrt[cur], (unsigned long long)rs);
+        atomicMin((long long *)&sc.run_exmin[cur], (long long)mn);
+    };
+    for (int i = 0; i < kItems && e0 + i < nvalid; ++i) {
+        const uint32_t e = e0 + i;
+        const Payload q = pay[e];
+        if (!(q.idx & F_EXIT)) continue;
+        const uint32_t r = sc.ev_run[e];
+        if (r != cur) {
+            flush();
+            cur = r;
+            c = er = 0;
+            rs = 0;
+            mn = INT64_MAX;
+        }
+        const uint64_t cnt = q.acq_prio & 0x7FFFFFFFu;
+        const int64_t rt = rt_in[q.idx & F_IDX];
+        c += cnt;
+        if (q.idx & F_ERROR) er += cnt;
+        rs += rt;
+        if (rt < mn) mn = rt;
+    }
+    flush();
+}
+
+// ------------------------------------------------------------------ per-resource resolve
+__device__ __forceinline__ bool default_cond(double count, int64_t sum, int32_t a) {
+    // curCount + acquireCount > count ? block : pass, curCount = (int) passQps, DefaultController.java:77
+    const int32_t cur = j_d2i((double)sum / 1.0);
+    return !((double)(int32_t)((uint32_t)cur + (uint32_t)a) > count);
+}
+
+__global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, FlowScratch sc,
+                                               const Payload *__restrict__ pay, const uint32_t *__restrict__ keys,
+                                               int64_t ts_base, const int64_t *__restrict__ rt_in,
+                                               const uint64_t *__restrict__ param_in, int8_t *decision,
+                                               int32_t *wait_ms) {
+    const Ctx c{st, max_rt};
+    const uint32_t nflows = sc.counters[2], nruns = sc.counters[1];
+    for (uint32_t fl = blockIdx.x * kT + threadIdx.x; fl < nflows; fl += gridDim.x * kT) {
+        const uint32_t r0 = sc.flow_first_run[fl];
+        const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        for (uint32_t r = r0; r < r1; ++r) {
+            const uint32_t res = sc.run_slot[r];
+            const ResDev R = st.res[res];
+            int64_t *node = st.node + (size_t)res * kNodeWords;
+            const uint32_t j0 = sc.run_start[r], j1 = sc.run_end[r];
+            const uint32_t nent = sc.run_nent[r];
+            const int32_t a = sc.run_amin[r];
+            const int64_t t0 = ts_base + (int64_t)sc.run_t0off[r];
+            bool fast = (R.fast & 1u) && sc.run_cp[r] == 0 && (nent == 0 || a == sc.run_amax[r]) && a >= 0;
+            if (fast) {  // no clock regression in this resource's windows
+                const int64_t *sb = node + kNodeSec + kMB * (int)((t0 / kSecW) % 2);
+                const int64_t *mb = node + kNodeMin + kMB * (int)((t0 / kMinW) % 60);
+                if ((sb[0] != kAbsent && t0 - t0 % kSecW < sb[0]) || (mb[0] != kAbsent && t0 - t0 % kMinW < mb[0]))
+                    fast = false;
+            }
+            if (fast && nent) {  // WarmUp sync must only see entries in one second (true: run is inside one 500 ms bucket)
+                const int64_t s0 = sec_sum(node, t0, MB_PASS);
+                if (s0 + (int64_t)nent * a + a >= (int64_t)INT32_MAX) fast = false;
+            }
+            if (!fast) {
+                for (uint32_t j = j0; j < j1; ++j) {
+                    const Payload q = pay[j];
+                    const int64_t t = ts_base + (int64_t)q.ts_off;
+                    const uint32_t idx = q.idx & F_IDX;
+                    const bool hp = (q.idx & F_PARAM) != 0;
+                    const uint64_t pv = hp ? param_in[idx] : 0;
+                    if (q.idx & F_EXIT) {
+                        chain_exit(c, res, t, rt_in[idx], (int)(q.acq_prio & 0x7FFFFFFFu), (q.idx & F_ERROR) != 0, hp, pv);
+                    } else {
+                        int64_t w = 0;
+                        decision[idx] = chain_entry(c, res, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
+                                                    hp, pv, &w);
+                        wait_ms[idx] = (int32_t)w;
+                    }
+                }
+                sc.run_mode[r] = RUN_DONE;
+                continue;
+            }
+            // ---- closed form: rotate both windows once at the run's first event
+            int64_t *sb = sec_current(node, t0, max_rt);
+            int64_t *mb = min_current(node, t0, max_rt);
+            uint32_t f = 0;
+            if (nent) {
+                FlowRuleDev &rule = st.rules[R.rule_off];
+                const int64_t s0 = sec_sum(node, t0, MB_PASS);
+                if (rule.behavior == 1) {
+                    // WarmUpController: sync once (the run is inside one second), then a fixed threshold
+                    const int64_t previous_qps = j_d2l(node_prev_pass_qps(c, node, t0));
+                    warmup_sync(rule, t0, previous_qps);
+                    const int64_t rest = rule.stored_tokens;
+                    double lim;
+                    if (rest >= rule.warning_token) {
+                        const int64_t above = rest - rule.warning_token;
+                        lim = j_next_up(1.0 / ((double)above * rule.slope + 1.0 / rule.count));
+                    } else {
+                        lim = rule.count;
+                    }
+                    uint32_t lo = 0, hi = nent;
+                    while (lo < hi) {
+                        const uint32_t mid = lo + ((hi - lo) >> 1);
+                        const int64_t pq = j_d2l((double)(s0 + (int64_t)mid * a) / 1.0);
+                        if ((double)(pq + a) <= lim) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    f = lo;
+                } else {
+                    uint32_t lo = 0, hi = nent;
+                    while (lo < hi) {
+                        const uint32_t mid = lo + ((hi - lo) >> 1);
+                        if (default_cond(rule.count, s0 + (int64_t)mid * a, a)) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    f = lo;
+                }
+            }
+            const int64_t pa = (int64_t)f * a, ba = (int64_t)(nent - f) * a;
+            const int64_t exc = (int64_t)sc.run_exc[r], exerr = (int64_t)sc.run_exerr[r];
+            const int64_t exrt = sc.run_exrt[r], exmin = sc.run_exmin[r];
+            sb[MB_PASS] += pa;
+            sb[MB_BLOCK] += ba;
+            sb[MB_SUCC] += exc;
+            sb[MB_RT] += exrt;
+            sb[MB_EXC] += exerr;
+            if (exmin < sb[MB_MINRT]) sb[MB_MINRT] = exmin;
+            mb[MB_PASS] += pa;
+            mb[MB_BLOCK] += ba;
+            mb[MB_SUCC] += exc;
+            mb[MB_RT] += exrt;
+            mb[MB_EXC] += exerr;
+            if (exmin < mb[MB_MINRT]) mb[MB_MINRT] = exmin;
+            node[kNodeThreads] += (int64_t)f - (int64_t)sc.run_nexit[r];
+            sc.run_f[r] = f;
+            sc.run_mode[r] = RUN_FAST;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kT) void k_lresults(FlowScratch sc, const Payload *__restrict__ pay, int8_t *decision) {
+    const uint32_t nvalid = sc.counters[0];
+    const uint32_t j = blockIdx.x * kT + threadIdx.x;
+    if (j >= nvalid) return;
+    const uint32_t r = sc.ev_run[j];
+    if (sc.run_mode[r] != RUN_FAST) return;
+    const Payload q = pay[j];
+    if (q.idx & F_EXIT) return;
+    decision[q.idx & F_IDX] = sc.ev_eidx[j] < sc.run_f[r] ? D_PASS : D_BLOCK_FLOW;
+}
+
+__global__ void k_node_view(FlowState st, int64_t max_rt, uint32_t r, int64_t now, double *dv, int64_t *iv) {
+    if (threadIdx.x || blockIdx.x) return;
+    const Ctx c{st, max_rt};
+    int64_t *node = st.node + (size_t)r * kNodeWords;
+    // StatisticNode getters (each rotates the current window first)
+    dv[0] = node_pass_qps(c, node, now);
+    sec_current(node, now, max_rt);
+    dv[1] = (double)sec_sum(node, now, MB_BLOCK) / 1.0;
+    dv[2] = (double)sec_sum(node, now, MB_SUCC) / 1.0;
+    dv[3] = (double)sec_sum(node, now, MB_EXC) / 1.0;
+    dv[4] = (double)sec_sum(node, now, MB_OPASS) / 1.0;
+    const int64_t succ = sec_sum(node, now, MB_SUCC);
+    dv[5] = succ == 0 ? 0.0 : (double)sec_sum(node, now, MB_RT) * 1.0 / (double)succ;
+    int64_t mr = max_rt;
+    for (int j = 0; j < 2; ++j) {
+        const int64_t *b = node + kNodeSec + kMB * j;
+        if (b[0] != kAbsent && !(now - b[0] > kSecInterval) && b[MB_MINRT] < mr) mr = b[MB_MINRT];
+    }
+    dv[6] = (double)(mr < 1 ? 1 : mr);
+    dv[7] = node_prev_pass_qps(c, node, now);
+    min_current(node, now, max_rt);
+    iv[0] = min_sum(node, now, MB_PASS);
+    iv[1] = min_sum(node, now, MB_BLOCK);
+    iv[2] = min_sum(node, now, MB_SUCC);
+    iv[3] = min_sum(node, now, MB_EXC);
+    iv[4] = node[kNodeThreads];
+    iv[5] = node_waiting(node, now);
+}
+
+__global__ void k_init_nodes(int64_t *node, uint32_t n, int64_t max_rt) {
+    const uint32_t r = blockIdx.x * kT + threadIdx.x;
+    if (r >= n) return;
+    int64_t *p = node + (size_t)r * kNodeWords;
+    for (int j = 0; j < 2; ++j) {
+        p[kNodeSec + kMB * j] = kAbsent;
+        mb_zero(p + kNodeSec + kMB * j, max_rt);
+        p[kNodeBor + 2 * j] = kAbsent;
+        p[kNodeBor + 2 * j + 1] = 0;
+    }
+    for (int j = 0; j < 60; ++j) {
+        p[kNodeMin + kMB * j] = kAbsent;
+        mb_zero(p + kNodeMin + kMB * j, max_rt);
+    }
+    p[kNodeThreads] = 0;
+}
+
+__global__ void k_clear_ptab(PEntry *t, uint32_t n) {
+    const uint32_t i = blockIdx.x * kT + threadIdx.x;
+    if (i < n) t[i] = PEntry{0, 0, 0, kPAbsent, kPAbsent};
+}
+
+}  // namespace
+
+// ======================================================================== host side
+FlowState FlowEngine::state() const {
+    FlowState s{};
+    s.node = d_node.p;
+    s.rules = d_rules.p;
+    s.prules = d_prules.p;
+    s.hot_v = d_hot_v.p;
+    s.hot_t = d_hot_t.p;
+    s.cbs = d_cbs.p;
+    s.res = d_res.p;
+    s.ptab = d_ptab.p;
+    s.ttab = d_ttab.p;
+    s.pmask = d_ptab.n ? (uint32_t)(d_ptab.n - 1) : 0;
+    s.tmask = d_ttab.n ? (uint32_t)(d_ttab.n - 1) : 0;
+    s.nres = nres;
+    s.overflow = d_overflow.p;
+    return s;
+}
+
+int FlowEngine::set_resources(uint32_t n) {
+    if (n == nres) return 0;
+    if (nres != 0) return SGA_EINVAL;  // resource table is fixed once set
+    nres = n;
+    d_node.alloc((size_t)n * kNodeWords);
+    hipLaunchKernelGGL(k_init_nodes, dim3((n + kT - 1) / kT), dim3(kT), 0, stream, d_node.p, n,
+                       (int64_t)cfg.statistic_max_rt);
+    h_res.assign(n, ResDev{});
+    d_overflow.alloc(1);
+    SGA_HIP_CHECK(hipMemsetAsync(d_overflow.p, 0, 4, stream));
+    // parameter tables: power of two, sized for the batch capacity
+    size_t pc = 1;
+    while (pc < (size_t)cfg.max_batch * 2) pc <<= 1;
+    pc = std::max<size_t>(pc, 1 << 16);
+    d_ptab.alloc(pc);
+    d_ttab.alloc(pc);
+    hipLaunchKernelGGL(k_clear_ptab, dim3((unsigned)((pc + kT - 1) / kT)), dim3(kT), 0, stream, d_ptab.p, (uint32_t)pc);
+    hipLaunchKernelGGL(k_clear_ptab, dim3((unsigned)((pc + kT - 1) / kT)), dim3(kT), 0, stream, d_ttab.p, (uint32_t)pc);
+    upload_res();
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    return 0;
+}
+
+void FlowEngine::upload_res() {
+    for (uint32_t r = 0; r < nres; ++r) {
+        ResDev &R = h_res[r];
+        R.fast &= 2u;  // bit1 (a thread-count map exists) is sticky
+        if (R.n_rules == 1 && R.n_prules == 0 && R.n_cbs == 0 && !(R.fast & 2u)) {
+            const FlowRuleDev &fr = h_rules[R.rule_off];
+            if (fr.grade == 1 && (fr.behavior == 0 || fr.behavior == 1)) R.fast = 1;
+        }
+    }
+    if (d_res.n < std::max<size_t>(nres, 1)) d_res.alloc(std::max<size_t>(nres, 1));
+    if (nres) SGA_HIP_CHECK(hipMemcpyAsync(d_res.p, h_res.data(), nres * sizeof(ResDev), hipMemcpyHostToDevice, stream));
+}
+
+// FlowRuleManager.loadRules -> FlowRuleUtil.buildFlowRuleMap/generateRater: raters regenerated
+// (controller state reset), node statistics kept.  FlowRuleUtil.java:84-195
+int FlowEngine::load_flow_rules(const sga_flow_rule *rules, size_t n) {
+    if (!nres) return SGA_EINVAL;
+    std::vector<std::vector<FlowRuleDev>> per(nres);
+    int valid = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const sga_flow_rule &r = rules[i];
+        if (r.resource >= nres) continue;
+        bool ok = r.count >= 0 && r.grade >= 0 && r.strategy >= 0 && r.control_behavior >= 0 && r.strategy == 0;
+        if (ok && r.grade == 1) {
+            switch (r.control_behavior) {
+            case 1: ok = r.warm_up_period_sec > 0; break;
+            case 2: ok = r.max_queueing_time_ms > 0; break;
+            case 3: ok = r.warm_up_period_sec > 0 && r.max_queueing_time_ms > 0; break;
+            default: break;
+            }
+        } else if (ok && r.grade != 0) {
+            ok = false;
+        }
+        if (!ok) continue;
+        FlowRuleDev d{};
+        d.behavior = r.grade == 1 ? r.control_behavior : 0;
+        if (d.behavior < 0 || d.behavior > 3) d.behavior = 0;
+        d.grade = r.grade;
+        d.count = r.count;
+        d.max_queue = r.max_queueing_time_ms;
+        d.cold_factor = cfg.cold_factor;
+        d.latest_passed = -1;
+        if (d.behavior == 1 || d.behavior == 3) {  // WarmUpController.construct, :83-106
+            d.warning_token = j_d2i((double)r.warm_up_period_sec * r.count) / (cfg.cold_factor - 1);
+            d.max_token = d.warning_token + j_d2i(2 * r.warm_up_period_sec * r.count / (1.0 + cfg.cold_factor));
+            d.slope = (cfg.cold_factor - 1.0) / r.count / (double)(d.max_token - d.warning_token);
+        }
+        per[r.resource].push_back(d);
+        valid++;
+    }
+    h_rules.clear();
+    for (uint32_t r = 0; r < nres; ++r) {
+        h_res[r].rule_off = (uint32_t)h_rules.size();
+        h_res[r].n_rules = (uint32_t)per[r].size();
+        h_rules.insert(h_rules.end(), per[r].begin(), per[r].end());
+    }
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    d_rules.alloc(std::max<size_t>(h_rules.size(), 1));
+    if (!h_rules.empty())
+        SGA_HIP_CHECK(hipMemcpyAsync(d_rules.p, h_rules.data(), h_rules.size() * sizeof(FlowRuleDev),
+                                     hipMemcpyHostToDevice, stream));
+    upload_res();
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    return valid;
+}
+
+static bool prule_equal(const sga_param_rule &a, const std::vector<uint64_t> &av, const std::vector<int32_t> &at,
+                        const sga_param_rule &b) {
+    if (a.resource != b.resource || a.grade != b.grade || a.count != b.count || a.control_behavior != b.control_behavior ||
+        a.max_queueing_time_ms != b.max_queueing_time_ms || a.burst_count != b.burst_count ||
+        a.param_idx != b.param_idx || a.duration_in_sec != b.duration_in_sec || a.n_hot != b.n_hot)
+        return false;
+    for (uint32_t i = 0; i < b.n_hot; ++i)
+        if (av[i] != b.hot_values[i] || at[i] != b.hot_thresholds[i]) return false;
+    return true;
+}
+
+// ParamFlowRuleManager.loadRules: rules grouped by resource in list order; ParameterMetric maps
+// are keyed by the rule, so an equal rule keeps its maps (ids), a new one starts empty.
+int FlowEngine::load_param_rules(const sga_param_rule *rules, size_t n) {
+    if (!nres) return SGA_EINVAL;
+    std::vector<std::vector<size_t>> per(nres);
+    for (size_t i = 0; i < n; ++i) {
+        const sga_param_rule &r = rules[i];
+        if (r.resource >= nres) continue;
+        if (!(r.count >= 0 && r.grade >= 0 && r.duration_in_sec > 0 && r.burst_count >= 0 && r.control_behavior >= 0 &&
+              r.max_queueing_time_ms >= 0))
+            continue;  // ParamFlowRuleUtil.isValidParamRule
+        if (r.n_hot && (!r.hot_values || !r.hot_thresholds)) continue;
+        per[r.resource].push_back(i);
+    }
+    std::vector<ParamRuleDev> nr;
+    std::vector<sga_param_rule> nsrc;
+    std::vector<std::vector<uint64_t>> nhv;
+    std::vector<std::vector<int32_t>> nht;
+    std::vector<uint64_t> hv;
+    std::vector<int32_t> ht;
+    std::vector<bool> used(h_prule_src.size(), false);
+    int valid = 0;
+    for (uint32_t res = 0; res < nres; ++res) {
+        h_res[res].prule_off = (uint32_t)nr.size();
+        h_res[res].n_prules = (uint32_t)per[res].size();
+        for (size_t i : per[res]) {
+            const sga_param_rule &r = rules[i];
+            uint32_t id = 0xFFFFFFFFu;
+            for (size_t k = 0; k < h_prule_src.size(); ++k)
+                if (!used[k] && prule_equal(h_prule_src[k], h_prule_hot_v[k], h_prule_hot_t[k], r)) {
+                    used[k] = true;
+                    id = h_prules[k].id;
+                    break;
+                }
+            if (id == 0xFFFFFFFFu) id = next_prule_id++;
+            ParamRuleDev d{};
+            d.grade = r.grade;
+            d.behavior = r.control_behavior;
+            d.count = r.count;
+            d.max_queue = r.max_queueing_time_ms;
+            d.burst = r.burst_count;
+            d.param_idx = r.param_idx;
+            d.duration = r.duration_in_sec;
+            d.n_hot = (int32_t)r.n_hot;
+            d.hot_off = (uint32_t)hv.size();
+            d.id = id;
+            for (uint32_t h = 0; h < r.n_hot; ++h) {
+                hv.push_back(r.hot_values[h]);
+                ht.push_back(r.hot_thresholds[h]);
+            }
+            nr.push_back(d);
+            sga_param_rule src = r;
+            src.hot_values = nullptr;
+            src.hot_thresholds = nullptr;
+            nsrc.push_back(src);
+            nhv.emplace_back(r.hot_values, r.hot_values + r.n_hot);
+            nht.emplace_back(r.hot_thresholds, r.hot_thresholds + r.n_hot);
+            valid++;
+        }
+    }
+    for (uint32_t res = 0; res < nres; ++res)
+        if (h_res[res].n_prules) h_res[res].fast |= 2u;  // ParameterMetric created on first rule load
+    h_prules = nr;
+    h_prule_src = nsrc;
+    h_prule_hot_v = nhv;
+    h_prule_hot_t = nht;
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    d_prules.alloc(std::max<size_t>(nr.size(), 1));
+    d_hot_v.alloc(std::max<size_t>(hv.size(), 1));
+    d_hot_t.alloc(std::max<size_t>(ht.size(), 1));
+    if (!nr.empty())
+        SGA_HIP_CHECK(hipMemcpyAsync(d_prules.p, nr.data(), nr.size() * sizeof(ParamRuleDev), hipMemcpyHostToDevice, stream));
+    if (!hv.empty()) {
+        SGA_HIP_CHECK(hipMemcpyAsync(d_hot_v.p, hv.data(), hv.size() * 8, hipMemcpyHostToDevice, stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(d_hot_t.p, ht.data(), ht.size() * 4, hipMemcpyHostToDevice, stream));
+    }
+    upload_res();
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    return valid;
+}
+
+// DegradeRuleManager.loadRules: an unchanged rule keeps its breaker (state and statistics).
+int FlowEngine::load_degrade_rules(const sga_degrade_rule *rules, size_t n) {
+    if (!nres) return SGA_EINVAL;
+    // current breaker states come back from the device first
+    if (!h_cbs.empty()) {
+        SGA_HIP_CHECK(hipMemcpyAsync(h_cbs.data(), d_cbs.p, h_cbs.size() * sizeof(CbDev), hipMemcpyDeviceToHost, stream));
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+    std::vector<CbDev> nc;
+    std::vector<sga_degrade_rule> nsrc;
+    std::vector<bool> used(h_cb_src.size(), false);
+    int valid = 0;
+    for (uint32_t res = 0; res < nres; ++res) {
+        h_res[res].cb_off = (uint32_t)nc.size();
+        uint32_t cnt = 0;
+        for (size_t i = 0; i < n; ++i) {
+            const sga_degrade_rule &r = rules[i];
+            if (r.resource != res) continue;
+            bool ok = r.count >= 0 && r.time_window > 0 && r.min_request_amount > 0 && r.stat_interval_ms > 0;
+            if (ok) {
+                switch (r.grade) {
+                case 0: ok = r.slow_ratio_threshold >= 0 && r.slow_ratio_threshold <= 1; break;
+                case 1: ok = r.count <= 1; break;
+                case 2: break;
+                default: ok = false;
+                }
+            }
+            if (!ok) continue;
+            int keep = -1;
+            for (size_t k = 0; k < h_cb_src.size(); ++k) {
+                const sga_degrade_rule &o = h_cb_src[k];
+                if (!used[k] && o.resource == r.resource && o.grade == r.grade && o.count == r.count &&
+                    o.time_window == r.time_window && o.min_request_amount == r.min_request_amount &&
+                    o.slow_ratio_threshold == r.slow_ratio_threshold && o.stat_interval_ms == r.stat_interval_ms) {
+                    used[k] = true;
+                    keep = (int)k;
+                    break;
+                }
+            }
+            CbDev d{};
+            if (keep >= 0) {
+                d = h_cbs[keep];
+            } else {
+                d.grade = r.grade;
+                d.min_req = r.min_request_amount;
+                d.count = r.count;
+                d.slow_ratio = r.slow_ratio_threshold;
+                d.stat_interval = r.stat_interval_ms;
+                d.state = 0;
+                d.recovery_ms = (int64_t)r.time_window * 1000;
+                d.max_allowed_rt = j_round(r.count);
+                d.next_retry = 0;
+                d.st_start = kAbsent;
+            }
+            nc.push_back(d);
+            nsrc.push_back(r);
+            cnt++;
+            valid++;
+        }
+        h_res[res].n_cbs = cnt;
+    }
+    h_cbs = nc;
+    h_cb_src = nsrc;
+    d_cbs.alloc(std::max<size_t>(nc.size(), 1));
+    if (!nc.empty())
+        SGA_HIP_CHECK(hipMemcpyAsync(d_cbs.p, nc.data(), nc.size() * sizeof(CbDev), hipMemcpyHostToDevice, stream));
+    upload_res();
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    return valid;
+}
+
+static size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int64_t *ts, const int32_t *acquire,
+                       const uint8_t *flags, const int64_t *rt, const uint64_t *param, size_t n, int8_t *decision,
+                       int32_t *wait_ms) {
+    if (!nres) return SGA_EINVAL;
+    if (n == 0) return 0;
+    const size_t cap = cfg.max_batch;
+    if (cap > F_IDX) return SGA_ERANGE;
+    if (scratch_cap < cap) {
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+        size_t hist = 0;
+        for (int b = 1; b <= 32; ++b) hist = std::max(hist, radix_hist_entries(cap, b));
+        const size_t ntiles = (cap + kTileElems - 1) / kTileElems + 1;
+        size_t bytes = 2 * al(cap * 4) + 2 * al(cap * sizeof(Payload)) + 2 * al(cap * 4) + 10 * al(cap * 4) +
+                       4 * al(cap * 8) + al(cap) + al(cap * 4) + 2 * al(ntiles * sizeof(LAgg)) + al(ntiles * 4) +
+                       al(64) + 2 * al(hist * 4) + al(scan_partials_needed(hist) * 4 + 64);
+        d_scratch.alloc(bytes);
+        char *p = (char *)d_scratch.p;
+        auto take = [&](size_t b) {
+            void *r = p;
+            p += al(b);
+            return r;
+        };
+        sc.keys[0] = (uint32_t *)take(cap * 4);
+        sc.keys[1] = (uint32_t *)take(cap * 4);
+        sc.pay[0] = (Payload *)take(cap * sizeof(Payload));
+        sc.pay[1] = (Payload *)take(cap * sizeof(Payload));
+        sc.ev_run = (uint32_t *)take(cap * 4);
+        sc.ev_eidx = (uint32_t *)take(cap * 4);
+        sc.run_start = (uint32_t *)take(cap * 4);
+        sc.run_end = (uint32_t *)take(cap * 4);
+        sc.run_slot = (uint32_t *)take(cap * 4);
+        sc.run_t0off = (uint32_t *)take(cap * 4);
+        sc.run_nent = (uint32_t *)take(cap * 4);
+        sc.run_cp = (uint32_t *)take(cap * 4);
+        sc.run_amin = (int32_t *)take(cap * 4);
+        sc.run_amax = (int32_t *)take(cap * 4);
+        sc.run_nexit = (uint32_t *)take(cap * 4);
+        sc.run_f = (uint32_t *)take(cap * 4);
+        sc.run_exc = (uint64_t *)take(cap * 8);
+        sc.run_exerr = (uint64_t *)take(cap * 8);
+        sc.run_exrt = (int64_t *)take(cap * 8);
+        sc.run_exmin = (int64_t *)take(cap * 8);
+        sc.run_mode = (uint8_t *)take(cap);
+        sc.flow_first_run = (uint32_t *)take(cap * 4);
+        sc.tile_agg = take(ntiles * sizeof(LAgg));
+        sc.tile_carry = take(ntiles * sizeof(LAgg));
+        sc.tile_valid = (uint32_t *)take(ntiles * 4);
+        sc.counters = (uint32_t *)take(64);
+        sc.radix.hist = (uint32_t *)take(hist * 4);
+        sc.radix.hist_scan = (uint32_t *)take(hist * 4);
+        sc.radix.partial = (uint32_t *)take(scan_partials_needed(hist) * 4 + 64);
+        sc.cap = cap;
+        scratch_cap = cap;
+        d_kind.alloc(cap);
+        d_flags.alloc(cap);
+        d_resid.alloc(cap);
+        d_ts.alloc(cap);
+        d_acq.alloc(cap);
+        d_rt.alloc(cap);
+        d_param.alloc(cap);
+        d_dec.alloc(cap);
+        d_wait.alloc(cap);
+    }
+    int bits = 1;
+    while (((uint64_t)1 << bits) < (uint64_t)nres + 1) ++bits;
+    std::vector<uint32_t> off;
+    std::vector<int64_t> zero_rt;
+    for (size_t b = 0; b < n;) {
+        size_t m = std::min(cap, n - b);
+        int64_t lo = ts[b], hi = ts[b];
+        for (size_t i = 0; i < m; ++i) {
+            const int64_t t = ts[b + i];
+            if (t < 0 || acquire[b + i] < 0) return SGA_EINVAL;
+            const int64_t nlo = std::min(lo, t), nhi = std::max(hi, t);
+            if (nhi - nlo > (int64_t)0xFFFFFFFFLL) {
+                m = i;
+                break;
+            }
+            lo = nlo;
+            hi = nhi;
+        }
+        off.resize(m);
+        for (size_t i = 0; i < m; ++i) off[i] = (uint32_t)(ts[b + i] - lo);
+        SGA_HIP_CHECK(hipMemcpyAsync(d_kind.p, kind + b, m, hipMemcpyHostToDevice, stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(d_resid.p, resource + b, m * 4, hipMemcpyHostToDevice, stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(d_ts.p, off.data(), m * 4, hipMemcpyHostToDevice, stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(d_acq.p, acquire + b, m * 4, hipMemcpyHostToDevice, stream));
+        if (flags) SGA_HIP_CHECK(hipMemcpyAsync(d_flags.p, flags + b, m, hipMemcpyHostToDevice, stream));
+        else SGA_HIP_CHECK(hipMemsetAsync(d_flags.p, 0, m, stream));
+        if (rt) SGA_HIP_CHECK(hipMemcpyAsync(d_rt.p, rt + b, m * 8, hipMemcpyHostToDevice, stream));
+        else SGA_HIP_CHECK(hipMemsetAsync(d_rt.p, 0, m * 8, stream));
+        if (param) SGA_HIP_CHECK(hipMemcpyAsync(d_param.p, param + b, m * 8, hipMemcpyHostToDevice, stream));
+        else SGA_HIP_CHECK(hipMemsetAsync(d_param.p, 0, m * 8, stream));
+        SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, stream));
+        const FlowState st = state();
+        const uint32_t nb = (uint32_t)((m + kT - 1) / kT);
+        hipLaunchKernelGGL(k_lclassify, dim3(nb), dim3(kT), 0, stream, st, d_kind.p, d_resid.p, d_ts.p, lo, d_acq.p,
+                           d_flags.p, (uint32_t)m, sc.keys[0], sc.pay[0], d_dec.p, d_wait.p);
+        const int np = radix_sort_pairs(sc.keys[0], sc.pay[0], sc.keys[1], sc.pay[1], m, bits, sc.radix, stream);
+        const uint32_t *keys = sc.keys[np & 1];
+        const Payload *pay = sc.pay[np & 1];
+        const uint32_t ntiles = (uint32_t)((m + kTileElems - 1) / kTileElems);
+        hipLaunchKernelGGL(k_lruns_up, dim3(ntiles), dim3(kT), 0, stream, keys, pay, (uint32_t)m, nres,
+                           (LAgg *)sc.tile_agg, sc.tile_valid);
+        hipLaunchKernelGGL(k_lruns_tiles, dim3(1), dim3(kT), 0, stream, (const LAgg *)sc.tile_agg, sc.tile_valid, ntiles,
+                           (LAgg *)sc.tile_carry, sc.counters);
+        hipLaunchKernelGGL(k_lruns_down, dim3(ntiles), dim3(kT), 0, stream, keys, pay, d_rt.p, nres,
+                           (const LAgg *)sc.tile_carry, sc);
+        hipLaunchKernelGGL(k_lexits, dim3(ntiles), dim3(kT), 0, stream, pay, d_rt.p, sc);
+        const uint32_t fthreads = (uint32_t)std::min<size_t>(m, nres);
+        hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, stream, st,
+                           (int64_t)cfg.statistic_max_rt, sc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p);
+        hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, stream, sc, pay, d_dec.p);
+        SGA_HIP_CHECK(hipGetLastError());
+        SGA_HIP_CHECK(hipMemcpyAsync(decision + b, d_dec.p, m, hipMemcpyDeviceToHost, stream));
+        if (wait_ms) SGA_HIP_CHECK(hipMemcpyAsync(wait_ms + b, d_wait.p, m * 4, hipMemcpyDeviceToHost, stream));
+        uint32_t ovf = 0;
+        SGA_HIP_CHECK(hipMemcpyAsync(&ovf, d_overflow.p, 4, hipMemcpyDeviceToHost, stream));
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+        if (ovf) return SGA_ENOMEM;  // parameter maps full
+        b += m;
+    }
+    return 0;
+}
+
+int FlowEngine::query(uint32_t r, int64_t now, sga_node_view *out) {
+    if (r >= nres || now < 0 || !out) return SGA_EINVAL;
+    if (!d_view.p) d_view.alloc(16);
+    hipLaunchKernelGGL(k_node_view, dim3(1), dim3(64), 0, stream, state(), (int64_t)cfg.statistic_max_rt, r, now,
+                       (double *)d_view.p, d_view.p + 8);
+    double dv[8];
+    int64_t iv[8];
+    SGA_HIP_CHECK(hipMemcpyAsync(dv, d_view.p, 64, hipMemcpyDeviceToHost, stream));
+    SGA_HIP_CHECK(hipMemcpyAsync(iv, d_view.p + 8, 64, hipMemcpyDeviceToHost, stream));
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    out->pass_qps = dv[0];
+    out->block_qps = dv[1];
+    out->success_qps = dv[2];
+    out->exception_qps = dv[3];
+    out->occupied_pass_qps = dv[4];
+    out->avg_rt = dv[5];
+    out->min_rt = dv[6];
+    out->previous_pass_qps = dv[7];
+    out->total_pass = iv[0];
+    out->total_block = iv[1];
+    out->total_success = iv[2];
+    out->total_exception = iv[3];
+    out->cur_thread_num = iv[4];
+    out->waiting = iv[5];
+    return 0;
+}
+
+int FlowEngine::cb_state(uint32_t r, uint32_t k) {
+    if (r >= nres || k >= h_res[r].n_cbs) return -1;
+    CbDev d;
+    SGA_HIP_CHECK(hipMemcpyAsync(&d, d_cbs.p + h_res[r].cb_off + k, sizeof(CbDev), hipMemcpyDeviceToHost, stream));
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    return d.state;
+}
+
+}  // namespace sga

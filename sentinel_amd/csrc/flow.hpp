@@ -1,13 +1,160 @@
-// Local flow path (StatisticSlot + FlowSlot controllers) -- device engine.
+// Local path (StatisticSlot + ParamFlowSlot + FlowSlot + DegradeSlot) -- device engine.
 #pragma once
 #include "../../include/sentinel_amd.h"
 #include "common.hpp"
+#include "radix_sort.hpp"
+
+#include <vector>
 
 namespace sga {
 
+// ---- node record (one ClusterNode per resource), int64 words -------------------
+// second window: OccupiableBucketLeapArray(2, 1000)  (StatisticNode.java:99-100)
+// borrow window: FutureBucketLeapArray(2, 1000)      (OccupiableBucketLeapArray.java:33-37)
+// minute window: BucketLeapArray(60, 60000)          (StatisticNode.java:106)
+// MetricBucket fields: start, PASS, BLOCK, EXCEPTION, SUCCESS, RT, OCCUPIED_PASS, minRt
+constexpr int kMB = 8;
+enum : int { MB_START = 0, MB_PASS, MB_BLOCK, MB_EXC, MB_SUCC, MB_RT, MB_OPASS, MB_MINRT };
+constexpr int kNodeSec = 0;                       // 2 x 8
+constexpr int kNodeBor = kNodeSec + 2 * kMB;      // 2 x 2 (start, PASS)
+constexpr int kNodeMin = kNodeBor + 4;            // 60 x 8
+constexpr int kNodeThreads = kNodeMin + 60 * kMB; // curThreadNum
+constexpr int kNodeWords = kNodeThreads + 4;      // 504 words = 4032 B (64-B aligned)
+
+struct FlowRuleDev {    // one rater (TrafficShapingController) + its FlowRule fields
+    int32_t behavior, grade;
+    double count;
+    int32_t max_queue, cold_factor;
+    int32_t warning_token, max_token;
+    double slope;
+    int64_t latest_passed;   // RateLimiterController / WarmUpRateLimiterController latestPassedTime
+    int64_t stored_tokens;   // WarmUpController.storedTokens
+    int64_t last_filled;     // WarmUpController.lastFilledTime
+};
+
+struct ParamRuleDev {
+    int32_t grade, behavior;
+    double count;
+    int32_t max_queue, burst;
+    int32_t param_idx, n_hot;
+    int64_t duration;
+    uint32_t hot_off, id;   // id: global param-rule id (hash-table key part)
+};
+
+struct CbDev {
+    int32_t grade, min_req;
+    double count, slow_ratio;
+    int32_t stat_interval, state;   // state: 0 CLOSED, 1 OPEN, 2 HALF_OPEN
+    int64_t recovery_ms, max_allowed_rt, next_retry;
+    int64_t st_start, st_bad, st_total;  // LeapArray(1, statIntervalMs) bucket
+};
+
+struct ResDev {
+    uint32_t rule_off, n_rules;
+    uint32_t prule_off, n_prules;
+    uint32_t cb_off, n_cbs;
+    uint32_t fast;   // bit0: single QPS Default/WarmUp rule, no param rules, no breakers;
+                     // bit1: the resource has a parameter thread-count map (sticky)
+    uint32_t pad;
+};
+
+// (rule, value) -> {time, tokens} for ParameterMetric rule maps; (resource, value) -> thread count
+struct alignas(32) PEntry {
+    uint64_t value;
+    uint32_t owner;   // rule id + 1 (param maps) or resource + 1 (thread counts); 0 = empty
+    uint32_t pad;
+    int64_t a;        // time counter / thread count
+    int64_t b;        // token counter
+};
+constexpr int64_t kPAbsent = INT64_MIN;
+
+struct FlowState {
+    int64_t *node;
+    FlowRuleDev *rules;
+    ParamRuleDev *prules;
+    const uint64_t *hot_v;
+    const int32_t *hot_t;
+    CbDev *cbs;
+    const ResDev *res;
+    PEntry *ptab;      // param time/token maps
+    PEntry *ttab;      // thread-count maps
+    uint32_t pmask, tmask;
+    uint32_t nres;
+    uint32_t *overflow;  // set when a param table is full
+};
+
+struct FlowScratch {
+    uint32_t *keys[2];
+    Payload *pay[2];
+    uint32_t *ev_run, *ev_eidx;
+    uint32_t *run_start, *run_end, *run_slot, *run_t0off, *run_nent, *run_cp;
+    int32_t *run_amin, *run_amax;
+    uint64_t *run_exc, *run_exerr;
+    int64_t *run_exrt, *run_exmin;
+    uint32_t *run_nexit;
+    uint32_t *run_f;
+    uint8_t *run_mode;
+    uint32_t *flow_first_run;
+    void *tile_agg, *tile_carry;
+    uint32_t *tile_valid;
+    uint32_t *counters;
+    RadixScratch radix;
+    size_t cap = 0;
+};
+
 struct FlowEngine {
-    void init(const sga_config &, hipStream_t) {}
+    sga_config cfg{};
+    hipStream_t stream = nullptr;
+    uint32_t nres = 0;
+    DevBuf<int64_t> d_node;
+    DevBuf<FlowRuleDev> d_rules;
+    DevBuf<ParamRuleDev> d_prules;
+    DevBuf<uint64_t> d_hot_v;
+    DevBuf<int32_t> d_hot_t;
+    DevBuf<CbDev> d_cbs;
+    DevBuf<ResDev> d_res;
+    DevBuf<PEntry> d_ptab, d_ttab;
+    DevBuf<uint32_t> d_overflow;
+    DevBuf<uint8_t> d_scratch;
+    FlowScratch sc;
+    size_t scratch_cap = 0;
+    // host mirrors for rule reloads
+    std::vector<FlowRuleDev> h_rules;
+    std::vector<sga_flow_rule> h_flow_src;
+    std::vector<ParamRuleDev> h_prules;
+    std::vector<sga_param_rule> h_prule_src;
+    std::vector<std::vector<uint64_t>> h_prule_hot_v;
+    std::vector<std::vector<int32_t>> h_prule_hot_t;
+    std::vector<CbDev> h_cbs;
+    std::vector<sga_degrade_rule> h_cb_src;
+    std::vector<ResDev> h_res;
+    uint32_t next_prule_id = 0;
+    // staging for host API
+    DevBuf<uint8_t> d_kind, d_flags;
+    DevBuf<uint32_t> d_resid, d_ts;
+    DevBuf<int32_t> d_acq;
+    DevBuf<int64_t> d_rt;
+    DevBuf<uint64_t> d_param;
+    DevBuf<int8_t> d_dec;
+    DevBuf<int32_t> d_wait;
+    DevBuf<int64_t> d_view;
+
+    void init(const sga_config &c, hipStream_t s) {
+        cfg = c;
+        stream = s;
+    }
     void release() {}
+    FlowState state() const;
+    int set_resources(uint32_t n);
+    int load_flow_rules(const sga_flow_rule *r, size_t n);
+    int load_param_rules(const sga_param_rule *r, size_t n);
+    int load_degrade_rules(const sga_degrade_rule *r, size_t n);
+    void upload_res();
+    int submit(const uint8_t *kind, const uint32_t *resource, const int64_t *ts, const int32_t *acquire,
+               const uint8_t *flags, const int64_t *rt, const uint64_t *param, size_t n, int8_t *decision,
+               int32_t *wait_ms);
+    int query(uint32_t resource, int64_t now, sga_node_view *out);
+    int cb_state(uint32_t resource, uint32_t k);
 };
 
 }  // namespace sga

@@ -1,0 +1,261 @@
+"""Host-side mirror of the reference's local (in-process) decision path.
+
+Same names and argument meaning as the Java API the engine replaces:
+  SphU.entry(resource, EntryType, batchCount, args...)  CORE/SphU.java:84-208  -> LocalSentinel.entry / submit
+  Entry.exit(count, args...)                              CORE/Entry.java:86-111  -> Entry.exit
+  Tracer.traceEntry(Throwable, Entry)                     CORE/Tracer.java:86-110 -> Entry.trace_error
+  FlowRuleManager.loadRules       CORE/slots/block/flow/FlowRuleManager.java:125-127
+  ParamFlowRuleManager.loadRules  PF/slots/block/flow/param/ParamFlowRuleManager.java:52
+  DegradeRuleManager.loadRules    CORE/slots/block/degrade/DegradeRuleManager.java:108
+  ClusterNode statistics          CORE/node/StatisticNode.java:185-250 -> LocalSentinel.node
+BlockException subclasses as in CORE/slots/block/BlockException.java and its subclasses.
+
+Every decision is computed by the HIP engine (libsentinel_amd.so).  The mocked
+TimeUtil clock of the reference tests is the explicit `now` / `ts` argument.
+Resources are registered up front (dense ids), like CtSph's chain map keys.
+"""
+import ctypes as C
+import struct
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import SgaDegradeRule, SgaFlowRule, SgaNodeView, SgaParamRule, check
+from .cluster import Engine  # noqa: F401  (one engine serves both paths)
+from .rules import DegradeRule, FlowRule, ParamFlowRule, RuleConstant  # noqa: F401
+
+
+class Decision:
+    PASS = 0
+    BLOCK_FLOW = 1
+    BLOCK_PARAM = 2
+    BLOCK_DEGRADE = 3
+    PASS_WAIT = 4
+
+
+EV_PRIORITIZED = 1
+EV_ERROR = 2
+EV_HAS_PARAM = 4
+KIND_ENTRY = 0
+KIND_EXIT = 1
+
+
+class BlockException(Exception):
+    def __init__(self, resource: str):
+        super().__init__(resource)
+        self.resource = resource
+
+
+class FlowException(BlockException):
+    pass
+
+
+class ParamFlowException(BlockException):
+    pass
+
+
+class DegradeException(BlockException):
+    pass
+
+
+_EXC = {Decision.BLOCK_FLOW: FlowException, Decision.BLOCK_PARAM: ParamFlowException,
+        Decision.BLOCK_DEGRADE: DegradeException}
+
+
+def param_value(x) -> int:
+    """64-bit key of a hot parameter (ParameterMetric maps compare args[idx] by equals()).
+
+    Integral values (Java byte/short/int/long, boolean) map to their two's-complement
+    long bits, floats to their IEEE-754 bits, strings to a 64-bit hash of the UTF-8 bytes
+    (distinct strings that collide would share a counter: documented divergence)."""
+    if isinstance(x, bool):
+        return 1 if x else 0
+    if isinstance(x, (int, np.integer)):
+        return int(x) & 0xFFFFFFFFFFFFFFFF
+    if isinstance(x, (float, np.floating)):
+        return struct.unpack("<Q", struct.pack("<d", float(x)))[0]
+    if isinstance(x, str):
+        import xxhash
+        return xxhash.xxh64_intdigest(x.encode("utf-8"), seed=0x5E47)
+    raise TypeError(f"unsupported parameter type {type(x).__name__}")
+
+
+@dataclass
+class NodeView:
+    pass_qps: float
+    block_qps: float
+    success_qps: float
+    exception_qps: float
+    occupied_pass_qps: float
+    avg_rt: float
+    min_rt: float
+    previous_pass_qps: float
+    total_pass: int
+    total_block: int
+    total_success: int
+    total_exception: int
+    cur_thread_num: int
+    waiting: int
+
+
+class Entry:
+    """A passed entry; exit() records RT / success (StatisticSlot.exit) and breaker completion."""
+
+    def __init__(self, owner: "LocalSentinel", rid: int, create_ts: int, count: int, param: Optional[int],
+                 wait_ms: int):
+        self._owner = owner
+        self.rid = rid
+        self.create_timestamp = create_ts
+        self.count = count
+        self.param = param
+        self.wait_ms = wait_ms
+        self.error = False
+        self.exited = False
+
+    def trace_error(self):
+        self.error = True
+
+    def exit(self, now: int):
+        if self.exited:
+            return
+        self.exited = True
+        fl = (EV_ERROR if self.error else 0) | (EV_HAS_PARAM if self.param is not None else 0)
+        self._owner.submit([KIND_EXIT], [self.rid], [now], [self.count], [fl], [now - self.create_timestamp],
+                           [self.param or 0])
+
+
+class LocalSentinel:
+    """The local slot chain (StatisticSlot, ParamFlowSlot, FlowSlot, DegradeSlot) on one engine."""
+
+    def __init__(self, engine: Engine, resources: Sequence[str]):
+        self.engine = engine
+        self.resources: List[str] = list(resources)
+        self.ids: Dict[str, int] = {r: i for i, r in enumerate(self.resources)}
+        if len(self.ids) != len(self.resources):
+            raise ValueError("duplicate resource names")
+        check(_lib.load().sga_flow_set_resources(engine.handle, len(self.resources)), engine.handle, "setResources")
+
+    def resource_id(self, name: str) -> int:
+        return self.ids[name]
+
+    # ---- batched form: the engine's native interface
+    def submit(self, kind, resource, ts, acquire, flags=None, rt=None, param=None):
+        k = np.ascontiguousarray(kind, dtype=np.uint8)
+        r = np.ascontiguousarray(resource, dtype=np.uint32)
+        t = np.ascontiguousarray(ts, dtype=np.int64)
+        a = np.ascontiguousarray(acquire, dtype=np.int32)
+        n = len(k)
+        if not (len(r) == len(t) == len(a) == n):
+            raise ValueError("event arrays differ in length")
+        f = np.ascontiguousarray(flags, dtype=np.uint8) if flags is not None else None
+        rtv = np.ascontiguousarray(rt, dtype=np.int64) if rt is not None else None
+        pv = np.ascontiguousarray(param, dtype=np.uint64) if param is not None else None
+        for x in (f, rtv, pv):
+            if x is not None and len(x) != n:
+                raise ValueError("event arrays differ in length")
+        dec = np.zeros(n, dtype=np.int8)
+        wait = np.zeros(n, dtype=np.int32)
+        rc = _lib.load().sga_submit_events(
+            self.engine.handle, k.ctypes.data, r.ctypes.data, t.ctypes.data, a.ctypes.data,
+            f.ctypes.data if f is not None else None, rtv.ctypes.data if rtv is not None else None,
+            pv.ctypes.data if pv is not None else None, n, dec.ctypes.data, wait.ctypes.data)
+        check(rc, self.engine.handle, "submitEvents")
+        return dec, wait
+
+    # ---- SphU-style single entry
+    def entry(self, resource: str, now: int, batch_count: int = 1, prioritized: bool = False, args=()) -> Entry:
+        rid = self.ids[resource]
+        param = param_value(args[0]) if len(args) > 0 else None
+        fl = (EV_PRIORITIZED if prioritized else 0) | (EV_HAS_PARAM if param is not None else 0)
+        dec, wait = self.submit([KIND_ENTRY], [rid], [now], [batch_count], [fl], None, [param or 0])
+        d = int(dec[0])
+        if d in _EXC:
+            raise _EXC[d](resource)
+        return Entry(self, rid, now, batch_count, param, int(wait[0]))
+
+    def node(self, resource, now: int) -> NodeView:
+        rid = resource if isinstance(resource, int) else self.ids[resource]
+        v = SgaNodeView()
+        check(_lib.load().sga_query_node(self.engine.handle, rid, now, C.byref(v)), self.engine.handle, "node")
+        return NodeView(*[getattr(v, f) for f, _ in SgaNodeView._fields_])
+
+    def circuit_breaker_state(self, resource, k: int = 0) -> int:
+        rid = resource if isinstance(resource, int) else self.ids[resource]
+        return _lib.load().sga_circuit_breaker_state(self.engine.handle, rid, k)
+
+
+class FlowRuleManager:
+    def __init__(self, sentinel: LocalSentinel):
+        self.s = sentinel
+
+    def load_rules(self, rules: List[FlowRule]) -> int:
+        rules = [r for r in rules if not r.cluster_mode and r.resource in self.s.ids]
+        arr = (SgaFlowRule * max(1, len(rules)))()
+        for i, r in enumerate(rules):
+            a = arr[i]
+            a.resource = self.s.ids[r.resource]
+            a.grade = r.grade
+            a.count = r.count
+            a.control_behavior = r.control_behavior
+            a.warm_up_period_sec = r.warm_up_period_sec
+            a.max_queueing_time_ms = r.max_queueing_time_ms
+            # non-default limitApp / RELATE / CHAIN are not served by the engine: rejected as invalid
+            a.strategy = r.strategy if r.limit_app == RuleConstant.LIMIT_APP_DEFAULT else -1
+        return check(_lib.load().sga_load_flow_rules(self.s.engine.handle, arr, len(rules)), self.s.engine.handle,
+                     "FlowRuleManager.loadRules")
+
+
+class ParamFlowRuleManager:
+    def __init__(self, sentinel: LocalSentinel):
+        self.s = sentinel
+        self._keep = []
+
+    def load_rules(self, rules: List[ParamFlowRule]) -> int:
+        rules = [r for r in rules if r.resource in self.s.ids]
+        arr = (SgaParamRule * max(1, len(rules)))()
+        keep = []
+        for i, r in enumerate(rules):
+            a = arr[i]
+            a.resource = self.s.ids[r.resource]
+            a.grade = r.grade
+            a.count = r.count
+            a.control_behavior = r.control_behavior
+            a.max_queueing_time_ms = r.max_queueing_time_ms
+            a.burst_count = r.burst_count
+            a.param_idx = r.param_idx
+            a.duration_in_sec = r.duration_in_sec
+            # ParamFlowRuleUtil.parseHotItems: later items with the same value win
+            hot: Dict[int, int] = {}
+            for it in r.param_flow_item_list:
+                hot[param_value(it.object)] = int(it.count)
+            hv = (C.c_uint64 * max(1, len(hot)))(*hot.keys())
+            ht = (C.c_int32 * max(1, len(hot)))(*hot.values())
+            keep += [hv, ht]
+            a.n_hot = len(hot)
+            a.hot_values = C.cast(hv, C.POINTER(C.c_uint64))
+            a.hot_thresholds = C.cast(ht, C.POINTER(C.c_int32))
+        rc = _lib.load().sga_load_param_rules(self.s.engine.handle, arr, len(rules))
+        self._keep = keep
+        return check(rc, self.s.engine.handle, "ParamFlowRuleManager.loadRules")
+
+
+class DegradeRuleManager:
+    def __init__(self, sentinel: LocalSentinel):
+        self.s = sentinel
+
+    def load_rules(self, rules: List[DegradeRule]) -> int:
+        rules = [r for r in rules if r.resource in self.s.ids]
+        arr = (SgaDegradeRule * max(1, len(rules)))()
+        for i, r in enumerate(rules):
+            a = arr[i]
+            a.resource = self.s.ids[r.resource]
+            a.grade = r.grade
+            a.count = r.count
+            a.time_window = r.time_window
+            a.min_request_amount = r.min_request_amount
+            a.slow_ratio_threshold = r.slow_ratio_threshold
+            a.stat_interval_ms = r.stat_interval_ms
+        return check(_lib.load().sga_load_degrade_rules(self.s.engine.handle, arr, len(rules)), self.s.engine.handle,
+                     "DegradeRuleManager.loadRules")

@@ -56,6 +56,33 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.SgaConfig) == 40
 
 
+_STRUCTS = {"SgaConfig": "sga_config", "SgaClusterFlowRule": "sga_cluster_flow_rule",
+            "SgaTokenResult": "sga_token_result", "SgaFlowRule": "sga_flow_rule", "SgaParamRule": "sga_param_rule",
+            "SgaDegradeRule": "sga_degrade_rule", "SgaNodeView": "sga_node_view"}
+
+
+def test_every_field_offset_matches_the_c_compiler(tmp_path):
+    """sizeof / offsetof of every ABI struct as gcc lays it out == the ctypes mirror."""
+    from sentinel_amd import _lib
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sentinel_amd.h"', "int main(void) {"]
+    expect = []
+    for py, c in _STRUCTS.items():
+        cls = getattr(_lib, py)
+        lines.append(f'printf("%zu\\n", sizeof({c}));')
+        expect.append(ctypes.sizeof(cls))
+        for f, _ in cls._fields_:
+            lines.append(f'printf("%zu\\n", offsetof({c}, {f}));')
+            expect.append(getattr(cls, f).offset)
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    import subprocess
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert got == expect
+
+
 def test_create_without_gpu_fails_loudly():
     """No GPU here: engine creation must fail with an error code, never fall back to a CPU path."""
     from sentinel_amd import _lib

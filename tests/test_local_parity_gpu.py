@@ -1,0 +1,281 @@
+"""GPU parity of the local path (StatisticSlot + ParamFlowSlot + FlowSlot + DegradeSlot)
+against the oracle, through the C-ABI (sga_submit_events / sga_query_node).
+
+Bar: decisions, wait times, node statistics and breaker states bit-identical to the
+oracle replay of the same stream (all integer state; derived doubles are computed
+from the same integers with the same operations, so they compare exactly too).
+"""
+import numpy as np
+import pytest
+
+from tests import local_trace as lt
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1_700_000_000_000
+
+
+def _engine(max_batch=1 << 16):
+    from sentinel_amd.cluster import Engine
+    return Engine(max_batch=max_batch)
+
+
+def _sentinel(n_res, max_batch=1 << 16):
+    from sentinel_amd.local import LocalSentinel
+    eng = _engine(max_batch)
+    return eng, LocalSentinel(eng, [f"r{i}" for i in range(n_res)])
+
+
+def _load(s, flow=None, param=None, degrade=None):
+    from sentinel_amd.local import DegradeRuleManager, FlowRuleManager, ParamFlowRuleManager
+    from sentinel_amd.rules import DegradeRule, FlowRule, ParamFlowItem, ParamFlowRule
+    if flow is not None:
+        FlowRuleManager(s).load_rules([FlowRule(resource=f"r{r['resource']}", count=r["count"], grade=r.get("grade", 1),
+                                                control_behavior=r.get("control_behavior", 0),
+                                                warm_up_period_sec=r.get("warm_up_period_sec", 10),
+                                                max_queueing_time_ms=r.get("max_queueing_time_ms", 500))
+                                       for r in flow])
+    if param is not None:
+        ParamFlowRuleManager(s).load_rules([
+            ParamFlowRule(resource=f"r{r['resource']}", grade=r.get("grade", 1), count=r["count"],
+                          param_idx=r.get("param_idx", 0), control_behavior=r.get("control_behavior", 0),
+                          max_queueing_time_ms=r.get("max_queueing_time_ms", 0), burst_count=r.get("burst_count", 0),
+                          duration_in_sec=r.get("duration_in_sec", 1),
+                          param_flow_item_list=[ParamFlowItem(int(k), int(v)) for k, v in r.get("hot", {}).items()])
+            for r in param])
+    if degrade is not None:
+        DegradeRuleManager(s).load_rules([
+            DegradeRule(resource=f"r{r['resource']}", grade=r.get("grade", 0), count=r["count"],
+                        time_window=r.get("time_window", 1), min_request_amount=r.get("min_request_amount", 5),
+                        slow_ratio_threshold=r.get("slow_ratio_threshold", 1.0),
+                        stat_interval_ms=r.get("stat_interval_ms", 1000))
+            for r in degrade])
+
+
+def _submit(s, st):
+    return s.submit(st["kind"], st["resource"], st["ts"], st["acquire"], st["flags"], st["rt"], st["param"])
+
+
+def _assert_same(st, got, exp, what=""):
+    gd, gw = got
+    ed, ew = exp
+    bad = np.nonzero((gd != ed) | (gw != ew))[0]
+    if len(bad):
+        i = bad[0]
+        raise AssertionError(f"{what}: {len(bad)} of {len(gd)} events differ; first at {i}: kind={st['kind'][i]} "
+                             f"res={st['resource'][i]} ts={st['ts'][i]} acq={st['acquire'][i]} "
+                             f"flags={st['flags'][i]} gpu=({gd[i]},{gw[i]}) oracle=({ed[i]},{ew[i]})")
+
+
+def _assert_nodes(s, orc, n_res, now):
+    for rid in range(n_res):
+        v = s.node(rid, now)
+        got = [getattr(v, g) for g in lt.NODE_GETTERS]
+        exp = orc.node(rid, now)
+        assert got == exp, (rid, list(zip(lt.NODE_GETTERS, got, exp)))
+
+
+def _run(n_res, flow=(), param=(), degrade=(), max_batch=1 << 16, **gen_kw):
+    gen = lt.Oracle(n_res, flow, param, degrade)
+    st = lt.generate(gen, n_res, t0=T0, **gen_kw)
+    gen.close()
+    orc = lt.Oracle(n_res, flow, param, degrade)
+    exp = orc.replay(st)
+    eng, s = _sentinel(n_res, max_batch)
+    _load(s, list(flow), list(param), list(degrade))
+    got = _submit(s, st)
+    _assert_same(st, got, exp, "decisions")
+    t_end = int(st["ts"].max())
+    _assert_nodes(s, orc, n_res, t_end)
+    for rid in range(n_res):
+        for k in range(4):
+            assert s.circuit_breaker_state(rid, k) == orc.cb_state(rid, k), (rid, k)
+    orc.close()
+    eng.close()
+    return st, exp
+
+
+def test_hello_world_20_qps():
+    # README quick start: FlowRule(count=20, QPS) and one entry per ms
+    st, (d, _) = _run(1, flow=[{"resource": 0, "count": 20}], n_entries=3000, seed=1, gap_mean=1.0, rt_max=5)
+    assert (d[st["kind"] == 0] == 0).sum() > 0
+
+
+def _random_flow_rules(rng, n_res, thread_ok=True):
+    rules = []
+    for r in range(n_res):
+        k = rng.integers(0, 7)
+        nr = 2 if rng.random() < 0.15 else 1
+        for _ in range(nr):
+            if k == 0 and thread_ok:
+                rules.append({"resource": r, "grade": 0, "count": int(rng.integers(1, 6))})
+            elif k in (1, 2):
+                rules.append({"resource": r, "count": float(rng.choice([5, 10, 20.5, 100]))})
+            elif k == 3:
+                rules.append({"resource": r, "count": float(rng.choice([10, 50])), "control_behavior": 1,
+                              "warm_up_period_sec": int(rng.integers(1, 5))})
+            elif k == 4:
+                rules.append({"resource": r, "count": float(rng.choice([5, 20, 333])), "control_behavior": 2,
+                              "max_queueing_time_ms": int(rng.choice([20, 500]))})
+            elif k == 5:
+                rules.append({"resource": r, "count": float(rng.choice([10, 40])), "control_behavior": 3,
+                              "warm_up_period_sec": 2, "max_queueing_time_ms": 300})
+            # k == 6: no rule
+    return rules
+
+
+@pytest.mark.parametrize("seed,max_batch", [(11, 1 << 16), (12, 4096), (13, 1000)])
+def test_mixed_controllers(seed, max_batch):
+    rng = np.random.default_rng(seed)
+    n_res = 40
+    flow = _random_flow_rules(rng, n_res)
+    _run(n_res, flow=flow, max_batch=max_batch, n_entries=15000, seed=seed, gap_mean=0.4, prio_pct=0.15,
+         acq_max=3, err_pct=0.1, rt_max=40, regress_pct=0.01)
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_param_flow(seed):
+    rng = np.random.default_rng(seed)
+    n_res = 12
+    param = []
+    for r in range(n_res):
+        kind = r % 6
+        if kind == 0:
+            param.append({"resource": r, "count": 5, "burst_count": int(rng.integers(0, 4))})
+        elif kind == 1:
+            param.append({"resource": r, "count": 3, "duration_in_sec": 2, "hot": {1: 10, 2: 0}})
+        elif kind == 2:
+            param.append({"resource": r, "count": 4, "control_behavior": 2, "max_queueing_time_ms": 200})
+        elif kind == 3:
+            param.append({"resource": r, "grade": 0, "count": 2, "hot": {0: 4}})
+        elif kind == 4:
+            param.append({"resource": r, "count": 6, "param_idx": -1})
+            param.append({"resource": r, "count": 1, "param_idx": 1})  # args.length <= idx: skipped
+    flow = [{"resource": r, "count": 30} for r in range(0, n_res, 3)]
+    _run(n_res, flow=flow, param=param, n_entries=12000, seed=seed, gap_mean=0.5, acq_max=2, rt_max=30,
+         params=5, prio_pct=0.05)
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_circuit_breakers(seed):
+    n_res = 9
+    degrade = []
+    for r in range(n_res):
+        g = r % 3
+        if g == 0:
+            degrade.append({"resource": r, "grade": 0, "count": 20, "time_window": 1, "slow_ratio_threshold": 0.4,
+                            "min_request_amount": 3, "stat_interval_ms": 1000})
+        elif g == 1:
+            degrade.append({"resource": r, "grade": 1, "count": 0.3, "time_window": 2, "min_request_amount": 4,
+                            "stat_interval_ms": 500})
+        else:
+            degrade.append({"resource": r, "grade": 2, "count": 3, "time_window": 1, "stat_interval_ms": 2000})
+            degrade.append({"resource": r, "grade": 0, "count": 100, "time_window": 3, "slow_ratio_threshold": 1.0})
+    flow = [{"resource": 0, "count": 50}, {"resource": 4, "grade": 0, "count": 3}]
+    _run(n_res, flow=flow, degrade=degrade, n_entries=10000, seed=seed, gap_mean=0.7, err_pct=0.35, rt_max=60)
+
+
+def test_rule_reload_between_batches():
+    n_res = 10
+    rng = np.random.default_rng(5)
+    flow1 = _random_flow_rules(rng, n_res)
+    flow2 = _random_flow_rules(rng, n_res)
+    deg1 = [{"resource": r, "grade": 2, "count": 2, "time_window": 1} for r in range(n_res)]
+    deg2 = deg1[:5] + [{"resource": r, "grade": 1, "count": 0.5, "time_window": 1} for r in range(5, n_res)]
+    par1 = [{"resource": r, "count": 3} for r in range(n_res)]
+    par2 = par1[::2] + [{"resource": r, "count": 4, "burst_count": 1} for r in range(1, n_res, 2)]
+    gen = lt.Oracle(n_res, flow1, par1, deg1)
+    s1 = lt.generate(gen, n_res, 4000, 1, T0, gap_mean=0.5, err_pct=0.3, rt_max=20, params=4)
+    gen.load(flow2, par2, deg2)
+    s2 = lt.generate(gen, n_res, 4000, 2, T0, gap_mean=0.5, err_pct=0.3, rt_max=20, params=4,
+                     t_start=int(s1["ts"].max()) + 1)
+    gen.close()
+    orc = lt.Oracle(n_res, flow1, par1, deg1)
+    eng, s = _sentinel(n_res)
+    _load(s, flow1, par1, deg1)
+    _assert_same(s1, _submit(s, s1), orc.replay(s1), "before reload")
+    orc.load(flow2, par2, deg2)
+    _load(s, flow2, par2, deg2)
+    _assert_same(s2, _submit(s, s2), orc.replay(s2), "after reload")
+    _assert_nodes(s, orc, n_res, int(s2["ts"].max()))
+    orc.close()
+    eng.close()
+
+
+def _fast_path_stream(n_res, n, seed, rate_per_ms):
+    """QPS Default / WarmUp rules only: exits never change a decision, so exits of
+    the passed entries can be added after an entries-only oracle replay."""
+    rng = np.random.default_rng(seed)
+    w = 1.0 / np.arange(1, n_res + 1) ** 1.1
+    w /= w.sum()
+    res = rng.choice(n_res, size=n, p=w).astype(np.uint32)
+    ts = T0 + np.sort(rng.integers(0, int(n / rate_per_ms), size=n)).astype(np.int64)
+    ent = {"kind": np.zeros(n, np.uint8), "resource": res, "ts": ts, "acquire": np.ones(n, np.int32),
+           "flags": np.zeros(n, np.uint8), "rt": np.zeros(n, np.int64), "param": np.zeros(n, np.uint64)}
+    return ent, rng
+
+
+def test_fast_path_large_stream():
+    n_res, n = 4096, 1 << 20
+    rng0 = np.random.default_rng(3)
+    flow = []
+    for r in range(n_res):
+        if r % 5 == 4:
+            flow.append({"resource": r, "count": float(rng0.integers(5, 200)), "control_behavior": 1,
+                         "warm_up_period_sec": int(rng0.integers(1, 4))})
+        elif r % 7 != 6:
+            flow.append({"resource": r, "count": float(rng0.integers(1, 500))})
+    ent, rng = _fast_path_stream(n_res, n, 3, rate_per_ms=200)
+    o1 = lt.Oracle(n_res, flow)
+    d, _ = o1.replay(ent)
+    o1.close()
+    passed = np.nonzero(d == 0)[0]
+    rt = rng.integers(0, 80, size=len(passed))
+    ex = {"kind": np.ones(len(passed), np.uint8), "resource": ent["resource"][passed],
+          "ts": ent["ts"][passed] + rt, "acquire": np.ones(len(passed), np.int32),
+          "flags": (rng.random(len(passed)) < 0.1).astype(np.uint8) * 2, "rt": rt.astype(np.int64),
+          "param": np.zeros(len(passed), np.uint64)}
+    st = lt.concat(ent, ex)
+    order = np.lexsort((st["kind"], st["ts"]))
+    st = {k: v[order] for k, v in st.items()}
+    orc = lt.Oracle(n_res, flow)
+    exp = orc.replay(st)
+    eng, s = _sentinel(n_res, max_batch=1 << 20)
+    _load(s, flow)
+    got = _submit(s, st)
+    _assert_same(st, got, exp, "fast path")
+    now = int(st["ts"].max())
+    for rid in list(range(64)) + list(range(n_res - 64, n_res)):
+        v = s.node(rid, now)
+        assert [getattr(v, g) for g in lt.NODE_GETTERS] == orc.node(rid, now), rid
+    orc.close()
+    eng.close()
+
+
+def test_edge_cases():
+    from sentinel_amd import EngineError
+    eng, s = _sentinel(3)
+    _load(s, [{"resource": 0, "count": 1}])
+    d, w = s.submit([], [], [], [])
+    assert len(d) == 0
+    # unknown resource id: no node, no rules -> pass
+    d, w = s.submit([0, 0], [7, 0], [T0, T0], [1, 1])
+    assert list(d) == [0, 0]
+    d, w = s.submit([0], [0], [T0 + 1], [1])
+    assert list(d) == [1]
+    with pytest.raises(EngineError):
+        s.submit([0], [0], [T0], [-1])
+    with pytest.raises(EngineError):
+        s.submit([0], [0], [-5], [1])
+    # SphU-style API
+    from sentinel_amd.local import FlowException
+    e = None
+    with pytest.raises(FlowException):
+        e = s.entry("r0", T0 + 2)
+    assert e is None
+    ok = s.entry("r1", T0 + 2)
+    ok.trace_error()
+    ok.exit(T0 + 9)
+    v = s.node("r1", T0 + 9)
+    assert v.total_exception == 1 and v.total_success == 1 and v.avg_rt == 7.0 and v.cur_thread_num == 0
+    eng.close()
