@@ -134,6 +134,37 @@ class ClusterFlowRuleManager:
         check(_lib.load().sga_set_connected_count(self.engine.handle, namespace.encode(), n), self.engine.handle)
 
 
+class GlobalRequestLimiter:
+    """CS/flow/statistic/limit/GlobalRequestLimiter.java:30-80 mirror (per-namespace QPS guard that
+    ClusterFlowChecker.allowProceed consults before a rule's metric)."""
+
+    DEFAULT_MAX_ALLOWED_QPS = 30000.0  # ServerFlowConfig.DEFAULT_MAX_ALLOWED_QPS
+
+    def __init__(self, engine: Engine):
+        self.engine = engine
+        self.limits = {}
+
+    def init_if_absent(self, namespace: str, max_allowed_qps: float = DEFAULT_MAX_ALLOWED_QPS):
+        if not namespace:
+            raise ValueError("namespace cannot be empty")
+        if namespace in self.limits:
+            return
+        check(_lib.load().sga_set_namespace_limit(self.engine.handle, namespace.encode(), float(max_allowed_qps)),
+              self.engine.handle, "initIfAbsent")
+        self.limits[namespace] = float(max_allowed_qps)
+
+    def apply_max_qps_change(self, max_allowed_qps: float):
+        if not max_allowed_qps >= 0:
+            raise ValueError("max allowed QPS should > 0")
+        for ns in self.limits:
+            check(_lib.load().sga_set_namespace_limit(self.engine.handle, ns.encode(), float(max_allowed_qps)),
+                  self.engine.handle, "applyMaxQpsChange")
+            self.limits[ns] = float(max_allowed_qps)
+
+    def get_max_allowed_qps(self, namespace: str) -> float:
+        return self.limits.get(namespace, 0.0)
+
+
 TOKEN_DTYPE = np.dtype([("remaining", "<i4"), ("wait_in_ms", "<i2"), ("status", "i1"), ("reserved", "i1")])
 
 

@@ -22,6 +22,8 @@
 //   5 results   : every event derives its TokenResult from its run record.
 #include "cluster.hpp"
 
+#include <cstdlib>
+
 #include <algorithm>
 
 namespace sga {
@@ -52,6 +54,10 @@ __device__ __forceinline__ HashEntry slot_lookup(const ClusterState &st, int64_t
 }
 
 // ---------------------------------------------------------------- classify
+// kClassifyItems requests per thread (strided by the block size, so every load stays coalesced);
+// the first hash probes of all of them are issued before any is resolved.
+constexpr int kClassifyItems = 4;
+
 __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const int64_t *__restrict__ flow_id,
                                                        const int32_t *__restrict__ acquire,
                                                        const uint8_t *__restrict__ prio,
@@ -59,26 +65,49 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
                                                        uint32_t n, int simple, uint32_t invalid_key, uint32_t *__restrict__ keys,
                                                        Payload *__restrict__ pay, uint64_t *__restrict__ out,
                                                        uint32_t *__restrict__ counters) {
-    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
-    bool valid = false;
-    if (i < n) {
-        const int64_t fid = flow_id[i];
-        const int32_t a = acquire[i];
+    const uint32_t base = blockIdx.x * (kThreads * kClassifyItems) + threadIdx.x;
+    int64_t fid[kClassifyItems];
+    int32_t acq[kClassifyItems];
+    uint32_t h[kClassifyItems];
+    HashEntry e[kClassifyItems];
+#pragma unroll
+    for (int u = 0; u < kClassifyItems; ++u) {
+        const uint32_t i = base + u * kThreads;
+        fid[u] = i < n ? flow_id[i] : 0;
+        acq[u] = i < n ? acquire[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kClassifyItems; ++u) {
+        h[u] = (uint32_t)hash_flow_id(fid[u]) & st.hmask;
+        e[u] = fid[u] > 0 ? st.htab[h[u]] : HashEntry{0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < kClassifyItems; ++u) {
+        const uint32_t i = base + u * kThreads;
+        if (i >= n) continue;
+        const int64_t f = fid[u];
+        const int32_t a = acq[u];
         int8_t status = TRS_OK;
-        HashEntry he{0, 0, 0};
-        if (!simple && (fid <= 0 || a <= 0)) {
+        HashEntry he = e[u];
+        if (!simple && (f <= 0 || a <= 0)) {
             status = TRS_BAD_REQUEST;  // DefaultTokenService.notValidRequest, :87-89
         } else {
             // ClusterFlowRuleManager.getFlowRuleById: validId(id > 0) && FLOW_RULES.get(id)
-            if (fid > 0) he = slot_lookup(st, fid);
-            if (he.key != fid || fid <= 0) status = TRS_NO_RULE_EXISTS;
+            if (f > 0 && he.key != f && he.key != 0) {  // continue the linear probe
+                uint32_t hh = h[u];
+                for (uint32_t probe = 1; probe <= st.hmask; ++probe) {
+                    hh = (hh + 1) & st.hmask;
+                    he = st.htab[hh];
+                    if (he.key == f || he.key == 0) break;
+                }
+            }
+            if (he.key != f || f <= 0) status = TRS_NO_RULE_EXISTS;
         }
         if (status != TRS_OK) {
             out[i] = pack_result(status, 0, 0);
             keys[i] = invalid_key;
             pay[i] = Payload{i, 0u, 0u, 0u};
         } else {
-            valid = true;
             keys[i] = he.slot;
             const uint32_t p = (!simple && prio && prio[i]) ? 0x80000000u : 0u;
             const uint32_t off = ts_off[i];
@@ -86,7 +115,6 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
             pay[i] = Payload{i, off, (uint32_t)a | p, (uint32_t)(t / (int64_t)he.W)};
         }
     }
-    (void)valid;
     (void)counters;  // the valid count is derived after the sort (invalid keys sort last)
 }
 
@@ -496,28 +524,42 @@ __device__ __forceinline__ bool pass_cond(double thr, double isec, int64_t sum, 
     return thr - (double)sum / isec - (double)a >= 0;
 }
 
-// One 16-lane group per rule; lanes load the record's start/PASS/WAITING vectors
-// in parallel, lane 0 of the group resolves the runs.
-constexpr int kGroup = 16;
-
+// G lanes per rule: lanes load the record's start/PASS/WAITING vectors in parallel, lane 0
+// of the group resolves the runs.  G = 1 (one rule per lane) keeps the most rules in flight.
+template <int G>
 __device__ __forceinline__ int64_t group_sum(int64_t v) {
 #pragma unroll
-    for (int o = kGroup / 2; o > 0; o >>= 1) {
-        const int lo = __shfl_xor((int)(uint32_t)v, o, kGroup);
-        const int hi = __shfl_xor((int)(uint32_t)((uint64_t)v >> 32), o, kGroup);
+    for (int o = G / 2; o > 0; o >>= 1) {
+        const int lo = __shfl_xor((int)(uint32_t)v, o, G);
+        const int hi = __shfl_xor((int)(uint32_t)((uint64_t)v >> 32), o, G);
         v += (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
     }
     return v;
 }
 
+// First k in [0, n] with !pass_cond(s0 + k*a): a closed-form guess corrected against the
+// exact predicate (monotone in k), so the result equals the sequential one.
+__device__ __forceinline__ uint32_t pass_prefix(double thr, double isec, int64_t s0, int32_t a, uint32_t n) {
+    if (n == 0) return 0;
+    if (a <= 0) return pass_cond(thr, isec, s0, a) ? n : 0u;
+    const double g = floor(((thr - (double)a) * isec - (double)s0) / (double)a) + 1.0;
+    uint32_t k = 0;
+    if (g >= (double)n) k = n;
+    else if (g > 0) k = (uint32_t)g;
+    while (k > 0 && !pass_cond(thr, isec, s0 + (int64_t)(k - 1) * a, a)) --k;
+    while (k < n && pass_cond(thr, isec, s0 + (int64_t)k * a, a)) ++k;
+    return k;
+}
+
+template <int G>
 __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratch sc, const Payload *__restrict__ pay,
                                                     int64_t ts_base, int simple, uint64_t *__restrict__ out) {
     const uint32_t nflows = sc.counters[2];
     const uint32_t nruns = sc.counters[1];
-    const int gl = threadIdx.x & (kGroup - 1);
-    const uint32_t groups_per_block = kThreads / kGroup;
+    const int gl = threadIdx.x & (G - 1);
+    const uint32_t groups_per_block = kThreads / G;
     const uint32_t stride = gridDim.x * groups_per_block;
-    for (uint32_t fl = blockIdx.x * groups_per_block + threadIdx.x / kGroup; fl < nflows; fl += stride) {
+    for (uint32_t fl = blockIdx.x * groups_per_block + threadIdx.x / G; fl < nflows; fl += stride) {
         const uint32_t r0 = sc.flow_first_run[fl];
         const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
         for (uint32_t r = r0; r < r1; ++r) {
@@ -553,15 +595,15 @@ __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratc
             // ---- window sums over the valid buckets other than the current one (rotation of the
             //      current bucket does not touch them); lanes split the buckets
             int64_t bp = 0, bw = 0;
-            for (int jj = gl; jj < P.S; jj += kGroup) {
+            for (int jj = gl; jj < P.S; jj += G) {
                 const int64_t w = R.start(jj);
                 if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
                     bp += R.cnt(CEV_PASS, jj);
                     bw += R.cnt(CEV_WAITING, jj);
                 }
             }
-            const int64_t base_pass = group_sum(bp);
-            const int64_t base_wait = group_sum(bw);
+            const int64_t base_pass = group_sum<G>(bp);
+            const int64_t base_wait = group_sum<G>(bw);
             if (gl != 0) continue;
             // ---- lane 0: rotate the current window (LeapArray.currentWindow(t0)), then resolve
             cur_window(st, P, s, t0);
@@ -569,13 +611,7 @@ __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratc
             const int64_t s0 = base_pass + R.cnt(CEV_PASS, cj);
             const int64_t w0 = base_wait + R.cnt(CEV_WAITING, cj);
             // pass prefix: first i with !cond(s0 + i*a, a)   (monotone in i)
-            uint32_t lo = 0, hi = n;
-            while (lo < hi) {
-                const uint32_t mid = lo + ((hi - lo) >> 1);
-                if (pass_cond(thr, P.isec, s0 + (int64_t)mid * a, a)) lo = mid + 1;
-                else hi = mid;
-            }
-            const uint32_t f = lo;
+            const uint32_t f = pass_prefix(thr, P.isec, s0, a, n);
             const uint32_t cpf = (f >= n) ? cp_tot : (cp_tot ? sc.ev_cp[j0 + f] : 0u);
             const uint32_t np_after = cp_tot - cpf;
             // occupied prefix among prioritized blocked requests (monotone in the count)
@@ -669,6 +705,128 @@ __global__ void k_init_slots(ClusterState st, const uint32_t *slots, uint32_t n)
     st.occ[s] = SlotOcc{0, 0, 0, 0};
 }
 
+
+// ---------------------------------------------------------------- namespace limiter (K9)
+// ClusterFlowChecker.allowProceed -> GlobalRequestLimiter.tryPass(namespace) runs before the
+// rule's metric is touched (CS/flow/ClusterFlowChecker.java:50-60), for every valid request
+// whose rule lives in a limited namespace, in arrival order.  The limiter depends only on that
+// arrival stream, so it is resolved as a pre-pass: the namespace's requests are compacted in
+// arrival order and cut into runs of one 100 ms limiter bucket.  Inside a run the other nine
+// buckets are fixed (the run rotates only its own bucket), so the passes of a run are a prefix
+// whose length is found by binary search over the exact predicate
+//   sum / 1.0 + 1 <= qpsAllowed     (RequestLimiter.canPass, :70-72)
+// One thread walks the runs in order; rejected requests get TOO_MANY_REQUEST and leave the batch.
+constexpr int kLimW = 100, kLimN = 10, kLimInterval = 1000;
+
+__global__ __launch_bounds__(kThreads) void k_lim_flag(ClusterState st, const uint32_t *__restrict__ keys, uint32_t n,
+                                                       uint32_t invalid, int32_t ns, uint32_t *__restrict__ flag) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = keys[i];
+    flag[i] = (k != invalid && st.param[k].ns == ns) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kThreads) void k_lim_compact(const uint32_t *__restrict__ flag,
+                                                          const uint32_t *__restrict__ pos, uint32_t n,
+                                                          uint32_t *__restrict__ list, uint32_t *counters) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    if (flag[i]) list[pos[i]] = i;
+    if (i == n - 1) counters[4] = pos[i] + flag[i];
+}
+
+__global__ __launch_bounds__(kThreads) void k_lim_heads(const uint32_t *__restrict__ list,
+                                                        const uint32_t *__restrict__ ts_off, int64_t ts_base,
+                                                        uint32_t n, const uint32_t *counters,
+                                                        uint32_t *__restrict__ head) {
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t m = counters[4];
+    uint32_t h = 0;
+    if (j < m) {
+        const int64_t b = (ts_base + (int64_t)ts_off[list[j]]) / kLimW;
+        h = (j == 0 || b != (ts_base + (int64_t)ts_off[list[j - 1]]) / kLimW) ? 1u : 0u;
+    }
+    head[j] = h;
+}
+
+__global__ __launch_bounds__(kThreads) void k_lim_starts(const uint32_t *__restrict__ head,
+                                                         const uint32_t *__restrict__ ridx, uint32_t n,
+                                                         uint32_t *counters, uint32_t *__restrict__ rstart) {
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    const uint32_t m = counters[4];
+    if (j >= m || j >= n) return;
+    if (head[j]) rstart[ridx[j]] = j;
+    if (j == m - 1) counters[5] = ridx[j] + head[j];
+}
+
+__global__ void k_lim_walk(NsLimiterDev *L, double qps_allowed, const uint32_t *__restrict__ list,
+                           const uint32_t *__restrict__ rstart, const uint32_t *counters,
+                           const uint32_t *__restrict__ ts_off, int64_t ts_base, uint32_t *__restrict__ rpass) {
+    if (threadIdx.x || blockIdx.x) return;
+    const uint32_t m = counters[4], R = counters[5];
+    for (uint32_t r = 0; r < R && m; ++r) {
+        const uint32_t j0 = rstart[r], j1 = r + 1 < R ? rstart[r + 1] : m;
+        const int64_t nr = (int64_t)(j1 - j0);
+        const int64_t t = ts_base + (int64_t)ts_off[list[j0]];
+        const int idx = (int)((t / kLimW) % kLimN);
+        const int64_t ws = t - t % kLimW;
+        bool detached = false;
+        if (L->start[idx] == kAbsent || ws > L->start[idx]) {  // new bucket / resetWindowTo
+            L->start[idx] = ws;
+            L->cnt[idx] = 0;
+        } else if (ws < L->start[idx]) {
+            detached = true;  // clock went back: a fresh detached bucket per call, adds lost
+        }
+        int64_t others = 0;
+        for (int k = 0; k < kLimN; ++k) {
+            if (!detached && k == idx) continue;
+            if (L->start[k] != kAbsent && !(t - L->start[k] > kLimInterval)) others += L->cnt[k];
+        }
+        int64_t pass;
+        if (detached) {
+            pass = ((double)others / 1.0 + 1 <= qps_allowed) ? nr : 0;
+        } else {
+            const int64_t c0 = L->cnt[idx];
+            int64_t lo = 0, hi = nr;
+            while (lo < hi) {
+                const int64_t mid = lo + ((hi - lo) >> 1);
+                if ((double)(others + c0 + mid) / 1.0 + 1 <= qps_allowed) lo = mid + 1;
+                else hi = mid;
+            }
+            pass = lo;
+            L->cnt[idx] = c0 + pass;
+        }
+        rpass[r] = (uint32_t)pass;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_lim_apply(const uint32_t *__restrict__ list,
+                                                        const uint32_t *__restrict__ head,
+                                                        const uint32_t *__restrict__ ridx,
+                                                        const uint32_t *__restrict__ rstart,
+                                                        const uint32_t *__restrict__ rpass, const uint32_t *counters,
+                                                        uint32_t n, uint32_t invalid, uint32_t *__restrict__ keys,
+                                                        uint64_t *__restrict__ out) {
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    const uint32_t m = counters[4];
+    if (j >= m || j >= n) return;
+    const uint32_t r = ridx[j] + head[j] - 1;
+    if (j - rstart[r] >= rpass[r]) {
+        const uint32_t i = list[j];
+        keys[i] = invalid;
+        out[i] = pack_result(TRS_TOO_MANY_REQUEST, 0, 0);
+    }
+}
+
+__global__ void k_lim_init(NsLimiterDev *L) {
+    const int k = threadIdx.x;
+    if (k < kLimN) {
+        L->start[k] = kAbsent;
+        L->cnt[k] = 0;
+    }
+}
+
 }  // namespace
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -697,6 +855,7 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += 2 * align_up(ntiles * sizeof(Agg)) + align_up(ntiles * 4);
     b += align_up(64);
     b += 2 * align_up(hist * 4) + align_up(scan_partials_needed(hist) * 4 + 64);
+    b += align_up(scan_partials_needed(cap) * 4 + 64);
     return b;
 }
 
@@ -739,12 +898,13 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.radix.hist = (uint32_t *)take(hist * 4);
     sc.radix.hist_scan = (uint32_t *)take(hist * 4);
     sc.radix.partial = (uint32_t *)take(scan_partials_needed(hist) * 4 + 64);
+    sc.lim_partial = (uint32_t *)take(scan_partials_needed(cap) * 4 + 64);
     sc.cap = cap;
 }
 
 void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
                           const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, int simple,
-                          void *out_v, hipStream_t s) {
+                          void *out_v, hipStream_t s, const LimiterPass *lims, int nlims) {
     if (n == 0) return;
     uint64_t *out = (uint64_t *)out_v;
     int bits = 1;
@@ -752,8 +912,26 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     const uint32_t invalid_key = st.nslots;
     SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, s));
     const uint32_t nb = (n + kThreads - 1) / kThreads;
-    hipLaunchKernelGGL(k_classify, dim3(nb), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n,
+    const uint32_t ncb = (n + kThreads * kClassifyItems - 1) / (kThreads * kClassifyItems);
+    hipLaunchKernelGGL(k_classify, dim3(ncb), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n,
                        simple, invalid_key, sc.keys[0], sc.pay[0], out, sc.counters);
+    for (int l = 0; l < nlims && !simple; ++l) {
+        // scratch: the sort's alternate buffers are free until the sort starts
+        uint32_t *flag = sc.keys[1];
+        uint32_t *u = (uint32_t *)sc.pay[1];
+        uint32_t *pos = u, *list = u + n, *rstart = u + 2 * (size_t)n, *rpass = u + 3 * (size_t)n;
+        hipLaunchKernelGGL(k_lim_flag, dim3(nb), dim3(kThreads), 0, s, st, sc.keys[0], n, invalid_key, lims[l].ns, flag);
+        exclusive_scan_u32(flag, pos, n, sc.lim_partial, s);
+        hipLaunchKernelGGL(k_lim_compact, dim3(nb), dim3(kThreads), 0, s, flag, pos, n, list, sc.counters);
+        uint32_t *head = flag, *ridx = pos;
+        hipLaunchKernelGGL(k_lim_heads, dim3(nb), dim3(kThreads), 0, s, list, ts_off, ts_base, n, sc.counters, head);
+        exclusive_scan_u32(head, ridx, n, sc.lim_partial, s);
+        hipLaunchKernelGGL(k_lim_starts, dim3(nb), dim3(kThreads), 0, s, head, ridx, n, sc.counters, rstart);
+        hipLaunchKernelGGL(k_lim_walk, dim3(1), dim3(64), 0, s, lims[l].state, lims[l].qps_allowed, list, rstart,
+                           sc.counters, ts_off, ts_base, rpass);
+        hipLaunchKernelGGL(k_lim_apply, dim3(nb), dim3(kThreads), 0, s, list, head, ridx, rstart, rpass, sc.counters, n,
+                           invalid_key, sc.keys[0], out);
+    }
     const int npass = radix_sort_pairs(sc.keys[0], sc.pay[0], sc.keys[1], sc.pay[1], n, bits, sc.radix, s);
     const uint32_t *keys = sc.keys[npass & 1];
     const Payload *pay = sc.pay[npass & 1];
@@ -765,10 +943,19 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, keys, pay, invalid_key,
                        (const Agg *)sc.tile_carry, sc);
     const uint64_t max_flows = n < st.nslots ? n : st.nslots;
-    uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows * kGroup + kThreads - 1) / kThreads, 16384);
+    static const int lanes = [] {
+        const char *e = getenv("SGA_FLOWS_LANES");  // A/B knob: lanes per rule in k_flows (1 or 16)
+        return (e && atoi(e) == 16) ? 16 : 1;
+    }();
+    uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows * lanes + kThreads - 1) / kThreads, 16384);
     if (fb == 0) fb = 1;
-    hipLaunchKernelGGL(k_flows, dim3(fb), dim3(kThreads), 0, s, st, sc, pay, ts_base, simple, out);
+    if (lanes == 16) hipLaunchKernelGGL(k_flows<16>, dim3(fb), dim3(kThreads), 0, s, st, sc, pay, ts_base, simple, out);
+    else hipLaunchKernelGGL(k_flows<1>, dim3(fb), dim3(kThreads), 0, s, st, sc, pay, ts_base, simple, out);
     hipLaunchKernelGGL(k_results, dim3(nb), dim3(kThreads), 0, s, st, sc, keys, pay, simple, out);
+}
+
+void cluster_init_limiter(NsLimiterDev *d, hipStream_t s) {
+    hipLaunchKernelGGL(k_lim_init, dim3(1), dim3(64), 0, s, d);
 }
 
 void cluster_metric_sums(const ClusterState &st, uint32_t slot, int64_t now, int64_t *d_out7, hipStream_t s) {

@@ -49,6 +49,19 @@ struct ClusterState {
     double max_occupy_ratio;
 };
 
+// GlobalRequestLimiter / RequestLimiter of one namespace over UnaryLeapArray(10, 1000)
+// (CS/flow/statistic/limit/RequestLimiter.java:29-87, GlobalRequestLimiter.java:32-55).
+struct NsLimiterDev {
+    int64_t start[10];  // window start (kAbsent = null)
+    int64_t cnt[10];    // LongAdder
+};
+
+struct LimiterPass {
+    int32_t ns;           // namespace index
+    double qps_allowed;   // RequestLimiter.qpsAllowed
+    NsLimiterDev *state;  // device
+};
+
 // Per-batch scratch (device), sized for max_batch events.
 struct BatchScratch {
     uint32_t *keys[2];
@@ -67,7 +80,8 @@ struct BatchScratch {
     void *tile_agg;
     void *tile_carry;
     uint32_t *tile_valid;
-    uint32_t *counters;  // [0]=nvalid [1]=nruns [2]=nflows [3]=flags
+    uint32_t *counters;  // [0]=nvalid [1]=nruns [2]=nflows [3]=flags [4]=limited [5]=limiter runs
+    uint32_t *lim_partial;  // scan partials over max_batch elements (namespace limiter pre-pass)
     RadixScratch radix;
     size_t cap = 0;
 };
@@ -79,7 +93,11 @@ void batch_scratch_carve(BatchScratch &b, void *base, size_t cap, uint32_t nslot
 // simple != 0 selects SimpleClusterFlowChecker semantics (Envoy RLS).
 void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
                           const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, int simple,
-                          void *out /* sga_token_result */, hipStream_t stream);
+                          void *out /* sga_token_result */, hipStream_t stream, const LimiterPass *lims = nullptr,
+                          int nlims = 0);
+
+// Fresh limiter state (every bucket absent).
+void cluster_init_limiter(NsLimiterDev *d, hipStream_t stream);
 
 // ClusterMetric.getSum for all 7 events at `now` (rotates the current window as the reference does).
 void cluster_metric_sums(const ClusterState &st, uint32_t slot, int64_t now, int64_t *d_out7, hipStream_t stream);

@@ -61,6 +61,7 @@ struct Engine {
     DevBuf<uint32_t> d_in_ts;
     DevBuf<uint64_t> d_out;
     DevBuf<int64_t> d_tmp7;
+    DevBuf<NsLimiterDev> d_lim;  // one per namespace index (used when the namespace has a limiter)
 
     // ---- local flow engine
     FlowEngine flow;
@@ -344,12 +345,21 @@ int sga_load_cluster_flow_rules(sga_engine *e, const char *ns, const sga_cluster
     });
 }
 
+// GlobalRequestLimiter.initIfAbsent(namespace) (first call: new RequestLimiter(maxAllowedQps))
+// and applyMaxQpsChange (later calls: setQpsAllowed), GlobalRequestLimiter.java:32-80.
 int sga_set_namespace_limit(sga_engine *e, const char *ns, double max_allowed_qps) {
-    if (!ns || !*ns || !(max_allowed_qps >= 0)) return SGA_EINVAL;
+    if (!ns || !*ns || !(max_allowed_qps >= 0)) return SGA_EINVAL;  // AssertUtil.isTrue(qpsAllowed >= 0)
     return guarded(e, [&](Engine &g) {
-        (void)g.ns_index(ns, true);
-        g.err = "namespace QPS limiter (GlobalRequestLimiter) is not implemented on the device path yet";
-        return SGA_ENOSYS;
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        const int i = g.ns_index(ns, true);
+        if (g.d_lim.n < g.nss.size()) g.d_lim.grow(std::max<size_t>(g.nss.size(), 2 * g.d_lim.n), g.stream);
+        if (!g.nss[i].has_limit) {
+            sga::cluster_init_limiter(g.d_lim.p + i, g.stream);
+            g.nss[i].has_limit = true;
+        }
+        g.nss[i].max_qps = max_allowed_qps;
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        return SGA_OK;
     });
 }
 
@@ -365,10 +375,11 @@ int sga_set_connected_count(sga_engine *e, const char *ns, int32_t connected) {
     });
 }
 
-static bool any_limit(const Engine &g) {
-    for (auto &n : g.nss)
-        if (n.has_limit) return true;
-    return false;
+static std::vector<sga::LimiterPass> limiter_passes(Engine &g) {
+    std::vector<sga::LimiterPass> v;
+    for (size_t i = 0; i < g.nss.size(); ++i)
+        if (g.nss[i].has_limit) v.push_back(sga::LimiterPass{(int32_t)i, g.nss[i].max_qps, g.d_lim.p + i});
+    return v;
 }
 
 int sga_request_tokens_device(sga_engine *e, const int64_t *d_flow_id, const int32_t *d_acquire,
@@ -378,11 +389,11 @@ int sga_request_tokens_device(sga_engine *e, const int64_t *d_flow_id, const int
     if (ts_base < 0) return SGA_EINVAL;
     return guarded(e, [&](Engine &g) {
         if (n > g.cfg.max_batch) return SGA_ERANGE;
-        if (any_limit(g)) return SGA_EINVAL;
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
         hipStream_t s = hip_stream ? (hipStream_t)hip_stream : g.stream;
+        const auto lims = limiter_passes(g);
         sga::cluster_decide_batch(g.state(), g.scratch, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off, (uint32_t)n,
-                                  0, d_out, s);
+                                  0, d_out, s, lims.data(), (int)lims.size());
         SGA_HIP_CHECK(hipGetLastError());
         return SGA_OK;
     });
@@ -400,6 +411,7 @@ static int run_host_batch(Engine &g, const int64_t *flow_id, const int32_t *acqu
         g.d_out.alloc(cap);
     }
     std::vector<uint32_t> off;
+    const auto lims = limiter_passes(g);
     for (size_t b = 0; b < n;) {
         // chunk: at most cap events and a timestamp span that fits u32 offsets
         size_t m = std::min(cap, n - b);
@@ -423,7 +435,7 @@ static int run_host_batch(Engine &g, const int64_t *flow_id, const int32_t *acqu
         else SGA_HIP_CHECK(hipMemsetAsync(g.d_in_prio.p, 0, m, g.stream));
         SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_ts.p, off.data(), m * 4, hipMemcpyHostToDevice, g.stream));
         sga::cluster_decide_batch(g.state(), g.scratch, g.d_in_fid.p, g.d_in_acq.p, g.d_in_prio.p, lo, g.d_in_ts.p,
-                                  (uint32_t)m, simple, g.d_out.p, g.stream);
+                                  (uint32_t)m, simple, g.d_out.p, g.stream, lims.data(), (int)lims.size());
         SGA_HIP_CHECK(hipGetLastError());
         SGA_HIP_CHECK(hipMemcpyAsync(out + b, g.d_out.p, m * 8, hipMemcpyDeviceToHost, g.stream));
         SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
@@ -437,7 +449,6 @@ int sga_request_tokens(sga_engine *e, const int64_t *flow_id, const int32_t *acq
     if (n && (!flow_id || !acquire || !ts || !out)) return SGA_EINVAL;
     static_assert(sizeof(sga_token_result) == 8, "token result is 8 bytes");
     return guarded(e, [&](Engine &g) {
-        if (any_limit(g)) return SGA_EINVAL;
         return run_host_batch(g, flow_id, acquire, prio, ts, n, (uint64_t *)out, 0);
     });
 }

@@ -279,3 +279,44 @@ def test_rls_descriptors(eng_mod):
         assert code[r] == (2 if blocked else 1)
     L.orc_cluster_free(oh)
     eng.close()
+
+
+@pytest.mark.parametrize("seed", [41, 42])
+def test_namespace_limiter(eng_mod, seed):
+    """GlobalRequestLimiter pre-pass: two limited namespaces and one unlimited, requests
+    without rules and bad requests interleaved, clock regressions, a limit change
+    mid-stream (applyMaxQpsChange) -- statuses and metrics equal the oracle."""
+    c = eng_mod
+    rng = np.random.default_rng(seed)
+    rules = {"ns-a": random_rules(rng, 0, ids=range(1, 51)), "ns-b": random_rules(rng, 0, ids=range(51, 101)),
+             "ns-c": random_rules(rng, 0, ids=range(101, 151))}
+    oh = oracle_cluster(rules)
+    L = H.lib()
+    eng = make_engine(c, max_batch=1 << 14)
+    engine_rules(c, eng, rules)
+    lim = c.GlobalRequestLimiter(eng)
+    for ns, q in (("ns-a", 40.0), ("ns-b", 7.5)):
+        L.orc_cluster_set_namespace_limit(oh, ns.encode(), q)
+        lim.init_if_absent(ns, q)
+    svc = c.DefaultTokenService(eng)
+    n = 40_000
+    fid = rng.integers(1, 160, size=n)
+    fid[rng.random(n) < 0.003] = -1
+    acq = np.where(rng.random(n) < 0.95, 1, 2)
+    prio = (rng.random(n) < 0.05).astype(np.uint8)
+    ts = T0 + np.cumsum(rng.integers(0, 2, size=n))
+    back = rng.random(n) < 0.01
+    ts[back] -= rng.integers(1, 400, size=back.sum())
+    for k, lo in enumerate(range(0, n, 10_000)):
+        if k == 2:
+            L.orc_cluster_set_namespace_limit(oh, b"ns-a", 12.0)
+            L.orc_cluster_set_namespace_limit(oh, b"ns-b", 12.0)
+            lim.apply_max_qps_change(12.0)
+        sl = slice(lo, lo + 10_000)
+        g = svc.request_tokens(fid[sl], acq[sl], prio[sl], ts[sl])
+        o = oracle_replay(oh, fid[sl], acq[sl], prio[sl], ts[sl])
+        assert_same(g, o, fid[sl], ts[sl], f"limiter seed={seed} batch {k}")
+        assert (o[0] == -2).any()
+    assert_metrics(c, eng, oh, range(1, 151), int(ts.max()))
+    L.orc_cluster_free(oh)
+    eng.close()
