@@ -236,13 +236,14 @@ def run_cpu_baseline(args, n_gpus):
     mine = shard_of(fid_all, n_gpus) == 0
     rules = np.zeros(int(mine.sum()), dtype=[("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"),
                                            ("sample_count", "<i4"), ("window_interval_ms", "<i4"), ("grade", "<i4"),
-                                           ("strategy", "<i4")])
+                                           ("strategy", "<i4"), ("reserved", "<i4")])
     rules["flow_id"] = fid_all[mine]
     rules["count"] = cnt_all[mine]
     rules["threshold_type"] = 1
     rules["sample_count"] = 10
     rules["window_interval_ms"] = 1000
     rules["grade"] = 1
+    assert rules.itemsize == C.sizeof(H.OrcClusterRule), "oracle rule layout mismatch"
     oh = L.orc_cluster_new(1.0, 1.0)
     L.orc_cluster_load_rules(oh, b"default", rules.ctypes.data_as(C.POINTER(H.OrcClusterRule)), len(rules))
     total, dt = 0, 0.0
