@@ -551,6 +551,167 @@ __device__ __forceinline__ uint32_t pass_prefix(double thr, double isec, int64_t
     return k;
 }
 
+__device__ __forceinline__ int64_t i64_lo(const int4 &v) {
+    return (int64_t)(((uint64_t)(uint32_t)v.y << 32) | (uint32_t)v.x);
+}
+__device__ __forceinline__ int64_t i64_hi(const int4 &v) {
+    return (int64_t)(((uint64_t)(uint32_t)v.w << 32) | (uint32_t)v.z);
+}
+
+// One rule per lane, fused window update: the current bucket's seven counters are
+// loaded once (or start from zero when LeapArray.currentWindow rotates it), updated in
+// registers and stored once; the head bucket (LeapArray.getValidHead) is read from the
+// same vector loads as the window sums.  Same decisions as k_flows<G>.
+__global__ __launch_bounds__(kThreads) void k_flows1(ClusterState st, BatchScratch sc, const Payload *__restrict__ pay,
+                                                     int64_t ts_base, int simple, uint64_t *__restrict__ out) {
+    const uint32_t nflows = sc.counters[2];
+    const uint32_t nruns = sc.counters[1];
+    for (uint32_t fl = blockIdx.x * kThreads + threadIdx.x; fl < nflows; fl += gridDim.x * kThreads) {
+        const uint32_t r0 = sc.flow_first_run[fl];
+        const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        for (uint32_t r = r0; r < r1; ++r) {
+            const uint32_t s = sc.run_slot[r];
+            const SlotParam P = st.param[s];
+            const Rec R = rec_of(st, P);
+            const uint32_t j0 = sc.run_start[r], j1 = sc.run_end[r];
+            const uint32_t n = j1 - j0;
+            const int64_t t0 = ts_base + (int64_t)sc.run_t0off[r];
+            const uint32_t cp_tot = sc.run_cp[r];
+            const int32_t a = sc.run_amin[r];
+            const double thr = simple ? P.thr_simple : P.thr;
+            const int64_t ws = t0 - t0 % P.W;
+            const int cj = (int)((t0 / P.W) % P.S);
+            const int64_t old = R.start(cj);
+            bool fast = (a == sc.run_amax[r]) && !(old != kAbsent && ws < old);
+            if (cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) fast = false;
+            if (!fast) {  // exact replay of every request of the run, in order
+                for (uint32_t j = j0; j < j1; ++j) {
+                    const Payload q = pay[j];
+                    const int64_t t = ts_base + (int64_t)q.ts_off;
+                    out[q.idx] = request_exact(st, s, t, (int32_t)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
+                                               simple);
+                }
+                sc.run_mode[r] = RUN_DONE;
+                continue;
+            }
+            const int jh = (int)(((t0 + P.W) / P.W) % P.S);  // LeapArray.getValidHead index
+            int64_t bp = 0, bw = 0, hstart = kAbsent, hpass = 0;
+            if ((P.S & 1) == 0) {
+                const int4 *v = reinterpret_cast<const int4 *>(R.r);
+                const int hs = P.S >> 1;
+                for (int q = 0; q < hs; ++q) {
+                    const int4 st2 = v[q], ps2 = v[hs + q], wt2 = v[2 * hs + q];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int jj = 2 * q + h;
+                        const int64_t w = h ? i64_hi(st2) : i64_lo(st2);
+                        const int64_t pv = h ? i64_hi(ps2) : i64_lo(ps2);
+                        if (jj == jh) {
+                            hstart = w;
+                            hpass = pv;
+                        }
+                        if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
+                            bp += pv;
+                            bw += h ? i64_hi(wt2) : i64_lo(wt2);
+                        }
+                    }
+                }
+            } else {
+                for (int jj = 0; jj < P.S; ++jj) {
+                    const int64_t w = R.start(jj);
+                    const int64_t pv = R.cnt(CEV_PASS, jj);
+                    if (jj == jh) {
+                        hstart = w;
+                        hpass = pv;
+                    }
+                    if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
+                        bp += pv;
+                        bw += R.cnt(CEV_WAITING, jj);
+                    }
+                }
+            }
+            // ---- LeapArray.currentWindow(t0) on the current bucket, in registers
+            const bool rot = old == kAbsent || ws > old;
+            int64_t c[CEV_N];
+            SlotOcc o{0, 0, 0};
+            bool occ_dirty = false;
+            if (rot) {
+#pragma unroll
+                for (int k = 0; k < CEV_N; ++k) c[k] = 0;
+                if (old != kAbsent) {  // resetWindowTo + transferOccupyToBucket
+                    o = st.occ[s];
+                    if (o.has_occ) {
+                        c[CEV_OCCUPIED_PASS] += o.occ_pass;
+                        c[CEV_PASS] += o.occ_pass;
+                        c[CEV_PASS_REQUEST] += o.occ_preq;
+                        o.occ_pass = 0;
+                        o.occ_preq = 0;
+                        o.has_occ = 0;
+                        occ_dirty = true;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < CEV_N; ++k) c[k] = R.cnt(k, cj);
+            }
+            // getValidHead after the rotation (the head is the current bucket when S == 1)
+            int64_t head;
+            if (jh == cj) head = c[CEV_PASS];
+            else head = (hstart != kAbsent && !(t0 - hstart > (int64_t)P.interval)) ? hpass : 0;
+            const int64_t s0 = bp + c[CEV_PASS];
+            const int64_t w0 = bw + c[CEV_WAITING];
+            const uint32_t f = pass_prefix(thr, P.isec, s0, a, n);
+            const uint32_t cpf = (f >= n) ? cp_tot : (cp_tot ? sc.ev_cp[j0 + f] : 0u);
+            const uint32_t np_after = cp_tot - cpf;
+            uint32_t cw = 0;
+            if (np_after > 0) {
+                if (!occ_dirty && !rot) o = st.occ[s];
+                else if (!occ_dirty) o = st.occ[s];
+                const double latest = (double)(s0 + (int64_t)f * a) / P.isec;
+                const double lim = st.max_occupy_ratio * thr;
+                const int64_t occ0 = o.occ_pass;
+                uint32_t l2 = 0, h2 = np_after;
+                while (l2 < h2) {
+                    const uint32_t cc = l2 + ((h2 - l2) >> 1);
+                    const int64_t add = (int64_t)cc * a;
+                    const bool ok = ((double)(w0 + add) / P.isec <= lim) &&
+                                    (latest + (double)((int64_t)a + occ0 + add) - (double)head <= thr);
+                    if (ok) l2 = cc + 1;
+                    else h2 = cc;
+                }
+                cw = l2;
+                if (cw > 0) {
+                    o.occ_pass += (int64_t)cw * a;
+                    o.occ_preq += cw;
+                    o.has_occ = 1;
+                    occ_dirty = true;
+                }
+            }
+            const int64_t wa = (int64_t)cw * a;
+            const uint32_t nblk = n - f - cw;
+            c[CEV_PASS] += (int64_t)f * a;
+            c[CEV_PASS_REQUEST] += f;
+            c[CEV_OCCUPIED_PASS] += (int64_t)cpf * a;
+            c[CEV_WAITING] += wa;
+            c[CEV_BLOCK] += (int64_t)nblk * a;
+            c[CEV_BLOCK_REQUEST] += nblk;
+            c[CEV_OCCUPIED_BLOCK] += (int64_t)(np_after - cw) * a;
+            if (rot) R.start(cj) = ws;
+#pragma unroll
+            for (int k = 0; k < CEV_N; ++k) R.cnt(k, cj) = c[k];
+            if (occ_dirty) st.occ[s] = o;
+            sc.run_s0[r] = s0;
+            sc.run_f[r] = f;
+            sc.run_cpf[r] = cpf;
+            sc.run_cw[r] = cw;
+            sc.run_thr[r] = thr;
+            sc.run_isec[r] = P.isec;
+            sc.run_wait[r] = 1000 / P.S;
+            sc.run_mode[r] = RUN_FAST;
+        }
+    }
+}
+
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratch sc, const Payload *__restrict__ pay,
                                                     int64_t ts_base, int simple, uint64_t *__restrict__ out) {
@@ -595,11 +756,31 @@ __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratc
             // ---- window sums over the valid buckets other than the current one (rotation of the
             //      current bucket does not touch them); lanes split the buckets
             int64_t bp = 0, bw = 0;
-            for (int jj = gl; jj < P.S; jj += G) {
-                const int64_t w = R.start(jj);
-                if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
-                    bp += R.cnt(CEV_PASS, jj);
-                    bw += R.cnt(CEV_WAITING, jj);
+            if (G == 1 && (P.S & 1) == 0) {
+                // start / PASS / WAITING vectors are contiguous and 16-B aligned: pairwise loads
+                const int4 *v = reinterpret_cast<const int4 *>(R.r);
+                const int hs = P.S >> 1;
+                for (int q = 0; q < hs; ++q) {
+                    const int4 st2 = v[q], ps2 = v[hs + q], wt2 = v[2 * hs + q];
+                    const int64_t w0 = (int64_t)(((uint64_t)(uint32_t)st2.y << 32) | (uint32_t)st2.x);
+                    const int64_t w1 = (int64_t)(((uint64_t)(uint32_t)st2.w << 32) | (uint32_t)st2.z);
+                    const int j0 = 2 * q, j1 = 2 * q + 1;
+                    if (j0 != cj && w0 != kAbsent && !(t0 - w0 > (int64_t)P.interval)) {
+                        bp += (int64_t)(((uint64_t)(uint32_t)ps2.y << 32) | (uint32_t)ps2.x);
+                        bw += (int64_t)(((uint64_t)(uint32_t)wt2.y << 32) | (uint32_t)wt2.x);
+                    }
+                    if (j1 != cj && w1 != kAbsent && !(t0 - w1 > (int64_t)P.interval)) {
+                        bp += (int64_t)(((uint64_t)(uint32_t)ps2.w << 32) | (uint32_t)ps2.z);
+                        bw += (int64_t)(((uint64_t)(uint32_t)wt2.w << 32) | (uint32_t)wt2.z);
+                    }
+                }
+            } else {
+                for (int jj = gl; jj < P.S; jj += G) {
+                    const int64_t w = R.start(jj);
+                    if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
+                        bp += R.cnt(CEV_PASS, jj);
+                        bw += R.cnt(CEV_WAITING, jj);
+                    }
                 }
             }
             const int64_t base_pass = group_sum<G>(bp);
@@ -945,12 +1126,15 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     const uint64_t max_flows = n < st.nslots ? n : st.nslots;
     static const int lanes = [] {
         const char *e = getenv("SGA_FLOWS_LANES");  // A/B knob: lanes per rule in k_flows (1 or 16)
-        return (e && atoi(e) == 16) ? 16 : 1;
+        const int v = e ? atoi(e) : 0;
+        return (v == 16 || v == 4 || v == 1) ? v : 0;  // 0: k_flows1
     }();
-    uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows * lanes + kThreads - 1) / kThreads, 16384);
+    uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows * (lanes ? lanes : 1) + kThreads - 1) / kThreads, 16384);
     if (fb == 0) fb = 1;
     if (lanes == 16) hipLaunchKernelGGL(k_flows<16>, dim3(fb), dim3(kThreads), 0, s, st, sc, pay, ts_base, simple, out);
-    else hipLaunchKernelGGL(k_flows<1>, dim3(fb), dim3(kThreads), 0, s, st, sc, pay, ts_base, simple, out);
+    else if (lanes == 4) hipLaunchKernelGGL(k_flows<4>, dim3(fb), dim3(kThreads), 0, s, st, sc, pay, ts_base, simple, out);
+    else if (lanes == 1) hipLaunchKernelGGL(k_flows<1>, dim3(fb), dim3(kThreads), 0, s, st, sc, pay, ts_base, simple, out);
+    else hipLaunchKernelGGL(k_flows1, dim3(fb), dim3(kThreads), 0, s, st, sc, pay, ts_base, simple, out);
     hipLaunchKernelGGL(k_results, dim3(nb), dim3(kThreads), 0, s, st, sc, keys, pay, simple, out);
 }
 

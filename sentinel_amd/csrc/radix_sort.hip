@@ -14,6 +14,8 @@
 //             per tile.
 #include "radix_sort.hpp"
 
+#include <cstdlib>
+
 namespace sga {
 
 namespace {
@@ -107,6 +109,252 @@ __global__ __launch_bounds__(kThreads) void k_rs_scatter(const uint32_t *__restr
             const uint32_t pos = goff[d] + wcnt[wave][d] + rank[r];
             keys_out[pos] = key[r];
             pay_out[pos] = pay_in[e];
+        }
+    }
+}
+
+// ---- single-sweep passes (decoupled look-back) ------------------------------
+// Per pass one kernel: a workgroup takes the next tile id from a counter, ranks its
+// 4096 keys (same ballot match as above), publishes its per-digit counts, looks
+// back over the previous tiles' published counts for its global digit offsets,
+// then stages the tile in LDS in sorted order so that keys and payloads leave as
+// contiguous per-digit segments (coalesced stores instead of one store per key).
+// Digit totals of every pass come from one up-front histogram read of the keys.
+constexpr uint32_t kFlagAgg = 1u << 30, kFlagPrefix = 2u << 30, kCountMask = (1u << 30) - 1;
+constexpr int kMaxPasses = 3;
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_rs_upfront(const uint32_t *__restrict__ keys, uint32_t n, int npass,
+                                                         uint32_t *__restrict__ ghist) {
+    constexpr int RADIX = 1 << D;
+    __shared__ uint32_t h[kMaxPasses][RADIX];
+    for (int d = threadIdx.x; d < kMaxPasses * RADIX; d += kThreads) (&h[0][0])[d] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * kTile;
+#pragma unroll 4
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t e = base + r * kThreads + threadIdx.x;
+        if (e < n) {
+            const uint32_t k = keys[e];
+            for (int p = 0; p < npass; ++p) atomicAdd(&h[p][(k >> (p * D)) & (RADIX - 1)], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < npass * RADIX; i += kThreads) {
+        const uint32_t v = (&h[0][0])[i];
+        if (v) atomicAdd(&ghist[i], v);
+    }
+}
+
+// exclusive scan of each pass's RADIX digit totals (one workgroup)
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_rs_digit_base(uint32_t *__restrict__ ghist, int npass) {
+    constexpr int RADIX = 1 << D;
+    constexpr int DPT = RADIX >= kThreads ? RADIX / kThreads : 1;
+    __shared__ uint32_t ws[kWaves];
+    for (int p = 0; p < npass; ++p) {
+        uint32_t *g = ghist + p * RADIX;
+        uint32_t v[DPT];
+        uint32_t sum = 0;
+#pragma unroll
+        for (int k = 0; k < DPT; ++k) {
+            const int d = threadIdx.x * DPT + k;
+            v[k] = d < RADIX ? g[d] : 0;
+            sum += v[k];
+        }
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        uint32_t x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) ws[wave] = x;
+        __syncthreads();
+        uint32_t pre = x - sum;
+        for (int w = 0; w < wave; ++w) pre += ws[w];
+#pragma unroll
+        for (int k = 0; k < DPT; ++k) {
+            const int d = threadIdx.x * DPT + k;
+            if (d < RADIX) g[d] = pre;
+            pre += v[k];
+        }
+        __syncthreads();
+    }
+}
+
+template <int D>
+struct OnesweepSmem {
+    static constexpr int RADIX = 1 << D;
+    uint32_t wcnt[kWaves][RADIX];  // per-wave digit counts, then exclusive prefixes over waves
+    uint32_t dstart[RADIX];        // tile-local exclusive digit start
+    uint32_t gbase[RADIX];         // global position of the tile's first key of digit d
+    uint32_t skey[kTile];
+    Payload spay[kTile / 2];
+    uint32_t tile;
+};
+
+// LB = true: decoupled look-back over `status`; LB = false: the tile's global digit offsets
+// come precomputed in `digit_base` (digit-major scan of the per-tile histograms).
+template <int D, bool LB>
+__global__ __launch_bounds__(kThreads) void k_rs_onesweep(const uint32_t *__restrict__ keys_in,
+                                                          const Payload *__restrict__ pay_in, uint32_t n, int shift,
+                                                          const uint32_t *__restrict__ digit_base,
+                                                          uint32_t *__restrict__ status, uint32_t *tile_ctr,
+                                                          uint32_t *__restrict__ keys_out,
+                                                          Payload *__restrict__ pay_out) {
+    constexpr int RADIX = 1 << D;
+    constexpr int DPT = RADIX >= kThreads ? RADIX / kThreads : 1;
+    __shared__ OnesweepSmem<D> sm;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) sm.tile = LB ? atomicAdd(tile_ctr, 1u) : blockIdx.x;
+    for (int d = threadIdx.x; d < RADIX; d += kThreads) {
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) sm.wcnt[w][d] = 0;
+    }
+    __syncthreads();
+    const uint32_t tile = sm.tile;
+    const uint32_t tbase = tile * kTile;
+    const uint32_t tn = min((uint32_t)kTile, n - tbase);
+
+    // ---- rank: wave-private running digit counts (arrival order kept)
+    const uint32_t wbase = tbase + wave * (kRounds * 64);
+    uint32_t key[kRounds];
+    uint32_t pos[kRounds];
+    Payload pv[kRounds];
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t e = wbase + r * 64 + lane;
+        const bool valid = e < n;
+        key[r] = valid ? keys_in[e] : 0u;
+        pv[r] = valid ? pay_in[e] : Payload{0, 0, 0, 0};
+        const uint32_t d = (key[r] >> shift) & (RADIX - 1);
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < D; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        uint32_t before = 0;
+        if (valid) before = sm.wcnt[wave][d];
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t my = (uint32_t)__popcll(peers & lanemask_lt(lane));
+        if (valid && my == 0) sm.wcnt[wave][d] = before + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        pos[r] = before + my;
+    }
+    __syncthreads();
+
+    // ---- per digit (blocked: thread t owns digits t*DPT ..): wave prefixes, tile totals,
+    //      publish the aggregate, tile-local digit starts (block scan)
+    uint32_t tot[DPT];
+    uint32_t tsum = 0;
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+        const int d = threadIdx.x * DPT + k;
+        uint32_t sacc = 0;
+        if (d < RADIX) {
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) {
+                const uint32_t c = sm.wcnt[w][d];
+                sm.wcnt[w][d] = sacc;
+                sacc += c;
+            }
+            if (LB)
+                __hip_atomic_store(&status[(size_t)tile * RADIX + d], (tile == 0 ? kFlagPrefix : kFlagAgg) | sacc,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        tot[k] = sacc;
+        tsum += sacc;
+    }
+    {
+        __shared__ uint32_t ws[kWaves];
+        uint32_t x = tsum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) ws[wave] = x;
+        __syncthreads();
+        uint32_t pre = x - tsum;
+        for (int w = 0; w < wave; ++w) pre += ws[w];
+#pragma unroll
+        for (int k = 0; k < DPT; ++k) {
+            const int d = threadIdx.x * DPT + k;
+            if (d < RADIX) sm.dstart[d] = pre;
+            pre += tot[k];
+        }
+    }
+    // ---- decoupled look-back: exclusive count of digit d over all previous tiles
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+        const int d = threadIdx.x * DPT + k;
+        if (d >= RADIX) continue;
+        if (!LB) {
+            sm.gbase[d] = digit_base[(size_t)d * gridDim.x + tile];
+            continue;
+        }
+        uint32_t excl = 0;
+        if (tile > 0) {
+            int64_t t = (int64_t)tile - 1;
+            while (true) {
+                uint32_t v;
+                do {
+                    v = __hip_atomic_load(&status[(size_t)t * RADIX + d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((v >> 30) == 0) __builtin_amdgcn_s_sleep(1);
+                } while ((v >> 30) == 0);
+                excl += v & kCountMask;
+                if ((v & kFlagPrefix) || t == 0) break;
+                --t;
+            }
+            __hip_atomic_store(&status[(size_t)tile * RADIX + d], kFlagPrefix | (excl + tot[k]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        sm.gbase[d] = digit_base[d] + excl;
+    }
+    __syncthreads();
+
+    // ---- stage keys in tile-sorted order, then write them out as digit segments
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t e = wbase + r * 64 + lane;
+        if (e < n) {
+            const uint32_t d = (key[r] >> shift) & (RADIX - 1);
+            pos[r] += sm.dstart[d] + sm.wcnt[wave][d];
+            sm.skey[pos[r]] = key[r];
+        }
+    }
+    __syncthreads();
+    uint32_t gpos[kRounds];
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t i = r * kThreads + threadIdx.x;
+        gpos[r] = 0;
+        if (i < tn) {
+            const uint32_t k = sm.skey[i];
+            const uint32_t d = (k >> shift) & (RADIX - 1);
+            gpos[r] = sm.gbase[d] + (i - sm.dstart[d]);
+            keys_out[gpos[r]] = k;
+        }
+    }
+    // ---- payloads in two halves of the tile (LDS budget)
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        const uint32_t lo = half * (kTile / 2);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kRounds; ++r) {
+            const uint32_t e = wbase + r * 64 + lane;
+            if (e < n && pos[r] >= lo && pos[r] < lo + kTile / 2) sm.spay[pos[r] - lo] = pv[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = half * (kRounds / 2); r < (half + 1) * (kRounds / 2); ++r) {
+            const uint32_t i = r * kThreads + threadIdx.x;
+            if (i < tn) pay_out[gpos[r]] = sm.spay[i - lo];
         }
     }
 }
@@ -213,46 +461,88 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, uint32_t *p
 
 size_t radix_tiles(size_t n) { return (n + kTile - 1) / kTile; }
 
+// status array (tiles x RADIX) + up-front digit histograms and tile counters
 size_t radix_hist_entries(size_t n, int bits) {
     const int npass = bits <= 0 ? 0 : (bits + kMaxDigitBits - 1) / kMaxDigitBits;
     const int d = npass ? (bits + npass - 1) / npass : 1;
-    return ((size_t)1 << d) * radix_tiles(n);
+    return ((size_t)1 << d) * radix_tiles(n) + (size_t)kMaxPasses * 2048 + 64;
+}
+
+static int max_digit_bits() {
+    static const int v = [] {
+        const char *e = getenv("SGA_RADIX_BITS");  // A/B knob: widest digit per pass (default 8)
+        int b = e ? atoi(e) : 8;
+        return b < 4 ? 4 : (b > kMaxDigitBits ? kMaxDigitBits : b);
+    }();
+    return v;
+}
+
+static int radix_mode() {
+    static const int v = [] {
+        const char *e = getenv("SGA_RADIX_MODE");  // A/B knob: 0 look-back, 1 staged scatter, 2 direct scatter
+        return e ? atoi(e) : 1;
+    }();
+    return v;
 }
 
 template <int D>
-static void pass(const uint32_t *kin, const Payload *pin, uint32_t *kout, Payload *pout, uint32_t n, int shift,
-                 RadixScratch &sc, hipStream_t s) {
+static void sort_passes(uint32_t *&ks, Payload *&ps, uint32_t *&kd, Payload *&pd, uint32_t n, int npass,
+                        RadixScratch &sc, hipStream_t s) {
+    constexpr int RADIX = 1 << D;
     const uint32_t nt = (uint32_t)radix_tiles(n);
-    hipLaunchKernelGGL((k_rs_hist<D>), dim3(nt), dim3(kThreads), 0, s, kin, n, shift, nt, sc.hist);
-    exclusive_scan_u32(sc.hist, sc.hist_scan, ((size_t)1 << D) * nt, sc.partial, s);
-    hipLaunchKernelGGL((k_rs_scatter<D>), dim3(nt), dim3(kThreads), 0, s, kin, pin, n, shift, nt, sc.hist_scan, kout,
-                       pout);
+    const int mode = radix_mode();
+    if (mode != 0) {
+        for (int p = 0; p < npass; ++p) {
+            hipLaunchKernelGGL((k_rs_hist<D>), dim3(nt), dim3(kThreads), 0, s, ks, n, p * D, nt, sc.hist);
+            exclusive_scan_u32(sc.hist, sc.hist_scan, (size_t)RADIX * nt, sc.partial, s);
+            if (mode == 1)
+                hipLaunchKernelGGL((k_rs_onesweep<D, false>), dim3(nt), dim3(kThreads), 0, s, ks, ps, n, p * D,
+                                   sc.hist_scan, nullptr, nullptr, kd, pd);
+            else
+                hipLaunchKernelGGL((k_rs_scatter<D>), dim3(nt), dim3(kThreads), 0, s, ks, ps, n, p * D, nt,
+                                   sc.hist_scan, kd, pd);
+            uint32_t *tk = ks; ks = kd; kd = tk;
+            Payload *tp = ps; ps = pd; pd = tp;
+        }
+        return;
+    }
+    uint32_t *status = sc.hist;
+    uint32_t *ghist = sc.hist_scan;                     // npass x RADIX digit totals -> bases
+    uint32_t *ctr = sc.hist_scan + kMaxPasses * 2048;   // one tile counter per pass
+    SGA_HIP_CHECK(hipMemsetAsync(ghist, 0, (kMaxPasses * 2048 + 64) * sizeof(uint32_t), s));
+    hipLaunchKernelGGL((k_rs_upfront<D>), dim3(nt), dim3(kThreads), 0, s, ks, n, npass, ghist);
+    hipLaunchKernelGGL((k_rs_digit_base<D>), dim3(1), dim3(kThreads), 0, s, ghist, npass);
+    for (int p = 0; p < npass; ++p) {
+        SGA_HIP_CHECK(hipMemsetAsync(status, 0, (size_t)nt * RADIX * sizeof(uint32_t), s));
+        hipLaunchKernelGGL((k_rs_onesweep<D, true>), dim3(nt), dim3(kThreads), 0, s, ks, ps, n, p * D, ghist + p * RADIX,
+                           status, ctr + p, kd, pd);
+        uint32_t *tk = ks; ks = kd; kd = tk;
+        Payload *tp = ps; ps = pd; pd = tp;
+    }
 }
 
 int radix_sort_pairs(uint32_t *keys, Payload *pay, uint32_t *keys_alt, Payload *pay_alt, size_t n, int bits,
                      RadixScratch &sc, hipStream_t s) {
     if (n == 0 || bits <= 0) return 0;
-    const int npass = (bits + kMaxDigitBits - 1) / kMaxDigitBits;
+    const int mb = max_digit_bits();
+    const int npass = (bits + mb - 1) / mb;
     const int d = (bits + npass - 1) / npass;
+    if (npass > kMaxPasses) return -1;
     uint32_t *ks = keys, *kd = keys_alt;
     Payload *ps = pay, *pd = pay_alt;
-    for (int p = 0; p < npass; ++p) {
-        const int shift = p * d;
-        switch (d) {
-        case 1: pass<1>(ks, ps, kd, pd, (uint32_t)n, shift, sc, s); break;
-        case 2: pass<2>(ks, ps, kd, pd, (uint32_t)n, shift, sc, s); break;
-        case 3: pass<3>(ks, ps, kd, pd, (uint32_t)n, shift, sc, s); break;
-        case 4: pass<4>(ks, ps, kd, pd, (uint32_t)n, shift, sc, s); break;
-        case 5: pass<5>(ks, ps, kd, pd, (uint32_t)n, shift, sc, s); break;
-        case 6: pass<6>(ks, ps, kd, pd, (uint32_t)n, shift, sc, s); break;
-        case 7: pass<7>(ks, ps, kd, pd, (uint32_t)n, shift, sc, s); break;
-        case 8: pass<8>(ks, ps, kd, pd, (uint32_t)n, shift, sc, s); break;
-        case 9: pass<9>(ks, ps, kd, pd, (uint32_t)n, shift, sc, s); break;
-        case 10: pass<10>(ks, ps, kd, pd, (uint32_t)n, shift, sc, s); break;
-        default: pass<11>(ks, ps, kd, pd, (uint32_t)n, shift, sc, s); break;
-        }
-        uint32_t *tk = ks; ks = kd; kd = tk;
-        Payload *tp = ps; ps = pd; pd = tp;
+    const uint32_t nn = (uint32_t)n;
+    switch (d) {
+    case 1: sort_passes<1>(ks, ps, kd, pd, nn, npass, sc, s); break;
+    case 2: sort_passes<2>(ks, ps, kd, pd, nn, npass, sc, s); break;
+    case 3: sort_passes<3>(ks, ps, kd, pd, nn, npass, sc, s); break;
+    case 4: sort_passes<4>(ks, ps, kd, pd, nn, npass, sc, s); break;
+    case 5: sort_passes<5>(ks, ps, kd, pd, nn, npass, sc, s); break;
+    case 6: sort_passes<6>(ks, ps, kd, pd, nn, npass, sc, s); break;
+    case 7: sort_passes<7>(ks, ps, kd, pd, nn, npass, sc, s); break;
+    case 8: sort_passes<8>(ks, ps, kd, pd, nn, npass, sc, s); break;
+    case 9: sort_passes<9>(ks, ps, kd, pd, nn, npass, sc, s); break;
+    case 10: sort_passes<10>(ks, ps, kd, pd, nn, npass, sc, s); break;
+    default: sort_passes<11>(ks, ps, kd, pd, nn, npass, sc, s); break;
     }
     return npass;  // result is in (keys, pay) if npass even, else in the alt buffers
 }
