@@ -1,0 +1,18 @@
+#!/bin/bash
+# Usage (on the GPU box): bash tools/gpu_check.sh <tag>
+# GPU parity tests, smoke, bench (with CPU baseline) and a rocprofv3 kernel-trace summary.
+set -o pipefail
+tag=${1:-run}
+export TMPDIR=/tmp
+out=gpurun_out/$tag
+mkdir -p $out
+nproc > $out/nproc.txt; lscpu > $out/lscpu.txt 2>&1
+timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $out/pytest_gpu.log; exit 1; }
+tail -3 $out/pytest_gpu.log
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { echo "smoke failed"; cat $out/smoke.log; exit 1; }
+cat $out/smoke.log
+timeout -k 10 300 python3 bench.py > $out/bench.json 2> $out/bench.err || { echo "bench failed"; tail -20 $out/bench.err; exit 1; }
+cat $out/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_$tag -o run --output-format csv -- python3 bench.py --no-cpu > $out/prof_bench.json 2> $out/prof_bench.err || { echo "prof failed"; tail -20 $out/prof_bench.err; exit 1; }
+find /tmp/prof_$tag -name "*kernel_stats.csv" -exec cp {} $out/kernel_stats.csv \;
+python3 tools/kstats.py $out/kernel_stats.csv | head -20
