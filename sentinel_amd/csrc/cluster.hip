@@ -53,88 +53,131 @@ __device__ __forceinline__ HashEntry slot_lookup(const ClusterState &st, int64_t
     return HashEntry{0, 0, 0};
 }
 
+// ---------------------------------------------------------------- packed sort element
+// One u64 per request carries everything after classify needs, so the sort and the scans move
+// 8 bytes per request:
+//   [63:40] rule slot (invalid requests: nslots, sorted last)
+//   [39:34] window-bucket delta  t / W - ts_base / W   (63 = escape: does not fit)
+//   [33]    prioritized
+//   [32:26] acquire count 1..127 (0 = escape: not representable, or the bucket escaped)
+//   [25:0]  request index (max_batch <= 2^26)
+// An escaped request forces its run onto the exact per-request replay, which re-reads the
+// original arrays; run boundaries are (slot, bucket delta) changes, exact whenever no escape.
+constexpr int kIdxBits = 26;
+constexpr int kAcqShift = 26, kPrioShift = 33, kBdShift = 34, kSlotShift = 40;
+constexpr uint32_t kAcqMax = 127, kBdEsc = 63;
+
+__device__ __forceinline__ uint64_t el_pack(uint32_t slot, uint32_t bd, uint32_t prio, uint32_t acq7, uint32_t idx) {
+    return ((uint64_t)slot << kSlotShift) | ((uint64_t)bd << kBdShift) | ((uint64_t)prio << kPrioShift) |
+           ((uint64_t)acq7 << kAcqShift) | (uint64_t)idx;
+}
+__device__ __forceinline__ uint32_t el_slot(uint64_t e) { return (uint32_t)(e >> kSlotShift); }
+__device__ __forceinline__ uint32_t el_runkey(uint64_t e) { return (uint32_t)(e >> kBdShift); }  // slot | bucket
+__device__ __forceinline__ uint32_t el_prio(uint64_t e) { return (uint32_t)(e >> kPrioShift) & 1u; }
+__device__ __forceinline__ int32_t el_acq(uint64_t e) { return (int32_t)((e >> kAcqShift) & kAcqMax); }
+__device__ __forceinline__ uint32_t el_idx(uint64_t e) { return (uint32_t)e & ((1u << kIdxBits) - 1); }
+
 // ---------------------------------------------------------------- classify
-// kClassifyItems requests per thread (strided by the block size, so every load stays coalesced);
-// the first hash probes of all of them are issued before any is resolved.
-constexpr int kClassifyItems = 4;
+// One workgroup per sort tile (4096 requests, kItems per thread strided by the block size so every
+// load is coalesced).  Validation (DefaultTokenService.notValidRequest, :87-89) and
+// ClusterFlowRuleManager.getFlowRuleById (open addressing) write BAD_REQUEST / NO_RULE_EXISTS
+// results directly.  The tile's histogram of the first radix digit is produced here (hist_d > 0).
+constexpr int kClsChunk = 4;  // hash probes in flight per thread
 
 __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const int64_t *__restrict__ flow_id,
                                                        const int32_t *__restrict__ acquire,
                                                        const uint8_t *__restrict__ prio,
                                                        const uint32_t *__restrict__ ts_off, int64_t ts_base,
-                                                       uint32_t n, int simple, uint32_t invalid_key, uint32_t *__restrict__ keys,
-                                                       Payload *__restrict__ pay, uint64_t *__restrict__ out,
-                                                       uint32_t *__restrict__ counters) {
-    const uint32_t base = blockIdx.x * (kThreads * kClassifyItems) + threadIdx.x;
-    int64_t fid[kClassifyItems];
-    int32_t acq[kClassifyItems];
-    uint32_t h[kClassifyItems];
-    HashEntry e[kClassifyItems];
-#pragma unroll
-    for (int u = 0; u < kClassifyItems; ++u) {
-        const uint32_t i = base + u * kThreads;
-        fid[u] = i < n ? flow_id[i] : 0;
-        acq[u] = i < n ? acquire[i] : 0;
+                                                       uint32_t n, int simple, uint32_t invalid_key,
+                                                       uint64_t *__restrict__ el, uint64_t *__restrict__ out,
+                                                       int hist_d, uint32_t ntiles, uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[256];
+    if (hist_d > 0) {
+        h[threadIdx.x] = 0;
+        __syncthreads();
     }
+    const uint32_t tbase = blockIdx.x * kTileElems;
+    for (int c = 0; c < kItems; c += kClsChunk) {
+        int64_t fid[kClsChunk];
+        int32_t acq[kClsChunk];
+        uint32_t hh[kClsChunk];
+        HashEntry e[kClsChunk];
 #pragma unroll
-    for (int u = 0; u < kClassifyItems; ++u) {
-        h[u] = (uint32_t)hash_flow_id(fid[u]) & st.hmask;
-        e[u] = fid[u] > 0 ? st.htab[h[u]] : HashEntry{0, 0, 0};
-    }
+        for (int u = 0; u < kClsChunk; ++u) {
+            const uint32_t i = tbase + (c + u) * kThreads + threadIdx.x;
+            fid[u] = i < n ? flow_id[i] : 0;
+            acq[u] = i < n ? acquire[i] : 0;
+        }
 #pragma unroll
-    for (int u = 0; u < kClassifyItems; ++u) {
-        const uint32_t i = base + u * kThreads;
-        if (i >= n) continue;
-        const int64_t f = fid[u];
-        const int32_t a = acq[u];
-        int8_t status = TRS_OK;
-        HashEntry he = e[u];
-        if (!simple && (f <= 0 || a <= 0)) {
-            status = TRS_BAD_REQUEST;  // DefaultTokenService.notValidRequest, :87-89
-        } else {
-            // ClusterFlowRuleManager.getFlowRuleById: validId(id > 0) && FLOW_RULES.get(id)
-            if (f > 0 && he.key != f && he.key != 0) {  // continue the linear probe
-                uint32_t hh = h[u];
-                for (uint32_t probe = 1; probe <= st.hmask; ++probe) {
-                    hh = (hh + 1) & st.hmask;
-                    he = st.htab[hh];
-                    if (he.key == f || he.key == 0) break;
+        for (int u = 0; u < kClsChunk; ++u) {
+            hh[u] = (uint32_t)hash_flow_id(fid[u]) & st.hmask;
+            e[u] = fid[u] > 0 ? st.htab[hh[u]] : HashEntry{0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < kClsChunk; ++u) {
+            const uint32_t i = tbase + (c + u) * kThreads + threadIdx.x;
+            if (i >= n) continue;
+            const int64_t f = fid[u];
+            const int32_t a = acq[u];
+            int8_t status = TRS_OK;
+            HashEntry he = e[u];
+            if (!simple && (f <= 0 || a <= 0)) {
+                status = TRS_BAD_REQUEST;
+            } else {
+                if (f > 0 && he.key != f && he.key != 0) {  // continue the linear probe
+                    uint32_t q = hh[u];
+                    for (uint32_t probe = 1; probe <= st.hmask; ++probe) {
+                        q = (q + 1) & st.hmask;
+                        he = st.htab[q];
+                        if (he.key == f || he.key == 0) break;
+                    }
                 }
+                if (he.key != f || f <= 0) status = TRS_NO_RULE_EXISTS;
             }
-            if (he.key != f || f <= 0) status = TRS_NO_RULE_EXISTS;
-        }
-        if (status != TRS_OK) {
-            out[i] = pack_result(status, 0, 0);
-            keys[i] = invalid_key;
-            pay[i] = Payload{i, 0u, 0u, 0u};
-        } else {
-            keys[i] = he.slot;
-            const uint32_t p = (!simple && prio && prio[i]) ? 0x80000000u : 0u;
-            const uint32_t off = ts_off[i];
-            const int64_t t = ts_base + (int64_t)off;
-            pay[i] = Payload{i, off, (uint32_t)a | p, (uint32_t)(t / (int64_t)he.W)};
+            uint32_t key = invalid_key;
+            if (status != TRS_OK) {
+                out[i] = pack_result(status, 0, 0);
+                el[i] = (uint64_t)invalid_key << kSlotShift;
+            } else {
+                key = he.slot;
+                const uint32_t p = (!simple && prio && prio[i]) ? 1u : 0u;
+                const int64_t W = (int64_t)he.W;
+                const int64_t bd = (ts_base + (int64_t)ts_off[i]) / W - ts_base / W;
+                uint32_t a7 = (a >= 1 && a <= (int32_t)kAcqMax) ? (uint32_t)a : 0u;
+                uint32_t bd6 = (uint32_t)bd;
+                if (bd >= (int64_t)kBdEsc) {
+                    bd6 = kBdEsc;
+                    a7 = 0;
+                }
+                el[i] = el_pack(key, bd6, p, a7, i);
+            }
+            if (hist_d > 0) atomicAdd(&h[key & ((1u << hist_d) - 1)], 1u);
         }
     }
-    (void)counters;  // the valid count is derived after the sort (invalid keys sort last)
+    if (hist_d > 0) {
+        __syncthreads();
+        if (threadIdx.x < (1u << hist_d)) hist[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+    }
 }
 
 // ---------------------------------------------------------------- runs (segmented scan)
 // A run = maximal group of sorted requests with the same (rule, window bucket).
-// Segmented scan value: run/flow head counts (plain sums) and, since the last
-// run head, the number of prioritized requests and the min/max acquire count.
+// Scan value: run / flow heads and prioritized requests (plain counts); since the last run
+// head: prioritized count and min / max acquire (segmented).
 struct Agg {
-    uint32_t nh, nf;  // run heads, flow heads
-    uint32_t flag;    // segment (run) head seen
-    uint32_t cnt;     // prioritized events since last run head
-    int32_t mn, mx;   // min / max acquire since last run head
+    uint32_t nh, nf, np;  // run heads, flow heads, prioritized (all since the batch start)
+    uint32_t flag;        // run head seen
+    uint32_t cnt;         // prioritized since the last run head
+    int32_t mn, mx;       // min / max acquire since the last run head
 };
 
-__device__ __forceinline__ Agg agg_identity() { return Agg{0, 0, 0, 0, INT32_MAX, INT32_MIN}; }
+__device__ __forceinline__ Agg agg_identity() { return Agg{0, 0, 0, 0, 0, INT32_MAX, INT32_MIN}; }
 
 __device__ __forceinline__ Agg agg_combine(const Agg &a, const Agg &b) {
     Agg r;
     r.nh = a.nh + b.nh;
     r.nf = a.nf + b.nf;
+    r.np = a.np + b.np;
     r.flag = a.flag | b.flag;
     r.cnt = b.flag ? b.cnt : a.cnt + b.cnt;
     r.mn = b.flag ? b.mn : min(a.mn, b.mn);
@@ -142,16 +185,17 @@ __device__ __forceinline__ Agg agg_combine(const Agg &a, const Agg &b) {
     return r;
 }
 
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
+__device__ __forceinline__ uint32_t shfl_up_u32(uint32_t v, int o) { return (uint32_t)__shfl_up((int)v, o, 64); }
+
 __device__ __forceinline__ Agg agg_shfl_up(const Agg &v, int o) {
-    return Agg{(uint32_t)__shfl_up((int)v.nh, o, 64), (uint32_t)__shfl_up((int)v.nf, o, 64),
-               (uint32_t)__shfl_up((int)v.flag, o, 64), (uint32_t)__shfl_up((int)v.cnt, o, 64),
-               __shfl_up(v.mn, o, 64), __shfl_up(v.mx, o, 64)};
+    return Agg{shfl_up_u32(v.nh, o), shfl_up_u32(v.nf, o), shfl_up_u32(v.np, o), shfl_up_u32(v.flag, o),
+               shfl_up_u32(v.cnt, o), __shfl_up(v.mn, o, 64), __shfl_up(v.mx, o, 64)};
 }
 
 __device__ __forceinline__ Agg agg_shfl(const Agg &v, int src) {
-    return Agg{(uint32_t)__shfl((int)v.nh, src, 64), (uint32_t)__shfl((int)v.nf, src, 64),
-               (uint32_t)__shfl((int)v.flag, src, 64), (uint32_t)__shfl((int)v.cnt, src, 64),
-               __shfl(v.mn, src, 64), __shfl(v.mx, src, 64)};
+    return Agg{shfl_u32(v.nh, src), shfl_u32(v.nf, src), shfl_u32(v.np, src), shfl_u32(v.flag, src),
+               shfl_u32(v.cnt, src), __shfl(v.mn, src, 64), __shfl(v.mx, src, 64)};
 }
 
 // inclusive scan over the 64 lanes of a wave (lane order = element order)
@@ -164,81 +208,84 @@ __device__ __forceinline__ Agg wave_incl_scan(Agg x, int lane) {
     return x;
 }
 
+// ordered reduction of the 64 lanes (result valid in every lane)
+__device__ __forceinline__ Agg wave_reduce(Agg v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const Agg y = agg_shfl(v, (lane + o) & 63);
+        if (lane + o < 64 && (lane & (2 * o - 1)) == 0) v = agg_combine(v, y);
+    }
+    return agg_shfl(v, 0);
+}
+
+// Results-side scan value (a projection of Agg): run heads, prioritized since the run head,
+// elements since the run head.
+__device__ __forceinline__ RAgg ragg_combine(const RAgg &a, const RAgg &b) {
+    return RAgg{a.nh + b.nh, a.flag | b.flag, b.flag ? b.cnt : a.cnt + b.cnt};
+}
+
+// Blocked arrangement: a 512-thread workgroup per 4096-request tile, each thread folds 8
+// consecutive elements serially; only per-thread aggregates cross lanes (one wave scan per 512
+// requests instead of one per 64).
 constexpr int kRunThreads = 512;
-constexpr int kRunRounds = 8;                       // rounds of 64 per wave
+constexpr int kPerThread = 8;
 constexpr int kRunWaves = kRunThreads / 64;         // 8
-constexpr int kWaveElems = kRunRounds * 64;         // 512
+constexpr int kWaveElems = 64 * kPerThread;         // 512 consecutive requests per wave
 static_assert(kWaveElems * kRunWaves == kTileElems, "tile geometry");
 
-struct RunIn {
-    uint32_t key;
-    Payload q;
-};
+__device__ __forceinline__ uint64_t el_load(const uint64_t *el, uint32_t e, uint32_t nlim, uint32_t invalid_key) {
+    return e < nlim ? el[e] : ((uint64_t)invalid_key << kSlotShift);
+}
 
-__device__ __forceinline__ RunIn run_load(const uint32_t *keys, const Payload *pay, uint32_t e, uint32_t nlim,
-                                          uint32_t invalid_key) {
-    RunIn x;
-    if (e < nlim) {
-        x.key = keys[e];
-        x.q = pay[e];
+__device__ __forceinline__ void el_load_blk(const uint64_t *el, uint32_t e0, uint32_t nlim, uint32_t invalid_key,
+                                            uint64_t (&x)[kPerThread]) {
+    if (e0 + kPerThread <= nlim) {
+        const ulonglong2 *v = reinterpret_cast<const ulonglong2 *>(el + e0);
+#pragma unroll
+        for (int k = 0; k < kPerThread / 2; ++k) {
+            const ulonglong2 t = v[k];
+            x[2 * k] = t.x;
+            x[2 * k + 1] = t.y;
+        }
     } else {
-        x.key = invalid_key;
-        x.q = Payload{0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < kPerThread; ++k) x[k] = el_load(el, e0 + k, nlim, invalid_key);
     }
-    return x;
 }
-
-__device__ __forceinline__ RunIn run_shfl_up1(const RunIn &x) {
-    RunIn y;
-    y.key = (uint32_t)__shfl_up((int)x.key, 1, 64);
-    y.q.idx = (uint32_t)__shfl_up((int)x.q.idx, 1, 64);
-    y.q.ts_off = (uint32_t)__shfl_up((int)x.q.ts_off, 1, 64);
-    y.q.acq_prio = (uint32_t)__shfl_up((int)x.q.acq_prio, 1, 64);
-    y.q.bucket = (uint32_t)__shfl_up((int)x.q.bucket, 1, 64);
-    return y;
-}
-
-__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
 
 // Agg contribution of element x with predecessor px (has_prev = x is not element 0)
-__device__ __forceinline__ Agg run_value(const RunIn &x, const RunIn &px, bool has_prev, bool valid) {
+__device__ __forceinline__ Agg run_value(uint64_t x, uint64_t px, bool has_prev, bool valid) {
     if (!valid) return agg_identity();
-    const bool fh = !has_prev || x.key != px.key;
-    const bool h = fh || x.q.bucket != px.q.bucket;
-    const int32_t a = (int32_t)(x.q.acq_prio & 0x7FFFFFFFu);
-    return Agg{h ? 1u : 0u, fh ? 1u : 0u, h ? 1u : 0u, x.q.acq_prio >> 31, a, a};
+    const bool fh = !has_prev || el_slot(x) != el_slot(px);
+    const bool h = !has_prev || el_runkey(x) != el_runkey(px);
+    const int32_t a = el_acq(x);
+    const uint32_t p = el_prio(x);
+    return Agg{h ? 1u : 0u, fh ? 1u : 0u, p, h ? 1u : 0u, p, a, a};
 }
 
 // Per tile: aggregate over its valid elements + count of valid elements.
-__global__ __launch_bounds__(kRunThreads) void k_runs_up(const uint32_t *__restrict__ keys,
-                                                      const Payload *__restrict__ pay, uint32_t n,
+__global__ __launch_bounds__(kRunThreads) void k_runs_up(const uint64_t *__restrict__ el, uint32_t n,
                                                       uint32_t invalid_key, Agg *__restrict__ tile_agg,
                                                       uint32_t *__restrict__ tile_valid) {
     __shared__ Agg wagg[kRunWaves];
     __shared__ uint32_t wval[kRunWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t wb = blockIdx.x * kTileElems + wave * kWaveElems;
-    RunIn last = run_load(keys, pay, wb - 1, wb > 0 ? min(wb, n) : 0, invalid_key);  // element wb-1 (if any)
+    const uint32_t e0 = blockIdx.x * kTileElems + threadIdx.x * kPerThread;
+    uint64_t x[kPerThread];
+    el_load_blk(el, e0, n, invalid_key, x);
+    uint64_t px = el_load(el, e0 - 1, e0 > 0 ? min(e0, n) : 0, invalid_key);
     Agg acc = agg_identity();
     uint32_t nval = 0;
-    for (int r = 0; r < kRunRounds; ++r) {
-        const uint32_t e = wb + r * 64 + lane;
-        const RunIn x = run_load(keys, pay, e, n, invalid_key);
-        const bool valid = x.key != invalid_key;
-        RunIn px = run_shfl_up1(x);
-        if (lane == 0) px = last;
-        Agg v = run_value(x, px, e > 0, valid);
-        // ordered tree reduction: lane 0 ends with lanes 0..63 combined in order
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const Agg y = agg_shfl(v, (lane + o) & 63);
-            if (lane + o < 64 && (lane & (2 * o - 1)) == 0) v = agg_combine(v, y);
-        }
-        acc = agg_combine(acc, agg_shfl(v, 0));
-        nval += (uint32_t)__popcll(__ballot(valid));
-        last.key = shfl_u32(x.key, 63);
-        last.q.bucket = shfl_u32(x.q.bucket, 63);
+    for (int k = 0; k < kPerThread; ++k) {
+        const bool valid = el_slot(x[k]) != invalid_key;
+        acc = agg_combine(acc, run_value(x[k], px, e0 + k > 0, valid));
+        nval += valid ? 1u : 0u;
+        px = x[k];
     }
+    acc = wave_reduce(acc, lane);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nval += (uint32_t)__shfl_down((int)nval, o, 64);
     if (lane == 0) {
         wagg[wave] = acc;
         wval[wave] = nval;
@@ -292,7 +339,6 @@ __global__ __launch_bounds__(kTileScanThreads) void k_runs_tiles(const Agg *__re
         const Agg ex = block_excl_scan_1024(v, &total);
         if (t < ntiles) tile_carry[t] = agg_combine(carry, ex);
         carry = agg_combine(carry, total);
-        // valid counts: plain block sum
         uint32_t s = c;
         for (int o = 32; o > 0; o >>= 1) s += (uint32_t)__shfl_down((int)s, o, 64);
         __shared__ uint32_t ws[kTileScanThreads / 64];
@@ -309,88 +355,64 @@ __global__ __launch_bounds__(kTileScanThreads) void k_runs_tiles(const Agg *__re
     }
 }
 
-// Per tile: per-event run id and prioritized prefix; run and flow records.
-__global__ __launch_bounds__(kRunThreads) void k_runs_down(const uint32_t *__restrict__ keys,
-                                                        const Payload *__restrict__ pay, uint32_t invalid_key,
+// Per tile: run and flow records, the list of prioritized positions, and each wave's carry
+// (for k_results, which re-derives run ids and prioritized ranks instead of reading them).
+__global__ __launch_bounds__(kRunThreads) void k_runs_down(const uint64_t *__restrict__ el, uint32_t invalid_key,
                                                         const Agg *__restrict__ tile_carry, BatchScratch sc) {
     __shared__ Agg wagg[kRunWaves];
     const uint32_t nvalid = sc.counters[0];
     const uint32_t base = blockIdx.x * kTileElems;
     if (base >= nvalid) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t wb = base + wave * kWaveElems;
-    RunIn x[kRunRounds];
-    const RunIn first_prev = run_load(keys, pay, wb - 1, wb > 0 ? min(wb, nvalid) : 0, invalid_key);
-    RunIn last = first_prev;
+    const uint32_t e0 = base + threadIdx.x * kPerThread;
+    uint64_t x[kPerThread];
+    el_load_blk(el, e0, nvalid, invalid_key, x);
+    const uint64_t first_prev = el_load(el, e0 - 1, e0 > 0 ? min(e0, nvalid) : 0, invalid_key);
+    const uint64_t after = el_load(el, e0 + kPerThread, nvalid, invalid_key);
     Agg acc = agg_identity();
-    // pass 1: ordered wave reduction per round (elements stay in registers)
+    {
+        uint64_t px = first_prev;
 #pragma unroll
-    for (int r = 0; r < kRunRounds; ++r) {
-        const uint32_t e = wb + r * 64 + lane;
-        x[r] = run_load(keys, pay, e, nvalid, invalid_key);
-        RunIn px = run_shfl_up1(x[r]);
-        if (lane == 0) px = last;
-        Agg v = run_value(x[r], px, e > 0, e < nvalid);
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const Agg y = agg_shfl(v, (lane + o) & 63);
-            if (lane + o < 64 && (lane & (2 * o - 1)) == 0) v = agg_combine(v, y);
+        for (int k = 0; k < kPerThread; ++k) {
+            acc = agg_combine(acc, run_value(x[k], px, e0 + k > 0, e0 + k < nvalid));
+            px = x[k];
         }
-        acc = agg_combine(acc, agg_shfl(v, 0));
-        last.key = shfl_u32(x[r].key, 63);
-        last.q.bucket = shfl_u32(x[r].q.bucket, 63);
     }
-    if (lane == 0) wagg[wave] = acc;
+    const Agg incl = wave_incl_scan(acc, lane);
+    Agg excl = agg_shfl_up(incl, 1);
+    if (lane == 0) excl = agg_identity();
+    if (lane == 63) wagg[wave] = incl;
     __syncthreads();
     Agg carry = tile_carry[blockIdx.x];
     for (int w = 0; w < wave; ++w) carry = agg_combine(carry, wagg[w]);
-    // element after this wave's sub-tile (for the last element of the last round)
-    const uint32_t enext = wb + kWaveElems;
-    const RunIn after = run_load(keys, pay, enext, nvalid, invalid_key);
-    // pass 2: inclusive scan per round with the running carry
+    // results-side carry at the wave's first request
+    if (lane == 0) sc.wave_carry[blockIdx.x * kRunWaves + wave] = RAgg{carry.nh, carry.flag, carry.cnt};
+    Agg run = agg_combine(carry, excl);
+    uint64_t px = first_prev;
 #pragma unroll
-    for (int r = 0; r < kRunRounds; ++r) {
-        const uint32_t e = wb + r * 64 + lane;
-        // cross-lane reads are done by every lane (a shuffle from an inactive lane is undefined)
-        RunIn px = run_shfl_up1(x[r]);
-        const uint32_t prev_key = r == 0 ? first_prev.key : shfl_u32(x[r > 0 ? r - 1 : 0].key, 63);
-        const uint32_t prev_bucket = r == 0 ? first_prev.q.bucket : shfl_u32(x[r > 0 ? r - 1 : 0].q.bucket, 63);
-        uint32_t nkey = (uint32_t)__shfl_down((int)x[r].key, 1, 64);
-        uint32_t nbucket = (uint32_t)__shfl_down((int)x[r].q.bucket, 1, 64);
-        const uint32_t next_key = r + 1 < kRunRounds ? shfl_u32(x[r + 1 < kRunRounds ? r + 1 : r].key, 0) : after.key;
-        const uint32_t next_bucket =
-            r + 1 < kRunRounds ? shfl_u32(x[r + 1 < kRunRounds ? r + 1 : r].q.bucket, 0) : after.q.bucket;
-        if (lane == 0) {
-            px.key = prev_key;
-            px.q.bucket = prev_bucket;
-        }
-        if (lane == 63) {
-            nkey = next_key;
-            nbucket = next_bucket;
-        }
-        const Agg vr = wave_incl_scan(run_value(x[r], px, e > 0, e < nvalid), lane);
-        const Agg run = agg_combine(carry, vr);  // inclusive up to e
-        carry = agg_combine(carry, agg_shfl(vr, 63));
-        if (e >= nvalid) continue;
+    for (int k = 0; k < kPerThread; ++k) {
+        const uint32_t e = e0 + k;
+        if (e >= nvalid) break;
+        const uint64_t cur = x[k];
+        run = agg_combine(run, run_value(cur, px, e > 0, true));
         const uint32_t rid = run.nh - 1;
-        const uint32_t p = x[r].q.acq_prio >> 31;
-        sc.ev_run[e] = rid;
-        sc.ev_cp[e] = run.cnt - p;
-        const bool fh = e == 0 || x[r].key != px.key;
-        const bool h = fh || x[r].q.bucket != px.q.bucket;
+        const uint32_t p = el_prio(cur);
+        const bool fh = e == 0 || el_slot(cur) != el_slot(px);
+        const bool h = e == 0 || el_runkey(cur) != el_runkey(px);
         if (h) {
             sc.run_start[rid] = e;
-            sc.run_slot[rid] = x[r].key;
-            sc.run_t0off[rid] = x[r].q.ts_off;
+            sc.run_slot[rid] = el_slot(cur);
+            sc.run_idx0[rid] = el_idx(cur);
+            sc.run_p0[rid] = run.np - p;
         }
         if (fh) sc.flow_first_run[run.nf - 1] = rid;
-        const bool last_of_run = (e + 1 >= nvalid) || nkey != x[r].key || nbucket != x[r].q.bucket;
-        if (last_of_run) {
-            sc.run_end[rid] = e + 1;
+        if (p) sc.plist[run.np - 1] = e;
+        const uint64_t nx = k + 1 < kPerThread ? x[k + 1 < kPerThread ? k + 1 : k] : after;
+        if (e + 1 >= nvalid || el_runkey(nx) != el_runkey(cur)) {
             sc.run_cp[rid] = run.cnt;
-            sc.run_amin[rid] = run.mn;
-            sc.run_amax[rid] = run.mx;
+            sc.run_acq[rid] = (run.mn == run.mx) ? run.mn : 0;  // 0: mixed or escaped -> replay
         }
+        px = cur;
     }
 }
 
@@ -524,19 +546,6 @@ __device__ __forceinline__ bool pass_cond(double thr, double isec, int64_t sum, 
     return thr - (double)sum / isec - (double)a >= 0;
 }
 
-// G lanes per rule: lanes load the record's start/PASS/WAITING vectors in parallel, lane 0
-// of the group resolves the runs.  G = 1 (one rule per lane) keeps the most rules in flight.
-template <int G>
-__device__ __forceinline__ int64_t group_sum(int64_t v) {
-#pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) {
-        const int lo = __shfl_xor((int)(uint32_t)v, o, G);
-        const int hi = __shfl_xor((int)(uint32_t)((uint64_t)v >> 32), o, G);
-        v += (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-    }
-    return v;
-}
-
 // First k in [0, n] with !pass_cond(s0 + k*a): a closed-form guess corrected against the
 // exact predicate (monotone in k), so the result equals the sequential one.
 __device__ __forceinline__ uint32_t pass_prefix(double thr, double isec, int64_t s0, int32_t a, uint32_t n) {
@@ -558,312 +567,312 @@ __device__ __forceinline__ int64_t i64_hi(const int4 &v) {
     return (int64_t)(((uint64_t)(uint32_t)v.w << 32) | (uint32_t)v.z);
 }
 
-// One rule per lane, fused window update: the current bucket's seven counters are
-// loaded once (or start from zero when LeapArray.currentWindow rotates it), updated in
-// registers and stored once; the head bucket (LeapArray.getValidHead) is read from the
-// same vector loads as the window sums.  Same decisions as k_flows<G>.
-__global__ __launch_bounds__(kThreads) void k_flows1(ClusterState st, BatchScratch sc, const Payload *__restrict__ pay,
-                                                     int64_t ts_base, int simple, uint64_t *__restrict__ out) {
+// Closed form for one run of equal acquire counts (no escape) without clock regression: the
+// window is rotated once in registers (LeapArray.currentWindow incl. the occupy transfer of
+// ClusterMetricLeapArray.resetWindowTo), the valid buckets summed, the pass prefix and the
+// occupied (SHOULD_WAIT) count found over the exact Java predicates, and the current bucket's
+// seven counters stored once.  Returns false (nothing touched) when the run is not eligible.
+// floor(a / b) for 0 <= a, 0 < b through one double division and an exact correction
+// (a < 2^53); the int64 division sequence costs many more registers and cycles.
+__device__ __forceinline__ int64_t div_pos(int64_t a, int64_t b) {
+    if (a >= ((int64_t)1 << 53)) return a / b;
+    int64_t q = (int64_t)((double)a / (double)b);
+    const int64_t r = a - q * b;
+    if (r < 0) --q;
+    else if (r >= b) ++q;
+    return q;
+}
+
+struct RunIn {
+    uint32_t j0, n, cp_tot, p0;
+    int32_t a;
+    int64_t t0;
+};
+
+__device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &sc, uint32_t s, const SlotParam &P,
+                                         const Rec &R, double thr, const RunIn &ri, uint32_t r) {
+    const int64_t t0 = ri.t0;
+    const int32_t a = ri.a;
+    const int64_t q = div_pos(t0, P.W);  // bucket number
+    const int64_t ws = q * P.W;
+    const int64_t qs = div_pos(q, P.S);
+    const int cj = (int)(q - qs * P.S);
+    const int jh = cj + 1 == P.S ? 0 : cj + 1;  // LeapArray.getValidHead index ((t0 + W) / W) % S
+    const int64_t old = R.start(cj);
+    if (a <= 0 || (old != kAbsent && ws < old)) return false;
+    if (ri.cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) return false;
+    int64_t bp = 0, hstart = kAbsent, hpass = 0;
+    uint32_t vmask = 0;  // valid buckets other than the current one
+    if ((P.S & 1) == 0) {
+        const int4 *v = reinterpret_cast<const int4 *>(R.r);
+        const int hs = P.S >> 1;
+        for (int q = 0; q < hs; ++q) {
+            const int4 st2 = v[q], ps2 = v[hs + q];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int jj = 2 * q + h;
+                const int64_t w = h ? i64_hi(st2) : i64_lo(st2);
+                const int64_t pv = h ? i64_hi(ps2) : i64_lo(ps2);
+                if (jj == jh) {
+                    hstart = w;
+                    hpass = pv;
+                }
+                if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
+                    bp += pv;
+                    vmask |= 1u << (jj & 31);
+                }
+            }
+        }
+    } else {
+        for (int jj = 0; jj < P.S; ++jj) {
+            const int64_t w = R.start(jj);
+            const int64_t pv = R.cnt(CEV_PASS, jj);
+            if (jj == jh) {
+                hstart = w;
+                hpass = pv;
+            }
+            if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
+                bp += pv;
+                vmask |= 1u << (jj & 31);
+            }
+        }
+    }
+    const bool rot = old == kAbsent || ws > old;
+    int64_t c[CEV_N];
+    SlotOcc o{0, 0, 0, 0};
+    bool occ_loaded = false, occ_dirty = false;
+    if (rot) {
+#pragma unroll
+        for (int k = 0; k < CEV_N; ++k) c[k] = 0;
+        if (old != kAbsent) {  // resetWindowTo + transferOccupyToBucket
+            o = st.occ[s];
+            occ_loaded = true;
+            if (o.has_occ) {
+                c[CEV_OCCUPIED_PASS] += o.occ_pass;
+                c[CEV_PASS] += o.occ_pass;
+                c[CEV_PASS_REQUEST] += o.occ_preq;
+                o.occ_pass = 0;
+                o.occ_preq = 0;
+                o.has_occ = 0;
+                occ_dirty = true;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < CEV_N; ++k) c[k] = R.cnt(k, cj);
+    }
+    int64_t head;  // getValidHead after the rotation (the head is the current bucket when S == 1)
+    if (jh == cj) head = c[CEV_PASS];
+    else head = (hstart != kAbsent && !(t0 - hstart > (int64_t)P.interval)) ? hpass : 0;
+    const int64_t s0 = bp + c[CEV_PASS];
+    const uint32_t n = ri.n;
+    const uint32_t f = pass_prefix(thr, P.isec, s0, a, n);
+    // prioritized requests among the first f: the run's prioritized positions are
+    // plist[p0 .. p0 + cp_tot) (ascending)
+    uint32_t cpf = ri.cp_tot;
+    if (f < n && ri.cp_tot > 0) {
+        uint32_t lo = 0, hi = ri.cp_tot;
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (sc.plist[ri.p0 + m] < ri.j0 + f) lo = m + 1;
+            else hi = m;
+        }
+        cpf = lo;
+    }
+    const uint32_t np_after = ri.cp_tot - cpf;
+    uint32_t cw = 0;
+    if (np_after > 0) {
+        // WAITING over the same valid buckets (only runs with prioritized blocked requests read it)
+        int64_t w0 = c[CEV_WAITING];
+        for (int jj = 0; jj < P.S; ++jj)
+            if (vmask & (1u << (jj & 31))) w0 += R.cnt(CEV_WAITING, jj);
+        if (!occ_loaded) o = st.occ[s];
+        const double latest = (double)(s0 + (int64_t)f * a) / P.isec;
+        const double lim = st.max_occupy_ratio * thr;
+        const int64_t occ0 = o.occ_pass;
+        uint32_t l2 = 0, h2 = np_after;
+        while (l2 < h2) {
+            const uint32_t cc = l2 + ((h2 - l2) >> 1);
+            const int64_t add = (int64_t)cc * a;
+            const bool ok = ((double)(w0 + add) / P.isec <= lim) &&
+                            (latest + (double)((int64_t)a + occ0 + add) - (double)head <= thr);
+            if (ok) l2 = cc + 1;
+            else h2 = cc;
+        }
+        cw = l2;
+        if (cw > 0) {
+            o.occ_pass += (int64_t)cw * a;
+            o.occ_preq += cw;
+            o.has_occ = 1;
+            occ_dirty = true;
+        }
+    }
+    const uint32_t nblk = n - f - cw;
+    c[CEV_PASS] += (int64_t)f * a;
+    c[CEV_PASS_REQUEST] += f;
+    c[CEV_OCCUPIED_PASS] += (int64_t)cpf * a;
+    c[CEV_WAITING] += (int64_t)cw * a;
+    c[CEV_BLOCK] += (int64_t)nblk * a;
+    c[CEV_BLOCK_REQUEST] += nblk;
+    c[CEV_OCCUPIED_BLOCK] += (int64_t)(np_after - cw) * a;
+    if (rot) R.start(cj) = ws;
+#pragma unroll
+    for (int k = 0; k < CEV_N; ++k) R.cnt(k, cj) = c[k];
+    if (occ_dirty) st.occ[s] = o;
+    RunOut ro;
+    ro.s0 = s0;
+    ro.thr = thr;
+    ro.isec = P.isec;
+    ro.f = f;
+    ro.cpf = cpf;
+    ro.cw = cw;
+    ro.wait = (uint16_t)(1000 / P.S);
+    ro.mode = RUN_FAST;
+    sc.run_out[r] = ro;
+    return true;
+}
+
+__device__ __forceinline__ RunIn run_in(const BatchScratch &sc, const uint32_t *ts_off, int64_t ts_base, uint32_t r,
+                                        uint32_t nruns, uint32_t nvalid) {
+    RunIn ri;
+    ri.j0 = sc.run_start[r];
+    ri.n = (r + 1 < nruns ? sc.run_start[r + 1] : nvalid) - ri.j0;
+    ri.cp_tot = sc.run_cp[r];
+    ri.p0 = sc.run_p0[r];
+    ri.a = sc.run_acq[r];
+    ri.t0 = ts_base + (int64_t)ts_off[sc.run_idx0[r]];
+    return ri;
+}
+
+// One rule per lane walks the rule's runs in time order, closed form only.  At the first run
+// that needs the per-request replay the rest of the rule is deferred to k_flows_slow (rare), so
+// this kernel stays small and keeps many rules in flight.
+__global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratch sc,
+                                                    const uint32_t *__restrict__ ts_off, int64_t ts_base,
+                                                    int simple) {
     const uint32_t nflows = sc.counters[2];
     const uint32_t nruns = sc.counters[1];
+    const uint32_t nvalid = sc.counters[0];
     for (uint32_t fl = blockIdx.x * kThreads + threadIdx.x; fl < nflows; fl += gridDim.x * kThreads) {
         const uint32_t r0 = sc.flow_first_run[fl];
         const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        const uint32_t s = sc.run_slot[r0];
+        const SlotParam P = st.param[s];
+        const Rec R = rec_of(st, P);
+        const double thr = simple ? P.thr_simple : P.thr;
         for (uint32_t r = r0; r < r1; ++r) {
-            const uint32_t s = sc.run_slot[r];
-            const SlotParam P = st.param[s];
-            const Rec R = rec_of(st, P);
-            const uint32_t j0 = sc.run_start[r], j1 = sc.run_end[r];
-            const uint32_t n = j1 - j0;
-            const int64_t t0 = ts_base + (int64_t)sc.run_t0off[r];
-            const uint32_t cp_tot = sc.run_cp[r];
-            const int32_t a = sc.run_amin[r];
-            const double thr = simple ? P.thr_simple : P.thr;
-            const int64_t ws = t0 - t0 % P.W;
-            const int cj = (int)((t0 / P.W) % P.S);
-            const int64_t old = R.start(cj);
-            bool fast = (a == sc.run_amax[r]) && !(old != kAbsent && ws < old);
-            if (cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) fast = false;
-            if (!fast) {  // exact replay of every request of the run, in order
-                for (uint32_t j = j0; j < j1; ++j) {
-                    const Payload q = pay[j];
-                    const int64_t t = ts_base + (int64_t)q.ts_off;
-                    out[q.idx] = request_exact(st, s, t, (int32_t)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
-                                               simple);
-                }
-                sc.run_mode[r] = RUN_DONE;
-                continue;
+            const RunIn ri = run_in(sc, ts_off, ts_base, r, nruns, nvalid);
+            if (!run_fast(st, sc, s, P, R, thr, ri, r)) {
+                const uint32_t k = atomicAdd(&sc.counters[6], 1u);
+                sc.deferred[2 * k] = fl;
+                sc.deferred[2 * k + 1] = r;
+                break;
             }
-            const int jh = (int)(((t0 + P.W) / P.W) % P.S);  // LeapArray.getValidHead index
-            int64_t bp = 0, bw = 0, hstart = kAbsent, hpass = 0;
-            if ((P.S & 1) == 0) {
-                const int4 *v = reinterpret_cast<const int4 *>(R.r);
-                const int hs = P.S >> 1;
-                for (int q = 0; q < hs; ++q) {
-                    const int4 st2 = v[q], ps2 = v[hs + q], wt2 = v[2 * hs + q];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int jj = 2 * q + h;
-                        const int64_t w = h ? i64_hi(st2) : i64_lo(st2);
-                        const int64_t pv = h ? i64_hi(ps2) : i64_lo(ps2);
-                        if (jj == jh) {
-                            hstart = w;
-                            hpass = pv;
-                        }
-                        if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
-                            bp += pv;
-                            bw += h ? i64_hi(wt2) : i64_lo(wt2);
-                        }
-                    }
-                }
-            } else {
-                for (int jj = 0; jj < P.S; ++jj) {
-                    const int64_t w = R.start(jj);
-                    const int64_t pv = R.cnt(CEV_PASS, jj);
-                    if (jj == jh) {
-                        hstart = w;
-                        hpass = pv;
-                    }
-                    if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
-                        bp += pv;
-                        bw += R.cnt(CEV_WAITING, jj);
-                    }
-                }
-            }
-            // ---- LeapArray.currentWindow(t0) on the current bucket, in registers
-            const bool rot = old == kAbsent || ws > old;
-            int64_t c[CEV_N];
-            SlotOcc o{0, 0, 0};
-            bool occ_dirty = false;
-            if (rot) {
-#pragma unroll
-                for (int k = 0; k < CEV_N; ++k) c[k] = 0;
-                if (old != kAbsent) {  // resetWindowTo + transferOccupyToBucket
-                    o = st.occ[s];
-                    if (o.has_occ) {
-                        c[CEV_OCCUPIED_PASS] += o.occ_pass;
-                        c[CEV_PASS] += o.occ_pass;
-                        c[CEV_PASS_REQUEST] += o.occ_preq;
-                        o.occ_pass = 0;
-                        o.occ_preq = 0;
-                        o.has_occ = 0;
-                        occ_dirty = true;
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < CEV_N; ++k) c[k] = R.cnt(k, cj);
-            }
-            // getValidHead after the rotation (the head is the current bucket when S == 1)
-            int64_t head;
-            if (jh == cj) head = c[CEV_PASS];
-            else head = (hstart != kAbsent && !(t0 - hstart > (int64_t)P.interval)) ? hpass : 0;
-            const int64_t s0 = bp + c[CEV_PASS];
-            const int64_t w0 = bw + c[CEV_WAITING];
-            const uint32_t f = pass_prefix(thr, P.isec, s0, a, n);
-            const uint32_t cpf = (f >= n) ? cp_tot : (cp_tot ? sc.ev_cp[j0 + f] : 0u);
-            const uint32_t np_after = cp_tot - cpf;
-            uint32_t cw = 0;
-            if (np_after > 0) {
-                if (!occ_dirty && !rot) o = st.occ[s];
-                else if (!occ_dirty) o = st.occ[s];
-                const double latest = (double)(s0 + (int64_t)f * a) / P.isec;
-                const double lim = st.max_occupy_ratio * thr;
-                const int64_t occ0 = o.occ_pass;
-                uint32_t l2 = 0, h2 = np_after;
-                while (l2 < h2) {
-                    const uint32_t cc = l2 + ((h2 - l2) >> 1);
-                    const int64_t add = (int64_t)cc * a;
-                    const bool ok = ((double)(w0 + add) / P.isec <= lim) &&
-                                    (latest + (double)((int64_t)a + occ0 + add) - (double)head <= thr);
-                    if (ok) l2 = cc + 1;
-                    else h2 = cc;
-                }
-                cw = l2;
-                if (cw > 0) {
-                    o.occ_pass += (int64_t)cw * a;
-                    o.occ_preq += cw;
-                    o.has_occ = 1;
-                    occ_dirty = true;
-                }
-            }
-            const int64_t wa = (int64_t)cw * a;
-            const uint32_t nblk = n - f - cw;
-            c[CEV_PASS] += (int64_t)f * a;
-            c[CEV_PASS_REQUEST] += f;
-            c[CEV_OCCUPIED_PASS] += (int64_t)cpf * a;
-            c[CEV_WAITING] += wa;
-            c[CEV_BLOCK] += (int64_t)nblk * a;
-            c[CEV_BLOCK_REQUEST] += nblk;
-            c[CEV_OCCUPIED_BLOCK] += (int64_t)(np_after - cw) * a;
-            if (rot) R.start(cj) = ws;
-#pragma unroll
-            for (int k = 0; k < CEV_N; ++k) R.cnt(k, cj) = c[k];
-            if (occ_dirty) st.occ[s] = o;
-            sc.run_s0[r] = s0;
-            sc.run_f[r] = f;
-            sc.run_cpf[r] = cpf;
-            sc.run_cw[r] = cw;
-            sc.run_thr[r] = thr;
-            sc.run_isec[r] = P.isec;
-            sc.run_wait[r] = 1000 / P.S;
-            sc.run_mode[r] = RUN_FAST;
         }
     }
 }
 
-template <int G>
-__global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratch sc, const Payload *__restrict__ pay,
-                                                    int64_t ts_base, int simple, uint64_t *__restrict__ out) {
+// Deferred rules: from the deferred run on, every run is resolved in closed form when eligible,
+// otherwise replayed request by request (request_exact) from the original arrays.
+__global__ __launch_bounds__(kThreads) void k_flows_slow(ClusterState st, BatchScratch sc,
+                                                         const int32_t *__restrict__ acquire,
+                                                         const uint8_t *__restrict__ prio,
+                                                         const uint32_t *__restrict__ ts_off, int64_t ts_base,
+                                                         const uint64_t *__restrict__ el, int simple,
+                                                         uint64_t *__restrict__ out) {
+    const uint32_t ndef = sc.counters[6];
     const uint32_t nflows = sc.counters[2];
     const uint32_t nruns = sc.counters[1];
-    const int gl = threadIdx.x & (G - 1);
-    const uint32_t groups_per_block = kThreads / G;
-    const uint32_t stride = gridDim.x * groups_per_block;
-    for (uint32_t fl = blockIdx.x * groups_per_block + threadIdx.x / G; fl < nflows; fl += stride) {
-        const uint32_t r0 = sc.flow_first_run[fl];
+    const uint32_t nvalid = sc.counters[0];
+    for (uint32_t d = blockIdx.x * kThreads + threadIdx.x; d < ndef; d += gridDim.x * kThreads) {
+        const uint32_t fl = sc.deferred[2 * d], rd = sc.deferred[2 * d + 1];
         const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
-        for (uint32_t r = r0; r < r1; ++r) {
-            const uint32_t s = sc.run_slot[r];
-            const SlotParam P = st.param[s];
-            const Rec R = rec_of(st, P);
-            const uint32_t j0 = sc.run_start[r], j1 = sc.run_end[r];
-            const uint32_t n = j1 - j0;
-            const int64_t t0 = ts_base + (int64_t)sc.run_t0off[r];
-            const uint32_t cp_tot = sc.run_cp[r];
-            const int32_t a = sc.run_amin[r];
-            const double thr = simple ? P.thr_simple : P.thr;
-            // ---- fast path eligibility: equal acquire counts, no clock regression,
-            //      prioritized requests only where the occupy path is regular
-            const int64_t ws = t0 - t0 % P.W;
-            const int cj = (int)((t0 / P.W) % P.S);
-            const int64_t old = R.start(cj);
-            bool fast = (a == sc.run_amax[r]) && !(old != kAbsent && ws < old);
-            if (cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) fast = false;
-            if (!fast) {
-                if (gl == 0) {  // exact replay of every request of the run, in order
-                    for (uint32_t j = j0; j < j1; ++j) {
-                        const Payload q = pay[j];
-                        const int64_t t = ts_base + (int64_t)q.ts_off;
-                        out[q.idx] = request_exact(st, s, t, (int32_t)(q.acq_prio & 0x7FFFFFFFu),
-                                                   (q.acq_prio >> 31) != 0, simple);
-                    }
-                    sc.run_mode[r] = RUN_DONE;
-                    __threadfence_block();
-                }
-                continue;
+        const uint32_t s = sc.run_slot[rd];
+        const SlotParam P = st.param[s];
+        const Rec R = rec_of(st, P);
+        const double thr = simple ? P.thr_simple : P.thr;
+        for (uint32_t r = rd; r < r1; ++r) {
+            const RunIn ri = run_in(sc, ts_off, ts_base, r, nruns, nvalid);
+            if (r > rd && run_fast(st, sc, s, P, R, thr, ri, r)) continue;
+            for (uint32_t j = ri.j0; j < ri.j0 + ri.n; ++j) {
+                const uint32_t i = el_idx(el[j]);
+                const int64_t t = ts_base + (int64_t)ts_off[i];
+                const bool p = !simple && prio && prio[i];
+                out[i] = request_exact(st, s, t, acquire[i], p, simple);
             }
-            // ---- window sums over the valid buckets other than the current one (rotation of the
-            //      current bucket does not touch them); lanes split the buckets
-            int64_t bp = 0, bw = 0;
-            if (G == 1 && (P.S & 1) == 0) {
-                // start / PASS / WAITING vectors are contiguous and 16-B aligned: pairwise loads
-                const int4 *v = reinterpret_cast<const int4 *>(R.r);
-                const int hs = P.S >> 1;
-                for (int q = 0; q < hs; ++q) {
-                    const int4 st2 = v[q], ps2 = v[hs + q], wt2 = v[2 * hs + q];
-                    const int64_t w0 = (int64_t)(((uint64_t)(uint32_t)st2.y << 32) | (uint32_t)st2.x);
-                    const int64_t w1 = (int64_t)(((uint64_t)(uint32_t)st2.w << 32) | (uint32_t)st2.z);
-                    const int j0 = 2 * q, j1 = 2 * q + 1;
-                    if (j0 != cj && w0 != kAbsent && !(t0 - w0 > (int64_t)P.interval)) {
-                        bp += (int64_t)(((uint64_t)(uint32_t)ps2.y << 32) | (uint32_t)ps2.x);
-                        bw += (int64_t)(((uint64_t)(uint32_t)wt2.y << 32) | (uint32_t)wt2.x);
-                    }
-                    if (j1 != cj && w1 != kAbsent && !(t0 - w1 > (int64_t)P.interval)) {
-                        bp += (int64_t)(((uint64_t)(uint32_t)ps2.w << 32) | (uint32_t)ps2.z);
-                        bw += (int64_t)(((uint64_t)(uint32_t)wt2.w << 32) | (uint32_t)wt2.z);
-                    }
-                }
-            } else {
-                for (int jj = gl; jj < P.S; jj += G) {
-                    const int64_t w = R.start(jj);
-                    if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
-                        bp += R.cnt(CEV_PASS, jj);
-                        bw += R.cnt(CEV_WAITING, jj);
-                    }
-                }
-            }
-            const int64_t base_pass = group_sum<G>(bp);
-            const int64_t base_wait = group_sum<G>(bw);
-            if (gl != 0) continue;
-            // ---- lane 0: rotate the current window (LeapArray.currentWindow(t0)), then resolve
-            cur_window(st, P, s, t0);
-            const int64_t head = head_pass(st, P, t0);
-            const int64_t s0 = base_pass + R.cnt(CEV_PASS, cj);
-            const int64_t w0 = base_wait + R.cnt(CEV_WAITING, cj);
-            // pass prefix: first i with !cond(s0 + i*a, a)   (monotone in i)
-            const uint32_t f = pass_prefix(thr, P.isec, s0, a, n);
-            const uint32_t cpf = (f >= n) ? cp_tot : (cp_tot ? sc.ev_cp[j0 + f] : 0u);
-            const uint32_t np_after = cp_tot - cpf;
-            // occupied prefix among prioritized blocked requests (monotone in the count)
-            uint32_t cw = 0;
-            if (np_after > 0) {
-                const double latest = (double)(s0 + (int64_t)f * a) / P.isec;
-                const double lim = st.max_occupy_ratio * thr;
-                const int64_t occ0 = st.occ[s].occ_pass;
-                uint32_t l2 = 0, h2 = np_after;
-                while (l2 < h2) {
-                    const uint32_t c = l2 + ((h2 - l2) >> 1);
-                    const int64_t add = (int64_t)c * a;
-                    const bool ok = ((double)(w0 + add) / P.isec <= lim) &&
-                                    (latest + (double)((int64_t)a + occ0 + add) - (double)head <= thr);
-                    if (ok) l2 = c + 1;
-                    else h2 = c;
-                }
-                cw = l2;
-            }
-            // counters of the current bucket
-            const int64_t wa = (int64_t)cw * a;
-            const uint32_t nblk = n - f - cw;
-            R.cnt(CEV_PASS, cj) += (int64_t)f * a;
-            R.cnt(CEV_PASS_REQUEST, cj) += f;
-            R.cnt(CEV_OCCUPIED_PASS, cj) += (int64_t)cpf * a;
-            R.cnt(CEV_WAITING, cj) += wa;
-            R.cnt(CEV_BLOCK, cj) += (int64_t)nblk * a;
-            R.cnt(CEV_BLOCK_REQUEST, cj) += nblk;
-            R.cnt(CEV_OCCUPIED_BLOCK, cj) += (int64_t)(np_after - cw) * a;
-            if (cw > 0) {
-                SlotOcc &o = st.occ[s];
-                o.occ_pass += wa;
-                o.occ_preq += cw;
-                o.has_occ = 1;
-            }
-            sc.run_s0[r] = s0;
-            sc.run_f[r] = f;
-            sc.run_cpf[r] = cpf;
-            sc.run_cw[r] = cw;
-            sc.run_thr[r] = thr;
-            sc.run_isec[r] = P.isec;
-            sc.run_wait[r] = 1000 / P.S;
-            sc.run_mode[r] = RUN_FAST;
-            __threadfence_block();  // the group's lanes re-read this record for the rule's next run
+            RunOut ro;
+            ro.mode = RUN_DONE;
+            sc.run_out[r] = ro;
         }
     }
 }
 
 // ---------------------------------------------------------------- results
-__global__ __launch_bounds__(kThreads) void k_results(ClusterState st, BatchScratch sc, const uint32_t *__restrict__ keys,
-                                                      const Payload *__restrict__ pay, int simple,
-                                                      uint64_t *__restrict__ out) {
+// Same tile geometry as k_runs_down; each wave starts from the carry k_runs_down stored and
+// re-derives every request's run id and prioritized rank, then writes its TokenResult.
+__global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const uint64_t *__restrict__ el,
+                                                         uint32_t invalid_key, uint64_t *__restrict__ out) {
     const uint32_t nvalid = sc.counters[0];
-    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
-    if (j >= nvalid) return;
-    const uint32_t r = sc.ev_run[j];
-    if (sc.run_mode[r] != RUN_FAST) return;
-    const Payload q = pay[j];
-    const uint32_t local = j - sc.run_start[r];
-    const uint32_t f = sc.run_f[r];
-    const int32_t a = (int32_t)(q.acq_prio & 0x7FFFFFFFu);
-    uint64_t res;
-    if (local < f) {
-        const int64_t sum = sc.run_s0[r] + (int64_t)local * a;
-        res = pack_result(TRS_OK, j_d2i(sc.run_thr[r] - (double)sum / sc.run_isec[r] - (double)a), 0);
-    } else if ((q.acq_prio >> 31) && sc.ev_cp[j] - sc.run_cpf[r] < sc.run_cw[r]) {
-        res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)sc.run_wait[r]);
-    } else {
-        res = pack_result(TRS_BLOCKED, 0, 0);
+    const uint32_t base = blockIdx.x * kTileElems;
+    if (base >= nvalid) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (base + wave * kWaveElems >= nvalid) return;
+    const uint32_t e0 = base + threadIdx.x * kPerThread;
+    uint64_t x[kPerThread];
+    el_load_blk(el, e0, nvalid, invalid_key, x);
+    const uint64_t first_prev = el_load(el, e0 - 1, e0 > 0 ? min(e0, nvalid) : 0, invalid_key);
+    RAgg acc{0, 0, 0};
+    {
+        uint64_t px = first_prev;
+#pragma unroll
+        for (int k = 0; k < kPerThread; ++k) {
+            const uint32_t e = e0 + k;
+            const bool valid = e < nvalid;
+            const bool h = valid && (e == 0 || el_runkey(x[k]) != el_runkey(px));
+            acc = ragg_combine(acc, RAgg{h ? 1u : 0u, h ? 1u : 0u, valid ? el_prio(x[k]) : 0u});
+            px = x[k];
+        }
     }
-    out[q.idx] = res;
+    RAgg v = acc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const RAgg y{shfl_up_u32(v.nh, o), shfl_up_u32(v.flag, o), shfl_up_u32(v.cnt, o)};
+        if (lane >= o) v = ragg_combine(y, v);
+    }
+    RAgg excl{shfl_up_u32(v.nh, 1), shfl_up_u32(v.flag, 1), shfl_up_u32(v.cnt, 1)};
+    if (lane == 0) excl = RAgg{0, 0, 0};
+    RAgg run = ragg_combine(sc.wave_carry[blockIdx.x * kRunWaves + wave], excl);
+    uint64_t px = first_prev;
+    uint32_t cur_rid = 0xFFFFFFFFu, rstart = 0;
+    RunOut ro;
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) {
+        const uint32_t e = e0 + k;
+        if (e >= nvalid) break;
+        const bool h = e == 0 || el_runkey(x[k]) != el_runkey(px);
+        const uint32_t p = el_prio(x[k]);
+        run = ragg_combine(run, RAgg{h ? 1u : 0u, h ? 1u : 0u, p});
+        px = x[k];
+        const uint32_t rid = run.nh - 1;
+        if (rid != cur_rid) {
+            cur_rid = rid;
+            ro = sc.run_out[rid];
+            rstart = sc.run_start[rid];
+        }
+        if (ro.mode != RUN_FAST) continue;
+        const uint32_t local = e - rstart;
+        const int32_t a = el_acq(x[k]);
+        uint64_t res;
+        if (local < ro.f) {
+            const int64_t sum = ro.s0 + (int64_t)local * a;
+            res = pack_result(TRS_OK, j_d2i(ro.thr - (double)sum / ro.isec - (double)a), 0);
+        } else if (p && (run.cnt - p) - ro.cpf < ro.cw) {
+            res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)ro.wait);
+        } else {
+            res = pack_result(TRS_BLOCKED, 0, 0);
+        }
+        out[el_idx(x[k])] = res;
+    }
 }
 
 __global__ void k_metric_sums(ClusterState st, uint32_t s, int64_t now, int64_t *out7) {
@@ -899,11 +908,11 @@ __global__ void k_init_slots(ClusterState st, const uint32_t *slots, uint32_t n)
 // One thread walks the runs in order; rejected requests get TOO_MANY_REQUEST and leave the batch.
 constexpr int kLimW = 100, kLimN = 10, kLimInterval = 1000;
 
-__global__ __launch_bounds__(kThreads) void k_lim_flag(ClusterState st, const uint32_t *__restrict__ keys, uint32_t n,
+__global__ __launch_bounds__(kThreads) void k_lim_flag(ClusterState st, const uint64_t *__restrict__ el, uint32_t n,
                                                        uint32_t invalid, int32_t ns, uint32_t *__restrict__ flag) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
     if (i >= n) return;
-    const uint32_t k = keys[i];
+    const uint32_t k = el_slot(el[i]);
     flag[i] = (k != invalid && st.param[k].ns == ns) ? 1u : 0u;
 }
 
@@ -987,7 +996,7 @@ __global__ __launch_bounds__(kThreads) void k_lim_apply(const uint32_t *__restri
                                                         const uint32_t *__restrict__ ridx,
                                                         const uint32_t *__restrict__ rstart,
                                                         const uint32_t *__restrict__ rpass, const uint32_t *counters,
-                                                        uint32_t n, uint32_t invalid, uint32_t *__restrict__ keys,
+                                                        uint32_t n, uint32_t invalid, uint64_t *__restrict__ el,
                                                         uint64_t *__restrict__ out) {
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
     const uint32_t m = counters[4];
@@ -995,7 +1004,7 @@ __global__ __launch_bounds__(kThreads) void k_lim_apply(const uint32_t *__restri
     const uint32_t r = ridx[j] + head[j] - 1;
     if (j - rstart[r] >= rpass[r]) {
         const uint32_t i = list[j];
-        keys[i] = invalid;
+        el[i] = (uint64_t)invalid << kSlotShift;
         out[i] = pack_result(TRS_TOO_MANY_REQUEST, 0, 0);
     }
 }
@@ -1012,12 +1021,12 @@ __global__ void k_lim_init(NsLimiterDev *L) {
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// the radix digit width depends on the live slot count: size for the worst width
+// the radix digit width depends on the live slot count: size for the widest
 static size_t max_hist_entries(size_t cap, uint32_t nslots_cap) {
     int bits = 1;
     while (((uint64_t)1 << bits) < (uint64_t)nslots_cap + 1) ++bits;
     size_t m = 0;
-    for (int b = 1; b <= bits; ++b) m = std::max(m, radix_hist_entries(cap, b));
+    for (int b = 1; b <= bits; ++b) m = std::max(m, ((size_t)1 << radix64_digit_bits(b)) * radix64_tiles(cap));
     return m;
 }
 
@@ -1025,14 +1034,12 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     const size_t ntiles = (cap + kTileElems - 1) / kTileElems + 1;
     const size_t hist = max_hist_entries(cap, nslots_cap);
     size_t b = 0;
-    b += 2 * align_up(cap * 4) + 2 * align_up(cap * sizeof(Payload));
-    b += 2 * align_up(cap * 4);                 // ev_run, ev_cp
-    b += 8 * align_up(cap * 4);                 // run_* u32/i32
-    b += align_up(cap * 8);                     // run_s0
-    b += 4 * align_up(cap * 4);                 // run_f, run_cpf, run_cw, run_wait
-    b += 2 * align_up(cap * 8);                 // run_thr, run_isec
-    b += align_up(cap);                         // run_mode
-    b += align_up(cap * 4);                     // flow_first_run
+    b += 2 * align_up(cap * 8);                 // elements (double buffer)
+    b += 7 * align_up((cap + 1) * 4);           // run_start/slot/idx0/cp/p0/acq, flow_first_run
+    b += align_up(cap * 4);                     // plist
+    b += align_up(cap * 8);                     // deferred (flow, run)
+    b += align_up(cap * sizeof(RunOut));        // run_out
+    b += align_up(ntiles * kRunWaves * sizeof(RAgg));
     b += 2 * align_up(ntiles * sizeof(Agg)) + align_up(ntiles * 4);
     b += align_up(64);
     b += 2 * align_up(hist * 4) + align_up(scan_partials_needed(hist) * 4 + 64);
@@ -1049,29 +1056,19 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
         p += align_up(bytes);
         return r;
     };
-    sc.keys[0] = (uint32_t *)take(cap * 4);
-    sc.keys[1] = (uint32_t *)take(cap * 4);
-    sc.pay[0] = (Payload *)take(cap * sizeof(Payload));
-    sc.pay[1] = (Payload *)take(cap * sizeof(Payload));
-    sc.ev_run = (uint32_t *)take(cap * 4);
-    sc.ev_cp = (uint32_t *)take(cap * 4);
-    sc.run_start = (uint32_t *)take(cap * 4);
-    sc.run_end = (uint32_t *)take(cap * 4);
-    sc.run_slot = (uint32_t *)take(cap * 4);
-    sc.run_t0off = (uint32_t *)take(cap * 4);
-    sc.run_cp = (uint32_t *)take(cap * 4);
-    sc.run_amin = (int32_t *)take(cap * 4);
-    sc.run_amax = (int32_t *)take(cap * 4);
-    (void)take(cap * 4);
-    sc.run_s0 = (int64_t *)take(cap * 8);
-    sc.run_f = (uint32_t *)take(cap * 4);
-    sc.run_cpf = (uint32_t *)take(cap * 4);
-    sc.run_cw = (uint32_t *)take(cap * 4);
-    sc.run_wait = (uint32_t *)take(cap * 4);
-    sc.run_thr = (double *)take(cap * 8);
-    sc.run_isec = (double *)take(cap * 8);
-    sc.run_mode = (uint8_t *)take(cap);
-    sc.flow_first_run = (uint32_t *)take(cap * 4);
+    sc.el[0] = (uint64_t *)take(cap * 8);
+    sc.el[1] = (uint64_t *)take(cap * 8);
+    sc.run_start = (uint32_t *)take((cap + 1) * 4);
+    sc.run_slot = (uint32_t *)take((cap + 1) * 4);
+    sc.run_idx0 = (uint32_t *)take((cap + 1) * 4);
+    sc.run_cp = (uint32_t *)take((cap + 1) * 4);
+    sc.run_p0 = (uint32_t *)take((cap + 1) * 4);
+    sc.run_acq = (int32_t *)take((cap + 1) * 4);
+    sc.flow_first_run = (uint32_t *)take((cap + 1) * 4);
+    sc.plist = (uint32_t *)take(cap * 4);
+    sc.deferred = (uint32_t *)take(cap * 8);
+    sc.run_out = (RunOut *)take(cap * sizeof(RunOut));
+    sc.wave_carry = (RAgg *)take(ntiles * kRunWaves * sizeof(RAgg));
     sc.tile_agg = take(ntiles * sizeof(Agg));
     sc.tile_carry = take(ntiles * sizeof(Agg));
     sc.tile_valid = (uint32_t *)take(ntiles * 4);
@@ -1091,17 +1088,19 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     int bits = 1;
     while (((uint64_t)1 << bits) < (uint64_t)st.nslots + 1) ++bits;
     const uint32_t invalid_key = st.nslots;
+    const bool limited = nlims > 0 && !simple;
+    const int d0 = radix64_digit_bits(bits);
+    const uint32_t ntiles = (n + kTileElems - 1) / kTileElems;
+    static_assert(kTileElems == kRadix64Tile, "classify tiles are sort tiles");
     SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, s));
     const uint32_t nb = (n + kThreads - 1) / kThreads;
-    const uint32_t ncb = (n + kThreads * kClassifyItems - 1) / (kThreads * kClassifyItems);
-    hipLaunchKernelGGL(k_classify, dim3(ncb), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n,
-                       simple, invalid_key, sc.keys[0], sc.pay[0], out, sc.counters);
+    hipLaunchKernelGGL(k_classify, dim3(ntiles), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n,
+                       simple, invalid_key, sc.el[0], out, limited ? 0 : d0, ntiles, sc.radix.hist);
     for (int l = 0; l < nlims && !simple; ++l) {
-        // scratch: the sort's alternate buffers are free until the sort starts
-        uint32_t *flag = sc.keys[1];
-        uint32_t *u = (uint32_t *)sc.pay[1];
-        uint32_t *pos = u, *list = u + n, *rstart = u + 2 * (size_t)n, *rpass = u + 3 * (size_t)n;
-        hipLaunchKernelGGL(k_lim_flag, dim3(nb), dim3(kThreads), 0, s, st, sc.keys[0], n, invalid_key, lims[l].ns, flag);
+        // scratch: the run arrays are free until the runs stage
+        uint32_t *flag = sc.run_start, *pos = sc.run_slot, *list = sc.run_idx0, *rstart = sc.run_cp,
+                 *rpass = sc.run_p0;
+        hipLaunchKernelGGL(k_lim_flag, dim3(nb), dim3(kThreads), 0, s, st, sc.el[0], n, invalid_key, lims[l].ns, flag);
         exclusive_scan_u32(flag, pos, n, sc.lim_partial, s);
         hipLaunchKernelGGL(k_lim_compact, dim3(nb), dim3(kThreads), 0, s, flag, pos, n, list, sc.counters);
         uint32_t *head = flag, *ridx = pos;
@@ -1111,31 +1110,23 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
         hipLaunchKernelGGL(k_lim_walk, dim3(1), dim3(64), 0, s, lims[l].state, lims[l].qps_allowed, list, rstart,
                            sc.counters, ts_off, ts_base, rpass);
         hipLaunchKernelGGL(k_lim_apply, dim3(nb), dim3(kThreads), 0, s, list, head, ridx, rstart, rpass, sc.counters, n,
-                           invalid_key, sc.keys[0], out);
+                           invalid_key, sc.el[0], out);
     }
-    const int npass = radix_sort_pairs(sc.keys[0], sc.pay[0], sc.keys[1], sc.pay[1], n, bits, sc.radix, s);
-    const uint32_t *keys = sc.keys[npass & 1];
-    const Payload *pay = sc.pay[npass & 1];
-    const uint32_t ntiles = (n + kTileElems - 1) / kTileElems;
-    hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, keys, pay, n, invalid_key, (Agg *)sc.tile_agg,
+    const int npass = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, !limited);
+    const uint64_t *el = sc.el[npass & 1];
+    hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
                        sc.tile_valid);
     hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
                        ntiles, (Agg *)sc.tile_carry, sc.counters);
-    hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, keys, pay, invalid_key,
-                       (const Agg *)sc.tile_carry, sc);
+    hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key, (const Agg *)sc.tile_carry,
+                       sc);
     const uint64_t max_flows = n < st.nslots ? n : st.nslots;
-    static const int lanes = [] {
-        const char *e = getenv("SGA_FLOWS_LANES");  // A/B knob: lanes per rule in k_flows (1 or 16)
-        const int v = e ? atoi(e) : 0;
-        return (v == 16 || v == 4 || v == 1) ? v : 0;  // 0: k_flows1
-    }();
-    uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows * (lanes ? lanes : 1) + kThreads - 1) / kThreads, 16384);
+    uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows + kThreads - 1) / kThreads, 16384);
     if (fb == 0) fb = 1;
-    if (lanes == 16) hipLaunchKernelGGL(k_flows<16>, dim3(fb), dim3(kThreads), 0, s, st, sc, pay, ts_base, simple, out);
-    else if (lanes == 4) hipLaunchKernelGGL(k_flows<4>, dim3(fb), dim3(kThreads), 0, s, st, sc, pay, ts_base, simple, out);
-    else if (lanes == 1) hipLaunchKernelGGL(k_flows<1>, dim3(fb), dim3(kThreads), 0, s, st, sc, pay, ts_base, simple, out);
-    else hipLaunchKernelGGL(k_flows1, dim3(fb), dim3(kThreads), 0, s, st, sc, pay, ts_base, simple, out);
-    hipLaunchKernelGGL(k_results, dim3(nb), dim3(kThreads), 0, s, st, sc, keys, pay, simple, out);
+    hipLaunchKernelGGL(k_flows, dim3(fb), dim3(kThreads), 0, s, st, sc, ts_off, ts_base, simple);
+    hipLaunchKernelGGL(k_flows_slow, dim3(std::min<uint32_t>(fb, 1024)), dim3(kThreads), 0, s, st, sc, acquire, prio,
+                       ts_off, ts_base, el, simple, out);
+    hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, invalid_key, out);
 }
 
 void cluster_init_limiter(NsLimiterDev *d, hipStream_t s) {

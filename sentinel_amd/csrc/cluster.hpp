@@ -62,29 +62,48 @@ struct LimiterPass {
     NsLimiterDev *state;  // device
 };
 
+// Per-run decision record written by k_flows, read by k_results (40 B).
+struct RunOut {
+    int64_t s0;     // window PASS sum before the run (closed form)
+    double thr;     // threshold used
+    double isec;    // intervalInSecond
+    uint32_t f;     // passing prefix length
+    uint32_t cpf;   // prioritized requests inside the prefix
+    uint32_t cw;    // occupied (SHOULD_WAIT) requests among the prioritized after the prefix
+    uint16_t wait;  // waitInMs = 1000 / sampleCount
+    uint8_t mode;   // 0 closed form, 1 replayed (results already written)
+    uint8_t pad;
+};
+
+// Results-side scan value (a projection of the run scan): run heads so far, run head seen,
+// prioritized requests since the last run head.
+struct RAgg {
+    uint32_t nh, flag, cnt;
+};
+
 // Per-batch scratch (device), sized for max_batch events.
 struct BatchScratch {
-    uint32_t *keys[2];
-    Payload *pay[2];
-    uint32_t *ev_run;   // run id per sorted event
-    uint32_t *ev_cp;    // prioritized events before this one in its run
-    // run records
-    uint32_t *run_start, *run_end, *run_slot, *run_t0off, *run_cp;
-    int32_t *run_amin, *run_amax;
-    int64_t *run_s0;
-    uint32_t *run_f, *run_cpf, *run_cw, *run_wait;
-    double *run_thr, *run_isec;
-    uint8_t *run_mode;
-    uint32_t *flow_first_run;
-    // tile scan
+    uint64_t *el[2];          // packed sort elements (double buffer)
+    // run records (index = run id, runs in sorted order)
+    uint32_t *run_start, *run_slot, *run_idx0, *run_cp, *run_p0;
+    int32_t *run_acq;         // common acquire count, 0 = mixed / escaped (replay)
+    uint32_t *flow_first_run; // per rule touched in the batch: its first run
+    uint32_t *plist;          // sorted positions of prioritized requests (ascending)
+    uint32_t *deferred;       // (flow, run) pairs handed from k_flows to k_flows_slow
+    RunOut *run_out;
+    RAgg *wave_carry;         // per 512-request wave slice: scan carry for k_results
     void *tile_agg;
     void *tile_carry;
     uint32_t *tile_valid;
-    uint32_t *counters;  // [0]=nvalid [1]=nruns [2]=nflows [3]=flags [4]=limited [5]=limiter runs
+    uint32_t *counters;  // [0]=nvalid [1]=nruns [2]=nflows [4]=limited [5]=limiter runs [6]=deferred flows
     uint32_t *lim_partial;  // scan partials over max_batch elements (namespace limiter pre-pass)
     RadixScratch radix;
     size_t cap = 0;
 };
+
+// Requests per batch are indexed with 26 bits inside the packed sort element; rule slots with 24.
+constexpr size_t kMaxBatch = (size_t)1 << 26;
+constexpr uint32_t kMaxSlots = (1u << 24) - 2;
 
 size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap);
 void batch_scratch_carve(BatchScratch &b, void *base, size_t cap, uint32_t nslots_cap);

@@ -229,7 +229,7 @@ int sga_create(const sga_config *cfg, sga_engine **out) {
     sga_config c;
     if (cfg) c = *cfg;
     else sga_config_default(&c);
-    if (c.max_batch == 0 || c.max_batch > (1u << 30)) return SGA_EINVAL;
+    if (c.max_batch == 0 || c.max_batch > sga::kMaxBatch) return SGA_EINVAL;
     if (c.cold_factor <= 1) c.cold_factor = 3;  // SentinelConfig.coldFactor() fallback, :224-238
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= c.device || c.device < 0) return SGA_ENODEV;
@@ -301,6 +301,14 @@ int sga_load_cluster_flow_rules(sga_engine *e, const char *ns, const sga_cluster
             if (r.strategy != 0) continue;
             if (!rule_map.count(r.flow_id)) order.push_back(r.flow_id);
             rule_map[r.flow_id] = &r;  // ruleMap.put: last one wins
+        }
+        {  // rule slots are 24-bit inside the packed sort element (cluster.hpp kMaxSlots)
+            size_t fresh_ids = 0;
+            for (int64_t fid : order) fresh_ids += g.slot_of.count(fid) ? 0 : 1;
+            if (g.slots.size() - g.free_slots.size() + fresh_ids > sga::kMaxSlots) {
+                g.err = "more than 16M cluster rules on one engine";
+                return SGA_ERANGE;
+            }
         }
         // clearAndResetRulesConditional: flowIds of this namespace not in the new map lose rule AND metric
         for (uint32_t s = 0; s < g.slots.size(); ++s) {

@@ -447,6 +447,143 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const uint32_t *__r
     }
 }
 
+
+// ---- u64 elements with an embedded key (kernel K0 of the cluster path) -----
+// The element carries everything the later stages need (rule slot, window-bucket delta,
+// prioritized flag, acquire count, request index), so a pass moves 8 bytes per request.
+// Per pass: tile histogram (fused into the producer for pass 0), digit-major scan, then a
+// ranking + LDS-staged scatter kernel as above.
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_rs64_hist(const uint64_t *__restrict__ el, uint32_t n, int shift,
+                                                        uint32_t ntiles, uint32_t *__restrict__ hist) {
+    constexpr int RADIX = 1 << D;
+    __shared__ uint32_t h[RADIX];
+    for (int d = threadIdx.x; d < RADIX; d += kThreads) h[d] = 0;
+    __syncthreads();
+    const uint32_t tile = blockIdx.x;
+    const uint32_t base = tile * kTile;
+#pragma unroll 4
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t e = base + r * kThreads + threadIdx.x;
+        if (e < n) atomicAdd(&h[(uint32_t)(el[e] >> shift) & (RADIX - 1)], 1u);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < RADIX; d += kThreads) hist[(size_t)d * ntiles + tile] = h[d];
+}
+
+template <int D>
+struct Sweep64Smem {
+    static constexpr int RADIX = 1 << D;
+    uint32_t wcnt[kWaves][RADIX];  // per-wave running digit counts, then exclusive prefixes over waves
+    uint32_t dstart[RADIX];        // tile-local exclusive digit start
+    uint32_t gbase[RADIX];         // global output position of the tile's first element of digit d
+    uint64_t sel[kTile];           // tile in sorted order
+};
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_rs64_sweep(const uint64_t *__restrict__ in, uint32_t n, int shift,
+                                                         const uint32_t *__restrict__ digit_base,
+                                                         uint64_t *__restrict__ out) {
+    constexpr int RADIX = 1 << D;
+    constexpr int DPT = RADIX >= kThreads ? RADIX / kThreads : 1;
+    __shared__ Sweep64Smem<D> sm;
+    __shared__ uint32_t ws[kWaves];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    for (int d = threadIdx.x; d < RADIX; d += kThreads) {
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) sm.wcnt[w][d] = 0;
+    }
+    __syncthreads();
+    const uint32_t tile = blockIdx.x;
+    const uint32_t tbase = tile * kTile;
+    const uint32_t tn = min((uint32_t)kTile, n - tbase);
+    const uint32_t wbase = tbase + wave * (kRounds * 64);
+    uint64_t key[kRounds];
+    uint32_t pos[kRounds];
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t e = wbase + r * 64 + lane;
+        key[r] = e < n ? in[e] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t e = wbase + r * 64 + lane;
+        const bool valid = e < n;
+        const uint32_t d = (uint32_t)(key[r] >> shift) & (RADIX - 1);
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < D; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        uint32_t before = 0;
+        if (valid) before = sm.wcnt[wave][d];
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t my = (uint32_t)__popcll(peers & lanemask_lt(lane));
+        if (valid && my == 0) sm.wcnt[wave][d] = before + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        pos[r] = before + my;
+    }
+    __syncthreads();
+    uint32_t tot[DPT];
+    uint32_t tsum = 0;
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+        const int d = threadIdx.x * DPT + k;
+        uint32_t sacc = 0;
+        if (d < RADIX) {
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) {
+                const uint32_t c = sm.wcnt[w][d];
+                sm.wcnt[w][d] = sacc;
+                sacc += c;
+            }
+            sm.gbase[d] = digit_base[(size_t)d * gridDim.x + tile];
+        }
+        tot[k] = sacc;
+        tsum += sacc;
+    }
+    {
+        uint32_t x = tsum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) ws[wave] = x;
+        __syncthreads();
+        uint32_t pre = x - tsum;
+        for (int w = 0; w < wave; ++w) pre += ws[w];
+#pragma unroll
+        for (int k = 0; k < DPT; ++k) {
+            const int d = threadIdx.x * DPT + k;
+            if (d < RADIX) sm.dstart[d] = pre;
+            pre += tot[k];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t e = wbase + r * 64 + lane;
+        if (e < n) {
+            const uint32_t d = (uint32_t)(key[r] >> shift) & (RADIX - 1);
+            sm.sel[pos[r] + sm.dstart[d] + sm.wcnt[wave][d]] = key[r];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t i = r * kThreads + threadIdx.x;
+        if (i < tn) {
+            const uint64_t k = sm.sel[i];
+            const uint32_t d = (uint32_t)(k >> shift) & (RADIX - 1);
+            out[sm.gbase[d] + (i - sm.dstart[d])] = k;
+        }
+    }
+}
+
 }  // namespace
 
 size_t scan_partials_needed(size_t n) { return (n + kScanTile - 1) / kScanTile; }
@@ -545,6 +682,54 @@ int radix_sort_pairs(uint32_t *keys, Payload *pay, uint32_t *keys_alt, Payload *
     default: sort_passes<11>(ks, ps, kd, pd, nn, npass, sc, s); break;
     }
     return npass;  // result is in (keys, pay) if npass even, else in the alt buffers
+}
+
+
+int radix64_digit_bits(int bits) {
+    if (bits <= 0) return 1;
+    const int mb = max_digit_bits() > 8 ? 8 : max_digit_bits();
+    const int npass = (bits + mb - 1) / mb;
+    return (bits + npass - 1) / npass;
+}
+
+size_t radix64_tiles(size_t n) { return (n + kTile - 1) / kTile; }
+
+template <int D>
+static int sort64_passes(uint64_t *a, uint64_t *alt, uint32_t n, int key_shift, int npass, RadixScratch &sc,
+                         hipStream_t s, bool hist0_ready) {
+    constexpr int RADIX = 1 << D;
+    const uint32_t nt = (uint32_t)radix64_tiles(n);
+    uint64_t *src = a, *dst = alt;
+    for (int p = 0; p < npass; ++p) {
+        const int shift = key_shift + p * D;
+        if (p > 0 || !hist0_ready)
+            hipLaunchKernelGGL((k_rs64_hist<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, nt, sc.hist);
+        exclusive_scan_u32(sc.hist, sc.hist_scan, (size_t)RADIX * nt, sc.partial, s);
+        hipLaunchKernelGGL((k_rs64_sweep<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, sc.hist_scan, dst);
+        uint64_t *t = src;
+        src = dst;
+        dst = t;
+    }
+    return npass;
+}
+
+int radix_sort_u64(uint64_t *a, uint64_t *alt, size_t n, int key_shift, int bits, RadixScratch &sc, hipStream_t s,
+                   bool hist0_ready) {
+    if (n == 0 || bits <= 0) return 0;
+    const int d = radix64_digit_bits(bits);
+    const int npass = (bits + d - 1) / d;
+    if (npass > kMaxPasses) return -1;
+    const uint32_t nn = (uint32_t)n;
+    switch (d) {
+    case 1: return sort64_passes<1>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    case 2: return sort64_passes<2>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    case 3: return sort64_passes<3>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    case 4: return sort64_passes<4>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    case 5: return sort64_passes<5>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    case 6: return sort64_passes<6>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    case 7: return sort64_passes<7>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    default: return sort64_passes<8>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    }
 }
 
 }  // namespace sga

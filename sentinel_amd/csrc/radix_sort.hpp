@@ -31,4 +31,14 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, uint32_t *p
 int radix_sort_pairs(uint32_t *keys, Payload *pay, uint32_t *keys_alt, Payload *pay_alt, size_t n, int bits,
                      RadixScratch &sc, hipStream_t s);
 
+// Stable LSD sort of u64 elements by their bits [key_shift, key_shift + bits), tiles of
+// radix64_tile() elements, radix64_digit_bits(bits) bits per pass.  When hist0_ready, the
+// first pass's per-tile digit histogram (digit-major: hist[d * ntiles + tile]) is already in
+// sc.hist.  Returns the number of passes: the result is in `a` when even, in `alt` when odd.
+constexpr int kRadix64Tile = 4096;
+int radix64_digit_bits(int bits);
+size_t radix64_tiles(size_t n);
+int radix_sort_u64(uint64_t *a, uint64_t *alt, size_t n, int key_shift, int bits, RadixScratch &sc, hipStream_t s,
+                   bool hist0_ready);
+
 }  // namespace sga
