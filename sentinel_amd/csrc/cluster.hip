@@ -108,10 +108,22 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
             fid[u] = i < n ? flow_id[i] : 0;
             acq[u] = i < n ? acquire[i] : 0;
         }
+        if (st.dense_n) {  // dense flowIds: one 4-byte load, no probe sequence
+            uint32_t d[kClsChunk];
 #pragma unroll
-        for (int u = 0; u < kClsChunk; ++u) {
-            hh[u] = (uint32_t)hash_flow_id(fid[u]) & st.hmask;
-            e[u] = fid[u] > 0 ? st.htab[hh[u]] : HashEntry{0, 0, 0};
+            for (int u = 0; u < kClsChunk; ++u)
+                d[u] = (fid[u] >= 1 && fid[u] <= (int64_t)st.dense_n) ? st.dense[fid[u] - 1] : ~0u;
+#pragma unroll
+            for (int u = 0; u < kClsChunk; ++u) {
+                hh[u] = 0;
+                e[u] = d[u] == ~0u ? HashEntry{-1, 0, 0} : HashEntry{fid[u], d[u] & 0xFFFFFFu, st.wtab[d[u] >> 24]};
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kClsChunk; ++u) {
+                hh[u] = (uint32_t)hash_flow_id(fid[u]) & st.hmask;
+                e[u] = fid[u] > 0 ? st.htab[hh[u]] : HashEntry{0, 0, 0};
+            }
         }
 #pragma unroll
         for (int u = 0; u < kClsChunk; ++u) {
@@ -124,7 +136,7 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
             if (!simple && (f <= 0 || a <= 0)) {
                 status = TRS_BAD_REQUEST;
             } else {
-                if (f > 0 && he.key != f && he.key != 0) {  // continue the linear probe
+                if (!st.dense_n && f > 0 && he.key != f && he.key != 0) {  // continue the linear probe
                     uint32_t q = hh[u];
                     for (uint32_t probe = 1; probe <= st.hmask; ++probe) {
                         q = (q + 1) & st.hmask;

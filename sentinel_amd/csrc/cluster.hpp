@@ -44,6 +44,9 @@ struct ClusterState {
     int64_t *rec;            // per slot: 8 fields x S buckets at rec[8*boff]; field 0 = window start
                              // (kAbsent = null), fields 1..7 = LongAdder sums per ClusterFlowEvent
     const HashEntry *htab;   // open-addressing flowId -> (slot, windowLengthInMs)
+    const uint32_t *dense;   // when flowIds are dense: dense[flowId - 1] = slot | wcode << 24 (~0u: none)
+    const uint32_t *wtab;    // wcode -> windowLengthInMs
+    uint32_t dense_n;        // dense table length (0: hash lookup)
     uint32_t hmask;
     uint32_t nslots;
     double max_occupy_ratio;

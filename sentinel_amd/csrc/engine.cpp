@@ -49,6 +49,9 @@ struct Engine {
     DevBuf<SlotOcc> d_occ;
     DevBuf<int64_t> d_rec;  // 8 int64 per bucket
     DevBuf<HashEntry> d_htab;
+    DevBuf<uint32_t> d_dense;  // dense flowId table (see sync_device)
+    DevBuf<uint32_t> d_wtab;
+    uint32_t dense_n = 0;
     DevBuf<uint32_t> d_fresh;
     uint32_t hmask = 0;
     DevBuf<uint8_t> d_scratch;
@@ -72,6 +75,9 @@ struct Engine {
         st.occ = d_occ.p;
         st.rec = d_rec.p;
         st.htab = d_htab.p;
+        st.dense = d_dense.p;
+        st.wtab = d_wtab.p;
+        st.dense_n = dense_n;
         st.hmask = hmask;
         st.nslots = (uint32_t)slots.size();
         st.max_occupy_ratio = cfg.max_occupy_ratio;
@@ -168,6 +174,42 @@ struct Engine {
         }
         SGA_HIP_CHECK(hipMemcpyAsync(d_htab.p, ht.data(), hcap * sizeof(HashEntry), hipMemcpyHostToDevice, stream));
         hmask = (uint32_t)(hcap - 1);
+        // Dense flowIds (the usual 1..N assignment): a direct table of 4-byte entries replaces the
+        // probe sequence when it costs at most 16 B per active rule and the rules use <= 255
+        // distinct window lengths.  Same lookup result as FLOW_RULES.get(flowId).
+        {
+            int64_t maxid = 0;
+            std::vector<uint32_t> wvals;
+            bool ok = nact > 0;
+            for (size_t i = 0; i < ns && ok; ++i) {
+                if (!slots[i].active) continue;
+                maxid = std::max(maxid, slots[i].flow_id);
+                const uint32_t W = (uint32_t)(slots[i].interval / slots[i].S);
+                if (std::find(wvals.begin(), wvals.end(), W) == wvals.end()) wvals.push_back(W);
+                if (wvals.size() > 255) ok = false;
+            }
+            if (ok && maxid <= (int64_t)(4 * nact + 4096) && maxid < (int64_t)0xFFFFFFFF) {
+                std::vector<uint32_t> dt((size_t)maxid, ~0u);
+                for (size_t i = 0; i < ns; ++i) {
+                    if (!slots[i].active) continue;
+                    const uint32_t W = (uint32_t)(slots[i].interval / slots[i].S);
+                    const uint32_t code = (uint32_t)(std::find(wvals.begin(), wvals.end(), W) - wvals.begin());
+                    dt[(size_t)slots[i].flow_id - 1] = (uint32_t)i | (code << 24);
+                }
+                wvals.resize(256, 1);
+                if (d_dense.n < dt.size()) {
+                    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+                    d_dense.alloc(dt.size());
+                }
+                if (d_wtab.n < 256) d_wtab.alloc(256);
+                SGA_HIP_CHECK(hipMemcpyAsync(d_dense.p, dt.data(), dt.size() * 4, hipMemcpyHostToDevice, stream));
+                SGA_HIP_CHECK(hipMemcpyAsync(d_wtab.p, wvals.data(), 256 * 4, hipMemcpyHostToDevice, stream));
+                SGA_HIP_CHECK(hipStreamSynchronize(stream));
+                dense_n = (uint32_t)maxid;
+            } else {
+                dense_n = 0;
+            }
+        }
         // fresh metrics: empty windows, no occupy (one kernel for all of them)
         if (!fresh.empty()) {
             if (d_fresh.n < fresh.size()) {

@@ -134,20 +134,26 @@ def test_request_validation(eng_mod):
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
 @pytest.mark.parametrize("mixed", [False, True])
-def test_random_traces_bit_exact(eng_mod, seed, mixed):
-    """Random rules (mixed window geometries, fractional counts), acquire mix,
-    10 % prioritized, bursts: every decision and counter equals the oracle."""
+@pytest.mark.parametrize("ids", ["dense", "sparse"])
+def test_random_traces_bit_exact(eng_mod, seed, mixed, ids):
+    """Random rules (mixed window geometries, fractional counts), acquire mix (incl. counts
+    beyond the packed 7-bit field), 10 % prioritized, bursts: every decision and counter equals
+    the oracle.  ids="dense" exercises the direct flowId table, "sparse" the hash probe."""
     c = eng_mod
     rng = np.random.default_rng(seed)
     nr = 300
-    rules = random_rules(rng, nr, mixed_geometry=mixed)
+    idmul = 1 if ids == "dense" else 1_000_003
+    rules = random_rules(rng, nr, ids=[i * idmul for i in range(1, nr + 1)], mixed_geometry=mixed)
     n = 60_000
     fid = rng.integers(1, nr + 40, size=n)          # some ids without rules
     fid[rng.random(n) < 0.002] = 0                  # BAD_REQUEST
     hot = rng.random(n) < 0.5
     fid[hot] = rng.integers(1, 6, size=hot.sum())   # hot rules -> long runs
     acq = np.where(rng.random(n) < 0.9, 1, rng.integers(1, 6, size=n)) if mixed else np.ones(n, np.int64)
+    if mixed:
+        acq[rng.random(n) < 0.002] = 300            # beyond the packed acquire field: replayed
     acq[rng.random(n) < 0.001] = 0                  # BAD_REQUEST
+    fid = np.where(fid > 0, fid * idmul, fid)
     prio = (rng.random(n) < 0.1).astype(np.uint8)
     ts = T0 + np.cumsum(rng.integers(0, 3, size=n))
     oh = oracle_cluster({"default": rules})
@@ -159,7 +165,7 @@ def test_random_traces_bit_exact(eng_mod, seed, mixed):
         g = svc.request_tokens(fid[sl], acq[sl], prio[sl], ts[sl])
         o = oracle_replay(oh, fid[sl], acq[sl], prio[sl], ts[sl])
         assert_same(g, o, fid[sl], ts[sl], f"seed={seed} batch@{lo}")
-    assert_metrics(c, eng, oh, range(1, nr + 1), int(ts[-1]))
+    assert_metrics(c, eng, oh, [i * idmul for i in range(1, nr + 1)], int(ts[-1]))
     H.lib().orc_cluster_free(oh)
     eng.close()
 
