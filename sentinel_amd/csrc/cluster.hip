@@ -336,34 +336,37 @@ __device__ Agg block_excl_scan_1024(const Agg &v, Agg *total) {
     return agg_combine(wpre, lane_excl);
 }
 
-// Single workgroup: tile carries, nvalid / nruns / nflows.
+// Single workgroup: tile carries, nvalid / nruns / nflows.  Blocked: each thread folds a run of
+// consecutive tiles serially, one block scan over the per-thread aggregates.
 __global__ __launch_bounds__(kTileScanThreads) void k_runs_tiles(const Agg *__restrict__ tile_agg,
                                                                  const uint32_t *__restrict__ tile_valid,
                                                                  uint32_t ntiles, Agg *__restrict__ tile_carry,
                                                                  uint32_t *__restrict__ counters) {
-    Agg carry = agg_identity();
-    uint32_t nvalid = 0;
-    for (uint32_t b = 0; b < ntiles; b += kTileScanThreads) {
-        const uint32_t t = b + threadIdx.x;
-        const Agg v = t < ntiles ? tile_agg[t] : agg_identity();
-        const uint32_t c = t < ntiles ? tile_valid[t] : 0;
-        Agg total;
-        const Agg ex = block_excl_scan_1024(v, &total);
-        if (t < ntiles) tile_carry[t] = agg_combine(carry, ex);
-        carry = agg_combine(carry, total);
-        uint32_t s = c;
-        for (int o = 32; o > 0; o >>= 1) s += (uint32_t)__shfl_down((int)s, o, 64);
-        __shared__ uint32_t ws[kTileScanThreads / 64];
-        if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
-        __syncthreads();
-        if (threadIdx.x == 0)
-            for (int w = 0; w < kTileScanThreads / 64; ++w) nvalid += ws[w];
-        __syncthreads();
+    __shared__ uint32_t ws[kTileScanThreads / 64];
+    const uint32_t per = (ntiles + kTileScanThreads - 1) / kTileScanThreads;
+    const uint32_t t0 = threadIdx.x * per, t1 = min(ntiles, t0 + per);
+    Agg acc = agg_identity();
+    uint32_t c = 0;
+    for (uint32_t t = t0; t < t1; ++t) {
+        acc = agg_combine(acc, tile_agg[t]);
+        c += tile_valid[t];
     }
+    Agg total;
+    Agg run = block_excl_scan_1024(acc, &total);
+    for (uint32_t t = t0; t < t1; ++t) {
+        tile_carry[t] = run;
+        run = agg_combine(run, tile_agg[t]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_down((int)c, o, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
     if (threadIdx.x == 0) {
+        uint32_t nvalid = 0;
+        for (int w = 0; w < kTileScanThreads / 64; ++w) nvalid += ws[w];
         counters[0] = nvalid;
-        counters[1] = carry.nh;
-        counters[2] = carry.nf;
+        counters[1] = total.nh;
+        counters[2] = total.nf;
     }
 }
 
@@ -601,8 +604,10 @@ struct RunIn {
     int64_t t0;
 };
 
+template <bool kPrio>
 __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &sc, uint32_t s, const SlotParam &P,
                                          const Rec &R, double thr, const RunIn &ri, uint32_t r) {
+    if (!kPrio && ri.cp_tot > 0) return false;  // prioritized runs go to k_flows_slow
     const int64_t t0 = ri.t0;
     const int32_t a = ri.a;
     const int64_t q = div_pos(t0, P.W);  // bucket number
@@ -774,7 +779,7 @@ __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratc
         const double thr = simple ? P.thr_simple : P.thr;
         for (uint32_t r = r0; r < r1; ++r) {
             const RunIn ri = run_in(sc, ts_off, ts_base, r, nruns, nvalid);
-            if (!run_fast(st, sc, s, P, R, thr, ri, r)) {
+            if (!run_fast<true>(st, sc, s, P, R, thr, ri, r)) {
                 const uint32_t k = atomicAdd(&sc.counters[6], 1u);
                 sc.deferred[2 * k] = fl;
                 sc.deferred[2 * k + 1] = r;
@@ -784,8 +789,8 @@ __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratc
     }
 }
 
-// Deferred rules: from the deferred run on, every run is resolved in closed form when eligible,
-// otherwise replayed request by request (request_exact) from the original arrays.
+// Deferred rules: the deferred run is replayed request by request (request_exact) from the
+// original arrays, later runs in closed form when eligible.
 __global__ __launch_bounds__(kThreads) void k_flows_slow(ClusterState st, BatchScratch sc,
                                                          const int32_t *__restrict__ acquire,
                                                          const uint8_t *__restrict__ prio,
@@ -805,7 +810,7 @@ __global__ __launch_bounds__(kThreads) void k_flows_slow(ClusterState st, BatchS
         const double thr = simple ? P.thr_simple : P.thr;
         for (uint32_t r = rd; r < r1; ++r) {
             const RunIn ri = run_in(sc, ts_off, ts_base, r, nruns, nvalid);
-            if (r > rd && run_fast(st, sc, s, P, R, thr, ri, r)) continue;
+            if (r > rd && run_fast<true>(st, sc, s, P, R, thr, ri, r)) continue;
             for (uint32_t j = ri.j0; j < ri.j0 + ri.n; ++j) {
                 const uint32_t i = el_idx(el[j]);
                 const int64_t t = ts_base + (int64_t)ts_off[i];
