@@ -91,9 +91,9 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
                                                        uint32_t n, int simple, uint32_t invalid_key,
                                                        uint64_t *__restrict__ el, uint64_t *__restrict__ out,
                                                        int hist_d, uint32_t ntiles, uint32_t *__restrict__ hist) {
-    __shared__ uint32_t h[256];
+    __shared__ uint32_t h[1024];
     if (hist_d > 0) {
-        h[threadIdx.x] = 0;
+        for (uint32_t d = threadIdx.x; d < (1u << hist_d); d += kThreads) h[d] = 0;
         __syncthreads();
     }
     const uint32_t tbase = blockIdx.x * kTileElems;
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
     }
     if (hist_d > 0) {
         __syncthreads();
-        if (threadIdx.x < (1u << hist_d)) hist[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+        for (uint32_t d = threadIdx.x; d < (1u << hist_d); d += kThreads) hist[(size_t)d * ntiles + blockIdx.x] = h[d];
     }
 }
 

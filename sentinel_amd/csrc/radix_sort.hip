@@ -687,7 +687,7 @@ int radix_sort_pairs(uint32_t *keys, Payload *pay, uint32_t *keys_alt, Payload *
 
 int radix64_digit_bits(int bits) {
     if (bits <= 0) return 1;
-    const int mb = max_digit_bits() > 8 ? 8 : max_digit_bits();
+    const int mb = max_digit_bits() > 10 ? 10 : max_digit_bits();
     const int npass = (bits + mb - 1) / mb;
     return (bits + npass - 1) / npass;
 }
@@ -728,7 +728,9 @@ int radix_sort_u64(uint64_t *a, uint64_t *alt, size_t n, int key_shift, int bits
     case 5: return sort64_passes<5>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
     case 6: return sort64_passes<6>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
     case 7: return sort64_passes<7>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
-    default: return sort64_passes<8>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    case 8: return sort64_passes<8>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    case 9: return sort64_passes<9>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    default: return sort64_passes<10>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
     }
 }
 
