@@ -17,6 +17,11 @@
  *   sga_set_connected_count   <- ConnectionManager.getConnectedCount (AVG_LOCAL thresholds)
  *                                CS/flow/rule/ClusterFlowRuleManager.java:333-343
  *   sga_cluster_metric_sums   <- ClusterMetric.getSum(ClusterFlowEvent)  CS/flow/statistic/metric/ClusterMetric.java:53-62
+ *   sga_load_cluster_param_rules <- ClusterParamFlowRuleManager.loadRules(String, List<ParamFlowRule>)
+ *                                CS/flow/rule/ClusterParamFlowRuleManager.java:270-276 (apply :318-368)
+ *   sga_request_param_tokens  <- TokenService.requestParamToken(Long, int, Collection<Object>)
+ *                                CORE/cluster/TokenService.java:46 ; DefaultTokenService.requestParamToken
+ *                                CS/flow/DefaultTokenService.java:52-64
  *   sga_rls_should_rate_limit <- SentinelEnvoyRlsServiceImpl.shouldRateLimit -> SimpleClusterFlowChecker
  *                                RLS/SentinelEnvoyRlsServiceImpl.java:51-134, RLS/flow/SimpleClusterFlowChecker.java:33-65
  *   sga_submit_events         <- SphU.entry(String, EntryType, int, Object...) / Entry.exit(int, Object...)
@@ -77,7 +82,8 @@ typedef struct sga_config {
     uint32_t max_rules;        /* initial rule-slot capacity (grows on load) */
     int32_t cold_factor;       /* csp.sentinel.flow.cold.factor, SentinelConfig.java:68 (3) */
     int32_t statistic_max_rt;  /* csp.sentinel.statistic.max.rt, SentinelConfig.java:69 (5000) */
-    int32_t reserved0;
+    uint32_t max_param_keys;   /* cluster parameter flow: (rule, value) keys kept on the device
+                                  (0 = 1M; at most 4M) */
     double exceed_count;       /* ServerFlowConfig.DEFAULT_EXCEED_COUNT (1.0), ServerFlowConfig.java:26 */
     double max_occupy_ratio;   /* ServerFlowConfig.DEFAULT_MAX_OCCUPY_RATIO (1.0), ServerFlowConfig.java:27 */
 } sga_config;
@@ -135,6 +141,48 @@ int sga_request_tokens_device(sga_engine *e, const int64_t *d_flow_id, const int
 /* ClusterMetric.getSum(event) for every ClusterFlowEvent at virtual time `now`
  * (rotation side effects included, as in the reference). out[7]. */
 int sga_cluster_metric_sums(sga_engine *e, int64_t flow_id, int64_t now, int64_t *out7);
+
+/* Cluster parameter flow rule = ParamFlowRule{count, grade, paramIdx, burstCount, controlBehavior,
+ * durationInSec, maxQueueingTimeMs, parsed hot items, clusterMode=true} + ParamFlowClusterConfig
+ * {flowId, thresholdType, sampleCount, windowIntervalMs}
+ * (PF/slots/block/flow/param/ParamFlowRule.java:45-83, ParamFlowClusterConfig.java:32-44).
+ * Fields other than flow_id / count / threshold_type / window geometry / hot items only take part
+ * in ParamFlowRuleUtil.isValidRule (PF/.../ParamFlowRuleUtil.java:46-70). */
+typedef struct sga_cluster_param_rule {
+    int64_t flow_id;
+    double count;
+    int32_t threshold_type;       /* AVG_LOCAL = 0 (ParamFlowClusterConfig default), GLOBAL = 1 */
+    int32_t sample_count;         /* default 10 */
+    int32_t window_interval_ms;   /* default 1000 */
+    int32_t grade;                /* QPS = 1 */
+    int32_t burst_count;          /* default 0 */
+    int32_t control_behavior;     /* default 0 */
+    int32_t max_queueing_time_ms; /* default 0 */
+    int32_t param_idx_set;        /* paramIdx != null */
+    int64_t duration_in_sec;      /* default 1 */
+    int32_t n_hot;                /* parsed hot items (value -> count), later entries win */
+    int32_t reserved;
+    const int64_t *hot_values;
+    const int32_t *hot_counts;
+} sga_cluster_param_rule;
+
+/* ClusterParamFlowRuleManager.loadRules(namespace, rules)  CS/flow/rule/ClusterParamFlowRuleManager.java:270-368:
+ * invalid rules dropped, metrics of flowIds that stay are kept (geometry fixed at creation), metrics
+ * of dropped flowIds removed.  Returns the number of rules applied or an error. */
+int sga_load_cluster_param_rules(sga_engine *e, const char *ns, const sga_cluster_param_rule *rules, size_t n);
+
+/* Batched DefaultTokenService.requestParamToken(flowId, acquireCount, params)
+ * (CS/flow/DefaultTokenService.java:52-64 -> ClusterParamFlowChecker.acquireClusterToken):
+ * request i carries the parameter values values[value_offsets[i] .. value_offsets[i+1]) (Java
+ * Objects as 64-bit values: the caller maps each parameter to a stable int64, e.g. the long value
+ * or a 64-bit hash of a String).  Decided in array order under a mocked clock ts[i].  Host buffers,
+ * synchronous.  -ENOMEM when the device key store (sga_config.max_param_keys) is exhausted. */
+int sga_request_param_tokens(sga_engine *e, const int64_t *flow_id, const int32_t *acquire,
+                             const uint32_t *value_offsets, const int64_t *values, const int64_t *ts, size_t n,
+                             sga_token_result *out);
+
+/* ClusterParamMetric.getSum(value) of a flow at `now` (rotation side effect included). */
+int sga_cluster_param_sum(sga_engine *e, int64_t flow_id, int64_t value, int64_t now, int64_t *out);
 
 /* Number of flow slots and device bytes of window state (for roofline tools). */
 int sga_cluster_stats(sga_engine *e, uint64_t *n_active_rules, uint64_t *state_bytes);

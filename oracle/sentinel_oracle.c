@@ -713,6 +713,7 @@ struct orc_cluster {
     double exceed_count, max_occupy_ratio;
     crule *tab;
     size_t cap, used;
+    struct orc_cparam *param;  /* ClusterParamFlowRuleManager state (oracle_cparam.c) */
     char *ns_name[ORC_MAX_NS];
     int32_t ns_connected[ORC_MAX_NS];
     orc_limiter *ns_limiter[ORC_MAX_NS];
@@ -759,8 +760,10 @@ orc_cluster *orc_cluster_new(double exceed_count, double max_occupy_ratio) {
     return c;
 }
 
+void orc_cparam_free_all(orc_cluster *c);
 void orc_cluster_free(orc_cluster *c) {
     if (!c) return;
+    orc_cparam_free_all(c);
     for (size_t i = 0; i < c->cap; i++) orc_cmetric_free(c->tab[i].metric);
     free(c->tab);
     for (int i = 0; i < c->nns; i++) {
@@ -770,7 +773,9 @@ void orc_cluster_free(orc_cluster *c) {
     free(c);
 }
 
-static int ns_index(orc_cluster *c, const char *ns, int create) {
+int orc_cluster_ns_index(orc_cluster *c, const char *ns, int create);
+static int ns_index(orc_cluster *c, const char *ns, int create) { return orc_cluster_ns_index(c, ns, create); }
+int orc_cluster_ns_index(orc_cluster *c, const char *ns, int create) {
     for (int i = 0; i < c->nns; i++)
         if (strcmp(c->ns_name[i], ns) == 0) return i;
     if (!create || c->nns >= ORC_MAX_NS) return -1;
@@ -816,6 +821,14 @@ int orc_cluster_load_rules(orc_cluster *c, const char *ns, const orc_cluster_rul
         }
     }
     return applied;
+}
+
+struct orc_cparam **orc_cluster_param_slot(orc_cluster *c) { return &c->param; }
+int32_t orc_cluster_connected(orc_cluster *c, int ns) { return ns >= 0 ? c->ns_connected[ns] : 0; }
+/* GlobalRequestLimiter.tryPass(namespace): no limiter for the namespace -> pass */
+int orc_cluster_limiter_try_pass(orc_cluster *c, int ns, int64_t now) {
+    if (ns < 0) return 0;
+    return c->ns_limiter[ns] ? orc_limiter_try_pass(c->ns_limiter[ns], now) : 1;
 }
 
 void orc_cluster_set_namespace_limit(orc_cluster *c, const char *ns, double max_allowed_qps) {

@@ -198,6 +198,43 @@ double orc_limiter_qps(orc_limiter *l, int64_t now);
 int orc_limiter_can_pass(orc_limiter *l, int64_t now);
 int orc_limiter_try_pass(orc_limiter *l, int64_t now);
 
+/* ---- cluster parameter flow (CS/flow/ClusterParamFlowChecker) ---------------- */
+typedef struct orc_cparam_rule {
+    int64_t flow_id;            /* ParamFlowClusterConfig.flowId */
+    double count;
+    int32_t threshold_type;     /* AVG_LOCAL = 0 (default), GLOBAL = 1 */
+    int32_t sample_count;       /* default 10 */
+    int32_t window_interval_ms; /* default 1000 */
+    int32_t grade;              /* ParamFlowRuleUtil.isValidRule fields */
+    int32_t burst_count;
+    int32_t control_behavior;
+    int32_t max_queueing_time_ms;
+    int32_t param_idx_set;      /* paramIdx != null */
+    int64_t duration_in_sec;
+    int32_t n_hot;              /* parsed hot items value -> count */
+    int32_t reserved;
+    const int64_t *hot_values;
+    const int32_t *hot_counts;
+} orc_cparam_rule;
+
+/* ClusterParamFlowRuleManager.loadRules(namespace, rules); returns #applied */
+int orc_cluster_load_param_rules(orc_cluster *c, const char *ns, const orc_cparam_rule *rules, size_t n);
+/* DefaultTokenService.requestParamToken(flowId, acquire, values) at `now` */
+orc_token_result orc_cluster_request_param_token(orc_cluster *c, int64_t flow_id, int32_t acquire,
+                                                 const int64_t *values, size_t nvalues, int64_t now);
+void orc_cluster_param_replay(orc_cluster *c, size_t n, const int64_t *flow_id, const int32_t *acquire,
+                              const uint32_t *value_offsets, const int64_t *values, const int64_t *ts,
+                              orc_token_result *out);
+/* standalone ClusterParamMetric (CS/flow/statistic/metric/ClusterParamMetric.java:41-88) for KATs */
+typedef struct orc_pmetric orc_pmetric;
+orc_pmetric *orc_pmetric_new(int sample_count, int interval_ms);
+void orc_pmetric_free(orc_pmetric *m);
+void orc_pmetric_add(orc_pmetric *m, int64_t now, int64_t value, int32_t count);
+int64_t orc_pmetric_sum(orc_pmetric *m, int64_t now, int64_t value);
+double orc_pmetric_avg(orc_pmetric *m, int64_t now, int64_t value);
+/* ClusterParamMetric.getSum(value) at now; -1 when the flow has no metric */
+int64_t orc_cluster_param_sum(orc_cluster *c, int64_t flow_id, int64_t value, int64_t now);
+
 /* ---- Java numerics exposed for tests ---------------------------------------- */
 int64_t orc_java_round(double d);
 double orc_java_next_up(double d);

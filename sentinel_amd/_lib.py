@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(_HERE, "libsentinel_amd.so")
 
 class SgaConfig(C.Structure):
     _fields_ = [("device", C.c_int32), ("max_batch", C.c_uint32), ("max_rules", C.c_uint32),
-                ("cold_factor", C.c_int32), ("statistic_max_rt", C.c_int32), ("reserved0", C.c_int32),
+                ("cold_factor", C.c_int32), ("statistic_max_rt", C.c_int32), ("max_param_keys", C.c_uint32),
                 ("exceed_count", C.c_double), ("max_occupy_ratio", C.c_double)]
 
 
@@ -20,6 +20,14 @@ class SgaClusterFlowRule(C.Structure):
     _fields_ = [("flow_id", C.c_int64), ("count", C.c_double), ("threshold_type", C.c_int32),
                 ("sample_count", C.c_int32), ("window_interval_ms", C.c_int32), ("grade", C.c_int32),
                 ("strategy", C.c_int32), ("reserved", C.c_int32)]
+
+
+class SgaClusterParamRule(C.Structure):
+    _fields_ = [("flow_id", C.c_int64), ("count", C.c_double), ("threshold_type", C.c_int32),
+                ("sample_count", C.c_int32), ("window_interval_ms", C.c_int32), ("grade", C.c_int32),
+                ("burst_count", C.c_int32), ("control_behavior", C.c_int32), ("max_queueing_time_ms", C.c_int32),
+                ("param_idx_set", C.c_int32), ("duration_in_sec", C.c_int64), ("n_hot", C.c_int32),
+                ("reserved", C.c_int32), ("hot_values", C.POINTER(C.c_int64)), ("hot_counts", C.POINTER(C.c_int32))]
 
 
 class SgaTokenResult(C.Structure):
@@ -71,6 +79,10 @@ SIGNATURES = {
                                             C.c_size_t, C.c_void_p, C.c_void_p]),
     "sga_cluster_metric_sums": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.POINTER(C.c_int64)]),
     "sga_cluster_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "sga_load_cluster_param_rules": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(SgaClusterParamRule), C.c_size_t]),
+    "sga_request_param_tokens": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_size_t, C.c_void_p]),
+    "sga_cluster_param_sum": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.POINTER(C.c_int64)]),
     "sga_rls_should_rate_limit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p, C.c_void_p]),
     "sga_flow_set_resources": (C.c_int, [C.c_void_p, C.c_uint32]),

@@ -5,6 +5,10 @@ Same names and argument meaning as the Java API the engine replaces:
       CORE/cluster/TokenService.java:36  -> DefaultTokenService.request_token / request_tokens
   ClusterFlowRuleManager.loadRules(String namespace, List<FlowRule> rules)
       CS/flow/rule/ClusterFlowRuleManager.java:254-260 -> ClusterFlowRuleManager.load_rules
+  TokenService.requestParamToken(Long ruleId, int acquireCount, Collection<Object> params)
+      CORE/cluster/TokenService.java:46 -> DefaultTokenService.request_param_token(s)
+  ClusterParamFlowRuleManager.loadRules(String namespace, List<ParamFlowRule> rules)
+      CS/flow/rule/ClusterParamFlowRuleManager.java:270-276 -> ClusterParamFlowRuleManager.load_rules
   TokenResult / TokenResultStatus  CORE/cluster/TokenResult.java, CORE/cluster/TokenResultStatus.java:27-60
 Every decision is computed by the HIP engine (libsentinel_amd.so); the mocked
 TimeUtil clock of the reference tests is the explicit `now`/`ts` argument.
@@ -16,8 +20,9 @@ from typing import List, Optional
 import numpy as np
 
 from . import _lib
-from ._lib import SgaClusterFlowRule, SgaConfig, SgaTokenResult, check
-from .rules import ClusterFlowConfig, ClusterRuleConstant, FlowRule  # noqa: F401 (re-exported)
+from ._lib import SgaClusterFlowRule, SgaClusterParamRule, SgaConfig, SgaTokenResult, check
+from .rules import (ClusterFlowConfig, ClusterRuleConstant, FlowRule, ParamFlowClusterConfig,  # noqa: F401
+                    ParamFlowItem, ParamFlowRule)
 
 
 class TokenResultStatus:
@@ -49,7 +54,7 @@ class Engine:
     """Owns one sga_engine (one GPU / one shard)."""
 
     def __init__(self, device: int = 0, max_batch: int = 1 << 20, max_rules: int = 1 << 16,
-                 exceed_count: float = 1.0, max_occupy_ratio: float = 1.0):
+                 exceed_count: float = 1.0, max_occupy_ratio: float = 1.0, max_param_keys: int = 0):
         L = _lib.load()
         cfg = SgaConfig()
         L.sga_config_default(C.byref(cfg))
@@ -58,6 +63,7 @@ class Engine:
         cfg.max_rules = max_rules
         cfg.exceed_count = exceed_count
         cfg.max_occupy_ratio = max_occupy_ratio
+        cfg.max_param_keys = max_param_keys
         h = C.c_void_p()
         rc = L.sga_create(C.byref(cfg), C.byref(h))
         if rc < 0:
@@ -134,6 +140,78 @@ class ClusterFlowRuleManager:
         check(_lib.load().sga_set_connected_count(self.engine.handle, namespace.encode(), n), self.engine.handle)
 
 
+def param_value_key(v) -> int:
+    """64-bit stand-in the engine uses for a Java parameter Object: ints as themselves, str by
+    String.hashCode, bool as Boolean.hashCode (1231 / 1237).  Collisions between distinct Objects
+    with equal keys would merge their counters; callers with such domains pass their own keys."""
+    if isinstance(v, bool):
+        return 1231 if v else 1237
+    if isinstance(v, int):
+        return v
+    if isinstance(v, str):
+        from .javautil import string_hash_code
+        return string_hash_code(v)
+    raise TypeError(f"unsupported parameter type {type(v).__name__}")
+
+
+def _hot_items(rule: ParamFlowRule):
+    """ParamFlowRuleUtil.parseHotItems (PF/.../ParamFlowRuleUtil.java:193-214): items with a null
+    object or a missing / negative count are skipped; later items win."""
+    hot = {}
+    for it in rule.param_flow_item_list:
+        if it.object is None or it.count is None or it.count < 0:
+            continue
+        obj = it.object
+        ct = it.class_type
+        if isinstance(obj, str) and ct in ("int", "java.lang.Integer", "long", "java.lang.Long"):
+            obj = int(obj)
+        hot[param_value_key(obj)] = int(it.count)
+    return hot
+
+
+class ClusterParamFlowRuleManager:
+    """CS/flow/rule/ClusterParamFlowRuleManager.java mirror bound to one engine."""
+
+    def __init__(self, engine: Engine):
+        self.engine = engine
+
+    def load_rules(self, namespace: str, rules: List[ParamFlowRule]) -> int:
+        rules = [r for r in rules if r.cluster_mode]  # applyClusterParamRules skips !isClusterMode
+        arr = (SgaClusterParamRule * max(1, len(rules)))()
+        keep = []
+        for i, r in enumerate(rules):
+            cc = r.cluster_config
+            a = arr[i]
+            a.flow_id = cc.flow_id if (cc is not None and cc.flow_id is not None) else 0
+            a.count = r.count
+            a.threshold_type = cc.threshold_type if cc is not None else 0
+            a.sample_count = cc.sample_count if cc is not None else 0
+            a.window_interval_ms = cc.window_interval_ms if cc is not None else 0
+            a.grade = r.grade
+            a.burst_count = r.burst_count
+            a.control_behavior = r.control_behavior
+            a.max_queueing_time_ms = r.max_queueing_time_ms
+            a.param_idx_set = 1 if r.param_idx is not None else 0
+            a.duration_in_sec = r.duration_in_sec
+            hot = _hot_items(r)
+            a.n_hot = len(hot)
+            if hot:
+                hv = (C.c_int64 * len(hot))(*hot.keys())
+                hc = (C.c_int32 * len(hot))(*hot.values())
+                keep += [hv, hc]
+                a.hot_values = C.cast(hv, C.POINTER(C.c_int64))
+                a.hot_counts = C.cast(hc, C.POINTER(C.c_int32))
+        rc = _lib.load().sga_load_cluster_param_rules(self.engine.handle, namespace.encode(), arr, len(rules))
+        return check(rc, self.engine.handle, "loadRules")
+
+    def param_sum(self, flow_id: int, value, now: int) -> int:
+        """ClusterParamMetric.getSum(value) of the flow's metric at `now`."""
+        out = C.c_int64()
+        check(_lib.load().sga_cluster_param_sum(self.engine.handle, flow_id, param_value_key(value), now,
+                                                C.byref(out)), self.engine.handle, "getSum")
+        return out.value
+
+
 class GlobalRequestLimiter:
     """CS/flow/statistic/limit/GlobalRequestLimiter.java:30-80 mirror (per-namespace QPS guard that
     ClusterFlowChecker.allowProceed consults before a rule's metric)."""
@@ -188,6 +266,31 @@ class DefaultTokenService:
 
     def request_token(self, rule_id: int, acquire_count: int, prioritized: bool, now: int) -> TokenResult:
         r = self.request_tokens([rule_id], [acquire_count], [1 if prioritized else 0], [now])[0]
+        return TokenResult(int(r["status"]), int(r["remaining"]), int(r["wait_in_ms"]))
+
+    def request_param_tokens(self, flow_id, acquire, params, ts) -> np.ndarray:
+        """requestParamToken for a batch: params[i] is the Collection of request i (sequence of ints /
+        strings, or already-mapped int64 keys)."""
+        fid = np.ascontiguousarray(flow_id, dtype=np.int64)
+        acq = np.ascontiguousarray(acquire, dtype=np.int32)
+        t = np.ascontiguousarray(ts, dtype=np.int64)
+        n = len(fid)
+        off = np.zeros(n + 1, dtype=np.uint32)
+        flat = []
+        for i, p in enumerate(params):
+            vals = [param_value_key(v) for v in (p if p is not None else [])]
+            flat += vals
+            off[i + 1] = off[i] + len(vals)
+        vals = np.ascontiguousarray(flat if flat else [0], dtype=np.int64)
+        out = np.zeros(n, dtype=TOKEN_DTYPE)
+        rc = _lib.load().sga_request_param_tokens(self.engine.handle, fid.ctypes.data, acq.ctypes.data,
+                                                  off.ctypes.data, vals.ctypes.data, t.ctypes.data, n,
+                                                  out.ctypes.data)
+        check(rc, self.engine.handle, "requestParamToken")
+        return out
+
+    def request_param_token(self, rule_id: int, acquire_count: int, params, now: int) -> TokenResult:
+        r = self.request_param_tokens([rule_id], [acquire_count], [params], [now])[0]
         return TokenResult(int(r["status"]), int(r["remaining"]), int(r["wait_in_ms"]))
 
     def metric_sums(self, flow_id: int, now: int) -> List[int]:

@@ -925,12 +925,14 @@ __global__ void k_init_slots(ClusterState st, const uint32_t *slots, uint32_t n)
 // One thread walks the runs in order; rejected requests get TOO_MANY_REQUEST and leave the batch.
 constexpr int kLimW = 100, kLimN = 10, kLimInterval = 1000;
 
-__global__ __launch_bounds__(kThreads) void k_lim_flag(ClusterState st, const uint64_t *__restrict__ el, uint32_t n,
-                                                       uint32_t invalid, int32_t ns, uint32_t *__restrict__ flag) {
+template <class RuleParam>
+__global__ __launch_bounds__(kThreads) void k_lim_flag(const RuleParam *param, const uint64_t *__restrict__ el,
+                                                       uint32_t n, uint32_t invalid, int32_t ns,
+                                                       uint32_t *__restrict__ flag) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
     if (i >= n) return;
     const uint32_t k = el_slot(el[i]);
-    flag[i] = (k != invalid && st.param[k].ns == ns) ? 1u : 0u;
+    flag[i] = (k != invalid && param[k].ns == ns) ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(kThreads) void k_lim_compact(const uint32_t *__restrict__ flag,
@@ -1034,9 +1036,385 @@ __global__ void k_lim_init(NsLimiterDev *L) {
     }
 }
 
+// ================================================================ cluster parameter flow (a26)
+// DefaultTokenService.requestParamToken -> ClusterParamFlowChecker.acquireClusterToken over
+// ClusterParamMetric (CS/flow/DefaultTokenService.java:52-64, CS/flow/ClusterParamFlowChecker.java:37-120,
+// CS/flow/statistic/metric/ClusterParamMetric.java:52-88, ClusterParameterLeapArray.java:39-49).
+//
+// A key (rule, value) holds [stamp x S][count x S]; the rule holds the LeapArray starts.  When a
+// rule's calls arrive in non-decreasing time (tmax before the batch <= every call, batch ascending)
+// and every request names one value, the rule-level rotation by other values' calls never
+// changes a key's sum (a stamp the rule start has moved past is already deprecated at the later
+// call, LeapArray.isWindowDeprecated), so keys are independent and each (key, bucket) run is
+// solved in closed form like a ClusterFlowChecker run.  Otherwise the rule's requests are
+// replayed one by one against the rule-level starts (k_pslow).
+constexpr uint32_t kErrKeys = 1, kErrPool = 2;
+
+__device__ __forceinline__ uint32_t prule_lookup(const CParamState &st, int64_t fid) {
+    uint32_t h = (uint32_t)hash_flow_id(fid) & st.hmask;
+    for (uint32_t probe = 0; probe <= st.hmask; ++probe) {
+        const HashEntry e = st.htab[h];
+        if (e.key == fid) return e.slot;
+        if (e.key == 0) break;
+        h = (h + 1) & st.hmask;
+    }
+    return 0xFFFFFFFFu;
+}
+
+// ParamFlowRule.retrieveExclusiveItemCount + calcGlobalThreshold (ClusterParamFlowChecker.java:101-120)
+__device__ __forceinline__ double prule_threshold(const CParamState &st, const PRuleParam &P, int64_t value) {
+    double count = P.count;
+    uint32_t lo = 0, hi = P.n_hot;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (st.hot_v[P.hot_off + m] < value) lo = m + 1;
+        else hi = m;
+    }
+    if (lo < P.n_hot && st.hot_v[P.hot_off + lo] == value) count = (double)st.hot_c[P.hot_off + lo];
+    if (P.threshold_type == 1) return count;  // FLOW_THRESHOLD_GLOBAL
+    return count * (double)(P.ns >= 0 ? st.ns_connected[P.ns] : 0);
+}
+
+// value -> vid (insert-only open addressing on the 64-bit value)
+__device__ __forceinline__ uint32_t vid_of(const CParamState &st, int64_t v, bool insert) {
+    if (v == kAbsent) return st.vmask + 1;
+    uint32_t h = (uint32_t)hash_flow_id(v) & st.vmask;
+    for (uint32_t probe = 0; probe <= st.vmask; ++probe) {
+        int64_t cur = st.vtab[h];
+        if (cur == v) return h;
+        if (cur == kAbsent) {
+            if (!insert) return 0xFFFFFFFFu;
+            const unsigned long long prev = atomicCAS((unsigned long long *)&st.vtab[h], (unsigned long long)kAbsent,
+                                                      (unsigned long long)v);
+            if ((int64_t)prev == kAbsent || (int64_t)prev == v) return h;
+        }
+        h = (h + 1) & st.vmask;
+    }
+    return 0xFFFFFFFFu;
+}
+
+// (slot, vid) -> kidx; the inserting lane allocates and initialises the key's record
+__device__ __forceinline__ uint32_t key_of(const CParamState &st, uint32_t slot, uint32_t vid, int64_t value,
+                                           bool insert) {
+    const uint64_t key = ((uint64_t)(slot + 1) << 32) | vid;
+    uint32_t h = (uint32_t)splitmix64(key) & st.kmask;
+    for (uint32_t probe = 0; probe <= st.kmask; ++probe) {
+        const uint64_t cur = st.ktab[h];
+        if (cur == key) return h;
+        if (cur == 0) {
+            if (!insert) return 0xFFFFFFFFu;
+            const unsigned long long prev = atomicCAS((unsigned long long *)&st.ktab[h], 0ull, key);
+            if (prev == 0) {
+                const int S = st.param[slot].S;
+                const uint32_t off = atomicAdd(&st.ctl[0], (uint32_t)(2 * S));
+                if ((uint64_t)off + 2 * S > st.krec_cap) {
+                    atomicOr(&st.ctl[1], kErrPool);
+                    st.koff[h] = 0;
+                } else {
+                    st.koff[h] = off;
+                    for (int j = 0; j < S; ++j) {
+                        st.krec[off + j] = kAbsent;
+                        st.krec[off + S + j] = 0;
+                    }
+                }
+                st.kslot[h] = slot;
+                st.kval[h] = value;
+                return h;
+            }
+            if (prev == key) return h;
+        }
+        h = (h + 1) & st.kmask;
+    }
+    atomicOr(&st.ctl[1], kErrKeys);
+    return 0xFFFFFFFFu;
+}
+
+// Stage 1a: validation (DefaultTokenService.notValidRequest || params empty -> BAD_REQUEST,
+// :54-56), rule lookup (NO_RULE_EXISTS), sequential-path triggers.
+__global__ __launch_bounds__(kThreads) void k_pcls(CParamState st, const int64_t *__restrict__ flow_id,
+                                                   const int32_t *__restrict__ acquire,
+                                                   const uint32_t *__restrict__ voff, int64_t ts_base,
+                                                   const uint32_t *__restrict__ ts_off, uint32_t n,
+                                                   uint32_t invalid_key, uint64_t *__restrict__ el,
+                                                   uint64_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const int64_t f = flow_id[i];
+    const int32_t a = acquire[i];
+    const uint32_t k = voff[i + 1] - voff[i];
+    if (i > 0 && ts_off[i] < ts_off[i - 1]) st.ctl[3] = 1;  // not ascending: everything sequential
+    if (f <= 0 || a <= 0 || k == 0) {
+        out[i] = pack_result(TRS_BAD_REQUEST, 0, 0);
+        el[i] = (uint64_t)invalid_key << kSlotShift;
+        return;
+    }
+    const uint32_t slot = prule_lookup(st, f);
+    if (slot == 0xFFFFFFFFu || !st.param[slot].active) {
+        out[i] = pack_result(TRS_NO_RULE_EXISTS, 0, 0);
+        el[i] = (uint64_t)invalid_key << kSlotShift;
+        return;
+    }
+    // sequential path for the rule: several values, time before the rule's last call, or a
+    // request the packed element cannot carry (acquire > 127, bucket delta >= 63)
+    const int64_t t = ts_base + (int64_t)ts_off[i];
+    const int32_t W = st.param[slot].W;
+    if (k > 1 || t < st.tmax[slot] || a > (int32_t)kAcqMax || t / W - ts_base / W >= (int64_t)kBdEsc)
+        st.coupled[slot] = 1;
+    el[i] = ((uint64_t)slot << kSlotShift) | i;
+}
+
+// Stage 1b (after the limiter): every value of an admitted request gets its key.
+__global__ __launch_bounds__(kThreads) void k_pkeys(CParamState st, const uint64_t *__restrict__ el,
+                                                    const uint32_t *__restrict__ voff,
+                                                    const int64_t *__restrict__ values, uint32_t n,
+                                                    uint32_t invalid_key, uint32_t *__restrict__ vkey) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t slot = el_slot(el[i]);
+    if (slot == invalid_key) return;
+    for (uint32_t v = voff[i]; v < voff[i + 1]; ++v) {
+        const int64_t x = values[v];
+        const uint32_t vid = vid_of(st, x, true);
+        vkey[v] = vid == 0xFFFFFFFFu ? 0xFFFFFFFFu : key_of(st, slot, vid, x, true);
+        if (vid == 0xFFFFFFFFu) atomicOr(&st.ctl[1], kErrKeys);
+    }
+}
+
+// Stage 1c: path choice.  Key-parallel element (kidx in the slot field) or sequential element.
+__global__ __launch_bounds__(kThreads) void k_ppath(CParamState st, uint64_t *__restrict__ el,
+                                                    uint64_t *__restrict__ els, const uint32_t *__restrict__ voff,
+                                                    const uint32_t *__restrict__ vkey, const int32_t *__restrict__ acquire,
+                                                    int64_t ts_base, const uint32_t *__restrict__ ts_off, uint32_t n,
+                                                    uint32_t invalid_key, uint32_t key_invalid) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t slot = el_slot(el[i]);
+    uint64_t fast = (uint64_t)key_invalid << kSlotShift, slow = (uint64_t)invalid_key << kSlotShift;
+    if (slot != invalid_key) {
+        if (st.ctl[3] || st.coupled[slot]) {
+            slow = ((uint64_t)slot << kSlotShift) | i;
+            atomicAdd(&st.ctl[2], 1u);
+        } else {
+            const uint32_t kidx = vkey[voff[i]];
+            const PRuleParam &P = st.param[slot];
+            const int32_t a = acquire[i];
+            const int64_t bd = (ts_base + (int64_t)ts_off[i]) / P.W - ts_base / P.W;
+            uint32_t a7 = (a >= 1 && a <= (int32_t)kAcqMax) ? (uint32_t)a : 0u;
+            uint32_t bd6 = (uint32_t)bd;
+            if (bd >= (int64_t)kBdEsc) {
+                bd6 = kBdEsc;
+                a7 = 0;
+            }
+            fast = el_pack(kidx, bd6, 0, a7, i);
+        }
+    }
+    el[i] = fast;
+    els[i] = slow;
+}
+
+// ClusterParamMetric over the rule-level starts for one call at t (exact, any time order):
+// currentWindow(t) (LeapArray.java:121-222) then the key's sum over valid buckets.
+__device__ __forceinline__ int pm_window(const CParamState &st, const PRuleParam &P, int64_t t) {
+    const int idx = (int)((t / P.W) % P.S);
+    const int64_t ws = t - t % P.W;
+    int64_t &rs = st.rstart[P.boff + idx];
+    if (rs == kAbsent || ws > rs) {  // newEmptyBucket / resetWindowTo: the bucket's map is empty
+        rs = ws;
+        return idx;
+    }
+    return ws == rs ? idx : -1;  // -1: detached bucket (clock went backwards), adds lost
+}
+
+__device__ __forceinline__ int64_t pm_key_sum(const CParamState &st, const PRuleParam &P, const int64_t *rec,
+                                              int64_t t) {
+    int64_t s = 0;
+    for (int j = 0; j < P.S; ++j) {
+        const int64_t rs = st.rstart[P.boff + j];
+        if (rs == kAbsent || t - rs > (int64_t)P.interval) continue;
+        if (rec[j] == rs) s += rec[P.S + j];
+    }
+    return s;
+}
+
+// Sequential path: one lane per rule replays its requests in arrival order.
+__global__ __launch_bounds__(kThreads) void k_pslow(CParamState st, BatchScratch sc, const uint64_t *__restrict__ els,
+                                                    const int32_t *__restrict__ acquire,
+                                                    const uint32_t *__restrict__ voff,
+                                                    const int64_t *__restrict__ values,
+                                                    const uint32_t *__restrict__ vkey, int64_t ts_base,
+                                                    const uint32_t *__restrict__ ts_off, uint64_t *__restrict__ out) {
+    const uint32_t nflows = sc.counters[2];
+    const uint32_t nruns = sc.counters[1];
+    const uint32_t nvalid = sc.counters[0];
+    for (uint32_t fl = blockIdx.x * kThreads + threadIdx.x; fl < nflows; fl += gridDim.x * kThreads) {
+        const uint32_t r0 = sc.flow_first_run[fl];
+        const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        const uint32_t j0 = sc.run_start[r0], j1 = r1 < nruns ? sc.run_start[r1] : nvalid;
+        const uint32_t slot = sc.run_slot[r0];
+        const PRuleParam P = st.param[slot];
+        int64_t tmax = st.tmax[slot];
+        for (uint32_t j = j0; j < j1; ++j) {
+            const uint32_t i = el_idx(els[j]);
+            const int64_t t = ts_base + (int64_t)ts_off[i];
+            const int32_t a = acquire[i];
+            const uint32_t v0 = voff[i], v1 = voff[i + 1];
+            double remaining = -1;
+            bool passed = true;
+            for (uint32_t v = v0; v < v1; ++v) {  // ClusterParamFlowChecker.java:61-71
+                const uint32_t kidx = vkey[v];
+                pm_window(st, P, t);
+                const int64_t sum = kidx == 0xFFFFFFFFu ? 0 : pm_key_sum(st, P, st.krec + st.koff[kidx], t);
+                const double next = prule_threshold(st, P, values[v]) - (double)sum / P.isec - (double)a;
+                remaining = next;
+                if (next < 0) {
+                    passed = false;
+                    break;
+                }
+            }
+            if (passed) {  // addValue for every value (:73-76)
+                for (uint32_t v = v0; v < v1; ++v) {
+                    const int idx = pm_window(st, P, t);
+                    const uint32_t kidx = vkey[v];
+                    if (idx < 0 || kidx == 0xFFFFFFFFu) continue;
+                    int64_t *rec = st.krec + st.koff[kidx];
+                    const int64_t rs = st.rstart[P.boff + idx];
+                    if (rec[idx] != rs) {
+                        rec[idx] = rs;
+                        rec[P.S + idx] = 0;
+                    }
+                    rec[P.S + idx] += a;
+                }
+            }
+            if (v1 - v0 > 1) remaining = -1;
+            out[i] = passed ? pack_result(TRS_OK, j_d2i(remaining), 0) : pack_result(TRS_BLOCKED, 0, 0);
+            tmax = t > tmax ? t : tmax;
+        }
+        st.tmax[slot] = tmax;
+        st.coupled[slot] = 0;
+    }
+}
+
+// Key-parallel path: one lane per key walks its (key, bucket) runs in time order.  Per run: the
+// key's lazily rotated window sum, the pass prefix over the exact predicate
+//   threshold - sum / intervalInSecond - count >= 0      (ClusterParamFlowChecker.java:62-66)
+// (blocked requests add nothing, so the prefix is the whole answer), the bucket count, and the
+// rule-level start / tmax raised to this run's bucket and time.
+__global__ __launch_bounds__(kThreads) void k_pflows(CParamState st, BatchScratch sc, const uint64_t *__restrict__ el,
+                                                     const int32_t *__restrict__ acquire, int64_t ts_base,
+                                                     const uint32_t *__restrict__ ts_off, uint64_t *__restrict__ out) {
+    const uint32_t nflows = sc.counters[2];
+    const uint32_t nruns = sc.counters[1];
+    const uint32_t nvalid = sc.counters[0];
+    for (uint32_t fl = blockIdx.x * kThreads + threadIdx.x; fl < nflows; fl += gridDim.x * kThreads) {
+        const uint32_t r0 = sc.flow_first_run[fl];
+        const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        const uint32_t kidx = sc.run_slot[r0];
+        const uint32_t slot = st.kslot[kidx];
+        const PRuleParam P = st.param[slot];
+        const double thr = prule_threshold(st, P, st.kval[kidx]);
+        int64_t *rec = st.krec + st.koff[kidx];
+        uint32_t j0 = sc.run_start[r0];
+        for (uint32_t r = r0; r < r1; ++r) {
+            const uint32_t j1 = r + 1 < nruns ? sc.run_start[r + 1] : nvalid;
+            const uint32_t n = j1 - j0;
+            const int32_t a = sc.run_acq[r];  // common acquire count, 0 = mixed
+            RunOut ro;
+            const int64_t t0 = ts_base + (int64_t)ts_off[sc.run_idx0[r]];
+            const int64_t q = t0 / P.W;
+            const int64_t ws = q * P.W;
+            const int cj = (int)(q % P.S);
+            int64_t s0 = 0;
+            for (int j = 0; j < P.S; ++j) {
+                const int64_t stp = rec[j];
+                if (stp == kAbsent || t0 - stp > (int64_t)P.interval) continue;
+                if (j == cj && stp != ws) continue;  // the current bucket was reset
+                s0 += rec[P.S + j];
+            }
+            const int64_t cur = (rec[cj] == ws) ? rec[P.S + cj] : 0;
+            uint32_t f = 0;
+            int64_t added = 0;
+            if (a > 0) {
+                f = pass_prefix(thr, P.isec, s0, a, n);
+                added = (int64_t)f * a;
+            } else {  // mixed acquire counts: request by request on the same lazily rotated sum
+                for (uint32_t j = j0; j < j1; ++j) {
+                    const uint32_t i = el_idx(el[j]);
+                    const int32_t ai = acquire[i];
+                    const double next = thr - (double)(s0 + added) / P.isec - (double)ai;
+                    if (next >= 0) {
+                        added += ai;
+                        out[i] = pack_result(TRS_OK, j_d2i(next), 0);
+                    } else {
+                        out[i] = pack_result(TRS_BLOCKED, 0, 0);
+                    }
+                }
+            }
+            rec[cj] = ws;
+            rec[P.S + cj] = cur + added;
+            atomicMax((long long *)&st.rstart[P.boff + cj], (long long)ws);
+            const int64_t tl = ts_base + (int64_t)ts_off[el_idx(el[j1 - 1])];
+            atomicMax((long long *)&st.tmax[slot], (long long)tl);
+            ro.s0 = s0;
+            ro.thr = thr;
+            ro.isec = P.isec;
+            ro.f = f;
+            ro.cpf = 0;
+            ro.cw = 0;
+            ro.wait = 0;
+            ro.mode = a > 0 ? RUN_FAST : RUN_DONE;
+            sc.run_out[r] = ro;
+            j0 = j1;
+        }
+    }
+}
+
+__global__ void k_psum(CParamState st, uint32_t slot, int64_t value, int64_t now, int64_t *out) {
+    if (threadIdx.x || blockIdx.x) return;
+    const PRuleParam P = st.param[slot];
+    pm_window(st, P, now);
+    const uint32_t vid = vid_of(st, value, false);
+    const uint32_t kidx = vid == 0xFFFFFFFFu ? 0xFFFFFFFFu : key_of(st, slot, vid, value, false);
+    *out = kidx == 0xFFFFFFFFu ? 0 : pm_key_sum(st, P, st.krec + st.koff[kidx], now);
+}
+
+__global__ void k_pinit_rule(CParamState st, uint32_t slot) {
+    const PRuleParam P = st.param[slot];
+    for (int j = threadIdx.x; j < P.S; j += blockDim.x) st.rstart[P.boff + j] = kAbsent;
+    if (threadIdx.x == 0) {
+        st.tmax[slot] = INT64_MIN;
+        st.coupled[slot] = 0;
+    }
+}
+
 }  // namespace
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Namespace limiter pre-pass (K9) over the elements of a batch: rejected requests get
+// TOO_MANY_REQUEST and the invalid key.  RuleParam: SlotParam or PRuleParam (both carry .ns).
+template <class RuleParam>
+static void apply_limiters(const RuleParam *param, BatchScratch &sc, uint64_t *el, uint32_t n, uint32_t invalid_key,
+                           int64_t ts_base, const uint32_t *ts_off, uint64_t *out, const LimiterPass *lims, int nlims,
+                           hipStream_t s) {
+    const uint32_t nb = (n + kThreads - 1) / kThreads;
+    for (int l = 0; l < nlims; ++l) {
+        // scratch: the run arrays are free until the runs stage
+        uint32_t *flag = sc.run_start, *pos = sc.run_slot, *list = sc.run_idx0, *rstart = sc.run_cp,
+                 *rpass = sc.run_p0;
+        hipLaunchKernelGGL(k_lim_flag<RuleParam>, dim3(nb), dim3(kThreads), 0, s, param, el, n, invalid_key,
+                           lims[l].ns, flag);
+        exclusive_scan_u32(flag, pos, n, sc.lim_partial, s);
+        hipLaunchKernelGGL(k_lim_compact, dim3(nb), dim3(kThreads), 0, s, flag, pos, n, list, sc.counters);
+        uint32_t *head = flag, *ridx = pos;
+        hipLaunchKernelGGL(k_lim_heads, dim3(nb), dim3(kThreads), 0, s, list, ts_off, ts_base, n, sc.counters, head);
+        exclusive_scan_u32(head, ridx, n, sc.lim_partial, s);
+        hipLaunchKernelGGL(k_lim_starts, dim3(nb), dim3(kThreads), 0, s, head, ridx, n, sc.counters, rstart);
+        hipLaunchKernelGGL(k_lim_walk, dim3(1), dim3(64), 0, s, lims[l].state, lims[l].qps_allowed, list, rstart,
+                           sc.counters, ts_off, ts_base, rpass);
+        hipLaunchKernelGGL(k_lim_apply, dim3(nb), dim3(kThreads), 0, s, list, head, ridx, rstart, rpass, sc.counters, n,
+                           invalid_key, el, out);
+    }
+}
 
 // the radix digit width depends on the live slot count: size for the widest
 static size_t max_hist_entries(size_t cap, uint32_t nslots_cap) {
@@ -1110,25 +1488,9 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     const uint32_t ntiles = (n + kTileElems - 1) / kTileElems;
     static_assert(kTileElems == kRadix64Tile, "classify tiles are sort tiles");
     SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, s));
-    const uint32_t nb = (n + kThreads - 1) / kThreads;
     hipLaunchKernelGGL(k_classify, dim3(ntiles), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n,
                        simple, invalid_key, sc.el[0], out, limited ? 0 : d0, ntiles, sc.radix.hist);
-    for (int l = 0; l < nlims && !simple; ++l) {
-        // scratch: the run arrays are free until the runs stage
-        uint32_t *flag = sc.run_start, *pos = sc.run_slot, *list = sc.run_idx0, *rstart = sc.run_cp,
-                 *rpass = sc.run_p0;
-        hipLaunchKernelGGL(k_lim_flag, dim3(nb), dim3(kThreads), 0, s, st, sc.el[0], n, invalid_key, lims[l].ns, flag);
-        exclusive_scan_u32(flag, pos, n, sc.lim_partial, s);
-        hipLaunchKernelGGL(k_lim_compact, dim3(nb), dim3(kThreads), 0, s, flag, pos, n, list, sc.counters);
-        uint32_t *head = flag, *ridx = pos;
-        hipLaunchKernelGGL(k_lim_heads, dim3(nb), dim3(kThreads), 0, s, list, ts_off, ts_base, n, sc.counters, head);
-        exclusive_scan_u32(head, ridx, n, sc.lim_partial, s);
-        hipLaunchKernelGGL(k_lim_starts, dim3(nb), dim3(kThreads), 0, s, head, ridx, n, sc.counters, rstart);
-        hipLaunchKernelGGL(k_lim_walk, dim3(1), dim3(64), 0, s, lims[l].state, lims[l].qps_allowed, list, rstart,
-                           sc.counters, ts_off, ts_base, rpass);
-        hipLaunchKernelGGL(k_lim_apply, dim3(nb), dim3(kThreads), 0, s, list, head, ridx, rstart, rpass, sc.counters, n,
-                           invalid_key, sc.el[0], out);
-    }
+    if (!simple) apply_limiters(st.param, sc, sc.el[0], n, invalid_key, ts_base, ts_off, out, lims, nlims, s);
     const int npass = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, !limited);
     const uint64_t *el = sc.el[npass & 1];
     hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
@@ -1144,6 +1506,81 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     hipLaunchKernelGGL(k_flows_slow, dim3(std::min<uint32_t>(fb, 1024)), dim3(kThreads), 0, s, st, sc, acquire, prio,
                        ts_off, ts_base, el, simple, out);
     hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, invalid_key, out);
+}
+
+// ---------------------------------------------------------------- cluster parameter flow (host)
+size_t cparam_scratch_bytes(size_t cap) { return 2 * align_up(cap * 8) + align_up(cap * 4); }
+
+void cparam_scratch_carve(CParamScratch &ps, void *base, size_t cap) {
+    char *p = (char *)base;
+    ps.els[0] = (uint64_t *)p;
+    p += align_up(cap * 8);
+    ps.els[1] = (uint64_t *)p;
+    p += align_up(cap * 8);
+    ps.vkey = (uint32_t *)p;
+}
+
+void cparam_stage1(const CParamState &st, BatchScratch &sc, CParamScratch &ps, const int64_t *flow_id,
+                   const int32_t *acquire, const uint32_t *voff, const int64_t *values, int64_t ts_base,
+                   const uint32_t *ts_off, uint32_t n, void *out_v, hipStream_t s, const LimiterPass *lims,
+                   int nlims) {
+    if (n == 0) return;
+    uint64_t *out = (uint64_t *)out_v;
+    const uint32_t invalid_key = st.nslots;
+    const uint32_t nb = (n + kThreads - 1) / kThreads;
+    SGA_HIP_CHECK(hipMemsetAsync(st.ctl + 1, 0, 3 * sizeof(uint32_t), s));
+    hipLaunchKernelGGL(k_pcls, dim3(nb), dim3(kThreads), 0, s, st, flow_id, acquire, voff, ts_base, ts_off, n,
+                       invalid_key, sc.el[0], out);
+    SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, s));
+    apply_limiters(st.param, sc, sc.el[0], n, invalid_key, ts_base, ts_off, out, lims, nlims, s);
+    hipLaunchKernelGGL(k_pkeys, dim3(nb), dim3(kThreads), 0, s, st, sc.el[0], voff, values, n, invalid_key, ps.vkey);
+    hipLaunchKernelGGL(k_ppath, dim3(nb), dim3(kThreads), 0, s, st, sc.el[0], ps.els[0], voff, ps.vkey, acquire,
+                       ts_base, ts_off, n, invalid_key, st.kmask + 1);
+}
+
+void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, const int32_t *acquire,
+                   const uint32_t *voff, const int64_t *values, int64_t ts_base, const uint32_t *ts_off, uint32_t n,
+                   uint32_t nslow, void *out_v, hipStream_t s) {
+    if (n == 0) return;
+    uint64_t *out = (uint64_t *)out_v;
+    const uint32_t ntiles = (n + kTileElems - 1) / kTileElems;
+    const uint32_t fb = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 16384));
+    auto runs = [&](const uint64_t *el, uint32_t invalid_key) {
+        SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, s));
+        hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
+                           sc.tile_valid);
+        hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
+                           ntiles, (Agg *)sc.tile_carry, sc.counters);
+        hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key,
+                           (const Agg *)sc.tile_carry, sc);
+    };
+    if (nslow < n) {  // key-parallel path (elements keyed by kidx, invalid = kmask + 1)
+        const uint32_t kinv = st.kmask + 1;
+        int bits = 1;
+        while (((uint64_t)1 << bits) < (uint64_t)kinv + 1) ++bits;
+        const int np = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, false);
+        const uint64_t *el = sc.el[np & 1];
+        runs(el, kinv);
+        hipLaunchKernelGGL(k_pflows, dim3(fb), dim3(kThreads), 0, s, st, sc, el, acquire, ts_base, ts_off, out);
+        hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, kinv, out);
+    }
+    if (nslow > 0) {  // sequential path, one lane per rule
+        int bits = 1;
+        while (((uint64_t)1 << bits) < (uint64_t)st.nslots + 1) ++bits;
+        const int np = radix_sort_u64(ps.els[0], ps.els[1], n, kSlotShift, bits, sc.radix, s, false);
+        const uint64_t *els = ps.els[np & 1];
+        runs(els, st.nslots);
+        hipLaunchKernelGGL(k_pslow, dim3(fb), dim3(kThreads), 0, s, st, sc, els, acquire, voff, values, ps.vkey,
+                           ts_base, ts_off, out);
+    }
+}
+
+void cparam_sum(const CParamState &st, uint32_t slot, int64_t value, int64_t now, int64_t *d_out, hipStream_t s) {
+    hipLaunchKernelGGL(k_psum, dim3(1), dim3(64), 0, s, st, slot, value, now, d_out);
+}
+
+void cparam_init_rule(const CParamState &st, uint32_t slot, hipStream_t s) {
+    hipLaunchKernelGGL(k_pinit_rule, dim3(1), dim3(64), 0, s, st, slot);
 }
 
 void cluster_init_limiter(NsLimiterDev *d, hipStream_t s) {

@@ -118,6 +118,66 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
                           void *out /* sga_token_result */, hipStream_t stream, const LimiterPass *lims = nullptr,
                           int nlims = 0);
 
+// ---------------------------------------------------------------------------------------------
+// Cluster parameter flow (ClusterParamFlowChecker + ClusterParamMetric, CS/flow/ClusterParamFlowChecker.java:37-120,
+// CS/flow/statistic/metric/ClusterParamMetric.java:41-88).  Per rule slot the rule-level LeapArray
+// starts; per (rule, value) key a record [stamp x S][count x S] where stamp = start of the
+// rule bucket the count belongs to (a count is live while its stamp equals the rule's start:
+// resetWindowTo clearing a bucket's map = the rule start moving past the stamp).
+struct PRuleParam {
+    double count;        // ParamFlowRule.count
+    double isec;         // intervalInMs / 1000.0
+    uint32_t boff;       // rule-level starts at rstart[boff .. boff + S)
+    int32_t S, W, interval;
+    int32_t active, ns, threshold_type;
+    uint32_t hot_off, n_hot;  // hot items (ascending value) at hot_v/hot_c[hot_off ..)
+};
+
+struct CParamState {
+    const PRuleParam *param;
+    int64_t *rstart;          // rule-level window starts (kAbsent = null)
+    int64_t *tmax;            // per rule slot: latest call time seen
+    uint8_t *coupled;         // per rule slot, per batch: needs the sequential path
+    const HashEntry *htab;    // flowId -> slot (open addressing)
+    uint32_t hmask, nslots;
+    const int64_t *hot_v;
+    const int32_t *hot_c;
+    const int32_t *ns_connected;
+    int64_t *vtab;            // value table: value -> vid = index (kAbsent = empty; kAbsent itself -> vid vcap)
+    uint32_t vmask;
+    uint64_t *ktab;           // key table: ((slot + 1) << 32 | vid) -> kidx = index (0 = empty)
+    uint32_t kmask;
+    uint32_t *koff;           // per kidx: record offset (int64 units) in krec
+    uint32_t *kslot;          // per kidx: rule slot
+    int64_t *kval;            // per kidx: value
+    int64_t *krec;
+    uint64_t krec_cap;        // int64 units
+    uint32_t *ctl;            // [0] krec cursor  [1] error flags (1 key table full, 2 record pool full)
+                              // [2] slow requests  [3] global slow (timestamps not ascending)
+};
+
+struct CParamScratch {
+    uint64_t *els[2];         // sequential-path elements (slot << 40 | request index)
+    uint32_t *vkey;           // per value of the batch: kidx
+};
+
+size_t cparam_scratch_bytes(size_t cap);
+void cparam_scratch_carve(CParamScratch &ps, void *base, size_t cap);
+
+// Batched DefaultTokenService.requestParamToken over DEVICE buffers (host API drives it and reads
+// st.ctl between the stages).  Stage 1: validation, rule lookup, namespace limiter, value/key
+// insertion, path choice.  Stage 2: key-parallel closed form + sequential per-rule replay.
+void cparam_stage1(const CParamState &st, BatchScratch &sc, CParamScratch &ps, const int64_t *flow_id,
+                   const int32_t *acquire, const uint32_t *voff, const int64_t *values, int64_t ts_base,
+                   const uint32_t *ts_off, uint32_t n, void *out, hipStream_t stream, const LimiterPass *lims,
+                   int nlims);
+void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, const int32_t *acquire,
+                   const uint32_t *voff, const int64_t *values, int64_t ts_base, const uint32_t *ts_off, uint32_t n,
+                   uint32_t nslow, void *out, hipStream_t stream);
+// ClusterParamMetric.getSum(value) at now (rotation side effect included); *d_out = -1 if no key
+void cparam_sum(const CParamState &st, uint32_t slot, int64_t value, int64_t now, int64_t *d_out, hipStream_t s);
+void cparam_init_rule(const CParamState &st, uint32_t slot, hipStream_t s);
+
 // Fresh limiter state (every bucket absent).
 void cluster_init_limiter(NsLimiterDev *d, hipStream_t stream);
 

@@ -24,6 +24,20 @@ struct SlotHost {
     uint32_t boff = 0, bcap = 0;
 };
 
+// Cluster parameter rule slot (ClusterParamFlowRuleManager PARAM_RULES + ClusterParamMetricStatistics).
+// Slots are never reused: keys (rule slot, value) of a dropped metric can never match a new one.
+struct PSlotHost {
+    int64_t flow_id = 0;
+    bool allocated = false;  // metric exists
+    bool active = false;     // PARAM_RULES holds the rule
+    int ns = -1;
+    double count = 0;
+    int threshold_type = 0;
+    int S = 0, interval = 0;  // metric geometry, fixed at creation
+    uint32_t boff = 0;
+    std::vector<std::pair<int64_t, int32_t>> hot;  // ascending value
+};
+
 struct NamespaceHost {
     std::string name;
     int32_t connected = 0;
@@ -65,6 +79,160 @@ struct Engine {
     DevBuf<uint64_t> d_out;
     DevBuf<int64_t> d_tmp7;
     DevBuf<NsLimiterDev> d_lim;  // one per namespace index (used when the namespace has a limiter)
+
+    // ---- cluster parameter flow
+    std::vector<PSlotHost> pslots;
+    std::unordered_map<int64_t, uint32_t> pslot_of;  // flowId -> slot (metric exists)
+    uint32_t pbucket_used = 0;
+    DevBuf<PRuleParam> d_pparam;
+    DevBuf<int64_t> d_prstart, d_ptmax;
+    DevBuf<uint8_t> d_pcoupled;
+    DevBuf<HashEntry> d_phtab;
+    uint32_t phmask = 0;
+    DevBuf<int64_t> d_hot_v;
+    DevBuf<int32_t> d_hot_c;
+    DevBuf<int32_t> d_ns_conn;
+    DevBuf<int64_t> d_vtab;
+    DevBuf<uint64_t> d_ktab;
+    DevBuf<uint32_t> d_koff, d_kslot;
+    DevBuf<int64_t> d_kval, d_krec;
+    DevBuf<uint32_t> d_pctl;
+    uint32_t vmask = 0, kmask = 0;
+    DevBuf<uint8_t> d_pscratch;
+    CParamScratch pscratch{};
+    DevBuf<uint32_t> d_in_voff;
+    DevBuf<int64_t> d_in_vals;
+
+    CParamState pstate() {
+        CParamState st{};
+        st.param = d_pparam.p;
+        st.rstart = d_prstart.p;
+        st.tmax = d_ptmax.p;
+        st.coupled = d_pcoupled.p;
+        st.htab = d_phtab.p;
+        st.hmask = phmask;
+        st.nslots = (uint32_t)pslots.size();
+        st.hot_v = d_hot_v.p;
+        st.hot_c = d_hot_c.p;
+        st.ns_connected = d_ns_conn.p;
+        st.vtab = d_vtab.p;
+        st.vmask = vmask;
+        st.ktab = d_ktab.p;
+        st.kmask = kmask;
+        st.koff = d_koff.p;
+        st.kslot = d_kslot.p;
+        st.kval = d_kval.p;
+        st.krec = d_krec.p;
+        st.krec_cap = d_krec.n;
+        st.ctl = d_pctl.p;
+        return st;
+    }
+
+    // key store + batch scratch of the param path, created with the first param rules
+    void ensure_param_store() {
+        if (d_pctl.p) return;
+        const uint32_t keys = cfg.max_param_keys ? cfg.max_param_keys : (1u << 20);
+        uint32_t cap = 1024;
+        while (cap < 2ull * keys) cap <<= 1;
+        d_vtab.alloc((size_t)cap + 1);
+        d_ktab.alloc(cap);
+        d_koff.alloc(cap);
+        d_kslot.alloc(cap);
+        d_kval.alloc(cap);
+        d_krec.alloc((size_t)keys * 20);  // 2 x 10 buckets per key on average
+        d_pctl.alloc(8);
+        SGA_HIP_CHECK(hipMemsetAsync(d_vtab.p, 0x00, d_vtab.bytes(), stream));
+        std::vector<int64_t> empty(d_vtab.n, INT64_MIN);  // kAbsent = empty value slot
+        SGA_HIP_CHECK(hipMemcpyAsync(d_vtab.p, empty.data(), d_vtab.bytes(), hipMemcpyHostToDevice, stream));
+        SGA_HIP_CHECK(hipMemsetAsync(d_ktab.p, 0, d_ktab.bytes(), stream));
+        SGA_HIP_CHECK(hipMemsetAsync(d_pctl.p, 0, d_pctl.bytes(), stream));
+        vmask = cap - 1;
+        kmask = cap - 1;
+        d_pscratch.alloc(cparam_scratch_bytes(cfg.max_batch));
+        cparam_scratch_carve(pscratch, d_pscratch.p, cfg.max_batch);
+        d_in_voff.alloc((size_t)cfg.max_batch + 1);
+        d_in_vals.alloc(cfg.max_batch);
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+
+    // Upload the param rule table, its flowId hash, hot items and connected counts.
+    void sync_param_device(const std::vector<uint32_t> &fresh) {
+        const size_t ns = pslots.size();
+        if (d_pparam.n < std::max<size_t>(ns, 1)) {
+            const size_t c = std::max<size_t>(std::max<size_t>(ns, 1), d_pparam.n * 2);
+            d_pparam.grow(c, stream);
+            d_ptmax.grow(c, stream);
+            d_pcoupled.grow(c, stream);
+        }
+        if (d_prstart.n < std::max<uint32_t>(pbucket_used, 1))
+            d_prstart.grow(std::max<size_t>(pbucket_used, d_prstart.n * 2), stream);
+        std::vector<PRuleParam> hp(ns);
+        std::vector<int64_t> hv;
+        std::vector<int32_t> hc;
+        for (size_t i = 0; i < ns; ++i) {
+            const PSlotHost &h = pslots[i];
+            PRuleParam &q = hp[i];
+            std::memset(&q, 0, sizeof(q));
+            q.count = h.count;
+            q.isec = h.interval / 1000.0;
+            q.boff = h.boff;
+            q.S = h.S ? h.S : 1;
+            q.W = h.S ? h.interval / h.S : 1;
+            q.interval = h.interval;
+            q.active = h.active ? 1 : 0;
+            q.ns = h.ns;
+            q.threshold_type = h.threshold_type;
+            q.hot_off = (uint32_t)hv.size();
+            q.n_hot = (uint32_t)h.hot.size();
+            for (auto &kv : h.hot) {
+                hv.push_back(kv.first);
+                hc.push_back(kv.second);
+            }
+        }
+        if (ns) SGA_HIP_CHECK(hipMemcpyAsync(d_pparam.p, hp.data(), ns * sizeof(PRuleParam), hipMemcpyHostToDevice, stream));
+        if (d_hot_v.n < std::max<size_t>(hv.size(), 1)) {
+            SGA_HIP_CHECK(hipStreamSynchronize(stream));
+            d_hot_v.alloc(std::max<size_t>(hv.size(), 1));
+            d_hot_c.alloc(std::max<size_t>(hv.size(), 1));
+        }
+        if (!hv.empty()) {
+            SGA_HIP_CHECK(hipMemcpyAsync(d_hot_v.p, hv.data(), hv.size() * 8, hipMemcpyHostToDevice, stream));
+            SGA_HIP_CHECK(hipMemcpyAsync(d_hot_c.p, hc.data(), hc.size() * 4, hipMemcpyHostToDevice, stream));
+        }
+        size_t nact = 0;
+        for (auto &h : pslots) nact += h.active ? 1 : 0;
+        size_t hcap = 1024;
+        while (hcap < 2 * nact + 1) hcap <<= 1;
+        std::vector<HashEntry> ht(hcap);
+        std::memset(ht.data(), 0, hcap * sizeof(HashEntry));
+        for (size_t i = 0; i < ns; ++i) {
+            if (!pslots[i].active) continue;
+            uint32_t h = (uint32_t)hash_flow_id(pslots[i].flow_id) & (uint32_t)(hcap - 1);
+            while (ht[h].key != 0) h = (h + 1) & (uint32_t)(hcap - 1);
+            ht[h].key = pslots[i].flow_id;
+            ht[h].slot = (uint32_t)i;
+            ht[h].W = (uint32_t)(pslots[i].interval / pslots[i].S);
+        }
+        if (d_phtab.n != hcap) {
+            SGA_HIP_CHECK(hipStreamSynchronize(stream));
+            d_phtab.alloc(hcap);
+        }
+        SGA_HIP_CHECK(hipMemcpyAsync(d_phtab.p, ht.data(), hcap * sizeof(HashEntry), hipMemcpyHostToDevice, stream));
+        phmask = (uint32_t)(hcap - 1);
+        upload_connected();
+        for (uint32_t sl : fresh) cparam_init_rule(pstate(), sl, stream);
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+
+    void upload_connected() {
+        std::vector<int32_t> c(std::max<size_t>(nss.size(), 1), 0);
+        for (size_t i = 0; i < nss.size(); ++i) c[i] = nss[i].connected;
+        if (d_ns_conn.n < c.size()) {
+            SGA_HIP_CHECK(hipStreamSynchronize(stream));
+            d_ns_conn.alloc(c.size() + 16);
+        }
+        SGA_HIP_CHECK(hipMemcpyAsync(d_ns_conn.p, c.data(), c.size() * 4, hipMemcpyHostToDevice, stream));
+    }
 
     // ---- local flow engine
     FlowEngine flow;
@@ -421,6 +589,8 @@ int sga_set_connected_count(sga_engine *e, const char *ns, int32_t connected) {
         g.nss[i].connected = connected;
         std::vector<uint32_t> none;
         g.sync_device(none);
+        g.upload_connected();
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
         return SGA_OK;
     });
 }
@@ -511,6 +681,170 @@ int sga_cluster_metric_sums(sga_engine *e, int64_t flow_id, int64_t now, int64_t
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
         sga::cluster_metric_sums(g.state(), it->second, now, g.d_tmp7.p, g.stream);
         SGA_HIP_CHECK(hipMemcpyAsync(out7, g.d_tmp7.p, 7 * 8, hipMemcpyDeviceToHost, g.stream));
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        return SGA_OK;
+    });
+}
+
+// ClusterParamFlowRuleManager.applyClusterParamRules, CS/flow/rule/ClusterParamFlowRuleManager.java:318-368
+int sga_load_cluster_param_rules(sga_engine *e, const char *ns, const sga_cluster_param_rule *rules, size_t n) {
+    if (!ns || !*ns || (n && !rules)) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        g.ensure_param_store();
+        const int nsi = g.ns_index(ns, true);
+        std::vector<uint32_t> fresh;
+        if (n == 0) {  // clearAndResetRulesFor (:195-207): rules dropped, metrics kept
+            for (auto &h : g.pslots)
+                if (h.allocated && h.ns == nsi) h.active = false;
+            g.sync_param_device(fresh);
+            return 0;
+        }
+        std::unordered_map<int64_t, const sga_cluster_param_rule *> rule_map;
+        std::vector<int64_t> order;
+        std::unordered_map<int64_t, const sga_cluster_param_rule *> first;  // putMetricIfAbsent geometry
+        for (size_t i = 0; i < n; ++i) {
+            const sga_cluster_param_rule &r = rules[i];
+            // ParamFlowRuleUtil.isValidRule + checkCluster (PF/.../ParamFlowRuleUtil.java:46-70)
+            if (!(r.count >= 0 && r.grade >= 0 && r.param_idx_set && r.burst_count >= 0 && r.control_behavior >= 0 &&
+                  r.duration_in_sec > 0 && r.max_queueing_time_ms >= 0))
+                continue;
+            if (!(r.sample_count > 0 && r.window_interval_ms > 0 && r.window_interval_ms % r.sample_count == 0))
+                continue;
+            if (r.flow_id <= 0) continue;
+            if (r.n_hot < 0 || (r.n_hot > 0 && (!r.hot_values || !r.hot_counts))) return SGA_EINVAL;
+            if (!rule_map.count(r.flow_id)) {
+                order.push_back(r.flow_id);
+                first[r.flow_id] = &r;
+            }
+            rule_map[r.flow_id] = &r;  // ruleMap.put: last one wins
+        }
+        // clearAndResetRulesConditional: ids of this namespace not in the new map lose rule AND metric
+        for (auto &h : g.pslots) {
+            if (!h.allocated || h.ns != nsi || !h.active) continue;
+            if (rule_map.count(h.flow_id)) continue;
+            h.active = false;
+            h.allocated = false;
+            g.pslot_of.erase(h.flow_id);
+        }
+        for (int64_t fid : order) {
+            const sga_cluster_param_rule &r = *rule_map[fid];
+            auto it = g.pslot_of.find(fid);
+            uint32_t sl;
+            if (it == g.pslot_of.end()) {  // putMetricIfAbsent -> new ClusterParamMetric(sampleCount, windowIntervalMs)
+                if (g.pslots.size() >= sga::kMaxSlots) {
+                    g.err = "too many cluster parameter rules";
+                    return SGA_ERANGE;
+                }
+                sl = (uint32_t)g.pslots.size();
+                g.pslots.emplace_back();
+                sga::PSlotHost &h = g.pslots.back();
+                const sga_cluster_param_rule &geo = *first[fid];
+                h.flow_id = fid;
+                h.allocated = true;
+                h.S = geo.sample_count;
+                h.interval = geo.window_interval_ms;
+                h.boff = g.pbucket_used;
+                g.pbucket_used += (uint32_t)h.S;
+                g.pslot_of[fid] = sl;
+                fresh.push_back(sl);
+            } else {
+                sl = it->second;
+            }
+            sga::PSlotHost &h = g.pslots[sl];
+            h.active = true;
+            h.ns = nsi;
+            h.count = r.count;
+            h.threshold_type = r.threshold_type;
+            std::unordered_map<int64_t, int32_t> hot;  // parsed hotItems (HashMap: later wins)
+            for (int32_t k = 0; k < r.n_hot; ++k) hot[r.hot_values[k]] = r.hot_counts[k];
+            h.hot.assign(hot.begin(), hot.end());
+            std::sort(h.hot.begin(), h.hot.end());
+        }
+        g.sync_param_device(fresh);
+        return (int)order.size();
+    });
+}
+
+int sga_request_param_tokens(sga_engine *e, const int64_t *flow_id, const int32_t *acquire,
+                             const uint32_t *value_offsets, const int64_t *values, const int64_t *ts, size_t n,
+                             sga_token_result *out) {
+    if (n && (!flow_id || !acquire || !value_offsets || !ts || !out)) return SGA_EINVAL;
+    if (n && value_offsets[n] > value_offsets[0] && !values) return SGA_EINVAL;
+    for (size_t i = 0; i < n; ++i)
+        if (value_offsets[i + 1] < value_offsets[i] || ts[i] < 0) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        g.ensure_param_store();
+        const size_t cap = g.cfg.max_batch;
+        if (g.d_in_fid.n < cap) {
+            g.d_in_fid.alloc(cap);
+            g.d_in_acq.alloc(cap);
+            g.d_in_prio.alloc(cap);
+            g.d_in_ts.alloc(cap);
+            g.d_out.alloc(cap);
+        }
+        const auto lims = limiter_passes(g);
+        std::vector<uint32_t> off, voff;
+        for (size_t b = 0; b < n;) {
+            // chunk: <= cap requests, <= cap values, timestamp span within u32 offsets
+            size_t m = 0;
+            int64_t lo = ts[b], hi = ts[b];
+            while (b + m < n && m < cap) {
+                const size_t i = b + m;
+                if ((size_t)(value_offsets[i + 1] - value_offsets[b]) > cap) break;
+                const int64_t nlo = std::min(lo, ts[i]), nhi = std::max(hi, ts[i]);
+                if (nhi - nlo > (int64_t)0xFFFFFFFFLL) break;
+                lo = nlo;
+                hi = nhi;
+                ++m;
+            }
+            if (m == 0) {
+                g.err = "a request carries more parameter values than max_batch";
+                return SGA_ERANGE;
+            }
+            off.resize(m);
+            voff.resize(m + 1);
+            for (size_t i = 0; i < m; ++i) off[i] = (uint32_t)(ts[b + i] - lo);
+            for (size_t i = 0; i <= m; ++i) voff[i] = value_offsets[b + i] - value_offsets[b];
+            const uint32_t nv = voff[m];
+            SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_fid.p, flow_id + b, m * 8, hipMemcpyHostToDevice, g.stream));
+            SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_acq.p, acquire + b, m * 4, hipMemcpyHostToDevice, g.stream));
+            SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_ts.p, off.data(), m * 4, hipMemcpyHostToDevice, g.stream));
+            SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_voff.p, voff.data(), (m + 1) * 4, hipMemcpyHostToDevice, g.stream));
+            if (nv)
+                SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_vals.p, values + value_offsets[b], (size_t)nv * 8,
+                                             hipMemcpyHostToDevice, g.stream));
+            const sga::CParamState st = g.pstate();
+            sga::cparam_stage1(st, g.scratch, g.pscratch, g.d_in_fid.p, g.d_in_acq.p, g.d_in_voff.p, g.d_in_vals.p, lo,
+                               g.d_in_ts.p, (uint32_t)m, g.d_out.p, g.stream, lims.data(), (int)lims.size());
+            uint32_t ctl[4];
+            SGA_HIP_CHECK(hipMemcpyAsync(ctl, g.d_pctl.p, sizeof(ctl), hipMemcpyDeviceToHost, g.stream));
+            SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+            if (ctl[1]) {
+                g.err = (ctl[1] & 1) ? "cluster parameter key table full (raise sga_config.max_param_keys)"
+                                     : "cluster parameter record pool full (raise sga_config.max_param_keys)";
+                return SGA_ENOMEM;
+            }
+            sga::cparam_stage2(st, g.scratch, g.pscratch, g.d_in_acq.p, g.d_in_voff.p, g.d_in_vals.p, lo, g.d_in_ts.p,
+                               (uint32_t)m, ctl[2], g.d_out.p, g.stream);
+            SGA_HIP_CHECK(hipGetLastError());
+            SGA_HIP_CHECK(hipMemcpyAsync(out + b, g.d_out.p, m * 8, hipMemcpyDeviceToHost, g.stream));
+            SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+            b += m;
+        }
+        return SGA_OK;
+    });
+}
+
+int sga_cluster_param_sum(sga_engine *e, int64_t flow_id, int64_t value, int64_t now, int64_t *out) {
+    if (!out || now < 0) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        auto it = g.pslot_of.find(flow_id);
+        if (it == g.pslot_of.end() || !g.d_pctl.p) return SGA_EINVAL;
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        sga::cparam_sum(g.pstate(), it->second, value, now, g.d_tmp7.p, g.stream);
+        SGA_HIP_CHECK(hipMemcpyAsync(out, g.d_tmp7.p, 8, hipMemcpyDeviceToHost, g.stream));
         SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
         return SGA_OK;
     });

@@ -1,7 +1,8 @@
 """Rule entities of the decision path, with the reference's field names and defaults.
 
   FlowRule         CORE/slots/block/flow/FlowRule.java:52-95 (+ ClusterFlowConfig, CORE/slots/block/flow/ClusterFlowConfig.java:34-74)
-  ParamFlowRule    PF/slots/block/flow/param/ParamFlowRule.java:45-83, ParamFlowItem.java:28-40
+  ParamFlowRule    PF/slots/block/flow/param/ParamFlowRule.java:45-83, ParamFlowItem.java:28-40,
+                   ParamFlowClusterConfig.java:32-44
   DegradeRule      CORE/slots/block/degrade/DegradeRule.java:59-84
   RuleConstant     CORE/slots/block/RuleConstant.java:24-61
 """
@@ -65,6 +66,16 @@ class ParamFlowItem:
 
 
 @dataclass
+class ParamFlowClusterConfig:
+    """PF/slots/block/flow/param/ParamFlowClusterConfig.java:32-44"""
+    flow_id: Optional[int] = None
+    threshold_type: int = ClusterRuleConstant.FLOW_THRESHOLD_AVG_LOCAL
+    fallback_to_local_when_fail: bool = False
+    sample_count: int = ClusterRuleConstant.DEFAULT_CLUSTER_SAMPLE_COUNT
+    window_interval_ms: int = 1000
+
+
+@dataclass
 class ParamFlowRule:
     resource: str = ""
     grade: int = RuleConstant.FLOW_GRADE_QPS
@@ -76,6 +87,7 @@ class ParamFlowRule:
     duration_in_sec: int = 1
     param_flow_item_list: List[ParamFlowItem] = field(default_factory=list)
     cluster_mode: bool = False
+    cluster_config: Optional[ParamFlowClusterConfig] = None
 
 
 @dataclass

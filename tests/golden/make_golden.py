@@ -214,6 +214,25 @@ _ops = [{"op": "flow_new", "id": "f", "n_resources": 1},
 scenario("README HelloWorld (count=20 => 20 pass/s)", "README.md:75-116", _ops, bases=[1_700_000_000_000])
 
 # -------------------------------------------------- cluster token server
+scenario("ClusterParamMetricTest.testClusterParamMetric",
+         CST + "/flow/statistic/metric/ClusterParamMetricTest.java:27-49 (getTopValues asserts not restated)",
+         [{"op": "set_time", "t": 0},
+          {"op": "pm_new", "id": "m", "sample_count": 5, "interval_ms": 25},
+          {"op": "pm_add", "id": "m", "value": "e1", "n": -1},
+          {"op": "pm_add", "id": "m", "value": "e1", "n": -2},
+          {"op": "pm_add", "id": "m", "value": "e2", "n": 100},
+          {"op": "pm_add", "id": "m", "value": "e2", "n": 23},
+          {"op": "pm_add", "id": "m", "value": "e3", "n": 100},
+          {"op": "pm_add", "id": "m", "value": "e3", "n": 230},
+          {"op": "pm_sum", "id": "m", "value": "e1", "expect": -3},
+          {"op": "pm_avg", "id": "m", "value": "e1", "expect": -120, "tol": 0.01},
+          {"op": "pm_avg", "id": "m", "value": "e3", "expect": 13200, "tol": 0.01},
+          {"op": "pm_avg", "id": "m", "value": "e2", "expect": 4920, "tol": 0.01},
+          {"op": "pm_add", "id": "m", "value": "e2", "n": 100},
+          {"op": "pm_add", "id": "m", "value": "e2", "n": 23},
+          {"op": "pm_sum", "id": "m", "value": "e2", "expect": 246},
+          {"op": "pm_avg", "id": "m", "value": "e2", "expect": 9840, "tol": 0.01}])
+
 scenario("ClusterMetricTest.testTryOccupyNext",
          CST + "/flow/statistic/metric/ClusterMetricTest.java:25-45",
          [{"op": "set_time", "t": 0},

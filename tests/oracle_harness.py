@@ -109,6 +109,15 @@ def lib():
         "orc_cmetric_sum": (I64, [P, I64, C.c_int]),
         "orc_cmetric_avg": (D, [P, I64, C.c_int]),
         "orc_cmetric_try_occupy_next": (I32, [P, I64, C.c_int, I32, D]),
+        "orc_pmetric_new": (P, [C.c_int, C.c_int]),
+        "orc_pmetric_free": (None, [P]),
+        "orc_pmetric_add": (None, [P, I64, I64, I32]),
+        "orc_pmetric_sum": (I64, [P, I64, I64]),
+        "orc_pmetric_avg": (D, [P, I64, I64]),
+        "orc_cluster_load_param_rules": (C.c_int, [P, C.c_char_p, C.POINTER(OrcClusterParamRule), C.c_size_t]),
+        "orc_cluster_request_param_token": (OrcTokenResult, [P, I64, I32, P, C.c_size_t, I64]),
+        "orc_cluster_param_replay": (None, [P, C.c_size_t, P, P, P, P, P, P]),
+        "orc_cluster_param_sum": (I64, [P, I64, I64, I64]),
         "orc_limiter_new": (P, [D]),
         "orc_limiter_free": (None, [P]),
         "orc_limiter_add": (None, [P, I64, C.c_int]),
@@ -216,6 +225,50 @@ def load_scenarios():
 
 class ScenarioFailure(AssertionError):
     pass
+
+
+def java_obj_key(v):
+    """64-bit stand-in for a Java parameter Object: Integer/Long values as themselves, Strings by
+    String.hashCode (the engine's contract: the caller maps each parameter to a stable int64)."""
+    if isinstance(v, str):
+        return int(lib().orc_java_string_hash(v.encode()))
+    return int(v)
+
+
+class OrcClusterParamRule(C.Structure):
+    _fields_ = [("flow_id", C.c_int64), ("count", C.c_double), ("threshold_type", C.c_int32),
+                ("sample_count", C.c_int32), ("window_interval_ms", C.c_int32), ("grade", C.c_int32),
+                ("burst_count", C.c_int32), ("control_behavior", C.c_int32), ("max_queueing_time_ms", C.c_int32),
+                ("param_idx_set", C.c_int32), ("duration_in_sec", C.c_int64), ("n_hot", C.c_int32),
+                ("reserved", C.c_int32), ("hot_values", C.POINTER(C.c_int64)), ("hot_counts", C.POINTER(C.c_int32))]
+
+
+def cluster_param_rules_array(rules, keep):
+    """rules: dicts {flow_id, count, threshold_type?, sample_count?, window_interval_ms?, hot?: {v: c}}.
+    `keep` collects the hot-item buffers so they outlive the call."""
+    arr = (OrcClusterParamRule * max(1, len(rules)))()
+    for i, r in enumerate(rules):
+        a = arr[i]
+        a.flow_id = r["flow_id"]
+        a.count = float(r["count"])
+        a.threshold_type = r.get("threshold_type", 0)
+        a.sample_count = r.get("sample_count", 10)
+        a.window_interval_ms = r.get("window_interval_ms", 1000)
+        a.grade = r.get("grade", 1)
+        a.burst_count = r.get("burst_count", 0)
+        a.control_behavior = r.get("control_behavior", 0)
+        a.max_queueing_time_ms = r.get("max_queueing_time_ms", 0)
+        a.param_idx_set = 1 if r.get("param_idx_set", True) else 0
+        a.duration_in_sec = r.get("duration_in_sec", 1)
+        hot = r.get("hot", {})
+        a.n_hot = len(hot)
+        if hot:
+            hv = (C.c_int64 * len(hot))(*[int(k) for k in hot])
+            hc = (C.c_int32 * len(hot))(*[int(v) for v in hot.values()])
+            keep.extend([hv, hc])
+            a.hot_values = C.cast(hv, C.POINTER(C.c_int64))
+            a.hot_counts = C.cast(hc, C.POINTER(C.c_int32))
+    return arr
 
 
 def run_scenario(sc, base):
@@ -343,6 +396,18 @@ def run_scenario(sc, base):
                 check(got == op["expect"], op, got)
             elif k == "cm_avg":
                 got = L.orc_cmetric_avg(objs[op["id"]], now, CEV[op["event"]])
+                check(abs(got - op["expect"]) <= op.get("tol", 0), op, got)
+            elif k == "pm_new":
+                h = L.orc_pmetric_new(op["sample_count"], op["interval_ms"])
+                objs[op["id"]] = h
+                frees.append((L.orc_pmetric_free, h))
+            elif k == "pm_add":
+                L.orc_pmetric_add(objs[op["id"]], now, java_obj_key(op["value"]), op["n"])
+            elif k == "pm_sum":
+                got = L.orc_pmetric_sum(objs[op["id"]], now, java_obj_key(op["value"]))
+                check(got == op["expect"], op, got)
+            elif k == "pm_avg":
+                got = L.orc_pmetric_avg(objs[op["id"]], now, java_obj_key(op["value"]))
                 check(abs(got - op["expect"]) <= op.get("tol", 0), op, got)
             elif k == "cm_try_occupy_next":
                 got = L.orc_cmetric_try_occupy_next(objs[op["id"]], now, CEV["PASS"], op["acquire"],

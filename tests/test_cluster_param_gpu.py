@@ -1,0 +1,188 @@
+"""GPU parity of the cluster parameter-flow token path:
+DefaultTokenService.requestParamToken -> ClusterParamFlowChecker over ClusterParamMetric,
+HIP engine (through the C-ABI) against the oracle's single-threaded replay on the same ordered
+trace under a mocked clock.  Decisions (status, remaining) and ClusterParamMetric sums must be
+bit-exact.  Parity is pinned while a bucket holds <= 4000 distinct values (no LRU eviction,
+SURVEY.md §8(c)); every trace here stays below that."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from tests import oracle_harness as H
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1_700_000_000_000
+
+
+@pytest.fixture(scope="module")
+def cm():
+    from sentinel_amd import cluster
+    return cluster
+
+
+def to_param_rules(cm, rules):
+    out = []
+    for r in rules:
+        items = [cm.ParamFlowItem(object=v, count=c, class_type="long") for v, c in r.get("hot", {}).items()]
+        out.append(cm.ParamFlowRule(resource=f"p{r['flow_id']}", count=r["count"], cluster_mode=True,
+                                    param_flow_item_list=items,
+                                    cluster_config=cm.ParamFlowClusterConfig(
+                                        flow_id=r["flow_id"], threshold_type=r.get("threshold_type", 0),
+                                        sample_count=r.get("sample_count", 10),
+                                        window_interval_ms=r.get("window_interval_ms", 1000))))
+    return out
+
+
+class Pair:
+    """Engine + oracle fed the same rule loads and requests."""
+
+    def __init__(self, cm, max_batch=1 << 16, max_param_keys=1 << 16):
+        self.cm = cm
+        self.eng = cm.Engine(max_batch=max_batch, max_param_keys=max_param_keys)
+        self.mgr = cm.ClusterParamFlowRuleManager(self.eng)
+        self.svc = cm.DefaultTokenService(self.eng)
+        self.L = H.lib()
+        self.oh = self.L.orc_cluster_new(1.0, 1.0)
+        self.keep = []
+
+    def load(self, ns, rules):
+        self.mgr.load_rules(ns, to_param_rules(self.cm, rules))
+        arr = H.cluster_param_rules_array(rules, self.keep)
+        self.L.orc_cluster_load_param_rules(self.oh, ns.encode(), arr, len(rules))
+
+    def connected(self, ns, n):
+        self.cm.ClusterFlowRuleManager(self.eng).set_connected_count(ns, n)
+        self.L.orc_cluster_set_connected_count(self.oh, ns.encode(), n)
+
+    def limit(self, ns, qps):
+        self.cm.GlobalRequestLimiter(self.eng).init_if_absent(ns, qps)
+        self.L.orc_cluster_set_namespace_limit(self.oh, ns.encode(), qps)
+
+    def run(self, fid, acq, params, ts, ctx=""):
+        got = self.svc.request_param_tokens(fid, acq, params, ts)
+        n = len(fid)
+        off = np.zeros(n + 1, dtype=np.uint32)
+        for i, p in enumerate(params):
+            off[i + 1] = off[i] + len(p)
+        flat = np.ascontiguousarray([self.cm.param_value_key(v) for p in params for v in p] or [0], np.int64)
+        out = (H.OrcTokenResult * n)()
+        f = np.ascontiguousarray(fid, np.int64)
+        a = np.ascontiguousarray(acq, np.int32)
+        t = np.ascontiguousarray(ts, np.int64)
+        self.L.orc_cluster_param_replay(self.oh, n, f.ctypes.data, a.ctypes.data, off.ctypes.data, flat.ctypes.data,
+                                        t.ctypes.data, out)
+        ref = np.frombuffer(out, dtype=np.int32).reshape(-1, 3)
+        bad = np.nonzero((got["status"] != ref[:, 0]) | (got["remaining"] != ref[:, 1]))[0]
+        if bad.size:
+            i = int(bad[0])
+            raise AssertionError(f"{ctx}: {bad.size} mismatches; first at {i}: flow={fid[i]} acq={acq[i]} "
+                                 f"params={params[i]} ts={ts[i]} gpu=({got['status'][i]},{got['remaining'][i]}) "
+                                 f"oracle=({ref[i, 0]},{ref[i, 1]})")
+        return got
+
+    def check_sums(self, flows_values, now):
+        for f, v in flows_values:
+            g = self.mgr.param_sum(f, v, now)
+            o = self.L.orc_cluster_param_sum(self.oh, f, self.cm.param_value_key(v), now)
+            assert g == o, (f, v, g, o)
+
+    def close(self):
+        self.L.orc_cluster_free(self.oh)
+        self.eng.close()
+
+
+def test_basic_semantics(cm):
+    """Validation, NO_RULE, count 5 per second per value, hot item override, remaining."""
+    p = Pair(cm)
+    p.load("default", [{"flow_id": 11, "count": 5, "threshold_type": 1, "hot": {7: 2}}])
+    fid = [11, 11, 0, 11, 99, 11] + [11] * 12
+    acq = [1, 1, 1, 0, 1, 1] + [1] * 12
+    params = [[3], [3], [3], [3], [3], []] + [[3]] * 6 + [[7]] * 6
+    ts = [T0 + i for i in range(len(fid))]
+    got = p.run(fid, acq, params, ts, "basic")
+    assert list(got["status"][:6]) == [0, 0, -4, -4, 3, -4]
+    assert list(got["status"][6:12]) == [0, 0, 0, 1, 1, 1]      # 5 per second for value 3
+    assert list(got["status"][12:18]) == [0, 0, 1, 1, 1, 1]     # hot item 7 -> 2
+    p.check_sums([(11, 3), (11, 7), (11, 8)], ts[-1])
+    p.close()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_single_value_traces(cm, seed):
+    """Key-parallel path: single-valued requests, ascending time, Zipf-like values, several rules
+    with hot items and AVG_LOCAL thresholds; several batches continue the same state."""
+    rng = np.random.default_rng(seed)
+    p = Pair(cm)
+    p.connected("default", 3)
+    rules = []
+    for f in range(1, 41):
+        r = {"flow_id": f, "count": float(rng.integers(1, 30)), "threshold_type": int(f % 2)}
+        if f % 5 == 0:
+            r["sample_count"], r["window_interval_ms"] = 5, 500
+        if f % 3 == 0:
+            r["hot"] = {int(v): int(rng.integers(0, 10)) for v in rng.integers(0, 50, size=3)}
+        rules.append(r)
+    p.load("default", rules)
+    n = 40_000
+    fid = rng.integers(1, 45, size=n)
+    vals = np.minimum(rng.zipf(1.3, size=n), 200) - 1
+    acq = np.where(rng.random(n) < 0.9, 1, rng.integers(1, 4, size=n))
+    ts = T0 + np.cumsum(rng.integers(0, 2, size=n))
+    params = [[int(v)] for v in vals]
+    for lo in range(0, n, 10_000):
+        sl = slice(lo, lo + 10_000)
+        p.run(fid[sl], acq[sl], params[sl], ts[sl], f"seed={seed} batch@{lo}")
+    p.check_sums([(int(f), int(v)) for f in range(1, 41) for v in (0, 1, 2, 5, 33)], int(ts[-1]))
+    p.close()
+
+
+def test_multi_value_and_regression(cm):
+    """Sequential path: collections of values (all must pass, every value is added, remaining -1),
+    time going backwards inside a batch, acquire counts beyond the packed field."""
+    rng = np.random.default_rng(7)
+    p = Pair(cm)
+    p.load("ns1", [{"flow_id": f, "count": float(rng.integers(2, 12)), "threshold_type": 1,
+                    "sample_count": 2, "window_interval_ms": 1000} for f in range(1, 9)])
+    n = 6000
+    fid = rng.integers(1, 10, size=n)
+    ts = T0 + np.cumsum(rng.integers(0, 3, size=n))
+    back = rng.random(n) < 0.01
+    ts[back] -= rng.integers(1, 900, size=back.sum())
+    acq = np.where(rng.random(n) < 0.95, 1, rng.integers(100, 300, size=n))
+    params = []
+    for i in range(n):
+        k = 1 if rng.random() < 0.6 else int(rng.integers(2, 4))
+        params.append([int(v) for v in rng.integers(0, 12, size=k)])
+    for lo in range(0, n, 2000):
+        sl = slice(lo, lo + 2000)
+        p.run(fid[sl], acq[sl], params[sl], ts[sl], f"batch@{lo}")
+    p.check_sums([(f, v) for f in range(1, 9) for v in range(12)], int(ts.max()))
+    p.close()
+
+
+def test_mixed_paths_limiter_and_reload(cm):
+    """Some rules take the sequential path (multi-value requests) while others stay key-parallel in
+    the same batch; a namespace QPS limiter shared with the flow path; rule reload keeps metrics of
+    flowIds that stay and drops the others."""
+    rng = np.random.default_rng(11)
+    p = Pair(cm)
+    p.limit("lim", 400.0)
+    p.load("lim", [{"flow_id": f, "count": 20.0, "threshold_type": 1} for f in range(1, 6)])
+    p.load("free", [{"flow_id": f, "count": 9.0, "threshold_type": 1, "sample_count": 4, "window_interval_ms": 200}
+                    for f in range(10, 16)])
+    n = 8000
+    fid = np.where(rng.random(n) < 0.5, rng.integers(1, 6, size=n), rng.integers(10, 16, size=n))
+    ts = T0 + np.cumsum(rng.integers(0, 2, size=n))
+    params = [[int(rng.integers(0, 30))] if (f >= 10 or rng.random() < 0.7) else
+              [int(x) for x in rng.integers(0, 30, size=2)] for f in fid]
+    acq = np.ones(n, np.int64)
+    p.run(fid[:4000], acq[:4000], params[:4000], ts[:4000], "before reload")
+    # reload: flowIds 10..12 stay (metrics kept), 13..15 dropped, 16 new
+    p.load("free", [{"flow_id": f, "count": 4.0, "threshold_type": 1, "sample_count": 4, "window_interval_ms": 200}
+                    for f in (10, 11, 12, 16)])
+    fid2 = np.where(fid[4000:] == 13, 16, fid[4000:])
+    p.run(fid2, acq[4000:], params[4000:], ts[4000:], "after reload")
+    p.check_sums([(f, v) for f in (1, 2, 10, 11, 16) for v in range(0, 30, 3)], int(ts[-1]))
+    p.close()
