@@ -34,6 +34,10 @@
  *   sga_load_param_rules      <- ParamFlowRuleManager.loadRules(List<ParamFlowRule>)  PF/slots/block/flow/param/ParamFlowRuleManager.java:52
  *   sga_load_degrade_rules    <- DegradeRuleManager.loadRules(List<DegradeRule>)  CORE/slots/block/degrade/DegradeRuleManager.java:108
  *   sga_query_node            <- Node views (ClusterNode) CORE/node/Node.java:40-203, StatisticNode.java:185-250
+ *   sga_metrics_snapshot      <- StatisticNode.metrics() as polled by MetricTimerListener.run
+ *                                CORE/node/StatisticNode.java:120-157, CORE/node/metric/MetricTimerListener.java:44-65
+ *   sga_cluster_metric_nodes* <- ClusterMetricNodeGenerator.flowToMetricNode
+ *                                CS/flow/statistic/ClusterMetricNodeGenerator.java:75-91
  */
 #ifndef SENTINEL_AMD_H
 #define SENTINEL_AMD_H
@@ -279,6 +283,43 @@ int sga_submit_events(sga_engine *e, const uint8_t *kind, const uint32_t *resour
 int sga_query_node(sga_engine *e, uint32_t resource, int64_t now, sga_node_view *out);
 /* circuit breaker k of a resource: 0 CLOSED, 1 OPEN, 2 HALF_OPEN (negative = no such breaker) */
 int sga_circuit_breaker_state(sga_engine *e, uint32_t resource, uint32_t k);
+
+/* ---------------------------------------------------------------------------
+ * Once-per-second metrics
+ * ------------------------------------------------------------------------- */
+
+/* MetricNode, CORE/node/metric/MetricNode.java:28-51 (thin-format fields); resource = dense id */
+typedef struct sga_metric_node {
+    int64_t timestamp;        /* second-window start (minute LeapArray bucket) */
+    int64_t pass_qps, block_qps, success_qps, exception_qps;
+    int64_t rt;               /* rt sum / success (ArrayMetric.fromBucket, :203-218) */
+    int64_t occupied_pass_qps;
+    uint32_t resource;
+    int32_t concurrency;      /* not filled by StatisticNode.metrics() (0) */
+} sga_metric_node;
+
+/* StatisticNode.metrics() of every resource's ClusterNode at `now` (CORE/node/StatisticNode.java:120-157):
+ * minute buckets with lastFetchTime < start < now - now % 1000 and a non-zero field, each node's
+ * lastFetchTime advanced as in the reference.  Up to `cap` nodes; *n = number written (the order
+ * between resources is unspecified, like the reference's ClusterNode map).  -ERANGE if more than
+ * `cap` nodes were due (the first `cap` are written, lastFetchTime still advanced). */
+int sga_metrics_snapshot(sga_engine *e, int64_t now, sga_metric_node *out, size_t cap, size_t *n);
+
+/* ClusterMetricNodeGenerator.flowToMetricNode for every active cluster flow rule
+ * (CS/flow/statistic/ClusterMetricNodeGenerator.java:75-91): passQps / blockQps =
+ * ClusterMetric.getAvg(PASS / BLOCK) at `now` (rotation side effect included). */
+typedef struct sga_cluster_metric_node {
+    int64_t flow_id;
+    double pass_qps;
+    double block_qps;
+    int64_t timestamp;
+} sga_cluster_metric_node;
+
+int sga_cluster_metric_nodes(sga_engine *e, int64_t now, sga_cluster_metric_node *out, size_t cap, size_t *n);
+/* Same into DEVICE memory on `hip_stream` (NULL = engine stream), count into *d_n (uint32, device):
+ * the input of the once-per-second RCCL all-gather across the node's GPUs. */
+int sga_cluster_metric_nodes_device(sga_engine *e, int64_t now, sga_cluster_metric_node *d_out, size_t cap,
+                                    uint32_t *d_n, void *hip_stream);
 
 /* Optional helper for tools: HIP stream of the engine (hipStream_t as void*). */
 void *sga_engine_stream(sga_engine *e);

@@ -33,6 +33,7 @@ struct orc_node {
     orc_leap *second; /* ArrayMetric(SAMPLE_COUNT, INTERVAL): occupiable, StatisticNode.java:99-100 */
     orc_leap *minute; /* ArrayMetric(60, 60*1000, false), StatisticNode.java:106 */
     int64_t threads;  /* curThreadNum LongAdder */
+    int64_t last_fetch; /* StatisticNode.lastFetchTime, StatisticNode.java:118 */
     int mock;
     double mock_pass_qps, mock_prev_pass_qps;
     int32_t mock_threads;

@@ -230,7 +230,53 @@ orc_node *orc_node_new(void) {
     orc_node *n = (orc_node *)calloc(1, sizeof(orc_node));
     n->second = orc_leap_new(ORC_LEAP_OCCUPIABLE, ORC_SAMPLE_COUNT, ORC_INTERVAL);
     n->minute = orc_leap_new(ORC_LEAP_BUCKET, 60, 60 * 1000);
+    n->last_fetch = -1;
     return n;
+}
+
+/* StatisticNode.metrics() (StatisticNode.java:120-157) over ArrayMetric.details() (ArrayMetric.java:166-218)
+ * and LeapArray.list(now) (LeapArray.java:304-326). */
+size_t orc_node_metrics(orc_node *n, int64_t now, uint32_t resource, orc_metric_node *out, size_t cap) {
+    const int64_t current = now - now % 1000;
+    orc_leap *m = n->minute;
+    orc_leap_current_window(m, now); /* data.currentWindow() */
+    int64_t newlast = n->last_fetch;
+    size_t k = 0;
+    for (int j = 0; j < m->sample_count; j++) {
+        if (!m->present[j]) continue;
+        const obucket *b = &m->b[j];
+        if (now - b->start > m->interval_ms) continue; /* isWindowDeprecated */
+        orc_metric_node x;
+        memset(&x, 0, sizeof(x));
+        x.timestamp = b->start;
+        x.pass_qps = b->c[ORC_EV_PASS];
+        x.block_qps = b->c[ORC_EV_BLOCK];
+        x.success_qps = b->c[ORC_EV_SUCCESS];
+        x.exception_qps = b->c[ORC_EV_EXCEPTION];
+        x.rt = x.success_qps != 0 ? b->c[ORC_EV_RT] / x.success_qps : b->c[ORC_EV_RT];
+        x.occupied_pass_qps = b->c[ORC_EV_OCCUPIED_PASS];
+        x.resource = resource;
+        const int in_time = x.timestamp > n->last_fetch && x.timestamp < current;
+        const int valid = x.pass_qps > 0 || x.block_qps > 0 || x.success_qps > 0 || x.exception_qps > 0 ||
+                          x.rt > 0 || x.occupied_pass_qps > 0;
+        if (in_time && valid) {
+            if (k < cap) out[k] = x;
+            k++;
+            if (x.timestamp > newlast) newlast = x.timestamp;
+        }
+    }
+    n->last_fetch = newlast;
+    return k;
+}
+
+/* MetricTimerListener.run over every resource's ClusterNode (MetricTimerListener.java:44-65) */
+size_t orc_flow_metrics(orc_flow *f, int64_t now, orc_metric_node *out, size_t cap) {
+    size_t k = 0;
+    for (uint32_t r = 0; r < f->n; r++) {
+        if (!f->res[r].node) continue;
+        k += orc_node_metrics(f->res[r].node, now, r, out ? out + (k < cap ? k : cap) : NULL, k < cap ? cap - k : 0);
+    }
+    return k;
 }
 
 orc_node *orc_node_new_mock(double pass_qps, double previous_pass_qps, int32_t threads) {

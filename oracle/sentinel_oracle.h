@@ -146,6 +146,17 @@ void orc_flow_replay(orc_flow *f, size_t n, const uint8_t *kind, const uint32_t 
                      const int32_t *acquire, const uint8_t *flags, const int64_t *rt, int8_t *decision,
                      int32_t *wait_ms);
 
+/* MetricNode (CORE/node/metric/MetricNode.java:28-51), same layout as sga_metric_node */
+typedef struct orc_metric_node {
+    int64_t timestamp;
+    int64_t pass_qps, block_qps, success_qps, exception_qps, rt, occupied_pass_qps;
+    uint32_t resource;
+    int32_t concurrency;
+} orc_metric_node;
+/* StatisticNode.metrics(): returns the number of due nodes (writes up to cap) */
+size_t orc_node_metrics(orc_node *n, int64_t now, uint32_t resource, orc_metric_node *out, size_t cap);
+size_t orc_flow_metrics(orc_flow *f, int64_t now, orc_metric_node *out, size_t cap);
+
 /* ---- cluster token server (CS/flow) ---------------------------------------- */
 typedef struct orc_cluster_rule {
     int64_t flow_id;

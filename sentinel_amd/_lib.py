@@ -54,6 +54,17 @@ class SgaDegradeRule(C.Structure):
                 ("stat_interval_ms", C.c_int32), ("reserved", C.c_int32)]
 
 
+class SgaMetricNode(C.Structure):
+    _fields_ = [("timestamp", C.c_int64), ("pass_qps", C.c_int64), ("block_qps", C.c_int64),
+                ("success_qps", C.c_int64), ("exception_qps", C.c_int64), ("rt", C.c_int64),
+                ("occupied_pass_qps", C.c_int64), ("resource", C.c_uint32), ("concurrency", C.c_int32)]
+
+
+class SgaClusterMetricNode(C.Structure):
+    _fields_ = [("flow_id", C.c_int64), ("pass_qps", C.c_double), ("block_qps", C.c_double),
+                ("timestamp", C.c_int64)]
+
+
 class SgaNodeView(C.Structure):
     _fields_ = [("pass_qps", C.c_double), ("block_qps", C.c_double), ("success_qps", C.c_double),
                 ("exception_qps", C.c_double), ("occupied_pass_qps", C.c_double), ("avg_rt", C.c_double),
@@ -93,6 +104,10 @@ SIGNATURES = {
                                     C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
     "sga_query_node": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int64, C.POINTER(SgaNodeView)]),
     "sga_circuit_breaker_state": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    "sga_metrics_snapshot": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "sga_cluster_metric_nodes": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "sga_cluster_metric_nodes_device": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.c_void_p,
+                                                  C.c_void_p]),
 }
 
 _lib = None

@@ -899,6 +899,23 @@ __global__ void k_metric_sums(ClusterState st, uint32_t s, int64_t now, int64_t 
     for (int k = 0; k < CEV_N; ++k) out7[k] = values_sum(st, P, now, k);
 }
 
+// ClusterMetricNodeGenerator.flowToMetricNode (CS/flow/statistic/ClusterMetricNodeGenerator.java:75-91):
+// getAvg(BLOCK) then getAvg(PASS), each rotating the current window first.
+__global__ __launch_bounds__(kThreads) void k_cluster_nodes(ClusterState st, const int64_t *__restrict__ slot_fid,
+                                                            int64_t now, sga_cluster_metric_node *out, uint32_t cap,
+                                                            uint32_t *count) {
+    const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
+    if (s >= st.nslots || !st.param[s].active) return;
+    const SlotParam P = st.param[s];
+    sga_cluster_metric_node m;
+    m.flow_id = slot_fid[s];
+    m.block_qps = get_avg(st, P, s, now, CEV_BLOCK);
+    m.pass_qps = get_avg(st, P, s, now, CEV_PASS);
+    m.timestamp = now;
+    const uint32_t k = atomicAdd(count, 1u);
+    if (k < cap) out[k] = m;
+}
+
 __global__ void k_init_slots(ClusterState st, const uint32_t *slots, uint32_t n) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
     if (i >= n) return;
@@ -1581,6 +1598,14 @@ void cparam_sum(const CParamState &st, uint32_t slot, int64_t value, int64_t now
 
 void cparam_init_rule(const CParamState &st, uint32_t slot, hipStream_t s) {
     hipLaunchKernelGGL(k_pinit_rule, dim3(1), dim3(64), 0, s, st, slot);
+}
+
+void cluster_metric_nodes(const ClusterState &st, const int64_t *slot_fid, int64_t now, void *out, uint32_t cap,
+                          uint32_t *count, hipStream_t s) {
+    SGA_HIP_CHECK(hipMemsetAsync(count, 0, 4, s));
+    if (st.nslots == 0) return;
+    hipLaunchKernelGGL(k_cluster_nodes, dim3((st.nslots + kThreads - 1) / kThreads), dim3(kThreads), 0, s, st,
+                       slot_fid, now, (sga_cluster_metric_node *)out, cap, count);
 }
 
 void cluster_init_limiter(NsLimiterDev *d, hipStream_t s) {

@@ -1,6 +1,7 @@
 // Device-side state and launch interface of the cluster token server path
 // (ClusterFlowChecker + ClusterMetric over ClusterMetricLeapArray).
 #pragma once
+#include "../../include/sentinel_amd.h"
 #include "common.hpp"
 #include "radix_sort.hpp"
 
@@ -177,6 +178,11 @@ void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
 // ClusterParamMetric.getSum(value) at now (rotation side effect included); *d_out = -1 if no key
 void cparam_sum(const CParamState &st, uint32_t slot, int64_t value, int64_t now, int64_t *d_out, hipStream_t s);
 void cparam_init_rule(const CParamState &st, uint32_t slot, hipStream_t s);
+
+// ClusterMetricNodeGenerator.flowToMetricNode for every active slot (out: sga_cluster_metric_node,
+// count: device u32; slot_fid: flowId per slot).
+void cluster_metric_nodes(const ClusterState &st, const int64_t *slot_fid, int64_t now, void *out, uint32_t cap,
+                          uint32_t *count, hipStream_t stream);
 
 // Fresh limiter state (every bucket absent).
 void cluster_init_limiter(NsLimiterDev *d, hipStream_t stream);

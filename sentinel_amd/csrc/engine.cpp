@@ -63,6 +63,9 @@ struct Engine {
     DevBuf<SlotOcc> d_occ;
     DevBuf<int64_t> d_rec;  // 8 int64 per bucket
     DevBuf<HashEntry> d_htab;
+    DevBuf<int64_t> d_slot_fid;  // flowId per slot (metric snapshots)
+    DevBuf<uint32_t> d_ncount;
+    DevBuf<uint8_t> d_nodes;
     DevBuf<uint32_t> d_dense;  // dense flowId table (see sync_device)
     DevBuf<uint32_t> d_wtab;
     uint32_t dense_n = 0;
@@ -321,6 +324,15 @@ struct Engine {
             p.ns = h.ns;
         }
         if (ns) SGA_HIP_CHECK(hipMemcpyAsync(d_param.p, hp.data(), ns * sizeof(SlotParam), hipMemcpyHostToDevice, stream));
+        {
+            std::vector<int64_t> fids(std::max<size_t>(ns, 1), 0);
+            for (size_t i = 0; i < ns; ++i) fids[i] = slots[i].flow_id;
+            if (d_slot_fid.n < fids.size()) {
+                SGA_HIP_CHECK(hipStreamSynchronize(stream));
+                d_slot_fid.alloc(std::max<size_t>(fids.size(), 2 * d_slot_fid.n));
+            }
+            SGA_HIP_CHECK(hipMemcpyAsync(d_slot_fid.p, fids.data(), fids.size() * 8, hipMemcpyHostToDevice, stream));
+        }
         // hash table over active rules
         size_t nact = 0;
         for (auto &h : slots) nact += h.active ? 1 : 0;
@@ -957,6 +969,51 @@ int sga_query_node(sga_engine *e, uint32_t resource, int64_t now, sga_node_view 
     return guarded(e, [&](Engine &g) {
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
         return g.flow.query(resource, now, out);
+    });
+}
+
+int sga_metrics_snapshot(sga_engine *e, int64_t now, sga_metric_node *out, size_t cap, size_t *n) {
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        return g.flow.metrics(now, out, cap, n);
+    });
+}
+
+static int cluster_nodes_impl(Engine &g, int64_t now, void *d_out, size_t cap, uint32_t *d_n, hipStream_t s) {
+    if (cap > 0xFFFFFFFFu) cap = 0xFFFFFFFFu;
+    if (!g.d_slot_fid.p) {
+        SGA_HIP_CHECK(hipMemsetAsync(d_n, 0, 4, s));
+        return SGA_OK;
+    }
+    sga::cluster_metric_nodes(g.state(), g.d_slot_fid.p, now, d_out, (uint32_t)cap, d_n, s);
+    SGA_HIP_CHECK(hipGetLastError());
+    return SGA_OK;
+}
+
+int sga_cluster_metric_nodes(sga_engine *e, int64_t now, sga_cluster_metric_node *out, size_t cap, size_t *n) {
+    if (now < 0 || !n || (cap && !out)) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        const size_t dcap = std::max<size_t>(cap, 1);
+        if (g.d_nodes.n < dcap * sizeof(sga_cluster_metric_node)) g.d_nodes.alloc(dcap * sizeof(sga_cluster_metric_node));
+        if (!g.d_ncount.p) g.d_ncount.alloc(1);
+        cluster_nodes_impl(g, now, g.d_nodes.p, cap, g.d_ncount.p, g.stream);
+        uint32_t cnt = 0;
+        SGA_HIP_CHECK(hipMemcpyAsync(&cnt, g.d_ncount.p, 4, hipMemcpyDeviceToHost, g.stream));
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        const size_t w = std::min<size_t>(cnt, cap);
+        if (w) SGA_HIP_CHECK(hipMemcpy(out, g.d_nodes.p, w * sizeof(sga_cluster_metric_node), hipMemcpyDeviceToHost));
+        *n = w;
+        return cnt > cap ? SGA_ERANGE : SGA_OK;
+    });
+}
+
+int sga_cluster_metric_nodes_device(sga_engine *e, int64_t now, sga_cluster_metric_node *d_out, size_t cap,
+                                    uint32_t *d_n, void *hip_stream) {
+    if (now < 0 || !d_n || (cap && !d_out)) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        return cluster_nodes_impl(g, now, d_out, cap, d_n, hip_stream ? (hipStream_t)hip_stream : g.stream);
     });
 }
 

@@ -974,6 +974,45 @@ __global__ void k_init_nodes(int64_t *node, uint32_t n, int64_t max_rt) {
         mb_zero(p + kNodeMin + kMB * j, max_rt);
     }
     p[kNodeThreads] = 0;
+    p[kNodeLastFetch] = -1;
+}
+
+// StatisticNode.metrics() (CORE/node/StatisticNode.java:120-157) over ArrayMetric.details()
+// (ArrayMetric.java:166-218): rotate the minute window at now, then every listed bucket
+// (LeapArray.list(now): not deprecated) becomes a MetricNode; those newer than lastFetchTime,
+// older than the current second and with a non-zero field are emitted.
+__global__ __launch_bounds__(kT) void k_metrics(FlowState st, int64_t max_rt, int64_t now, sga_metric_node *out,
+                                                uint32_t cap, uint32_t *count) {
+    const uint32_t r = blockIdx.x * kT + threadIdx.x;
+    if (r >= st.nres) return;
+    int64_t *node = st.node + (size_t)r * kNodeWords;
+    const int64_t cur = now - now % 1000;
+    min_current(node, now, max_rt);
+    const int64_t last = node[kNodeLastFetch];
+    int64_t nlast = last;
+    for (int j = 0; j < 60; ++j) {
+        const int64_t *b = node + kNodeMin + kMB * j;
+        if (b[0] == kAbsent || now - b[0] > kMinInterval) continue;
+        sga_metric_node m;
+        m.timestamp = b[0];
+        m.pass_qps = b[MB_PASS];
+        m.block_qps = b[MB_BLOCK];
+        m.success_qps = b[MB_SUCC];
+        m.exception_qps = b[MB_EXC];
+        m.rt = m.success_qps != 0 ? b[MB_RT] / m.success_qps : b[MB_RT];
+        m.occupied_pass_qps = b[MB_OPASS];
+        m.resource = r;
+        m.concurrency = 0;
+        const bool in_time = m.timestamp > last && m.timestamp < cur;
+        const bool valid = m.pass_qps > 0 || m.block_qps > 0 || m.success_qps > 0 || m.exception_qps > 0 ||
+                           m.rt > 0 || m.occupied_pass_qps > 0;
+        if (in_time && valid) {
+            const uint32_t k = atomicAdd(count, 1u);
+            if (k < cap) out[k] = m;
+            nlast = m.timestamp > nlast ? m.timestamp : nlast;
+        }
+    }
+    node[kNodeLastFetch] = nlast;
 }
 
 __global__ void k_clear_ptab(PEntry *t, uint32_t n) {
@@ -1406,6 +1445,25 @@ int FlowEngine::query(uint32_t r, int64_t now, sga_node_view *out) {
     out->cur_thread_num = iv[4];
     out->waiting = iv[5];
     return 0;
+}
+
+int FlowEngine::metrics(int64_t now, sga_metric_node *out, size_t cap, size_t *n) {
+    if (now < 0 || !n || (cap && !out)) return SGA_EINVAL;
+    *n = 0;
+    if (nres == 0) return 0;
+    const size_t dcap = std::max<size_t>(cap, 1);
+    if (d_metrics.n < dcap) d_metrics.alloc(dcap);
+    if (!d_mcount.p) d_mcount.alloc(1);
+    SGA_HIP_CHECK(hipMemsetAsync(d_mcount.p, 0, 4, stream));
+    hipLaunchKernelGGL(k_metrics, dim3((nres + kT - 1) / kT), dim3(kT), 0, stream, state(),
+                       (int64_t)cfg.statistic_max_rt, now, d_metrics.p, (uint32_t)cap, d_mcount.p);
+    uint32_t cnt = 0;
+    SGA_HIP_CHECK(hipMemcpyAsync(&cnt, d_mcount.p, 4, hipMemcpyDeviceToHost, stream));
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    const size_t w = std::min<size_t>(cnt, cap);
+    if (w) SGA_HIP_CHECK(hipMemcpy(out, d_metrics.p, w * sizeof(sga_metric_node), hipMemcpyDeviceToHost));
+    *n = w;
+    return cnt > cap ? SGA_ERANGE : 0;
 }
 
 int FlowEngine::cb_state(uint32_t r, uint32_t k) {

@@ -19,6 +19,7 @@ constexpr int kNodeSec = 0;                       // 2 x 8
 constexpr int kNodeBor = kNodeSec + 2 * kMB;      // 2 x 2 (start, PASS)
 constexpr int kNodeMin = kNodeBor + 4;            // 60 x 8
 constexpr int kNodeThreads = kNodeMin + 60 * kMB; // curThreadNum
+constexpr int kNodeLastFetch = kNodeThreads + 1;  // StatisticNode.lastFetchTime (-1 initially)
 constexpr int kNodeWords = kNodeThreads + 4;      // 504 words = 4032 B (64-B aligned)
 
 struct FlowRuleDev {    // one rater (TrafficShapingController) + its FlowRule fields
@@ -155,6 +156,9 @@ struct FlowEngine {
                int32_t *wait_ms);
     int query(uint32_t resource, int64_t now, sga_node_view *out);
     int cb_state(uint32_t resource, uint32_t k);
+    int metrics(int64_t now, sga_metric_node *out, size_t cap, size_t *n);
+    DevBuf<sga_metric_node> d_metrics;
+    DevBuf<uint32_t> d_mcount;
 };
 
 }  // namespace sga

@@ -100,6 +100,27 @@ class NodeView:
     waiting: int
 
 
+@dataclass
+class MetricNode:
+    """CORE/node/metric/MetricNode.java:28-51 (one resource, one second)."""
+    timestamp: int
+    resource: str
+    pass_qps: int
+    block_qps: int
+    success_qps: int
+    exception_qps: int
+    rt: int
+    occupied_pass_qps: int
+    concurrency: int = 0
+    classification: int = 0
+
+    def to_thin_string(self) -> str:
+        """MetricNode.toThinString (:160-176): the metric log line the dashboard reads."""
+        return "|".join(str(x) for x in (self.timestamp, self.resource.replace("|", "_"), self.pass_qps,
+                                         self.block_qps, self.success_qps, self.exception_qps, self.rt,
+                                         self.occupied_pass_qps, self.concurrency, self.classification))
+
+
 class Entry:
     """A passed entry; exit() records RT / success (StatisticSlot.exit) and breaker completion."""
 
@@ -180,6 +201,19 @@ class LocalSentinel:
         v = SgaNodeView()
         check(_lib.load().sga_query_node(self.engine.handle, rid, now, C.byref(v)), self.engine.handle, "node")
         return NodeView(*[getattr(v, f) for f, _ in SgaNodeView._fields_])
+
+    def metrics(self, now: int, cap: int = 1 << 16) -> List[MetricNode]:
+        """MetricTimerListener.run (CORE/node/metric/MetricTimerListener.java:44-65): StatisticNode.metrics()
+        of every resource at `now`, ordered by timestamp then resource (the TreeMap the reference writes)."""
+        buf = (_lib.SgaMetricNode * max(1, cap))()
+        n = C.c_size_t()
+        rc = _lib.load().sga_metrics_snapshot(self.engine.handle, now, buf, cap, C.byref(n))
+        _lib.check(rc, self.engine.handle, "metrics")
+        out = [MetricNode(b.timestamp, self.resources[b.resource], b.pass_qps, b.block_qps, b.success_qps,
+                          b.exception_qps, b.rt, b.occupied_pass_qps, b.concurrency)
+               for b in buf[:n.value]]
+        out.sort(key=lambda m: (m.timestamp, self.ids[m.resource]))
+        return out
 
     def circuit_breaker_state(self, resource, k: int = 0) -> int:
         rid = resource if isinstance(resource, int) else self.ids[resource]

@@ -109,6 +109,7 @@ def lib():
         "orc_cmetric_sum": (I64, [P, I64, C.c_int]),
         "orc_cmetric_avg": (D, [P, I64, C.c_int]),
         "orc_cmetric_try_occupy_next": (I32, [P, I64, C.c_int, I32, D]),
+        "orc_flow_metrics": (C.c_size_t, [P, I64, P, C.c_size_t]),
         "orc_pmetric_new": (P, [C.c_int, C.c_int]),
         "orc_pmetric_free": (None, [P]),
         "orc_pmetric_add": (None, [P, I64, I64, I32]),
@@ -233,6 +234,12 @@ def java_obj_key(v):
     if isinstance(v, str):
         return int(lib().orc_java_string_hash(v.encode()))
     return int(v)
+
+
+class OrcMetricNode(C.Structure):
+    _fields_ = [("timestamp", C.c_int64), ("pass_qps", C.c_int64), ("block_qps", C.c_int64),
+                ("success_qps", C.c_int64), ("exception_qps", C.c_int64), ("rt", C.c_int64),
+                ("occupied_pass_qps", C.c_int64), ("resource", C.c_uint32), ("concurrency", C.c_int32)]
 
 
 class OrcClusterParamRule(C.Structure):
