@@ -181,6 +181,15 @@ def main():
     if rank == 0 and not args.no_cpu:
         cpu_baseline = run_cpu_baseline(args, n_gpus)
 
+    # HBM traffic per step from the committed rocprofv3 PMC passes of this pipeline
+    # (tools/pmc_bench.sh -> tools/pmc_summary.py --json; 2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction)
+    traffic, traffic_src = None, None
+    tpath = os.path.join(ROOT, "profiles", "traffic_c3.json")
+    if os.path.exists(tpath) and args.batch == PER_RANK_BATCH and args.rules == N_RULES:
+        with open(tpath) as fh:
+            tj = json.load(fh)
+        traffic, traffic_src = tj["traffic_bytes_per_step"], "profiles/traffic_c3.json (" + tj.get("run", "") + ")"
+
     if rank == 0:
         value = total_events / wall_max
         per_gpu_events = total_events / n_gpus
@@ -206,7 +215,8 @@ def main():
                        "global_requests_per_step": args.batch * n_gpus, "lambda_per_virtual_s": lam,
                        "parallelism": f"shard{n_gpus}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "sga_request_tokens_device pipeline (classify+sort+runs+flows+results), "
                                    "HIP events on the engine stream",
                          "bytes_alg_per_step_per_gpu": bytes_alg / args.steps,
@@ -222,49 +232,87 @@ def main():
 
 
 def run_cpu_baseline(args, n_gpus):
-    """Oracle (single-threaded C restatement of ClusterFlowChecker) on a bounded
-    sample of the same workload: the first `cpu_sample` requests of rank 0's
-    shard stream at 1M rules."""
+    """CPU restatement of the same path on this host (the reference's JMH harness needs a JDK,
+    which the image lacks).  Bounded sample: the first `cpu_sample` requests of rank 0's shard
+    stream of the same C3 trace at 1M rules.
+      1 thread : the single-threaded C oracle (oracle/sentinel_oracle.c, ClusterFlowChecker
+                 restatement) replays the sample in order;
+      T threads: the sample's rules split by splitmix64(flowId) mod T, one oracle instance per
+                 thread replaying its sub-stream (rules are independent, as on the GPUs);
+                 ctypes releases the GIL, so the threads run in parallel.  `value` is this one."""
+    import threading
     try:
         from tests import oracle_harness as H
         from sentinel_amd.workload import ClusterTrace, shard_of
     except Exception as e:  # pragma: no cover
         return {"value": None, "error": str(e)}
     L = H.lib()
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
     tr = ClusterTrace(n_rules=args.rules, lam=LAMBDA_PER_GPU * n_gpus)
     fid_all, cnt_all = tr.rules()
     mine = shard_of(fid_all, n_gpus) == 0
-    rules = np.zeros(int(mine.sum()), dtype=[("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"),
-                                           ("sample_count", "<i4"), ("window_interval_ms", "<i4"), ("grade", "<i4"),
-                                           ("strategy", "<i4"), ("reserved", "<i4")])
-    rules["flow_id"] = fid_all[mine]
-    rules["count"] = cnt_all[mine]
-    rules["threshold_type"] = 1
-    rules["sample_count"] = 10
-    rules["window_interval_ms"] = 1000
-    rules["grade"] = 1
-    assert rules.itemsize == C.sizeof(H.OrcClusterRule), "oracle rule layout mismatch"
-    oh = L.orc_cluster_new(1.0, 1.0)
-    L.orc_cluster_load_rules(oh, b"default", rules.ctypes.data_as(C.POINTER(H.OrcClusterRule)), len(rules))
-    total, dt = 0, 0.0
-    chunk = 1 << 22
-    g = 0
+    fid_m, cnt_m = fid_all[mine], cnt_all[mine]
+
+    def new_oracle(sel):
+        rules = np.zeros(int(sel.sum()), dtype=[("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"),
+                                                ("sample_count", "<i4"), ("window_interval_ms", "<i4"),
+                                                ("grade", "<i4"), ("strategy", "<i4"), ("reserved", "<i4")])
+        rules["flow_id"] = fid_m[sel]
+        rules["count"] = cnt_m[sel]
+        rules["threshold_type"] = 1
+        rules["sample_count"] = 10
+        rules["window_interval_ms"] = 1000
+        rules["grade"] = 1
+        assert rules.itemsize == C.sizeof(H.OrcClusterRule), "oracle rule layout mismatch"
+        oh = L.orc_cluster_new(1.0, 1.0)
+        L.orc_cluster_load_rules(oh, b"default", rules.ctypes.data_as(C.POINTER(H.OrcClusterRule)), len(rules))
+        return oh
+
+    # the bounded sample (generation untimed)
+    chunks, total, g, chunk = [], 0, 0, 1 << 22
     while total < args.cpu_sample:
         f, a, p, ts = tr.events(g, chunk)
         g += chunk
         sel = shard_of(f, n_gpus) == 0
         f, a, p, ts = [np.ascontiguousarray(x[sel]) for x in (f, a, p, ts)]
-        out = (H.OrcTokenResult * len(f))()
-        t0 = time.perf_counter()
-        L.orc_cluster_replay(oh, len(f), f.ctypes.data, a.ctypes.data, p.ctypes.data, ts.ctypes.data, out)
-        dt += time.perf_counter() - t0
+        chunks.append((f, a, p, ts))
         total += len(f)
+
+    def replay(oh, parts):
+        for f, a, p, ts in parts:
+            out = (H.OrcTokenResult * max(1, len(f)))()
+            L.orc_cluster_replay(oh, len(f), f.ctypes.data, a.ctypes.data, p.ctypes.data, ts.ctypes.data, out)
+
+    oh = new_oracle(np.ones(len(fid_m), dtype=bool))
+    t0 = time.perf_counter()
+    replay(oh, chunks)
+    dt1 = time.perf_counter() - t0
     L.orc_cluster_free(oh)
-    return {"value": total / dt, "unit": "decisions/s", "cores": 1, "kind": "port",
-            "sample": f"{total} requests of the rank-0 shard stream of the same C3 trace, replayed by the "
-                      f"single-threaded C oracle (oracle/sentinel_oracle.c ClusterFlowChecker restatement); "
-                      f"JMH reference unavailable (no JDK on host)",
-            "seconds": dt}
+
+    sub = shard_of(fid_m, threads)
+    ohs = [new_oracle(sub == k) for k in range(threads)]
+    parts = [[] for _ in range(threads)]
+    for f, a, p, ts in chunks:
+        fs = shard_of(f, threads)
+        for k in range(threads):
+            m = fs == k
+            parts[k].append(tuple(np.ascontiguousarray(x[m]) for x in (f, a, p, ts)))
+    ths = [threading.Thread(target=replay, args=(ohs[k], parts[k])) for k in range(threads)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    dtn = time.perf_counter() - t0
+    for o in ohs:
+        L.orc_cluster_free(o)
+    return {"value": total / dtn, "unit": "decisions/s", "cores": threads, "kind": "port",
+            "value_1thread": total / dt1,
+            "sample": f"{total} requests of the rank-0 shard stream of the same C3 trace (1M rules), replayed by "
+                      f"the C oracle (oracle/sentinel_oracle.c ClusterFlowChecker restatement): {threads} threads "
+                      f"over disjoint rule subsets (splitmix64(flowId) mod {threads}); value_1thread = one "
+                      f"thread in arrival order; reference JMH harness unavailable (no JDK on host)",
+            "seconds": dtn, "seconds_1thread": dt1}
 
 
 if __name__ == "__main__":

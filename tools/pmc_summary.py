@@ -49,5 +49,6 @@ if steps:
     if a.json:
         json.dump({"traffic_bytes_per_step": per_step, "fetch_bytes_per_step_raw": tot_fetch / steps,
                    "write_bytes_per_step": tot_write / steps, "dispatch_sets": steps,
+                   "run": os.path.basename(os.path.normpath(a.dir)),
                    "note": "2*FETCH_SIZE+WRITE_SIZE (KiB->B) summed over the engine kernels of one step"},
                   open(a.json, "w"), indent=1)
