@@ -90,10 +90,14 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
                                                        const uint32_t *__restrict__ ts_off, int64_t ts_base,
                                                        uint32_t n, int simple, uint32_t invalid_key,
                                                        uint64_t *__restrict__ el, uint64_t *__restrict__ out,
-                                                       int hist_d, uint32_t ntiles, uint32_t *__restrict__ hist) {
+                                                       int hist_d, uint32_t ntiles, uint32_t *__restrict__ hist,
+                                                       int lb_npass, uint32_t *__restrict__ ghist) {
+    // hist_d > 0: this tile's histogram of the first digit (hist + scan sorts);
+    // lb_npass > 0: the global totals of every digit (look-back sorts)
     __shared__ uint32_t h[1024];
-    if (hist_d > 0) {
-        for (uint32_t d = threadIdx.x; d < (1u << hist_d); d += kThreads) h[d] = 0;
+    const uint32_t nh = lb_npass > 0 ? (uint32_t)lb_npass << hist_d : (hist_d > 0 ? 1u << hist_d : 0u);
+    if (nh) {
+        for (uint32_t d = threadIdx.x; d < nh; d += kThreads) h[d] = 0;
         __syncthreads();
     }
     const uint32_t tbase = blockIdx.x * kTileElems;
@@ -163,12 +167,22 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
                 }
                 el[i] = el_pack(key, bd6, p, a7, i);
             }
-            if (hist_d > 0) atomicAdd(&h[key & ((1u << hist_d) - 1)], 1u);
+            if (lb_npass > 0) {
+                for (int p = 0; p < lb_npass; ++p)
+                    atomicAdd(&h[((uint32_t)p << hist_d) + ((key >> (p * hist_d)) & ((1u << hist_d) - 1))], 1u);
+            } else if (hist_d > 0) {
+                atomicAdd(&h[key & ((1u << hist_d) - 1)], 1u);
+            }
         }
     }
-    if (hist_d > 0) {
+    if (nh) {
         __syncthreads();
-        for (uint32_t d = threadIdx.x; d < (1u << hist_d); d += kThreads) hist[(size_t)d * ntiles + blockIdx.x] = h[d];
+        if (lb_npass > 0) {
+            for (uint32_t i = threadIdx.x; i < nh; i += kThreads)
+                if (h[i]) atomicAdd(&ghist[i], h[i]);
+        } else {
+            for (uint32_t d = threadIdx.x; d < nh; d += kThreads) hist[(size_t)d * ntiles + blockIdx.x] = h[d];
+        }
     }
 }
 
@@ -415,9 +429,11 @@ __global__ __launch_bounds__(kRunThreads) void k_runs_down(const uint64_t *__res
         const bool fh = e == 0 || el_slot(cur) != el_slot(px);
         const bool h = e == 0 || el_runkey(cur) != el_runkey(px);
         if (h) {
+            const uint32_t bd = (uint32_t)((cur >> kBdShift) & kBdEsc);
             sc.run_start[rid] = e;
             sc.run_slot[rid] = el_slot(cur);
             sc.run_idx0[rid] = el_idx(cur);
+            sc.run_bd[rid] = (uint8_t)bd;
             sc.run_p0[rid] = run.np - p;
         }
         if (fh) sc.flow_first_run[run.nf - 1] = rid;
@@ -601,17 +617,20 @@ __device__ __forceinline__ int64_t div_pos(int64_t a, int64_t b) {
 struct RunIn {
     uint32_t j0, n, cp_tot, p0;
     int32_t a;
-    int64_t t0;
+    uint32_t bd;  // bucket delta of the run (its bucket = ts_base / W + bd)
 };
 
 template <bool kPrio>
 __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &sc, uint32_t s, const SlotParam &P,
-                                         const Rec &R, double thr, const RunIn &ri, uint32_t r) {
+                                         const Rec &R, double thr, int64_t qbase, const RunIn &ri, uint32_t r) {
     if (!kPrio && ri.cp_tot > 0) return false;  // prioritized runs go to k_flows_slow
-    const int64_t t0 = ri.t0;
+    // Cluster rules have intervalInMs = sampleCount x windowLengthInMs (checkClusterField), so every
+    // validity test below (isWindowDeprecated, getValidHead) gives the same answer for any time in
+    // the run's bucket: the bucket start stands in for the first request's time.
     const int32_t a = ri.a;
-    const int64_t q = div_pos(t0, P.W);  // bucket number
+    const int64_t q = qbase + ri.bd;  // bucket number
     const int64_t ws = q * P.W;
+    const int64_t t0 = ws;
     const int64_t qs = div_pos(q, P.S);
     const int cj = (int)(q - qs * P.S);
     const int jh = cj + 1 == P.S ? 0 : cj + 1;  // LeapArray.getValidHead index ((t0 + W) / W) % S
@@ -749,24 +768,21 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
     return true;
 }
 
-__device__ __forceinline__ RunIn run_in(const BatchScratch &sc, const uint32_t *ts_off, int64_t ts_base, uint32_t r,
-                                        uint32_t nruns, uint32_t nvalid) {
+__device__ __forceinline__ RunIn run_in(const BatchScratch &sc, uint32_t r, uint32_t nruns, uint32_t nvalid) {
     RunIn ri;
     ri.j0 = sc.run_start[r];
     ri.n = (r + 1 < nruns ? sc.run_start[r + 1] : nvalid) - ri.j0;
     ri.cp_tot = sc.run_cp[r];
     ri.p0 = sc.run_p0[r];
     ri.a = sc.run_acq[r];
-    ri.t0 = ts_base + (int64_t)ts_off[sc.run_idx0[r]];
+    ri.bd = sc.run_bd[r];
     return ri;
 }
 
 // One rule per lane walks the rule's runs in time order, closed form only.  At the first run
 // that needs the per-request replay the rest of the rule is deferred to k_flows_slow (rare), so
 // this kernel stays small and keeps many rules in flight.
-__global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratch sc,
-                                                    const uint32_t *__restrict__ ts_off, int64_t ts_base,
-                                                    int simple) {
+__global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratch sc, int64_t ts_base, int simple) {
     const uint32_t nflows = sc.counters[2];
     const uint32_t nruns = sc.counters[1];
     const uint32_t nvalid = sc.counters[0];
@@ -777,9 +793,10 @@ __global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratc
         const SlotParam P = st.param[s];
         const Rec R = rec_of(st, P);
         const double thr = simple ? P.thr_simple : P.thr;
+        const int64_t qbase = div_pos(ts_base, P.W);
         for (uint32_t r = r0; r < r1; ++r) {
-            const RunIn ri = run_in(sc, ts_off, ts_base, r, nruns, nvalid);
-            if (!run_fast<true>(st, sc, s, P, R, thr, ri, r)) {
+            const RunIn ri = run_in(sc, r, nruns, nvalid);
+            if (!run_fast<true>(st, sc, s, P, R, thr, qbase, ri, r)) {
                 const uint32_t k = atomicAdd(&sc.counters[6], 1u);
                 sc.deferred[2 * k] = fl;
                 sc.deferred[2 * k + 1] = r;
@@ -808,9 +825,10 @@ __global__ __launch_bounds__(kThreads) void k_flows_slow(ClusterState st, BatchS
         const SlotParam P = st.param[s];
         const Rec R = rec_of(st, P);
         const double thr = simple ? P.thr_simple : P.thr;
+        const int64_t qbase = div_pos(ts_base, P.W);
         for (uint32_t r = rd; r < r1; ++r) {
-            const RunIn ri = run_in(sc, ts_off, ts_base, r, nruns, nvalid);
-            if (r > rd && run_fast<true>(st, sc, s, P, R, thr, ri, r)) continue;
+            const RunIn ri = run_in(sc, r, nruns, nvalid);
+            if (r > rd && run_fast<true>(st, sc, s, P, R, thr, qbase, ri, r)) continue;
             for (uint32_t j = ri.j0; j < ri.j0 + ri.n; ++j) {
                 const uint32_t i = el_idx(el[j]);
                 const int64_t t = ts_base + (int64_t)ts_off[i];
@@ -1448,6 +1466,7 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     size_t b = 0;
     b += 2 * align_up(cap * 8);                 // elements (double buffer)
     b += 7 * align_up((cap + 1) * 4);           // run_start/slot/idx0/cp/p0/acq, flow_first_run
+    b += align_up(cap + 1);                     // run_bd
     b += align_up(cap * 4);                     // plist
     b += align_up(cap * 8);                     // deferred (flow, run)
     b += align_up(cap * sizeof(RunOut));        // run_out
@@ -1456,6 +1475,7 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up(64);
     b += 2 * align_up(hist * 4) + align_up(scan_partials_needed(hist) * 4 + 64);
     b += align_up(scan_partials_needed(cap) * 4 + 64);
+    b += align_up(kRadixGhistWords * 4) + align_up(64);  // look-back digit totals, error flag
     return b;
 }
 
@@ -1477,6 +1497,7 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.run_p0 = (uint32_t *)take((cap + 1) * 4);
     sc.run_acq = (int32_t *)take((cap + 1) * 4);
     sc.flow_first_run = (uint32_t *)take((cap + 1) * 4);
+    sc.run_bd = (uint8_t *)take(cap + 1);
     sc.plist = (uint32_t *)take(cap * 4);
     sc.deferred = (uint32_t *)take(cap * 8);
     sc.run_out = (RunOut *)take(cap * sizeof(RunOut));
@@ -1489,6 +1510,8 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.radix.hist_scan = (uint32_t *)take(hist * 4);
     sc.radix.partial = (uint32_t *)take(scan_partials_needed(hist) * 4 + 64);
     sc.lim_partial = (uint32_t *)take(scan_partials_needed(cap) * 4 + 64);
+    sc.radix.ghist = (uint32_t *)take(kRadixGhistWords * 4);
+    sc.radix.err = (uint32_t *)take(64);
     sc.cap = cap;
 }
 
@@ -1505,11 +1528,16 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     const uint32_t ntiles = (n + kTileElems - 1) / kTileElems;
     static_assert(kTileElems == kRadix64Tile, "classify tiles are sort tiles");
     SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, s));
+    const bool lb = radix64_lookback() != 0;
+    const int npass = (bits + d0 - 1) / d0;
+    if (lb) SGA_HIP_CHECK(hipMemsetAsync(sc.radix.ghist, 0, kRadixGhistWords * sizeof(uint32_t), s));
+    if (lb) SGA_HIP_CHECK(hipMemsetAsync(sc.radix.err, 0, sizeof(uint32_t), s));
     hipLaunchKernelGGL(k_classify, dim3(ntiles), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n,
-                       simple, invalid_key, sc.el[0], out, limited ? 0 : d0, ntiles, sc.radix.hist);
+                       simple, invalid_key, sc.el[0], out, limited ? 0 : d0, ntiles, sc.radix.hist,
+                       (lb && !limited) ? npass : 0, sc.radix.ghist);
     if (!simple) apply_limiters(st.param, sc, sc.el[0], n, invalid_key, ts_base, ts_off, out, lims, nlims, s);
-    const int npass = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, !limited);
-    const uint64_t *el = sc.el[npass & 1];
+    const int np = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, !limited);
+    const uint64_t *el = sc.el[np & 1];
     hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
                        sc.tile_valid);
     hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
@@ -1519,7 +1547,7 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     const uint64_t max_flows = n < st.nslots ? n : st.nslots;
     uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows + kThreads - 1) / kThreads, 16384);
     if (fb == 0) fb = 1;
-    hipLaunchKernelGGL(k_flows, dim3(fb), dim3(kThreads), 0, s, st, sc, ts_off, ts_base, simple);
+    hipLaunchKernelGGL(k_flows, dim3(fb), dim3(kThreads), 0, s, st, sc, ts_base, simple);
     hipLaunchKernelGGL(k_flows_slow, dim3(std::min<uint32_t>(fb, 1024)), dim3(kThreads), 0, s, st, sc, acquire, prio,
                        ts_off, ts_base, el, simple, out);
     hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, invalid_key, out);

@@ -91,6 +91,7 @@ struct BatchScratch {
     // run records (index = run id, runs in sorted order)
     uint32_t *run_start, *run_slot, *run_idx0, *run_cp, *run_p0;
     int32_t *run_acq;         // common acquire count, 0 = mixed / escaped (replay)
+    uint8_t *run_bd;          // bucket delta of the run
     uint32_t *flow_first_run; // per rule touched in the batch: its first run
     uint32_t *plist;          // sorted positions of prioritized requests (ascending)
     uint32_t *deferred;       // (flow, run) pairs handed from k_flows to k_flows_slow

@@ -671,6 +671,14 @@ static int run_host_batch(Engine &g, const int64_t *flow_id, const int32_t *acqu
         SGA_HIP_CHECK(hipGetLastError());
         SGA_HIP_CHECK(hipMemcpyAsync(out + b, g.d_out.p, m * 8, hipMemcpyDeviceToHost, g.stream));
         SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        if (sga::radix64_lookback()) {  // a look-back that gave up would have sorted wrongly
+            uint32_t err = 0;
+            SGA_HIP_CHECK(hipMemcpy(&err, g.scratch.radix.err, 4, hipMemcpyDeviceToHost));
+            if (err) {
+                g.err = "radix look-back timed out";
+                return SGA_EIO;
+            }
+        }
         b += m;
     }
     return SGA_OK;

@@ -471,6 +471,28 @@ __global__ __launch_bounds__(kThreads) void k_rs64_hist(const uint64_t *__restri
     for (int d = threadIdx.x; d < RADIX; d += kThreads) hist[(size_t)d * ntiles + tile] = h[d];
 }
 
+// Global digit totals of every pass in one read of the elements (look-back mode).
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_rs64_upfront(const uint64_t *__restrict__ el, uint32_t n, int shift,
+                                                           int npass, uint32_t *__restrict__ ghist) {
+    constexpr int RADIX = 1 << D;
+    __shared__ uint32_t h[kMaxPasses * RADIX];
+    for (int d = threadIdx.x; d < kMaxPasses * RADIX; d += kThreads) h[d] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * kTile;
+#pragma unroll 4
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t e = base + r * kThreads + threadIdx.x;
+        if (e < n) {
+            const uint64_t k = el[e];
+            for (int p = 0; p < npass; ++p) atomicAdd(&h[p * RADIX + ((uint32_t)(k >> (shift + p * D)) & (RADIX - 1))], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < npass * RADIX; i += kThreads)
+        if (h[i]) atomicAdd(&ghist[i], h[i]);
+}
+
 template <int D>
 struct Sweep64Smem {
     static constexpr int RADIX = 1 << D;
@@ -562,6 +584,152 @@ __global__ __launch_bounds__(kThreads) void k_rs64_sweep(const uint64_t *__restr
             if (d < RADIX) sm.dstart[d] = pre;
             pre += tot[k];
         }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t e = wbase + r * 64 + lane;
+        if (e < n) {
+            const uint32_t d = (uint32_t)(key[r] >> shift) & (RADIX - 1);
+            sm.sel[pos[r] + sm.dstart[d] + sm.wcnt[wave][d]] = key[r];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t i = r * kThreads + threadIdx.x;
+        if (i < tn) {
+            const uint64_t k = sm.sel[i];
+            const uint32_t d = (uint32_t)(k >> shift) & (RADIX - 1);
+            out[sm.gbase[d] + (i - sm.dstart[d])] = k;
+        }
+    }
+}
+
+
+// Single pass per digit (decoupled look-back): the tile id comes from a counter (tiles start in
+// order, so every look-back target has started), the tile publishes its per-digit counts as an
+// aggregate, walks back over predecessors until an inclusive prefix, then publishes its own
+// inclusive prefix.  Status words: flag (bits 31:30) | count, published by agent-scope atomic adds
+// and polled with agent-scope loads (cross-XCD visible).  The wait is bounded: a look-back that
+// gives up sets err[0] (never expected; the host API reports it) instead of hanging the GPU.
+constexpr uint32_t kLbAgg = 1u << 30, kLbPrefix = 2u << 30, kLbCount = (1u << 30) - 1;
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_rs64_sweep_lb(const uint64_t *__restrict__ in, uint32_t n, int shift,
+                                                            const uint32_t *__restrict__ digit_base,
+                                                            uint32_t *__restrict__ status, uint32_t *tile_ctr,
+                                                            uint32_t *err, uint64_t *__restrict__ out) {
+    constexpr int RADIX = 1 << D;
+    constexpr int DPT = RADIX >= kThreads ? RADIX / kThreads : 1;
+    __shared__ Sweep64Smem<D> sm;
+    __shared__ uint32_t ws[kWaves];
+    __shared__ uint32_t stile;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) stile = atomicAdd(tile_ctr, 1u);
+    for (int d = threadIdx.x; d < RADIX; d += kThreads) {
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) sm.wcnt[w][d] = 0;
+    }
+    __syncthreads();
+    const uint32_t tile = stile;
+    const uint32_t tbase = tile * kTile;
+    const uint32_t tn = min((uint32_t)kTile, n - tbase);
+    const uint32_t wbase = tbase + wave * (kRounds * 64);
+    uint64_t key[kRounds];
+    uint32_t pos[kRounds];
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t e = wbase + r * 64 + lane;
+        key[r] = e < n ? in[e] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t e = wbase + r * 64 + lane;
+        const bool valid = e < n;
+        const uint32_t d = (uint32_t)(key[r] >> shift) & (RADIX - 1);
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < D; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        uint32_t before = 0;
+        if (valid) before = sm.wcnt[wave][d];
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t my = (uint32_t)__popcll(peers & lanemask_lt(lane));
+        if (valid && my == 0) sm.wcnt[wave][d] = before + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        pos[r] = before + my;
+    }
+    __syncthreads();
+    uint32_t tot[DPT];
+    uint32_t tsum = 0;
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+        const int d = threadIdx.x * DPT + k;
+        uint32_t sacc = 0;
+        if (d < RADIX) {
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) {
+                const uint32_t c = sm.wcnt[w][d];
+                sm.wcnt[w][d] = sacc;
+                sacc += c;
+            }
+            // publish the aggregate (tile 0: its inclusive prefix right away)
+            atomicAdd(&status[(size_t)tile * RADIX + d], (tile == 0 ? kLbPrefix : kLbAgg) | sacc);
+        }
+        tot[k] = sacc;
+        tsum += sacc;
+    }
+    {
+        uint32_t x = tsum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) ws[wave] = x;
+        __syncthreads();
+        uint32_t pre = x - tsum;
+        for (int w = 0; w < wave; ++w) pre += ws[w];
+#pragma unroll
+        for (int k = 0; k < DPT; ++k) {
+            const int d = threadIdx.x * DPT + k;
+            if (d < RADIX) sm.dstart[d] = pre;
+            pre += tot[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+        const int d = threadIdx.x * DPT + k;
+        if (d >= RADIX) continue;
+        uint32_t excl = 0;
+        if (tile > 0) {
+            int64_t t = (int64_t)tile - 1;
+            uint32_t spins = 0;
+            while (true) {
+                uint32_t v = __hip_atomic_load(&status[(size_t)t * RADIX + d], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                while ((v >> 30) == 0) {
+                    if (++spins > (1u << 24)) {
+                        atomicOr(err, 1u);
+                        v = kLbPrefix;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    v = __hip_atomic_load(&status[(size_t)t * RADIX + d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                excl += v & kLbCount;
+                if ((v & kLbPrefix) || t == 0) break;
+                --t;
+            }
+            // aggregate -> inclusive prefix: add the difference of the two status words
+            atomicAdd(&status[(size_t)tile * RADIX + d], (kLbPrefix | (excl + tot[k])) - (kLbAgg | tot[k]));
+        }
+        sm.gbase[d] = digit_base[d] + excl;
     }
     __syncthreads();
 #pragma unroll
@@ -694,12 +862,38 @@ int radix64_digit_bits(int bits) {
 
 size_t radix64_tiles(size_t n) { return (n + kTile - 1) / kTile; }
 
+int radix64_lookback() {
+    static const int v = [] {
+        const char *e = getenv("SGA_RADIX_MODE");  // A/B knob: 0 single-pass look-back, 1 hist + scan + sweep
+        return e ? (atoi(e) == 0) : 0;
+    }();
+    return v;
+}
+
 template <int D>
 static int sort64_passes(uint64_t *a, uint64_t *alt, uint32_t n, int key_shift, int npass, RadixScratch &sc,
                          hipStream_t s, bool hist0_ready) {
     constexpr int RADIX = 1 << D;
     const uint32_t nt = (uint32_t)radix64_tiles(n);
     uint64_t *src = a, *dst = alt;
+    if (radix64_lookback() && sc.ghist) {
+        // global digit totals of every pass: counted by the producer into sc.ghist when hist0_ready
+        if (!hist0_ready) {
+            SGA_HIP_CHECK(hipMemsetAsync(sc.ghist, 0, kRadixGhistWords * sizeof(uint32_t), s));
+            hipLaunchKernelGGL((k_rs64_upfront<D>), dim3(nt), dim3(kThreads), 0, s, src, n, key_shift, npass,
+                               sc.ghist);
+        }
+        hipLaunchKernelGGL((k_rs_digit_base<D>), dim3(1), dim3(kThreads), 0, s, sc.ghist, npass);
+        for (int p = 0; p < npass; ++p) {
+            SGA_HIP_CHECK(hipMemsetAsync(sc.hist, 0, (size_t)nt * RADIX * sizeof(uint32_t), s));
+            hipLaunchKernelGGL((k_rs64_sweep_lb<D>), dim3(nt), dim3(kThreads), 0, s, src, n, key_shift + p * D,
+                               sc.ghist + p * RADIX, sc.hist, sc.ghist + kMaxPasses * 2048 + p, sc.err, dst);
+            uint64_t *t = src;
+            src = dst;
+            dst = t;
+        }
+        return npass;
+    }
     for (int p = 0; p < npass; ++p) {
         const int shift = key_shift + p * D;
         if (p > 0 || !hist0_ready)

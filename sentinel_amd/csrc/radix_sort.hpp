@@ -16,6 +16,8 @@ struct alignas(16) Payload {
 constexpr int kMaxDigitBits = 11;
 
 struct RadixScratch {
+    uint32_t *ghist = nullptr;      // look-back mode: kRadixMaxPasses x 2048 digit totals + tile counters
+    uint32_t *err = nullptr;        // look-back mode: error flag (a look-back gave up)
     uint32_t *hist = nullptr;       // radix_hist_entries(n, bits)
     uint32_t *hist_scan = nullptr;  // same size
     uint32_t *partial = nullptr;    // scan_partials_needed(hist entries)
@@ -36,6 +38,11 @@ int radix_sort_pairs(uint32_t *keys, Payload *pay, uint32_t *keys_alt, Payload *
 // first pass's per-tile digit histogram (digit-major: hist[d * ntiles + tile]) is already in
 // sc.hist.  Returns the number of passes: the result is in `a` when even, in `alt` when odd.
 constexpr int kRadix64Tile = 4096;
+constexpr int kRadixMaxPasses = 3;
+constexpr size_t kRadixGhistWords = kRadixMaxPasses * 2048 + 64;
+// 1 when the u64 sort runs single-pass look-back sweeps (SGA_RADIX_MODE=0): the producer of the
+// elements then counts every pass's global digit totals into sc.ghist (zeroed first).
+int radix64_lookback();
 int radix64_digit_bits(int bits);
 size_t radix64_tiles(size_t n);
 int radix_sort_u64(uint64_t *a, uint64_t *alt, size_t n, int key_shift, int bits, RadixScratch &sc, hipStream_t s,
