@@ -449,18 +449,18 @@ __global__ __launch_bounds__(kRunThreads) void k_runs_down(const uint64_t *__res
 
 // ---------------------------------------------------------------- exact per-request replay (device)
 // Window state of a rule lives in one contiguous record of 8 x S int64:
-//   [start x S][PASS x S][WAITING x S][per bucket j: BLOCK, PASS_REQUEST, BLOCK_REQUEST,
+//   [per bucket j: start, PASS] [per bucket j: WAITING, BLOCK, PASS_REQUEST, BLOCK_REQUEST,
 //   OCCUPIED_PASS, OCCUPIED_BLOCK]
-// so the window sums read 3 dense vectors and a run's update writes the current bucket's
-// PASS, WAITING and one 40-byte group.
+// so the window sums read one dense vector of 16-byte pairs and a run's update writes one pair
+// and one 48-byte group.
 struct Rec {
     int64_t *r;
     int S;
-    __device__ __forceinline__ int64_t &start(int j) const { return r[j]; }
+    __device__ __forceinline__ int64_t &start(int j) const { return r[2 * j]; }
     __device__ __forceinline__ int64_t &cnt(int ev, int j) const {
-        if (ev == CEV_PASS) return r[S + j];
-        if (ev == CEV_WAITING) return r[2 * S + j];
-        return r[3 * S + 5 * j + (ev - 1)];  // BLOCK..OCCUPIED_BLOCK = ordinals 1..5
+        if (ev == CEV_PASS) return r[2 * j + 1];
+        if (ev == CEV_WAITING) return r[2 * S + 6 * j];
+        return r[2 * S + 6 * j + ev];  // BLOCK..OCCUPIED_BLOCK = ordinals 1..5
     }
 };
 
@@ -639,30 +639,12 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
     if (ri.cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) return false;
     int64_t bp = 0, hstart = kAbsent, hpass = 0;
     uint32_t vmask = 0;  // valid buckets other than the current one
-    if ((P.S & 1) == 0) {
+    {
+        // (start, PASS) pairs: one 16-byte load per bucket
         const int4 *v = reinterpret_cast<const int4 *>(R.r);
-        const int hs = P.S >> 1;
-        for (int q = 0; q < hs; ++q) {
-            const int4 st2 = v[q], ps2 = v[hs + q];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int jj = 2 * q + h;
-                const int64_t w = h ? i64_hi(st2) : i64_lo(st2);
-                const int64_t pv = h ? i64_hi(ps2) : i64_lo(ps2);
-                if (jj == jh) {
-                    hstart = w;
-                    hpass = pv;
-                }
-                if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
-                    bp += pv;
-                    vmask |= 1u << (jj & 31);
-                }
-            }
-        }
-    } else {
         for (int jj = 0; jj < P.S; ++jj) {
-            const int64_t w = R.start(jj);
-            const int64_t pv = R.cnt(CEV_PASS, jj);
+            const int4 sp = v[jj];
+            const int64_t w = i64_lo(sp), pv = i64_hi(sp);
             if (jj == jh) {
                 hstart = w;
                 hpass = pv;
