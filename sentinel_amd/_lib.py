@@ -73,6 +73,14 @@ class SgaNodeView(C.Structure):
                 ("cur_thread_num", C.c_int64), ("waiting", C.c_int64)]
 
 
+class SgaWireBatch(C.Structure):  # include/sga_wire.h
+    _fields_ = [("cap", C.c_size_t), ("vcap", C.c_size_t), ("n", C.c_size_t), ("nv", C.c_size_t),
+                ("xid", C.c_void_p), ("type", C.c_void_p), ("kind", C.c_void_p), ("flow_id", C.c_void_p),
+                ("count", C.c_void_p), ("prio", C.c_void_p), ("voff", C.c_void_p), ("values", C.c_void_p),
+                ("ns_off", C.c_void_p), ("ns_len", C.c_void_p), ("ns_bytes", C.c_void_p),
+                ("ns_cap", C.c_size_t), ("ns_used", C.c_size_t)]
+
+
 # (restype, argtypes) for every exported symbol; tests check this list against include/*.h
 SIGNATURES = {
     "sga_abi_version": (C.c_int, []),
@@ -106,6 +114,9 @@ SIGNATURES = {
     "sga_circuit_breaker_state": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
     "sga_metrics_snapshot": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "sga_cluster_metric_nodes": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "sga_wire_decode": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(SgaWireBatch)]),
+    "sga_wire_encode": (C.c_int, [C.c_void_p] * 7 + [C.c_size_t, C.c_void_p, C.c_size_t]),
+    "sga_wire_string_key": (C.c_int64, [C.c_char_p, C.c_size_t]),
     "sga_cluster_metric_nodes_device": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.c_void_p,
                                                   C.c_void_p]),
 }

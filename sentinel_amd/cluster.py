@@ -141,16 +141,22 @@ class ClusterFlowRuleManager:
 
 
 def param_value_key(v) -> int:
-    """64-bit stand-in the engine uses for a Java parameter Object: ints as themselves, str by
-    String.hashCode, bool as Boolean.hashCode (1231 / 1237).  Collisions between distinct Objects
-    with equal keys would merge their counters; callers with such domains pass their own keys."""
+    """64-bit stand-in the engine uses for a Java parameter Object, the same mapping as the wire
+    decoder (include/sga_wire.h): integers as themselves, bool as Boolean.hashCode (1231 / 1237),
+    float by its IEEE-754 double bits, str by FNV-1a 64 of its UTF-8 bytes.  Distinct Objects with
+    equal keys would share a counter; callers with such domains pass their own keys."""
     if isinstance(v, bool):
         return 1231 if v else 1237
-    if isinstance(v, int):
-        return v
+    if isinstance(v, (int, np.integer)):
+        return int(v)
+    if isinstance(v, float):
+        import struct
+        return struct.unpack("<q", struct.pack("<d", v))[0]
     if isinstance(v, str):
-        from .javautil import string_hash_code
-        return string_hash_code(v)
+        h = 0xcbf29ce484222325
+        for b in v.encode():
+            h = ((h ^ b) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+        return h - (1 << 64) if h >= (1 << 63) else h
     raise TypeError(f"unsupported parameter type {type(v).__name__}")
 
 
