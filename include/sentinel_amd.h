@@ -195,11 +195,14 @@ int sga_cluster_stats(sga_engine *e, uint64_t *n_active_rules, uint64_t *state_b
  * requests.  Each request has desc_count descriptors; descriptor d has flowId
  * d_flow_id (= Integer.MAX_VALUE + key.hashCode(), EnvoySentinelRuleConverter.java:67-72)
  * and hitsAddend.  Every descriptor consumes (no short-circuit).  code[r]:
- * 1 = OK, 2 = OVER_LIMIT (envoy RateLimitResponse.Code); per-descriptor status
- * in desc_status (TokenResultStatus). */
+ * 1 = OK, 2 = OVER_LIMIT (envoy RateLimitResponse.Code), -1 = hitsAddend < 0 (onError).
+ * Optional per-descriptor outputs: desc_status = the TokenResult status of
+ * SimpleClusterFlowChecker.acquireClusterToken (NO_RULE_EXISTS for an absent rule -- the
+ * descriptor's Code is then OK and it carries no current_limit, :65-83) and desc_remaining =
+ * TokenResult.remaining (DescriptorStatus.limit_remaining). */
 int sga_rls_should_rate_limit(sga_engine *e, const uint32_t *desc_offsets, size_t n_requests,
                               const int64_t *desc_flow_id, const int32_t *hits_addend, const int64_t *ts,
-                              int8_t *desc_status, int32_t *code);
+                              int8_t *desc_status, int32_t *desc_remaining, int32_t *code);
 
 /* ---------------------------------------------------------------------------
  * Local path: resources are dense ids 0..n_resources-1 (the host keeps the

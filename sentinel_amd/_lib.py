@@ -103,7 +103,7 @@ SIGNATURES = {
                                            C.c_size_t, C.c_void_p]),
     "sga_cluster_param_sum": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.POINTER(C.c_int64)]),
     "sga_rls_should_rate_limit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p,
-                                            C.c_void_p, C.c_void_p]),
+                                            C.c_void_p, C.c_void_p, C.c_void_p]),
     "sga_flow_set_resources": (C.c_int, [C.c_void_p, C.c_uint32]),
     "sga_load_flow_rules": (C.c_int, [C.c_void_p, C.POINTER(SgaFlowRule), C.c_size_t]),
     "sga_load_param_rules": (C.c_int, [C.c_void_p, C.POINTER(SgaParamRule), C.c_size_t]),

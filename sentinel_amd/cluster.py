@@ -316,19 +316,26 @@ class EnvoyRlsService:
 
     @staticmethod
     def generate_flow_id(key: str) -> int:
-        # EnvoySentinelRuleConverter.generateFlowId: (long) Integer.MAX_VALUE + key.hashCode()
-        from .javautil import string_hash_code
-        return 2147483647 + string_hash_code(key)
+        # EnvoySentinelRuleConverter.generateFlowId: -1 for a blank key, else
+        # (long) Integer.MAX_VALUE + key.hashCode()
+        from .javautil import is_blank, string_hash_code
+        return -1 if is_blank(key) else 2147483647 + string_hash_code(key)
 
-    def should_rate_limit(self, desc_offsets, desc_flow_id, hits_addend, ts):
+    def should_rate_limit(self, desc_offsets, desc_flow_id, hits_addend, ts, with_remaining: bool = False):
+        """Returns (code per request, TokenResult status per descriptor[, remaining per descriptor])."""
         off = np.ascontiguousarray(desc_offsets, dtype=np.uint32)
         fid = np.ascontiguousarray(desc_flow_id, dtype=np.int64)
         hits = np.ascontiguousarray(hits_addend, dtype=np.int32)
         t = np.ascontiguousarray(ts, dtype=np.int64)
         nreq = len(hits)
-        st = np.zeros(len(fid), dtype=np.int8)
-        code = np.zeros(nreq, dtype=np.int32)
+        if len(off) != nreq + 1 or len(t) != nreq or (nreq and int(off[-1]) != len(fid)):
+            raise ValueError("desc_offsets must have n_requests + 1 entries ending at len(desc_flow_id)")
+        st = np.zeros(max(len(fid), 1), dtype=np.int8)
+        rem = np.zeros(max(len(fid), 1), dtype=np.int32)
+        code = np.zeros(max(nreq, 1), dtype=np.int32)
         rc = _lib.load().sga_rls_should_rate_limit(self.engine.handle, off.ctypes.data, nreq, fid.ctypes.data,
-                                                   hits.ctypes.data, t.ctypes.data, st.ctypes.data, code.ctypes.data)
+                                                   hits.ctypes.data, t.ctypes.data, st.ctypes.data, rem.ctypes.data,
+                                                   code.ctypes.data)
         check(rc, self.engine.handle, "shouldRateLimit")
-        return code, st
+        n = len(fid)
+        return (code[:nreq], st[:n], rem[:n]) if with_remaining else (code[:nreq], st[:n])

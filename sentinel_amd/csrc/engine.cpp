@@ -885,7 +885,7 @@ int sga_cluster_stats(sga_engine *e, uint64_t *n_active, uint64_t *state_bytes) 
 // SentinelEnvoyRlsServiceImpl.shouldRateLimit, RLS/SentinelEnvoyRlsServiceImpl.java:51-101
 int sga_rls_should_rate_limit(sga_engine *e, const uint32_t *desc_offsets, size_t n_requests,
                               const int64_t *desc_flow_id, const int32_t *hits_addend, const int64_t *ts,
-                              int8_t *desc_status, int32_t *code) {
+                              int8_t *desc_status, int32_t *desc_remaining, int32_t *code) {
     if (n_requests && (!desc_offsets || !hits_addend || !ts || !code)) return SGA_EINVAL;
     return guarded(e, [&](Engine &g) {
         const size_t nd = desc_offsets[n_requests];
@@ -909,11 +909,12 @@ int sga_rls_should_rate_limit(sga_engine *e, const uint32_t *desc_offsets, size_
         int rc = fid.empty() ? SGA_OK
                              : run_host_batch(g, fid.data(), acq.data(), nullptr, t.data(), fid.size(), res.data(), 1);
         if (rc != SGA_OK) return rc;
-        std::vector<int8_t> st(nd, 0);
+        // a request with hitsAddend < 0 checks nothing: its descriptors report NO_RULE_EXISTS, 0
+        std::vector<int8_t> st(nd, SGA_TOKEN_NO_RULE_EXISTS);
+        std::vector<int32_t> rem(nd, 0);
         for (size_t k = 0; k < res.size(); ++k) {
-            int8_t s = (int8_t)(res[k] >> 48);
-            if (s == SGA_TOKEN_NO_RULE_EXISTS) s = SGA_TOKEN_OK;  // absent rule passes
-            st[where[k]] = s;
+            st[where[k]] = (int8_t)(res[k] >> 48);
+            rem[where[k]] = (int32_t)(uint32_t)res[k];
         }
         for (size_t r = 0; r < n_requests; ++r) {
             if (hits_addend[r] < 0) {
@@ -921,11 +922,13 @@ int sga_rls_should_rate_limit(sga_engine *e, const uint32_t *desc_offsets, size_
                 continue;
             }
             bool blocked = false;
-            for (uint32_t d = desc_offsets[r]; d < desc_offsets[r + 1]; ++d) blocked |= st[d] != SGA_TOKEN_OK;
+            // an absent rule passes (NO_RULE_EXISTS -> OK, :65-68)
+            for (uint32_t d = desc_offsets[r]; d < desc_offsets[r + 1]; ++d)
+                blocked |= st[d] != SGA_TOKEN_OK && st[d] != SGA_TOKEN_NO_RULE_EXISTS;
             code[r] = blocked ? 2 : 1;  // Code.OVER_LIMIT : Code.OK
         }
-        if (desc_status)
-            for (size_t d = 0; d < nd; ++d) desc_status[d] = st[d];
+        if (desc_status) std::copy(st.begin(), st.end(), desc_status);
+        if (desc_remaining) std::copy(rem.begin(), rem.end(), desc_remaining);
         return SGA_OK;
     });
 }

@@ -11,6 +11,14 @@ def string_hash_code(s: str) -> int:
     return h - (1 << 32) if h >= (1 << 31) else h
 
 
+def is_blank(s) -> bool:
+    """StringUtil.isBlank: null, empty or only Character.isWhitespace chars (sentinel-core util/StringUtil.java:43-54)."""
+    if not s:
+        return True
+    return all(c in " \t\n\x0b\f\r\x1c\x1d\x1e\x1f" or (c.isspace() and c not in "\x85\xa0\u2007\u202f")
+               for c in s)
+
+
 def rls_key(domain: str, entries) -> str:
     """SentinelEnvoyRlsServiceImpl.generateKey: domain|k|v|k|v (RLS/SentinelEnvoyRlsServiceImpl.java:127-133)."""
     parts = [domain]

@@ -269,19 +269,19 @@ def test_rls_descriptors(eng_mod):
     hits = rng.integers(0, 3, size=nreq).astype(np.int32)
     hits[5] = -1
     ts = T0 + np.arange(nreq) * 7
-    code, st = svc.should_rate_limit(off, dfid, hits, ts)
+    code, st, rem = svc.should_rate_limit(off, dfid, hits, ts, with_remaining=True)
     L = H.lib()
     for r in range(nreq):
         if hits[r] < 0:
             assert code[r] == -1
+            assert all(st[d] == 3 and rem[d] == 0 for d in range(off[r], off[r + 1]))
             continue
         a = 1 if hits[r] == 0 else int(hits[r])
         blocked = False
         for d in range(off[r], off[r + 1]):
             res = L.orc_cluster_request_token_simple(oh, int(dfid[d]), a, int(ts[r]))
-            s = 0 if res.status == 3 else res.status
-            assert st[d] == s, (r, d, st[d], s)
-            blocked |= s != 0
+            assert (st[d], rem[d]) == (res.status, res.remaining), (r, d, st[d], rem[d], res.status, res.remaining)
+            blocked |= res.status not in (0, 3)  # NO_RULE_EXISTS passes
         assert code[r] == (2 if blocked else 1)
     L.orc_cluster_free(oh)
     eng.close()
