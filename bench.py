@@ -254,9 +254,8 @@ def run_cpu_baseline(args, n_gpus):
     fid_m, cnt_m = fid_all[mine], cnt_all[mine]
 
     def new_oracle(sel):
-        rules = np.zeros(int(sel.sum()), dtype=[("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"),
-                                                ("sample_count", "<i4"), ("window_interval_ms", "<i4"),
-                                                ("grade", "<i4"), ("strategy", "<i4"), ("reserved", "<i4")])
+        from sentinel_amd.cluster import CLUSTER_RULE_DTYPE
+        rules = np.zeros(int(sel.sum()), dtype=CLUSTER_RULE_DTYPE)
         rules["flow_id"] = fid_m[sel]
         rules["count"] = cnt_m[sel]
         rules["threshold_type"] = 1

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define SGA_ABI_VERSION 1
+#define SGA_ABI_VERSION 2
 
 /* error codes (negated errno values) */
 #define SGA_OK 0
@@ -68,6 +68,8 @@ extern "C" {
 #define SGA_TOKEN_BLOCKED 1
 #define SGA_TOKEN_SHOULD_WAIT 2
 #define SGA_TOKEN_NO_RULE_EXISTS 3
+#define SGA_TOKEN_RELEASE_OK 6
+#define SGA_TOKEN_ALREADY_RELEASE 7
 
 /* ClusterFlowEvent ordinals, CS/flow/statistic/data/ClusterFlowEvent.java:22-52 */
 #define SGA_CEV_PASS 0
@@ -93,17 +95,20 @@ typedef struct sga_config {
 } sga_config;
 
 /* Cluster flow rule = FlowRule{count, grade, strategy, clusterMode=true} +
- * ClusterFlowConfig{flowId, thresholdType, sampleCount, windowIntervalMs}
- * (CORE/slots/block/flow/FlowRule.java:52-95, CORE/slots/block/flow/ClusterFlowConfig.java:34-74). */
+ * ClusterFlowConfig{flowId, thresholdType, sampleCount, windowIntervalMs, resourceTimeout,
+ * clientOfflineTime} (CORE/slots/block/flow/FlowRule.java:52-95,
+ * CORE/slots/block/flow/ClusterFlowConfig.java:34-105). */
 typedef struct sga_cluster_flow_rule {
     int64_t flow_id;
     double count;
     int32_t threshold_type;     /* ClusterRuleConstant: AVG_LOCAL = 0, GLOBAL = 1 */
     int32_t sample_count;       /* default 10 (ClusterRuleConstant.DEFAULT_CLUSTER_SAMPLE_COUNT) */
     int32_t window_interval_ms; /* default 1000 */
-    int32_t grade;              /* RuleConstant.FLOW_GRADE_QPS = 1 */
+    int32_t grade;              /* RuleConstant.FLOW_GRADE_QPS = 1 (THREAD = 0: concurrency tokens) */
     int32_t strategy;           /* ClusterFlowConfig.strategy, NORMAL = 0 */
     int32_t reserved;
+    int64_t resource_timeout_ms;     /* ClusterFlowConfig.resourceTimeout (default 2000) */
+    int64_t client_offline_time_ms;  /* ClusterFlowConfig.clientOfflineTime (default 2000) */
 } sga_cluster_flow_rule;
 
 /* TokenResult as the engine writes it: 8 bytes per decision.
@@ -190,6 +195,55 @@ int sga_cluster_param_sum(sga_engine *e, int64_t flow_id, int64_t value, int64_t
 
 /* Number of flow slots and device bytes of window state (for roofline tools). */
 int sga_cluster_stats(sga_engine *e, uint64_t *n_active_rules, uint64_t *state_bytes);
+
+/* ---------------------------------------------------------------------------
+ * Cluster concurrency tokens: TokenService.requestConcurrentToken / releaseConcurrentToken
+ * (CORE/cluster/TokenService.java:58-73) -> DefaultTokenService.java:67-86 ->
+ * ConcurrentClusterFlowChecker.java:37-104, TokenCacheNodeManager, CurrentConcurrencyManager,
+ * RegularExpireStrategy.java:78-134 (CS = sentinel-cluster-server-default/.../cluster).
+ * Client addresses are dense ids of a host table (SGA_CLIENT_NONE = null or "").
+ * ------------------------------------------------------------------------- */
+#define SGA_CONCURRENT_ACQUIRE 0
+#define SGA_CONCURRENT_RELEASE 1
+#define SGA_CLIENT_NONE 0xFFFFFFFFu
+
+typedef struct sga_concurrent_result {
+    int64_t token_id;  /* TokenResult.tokenId (acquire OK; 0 otherwise) */
+    int32_t status;    /* TokenResultStatus: OK, BLOCKED, NO_RULE_EXISTS, BAD_REQUEST, RELEASE_OK,
+                          ALREADY_RELEASE */
+    int32_t reserved;
+} sga_concurrent_result;
+
+/* TokenCacheNode (TokenCacheNode.java:25-60); the timeouts are absolute, as the setters store them. */
+typedef struct sga_token_cache_node {
+    int64_t token_id;
+    int64_t flow_id;
+    int64_t client_timeout;    /* clientOfflineTime + creation time */
+    int64_t resource_timeout;  /* resourceTimeout + creation time */
+    int32_t acquire_count;
+    uint32_t client;
+} sga_token_cache_node;
+
+/* A batch of acquire / release operations decided in arrival order.  op[i] = SGA_CONCURRENT_*;
+ * acquire: id = flowId (ruleId), client[i], acquire[i], ts[i] = TimeUtil/System time of the call;
+ * release: id = tokenId (client / acquire ignored).  Token ids are 64-bit values unique per engine
+ * (the reference draws UUID.randomUUID().getMostSignificantBits()). */
+int sga_concurrent_ops(sga_engine *e, const uint8_t *op, const uint32_t *client, const int64_t *id,
+                       const int32_t *acquire, const int64_t *ts, size_t n, sga_concurrent_result *out);
+
+/* One RegularExpireStrategy pass at `now` over every cached token.  online_bits: bit c set when
+ * client c is connected (ConnectionManager.isClientOnline).  *n_removed = tokens removed. */
+int sga_concurrent_expire(sga_engine *e, int64_t now, const uint32_t *online_bits, uint32_t n_clients,
+                          uint64_t *n_removed);
+
+/* CurrentConcurrencyManager.get(flowId): returns 1 and *now_calls when present, 0 when absent. */
+int sga_concurrent_now_calls(sga_engine *e, int64_t flow_id, int32_t *now_calls);
+
+/* TokenCacheNodeManager.getSize() */
+int sga_concurrent_token_count(sga_engine *e, uint64_t *n);
+
+/* TokenCacheNodeManager.getTokenCacheNode(tokenId): 1 and *out when cached, 0 when absent. */
+int sga_concurrent_get_token(sga_engine *e, int64_t token_id, sga_token_cache_node *out);
 
 /* Envoy RLS: SentinelEnvoyRlsServiceImpl.shouldRateLimit over a batch of
  * requests.  Each request has desc_count descriptors; descriptor d has flowId

@@ -752,6 +752,8 @@ typedef struct crule {
     int ns;               /* namespace index */
     int active;           /* in FLOW_RULES */
     orc_cmetric *metric;  /* ClusterMetricStatistics entry (may outlive the rule) */
+    int conc_live;        /* CurrentConcurrencyManager NOW_CALLS_MAP holds flow_id */
+    int32_t now_calls;    /* its AtomicInteger */
 } crule;
 
 #define ORC_MAX_NS 64
@@ -760,6 +762,7 @@ struct orc_cluster {
     crule *tab;
     size_t cap, used;
     struct orc_cparam *param;  /* ClusterParamFlowRuleManager state (oracle_cparam.c) */
+    struct orc_conc *conc;     /* TokenCacheNodeManager state (oracle_conc.c) */
     char *ns_name[ORC_MAX_NS];
     int32_t ns_connected[ORC_MAX_NS];
     orc_limiter *ns_limiter[ORC_MAX_NS];
@@ -807,9 +810,11 @@ orc_cluster *orc_cluster_new(double exceed_count, double max_occupy_ratio) {
 }
 
 void orc_cparam_free_all(orc_cluster *c);
+void orc_conc_free_all(orc_cluster *c);
 void orc_cluster_free(orc_cluster *c) {
     if (!c) return;
     orc_cparam_free_all(c);
+    orc_conc_free_all(c);
     for (size_t i = 0; i < c->cap; i++) orc_cmetric_free(c->tab[i].metric);
     free(c->tab);
     for (int i = 0; i < c->nns; i++) {
@@ -836,7 +841,10 @@ int orc_cluster_load_rules(orc_cluster *c, const char *ns, const orc_cluster_rul
     if (nsi < 0) return -1;
     if (n == 0) { /* clearAndResetRulesFor (:281-296): rules dropped, metrics kept */
         for (size_t i = 0; i < c->cap; i++)
-            if (c->tab[i].flow_id != 0 && c->tab[i].ns == nsi) c->tab[i].active = 0;
+            if (c->tab[i].flow_id != 0 && c->tab[i].ns == nsi) {
+                c->tab[i].active = 0;
+                c->tab[i].conc_live = 0; /* CurrentConcurrencyManager.remove(flowId) */
+            }
         return 0;
     }
     /* mark every flowId of this namespace as "old" */
@@ -855,6 +863,10 @@ int orc_cluster_load_rules(orc_cluster *c, const char *ns, const orc_cluster_rul
         e->r = *r;
         e->ns = nsi;
         e->active = 1;
+        if (!e->conc_live) { /* CurrentConcurrencyManager.put(flowId, 0) when absent (:356-358) */
+            e->conc_live = 1;
+            e->now_calls = 0;
+        }
         if (!e->metric) e->metric = orc_cmetric_new(r->sample_count, r->window_interval_ms); /* putMetricIfAbsent */
         applied++;
     }
@@ -862,6 +874,7 @@ int orc_cluster_load_rules(orc_cluster *c, const char *ns, const orc_cluster_rul
     for (size_t i = 0; i < c->cap; i++) {
         if (c->tab[i].flow_id != 0 && c->tab[i].ns == nsi && c->tab[i].active == 2) {
             c->tab[i].active = 0;
+            c->tab[i].conc_live = 0;
             orc_cmetric_free(c->tab[i].metric);
             c->tab[i].metric = NULL;
         }
@@ -870,6 +883,16 @@ int orc_cluster_load_rules(orc_cluster *c, const char *ns, const orc_cluster_rul
 }
 
 struct orc_cparam **orc_cluster_param_slot(orc_cluster *c) { return &c->param; }
+struct orc_conc **orc_cluster_conc_slot(orc_cluster *c) { return &c->conc; }
+/* ClusterFlowRuleManager.getFlowRuleById + CurrentConcurrencyManager.get: the active rule (NULL when
+ * absent), its namespace and its nowCalls counter (*now_calls = NULL when absent). */
+const orc_cluster_rule *orc_cluster_active_rule(orc_cluster *c, int64_t flow_id, int *ns, int32_t **now_calls) {
+    crule *e = flow_id > 0 ? ctab_find(c, flow_id, 0) : NULL;
+    if (now_calls) *now_calls = (e && e->conc_live) ? &e->now_calls : NULL;
+    if (!e || !e->active) return NULL;
+    if (ns) *ns = e->ns;
+    return &e->r;
+}
 int32_t orc_cluster_connected(orc_cluster *c, int ns) { return ns >= 0 ? c->ns_connected[ns] : 0; }
 /* GlobalRequestLimiter.tryPass(namespace): no limiter for the namespace -> pass */
 int orc_cluster_limiter_try_pass(orc_cluster *c, int ns, int64_t now) {

@@ -166,6 +166,9 @@ typedef struct orc_cluster_rule {
     int32_t window_interval_ms;
     int32_t grade;          /* must be QPS for token requests */
     int32_t strategy;       /* ClusterFlowConfig.strategy (NORMAL=0) */
+    int32_t reserved;
+    int64_t resource_timeout_ms;    /* ClusterFlowConfig.resourceTimeout (2000) */
+    int64_t client_offline_time_ms; /* ClusterFlowConfig.clientOfflineTime (2000) */
 } orc_cluster_rule;
 
 typedef struct orc_token_result {
@@ -245,6 +248,22 @@ int64_t orc_pmetric_sum(orc_pmetric *m, int64_t now, int64_t value);
 double orc_pmetric_avg(orc_pmetric *m, int64_t now, int64_t value);
 /* ClusterParamMetric.getSum(value) at now; -1 when the flow has no metric */
 int64_t orc_cluster_param_sum(orc_cluster *c, int64_t flow_id, int64_t value, int64_t now);
+
+/* ---- cluster concurrency tokens (oracle_conc.c) ----------------------------- */
+#define ORC_CLIENT_NONE 0xFFFFFFFFu
+typedef struct orc_conc_result {
+    int32_t status;   /* TokenResultStatus */
+    int32_t reserved;
+    int64_t token_id; /* TokenResult.tokenId when OK */
+} orc_conc_result;
+orc_conc_result orc_cluster_concurrent_acquire(orc_cluster *c, uint32_t client, int64_t flow_id, int32_t acquire,
+                                               int64_t now, int64_t token_id);
+int32_t orc_cluster_concurrent_release(orc_cluster *c, int64_t token_id);
+uint64_t orc_cluster_concurrent_expire(orc_cluster *c, int64_t now, const uint32_t *online_bits, uint32_t nclients);
+int orc_cluster_concurrent_now_calls(orc_cluster *c, int64_t flow_id, int32_t *out);
+size_t orc_cluster_concurrent_tokens(orc_cluster *c);
+int orc_cluster_concurrent_get(orc_cluster *c, int64_t token_id, int64_t *flow_id, int64_t *client_deadline,
+                               int64_t *resource_deadline, int32_t *acquire);
 
 /* ---- Java numerics exposed for tests ---------------------------------------- */
 int64_t orc_java_round(double d);

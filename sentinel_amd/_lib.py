@@ -19,7 +19,17 @@ class SgaConfig(C.Structure):
 class SgaClusterFlowRule(C.Structure):
     _fields_ = [("flow_id", C.c_int64), ("count", C.c_double), ("threshold_type", C.c_int32),
                 ("sample_count", C.c_int32), ("window_interval_ms", C.c_int32), ("grade", C.c_int32),
-                ("strategy", C.c_int32), ("reserved", C.c_int32)]
+                ("strategy", C.c_int32), ("reserved", C.c_int32), ("resource_timeout_ms", C.c_int64),
+                ("client_offline_time_ms", C.c_int64)]
+
+
+class SgaConcurrentResult(C.Structure):
+    _fields_ = [("token_id", C.c_int64), ("status", C.c_int32), ("reserved", C.c_int32)]
+
+
+class SgaTokenCacheNode(C.Structure):
+    _fields_ = [("token_id", C.c_int64), ("flow_id", C.c_int64), ("client_timeout", C.c_int64),
+                ("resource_timeout", C.c_int64), ("acquire_count", C.c_int32), ("client", C.c_uint32)]
 
 
 class SgaClusterParamRule(C.Structure):
@@ -104,6 +114,12 @@ SIGNATURES = {
     "sga_cluster_param_sum": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.POINTER(C.c_int64)]),
     "sga_rls_should_rate_limit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p, C.c_void_p, C.c_void_p]),
+    "sga_concurrent_ops": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_size_t, C.c_void_p]),
+    "sga_concurrent_expire": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]),
+    "sga_concurrent_now_calls": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(C.c_int32)]),
+    "sga_concurrent_token_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "sga_concurrent_get_token": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(SgaTokenCacheNode)]),
     "sga_flow_set_resources": (C.c_int, [C.c_void_p, C.c_uint32]),
     "sga_load_flow_rules": (C.c_int, [C.c_void_p, C.POINTER(SgaFlowRule), C.c_size_t]),
     "sga_load_param_rules": (C.c_int, [C.c_void_p, C.POINTER(SgaParamRule), C.c_size_t]),

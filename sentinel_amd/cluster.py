@@ -39,6 +39,10 @@ class TokenResultStatus:
     ALREADY_RELEASE = 7
 
 
+CONCURRENT_ACQUIRE, CONCURRENT_RELEASE = 0, 1
+CLIENT_NONE = 0xFFFFFFFF
+
+
 class ClusterFlowEvent:
     PASS, BLOCK, PASS_REQUEST, BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK, WAITING = range(7)
 
@@ -48,6 +52,7 @@ class TokenResult:
     status: int
     remaining: int = 0
     wait_in_ms: int = 0
+    token_id: int = 0
 
 
 class Engine:
@@ -70,6 +75,16 @@ class Engine:
             raise _lib.EngineError(f"sga_create failed rc={rc}")
         self._h = h
         self.max_batch = max_batch
+        self.clients: dict = {}  # client address -> dense id (concurrency tokens)
+
+    def client_id(self, address: Optional[str]) -> int:
+        """Dense id of a client address; null or "" -> SGA_CLIENT_NONE (a BAD_REQUEST)."""
+        if not address:
+            return CLIENT_NONE
+        c = self.clients.get(address)
+        if c is None:
+            c = self.clients[address] = len(self.clients)
+        return c
 
     @property
     def handle(self):
@@ -93,6 +108,13 @@ class Engine:
         self.close()
 
 
+# sga_cluster_flow_rule as a numpy record (bulk loads; the oracle's orc_cluster_rule has the same layout)
+CLUSTER_RULE_DTYPE = np.dtype([("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"), ("sample_count", "<i4"),
+                               ("window_interval_ms", "<i4"), ("grade", "<i4"), ("strategy", "<i4"),
+                               ("reserved", "<i4"), ("resource_timeout_ms", "<i8"),
+                               ("client_offline_time_ms", "<i8")])
+
+
 def _rules_array(rules: List[FlowRule]):
     arr = (SgaClusterFlowRule * max(1, len(rules)))()
     for i, r in enumerate(rules):
@@ -104,6 +126,8 @@ def _rules_array(rules: List[FlowRule]):
         arr[i].window_interval_ms = cc.window_interval_ms
         arr[i].grade = r.grade
         arr[i].strategy = cc.strategy
+        arr[i].resource_timeout_ms = cc.resource_timeout
+        arr[i].client_offline_time_ms = cc.client_offline_time
     return arr
 
 
@@ -123,15 +147,15 @@ class ClusterFlowRuleManager:
                          window_interval_ms=1000) -> int:
         """Bulk form for large rule sets (numpy arrays)."""
         n = len(flow_id)
-        dt = np.dtype([("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"), ("sample_count", "<i4"),
-                       ("window_interval_ms", "<i4"), ("grade", "<i4"), ("strategy", "<i4"), ("reserved", "<i4")])
-        a = np.zeros(n, dtype=dt)
+        a = np.zeros(n, dtype=CLUSTER_RULE_DTYPE)
         a["flow_id"] = flow_id
         a["count"] = count
         a["threshold_type"] = threshold_type
         a["sample_count"] = sample_count
         a["window_interval_ms"] = window_interval_ms
         a["grade"] = 1
+        a["resource_timeout_ms"] = 2000
+        a["client_offline_time_ms"] = 2000
         ptr = a.ctypes.data_as(C.POINTER(SgaClusterFlowRule))
         rc = _lib.load().sga_load_cluster_flow_rules(self.engine.handle, namespace.encode(), ptr, n)
         return check(rc, self.engine.handle, "loadRules")
@@ -250,6 +274,7 @@ class GlobalRequestLimiter:
 
 
 TOKEN_DTYPE = np.dtype([("remaining", "<i4"), ("wait_in_ms", "<i2"), ("status", "i1"), ("reserved", "i1")])
+CONC_RESULT_DTYPE = np.dtype([("token_id", "<i8"), ("status", "<i4"), ("reserved", "<i4")])  # sga_concurrent_result
 
 
 class DefaultTokenService:
@@ -298,6 +323,64 @@ class DefaultTokenService:
     def request_param_token(self, rule_id: int, acquire_count: int, params, now: int) -> TokenResult:
         r = self.request_param_tokens([rule_id], [acquire_count], [params], [now])[0]
         return TokenResult(int(r["status"]), int(r["remaining"]), int(r["wait_in_ms"]))
+
+    # ---- concurrency tokens (DefaultTokenService.java:67-86 -> ConcurrentClusterFlowChecker)
+    def concurrent_ops(self, op, client, ids, acquire, ts) -> np.ndarray:
+        """Acquire (op 0: ids = flowIds) / release (op 1: ids = tokenIds) operations decided in
+        order; returns CONC_RESULT_DTYPE records (token_id, status)."""
+        o = np.ascontiguousarray(op, dtype=np.uint8)
+        cl = np.ascontiguousarray(client, dtype=np.uint32)
+        x = np.ascontiguousarray(ids, dtype=np.int64)
+        a = np.ascontiguousarray(acquire, dtype=np.int32)
+        t = np.ascontiguousarray(ts, dtype=np.int64)
+        n = len(o)
+        if not (len(cl) == len(x) == len(a) == len(t) == n):
+            raise ValueError("operation arrays differ in length")
+        out = np.zeros(max(n, 1), dtype=CONC_RESULT_DTYPE)
+        rc = _lib.load().sga_concurrent_ops(self.engine.handle, o.ctypes.data, cl.ctypes.data, x.ctypes.data,
+                                            a.ctypes.data, t.ctypes.data, n, out.ctypes.data)
+        check(rc, self.engine.handle, "concurrentOps")
+        return out[:n]
+
+    def request_concurrent_token(self, client_address: Optional[str], rule_id: int, acquire_count: int,
+                                 now: int) -> TokenResult:
+        r = self.concurrent_ops([CONCURRENT_ACQUIRE], [self.engine.client_id(client_address)], [rule_id],
+                                [acquire_count], [now])[0]
+        return TokenResult(int(r["status"]), token_id=int(r["token_id"]))
+
+    def release_concurrent_token(self, token_id: int, now: int = 0) -> int:
+        """ConcurrentClusterFlowChecker.releaseConcurrentToken status (the SPI method returns void)."""
+        return int(self.concurrent_ops([CONCURRENT_RELEASE], [CLIENT_NONE], [token_id], [0], [now])[0]["status"])
+
+    def expire_concurrent_tokens(self, now: int, online_addresses=()) -> int:
+        """One RegularExpireStrategy pass; online_addresses = ConnectionManager's connected clients."""
+        n = len(self.engine.clients)
+        bits = np.zeros(max((n + 31) // 32, 1), dtype=np.uint32)
+        for a in online_addresses:
+            c = self.engine.clients.get(a)
+            if c is not None:
+                bits[c >> 5] |= np.uint32(1 << (c & 31))
+        removed = C.c_uint64()
+        check(_lib.load().sga_concurrent_expire(self.engine.handle, now, bits.ctypes.data, n, C.byref(removed)),
+              self.engine.handle, "expire")
+        return removed.value
+
+    def concurrent_now_calls(self, flow_id: int) -> Optional[int]:
+        """CurrentConcurrencyManager.get(flowId).get(), None when absent."""
+        v = C.c_int32()
+        rc = check(_lib.load().sga_concurrent_now_calls(self.engine.handle, flow_id, C.byref(v)), self.engine.handle)
+        return v.value if rc == 1 else None
+
+    def concurrent_token_count(self) -> int:
+        n = C.c_uint64()
+        check(_lib.load().sga_concurrent_token_count(self.engine.handle, C.byref(n)), self.engine.handle)
+        return n.value
+
+    def get_token_cache_node(self, token_id: int):
+        node = _lib.SgaTokenCacheNode()
+        rc = check(_lib.load().sga_concurrent_get_token(self.engine.handle, token_id, C.byref(node)),
+                   self.engine.handle)
+        return node if rc == 1 else None
 
     def metric_sums(self, flow_id: int, now: int) -> List[int]:
         out = (C.c_int64 * 7)()

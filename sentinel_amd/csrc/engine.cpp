@@ -2,11 +2,13 @@
 // mirror), device state ownership and the extern "C" ABI of include/sentinel_amd.h.
 #include "../../include/sentinel_amd.h"
 #include "cluster.hpp"
+#include "concurrent.hpp"
 #include "flow.hpp"
 
 #include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <random>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -22,6 +24,8 @@ struct SlotHost {
     int threshold_type = 0;
     int S = 0, interval = 0;  // metric geometry, fixed at metric creation (putMetricIfAbsent)
     uint32_t boff = 0, bcap = 0;
+    int64_t resource_timeout = 2000, client_offline = 2000;  // ClusterFlowConfig defaults
+    bool conc_live = false;  // CurrentConcurrencyManager holds flow_id
 };
 
 // Cluster parameter rule slot (ClusterParamFlowRuleManager PARAM_RULES + ClusterParamMetricStatistics).
@@ -105,6 +109,83 @@ struct Engine {
     CParamScratch pscratch{};
     DevBuf<uint32_t> d_in_voff;
     DevBuf<int64_t> d_in_vals;
+
+    // ---- cluster concurrency tokens
+    DevBuf<ConcParam> d_cparam;   // per slot
+    DevBuf<int32_t> d_now_calls;  // per slot
+    DevBuf<TokenEntry> d_tok;
+    DevBuf<uint32_t> d_tctr;      // [0] live [1] tombstones [2] expired by the last pass
+    uint32_t tmask = 0, tepoch = 1;
+    uint64_t tlive = 0, ttomb = 0;
+    uint64_t token_base = 0;
+    DevBuf<uint8_t> d_cscratch;
+    ConcScratch cscratch;
+    DevBuf<uint8_t> d_cin_op;
+    DevBuf<uint32_t> d_cin_client, d_online, d_creset;
+    DevBuf<int64_t> d_cin_id, d_cin_ts;
+    DevBuf<int32_t> d_cin_acq;
+    DevBuf<sga_concurrent_result> d_cout;
+    DevBuf<TokenEntry> d_tfind;
+
+    ConcState cstate() const {
+        ConcState c{};
+        c.cs = state();
+        c.cparam = d_cparam.p;
+        c.now_calls = d_now_calls.p;
+        c.tok = d_tok.p;
+        c.tmask = tmask;
+        c.epoch = tepoch;
+        c.ctr = d_tctr.p;
+        return c;
+    }
+
+    // token table + operation scratch, created with the first concurrency call
+    void ensure_conc() {
+        if (d_cscratch.p) return;
+        const size_t cap = cfg.max_batch;
+        d_cscratch.alloc(conc_scratch_bytes(cap));
+        conc_scratch_carve(cscratch, d_cscratch.p, cap);
+        d_cin_op.alloc(cap);
+        d_cin_client.alloc(cap);
+        d_cin_id.alloc(cap);
+        d_cin_ts.alloc(cap);
+        d_cin_acq.alloc(cap);
+        d_cout.alloc(cap);
+        d_tctr.alloc(4);
+        d_tfind.alloc(1);
+        SGA_HIP_CHECK(hipMemsetAsync(d_tctr.p, 0, d_tctr.bytes(), stream));
+        d_tok.alloc(1024);
+        SGA_HIP_CHECK(hipMemsetAsync(d_tok.p, 0, d_tok.bytes(), stream));
+        tmask = 1023;
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+
+    // keeps live + tombstones + `incoming` at most half the table (rehash drops the tombstones)
+    bool reserve_tokens(uint64_t incoming) {
+        const uint64_t cap = (uint64_t)tmask + 1;
+        if (2 * (tlive + ttomb + incoming) <= cap) return true;
+        uint64_t ncap = 1024;
+        while (ncap < 4 * (tlive + incoming)) ncap <<= 1;
+        if (ncap > (1ull << 31)) return false;
+        DevBuf<TokenEntry> nt;
+        nt.alloc(ncap);
+        conc_rehash(d_tok.p, (uint32_t)cap, nt.p, (uint32_t)(ncap - 1), stream);
+        const uint32_t z = 0;
+        SGA_HIP_CHECK(hipMemcpyAsync(d_tctr.p + 1, &z, 4, hipMemcpyHostToDevice, stream));
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+        std::swap(d_tok.p, nt.p);
+        std::swap(d_tok.n, nt.n);
+        tmask = (uint32_t)(ncap - 1);
+        ttomb = 0;
+        return true;
+    }
+
+    void read_token_counters() {
+        uint32_t c[3];
+        SGA_HIP_CHECK(hipMemcpy(c, d_tctr.p, 12, hipMemcpyDeviceToHost));
+        tlive = c[0];
+        ttomb = c[1];
+    }
 
     CParamState pstate() {
         CParamState st{};
@@ -324,6 +405,23 @@ struct Engine {
             p.ns = h.ns;
         }
         if (ns) SGA_HIP_CHECK(hipMemcpyAsync(d_param.p, hp.data(), ns * sizeof(SlotParam), hipMemcpyHostToDevice, stream));
+        {  // concurrency: ConcurrentClusterFlowChecker.calcGlobalThreshold (no exceedCount), timeouts
+            if (d_cparam.n < slot_cap) {
+                const size_t c = std::max<size_t>(slot_cap, d_cparam.n * 2);
+                d_cparam.grow(c, stream);
+                d_now_calls.grow(c, stream);
+            }
+            std::vector<ConcParam> cp(ns);
+            for (size_t i = 0; i < ns; ++i) {
+                const SlotHost &h = slots[i];
+                const int conn = h.ns >= 0 ? nss[h.ns].connected : 0;
+                cp[i].thr = h.threshold_type == 1 ? h.count : h.count * (double)conn;
+                cp[i].resource_timeout = h.resource_timeout;
+                cp[i].client_offline = h.client_offline;
+            }
+            if (ns) SGA_HIP_CHECK(hipMemcpyAsync(d_cparam.p, cp.data(), ns * sizeof(ConcParam), hipMemcpyHostToDevice,
+                                                 stream));
+        }
         {
             std::vector<int64_t> fids(std::max<size_t>(ns, 1), 0);
             for (size_t i = 0; i < ns; ++i) fids[i] = slots[i].flow_id;
@@ -470,6 +568,8 @@ int sga_create(const sga_config *cfg, sga_engine **out) {
         g.d_tmp7.alloc(8);
         g.flow.init(c, g.stream);
         g.ensure_scratch();
+        std::random_device rd;  // token ids: a random start, then splitmix64 of a counter (bijective)
+        g.token_base = ((uint64_t)rd() << 32) ^ (uint64_t)rd();
         return SGA_OK;
     });
     if (rc != SGA_OK) {
@@ -507,12 +607,16 @@ int sga_load_cluster_flow_rules(sga_engine *e, const char *ns, const sga_cluster
         std::vector<uint32_t> fresh;
         if (n == 0) {  // clearAndResetRulesFor: rules dropped, metrics kept (:281-296)
             for (auto &h : g.slots)
-                if (h.allocated && h.ns == nsi) h.active = false;
+                if (h.allocated && h.ns == nsi) {
+                    h.active = false;
+                    h.conc_live = false;  // CurrentConcurrencyManager.remove(flowId)
+                }
             g.sync_device(fresh);
             return 0;
         }
         std::unordered_map<int64_t, const sga_cluster_flow_rule *> rule_map;
         std::vector<int64_t> order;
+        std::vector<uint32_t> reset;
         for (size_t i = 0; i < n; ++i) {
             const sga_cluster_flow_rule &r = rules[i];
             // FlowRuleUtil.isValidRule + checkClusterField (FlowRuleUtil.java:176-231)
@@ -539,6 +643,7 @@ int sga_load_cluster_flow_rules(sga_engine *e, const char *ns, const sga_cluster
             if (rule_map.count(h.flow_id)) continue;
             h.active = false;
             h.allocated = false;
+            h.conc_live = false;
             g.slot_of.erase(h.flow_id);
             g.free_slots.push_back(s);
         }
@@ -569,8 +674,20 @@ int sga_load_cluster_flow_rules(sga_engine *e, const char *ns, const sga_cluster
             h.ns = nsi;
             h.count = r.count;
             h.threshold_type = r.threshold_type;
+            h.resource_timeout = r.resource_timeout_ms;
+            h.client_offline = r.client_offline_time_ms;
+            if (!h.conc_live) {  // CurrentConcurrencyManager.put(flowId, 0) when absent (:356-358)
+                h.conc_live = true;
+                reset.push_back(s);
+            }
         }
         g.sync_device(fresh);
+        if (!reset.empty()) {
+            if (g.d_creset.n < reset.size()) g.d_creset.alloc(reset.size());
+            SGA_HIP_CHECK(hipMemcpyAsync(g.d_creset.p, reset.data(), reset.size() * 4, hipMemcpyHostToDevice, g.stream));
+            sga::conc_reset_calls(g.d_now_calls.p, g.d_creset.p, (uint32_t)reset.size(), g.stream);
+            SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        }
         return (int)order.size();
     });
 }
@@ -879,6 +996,122 @@ int sga_cluster_stats(sga_engine *e, uint64_t *n_active, uint64_t *state_bytes) 
             *state_bytes = (uint64_t)g.bucket_used * 64 + g.slots.size() * (sizeof(sga::SlotParam) +
                                                                                       sizeof(sga::SlotOcc));
         return SGA_OK;
+    });
+}
+
+// ---------------------------------------------------------------- concurrency tokens
+// DefaultTokenService.requestConcurrentToken / releaseConcurrentToken (CS/flow/DefaultTokenService.java:67-86)
+int sga_concurrent_ops(sga_engine *e, const uint8_t *op, const uint32_t *client, const int64_t *id,
+                       const int32_t *acquire, const int64_t *ts, size_t n, sga_concurrent_result *out) {
+    if (n && (!op || !client || !id || !acquire || !ts || !out)) return SGA_EINVAL;
+    static_assert(sizeof(sga_concurrent_result) == 16, "concurrent result is 16 bytes");
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        g.ensure_conc();
+        g.ensure_scratch();
+        const size_t cap = g.cfg.max_batch;
+        for (size_t b = 0; b < n;) {
+            const size_t m = std::min(cap, n - b);
+            size_t nacq = 0;
+            for (size_t i = 0; i < m; ++i) {
+                if (op[b + i] > 1) return SGA_EINVAL;
+                nacq += op[b + i] == 0;
+            }
+            if (!g.reserve_tokens(nacq)) {
+                g.err = "token cache above 2^29 tokens";
+                return SGA_ENOMEM;
+            }
+            SGA_HIP_CHECK(hipMemcpyAsync(g.d_cin_op.p, op + b, m, hipMemcpyHostToDevice, g.stream));
+            SGA_HIP_CHECK(hipMemcpyAsync(g.d_cin_client.p, client + b, m * 4, hipMemcpyHostToDevice, g.stream));
+            SGA_HIP_CHECK(hipMemcpyAsync(g.d_cin_id.p, id + b, m * 8, hipMemcpyHostToDevice, g.stream));
+            SGA_HIP_CHECK(hipMemcpyAsync(g.d_cin_acq.p, acquire + b, m * 4, hipMemcpyHostToDevice, g.stream));
+            SGA_HIP_CHECK(hipMemcpyAsync(g.d_cin_ts.p, ts + b, m * 8, hipMemcpyHostToDevice, g.stream));
+            ++g.tepoch;
+            sga::conc_ops(g.cstate(), g.cscratch, g.d_cin_op.p, g.d_cin_client.p, g.d_cin_id.p, g.d_cin_acq.p,
+                          g.d_cin_ts.p, (uint32_t)m, g.token_base, g.d_cout.p, g.stream);
+            SGA_HIP_CHECK(hipGetLastError());
+            g.token_base += m;
+            SGA_HIP_CHECK(hipMemcpyAsync(out + b, g.d_cout.p, m * sizeof(sga_concurrent_result), hipMemcpyDeviceToHost,
+                                         g.stream));
+            SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+            g.read_token_counters();
+            if (sga::radix64_lookback()) {
+                uint32_t err = 0;
+                SGA_HIP_CHECK(hipMemcpy(&err, g.cscratch.radix.err, 4, hipMemcpyDeviceToHost));
+                if (err) {
+                    g.err = "radix look-back timed out";
+                    return SGA_EIO;
+                }
+            }
+            b += m;
+        }
+        return SGA_OK;
+    });
+}
+
+// RegularExpireStrategy.clearToken, CS/flow/statistic/concurrent/expire/RegularExpireStrategy.java:78-134
+int sga_concurrent_expire(sga_engine *e, int64_t now, const uint32_t *online_bits, uint32_t n_clients,
+                          uint64_t *n_removed) {
+    if (n_clients && !online_bits) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        g.ensure_conc();
+        const size_t words = std::max<size_t>(((size_t)n_clients + 31) / 32, 1);
+        if (g.d_online.n < words) g.d_online.alloc(std::max<size_t>(words, 2 * g.d_online.n));
+        if (n_clients)
+            SGA_HIP_CHECK(hipMemcpyAsync(g.d_online.p, online_bits, ((size_t)n_clients + 31) / 32 * 4,
+                                         hipMemcpyHostToDevice, g.stream));
+        ++g.tepoch;
+        sga::conc_expire(g.cstate(), now, g.d_online.p, n_clients, g.stream);
+        SGA_HIP_CHECK(hipGetLastError());
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        uint32_t c[3];
+        SGA_HIP_CHECK(hipMemcpy(c, g.d_tctr.p, 12, hipMemcpyDeviceToHost));
+        g.tlive = c[0];
+        g.ttomb = c[1];
+        if (n_removed) *n_removed = c[2];
+        return SGA_OK;
+    });
+}
+
+int sga_concurrent_now_calls(sga_engine *e, int64_t flow_id, int32_t *now_calls) {
+    if (!now_calls) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        auto it = g.slot_of.find(flow_id);
+        if (it == g.slot_of.end() || !g.slots[it->second].conc_live) return 0;
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        SGA_HIP_CHECK(hipMemcpy(now_calls, g.d_now_calls.p + it->second, 4, hipMemcpyDeviceToHost));
+        return 1;
+    });
+}
+
+int sga_concurrent_token_count(sga_engine *e, uint64_t *n) {
+    if (!n) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        *n = g.tlive;
+        return SGA_OK;
+    });
+}
+
+int sga_concurrent_get_token(sga_engine *e, int64_t token_id, sga_token_cache_node *out) {
+    if (!out) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        g.ensure_conc();
+        sga::conc_find(g.cstate(), token_id, g.d_tfind.p, g.stream);
+        SGA_HIP_CHECK(hipGetLastError());
+        sga::TokenEntry t;
+        SGA_HIP_CHECK(hipMemcpyAsync(&t, g.d_tfind.p, sizeof(t), hipMemcpyDeviceToHost, g.stream));
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        if (t.state != sga::kTokLive) return 0;
+        out->token_id = t.token;
+        out->flow_id = t.flow_id;
+        out->client_timeout = t.client_deadline;
+        out->resource_timeout = t.resource_deadline;
+        out->acquire_count = t.acquire;
+        out->client = t.client;
+        return 1;
     });
 }
 

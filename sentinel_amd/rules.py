@@ -42,6 +42,8 @@ class ClusterFlowConfig:
     sample_count: int = ClusterRuleConstant.DEFAULT_CLUSTER_SAMPLE_COUNT
     window_interval_ms: int = 1000
     strategy: int = ClusterRuleConstant.FLOW_CLUSTER_STRATEGY_NORMAL
+    resource_timeout: int = 2000     # ClusterFlowConfig.resourceTimeout (concurrency tokens)
+    client_offline_time: int = 2000  # ClusterFlowConfig.clientOfflineTime
 
 
 @dataclass

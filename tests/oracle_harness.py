@@ -32,7 +32,12 @@ class OrcFlowRule(C.Structure):
 class OrcClusterRule(C.Structure):
     _fields_ = [("flow_id", C.c_int64), ("count", C.c_double), ("threshold_type", C.c_int32),
                 ("sample_count", C.c_int32), ("window_interval_ms", C.c_int32), ("grade", C.c_int32),
-                ("strategy", C.c_int32)]
+                ("strategy", C.c_int32), ("reserved", C.c_int32), ("resource_timeout_ms", C.c_int64),
+                ("client_offline_time_ms", C.c_int64)]
+
+
+class OrcConcResult(C.Structure):
+    _fields_ = [("status", C.c_int32), ("reserved", C.c_int32), ("token_id", C.c_int64)]
 
 
 class OrcParamRule(C.Structure):
@@ -119,6 +124,13 @@ def lib():
         "orc_cluster_request_param_token": (OrcTokenResult, [P, I64, I32, P, C.c_size_t, I64]),
         "orc_cluster_param_replay": (None, [P, C.c_size_t, P, P, P, P, P, P]),
         "orc_cluster_param_sum": (I64, [P, I64, I64, I64]),
+        "orc_cluster_concurrent_acquire": (OrcConcResult, [P, U32, I64, I32, I64, I64]),
+        "orc_cluster_concurrent_release": (I32, [P, I64]),
+        "orc_cluster_concurrent_expire": (C.c_uint64, [P, I64, P, U32]),
+        "orc_cluster_concurrent_now_calls": (C.c_int, [P, I64, C.POINTER(I32)]),
+        "orc_cluster_concurrent_tokens": (C.c_size_t, [P]),
+        "orc_cluster_concurrent_get": (C.c_int, [P, I64, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64),
+                                                 C.POINTER(I32)]),
         "orc_limiter_new": (P, [D]),
         "orc_limiter_free": (None, [P]),
         "orc_limiter_add": (None, [P, I64, C.c_int]),
@@ -172,6 +184,8 @@ def cluster_rules_array(rules):
         arr[i].window_interval_ms = r.get("window_interval_ms", 1000)
         arr[i].grade = r.get("grade", 1)
         arr[i].strategy = r.get("strategy", 0)
+        arr[i].resource_timeout_ms = r.get("resource_timeout", 2000)
+        arr[i].client_offline_time_ms = r.get("client_offline_time", 2000)
     return arr
 
 

@@ -46,19 +46,20 @@ def test_python_mirror_binds_every_symbol():
     L = _lib.load()
     decl = {s for s in declared_symbols() if not s.startswith("sgaw_")}
     assert decl <= set(_lib.SIGNATURES), decl - set(_lib.SIGNATURES)
-    assert L.sga_abi_version() == 1
+    assert L.sga_abi_version() == 2
 
 
 def test_struct_layouts_match_header():
     from sentinel_amd import _lib
     assert ctypes.sizeof(_lib.SgaTokenResult) == 8
-    assert ctypes.sizeof(_lib.SgaClusterFlowRule) == 40
+    assert ctypes.sizeof(_lib.SgaClusterFlowRule) == 56
     assert ctypes.sizeof(_lib.SgaConfig) == 40
 
 
 _STRUCTS = {"SgaConfig": "sga_config", "SgaClusterFlowRule": "sga_cluster_flow_rule",
             "SgaTokenResult": "sga_token_result", "SgaFlowRule": "sga_flow_rule", "SgaParamRule": "sga_param_rule",
-            "SgaDegradeRule": "sga_degrade_rule", "SgaNodeView": "sga_node_view"}
+            "SgaDegradeRule": "sga_degrade_rule", "SgaNodeView": "sga_node_view",
+            "SgaConcurrentResult": "sga_concurrent_result", "SgaTokenCacheNode": "sga_token_cache_node"}
 
 
 def test_every_field_offset_matches_the_c_compiler(tmp_path):

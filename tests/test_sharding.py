@@ -24,9 +24,8 @@ LAM = 2_000_000
 
 
 def _rules_struct(fid, cnt):
-    rules = np.zeros(len(fid), dtype=[("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"),
-                                     ("sample_count", "<i4"), ("window_interval_ms", "<i4"), ("grade", "<i4"),
-                                     ("strategy", "<i4"), ("reserved", "<i4")])
+    from sentinel_amd.cluster import CLUSTER_RULE_DTYPE
+    rules = np.zeros(len(fid), dtype=CLUSTER_RULE_DTYPE)
     rules["flow_id"] = fid
     rules["count"] = cnt
     rules["threshold_type"] = 1
