@@ -193,6 +193,13 @@ int sga_request_param_tokens(sga_engine *e, const int64_t *flow_id, const int32_
 /* ClusterParamMetric.getSum(value) of a flow at `now` (rotation side effect included). */
 int sga_cluster_param_sum(sga_engine *e, int64_t flow_id, int64_t value, int64_t now, int64_t *out);
 
+/* ClusterParamMetric.getTopValues(number) of a param flow at `now` (rotation side effect included):
+ * up to `number` (1..1024) values with the largest sums over the valid buckets, as value keys and
+ * qps = sum / intervalInSecond, largest first (equal sums: smaller value key first; the reference's
+ * order among equal sums is its HashMap's).  *n_out = 0 when the flow has no metric. */
+int sga_cluster_param_top_values(sga_engine *e, int64_t flow_id, int64_t now, uint32_t number, int64_t *values,
+                                 double *qps, uint32_t *n_out);
+
 /* Number of flow slots and device bytes of window state (for roofline tools). */
 int sga_cluster_stats(sga_engine *e, uint64_t *n_active_rules, uint64_t *state_bytes);
 

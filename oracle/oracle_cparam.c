@@ -337,6 +337,49 @@ int64_t orc_cluster_param_sum(orc_cluster *c, int64_t flow_id, int64_t value, in
     return pm_sum(e->metric, value, now);
 }
 
+/* ClusterParamMetric.getTopValues(number), ClusterParamMetric.java:90-133: currentWindow(), merge
+ * every valid bucket's map, largest sums first.  Equal sums: smaller value key first (the
+ * reference sorts its HashMap's entries stably, so its order among equal sums is the HashMap's
+ * iteration order of the Java objects -- not restated: parity unpinned for ties).  Returns the
+ * number of values written (0 when the flow has no metric). */
+static int top_before(int64_t c1, int64_t v1, int64_t c2, int64_t v2) { return c1 > c2 || (c1 == c2 && v1 < v2); }
+
+size_t orc_cluster_param_top_values(orc_cluster *c, int64_t flow_id, int64_t now, size_t number, int64_t *vals,
+                                    double *qps) {
+    prule *e = ptab_find(param_of(c), flow_id, 0);
+    if (!e || !e->metric || number == 0) return 0;
+    pmetric *m = e->metric;
+    pm_current_window(m, now);
+    vmap acc = {0};
+    for (int j = 0; j < m->S; j++) {
+        if (m->start[j] == P_ABSENT || now - m->start[j] > m->interval) continue; /* values(): valid buckets */
+        const vmap *b = &m->map[j];
+        for (size_t i = 0; i < b->cap; i++)
+            if (b->used[i]) *vmap_slot(&acc, b->key[i], 1) += b->val[i];
+    }
+    size_t got = 0;
+    int64_t lc = INT64_MAX, lv = INT64_MIN;
+    while (got < number) {
+        int64_t bc = -1, bv = 0;
+        for (size_t i = 0; i < acc.cap; i++) {
+            if (!acc.used[i]) continue;
+            const int64_t cc = acc.val[i], v = acc.key[i];
+            if (top_before(lc, lv, cc, v) && top_before(cc, v, bc, bv)) {
+                bc = cc;
+                bv = v;
+            }
+        }
+        if (bc <= 0) break; /* x.getValue() == 0: stop */
+        vals[got] = bv;
+        qps[got] = (double)bc / m->interval_sec;
+        lc = bc;
+        lv = bv;
+        got++;
+    }
+    vmap_free(&acc);
+    return got;
+}
+
 /* standalone ClusterParamMetric for the transcribed ClusterParamMetricTest (values are the caller's
  * 64-bit stand-ins for the Java Objects) */
 typedef struct orc_pmetric orc_pmetric;

@@ -249,6 +249,10 @@ double orc_pmetric_avg(orc_pmetric *m, int64_t now, int64_t value);
 /* ClusterParamMetric.getSum(value) at now; -1 when the flow has no metric */
 int64_t orc_cluster_param_sum(orc_cluster *c, int64_t flow_id, int64_t value, int64_t now);
 
+/* ClusterParamMetric.getTopValues(number) at now; returns the values written */
+size_t orc_cluster_param_top_values(orc_cluster *c, int64_t flow_id, int64_t now, size_t number, int64_t *vals,
+                                    double *qps);
+
 /* ---- cluster concurrency tokens (oracle_conc.c) ----------------------------- */
 #define ORC_CLIENT_NONE 0xFFFFFFFFu
 typedef struct orc_conc_result {

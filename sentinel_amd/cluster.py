@@ -241,6 +241,18 @@ class ClusterParamFlowRuleManager:
                                                 C.byref(out)), self.engine.handle, "getSum")
         return out.value
 
+    def top_values(self, flow_id: int, now: int, number: int = 5) -> List[tuple]:
+        """ClusterParamMetric.getTopValues(number): [(value key, qps)], largest first -- the
+        topParams of ClusterMetricNodeGenerator.paramToMetricNode (ClusterMetricNodeGenerator.java:93-105)."""
+        if number <= 0:
+            raise ValueError("number must be positive")
+        vals = (C.c_int64 * number)()
+        qps = (C.c_double * number)()
+        n = C.c_uint32()
+        check(_lib.load().sga_cluster_param_top_values(self.engine.handle, flow_id, now, number, vals, qps,
+                                                       C.byref(n)), self.engine.handle, "getTopValues")
+        return [(vals[i], qps[i]) for i in range(n.value)]
+
 
 class GlobalRequestLimiter:
     """CS/flow/statistic/limit/GlobalRequestLimiter.java:30-80 mirror (per-namespace QPS guard that

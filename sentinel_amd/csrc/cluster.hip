@@ -1394,6 +1394,74 @@ __global__ void k_psum(CParamState st, uint32_t slot, int64_t value, int64_t now
     *out = kidx == 0xFFFFFFFFu ? 0 : pm_key_sum(st, P, st.krec + st.koff[kidx], now);
 }
 
+// ClusterParamMetric.getTopValues(number), CS/flow/statistic/metric/ClusterParamMetric.java:90-133:
+// currentWindow(), per value the sum over the valid buckets, the `number` largest (ties: smaller
+// value key first -- the reference's order among equal counts is its HashMap's iteration order).
+__global__ void k_pwindow(CParamState st, uint32_t slot, int64_t now) {
+    if (threadIdx.x || blockIdx.x) return;
+    pm_window(st, st.param[slot], now);
+}
+
+// every key of the rule with a positive sum -> (count, value) appended to `list`
+__global__ __launch_bounds__(kThreads) void k_ptop_collect(CParamState st, uint32_t slot, int64_t now,
+                                                           int64_t *list, uint32_t *count) {
+    const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
+    if (k > st.kmask || st.ktab[k] == 0 || st.kslot[k] != slot) return;
+    const PRuleParam P = st.param[slot];
+    const int64_t s = pm_key_sum(st, P, st.krec + st.koff[k], now);
+    if (s <= 0) return;
+    const uint32_t at = atomicAdd(count, 1u);
+    list[2 * at] = s;
+    list[2 * at + 1] = st.kval[k];
+}
+
+__device__ __forceinline__ bool top_before(int64_t c1, int64_t v1, int64_t c2, int64_t v2) {
+    return c1 > c2 || (c1 == c2 && v1 < v2);
+}
+
+// `number` rounds of a block-wide arg-max over the collected list, each strictly after the last pick
+__global__ __launch_bounds__(1024) void k_ptop_select(CParamState st, uint32_t slot, const int64_t *list,
+                                                      const uint32_t *count, uint32_t number, int64_t *out_val,
+                                                      double *out_qps, uint32_t *n_out) {
+    __shared__ int64_t sc[1024], sv[1024];
+    const uint32_t m = *count;
+    const double isec = st.param[slot].isec;
+    int64_t lc = INT64_MAX, lv = INT64_MIN;
+    uint32_t got = 0;
+    for (uint32_t r = 0; r < number; ++r) {
+        int64_t bc = -1, bv = 0;
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+            const int64_t c = list[2 * i], v = list[2 * i + 1];
+            if (top_before(lc, lv, c, v) && top_before(c, v, bc, bv)) {
+                bc = c;
+                bv = v;
+            }
+        }
+        sc[threadIdx.x] = bc;
+        sv[threadIdx.x] = bv;
+        __syncthreads();
+        for (uint32_t o = blockDim.x / 2; o > 0; o >>= 1) {
+            if (threadIdx.x < o && top_before(sc[threadIdx.x + o], sv[threadIdx.x + o], sc[threadIdx.x], sv[threadIdx.x])) {
+                sc[threadIdx.x] = sc[threadIdx.x + o];
+                sv[threadIdx.x] = sv[threadIdx.x + o];
+            }
+            __syncthreads();
+        }
+        bc = sc[0];
+        bv = sv[0];
+        __syncthreads();
+        if (bc <= 0) break;  // fewer values than `number`
+        if (threadIdx.x == 0) {
+            out_val[r] = bv;
+            out_qps[r] = (double)bc / isec;
+        }
+        lc = bc;
+        lv = bv;
+        ++got;
+    }
+    if (threadIdx.x == 0) *n_out = got;
+}
+
 __global__ void k_pinit_rule(CParamState st, uint32_t slot) {
     const PRuleParam P = st.param[slot];
     for (int j = threadIdx.x; j < P.S; j += blockDim.x) st.rstart[P.boff + j] = kAbsent;
@@ -1604,6 +1672,17 @@ void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
 
 void cparam_sum(const CParamState &st, uint32_t slot, int64_t value, int64_t now, int64_t *d_out, hipStream_t s) {
     hipLaunchKernelGGL(k_psum, dim3(1), dim3(64), 0, s, st, slot, value, now, d_out);
+}
+
+void cparam_top_values(const CParamState &st, uint32_t slot, int64_t now, uint32_t number, int64_t *d_list,
+                       uint32_t *d_count, int64_t *d_val, double *d_qps, uint32_t *d_n, hipStream_t s) {
+    hipLaunchKernelGGL(k_pwindow, dim3(1), dim3(64), 0, s, st, slot, now);
+    SGA_HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint32_t), s));
+    const uint32_t nk = st.kmask + 1;
+    hipLaunchKernelGGL(k_ptop_collect, dim3((nk + kThreads - 1) / kThreads), dim3(kThreads), 0, s, st, slot, now,
+                       d_list, d_count);
+    hipLaunchKernelGGL(k_ptop_select, dim3(1), dim3(1024), 0, s, st, slot, d_list, d_count, number, d_val, d_qps,
+                       d_n);
 }
 
 void cparam_init_rule(const CParamState &st, uint32_t slot, hipStream_t s) {

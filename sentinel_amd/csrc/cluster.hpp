@@ -179,6 +179,9 @@ void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
 // ClusterParamMetric.getSum(value) at now (rotation side effect included); *d_out = -1 if no key
 void cparam_sum(const CParamState &st, uint32_t slot, int64_t value, int64_t now, int64_t *d_out, hipStream_t s);
 void cparam_init_rule(const CParamState &st, uint32_t slot, hipStream_t s);
+// ClusterParamMetric.getTopValues(number) of one rule at now: d_list holds 2 x (kmask + 1) int64.
+void cparam_top_values(const CParamState &st, uint32_t slot, int64_t now, uint32_t number, int64_t *d_list,
+                       uint32_t *d_count, int64_t *d_val, double *d_qps, uint32_t *d_n, hipStream_t s);
 
 // ClusterMetricNodeGenerator.flowToMetricNode for every active slot (out: sga_cluster_metric_node,
 // count: device u32; slot_fid: flowId per slot).

@@ -109,6 +109,9 @@ struct Engine {
     CParamScratch pscratch{};
     DevBuf<uint32_t> d_in_voff;
     DevBuf<int64_t> d_in_vals;
+    DevBuf<int64_t> d_top_list, d_top_val;
+    DevBuf<double> d_top_qps;
+    DevBuf<uint32_t> d_top_n;
 
     // ---- cluster concurrency tokens
     DevBuf<ConcParam> d_cparam;   // per slot
@@ -983,6 +986,37 @@ int sga_cluster_param_sum(sga_engine *e, int64_t flow_id, int64_t value, int64_t
         sga::cparam_sum(g.pstate(), it->second, value, now, g.d_tmp7.p, g.stream);
         SGA_HIP_CHECK(hipMemcpyAsync(out, g.d_tmp7.p, 8, hipMemcpyDeviceToHost, g.stream));
         SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        return SGA_OK;
+    });
+}
+
+// ClusterParamMetric.getTopValues, CS/flow/statistic/metric/ClusterParamMetric.java:90-133
+int sga_cluster_param_top_values(sga_engine *e, int64_t flow_id, int64_t now, uint32_t number, int64_t *values,
+                                 double *qps, uint32_t *n_out) {
+    if (!values || !qps || !n_out || number == 0 || number > 1024 || now < 0) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        *n_out = 0;
+        auto it = g.pslot_of.find(flow_id);
+        if (it == g.pslot_of.end() || !g.d_pctl.p) return SGA_OK;  // no metric: empty map
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        const size_t nk = (size_t)g.kmask + 1;
+        if (g.d_top_list.n < 2 * nk) g.d_top_list.alloc(2 * nk);
+        if (g.d_top_val.n < number) {
+            g.d_top_val.alloc(number);
+            g.d_top_qps.alloc(number);
+        }
+        if (!g.d_top_n.p) g.d_top_n.alloc(2);
+        sga::cparam_top_values(g.pstate(), it->second, now, number, g.d_top_list.p, g.d_top_n.p + 1, g.d_top_val.p,
+                               g.d_top_qps.p, g.d_top_n.p, g.stream);
+        SGA_HIP_CHECK(hipGetLastError());
+        uint32_t n = 0;
+        SGA_HIP_CHECK(hipMemcpyAsync(&n, g.d_top_n.p, 4, hipMemcpyDeviceToHost, g.stream));
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        if (n) {
+            SGA_HIP_CHECK(hipMemcpy(values, g.d_top_val.p, n * 8, hipMemcpyDeviceToHost));
+            SGA_HIP_CHECK(hipMemcpy(qps, g.d_top_qps.p, n * 8, hipMemcpyDeviceToHost));
+        }
+        *n_out = n;
         return SGA_OK;
     });
 }

@@ -124,6 +124,7 @@ def lib():
         "orc_cluster_request_param_token": (OrcTokenResult, [P, I64, I32, P, C.c_size_t, I64]),
         "orc_cluster_param_replay": (None, [P, C.c_size_t, P, P, P, P, P, P]),
         "orc_cluster_param_sum": (I64, [P, I64, I64, I64]),
+        "orc_cluster_param_top_values": (C.c_size_t, [P, I64, I64, C.c_size_t, P, P]),
         "orc_cluster_concurrent_acquire": (OrcConcResult, [P, U32, I64, I32, I64, I64]),
         "orc_cluster_concurrent_release": (I32, [P, I64]),
         "orc_cluster_concurrent_expire": (C.c_uint64, [P, I64, P, U32]),

@@ -88,6 +88,15 @@ class Pair:
             o = self.L.orc_cluster_param_sum(self.oh, f, self.cm.param_value_key(v), now)
             assert g == o, (f, v, g, o)
 
+    def check_top(self, flows, now, number=5):
+        """ClusterParamMetric.getTopValues (the topParams of paramToMetricNode)."""
+        for f in flows:
+            got = self.mgr.top_values(f, now, number)
+            vals = (C.c_int64 * number)()
+            qps = (C.c_double * number)()
+            k = self.L.orc_cluster_param_top_values(self.oh, f, now, number, vals, qps)
+            assert got == [(vals[i], qps[i]) for i in range(k)], (f, now, got)
+
     def close(self):
         self.L.orc_cluster_free(self.oh)
         self.eng.close()
@@ -135,6 +144,9 @@ def test_random_single_value_traces(cm, seed):
         sl = slice(lo, lo + 10_000)
         p.run(fid[sl], acq[sl], params[sl], ts[sl], f"seed={seed} batch@{lo}")
     p.check_sums([(int(f), int(v)) for f in range(1, 41) for v in (0, 1, 2, 5, 33)], int(ts[-1]))
+    p.check_top(range(1, 46), int(ts[-1]))
+    p.check_top(range(1, 41, 7), int(ts[-1]) + 450, number=12)
+    p.check_top([3, 4], int(ts[-1]) + 5000)  # every bucket deprecated: empty
     p.close()
 
 
@@ -159,6 +171,7 @@ def test_multi_value_and_regression(cm):
         sl = slice(lo, lo + 2000)
         p.run(fid[sl], acq[sl], params[sl], ts[sl], f"batch@{lo}")
     p.check_sums([(f, v) for f in range(1, 9) for v in range(12)], int(ts.max()))
+    p.check_top(range(1, 10), int(ts.max()), number=20)
     p.close()
 
 

@@ -81,3 +81,21 @@ def test_replay_matches_single_calls():
         assert req(L, h2, int(fid[i]), 1, [int(vals[i])], int(ts[i])) == (ref[i, 0], ref[i, 1])
     L.orc_cluster_free(h1)
     L.orc_cluster_free(h2)
+
+
+def test_top_values():
+    """ClusterParamMetric.getTopValues(number): merged valid buckets, largest first, qps = sum /
+    intervalInSecond, zero-count values never listed; equal sums -> smaller value key first."""
+    L, h, _ = make([{"flow_id": 11, "count": 100, "threshold_type": 1, "sample_count": 2,
+                     "window_interval_ms": 1000}])
+    for v, k, t in ((1001, 5, 0), (7, 2, 0), (7, 1, 600), (2, 3, 600), (9, 1, 700)):
+        for i in range(k):
+            assert req(L, h, 11, 1, [v], T0 + t + i)[0] == 0
+    vals, qps = (C.c_int64 * 8)(), (C.c_double * 8)()
+    n = L.orc_cluster_param_top_values(h, 11, T0 + 800, 3, vals, qps)
+    assert [(vals[i], qps[i]) for i in range(n)] == [(1001, 5.0), (2, 3.0), (7, 3.0)]
+    n = L.orc_cluster_param_top_values(h, 11, T0 + 1200, 8, vals, qps)  # first bucket deprecated
+    assert [(vals[i], qps[i]) for i in range(n)] == [(2, 3.0), (7, 1.0), (9, 1.0)]
+    assert L.orc_cluster_param_top_values(h, 11, T0 + 5000, 8, vals, qps) == 0
+    assert L.orc_cluster_param_top_values(h, 99, T0, 8, vals, qps) == 0  # no metric
+    L.orc_cluster_free(h)
