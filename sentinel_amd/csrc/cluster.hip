@@ -77,13 +77,23 @@ __device__ __forceinline__ uint32_t el_prio(uint64_t e) { return (uint32_t)(e >>
 __device__ __forceinline__ int32_t el_acq(uint64_t e) { return (int32_t)((e >> kAcqShift) & kAcqMax); }
 __device__ __forceinline__ uint32_t el_idx(uint64_t e) { return (uint32_t)e & ((1u << kIdxBits) - 1); }
 
+// floor(a / b) for 0 <= a, 0 < b through one double division and an exact correction
+// (a < 2^53); the int64 division sequence costs many more registers and cycles.
+__device__ __forceinline__ int64_t div_pos(int64_t a, int64_t b) {
+    if (a >= ((int64_t)1 << 53)) return a / b;
+    int64_t q = (int64_t)((double)a / (double)b);
+    const int64_t r = a - q * b;
+    if (r < 0) --q;
+    else if (r >= b) ++q;
+    return q;
+}
+
 // ---------------------------------------------------------------- classify
 // One workgroup per sort tile (4096 requests, kItems per thread strided by the block size so every
 // load is coalesced).  Validation (DefaultTokenService.notValidRequest, :87-89) and
 // ClusterFlowRuleManager.getFlowRuleById (open addressing) write BAD_REQUEST / NO_RULE_EXISTS
 // results directly.  The tile's histogram of the first radix digit is produced here (hist_d > 0).
-constexpr int kClsChunk = 4;  // hash probes in flight per thread
-
+template <int kClsChunk>  // table lookups in flight per thread
 __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const int64_t *__restrict__ flow_id,
                                                        const int32_t *__restrict__ acquire,
                                                        const uint8_t *__restrict__ prio,
@@ -104,6 +114,7 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
     for (int c = 0; c < kItems; c += kClsChunk) {
         int64_t fid[kClsChunk];
         int32_t acq[kClsChunk];
+        uint32_t tso[kClsChunk], pr[kClsChunk];
         uint32_t hh[kClsChunk];
         HashEntry e[kClsChunk];
 #pragma unroll
@@ -111,6 +122,8 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
             const uint32_t i = tbase + (c + u) * kThreads + threadIdx.x;
             fid[u] = i < n ? flow_id[i] : 0;
             acq[u] = i < n ? acquire[i] : 0;
+            tso[u] = i < n ? ts_off[i] : 0;
+            pr[u] = (i < n && !simple && prio) ? prio[i] : 0;
         }
         if (st.dense_n) {  // dense flowIds: one 4-byte load, no probe sequence
             uint32_t d[kClsChunk];
@@ -156,9 +169,9 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
                 el[i] = (uint64_t)invalid_key << kSlotShift;
             } else {
                 key = he.slot;
-                const uint32_t p = (!simple && prio && prio[i]) ? 1u : 0u;
+                const uint32_t p = pr[u] ? 1u : 0u;
                 const int64_t W = (int64_t)he.W;
-                const int64_t bd = (ts_base + (int64_t)ts_off[i]) / W - ts_base / W;
+                const int64_t bd = div_pos(ts_base + (int64_t)tso[u], W) - div_pos(ts_base, W);
                 uint32_t a7 = (a >= 1 && a <= (int32_t)kAcqMax) ? (uint32_t)a : 0u;
                 uint32_t bd6 = (uint32_t)bd;
                 if (bd >= (int64_t)kBdEsc) {
@@ -603,16 +616,6 @@ __device__ __forceinline__ int64_t i64_hi(const int4 &v) {
 // ClusterMetricLeapArray.resetWindowTo), the valid buckets summed, the pass prefix and the
 // occupied (SHOULD_WAIT) count found over the exact Java predicates, and the current bucket's
 // seven counters stored once.  Returns false (nothing touched) when the run is not eligible.
-// floor(a / b) for 0 <= a, 0 < b through one double division and an exact correction
-// (a < 2^53); the int64 division sequence costs many more registers and cycles.
-__device__ __forceinline__ int64_t div_pos(int64_t a, int64_t b) {
-    if (a >= ((int64_t)1 << 53)) return a / b;
-    int64_t q = (int64_t)((double)a / (double)b);
-    const int64_t r = a - q * b;
-    if (r < 0) --q;
-    else if (r >= b) ++q;
-    return q;
-}
 
 struct RunIn {
     uint32_t j0, n, cp_tot, p0;
@@ -1215,7 +1218,7 @@ __global__ __launch_bounds__(kThreads) void k_ppath(CParamState st, uint64_t *__
             const uint32_t kidx = vkey[voff[i]];
             const PRuleParam &P = st.param[slot];
             const int32_t a = acquire[i];
-            const int64_t bd = (ts_base + (int64_t)ts_off[i]) / P.W - ts_base / P.W;
+            const int64_t bd = div_pos(ts_base + (int64_t)ts_off[i], P.W) - div_pos(ts_base, P.W);
             uint32_t a7 = (a >= 1 && a <= (int32_t)kAcqMax) ? (uint32_t)a : 0u;
             uint32_t bd6 = (uint32_t)bd;
             if (bd >= (int64_t)kBdEsc) {
@@ -1582,11 +1585,15 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     const int npass = (bits + d0 - 1) / d0;
     if (lb) SGA_HIP_CHECK(hipMemsetAsync(sc.radix.ghist, 0, kRadixGhistWords * sizeof(uint32_t), s));
     if (lb) SGA_HIP_CHECK(hipMemsetAsync(sc.radix.err, 0, sizeof(uint32_t), s));
-    hipLaunchKernelGGL(k_classify, dim3(ntiles), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n,
-                       simple, invalid_key, sc.el[0], out, limited ? 0 : d0, ntiles, sc.radix.hist,
+    static const int chunk = getenv("SGA_CLS_CHUNK") ? atoi(getenv("SGA_CLS_CHUNK")) : 2;  // A/B knob
+    auto cls = chunk >= 16 ? k_classify<16>
+                           : (chunk >= 8 ? k_classify<8> : (chunk >= 4 ? k_classify<4> : (chunk >= 2 ? k_classify<2> : k_classify<1>)));
+    static const int nofuse = getenv("SGA_XP_NOFUSE") ? atoi(getenv("SGA_XP_NOFUSE")) : 0;  // A/B knob
+    hipLaunchKernelGGL(cls, dim3(ntiles), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n,
+                       simple, invalid_key, sc.el[0], out, (limited || nofuse) ? 0 : d0, ntiles, sc.radix.hist,
                        (lb && !limited) ? npass : 0, sc.radix.ghist);
     if (!simple) apply_limiters(st.param, sc, sc.el[0], n, invalid_key, ts_base, ts_off, out, lims, nlims, s);
-    const int np = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, !limited);
+    const int np = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, !limited && !nofuse);
     const uint64_t *el = sc.el[np & 1];
     hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
                        sc.tile_valid);

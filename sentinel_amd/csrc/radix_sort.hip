@@ -456,16 +456,34 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const uint32_t *__r
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_rs64_hist(const uint64_t *__restrict__ el, uint32_t n, int shift,
                                                         uint32_t ntiles, uint32_t *__restrict__ hist) {
+    // After the first pass equal keys sit next to each other, so one digit often fills a whole
+    // wave: lanes with equal digits are matched by ballots (as in the sweep) and only the first
+    // of them adds the group's size -- at most one LDS atomic per distinct digit per wave.
     constexpr int RADIX = 1 << D;
     __shared__ uint32_t h[RADIX];
     for (int d = threadIdx.x; d < RADIX; d += kThreads) h[d] = 0;
     __syncthreads();
     const uint32_t tile = blockIdx.x;
-    const uint32_t base = tile * kTile;
-#pragma unroll 4
+    const int lane = threadIdx.x & 63;
+    const uint32_t wbase = tile * kTile + (threadIdx.x >> 6) * (kRounds * 64);
+    uint64_t key[kRounds];
+#pragma unroll
     for (int r = 0; r < kRounds; ++r) {
-        const uint32_t e = base + r * kThreads + threadIdx.x;
-        if (e < n) atomicAdd(&h[(uint32_t)(el[e] >> shift) & (RADIX - 1)], 1u);
+        const uint32_t e = wbase + r * 64 + lane;
+        key[r] = e < n ? el[e] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const bool valid = wbase + r * 64 + lane < n;
+        const uint32_t d = (uint32_t)(key[r] >> shift) & (RADIX - 1);
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < D; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        if (valid && (peers & lanemask_lt(lane)) == 0) atomicAdd(&h[d], (uint32_t)__popcll(peers));
     }
     __syncthreads();
     for (int d = threadIdx.x; d < RADIX; d += kThreads) hist[(size_t)d * ntiles + tile] = h[d];
@@ -775,9 +793,11 @@ size_t radix_hist_entries(size_t n, int bits) {
 
 static int max_digit_bits() {
     static const int v = [] {
-        const char *e = getenv("SGA_RADIX_BITS");  // A/B knob: widest digit per pass (default 8)
+        // A/B knob: widest digit per pass (default 8).  At least 8: 24-bit slot keys must sort in
+        // kMaxPasses (3) passes.
+        const char *e = getenv("SGA_RADIX_BITS");
         int b = e ? atoi(e) : 8;
-        return b < 4 ? 4 : (b > kMaxDigitBits ? kMaxDigitBits : b);
+        return b < 8 ? 8 : (b > kMaxDigitBits ? kMaxDigitBits : b);
     }();
     return v;
 }
