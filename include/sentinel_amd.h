@@ -277,11 +277,16 @@ int sga_rls_should_rate_limit(sga_engine *e, const uint32_t *desc_offsets, size_
 #define SGA_BLOCK_PARAM 2    /* ParamFlowException */
 #define SGA_BLOCK_DEGRADE 3  /* DegradeException */
 #define SGA_PASS_WAIT 4      /* PriorityWaitException: passed after wait_ms, not counted as pass */
+#define SGA_BLOCK_SYSTEM 5   /* SystemBlockException (SystemSlot, inbound entries only) */
 
 /* event flags */
 #define SGA_EV_PRIORITIZED 1u
 #define SGA_EV_ERROR 2u      /* exit of an entry that recorded a business error (Tracer.traceEntry) */
 #define SGA_EV_HAS_PARAM 4u  /* args[0] present (param field) */
+#define SGA_EV_INBOUND 8u    /* EntryType.IN (on entries and their exits): Constants.ENTRY_NODE + SystemSlot */
+
+/* resource id of Constants.ENTRY_NODE ("__total_inbound_traffic__") in sga_query_node and metric rows */
+#define SGA_ENTRY_NODE 0xFFFFFFFFu
 
 /* FlowRule, CORE/slots/block/flow/FlowRule.java:52-95 (limitApp default, strategy DIRECT) */
 typedef struct sga_flow_rule {
@@ -345,6 +350,26 @@ int sga_submit_events(sga_engine *e, const uint8_t *kind, const uint32_t *resour
                       const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
                       size_t n, int8_t *decision, int32_t *wait_ms);
 int sga_query_node(sga_engine *e, uint32_t resource, int64_t now, sga_node_view *out);
+
+/* SystemRule (CORE/slots/system/SystemRule.java:43-50); negative = not set. */
+typedef struct sga_system_rule {
+    double highest_system_load;
+    double highest_cpu_usage;  /* > 1 is ignored as invalid */
+    double qps;
+    int64_t avg_rt;
+    int64_t max_thread;
+} sga_system_rule;
+
+/* SystemRuleManager.loadRules (SystemPropertyListener.configUpdate + loadSystemConf,
+ * SystemRuleManager.java:191-300): the minimum of every field over the rules; the check is on
+ * when the LAST rule sets any field (the reference sets the switch per rule); an empty list turns
+ * it off.  While on, inbound entries (SGA_EV_INBOUND) pass SystemRuleManager.checkSystem against
+ * ENTRY_NODE before the other slots -- a global order dependency: such batches are decided by
+ * one sequential lane (exact).  Returns the number of rules that set a field. */
+int sga_load_system_rules(sga_engine *e, const sga_system_rule *rules, size_t n);
+
+/* SystemStatusListener readings (system load average, CPU usage 0..1; -1 = not measured yet). */
+int sga_set_system_status(sga_engine *e, double avg_load, double cpu_usage);
 /* circuit breaker k of a resource: 0 CLOSED, 1 OPEN, 2 HALF_OPEN (negative = no such breaker) */
 int sga_circuit_breaker_state(sga_engine *e, uint32_t resource, uint32_t k);
 

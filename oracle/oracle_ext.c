@@ -529,21 +529,137 @@ void orc_flow_exit_p(orc_flow *f, uint32_t resource, int64_t now, int64_t rt, in
     for (int k = 0; k < fr->ncb; k++) cb_on_complete(fr->cb[k], now, rt, error);
 }
 
+/* ---- SystemSlot (CORE/slots/system) --------------------------------------- */
+#include <float.h>
+
+/* SystemPropertyListener.restoreSetting, SystemRuleManager.java:225-240 */
+void orc_flow_system_restore(orc_flow *f) {
+    f->sys.check = 0;
+    f->sys.load = DBL_MAX;
+    f->sys.cpu = DBL_MAX;
+    f->sys.qps = DBL_MAX;
+    f->sys.max_rt = INT64_MAX;
+    f->sys.max_thread = INT64_MAX;
+    f->sys.load_set = 0;
+    f->sys.cpu_set = 0;
+}
+
+/* SystemPropertyListener.configUpdate + loadSystemConf, SystemRuleManager.java:191-300: every field
+ * >= 0 lowers its threshold; checkSystemStatus ends as the LAST rule's "some field set" (the
+ * reference sets it per rule); an empty list switches the check off.  Returns the rules applied. */
+int orc_flow_load_system_rules(orc_flow *f, const orc_system_rule *rules, size_t n) {
+    orc_flow_system_restore(f);
+    int applied = 0;
+    for (size_t i = 0; i < n; i++) {
+        const orc_system_rule *r = &rules[i];
+        int st = 0;
+        if (r->highest_system_load >= 0) {
+            if (r->highest_system_load < f->sys.load) f->sys.load = r->highest_system_load;
+            f->sys.load_set = 1;
+            st = 1;
+        }
+        if (r->highest_cpu_usage >= 0 && r->highest_cpu_usage <= 1) { /* > 1: ignored as invalid */
+            if (r->highest_cpu_usage < f->sys.cpu) f->sys.cpu = r->highest_cpu_usage;
+            f->sys.cpu_set = 1;
+            st = 1;
+        }
+        if (r->avg_rt >= 0) {
+            if (r->avg_rt < f->sys.max_rt) f->sys.max_rt = r->avg_rt;
+            st = 1;
+        }
+        if (r->max_thread >= 0) {
+            if (r->max_thread < f->sys.max_thread) f->sys.max_thread = r->max_thread;
+            st = 1;
+        }
+        if (r->qps >= 0) {
+            if (r->qps < f->sys.qps) f->sys.qps = r->qps;
+            st = 1;
+        }
+        f->sys.check = st;
+        applied += st;
+    }
+    return applied;
+}
+
+/* SystemStatusListener readings (OperatingSystemMXBean load average / CPU usage, sampled each second) */
+void orc_flow_set_system_status(orc_flow *f, double avg_load, double cpu_usage) {
+    f->sys.cur_load = avg_load;
+    f->sys.cur_cpu = cpu_usage;
+}
+
+/* SystemRuleManager.checkSystem + checkBbr for an inbound entry, SystemRuleManager.java:298-353 */
+static int system_blocks(orc_flow *f, int64_t now, int count) {
+    if (!f->sys.check) return 0;
+    orc_node *e = f->entry;
+    if (orc_node_pass_qps(e, now) + count > f->sys.qps) return 1;
+    const int32_t thr = orc_node_cur_thread_num(e);
+    if ((int64_t)thr > f->sys.max_thread) return 1;
+    if (orc_node_avg_rt(e, now) > (double)f->sys.max_rt) return 1;
+    if (f->sys.load_set && f->sys.cur_load > f->sys.load) {
+        if (thr > 1 && thr > orc_node_max_success_qps(e, now) * orc_node_min_rt(e, now) / 1000) return 1;
+    }
+    if (f->sys.cpu_set && f->sys.cur_cpu > f->sys.cpu) return 1;
+    return 0;
+}
+
+/* The slot chain for one entry with its EntryType: SystemSlot before ParamFlowSlot / FlowSlot /
+ * DegradeSlot, and StatisticSlot's ENTRY_NODE updates for inbound traffic (StatisticSlot.java:54-137). */
+int orc_flow_entry_x(orc_flow *f, uint32_t resource, int64_t now, int acquire, int prioritized, int has_param,
+                     uint64_t param, int inbound, int64_t *wait_ms) {
+    int64_t dummy;
+    if (!wait_ms) wait_ms = &dummy;
+    *wait_ms = 0;
+    if (resource >= f->n) return ORC_PASS;
+    int d;
+    if (inbound && system_blocks(f, now, acquire)) {
+        orc_node_increase_block_qps(f->res[resource].node, now, acquire);
+        d = ORC_BLOCK_SYSTEM;
+    } else {
+        d = orc_flow_entry_p(f, resource, now, acquire, prioritized, has_param, param, wait_ms);
+    }
+    if (inbound) {
+        if (d == ORC_PASS) {
+            orc_node_increase_thread_num(f->entry);
+            orc_node_add_pass_request(f->entry, now, acquire);
+        } else if (d == ORC_PASS_WAIT) {
+            orc_node_increase_thread_num(f->entry);
+        } else {
+            orc_node_increase_block_qps(f->entry, now, acquire);
+        }
+    }
+    return d;
+}
+
+void orc_flow_exit_x(orc_flow *f, uint32_t resource, int64_t now, int64_t rt, int count, int error, int has_param,
+                     uint64_t param, int inbound) {
+    if (resource >= f->n) return;
+    orc_flow_exit_p(f, resource, now, rt, count, error, has_param, param);
+    if (inbound) { /* recordCompleteFor(Constants.ENTRY_NODE, ...) */
+        orc_node_add_rt_and_success(f->entry, now, rt, count);
+        orc_node_decrease_thread_num(f->entry);
+        if (error) orc_node_increase_exception_qps(f->entry, now, count);
+    }
+}
+
+orc_node *orc_flow_entry_node(orc_flow *f) { return f->entry; }
+
+/* flags: bit 0 prioritized, bit 1 error, bit 2 has_param, bit 3 inbound (EntryType.IN) */
 void orc_flow_replay_p(orc_flow *f, size_t n, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
                        const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
                        int8_t *decision, int32_t *wait_ms) {
     for (size_t i = 0; i < n; i++) {
         const uint8_t fl = flags ? flags[i] : 0;
         const int hp = (fl & 4) != 0;
+        const int in = (fl & 8) != 0;
         const uint64_t pv = param ? param[i] : 0;
         if (kind && kind[i] == 1) {
-            orc_flow_exit_p(f, resource[i], ts[i], rt ? rt[i] : 0, acquire[i], (fl & 2) != 0, hp, pv);
+            orc_flow_exit_x(f, resource[i], ts[i], rt ? rt[i] : 0, acquire[i], (fl & 2) != 0, hp, pv, in);
             if (decision) decision[i] = ORC_PASS;
             if (wait_ms) wait_ms[i] = 0;
             continue;
         }
         int64_t w = 0;
-        int d = orc_flow_entry_p(f, resource[i], ts[i], acquire[i], fl & 1, hp, pv, &w);
+        int d = orc_flow_entry_x(f, resource[i], ts[i], acquire[i], fl & 1, hp, pv, in, &w);
         if (decision) decision[i] = (int8_t)d;
         if (wait_ms) wait_ms[i] = (int32_t)w;
     }

@@ -62,6 +62,22 @@ int orc_flow_cb_state(orc_flow *f, uint32_t resource, int k);
 
 /* Batch replay with parameters: kind 0 entry / 1 exit; flags bit0 prioritized,
  * bit1 error (exit), bit2 has_param. */
+/* SystemRule fields (CORE/slots/system/SystemRule.java:43-50); negative = not set */
+typedef struct orc_system_rule {
+    double highest_system_load;
+    double highest_cpu_usage;
+    double qps;
+    int64_t avg_rt;
+    int64_t max_thread;
+} orc_system_rule;
+int orc_flow_load_system_rules(orc_flow *f, const orc_system_rule *rules, size_t n);
+void orc_flow_set_system_status(orc_flow *f, double avg_load, double cpu_usage);
+int orc_flow_entry_x(orc_flow *f, uint32_t resource, int64_t now, int acquire, int prioritized, int has_param,
+                     uint64_t param, int inbound, int64_t *wait_ms);
+void orc_flow_exit_x(orc_flow *f, uint32_t resource, int64_t now, int64_t rt, int count, int error, int has_param,
+                     uint64_t param, int inbound);
+orc_node *orc_flow_entry_node(orc_flow *f);
+
 void orc_flow_replay_p(orc_flow *f, size_t n, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
                        const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
                        int8_t *decision, int32_t *wait_ms);

@@ -65,13 +65,25 @@ typedef struct flow_res {
     int ncb;
 } flow_res;
 
+/* SystemRuleManager thresholds (SystemRuleManager.java:62-74) and SystemStatusListener readings */
+typedef struct orc_sys {
+    int check;  /* checkSystemStatus */
+    int load_set, cpu_set;
+    double load, cpu, qps;
+    int64_t max_rt, max_thread;
+    double cur_load, cur_cpu;  /* SystemStatusListener: -1 until measured */
+} orc_sys;
+
 struct orc_flow {
     uint32_t n;
     int cold_factor;
     flow_res *res;
+    orc_node *entry; /* Constants.ENTRY_NODE: inbound traffic of every resource */
+    orc_sys sys;
 };
 
-/* helpers implemented in sentinel_oracle.c */
+/* helpers implemented in sentinel_oracle.c / oracle_ext.c */
+void orc_flow_system_restore(orc_flow *f);
 int orc_flow_rule_check(orc_flow *f, uint32_t resource, int64_t now, int acquire, int prioritized, int64_t *wait_ms);
 void orc_flow_res_free_ext(flow_res *fr);
 

@@ -276,6 +276,8 @@ size_t orc_flow_metrics(orc_flow *f, int64_t now, orc_metric_node *out, size_t c
         if (!f->res[r].node) continue;
         k += orc_node_metrics(f->res[r].node, now, r, out ? out + (k < cap ? k : cap) : NULL, k < cap ? cap - k : 0);
     }
+    /* MetricTimerListener.run aggregates Constants.ENTRY_NODE after the cluster nodes (:56) */
+    k += orc_node_metrics(f->entry, now, ORC_ENTRY_NODE, out ? out + (k < cap ? k : cap) : NULL, k < cap ? cap - k : 0);
     return k;
 }
 
@@ -344,6 +346,19 @@ double orc_node_min_rt(orc_node *n, int64_t now) {
         if (l->b[i].min_rt < rt) rt = l->b[i].min_rt;
     }
     return (double)(rt < 1 ? 1 : rt);
+}
+/* StatisticNode.maxSuccessQps = ArrayMetric.maxSuccess() * sampleCount / intervalInSec,
+ * StatisticNode.java:225-230, ArrayMetric.java:82-93 */
+double orc_node_max_success_qps(orc_node *n, int64_t now) {
+    orc_leap *l = n->second;
+    leap_current(l, now);
+    int64_t s = 0;
+    for (int i = 0; i < l->sample_count; i++) {
+        if (!l->present[i] || leap_deprecated(l, now, &l->b[i])) continue;
+        if (l->b[i].c[ORC_EV_SUCCESS] > s) s = l->b[i].c[ORC_EV_SUCCESS];
+    }
+    if (s < 1) s = 1;
+    return (double)s * (double)l->sample_count / l->interval_sec;
 }
 int64_t orc_node_total_pass(orc_node *n, int64_t now) { return am_sum(n->minute, now, ORC_EV_PASS); }
 int64_t orc_node_total_block(orc_node *n, int64_t now) { return am_sum(n->minute, now, ORC_EV_BLOCK); }
@@ -571,6 +586,10 @@ orc_flow *orc_flow_new(uint32_t n_resources, int cold_factor) {
     f->cold_factor = cold_factor > 1 ? cold_factor : 3; /* SentinelConfig.coldFactor, :224-238 */
     f->res = (flow_res *)calloc(n_resources, sizeof(flow_res));
     for (uint32_t i = 0; i < n_resources; i++) f->res[i].node = orc_node_new();
+    f->entry = orc_node_new();
+    orc_flow_system_restore(f);
+    f->sys.cur_load = -1;
+    f->sys.cur_cpu = -1;
     return f;
 }
 
@@ -583,6 +602,7 @@ void orc_flow_free(orc_flow *f) {
         orc_flow_res_free_ext(&f->res[i]);
     }
     free(f->res);
+    orc_node_free(f->entry);
     free(f);
 }
 

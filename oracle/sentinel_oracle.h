@@ -102,7 +102,8 @@ void orc_node_set_mock(orc_node *n, double pass_qps, double previous_pass_qps, i
 enum { ORC_CTRL_DEFAULT = 0, ORC_CTRL_WARM_UP = 1, ORC_CTRL_RATE_LIMITER = 2, ORC_CTRL_WARM_UP_RATE_LIMITER = 3 };
 enum { ORC_GRADE_THREAD = 0, ORC_GRADE_QPS = 1 };
 /* decision codes shared with include/sentinel_amd.h */
-enum { ORC_PASS = 0, ORC_BLOCK_FLOW = 1, ORC_BLOCK_PARAM = 2, ORC_BLOCK_DEGRADE = 3, ORC_PASS_WAIT = 4 };
+enum { ORC_PASS = 0, ORC_BLOCK_FLOW = 1, ORC_BLOCK_PARAM = 2, ORC_BLOCK_DEGRADE = 3, ORC_PASS_WAIT = 4,
+       ORC_BLOCK_SYSTEM = 5 };
 
 typedef struct orc_ctrl orc_ctrl;
 orc_ctrl *orc_ctrl_new(int behavior, int grade, double count, int warm_up_period_sec, int max_queueing_time_ms,
@@ -156,6 +157,8 @@ typedef struct orc_metric_node {
 /* StatisticNode.metrics(): returns the number of due nodes (writes up to cap) */
 size_t orc_node_metrics(orc_node *n, int64_t now, uint32_t resource, orc_metric_node *out, size_t cap);
 size_t orc_flow_metrics(orc_flow *f, int64_t now, orc_metric_node *out, size_t cap);
+#define ORC_ENTRY_NODE 0xFFFFFFFFu /* resource id of Constants.ENTRY_NODE in metric rows and node queries */
+double orc_node_max_success_qps(orc_node *n, int64_t now);
 
 /* ---- cluster token server (CS/flow) ---------------------------------------- */
 typedef struct orc_cluster_rule {

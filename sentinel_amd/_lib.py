@@ -23,6 +23,11 @@ class SgaClusterFlowRule(C.Structure):
                 ("client_offline_time_ms", C.c_int64)]
 
 
+class SgaSystemRule(C.Structure):
+    _fields_ = [("highest_system_load", C.c_double), ("highest_cpu_usage", C.c_double), ("qps", C.c_double),
+                ("avg_rt", C.c_int64), ("max_thread", C.c_int64)]
+
+
 class SgaConcurrentResult(C.Structure):
     _fields_ = [("token_id", C.c_int64), ("status", C.c_int32), ("reserved", C.c_int32)]
 
@@ -123,6 +128,8 @@ SIGNATURES = {
     "sga_concurrent_token_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     "sga_concurrent_get_token": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(SgaTokenCacheNode)]),
     "sga_flow_set_resources": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "sga_load_system_rules": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "sga_set_system_status": (C.c_int, [C.c_void_p, C.c_double, C.c_double]),
     "sga_load_flow_rules": (C.c_int, [C.c_void_p, C.POINTER(SgaFlowRule), C.c_size_t]),
     "sga_load_param_rules": (C.c_int, [C.c_void_p, C.POINTER(SgaParamRule), C.c_size_t]),
     "sga_load_degrade_rules": (C.c_int, [C.c_void_p, C.POINTER(SgaDegradeRule), C.c_size_t]),

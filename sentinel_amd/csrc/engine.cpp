@@ -1250,6 +1250,19 @@ int sga_query_node(sga_engine *e, uint32_t resource, int64_t now, sga_node_view 
     });
 }
 
+int sga_load_system_rules(sga_engine *e, const sga_system_rule *rules, size_t n) {
+    if (n && !rules) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) { return g.flow.load_system_rules(rules, n); });
+}
+
+int sga_set_system_status(sga_engine *e, double avg_load, double cpu_usage) {
+    return guarded(e, [&](Engine &g) {
+        g.flow.sys.cur_load = avg_load;
+        g.flow.sys.cur_cpu = cpu_usage;
+        return SGA_OK;
+    });
+}
+
 int sga_metrics_snapshot(sga_engine *e, int64_t now, sga_metric_node *out, size_t cap, size_t *n) {
     return guarded(e, [&](Engine &g) {
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));

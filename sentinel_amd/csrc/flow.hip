@@ -32,7 +32,8 @@ constexpr int kTileElems = kT * kItems;  // 4096
 constexpr int kSecW = 500, kSecInterval = 1000;   // SampleCountProperty.SAMPLE_COUNT = 2, INTERVAL = 1000
 constexpr int kMinW = 1000, kMinInterval = 60000;
 constexpr int kOccupyTimeout = 500;               // OccupyTimeoutProperty
-enum : int8_t { D_PASS = 0, D_BLOCK_FLOW = 1, D_BLOCK_PARAM = 2, D_BLOCK_DEGRADE = 3, D_PASS_WAIT = 4 };
+enum : int8_t { D_PASS = 0, D_BLOCK_FLOW = 1, D_BLOCK_PARAM = 2, D_BLOCK_DEGRADE = 3, D_PASS_WAIT = 4,
+                D_BLOCK_SYSTEM = 5 };
 enum : uint32_t { F_EXIT = 1u << 30, F_ERROR = 1u << 29, F_PARAM = 1u << 28, F_IDX = (1u << 28) - 1 };
 enum : uint8_t { RUN_FAST = 0, RUN_DONE = 1 };
 
@@ -560,6 +561,201 @@ __device__ void chain_exit(const Ctx &c, uint32_t r, int64_t t, int64_t rt, int 
     for (uint32_t k = 0; k < R.n_cbs; ++k) cb_on_complete(c.st.cbs[R.cb_off + k], t, rt, error);
 }
 
+// ------------------------------------------------------------------ SystemSlot / ENTRY_NODE
+// Constants.ENTRY_NODE is node record nres.  StatisticSlot (StatisticSlot.java:54-137) updates it
+// for inbound (EntryType.IN) entries and their exits.
+__device__ __forceinline__ int64_t *entry_node(const Ctx &c) { return c.st.node + (size_t)c.st.nres * kNodeWords; }
+
+// SystemRuleManager.checkSystem + checkBbr (SystemRuleManager.java:298-353) for an inbound entry
+__device__ bool system_blocks(const Ctx &c, const SysDev &s, int64_t t, int count) {
+    if (!s.check) return false;
+    int64_t *e = entry_node(c);
+    if (node_pass_qps(c, e, t) + (double)count > s.qps) return true;  // ENTRY_NODE.passQps()
+    const int32_t thr = (int32_t)e[kNodeThreads];                    // curThreadNum()
+    if ((int64_t)thr > s.max_thread) return true;
+    sec_current(e, t, c.max_rt);                                      // avgRt(): success(), rt()
+    const int64_t succ = sec_sum(e, t, MB_SUCC);
+    const double rt = succ == 0 ? 0.0 : (double)sec_sum(e, t, MB_RT) * 1.0 / (double)succ;
+    if (rt > (double)s.max_rt) return true;
+    if (s.load_set && s.cur_load > s.load) {
+        if (thr > 1) {
+            // maxSuccessQps() = maxSuccess * sampleCount / intervalInSec; minRt() = max(1, min bucket minRt)
+            int64_t ms = 0, mr = c.max_rt;
+            for (int j = 0; j < 2; ++j) {
+                const int64_t *b = e + kNodeSec + kMB * j;
+                if (b[0] == kAbsent || t - b[0] > kSecInterval) continue;
+                if (b[MB_SUCC] > ms) ms = b[MB_SUCC];
+                if (b[MB_MINRT] < mr) mr = b[MB_MINRT];
+            }
+            if (ms < 1) ms = 1;
+            if (mr < 1) mr = 1;
+            const double cap = (double)ms * 2.0 / 1.0 * (double)mr / 1000;
+            if ((double)thr > cap) return true;
+        }
+    }
+    if (s.cpu_set && s.cur_cpu > s.cpu) return true;
+    return false;
+}
+
+__device__ __forceinline__ void entry_node_after_entry(const Ctx &c, int64_t t, int a, int8_t d) {
+    int64_t *e = entry_node(c);
+    if (d == D_PASS) {
+        e[kNodeThreads] += 1;
+        node_add(c, e, t, MB_PASS, a);
+    } else if (d == D_PASS_WAIT) {
+        e[kNodeThreads] += 1;
+    } else {
+        node_add(c, e, t, MB_BLOCK, a);
+    }
+}
+
+__device__ __forceinline__ void entry_node_after_exit(const Ctx &c, int64_t t, int64_t rt, int a, bool error) {
+    int64_t *e = entry_node(c);
+    node_add_rt_success(c, e, t, rt, a);
+    e[kNodeThreads] -= 1;
+    if (error) node_add(c, e, t, MB_EXC, a);
+}
+
+// System-rule mode: the whole batch by one lane in arrival order (checkSystem reads ENTRY_NODE,
+// which every earlier inbound decision of every resource changed).
+__global__ void k_lseq(FlowState st, int64_t max_rt, SysDev sys, const uint8_t *__restrict__ kind,
+                       const uint32_t *__restrict__ resource, const uint32_t *__restrict__ ts_off, int64_t ts_base,
+                       const int32_t *__restrict__ acquire, const uint8_t *__restrict__ flags,
+                       const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in, uint32_t n,
+                       int8_t *decision, int32_t *wait_ms) {
+    if (threadIdx.x || blockIdx.x) return;
+    const Ctx c{st, max_rt};
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t r = resource[i];
+        decision[i] = D_PASS;
+        wait_ms[i] = 0;
+        if (r >= st.nres) continue;  // unknown resource: no node, no rules
+        const int64_t t = ts_base + (int64_t)ts_off[i];
+        const uint8_t fl = flags[i];
+        const bool in = (fl & SGA_EV_INBOUND) != 0, hp = (fl & SGA_EV_HAS_PARAM) != 0;
+        const int a = (int)((uint32_t)acquire[i] & 0x7FFFFFFFu);
+        if (kind[i] == 1) {
+            chain_exit(c, r, t, rt_in[i], a, (fl & SGA_EV_ERROR) != 0, hp, param_in[i]);
+            if (in) entry_node_after_exit(c, t, rt_in[i], a, (fl & SGA_EV_ERROR) != 0);
+            continue;
+        }
+        int8_t d;
+        int64_t w = 0;
+        if (in && system_blocks(c, sys, t, a)) {
+            node_add(c, st.node + (size_t)r * kNodeWords, t, MB_BLOCK, a);  // StatisticSlot: increaseBlockQps
+            d = D_BLOCK_SYSTEM;
+        } else {
+            d = chain_entry(c, r, t, a, (fl & SGA_EV_PRIORITIZED) != 0, hp, param_in[i], &w);
+        }
+        if (in) entry_node_after_entry(c, t, a, d);
+        decision[i] = d;
+        wait_ms[i] = (int32_t)w;
+    }
+}
+
+// ENTRY_NODE statistics after a parallel batch (no system check): one workgroup walks the batch
+// in tiles.  A tile whose times do not decrease (and do not go below the previous tile's last
+// time) is reduced per 500 ms second-window bucket and applied bucket by bucket -- the same
+// window rotations as event by event, since a 500 ms bucket lies inside one 1 s minute bucket;
+// any other tile is applied event by event by one lane.
+constexpr int kEnTile = 1024, kEnBuckets = 64;
+__global__ __launch_bounds__(kEnTile) void k_entry_stats(FlowState st, int64_t max_rt,
+                                                         const uint8_t *__restrict__ kind,
+                                                         const uint32_t *__restrict__ resource,
+                                                         const uint32_t *__restrict__ ts_off, int64_t ts_base,
+                                                         const int32_t *__restrict__ acquire,
+                                                         const uint8_t *__restrict__ flags,
+                                                         const int64_t *__restrict__ rt_in,
+                                                         const int8_t *__restrict__ decision, uint32_t n) {
+    __shared__ unsigned long long bs[kEnBuckets][5];  // pass, block, success, rt, exception (two's complement)
+    __shared__ long long bmin[kEnBuckets];            // min rt
+    __shared__ unsigned long long thr_delta;
+    __shared__ int mono, any;
+    __shared__ int64_t prev_last;
+    const Ctx c{st, max_rt};
+    if (threadIdx.x == 0) prev_last = INT64_MIN;
+    for (uint32_t base = 0; base < n; base += kEnTile) {
+        const uint32_t i = base + threadIdx.x;
+        const bool live = i < n && resource[i] < st.nres && (flags[i] & SGA_EV_INBOUND);
+        const int64_t t = i < n ? ts_base + (int64_t)ts_off[i] : INT64_MAX;
+        for (int k = threadIdx.x; k < kEnBuckets * 5; k += kEnTile) bs[k / 5][k % 5] = 0;
+        for (int k = threadIdx.x; k < kEnBuckets; k += kEnTile) bmin[k] = max_rt;
+        if (threadIdx.x == 0) {
+            mono = 1;
+            any = 0;
+            thr_delta = 0;
+        }
+        __syncthreads();
+        const int64_t t0 = ts_base + (int64_t)ts_off[base];
+        if (i < n) {
+            const int64_t tp = threadIdx.x == 0 ? prev_last : ts_base + (int64_t)ts_off[i - 1];
+            if (t < tp || t / kSecW - t0 / kSecW >= kEnBuckets) mono = 0;
+        }
+        if (live) any = 1;
+        __syncthreads();
+        if (any && mono) {
+            if (live) {
+                const int bk = (int)(t / kSecW - t0 / kSecW);
+                const int a = (int)((uint32_t)acquire[i] & 0x7FFFFFFFu);
+                typedef unsigned long long u64;
+                if (kind[i] == 1) {
+                    atomicAdd(&bs[bk][2], (u64)a);
+                    atomicAdd(&bs[bk][3], (u64)rt_in[i]);
+                    if (flags[i] & SGA_EV_ERROR) atomicAdd(&bs[bk][4], (u64)a);
+                    atomicMin(&bmin[bk], (long long)rt_in[i]);
+                    atomicAdd(&thr_delta, ~0ull);  // -1
+                } else {
+                    const int8_t d = decision[i];
+                    if (d == D_PASS) {
+                        atomicAdd(&bs[bk][0], (u64)a);
+                        atomicAdd(&thr_delta, 1ull);
+                    } else if (d == D_PASS_WAIT) {
+                        atomicAdd(&thr_delta, 1ull);
+                    } else {
+                        atomicAdd(&bs[bk][1], (u64)a);
+                    }
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                int64_t *e = entry_node(c);
+                const int64_t last_t = ts_base + (int64_t)ts_off[min(base + kEnTile, n) - 1];
+                const int nb = (int)(last_t / kSecW - t0 / kSecW) + 1;
+                for (int b = 0; b < nb; ++b) {
+                    int64_t v[6];
+                    for (int q = 0; q < 5; ++q) v[q] = (int64_t)bs[b][q];
+                    v[5] = bmin[b];
+                    const bool has_sec = v[0] || v[1] || v[2] || v[3] || v[4] || v[5] != max_rt;
+                    if (!has_sec) continue;
+                    const int64_t tb = (t0 / kSecW + b) * kSecW;
+                    int64_t *w2[2] = {sec_current(e, tb, max_rt), min_current(e, tb, max_rt)};
+                    for (int q = 0; q < 2; ++q) {
+                        int64_t *w = w2[q];
+                        if (!w) continue;
+                        w[MB_PASS] += v[0];
+                        w[MB_BLOCK] += v[1];
+                        w[MB_SUCC] += v[2];
+                        w[MB_RT] += v[3];
+                        w[MB_EXC] += v[4];
+                        if (v[5] < w[MB_MINRT]) w[MB_MINRT] = v[5];
+                    }
+                }
+                e[kNodeThreads] += (int64_t)thr_delta;
+            }
+        } else if (any && threadIdx.x == 0) {  // out of order: event by event
+            for (uint32_t j = base; j < min(base + kEnTile, n); ++j) {
+                if (resource[j] >= st.nres || !(flags[j] & SGA_EV_INBOUND)) continue;
+                const int64_t tj = ts_base + (int64_t)ts_off[j];
+                const int a = (int)((uint32_t)acquire[j] & 0x7FFFFFFFu);
+                if (kind[j] == 1) entry_node_after_exit(c, tj, rt_in[j], a, (flags[j] & SGA_EV_ERROR) != 0);
+                else entry_node_after_entry(c, tj, a, decision[j]);
+            }
+        }
+        if (threadIdx.x == 0) prev_last = ts_base + (int64_t)ts_off[min(base + kEnTile, n) - 1];
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------------------ classify
 __global__ __launch_bounds__(kT) void k_lclassify(FlowState st, const uint8_t *__restrict__ kind,
                                                   const uint32_t *__restrict__ resource,
@@ -984,7 +1180,7 @@ __global__ void k_init_nodes(int64_t *node, uint32_t n, int64_t max_rt) {
 __global__ __launch_bounds__(kT) void k_metrics(FlowState st, int64_t max_rt, int64_t now, sga_metric_node *out,
                                                 uint32_t cap, uint32_t *count) {
     const uint32_t r = blockIdx.x * kT + threadIdx.x;
-    if (r >= st.nres) return;
+    if (r > st.nres) return;  // node nres = ENTRY_NODE
     int64_t *node = st.node + (size_t)r * kNodeWords;
     const int64_t cur = now - now % 1000;
     min_current(node, now, max_rt);
@@ -1001,7 +1197,7 @@ __global__ __launch_bounds__(kT) void k_metrics(FlowState st, int64_t max_rt, in
         m.exception_qps = b[MB_EXC];
         m.rt = m.success_qps != 0 ? b[MB_RT] / m.success_qps : b[MB_RT];
         m.occupied_pass_qps = b[MB_OPASS];
-        m.resource = r;
+        m.resource = r == st.nres ? SGA_ENTRY_NODE : r;
         m.concurrency = 0;
         const bool in_time = m.timestamp > last && m.timestamp < cur;
         const bool valid = m.pass_qps > 0 || m.block_qps > 0 || m.success_qps > 0 || m.exception_qps > 0 ||
@@ -1045,8 +1241,8 @@ int FlowEngine::set_resources(uint32_t n) {
     if (n == nres) return 0;
     if (nres != 0) return SGA_EINVAL;  // resource table is fixed once set
     nres = n;
-    d_node.alloc((size_t)n * kNodeWords);
-    hipLaunchKernelGGL(k_init_nodes, dim3((n + kT - 1) / kT), dim3(kT), 0, stream, d_node.p, n,
+    d_node.alloc(((size_t)n + 1) * kNodeWords);  // + Constants.ENTRY_NODE at index n
+    hipLaunchKernelGGL(k_init_nodes, dim3((n + 1 + kT - 1) / kT), dim3(kT), 0, stream, d_node.p, n + 1,
                        (int64_t)cfg.statistic_max_rt);
     h_res.assign(n, ResDev{});
     d_overflow.alloc(1);
@@ -1391,6 +1587,22 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, stream));
         const FlowState st = state();
         const uint32_t nb = (uint32_t)((m + kT - 1) / kT);
+        bool has_in = false;
+        for (size_t i = 0; flags && i < m && !has_in; ++i) has_in = (flags[b + i] & SGA_EV_INBOUND) && resource[b + i] < nres;
+        if (has_in && sys.check) {  // SystemSlot: one lane in arrival order
+            hipLaunchKernelGGL(k_lseq, dim3(1), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sys, d_kind.p,
+                               d_resid.p, d_ts.p, lo, d_acq.p, d_flags.p, d_rt.p, d_param.p, (uint32_t)m, d_dec.p,
+                               d_wait.p);
+            SGA_HIP_CHECK(hipGetLastError());
+            SGA_HIP_CHECK(hipMemcpyAsync(decision + b, d_dec.p, m, hipMemcpyDeviceToHost, stream));
+            if (wait_ms) SGA_HIP_CHECK(hipMemcpyAsync(wait_ms + b, d_wait.p, m * 4, hipMemcpyDeviceToHost, stream));
+            uint32_t ovf = 0;
+            SGA_HIP_CHECK(hipMemcpyAsync(&ovf, d_overflow.p, 4, hipMemcpyDeviceToHost, stream));
+            SGA_HIP_CHECK(hipStreamSynchronize(stream));
+            if (ovf) return SGA_ENOMEM;
+            b += m;
+            continue;
+        }
         hipLaunchKernelGGL(k_lclassify, dim3(nb), dim3(kT), 0, stream, st, d_kind.p, d_resid.p, d_ts.p, lo, d_acq.p,
                            d_flags.p, (uint32_t)m, sc.keys[0], sc.pay[0], d_dec.p, d_wait.p);
         const int np = radix_sort_pairs(sc.keys[0], sc.pay[0], sc.keys[1], sc.pay[1], m, bits, sc.radix, stream);
@@ -1408,6 +1620,9 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, stream, st,
                            (int64_t)cfg.statistic_max_rt, sc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p);
         hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, stream, sc, pay, d_dec.p);
+        if (has_in)  // ENTRY_NODE statistics of the inbound events
+            hipLaunchKernelGGL(k_entry_stats, dim3(1), dim3(kEnTile), 0, stream, st, (int64_t)cfg.statistic_max_rt,
+                               d_kind.p, d_resid.p, d_ts.p, lo, d_acq.p, d_flags.p, d_rt.p, d_dec.p, (uint32_t)m);
         SGA_HIP_CHECK(hipGetLastError());
         SGA_HIP_CHECK(hipMemcpyAsync(decision + b, d_dec.p, m, hipMemcpyDeviceToHost, stream));
         if (wait_ms) SGA_HIP_CHECK(hipMemcpyAsync(wait_ms + b, d_wait.p, m * 4, hipMemcpyDeviceToHost, stream));
@@ -1421,7 +1636,9 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
 }
 
 int FlowEngine::query(uint32_t r, int64_t now, sga_node_view *out) {
-    if (r >= nres || now < 0 || !out) return SGA_EINVAL;
+    if (r == SGA_ENTRY_NODE && nres) r = nres;
+    else if (r >= nres) return SGA_EINVAL;
+    if (now < 0 || !out) return SGA_EINVAL;
     if (!d_view.p) d_view.alloc(16);
     hipLaunchKernelGGL(k_node_view, dim3(1), dim3(64), 0, stream, state(), (int64_t)cfg.statistic_max_rt, r, now,
                        (double *)d_view.p, d_view.p + 8);
@@ -1455,7 +1672,7 @@ int FlowEngine::metrics(int64_t now, sga_metric_node *out, size_t cap, size_t *n
     if (d_metrics.n < dcap) d_metrics.alloc(dcap);
     if (!d_mcount.p) d_mcount.alloc(1);
     SGA_HIP_CHECK(hipMemsetAsync(d_mcount.p, 0, 4, stream));
-    hipLaunchKernelGGL(k_metrics, dim3((nres + kT - 1) / kT), dim3(kT), 0, stream, state(),
+    hipLaunchKernelGGL(k_metrics, dim3((nres + 1 + kT - 1) / kT), dim3(kT), 0, stream, state(),
                        (int64_t)cfg.statistic_max_rt, now, d_metrics.p, (uint32_t)cap, d_mcount.p);
     uint32_t cnt = 0;
     SGA_HIP_CHECK(hipMemcpyAsync(&cnt, d_mcount.p, 4, hipMemcpyDeviceToHost, stream));
@@ -1464,6 +1681,48 @@ int FlowEngine::metrics(int64_t now, sga_metric_node *out, size_t cap, size_t *n
     if (w) SGA_HIP_CHECK(hipMemcpy(out, d_metrics.p, w * sizeof(sga_metric_node), hipMemcpyDeviceToHost));
     *n = w;
     return cnt > cap ? SGA_ERANGE : 0;
+}
+
+// SystemPropertyListener.configUpdate + loadSystemConf, SystemRuleManager.java:191-300
+int FlowEngine::load_system_rules(const sga_system_rule *r, size_t n) {
+    const double dmax = 1.7976931348623157e308;
+    sys.check = 0;
+    sys.load = dmax;
+    sys.cpu = dmax;
+    sys.qps = dmax;
+    sys.max_rt = INT64_MAX;
+    sys.max_thread = INT64_MAX;
+    sys.load_set = 0;
+    sys.cpu_set = 0;
+    int applied = 0;
+    for (size_t i = 0; i < n; ++i) {
+        int st = 0;
+        if (r[i].highest_system_load >= 0) {
+            sys.load = std::min(sys.load, r[i].highest_system_load);
+            sys.load_set = 1;
+            st = 1;
+        }
+        if (r[i].highest_cpu_usage >= 0 && r[i].highest_cpu_usage <= 1) {  // > 1: "Ignoring invalid SystemRule"
+            sys.cpu = std::min(sys.cpu, r[i].highest_cpu_usage);
+            sys.cpu_set = 1;
+            st = 1;
+        }
+        if (r[i].avg_rt >= 0) {
+            sys.max_rt = std::min(sys.max_rt, r[i].avg_rt);
+            st = 1;
+        }
+        if (r[i].max_thread >= 0) {
+            sys.max_thread = std::min(sys.max_thread, r[i].max_thread);
+            st = 1;
+        }
+        if (r[i].qps >= 0) {
+            sys.qps = std::min(sys.qps, r[i].qps);
+            st = 1;
+        }
+        sys.check = st;  // checkSystemStatus.set(checkStatus) per rule: the last rule decides
+        applied += st;
+    }
+    return applied;
 }
 
 int FlowEngine::cb_state(uint32_t r, uint32_t k) {

@@ -69,6 +69,14 @@ struct alignas(32) PEntry {
 };
 constexpr int64_t kPAbsent = INT64_MIN;
 
+// SystemRuleManager thresholds (SystemRuleManager.java:62-74) + SystemStatusListener readings
+struct SysDev {
+    int32_t check, load_set, cpu_set, pad;
+    double load, cpu, qps;
+    int64_t max_rt, max_thread;
+    double cur_load, cur_cpu;
+};
+
 struct FlowState {
     int64_t *node;
     FlowRuleDev *rules;
@@ -157,6 +165,9 @@ struct FlowEngine {
     int query(uint32_t resource, int64_t now, sga_node_view *out);
     int cb_state(uint32_t resource, uint32_t k);
     int metrics(int64_t now, sga_metric_node *out, size_t cap, size_t *n);
+    int load_system_rules(const sga_system_rule *r, size_t n);
+    SysDev sys{0, 0, 0, 0, 1.7976931348623157e308, 1.7976931348623157e308, 1.7976931348623157e308, INT64_MAX,
+               INT64_MAX, -1.0, -1.0};
     DevBuf<sga_metric_node> d_metrics;
     DevBuf<uint32_t> d_mcount;
 };

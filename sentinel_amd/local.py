@@ -7,6 +7,8 @@ Same names and argument meaning as the Java API the engine replaces:
   FlowRuleManager.loadRules       CORE/slots/block/flow/FlowRuleManager.java:125-127
   ParamFlowRuleManager.loadRules  PF/slots/block/flow/param/ParamFlowRuleManager.java:52
   DegradeRuleManager.loadRules    CORE/slots/block/degrade/DegradeRuleManager.java:108
+  SystemRuleManager.loadRules     CORE/slots/system/SystemRuleManager.java:114-300 (SystemSlot, inbound only)
+  Constants.ENTRY_NODE            CORE/Constants.java:66 -> LocalSentinel.node(ENTRY_NODE), metrics rows
   ClusterNode statistics          CORE/node/StatisticNode.java:185-250 -> LocalSentinel.node
 BlockException subclasses as in CORE/slots/block/BlockException.java and its subclasses.
 
@@ -33,11 +35,15 @@ class Decision:
     BLOCK_PARAM = 2
     BLOCK_DEGRADE = 3
     PASS_WAIT = 4
+    BLOCK_SYSTEM = 5
 
 
 EV_PRIORITIZED = 1
 EV_ERROR = 2
 EV_HAS_PARAM = 4
+EV_INBOUND = 8          # EntryType.IN
+ENTRY_NODE = 0xFFFFFFFF  # resource id of Constants.ENTRY_NODE
+TOTAL_IN_RESOURCE_NAME = "__total_inbound_traffic__"  # Constants.TOTAL_IN_RESOURCE_NAME
 KIND_ENTRY = 0
 KIND_EXIT = 1
 
@@ -60,8 +66,12 @@ class DegradeException(BlockException):
     pass
 
 
+class SystemBlockException(BlockException):
+    pass
+
+
 _EXC = {Decision.BLOCK_FLOW: FlowException, Decision.BLOCK_PARAM: ParamFlowException,
-        Decision.BLOCK_DEGRADE: DegradeException}
+        Decision.BLOCK_DEGRADE: DegradeException, Decision.BLOCK_SYSTEM: SystemBlockException}
 
 
 def param_value(x) -> int:
@@ -125,8 +135,9 @@ class Entry:
     """A passed entry; exit() records RT / success (StatisticSlot.exit) and breaker completion."""
 
     def __init__(self, owner: "LocalSentinel", rid: int, create_ts: int, count: int, param: Optional[int],
-                 wait_ms: int):
+                 wait_ms: int, inbound: bool = False):
         self._owner = owner
+        self.inbound = inbound
         self.rid = rid
         self.create_timestamp = create_ts
         self.count = count
@@ -142,7 +153,8 @@ class Entry:
         if self.exited:
             return
         self.exited = True
-        fl = (EV_ERROR if self.error else 0) | (EV_HAS_PARAM if self.param is not None else 0)
+        fl = (EV_ERROR if self.error else 0) | (EV_HAS_PARAM if self.param is not None else 0) | \
+            (EV_INBOUND if self.inbound else 0)
         self._owner.submit([KIND_EXIT], [self.rid], [now], [self.count], [fl], [now - self.create_timestamp],
                            [self.param or 0])
 
@@ -186,17 +198,24 @@ class LocalSentinel:
         return dec, wait
 
     # ---- SphU-style single entry
-    def entry(self, resource: str, now: int, batch_count: int = 1, prioritized: bool = False, args=()) -> Entry:
+    def entry(self, resource: str, now: int, batch_count: int = 1, prioritized: bool = False, args=(),
+              entry_type: str = "OUT") -> Entry:
+        """SphU.entry(resource, entryType, batchCount, args); entry_type "IN" marks inbound traffic."""
         rid = self.ids[resource]
+        inbound = entry_type == "IN"
         param = param_value(args[0]) if len(args) > 0 else None
-        fl = (EV_PRIORITIZED if prioritized else 0) | (EV_HAS_PARAM if param is not None else 0)
+        fl = (EV_PRIORITIZED if prioritized else 0) | (EV_HAS_PARAM if param is not None else 0) | \
+            (EV_INBOUND if inbound else 0)
         dec, wait = self.submit([KIND_ENTRY], [rid], [now], [batch_count], [fl], None, [param or 0])
         d = int(dec[0])
         if d in _EXC:
             raise _EXC[d](resource)
-        return Entry(self, rid, now, batch_count, param, int(wait[0]))
+        return Entry(self, rid, now, batch_count, param, int(wait[0]), inbound)
 
     def node(self, resource, now: int) -> NodeView:
+        """ClusterNode views; resource ENTRY_NODE (or TOTAL_IN_RESOURCE_NAME) is Constants.ENTRY_NODE."""
+        if resource == TOTAL_IN_RESOURCE_NAME:
+            resource = ENTRY_NODE
         rid = resource if isinstance(resource, int) else self.ids[resource]
         v = SgaNodeView()
         check(_lib.load().sga_query_node(self.engine.handle, rid, now, C.byref(v)), self.engine.handle, "node")
@@ -209,10 +228,13 @@ class LocalSentinel:
         n = C.c_size_t()
         rc = _lib.load().sga_metrics_snapshot(self.engine.handle, now, buf, cap, C.byref(n))
         _lib.check(rc, self.engine.handle, "metrics")
-        out = [MetricNode(b.timestamp, self.resources[b.resource], b.pass_qps, b.block_qps, b.success_qps,
+        def name(r):
+            return TOTAL_IN_RESOURCE_NAME if r == ENTRY_NODE else self.resources[r]
+
+        out = [MetricNode(b.timestamp, name(b.resource), b.pass_qps, b.block_qps, b.success_qps,
                           b.exception_qps, b.rt, b.occupied_pass_qps, b.concurrency)
                for b in buf[:n.value]]
-        out.sort(key=lambda m: (m.timestamp, self.ids[m.resource]))
+        out.sort(key=lambda m: (m.timestamp, self.ids.get(m.resource, ENTRY_NODE)))
         return out
 
     def circuit_breaker_state(self, resource, k: int = 0) -> int:
@@ -293,3 +315,34 @@ class DegradeRuleManager:
             a.stat_interval_ms = r.stat_interval_ms
         return check(_lib.load().sga_load_degrade_rules(self.s.engine.handle, arr, len(rules)), self.s.engine.handle,
                      "DegradeRuleManager.loadRules")
+
+
+@dataclass
+class SystemRule:
+    """CORE/slots/system/SystemRule.java:43-50 (negative = not set)."""
+    highest_system_load: float = -1.0
+    highest_cpu_usage: float = -1.0
+    qps: float = -1.0
+    avg_rt: int = -1
+    max_thread: int = -1
+
+
+class SystemRuleManager:
+    """SystemRuleManager.loadRules + the SystemStatusListener readings the host measures."""
+
+    def __init__(self, sentinel: LocalSentinel):
+        self.s = sentinel
+
+    def load_rules(self, rules: List[SystemRule]) -> int:
+        arr = (_lib.SgaSystemRule * max(1, len(rules)))()
+        for i, r in enumerate(rules):
+            arr[i].highest_system_load = r.highest_system_load
+            arr[i].highest_cpu_usage = r.highest_cpu_usage
+            arr[i].qps = r.qps
+            arr[i].avg_rt = r.avg_rt
+            arr[i].max_thread = r.max_thread
+        return check(_lib.load().sga_load_system_rules(self.s.engine.handle, arr, len(rules)), self.s.engine.handle,
+                     "SystemRuleManager.loadRules")
+
+    def set_system_status(self, avg_load: float, cpu_usage: float):
+        check(_lib.load().sga_set_system_status(self.s.engine.handle, avg_load, cpu_usage), self.s.engine.handle)

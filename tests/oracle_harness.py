@@ -36,6 +36,11 @@ class OrcClusterRule(C.Structure):
                 ("client_offline_time_ms", C.c_int64)]
 
 
+class OrcSystemRule(C.Structure):
+    _fields_ = [("highest_system_load", C.c_double), ("highest_cpu_usage", C.c_double), ("qps", C.c_double),
+                ("avg_rt", C.c_int64), ("max_thread", C.c_int64)]
+
+
 class OrcConcResult(C.Structure):
     _fields_ = [("status", C.c_int32), ("reserved", C.c_int32), ("token_id", C.c_int64)]
 
@@ -124,6 +129,12 @@ def lib():
         "orc_cluster_request_param_token": (OrcTokenResult, [P, I64, I32, P, C.c_size_t, I64]),
         "orc_cluster_param_replay": (None, [P, C.c_size_t, P, P, P, P, P, P]),
         "orc_cluster_param_sum": (I64, [P, I64, I64, I64]),
+        "orc_flow_load_system_rules": (C.c_int, [P, C.POINTER(OrcSystemRule), C.c_size_t]),
+        "orc_flow_set_system_status": (None, [P, D, D]),
+        "orc_flow_entry_x": (C.c_int, [P, U32, I64, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, C.POINTER(I64)]),
+        "orc_flow_exit_x": (None, [P, U32, I64, I64, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int]),
+        "orc_flow_entry_node": (P, [P]),
+        "orc_node_max_success_qps": (D, [P, I64]),
         "orc_cluster_param_top_values": (C.c_size_t, [P, I64, I64, C.c_size_t, P, P]),
         "orc_cluster_concurrent_acquire": (OrcConcResult, [P, U32, I64, I32, I64, I64]),
         "orc_cluster_concurrent_release": (I32, [P, I64]),

@@ -59,7 +59,8 @@ def test_struct_layouts_match_header():
 _STRUCTS = {"SgaConfig": "sga_config", "SgaClusterFlowRule": "sga_cluster_flow_rule",
             "SgaTokenResult": "sga_token_result", "SgaFlowRule": "sga_flow_rule", "SgaParamRule": "sga_param_rule",
             "SgaDegradeRule": "sga_degrade_rule", "SgaNodeView": "sga_node_view",
-            "SgaConcurrentResult": "sga_concurrent_result", "SgaTokenCacheNode": "sga_token_cache_node"}
+            "SgaConcurrentResult": "sga_concurrent_result", "SgaTokenCacheNode": "sga_token_cache_node",
+            "SgaSystemRule": "sga_system_rule"}
 
 
 def test_every_field_offset_matches_the_c_compiler(tmp_path):
