@@ -1027,11 +1027,112 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
             const int32_t a = sc.run_amin[r];
             const int64_t t0 = ts_base + (int64_t)sc.run_t0off[r];
             bool fast = (R.fast & 1u) && sc.run_cp[r] == 0 && (nent == 0 || a == sc.run_amax[r]) && a >= 0;
-            if (fast) {  // no clock regression in this resource's windows
+            bool pace = (R.fast & 4u) != 0;
+            if (fast || pace) {  // no clock regression in this resource's windows
                 const int64_t *sb = node + kNodeSec + kMB * (int)((t0 / kSecW) % 2);
                 const int64_t *mb = node + kNodeMin + kMB * (int)((t0 / kMinW) % 60);
                 if ((sb[0] != kAbsent && t0 - t0 % kSecW < sb[0]) || (mb[0] != kAbsent && t0 - t0 % kMinW < mb[0]))
-                    fast = false;
+                    fast = pace = false;
+            }
+            if (pace) {
+                // RateLimiterController alone (RateLimiterController.java:46-91): the decisions depend on
+                // latestPassedTime only, so the run's entries are paced in registers, in order; the run's
+                // statistics (one 500 ms bucket) are added once, like the closed form below.
+                FlowRuleDev &rule = st.rules[R.rule_off];
+                int64_t latest = rule.latest_passed;
+                // the rule fields in registers: the decision stores could alias them otherwise, and
+                // every reload would wait behind the previous stores
+                const double rcount = rule.count;
+                const int64_t rqueue = rule.max_queue;
+                int64_t pa = 0, ba = 0, npass = 0;
+                int last_aq = -1;  // Math.round(1.0 * acquire / count * 1000) of the last acquire count
+                int64_t last_cost = 0;
+                // decide one event in registers; returns its (index, decision, wait) for the store
+                auto pace_one = [&](const Payload &q, uint32_t &idx, int8_t &d, int32_t &wo) {
+                    idx = q.idx & F_IDX;
+                    d = D_PASS;
+                    wo = 0;
+                    if (q.idx & F_EXIT) return false;
+                    const int64_t t = ts_base + (int64_t)q.ts_off;
+                    const int aq = (int)(q.acq_prio & 0x7FFFFFFFu);
+                    int64_t w = 0;
+                    if (aq > 0) {
+                        if (rcount <= 0) {
+                            d = D_BLOCK_FLOW;
+                        } else {
+                            if (aq != last_aq) {
+                                last_aq = aq;
+                                last_cost = j_round(1.0 * aq / rcount * 1000);
+                            }
+                            const int64_t cost = last_cost;
+                            if (cost + latest <= t) {
+                                latest = t;
+                            } else if (cost + latest - t > rqueue) {
+                                d = D_BLOCK_FLOW;
+                            } else {
+                                latest += cost;
+                                w = latest - t;
+                                if (w > rqueue) {
+                                    latest -= cost;
+                                    d = D_BLOCK_FLOW;
+                                    w = 0;
+                                } else if (w < 0) {
+                                    w = 0;
+                                }
+                            }
+                        }
+                    }
+                    wo = (int32_t)w;
+                    if (d == D_PASS) {
+                        pa += aq;
+                        ++npass;
+                    } else {
+                        ba += aq;
+                    }
+                    return true;
+                };
+                // software pipeline: the next 4 payloads are loaded before this group's stores are
+                // issued, so a load never waits behind the previous group's scattered stores
+                constexpr uint32_t kG = 4;
+                const Payload none{F_EXIT, 0, 0, 0};
+                Payload c0 = j0 < j1 ? pay[j0] : none, c1 = j0 + 1 < j1 ? pay[j0 + 1] : none;
+                Payload c2 = j0 + 2 < j1 ? pay[j0 + 2] : none, c3 = j0 + 3 < j1 ? pay[j0 + 3] : none;
+                for (uint32_t g = j0; g < j1; g += kG) {
+                    const uint32_t nx = g + kG;
+                    const Payload n0 = nx < j1 ? pay[nx] : none, n1 = nx + 1 < j1 ? pay[nx + 1] : none;
+                    const Payload n2 = nx + 2 < j1 ? pay[nx + 2] : none, n3 = nx + 3 < j1 ? pay[nx + 3] : none;
+                    uint32_t i0, i1, i2, i3;
+                    int8_t d0, d1, d2, d3;
+                    int32_t w0, w1, w2, w3;
+                    const bool v0 = pace_one(c0, i0, d0, w0), v1 = pace_one(c1, i1, d1, w1);
+                    const bool v2 = pace_one(c2, i2, d2, w2), v3 = pace_one(c3, i3, d3, w3);
+                    if (v0) { decision[i0] = d0; wait_ms[i0] = w0; }
+                    if (v1) { decision[i1] = d1; wait_ms[i1] = w1; }
+                    if (v2) { decision[i2] = d2; wait_ms[i2] = w2; }
+                    if (v3) { decision[i3] = d3; wait_ms[i3] = w3; }
+                    c0 = n0;
+                    c1 = n1;
+                    c2 = n2;
+                    c3 = n3;
+                }
+                rule.latest_passed = latest;
+                int64_t *sb = sec_current(node, t0, max_rt);
+                int64_t *mb = min_current(node, t0, max_rt);
+                const int64_t exc = (int64_t)sc.run_exc[r], exerr = (int64_t)sc.run_exerr[r];
+                const int64_t exrt = sc.run_exrt[r], exmin = sc.run_exmin[r];
+                int64_t *w2[2] = {sb, mb};
+                for (int k = 0; k < 2; ++k) {
+                    int64_t *b = w2[k];
+                    b[MB_PASS] += pa;
+                    b[MB_BLOCK] += ba;
+                    b[MB_SUCC] += exc;
+                    b[MB_RT] += exrt;
+                    b[MB_EXC] += exerr;
+                    if (exmin < b[MB_MINRT]) b[MB_MINRT] = exmin;
+                }
+                node[kNodeThreads] += npass - (int64_t)sc.run_nexit[r];
+                sc.run_mode[r] = RUN_DONE;
+                continue;
             }
             if (fast && nent) {  // WarmUp sync must only see entries in one second (true: run is inside one 500 ms bucket)
                 const int64_t s0 = sec_sum(node, t0, MB_PASS);
@@ -1267,6 +1368,7 @@ void FlowEngine::upload_res() {
         if (R.n_rules == 1 && R.n_prules == 0 && R.n_cbs == 0 && !(R.fast & 2u)) {
             const FlowRuleDev &fr = h_rules[R.rule_off];
             if (fr.grade == 1 && (fr.behavior == 0 || fr.behavior == 1)) R.fast = 1;
+            else if (fr.grade == 1 && fr.behavior == 2) R.fast = 4;  // pacing only: k_lflows register loop
         }
     }
     if (d_res.n < std::max<size_t>(nres, 1)) d_res.alloc(std::max<size_t>(nres, 1));
