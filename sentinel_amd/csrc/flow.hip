@@ -35,6 +35,7 @@ constexpr int kOccupyTimeout = 500;               // OccupyTimeoutProperty
 enum : int8_t { D_PASS = 0, D_BLOCK_FLOW = 1, D_BLOCK_PARAM = 2, D_BLOCK_DEGRADE = 3, D_PASS_WAIT = 4,
                 D_BLOCK_SYSTEM = 5 };
 enum : uint32_t { F_EXIT = 1u << 30, F_ERROR = 1u << 29, F_PARAM = 1u << 28, F_IDX = (1u << 28) - 1 };
+constexpr uint32_t kHeavyEvents = 1024;  // per batch: replayed by k_lheavy instead of one k_lflows lane
 enum : uint8_t { RUN_FAST = 0, RUN_DONE = 1 };
 
 struct Ctx {
@@ -470,10 +471,22 @@ __device__ void cb_on_complete(CbDev &b, int64_t t, int64_t rt, bool error) {
 }
 
 // ------------------------------------------------------------------ slot chain (one event)
-__device__ int8_t chain_entry(const Ctx &c, uint32_t r, int64_t t, int acquire, bool prio, bool has_param,
-                              uint64_t param, int64_t *wait_ms) {
+// Where a resource's mutable state lives during a replay: global memory, or the LDS copy a
+// heavy resource's workgroup works on (k_lheavy).
+struct ResMem {
+    int64_t *node;
+    FlowRuleDev *rules;  // the resource's rules (st.rules + rule_off)
+    CbDev *cbs;          // its circuit breakers (st.cbs + cb_off)
+};
+
+__device__ __forceinline__ ResMem res_global(const Ctx &c, uint32_t r, const ResDev &R) {
+    return ResMem{c.st.node + (size_t)r * kNodeWords, c.st.rules + R.rule_off, c.st.cbs + R.cb_off};
+}
+
+__device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t t, int acquire, bool prio,
+                              bool has_param, uint64_t param, int64_t *wait_ms) {
     const ResDev R = c.st.res[r];
-    int64_t *node = c.st.node + (size_t)r * kNodeWords;
+    int64_t *node = m.node;
     *wait_ms = 0;
     int64_t total_wait = 0;
     // ParamFlowSlot (ParamFlowSlot.java:65-92): args = [param] or []
@@ -498,7 +511,7 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, int64_t t, int acquire, 
     // FlowSlot
     for (uint32_t k = 0; k < R.n_rules; ++k) {
         int64_t w = 0;
-        const int8_t d = rater_can_pass(c, c.st.rules[R.rule_off + k], node, t, acquire, prio, &w);
+        const int8_t d = rater_can_pass(c, m.rules[k], node, t, acquire, prio, &w);
         if (d == D_BLOCK_FLOW) {
             node_add(c, node, t, MB_BLOCK, acquire);
             return D_BLOCK_FLOW;
@@ -517,7 +530,7 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, int64_t t, int acquire, 
     // DegradeSlot
     uint64_t half_mask = 0;
     for (uint32_t k = 0; k < R.n_cbs; ++k) {
-        CbDev &b = c.st.cbs[R.cb_off + k];
+        CbDev &b = m.cbs[k];
         bool ok = false;
         if (b.state == 0) ok = true;
         else if (b.state == 1 && t >= b.next_retry) {
@@ -527,7 +540,7 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, int64_t t, int acquire, 
         }
         if (!ok) {
             for (uint32_t q = 0; q < k && q < 64; ++q) {
-                CbDev &bq = c.st.cbs[R.cb_off + q];
+                CbDev &bq = m.cbs[q];
                 if (((half_mask >> q) & 1) && bq.state == 2) bq.state = 1;
             }
             node_add(c, node, t, MB_BLOCK, acquire);
@@ -544,10 +557,10 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, int64_t t, int acquire, 
     return D_PASS;
 }
 
-__device__ void chain_exit(const Ctx &c, uint32_t r, int64_t t, int64_t rt, int count, bool error, bool has_param,
-                           uint64_t param) {
+__device__ void chain_exit(const Ctx &c, uint32_t r, const ResMem &m, int64_t t, int64_t rt, int count, bool error,
+                           bool has_param, uint64_t param) {
     const ResDev R = c.st.res[r];
-    int64_t *node = c.st.node + (size_t)r * kNodeWords;
+    int64_t *node = m.node;
     node_add_rt_success(c, node, t, rt, count);
     node[kNodeThreads] -= 1;
     if (error) node_add(c, node, t, MB_EXC, count);
@@ -558,7 +571,17 @@ __device__ void chain_exit(const Ctx &c, uint32_t r, int64_t t, int64_t rt, int 
             else if (--te->a <= 0) te->a = kPAbsent;  // remove(value)
         }
     }
-    for (uint32_t k = 0; k < R.n_cbs; ++k) cb_on_complete(c.st.cbs[R.cb_off + k], t, rt, error);
+    for (uint32_t k = 0; k < R.n_cbs; ++k) cb_on_complete(m.cbs[k], t, rt, error);
+}
+
+__device__ __forceinline__ int8_t chain_entry(const Ctx &c, uint32_t r, int64_t t, int acquire, bool prio,
+                                              bool has_param, uint64_t param, int64_t *wait_ms) {
+    return chain_entry(c, r, res_global(c, r, c.st.res[r]), t, acquire, prio, has_param, param, wait_ms);
+}
+
+__device__ __forceinline__ void chain_exit(const Ctx &c, uint32_t r, int64_t t, int64_t rt, int count, bool error,
+                                           bool has_param, uint64_t param) {
+    chain_exit(c, r, res_global(c, r, c.st.res[r]), t, rt, count, error, has_param, param);
 }
 
 // ------------------------------------------------------------------ SystemSlot / ENTRY_NODE
@@ -1018,6 +1041,13 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
     for (uint32_t fl = blockIdx.x * kT + threadIdx.x; fl < nflows; fl += gridDim.x * kT) {
         const uint32_t r0 = sc.flow_first_run[fl];
         const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        {  // a long event-by-event replay goes to k_lheavy (its state in LDS)
+            const uint32_t res = sc.run_slot[r0];
+            if ((st.res[res].fast & 5u) == 0 && sc.run_end[r1 - 1] - sc.run_start[r0] >= kHeavyEvents) {
+                sc.heavy[atomicAdd(&sc.counters[8], 1u)] = fl;
+                continue;
+            }
+        }
         for (uint32_t r = r0; r < r1; ++r) {
             const uint32_t res = sc.run_slot[r];
             const ResDev R = st.res[res];
@@ -1213,6 +1243,90 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
             sc.run_f[r] = f;
             sc.run_mode[r] = RUN_FAST;
         }
+    }
+}
+
+// Heavy resources (many events, no closed form): one workgroup each; its node record, rules and
+// breakers are copied to LDS, lane 0 replays every event in order against the LDS copy (an LDS
+// round trip instead of a global one per state access), and the state is written back.
+constexpr int kHeavyRules = 16, kHeavyCbs = 16, kHeavyChunk = 512;
+__global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, FlowScratch sc,
+                                               const Payload *__restrict__ pay, int64_t ts_base,
+                                               const int64_t *__restrict__ rt_in,
+                                               const uint64_t *__restrict__ param_in, int8_t *decision,
+                                               int32_t *wait_ms) {
+    __shared__ int64_t lnode[kNodeWords];
+    __shared__ FlowRuleDev lrules[kHeavyRules];
+    __shared__ CbDev lcbs[kHeavyCbs];
+    __shared__ Payload qpay[kHeavyChunk];
+    __shared__ int64_t qrt[kHeavyChunk];
+    __shared__ uint64_t qpv[kHeavyChunk];
+    __shared__ int8_t qd[kHeavyChunk];
+    __shared__ int32_t qw[kHeavyChunk];
+    const Ctx c{st, max_rt};
+    const uint32_t nheavy = sc.counters[8], nflows = sc.counters[2], nruns = sc.counters[1];
+    for (uint32_t h = blockIdx.x; h < nheavy; h += gridDim.x) {
+        const uint32_t fl = sc.heavy[h];
+        const uint32_t r0 = sc.flow_first_run[fl];
+        const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        const uint32_t res = sc.run_slot[r0];
+        const ResDev R = st.res[res];
+        ResMem g = res_global(c, res, R);
+        const bool lr = R.n_rules <= (uint32_t)kHeavyRules, lc = R.n_cbs <= (uint32_t)kHeavyCbs;
+        for (int k = threadIdx.x; k < kNodeWords; k += 64) lnode[k] = g.node[k];
+        if (lr)
+            for (uint32_t k = threadIdx.x; k < R.n_rules; k += 64) lrules[k] = g.rules[k];
+        if (lc)
+            for (uint32_t k = threadIdx.x; k < R.n_cbs; k += 64) lcbs[k] = g.cbs[k];
+        __syncthreads();
+        // events in chunks: the 64 lanes stage payloads, RTs and parameters into LDS, lane 0 replays
+        // the chunk from LDS, then the lanes store its decisions
+        const ResMem m{lnode, lr ? lrules : g.rules, lc ? lcbs : g.cbs};
+        const uint32_t jb = sc.run_start[r0], je = sc.run_end[r1 - 1];
+        for (uint32_t base = jb; base < je; base += kHeavyChunk) {
+            const uint32_t cnt = min((uint32_t)kHeavyChunk, je - base);
+            for (uint32_t k = threadIdx.x; k < cnt; k += 64) {
+                const Payload q = pay[base + k];
+                const uint32_t idx = q.idx & F_IDX;
+                qpay[k] = q;
+                qrt[k] = (q.idx & F_EXIT) ? rt_in[idx] : 0;
+                qpv[k] = (q.idx & F_PARAM) ? param_in[idx] : 0;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    const Payload q = qpay[k];
+                    const int64_t t = ts_base + (int64_t)q.ts_off;
+                    const bool hp = (q.idx & F_PARAM) != 0;
+                    if (q.idx & F_EXIT) {
+                        chain_exit(c, res, m, t, qrt[k], (int)(q.acq_prio & 0x7FFFFFFFu), (q.idx & F_ERROR) != 0, hp,
+                                   qpv[k]);
+                    } else {
+                        int64_t w = 0;
+                        qd[k] = chain_entry(c, res, m, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
+                                            hp, qpv[k], &w);
+                        qw[k] = (int32_t)w;
+                    }
+                }
+            }
+            __syncthreads();
+            for (uint32_t k = threadIdx.x; k < cnt; k += 64) {
+                const Payload q = qpay[k];
+                if (!(q.idx & F_EXIT)) {
+                    decision[q.idx & F_IDX] = qd[k];
+                    wait_ms[q.idx & F_IDX] = qw[k];
+                }
+            }
+            __syncthreads();
+        }
+        for (uint32_t r = r0 + threadIdx.x; r < r1; r += 64) sc.run_mode[r] = RUN_DONE;
+        __syncthreads();
+        for (int k = threadIdx.x; k < kNodeWords; k += 64) g.node[k] = lnode[k];
+        if (lr)
+            for (uint32_t k = threadIdx.x; k < R.n_rules; k += 64) g.rules[k] = lrules[k];
+        if (lc)
+            for (uint32_t k = threadIdx.x; k < R.n_cbs; k += 64) g.cbs[k] = lcbs[k];
+        __syncthreads();
     }
 }
 
@@ -1606,7 +1720,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         for (int b = 1; b <= 32; ++b) hist = std::max(hist, radix_hist_entries(cap, b));
         const size_t ntiles = (cap + kTileElems - 1) / kTileElems + 1;
         size_t bytes = 2 * al(cap * 4) + 2 * al(cap * sizeof(Payload)) + 2 * al(cap * 4) + 10 * al(cap * 4) +
-                       4 * al(cap * 8) + al(cap) + al(cap * 4) + 2 * al(ntiles * sizeof(LAgg)) + al(ntiles * 4) +
+                       4 * al(cap * 8) + al(cap) + 2 * al(cap * 4) + 2 * al(ntiles * sizeof(LAgg)) + al(ntiles * 4) +
                        al(64) + 2 * al(hist * 4) + al(scan_partials_needed(hist) * 4 + 64);
         d_scratch.alloc(bytes);
         char *p = (char *)d_scratch.p;
@@ -1637,6 +1751,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         sc.run_exmin = (int64_t *)take(cap * 8);
         sc.run_mode = (uint8_t *)take(cap);
         sc.flow_first_run = (uint32_t *)take(cap * 4);
+        sc.heavy = (uint32_t *)take(cap * 4);
         sc.tile_agg = take(ntiles * sizeof(LAgg));
         sc.tile_carry = take(ntiles * sizeof(LAgg));
         sc.tile_valid = (uint32_t *)take(ntiles * 4);
@@ -1721,6 +1836,9 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         const uint32_t fthreads = (uint32_t)std::min<size_t>(m, nres);
         hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, stream, st,
                            (int64_t)cfg.statistic_max_rt, sc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p);
+        hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
+                           dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
+                           d_dec.p, d_wait.p);
         hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, stream, sc, pay, d_dec.p);
         if (has_in)  // ENTRY_NODE statistics of the inbound events
             hipLaunchKernelGGL(k_entry_stats, dim3(1), dim3(kEnTile), 0, stream, st, (int64_t)cfg.statistic_max_rt,

@@ -104,6 +104,7 @@ struct FlowScratch {
     uint32_t *run_f;
     uint8_t *run_mode;
     uint32_t *flow_first_run;
+    uint32_t *heavy;  // flows replayed by k_lheavy (count in counters[8])
     void *tile_agg, *tile_carry;
     uint32_t *tile_valid;
     uint32_t *counters;
