@@ -59,7 +59,8 @@ class Engine:
     """Owns one sga_engine (one GPU / one shard)."""
 
     def __init__(self, device: int = 0, max_batch: int = 1 << 20, max_rules: int = 1 << 16,
-                 exceed_count: float = 1.0, max_occupy_ratio: float = 1.0, max_param_keys: int = 0):
+                 exceed_count: float = 1.0, max_occupy_ratio: float = 1.0, max_param_keys: int = 0,
+                 hot_rules: bool = False, hot_min_requests: int = 64):
         L = _lib.load()
         cfg = SgaConfig()
         L.sga_config_default(C.byref(cfg))
@@ -75,6 +76,7 @@ class Engine:
             raise _lib.EngineError(f"sga_create failed rc={rc}")
         self._h = h
         self.max_batch = max_batch
+        self.set_hot_rules(hot_rules, hot_min_requests)
         self.clients: dict = {}  # client address -> dense id (concurrency tokens)
 
     def client_id(self, address: Optional[str]) -> int:
@@ -85,6 +87,13 @@ class Engine:
         if c is None:
             c = self.clients[address] = len(self.clients)
         return c
+
+    def set_hot_rules(self, enabled: bool = True, min_requests: int = 64):
+        """Engine tuning (sga_set_hot_rules): the hottest rules skip the sort (experimental, off by
+        default: measured slower at C3, DESIGN.md section 3).  Decisions do not depend on it;
+        tests use min_requests=1 to send nearly every rule down the hot path."""
+        _lib.check(_lib.load().sga_set_hot_rules(self._h, 1 if enabled else 0, int(min_requests)), self._h,
+                   "sga_set_hot_rules")
 
     @property
     def handle(self):

@@ -43,6 +43,8 @@ __device__ __forceinline__ uint64_t pack_result(int8_t status, int32_t remaining
            ((uint64_t)(uint8_t)status << 48);
 }
 
+__device__ __forceinline__ uint64_t lanemask_lt64(int lane) { return (1ULL << lane) - 1ULL; }
+
 __device__ __forceinline__ HashEntry slot_lookup(const ClusterState &st, int64_t fid) {
     uint32_t h = (uint32_t)hash_flow_id(fid) & st.hmask;
     for (uint32_t probe = 0; probe <= st.hmask; ++probe) {
@@ -305,10 +307,12 @@ __device__ __forceinline__ Agg run_value(uint64_t x, uint64_t px, bool has_prev,
 // Per tile: aggregate over its valid elements + count of valid elements.
 __global__ __launch_bounds__(kRunThreads) void k_runs_up(const uint64_t *__restrict__ el, uint32_t n,
                                                       uint32_t invalid_key, Agg *__restrict__ tile_agg,
-                                                      uint32_t *__restrict__ tile_valid) {
+                                                      uint32_t *__restrict__ tile_valid,
+                                                      const uint32_t *__restrict__ dn) {
     __shared__ Agg wagg[kRunWaves];
     __shared__ uint32_t wval[kRunWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (dn) n = min(n, *dn);  // hot/cold split: elements past the cold + hot count are stale
     const uint32_t e0 = blockIdx.x * kTileElems + threadIdx.x * kPerThread;
     uint64_t x[kPerThread];
     el_load_blk(el, e0, n, invalid_key, x);
@@ -400,7 +404,8 @@ __global__ __launch_bounds__(kTileScanThreads) void k_runs_tiles(const Agg *__re
 // Per tile: run and flow records, the list of prioritized positions, and each wave's carry
 // (for k_results, which re-derives run ids and prioritized ranks instead of reading them).
 __global__ __launch_bounds__(kRunThreads) void k_runs_down(const uint64_t *__restrict__ el, uint32_t invalid_key,
-                                                        const Agg *__restrict__ tile_carry, BatchScratch sc) {
+                                                        const Agg *__restrict__ tile_carry, BatchScratch sc,
+                                                        int hot) {
     __shared__ Agg wagg[kRunWaves];
     const uint32_t nvalid = sc.counters[0];
     const uint32_t base = blockIdx.x * kTileElems;
@@ -449,7 +454,13 @@ __global__ __launch_bounds__(kRunThreads) void k_runs_down(const uint64_t *__res
             sc.run_bd[rid] = (uint8_t)bd;
             sc.run_p0[rid] = run.np - p;
         }
-        if (fh) sc.flow_first_run[run.nf - 1] = rid;
+        if (fh) {
+            sc.flow_first_run[run.nf - 1] = rid;
+            if (hot && e >= sc.counters[8]) {  // hot region: k_hot_results finds the rule's runs here
+                const uint32_t hid = sc.hot_of[el_slot(cur)];
+                if (hid < (uint32_t)kHot) sc.hot_first_run[hid] = rid;
+            }
+        }
         if (p) sc.plist[run.np - 1] = e;
         const uint64_t nx = k + 1 < kPerThread ? x[k + 1 < kPerThread ? k + 1 : k] : after;
         if (e + 1 >= nvalid || el_runkey(nx) != el_runkey(cur)) {
@@ -831,8 +842,10 @@ __global__ __launch_bounds__(kThreads) void k_flows_slow(ClusterState st, BatchS
 // Same tile geometry as k_runs_down; each wave starts from the carry k_runs_down stored and
 // re-derives every request's run id and prioritized rank, then writes its TokenResult.
 __global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const uint64_t *__restrict__ el,
-                                                         uint32_t invalid_key, uint64_t *__restrict__ out) {
-    const uint32_t nvalid = sc.counters[0];
+                                                         uint32_t invalid_key, uint64_t *__restrict__ out, int hot) {
+    // hot/cold split: only the cold region [0, counters[8]) -- hot requests are answered in input
+    // order by k_hot_results
+    const uint32_t nvalid = hot ? min(sc.counters[0], sc.counters[8]) : sc.counters[0];
     const uint32_t base = blockIdx.x * kTileElems;
     if (base >= nvalid) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -893,6 +906,535 @@ __global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const 
         }
         out[el_idx(x[k])] = res;
     }
+}
+
+// ---------------------------------------------------------------- hot/cold split
+// Under Zipf skew a few thousand rules carry most requests.  Those "hot" rules (hot id < kHot,
+// chosen from the previous batch's counts) skip the radix sort: classify ranks each hot request
+// among the tile's requests of the same rule (wave-private LDS counters, waves own contiguous
+// 1024-request slices so ranks follow arrival order), the per-tile counts are scanned over tiles
+// per hot id, and one scatter places every hot request at
+//   hot region start + hot_base[hid] + prefix over earlier tiles + in-tile rank
+// -- a stable counting sort by rule.  The hot region is appended to the sorted cold elements, so
+// runs / flows see exactly the arrival-ordered per-rule segments they see without the split.
+// k_hot_results then answers hot requests in INPUT order (coalesced stores) from the run records.
+constexpr int kHidShift = 52, kRankShift = 40;
+constexpr uint64_t kLow40 = ((uint64_t)1 << 40) - 1;
+constexpr int kHotGroup = 16;  // tiles per group of the tile scan
+constexpr int kClsWaves = kThreads / 64;
+constexpr int kClsRounds = kTileElems / kThreads;  // 64-request rounds per wave
+
+template <int kClsChunk>
+__global__ __launch_bounds__(kThreads) void k_classify_hot(ClusterState st, BatchScratch sc,
+                                                           const int64_t *__restrict__ flow_id,
+                                                           const int32_t *__restrict__ acquire,
+                                                           const uint8_t *__restrict__ prio,
+                                                           const uint32_t *__restrict__ ts_off, int64_t ts_base,
+                                                           uint32_t n, int simple, uint64_t *__restrict__ out,
+                                                           int hist_d, uint32_t ntiles, uint32_t *__restrict__ hist) {
+    // Wave w owns the 1024-request segment [w * 1024, (w + 1) * 1024) of the tile and writes its
+    // cold elements from the segment start and its hot elements from the segment end as it goes
+    // (nothing held in registers across rounds); hot elements first carry their rank among the
+    // wave's requests of the rule, and the wave prefix is added in a fix-up pass at the end.
+    __shared__ uint16_t wcnt[kClsWaves][kHot];  // per wave, per hot id: requests so far -> wave prefix
+    __shared__ uint32_t h[1024];
+    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt = lanemask_lt64(lane);
+    for (uint32_t i = threadIdx.x; i < nhot; i += kThreads)
+#pragma unroll
+        for (int w = 0; w < kClsWaves; ++w) wcnt[w][i] = 0;
+    const uint32_t nh = hist_d > 0 ? 1u << hist_d : 0u;
+    for (uint32_t d = threadIdx.x; d < nh; d += kThreads) h[d] = 0;
+    __syncthreads();
+    const uint32_t tile = blockIdx.x, tbase = tile * kTileElems;
+    const uint32_t wbase = tbase + wave * (kClsRounds * 64);
+    uint64_t *seg = sc.el_tile + wbase;            // cold from seg[0], hot from seg[1023] downwards
+    uint32_t nc_w = 0, nh_w = 0;
+    // software pipeline: the request fields of chunk c + 1 are loaded while chunk c is processed
+    int64_t fid[kClsChunk], nfid[kClsChunk];
+    int32_t acq[kClsChunk], nacq[kClsChunk];
+    uint32_t tso[kClsChunk], pr[kClsChunk], ntso[kClsChunk], npr[kClsChunk];
+    auto load_chunk = [&](int c, int64_t (&f)[kClsChunk], int32_t (&a)[kClsChunk], uint32_t (&t)[kClsChunk],
+                          uint32_t (&p)[kClsChunk]) {
+#pragma unroll
+        for (int u = 0; u < kClsChunk; ++u) {
+            const uint32_t i = wbase + (c + u) * 64 + lane;
+            f[u] = i < n ? flow_id[i] : 0;
+            a[u] = i < n ? acquire[i] : 0;
+            t[u] = i < n ? ts_off[i] : 0;
+            p[u] = (i < n && !simple && prio) ? prio[i] : 0;
+        }
+    };
+    load_chunk(0, fid, acq, tso, pr);
+    for (int c = 0; c < kClsRounds; c += kClsChunk) {
+        uint32_t hh[kClsChunk], hf[kClsChunk];
+        HashEntry e[kClsChunk];
+        if (st.dense_n) {  // the hot id is gathered beside the slot entry (both keyed by flowId)
+            uint32_t d[kClsChunk];
+#pragma unroll
+            for (int u = 0; u < kClsChunk; ++u) {
+                const bool in = fid[u] >= 1 && fid[u] <= (int64_t)st.dense_n;
+                d[u] = in ? st.dense[fid[u] - 1] : ~0u;
+                hf[u] = (in && nhot) ? st.hot_fid[fid[u] - 1] : kColdId;
+            }
+#pragma unroll
+            for (int u = 0; u < kClsChunk; ++u) {
+                hh[u] = 0;
+                e[u] = d[u] == ~0u ? HashEntry{-1, 0, 0} : HashEntry{fid[u], d[u] & 0xFFFFFFu, st.wtab[d[u] >> 24]};
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kClsChunk; ++u) {
+                hh[u] = (uint32_t)hash_flow_id(fid[u]) & st.hmask;
+                e[u] = fid[u] > 0 ? st.htab[hh[u]] : HashEntry{0, 0, 0};
+                hf[u] = kColdId;
+            }
+        }
+        if (c + kClsChunk < kClsRounds) load_chunk(c + kClsChunk, nfid, nacq, ntso, npr);
+#pragma unroll
+        for (int u = 0; u < kClsChunk; ++u) {
+            const uint32_t i = wbase + (c + u) * 64 + lane;
+            uint32_t kind = 0, hid = kColdId, slot = 0;
+            uint64_t x = 0;
+            if (i < n) {
+                const int64_t f = fid[u];
+                const int32_t a = acq[u];
+                int8_t status = TRS_OK;
+                HashEntry he = e[u];
+                if (!simple && (f <= 0 || a <= 0)) {
+                    status = TRS_BAD_REQUEST;
+                } else {
+                    if (!st.dense_n && f > 0 && he.key != f && he.key != 0) {
+                        uint32_t q = hh[u];
+                        for (uint32_t probe = 1; probe <= st.hmask; ++probe) {
+                            q = (q + 1) & st.hmask;
+                            he = st.htab[q];
+                            if (he.key == f || he.key == 0) break;
+                        }
+                    }
+                    if (he.key != f || f <= 0) status = TRS_NO_RULE_EXISTS;
+                }
+                if (status != TRS_OK) {
+                    out[i] = pack_result(status, 0, 0);
+                } else {
+                    slot = he.slot;
+                    const int64_t W = (int64_t)he.W;
+                    const int64_t bd = div_pos(ts_base + (int64_t)tso[u], W) - div_pos(ts_base, W);
+                    uint32_t a7 = (a >= 1 && a <= (int32_t)kAcqMax) ? (uint32_t)a : 0u;
+                    uint32_t bd6 = (uint32_t)bd;
+                    if (bd >= (int64_t)kBdEsc) {
+                        bd6 = kBdEsc;
+                        a7 = 0;
+                    }
+                    x = el_pack(slot, bd6, pr[u] ? 1u : 0u, a7, i);
+                    kind = 1;
+                    if (nhot) {
+                        hid = st.dense_n ? hf[u] : sc.hot_of[slot];
+                        if (hid < nhot) kind = 2;
+                    }
+                }
+            }
+            const uint64_t bc = __ballot(kind == 1);
+            if (kind == 1) {
+                seg[nc_w + (uint32_t)__popcll(bc & lt)] = x;
+                if (nh) atomicAdd(&h[slot & (nh - 1)], 1u);
+            }
+            nc_w += (uint32_t)__popcll(bc);
+            const uint64_t bh = __ballot(kind == 2);
+            if (bh) {
+                uint64_t peers = bh;
+#pragma unroll
+                for (int b = 0; b < 12; ++b) {
+                    const bool bit = (hid >> b) & 1u;
+                    const uint64_t bb = __ballot(bit);
+                    peers &= bit ? bb : ~bb;
+                }
+                uint32_t before = 0;
+                if (kind == 2) before = wcnt[wave][hid];
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t my = (uint32_t)__popcll(peers & lt);
+                if (kind == 2 && my == 0) wcnt[wave][hid] = (uint16_t)(before + (uint32_t)__popcll(peers));
+                __builtin_amdgcn_wave_barrier();
+                if (kind == 2)
+                    seg[kClsRounds * 64 - 1 - (nh_w + (uint32_t)__popcll(bh & lt))] =
+                        ((uint64_t)hid << kHidShift) | ((uint64_t)(before + my) << kRankShift) | (x & kLow40);
+                nh_w += (uint32_t)__popcll(bh);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kClsChunk; ++u) {
+            fid[u] = nfid[u];
+            acq[u] = nacq[u];
+            tso[u] = ntso[u];
+            pr[u] = npr[u];
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nhot; i += kThreads) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int w = 0; w < kClsWaves; ++w) {
+            const uint32_t c = wcnt[w][i];
+            wcnt[w][i] = (uint16_t)acc;
+            acc += c;
+        }
+        sc.hcnt[(size_t)tile * kHot + i] = (uint16_t)acc;
+    }
+    if (lane == 0) {  // totals: k_hs_group / k_hs_base (same-address atomics from every wave serialize)
+        sc.tile_nc[tile * kClsWaves + wave] = nc_w;
+        sc.tile_nh[tile * kClsWaves + wave] = nh_w;
+    }
+    __syncthreads();
+    // fix-up: in-tile rank = wave prefix of the rule + rank within the wave (wave 0 has no prefix)
+    if (wave > 0) {
+        uint64_t *top = seg + kClsRounds * 64 - 1;
+        for (uint32_t k0 = 0; k0 < nh_w; k0 += 64 * 4) {
+            uint64_t x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t k = k0 + u * 64 + lane;
+                x[u] = k < nh_w ? *(top - k) : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t k = k0 + u * 64 + lane;
+                if (k < nh_w) *(top - k) = x[u] + ((uint64_t)wcnt[wave][(uint32_t)(x[u] >> kHidShift)] << kRankShift);
+            }
+        }
+    }
+    for (uint32_t d = threadIdx.x; d < nh; d += kThreads) hist[(size_t)d * ntiles + tile] = h[d];
+}
+
+// Tile scan per hot id, in three steps over groups of kHotGroup tiles.
+__global__ __launch_bounds__(kThreads) void k_hs_group(BatchScratch sc, uint32_t ntiles) {
+    if (blockIdx.y == 0 && threadIdx.x < 64) {  // the group's cold / hot element counts
+        const uint32_t i = blockIdx.x * kHotGroup * kClsWaves + threadIdx.x;  // 64 = kHotGroup x kClsWaves
+        uint32_t c = i < ntiles * kClsWaves ? sc.tile_nc[i] : 0u;
+        uint32_t h = i < ntiles * kClsWaves ? sc.tile_nh[i] : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            c += (uint32_t)__shfl_down((int)c, o, 64);
+            h += (uint32_t)__shfl_down((int)h, o, 64);
+        }
+        if (threadIdx.x == 0) {
+            sc.hgcnt[2 * blockIdx.x] = c;
+            sc.hgcnt[2 * blockIdx.x + 1] = h;
+        }
+    }
+    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
+    const uint32_t hid = blockIdx.y * kThreads + threadIdx.x;
+    if (hid >= nhot) return;
+    const uint32_t t0 = blockIdx.x * kHotGroup;
+    uint32_t v[kHotGroup], s = 0;
+#pragma unroll
+    for (int k = 0; k < kHotGroup; ++k) v[k] = t0 + k < ntiles ? sc.hcnt[(size_t)(t0 + k) * kHot + hid] : 0u;
+#pragma unroll
+    for (int k = 0; k < kHotGroup; ++k) s += v[k];
+    sc.hgsum[(size_t)blockIdx.x * kHot + hid] = s;
+}
+
+__global__ __launch_bounds__(kThreads) void k_hs_mid(BatchScratch sc, uint32_t ngroups) {
+    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
+    const uint32_t hid = blockIdx.x * kThreads + threadIdx.x;
+    if (hid >= nhot) return;
+    uint32_t acc = 0;
+#pragma unroll 8
+    for (uint32_t g = 0; g < ngroups; ++g) {
+        const uint32_t v = sc.hgsum[(size_t)g * kHot + hid];
+        sc.hgsum[(size_t)g * kHot + hid] = acc;
+        acc += v;
+    }
+    sc.hot_tot[hid] = acc;
+}
+
+// hot_base = exclusive scan of the per-hot-id totals (one workgroup, 4 ids per thread); the batch's
+// cold / hot element totals into counters[8..10]
+__global__ __launch_bounds__(1024) void k_hs_base(BatchScratch sc, uint32_t ngroups) {
+    __shared__ uint32_t ws[16];
+    __shared__ uint32_t ct[2][16];
+    {
+        uint32_t c = 0, h = 0;
+        for (uint32_t g = threadIdx.x; g < ngroups; g += 1024) {
+            c += sc.hgcnt[2 * g];
+            h += sc.hgcnt[2 * g + 1];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            c += (uint32_t)__shfl_down((int)c, o, 64);
+            h += (uint32_t)__shfl_down((int)h, o, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            ct[0][threadIdx.x >> 6] = c;
+            ct[1][threadIdx.x >> 6] = h;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tc = 0, th = 0;
+            for (int w = 0; w < 16; ++w) {
+                tc += ct[0][w];
+                th += ct[1][w];
+            }
+            sc.counters[8] = tc;
+            sc.counters[9] = th;
+            sc.counters[10] = tc + th;
+        }
+    }
+    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t v[4], s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t i = threadIdx.x * 4 + k;
+        v[k] = i < nhot ? sc.hot_tot[i] : 0u;
+        s += v[k];
+    }
+    uint32_t x = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) ws[wave] = x;
+    __syncthreads();
+    uint32_t pre = x - s;
+    for (int w = 0; w < wave; ++w) pre += ws[w];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t i = threadIdx.x * 4 + k;
+        if (i < nhot) sc.hot_base[i] = pre;
+        pre += v[k];
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_hs_down(BatchScratch sc, uint32_t ntiles) {
+    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
+    const uint32_t hid = blockIdx.y * kThreads + threadIdx.x;
+    if (hid >= nhot) return;
+    const uint32_t t0 = blockIdx.x * kHotGroup;
+    uint32_t v[kHotGroup];
+#pragma unroll
+    for (int k = 0; k < kHotGroup; ++k) v[k] = t0 + k < ntiles ? sc.hcnt[(size_t)(t0 + k) * kHot + hid] : 0u;
+    uint32_t run = sc.hgsum[(size_t)blockIdx.x * kHot + hid] + sc.hot_base[hid];
+#pragma unroll
+    for (int k = 0; k < kHotGroup; ++k) {
+        if (t0 + k < ntiles) sc.hpre[(size_t)(t0 + k) * kHot + hid] = run;
+        run += v[k];
+    }
+}
+
+// Hot elements to their rule segment in the hot region (after the cold elements) of `dst`.  The
+// tile's row of segment positions is staged in LDS (one batch of loads per thread); each thread
+// keeps kHotIlp elements in flight.  Wave segment w of the tile holds tile_nh[4 t + w] hot
+// elements at its end (descending addresses = arrival order).
+constexpr int kHotIlp = 4;
+constexpr int kHotPer = kHot / kThreads;  // LDS row entries per thread
+
+__device__ __forceinline__ void hot_row_to_lds(const uint32_t *__restrict__ row, uint32_t add, uint32_t nhot,
+                                               uint32_t *lds) {
+    uint32_t v[kHotPer];
+#pragma unroll
+    for (int k = 0; k < kHotPer; ++k) {
+        const uint32_t i = k * kThreads + threadIdx.x;
+        v[k] = i < nhot ? row[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kHotPer; ++k) lds[k * kThreads + threadIdx.x] = v[k] + add;
+}
+
+__device__ __forceinline__ uint32_t hot_tile_total(const BatchScratch &sc, uint32_t tile, uint32_t (&nw)[kClsWaves]) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < kClsWaves; ++w) {
+        nw[w] = sc.tile_nh[tile * kClsWaves + w];
+        t += nw[w];
+    }
+    return t;
+}
+
+__global__ __launch_bounds__(kThreads) void k_hot_scatter(BatchScratch sc, uint64_t *__restrict__ dst) {
+    __shared__ uint32_t base[kHot];
+    const uint32_t tile = blockIdx.x, tbase = tile * kTileElems;
+    uint32_t nw[kClsWaves];
+    if (!hot_tile_total(sc, tile, nw)) return;
+    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
+    const uint32_t nc = sc.counters[8], lim = nc + sc.counters[9];
+    hot_row_to_lds(sc.hpre + (size_t)tile * kHot, nc, nhot, base);
+    __syncthreads();
+#pragma unroll 1
+    for (int w = 0; w < kClsWaves; ++w) {
+        const uint64_t *src = sc.el_tile + tbase + (w + 1) * (kClsRounds * 64) - 1;
+        uint64_t x[kHotIlp];
+#pragma unroll
+        for (int u = 0; u < kHotIlp; ++u) {
+            const uint32_t k = u * kThreads + threadIdx.x;
+            x[u] = k < nw[w] ? *(src - k) : ~0ull;
+        }
+        uint32_t sl[kHotIlp];
+#pragma unroll
+        for (int u = 0; u < kHotIlp; ++u) sl[u] = x[u] != ~0ull ? sc.hot_slot[(uint32_t)(x[u] >> kHidShift)] : 0u;
+#pragma unroll
+        for (int u = 0; u < kHotIlp; ++u) {
+            if (x[u] == ~0ull) continue;
+            const uint32_t hid = (uint32_t)(x[u] >> kHidShift);
+            const uint32_t e = base[hid] + (uint32_t)((x[u] >> kRankShift) & 0xFFFu);
+            if (e < lim) dst[e] = (x[u] & kLow40) | ((uint64_t)sl[u] << kSlotShift);
+        }
+    }
+}
+
+// TokenResults of the tile's hot requests, in input order, from the run records of their rule.
+__global__ __launch_bounds__(kThreads) void k_hot_results(BatchScratch sc, uint64_t *__restrict__ out) {
+    __shared__ uint32_t base[kHot];
+    __shared__ uint32_t frun[kHot];
+    const uint32_t tile = blockIdx.x, tbase = tile * kTileElems;
+    uint32_t nw[kClsWaves];
+    if (!hot_tile_total(sc, tile, nw)) return;
+    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
+    const uint32_t nc = sc.counters[8], nruns = sc.counters[1];
+    hot_row_to_lds(sc.hpre + (size_t)tile * kHot, nc, nhot, base);
+    hot_row_to_lds(sc.hot_first_run, 0, nhot, frun);
+    __syncthreads();
+#pragma unroll 1
+    for (int w = 0; w < kClsWaves; ++w) {
+        const uint64_t *src = sc.el_tile + tbase + (w + 1) * (kClsRounds * 64) - 1;
+        uint64_t x[kHotIlp];
+#pragma unroll
+        for (int u = 0; u < kHotIlp; ++u) {
+            const uint32_t k = u * kThreads + threadIdx.x;
+            x[u] = k < nw[w] ? *(src - k) : ~0ull;
+        }
+        uint32_t e[kHotIlp], r[kHotIlp];
+#pragma unroll
+        for (int u = 0; u < kHotIlp; ++u) {
+            const uint32_t hid = (uint32_t)(x[u] >> kHidShift) & (kHot - 1);
+            e[u] = base[hid] + (uint32_t)((x[u] >> kRankShift) & 0xFFFu);
+            r[u] = x[u] != ~0ull ? frun[hid] : nruns;
+        }
+        // the rule's run holding e: usually its first or second run (a batch spans a few buckets)
+        uint32_t nx[kHotIlp];
+#pragma unroll
+        for (int u = 0; u < kHotIlp; ++u) nx[u] = r[u] + 1 < nruns ? sc.run_start[r[u] + 1] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int u = 0; u < kHotIlp; ++u) {
+            while (nx[u] <= e[u]) {
+                ++r[u];
+                nx[u] = r[u] + 1 < nruns ? sc.run_start[r[u] + 1] : 0xFFFFFFFFu;
+            }
+        }
+        RunOut ro[kHotIlp];
+        uint32_t rs[kHotIlp];
+#pragma unroll
+        for (int u = 0; u < kHotIlp; ++u) {
+            if (r[u] < nruns) {
+                ro[u] = sc.run_out[r[u]];
+                rs[u] = sc.run_start[r[u]];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kHotIlp; ++u) {
+            if (r[u] >= nruns || ro[u].mode != RUN_FAST) continue;  // replayed: k_flows_slow wrote it
+            const uint32_t local = e[u] - rs[u];
+            const int32_t a = el_acq(x[u]);
+            uint64_t res;
+            if (local < ro[u].f) {
+                const int64_t sum = ro[u].s0 + (int64_t)local * a;
+                res = pack_result(TRS_OK, j_d2i(ro[u].thr - (double)sum / ro[u].isec - (double)a), 0);
+            } else if (el_prio(x[u])) {
+                // prioritized requests of the run before this one: lower bound of e in the run's plist
+                const uint32_t p0 = sc.run_p0[r[u]];
+                uint32_t lo = 0, hi = sc.run_cp[r[u]];
+                while (lo < hi) {
+                    const uint32_t m = (lo + hi) >> 1;
+                    if (sc.plist[p0 + m] < e[u]) lo = m + 1;
+                    else hi = m;
+                }
+                res = lo - ro[u].cpf < ro[u].cw ? pack_result(TRS_SHOULD_WAIT, 0, (int32_t)ro[u].wait)
+                                                : pack_result(TRS_BLOCKED, 0, 0);
+            } else {
+                res = pack_result(TRS_BLOCKED, 0, 0);
+            }
+            out[el_idx(x[u])] = res;
+        }
+    }
+}
+
+// ---- next batch's hot set: rules with at least T requests in this batch, T the smallest power of
+// two (>= hot_min) that admits at most kHot rules.
+__device__ __forceinline__ uint32_t flow_count(const BatchScratch &sc, uint32_t fl, uint32_t nflows,
+                                               uint32_t nvalid) {
+    const uint32_t e0 = sc.run_start[sc.flow_first_run[fl]];
+    const uint32_t e1 = fl + 1 < nflows ? sc.run_start[sc.flow_first_run[fl + 1]] : nvalid;
+    return e1 - e0;
+}
+
+__global__ __launch_bounds__(kThreads) void k_hot_hist(BatchScratch sc) {
+    __shared__ uint32_t bins[32];
+    if (threadIdx.x < 32) bins[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t nflows = sc.counters[2], nvalid = sc.counters[0];
+    for (uint32_t fl = blockIdx.x * kThreads + threadIdx.x; fl < nflows; fl += gridDim.x * kThreads) {
+        const uint32_t c = flow_count(sc, fl, nflows, nvalid);
+        if (c) atomicAdd(&bins[31 - __clz(c)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 32 && bins[threadIdx.x]) atomicAdd(&sc.hot_ctl[8 + threadIdx.x], bins[threadIdx.x]);
+}
+
+__device__ __forceinline__ void hot_fid_set(const ClusterState &st, uint32_t slot, uint16_t v) {
+    if (!st.dense_n) return;
+    const int64_t f = st.slot_fid[slot];
+    if (f >= 1 && f <= (int64_t)st.dense_n) st.hot_fid[f - 1] = v;
+}
+
+__global__ __launch_bounds__(kThreads) void k_hot_clear(ClusterState st, BatchScratch sc) {
+    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
+    const uint32_t hid = blockIdx.x * kThreads + threadIdx.x;
+    if (hid < nhot) {
+        const uint32_t slot = sc.hot_slot[hid];
+        sc.hot_of[slot] = kColdId;
+        hot_fid_set(st, slot, kColdId);
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_hot_pick(ClusterState st, BatchScratch sc, uint32_t hot_min) {
+    __shared__ uint32_t thr;
+    if (threadIdx.x == 0) {
+        uint32_t cum = 0, t = 0xFFFFFFFFu;
+        for (int b = 31; b >= 0; --b) {
+            cum += sc.hot_ctl[8 + b];
+            if (cum > (uint32_t)kHot) break;
+            t = 1u << b;
+        }
+        thr = max(t, max(hot_min, 1u));
+    }
+    __syncthreads();
+    const uint32_t nflows = sc.counters[2], nvalid = sc.counters[0];
+    for (uint32_t fl = blockIdx.x * kThreads + threadIdx.x; fl < nflows; fl += gridDim.x * kThreads) {
+        if (flow_count(sc, fl, nflows, nvalid) < thr) continue;
+        const uint32_t hid = atomicAdd(&sc.hot_ctl[1], 1u);
+        if (hid < (uint32_t)kHot) {
+            const uint32_t slot = sc.run_slot[sc.flow_first_run[fl]];
+            sc.hot_slot[hid] = slot;
+            sc.hot_of[slot] = (uint16_t)hid;
+            hot_fid_set(st, slot, (uint16_t)hid);
+        }
+    }
+}
+
+__global__ void k_hot_fin(BatchScratch sc) {
+    if (threadIdx.x == 0) sc.hot_ctl[0] = min(sc.hot_ctl[1], (uint32_t)kHot);
+    if (threadIdx.x == 0) sc.hot_ctl[1] = 0;
+    if (threadIdx.x < 32) sc.hot_ctl[8 + threadIdx.x] = 0;
+}
+
+__global__ void k_hot_reset(ClusterState st, BatchScratch sc, uint32_t nslots_cap) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nslots_cap; i += gridDim.x * blockDim.x)
+        sc.hot_of[i] = kColdId;
+    if (st.hot_fid)
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < st.dense_n; i += gridDim.x * blockDim.x)
+            st.hot_fid[i] = kColdId;
+    if (blockIdx.x == 0 && threadIdx.x < 64) sc.hot_ctl[threadIdx.x] = 0;
 }
 
 __global__ void k_metric_sums(ClusterState st, uint32_t s, int64_t now, int64_t *out7) {
@@ -1529,6 +2071,14 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += 2 * align_up(hist * 4) + align_up(scan_partials_needed(hist) * 4 + 64);
     b += align_up(scan_partials_needed(cap) * 4 + 64);
     b += align_up(kRadixGhistWords * 4) + align_up(64);  // look-back digit totals, error flag
+    // hot/cold split
+    const size_t ngroups = (ntiles + kHotGroup - 1) / kHotGroup;
+    b += align_up((size_t)nslots_cap * 2) + align_up(kHot * 4) + align_up(64 * 4);  // hot_of, hot_slot, hot_ctl
+    b += align_up(ntiles * kTileElems * 8);                                       // el_tile
+    b += 2 * align_up(ntiles * kClsWaves * 4);                                    // tile_nc / tile_nh
+    b += align_up(ntiles * kHot * 2) + align_up(ntiles * kHot * 4);               // hcnt, hpre
+    b += align_up(ngroups * kHot * 4) + 3 * align_up(kHot * 4);                   // hgsum, tot/base/first_run
+    b += align_up(ngroups * 2 * 4);                                               // hgcnt
     return b;
 }
 
@@ -1565,7 +2115,71 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.lim_partial = (uint32_t *)take(scan_partials_needed(cap) * 4 + 64);
     sc.radix.ghist = (uint32_t *)take(kRadixGhistWords * 4);
     sc.radix.err = (uint32_t *)take(64);
+    const size_t ngroups = (ntiles + kHotGroup - 1) / kHotGroup;
+    sc.hot_of = (uint16_t *)take((size_t)nslots_cap * 2);
+    sc.hot_slot = (uint32_t *)take(kHot * 4);
+    sc.hot_ctl = (uint32_t *)take(64 * 4);
+    sc.el_tile = (uint64_t *)take(ntiles * kTileElems * 8);
+    sc.tile_nc = (uint32_t *)take(ntiles * kClsWaves * 4);
+    sc.tile_nh = (uint32_t *)take(ntiles * kClsWaves * 4);
+    sc.hcnt = (uint16_t *)take(ntiles * kHot * 2);
+    sc.hpre = (uint32_t *)take(ntiles * kHot * 4);
+    sc.hgsum = (uint32_t *)take(ngroups * kHot * 4);
+    sc.hot_tot = (uint32_t *)take(kHot * 4);
+    sc.hot_base = (uint32_t *)take(kHot * 4);
+    sc.hot_first_run = (uint32_t *)take(kHot * 4);
+    sc.hgcnt = (uint32_t *)take(ngroups * 2 * 4);
     sc.cap = cap;
+}
+
+void hot_reset(const ClusterState &st, BatchScratch &sc, uint32_t nslots_cap, hipStream_t s) {
+    const uint32_t m = std::max(nslots_cap, st.hot_fid ? st.dense_n : 0u);
+    hipLaunchKernelGGL(k_hot_reset, dim3(std::max<uint32_t>(1, std::min<uint32_t>((m + 255) / 256, 4096))),
+                       dim3(256), 0, s, st, sc, nslots_cap);
+}
+
+// Hot/cold split batch (see the kernels above): classify -> tile scan per hot id -> hot scatter ->
+// radix sort of the cold elements -> runs / flows over [cold sorted | hot segments] -> cold results
+// (scattered) + hot results (input order) -> next batch's hot set.
+static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id,
+                             const int32_t *acquire, const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off,
+                             uint32_t n, int simple, uint64_t *out, hipStream_t s, int bits, int d0,
+                             uint32_t ntiles) {
+    const uint32_t invalid_key = st.nslots;
+    static const int chunk = getenv("SGA_CLS_CHUNK") ? atoi(getenv("SGA_CLS_CHUNK")) : 2;  // A/B knob
+    auto cls = chunk >= 4 ? k_classify_hot<4> : (chunk >= 2 ? k_classify_hot<2> : k_classify_hot<1>);
+    hipLaunchKernelGGL(cls, dim3(ntiles), dim3(kThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n,
+                       simple, out, d0, ntiles, sc.radix.hist);
+    const uint32_t ngroups = (ntiles + kHotGroup - 1) / kHotGroup;
+    hipLaunchKernelGGL(k_hs_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, ntiles);
+    hipLaunchKernelGGL(k_hs_mid, dim3(kHot / kThreads), dim3(kThreads), 0, s, sc, ngroups);
+    hipLaunchKernelGGL(k_hs_base, dim3(1), dim3(1024), 0, s, sc, ngroups);
+    hipLaunchKernelGGL(k_hs_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, ntiles);
+    const int npass = (bits + d0 - 1) / d0;
+    uint64_t *el = (npass & 1) ? sc.el[0] : sc.el[1];  // where radix_sort_u64_tiled leaves the result
+    hipLaunchKernelGGL(k_hot_scatter, dim3(ntiles), dim3(kThreads), 0, s, sc, el);
+    const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + 8, sc.el[0], sc.el[1], n, kSlotShift,
+                                        bits, sc.radix, s, true);
+    (void)np;
+    hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
+                       sc.tile_valid, sc.counters + 10);
+    hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
+                       ntiles, (Agg *)sc.tile_carry, sc.counters);
+    hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key, (const Agg *)sc.tile_carry,
+                       sc, 1);
+    const uint64_t max_flows = n < st.nslots ? n : st.nslots;
+    uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows + kThreads - 1) / kThreads, 16384);
+    if (fb == 0) fb = 1;
+    hipLaunchKernelGGL(k_flows, dim3(fb), dim3(kThreads), 0, s, st, sc, ts_base, simple);
+    hipLaunchKernelGGL(k_flows_slow, dim3(std::min<uint32_t>(fb, 1024)), dim3(kThreads), 0, s, st, sc, acquire, prio,
+                       ts_off, ts_base, el, simple, out);
+    hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, invalid_key, out, 1);
+    hipLaunchKernelGGL(k_hot_results, dim3(ntiles), dim3(kThreads), 0, s, sc, out);
+    const uint32_t sb = std::min<uint32_t>(fb, 1024);
+    hipLaunchKernelGGL(k_hot_hist, dim3(sb), dim3(kThreads), 0, s, sc);
+    hipLaunchKernelGGL(k_hot_clear, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc);
+    hipLaunchKernelGGL(k_hot_pick, dim3(sb), dim3(kThreads), 0, s, st, sc, sc.hot_min);
+    hipLaunchKernelGGL(k_hot_fin, dim3(1), dim3(64), 0, s, sc);
 }
 
 void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
@@ -1589,6 +2203,10 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     auto cls = chunk >= 16 ? k_classify<16>
                            : (chunk >= 8 ? k_classify<8> : (chunk >= 4 ? k_classify<4> : (chunk >= 2 ? k_classify<2> : k_classify<1>)));
     static const int nofuse = getenv("SGA_XP_NOFUSE") ? atoi(getenv("SGA_XP_NOFUSE")) : 0;  // A/B knob
+    if (sc.hot_enabled && !limited && !lb && !nofuse) {
+        decide_batch_hot(st, sc, flow_id, acquire, prio, ts_base, ts_off, n, simple, out, s, bits, d0, ntiles);
+        return;
+    }
     hipLaunchKernelGGL(cls, dim3(ntiles), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n,
                        simple, invalid_key, sc.el[0], out, (limited || nofuse) ? 0 : d0, ntiles, sc.radix.hist,
                        (lb && !limited) ? npass : 0, sc.radix.ghist);
@@ -1596,18 +2214,18 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     const int np = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, !limited && !nofuse);
     const uint64_t *el = sc.el[np & 1];
     hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
-                       sc.tile_valid);
+                       sc.tile_valid, nullptr);
     hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
                        ntiles, (Agg *)sc.tile_carry, sc.counters);
     hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key, (const Agg *)sc.tile_carry,
-                       sc);
+                       sc, 0);
     const uint64_t max_flows = n < st.nslots ? n : st.nslots;
     uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows + kThreads - 1) / kThreads, 16384);
     if (fb == 0) fb = 1;
     hipLaunchKernelGGL(k_flows, dim3(fb), dim3(kThreads), 0, s, st, sc, ts_base, simple);
     hipLaunchKernelGGL(k_flows_slow, dim3(std::min<uint32_t>(fb, 1024)), dim3(kThreads), 0, s, st, sc, acquire, prio,
                        ts_off, ts_base, el, simple, out);
-    hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, invalid_key, out);
+    hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, invalid_key, out, 0);
 }
 
 // ---------------------------------------------------------------- cluster parameter flow (host)
@@ -1650,11 +2268,11 @@ void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
     auto runs = [&](const uint64_t *el, uint32_t invalid_key) {
         SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, s));
         hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
-                           sc.tile_valid);
+                           sc.tile_valid, nullptr);
         hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
                            ntiles, (Agg *)sc.tile_carry, sc.counters);
         hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key,
-                           (const Agg *)sc.tile_carry, sc);
+                           (const Agg *)sc.tile_carry, sc, 0);
     };
     if (nslow < n) {  // key-parallel path (elements keyed by kidx, invalid = kmask + 1)
         const uint32_t kinv = st.kmask + 1;
@@ -1664,7 +2282,7 @@ void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
         const uint64_t *el = sc.el[np & 1];
         runs(el, kinv);
         hipLaunchKernelGGL(k_pflows, dim3(fb), dim3(kThreads), 0, s, st, sc, el, acquire, ts_base, ts_off, out);
-        hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, kinv, out);
+        hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, kinv, out, 0);
     }
     if (nslow > 0) {  // sequential path, one lane per rule
         int bits = 1;

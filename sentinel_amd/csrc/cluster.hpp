@@ -47,6 +47,9 @@ struct ClusterState {
     const HashEntry *htab;   // open-addressing flowId -> (slot, windowLengthInMs)
     const uint32_t *dense;   // when flowIds are dense: dense[flowId - 1] = slot | wcode << 24 (~0u: none)
     const uint32_t *wtab;    // wcode -> windowLengthInMs
+    uint16_t *hot_fid;       // dense flowIds: hot id per flowId (hot_fid[flowId - 1]; kColdId = cold), so the
+                             // hot test is a gather independent of the slot lookup
+    const int64_t *slot_fid; // flowId per slot
     uint32_t dense_n;        // dense table length (0: hash lookup)
     uint32_t hmask;
     uint32_t nslots;
@@ -101,10 +104,34 @@ struct BatchScratch {
     void *tile_carry;
     uint32_t *tile_valid;
     uint32_t *counters;  // [0]=nvalid [1]=nruns [2]=nflows [4]=limited [5]=limiter runs [6]=deferred flows
+                         // [8]=cold elements [9]=hot elements [10]=both (hot/cold split batches)
     uint32_t *lim_partial;  // scan partials over max_batch elements (namespace limiter pre-pass)
     RadixScratch radix;
     size_t cap = 0;
+    // Hot rules (hot/cold split).  The set persists across batches (chosen from
+    // the previous batch's per-rule request counts); it only decides how a request reaches its
+    // rule's arrival-ordered segment, never what is decided.
+    uint16_t *hot_of;         // per rule slot: hot id, kColdId = cold
+    uint32_t *hot_slot;       // per hot id: rule slot
+    uint32_t *hot_ctl;        // [0] hot ids in use  [1] picks of the running selection  [8..40) log2 count bins
+    uint64_t *el_tile;        // classify output, per 1024-request wave segment: cold elements from the front
+                              // (arrival order), hot elements from the back (hot id and in-tile rank in the
+                              // slot field)
+    uint32_t *tile_nc, *tile_nh;  // per tile and wave segment (4 x 1024 slots): cold / hot elements
+    uint16_t *hcnt;           // [tile][kHot]: hot requests of the tile per hot id
+    uint32_t *hpre;           // [tile][kHot]: hot-region position of the tile's first request of the hot id
+    uint32_t *hgsum;          // [tile group][kHot]: group sums, then exclusive prefixes over groups
+    uint32_t *hot_tot, *hot_base, *hot_first_run;  // per hot id
+    uint32_t *hgcnt;          // per tile group: cold, hot element counts
+    int hot_enabled = 0;      // host policy (sga_set_hot_rules); off by default (slower at C3)
+    uint32_t hot_min = 64;    // smallest per-batch request count that makes a rule hot
 };
+
+constexpr int kHot = 4096;          // hot ids (12 bits in the hot element)
+constexpr uint16_t kColdId = 0xFFFF;
+
+// Forget the hot set (rule slots changed or scratch re-carved).
+void hot_reset(const ClusterState &st, BatchScratch &b, uint32_t nslots_cap, hipStream_t stream);
 
 // Requests per batch are indexed with 26 bits inside the packed sort element; rule slots with 24.
 constexpr size_t kMaxBatch = (size_t)1 << 26;

@@ -71,6 +71,7 @@ struct Engine {
     DevBuf<uint32_t> d_ncount;
     DevBuf<uint8_t> d_nodes;
     DevBuf<uint32_t> d_dense;  // dense flowId table (see sync_device)
+    DevBuf<uint16_t> d_hot_fid;  // dense flowIds: hot id per flowId (hot/cold split)
     DevBuf<uint32_t> d_wtab;
     uint32_t dense_n = 0;
     DevBuf<uint32_t> d_fresh;
@@ -331,6 +332,8 @@ struct Engine {
         st.rec = d_rec.p;
         st.htab = d_htab.p;
         st.dense = d_dense.p;
+        st.hot_fid = dense_n ? d_hot_fid.p : nullptr;
+        st.slot_fid = d_slot_fid.p;
         st.wtab = d_wtab.p;
         st.dense_n = dense_n;
         st.hmask = hmask;
@@ -361,6 +364,7 @@ struct Engine {
         d_scratch.alloc(bytes);
         batch_scratch_carve(scratch, d_scratch.p, cfg.max_batch, p2);
         scratch_slots_cap = p2;
+        hot_reset(state(), scratch, p2, stream);
     }
 
     uint32_t alloc_slot() {
@@ -482,6 +486,10 @@ struct Engine {
                     SGA_HIP_CHECK(hipStreamSynchronize(stream));
                     d_dense.alloc(dt.size());
                 }
+                if (d_hot_fid.n < dt.size()) {
+                    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+                    d_hot_fid.alloc(dt.size());
+                }
                 if (d_wtab.n < 256) d_wtab.alloc(256);
                 SGA_HIP_CHECK(hipMemcpyAsync(d_dense.p, dt.data(), dt.size() * 4, hipMemcpyHostToDevice, stream));
                 SGA_HIP_CHECK(hipMemcpyAsync(d_wtab.p, wvals.data(), 256 * 4, hipMemcpyHostToDevice, stream));
@@ -502,6 +510,9 @@ struct Engine {
         }
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
         ensure_scratch();
+        // slots may have been freed or reused: forget the hot-rule set (the next batch re-chooses it)
+        hot_reset(state(), scratch, scratch_slots_cap, stream);
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
     }
 };
 
@@ -697,6 +708,19 @@ int sga_load_cluster_flow_rules(sga_engine *e, const char *ns, const sga_cluster
 
 // GlobalRequestLimiter.initIfAbsent(namespace) (first call: new RequestLimiter(maxAllowedQps))
 // and applyMaxQpsChange (later calls: setQpsAllowed), GlobalRequestLimiter.java:32-80.
+int sga_set_hot_rules(sga_engine *e, int32_t enabled, uint32_t min_requests) {
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        g.scratch.hot_enabled = enabled ? 1 : 0;
+        g.scratch.hot_min = min_requests ? min_requests : 1;
+        if (g.d_scratch.p) {
+            sga::hot_reset(g.state(), g.scratch, g.scratch_slots_cap, g.stream);
+            SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        }
+        return SGA_OK;
+    });
+}
+
 int sga_set_namespace_limit(sga_engine *e, const char *ns, double max_allowed_qps) {
     if (!ns || !*ns || !(max_allowed_qps >= 0)) return SGA_EINVAL;  // AssertUtil.isTrue(qpsAllowed >= 0)
     return guarded(e, [&](Engine &g) {

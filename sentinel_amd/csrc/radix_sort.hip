@@ -455,7 +455,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const uint32_t *__r
 // ranking + LDS-staged scatter kernel as above.
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_rs64_hist(const uint64_t *__restrict__ el, uint32_t n, int shift,
-                                                        uint32_t ntiles, uint32_t *__restrict__ hist) {
+                                                        uint32_t ntiles, uint32_t *__restrict__ hist,
+                                                        const uint32_t *__restrict__ dn) {
+    // dn: element count on the device (a producer that compacts); tiles past it count nothing
     // After the first pass equal keys sit next to each other, so one digit often fills a whole
     // wave: lanes with equal digits are matched by ballots (as in the sweep) and only the first
     // of them adds the group's size -- at most one LDS atomic per distinct digit per wave.
@@ -466,6 +468,7 @@ __global__ __launch_bounds__(kThreads) void k_rs64_hist(const uint64_t *__restri
     const uint32_t tile = blockIdx.x;
     const int lane = threadIdx.x & 63;
     const uint32_t wbase = tile * kTile + (threadIdx.x >> 6) * (kRounds * 64);
+    if (dn) n = min(n, *dn);
     uint64_t key[kRounds];
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
@@ -523,7 +526,12 @@ struct Sweep64Smem {
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_rs64_sweep(const uint64_t *__restrict__ in, uint32_t n, int shift,
                                                          const uint32_t *__restrict__ digit_base,
-                                                         uint64_t *__restrict__ out) {
+                                                         uint64_t *__restrict__ out,
+                                                         const uint32_t *__restrict__ tile_n,
+                                                         const uint32_t *__restrict__ dn) {
+    // tile_n: segmented producer -- wave w of tile t holds tile_n[t * kWaves + w] elements at
+    // in[t * kTile + w * kRounds * 64 ..] (arrival order: segment w before w + 1);
+    // dn: element count on the device.  Either may be null (contiguous input of n elements).
     constexpr int RADIX = 1 << D;
     constexpr int DPT = RADIX >= kThreads ? RADIX / kThreads : 1;
     __shared__ Sweep64Smem<D> sm;
@@ -537,19 +545,29 @@ __global__ __launch_bounds__(kThreads) void k_rs64_sweep(const uint64_t *__restr
     __syncthreads();
     const uint32_t tile = blockIdx.x;
     const uint32_t tbase = tile * kTile;
-    const uint32_t tn = min((uint32_t)kTile, n - tbase);
-    const uint32_t wbase = tbase + wave * (kRounds * 64);
+    if (dn) n = min(n, *dn);
+    const uint32_t wloc = wave * (kRounds * 64);
+    uint32_t tn, wn;
+    if (tile_n) {
+        tn = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) tn += tile_n[tile * kWaves + w];
+        wn = tile_n[tile * kWaves + wave];
+    } else {
+        tn = n > tbase ? min((uint32_t)kTile, n - tbase) : 0u;
+        wn = tn > wloc ? tn - wloc : 0u;
+    }
+    const uint32_t wbase = tbase + wloc;
     uint64_t key[kRounds];
     uint32_t pos[kRounds];
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
         const uint32_t e = wbase + r * 64 + lane;
-        key[r] = e < n ? in[e] : 0ull;
+        key[r] = (uint32_t)(r * 64 + lane) < wn ? in[e] : 0ull;
     }
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
-        const uint32_t e = wbase + r * 64 + lane;
-        const bool valid = e < n;
+        const bool valid = (uint32_t)(r * 64 + lane) < wn;
         const uint32_t d = (uint32_t)(key[r] >> shift) & (RADIX - 1);
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -606,8 +624,7 @@ __global__ __launch_bounds__(kThreads) void k_rs64_sweep(const uint64_t *__restr
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
-        const uint32_t e = wbase + r * 64 + lane;
-        if (e < n) {
+        if ((uint32_t)(r * 64 + lane) < wn) {
             const uint32_t d = (uint32_t)(key[r] >> shift) & (RADIX - 1);
             sm.sel[pos[r] + sm.dstart[d] + sm.wcnt[wave][d]] = key[r];
         }
@@ -892,9 +909,25 @@ int radix64_lookback() {
 
 template <int D>
 static int sort64_passes(uint64_t *a, uint64_t *alt, uint32_t n, int key_shift, int npass, RadixScratch &sc,
-                         hipStream_t s, bool hist0_ready) {
+                         hipStream_t s, bool hist0_ready, const uint64_t *first_src = nullptr,
+                         const uint32_t *tile_n0 = nullptr, const uint32_t *dn = nullptr) {
     constexpr int RADIX = 1 << D;
     const uint32_t nt = (uint32_t)radix64_tiles(n);
+    if (first_src) {
+        // pass 0 reads the producer's tile-compacted buffer, later passes alternate a <-> alt
+        for (int p = 0; p < npass; ++p) {
+            const int shift = key_shift + p * D;
+            const uint64_t *src = p == 0 ? first_src : ((p & 1) ? a : alt);
+            uint64_t *dst = (p & 1) ? alt : a;
+            if (p > 0 || !hist0_ready)
+                hipLaunchKernelGGL((k_rs64_hist<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, nt, sc.hist,
+                                   p == 0 ? nullptr : dn);
+            exclusive_scan_u32(sc.hist, sc.hist_scan, (size_t)RADIX * nt, sc.partial, s);
+            hipLaunchKernelGGL((k_rs64_sweep<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, sc.hist_scan, dst,
+                               p == 0 ? tile_n0 : nullptr, p == 0 ? nullptr : dn);
+        }
+        return npass;
+    }
     uint64_t *src = a, *dst = alt;
     if (radix64_lookback() && sc.ghist) {
         // global digit totals of every pass: counted by the producer into sc.ghist when hist0_ready
@@ -917,9 +950,11 @@ static int sort64_passes(uint64_t *a, uint64_t *alt, uint32_t n, int key_shift, 
     for (int p = 0; p < npass; ++p) {
         const int shift = key_shift + p * D;
         if (p > 0 || !hist0_ready)
-            hipLaunchKernelGGL((k_rs64_hist<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, nt, sc.hist);
+            hipLaunchKernelGGL((k_rs64_hist<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, nt, sc.hist,
+                               nullptr);
         exclusive_scan_u32(sc.hist, sc.hist_scan, (size_t)RADIX * nt, sc.partial, s);
-        hipLaunchKernelGGL((k_rs64_sweep<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, sc.hist_scan, dst);
+        hipLaunchKernelGGL((k_rs64_sweep<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, sc.hist_scan, dst,
+                           nullptr, nullptr);
         uint64_t *t = src;
         src = dst;
         dst = t;
@@ -945,6 +980,32 @@ int radix_sort_u64(uint64_t *a, uint64_t *alt, size_t n, int key_shift, int bits
     case 8: return sort64_passes<8>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
     case 9: return sort64_passes<9>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
     default: return sort64_passes<10>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    }
+}
+
+}  // namespace sga
+
+namespace sga {
+
+int radix_sort_u64_tiled(const uint64_t *src, const uint32_t *tile_n0, const uint32_t *dn, uint64_t *a,
+                         uint64_t *alt, size_t n, int key_shift, int bits, RadixScratch &sc, hipStream_t s,
+                         bool hist0_ready) {
+    if (n == 0 || bits <= 0) return 0;
+    const int d = radix64_digit_bits(bits);
+    const int npass = (bits + d - 1) / d;
+    if (npass > kMaxPasses) return -1;
+    const uint32_t nn = (uint32_t)n;
+    switch (d) {
+    case 1: return sort64_passes<1>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
+    case 2: return sort64_passes<2>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
+    case 3: return sort64_passes<3>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
+    case 4: return sort64_passes<4>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
+    case 5: return sort64_passes<5>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
+    case 6: return sort64_passes<6>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
+    case 7: return sort64_passes<7>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
+    case 8: return sort64_passes<8>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
+    case 9: return sort64_passes<9>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
+    default: return sort64_passes<10>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
     }
 }
 

@@ -47,5 +47,12 @@ int radix64_digit_bits(int bits);
 size_t radix64_tiles(size_t n);
 int radix_sort_u64(uint64_t *a, uint64_t *alt, size_t n, int key_shift, int bits, RadixScratch &sc, hipStream_t s,
                    bool hist0_ready);
+// Same sort, pass 0 reading a segmented producer buffer: each tile is 4 segments of 1024 slots,
+// segment w of tile t holds tile_n0[4 t + w] elements from its start (arrival order);
+// dn = total element count on the device.  `src` is only read.  Pass p
+// writes `a` when p is even, `alt` when odd: the result is in `a` when the pass count is odd.
+int radix_sort_u64_tiled(const uint64_t *src, const uint32_t *tile_n0, const uint32_t *dn, uint64_t *a,
+                         uint64_t *alt, size_t n, int key_shift, int bits, RadixScratch &sc, hipStream_t s,
+                         bool hist0_ready);
 
 }  // namespace sga

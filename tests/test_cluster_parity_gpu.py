@@ -45,8 +45,16 @@ def eng_mod():
     return cluster
 
 
-def make_engine(cluster, **kw):
+HOT_MODES = {"off": dict(hot_rules=False), "on": dict(hot_rules=True, hot_min_requests=64),
+             "all": dict(hot_rules=True, hot_min_requests=1)}
+
+
+def make_engine(cluster, hot="off", **kw):
+    """hot: the engine's hot-rule policy (decisions must not depend on it).  "off" (the default)
+    sorts every request, "on" sends rules with >= 64 requests in the previous batch down the
+    hot/cold split, "all" every rule seen in the previous batch (up to 4096)."""
     kw.setdefault("max_batch", 1 << 20)
+    kw.update(HOT_MODES[hot])
     return cluster.Engine(**kw)
 
 
@@ -132,10 +140,11 @@ def test_request_validation(eng_mod):
     assert r["remaining"][5] == 2
 
 
+@pytest.mark.parametrize("hot", ["off", "on", "all"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
 @pytest.mark.parametrize("mixed", [False, True])
 @pytest.mark.parametrize("ids", ["dense", "sparse"])
-def test_random_traces_bit_exact(eng_mod, seed, mixed, ids):
+def test_random_traces_bit_exact(eng_mod, seed, mixed, ids, hot):
     """Random rules (mixed window geometries, fractional counts), acquire mix (incl. counts
     beyond the packed 7-bit field), 10 % prioritized, bursts: every decision and counter equals
     the oracle.  ids="dense" exercises the direct flowId table, "sparse" the hash probe."""
@@ -147,8 +156,8 @@ def test_random_traces_bit_exact(eng_mod, seed, mixed, ids):
     n = 60_000
     fid = rng.integers(1, nr + 40, size=n)          # some ids without rules
     fid[rng.random(n) < 0.002] = 0                  # BAD_REQUEST
-    hot = rng.random(n) < 0.5
-    fid[hot] = rng.integers(1, 6, size=hot.sum())   # hot rules -> long runs
+    busy = rng.random(n) < 0.5
+    fid[busy] = rng.integers(1, 6, size=busy.sum())  # hot rules -> long runs
     acq = np.where(rng.random(n) < 0.9, 1, rng.integers(1, 6, size=n)) if mixed else np.ones(n, np.int64)
     if mixed:
         acq[rng.random(n) < 0.002] = 300            # beyond the packed acquire field: replayed
@@ -157,10 +166,10 @@ def test_random_traces_bit_exact(eng_mod, seed, mixed, ids):
     prio = (rng.random(n) < 0.1).astype(np.uint8)
     ts = T0 + np.cumsum(rng.integers(0, 3, size=n))
     oh = oracle_cluster({"default": rules})
-    eng = make_engine(c, max_batch=1 << 16)
+    eng = make_engine(c, hot=hot, max_batch=1 << 16)
     engine_rules(c, eng, {"default": rules})
     svc = c.DefaultTokenService(eng)
-    for lo in range(0, n, 20_000):  # several batches continue the same state
+    for lo in range(0, n, 20_000):  # several batches continue the same state (and move the hot set)
         sl = slice(lo, lo + 20_000)
         g = svc.request_tokens(fid[sl], acq[sl], prio[sl], ts[sl])
         o = oracle_replay(oh, fid[sl], acq[sl], prio[sl], ts[sl])
@@ -205,13 +214,14 @@ def test_avg_local_threshold_and_reload(eng_mod):
     eng.close()
 
 
-def test_time_regression_and_gaps(eng_mod):
+@pytest.mark.parametrize("hot", ["on", "all"])
+def test_time_regression_and_gaps(eng_mod, hot):
     """Clock going backwards (detached windows) and long idle gaps."""
     c = eng_mod
     rules = [{"flow_id": 1, "count": 4, "threshold_type": 1, "sample_count": 5, "window_interval_ms": 500},
              {"flow_id": 2, "count": 2, "threshold_type": 1}]
     oh = oracle_cluster({"default": rules})
-    eng = make_engine(c, max_batch=1 << 12)
+    eng = make_engine(c, hot=hot, max_batch=1 << 12)
     engine_rules(c, eng, {"default": rules})
     svc = c.DefaultTokenService(eng)
     ts = np.array([T0, T0 + 10, T0 + 250, T0 + 120, T0 + 130, T0 + 5000, T0 + 4000, T0 + 5001, T0 + 90000,
@@ -219,14 +229,17 @@ def test_time_regression_and_gaps(eng_mod):
     fid = np.where(np.arange(len(ts)) % 3 == 2, 2, 1).astype(np.int64)
     prio = np.array([0, 1] * (len(ts) // 2) + [1] * (len(ts) % 2), dtype=np.uint8)
     acq = np.ones(len(ts), np.int64)
-    g = svc.request_tokens(fid, acq, prio, ts)
-    o = oracle_replay(oh, fid, acq, prio, ts)
-    assert_same(g, o, fid, ts)
+    for rep in range(3):  # the same pattern again, later: batches 2 and 3 run with both rules hot
+        tsr = ts + rep * 200_000
+        g = svc.request_tokens(fid, acq, prio, tsr)
+        o = oracle_replay(oh, fid, acq, prio, tsr)
+        assert_same(g, o, fid, tsr, f"rep {rep}")
     H.lib().orc_cluster_free(oh)
     eng.close()
 
 
-def test_zipf_c3_slice_bit_exact(eng_mod):
+@pytest.mark.parametrize("hot", ["on", "all"])
+def test_zipf_c3_slice_bit_exact(eng_mod, hot):
     """C3 trace slice (100k rules, 2^21 requests, Zipf(1.1), 1 % prioritized)."""
     from sentinel_amd.workload import ClusterTrace
     c = eng_mod
@@ -234,16 +247,16 @@ def test_zipf_c3_slice_bit_exact(eng_mod):
     fid_r, cnt = tr.rules()
     rules = [{"flow_id": int(f), "count": float(x), "threshold_type": 1} for f, x in zip(fid_r, cnt)]
     oh = oracle_cluster({"default": rules})
-    eng = make_engine(c, max_batch=1 << 20, max_rules=1 << 17)
+    eng = make_engine(c, hot=hot, max_batch=1 << 20, max_rules=1 << 17)
     c.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_r, cnt)
     svc = c.DefaultTokenService(eng)
-    for b in range(2):
+    for b in range(3):
         fid, acq, prio, ts = tr.events(b << 20, 1 << 20)
         g = svc.request_tokens(fid, acq, prio, ts)
         o = oracle_replay(oh, fid, acq, prio, ts)
         assert_same(g, o, fid, ts, f"batch {b}")
-    hot = np.unique(fid)[:200]
-    assert_metrics(c, eng, oh, hot, int(ts[-1]))
+    seen = np.unique(fid)[:200]
+    assert_metrics(c, eng, oh, seen, int(ts[-1]))
     H.lib().orc_cluster_free(oh)
     eng.close()
 
@@ -325,4 +338,44 @@ def test_namespace_limiter(eng_mod, seed):
         assert (o[0] == -2).any()
     assert_metrics(c, eng, oh, range(1, 151), int(ts.max()))
     L.orc_cluster_free(oh)
+    eng.close()
+
+
+@pytest.mark.parametrize("hot", ["on", "all"])
+def test_hot_rules_skew_prio_mixed(eng_mod, hot):
+    """Hot-rule path under heavy skew: a few rules carry most requests (runs spanning many tiles and
+    several window buckets), 5 % prioritized with tight thresholds (SHOULD_WAIT inside hot runs),
+    mixed acquire counts on some hot rules (their runs replayed), requests without rules, and a
+    rule reload between batches (the hot set is forgotten and chosen again)."""
+    c = eng_mod
+    rng = np.random.default_rng(11)
+    nr = 6000
+    rules = [{"flow_id": i, "count": float(rng.integers(5, 400)), "threshold_type": 1} for i in range(1, nr + 1)]
+    oh = oracle_cluster({"default": rules})
+    eng = make_engine(c, hot=hot, max_batch=1 << 17)
+    mgr = engine_rules(c, eng, {"default": rules})
+    svc = c.DefaultTokenService(eng)
+    t = T0
+    for b in range(6):
+        n = 100_000
+        z = rng.zipf(1.3, size=n)
+        fid = np.where(z <= nr + 50, z, rng.integers(1, nr + 1, size=n)).astype(np.int64)
+        acq = np.ones(n, np.int64)
+        mixed = (fid % 7 == 3) & (rng.random(n) < 0.3)
+        acq[mixed] = rng.integers(2, 5, size=int(mixed.sum()))
+        prio = (rng.random(n) < 0.05).astype(np.uint8)
+        ts = t + np.sort(rng.integers(0, 700, size=n))
+        t = int(ts[-1]) + int(rng.integers(0, 300))
+        g = svc.request_tokens(fid, acq, prio, ts)
+        o = oracle_replay(oh, fid, acq, prio, ts)
+        assert_same(g, o, fid, ts, f"hot={hot} batch {b}")
+        if b == 3:  # reload: counts change for the first 100 flowIds, metrics kept
+            for r in rules[:100]:
+                r["count"] = float(rng.integers(5, 400))
+            arr = H.cluster_rules_array(rules)
+            H.lib().orc_cluster_load_rules(oh, b"default", arr, len(rules))
+            mgr.load_rule_arrays("default", np.array([r["flow_id"] for r in rules], np.int64),
+                                 np.array([r["count"] for r in rules]))
+    assert_metrics(c, eng, oh, range(1, 60), t)
+    H.lib().orc_cluster_free(oh)
     eng.close()
