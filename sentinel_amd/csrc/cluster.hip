@@ -113,20 +113,27 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
         __syncthreads();
     }
     const uint32_t tbase = blockIdx.x * kTileElems;
-    for (int c = 0; c < kItems; c += kClsChunk) {
-        int64_t fid[kClsChunk];
-        int32_t acq[kClsChunk];
-        uint32_t tso[kClsChunk], pr[kClsChunk];
-        uint32_t hh[kClsChunk];
-        HashEntry e[kClsChunk];
+    // software pipeline: chunk c + 1's request fields load while chunk c's lookups resolve
+    int64_t fid[kClsChunk], nfid[kClsChunk];
+    int32_t acq[kClsChunk], nacq[kClsChunk];
+    uint32_t tso[kClsChunk], pr[kClsChunk], ntso[kClsChunk], npr[kClsChunk];
+    auto load_chunk = [&](int c, int64_t (&f)[kClsChunk], int32_t (&a)[kClsChunk], uint32_t (&t)[kClsChunk],
+                          uint32_t (&p)[kClsChunk]) {
 #pragma unroll
         for (int u = 0; u < kClsChunk; ++u) {
             const uint32_t i = tbase + (c + u) * kThreads + threadIdx.x;
-            fid[u] = i < n ? flow_id[i] : 0;
-            acq[u] = i < n ? acquire[i] : 0;
-            tso[u] = i < n ? ts_off[i] : 0;
-            pr[u] = (i < n && !simple && prio) ? prio[i] : 0;
+            f[u] = i < n ? flow_id[i] : 0;
+            a[u] = i < n ? acquire[i] : 0;
+            t[u] = i < n ? ts_off[i] : 0;
+            p[u] = (i < n && !simple && prio) ? prio[i] : 0;
         }
+    };
+    constexpr bool pipelined = true;
+    if (pipelined) load_chunk(0, fid, acq, tso, pr);
+    for (int c = 0; c < kItems; c += kClsChunk) {
+        uint32_t hh[kClsChunk];
+        HashEntry e[kClsChunk];
+        if (!pipelined) load_chunk(c, fid, acq, tso, pr);
         if (st.dense_n) {  // dense flowIds: one 4-byte load, no probe sequence
             uint32_t d[kClsChunk];
 #pragma unroll
@@ -144,10 +151,13 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
                 e[u] = fid[u] > 0 ? st.htab[hh[u]] : HashEntry{0, 0, 0};
             }
         }
+        if (pipelined && c + kClsChunk < kItems) load_chunk(c + kClsChunk, nfid, nacq, ntso, npr);
 #pragma unroll
         for (int u = 0; u < kClsChunk; ++u) {
             const uint32_t i = tbase + (c + u) * kThreads + threadIdx.x;
-            if (i >= n) continue;
+            const bool valid = i < n;
+            uint32_t key = invalid_key;
+            if (valid) {
             const int64_t f = fid[u];
             const int32_t a = acq[u];
             int8_t status = TRS_OK;
@@ -165,7 +175,6 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
                 }
                 if (he.key != f || f <= 0) status = TRS_NO_RULE_EXISTS;
             }
-            uint32_t key = invalid_key;
             if (status != TRS_OK) {
                 out[i] = pack_result(status, 0, 0);
                 el[i] = (uint64_t)invalid_key << kSlotShift;
@@ -182,11 +191,22 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
                 }
                 el[i] = el_pack(key, bd6, p, a7, i);
             }
+            }
             if (lb_npass > 0) {
-                for (int p = 0; p < lb_npass; ++p)
-                    atomicAdd(&h[((uint32_t)p << hist_d) + ((key >> (p * hist_d)) & ((1u << hist_d) - 1))], 1u);
-            } else if (hist_d > 0) {
+                if (valid)
+                    for (int p = 0; p < lb_npass; ++p)
+                        atomicAdd(&h[((uint32_t)p << hist_d) + ((key >> (p * hist_d)) & ((1u << hist_d) - 1))], 1u);
+            } else if (hist_d > 0 && valid) {
                 atomicAdd(&h[key & ((1u << hist_d) - 1)], 1u);
+            }
+        }
+        if (pipelined) {
+#pragma unroll
+            for (int u = 0; u < kClsChunk; ++u) {
+                fid[u] = nfid[u];
+                acq[u] = nacq[u];
+                tso[u] = ntso[u];
+                pr[u] = npr[u];
             }
         }
     }
