@@ -895,36 +895,57 @@ __global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const 
     RAgg excl{shfl_up_u32(v.nh, 1), shfl_up_u32(v.flag, 1), shfl_up_u32(v.cnt, 1)};
     if (lane == 0) excl = RAgg{0, 0, 0};
     RAgg run = ragg_combine(sc.wave_carry[blockIdx.x * kRunWaves + wave], excl);
-    uint64_t px = first_prev;
-    uint32_t cur_rid = 0xFFFFFFFFu, rstart = 0;
-    RunOut ro;
+    // phase 1 (registers only): run id and prioritized-before count of each element
+    uint32_t rid[kPerThread], pcb[kPerThread];
+    {
+        uint64_t px = first_prev;
 #pragma unroll
-    for (int k = 0; k < kPerThread; ++k) {
-        const uint32_t e = e0 + k;
-        if (e >= nvalid) break;
-        const bool h = e == 0 || el_runkey(x[k]) != el_runkey(px);
-        const uint32_t p = el_prio(x[k]);
-        run = ragg_combine(run, RAgg{h ? 1u : 0u, h ? 1u : 0u, p});
-        px = x[k];
-        const uint32_t rid = run.nh - 1;
-        if (rid != cur_rid) {
-            cur_rid = rid;
-            ro = sc.run_out[rid];
-            rstart = sc.run_start[rid];
+        for (int k = 0; k < kPerThread; ++k) {
+            const uint32_t e = e0 + k;
+            const bool h = e < nvalid && (e == 0 || el_runkey(x[k]) != el_runkey(px));
+            const uint32_t p = e < nvalid ? el_prio(x[k]) : 0u;
+            run = ragg_combine(run, RAgg{h ? 1u : 0u, h ? 1u : 0u, p});
+            px = x[k];
+            rid[k] = run.nh - 1;
+            pcb[k] = run.cnt - p;
         }
-        if (ro.mode != RUN_FAST) continue;
-        const uint32_t local = e - rstart;
-        const int32_t a = el_acq(x[k]);
-        uint64_t res;
-        if (local < ro.f) {
-            const int64_t sum = ro.s0 + (int64_t)local * a;
-            res = pack_result(TRS_OK, j_d2i(ro.thr - (double)sum / ro.isec - (double)a), 0);
-        } else if (p && (run.cnt - p) - ro.cpf < ro.cw) {
-            res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)ro.wait);
-        } else {
-            res = pack_result(TRS_BLOCKED, 0, 0);
+    }
+    // phase 2: the run records of kResIlp elements are loaded together (one load per run change,
+    // issued before any is used), then the results are computed and stored
+    constexpr int kResIlp = 4;
+#pragma unroll
+    for (int k0 = 0; k0 < kPerThread; k0 += kResIlp) {
+        RunOut ro[kResIlp];
+        uint32_t rs[kResIlp];
+#pragma unroll
+        for (int u = 0; u < kResIlp; ++u) {
+            const int k = k0 + u;
+            if (e0 + k < nvalid && (u == 0 || rid[k] != rid[k - 1])) {
+                ro[u] = sc.run_out[rid[k]];
+                rs[u] = sc.run_start[rid[k]];
+            } else if (u > 0) {
+                ro[u] = ro[u - 1];
+                rs[u] = rs[u - 1];
+            }
         }
-        out[el_idx(x[k])] = res;
+#pragma unroll
+        for (int u = 0; u < kResIlp; ++u) {
+            const int k = k0 + u;
+            const uint32_t e = e0 + k;
+            if (e >= nvalid || ro[u].mode != RUN_FAST) continue;
+            const uint32_t local = e - rs[u];
+            const int32_t a = el_acq(x[k]);
+            uint64_t res;
+            if (local < ro[u].f) {
+                const int64_t sum = ro[u].s0 + (int64_t)local * a;
+                res = pack_result(TRS_OK, j_d2i(ro[u].thr - (double)sum / ro[u].isec - (double)a), 0);
+            } else if (el_prio(x[k]) && pcb[k] - ro[u].cpf < ro[u].cw) {
+                res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)ro[u].wait);
+            } else {
+                res = pack_result(TRS_BLOCKED, 0, 0);
+            }
+            out[el_idx(x[k])] = res;
+        }
     }
 }
 
