@@ -912,7 +912,7 @@ __global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const 
     }
     // phase 2: the run records of kResIlp elements are loaded together (one load per run change,
     // issued before any is used), then the results are computed and stored
-    constexpr int kResIlp = 4;
+    constexpr int kResIlp = 8;
 #pragma unroll
     for (int k0 = 0; k0 < kPerThread; k0 += kResIlp) {
         RunOut ro[kResIlp];
