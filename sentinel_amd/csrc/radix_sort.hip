@@ -448,6 +448,49 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const uint32_t *__r
 }
 
 
+// Per-digit prefix over tiles (one workgroup per digit row of the digit-major histogram) and the
+// row total; the sweep adds the digit offsets (scan of the totals).  One launch instead of the
+// three of a flat scan over digits x tiles.
+constexpr int kRowItems = 8;
+__global__ __launch_bounds__(kThreads) void k_row_scan(const uint32_t *__restrict__ hist, uint32_t nt,
+                                                       uint32_t *__restrict__ hist_scan, uint32_t *__restrict__ tot) {
+    __shared__ uint32_t ws[kWaves];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t *row = hist + (size_t)blockIdx.x * nt;
+    uint32_t *orow = hist_scan + (size_t)blockIdx.x * nt;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nt; base += kThreads * kRowItems) {
+        const uint32_t i0 = base + threadIdx.x * kRowItems;
+        uint32_t v[kRowItems], s = 0;
+#pragma unroll
+        for (int k = 0; k < kRowItems; ++k) {
+            v[k] = i0 + k < nt ? row[i0 + k] : 0u;
+            s += v[k];
+        }
+        uint32_t x = s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) ws[wave] = x;
+        __syncthreads();
+        uint32_t pre = carry + x - s, total = 0;
+        for (int w = 0; w < kWaves; ++w) {
+            if (w < wave) pre += ws[w];
+            total += ws[w];
+        }
+#pragma unroll
+        for (int k = 0; k < kRowItems; ++k) {
+            if (i0 + k < nt) orow[i0 + k] = pre;
+            pre += v[k];
+        }
+        carry += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tot[blockIdx.x] = carry;
+}
+
 // ---- u64 elements with an embedded key (kernel K0 of the cluster path) -----
 // The element carries everything the later stages need (rule slot, window-bucket delta,
 // prioritized flag, acquire count, request index), so a pass moves 8 bytes per request.
@@ -528,16 +571,48 @@ __global__ __launch_bounds__(kThreads) void k_rs64_sweep(const uint64_t *__restr
                                                          const uint32_t *__restrict__ digit_base,
                                                          uint64_t *__restrict__ out,
                                                          const uint32_t *__restrict__ tile_n,
-                                                         const uint32_t *__restrict__ dn) {
+                                                         const uint32_t *__restrict__ dn,
+                                                         const uint32_t *__restrict__ digit_tot) {
     // tile_n: segmented producer -- wave w of tile t holds tile_n[t * kWaves + w] elements at
     // in[t * kTile + w * kRounds * 64 ..] (arrival order: segment w before w + 1);
     // dn: element count on the device.  Either may be null (contiguous input of n elements).
+    // digit_tot: per-digit totals when digit_base holds per-digit (row) prefixes over tiles; the
+    // digit offsets are then scanned here.  Null: digit_base is the full digit-major scan.
     constexpr int RADIX = 1 << D;
     constexpr int DPT = RADIX >= kThreads ? RADIX / kThreads : 1;
     __shared__ Sweep64Smem<D> sm;
     __shared__ uint32_t ws[kWaves];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
+    uint32_t dexc[DPT];
+    if (digit_tot) {
+        __shared__ uint32_t ws2[kWaves];
+        uint32_t v[DPT], s = 0;
+#pragma unroll
+        for (int k = 0; k < DPT; ++k) {
+            const int d = threadIdx.x * DPT + k;
+            v[k] = d < RADIX ? digit_tot[d] : 0u;
+            s += v[k];
+        }
+        uint32_t x = s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) ws2[wave] = x;
+        __syncthreads();
+        uint32_t pre = x - s;
+        for (int w = 0; w < wave; ++w) pre += ws2[w];
+#pragma unroll
+        for (int k = 0; k < DPT; ++k) {
+            dexc[k] = pre;
+            pre += v[k];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < DPT; ++k) dexc[k] = 0;
+    }
     for (int d = threadIdx.x; d < RADIX; d += kThreads) {
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) sm.wcnt[w][d] = 0;
@@ -598,7 +673,7 @@ __global__ __launch_bounds__(kThreads) void k_rs64_sweep(const uint64_t *__restr
                 sm.wcnt[w][d] = sacc;
                 sacc += c;
             }
-            sm.gbase[d] = digit_base[(size_t)d * gridDim.x + tile];
+            sm.gbase[d] = digit_base[(size_t)d * gridDim.x + tile] + dexc[k];
         }
         tot[k] = sacc;
         tsum += sacc;
@@ -922,9 +997,9 @@ static int sort64_passes(uint64_t *a, uint64_t *alt, uint32_t n, int key_shift, 
             if (p > 0 || !hist0_ready)
                 hipLaunchKernelGGL((k_rs64_hist<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, nt, sc.hist,
                                    p == 0 ? nullptr : dn);
-            exclusive_scan_u32(sc.hist, sc.hist_scan, (size_t)RADIX * nt, sc.partial, s);
+            hipLaunchKernelGGL(k_row_scan, dim3(RADIX), dim3(kThreads), 0, s, sc.hist, nt, sc.hist_scan, sc.ghist);
             hipLaunchKernelGGL((k_rs64_sweep<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, sc.hist_scan, dst,
-                               p == 0 ? tile_n0 : nullptr, p == 0 ? nullptr : dn);
+                               p == 0 ? tile_n0 : nullptr, p == 0 ? nullptr : dn, sc.ghist);
         }
         return npass;
     }
@@ -952,9 +1027,9 @@ static int sort64_passes(uint64_t *a, uint64_t *alt, uint32_t n, int key_shift, 
         if (p > 0 || !hist0_ready)
             hipLaunchKernelGGL((k_rs64_hist<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, nt, sc.hist,
                                nullptr);
-        exclusive_scan_u32(sc.hist, sc.hist_scan, (size_t)RADIX * nt, sc.partial, s);
+        hipLaunchKernelGGL(k_row_scan, dim3(RADIX), dim3(kThreads), 0, s, sc.hist, nt, sc.hist_scan, sc.ghist);
         hipLaunchKernelGGL((k_rs64_sweep<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, sc.hist_scan, dst,
-                           nullptr, nullptr);
+                           nullptr, nullptr, sc.ghist);
         uint64_t *t = src;
         src = dst;
         dst = t;

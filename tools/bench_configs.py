@@ -42,6 +42,7 @@ def time_gpu(s, st, chunk, reps=3):
             sl = slice(lo, lo + chunk)
             s.submit(st["kind"][sl], st["resource"][sl], st["ts"][sl], st["acquire"][sl], st["flags"][sl],
                      st["rt"][sl], st["param"][sl])
+            print(f"  chunk @{lo}: {time.perf_counter() - t:.2f} s", file=sys.stderr, flush=True)
         dt = time.perf_counter() - t
         best = dt if best is None else min(best, dt)
     return best

@@ -11,4 +11,4 @@ tail -5 $out/pytest.log
 timeout -k 10 200 python3 bench.py --no-cpu > $out/bench.json || exit 1
 python3 -c "import json;d=json.load(open('$out/bench.json'));print('value %.4g gpu_ms %.3f frac %.4f'%(d['value'],d['roofline']['gpu_ms_per_step'],d['roofline']['frac']))"
 bash tools/prof_bench.sh $tag --no-cpu --steps 5 --warmup 1 || exit 1
-python3 tools/kstats.py gpurun_out/prof_$tag/run_kernel_stats.csv | grep -E 'k_(classify|rs64|scan|runs|flows|results|hs_|hot_)'
+python3 tools/kstats.py gpurun_out/prof_$tag/run_kernel_stats.csv | grep -E 'k_(classify|rs64|scan|row_scan|runs|flows|results|hs_|hot_)'
