@@ -306,7 +306,10 @@ __device__ int8_t rater_can_pass(const Ctx &c, FlowRuleDev &r, int64_t *node, in
 __device__ PEntry *ptab_get(PEntry *tab, uint32_t mask, uint32_t owner, uint64_t value, bool create,
                             uint32_t *overflow) {
     uint32_t h = (uint32_t)splitmix64(value ^ ((uint64_t)owner << 40) ^ 0xA5A5ULL) & mask;
-    for (uint32_t probe = 0; probe <= mask; ++probe) {
+    // the maps stay at most half full (FlowEngine::ensure_maps), so a long probe sequence means a
+    // broken invariant: fail the batch (overflow -> -ENOMEM) instead of walking the whole table
+    const uint32_t max_probe = mask < 4096u ? mask : 4096u;
+    for (uint32_t probe = 0; probe <= max_probe; ++probe) {
         PEntry *e = &tab[h];
         uint32_t o = __hip_atomic_load(&e->owner, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         if (o == 0) {
@@ -1431,6 +1434,42 @@ __global__ void k_clear_ptab(PEntry *t, uint32_t n) {
     if (i < n) t[i] = PEntry{0, 0, 0, kPAbsent, kPAbsent};
 }
 
+// keys held by a map (one atomic per workgroup)
+__global__ void k_count_keys(const PEntry *__restrict__ t, uint32_t n, uint32_t *__restrict__ out) {
+    __shared__ uint32_t ws[kT / 64];
+    uint32_t c = 0;
+    for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) c += t[i].owner != 0 ? 1u : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_down((int)c, o, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t2 = 0;
+        for (int w = 0; w < kT / 64; ++w) t2 += ws[w];
+        if (t2) atomicAdd(out, t2);
+    }
+}
+
+// every key of `old` into the empty table `nt` (same hash as ptab_get; entries keep their counters)
+__global__ void k_rehash(const PEntry *__restrict__ old, uint32_t oldn, PEntry *__restrict__ nt, uint32_t nmask,
+                         uint32_t *overflow) {
+    const uint32_t i = blockIdx.x * kT + threadIdx.x;
+    if (i >= oldn) return;
+    const PEntry e = old[i];
+    if (e.owner == 0) return;
+    uint32_t h = (uint32_t)splitmix64(e.value ^ ((uint64_t)e.owner << 40) ^ 0xA5A5ULL) & nmask;
+    for (uint32_t probe = 0; probe <= nmask; ++probe) {
+        if (atomicCAS(&nt[h].owner, 0u, e.owner) == 0u) {
+            nt[h].value = e.value;
+            nt[h].a = e.a;
+            nt[h].b = e.b;
+            return;
+        }
+        h = (h + 1) & nmask;
+    }
+    atomicOr(overflow, 1u);
+}
+
 }  // namespace
 
 // ======================================================================== host side
@@ -1707,6 +1746,48 @@ int FlowEngine::load_degrade_rules(const sga_degrade_rule *rules, size_t n) {
 
 static size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
+void FlowEngine::grow_map(DevBuf<PEntry> &tab, size_t &ub, size_t add) {
+    if (ub + add <= tab.n / 2) {
+        ub += add;
+        return;
+    }
+    if (!d_keycount.p) d_keycount.alloc(1);
+    SGA_HIP_CHECK(hipMemsetAsync(d_keycount.p, 0, 4, stream));
+    hipLaunchKernelGGL(k_count_keys, dim3((unsigned)std::min<size_t>((tab.n + kT - 1) / kT, 2048)), dim3(kT), 0, stream,
+                       tab.p, (uint32_t)tab.n, d_keycount.p);
+    uint32_t keys = 0;
+    SGA_HIP_CHECK(hipMemcpyAsync(&keys, d_keycount.p, 4, hipMemcpyDeviceToHost, stream));
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    ub = keys;
+    if (ub + add > tab.n / 2) {  // rehash into a table that stays at most half full after this batch
+        size_t nn = tab.n;
+        while (ub + add > nn / 2) nn <<= 1;
+        DevBuf<PEntry> nt;
+        nt.alloc(nn);
+        hipLaunchKernelGGL(k_clear_ptab, dim3((unsigned)((nn + kT - 1) / kT)), dim3(kT), 0, stream, nt.p, (uint32_t)nn);
+        hipLaunchKernelGGL(k_rehash, dim3((unsigned)((tab.n + kT - 1) / kT)), dim3(kT), 0, stream, tab.p,
+                           (uint32_t)tab.n, nt.p, (uint32_t)(nn - 1), d_overflow.p);
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+        std::swap(tab.p, nt.p);
+        std::swap(tab.n, nt.n);
+    }
+    ub += add;
+}
+
+// ParameterMetric maps have no eviction here (parity is unpinned past the reference's
+// CacheMap capacity), so they grow: before a batch of m events the maps get room for every key
+// the batch could add (m per parameter rule of a resource for the rule maps, m for thread counts).
+int FlowEngine::ensure_maps(size_t m) {
+    uint32_t mpr = 0;
+    for (const ResDev &r : h_res) mpr = std::max<uint32_t>(mpr, r.n_prules);
+    if (!mpr) return 0;
+    const size_t limit = (size_t)1 << 31;  // 32-bit map indices
+    if ((pkeys_ub + m * mpr) * 2 > limit || (tkeys_ub + m) * 2 > limit) return SGA_ENOMEM;
+    grow_map(d_ptab, pkeys_ub, m * mpr);
+    grow_map(d_ttab, tkeys_ub, m);
+    return 0;
+}
+
 int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int64_t *ts, const int32_t *acquire,
                        const uint8_t *flags, const int64_t *rt, const uint64_t *param, size_t n, int8_t *decision,
                        int32_t *wait_ms) {
@@ -1791,6 +1872,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         }
         off.resize(m);
         for (size_t i = 0; i < m; ++i) off[i] = (uint32_t)(ts[b + i] - lo);
+        if (const int rc = ensure_maps(m)) return rc;
         SGA_HIP_CHECK(hipMemcpyAsync(d_kind.p, kind + b, m, hipMemcpyHostToDevice, stream));
         SGA_HIP_CHECK(hipMemcpyAsync(d_resid.p, resource + b, m * 4, hipMemcpyHostToDevice, stream));
         SGA_HIP_CHECK(hipMemcpyAsync(d_ts.p, off.data(), m * 4, hipMemcpyHostToDevice, stream));

@@ -125,6 +125,12 @@ struct FlowEngine {
     DevBuf<ResDev> d_res;
     DevBuf<PEntry> d_ptab, d_ttab;
     DevBuf<uint32_t> d_overflow;
+    DevBuf<uint32_t> d_keycount;
+    // upper bounds of the keys held by the parameter / thread-count maps (exact after a count);
+    // the maps are rehashed into twice the room before a batch could fill them past half
+    size_t pkeys_ub = 0, tkeys_ub = 0;
+    int ensure_maps(size_t m);
+    void grow_map(DevBuf<PEntry> &tab, size_t &ub, size_t add);
     DevBuf<uint8_t> d_scratch;
     FlowScratch sc;
     size_t scratch_cap = 0;
