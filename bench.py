@@ -61,6 +61,8 @@ def main():
     import torch.distributed as dist
     if world > 1:
         dist.init_process_group("gloo")
+    if os.environ.get("SGA_BENCH_ONE_DEVICE") == "1":
+        local = 0  # rehearsal of the N-rank path on a one-GPU box (every rank on device 0)
     torch.cuda.set_device(local)
 
     from sentinel_amd import _lib, cluster
