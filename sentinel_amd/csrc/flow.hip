@@ -41,6 +41,8 @@ enum : uint8_t { RUN_FAST = 0, RUN_DONE = 1 };
 struct Ctx {
     FlowState st;
     int64_t max_rt;  // csp.sentinel.statistic.max.rt
+    PEntry *pentry;  // k_lheavy: the current event's entry of the resource's only parameter rule, an
+                     // LDS copy of the map entry (null: look the entry up in the map)
 };
 
 // ------------------------------------------------------------------ MetricBucket windows
@@ -355,7 +357,7 @@ __device__ bool param_pass(const Ctx &c, const ParamRuleDev &p, uint64_t v, int 
         int64_t token_count = j_d2l(p.count);
         if (hot_lookup(c, p, v, &hot)) token_count = hot;
         if (token_count == 0) return false;
-        PEntry *e = ptab_get(c.st.ptab, c.st.pmask, p.id + 1, v, true, c.st.overflow);
+        PEntry *e = c.pentry ? c.pentry : ptab_get(c.st.ptab, c.st.pmask, p.id + 1, v, true, c.st.overflow);
         if (!e) return false;
         if (p.behavior == 2) {  // throttle, ParamFlowChecker.java:224-281
             const int64_t cost = j_round(1.0 * 1000 * (double)acquire * (double)p.duration / (double)token_count);
@@ -1252,7 +1254,7 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
 // Heavy resources (many events, no closed form): one workgroup each; its node record, rules and
 // breakers are copied to LDS, lane 0 replays every event in order against the LDS copy (an LDS
 // round trip instead of a global one per state access), and the state is written back.
-constexpr int kHeavyRules = 16, kHeavyCbs = 16, kHeavyChunk = 512;
+constexpr int kHeavyRules = 16, kHeavyCbs = 16, kHeavyChunk = 512, kHeavySlots = 1024;
 __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, FlowScratch sc,
                                                const Payload *__restrict__ pay, int64_t ts_base,
                                                const int64_t *__restrict__ rt_in,
@@ -1266,7 +1268,14 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
     __shared__ uint64_t qpv[kHeavyChunk];
     __shared__ int8_t qd[kHeavyChunk];
     __shared__ int32_t qw[kHeavyChunk];
-    const Ctx c{st, max_rt};
+    // parameter-map entries of the chunk (resources with one token-bucket / throttle parameter rule):
+    // resolved by all lanes in parallel, deduplicated into LDS copies, replayed by lane 0 without a
+    // global access per event, written back once per chunk
+    __shared__ PEntry lent[kHeavySlots];
+    __shared__ uint32_t lkey[kHeavySlots];  // map index + 1 (0 = free)
+    __shared__ uint16_t qslot[kHeavyChunk];
+    const Ctx c{st, max_rt, nullptr};
+    for (int k = threadIdx.x; k < kHeavySlots; k += 64) lkey[k] = 0;
     const uint32_t nheavy = sc.counters[8], nflows = sc.counters[2], nruns = sc.counters[1];
     for (uint32_t h = blockIdx.x; h < nheavy; h += gridDim.x) {
         const uint32_t fl = sc.heavy[h];
@@ -1285,6 +1294,9 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
         // events in chunks: the 64 lanes stage payloads, RTs and parameters into LDS, lane 0 replays
         // the chunk from LDS, then the lanes store its decisions
         const ResMem m{lnode, lr ? lrules : g.rules, lc ? lcbs : g.cbs};
+        // one parameter rule with a map (QPS grade): its entries go through the LDS cache
+        const ParamRuleDev *cache_p =
+            (R.n_prules == 1 && st.prules[R.prule_off].grade == 1) ? &st.prules[R.prule_off] : nullptr;
         const uint32_t jb = sc.run_start[r0], je = sc.run_end[r1 - 1];
         for (uint32_t base = jb; base < je; base += kHeavyChunk) {
             const uint32_t cnt = min((uint32_t)kHeavyChunk, je - base);
@@ -1295,8 +1307,35 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                 qrt[k] = (q.idx & F_EXIT) ? rt_in[idx] : 0;
                 qpv[k] = (q.idx & F_PARAM) ? param_in[idx] : 0;
             }
+            if (cache_p) {
+                // an entry exists for every event that may reach the rule's map (creating one early is
+                // invisible: a fresh entry is the reference's "not seen yet")
+                for (uint32_t k = threadIdx.x; k < cnt; k += 64) {
+                    const Payload q = pay[base + k];
+                    uint16_t sl = 0xFFFF;
+                    if ((q.idx & F_PARAM) && !(q.idx & F_EXIT)) {
+                        PEntry *e = ptab_get(st.ptab, st.pmask, cache_p->id + 1, param_in[q.idx & F_IDX], true,
+                                             st.overflow);
+                        if (e) {
+                            const uint32_t gi = (uint32_t)(e - st.ptab);
+                            uint32_t h = (uint32_t)splitmix64(gi) & (kHeavySlots - 1);
+                            for (int probe = 0; probe < kHeavySlots; ++probe) {
+                                const uint32_t old = atomicCAS(&lkey[h], 0u, gi + 1);
+                                if (old == 0u) lent[h] = *e;  // this lane claimed the slot: copy the entry
+                                if (old == 0u || old == gi + 1) {
+                                    sl = (uint16_t)h;
+                                    break;
+                                }
+                                h = (h + 1) & (kHeavySlots - 1);
+                            }
+                        }
+                    }
+                    qslot[k] = sl;
+                }
+            }
             __syncthreads();
             if (threadIdx.x == 0) {
+                Ctx cc = c;
                 for (uint32_t k = 0; k < cnt; ++k) {
                     const Payload q = qpay[k];
                     const int64_t t = ts_base + (int64_t)q.ts_off;
@@ -1306,13 +1345,24 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                                    qpv[k]);
                     } else {
                         int64_t w = 0;
-                        qd[k] = chain_entry(c, res, m, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
+                        cc.pentry = (cache_p && qslot[k] != 0xFFFF) ? &lent[qslot[k]] : nullptr;
+                        qd[k] = chain_entry(cc, res, m, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
                                             hp, qpv[k], &w);
                         qw[k] = (int32_t)w;
                     }
                 }
             }
             __syncthreads();
+            if (cache_p) {  // write the chunk's entries back, free the slots
+                for (int k = threadIdx.x; k < kHeavySlots; k += 64) {
+                    if (lkey[k]) {
+                        PEntry *e = st.ptab + (lkey[k] - 1);
+                        e->a = lent[k].a;
+                        e->b = lent[k].b;
+                        lkey[k] = 0;
+                    }
+                }
+            }
             for (uint32_t k = threadIdx.x; k < cnt; k += 64) {
                 const Payload q = qpay[k];
                 if (!(q.idx & F_EXIT)) {
