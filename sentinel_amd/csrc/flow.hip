@@ -43,6 +43,8 @@ struct Ctx {
     int64_t max_rt;  // csp.sentinel.statistic.max.rt
     PEntry *pentry;  // k_lheavy: the current event's entry of the resource's only parameter rule, an
                      // LDS copy of the map entry (null: look the entry up in the map)
+    int8_t pre_param;   // k_lheavy: that rule's check already decided by the value's lane (1 pass, 2 block)
+    int64_t pre_wait;   // its wait
 };
 
 // ------------------------------------------------------------------ MetricBucket windows
@@ -305,6 +307,11 @@ __device__ int8_t rater_can_pass(const Ctx &c, FlowRuleDev &r, int64_t *node, in
 }
 
 // ------------------------------------------------------------------ parameter maps
+// Concurrency contract: the entries of one owner (a parameter rule, or a resource for thread
+// counts) are touched by one lane at a time (k_lflows, k_lseq, lane 0 of k_lheavy) or through
+// k_lheavy's dedupe / find / insert phases.  Lanes of other owners only need a slot's owner to skip
+// it, and the claiming CAS publishes the owner itself, so no fence is needed.  (An agent-scope
+// release per insert writes back the XCD's L2 and made C4's 10M-value maps crawl.)
 __device__ PEntry *ptab_get(PEntry *tab, uint32_t mask, uint32_t owner, uint64_t value, bool create,
                             uint32_t *overflow) {
     uint32_t h = (uint32_t)splitmix64(value ^ ((uint64_t)owner << 40) ^ 0xA5A5ULL) & mask;
@@ -313,23 +320,40 @@ __device__ PEntry *ptab_get(PEntry *tab, uint32_t mask, uint32_t owner, uint64_t
     const uint32_t max_probe = mask < 4096u ? mask : 4096u;
     for (uint32_t probe = 0; probe <= max_probe; ++probe) {
         PEntry *e = &tab[h];
-        uint32_t o = __hip_atomic_load(&e->owner, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t o = __hip_atomic_load(&e->owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (o == 0) {
             if (!create) return nullptr;
-            // claim: the value is written before the owner becomes visible to other lanes
-            const uint32_t prev = atomicCAS(&e->owner, 0u, 0xFFFFFFFFu);
+            const uint32_t prev = atomicCAS(&e->owner, 0u, owner);  // the claim publishes the owner
             if (prev == 0) {
                 e->value = value;
                 e->a = kPAbsent;
                 e->b = kPAbsent;
-                __threadfence();
-                __hip_atomic_store(&e->owner, owner, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                 return e;
             }
             o = prev;
         }
-        while (o == 0xFFFFFFFFu) o = __hip_atomic_load(&e->owner, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         if (o == owner && e->value == value) return e;
+        h = (h + 1) & mask;
+    }
+    atomicOr(overflow, 1u);
+    return nullptr;
+}
+
+// Insert of a key known to be absent (k_lheavy, after a find): the first free slot of the probe
+// sequence, no value comparisons (so no read of an entry another lane is still filling).
+__device__ PEntry *ptab_insert_absent(PEntry *tab, uint32_t mask, uint32_t owner, uint64_t value,
+                                      uint32_t *overflow) {
+    uint32_t h = (uint32_t)splitmix64(value ^ ((uint64_t)owner << 40) ^ 0xA5A5ULL) & mask;
+    const uint32_t max_probe = mask < 4096u ? mask : 4096u;
+    for (uint32_t probe = 0; probe <= max_probe; ++probe) {
+        PEntry *e = &tab[h];
+        if (__hip_atomic_load(&e->owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+            atomicCAS(&e->owner, 0u, owner) == 0u) {
+            e->value = value;
+            e->a = kPAbsent;
+            e->b = kPAbsent;
+            return e;
+        }
         h = (h + 1) & mask;
     }
     atomicOr(overflow, 1u);
@@ -507,7 +531,8 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
             tc = (te && te->a != kPAbsent) ? te->a : 0;
         }
         int64_t w = 0;
-        if (!param_pass(c, p, param, acquire, t, tc, &w)) {
+        const bool ok = c.pre_param ? (w = c.pre_wait, c.pre_param == 1) : param_pass(c, p, param, acquire, t, tc, &w);
+        if (!ok) {
             node_add(c, node, t, MB_BLOCK, acquire);
             return D_BLOCK_PARAM;
         }
@@ -1272,10 +1297,21 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
     // resolved by all lanes in parallel, deduplicated into LDS copies, replayed by lane 0 without a
     // global access per event, written back once per chunk
     __shared__ PEntry lent[kHeavySlots];
-    __shared__ uint32_t lkey[kHeavySlots];  // map index + 1 (0 = free)
+    __shared__ uint64_t lval[kHeavySlots];  // parameter value of the slot (kLEmpty = free)
+    __shared__ uint32_t lgi[kHeavySlots];   // map index of the slot's entry
     __shared__ uint16_t qslot[kHeavyChunk];
-    const Ctx c{st, max_rt, nullptr};
-    for (int k = threadIdx.x; k < kHeavySlots; k += 64) lkey[k] = 0;
+    // parameter-only resources: the rule check of each event is decided by the lane that owns the
+    // event's value (lane = LDS slot mod 64), every lane walking its values' events in arrival
+    // order (the maps of different values are independent); lane 0 then does the statistics
+    __shared__ int8_t qpre[kHeavyChunk];
+    __shared__ int32_t qpw[kHeavyChunk];
+    __shared__ uint16_t qrank[kHeavyChunk], qord[kHeavyChunk];
+    __shared__ uint32_t lcnt[64];
+    __shared__ int64_t qbq[kHeavyChunk];  // second-window bucket (t / 500) of each event
+    const Ctx c{st, max_rt, nullptr, 0, 0};
+    constexpr uint64_t kLEmpty = ~0ull;  // a value equal to it bypasses the cache (map path)
+    constexpr uint32_t kGiNone = 0xFFFFFFFFu, kGiFail = 0xFFFFFFFEu;
+    for (int k = threadIdx.x; k < kHeavySlots; k += 64) lval[k] = kLEmpty;
     const uint32_t nheavy = sc.counters[8], nflows = sc.counters[2], nruns = sc.counters[1];
     for (uint32_t h = blockIdx.x; h < nheavy; h += gridDim.x) {
         const uint32_t fl = sc.heavy[h];
@@ -1297,6 +1333,10 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
         // one parameter rule with a map (QPS grade): its entries go through the LDS cache
         const ParamRuleDev *cache_p =
             (R.n_prules == 1 && st.prules[R.prule_off].grade == 1) ? &st.prules[R.prule_off] : nullptr;
+        const bool par = cache_p && R.n_rules == 0 && R.n_cbs == 0 && !(R.fast & 2u);
+        int pidx = cache_p ? cache_p->param_idx : 0;  // ParamFlowSlot index with one argument
+        if (pidx < 0) pidx = (-pidx <= 1) ? 1 + pidx : -pidx;
+        const bool p_applies = pidx < 1;
         const uint32_t jb = sc.run_start[r0], je = sc.run_end[r1 - 1];
         for (uint32_t base = jb; base < je; base += kHeavyChunk) {
             const uint32_t cnt = min((uint32_t)kHeavyChunk, je - base);
@@ -1307,34 +1347,169 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                 qrt[k] = (q.idx & F_EXIT) ? rt_in[idx] : 0;
                 qpv[k] = (q.idx & F_PARAM) ? param_in[idx] : 0;
             }
+            __syncthreads();
             if (cache_p) {
-                // an entry exists for every event that may reach the rule's map (creating one early is
-                // invisible: a fresh entry is the reference's "not seen yet")
+                // 1. the chunk's distinct values into LDS slots (64-bit CAS on the value)
                 for (uint32_t k = threadIdx.x; k < cnt; k += 64) {
-                    const Payload q = pay[base + k];
+                    const Payload q = qpay[k];
                     uint16_t sl = 0xFFFF;
-                    if ((q.idx & F_PARAM) && !(q.idx & F_EXIT)) {
-                        PEntry *e = ptab_get(st.ptab, st.pmask, cache_p->id + 1, param_in[q.idx & F_IDX], true,
-                                             st.overflow);
-                        if (e) {
-                            const uint32_t gi = (uint32_t)(e - st.ptab);
-                            uint32_t h = (uint32_t)splitmix64(gi) & (kHeavySlots - 1);
-                            for (int probe = 0; probe < kHeavySlots; ++probe) {
-                                const uint32_t old = atomicCAS(&lkey[h], 0u, gi + 1);
-                                if (old == 0u) lent[h] = *e;  // this lane claimed the slot: copy the entry
-                                if (old == 0u || old == gi + 1) {
-                                    sl = (uint16_t)h;
-                                    break;
-                                }
-                                h = (h + 1) & (kHeavySlots - 1);
+                    if ((q.idx & F_PARAM) && !(q.idx & F_EXIT) && qpv[k] != kLEmpty) {
+                        const uint64_t v = qpv[k];
+                        uint32_t h = (uint32_t)splitmix64(v) & (kHeavySlots - 1);
+                        for (int probe = 0; probe < kHeavySlots; ++probe) {
+                            const uint64_t old = atomicCAS((unsigned long long *)&lval[h], kLEmpty, v);
+                            if (old == kLEmpty) lgi[h] = kGiNone;
+                            if (old == kLEmpty || old == v) {
+                                sl = (uint16_t)h;
+                                break;
                             }
+                            h = (h + 1) & (kHeavySlots - 1);
                         }
                     }
                     qslot[k] = sl;
                 }
+                __syncthreads();
+                // 2. find the values' entries (lookups only: nothing is being filled meanwhile)
+                for (int h = threadIdx.x; h < kHeavySlots; h += 64) {
+                    if (lval[h] == kLEmpty) continue;
+                    PEntry *e = ptab_get(st.ptab, st.pmask, cache_p->id + 1, lval[h], false, st.overflow);
+                    if (e) {
+                        lgi[h] = (uint32_t)(e - st.ptab);
+                        lent[h] = *e;
+                    }
+                }
+                __syncthreads();
+                // 3. insert the absent ones (a fresh entry is the reference's "not seen yet"; creating
+                //    it for an event that never reaches the rule changes nothing)
+                for (int h = threadIdx.x; h < kHeavySlots; h += 64) {
+                    if (lval[h] == kLEmpty || lgi[h] != kGiNone) continue;
+                    PEntry *e = ptab_insert_absent(st.ptab, st.pmask, cache_p->id + 1, lval[h], st.overflow);
+                    lgi[h] = e ? (uint32_t)(e - st.ptab) : kGiFail;
+                    lent[h] = PEntry{lval[h], cache_p->id + 1, 0, kPAbsent, kPAbsent};
+                }
             }
             __syncthreads();
-            if (threadIdx.x == 0) {
+            if (par && p_applies) {
+                const int lane = threadIdx.x;
+                const uint64_t lt = (1ull << lane) - 1ull;
+                lcnt[lane] = 0;
+                // stable ranking of the chunk's rule checks by owner lane (ballot-matched owners)
+                for (uint32_t r0 = 0; r0 < cnt; r0 += 64) {
+                    const uint32_t k = r0 + lane;
+                    bool ok = false;
+                    uint32_t own = 0;
+                    if (k < cnt) {
+                        const Payload q = qpay[k];
+                        ok = !(q.idx & F_EXIT) && (q.idx & F_PARAM) && qslot[k] != 0xFFFF;
+                        own = qslot[k] & 63u;
+                        qpre[k] = 0;
+                        qbq[k] = (ts_base + (int64_t)q.ts_off) / kSecW;
+                    }
+                    uint64_t peers = __ballot(ok);
+#pragma unroll
+                    for (int b = 0; b < 6; ++b) {
+                        const bool bit = (own >> b) & 1u;
+                        const uint64_t bb = __ballot(bit);
+                        peers &= bit ? bb : ~bb;
+                    }
+                    uint32_t before = 0;
+                    if (ok) before = lcnt[own];
+                    __builtin_amdgcn_wave_barrier();
+                    const uint32_t my = (uint32_t)__popcll(peers & lt);
+                    if (ok && my == 0) lcnt[own] = before + (uint32_t)__popcll(peers);
+                    __builtin_amdgcn_wave_barrier();
+                    if (k < cnt) qrank[k] = ok ? (uint16_t)(before + my) : (uint16_t)0xFFFF;
+                }
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t mine = lcnt[lane];
+                uint32_t x = mine;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(x, o, 64);
+                    if (lane >= o) x += y;
+                }
+                const uint32_t start = x - mine;
+                __builtin_amdgcn_wave_barrier();
+                lcnt[lane] = start;
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t k = lane; k < cnt; k += 64)
+                    if (qrank[k] != 0xFFFF) qord[lcnt[qslot[k] & 63u] + qrank[k]] = (uint16_t)k;
+                __builtin_amdgcn_wave_barrier();
+                Ctx cl = c;
+                for (uint32_t i = start; i < start + mine; ++i) {
+                    const uint32_t k = qord[i];
+                    const Payload q = qpay[k];
+                    cl.pentry = &lent[qslot[k]];
+                    int64_t w = 0;
+                    const bool pass = param_pass(cl, *cache_p, qpv[k], (int)(q.acq_prio & 0x7FFFFFFFu),
+                                                 ts_base + (int64_t)q.ts_off, 0, &w);
+                    qpre[k] = pass ? 1 : 2;
+                    qpw[k] = (int32_t)w;
+                }
+            }
+            __syncthreads();
+            bool agg = par && p_applies;
+            if (agg && threadIdx.x == 0)
+                for (uint32_t k = 0; k < cnt && agg; ++k) {
+                    const uint32_t f = qpay[k].idx;
+                    if (!(f & F_EXIT) && (f & F_PARAM) && qslot[k] == 0xFFFF) agg = false;  // map full
+                }
+            if (agg && threadIdx.x == 0) {
+                // StatisticSlot in aggregate: a parameter-only resource's decisions never read its node,
+                // and every event of a 500 ms second-window bucket (nested in one minute bucket) sees the
+                // same window rotation, so each run of consecutive same-bucket events is applied once at
+                // its first event's time (commutative adds, min RT, thread count)
+                int64_t cur = INT64_MIN, tf = 0, pass_acq = 0, block_acq = 0, succ = 0, rt_sum = 0,
+                        rt_min = INT64_MAX, exc = 0, threads = 0;
+                bool any = false;
+                auto flush = [&]() {
+                    if (!any) return;
+                    int64_t *b = sec_current(lnode, tf, max_rt);
+                    int64_t *bm = min_current(lnode, tf, max_rt);
+                    int64_t *bs[2] = {b, bm};
+                    for (int u = 0; u < 2; ++u) {
+                        int64_t *x = bs[u];
+                        if (!x) continue;
+                        x[MB_PASS] += pass_acq;
+                        x[MB_BLOCK] += block_acq;
+                        x[MB_SUCC] += succ;
+                        x[MB_RT] += rt_sum;
+                        if (rt_min < x[MB_MINRT]) x[MB_MINRT] = rt_min;
+                        x[MB_EXC] += exc;
+                    }
+                    lnode[kNodeThreads] += threads;
+                };
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    const Payload q = qpay[k];
+                    if (qbq[k] != cur) {
+                        flush();
+                        cur = qbq[k];
+                        tf = ts_base + (int64_t)q.ts_off;
+                        pass_acq = block_acq = succ = rt_sum = exc = threads = 0;
+                        rt_min = INT64_MAX;
+                        any = true;
+                    }
+                    const int64_t a = (int64_t)(int)(q.acq_prio & 0x7FFFFFFFu);
+                    if (q.idx & F_EXIT) {  // chain_exit without maps or breakers
+                        succ += a;
+                        rt_sum += qrt[k];
+                        if (qrt[k] < rt_min) rt_min = qrt[k];
+                        if (q.idx & F_ERROR) exc += a;
+                        threads -= 1;
+                    } else if (qpre[k] == 2) {  // ParamFlowException
+                        block_acq += a;
+                        qd[k] = D_BLOCK_PARAM;
+                        qw[k] = 0;
+                    } else {  // passed (or the rule does not apply: no argument)
+                        pass_acq += a;
+                        threads += 1;
+                        qd[k] = D_PASS;
+                        qw[k] = qpre[k] == 1 ? qpw[k] : 0;
+                    }
+                }
+                flush();
+            }
+            if (!agg && threadIdx.x == 0) {
                 Ctx cc = c;
                 for (uint32_t k = 0; k < cnt; ++k) {
                     const Payload q = qpay[k];
@@ -1346,6 +1521,8 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     } else {
                         int64_t w = 0;
                         cc.pentry = (cache_p && qslot[k] != 0xFFFF) ? &lent[qslot[k]] : nullptr;
+                        cc.pre_param = (par && p_applies) ? qpre[k] : 0;
+                        cc.pre_wait = (par && p_applies) ? qpw[k] : 0;
                         qd[k] = chain_entry(cc, res, m, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
                                             hp, qpv[k], &w);
                         qw[k] = (int32_t)w;
@@ -1355,11 +1532,13 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
             __syncthreads();
             if (cache_p) {  // write the chunk's entries back, free the slots
                 for (int k = threadIdx.x; k < kHeavySlots; k += 64) {
-                    if (lkey[k]) {
-                        PEntry *e = st.ptab + (lkey[k] - 1);
-                        e->a = lent[k].a;
-                        e->b = lent[k].b;
-                        lkey[k] = 0;
+                    if (lval[k] != kLEmpty) {
+                        if (lgi[k] < kGiFail) {
+                            PEntry *e = st.ptab + lgi[k];
+                            e->a = lent[k].a;
+                            e->b = lent[k].b;
+                        }
+                        lval[k] = kLEmpty;
                     }
                 }
             }

@@ -156,6 +156,23 @@ def test_param_flow(seed):
          params=5, prio_pct=0.05)
 
 
+@pytest.mark.parametrize("seed", [23, 24])
+def test_param_heavy_resources(seed):
+    """Parameter-only resources with thousands of events per batch (k_lheavy): the rule check of
+    each event is decided by the lane owning its value, the statistics by one lane in order.
+    Token buckets (burst, hot items, duration 2 s), throttling, a thread-grade rule beside them
+    (stays on the sequential path), many values, and batches smaller than the stream."""
+    n_res = 5
+    param = [{"resource": 0, "count": 4, "burst_count": 2},
+             {"resource": 1, "count": 3, "duration_in_sec": 2, "hot": {1: 10, 2: 0, 7: 1}},
+             {"resource": 2, "count": 5, "control_behavior": 2, "max_queueing_time_ms": 300},
+             {"resource": 3, "grade": 0, "count": 2},
+             {"resource": 4, "count": 2, "param_idx": -1}]
+    for mb in (1 << 16, 6000):
+        _run(n_res, param=param, n_entries=30000, seed=seed, gap_mean=0.05, acq_max=2, rt_max=20, params=120,
+             max_batch=mb)
+
+
 @pytest.mark.parametrize("seed", [31, 32])
 def test_circuit_breakers(seed):
     n_res = 9
