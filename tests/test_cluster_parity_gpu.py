@@ -379,3 +379,37 @@ def test_hot_rules_skew_prio_mixed(eng_mod, hot):
     assert_metrics(c, eng, oh, range(1, 60), t)
     H.lib().orc_cluster_free(oh)
     eng.close()
+
+
+@pytest.mark.parametrize("hot", ["off", "on"])
+def test_c3_full_size_sampled_rules_bit_exact(eng_mod, hot):
+    """BASELINE C3 at full size: 1M cluster rules, two batches of 2^24 Zipf(1.1) requests.  Rules
+    are independent (GLOBAL thresholds, no namespace limiter), so the requests of a sample of
+    rules -- the 16 hottest ranks and 2000 random flowIds -- replayed alone by the oracle must get
+    the same TokenResults; every other request is checked for the size-independent properties
+    (status domain, waitInMs, non-negative remaining, metric counters of sampled rules)."""
+    from sentinel_amd.workload import ClusterTrace
+    c = eng_mod
+    tr = ClusterTrace()
+    fid_r, cnt = tr.rules()
+    rng = np.random.default_rng(99)
+    sample = np.unique(np.concatenate([tr.perm[:16] + 1, rng.integers(1, tr.n + 1, size=2000)])).astype(np.int64)
+    rules = [{"flow_id": int(f), "count": float(cnt[f - 1]), "threshold_type": 1} for f in sample]
+    oh = oracle_cluster({"default": rules})
+    eng = make_engine(c, hot=hot, max_batch=1 << 24, max_rules=1 << 20)
+    c.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_r, cnt)
+    svc = c.DefaultTokenService(eng)
+    for b in range(2):
+        fid, acq, prio, ts = tr.events(b << 24, 1 << 24)
+        g = svc.request_tokens(fid, acq, prio, ts)
+        st = g["status"]
+        assert np.isin(st, [0, 1, 2]).all()
+        assert (g["wait_in_ms"][st == 2] == 100).all() and (g["wait_in_ms"][st != 2] == 0).all()
+        assert (g["remaining"][st == 0] >= 0).all() and (g["remaining"][st != 0] == 0).all()
+        m = np.isin(fid, sample)
+        o = oracle_replay(oh, fid[m], acq[m], prio[m], ts[m])
+        sub = {k: g[k][m] for k in ("status", "remaining", "wait_in_ms")}
+        assert_same(sub, o, fid[m], ts[m], f"hot={hot} batch {b} ({int(m.sum())} sampled requests)")
+    assert_metrics(c, eng, oh, sample[:64], int(ts[-1]))
+    H.lib().orc_cluster_free(oh)
+    eng.close()
