@@ -121,14 +121,21 @@ def main():
 
     eng = cluster.Engine(device=local, max_batch=max_n + 1024, max_rules=max(1 << 16, int(mine.sum()) + 1))
     cluster.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_all[mine], cnt_all[mine])
-    out = torch.empty(max_n + 1024, dtype=torch.int64, device=dev)
     L = _lib.load()
     estream = L.sga_engine_stream(eng.handle)
 
+    # one synchronous sga_request_tokens_device per batch; SGA_BENCH_ASYNC=1 queues them with the
+    # pipelined entry instead (stage A of batch b + 1 beside stage B of batch b: measured no faster,
+    # DESIGN.md section 3)
+    submit = L.sga_request_tokens_device_async if os.environ.get("SGA_BENCH_ASYNC") == "1" else \
+        L.sga_request_tokens_device
+    outs = [torch.empty(max_n + 1024, dtype=torch.int64, device=dev) for _ in range(2)]
+
     def step(b):
         f, a, p, t, ts_base, n = batches[b]
-        rc = L.sga_request_tokens_device(eng.handle, f.data_ptr(), a.data_ptr(), p.data_ptr(), ts_base, t.data_ptr(),
-                                         n, out.data_ptr(), None)
+        o = outs[b & 1]  # a queued batch's results stay untouched until the next batch but one
+        rc = submit(eng.handle, f.data_ptr(), a.data_ptr(), p.data_ptr(), ts_base, t.data_ptr(), n, o.data_ptr(),
+                    None)
         if rc != 0:
             raise RuntimeError(f"sga_request_tokens_device rc={rc}: {L.sga_last_error(eng.handle)}")
 
@@ -153,6 +160,7 @@ def main():
     hip.hipEventRecord(ev0, estream)
     for b in range(args.warmup, nb):
         step(b)
+    L.sga_stream_wait(eng.handle, None)  # the engine stream waits for every queued batch
     hip.hipEventRecord(ev1, estream)
     torch.cuda.synchronize(dev)
     t_end = time.perf_counter()
@@ -175,7 +183,7 @@ def main():
     wall_max, gpu_max, total_events, total_touched = [float(x) for x in stats]
 
     # correctness spot-check of the last batch's statuses (cheap invariants)
-    res = out[: batches[-1][5]].cpu().numpy().view(np.uint64)
+    res = outs[(nb - 1) & 1][: batches[-1][5]].cpu().numpy().view(np.uint64)
     status = ((res >> np.uint64(48)) & np.uint64(0xFF)).astype(np.int8)
     frac_ok = float((status == 0).mean())
 

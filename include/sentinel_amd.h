@@ -155,6 +155,21 @@ int sga_request_tokens_device(sga_engine *e, const int64_t *d_flow_id, const int
                               const uint8_t *d_prioritized, int64_t ts_base, const uint32_t *d_ts_off, size_t n,
                               sga_token_result *d_out, void *hip_stream);
 
+/* Pipelined form of sga_request_tokens_device for a stream of batches (a token server draining
+ * its request queue): returns once the batch is queued.  Stage A of a batch (classify, sort,
+ * runs -- no rule state) runs beside stage B of the previous one (flows, results -- the rule
+ * state, in submission order) on the engine's own streams, so decisions are the same as one
+ * synchronous call per batch in submission order.  The inputs must be ready on `hip_stream`
+ * (null: the engine stream) when the call is made; they and d_out must stay valid until
+ * sga_sync / sga_stream_wait.  Any other engine call first waits for queued batches. */
+int sga_request_tokens_device_async(sga_engine *e, const int64_t *d_flow_id, const int32_t *d_acquire,
+                                    const uint8_t *d_prio, int64_t ts_base, const uint32_t *d_ts_off, size_t n,
+                                    sga_token_result *d_out, void *hip_stream);
+/* Make `hip_stream` (null: the engine stream) wait for every queued batch (no host wait). */
+int sga_stream_wait(sga_engine *e, void *hip_stream);
+/* Host wait for every queued batch. */
+int sga_sync(sga_engine *e);
+
 /* ClusterMetric.getSum(event) for every ClusterFlowEvent at virtual time `now`
  * (rotation side effects included, as in the reference). out[7]. */
 int sga_cluster_metric_sums(sga_engine *e, int64_t flow_id, int64_t now, int64_t *out7);

@@ -112,6 +112,10 @@ SIGNATURES = {
                                      C.c_void_p]),
     "sga_request_tokens_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
                                             C.c_size_t, C.c_void_p, C.c_void_p]),
+    "sga_request_tokens_device_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
+                                            C.c_size_t, C.c_void_p, C.c_void_p]),
+    "sga_stream_wait": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "sga_sync": (C.c_int, [C.c_void_p]),
     "sga_cluster_metric_sums": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.POINTER(C.c_int64)]),
     "sga_cluster_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "sga_load_cluster_param_rules": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(SgaClusterParamRule), C.c_size_t]),

@@ -2225,7 +2225,7 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
 
 void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
                           const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, int simple,
-                          void *out_v, hipStream_t s, const LimiterPass *lims, int nlims) {
+                          void *out_v, hipStream_t s, const LimiterPass *lims, int nlims, int stages) {
     if (n == 0) return;
     uint64_t *out = (uint64_t *)out_v;
     int bits = 1;
@@ -2235,31 +2235,39 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     const int d0 = radix64_digit_bits(bits);
     const uint32_t ntiles = (n + kTileElems - 1) / kTileElems;
     static_assert(kTileElems == kRadix64Tile, "classify tiles are sort tiles");
-    SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, s));
     const bool lb = radix64_lookback() != 0;
     const int npass = (bits + d0 - 1) / d0;
-    if (lb) SGA_HIP_CHECK(hipMemsetAsync(sc.radix.ghist, 0, kRadixGhistWords * sizeof(uint32_t), s));
-    if (lb) SGA_HIP_CHECK(hipMemsetAsync(sc.radix.err, 0, sizeof(uint32_t), s));
+    if (stages & 1) {
+        SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, s));
+        if (lb) SGA_HIP_CHECK(hipMemsetAsync(sc.radix.ghist, 0, kRadixGhistWords * sizeof(uint32_t), s));
+        if (lb) SGA_HIP_CHECK(hipMemsetAsync(sc.radix.err, 0, sizeof(uint32_t), s));
+    }
     static const int chunk = getenv("SGA_CLS_CHUNK") ? atoi(getenv("SGA_CLS_CHUNK")) : 2;  // A/B knob
     auto cls = chunk >= 16 ? k_classify<16>
                            : (chunk >= 8 ? k_classify<8> : (chunk >= 4 ? k_classify<4> : (chunk >= 2 ? k_classify<2> : k_classify<1>)));
     static const int nofuse = getenv("SGA_XP_NOFUSE") ? atoi(getenv("SGA_XP_NOFUSE")) : 0;  // A/B knob
-    if (sc.hot_enabled && !limited && !lb && !nofuse) {
+    if (sc.hot_enabled && !limited && !lb && !nofuse && stages == 3) {
         decide_batch_hot(st, sc, flow_id, acquire, prio, ts_base, ts_off, n, simple, out, s, bits, d0, ntiles);
         return;
     }
-    hipLaunchKernelGGL(cls, dim3(ntiles), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n,
-                       simple, invalid_key, sc.el[0], out, (limited || nofuse) ? 0 : d0, ntiles, sc.radix.hist,
-                       (lb && !limited) ? npass : 0, sc.radix.ghist);
-    if (!simple) apply_limiters(st.param, sc, sc.el[0], n, invalid_key, ts_base, ts_off, out, lims, nlims, s);
-    const int np = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, !limited && !nofuse);
-    const uint64_t *el = sc.el[np & 1];
-    hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
-                       sc.tile_valid, nullptr);
-    hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
-                       ntiles, (Agg *)sc.tile_carry, sc.counters);
-    hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key, (const Agg *)sc.tile_carry,
-                       sc, 0);
+    // the sort's result buffer (radix_sort_u64 returns npass)
+    const uint64_t *el = sc.el[npass & 1];
+    if (stages & 1) {  // stage A: classify, limiter pre-pass, sort, runs (no rule state read or written)
+        hipLaunchKernelGGL(cls, dim3(ntiles), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n,
+                           simple, invalid_key, sc.el[0], out, (limited || nofuse) ? 0 : d0, ntiles, sc.radix.hist,
+                           (lb && !limited) ? npass : 0, sc.radix.ghist);
+        if (!simple) apply_limiters(st.param, sc, sc.el[0], n, invalid_key, ts_base, ts_off, out, lims, nlims, s);
+        const int np = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, !limited && !nofuse);
+        if (np != npass) throw HipError("radix pass count mismatch", __FILE__, __LINE__);
+        hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
+                           sc.tile_valid, nullptr);
+        hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg,
+                           sc.tile_valid, ntiles, (Agg *)sc.tile_carry, sc.counters);
+        hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key,
+                           (const Agg *)sc.tile_carry, sc, 0);
+    }
+    if (!(stages & 2)) return;
+    // stage B: flows (the rule state), deferred replays, results
     const uint64_t max_flows = n < st.nslots ? n : st.nslots;
     uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows + kThreads - 1) / kThreads, 16384);
     if (fb == 0) fb = 1;

@@ -145,7 +145,10 @@ void batch_scratch_carve(BatchScratch &b, void *base, size_t cap, uint32_t nslot
 void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
                           const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, int simple,
                           void *out /* sga_token_result */, hipStream_t stream, const LimiterPass *lims = nullptr,
-                          int nlims = 0);
+                          int nlims = 0, int stages = 3);
+// stages: 1 = stage A only (classify, limiter pre-pass, sort, runs: reads no rule state), 2 = stage B
+// only (flows, deferred replays, results, on the same scratch), 3 = both.  A pipelined caller runs
+// stage A of batch b + 1 beside stage B of batch b on two scratch sets (no limiters, no hot split).
 
 // ---------------------------------------------------------------------------------------------
 // Cluster parameter flow (ClusterParamFlowChecker + ClusterParamMetric, CS/flow/ClusterParamFlowChecker.java:37-120,

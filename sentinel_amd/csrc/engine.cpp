@@ -364,7 +364,56 @@ struct Engine {
         d_scratch.alloc(bytes);
         batch_scratch_carve(scratch, d_scratch.p, cfg.max_batch, p2);
         scratch_slots_cap = p2;
+        d_scratch2.release();  // the pipeline's second scratch set is re-carved on its next use
         hot_reset(state(), scratch, p2, stream);
+    }
+
+    // ---- pipelined device batches (sga_request_tokens_device_async): stage A (classify, sort, runs)
+    // of batch b + 1 runs on pst[0] beside stage B (flows, results) of batch b on pst[1]; batches
+    // alternate between two scratch sets.  Every other API call drains the pipeline first.
+    hipStream_t pst[2] = {nullptr, nullptr};
+    hipEvent_t pev_in = nullptr, pev_a[2] = {nullptr, nullptr}, pev_b[2] = {nullptr, nullptr};
+    bool pev_b_live[2] = {false, false};
+    DevBuf<uint8_t> d_scratch2;
+    BatchScratch scratch2;
+    uint64_t pseq = 0;
+    bool pipe_busy = false;
+
+    void drain() {
+        if (!pipe_busy) return;
+        SGA_HIP_CHECK(hipStreamSynchronize(pst[0]));
+        SGA_HIP_CHECK(hipStreamSynchronize(pst[1]));
+        pipe_busy = false;
+    }
+
+    void ensure_pipeline() {
+        if (!pst[0]) {
+            for (int i = 0; i < 2; ++i) {
+                SGA_HIP_CHECK(hipStreamCreateWithFlags(&pst[i], hipStreamNonBlocking));
+                SGA_HIP_CHECK(hipEventCreateWithFlags(&pev_a[i], hipEventDisableTiming));
+                SGA_HIP_CHECK(hipEventCreateWithFlags(&pev_b[i], hipEventDisableTiming));
+            }
+            SGA_HIP_CHECK(hipEventCreateWithFlags(&pev_in, hipEventDisableTiming));
+        }
+        ensure_scratch();
+        if (!d_scratch2.p) {
+            SGA_HIP_CHECK(hipStreamSynchronize(stream));
+            d_scratch2.alloc(batch_scratch_bytes(cfg.max_batch, scratch_slots_cap));
+            batch_scratch_carve(scratch2, d_scratch2.p, cfg.max_batch, scratch_slots_cap);
+            scratch2.hot_enabled = 0;
+            pev_b_live[1] = false;
+        }
+    }
+
+    void release_pipeline() {
+        for (int i = 0; i < 2; ++i) {
+            if (pst[i]) (void)hipStreamDestroy(pst[i]);
+            if (pev_a[i]) (void)hipEventDestroy(pev_a[i]);
+            if (pev_b[i]) (void)hipEventDestroy(pev_b[i]);
+            pst[i] = nullptr;
+        }
+        if (pev_in) (void)hipEventDestroy(pev_in);
+        pev_in = nullptr;
     }
 
     uint32_t alloc_slot() {
@@ -527,10 +576,11 @@ using sga::SlotHost;
 using sga::CEV_N;
 
 template <typename F>
-static int guarded(sga_engine *e, F &&f) {
+static int guarded(sga_engine *e, F &&f, bool drain_first = true) {
     if (!e) return SGA_EINVAL;
     std::lock_guard<std::mutex> lk(e->impl.mu);
     try {
+        if (drain_first) e->impl.drain();  // pipelined batches complete before any other call
         return f(e->impl);
     } catch (const sga::HipError &h) {
         e->impl.err = h.what;
@@ -600,6 +650,9 @@ int sga_destroy(sga_engine *e) {
         std::lock_guard<std::mutex> lk(e->impl.mu);
         if (e->impl.stream) {
             (void)hipStreamSynchronize(e->impl.stream);
+            for (int i = 0; i < 2; ++i)
+                if (e->impl.pst[i]) (void)hipStreamSynchronize(e->impl.pst[i]);
+            e->impl.release_pipeline();
             e->impl.flow.release();
             (void)hipStreamDestroy(e->impl.stream);
         }
@@ -773,6 +826,65 @@ int sga_request_tokens_device(sga_engine *e, const int64_t *d_flow_id, const int
         SGA_HIP_CHECK(hipGetLastError());
         return SGA_OK;
     });
+}
+
+int sga_request_tokens_device_async(sga_engine *e, const int64_t *d_flow_id, const int32_t *d_acquire,
+                                    const uint8_t *d_prio, int64_t ts_base, const uint32_t *d_ts_off, size_t n,
+                                    sga_token_result *d_out, void *hip_stream) {
+    if (n && (!d_flow_id || !d_acquire || !d_ts_off || !d_out)) return SGA_EINVAL;
+    if (ts_base < 0) return SGA_EINVAL;
+    return guarded(
+        e,
+        [&](Engine &g) {
+            if (n > g.cfg.max_batch) return SGA_ERANGE;
+            SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+            hipStream_t cs = hip_stream ? (hipStream_t)hip_stream : g.stream;
+            const auto lims = limiter_passes(g);
+            if (!lims.empty() || g.scratch.hot_enabled || sga::radix64_lookback()) {
+                // namespace limiters / hot split / look-back sort: one stream, in submission order
+                g.drain();
+                sga::cluster_decide_batch(g.state(), g.scratch, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off,
+                                          (uint32_t)n, 0, d_out, cs, lims.data(), (int)lims.size());
+                SGA_HIP_CHECK(hipGetLastError());
+                return SGA_OK;
+            }
+            g.ensure_pipeline();
+            const int slot = (int)(g.pseq & 1);
+            sga::BatchScratch &sc = slot ? g.scratch2 : g.scratch;
+            const sga::ClusterState st = g.state();
+            SGA_HIP_CHECK(hipEventRecord(g.pev_in, cs));  // inputs ready on the caller's stream
+            SGA_HIP_CHECK(hipStreamWaitEvent(g.pst[0], g.pev_in, 0));
+            if (g.pev_b_live[slot]) SGA_HIP_CHECK(hipStreamWaitEvent(g.pst[0], g.pev_b[slot], 0));  // scratch free
+            sga::cluster_decide_batch(st, sc, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off, (uint32_t)n, 0, d_out,
+                                      g.pst[0], nullptr, 0, 1);
+            SGA_HIP_CHECK(hipEventRecord(g.pev_a[slot], g.pst[0]));
+            SGA_HIP_CHECK(hipStreamWaitEvent(g.pst[1], g.pev_a[slot], 0));
+            sga::cluster_decide_batch(st, sc, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off, (uint32_t)n, 0, d_out,
+                                      g.pst[1], nullptr, 0, 2);
+            SGA_HIP_CHECK(hipEventRecord(g.pev_b[slot], g.pst[1]));
+            SGA_HIP_CHECK(hipGetLastError());
+            g.pev_b_live[slot] = true;
+            ++g.pseq;
+            g.pipe_busy = true;
+            return SGA_OK;
+        },
+        false);
+}
+
+int sga_stream_wait(sga_engine *e, void *hip_stream) {
+    return guarded(
+        e,
+        [&](Engine &g) {
+            if (!g.pipe_busy) return SGA_OK;
+            hipStream_t cs = hip_stream ? (hipStream_t)hip_stream : g.stream;
+            SGA_HIP_CHECK(hipStreamWaitEvent(cs, g.pev_b[(g.pseq - 1) & 1], 0));
+            return SGA_OK;
+        },
+        false);
+}
+
+int sga_sync(sga_engine *e) {
+    return guarded(e, [&](Engine &) { return SGA_OK; });  // guarded drains the pipeline
 }
 
 static int run_host_batch(Engine &g, const int64_t *flow_id, const int32_t *acquire, const uint8_t *prio,

@@ -413,3 +413,58 @@ def test_c3_full_size_sampled_rules_bit_exact(eng_mod, hot):
     assert_metrics(c, eng, oh, sample[:64], int(ts[-1]))
     H.lib().orc_cluster_free(oh)
     eng.close()
+
+
+def test_pipelined_device_batches_match_sync(eng_mod):
+    """sga_request_tokens_device_async (stage A of batch b + 1 beside stage B of batch b, two
+    scratch sets) decides exactly like one synchronous sga_request_tokens_device per batch:
+    identical TokenResults for every batch and identical metric counters afterwards; the sampled
+    rules' requests also equal the oracle's replay."""
+    import torch
+    from sentinel_amd import _lib
+    from sentinel_amd.workload import ClusterTrace
+    c = eng_mod
+    L = _lib.load()
+    dev = torch.device("cuda", 0)
+    tr = ClusterTrace(n_rules=200_000, lam=20_000_000)
+    fid_r, cnt = tr.rules()
+    nb, m = 7, 1 << 19
+    host = [tr.events(b * m, m) for b in range(nb)]
+    res = {}
+    for mode in ("sync", "async"):
+        eng = make_engine(c, max_batch=m, max_rules=1 << 18)
+        c.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_r, cnt)
+        fn = L.sga_request_tokens_device if mode == "sync" else L.sga_request_tokens_device_async
+        keep, outs = [], []
+        for b, (f, a, p, ts) in enumerate(host):
+            base = int(ts[0])
+            d = (torch.from_numpy(f).to(dev), torch.from_numpy(a).to(dev), torch.from_numpy(p).to(dev),
+                 torch.from_numpy((ts - base).astype(np.int32)).to(dev))
+            o = torch.zeros(m, dtype=torch.int64, device=dev)
+            torch.cuda.synchronize()
+            rc = fn(eng.handle, d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), base, d[3].data_ptr(), m,
+                    o.data_ptr(), None)
+            assert rc == 0, (mode, b, rc, L.sga_last_error(eng.handle))
+            keep.append(d)
+            outs.append(o)
+        assert L.sga_sync(eng.handle) == 0
+        torch.cuda.synchronize()
+        res[mode] = [o.cpu().numpy() for o in outs]
+        sample = np.unique(np.concatenate([tr.perm[:8] + 1, np.arange(1, 200_001, 997)])).astype(np.int64)
+        res[mode + "_metrics"] = [c.DefaultTokenService(eng).metric_sums(int(x), int(host[-1][3][-1])) for x in sample]
+        eng.close()
+    for b in range(nb):
+        assert np.array_equal(res["sync"][b], res["async"][b]), f"batch {b}"
+    assert res["sync_metrics"] == res["async_metrics"]
+    # and the sampled rules against the oracle
+    rules = [{"flow_id": int(x), "count": float(cnt[x - 1]), "threshold_type": 1} for x in sample]
+    oh = oracle_cluster({"default": rules})
+    for b, (f, a, p, ts) in enumerate(host):
+        sel = np.isin(f, sample)
+        o = oracle_replay(oh, f[sel], a[sel], p[sel], ts[sel])
+        r = res["async"][b].view(np.uint64)[sel]
+        got = {"status": ((r >> np.uint64(48)) & np.uint64(0xFF)).astype(np.int8).astype(np.int32),
+               "remaining": (r & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32),
+               "wait_in_ms": ((r >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.uint16).view(np.int16).astype(np.int32)}
+        assert_same(got, o, f[sel], ts[sel], f"async batch {b}")
+    H.lib().orc_cluster_free(oh)
