@@ -45,6 +45,7 @@ struct Ctx {
                      // LDS copy of the map entry (null: look the entry up in the map)
     int8_t pre_param;   // k_lheavy: that rule's check already decided by the value's lane (1 pass, 2 block)
     int64_t pre_wait;   // its wait
+    const ResDev *res;  // k_lheavy: the resource's record, held by the replaying lane (null: st.res)
 };
 
 // ------------------------------------------------------------------ MetricBucket windows
@@ -514,7 +515,7 @@ __device__ __forceinline__ ResMem res_global(const Ctx &c, uint32_t r, const Res
 
 __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t t, int acquire, bool prio,
                               bool has_param, uint64_t param, int64_t *wait_ms) {
-    const ResDev R = c.st.res[r];
+    const ResDev R = c.res ? *c.res : c.st.res[r];
     int64_t *node = m.node;
     *wait_ms = 0;
     int64_t total_wait = 0;
@@ -589,7 +590,7 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
 
 __device__ void chain_exit(const Ctx &c, uint32_t r, const ResMem &m, int64_t t, int64_t rt, int count, bool error,
                            bool has_param, uint64_t param) {
-    const ResDev R = c.st.res[r];
+    const ResDev R = c.res ? *c.res : c.st.res[r];
     int64_t *node = m.node;
     node_add_rt_success(c, node, t, rt, count);
     node[kNodeThreads] -= 1;
@@ -1308,7 +1309,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
     __shared__ uint16_t qrank[kHeavyChunk], qord[kHeavyChunk];
     __shared__ uint32_t lcnt[64];
     __shared__ int64_t qbq[kHeavyChunk];  // second-window bucket (t / 500) of each event
-    const Ctx c{st, max_rt, nullptr, 0, 0};
+    const Ctx c{st, max_rt, nullptr, 0, 0, nullptr};
     constexpr uint64_t kLEmpty = ~0ull;  // a value equal to it bypasses the cache (map path)
     constexpr uint32_t kGiNone = 0xFFFFFFFFu, kGiFail = 0xFFFFFFFEu;
     for (int k = threadIdx.x; k < kHeavySlots; k += 64) lval[k] = kLEmpty;
@@ -1511,12 +1512,13 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
             }
             if (!agg && threadIdx.x == 0) {
                 Ctx cc = c;
+                cc.res = &R;
                 for (uint32_t k = 0; k < cnt; ++k) {
                     const Payload q = qpay[k];
                     const int64_t t = ts_base + (int64_t)q.ts_off;
                     const bool hp = (q.idx & F_PARAM) != 0;
                     if (q.idx & F_EXIT) {
-                        chain_exit(c, res, m, t, qrt[k], (int)(q.acq_prio & 0x7FFFFFFFu), (q.idx & F_ERROR) != 0, hp,
+                        chain_exit(cc, res, m, t, qrt[k], (int)(q.acq_prio & 0x7FFFFFFFu), (q.idx & F_ERROR) != 0, hp,
                                    qpv[k]);
                     } else {
                         int64_t w = 0;
