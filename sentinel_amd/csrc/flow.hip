@@ -1285,7 +1285,8 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                                                const Payload *__restrict__ pay, int64_t ts_base,
                                                const int64_t *__restrict__ rt_in,
                                                const uint64_t *__restrict__ param_in, int8_t *decision,
-                                               int32_t *wait_ms) {
+                                               int32_t *wait_ms, uint64_t *prof) {
+    // prof (SGA_HEAVY_PROF=1): per workgroup, wall-clock ticks spent in each phase of the chunks
     __shared__ int64_t lnode[kNodeWords];
     __shared__ FlowRuleDev lrules[kHeavyRules];
     __shared__ CbDev lcbs[kHeavyCbs];
@@ -1300,6 +1301,9 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
     __shared__ PEntry lent[kHeavySlots];
     __shared__ uint64_t lval[kHeavySlots];  // parameter value of the slot (kLEmpty = free)
     __shared__ uint32_t lgi[kHeavySlots];   // map index of the slot's entry
+    __shared__ PEntry tent[kHeavySlots];    // per-value lanes: the value's thread-count entry (ParameterMetric)
+    __shared__ uint32_t tgi[kHeavySlots];
+    __shared__ int nocache;                 // a parameter event of the chunk got no slot
     __shared__ uint16_t qslot[kHeavyChunk];
     // parameter-only resources: the rule check of each event is decided by the lane that owns the
     // event's value (lane = LDS slot mod 64), every lane walking its values' events in arrival
@@ -1334,11 +1338,21 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
         // one parameter rule with a map (QPS grade): its entries go through the LDS cache
         const ParamRuleDev *cache_p =
             (R.n_prules == 1 && st.prules[R.prule_off].grade == 1) ? &st.prules[R.prule_off] : nullptr;
-        const bool par = cache_p && R.n_rules == 0 && R.n_cbs == 0 && !(R.fast & 2u);
+        // parameter-only resource: per-value lanes own the rule map entry and the thread-count entry
+        const bool par = cache_p && R.n_rules == 0 && R.n_cbs == 0;
         int pidx = cache_p ? cache_p->param_idx : 0;  // ParamFlowSlot index with one argument
         if (pidx < 0) pidx = (-pidx <= 1) ? 1 + pidx : -pidx;
         const bool p_applies = pidx < 1;
         const uint32_t jb = sc.run_start[r0], je = sc.run_end[r1 - 1];
+        uint64_t tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        uint64_t tprev = prof ? wall_clock64() : 0;
+        auto tick = [&](int ph) {
+            if (prof && threadIdx.x == 0) {
+                const uint64_t t = wall_clock64();
+                tk[ph] += t - tprev;
+                tprev = t;
+            }
+        };
         for (uint32_t base = jb; base < je; base += kHeavyChunk) {
             const uint32_t cnt = min((uint32_t)kHeavyChunk, je - base);
             for (uint32_t k = threadIdx.x; k < cnt; k += 64) {
@@ -1349,17 +1363,26 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                 qpv[k] = (q.idx & F_PARAM) ? param_in[idx] : 0;
             }
             __syncthreads();
+            tick(0);
+            if (threadIdx.x == 0) nocache = 0;
+            __syncthreads();
+            const bool pt = par && p_applies;  // exits of parameter events go to the value lanes too
             if (cache_p) {
                 // 1. the chunk's distinct values into LDS slots (64-bit CAS on the value)
                 for (uint32_t k = threadIdx.x; k < cnt; k += 64) {
                     const Payload q = qpay[k];
                     uint16_t sl = 0xFFFF;
-                    if ((q.idx & F_PARAM) && !(q.idx & F_EXIT) && qpv[k] != kLEmpty) {
+                    const bool want = (q.idx & F_PARAM) && (pt || !(q.idx & F_EXIT));
+                    if (want && qpv[k] == kLEmpty) nocache = 1;
+                    if (want && qpv[k] != kLEmpty) {
                         const uint64_t v = qpv[k];
                         uint32_t h = (uint32_t)splitmix64(v) & (kHeavySlots - 1);
                         for (int probe = 0; probe < kHeavySlots; ++probe) {
                             const uint64_t old = atomicCAS((unsigned long long *)&lval[h], kLEmpty, v);
-                            if (old == kLEmpty) lgi[h] = kGiNone;
+                            if (old == kLEmpty) {
+                                lgi[h] = kGiNone;
+                                tgi[h] = kGiNone;
+                            }
                             if (old == kLEmpty || old == v) {
                                 sl = (uint16_t)h;
                                 break;
@@ -1378,6 +1401,13 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                         lgi[h] = (uint32_t)(e - st.ptab);
                         lent[h] = *e;
                     }
+                    if (pt) {
+                        PEntry *te = ptab_get(st.ttab, st.tmask, res + 1, lval[h], false, st.overflow);
+                        if (te) {
+                            tgi[h] = (uint32_t)(te - st.ttab);
+                            tent[h] = *te;
+                        }
+                    }
                 }
                 __syncthreads();
                 // 3. insert the absent ones (a fresh entry is the reference's "not seen yet"; creating
@@ -1388,9 +1418,18 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     lgi[h] = e ? (uint32_t)(e - st.ptab) : kGiFail;
                     lent[h] = PEntry{lval[h], cache_p->id + 1, 0, kPAbsent, kPAbsent};
                 }
+                if (pt)
+                    for (int h = threadIdx.x; h < kHeavySlots; h += 64) {
+                        if (lval[h] == kLEmpty || tgi[h] != kGiNone) continue;
+                        PEntry *te = ptab_insert_absent(st.ttab, st.tmask, res + 1, lval[h], st.overflow);
+                        tgi[h] = te ? (uint32_t)(te - st.ttab) : kGiFail;
+                        tent[h] = PEntry{lval[h], res + 1, 0, kPAbsent, kPAbsent};
+                    }
             }
             __syncthreads();
-            if (par && p_applies) {
+            tick(1);
+            const bool par_ok = pt && !nocache;
+            if (par_ok) {
                 const int lane = threadIdx.x;
                 const uint64_t lt = (1ull << lane) - 1ull;
                 lcnt[lane] = 0;
@@ -1401,7 +1440,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     uint32_t own = 0;
                     if (k < cnt) {
                         const Payload q = qpay[k];
-                        ok = !(q.idx & F_EXIT) && (q.idx & F_PARAM) && qslot[k] != 0xFFFF;
+                        ok = (q.idx & F_PARAM) && qslot[k] != 0xFFFF;  // entries and exits
                         own = qslot[k] & 63u;
                         qpre[k] = 0;
                         qbq[k] = (ts_base + (int64_t)q.ts_off) / kSecW;
@@ -1440,21 +1479,28 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                 for (uint32_t i = start; i < start + mine; ++i) {
                     const uint32_t k = qord[i];
                     const Payload q = qpay[k];
+                    PEntry &te = tent[qslot[k]];
+                    const bool tmap = (R.fast & 2u) != 0;  // ParameterMetric thread counts exist
+                    if (q.idx & F_EXIT) {  // ParameterMetric.decreaseThreadCount (chain_exit)
+                        if (tmap) {
+                            if (te.a == kPAbsent) te.a = 0;
+                            else if (--te.a <= 0) te.a = kPAbsent;
+                        }
+                        continue;
+                    }
                     cl.pentry = &lent[qslot[k]];
                     int64_t w = 0;
+                    // a QPS rule does not read the thread count
                     const bool pass = param_pass(cl, *cache_p, qpv[k], (int)(q.acq_prio & 0x7FFFFFFFu),
                                                  ts_base + (int64_t)q.ts_off, 0, &w);
                     qpre[k] = pass ? 1 : 2;
                     qpw[k] = (int32_t)w;
+                    if (pass && tmap) te.a = (te.a == kPAbsent ? 0 : te.a) + 1;  // ParameterMetric.addThreadCount
                 }
             }
             __syncthreads();
-            bool agg = par && p_applies;
-            if (agg && threadIdx.x == 0)
-                for (uint32_t k = 0; k < cnt && agg; ++k) {
-                    const uint32_t f = qpay[k].idx;
-                    if (!(f & F_EXIT) && (f & F_PARAM) && qslot[k] == 0xFFFF) agg = false;  // map full
-                }
+            tick(2);
+            const bool agg = par_ok;
             if (agg && threadIdx.x == 0) {
                 // StatisticSlot in aggregate: a parameter-only resource's decisions never read its node,
                 // and every event of a 500 ms second-window bucket (nested in one minute bucket) sees the
@@ -1523,8 +1569,8 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     } else {
                         int64_t w = 0;
                         cc.pentry = (cache_p && qslot[k] != 0xFFFF) ? &lent[qslot[k]] : nullptr;
-                        cc.pre_param = (par && p_applies) ? qpre[k] : 0;
-                        cc.pre_wait = (par && p_applies) ? qpw[k] : 0;
+                        cc.pre_param = 0;  // not aggregated: lane 0 decides everything
+                        cc.pre_wait = 0;
                         qd[k] = chain_entry(cc, res, m, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
                                             hp, qpv[k], &w);
                         qw[k] = (int32_t)w;
@@ -1532,6 +1578,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                 }
             }
             __syncthreads();
+            tick(3);
             if (cache_p) {  // write the chunk's entries back, free the slots
                 for (int k = threadIdx.x; k < kHeavySlots; k += 64) {
                     if (lval[k] != kLEmpty) {
@@ -1540,6 +1587,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                             e->a = lent[k].a;
                             e->b = lent[k].b;
                         }
+                        if (par_ok && tgi[k] < kGiFail) st.ttab[tgi[k]].a = tent[k].a;
                         lval[k] = kLEmpty;
                     }
                 }
@@ -1552,6 +1600,11 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                 }
             }
             __syncthreads();
+            tick(4);
+        }
+        if (prof && threadIdx.x == 0) {
+            for (int i = 0; i < 5; ++i) prof[blockIdx.x * 8 + i] += tk[i];
+            prof[blockIdx.x * 8 + 5] += je - jb;
         }
         for (uint32_t r = r0 + threadIdx.x; r < r1; r += 64) sc.run_mode[r] = RUN_DONE;
         __syncthreads();
@@ -2019,6 +2072,32 @@ int FlowEngine::ensure_maps(size_t m) {
     return 0;
 }
 
+// SGA_HEAVY_PROF=1: k_lheavy phase timers (1024 workgroups x 8 counters), printed by
+// FlowEngine::print_heavy_prof at engine release.  Diagnostics only.
+static uint64_t *g_heavy_prof = nullptr;
+static uint64_t *heavy_prof() {
+    static const bool on = getenv("SGA_HEAVY_PROF") && atoi(getenv("SGA_HEAVY_PROF")) == 1;
+    if (on && !g_heavy_prof) {
+        SGA_HIP_CHECK(hipMalloc((void **)&g_heavy_prof, 1024 * 8 * sizeof(uint64_t)));
+        SGA_HIP_CHECK(hipMemset(g_heavy_prof, 0, 1024 * 8 * sizeof(uint64_t)));
+    }
+    return on ? g_heavy_prof : nullptr;
+}
+
+void print_heavy_prof() {
+    if (!g_heavy_prof) return;
+    std::vector<uint64_t> h(1024 * 8);
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpy(h.data(), g_heavy_prof, h.size() * 8, hipMemcpyDeviceToHost);
+    int best = 0;
+    for (int b = 0; b < 1024; ++b)
+        if (h[b * 8 + 5] > h[best * 8 + 5]) best = b;
+    fprintf(stderr, "k_lheavy busiest workgroup %d: %llu events; ms stage %.2f dedupe+find+insert %.2f "
+            "lanes %.2f replay %.2f writeback+stores %.2f (100 MHz wall clock)\n", best,
+            (unsigned long long)h[best * 8 + 5], h[best * 8] / 1e5, h[best * 8 + 1] / 1e5, h[best * 8 + 2] / 1e5,
+            h[best * 8 + 3] / 1e5, h[best * 8 + 4] / 1e5);
+}
+
 int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int64_t *ts, const int32_t *acquire,
                        const uint8_t *flags, const int64_t *rt, const uint64_t *param, size_t n, int8_t *decision,
                        int32_t *wait_ms) {
@@ -2151,7 +2230,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
                            (int64_t)cfg.statistic_max_rt, sc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p);
         hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
-                           d_dec.p, d_wait.p);
+                           d_dec.p, d_wait.p, heavy_prof());
         hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, stream, sc, pay, d_dec.p);
         if (has_in)  // ENTRY_NODE statistics of the inbound events
             hipLaunchKernelGGL(k_entry_stats, dim3(1), dim3(kEnTile), 0, stream, st, (int64_t)cfg.statistic_max_rt,

@@ -112,6 +112,8 @@ struct FlowScratch {
     size_t cap = 0;
 };
 
+void print_heavy_prof();  // SGA_HEAVY_PROF=1 diagnostics (flow.hip)
+
 struct FlowEngine {
     sga_config cfg{};
     hipStream_t stream = nullptr;
@@ -159,7 +161,7 @@ struct FlowEngine {
         cfg = c;
         stream = s;
     }
-    void release() {}
+    void release() { print_heavy_prof(); }
     FlowState state() const;
     int set_resources(uint32_t n);
     int load_flow_rules(const sga_flow_rule *r, size_t n);
