@@ -460,6 +460,30 @@ __device__ void cb_stat_current(CbDev &b, int64_t t) {  // LeapArray(1, statInte
     }
 }
 
+// DegradeSlot.entry over the resource's breakers (DegradeSlot.java:52-66): tryPass of each in order;
+// a breaker moved to HALF_OPEN goes back to OPEN when a later one blocks (whenTerminate, blockError)
+__device__ bool degrade_pass(CbDev *cbs, uint32_t n, int64_t t) {
+    uint64_t half_mask = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        CbDev &b = cbs[k];
+        bool ok = false;
+        if (b.state == 0) ok = true;
+        else if (b.state == 1 && t >= b.next_retry) {
+            b.state = 2;
+            if (k < 64) half_mask |= 1ULL << k;
+            ok = true;
+        }
+        if (!ok) {
+            for (uint32_t q = 0; q < k && q < 64; ++q) {
+                CbDev &bq = cbs[q];
+                if (((half_mask >> q) & 1) && bq.state == 2) bq.state = 1;
+            }
+            return false;
+        }
+    }
+    return true;
+}
+
 __device__ void cb_on_complete(CbDev &b, int64_t t, int64_t rt, bool error) {
     const bool is_rt = b.grade == 0;
     const bool bad = is_rt ? rt > b.max_allowed_rt : error;
@@ -559,24 +583,9 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
         total_wait += w;
     }
     // DegradeSlot
-    uint64_t half_mask = 0;
-    for (uint32_t k = 0; k < R.n_cbs; ++k) {
-        CbDev &b = m.cbs[k];
-        bool ok = false;
-        if (b.state == 0) ok = true;
-        else if (b.state == 1 && t >= b.next_retry) {
-            b.state = 2;
-            if (k < 64) half_mask |= 1ULL << k;
-            ok = true;
-        }
-        if (!ok) {
-            for (uint32_t q = 0; q < k && q < 64; ++q) {
-                CbDev &bq = m.cbs[q];
-                if (((half_mask >> q) & 1) && bq.state == 2) bq.state = 1;
-            }
-            node_add(c, node, t, MB_BLOCK, acquire);
-            return D_BLOCK_DEGRADE;
-        }
+    if (!degrade_pass(m.cbs, R.n_cbs, t)) {
+        node_add(c, node, t, MB_BLOCK, acquire);
+        return D_BLOCK_DEGRADE;
     }
     node[kNodeThreads] += 1;
     node_add(c, node, t, MB_PASS, acquire);
@@ -1500,7 +1509,10 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
             }
             __syncthreads();
             tick(2);
-            const bool agg = par_ok;
+            // breaker-only resources: lane 0 runs the breakers event by event (a sequential state
+            // machine) and the node statistics in aggregate, as for parameter-only resources
+            const bool dgo = R.n_cbs > 0 && R.n_rules == 0 && R.n_prules == 0 && lc;
+            const bool agg = par_ok || dgo;
             if (agg && threadIdx.x == 0) {
                 // StatisticSlot in aggregate: a parameter-only resource's decisions never read its node,
                 // and every event of a 500 ms second-window bucket (nested in one minute bucket) sees the
@@ -1528,21 +1540,35 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                 };
                 for (uint32_t k = 0; k < cnt; ++k) {
                     const Payload q = qpay[k];
-                    if (qbq[k] != cur) {
+                    const int64_t bq = par_ok ? qbq[k] : (ts_base + (int64_t)q.ts_off) / kSecW;
+                    if (bq != cur) {
                         flush();
-                        cur = qbq[k];
+                        cur = bq;
                         tf = ts_base + (int64_t)q.ts_off;
                         pass_acq = block_acq = succ = rt_sum = exc = threads = 0;
                         rt_min = INT64_MAX;
                         any = true;
                     }
                     const int64_t a = (int64_t)(int)(q.acq_prio & 0x7FFFFFFFu);
-                    if (q.idx & F_EXIT) {  // chain_exit without maps or breakers
+                    if (q.idx & F_EXIT) {  // chain_exit: statistics in aggregate, breakers in order
                         succ += a;
                         rt_sum += qrt[k];
                         if (qrt[k] < rt_min) rt_min = qrt[k];
                         if (q.idx & F_ERROR) exc += a;
                         threads -= 1;
+                        if (dgo)
+                            for (uint32_t b = 0; b < R.n_cbs; ++b)
+                                cb_on_complete(lcbs[b], ts_base + (int64_t)q.ts_off, qrt[k], (q.idx & F_ERROR) != 0);
+                    } else if (dgo) {  // DegradeSlot
+                        if (degrade_pass(lcbs, R.n_cbs, ts_base + (int64_t)q.ts_off)) {
+                            pass_acq += a;
+                            threads += 1;
+                            qd[k] = D_PASS;
+                        } else {
+                            block_acq += a;
+                            qd[k] = D_BLOCK_DEGRADE;
+                        }
+                        qw[k] = 0;
                     } else if (qpre[k] == 2) {  // ParamFlowException
                         block_acq += a;
                         qd[k] = D_BLOCK_PARAM;

@@ -192,6 +192,24 @@ def test_circuit_breakers(seed):
     _run(n_res, flow=flow, degrade=degrade, n_entries=10000, seed=seed, gap_mean=0.7, err_pct=0.35, rt_max=60)
 
 
+@pytest.mark.parametrize("seed", [33, 34])
+def test_breaker_heavy_resources(seed):
+    """Breaker-only resources with thousands of events per batch (k_lheavy): breakers event by
+    event in arrival order, node statistics applied per 500 ms bucket run; slow-RT, error-ratio
+    and error-count breakers (two on one resource), batches smaller than the stream."""
+    n_res = 4
+    degrade = [{"resource": 0, "grade": 0, "count": 25, "time_window": 1, "slow_ratio_threshold": 0.3,
+                "min_request_amount": 5, "stat_interval_ms": 1000},
+               {"resource": 1, "grade": 1, "count": 0.25, "time_window": 1, "min_request_amount": 4,
+                "stat_interval_ms": 500},
+               {"resource": 2, "grade": 2, "count": 6, "time_window": 1, "stat_interval_ms": 700},
+               {"resource": 2, "grade": 0, "count": 40, "time_window": 2, "slow_ratio_threshold": 0.8},
+               {"resource": 3, "grade": 1, "count": 0.5, "time_window": 3, "min_request_amount": 10}]
+    for mb in (1 << 16, 5000):
+        _run(n_res, degrade=degrade, n_entries=30000, seed=seed, gap_mean=0.05, err_pct=0.3, rt_max=60,
+             max_batch=mb)
+
+
 def test_rule_reload_between_batches():
     n_res = 10
     rng = np.random.default_rng(5)
