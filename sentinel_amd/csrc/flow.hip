@@ -451,8 +451,7 @@ __device__ void cb_to_open(CbDev &b, int64_t t) {
     }
 }
 
-__device__ void cb_stat_current(CbDev &b, int64_t t) {  // LeapArray(1, statIntervalMs).currentWindow(t)
-    const int64_t ws = t - t % b.stat_interval;
+__device__ void cb_stat_at(CbDev &b, int64_t ws) {  // LeapArray(1, statIntervalMs).currentWindow(t), ws = its start
     if (b.st_start == kAbsent || ws > b.st_start) {
         b.st_start = ws;
         b.st_bad = 0;
@@ -484,12 +483,13 @@ __device__ bool degrade_pass(CbDev *cbs, uint32_t n, int64_t t) {
     return true;
 }
 
-__device__ void cb_on_complete(CbDev &b, int64_t t, int64_t rt, bool error) {
+// AbstractCircuitBreaker.onRequestComplete with the stat window start ws = t - t % statIntervalMs
+// given (k_lheavy computes it for a chunk on all lanes)
+__device__ void cb_on_complete_ws(CbDev &b, int64_t t, int64_t ws, int64_t rt, bool error) {
     const bool is_rt = b.grade == 0;
     const bool bad = is_rt ? rt > b.max_allowed_rt : error;
-    const int64_t ws = t - t % b.stat_interval;
     const bool detached = b.st_start != kAbsent && ws < b.st_start;
-    cb_stat_current(b, t);
+    cb_stat_at(b, ws);
     if (!detached) {
         if (bad) b.st_bad += 1;
         b.st_total += 1;
@@ -499,7 +499,7 @@ __device__ void cb_on_complete(CbDev &b, int64_t t, int64_t rt, bool error) {
         if (bad) cb_to_open(b, t);
         else {
             b.state = 0;  // fromHalfOpenToClose -> resetStat on currentWindow()
-            cb_stat_current(b, t);
+            cb_stat_at(b, ws);
             if (!(b.st_start != kAbsent && ws < b.st_start)) {
                 b.st_bad = 0;
                 b.st_total = 0;
@@ -522,6 +522,10 @@ __device__ void cb_on_complete(CbDev &b, int64_t t, int64_t rt, bool error) {
         if (b.grade == 1) cur = (double)badc * 1.0 / (double)total;
         if (cur > b.count) cb_to_open(b, t);
     }
+}
+
+__device__ __forceinline__ void cb_on_complete(CbDev &b, int64_t t, int64_t rt, bool error) {
+    cb_on_complete_ws(b, t, t - t % b.stat_interval, rt, error);
 }
 
 // ------------------------------------------------------------------ slot chain (one event)
@@ -1322,6 +1326,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
     __shared__ uint16_t qrank[kHeavyChunk], qord[kHeavyChunk];
     __shared__ uint32_t lcnt[64];
     __shared__ int64_t qbq[kHeavyChunk];  // second-window bucket (t / 500) of each event
+    __shared__ int64_t qrank_ws[kHeavyChunk];  // breaker-only resources: the breaker's stat window start
     const Ctx c{st, max_rt, nullptr, 0, 0, nullptr};
     constexpr uint64_t kLEmpty = ~0ull;  // a value equal to it bypasses the cache (map path)
     constexpr uint32_t kGiNone = 0xFFFFFFFFu, kGiFail = 0xFFFFFFFEu;
@@ -1513,6 +1518,16 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
             // machine) and the node statistics in aggregate, as for parameter-only resources
             const bool dgo = R.n_cbs > 0 && R.n_rules == 0 && R.n_prules == 0 && lc;
             const bool agg = par_ok || dgo;
+            if (dgo) {  // second-window buckets (and the one breaker's stat window starts) on all lanes:
+                        // lane 0 would divide per event
+                const int64_t si = R.n_cbs == 1 ? (int64_t)lcbs[0].stat_interval : 1;
+                for (uint32_t k = threadIdx.x; k < cnt; k += 64) {
+                    const int64_t t = ts_base + (int64_t)qpay[k].ts_off;
+                    qbq[k] = t / kSecW;
+                    qrank_ws[k] = t - t % si;
+                }
+                __syncthreads();
+            }
             if (agg && threadIdx.x == 0) {
                 // StatisticSlot in aggregate: a parameter-only resource's decisions never read its node,
                 // and every event of a 500 ms second-window bucket (nested in one minute bucket) sees the
@@ -1540,7 +1555,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                 };
                 for (uint32_t k = 0; k < cnt; ++k) {
                     const Payload q = qpay[k];
-                    const int64_t bq = par_ok ? qbq[k] : (ts_base + (int64_t)q.ts_off) / kSecW;
+                    const int64_t bq = qbq[k];
                     if (bq != cur) {
                         flush();
                         cur = bq;
@@ -1556,9 +1571,13 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                         if (qrt[k] < rt_min) rt_min = qrt[k];
                         if (q.idx & F_ERROR) exc += a;
                         threads -= 1;
-                        if (dgo)
-                            for (uint32_t b = 0; b < R.n_cbs; ++b)
-                                cb_on_complete(lcbs[b], ts_base + (int64_t)q.ts_off, qrt[k], (q.idx & F_ERROR) != 0);
+                        if (dgo) {
+                            const int64_t t = ts_base + (int64_t)q.ts_off;
+                            if (R.n_cbs == 1) cb_on_complete_ws(lcbs[0], t, qrank_ws[k], qrt[k], (q.idx & F_ERROR) != 0);
+                            else
+                                for (uint32_t b = 0; b < R.n_cbs; ++b)
+                                    cb_on_complete(lcbs[b], t, qrt[k], (q.idx & F_ERROR) != 0);
+                        }
                     } else if (dgo) {  // DegradeSlot
                         if (degrade_pass(lcbs, R.n_cbs, ts_base + (int64_t)q.ts_off)) {
                             pass_acq += a;
