@@ -316,7 +316,7 @@ __device__ int8_t rater_can_pass(const Ctx &c, FlowRuleDev &r, int64_t *node, in
 __device__ PEntry *ptab_get(PEntry *tab, uint32_t mask, uint32_t owner, uint64_t value, bool create,
                             uint32_t *overflow) {
     uint32_t h = (uint32_t)splitmix64(value ^ ((uint64_t)owner << 40) ^ 0xA5A5ULL) & mask;
-    // the maps stay at most half full (FlowEngine::ensure_maps), so a long probe sequence means a
+    // the maps stay at most a quarter full (FlowEngine::ensure_maps), so a long probe sequence means a
     // broken invariant: fail the batch (overflow -> -ENOMEM) instead of walking the whole table
     const uint32_t max_probe = mask < 4096u ? mask : 4096u;
     for (uint32_t probe = 0; probe <= max_probe; ++probe) {
@@ -2076,7 +2076,7 @@ int FlowEngine::load_degrade_rules(const sga_degrade_rule *rules, size_t n) {
 static size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
 void FlowEngine::grow_map(DevBuf<PEntry> &tab, size_t &ub, size_t add) {
-    if (ub + add <= tab.n / 2) {
+    if (ub + add <= tab.n / 4) {
         ub += add;
         return;
     }
@@ -2088,9 +2088,9 @@ void FlowEngine::grow_map(DevBuf<PEntry> &tab, size_t &ub, size_t add) {
     SGA_HIP_CHECK(hipMemcpyAsync(&keys, d_keycount.p, 4, hipMemcpyDeviceToHost, stream));
     SGA_HIP_CHECK(hipStreamSynchronize(stream));
     ub = keys;
-    if (ub + add > tab.n / 2) {  // rehash into a table that stays at most half full after this batch
+    if (ub + add > tab.n / 4) {  // rehash into a table that stays at most a quarter full after this batch
         size_t nn = tab.n;
-        while (ub + add > nn / 2) nn <<= 1;
+        while (ub + add > nn / 4) nn <<= 1;
         DevBuf<PEntry> nt;
         nt.alloc(nn);
         hipLaunchKernelGGL(k_clear_ptab, dim3((unsigned)((nn + kT - 1) / kT)), dim3(kT), 0, stream, nt.p, (uint32_t)nn);
@@ -2111,7 +2111,7 @@ int FlowEngine::ensure_maps(size_t m) {
     for (const ResDev &r : h_res) mpr = std::max<uint32_t>(mpr, r.n_prules);
     if (!mpr) return 0;
     const size_t limit = (size_t)1 << 31;  // 32-bit map indices
-    if ((pkeys_ub + m * mpr) * 2 > limit || (tkeys_ub + m) * 2 > limit) return SGA_ENOMEM;
+    if ((pkeys_ub + m * mpr) * 4 > limit || (tkeys_ub + m) * 4 > limit) return SGA_ENOMEM;
     grow_map(d_ptab, pkeys_ub, m * mpr);
     grow_map(d_ttab, tkeys_ub, m);
     return 0;

@@ -129,7 +129,7 @@ struct FlowEngine {
     DevBuf<uint32_t> d_overflow;
     DevBuf<uint32_t> d_keycount;
     // upper bounds of the keys held by the parameter / thread-count maps (exact after a count);
-    // the maps are rehashed into twice the room before a batch could fill them past half
+    // the maps are rehashed into more room before a batch could fill them past a quarter
     size_t pkeys_ub = 0, tkeys_ub = 0;
     int ensure_maps(size_t m);
     void grow_map(DevBuf<PEntry> &tab, size_t &ub, size_t add);
