@@ -483,6 +483,19 @@ __device__ bool degrade_pass(CbDev *cbs, uint32_t n, int64_t t) {
     return true;
 }
 
+// handleStateChangeWhenThresholdExceeded of a CLOSED breaker over its current window's counts
+// (ResponseTimeCircuitBreaker.java:88-106, ExceptionCircuitBreaker.java:75-94)
+__device__ __forceinline__ bool cb_trips(const CbDev &b, int64_t badc, int64_t total) {
+    if (total < b.min_req) return false;
+    if (b.grade == 0) {
+        const double ratio = (double)badc * 1.0 / (double)total;
+        return ratio > b.slow_ratio || (ratio == b.slow_ratio && b.slow_ratio == 1.0);
+    }
+    double cur = (double)badc;
+    if (b.grade == 1) cur = (double)badc * 1.0 / (double)total;
+    return cur > b.count;
+}
+
 // AbstractCircuitBreaker.onRequestComplete with the stat window start ws = t - t % statIntervalMs
 // given (k_lheavy computes it for a chunk on all lanes)
 __device__ void cb_on_complete_ws(CbDev &b, int64_t t, int64_t ws, int64_t rt, bool error) {
@@ -512,16 +525,7 @@ __device__ void cb_on_complete_ws(CbDev &b, int64_t t, int64_t ws, int64_t rt, b
         badc = b.st_bad;
         total = b.st_total;
     }
-    if (total < b.min_req) return;
-    if (is_rt) {
-        const double ratio = (double)badc * 1.0 / (double)total;
-        if (ratio > b.slow_ratio) cb_to_open(b, t);
-        if (ratio == b.slow_ratio && b.slow_ratio == 1.0) cb_to_open(b, t);
-    } else {
-        double cur = (double)badc;
-        if (b.grade == 1) cur = (double)badc * 1.0 / (double)total;
-        if (cur > b.count) cb_to_open(b, t);
-    }
+    if (cb_trips(b, badc, total)) cb_to_open(b, t);
 }
 
 __device__ __forceinline__ void cb_on_complete(CbDev &b, int64_t t, int64_t rt, bool error) {
@@ -1327,6 +1331,8 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
     __shared__ uint32_t lcnt[64];
     __shared__ int64_t qbq[kHeavyChunk];  // second-window bucket (t / 500) of each event
     __shared__ int64_t qrank_ws[kHeavyChunk];  // breaker-only resources: the breaker's stat window start
+    __shared__ int64_t sbad[kHeavyChunk], stot[kHeavyChunk];  // CLOSED-breaker scan: window counts after each exit
+    __shared__ int bulk_end;                  // events [0, bulk_end) need no breaker call (-1: no bulk)
     const Ctx c{st, max_rt, nullptr, 0, 0, nullptr};
     constexpr uint64_t kLEmpty = ~0ull;  // a value equal to it bypasses the cache (map path)
     constexpr uint32_t kGiNone = 0xFFFFFFFFu, kGiFail = 0xFFFFFFFEu;
@@ -1527,6 +1533,74 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     qrank_ws[k] = t - t % si;
                 }
                 __syncthreads();
+                // A CLOSED breaker lets every entry pass; its exits only add to the stat window until
+                // one trips it.  The window counts after every exit come from one segmented scan
+                // (segments = stat windows, non-decreasing over the chunk's exits), the first exit
+                // whose counts trip it ends the bulk part; lane 0 replays from there.
+                const int lane = threadIdx.x;
+                if (lane == 0) bulk_end = -1;
+                const CbDev &b0 = lcbs[0];
+                if (R.n_cbs == 1 && b0.state == 0) {
+                    int64_t cws = b0.st_start, cbad = b0.st_bad, ctot = b0.st_total;  // running window
+                    bool mono = true;
+                    uint32_t trip = 0xFFFFFFFFu;
+                    for (uint32_t r0 = 0; r0 < cnt && trip == 0xFFFFFFFFu; r0 += 64) {
+                        const uint32_t k = r0 + lane;
+                        const bool ex = k < cnt && (qpay[k].idx & F_EXIT);
+                        const int64_t ws = ex ? qrank_ws[k] : INT64_MIN;
+                        const bool badv = ex && (b0.grade == 0 ? qrt[k] > b0.max_allowed_rt
+                                                               : (qpay[k].idx & F_ERROR) != 0);
+                        // previous exit's window: prefix max over the lanes (windows only grow)
+                        int64_t pm = ws;
+#pragma unroll
+                        for (int o = 1; o < 64; o <<= 1) {
+                            const int64_t y = __shfl_up(pm, o, 64);
+                            if (lane >= o && y > pm) pm = y;
+                        }
+                        int64_t prev = __shfl_up(pm, 1, 64);
+                        if (lane == 0) prev = INT64_MIN;
+                        if (prev < cws) prev = cws;  // carry from earlier rounds / the breaker
+                        if (ex && prev != kAbsent && ws < prev) mono = false;  // clock went back: no bulk
+                        const bool head = ex && (prev == kAbsent || ws != prev);
+                        // segmented inclusive scan of (bad, total) over the exits
+                        int64_t sb = badv ? 1 : 0, stt = ex ? 1 : 0;
+                        uint32_t hd = head ? 1u : 0u;
+#pragma unroll
+                        for (int o = 1; o < 64; o <<= 1) {
+                            const int64_t yb = __shfl_up(sb, o, 64), yt = __shfl_up(stt, o, 64);
+                            const uint32_t yh = (uint32_t)__shfl_up((int)hd, o, 64);
+                            if (lane >= o && !hd) {
+                                sb += yb;
+                                stt += yt;
+                            }
+                            if (lane >= o) hd |= yh;
+                        }
+                        if (!hd) {  // no window start before this lane in the round: continue the carry
+                            sb += (prev == cws) ? cbad : 0;
+                            stt += (prev == cws) ? ctot : 0;
+                        }
+                        if (ex) {
+                            sbad[k] = sb;
+                            stot[k] = stt;
+                        }
+                        const uint64_t tb = __ballot(ex && cb_trips(b0, sb, stt));
+                        if (!__all(mono)) {
+                            trip = 0xFFFFFFFEu;
+                            break;
+                        }
+                        if (tb) trip = r0 + (uint32_t)__ffsll((unsigned long long)tb) - 1;
+                        // carry: the round's last exit
+                        const uint64_t eb = __ballot(ex);
+                        if (eb) {
+                            const int last = 63 - __clzll((unsigned long long)eb);
+                            cws = __shfl(ws, last, 64);
+                            cbad = __shfl(sb, last, 64);
+                            ctot = __shfl(stt, last, 64);
+                        }
+                    }
+                    if (lane == 0 && trip != 0xFFFFFFFEu) bulk_end = trip == 0xFFFFFFFFu ? (int)cnt : (int)trip;
+                }
+                __syncthreads();
             }
             if (agg && threadIdx.x == 0) {
                 // StatisticSlot in aggregate: a parameter-only resource's decisions never read its node,
@@ -1553,8 +1627,19 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     }
                     lnode[kNodeThreads] += threads;
                 };
+                const int bend = dgo ? bulk_end : -1;
+                int last_ex = -1;  // last exit inside the bulk part
+                auto bulk_done = [&]() {  // the breaker's window as the scan left it after the bulk part
+                    if (last_ex >= 0) {
+                        lcbs[0].st_start = qrank_ws[last_ex];
+                        lcbs[0].st_bad = sbad[last_ex];
+                        lcbs[0].st_total = stot[last_ex];
+                    }
+                };
                 for (uint32_t k = 0; k < cnt; ++k) {
                     const Payload q = qpay[k];
+                    if ((int)k == bend) bulk_done();
+                    const bool bulk = (int)k < bend;
                     const int64_t bq = qbq[k];
                     if (bq != cur) {
                         flush();
@@ -1571,7 +1656,9 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                         if (qrt[k] < rt_min) rt_min = qrt[k];
                         if (q.idx & F_ERROR) exc += a;
                         threads -= 1;
-                        if (dgo) {
+                        if (bulk) {
+                            last_ex = (int)k;
+                        } else if (dgo) {
                             const int64_t t = ts_base + (int64_t)q.ts_off;
                             if (R.n_cbs == 1) cb_on_complete_ws(lcbs[0], t, qrank_ws[k], qrt[k], (q.idx & F_ERROR) != 0);
                             else
@@ -1579,7 +1666,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                                     cb_on_complete(lcbs[b], t, qrt[k], (q.idx & F_ERROR) != 0);
                         }
                     } else if (dgo) {  // DegradeSlot
-                        if (degrade_pass(lcbs, R.n_cbs, ts_base + (int64_t)q.ts_off)) {
+                        if (bulk || degrade_pass(lcbs, R.n_cbs, ts_base + (int64_t)q.ts_off)) {
                             pass_acq += a;
                             threads += 1;
                             qd[k] = D_PASS;
@@ -1600,6 +1687,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     }
                 }
                 flush();
+                if (bend == (int)cnt) bulk_done();
             }
             if (!agg && threadIdx.x == 0) {
                 Ctx cc = c;
