@@ -1602,92 +1602,131 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                 }
                 __syncthreads();
             }
-            if (agg && threadIdx.x == 0) {
-                // StatisticSlot in aggregate: a parameter-only resource's decisions never read its node,
-                // and every event of a 500 ms second-window bucket (nested in one minute bucket) sees the
-                // same window rotation, so each run of consecutive same-bucket events is applied once at
-                // its first event's time (commutative adds, min RT, thread count)
-                int64_t cur = INT64_MIN, tf = 0, pass_acq = 0, block_acq = 0, succ = 0, rt_sum = 0,
-                        rt_min = INT64_MAX, exc = 0, threads = 0;
+            if (agg) {
+                // Decisions first (a breaker or a parameter verdict never reads the node statistics),
+                // then StatisticSlot in aggregate over all lanes: a parameter-only or breaker-only
+                // resource's decisions never read its node, and every event of a 500 ms second-window
+                // bucket (nested in one minute bucket) sees the same window rotation, so each run of
+                // consecutive same-bucket events is applied once at its first event's time
+                // (commutative adds, min RT, thread count).
+                const int lane = threadIdx.x;
+                if (dgo) {
+                    const int bend = bulk_end;
+                    const uint32_t nb = bend > 0 ? (uint32_t)bend : 0u;
+                    int le = -1;  // last exit inside the bulk part
+                    for (uint32_t k = lane; k < nb; k += 64) {
+                        if (qpay[k].idx & F_EXIT) le = (int)k;
+                        else {  // a CLOSED breaker lets the entry pass
+                            qd[k] = D_PASS;
+                            qw[k] = 0;
+                        }
+                    }
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) le = max(le, __shfl_xor(le, o, 64));
+                    if (lane == 0) {
+                        if (le >= 0) {  // the breaker's window as the scan left it after the bulk part
+                            lcbs[0].st_start = qrank_ws[le];
+                            lcbs[0].st_bad = sbad[le];
+                            lcbs[0].st_total = stot[le];
+                        }
+                        for (uint32_t k = nb; k < cnt; ++k) {  // the breakers in order from the trip on
+                            const Payload q = qpay[k];
+                            const int64_t t = ts_base + (int64_t)q.ts_off;
+                            if (q.idx & F_EXIT) {
+                                if (R.n_cbs == 1) cb_on_complete_ws(lcbs[0], t, qrank_ws[k], qrt[k], (q.idx & F_ERROR) != 0);
+                                else
+                                    for (uint32_t b = 0; b < R.n_cbs; ++b)
+                                        cb_on_complete(lcbs[b], t, qrt[k], (q.idx & F_ERROR) != 0);
+                            } else {  // DegradeSlot
+                                qd[k] = degrade_pass(lcbs, R.n_cbs, t) ? D_PASS : D_BLOCK_DEGRADE;
+                                qw[k] = 0;
+                            }
+                        }
+                    }
+                } else {
+                    for (uint32_t k = lane; k < cnt; k += 64) {
+                        if (qpay[k].idx & F_EXIT) continue;
+                        if (qpre[k] == 2) {  // ParamFlowException
+                            qd[k] = D_BLOCK_PARAM;
+                            qw[k] = 0;
+                        } else {  // passed (or the rule does not apply: no argument)
+                            qd[k] = D_PASS;
+                            qw[k] = qpre[k] == 1 ? qpw[k] : 0;
+                        }
+                    }
+                }
+                __syncthreads();
+                // s: pass acquire, block acquire, success, rt sum, exceptions, thread delta (uniform
+                // over the lanes; lane 0 applies them)
+                int64_t cur = INT64_MIN, tf = 0, s[6] = {0, 0, 0, 0, 0, 0}, rt_min = INT64_MAX;
                 bool any = false;
                 auto flush = [&]() {
-                    if (!any) return;
+                    if (!any || lane != 0) return;
                     int64_t *b = sec_current(lnode, tf, max_rt);
                     int64_t *bm = min_current(lnode, tf, max_rt);
                     int64_t *bs[2] = {b, bm};
                     for (int u = 0; u < 2; ++u) {
                         int64_t *x = bs[u];
                         if (!x) continue;
-                        x[MB_PASS] += pass_acq;
-                        x[MB_BLOCK] += block_acq;
-                        x[MB_SUCC] += succ;
-                        x[MB_RT] += rt_sum;
+                        x[MB_PASS] += s[0];
+                        x[MB_BLOCK] += s[1];
+                        x[MB_SUCC] += s[2];
+                        x[MB_RT] += s[3];
                         if (rt_min < x[MB_MINRT]) x[MB_MINRT] = rt_min;
-                        x[MB_EXC] += exc;
+                        x[MB_EXC] += s[4];
                     }
-                    lnode[kNodeThreads] += threads;
+                    lnode[kNodeThreads] += s[5];
                 };
-                const int bend = dgo ? bulk_end : -1;
-                int last_ex = -1;  // last exit inside the bulk part
-                auto bulk_done = [&]() {  // the breaker's window as the scan left it after the bulk part
-                    if (last_ex >= 0) {
-                        lcbs[0].st_start = qrank_ws[last_ex];
-                        lcbs[0].st_bad = sbad[last_ex];
-                        lcbs[0].st_total = stot[last_ex];
-                    }
+                auto open = [&](uint32_t k) {  // a new bucket run starts at event k
+                    flush();
+                    cur = qbq[k];
+                    tf = ts_base + (int64_t)qpay[k].ts_off;
+                    for (int i = 0; i < 6; ++i) s[i] = 0;
+                    rt_min = INT64_MAX;
+                    any = true;
                 };
-                for (uint32_t k = 0; k < cnt; ++k) {
+                auto contrib = [&](uint32_t k, int64_t *v, int64_t &mn) {
                     const Payload q = qpay[k];
-                    if ((int)k == bend) bulk_done();
-                    const bool bulk = (int)k < bend;
-                    const int64_t bq = qbq[k];
-                    if (bq != cur) {
-                        flush();
-                        cur = bq;
-                        tf = ts_base + (int64_t)q.ts_off;
-                        pass_acq = block_acq = succ = rt_sum = exc = threads = 0;
-                        rt_min = INT64_MAX;
-                        any = true;
-                    }
                     const int64_t a = (int64_t)(int)(q.acq_prio & 0x7FFFFFFFu);
-                    if (q.idx & F_EXIT) {  // chain_exit: statistics in aggregate, breakers in order
-                        succ += a;
-                        rt_sum += qrt[k];
-                        if (qrt[k] < rt_min) rt_min = qrt[k];
-                        if (q.idx & F_ERROR) exc += a;
-                        threads -= 1;
-                        if (bulk) {
-                            last_ex = (int)k;
-                        } else if (dgo) {
-                            const int64_t t = ts_base + (int64_t)q.ts_off;
-                            if (R.n_cbs == 1) cb_on_complete_ws(lcbs[0], t, qrank_ws[k], qrt[k], (q.idx & F_ERROR) != 0);
-                            else
-                                for (uint32_t b = 0; b < R.n_cbs; ++b)
-                                    cb_on_complete(lcbs[b], t, qrt[k], (q.idx & F_ERROR) != 0);
+                    if (q.idx & F_EXIT) {  // chain_exit
+                        v[2] += a;
+                        v[3] += qrt[k];
+                        if (qrt[k] < mn) mn = qrt[k];
+                        if (q.idx & F_ERROR) v[4] += a;
+                        v[5] -= 1;
+                    } else if (qd[k] == D_PASS) {
+                        v[0] += a;
+                        v[5] += 1;
+                    } else {
+                        v[1] += a;
+                    }
+                };
+                for (uint32_t r0 = 0; r0 < cnt; r0 += 64) {
+                    const uint32_t k = r0 + lane;
+                    const bool valid = k < cnt;
+                    const int64_t b0 = qbq[r0];
+                    if (__all(!valid || qbq[k] == b0)) {  // one bucket over the round: a wave reduction
+                        if (b0 != cur) open(r0);
+                        int64_t v[6] = {0, 0, 0, 0, 0, 0}, mn = INT64_MAX;
+                        if (valid) contrib(k, v, mn);
+#pragma unroll
+                        for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+                            for (int i = 0; i < 6; ++i) v[i] += __shfl_xor(v[i], o, 64);
+                            const int64_t y = __shfl_xor(mn, o, 64);
+                            if (y < mn) mn = y;
                         }
-                    } else if (dgo) {  // DegradeSlot
-                        if (bulk || degrade_pass(lcbs, R.n_cbs, ts_base + (int64_t)q.ts_off)) {
-                            pass_acq += a;
-                            threads += 1;
-                            qd[k] = D_PASS;
-                        } else {
-                            block_acq += a;
-                            qd[k] = D_BLOCK_DEGRADE;
+                        for (int i = 0; i < 6; ++i) s[i] += v[i];
+                        if (mn < rt_min) rt_min = mn;
+                    } else {  // a bucket boundary inside the round: event by event (uniform)
+                        const uint32_t e = min(cnt, r0 + 64);
+                        for (uint32_t j = r0; j < e; ++j) {
+                            if (qbq[j] != cur) open(j);
+                            contrib(j, s, rt_min);
                         }
-                        qw[k] = 0;
-                    } else if (qpre[k] == 2) {  // ParamFlowException
-                        block_acq += a;
-                        qd[k] = D_BLOCK_PARAM;
-                        qw[k] = 0;
-                    } else {  // passed (or the rule does not apply: no argument)
-                        pass_acq += a;
-                        threads += 1;
-                        qd[k] = D_PASS;
-                        qw[k] = qpre[k] == 1 ? qpw[k] : 0;
                     }
                 }
                 flush();
-                if (bend == (int)cnt) bulk_done();
             }
             if (!agg && threadIdx.x == 0) {
                 Ctx cc = c;
