@@ -1332,7 +1332,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
     __shared__ int64_t qbq[kHeavyChunk];  // second-window bucket (t / 500) of each event
     __shared__ int64_t qrank_ws[kHeavyChunk];  // breaker-only resources: the breaker's stat window start
     __shared__ int64_t sbad[kHeavyChunk], stot[kHeavyChunk];  // CLOSED-breaker scan: window counts after each exit
-    __shared__ int bulk_end;                  // events [0, bulk_end) need no breaker call (-1: no bulk)
+    __shared__ int bulk_end;                  // breaker-only resources: where the next bulk part starts
     const Ctx c{st, max_rt, nullptr, 0, 0, nullptr};
     constexpr uint64_t kLEmpty = ~0ull;  // a value equal to it bypasses the cache (map path)
     constexpr uint32_t kGiNone = 0xFFFFFFFFu, kGiFail = 0xFFFFFFFEu;
@@ -1533,74 +1533,6 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     qrank_ws[k] = t - t % si;
                 }
                 __syncthreads();
-                // A CLOSED breaker lets every entry pass; its exits only add to the stat window until
-                // one trips it.  The window counts after every exit come from one segmented scan
-                // (segments = stat windows, non-decreasing over the chunk's exits), the first exit
-                // whose counts trip it ends the bulk part; lane 0 replays from there.
-                const int lane = threadIdx.x;
-                if (lane == 0) bulk_end = -1;
-                const CbDev &b0 = lcbs[0];
-                if (R.n_cbs == 1 && b0.state == 0) {
-                    int64_t cws = b0.st_start, cbad = b0.st_bad, ctot = b0.st_total;  // running window
-                    bool mono = true;
-                    uint32_t trip = 0xFFFFFFFFu;
-                    for (uint32_t r0 = 0; r0 < cnt && trip == 0xFFFFFFFFu; r0 += 64) {
-                        const uint32_t k = r0 + lane;
-                        const bool ex = k < cnt && (qpay[k].idx & F_EXIT);
-                        const int64_t ws = ex ? qrank_ws[k] : INT64_MIN;
-                        const bool badv = ex && (b0.grade == 0 ? qrt[k] > b0.max_allowed_rt
-                                                               : (qpay[k].idx & F_ERROR) != 0);
-                        // previous exit's window: prefix max over the lanes (windows only grow)
-                        int64_t pm = ws;
-#pragma unroll
-                        for (int o = 1; o < 64; o <<= 1) {
-                            const int64_t y = __shfl_up(pm, o, 64);
-                            if (lane >= o && y > pm) pm = y;
-                        }
-                        int64_t prev = __shfl_up(pm, 1, 64);
-                        if (lane == 0) prev = INT64_MIN;
-                        if (prev < cws) prev = cws;  // carry from earlier rounds / the breaker
-                        if (ex && prev != kAbsent && ws < prev) mono = false;  // clock went back: no bulk
-                        const bool head = ex && (prev == kAbsent || ws != prev);
-                        // segmented inclusive scan of (bad, total) over the exits
-                        int64_t sb = badv ? 1 : 0, stt = ex ? 1 : 0;
-                        uint32_t hd = head ? 1u : 0u;
-#pragma unroll
-                        for (int o = 1; o < 64; o <<= 1) {
-                            const int64_t yb = __shfl_up(sb, o, 64), yt = __shfl_up(stt, o, 64);
-                            const uint32_t yh = (uint32_t)__shfl_up((int)hd, o, 64);
-                            if (lane >= o && !hd) {
-                                sb += yb;
-                                stt += yt;
-                            }
-                            if (lane >= o) hd |= yh;
-                        }
-                        if (!hd) {  // no window start before this lane in the round: continue the carry
-                            sb += (prev == cws) ? cbad : 0;
-                            stt += (prev == cws) ? ctot : 0;
-                        }
-                        if (ex) {
-                            sbad[k] = sb;
-                            stot[k] = stt;
-                        }
-                        const uint64_t tb = __ballot(ex && cb_trips(b0, sb, stt));
-                        if (!__all(mono)) {
-                            trip = 0xFFFFFFFEu;
-                            break;
-                        }
-                        if (tb) trip = r0 + (uint32_t)__ffsll((unsigned long long)tb) - 1;
-                        // carry: the round's last exit
-                        const uint64_t eb = __ballot(ex);
-                        if (eb) {
-                            const int last = 63 - __clzll((unsigned long long)eb);
-                            cws = __shfl(ws, last, 64);
-                            cbad = __shfl(sb, last, 64);
-                            ctot = __shfl(stt, last, 64);
-                        }
-                    }
-                    if (lane == 0 && trip != 0xFFFFFFFEu) bulk_end = trip == 0xFFFFFFFFu ? (int)cnt : (int)trip;
-                }
-                __syncthreads();
             }
             if (agg) {
                 // Decisions first (a breaker or a parameter verdict never reads the node statistics),
@@ -1611,37 +1543,129 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                 // (commutative adds, min RT, thread count).
                 const int lane = threadIdx.x;
                 if (dgo) {
-                    const int bend = bulk_end;
-                    const uint32_t nb = bend > 0 ? (uint32_t)bend : 0u;
-                    int le = -1;  // last exit inside the bulk part
-                    for (uint32_t k = lane; k < nb; k += 64) {
-                        if (qpay[k].idx & F_EXIT) le = (int)k;
-                        else {  // a CLOSED breaker lets the entry pass
-                            qd[k] = D_PASS;
-                            qw[k] = 0;
-                        }
-                    }
+                    // One breaker: the chunk alternates bulk parts and short replays.  A CLOSED breaker
+                    // lets every entry pass and its exits only add to the stat window until one trips
+                    // it; an OPEN one blocks every entry before its retry time and its exits only
+                    // count.  One segmented scan over the exits (segments = stat windows,
+                    // non-decreasing) gives the window counts after every exit; the bulk part ends at
+                    // the first exit whose counts trip a CLOSED breaker (cb_trips, the predicate of
+                    // cb_on_complete) or at the first entry at or after an OPEN breaker's retry time.
+                    // Lane 0 replays from there while the breaker is HALF_OPEN.  Several breakers, or
+                    // a stat window that goes back, replay in order on lane 0.
+                    uint32_t pos = 0;
+                    while (pos < cnt) {
+                        const CbDev &b0 = lcbs[0];
+                        const int bst = b0.state;
+                        uint32_t end = pos;
+                        bool seq_rest = R.n_cbs != 1;
+                        if (!seq_rest && bst != 2) {
+                            int64_t cws = b0.st_start, cbad = b0.st_bad, ctot = b0.st_total;  // running window
+                            uint32_t stop = 0xFFFFFFFFu;
+                            for (uint32_t r0 = pos; r0 < cnt; r0 += 64) {
+                                const uint32_t k = r0 + lane;
+                                const bool valid = k < cnt;
+                                const bool ex = valid && (qpay[k].idx & F_EXIT);
+                                const int64_t ws = ex ? qrank_ws[k] : INT64_MIN;
+                                const bool badv = ex && (b0.grade == 0 ? qrt[k] > b0.max_allowed_rt
+                                                                       : (qpay[k].idx & F_ERROR) != 0);
+                                // previous exit's window: prefix max over the lanes (windows only grow)
+                                int64_t pm = ws;
 #pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) le = max(le, __shfl_xor(le, o, 64));
-                    if (lane == 0) {
-                        if (le >= 0) {  // the breaker's window as the scan left it after the bulk part
-                            lcbs[0].st_start = qrank_ws[le];
-                            lcbs[0].st_bad = sbad[le];
-                            lcbs[0].st_total = stot[le];
+                                for (int o = 1; o < 64; o <<= 1) {
+                                    const int64_t y = __shfl_up(pm, o, 64);
+                                    if (lane >= o && y > pm) pm = y;
+                                }
+                                int64_t prev = __shfl_up(pm, 1, 64);
+                                if (lane == 0) prev = INT64_MIN;
+                                if (prev < cws) prev = cws;  // carry from earlier rounds / the breaker
+                                const bool mono = !(ex && prev != kAbsent && ws < prev);
+                                if (!__all(mono)) {  // the clock went back: the rest replays in order
+                                    stop = r0;
+                                    seq_rest = true;
+                                    break;
+                                }
+                                const bool head = ex && (prev == kAbsent || ws != prev);
+                                // segmented inclusive scan of (bad, total) over the exits
+                                int64_t sb = badv ? 1 : 0, stt = ex ? 1 : 0;
+                                uint32_t hd = head ? 1u : 0u;
+#pragma unroll
+                                for (int o = 1; o < 64; o <<= 1) {
+                                    const int64_t yb = __shfl_up(sb, o, 64), yt = __shfl_up(stt, o, 64);
+                                    const uint32_t yh = (uint32_t)__shfl_up((int)hd, o, 64);
+                                    if (lane >= o && !hd) {
+                                        sb += yb;
+                                        stt += yt;
+                                    }
+                                    if (lane >= o) hd |= yh;
+                                }
+                                if (!hd) {  // no window start before this lane in the round: continue the carry
+                                    sb += (prev == cws) ? cbad : 0;
+                                    stt += (prev == cws) ? ctot : 0;
+                                }
+                                if (ex) {
+                                    sbad[k] = sb;
+                                    stot[k] = stt;
+                                }
+                                const uint64_t tb =
+                                    bst == 0 ? __ballot(ex && cb_trips(b0, sb, stt))
+                                             : __ballot(valid && !ex &&
+                                                        ts_base + (int64_t)qpay[k].ts_off >= b0.next_retry);
+                                if (tb) {
+                                    stop = r0 + (uint32_t)__ffsll((unsigned long long)tb) - 1;
+                                    break;
+                                }
+                                // carry: the round's last exit
+                                const uint64_t eb = __ballot(ex);
+                                if (eb) {
+                                    const int last = 63 - __clzll((unsigned long long)eb);
+                                    cws = __shfl(ws, last, 64);
+                                    cbad = __shfl(sb, last, 64);
+                                    ctot = __shfl(stt, last, 64);
+                                }
+                            }
+                            end = stop == 0xFFFFFFFFu ? cnt : stop;
                         }
-                        for (uint32_t k = nb; k < cnt; ++k) {  // the breakers in order from the trip on
-                            const Payload q = qpay[k];
-                            const int64_t t = ts_base + (int64_t)q.ts_off;
-                            if (q.idx & F_EXIT) {
-                                if (R.n_cbs == 1) cb_on_complete_ws(lcbs[0], t, qrank_ws[k], qrt[k], (q.idx & F_ERROR) != 0);
-                                else
-                                    for (uint32_t b = 0; b < R.n_cbs; ++b)
-                                        cb_on_complete(lcbs[b], t, qrt[k], (q.idx & F_ERROR) != 0);
-                            } else {  // DegradeSlot
-                                qd[k] = degrade_pass(lcbs, R.n_cbs, t) ? D_PASS : D_BLOCK_DEGRADE;
+                        int le = -1;  // last exit inside the bulk part
+                        for (uint32_t k = pos + lane; k < end; k += 64) {
+                            if (qpay[k].idx & F_EXIT) le = (int)k;
+                            else {
+                                qd[k] = bst == 0 ? D_PASS : D_BLOCK_DEGRADE;
                                 qw[k] = 0;
                             }
                         }
+#pragma unroll
+                        for (int o = 1; o < 64; o <<= 1) le = max(le, __shfl_xor(le, o, 64));
+                        __syncthreads();
+                        if (lane == 0) {
+                            if (le >= 0) {  // the breaker's window as the scan left it after the bulk part
+                                lcbs[0].st_start = qrank_ws[le];
+                                lcbs[0].st_bad = sbad[le];
+                                lcbs[0].st_total = stot[le];
+                            }
+                            auto step = [&](uint32_t k) {
+                                const Payload q = qpay[k];
+                                const int64_t t = ts_base + (int64_t)q.ts_off;
+                                if (q.idx & F_EXIT) {
+                                    if (R.n_cbs == 1) cb_on_complete_ws(lcbs[0], t, qrank_ws[k], qrt[k], (q.idx & F_ERROR) != 0);
+                                    else
+                                        for (uint32_t b = 0; b < R.n_cbs; ++b)
+                                            cb_on_complete(lcbs[b], t, qrt[k], (q.idx & F_ERROR) != 0);
+                                } else {  // DegradeSlot
+                                    qd[k] = degrade_pass(lcbs, R.n_cbs, t) ? D_PASS : D_BLOCK_DEGRADE;
+                                    qw[k] = 0;
+                                }
+                            };
+                            uint32_t k = end;
+                            if (seq_rest) {
+                                for (; k < cnt; ++k) step(k);
+                            } else if (k < cnt) {  // the event that ended the bulk part, then HALF_OPEN
+                                step(k++);
+                                while (k < cnt && lcbs[0].state == 2) step(k++);
+                            }
+                            bulk_end = (int)k;
+                        }
+                        __syncthreads();
+                        pos = (uint32_t)bulk_end;
                     }
                 } else {
                     for (uint32_t k = lane; k < cnt; k += 64) {

@@ -210,6 +210,23 @@ def test_breaker_heavy_resources(seed):
              max_batch=mb)
 
 
+@pytest.mark.parametrize("seed", [35, 36])
+def test_breaker_heavy_open_close_cycles(seed):
+    """One breaker per hot resource that trips, stays OPEN, probes HALF_OPEN and closes many times
+    within a batch (the C5 pattern): k_lheavy alternates CLOSED bulk parts (entries pass up to the
+    tripping exit), OPEN bulk parts (entries blocked up to the retry time, exits only count) and
+    lane-0 replays while HALF_OPEN."""
+    n_res = 3
+    degrade = [{"resource": 0, "grade": 0, "count": 30, "time_window": 1, "slow_ratio_threshold": 0.5,
+                "min_request_amount": 5, "stat_interval_ms": 1000},
+               {"resource": 1, "grade": 1, "count": 0.3, "time_window": 1, "min_request_amount": 5,
+                "stat_interval_ms": 400},
+               {"resource": 2, "grade": 2, "count": 10, "time_window": 2, "stat_interval_ms": 1000}]
+    for mb in (1 << 16, 3000):
+        _run(n_res, degrade=degrade, n_entries=40000, seed=seed, gap_mean=0.02, err_pct=0.3, rt_max=60,
+             max_batch=mb)
+
+
 def test_rule_reload_between_batches():
     n_res = 10
     rng = np.random.default_rng(5)

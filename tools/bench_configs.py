@@ -125,11 +125,14 @@ def c5(rng, n):
     hits = np.ones(nreq, np.int32)
     ts = T0 + (np.arange(nreq) // 1000)
     best = None
-    for _ in range(3):
+    for rep in range(3):
+        # each repetition continues the clock (a stream that restarts at T0 would go back in time
+        # and send every rule through the per-request replay)
+        ts_rep = ts + rep * (nreq // 1000 + 10_000)
         t = time.perf_counter()
         for lo in range(0, nreq, 1 << 20):
             hi = min(nreq, lo + (1 << 20))
-            svc.should_rate_limit(off[lo:hi + 1] - off[lo], dfid[off[lo]:off[hi]], hits[lo:hi], ts[lo:hi])
+            svc.should_rate_limit(off[lo:hi + 1] - off[lo], dfid[off[lo]:off[hi]], hits[lo:hi], ts_rep[lo:hi])
         dt = time.perf_counter() - t
         best = dt if best is None else min(best, dt)
     eng.close()
