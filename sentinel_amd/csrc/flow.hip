@@ -313,6 +313,10 @@ __device__ int8_t rater_can_pass(const Ctx &c, FlowRuleDev &r, int64_t *node, in
 // k_lheavy's dedupe / find / insert phases.  Lanes of other owners only need a slot's owner to skip
 // it, and the claiming CAS publishes the owner itself, so no fence is needed.  (An agent-scope
 // release per insert writes back the XCD's L2 and made C4's 10M-value maps crawl.)
+__device__ __forceinline__ uint32_t ptab_home(uint32_t mask, uint32_t owner, uint64_t value) {
+    return (uint32_t)splitmix64(value ^ ((uint64_t)owner << 40) ^ 0xA5A5ULL) & mask;
+}
+
 __device__ PEntry *ptab_get(PEntry *tab, uint32_t mask, uint32_t owner, uint64_t value, bool create,
                             uint32_t *overflow) {
     uint32_t h = (uint32_t)splitmix64(value ^ ((uint64_t)owner << 40) ^ 0xA5A5ULL) & mask;
@@ -1413,38 +1417,115 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     qslot[k] = sl;
                 }
                 __syncthreads();
-                // 2. find the values' entries (lookups only: nothing is being filled meanwhile)
-                for (int h = threadIdx.x; h < kHeavySlots; h += 64) {
-                    if (lval[h] == kLEmpty) continue;
-                    PEntry *e = ptab_get(st.ptab, st.pmask, cache_p->id + 1, lval[h], false, st.overflow);
-                    if (e) {
-                        lgi[h] = (uint32_t)(e - st.ptab);
-                        lent[h] = *e;
+                // 2. find the values' entries (lookups only: nothing is being filled meanwhile).  The
+                //    maps stay at most a quarter full, so most values resolve at their home slot: the
+                //    home slots of kG of a lane's LDS slots are read together, and only a value whose
+                //    home holds another key walks its probe sequence (ptab_get).
+                constexpr int kSl = kHeavySlots / 64, kG = 8;
+                const uint32_t pown = cache_p->id + 1, town = res + 1;
+                uint32_t pfree = 0, tfree = 0;  // bit i: LDS slot lane + 64 i is absent and its home is free
+                for (int g0 = 0; g0 < kSl; g0 += kG) {
+                    uint64_t val[kG], pv[kG], tv[kG];
+                    uint32_t po[kG], to[kG];
+#pragma unroll
+                    for (int u = 0; u < kG; ++u) {
+                        val[u] = lval[threadIdx.x + 64 * (g0 + u)];
+                        po[u] = to[u] = 0xFFFFFFFFu;
+                        pv[u] = tv[u] = 0;
+                        if (val[u] == kLEmpty) continue;
+                        const PEntry *pe = &st.ptab[ptab_home(st.pmask, pown, val[u])];
+                        po[u] = __hip_atomic_load(&pe->owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        pv[u] = pe->value;
+                        if (pt) {
+                            const PEntry *te = &st.ttab[ptab_home(st.tmask, town, val[u])];
+                            to[u] = __hip_atomic_load(&te->owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            tv[u] = te->value;
+                        }
                     }
-                    if (pt) {
-                        PEntry *te = ptab_get(st.ttab, st.tmask, res + 1, lval[h], false, st.overflow);
-                        if (te) {
-                            tgi[h] = (uint32_t)(te - st.ttab);
-                            tent[h] = *te;
+#pragma unroll
+                    for (int u = 0; u < kG; ++u) {
+                        if (val[u] == kLEmpty) continue;
+                        const int h = threadIdx.x + 64 * (g0 + u);
+                        PEntry *e;
+                        if (po[u] == 0) {
+                            e = nullptr;
+                            pfree |= 1u << (g0 + u);
+                        } else if (po[u] == pown && pv[u] == val[u]) {
+                            e = &st.ptab[ptab_home(st.pmask, pown, val[u])];
+                        } else {
+                            e = ptab_get(st.ptab, st.pmask, pown, val[u], false, st.overflow);
+                        }
+                        if (e) {
+                            lgi[h] = (uint32_t)(e - st.ptab);
+                            lent[h] = *e;
+                        }
+                        if (pt) {
+                            PEntry *te;
+                            if (to[u] == 0) {
+                                te = nullptr;
+                                tfree |= 1u << (g0 + u);
+                            } else if (to[u] == town && tv[u] == val[u]) {
+                                te = &st.ttab[ptab_home(st.tmask, town, val[u])];
+                            } else {
+                                te = ptab_get(st.ttab, st.tmask, town, val[u], false, st.overflow);
+                            }
+                            if (te) {
+                                tgi[h] = (uint32_t)(te - st.ttab);
+                                tent[h] = *te;
+                            }
                         }
                     }
                 }
                 __syncthreads();
                 // 3. insert the absent ones (a fresh entry is the reference's "not seen yet"; creating
-                //    it for an event that never reaches the rule changes nothing)
-                for (int h = threadIdx.x; h < kHeavySlots; h += 64) {
-                    if (lval[h] == kLEmpty || lgi[h] != kGiNone) continue;
-                    PEntry *e = ptab_insert_absent(st.ptab, st.pmask, cache_p->id + 1, lval[h], st.overflow);
-                    lgi[h] = e ? (uint32_t)(e - st.ptab) : kGiFail;
-                    lent[h] = PEntry{lval[h], cache_p->id + 1, 0, kPAbsent, kPAbsent};
-                }
-                if (pt)
-                    for (int h = threadIdx.x; h < kHeavySlots; h += 64) {
-                        if (lval[h] == kLEmpty || tgi[h] != kGiNone) continue;
-                        PEntry *te = ptab_insert_absent(st.ttab, st.tmask, res + 1, lval[h], st.overflow);
-                        tgi[h] = te ? (uint32_t)(te - st.ttab) : kGiFail;
-                        tent[h] = PEntry{lval[h], res + 1, 0, kPAbsent, kPAbsent};
+                //    it for an event that never reaches the rule changes nothing): the claims of the
+                //    free home slots go out together, a lost claim walks the probe sequence
+                for (int g0 = 0; g0 < kSl; g0 += kG) {
+                    uint32_t pc[kG], tc[kG];
+#pragma unroll
+                    for (int u = 0; u < kG; ++u) {
+                        const int h = threadIdx.x + 64 * (g0 + u);
+                        pc[u] = tc[u] = 1u;
+                        const uint64_t v = lval[h];
+                        if (v == kLEmpty) continue;
+                        if (lgi[h] == kGiNone && ((pfree >> (g0 + u)) & 1u))
+                            pc[u] = atomicCAS(&st.ptab[ptab_home(st.pmask, pown, v)].owner, 0u, pown);
+                        if (pt && tgi[h] == kGiNone && ((tfree >> (g0 + u)) & 1u))
+                            tc[u] = atomicCAS(&st.ttab[ptab_home(st.tmask, town, v)].owner, 0u, town);
                     }
+#pragma unroll
+                    for (int u = 0; u < kG; ++u) {
+                        const int h = threadIdx.x + 64 * (g0 + u);
+                        const uint64_t v = lval[h];
+                        if (v == kLEmpty) continue;
+                        if (lgi[h] == kGiNone) {
+                            PEntry *e;
+                            if (pc[u] == 0u) {  // claimed the home slot (the CAS publishes the owner)
+                                e = &st.ptab[ptab_home(st.pmask, pown, v)];
+                                e->value = v;
+                                e->a = kPAbsent;
+                                e->b = kPAbsent;
+                            } else {
+                                e = ptab_insert_absent(st.ptab, st.pmask, pown, v, st.overflow);
+                            }
+                            lgi[h] = e ? (uint32_t)(e - st.ptab) : kGiFail;
+                            lent[h] = PEntry{v, pown, 0, kPAbsent, kPAbsent};
+                        }
+                        if (pt && tgi[h] == kGiNone) {
+                            PEntry *te;
+                            if (tc[u] == 0u) {
+                                te = &st.ttab[ptab_home(st.tmask, town, v)];
+                                te->value = v;
+                                te->a = kPAbsent;
+                                te->b = kPAbsent;
+                            } else {
+                                te = ptab_insert_absent(st.ttab, st.tmask, town, v, st.overflow);
+                            }
+                            tgi[h] = te ? (uint32_t)(te - st.ttab) : kGiFail;
+                            tent[h] = PEntry{v, town, 0, kPAbsent, kPAbsent};
+                        }
+                    }
+                }
             }
             __syncthreads();
             tick(1);
