@@ -1417,6 +1417,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     qslot[k] = sl;
                 }
                 __syncthreads();
+                tick(6);
                 // 2. find the values' entries (lookups only: nothing is being filled meanwhile).  The
                 //    maps stay at most a quarter full, so most values resolve at their home slot: the
                 //    home slots of kG of a lane's LDS slots are read together, and only a value whose
@@ -1477,6 +1478,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     }
                 }
                 __syncthreads();
+                tick(7);
                 // 3. insert the absent ones (a fresh entry is the reference's "not seen yet"; creating
                 //    it for an event that never reaches the rule changes nothing): the claims of the
                 //    free home slots go out together, a lost claim walks the probe sequence
@@ -1881,6 +1883,8 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
         }
         if (prof && threadIdx.x == 0) {
             for (int i = 0; i < 5; ++i) prof[blockIdx.x * 8 + i] += tk[i];
+            prof[blockIdx.x * 8 + 6] += tk[6];
+            prof[blockIdx.x * 8 + 7] += tk[7];
             prof[blockIdx.x * 8 + 5] += je - jb;
         }
         for (uint32_t r = r0 + threadIdx.x; r < r1; r += 64) sc.run_mode[r] = RUN_DONE;
@@ -2369,10 +2373,10 @@ void print_heavy_prof() {
     int best = 0;
     for (int b = 0; b < 1024; ++b)
         if (h[b * 8 + 5] > h[best * 8 + 5]) best = b;
-    fprintf(stderr, "k_lheavy busiest workgroup %d: %llu events; ms stage %.2f dedupe+find+insert %.2f "
-            "lanes %.2f replay %.2f writeback+stores %.2f (100 MHz wall clock)\n", best,
+    fprintf(stderr, "k_lheavy busiest workgroup %d: %llu events; ms stage %.2f insert %.2f "
+            "lanes %.2f replay %.2f writeback+stores %.2f dedupe %.2f find %.2f (100 MHz wall clock)\n", best,
             (unsigned long long)h[best * 8 + 5], h[best * 8] / 1e5, h[best * 8 + 1] / 1e5, h[best * 8 + 2] / 1e5,
-            h[best * 8 + 3] / 1e5, h[best * 8 + 4] / 1e5);
+            h[best * 8 + 3] / 1e5, h[best * 8 + 4] / 1e5, h[best * 8 + 6] / 1e5, h[best * 8 + 7] / 1e5);
 }
 
 int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int64_t *ts, const int32_t *acquire,
