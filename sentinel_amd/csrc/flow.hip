@@ -1093,17 +1093,17 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
     for (uint32_t fl = blockIdx.x * kT + threadIdx.x; fl < nflows; fl += gridDim.x * kT) {
         const uint32_t r0 = sc.flow_first_run[fl];
         const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
-        // a flow is one resource's runs: its record is read once, not once per run (a resource with
-        // many runs would wait on that load chain at every run)
-        const uint32_t res = sc.run_slot[r0];
-        const ResDev R = st.res[res];
-        int64_t *node = st.node + (size_t)res * kNodeWords;
-        // a long event-by-event replay goes to k_lheavy (its state in LDS)
-        if ((R.fast & 5u) == 0 && sc.run_end[r1 - 1] - sc.run_start[r0] >= kHeavyEvents) {
-            sc.heavy[atomicAdd(&sc.counters[8], 1u)] = fl;
-            continue;
+        {  // a long event-by-event replay goes to k_lheavy (its state in LDS)
+            const uint32_t res = sc.run_slot[r0];
+            if ((st.res[res].fast & 5u) == 0 && sc.run_end[r1 - 1] - sc.run_start[r0] >= kHeavyEvents) {
+                sc.heavy[atomicAdd(&sc.counters[8], 1u)] = fl;
+                continue;
+            }
         }
         for (uint32_t r = r0; r < r1; ++r) {
+            const uint32_t res = sc.run_slot[r];
+            const ResDev R = st.res[res];
+            int64_t *node = st.node + (size_t)res * kNodeWords;
             const uint32_t j0 = sc.run_start[r], j1 = sc.run_end[r];
             const uint32_t nent = sc.run_nent[r];
             const int32_t a = sc.run_amin[r];
