@@ -182,6 +182,8 @@ def main():
         stats = torch.cat([tmax, tsum])
     wall_max, gpu_max, total_events, total_touched = [float(x) for x in stats]
 
+    path = eng.batch_info()  # which path the last timed batch took (hot path or plain sort)
+
     # correctness spot-check of the last batch's statuses (cheap invariants)
     res = outs[(nb - 1) & 1][: batches[-1][5]].cpu().numpy().view(np.uint64)
     status = ((res >> np.uint64(48)) & np.uint64(0xFF)).astype(np.int8)
@@ -234,6 +236,7 @@ def main():
                          "gpu_ms_per_step": gpu_max / args.steps * 1e3},
             "cpu_baseline": cpu_baseline,
             "ok_fraction_last_batch": frac_ok,
+            "last_batch_path": path,
         }
         print(json.dumps(line), flush=True)
     eng.close()

@@ -135,11 +135,11 @@ int sga_set_namespace_limit(sga_engine *e, const char *ns, double max_allowed_qp
 int sga_set_connected_count(sga_engine *e, const char *ns, int32_t connected);
 
 /* Engine tuning, no reference counterpart (decisions never depend on it): the cluster token
- * path answers the requests of its hottest rules (at most 4096, each with at least
- * `min_requests` requests in the previous batch) without sorting them -- a per-rule counting
- * sort in arrival order plus results stored in input order.
- * enabled = 0 sends every request through the radix sort.  Default: disabled (experimental: it
- * is parity-exact but measured slower than the plain sort at C3), min_requests 64. */
+ * path decides the requests of its hottest rules (at most 4096, each with at least `min_requests`
+ * requests in the previous batch, one window length) in input order without sorting them: each
+ * request's rank among its rule's requests comes from a per-segment count and a column prefix
+ * (DESIGN.md section 3).  enabled = 0 sends every request through the radix sort.  Default:
+ * enabled, min_requests 64. */
 int sga_set_hot_rules(sga_engine *e, int32_t enabled, uint32_t min_requests);
 
 /* Batched DefaultTokenService.requestToken over host buffers; synchronous.
@@ -150,22 +150,19 @@ int sga_request_tokens(sga_engine *e, const int64_t *flow_id, const int32_t *acq
 
 /* Same over DEVICE buffers, asynchronous on `hip_stream` (NULL = engine stream).
  * Timestamps are ts_base + ts_off[i].  Inputs must stay valid until the stream
- * reaches the end of the call's work. */
+ * reaches the end of the call's work.  A caller stream first waits for all earlier engine work
+ * and the engine stream then waits for the batch, so later engine calls (rule loads, other
+ * batches on any stream) never overlap it. */
 int sga_request_tokens_device(sga_engine *e, const int64_t *d_flow_id, const int32_t *d_acquire,
                               const uint8_t *d_prioritized, int64_t ts_base, const uint32_t *d_ts_off, size_t n,
                               sga_token_result *d_out, void *hip_stream);
 
-/* Pipelined form of sga_request_tokens_device for a stream of batches (a token server draining
- * its request queue): returns once the batch is queued.  Stage A of a batch (classify, sort,
- * runs -- no rule state) runs beside stage B of the previous one (flows, results -- the rule
- * state, in submission order) on the engine's own streams, so decisions are the same as one
- * synchronous call per batch in submission order.  The inputs must be ready on `hip_stream`
- * (null: the engine stream) when the call is made; they and d_out must stay valid until
- * sga_sync / sga_stream_wait.  Any other engine call first waits for queued batches. */
+/* Round-1 name of sga_request_tokens_device (kept for its callers): the device entry already
+ * returns once the batch is queued on the engine stream, and batches run in submission order. */
 int sga_request_tokens_device_async(sga_engine *e, const int64_t *d_flow_id, const int32_t *d_acquire,
                                     const uint8_t *d_prio, int64_t ts_base, const uint32_t *d_ts_off, size_t n,
                                     sga_token_result *d_out, void *hip_stream);
-/* Make `hip_stream` (null: the engine stream) wait for every queued batch (no host wait). */
+/* Make `hip_stream` wait for every queued engine batch (no host wait). */
 int sga_stream_wait(sga_engine *e, void *hip_stream);
 /* Host wait for every queued batch. */
 int sga_sync(sga_engine *e);
@@ -225,6 +222,19 @@ int sga_cluster_param_top_values(sga_engine *e, int64_t flow_id, int64_t now, ui
 
 /* Number of flow slots and device bytes of window state (for roofline tools). */
 int sga_cluster_stats(sga_engine *e, uint64_t *n_active_rules, uint64_t *state_bytes);
+/* Host-side event routing for a node of G engines (no reference
+ * counterpart -- the reference runs one token server): order[] receives the request indices of a
+ * global batch grouped by shard = splitmix64(flowId) mod G, arrival order kept inside a shard (a
+ * stable counting sort); shard g's requests are order[shard_off[g] .. shard_off[g + 1]).
+ * n_threads host threads (slices counted in parallel, one offset scan).  n < 2^32. */
+int sga_route_shards(const int64_t *flow_id, size_t n, uint32_t n_shards, uint32_t n_threads, uint32_t *order,
+                     uint64_t *shard_off);
+
+/* Diagnostics of the last token batch (no reference counterpart): out[0] 1 when it ran the hot
+ * path, [1] fallback flags, [2] sorted elements, [3] cold elements, [4] prioritized hot requests,
+ * [5] hot rules for the next batch, [6..7] first / last hot bucket delta, [8] hot runs that
+ * needed a replay (always 0), [9] in-segment bucket boundaries.  Synchronous. */
+int sga_cluster_batch_info(sga_engine *e, uint32_t *out, size_t n);
 
 /* ---------------------------------------------------------------------------
  * Cluster concurrency tokens: TokenService.requestConcurrentToken / releaseConcurrentToken

@@ -118,6 +118,8 @@ SIGNATURES = {
     "sga_sync": (C.c_int, [C.c_void_p]),
     "sga_cluster_metric_sums": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.POINTER(C.c_int64)]),
     "sga_cluster_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "sga_cluster_batch_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t]),
+    "sga_route_shards": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
     "sga_load_cluster_param_rules": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(SgaClusterParamRule), C.c_size_t]),
     "sga_request_param_tokens": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                            C.c_size_t, C.c_void_p]),

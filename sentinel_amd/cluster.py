@@ -60,7 +60,7 @@ class Engine:
 
     def __init__(self, device: int = 0, max_batch: int = 1 << 20, max_rules: int = 1 << 16,
                  exceed_count: float = 1.0, max_occupy_ratio: float = 1.0, max_param_keys: int = 0,
-                 hot_rules: bool = False, hot_min_requests: int = 64):
+                 hot_rules: bool = True, hot_min_requests: int = 64):
         L = _lib.load()
         cfg = SgaConfig()
         L.sga_config_default(C.byref(cfg))
@@ -89,11 +89,20 @@ class Engine:
         return c
 
     def set_hot_rules(self, enabled: bool = True, min_requests: int = 64):
-        """Engine tuning (sga_set_hot_rules): the hottest rules skip the sort (experimental, off by
-        default: measured slower at C3, DESIGN.md section 3).  Decisions do not depend on it;
+        """Engine tuning (sga_set_hot_rules): the hottest rules (at most 4096, each with at least
+        `min_requests` requests in the previous batch) are decided in input order without being
+        sorted (the hot path, DESIGN.md section 3; on by default).  Decisions do not depend on it;
         tests use min_requests=1 to send nearly every rule down the hot path."""
         _lib.check(_lib.load().sga_set_hot_rules(self._h, 1 if enabled else 0, int(min_requests)), self._h,
                    "sga_set_hot_rules")
+
+    def batch_info(self) -> dict:
+        """Path of the last token batch (sga_cluster_batch_info)."""
+        v = (C.c_uint32 * 10)()
+        _lib.check(_lib.load().sga_cluster_batch_info(self._h, v, 10), self._h, "sga_cluster_batch_info")
+        keys = ("hot_mode", "flags", "n_sort", "n_cold", "n_prio", "n_hot_next", "bd_lo", "bd_hi", "hot_err",
+                "n_pre")
+        return dict(zip(keys, [int(x) for x in v]))
 
     @property
     def handle(self):

@@ -332,7 +332,7 @@ __global__ __launch_bounds__(kRunThreads) void k_runs_up(const uint64_t *__restr
     __shared__ Agg wagg[kRunWaves];
     __shared__ uint32_t wval[kRunWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (dn) n = min(n, *dn);  // hot/cold split: elements past the cold + hot count are stale
+    if (dn) n = min(n, *dn);  // hot path: the sorted cold elements come first, then prioritized hot ones
     const uint32_t e0 = blockIdx.x * kTileElems + threadIdx.x * kPerThread;
     uint64_t x[kPerThread];
     el_load_blk(el, e0, n, invalid_key, x);
@@ -424,8 +424,7 @@ __global__ __launch_bounds__(kTileScanThreads) void k_runs_tiles(const Agg *__re
 // Per tile: run and flow records, the list of prioritized positions, and each wave's carry
 // (for k_results, which re-derives run ids and prioritized ranks instead of reading them).
 __global__ __launch_bounds__(kRunThreads) void k_runs_down(const uint64_t *__restrict__ el, uint32_t invalid_key,
-                                                        const Agg *__restrict__ tile_carry, BatchScratch sc,
-                                                        int hot) {
+                                                        const Agg *__restrict__ tile_carry, BatchScratch sc) {
     __shared__ Agg wagg[kRunWaves];
     const uint32_t nvalid = sc.counters[0];
     const uint32_t base = blockIdx.x * kTileElems;
@@ -474,13 +473,7 @@ __global__ __launch_bounds__(kRunThreads) void k_runs_down(const uint64_t *__res
             sc.run_bd[rid] = (uint8_t)bd;
             sc.run_p0[rid] = run.np - p;
         }
-        if (fh) {
-            sc.flow_first_run[run.nf - 1] = rid;
-            if (hot && e >= sc.counters[8]) {  // hot region: k_hot_results finds the rule's runs here
-                const uint32_t hid = sc.hot_of[el_slot(cur)];
-                if (hid < (uint32_t)kHot) sc.hot_first_run[hid] = rid;
-            }
-        }
+        if (fh) sc.flow_first_run[run.nf - 1] = rid;
         if (p) sc.plist[run.np - 1] = e;
         const uint64_t nx = k + 1 < kPerThread ? x[k + 1 < kPerThread ? k + 1 : k] : after;
         if (e + 1 >= nvalid || el_runkey(nx) != el_runkey(cur)) {
@@ -672,7 +665,6 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
     if (a <= 0 || (old != kAbsent && ws < old)) return false;
     if (ri.cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) return false;
     int64_t bp = 0, hstart = kAbsent, hpass = 0;
-    uint32_t vmask = 0;  // valid buckets other than the current one
     {
         // (start, PASS) pairs: one 16-byte load per bucket
         const int4 *v = reinterpret_cast<const int4 *>(R.r);
@@ -683,10 +675,7 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
                 hstart = w;
                 hpass = pv;
             }
-            if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) {
-                bp += pv;
-                vmask |= 1u << (jj & 31);
-            }
+            if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) bp += pv;
         }
     }
     const bool rot = old == kAbsent || ws > old;
@@ -734,10 +723,13 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
     const uint32_t np_after = ri.cp_tot - cpf;
     uint32_t cw = 0;
     if (np_after > 0) {
-        // WAITING over the same valid buckets (only runs with prioritized blocked requests read it)
+        // WAITING over the same valid buckets (only runs with prioritized blocked requests read it;
+        // validity is re-tested per bucket, so any sampleCount works)
         int64_t w0 = c[CEV_WAITING];
-        for (int jj = 0; jj < P.S; ++jj)
-            if (vmask & (1u << (jj & 31))) w0 += R.cnt(CEV_WAITING, jj);
+        for (int jj = 0; jj < P.S; ++jj) {
+            const int64_t w = R.start(jj);
+            if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) w0 += R.cnt(CEV_WAITING, jj);
+        }
         if (!occ_loaded) o = st.occ[s];
         const double latest = (double)(s0 + (int64_t)f * a) / P.isec;
         const double lim = st.max_occupy_ratio * thr;
@@ -862,10 +854,8 @@ __global__ __launch_bounds__(kThreads) void k_flows_slow(ClusterState st, BatchS
 // Same tile geometry as k_runs_down; each wave starts from the carry k_runs_down stored and
 // re-derives every request's run id and prioritized rank, then writes its TokenResult.
 __global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const uint64_t *__restrict__ el,
-                                                         uint32_t invalid_key, uint64_t *__restrict__ out, int hot) {
-    // hot/cold split: only the cold region [0, counters[8]) -- hot requests are answered in input
-    // order by k_hot_results
-    const uint32_t nvalid = hot ? min(sc.counters[0], sc.counters[8]) : sc.counters[0];
+                                                         uint32_t invalid_key, uint64_t *__restrict__ out) {
+    const uint32_t nvalid = sc.counters[0];
     const uint32_t base = blockIdx.x * kTileElems;
     if (base >= nvalid) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -949,459 +939,662 @@ __global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const 
     }
 }
 
-// ---------------------------------------------------------------- hot/cold split
-// Under Zipf skew a few thousand rules carry most requests.  Those "hot" rules (hot id < kHot,
-// chosen from the previous batch's counts) skip the radix sort: classify ranks each hot request
-// among the tile's requests of the same rule (wave-private LDS counters, waves own contiguous
-// 1024-request slices so ranks follow arrival order), the per-tile counts are scanned over tiles
-// per hot id, and one scatter places every hot request at
-//   hot region start + hot_base[hid] + prefix over earlier tiles + in-tile rank
-// -- a stable counting sort by rule.  The hot region is appended to the sorted cold elements, so
-// runs / flows see exactly the arrival-ordered per-rule segments they see without the split.
-// k_hot_results then answers hot requests in INPUT order (coalesced stores) from the run records.
-constexpr int kHidShift = 52, kRankShift = 40;
-constexpr uint64_t kLow40 = ((uint64_t)1 << 40) - 1;
-constexpr int kHotGroup = 16;  // tiles per group of the tile scan
-constexpr int kClsWaves = kThreads / 64;
-constexpr int kClsRounds = kTileElems / kThreads;  // 64-request rounds per wave
+// ---------------------------------------------------------------- hot path
+// Under Zipf skew a few thousand rules carry most requests (C3: the 4096 hottest of 1M rules carry
+// 77 % of them).  Those "hot" rules (hot id < kHot, picked from the previous batch's counts, all
+// with one window length W) are decided without moving their requests:
+//   k_hot_classify  one pass in input order.  Each wave owns kHotSeg consecutive requests and ranks
+//                   every hot request among the segment's requests of its rule (12 ballots match
+//                   equal hot ids, wave-private LDS counters keep arrival order); rank and bucket
+//                   are stored as a 4-byte code per request, the per-rule counts as one row per
+//                   segment.  Cold requests and prioritized hot ones are compacted into the sort
+//                   input, 1024-request segments in arrival order.
+//   k_hscan_*       column prefix of the count rows: rank of each segment's first request of each
+//                   hot rule.  The position where each window bucket starts is recorded (segment,
+//                   plus a snapshot of the counts before it when it falls inside a segment), so
+//                   each run's first rank follows.
+//   k_hot_flows     one wave per hot rule walks its runs (one per bucket of the batch) in time
+//                   order with the closed form of the cold path (pass prefix, occupy count).
+//   k_hot_final     each hot request's TokenResult from its rank, in input order (coalesced).
+// Prioritized hot requests are sorted as key nslots + 1 + hot id, after every cold element, so
+// each rule's prioritized ranks form one ascending list (the occupy decisions need the number of
+// prioritized requests before a position); k_prio_results answers them.
+// Preconditions, checked on the device before any rule state is touched (else the batch
+// re-classifies every request as cold and takes the sort path): timestamps non-decreasing over the
+// batch (then bucket order is arrival order for every rule), hot requests with acquireCount 1, at
+// most kHotBuckets buckets, no hot rule window holding a bucket newer than the batch.
+constexpr int kH1Waves = kThreads / 64;          // segments per workgroup
+constexpr int kSubRounds = kSubSeg / 64;          // rounds per compaction segment (16)
+constexpr int kSubPerSeg = kHotSeg / kSubSeg;     // 8
+constexpr int kH1Chunk = 4;                       // rounds whose loads are in flight together
+static_assert(kSubRounds % kH1Chunk == 0, "chunks tile a compaction segment");
+static_assert(kSubSeg * 4 == kRadix64Tile, "compaction segments are the sort's input segments");
+constexpr uint32_t kNoCode = 0xFFFFFFFFu;
 
-template <int kClsChunk>
-__global__ __launch_bounds__(kThreads) void k_classify_hot(ClusterState st, BatchScratch sc,
+// Cross-lane moves that do not depend on which lanes are active (a __shfl is a ds_bpermute, and the
+// compiler may sink one into a branch where its source lanes are masked off, which then read 0):
+// DPP wave shifts and v_readlane.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t lane0) {  // lane i <- lane i - 1
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t v, uint32_t lane63) {  // lane i <- lane i + 1
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)lane63, (int)v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ int64_t lane_i64(int64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ uint64_t match_hot_id(uint64_t mask, uint32_t key) {
+#pragma unroll
+    for (int b = 0; b < 12; ++b) {
+        const bool bit = (key >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        mask &= bit ? bb : ~bb;
+    }
+    return mask;
+}
+
+// In-order rank of the lanes of `part` among the wave's requests of their hot id so far.
+__device__ __forceinline__ uint32_t rank_part(uint16_t *c, uint64_t part, uint32_t hid, int lane, uint64_t lt) {
+    const bool in = (part >> lane) & 1ull;
+    const uint64_t peers = match_hot_id(part, hid);
+    uint32_t before = 0;
+    if (in) before = c[hid];
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t my = (uint32_t)__popcll(peers & lt);
+    if (in && my == 0) c[hid] = (uint16_t)(before + (uint32_t)__popcll(peers));
+    __builtin_amdgcn_wave_barrier();
+    return before + my;
+}
+
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t hot_count(const BatchScratch &sc) {
+    return min(sc.hot_ctl[0], (uint32_t)kHot);
+}
+
+// No hot rule's window may hold a bucket newer than the batch's first request (batches submitted
+// out of time order): the closed form needs each run's bucket to be the newest.
+__global__ __launch_bounds__(kThreads) void k_hot_precheck(ClusterState st, BatchScratch sc,
+                                                           const uint32_t *__restrict__ ts_off, int64_t ts_base,
+                                                           uint32_t n) {
+    const uint32_t h = blockIdx.x * kThreads + threadIdx.x;
+    if (h >= hot_count(sc) || n == 0) return;
+    const int64_t W = (int64_t)sc.hot_ctl[2];
+    const int64_t t0 = ts_base + (int64_t)ts_off[0];
+    const int64_t ws0 = t0 - t0 % W;
+    const uint32_t s = sc.hot_slot[h];
+    const SlotParam P = st.param[s];
+    bool bad = P.W != (int32_t)W || !P.active || P.S <= 1 || P.S > 64;
+    const Rec R = rec_of(st, P);
+    for (int j = 0; j < P.S && !bad; ++j) {
+        const int64_t w = R.start(j);
+        if (w != kAbsent && w > ws0) bad = true;
+    }
+    if (bad) atomicOr(&sc.counters[CTL_FLAGS], kFlagState);
+}
+
+// Pass 0: the hot classification above.  Pass 1 (launched always, returns at once unless pass 0
+// raised a fallback flag): every valid request becomes a cold element, overwriting pass 0's sort
+// input.  Both write the BAD_REQUEST / NO_RULE_EXISTS results directly.
+template <int kPass>
+__global__ __launch_bounds__(kThreads) void k_hot_classify(ClusterState st, BatchScratch sc,
                                                            const int64_t *__restrict__ flow_id,
                                                            const int32_t *__restrict__ acquire,
                                                            const uint8_t *__restrict__ prio,
                                                            const uint32_t *__restrict__ ts_off, int64_t ts_base,
-                                                           uint32_t n, int simple, uint64_t *__restrict__ out,
-                                                           int hist_d, uint32_t ntiles, uint32_t *__restrict__ hist) {
-    // Wave w owns the 1024-request segment [w * 1024, (w + 1) * 1024) of the tile and writes its
-    // cold elements from the segment start and its hot elements from the segment end as it goes
-    // (nothing held in registers across rounds); hot elements first carry their rank among the
-    // wave's requests of the rule, and the wave prefix is added in a fix-up pass at the end.
-    __shared__ uint16_t wcnt[kClsWaves][kHot];  // per wave, per hot id: requests so far -> wave prefix
-    __shared__ uint32_t h[1024];
-    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
+                                                           uint32_t n, uint64_t *__restrict__ out) {
+    __shared__ uint16_t cnt[kH1Waves][kHot];
+    const uint32_t flags0 = sc.counters[CTL_FLAGS];
+    if (kPass == 1 && !(flags0 & kFlagRerun)) return;
+    const uint32_t nhot = (kPass == 0 && !(flags0 & kFlagState)) ? hot_count(sc) : 0u;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lt = lanemask_lt64(lane);
-    for (uint32_t i = threadIdx.x; i < nhot; i += kThreads)
+    const uint32_t seg = blockIdx.x * kH1Waves + wave;
+    const uint32_t sbase = seg * kHotSeg;
+    uint16_t *c = cnt[wave];
+    if (nhot)
+        for (uint32_t h = lane; h < (uint32_t)kHot; h += 64) c[h] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const int64_t Wh = nhot ? (int64_t)sc.hot_ctl[2] : 1;
+    const int64_t qbh = div_pos(ts_base, Wh);
+    // the request before the segment (time order; a bucket boundary at the segment start)
+    bool has_prev = false;
+    uint32_t ptso = 0, pbd = 0;
+    if (nhot && sbase > 0 && sbase - 1 < n) {
+        ptso = ts_off[sbase - 1];
+        pbd = (uint32_t)min(div_pos(ts_base + (int64_t)ptso, Wh) - qbh, (int64_t)kHotBuckets);
+        has_prev = true;
+    }
+    uint32_t wflags = 0, ntot = 0, nprio = 0, bdmax = 0;
+    const bool use_prio = prio != nullptr;
+    for (int sub = 0; sub < kSubPerSeg; ++sub) {
+        const uint32_t ubase = sbase + sub * kSubSeg;
+        uint64_t *dst = sc.el_tile + (size_t)ubase;
+        uint32_t nc = 0;
+        if (ubase < n) {
+            int64_t fid[kH1Chunk], nfid[kH1Chunk];
+            int32_t acq[kH1Chunk], nacq[kH1Chunk];
+            uint32_t tso[kH1Chunk], pr[kH1Chunk], ntso[kH1Chunk], npr[kH1Chunk];
+            auto load_chunk = [&](int r0, int64_t (&f)[kH1Chunk], int32_t (&a)[kH1Chunk], uint32_t (&t)[kH1Chunk],
+                                  uint32_t (&p)[kH1Chunk]) {
 #pragma unroll
-        for (int w = 0; w < kClsWaves; ++w) wcnt[w][i] = 0;
-    const uint32_t nh = hist_d > 0 ? 1u << hist_d : 0u;
-    for (uint32_t d = threadIdx.x; d < nh; d += kThreads) h[d] = 0;
-    __syncthreads();
-    const uint32_t tile = blockIdx.x, tbase = tile * kTileElems;
-    const uint32_t wbase = tbase + wave * (kClsRounds * 64);
-    uint64_t *seg = sc.el_tile + wbase;            // cold from seg[0], hot from seg[1023] downwards
-    uint32_t nc_w = 0, nh_w = 0;
-    // software pipeline: the request fields of chunk c + 1 are loaded while chunk c is processed
-    int64_t fid[kClsChunk], nfid[kClsChunk];
-    int32_t acq[kClsChunk], nacq[kClsChunk];
-    uint32_t tso[kClsChunk], pr[kClsChunk], ntso[kClsChunk], npr[kClsChunk];
-    auto load_chunk = [&](int c, int64_t (&f)[kClsChunk], int32_t (&a)[kClsChunk], uint32_t (&t)[kClsChunk],
-                          uint32_t (&p)[kClsChunk]) {
+                for (int u = 0; u < kH1Chunk; ++u) {
+                    const uint32_t i = ubase + (r0 + u) * 64 + lane;
+                    f[u] = i < n ? flow_id[i] : 0;
+                    a[u] = i < n ? acquire[i] : 0;
+                    t[u] = i < n ? ts_off[i] : 0;
+                    p[u] = (i < n && use_prio) ? prio[i] : 0;
+                }
+            };
+            load_chunk(0, fid, acq, tso, pr);
+            for (int r0 = 0; r0 < kSubRounds; r0 += kH1Chunk) {
+                uint32_t hh[kH1Chunk], hf[kH1Chunk];
+                HashEntry e[kH1Chunk];
+                if (st.dense_n) {
+                    uint32_t d[kH1Chunk];
 #pragma unroll
-        for (int u = 0; u < kClsChunk; ++u) {
-            const uint32_t i = wbase + (c + u) * 64 + lane;
-            f[u] = i < n ? flow_id[i] : 0;
-            a[u] = i < n ? acquire[i] : 0;
-            t[u] = i < n ? ts_off[i] : 0;
-            p[u] = (i < n && !simple && prio) ? prio[i] : 0;
-        }
-    };
-    load_chunk(0, fid, acq, tso, pr);
-    for (int c = 0; c < kClsRounds; c += kClsChunk) {
-        uint32_t hh[kClsChunk], hf[kClsChunk];
-        HashEntry e[kClsChunk];
-        if (st.dense_n) {  // the hot id is gathered beside the slot entry (both keyed by flowId)
-            uint32_t d[kClsChunk];
+                    for (int u = 0; u < kH1Chunk; ++u) {
+                        const bool in = fid[u] >= 1 && fid[u] <= (int64_t)st.dense_n;
+                        d[u] = in ? st.dense[fid[u] - 1] : ~0u;
+                        hf[u] = (in && nhot) ? st.hot_fid[fid[u] - 1] : kColdId;
+                    }
 #pragma unroll
-            for (int u = 0; u < kClsChunk; ++u) {
-                const bool in = fid[u] >= 1 && fid[u] <= (int64_t)st.dense_n;
-                d[u] = in ? st.dense[fid[u] - 1] : ~0u;
-                hf[u] = (in && nhot) ? st.hot_fid[fid[u] - 1] : kColdId;
-            }
-#pragma unroll
-            for (int u = 0; u < kClsChunk; ++u) {
-                hh[u] = 0;
-                e[u] = d[u] == ~0u ? HashEntry{-1, 0, 0} : HashEntry{fid[u], d[u] & 0xFFFFFFu, st.wtab[d[u] >> 24]};
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < kClsChunk; ++u) {
-                hh[u] = (uint32_t)hash_flow_id(fid[u]) & st.hmask;
-                e[u] = fid[u] > 0 ? st.htab[hh[u]] : HashEntry{0, 0, 0};
-                hf[u] = kColdId;
-            }
-        }
-        if (c + kClsChunk < kClsRounds) load_chunk(c + kClsChunk, nfid, nacq, ntso, npr);
-#pragma unroll
-        for (int u = 0; u < kClsChunk; ++u) {
-            const uint32_t i = wbase + (c + u) * 64 + lane;
-            uint32_t kind = 0, hid = kColdId, slot = 0;
-            uint64_t x = 0;
-            if (i < n) {
-                const int64_t f = fid[u];
-                const int32_t a = acq[u];
-                int8_t status = TRS_OK;
-                HashEntry he = e[u];
-                if (!simple && (f <= 0 || a <= 0)) {
-                    status = TRS_BAD_REQUEST;
+                    for (int u = 0; u < kH1Chunk; ++u) {
+                        hh[u] = 0;
+                        e[u] = d[u] == ~0u ? HashEntry{-1, 0, 0}
+                                           : HashEntry{fid[u], d[u] & 0xFFFFFFu, st.wtab[d[u] >> 24]};
+                    }
                 } else {
-                    if (!st.dense_n && f > 0 && he.key != f && he.key != 0) {
-                        uint32_t q = hh[u];
-                        for (uint32_t probe = 1; probe <= st.hmask; ++probe) {
-                            q = (q + 1) & st.hmask;
-                            he = st.htab[q];
-                            if (he.key == f || he.key == 0) break;
+#pragma unroll
+                    for (int u = 0; u < kH1Chunk; ++u) {
+                        hh[u] = (uint32_t)hash_flow_id(fid[u]) & st.hmask;
+                        e[u] = fid[u] > 0 ? st.htab[hh[u]] : HashEntry{0, 0, 0};
+                        hf[u] = kColdId;
+                    }
+                }
+                if (r0 + kH1Chunk < kSubRounds) load_chunk(r0 + kH1Chunk, nfid, nacq, ntso, npr);
+#pragma unroll
+                for (int u = 0; u < kH1Chunk; ++u) {
+                    const uint32_t rbase = ubase + (r0 + u) * 64;
+                    const uint32_t i = rbase + lane;
+                    const bool valid = i < n;
+                    uint32_t kind = 0, hid = kColdId, slot = 0, bd6 = 0, a7 = 0;
+                    const uint32_t p = pr[u] ? 1u : 0u;
+                    if (valid) {
+                        const int64_t f = fid[u];
+                        const int32_t a = acq[u];
+                        int8_t status = TRS_OK;
+                        HashEntry he = e[u];
+                        if (f <= 0 || a <= 0) {
+                            status = TRS_BAD_REQUEST;
+                        } else {
+                            if (!st.dense_n && he.key != f && he.key != 0) {  // continue the linear probe
+                                uint32_t q = hh[u];
+                                for (uint32_t probe = 1; probe <= st.hmask; ++probe) {
+                                    q = (q + 1) & st.hmask;
+                                    he = st.htab[q];
+                                    if (he.key == f || he.key == 0) break;
+                                }
+                            }
+                            if (he.key != f) status = TRS_NO_RULE_EXISTS;
+                        }
+                        if (status != TRS_OK) {
+                            out[i] = pack_result(status, 0, 0);
+                        } else {
+                            slot = he.slot;
+                            const int64_t W = (int64_t)he.W;
+                            const int64_t bd = div_pos(ts_base + (int64_t)tso[u], W) - div_pos(ts_base, W);
+                            a7 = (a >= 1 && a <= (int32_t)kAcqMax) ? (uint32_t)a : 0u;
+                            bd6 = (uint32_t)bd;
+                            if (bd >= (int64_t)kBdEsc) {
+                                bd6 = kBdEsc;
+                                a7 = 0;
+                            }
+                            kind = 1;
+                            if (nhot) {
+                                hid = st.dense_n ? hf[u] : sc.hot_of[slot];
+                                if (hid < nhot) {
+                                    kind = 2;
+                                    if (a != 1) wflags |= kFlagMixed;
+                                }
+                            }
                         }
                     }
-                    if (he.key != f || f <= 0) status = TRS_NO_RULE_EXISTS;
-                }
-                if (status != TRS_OK) {
-                    out[i] = pack_result(status, 0, 0);
-                } else {
-                    slot = he.slot;
-                    const int64_t W = (int64_t)he.W;
-                    const int64_t bd = div_pos(ts_base + (int64_t)tso[u], W) - div_pos(ts_base, W);
-                    uint32_t a7 = (a >= 1 && a <= (int32_t)kAcqMax) ? (uint32_t)a : 0u;
-                    uint32_t bd6 = (uint32_t)bd;
-                    if (bd >= (int64_t)kBdEsc) {
-                        bd6 = kBdEsc;
-                        a7 = 0;
-                    }
-                    x = el_pack(slot, bd6, pr[u] ? 1u : 0u, a7, i);
-                    kind = 1;
+                    uint32_t r_in = 0, bdh = 0;
                     if (nhot) {
-                        hid = st.dense_n ? hf[u] : sc.hot_of[slot];
-                        if (hid < nhot) kind = 2;
+                        // time order and hot buckets: every request with an index counts
+                        const uint32_t pt = wave_shr1(tso[u], ptso);
+                        const bool hp = lane ? true : has_prev;
+                        const int64_t q = valid ? div_pos(ts_base + (int64_t)tso[u], Wh) - qbh : 0;
+                        bdh = (uint32_t)min(q, (int64_t)kHotBuckets);
+                        const uint32_t pb = wave_shr1(bdh, pbd);
+                        bool bnd_here = false;
+                        if (valid) {
+                            if (hp && tso[u] < pt) wflags |= kFlagUnsorted;
+                            if (q >= (int64_t)kHotBuckets) wflags |= kFlagBucket;
+                            if (i == 0) sc.counters[CTL_BDLO] = bdh;
+                            bdmax = max(bdmax, bdh);
+                            bnd_here = hp && bdh > pb;
+                        }
+                        ptso = lane_u32(tso[u], 63);
+                        pbd = lane_u32(bdh, 63);
+                        has_prev = true;
+                        // ranks; at a bucket boundary, the counts before it are snapshot first
+                        const uint64_t hb = __ballot(kind == 2);
+                        const uint64_t bm = __ballot(bnd_here);
+                        if (bm == 0) {
+                            if (hb) r_in = rank_part(c, hb, hid, lane, lt);
+                        } else {
+                            uint64_t rem = bm, done = 0;
+                            while (rem) {
+                                const int b = __builtin_ctzll(rem);
+                                rem &= rem - 1;
+                                const uint64_t below = (1ull << b) - 1ull;
+                                const uint64_t part = hb & below & ~done;
+                                if (part) {
+                                    const uint32_t rr = rank_part(c, part, hid, lane, lt);
+                                    if ((part >> lane) & 1ull) r_in = rr;
+                                }
+                                done |= below;
+                                const uint32_t bq = lane_u32(bdh, b);
+                                const uint32_t pq = lane_u32(pb, b);
+                                uint32_t krow = 0;
+                                if (rbase + b != sbase) {  // inside the segment: snapshot the counts
+                                    uint32_t k = 0;
+                                    if (lane == 0) k = atomicAdd(&sc.counters[CTL_NPRE], 1u);
+                                    k = lane_u32(k, 0);
+                                    if (k < (uint32_t)kHotPreRows) {
+                                        krow = k + 1;
+                                        for (uint32_t h = lane; h < (uint32_t)kHot; h += 64)
+                                            sc.hpre[(size_t)k * kHot + h] = c[h];
+                                    } else {
+                                        wflags |= kFlagPre;
+                                    }
+                                }
+                                if (lane == 0)
+                                    for (uint32_t qq = pq + 1; qq <= bq && qq < (uint32_t)kHotBuckets; ++qq)
+                                        sc.hbnd[qq] = (seg << 9) | krow;
+                            }
+                            const uint64_t part = hb & ~done;
+                            if (part) {
+                                const uint32_t rr = rank_part(c, part, hid, lane, lt);
+                                if ((part >> lane) & 1ull) r_in = rr;
+                            }
+                        }
+                        if (valid)
+                            sc.hcode[i] = (kind == 2 && !p) ? (hid | (r_in << 12) | (min(bdh, 63u) << 25)) : kNoCode;
                     }
+                    // cold elements and prioritized hot requests, compacted in arrival order
+                    uint64_t x = 0;
+                    if (kind == 1) x = el_pack(slot, bd6, p, a7, i);
+                    else if (kind == 2 && p) x = el_pack(st.nslots + 1 + hid, r_in >> 7, 1u, r_in & 127u, i);
+                    const bool emit = kind == 1 || (kind == 2 && p);
+                    const uint64_t em = __ballot(emit);
+                    if (emit) dst[nc + (uint32_t)__popcll(em & lt)] = x;
+                    nc += (uint32_t)__popcll(em);
+                    nprio += (uint32_t)__popcll(__ballot(kind == 2 && p));
+                }
+#pragma unroll
+                for (int u = 0; u < kH1Chunk; ++u) {
+                    fid[u] = nfid[u];
+                    acq[u] = nacq[u];
+                    tso[u] = ntso[u];
+                    pr[u] = npr[u];
                 }
             }
-            const uint64_t bc = __ballot(kind == 1);
-            if (kind == 1) {
-                seg[nc_w + (uint32_t)__popcll(bc & lt)] = x;
-                if (nh) atomicAdd(&h[slot & (nh - 1)], 1u);
-            }
-            nc_w += (uint32_t)__popcll(bc);
-            const uint64_t bh = __ballot(kind == 2);
-            if (bh) {
-                uint64_t peers = bh;
-#pragma unroll
-                for (int b = 0; b < 12; ++b) {
-                    const bool bit = (hid >> b) & 1u;
-                    const uint64_t bb = __ballot(bit);
-                    peers &= bit ? bb : ~bb;
-                }
-                uint32_t before = 0;
-                if (kind == 2) before = wcnt[wave][hid];
-                __builtin_amdgcn_wave_barrier();
-                const uint32_t my = (uint32_t)__popcll(peers & lt);
-                if (kind == 2 && my == 0) wcnt[wave][hid] = (uint16_t)(before + (uint32_t)__popcll(peers));
-                __builtin_amdgcn_wave_barrier();
-                if (kind == 2)
-                    seg[kClsRounds * 64 - 1 - (nh_w + (uint32_t)__popcll(bh & lt))] =
-                        ((uint64_t)hid << kHidShift) | ((uint64_t)(before + my) << kRankShift) | (x & kLow40);
-                nh_w += (uint32_t)__popcll(bh);
-            }
         }
-#pragma unroll
-        for (int u = 0; u < kClsChunk; ++u) {
-            fid[u] = nfid[u];
-            acq[u] = nacq[u];
-            tso[u] = ntso[u];
-            pr[u] = npr[u];
-        }
+        if (lane == 0) sc.tile_nc[seg * kSubPerSeg + sub] = nc;
+        ntot += nc;
     }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nhot; i += kThreads) {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int w = 0; w < kClsWaves; ++w) {
-            const uint32_t c = wcnt[w][i];
-            wcnt[w][i] = (uint16_t)acc;
-            acc += c;
-        }
-        sc.hcnt[(size_t)tile * kHot + i] = (uint16_t)acc;
+    if (nhot && sbase < n) {  // this segment's count row
+        uint32_t *row = reinterpret_cast<uint32_t *>(sc.hcnt + (size_t)seg * kHot);
+        const uint32_t *cw = reinterpret_cast<const uint32_t *>(c);
+        for (uint32_t k = lane; k < (nhot + 1) / 2; k += 64) row[k] = cw[k];
     }
-    if (lane == 0) {  // totals: k_hs_group / k_hs_base (same-address atomics from every wave serialize)
-        sc.tile_nc[tile * kClsWaves + wave] = nc_w;
-        sc.tile_nh[tile * kClsWaves + wave] = nh_w;
-    }
-    __syncthreads();
-    // fix-up: in-tile rank = wave prefix of the rule + rank within the wave (wave 0 has no prefix)
-    if (wave > 0) {
-        uint64_t *top = seg + kClsRounds * 64 - 1;
-        for (uint32_t k0 = 0; k0 < nh_w; k0 += 64 * 4) {
-            uint64_t x[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t k = k0 + u * 64 + lane;
-                x[u] = k < nh_w ? *(top - k) : 0ull;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t k = k0 + u * 64 + lane;
-                if (k < nh_w) *(top - k) = x[u] + ((uint64_t)wcnt[wave][(uint32_t)(x[u] >> kHidShift)] << kRankShift);
-            }
-        }
+    for (int o = 32; o > 0; o >>= 1) bdmax = max(bdmax, (uint32_t)__shfl_xor((int)bdmax, o, 64));
+    if (wflags) atomicOr(&sc.counters[CTL_FLAGS], wflags);
+    if (lane == 0) {
+        if (ntot) atomicAdd(&sc.counters[kPass ? CTL_NEL1 : CTL_NEL0], ntot);
+        if (nprio) atomicAdd(&sc.counters[CTL_NPRIO], nprio);
+        if (nhot && sbase < n) atomicMax(&sc.counters[CTL_BDHI], bdmax);
     }
-    for (uint32_t d = threadIdx.x; d < nh; d += kThreads) hist[(size_t)d * ntiles + tile] = h[d];
 }
 
-// Tile scan per hot id, in three steps over groups of kHotGroup tiles.
-__global__ __launch_bounds__(kThreads) void k_hs_group(BatchScratch sc, uint32_t ntiles) {
-    if (blockIdx.y == 0 && threadIdx.x < 64) {  // the group's cold / hot element counts
-        const uint32_t i = blockIdx.x * kHotGroup * kClsWaves + threadIdx.x;  // 64 = kHotGroup x kClsWaves
-        uint32_t c = i < ntiles * kClsWaves ? sc.tile_nc[i] : 0u;
-        uint32_t h = i < ntiles * kClsWaves ? sc.tile_nh[i] : 0u;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            c += (uint32_t)__shfl_down((int)c, o, 64);
-            h += (uint32_t)__shfl_down((int)h, o, 64);
-        }
-        if (threadIdx.x == 0) {
-            sc.hgcnt[2 * blockIdx.x] = c;
-            sc.hgcnt[2 * blockIdx.x + 1] = h;
-        }
-    }
-    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
-    const uint32_t hid = blockIdx.y * kThreads + threadIdx.x;
-    if (hid >= nhot) return;
-    const uint32_t t0 = blockIdx.x * kHotGroup;
-    uint32_t v[kHotGroup], s = 0;
-#pragma unroll
-    for (int k = 0; k < kHotGroup; ++k) v[k] = t0 + k < ntiles ? sc.hcnt[(size_t)(t0 + k) * kHot + hid] : 0u;
-#pragma unroll
-    for (int k = 0; k < kHotGroup; ++k) s += v[k];
-    sc.hgsum[(size_t)blockIdx.x * kHot + hid] = s;
+// The batch's path and element counts (one lane).
+__global__ void k_hot_mode(BatchScratch sc) {
+    if (threadIdx.x != 0) return;
+    const uint32_t f = sc.counters[CTL_FLAGS];
+    const bool rerun = (f & kFlagRerun) != 0;
+    const uint32_t nhot = (f & (kFlagRerun | kFlagState)) ? 0u : hot_count(sc);
+    const uint32_t ns = rerun ? sc.counters[CTL_NEL1] : sc.counters[CTL_NEL0];
+    sc.counters[CTL_NSORT] = ns;
+    sc.counters[CTL_NCOLD] = ns - (nhot ? sc.counters[CTL_NPRIO] : 0u);
+    sc.counters[CTL_MODE] = nhot ? 1u : 0u;
 }
 
-__global__ __launch_bounds__(kThreads) void k_hs_mid(BatchScratch sc, uint32_t ngroups) {
-    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
-    const uint32_t hid = blockIdx.x * kThreads + threadIdx.x;
-    if (hid >= nhot) return;
+// Column prefix of the count rows over segments, in groups of kHotGroupRows rows.
+__global__ __launch_bounds__(kThreads) void k_hscan_group(BatchScratch sc, uint32_t nrows) {
+    if (!sc.counters[CTL_MODE]) return;
+    const uint32_t h = blockIdx.y * kThreads + threadIdx.x;
+    if (h >= hot_count(sc)) return;
+    const uint32_t r0 = blockIdx.x * kHotGroupRows;
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kHotGroupRows; ++k)
+        if (r0 + k < nrows) s += sc.hcnt[(size_t)(r0 + k) * kHot + h];
+    sc.hgsum[(size_t)blockIdx.x * kHot + h] = s;
+}
+
+__global__ __launch_bounds__(kThreads) void k_hscan_mid(BatchScratch sc, uint32_t ngroups) {
+    if (!sc.counters[CTL_MODE]) return;
+    const uint32_t h = blockIdx.x * kThreads + threadIdx.x;
+    if (h >= hot_count(sc)) return;
     uint32_t acc = 0;
 #pragma unroll 8
     for (uint32_t g = 0; g < ngroups; ++g) {
-        const uint32_t v = sc.hgsum[(size_t)g * kHot + hid];
-        sc.hgsum[(size_t)g * kHot + hid] = acc;
+        const uint32_t v = sc.hgsum[(size_t)g * kHot + h];
+        sc.hgsum[(size_t)g * kHot + h] = acc;
         acc += v;
     }
-    sc.hot_tot[hid] = acc;
+    sc.hot_tot[h] = acc;
 }
 
-// hot_base = exclusive scan of the per-hot-id totals (one workgroup, 4 ids per thread); the batch's
-// cold / hot element totals into counters[8..10]
-__global__ __launch_bounds__(1024) void k_hs_base(BatchScratch sc, uint32_t ngroups) {
-    __shared__ uint32_t ws[16];
-    __shared__ uint32_t ct[2][16];
-    {
-        uint32_t c = 0, h = 0;
-        for (uint32_t g = threadIdx.x; g < ngroups; g += 1024) {
-            c += sc.hgcnt[2 * g];
-            h += sc.hgcnt[2 * g + 1];
-        }
+__global__ __launch_bounds__(kThreads) void k_hscan_down(BatchScratch sc, uint32_t nrows) {
+    if (!sc.counters[CTL_MODE]) return;
+    const uint32_t h = blockIdx.y * kThreads + threadIdx.x;
+    if (h >= hot_count(sc)) return;
+    const uint32_t r0 = blockIdx.x * kHotGroupRows;
+    uint32_t v[kHotGroupRows];
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            c += (uint32_t)__shfl_down((int)c, o, 64);
-            h += (uint32_t)__shfl_down((int)h, o, 64);
-        }
-        if ((threadIdx.x & 63) == 0) {
-            ct[0][threadIdx.x >> 6] = c;
-            ct[1][threadIdx.x >> 6] = h;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t tc = 0, th = 0;
-            for (int w = 0; w < 16; ++w) {
-                tc += ct[0][w];
-                th += ct[1][w];
-            }
-            sc.counters[8] = tc;
-            sc.counters[9] = th;
-            sc.counters[10] = tc + th;
-        }
-    }
-    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t v[4], s = 0;
+    for (int k = 0; k < kHotGroupRows; ++k) v[k] = r0 + k < nrows ? sc.hcnt[(size_t)(r0 + k) * kHot + h] : 0u;
+    uint32_t run = sc.hgsum[(size_t)blockIdx.x * kHot + h];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t i = threadIdx.x * 4 + k;
-        v[k] = i < nhot ? sc.hot_tot[i] : 0u;
-        s += v[k];
-    }
-    uint32_t x = s;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) ws[wave] = x;
-    __syncthreads();
-    uint32_t pre = x - s;
-    for (int w = 0; w < wave; ++w) pre += ws[w];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t i = threadIdx.x * 4 + k;
-        if (i < nhot) sc.hot_base[i] = pre;
-        pre += v[k];
-    }
-}
-
-__global__ __launch_bounds__(kThreads) void k_hs_down(BatchScratch sc, uint32_t ntiles) {
-    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
-    const uint32_t hid = blockIdx.y * kThreads + threadIdx.x;
-    if (hid >= nhot) return;
-    const uint32_t t0 = blockIdx.x * kHotGroup;
-    uint32_t v[kHotGroup];
-#pragma unroll
-    for (int k = 0; k < kHotGroup; ++k) v[k] = t0 + k < ntiles ? sc.hcnt[(size_t)(t0 + k) * kHot + hid] : 0u;
-    uint32_t run = sc.hgsum[(size_t)blockIdx.x * kHot + hid] + sc.hot_base[hid];
-#pragma unroll
-    for (int k = 0; k < kHotGroup; ++k) {
-        if (t0 + k < ntiles) sc.hpre[(size_t)(t0 + k) * kHot + hid] = run;
+    for (int k = 0; k < kHotGroupRows; ++k) {
+        if (r0 + k < nrows) sc.hbase[(size_t)(r0 + k) * kHot + h] = run;
         run += v[k];
     }
 }
 
-// Hot elements to their rule segment in the hot region (after the cold elements) of `dst`.  The
-// tile's row of segment positions is staged in LDS (one batch of loads per thread); each thread
-// keeps kHotIlp elements in flight.  Wave segment w of the tile holds tile_nh[4 t + w] hot
-// elements at its end (descending addresses = arrival order).
-constexpr int kHotIlp = 4;
-constexpr int kHotPer = kHot / kThreads;  // LDS row entries per thread
-
-__device__ __forceinline__ void hot_row_to_lds(const uint32_t *__restrict__ row, uint32_t add, uint32_t nhot,
-                                               uint32_t *lds) {
-    uint32_t v[kHotPer];
-#pragma unroll
-    for (int k = 0; k < kHotPer; ++k) {
-        const uint32_t i = k * kThreads + threadIdx.x;
-        v[k] = i < nhot ? row[i] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < kHotPer; ++k) lds[k * kThreads + threadIdx.x] = v[k] + add;
-}
-
-__device__ __forceinline__ uint32_t hot_tile_total(const BatchScratch &sc, uint32_t tile, uint32_t (&nw)[kClsWaves]) {
-    uint32_t t = 0;
-#pragma unroll
-    for (int w = 0; w < kClsWaves; ++w) {
-        nw[w] = sc.tile_nh[tile * kClsWaves + w];
-        t += nw[w];
-    }
-    return t;
-}
-
-__global__ __launch_bounds__(kThreads) void k_hot_scatter(BatchScratch sc, uint64_t *__restrict__ dst) {
-    __shared__ uint32_t base[kHot];
-    const uint32_t tile = blockIdx.x, tbase = tile * kTileElems;
-    uint32_t nw[kClsWaves];
-    if (!hot_tile_total(sc, tile, nw)) return;
-    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
-    const uint32_t nc = sc.counters[8], lim = nc + sc.counters[9];
-    hot_row_to_lds(sc.hpre + (size_t)tile * kHot, nc, nhot, base);
-    __syncthreads();
-#pragma unroll 1
-    for (int w = 0; w < kClsWaves; ++w) {
-        const uint64_t *src = sc.el_tile + tbase + (w + 1) * (kClsRounds * 64) - 1;
-        uint64_t x[kHotIlp];
-#pragma unroll
-        for (int u = 0; u < kHotIlp; ++u) {
-            const uint32_t k = u * kThreads + threadIdx.x;
-            x[u] = k < nw[w] ? *(src - k) : ~0ull;
-        }
-        uint32_t sl[kHotIlp];
-#pragma unroll
-        for (int u = 0; u < kHotIlp; ++u) sl[u] = x[u] != ~0ull ? sc.hot_slot[(uint32_t)(x[u] >> kHidShift)] : 0u;
-#pragma unroll
-        for (int u = 0; u < kHotIlp; ++u) {
-            if (x[u] == ~0ull) continue;
-            const uint32_t hid = (uint32_t)(x[u] >> kHidShift);
-            const uint32_t e = base[hid] + (uint32_t)((x[u] >> kRankShift) & 0xFFFu);
-            if (e < lim) dst[e] = (x[u] & kLow40) | ((uint64_t)sl[u] << kSlotShift);
-        }
+// Rank of each prioritized hot request (sorted region: hot id major, arrival order within) and each
+// hot id's range in the region.
+__global__ __launch_bounds__(kThreads) void k_prio_rank(ClusterState st, BatchScratch sc,
+                                                        const uint64_t *__restrict__ el) {
+    if (!sc.counters[CTL_MODE]) return;
+    const uint32_t np = sc.counters[CTL_NPRIO], base = sc.counters[CTL_NCOLD];
+    const uint32_t key0 = st.nslots + 1;
+    for (uint32_t j = blockIdx.x * kThreads + threadIdx.x; j < np; j += gridDim.x * kThreads) {
+        const uint64_t e = el[base + j];
+        const uint32_t h = el_slot(e) - key0;
+        const uint32_t r_in = (((uint32_t)(e >> kBdShift) & kBdEsc) << 7) | (uint32_t)((e >> kAcqShift) & kAcqMax);
+        const uint32_t seg = el_idx(e) / (uint32_t)kHotSeg;
+        sc.prank[j] = sc.hbase[(size_t)seg * kHot + h] + r_in;
+        if (j == 0 || el_slot(el[base + j - 1]) != el_slot(e)) sc.plo[h] = j;
+        if (j + 1 == np || el_slot(el[base + j + 1]) != el_slot(e)) sc.phi[h] = j + 1;
     }
 }
 
-// TokenResults of the tile's hot requests, in input order, from the run records of their rule.
-__global__ __launch_bounds__(kThreads) void k_hot_results(BatchScratch sc, uint64_t *__restrict__ out) {
-    __shared__ uint32_t base[kHot];
-    __shared__ uint32_t frun[kHot];
-    const uint32_t tile = blockIdx.x, tbase = tile * kTileElems;
-    uint32_t nw[kClsWaves];
-    if (!hot_tile_total(sc, tile, nw)) return;
-    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
-    const uint32_t nc = sc.counters[8], nruns = sc.counters[1];
-    hot_row_to_lds(sc.hpre + (size_t)tile * kHot, nc, nhot, base);
-    hot_row_to_lds(sc.hot_first_run, 0, nhot, frun);
-    __syncthreads();
-#pragma unroll 1
-    for (int w = 0; w < kClsWaves; ++w) {
-        const uint64_t *src = sc.el_tile + tbase + (w + 1) * (kClsRounds * 64) - 1;
-        uint64_t x[kHotIlp];
-#pragma unroll
-        for (int u = 0; u < kHotIlp; ++u) {
-            const uint32_t k = u * kThreads + threadIdx.x;
-            x[u] = k < nw[w] ? *(src - k) : ~0ull;
+// First index in [lo, hi) with a[index] >= key (a ascending), the whole wave searching: 64 probes
+// per step.
+__device__ __forceinline__ uint32_t wave_lower_bound(const uint32_t *__restrict__ a, uint32_t lo, uint32_t hi,
+                                                     uint32_t key, int lane) {
+    while (hi - lo > 64) {
+        const uint32_t step = (hi - lo + 63) / 64;
+        const uint32_t idx = lo + (uint32_t)lane * step;
+        const bool below = idx < hi && a[idx] < key;
+        const uint32_t k = (uint32_t)__popcll(__ballot(below));  // probes 0..k-1 are below the key
+        if (k == 0) return lo;
+        const uint32_t nlo = lo + (k - 1) * step + 1;
+        hi = min(hi, lo + k * step);
+        lo = nlo;
+    }
+    const uint32_t idx = lo + (uint32_t)lane;
+    const bool below = idx < hi && a[idx] < key;
+    return lo + (uint32_t)__popcll(__ballot(below));
+}
+
+// One wave per hot rule: its runs in bucket order, each with the closed form of run_fast (the S
+// window buckets are read by S lanes, the sums are wave reductions, the decisions are uniform
+// scalar arithmetic, lane 0 stores the bucket).
+__global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchScratch sc, int64_t ts_base) {
+    if (!sc.counters[CTL_MODE]) return;
+    const int lane = threadIdx.x & 63;
+    const uint32_t h = blockIdx.x * kH1Waves + (threadIdx.x >> 6);
+    if (h >= hot_count(sc)) return;
+    const uint32_t bd_lo = sc.counters[CTL_BDLO];
+    const uint32_t bd_hi = min(sc.counters[CTL_BDHI], (uint32_t)kHotBuckets - 1);
+    const uint32_t nb = bd_hi >= bd_lo ? bd_hi - bd_lo + 1 : 0;
+    const uint32_t tot = sc.hot_tot[h];
+    uint32_t stb = 0;
+    if ((uint32_t)lane < nb && lane > 0) {
+        const uint32_t e = sc.hbnd[bd_lo + lane];
+        const uint32_t seg = e >> 9, kr = e & 511u;
+        stb = sc.hbase[(size_t)seg * kHot + h] + (kr ? sc.hpre[(size_t)(kr - 1) * kHot + h] : 0u);
+    }
+    uint32_t stn = wave_shl1(stb, 0u);
+    if ((uint32_t)lane + 1 == nb) stn = tot;
+    const uint32_t nrun = (uint32_t)lane < nb ? stn - stb : 0u;
+    HotRun *hr_row = sc.hrun + (size_t)h * kHotBuckets;
+    if ((uint32_t)lane < nb && nrun == 0) {
+        HotRun z{};
+        z.start = stb;
+        hr_row[bd_lo + lane] = z;
+    }
+    uint64_t rm = __ballot(nrun > 0);
+    if (!rm) return;
+    const uint32_t s = sc.hot_slot[h];
+    const SlotParam P = st.param[s];
+    const Rec R = rec_of(st, P);
+    const double thr = P.thr;
+    const int64_t qbase = div_pos(ts_base, P.W);
+    const uint32_t plo = sc.plo[h], phi = max(sc.phi[h], plo);
+    const uint32_t *pr = sc.prank;
+    while (rm) {
+        const int lb = __builtin_ctzll(rm);
+        rm &= rm - 1;
+        const uint32_t j0 = lane_u32(stb, lb);
+        const uint32_t n = lane_u32(nrun, lb);
+        const uint32_t b = bd_lo + (uint32_t)lb;
+        const uint32_t p0 = plo < phi ? wave_lower_bound(pr, plo, phi, j0, lane) : plo;
+        const uint32_t p1 = plo < phi ? wave_lower_bound(pr, p0, phi, j0 + n, lane) : plo;
+        const uint32_t cp_tot = p1 - p0;
+        // window of the run's bucket (cluster rules: interval = S x W, so validity is the same for
+        // any time in the bucket and the bucket start stands in for the request times)
+        const int64_t q = qbase + (int64_t)b;
+        const int64_t ws = q * P.W;
+        const int64_t t0 = ws;
+        const int64_t qs = div_pos(q, P.S);
+        const int cj = (int)(q - qs * P.S);
+        const int jh = cj + 1 == P.S ? 0 : cj + 1;
+        int64_t w = kAbsent, pv = 0;
+        if (lane < P.S) {
+            w = R.start(lane);
+            pv = R.cnt(CEV_PASS, lane);
         }
-        uint32_t e[kHotIlp], r[kHotIlp];
-#pragma unroll
-        for (int u = 0; u < kHotIlp; ++u) {
-            const uint32_t hid = (uint32_t)(x[u] >> kHidShift) & (kHot - 1);
-            e[u] = base[hid] + (uint32_t)((x[u] >> kRankShift) & 0xFFFu);
-            r[u] = x[u] != ~0ull ? frun[hid] : nruns;
-        }
-        // the rule's run holding e: usually its first or second run (a batch spans a few buckets)
-        uint32_t nx[kHotIlp];
-#pragma unroll
-        for (int u = 0; u < kHotIlp; ++u) nx[u] = r[u] + 1 < nruns ? sc.run_start[r[u] + 1] : 0xFFFFFFFFu;
-#pragma unroll
-        for (int u = 0; u < kHotIlp; ++u) {
-            while (nx[u] <= e[u]) {
-                ++r[u];
-                nx[u] = r[u] + 1 < nruns ? sc.run_start[r[u] + 1] : 0xFFFFFFFFu;
+        const bool valid_b = lane < P.S && lane != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval);
+        const int64_t bp = wave_sum_i64(valid_b ? pv : 0);
+        const int64_t old = lane_i64(w, cj);
+        const int64_t hstart = lane_i64(w, jh), hpass = lane_i64(pv, jh);
+        bool ok = !(old != kAbsent && ws < old);
+        const bool rot = old == kAbsent || ws > old;
+        int64_t cl = 0;  // lane k < CEV_N: counter k of the current bucket after the rotation
+        SlotOcc o{0, 0, 0, 0};
+        bool occ_dirty = false;
+        if (!rot && lane < CEV_N) cl = R.cnt(lane, cj);
+        if (rot && old != kAbsent) {  // resetWindowTo + transferOccupyToBucket
+            o = st.occ[s];
+            if (o.has_occ) {
+                if (lane == CEV_OCCUPIED_PASS || lane == CEV_PASS) cl += o.occ_pass;
+                if (lane == CEV_PASS_REQUEST) cl += o.occ_preq;
+                o.occ_pass = 0;
+                o.occ_preq = 0;
+                o.has_occ = 0;
+                occ_dirty = true;
             }
         }
-        RunOut ro[kHotIlp];
-        uint32_t rs[kHotIlp];
+        const int64_t cpass = lane_i64(cl, CEV_PASS);
+        const int64_t head = jh == cj ? cpass : ((hstart != kAbsent && !(t0 - hstart > (int64_t)P.interval)) ? hpass : 0);
+        const int64_t s0 = bp + cpass;
+        const uint32_t f = pass_prefix(thr, P.isec, s0, 1, n);
+        uint32_t cpf = cp_tot;
+        if (f < n && cp_tot > 0) cpf = wave_lower_bound(pr, p0, p1, j0 + f, lane) - p0;
+        const uint32_t np_after = cp_tot - cpf;
+        uint32_t cw = 0;
+        if (np_after > 0) {
+            const int64_t wt = (lane < P.S && valid_b) ? R.cnt(CEV_WAITING, lane) : 0;
+            const int64_t w0 = lane_i64(cl, CEV_WAITING) + wave_sum_i64(wt);
+            if (!(rot && old != kAbsent)) o = st.occ[s];  // not loaded by the rotation above
+            const double latest = (double)(s0 + (int64_t)f) / P.isec;
+            const double lim = st.max_occupy_ratio * thr;
+            const int64_t occ0 = o.occ_pass;
+            uint32_t l2 = 0, h2 = np_after;
+            while (l2 < h2) {
+                const uint32_t cc = l2 + ((h2 - l2) >> 1);
+                const int64_t add = (int64_t)cc;
+                const bool fits = ((double)(w0 + add) / P.isec <= lim) &&
+                                  (latest + (double)(1 + occ0 + add) - (double)head <= thr);
+                if (fits) l2 = cc + 1;
+                else h2 = cc;
+            }
+            cw = l2;
+            if (cw > 0) {
+                o.occ_pass += (int64_t)cw;
+                o.occ_preq += cw;
+                o.has_occ = 1;
+                occ_dirty = true;
+            }
+        }
+        const uint32_t nblk = n - f - cw;
+        if (lane == CEV_PASS) cl += (int64_t)f;
+        if (lane == CEV_PASS_REQUEST) cl += f;
+        if (lane == CEV_OCCUPIED_PASS) cl += (int64_t)cpf;
+        if (lane == CEV_WAITING) cl += (int64_t)cw;
+        if (lane == CEV_BLOCK) cl += (int64_t)nblk;
+        if (lane == CEV_BLOCK_REQUEST) cl += nblk;
+        if (lane == CEV_OCCUPIED_BLOCK) cl += (int64_t)(np_after - cw);
+        if (ok) {
+            if (lane < CEV_N) R.cnt(lane, cj) = cl;
+            if (lane == 0) {
+                if (rot) R.start(cj) = ws;
+                if (occ_dirty) st.occ[s] = o;
+            }
+        } else if (lane == 0) {
+            atomicAdd(&sc.counters[CTL_HOTERR], 1u);
+        }
+        if (lane == 0) {
+            HotRun r{};
+            r.s0 = s0;
+            r.thr = thr;
+            r.isec = P.isec;
+            r.f = f;
+            r.start = j0;
+            r.n = n;
+            r.p0 = p0;
+            r.cpf = cpf;
+            r.cw = cw;
+            r.wait = (uint16_t)(1000 / P.S);
+            r.ok = ok ? 1 : 0;
+            hr_row[b] = r;
+        }
+    }
+}
+
+// TokenResults of the non-prioritized hot requests, in input order.
+constexpr int kFinChunk = 8;
+__global__ __launch_bounds__(kThreads) void k_hot_final(BatchScratch sc, uint32_t n, uint64_t *__restrict__ out) {
+    __shared__ uint32_t base[kH1Waves][kHot];
+    if (!sc.counters[CTL_MODE]) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t seg = blockIdx.x * kH1Waves + wave;
+    const uint32_t sbase = seg * kHotSeg;
+    if (sbase >= n) return;
+    const uint32_t nhot = hot_count(sc);
+    uint32_t *bw = base[wave];
+    for (uint32_t h = lane; h < nhot; h += 64) bw[h] = sc.hbase[(size_t)seg * kHot + h];
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t send = min(n, sbase + (uint32_t)kHotSeg);
+    for (uint32_t r0 = sbase; r0 < send; r0 += kFinChunk * 64) {
+        uint32_t code[kFinChunk];
 #pragma unroll
-        for (int u = 0; u < kHotIlp; ++u) {
-            if (r[u] < nruns) {
-                ro[u] = sc.run_out[r[u]];
-                rs[u] = sc.run_start[r[u]];
+        for (int u = 0; u < kFinChunk; ++u) {
+            const uint32_t i = r0 + u * 64 + lane;
+            code[u] = i < send ? sc.hcode[i] : kNoCode;
+        }
+        const HotRun *hrp[kFinChunk];
+        int64_t s0[kFinChunk];
+        double thr[kFinChunk], isec[kFinChunk];
+        uint32_t f[kFinChunk], st0[kFinChunk];
+#pragma unroll
+        for (int u = 0; u < kFinChunk; ++u) {
+            hrp[u] = sc.hrun + (size_t)(code[u] & 0xFFFu) * kHotBuckets + (code[u] >> 25);
+            if (code[u] != kNoCode) {
+                s0[u] = hrp[u]->s0;
+                thr[u] = hrp[u]->thr;
+                isec[u] = hrp[u]->isec;
+                f[u] = hrp[u]->f;
+                st0[u] = hrp[u]->start;
             }
         }
 #pragma unroll
-        for (int u = 0; u < kHotIlp; ++u) {
-            if (r[u] >= nruns || ro[u].mode != RUN_FAST) continue;  // replayed: k_flows_slow wrote it
-            const uint32_t local = e[u] - rs[u];
-            const int32_t a = el_acq(x[u]);
+        for (int u = 0; u < kFinChunk; ++u) {
+            if (code[u] == kNoCode) continue;
+            const uint32_t local = bw[code[u] & 0xFFFu] + ((code[u] >> 12) & 0x1FFFu) - st0[u];
             uint64_t res;
-            if (local < ro[u].f) {
-                const int64_t sum = ro[u].s0 + (int64_t)local * a;
-                res = pack_result(TRS_OK, j_d2i(ro[u].thr - (double)sum / ro[u].isec - (double)a), 0);
-            } else if (el_prio(x[u])) {
-                // prioritized requests of the run before this one: lower bound of e in the run's plist
-                const uint32_t p0 = sc.run_p0[r[u]];
-                uint32_t lo = 0, hi = sc.run_cp[r[u]];
-                while (lo < hi) {
-                    const uint32_t m = (lo + hi) >> 1;
-                    if (sc.plist[p0 + m] < e[u]) lo = m + 1;
-                    else hi = m;
-                }
-                res = lo - ro[u].cpf < ro[u].cw ? pack_result(TRS_SHOULD_WAIT, 0, (int32_t)ro[u].wait)
-                                                : pack_result(TRS_BLOCKED, 0, 0);
+            if (local < f[u]) {
+                const int64_t sum = s0[u] + (int64_t)local;
+                res = pack_result(TRS_OK, j_d2i(thr[u] - (double)sum / isec[u] - 1.0), 0);
             } else {
                 res = pack_result(TRS_BLOCKED, 0, 0);
             }
-            out[el_idx(x[u])] = res;
+            out[r0 + u * 64 + lane] = res;
         }
+    }
+}
+
+// TokenResults of the prioritized hot requests.
+__global__ __launch_bounds__(kThreads) void k_prio_results(ClusterState st, BatchScratch sc,
+                                                           const uint64_t *__restrict__ el,
+                                                           uint64_t *__restrict__ out) {
+    if (!sc.counters[CTL_MODE]) return;
+    const uint32_t np = sc.counters[CTL_NPRIO], base = sc.counters[CTL_NCOLD];
+    const uint32_t bd_lo = sc.counters[CTL_BDLO];
+    const uint32_t bd_hi = min(sc.counters[CTL_BDHI], (uint32_t)kHotBuckets - 1);
+    for (uint32_t j = blockIdx.x * kThreads + threadIdx.x; j < np; j += gridDim.x * kThreads) {
+        const uint64_t e = el[base + j];
+        const uint32_t h = el_slot(e) - (st.nslots + 1);
+        const uint32_t rank = sc.prank[j];
+        const HotRun *row = sc.hrun + (size_t)h * kHotBuckets;
+        uint32_t b = bd_lo;
+        for (; b < bd_hi; ++b)
+            if (rank - row[b].start < row[b].n) break;
+        const HotRun hr = row[b];
+        const uint32_t local = rank - hr.start;
+        uint64_t res;
+        if (local < hr.f) {
+            const int64_t sum = hr.s0 + (int64_t)local;
+            res = pack_result(TRS_OK, j_d2i(hr.thr - (double)sum / hr.isec - 1.0), 0);
+        } else if (j - hr.p0 - hr.cpf < hr.cw) {
+            res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)hr.wait);
+        } else {
+            res = pack_result(TRS_BLOCKED, 0, 0);
+        }
+        out[el_idx(e)] = res;
     }
 }
 
 // ---- next batch's hot set: rules with at least T requests in this batch, T the smallest power of
-// two (>= hot_min) that admits at most kHot rules.
+// two (>= hot_min) that admits at most kHot rules; all of them with the window length of the
+// busiest one, 1 < sampleCount <= 64 (the occupy path needs 1000 / sampleCount > 0).
 __device__ __forceinline__ uint32_t flow_count(const BatchScratch &sc, uint32_t fl, uint32_t nflows,
                                                uint32_t nvalid) {
     const uint32_t e0 = sc.run_start[sc.flow_first_run[fl]];
@@ -1409,37 +1602,59 @@ __device__ __forceinline__ uint32_t flow_count(const BatchScratch &sc, uint32_t 
     return e1 - e0;
 }
 
-__global__ __launch_bounds__(kThreads) void k_hot_hist(BatchScratch sc) {
-    __shared__ uint32_t bins[32];
-    if (threadIdx.x < 32) bins[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t nflows = sc.counters[2], nvalid = sc.counters[0];
-    for (uint32_t fl = blockIdx.x * kThreads + threadIdx.x; fl < nflows; fl += gridDim.x * kThreads) {
-        const uint32_t c = flow_count(sc, fl, nflows, nvalid);
-        if (c) atomicAdd(&bins[31 - __clz(c)], 1u);
+__device__ __forceinline__ bool hot_eligible(const SlotParam &P) { return P.S > 1 && P.S <= 64 && P.active; }
+
+// candidate i of this batch: cold flows, then (hot path batches) the hot ids
+__device__ __forceinline__ bool hot_candidate(const ClusterState &st, const BatchScratch &sc, uint32_t i,
+                                              uint32_t nflows, uint32_t nvalid, uint32_t &slot, uint32_t &count) {
+    if (i < nflows) {
+        count = flow_count(sc, i, nflows, nvalid);
+        slot = sc.run_slot[sc.flow_first_run[i]];
+    } else {
+        count = sc.hot_tot[i - nflows];
+        slot = sc.hot_slot[i - nflows];
     }
+    return count > 0 && hot_eligible(st.param[slot]);
+}
+
+__global__ __launch_bounds__(kThreads) void k_hot_hist(ClusterState st, BatchScratch sc) {
+    __shared__ uint32_t bins[32];
+    __shared__ unsigned long long best;
+    if (threadIdx.x < 32) bins[threadIdx.x] = 0;
+    if (threadIdx.x == 0) best = 0;
+    __syncthreads();
+    const uint32_t nflows = sc.counters[CTL_NFLOWS], nvalid = sc.counters[CTL_NVALID];
+    const uint32_t ncand = nflows + (sc.counters[CTL_MODE] ? hot_count(sc) : 0u);
+    unsigned long long mine = 0;
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < ncand; i += gridDim.x * kThreads) {
+        uint32_t slot, c;
+        if (!hot_candidate(st, sc, i, nflows, nvalid, slot, c)) continue;
+        atomicAdd(&bins[31 - __clz(c)], 1u);
+        mine = max(mine, ((unsigned long long)c << 32) | slot);
+    }
+    if (mine) atomicMax(&best, mine);
     __syncthreads();
     if (threadIdx.x < 32 && bins[threadIdx.x]) atomicAdd(&sc.hot_ctl[8 + threadIdx.x], bins[threadIdx.x]);
+    if (threadIdx.x == 0 && best) atomicMax(reinterpret_cast<unsigned long long *>(sc.hot_ctl + 4), best);
 }
 
 __device__ __forceinline__ void hot_fid_set(const ClusterState &st, uint32_t slot, uint16_t v) {
-    if (!st.dense_n) return;
+    if (!st.dense_n || !st.hot_fid) return;
     const int64_t f = st.slot_fid[slot];
     if (f >= 1 && f <= (int64_t)st.dense_n) st.hot_fid[f - 1] = v;
 }
 
 __global__ __launch_bounds__(kThreads) void k_hot_clear(ClusterState st, BatchScratch sc) {
-    const uint32_t nhot = min(sc.hot_ctl[0], (uint32_t)kHot);
-    const uint32_t hid = blockIdx.x * kThreads + threadIdx.x;
-    if (hid < nhot) {
-        const uint32_t slot = sc.hot_slot[hid];
+    const uint32_t h = blockIdx.x * kThreads + threadIdx.x;
+    if (h < hot_count(sc)) {
+        const uint32_t slot = sc.hot_slot[h];
         sc.hot_of[slot] = kColdId;
         hot_fid_set(st, slot, kColdId);
     }
 }
 
 __global__ __launch_bounds__(kThreads) void k_hot_pick(ClusterState st, BatchScratch sc, uint32_t hot_min) {
-    __shared__ uint32_t thr;
+    __shared__ uint32_t thr, wbest;
     if (threadIdx.x == 0) {
         uint32_t cum = 0, t = 0xFFFFFFFFu;
         for (int b = 31; b >= 0; --b) {
@@ -1448,24 +1663,42 @@ __global__ __launch_bounds__(kThreads) void k_hot_pick(ClusterState st, BatchScr
             t = 1u << b;
         }
         thr = max(t, max(hot_min, 1u));
+        const unsigned long long best = *reinterpret_cast<const unsigned long long *>(sc.hot_ctl + 4);
+        wbest = best ? (uint32_t)st.param[(uint32_t)best].W : 0u;
     }
     __syncthreads();
-    const uint32_t nflows = sc.counters[2], nvalid = sc.counters[0];
-    for (uint32_t fl = blockIdx.x * kThreads + threadIdx.x; fl < nflows; fl += gridDim.x * kThreads) {
-        if (flow_count(sc, fl, nflows, nvalid) < thr) continue;
+    if (!wbest) return;
+    const uint32_t nflows = sc.counters[CTL_NFLOWS], nvalid = sc.counters[CTL_NVALID];
+    const uint32_t ncand = nflows + (sc.counters[CTL_MODE] ? hot_count(sc) : 0u);
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < ncand; i += gridDim.x * kThreads) {
+        uint32_t slot, c;
+        if (!hot_candidate(st, sc, i, nflows, nvalid, slot, c) || c < thr) continue;
+        if ((uint32_t)st.param[slot].W != wbest) continue;
         const uint32_t hid = atomicAdd(&sc.hot_ctl[1], 1u);
         if (hid < (uint32_t)kHot) {
-            const uint32_t slot = sc.run_slot[sc.flow_first_run[fl]];
-            sc.hot_slot[hid] = slot;
+            sc.hot_next[hid] = slot;
             sc.hot_of[slot] = (uint16_t)hid;
             hot_fid_set(st, slot, (uint16_t)hid);
         }
     }
 }
 
-__global__ void k_hot_fin(BatchScratch sc) {
-    if (threadIdx.x == 0) sc.hot_ctl[0] = min(sc.hot_ctl[1], (uint32_t)kHot);
-    if (threadIdx.x == 0) sc.hot_ctl[1] = 0;
+__global__ __launch_bounds__(kThreads) void k_hot_fin(ClusterState st, BatchScratch sc) {
+    __shared__ uint32_t nn;
+    if (threadIdx.x == 0) {
+        nn = min(sc.hot_ctl[1], (uint32_t)kHot);
+        const unsigned long long best = *reinterpret_cast<const unsigned long long *>(sc.hot_ctl + 4);
+        sc.hot_ctl[2] = best ? (uint32_t)st.param[(uint32_t)best].W : 1u;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nn; i += kThreads) sc.hot_slot[i] = sc.hot_next[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        sc.hot_ctl[0] = nn;
+        sc.hot_ctl[1] = 0;
+        sc.hot_ctl[4] = 0;
+        sc.hot_ctl[5] = 0;
+    }
     if (threadIdx.x < 32) sc.hot_ctl[8 + threadIdx.x] = 0;
 }
 
@@ -2090,15 +2323,20 @@ static void apply_limiters(const RuleParam *param, BatchScratch &sc, uint64_t *e
 // the radix digit width depends on the live slot count: size for the widest
 static size_t max_hist_entries(size_t cap, uint32_t nslots_cap) {
     int bits = 1;
-    while (((uint64_t)1 << bits) < (uint64_t)nslots_cap + 1) ++bits;
+    while (((uint64_t)1 << bits) < (uint64_t)nslots_cap + kHot + 2) ++bits;
     size_t m = 0;
     for (int b = 1; b <= bits; ++b) m = std::max(m, ((size_t)1 << radix64_digit_bits(b)) * radix64_tiles(cap));
     return m;
 }
 
+static size_t hot_rows(size_t cap) { return (cap + kHotSeg - 1) / kHotSeg; }
+static size_t hot_groups(size_t cap) { return (hot_rows(cap) + kHotGroupRows - 1) / kHotGroupRows; }
+
 size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     const size_t ntiles = (cap + kTileElems - 1) / kTileElems + 1;
     const size_t hist = max_hist_entries(cap, nslots_cap);
+    const size_t nseg = hot_rows(cap) + 1;  // segments of k_hot_classify (whole workgroups: 4 per)
+    const size_t segs_alloc = ((nseg + kH1Waves - 1) / kH1Waves) * kH1Waves;
     size_t b = 0;
     b += 2 * align_up(cap * 8);                 // elements (double buffer)
     b += 7 * align_up((cap + 1) * 4);           // run_start/slot/idx0/cp/p0/acq, flow_first_run
@@ -2108,24 +2346,29 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up(cap * sizeof(RunOut));        // run_out
     b += align_up(ntiles * kRunWaves * sizeof(RAgg));
     b += 2 * align_up(ntiles * sizeof(Agg)) + align_up(ntiles * 4);
-    b += align_up(64);
+    b += align_up(CTL_WORDS * 4);
     b += 2 * align_up(hist * 4) + align_up(scan_partials_needed(hist) * 4 + 64);
     b += align_up(scan_partials_needed(cap) * 4 + 64);
     b += align_up(kRadixGhistWords * 4) + align_up(64);  // look-back digit totals, error flag
-    // hot/cold split
-    const size_t ngroups = (ntiles + kHotGroup - 1) / kHotGroup;
-    b += align_up((size_t)nslots_cap * 2) + align_up(kHot * 4) + align_up(64 * 4);  // hot_of, hot_slot, hot_ctl
-    b += align_up(ntiles * kTileElems * 8);                                       // el_tile
-    b += 2 * align_up(ntiles * kClsWaves * 4);                                    // tile_nc / tile_nh
-    b += align_up(ntiles * kHot * 2) + align_up(ntiles * kHot * 4);               // hcnt, hpre
-    b += align_up(ngroups * kHot * 4) + 3 * align_up(kHot * 4);                   // hgsum, tot/base/first_run
-    b += align_up(ngroups * 2 * 4);                                               // hgcnt
+    // hot path
+    b += align_up((size_t)nslots_cap * 2) + 2 * align_up(kHot * 4) + align_up(64 * 4);  // hot_of/slot/next/ctl
+    b += align_up(segs_alloc * kHotSeg * 8);                                       // el_tile
+    b += align_up(segs_alloc * kSubPerSeg * 4);                                    // tile_nc
+    b += align_up(segs_alloc * kHotSeg * 4);                                       // hcode
+    b += align_up(segs_alloc * kHot * 2) + align_up(segs_alloc * kHot * 4);        // hcnt, hbase
+    b += align_up(hot_groups(cap) * kHot * 4);                                     // hgsum
+    b += align_up((size_t)kHotPreRows * kHot * 2) + align_up(kHotBuckets * 4);     // hpre, hbnd
+    b += align_up((size_t)kHot * kHotBuckets * sizeof(HotRun));                   // hrun
+    b += align_up(cap * 4);                                                        // prank
+    b += 3 * align_up(kHot * 4);                                                   // plo, phi, hot_tot
     return b;
 }
 
 void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslots_cap) {
     const size_t ntiles = (cap + kTileElems - 1) / kTileElems + 1;
     const size_t hist = max_hist_entries(cap, nslots_cap);
+    const size_t nseg = hot_rows(cap) + 1;
+    const size_t segs_alloc = ((nseg + kH1Waves - 1) / kH1Waves) * kH1Waves;
     char *p = (char *)base;
     auto take = [&](size_t bytes) {
         void *r = p;
@@ -2149,27 +2392,30 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.tile_agg = take(ntiles * sizeof(Agg));
     sc.tile_carry = take(ntiles * sizeof(Agg));
     sc.tile_valid = (uint32_t *)take(ntiles * 4);
-    sc.counters = (uint32_t *)take(64);
+    sc.counters = (uint32_t *)take(CTL_WORDS * 4);
     sc.radix.hist = (uint32_t *)take(hist * 4);
     sc.radix.hist_scan = (uint32_t *)take(hist * 4);
     sc.radix.partial = (uint32_t *)take(scan_partials_needed(hist) * 4 + 64);
     sc.lim_partial = (uint32_t *)take(scan_partials_needed(cap) * 4 + 64);
     sc.radix.ghist = (uint32_t *)take(kRadixGhistWords * 4);
     sc.radix.err = (uint32_t *)take(64);
-    const size_t ngroups = (ntiles + kHotGroup - 1) / kHotGroup;
     sc.hot_of = (uint16_t *)take((size_t)nslots_cap * 2);
     sc.hot_slot = (uint32_t *)take(kHot * 4);
+    sc.hot_next = (uint32_t *)take(kHot * 4);
     sc.hot_ctl = (uint32_t *)take(64 * 4);
-    sc.el_tile = (uint64_t *)take(ntiles * kTileElems * 8);
-    sc.tile_nc = (uint32_t *)take(ntiles * kClsWaves * 4);
-    sc.tile_nh = (uint32_t *)take(ntiles * kClsWaves * 4);
-    sc.hcnt = (uint16_t *)take(ntiles * kHot * 2);
-    sc.hpre = (uint32_t *)take(ntiles * kHot * 4);
-    sc.hgsum = (uint32_t *)take(ngroups * kHot * 4);
+    sc.el_tile = (uint64_t *)take(segs_alloc * kHotSeg * 8);
+    sc.tile_nc = (uint32_t *)take(segs_alloc * kSubPerSeg * 4);
+    sc.hcode = (uint32_t *)take(segs_alloc * kHotSeg * 4);
+    sc.hcnt = (uint16_t *)take(segs_alloc * kHot * 2);
+    sc.hbase = (uint32_t *)take(segs_alloc * kHot * 4);
+    sc.hgsum = (uint32_t *)take(hot_groups(cap) * kHot * 4);
+    sc.hpre = (uint16_t *)take((size_t)kHotPreRows * kHot * 2);
+    sc.hbnd = (uint32_t *)take(kHotBuckets * 4);
+    sc.hrun = (HotRun *)take((size_t)kHot * kHotBuckets * sizeof(HotRun));
+    sc.prank = (uint32_t *)take(cap * 4);
+    sc.plo = (uint32_t *)take(kHot * 4);
+    sc.phi = (uint32_t *)take(kHot * 4);
     sc.hot_tot = (uint32_t *)take(kHot * 4);
-    sc.hot_base = (uint32_t *)take(kHot * 4);
-    sc.hot_first_run = (uint32_t *)take(kHot * 4);
-    sc.hgcnt = (uint32_t *)take(ngroups * 2 * 4);
     sc.cap = cap;
 }
 
@@ -2179,53 +2425,62 @@ void hot_reset(const ClusterState &st, BatchScratch &sc, uint32_t nslots_cap, hi
                        dim3(256), 0, s, st, sc, nslots_cap);
 }
 
-// Hot/cold split batch (see the kernels above): classify -> tile scan per hot id -> hot scatter ->
-// radix sort of the cold elements -> runs / flows over [cold sorted | hot segments] -> cold results
-// (scattered) + hot results (input order) -> next batch's hot set.
+// Hot path batch (kernels above): precheck -> classify (+ fallback re-classification) -> count
+// scan -> sort of the cold (and prioritized hot) elements -> cold runs / flows / results -> hot
+// runs (k_hot_flows) -> hot results in input order -> prioritized hot results -> next hot set.
+// Every kernel reads the batch's path from the control words, so no host synchronisation.
 static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id,
                              const int32_t *acquire, const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off,
-                             uint32_t n, int simple, uint64_t *out, hipStream_t s, int bits, int d0,
-                             uint32_t ntiles) {
+                             uint32_t n, uint64_t *out, hipStream_t s) {
     const uint32_t invalid_key = st.nslots;
-    static const int chunk = getenv("SGA_CLS_CHUNK") ? atoi(getenv("SGA_CLS_CHUNK")) : 2;  // A/B knob
-    auto cls = chunk >= 4 ? k_classify_hot<4> : (chunk >= 2 ? k_classify_hot<2> : k_classify_hot<1>);
-    hipLaunchKernelGGL(cls, dim3(ntiles), dim3(kThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n,
-                       simple, out, d0, ntiles, sc.radix.hist);
-    const uint32_t ngroups = (ntiles + kHotGroup - 1) / kHotGroup;
-    hipLaunchKernelGGL(k_hs_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, ntiles);
-    hipLaunchKernelGGL(k_hs_mid, dim3(kHot / kThreads), dim3(kThreads), 0, s, sc, ngroups);
-    hipLaunchKernelGGL(k_hs_base, dim3(1), dim3(1024), 0, s, sc, ngroups);
-    hipLaunchKernelGGL(k_hs_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, ntiles);
-    const int npass = (bits + d0 - 1) / d0;
-    uint64_t *el = (npass & 1) ? sc.el[0] : sc.el[1];  // where radix_sort_u64_tiled leaves the result
-    hipLaunchKernelGGL(k_hot_scatter, dim3(ntiles), dim3(kThreads), 0, s, sc, el);
-    const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + 8, sc.el[0], sc.el[1], n, kSlotShift,
-                                        bits, sc.radix, s, true);
-    (void)np;
+    int bits = 1;
+    while (((uint64_t)1 << bits) < (uint64_t)st.nslots + kHot + 2) ++bits;  // hot keys nslots + 1 + id
+    const uint32_t ntiles = (n + kTileElems - 1) / kTileElems;
+    const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
+    const uint32_t nwg = (nseg + kH1Waves - 1) / kH1Waves;
+    const uint32_t ngroups = (nseg + kHotGroupRows - 1) / kHotGroupRows;
+    SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, CTL_WORDS * 4, s));
+    SGA_HIP_CHECK(hipMemsetAsync(sc.plo, 0, 2 * align_up(kHot * 4), s));  // plo and phi (adjacent)
+    hipLaunchKernelGGL(k_hot_precheck, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc, ts_off, ts_base, n);
+    hipLaunchKernelGGL(k_hot_classify<0>, dim3(nwg), dim3(kThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off,
+                       ts_base, n, out);
+    hipLaunchKernelGGL(k_hot_classify<1>, dim3(nwg), dim3(kThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off,
+                       ts_base, n, out);
+    hipLaunchKernelGGL(k_hot_mode, dim3(1), dim3(64), 0, s, sc);
+    hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
+    hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, s, sc, ngroups);
+    hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
+    const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
+                                        kSlotShift, bits, sc.radix, s, false);
+    const uint64_t *el = (np & 1) ? sc.el[0] : sc.el[1];
+    const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
+    hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el);
+    hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, s, st, sc, ts_base);
     hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
-                       sc.tile_valid, sc.counters + 10);
+                       sc.tile_valid, sc.counters + CTL_NCOLD);
     hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
                        ntiles, (Agg *)sc.tile_carry, sc.counters);
     hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key, (const Agg *)sc.tile_carry,
-                       sc, 1);
+                       sc);
     const uint64_t max_flows = n < st.nslots ? n : st.nslots;
     uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows + kThreads - 1) / kThreads, 16384);
     if (fb == 0) fb = 1;
-    hipLaunchKernelGGL(k_flows, dim3(fb), dim3(kThreads), 0, s, st, sc, ts_base, simple);
+    hipLaunchKernelGGL(k_flows, dim3(fb), dim3(kThreads), 0, s, st, sc, ts_base, 0);
     hipLaunchKernelGGL(k_flows_slow, dim3(std::min<uint32_t>(fb, 1024)), dim3(kThreads), 0, s, st, sc, acquire, prio,
-                       ts_off, ts_base, el, simple, out);
-    hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, invalid_key, out, 1);
-    hipLaunchKernelGGL(k_hot_results, dim3(ntiles), dim3(kThreads), 0, s, sc, out);
+                       ts_off, ts_base, el, 0, out);
+    hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, invalid_key, out);
+    hipLaunchKernelGGL(k_hot_final, dim3(nwg), dim3(kThreads), 0, s, sc, n, out);
+    hipLaunchKernelGGL(k_prio_results, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el, out);
     const uint32_t sb = std::min<uint32_t>(fb, 1024);
-    hipLaunchKernelGGL(k_hot_hist, dim3(sb), dim3(kThreads), 0, s, sc);
+    hipLaunchKernelGGL(k_hot_hist, dim3(sb), dim3(kThreads), 0, s, st, sc);
     hipLaunchKernelGGL(k_hot_clear, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc);
     hipLaunchKernelGGL(k_hot_pick, dim3(sb), dim3(kThreads), 0, s, st, sc, sc.hot_min);
-    hipLaunchKernelGGL(k_hot_fin, dim3(1), dim3(64), 0, s, sc);
+    hipLaunchKernelGGL(k_hot_fin, dim3(1), dim3(kThreads), 0, s, st, sc);
 }
 
 void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
                           const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, int simple,
-                          void *out_v, hipStream_t s, const LimiterPass *lims, int nlims, int stages) {
+                          void *out_v, hipStream_t s, const LimiterPass *lims, int nlims) {
     if (n == 0) return;
     uint64_t *out = (uint64_t *)out_v;
     int bits = 1;
@@ -2237,44 +2492,38 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     static_assert(kTileElems == kRadix64Tile, "classify tiles are sort tiles");
     const bool lb = radix64_lookback() != 0;
     const int npass = (bits + d0 - 1) / d0;
-    if (stages & 1) {
-        SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, s));
-        if (lb) SGA_HIP_CHECK(hipMemsetAsync(sc.radix.ghist, 0, kRadixGhistWords * sizeof(uint32_t), s));
-        if (lb) SGA_HIP_CHECK(hipMemsetAsync(sc.radix.err, 0, sizeof(uint32_t), s));
-    }
     static const int chunk = getenv("SGA_CLS_CHUNK") ? atoi(getenv("SGA_CLS_CHUNK")) : 2;  // A/B knob
     auto cls = chunk >= 16 ? k_classify<16>
                            : (chunk >= 8 ? k_classify<8> : (chunk >= 4 ? k_classify<4> : (chunk >= 2 ? k_classify<2> : k_classify<1>)));
     static const int nofuse = getenv("SGA_XP_NOFUSE") ? atoi(getenv("SGA_XP_NOFUSE")) : 0;  // A/B knob
-    if (sc.hot_enabled && !limited && !lb && !nofuse && stages == 3) {
-        decide_batch_hot(st, sc, flow_id, acquire, prio, ts_base, ts_off, n, simple, out, s, bits, d0, ntiles);
+    if (sc.hot_enabled && !simple && !limited && !lb && st.nslots + (uint64_t)kHot + 2 < kMaxSlots) {
+        decide_batch_hot(st, sc, flow_id, acquire, prio, ts_base, ts_off, n, out, s);
         return;
     }
+    SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, CTL_WORDS * 4, s));
+    if (lb) SGA_HIP_CHECK(hipMemsetAsync(sc.radix.ghist, 0, kRadixGhistWords * sizeof(uint32_t), s));
+    if (lb) SGA_HIP_CHECK(hipMemsetAsync(sc.radix.err, 0, sizeof(uint32_t), s));
     // the sort's result buffer (radix_sort_u64 returns npass)
     const uint64_t *el = sc.el[npass & 1];
-    if (stages & 1) {  // stage A: classify, limiter pre-pass, sort, runs (no rule state read or written)
-        hipLaunchKernelGGL(cls, dim3(ntiles), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n,
-                           simple, invalid_key, sc.el[0], out, (limited || nofuse) ? 0 : d0, ntiles, sc.radix.hist,
-                           (lb && !limited) ? npass : 0, sc.radix.ghist);
-        if (!simple) apply_limiters(st.param, sc, sc.el[0], n, invalid_key, ts_base, ts_off, out, lims, nlims, s);
-        const int np = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, !limited && !nofuse);
-        if (np != npass) throw HipError("radix pass count mismatch", __FILE__, __LINE__);
-        hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
-                           sc.tile_valid, nullptr);
-        hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg,
-                           sc.tile_valid, ntiles, (Agg *)sc.tile_carry, sc.counters);
-        hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key,
-                           (const Agg *)sc.tile_carry, sc, 0);
-    }
-    if (!(stages & 2)) return;
-    // stage B: flows (the rule state), deferred replays, results
+    hipLaunchKernelGGL(cls, dim3(ntiles), dim3(kThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base, n, simple,
+                       invalid_key, sc.el[0], out, (limited || nofuse) ? 0 : d0, ntiles, sc.radix.hist,
+                       (lb && !limited) ? npass : 0, sc.radix.ghist);
+    if (!simple) apply_limiters(st.param, sc, sc.el[0], n, invalid_key, ts_base, ts_off, out, lims, nlims, s);
+    const int np = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, !limited && !nofuse);
+    if (np != npass) throw HipError("radix pass count mismatch", __FILE__, __LINE__);
+    hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
+                       sc.tile_valid, nullptr);
+    hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
+                       ntiles, (Agg *)sc.tile_carry, sc.counters);
+    hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key, (const Agg *)sc.tile_carry,
+                       sc);
     const uint64_t max_flows = n < st.nslots ? n : st.nslots;
     uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows + kThreads - 1) / kThreads, 16384);
     if (fb == 0) fb = 1;
     hipLaunchKernelGGL(k_flows, dim3(fb), dim3(kThreads), 0, s, st, sc, ts_base, simple);
     hipLaunchKernelGGL(k_flows_slow, dim3(std::min<uint32_t>(fb, 1024)), dim3(kThreads), 0, s, st, sc, acquire, prio,
                        ts_off, ts_base, el, simple, out);
-    hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, invalid_key, out, 0);
+    hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, invalid_key, out);
 }
 
 // ---------------------------------------------------------------- cluster parameter flow (host)
@@ -2321,7 +2570,7 @@ void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
         hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
                            ntiles, (Agg *)sc.tile_carry, sc.counters);
         hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key,
-                           (const Agg *)sc.tile_carry, sc, 0);
+                           (const Agg *)sc.tile_carry, sc);
     };
     if (nslow < n) {  // key-parallel path (elements keyed by kidx, invalid = kmask + 1)
         const uint32_t kinv = st.kmask + 1;
@@ -2331,7 +2580,7 @@ void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
         const uint64_t *el = sc.el[np & 1];
         runs(el, kinv);
         hipLaunchKernelGGL(k_pflows, dim3(fb), dim3(kThreads), 0, s, st, sc, el, acquire, ts_base, ts_off, out);
-        hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, kinv, out, 0);
+        hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, kinv, out);
     }
     if (nslow > 0) {  // sequential path, one lane per rule
         int bits = 1;

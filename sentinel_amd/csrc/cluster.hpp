@@ -88,6 +88,59 @@ struct RAgg {
     uint32_t nh, flag, cnt;
 };
 
+// Per-run record of a hot rule (k_hot_flows), read per request by k_hot_final / k_prio_results.
+// The first 32 bytes are all that a non-prioritized request needs.
+struct HotRun {
+    int64_t s0;       // window PASS sum before the run
+    double thr;       // threshold used
+    double isec;      // intervalInSecond
+    uint32_t f;       // passing prefix length
+    uint32_t start;   // rank of the run's first request among the rule's requests of the batch
+    uint32_t n;       // requests in the run (0: the rule has no request in this bucket)
+    uint32_t p0;      // index of the run's first prioritized request in the prioritized region
+    uint32_t cpf;     // prioritized requests inside the prefix
+    uint32_t cw;      // occupied (SHOULD_WAIT) requests among the prioritized after the prefix
+    uint16_t wait;    // waitInMs = 1000 / sampleCount
+    uint8_t ok;       // closed form applied (0: never expected, counted in the error flags)
+    uint8_t pad;
+    uint32_t pad2[3];
+};
+static_assert(sizeof(HotRun) == 64, "hot run record");
+
+// Hot path geometry.
+constexpr int kHot = 4096;          // hot ids (12 bits in the request code)
+constexpr uint16_t kColdId = 0xFFFF;
+constexpr int kHotSeg = 8192;       // requests per wave segment of k_hot_classify (one count row)
+constexpr int kSubSeg = 1024;       // cold compaction segment = sort input segment (4 per sort tile)
+constexpr int kHotBuckets = 64;     // window buckets a batch may span on the hot path (6 bits)
+constexpr int kHotPreRows = 256;    // count snapshots at bucket boundaries inside a segment
+constexpr int kHotGroupRows = 16;   // count rows per group of the column scan
+
+// Per-batch control words (BatchScratch::counters, zeroed per batch).
+enum : int {
+    CTL_NVALID = 0, CTL_NRUNS = 1, CTL_NFLOWS = 2, CTL_LIMITED = 4, CTL_LIMRUNS = 5, CTL_DEFERRED = 6,
+    CTL_FLAGS = 16,      // hot-path fallback reasons (kFlag*)
+    CTL_NEL0 = 17,       // elements emitted by k_hot_classify pass 0 (cold + prioritized hot)
+    CTL_NEL1 = 18,       // elements emitted by pass 1 (fallback: every valid request)
+    CTL_NPRIO = 19,      // prioritized hot requests (pass 0)
+    CTL_NSORT = 20,      // elements to sort
+    CTL_NCOLD = 21,      // cold elements (the sorted prefix the run kernels read)
+    CTL_NPRE = 22,       // count snapshots used
+    CTL_BDLO = 23,       // hot bucket delta of the batch's first request
+    CTL_BDHI = 24,       // largest hot bucket delta
+    CTL_MODE = 25,       // 1: the batch runs the hot path
+    CTL_HOTERR = 26,     // hot runs that needed a replay (never expected)
+    CTL_WORDS = 64
+};
+enum : uint32_t {
+    kFlagUnsorted = 1,   // timestamps decrease somewhere: no bucket order to rank by
+    kFlagMixed = 2,      // a hot request with acquireCount != 1
+    kFlagBucket = 4,     // the batch spans more than kHotBuckets hot buckets
+    kFlagPre = 8,        // more than kHotPreRows in-segment bucket boundaries
+    kFlagRerun = 15,     // any of the above: pass 1 re-classifies every request as cold
+    kFlagState = 16      // a hot rule's window holds a bucket newer than the batch (precheck)
+};
+
 // Per-batch scratch (device), sized for max_batch events.
 struct BatchScratch {
     uint64_t *el[2];          // packed sort elements (double buffer)
@@ -103,32 +156,34 @@ struct BatchScratch {
     void *tile_agg;
     void *tile_carry;
     uint32_t *tile_valid;
-    uint32_t *counters;  // [0]=nvalid [1]=nruns [2]=nflows [4]=limited [5]=limiter runs [6]=deferred flows
-                         // [8]=cold elements [9]=hot elements [10]=both (hot/cold split batches)
-    uint32_t *lim_partial;  // scan partials over max_batch elements (namespace limiter pre-pass)
+    uint32_t *counters;       // CTL_* words
+    uint32_t *lim_partial;    // scan partials over max_batch elements (namespace limiter pre-pass)
     RadixScratch radix;
     size_t cap = 0;
-    // Hot rules (hot/cold split).  The set persists across batches (chosen from
-    // the previous batch's per-rule request counts); it only decides how a request reaches its
-    // rule's arrival-ordered segment, never what is decided.
+    // ---- hot path.  The hot set persists across batches (chosen from the previous batch's
+    // per-rule request counts); it only decides how a request reaches its decision, never what
+    // is decided.
     uint16_t *hot_of;         // per rule slot: hot id, kColdId = cold
     uint32_t *hot_slot;       // per hot id: rule slot
-    uint32_t *hot_ctl;        // [0] hot ids in use  [1] picks of the running selection  [8..40) log2 count bins
-    uint64_t *el_tile;        // classify output, per 1024-request wave segment: cold elements from the front
-                              // (arrival order), hot elements from the back (hot id and in-tile rank in the
-                              // slot field)
-    uint32_t *tile_nc, *tile_nh;  // per tile and wave segment (4 x 1024 slots): cold / hot elements
-    uint16_t *hcnt;           // [tile][kHot]: hot requests of the tile per hot id
-    uint32_t *hpre;           // [tile][kHot]: hot-region position of the tile's first request of the hot id
-    uint32_t *hgsum;          // [tile group][kHot]: group sums, then exclusive prefixes over groups
-    uint32_t *hot_tot, *hot_base, *hot_first_run;  // per hot id
-    uint32_t *hgcnt;          // per tile group: cold, hot element counts
-    int hot_enabled = 0;      // host policy (sga_set_hot_rules); off by default (slower at C3)
+    uint32_t *hot_next;       // next batch's hot set while it is picked
+    uint32_t *hot_ctl;        // [0] hot ids in use [1] picks [2] hot window length [3] next window length
+                              // [4..5] best (count << 32 | slot) [8..40) log2 count bins
+    uint64_t *el_tile;        // classify output per 1024-request segment: cold elements + prioritized hot
+                              // requests (hot key), arrival order
+    uint32_t *tile_nc;        // per 1024-request segment: elements
+    uint32_t *hcode;          // per request: hot id | in-segment rank << 12 | bucket << 25 (~0: other)
+    uint16_t *hcnt;           // [segment][kHot] hot requests per hot id
+    uint32_t *hbase;          // [segment][kHot] rank of the segment's first request of the hot id
+    uint32_t *hgsum;          // [group][kHot] group sums, then exclusive prefixes over groups
+    uint16_t *hpre;           // [kHotPreRows][kHot] counts before an in-segment bucket boundary
+    uint32_t *hbnd;           // [kHotBuckets] first request of the bucket: segment << 9 | pre row + 1
+    HotRun *hrun;             // [kHot][kHotBuckets]
+    uint32_t *prank;          // per prioritized hot request (sorted region order): its rank
+    uint32_t *plo, *phi;      // per hot id: its range in the prioritized region
+    uint32_t *hot_tot;        // per hot id: requests in the batch
+    int hot_enabled = 1;      // host policy (sga_set_hot_rules)
     uint32_t hot_min = 64;    // smallest per-batch request count that makes a rule hot
 };
-
-constexpr int kHot = 4096;          // hot ids (12 bits in the hot element)
-constexpr uint16_t kColdId = 0xFFFF;
 
 // Forget the hot set (rule slots changed or scratch re-carved).
 void hot_reset(const ClusterState &st, BatchScratch &b, uint32_t nslots_cap, hipStream_t stream);
@@ -145,10 +200,7 @@ void batch_scratch_carve(BatchScratch &b, void *base, size_t cap, uint32_t nslot
 void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
                           const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, int simple,
                           void *out /* sga_token_result */, hipStream_t stream, const LimiterPass *lims = nullptr,
-                          int nlims = 0, int stages = 3);
-// stages: 1 = stage A only (classify, limiter pre-pass, sort, runs: reads no rule state), 2 = stage B
-// only (flows, deferred replays, results, on the same scratch), 3 = both.  A pipelined caller runs
-// stage A of batch b + 1 beside stage B of batch b on two scratch sets (no limiters, no hot split).
+                          int nlims = 0);
 
 // ---------------------------------------------------------------------------------------------
 // Cluster parameter flow (ClusterParamFlowChecker + ClusterParamMetric, CS/flow/ClusterParamFlowChecker.java:37-120,

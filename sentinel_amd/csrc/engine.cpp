@@ -364,56 +364,37 @@ struct Engine {
         d_scratch.alloc(bytes);
         batch_scratch_carve(scratch, d_scratch.p, cfg.max_batch, p2);
         scratch_slots_cap = p2;
-        d_scratch2.release();  // the pipeline's second scratch set is re-carved on its next use
         hot_reset(state(), scratch, p2, stream);
     }
 
-    // ---- pipelined device batches (sga_request_tokens_device_async): stage A (classify, sort, runs)
-    // of batch b + 1 runs on pst[0] beside stage B (flows, results) of batch b on pst[1]; batches
-    // alternate between two scratch sets.  Every other API call drains the pipeline first.
-    hipStream_t pst[2] = {nullptr, nullptr};
-    hipEvent_t pev_in = nullptr, pev_a[2] = {nullptr, nullptr}, pev_b[2] = {nullptr, nullptr};
-    bool pev_b_live[2] = {false, false};
-    DevBuf<uint8_t> d_scratch2;
-    BatchScratch scratch2;
-    uint64_t pseq = 0;
-    bool pipe_busy = false;
+    // ---- caller streams (device entries).  Every device batch is ordered after all earlier
+    // engine work and all later engine work is ordered after it, whichever stream it ran on: the
+    // caller's stream first waits for the engine stream, then the engine stream waits for the
+    // caller's stream.  Rule loads, the shared batch scratch and host-side calls therefore never
+    // overlap a batch still in flight on another stream.
+    hipEvent_t ev_eng = nullptr, ev_call = nullptr;
 
-    void drain() {
-        if (!pipe_busy) return;
-        SGA_HIP_CHECK(hipStreamSynchronize(pst[0]));
-        SGA_HIP_CHECK(hipStreamSynchronize(pst[1]));
-        pipe_busy = false;
+    hipStream_t enter_stream(void *hs) {
+        if (!hs || (hipStream_t)hs == stream) return stream;
+        if (!ev_eng) {
+            SGA_HIP_CHECK(hipEventCreateWithFlags(&ev_eng, hipEventDisableTiming));
+            SGA_HIP_CHECK(hipEventCreateWithFlags(&ev_call, hipEventDisableTiming));
+        }
+        SGA_HIP_CHECK(hipEventRecord(ev_eng, stream));
+        SGA_HIP_CHECK(hipStreamWaitEvent((hipStream_t)hs, ev_eng, 0));
+        return (hipStream_t)hs;
     }
 
-    void ensure_pipeline() {
-        if (!pst[0]) {
-            for (int i = 0; i < 2; ++i) {
-                SGA_HIP_CHECK(hipStreamCreateWithFlags(&pst[i], hipStreamNonBlocking));
-                SGA_HIP_CHECK(hipEventCreateWithFlags(&pev_a[i], hipEventDisableTiming));
-                SGA_HIP_CHECK(hipEventCreateWithFlags(&pev_b[i], hipEventDisableTiming));
-            }
-            SGA_HIP_CHECK(hipEventCreateWithFlags(&pev_in, hipEventDisableTiming));
-        }
-        ensure_scratch();
-        if (!d_scratch2.p) {
-            SGA_HIP_CHECK(hipStreamSynchronize(stream));
-            d_scratch2.alloc(batch_scratch_bytes(cfg.max_batch, scratch_slots_cap));
-            batch_scratch_carve(scratch2, d_scratch2.p, cfg.max_batch, scratch_slots_cap);
-            scratch2.hot_enabled = 0;
-            pev_b_live[1] = false;
-        }
+    void leave_stream(hipStream_t cs) {
+        if (cs == stream) return;
+        SGA_HIP_CHECK(hipEventRecord(ev_call, cs));
+        SGA_HIP_CHECK(hipStreamWaitEvent(stream, ev_call, 0));
     }
 
-    void release_pipeline() {
-        for (int i = 0; i < 2; ++i) {
-            if (pst[i]) (void)hipStreamDestroy(pst[i]);
-            if (pev_a[i]) (void)hipEventDestroy(pev_a[i]);
-            if (pev_b[i]) (void)hipEventDestroy(pev_b[i]);
-            pst[i] = nullptr;
-        }
-        if (pev_in) (void)hipEventDestroy(pev_in);
-        pev_in = nullptr;
+    void release_events() {
+        if (ev_eng) (void)hipEventDestroy(ev_eng);
+        if (ev_call) (void)hipEventDestroy(ev_call);
+        ev_eng = ev_call = nullptr;
     }
 
     uint32_t alloc_slot() {
@@ -575,12 +556,13 @@ using sga::Engine;
 using sga::SlotHost;
 using sga::CEV_N;
 
+// No exception crosses the C ABI: HIP errors map to -EIO, host allocation failures to -ENOMEM and
+// anything else (a standard-library container throwing, say) to -EIO with its message.
 template <typename F>
-static int guarded(sga_engine *e, F &&f, bool drain_first = true) {
+static int guarded(sga_engine *e, F &&f) {
     if (!e) return SGA_EINVAL;
     std::lock_guard<std::mutex> lk(e->impl.mu);
     try {
-        if (drain_first) e->impl.drain();  // pipelined batches complete before any other call
         return f(e->impl);
     } catch (const sga::HipError &h) {
         e->impl.err = h.what;
@@ -588,6 +570,12 @@ static int guarded(sga_engine *e, F &&f, bool drain_first = true) {
     } catch (const std::bad_alloc &) {
         e->impl.err = "out of host memory";
         return SGA_ENOMEM;
+    } catch (const std::exception &x) {
+        e->impl.err = std::string("internal error: ") + x.what();
+        return SGA_EIO;
+    } catch (...) {
+        e->impl.err = "internal error";
+        return SGA_EIO;
     }
 }
 
@@ -650,9 +638,7 @@ int sga_destroy(sga_engine *e) {
         std::lock_guard<std::mutex> lk(e->impl.mu);
         if (e->impl.stream) {
             (void)hipStreamSynchronize(e->impl.stream);
-            for (int i = 0; i < 2; ++i)
-                if (e->impl.pst[i]) (void)hipStreamSynchronize(e->impl.pst[i]);
-            e->impl.release_pipeline();
+            e->impl.release_events();
             e->impl.flow.release();
             (void)hipStreamDestroy(e->impl.stream);
         }
@@ -819,72 +805,37 @@ int sga_request_tokens_device(sga_engine *e, const int64_t *d_flow_id, const int
     return guarded(e, [&](Engine &g) {
         if (n > g.cfg.max_batch) return SGA_ERANGE;
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
-        hipStream_t s = hip_stream ? (hipStream_t)hip_stream : g.stream;
+        hipStream_t s = g.enter_stream(hip_stream);
         const auto lims = limiter_passes(g);
         sga::cluster_decide_batch(g.state(), g.scratch, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off, (uint32_t)n,
                                   0, d_out, s, lims.data(), (int)lims.size());
         SGA_HIP_CHECK(hipGetLastError());
+        g.leave_stream(s);
         return SGA_OK;
     });
 }
 
+// Kept for callers of the round-1 ABI: the device entry already returns once the batch is queued,
+// so the "async" form is the same call (batches run in submission order on the engine stream).
 int sga_request_tokens_device_async(sga_engine *e, const int64_t *d_flow_id, const int32_t *d_acquire,
                                     const uint8_t *d_prio, int64_t ts_base, const uint32_t *d_ts_off, size_t n,
                                     sga_token_result *d_out, void *hip_stream) {
-    if (n && (!d_flow_id || !d_acquire || !d_ts_off || !d_out)) return SGA_EINVAL;
-    if (ts_base < 0) return SGA_EINVAL;
-    return guarded(
-        e,
-        [&](Engine &g) {
-            if (n > g.cfg.max_batch) return SGA_ERANGE;
-            SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
-            hipStream_t cs = hip_stream ? (hipStream_t)hip_stream : g.stream;
-            const auto lims = limiter_passes(g);
-            if (!lims.empty() || g.scratch.hot_enabled || sga::radix64_lookback()) {
-                // namespace limiters / hot split / look-back sort: one stream, in submission order
-                g.drain();
-                sga::cluster_decide_batch(g.state(), g.scratch, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off,
-                                          (uint32_t)n, 0, d_out, cs, lims.data(), (int)lims.size());
-                SGA_HIP_CHECK(hipGetLastError());
-                return SGA_OK;
-            }
-            g.ensure_pipeline();
-            const int slot = (int)(g.pseq & 1);
-            sga::BatchScratch &sc = slot ? g.scratch2 : g.scratch;
-            const sga::ClusterState st = g.state();
-            SGA_HIP_CHECK(hipEventRecord(g.pev_in, cs));  // inputs ready on the caller's stream
-            SGA_HIP_CHECK(hipStreamWaitEvent(g.pst[0], g.pev_in, 0));
-            if (g.pev_b_live[slot]) SGA_HIP_CHECK(hipStreamWaitEvent(g.pst[0], g.pev_b[slot], 0));  // scratch free
-            sga::cluster_decide_batch(st, sc, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off, (uint32_t)n, 0, d_out,
-                                      g.pst[0], nullptr, 0, 1);
-            SGA_HIP_CHECK(hipEventRecord(g.pev_a[slot], g.pst[0]));
-            SGA_HIP_CHECK(hipStreamWaitEvent(g.pst[1], g.pev_a[slot], 0));
-            sga::cluster_decide_batch(st, sc, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off, (uint32_t)n, 0, d_out,
-                                      g.pst[1], nullptr, 0, 2);
-            SGA_HIP_CHECK(hipEventRecord(g.pev_b[slot], g.pst[1]));
-            SGA_HIP_CHECK(hipGetLastError());
-            g.pev_b_live[slot] = true;
-            ++g.pseq;
-            g.pipe_busy = true;
-            return SGA_OK;
-        },
-        false);
+    return sga_request_tokens_device(e, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off, n, d_out, hip_stream);
 }
 
 int sga_stream_wait(sga_engine *e, void *hip_stream) {
-    return guarded(
-        e,
-        [&](Engine &g) {
-            if (!g.pipe_busy) return SGA_OK;
-            hipStream_t cs = hip_stream ? (hipStream_t)hip_stream : g.stream;
-            SGA_HIP_CHECK(hipStreamWaitEvent(cs, g.pev_b[(g.pseq - 1) & 1], 0));
-            return SGA_OK;
-        },
-        false);
+    return guarded(e, [&](Engine &g) {
+        if (!hip_stream || (hipStream_t)hip_stream == g.stream) return SGA_OK;
+        (void)g.enter_stream(hip_stream);  // the caller's stream waits for every queued engine batch
+        return SGA_OK;
+    });
 }
 
 int sga_sync(sga_engine *e) {
-    return guarded(e, [&](Engine &) { return SGA_OK; });  // guarded drains the pipeline
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        return SGA_OK;
+    });
 }
 
 static int run_host_batch(Engine &g, const int64_t *flow_id, const int32_t *acquire, const uint8_t *prio,
@@ -1169,6 +1120,24 @@ int sga_cluster_stats(sga_engine *e, uint64_t *n_active, uint64_t *state_bytes) 
     });
 }
 
+// Path taken by the last token batch (engine diagnostics, no reference counterpart).
+int sga_cluster_batch_info(sga_engine *e, uint32_t *out, size_t n) {
+    if (!out || n == 0) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        uint32_t c[sga::CTL_WORDS];
+        uint32_t hc[8];
+        SGA_HIP_CHECK(hipMemcpyAsync(c, g.scratch.counters, sizeof(c), hipMemcpyDeviceToHost, g.stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(hc, g.scratch.hot_ctl, sizeof(hc), hipMemcpyDeviceToHost, g.stream));
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        const uint32_t v[10] = {c[sga::CTL_MODE],  c[sga::CTL_FLAGS], c[sga::CTL_NSORT], c[sga::CTL_NCOLD],
+                                c[sga::CTL_NPRIO], hc[0],             c[sga::CTL_BDLO],  c[sga::CTL_BDHI],
+                                c[sga::CTL_HOTERR], c[sga::CTL_NPRE]};
+        for (size_t i = 0; i < n && i < 10; ++i) out[i] = v[i];
+        return SGA_OK;
+    });
+}
+
 // ---------------------------------------------------------------- concurrency tokens
 // DefaultTokenService.requestConcurrentToken / releaseConcurrentToken (CS/flow/DefaultTokenService.java:67-86)
 int sga_concurrent_ops(sga_engine *e, const uint8_t *op, const uint32_t *client, const int64_t *id,
@@ -1440,7 +1409,10 @@ int sga_cluster_metric_nodes_device(sga_engine *e, int64_t now, sga_cluster_metr
     if (now < 0 || !d_n || (cap && !d_out)) return SGA_EINVAL;
     return guarded(e, [&](Engine &g) {
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
-        return cluster_nodes_impl(g, now, d_out, cap, d_n, hip_stream ? (hipStream_t)hip_stream : g.stream);
+        hipStream_t s = g.enter_stream(hip_stream);  // the window rotations write rule state
+        const int rc = cluster_nodes_impl(g, now, d_out, cap, d_n, s);
+        g.leave_stream(s);
+        return rc;
     });
 }
 

@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <new>
 
 namespace sga {
 
@@ -2332,7 +2333,14 @@ void FlowEngine::grow_map(DevBuf<PEntry> &tab, size_t &ub, size_t add) {
         hipLaunchKernelGGL(k_clear_ptab, dim3((unsigned)((nn + kT - 1) / kT)), dim3(kT), 0, stream, nt.p, (uint32_t)nn);
         hipLaunchKernelGGL(k_rehash, dim3((unsigned)((tab.n + kT - 1) / kT)), dim3(kT), 0, stream, tab.p,
                            (uint32_t)tab.n, nt.p, (uint32_t)(nn - 1), d_overflow.p);
+        uint32_t ovf = 0;
+        SGA_HIP_CHECK(hipMemcpyAsync(&ovf, d_overflow.p, 4, hipMemcpyDeviceToHost, stream));
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
+        if (ovf) {  // a key found no slot in the new table: keep the old one, report -ENOMEM
+            SGA_HIP_CHECK(hipMemsetAsync(d_overflow.p, 0, 4, stream));
+            SGA_HIP_CHECK(hipStreamSynchronize(stream));
+            throw std::bad_alloc();
+        }
         std::swap(tab.p, nt.p);
         std::swap(tab.n, nt.n);
     }
@@ -2475,6 +2483,10 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         if (param) SGA_HIP_CHECK(hipMemcpyAsync(d_param.p, param + b, m * 8, hipMemcpyHostToDevice, stream));
         else SGA_HIP_CHECK(hipMemsetAsync(d_param.p, 0, m * 8, stream));
         SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, stream));
+        // per chunk: a probe sequence that overflowed in an earlier (failed) batch must not fail
+        // every later one.  A failed batch has been partly applied (its node and breaker updates
+        // stay); the call reports -ENOMEM.
+        SGA_HIP_CHECK(hipMemsetAsync(d_overflow.p, 0, 4, stream));
         const FlowState st = state();
         const uint32_t nb = (uint32_t)((m + kT - 1) / kT);
         bool has_in = false;

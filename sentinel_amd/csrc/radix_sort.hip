@@ -499,8 +499,11 @@ __global__ __launch_bounds__(kThreads) void k_row_scan(const uint32_t *__restric
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_rs64_hist(const uint64_t *__restrict__ el, uint32_t n, int shift,
                                                         uint32_t ntiles, uint32_t *__restrict__ hist,
-                                                        const uint32_t *__restrict__ dn) {
-    // dn: element count on the device (a producer that compacts); tiles past it count nothing
+                                                        const uint32_t *__restrict__ dn,
+                                                        const uint32_t *__restrict__ tile_n) {
+    // dn: element count on the device (a producer that compacts); tiles past it count nothing.
+    // tile_n: segmented producer (as in k_rs64_sweep): wave w of tile t counts tile_n[4 t + w]
+    // elements from its segment's start.
     // After the first pass equal keys sit next to each other, so one digit often fills a whole
     // wave: lanes with equal digits are matched by ballots (as in the sweep) and only the first
     // of them adds the group's size -- at most one LDS atomic per distinct digit per wave.
@@ -512,15 +515,18 @@ __global__ __launch_bounds__(kThreads) void k_rs64_hist(const uint64_t *__restri
     const int lane = threadIdx.x & 63;
     const uint32_t wbase = tile * kTile + (threadIdx.x >> 6) * (kRounds * 64);
     if (dn) n = min(n, *dn);
+    uint32_t wn;  // elements of this wave's segment
+    if (tile_n) wn = tile_n[tile * kWaves + (threadIdx.x >> 6)];
+    else wn = n > wbase ? min((uint32_t)(kRounds * 64), n - wbase) : 0u;
     uint64_t key[kRounds];
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
         const uint32_t e = wbase + r * 64 + lane;
-        key[r] = e < n ? el[e] : 0ull;
+        key[r] = (uint32_t)(r * 64 + lane) < wn ? el[e] : 0ull;
     }
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
-        const bool valid = wbase + r * 64 + lane < n;
+        const bool valid = (uint32_t)(r * 64 + lane) < wn;
         const uint32_t d = (uint32_t)(key[r] >> shift) & (RADIX - 1);
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -996,7 +1002,7 @@ static int sort64_passes(uint64_t *a, uint64_t *alt, uint32_t n, int key_shift, 
             uint64_t *dst = (p & 1) ? alt : a;
             if (p > 0 || !hist0_ready)
                 hipLaunchKernelGGL((k_rs64_hist<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, nt, sc.hist,
-                                   p == 0 ? nullptr : dn);
+                                   p == 0 ? nullptr : dn, p == 0 ? tile_n0 : nullptr);
             hipLaunchKernelGGL(k_row_scan, dim3(RADIX), dim3(kThreads), 0, s, sc.hist, nt, sc.hist_scan, sc.ghist);
             hipLaunchKernelGGL((k_rs64_sweep<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, sc.hist_scan, dst,
                                p == 0 ? tile_n0 : nullptr, p == 0 ? nullptr : dn, sc.ghist);
@@ -1026,7 +1032,7 @@ static int sort64_passes(uint64_t *a, uint64_t *alt, uint32_t n, int key_shift, 
         const int shift = key_shift + p * D;
         if (p > 0 || !hist0_ready)
             hipLaunchKernelGGL((k_rs64_hist<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, nt, sc.hist,
-                               nullptr);
+                               nullptr, nullptr);
         hipLaunchKernelGGL(k_row_scan, dim3(RADIX), dim3(kThreads), 0, s, sc.hist, nt, sc.hist_scan, sc.ghist);
         hipLaunchKernelGGL((k_rs64_sweep<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, sc.hist_scan, dst,
                            nullptr, nullptr, sc.ghist);

@@ -163,7 +163,9 @@ class ClusterTokenServer:
                             writer.close()
                             return
                         self.conn_of += [cid] * (self.batch.n - before)
-                        full = self.batch.n >= self.batch.s.cap
+                        # the decoder also stops when the batch's value or namespace buffer is full;
+                        # a complete frame left undecoded means such a capacity stop, not a partial frame
+                        full = self.batch.n >= self.batch.s.cap or _complete_frame_at(pending, used)
                     pending = pending[used:]
                     if full:
                         await self.flush()  # drain, then decode the rest
@@ -171,10 +173,12 @@ class ClusterTokenServer:
                         break  # a partial frame waits for more bytes
                 self._schedule()
         finally:
-            await self.flush()
-            self.writers.pop(cid, None)
-            for ns in self.cm.remove_connection(self.addr.get(cid, "")):  # channelInactive
-                self.svc_connected(ns)
+            try:
+                await self.flush()
+            finally:
+                self.writers.pop(cid, None)
+                for ns in self.cm.remove_connection(self.addr.get(cid, "")):  # channelInactive
+                    self.svc_connected(ns)
 
     def svc_connected(self, ns: str):
         from .cluster import ClusterFlowRuleManager
@@ -187,7 +191,8 @@ class ClusterTokenServer:
 
     def _fire(self):
         self._scheduled = False
-        asyncio.ensure_future(self.flush())
+        fut = asyncio.ensure_future(self.flush())
+        fut.add_done_callback(_consume_exception)
 
     async def flush(self):
         async with self._lock:
@@ -231,11 +236,35 @@ class ClusterTokenServer:
                                                wait[idx], ping[idx])
             b.reset()
             self.conn_of = []
+        # one client that reset or closed its connection must not keep the others' responses back:
+        # write errors drop that connection only
         for cid, data in frames.items():
             w = self.writers.get(cid)
-            if w is not None and data:
+            if w is None or not data:
+                continue
+            try:
+                if w.is_closing():
+                    raise ConnectionResetError("closed")
                 w.write(data)
                 await w.drain()
+            except (ConnectionError, OSError, RuntimeError):
+                self.writers.pop(cid, None)
+                try:
+                    w.close()
+                except Exception:  # noqa: BLE001 - already torn down
+                    pass
+
+
+def _complete_frame_at(buf: bytes, at: int) -> bool:
+    """True when buf[at:] starts with a whole length-prefixed frame."""
+    if len(buf) - at < 2:
+        return False
+    return len(buf) - at - 2 >= int.from_bytes(buf[at:at + 2], "big")
+
+
+def _consume_exception(fut: "asyncio.Future") -> None:
+    if not fut.cancelled():
+        fut.exception()  # retrieved: a failed timed flush is not reported as "never retrieved"
 
 
 # ---------------------------------------------------------------- client side (tests, tools)
