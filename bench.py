@@ -2,7 +2,8 @@
 """Headline benchmark: admission decisions/s of the cluster token server at 1M
 rules, Zipf(1.1) (BASELINE.json metric).
 
-One process per GPU (torch.distributed.run for N > 1).  Rules shard by
+One process per GPU: `--gpus N` under torch.distributed.run (the driver's launch), or bare, in which
+case this script starts the N ranks itself.  Rules shard by
 splitmix64(flowId) mod N; every rank owns its shard's rules and decides the
 requests routed to it (no data-path collective; "weak" scaling: each rank sees
 a global batch of N * 2^24 requests at lambda = N * 1e8 requests per virtual
@@ -49,19 +50,43 @@ def parse():
     return ap.parse_args()
 
 
+def launch_ranks(args):
+    """`--gpus N` without a launcher: start N ranks with torch.distributed.run as a child process
+    (before this process touches the GPU) and exit with its code.  Rank 0 prints the line."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus={args.gpus}")
     n_gpus = world
+    one_device = os.environ.get("SGA_BENCH_ONE_DEVICE") == "1"
     import torch
     import torch.distributed as dist
+    coll = None       # process group of the metric all-gather
+    coll_backend = None
     if world > 1:
-        dist.init_process_group("gloo")
-    if os.environ.get("SGA_BENCH_ONE_DEVICE") == "1":
+        dist.init_process_group("gloo")  # barriers and the max-over-ranks timing (CPU tensors)
+        # RCCL over xGMI for the once-per-virtual-second metric all-gather; RCCL needs one device per
+        # rank, so the one-GPU rehearsal of the N-rank path gathers over gloo instead
+        coll_backend = "gloo" if one_device else "nccl"
+        coll = dist.new_group(backend=coll_backend)
+    if one_device:
         local = 0  # rehearsal of the N-rank path on a one-GPU box (every rank on device 0)
     torch.cuda.set_device(local)
 
@@ -123,64 +148,117 @@ def main():
     cluster.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_all[mine], cnt_all[mine])
     L = _lib.load()
     estream = L.sga_engine_stream(eng.handle)
-
-    # one synchronous sga_request_tokens_device per batch; SGA_BENCH_ASYNC=1 queues them with the
-    # pipelined entry instead (stage A of batch b + 1 beside stage B of batch b: measured no faster,
-    # DESIGN.md section 3)
-    submit = L.sga_request_tokens_device_async if os.environ.get("SGA_BENCH_ASYNC") == "1" else \
-        L.sga_request_tokens_device
     outs = [torch.empty(max_n + 1024, dtype=torch.int64, device=dev) for _ in range(2)]
 
-    def step(b):
-        f, a, p, t, ts_base, n = batches[b]
-        o = outs[b & 1]  # a queued batch's results stay untouched until the next batch but one
-        rc = submit(eng.handle, f.data_ptr(), a.data_ptr(), p.data_ptr(), ts_base, t.data_ptr(), n, o.data_ptr(),
-                    None)
-        if rc != 0:
-            raise RuntimeError(f"sga_request_tokens_device rc={rc}: {L.sga_last_error(eng.handle)}")
-
-    for b in range(args.warmup):
-        step(b)
-    torch.cuda.synchronize(dev)
-
-    # HIP events on the engine's stream bracket the timed steps (kernel-side duration)
+    # HIP events on the engine stream: around the whole timed region and around every batch
     hip = C.CDLL("libamdhip64.so.7")
     hip.hipEventCreate.argtypes = [C.POINTER(C.c_void_p)]
     hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
     hip.hipEventSynchronize.argtypes = [C.c_void_p]
     hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
-    ev0, ev1 = C.c_void_p(), C.c_void_p()
-    hip.hipEventCreate(C.byref(ev0))
-    hip.hipEventCreate(C.byref(ev1))
+
+    def new_event():
+        ev = C.c_void_p()
+        hip.hipEventCreate(C.byref(ev))
+        return ev
+
+    def elapsed_ms(e0, e1):
+        ms = C.c_float()
+        hip.hipEventElapsedTime(C.byref(ms), e0, e1)
+        return ms.value
+
+    ev0, ev1 = new_event(), new_event()
+    bev = [(new_event(), new_event()) for _ in range(args.steps)]
+
+    # once per virtual second: ClusterMetricNodeGenerator snapshot of this shard into HBM
+    # (sga_cluster_metric_nodes_device) + the node-wide all-gather (RCCL over xGMI at N > 1)
+    step_virtual_ms = glob_batch * 1000.0 / lam
+    metric_every = max(1, int(round(1000.0 / step_virtual_ms)))
+    act = C.c_uint64()
+    _lib.check(L.sga_cluster_stats(eng.handle, C.byref(act), None), eng.handle, "stats")
+    cap_rows = max(int(act.value), 1)
+    if world > 1:
+        caps = torch.tensor([cap_rows], dtype=torch.int64)
+        dist.all_reduce(caps, op=dist.ReduceOp.MAX)
+        cap_rows = int(caps.item())
+    side = torch.cuda.Stream(dev)
+    rows = torch.zeros((cap_rows, 4), dtype=torch.int64, device=dev)
+    cnt_rows = torch.zeros(2, dtype=torch.int32, device=dev)
+    gdev = dev if coll_backend != "gloo" else torch.device("cpu")
+    gathered = torch.empty((world * cap_rows, 4), dtype=torch.int64, device=gdev) if world > 1 else None
+    gcount = torch.empty(world * 2, dtype=torch.int32, device=gdev) if world > 1 else None
+    mev = []
+
+    def metric_snapshot(now):
+        e0, e1 = new_event(), new_event()
+        hip.hipEventRecord(e0, C.c_void_p(side.cuda_stream))
+        _lib.check(L.sga_cluster_metric_nodes_device(eng.handle, now, rows.data_ptr(), cap_rows, cnt_rows.data_ptr(),
+                                                     C.c_void_p(side.cuda_stream)), eng.handle, "clusterMetricNodes")
+        if world > 1:
+            with torch.cuda.stream(side):
+                if coll_backend == "gloo":
+                    dist.all_gather(list(gathered.chunk(world)), rows.cpu(), group=coll)
+                    dist.all_gather(list(gcount.chunk(world)), cnt_rows.cpu(), group=coll)
+                else:
+                    dist.all_gather_into_tensor(gathered, rows, group=coll)
+                    dist.all_gather_into_tensor(gcount, cnt_rows, group=coll)
+        hip.hipEventRecord(e1, C.c_void_p(side.cuda_stream))
+        mev.append((e0, e1))
+
+    def step(b, k=None):
+        f, a, p, t, ts_base, n = batches[b]
+        o = outs[b & 1]
+        if k is not None:
+            hip.hipEventRecord(bev[k][0], estream)
+        rc = L.sga_request_tokens_device(eng.handle, f.data_ptr(), a.data_ptr(), p.data_ptr(), ts_base, t.data_ptr(),
+                                         n, o.data_ptr(), None)
+        if rc != 0:
+            raise RuntimeError(f"sga_request_tokens_device rc={rc}: {L.sga_last_error(eng.handle)}")
+        if k is not None:
+            hip.hipEventRecord(bev[k][1], estream)
+            if (k + 1) % metric_every == 0:
+                metric_snapshot(int(ts_base + step_virtual_ms))
+
+    for b in range(args.warmup):
+        step(b)
+    torch.cuda.synchronize(dev)
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     hip.hipEventRecord(ev0, estream)
-    for b in range(args.warmup, nb):
-        step(b)
-    L.sga_stream_wait(eng.handle, None)  # the engine stream waits for every queued batch
+    for k, b in enumerate(range(args.warmup, nb)):
+        step(b, k)
     hip.hipEventRecord(ev1, estream)
     torch.cuda.synchronize(dev)
     t_end = time.perf_counter()
     if world > 1:
         dist.barrier()
     hip.hipEventSynchronize(ev1)
-    ms_ev = C.c_float()
-    hip.hipEventElapsedTime(C.byref(ms_ev), ev0, ev1)
+    ms_ev = elapsed_ms(ev0, ev1)
+    ms_batches = sum(elapsed_ms(e0, e1) for e0, e1 in bev)
+    ms_metrics = [elapsed_ms(e0, e1) for e0, e1 in mev]
+    coll_world, flows_gathered = None, None
+    if mev:
+        if world > 1:
+            coll_world = dist.get_world_size(coll)
+            flows_gathered = int(gcount.view(world, 2)[:, 0].to(torch.int64).sum().item())
+        else:
+            coll_world, flows_gathered = 1, int(cnt_rows[0].item())
 
     wall = t_end - t_start
     my_events = sum(batches[b][5] for b in range(args.warmup, nb))
     my_touched = sum(touched[b] for b in range(args.warmup, nb))
-    stats = torch.tensor([wall, ms_ev.value / 1e3, float(my_events), float(my_touched)], dtype=torch.float64)
+    stats = torch.tensor([wall, ms_ev / 1e3, ms_batches / 1e3, float(my_events), float(my_touched)],
+                         dtype=torch.float64)
     if world > 1:
-        tmax = stats[:2].clone()
+        tmax = stats[:3].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = stats[2:].clone()
+        tsum = stats[3:].clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         stats = torch.cat([tmax, tsum])
-    wall_max, gpu_max, total_events, total_touched = [float(x) for x in stats]
+    wall_max, gpu_max, batches_max, total_events, total_touched = [float(x) for x in stats]
 
     path = eng.batch_info()  # which path the last timed batch took (hot path or plain sort)
 
@@ -189,12 +267,15 @@ def main():
     status = ((res >> np.uint64(48)) & np.uint64(0xFF)).astype(np.int8)
     frac_ok = float((status == 0).mean())
 
-    cpu_baseline = None
+    cpu_baseline, router = None, None
     if rank == 0 and not args.no_cpu:
-        cpu_baseline = run_cpu_baseline(args, n_gpus)
+        if n_gpus == 1:
+            cpu_baseline, router = run_cpu_baseline(args, n_gpus)
+        else:
+            router = run_router_sample(args, n_gpus)
 
     # HBM traffic per step from the committed rocprofv3 PMC passes of this pipeline
-    # (tools/pmc_bench.sh -> tools/pmc_summary.py --json; 2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction)
+    # (tools/pmc_bench.sh -> tools/pmc_summary.py --json; per-kernel corrected counters)
     traffic, traffic_src = None, None
     tpath = os.path.join(ROOT, "profiles", "traffic_c3.json")
     if os.path.exists(tpath) and args.batch == PER_RANK_BATCH and args.rules == N_RULES:
@@ -207,7 +288,7 @@ def main():
         per_gpu_events = total_events / n_gpus
         per_gpu_touched = total_touched / n_gpus
         bytes_alg = per_gpu_events * (E_IN + E_OUT) + per_gpu_touched * 2 * S_FLOW  # per GPU, all timed steps
-        achieved = bytes_alg / gpu_max / 1e9
+        achieved = bytes_alg / batches_max / 1e9
         line = {
             "metric": "admission decisions/sec at 1M rules Zipf(1.1), 1/2/4/8 GPU; % HBM peak",
             "value": value,
@@ -229,12 +310,22 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "sga_request_tokens_device pipeline (classify+sort+runs+flows+results), "
-                                   "HIP events on the engine stream",
+                         "kernel": "sga_request_tokens_device pipeline (hot path + cold sort path), HIP events "
+                                   "around each batch on the engine stream",
                          "bytes_alg_per_step_per_gpu": bytes_alg / args.steps,
                          "touched_rules_per_step_per_gpu": per_gpu_touched / args.steps,
-                         "gpu_ms_per_step": gpu_max / args.steps * 1e3},
+                         "gpu_ms_per_step": batches_max / args.steps * 1e3,
+                         "engine_stream_ms_per_step": gpu_max / args.steps * 1e3},
             "cpu_baseline": cpu_baseline,
+            "metric_allgather": {"every_steps": metric_every, "calls": len(ms_metrics),
+                                 "ms_per_call": (sum(ms_metrics) / len(ms_metrics)) if ms_metrics else None,
+                                 "backend": coll_backend or "none (one rank)", "group_size": coll_world,
+                                 "flows_gathered_last_call": flows_gathered,
+                                 "rows_per_rank": cap_rows,
+                                 "what": "sga_cluster_metric_nodes_device (ClusterMetricNodeGenerator over the "
+                                         "shard's flows) + all_gather_into_tensor, once per virtual second, "
+                                         "inside the timed loop on a side stream"},
+            "host_router": router,
             "ok_fraction_last_batch": frac_ok,
             "last_batch_path": path,
         }
@@ -242,6 +333,31 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def _time_router(f, n_shards, threads):
+    from sentinel_amd import _lib
+    L = _lib.load()
+    f = np.ascontiguousarray(f, dtype=np.int64)
+    order = np.empty(len(f), dtype=np.uint32)
+    off = np.empty(n_shards + 1, dtype=np.uint64)
+    t0 = time.perf_counter()
+    rc = L.sga_route_shards(f.ctypes.data, len(f), n_shards, threads, order.ctypes.data, off.ctypes.data)
+    dt = time.perf_counter() - t0
+    if rc != 0:
+        return {"error": f"sga_route_shards rc={rc}"}
+    return {"requests": int(len(f)), "shards": n_shards, "threads": threads, "seconds": dt,
+            "requests_per_s": len(f) / dt,
+            "what": "sga_route_shards: stable counting sort of a global batch by splitmix64(flowId) mod G "
+                    "(host-side event routing, SURVEY.md 8(e)), timed on a sample of the C3 trace"}
+
+
+def run_router_sample(args, n_gpus):
+    from sentinel_amd.workload import ClusterTrace
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    tr = ClusterTrace(n_rules=args.rules, lam=LAMBDA_PER_GPU * n_gpus)
+    f, _, _, _ = tr.events(0, 1 << 22)
+    return _time_router(f, max(n_gpus, 8), threads)
 
 
 def run_cpu_baseline(args, n_gpus):
@@ -318,13 +434,14 @@ def run_cpu_baseline(args, n_gpus):
     dtn = time.perf_counter() - t0
     for o in ohs:
         L.orc_cluster_free(o)
+    router = _time_router(np.concatenate([c[0] for c in chunks]), 8, threads)
     return {"value": total / dtn, "unit": "decisions/s", "cores": threads, "kind": "port",
             "value_1thread": total / dt1,
             "sample": f"{total} requests of the rank-0 shard stream of the same C3 trace (1M rules), replayed by "
                       f"the C oracle (oracle/sentinel_oracle.c ClusterFlowChecker restatement): {threads} threads "
                       f"over disjoint rule subsets (splitmix64(flowId) mod {threads}); value_1thread = one "
                       f"thread in arrival order; reference JMH harness unavailable (no JDK on host)",
-            "seconds": dtn, "seconds_1thread": dt1}
+            "seconds": dtn, "seconds_1thread": dt1}, router
 
 
 if __name__ == "__main__":

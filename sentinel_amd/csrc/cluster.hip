@@ -138,7 +138,7 @@ __global__ __launch_bounds__(kThreads) void k_classify(ClusterState st, const in
             uint32_t d[kClsChunk];
 #pragma unroll
             for (int u = 0; u < kClsChunk; ++u)
-                d[u] = (fid[u] >= 1 && fid[u] <= (int64_t)st.dense_n) ? st.dense[fid[u] - 1] : ~0u;
+                d[u] = (fid[u] >= 1 && fid[u] <= (int64_t)st.dense_n) ? (uint32_t)st.dense[fid[u] - 1] : ~0u;
 #pragma unroll
             for (int u = 0; u < kClsChunk; ++u) {
                 hh[u] = 0;
@@ -333,6 +333,7 @@ __global__ __launch_bounds__(kRunThreads) void k_runs_up(const uint64_t *__restr
     __shared__ uint32_t wval[kRunWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (dn) n = min(n, *dn);  // hot path: the sorted cold elements come first, then prioritized hot ones
+    if (dn && blockIdx.x * (uint32_t)kTileElems >= n) return;  // past the live tiles (k_runs_tiles stops there)
     const uint32_t e0 = blockIdx.x * kTileElems + threadIdx.x * kPerThread;
     uint64_t x[kPerThread];
     el_load_blk(el, e0, n, invalid_key, x);
@@ -392,8 +393,10 @@ __device__ Agg block_excl_scan_1024(const Agg &v, Agg *total) {
 __global__ __launch_bounds__(kTileScanThreads) void k_runs_tiles(const Agg *__restrict__ tile_agg,
                                                                  const uint32_t *__restrict__ tile_valid,
                                                                  uint32_t ntiles, Agg *__restrict__ tile_carry,
-                                                                 uint32_t *__restrict__ counters) {
+                                                                 uint32_t *__restrict__ counters,
+                                                                 const uint32_t *__restrict__ dn) {
     __shared__ uint32_t ws[kTileScanThreads / 64];
+    if (dn) ntiles = min(ntiles, (*dn + kTileElems - 1) / kTileElems);  // live tiles only
     const uint32_t per = (ntiles + kTileScanThreads - 1) / kTileScanThreads;
     const uint32_t t0 = threadIdx.x * per, t1 = min(ntiles, t0 + per);
     Agg acc = agg_identity();
@@ -966,7 +969,7 @@ __global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const 
 constexpr int kH1Waves = kThreads / 64;          // segments per workgroup
 constexpr int kSubRounds = kSubSeg / 64;          // rounds per compaction segment (16)
 constexpr int kSubPerSeg = kHotSeg / kSubSeg;     // 8
-constexpr int kH1Chunk = 4;                       // rounds whose loads are in flight together
+constexpr int kH1Chunk = 4;                       // rounds per pipeline chunk
 static_assert(kSubRounds % kH1Chunk == 0, "chunks tile a compaction segment");
 static_assert(kSubSeg * 4 == kRadix64Tile, "compaction segments are the sort's input segments");
 constexpr uint32_t kNoCode = 0xFFFFFFFFu;
@@ -1022,11 +1025,31 @@ __device__ __forceinline__ uint32_t hot_count(const BatchScratch &sc) {
     return min(sc.hot_ctl[0], (uint32_t)kHot);
 }
 
-// No hot rule's window may hold a bucket newer than the batch's first request (batches submitted
-// out of time order): the closed form needs each run's bucket to be the newest.
+// floor((ts_base + t) / W) - floor(ts_base / W) = floor((r0 + t) / W), r0 = ts_base mod W: one double
+// multiply and an exact correction instead of two int64 divisions.
+__device__ __forceinline__ uint32_t bucket_delta(uint32_t t, uint32_t W, uint32_t r0, double inv) {
+    const uint64_t x = (uint64_t)r0 + t;
+    int64_t q = (int64_t)((double)x * inv);
+    const int64_t r = (int64_t)x - q * (int64_t)W;
+    if (r < 0) --q;
+    else if (r >= (int64_t)W) ++q;
+    return (uint32_t)q;
+}
+
+// Per batch: r0 and 1/W of every window-length code (the dense flowId table's wcode), and the
+// precheck: no hot rule's window may hold a bucket newer than the batch's first request (batches
+// submitted out of time order), as the closed form needs each run's bucket to be the newest.
 __global__ __launch_bounds__(kThreads) void k_hot_precheck(ClusterState st, BatchScratch sc,
                                                            const uint32_t *__restrict__ ts_off, int64_t ts_base,
                                                            uint32_t n) {
+    if (blockIdx.x == 0 && st.dense_n) {
+        const uint32_t W = st.wtab[threadIdx.x];
+        WConst wc;
+        wc.W = W;
+        wc.r0 = (uint32_t)(ts_base % (int64_t)W);
+        wc.inv = 1.0 / (double)W;
+        sc.wconst[threadIdx.x] = wc;
+    }
     const uint32_t h = blockIdx.x * kThreads + threadIdx.x;
     if (h >= hot_count(sc) || n == 0) return;
     const int64_t W = (int64_t)sc.hot_ctl[2];
@@ -1043,220 +1066,306 @@ __global__ __launch_bounds__(kThreads) void k_hot_precheck(ClusterState st, Batc
     if (bad) atomicOr(&sc.counters[CTL_FLAGS], kFlagState);
 }
 
-// Pass 0: the hot classification above.  Pass 1 (launched always, returns at once unless pass 0
-// raised a fallback flag): every valid request becomes a cold element, overwriting pass 0's sort
-// input.  Both write the BAD_REQUEST / NO_RULE_EXISTS results directly.
-template <int kPass>
-__global__ __launch_bounds__(kThreads) void k_hot_classify(ClusterState st, BatchScratch sc,
-                                                           const int64_t *__restrict__ flow_id,
-                                                           const int32_t *__restrict__ acquire,
-                                                           const uint8_t *__restrict__ prio,
-                                                           const uint32_t *__restrict__ ts_off, int64_t ts_base,
-                                                           uint32_t n, uint64_t *__restrict__ out) {
-    __shared__ uint16_t cnt[kH1Waves][kHot];
+// Pass A (k_hot_key): one wave per 1024-request compaction segment, every request independently:
+// validation (BAD_REQUEST / NO_RULE_EXISTS written directly), rule lookup, bucket deltas.  Cold
+// requests become sort elements (compacted in arrival order); every request gets a 4-byte key for
+// pass B: hot id | prioritized << 12 | hot bucket << 13 | hot << 19 (kNoKey bits when not hot).
+// Pass 1 of the batch is pass A again with no hot rules (launched always, returns at once unless
+// a fallback flag is up): every valid request becomes a cold element.
+// Software pipeline over chunks of kH1Chunk rounds with three register buffers used in rotation
+// (the loop is unrolled three times, so no buffer is copied: copying a register a load is still
+// writing waits for that load).  While chunk c is processed, the table lookups of chunk c + 1 and
+// the field loads of chunk c + 2 are in flight; loads and lookups are unconditional (clamped
+// indices, values masked when processed), so no branch stands around a load.
+constexpr uint32_t kKeyHot = 1u << 19;
+template <int kPass, bool kDense>
+__global__ __launch_bounds__(kThreads) void k_hot_key(ClusterState st, BatchScratch sc,
+                                                      const int64_t *__restrict__ flow_id,
+                                                      const int32_t *__restrict__ acquire,
+                                                      const uint8_t *__restrict__ prio,
+                                                      const uint32_t *__restrict__ ts_off, int64_t ts_base, uint32_t n,
+                                                      uint64_t *__restrict__ out) {
+    __shared__ WConst wcs[256];
     const uint32_t flags0 = sc.counters[CTL_FLAGS];
     if (kPass == 1 && !(flags0 & kFlagRerun)) return;
     const uint32_t nhot = (kPass == 0 && !(flags0 & kFlagState)) ? hot_count(sc) : 0u;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lt = lanemask_lt64(lane);
-    const uint32_t seg = blockIdx.x * kH1Waves + wave;
-    const uint32_t sbase = seg * kHotSeg;
-    uint16_t *c = cnt[wave];
-    if (nhot)
-        for (uint32_t h = lane; h < (uint32_t)kHot; h += 64) c[h] = 0;
-    __builtin_amdgcn_wave_barrier();
-    const int64_t Wh = nhot ? (int64_t)sc.hot_ctl[2] : 1;
-    const int64_t qbh = div_pos(ts_base, Wh);
-    // the request before the segment (time order; a bucket boundary at the segment start)
-    bool has_prev = false;
-    uint32_t ptso = 0, pbd = 0;
-    if (nhot && sbase > 0 && sbase - 1 < n) {
-        ptso = ts_off[sbase - 1];
-        pbd = (uint32_t)min(div_pos(ts_base + (int64_t)ptso, Wh) - qbh, (int64_t)kHotBuckets);
-        has_prev = true;
+    if (kDense) wcs[threadIdx.x] = sc.wconst[threadIdx.x];  // 256 window-length codes
+    __syncthreads();
+    const uint32_t sub = blockIdx.x * kH1Waves + wave;
+    const uint32_t ubase = sub * kSubSeg;
+    if (ubase >= n) {
+        if (lane == 0) sc.tile_nc[sub] = 0;
+        return;
     }
-    uint32_t wflags = 0, ntot = 0, nprio = 0, bdmax = 0;
+    const uint32_t Wh = nhot ? sc.hot_ctl[2] : 1u;
+    const uint32_t r0h = (uint32_t)(ts_base % (int64_t)Wh);
+    const double invh = 1.0 / (double)Wh;
+    uint32_t ptso = ubase > 0 ? ts_off[ubase - 1] : 0u;  // time order across the segment start
+    const bool first_seg = ubase == 0;
+    uint32_t wflags = 0, nc = 0;
     const bool use_prio = prio != nullptr;
-    for (int sub = 0; sub < kSubPerSeg; ++sub) {
-        const uint32_t ubase = sbase + sub * kSubSeg;
-        uint64_t *dst = sc.el_tile + (size_t)ubase;
-        uint32_t nc = 0;
-        if (ubase < n) {
-            int64_t fid[kH1Chunk], nfid[kH1Chunk];
-            int32_t acq[kH1Chunk], nacq[kH1Chunk];
-            uint32_t tso[kH1Chunk], pr[kH1Chunk], ntso[kH1Chunk], npr[kH1Chunk];
-            auto load_chunk = [&](int r0, int64_t (&f)[kH1Chunk], int32_t (&a)[kH1Chunk], uint32_t (&t)[kH1Chunk],
-                                  uint32_t (&p)[kH1Chunk]) {
+    const uint32_t send = min(n, ubase + (uint32_t)kSubSeg);
+    const int nchunks = (int)((send - ubase + kH1Chunk * 64 - 1) / (kH1Chunk * 64));
+    struct Buf {
+        int64_t f[kH1Chunk];
+        int32_t a[kH1Chunk];
+        uint32_t t[kH1Chunk], p[kH1Chunk], d[kH1Chunk], hf[kH1Chunk];
+        HashEntry e[kH1Chunk];
+    };
+    Buf B0, B1, B2;
+    // a missing prio array reads the acquire bytes instead, masked off when processed
+    const uint8_t *pr_src = use_prio ? prio : reinterpret_cast<const uint8_t *>(acquire);
+    auto load = [&](int ch, Buf &B) {
 #pragma unroll
-                for (int u = 0; u < kH1Chunk; ++u) {
-                    const uint32_t i = ubase + (r0 + u) * 64 + lane;
-                    f[u] = i < n ? flow_id[i] : 0;
-                    a[u] = i < n ? acquire[i] : 0;
-                    t[u] = i < n ? ts_off[i] : 0;
-                    p[u] = (i < n && use_prio) ? prio[i] : 0;
-                }
-            };
-            load_chunk(0, fid, acq, tso, pr);
-            for (int r0 = 0; r0 < kSubRounds; r0 += kH1Chunk) {
-                uint32_t hh[kH1Chunk], hf[kH1Chunk];
-                HashEntry e[kH1Chunk];
-                if (st.dense_n) {
-                    uint32_t d[kH1Chunk];
+        for (int u = 0; u < kH1Chunk; ++u) {
+            const uint32_t i = min(ubase + (uint32_t)(ch * kH1Chunk + u) * 64 + lane, n - 1);
+            B.f[u] = flow_id[i];
+            B.a[u] = acquire[i];
+            B.t[u] = ts_off[i];
+            B.p[u] = pr_src[i];
+        }
+    };
+    auto lookup = [&](Buf &B) {
 #pragma unroll
-                    for (int u = 0; u < kH1Chunk; ++u) {
-                        const bool in = fid[u] >= 1 && fid[u] <= (int64_t)st.dense_n;
-                        d[u] = in ? st.dense[fid[u] - 1] : ~0u;
-                        hf[u] = (in && nhot) ? st.hot_fid[fid[u] - 1] : kColdId;
-                    }
-#pragma unroll
-                    for (int u = 0; u < kH1Chunk; ++u) {
-                        hh[u] = 0;
-                        e[u] = d[u] == ~0u ? HashEntry{-1, 0, 0}
-                                           : HashEntry{fid[u], d[u] & 0xFFFFFFu, st.wtab[d[u] >> 24]};
-                    }
-                } else {
-#pragma unroll
-                    for (int u = 0; u < kH1Chunk; ++u) {
-                        hh[u] = (uint32_t)hash_flow_id(fid[u]) & st.hmask;
-                        e[u] = fid[u] > 0 ? st.htab[hh[u]] : HashEntry{0, 0, 0};
-                        hf[u] = kColdId;
-                    }
-                }
-                if (r0 + kH1Chunk < kSubRounds) load_chunk(r0 + kH1Chunk, nfid, nacq, ntso, npr);
-#pragma unroll
-                for (int u = 0; u < kH1Chunk; ++u) {
-                    const uint32_t rbase = ubase + (r0 + u) * 64;
-                    const uint32_t i = rbase + lane;
-                    const bool valid = i < n;
-                    uint32_t kind = 0, hid = kColdId, slot = 0, bd6 = 0, a7 = 0;
-                    const uint32_t p = pr[u] ? 1u : 0u;
-                    if (valid) {
-                        const int64_t f = fid[u];
-                        const int32_t a = acq[u];
-                        int8_t status = TRS_OK;
-                        HashEntry he = e[u];
-                        if (f <= 0 || a <= 0) {
-                            status = TRS_BAD_REQUEST;
-                        } else {
-                            if (!st.dense_n && he.key != f && he.key != 0) {  // continue the linear probe
-                                uint32_t q = hh[u];
-                                for (uint32_t probe = 1; probe <= st.hmask; ++probe) {
-                                    q = (q + 1) & st.hmask;
-                                    he = st.htab[q];
-                                    if (he.key == f || he.key == 0) break;
-                                }
-                            }
-                            if (he.key != f) status = TRS_NO_RULE_EXISTS;
-                        }
-                        if (status != TRS_OK) {
-                            out[i] = pack_result(status, 0, 0);
-                        } else {
-                            slot = he.slot;
-                            const int64_t W = (int64_t)he.W;
-                            const int64_t bd = div_pos(ts_base + (int64_t)tso[u], W) - div_pos(ts_base, W);
-                            a7 = (a >= 1 && a <= (int32_t)kAcqMax) ? (uint32_t)a : 0u;
-                            bd6 = (uint32_t)bd;
-                            if (bd >= (int64_t)kBdEsc) {
-                                bd6 = kBdEsc;
-                                a7 = 0;
-                            }
-                            kind = 1;
-                            if (nhot) {
-                                hid = st.dense_n ? hf[u] : sc.hot_of[slot];
-                                if (hid < nhot) {
-                                    kind = 2;
-                                    if (a != 1) wflags |= kFlagMixed;
-                                }
-                            }
-                        }
-                    }
-                    uint32_t r_in = 0, bdh = 0;
-                    if (nhot) {
-                        // time order and hot buckets: every request with an index counts
-                        const uint32_t pt = wave_shr1(tso[u], ptso);
-                        const bool hp = lane ? true : has_prev;
-                        const int64_t q = valid ? div_pos(ts_base + (int64_t)tso[u], Wh) - qbh : 0;
-                        bdh = (uint32_t)min(q, (int64_t)kHotBuckets);
-                        const uint32_t pb = wave_shr1(bdh, pbd);
-                        bool bnd_here = false;
-                        if (valid) {
-                            if (hp && tso[u] < pt) wflags |= kFlagUnsorted;
-                            if (q >= (int64_t)kHotBuckets) wflags |= kFlagBucket;
-                            if (i == 0) sc.counters[CTL_BDLO] = bdh;
-                            bdmax = max(bdmax, bdh);
-                            bnd_here = hp && bdh > pb;
-                        }
-                        ptso = lane_u32(tso[u], 63);
-                        pbd = lane_u32(bdh, 63);
-                        has_prev = true;
-                        // ranks; at a bucket boundary, the counts before it are snapshot first
-                        const uint64_t hb = __ballot(kind == 2);
-                        const uint64_t bm = __ballot(bnd_here);
-                        if (bm == 0) {
-                            if (hb) r_in = rank_part(c, hb, hid, lane, lt);
-                        } else {
-                            uint64_t rem = bm, done = 0;
-                            while (rem) {
-                                const int b = __builtin_ctzll(rem);
-                                rem &= rem - 1;
-                                const uint64_t below = (1ull << b) - 1ull;
-                                const uint64_t part = hb & below & ~done;
-                                if (part) {
-                                    const uint32_t rr = rank_part(c, part, hid, lane, lt);
-                                    if ((part >> lane) & 1ull) r_in = rr;
-                                }
-                                done |= below;
-                                const uint32_t bq = lane_u32(bdh, b);
-                                const uint32_t pq = lane_u32(pb, b);
-                                uint32_t krow = 0;
-                                if (rbase + b != sbase) {  // inside the segment: snapshot the counts
-                                    uint32_t k = 0;
-                                    if (lane == 0) k = atomicAdd(&sc.counters[CTL_NPRE], 1u);
-                                    k = lane_u32(k, 0);
-                                    if (k < (uint32_t)kHotPreRows) {
-                                        krow = k + 1;
-                                        for (uint32_t h = lane; h < (uint32_t)kHot; h += 64)
-                                            sc.hpre[(size_t)k * kHot + h] = c[h];
-                                    } else {
-                                        wflags |= kFlagPre;
-                                    }
-                                }
-                                if (lane == 0)
-                                    for (uint32_t qq = pq + 1; qq <= bq && qq < (uint32_t)kHotBuckets; ++qq)
-                                        sc.hbnd[qq] = (seg << 9) | krow;
-                            }
-                            const uint64_t part = hb & ~done;
-                            if (part) {
-                                const uint32_t rr = rank_part(c, part, hid, lane, lt);
-                                if ((part >> lane) & 1ull) r_in = rr;
-                            }
-                        }
-                        if (valid)
-                            sc.hcode[i] = (kind == 2 && !p) ? (hid | (r_in << 12) | (min(bdh, 63u) << 25)) : kNoCode;
-                    }
-                    // cold elements and prioritized hot requests, compacted in arrival order
-                    uint64_t x = 0;
-                    if (kind == 1) x = el_pack(slot, bd6, p, a7, i);
-                    else if (kind == 2 && p) x = el_pack(st.nslots + 1 + hid, r_in >> 7, 1u, r_in & 127u, i);
-                    const bool emit = kind == 1 || (kind == 2 && p);
-                    const uint64_t em = __ballot(emit);
-                    if (emit) dst[nc + (uint32_t)__popcll(em & lt)] = x;
-                    nc += (uint32_t)__popcll(em);
-                    nprio += (uint32_t)__popcll(__ballot(kind == 2 && p));
-                }
-#pragma unroll
-                for (int u = 0; u < kH1Chunk; ++u) {
-                    fid[u] = nfid[u];
-                    acq[u] = nacq[u];
-                    tso[u] = ntso[u];
-                    pr[u] = npr[u];
-                }
+        for (int u = 0; u < kH1Chunk; ++u) {
+            if (kDense) {
+                const uint64_t k = (uint64_t)(B.f[u] - 1);
+                const uint32_t kk = k < (uint64_t)st.dense_n ? (uint32_t)k : 0u;
+                const uint64_t ev = st.dense[kk];
+                B.d[u] = (uint32_t)ev;
+                B.hf[u] = (uint32_t)(ev >> 32) & 0xFFFFu;
+            } else {
+                B.d[u] = (uint32_t)hash_flow_id(B.f[u]) & st.hmask;
+                B.e[u] = st.htab[B.d[u]];
+                B.hf[u] = kColdId;
             }
         }
-        if (lane == 0) sc.tile_nc[seg * kSubPerSeg + sub] = nc;
-        ntot += nc;
+    };
+    auto process = [&](Buf &B, int ch) {
+#pragma unroll
+        for (int u = 0; u < kH1Chunk; ++u) {
+            const uint32_t rbase = ubase + (uint32_t)(ch * kH1Chunk + u) * 64;
+            const uint32_t i = rbase + lane;
+            const bool valid = i < send;
+            uint32_t d = B.d[u], hfv = B.hf[u];
+            if (kDense) {
+                const bool in = (uint64_t)(B.f[u] - 1) < (uint64_t)st.dense_n;
+                if (!in) d = ~0u;
+                if (!in || !nhot) hfv = kColdId;
+            }
+            const uint32_t p = (use_prio && B.p[u]) ? 1u : 0u;
+            uint32_t kind = 0, hid = kColdId, slot = 0, bd6 = 0, a7 = 0;
+            if (valid) {
+                const int64_t f = B.f[u];
+                const int32_t a = B.a[u];
+                int8_t status = TRS_OK;
+                uint32_t W = 0, r0 = 0;
+                double inv = 0;
+                if (f <= 0 || a <= 0) {
+                    status = TRS_BAD_REQUEST;
+                } else if (kDense) {
+                    if (d == ~0u) {
+                        status = TRS_NO_RULE_EXISTS;
+                    } else {
+                        slot = d & 0xFFFFFFu;
+                        const WConst wc = wcs[d >> 24];
+                        W = wc.W;
+                        r0 = wc.r0;
+                        inv = wc.inv;
+                    }
+                } else {
+                    HashEntry he = B.e[u];
+                    if (he.key != f && he.key != 0) {  // continue the linear probe
+                        uint32_t q = d;
+                        for (uint32_t probe = 1; probe <= st.hmask; ++probe) {
+                            q = (q + 1) & st.hmask;
+                            he = st.htab[q];
+                            if (he.key == f || he.key == 0) break;
+                        }
+                    }
+                    if (he.key != f) {
+                        status = TRS_NO_RULE_EXISTS;
+                    } else {
+                        slot = he.slot;
+                        W = he.W;
+                        r0 = (uint32_t)(ts_base % (int64_t)W);
+                        inv = 1.0 / (double)W;
+                    }
+                }
+                if (status != TRS_OK) {
+                    out[i] = pack_result(status, 0, 0);
+                } else {
+                    const uint32_t bd = bucket_delta(B.t[u], W, r0, inv);
+                    a7 = (a >= 1 && a <= (int32_t)kAcqMax) ? (uint32_t)a : 0u;
+                    bd6 = bd;
+                    if (bd >= kBdEsc) {
+                        bd6 = kBdEsc;
+                        a7 = 0;
+                    }
+                    kind = 1;
+                    if (nhot) {
+                        hid = kDense ? hfv : sc.hot_of[slot];
+                        if (hid < nhot) {
+                            kind = 2;
+                            if (a != 1) wflags |= kFlagMixed;
+                        }
+                    }
+                }
+            }
+            if (nhot) {
+                // time order (every request with an index counts) and the key for pass B
+                const uint32_t pt = wave_shr1(B.t[u], ptso);
+                const bool hp = lane ? true : !first_seg || rbase != 0;
+                if (valid && hp && B.t[u] < pt) wflags |= kFlagUnsorted;
+                ptso = lane_u32(B.t[u], 63);
+                const uint32_t q = valid ? bucket_delta(B.t[u], Wh, r0h, invh) : 0u;
+                if (valid && q >= (uint32_t)kHotBuckets) wflags |= kFlagBucket;
+                const uint32_t bdh = min(q, (uint32_t)kHotBuckets - 1);
+                if (valid) sc.hcode[i] = (kind == 2 ? (kKeyHot | hid | (p << 12)) : 0u) | (bdh << 13);
+            }
+            // cold elements, compacted in arrival order
+            const bool emit = kind == 1;
+            const uint64_t em = __ballot(emit);
+            if (emit) sc.el_tile[(size_t)ubase + nc + (uint32_t)__popcll(em & lt)] = el_pack(slot, bd6, p, a7, i);
+            nc += (uint32_t)__popcll(em);
+        }
+    };
+    load(0, B0);
+    lookup(B0);
+    load(1, B1);
+    for (int ch = 0; ch < nchunks; ch += 3) {
+        lookup(B1);
+        load(ch + 2, B2);
+        process(B0, ch);
+        if (ch + 1 >= nchunks) break;
+        lookup(B2);
+        load(ch + 3, B0);
+        process(B1, ch + 1);
+        if (ch + 2 >= nchunks) break;
+        lookup(B0);
+        load(ch + 4, B1);
+        process(B2, ch + 2);
     }
-    if (nhot && sbase < n) {  // this segment's count row
+    if (wflags) atomicOr(&sc.counters[CTL_FLAGS], wflags);
+    if (lane == 0) sc.tile_nc[sub] = nc;  // totals: k_hot_mode (no same-address atomic per wave)
+}
+
+// Pass B (k_hot_rank): one wave per kHotSeg-request segment ranks every hot request among the
+// segment's requests of its rule in arrival order (12 ballots match equal hot ids; wave-private LDS
+// counters), rewrites its key as the code hot id | rank << 12 | bucket << 25 (kNoCode: not a
+// non-prioritized hot request), appends the prioritized hot requests to their compaction
+// segment's elements (key nslots + 1 + hot id, rank in the bucket/acquire fields), and writes the
+// segment's count row.  At a hot bucket boundary inside the segment the counts before it are
+// snapshot into a pre row; the boundary table records where every bucket of the batch starts.
+constexpr int kRankPf = 8;  // rounds of keys loaded ahead
+__global__ __launch_bounds__(kThreads) void k_hot_rank(ClusterState st, BatchScratch sc, uint32_t n) {
+    __shared__ uint16_t cnt[kH1Waves][kHot];
+    const uint32_t flags0 = sc.counters[CTL_FLAGS];
+    const uint32_t nhot = (flags0 & (kFlagRerun | kFlagState)) ? 0u : hot_count(sc);
+    if (!nhot) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt = lanemask_lt64(lane);
+    const uint32_t seg = blockIdx.x * kH1Waves + wave;
+    const uint32_t sbase = seg * kHotSeg;
+    if (sbase >= n) return;
+    uint16_t *c = cnt[wave];
+    for (uint32_t h = lane; h < (uint32_t)kHot; h += 64) c[h] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t send = min(n, sbase + (uint32_t)kHotSeg);
+    const uint32_t nrounds = (send - sbase + 63) / 64;
+    uint32_t pbd = sbase > 0 ? (sc.hcode[sbase - 1] >> 13) & 63u : 0u;
+    const bool seg0 = sbase == 0;
+    uint32_t wflags = 0, nprio = 0, bdmax = 0, np_sub = 0, nc_sub = 0;
+    uint32_t key[kRankPf];
+#pragma unroll
+    for (int k = 0; k < kRankPf; ++k) key[k] = sc.hcode[min(sbase + (uint32_t)k * 64 + lane, n - 1)];
+    for (uint32_t r0 = 0; r0 < nrounds; r0 += kRankPf) {
+        uint32_t nk[kRankPf];
+#pragma unroll
+        for (int k = 0; k < kRankPf; ++k) nk[k] = sc.hcode[min(sbase + (r0 + kRankPf + k) * 64 + lane, n - 1)];
+#pragma unroll
+        for (int k = 0; k < kRankPf; ++k) {
+            const uint32_t r = r0 + k;
+            if (r >= nrounds) break;
+            const uint32_t rbase = sbase + r * 64;
+            const uint32_t i = rbase + lane;
+            const bool valid = i < send;
+            if ((rbase & (kSubSeg - 1)) == 0) {  // a compaction segment starts: its cold element count
+                nc_sub = sc.tile_nc[rbase / kSubSeg];
+                np_sub = 0;
+            }
+            const uint32_t kv = key[k];
+            const bool hot = valid && (kv & kKeyHot);
+            const uint32_t hid = kv & 0xFFFu;
+            const uint32_t p = (kv >> 12) & 1u;
+            const uint32_t bdh = (kv >> 13) & 63u;
+            const uint32_t pbk = wave_shr1(bdh, pbd);
+            const bool hp = lane ? true : !(seg0 && r == 0);
+            const bool bnd_here = valid && hp && bdh > pbk;
+            if (valid) bdmax = max(bdmax, bdh);
+            if (i == 0) sc.counters[CTL_BDLO] = bdh;
+            pbd = lane_u32(bdh, 63);
+            uint32_t r_in = 0;
+            const uint64_t hmask = __ballot(hot);
+            const uint64_t bm = __ballot(bnd_here);
+            if (bm == 0) {
+                if (hmask) r_in = rank_part(c, hmask, hid, lane, lt);
+            } else {
+                uint64_t rem = bm, done = 0;
+                while (rem) {
+                    const int b = __builtin_ctzll(rem);
+                    rem &= rem - 1;
+                    const uint64_t below = (1ull << b) - 1ull;
+                    const uint64_t part = hmask & below & ~done;
+                    if (part) {
+                        const uint32_t rr = rank_part(c, part, hid, lane, lt);
+                        if ((part >> lane) & 1ull) r_in = rr;
+                    }
+                    done |= below;
+                    const uint32_t bq = lane_u32(bdh, b);
+                    const uint32_t pq = lane_u32(pbk, b);
+                    uint32_t krow = 0;
+                    if (rbase + b != sbase) {  // inside the segment: snapshot the counts
+                        uint32_t kk = 0;
+                        if (lane == 0) kk = atomicAdd(&sc.counters[CTL_NPRE], 1u);
+                        kk = lane_u32(kk, 0);
+                        if (kk < (uint32_t)kHotPreRows) {
+                            krow = kk + 1;
+                            for (uint32_t h = lane; h < (uint32_t)kHot; h += 64) sc.hpre[(size_t)kk * kHot + h] = c[h];
+                        } else {
+                            wflags |= kFlagPre;
+                        }
+                    }
+                    if (lane == 0)
+                        for (uint32_t qq = pq + 1; qq <= bq && qq < (uint32_t)kHotBuckets; ++qq)
+                            sc.hbnd[qq] = (seg << 9) | krow;
+                }
+                const uint64_t part = hmask & ~done;
+                if (part) {
+                    const uint32_t rr = rank_part(c, part, hid, lane, lt);
+                    if ((part >> lane) & 1ull) r_in = rr;
+                }
+            }
+            if (valid) sc.hcode[i] = (hot && !p) ? (hid | (r_in << 12) | (bdh << 25)) : kNoCode;
+            // prioritized hot requests join their compaction segment's elements
+            const bool emit = hot && p;
+            const uint64_t em = __ballot(emit);
+            if (emit)
+                sc.el_tile[(size_t)(rbase & ~(uint32_t)(kSubSeg - 1)) + nc_sub + np_sub + (uint32_t)__popcll(em & lt)] =
+                    el_pack(st.nslots + 1 + hid, r_in >> 7, 1u, r_in & 127u, i);
+            np_sub += (uint32_t)__popcll(em);
+            if (((rbase + 64) & (kSubSeg - 1)) == 0 || rbase + 64 >= send) {
+                if (lane == 0 && np_sub) sc.tile_nc[rbase / kSubSeg] = nc_sub + np_sub;
+                nprio += np_sub;
+                np_sub = 0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kRankPf; ++k) key[k] = nk[k];
+    }
+    {  // this segment's count row
         uint32_t *row = reinterpret_cast<uint32_t *>(sc.hcnt + (size_t)seg * kHot);
         const uint32_t *cw = reinterpret_cast<const uint32_t *>(c);
         for (uint32_t k = lane; k < (nhot + 1) / 2; k += 64) row[k] = cw[k];
@@ -1264,23 +1373,50 @@ __global__ __launch_bounds__(kThreads) void k_hot_classify(ClusterState st, Batc
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) bdmax = max(bdmax, (uint32_t)__shfl_xor((int)bdmax, o, 64));
     if (wflags) atomicOr(&sc.counters[CTL_FLAGS], wflags);
-    if (lane == 0) {
-        if (ntot) atomicAdd(&sc.counters[kPass ? CTL_NEL1 : CTL_NEL0], ntot);
-        if (nprio) atomicAdd(&sc.counters[CTL_NPRIO], nprio);
-        if (nhot && sbase < n) atomicMax(&sc.counters[CTL_BDHI], bdmax);
+    if (lane == 0) {  // reduced by k_hot_mode: thousands of same-address atomics would serialize
+        sc.seg_stat[2 * seg] = nprio;
+        sc.seg_stat[2 * seg + 1] = bdmax;
     }
 }
 
-// The batch's path and element counts (one lane).
-__global__ void k_hot_mode(BatchScratch sc) {
-    if (threadIdx.x != 0) return;
+// The batch's path and element counts: sums over the compaction segments and the rank segments
+// (one workgroup).
+__global__ __launch_bounds__(1024) void k_hot_mode(BatchScratch sc, uint32_t nsub, uint32_t nseg) {
+    __shared__ uint32_t red[3][16];
     const uint32_t f = sc.counters[CTL_FLAGS];
-    const bool rerun = (f & kFlagRerun) != 0;
     const uint32_t nhot = (f & (kFlagRerun | kFlagState)) ? 0u : hot_count(sc);
-    const uint32_t ns = rerun ? sc.counters[CTL_NEL1] : sc.counters[CTL_NEL0];
-    sc.counters[CTL_NSORT] = ns;
-    sc.counters[CTL_NCOLD] = ns - (nhot ? sc.counters[CTL_NPRIO] : 0u);
-    sc.counters[CTL_MODE] = nhot ? 1u : 0u;
+    uint32_t ns = 0, np = 0, bd = 0;
+    for (uint32_t k = threadIdx.x; k < nsub; k += 1024) ns += sc.tile_nc[k];
+    if (nhot)
+        for (uint32_t k = threadIdx.x; k < nseg; k += 1024) {
+            np += sc.seg_stat[2 * k];
+            bd = max(bd, sc.seg_stat[2 * k + 1]);
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        ns += (uint32_t)__shfl_xor((int)ns, o, 64);
+        np += (uint32_t)__shfl_xor((int)np, o, 64);
+        bd = max(bd, (uint32_t)__shfl_xor((int)bd, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = ns;
+        red[1][threadIdx.x >> 6] = np;
+        red[2][threadIdx.x >> 6] = bd;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t a = 0, b = 0, m = 0;
+        for (int w = 0; w < 16; ++w) {
+            a += red[0][w];
+            b += red[1][w];
+            m = max(m, red[2][w]);
+        }
+        sc.counters[CTL_NSORT] = a;
+        sc.counters[CTL_NPRIO] = b;
+        sc.counters[CTL_NCOLD] = a - b;
+        sc.counters[CTL_BDHI] = m;
+        sc.counters[CTL_MODE] = nhot ? 1u : 0u;
+    }
 }
 
 // Column prefix of the count rows over segments, in groups of kHotGroupRows rows.
@@ -1605,19 +1741,23 @@ __device__ __forceinline__ uint32_t flow_count(const BatchScratch &sc, uint32_t 
 __device__ __forceinline__ bool hot_eligible(const SlotParam &P) { return P.S > 1 && P.S <= 64 && P.active; }
 
 // candidate i of this batch: cold flows, then (hot path batches) the hot ids
+// (a rule's parameters are read only when its count can make it hot)
 __device__ __forceinline__ bool hot_candidate(const ClusterState &st, const BatchScratch &sc, uint32_t i,
-                                              uint32_t nflows, uint32_t nvalid, uint32_t &slot, uint32_t &count) {
+                                              uint32_t nflows, uint32_t nvalid, uint32_t hot_min, uint32_t &slot,
+                                              uint32_t &count) {
     if (i < nflows) {
         count = flow_count(sc, i, nflows, nvalid);
+        if (count < hot_min) return false;
         slot = sc.run_slot[sc.flow_first_run[i]];
     } else {
         count = sc.hot_tot[i - nflows];
+        if (count < hot_min) return false;
         slot = sc.hot_slot[i - nflows];
     }
     return count > 0 && hot_eligible(st.param[slot]);
 }
 
-__global__ __launch_bounds__(kThreads) void k_hot_hist(ClusterState st, BatchScratch sc) {
+__global__ __launch_bounds__(kThreads) void k_hot_hist(ClusterState st, BatchScratch sc, uint32_t hot_min) {
     __shared__ uint32_t bins[32];
     __shared__ unsigned long long best;
     if (threadIdx.x < 32) bins[threadIdx.x] = 0;
@@ -1628,7 +1768,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_hist(ClusterState st, BatchScr
     unsigned long long mine = 0;
     for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < ncand; i += gridDim.x * kThreads) {
         uint32_t slot, c;
-        if (!hot_candidate(st, sc, i, nflows, nvalid, slot, c)) continue;
+        if (!hot_candidate(st, sc, i, nflows, nvalid, hot_min, slot, c)) continue;
         atomicAdd(&bins[31 - __clz(c)], 1u);
         mine = max(mine, ((unsigned long long)c << 32) | slot);
     }
@@ -1639,9 +1779,9 @@ __global__ __launch_bounds__(kThreads) void k_hot_hist(ClusterState st, BatchScr
 }
 
 __device__ __forceinline__ void hot_fid_set(const ClusterState &st, uint32_t slot, uint16_t v) {
-    if (!st.dense_n || !st.hot_fid) return;
+    if (!st.dense_n || !st.dense_hot) return;
     const int64_t f = st.slot_fid[slot];
-    if (f >= 1 && f <= (int64_t)st.dense_n) st.hot_fid[f - 1] = v;
+    if (f >= 1 && f <= (int64_t)st.dense_n) st.dense_hot[4 * (f - 1) + 2] = v;  // bits 32..47 of the entry
 }
 
 __global__ __launch_bounds__(kThreads) void k_hot_clear(ClusterState st, BatchScratch sc) {
@@ -1672,7 +1812,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_pick(ClusterState st, BatchScr
     const uint32_t ncand = nflows + (sc.counters[CTL_MODE] ? hot_count(sc) : 0u);
     for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < ncand; i += gridDim.x * kThreads) {
         uint32_t slot, c;
-        if (!hot_candidate(st, sc, i, nflows, nvalid, slot, c) || c < thr) continue;
+        if (!hot_candidate(st, sc, i, nflows, nvalid, thr, slot, c)) continue;
         if ((uint32_t)st.param[slot].W != wbest) continue;
         const uint32_t hid = atomicAdd(&sc.hot_ctl[1], 1u);
         if (hid < (uint32_t)kHot) {
@@ -1705,9 +1845,9 @@ __global__ __launch_bounds__(kThreads) void k_hot_fin(ClusterState st, BatchScra
 __global__ void k_hot_reset(ClusterState st, BatchScratch sc, uint32_t nslots_cap) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nslots_cap; i += gridDim.x * blockDim.x)
         sc.hot_of[i] = kColdId;
-    if (st.hot_fid)
+    if (st.dense_hot)
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < st.dense_n; i += gridDim.x * blockDim.x)
-            st.hot_fid[i] = kColdId;
+            st.dense_hot[4 * (size_t)i + 2] = kColdId;
     if (blockIdx.x == 0 && threadIdx.x < 64) sc.hot_ctl[threadIdx.x] = 0;
 }
 
@@ -1723,16 +1863,37 @@ __global__ void k_metric_sums(ClusterState st, uint32_t s, int64_t now, int64_t 
 __global__ __launch_bounds__(kThreads) void k_cluster_nodes(ClusterState st, const int64_t *__restrict__ slot_fid,
                                                             int64_t now, sga_cluster_metric_node *out, uint32_t cap,
                                                             uint32_t *count) {
+    __shared__ uint32_t wbase[kThreads / 64];
+    __shared__ uint32_t base;
     const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
-    if (s >= st.nslots || !st.param[s].active) return;
-    const SlotParam P = st.param[s];
-    sga_cluster_metric_node m;
-    m.flow_id = slot_fid[s];
-    m.block_qps = get_avg(st, P, s, now, CEV_BLOCK);
-    m.pass_qps = get_avg(st, P, s, now, CEV_PASS);
-    m.timestamp = now;
-    const uint32_t k = atomicAdd(count, 1u);
-    if (k < cap) out[k] = m;
+    const bool act = s < st.nslots && st.param[s].active;
+    sga_cluster_metric_node m{};
+    if (act) {
+        const SlotParam P = st.param[s];
+        m.flow_id = slot_fid[s];
+        m.block_qps = get_avg(st, P, s, now, CEV_BLOCK);
+        m.pass_qps = get_avg(st, P, s, now, CEV_PASS);
+        m.timestamp = now;
+    }
+    // one reservation per workgroup (a same-address atomic per node would serialize the kernel)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t bm = __ballot(act);
+    if (lane == 0) wbase[wave] = (uint32_t)__popcll(bm);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < kThreads / 64; ++w) {
+            const uint32_t c = wbase[w];
+            wbase[w] = t;
+            t += c;
+        }
+        base = t ? atomicAdd(count, t) : 0u;
+    }
+    __syncthreads();
+    if (act) {
+        const uint32_t k = base + wbase[wave] + (uint32_t)__popcll(bm & lanemask_lt64(lane));
+        if (k < cap) out[k] = m;
+    }
 }
 
 __global__ void k_init_slots(ClusterState st, const uint32_t *slots, uint32_t n) {
@@ -2361,6 +2522,8 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up((size_t)kHot * kHotBuckets * sizeof(HotRun));                   // hrun
     b += align_up(cap * 4);                                                        // prank
     b += 3 * align_up(kHot * 4);                                                   // plo, phi, hot_tot
+    b += align_up(256 * sizeof(WConst));
+    b += align_up(segs_alloc * 2 * 4);                                             // seg_stat
     return b;
 }
 
@@ -2416,11 +2579,13 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.plo = (uint32_t *)take(kHot * 4);
     sc.phi = (uint32_t *)take(kHot * 4);
     sc.hot_tot = (uint32_t *)take(kHot * 4);
+    sc.wconst = (WConst *)take(256 * sizeof(WConst));
+    sc.seg_stat = (uint32_t *)take(segs_alloc * 2 * 4);
     sc.cap = cap;
 }
 
 void hot_reset(const ClusterState &st, BatchScratch &sc, uint32_t nslots_cap, hipStream_t s) {
-    const uint32_t m = std::max(nslots_cap, st.hot_fid ? st.dense_n : 0u);
+    const uint32_t m = std::max(nslots_cap, st.dense_hot ? st.dense_n : 0u);
     hipLaunchKernelGGL(k_hot_reset, dim3(std::max<uint32_t>(1, std::min<uint32_t>((m + 255) / 256, 4096))),
                        dim3(256), 0, s, st, sc, nslots_cap);
 }
@@ -2442,11 +2607,13 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, CTL_WORDS * 4, s));
     SGA_HIP_CHECK(hipMemsetAsync(sc.plo, 0, 2 * align_up(kHot * 4), s));  // plo and phi (adjacent)
     hipLaunchKernelGGL(k_hot_precheck, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc, ts_off, ts_base, n);
-    hipLaunchKernelGGL(k_hot_classify<0>, dim3(nwg), dim3(kThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off,
-                       ts_base, n, out);
-    hipLaunchKernelGGL(k_hot_classify<1>, dim3(nwg), dim3(kThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off,
-                       ts_base, n, out);
-    hipLaunchKernelGGL(k_hot_mode, dim3(1), dim3(64), 0, s, sc);
+    auto hka = st.dense_n ? k_hot_key<0, true> : k_hot_key<0, false>;
+    auto hkb = st.dense_n ? k_hot_key<1, true> : k_hot_key<1, false>;
+    const uint32_t nsub_wg = (n + kH1Waves * kSubSeg - 1) / (kH1Waves * kSubSeg);
+    hipLaunchKernelGGL(hka, dim3(nsub_wg), dim3(kThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out);
+    hipLaunchKernelGGL(k_hot_rank, dim3(nwg), dim3(kThreads), 0, s, st, sc, n);
+    hipLaunchKernelGGL(hkb, dim3(nsub_wg), dim3(kThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out);
+    hipLaunchKernelGGL(k_hot_mode, dim3(1), dim3(1024), 0, s, sc, nsub_wg * kH1Waves, nseg);
     hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
     hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, s, sc, ngroups);
     hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
@@ -2459,7 +2626,7 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
                        sc.tile_valid, sc.counters + CTL_NCOLD);
     hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
-                       ntiles, (Agg *)sc.tile_carry, sc.counters);
+                       ntiles, (Agg *)sc.tile_carry, sc.counters, sc.counters + CTL_NCOLD);
     hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key, (const Agg *)sc.tile_carry,
                        sc);
     const uint64_t max_flows = n < st.nslots ? n : st.nslots;
@@ -2471,8 +2638,8 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, invalid_key, out);
     hipLaunchKernelGGL(k_hot_final, dim3(nwg), dim3(kThreads), 0, s, sc, n, out);
     hipLaunchKernelGGL(k_prio_results, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el, out);
-    const uint32_t sb = std::min<uint32_t>(fb, 1024);
-    hipLaunchKernelGGL(k_hot_hist, dim3(sb), dim3(kThreads), 0, s, st, sc);
+    const uint32_t sb = std::min<uint32_t>(fb, 128);  // few workgroups: their bins meet in global atomics
+    hipLaunchKernelGGL(k_hot_hist, dim3(sb), dim3(kThreads), 0, s, st, sc, std::max<uint32_t>(sc.hot_min, 1));
     hipLaunchKernelGGL(k_hot_clear, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc);
     hipLaunchKernelGGL(k_hot_pick, dim3(sb), dim3(kThreads), 0, s, st, sc, sc.hot_min);
     hipLaunchKernelGGL(k_hot_fin, dim3(1), dim3(kThreads), 0, s, st, sc);
@@ -2514,7 +2681,7 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
                        sc.tile_valid, nullptr);
     hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
-                       ntiles, (Agg *)sc.tile_carry, sc.counters);
+                       ntiles, (Agg *)sc.tile_carry, sc.counters, nullptr);
     hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key, (const Agg *)sc.tile_carry,
                        sc);
     const uint64_t max_flows = n < st.nslots ? n : st.nslots;
@@ -2568,7 +2735,7 @@ void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
         hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
                            sc.tile_valid, nullptr);
         hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
-                           ntiles, (Agg *)sc.tile_carry, sc.counters);
+                           ntiles, (Agg *)sc.tile_carry, sc.counters, nullptr);
         hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key,
                            (const Agg *)sc.tile_carry, sc);
     };

@@ -45,10 +45,10 @@ struct ClusterState {
     int64_t *rec;            // per slot: 8 fields x S buckets at rec[8*boff]; field 0 = window start
                              // (kAbsent = null), fields 1..7 = LongAdder sums per ClusterFlowEvent
     const HashEntry *htab;   // open-addressing flowId -> (slot, windowLengthInMs)
-    const uint32_t *dense;   // when flowIds are dense: dense[flowId - 1] = slot | wcode << 24 (~0u: none)
+    const uint64_t *dense;   // when flowIds are dense, per flowId - 1: bits 0..31 slot | wcode << 24 (all ones:
+                             // no rule), bits 32..47 hot id (kColdId: cold) -- one gather answers both
     const uint32_t *wtab;    // wcode -> windowLengthInMs
-    uint16_t *hot_fid;       // dense flowIds: hot id per flowId (hot_fid[flowId - 1]; kColdId = cold), so the
-                             // hot test is a gather independent of the slot lookup
+    uint16_t *dense_hot;      // the hot-id halfwords of `dense` (written when the hot set changes)
     const int64_t *slot_fid; // flowId per slot
     uint32_t dense_n;        // dense table length (0: hash lookup)
     uint32_t hmask;
@@ -120,8 +120,6 @@ constexpr int kHotGroupRows = 16;   // count rows per group of the column scan
 enum : int {
     CTL_NVALID = 0, CTL_NRUNS = 1, CTL_NFLOWS = 2, CTL_LIMITED = 4, CTL_LIMRUNS = 5, CTL_DEFERRED = 6,
     CTL_FLAGS = 16,      // hot-path fallback reasons (kFlag*)
-    CTL_NEL0 = 17,       // elements emitted by k_hot_classify pass 0 (cold + prioritized hot)
-    CTL_NEL1 = 18,       // elements emitted by pass 1 (fallback: every valid request)
     CTL_NPRIO = 19,      // prioritized hot requests (pass 0)
     CTL_NSORT = 20,      // elements to sort
     CTL_NCOLD = 21,      // cold elements (the sorted prefix the run kernels read)
@@ -139,6 +137,13 @@ enum : uint32_t {
     kFlagPre = 8,        // more than kHotPreRows in-segment bucket boundaries
     kFlagRerun = 15,     // any of the above: pass 1 re-classifies every request as cold
     kFlagState = 16      // a hot rule's window holds a bucket newer than the batch (precheck)
+};
+
+// Per batch and window-length code: windowLengthInMs, ts_base mod W, 1 / W (bucket deltas without
+// int64 division).
+struct WConst {
+    uint32_t W, r0;
+    double inv;
 };
 
 // Per-batch scratch (device), sized for max_batch events.
@@ -181,6 +186,8 @@ struct BatchScratch {
     uint32_t *prank;          // per prioritized hot request (sorted region order): its rank
     uint32_t *plo, *phi;      // per hot id: its range in the prioritized region
     uint32_t *hot_tot;        // per hot id: requests in the batch
+    WConst *wconst;           // [256] per window-length code
+    uint32_t *seg_stat;       // per rank segment: prioritized hot requests, largest hot bucket delta
     int hot_enabled = 1;      // host policy (sga_set_hot_rules)
     uint32_t hot_min = 64;    // smallest per-batch request count that makes a rule hot
 };

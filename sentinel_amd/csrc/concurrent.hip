@@ -38,7 +38,7 @@ __device__ __forceinline__ uint32_t rule_slot(const ClusterState &cs, int64_t fi
     if (fid <= 0) return kNone;
     if (cs.dense_n) {
         if (fid > (int64_t)cs.dense_n) return kNone;
-        const uint32_t u = cs.dense[fid - 1];
+        const uint32_t u = (uint32_t)cs.dense[fid - 1];
         return u == ~0u ? kNone : (u & 0xFFFFFFu);
     }
     uint32_t h = (uint32_t)hash_flow_id(fid) & cs.hmask;

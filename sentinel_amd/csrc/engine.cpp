@@ -70,8 +70,7 @@ struct Engine {
     DevBuf<int64_t> d_slot_fid;  // flowId per slot (metric snapshots)
     DevBuf<uint32_t> d_ncount;
     DevBuf<uint8_t> d_nodes;
-    DevBuf<uint32_t> d_dense;  // dense flowId table (see sync_device)
-    DevBuf<uint16_t> d_hot_fid;  // dense flowIds: hot id per flowId (hot/cold split)
+    DevBuf<uint64_t> d_dense;  // dense flowId table (see sync_device): slot entry + hot id per flowId
     DevBuf<uint32_t> d_wtab;
     uint32_t dense_n = 0;
     DevBuf<uint32_t> d_fresh;
@@ -332,7 +331,7 @@ struct Engine {
         st.rec = d_rec.p;
         st.htab = d_htab.p;
         st.dense = d_dense.p;
-        st.hot_fid = dense_n ? d_hot_fid.p : nullptr;
+        st.dense_hot = dense_n ? reinterpret_cast<uint16_t *>(d_dense.p) : nullptr;
         st.slot_fid = d_slot_fid.p;
         st.wtab = d_wtab.p;
         st.dense_n = dense_n;
@@ -504,24 +503,22 @@ struct Engine {
                 if (wvals.size() > 255) ok = false;
             }
             if (ok && maxid <= (int64_t)(4 * nact + 4096) && maxid < (int64_t)0xFFFFFFFF) {
-                std::vector<uint32_t> dt((size_t)maxid, ~0u);
+                // entry: slot | wcode << 24 in bits 0..31, hot id (cold until the hot set is picked) in 32..47
+                const uint64_t cold = (uint64_t)kColdId << 32;
+                std::vector<uint64_t> dt((size_t)maxid, cold | 0xFFFFFFFFull);
                 for (size_t i = 0; i < ns; ++i) {
                     if (!slots[i].active) continue;
                     const uint32_t W = (uint32_t)(slots[i].interval / slots[i].S);
                     const uint32_t code = (uint32_t)(std::find(wvals.begin(), wvals.end(), W) - wvals.begin());
-                    dt[(size_t)slots[i].flow_id - 1] = (uint32_t)i | (code << 24);
+                    dt[(size_t)slots[i].flow_id - 1] = cold | (uint32_t)i | (code << 24);
                 }
                 wvals.resize(256, 1);
                 if (d_dense.n < dt.size()) {
                     SGA_HIP_CHECK(hipStreamSynchronize(stream));
                     d_dense.alloc(dt.size());
                 }
-                if (d_hot_fid.n < dt.size()) {
-                    SGA_HIP_CHECK(hipStreamSynchronize(stream));
-                    d_hot_fid.alloc(dt.size());
-                }
                 if (d_wtab.n < 256) d_wtab.alloc(256);
-                SGA_HIP_CHECK(hipMemcpyAsync(d_dense.p, dt.data(), dt.size() * 4, hipMemcpyHostToDevice, stream));
+                SGA_HIP_CHECK(hipMemcpyAsync(d_dense.p, dt.data(), dt.size() * 8, hipMemcpyHostToDevice, stream));
                 SGA_HIP_CHECK(hipMemcpyAsync(d_wtab.p, wvals.data(), 256 * 4, hipMemcpyHostToDevice, stream));
                 SGA_HIP_CHECK(hipStreamSynchronize(stream));
                 dense_n = (uint32_t)maxid;

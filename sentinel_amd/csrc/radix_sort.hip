@@ -453,11 +453,14 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const uint32_t *__r
 // three of a flat scan over digits x tiles.
 constexpr int kRowItems = 8;
 __global__ __launch_bounds__(kThreads) void k_row_scan(const uint32_t *__restrict__ hist, uint32_t nt,
-                                                       uint32_t *__restrict__ hist_scan, uint32_t *__restrict__ tot) {
+                                                       uint32_t *__restrict__ hist_scan, uint32_t *__restrict__ tot,
+                                                       const uint32_t *__restrict__ dn) {
+    // dn: live element count on the device -- tiles past it have no histogram column
     __shared__ uint32_t ws[kWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t *row = hist + (size_t)blockIdx.x * nt;
     uint32_t *orow = hist_scan + (size_t)blockIdx.x * nt;
+    if (dn) nt = min(nt, (*dn + kTile - 1) / kTile);
     uint32_t carry = 0;
     for (uint32_t base = 0; base < nt; base += kThreads * kRowItems) {
         const uint32_t i0 = base + threadIdx.x * kRowItems;
@@ -515,6 +518,7 @@ __global__ __launch_bounds__(kThreads) void k_rs64_hist(const uint64_t *__restri
     const int lane = threadIdx.x & 63;
     const uint32_t wbase = tile * kTile + (threadIdx.x >> 6) * (kRounds * 64);
     if (dn) n = min(n, *dn);
+    if (!tile_n && tile * kTile >= n) return;  // past the live elements (k_row_scan skips the tile)
     uint32_t wn;  // elements of this wave's segment
     if (tile_n) wn = tile_n[tile * kWaves + (threadIdx.x >> 6)];
     else wn = n > wbase ? min((uint32_t)(kRounds * 64), n - wbase) : 0u;
@@ -590,6 +594,7 @@ __global__ __launch_bounds__(kThreads) void k_rs64_sweep(const uint64_t *__restr
     __shared__ uint32_t ws[kWaves];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
+    if (!tile_n && dn && blockIdx.x * (uint32_t)kTile >= min(n, *dn)) return;  // no live element
     uint32_t dexc[DPT];
     if (digit_tot) {
         __shared__ uint32_t ws2[kWaves];
@@ -1003,7 +1008,8 @@ static int sort64_passes(uint64_t *a, uint64_t *alt, uint32_t n, int key_shift, 
             if (p > 0 || !hist0_ready)
                 hipLaunchKernelGGL((k_rs64_hist<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, nt, sc.hist,
                                    p == 0 ? nullptr : dn, p == 0 ? tile_n0 : nullptr);
-            hipLaunchKernelGGL(k_row_scan, dim3(RADIX), dim3(kThreads), 0, s, sc.hist, nt, sc.hist_scan, sc.ghist);
+            hipLaunchKernelGGL(k_row_scan, dim3(RADIX), dim3(kThreads), 0, s, sc.hist, nt, sc.hist_scan, sc.ghist,
+                               p == 0 ? nullptr : dn);
             hipLaunchKernelGGL((k_rs64_sweep<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, sc.hist_scan, dst,
                                p == 0 ? tile_n0 : nullptr, p == 0 ? nullptr : dn, sc.ghist);
         }
@@ -1033,7 +1039,8 @@ static int sort64_passes(uint64_t *a, uint64_t *alt, uint32_t n, int key_shift, 
         if (p > 0 || !hist0_ready)
             hipLaunchKernelGGL((k_rs64_hist<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, nt, sc.hist,
                                nullptr, nullptr);
-        hipLaunchKernelGGL(k_row_scan, dim3(RADIX), dim3(kThreads), 0, s, sc.hist, nt, sc.hist_scan, sc.ghist);
+        hipLaunchKernelGGL(k_row_scan, dim3(RADIX), dim3(kThreads), 0, s, sc.hist, nt, sc.hist_scan, sc.ghist,
+                           nullptr);
         hipLaunchKernelGGL((k_rs64_sweep<D>), dim3(nt), dim3(kThreads), 0, s, src, n, shift, sc.hist_scan, dst,
                            nullptr, nullptr, sc.ghist);
         uint64_t *t = src;
