@@ -669,16 +669,28 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
     if (ri.cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) return false;
     int64_t bp = 0, hstart = kAbsent, hpass = 0;
     {
-        // (start, PASS) pairs: one 16-byte load per bucket
+        // (start, PASS) pairs: one 16-byte load per bucket.  Up to 16 buckets (sampleCount 10 is
+        // the default) the loads are issued together before any is used: a loop that waits for
+        // each bucket's load in turn pays S memory latencies per run.
         const int4 *v = reinterpret_cast<const int4 *>(R.r);
-        for (int jj = 0; jj < P.S; ++jj) {
-            const int4 sp = v[jj];
+        auto take = [&](int jj, const int4 &sp) {
             const int64_t w = i64_lo(sp), pv = i64_hi(sp);
             if (jj == jh) {
                 hstart = w;
                 hpass = pv;
             }
             if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) bp += pv;
+        };
+        if (P.S <= 16) {
+            int4 sp[16];
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj)
+                if (jj < P.S) sp[jj] = v[jj];
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj)
+                if (jj < P.S) take(jj, sp[jj]);
+        } else {
+            for (int jj = 0; jj < P.S; ++jj) take(jj, v[jj]);
         }
     }
     const bool rot = old == kAbsent || ws > old;
@@ -939,6 +951,326 @@ __global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const 
             }
             out[el_idx(x[k])] = res;
         }
+    }
+}
+
+// ---------------------------------------------------------------- fused runs / flows / results
+// One workgroup per 2048-element chunk of the sorted elements does what k_runs_* / k_flows /
+// k_flows_slow / k_results did in five launches: it owns the rules whose first element lies in its
+// chunk (the chunk's leading elements of a rule begun earlier belong to the previous chunk), so a
+// rule that runs past the chunk end is followed to its end (region [h0, E)).
+//   1 runs    : a blocked segmented scan over the region finds run heads (slot, bucket) and rule
+//               heads; each run's length, prioritized count, first prioritized index and common
+//               acquire count are written at its head position (run arrays indexed by position),
+//               prioritized positions are compacted into plist[h0 ..), rule heads into LDS.
+//   2 flows   : one lane per owned rule walks its runs in time order -- the closed form
+//               (run_fast) or the exact per-request replay (request_exact) -- and the rule's
+//               request count feeds the next batch's hot-set candidates.
+//   3 results : the same scan again; every request reads its run's record and writes its
+//               TokenResult (runs replayed in step 2 wrote theirs already).
+// Run records live in global scratch but are written and read by the same workgroup, so they
+// stay in the XCD's L2.  Elements with a slot >= nkey (invalid requests, prioritized hot
+// requests) end the data.
+constexpr int kFzThreads = 256, kFzPer = 8, kFzChunk = kFzThreads * kFzPer;  // 2048
+
+struct FAgg {
+    uint32_t hpos;  // (run head position + 1) of the last run head so far (0: none)
+    uint32_t np;    // prioritized requests so far (region-relative)
+    uint32_t hp;    // np before the last run head
+    uint32_t flag;  // run head seen
+    int32_t mn, mx; // acquire min / max since the last run head
+};
+__device__ __forceinline__ FAgg fagg_id() { return FAgg{0, 0, 0, 0, INT32_MAX, INT32_MIN}; }
+__device__ __forceinline__ FAgg fagg_combine(const FAgg &a, const FAgg &b) {
+    FAgg r;
+    r.hpos = max(a.hpos, b.hpos);
+    r.np = a.np + b.np;
+    r.hp = b.flag ? a.np + b.hp : a.hp;
+    r.flag = a.flag | b.flag;
+    r.mn = b.flag ? b.mn : min(a.mn, b.mn);
+    r.mx = b.flag ? b.mx : max(a.mx, b.mx);
+    return r;
+}
+__device__ __forceinline__ FAgg fagg_shfl_up(const FAgg &v, int o) {
+    return FAgg{shfl_up_u32(v.hpos, o), shfl_up_u32(v.np, o), shfl_up_u32(v.hp, o), shfl_up_u32(v.flag, o),
+                __shfl_up(v.mn, o, 64), __shfl_up(v.mx, o, 64)};
+}
+
+// Exclusive workgroup scan of one FAgg per thread (thread order = element order).  Returns the
+// exclusive prefix; *total gets the workgroup total.
+__device__ __forceinline__ FAgg fagg_block_excl(const FAgg &v, FAgg *total, FAgg *wtot) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    FAgg x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const FAgg y = fagg_shfl_up(x, o);
+        if (lane >= o) x = fagg_combine(y, x);
+    }
+    if (lane == 63) wtot[wave] = x;
+    __syncthreads();
+    FAgg pre = fagg_id(), t = fagg_id();
+#pragma unroll
+    for (int w = 0; w < kFzThreads / 64; ++w) {
+        if (w < wave) pre = fagg_combine(pre, wtot[w]);
+        t = fagg_combine(t, wtot[w]);
+    }
+    FAgg ex = fagg_shfl_up(x, 1);
+    if (lane == 0) ex = fagg_id();
+    *total = t;
+    __syncthreads();
+    return fagg_combine(pre, ex);
+}
+
+__global__ __launch_bounds__(kFzThreads) void k_cold_fused(ClusterState st, BatchScratch sc,
+                                                           const uint64_t *__restrict__ el, uint32_t nhost,
+                                                           const uint32_t *__restrict__ dn, uint32_t nkey,
+                                                           const int32_t *__restrict__ acquire,
+                                                           const uint8_t *__restrict__ prio,
+                                                           const uint32_t *__restrict__ ts_off, int64_t ts_base,
+                                                           int simple, uint32_t hot_min, uint64_t *__restrict__ out,
+                                                           int dbg) {
+    __shared__ uint32_t fheads[kFzChunk + 1];
+    __shared__ FAgg wtot[kFzThreads / 64];
+    __shared__ uint32_t s_h0, s_E, s_wcnt[kFzThreads / 64];
+    __shared__ uint32_t s_ncand, s_cbase, s_cand[2 * kFzThreads];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t n = dn ? min(nhost, *dn) : nhost;
+    const uint32_t c0 = blockIdx.x * kFzChunk;
+    if (c0 >= n) return;
+    const uint32_t c1 = min(n, c0 + kFzChunk);
+    auto slot_at = [&](uint32_t p) -> uint32_t { return p < n ? el_slot(el[p]) : nkey; };
+    // ---- ownership: the first rule head in the chunk (h0) and the end of the last owned rule (E)
+    if (threadIdx.x == 0) {
+        s_h0 = c1;
+        s_E = c1;
+    }
+    __syncthreads();
+    {
+        uint32_t first_head = c1, first_inv = c1;
+        for (uint32_t p = c0 + threadIdx.x; p < c1; p += kFzThreads) {
+            const uint32_t s = el_slot(el[p]);
+            if (s >= nkey) first_inv = min(first_inv, p);  // sorted: invalid / foreign keys form a suffix
+            else if (p == 0 || el_slot(el[p - 1]) != s) first_head = min(first_head, p);
+        }
+        if (first_head < c1) atomicMin(&s_h0, first_head);
+        if (first_inv < c1) atomicMin(&s_E, first_inv);
+    }
+    __syncthreads();
+    const uint32_t h0 = s_h0;
+    if (h0 >= s_E) return;  // uniform: the chunk holds no rule head
+    if (s_E == c1 && c1 < n) {  // the last owned rule may continue past the chunk
+        const uint32_t ls = el_slot(el[c1 - 1]);
+        if (el_slot(el[c1]) == ls) {  // uniform
+            __syncthreads();
+            if (threadIdx.x == 0) s_E = 0xFFFFFFFFu;
+            __syncthreads();
+            // one chunk ahead with the whole workgroup, then (long rules only) gallop + bisect
+            for (uint32_t p = c1 + threadIdx.x; p < min(n, c1 + kFzChunk); p += kFzThreads)
+                if (el_slot(el[p]) != ls) {
+                    atomicMin(&s_E, p);
+                    break;
+                }
+            __syncthreads();
+            if (threadIdx.x == 0 && s_E == 0xFFFFFFFFu) {
+                uint32_t lo = min(n, c1 + kFzChunk), step = kFzChunk;  // slot(el[lo - 1]) == ls
+                uint32_t hi = lo;
+                while (true) {  // gallop: first probe with slot != ls (or n)
+                    hi = (uint32_t)min((uint64_t)n, (uint64_t)lo + step);
+                    if (hi >= n || slot_at(hi) != ls) break;
+                    lo = hi + 1;
+                    step *= 2;
+                }
+                while (lo < hi) {  // first position in [lo, hi] with slot != ls
+                    const uint32_t m = lo + (hi - lo) / 2;
+                    if (slot_at(m) != ls) hi = m;
+                    else lo = m + 1;
+                }
+                s_E = lo;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t E = s_E;
+    // ---- 1 runs (blocks of kFzChunk elements over [h0, E))
+    FAgg carry = fagg_id();
+    uint32_t nf_carry = 0;
+    for (uint32_t b0 = h0; b0 < E; b0 += kFzChunk) {
+        const uint32_t e0 = b0 + threadIdx.x * kFzPer;
+        uint64_t x[kFzPer];
+#pragma unroll
+        for (int k = 0; k < kFzPer; ++k) x[k] = e0 + k < E ? el[e0 + k] : 0ull;
+        uint64_t px = e0 > h0 && e0 - 1 < E ? el[e0 - 1] : 0ull;
+        FAgg acc = fagg_id();
+        uint32_t nfl = 0;
+        bool hd[kFzPer], fh[kFzPer];
+#pragma unroll
+        for (int k = 0; k < kFzPer; ++k) {
+            const uint32_t p = e0 + k;
+            const bool in = p < E;
+            hd[k] = in && (p == h0 || el_runkey(x[k]) != el_runkey(px));
+            fh[k] = in && (p == h0 || el_slot(x[k]) != el_slot(px));
+            const uint32_t pr = in ? el_prio(x[k]) : 0u;
+            const int32_t a = el_acq(x[k]);
+            const FAgg v{hd[k] ? p + 1 : 0u, pr, 0u, hd[k] ? 1u : 0u, in ? a : INT32_MAX, in ? a : INT32_MIN};
+            acc = fagg_combine(acc, v);
+            nfl += fh[k] ? 1u : 0u;
+            px = x[k];
+        }
+        FAgg tot;
+        FAgg run = fagg_combine(carry, fagg_block_excl(acc, &tot, wtot));
+        // rule heads: compacted in order (wave counts through LDS)
+        uint32_t fx = nfl;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = shfl_up_u32(fx, o);
+            if (lane >= o) fx += y;
+        }
+        if (lane == 63) s_wcnt[wave] = fx;
+        __syncthreads();
+        uint32_t fbase = nf_carry + fx - nfl, ftot = 0;
+#pragma unroll
+        for (int w = 0; w < kFzThreads / 64; ++w) {
+            if (w < wave) fbase += s_wcnt[w];
+            ftot += s_wcnt[w];
+        }
+#pragma unroll
+        for (int k = 0; k < kFzPer; ++k) {
+            const uint32_t p = e0 + k;
+            if (p >= E) break;
+            const uint32_t pr = el_prio(x[k]);
+            const FAgg v{hd[k] ? p + 1 : 0u, pr, 0u, hd[k] ? 1u : 0u, el_acq(x[k]), el_acq(x[k])};
+            const uint32_t np_before = run.np;
+            run = fagg_combine(run, v);
+            if (fh[k]) fheads[fbase++] = p;
+            if (pr) sc.plist[h0 + np_before] = p;
+            // run end: this is the last element of its run
+            const bool last = p + 1 >= E || (k + 1 < kFzPer ? hd[k + 1] : (p + 1 < E && el_runkey(el[p + 1]) != el_runkey(x[k])));
+            if (last) {
+                const uint32_t head = run.hpos - 1;
+                sc.run_start[head] = p + 1 - head;  // run length (run arrays are indexed by head position)
+                sc.run_cp[head] = run.np - run.hp;
+                sc.run_p0[head] = h0 + run.hp;
+                sc.run_acq[head] = run.mn == run.mx ? run.mn : 0;  // 0: mixed or escaped -> replay
+                sc.run_bd[head] = (uint8_t)((x[k] >> kBdShift) & kBdEsc);
+            }
+        }
+        carry = fagg_combine(carry, tot);
+        nf_carry += ftot;
+        __syncthreads();
+    }
+    const uint32_t nf = nf_carry;
+    if (threadIdx.x == 0) s_ncand = 0;
+    __syncthreads();  // run records and plist (global, this workgroup) before the flows read them
+    // next-hot-set candidates: counts of at least the floor (half the last pick threshold) are
+    // gathered in LDS and published with one global reservation per workgroup
+    const uint32_t cand_floor = max(hot_min, sc.hot_ctl[7] >> 1);
+    // ---- 2 flows: one lane per owned rule
+    for (uint32_t f = threadIdx.x; f < ((dbg & 1) ? 0u : nf); f += kFzThreads) {
+        const uint32_t r0 = fheads[f];
+        const uint32_t r1 = f + 1 < nf ? fheads[f + 1] : E;
+        const uint32_t s = el_slot(el[r0]);
+        if (r1 - r0 >= cand_floor) {  // next batch's hot-set candidate
+            const uint32_t k = atomicAdd(&s_ncand, 1u);
+            if (k < (uint32_t)kFzThreads) {
+                s_cand[2 * k] = s;
+                s_cand[2 * k + 1] = r1 - r0;
+            }
+        }
+        const SlotParam P = st.param[s];
+        const Rec R = rec_of(st, P);
+        const double thr = simple ? P.thr_simple : P.thr;
+        const int64_t qbase = div_pos(ts_base, P.W);
+        for (uint32_t r = r0; r < r1;) {
+            RunIn ri;
+            ri.j0 = r;
+            ri.n = sc.run_start[r];
+            ri.cp_tot = sc.run_cp[r];
+            ri.p0 = sc.run_p0[r];
+            ri.a = sc.run_acq[r];
+            ri.bd = sc.run_bd[r];
+            if (run_fast<true>(st, sc, s, P, R, thr, qbase, ri, r)) {
+                r += ri.n;
+                continue;
+            }
+            for (uint32_t j = r; j < r + ri.n; ++j) {
+                const uint32_t i = el_idx(el[j]);
+                const int64_t t = ts_base + (int64_t)ts_off[i];
+                const bool p = !simple && prio && prio[i];
+                out[i] = request_exact(st, s, t, acquire[i], p, simple);
+            }
+            RunOut ro;
+            ro.mode = RUN_DONE;
+            sc.run_out[r] = ro;
+            r += ri.n;
+        }
+    }
+    __syncthreads();  // run_out of every owned run
+    {
+        const uint32_t nc = min(s_ncand, (uint32_t)kFzThreads);
+        if (threadIdx.x == 0) s_cbase = nc ? atomicAdd(&sc.hot_ctl[6], nc) : 0u;
+        __syncthreads();
+        const uint32_t k = s_cbase + threadIdx.x;
+        if (threadIdx.x < nc && k < (uint32_t)kHotCand) {
+            sc.hot_cand[2 * k] = s_cand[2 * threadIdx.x];
+            sc.hot_cand[2 * k + 1] = s_cand[2 * threadIdx.x + 1];
+        }
+    }
+    // ---- 3 results (the scan again)
+    carry = fagg_id();
+    for (uint32_t b0 = h0; b0 < ((dbg & 2) ? h0 : E); b0 += kFzChunk) {
+        const uint32_t e0 = b0 + threadIdx.x * kFzPer;
+        uint64_t x[kFzPer];
+#pragma unroll
+        for (int k = 0; k < kFzPer; ++k) x[k] = e0 + k < E ? el[e0 + k] : 0ull;
+        uint64_t px = e0 > h0 && e0 - 1 < E ? el[e0 - 1] : 0ull;
+        FAgg acc = fagg_id();
+        bool hd[kFzPer];
+#pragma unroll
+        for (int k = 0; k < kFzPer; ++k) {
+            const uint32_t p = e0 + k;
+            const bool in = p < E;
+            hd[k] = in && (p == h0 || el_runkey(x[k]) != el_runkey(px));
+            const FAgg v{hd[k] ? p + 1 : 0u, in ? el_prio(x[k]) : 0u, 0u, hd[k] ? 1u : 0u, 0, 0};
+            acc = fagg_combine(acc, v);
+            px = x[k];
+        }
+        FAgg tot;
+        FAgg run = fagg_combine(carry, fagg_block_excl(acc, &tot, wtot));
+        uint32_t head[kFzPer], kp[kFzPer];
+#pragma unroll
+        for (int k = 0; k < kFzPer; ++k) {
+            const uint32_t p = e0 + k;
+            const uint32_t pr = p < E ? el_prio(x[k]) : 0u;
+            run = fagg_combine(run, FAgg{hd[k] ? p + 1 : 0u, pr, 0u, hd[k] ? 1u : 0u, 0, 0});
+            head[k] = run.hpos - 1;
+            kp[k] = run.np - pr - run.hp;  // prioritized requests of the run before this one
+        }
+        // run records of the 8 elements loaded together (one per run change)
+        RunOut ro[kFzPer];
+#pragma unroll
+        for (int k = 0; k < kFzPer; ++k) {
+            if (e0 + k < E && (k == 0 || head[k] != head[k - 1])) ro[k] = sc.run_out[head[k]];
+            else if (k > 0) ro[k] = ro[k - 1];
+        }
+#pragma unroll
+        for (int k = 0; k < kFzPer; ++k) {
+            const uint32_t p = e0 + k;
+            if (p >= E || ro[k].mode != RUN_FAST) continue;
+            const uint32_t local = p - head[k];
+            const int32_t a = el_acq(x[k]);
+            uint64_t res;
+            if (local < ro[k].f) {
+                const int64_t sum = ro[k].s0 + (int64_t)local * a;
+                res = pack_result(TRS_OK, j_d2i(ro[k].thr - (double)sum / ro[k].isec - (double)a), 0);
+            } else if (el_prio(x[k]) && kp[k] - ro[k].cpf < ro[k].cw) {
+                res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)ro[k].wait);
+            } else {
+                res = pack_result(TRS_BLOCKED, 0, 0);
+            }
+            out[el_idx(x[k])] = res;
+        }
+        carry = fagg_combine(carry, tot);
+        __syncthreads();
     }
 }
 
@@ -1730,31 +2062,28 @@ __global__ __launch_bounds__(kThreads) void k_prio_results(ClusterState st, Batc
 
 // ---- next batch's hot set: rules with at least T requests in this batch, T the smallest power of
 // two (>= hot_min) that admits at most kHot rules; all of them with the window length of the
-// busiest one, 1 < sampleCount <= 64 (the occupy path needs 1000 / sampleCount > 0).
-__device__ __forceinline__ uint32_t flow_count(const BatchScratch &sc, uint32_t fl, uint32_t nflows,
-                                               uint32_t nvalid) {
-    const uint32_t e0 = sc.run_start[sc.flow_first_run[fl]];
-    const uint32_t e1 = fl + 1 < nflows ? sc.run_start[sc.flow_first_run[fl + 1]] : nvalid;
-    return e1 - e0;
-}
-
+// busiest one, 1 < sampleCount <= 64 (the occupy path needs 1000 / sampleCount > 0).  Candidates:
+// the cold rules k_cold_fused saw with at least hot_min requests, and (hot-path batches) the hot
+// rules.
 __device__ __forceinline__ bool hot_eligible(const SlotParam &P) { return P.S > 1 && P.S <= 64 && P.active; }
 
-// candidate i of this batch: cold flows, then (hot path batches) the hot ids
+__device__ __forceinline__ uint32_t hot_ncand(const BatchScratch &sc, uint32_t &ncold) {
+    ncold = min(sc.hot_ctl[6], (uint32_t)kHotCand);
+    return ncold + (sc.counters[CTL_MODE] ? hot_count(sc) : 0u);
+}
+
 // (a rule's parameters are read only when its count can make it hot)
 __device__ __forceinline__ bool hot_candidate(const ClusterState &st, const BatchScratch &sc, uint32_t i,
-                                              uint32_t nflows, uint32_t nvalid, uint32_t hot_min, uint32_t &slot,
-                                              uint32_t &count) {
-    if (i < nflows) {
-        count = flow_count(sc, i, nflows, nvalid);
-        if (count < hot_min) return false;
-        slot = sc.run_slot[sc.flow_first_run[i]];
+                                              uint32_t ncold, uint32_t hot_min, uint32_t &slot, uint32_t &count) {
+    if (i < ncold) {
+        slot = sc.hot_cand[2 * i];
+        count = sc.hot_cand[2 * i + 1];
     } else {
-        count = sc.hot_tot[i - nflows];
-        if (count < hot_min) return false;
-        slot = sc.hot_slot[i - nflows];
+        count = sc.hot_tot[i - ncold];
+        slot = sc.hot_slot[i - ncold];
     }
-    return count > 0 && hot_eligible(st.param[slot]);
+    if (count < hot_min || count == 0) return false;
+    return hot_eligible(st.param[slot]);
 }
 
 __global__ __launch_bounds__(kThreads) void k_hot_hist(ClusterState st, BatchScratch sc, uint32_t hot_min) {
@@ -1763,12 +2092,12 @@ __global__ __launch_bounds__(kThreads) void k_hot_hist(ClusterState st, BatchScr
     if (threadIdx.x < 32) bins[threadIdx.x] = 0;
     if (threadIdx.x == 0) best = 0;
     __syncthreads();
-    const uint32_t nflows = sc.counters[CTL_NFLOWS], nvalid = sc.counters[CTL_NVALID];
-    const uint32_t ncand = nflows + (sc.counters[CTL_MODE] ? hot_count(sc) : 0u);
+    uint32_t ncold;
+    const uint32_t ncand = hot_ncand(sc, ncold);
     unsigned long long mine = 0;
     for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < ncand; i += gridDim.x * kThreads) {
         uint32_t slot, c;
-        if (!hot_candidate(st, sc, i, nflows, nvalid, hot_min, slot, c)) continue;
+        if (!hot_candidate(st, sc, i, ncold, hot_min, slot, c)) continue;
         atomicAdd(&bins[31 - __clz(c)], 1u);
         mine = max(mine, ((unsigned long long)c << 32) | slot);
     }
@@ -1803,16 +2132,17 @@ __global__ __launch_bounds__(kThreads) void k_hot_pick(ClusterState st, BatchScr
             t = 1u << b;
         }
         thr = max(t, max(hot_min, 1u));
+        sc.hot_ctl[7] = thr;  // next batch's candidate floor is half of it
         const unsigned long long best = *reinterpret_cast<const unsigned long long *>(sc.hot_ctl + 4);
         wbest = best ? (uint32_t)st.param[(uint32_t)best].W : 0u;
     }
     __syncthreads();
     if (!wbest) return;
-    const uint32_t nflows = sc.counters[CTL_NFLOWS], nvalid = sc.counters[CTL_NVALID];
-    const uint32_t ncand = nflows + (sc.counters[CTL_MODE] ? hot_count(sc) : 0u);
+    uint32_t ncold;
+    const uint32_t ncand = hot_ncand(sc, ncold);
     for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < ncand; i += gridDim.x * kThreads) {
         uint32_t slot, c;
-        if (!hot_candidate(st, sc, i, nflows, nvalid, thr, slot, c)) continue;
+        if (!hot_candidate(st, sc, i, ncold, thr, slot, c)) continue;
         if ((uint32_t)st.param[slot].W != wbest) continue;
         const uint32_t hid = atomicAdd(&sc.hot_ctl[1], 1u);
         if (hid < (uint32_t)kHot) {
@@ -1838,6 +2168,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_fin(ClusterState st, BatchScra
         sc.hot_ctl[1] = 0;
         sc.hot_ctl[4] = 0;
         sc.hot_ctl[5] = 0;
+        sc.hot_ctl[6] = 0;  // the next batch's candidates
     }
     if (threadIdx.x < 32) sc.hot_ctl[8 + threadIdx.x] = 0;
 }
@@ -2490,6 +2821,12 @@ static size_t max_hist_entries(size_t cap, uint32_t nslots_cap) {
     return m;
 }
 
+// A/B knob for profiling only (results are wrong when set): 1 skips k_cold_fused's flows, 2 its results
+static int fz_debug() {
+    static const int v = getenv("SGA_FZ_DEBUG") ? atoi(getenv("SGA_FZ_DEBUG")) : 0;
+    return v;
+}
+
 static size_t hot_rows(size_t cap) { return (cap + kHotSeg - 1) / kHotSeg; }
 static size_t hot_groups(size_t cap) { return (hot_rows(cap) + kHotGroupRows - 1) / kHotGroupRows; }
 
@@ -2524,6 +2861,7 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += 3 * align_up(kHot * 4);                                                   // plo, phi, hot_tot
     b += align_up(256 * sizeof(WConst));
     b += align_up(segs_alloc * 2 * 4);                                             // seg_stat
+    b += align_up((size_t)kHotCand * 2 * 4);                                       // hot_cand
     return b;
 }
 
@@ -2581,6 +2919,7 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.hot_tot = (uint32_t *)take(kHot * 4);
     sc.wconst = (WConst *)take(256 * sizeof(WConst));
     sc.seg_stat = (uint32_t *)take(segs_alloc * 2 * 4);
+    sc.hot_cand = (uint32_t *)take((size_t)kHotCand * 2 * 4);
     sc.cap = cap;
 }
 
@@ -2600,7 +2939,6 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     const uint32_t invalid_key = st.nslots;
     int bits = 1;
     while (((uint64_t)1 << bits) < (uint64_t)st.nslots + kHot + 2) ++bits;  // hot keys nslots + 1 + id
-    const uint32_t ntiles = (n + kTileElems - 1) / kTileElems;
     const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
     const uint32_t nwg = (nseg + kH1Waves - 1) / kH1Waves;
     const uint32_t ngroups = (nseg + kHotGroupRows - 1) / kHotGroupRows;
@@ -2623,22 +2961,12 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
     hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el);
     hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, s, st, sc, ts_base);
-    hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
-                       sc.tile_valid, sc.counters + CTL_NCOLD);
-    hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
-                       ntiles, (Agg *)sc.tile_carry, sc.counters, sc.counters + CTL_NCOLD);
-    hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key, (const Agg *)sc.tile_carry,
-                       sc);
-    const uint64_t max_flows = n < st.nslots ? n : st.nslots;
-    uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows + kThreads - 1) / kThreads, 16384);
-    if (fb == 0) fb = 1;
-    hipLaunchKernelGGL(k_flows, dim3(fb), dim3(kThreads), 0, s, st, sc, ts_base, 0);
-    hipLaunchKernelGGL(k_flows_slow, dim3(std::min<uint32_t>(fb, 1024)), dim3(kThreads), 0, s, st, sc, acquire, prio,
-                       ts_off, ts_base, el, 0, out);
-    hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, invalid_key, out);
+    hipLaunchKernelGGL(k_cold_fused, dim3((n + kFzChunk - 1) / kFzChunk), dim3(kFzThreads), 0, s, st, sc, el, n,
+                       sc.counters + CTL_NCOLD, invalid_key, acquire, prio, ts_off, ts_base, 0,
+                       std::max<uint32_t>(sc.hot_min, 1), out, fz_debug());
     hipLaunchKernelGGL(k_hot_final, dim3(nwg), dim3(kThreads), 0, s, sc, n, out);
     hipLaunchKernelGGL(k_prio_results, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el, out);
-    const uint32_t sb = std::min<uint32_t>(fb, 128);  // few workgroups: their bins meet in global atomics
+    const uint32_t sb = 64;  // few workgroups: their bins meet in global atomics
     hipLaunchKernelGGL(k_hot_hist, dim3(sb), dim3(kThreads), 0, s, st, sc, std::max<uint32_t>(sc.hot_min, 1));
     hipLaunchKernelGGL(k_hot_clear, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc);
     hipLaunchKernelGGL(k_hot_pick, dim3(sb), dim3(kThreads), 0, s, st, sc, sc.hot_min);
@@ -2678,19 +3006,8 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     if (!simple) apply_limiters(st.param, sc, sc.el[0], n, invalid_key, ts_base, ts_off, out, lims, nlims, s);
     const int np = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, !limited && !nofuse);
     if (np != npass) throw HipError("radix pass count mismatch", __FILE__, __LINE__);
-    hipLaunchKernelGGL(k_runs_up, dim3(ntiles), dim3(kRunThreads), 0, s, el, n, invalid_key, (Agg *)sc.tile_agg,
-                       sc.tile_valid, nullptr);
-    hipLaunchKernelGGL(k_runs_tiles, dim3(1), dim3(kTileScanThreads), 0, s, (const Agg *)sc.tile_agg, sc.tile_valid,
-                       ntiles, (Agg *)sc.tile_carry, sc.counters, nullptr);
-    hipLaunchKernelGGL(k_runs_down, dim3(ntiles), dim3(kRunThreads), 0, s, el, invalid_key, (const Agg *)sc.tile_carry,
-                       sc);
-    const uint64_t max_flows = n < st.nslots ? n : st.nslots;
-    uint32_t fb = (uint32_t)std::min<uint64_t>((max_flows + kThreads - 1) / kThreads, 16384);
-    if (fb == 0) fb = 1;
-    hipLaunchKernelGGL(k_flows, dim3(fb), dim3(kThreads), 0, s, st, sc, ts_base, simple);
-    hipLaunchKernelGGL(k_flows_slow, dim3(std::min<uint32_t>(fb, 1024)), dim3(kThreads), 0, s, st, sc, acquire, prio,
-                       ts_off, ts_base, el, simple, out);
-    hipLaunchKernelGGL(k_results, dim3(ntiles), dim3(kRunThreads), 0, s, sc, el, invalid_key, out);
+    hipLaunchKernelGGL(k_cold_fused, dim3((n + kFzChunk - 1) / kFzChunk), dim3(kFzThreads), 0, s, st, sc, el, n,
+                       nullptr, invalid_key, acquire, prio, ts_off, ts_base, simple, 0xFFFFFFFFu, out, fz_debug());
 }
 
 // ---------------------------------------------------------------- cluster parameter flow (host)

@@ -115,6 +115,7 @@ constexpr int kSubSeg = 1024;       // cold compaction segment = sort input segm
 constexpr int kHotBuckets = 64;     // window buckets a batch may span on the hot path (6 bits)
 constexpr int kHotPreRows = 256;    // count snapshots at bucket boundaries inside a segment
 constexpr int kHotGroupRows = 16;   // count rows per group of the column scan
+constexpr int kHotCand = 1 << 16;   // next-hot-set candidates gathered per batch
 
 // Per-batch control words (BatchScratch::counters, zeroed per batch).
 enum : int {
@@ -172,7 +173,8 @@ struct BatchScratch {
     uint32_t *hot_slot;       // per hot id: rule slot
     uint32_t *hot_next;       // next batch's hot set while it is picked
     uint32_t *hot_ctl;        // [0] hot ids in use [1] picks [2] hot window length [3] next window length
-                              // [4..5] best (count << 32 | slot) [8..40) log2 count bins
+                              // [4..5] best (count << 32 | slot) [6] candidates [7] last pick threshold
+                              // [8..40) log2 count bins
     uint64_t *el_tile;        // classify output per 1024-request segment: cold elements + prioritized hot
                               // requests (hot key), arrival order
     uint32_t *tile_nc;        // per 1024-request segment: elements
@@ -188,6 +190,7 @@ struct BatchScratch {
     uint32_t *hot_tot;        // per hot id: requests in the batch
     WConst *wconst;           // [256] per window-length code
     uint32_t *seg_stat;       // per rank segment: prioritized hot requests, largest hot bucket delta
+    uint32_t *hot_cand;       // [kHotCand] (slot, count) of cold rules with >= hot_min requests (hot_ctl[6])
     int hot_enabled = 1;      // host policy (sga_set_hot_rules)
     uint32_t hot_min = 64;    // smallest per-batch request count that makes a rule hot
 };

@@ -15,4 +15,5 @@ timeout -k 10 300 python3 bench.py --no-cpu > $out/bench.json 2> $out/bench.err 
 python3 -c "import json;d=json.load(open('$out/bench.json'));r=d['roofline'];print('value %.3e ms/step %.3f gpu_ms %.3f frac %.3f path %s'%(d['value'],d['ms_per_step'],r['gpu_ms_per_step'],r['frac'],d.get('last_batch_path')))"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_$tag -o run --output-format csv -- python3 bench.py --no-cpu > $out/prof_bench.json 2> $out/prof.err || { tail -5 $out/prof.err; exit 1; }
 find /tmp/prof_$tag -name "*kernel_stats.csv" -exec cp {} $out/kernel_stats.csv \;
-python3 tools/kstats.py $out/kernel_stats.csv | grep -v "k_hist \|k_emit\|k_flags\|k_scan\|at::native\|rocclr\|k_init_slots\|k_conc_reset\|k_hot_reset" | head -40
+find /tmp/prof_$tag -name "*kernel_trace.csv" -exec cp {} $out/kernel_trace.csv \;
+python3 tools/ktrace.py $out/kernel_trace.csv --last 10 | grep -v "k_hist \|k_emit\|k_flags\|k_scan\|at::native\|rocclr\|k_init_slots\|k_conc_reset\|k_hot_reset" | head -40
