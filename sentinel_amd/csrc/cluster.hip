@@ -1398,317 +1398,326 @@ __global__ __launch_bounds__(kThreads) void k_hot_precheck(ClusterState st, Batc
     if (bad) atomicOr(&sc.counters[CTL_FLAGS], kFlagState);
 }
 
-// Pass A (k_hot_key): one wave per 1024-request compaction segment, every request independently:
-// validation (BAD_REQUEST / NO_RULE_EXISTS written directly), rule lookup, bucket deltas.  Cold
-// requests become sort elements (compacted in arrival order); every request gets a 4-byte key for
-// pass B: hot id | prioritized << 12 | hot bucket << 13 | hot << 19 (kNoKey bits when not hot).
-// Pass 1 of the batch is pass A again with no hot rules (launched always, returns at once unless
-// a fallback flag is up): every valid request becomes a cold element.
+// k_hot_key: one workgroup per kHotSeg-request rank segment, one wave per 1024-request compaction
+// segment (sub).  Every request independently: validation (BAD_REQUEST / NO_RULE_EXISTS written
+// directly), rule lookup, bucket deltas; cold requests become sort elements (compacted in arrival
+// order).  Hot requests are ranked among the sub's requests of their rule in arrival order as they
+// are classified (12 ballots match equal hot ids; wave-private LDS counters), the in-wave code
+// (hot id | rank << 12 | bucket << 25, bit 31 prioritized) is stored, and once every wave of the
+// segment is done the counters become per-wave prefixes (column scan over the 8 waves), the codes
+// are re-read (L2) and fixed up to in-segment ranks, prioritized hot requests join their sub's
+// elements (key nslots + 1 + hot id, rank in the bucket/acquire fields), and the segment's count
+// row is written.  At a hot bucket boundary inside the segment the wave's counts before it are
+// snapshot into a pre row (earlier waves' totals added after the scan); the boundary table records
+// where every bucket of the batch starts.
+// Pass 1 of the batch is this kernel again with no hot rules (launched always, returns at once
+// unless a fallback flag is up): every valid request becomes a cold element.
 // Software pipeline over chunks of kH1Chunk rounds with three register buffers used in rotation
 // (the loop is unrolled three times, so no buffer is copied: copying a register a load is still
 // writing waits for that load).  While chunk c is processed, the table lookups of chunk c + 1 and
 // the field loads of chunk c + 2 are in flight; loads and lookups are unconditional (clamped
 // indices, values masked when processed), so no branch stands around a load.
 constexpr uint32_t kKeyHot = 1u << 19;
+constexpr int kKeyWaves = kHotSeg / kSubSeg;  // 8: one rank segment per workgroup
+constexpr int kKeyThreads = kKeyWaves * 64;
+static_assert(kKeyWaves == kSubPerSeg, "one wave per compaction segment");
+struct KeyShared {
+    WConst wcs[256];
+    uint16_t cnt[kKeyWaves][kHot];  // per wave: hot requests so far per hot id
+    uint32_t s_np[kKeyWaves], s_bd[kKeyWaves];
+};
 template <int kPass, bool kDense>
-__global__ __launch_bounds__(kThreads) void k_hot_key(ClusterState st, BatchScratch sc,
-                                                      const int64_t *__restrict__ flow_id,
-                                                      const int32_t *__restrict__ acquire,
-                                                      const uint8_t *__restrict__ prio,
-                                                      const uint32_t *__restrict__ ts_off, int64_t ts_base, uint32_t n,
-                                                      uint64_t *__restrict__ out) {
-    __shared__ WConst wcs[256];
+__device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, const BatchScratch &sc,
+                                        const int64_t *__restrict__ flow_id, const int32_t *__restrict__ acquire,
+                                        const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off,
+                                        int64_t ts_base, uint32_t n, uint64_t *__restrict__ out) {
+    WConst *wcs = sh.wcs;
+    auto &cnt = sh.cnt;
+    uint32_t *s_np = sh.s_np, *s_bd = sh.s_bd;
     const uint32_t flags0 = sc.counters[CTL_FLAGS];
     if (kPass == 1 && !(flags0 & kFlagRerun)) return;
     const uint32_t nhot = (kPass == 0 && !(flags0 & kFlagState)) ? hot_count(sc) : 0u;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lt = lanemask_lt64(lane);
-    if (kDense) wcs[threadIdx.x] = sc.wconst[threadIdx.x];  // 256 window-length codes
-    __syncthreads();
-    const uint32_t sub = blockIdx.x * kH1Waves + wave;
-    const uint32_t ubase = sub * kSubSeg;
-    if (ubase >= n) {
-        if (lane == 0) sc.tile_nc[sub] = 0;
-        return;
+    if (kDense)
+        for (int k = threadIdx.x; k < 256; k += kKeyThreads) wcs[k] = sc.wconst[k];  // window-length codes
+    if (nhot) {
+        uint4 *cz = reinterpret_cast<uint4 *>(&cnt[0][0]);
+        for (int k = threadIdx.x; k < (int)(sizeof(cnt) / 16); k += kKeyThreads) cz[k] = make_uint4(0, 0, 0, 0);
     }
+    __syncthreads();
+    const uint32_t seg = blockIdx.x;
+    const uint32_t sub = seg * kKeyWaves + wave;
+    const uint32_t ubase = sub * kSubSeg;
+    const bool active = ubase < n;
+    uint16_t *c = cnt[wave];
     const uint32_t Wh = nhot ? sc.hot_ctl[2] : 1u;
     const uint32_t r0h = (uint32_t)(ts_base % (int64_t)Wh);
     const double invh = 1.0 / (double)Wh;
-    uint32_t ptso = ubase > 0 ? ts_off[ubase - 1] : 0u;  // time order across the segment start
-    const bool first_seg = ubase == 0;
-    uint32_t wflags = 0, nc = 0;
-    const bool use_prio = prio != nullptr;
+    uint32_t wflags = 0, nc = 0, np = 0, bdmax = 0;
     const uint32_t send = min(n, ubase + (uint32_t)kSubSeg);
-    const int nchunks = (int)((send - ubase + kH1Chunk * 64 - 1) / (kH1Chunk * 64));
-    struct Buf {
-        int64_t f[kH1Chunk];
-        int32_t a[kH1Chunk];
-        uint32_t t[kH1Chunk], p[kH1Chunk], d[kH1Chunk], hf[kH1Chunk];
-        HashEntry e[kH1Chunk];
-    };
-    Buf B0, B1, B2;
-    // a missing prio array reads the acquire bytes instead, masked off when processed
-    const uint8_t *pr_src = use_prio ? prio : reinterpret_cast<const uint8_t *>(acquire);
-    auto load = [&](int ch, Buf &B) {
+    if (active) {
+        uint32_t ptso = ubase > 0 ? ts_off[ubase - 1] : 0u;  // time order across the sub start
+        // hot bucket of the previous request (bucket boundaries)
+        uint32_t pbd = (nhot && ubase > 0) ? min(bucket_delta(ptso, Wh, r0h, invh), (uint32_t)kHotBuckets - 1) : 0u;
+        const bool use_prio = prio != nullptr;
+        const int nchunks = (int)((send - ubase + kH1Chunk * 64 - 1) / (kH1Chunk * 64));
+        struct Buf {
+            int64_t f[kH1Chunk];
+            int32_t a[kH1Chunk];
+            uint32_t t[kH1Chunk], p[kH1Chunk], d[kH1Chunk], hf[kH1Chunk], m[kH1Chunk];
+            HashEntry e[kH1Chunk];
+        };
+        Buf B0, B1, B2;
+        // a missing prio array reads the acquire bytes instead, masked off when processed
+        const uint8_t *pr_src = use_prio ? prio : reinterpret_cast<const uint8_t *>(acquire);
+        auto load = [&](int ch, Buf &B) {
 #pragma unroll
-        for (int u = 0; u < kH1Chunk; ++u) {
-            const uint32_t i = min(ubase + (uint32_t)(ch * kH1Chunk + u) * 64 + lane, n - 1);
-            B.f[u] = flow_id[i];
-            B.a[u] = acquire[i];
-            B.t[u] = ts_off[i];
-            B.p[u] = pr_src[i];
-        }
-    };
-    auto lookup = [&](Buf &B) {
-#pragma unroll
-        for (int u = 0; u < kH1Chunk; ++u) {
-            if (kDense) {
-                const uint64_t k = (uint64_t)(B.f[u] - 1);
-                const uint32_t kk = k < (uint64_t)st.dense_n ? (uint32_t)k : 0u;
-                const uint64_t ev = st.dense[kk];
-                B.d[u] = (uint32_t)ev;
-                B.hf[u] = (uint32_t)(ev >> 32) & 0xFFFFu;
-            } else {
-                B.d[u] = (uint32_t)hash_flow_id(B.f[u]) & st.hmask;
-                B.e[u] = st.htab[B.d[u]];
-                B.hf[u] = kColdId;
+            for (int u = 0; u < kH1Chunk; ++u) {
+                const uint32_t i = min(ubase + (uint32_t)(ch * kH1Chunk + u) * 64 + lane, n - 1);
+                B.f[u] = flow_id[i];
+                B.a[u] = acquire[i];
+                B.t[u] = ts_off[i];
+                B.p[u] = pr_src[i];
             }
-        }
-    };
-    auto process = [&](Buf &B, int ch) {
+        };
+        auto lookup = [&](Buf &B) {
 #pragma unroll
-        for (int u = 0; u < kH1Chunk; ++u) {
-            const uint32_t rbase = ubase + (uint32_t)(ch * kH1Chunk + u) * 64;
-            const uint32_t i = rbase + lane;
-            const bool valid = i < send;
-            uint32_t d = B.d[u], hfv = B.hf[u];
-            if (kDense) {
-                const bool in = (uint64_t)(B.f[u] - 1) < (uint64_t)st.dense_n;
-                if (!in) d = ~0u;
-                if (!in || !nhot) hfv = kColdId;
-            }
-            const uint32_t p = (use_prio && B.p[u]) ? 1u : 0u;
-            uint32_t kind = 0, hid = kColdId, slot = 0, bd6 = 0, a7 = 0;
-            if (valid) {
+            for (int u = 0; u < kH1Chunk; ++u) {
+                // what processing needs of flowId / acquireCount / prioritized, in one register
+                // (the 64-bit flowId and the acquire count are dead after this in the dense case)
                 const int64_t f = B.f[u];
                 const int32_t a = B.a[u];
-                int8_t status = TRS_OK;
-                uint32_t W = 0, r0 = 0;
-                double inv = 0;
-                if (f <= 0 || a <= 0) {
-                    status = TRS_BAD_REQUEST;
-                } else if (kDense) {
-                    if (d == ~0u) {
-                        status = TRS_NO_RULE_EXISTS;
-                    } else {
-                        slot = d & 0xFFFFFFu;
-                        const WConst wc = wcs[d >> 24];
-                        W = wc.W;
-                        r0 = wc.r0;
-                        inv = wc.inv;
-                    }
+                B.m[u] = ((use_prio && B.p[u]) ? 1u : 0u) | ((f <= 0 || a <= 0) ? 2u : 0u) |
+                         ((uint64_t)(f - 1) < (uint64_t)st.dense_n ? 4u : 0u) | (a == 1 ? 8u : 0u) |
+                         ((a >= 1 && a <= (int32_t)kAcqMax ? (uint32_t)a : 0u) << 8);
+                if (kDense) {
+                    const uint64_t k = (uint64_t)(B.f[u] - 1);
+                    const uint32_t kk = k < (uint64_t)st.dense_n ? (uint32_t)k : 0u;
+                    const uint64_t ev = st.dense[kk];
+                    B.d[u] = (uint32_t)ev;
+                    B.hf[u] = (uint32_t)(ev >> 32) & 0xFFFFu;
                 } else {
-                    HashEntry he = B.e[u];
-                    if (he.key != f && he.key != 0) {  // continue the linear probe
-                        uint32_t q = d;
-                        for (uint32_t probe = 1; probe <= st.hmask; ++probe) {
-                            q = (q + 1) & st.hmask;
-                            he = st.htab[q];
-                            if (he.key == f || he.key == 0) break;
-                        }
-                    }
-                    if (he.key != f) {
-                        status = TRS_NO_RULE_EXISTS;
-                    } else {
-                        slot = he.slot;
-                        W = he.W;
-                        r0 = (uint32_t)(ts_base % (int64_t)W);
-                        inv = 1.0 / (double)W;
-                    }
-                }
-                if (status != TRS_OK) {
-                    out[i] = pack_result(status, 0, 0);
-                } else {
-                    const uint32_t bd = bucket_delta(B.t[u], W, r0, inv);
-                    a7 = (a >= 1 && a <= (int32_t)kAcqMax) ? (uint32_t)a : 0u;
-                    bd6 = bd;
-                    if (bd >= kBdEsc) {
-                        bd6 = kBdEsc;
-                        a7 = 0;
-                    }
-                    kind = 1;
-                    if (nhot) {
-                        hid = kDense ? hfv : sc.hot_of[slot];
-                        if (hid < nhot) {
-                            kind = 2;
-                            if (a != 1) wflags |= kFlagMixed;
-                        }
-                    }
+                    B.d[u] = (uint32_t)hash_flow_id(B.f[u]) & st.hmask;
+                    B.e[u] = st.htab[B.d[u]];
+                    B.hf[u] = kColdId;
                 }
             }
-            if (nhot) {
-                // time order (every request with an index counts) and the key for pass B
-                const uint32_t pt = wave_shr1(B.t[u], ptso);
-                const bool hp = lane ? true : !first_seg || rbase != 0;
-                if (valid && hp && B.t[u] < pt) wflags |= kFlagUnsorted;
-                ptso = lane_u32(B.t[u], 63);
-                const uint32_t q = valid ? bucket_delta(B.t[u], Wh, r0h, invh) : 0u;
-                if (valid && q >= (uint32_t)kHotBuckets) wflags |= kFlagBucket;
-                const uint32_t bdh = min(q, (uint32_t)kHotBuckets - 1);
-                if (valid) sc.hcode[i] = (kind == 2 ? (kKeyHot | hid | (p << 12)) : 0u) | (bdh << 13);
+        };
+        auto process = [&](Buf &B, int ch) {
+#pragma unroll
+            for (int u = 0; u < kH1Chunk; ++u) {
+                const uint32_t rbase = ubase + (uint32_t)(ch * kH1Chunk + u) * 64;
+                const uint32_t i = rbase + lane;
+                const bool valid = i < send;
+                uint32_t d = B.d[u], hfv = B.hf[u];
+                const uint32_t m = B.m[u];
+                if (kDense) {
+                    const bool in = m & 4u;
+                    if (!in) d = ~0u;
+                    if (!in || !nhot) hfv = kColdId;
+                }
+                const uint32_t p = m & 1u;
+                uint32_t kind = 0, hid = kColdId, slot = 0, bd6 = 0, a7 = 0;
+                if (valid) {
+                    int8_t status = TRS_OK;
+                    uint32_t W = 0, r0 = 0;
+                    double inv = 0;
+                    if (m & 2u) {
+                        status = TRS_BAD_REQUEST;
+                    } else if (kDense) {
+                        if (d == ~0u) {
+                            status = TRS_NO_RULE_EXISTS;
+                        } else {
+                            slot = d & 0xFFFFFFu;
+                            const WConst wc = wcs[d >> 24];
+                            W = wc.W;
+                            r0 = wc.r0;
+                            inv = wc.inv;
+                        }
+                    } else {
+                        const int64_t f = B.f[u];
+                        HashEntry he = B.e[u];
+                        if (he.key != f && he.key != 0) {  // continue the linear probe
+                            uint32_t q = d;
+                            for (uint32_t probe = 1; probe <= st.hmask; ++probe) {
+                                q = (q + 1) & st.hmask;
+                                he = st.htab[q];
+                                if (he.key == f || he.key == 0) break;
+                            }
+                        }
+                        if (he.key != f) {
+                            status = TRS_NO_RULE_EXISTS;
+                        } else {
+                            slot = he.slot;
+                            W = he.W;
+                            r0 = (uint32_t)(ts_base % (int64_t)W);
+                            inv = 1.0 / (double)W;
+                        }
+                    }
+                    if (status != TRS_OK) {
+                        out[i] = pack_result(status, 0, 0);
+                    } else {
+                        const uint32_t bd = bucket_delta(B.t[u], W, r0, inv);
+                        a7 = (m >> 8) & kAcqMax;
+                        bd6 = bd;
+                        if (bd >= kBdEsc) {
+                            bd6 = kBdEsc;
+                            a7 = 0;
+                        }
+                        kind = 1;
+                        if (nhot) {
+                            hid = kDense ? hfv : sc.hot_of[slot];
+                            if (hid < nhot) {
+                                kind = 2;
+                                if (!(m & 8u)) wflags |= kFlagMixed;
+                            }
+                        }
+                    }
+                }
+                if (nhot) {
+                    // time order (every request with an index counts), hot bucket, in-wave rank
+                    const uint32_t pt = wave_shr1(B.t[u], ptso);
+                    const bool hp = lane ? true : i != 0;
+                    if (valid && hp && B.t[u] < pt) wflags |= kFlagUnsorted;
+                    ptso = lane_u32(B.t[u], 63);
+                    const uint32_t q = valid ? bucket_delta(B.t[u], Wh, r0h, invh) : 0u;
+                    if (valid && q >= (uint32_t)kHotBuckets) wflags |= kFlagBucket;
+                    const uint32_t bdh = min(q, (uint32_t)kHotBuckets - 1);
+                    if (valid) bdmax = max(bdmax, bdh);
+                    if (i == 0) sc.counters[CTL_BDLO] = bdh;
+                    const uint32_t pbk = wave_shr1(bdh, pbd);
+                    if (valid && hp && bdh > pbk)  // the first request of buckets pbk + 1 .. bdh
+                        for (uint32_t qq = pbk + 1; qq <= bdh; ++qq) sc.hbnd[qq] = i;
+                    pbd = lane_u32(bdh, 63);
+                    if (valid) sc.hcode[i] = (kind == 2 ? (kKeyHot | hid | (p << 12)) : 0u) | (bdh << 13);
+                }
+                // cold elements, compacted in arrival order
+                const bool emit = kind == 1;
+                const uint64_t em = __ballot(emit);
+                if (emit) sc.el_tile[(size_t)ubase + nc + (uint32_t)__popcll(em & lt)] = el_pack(slot, bd6, p, a7, i);
+                nc += (uint32_t)__popcll(em);
             }
-            // cold elements, compacted in arrival order
-            const bool emit = kind == 1;
-            const uint64_t em = __ballot(emit);
-            if (emit) sc.el_tile[(size_t)ubase + nc + (uint32_t)__popcll(em & lt)] = el_pack(slot, bd6, p, a7, i);
-            nc += (uint32_t)__popcll(em);
-        }
-    };
-    load(0, B0);
-    lookup(B0);
-    load(1, B1);
-    for (int ch = 0; ch < nchunks; ch += 3) {
-        lookup(B1);
-        load(ch + 2, B2);
-        process(B0, ch);
-        if (ch + 1 >= nchunks) break;
-        lookup(B2);
-        load(ch + 3, B0);
-        process(B1, ch + 1);
-        if (ch + 2 >= nchunks) break;
+        };
+        load(0, B0);
         lookup(B0);
-        load(ch + 4, B1);
-        process(B2, ch + 2);
+        load(1, B1);
+        for (int ch = 0; ch < nchunks; ch += 3) {
+            lookup(B1);
+            load(ch + 2, B2);
+            process(B0, ch);
+            if (ch + 1 >= nchunks) break;
+            lookup(B2);
+            load(ch + 3, B0);
+            process(B1, ch + 1);
+            if (ch + 2 >= nchunks) break;
+            lookup(B0);
+            load(ch + 4, B1);
+            process(B2, ch + 2);
+        }
+        if (nhot) {
+            // rank pass over the sub's keys (just written: L2; all 16 loads in flight together, the
+            // pipeline's registers are free), one round at a time: a scheduling barrier keeps the
+            // 12 ballots of different rounds from interleaving (they would not fit the scalar
+            // registers)
+            uint32_t key[kSubRounds];
+#pragma unroll
+            for (int r = 0; r < kSubRounds; ++r) key[r] = sc.hcode[min(ubase + (uint32_t)r * 64 + lane, n - 1)];
+#pragma unroll
+            for (int r = 0; r < kSubRounds; ++r) {
+                __builtin_amdgcn_sched_barrier(0);
+                const uint32_t i = ubase + (uint32_t)r * 64 + lane;
+                const uint32_t kv = key[r];
+                const bool hot = i < send && (kv & kKeyHot);
+                const uint32_t hid = kv & 0xFFFu, p = (kv >> 12) & 1u, bdh = (kv >> 13) & 63u;
+                const uint64_t hmask = __ballot(hot);
+                const uint32_t r_in = hmask ? rank_part(c, hmask, hid, lane, lt) : 0u;
+                np += (uint32_t)__popcll(__ballot(hot && p));
+                if (hot) sc.hcode[i] = (p << 31) | hid | (r_in << 12) | (bdh << 25);
+                else if (i < send) sc.hcode[i] = kNoCode;
+            }
+        }
     }
     if (wflags) atomicOr(&sc.counters[CTL_FLAGS], wflags);
-    if (lane == 0) sc.tile_nc[sub] = nc;  // totals: k_hot_mode (no same-address atomic per wave)
-}
-
-// Pass B (k_hot_rank): one wave per kHotSeg-request segment ranks every hot request among the
-// segment's requests of its rule in arrival order (12 ballots match equal hot ids; wave-private LDS
-// counters), rewrites its key as the code hot id | rank << 12 | bucket << 25 (kNoCode: not a
-// non-prioritized hot request), appends the prioritized hot requests to their compaction
-// segment's elements (key nslots + 1 + hot id, rank in the bucket/acquire fields), and writes the
-// segment's count row.  At a hot bucket boundary inside the segment the counts before it are
-// snapshot into a pre row; the boundary table records where every bucket of the batch starts.
-constexpr int kRankPf = 8;  // rounds of keys loaded ahead
-__global__ __launch_bounds__(kThreads) void k_hot_rank(ClusterState st, BatchScratch sc, uint32_t n) {
-    __shared__ uint16_t cnt[kH1Waves][kHot];
-    const uint32_t flags0 = sc.counters[CTL_FLAGS];
-    const uint32_t nhot = (flags0 & (kFlagRerun | kFlagState)) ? 0u : hot_count(sc);
-    if (!nhot) return;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t lt = lanemask_lt64(lane);
-    const uint32_t seg = blockIdx.x * kH1Waves + wave;
-    const uint32_t sbase = seg * kHotSeg;
-    if (sbase >= n) return;
-    uint16_t *c = cnt[wave];
-    for (uint32_t h = lane; h < (uint32_t)kHot; h += 64) c[h] = 0;
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t send = min(n, sbase + (uint32_t)kHotSeg);
-    const uint32_t nrounds = (send - sbase + 63) / 64;
-    uint32_t pbd = sbase > 0 ? (sc.hcode[sbase - 1] >> 13) & 63u : 0u;
-    const bool seg0 = sbase == 0;
-    uint32_t wflags = 0, nprio = 0, bdmax = 0, np_sub = 0, nc_sub = 0;
-    uint32_t key[kRankPf];
-#pragma unroll
-    for (int k = 0; k < kRankPf; ++k) key[k] = sc.hcode[min(sbase + (uint32_t)k * 64 + lane, n - 1)];
-    for (uint32_t r0 = 0; r0 < nrounds; r0 += kRankPf) {
-        uint32_t nk[kRankPf];
-#pragma unroll
-        for (int k = 0; k < kRankPf; ++k) nk[k] = sc.hcode[min(sbase + (r0 + kRankPf + k) * 64 + lane, n - 1)];
-#pragma unroll
-        for (int k = 0; k < kRankPf; ++k) {
-            const uint32_t r = r0 + k;
-            if (r >= nrounds) break;
-            const uint32_t rbase = sbase + r * 64;
-            const uint32_t i = rbase + lane;
-            const bool valid = i < send;
-            if ((rbase & (kSubSeg - 1)) == 0) {  // a compaction segment starts: its cold element count
-                nc_sub = sc.tile_nc[rbase / kSubSeg];
-                np_sub = 0;
-            }
-            const uint32_t kv = key[k];
-            const bool hot = valid && (kv & kKeyHot);
-            const uint32_t hid = kv & 0xFFFu;
-            const uint32_t p = (kv >> 12) & 1u;
-            const uint32_t bdh = (kv >> 13) & 63u;
-            const uint32_t pbk = wave_shr1(bdh, pbd);
-            const bool hp = lane ? true : !(seg0 && r == 0);
-            const bool bnd_here = valid && hp && bdh > pbk;
-            if (valid) bdmax = max(bdmax, bdh);
-            if (i == 0) sc.counters[CTL_BDLO] = bdh;
-            pbd = lane_u32(bdh, 63);
-            uint32_t r_in = 0;
-            const uint64_t hmask = __ballot(hot);
-            const uint64_t bm = __ballot(bnd_here);
-            if (bm == 0) {
-                if (hmask) r_in = rank_part(c, hmask, hid, lane, lt);
-            } else {
-                uint64_t rem = bm, done = 0;
-                while (rem) {
-                    const int b = __builtin_ctzll(rem);
-                    rem &= rem - 1;
-                    const uint64_t below = (1ull << b) - 1ull;
-                    const uint64_t part = hmask & below & ~done;
-                    if (part) {
-                        const uint32_t rr = rank_part(c, part, hid, lane, lt);
-                        if ((part >> lane) & 1ull) r_in = rr;
-                    }
-                    done |= below;
-                    const uint32_t bq = lane_u32(bdh, b);
-                    const uint32_t pq = lane_u32(pbk, b);
-                    uint32_t krow = 0;
-                    if (rbase + b != sbase) {  // inside the segment: snapshot the counts
-                        uint32_t kk = 0;
-                        if (lane == 0) kk = atomicAdd(&sc.counters[CTL_NPRE], 1u);
-                        kk = lane_u32(kk, 0);
-                        if (kk < (uint32_t)kHotPreRows) {
-                            krow = kk + 1;
-                            for (uint32_t h = lane; h < (uint32_t)kHot; h += 64) sc.hpre[(size_t)kk * kHot + h] = c[h];
-                        } else {
-                            wflags |= kFlagPre;
-                        }
-                    }
-                    if (lane == 0)
-                        for (uint32_t qq = pq + 1; qq <= bq && qq < (uint32_t)kHotBuckets; ++qq)
-                            sc.hbnd[qq] = (seg << 9) | krow;
-                }
-                const uint64_t part = hmask & ~done;
-                if (part) {
-                    const uint32_t rr = rank_part(c, part, hid, lane, lt);
-                    if ((part >> lane) & 1ull) r_in = rr;
-                }
-            }
-            if (valid) sc.hcode[i] = (hot && !p) ? (hid | (r_in << 12) | (bdh << 25)) : kNoCode;
-            // prioritized hot requests join their compaction segment's elements
-            const bool emit = hot && p;
-            const uint64_t em = __ballot(emit);
-            if (emit)
-                sc.el_tile[(size_t)(rbase & ~(uint32_t)(kSubSeg - 1)) + nc_sub + np_sub + (uint32_t)__popcll(em & lt)] =
-                    el_pack(st.nslots + 1 + hid, r_in >> 7, 1u, r_in & 127u, i);
-            np_sub += (uint32_t)__popcll(em);
-            if (((rbase + 64) & (kSubSeg - 1)) == 0 || rbase + 64 >= send) {
-                if (lane == 0 && np_sub) sc.tile_nc[rbase / kSubSeg] = nc_sub + np_sub;
-                nprio += np_sub;
-                np_sub = 0;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kRankPf; ++k) key[k] = nk[k];
-    }
-    {  // this segment's count row
-        uint32_t *row = reinterpret_cast<uint32_t *>(sc.hcnt + (size_t)seg * kHot);
-        const uint32_t *cw = reinterpret_cast<const uint32_t *>(c);
-        for (uint32_t k = lane; k < (nhot + 1) / 2; k += 64) row[k] = cw[k];
+    if (!nhot) {
+        if (lane == 0) sc.tile_nc[sub] = active ? nc : 0u;  // totals: k_hot_mode
+        return;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) bdmax = max(bdmax, (uint32_t)__shfl_xor((int)bdmax, o, 64));
-    if (wflags) atomicOr(&sc.counters[CTL_FLAGS], wflags);
-    if (lane == 0) {  // reduced by k_hot_mode: thousands of same-address atomics would serialize
-        sc.seg_stat[2 * seg] = nprio;
-        sc.seg_stat[2 * seg + 1] = bdmax;
+    if (lane == 0) {
+        s_np[wave] = np;
+        s_bd[wave] = bdmax;
     }
+    __syncthreads();
+    {  // per-wave counters -> exclusive prefixes over the waves (two hot ids per word: counts < 2^16)
+        uint32_t *cw = reinterpret_cast<uint32_t *>(&cnt[0][0]);
+        uint32_t *row = reinterpret_cast<uint32_t *>(sc.hcnt + (size_t)seg * kHot);
+        for (uint32_t k = threadIdx.x; k < (nhot + 1) / 2; k += kKeyThreads) {
+            uint32_t run = 0;
+#pragma unroll
+            for (int w = 0; w < kKeyWaves; ++w) {
+                const uint32_t v = cw[w * (kHot / 2) + k];
+                cw[w * (kHot / 2) + k] = run;
+                run += v;
+            }
+            row[k] = run;  // this segment's count row
+        }
+    }
+    if (threadIdx.x == 0) {  // reduced by k_hot_mode: thousands of same-address atomics would serialize
+        uint32_t a = 0, m = 0;
+        for (int w = 0; w < kKeyWaves; ++w) {
+            a += s_np[w];
+            m = max(m, s_bd[w]);
+        }
+        sc.seg_stat[2 * seg] = a;
+        sc.seg_stat[2 * seg + 1] = m;
+    }
+    __syncthreads();
+    if (!active) {
+        if (lane == 0) sc.tile_nc[sub] = 0;
+        return;
+    }
+    // codes: in-wave ranks -> in-segment ranks; prioritized hot requests join the sub's elements
+    uint32_t npos = nc;
+    uint32_t code[kSubRounds];
+#pragma unroll
+    for (int r = 0; r < kSubRounds; ++r) code[r] = sc.hcode[min(ubase + (uint32_t)r * 64 + lane, n - 1)];
+#pragma unroll
+    for (int r = 0; r < kSubRounds; ++r) {
+        const uint32_t i = ubase + (uint32_t)r * 64 + lane;
+        const uint32_t cd = code[r];
+        const bool hot = i < send && cd != kNoCode;
+        const uint32_t hid = cd & 0xFFFu;
+        const uint32_t r_seg = hot ? ((cd >> 12) & 0x1FFFu) + c[hid] : 0u;
+        const bool pr = hot && (cd >> 31);
+        if (hot && (wave || pr)) sc.hcode[i] = (cd & ~(0x1FFFu << 12)) | (r_seg << 12);
+        const uint64_t em = __ballot(pr);
+        if (pr)
+            sc.el_tile[(size_t)ubase + npos + (uint32_t)__popcll(em & lt)] =
+                el_pack(st.nslots + 1 + hid, r_seg >> 7, 1u, r_seg & 127u, i);
+        npos += (uint32_t)__popcll(em);
+    }
+    if (lane == 0) sc.tile_nc[sub] = npos;
+}
+
+// Dense flowId table (the production layout): 4 waves per SIMD, two workgroups per CU.
+template <int kPass>
+__global__ __launch_bounds__(kKeyThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_hot_key_dense(
+    ClusterState st, BatchScratch sc, const int64_t *__restrict__ flow_id, const int32_t *__restrict__ acquire,
+    const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off, int64_t ts_base, uint32_t n,
+    uint64_t *__restrict__ out) {
+    __shared__ KeyShared sh;
+    hot_key<kPass, true>(sh, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out);
+}
+// Hashed flowId table (sparse flowIds): the probe loop needs more registers.
+template <int kPass>
+__global__ __launch_bounds__(kKeyThreads) void k_hot_key_hash(
+    ClusterState st, BatchScratch sc, const int64_t *__restrict__ flow_id, const int32_t *__restrict__ acquire,
+    const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off, int64_t ts_base, uint32_t n,
+    uint64_t *__restrict__ out) {
+    __shared__ KeyShared sh;
+    hot_key<kPass, false>(sh, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out);
 }
 
 // The batch's path and element counts: sums over the compaction segments and the rank segments
@@ -1794,6 +1803,30 @@ __global__ __launch_bounds__(kThreads) void k_hscan_down(BatchScratch sc, uint32
     }
 }
 
+// Per hot bucket starting inside a rank segment: the segment's hot requests before its first
+// request, per hot id (the bucket's first rank is the segment's base plus these).
+__global__ __launch_bounds__(kThreads) void k_hot_pre(BatchScratch sc) {
+    __shared__ uint32_t cnt[kHot];
+    if (!sc.counters[CTL_MODE]) return;
+    const uint32_t b = blockIdx.x;
+    const uint32_t bd_lo = sc.counters[CTL_BDLO];
+    const uint32_t bd_hi = min(sc.counters[CTL_BDHI], (uint32_t)kHotBuckets - 1);
+    if (b <= bd_lo || b > bd_hi) return;
+    const uint32_t P = sc.hbnd[b];
+    const uint32_t s0 = P & ~(uint32_t)(kHotSeg - 1);
+    if (P == s0) return;
+    if (threadIdx.x == 0) atomicAdd(&sc.counters[CTL_NPRE], 1u);
+    for (uint32_t h = threadIdx.x; h < (uint32_t)kHot; h += kThreads) cnt[h] = 0;
+    __syncthreads();
+    for (uint32_t i = s0 + threadIdx.x; i < P; i += kThreads) {
+        const uint32_t cd = sc.hcode[i];
+        if (cd != kNoCode) atomicAdd(&cnt[cd & 0xFFFu], 1u);
+    }
+    __syncthreads();
+    const uint32_t nhot = hot_count(sc);
+    for (uint32_t h = threadIdx.x; h < nhot; h += kThreads) sc.hpre[(size_t)b * kHot + h] = (uint16_t)cnt[h];
+}
+
 // Rank of each prioritized hot request (sorted region: hot id major, arrival order within) and each
 // hot id's range in the region.
 __global__ __launch_bounds__(kThreads) void k_prio_rank(ClusterState st, BatchScratch sc,
@@ -1845,9 +1878,9 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
     const uint32_t tot = sc.hot_tot[h];
     uint32_t stb = 0;
     if ((uint32_t)lane < nb && lane > 0) {
-        const uint32_t e = sc.hbnd[bd_lo + lane];
-        const uint32_t seg = e >> 9, kr = e & 511u;
-        stb = sc.hbase[(size_t)seg * kHot + h] + (kr ? sc.hpre[(size_t)(kr - 1) * kHot + h] : 0u);
+        const uint32_t P = sc.hbnd[bd_lo + lane];  // the bucket's first request
+        stb = sc.hbase[(size_t)(P / kHotSeg) * kHot + h] +
+              ((P % kHotSeg) ? sc.hpre[(size_t)(bd_lo + lane) * kHot + h] : 0u);
     }
     uint32_t stn = wave_shl1(stb, 0u);
     if ((uint32_t)lane + 1 == nb) stn = tot;
@@ -1977,50 +2010,63 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
     }
 }
 
-// TokenResults of the non-prioritized hot requests, in input order.
+// TokenResults of the non-prioritized hot requests, in input order: one workgroup per rank segment
+// (its base row in LDS), each wave a quarter of it in chunks of kFinChunk rounds; the next chunk's
+// codes are in flight while a chunk's run records (two 16-byte loads each) are gathered.
 constexpr int kFinChunk = 8;
+constexpr int kFinWaves = kThreads / 64;
+constexpr uint32_t kFinSpan = kHotSeg / kFinWaves;  // requests per wave
+__device__ __forceinline__ int64_t i64_of(uint32_t lo, uint32_t hi) {
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double f64_of(uint32_t lo, uint32_t hi) {
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 __global__ __launch_bounds__(kThreads) void k_hot_final(BatchScratch sc, uint32_t n, uint64_t *__restrict__ out) {
-    __shared__ uint32_t base[kH1Waves][kHot];
+    __shared__ uint32_t base[kHot];
     if (!sc.counters[CTL_MODE]) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t seg = blockIdx.x * kH1Waves + wave;
+    const uint32_t seg = blockIdx.x;
     const uint32_t sbase = seg * kHotSeg;
-    if (sbase >= n) return;
     const uint32_t nhot = hot_count(sc);
-    uint32_t *bw = base[wave];
-    for (uint32_t h = lane; h < nhot; h += 64) bw[h] = sc.hbase[(size_t)seg * kHot + h];
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t send = min(n, sbase + (uint32_t)kHotSeg);
-    for (uint32_t r0 = sbase; r0 < send; r0 += kFinChunk * 64) {
+    for (uint32_t h = threadIdx.x; h < nhot; h += kThreads) base[h] = sc.hbase[(size_t)seg * kHot + h];
+    __syncthreads();
+    const uint32_t wbase = sbase + (uint32_t)wave * kFinSpan;
+    const uint32_t wend = min(n, wbase + kFinSpan);
+    if (wbase >= wend) return;
+    uint32_t cn[kFinChunk];
+#pragma unroll
+    for (int u = 0; u < kFinChunk; ++u) cn[u] = sc.hcode[min(wbase + (uint32_t)u * 64 + lane, n - 1)];
+    for (uint32_t r0 = wbase; r0 < wend; r0 += kFinChunk * 64) {
         uint32_t code[kFinChunk];
 #pragma unroll
         for (int u = 0; u < kFinChunk; ++u) {
             const uint32_t i = r0 + u * 64 + lane;
-            code[u] = i < send ? sc.hcode[i] : kNoCode;
+            code[u] = (i < wend && !(cn[u] >> 31)) ? cn[u] : kNoCode;  // prioritized: k_prio_results
         }
-        const HotRun *hrp[kFinChunk];
-        int64_t s0[kFinChunk];
-        double thr[kFinChunk], isec[kFinChunk];
-        uint32_t f[kFinChunk], st0[kFinChunk];
+#pragma unroll
+        for (int u = 0; u < kFinChunk; ++u)
+            cn[u] = sc.hcode[min(r0 + (uint32_t)(kFinChunk + u) * 64 + lane, n - 1)];
+        uint4 ra[kFinChunk], rb[kFinChunk];
 #pragma unroll
         for (int u = 0; u < kFinChunk; ++u) {
-            hrp[u] = sc.hrun + (size_t)(code[u] & 0xFFFu) * kHotBuckets + (code[u] >> 25);
-            if (code[u] != kNoCode) {
-                s0[u] = hrp[u]->s0;
-                thr[u] = hrp[u]->thr;
-                isec[u] = hrp[u]->isec;
-                f[u] = hrp[u]->f;
-                st0[u] = hrp[u]->start;
-            }
+            const uint32_t cd = code[u] == kNoCode ? 0u : code[u];  // clamped: the load is unconditional
+            const uint4 *hp = reinterpret_cast<const uint4 *>(sc.hrun + (size_t)(cd & 0xFFFu) * kHotBuckets + (cd >> 25));
+            ra[u] = hp[0];  // s0, thr
+            rb[u] = hp[1];  // isec, f, start
         }
 #pragma unroll
         for (int u = 0; u < kFinChunk; ++u) {
             if (code[u] == kNoCode) continue;
-            const uint32_t local = bw[code[u] & 0xFFFu] + ((code[u] >> 12) & 0x1FFFu) - st0[u];
+            const int64_t s0 = i64_of(ra[u].x, ra[u].y);
+            const double thr = f64_of(ra[u].z, ra[u].w);
+            const double isec = f64_of(rb[u].x, rb[u].y);
+            const uint32_t f = rb[u].z, st0 = rb[u].w;
+            const uint32_t local = base[code[u] & 0xFFFu] + ((code[u] >> 12) & 0x1FFFu) - st0;
             uint64_t res;
-            if (local < f[u]) {
-                const int64_t sum = s0[u] + (int64_t)local;
-                res = pack_result(TRS_OK, j_d2i(thr[u] - (double)sum / isec[u] - 1.0), 0);
+            if (local < f) {
+                const int64_t sum = s0 + (int64_t)local;
+                res = pack_result(TRS_OK, j_d2i(thr - (double)sum / isec - 1.0), 0);
             } else {
                 res = pack_result(TRS_BLOCKED, 0, 0);
             }
@@ -2855,7 +2901,7 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up(segs_alloc * kHotSeg * 4);                                       // hcode
     b += align_up(segs_alloc * kHot * 2) + align_up(segs_alloc * kHot * 4);        // hcnt, hbase
     b += align_up(hot_groups(cap) * kHot * 4);                                     // hgsum
-    b += align_up((size_t)kHotPreRows * kHot * 2) + align_up(kHotBuckets * 4);     // hpre, hbnd
+    b += align_up((size_t)kHotBuckets * kHot * 2) + align_up(kHotBuckets * 4);     // hpre, hbnd
     b += align_up((size_t)kHot * kHotBuckets * sizeof(HotRun));                   // hrun
     b += align_up(cap * 4);                                                        // prank
     b += 3 * align_up(kHot * 4);                                                   // plo, phi, hot_tot
@@ -2910,7 +2956,7 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.hcnt = (uint16_t *)take(segs_alloc * kHot * 2);
     sc.hbase = (uint32_t *)take(segs_alloc * kHot * 4);
     sc.hgsum = (uint32_t *)take(hot_groups(cap) * kHot * 4);
-    sc.hpre = (uint16_t *)take((size_t)kHotPreRows * kHot * 2);
+    sc.hpre = (uint16_t *)take((size_t)kHotBuckets * kHot * 2);
     sc.hbnd = (uint32_t *)take(kHotBuckets * 4);
     sc.hrun = (HotRun *)take((size_t)kHot * kHotBuckets * sizeof(HotRun));
     sc.prank = (uint32_t *)take(cap * 4);
@@ -2940,18 +2986,15 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     int bits = 1;
     while (((uint64_t)1 << bits) < (uint64_t)st.nslots + kHot + 2) ++bits;  // hot keys nslots + 1 + id
     const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
-    const uint32_t nwg = (nseg + kH1Waves - 1) / kH1Waves;
     const uint32_t ngroups = (nseg + kHotGroupRows - 1) / kHotGroupRows;
     SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, CTL_WORDS * 4, s));
     SGA_HIP_CHECK(hipMemsetAsync(sc.plo, 0, 2 * align_up(kHot * 4), s));  // plo and phi (adjacent)
     hipLaunchKernelGGL(k_hot_precheck, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc, ts_off, ts_base, n);
-    auto hka = st.dense_n ? k_hot_key<0, true> : k_hot_key<0, false>;
-    auto hkb = st.dense_n ? k_hot_key<1, true> : k_hot_key<1, false>;
-    const uint32_t nsub_wg = (n + kH1Waves * kSubSeg - 1) / (kH1Waves * kSubSeg);
-    hipLaunchKernelGGL(hka, dim3(nsub_wg), dim3(kThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out);
-    hipLaunchKernelGGL(k_hot_rank, dim3(nwg), dim3(kThreads), 0, s, st, sc, n);
-    hipLaunchKernelGGL(hkb, dim3(nsub_wg), dim3(kThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out);
-    hipLaunchKernelGGL(k_hot_mode, dim3(1), dim3(1024), 0, s, sc, nsub_wg * kH1Waves, nseg);
+    auto hka = st.dense_n ? k_hot_key_dense<0> : k_hot_key_hash<0>;
+    auto hkb = st.dense_n ? k_hot_key_dense<1> : k_hot_key_hash<1>;
+    hipLaunchKernelGGL(hka, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out);
+    hipLaunchKernelGGL(hkb, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out);
+    hipLaunchKernelGGL(k_hot_mode, dim3(1), dim3(1024), 0, s, sc, nseg * kKeyWaves, nseg);
     hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
     hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, s, sc, ngroups);
     hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
@@ -2960,11 +3003,12 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     const uint64_t *el = (np & 1) ? sc.el[0] : sc.el[1];
     const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
     hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el);
+    hipLaunchKernelGGL(k_hot_pre, dim3(kHotBuckets), dim3(kThreads), 0, s, sc);
     hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, s, st, sc, ts_base);
     hipLaunchKernelGGL(k_cold_fused, dim3((n + kFzChunk - 1) / kFzChunk), dim3(kFzThreads), 0, s, st, sc, el, n,
                        sc.counters + CTL_NCOLD, invalid_key, acquire, prio, ts_off, ts_base, 0,
                        std::max<uint32_t>(sc.hot_min, 1), out, fz_debug());
-    hipLaunchKernelGGL(k_hot_final, dim3(nwg), dim3(kThreads), 0, s, sc, n, out);
+    hipLaunchKernelGGL(k_hot_final, dim3(nseg), dim3(kThreads), 0, s, sc, n, out);
     hipLaunchKernelGGL(k_prio_results, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el, out);
     const uint32_t sb = 64;  // few workgroups: their bins meet in global atomics
     hipLaunchKernelGGL(k_hot_hist, dim3(sb), dim3(kThreads), 0, s, st, sc, std::max<uint32_t>(sc.hot_min, 1));

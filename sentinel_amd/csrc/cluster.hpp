@@ -113,7 +113,6 @@ constexpr uint16_t kColdId = 0xFFFF;
 constexpr int kHotSeg = 8192;       // requests per wave segment of k_hot_classify (one count row)
 constexpr int kSubSeg = 1024;       // cold compaction segment = sort input segment (4 per sort tile)
 constexpr int kHotBuckets = 64;     // window buckets a batch may span on the hot path (6 bits)
-constexpr int kHotPreRows = 256;    // count snapshots at bucket boundaries inside a segment
 constexpr int kHotGroupRows = 16;   // count rows per group of the column scan
 constexpr int kHotCand = 1 << 16;   // next-hot-set candidates gathered per batch
 
@@ -124,7 +123,7 @@ enum : int {
     CTL_NPRIO = 19,      // prioritized hot requests (pass 0)
     CTL_NSORT = 20,      // elements to sort
     CTL_NCOLD = 21,      // cold elements (the sorted prefix the run kernels read)
-    CTL_NPRE = 22,       // count snapshots used
+    CTL_NPRE = 22,       // hot buckets starting inside a rank segment (k_hot_pre rows)
     CTL_BDLO = 23,       // hot bucket delta of the batch's first request
     CTL_BDHI = 24,       // largest hot bucket delta
     CTL_MODE = 25,       // 1: the batch runs the hot path
@@ -135,8 +134,7 @@ enum : uint32_t {
     kFlagUnsorted = 1,   // timestamps decrease somewhere: no bucket order to rank by
     kFlagMixed = 2,      // a hot request with acquireCount != 1
     kFlagBucket = 4,     // the batch spans more than kHotBuckets hot buckets
-    kFlagPre = 8,        // more than kHotPreRows in-segment bucket boundaries
-    kFlagRerun = 15,     // any of the above: pass 1 re-classifies every request as cold
+    kFlagRerun = 7,      // any of the above: pass 1 re-classifies every request as cold
     kFlagState = 16      // a hot rule's window holds a bucket newer than the batch (precheck)
 };
 
@@ -178,12 +176,13 @@ struct BatchScratch {
     uint64_t *el_tile;        // classify output per 1024-request segment: cold elements + prioritized hot
                               // requests (hot key), arrival order
     uint32_t *tile_nc;        // per 1024-request segment: elements
-    uint32_t *hcode;          // per request: hot id | in-segment rank << 12 | bucket << 25 (~0: other)
+    uint32_t *hcode;          // per request: hot id | in-segment rank << 12 | bucket << 25 | prioritized << 31
+                              // (~0: not a hot request)
     uint16_t *hcnt;           // [segment][kHot] hot requests per hot id
     uint32_t *hbase;          // [segment][kHot] rank of the segment's first request of the hot id
     uint32_t *hgsum;          // [group][kHot] group sums, then exclusive prefixes over groups
-    uint16_t *hpre;           // [kHotPreRows][kHot] counts before an in-segment bucket boundary
-    uint32_t *hbnd;           // [kHotBuckets] first request of the bucket: segment << 9 | pre row + 1
+    uint16_t *hpre;           // [kHotBuckets][kHot] the segment's hot requests before the bucket's first
+    uint32_t *hbnd;           // [kHotBuckets] the bucket's first request
     HotRun *hrun;             // [kHot][kHotBuckets]
     uint32_t *prank;          // per prioritized hot request (sorted region order): its rank
     uint32_t *plo, *phi;      // per hot id: its range in the prioritized region
