@@ -233,7 +233,9 @@ int sga_route_shards(const int64_t *flow_id, size_t n, uint32_t n_shards, uint32
 /* Diagnostics of the last token batch (no reference counterpart): out[0] 1 when it ran the hot
  * path, [1] fallback flags, [2] sorted elements, [3] cold elements, [4] prioritized hot requests,
  * [5] hot rules for the next batch, [6..7] first / last hot bucket delta, [8] hot runs that
- * needed a replay (always 0), [9] in-segment bucket boundaries.  Synchronous. */
+ * needed a replay (always 0), [9] in-segment bucket boundaries, [10] 1 when the device passed the
+ * LDS lane-order probe the hot path's ranking relies on (else the hot path stays off).
+ * Synchronous. */
 int sga_cluster_batch_info(sga_engine *e, uint32_t *out, size_t n);
 
 /* ---------------------------------------------------------------------------

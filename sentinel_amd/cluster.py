@@ -98,10 +98,10 @@ class Engine:
 
     def batch_info(self) -> dict:
         """Path of the last token batch (sga_cluster_batch_info)."""
-        v = (C.c_uint32 * 10)()
-        _lib.check(_lib.load().sga_cluster_batch_info(self._h, v, 10), self._h, "sga_cluster_batch_info")
+        v = (C.c_uint32 * 11)()
+        _lib.check(_lib.load().sga_cluster_batch_info(self._h, v, 11), self._h, "sga_cluster_batch_info")
         keys = ("hot_mode", "flags", "n_sort", "n_cold", "n_prio", "n_hot_next", "bd_lo", "bd_hi", "hot_err",
-                "n_pre")
+                "n_pre", "lane_order_ok")
         return dict(zip(keys, [int(x) for x in v]))
 
     @property

@@ -22,6 +22,7 @@
 //   5 results   : every event derives its TokenResult from its run record.
 #include "cluster.hpp"
 
+#include <cstdio>
 #include <cstdlib>
 
 #include <algorithm>
@@ -488,19 +489,23 @@ __global__ __launch_bounds__(kRunThreads) void k_runs_down(const uint64_t *__res
 }
 
 // ---------------------------------------------------------------- exact per-request replay (device)
-// Window state of a rule lives in one contiguous record of 8 x S int64:
-//   [per bucket j: start, PASS] [per bucket j: WAITING, BLOCK, PASS_REQUEST, BLOCK_REQUEST,
-//   OCCUPIED_PASS, OCCUPIED_BLOCK]
-// so the window sums read one dense vector of 16-byte pairs and a run's update writes one pair
-// and one 48-byte group.
+// Window state of a rule lives in one contiguous record of 8 x S + 4 int64 (S + 1 64-byte units):
+//   [per bucket j: start, PASS] [occupy state: occupyCounter PASS, PASS_REQUEST, hasOccupied]
+//   [per bucket j: WAITING, BLOCK, PASS_REQUEST, BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK]
+// so the window sums read one dense vector of 16-byte pairs whose two cache lines also hold the
+// occupy state (a 64-byte aligned record puts pairs + occupy, 16 S + 32 bytes, in the same two
+// 128-byte lines for S = 10), and a run's update writes one pair and one 48-byte group.
+constexpr int kOccWords = 4;  // SlotOcc inside the record
+static_assert(sizeof(SlotOcc) <= kOccWords * 8, "occupy state fits its words");
 struct Rec {
     int64_t *r;
     int S;
     __device__ __forceinline__ int64_t &start(int j) const { return r[2 * j]; }
+    __device__ __forceinline__ SlotOcc &occ() const { return *reinterpret_cast<SlotOcc *>(r + 2 * S); }
     __device__ __forceinline__ int64_t &cnt(int ev, int j) const {
         if (ev == CEV_PASS) return r[2 * j + 1];
-        if (ev == CEV_WAITING) return r[2 * S + 6 * j];
-        return r[2 * S + 6 * j + ev];  // BLOCK..OCCUPIED_BLOCK = ordinals 1..5
+        if (ev == CEV_WAITING) return r[2 * S + kOccWords + 6 * j];
+        return r[2 * S + kOccWords + 6 * j + ev];  // BLOCK..OCCUPIED_BLOCK = ordinals 1..5
     }
 };
 
@@ -533,7 +538,7 @@ __device__ WinRef cur_window(const ClusterState &st, const SlotParam &P, uint32_
     if (ws > old) {  // resetWindowTo + transferOccupyToBucket
         R.start(j) = ws;
         bucket_zero(R, j);
-        SlotOcc &o = st.occ[s];
+        SlotOcc &o = R.occ();
         if (o.has_occ) {
             R.cnt(CEV_OCCUPIED_PASS, j) += o.occ_pass;
             R.cnt(CEV_PASS, j) += o.occ_pass;
@@ -594,7 +599,7 @@ __device__ uint64_t request_exact(const ClusterState &st, uint32_t s, int64_t t,
             // ClusterMetric.tryOccupyNext(PASS, a, thr)
             const double latest2 = get_avg(st, P, s, t, CEV_PASS);
             const int64_t head = head_pass(st, P, t);
-            SlotOcc &o = st.occ[s];
+            SlotOcc &o = rec_of(st, P).occ();
             if (latest2 + (double)((int64_t)a + o.occ_pass) - (double)head <= thr) {
                 o.occ_pass += a;
                 o.occ_preq += 1;
@@ -650,10 +655,11 @@ struct RunIn {
     uint32_t bd;  // bucket delta of the run (its bucket = ts_base / W + bd)
 };
 
-template <bool kPrio>
-__device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &sc, uint32_t s, const SlotParam &P,
-                                         const Rec &R, double thr, int64_t qbase, const RunIn &ri, uint32_t r) {
-    if (!kPrio && ri.cp_tot > 0) return false;  // prioritized runs go to k_flows_slow
+// prio_before(k): prioritized requests among the run's first k (asked only when some prioritized
+// request is past the passing prefix).
+template <class PrioBefore>
+__device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam &P, const Rec &R, double thr,
+                                         int64_t qbase, const RunIn &ri, PrioBefore prio_before, RunOut &ro) {
     // Cluster rules have intervalInMs = sampleCount x windowLengthInMs (checkClusterField), so every
     // validity test below (isWindowDeprecated, getValidHead) gives the same answer for any time in
     // the run's bucket: the bucket start stands in for the first request's time.
@@ -664,7 +670,16 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
     const int64_t qs = div_pos(q, P.S);
     const int cj = (int)(q - qs * P.S);
     const int jh = cj + 1 == P.S ? 0 : cj + 1;  // LeapArray.getValidHead index ((t0 + W) / W) % S
-    const int64_t old = R.start(cj);
+    // The record's loads are issued before any is used (one memory latency per run, not one per
+    // dependent step): the current bucket's (start, PASS) pair and its six other counters
+    // (WAITING, BLOCK, PASS_REQUEST, BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK), the occupy
+    // state (in the lines of the pairs), and below the (start, PASS) pairs of every bucket.
+    const int4 *v = reinterpret_cast<const int4 *>(R.r);
+    const int4 cur = v[cj];
+    const int4 *cv = reinterpret_cast<const int4 *>(R.r + 2 * P.S + kOccWords + 6 * cj);
+    const int4 c01 = cv[0], c23 = cv[1], c45 = cv[2];
+    const SlotOcc occ_ld = R.occ();
+    const int64_t old = i64_lo(cur);
     if (a <= 0 || (old != kAbsent && ws < old)) return false;
     if (ri.cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) return false;
     int64_t bp = 0, hstart = kAbsent, hpass = 0;
@@ -672,7 +687,6 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
         // (start, PASS) pairs: one 16-byte load per bucket.  Up to 16 buckets (sampleCount 10 is
         // the default) the loads are issued together before any is used: a loop that waits for
         // each bucket's load in turn pays S memory latencies per run.
-        const int4 *v = reinterpret_cast<const int4 *>(R.r);
         auto take = [&](int jj, const int4 &sp) {
             const int64_t w = i64_lo(sp), pv = i64_hi(sp);
             if (jj == jh) {
@@ -701,7 +715,7 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
 #pragma unroll
         for (int k = 0; k < CEV_N; ++k) c[k] = 0;
         if (old != kAbsent) {  // resetWindowTo + transferOccupyToBucket
-            o = st.occ[s];
+            o = occ_ld;
             occ_loaded = true;
             if (o.has_occ) {
                 c[CEV_OCCUPIED_PASS] += o.occ_pass;
@@ -714,8 +728,13 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
             }
         }
     } else {
-#pragma unroll
-        for (int k = 0; k < CEV_N; ++k) c[k] = R.cnt(k, cj);
+        c[CEV_PASS] = i64_hi(cur);
+        c[CEV_WAITING] = i64_lo(c01);
+        c[CEV_BLOCK] = i64_hi(c01);
+        c[CEV_PASS_REQUEST] = i64_lo(c23);
+        c[CEV_BLOCK_REQUEST] = i64_hi(c23);
+        c[CEV_OCCUPIED_PASS] = i64_lo(c45);
+        c[CEV_OCCUPIED_BLOCK] = i64_hi(c45);
     }
     int64_t head;  // getValidHead after the rotation (the head is the current bucket when S == 1)
     if (jh == cj) head = c[CEV_PASS];
@@ -726,15 +745,7 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
     // prioritized requests among the first f: the run's prioritized positions are
     // plist[p0 .. p0 + cp_tot) (ascending)
     uint32_t cpf = ri.cp_tot;
-    if (f < n && ri.cp_tot > 0) {
-        uint32_t lo = 0, hi = ri.cp_tot;
-        while (lo < hi) {
-            const uint32_t m = (lo + hi) >> 1;
-            if (sc.plist[ri.p0 + m] < ri.j0 + f) lo = m + 1;
-            else hi = m;
-        }
-        cpf = lo;
-    }
+    if (f < n && ri.cp_tot > 0) cpf = prio_before(f);
     const uint32_t np_after = ri.cp_tot - cpf;
     uint32_t cw = 0;
     if (np_after > 0) {
@@ -745,7 +756,7 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
             const int64_t w = R.start(jj);
             if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) w0 += R.cnt(CEV_WAITING, jj);
         }
-        if (!occ_loaded) o = st.occ[s];
+        if (!occ_loaded) o = occ_ld;
         const double latest = (double)(s0 + (int64_t)f * a) / P.isec;
         const double lim = st.max_occupy_ratio * thr;
         const int64_t occ0 = o.occ_pass;
@@ -777,8 +788,7 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
     if (rot) R.start(cj) = ws;
 #pragma unroll
     for (int k = 0; k < CEV_N; ++k) R.cnt(k, cj) = c[k];
-    if (occ_dirty) st.occ[s] = o;
-    RunOut ro;
+    if (occ_dirty) R.occ() = o;
     ro.s0 = s0;
     ro.thr = thr;
     ro.isec = P.isec;
@@ -787,87 +797,9 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, BatchScratch &s
     ro.cw = cw;
     ro.wait = (uint16_t)(1000 / P.S);
     ro.mode = RUN_FAST;
-    sc.run_out[r] = ro;
     return true;
 }
 
-__device__ __forceinline__ RunIn run_in(const BatchScratch &sc, uint32_t r, uint32_t nruns, uint32_t nvalid) {
-    RunIn ri;
-    ri.j0 = sc.run_start[r];
-    ri.n = (r + 1 < nruns ? sc.run_start[r + 1] : nvalid) - ri.j0;
-    ri.cp_tot = sc.run_cp[r];
-    ri.p0 = sc.run_p0[r];
-    ri.a = sc.run_acq[r];
-    ri.bd = sc.run_bd[r];
-    return ri;
-}
-
-// One rule per lane walks the rule's runs in time order, closed form only.  At the first run
-// that needs the per-request replay the rest of the rule is deferred to k_flows_slow (rare), so
-// this kernel stays small and keeps many rules in flight.
-__global__ __launch_bounds__(kThreads) void k_flows(ClusterState st, BatchScratch sc, int64_t ts_base, int simple) {
-    const uint32_t nflows = sc.counters[2];
-    const uint32_t nruns = sc.counters[1];
-    const uint32_t nvalid = sc.counters[0];
-    for (uint32_t fl = blockIdx.x * kThreads + threadIdx.x; fl < nflows; fl += gridDim.x * kThreads) {
-        const uint32_t r0 = sc.flow_first_run[fl];
-        const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
-        const uint32_t s = sc.run_slot[r0];
-        const SlotParam P = st.param[s];
-        const Rec R = rec_of(st, P);
-        const double thr = simple ? P.thr_simple : P.thr;
-        const int64_t qbase = div_pos(ts_base, P.W);
-        for (uint32_t r = r0; r < r1; ++r) {
-            const RunIn ri = run_in(sc, r, nruns, nvalid);
-            if (!run_fast<true>(st, sc, s, P, R, thr, qbase, ri, r)) {
-                const uint32_t k = atomicAdd(&sc.counters[6], 1u);
-                sc.deferred[2 * k] = fl;
-                sc.deferred[2 * k + 1] = r;
-                break;
-            }
-        }
-    }
-}
-
-// Deferred rules: the deferred run is replayed request by request (request_exact) from the
-// original arrays, later runs in closed form when eligible.
-__global__ __launch_bounds__(kThreads) void k_flows_slow(ClusterState st, BatchScratch sc,
-                                                         const int32_t *__restrict__ acquire,
-                                                         const uint8_t *__restrict__ prio,
-                                                         const uint32_t *__restrict__ ts_off, int64_t ts_base,
-                                                         const uint64_t *__restrict__ el, int simple,
-                                                         uint64_t *__restrict__ out) {
-    const uint32_t ndef = sc.counters[6];
-    const uint32_t nflows = sc.counters[2];
-    const uint32_t nruns = sc.counters[1];
-    const uint32_t nvalid = sc.counters[0];
-    for (uint32_t d = blockIdx.x * kThreads + threadIdx.x; d < ndef; d += gridDim.x * kThreads) {
-        const uint32_t fl = sc.deferred[2 * d], rd = sc.deferred[2 * d + 1];
-        const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
-        const uint32_t s = sc.run_slot[rd];
-        const SlotParam P = st.param[s];
-        const Rec R = rec_of(st, P);
-        const double thr = simple ? P.thr_simple : P.thr;
-        const int64_t qbase = div_pos(ts_base, P.W);
-        for (uint32_t r = rd; r < r1; ++r) {
-            const RunIn ri = run_in(sc, r, nruns, nvalid);
-            if (r > rd && run_fast<true>(st, sc, s, P, R, thr, qbase, ri, r)) continue;
-            for (uint32_t j = ri.j0; j < ri.j0 + ri.n; ++j) {
-                const uint32_t i = el_idx(el[j]);
-                const int64_t t = ts_base + (int64_t)ts_off[i];
-                const bool p = !simple && prio && prio[i];
-                out[i] = request_exact(st, s, t, acquire[i], p, simple);
-            }
-            RunOut ro;
-            ro.mode = RUN_DONE;
-            sc.run_out[r] = ro;
-        }
-    }
-}
-
-// ---------------------------------------------------------------- results
-// Same tile geometry as k_runs_down; each wave starts from the carry k_runs_down stored and
-// re-derives every request's run id and prioritized rank, then writes its TokenResult.
 __global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const uint64_t *__restrict__ el,
                                                          uint32_t invalid_key, uint64_t *__restrict__ out) {
     const uint32_t nvalid = sc.counters[0];
@@ -961,17 +893,29 @@ __global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const 
 // rule that runs past the chunk end is followed to its end (region [h0, E)).
 //   1 runs    : a blocked segmented scan over the region finds run heads (slot, bucket) and rule
 //               heads; each run's length, prioritized count, first prioritized index and common
-//               acquire count are written at its head position (run arrays indexed by position),
+//               acquire count are written at its head position (run records indexed by position),
 //               prioritized positions are compacted into plist[h0 ..), rule heads into LDS.
 //   2 flows   : one lane per owned rule walks its runs in time order -- the closed form
 //               (run_fast) or the exact per-request replay (request_exact) -- and the rule's
 //               request count feeds the next batch's hot-set candidates.
 //   3 results : the same scan again; every request reads its run's record and writes its
 //               TokenResult (runs replayed in step 2 wrote theirs already).
-// Run records live in global scratch but are written and read by the same workgroup, so they
-// stay in the XCD's L2.  Elements with a slot >= nkey (invalid requests, prioritized hot
+// Run records live in LDS (runs starting within a chunk's length of h0; the later runs of a rule
+// that continues past the chunk use global run arrays), run decisions in global scratch written
+// and read by the same workgroup.  Elements with a slot >= nkey (invalid requests, prioritized hot
 // requests) end the data.
 constexpr int kFzThreads = 256, kFzPer = 8, kFzChunk = kFzThreads * kFzPer;  // 2048
+
+// Profiling only (SGA_FZ_DEBUG bit 16): per-phase cycles of k_cold_fused summed over workgroups.
+__device__ unsigned long long g_fz_phase[8];
+__device__ __forceinline__ void fz_mark(int dbg, int ph, unsigned long long &t) {
+    if (!(dbg & 16)) return;
+    __syncthreads();
+    const unsigned long long now = wall_clock64();
+    if (threadIdx.x == 0 && ph > 0) atomicAdd(&g_fz_phase[ph - 1], now - t);
+    if (threadIdx.x == 0 && ph == 3) atomicAdd(&g_fz_phase[7], 1ull);
+    t = now;
+}
 
 struct FAgg {
     uint32_t hpos;  // (run head position + 1) of the last run head so far (0: none)
@@ -1029,7 +973,11 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused(ClusterState st, Batc
                                                            const uint32_t *__restrict__ ts_off, int64_t ts_base,
                                                            int simple, uint32_t hot_min, uint64_t *__restrict__ out,
                                                            int dbg) {
-    __shared__ uint32_t fheads[kFzChunk + 1];
+    __shared__ uint32_t fheads[kFzChunk + 1], fslot[kFzChunk + 1];  // owned rules: first position, slot
+    // run records of the runs that start in [h0, h0 + kFzChunk) (every run but the later runs of
+    // a rule that continues past the chunk, which use the global run arrays): length,
+    // prioritized count, first prioritized index, acquire count | bucket delta << 8
+    __shared__ uint32_t rl_n[kFzChunk], rl_cp[kFzChunk], rl_p0[kFzChunk], rl_ab[kFzChunk];
     __shared__ FAgg wtot[kFzThreads / 64];
     __shared__ uint32_t s_h0, s_E, s_wcnt[kFzThreads / 64];
     __shared__ uint32_t s_ncand, s_cbase, s_cand[2 * kFzThreads];
@@ -1091,6 +1039,8 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused(ClusterState st, Batc
     }
     __syncthreads();
     const uint32_t E = s_E;
+    unsigned long long fzt = 0;
+    fz_mark(dbg, 0, fzt);
     // ---- 1 runs (blocks of kFzChunk elements over [h0, E))
     FAgg carry = fagg_id();
     uint32_t nf_carry = 0;
@@ -1141,17 +1091,29 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused(ClusterState st, Batc
             const FAgg v{hd[k] ? p + 1 : 0u, pr, 0u, hd[k] ? 1u : 0u, el_acq(x[k]), el_acq(x[k])};
             const uint32_t np_before = run.np;
             run = fagg_combine(run, v);
-            if (fh[k]) fheads[fbase++] = p;
+            if (fh[k]) {
+                fslot[fbase] = el_slot(x[k]);
+                fheads[fbase++] = p;
+            }
             if (pr) sc.plist[h0 + np_before] = p;
             // run end: this is the last element of its run
             const bool last = p + 1 >= E || (k + 1 < kFzPer ? hd[k + 1] : (p + 1 < E && el_runkey(el[p + 1]) != el_runkey(x[k])));
             if (last) {
                 const uint32_t head = run.hpos - 1;
-                sc.run_start[head] = p + 1 - head;  // run length (run arrays are indexed by head position)
-                sc.run_cp[head] = run.np - run.hp;
-                sc.run_p0[head] = h0 + run.hp;
-                sc.run_acq[head] = run.mn == run.mx ? run.mn : 0;  // 0: mixed or escaped -> replay
-                sc.run_bd[head] = (uint8_t)((x[k] >> kBdShift) & kBdEsc);
+                const int32_t acq = run.mn == run.mx ? run.mn : 0;  // 0: mixed or escaped -> replay
+                const uint32_t bd = (uint32_t)((x[k] >> kBdShift) & kBdEsc);
+                if (head - h0 < (uint32_t)kFzChunk) {
+                    rl_n[head - h0] = p + 1 - head;
+                    rl_cp[head - h0] = run.np - run.hp;
+                    rl_p0[head - h0] = h0 + run.hp;
+                    rl_ab[head - h0] = (uint32_t)acq | (bd << 8);
+                } else {  // global run arrays, indexed by head position
+                    sc.run_start[head] = p + 1 - head;
+                    sc.run_cp[head] = run.np - run.hp;
+                    sc.run_p0[head] = h0 + run.hp;
+                    sc.run_acq[head] = acq;
+                    sc.run_bd[head] = (uint8_t)bd;
+                }
             }
         }
         carry = fagg_combine(carry, tot);
@@ -1164,11 +1126,12 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused(ClusterState st, Batc
     // next-hot-set candidates: counts of at least the floor (half the last pick threshold) are
     // gathered in LDS and published with one global reservation per workgroup
     const uint32_t cand_floor = max(hot_min, sc.hot_ctl[7] >> 1);
+    fz_mark(dbg, 1, fzt);
     // ---- 2 flows: one lane per owned rule
     for (uint32_t f = threadIdx.x; f < ((dbg & 1) ? 0u : nf); f += kFzThreads) {
         const uint32_t r0 = fheads[f];
         const uint32_t r1 = f + 1 < nf ? fheads[f + 1] : E;
-        const uint32_t s = el_slot(el[r0]);
+        const uint32_t s = fslot[f];
         if (r1 - r0 >= cand_floor) {  // next batch's hot-set candidate
             const uint32_t k = atomicAdd(&s_ncand, 1u);
             if (k < (uint32_t)kFzThreads) {
@@ -1183,12 +1146,34 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused(ClusterState st, Batc
         for (uint32_t r = r0; r < r1;) {
             RunIn ri;
             ri.j0 = r;
-            ri.n = sc.run_start[r];
-            ri.cp_tot = sc.run_cp[r];
-            ri.p0 = sc.run_p0[r];
-            ri.a = sc.run_acq[r];
-            ri.bd = sc.run_bd[r];
-            if (run_fast<true>(st, sc, s, P, R, thr, qbase, ri, r)) {
+            if (r - h0 < (uint32_t)kFzChunk) {
+                ri.n = rl_n[r - h0];
+                ri.cp_tot = rl_cp[r - h0];
+                ri.p0 = rl_p0[r - h0];
+                const uint32_t ab = rl_ab[r - h0];
+                ri.a = (int32_t)(ab & 0xFFu);
+                ri.bd = ab >> 8;
+            } else {
+                ri.n = sc.run_start[r];
+                ri.cp_tot = sc.run_cp[r];
+                ri.p0 = sc.run_p0[r];
+                ri.a = sc.run_acq[r];
+                ri.bd = sc.run_bd[r];
+            }
+            // prioritized requests among the run's first k: plist[p0 .. p0 + cp_tot) holds the
+            // run's prioritized positions (ascending)
+            auto prio_before = [&](uint32_t k) -> uint32_t {
+                uint32_t lo = 0, hi = ri.cp_tot;
+                while (lo < hi) {
+                    const uint32_t m = (lo + hi) >> 1;
+                    if (sc.plist[ri.p0 + m] < ri.j0 + k) lo = m + 1;
+                    else hi = m;
+                }
+                return lo;
+            };
+            RunOut ro;
+            if (run_fast(st, P, R, thr, qbase, ri, prio_before, ro)) {
+                sc.run_out[r] = ro;
                 r += ri.n;
                 continue;
             }
@@ -1198,13 +1183,13 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused(ClusterState st, Batc
                 const bool p = !simple && prio && prio[i];
                 out[i] = request_exact(st, s, t, acquire[i], p, simple);
             }
-            RunOut ro;
             ro.mode = RUN_DONE;
             sc.run_out[r] = ro;
             r += ri.n;
         }
     }
     __syncthreads();  // run_out of every owned run
+    fz_mark(dbg, 2, fzt);
     {
         const uint32_t nc = min(s_ncand, (uint32_t)kFzThreads);
         if (threadIdx.x == 0) s_cbase = nc ? atomicAdd(&sc.hot_ctl[6], nc) : 0u;
@@ -1272,6 +1257,7 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused(ClusterState st, Batc
         carry = fagg_combine(carry, tot);
         __syncthreads();
     }
+    fz_mark(dbg, 3, fzt);
 }
 
 // ---------------------------------------------------------------- hot path
@@ -1324,27 +1310,14 @@ __device__ __forceinline__ int64_t lane_i64(int64_t v, int l) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-__device__ __forceinline__ uint64_t match_hot_id(uint64_t mask, uint32_t key) {
-#pragma unroll
-    for (int b = 0; b < 12; ++b) {
-        const bool bit = (key >> b) & 1u;
-        const uint64_t bb = __ballot(bit);
-        mask &= bit ? bb : ~bb;
-    }
-    return mask;
-}
-
-// In-order rank of the lanes of `part` among the wave's requests of their hot id so far.
-__device__ __forceinline__ uint32_t rank_part(uint16_t *c, uint64_t part, uint32_t hid, int lane, uint64_t lt) {
-    const bool in = (part >> lane) & 1ull;
-    const uint64_t peers = match_hot_id(part, hid);
-    uint32_t before = 0;
-    if (in) before = c[hid];
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t my = (uint32_t)__popcll(peers & lt);
-    if (in && my == 0) c[hid] = (uint16_t)(before + (uint32_t)__popcll(peers));
-    __builtin_amdgcn_wave_barrier();
-    return before + my;
+// In-order rank of a wave's hot lanes among its requests of their hot id so far: one LDS atomic
+// add with return per round on per-wave counters packed two hot ids per word.  The lanes of one
+// wave instruction that add to the same LDS word receive the old values in lane order on gfx950
+// (probed once per process by lds_lane_order_ok(); the hot path stays off if it ever fails), so
+// the returned count is the number of earlier requests of that hot id: arrival order.
+__device__ __forceinline__ uint32_t rank_hot(uint32_t *cw, uint32_t hid) {
+    const uint32_t sh = (hid & 1u) << 4;
+    return (atomicAdd(&cw[hid >> 1], 1u << sh) >> sh) & 0xFFFFu;
 }
 
 __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
@@ -1430,7 +1403,7 @@ template <int kPass, bool kDense>
 __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, const BatchScratch &sc,
                                         const int64_t *__restrict__ flow_id, const int32_t *__restrict__ acquire,
                                         const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off,
-                                        int64_t ts_base, uint32_t n, uint64_t *__restrict__ out) {
+                                        int64_t ts_base, uint32_t n, uint64_t *__restrict__ out, int dbg) {
     WConst *wcs = sh.wcs;
     auto &cnt = sh.cnt;
     uint32_t *s_np = sh.s_np, *s_bd = sh.s_bd;
@@ -1519,6 +1492,9 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                 }
                 const uint32_t p = m & 1u;
                 uint32_t kind = 0, hid = kColdId, slot = 0, bd6 = 0, a7 = 0;
+                // hot bucket (window length of the hot rules) of every request: time order of the
+                // buckets; the request's own bucket when its rule has that window length too
+                const uint32_t q = (nhot && valid) ? bucket_delta(B.t[u], Wh, r0h, invh) : 0u;
                 if (valid) {
                     int8_t status = TRS_OK;
                     uint32_t W = 0, r0 = 0;
@@ -1558,7 +1534,8 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                     if (status != TRS_OK) {
                         out[i] = pack_result(status, 0, 0);
                     } else {
-                        const uint32_t bd = bucket_delta(B.t[u], W, r0, inv);
+                        uint32_t bd = q;
+                        if (!nhot || W != Wh) bd = bucket_delta(B.t[u], W, r0, inv);
                         a7 = (m >> 8) & kAcqMax;
                         bd6 = bd;
                         if (bd >= kBdEsc) {
@@ -1581,7 +1558,6 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                     const bool hp = lane ? true : i != 0;
                     if (valid && hp && B.t[u] < pt) wflags |= kFlagUnsorted;
                     ptso = lane_u32(B.t[u], 63);
-                    const uint32_t q = valid ? bucket_delta(B.t[u], Wh, r0h, invh) : 0u;
                     if (valid && q >= (uint32_t)kHotBuckets) wflags |= kFlagBucket;
                     const uint32_t bdh = min(q, (uint32_t)kHotBuckets - 1);
                     if (valid) bdmax = max(bdmax, bdh);
@@ -1615,23 +1591,20 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
             load(ch + 4, B1);
             process(B2, ch + 2);
         }
-        if (nhot) {
+        if (nhot && !(dbg & 4)) {
             // rank pass over the sub's keys (just written: L2; all 16 loads in flight together, the
-            // pipeline's registers are free), one round at a time: a scheduling barrier keeps the
-            // 12 ballots of different rounds from interleaving (they would not fit the scalar
-            // registers)
+            // pipeline's registers are free), one round at a time
             uint32_t key[kSubRounds];
 #pragma unroll
             for (int r = 0; r < kSubRounds; ++r) key[r] = sc.hcode[min(ubase + (uint32_t)r * 64 + lane, n - 1)];
 #pragma unroll
             for (int r = 0; r < kSubRounds; ++r) {
-                __builtin_amdgcn_sched_barrier(0);
                 const uint32_t i = ubase + (uint32_t)r * 64 + lane;
                 const uint32_t kv = key[r];
                 const bool hot = i < send && (kv & kKeyHot);
                 const uint32_t hid = kv & 0xFFFu, p = (kv >> 12) & 1u, bdh = (kv >> 13) & 63u;
-                const uint64_t hmask = __ballot(hot);
-                const uint32_t r_in = hmask ? rank_part(c, hmask, hid, lane, lt) : 0u;
+                uint32_t r_in = 0;
+                if (hot) r_in = rank_hot(reinterpret_cast<uint32_t *>(c), hid);
                 np += (uint32_t)__popcll(__ballot(hot && p));
                 if (hot) sc.hcode[i] = (p << 31) | hid | (r_in << 12) | (bdh << 25);
                 else if (i < send) sc.hcode[i] = kNoCode;
@@ -1684,7 +1657,7 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
 #pragma unroll
     for (int r = 0; r < kSubRounds; ++r) code[r] = sc.hcode[min(ubase + (uint32_t)r * 64 + lane, n - 1)];
 #pragma unroll
-    for (int r = 0; r < kSubRounds; ++r) {
+    for (int r = 0; r < ((dbg & 8) ? 0 : kSubRounds); ++r) {
         const uint32_t i = ubase + (uint32_t)r * 64 + lane;
         const uint32_t cd = code[r];
         const bool hot = i < send && cd != kNoCode;
@@ -1706,18 +1679,18 @@ template <int kPass>
 __global__ __launch_bounds__(kKeyThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_hot_key_dense(
     ClusterState st, BatchScratch sc, const int64_t *__restrict__ flow_id, const int32_t *__restrict__ acquire,
     const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off, int64_t ts_base, uint32_t n,
-    uint64_t *__restrict__ out) {
+    uint64_t *__restrict__ out, int dbg) {
     __shared__ KeyShared sh;
-    hot_key<kPass, true>(sh, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out);
+    hot_key<kPass, true>(sh, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out, dbg);
 }
 // Hashed flowId table (sparse flowIds): the probe loop needs more registers.
 template <int kPass>
 __global__ __launch_bounds__(kKeyThreads) void k_hot_key_hash(
     ClusterState st, BatchScratch sc, const int64_t *__restrict__ flow_id, const int32_t *__restrict__ acquire,
     const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off, int64_t ts_base, uint32_t n,
-    uint64_t *__restrict__ out) {
+    uint64_t *__restrict__ out, int dbg) {
     __shared__ KeyShared sh;
-    hot_key<kPass, false>(sh, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out);
+    hot_key<kPass, false>(sh, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out, dbg);
 }
 
 // The batch's path and element counts: sums over the compaction segments and the rank segments
@@ -1933,7 +1906,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
         bool occ_dirty = false;
         if (!rot && lane < CEV_N) cl = R.cnt(lane, cj);
         if (rot && old != kAbsent) {  // resetWindowTo + transferOccupyToBucket
-            o = st.occ[s];
+            o = R.occ();
             if (o.has_occ) {
                 if (lane == CEV_OCCUPIED_PASS || lane == CEV_PASS) cl += o.occ_pass;
                 if (lane == CEV_PASS_REQUEST) cl += o.occ_preq;
@@ -1954,7 +1927,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
         if (np_after > 0) {
             const int64_t wt = (lane < P.S && valid_b) ? R.cnt(CEV_WAITING, lane) : 0;
             const int64_t w0 = lane_i64(cl, CEV_WAITING) + wave_sum_i64(wt);
-            if (!(rot && old != kAbsent)) o = st.occ[s];  // not loaded by the rotation above
+            if (!(rot && old != kAbsent)) o = R.occ();  // not loaded by the rotation above
             const double latest = (double)(s0 + (int64_t)f) / P.isec;
             const double lim = st.max_occupy_ratio * thr;
             const int64_t occ0 = o.occ_pass;
@@ -1987,7 +1960,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
             if (lane < CEV_N) R.cnt(lane, cj) = cl;
             if (lane == 0) {
                 if (rot) R.start(cj) = ws;
-                if (occ_dirty) st.occ[s] = o;
+                if (occ_dirty) R.occ() = o;
             }
         } else if (lane == 0) {
             atomicAdd(&sc.counters[CTL_HOTERR], 1u);
@@ -2283,7 +2256,7 @@ __global__ void k_init_slots(ClusterState st, const uint32_t *slots, uint32_t n)
         R.start(j) = kAbsent;
         bucket_zero(R, j);
     }
-    st.occ[s] = SlotOcc{0, 0, 0, 0};
+    R.occ() = SlotOcc{0, 0, 0, 0};
 }
 
 
@@ -2867,7 +2840,8 @@ static size_t max_hist_entries(size_t cap, uint32_t nslots_cap) {
     return m;
 }
 
-// A/B knob for profiling only (results are wrong when set): 1 skips k_cold_fused's flows, 2 its results
+// A/B knob for profiling only (results are wrong when set): 1 skips k_cold_fused's flows, 2 its results,
+// 4 k_hot_key's rank pass, 8 its code fix-up
 static int fz_debug() {
     static const int v = getenv("SGA_FZ_DEBUG") ? atoi(getenv("SGA_FZ_DEBUG")) : 0;
     return v;
@@ -2969,6 +2943,63 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.cap = cap;
 }
 
+// Probe of the LDS property rank_hot relies on: random hot ids (dense, skewed and sparse, all and
+// half the lanes active) ranked by the packed atomic and by a ballot match of all 12 id bits;
+// mismatches are counted.
+__device__ __forceinline__ uint32_t probe_mix(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+__global__ __launch_bounds__(kThreads) void k_lds_order_probe(uint32_t *bad) {
+    __shared__ uint32_t cw[kThreads / 64][kHot / 2];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t K = 1u << (blockIdx.x % 13);  // 1 .. 4096 distinct ids
+    const int mode = (blockIdx.x / 13) % 3;
+    for (int k = lane; k < kHot / 2; k += 64) cw[w][k] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t lt = lanemask_lt64(lane);
+    uint32_t nb = 0;
+    for (uint32_t r = 0; r < 32; ++r) {
+        const uint32_t x = probe_mix((blockIdx.x * 1315423911u) ^ (r * 2654435761u) ^ (threadIdx.x * 97u));
+        uint32_t hid = x % K;
+        if (mode == 1 && (x & 1u)) hid = 7 % K;
+        const bool act = mode == 2 ? ((x >> 8) & 1u) : true;
+        const uint32_t sh = (hid & 1u) << 4;
+        const uint32_t before = (cw[w][hid >> 1] >> sh) & 0xFFFFu;
+        __builtin_amdgcn_wave_barrier();
+        uint64_t peers = __ballot(act);
+        for (int b = 0; b < 12; ++b) {
+            const bool bit = (hid >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t expect = before + (uint32_t)__popcll(peers & lt);
+        __builtin_amdgcn_wave_barrier();
+        uint32_t got = expect;
+        if (act) got = rank_hot(cw[w], hid);
+        __builtin_amdgcn_wave_barrier();
+        if (got != expect) ++nb;
+    }
+    if (nb) atomicAdd(bad, nb);
+}
+
+bool lds_lane_order_ok(hipStream_t s) {
+    uint32_t *d = nullptr, h = 1;
+    if (hipMalloc(&d, 4) != hipSuccess) return false;
+    bool ok = hipMemsetAsync(d, 0, 4, s) == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(k_lds_order_probe, dim3(13 * 3 * 64), dim3(kThreads), 0, s, d);
+        ok = hipMemcpyAsync(&h, d, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+             hipStreamSynchronize(s) == hipSuccess && h == 0;
+    }
+    (void)hipFree(d);
+    return ok;
+}
+
 void hot_reset(const ClusterState &st, BatchScratch &sc, uint32_t nslots_cap, hipStream_t s) {
     const uint32_t m = std::max(nslots_cap, st.dense_hot ? st.dense_n : 0u);
     hipLaunchKernelGGL(k_hot_reset, dim3(std::max<uint32_t>(1, std::min<uint32_t>((m + 255) / 256, 4096))),
@@ -2992,8 +3023,10 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(k_hot_precheck, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc, ts_off, ts_base, n);
     auto hka = st.dense_n ? k_hot_key_dense<0> : k_hot_key_hash<0>;
     auto hkb = st.dense_n ? k_hot_key_dense<1> : k_hot_key_hash<1>;
-    hipLaunchKernelGGL(hka, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out);
-    hipLaunchKernelGGL(hkb, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out);
+    hipLaunchKernelGGL(hka, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out,
+                       fz_debug());
+    hipLaunchKernelGGL(hkb, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out,
+                       fz_debug());
     hipLaunchKernelGGL(k_hot_mode, dim3(1), dim3(1024), 0, s, sc, nseg * kKeyWaves, nseg);
     hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
     hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, s, sc, ngroups);
@@ -3008,6 +3041,16 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(k_cold_fused, dim3((n + kFzChunk - 1) / kFzChunk), dim3(kFzThreads), 0, s, st, sc, el, n,
                        sc.counters + CTL_NCOLD, invalid_key, acquire, prio, ts_off, ts_base, 0,
                        std::max<uint32_t>(sc.hot_min, 1), out, fz_debug());
+    if (fz_debug() & 16) {  // profiling only: k_cold_fused phase cycles per workgroup
+        unsigned long long ph[8];
+        SGA_HIP_CHECK(hipMemcpyFromSymbolAsync(ph, HIP_SYMBOL(g_fz_phase), sizeof(ph), 0, hipMemcpyDeviceToHost, s));
+        SGA_HIP_CHECK(hipStreamSynchronize(s));
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        SGA_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fz_phase), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
+        if (ph[7])
+            fprintf(stderr, "fz phases (wall_clock64 ticks per workgroup, %llu wgs): runs %.0f flows %.0f results %.0f\n",
+                    ph[7], (double)ph[0] / ph[7], (double)ph[1] / ph[7], (double)ph[2] / ph[7]);
+    }
     hipLaunchKernelGGL(k_hot_final, dim3(nseg), dim3(kThreads), 0, s, sc, n, out);
     hipLaunchKernelGGL(k_prio_results, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el, out);
     const uint32_t sb = 64;  // few workgroups: their bins meet in global atomics
@@ -3035,7 +3078,8 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     auto cls = chunk >= 16 ? k_classify<16>
                            : (chunk >= 8 ? k_classify<8> : (chunk >= 4 ? k_classify<4> : (chunk >= 2 ? k_classify<2> : k_classify<1>)));
     static const int nofuse = getenv("SGA_XP_NOFUSE") ? atoi(getenv("SGA_XP_NOFUSE")) : 0;  // A/B knob
-    if (sc.hot_enabled && !simple && !limited && !lb && st.nslots + (uint64_t)kHot + 2 < kMaxSlots) {
+    if (sc.hot_enabled && sc.hot_lane_order && !simple && !limited && !lb &&
+        st.nslots + (uint64_t)kHot + 2 < kMaxSlots) {
         decide_batch_hot(st, sc, flow_id, acquire, prio, ts_base, ts_off, n, out, s);
         return;
     }

@@ -20,7 +20,8 @@ struct SlotParam {
     int32_t ns;         // namespace index
 };
 
-// Per slot mutable occupy state: ClusterMetricLeapArray.occupyCounter/hasOccupied
+// Per slot mutable occupy state: ClusterMetricLeapArray.occupyCounter/hasOccupied (kept inside the
+// slot's window record, after the (start, PASS) pairs)
 struct SlotOcc {
     int64_t occ_pass;   // occupyCounter[PASS]
     int64_t occ_preq;   // occupyCounter[PASS_REQUEST]
@@ -41,7 +42,6 @@ struct alignas(16) HashEntry {
 
 struct ClusterState {
     const SlotParam *param;
-    SlotOcc *occ;
     int64_t *rec;            // per slot: 8 fields x S buckets at rec[8*boff]; field 0 = window start
                              // (kAbsent = null), fields 1..7 = LongAdder sums per ClusterFlowEvent
     const HashEntry *htab;   // open-addressing flowId -> (slot, windowLengthInMs)
@@ -191,8 +191,13 @@ struct BatchScratch {
     uint32_t *seg_stat;       // per rank segment: prioritized hot requests, largest hot bucket delta
     uint32_t *hot_cand;       // [kHotCand] (slot, count) of cold rules with >= hot_min requests (hot_ctl[6])
     int hot_enabled = 1;      // host policy (sga_set_hot_rules)
+    int hot_lane_order = 0;   // lds_lane_order_ok() held on this device (set when the scratch is made)
     uint32_t hot_min = 64;    // smallest per-batch request count that makes a rule hot
 };
+
+// The hot path's in-order ranks come from LDS atomics whose same-word lanes are served in lane
+// order; this probes that on the current device (once per engine scratch).
+bool lds_lane_order_ok(hipStream_t stream);
 
 // Forget the hot set (rule slots changed or scratch re-carved).
 void hot_reset(const ClusterState &st, BatchScratch &b, uint32_t nslots_cap, hipStream_t stream);

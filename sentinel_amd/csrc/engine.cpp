@@ -64,7 +64,6 @@ struct Engine {
 
     // ---- device state
     DevBuf<SlotParam> d_param;
-    DevBuf<SlotOcc> d_occ;
     DevBuf<int64_t> d_rec;  // 8 int64 per bucket
     DevBuf<HashEntry> d_htab;
     DevBuf<int64_t> d_slot_fid;  // flowId per slot (metric snapshots)
@@ -327,7 +326,6 @@ struct Engine {
     ClusterState state() const {
         ClusterState st{};
         st.param = d_param.p;
-        st.occ = d_occ.p;
         st.rec = d_rec.p;
         st.htab = d_htab.p;
         st.dense = d_dense.p;
@@ -362,6 +360,7 @@ struct Engine {
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
         d_scratch.alloc(bytes);
         batch_scratch_carve(scratch, d_scratch.p, cfg.max_batch, p2);
+        scratch.hot_lane_order = lds_lane_order_ok(stream) ? 1 : 0;
         scratch_slots_cap = p2;
         hot_reset(state(), scratch, p2, stream);
     }
@@ -414,7 +413,6 @@ struct Engine {
         if (d_param.n < slot_cap) {
             size_t c = std::max<size_t>(slot_cap, d_param.n * 2);
             d_param.grow(c, stream);
-            d_occ.grow(c, stream);
         }
         if (d_rec.n < 8 * (size_t)std::max<uint32_t>(bucket_used, 1)) {
             size_t c = std::max<size_t>(8 * (size_t)bucket_used, d_rec.n * 2);
@@ -704,7 +702,7 @@ int sga_load_cluster_flow_rules(sga_engine *e, const char *ns, const sga_cluster
             if (it == g.slot_of.end()) {  // putMetricIfAbsent -> new ClusterMetric(sampleCount, windowIntervalMs)
                 s = g.alloc_slot();
                 SlotHost &h = g.slots[s];
-                const uint32_t need = (uint32_t)r.sample_count;
+                const uint32_t need = (uint32_t)r.sample_count + 1;  // buckets + the occupy state (64-byte units)
                 if (h.bcap < need) {
                     h.boff = g.bucket_used;
                     h.bcap = need;
@@ -1111,8 +1109,7 @@ int sga_cluster_stats(sga_engine *e, uint64_t *n_active, uint64_t *state_bytes) 
         for (auto &h : g.slots) a += h.active ? 1 : 0;
         if (n_active) *n_active = a;
         if (state_bytes)
-            *state_bytes = (uint64_t)g.bucket_used * 64 + g.slots.size() * (sizeof(sga::SlotParam) +
-                                                                                      sizeof(sga::SlotOcc));
+            *state_bytes = (uint64_t)g.bucket_used * 64 + g.slots.size() * sizeof(sga::SlotParam);
         return SGA_OK;
     });
 }
@@ -1127,10 +1124,10 @@ int sga_cluster_batch_info(sga_engine *e, uint32_t *out, size_t n) {
         SGA_HIP_CHECK(hipMemcpyAsync(c, g.scratch.counters, sizeof(c), hipMemcpyDeviceToHost, g.stream));
         SGA_HIP_CHECK(hipMemcpyAsync(hc, g.scratch.hot_ctl, sizeof(hc), hipMemcpyDeviceToHost, g.stream));
         SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
-        const uint32_t v[10] = {c[sga::CTL_MODE],  c[sga::CTL_FLAGS], c[sga::CTL_NSORT], c[sga::CTL_NCOLD],
+        const uint32_t v[11] = {c[sga::CTL_MODE],  c[sga::CTL_FLAGS], c[sga::CTL_NSORT], c[sga::CTL_NCOLD],
                                 c[sga::CTL_NPRIO], hc[0],             c[sga::CTL_BDLO],  c[sga::CTL_BDHI],
-                                c[sga::CTL_HOTERR], c[sga::CTL_NPRE]};
-        for (size_t i = 0; i < n && i < 10; ++i) out[i] = v[i];
+                                c[sga::CTL_HOTERR], c[sga::CTL_NPRE], (uint32_t)g.scratch.hot_lane_order};
+        for (size_t i = 0; i < n && i < 11; ++i) out[i] = v[i];
         return SGA_OK;
     });
 }
