@@ -78,6 +78,19 @@ def main():
     one_device = os.environ.get("SGA_BENCH_ONE_DEVICE") == "1"
     import torch
     import torch.distributed as dist
+    if os.environ.get("SGA_BENCH_DRY") == "1":
+        # launch check only (tests/test_sharding.py, CPU): every rank joins the process group,
+        # all-reduces its rank and reports, before anything touches a GPU
+        if world > 1:
+            dist.init_process_group("gloo")
+        t = torch.tensor([rank], dtype=torch.int64)
+        if world > 1:
+            dist.all_reduce(t)
+        print(json.dumps({"dry": True, "rank": rank, "world": world, "gpus": args.gpus, "rank_sum": int(t.item())}),
+              flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     coll = None       # process group of the metric all-gather
     coll_backend = None
     if world > 1:

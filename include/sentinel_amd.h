@@ -141,6 +141,11 @@ int sga_set_connected_count(sga_engine *e, const char *ns, int32_t connected);
  * (DESIGN.md section 3).  enabled = 0 sends every request through the radix sort.  Default:
  * enabled, min_requests 64. */
 int sga_set_hot_rules(sga_engine *e, int32_t enabled, uint32_t min_requests);
+/* Engine tuning (no reference counterpart): token batches of at most max_requests requests (capped
+ * at 4096, 0 = off; default 4096) are classified and ordered by one workgroup instead of the
+ * multi-launch sort pipeline -- the latency path of a single requestToken.  Decisions are the same
+ * either way. */
+int sga_set_small_batch(sga_engine *e, uint32_t max_requests);
 
 /* Batched DefaultTokenService.requestToken over host buffers; synchronous.
  * Requests are decided in array order as if issued one by one under a mocked

@@ -60,7 +60,7 @@ class Engine:
 
     def __init__(self, device: int = 0, max_batch: int = 1 << 20, max_rules: int = 1 << 16,
                  exceed_count: float = 1.0, max_occupy_ratio: float = 1.0, max_param_keys: int = 0,
-                 hot_rules: bool = True, hot_min_requests: int = 64):
+                 hot_rules: bool = True, hot_min_requests: int = 64, small_batch: int = 4096):
         L = _lib.load()
         cfg = SgaConfig()
         L.sga_config_default(C.byref(cfg))
@@ -77,6 +77,7 @@ class Engine:
         self._h = h
         self.max_batch = max_batch
         self.set_hot_rules(hot_rules, hot_min_requests)
+        self.set_small_batch(small_batch)
         self.clients: dict = {}  # client address -> dense id (concurrency tokens)
 
     def client_id(self, address: Optional[str]) -> int:
@@ -95,6 +96,11 @@ class Engine:
         tests use min_requests=1 to send nearly every rule down the hot path."""
         _lib.check(_lib.load().sga_set_hot_rules(self._h, 1 if enabled else 0, int(min_requests)), self._h,
                    "sga_set_hot_rules")
+
+    def set_small_batch(self, max_requests: int = 4096):
+        """Engine tuning (sga_set_small_batch): token batches of at most `max_requests` (<= 4096,
+        0 = off) are ordered by one workgroup -- the latency path of a single requestToken."""
+        _lib.check(_lib.load().sga_set_small_batch(self._h, int(max_requests)), self._h, "sga_set_small_batch")
 
     def batch_info(self) -> dict:
         """Path of the last token batch (sga_cluster_batch_info)."""

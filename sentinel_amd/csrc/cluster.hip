@@ -1260,6 +1260,93 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused(ClusterState st, Batc
     fz_mark(dbg, 3, fzt);
 }
 
+// ---------------------------------------------------------------- small batches (one call, few requests)
+// A batch of at most kSmall requests (a single TokenService.requestToken, or the few a coalescing
+// queue gathered) is classified and ordered by (rule, arrival) inside one workgroup -- a bitonic
+// sort of the packed elements in LDS on the key slot << 32 | index -- and handed to k_cold_fused:
+// two launches instead of the classify / three radix passes / runs pipeline.
+constexpr int kSmall = 4096;
+constexpr int kSmallThreads = 1024;
+__device__ __forceinline__ uint64_t small_key(uint64_t e) { return ((uint64_t)el_slot(e) << 32) | el_idx(e); }
+__global__ __launch_bounds__(kSmallThreads) void k_small_sort(ClusterState st, const int64_t *__restrict__ flow_id,
+                                                              const int32_t *__restrict__ acquire,
+                                                              const uint8_t *__restrict__ prio,
+                                                              const uint32_t *__restrict__ ts_off, int64_t ts_base,
+                                                              uint32_t n, uint32_t m, int simple, uint32_t invalid_key,
+                                                              uint64_t *__restrict__ el, uint64_t *__restrict__ out) {
+    __shared__ uint64_t e[kSmall];
+    for (uint32_t i = threadIdx.x; i < m; i += kSmallThreads) {
+        if (i >= n) {
+            e[i] = ~0ull;  // padding: sorts last
+            continue;
+        }
+        const int64_t f = flow_id[i];
+        const int32_t a = acquire[i];
+        int8_t status = TRS_OK;
+        uint32_t slot = 0, W = 1;
+        if (!simple && (f <= 0 || a <= 0)) {
+            status = TRS_BAD_REQUEST;
+        } else if (f <= 0) {
+            status = TRS_NO_RULE_EXISTS;
+        } else if (st.dense_n) {
+            if (f <= (int64_t)st.dense_n) {
+                const uint32_t d = (uint32_t)st.dense[f - 1];
+                if (d == ~0u) status = TRS_NO_RULE_EXISTS;
+                else {
+                    slot = d & 0xFFFFFFu;
+                    W = st.wtab[d >> 24];
+                }
+            } else {
+                status = TRS_NO_RULE_EXISTS;
+            }
+        } else {
+            uint32_t q = (uint32_t)hash_flow_id(f) & st.hmask;
+            HashEntry he = st.htab[q];
+            for (uint32_t probe = 1; probe <= st.hmask && he.key != f && he.key != 0; ++probe) {
+                q = (q + 1) & st.hmask;
+                he = st.htab[q];
+            }
+            if (he.key != f) status = TRS_NO_RULE_EXISTS;
+            else {
+                slot = he.slot;
+                W = he.W;
+            }
+        }
+        if (status != TRS_OK) {
+            out[i] = pack_result(status, 0, 0);
+            e[i] = ((uint64_t)invalid_key << kSlotShift) | i;
+        } else {
+            const uint32_t p = (!simple && prio && prio[i]) ? 1u : 0u;
+            const int64_t bd = div_pos(ts_base + (int64_t)ts_off[i], (int64_t)W) - div_pos(ts_base, (int64_t)W);
+            uint32_t a7 = (a >= 1 && a <= (int32_t)kAcqMax) ? (uint32_t)a : 0u;
+            uint32_t bd6 = (uint32_t)bd;
+            if (bd >= (int64_t)kBdEsc) {
+                bd6 = kBdEsc;
+                a7 = 0;
+            }
+            e[i] = el_pack(slot, bd6, p, a7, i);
+        }
+    }
+    __syncthreads();
+    // bitonic sort of m (a power of two) elements
+    for (uint32_t k = 2; k <= m; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < m / 2; t += kSmallThreads) {
+                const uint32_t i = 2 * t - (t & (j - 1));  // lower index of the pair (i, i + j)
+                const uint32_t l = i + j;
+                const uint64_t x = e[i], y = e[l];
+                const bool up = (i & k) == 0;
+                if ((small_key(x) > small_key(y)) == up) {
+                    e[i] = y;
+                    e[l] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += kSmallThreads) el[i] = e[i];
+}
+
 // ---------------------------------------------------------------- hot path
 // Under Zipf skew a few thousand rules carry most requests (C3: the 4096 hottest of 1M rules carry
 // 77 % of them).  Those "hot" rules (hot id < kHot, picked from the previous batch's counts, all
@@ -3078,6 +3165,15 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     auto cls = chunk >= 16 ? k_classify<16>
                            : (chunk >= 8 ? k_classify<8> : (chunk >= 4 ? k_classify<4> : (chunk >= 2 ? k_classify<2> : k_classify<1>)));
     static const int nofuse = getenv("SGA_XP_NOFUSE") ? atoi(getenv("SGA_XP_NOFUSE")) : 0;  // A/B knob
+    if (n <= std::min<uint32_t>(sc.small_max, kSmall) && !limited && !lb) {  // one call's worth of requests: two launches
+        uint32_t m = 64;
+        while (m < n) m <<= 1;
+        hipLaunchKernelGGL(k_small_sort, dim3(1), dim3(kSmallThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base,
+                           n, m, simple, invalid_key, sc.el[0], out);
+        hipLaunchKernelGGL(k_cold_fused, dim3((n + kFzChunk - 1) / kFzChunk), dim3(kFzThreads), 0, s, st, sc, sc.el[0],
+                           n, nullptr, invalid_key, acquire, prio, ts_off, ts_base, simple, 0xFFFFFFFFu, out, 0);
+        return;
+    }
     if (sc.hot_enabled && sc.hot_lane_order && !simple && !limited && !lb &&
         st.nslots + (uint64_t)kHot + 2 < kMaxSlots) {
         decide_batch_hot(st, sc, flow_id, acquire, prio, ts_base, ts_off, n, out, s);

@@ -191,6 +191,7 @@ struct BatchScratch {
     uint32_t *seg_stat;       // per rank segment: prioritized hot requests, largest hot bucket delta
     uint32_t *hot_cand;       // [kHotCand] (slot, count) of cold rules with >= hot_min requests (hot_ctl[6])
     int hot_enabled = 1;      // host policy (sga_set_hot_rules)
+    uint32_t small_max = 4096; // batches of at most this many requests take the one-workgroup path (sga_set_small_batch)
     int hot_lane_order = 0;   // lds_lane_order_ok() held on this device (set when the scratch is made)
     uint32_t hot_min = 64;    // smallest per-batch request count that makes a rule hot
 };

@@ -755,6 +755,16 @@ int sga_set_hot_rules(sga_engine *e, int32_t enabled, uint32_t min_requests) {
     });
 }
 
+// Engine tuning (no reference counterpart): token batches of at most max_requests requests (at
+// most 4096; 0 turns it off) are classified and sorted by one workgroup (k_small_sort) instead of
+// the multi-launch pipeline -- the path a single requestToken takes.  Decisions do not depend on it.
+int sga_set_small_batch(sga_engine *e, uint32_t max_requests) {
+    return guarded(e, [&](Engine &g) {
+        g.scratch.small_max = std::min<uint32_t>(max_requests, 4096u);
+        return SGA_OK;
+    });
+}
+
 int sga_set_namespace_limit(sga_engine *e, const char *ns, double max_allowed_qps) {
     if (!ns || !*ns || !(max_allowed_qps >= 0)) return SGA_EINVAL;  // AssertUtil.isTrue(qpsAllowed >= 0)
     return guarded(e, [&](Engine &g) {

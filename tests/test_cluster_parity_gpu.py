@@ -45,14 +45,16 @@ def eng_mod():
     return cluster
 
 
-HOT_MODES = {"off": dict(hot_rules=False), "on": dict(hot_rules=True, hot_min_requests=64),
-             "all": dict(hot_rules=True, hot_min_requests=1)}
+HOT_MODES = {"off": dict(hot_rules=False, small_batch=0), "on": dict(hot_rules=True, hot_min_requests=64, small_batch=0),
+             "all": dict(hot_rules=True, hot_min_requests=1, small_batch=0),
+             "small": dict(hot_rules=False, small_batch=4096)}
 
 
 def make_engine(cluster, hot="off", **kw):
-    """hot: the engine's hot-rule policy (decisions must not depend on it).  "off" (the default)
+    """hot: the engine's path policy (decisions must not depend on it).  "off" (the default)
     sorts every request, "on" sends rules with >= 64 requests in the previous batch down the
-    hot/cold split, "all" every rule seen in the previous batch (up to 4096)."""
+    hot/cold split, "all" every rule seen in the previous batch (up to 4096), "small" orders
+    batches of up to 4096 requests in one workgroup (k_small_sort) and sorts larger ones."""
     kw.setdefault("max_batch", 1 << 20)
     kw.update(HOT_MODES[hot])
     return cluster.Engine(**kw)
@@ -140,7 +142,7 @@ def test_request_validation(eng_mod):
     assert r["remaining"][5] == 2
 
 
-@pytest.mark.parametrize("hot", ["off", "on", "all"])
+@pytest.mark.parametrize("hot", ["off", "on", "all", "small"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
 @pytest.mark.parametrize("mixed", [False, True])
 @pytest.mark.parametrize("ids", ["dense", "sparse"])

@@ -136,3 +136,30 @@ def test_engine_shards_equal_single_engine():
         got = cluster.DefaultTokenService(e).request_tokens(f[sel], a[sel], p[sel], ts[sel])
         e.close()
         assert np.array_equal(got, full[sel]), r
+
+
+def test_bench_gpus2_launches_two_ranks():
+    """`bench.py --gpus 2` run bare starts two ranks itself (torch.distributed.run child process,
+    before any GPU call); both join one process group (SGA_BENCH_DRY stops them before the GPU)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SGA_BENCH_DRY="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert sorted(d["rank"] for d in lines) == [0, 1]
+    assert all(d["world"] == 2 and d["gpus"] == 2 and d["rank_sum"] == 1 for d in lines)
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SGA_BENCH_DRY="1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus=2" in r.stderr

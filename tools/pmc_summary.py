@@ -1,11 +1,20 @@
 #!/usr/bin/env python3
-"""Summarise tools/pmc_bench.sh output.
+"""HBM traffic of the engine pipeline per bench step from rocprofv3 PMC passes (tools/pmc_bench.sh).
 
-Per kernel: mean counter value per dispatch.  Per step: HBM traffic of the
-engine pipeline = sum over its kernels of (2 x FETCH_SIZE + WRITE_SIZE) per
-dispatch x dispatches per step.  rocprofv3 reports FETCH_SIZE and WRITE_SIZE in
-KiB; FETCH_SIZE is doubled because gfx950 tallies 128-B read requests at 64 B
-(MI355X_MICROARCH.md, HBM section).  --json writes the per-step figure."""
+Counted: the engine's own dispatches only -- kernels of namespace sga:: that run once per batch.
+Excluded: the workload generator's kernels (k_flags / k_emit / k_hist and the exclusive-scan kernels
+k_scan_* it runs once per generated batch), one-time set-up kernels (k_init_slots, k_hot_reset,
+k_lds_order_probe, k_conc_reset), and torch / runtime kernels.
+
+Corrections (MI355X_MICROARCH.md, HBM section, and tools/calib/pmccal.hip measured on the box):
+FETCH_SIZE counts 128-B requests at 64 B, so a wide coalesced streaming read reports half its bytes;
+the x2 applies to the kernels whose reads are coalesced streams (STREAMING below).  Kernels whose
+reads are dominated by random sector gathers (RANDOM below) get the factor the calibration measured
+for random 16-byte reads (--cal JSON; 1.0 without one).  WRITE_SIZE is taken as reported.
+
+Per kernel: calls per step, raw and corrected read MB, write MB, traffic MB per step, and (with
+--trace, a kernel_trace.csv of the same bench) the average duration, so the table's time column sums
+to the step's kernel time.  --json writes the per-step totals and the table."""
 import argparse
 import csv
 import glob
@@ -14,41 +23,107 @@ import os
 import re
 from collections import defaultdict
 
-ap = argparse.ArgumentParser()
-ap.add_argument("dir")
-ap.add_argument("--steps-from", default=None, help="bench output whose JSON line gives steps+warmup")
-ap.add_argument("--json", default=None)
-a = ap.parse_args()
+WORKLOAD = {"k_flags", "k_emit", "k_hist", "k_scan_reduce", "k_scan_apply", "k_scan_partials"}
+ONE_TIME = {"k_init_slots", "k_hot_reset", "k_lds_order_probe", "k_conc_reset", "k_lim_init"}
+# reads are coalesced streams (input arrays, sort tiles, codes, count rows)
+STREAMING = {"k_hot_key_dense<0>", "k_hot_key_dense<1>", "k_hot_final", "k_rs64_hist<7>", "k_rs64_sweep<7>",
+             "k_row_scan", "k_hscan_group", "k_hscan_mid", "k_hscan_down", "k_hot_pre", "k_hot_mode",
+             "k_prio_rank", "k_prio_results"}
+# reads are dominated by random gathers of rule records / parameters
+RANDOM = {"k_cold_fused", "k_hot_flows", "k_hot_precheck", "k_hot_hist", "k_hot_pick", "k_hot_clear", "k_hot_fin",
+          "k_cluster_nodes"}
 
-agg = defaultdict(lambda: defaultdict(list))
-for f in sorted(glob.glob(os.path.join(a.dir, "counters_*.csv"))):
-    for row in csv.DictReader(open(f)):
-        name = row.get("Kernel_Name", row.get("Kernel-Name", "?"))
-        m = re.search(r'(k_\w+(<\d+>)?)', name)
-        agg[m.group(1) if m else name[:60]][row["Counter_Name"]].append(float(row["Counter_Value"]))
 
-steps = None
-if a.steps_from and os.path.exists(a.steps_from):
-    for line in open(a.steps_from):
-        if line.startswith("{"):
-            d = json.loads(line)
-            steps = d["steps"] + d["warmup"]
-tot_fetch = tot_write = 0.0
-for k, cs in sorted(agg.items()):
-    print(k)
-    for c, v in sorted(cs.items()):
-        print(f"   {c:28s} {sum(v) / len(v):16.6g}  (n={len(v)})")
-    if "FETCH_SIZE" in cs:
-        tot_fetch += sum(cs["FETCH_SIZE"]) * 1024.0
-    if "WRITE_SIZE" in cs:
-        tot_write += sum(cs["WRITE_SIZE"]) * 1024.0
-if steps:
-    per_step = (2 * tot_fetch + tot_write) / steps
-    print(f"per step (all engine kernels): FETCH_SIZE {tot_fetch / steps / 1e6:.1f} MB (x2 = {2 * tot_fetch / steps / 1e6:.1f}), "
-          f"WRITE_SIZE {tot_write / steps / 1e6:.1f} MB, traffic {per_step / 1e6:.1f} MB")
+def short(name):
+    m = re.search(r"(k_\w+(<[^>]*>)?)", name)
+    return m.group(1) if m else name[:60]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--steps-from", default=None, help="bench output whose JSON line gives steps+warmup")
+    ap.add_argument("--cal", default=None, help="calibration JSON (tools/pmc_cal.py) with random-read factors")
+    ap.add_argument("--trace", default=None, help="kernel_trace.csv of the same bench for durations")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+
+    agg = defaultdict(lambda: defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(a.dir, "counters_*.csv"))):
+        for row in csv.DictReader(open(f)):
+            name = row.get("Kernel_Name", row.get("Kernel-Name", "?"))
+            agg[(short(name), "sga::" in name)][row["Counter_Name"]].append(float(row["Counter_Value"]))
+
+    sets = None
+    if a.steps_from and os.path.exists(a.steps_from):
+        for line in open(a.steps_from):
+            if line.startswith("{"):
+                d = json.loads(line)
+                sets = d["steps"] + d["warmup"]
+    rand_factor = 1.0
+    if a.cal and os.path.exists(a.cal):
+        rand_factor = float(json.load(open(a.cal)).get("random16_fetch_factor", 1.0))
+
+    durations = defaultdict(list)
+    if a.trace and os.path.exists(a.trace):
+        for row in csv.DictReader(open(a.trace)):
+            durations[short(row.get("Kernel_Name", "?"))].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+
+    # every counter of a kernel, averaged per dispatch (diagnostics)
+    for (k, eng), cs in sorted(agg.items()):
+        print(f"{k}{'' if eng else '  (not engine)'}")
+        for c, v in sorted(cs.items()):
+            print(f"   {c:28s} {sum(v) / len(v):16.6g}  (n={len(v)})")
+
+    if not sets:
+        return
+    table = []
+    tot = {"fetch_raw": 0.0, "fetch": 0.0, "write": 0.0, "us": 0.0}
+    for (k, eng), cs in sorted(agg.items()):
+        if not eng or k in WORKLOAD or k in ONE_TIME:
+            continue
+        if "FETCH_SIZE" not in cs and "WRITE_SIZE" not in cs:
+            continue
+        n_calls = max(len(cs.get("FETCH_SIZE", [])), len(cs.get("WRITE_SIZE", [])))
+        per_step = n_calls / sets
+        fr = (sum(cs.get("FETCH_SIZE", [0.0])) / max(1, len(cs.get("FETCH_SIZE", [])))) * 1024.0
+        wr = (sum(cs.get("WRITE_SIZE", [0.0])) / max(1, len(cs.get("WRITE_SIZE", [])))) * 1024.0
+        kind = "stream" if k in STREAMING else ("random" if k in RANDOM else "other")
+        fac = 2.0 if kind == "stream" else (rand_factor if kind == "random" else 1.0)
+        us = None
+        if durations.get(k):
+            dd = sorted(durations[k])  # median dispatch (warmup / fallback batches included)
+            us = dd[len(dd) // 2] / 1e3 * per_step
+            tot["us"] += us
+        row = {"kernel": k, "kind": kind, "calls_per_step": per_step, "fetch_raw_mb": fr * per_step / 1e6,
+               "fetch_factor": fac, "fetch_mb": fr * fac * per_step / 1e6, "write_mb": wr * per_step / 1e6,
+               "us_per_step": us}
+        row["traffic_mb"] = row["fetch_mb"] + row["write_mb"]
+        tot["fetch_raw"] += row["fetch_raw_mb"]
+        tot["fetch"] += row["fetch_mb"]
+        tot["write"] += row["write_mb"]
+        table.append(row)
+    table.sort(key=lambda r: -r["traffic_mb"])
+    print(f"\nper step ({sets} dispatch sets; engine kernels only; FETCH x2 for streaming kernels, "
+          f"x{rand_factor:.2f} for random-gather kernels)")
+    print(f"{'kernel':24s} {'kind':7s} {'calls':>5s} {'fetch_raw':>10s} {'fetch':>10s} {'write':>10s} {'traffic':>10s} {'us':>8s}")
+    for r in table:
+        us = f"{r['us_per_step']:8.1f}" if r["us_per_step"] is not None else "       -"
+        print(f"{r['kernel']:24s} {r['kind']:7s} {r['calls_per_step']:5.2f} {r['fetch_raw_mb']:10.1f} {r['fetch_mb']:10.1f} "
+              f"{r['write_mb']:10.1f} {r['traffic_mb']:10.1f} {us}")
+    traffic = (tot["fetch"] + tot["write"]) * 1e6
+    print(f"{'total':24s} {'':7s} {'':5s} {tot['fetch_raw']:10.1f} {tot['fetch']:10.1f} {tot['write']:10.1f} "
+          f"{traffic / 1e6:10.1f} {tot['us']:8.1f}")
     if a.json:
-        json.dump({"traffic_bytes_per_step": per_step, "fetch_bytes_per_step_raw": tot_fetch / steps,
-                   "write_bytes_per_step": tot_write / steps, "dispatch_sets": steps,
-                   "run": os.path.basename(os.path.normpath(a.dir)),
-                   "note": "2*FETCH_SIZE+WRITE_SIZE (KiB->B) summed over the engine kernels of one step"},
+        json.dump({"traffic_bytes_per_step": traffic, "fetch_bytes_per_step": tot["fetch"] * 1e6,
+                   "fetch_bytes_per_step_raw": tot["fetch_raw"] * 1e6, "write_bytes_per_step": tot["write"] * 1e6,
+                   "kernel_us_per_step": tot["us"], "dispatch_sets": sets, "random_fetch_factor": rand_factor,
+                   "run": os.path.basename(os.path.normpath(a.dir)), "kernels": table,
+                   "note": "engine kernels only (sga::, per batch); FETCH_SIZE x2 for coalesced streaming kernels, "
+                           "x random16_fetch_factor (tools/calib/pmccal.hip) for random-gather kernels; WRITE_SIZE as "
+                           "reported"},
                   open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
