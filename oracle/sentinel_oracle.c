@@ -1000,6 +1000,13 @@ void orc_cluster_replay(orc_cluster *c, size_t n, const int64_t *flow_id, const 
         out[i] = orc_cluster_request_token(c, flow_id[i], acquire[i], prio ? prio[i] : 0, ts[i]);
 }
 
+/* Envoy RLS replay: SimpleClusterFlowChecker per descriptor (sentinel-cluster-server-envoy-rls
+ * .../flow/SimpleClusterFlowChecker.java:35-60), descriptors in order. */
+void orc_cluster_replay_simple(orc_cluster *c, size_t n, const int64_t *flow_id, const int32_t *acquire,
+                               const int64_t *ts, orc_token_result *out) {
+    for (size_t i = 0; i < n; i++) out[i] = orc_cluster_request_token_simple(c, flow_id[i], acquire[i], ts[i]);
+}
+
 int64_t orc_cluster_metric_sum(orc_cluster *c, int64_t flow_id, int ev, int64_t now) {
     crule *e = ctab_find(c, flow_id, 0);
     if (!e || !e->metric) return -1;

@@ -195,6 +195,9 @@ orc_token_result orc_cluster_request_token(orc_cluster *c, int64_t flow_id, int3
 orc_token_result orc_cluster_request_token_simple(orc_cluster *c, int64_t flow_id, int32_t acquire, int64_t now);
 void orc_cluster_replay(orc_cluster *c, size_t n, const int64_t *flow_id, const int32_t *acquire,
                         const uint8_t *prio, const int64_t *ts, orc_token_result *out);
+/* SimpleClusterFlowChecker per descriptor, in order (Envoy RLS front end). */
+void orc_cluster_replay_simple(orc_cluster *c, size_t n, const int64_t *flow_id, const int32_t *acquire,
+                               const int64_t *ts, orc_token_result *out);
 /* sum of a ClusterFlowEvent over valid buckets of flow's metric at now (ClusterMetric.getSum) */
 int64_t orc_cluster_metric_sum(orc_cluster *c, int64_t flow_id, int ev, int64_t now);
 /* standalone ClusterMetric (CS/flow/statistic/metric/ClusterMetric.java) for KATs */

@@ -112,6 +112,7 @@ def lib():
         "orc_cluster_request_token": (OrcTokenResult, [P, I64, I32, C.c_int, I64]),
         "orc_cluster_request_token_simple": (OrcTokenResult, [P, I64, I32, I64]),
         "orc_cluster_replay": (None, [P, C.c_size_t, P, P, P, P, P]),
+        "orc_cluster_replay_simple": (None, [P, C.c_size_t, P, P, P, P]),
         "orc_cluster_metric_sum": (I64, [P, I64, C.c_int, I64]),
         "orc_cmetric_new": (P, [C.c_int, C.c_int]),
         "orc_cmetric_free": (None, [P]),

@@ -1,0 +1,194 @@
+"""BASELINE.json configurations C1, C2, C4 and C5 at their stated sizes on the GPU, bit-exact against
+the oracle replay of the same stream (C3 is test_c3_full_size_* in
+test_cluster_parity_gpu.py).
+
+Streams are generated window by window (tests/local_trace.generate_windows): entries are decided by a
+generator oracle, the ones that pass exit later with a response time (and an error flag), so exits
+follow real entries as StatisticSlot.exit does.  The engine then replays the whole stream through the
+C-ABI in max_batch chunks and a fresh oracle replays it in one pass; decisions and wait times of every
+event, every resource's MetricNode rows (StatisticNode.metrics at the end), the node views of the
+hottest resources and every breaker's state must be equal.
+
+  C1  HelloWorld: one resource, QPS FlowRule count 20, DefaultController, 1M entries (~1 per ms).
+  C2  100k FlowRules 40 % DefaultController / 30 % RateLimiter / 30 % WarmUp over 100k resources,
+      Zipf(1.1) traffic, 2^22 entries with exits, 5 % of them acquiring 2..5.
+  C4  10k ParamFlowRules (90 % QPS default / 10 % throttle), Zipf parameter values over 10M folded to at
+      most 4000 distinct values per rule (inside the CacheMap capacity min(4000 * duration, 200000), so
+      the reference's map never evicts: the pinned mode of SURVEY.md 8(d)).
+  C5  (a) Envoy RLS: 100k descriptor rules, requests of 1..4 descriptors, SimpleClusterFlowChecker per
+      descriptor; (b) DegradeSlot: 10k DegradeRules, 50 % slow-RT / 50 % exception-ratio breakers,
+      log-normal response times, 5 % errors.
+"""
+import numpy as np
+import pytest
+
+from tests import local_trace as lt
+from tests import oracle_harness as H
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1_700_000_000_000
+
+
+def _zipf(rng, n_items, size, s=1.1):
+    p = 1.0 / np.arange(1, n_items + 1) ** s
+    p /= p.sum()
+    return rng.choice(n_items, size=size, p=p)
+
+
+def _local(n_res, flow=(), param=(), degrade=(), max_batch=1 << 20):
+    from sentinel_amd.cluster import Engine
+    from sentinel_amd.local import LocalSentinel
+    from tests.test_local_parity_gpu import _load
+    eng = Engine(max_batch=max_batch)
+    s = LocalSentinel(eng, [f"r{i}" for i in range(n_res)])
+    _load(s, flow=list(flow) or None, param=list(param) or None, degrade=list(degrade) or None)
+    return eng, s
+
+
+def _check_local(n_res, st, flow=(), param=(), degrade=(), max_batch=1 << 20, hot_nodes=64):
+    orc = lt.Oracle(n_res, list(flow), list(param), list(degrade))
+    exp_d, exp_w = orc.replay(st)
+    eng, s = _local(n_res, flow, param, degrade, max_batch)
+    n = len(st["kind"])
+    got_d = np.zeros(n, np.int8)
+    got_w = np.zeros(n, np.int32)
+    for lo in range(0, n, max_batch):  # the engine sees the stream in max_batch chunks
+        sub = {k: np.ascontiguousarray(v[lo:lo + max_batch]) for k, v in st.items()}
+        d, w = s.submit(sub["kind"], sub["resource"], sub["ts"], sub["acquire"], sub["flags"], sub["rt"],
+                        sub["param"])
+        got_d[lo:lo + len(d)] = d
+        got_w[lo:lo + len(w)] = w
+    bad = np.nonzero((got_d != exp_d) | (got_w != exp_w))[0]
+    assert len(bad) == 0, (f"{len(bad)} of {n} events differ; first at {bad[0]}: kind={st['kind'][bad[0]]} "
+                           f"res={st['resource'][bad[0]]} gpu=({got_d[bad[0]]},{got_w[bad[0]]}) "
+                           f"oracle=({exp_d[bad[0]]},{exp_w[bad[0]]})")
+    now = int(st["ts"].max()) + 1
+    got = [(m.timestamp, s.resource_id(m.resource), m.pass_qps, m.block_qps, m.success_qps, m.exception_qps, m.rt,
+            m.occupied_pass_qps) for m in s.metrics(now, cap=1 << 20)]
+    exp = orc.metrics(now, cap=1 << 20)
+    assert got == exp, (len(got), len(exp))
+    hot = np.argsort(-np.bincount(st["resource"].astype(np.int64), minlength=n_res))[:hot_nodes]
+    for rid in hot:
+        v = s.node(int(rid), now)
+        assert [getattr(v, g) for g in lt.NODE_GETTERS] == orc.node(int(rid), now), int(rid)
+    if degrade:
+        for r in degrade:
+            rid = r["resource"]
+            assert s.circuit_breaker_state(rid, 0) == orc.cb_state(rid, 0), rid
+    orc.close()
+    eng.close()
+    return exp_d
+
+
+def test_c1_hello_world_1m_entries():
+    rng = np.random.default_rng(101)
+    n = 1_000_000
+    flow = [{"resource": 0, "count": 20.0}]
+    ts = T0 + np.cumsum(rng.integers(0, 3, size=n))  # ~1 entry per ms
+    gen = lt.Oracle(1, flow)
+    st = lt.generate_windows(gen, np.zeros(n), ts, np.ones(n), np.zeros(n, np.uint8), np.zeros(n, np.uint64),
+                             rng.integers(5, 60, size=n), rng.random(n) < 0.02, window_ms=5)
+    gen.close()
+    d = _check_local(1, st, flow=flow, max_batch=1 << 20)
+    ent = st["kind"] == 0
+    assert (d[ent] == 0).sum() > 10_000 and (d[ent] == 1).sum() > 100_000  # 20 QPS passes, the rest blocks
+
+
+def test_c2_100k_mixed_controllers_zipf():
+    rng = np.random.default_rng(102)
+    n_res, n = 100_000, 1 << 22
+    flow = []
+    for r in range(n_res):
+        u = r % 10
+        if u < 4:
+            flow.append({"resource": r, "count": float(rng.integers(5, 500))})
+        elif u < 7:
+            flow.append({"resource": r, "count": float(rng.integers(5, 500)), "control_behavior": 2,
+                         "max_queueing_time_ms": int(rng.choice([20, 500]))})
+        else:
+            flow.append({"resource": r, "count": float(rng.integers(5, 500)), "control_behavior": 1,
+                         "warm_up_period_sec": int(rng.integers(1, 11))})
+    res = _zipf(rng, n_res, n)
+    ts = T0 + (np.arange(n) // 1000)  # 1M entries per virtual second
+    acq = np.where(rng.random(n) < 0.05, rng.integers(2, 6, size=n), 1)
+    gen = lt.Oracle(n_res, flow)
+    st = lt.generate_windows(gen, res, ts, acq, np.zeros(n, np.uint8), np.zeros(n, np.uint64),
+                             rng.integers(1, 40, size=n), rng.random(n) < 0.01, window_ms=1)
+    gen.close()
+    d = _check_local(n_res, st, flow=flow, max_batch=1 << 21)
+    ent = st["kind"] == 0
+    assert (d[ent] == 0).any() and (d[ent] == 1).any() and (st["kind"] == 1).sum() > 100_000
+
+
+def test_c4_10k_param_rules_pinned():
+    rng = np.random.default_rng(104)
+    n_res, n = 10_000, 1 << 22
+    param = [{"resource": r, "count": float(rng.integers(1, 100)),
+              **({"control_behavior": 2, "max_queueing_time_ms": int(rng.choice([0, 50, 200]))} if r % 10 == 9 else {})}
+             for r in range(n_res)]
+    res = _zipf(rng, n_res, n)
+    vals = _zipf(rng, 10_000_000, n) % 4000  # at most 4000 distinct values per rule: no CacheMap eviction
+    ts = T0 + (np.arange(n) // 1000)
+    gen = lt.Oracle(n_res, [], param)
+    st = lt.generate_windows(gen, res, ts, np.ones(n), np.full(n, 4, np.uint8), vals.astype(np.uint64),
+                             rng.integers(1, 30, size=n), np.zeros(n, bool), window_ms=1)
+    gen.close()
+    d = _check_local(n_res, st, param=param, max_batch=1 << 21)
+    ent = st["kind"] == 0
+    assert (d[ent] == 0).any() and (d[ent] == 2).any()  # ParamFlowException blocks happen
+
+
+def test_c5b_10k_degrade_rules_lognormal_rt():
+    rng = np.random.default_rng(105)
+    n_res, n = 10_000, 1 << 21
+    degrade = [{"resource": r, "grade": 0 if r % 2 == 0 else 1, "count": 50.0 if r % 2 == 0 else 0.3,
+                "time_window": int(rng.integers(1, 4)), "min_request_amount": 5, "slow_ratio_threshold": 0.5,
+                "stat_interval_ms": 1000} for r in range(n_res)]
+    res = _zipf(rng, n_res, n)
+    ts = T0 + (np.arange(n) // 1000)
+    rt = np.clip(np.round(rng.lognormal(mean=3.0, sigma=1.0, size=n)), 1, 5000).astype(np.int64)
+    gen = lt.Oracle(n_res, [], [], degrade)
+    st = lt.generate_windows(gen, res, ts, np.ones(n), np.zeros(n, np.uint8), np.zeros(n, np.uint64), rt,
+                             rng.random(n) < 0.05, window_ms=1)
+    gen.close()
+    d = _check_local(n_res, st, degrade=degrade, max_batch=1 << 20)
+    ent = st["kind"] == 0
+    assert (d[ent] == 3).any() and (d[ent] == 0).any()  # breakers open and close
+
+
+def test_c5a_rls_100k_descriptors():
+    from sentinel_amd import cluster
+    rng = np.random.default_rng(106)
+    n_rules, nreq = 100_000, 1 << 20
+    fids = np.arange(1, n_rules + 1, dtype=np.int64) * 7919 + 2147483647
+    counts = rng.integers(10, 1000, size=n_rules)
+    eng = cluster.Engine(max_batch=1 << 22)
+    cluster.ClusterFlowRuleManager(eng).load_rule_arrays("default", fids, counts, threshold_type=1, sample_count=1)
+    L = H.lib()
+    oh = L.orc_cluster_new(1.0, 1.0)
+    arr = H.cluster_rules_array([{"flow_id": int(f), "count": float(c), "threshold_type": 1, "sample_count": 1}
+                                 for f, c in zip(fids, counts)])
+    L.orc_cluster_load_rules(oh, b"default", arr, n_rules)
+    ndesc = rng.integers(1, 5, size=nreq)
+    off = np.concatenate([[0], np.cumsum(ndesc)]).astype(np.uint32)
+    dfid = fids[_zipf(rng, n_rules, int(off[-1]))]
+    dfid[rng.random(len(dfid)) < 0.01] = 42  # descriptors without a rule: NO_RULE_EXISTS answers OK
+    hits = rng.integers(0, 4, size=nreq).astype(np.int32)  # hitsAddend 0 counts as 1
+    ts = T0 + (np.arange(nreq) // 500)
+    svc = cluster.EnvoyRlsService(eng)
+    code, st, rem = svc.should_rate_limit(off, dfid, hits, ts, with_remaining=True)
+    acq = np.repeat(np.where(hits == 0, 1, hits), ndesc).astype(np.int32)
+    dts = np.repeat(ts, ndesc).astype(np.int64)
+    out = (H.OrcTokenResult * len(dfid))()
+    L.orc_cluster_replay_simple(oh, len(dfid), dfid.ctypes.data, acq.ctypes.data, dts.ctypes.data, out)
+    exp = np.frombuffer(out, dtype=np.dtype([("status", np.int32), ("remaining", np.int32), ("wait", np.int32)]))
+    es = exp["status"].astype(np.int64)
+    er = exp["remaining"].astype(np.int64)
+    assert np.array_equal(np.asarray(st, np.int64), es)
+    assert np.array_equal(np.asarray(rem, np.int64), er)
+    blocked = np.add.reduceat((es != 0) & (es != 3), off[:-1].astype(np.int64)) > 0
+    assert np.array_equal(np.asarray(code), np.where(blocked, 2, 1))
+    assert blocked.any() and (~blocked).any()
+    L.orc_cluster_free(oh)
+    eng.close()
