@@ -59,6 +59,7 @@ extern "C" {
 #define SGA_ENODEV (-19)  /* no usable gfx950 device */
 #define SGA_ERANGE (-34)  /* batch larger than the configured capacity */
 #define SGA_ENOSYS (-38)  /* feature not available on this build */
+#define SGA_EAGAIN (-11)  /* sga_poll: the request is not decided yet */
 
 /* TokenResultStatus codes, CORE/cluster/TokenResultStatus.java:27-60 */
 #define SGA_TOKEN_BAD_REQUEST (-4)
@@ -152,6 +153,22 @@ int sga_set_small_batch(sga_engine *e, uint32_t max_requests);
  * TimeUtil returning ts[i] (epoch ms).  Host-pinned or pageable buffers. */
 int sga_request_tokens(sga_engine *e, const int64_t *flow_id, const int32_t *acquire, const uint8_t *prioritized,
                        const int64_t *ts, size_t n, sga_token_result *out);
+
+/* Coalescing queue for single requests.  TokenService.requestToken is called once per request from
+ * many threads (FlowRequestProcessor.java:43 -> DefaultTokenService.requestToken,
+ * CS/flow/DefaultTokenService.java:39-54); calling sga_request_tokens with n = 1 from each would
+ * launch one pipeline per request.  sga_token_submit enqueues one request (lock-free, any thread)
+ * and returns a ticket; sga_poll returns SGA_OK with its TokenResult once decided, SGA_EAGAIN before
+ * (a poller that finds no batch running decides every queued request as one batch, so concurrent
+ * callers share a launch); each ticket is polled to SGA_OK exactly once.  sga_request_token_one =
+ * submit + poll until decided (the drop-in for a synchronous requestToken).  Decisions equal one
+ * sga_request_tokens batch per request in ticket order.  A batch that fails answers
+ * TokenResultStatus.FAIL (-1). */
+int sga_token_submit(sga_engine *e, int64_t flow_id, int32_t acquire, uint8_t prioritized, int64_t ts,
+                     uint64_t *ticket);
+int sga_poll(sga_engine *e, uint64_t ticket, sga_token_result *out);
+int sga_request_token_one(sga_engine *e, int64_t flow_id, int32_t acquire, uint8_t prioritized, int64_t ts,
+                          sga_token_result *out);
 
 /* Same over DEVICE buffers, asynchronous on `hip_stream` (NULL = engine stream).
  * Timestamps are ts_base + ts_off[i].  Inputs must stay valid until the stream

@@ -332,7 +332,31 @@ class DefaultTokenService:
         return out
 
     def request_token(self, rule_id: int, acquire_count: int, prioritized: bool, now: int) -> TokenResult:
-        r = self.request_tokens([rule_id], [acquire_count], [1 if prioritized else 0], [now])[0]
+        """TokenService.requestToken, one call: through the engine's coalescing queue
+        (sga_request_token_one), so concurrent callers share one launch."""
+        out = np.zeros(1, dtype=TOKEN_DTYPE)
+        rc = _lib.load().sga_request_token_one(self.engine.handle, int(rule_id), int(acquire_count),
+                                               1 if prioritized else 0, int(now), out.ctypes.data)
+        check(rc, self.engine.handle, "requestToken")
+        r = out[0]
+        return TokenResult(int(r["status"]), int(r["remaining"]), int(r["wait_in_ms"]))
+
+    def submit(self, rule_id: int, acquire_count: int, prioritized: bool, now: int) -> int:
+        """Asynchronous requestToken (sga_token_submit): returns a ticket for poll()."""
+        t = C.c_uint64()
+        rc = _lib.load().sga_token_submit(self.engine.handle, int(rule_id), int(acquire_count),
+                                          1 if prioritized else 0, int(now), C.byref(t))
+        check(rc, self.engine.handle, "submit")
+        return int(t.value)
+
+    def poll(self, ticket: int) -> Optional[TokenResult]:
+        """sga_poll: the ticket's TokenResult once decided (each ticket answers once), else None."""
+        out = np.zeros(1, dtype=TOKEN_DTYPE)
+        rc = _lib.load().sga_poll(self.engine.handle, int(ticket), out.ctypes.data)
+        if rc == -11:  # SGA_EAGAIN
+            return None
+        check(rc, self.engine.handle, "poll")
+        r = out[0]
         return TokenResult(int(r["status"]), int(r["remaining"]), int(r["wait_in_ms"]))
 
     def request_param_tokens(self, flow_id, acquire, params, ts) -> np.ndarray:

@@ -83,6 +83,26 @@ struct HipError {
 };
 
 // Minimal owning device buffer.
+// Page-locked host staging (one DMA per direction for small batches).
+struct PinnedBuf {
+    uint8_t *p = nullptr;
+    size_t n = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf &) = delete;
+    PinnedBuf &operator=(const PinnedBuf &) = delete;
+    ~PinnedBuf() { release(); }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void alloc(size_t bytes) {
+        release();
+        SGA_HIP_CHECK(hipHostMalloc((void **)&p, bytes, hipHostMallocDefault));
+        n = bytes;
+    }
+};
+
 template <typename T>
 struct DevBuf {
     T *p = nullptr;

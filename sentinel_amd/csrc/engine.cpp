@@ -6,6 +6,9 @@
 #include "flow.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <memory>
+#include <thread>
 #include <cstring>
 #include <mutex>
 #include <random>
@@ -49,11 +52,41 @@ struct NamespaceHost {
     double max_qps = 0;
 };
 
+// Coalescing queue of single token requests (TokenService.requestToken is called once per request,
+// from many Netty threads: FlowRequestProcessor.java:43).  Producers take a ticket with one atomic
+// add and fill the ring slot the ticket names (a bounded multi-producer ring with per-slot sequence
+// numbers: slot seq == t free for ticket t, t + 1 filled, t + 2 decided; the poller frees it for
+// t + kCap).  Whoever polls while no batch is running becomes the combiner: it takes every filled
+// slot from the head in ticket order and decides them as ONE engine batch, so concurrent callers
+// share a launch, and decisions equal one batch per call in ticket order.
+struct TokenQueue {
+    static constexpr uint64_t kCap = 1u << 16;
+    struct Slot {
+        std::atomic<uint64_t> seq{0};
+        int64_t flow_id = 0, ts = 0;
+        int32_t acquire = 0;
+        uint8_t prio = 0;
+        uint64_t result = 0;
+    };
+    std::unique_ptr<Slot[]> ring{new Slot[kCap]};
+    std::atomic<uint64_t> tail{0};
+    uint64_t head = 0;  // combiner only
+    std::atomic<bool> combining{false};
+    std::vector<int64_t> fid, ts;
+    std::vector<int32_t> acq;
+    std::vector<uint8_t> prio;
+    std::vector<uint64_t> out;
+    TokenQueue() {
+        for (uint64_t i = 0; i < kCap; ++i) ring[i].seq.store(i, std::memory_order_relaxed);
+    }
+};
+
 struct Engine {
     sga_config cfg{};
     hipStream_t stream = nullptr;
     std::string err;
     std::mutex mu;
+    TokenQueue tq;
 
     // ---- cluster rules (host mirror)
     std::vector<SlotHost> slots;
@@ -83,6 +116,11 @@ struct Engine {
     DevBuf<uint8_t> d_in_prio;
     DevBuf<uint32_t> d_in_ts;
     DevBuf<uint64_t> d_out;
+    // small batches (<= kSmallStage requests): inputs packed [flowId | acquire | ts offset | prio] in
+    // page-locked memory, one copy each way
+    static constexpr size_t kSmallStage = 4096;
+    PinnedBuf h_stage, h_res;
+    DevBuf<uint8_t> d_stage;
     DevBuf<int64_t> d_tmp7;
     DevBuf<NsLimiterDev> d_lim;  // one per namespace index (used when the namespace has a limiter)
 
@@ -635,6 +673,8 @@ int sga_destroy(sga_engine *e) {
             (void)hipStreamSynchronize(e->impl.stream);
             e->impl.release_events();
             e->impl.flow.release();
+            e->impl.h_stage.release();
+            e->impl.h_res.release();
             (void)hipStreamDestroy(e->impl.stream);
         }
     }
@@ -856,6 +896,48 @@ static int run_host_batch(Engine &g, const int64_t *flow_id, const int32_t *acqu
     }
     std::vector<uint32_t> off;
     const auto lims = limiter_passes(g);
+    if (n <= std::min(Engine::kSmallStage, cap) && n > 0) {  // one staged copy each way
+        int64_t lo = ts[0], hi = ts[0];
+        for (size_t i = 0; i < n; ++i) {
+            if (ts[i] < 0) return SGA_EINVAL;  // LeapArray.currentWindow(t < 0) returns null
+            lo = std::min(lo, ts[i]);
+            hi = std::max(hi, ts[i]);
+        }
+        if (hi - lo <= (int64_t)0xFFFFFFFFLL) {
+            const size_t cap_b = Engine::kSmallStage * 17;
+            if (!g.h_stage.p) {
+                g.h_stage.alloc(cap_b);
+                g.h_res.alloc(Engine::kSmallStage * 8);
+                g.d_stage.alloc(cap_b);
+            }
+            uint8_t *h = g.h_stage.p;
+            std::memcpy(h, flow_id, n * 8);
+            std::memcpy(h + 8 * n, acquire, n * 4);
+            uint32_t *to = reinterpret_cast<uint32_t *>(h + 12 * n);
+            for (size_t i = 0; i < n; ++i) to[i] = (uint32_t)(ts[i] - lo);
+            if (prio) std::memcpy(h + 16 * n, prio, n);
+            else std::memset(h + 16 * n, 0, n);
+            SGA_HIP_CHECK(hipMemcpyAsync(g.d_stage.p, h, 17 * n, hipMemcpyHostToDevice, g.stream));
+            uint8_t *d = g.d_stage.p;
+            sga::cluster_decide_batch(g.state(), g.scratch, reinterpret_cast<const int64_t *>(d),
+                                      reinterpret_cast<const int32_t *>(d + 8 * n), d + 16 * n, lo,
+                                      reinterpret_cast<const uint32_t *>(d + 12 * n), (uint32_t)n, simple, g.d_out.p,
+                                      g.stream, lims.data(), (int)lims.size());
+            SGA_HIP_CHECK(hipGetLastError());
+            SGA_HIP_CHECK(hipMemcpyAsync(g.h_res.p, g.d_out.p, n * 8, hipMemcpyDeviceToHost, g.stream));
+            SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+            std::memcpy(out, g.h_res.p, n * 8);
+            if (sga::radix64_lookback()) {
+                uint32_t err = 0;
+                SGA_HIP_CHECK(hipMemcpy(&err, g.scratch.radix.err, 4, hipMemcpyDeviceToHost));
+                if (err) {
+                    g.err = "radix look-back timed out";
+                    return SGA_EIO;
+                }
+            }
+            return SGA_OK;
+        }
+    }
     for (size_t b = 0; b < n;) {
         // chunk: at most cap events and a timestamp span that fits u32 offsets
         size_t m = std::min(cap, n - b);
@@ -903,6 +985,99 @@ int sga_request_tokens(sga_engine *e, const int64_t *flow_id, const int32_t *acq
     return guarded(e, [&](Engine &g) {
         return run_host_batch(g, flow_id, acquire, prio, ts, n, (uint64_t *)out, 0);
     });
+}
+
+// ---- coalescing queue (TokenQueue above)
+int sga_token_submit(sga_engine *e, int64_t flow_id, int32_t acquire, uint8_t prioritized, int64_t ts,
+                     uint64_t *ticket) {
+    if (!e || !ticket) return SGA_EINVAL;
+    sga::TokenQueue &q = e->impl.tq;
+    const uint64_t t = q.tail.fetch_add(1, std::memory_order_relaxed);
+    sga::TokenQueue::Slot &sl = q.ring[t & (sga::TokenQueue::kCap - 1)];
+    // a full ring (the ticket kCap earlier not collected yet) waits for its poller
+    for (int spin = 0; sl.seq.load(std::memory_order_acquire) != t; ++spin)
+        if (spin > 64) std::this_thread::yield();
+    sl.flow_id = flow_id;
+    sl.acquire = acquire;
+    sl.prio = prioritized ? 1 : 0;
+    sl.ts = ts;
+    sl.seq.store(t + 1, std::memory_order_release);
+    *ticket = t;
+    return SGA_OK;
+}
+
+// One combining round: decide every filled slot from the head as one batch (at most max_batch).
+// Returns the engine status of the batch (results of a failed batch carry TokenResultStatus.FAIL).
+static int combine_round(sga_engine *e) {
+    sga::TokenQueue &q = e->impl.tq;
+    bool expect = false;
+    if (!q.combining.compare_exchange_strong(expect, true, std::memory_order_acquire)) return SGA_OK;
+    const uint64_t h = q.head;
+    const uint64_t cap = std::min<uint64_t>(e->impl.cfg.max_batch, sga::TokenQueue::kCap);
+    uint64_t k = 0;
+    q.fid.clear();
+    q.acq.clear();
+    q.prio.clear();
+    q.ts.clear();
+    while (k < cap) {
+        sga::TokenQueue::Slot &sl = q.ring[(h + k) & (sga::TokenQueue::kCap - 1)];
+        if (sl.seq.load(std::memory_order_acquire) != h + k + 1) break;  // not filled yet: next round
+        q.fid.push_back(sl.flow_id);
+        q.acq.push_back(sl.acquire);
+        q.prio.push_back(sl.prio);
+        q.ts.push_back(sl.ts);
+        ++k;
+    }
+    int rc = SGA_OK;
+    if (k) {
+        q.out.assign(k, 0);
+        rc = sga_request_tokens(e, q.fid.data(), q.acq.data(), q.prio.data(), q.ts.data(), k,
+                                reinterpret_cast<sga_token_result *>(q.out.data()));
+        for (uint64_t j = 0; j < k; ++j) {
+            sga::TokenQueue::Slot &sl = q.ring[(h + j) & (sga::TokenQueue::kCap - 1)];
+            if (rc == SGA_OK) {
+                sl.result = q.out[j];
+            } else {  // TokenResultStatus.FAIL (-1) in the status byte
+                sga_token_result r{};
+                r.status = -1;
+                std::memcpy(&sl.result, &r, sizeof(r));
+            }
+            sl.seq.store(h + j + 2, std::memory_order_release);
+        }
+        q.head = h + k;
+    }
+    q.combining.store(false, std::memory_order_release);
+    return rc;
+}
+
+int sga_poll(sga_engine *e, uint64_t ticket, sga_token_result *out) {
+    if (!e || !out) return SGA_EINVAL;
+    sga::TokenQueue &q = e->impl.tq;
+    sga::TokenQueue::Slot &sl = q.ring[ticket & (sga::TokenQueue::kCap - 1)];
+    for (int pass = 0; pass < 2; ++pass) {
+        const uint64_t s = sl.seq.load(std::memory_order_acquire);
+        if (s == ticket + 2) {
+            std::memcpy(out, &sl.result, sizeof(*out));
+            sl.seq.store(ticket + sga::TokenQueue::kCap, std::memory_order_release);
+            return SGA_OK;
+        }
+        if (s != ticket + 1) return SGA_EINVAL;  // not a live ticket
+        if (pass == 0) (void)combine_round(e);
+    }
+    return SGA_EAGAIN;
+}
+
+int sga_request_token_one(sga_engine *e, int64_t flow_id, int32_t acquire, uint8_t prioritized, int64_t ts,
+                          sga_token_result *out) {
+    if (!e || !out) return SGA_EINVAL;
+    uint64_t t = 0;
+    int rc = sga_token_submit(e, flow_id, acquire, prioritized, ts, &t);
+    if (rc != SGA_OK) return rc;
+    for (int spin = 0;; ++spin) {
+        rc = sga_poll(e, t, out);
+        if (rc != SGA_EAGAIN) return rc;
+        if (spin > 16) std::this_thread::yield();
+    }
 }
 
 int sga_cluster_metric_sums(sga_engine *e, int64_t flow_id, int64_t now, int64_t *out7) {

@@ -470,3 +470,49 @@ def test_pipelined_device_batches_match_sync(eng_mod):
                "wait_in_ms": ((r >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.uint16).view(np.int16).astype(np.int32)}
         assert_same(got, o, f[sel], ts[sel], f"async batch {b}")
     H.lib().orc_cluster_free(oh)
+
+
+def test_coalescing_queue_threads_equal_ticket_order(eng_mod):
+    """sga_token_submit / sga_poll from 8 threads at once (the Netty worker pattern of
+    FlowRequestProcessor.java:43): every request is decided once, and the decisions and the rules'
+    metrics equal the oracle replaying the requests one by one in ticket order."""
+    import threading
+    c = eng_mod
+    rng = np.random.default_rng(77)
+    rules = {"default": random_rules(rng, 0, ids=range(1, 41))}
+    eng = make_engine(c, max_batch=1 << 12)
+    engine_rules(c, eng, rules)
+    svc = c.DefaultTokenService(eng)
+    n_thr, per = 8, 1500
+    got = [[] for _ in range(n_thr)]
+
+    def worker(k):
+        r = np.random.default_rng(1000 + k)
+        for i in range(per):
+            fid = int(r.integers(1, 45))  # some ids without a rule
+            acq = int(r.integers(1, 3))
+            pr = bool(r.random() < 0.1)
+            now = T0 + i  # each thread's clock moves forward; threads interleave
+            t = svc.submit(fid, acq, pr, now)
+            res = None
+            while res is None:
+                res = svc.poll(t)
+            got[k].append((t, fid, acq, pr, now, res))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(n_thr)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    allr = sorted(x for g in got for x in g)
+    assert len(allr) == n_thr * per and len({x[0] for x in allr}) == len(allr)
+    oh = oracle_cluster(rules)
+    L = H.lib()
+    for t, fid, acq, pr, now, res in allr:
+        o = L.orc_cluster_request_token(oh, fid, acq, 1 if pr else 0, now)
+        assert (res.status, res.remaining, res.wait_in_ms) == (o.status, o.remaining, o.wait_in_ms), (t, fid, now)
+    assert_metrics(c, eng, oh, range(1, 41), T0 + per)
+    L.orc_cluster_free(oh)
+    one = svc.request_token(1, 1, False, T0 + 10_000)
+    assert one.status in (0, 1)
+    eng.close()
