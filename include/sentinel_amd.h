@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define SGA_ABI_VERSION 2
+#define SGA_ABI_VERSION 3
 
 /* error codes (negated errno values) */
 #define SGA_OK 0
@@ -354,6 +354,16 @@ typedef struct sga_flow_rule {
     int32_t warm_up_period_sec;    /* default 10 */
     int32_t max_queueing_time_ms;  /* default 500 */
     int32_t strategy;              /* STRATEGY_DIRECT 0 only */
+    /* FlowRule.clusterMode (FlowRuleChecker.passClusterCheck, FlowRuleChecker.java:168-230): the
+     * rule asks the token service; with the embedded server (sga_set_cluster_server) that is this
+     * engine's cluster rules (sga_load_cluster_flow_rules, keyed by flowId) */
+    int32_t cluster_mode;
+    int32_t cluster_fallback;      /* ClusterFlowConfig.fallbackToLocalWhenFail (default 1) */
+    int64_t cluster_flow_id;       /* ClusterFlowConfig.flowId (> 0 for a valid cluster rule) */
+    int32_t cluster_sample_count;  /* ClusterFlowConfig.sampleCount / windowIntervalMs / strategy: */
+    int32_t cluster_window_ms;     /*   validity only (FlowRuleUtil.checkClusterField) */
+    int32_t cluster_strategy;
+    int32_t reserved;
 } sga_flow_rule;
 
 /* ParamFlowRule, PF/slots/block/flow/param/ParamFlowRule.java:45-83 */
@@ -395,6 +405,14 @@ typedef struct sga_node_view {
 
 int sga_flow_set_resources(sga_engine *e, uint32_t n_resources);
 int sga_load_flow_rules(sga_engine *e, const sga_flow_rule *rules, size_t n);
+/* ClusterStateManager for the local path's cluster-mode FlowRules (FlowRuleChecker.pickClusterService):
+ * 0 = neither client nor server (cluster-mode rules fall back: fallbackToLocalOrPass), 1 = embedded
+ * token server -- the rule's flowId is decided by this engine's cluster path in event order
+ * (DefaultTokenService.requestToken, then applyTokenResult: OK pass, SHOULD_WAIT pass after waitInMs,
+ * BLOCKED block, NO_RULE_EXISTS / BAD_REQUEST / FAIL / TOO_MANY_REQUEST fall back).  A cluster
+ * flowId must belong to one resource's rules, and its namespace must have no GlobalRequestLimiter
+ * (-ENOSYS otherwise). */
+int sga_set_cluster_server(sga_engine *e, int32_t mode);
 int sga_load_param_rules(sga_engine *e, const sga_param_rule *rules, size_t n);
 int sga_load_degrade_rules(sga_engine *e, const sga_degrade_rule *rules, size_t n);
 

@@ -58,6 +58,8 @@ typedef struct flow_res {
     orc_node *node;  /* ClusterNode of the resource (ClusterBuilderSlot.java:82-110) */
     orc_ctrl **ctrl; /* rules' raters in FlowRuleComparator order */
     int nctrl;
+    int32_t *cmode, *cfallback; /* per rule: clusterMode, fallbackToLocalWhenFail */
+    int64_t *cflow;             /* per rule: ClusterFlowConfig.flowId */
     orc_prule **prule;  /* ParamFlowRuleManager rules of the resource, list order */
     int nprule;
     orc_pmap *pthreads; /* ParameterMetric.threadCountMap[0] */
@@ -80,6 +82,8 @@ struct orc_flow {
     flow_res *res;
     orc_node *entry; /* Constants.ENTRY_NODE: inbound traffic of every resource */
     orc_sys sys;
+    struct orc_cluster *server; /* embedded token server (cluster-mode rules), or NULL */
+    int cluster_mode;           /* 1: the server decides; 0: no token service */
 };
 
 /* helpers implemented in sentinel_oracle.c / oracle_ext.c */

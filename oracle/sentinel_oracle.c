@@ -598,6 +598,9 @@ void orc_flow_free(orc_flow *f) {
     for (uint32_t i = 0; i < f->n; i++) {
         for (int k = 0; k < f->res[i].nctrl; k++) orc_ctrl_free(f->res[i].ctrl[k]);
         free(f->res[i].ctrl);
+        free(f->res[i].cmode);
+        free(f->res[i].cfallback);
+        free(f->res[i].cflow);
         orc_node_free(f->res[i].node);
         orc_flow_res_free_ext(&f->res[i]);
     }
@@ -609,6 +612,12 @@ void orc_flow_free(orc_flow *f) {
 /* FlowRuleUtil.isValidRule (local, non-cluster), FlowRuleUtil.java:176-235 */
 static int flow_rule_valid(const orc_flow_rule *r) {
     if (!(r->count >= 0 && r->grade >= 0 && r->strategy >= 0 && r->control_behavior >= 0)) return 0;
+    if (r->cluster_mode) { /* FlowRuleUtil.checkClusterField / checkClusterConcurrentField, :197-240 */
+        if (r->cluster_flow_id <= 0) return 0;                                   /* validClusterRuleId */
+        if (!(r->cluster_sample_count > 0 && r->cluster_window_ms > 0 &&
+              r->cluster_window_ms % r->cluster_sample_count == 0)) return 0;      /* isWindowConfigValid */
+        if (r->grade == ORC_GRADE_QPS && r->cluster_strategy != 0) return 0;      /* NORMAL only */
+    }
     if (r->grade == ORC_GRADE_QPS) {
         if (r->strategy != 0) return 0; /* engine supports DIRECT only (RELATE/CHAIN need refResource) */
         switch (r->control_behavior) {
@@ -629,7 +638,12 @@ int orc_flow_load_rules(orc_flow *f, const orc_flow_rule *rules, size_t n) {
     for (uint32_t i = 0; i < f->n; i++) {
         for (int k = 0; k < f->res[i].nctrl; k++) orc_ctrl_free(f->res[i].ctrl[k]);
         free(f->res[i].ctrl);
+        free(f->res[i].cmode);
+        free(f->res[i].cfallback);
+        free(f->res[i].cflow);
         f->res[i].ctrl = NULL;
+        f->res[i].cmode = f->res[i].cfallback = NULL;
+        f->res[i].cflow = NULL;
         f->res[i].nctrl = 0;
     }
     int valid = 0;
@@ -638,6 +652,12 @@ int orc_flow_load_rules(orc_flow *f, const orc_flow_rule *rules, size_t n) {
         if (r->resource >= f->n || !flow_rule_valid(r)) continue;
         flow_res *fr = &f->res[r->resource];
         fr->ctrl = (orc_ctrl **)realloc(fr->ctrl, sizeof(orc_ctrl *) * (size_t)(fr->nctrl + 1));
+        fr->cmode = (int32_t *)realloc(fr->cmode, sizeof(int32_t) * (size_t)(fr->nctrl + 1));
+        fr->cfallback = (int32_t *)realloc(fr->cfallback, sizeof(int32_t) * (size_t)(fr->nctrl + 1));
+        fr->cflow = (int64_t *)realloc(fr->cflow, sizeof(int64_t) * (size_t)(fr->nctrl + 1));
+        fr->cmode[fr->nctrl] = r->cluster_mode ? 1 : 0;
+        fr->cfallback[fr->nctrl] = r->cluster_fallback ? 1 : 0;
+        fr->cflow[fr->nctrl] = r->cluster_flow_id;
         fr->ctrl[fr->nctrl++] = orc_ctrl_new(r->control_behavior, r->grade, r->count, r->warm_up_period_sec,
                                              r->max_queueing_time_ms, f->cold_factor);
         valid++;
@@ -646,6 +666,11 @@ int orc_flow_load_rules(orc_flow *f, const orc_flow_rule *rules, size_t n) {
 }
 
 orc_node *orc_flow_node(orc_flow *f, uint32_t resource) { return resource < f->n ? f->res[resource].node : NULL; }
+
+void orc_flow_set_cluster(orc_flow *f, orc_cluster *server, int mode) {
+    f->server = server;
+    f->cluster_mode = mode;
+}
 
 /* FlowSlot.checkFlow (FlowSlot.java:161-172, FlowRuleChecker.java:44-60; DIRECT +
  * default limitApp selects the ClusterNode, FlowRuleChecker.java:118-166):
@@ -657,6 +682,22 @@ int orc_flow_rule_check(orc_flow *f, uint32_t resource, int64_t now, int acquire
     *wait_ms = 0;
     for (int k = 0; k < fr->nctrl; k++) {
         int64_t w = 0;
+        if (fr->cmode && fr->cmode[k]) {
+            /* FlowRuleChecker.passClusterCheck (:168-188): pickClusterService -> requestToken ->
+             * applyTokenResult (:203-230); no service -> fallbackToLocalOrPass (:190-198) */
+            int status = -1; /* TokenResultStatus.FAIL stands for "no service" (both fall back) */
+            int32_t tw = 0;
+            if (f->server && f->cluster_mode == 1) {
+                const orc_token_result r = orc_cluster_request_token(f->server, fr->cflow[k], acquire, prioritized, now);
+                status = r.status;
+                tw = r.wait_in_ms;
+            }
+            if (status == 0) continue;                      /* OK */
+            if (status == 2) { total_wait += tw; continue; } /* SHOULD_WAIT: sleep, then pass */
+            if (status == 1) return ORC_BLOCK_FLOW;         /* BLOCKED */
+            if (status != 3 && status != -4 && status != -1 && status != -2) return ORC_BLOCK_FLOW; /* default */
+            if (!fr->cfallback[k]) continue;                /* fallbackToLocalOrPass: pass */
+        }
         int d = orc_ctrl_can_pass(fr->ctrl[k], fr->node, now, acquire, prioritized, &w);
         if (d == ORC_BLOCK_FLOW) return ORC_BLOCK_FLOW;
         if (d == ORC_PASS_WAIT) {

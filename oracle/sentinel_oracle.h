@@ -129,6 +129,14 @@ typedef struct orc_flow_rule {
     int32_t warm_up_period_sec;
     int32_t max_queueing_time_ms;
     int32_t strategy;      /* only DIRECT(0) is supported by the engine */
+    /* FlowRule.clusterMode + ClusterFlowConfig (FlowRuleChecker.passClusterCheck, :168-230) */
+    int32_t cluster_mode;
+    int32_t cluster_fallback;      /* fallbackToLocalWhenFail */
+    int64_t cluster_flow_id;
+    int32_t cluster_sample_count;  /* validity only (FlowRuleUtil.checkClusterField) */
+    int32_t cluster_window_ms;
+    int32_t cluster_strategy;
+    int32_t reserved;
 } orc_flow_rule;
 
 typedef struct orc_flow orc_flow;
@@ -137,6 +145,11 @@ void orc_flow_free(orc_flow *f);
 /* FlowRuleManager.loadRules: validity filter, rater regenerated (controller
  * state reset), node statistics kept.  Returns #valid rules. */
 int orc_flow_load_rules(orc_flow *f, const orc_flow_rule *rules, size_t n);
+/* ClusterStateManager for cluster-mode rules (FlowRuleChecker.pickClusterService): mode 0 = neither
+ * client nor server (fallbackToLocalOrPass), 1 = embedded token server `server` (its
+ * DefaultTokenService decides the rule's flowId). */
+typedef struct orc_cluster orc_cluster;
+void orc_flow_set_cluster(orc_flow *f, orc_cluster *server, int mode);
 /* SphU.entry(resource, type, acquire) -> decision (ORC_*), wait ms */
 int orc_flow_entry(orc_flow *f, uint32_t resource, int64_t now, int acquire, int prioritized, int64_t *wait_ms);
 /* Entry.exit for a PASSED entry: rt = now - createTimestamp supplied by caller */

@@ -52,7 +52,10 @@ class SgaTokenResult(C.Structure):
 class SgaFlowRule(C.Structure):
     _fields_ = [("resource", C.c_uint32), ("grade", C.c_int32), ("count", C.c_double),
                 ("control_behavior", C.c_int32), ("warm_up_period_sec", C.c_int32),
-                ("max_queueing_time_ms", C.c_int32), ("strategy", C.c_int32)]
+                ("max_queueing_time_ms", C.c_int32), ("strategy", C.c_int32),
+                ("cluster_mode", C.c_int32), ("cluster_fallback", C.c_int32), ("cluster_flow_id", C.c_int64),
+                ("cluster_sample_count", C.c_int32), ("cluster_window_ms", C.c_int32),
+                ("cluster_strategy", C.c_int32), ("reserved", C.c_int32)]
 
 
 class SgaParamRule(C.Structure):
@@ -142,6 +145,7 @@ SIGNATURES = {
     "sga_load_system_rules": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     "sga_set_system_status": (C.c_int, [C.c_void_p, C.c_double, C.c_double]),
     "sga_load_flow_rules": (C.c_int, [C.c_void_p, C.POINTER(SgaFlowRule), C.c_size_t]),
+    "sga_set_cluster_server": (C.c_int, [C.c_void_p, C.c_int32]),
     "sga_load_param_rules": (C.c_int, [C.c_void_p, C.POINTER(SgaParamRule), C.c_size_t]),
     "sga_load_degrade_rules": (C.c_int, [C.c_void_p, C.POINTER(SgaDegradeRule), C.c_size_t]),
     "sga_submit_events": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,

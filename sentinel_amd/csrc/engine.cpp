@@ -87,6 +87,10 @@ struct Engine {
     std::string err;
     std::mutex mu;
     TokenQueue tq;
+    // cluster-mode FlowRules of the local path: ClusterStateManager mode (sga_set_cluster_server) and
+    // a generation of the cluster rule set their slots were resolved against
+    int32_t cluster_server = 0;
+    uint64_t cluster_gen = 1;
 
     // ---- cluster rules (host mirror)
     std::vector<SlotHost> slots;
@@ -691,6 +695,7 @@ int sga_load_cluster_flow_rules(sga_engine *e, const char *ns, const sga_cluster
     if (!ns || !*ns || (n && !rules)) return SGA_EINVAL;  // AssertUtil.notEmpty(namespace)
     return guarded(e, [&](Engine &g) {
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        ++g.cluster_gen;  // cluster-mode local rules re-resolve their slots
         const int nsi = g.ns_index(ns, true);
         std::vector<uint32_t> fresh;
         if (n == 0) {  // clearAndResetRulesFor: rules dropped, metrics kept (:281-296)
@@ -809,6 +814,7 @@ int sga_set_namespace_limit(sga_engine *e, const char *ns, double max_allowed_qp
     if (!ns || !*ns || !(max_allowed_qps >= 0)) return SGA_EINVAL;  // AssertUtil.isTrue(qpsAllowed >= 0)
     return guarded(e, [&](Engine &g) {
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        ++g.cluster_gen;  // cluster-mode local rules re-resolve their slots
         const int i = g.ns_index(ns, true);
         if (g.d_lim.n < g.nss.size()) g.d_lim.grow(std::max<size_t>(g.nss.size(), 2 * g.d_lim.n), g.stream);
         if (!g.nss[i].has_limit) {
@@ -1493,6 +1499,15 @@ int sga_flow_set_resources(sga_engine *e, uint32_t n_resources) {
     });
 }
 
+int sga_set_cluster_server(sga_engine *e, int32_t mode) {
+    if (mode != 0 && mode != 1) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        g.cluster_server = mode;
+        ++g.cluster_gen;
+        return SGA_OK;
+    });
+}
+
 int sga_load_flow_rules(sga_engine *e, const sga_flow_rule *rules, size_t n) {
     if (n && !rules) return SGA_EINVAL;
     return guarded(e, [&](Engine &g) {
@@ -1523,6 +1538,24 @@ int sga_submit_events(sga_engine *e, const uint8_t *kind, const uint32_t *resour
     if (n && (!kind || !resource || !ts || !acquire || !decision)) return SGA_EINVAL;
     return guarded(e, [&](Engine &g) {
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        g.flow.cluster_on = g.cluster_server == 1 ? 1 : 0;
+        if (g.flow.has_cluster_rules) {
+            g.flow.cluster_st = g.state();
+            const int rc = g.flow.resolve_cluster(
+                [&](int64_t fid) -> int32_t {
+                    auto it = g.slot_of.find(fid);
+                    if (it == g.slot_of.end()) return -1;
+                    const SlotHost &h = g.slots[it->second];
+                    if (!h.active) return -1;
+                    if (h.ns >= 0 && g.nss[h.ns].has_limit) return -2;
+                    return (int32_t)it->second;
+                },
+                g.cluster_gen);
+            if (rc != SGA_OK) {
+                g.err = "cluster-mode flow rule: flowId shared by two resources or namespace with a request limiter";
+                return rc;
+            }
+        }
         return g.flow.submit(kind, resource, ts, acquire, flags, rt, param, n, decision, wait_ms);
     });
 }

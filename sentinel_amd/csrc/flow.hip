@@ -18,6 +18,7 @@
 // Java predicate, all exits of the run applied as one segmented reduction.  Every other run is
 // replayed event by event with a device restatement of the whole slot chain.
 #include "flow.hpp"
+#include "cluster_exact.hpp"
 
 #include <algorithm>
 #include <cstring>
@@ -579,7 +580,35 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
     // FlowSlot
     for (uint32_t k = 0; k < R.n_rules; ++k) {
         int64_t w = 0;
-        const int8_t d = rater_can_pass(c, m.rules[k], node, t, acquire, prio, &w);
+        FlowRuleDev &fr = m.rules[k];
+        if (fr.cluster) {
+            // FlowRuleChecker.passClusterCheck (:168-188): the token service decides; the embedded
+            // server is this engine's cluster path (DefaultTokenService.requestToken), in event order
+            int8_t ts = TRS_FAIL;  // no service: fallbackToLocalOrPass
+            int32_t tw = 0;
+            if (c.st.cluster_on) {
+                if (acquire <= 0) {
+                    ts = TRS_BAD_REQUEST;
+                } else if (fr.cslot < 0) {
+                    ts = TRS_NO_RULE_EXISTS;
+                } else {
+                    const uint64_t res = request_exact(c.st.cst, (uint32_t)fr.cslot, t, acquire, prio, 0);
+                    ts = (int8_t)(res >> 48);
+                    tw = (int16_t)(res >> 32);
+                }
+            }
+            if (ts == TRS_OK) continue;  // applyTokenResult (:203-230)
+            if (ts == TRS_SHOULD_WAIT) {  // Thread.sleep(waitInMs), then pass
+                total_wait += tw;
+                continue;
+            }
+            if (ts == TRS_BLOCKED) {
+                node_add(c, node, t, MB_BLOCK, acquire);
+                return D_BLOCK_FLOW;
+            }
+            if (!fr.cfallback) continue;  // fallbackToLocalOrPass: the rule is not activated
+        }
+        const int8_t d = rater_can_pass(c, fr, node, t, acquire, prio, &w);
         if (d == D_BLOCK_FLOW) {
             node_add(c, node, t, MB_BLOCK, acquire);
             return D_BLOCK_FLOW;
@@ -2054,7 +2083,51 @@ FlowState FlowEngine::state() const {
     s.tmask = d_ttab.n ? (uint32_t)(d_ttab.n - 1) : 0;
     s.nres = nres;
     s.overflow = d_overflow.p;
+    s.cst = cluster_st;
+    s.cluster_on = cluster_on;
     return s;
+}
+
+__global__ void k_set_cslot(FlowRuleDev *rules, const uint32_t *idx, const int32_t *slot, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) rules[idx[i]].cslot = slot[i];
+}
+
+// The token server's slot of every cluster-mode rule's flowId (-1: no active cluster rule), written
+// into the device rules without touching their controller state.  A flowId shared by the cluster
+// rules of two resources would be decided by two lanes at once: refused.
+int FlowEngine::resolve_cluster(const std::function<int32_t(int64_t)> &slot_of_flow, uint64_t gen) {
+    if (!has_cluster_rules || gen == cluster_resolved_gen) return 0;
+    std::vector<uint32_t> idx;
+    std::vector<int32_t> slot;
+    std::vector<std::pair<int64_t, uint32_t>> owner;
+    for (uint32_t r = 0; r < nres; ++r)
+        for (uint32_t k = 0; k < h_res[r].n_rules; ++k) {
+            FlowRuleDev &d = h_rules[h_res[r].rule_off + k];
+            if (!d.cluster) continue;
+            const int32_t sl = slot_of_flow(d.cflow);
+            if (sl == -2) return SGA_ENOSYS;  // the flowId's namespace has a GlobalRequestLimiter
+            d.cslot = sl;
+            idx.push_back(h_res[r].rule_off + k);
+            slot.push_back(sl);
+            owner.emplace_back(d.cflow, r);
+        }
+    std::sort(owner.begin(), owner.end());
+    for (size_t i = 1; i < owner.size(); ++i)
+        if (owner[i].first == owner[i - 1].first && owner[i].second != owner[i - 1].second) return SGA_ENOSYS;
+    if (!idx.empty()) {
+        DevBuf<uint32_t> di;
+        DevBuf<int32_t> ds;
+        di.alloc(idx.size());
+        ds.alloc(slot.size());
+        SGA_HIP_CHECK(hipMemcpyAsync(di.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(ds.p, slot.data(), slot.size() * 4, hipMemcpyHostToDevice, stream));
+        hipLaunchKernelGGL(k_set_cslot, dim3((unsigned)((idx.size() + kT - 1) / kT)), dim3(kT), 0, stream, d_rules.p,
+                           di.p, ds.p, (uint32_t)idx.size());
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+    cluster_resolved_gen = gen;
+    return 0;
 }
 
 int FlowEngine::set_resources(uint32_t n) {
@@ -2086,7 +2159,9 @@ void FlowEngine::upload_res() {
         R.fast &= 2u;  // bit1 (a thread-count map exists) is sticky
         if (R.n_rules == 1 && R.n_prules == 0 && R.n_cbs == 0 && !(R.fast & 2u)) {
             const FlowRuleDev &fr = h_rules[R.rule_off];
-            if (fr.grade == 1 && (fr.behavior == 0 || fr.behavior == 1)) R.fast = 1;
+            if (fr.cluster) {
+                // cluster-mode rule: every entry asks the token server (per-event replay)
+            } else if (fr.grade == 1 && (fr.behavior == 0 || fr.behavior == 1)) R.fast = 1;
             else if (fr.grade == 1 && fr.behavior == 2) R.fast = 4;  // pacing only: k_lflows register loop
         }
     }
@@ -2104,6 +2179,10 @@ int FlowEngine::load_flow_rules(const sga_flow_rule *rules, size_t n) {
         const sga_flow_rule &r = rules[i];
         if (r.resource >= nres) continue;
         bool ok = r.count >= 0 && r.grade >= 0 && r.strategy >= 0 && r.control_behavior >= 0 && r.strategy == 0;
+        if (ok && r.cluster_mode) {  // FlowRuleUtil.checkClusterField / checkClusterConcurrentField (:197-240)
+            ok = r.cluster_flow_id > 0 && r.cluster_sample_count > 0 && r.cluster_window_ms > 0 &&
+                 r.cluster_window_ms % r.cluster_sample_count == 0 && (r.grade != 1 || r.cluster_strategy == 0);
+        }
         if (ok && r.grade == 1) {
             switch (r.control_behavior) {
             case 1: ok = r.warm_up_period_sec > 0; break;
@@ -2123,6 +2202,10 @@ int FlowEngine::load_flow_rules(const sga_flow_rule *rules, size_t n) {
         d.max_queue = r.max_queueing_time_ms;
         d.cold_factor = cfg.cold_factor;
         d.latest_passed = -1;
+        d.cluster = r.cluster_mode ? 1 : 0;
+        d.cfallback = r.cluster_fallback ? 1 : 0;
+        d.cflow = r.cluster_flow_id;
+        d.cslot = -1;
         if (d.behavior == 1 || d.behavior == 3) {  // WarmUpController.construct, :83-106
             d.warning_token = j_d2i((double)r.warm_up_period_sec * r.count) / (cfg.cold_factor - 1);
             d.max_token = d.warning_token + j_d2i(2 * r.warm_up_period_sec * r.count / (1.0 + cfg.cold_factor));
@@ -2132,7 +2215,10 @@ int FlowEngine::load_flow_rules(const sga_flow_rule *rules, size_t n) {
         valid++;
     }
     h_rules.clear();
+    has_cluster_rules = false;
+    cluster_resolved_gen = ~0ull;
     for (uint32_t r = 0; r < nres; ++r) {
+        for (const FlowRuleDev &d : per[r]) has_cluster_rules |= d.cluster != 0;
         h_res[r].rule_off = (uint32_t)h_rules.size();
         h_res[r].n_rules = (uint32_t)per[r].size();
         h_rules.insert(h_rules.end(), per[r].begin(), per[r].end());

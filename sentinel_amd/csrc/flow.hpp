@@ -1,5 +1,8 @@
 // Local path (StatisticSlot + ParamFlowSlot + FlowSlot + DegradeSlot) -- device engine.
 #pragma once
+#include <functional>
+
+#include "cluster.hpp"
 #include "../../include/sentinel_amd.h"
 #include "common.hpp"
 #include "radix_sort.hpp"
@@ -31,6 +34,11 @@ struct FlowRuleDev {    // one rater (TrafficShapingController) + its FlowRule f
     int64_t latest_passed;   // RateLimiterController / WarmUpRateLimiterController latestPassedTime
     int64_t stored_tokens;   // WarmUpController.storedTokens
     int64_t last_filled;     // WarmUpController.lastFilledTime
+    // FlowRule.clusterMode (FlowRuleChecker.passClusterCheck): the token server's rule slot for the
+    // rule's flowId (-1: no such cluster rule -> NO_RULE_EXISTS), resolved on the host before a batch
+    int32_t cluster, cfallback;
+    int64_t cflow;
+    int32_t cslot, cpad;
 };
 
 struct ParamRuleDev {
@@ -90,6 +98,9 @@ struct FlowState {
     uint32_t pmask, tmask;
     uint32_t nres;
     uint32_t *overflow;  // set when a param table is full
+    // embedded cluster token server for cluster-mode FlowRules (sga_set_cluster_server 1)
+    ClusterState cst;
+    int32_t cluster_on;
 };
 
 struct FlowScratch {
@@ -163,6 +174,13 @@ struct FlowEngine {
     }
     void release() { print_heavy_prof(); }
     FlowState state() const;
+    // cluster-mode FlowRules: the engine's cluster state and ClusterStateManager mode, set before
+    // each batch (sga_set_cluster_server); resolve_cluster fills every cluster rule's slot
+    ClusterState cluster_st{};
+    int32_t cluster_on = 0;
+    bool has_cluster_rules = false;
+    uint64_t cluster_resolved_gen = ~0ull;
+    int resolve_cluster(const std::function<int32_t(int64_t)> &slot_of_flow, uint64_t gen);
     int set_resources(uint32_t n);
     int load_flow_rules(const sga_flow_rule *r, size_t n);
     int load_param_rules(const sga_param_rule *r, size_t n);

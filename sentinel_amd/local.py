@@ -242,12 +242,33 @@ class LocalSentinel:
         return _lib.load().sga_circuit_breaker_state(self.engine.handle, rid, k)
 
 
+class ClusterStateManager:
+    """ClusterStateManager (CORE/cluster/ClusterStateManager.java) as the local path sees it:
+    CLUSTER_SERVER = the embedded token server is this engine (sga_set_cluster_server 1);
+    CLUSTER_NOT_STARTED = no token service, cluster-mode rules fall back.  The client mode (a
+    remote token server over the network) is outside the decision path."""
+    CLUSTER_NOT_STARTED, CLUSTER_SERVER = 0, 1
+
+    def __init__(self, sentinel: "LocalSentinel"):
+        self.s = sentinel
+
+    def set_to_server(self):
+        check(_lib.load().sga_set_cluster_server(self.s.engine.handle, 1), self.s.engine.handle, "setToServer")
+
+    def stop(self):
+        check(_lib.load().sga_set_cluster_server(self.s.engine.handle, 0), self.s.engine.handle, "stop")
+
+
 class FlowRuleManager:
     def __init__(self, sentinel: LocalSentinel):
         self.s = sentinel
 
     def load_rules(self, rules: List[FlowRule]) -> int:
-        rules = [r for r in rules if not r.cluster_mode and r.resource in self.s.ids]
+        """FlowRuleManager.loadRules.  Cluster-mode rules ask the token service when checked
+        (FlowRuleChecker.passClusterCheck): with ClusterStateManager set to server the engine's own
+        cluster rules (ClusterFlowRuleManager on the same Engine) decide their flowId, otherwise
+        they fall back (fallbackToLocalWhenFail: the local rater, else pass)."""
+        rules = [r for r in rules if r.resource in self.s.ids]
         arr = (SgaFlowRule * max(1, len(rules)))()
         for i, r in enumerate(rules):
             a = arr[i]
@@ -259,6 +280,14 @@ class FlowRuleManager:
             a.max_queueing_time_ms = r.max_queueing_time_ms
             # non-default limitApp / RELATE / CHAIN are not served by the engine: rejected as invalid
             a.strategy = r.strategy if r.limit_app == RuleConstant.LIMIT_APP_DEFAULT else -1
+            if r.cluster_mode:
+                cc = r.cluster_config
+                a.cluster_mode = 1
+                a.cluster_fallback = 1 if cc is None or cc.fallback_to_local_when_fail else 0
+                a.cluster_flow_id = -1 if cc is None or cc.flow_id is None else int(cc.flow_id)
+                a.cluster_sample_count = 0 if cc is None else cc.sample_count
+                a.cluster_window_ms = 0 if cc is None else cc.window_interval_ms
+                a.cluster_strategy = 0 if cc is None else cc.strategy
         return check(_lib.load().sga_load_flow_rules(self.s.engine.handle, arr, len(rules)), self.s.engine.handle,
                      "FlowRuleManager.loadRules")
 

@@ -44,6 +44,7 @@ class ClusterFlowConfig:
     strategy: int = ClusterRuleConstant.FLOW_CLUSTER_STRATEGY_NORMAL
     resource_timeout: int = 2000     # ClusterFlowConfig.resourceTimeout (concurrency tokens)
     client_offline_time: int = 2000  # ClusterFlowConfig.clientOfflineTime
+    fallback_to_local_when_fail: bool = True  # ClusterFlowConfig.fallbackToLocalWhenFail
 
 
 @dataclass

@@ -26,7 +26,10 @@ TOKEN_STATUS = {"BAD_REQUEST": -4, "TOO_MANY_REQUEST": -2, "FAIL": -1, "OK": 0, 
 class OrcFlowRule(C.Structure):
     _fields_ = [("resource", C.c_uint32), ("grade", C.c_int32), ("count", C.c_double),
                 ("control_behavior", C.c_int32), ("warm_up_period_sec", C.c_int32),
-                ("max_queueing_time_ms", C.c_int32), ("strategy", C.c_int32)]
+                ("max_queueing_time_ms", C.c_int32), ("strategy", C.c_int32),
+                ("cluster_mode", C.c_int32), ("cluster_fallback", C.c_int32), ("cluster_flow_id", C.c_int64),
+                ("cluster_sample_count", C.c_int32), ("cluster_window_ms", C.c_int32),
+                ("cluster_strategy", C.c_int32), ("reserved", C.c_int32)]
 
 
 class OrcClusterRule(C.Structure):
@@ -100,6 +103,7 @@ def lib():
         "orc_flow_new": (P, [U32, C.c_int]),
         "orc_flow_free": (None, [P]),
         "orc_flow_load_rules": (C.c_int, [P, C.POINTER(OrcFlowRule), C.c_size_t]),
+        "orc_flow_set_cluster": (None, [P, P, C.c_int]),
         "orc_flow_entry": (C.c_int, [P, U32, I64, C.c_int, C.c_int, C.POINTER(I64)]),
         "orc_flow_exit": (None, [P, U32, I64, I64, C.c_int, C.c_int]),
         "orc_flow_replay": (None, [P, C.c_size_t, P, P, P, P, P, P, P, P]),
@@ -184,6 +188,12 @@ def flow_rules_array(rules):
         arr[i].warm_up_period_sec = r.get("warm_up_period_sec", 10)
         arr[i].max_queueing_time_ms = r.get("max_queueing_time_ms", 500)
         arr[i].strategy = r.get("strategy", 0)
+        arr[i].cluster_mode = 1 if r.get("cluster_mode") else 0
+        arr[i].cluster_fallback = 1 if r.get("cluster_fallback", True) else 0
+        arr[i].cluster_flow_id = r.get("cluster_flow_id", 0)
+        arr[i].cluster_sample_count = r.get("cluster_sample_count", 10)
+        arr[i].cluster_window_ms = r.get("cluster_window_ms", 1000)
+        arr[i].cluster_strategy = r.get("cluster_strategy", 0)
     return arr
 
 

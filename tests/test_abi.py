@@ -46,7 +46,7 @@ def test_python_mirror_binds_every_symbol():
     L = _lib.load()
     decl = {s for s in declared_symbols() if not s.startswith("sgaw_")}
     assert decl <= set(_lib.SIGNATURES), decl - set(_lib.SIGNATURES)
-    assert L.sga_abi_version() == 2
+    assert L.sga_abi_version() == 3
 
 
 def test_struct_layouts_match_header():

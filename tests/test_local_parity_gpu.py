@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from tests import local_trace as lt
+from tests import oracle_harness as H
 
 pytestmark = pytest.mark.gpu
 
@@ -30,10 +31,17 @@ def _load(s, flow=None, param=None, degrade=None):
     from sentinel_amd.local import DegradeRuleManager, FlowRuleManager, ParamFlowRuleManager
     from sentinel_amd.rules import DegradeRule, FlowRule, ParamFlowItem, ParamFlowRule
     if flow is not None:
+        from sentinel_amd.rules import ClusterFlowConfig
         FlowRuleManager(s).load_rules([FlowRule(resource=f"r{r['resource']}", count=r["count"], grade=r.get("grade", 1),
                                                 control_behavior=r.get("control_behavior", 0),
                                                 warm_up_period_sec=r.get("warm_up_period_sec", 10),
-                                                max_queueing_time_ms=r.get("max_queueing_time_ms", 500))
+                                                max_queueing_time_ms=r.get("max_queueing_time_ms", 500),
+                                                cluster_mode=bool(r.get("cluster_mode", False)),
+                                                cluster_config=ClusterFlowConfig(
+                                                    flow_id=r.get("cluster_flow_id"),
+                                                    sample_count=r.get("cluster_sample_count", 10),
+                                                    window_interval_ms=r.get("cluster_window_ms", 1000),
+                                                    fallback_to_local_when_fail=r.get("cluster_fallback", True)))
                                        for r in flow])
     if param is not None:
         ParamFlowRuleManager(s).load_rules([
@@ -330,4 +338,60 @@ def test_edge_cases():
     ok.exit(T0 + 9)
     v = s.node("r1", T0 + 9)
     assert v.total_exception == 1 and v.total_success == 1 and v.avg_rt == 7.0 and v.cur_thread_num == 0
+    eng.close()
+
+
+@pytest.mark.parametrize("server", [1, 0])
+def test_cluster_mode_flow_rules(server):
+    """FlowSlot with cluster-mode rules (FlowRuleChecker.passClusterCheck / applyTokenResult /
+    fallbackToLocalOrPass, FlowRuleChecker.java:168-230).  server=1: the embedded token server is the
+    same engine's cluster path -- OK passes, SHOULD_WAIT passes after waitInMs, BLOCKED blocks,
+    NO_RULE_EXISTS (a flowId without a cluster rule) falls back to the local rater or passes;
+    server=0: no token service, every cluster rule falls back.  Decisions, wait times, node views and
+    the cluster rules' metrics equal the oracle (whose FlowSlot asks its own token server)."""
+    from sentinel_amd import cluster as CL
+    from sentinel_amd.local import ClusterStateManager
+    from tests.test_cluster_parity_gpu import assert_metrics, engine_rules, oracle_cluster
+    rng = np.random.default_rng(91 + server)
+    n_res = 12
+    flow, crules = [], []
+    for r in range(n_res):
+        fid = 1000 + r
+        if r % 3 == 0:
+            flow.append({"resource": r, "count": float(rng.choice([5, 20]))})
+        else:
+            flow.append({"resource": r, "count": float(rng.choice([3, 10])), "cluster_mode": True,
+                         "cluster_flow_id": fid, "cluster_fallback": r % 3 == 1,
+                         "control_behavior": int(rng.choice([0, 2])), "max_queueing_time_ms": 300})
+            if r % 4 != 2:  # the others have no cluster rule: NO_RULE_EXISTS -> fallback
+                crules.append({"flow_id": fid, "count": float(rng.choice([4, 15, 40])), "threshold_type": 1})
+        if r % 5 == 4:  # a second, local rule after the cluster one
+            flow.append({"resource": r, "count": 25.0})
+    rules = {"default": crules}
+    L = lt.lib()
+    gen = lt.Oracle(n_res, flow)
+    ohg = oracle_cluster(rules)
+    L.orc_flow_set_cluster(gen.h, ohg, server)
+    st = lt.generate(gen, n_res, n_entries=12000, seed=17 + server, t0=T0, gap_mean=0.5, prio_pct=0.2,
+                     acq_max=2, rt_max=30)
+    gen.close()
+    orc = lt.Oracle(n_res, flow)
+    oh = oracle_cluster(rules)
+    L.orc_flow_set_cluster(orc.h, oh, server)
+    exp = orc.replay(st)
+    eng, s = _sentinel(n_res, 1 << 14)
+    engine_rules(CL, eng, rules)
+    _load(s, flow)
+    if server:
+        ClusterStateManager(s).set_to_server()
+    got = _submit(s, st)
+    _assert_same(st, got, exp, f"cluster-mode rules, server={server}")
+    t_end = int(st["ts"].max())
+    _assert_nodes(s, orc, n_res, t_end)
+    assert_metrics(CL, eng, oh, [c["flow_id"] for c in crules], t_end)
+    d = exp[0][st["kind"] == 0]
+    assert (d == 0).any() and (d == 1).any()
+    H.lib().orc_cluster_free(oh)
+    H.lib().orc_cluster_free(ohg)
+    orc.close()
     eng.close()
