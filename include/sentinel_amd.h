@@ -341,6 +341,9 @@ int sga_rls_should_rate_limit(sga_engine *e, const uint32_t *desc_offsets, size_
 #define SGA_EV_ERROR 2u      /* exit of an entry that recorded a business error (Tracer.traceEntry) */
 #define SGA_EV_HAS_PARAM 4u  /* args[0] present (param field) */
 #define SGA_EV_INBOUND 8u    /* EntryType.IN (on entries and their exits): Constants.ENTRY_NODE + SystemSlot */
+#define SGA_EV_PARAM_LIST 16u /* with HAS_PARAM: args[0] is a Collection / array; param = offset << 32 | count
+                               * into sga_submit_events_ex's param_values (every element is checked,
+                               * ParamFlowChecker.passLocalCheck, and counted by ParameterMetric) */
 
 /* resource id of Constants.ENTRY_NODE ("__total_inbound_traffic__") in sga_query_node and metric rows */
 #define SGA_ENTRY_NODE 0xFFFFFFFFu
@@ -424,6 +427,12 @@ int sga_load_degrade_rules(sga_engine *e, const sga_degrade_rule *rules, size_t 
 int sga_submit_events(sga_engine *e, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
                       const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
                       size_t n, int8_t *decision, int32_t *wait_ms);
+/* sga_submit_events with Collection / array arguments: events flagged SGA_EV_PARAM_LIST take their
+ * values from param_values[param >> 32 .. (param >> 32) + (param & 0xffffffff)). */
+int sga_submit_events_ex(sga_engine *e, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
+                         const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
+                         size_t n, const uint64_t *param_values, size_t n_values, int8_t *decision,
+                         int32_t *wait_ms);
 int sga_query_node(sga_engine *e, uint32_t resource, int64_t now, sga_node_view *out);
 
 /* SystemRule (CORE/slots/system/SystemRule.java:43-50); negative = not set. */

@@ -431,21 +431,31 @@ void orc_flow_res_free_ext(flow_res *fr) {
 }
 
 /* ---------------------------------------------------------------- slot chain */
-static void param_thread_add(flow_res *fr, int has_param, uint64_t param) { /* ParameterMetric.addThreadCount */
+/* ParameterMetric.addThreadCount / decreaseThreadCount (ParameterMetric.java:125-230): every element
+ * of a Collection / array argument, else the single value. */
+static void param_thread_add(const orc_flow *f, flow_res *fr, int has_param, uint64_t param) {
     if (!fr->pthreads || !has_param) return;
-    int64_t *c = pm_find(fr->pthreads, param);
-    if (c) (*c)++;
-    else pm_put(fr->pthreads, param, 1);
+    const uint64_t *v = f->plist ? f->plist : &param;
+    const uint32_t nv = f->plist ? f->plist_n : 1;
+    for (uint32_t i = 0; i < nv; i++) {
+        int64_t *c = pm_find(fr->pthreads, v[i]);
+        if (c) (*c)++;
+        else pm_put(fr->pthreads, v[i], 1);
+    }
 }
 
-static void param_thread_dec(flow_res *fr, int has_param, uint64_t param) { /* ParameterMetric.decreaseThreadCount */
+static void param_thread_dec(const orc_flow *f, flow_res *fr, int has_param, uint64_t param) {
     if (!fr->pthreads || !has_param) return;
-    int64_t *c = pm_find(fr->pthreads, param);
-    if (!c) {
-        pm_put(fr->pthreads, param, 0); /* putIfAbsent(value, new AtomicInteger()) */
-        return;
+    const uint64_t *v = f->plist ? f->plist : &param;
+    const uint32_t nv = f->plist ? f->plist_n : 1;
+    for (uint32_t i = 0; i < nv; i++) {
+        int64_t *c = pm_find(fr->pthreads, v[i]);
+        if (!c) {
+            pm_put(fr->pthreads, v[i], 0); /* putIfAbsent(value, new AtomicInteger()) */
+            continue;
+        }
+        if (--(*c) <= 0) pm_remove(fr->pthreads, v[i]);
     }
-    if (--(*c) <= 0) pm_remove(fr->pthreads, param);
 }
 
 /* CtSph.entryWithPriority -> StatisticSlot.entry (StatisticSlot.java:64-145) around
@@ -466,17 +476,24 @@ int orc_flow_entry_p(orc_flow *f, uint32_t resource, int64_t now, int acquire, i
         int idx = p->r.param_idx;
         if (idx < 0) idx = (-idx <= nargs) ? nargs + idx : -idx; /* applyRealParamIdx */
         if (nargs <= idx) continue;                               /* args.length <= paramIdx -> pass */
-        int64_t tc = 0;
-        if (idx == 0 && fr->pthreads) {
-            int64_t *c = pm_find(fr->pthreads, param);
-            tc = c ? *c : 0;
+        /* passLocalCheck (ParamFlowChecker.java:79-106): a Collection / array argument passes when
+         * every element passes, checked in order (the elements before a failing one keep their
+         * token updates) */
+        const uint64_t *vals = f->plist ? f->plist : &param;
+        const uint32_t nv = f->plist ? f->plist_n : 1;
+        for (uint32_t q = 0; q < nv; q++) {
+            int64_t tc = 0;
+            if (idx == 0 && fr->pthreads) {
+                int64_t *c = pm_find(fr->pthreads, vals[q]);
+                tc = c ? *c : 0;
+            }
+            int64_t w = 0;
+            if (!orc_prule_pass_single(p, vals[q], acquire, now, tc, &w)) {
+                orc_node_increase_block_qps(fr->node, now, acquire);
+                return ORC_BLOCK_PARAM;
+            }
+            total_wait += w;
         }
-        int64_t w = 0;
-        if (!orc_prule_pass_single(p, param, acquire, now, tc, &w)) {
-            orc_node_increase_block_qps(fr->node, now, acquire);
-            return ORC_BLOCK_PARAM;
-        }
-        total_wait += w;
     }
     /* FlowSlot */
     int64_t w = 0;
@@ -487,7 +504,7 @@ int orc_flow_entry_p(orc_flow *f, uint32_t resource, int64_t now, int acquire, i
     }
     if (d == ORC_PASS_WAIT) { /* PriorityWaitException: thread++ and entry callbacks only */
         orc_node_increase_thread_num(fr->node);
-        param_thread_add(fr, has_param, param);
+        param_thread_add(f, fr, has_param, param);
         *wait_ms = w;
         return ORC_PASS_WAIT;
     }
@@ -510,7 +527,7 @@ int orc_flow_entry_p(orc_flow *f, uint32_t resource, int64_t now, int acquire, i
     }
     orc_node_increase_thread_num(fr->node);
     orc_node_add_pass_request(fr->node, now, acquire);
-    param_thread_add(fr, has_param, param);
+    param_thread_add(f, fr, has_param, param);
     *wait_ms = total_wait;
     return ORC_PASS;
 }
@@ -525,7 +542,7 @@ void orc_flow_exit_p(orc_flow *f, uint32_t resource, int64_t now, int64_t rt, in
     orc_node_add_rt_and_success(n, now, rt, count);
     orc_node_decrease_thread_num(n);
     if (error) orc_node_increase_exception_qps(n, now, count);
-    param_thread_dec(fr, has_param, param);
+    param_thread_dec(f, fr, has_param, param);
     for (int k = 0; k < fr->ncb; k++) cb_on_complete(fr->cb[k], now, rt, error);
 }
 
@@ -642,6 +659,25 @@ void orc_flow_exit_x(orc_flow *f, uint32_t resource, int64_t now, int64_t rt, in
 }
 
 orc_node *orc_flow_entry_node(orc_flow *f) { return f->entry; }
+
+/* As orc_flow_replay_p, with flags bit 4 (SGA_EV_PARAM_LIST): args[0] is a Collection / array whose
+ * values are pvals[param >> 32 .. (param >> 32) + (param & 0xffffffff)). */
+void orc_flow_replay_pl(orc_flow *f, size_t n, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
+                        const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
+                        const uint64_t *pvals, int8_t *decision, int32_t *wait_ms) {
+    for (size_t i = 0; i < n; i++) {
+        const uint8_t fl = flags ? flags[i] : 0;
+        if ((fl & 16) && (fl & 4)) {
+            f->plist = pvals + (param[i] >> 32);
+            f->plist_n = (uint32_t)(param[i] & 0xffffffffu);
+        }
+        orc_flow_replay_p(f, 1, kind ? kind + i : NULL, resource + i, ts + i, acquire + i, flags ? flags + i : NULL,
+                          rt ? rt + i : NULL, param ? param + i : NULL, decision ? decision + i : NULL,
+                          wait_ms ? wait_ms + i : NULL);
+        f->plist = NULL;
+        f->plist_n = 0;
+    }
+}
 
 /* flags: bit 0 prioritized, bit 1 error, bit 2 has_param, bit 3 inbound (EntryType.IN) */
 void orc_flow_replay_p(orc_flow *f, size_t n, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,

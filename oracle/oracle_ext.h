@@ -81,6 +81,10 @@ orc_node *orc_flow_entry_node(orc_flow *f);
 void orc_flow_replay_p(orc_flow *f, size_t n, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
                        const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
                        int8_t *decision, int32_t *wait_ms);
+/* flags bit 4: args[0] is a Collection / array (pvals[param >> 32 ..], param & 0xffffffff values) */
+void orc_flow_replay_pl(orc_flow *f, size_t n, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
+                        const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
+                        const uint64_t *pvals, int8_t *decision, int32_t *wait_ms);
 
 /* Standalone ParamFlowChecker.passSingleValueCheck on one rule (KATs): the rule's
  * maps persist in the handle. */

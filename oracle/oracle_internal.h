@@ -84,6 +84,10 @@ struct orc_flow {
     orc_sys sys;
     struct orc_cluster *server; /* embedded token server (cluster-mode rules), or NULL */
     int cluster_mode;           /* 1: the server decides; 0: no token service */
+    /* args[0] of the current event when it is a Collection / array (ParamFlowChecker.passLocalCheck
+     * checks every element): its values, or NULL for a single value */
+    const uint64_t *plist;
+    uint32_t plist_n;
 };
 
 /* helpers implemented in sentinel_oracle.c / oracle_ext.c */

@@ -1535,6 +1535,13 @@ int sga_load_degrade_rules(sga_engine *e, const sga_degrade_rule *rules, size_t 
 int sga_submit_events(sga_engine *e, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
                       const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
                       size_t n, int8_t *decision, int32_t *wait_ms) {
+    return sga_submit_events_ex(e, kind, resource, ts, acquire, flags, rt, param, n, nullptr, 0, decision, wait_ms);
+}
+
+int sga_submit_events_ex(sga_engine *e, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
+                         const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
+                         size_t n, const uint64_t *param_values, size_t n_values, int8_t *decision,
+                         int32_t *wait_ms) {
     if (n && (!kind || !resource || !ts || !acquire || !decision)) return SGA_EINVAL;
     return guarded(e, [&](Engine &g) {
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
@@ -1556,7 +1563,8 @@ int sga_submit_events(sga_engine *e, const uint8_t *kind, const uint32_t *resour
                 return rc;
             }
         }
-        return g.flow.submit(kind, resource, ts, acquire, flags, rt, param, n, decision, wait_ms);
+        return g.flow.submit(kind, resource, ts, acquire, flags, rt, param, n, decision, wait_ms, param_values,
+                             n_values);
     });
 }
 

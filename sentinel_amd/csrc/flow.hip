@@ -551,12 +551,34 @@ __device__ __forceinline__ ResMem res_global(const Ctx &c, uint32_t r, const Res
     return ResMem{c.st.node + (size_t)r * kNodeWords, c.st.rules + R.rule_off, c.st.cbs + R.cb_off};
 }
 
+// args[0] of an event: one value, or the elements of a Collection / array (SGA_EV_PARAM_LIST)
+struct PArgs {
+    const uint64_t *v;
+    uint32_t n;
+};
+
+// ParameterMetric.addThreadCount / decreaseThreadCount over every element (ParameterMetric.java:125-230)
+__device__ void param_threads(const Ctx &c, uint32_t r, const PArgs &pa, int delta) {
+    for (uint32_t q = 0; q < pa.n; ++q) {
+        PEntry *te = ptab_get(c.st.ttab, c.st.tmask, r + 1, pa.v[q], true, c.st.overflow);
+        if (!te) continue;
+        if (delta > 0) {
+            te->a = (te->a == kPAbsent ? 0 : te->a) + 1;
+        } else if (te->a == kPAbsent) {
+            te->a = 0;  // putIfAbsent(value, new AtomicInteger())
+        } else if (--te->a <= 0) {
+            te->a = kPAbsent;  // remove(value)
+        }
+    }
+}
+
 __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t t, int acquire, bool prio,
-                              bool has_param, uint64_t param, int64_t *wait_ms) {
+                              bool has_param, uint64_t param, int64_t *wait_ms, PArgs pa = PArgs{nullptr, 0}) {
     const ResDev R = c.res ? *c.res : c.st.res[r];
     int64_t *node = m.node;
     *wait_ms = 0;
     int64_t total_wait = 0;
+    if (!pa.v) pa = PArgs{&param, 1u};
     // ParamFlowSlot (ParamFlowSlot.java:65-92): args = [param] or []
     const int nargs = has_param ? 1 : 0;
     for (uint32_t k = 0; k < R.n_prules; ++k) {
@@ -564,18 +586,23 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
         int idx = p.param_idx;
         if (idx < 0) idx = (-idx <= nargs) ? nargs + idx : -idx;
         if (nargs <= idx) continue;
-        int64_t tc = 0;
-        if (idx == 0 && (R.fast & 2u)) {
-            PEntry *te = ptab_get(c.st.ttab, c.st.tmask, r + 1, param, false, c.st.overflow);
-            tc = (te && te->a != kPAbsent) ? te->a : 0;
+        // passLocalCheck (ParamFlowChecker.java:79-106): a Collection / array passes when every
+        // element passes, in order (elements before a failing one keep their token updates)
+        for (uint32_t q = 0; q < pa.n; ++q) {
+            const uint64_t v = pa.v[q];
+            int64_t tc = 0;
+            if (idx == 0 && (R.fast & 2u)) {
+                PEntry *te = ptab_get(c.st.ttab, c.st.tmask, r + 1, v, false, c.st.overflow);
+                tc = (te && te->a != kPAbsent) ? te->a : 0;
+            }
+            int64_t w = 0;
+            const bool ok = c.pre_param ? (w = c.pre_wait, c.pre_param == 1) : param_pass(c, p, v, acquire, t, tc, &w);
+            if (!ok) {
+                node_add(c, node, t, MB_BLOCK, acquire);
+                return D_BLOCK_PARAM;
+            }
+            total_wait += w;
         }
-        int64_t w = 0;
-        const bool ok = c.pre_param ? (w = c.pre_wait, c.pre_param == 1) : param_pass(c, p, param, acquire, t, tc, &w);
-        if (!ok) {
-            node_add(c, node, t, MB_BLOCK, acquire);
-            return D_BLOCK_PARAM;
-        }
-        total_wait += w;
     }
     // FlowSlot
     for (uint32_t k = 0; k < R.n_rules; ++k) {
@@ -615,10 +642,7 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
         }
         if (d == D_PASS_WAIT) {
             node[kNodeThreads] += 1;
-            if (has_param && (R.fast & 2u)) {
-                PEntry *te = ptab_get(c.st.ttab, c.st.tmask, r + 1, param, true, c.st.overflow);
-                if (te) te->a = (te->a == kPAbsent ? 0 : te->a) + 1;
-            }
+            if (has_param && (R.fast & 2u)) param_threads(c, r, pa, 1);
             *wait_ms = w;
             return D_PASS_WAIT;
         }
@@ -631,39 +655,32 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
     }
     node[kNodeThreads] += 1;
     node_add(c, node, t, MB_PASS, acquire);
-    if (has_param && (R.fast & 2u)) {
-        PEntry *te = ptab_get(c.st.ttab, c.st.tmask, r + 1, param, true, c.st.overflow);
-        if (te) te->a = (te->a == kPAbsent ? 0 : te->a) + 1;
-    }
+    if (has_param && (R.fast & 2u)) param_threads(c, r, pa, 1);
     *wait_ms = total_wait;
     return D_PASS;
 }
 
 __device__ void chain_exit(const Ctx &c, uint32_t r, const ResMem &m, int64_t t, int64_t rt, int count, bool error,
-                           bool has_param, uint64_t param) {
+                           bool has_param, uint64_t param, PArgs pa = PArgs{nullptr, 0}) {
     const ResDev R = c.res ? *c.res : c.st.res[r];
     int64_t *node = m.node;
     node_add_rt_success(c, node, t, rt, count);
     node[kNodeThreads] -= 1;
     if (error) node_add(c, node, t, MB_EXC, count);
-    if (has_param && (R.fast & 2u)) {  // ParameterMetric.decreaseThreadCount
-        PEntry *te = ptab_get(c.st.ttab, c.st.tmask, r + 1, param, true, c.st.overflow);
-        if (te) {
-            if (te->a == kPAbsent) te->a = 0;
-            else if (--te->a <= 0) te->a = kPAbsent;  // remove(value)
-        }
-    }
+    if (!pa.v) pa = PArgs{&param, 1u};
+    if (has_param && (R.fast & 2u)) param_threads(c, r, pa, -1);  // ParameterMetric.decreaseThreadCount
     for (uint32_t k = 0; k < R.n_cbs; ++k) cb_on_complete(m.cbs[k], t, rt, error);
 }
 
 __device__ __forceinline__ int8_t chain_entry(const Ctx &c, uint32_t r, int64_t t, int acquire, bool prio,
-                                              bool has_param, uint64_t param, int64_t *wait_ms) {
-    return chain_entry(c, r, res_global(c, r, c.st.res[r]), t, acquire, prio, has_param, param, wait_ms);
+                                              bool has_param, uint64_t param, int64_t *wait_ms,
+                                              PArgs pa = PArgs{nullptr, 0}) {
+    return chain_entry(c, r, res_global(c, r, c.st.res[r]), t, acquire, prio, has_param, param, wait_ms, pa);
 }
 
 __device__ __forceinline__ void chain_exit(const Ctx &c, uint32_t r, int64_t t, int64_t rt, int count, bool error,
-                                           bool has_param, uint64_t param) {
-    chain_exit(c, r, res_global(c, r, c.st.res[r]), t, rt, count, error, has_param, param);
+                                           bool has_param, uint64_t param, PArgs pa = PArgs{nullptr, 0}) {
+    chain_exit(c, r, res_global(c, r, c.st.res[r]), t, rt, count, error, has_param, param, pa);
 }
 
 // ------------------------------------------------------------------ SystemSlot / ENTRY_NODE
@@ -727,7 +744,7 @@ __global__ void k_lseq(FlowState st, int64_t max_rt, SysDev sys, const uint8_t *
                        const uint32_t *__restrict__ resource, const uint32_t *__restrict__ ts_off, int64_t ts_base,
                        const int32_t *__restrict__ acquire, const uint8_t *__restrict__ flags,
                        const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in, uint32_t n,
-                       int8_t *decision, int32_t *wait_ms) {
+                       int8_t *decision, int32_t *wait_ms, const uint64_t *__restrict__ pvals) {
     if (threadIdx.x || blockIdx.x) return;
     const Ctx c{st, max_rt};
     for (uint32_t i = 0; i < n; ++i) {
@@ -739,8 +756,10 @@ __global__ void k_lseq(FlowState st, int64_t max_rt, SysDev sys, const uint8_t *
         const uint8_t fl = flags[i];
         const bool in = (fl & SGA_EV_INBOUND) != 0, hp = (fl & SGA_EV_HAS_PARAM) != 0;
         const int a = (int)((uint32_t)acquire[i] & 0x7FFFFFFFu);
+        PArgs pa{nullptr, 0};
+        if (hp && (fl & SGA_EV_PARAM_LIST) && pvals) pa = PArgs{pvals + (param_in[i] >> 32), (uint32_t)param_in[i]};
         if (kind[i] == 1) {
-            chain_exit(c, r, t, rt_in[i], a, (fl & SGA_EV_ERROR) != 0, hp, param_in[i]);
+            chain_exit(c, r, t, rt_in[i], a, (fl & SGA_EV_ERROR) != 0, hp, param_in[i], pa);
             if (in) entry_node_after_exit(c, t, rt_in[i], a, (fl & SGA_EV_ERROR) != 0);
             continue;
         }
@@ -750,7 +769,7 @@ __global__ void k_lseq(FlowState st, int64_t max_rt, SysDev sys, const uint8_t *
             node_add(c, st.node + (size_t)r * kNodeWords, t, MB_BLOCK, a);  // StatisticSlot: increaseBlockQps
             d = D_BLOCK_SYSTEM;
         } else {
-            d = chain_entry(c, r, t, a, (fl & SGA_EV_PRIORITIZED) != 0, hp, param_in[i], &w);
+            d = chain_entry(c, r, t, a, (fl & SGA_EV_PRIORITIZED) != 0, hp, param_in[i], &w, pa);
         }
         if (in) entry_node_after_entry(c, t, a, d);
         decision[i] = d;
@@ -2475,9 +2494,26 @@ void print_heavy_prof() {
 
 int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int64_t *ts, const int32_t *acquire,
                        const uint8_t *flags, const int64_t *rt, const uint64_t *param, size_t n, int8_t *decision,
-                       int32_t *wait_ms) {
+                       int32_t *wait_ms, const uint64_t *pvals, size_t npvals) {
     if (!nres) return SGA_EINVAL;
     if (n == 0) return 0;
+    // Collection / array arguments (SGA_EV_PARAM_LIST): the value array goes to the device once;
+    // chunks holding such events are replayed in arrival order by one lane (k_lseq)
+    bool any_list = false;
+    for (size_t i = 0; flags && param && i < n && !any_list; ++i) {
+        if ((flags[i] & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) {
+            if (!pvals || (param[i] >> 32) + (param[i] & 0xFFFFFFFFu) > npvals) return SGA_EINVAL;
+            any_list = true;
+        }
+    }
+    for (size_t i = 0; any_list && i < n; ++i)
+        if ((flags[i] & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM) &&
+            (param[i] >> 32) + (param[i] & 0xFFFFFFFFu) > npvals)
+            return SGA_EINVAL;
+    if (any_list) {
+        if (d_pvals.n < std::max<size_t>(npvals, 1)) d_pvals.alloc(std::max<size_t>(npvals, 1));
+        if (npvals) SGA_HIP_CHECK(hipMemcpyAsync(d_pvals.p, pvals, npvals * 8, hipMemcpyHostToDevice, stream));
+    }
     const size_t cap = cfg.max_batch;
     if (cap > F_IDX) return SGA_ERANGE;
     if (scratch_cap < cap) {
@@ -2557,7 +2593,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         }
         off.resize(m);
         for (size_t i = 0; i < m; ++i) off[i] = (uint32_t)(ts[b + i] - lo);
-        if (const int rc = ensure_maps(m)) return rc;
+        if (const int rc = ensure_maps(m + (any_list ? npvals : 0))) return rc;
         SGA_HIP_CHECK(hipMemcpyAsync(d_kind.p, kind + b, m, hipMemcpyHostToDevice, stream));
         SGA_HIP_CHECK(hipMemcpyAsync(d_resid.p, resource + b, m * 4, hipMemcpyHostToDevice, stream));
         SGA_HIP_CHECK(hipMemcpyAsync(d_ts.p, off.data(), m * 4, hipMemcpyHostToDevice, stream));
@@ -2575,12 +2611,14 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         SGA_HIP_CHECK(hipMemsetAsync(d_overflow.p, 0, 4, stream));
         const FlowState st = state();
         const uint32_t nb = (uint32_t)((m + kT - 1) / kT);
-        bool has_in = false;
+        bool has_in = false, has_list = false;
         for (size_t i = 0; flags && i < m && !has_in; ++i) has_in = (flags[b + i] & SGA_EV_INBOUND) && resource[b + i] < nres;
-        if (has_in && sys.check) {  // SystemSlot: one lane in arrival order
+        for (size_t i = 0; any_list && i < m && !has_list; ++i)
+            has_list = (flags[b + i] & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM);
+        if ((has_in && sys.check) || has_list) {  // SystemSlot / collection arguments: one lane in arrival order
             hipLaunchKernelGGL(k_lseq, dim3(1), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sys, d_kind.p,
                                d_resid.p, d_ts.p, lo, d_acq.p, d_flags.p, d_rt.p, d_param.p, (uint32_t)m, d_dec.p,
-                               d_wait.p);
+                               d_wait.p, has_list ? d_pvals.p : nullptr);
             SGA_HIP_CHECK(hipGetLastError());
             SGA_HIP_CHECK(hipMemcpyAsync(decision + b, d_dec.p, m, hipMemcpyDeviceToHost, stream));
             if (wait_ms) SGA_HIP_CHECK(hipMemcpyAsync(wait_ms + b, d_wait.p, m * 4, hipMemcpyDeviceToHost, stream));

@@ -188,7 +188,8 @@ struct FlowEngine {
     void upload_res();
     int submit(const uint8_t *kind, const uint32_t *resource, const int64_t *ts, const int32_t *acquire,
                const uint8_t *flags, const int64_t *rt, const uint64_t *param, size_t n, int8_t *decision,
-               int32_t *wait_ms);
+               int32_t *wait_ms, const uint64_t *pvals = nullptr, size_t npvals = 0);
+    DevBuf<uint64_t> d_pvals;  // values of Collection / array arguments (SGA_EV_PARAM_LIST)
     int query(uint32_t resource, int64_t now, sga_node_view *out);
     int cb_state(uint32_t resource, uint32_t k);
     int metrics(int64_t now, sga_metric_node *out, size_t cap, size_t *n);

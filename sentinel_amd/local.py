@@ -174,7 +174,9 @@ class LocalSentinel:
         return self.ids[name]
 
     # ---- batched form: the engine's native interface
-    def submit(self, kind, resource, ts, acquire, flags=None, rt=None, param=None):
+    def submit(self, kind, resource, ts, acquire, flags=None, rt=None, param=None, param_values=None):
+        """Events in arrival order.  param_values: the values of Collection / array arguments
+        (events flagged SGA_EV_PARAM_LIST = 16 carry param = offset << 32 | count into it)."""
         k = np.ascontiguousarray(kind, dtype=np.uint8)
         r = np.ascontiguousarray(resource, dtype=np.uint32)
         t = np.ascontiguousarray(ts, dtype=np.int64)
@@ -190,10 +192,13 @@ class LocalSentinel:
                 raise ValueError("event arrays differ in length")
         dec = np.zeros(n, dtype=np.int8)
         wait = np.zeros(n, dtype=np.int32)
-        rc = _lib.load().sga_submit_events(
+        vals = np.ascontiguousarray(param_values, dtype=np.uint64) if param_values is not None else None
+        rc = _lib.load().sga_submit_events_ex(
             self.engine.handle, k.ctypes.data, r.ctypes.data, t.ctypes.data, a.ctypes.data,
             f.ctypes.data if f is not None else None, rtv.ctypes.data if rtv is not None else None,
-            pv.ctypes.data if pv is not None else None, n, dec.ctypes.data, wait.ctypes.data)
+            pv.ctypes.data if pv is not None else None, n,
+            vals.ctypes.data if vals is not None and len(vals) else None, len(vals) if vals is not None else 0,
+            dec.ctypes.data, wait.ctypes.data)
         check(rc, self.engine.handle, "submitEvents")
         return dec, wait
 

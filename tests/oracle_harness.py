@@ -161,6 +161,7 @@ def lib():
         "orc_flow_exit_p": (None, [P, U32, I64, I64, C.c_int, C.c_int, C.c_int, C.c_uint64]),
         "orc_flow_cb_state": (C.c_int, [P, U32, C.c_int]),
         "orc_flow_replay_p": (None, [P, C.c_size_t, P, P, P, P, P, P, P, P, P]),
+        "orc_flow_replay_pl": (None, [P, C.c_size_t, P, P, P, P, P, P, P, P, P, P]),
         "orc_prule_new": (P, [C.POINTER(OrcParamRule)]),
         "orc_prule_free": (None, [P]),
         "orc_prule_pass_single": (C.c_int, [P, C.c_uint64, C.c_int, I64, I64, C.POINTER(I64)]),

@@ -395,3 +395,60 @@ def test_cluster_mode_flow_rules(server):
     H.lib().orc_cluster_free(ohg)
     orc.close()
     eng.close()
+
+
+def test_collection_and_array_parameters():
+    """ParamFlowChecker.passLocalCheck with a Collection / array argument (ParamFlowChecker.java:79-106):
+    every element is checked in order and the entry passes only if all pass (the elements before a
+    failing one keep their token updates); ParameterMetric counts a thread for every element and the
+    exit releases them (ParameterMetric.java:125-230).  Lists of 0..4 values (SGA_EV_PARAM_LIST),
+    single values and entries without arguments are mixed over default, throttle and thread-grade
+    rules with hot items; decisions, waits and node views equal the oracle."""
+    rng = np.random.default_rng(61)
+    n_res, n = 16, 40000
+    param = []
+    for r in range(n_res):
+        k = r % 4
+        if k == 0:
+            param.append({"resource": r, "count": float(rng.integers(2, 20)), "hot": {3: 50, 7: 1}})
+        elif k == 1:
+            param.append({"resource": r, "count": float(rng.integers(2, 10)), "control_behavior": 2,
+                          "max_queueing_time_ms": int(rng.choice([0, 100]))})
+        elif k == 2:
+            param.append({"resource": r, "grade": 0, "count": float(rng.integers(1, 4)), "hot": {5: 2}})
+        else:
+            param.append({"resource": r, "count": float(rng.integers(5, 40)), "burst_count": 3,
+                          "duration_in_sec": int(rng.choice([1, 2]))})
+    res = rng.integers(0, n_res, size=n)
+    ts = T0 + np.sort(rng.integers(0, 20_000, size=n))
+    kind = rng.random(n)
+    flags = np.zeros(n, np.uint8)
+    pv = np.zeros(n, np.uint64)
+    values = []
+    for i in range(n):
+        if kind[i] < 0.35:  # a Collection / array argument
+            m = int(rng.integers(0, 5))
+            pv[i] = (len(values) << 32) | m
+            values.extend(int(x) for x in rng.integers(0, 12, size=m))
+            flags[i] = 4 | 16
+        elif kind[i] < 0.9:
+            pv[i] = int(rng.integers(0, 12))
+            flags[i] = 4
+    values = np.array(values, dtype=np.uint64)
+    gen = lt.Oracle(n_res, [], param)
+    st = lt.generate_windows(gen, res, ts, rng.integers(1, 3, size=n), flags, pv, rng.integers(2, 80, size=n),
+                             rng.random(n) < 0.05, window_ms=2, param_values=values)
+    gen.close()
+    orc = lt.Oracle(n_res, [], param)
+    exp = orc.replay(st)
+    eng, s = _sentinel(n_res, 1 << 14)
+    _load(s, param=param)
+    got = s.submit(st["kind"], st["resource"], st["ts"], st["acquire"], st["flags"], st["rt"], st["param"],
+                   param_values=st["param_values"])
+    _assert_same(st, got, exp, "collection parameters")
+    _assert_nodes(s, orc, n_res, int(st["ts"].max()))
+    d = exp[0][st["kind"] == 0]
+    lst = (st["flags"][st["kind"] == 0] & 16) != 0
+    assert (d[lst] == 2).any() and (d[lst] == 0).any()
+    orc.close()
+    eng.close()
