@@ -86,8 +86,13 @@ def main():
         t = torch.tensor([rank], dtype=torch.int64)
         if world > 1:
             dist.all_reduce(t)
-        print(json.dumps({"dry": True, "rank": rank, "world": world, "gpus": args.gpus, "rank_sum": int(t.item())}),
-              flush=True)
+        line = json.dumps({"dry": True, "rank": rank, "world": world, "gpus": args.gpus, "rank_sum": int(t.item())})
+        out_dir = os.environ.get("SGA_BENCH_DRY_OUT")
+        if out_dir:  # one file per rank: the ranks' stdout lines may interleave
+            with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as fh:
+                fh.write(line)
+        else:
+            print(line, flush=True)
         if world > 1:
             dist.destroy_process_group()
         return

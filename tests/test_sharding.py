@@ -144,13 +144,15 @@ def test_bench_gpus2_launches_two_ranks():
     import json
     import subprocess
     import sys
+    import tempfile
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, SGA_BENCH_DRY="1")
+    out = tempfile.mkdtemp()
+    env = dict(os.environ, SGA_BENCH_DRY="1", SGA_BENCH_DRY_OUT=out)
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    lines = [json.load(open(os.path.join(out, f))) for f in sorted(os.listdir(out))]
     assert sorted(d["rank"] for d in lines) == [0, 1]
     assert all(d["world"] == 2 and d["gpus"] == 2 and d["rank_sum"] == 1 for d in lines)
 
