@@ -1351,13 +1351,16 @@ struct KeyShared {
     WConst wcs[256];
     uint16_t cnt[kKeyWaves][kHot];  // per wave: hot requests so far per hot id
     uint32_t s_np[kKeyWaves], s_bd[kKeyWaves];
+    uint32_t hist0[2][256];         // per sort tile of the segment: the first radix digit's counts
 };
 template <int kPass, bool kDense>
 __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, const BatchScratch &sc,
                                         const int64_t *__restrict__ flow_id, const int32_t *__restrict__ acquire,
                                         const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off,
-                                        int64_t ts_base, uint32_t n, uint64_t *__restrict__ out, int dbg) {
+                                        int64_t ts_base, uint32_t n, uint64_t *__restrict__ out, int dbg,
+                                        int d0, uint32_t *__restrict__ hist, uint32_t ntiles) {
     WConst *wcs = sh.wcs;
+    const uint32_t dmask = (1u << d0) - 1u;
     auto &cnt = sh.cnt;
     uint32_t *s_np = sh.s_np, *s_bd = sh.s_bd;
     const uint32_t flags0 = sc.counters[CTL_FLAGS];
@@ -1367,6 +1370,7 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
     const uint64_t lt = lanemask_lt64(lane);
     if (kDense)
         for (int k = threadIdx.x; k < 256; k += kKeyThreads) wcs[k] = sc.wconst[k];  // window-length codes
+    for (int k = threadIdx.x; k < 2 * 256; k += kKeyThreads) (&sh.hist0[0][0])[k] = 0;
     if (nhot) {
         uint4 *cz = reinterpret_cast<uint4 *>(&cnt[0][0]);
         for (int k = threadIdx.x; k < (int)(sizeof(cnt) / 16); k += kKeyThreads) cz[k] = make_uint4(0, 0, 0, 0);
@@ -1524,7 +1528,10 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                 // cold elements, compacted in arrival order
                 const bool emit = kind == 1;
                 const uint64_t em = __ballot(emit);
-                if (emit) sc.el_tile[(size_t)ubase + nc + (uint32_t)__popcll(em & lt)] = el_pack(slot, bd6, p, a7, i);
+                if (emit) {
+                    sc.el_tile[(size_t)ubase + nc + (uint32_t)__popcll(em & lt)] = el_pack(slot, bd6, p, a7, i);
+                    if (d0) atomicAdd(&sh.hist0[wave >> 2][slot & dmask], 1u);
+                }
                 nc += (uint32_t)__popcll(em);
             }
         };
@@ -1565,66 +1572,70 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
         }
     }
     if (wflags) atomicOr(&sc.counters[CTL_FLAGS], wflags);
-    if (!nhot) {
-        if (lane == 0) sc.tile_nc[sub] = active ? nc : 0u;  // totals: k_hot_mode
-        return;
-    }
+    if (nhot) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) bdmax = max(bdmax, (uint32_t)__shfl_xor((int)bdmax, o, 64));
-    if (lane == 0) {
-        s_np[wave] = np;
-        s_bd[wave] = bdmax;
-    }
-    __syncthreads();
-    {  // per-wave counters -> exclusive prefixes over the waves (two hot ids per word: counts < 2^16)
-        uint32_t *cw = reinterpret_cast<uint32_t *>(&cnt[0][0]);
-        uint32_t *row = reinterpret_cast<uint32_t *>(sc.hcnt + (size_t)seg * kHot);
-        for (uint32_t k = threadIdx.x; k < (nhot + 1) / 2; k += kKeyThreads) {
-            uint32_t run = 0;
+        for (int o = 32; o > 0; o >>= 1) bdmax = max(bdmax, (uint32_t)__shfl_xor((int)bdmax, o, 64));
+        if (lane == 0) {
+            s_np[wave] = np;
+            s_bd[wave] = bdmax;
+        }
+        __syncthreads();
+        {  // per-wave counters -> exclusive prefixes over the waves (two hot ids per word: counts < 2^16)
+            uint32_t *cw = reinterpret_cast<uint32_t *>(&cnt[0][0]);
+            uint32_t *row = reinterpret_cast<uint32_t *>(sc.hcnt + (size_t)seg * kHot);
+            for (uint32_t k = threadIdx.x; k < (nhot + 1) / 2; k += kKeyThreads) {
+                uint32_t run = 0;
 #pragma unroll
-            for (int w = 0; w < kKeyWaves; ++w) {
-                const uint32_t v = cw[w * (kHot / 2) + k];
-                cw[w * (kHot / 2) + k] = run;
-                run += v;
+                for (int w = 0; w < kKeyWaves; ++w) {
+                    const uint32_t v = cw[w * (kHot / 2) + k];
+                    cw[w * (kHot / 2) + k] = run;
+                    run += v;
+                }
+                row[k] = run;  // this segment's count row
             }
-            row[k] = run;  // this segment's count row
+        }
+        if (threadIdx.x == 0) {  // reduced by k_hot_mode: thousands of same-address atomics would serialize
+            uint32_t a = 0, m = 0;
+            for (int w = 0; w < kKeyWaves; ++w) {
+                a += s_np[w];
+                m = max(m, s_bd[w]);
+            }
+            sc.seg_stat[2 * seg] = a;
+            sc.seg_stat[2 * seg + 1] = m;
+        }
+        __syncthreads();
+        if (active) {
+            // codes: in-wave ranks -> in-segment ranks; prioritized hot requests join the sub's elements
+            uint32_t code[kSubRounds];
+#pragma unroll
+            for (int r = 0; r < kSubRounds; ++r) code[r] = sc.hcode[min(ubase + (uint32_t)r * 64 + lane, n - 1)];
+#pragma unroll
+            for (int r = 0; r < ((dbg & 8) ? 0 : kSubRounds); ++r) {
+                const uint32_t i = ubase + (uint32_t)r * 64 + lane;
+                const uint32_t cd = code[r];
+                const bool hot = i < send && cd != kNoCode;
+                const uint32_t hid = cd & 0xFFFu;
+                const uint32_t r_seg = hot ? ((cd >> 12) & 0x1FFFu) + c[hid] : 0u;
+                const bool pr = hot && (cd >> 31);
+                if (hot && (wave || pr)) sc.hcode[i] = (cd & ~(0x1FFFu << 12)) | (r_seg << 12);
+                const uint64_t em = __ballot(pr);
+                if (pr) {
+                    sc.el_tile[(size_t)ubase + nc + (uint32_t)__popcll(em & lt)] =
+                        el_pack(st.nslots + 1 + hid, r_seg >> 7, 1u, r_seg & 127u, i);
+                    if (d0) atomicAdd(&sh.hist0[wave >> 2][(st.nslots + 1 + hid) & dmask], 1u);
+                }
+                nc += (uint32_t)__popcll(em);
+            }
         }
     }
-    if (threadIdx.x == 0) {  // reduced by k_hot_mode: thousands of same-address atomics would serialize
-        uint32_t a = 0, m = 0;
-        for (int w = 0; w < kKeyWaves; ++w) {
-            a += s_np[w];
-            m = max(m, s_bd[w]);
+    if (lane == 0) sc.tile_nc[sub] = active ? nc : 0u;  // totals: k_hot_mode
+    if (d0) {  // the sort's first-pass histogram rows of this segment's two tiles
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < (2u << d0); k += kKeyThreads) {
+            const uint32_t t = k >> d0, d = k & dmask, tile = seg * 2 + t;
+            if (tile < ntiles) hist[(size_t)d * ntiles + tile] = sh.hist0[t][d];
         }
-        sc.seg_stat[2 * seg] = a;
-        sc.seg_stat[2 * seg + 1] = m;
     }
-    __syncthreads();
-    if (!active) {
-        if (lane == 0) sc.tile_nc[sub] = 0;
-        return;
-    }
-    // codes: in-wave ranks -> in-segment ranks; prioritized hot requests join the sub's elements
-    uint32_t npos = nc;
-    uint32_t code[kSubRounds];
-#pragma unroll
-    for (int r = 0; r < kSubRounds; ++r) code[r] = sc.hcode[min(ubase + (uint32_t)r * 64 + lane, n - 1)];
-#pragma unroll
-    for (int r = 0; r < ((dbg & 8) ? 0 : kSubRounds); ++r) {
-        const uint32_t i = ubase + (uint32_t)r * 64 + lane;
-        const uint32_t cd = code[r];
-        const bool hot = i < send && cd != kNoCode;
-        const uint32_t hid = cd & 0xFFFu;
-        const uint32_t r_seg = hot ? ((cd >> 12) & 0x1FFFu) + c[hid] : 0u;
-        const bool pr = hot && (cd >> 31);
-        if (hot && (wave || pr)) sc.hcode[i] = (cd & ~(0x1FFFu << 12)) | (r_seg << 12);
-        const uint64_t em = __ballot(pr);
-        if (pr)
-            sc.el_tile[(size_t)ubase + npos + (uint32_t)__popcll(em & lt)] =
-                el_pack(st.nslots + 1 + hid, r_seg >> 7, 1u, r_seg & 127u, i);
-        npos += (uint32_t)__popcll(em);
-    }
-    if (lane == 0) sc.tile_nc[sub] = npos;
 }
 
 // Dense flowId table (the production layout): 4 waves per SIMD, two workgroups per CU.
@@ -1632,18 +1643,18 @@ template <int kPass>
 __global__ __launch_bounds__(kKeyThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_hot_key_dense(
     ClusterState st, BatchScratch sc, const int64_t *__restrict__ flow_id, const int32_t *__restrict__ acquire,
     const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off, int64_t ts_base, uint32_t n,
-    uint64_t *__restrict__ out, int dbg) {
+    uint64_t *__restrict__ out, int dbg, int d0, uint32_t *__restrict__ hist, uint32_t ntiles) {
     __shared__ KeyShared sh;
-    hot_key<kPass, true>(sh, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out, dbg);
+    hot_key<kPass, true>(sh, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out, dbg, d0, hist, ntiles);
 }
 // Hashed flowId table (sparse flowIds): the probe loop needs more registers.
 template <int kPass>
 __global__ __launch_bounds__(kKeyThreads) void k_hot_key_hash(
     ClusterState st, BatchScratch sc, const int64_t *__restrict__ flow_id, const int32_t *__restrict__ acquire,
     const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off, int64_t ts_base, uint32_t n,
-    uint64_t *__restrict__ out, int dbg) {
+    uint64_t *__restrict__ out, int dbg, int d0, uint32_t *__restrict__ hist, uint32_t ntiles) {
     __shared__ KeyShared sh;
-    hot_key<kPass, false>(sh, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out, dbg);
+    hot_key<kPass, false>(sh, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out, dbg, d0, hist, ntiles);
 }
 
 // The batch's path and element counts: sums over the compaction segments and the rank segments
@@ -2976,16 +2987,19 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(k_hot_precheck, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc, ts_off, ts_base, n);
     auto hka = st.dense_n ? k_hot_key_dense<0> : k_hot_key_hash<0>;
     auto hkb = st.dense_n ? k_hot_key_dense<1> : k_hot_key_hash<1>;
+    // the key kernels count the sort's first digit per tile as they write the elements
+    const int d0 = radix64_digit_bits(bits);
+    const uint32_t ntiles_sort = (uint32_t)radix64_tiles(n);
     hipLaunchKernelGGL(hka, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out,
-                       fz_debug());
+                       fz_debug(), d0, sc.radix.hist, ntiles_sort);
     hipLaunchKernelGGL(hkb, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out,
-                       fz_debug());
+                       fz_debug(), d0, sc.radix.hist, ntiles_sort);
     hipLaunchKernelGGL(k_hot_mode, dim3(1), dim3(1024), 0, s, sc, nseg * kKeyWaves, nseg);
     hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
     hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, s, sc, ngroups);
     hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
     const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
-                                        kSlotShift, bits, sc.radix, s, false);
+                                        kSlotShift, bits, sc.radix, s, true);
     const uint64_t *el = (np & 1) ? sc.el[0] : sc.el[1];
     const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
     hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el);
