@@ -433,6 +433,19 @@ int sga_submit_events_ex(sga_engine *e, const uint8_t *kind, const uint32_t *res
                          const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
                          size_t n, const uint64_t *param_values, size_t n_values, int8_t *decision,
                          int32_t *wait_ms);
+/* sga_submit_events_ex over DEVICE buffers, asynchronous on `hip_stream` (NULL = engine stream), with
+ * the stream ordering of sga_request_tokens_device.  One chunk: n <= max_batch.  Timestamps are
+ * ts_base + ts_off[i]; d_flags, d_rt, d_param, d_param_values and d_wait_ms may be NULL (zeros /
+ * not written).  The checks the host entry makes by scanning the events (SystemSlot or Collection
+ * arguments -> arrival-order replay, inbound statistics, acquire >= 0, value ranges inside
+ * param_values) run on the device; a chunk that fails them is not applied and answers -1 for
+ * every event.  sga_events_device_status waits for the engine stream and reports SGA_EINVAL for
+ * such a chunk or SGA_ENOMEM when a parameter map filled, since its last call. */
+int sga_submit_events_device(sga_engine *e, const uint8_t *d_kind, const uint32_t *d_resource, int64_t ts_base,
+                             const uint32_t *d_ts_off, const int32_t *d_acquire, const uint8_t *d_flags,
+                             const int64_t *d_rt, const uint64_t *d_param, size_t n, const uint64_t *d_param_values,
+                             size_t n_values, int8_t *d_decision, int32_t *d_wait_ms, void *hip_stream);
+int sga_events_device_status(sga_engine *e);
 int sga_query_node(sga_engine *e, uint32_t resource, int64_t now, sga_node_view *out);
 
 /* SystemRule (CORE/slots/system/SystemRule.java:43-50); negative = not set. */

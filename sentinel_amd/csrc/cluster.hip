@@ -1834,6 +1834,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
     const SlotParam P = st.param[s];
     const Rec R = rec_of(st, P);
     const double thr = P.thr;
+    if (lane == 0) sc.hthr[h] = make_double2(thr, P.isec);
     const int64_t qbase = div_pos(ts_base, P.W);
     const uint32_t plo = sc.plo[h], phi = max(sc.phi[h], plo);
     const uint32_t *pr = sc.prank;
@@ -1947,68 +1948,112 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
     }
 }
 
-// TokenResults of the non-prioritized hot requests, in input order: one workgroup per rank segment
-// (its base row in LDS), each wave a quarter of it in chunks of kFinChunk rounds; the next chunk's
-// codes are in flight while a chunk's run records (two 16-byte loads each) are gathered.
+// TokenResults of the non-prioritized hot requests, in input order: one 16-wave workgroup per rank
+// segment (its base row in LDS), kFinChunk rounds per wave.  The runs of the kFinCache hottest ids
+// (k_hot_pick numbers them first) in the segment's first two buckets are staged in LDS; a lane whose
+// run is staged still issues its gather, pointed at one shared line, so the loads stay unconditional.
 constexpr int kFinChunk = 8;
-constexpr int kFinWaves = kThreads / 64;
+constexpr uint32_t kFinCache = 1024;
+constexpr int kFinWgThreads = 1024;
+constexpr int kFinWaves = kFinWgThreads / 64;
 constexpr uint32_t kFinSpan = kHotSeg / kFinWaves;  // requests per wave
+static_assert(kFinSpan == kFinChunk * 64, "one chunk per wave");
 __device__ __forceinline__ int64_t i64_of(uint32_t lo, uint32_t hi) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ double f64_of(uint32_t lo, uint32_t hi) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
-__global__ __launch_bounds__(kThreads) void k_hot_final(BatchScratch sc, uint32_t n, uint64_t *__restrict__ out) {
+__global__ __launch_bounds__(kFinWgThreads) void k_hot_final(BatchScratch sc, uint32_t n, uint64_t *__restrict__ out,
+                                                             uint32_t cache_cap) {
     __shared__ uint32_t base[kHot];
+    __shared__ double2 c_ti[kFinCache];      // thr, isec
+    __shared__ int64_t c_s0[2][kFinCache];   // s0 of the runs in buckets b0, b0 + 1
+    __shared__ uint2 c_fs[2][kFinCache];     // (f, start) of those runs
+    __shared__ uint32_t s_b0;
     if (!sc.counters[CTL_MODE]) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t seg = blockIdx.x;
     const uint32_t sbase = seg * kHotSeg;
     const uint32_t nhot = hot_count(sc);
-    for (uint32_t h = threadIdx.x; h < nhot; h += kThreads) base[h] = sc.hbase[(size_t)seg * kHot + h];
-    __syncthreads();
     const uint32_t wbase = sbase + (uint32_t)wave * kFinSpan;
-    const uint32_t wend = min(n, wbase + kFinSpan);
-    if (wbase >= wend) return;
     uint32_t cn[kFinChunk];
 #pragma unroll
     for (int u = 0; u < kFinChunk; ++u) cn[u] = sc.hcode[min(wbase + (uint32_t)u * 64 + lane, n - 1)];
-    for (uint32_t r0 = wbase; r0 < wend; r0 += kFinChunk * 64) {
-        uint32_t code[kFinChunk];
+    if (wave == 0) {  // the segment's first bucket: the smallest among its first 64 codes
+        uint32_t bk = (cn[0] >> 31) ? 0xFFu : (cn[0] >> 25);
 #pragma unroll
-        for (int u = 0; u < kFinChunk; ++u) {
-            const uint32_t i = r0 + u * 64 + lane;
-            code[u] = (i < wend && !(cn[u] >> 31)) ? cn[u] : kNoCode;  // prioritized: k_prio_results
+        for (int d = 32; d >= 1; d >>= 1) bk = min(bk, (uint32_t)__shfl_xor((int)bk, d));
+        if (lane == 0) s_b0 = bk == 0xFFu ? sc.counters[CTL_BDLO] : bk;
+    }
+    for (uint32_t h = threadIdx.x; h < nhot; h += kFinWgThreads) base[h] = sc.hbase[(size_t)seg * kHot + h];
+    __syncthreads();
+    const uint32_t b0 = s_b0;
+    const uint32_t ncache = min(nhot, cache_cap & 0xFFFFu);
+    for (uint32_t h = threadIdx.x; h < ncache; h += kFinWgThreads) {
+        c_ti[h] = sc.hthr[h];
+#pragma unroll
+        for (uint32_t k = 0; k < 2; ++k) {
+            const uint32_t b = min(b0 + k, (uint32_t)kHotBuckets - 1);
+            const uint4 *hp = reinterpret_cast<const uint4 *>(sc.hrun + (size_t)h * kHotBuckets + b);
+            const uint2 s0 = *reinterpret_cast<const uint2 *>(hp);
+            const uint4 r1 = hp[1];
+            c_s0[k][h] = i64_of(s0.x, s0.y);
+            c_fs[k][h] = make_uint2(r1.z, r1.w);
         }
+    }
+    __syncthreads();
+    const uint32_t wend = min(n, wbase + kFinSpan);
+    if (wbase >= wend) return;
+    uint32_t code[kFinChunk];
+    bool hit[kFinChunk];
+    uint4 ra[kFinChunk], rb[kFinChunk];
 #pragma unroll
-        for (int u = 0; u < kFinChunk; ++u)
-            cn[u] = sc.hcode[min(r0 + (uint32_t)(kFinChunk + u) * 64 + lane, n - 1)];
-        uint4 ra[kFinChunk], rb[kFinChunk];
+    for (int u = 0; u < kFinChunk; ++u) {
+        const uint32_t i = wbase + u * 64 + lane;
+        code[u] = (i < wend && !(cn[u] >> 31)) ? cn[u] : kNoCode;  // prioritized: k_prio_results
+        const uint32_t cd = code[u];
+        hit[u] = cd == kNoCode || ((cd & 0xFFFu) < (cache_cap & 0xFFFFu) && (cd >> 25) - b0 < 2u);
+        const size_t at = hit[u] ? 0 : (size_t)(cd & 0xFFFu) * kHotBuckets + (cd >> 25);
+        const uint4 *hp = reinterpret_cast<const uint4 *>(sc.hrun + at);
+        ra[u] = hp[0];  // s0, thr
+        rb[u] = hp[1];  // isec, f, start
+    }
 #pragma unroll
-        for (int u = 0; u < kFinChunk; ++u) {
-            const uint32_t cd = code[u] == kNoCode ? 0u : code[u];  // clamped: the load is unconditional
-            const uint4 *hp = reinterpret_cast<const uint4 *>(sc.hrun + (size_t)(cd & 0xFFFu) * kHotBuckets + (cd >> 25));
-            ra[u] = hp[0];  // s0, thr
-            rb[u] = hp[1];  // isec, f, start
+    for (int u = 0; u < kFinChunk; ++u) {
+        const uint32_t cd = code[u];
+        if (cd == kNoCode) {
+            if (cache_cap & 0x10000u) out[wbase + u * 64 + lane] = 0;  // timing experiment only
+            continue;
         }
-#pragma unroll
-        for (int u = 0; u < kFinChunk; ++u) {
-            if (code[u] == kNoCode) continue;
-            const int64_t s0 = i64_of(ra[u].x, ra[u].y);
-            const double thr = f64_of(ra[u].z, ra[u].w);
-            const double isec = f64_of(rb[u].x, rb[u].y);
-            const uint32_t f = rb[u].z, st0 = rb[u].w;
-            const uint32_t local = base[code[u] & 0xFFFu] + ((code[u] >> 12) & 0x1FFFu) - st0;
-            uint64_t res;
-            if (local < f) {
-                const int64_t sum = s0 + (int64_t)local;
-                res = pack_result(TRS_OK, j_d2i(thr - (double)sum / isec - 1.0), 0);
-            } else {
-                res = pack_result(TRS_BLOCKED, 0, 0);
-            }
-            out[r0 + u * 64 + lane] = res;
+        const uint32_t h = cd & 0xFFFu, k = ((cd >> 25) - b0) & 1u;
+        int64_t s0;
+        double thr, isec;
+        uint32_t f, st0;
+        if (hit[u]) {
+            s0 = c_s0[k][h];
+            const double2 ti = c_ti[h];
+            thr = ti.x;
+            isec = ti.y;
+            const uint2 fs = c_fs[k][h];
+            f = fs.x;
+            st0 = fs.y;
+        } else {
+            s0 = i64_of(ra[u].x, ra[u].y);
+            thr = f64_of(ra[u].z, ra[u].w);
+            isec = f64_of(rb[u].x, rb[u].y);
+            f = rb[u].z;
+            st0 = rb[u].w;
         }
+        const uint32_t local = base[h] + ((cd >> 12) & 0x1FFFu) - st0;
+        uint64_t res;
+        if (local < f) {
+            const int64_t sum = s0 + (int64_t)local;
+            res = pack_result(TRS_OK, j_d2i(thr - (double)sum / isec - 1.0), 0);
+        } else {
+            res = pack_result(TRS_BLOCKED, 0, 0);
+        }
+        out[wbase + u * 64 + lane] = res;
     }
 }
 
@@ -2105,17 +2150,22 @@ __global__ __launch_bounds__(kThreads) void k_hot_clear(ClusterState st, BatchSc
     }
 }
 
+// Hot ids go out in descending count-bin order (bin b holds counts in [2^b, 2^(b+1))): each bin
+// owns a block of ids, so after k_hot_fin compacts the holes left by rules of another window
+// length, the hottest rules have the smallest ids (k_hot_final caches the first kFinCache of them).
 __global__ __launch_bounds__(kThreads) void k_hot_pick(ClusterState st, BatchScratch sc, uint32_t hot_min) {
-    __shared__ uint32_t thr, wbest;
+    __shared__ uint32_t thr, wbest, bcnt[32], bbase[32], lcnt[32], gbase[32];
+    if (threadIdx.x < 32) bcnt[threadIdx.x] = sc.hot_ctl[8 + threadIdx.x];
+    __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t cum = 0, t = 0xFFFFFFFFu;
         for (int b = 31; b >= 0; --b) {
-            cum += sc.hot_ctl[8 + b];
-            if (cum > (uint32_t)kHot) break;
-            t = 1u << b;
+            bbase[b] = cum;
+            cum += bcnt[b];
+            if (cum <= (uint32_t)kHot) t = 1u << b;
         }
         thr = max(t, max(hot_min, 1u));
-        sc.hot_ctl[7] = thr;  // next batch's candidate floor is half of it
+        if (blockIdx.x == 0) sc.hot_ctl[7] = thr;  // next batch's candidate floor is half of it
         const unsigned long long best = *reinterpret_cast<const unsigned long long *>(sc.hot_ctl + 4);
         wbest = best ? (uint32_t)st.param[(uint32_t)best].W : 0u;
     }
@@ -2123,37 +2173,81 @@ __global__ __launch_bounds__(kThreads) void k_hot_pick(ClusterState st, BatchScr
     if (!wbest) return;
     uint32_t ncold;
     const uint32_t ncand = hot_ncand(sc, ncold);
-    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < ncand; i += gridDim.x * kThreads) {
-        uint32_t slot, c;
-        if (!hot_candidate(st, sc, i, ncold, thr, slot, c)) continue;
-        if ((uint32_t)st.param[slot].W != wbest) continue;
-        const uint32_t hid = atomicAdd(&sc.hot_ctl[1], 1u);
-        if (hid < (uint32_t)kHot) {
-            sc.hot_next[hid] = slot;
-            sc.hot_of[slot] = (uint16_t)hid;
-            hot_fid_set(st, slot, (uint16_t)hid);
+    for (uint32_t r0 = blockIdx.x * kThreads; r0 < ncand; r0 += gridDim.x * kThreads) {  // uniform per block
+        if (threadIdx.x < 32) lcnt[threadIdx.x] = 0;
+        __syncthreads();
+        const uint32_t i = r0 + threadIdx.x;
+        uint32_t slot = 0, c = 0, lo = 0;
+        int b = -1;
+        if (i < ncand && hot_candidate(st, sc, i, ncold, thr, slot, c) && (uint32_t)st.param[slot].W == wbest) {
+            b = 31 - __clz(c);
+            lo = atomicAdd(&lcnt[b], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < 32 && lcnt[threadIdx.x]) gbase[threadIdx.x] = atomicAdd(&sc.hot_ctl[64 + threadIdx.x], lcnt[threadIdx.x]);
+        __syncthreads();
+        if (b >= 0) {
+            const uint32_t hid = bbase[b] + gbase[b] + lo;
+            if (hid < (uint32_t)kHot) {
+                sc.hot_next[hid] = slot;
+                sc.hot_of[slot] = (uint16_t)hid;
+                hot_fid_set(st, slot, (uint16_t)hid);
+            }
         }
     }
 }
 
-__global__ __launch_bounds__(kThreads) void k_hot_fin(ClusterState st, BatchScratch sc) {
-    __shared__ uint32_t nn;
+// Compacts the picked ids (stable, so the count-bin order stays) and publishes them.  Holes are
+// left only by candidates of another window length; a rule whose id moves is renamed here.
+constexpr int kFinThreads = 1024;
+constexpr int kFinPer = kHot / kFinThreads;
+__global__ __launch_bounds__(kFinThreads) void k_hot_fin(ClusterState st, BatchScratch sc) {
+    __shared__ uint32_t wsum[kFinThreads / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t sl[kFinPer], cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kFinPer; ++k) {
+        sl[k] = sc.hot_next[threadIdx.x * kFinPer + k];
+        cnt += sl[k] != kNoSlot;
+    }
+    uint32_t inc = cnt;  // inclusive wave scan
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t v = __shfl_up(inc, d);
+        if (lane >= d) inc += v;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int w = 0; w < kFinThreads / 64; ++w) {
+        off += w < wave ? wsum[w] : 0u;
+        tot += wsum[w];
+    }
+    uint32_t hid = off + inc - cnt;
+#pragma unroll
+    for (int k = 0; k < kFinPer; ++k) {
+        const uint32_t at = threadIdx.x * kFinPer + k;
+        if (sl[k] == kNoSlot) continue;
+        sc.hot_slot[hid] = sl[k];
+        if (hid != at) {
+            sc.hot_of[sl[k]] = (uint16_t)hid;
+            hot_fid_set(st, sl[k], (uint16_t)hid);
+        }
+        sc.hot_next[at] = kNoSlot;
+        ++hid;
+    }
     if (threadIdx.x == 0) {
-        nn = min(sc.hot_ctl[1], (uint32_t)kHot);
         const unsigned long long best = *reinterpret_cast<const unsigned long long *>(sc.hot_ctl + 4);
         sc.hot_ctl[2] = best ? (uint32_t)st.param[(uint32_t)best].W : 1u;
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nn; i += kThreads) sc.hot_slot[i] = sc.hot_next[i];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        sc.hot_ctl[0] = nn;
-        sc.hot_ctl[1] = 0;
+        sc.hot_ctl[0] = tot;
         sc.hot_ctl[4] = 0;
         sc.hot_ctl[5] = 0;
         sc.hot_ctl[6] = 0;  // the next batch's candidates
     }
-    if (threadIdx.x < 32) sc.hot_ctl[8 + threadIdx.x] = 0;
+    if (threadIdx.x < 32) {
+        sc.hot_ctl[8 + threadIdx.x] = 0;
+        sc.hot_ctl[64 + threadIdx.x] = 0;
+    }
 }
 
 __global__ void k_hot_reset(ClusterState st, BatchScratch sc, uint32_t nslots_cap) {
@@ -2162,7 +2256,9 @@ __global__ void k_hot_reset(ClusterState st, BatchScratch sc, uint32_t nslots_ca
     if (st.dense_hot)
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < st.dense_n; i += gridDim.x * blockDim.x)
             st.dense_hot[4 * (size_t)i + 2] = kColdId;
-    if (blockIdx.x == 0 && threadIdx.x < 64) sc.hot_ctl[threadIdx.x] = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)kHot; i += gridDim.x * blockDim.x)
+        sc.hot_next[i] = kNoSlot;
+    if (blockIdx.x == 0 && threadIdx.x < kHotCtlWords) sc.hot_ctl[threadIdx.x] = 0;
 }
 
 __global__ void k_metric_sums(ClusterState st, uint32_t s, int64_t now, int64_t *out7) {
@@ -2811,6 +2907,11 @@ static int fz_debug() {
     return v;
 }
 
+static uint32_t fin_cache() {  // profiling knob: SGA_FIN_CACHE=0 turns k_hot_final's LDS cache off
+    static const uint32_t v = getenv("SGA_FIN_CACHE") ? (uint32_t)atoi(getenv("SGA_FIN_CACHE")) : kFinCache;
+    return v;
+}
+
 static size_t hot_rows(size_t cap) { return (cap + kHotSeg - 1) / kHotSeg; }
 static size_t hot_groups(size_t cap) { return (hot_rows(cap) + kHotGroupRows - 1) / kHotGroupRows; }
 
@@ -2833,7 +2934,7 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up(scan_partials_needed(cap) * 4 + 64);
     b += align_up(kRadixGhistWords * 4) + align_up(64);  // look-back digit totals, error flag
     // hot path
-    b += align_up((size_t)nslots_cap * 2) + 2 * align_up(kHot * 4) + align_up(64 * 4);  // hot_of/slot/next/ctl
+    b += align_up((size_t)nslots_cap * 2) + 2 * align_up(kHot * 4) + align_up(kHotCtlWords * 4);  // hot_of/slot/next/ctl
     b += align_up(segs_alloc * kHotSeg * 8);                                       // el_tile
     b += align_up(segs_alloc * kSubPerSeg * 4);                                    // tile_nc
     b += align_up(segs_alloc * kHotSeg * 4);                                       // hcode
@@ -2841,6 +2942,7 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up(hot_groups(cap) * kHot * 4);                                     // hgsum
     b += align_up((size_t)kHotBuckets * kHot * 2) + align_up(kHotBuckets * 4);     // hpre, hbnd
     b += align_up((size_t)kHot * kHotBuckets * sizeof(HotRun));                   // hrun
+    b += align_up(kHot * sizeof(double2));                                        // hthr
     b += align_up(cap * 4);                                                        // prank
     b += 3 * align_up(kHot * 4);                                                   // plo, phi, hot_tot
     b += align_up(256 * sizeof(WConst));
@@ -2887,7 +2989,7 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.hot_of = (uint16_t *)take((size_t)nslots_cap * 2);
     sc.hot_slot = (uint32_t *)take(kHot * 4);
     sc.hot_next = (uint32_t *)take(kHot * 4);
-    sc.hot_ctl = (uint32_t *)take(64 * 4);
+    sc.hot_ctl = (uint32_t *)take(kHotCtlWords * 4);
     sc.el_tile = (uint64_t *)take(segs_alloc * kHotSeg * 8);
     sc.tile_nc = (uint32_t *)take(segs_alloc * kSubPerSeg * 4);
     sc.hcode = (uint32_t *)take(segs_alloc * kHotSeg * 4);
@@ -2897,6 +2999,7 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.hpre = (uint16_t *)take((size_t)kHotBuckets * kHot * 2);
     sc.hbnd = (uint32_t *)take(kHotBuckets * 4);
     sc.hrun = (HotRun *)take((size_t)kHot * kHotBuckets * sizeof(HotRun));
+    sc.hthr = (double2 *)take(kHot * sizeof(double2));
     sc.prank = (uint32_t *)take(cap * 4);
     sc.plo = (uint32_t *)take(kHot * 4);
     sc.phi = (uint32_t *)take(kHot * 4);
@@ -3018,13 +3121,13 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
             fprintf(stderr, "fz phases (wall_clock64 ticks per workgroup, %llu wgs): runs %.0f flows %.0f results %.0f\n",
                     ph[7], (double)ph[0] / ph[7], (double)ph[1] / ph[7], (double)ph[2] / ph[7]);
     }
-    hipLaunchKernelGGL(k_hot_final, dim3(nseg), dim3(kThreads), 0, s, sc, n, out);
+    hipLaunchKernelGGL(k_hot_final, dim3(nseg), dim3(kFinWgThreads), 0, s, sc, n, out, fin_cache());
     hipLaunchKernelGGL(k_prio_results, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el, out);
     const uint32_t sb = 64;  // few workgroups: their bins meet in global atomics
     hipLaunchKernelGGL(k_hot_hist, dim3(sb), dim3(kThreads), 0, s, st, sc, std::max<uint32_t>(sc.hot_min, 1));
     hipLaunchKernelGGL(k_hot_clear, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc);
     hipLaunchKernelGGL(k_hot_pick, dim3(sb), dim3(kThreads), 0, s, st, sc, sc.hot_min);
-    hipLaunchKernelGGL(k_hot_fin, dim3(1), dim3(kThreads), 0, s, st, sc);
+    hipLaunchKernelGGL(k_hot_fin, dim3(1), dim3(kFinThreads), 0, s, st, sc);
 }
 
 void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,

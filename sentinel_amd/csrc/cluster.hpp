@@ -110,6 +110,8 @@ static_assert(sizeof(HotRun) == 64, "hot run record");
 // Hot path geometry.
 constexpr int kHot = 4096;          // hot ids (12 bits in the request code)
 constexpr uint16_t kColdId = 0xFFFF;
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;  // hot_next: id not taken
+constexpr int kHotCtlWords = 128;        // hot_ctl: [0..8) state, [8..40) count bins, [64..96) bin cursors
 constexpr int kHotSeg = 8192;       // requests per wave segment of k_hot_classify (one count row)
 constexpr int kSubSeg = 1024;       // cold compaction segment = sort input segment (4 per sort tile)
 constexpr int kHotBuckets = 64;     // window buckets a batch may span on the hot path (6 bits)
@@ -184,6 +186,7 @@ struct BatchScratch {
     uint16_t *hpre;           // [kHotBuckets][kHot] the segment's hot requests before the bucket's first
     uint32_t *hbnd;           // [kHotBuckets] the bucket's first request
     HotRun *hrun;             // [kHot][kHotBuckets]
+    double2 *hthr;            // [kHot] threshold and intervalInSecond of each hot rule (k_hot_flows)
     uint32_t *prank;          // per prioritized hot request (sorted region order): its rank
     uint32_t *plo, *phi;      // per hot id: its range in the prioritized region
     uint32_t *hot_tot;        // per hot id: requests in the batch

@@ -1568,6 +1568,51 @@ int sga_submit_events_ex(sga_engine *e, const uint8_t *kind, const uint32_t *res
     });
 }
 
+int sga_submit_events_device(sga_engine *e, const uint8_t *d_kind, const uint32_t *d_resource, int64_t ts_base,
+                             const uint32_t *d_ts_off, const int32_t *d_acquire, const uint8_t *d_flags,
+                             const int64_t *d_rt, const uint64_t *d_param, size_t n, const uint64_t *d_param_values,
+                             size_t n_values, int8_t *d_decision, int32_t *d_wait_ms, void *hip_stream) {
+    if (n && (!d_kind || !d_resource || !d_ts_off || !d_acquire || !d_decision)) return SGA_EINVAL;
+    if (ts_base < 0) return SGA_EINVAL;  // LeapArray.currentWindow(t < 0) returns null
+    return guarded(e, [&](Engine &g) {
+        if (n > g.cfg.max_batch) return SGA_ERANGE;
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        g.flow.cluster_on = g.cluster_server == 1 ? 1 : 0;
+        if (g.flow.has_cluster_rules) {
+            g.flow.cluster_st = g.state();
+            const int rc = g.flow.resolve_cluster(
+                [&](int64_t fid) -> int32_t {
+                    auto it = g.slot_of.find(fid);
+                    if (it == g.slot_of.end()) return -1;
+                    const SlotHost &h = g.slots[it->second];
+                    if (!h.active) return -1;
+                    if (h.ns >= 0 && g.nss[h.ns].has_limit) return -2;
+                    return (int32_t)it->second;
+                },
+                g.cluster_gen);
+            if (rc != SGA_OK) {
+                g.err = "cluster-mode flow rule: flowId shared by two resources or namespace with a request limiter";
+                return rc;
+            }
+        }
+        // buffers grow on the engine stream before a caller stream is ordered after it
+        if (const int rc = g.flow.ensure_scratch()) return rc;
+        if (const int rc = g.flow.ensure_maps(n + n_values)) return rc;
+        hipStream_t s = g.enter_stream(hip_stream);
+        const int rc = g.flow.submit_device(d_kind, d_resource, ts_base, d_ts_off, d_acquire, d_flags, d_rt, d_param, n,
+                                            d_param_values, n_values, d_decision, d_wait_ms, s);
+        g.leave_stream(s);
+        return rc;
+    });
+}
+
+int sga_events_device_status(sga_engine *e) {
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        return g.flow.device_status();
+    });
+}
+
 int sga_query_node(sga_engine *e, uint32_t resource, int64_t now, sga_node_view *out) {
     return guarded(e, [&](Engine &g) {
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));

@@ -740,12 +740,56 @@ __device__ __forceinline__ void entry_node_after_exit(const Ctx &c, int64_t t, i
 
 // System-rule mode: the whole batch by one lane in arrival order (checkSystem reads ENTRY_NODE,
 // which every earlier inbound decision of every resource changed).
+// Device entry gate (FlowEngine::submit_device): k_lgate sets kGateSeq when the chunk must be replayed
+// in arrival order (inbound events under a SystemRule, or Collection arguments), kGateIn when it holds
+// inbound events, kGateBad on invalid input (the chunk is not applied).  A null gate (host entry)
+// lets every kernel run; the host launches only the ones the chunk needs.
+constexpr uint32_t kGateSeq = 1, kGateIn = 2, kGateBad = 4;
+__device__ __forceinline__ bool gate_is(const uint32_t *g, uint32_t mask, uint32_t want) {
+    return !g || (*g & mask) == want;
+}
+
+__global__ __launch_bounds__(kT) void k_lgate(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ resource,
+                                              const int32_t *__restrict__ acquire, const uint8_t *__restrict__ flags,
+                                              const uint64_t *__restrict__ param_in, uint32_t n, uint32_t nres,
+                                              int sys_check, uint64_t npvals, uint32_t *gate) {
+    uint32_t g = 0;
+    for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
+        const uint8_t fl = flags ? flags[i] : 0;
+        if (acquire[i] < 0 || kind[i] > 1) g |= kGateBad;
+        if ((fl & SGA_EV_INBOUND) && resource[i] < nres) g |= sys_check ? (kGateIn | kGateSeq) : kGateIn;
+        if ((fl & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) {
+            const uint64_t pv = param_in ? param_in[i] : 0;
+            if ((pv >> 32) + (pv & 0xFFFFFFFFu) > npvals) g |= kGateBad;
+            g |= kGateSeq;
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) g |= (uint32_t)__shfl_xor((int)g, d);
+    if ((threadIdx.x & 63) == 0 && g) atomicOr(gate, g);
+}
+
+// Last kernel of a device chunk: an invalid chunk answers -1 for every event; the sticky word
+// (device_status) collects invalid chunks (bit 0) and full parameter maps (bit 1).
+__global__ __launch_bounds__(kT) void k_lfail(const uint32_t *gate, const uint32_t *overflow, uint32_t *sticky,
+                                              uint32_t n, int8_t *decision, int32_t *wait_ms) {
+    const uint32_t g = *gate;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const uint32_t e = ((g & kGateBad) ? 1u : 0u) | (*overflow ? 2u : 0u);
+        if (e) atomicOr(sticky, e);
+    }
+    if (!(g & kGateBad)) return;
+    for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
+        decision[i] = -1;
+        wait_ms[i] = 0;
+    }
+}
+
 __global__ void k_lseq(FlowState st, int64_t max_rt, SysDev sys, const uint8_t *__restrict__ kind,
                        const uint32_t *__restrict__ resource, const uint32_t *__restrict__ ts_off, int64_t ts_base,
                        const int32_t *__restrict__ acquire, const uint8_t *__restrict__ flags,
                        const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in, uint32_t n,
                        int8_t *decision, int32_t *wait_ms, const uint64_t *__restrict__ pvals) {
-    if (threadIdx.x || blockIdx.x) return;
+    if (threadIdx.x || blockIdx.x || !gate_is(st.gate, kGateSeq | kGateBad, kGateSeq)) return;
     const Ctx c{st, max_rt};
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t r = resource[i];
@@ -796,6 +840,7 @@ __global__ __launch_bounds__(kEnTile) void k_entry_stats(FlowState st, int64_t m
     __shared__ unsigned long long thr_delta;
     __shared__ int mono, any;
     __shared__ int64_t prev_last;
+    if (!gate_is(st.gate, kGateSeq | kGateIn | kGateBad, kGateIn)) return;
     const Ctx c{st, max_rt};
     if (threadIdx.x == 0) prev_last = INT64_MIN;
     for (uint32_t base = 0; base < n; base += kEnTile) {
@@ -889,6 +934,11 @@ __global__ __launch_bounds__(kT) void k_lclassify(FlowState st, const uint8_t *_
                                                   Payload *pay, int8_t *decision, int32_t *wait_ms) {
     const uint32_t i = blockIdx.x * kT + threadIdx.x;
     if (i >= n) return;
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) {  // k_lseq or k_lfail answers: every event a no-op here
+        keys[i] = st.nres;
+        pay[i] = Payload{i, 0, 0, 0};
+        return;
+    }
     const uint32_t r = resource[i];
     const uint8_t fl = flags ? flags[i] : 0;
     const bool ex = kind[i] == 1;
@@ -1137,6 +1187,7 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
                                                int64_t ts_base, const int64_t *__restrict__ rt_in,
                                                const uint64_t *__restrict__ param_in, int8_t *decision,
                                                int32_t *wait_ms) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
     const Ctx c{st, max_rt};
     const uint32_t nflows = sc.counters[2], nruns = sc.counters[1];
     for (uint32_t fl = blockIdx.x * kT + threadIdx.x; fl < nflows; fl += gridDim.x * kT) {
@@ -1357,6 +1408,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                                                const uint64_t *__restrict__ param_in, int8_t *decision,
                                                int32_t *wait_ms, uint64_t *prof) {
     // prof (SGA_HEAVY_PROF=1): per workgroup, wall-clock ticks spent in each phase of the chunks
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
     __shared__ int64_t lnode[kNodeWords];
     __shared__ FlowRuleDev lrules[kHeavyRules];
     __shared__ CbDev lcbs[kHeavyCbs];
@@ -1948,6 +2000,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
 }
 
 __global__ __launch_bounds__(kT) void k_lresults(FlowScratch sc, const Payload *__restrict__ pay, int8_t *decision) {
+    if (!gate_is(sc.gate, kGateSeq | kGateBad, 0)) return;
     const uint32_t nvalid = sc.counters[0];
     const uint32_t j = blockIdx.x * kT + threadIdx.x;
     if (j >= nvalid) return;
@@ -2104,6 +2157,7 @@ FlowState FlowEngine::state() const {
     s.overflow = d_overflow.p;
     s.cst = cluster_st;
     s.cluster_on = cluster_on;
+    s.gate = nullptr;
     return s;
 }
 
@@ -2492,28 +2546,7 @@ void print_heavy_prof() {
             h[best * 8 + 3] / 1e5, h[best * 8 + 4] / 1e5, h[best * 8 + 6] / 1e5, h[best * 8 + 7] / 1e5);
 }
 
-int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int64_t *ts, const int32_t *acquire,
-                       const uint8_t *flags, const int64_t *rt, const uint64_t *param, size_t n, int8_t *decision,
-                       int32_t *wait_ms, const uint64_t *pvals, size_t npvals) {
-    if (!nres) return SGA_EINVAL;
-    if (n == 0) return 0;
-    // Collection / array arguments (SGA_EV_PARAM_LIST): the value array goes to the device once;
-    // chunks holding such events are replayed in arrival order by one lane (k_lseq)
-    bool any_list = false;
-    for (size_t i = 0; flags && param && i < n && !any_list; ++i) {
-        if ((flags[i] & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) {
-            if (!pvals || (param[i] >> 32) + (param[i] & 0xFFFFFFFFu) > npvals) return SGA_EINVAL;
-            any_list = true;
-        }
-    }
-    for (size_t i = 0; any_list && i < n; ++i)
-        if ((flags[i] & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM) &&
-            (param[i] >> 32) + (param[i] & 0xFFFFFFFFu) > npvals)
-            return SGA_EINVAL;
-    if (any_list) {
-        if (d_pvals.n < std::max<size_t>(npvals, 1)) d_pvals.alloc(std::max<size_t>(npvals, 1));
-        if (npvals) SGA_HIP_CHECK(hipMemcpyAsync(d_pvals.p, pvals, npvals * 8, hipMemcpyHostToDevice, stream));
-    }
+int FlowEngine::ensure_scratch() {
     const size_t cap = cfg.max_batch;
     if (cap > F_IDX) return SGA_ERANGE;
     if (scratch_cap < cap) {
@@ -2573,6 +2606,33 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         d_dec.alloc(cap);
         d_wait.alloc(cap);
     }
+    return 0;
+}
+
+int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int64_t *ts, const int32_t *acquire,
+                       const uint8_t *flags, const int64_t *rt, const uint64_t *param, size_t n, int8_t *decision,
+                       int32_t *wait_ms, const uint64_t *pvals, size_t npvals) {
+    if (!nres) return SGA_EINVAL;
+    if (n == 0) return 0;
+    // Collection / array arguments (SGA_EV_PARAM_LIST): the value array goes to the device once;
+    // chunks holding such events are replayed in arrival order by one lane (k_lseq)
+    bool any_list = false;
+    for (size_t i = 0; flags && param && i < n && !any_list; ++i) {
+        if ((flags[i] & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) {
+            if (!pvals || (param[i] >> 32) + (param[i] & 0xFFFFFFFFu) > npvals) return SGA_EINVAL;
+            any_list = true;
+        }
+    }
+    for (size_t i = 0; any_list && i < n; ++i)
+        if ((flags[i] & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM) &&
+            (param[i] >> 32) + (param[i] & 0xFFFFFFFFu) > npvals)
+            return SGA_EINVAL;
+    if (any_list) {
+        if (d_pvals.n < std::max<size_t>(npvals, 1)) d_pvals.alloc(std::max<size_t>(npvals, 1));
+        if (npvals) SGA_HIP_CHECK(hipMemcpyAsync(d_pvals.p, pvals, npvals * 8, hipMemcpyHostToDevice, stream));
+    }
+    const size_t cap = cfg.max_batch;
+    if (const int rc = ensure_scratch()) return rc;
     int bits = 1;
     while (((uint64_t)1 << bits) < (uint64_t)nres + 1) ++bits;
     std::vector<uint32_t> off;
@@ -2661,6 +2721,88 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         if (ovf) return SGA_ENOMEM;  // parameter maps full
         b += m;
     }
+    return 0;
+}
+
+// Device entry: one chunk of events already in HBM, launched on s without a host wait.  What the host
+// entry decides by scanning the events (arrival-order replay, inbound statistics, validation) is
+// decided by k_lgate on the device: both the parallel pipeline and k_lseq are launched and the gate
+// word lets exactly one of them act.  Errors surface through device_status.
+int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resource, int64_t ts_base,
+                              const uint32_t *d_ts_off, const int32_t *d_acquire, const uint8_t *d_flags_in,
+                              const int64_t *d_rt_in, const uint64_t *d_param_in, size_t n,
+                              const uint64_t *d_param_values, size_t n_values, int8_t *d_decision, int32_t *d_wait,
+                              hipStream_t s) {
+    if (!nres) return SGA_EINVAL;
+    if (n == 0) return 0;
+    if (n > cfg.max_batch) return SGA_ERANGE;
+    if (const int rc = ensure_scratch()) return rc;
+    if (const int rc = ensure_maps(n + n_values)) return rc;
+    if (!d_gate.p) {
+        d_gate.alloc(2);
+        SGA_HIP_CHECK(hipMemsetAsync(d_gate.p, 0, 8, s));
+    }
+    const uint32_t m = (uint32_t)n;
+    int bits = 1;
+    while (((uint64_t)1 << bits) < (uint64_t)nres + 1) ++bits;
+    // absent optional columns read as zeros
+    if (!d_rt_in) SGA_HIP_CHECK(hipMemsetAsync(d_rt.p, 0, n * 8, s));
+    if (!d_param_in) SGA_HIP_CHECK(hipMemsetAsync(d_param.p, 0, n * 8, s));
+    if (!d_flags_in) SGA_HIP_CHECK(hipMemsetAsync(d_flags.p, 0, n, s));
+    const int64_t *rt_p = d_rt_in ? d_rt_in : d_rt.p;
+    const uint64_t *param_p = d_param_in ? d_param_in : d_param.p;
+    const uint8_t *flags_p = d_flags_in ? d_flags_in : d_flags.p;
+    int32_t *wait_p = d_wait ? d_wait : this->d_wait.p;
+    SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, 64, s));
+    SGA_HIP_CHECK(hipMemsetAsync(d_overflow.p, 0, 4, s));
+    SGA_HIP_CHECK(hipMemsetAsync(d_gate.p, 0, 4, s));
+    const uint32_t nb = (m + kT - 1) / kT;
+    const uint32_t gb = std::min<uint32_t>(nb, 1024);
+    hipLaunchKernelGGL(k_lgate, dim3(gb), dim3(kT), 0, s, d_kind_in, d_resource, d_acquire, flags_p, param_p, m, nres,
+                       (int)sys.check, (uint64_t)(d_param_values ? n_values : 0), d_gate.p);
+    FlowState st = state();
+    st.gate = d_gate.p;
+    FlowScratch gsc = sc;
+    gsc.gate = d_gate.p;
+    hipLaunchKernelGGL(k_lclassify, dim3(nb), dim3(kT), 0, s, st, d_kind_in, d_resource, d_ts_off, ts_base, d_acquire,
+                       flags_p, m, gsc.keys[0], gsc.pay[0], d_decision, wait_p);
+    const int np = radix_sort_pairs(gsc.keys[0], gsc.pay[0], gsc.keys[1], gsc.pay[1], m, bits, gsc.radix, s);
+    const uint32_t *keys = gsc.keys[np & 1];
+    const Payload *pay = gsc.pay[np & 1];
+    const uint32_t ntiles = (m + kTileElems - 1) / kTileElems;
+    hipLaunchKernelGGL(k_lruns_up, dim3(ntiles), dim3(kT), 0, s, keys, pay, m, nres, (LAgg *)gsc.tile_agg,
+                       gsc.tile_valid);
+    hipLaunchKernelGGL(k_lruns_tiles, dim3(1), dim3(kT), 0, s, (const LAgg *)gsc.tile_agg, gsc.tile_valid, ntiles,
+                       (LAgg *)gsc.tile_carry, gsc.counters);
+    hipLaunchKernelGGL(k_lruns_down, dim3(ntiles), dim3(kT), 0, s, keys, pay, rt_p, nres, (const LAgg *)gsc.tile_carry,
+                       gsc);
+    hipLaunchKernelGGL(k_lexits, dim3(ntiles), dim3(kT), 0, s, pay, rt_p, gsc);
+    const uint32_t fthreads = std::min<uint32_t>(m, nres);
+    hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc,
+                       pay, keys, ts_base, rt_p, param_p, d_decision, wait_p);
+    hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
+                       st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
+                       heavy_prof());
+    hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, s, gsc, pay, d_decision);
+    hipLaunchKernelGGL(k_entry_stats, dim3(1), dim3(kEnTile), 0, s, st, (int64_t)cfg.statistic_max_rt, d_kind_in,
+                       d_resource, d_ts_off, ts_base, d_acquire, flags_p, rt_p, d_decision, m);
+    if (sys.check || d_param_values)
+        hipLaunchKernelGGL(k_lseq, dim3(1), dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, sys, d_kind_in,
+                           d_resource, d_ts_off, ts_base, d_acquire, flags_p, rt_p, param_p, m, d_decision, wait_p,
+                           d_param_values);
+    hipLaunchKernelGGL(k_lfail, dim3(gb), dim3(kT), 0, s, d_gate.p, d_overflow.p, d_gate.p + 1, m, d_decision, wait_p);
+    SGA_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int FlowEngine::device_status() {
+    if (!d_gate.p) return 0;
+    uint32_t e = 0;
+    SGA_HIP_CHECK(hipMemcpyAsync(&e, d_gate.p + 1, 4, hipMemcpyDeviceToHost, stream));
+    SGA_HIP_CHECK(hipMemsetAsync(d_gate.p + 1, 0, 4, stream));
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    if (e & 1u) return SGA_EINVAL;
+    if (e & 2u) return SGA_ENOMEM;
     return 0;
 }
 

@@ -101,6 +101,9 @@ struct FlowState {
     // embedded cluster token server for cluster-mode FlowRules (sga_set_cluster_server 1)
     ClusterState cst;
     int32_t cluster_on;
+    // device entry (sga_submit_events_device): the chunk's gate word, written by k_lgate; nullptr on
+    // the host entry, which chooses the kernels itself
+    const uint32_t *gate;
 };
 
 struct FlowScratch {
@@ -121,6 +124,7 @@ struct FlowScratch {
     uint32_t *counters;
     RadixScratch radix;
     size_t cap = 0;
+    const uint32_t *gate = nullptr;  // as FlowState::gate
 };
 
 void print_heavy_prof();  // SGA_HEAVY_PROF=1 diagnostics (flow.hip)
@@ -190,6 +194,14 @@ struct FlowEngine {
                const uint8_t *flags, const int64_t *rt, const uint64_t *param, size_t n, int8_t *decision,
                int32_t *wait_ms, const uint64_t *pvals = nullptr, size_t npvals = 0);
     DevBuf<uint64_t> d_pvals;  // values of Collection / array arguments (SGA_EV_PARAM_LIST)
+    // the same over device buffers, asynchronous on s: one chunk of n <= max_batch events
+    int submit_device(const uint8_t *d_kind, const uint32_t *d_resource, int64_t ts_base, const uint32_t *d_ts_off,
+                      const int32_t *d_acquire, const uint8_t *d_flags, const int64_t *d_rt_in,
+                      const uint64_t *d_param_in, size_t n, const uint64_t *d_param_values, size_t n_values,
+                      int8_t *d_decision, int32_t *d_wait, hipStream_t s);
+    int device_status();  // sticky error of the device entry since the last call (host wait)
+    int ensure_scratch();
+    DevBuf<uint32_t> d_gate;  // [0] gate word of the running chunk, [1] sticky error bits
     int query(uint32_t resource, int64_t now, sga_node_view *out);
     int cb_state(uint32_t resource, uint32_t k);
     int metrics(int64_t now, sga_metric_node *out, size_t cap, size_t *n);

@@ -202,6 +202,40 @@ class LocalSentinel:
         check(rc, self.engine.handle, "submitEvents")
         return dec, wait
 
+    def submit_device(self, kind, resource, ts_base, ts_off, acquire, flags=None, rt=None, param=None,
+                      param_values=None, decision=None, wait=None, stream=None):
+        """submit over device tensors (torch, on the engine's GPU), asynchronous on `stream` (torch stream or
+        None = the engine stream): one chunk of at most max_batch events with timestamps ts_base + ts_off.
+        Returns (decision int8, wait int32) device tensors; device_status() reports a chunk the device
+        checks rejected (rc -EINVAL) or a full parameter map (rc -ENOMEM) as EngineError."""
+        import torch
+        n = kind.numel()
+        for x in (resource, ts_off, acquire) + tuple(v for v in (flags, rt, param) if v is not None):
+            if x.numel() != n or not x.is_cuda or not x.is_contiguous():
+                raise ValueError("event tensors must be contiguous device tensors of one length")
+        want = {"kind": (kind, torch.uint8), "resource": (resource, torch.int32), "ts_off": (ts_off, torch.int32),
+                "acquire": (acquire, torch.int32), "flags": (flags, torch.uint8), "rt": (rt, torch.int64),
+                "param": (param, torch.int64), "param_values": (param_values, torch.int64)}
+        for name, (x, dt) in want.items():
+            if x is not None and x.element_size() != torch.empty(0, dtype=dt).element_size():
+                raise ValueError(f"{name}: element size of {dt} expected")
+        if decision is None:
+            decision = torch.empty(n, dtype=torch.int8, device=kind.device)
+        if wait is None:
+            wait = torch.empty(n, dtype=torch.int32, device=kind.device)
+        ptr = (lambda x: x.data_ptr() if x is not None else None)
+        rc = _lib.load().sga_submit_events_device(
+            self.engine.handle, kind.data_ptr(), resource.data_ptr(), int(ts_base), ts_off.data_ptr(),
+            acquire.data_ptr(), ptr(flags), ptr(rt), ptr(param), n, ptr(param_values),
+            param_values.numel() if param_values is not None else 0, decision.data_ptr(), wait.data_ptr(),
+            stream.cuda_stream if stream is not None else None)
+        check(rc, self.engine.handle, "submitEventsDevice")
+        return decision, wait
+
+    def device_status(self):
+        """Waits for the engine stream; EngineError for a rejected device chunk or a full parameter map."""
+        check(_lib.load().sga_events_device_status(self.engine.handle), self.engine.handle, "submitEventsDevice")
+
     # ---- SphU-style single entry
     def entry(self, resource: str, now: int, batch_count: int = 1, prioritized: bool = False, args=(),
               entry_type: str = "OUT") -> Entry:
