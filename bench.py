@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--rules", type=int, default=N_RULES)
     ap.add_argument("--cpu-sample", type=int, default=1 << 25, help="oracle replay sample (requests)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c5a", "c5b"],
+                    help="BASELINE.json configuration (SURVEY.md 8(d)); c3 = the headline, the others run on one "
+                         "GPU through bench_local.py")
     return ap.parse_args()
 
 
@@ -67,6 +70,12 @@ def launch_ranks(args):
 
 def main():
     args = parse()
+    if args.config != "c3":
+        if args.gpus != 1:
+            raise SystemExit("bench.py: --config c1/c2/c4/c5a/c5b run on one GPU")
+        import bench_local
+        bench_local.run(args)
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))

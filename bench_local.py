@@ -1,0 +1,373 @@
+"""`python bench.py --config c1|c2|c4|c5a|c5b`: the other BASELINE.json configurations (SURVEY.md 8(d)
+table) through the device-resident entries, one JSON line each (bench.py's contract; one GPU).
+
+A step is one pass of the local slot chain over one pre-generated, HBM-resident batch: the batch's
+entries (sga_submit_events_device), then the exits of the entries that passed (their resource id is
+masked to "unknown", a no-op, on the device when the entry was blocked -- a blocked SphU.entry
+returns no Entry to exit).  C5a is the Envoy RLS service (sga_rls_should_rate_limit_device).  Every
+step shifts the batch's clock past the previous one, so each step is new virtual time.
+
+value = entries (C5a: descriptors) decided per second of wall time over the K timed steps.
+roofline.achieved = the algorithmic bytes of SURVEY.md 8(d) (N*(E_in+E_out) + per batch, per touched
+key, 2*S_k) / the GPU time of the steps (torch events on the one stream every call runs on).
+cpu_baseline = the C oracle (oracle/, test infrastructure) replaying a bounded sample of the same
+batch on one host thread."""
+import json
+import time
+
+import numpy as np
+
+T0 = 1_700_000_000_000
+HBM_PEAK_GBS = 8000.0
+KIND_ENTRY, KIND_EXIT = 0, 1
+EV_ERROR, EV_HAS_PARAM = 2, 4
+# E_in / E_out and per-key state bytes S_k
+E_ENTRY, E_PARAM_ENTRY, E_EXIT, E_DEC = 12, 20, 12, 1
+E_RLS_IN, E_RLS_OUT, S_RLS = 12, 8, 72
+S_NODE, S_WARMUP_EXTRA, S_RL, S_WU, S_WURL = 192, 64, 8, 16, 24
+S_PARAM, S_PARAM_THROTTLE, S_BREAKER = 24, 16, 32
+
+
+def _zipf(rng, n_items, size, s=1.1):
+    p = 1.0 / np.arange(1, n_items + 1) ** s
+    p /= p.sum()
+    return rng.choice(n_items, size=size, p=p)
+
+
+class Batch:
+    """One batch: entries, then exits (exit i belongs to entry exit_of[i]); host arrays."""
+
+    def __init__(self, res, ts, acq=None, flags=None, param=None, exit_rt=None, exit_err=None):
+        n = len(res)
+        self.n = n
+        self.res = res.astype(np.uint32)
+        self.ts = ts.astype(np.int64)
+        self.acq = (np.ones(n) if acq is None else acq).astype(np.int32)
+        self.flags = (np.zeros(n) if flags is None else flags).astype(np.uint8)
+        self.param = (np.zeros(n) if param is None else param).astype(np.uint64)
+        self.exit_of = None
+        if exit_rt is not None:
+            ets = self.ts + exit_rt.astype(np.int64)
+            order = np.argsort(ets, kind="stable")
+            self.exit_of = order.astype(np.int64)
+            self.exit_ts = ets[order]
+            self.exit_rt = exit_rt.astype(np.int64)[order]
+            self.exit_flags = (self.flags[order] & EV_HAS_PARAM) | \
+                (np.zeros(n, np.uint8) if exit_err is None else (exit_err[order] * EV_ERROR).astype(np.uint8))
+        self.t_lo = int(min(self.ts.min(), self.exit_ts.min() if self.exit_of is not None else self.ts.min()))
+        self.t_hi = int(max(self.ts.max(), self.exit_ts.max() if self.exit_of is not None else self.ts.max()))
+
+
+def _cfg_c1(rng):
+    n = 1_000_000
+    ts = T0 + np.arange(n) // 20  # lambda = 20 events / ms, 50 virtual s
+    b = Batch(np.zeros(n), ts, exit_rt=rng.integers(0, 6, size=n))
+    return dict(name="C1 HelloWorld: 1 FlowRule QPS 20 DefaultController, 1M entries + exits",
+                n_res=1, flow=[dict(resource=0, count=20.0)], batch=b, sample=n)
+
+
+def _cfg_c2(rng):
+    n_res, n = 100_000, 1 << 24
+    flow = []
+    beh = rng.random(n_res)
+    cnt = rng.integers(5, 5001, size=n_res)
+    for r in range(n_res):
+        if beh[r] < 0.4:
+            flow.append(dict(resource=r, count=float(cnt[r])))
+        elif beh[r] < 0.7:
+            flow.append(dict(resource=r, count=float(cnt[r]), control_behavior=2, max_queueing_time_ms=500))
+        else:
+            flow.append(dict(resource=r, count=float(cnt[r]), control_behavior=1, warm_up_period_sec=10))
+    res = _zipf(rng, n_res, n)
+    ts = T0 + np.arange(n) // 10_000  # lambda = 1e7 / virtual s
+    acq = np.where(rng.random(n) < 0.05, rng.integers(2, 6, size=n), 1)
+    b = Batch(res, ts, acq=acq, exit_rt=rng.geometric(1.0 / 5.0, size=n))
+    return dict(name="C2 100k FlowRules 40% Default / 30% RateLimiter(500 ms) / 30% WarmUp(10 s), Zipf(1.1), "
+                     "2^24 entries + exits per batch",
+                n_res=n_res, flow=flow, batch=b, sample=1 << 21)
+
+
+def _cfg_c4(rng):
+    n_res, n = 10_000, 1 << 22
+    param = []
+    for r in range(n_res):
+        p = dict(resource=r, count=float(rng.integers(5, 101)))
+        if rng.random() < 0.1:
+            p.update(control_behavior=2, max_queueing_time_ms=0)
+        param.append(p)
+    res = _zipf(rng, n_res, n)
+    vals = _zipf(rng, 10_000_000, n) % 4000  # pinned mode: <= 4000 keys per rule (no CacheMap eviction)
+    ts = T0 + np.arange(n) // 10_000
+    b = Batch(res, ts, flags=np.full(n, EV_HAS_PARAM), param=vals, exit_rt=rng.integers(1, 30, size=n))
+    return dict(name="C4 10k ParamFlowRules (90% default / 10% throttle), Zipf(1.1) values over 10^7 folded to "
+                     "<= 4000 per rule (pinned mode), 2^22 entries + exits per batch",
+                n_res=n_res, param=param, batch=b, sample=1 << 20)
+
+
+def _cfg_c5b(rng):
+    n_res, n = 10_000, 1 << 22
+    degrade = []
+    for r in range(n_res):
+        if r % 2 == 0:
+            degrade.append(dict(resource=r, grade=0, count=50.0, slow_ratio_threshold=0.5, min_request_amount=5,
+                                stat_interval_ms=1000, time_window=5))
+        else:
+            degrade.append(dict(resource=r, grade=1, count=0.2, min_request_amount=5, stat_interval_ms=1000,
+                                time_window=5))
+    res = _zipf(rng, n_res, n)
+    ts = T0 + np.arange(n) // 10_000
+    rt = np.clip(np.round(rng.lognormal(mean=np.log(20.0), sigma=1.0, size=n)), 1, 10_000)
+    b = Batch(res, ts, exit_rt=rt, exit_err=rng.random(n) < 0.03)
+    return dict(name="C5b DegradeSlot: 10k DegradeRules (50% slow-RT 50 ms / 50% exception ratio 0.2), lognormal "
+                     "RT (median 20 ms), 3% errors, 2^22 entries + exits per batch",
+                n_res=n_res, degrade=degrade, batch=b, sample=1 << 20)
+
+
+def _load_rules(s, cfg):
+    from sentinel_amd.local import DegradeRuleManager, FlowRuleManager, ParamFlowRuleManager
+    from sentinel_amd.rules import DegradeRule, FlowRule, ParamFlowRule
+    if cfg.get("flow"):
+        FlowRuleManager(s).load_rules([FlowRule(resource=f"r{r['resource']}", **{k: v for k, v in r.items()
+                                                                                  if k != "resource"})
+                                       for r in cfg["flow"]])
+    if cfg.get("param"):
+        ParamFlowRuleManager(s).load_rules([ParamFlowRule(resource=f"r{r['resource']}",
+                                                          **{k: v for k, v in r.items() if k != "resource"})
+                                            for r in cfg["param"]])
+    if cfg.get("degrade"):
+        DegradeRuleManager(s).load_rules([DegradeRule(resource=f"r{r['resource']}",
+                                                      **{k: v for k, v in r.items() if k != "resource"})
+                                          for r in cfg["degrade"]])
+
+
+def _state_bytes(cfg, b):
+    """Sum over the batch's touched keys of 2 * S_k."""
+    touched = np.unique(b.res)
+    per_res = np.full(cfg["n_res"], S_NODE, np.int64)
+    for r in cfg.get("flow", []):
+        cb = r.get("control_behavior", 0)
+        per_res[r["resource"]] += {0: 0, 1: S_WARMUP_EXTRA + S_WU, 2: S_RL, 3: S_WARMUP_EXTRA + S_WURL}[cb]
+    for r in cfg.get("degrade", []):
+        per_res[r["resource"]] += S_BREAKER
+    total = int(per_res[touched].sum())
+    if cfg.get("param"):
+        thr = np.zeros(cfg["n_res"], bool)
+        for r in cfg["param"]:
+            thr[r["resource"]] = r.get("control_behavior", 0) == 2
+        keys = np.unique(b.res.astype(np.uint64) << np.uint64(32) | b.param.astype(np.uint64))
+        kr = (keys >> np.uint64(32)).astype(np.int64)
+        total += int(np.where(thr[kr], S_PARAM_THROTTLE, S_PARAM).sum())
+    return 2 * total
+
+
+def _cpu_local(cfg, b):
+    """One host thread: the C oracle replays the first `sample` entries, then their exits (masked by
+    the oracle's own decisions, as the GPU masks by its decisions)."""
+    from tests import local_trace as lt
+    m = min(cfg["sample"], b.n)
+    orc = lt.Oracle(cfg["n_res"], cfg.get("flow", []), cfg.get("param", []), cfg.get("degrade", []))
+    ent = {"kind": np.zeros(m, np.uint8), "resource": b.res[:m], "ts": b.ts[:m], "acquire": b.acq[:m],
+           "flags": b.flags[:m], "rt": np.zeros(m, np.int64), "param": b.param[:m]}
+    t0 = time.perf_counter()
+    dec, _ = orc.replay(ent)
+    dt = time.perf_counter() - t0
+    n_ev = m
+    if b.exit_of is not None:
+        sel = b.exit_of[b.exit_of < m]
+        ok = (dec[sel] == 0) | (dec[sel] == 4)
+        sel = sel[ok]
+        # exit times / rt / flags of the selected entries, in the batch's exit order
+        pos = np.empty(b.n, np.int64)
+        pos[b.exit_of] = np.arange(b.n)
+        order = np.sort(pos[sel])
+        ex = {"kind": np.ones(len(order), np.uint8), "resource": b.res[b.exit_of[order]], "ts": b.exit_ts[order],
+              "acquire": b.acq[b.exit_of[order]], "flags": b.exit_flags[order], "rt": b.exit_rt[order],
+              "param": b.param[b.exit_of[order]]}
+        t0 = time.perf_counter()
+        orc.replay(ex)
+        dt += time.perf_counter() - t0
+        n_ev += len(order)
+    orc.close()
+    return {"value": m / dt, "unit": "decisions/s", "cores": 1, "kind": "port",
+            "events_per_s": n_ev / dt,
+            "sample": f"the first {m} entries of the batch and the exits of those that passed ({n_ev} events), "
+                      f"replayed by the C oracle (oracle/sentinel_oracle.c slot-chain restatement), one thread"}
+
+
+def run_local(args, cfg_name):
+    import torch
+    from sentinel_amd.cluster import Engine
+    from sentinel_amd.local import LocalSentinel
+    rng = np.random.default_rng({"c1": 101, "c2": 102, "c4": 104, "c5b": 105}[cfg_name])
+    cfg = {"c1": _cfg_c1, "c2": _cfg_c2, "c4": _cfg_c4, "c5b": _cfg_c5b}[cfg_name](rng)
+    b = cfg["batch"]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    eng = Engine(device=0, max_batch=b.n)
+    s = LocalSentinel(eng, [f"r{i}" for i in range(cfg["n_res"])])
+    _load_rules(s, cfg)
+    stream = torch.cuda.Stream(dev)  # every call and the exit masking run on this one stream
+    torch.cuda.set_stream(stream)
+
+    def up(a, dt):
+        return torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(dev)
+
+    span = b.t_hi - b.t_lo + 1000
+    e_kind = torch.zeros(b.n, dtype=torch.uint8, device=dev)
+    e_res, e_acq = up(b.res, np.int32), up(b.acq, np.int32)
+    e_flags, e_param = up(b.flags, np.uint8), up(b.param, np.int64)
+    e_off = up((b.ts - b.t_lo).astype(np.uint32), np.int32)
+    dec = torch.empty(b.n, dtype=torch.int8, device=dev)
+    wait = torch.empty(b.n, dtype=torch.int32, device=dev)
+    has_exit = b.exit_of is not None
+    if has_exit:
+        x_kind = torch.ones(b.n, dtype=torch.uint8, device=dev)
+        x_of = up(b.exit_of, np.int64)
+        x_res_all = e_res[x_of]
+        x_acq = e_acq[x_of].contiguous()
+        x_param = e_param[x_of].contiguous()
+        x_flags = up(b.exit_flags, np.uint8)
+        x_rt = up(b.exit_rt, np.int64)
+        x_off = up((b.exit_ts - b.t_lo).astype(np.uint32), np.int32)
+        x_dec = torch.empty(b.n, dtype=torch.int8, device=dev)
+        unknown = torch.tensor(cfg["n_res"], dtype=torch.int32, device=dev)
+
+    def step(k):
+        base = b.t_lo + k * span
+        s.submit_device(e_kind, e_res, base, e_off, e_acq, flags=e_flags, param=e_param, decision=dec, wait=wait,
+                        stream=stream)
+        if has_exit:
+            d = dec[x_of]
+            x_res = torch.where((d == 0) | (d == 4), x_res_all, unknown)
+            s.submit_device(x_kind, x_res, base, x_off, x_acq, flags=x_flags, rt=x_rt, param=x_param,
+                            decision=x_dec, wait=None, stream=stream)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize(dev)
+    s.device_status()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for k in range(args.warmup, args.warmup + args.steps):
+        step(k)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    s.device_status()  # raises if a chunk was rejected or a parameter map filled
+    gpu_s = ev0.elapsed_time(ev1) / 1e3
+    d = dec.cpu().numpy()
+    n_ent = b.n * args.steps
+    n_exit = int(((d == 0) | (d == 4)).sum()) * args.steps if has_exit else 0
+    e_in = E_PARAM_ENTRY if cfg.get("param") else E_ENTRY
+    bytes_alg = n_ent * (e_in + E_DEC) + n_exit * E_EXIT + _state_bytes(cfg, b) * args.steps
+    achieved = bytes_alg / gpu_s / 1e9
+    cpu = None if args.no_cpu else _cpu_local(cfg, b)
+    eng.close()
+    return {
+        "metric": f"admission decisions/sec, config {cfg_name.upper()} (SURVEY.md 8(d)); % HBM peak",
+        "value": n_ent / wall, "unit": "decisions/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "int64", "data": "synthetic (numpy, seeded), staged in HBM before the timed region",
+        "config": {"workload": cfg["name"], "entries_per_step": b.n, "exits_per_step": n_exit // max(1, args.steps),
+                   "resources": cfg["n_res"], "parallelism": "shard1"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "sga_submit_events_device pipeline (entries, then masked exits), torch events on "
+                               "the stream every call runs on",
+                     "bytes_alg_per_step": bytes_alg / args.steps, "gpu_ms_per_step": gpu_s / args.steps * 1e3,
+                     "lower_bound_bytes_per_step": (n_ent * (e_in + E_DEC) + n_exit * E_EXIT) / args.steps},
+        "cpu_baseline": cpu,
+        "pass_fraction": float(((d == 0) | (d == 4)).mean()),
+    }
+
+
+def run_rls(args):
+    """C5a: Envoy RLS, 100k descriptor rules (count U{10..1000}), 1-4 descriptors per request,
+    hitsAddend 1, Zipf(1.1) descriptors; 2^20 requests per step."""
+    import torch
+    from sentinel_amd import cluster
+    from tests import oracle_harness as H
+    rng = np.random.default_rng(0x53454E55)
+    n_rules, nreq = 100_000, 1 << 20
+    fids = np.arange(1, n_rules + 1, dtype=np.int64) * 7919 + 2147483647
+    counts = rng.integers(10, 1001, size=n_rules)
+    ndesc = rng.integers(1, 5, size=nreq)
+    off = np.concatenate([[0], np.cumsum(ndesc)]).astype(np.uint32)
+    nd = int(off[-1])
+    dfid = fids[_zipf(rng, n_rules, nd)]
+    hits = np.ones(nreq, np.int32)
+    ts = (np.arange(nreq) // 4_000).astype(np.int64)  # 1e7 descriptors / virtual s
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    eng = cluster.Engine(device=0, max_batch=nd)
+    cluster.ClusterFlowRuleManager(eng).load_rule_arrays("default", fids, counts, threshold_type=1, sample_count=1)
+    svc = cluster.EnvoyRlsService(eng)
+    up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d_off, d_fid, d_hits, d_ts = up(off.view(np.int32)), up(dfid), up(hits), up(ts.astype(np.uint32).view(np.int32))
+    span = int(ts.max()) + 1000
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    out = {}
+
+    def step(k):
+        out["r"] = svc.should_rate_limit_device(d_off, d_fid, d_hits, T0 + k * span, d_ts, stream=stream)
+
+    for k in range(args.warmup):
+        step(k)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for k in range(args.warmup, args.warmup + args.steps):
+        step(k)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    gpu_s = ev0.elapsed_time(ev1) / 1e3
+    code = out["r"][0].cpu().numpy()
+    touched = len(np.unique(dfid))
+    bytes_alg = (nd * (E_RLS_IN + E_RLS_OUT) + 2 * touched * S_RLS) * args.steps
+    achieved = bytes_alg / gpu_s / 1e9
+    eng.close()
+    cpu = None
+    if not args.no_cpu:
+        L = H.lib()
+        oh = L.orc_cluster_new(1.0, 1.0)
+        arr = H.cluster_rules_array([{"flow_id": int(f), "count": float(c), "threshold_type": 1, "sample_count": 1}
+                                     for f, c in zip(fids, counts)])
+        L.orc_cluster_load_rules(oh, b"default", arr, n_rules)
+        m = min(nd, 1 << 21)
+        dts = (T0 + np.repeat(ts, ndesc))[:m].astype(np.int64)
+        f_s = np.ascontiguousarray(dfid[:m])
+        a_s = np.ones(m, np.int32)
+        res = (H.OrcTokenResult * m)()
+        t0 = time.perf_counter()
+        L.orc_cluster_replay_simple(oh, m, f_s.ctypes.data, a_s.ctypes.data, dts.ctypes.data, res)
+        dt = time.perf_counter() - t0
+        L.orc_cluster_free(oh)
+        cpu = {"value": m / dt, "unit": "descriptors/s", "cores": 1, "kind": "port",
+               "sample": f"the first {m} descriptors of the batch, replayed by the C oracle's "
+                         f"SimpleClusterFlowChecker restatement (oracle/sentinel_oracle.c), one thread"}
+    return {
+        "metric": "admission decisions/sec, config C5A (Envoy RLS descriptors, SURVEY.md 8(d)); % HBM peak",
+        "value": nd * args.steps / wall, "unit": "descriptors/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int64", "data": "synthetic (numpy, seeded), staged in HBM",
+        "config": {"workload": "C5a Envoy RLS: 100k descriptor rules (count U{10..1000}, sampleCount 1), 1-4 "
+                               "descriptors per request, Zipf(1.1), 2^20 requests per step",
+                   "requests_per_step": nreq, "descriptors_per_step": nd, "parallelism": "shard1"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "sga_rls_should_rate_limit_device pipeline, torch events on its stream",
+                     "bytes_alg_per_step": bytes_alg / args.steps, "gpu_ms_per_step": gpu_s / args.steps * 1e3},
+        "cpu_baseline": cpu,
+        "over_limit_fraction": float((code == 2).mean()),
+    }
+
+
+def run(args):
+    name = args.config.lower()
+    line = run_rls(args) if name == "c5a" else run_local(args, name)
+    print(json.dumps(line), flush=True)

@@ -321,6 +321,14 @@ int sga_concurrent_get_token(sga_engine *e, int64_t token_id, sga_token_cache_no
 int sga_rls_should_rate_limit(sga_engine *e, const uint32_t *desc_offsets, size_t n_requests,
                               const int64_t *desc_flow_id, const int32_t *hits_addend, const int64_t *ts,
                               int8_t *desc_status, int32_t *desc_remaining, int32_t *code);
+/* The same over DEVICE buffers, asynchronous on `hip_stream` with the stream ordering of
+ * sga_request_tokens_device: desc_offsets[n_requests + 1] (offsets[n_requests] = n_descriptors
+ * <= max_batch), request times ts_base + ts_off[r].  d_desc_status / d_desc_remaining may be NULL. */
+int sga_rls_should_rate_limit_device(sga_engine *e, const uint32_t *d_desc_offsets, size_t n_requests,
+                                     size_t n_descriptors, const int64_t *d_desc_flow_id,
+                                     const int32_t *d_hits_addend, int64_t ts_base, const uint32_t *d_ts_off,
+                                     int8_t *d_desc_status, int32_t *d_desc_remaining, int32_t *d_code,
+                                     void *hip_stream);
 
 /* ---------------------------------------------------------------------------
  * Local path: resources are dense ids 0..n_resources-1 (the host keeps the

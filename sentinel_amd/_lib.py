@@ -157,6 +157,9 @@ SIGNATURES = {
                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                            C.c_void_p, C.c_void_p, C.c_void_p]),
     "sga_events_device_status": (C.c_int, [C.c_void_p]),
+    "sga_rls_should_rate_limit_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p,
+                                                   C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                   C.c_void_p, C.c_void_p]),
     "sga_query_node": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int64, C.POINTER(SgaNodeView)]),
     "sga_circuit_breaker_state": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
     "sga_metrics_snapshot": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),

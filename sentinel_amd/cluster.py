@@ -482,3 +482,27 @@ class EnvoyRlsService:
         check(rc, self.engine.handle, "shouldRateLimit")
         n = len(fid)
         return (code[:nreq], st[:n], rem[:n]) if with_remaining else (code[:nreq], st[:n])
+
+    def should_rate_limit_device(self, desc_offsets, desc_flow_id, hits_addend, ts_base, ts_off, stream=None):
+        """shouldRateLimit over device tensors (uint32/int32 offsets [n+1], int64 flowIds, int32 hits,
+        request times ts_base + ts_off), asynchronous on `stream` (torch stream or None = engine
+        stream).  Returns device tensors (code int32 per request, status int8 and remaining int32 per
+        descriptor)."""
+        import torch
+        nreq = hits_addend.numel()
+        nd = desc_flow_id.numel()
+        if desc_offsets.numel() != nreq + 1 or ts_off.numel() != nreq:
+            raise ValueError("desc_offsets must have n_requests + 1 entries; ts_off one per request")
+        for x in (desc_offsets, desc_flow_id, hits_addend, ts_off):
+            if not x.is_cuda or not x.is_contiguous():
+                raise ValueError("inputs must be contiguous device tensors")
+        dev = hits_addend.device
+        code = torch.empty(nreq, dtype=torch.int32, device=dev)
+        st = torch.empty(max(nd, 1), dtype=torch.int8, device=dev)
+        rem = torch.empty(max(nd, 1), dtype=torch.int32, device=dev)
+        rc = _lib.load().sga_rls_should_rate_limit_device(
+            self.engine.handle, desc_offsets.data_ptr(), nreq, nd, desc_flow_id.data_ptr(), hits_addend.data_ptr(),
+            int(ts_base), ts_off.data_ptr(), st.data_ptr(), rem.data_ptr(), code.data_ptr(),
+            stream.cuda_stream if stream is not None else None)
+        check(rc, self.engine.handle, "shouldRateLimit")
+        return code, st[:nd], rem[:nd]

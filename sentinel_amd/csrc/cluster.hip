@@ -1989,7 +1989,7 @@ __global__ __launch_bounds__(kFinWgThreads) void k_hot_final(BatchScratch sc, ui
     for (uint32_t h = threadIdx.x; h < nhot; h += kFinWgThreads) base[h] = sc.hbase[(size_t)seg * kHot + h];
     __syncthreads();
     const uint32_t b0 = s_b0;
-    const uint32_t ncache = min(nhot, cache_cap & 0xFFFFu);
+    const uint32_t ncache = min(nhot, cache_cap);
     for (uint32_t h = threadIdx.x; h < ncache; h += kFinWgThreads) {
         c_ti[h] = sc.hthr[h];
 #pragma unroll
@@ -2013,7 +2013,7 @@ __global__ __launch_bounds__(kFinWgThreads) void k_hot_final(BatchScratch sc, ui
         const uint32_t i = wbase + u * 64 + lane;
         code[u] = (i < wend && !(cn[u] >> 31)) ? cn[u] : kNoCode;  // prioritized: k_prio_results
         const uint32_t cd = code[u];
-        hit[u] = cd == kNoCode || ((cd & 0xFFFu) < (cache_cap & 0xFFFFu) && (cd >> 25) - b0 < 2u);
+        hit[u] = cd == kNoCode || ((cd & 0xFFFu) < cache_cap && (cd >> 25) - b0 < 2u);
         const size_t at = hit[u] ? 0 : (size_t)(cd & 0xFFFu) * kHotBuckets + (cd >> 25);
         const uint4 *hp = reinterpret_cast<const uint4 *>(sc.hrun + at);
         ra[u] = hp[0];  // s0, thr
@@ -2022,10 +2022,7 @@ __global__ __launch_bounds__(kFinWgThreads) void k_hot_final(BatchScratch sc, ui
 #pragma unroll
     for (int u = 0; u < kFinChunk; ++u) {
         const uint32_t cd = code[u];
-        if (cd == kNoCode) {
-            if (cache_cap & 0x10000u) out[wbase + u * 64 + lane] = 0;  // timing experiment only
-            continue;
-        }
+        if (cd == kNoCode) continue;
         const uint32_t h = cd & 0xFFFu, k = ((cd >> 25) - b0) & 1u;
         int64_t s0;
         double thr, isec;
@@ -2908,7 +2905,7 @@ static int fz_debug() {
 }
 
 static uint32_t fin_cache() {  // profiling knob: SGA_FIN_CACHE=0 turns k_hot_final's LDS cache off
-    static const uint32_t v = getenv("SGA_FIN_CACHE") ? (uint32_t)atoi(getenv("SGA_FIN_CACHE")) : kFinCache;
+    static const uint32_t v = getenv("SGA_FIN_CACHE") ? std::min<uint32_t>(atoi(getenv("SGA_FIN_CACHE")), kFinCache) : kFinCache;
     return v;
 }
 
@@ -3273,6 +3270,61 @@ void cluster_metric_nodes(const ClusterState &st, const int64_t *slot_fid, int64
 
 void cluster_init_limiter(NsLimiterDev *d, hipStream_t s) {
     hipLaunchKernelGGL(k_lim_init, dim3(1), dim3(64), 0, s, d);
+}
+
+// ---- Envoy RLS over device buffers (SentinelEnvoyRlsServiceImpl.shouldRateLimit,
+// envoy/rls/SentinelEnvoyRlsServiceImpl.java:52-90): every descriptor of a request is one
+// SimpleClusterFlowChecker request at the request's time with acquire = hitsAddend (0 -> 1).
+// A request with hitsAddend < 0 checks nothing: its descriptors take flowId 0, which no rule can
+// hold (cluster rules need flowId > 0), so they answer NO_RULE_EXISTS without touching a window.
+__global__ __launch_bounds__(kThreads) void k_rls_expand(const uint32_t *__restrict__ off, uint32_t nreq,
+                                                         const int64_t *__restrict__ dfid,
+                                                         const int32_t *__restrict__ hits,
+                                                         const uint32_t *__restrict__ ts_off, int64_t *fid_out,
+                                                         int32_t *acq_out, uint32_t *ts_out) {
+    const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
+    if (r >= nreq) return;
+    const int32_t h = hits[r];
+    const int32_t a = h <= 0 ? 1 : h;
+    const uint32_t t = ts_off[r];
+    for (uint32_t d = off[r]; d < off[r + 1]; ++d) {
+        fid_out[d] = h < 0 ? 0 : dfid[d];
+        acq_out[d] = a;
+        ts_out[d] = t;
+    }
+}
+
+// Code.OVER_LIMIT (2) when a descriptor is neither OK nor NO_RULE_EXISTS, Code.OK (1) otherwise,
+// -1 for hitsAddend < 0 (onError); per descriptor the TokenResult status and remaining.
+__global__ __launch_bounds__(kThreads) void k_rls_finish(const uint32_t *__restrict__ off, uint32_t nreq,
+                                                         const int32_t *__restrict__ hits,
+                                                         const uint64_t *__restrict__ res, int8_t *desc_status,
+                                                         int32_t *desc_rem, int32_t *code) {
+    const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
+    if (r >= nreq) return;
+    const bool skip = hits[r] < 0;
+    bool blocked = false;
+    for (uint32_t d = off[r]; d < off[r + 1]; ++d) {
+        const int8_t stt = skip ? (int8_t)TRS_NO_RULE_EXISTS : (int8_t)(res[d] >> 48);
+        blocked |= stt != TRS_OK && stt != TRS_NO_RULE_EXISTS;
+        if (desc_status) desc_status[d] = stt;
+        if (desc_rem) desc_rem[d] = skip ? 0 : (int32_t)(uint32_t)res[d];
+    }
+    code[r] = skip ? -1 : (blocked ? 2 : 1);
+}
+
+void rls_expand(const uint32_t *off, uint32_t nreq, const int64_t *dfid, const int32_t *hits, const uint32_t *ts_off,
+                int64_t *fid_out, int32_t *acq_out, uint32_t *ts_out, hipStream_t s) {
+    if (!nreq) return;
+    hipLaunchKernelGGL(k_rls_expand, dim3((nreq + kThreads - 1) / kThreads), dim3(kThreads), 0, s, off, nreq, dfid,
+                       hits, ts_off, fid_out, acq_out, ts_out);
+}
+
+void rls_finish(const uint32_t *off, uint32_t nreq, const int32_t *hits, const uint64_t *res, int8_t *desc_status,
+                int32_t *desc_rem, int32_t *code, hipStream_t s) {
+    if (!nreq) return;
+    hipLaunchKernelGGL(k_rls_finish, dim3((nreq + kThreads - 1) / kThreads), dim3(kThreads), 0, s, off, nreq, hits,
+                       res, desc_status, desc_rem, code);
 }
 
 void cluster_metric_sums(const ClusterState &st, uint32_t slot, int64_t now, int64_t *d_out7, hipStream_t s) {

@@ -290,6 +290,11 @@ void cluster_metric_nodes(const ClusterState &st, const int64_t *slot_fid, int64
 
 // Fresh limiter state (every bucket absent).
 void cluster_init_limiter(NsLimiterDev *d, hipStream_t stream);
+// Envoy RLS over device buffers: descriptors -> token requests, token results -> codes
+void rls_expand(const uint32_t *off, uint32_t nreq, const int64_t *dfid, const int32_t *hits, const uint32_t *ts_off,
+                int64_t *fid_out, int32_t *acq_out, uint32_t *ts_out, hipStream_t s);
+void rls_finish(const uint32_t *off, uint32_t nreq, const int32_t *hits, const uint64_t *res, int8_t *desc_status,
+                int32_t *desc_rem, int32_t *code, hipStream_t s);
 
 // ClusterMetric.getSum for all 7 events at `now` (rotates the current window as the reference does).
 void cluster_metric_sums(const ClusterState &st, uint32_t slot, int64_t now, int64_t *d_out7, hipStream_t stream);

@@ -1490,6 +1490,40 @@ int sga_rls_should_rate_limit(sga_engine *e, const uint32_t *desc_offsets, size_
     });
 }
 
+int sga_rls_should_rate_limit_device(sga_engine *e, const uint32_t *d_desc_offsets, size_t n_requests,
+                                     size_t n_descriptors, const int64_t *d_desc_flow_id,
+                                     const int32_t *d_hits_addend, int64_t ts_base, const uint32_t *d_ts_off,
+                                     int8_t *d_desc_status, int32_t *d_desc_remaining, int32_t *d_code,
+                                     void *hip_stream) {
+    if (n_requests && (!d_desc_offsets || !d_hits_addend || !d_ts_off || !d_code)) return SGA_EINVAL;
+    if (n_descriptors && !d_desc_flow_id) return SGA_EINVAL;
+    if (ts_base < 0) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        if (n_descriptors > g.cfg.max_batch || n_requests > g.cfg.max_batch) return SGA_ERANGE;
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        const size_t cap = g.cfg.max_batch;
+        if (g.d_in_fid.n < cap) {  // grown on the engine stream before a caller stream is ordered after it
+            g.d_in_fid.alloc(cap);
+            g.d_in_acq.alloc(cap);
+            g.d_in_prio.alloc(cap);
+            g.d_in_ts.alloc(cap);
+            g.d_out.alloc(cap);
+        }
+        hipStream_t s = g.enter_stream(hip_stream);
+        const auto lims = limiter_passes(g);
+        sga::rls_expand(d_desc_offsets, (uint32_t)n_requests, d_desc_flow_id, d_hits_addend, d_ts_off, g.d_in_fid.p,
+                        g.d_in_acq.p, g.d_in_ts.p, s);
+        if (n_descriptors)
+            sga::cluster_decide_batch(g.state(), g.scratch, g.d_in_fid.p, g.d_in_acq.p, nullptr, ts_base, g.d_in_ts.p,
+                                      (uint32_t)n_descriptors, 1, g.d_out.p, s, lims.data(), (int)lims.size());
+        sga::rls_finish(d_desc_offsets, (uint32_t)n_requests, d_hits_addend, g.d_out.p, d_desc_status,
+                        d_desc_remaining, d_code, s);
+        SGA_HIP_CHECK(hipGetLastError());
+        g.leave_stream(s);
+        return SGA_OK;
+    });
+}
+
 // ---------------------------------------------------------------- local path
 int sga_flow_set_resources(sga_engine *e, uint32_t n_resources) {
     if (n_resources == 0 || n_resources >= (1u << 30)) return SGA_EINVAL;

@@ -1182,6 +1182,208 @@ __device__ __forceinline__ bool default_cond(double count, int64_t sum, int32_t 
     return !((double)(int32_t)((uint32_t)cur + (uint32_t)a) > count);
 }
 
+// One run of a resource decided by one lane (k_lflows; k_lwave's lane 0 for runs it cannot split):
+// RateLimiter pacing in registers, the per-event slot chain, or the closed form (RUN_FAST: k_lresults
+// writes the decisions from run_f).
+__device__ void lane_run(const Ctx &c, int64_t max_rt, FlowScratch &sc, const Payload *__restrict__ pay,
+                         int64_t ts_base, const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in,
+                         int8_t *decision, int32_t *wait_ms, uint32_t r) {
+    const FlowState &st = c.st;
+    const uint32_t res = sc.run_slot[r];
+    const ResDev R = st.res[res];
+    int64_t *node = st.node + (size_t)res * kNodeWords;
+    const uint32_t j0 = sc.run_start[r], j1 = sc.run_end[r];
+    const uint32_t nent = sc.run_nent[r];
+    const int32_t a = sc.run_amin[r];
+    const int64_t t0 = ts_base + (int64_t)sc.run_t0off[r];
+    bool fast = (R.fast & 1u) && sc.run_cp[r] == 0 && (nent == 0 || a == sc.run_amax[r]) && a >= 0;
+    bool pace = (R.fast & 4u) != 0;
+    if (fast || pace) {  // no clock regression in this resource's windows
+        const int64_t *sb = node + kNodeSec + kMB * (int)((t0 / kSecW) % 2);
+        const int64_t *mb = node + kNodeMin + kMB * (int)((t0 / kMinW) % 60);
+        if ((sb[0] != kAbsent && t0 - t0 % kSecW < sb[0]) || (mb[0] != kAbsent && t0 - t0 % kMinW < mb[0]))
+            fast = pace = false;
+    }
+    if (pace) {
+        // RateLimiterController alone (RateLimiterController.java:46-91): the decisions depend on
+        // latestPassedTime only, so the run's entries are paced in registers, in order; the run's
+        // statistics (one 500 ms bucket) are added once, like the closed form below.
+        FlowRuleDev &rule = st.rules[R.rule_off];
+        int64_t latest = rule.latest_passed;
+        // the rule fields in registers: the decision stores could alias them otherwise, and
+        // every reload would wait behind the previous stores
+        const double rcount = rule.count;
+        const int64_t rqueue = rule.max_queue;
+        int64_t pa = 0, ba = 0, npass = 0;
+        int last_aq = -1;  // Math.round(1.0 * acquire / count * 1000) of the last acquire count
+        int64_t last_cost = 0;
+        // decide one event in registers; returns its (index, decision, wait) for the store
+        auto pace_one = [&](const Payload &q, uint32_t &idx, int8_t &d, int32_t &wo) {
+            idx = q.idx & F_IDX;
+            d = D_PASS;
+            wo = 0;
+            if (q.idx & F_EXIT) return false;
+            const int64_t t = ts_base + (int64_t)q.ts_off;
+            const int aq = (int)(q.acq_prio & 0x7FFFFFFFu);
+            int64_t w = 0;
+            if (aq > 0) {
+                if (rcount <= 0) {
+                    d = D_BLOCK_FLOW;
+                } else {
+                    if (aq != last_aq) {
+                        last_aq = aq;
+                        last_cost = j_round(1.0 * aq / rcount * 1000);
+                    }
+                    const int64_t cost = last_cost;
+                    if (cost + latest <= t) {
+                        latest = t;
+                    } else if (cost + latest - t > rqueue) {
+                        d = D_BLOCK_FLOW;
+                    } else {
+                        latest += cost;
+                        w = latest - t;
+                        if (w > rqueue) {
+                            latest -= cost;
+                            d = D_BLOCK_FLOW;
+                            w = 0;
+                        } else if (w < 0) {
+                            w = 0;
+                        }
+                    }
+                }
+            }
+            wo = (int32_t)w;
+            if (d == D_PASS) {
+                pa += aq;
+                ++npass;
+            } else {
+                ba += aq;
+            }
+            return true;
+        };
+        // software pipeline: the next 4 payloads are loaded before this group's stores are
+        // issued, so a load never waits behind the previous group's scattered stores
+        constexpr uint32_t kG = 4;
+        const Payload none{F_EXIT, 0, 0, 0};
+        Payload c0 = j0 < j1 ? pay[j0] : none, c1 = j0 + 1 < j1 ? pay[j0 + 1] : none;
+        Payload c2 = j0 + 2 < j1 ? pay[j0 + 2] : none, c3 = j0 + 3 < j1 ? pay[j0 + 3] : none;
+        for (uint32_t g = j0; g < j1; g += kG) {
+            const uint32_t nx = g + kG;
+            const Payload n0 = nx < j1 ? pay[nx] : none, n1 = nx + 1 < j1 ? pay[nx + 1] : none;
+            const Payload n2 = nx + 2 < j1 ? pay[nx + 2] : none, n3 = nx + 3 < j1 ? pay[nx + 3] : none;
+            uint32_t i0, i1, i2, i3;
+            int8_t d0, d1, d2, d3;
+            int32_t w0, w1, w2, w3;
+            const bool v0 = pace_one(c0, i0, d0, w0), v1 = pace_one(c1, i1, d1, w1);
+            const bool v2 = pace_one(c2, i2, d2, w2), v3 = pace_one(c3, i3, d3, w3);
+            if (v0) { decision[i0] = d0; wait_ms[i0] = w0; }
+            if (v1) { decision[i1] = d1; wait_ms[i1] = w1; }
+            if (v2) { decision[i2] = d2; wait_ms[i2] = w2; }
+            if (v3) { decision[i3] = d3; wait_ms[i3] = w3; }
+            c0 = n0;
+            c1 = n1;
+            c2 = n2;
+            c3 = n3;
+        }
+        rule.latest_passed = latest;
+        int64_t *sb = sec_current(node, t0, max_rt);
+        int64_t *mb = min_current(node, t0, max_rt);
+        const int64_t exc = (int64_t)sc.run_exc[r], exerr = (int64_t)sc.run_exerr[r];
+        const int64_t exrt = sc.run_exrt[r], exmin = sc.run_exmin[r];
+        int64_t *w2[2] = {sb, mb};
+        for (int k = 0; k < 2; ++k) {
+            int64_t *b = w2[k];
+            b[MB_PASS] += pa;
+            b[MB_BLOCK] += ba;
+            b[MB_SUCC] += exc;
+            b[MB_RT] += exrt;
+            b[MB_EXC] += exerr;
+            if (exmin < b[MB_MINRT]) b[MB_MINRT] = exmin;
+        }
+        node[kNodeThreads] += npass - (int64_t)sc.run_nexit[r];
+        sc.run_mode[r] = RUN_DONE;
+        return;
+    }
+    if (fast && nent) {  // WarmUp sync must only see entries in one second (true: run is inside one 500 ms bucket)
+        const int64_t s0 = sec_sum(node, t0, MB_PASS);
+        if (s0 + (int64_t)nent * a + a >= (int64_t)INT32_MAX) fast = false;
+    }
+    if (!fast) {
+        for (uint32_t j = j0; j < j1; ++j) {
+            const Payload q = pay[j];
+            const int64_t t = ts_base + (int64_t)q.ts_off;
+            const uint32_t idx = q.idx & F_IDX;
+            const bool hp = (q.idx & F_PARAM) != 0;
+            const uint64_t pv = hp ? param_in[idx] : 0;
+            if (q.idx & F_EXIT) {
+                chain_exit(c, res, t, rt_in[idx], (int)(q.acq_prio & 0x7FFFFFFFu), (q.idx & F_ERROR) != 0, hp, pv);
+            } else {
+                int64_t w = 0;
+                decision[idx] = chain_entry(c, res, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
+                                            hp, pv, &w);
+                wait_ms[idx] = (int32_t)w;
+            }
+        }
+        sc.run_mode[r] = RUN_DONE;
+        return;
+    }
+    // ---- closed form: rotate both windows once at the run's first event
+    int64_t *sb = sec_current(node, t0, max_rt);
+    int64_t *mb = min_current(node, t0, max_rt);
+    uint32_t f = 0;
+    if (nent) {
+        FlowRuleDev &rule = st.rules[R.rule_off];
+        const int64_t s0 = sec_sum(node, t0, MB_PASS);
+        if (rule.behavior == 1) {
+            // WarmUpController: sync once (the run is inside one second), then a fixed threshold
+            const int64_t previous_qps = j_d2l(node_prev_pass_qps(c, node, t0));
+            warmup_sync(rule, t0, previous_qps);
+            const int64_t rest = rule.stored_tokens;
+            double lim;
+            if (rest >= rule.warning_token) {
+                const int64_t above = rest - rule.warning_token;
+                lim = j_next_up(1.0 / ((double)above * rule.slope + 1.0 / rule.count));
+            } else {
+                lim = rule.count;
+            }
+            uint32_t lo = 0, hi = nent;
+            while (lo < hi) {
+                const uint32_t mid = lo + ((hi - lo) >> 1);
+                const int64_t pq = j_d2l((double)(s0 + (int64_t)mid * a) / 1.0);
+                if ((double)(pq + a) <= lim) lo = mid + 1;
+                else hi = mid;
+            }
+            f = lo;
+        } else {
+            uint32_t lo = 0, hi = nent;
+            while (lo < hi) {
+                const uint32_t mid = lo + ((hi - lo) >> 1);
+                if (default_cond(rule.count, s0 + (int64_t)mid * a, a)) lo = mid + 1;
+                else hi = mid;
+            }
+            f = lo;
+        }
+    }
+    const int64_t pa = (int64_t)f * a, ba = (int64_t)(nent - f) * a;
+    const int64_t exc = (int64_t)sc.run_exc[r], exerr = (int64_t)sc.run_exerr[r];
+    const int64_t exrt = sc.run_exrt[r], exmin = sc.run_exmin[r];
+    sb[MB_PASS] += pa;
+    sb[MB_BLOCK] += ba;
+    sb[MB_SUCC] += exc;
+    sb[MB_RT] += exrt;
+    sb[MB_EXC] += exerr;
+    if (exmin < sb[MB_MINRT]) sb[MB_MINRT] = exmin;
+    mb[MB_PASS] += pa;
+    mb[MB_BLOCK] += ba;
+    mb[MB_SUCC] += exc;
+    mb[MB_RT] += exrt;
+    mb[MB_EXC] += exerr;
+    if (exmin < mb[MB_MINRT]) mb[MB_MINRT] = exmin;
+    node[kNodeThreads] += (int64_t)f - (int64_t)sc.run_nexit[r];
+    sc.run_f[r] = f;
+    sc.run_mode[r] = RUN_FAST;
+}
+
 __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, FlowScratch sc,
                                                const Payload *__restrict__ pay, const uint32_t *__restrict__ keys,
                                                int64_t ts_base, const int64_t *__restrict__ rt_in,
@@ -1195,109 +1397,174 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
         const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
         {  // a long event-by-event replay goes to k_lheavy (its state in LDS)
             const uint32_t res = sc.run_slot[r0];
-            if ((st.res[res].fast & 5u) == 0 && sc.run_end[r1 - 1] - sc.run_start[r0] >= kHeavyEvents) {
+            const uint32_t nev = sc.run_end[r1 - 1] - sc.run_start[r0];
+            if ((st.res[res].fast & 5u) == 0 && nev >= kHeavyEvents) {
                 sc.heavy[atomicAdd(&sc.counters[8], 1u)] = fl;
                 continue;
             }
+            if ((st.res[res].fast & 5u) && nev >= kHeavyEvents) {  // a long single-rule fast path: k_lwave
+                sc.pace[atomicAdd(&sc.counters[9], 1u)] = fl;
+                continue;
+            }
         }
+        for (uint32_t r = r0; r < r1; ++r)
+            lane_run(c, max_rt, sc, pay, ts_base, rt_in, param_in, decision, wait_ms, r);
+    }
+}
+
+// Heavy resources (many events, no closed form): one workgroup each; its node record, rules and
+// breakers are copied to LDS, lane 0 replays every event in order against the LDS copy (an LDS
+// round trip instead of a global one per state access), and the state is written back.
+constexpr int kHeavyRules = 16, kHeavyCbs = 16, kHeavyChunk = 512, kHeavySlots = 1024;
+// Resources with a long batch and a single-rule fast path (k_lflows sends them here), one wave each.
+// Both fast controllers decide an entry by a monotone test against state that only passing entries
+// move, so a window of 64 entries is decided by finding its first passing lane (a ballot), blocking
+// every open lane before it, applying that pass and repeating from the next lane:
+//   RateLimiterController alone (RateLimiterController.java:46-91): an entry passes iff
+//     cost + latest <= t or cost + latest - t <= maxQueueingTimeMs; a pass moves latestPassedTime;
+//   DefaultController / WarmUpController with mixed acquire counts (DefaultController.java:47-77,
+//     WarmUpController.java:115-138): an entry passes iff curCount(S) + acquire fits the run's fixed
+//     threshold, S the passed count so far; before the first block a window is one prefix sum.
+// A window costs one iteration per pass after its first block, instead of one dependent step per entry.
+// Runs with a uniform acquire keep the closed form, and runs that go back in time or hold prioritized
+// entries take lane_run on lane 0, exactly as in k_lflows.
+__global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, FlowScratch sc,
+                                              const Payload *__restrict__ pay, int64_t ts_base,
+                                              const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in,
+                                              int8_t *decision, int32_t *wait_ms) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    const Ctx c{st, max_rt};
+    const int lane = threadIdx.x;
+    const uint32_t nwave = sc.counters[9], nflows = sc.counters[2], nruns = sc.counters[1];
+    for (uint32_t h = blockIdx.x; h < nwave; h += gridDim.x) {
+        const uint32_t fl = sc.pace[h];
+        const uint32_t r0 = sc.flow_first_run[fl];
+        const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
         for (uint32_t r = r0; r < r1; ++r) {
             const uint32_t res = sc.run_slot[r];
             const ResDev R = st.res[res];
             int64_t *node = st.node + (size_t)res * kNodeWords;
             const uint32_t j0 = sc.run_start[r], j1 = sc.run_end[r];
             const uint32_t nent = sc.run_nent[r];
-            const int32_t a = sc.run_amin[r];
+            const int32_t amin = sc.run_amin[r], amax = sc.run_amax[r];
             const int64_t t0 = ts_base + (int64_t)sc.run_t0off[r];
-            bool fast = (R.fast & 1u) && sc.run_cp[r] == 0 && (nent == 0 || a == sc.run_amax[r]) && a >= 0;
-            bool pace = (R.fast & 4u) != 0;
-            if (fast || pace) {  // no clock regression in this resource's windows
+            bool regress;
+            {
                 const int64_t *sb = node + kNodeSec + kMB * (int)((t0 / kSecW) % 2);
                 const int64_t *mb = node + kNodeMin + kMB * (int)((t0 / kMinW) % 60);
-                if ((sb[0] != kAbsent && t0 - t0 % kSecW < sb[0]) || (mb[0] != kAbsent && t0 - t0 % kMinW < mb[0]))
-                    fast = pace = false;
+                regress = (sb[0] != kAbsent && t0 - t0 % kSecW < sb[0]) || (mb[0] != kAbsent && t0 - t0 % kMinW < mb[0]);
             }
-            if (pace) {
-                // RateLimiterController alone (RateLimiterController.java:46-91): the decisions depend on
-                // latestPassedTime only, so the run's entries are paced in registers, in order; the run's
-                // statistics (one 500 ms bucket) are added once, like the closed form below.
-                FlowRuleDev &rule = st.rules[R.rule_off];
-                int64_t latest = rule.latest_passed;
-                // the rule fields in registers: the decision stores could alias them otherwise, and
-                // every reload would wait behind the previous stores
-                const double rcount = rule.count;
-                const int64_t rqueue = rule.max_queue;
-                int64_t pa = 0, ba = 0, npass = 0;
-                int last_aq = -1;  // Math.round(1.0 * acquire / count * 1000) of the last acquire count
-                int64_t last_cost = 0;
-                // decide one event in registers; returns its (index, decision, wait) for the store
-                auto pace_one = [&](const Payload &q, uint32_t &idx, int8_t &d, int32_t &wo) {
-                    idx = q.idx & F_IDX;
-                    d = D_PASS;
-                    wo = 0;
-                    if (q.idx & F_EXIT) return false;
-                    const int64_t t = ts_base + (int64_t)q.ts_off;
-                    const int aq = (int)(q.acq_prio & 0x7FFFFFFFu);
-                    int64_t w = 0;
-                    if (aq > 0) {
-                        if (rcount <= 0) {
-                            d = D_BLOCK_FLOW;
-                        } else {
-                            if (aq != last_aq) {
-                                last_aq = aq;
-                                last_cost = j_round(1.0 * aq / rcount * 1000);
-                            }
-                            const int64_t cost = last_cost;
-                            if (cost + latest <= t) {
-                                latest = t;
-                            } else if (cost + latest - t > rqueue) {
-                                d = D_BLOCK_FLOW;
-                            } else {
-                                latest += cost;
-                                w = latest - t;
-                                if (w > rqueue) {
-                                    latest -= cost;
-                                    d = D_BLOCK_FLOW;
-                                    w = 0;
-                                } else if (w < 0) {
-                                    w = 0;
-                                }
-                            }
-                        }
+            const bool pace = (R.fast & 4u) && !regress;
+            bool greedy = (R.fast & 1u) && !regress && sc.run_cp[r] == 0 && amin >= 0 && nent > 0 && amin != amax;
+            FlowRuleDev &rule = st.rules[R.rule_off];
+            int64_t s0 = 0;
+            double lim = 0;
+            if (greedy) {  // the closed form's prologue: rotate once, the run's fixed threshold
+                if (lane == 0) {
+                    sec_current(node, t0, max_rt);
+                    min_current(node, t0, max_rt);
+                    s0 = sec_sum(node, t0, MB_PASS);
+                    if (rule.behavior == 1 && s0 + (int64_t)nent * amax + amax >= (int64_t)INT32_MAX) {
+                        lim = -1;  // the int passQps could overflow: per-event chain
+                    } else if (rule.behavior == 1) {
+                        warmup_sync(rule, t0, j_d2l(node_prev_pass_qps(c, node, t0)));
+                        const int64_t rest = rule.stored_tokens;
+                        lim = rest >= rule.warning_token
+                                  ? j_next_up(1.0 / ((double)(rest - rule.warning_token) * rule.slope + 1.0 / rule.count))
+                                  : rule.count;
+                    } else {
+                        lim = rule.count;
                     }
-                    wo = (int32_t)w;
+                }
+                s0 = __shfl(s0, 0);
+                lim = __shfl(lim, 0);
+                if (rule.behavior == 1 && lim == -1) greedy = false;
+            }
+            if (!pace && !greedy) {  // closed form, prioritized entries or a clock regression: one lane
+                if (lane == 0) lane_run(c, max_rt, sc, pay, ts_base, rt_in, param_in, decision, wait_ms, r);
+                __syncthreads();
+                continue;
+            }
+            const bool warm = rule.behavior == 1;
+            const double rcount = rule.count;
+            const int64_t rqueue = rule.max_queue;
+            int64_t latest = pace ? rule.latest_passed : 0;
+            int64_t S = s0;
+            // entry passes against the current state
+            auto passes = [&](int64_t tt, int64_t cost, int aq) -> bool {
+                if (pace) return aq <= 0 || (rcount > 0 && (cost + latest <= tt || cost + latest - tt <= rqueue));
+                return warm ? (double)(j_d2l((double)S / 1.0) + aq) <= lim : default_cond(rcount, S, aq);
+            };
+            int64_t pa = 0, ba = 0, npass = 0;  // this lane's share
+            for (uint32_t g = j0; g < j1; g += 64) {
+                const uint32_t j = g + (uint32_t)lane;
+                Payload q{F_EXIT, 0, 0, 0};
+                if (j < j1) q = pay[j];
+                const bool ent = !(q.idx & F_EXIT);
+                const int64_t t = ts_base + (int64_t)q.ts_off;
+                const int aq = ent ? (int)(q.acq_prio & 0x7FFFFFFFu) : 0;
+                const int64_t cost = (pace && ent && aq > 0 && rcount > 0) ? j_round(1.0 * aq / rcount * 1000) : 0;
+                int8_t d = D_PASS;
+                int64_t w = 0;
+                uint64_t rem = __ballot(ent);
+                if (!pace) {  // before the window's first block every entry passes: one prefix sum
+                    int64_t incl = aq;
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const int64_t v = __shfl_up(incl, o);
+                        if (lane >= o) incl += v;
+                    }
+                    const int64_t before = S + incl - aq;
+                    const bool ok_pre = warm ? (double)(j_d2l((double)before / 1.0) + aq) <= lim
+                                             : default_cond(rcount, before, aq);
+                    const uint64_t bad = __ballot(ent && !ok_pre);
+                    const int b = bad ? __builtin_ctzll(bad) : 64;
+                    const int64_t upto = b == 0 ? 0 : __shfl(incl, b - 1);  // entries' acquire before lane b
+                    S += upto;
+                    rem &= b >= 64 ? 0ull : (~0ull << b);
+                }
+                while (rem) {
+                    const bool open = (rem >> lane) & 1ull;
+                    const uint64_t pm = __ballot(open && passes(t, cost, aq));
+                    const int first = pm ? __builtin_ctzll(pm) : 64;
+                    if (open && lane < first && (pace ? aq > 0 : true)) d = D_BLOCK_FLOW;
+                    if (first == 64) break;
+                    const int af = __shfl(aq, first);
+                    if (pace) {
+                        const int64_t tf = __shfl(t, first), cf = __shfl(cost, first);
+                        if (af > 0) {
+                            int64_t wf = 0;
+                            if (cf + latest <= tf) {
+                                latest = tf;
+                            } else {
+                                latest += cf;
+                                wf = latest - tf;
+                            }
+                            if (lane == first) w = wf;
+                        }
+                    } else {
+                        S += af;
+                    }
+                    rem &= (first == 63) ? 0ull : (~0ull << (first + 1));
+                }
+                if (ent && j < j1) {
+                    const uint32_t idx = q.idx & F_IDX;
+                    decision[idx] = d;
+                    wait_ms[idx] = (int32_t)w;
                     if (d == D_PASS) {
                         pa += aq;
                         ++npass;
                     } else {
                         ba += aq;
                     }
-                    return true;
-                };
-                // software pipeline: the next 4 payloads are loaded before this group's stores are
-                // issued, so a load never waits behind the previous group's scattered stores
-                constexpr uint32_t kG = 4;
-                const Payload none{F_EXIT, 0, 0, 0};
-                Payload c0 = j0 < j1 ? pay[j0] : none, c1 = j0 + 1 < j1 ? pay[j0 + 1] : none;
-                Payload c2 = j0 + 2 < j1 ? pay[j0 + 2] : none, c3 = j0 + 3 < j1 ? pay[j0 + 3] : none;
-                for (uint32_t g = j0; g < j1; g += kG) {
-                    const uint32_t nx = g + kG;
-                    const Payload n0 = nx < j1 ? pay[nx] : none, n1 = nx + 1 < j1 ? pay[nx + 1] : none;
-                    const Payload n2 = nx + 2 < j1 ? pay[nx + 2] : none, n3 = nx + 3 < j1 ? pay[nx + 3] : none;
-                    uint32_t i0, i1, i2, i3;
-                    int8_t d0, d1, d2, d3;
-                    int32_t w0, w1, w2, w3;
-                    const bool v0 = pace_one(c0, i0, d0, w0), v1 = pace_one(c1, i1, d1, w1);
-                    const bool v2 = pace_one(c2, i2, d2, w2), v3 = pace_one(c3, i3, d3, w3);
-                    if (v0) { decision[i0] = d0; wait_ms[i0] = w0; }
-                    if (v1) { decision[i1] = d1; wait_ms[i1] = w1; }
-                    if (v2) { decision[i2] = d2; wait_ms[i2] = w2; }
-                    if (v3) { decision[i3] = d3; wait_ms[i3] = w3; }
-                    c0 = n0;
-                    c1 = n1;
-                    c2 = n2;
-                    c3 = n3;
                 }
-                rule.latest_passed = latest;
+            }
+            for (int o = 32; o >= 1; o >>= 1) {
+                pa += __shfl_xor(pa, o);
+                ba += __shfl_xor(ba, o);
+                npass += __shfl_xor(npass, o);
+            }
+            if (lane == 0) {
+                if (pace) rule.latest_passed = latest;
                 int64_t *sb = sec_current(node, t0, max_rt);
                 int64_t *mb = min_current(node, t0, max_rt);
                 const int64_t exc = (int64_t)sc.run_exc[r], exerr = (int64_t)sc.run_exerr[r];
@@ -1314,94 +1581,12 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
                 }
                 node[kNodeThreads] += npass - (int64_t)sc.run_nexit[r];
                 sc.run_mode[r] = RUN_DONE;
-                continue;
             }
-            if (fast && nent) {  // WarmUp sync must only see entries in one second (true: run is inside one 500 ms bucket)
-                const int64_t s0 = sec_sum(node, t0, MB_PASS);
-                if (s0 + (int64_t)nent * a + a >= (int64_t)INT32_MAX) fast = false;
-            }
-            if (!fast) {
-                for (uint32_t j = j0; j < j1; ++j) {
-                    const Payload q = pay[j];
-                    const int64_t t = ts_base + (int64_t)q.ts_off;
-                    const uint32_t idx = q.idx & F_IDX;
-                    const bool hp = (q.idx & F_PARAM) != 0;
-                    const uint64_t pv = hp ? param_in[idx] : 0;
-                    if (q.idx & F_EXIT) {
-                        chain_exit(c, res, t, rt_in[idx], (int)(q.acq_prio & 0x7FFFFFFFu), (q.idx & F_ERROR) != 0, hp, pv);
-                    } else {
-                        int64_t w = 0;
-                        decision[idx] = chain_entry(c, res, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
-                                                    hp, pv, &w);
-                        wait_ms[idx] = (int32_t)w;
-                    }
-                }
-                sc.run_mode[r] = RUN_DONE;
-                continue;
-            }
-            // ---- closed form: rotate both windows once at the run's first event
-            int64_t *sb = sec_current(node, t0, max_rt);
-            int64_t *mb = min_current(node, t0, max_rt);
-            uint32_t f = 0;
-            if (nent) {
-                FlowRuleDev &rule = st.rules[R.rule_off];
-                const int64_t s0 = sec_sum(node, t0, MB_PASS);
-                if (rule.behavior == 1) {
-                    // WarmUpController: sync once (the run is inside one second), then a fixed threshold
-                    const int64_t previous_qps = j_d2l(node_prev_pass_qps(c, node, t0));
-                    warmup_sync(rule, t0, previous_qps);
-                    const int64_t rest = rule.stored_tokens;
-                    double lim;
-                    if (rest >= rule.warning_token) {
-                        const int64_t above = rest - rule.warning_token;
-                        lim = j_next_up(1.0 / ((double)above * rule.slope + 1.0 / rule.count));
-                    } else {
-                        lim = rule.count;
-                    }
-                    uint32_t lo = 0, hi = nent;
-                    while (lo < hi) {
-                        const uint32_t mid = lo + ((hi - lo) >> 1);
-                        const int64_t pq = j_d2l((double)(s0 + (int64_t)mid * a) / 1.0);
-                        if ((double)(pq + a) <= lim) lo = mid + 1;
-                        else hi = mid;
-                    }
-                    f = lo;
-                } else {
-                    uint32_t lo = 0, hi = nent;
-                    while (lo < hi) {
-                        const uint32_t mid = lo + ((hi - lo) >> 1);
-                        if (default_cond(rule.count, s0 + (int64_t)mid * a, a)) lo = mid + 1;
-                        else hi = mid;
-                    }
-                    f = lo;
-                }
-            }
-            const int64_t pa = (int64_t)f * a, ba = (int64_t)(nent - f) * a;
-            const int64_t exc = (int64_t)sc.run_exc[r], exerr = (int64_t)sc.run_exerr[r];
-            const int64_t exrt = sc.run_exrt[r], exmin = sc.run_exmin[r];
-            sb[MB_PASS] += pa;
-            sb[MB_BLOCK] += ba;
-            sb[MB_SUCC] += exc;
-            sb[MB_RT] += exrt;
-            sb[MB_EXC] += exerr;
-            if (exmin < sb[MB_MINRT]) sb[MB_MINRT] = exmin;
-            mb[MB_PASS] += pa;
-            mb[MB_BLOCK] += ba;
-            mb[MB_SUCC] += exc;
-            mb[MB_RT] += exrt;
-            mb[MB_EXC] += exerr;
-            if (exmin < mb[MB_MINRT]) mb[MB_MINRT] = exmin;
-            node[kNodeThreads] += (int64_t)f - (int64_t)sc.run_nexit[r];
-            sc.run_f[r] = f;
-            sc.run_mode[r] = RUN_FAST;
+            __syncthreads();
         }
     }
 }
 
-// Heavy resources (many events, no closed form): one workgroup each; its node record, rules and
-// breakers are copied to LDS, lane 0 replays every event in order against the LDS copy (an LDS
-// round trip instead of a global one per state access), and the state is written back.
-constexpr int kHeavyRules = 16, kHeavyCbs = 16, kHeavyChunk = 512, kHeavySlots = 1024;
 __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, FlowScratch sc,
                                                const Payload *__restrict__ pay, int64_t ts_base,
                                                const int64_t *__restrict__ rt_in,
@@ -2555,7 +2740,7 @@ int FlowEngine::ensure_scratch() {
         for (int b = 1; b <= 32; ++b) hist = std::max(hist, radix_hist_entries(cap, b));
         const size_t ntiles = (cap + kTileElems - 1) / kTileElems + 1;
         size_t bytes = 2 * al(cap * 4) + 2 * al(cap * sizeof(Payload)) + 2 * al(cap * 4) + 10 * al(cap * 4) +
-                       4 * al(cap * 8) + al(cap) + 2 * al(cap * 4) + 2 * al(ntiles * sizeof(LAgg)) + al(ntiles * 4) +
+                       4 * al(cap * 8) + al(cap) + 3 * al(cap * 4) + 2 * al(ntiles * sizeof(LAgg)) + al(ntiles * 4) +
                        al(64) + 2 * al(hist * 4) + al(scan_partials_needed(hist) * 4 + 64);
         d_scratch.alloc(bytes);
         char *p = (char *)d_scratch.p;
@@ -2587,6 +2772,7 @@ int FlowEngine::ensure_scratch() {
         sc.run_mode = (uint8_t *)take(cap);
         sc.flow_first_run = (uint32_t *)take(cap * 4);
         sc.heavy = (uint32_t *)take(cap * 4);
+        sc.pace = (uint32_t *)take(cap * 4);
         sc.tile_agg = take(ntiles * sizeof(LAgg));
         sc.tile_carry = take(ntiles * sizeof(LAgg));
         sc.tile_valid = (uint32_t *)take(ntiles * 4);
@@ -2705,6 +2891,9 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         const uint32_t fthreads = (uint32_t)std::min<size_t>(m, nres);
         hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, stream, st,
                            (int64_t)cfg.statistic_max_rt, sc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p);
+        hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
+                           dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
+                           d_dec.p, d_wait.p);
         hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
                            d_dec.p, d_wait.p, heavy_prof());
@@ -2780,6 +2969,8 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
     const uint32_t fthreads = std::min<uint32_t>(m, nres);
     hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc,
                        pay, keys, ts_base, rt_p, param_p, d_decision, wait_p);
+    hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
+                       st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p);
     hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
                        st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
                        heavy_prof());

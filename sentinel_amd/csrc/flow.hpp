@@ -119,6 +119,7 @@ struct FlowScratch {
     uint8_t *run_mode;
     uint32_t *flow_first_run;
     uint32_t *heavy;  // flows replayed by k_lheavy (count in counters[8])
+    uint32_t *pace;   // long single-rule fast-path flows decided by k_lwave (count in counters[9])
     void *tile_agg, *tile_carry;
     uint32_t *tile_valid;
     uint32_t *counters;

@@ -235,6 +235,38 @@ def test_breaker_heavy_open_close_cycles(seed):
              max_batch=mb)
 
 
+@pytest.mark.parametrize("seed,regress", [(31, 0.0), (32, 0.002)])
+def test_pacing_heavy_resources(seed, regress):
+    """RateLimiterController-only resources with thousands of entries per batch go to k_lwave (one wave
+    per resource, a ballot finds each window's next passing entry); acquire 1..3 (cost differs per
+    entry), queues of 0 / 20 / 500 ms, a zero-count rule (every entry blocks), exits interleaved, and
+    clock regressions (those runs take the per-event chain)."""
+    n_res = 6
+    flow = [{"resource": 0, "count": 50.0, "control_behavior": 2, "max_queueing_time_ms": 500},
+            {"resource": 1, "count": 7.5, "control_behavior": 2, "max_queueing_time_ms": 20},
+            {"resource": 2, "count": 200.0, "control_behavior": 2, "max_queueing_time_ms": 0},
+            {"resource": 3, "count": 0.0, "control_behavior": 2, "max_queueing_time_ms": 100},
+            {"resource": 4, "count": 1000.0, "control_behavior": 2, "max_queueing_time_ms": 500}]
+    _run(n_res, flow=flow, max_batch=1 << 15, n_entries=40000, seed=seed, gap_mean=0.05, acq_max=3, rt_max=20,
+         err_pct=0.05, regress_pct=regress)
+
+
+@pytest.mark.parametrize("seed,regress", [(33, 0.0), (34, 0.002)])
+def test_mixed_acquire_heavy_resources(seed, regress):
+    """DefaultController / WarmUpController resources with thousands of entries per batch and mixed
+    acquire counts (no closed form): k_lwave decides each window by one prefix sum up to its first
+    block, then a ballot per further pass; prioritized entries and clock regressions keep the
+    per-event chain."""
+    n_res = 6
+    flow = [{"resource": 0, "count": 120.0},
+            {"resource": 1, "count": 9.0},
+            {"resource": 2, "count": 300.0, "control_behavior": 1, "warm_up_period_sec": 2},
+            {"resource": 3, "count": 40.0, "control_behavior": 1, "warm_up_period_sec": 5},
+            {"resource": 4, "count": 2000.0}]
+    _run(n_res, flow=flow, max_batch=1 << 15, n_entries=40000, seed=seed, gap_mean=0.05, acq_max=4, rt_max=20,
+         err_pct=0.05, regress_pct=regress, prio_pct=0.002 if regress else 0.0)
+
+
 def test_rule_reload_between_batches():
     n_res = 10
     rng = np.random.default_rng(5)
