@@ -7,7 +7,10 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsentinel_amd.so")
+# SGA_LIB_VARIANT=X loads libsentinel_amd_X.so (kernel A/B builds made by tools; the default build
+# is the product library)
+LIB_PATH = os.path.join(_HERE, "libsentinel_amd" + (("_" + os.environ["SGA_LIB_VARIANT"])
+                                                     if os.environ.get("SGA_LIB_VARIANT") else "") + ".so")
 
 
 class SgaConfig(C.Structure):

@@ -130,6 +130,7 @@ enum : int {
     CTL_BDHI = 24,       // largest hot bucket delta
     CTL_MODE = 25,       // 1: the batch runs the hot path
     CTL_HOTERR = 26,     // hot runs that needed a replay (never expected)
+    CTL_NCRULE = 27,     // cold rules published to BatchScratch::crule (split cold pipeline)
     CTL_WORDS = 64
 };
 enum : uint32_t {
@@ -158,6 +159,9 @@ struct BatchScratch {
     uint32_t *plist;          // sorted positions of prioritized requests (ascending)
     uint32_t *deferred;       // (flow, run) pairs handed from k_flows to k_flows_slow
     RunOut *run_out;
+    uint4 *run_rec;           // split cold pipeline, per run head position: requests, prioritized count,
+                              // first plist index, acquire | bucket delta << 8
+    uint4 *crule;             // split cold pipeline: (slot, first position, end position) per touched rule
     RAgg *wave_carry;         // per 512-request wave slice: scan carry for k_results
     void *tile_agg;
     void *tile_carry;
@@ -197,6 +201,10 @@ struct BatchScratch {
     uint32_t small_max = 4096; // batches of at most this many requests take the one-workgroup path (sga_set_small_batch)
     int hot_lane_order = 0;   // lds_lane_order_ok() held on this device (set when the scratch is made)
     uint32_t hot_min = 64;    // smallest per-batch request count that makes a rule hot
+    // hot/cold overlap: after the sort the hot side (ranks, hot runs, hot results) runs on `side`
+    // beside the cold stage on the batch's stream (fork and join by events; made on first use)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 // The hot path's in-order ranks come from LDS atomics whose same-word lanes are served in lane
@@ -205,6 +213,8 @@ bool lds_lane_order_ok(hipStream_t stream);
 
 // Forget the hot set (rule slots changed or scratch re-carved).
 void hot_reset(const ClusterState &st, BatchScratch &b, uint32_t nslots_cap, hipStream_t stream);
+// Releases the side stream and events of a scratch (engine teardown).
+void batch_scratch_release(BatchScratch &b);
 
 // Requests per batch are indexed with 26 bits inside the packed sort element; rule slots with 24.
 constexpr size_t kMaxBatch = (size_t)1 << 26;

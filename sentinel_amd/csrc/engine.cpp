@@ -676,6 +676,7 @@ int sga_destroy(sga_engine *e) {
         if (e->impl.stream) {
             (void)hipStreamSynchronize(e->impl.stream);
             e->impl.release_events();
+            batch_scratch_release(e->impl.scratch);
             e->impl.flow.release();
             e->impl.h_stage.release();
             e->impl.h_res.release();
