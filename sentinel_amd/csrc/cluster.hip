@@ -2143,6 +2143,12 @@ __device__ __forceinline__ uint32_t wave_lower_bound(const uint32_t *__restrict_
 // One wave per hot rule: its runs in bucket order, each with the closed form of run_fast (the S
 // window buckets are read by S lanes, the sums are wave reductions, the decisions are uniform
 // scalar arithmetic, lane 0 stores the bucket).
+// Hot run records, bucket-major: a bucket's runs of consecutive hot ids are adjacent, so
+// k_hot_final's cache fill (the hottest ids' runs of two buckets) reads contiguous records.
+__device__ __forceinline__ HotRun *hrun_at(const BatchScratch &sc, uint32_t h, uint32_t b) {
+    return sc.hrun + (size_t)b * kHot + h;
+}
+
 __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchScratch sc, int64_t ts_base) {
     if (!sc.counters[CTL_MODE]) return;
     const int lane = threadIdx.x & 63;
@@ -2161,11 +2167,10 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
     uint32_t stn = wave_shl1(stb, 0u);
     if ((uint32_t)lane + 1 == nb) stn = tot;
     const uint32_t nrun = (uint32_t)lane < nb ? stn - stb : 0u;
-    HotRun *hr_row = sc.hrun + (size_t)h * kHotBuckets;
     if ((uint32_t)lane < nb && nrun == 0) {
         HotRun z{};
         z.start = stb;
-        hr_row[bd_lo + lane] = z;
+        *hrun_at(sc, h, bd_lo + lane) = z;
     }
     uint64_t rm = __ballot(nrun > 0);
     if (!rm) return;
@@ -2282,7 +2287,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
             r.cw = cw;
             r.wait = (uint16_t)(1000 / P.S);
             r.ok = ok ? 1 : 0;
-            hr_row[b] = r;
+            *hrun_at(sc, h, b) = r;
         }
     }
 }
@@ -2334,7 +2339,7 @@ __global__ __launch_bounds__(kFinWgThreads) void k_hot_final(BatchScratch sc, ui
 #pragma unroll
         for (uint32_t k = 0; k < 2; ++k) {
             const uint32_t b = min(b0 + k, (uint32_t)kHotBuckets - 1);
-            const uint4 *hp = reinterpret_cast<const uint4 *>(sc.hrun + (size_t)h * kHotBuckets + b);
+            const uint4 *hp = reinterpret_cast<const uint4 *>(hrun_at(sc, h, b));
             const uint2 s0 = *reinterpret_cast<const uint2 *>(hp);
             const uint4 r1 = hp[1];
             c_s0[k][h] = i64_of(s0.x, s0.y);
@@ -2353,8 +2358,7 @@ __global__ __launch_bounds__(kFinWgThreads) void k_hot_final(BatchScratch sc, ui
         code[u] = (i < wend && !(cn[u] >> 31)) ? cn[u] : kNoCode;  // prioritized: k_prio_results
         const uint32_t cd = code[u];
         hit[u] = cd == kNoCode || ((cd & 0xFFFu) < cache_cap && (cd >> 25) - b0 < 2u);
-        const size_t at = hit[u] ? 0 : (size_t)(cd & 0xFFFu) * kHotBuckets + (cd >> 25);
-        const uint4 *hp = reinterpret_cast<const uint4 *>(sc.hrun + at);
+        const uint4 *hp = reinterpret_cast<const uint4 *>(hit[u] ? sc.hrun : hrun_at(sc, cd & 0xFFFu, cd >> 25));
         ra[u] = hp[0];  // s0, thr
         rb[u] = hp[1];  // isec, f, start
     }
@@ -2405,11 +2409,10 @@ __global__ __launch_bounds__(kThreads) void k_prio_results(ClusterState st, Batc
         const uint64_t e = el[base + j];
         const uint32_t h = el_slot(e) - (st.nslots + 1);
         const uint32_t rank = sc.prank[j];
-        const HotRun *row = sc.hrun + (size_t)h * kHotBuckets;
         uint32_t b = bd_lo;
         for (; b < bd_hi; ++b)
-            if (rank - row[b].start < row[b].n) break;
-        const HotRun hr = row[b];
+            if (rank - hrun_at(sc, h, b)->start < hrun_at(sc, h, b)->n) break;
+        const HotRun hr = *hrun_at(sc, h, b);
         const uint32_t local = rank - hr.start;
         uint64_t res;
         if (local < hr.f) {
