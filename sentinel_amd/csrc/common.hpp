@@ -135,4 +135,56 @@ struct DevBuf {
     }
     size_t bytes() const { return n * sizeof(T); }
 };
+// ---- wave64 scans on DPP (VALU lane moves: no LDS round trip per step, unlike __shfl_up).
+// Hillis-Steele inside each 16-lane row (row_shr 1, 2, 4, 8), then row 0's / row 2's totals into
+// rows 1 / 3 (row_bcast:15) and the first half's total into rows 2 and 3 (row_bcast:31).  Lanes whose
+// source is outside the row, or whose row is masked off, read `old` = the identity.
+namespace dpp {
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ int64_t mov64(int64_t old, int64_t v) {
+    const int lo = __builtin_amdgcn_update_dpp((int)(uint32_t)old, (int)(uint32_t)v, kCtrl, kRowMask, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)((uint64_t)old >> 32), (int)(uint32_t)((uint64_t)v >> 32),
+                                               kCtrl, kRowMask, 0xf, false);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+}  // namespace dpp
+
+// inclusive prefix sum of an int64 over the wave (lane order)
+__device__ __forceinline__ int64_t wave_incl_sum_i64(int64_t v) {
+    v += dpp::mov64<0x111, 0xf>(0, v);
+    v += dpp::mov64<0x112, 0xf>(0, v);
+    v += dpp::mov64<0x114, 0xf>(0, v);
+    v += dpp::mov64<0x118, 0xf>(0, v);
+    v += dpp::mov64<0x142, 0xa>(0, v);
+    v += dpp::mov64<0x143, 0xc>(0, v);
+    return v;
+}
+
+// inclusive max-plus scan: lane k ends with the composition of f_0 .. f_k, f_i(x) = max(x + A_i, B_i);
+// (A1, B1) then (A2, B2) = (A1 + A2, max(B1 + A2, B2)); identity (0, kNegInf)
+constexpr int64_t kMaxPlusNegInf = INT64_MIN / 4;
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void maxplus_step(int64_t &A, int64_t &B) {
+    const int64_t a = dpp::mov64<kCtrl, kRowMask>(0, A), b = dpp::mov64<kCtrl, kRowMask>(kMaxPlusNegInf, B);
+    B = max(b + A, B);
+    A += a;
+}
+__device__ __forceinline__ void wave_incl_maxplus(int64_t &A, int64_t &B) {
+    maxplus_step<0x111, 0xf>(A, B);
+    maxplus_step<0x112, 0xf>(A, B);
+    maxplus_step<0x114, 0xf>(A, B);
+    maxplus_step<0x118, 0xf>(A, B);
+    maxplus_step<0x142, 0xa>(A, B);
+    maxplus_step<0x143, 0xc>(A, B);
+}
+
+// lane i <- lane i - 1 (lane 0 <- fill), whole wave (wave_shr:1)
+__device__ __forceinline__ int64_t wave_shr1_i64(int64_t v, int64_t fill) { return dpp::mov64<0x138, 0xf>(fill, v); }
+
+// one lane's value, wave-uniform (v_readlane)
+__device__ __forceinline__ int64_t readlane_i64(int64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 }  // namespace sga

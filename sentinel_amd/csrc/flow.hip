@@ -1196,6 +1196,31 @@ __device__ void lane_run(const Ctx &c, int64_t max_rt, FlowScratch &sc, const Pa
     const uint32_t nent = sc.run_nent[r];
     const int32_t a = sc.run_amin[r];
     const int64_t t0 = ts_base + (int64_t)sc.run_t0off[r];
+    if (nent == 0 && (R.fast & 5u)) {
+        // An exit-only run of a single-rule resource (no parameter rules, no breakers: an exit only
+        // adds to the node).  Its exits share one second bucket and one minute bucket, so each
+        // window either takes all of the run's adds (the bucket is current, or older and rotated at
+        // the first exit) or none (the window already holds a newer bucket: LeapArray.currentWindow
+        // returns a detached bucket, LeapArray.java:216-220) -- also when exits are submitted after
+        // later entries.  curThreadNum drops in every case (StatisticNode.decreaseThreadNum).
+        const int64_t *sb0 = node + kNodeSec + kMB * (int)((t0 / kSecW) % 2);
+        const int64_t *mb0 = node + kNodeMin + kMB * (int)((t0 / kMinW) % 60);
+        const bool sdet = sb0[0] != kAbsent && t0 - t0 % kSecW < sb0[0];
+        const bool mdet = mb0[0] != kAbsent && t0 - t0 % kMinW < mb0[0];
+        const int64_t exc = (int64_t)sc.run_exc[r], exerr = (int64_t)sc.run_exerr[r];
+        const int64_t exrt = sc.run_exrt[r], exmin = sc.run_exmin[r];
+        for (int k = 0; k < 2; ++k) {
+            if (k == 0 ? sdet : mdet) continue;
+            int64_t *b = k == 0 ? sec_current(node, t0, max_rt) : min_current(node, t0, max_rt);
+            b[MB_SUCC] += exc;
+            b[MB_RT] += exrt;
+            b[MB_EXC] += exerr;
+            if (exmin < b[MB_MINRT]) b[MB_MINRT] = exmin;
+        }
+        node[kNodeThreads] -= (int64_t)sc.run_nexit[r];
+        sc.run_mode[r] = RUN_DONE;
+        return;
+    }
     bool fast = (R.fast & 1u) && sc.run_cp[r] == 0 && (nent == 0 || a == sc.run_amax[r]) && a >= 0;
     bool pace = (R.fast & 4u) != 0;
     if (fast || pace) {  // no clock regression in this resource's windows
@@ -1265,12 +1290,17 @@ __device__ void lane_run(const Ctx &c, int64_t max_rt, FlowScratch &sc, const Pa
         // issued, so a load never waits behind the previous group's scattered stores
         constexpr uint32_t kG = 4;
         const Payload none{F_EXIT, 0, 0, 0};
-        Payload c0 = j0 < j1 ? pay[j0] : none, c1 = j0 + 1 < j1 ? pay[j0 + 1] : none;
-        Payload c2 = j0 + 2 < j1 ? pay[j0 + 2] : none, c3 = j0 + 3 < j1 ? pay[j0 + 3] : none;
+        // loads at clamped indices, the out-of-run ones replaced after the load (a load under a
+        // branch is waited for before the branch closes)
+        auto ld = [&](uint32_t j) {
+            Payload q = pay[min(j, j1 - 1)];
+            if (j >= j1) q = none;
+            return q;
+        };
+        Payload c0 = ld(j0), c1 = ld(j0 + 1), c2 = ld(j0 + 2), c3 = ld(j0 + 3);
         for (uint32_t g = j0; g < j1; g += kG) {
             const uint32_t nx = g + kG;
-            const Payload n0 = nx < j1 ? pay[nx] : none, n1 = nx + 1 < j1 ? pay[nx + 1] : none;
-            const Payload n2 = nx + 2 < j1 ? pay[nx + 2] : none, n3 = nx + 3 < j1 ? pay[nx + 3] : none;
+            const Payload n0 = ld(nx), n1 = ld(nx + 1), n2 = ld(nx + 2), n3 = ld(nx + 3);
             uint32_t i0, i1, i2, i3;
             int8_t d0, d1, d2, d3;
             int32_t w0, w1, w2, w3;
@@ -1428,18 +1458,21 @@ constexpr int kHeavyRules = 16, kHeavyCbs = 16, kHeavyChunk = 512, kHeavySlots =
 // A window costs one iteration per pass after its first block, instead of one dependent step per entry.
 // Runs with a uniform acquire keep the closed form, and runs that go back in time or hold prioritized
 // entries take lane_run on lane 0, exactly as in k_lflows.
+constexpr int kWavePf = 8;  // k_lwave: windows loaded ahead
 __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, FlowScratch sc,
                                               const Payload *__restrict__ pay, int64_t ts_base,
                                               const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in,
-                                              int8_t *decision, int32_t *wait_ms) {
+                                              int8_t *decision, int32_t *wait_ms, uint64_t *prof) {
     if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
     const Ctx c{st, max_rt};
     const int lane = threadIdx.x;
     const uint32_t nwave = sc.counters[9], nflows = sc.counters[2], nruns = sc.counters[1];
+    uint64_t pr_iter = 0, pr_lr = 0, pr_lrt = 0;  // profiling (SGA_LWAVE_PROF=1)
     for (uint32_t h = blockIdx.x; h < nwave; h += gridDim.x) {
         const uint32_t fl = sc.pace[h];
         const uint32_t r0 = sc.flow_first_run[fl];
         const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        const uint64_t pt0 = prof ? wall_clock64() : 0;
         for (uint32_t r = r0; r < r1; ++r) {
             const uint32_t res = sc.run_slot[r];
             const ResDev R = st.res[res];
@@ -1481,8 +1514,13 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                 if (rule.behavior == 1 && lim == -1) greedy = false;
             }
             if (!pace && !greedy) {  // closed form, prioritized entries or a clock regression: one lane
+                const uint64_t lt0 = prof ? wall_clock64() : 0;
                 if (lane == 0) lane_run(c, max_rt, sc, pay, ts_base, rt_in, param_in, decision, wait_ms, r);
                 __syncthreads();
+                if (prof) {
+                    pr_lrt += wall_clock64() - lt0;
+                    ++pr_lr;
+                }
                 continue;
             }
             const bool warm = rule.behavior == 1;
@@ -1496,10 +1534,15 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                 return warm ? (double)(j_d2l((double)S / 1.0) + aq) <= lim : default_cond(rcount, S, aq);
             };
             int64_t pa = 0, ba = 0, npass = 0;  // this lane's share
-            for (uint32_t g = j0; g < j1; g += 64) {
+            // windows of 64 entries, kWavePf of them loaded ahead in a register ring (unconditional
+            // loads at a clamped index, so no load waits at a branch): the state chain between
+            // windows is a few ballots, the payload load latency is paid once per ring
+            Payload ring[kWavePf];
+#pragma unroll
+            for (int k = 0; k < kWavePf; ++k) ring[k] = pay[min(j0 + (uint32_t)(k * 64 + lane), j1 - 1)];
+            auto window = [&](uint32_t g, Payload q) {
                 const uint32_t j = g + (uint32_t)lane;
-                Payload q{F_EXIT, 0, 0, 0};
-                if (j < j1) q = pay[j];
+                if (j >= j1) q.idx = F_EXIT;
                 const bool ent = !(q.idx & F_EXIT);
                 const int64_t t = ts_base + (int64_t)q.ts_off;
                 const int aq = ent ? (int)(q.acq_prio & 0x7FFFFFFFu) : 0;
@@ -1508,29 +1551,26 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                 int64_t w = 0;
                 uint64_t rem = __ballot(ent);
                 if (!pace) {  // before the window's first block every entry passes: one prefix sum
-                    int64_t incl = aq;
-                    for (int o = 1; o < 64; o <<= 1) {
-                        const int64_t v = __shfl_up(incl, o);
-                        if (lane >= o) incl += v;
-                    }
+                    const int64_t incl = wave_incl_sum_i64(aq);
                     const int64_t before = S + incl - aq;
                     const bool ok_pre = warm ? (double)(j_d2l((double)before / 1.0) + aq) <= lim
                                              : default_cond(rcount, before, aq);
                     const uint64_t bad = __ballot(ent && !ok_pre);
                     const int b = bad ? __builtin_ctzll(bad) : 64;
-                    const int64_t upto = b == 0 ? 0 : __shfl(incl, b - 1);  // entries' acquire before lane b
+                    const int64_t upto = b == 0 ? 0 : readlane_i64(incl, b - 1);  // entries' acquire before lane b
                     S += upto;
                     rem &= b >= 64 ? 0ull : (~0ull << b);
                 }
                 while (rem) {
-                    const bool open = (rem >> lane) & 1ull;
+                    if (prof) ++pr_iter;
+                    bool open = (rem >> lane) & 1ull;
                     const uint64_t pm = __ballot(open && passes(t, cost, aq));
                     const int first = pm ? __builtin_ctzll(pm) : 64;
                     if (open && lane < first && (pace ? aq > 0 : true)) d = D_BLOCK_FLOW;
                     if (first == 64) break;
-                    const int af = __shfl(aq, first);
+                    const int af = __builtin_amdgcn_readlane(aq, first);
                     if (pace) {
-                        const int64_t tf = __shfl(t, first), cf = __shfl(cost, first);
+                        const int64_t tf = readlane_i64(t, first), cf = readlane_i64(cost, first);
                         if (af > 0) {
                             int64_t wf = 0;
                             if (cf + latest <= tf) {
@@ -1545,6 +1585,24 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                         S += af;
                     }
                     rem &= (first == 63) ? 0ull : (~0ull << (first + 1));
+                    if (pace && rcount > 0 && rem) {
+                        open = (rem >> lane) & 1ull;
+                        // after a pass, the open entries up to the next block pass in one step: while entries pass,
+                        // latestPassedTime follows L = max(L + cost, now) (the pass branches of
+                        // RateLimiterController.java:63-86), a max-plus scan over the lanes; entries with
+                        // acquireCount <= 0 pass and leave it alone (:48-50)
+                        const bool mv = open && aq > 0;
+                        int64_t A = mv ? cost : 0, B = mv ? t : kMaxPlusNegInf;
+                        wave_incl_maxplus(A, B);
+                        const int64_t Lk = max(latest + A, B);
+                        const int64_t Lprev = wave_shr1_i64(Lk, latest);
+                        const bool ok = !mv || cost + Lprev <= t || cost + Lprev - t <= rqueue;
+                        const uint64_t bad = __ballot(open && !ok);
+                        const int bl = bad ? __builtin_ctzll(bad) : 64;
+                        if (open && lane < bl && mv) w = Lk - t;
+                        if (bl > 0) latest = readlane_i64(Lk, bl - 1);
+                        rem &= bl >= 64 ? 0ull : (~0ull << bl);
+                    }
                 }
                 if (ent && j < j1) {
                     const uint32_t idx = q.idx & F_IDX;
@@ -1556,6 +1614,15 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                     } else {
                         ba += aq;
                     }
+                }
+            };
+            for (uint32_t g0 = j0; g0 < j1; g0 += 64 * kWavePf) {
+#pragma unroll
+                for (int k = 0; k < kWavePf; ++k) {
+                    const uint32_t g = g0 + (uint32_t)k * 64;
+                    const Payload q = ring[k];
+                    ring[k] = pay[min(g + (uint32_t)(kWavePf * 64 + lane), j1 - 1)];
+                    if (g < j1) window(g, q);  // wave-uniform
                 }
             }
             for (int o = 32; o >= 1; o >>= 1) {
@@ -1584,6 +1651,25 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
             }
             __syncthreads();
         }
+        if (prof && lane == 0) {
+            const uint64_t dt = wall_clock64() - pt0;
+            const uint32_t nev = sc.run_end[r1 - 1] - sc.run_start[r0];
+            uint64_t *p = prof + (size_t)(blockIdx.x % 1024) * 8;
+            p[0] += 1;
+            p[1] += nev;
+            p[2] += dt;
+            if (dt > p[6]) {
+                p[6] = dt;
+                p[7] = ((uint64_t)nev << 32) | (uint64_t)(st.res[sc.run_slot[r0]].fast & 0xFFu) |
+                       ((uint64_t)(r1 - r0) << 8);
+            }
+        }
+    }
+    if (prof && lane == 0) {
+        uint64_t *p = prof + (size_t)(blockIdx.x % 1024) * 8;
+        p[3] += pr_lrt;
+        p[4] += pr_lr;
+        p[5] += pr_iter;
     }
 }
 
@@ -2717,6 +2803,32 @@ static uint64_t *heavy_prof() {
     return on ? g_heavy_prof : nullptr;
 }
 
+// SGA_LWAVE_PROF=1: k_lwave per-workgroup counters, printed after every launch (diagnostics only)
+static uint64_t *g_lwave_prof = nullptr;
+static uint64_t *lwave_prof() {
+    static const bool on = getenv("SGA_LWAVE_PROF") && atoi(getenv("SGA_LWAVE_PROF")) == 1;
+    if (on && !g_lwave_prof) SGA_HIP_CHECK(hipMalloc((void **)&g_lwave_prof, 1024 * 8 * sizeof(uint64_t)));
+    if (on) SGA_HIP_CHECK(hipMemset(g_lwave_prof, 0, 1024 * 8 * sizeof(uint64_t)));
+    return on ? g_lwave_prof : nullptr;
+}
+static void print_lwave_prof(hipStream_t s) {
+    if (!g_lwave_prof) return;
+    std::vector<uint64_t> h(1024 * 8);
+    SGA_HIP_CHECK(hipStreamSynchronize(s));
+    SGA_HIP_CHECK(hipMemcpy(h.data(), g_lwave_prof, h.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<int> o(1024);
+    for (int b = 0; b < 1024; ++b) o[b] = b;
+    std::sort(o.begin(), o.end(), [&](int a, int b) { return h[a * 8 + 2] > h[b * 8 + 2]; });
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t *p = &h[o[k] * 8];
+        fprintf(stderr, "k_lwave wg %d: resources %llu events %llu ms %.2f lane_run %llu (%.2f ms) iters %llu; "
+                "longest resource %.2f ms, %llu events, %llu runs, fast %llu\n", o[k], (unsigned long long)p[0],
+                (unsigned long long)p[1], p[2] / 1e5, (unsigned long long)p[4], p[3] / 1e5,
+                (unsigned long long)p[5], p[6] / 1e5, (unsigned long long)(p[7] >> 32),
+                (unsigned long long)((p[7] >> 8) & 0xFFFFFFu), (unsigned long long)(p[7] & 0xFFu));
+    }
+}
+
 void print_heavy_prof() {
     if (!g_heavy_prof) return;
     std::vector<uint64_t> h(1024 * 8);
@@ -2893,7 +3005,8 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
                            (int64_t)cfg.statistic_max_rt, sc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p);
         hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
-                           d_dec.p, d_wait.p);
+                           d_dec.p, d_wait.p, lwave_prof());
+        print_lwave_prof(stream);
         hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
                            d_dec.p, d_wait.p, heavy_prof());
@@ -2970,7 +3083,9 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
     hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc,
                        pay, keys, ts_base, rt_p, param_p, d_decision, wait_p);
     hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
-                       st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p);
+                       st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
+                       lwave_prof());
+    print_lwave_prof(s);
     hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
                        st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
                        heavy_prof());
