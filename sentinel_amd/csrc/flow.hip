@@ -38,7 +38,9 @@ enum : int8_t { D_PASS = 0, D_BLOCK_FLOW = 1, D_BLOCK_PARAM = 2, D_BLOCK_DEGRADE
                 D_BLOCK_SYSTEM = 5 };
 enum : uint32_t { F_EXIT = 1u << 30, F_ERROR = 1u << 29, F_PARAM = 1u << 28, F_IDX = (1u << 28) - 1 };
 constexpr uint32_t kHeavyEvents = 1024;  // per batch: replayed by k_lheavy instead of one k_lflows lane
-enum : uint8_t { RUN_FAST = 0, RUN_DONE = 1 };
+// RUN_POS: k_lwave left each entry's decision and wait in ev_eidx (wait << 1 | blocked; ~0: written
+// already), k_lresults scatters them in parallel
+enum : uint8_t { RUN_FAST = 0, RUN_DONE = 1, RUN_POS = 2 };
 
 struct Ctx {
     FlowState st;
@@ -1540,6 +1542,7 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
             Payload ring[kWavePf];
 #pragma unroll
             for (int k = 0; k < kWavePf; ++k) ring[k] = pay[min(j0 + (uint32_t)(k * 64 + lane), j1 - 1)];
+            bool pred_c = true;  // pacing: the last decision of an entry with a nonzero cost
             auto window = [&](uint32_t g, Payload q) {
                 const uint32_t j = g + (uint32_t)lane;
                 if (j >= j1) q.idx = F_EXIT;
@@ -1550,7 +1553,57 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                 int8_t d = D_PASS;
                 int64_t w = 0;
                 uint64_t rem = __ballot(ent);
-                if (!pace) {  // before the window's first block every entry passes: one prefix sum
+                if (pace) {
+                    // RateLimiterController (RateLimiterController.java:46-91) by speculation: every open
+                    // entry gets a predicted decision (acquireCount <= 0: pass; count <= 0: block;
+                    // cost 0: pass; otherwise the last decision of a costly entry), latestPassedTime
+                    // follows the predicted passes as a max-plus scan (a pass sets it to
+                    // max(latest + cost, now)), and every prediction is checked against the state
+                    // before it.  Lanes up to the first wrong prediction are decided; that lane takes
+                    // its true decision, and the rest of the window goes round again.
+                    while (rem) {
+                        if (prof) ++pr_iter;
+                        const bool open = (rem >> lane) & 1ull;
+                        const bool mv = open && aq > 0 && rcount > 0;
+                        const bool spec = aq <= 0 || (rcount > 0 && (cost == 0 || pred_c));
+                        int64_t A = (mv && spec) ? cost : 0, B = (mv && spec) ? t : kMaxPlusNegInf;
+                        wave_incl_maxplus(A, B);
+                        const int64_t Lk = max(latest + A, B);
+                        const int64_t Lprev = wave_shr1_i64(Lk, latest);
+                        const bool actual = aq <= 0 || (rcount > 0 && (cost + Lprev <= t || cost + Lprev - t <= rqueue));
+                        const uint64_t mis = __ballot(open && actual != spec);
+                        const int m = mis ? __builtin_ctzll(mis) : 64;
+                        if (open && lane < m) {
+                            d = spec ? D_PASS : D_BLOCK_FLOW;
+                            if (spec && mv) w = Lk - t;
+                        }
+                        if (m == 64) {
+                            latest = readlane_i64(Lk, 63);
+                            break;
+                        }
+                        if (m > 0) latest = readlane_i64(Lk, m - 1);
+                        // lane m: its true decision (the state before it is now exact)
+                        const int am = __builtin_amdgcn_readlane(aq, m);
+                        const int64_t tm = readlane_i64(t, m), cm = readlane_i64(cost, m);
+                        const bool pm = (__ballot(actual) >> m) & 1ull;
+                        if (lane == m) d = pm ? D_PASS : D_BLOCK_FLOW;
+                        if (pm && am > 0) {
+                            const int64_t lm = max(latest + cm, tm);
+                            if (lane == m) w = lm - tm;
+                            latest = lm;
+                        }
+                        if (am > 0 && cm > 0) pred_c = pm;
+                        rem &= (m == 63) ? 0ull : (~0ull << (m + 1));
+                    }
+                    rem = 0;
+                }
+                if (!pace && !passes(0, 0, amin)) {
+                    // saturated: not even the run's smallest acquireCount fits, and blocked entries
+                    // leave the pass count alone, so the rest of the run blocks without a scan
+                    if (ent) d = D_BLOCK_FLOW;
+                    rem = 0;
+                }
+                if (!pace && rem) {  // before the window's first block every entry passes: one prefix sum
                     const int64_t incl = wave_incl_sum_i64(aq);
                     const int64_t before = S + incl - aq;
                     const bool ok_pre = warm ? (double)(j_d2l((double)before / 1.0) + aq) <= lim
@@ -1585,29 +1638,17 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                         S += af;
                     }
                     rem &= (first == 63) ? 0ull : (~0ull << (first + 1));
-                    if (pace && rcount > 0 && rem) {
-                        open = (rem >> lane) & 1ull;
-                        // after a pass, the open entries up to the next block pass in one step: while entries pass,
-                        // latestPassedTime follows L = max(L + cost, now) (the pass branches of
-                        // RateLimiterController.java:63-86), a max-plus scan over the lanes; entries with
-                        // acquireCount <= 0 pass and leave it alone (:48-50)
-                        const bool mv = open && aq > 0;
-                        int64_t A = mv ? cost : 0, B = mv ? t : kMaxPlusNegInf;
-                        wave_incl_maxplus(A, B);
-                        const int64_t Lk = max(latest + A, B);
-                        const int64_t Lprev = wave_shr1_i64(Lk, latest);
-                        const bool ok = !mv || cost + Lprev <= t || cost + Lprev - t <= rqueue;
-                        const uint64_t bad = __ballot(open && !ok);
-                        const int bl = bad ? __builtin_ctzll(bad) : 64;
-                        if (open && lane < bl && mv) w = Lk - t;
-                        if (bl > 0) latest = readlane_i64(Lk, bl - 1);
-                        rem &= bl >= 64 ? 0ull : (~0ull << bl);
-                    }
                 }
                 if (ent && j < j1) {
-                    const uint32_t idx = q.idx & F_IDX;
-                    decision[idx] = d;
-                    wait_ms[idx] = (int32_t)w;
+                    // sorted-order (coalesced) store; k_lresults scatters it by request index
+                    if (w < ((int64_t)1 << 30)) {
+                        sc.ev_eidx[j] = ((uint32_t)w << 1) | (d != D_PASS ? 1u : 0u);
+                    } else {
+                        const uint32_t idx = q.idx & F_IDX;
+                        decision[idx] = d;
+                        wait_ms[idx] = (int32_t)w;
+                        sc.ev_eidx[j] = ~0u;
+                    }
                     if (d == D_PASS) {
                         pa += aq;
                         ++npass;
@@ -1647,7 +1688,7 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                     if (exmin < b[MB_MINRT]) b[MB_MINRT] = exmin;
                 }
                 node[kNodeThreads] += npass - (int64_t)sc.run_nexit[r];
-                sc.run_mode[r] = RUN_DONE;
+                sc.run_mode[r] = RUN_POS;
             }
             __syncthreads();
         }
@@ -2270,16 +2311,25 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
     }
 }
 
-__global__ __launch_bounds__(kT) void k_lresults(FlowScratch sc, const Payload *__restrict__ pay, int8_t *decision) {
+__global__ __launch_bounds__(kT) void k_lresults(FlowScratch sc, const Payload *__restrict__ pay, int8_t *decision,
+                                                 int32_t *wait_ms) {
     if (!gate_is(sc.gate, kGateSeq | kGateBad, 0)) return;
     const uint32_t nvalid = sc.counters[0];
     const uint32_t j = blockIdx.x * kT + threadIdx.x;
     if (j >= nvalid) return;
     const uint32_t r = sc.ev_run[j];
-    if (sc.run_mode[r] != RUN_FAST) return;
+    const uint8_t mode = sc.run_mode[r];
+    if (mode == RUN_DONE) return;
     const Payload q = pay[j];
     if (q.idx & F_EXIT) return;
-    decision[q.idx & F_IDX] = sc.ev_eidx[j] < sc.run_f[r] ? D_PASS : D_BLOCK_FLOW;
+    if (mode == RUN_FAST) {
+        decision[q.idx & F_IDX] = sc.ev_eidx[j] < sc.run_f[r] ? D_PASS : D_BLOCK_FLOW;
+    } else {
+        const uint32_t v = sc.ev_eidx[j];
+        if (v == ~0u) return;
+        decision[q.idx & F_IDX] = (v & 1u) ? D_BLOCK_FLOW : D_PASS;
+        if (wait_ms) wait_ms[q.idx & F_IDX] = (int32_t)(v >> 1);
+    }
 }
 
 __global__ void k_node_view(FlowState st, int64_t max_rt, uint32_t r, int64_t now, double *dv, int64_t *iv) {
@@ -3010,7 +3060,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
                            d_dec.p, d_wait.p, heavy_prof());
-        hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, stream, sc, pay, d_dec.p);
+        hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, stream, sc, pay, d_dec.p, d_wait.p);
         if (has_in)  // ENTRY_NODE statistics of the inbound events
             hipLaunchKernelGGL(k_entry_stats, dim3(1), dim3(kEnTile), 0, stream, st, (int64_t)cfg.statistic_max_rt,
                                d_kind.p, d_resid.p, d_ts.p, lo, d_acq.p, d_flags.p, d_rt.p, d_dec.p, (uint32_t)m);
@@ -3089,7 +3139,7 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
     hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
                        st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
                        heavy_prof());
-    hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, s, gsc, pay, d_decision);
+    hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, s, gsc, pay, d_decision, wait_p);
     hipLaunchKernelGGL(k_entry_stats, dim3(1), dim3(kEnTile), 0, s, st, (int64_t)cfg.statistic_max_rt, d_kind_in,
                        d_resource, d_ts_off, ts_base, d_acquire, flags_p, rt_p, d_decision, m);
     if (sys.check || d_param_values)
