@@ -149,6 +149,53 @@ __device__ __forceinline__ int64_t mov64(int64_t old, int64_t v) {
 }
 }  // namespace dpp
 
+namespace dpp {
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ int mov32(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, kCtrl, kRowMask, 0xf, false);
+}
+}  // namespace dpp
+
+// inclusive prefix max / min of an int64 over the wave (lane order)
+__device__ __forceinline__ int64_t wave_incl_max_i64(int64_t v) {
+    v = max(v, dpp::mov64<0x111, 0xf>(INT64_MIN, v));
+    v = max(v, dpp::mov64<0x112, 0xf>(INT64_MIN, v));
+    v = max(v, dpp::mov64<0x114, 0xf>(INT64_MIN, v));
+    v = max(v, dpp::mov64<0x118, 0xf>(INT64_MIN, v));
+    v = max(v, dpp::mov64<0x142, 0xa>(INT64_MIN, v));
+    v = max(v, dpp::mov64<0x143, 0xc>(INT64_MIN, v));
+    return v;
+}
+__device__ __forceinline__ int64_t wave_incl_min_i64(int64_t v) {
+    v = min(v, dpp::mov64<0x111, 0xf>(INT64_MAX, v));
+    v = min(v, dpp::mov64<0x112, 0xf>(INT64_MAX, v));
+    v = min(v, dpp::mov64<0x114, 0xf>(INT64_MAX, v));
+    v = min(v, dpp::mov64<0x118, 0xf>(INT64_MAX, v));
+    v = min(v, dpp::mov64<0x142, 0xa>(INT64_MAX, v));
+    v = min(v, dpp::mov64<0x143, 0xc>(INT64_MAX, v));
+    return v;
+}
+
+// segmented inclusive sum of two int32 counters (a head flag starts a new segment at its lane)
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void segsum2_step(int &a, int &b, int &hd) {
+    const int ya = dpp::mov32<kCtrl, kRowMask>(0, a), yb = dpp::mov32<kCtrl, kRowMask>(0, b);
+    const int yh = dpp::mov32<kCtrl, kRowMask>(0, hd);
+    if (!hd) {
+        a += ya;
+        b += yb;
+    }
+    hd |= yh;
+}
+__device__ __forceinline__ void wave_incl_segsum2(int &a, int &b, int &hd) {
+    segsum2_step<0x111, 0xf>(a, b, hd);
+    segsum2_step<0x112, 0xf>(a, b, hd);
+    segsum2_step<0x114, 0xf>(a, b, hd);
+    segsum2_step<0x118, 0xf>(a, b, hd);
+    segsum2_step<0x142, 0xa>(a, b, hd);
+    segsum2_step<0x143, 0xc>(a, b, hd);
+}
+
 // inclusive prefix sum of an int64 over the wave (lane order)
 __device__ __forceinline__ int64_t wave_incl_sum_i64(int64_t v) {
     v += dpp::mov64<0x111, 0xf>(0, v);

@@ -1992,6 +1992,9 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     if (qrank[k] != 0xFFFF) qord[lcnt[qslot[k] & 63u] + qrank[k]] = (uint16_t)k;
                 __builtin_amdgcn_wave_barrier();
                 Ctx cl = c;
+                // the rule in registers: through a generic pointer its fields would be reloaded after
+                // every store to the LDS entries (possible aliasing), one global latency per event
+                const ParamRuleDev prule = *cache_p;
                 for (uint32_t i = start; i < start + mine; ++i) {
                     const uint32_t k = qord[i];
                     const Payload q = qpay[k];
@@ -2007,7 +2010,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     cl.pentry = &lent[qslot[k]];
                     int64_t w = 0;
                     // a QPS rule does not read the thread count
-                    const bool pass = param_pass(cl, *cache_p, qpv[k], (int)(q.acq_prio & 0x7FFFFFFFu),
+                    const bool pass = param_pass(cl, prule, qpv[k], (int)(q.acq_prio & 0x7FFFFFFFu),
                                                  ts_base + (int64_t)q.ts_off, 0, &w);
                     qpre[k] = pass ? 1 : 2;
                     qpw[k] = (int32_t)w;
@@ -2046,8 +2049,9 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     // non-decreasing) gives the window counts after every exit; the bulk part ends at
                     // the first exit whose counts trip a CLOSED breaker (cb_trips, the predicate of
                     // cb_on_complete) or at the first entry at or after an OPEN breaker's retry time.
-                    // Lane 0 replays from there while the breaker is HALF_OPEN.  Several breakers, or
-                    // a stat window that goes back, replay in order on lane 0.
+                    // Lane 0 steps the event that ends a bulk part; while the breaker is HALF_OPEN the
+                    // entries up to the next exit block in bulk.  Several breakers, or a stat window
+                    // that goes back, replay in order on lane 0.
                     uint32_t pos = 0;
                     while (pos < cnt) {
                         const CbDev &b0 = lcbs[0];
@@ -2065,14 +2069,8 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                                 const bool badv = ex && (b0.grade == 0 ? qrt[k] > b0.max_allowed_rt
                                                                        : (qpay[k].idx & F_ERROR) != 0);
                                 // previous exit's window: prefix max over the lanes (windows only grow)
-                                int64_t pm = ws;
-#pragma unroll
-                                for (int o = 1; o < 64; o <<= 1) {
-                                    const int64_t y = __shfl_up(pm, o, 64);
-                                    if (lane >= o && y > pm) pm = y;
-                                }
-                                int64_t prev = __shfl_up(pm, 1, 64);
-                                if (lane == 0) prev = INT64_MIN;
+                                const int64_t pm = wave_incl_max_i64(ws);
+                                int64_t prev = wave_shr1_i64(pm, INT64_MIN);
                                 if (prev < cws) prev = cws;  // carry from earlier rounds / the breaker
                                 const bool mono = !(ex && prev != kAbsent && ws < prev);
                                 if (!__all(mono)) {  // the clock went back: the rest replays in order
@@ -2082,18 +2080,9 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                                 }
                                 const bool head = ex && (prev == kAbsent || ws != prev);
                                 // segmented inclusive scan of (bad, total) over the exits
-                                int64_t sb = badv ? 1 : 0, stt = ex ? 1 : 0;
-                                uint32_t hd = head ? 1u : 0u;
-#pragma unroll
-                                for (int o = 1; o < 64; o <<= 1) {
-                                    const int64_t yb = __shfl_up(sb, o, 64), yt = __shfl_up(stt, o, 64);
-                                    const uint32_t yh = (uint32_t)__shfl_up((int)hd, o, 64);
-                                    if (lane >= o && !hd) {
-                                        sb += yb;
-                                        stt += yt;
-                                    }
-                                    if (lane >= o) hd |= yh;
-                                }
+                                int sb32 = badv ? 1 : 0, st32 = ex ? 1 : 0, hd = head ? 1 : 0;
+                                wave_incl_segsum2(sb32, st32, hd);  // counts inside the round (< 64)
+                                int64_t sb = sb32, stt = st32;
                                 if (!hd) {  // no window start before this lane in the round: continue the carry
                                     sb += (prev == cws) ? cbad : 0;
                                     stt += (prev == cws) ? ctot : 0;
@@ -2114,12 +2103,26 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                                 const uint64_t eb = __ballot(ex);
                                 if (eb) {
                                     const int last = 63 - __clzll((unsigned long long)eb);
-                                    cws = __shfl(ws, last, 64);
-                                    cbad = __shfl(sb, last, 64);
-                                    ctot = __shfl(stt, last, 64);
+                                    cws = readlane_i64(ws, last);
+                                    cbad = readlane_i64(sb, last);
+                                    ctot = readlane_i64(stt, last);
                                 }
                             }
                             end = stop == 0xFFFFFFFFu ? cnt : stop;
+                        } else if (!seq_rest) {
+                            // HALF_OPEN: tryPass blocks every entry (AbstractCircuitBreaker.tryPass) until
+                            // the next exit decides the probe (onRequestComplete closes or reopens), so the
+                            // bulk part runs up to that exit
+                            uint32_t stop = cnt;
+                            for (uint32_t r0 = pos; r0 < cnt; r0 += 64) {
+                                const uint32_t k = r0 + lane;
+                                const uint64_t eb = __ballot(k < cnt && (qpay[k].idx & F_EXIT));
+                                if (eb) {
+                                    stop = r0 + (uint32_t)__ffsll((unsigned long long)eb) - 1;
+                                    break;
+                                }
+                            }
+                            end = stop;
                         }
                         int le = -1;  // last exit inside the bulk part
                         for (uint32_t k = pos + lane; k < end; k += 64) {
@@ -2154,9 +2157,9 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                             uint32_t k = end;
                             if (seq_rest) {
                                 for (; k < cnt; ++k) step(k);
-                            } else if (k < cnt) {  // the event that ended the bulk part, then HALF_OPEN
+                            } else if (k < cnt) {  // the event that ended the bulk part (a HALF_OPEN
+                                                   // stretch after it is the next bulk part)
                                 step(k++);
-                                while (k < cnt && lcbs[0].state == 2) step(k++);
                             }
                             bulk_end = (int)k;
                         }
@@ -2179,6 +2182,19 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                 // s: pass acquire, block acquire, success, rt sum, exceptions, thread delta (uniform
                 // over the lanes; lane 0 applies them)
                 int64_t cur = INT64_MIN, tf = 0, s[6] = {0, 0, 0, 0, 0, 0}, rt_min = INT64_MAX;
+                // per-lane partial sums of the current bucket run, reduced (DPP) only when the run
+                // ends or a round crosses a bucket boundary
+                int64_t lv[6] = {0, 0, 0, 0, 0, 0}, lmn = INT64_MAX;
+                auto fold = [&]() {
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) {
+                        s[i] += readlane_i64(wave_incl_sum_i64(lv[i]), 63);
+                        lv[i] = 0;
+                    }
+                    const int64_t mn = readlane_i64(wave_incl_min_i64(lmn), 63);
+                    if (mn < rt_min) rt_min = mn;
+                    lmn = INT64_MAX;
+                };
                 bool any = false;
                 auto flush = [&]() {
                     if (!any || lane != 0) return;
@@ -2198,6 +2214,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     lnode[kNodeThreads] += s[5];
                 };
                 auto open = [&](uint32_t k) {  // a new bucket run starts at event k
+                    fold();
                     flush();
                     cur = qbq[k];
                     tf = ts_base + (int64_t)qpay[k].ts_off;
@@ -2227,18 +2244,9 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     const int64_t b0 = qbq[r0];
                     if (__all(!valid || qbq[k] == b0)) {  // one bucket over the round: a wave reduction
                         if (b0 != cur) open(r0);
-                        int64_t v[6] = {0, 0, 0, 0, 0, 0}, mn = INT64_MAX;
-                        if (valid) contrib(k, v, mn);
-#pragma unroll
-                        for (int o = 1; o < 64; o <<= 1) {
-#pragma unroll
-                            for (int i = 0; i < 6; ++i) v[i] += __shfl_xor(v[i], o, 64);
-                            const int64_t y = __shfl_xor(mn, o, 64);
-                            if (y < mn) mn = y;
-                        }
-                        for (int i = 0; i < 6; ++i) s[i] += v[i];
-                        if (mn < rt_min) rt_min = mn;
+                        if (valid) contrib(k, lv, lmn);
                     } else {  // a bucket boundary inside the round: event by event (uniform)
+                        fold();
                         const uint32_t e = min(cnt, r0 + 64);
                         for (uint32_t j = r0; j < e; ++j) {
                             if (qbq[j] != cur) open(j);
@@ -2246,6 +2254,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                         }
                     }
                 }
+                fold();
                 flush();
             }
             if (!agg && threadIdx.x == 0) {
@@ -2891,6 +2900,7 @@ void print_heavy_prof() {
             "lanes %.2f replay %.2f writeback+stores %.2f dedupe %.2f find %.2f (100 MHz wall clock)\n", best,
             (unsigned long long)h[best * 8 + 5], h[best * 8] / 1e5, h[best * 8 + 1] / 1e5, h[best * 8 + 2] / 1e5,
             h[best * 8 + 3] / 1e5, h[best * 8 + 4] / 1e5, h[best * 8 + 6] / 1e5, h[best * 8 + 7] / 1e5);
+    (void)hipMemset(g_heavy_prof, 0, 1024 * 8 * sizeof(uint64_t));
 }
 
 int FlowEngine::ensure_scratch() {
@@ -3060,6 +3070,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
                            d_dec.p, d_wait.p, heavy_prof());
+        if (heavy_prof()) print_heavy_prof();
         hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, stream, sc, pay, d_dec.p, d_wait.p);
         if (has_in)  // ENTRY_NODE statistics of the inbound events
             hipLaunchKernelGGL(k_entry_stats, dim3(1), dim3(kEnTile), 0, stream, st, (int64_t)cfg.statistic_max_rt,
@@ -3139,6 +3150,7 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
     hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
                        st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
                        heavy_prof());
+        if (heavy_prof()) print_heavy_prof();
     hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, s, gsc, pay, d_decision, wait_p);
     hipLaunchKernelGGL(k_entry_stats, dim3(1), dim3(kEnTile), 0, s, st, (int64_t)cfg.statistic_max_rt, d_kind_in,
                        d_resource, d_ts_off, ts_base, d_acquire, flags_p, rt_p, d_decision, m);
