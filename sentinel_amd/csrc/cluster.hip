@@ -2297,7 +2297,10 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
 // (k_hot_pick numbers them first) in the segment's first two buckets are staged in LDS; a lane whose
 // run is staged still issues its gather, pointed at one shared line, so the loads stay unconditional.
 constexpr int kFinChunk = 8;
-constexpr uint32_t kFinCache = 1024;
+#ifndef SGA_FIN_CACHE_N
+#define SGA_FIN_CACHE_N 1024
+#endif
+constexpr uint32_t kFinCache = SGA_FIN_CACHE_N;
 constexpr int kFinWgThreads = 1024;
 constexpr int kFinWaves = kFinWgThreads / 64;
 constexpr uint32_t kFinSpan = kHotSeg / kFinWaves;  // requests per wave
@@ -3260,8 +3263,10 @@ void batch_scratch_release(BatchScratch &sc) {
     if (sc.side) (void)hipStreamDestroy(sc.side);
     if (sc.ev_fork) (void)hipEventDestroy(sc.ev_fork);
     if (sc.ev_join) (void)hipEventDestroy(sc.ev_join);
+    if (sc.ev_fork0) (void)hipEventDestroy(sc.ev_fork0);
+    if (sc.ev_pre) (void)hipEventDestroy(sc.ev_pre);
     sc.side = nullptr;
-    sc.ev_fork = sc.ev_join = nullptr;
+    sc.ev_fork = sc.ev_join = sc.ev_fork0 = sc.ev_pre = nullptr;
 }
 
 static int cold_split() {  // A/B knob: 1 (cooperative flows) / 2 (per-lane flows) split the cold stage into
@@ -3486,29 +3491,37 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(hkb, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out,
                        fz_debug(), d0, sc.radix.hist, ntiles_sort);
     hipLaunchKernelGGL(k_hot_mode, dim3(1), dim3(1024), 0, s, sc, nseg * kKeyWaves, nseg);
-    hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
-    hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, s, sc, ngroups);
-    hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
-    const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
-                                        kSlotShift, bits, sc.radix, s, true);
-    const uint64_t *el = (np & 1) ? sc.el[0] : sc.el[1];
-    const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
-    // the hot side (disjoint rules, disjoint results) beside the cold stage: the cold flows are bound
-    // by record-load latency at low occupancy, the hot results stream
+    // the hot side (disjoint rules, disjoint results) runs on a side stream: its count scans beside
+    // the sort, its runs and results beside the cold stage (the cold flows are bound by record-load
+    // latency at low occupancy, the hot results stream)
     const bool ovl = hot_overlap() && !(fz_debug() & 16);
     hipStream_t hs = s;
     if (ovl) {
         if (!sc.side) {
             SGA_HIP_CHECK(hipStreamCreateWithFlags(&sc.side, hipStreamNonBlocking));
+            SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork0, hipEventDisableTiming));
             SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork, hipEventDisableTiming));
             SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_join, hipEventDisableTiming));
         }
-        SGA_HIP_CHECK(hipEventRecord(sc.ev_fork, s));
-        SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork, 0));
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_fork0, s));
+        SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork0, 0));
         hs = sc.side;
     }
-    hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, el);
+    hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
+    hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, hs, sc, ngroups);
+    hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
     hipLaunchKernelGGL(k_hot_pre, dim3(kHotBuckets), dim3(kThreads), 0, hs, sc);
+    const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
+                                        kSlotShift, bits, sc.radix, s, true);
+    const uint64_t *el = (np & 1) ? sc.el[0] : sc.el[1];
+    const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
+    // the hot runs and results once the sort is done (the prioritized hot requests are sorted with
+    // the cold ones), beside the cold stage
+    if (ovl) {
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_fork, s));
+        SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork, 0));
+    }
+    hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, el);
     hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, hs, st, sc, ts_base);
     if (ovl) {
         hipLaunchKernelGGL(k_hot_final, dim3(nseg), dim3(kFinWgThreads), 0, hs, sc, n, out, fin_cache());
