@@ -839,9 +839,12 @@ __device__ __forceinline__ FAgg fagg_block_excl(const FAgg &v, FAgg *total, FAgg
 // kMode: kFzAll = the three phases in one launch (small batches: one workgroup's worth of
 // launches); kFzRuns = phase 1 only, every run record to the global packed array and the owned
 // rules published to the global rule list (k_cold_flows decides them); kFzResults = phase 3 only.
+#ifndef SGA_FZ_WAVES
+#define SGA_FZ_WAVES 2
+#endif
 enum : int { kFzAll = 0, kFzRuns = 1, kFzResults = 2 };
 template <int kMode>
-__global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, BatchScratch sc,
+__global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(SGA_FZ_WAVES))) void k_cold_fused_t(ClusterState st, BatchScratch sc,
                                                              const uint64_t *__restrict__ el, uint32_t nhost,
                                                              const uint32_t *__restrict__ dn, uint32_t nkey,
                                                              const int32_t *__restrict__ acquire,

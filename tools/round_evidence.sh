@@ -19,4 +19,8 @@ timeout -k 10 400 python3 bench.py > $out/bench.json 2> $out/bench.err || { echo
 cat $out/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_$tag -o run --output-format csv -- python3 bench.py --no-cpu > $out/prof_bench.json 2> $out/prof_bench.err || { echo "prof failed"; tail -20 $out/prof_bench.err; exit 1; }
 find /tmp/prof_$tag -name "*kernel_stats.csv" -exec cp {} $out/kernel_stats.csv \;
-python3 tools/kstats.py $out/kernel_stats.csv | grep -E 'k_(classify|rs64|scan|row_scan|runs|flows|results)'
+find /tmp/prof_$tag -name "*kernel_trace.csv" -exec cp {} $out/kernel_trace.csv \;
+python3 tools/kstats.py $out/kernel_stats.csv > $out/kstats.txt
+python3 tools/ktrace.py $out/kernel_trace.csv --last 10 > $out/ktrace.txt
+head -24 $out/ktrace.txt
+bash tools/local_configs.sh ${tag}_lc
