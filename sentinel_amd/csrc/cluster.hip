@@ -2174,6 +2174,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
         HotRun z{};
         z.start = stb;
         *hrun_at(sc, h, bd_lo + lane) = z;
+        sc.hfin[(size_t)(bd_lo + lane) * kHot + h] = make_uint4(0u, 0u, 0u, stb);
     }
     uint64_t rm = __ballot(nrun > 0);
     if (!rm) return;
@@ -2291,6 +2292,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
             r.wait = (uint16_t)(1000 / P.S);
             r.ok = ok ? 1 : 0;
             *hrun_at(sc, h, b) = r;
+            sc.hfin[(size_t)b * kHot + h] = make_uint4((uint32_t)s0, (uint32_t)((uint64_t)s0 >> 32), f, j0);
         }
     }
 }
@@ -2345,11 +2347,9 @@ __global__ __launch_bounds__(kFinWgThreads) void k_hot_final(BatchScratch sc, ui
 #pragma unroll
         for (uint32_t k = 0; k < 2; ++k) {
             const uint32_t b = min(b0 + k, (uint32_t)kHotBuckets - 1);
-            const uint4 *hp = reinterpret_cast<const uint4 *>(hrun_at(sc, h, b));
-            const uint2 s0 = *reinterpret_cast<const uint2 *>(hp);
-            const uint4 r1 = hp[1];
-            c_s0[k][h] = i64_of(s0.x, s0.y);
-            c_fs[k][h] = make_uint2(r1.z, r1.w);
+            const uint4 fr = sc.hfin[(size_t)b * kHot + h];  // contiguous over h
+            c_s0[k][h] = i64_of(fr.x, fr.y);
+            c_fs[k][h] = make_uint2(fr.z, fr.w);
         }
     }
     __syncthreads();
@@ -3336,6 +3336,7 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up(hot_groups(cap) * kHot * 4);                                     // hgsum
     b += align_up((size_t)kHotBuckets * kHot * 2) + align_up(kHotBuckets * 4);     // hpre, hbnd
     b += align_up((size_t)kHot * kHotBuckets * sizeof(HotRun));                   // hrun
+    b += align_up((size_t)kHot * kHotBuckets * sizeof(uint4));                    // hfin
     b += align_up(kHot * sizeof(double2));                                        // hthr
     b += align_up(cap * 4);                                                        // prank
     b += 3 * align_up(kHot * 4);                                                   // plo, phi, hot_tot
@@ -3395,6 +3396,7 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.hpre = (uint16_t *)take((size_t)kHotBuckets * kHot * 2);
     sc.hbnd = (uint32_t *)take(kHotBuckets * 4);
     sc.hrun = (HotRun *)take((size_t)kHot * kHotBuckets * sizeof(HotRun));
+    sc.hfin = (uint4 *)take((size_t)kHot * kHotBuckets * sizeof(uint4));
     sc.hthr = (double2 *)take(kHot * sizeof(double2));
     sc.prank = (uint32_t *)take(cap * 4);
     sc.plo = (uint32_t *)take(kHot * 4);

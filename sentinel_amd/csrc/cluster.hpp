@@ -189,7 +189,8 @@ struct BatchScratch {
     uint32_t *hgsum;          // [group][kHot] group sums, then exclusive prefixes over groups
     uint16_t *hpre;           // [kHotBuckets][kHot] the segment's hot requests before the bucket's first
     uint32_t *hbnd;           // [kHotBuckets] the bucket's first request
-    HotRun *hrun;             // [kHot][kHotBuckets]
+    HotRun *hrun;             // [kHotBuckets][kHot]
+    uint4 *hfin;              // [kHotBuckets][kHot]: (s0, f, start) of each hot run, what k_hot_final caches
     double2 *hthr;            // [kHot] threshold and intervalInSecond of each hot rule (k_hot_flows)
     uint32_t *prank;          // per prioritized hot request (sorted region order): its rank
     uint32_t *plo, *phi;      // per hot id: its range in the prioritized region
