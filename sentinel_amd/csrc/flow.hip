@@ -382,28 +382,28 @@ __device__ bool hot_lookup(const Ctx &c, const ParamRuleDev &p, uint64_t v, int6
 }
 
 // ParamFlowChecker.passSingleValueCheck / passDefaultLocalCheck / passThrottleLocalCheck
-__device__ bool param_pass(const Ctx &c, const ParamRuleDev &p, uint64_t v, int acquire, int64_t t,
-                           int64_t thread_count, int64_t *wait_ms) {
+// QPS grade against the value's (lastAddTokenTime, tokens) or throttle-time entry e
+template <class E>
+__device__ __forceinline__ bool param_pass_qps(const Ctx &c, const ParamRuleDev &p, E &e, uint64_t v, int acquire,
+                                               int64_t t, int64_t *wait_ms) {
     *wait_ms = 0;
     int64_t hot;
-    if (p.grade == 1) {
+    {
         int64_t token_count = j_d2l(p.count);
         if (hot_lookup(c, p, v, &hot)) token_count = hot;
         if (token_count == 0) return false;
-        PEntry *e = c.pentry ? c.pentry : ptab_get(c.st.ptab, c.st.pmask, p.id + 1, v, true, c.st.overflow);
-        if (!e) return false;
         if (p.behavior == 2) {  // throttle, ParamFlowChecker.java:224-281
             const int64_t cost = j_round(1.0 * 1000 * (double)acquire * (double)p.duration / (double)token_count);
-            if (e->a == kPAbsent) {
-                e->a = t;
+            if (e.a == kPAbsent) {
+                e.a = t;
                 return true;
             }
-            const int64_t expected = e->a + cost;
+            const int64_t expected = e.a + cost;
             if (expected <= t || expected - t < p.max_queue) {
-                e->a = t;
+                e.a = t;
                 const int64_t wait = expected - t;
                 if (wait > 0) {
-                    e->a = expected;
+                    e.a = expected;
                     *wait_ms = wait;
                 }
                 return true;
@@ -413,36 +413,50 @@ __device__ bool param_pass(const Ctx &c, const ParamRuleDev &p, uint64_t v, int 
         // token bucket, ParamFlowChecker.java:132-222
         const int64_t max_count = lwrap_add(token_count, p.burst);
         if ((int64_t)acquire > max_count) return false;
-        if (e->a == kPAbsent) {
-            e->a = t;
-            if (e->b == kPAbsent) e->b = max_count - acquire;
+        if (e.a == kPAbsent) {
+            e.a = t;
+            if (e.b == kPAbsent) e.b = max_count - acquire;
             return true;
         }
-        const int64_t pass_time = t - e->a;
+        const int64_t pass_time = t - e.a;
         const int64_t dur_ms = lwrap_mul(p.duration, 1000);
         if (pass_time > dur_ms) {
-            if (e->b == kPAbsent) {
-                e->b = max_count - acquire;
-                e->a = t;
+            if (e.b == kPAbsent) {
+                e.b = max_count - acquire;
+                e.a = t;
                 return true;
             }
-            const int64_t rest = e->b;
+            const int64_t rest = e.b;
             const int64_t to_add = lwrap_mul(pass_time, token_count) / dur_ms;
             const int64_t nq = lwrap_add(to_add, rest) > max_count ? max_count - acquire
                                                                    : lwrap_add(rest, to_add) - acquire;
             if (nq < 0) return false;
-            e->b = nq;
-            e->a = t;
+            e.b = nq;
+            e.a = t;
             return true;
         }
-        if (e->b != kPAbsent) {
-            if (e->b - acquire >= 0) {
-                e->b -= acquire;
+        if (e.b != kPAbsent) {
+            if (e.b - acquire >= 0) {
+                e.b -= acquire;
                 return true;
             }
             return false;
         }
         return false;
+    }
+}
+
+__device__ bool param_pass(const Ctx &c, const ParamRuleDev &p, uint64_t v, int acquire, int64_t t,
+                           int64_t thread_count, int64_t *wait_ms) {
+    *wait_ms = 0;
+    int64_t hot;
+    if (p.grade == 1) {
+        int64_t token_count = j_d2l(p.count);
+        if (hot_lookup(c, p, v, &hot)) token_count = hot;
+        if (token_count == 0) return false;  // before any map access, as the reference
+        PEntry *e = c.pentry ? c.pentry : ptab_get(c.st.ptab, c.st.pmask, p.id + 1, v, true, c.st.overflow);
+        if (!e) return false;
+        return param_pass_qps(c, p, *e, v, acquire, t, wait_ms);
     }
     if (p.grade == 0) {
         if (hot_lookup(c, p, v, &hot)) return ++thread_count <= hot;
@@ -1839,53 +1853,66 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                 const uint32_t pown = cache_p->id + 1, town = res + 1;
                 uint32_t pfree = 0, tfree = 0;  // bit i: LDS slot lane + 64 i is absent and its home is free
                 for (int g0 = 0; g0 < kSl; g0 += kG) {
-                    uint64_t val[kG], pv[kG], tv[kG];
-                    uint32_t po[kG], to[kG];
+                    // the whole home entries are loaded together and unconditionally (an empty LDS
+                    // slot reads some valid home): a load under a branch would be waited for at the
+                    // branch, and an entry found at its home needs no second read
+                    uint64_t val[kG];
+                    int4 pe0[kG], pe1[kG], te0[kG], te1[kG];
+                    uint32_t ph[kG], th[kG];
 #pragma unroll
                     for (int u = 0; u < kG; ++u) {
                         val[u] = lval[threadIdx.x + 64 * (g0 + u)];
-                        po[u] = to[u] = 0xFFFFFFFFu;
-                        pv[u] = tv[u] = 0;
-                        if (val[u] == kLEmpty) continue;
-                        const PEntry *pe = &st.ptab[ptab_home(st.pmask, pown, val[u])];
-                        po[u] = __hip_atomic_load(&pe->owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        pv[u] = pe->value;
+                        const uint64_t vv = val[u] == kLEmpty ? 0ull : val[u];
+                        ph[u] = ptab_home(st.pmask, pown, vv);
+                        const int4 *pp = reinterpret_cast<const int4 *>(&st.ptab[ph[u]]);
+                        pe0[u] = pp[0];
+                        pe1[u] = pp[1];
+                        th[u] = ptab_home(st.tmask, town, vv);
                         if (pt) {
-                            const PEntry *te = &st.ttab[ptab_home(st.tmask, town, val[u])];
-                            to[u] = __hip_atomic_load(&te->owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            tv[u] = te->value;
+                            const int4 *tp = reinterpret_cast<const int4 *>(&st.ttab[th[u]]);
+                            te0[u] = tp[0];
+                            te1[u] = tp[1];
                         }
                     }
+                    auto as_entry = [](const int4 &x, const int4 &y) {
+                        PEntry e;
+                        e.value = ((uint64_t)(uint32_t)x.y << 32) | (uint32_t)x.x;
+                        e.owner = (uint32_t)x.z;
+                        e.pad = (uint32_t)x.w;
+                        e.a = (int64_t)(((uint64_t)(uint32_t)y.y << 32) | (uint32_t)y.x);
+                        e.b = (int64_t)(((uint64_t)(uint32_t)y.w << 32) | (uint32_t)y.z);
+                        return e;
+                    };
 #pragma unroll
                     for (int u = 0; u < kG; ++u) {
                         if (val[u] == kLEmpty) continue;
                         const int h = threadIdx.x + 64 * (g0 + u);
-                        PEntry *e;
-                        if (po[u] == 0) {
-                            e = nullptr;
+                        const PEntry hp = as_entry(pe0[u], pe1[u]);
+                        if (hp.owner == 0) {
                             pfree |= 1u << (g0 + u);
-                        } else if (po[u] == pown && pv[u] == val[u]) {
-                            e = &st.ptab[ptab_home(st.pmask, pown, val[u])];
+                        } else if (hp.owner == pown && hp.value == val[u]) {
+                            lgi[h] = ph[u];
+                            lent[h] = hp;
                         } else {
-                            e = ptab_get(st.ptab, st.pmask, pown, val[u], false, st.overflow);
-                        }
-                        if (e) {
-                            lgi[h] = (uint32_t)(e - st.ptab);
-                            lent[h] = *e;
+                            PEntry *e = ptab_get(st.ptab, st.pmask, pown, val[u], false, st.overflow);
+                            if (e) {
+                                lgi[h] = (uint32_t)(e - st.ptab);
+                                lent[h] = *e;
+                            }
                         }
                         if (pt) {
-                            PEntry *te;
-                            if (to[u] == 0) {
-                                te = nullptr;
+                            const PEntry ht = as_entry(te0[u], te1[u]);
+                            if (ht.owner == 0) {
                                 tfree |= 1u << (g0 + u);
-                            } else if (to[u] == town && tv[u] == val[u]) {
-                                te = &st.ttab[ptab_home(st.tmask, town, val[u])];
+                            } else if (ht.owner == town && ht.value == val[u]) {
+                                tgi[h] = th[u];
+                                tent[h] = ht;
                             } else {
-                                te = ptab_get(st.ttab, st.tmask, town, val[u], false, st.overflow);
-                            }
-                            if (te) {
-                                tgi[h] = (uint32_t)(te - st.ttab);
-                                tent[h] = *te;
+                                PEntry *te = ptab_get(st.ttab, st.tmask, town, val[u], false, st.overflow);
+                                if (te) {
+                                    tgi[h] = (uint32_t)(te - st.ttab);
+                                    tent[h] = *te;
+                                }
                             }
                         }
                     }
@@ -2007,11 +2034,13 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                         }
                         continue;
                     }
-                    cl.pentry = &lent[qslot[k]];
                     int64_t w = 0;
-                    // a QPS rule does not read the thread count
-                    const bool pass = param_pass(cl, prule, qpv[k], (int)(q.acq_prio & 0x7FFFFFFFu),
-                                                 ts_base + (int64_t)q.ts_off, 0, &w);
+                    // a QPS rule does not read the thread count; the entry is read and written back
+                    // through LDS directly (a generic pointer would turn every access into a flat op)
+                    PEntry pe = lent[qslot[k]];
+                    const bool pass = param_pass_qps(cl, prule, pe, qpv[k], (int)(q.acq_prio & 0x7FFFFFFFu),
+                                                     ts_base + (int64_t)q.ts_off, &w);
+                    lent[qslot[k]] = pe;
                     qpre[k] = pass ? 1 : 2;
                     qpw[k] = (int32_t)w;
                     if (pass && tmap) te.a = (te.a == kPAbsent ? 0 : te.a) + 1;  // ParameterMetric.addThreadCount
