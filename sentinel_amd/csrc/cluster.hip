@@ -3272,6 +3272,11 @@ void batch_scratch_release(BatchScratch &sc) {
     sc.ev_fork = sc.ev_join = sc.ev_fork0 = sc.ev_pre = nullptr;
 }
 
+static int hot_runs_main() {  // A/B knob: SGA_HOT_RUNS_MAIN=1 decides the hot runs before the cold stage
+    static const int v = getenv("SGA_HOT_RUNS_MAIN") ? atoi(getenv("SGA_HOT_RUNS_MAIN")) : 0;
+    return v;
+}
+
 static int cold_split() {  // A/B knob: 1 (cooperative flows) / 2 (per-lane flows) split the cold stage into
                            // runs, flows and results launches; 0 (default, measured faster) keeps the fused kernel
     static const int v = getenv("SGA_COLD_SPLIT") ? atoi(getenv("SGA_COLD_SPLIT")) : 0;
@@ -3516,18 +3521,30 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, hs, sc, ngroups);
     hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
     hipLaunchKernelGGL(k_hot_pre, dim3(kHotBuckets), dim3(kThreads), 0, hs, sc);
+    const bool hm = ovl && hot_runs_main();
+    if (hm) {
+        if (!sc.ev_pre) SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_pre, hipEventDisableTiming));
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_pre, hs));
+    }
     const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
                                         kSlotShift, bits, sc.radix, s, true);
     const uint64_t *el = (np & 1) ? sc.el[0] : sc.el[1];
     const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
     // the hot runs and results once the sort is done (the prioritized hot requests are sorted with
     // the cold ones), beside the cold stage
+    if (hm) {  // the hot runs (short, latency-bound) on the batch stream before the cold stage takes the CUs
+        SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_pre, 0));
+        hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el);
+        hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, s, st, sc, ts_base);
+    }
     if (ovl) {
         SGA_HIP_CHECK(hipEventRecord(sc.ev_fork, s));
         SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork, 0));
     }
-    hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, el);
-    hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, hs, st, sc, ts_base);
+    if (!hm) {
+        hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, el);
+        hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, hs, st, sc, ts_base);
+    }
     if (ovl) {
         hipLaunchKernelGGL(k_hot_final, dim3(nseg), dim3(kFinWgThreads), 0, hs, sc, n, out, fin_cache());
         hipLaunchKernelGGL(k_prio_results, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, el, out);
