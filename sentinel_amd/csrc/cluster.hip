@@ -811,16 +811,33 @@ __device__ __forceinline__ FAgg fagg_shfl_up(const FAgg &v, int o) {
                 __shfl_up(v.mn, o, 64), __shfl_up(v.mx, o, 64)};
 }
 
+// FAgg lane moves on DPP (identity where the source is outside the row / wave)
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ FAgg fagg_dpp(const FAgg &v) {
+    const FAgg id = fagg_id();
+    auto mv = [](uint32_t old, uint32_t x) {
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, kCtrl, kRowMask, 0xf, false);
+    };
+    return FAgg{mv(id.hpos, v.hpos), mv(id.np, v.np), mv(id.hp, v.hp), mv(id.flag, v.flag),
+                (int32_t)mv((uint32_t)id.mn, (uint32_t)v.mn), (int32_t)mv((uint32_t)id.mx, (uint32_t)v.mx)};
+}
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void fagg_scan_step(FAgg &x) {
+    x = fagg_combine(fagg_dpp<kCtrl, kRowMask>(x), x);
+}
+
 // Exclusive workgroup scan of one FAgg per thread (thread order = element order).  Returns the
-// exclusive prefix; *total gets the workgroup total.
+// exclusive prefix; *total gets the workgroup total.  The wave scan is DPP (row shifts, then row
+// broadcasts), not LDS shuffles.
 __device__ __forceinline__ FAgg fagg_block_excl(const FAgg &v, FAgg *total, FAgg *wtot) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     FAgg x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const FAgg y = fagg_shfl_up(x, o);
-        if (lane >= o) x = fagg_combine(y, x);
-    }
+    fagg_scan_step<0x111, 0xf>(x);
+    fagg_scan_step<0x112, 0xf>(x);
+    fagg_scan_step<0x114, 0xf>(x);
+    fagg_scan_step<0x118, 0xf>(x);
+    fagg_scan_step<0x142, 0xa>(x);
+    fagg_scan_step<0x143, 0xc>(x);
     if (lane == 63) wtot[wave] = x;
     __syncthreads();
     FAgg pre = fagg_id(), t = fagg_id();
@@ -829,8 +846,7 @@ __device__ __forceinline__ FAgg fagg_block_excl(const FAgg &v, FAgg *total, FAgg
         if (w < wave) pre = fagg_combine(pre, wtot[w]);
         t = fagg_combine(t, wtot[w]);
     }
-    FAgg ex = fagg_shfl_up(x, 1);
-    if (lane == 0) ex = fagg_id();
+    const FAgg ex = fagg_dpp<0x138, 0xf>(x);  // wave_shr:1, lane 0 gets the identity
     *total = t;
     __syncthreads();
     return fagg_combine(pre, ex);
@@ -1651,6 +1667,10 @@ __global__ __launch_bounds__(kThreads) void k_hot_precheck(ClusterState st, Batc
         sc.wconst[threadIdx.x] = wc;
     }
     const uint32_t h = blockIdx.x * kThreads + threadIdx.x;
+    if (h < (uint32_t)kHot) {  // the prioritized-range table of this batch (k_prio_rank fills it)
+        sc.plo[h] = 0;
+        sc.phi[h] = 0;
+    }
     if (h >= hot_count(sc) || n == 0) return;
     const int64_t W = (int64_t)sc.hot_ctl[2];
     const int64_t t0 = ts_base + (int64_t)ts_off[0];
@@ -3489,7 +3509,6 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
     const uint32_t ngroups = (nseg + kHotGroupRows - 1) / kHotGroupRows;
     SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, CTL_WORDS * 4, s));
-    SGA_HIP_CHECK(hipMemsetAsync(sc.plo, 0, 2 * align_up(kHot * 4), s));  // plo and phi (adjacent)
     hipLaunchKernelGGL(k_hot_precheck, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc, ts_off, ts_base, n);
     auto hka = st.dense_n ? k_hot_key_dense<0> : k_hot_key_hash<0>;
     auto hkb = st.dense_n ? k_hot_key_dense<1> : k_hot_key_hash<1>;
