@@ -852,15 +852,9 @@ __device__ __forceinline__ FAgg fagg_block_excl(const FAgg &v, FAgg *total, FAgg
     return fagg_combine(pre, ex);
 }
 
-// kMode: kFzAll = the three phases in one launch (small batches: one workgroup's worth of
-// launches); kFzRuns = phase 1 only, every run record to the global packed array and the owned
-// rules published to the global rule list (k_cold_flows decides them); kFzResults = phase 3 only.
-#ifndef SGA_FZ_WAVES
-#define SGA_FZ_WAVES 2
-#endif
-enum : int { kFzAll = 0, kFzRuns = 1, kFzResults = 2 };
+enum : int { kFzAll = 0 };
 template <int kMode>
-__global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(SGA_FZ_WAVES))) void k_cold_fused_t(ClusterState st, BatchScratch sc,
+__global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, BatchScratch sc,
                                                              const uint64_t *__restrict__ el, uint32_t nhost,
                                                              const uint32_t *__restrict__ dn, uint32_t nkey,
                                                              const int32_t *__restrict__ acquire,
@@ -939,7 +933,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(SGA_
     // ---- 1 runs (blocks of kFzChunk elements over [h0, E))
     FAgg carry = fagg_id();
     uint32_t nf_carry = 0;
-    for (uint32_t b0 = h0; b0 < (kMode == kFzResults ? h0 : E); b0 += kFzChunk) {
+    for (uint32_t b0 = h0; b0 < E; b0 += kFzChunk) {
         const uint32_t e0 = b0 + threadIdx.x * kFzPer;
         uint64_t x[kFzPer];
 #pragma unroll
@@ -997,9 +991,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(SGA_
                 const uint32_t head = run.hpos - 1;
                 const int32_t acq = run.mn == run.mx ? run.mn : 0;  // 0: mixed or escaped -> replay
                 const uint32_t bd = (uint32_t)((x[k] >> kBdShift) & kBdEsc);
-                if (kMode == kFzRuns) {  // packed record for k_cold_flows
-                    sc.run_rec[head] = make_uint4(p + 1 - head, run.np - run.hp, h0 + run.hp, (uint32_t)acq | (bd << 8));
-                } else if (head - h0 < (uint32_t)kFzChunk) {
+                if (head - h0 < (uint32_t)kFzChunk) {
                     rl_n[head - h0] = p + 1 - head;
                     rl_cp[head - h0] = run.np - run.hp;
                     rl_p0[head - h0] = h0 + run.hp;
@@ -1018,14 +1010,6 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(SGA_
         __syncthreads();
     }
     const uint32_t nf = nf_carry;
-    if (kMode == kFzRuns) {  // publish the owned rules: one reservation per workgroup
-        __syncthreads();
-        if (threadIdx.x == 0) s_cbase = nf ? atomicAdd(&sc.counters[CTL_NCRULE], nf) : 0u;
-        __syncthreads();
-        for (uint32_t f = threadIdx.x; f < nf; f += kFzThreads)
-            sc.crule[s_cbase + f] = make_uint4(fslot[f], fheads[f], f + 1 < nf ? fheads[f + 1] : E, 0u);
-        return;
-    }
     if (threadIdx.x == 0) s_ncand = 0;
     __syncthreads();  // run records and plist (global, this workgroup) before the flows read them
     // next-hot-set candidates: counts of at least the floor (half the last pick threshold) are
@@ -1033,7 +1017,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(SGA_
     const uint32_t cand_floor = max(hot_min, sc.hot_ctl[7] >> 1);
     fz_mark(dbg, 1, fzt);
     // ---- 2 flows: one lane per owned rule
-    for (uint32_t f = threadIdx.x; f < ((dbg & 1) || kMode == kFzResults ? 0u : nf); f += kFzThreads) {
+    for (uint32_t f = threadIdx.x; f < ((dbg & 1) ? 0u : nf); f += kFzThreads) {
         const uint32_t r0 = fheads[f];
         const uint32_t r1 = f + 1 < nf ? fheads[f + 1] : E;
         const uint32_t s = fslot[f];
@@ -1095,7 +1079,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(SGA_
     }
     __syncthreads();  // run_out of every owned run
     fz_mark(dbg, 2, fzt);
-    if (kMode == kFzAll) {
+    {
         const uint32_t nc = min(s_ncand, (uint32_t)kFzThreads);
         if (threadIdx.x == 0) s_cbase = nc ? atomicAdd(&sc.hot_ctl[6], nc) : 0u;
         __syncthreads();
@@ -1165,324 +1149,6 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(SGA_
     fz_mark(dbg, 3, fzt);
 }
 #define k_cold_fused k_cold_fused_t<kFzAll>
-
-// Cold flows of a large batch: one lane per rule of the global rule list k_cold_fused_t<kFzRuns>
-// published (rules are independent, so list order is free), walking its runs in time order with
-// the closed form or the exact replay.  Apart from the phases around it this kernel holds no LDS
-// and few registers, so many more rules are in flight than in the fused kernel (whose runs and
-// results phases need ~230 registers): the flows are bound by the latency of the record loads.
-constexpr int kCfThreads = 256;
-#ifndef SGA_CF_PAIRS
-#define SGA_CF_PAIRS 10
-#endif
-constexpr int kCfPairs = SGA_CF_PAIRS;  // buckets whose loads are issued together (sampleCount 10 = the default)
-__global__ __launch_bounds__(kCfThreads) void k_cold_flows(
-    ClusterState st, BatchScratch sc, const uint64_t *__restrict__ el, const int32_t *__restrict__ acquire,
-    const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off, int64_t ts_base, int simple,
-    uint32_t hot_min, uint64_t *__restrict__ out) {
-    const uint32_t nr = sc.counters[CTL_NCRULE];
-    const uint32_t cand_floor = max(hot_min, sc.hot_ctl[7] >> 1);
-    const int lane = threadIdx.x & 63;
-    const uint64_t lt = lanemask_lt64(lane);
-    const uint32_t stride = gridDim.x * kCfThreads;
-    for (uint32_t wb = blockIdx.x * kCfThreads + (threadIdx.x & ~63u); wb < nr; wb += stride) {  // wave-uniform
-        const uint32_t fi = wb + lane;
-        const bool act = fi < nr;
-        const uint4 ent = sc.crule[act ? fi : wb];
-        const uint32_t s = ent.x, r0 = ent.y, r1 = ent.z;
-        // next batch's hot-set candidates: one reservation per wave that has any
-        const bool cand = act && r1 - r0 >= cand_floor;
-        const uint64_t cm = __ballot(cand);
-        if (cm) {
-            const int first = __ffsll((long long)cm) - 1;
-            uint32_t b0 = 0;
-            if (lane == first) b0 = atomicAdd(&sc.hot_ctl[6], (uint32_t)__popcll(cm));
-            b0 = (uint32_t)__shfl((int)b0, first, 64);
-            const uint32_t k = b0 + (uint32_t)__popcll(cm & lt);
-            if (cand && k < (uint32_t)kHotCand) {
-                sc.hot_cand[2 * k] = s;
-                sc.hot_cand[2 * k + 1] = r1 - r0;
-            }
-        }
-        if (!act) continue;
-        const SlotParam P = st.param[s];
-        const Rec R = rec_of(st, P);
-        const double thr = simple ? P.thr_simple : P.thr;
-        const int64_t qbase = div_pos(ts_base, P.W);
-        for (uint32_t r = r0; r < r1;) {
-            const uint4 rr = sc.run_rec[r];
-            RunIn ri;
-            ri.j0 = r;
-            ri.n = rr.x;
-            ri.cp_tot = rr.y;
-            ri.p0 = rr.z;
-            ri.a = (int32_t)(rr.w & 0xFFu);
-            ri.bd = rr.w >> 8;
-            auto prio_before = [&](uint32_t k) -> uint32_t {
-                uint32_t lo = 0, hi = ri.cp_tot;
-#pragma nounroll
-                while (lo < hi) {
-                    const uint32_t m = (lo + hi) >> 1;
-                    if (sc.plist[ri.p0 + m] < ri.j0 + k) lo = m + 1;
-                    else hi = m;
-                }
-                return lo;
-            };
-            RunOut ro;
-            if (!run_fast<decltype(prio_before), kCfPairs>(st, P, R, thr, qbase, ri, prio_before, ro)) {
-                // this run and the rule's later runs are replayed by k_cold_slow (rare: escapes,
-                // mixed acquire counts, a clock regression); the replay's registers stay out of here
-                const uint32_t k = atomicAdd(&sc.counters[CTL_DEFERRED], 1u);
-                sc.deferred[2 * k] = fi;
-                sc.deferred[2 * k + 1] = r;
-                break;
-            }
-            sc.run_out[r] = ro;
-            r += ri.n;
-        }
-    }
-}
-
-// Cold flows, cooperative form: 16 lanes per rule (a DPP row), four rules per wave.  Lane j of a
-// row loads bucket j's (start, PASS) pair, lanes 0..2 the current bucket's other six counters and
-// lanes 3..4 the occupy state, so one wave-instruction touches the few lines of four records
-// instead of 64 lanes touching 64 records (the per-lane form is bound by that access shape, not by
-// bytes).  The arithmetic is run_fast's, computed redundantly by the 16 lanes; a rule's later runs
-// reuse the pairs in registers (lane cj updates its own pair).  Rules with S > 16, and any run the
-// closed form does not take, defer the rest of the rule to k_cold_slow (exact replay).
-constexpr int kRowLanes = 16;
-__device__ __forceinline__ int64_t row_sum_i64(int64_t v) {
-#pragma unroll
-    for (int o = 1; o < kRowLanes; o <<= 1) v += __shfl_xor(v, o, kRowLanes);
-    return v;
-}
-__device__ __forceinline__ int64_t row_get_i64(int64_t v, int src) { return __shfl(v, src, kRowLanes); }
-
-__global__ __launch_bounds__(kCfThreads) void k_cold_flows_coop(ClusterState st, BatchScratch sc,
-                                                                  int64_t ts_base, int simple, uint32_t hot_min) {
-    const uint32_t nr = sc.counters[CTL_NCRULE];
-    const uint32_t cand_floor = max(hot_min, sc.hot_ctl[7] >> 1);
-    const int lane = threadIdx.x & 63, gl = lane & (kRowLanes - 1);
-    const uint32_t per_wave = 64 / kRowLanes;
-    const uint32_t stride = gridDim.x * (kCfThreads / 64) * per_wave;
-    for (uint32_t wb = (blockIdx.x * (kCfThreads / 64) + (threadIdx.x >> 6)) * per_wave; wb < nr; wb += stride) {
-        const uint32_t fi = wb + (uint32_t)(lane / kRowLanes);
-        const bool act = fi < nr;  // row-uniform
-        const uint4 ent = sc.crule[act ? fi : wb];
-        const uint32_t s = ent.x, r0 = ent.y, r1 = ent.z;
-        {  // next batch's hot-set candidates (row leaders), one reservation per wave
-            const bool cand = act && gl == 0 && r1 - r0 >= cand_floor;
-            const uint64_t cm = __ballot(cand);
-            if (cm) {
-                const int first = __ffsll((long long)cm) - 1;
-                uint32_t b0 = 0;
-                if (lane == first) b0 = atomicAdd(&sc.hot_ctl[6], (uint32_t)__popcll(cm));
-                b0 = (uint32_t)__shfl((int)b0, first, 64);
-                const uint32_t k = b0 + (uint32_t)__popcll(cm & lanemask_lt64(lane));
-                if (cand && k < (uint32_t)kHotCand) {
-                    sc.hot_cand[2 * k] = s;
-                    sc.hot_cand[2 * k + 1] = r1 - r0;
-                }
-            }
-        }
-        if (!act) continue;
-        const SlotParam P = st.param[s];
-        uint4 rr = sc.run_rec[r0];
-        const Rec R = rec_of(st, P);
-        const int S = P.S;
-        auto defer = [&](uint32_t r) {
-            if (gl == 0) {
-                const uint32_t k = atomicAdd(&sc.counters[CTL_DEFERRED], 1u);
-                sc.deferred[2 * k] = fi;
-                sc.deferred[2 * k + 1] = r;
-            }
-        };
-        if (S > kRowLanes || S < 1) {
-            defer(r0);
-            continue;
-        }
-        const double thr = simple ? P.thr_simple : P.thr;
-        const int64_t qbase = div_pos(ts_base, P.W);
-        // first run's bucket, so the counter group can be loaded with the pairs
-        int64_t q = qbase + (int64_t)(rr.w >> 8);
-        int64_t qs = div_pos(q, S);
-        int cj = (int)(q - qs * S);
-        const int4 *v = reinterpret_cast<const int4 *>(R.r);
-        int4 pr = make_int4(0, 0, 0, 0), cx = make_int4(0, 0, 0, 0), oc = make_int4(0, 0, 0, 0);
-        if (gl < S) pr = v[gl];
-        if (gl < 3) cx = reinterpret_cast<const int4 *>(R.r + 2 * S + kOccWords + 6 * cj)[gl];
-        if (gl == 3) oc = reinterpret_cast<const int4 *>(R.r + 2 * S)[0];
-        if (gl == 4) oc = reinterpret_cast<const int4 *>(R.r + 2 * S)[1];
-        int64_t my_s = gl < S ? i64_lo(pr) : kAbsent, my_p = i64_hi(pr);
-        // occupy state (SlotOcc: occ_pass, occ_preq, has_occ) in every lane of the row
-        int64_t o_pass = row_get_i64(i64_lo(oc), 3), o_preq = row_get_i64(i64_hi(oc), 3);
-        int32_t o_has = __shfl(oc.x, 4, kRowLanes);
-        bool loaded_cx = true;
-        for (uint32_t r = r0; r < r1;) {  // row-uniform
-            if (r != r0) {
-                rr = sc.run_rec[r];
-                q = qbase + (int64_t)(rr.w >> 8);
-                qs = div_pos(q, S);
-                cj = (int)(q - qs * S);
-                loaded_cx = false;
-            }
-            const uint32_t n = rr.x, cp_tot = rr.y, p0 = rr.z;
-            const int32_t a = (int32_t)(rr.w & 0xFFu);
-            const int64_t ws = q * P.W, t0 = ws;
-            const int jh = cj + 1 == S ? 0 : cj + 1;
-            const int64_t old = row_get_i64(my_s, cj);
-            if (a <= 0 || (old != kAbsent && ws < old) || (cp_tot > 0 && (S <= 1 || 1000 / S <= 0))) {
-                defer(r);
-                break;
-            }
-            const bool valid = gl < S && my_s != kAbsent && !(t0 - my_s > (int64_t)P.interval);
-            const int64_t bp = row_sum_i64((gl != cj && valid) ? my_p : 0);
-            const int64_t hstart = row_get_i64(my_s, jh), hpass = row_get_i64(my_p, jh);
-            const bool rot = old == kAbsent || ws > old;
-            int64_t c[CEV_N];
-            bool occ_dirty = false;
-            if (rot) {
-#pragma unroll
-                for (int k = 0; k < CEV_N; ++k) c[k] = 0;
-                if (old != kAbsent && o_has) {  // resetWindowTo + transferOccupyToBucket
-                    c[CEV_OCCUPIED_PASS] += o_pass;
-                    c[CEV_PASS] += o_pass;
-                    c[CEV_PASS_REQUEST] += o_preq;
-                    o_pass = 0;
-                    o_preq = 0;
-                    o_has = 0;
-                    occ_dirty = true;
-                }
-            } else {
-                if (!loaded_cx) {  // the group may have been written by another lane of this row
-                    __threadfence_block();
-                    if (gl < 3) cx = reinterpret_cast<const int4 *>(R.r + 2 * S + kOccWords + 6 * cj)[gl];
-                }
-                c[CEV_PASS] = row_get_i64(my_p, cj);
-                c[CEV_WAITING] = row_get_i64(i64_lo(cx), 0);
-                c[CEV_BLOCK] = row_get_i64(i64_hi(cx), 0);
-                c[CEV_PASS_REQUEST] = row_get_i64(i64_lo(cx), 1);
-                c[CEV_BLOCK_REQUEST] = row_get_i64(i64_hi(cx), 1);
-                c[CEV_OCCUPIED_PASS] = row_get_i64(i64_lo(cx), 2);
-                c[CEV_OCCUPIED_BLOCK] = row_get_i64(i64_hi(cx), 2);
-            }
-            int64_t head;  // getValidHead after the rotation
-            if (jh == cj) head = c[CEV_PASS];
-            else head = (hstart != kAbsent && !(t0 - hstart > (int64_t)P.interval)) ? hpass : 0;
-            const int64_t s0 = bp + c[CEV_PASS];
-            const uint32_t f = pass_prefix(thr, P.isec, s0, a, n);
-            uint32_t cpf = cp_tot;
-            if (f < n && cp_tot > 0) {  // prioritized requests among the first f (plist ascending)
-                uint32_t lo = 0, hi = cp_tot;
-#pragma nounroll
-                while (lo < hi) {
-                    const uint32_t m = (lo + hi) >> 1;
-                    if (sc.plist[p0 + m] < r + f) lo = m + 1;
-                    else hi = m;
-                }
-                cpf = lo;
-            }
-            const uint32_t np_after = cp_tot - cpf;
-            uint32_t cw = 0;
-            if (np_after > 0) {  // row-uniform
-                __threadfence_block();
-                const int64_t wv = (gl != cj && valid) ? R.cnt(CEV_WAITING, gl) : 0;
-                const int64_t w0 = c[CEV_WAITING] + row_sum_i64(wv);
-                const double latest = (double)(s0 + (int64_t)f * a) / P.isec;
-                const double lim = st.max_occupy_ratio * thr;
-                uint32_t l2 = 0, h2 = np_after;
-#pragma nounroll
-                while (l2 < h2) {
-                    const uint32_t cc = l2 + ((h2 - l2) >> 1);
-                    const int64_t add = (int64_t)cc * a;
-                    const bool ok = ((double)(w0 + add) / P.isec <= lim) &&
-                                    (latest + (double)((int64_t)a + o_pass + add) - (double)head <= thr);
-                    if (ok) l2 = cc + 1;
-                    else h2 = cc;
-                }
-                cw = l2;
-                if (cw > 0) {
-                    o_pass += (int64_t)cw * a;
-                    o_preq += cw;
-                    o_has = 1;
-                    occ_dirty = true;
-                }
-            }
-            const uint32_t nblk = n - f - cw;
-            c[CEV_PASS] += (int64_t)f * a;
-            c[CEV_PASS_REQUEST] += f;
-            c[CEV_OCCUPIED_PASS] += (int64_t)cpf * a;
-            c[CEV_WAITING] += (int64_t)cw * a;
-            c[CEV_BLOCK] += (int64_t)nblk * a;
-            c[CEV_BLOCK_REQUEST] += nblk;
-            c[CEV_OCCUPIED_BLOCK] += (int64_t)(np_after - cw) * a;
-            // stores: lane cj its pair (kept in its registers for the rule's later runs), lanes 0..2
-            // the counter group, lanes 3..4 the occupy state, lanes 5..7 the run's decision record
-            if (gl == cj) {
-                if (rot) my_s = ws;
-                my_p = c[CEV_PASS];
-                reinterpret_cast<int4 *>(R.r)[cj] =
-                    make_int4((int)(uint32_t)my_s, (int)(my_s >> 32), (int)(uint32_t)my_p, (int)(my_p >> 32));
-            }
-            if (gl < 3) {
-                const int64_t lo = gl == 0 ? c[CEV_WAITING] : (gl == 1 ? c[CEV_PASS_REQUEST] : c[CEV_OCCUPIED_PASS]);
-                const int64_t hi = gl == 0 ? c[CEV_BLOCK] : (gl == 1 ? c[CEV_BLOCK_REQUEST] : c[CEV_OCCUPIED_BLOCK]);
-                cx = make_int4((int)(uint32_t)lo, (int)(lo >> 32), (int)(uint32_t)hi, (int)(hi >> 32));
-                reinterpret_cast<int4 *>(R.r + 2 * S + kOccWords + 6 * cj)[gl] = cx;
-            }
-            if (occ_dirty) {
-                if (gl == 3)
-                    reinterpret_cast<int4 *>(R.r + 2 * S)[0] = make_int4((int)(uint32_t)o_pass, (int)(o_pass >> 32),
-                                                                         (int)(uint32_t)o_preq, (int)(o_preq >> 32));
-                if (gl == 4) reinterpret_cast<int32_t *>(R.r + 2 * S)[4] = o_has;
-            }
-            if (gl >= 5 && gl < 8) {
-                RunOut *ro = sc.run_out + r;
-                if (gl == 5) {
-                    ro->s0 = s0;
-                    ro->thr = thr;
-                } else if (gl == 6) {
-                    ro->isec = P.isec;
-                    ro->f = f;
-                    ro->cpf = cpf;
-                } else {
-                    ro->cw = cw;
-                    ro->wait = (uint16_t)(1000 / S);
-                    ro->mode = RUN_FAST;
-                }
-            }
-            r += n;
-        }
-    }
-}
-
-// The deferred tails of k_cold_flows: one lane per (rule, first run to replay) replays every later
-// request of the rule in order with the exact restatement (request_exact) and marks the runs done.
-__global__ __launch_bounds__(kCfThreads) void k_cold_slow(ClusterState st, BatchScratch sc,
-                                                           const uint64_t *__restrict__ el,
-                                                           const int32_t *__restrict__ acquire,
-                                                           const uint8_t *__restrict__ prio,
-                                                           const uint32_t *__restrict__ ts_off, int64_t ts_base,
-                                                           int simple, uint64_t *__restrict__ out) {
-    const uint32_t nd = sc.counters[CTL_DEFERRED];
-    for (uint32_t k = blockIdx.x * kCfThreads + threadIdx.x; k < nd; k += gridDim.x * kCfThreads) {
-        const uint4 ent = sc.crule[sc.deferred[2 * k]];
-        const uint32_t s = ent.x, r1 = ent.z;
-        for (uint32_t r = sc.deferred[2 * k + 1]; r < r1;) {
-            const uint32_t nrun = sc.run_rec[r].x;
-            for (uint32_t j = r; j < r + nrun; ++j) {
-                const uint32_t i = el_idx(el[j]);
-                const int64_t t = ts_base + (int64_t)ts_off[i];
-                const bool p = !simple && prio && prio[i];
-                out[i] = request_exact(st, s, t, acquire[i], p, simple);
-            }
-            RunOut ro;
-            ro.mode = RUN_DONE;
-            sc.run_out[r] = ro;
-            r += nrun;
-        }
-    }
-}
 
 // ---------------------------------------------------------------- small batches (one call, few requests)
 // A batch of at most kSmall requests (a single TokenService.requestToken, or the few a coalescing
@@ -3287,47 +2953,17 @@ void batch_scratch_release(BatchScratch &sc) {
     if (sc.ev_fork) (void)hipEventDestroy(sc.ev_fork);
     if (sc.ev_join) (void)hipEventDestroy(sc.ev_join);
     if (sc.ev_fork0) (void)hipEventDestroy(sc.ev_fork0);
-    if (sc.ev_pre) (void)hipEventDestroy(sc.ev_pre);
     sc.side = nullptr;
-    sc.ev_fork = sc.ev_join = sc.ev_fork0 = sc.ev_pre = nullptr;
+    sc.ev_fork = sc.ev_join = sc.ev_fork0 = nullptr;
 }
 
-static int hot_runs_main() {  // A/B knob: SGA_HOT_RUNS_MAIN=1 decides the hot runs before the cold stage
-    static const int v = getenv("SGA_HOT_RUNS_MAIN") ? atoi(getenv("SGA_HOT_RUNS_MAIN")) : 0;
-    return v;
-}
 
-static int cold_split() {  // A/B knob: 1 (cooperative flows) / 2 (per-lane flows) split the cold stage into
-                           // runs, flows and results launches; 0 (default, measured faster) keeps the fused kernel
-    static const int v = getenv("SGA_COLD_SPLIT") ? atoi(getenv("SGA_COLD_SPLIT")) : 0;
-    return v;
-}
-
-// Cold stage of a large batch over the sorted elements: runs (+ rule list), flows, results.
+// Cold stage of a large batch over the sorted elements: runs, flows and results in one kernel.
 static void cold_stage(const ClusterState &st, BatchScratch &sc, const uint64_t *el, uint32_t n, const uint32_t *dn,
                        uint32_t invalid_key, const int32_t *acquire, const uint8_t *prio, const uint32_t *ts_off,
                        int64_t ts_base, int simple, uint32_t hot_min, uint64_t *out, hipStream_t s) {
-    const dim3 grid((n + kFzChunk - 1) / kFzChunk);
-    if (!cold_split() || (fz_debug() & 16)) {
-        hipLaunchKernelGGL(k_cold_fused, grid, dim3(kFzThreads), 0, s, st, sc, el, n, dn, invalid_key, acquire, prio,
-                           ts_off, ts_base, simple, hot_min, out, fz_debug());
-        return;
-    }
-    hipLaunchKernelGGL(k_cold_fused_t<kFzRuns>, grid, dim3(kFzThreads), 0, s, st, sc, el, n, dn, invalid_key, acquire,
-                       prio, ts_off, ts_base, simple, hot_min, out, 0);
-    if (cold_split() == 2) {  // per-lane flows (A/B)
-        const uint32_t fgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kCfThreads - 1) / kCfThreads, 4096));
-        hipLaunchKernelGGL(k_cold_flows, dim3(fgrid), dim3(kCfThreads), 0, s, st, sc, el, acquire, prio, ts_off,
-                           ts_base, simple, hot_min, out);
-    } else {
-        const uint32_t per_wg = (kCfThreads / 64) * (64 / kRowLanes);
-        const uint32_t fgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + per_wg - 1) / per_wg, 8192));
-        hipLaunchKernelGGL(k_cold_flows_coop, dim3(fgrid), dim3(kCfThreads), 0, s, st, sc, ts_base, simple, hot_min);
-    }
-    hipLaunchKernelGGL(k_cold_slow, dim3(64), dim3(kCfThreads), 0, s, st, sc, el, acquire, prio, ts_off, ts_base,
-                       simple, out);
-    hipLaunchKernelGGL(k_cold_fused_t<kFzResults>, grid, dim3(kFzThreads), 0, s, st, sc, el, n, dn, invalid_key,
-                       acquire, prio, ts_off, ts_base, simple, hot_min, out, 0);
+    hipLaunchKernelGGL(k_cold_fused, dim3((n + kFzChunk - 1) / kFzChunk), dim3(kFzThreads), 0, s, st, sc, el, n, dn,
+                       invalid_key, acquire, prio, ts_off, ts_base, simple, hot_min, out, fz_debug());
 }
 
 static size_t hot_rows(size_t cap) { return (cap + kHotSeg - 1) / kHotSeg; }
@@ -3345,7 +2981,6 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up(cap * 4);                     // plist
     b += align_up(cap * 8);                     // deferred (flow, run)
     b += align_up(cap * sizeof(RunOut));        // run_out
-    b += 2 * align_up(cap * sizeof(uint4));     // run_rec, crule
     b += align_up(ntiles * kRunWaves * sizeof(RAgg));
     b += 2 * align_up(ntiles * sizeof(Agg)) + align_up(ntiles * 4);
     b += align_up(CTL_WORDS * 4);
@@ -3395,8 +3030,6 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.plist = (uint32_t *)take(cap * 4);
     sc.deferred = (uint32_t *)take(cap * 8);
     sc.run_out = (RunOut *)take(cap * sizeof(RunOut));
-    sc.run_rec = (uint4 *)take(cap * sizeof(uint4));
-    sc.crule = (uint4 *)take(cap * sizeof(uint4));
     sc.wave_carry = (RAgg *)take(ntiles * kRunWaves * sizeof(RAgg));
     sc.tile_agg = take(ntiles * sizeof(Agg));
     sc.tile_carry = take(ntiles * sizeof(Agg));
@@ -3540,30 +3173,18 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, hs, sc, ngroups);
     hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
     hipLaunchKernelGGL(k_hot_pre, dim3(kHotBuckets), dim3(kThreads), 0, hs, sc);
-    const bool hm = ovl && hot_runs_main();
-    if (hm) {
-        if (!sc.ev_pre) SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_pre, hipEventDisableTiming));
-        SGA_HIP_CHECK(hipEventRecord(sc.ev_pre, hs));
-    }
     const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
                                         kSlotShift, bits, sc.radix, s, true);
     const uint64_t *el = (np & 1) ? sc.el[0] : sc.el[1];
     const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
     // the hot runs and results once the sort is done (the prioritized hot requests are sorted with
     // the cold ones), beside the cold stage
-    if (hm) {  // the hot runs (short, latency-bound) on the batch stream before the cold stage takes the CUs
-        SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_pre, 0));
-        hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el);
-        hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, s, st, sc, ts_base);
-    }
     if (ovl) {
         SGA_HIP_CHECK(hipEventRecord(sc.ev_fork, s));
         SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork, 0));
     }
-    if (!hm) {
-        hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, el);
-        hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, hs, st, sc, ts_base);
-    }
+    hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, el);
+    hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, hs, st, sc, ts_base);
     if (ovl) {
         hipLaunchKernelGGL(k_hot_final, dim3(nseg), dim3(kFinWgThreads), 0, hs, sc, n, out, fin_cache());
         hipLaunchKernelGGL(k_prio_results, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, el, out);

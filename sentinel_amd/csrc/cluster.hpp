@@ -130,7 +130,6 @@ enum : int {
     CTL_BDHI = 24,       // largest hot bucket delta
     CTL_MODE = 25,       // 1: the batch runs the hot path
     CTL_HOTERR = 26,     // hot runs that needed a replay (never expected)
-    CTL_NCRULE = 27,     // cold rules published to BatchScratch::crule (split cold pipeline)
     CTL_WORDS = 64
 };
 enum : uint32_t {
@@ -159,9 +158,6 @@ struct BatchScratch {
     uint32_t *plist;          // sorted positions of prioritized requests (ascending)
     uint32_t *deferred;       // (flow, run) pairs handed from k_flows to k_flows_slow
     RunOut *run_out;
-    uint4 *run_rec;           // split cold pipeline, per run head position: requests, prioritized count,
-                              // first plist index, acquire | bucket delta << 8
-    uint4 *crule;             // split cold pipeline: (slot, first position, end position) per touched rule
     RAgg *wave_carry;         // per 512-request wave slice: scan carry for k_results
     void *tile_agg;
     void *tile_carry;
@@ -205,7 +201,7 @@ struct BatchScratch {
     // hot/cold overlap: after the sort the hot side (ranks, hot runs, hot results) runs on `side`
     // beside the cold stage on the batch's stream (fork and join by events; made on first use)
     hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork0 = nullptr, ev_pre = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork0 = nullptr;
 };
 
 // The hot path's in-order ranks come from LDS atomics whose same-word lanes are served in lane
