@@ -1414,12 +1414,16 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
     const double invh = 1.0 / (double)Wh;
     uint32_t wflags = 0, nc = 0, np = 0, bdmax = 0;
     const uint32_t send = min(n, ubase + (uint32_t)kSubSeg);
+    // the sub's request codes stay in registers through the rank and fix-up passes (written once)
+    uint32_t hc[kSubRounds];
+#pragma unroll
+    for (int r = 0; r < kSubRounds; ++r) hc[r] = kNoCode;
     if (active) {
         uint32_t ptso = ubase > 0 ? ts_off[ubase - 1] : 0u;  // time order across the sub start
         // hot bucket of the previous request (bucket boundaries)
         uint32_t pbd = (nhot && ubase > 0) ? min(bucket_delta(ptso, Wh, r0h, invh), (uint32_t)kHotBuckets - 1) : 0u;
         const bool use_prio = prio != nullptr;
-        const int nchunks = (int)((send - ubase + kH1Chunk * 64 - 1) / (kH1Chunk * 64));
+        constexpr int nchunks = kSubRounds / kH1Chunk;  // a short last sub runs masked rounds
         struct Buf {
             int64_t f[kH1Chunk];
             int32_t a[kH1Chunk];
@@ -1551,7 +1555,7 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                     if (valid && hp && bdh > pbk)  // the first request of buckets pbk + 1 .. bdh
                         for (uint32_t qq = pbk + 1; qq <= bdh; ++qq) sc.hbnd[qq] = i;
                     pbd = lane_u32(bdh, 63);
-                    if (valid) sc.hcode[i] = (kind == 2 ? (kKeyHot | hid | (p << 12)) : 0u) | (bdh << 13);
+                    if (valid) hc[ch * kH1Chunk + u] = (kind == 2 ? (kKeyHot | hid | (p << 12)) : 0u) | (bdh << 13);
                 }
                 // cold elements, compacted in arrival order
                 const bool emit = kind == 1;
@@ -1566,6 +1570,7 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
         load(0, B0);
         lookup(B0);
         load(1, B1);
+#pragma unroll
         for (int ch = 0; ch < nchunks; ch += 3) {
             lookup(B1);
             load(ch + 2, B2);
@@ -1582,20 +1587,16 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
         if (nhot && !(dbg & 4)) {
             // rank pass over the sub's keys (just written: L2; all 16 loads in flight together, the
             // pipeline's registers are free), one round at a time
-            uint32_t key[kSubRounds];
-#pragma unroll
-            for (int r = 0; r < kSubRounds; ++r) key[r] = sc.hcode[min(ubase + (uint32_t)r * 64 + lane, n - 1)];
 #pragma unroll
             for (int r = 0; r < kSubRounds; ++r) {
                 const uint32_t i = ubase + (uint32_t)r * 64 + lane;
-                const uint32_t kv = key[r];
+                const uint32_t kv = hc[r];
                 const bool hot = i < send && (kv & kKeyHot);
                 const uint32_t hid = kv & 0xFFFu, p = (kv >> 12) & 1u, bdh = (kv >> 13) & 63u;
                 uint32_t r_in = 0;
                 if (hot) r_in = rank_hot(reinterpret_cast<uint32_t *>(c), hid);
                 np += (uint32_t)__popcll(__ballot(hot && p));
-                if (hot) sc.hcode[i] = (p << 31) | hid | (r_in << 12) | (bdh << 25);
-                else if (i < send) sc.hcode[i] = kNoCode;
+                hc[r] = hot ? ((p << 31) | hid | (r_in << 12) | (bdh << 25)) : kNoCode;
             }
         }
     }
@@ -1634,18 +1635,15 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
         __syncthreads();
         if (active) {
             // codes: in-wave ranks -> in-segment ranks; prioritized hot requests join the sub's elements
-            uint32_t code[kSubRounds];
 #pragma unroll
-            for (int r = 0; r < kSubRounds; ++r) code[r] = sc.hcode[min(ubase + (uint32_t)r * 64 + lane, n - 1)];
-#pragma unroll
-            for (int r = 0; r < ((dbg & 8) ? 0 : kSubRounds); ++r) {
+            for (int r = 0; r < kSubRounds; ++r) {
                 const uint32_t i = ubase + (uint32_t)r * 64 + lane;
-                const uint32_t cd = code[r];
+                const uint32_t cd = hc[r];
                 const bool hot = i < send && cd != kNoCode;
                 const uint32_t hid = cd & 0xFFFu;
                 const uint32_t r_seg = hot ? ((cd >> 12) & 0x1FFFu) + c[hid] : 0u;
                 const bool pr = hot && (cd >> 31);
-                if (hot && (wave || pr)) sc.hcode[i] = (cd & ~(0x1FFFu << 12)) | (r_seg << 12);
+                if (i < send) sc.hcode[i] = hot ? ((cd & ~(0x1FFFu << 12)) | (r_seg << 12)) : kNoCode;
                 const uint64_t em = __ballot(pr);
                 if (pr) {
                     sc.el_tile[(size_t)ubase + nc + (uint32_t)__popcll(em & lt)] =
