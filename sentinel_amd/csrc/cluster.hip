@@ -2277,6 +2277,10 @@ __global__ __launch_bounds__(kFinThreads) void k_hot_fin(ClusterState st, BatchS
         sc.hot_ctl[8 + threadIdx.x] = 0;
         sc.hot_ctl[64 + threadIdx.x] = 0;
     }
+    if (threadIdx.x < CTL_WORDS) {  // the batch's control words for sga_cluster_batch_info; the next batch starts clear
+        sc.counters_last[threadIdx.x] = sc.counters[threadIdx.x];
+        sc.counters[threadIdx.x] = 0;
+    }
 }
 
 __global__ void k_hot_reset(ClusterState st, BatchScratch sc, uint32_t nslots_cap) {
@@ -2981,7 +2985,7 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up(cap * sizeof(RunOut));        // run_out
     b += align_up(ntiles * kRunWaves * sizeof(RAgg));
     b += 2 * align_up(ntiles * sizeof(Agg)) + align_up(ntiles * 4);
-    b += align_up(CTL_WORDS * 4);
+    b += 2 * align_up(CTL_WORDS * 4);  // counters, counters_last
     b += 2 * align_up(hist * 4) + align_up(scan_partials_needed(hist) * 4 + 64);
     b += align_up(scan_partials_needed(cap) * 4 + 64);
     b += align_up(kRadixGhistWords * 4) + align_up(64);  // look-back digit totals, error flag
@@ -3033,6 +3037,8 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.tile_carry = take(ntiles * sizeof(Agg));
     sc.tile_valid = (uint32_t *)take(ntiles * 4);
     sc.counters = (uint32_t *)take(CTL_WORDS * 4);
+    sc.counters_last = (uint32_t *)take(CTL_WORDS * 4);
+    sc.counters_clean = 0;
     sc.radix.hist = (uint32_t *)take(hist * 4);
     sc.radix.hist_scan = (uint32_t *)take(hist * 4);
     sc.radix.partial = (uint32_t *)take(scan_partials_needed(hist) * 4 + 64);
@@ -3133,13 +3139,13 @@ void hot_reset(const ClusterState &st, BatchScratch &sc, uint32_t nslots_cap, hi
 // Every kernel reads the batch's path from the control words, so no host synchronisation.
 static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id,
                              const int32_t *acquire, const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off,
-                             uint32_t n, uint64_t *out, hipStream_t s) {
+                             uint32_t n, uint64_t *out, hipStream_t s, bool clean) {
     const uint32_t invalid_key = st.nslots;
     int bits = 1;
     while (((uint64_t)1 << bits) < (uint64_t)st.nslots + kHot + 2) ++bits;  // hot keys nslots + 1 + id
     const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
     const uint32_t ngroups = (nseg + kHotGroupRows - 1) / kHotGroupRows;
-    SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, CTL_WORDS * 4, s));
+    if (!clean) SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, CTL_WORDS * 4, s));
     hipLaunchKernelGGL(k_hot_precheck, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc, ts_off, ts_base, n);
     auto hka = st.dense_n ? k_hot_key_dense<0> : k_hot_key_hash<0>;
     auto hkb = st.dense_n ? k_hot_key_dense<1> : k_hot_key_hash<1>;
@@ -3211,12 +3217,15 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(k_hot_clear, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc);
     hipLaunchKernelGGL(k_hot_pick, dim3(sb), dim3(kThreads), 0, s, st, sc, sc.hot_min);
     hipLaunchKernelGGL(k_hot_fin, dim3(1), dim3(kFinThreads), 0, s, st, sc);
+    sc.counters_clean = 1;
 }
 
 void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
                           const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, int simple,
                           void *out_v, hipStream_t s, const LimiterPass *lims, int nlims) {
     if (n == 0) return;
+    const bool clean = sc.counters_clean != 0;
+    sc.counters_clean = 0;
     uint64_t *out = (uint64_t *)out_v;
     int bits = 1;
     while (((uint64_t)1 << bits) < (uint64_t)st.nslots + 1) ++bits;
@@ -3242,7 +3251,7 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     }
     if (sc.hot_enabled && sc.hot_lane_order && !simple && !limited && !lb &&
         st.nslots + (uint64_t)kHot + 2 < kMaxSlots) {
-        decide_batch_hot(st, sc, flow_id, acquire, prio, ts_base, ts_off, n, out, s);
+        decide_batch_hot(st, sc, flow_id, acquire, prio, ts_base, ts_off, n, out, s, clean);
         return;
     }
     SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, CTL_WORDS * 4, s));
@@ -3275,7 +3284,10 @@ void cparam_stage1(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
                    const int32_t *acquire, const uint32_t *voff, const int64_t *values, int64_t ts_base,
                    const uint32_t *ts_off, uint32_t n, void *out_v, hipStream_t s, const LimiterPass *lims,
                    int nlims) {
+    sc.counters_clean = 0;  // the stages use the control words
     if (n == 0) return;
+    const bool clean = sc.counters_clean != 0;
+    sc.counters_clean = 0;
     uint64_t *out = (uint64_t *)out_v;
     const uint32_t invalid_key = st.nslots;
     const uint32_t nb = (n + kThreads - 1) / kThreads;
@@ -3292,7 +3304,10 @@ void cparam_stage1(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
 void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, const int32_t *acquire,
                    const uint32_t *voff, const int64_t *values, int64_t ts_base, const uint32_t *ts_off, uint32_t n,
                    uint32_t nslow, void *out_v, hipStream_t s) {
+    sc.counters_clean = 0;  // the stages use the control words
     if (n == 0) return;
+    const bool clean = sc.counters_clean != 0;
+    sc.counters_clean = 0;
     uint64_t *out = (uint64_t *)out_v;
     const uint32_t ntiles = (n + kTileElems - 1) / kTileElems;
     const uint32_t fb = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 16384));

@@ -163,6 +163,9 @@ struct BatchScratch {
     void *tile_carry;
     uint32_t *tile_valid;
     uint32_t *counters;       // CTL_* words
+    uint32_t *counters_last;  // the last hot-path batch's CTL_* words (k_hot_fin saves them, then clears
+                              // the live ones for the next batch: no clearing launch per batch)
+    int counters_clean = 0;   // host: the live words are zero once the queued work has run
     uint32_t *lim_partial;    // scan partials over max_batch elements (namespace limiter pre-pass)
     RadixScratch radix;
     size_t cap = 0;

@@ -1313,7 +1313,9 @@ int sga_cluster_batch_info(sga_engine *e, uint32_t *out, size_t n) {
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
         uint32_t c[sga::CTL_WORDS];
         uint32_t hc[8];
-        SGA_HIP_CHECK(hipMemcpyAsync(c, g.scratch.counters, sizeof(c), hipMemcpyDeviceToHost, g.stream));
+        // a hot-path batch leaves its words in counters_last (k_hot_fin clears the live ones)
+        const uint32_t *src = g.scratch.counters_clean ? g.scratch.counters_last : g.scratch.counters;
+        SGA_HIP_CHECK(hipMemcpyAsync(c, src, sizeof(c), hipMemcpyDeviceToHost, g.stream));
         SGA_HIP_CHECK(hipMemcpyAsync(hc, g.scratch.hot_ctl, sizeof(hc), hipMemcpyDeviceToHost, g.stream));
         SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
         const uint32_t v[11] = {c[sga::CTL_MODE],  c[sga::CTL_FLAGS], c[sga::CTL_NSORT], c[sga::CTL_NCOLD],
