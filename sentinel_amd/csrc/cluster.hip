@@ -1061,7 +1061,12 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
                 return lo;
             };
             RunOut ro;
-            if (run_fast(st, P, R, thr, qbase, ri, prio_before, ro)) {
+            // sampleCount <= 10 (the default, every C3 rule) issues exactly ten pair loads: the
+            // 16-pair form re-reads the last pair six times, and the flows phase is bound by the
+            // number of load requests in flight
+            const bool fast = P.S <= 10 ? run_fast<decltype(prio_before), 10>(st, P, R, thr, qbase, ri, prio_before, ro)
+                                        : run_fast(st, P, R, thr, qbase, ri, prio_before, ro);
+            if (fast) {
                 sc.run_out[r] = ro;
                 r += ri.n;
                 continue;
@@ -3150,7 +3155,9 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     auto hka = st.dense_n ? k_hot_key_dense<0> : k_hot_key_hash<0>;
     auto hkb = st.dense_n ? k_hot_key_dense<1> : k_hot_key_hash<1>;
     // the key kernels count the sort's first digit per tile as they write the elements
-    const int d0 = radix64_digit_bits(bits);
+    // (their LDS counts hold 8-bit digits; a wider first digit is counted by the sort itself)
+    const int dsort = radix64_digit_bits(bits);
+    const int d0 = dsort <= 8 ? dsort : 0;
     const uint32_t ntiles_sort = (uint32_t)radix64_tiles(n);
     hipLaunchKernelGGL(hka, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out,
                        fz_debug(), d0, sc.radix.hist, ntiles_sort);
@@ -3178,7 +3185,7 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
     hipLaunchKernelGGL(k_hot_pre, dim3(kHotBuckets), dim3(kThreads), 0, hs, sc);
     const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
-                                        kSlotShift, bits, sc.radix, s, true);
+                                        kSlotShift, bits, sc.radix, s, d0 > 0);
     const uint64_t *el = (np & 1) ? sc.el[0] : sc.el[1];
     const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
     // the hot runs and results once the sort is done (the prioritized hot requests are sorted with
@@ -3236,6 +3243,8 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     static_assert(kTileElems == kRadix64Tile, "classify tiles are sort tiles");
     const bool lb = radix64_lookback() != 0;
     const int npass = (bits + d0 - 1) / d0;
+    if (lb && (npass << d0) > 1024)  // k_classify counts every pass's digits in 1024 LDS words
+        throw HipError("look-back sort (SGA_RADIX_MODE=0) needs npass << digit bits <= 1024", __FILE__, __LINE__);
     static const int chunk = getenv("SGA_CLS_CHUNK") ? atoi(getenv("SGA_CLS_CHUNK")) : 2;  // A/B knob
     auto cls = chunk >= 16 ? k_classify<16>
                            : (chunk >= 8 ? k_classify<8> : (chunk >= 4 ? k_classify<4> : (chunk >= 2 ? k_classify<2> : k_classify<1>)));
@@ -3286,8 +3295,6 @@ void cparam_stage1(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
                    int nlims) {
     sc.counters_clean = 0;  // the stages use the control words
     if (n == 0) return;
-    const bool clean = sc.counters_clean != 0;
-    sc.counters_clean = 0;
     uint64_t *out = (uint64_t *)out_v;
     const uint32_t invalid_key = st.nslots;
     const uint32_t nb = (n + kThreads - 1) / kThreads;
@@ -3306,8 +3313,6 @@ void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
                    uint32_t nslow, void *out_v, hipStream_t s) {
     sc.counters_clean = 0;  // the stages use the control words
     if (n == 0) return;
-    const bool clean = sc.counters_clean != 0;
-    sc.counters_clean = 0;
     uint64_t *out = (uint64_t *)out_v;
     const uint32_t ntiles = (n + kTileElems - 1) / kTileElems;
     const uint32_t fb = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 16384));
