@@ -522,6 +522,7 @@ __global__ __launch_bounds__(kThreads) void k_rs64_hist(const uint64_t *__restri
     uint32_t wn;  // elements of this wave's segment
     if (tile_n) wn = tile_n[tile * kWaves + (threadIdx.x >> 6)];
     else wn = n > wbase ? min((uint32_t)(kRounds * 64), n - wbase) : 0u;
+    wn = __builtin_amdgcn_readfirstlane(wn);
     uint64_t key[kRounds];
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
@@ -530,6 +531,7 @@ __global__ __launch_bounds__(kThreads) void k_rs64_hist(const uint64_t *__restri
     }
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
+        if ((uint32_t)(r * 64) >= wn) continue;  // wave-uniform: past the segment's elements
         const bool valid = (uint32_t)(r * 64 + lane) < wn;
         const uint32_t d = (uint32_t)(key[r] >> shift) & (RADIX - 1);
         uint64_t peers = __ballot(valid);
@@ -644,6 +646,9 @@ __global__ __launch_bounds__(kThreads) void k_rs64_sweep(const uint64_t *__restr
         wn = tn > wloc ? tn - wloc : 0u;
     }
     const uint32_t wbase = tbase + wloc;
+    // rounds past the wave's last element are skipped whole (wave-uniform): a segmented producer's
+    // segments are often a quarter full
+    wn = __builtin_amdgcn_readfirstlane(wn);
     uint64_t key[kRounds];
     uint32_t pos[kRounds];
 #pragma unroll
@@ -653,6 +658,8 @@ __global__ __launch_bounds__(kThreads) void k_rs64_sweep(const uint64_t *__restr
     }
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
+        pos[r] = 0;
+        if ((uint32_t)(r * 64) >= wn) continue;
         const bool valid = (uint32_t)(r * 64 + lane) < wn;
         const uint32_t d = (uint32_t)(key[r] >> shift) & (RADIX - 1);
         uint64_t peers = __ballot(valid);
