@@ -2955,13 +2955,19 @@ static int hot_overlap() {  // A/B knob: SGA_HOT_OVERLAP=0 runs the hot side aft
     return v;
 }
 
+static int tail_early() {  // A/B knob: SGA_HOT_TAIL_EARLY=0 starts the next hot set after the hot results
+    static const int v = getenv("SGA_HOT_TAIL_EARLY") ? atoi(getenv("SGA_HOT_TAIL_EARLY")) : 1;
+    return v;
+}
+
 void batch_scratch_release(BatchScratch &sc) {
     if (sc.side) (void)hipStreamDestroy(sc.side);
     if (sc.ev_fork) (void)hipEventDestroy(sc.ev_fork);
     if (sc.ev_join) (void)hipEventDestroy(sc.ev_join);
     if (sc.ev_fork0) (void)hipEventDestroy(sc.ev_fork0);
+    if (sc.ev_mid) (void)hipEventDestroy(sc.ev_mid);
     sc.side = nullptr;
-    sc.ev_fork = sc.ev_join = sc.ev_fork0 = nullptr;
+    sc.ev_fork = sc.ev_join = sc.ev_fork0 = sc.ev_mid = nullptr;
 }
 
 
@@ -3175,6 +3181,7 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
             SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork0, hipEventDisableTiming));
             SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork, hipEventDisableTiming));
             SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_join, hipEventDisableTiming));
+            SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_mid, hipEventDisableTiming));
         }
         SGA_HIP_CHECK(hipEventRecord(sc.ev_fork0, s));
         SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork0, 0));
@@ -3197,6 +3204,7 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, el);
     hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, hs, st, sc, ts_base);
     if (ovl) {
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_mid, hs));  // the hot runs read hot_slot; the next hot set may start
         hipLaunchKernelGGL(k_hot_final, dim3(nseg), dim3(kFinWgThreads), 0, hs, sc, n, out, fin_cache());
         hipLaunchKernelGGL(k_prio_results, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, el, out);
         SGA_HIP_CHECK(hipEventRecord(sc.ev_join, hs));
@@ -3213,16 +3221,22 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
             fprintf(stderr, "fz phases (wall_clock64 ticks per workgroup, %llu wgs): runs %.0f flows %.0f results %.0f\n",
                     ph[7], (double)ph[0] / ph[7], (double)ph[1] / ph[7], (double)ph[2] / ph[7]);
     }
-    if (ovl) {
-        SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_join, 0));
-    } else {
+    if (!ovl) {
         hipLaunchKernelGGL(k_hot_final, dim3(nseg), dim3(kFinWgThreads), 0, s, sc, n, out, fin_cache());
         hipLaunchKernelGGL(k_prio_results, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el, out);
+    } else if (!tail_early()) {
+        SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_join, 0));
+    } else {
+        // the next hot set needs the cold candidates (this stream) and the hot runs done (they read
+        // hot_slot); it writes hot_of / hot_next / the dense hot ids, which the hot results do not
+        // read, so it runs beside k_hot_final.  k_hot_fin (renames, control words) waits for both.
+        SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_mid, 0));
     }
     const uint32_t sb = 64;  // few workgroups: their bins meet in global atomics
     hipLaunchKernelGGL(k_hot_hist, dim3(sb), dim3(kThreads), 0, s, st, sc, std::max<uint32_t>(sc.hot_min, 1));
     hipLaunchKernelGGL(k_hot_clear, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc);
     hipLaunchKernelGGL(k_hot_pick, dim3(sb), dim3(kThreads), 0, s, st, sc, sc.hot_min);
+    if (ovl && tail_early()) SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_join, 0));
     hipLaunchKernelGGL(k_hot_fin, dim3(1), dim3(kFinThreads), 0, s, st, sc);
     sc.counters_clean = 1;
 }

@@ -204,7 +204,7 @@ struct BatchScratch {
     // hot/cold overlap: after the sort the hot side (ranks, hot runs, hot results) runs on `side`
     // beside the cold stage on the batch's stream (fork and join by events; made on first use)
     hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork0 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork0 = nullptr, ev_mid = nullptr;
 };
 
 // The hot path's in-order ranks come from LDS atomics whose same-word lanes are served in lane
