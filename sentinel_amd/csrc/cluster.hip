@@ -1261,7 +1261,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small_sort(ClusterState st, c
 //   k_hot_final     each hot request's TokenResult from its rank, in input order (coalesced).
 // Prioritized hot requests are sorted as key nslots + 1 + hot id, after every cold element, so
 // each rule's prioritized ranks form one ascending list (the occupy decisions need the number of
-// prioritized requests before a position); k_prio_results answers them.
+// prioritized requests before a position); k_hot_final's first workgroups answer them.
 // Preconditions, checked on the device before any rule state is touched (else the batch
 // re-classifies every request as cold and takes the sort path): timestamps non-decreasing over the
 // batch (then bucket order is arrival order for every rule), hot requests with acquireCount 1, at
@@ -1986,6 +1986,37 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
     }
 }
 
+// TokenResults of the prioritized hot requests (the sorted elements past the cold ones): the
+// first workgroups of k_hot_final (no launch of its own on the hot side's critical path).
+__device__ __forceinline__ void prio_results_range(const ClusterState &st, const BatchScratch &sc,
+                                                   const uint64_t *__restrict__ el, uint64_t *__restrict__ out,
+                                                   uint32_t j0, uint32_t stride) {
+    const uint32_t np = sc.counters[CTL_NPRIO], base = sc.counters[CTL_NCOLD];
+    const uint32_t bd_lo = sc.counters[CTL_BDLO];
+    const uint32_t bd_hi = min(sc.counters[CTL_BDHI], (uint32_t)kHotBuckets - 1);
+    for (uint32_t j = j0; j < np; j += stride) {
+        const uint64_t e = el[base + j];
+        const uint32_t h = el_slot(e) - (st.nslots + 1);
+        const uint32_t rank = sc.prank[j];
+        uint32_t b = bd_lo;
+        for (; b < bd_hi; ++b)
+            if (rank - hrun_at(sc, h, b)->start < hrun_at(sc, h, b)->n) break;
+        const HotRun hr = *hrun_at(sc, h, b);
+        const uint32_t local = rank - hr.start;
+        uint64_t res;
+        if (local < hr.f) {
+            const int64_t sum = hr.s0 + (int64_t)local;
+            res = pack_result(TRS_OK, j_d2i(hr.thr - (double)sum / hr.isec - 1.0), 0);
+        } else if (j - hr.p0 - hr.cpf < hr.cw) {
+            res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)hr.wait);
+        } else {
+            res = pack_result(TRS_BLOCKED, 0, 0);
+        }
+        out[el_idx(e)] = res;
+    }
+}
+
+
 // TokenResults of the non-prioritized hot requests, in input order: one 16-wave workgroup per rank
 // segment (its base row in LDS), kFinChunk rounds per wave.  The runs of the kFinCache hottest ids
 // (k_hot_pick numbers them first) in the segment's first two buckets are staged in LDS; a lane whose
@@ -2005,16 +2036,23 @@ __device__ __forceinline__ int64_t i64_of(uint32_t lo, uint32_t hi) {
 __device__ __forceinline__ double f64_of(uint32_t lo, uint32_t hi) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
-__global__ __launch_bounds__(kFinWgThreads) void k_hot_final(BatchScratch sc, uint32_t n, uint64_t *__restrict__ out,
-                                                             uint32_t cache_cap) {
+// The first kFinPrioWgs workgroups answer the prioritized hot requests, the rest one segment each.
+constexpr uint32_t kFinPrioWgs = 32;
+__global__ __launch_bounds__(kFinWgThreads) void k_hot_final(ClusterState st, BatchScratch sc, uint32_t n,
+                                                             const uint64_t *__restrict__ el,
+                                                             uint64_t *__restrict__ out, uint32_t cache_cap) {
     __shared__ uint32_t base[kHot];
     __shared__ double2 c_ti[kFinCache];      // thr, isec
     __shared__ int64_t c_s0[2][kFinCache];   // s0 of the runs in buckets b0, b0 + 1
     __shared__ uint2 c_fs[2][kFinCache];     // (f, start) of those runs
     __shared__ uint32_t s_b0;
     if (!sc.counters[CTL_MODE]) return;
+    if (blockIdx.x < kFinPrioWgs) {  // dispatched first, so they overlap the segments
+        prio_results_range(st, sc, el, out, blockIdx.x * kFinWgThreads + threadIdx.x, kFinPrioWgs * kFinWgThreads);
+        return;
+    }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t seg = blockIdx.x;
+    const uint32_t seg = blockIdx.x - kFinPrioWgs;
     const uint32_t sbase = seg * kHotSeg;
     const uint32_t nhot = hot_count(sc);
     const uint32_t wbase = sbase + (uint32_t)wave * kFinSpan;
@@ -2050,7 +2088,7 @@ __global__ __launch_bounds__(kFinWgThreads) void k_hot_final(BatchScratch sc, ui
 #pragma unroll
     for (int u = 0; u < kFinChunk; ++u) {
         const uint32_t i = wbase + u * 64 + lane;
-        code[u] = (i < wend && !(cn[u] >> 31)) ? cn[u] : kNoCode;  // prioritized: k_prio_results
+        code[u] = (i < wend && !(cn[u] >> 31)) ? cn[u] : kNoCode;  // prioritized: prio_results_range
         const uint32_t cd = code[u];
         hit[u] = cd == kNoCode || ((cd & 0xFFFu) < cache_cap && (cd >> 25) - b0 < 2u);
         const uint4 *hp = reinterpret_cast<const uint4 *>(hit[u] ? sc.hrun : hrun_at(sc, cd & 0xFFFu, cd >> 25));
@@ -2089,36 +2127,6 @@ __global__ __launch_bounds__(kFinWgThreads) void k_hot_final(BatchScratch sc, ui
             res = pack_result(TRS_BLOCKED, 0, 0);
         }
         out[wbase + u * 64 + lane] = res;
-    }
-}
-
-// TokenResults of the prioritized hot requests.
-__global__ __launch_bounds__(kThreads) void k_prio_results(ClusterState st, BatchScratch sc,
-                                                           const uint64_t *__restrict__ el,
-                                                           uint64_t *__restrict__ out) {
-    if (!sc.counters[CTL_MODE]) return;
-    const uint32_t np = sc.counters[CTL_NPRIO], base = sc.counters[CTL_NCOLD];
-    const uint32_t bd_lo = sc.counters[CTL_BDLO];
-    const uint32_t bd_hi = min(sc.counters[CTL_BDHI], (uint32_t)kHotBuckets - 1);
-    for (uint32_t j = blockIdx.x * kThreads + threadIdx.x; j < np; j += gridDim.x * kThreads) {
-        const uint64_t e = el[base + j];
-        const uint32_t h = el_slot(e) - (st.nslots + 1);
-        const uint32_t rank = sc.prank[j];
-        uint32_t b = bd_lo;
-        for (; b < bd_hi; ++b)
-            if (rank - hrun_at(sc, h, b)->start < hrun_at(sc, h, b)->n) break;
-        const HotRun hr = *hrun_at(sc, h, b);
-        const uint32_t local = rank - hr.start;
-        uint64_t res;
-        if (local < hr.f) {
-            const int64_t sum = hr.s0 + (int64_t)local;
-            res = pack_result(TRS_OK, j_d2i(hr.thr - (double)sum / hr.isec - 1.0), 0);
-        } else if (j - hr.p0 - hr.cpf < hr.cw) {
-            res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)hr.wait);
-        } else {
-            res = pack_result(TRS_BLOCKED, 0, 0);
-        }
-        out[el_idx(e)] = res;
     }
 }
 
@@ -3205,8 +3213,8 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, hs, st, sc, ts_base);
     if (ovl) {
         SGA_HIP_CHECK(hipEventRecord(sc.ev_mid, hs));  // the hot runs read hot_slot; the next hot set may start
-        hipLaunchKernelGGL(k_hot_final, dim3(nseg), dim3(kFinWgThreads), 0, hs, sc, n, out, fin_cache());
-        hipLaunchKernelGGL(k_prio_results, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, el, out);
+        hipLaunchKernelGGL(k_hot_final, dim3(nseg + kFinPrioWgs), dim3(kFinWgThreads), 0, hs, st, sc, n, el, out,
+                           fin_cache());
         SGA_HIP_CHECK(hipEventRecord(sc.ev_join, hs));
     }
     cold_stage(st, sc, el, n, sc.counters + CTL_NCOLD, invalid_key, acquire, prio, ts_off, ts_base, 0,
@@ -3222,8 +3230,8 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
                     ph[7], (double)ph[0] / ph[7], (double)ph[1] / ph[7], (double)ph[2] / ph[7]);
     }
     if (!ovl) {
-        hipLaunchKernelGGL(k_hot_final, dim3(nseg), dim3(kFinWgThreads), 0, s, sc, n, out, fin_cache());
-        hipLaunchKernelGGL(k_prio_results, dim3(pgrid), dim3(kThreads), 0, s, st, sc, el, out);
+        hipLaunchKernelGGL(k_hot_final, dim3(nseg + kFinPrioWgs), dim3(kFinWgThreads), 0, s, st, sc, n, el, out,
+                           fin_cache());
     } else if (!tail_early()) {
         SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_join, 0));
     } else {
