@@ -1842,20 +1842,27 @@ __device__ __forceinline__ HotRun *hrun_at(const BatchScratch &sc, uint32_t h, u
 }
 
 __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchScratch sc, int64_t ts_base) {
-    if (!sc.counters[CTL_MODE]) return;
+    // Beside the cold stage every dependent load waits the loaded latency, so the loads that do not
+    // depend on each other are issued together, before any early exit, at clamped (valid) indices.
     const int lane = threadIdx.x & 63;
-    const uint32_t h = blockIdx.x * kH1Waves + (threadIdx.x >> 6);
-    if (h >= hot_count(sc)) return;
+    const uint32_t h = blockIdx.x * kH1Waves + (threadIdx.x >> 6);  // < kHot
+    const uint32_t mode = sc.counters[CTL_MODE], nhot = hot_count(sc);
     const uint32_t bd_lo = sc.counters[CTL_BDLO];
     const uint32_t bd_hi = min(sc.counters[CTL_BDHI], (uint32_t)kHotBuckets - 1);
-    const uint32_t nb = bd_hi >= bd_lo ? bd_hi - bd_lo + 1 : 0;
     const uint32_t tot = sc.hot_tot[h];
-    uint32_t stb = 0;
-    if ((uint32_t)lane < nb && lane > 0) {
-        const uint32_t P = sc.hbnd[bd_lo + lane];  // the bucket's first request
-        stb = sc.hbase[(size_t)(P / kHotSeg) * kHot + h] +
-              ((P % kHotSeg) ? sc.hpre[(size_t)(bd_lo + lane) * kHot + h] : 0u);
-    }
+    const uint32_t s_raw = sc.hot_slot[h];
+    const uint32_t plo = sc.plo[h], phi = max(sc.phi[h], plo);
+    const uint32_t s = s_raw < st.nslots ? s_raw : 0u;  // ids past the hot count hold stale slots
+    const SlotParam P = st.param[s];
+    if (!mode || h >= nhot) return;
+    const uint32_t nb = bd_hi >= bd_lo ? bd_hi - bd_lo + 1 : 0;
+    const bool bl = (uint32_t)lane < nb && lane > 0;
+    const uint32_t bq = min(bd_lo + (uint32_t)lane, (uint32_t)kHotBuckets - 1);
+    const uint32_t Pq = sc.hbnd[bq];  // the bucket's first request
+    const uint32_t Pc = bl ? Pq : 0u;
+    const uint32_t hb = sc.hbase[(size_t)(Pc / kHotSeg) * kHot + h];
+    const uint32_t hp = sc.hpre[(size_t)bq * kHot + h];
+    const uint32_t stb = bl ? hb + ((Pc % kHotSeg) ? hp : 0u) : 0u;
     uint32_t stn = wave_shl1(stb, 0u);
     if ((uint32_t)lane + 1 == nb) stn = tot;
     const uint32_t nrun = (uint32_t)lane < nb ? stn - stb : 0u;
@@ -1867,23 +1874,19 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
     }
     uint64_t rm = __ballot(nrun > 0);
     if (!rm) return;
-    const uint32_t s = sc.hot_slot[h];
-    const SlotParam P = st.param[s];
     const Rec R = rec_of(st, P);
     const double thr = P.thr;
     if (lane == 0) sc.hthr[h] = make_double2(thr, P.isec);
     const int64_t qbase = div_pos(ts_base, P.W);
-    const uint32_t plo = sc.plo[h], phi = max(sc.phi[h], plo);
     const uint32_t *pr = sc.prank;
+    const int jl = min(lane, P.S - 1);   // bucket lane (clamped: the loads stay unconditional)
+    const int kl = min(lane, CEV_N - 1);  // counter lane
     while (rm) {
         const int lb = __builtin_ctzll(rm);
         rm &= rm - 1;
         const uint32_t j0 = lane_u32(stb, lb);
         const uint32_t n = lane_u32(nrun, lb);
         const uint32_t b = bd_lo + (uint32_t)lb;
-        const uint32_t p0 = plo < phi ? wave_lower_bound(pr, plo, phi, j0, lane) : plo;
-        const uint32_t p1 = plo < phi ? wave_lower_bound(pr, p0, phi, j0 + n, lane) : plo;
-        const uint32_t cp_tot = p1 - p0;
         // window of the run's bucket (cluster rules: interval = S x W, so validity is the same for
         // any time in the bucket and the bucket start stands in for the request times)
         const int64_t q = qbase + (int64_t)b;
@@ -1892,11 +1895,13 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
         const int64_t qs = div_pos(q, P.S);
         const int cj = (int)(q - qs * P.S);
         const int jh = cj + 1 == P.S ? 0 : cj + 1;
-        int64_t w = kAbsent, pv = 0;
-        if (lane < P.S) {
-            w = R.start(lane);
-            pv = R.cnt(CEV_PASS, lane);
-        }
+        const int64_t w_ld = R.start(jl), pv_ld = R.cnt(CEV_PASS, jl);
+        const int64_t cl_ld = R.cnt(kl, cj);
+        const SlotOcc o_ld = R.occ();
+        const uint32_t p0 = plo < phi ? wave_lower_bound(pr, plo, phi, j0, lane) : plo;
+        const uint32_t p1 = plo < phi ? wave_lower_bound(pr, p0, phi, j0 + n, lane) : plo;
+        const uint32_t cp_tot = p1 - p0;
+        const int64_t w = lane < P.S ? w_ld : kAbsent, pv = lane < P.S ? pv_ld : 0;
         const bool valid_b = lane < P.S && lane != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval);
         const int64_t bp = wave_sum_i64(valid_b ? pv : 0);
         const int64_t old = lane_i64(w, cj);
@@ -1906,9 +1911,9 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
         int64_t cl = 0;  // lane k < CEV_N: counter k of the current bucket after the rotation
         SlotOcc o{0, 0, 0, 0};
         bool occ_dirty = false;
-        if (!rot && lane < CEV_N) cl = R.cnt(lane, cj);
+        if (!rot && lane < CEV_N) cl = cl_ld;
         if (rot && old != kAbsent) {  // resetWindowTo + transferOccupyToBucket
-            o = R.occ();
+            o = o_ld;
             if (o.has_occ) {
                 if (lane == CEV_OCCUPIED_PASS || lane == CEV_PASS) cl += o.occ_pass;
                 if (lane == CEV_PASS_REQUEST) cl += o.occ_preq;
@@ -1929,7 +1934,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
         if (np_after > 0) {
             const int64_t wt = (lane < P.S && valid_b) ? R.cnt(CEV_WAITING, lane) : 0;
             const int64_t w0 = lane_i64(cl, CEV_WAITING) + wave_sum_i64(wt);
-            if (!(rot && old != kAbsent)) o = R.occ();  // not loaded by the rotation above
+            if (!(rot && old != kAbsent)) o = o_ld;  // not taken by the rotation above
             const double latest = (double)(s0 + (int64_t)f) / P.isec;
             const double lim = st.max_occupy_ratio * thr;
             const int64_t occ0 = o.occ_pass;
