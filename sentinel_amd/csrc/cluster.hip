@@ -3190,7 +3190,14 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipStream_t hs = s;
     if (ovl) {
         if (!sc.side) {
-            SGA_HIP_CHECK(hipStreamCreateWithFlags(&sc.side, hipStreamNonBlocking));
+            static const int side_prio = getenv("SGA_SIDE_PRIO") ? atoi(getenv("SGA_SIDE_PRIO")) : 0;  // A/B knob
+            if (side_prio) {
+                int lo = 0, hi = 0;  // hi: the greatest priority (numerically lowest)
+                SGA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+                SGA_HIP_CHECK(hipStreamCreateWithPriority(&sc.side, hipStreamNonBlocking, side_prio > 0 ? hi : lo));
+            } else {
+                SGA_HIP_CHECK(hipStreamCreateWithFlags(&sc.side, hipStreamNonBlocking));
+            }
             SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork0, hipEventDisableTiming));
             SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork, hipEventDisableTiming));
             SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_join, hipEventDisableTiming));
