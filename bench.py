@@ -183,6 +183,7 @@ def main():
     hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
     hip.hipEventSynchronize.argtypes = [C.c_void_p]
     hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
+    hip.hipStreamWaitEvent.argtypes = [C.c_void_p, C.c_void_p, C.c_uint]
 
     def new_event():
         ev = C.c_void_p()
@@ -216,8 +217,14 @@ def main():
     gcount = torch.empty(world * 2, dtype=torch.int32, device=gdev) if world > 1 else None
     mev = []
 
+    ev_q = new_event()
+
     def metric_snapshot(now):
         e0, e1 = new_event(), new_event()
+        # the snapshot's time starts once the engine stream's queued batches are done (the call
+        # orders itself after them; e0 would otherwise time that wait as well)
+        hip.hipEventRecord(ev_q, estream)
+        hip.hipStreamWaitEvent(C.c_void_p(side.cuda_stream), ev_q, 0)
         hip.hipEventRecord(e0, C.c_void_p(side.cuda_stream))
         _lib.check(L.sga_cluster_metric_nodes_device(eng.handle, now, rows.data_ptr(), cap_rows, cnt_rows.data_ptr(),
                                                      C.c_void_p(side.cuda_stream)), eng.handle, "clusterMetricNodes")

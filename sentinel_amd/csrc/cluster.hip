@@ -2332,8 +2332,34 @@ __global__ __launch_bounds__(kThreads) void k_cluster_nodes(ClusterState st, con
     if (act) {
         const SlotParam P = st.param[s];
         m.flow_id = slot_fid[s];
-        m.block_qps = get_avg(st, P, s, now, CEV_BLOCK);
-        m.pass_qps = get_avg(st, P, s, now, CEV_PASS);
+        // getAvg(BLOCK) rotates the current window; getAvg(PASS)'s rotation at the same time is then
+        // a no-op, so one rotation and one pass over the buckets give both sums
+        cur_window(st, P, s, now);
+        const Rec R = rec_of(st, P);
+        int64_t sb = 0, sp = 0;
+        if (P.S <= 10) {  // unconditional loads (clamped index), issued together
+            int4 pr[10];
+            int64_t bl[10];
+#pragma unroll
+            for (int j = 0; j < 10; ++j) {
+                const int jj = min(j, P.S - 1);
+                pr[j] = reinterpret_cast<const int4 *>(R.r)[jj];
+                bl[j] = R.cnt(CEV_BLOCK, jj);
+            }
+#pragma unroll
+            for (int j = 0; j < 10; ++j) {
+                const int64_t w = i64_lo(pr[j]);
+                if (j < P.S && w != kAbsent && !(now - w > (int64_t)P.interval)) {
+                    sp += i64_hi(pr[j]);
+                    sb += bl[j];
+                }
+            }
+        } else {
+            sb = values_sum(st, P, now, CEV_BLOCK);
+            sp = values_sum(st, P, now, CEV_PASS);
+        }
+        m.block_qps = (double)sb / P.isec;
+        m.pass_qps = (double)sp / P.isec;
         m.timestamp = now;
     }
     // one reservation per workgroup (a same-address atomic per node would serialize the kernel)
