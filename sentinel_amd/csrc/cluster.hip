@@ -543,13 +543,10 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
     // (WAITING, BLOCK, PASS_REQUEST, BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK), the occupy
     // state (in the lines of the pairs), and below the (start, PASS) pairs of every bucket.
     const int4 *v = reinterpret_cast<const int4 *>(R.r);
-    const int4 cur = v[cj];
     const int4 *cv = reinterpret_cast<const int4 *>(R.r + 2 * P.S + kOccWords + 6 * cj);
     const int4 c01 = cv[0], c23 = cv[1], c45 = cv[2];
     const SlotOcc occ_ld = R.occ();
-    const int64_t old = i64_lo(cur);
-    if (a <= 0 || (old != kAbsent && ws < old)) return false;
-    if (ri.cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) return false;
+    int4 cur;  // the current bucket's pair: taken from the pair loads below (no load of its own)
     int64_t bp = 0, hstart = kAbsent, hpass = 0;
     {
         // (start, PASS) pairs: one 16-byte load per bucket.  Up to 16 buckets (sampleCount 10 is
@@ -569,13 +566,21 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
             int4 sp[kMaxPairs];
 #pragma unroll
             for (int jj = 0; jj < kMaxPairs; ++jj) sp[jj] = v[min(jj, P.S - 1)];
+            cur = sp[0];
+#pragma unroll
+            for (int jj = 1; jj < kMaxPairs; ++jj)
+                if (jj == cj) cur = sp[jj];
 #pragma unroll
             for (int jj = 0; jj < kMaxPairs; ++jj)
                 if (jj < P.S) take(jj, sp[jj]);
         } else {
+            cur = v[cj];
             for (int jj = 0; jj < P.S; ++jj) take(jj, v[jj]);
         }
     }
+    const int64_t old = i64_lo(cur);
+    if (a <= 0 || (old != kAbsent && ws < old)) return false;
+    if (ri.cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) return false;
     const bool rot = old == kAbsent || ws > old;
     int64_t c[CEV_N];
     SlotOcc o{0, 0, 0, 0};
