@@ -103,14 +103,178 @@ static void pm_remove(orc_pmap *m, uint64_t key) {
     }
 }
 
+/* ---------------------------------------------------------------- capacity-bounded LRU map
+ * CacheMap / ConcurrentLinkedHashMapWrapper (PF/slots/statistic/cache/ConcurrentLinkedHashMapWrapper.java:
+ * 35-44) over com.googlecode.concurrentlinkedhashmap:concurrentlinkedhashmap-lru:1.4.2, which is not
+ * vendored in the reference.  Restated from CLHM's published algorithm for ONE thread: an
+ * access-ordered deque; get / putIfAbsent on a present key record a read (the key moves to the MRU
+ * end), put / an insert record a write (MRU end), and after an insert that takes the size above the
+ * capacity the LRU end is evicted (singleton weigher: every entry weighs 1).  CLHM buffers reads and
+ * drains them before a write is applied, so single-threaded its order is exactly this strict LRU.
+ * Parity vs CLHM itself: unpinned (no reference test evicts); exact vs this restatement. */
+typedef struct {
+    uint64_t key;
+    int64_t val;
+    int32_t prev, next; /* towards LRU / towards MRU; -1 at the ends */
+} lru_node;
+
+struct orc_lru {
+    orc_pmap *idx; /* key -> node index */
+    lru_node *nodes;
+    int32_t *free_list;
+    int32_t nfree, head, tail; /* head = least recently used */
+    size_t cap, n, alloc, hw;
+    uint64_t evictions;
+};
+
+static orc_lru *lru_new(size_t cap) {
+    orc_lru *m = (orc_lru *)calloc(1, sizeof(orc_lru));
+    m->idx = pm_new();
+    m->cap = cap;
+    m->head = m->tail = -1;
+    return m;
+}
+
+static void lru_free(orc_lru *m) {
+    if (!m) return;
+    pm_free(m->idx);
+    free(m->nodes);
+    free(m->free_list);
+    free(m);
+}
+
+static void lru_unlink(orc_lru *m, int32_t i) {
+    lru_node *x = &m->nodes[i];
+    if (x->prev >= 0) m->nodes[x->prev].next = x->next;
+    else m->head = x->next;
+    if (x->next >= 0) m->nodes[x->next].prev = x->prev;
+    else m->tail = x->prev;
+    x->prev = x->next = -1;
+}
+
+static void lru_append(orc_lru *m, int32_t i) { /* at the MRU end */
+    lru_node *x = &m->nodes[i];
+    x->prev = m->tail;
+    x->next = -1;
+    if (m->tail >= 0) m->nodes[m->tail].next = i;
+    else m->head = i;
+    m->tail = i;
+}
+
+static void lru_touch(orc_lru *m, int32_t i) {
+    if (m->tail == i) return;
+    lru_unlink(m, i);
+    lru_append(m, i);
+}
+
+static void lru_drop(orc_lru *m, int32_t i) {
+    lru_unlink(m, i);
+    pm_remove(m->idx, m->nodes[i].key);
+    m->free_list[m->nfree++] = i;
+    m->n--;
+}
+
+/* the node of `key` without recording an access, or NULL */
+static int64_t *lru_peek(orc_lru *m, uint64_t key) {
+    int64_t *p = pm_find(m->idx, key);
+    return p ? &m->nodes[*p].val : NULL;
+}
+
+/* CacheMap.get: a read of a present key */
+static int64_t *lru_get(orc_lru *m, uint64_t key) {
+    int64_t *p = pm_find(m->idx, key);
+    if (!p) return NULL;
+    const int32_t i = (int32_t)*p;
+    lru_touch(m, i);
+    return &m->nodes[i].val;
+}
+
+static int32_t lru_insert(orc_lru *m, uint64_t key, int64_t val) {
+    int32_t i;
+    if (m->nfree) {
+        i = m->free_list[--m->nfree];
+    } else {
+        if (m->hw == m->alloc) {
+            const size_t na = m->alloc ? m->alloc * 2 : 64;
+            m->nodes = (lru_node *)realloc(m->nodes, na * sizeof(lru_node));
+            m->free_list = (int32_t *)realloc(m->free_list, na * sizeof(int32_t));
+            m->alloc = na;
+        }
+        i = (int32_t)m->hw++;
+    }
+    m->nodes[i].key = key;
+    m->nodes[i].val = val;
+    pm_put(m->idx, key, i);
+    m->n++;
+    lru_append(m, i);
+    while (m->n > m->cap && m->head >= 0) { /* evict from the LRU end */
+        m->evictions++;
+        lru_drop(m, m->head);
+    }
+    return i;
+}
+
+/* CacheMap.putIfAbsent: NULL after inserting `val` (the key was absent), else the present value
+ * (a read: the key moves to the MRU end, the value is kept) */
+static int64_t *lru_put_if_absent(orc_lru *m, uint64_t key, int64_t val) {
+    int64_t *p = pm_find(m->idx, key);
+    if (p) {
+        const int32_t i = (int32_t)*p;
+        lru_touch(m, i);
+        return &m->nodes[i].val;
+    }
+    lru_insert(m, key, val);
+    return NULL;
+}
+
+/* CacheMap.put: insert or replace (a write: MRU end) */
+static void lru_put(orc_lru *m, uint64_t key, int64_t val) {
+    int64_t *p = pm_find(m->idx, key);
+    if (p) {
+        const int32_t i = (int32_t)*p;
+        m->nodes[i].val = val;
+        lru_touch(m, i);
+        return;
+    }
+    lru_insert(m, key, val);
+}
+
+/* CacheMap.remove */
+static void lru_remove(orc_lru *m, uint64_t key) {
+    int64_t *p = pm_find(m->idx, key);
+    if (p) lru_drop(m, (int32_t)*p);
+}
+
+size_t orc_lru_size(const orc_lru *m) { return m ? m->n : 0; }
+uint64_t orc_lru_evictions(const orc_lru *m) { return m ? m->evictions : 0; }
+/* the keys from least to most recently used (test introspection) */
+size_t orc_lru_keys(const orc_lru *m, uint64_t *out, int64_t *vals, size_t cap) {
+    size_t k = 0;
+    for (int32_t i = m ? m->head : -1; i >= 0 && k < cap; i = m->nodes[i].next, k++) {
+        out[k] = m->nodes[i].key;
+        if (vals) vals[k] = m->nodes[i].val;
+    }
+    return k;
+}
+
 /* ---------------------------------------------------------------- param rules */
+/* ParameterMetric capacities, PF/slots/block/flow/param/ParameterMetric.java:37-39 */
+#define PM_THREAD_COUNT_MAX_CAPACITY 4000
+#define PM_BASE_PARAM_MAX_CAPACITY 4000
+#define PM_TOTAL_MAX_CAPACITY 200000
+
 struct orc_prule {
     orc_param_rule r;
     uint64_t *hot_v;
     int32_t *hot_t;
-    orc_pmap *time;   /* ParameterMetric.ruleTimeCounters[rule] */
-    orc_pmap *token;  /* ParameterMetric.ruleTokenCounter[rule] */
+    orc_lru *time;   /* ParameterMetric.ruleTimeCounters[rule], capacity min(4000 * duration, 200000) */
+    orc_lru *token;  /* ParameterMetric.ruleTokenCounter[rule], same capacity (ParameterMetric.java:95-112) */
 };
+
+static size_t param_capacity(const orc_param_rule *r) { /* Math.min(BASE * durationInSec, TOTAL) */
+    const int64_t c = (int64_t)PM_BASE_PARAM_MAX_CAPACITY * (int64_t)r->duration_in_sec;
+    return (size_t)(c < PM_TOTAL_MAX_CAPACITY ? c : PM_TOTAL_MAX_CAPACITY);
+}
 
 orc_prule *orc_prule_new(const orc_param_rule *r) {
     orc_prule *p = (orc_prule *)calloc(1, sizeof(orc_prule));
@@ -123,8 +287,8 @@ orc_prule *orc_prule_new(const orc_param_rule *r) {
     }
     p->r.hot_values = p->hot_v;
     p->r.hot_thresholds = p->hot_t;
-    p->time = pm_new();
-    p->token = pm_new();
+    p->time = lru_new(param_capacity(r));
+    p->token = lru_new(param_capacity(r));
     return p;
 }
 
@@ -132,8 +296,8 @@ void orc_prule_free(orc_prule *p) {
     if (!p) return;
     free(p->hot_v);
     free(p->hot_t);
-    pm_free(p->time);
-    pm_free(p->token);
+    lru_free(p->time);
+    lru_free(p->token);
     free(p);
 }
 
@@ -149,7 +313,13 @@ static int hot_lookup(const orc_prule *p, uint64_t value, int64_t *thr) {
 static int64_t lwrap_mul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
 static int64_t lwrap_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
 
-/* ParamFlowChecker.passDefaultLocalCheck, PF/slots/block/flow/param/ParamFlowChecker.java:132-222 */
+/* ParamFlowChecker.passDefaultLocalCheck, PF/slots/block/flow/param/ParamFlowChecker.java:132-222.
+ * Every map call below is an access of the LRU maps (CacheMap.putIfAbsent / get).  The time and the
+ * token map have the same capacity and see the same key sequence (each check that reaches the maps
+ * accesses the time map, then the token map, with the same value), so single-threaded they always
+ * hold the same keys: the reference's spin (:205-219, time kept and token evicted: Thread.yield until
+ * passTime > duration) cannot arise here.  Should it, it is resolved as the spin ends in the
+ * reference: the refill branch at the current time (token = maxCount - acquireCount, time = now). */
 static int pass_default(orc_prule *p, uint64_t value, int acquire, int64_t now) {
     int64_t token_count = j_d2l(p->r.count);
     int64_t hot;
@@ -157,19 +327,17 @@ static int pass_default(orc_prule *p, uint64_t value, int acquire, int64_t now) 
     if (token_count == 0) return 0;
     const int64_t max_count = lwrap_add(token_count, p->r.burst_count);
     if ((int64_t)acquire > max_count) return 0;
-    int64_t *last = pm_find(p->time, value);
-    if (!last) {
-        pm_put(p->time, value, now);
-        if (!pm_find(p->token, value)) pm_put(p->token, value, max_count - acquire);
+    int64_t *last = lru_put_if_absent(p->time, value, now);
+    if (!last) { /* token never added */
+        lru_put_if_absent(p->token, value, max_count - acquire);
         return 1;
     }
     const int64_t pass_time = now - *last;
     const int64_t dur_ms = lwrap_mul(p->r.duration_in_sec, 1000);
     if (pass_time > dur_ms) {
-        int64_t *old = pm_find(p->token, value);
+        int64_t *old = lru_put_if_absent(p->token, value, max_count - acquire);
         if (!old) {
-            pm_put(p->token, value, max_count - acquire);
-            *pm_find(p->time, value) = now;
+            *lru_peek(p->time, value) = now; /* lastAddTokenTime.set(currentTime) */
             return 1;
         }
         const int64_t rest = *old;
@@ -178,10 +346,10 @@ static int pass_default(orc_prule *p, uint64_t value, int acquire, int64_t now) 
             lwrap_add(to_add, rest) > max_count ? max_count - acquire : lwrap_add(rest, to_add) - acquire;
         if (new_qps < 0) return 0;
         *old = new_qps;
-        *pm_find(p->time, value) = now;
+        *lru_peek(p->time, value) = now;
         return 1;
     }
-    int64_t *old = pm_find(p->token, value);
+    int64_t *old = lru_get(p->token, value);
     if (old) {
         if (*old - acquire >= 0) {
             *old -= acquire;
@@ -189,11 +357,13 @@ static int pass_default(orc_prule *p, uint64_t value, int acquire, int64_t now) 
         }
         return 0;
     }
-    /* token evicted but time kept: the reference spins (Thread.yield loop); maps never evict here */
-    return 0;
+    /* the spin case (unreachable under one thread, see above): the refill branch at `now` */
+    lru_put_if_absent(p->token, value, max_count - acquire);
+    *lru_peek(p->time, value) = now;
+    return 1;
 }
 
-/* ParamFlowChecker.passThrottleLocalCheck, ParamFlowChecker.java:224-281 */
+/* ParamFlowChecker.passThrottleLocalCheck, ParamFlowChecker.java:224-281 (time map only) */
 static int pass_throttle(orc_prule *p, uint64_t value, int acquire, int64_t now, int64_t *wait_ms) {
     int64_t token_count = j_d2l(p->r.count);
     int64_t hot;
@@ -201,14 +371,12 @@ static int pass_throttle(orc_prule *p, uint64_t value, int acquire, int64_t now,
     if (token_count == 0) return 0;
     const int64_t cost =
         j_round(1.0 * 1000 * (double)acquire * (double)p->r.duration_in_sec / (double)token_count);
-    int64_t *rec = pm_find(p->time, value);
-    if (!rec) {
-        pm_put(p->time, value, now);
-        return 1;
-    }
+    int64_t *rec = lru_put_if_absent(p->time, value, now);
+    if (!rec) return 1;
     const int64_t last = *rec;
     const int64_t expected = last + cost;
     if (expected <= now || expected - now < p->r.max_queueing_time_ms) {
+        rec = lru_get(p->time, value); /* timeRecorderMap.get(value): already the MRU key */
         *rec = now;
         const int64_t wait = expected - now;
         if (wait > 0) {
@@ -370,7 +538,7 @@ int orc_flow_load_param_rules(orc_flow *f, const orc_param_rule *rules, size_t n
         }
         for (int k = 0; k < nold; k++) orc_prule_free(old[k]);
         free(old);
-        if (fr->nprule && !fr->pthreads) fr->pthreads = pm_new();
+        if (fr->nprule && !fr->pthreads) fr->pthreads = lru_new(PM_THREAD_COUNT_MAX_CAPACITY);
     }
     return valid;
 }
@@ -425,22 +593,23 @@ int orc_flow_load_degrade_rules(orc_flow *f, const orc_degrade_rule *rules, size
 void orc_flow_res_free_ext(flow_res *fr) {
     for (int k = 0; k < fr->nprule; k++) orc_prule_free(fr->prule[k]);
     free(fr->prule);
-    pm_free(fr->pthreads);
+    lru_free(fr->pthreads);
     for (int k = 0; k < fr->ncb; k++) cb_free(fr->cb[k]);
     free(fr->cb);
 }
 
 /* ---------------------------------------------------------------- slot chain */
 /* ParameterMetric.addThreadCount / decreaseThreadCount (ParameterMetric.java:125-230): every element
- * of a Collection / array argument, else the single value. */
+ * of a Collection / array argument, else the single value; the thread map is a CacheMap of capacity
+ * 4000 (THREAD_COUNT_MAX_CAPACITY, :37, :115-120), LRU as above. */
 static void param_thread_add(const orc_flow *f, flow_res *fr, int has_param, uint64_t param) {
     if (!fr->pthreads || !has_param) return;
     const uint64_t *v = f->plist ? f->plist : &param;
     const uint32_t nv = f->plist ? f->plist_n : 1;
     for (uint32_t i = 0; i < nv; i++) {
-        int64_t *c = pm_find(fr->pthreads, v[i]);
-        if (c) (*c)++;
-        else pm_put(fr->pthreads, v[i], 1);
+        int64_t *c = lru_put_if_absent(fr->pthreads, v[i], 0); /* putIfAbsent(value, new AtomicInteger()) */
+        if (c) (*c)++;                                          /* oldValue.incrementAndGet() */
+        else lru_put(fr->pthreads, v[i], 1);                    /* put(value, new AtomicInteger(1)) */
     }
 }
 
@@ -449,12 +618,8 @@ static void param_thread_dec(const orc_flow *f, flow_res *fr, int has_param, uin
     const uint64_t *v = f->plist ? f->plist : &param;
     const uint32_t nv = f->plist ? f->plist_n : 1;
     for (uint32_t i = 0; i < nv; i++) {
-        int64_t *c = pm_find(fr->pthreads, v[i]);
-        if (!c) {
-            pm_put(fr->pthreads, v[i], 0); /* putIfAbsent(value, new AtomicInteger()) */
-            continue;
-        }
-        if (--(*c) <= 0) pm_remove(fr->pthreads, v[i]);
+        int64_t *c = lru_put_if_absent(fr->pthreads, v[i], 0); /* absent: stays as a 0 entry */
+        if (c && --(*c) <= 0) lru_remove(fr->pthreads, v[i]);
     }
 }
 
@@ -483,8 +648,8 @@ int orc_flow_entry_p(orc_flow *f, uint32_t resource, int64_t now, int acquire, i
         const uint32_t nv = f->plist ? f->plist_n : 1;
         for (uint32_t q = 0; q < nv; q++) {
             int64_t tc = 0;
-            if (idx == 0 && fr->pthreads) {
-                int64_t *c = pm_find(fr->pthreads, vals[q]);
+            if (idx == 0 && fr->pthreads && p->r.grade == ORC_GRADE_THREAD) {
+                int64_t *c = lru_get(fr->pthreads, vals[q]); /* getThreadCount: CacheMap.get */
                 tc = c ? *c : 0;
             }
             int64_t w = 0;
@@ -699,4 +864,21 @@ void orc_flow_replay_p(orc_flow *f, size_t n, const uint8_t *kind, const uint32_
         if (decision) decision[i] = (int8_t)d;
         if (wait_ms) wait_ms[i] = (int32_t)w;
     }
+}
+
+/* Test introspection of the LRU maps: which = 0 time map, 1 token map of a rule */
+size_t orc_prule_map_size(const orc_prule *p, int which) { return orc_lru_size(which ? p->token : p->time); }
+uint64_t orc_prule_map_evictions(const orc_prule *p, int which) {
+    return orc_lru_evictions(which ? p->token : p->time);
+}
+size_t orc_prule_map_keys(const orc_prule *p, int which, uint64_t *keys, int64_t *vals, size_t cap) {
+    return orc_lru_keys(which ? p->token : p->time, keys, vals, cap);
+}
+/* resource `r`'s k-th parameter rule's maps (which 0/1) or its thread map (which 2) */
+size_t orc_flow_param_map_size(const orc_flow *f, uint32_t r, int k, int which) {
+    if (r >= f->n) return 0;
+    const flow_res *fr = &f->res[r];
+    if (which == 2) return orc_lru_size(fr->pthreads);
+    if (k >= fr->nprule) return 0;
+    return orc_prule_map_size(fr->prule[k], which);
 }

@@ -91,6 +91,11 @@ void orc_flow_replay_pl(orc_flow *f, size_t n, const uint8_t *kind, const uint32
 typedef struct orc_prule orc_prule;
 orc_prule *orc_prule_new(const orc_param_rule *r);
 void orc_prule_free(orc_prule *p);
+/* LRU CacheMap introspection (tests): which 0 = time map, 1 = token map, 2 = the resource's thread map */
+size_t orc_prule_map_size(const orc_prule *p, int which);
+uint64_t orc_prule_map_evictions(const orc_prule *p, int which);
+size_t orc_prule_map_keys(const orc_prule *p, int which, uint64_t *keys, int64_t *vals, size_t cap);
+size_t orc_flow_param_map_size(const orc_flow *f, uint32_t r, int k, int which);
 int orc_prule_pass_single(orc_prule *p, uint64_t value, int acquire, int64_t now, int64_t thread_count,
                           int64_t *wait_ms);
 

@@ -53,6 +53,7 @@ struct orc_ctrl {
 
 typedef struct orc_cb orc_cb;        /* circuit breaker (oracle_ext.c) */
 typedef struct orc_pmap orc_pmap;    /* u64 -> i64 map (oracle_ext.c) */
+typedef struct orc_lru orc_lru;      /* capacity-bounded LRU CacheMap (oracle_ext.c) */
 
 typedef struct flow_res {
     orc_node *node;  /* ClusterNode of the resource (ClusterBuilderSlot.java:82-110) */
@@ -62,7 +63,7 @@ typedef struct flow_res {
     int64_t *cflow;             /* per rule: ClusterFlowConfig.flowId */
     orc_prule **prule;  /* ParamFlowRuleManager rules of the resource, list order */
     int nprule;
-    orc_pmap *pthreads; /* ParameterMetric.threadCountMap[0] */
+    orc_lru *pthreads;  /* ParameterMetric.threadCountMap[0] (LRU, capacity 4000) */
     orc_cb **cb;        /* DegradeRuleManager circuit breakers, list order */
     int ncb;
 } flow_res;

@@ -34,6 +34,47 @@ RANDOM = {"k_cold_fused", "k_hot_flows", "k_hot_precheck", "k_hot_hist", "k_hot_
           "k_cluster_nodes"}
 
 
+def base(k):
+    """k_cold_fused_t<0> -> k_cold_fused; k_rs64_sweep<7> -> k_rs64_sweep (template instances and the
+    _t suffix of templated kernels are classified by their base name)."""
+    b = re.sub(r"<.*", "", k)
+    return b[:-2] if b.endswith("_t") else b
+
+
+STREAMING_BASE = {base(k) for k in STREAMING}
+RANDOM_BASE = {base(k) for k in RANDOM}
+
+
+def kind_of(k):
+    b = base(k)
+    return "stream" if b in STREAMING_BASE else ("random" if b in RANDOM_BASE else "other")
+
+
+def alg_bytes(k, bl):
+    """Per-kernel share of SURVEY.md 8(d)'s algorithmic bytes per step, from the bench line `bl`:
+    the key kernel reads every request (E_in = 12 B), the cold stage writes the cold results and reads
+    + writes the cold touched rules, the hot runs read + write the hot rules, the hot results kernel
+    writes the hot results (E_out = 8 B).  Everything else (the sort, scans, next hot set) is 0:
+    traffic there is non-algorithmic.  Hot touched rules ~ the hot-set size of the last batch."""
+    if not bl:
+        return None
+    n = bl["config"]["requests_per_step_per_gpu"]
+    touched = bl["roofline"]["touched_rules_per_step_per_gpu"]
+    lp = bl.get("last_batch_path") or {}
+    n_cold = lp.get("n_cold", n)
+    t_hot = min(lp.get("n_hot_next", 0), touched)
+    b = base(k)
+    if b == "k_hot_key_dense" and k.endswith("<0>"):
+        return n * 12.0
+    if b == "k_cold_fused":
+        return n_cold * 8.0 + (touched - t_hot) * 2 * 704.0
+    if b == "k_hot_flows":
+        return t_hot * 2 * 704.0
+    if b == "k_hot_final":
+        return (n - n_cold) * 8.0
+    return 0.0
+
+
 def short(name):
     m = re.search(r"(k_\w+(<[^>]*>)?)", name)
     return m.group(1) if m else name[:60]
@@ -54,12 +95,13 @@ def main():
             name = row.get("Kernel_Name", row.get("Kernel-Name", "?"))
             agg[(short(name), "sga::" in name)][row["Counter_Name"]].append(float(row["Counter_Value"]))
 
-    sets = None
+    sets, bline = None, None
     if a.steps_from and os.path.exists(a.steps_from):
         for line in open(a.steps_from):
             if line.startswith("{"):
                 d = json.loads(line)
                 sets = d["steps"] + d["warmup"]
+                bline = d
     rand_factor = 1.0
     if a.cal and os.path.exists(a.cal):
         rand_factor = float(json.load(open(a.cal)).get("random16_fetch_factor", 1.0))
@@ -88,7 +130,7 @@ def main():
         per_step = n_calls / sets
         fr = (sum(cs.get("FETCH_SIZE", [0.0])) / max(1, len(cs.get("FETCH_SIZE", [])))) * 1024.0
         wr = (sum(cs.get("WRITE_SIZE", [0.0])) / max(1, len(cs.get("WRITE_SIZE", [])))) * 1024.0
-        kind = "stream" if k in STREAMING else ("random" if k in RANDOM else "other")
+        kind = kind_of(k)
         fac = 2.0 if kind == "stream" else (rand_factor if kind == "random" else 1.0)
         us = None
         if durations.get(k):
@@ -99,6 +141,9 @@ def main():
                "fetch_factor": fac, "fetch_mb": fr * fac * per_step / 1e6, "write_mb": wr * per_step / 1e6,
                "us_per_step": us}
         row["traffic_mb"] = row["fetch_mb"] + row["write_mb"]
+        ab = alg_bytes(k, bline)
+        row["alg_mb"] = None if ab is None else ab / 1e6
+        row["traffic_over_alg"] = (row["traffic_mb"] / row["alg_mb"]) if row["alg_mb"] else None
         tot["fetch_raw"] += row["fetch_raw_mb"]
         tot["fetch"] += row["fetch_mb"]
         tot["write"] += row["write_mb"]
@@ -106,11 +151,13 @@ def main():
     table.sort(key=lambda r: -r["traffic_mb"])
     print(f"\nper step ({sets} dispatch sets; engine kernels only; FETCH x2 for streaming kernels, "
           f"x{rand_factor:.2f} for random-gather kernels)")
-    print(f"{'kernel':24s} {'kind':7s} {'calls':>5s} {'fetch_raw':>10s} {'fetch':>10s} {'write':>10s} {'traffic':>10s} {'us':>8s}")
+    print(f"{'kernel':24s} {'kind':7s} {'calls':>5s} {'fetch_raw':>10s} {'fetch':>10s} {'write':>10s} {'traffic':>10s} "
+          f"{'alg':>8s} {'us':>8s}")
     for r in table:
         us = f"{r['us_per_step']:8.1f}" if r["us_per_step"] is not None else "       -"
+        al = f"{r['alg_mb']:8.1f}" if r["alg_mb"] is not None else "       -"
         print(f"{r['kernel']:24s} {r['kind']:7s} {r['calls_per_step']:5.2f} {r['fetch_raw_mb']:10.1f} {r['fetch_mb']:10.1f} "
-              f"{r['write_mb']:10.1f} {r['traffic_mb']:10.1f} {us}")
+              f"{r['write_mb']:10.1f} {r['traffic_mb']:10.1f} {al} {us}")
     traffic = (tot["fetch"] + tot["write"]) * 1e6
     print(f"{'total':24s} {'':7s} {'':5s} {tot['fetch_raw']:10.1f} {tot['fetch']:10.1f} {tot['write']:10.1f} "
           f"{traffic / 1e6:10.1f} {tot['us']:8.1f}")
@@ -119,6 +166,7 @@ def main():
                    "fetch_bytes_per_step_raw": tot["fetch_raw"] * 1e6, "write_bytes_per_step": tot["write"] * 1e6,
                    "kernel_us_per_step": tot["us"], "dispatch_sets": sets, "random_fetch_factor": rand_factor,
                    "run": os.path.basename(os.path.normpath(a.dir)), "kernels": table,
+                   "alg_bytes_per_step": sum((r["alg_mb"] or 0.0) for r in table) * 1e6 if bline else None,
                    "note": "engine kernels only (sga::, per batch); FETCH_SIZE x2 for coalesced streaming kernels, "
                            "x random16_fetch_factor (tools/calib/pmccal.hip) for random-gather kernels; WRITE_SIZE as "
                            "reported"},
