@@ -11,7 +11,7 @@ independently of the C oracle, over ParamFlowChecker.passDefaultLocalCheck / pas
 (ParamFlowChecker.java:132-281).  They pin the oracle's LRU restatement (tests/test_oracle_lru.py);
 parity with CLHM itself stays unpinned.
 
-Run: python3 tests/golden/make_lru_golden.py  (writes tests/golden/kat_lru_*.json)."""
+Run: python3 tests/golden/make_lru_golden.py  (writes tests/golden/lrukat_*.json)."""
 import json
 import os
 import random
@@ -158,7 +158,7 @@ def main():
             "events": [list(e) for e in events], "expect": expect,
             "final_time_map_size": len(keys_sorted), "final_time_map_lru_head": lru_head,
         }
-        with open(os.path.join(HERE, f"kat_lru_{name}.json"), "w") as fh:
+        with open(os.path.join(HERE, f"lrukat_{name}.json"), "w") as fh:
             json.dump(doc, fh, separators=(",", ":"))
         print(name, len(events), "events,", sum(d for d, _ in expect), "passed")
 

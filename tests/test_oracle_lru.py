@@ -11,7 +11,7 @@ import pytest
 
 from tests import oracle_harness as H
 
-GOLD = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "kat_lru_*.json")))
+GOLD = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "lrukat_*.json")))
 
 
 def _lib():
@@ -27,7 +27,7 @@ def _lib():
     return L
 
 
-@pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p)[8:-5] for p in GOLD])
+@pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p)[7:-5] for p in GOLD])
 def test_lru_eviction_vectors(path):
     doc = json.load(open(path))
     L = _lib()
