@@ -352,6 +352,16 @@ int sga_rls_should_rate_limit_device(sga_engine *e, const uint32_t *d_desc_offse
 #define SGA_EV_PARAM_LIST 16u /* with HAS_PARAM: args[0] is a Collection / array; param = offset << 32 | count
                                * into sga_submit_events_ex's param_values (every element is checked,
                                * ParamFlowChecker.passLocalCheck, and counted by ParameterMetric) */
+#define SGA_EV_ARGS 32u       /* the event's whole argument vector (SphU.entry(..., Object... args)):
+                               * param = offset << 32 | nargs into param_values, two words per argument:
+                               * param_values[offset + 2k] = kind << 62 | list length, param_values[offset
+                               * + 2k + 1] = the argument's 64-bit key (SGA_ARG_SCALAR) or the offset of its
+                               * elements in param_values (SGA_ARG_LIST: a Collection / array); SGA_ARG_NULL
+                               * is a null argument.  HAS_PARAM / PARAM_LIST are ignored on such events.
+                               * Chunks holding them are decided in arrival order by one lane. */
+#define SGA_ARG_SCALAR 0u
+#define SGA_ARG_NULL 1u
+#define SGA_ARG_LIST 2u
 
 /* resource id of Constants.ENTRY_NODE ("__total_inbound_traffic__") in sga_query_node and metric rows */
 #define SGA_ENTRY_NODE 0xFFFFFFFFu
@@ -385,12 +395,23 @@ typedef struct sga_param_rule {
     int32_t control_behavior;      /* 0 token bucket, 2 throttle (RATE_LIMITER) */
     int32_t max_queueing_time_ms;  /* default 0 */
     int32_t burst_count;           /* default 0 */
-    int32_t param_idx;             /* 0 (or -1): the event's single parameter */
+    int32_t param_idx;             /* args index; negative counts from the end, fixed on the rule at its first
+                                    * check (ParamFlowSlot.applyRealParamIdx, ParamFlowSlot.java:56-66);
+                                    * -64 <= param_idx < 64 */
     int64_t duration_in_sec;       /* default 1 */
     uint32_t n_hot;                /* parsed hot items: value -> threshold */
     uint32_t reserved;
     const uint64_t *hot_values;
     const int32_t *hot_thresholds;
+    /* ParamFlowRule.clusterMode + ParamFlowClusterConfig (ParamFlowClusterConfig.java:32-44): with the
+     * embedded token server on (sga_set_cluster_server 1) a QPS rule asks this engine's cluster parameter
+     * path (TokenService.requestParamToken -> ClusterParamFlowChecker) in event order: OK passes,
+     * BLOCKED blocks, anything else falls back (ParamFlowChecker.passClusterCheck, :305-343) */
+    int32_t cluster_mode;
+    int32_t cluster_fallback;      /* fallbackToLocalWhenFail, default 0 */
+    int64_t cluster_flow_id;
+    int32_t cluster_sample_count;  /* validity only (ParamFlowRuleUtil.checkCluster): default 10 */
+    int32_t cluster_window_ms;     /* default 1000 */
 } sga_param_rule;
 
 /* DegradeRule, CORE/slots/block/degrade/DegradeRule.java:59-84 */

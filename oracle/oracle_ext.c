@@ -265,6 +265,8 @@ size_t orc_lru_keys(const orc_lru *m, uint64_t *out, int64_t *vals, size_t cap) 
 
 struct orc_prule {
     orc_param_rule r;
+    int32_t idx;      /* paramIdx after ParamFlowSlot.applyRealParamIdx (ParamFlowSlot.java:56-66) */
+    int resolved;     /* the rule was checked once: idx is final (the reference mutates the rule) */
     uint64_t *hot_v;
     int32_t *hot_t;
     orc_lru *time;   /* ParameterMetric.ruleTimeCounters[rule], capacity min(4000 * duration, 200000) */
@@ -497,25 +499,63 @@ int orc_flow_cb_state(orc_flow *f, uint32_t resource, int k) {
 }
 
 /* ---------------------------------------------------------------- rule loading */
-static int param_rule_valid(const orc_param_rule *r) { /* ParamFlowRuleUtil.isValidParamRule, :40-50 */
-    return r->count >= 0 && r->grade >= 0 && r->duration_in_sec > 0 && r->burst_count >= 0 &&
-           r->control_behavior >= 0 && r->max_queueing_time_ms >= 0;
+static int param_rule_valid(const orc_param_rule *r) { /* ParamFlowRuleUtil.isValidRule + checkCluster, :46-69 */
+    if (!(r->count >= 0 && r->grade >= 0 && r->duration_in_sec > 0 && r->burst_count >= 0 &&
+          r->control_behavior >= 0 && r->max_queueing_time_ms >= 0))
+        return 0;
+    if (!r->cluster_mode) return 1;
+    if (!(r->cluster_sample_count > 0 && r->cluster_window_ms > 0 && r->cluster_window_ms % r->cluster_sample_count == 0))
+        return 0; /* FlowRuleUtil.isWindowConfigValid */
+    return r->cluster_flow_id > 0; /* validClusterRuleId */
 }
 
-static int param_rule_equal(const orc_param_rule *a, const orc_param_rule *b) {
+/* ParamFlowRule.equals (ParamFlowRule.java:192-210) of a loaded rule `old` -- whose paramIdx the slot
+ * may have rewritten (applyRealParamIdx mutates the rule object) -- and a new rule b */
+static int param_rule_equal(const orc_prule *old, const orc_param_rule *b) {
+    const orc_param_rule *a = &old->r;
+    const int32_t aidx = old->resolved ? old->idx : a->param_idx;
     if (a->grade != b->grade || a->count != b->count || a->control_behavior != b->control_behavior ||
         a->max_queueing_time_ms != b->max_queueing_time_ms || a->burst_count != b->burst_count ||
-        a->param_idx != b->param_idx || a->duration_in_sec != b->duration_in_sec || a->n_hot != b->n_hot)
+        aidx != b->param_idx || a->duration_in_sec != b->duration_in_sec || a->n_hot != b->n_hot ||
+        a->cluster_mode != b->cluster_mode)
+        return 0;
+    if (a->cluster_mode && (a->cluster_fallback != b->cluster_fallback || a->cluster_flow_id != b->cluster_flow_id ||
+                            a->cluster_sample_count != b->cluster_sample_count ||
+                            a->cluster_window_ms != b->cluster_window_ms))
         return 0;
     for (uint32_t i = 0; i < a->n_hot; i++)
         if (a->hot_values[i] != b->hot_values[i] || a->hot_thresholds[i] != b->hot_thresholds[i]) return 0;
     return 1;
 }
 
-/* ParamFlowRuleManager.loadRules: rules grouped by resource in list order; the
- * ParameterMetric maps are keyed by the rule (equal rules keep their maps). */
+static void thread_map_remove(flow_res *fr, int32_t idx) { /* threadCountMap.remove(idx) */
+    for (int k = 0; k < fr->npt; k++)
+        if (fr->pt_idx[k] == idx) {
+            lru_free(fr->pt_map[k]);
+            fr->pt_idx[k] = fr->pt_idx[fr->npt - 1];
+            fr->pt_map[k] = fr->pt_map[fr->npt - 1];
+            fr->npt--;
+            return;
+        }
+}
+
+static void thread_maps_clear(flow_res *fr) { /* ParameterMetricStorage.clearParamMetricForResource */
+    for (int k = 0; k < fr->npt; k++) lru_free(fr->pt_map[k]);
+    fr->npt = 0;
+}
+
+/* ParamFlowRuleManager.loadRules (ParamFlowRuleManager.java:101-150): rules grouped by resource in list
+ * order; the ParameterMetric maps are keyed by the rule (equal rules keep their maps).
+ * aggregateAndPrepareParamRules: no rules at all clears every metric; a resource left without rules
+ * loses its metric; each removed rule clears its maps and the thread-count map of its paramIdx
+ * (ParameterMetric.clearForRule, ParameterMetric.java:86-92). */
 int orc_flow_load_param_rules(orc_flow *f, const orc_param_rule *rules, size_t n) {
     int valid = 0;
+    for (size_t j = 0; j < n; j++)
+        if (rules[j].resource < f->n && param_rule_valid(&rules[j])) valid++;
+    if (valid == 0)
+        for (uint32_t i = 0; i < f->n; i++) thread_maps_clear(&f->res[i]);
+    valid = 0;
     for (uint32_t i = 0; i < f->n; i++) {
         flow_res *fr = &f->res[i];
         orc_prule **old = fr->prule;
@@ -526,7 +566,7 @@ int orc_flow_load_param_rules(orc_flow *f, const orc_param_rule *rules, size_t n
             if (rules[j].resource != i || !param_rule_valid(&rules[j])) continue;
             orc_prule *keep = NULL;
             for (int k = 0; k < nold; k++)
-                if (old[k] && param_rule_equal(&old[k]->r, &rules[j])) {
+                if (old[k] && param_rule_equal(old[k], &rules[j])) {
                     keep = old[k];
                     old[k] = NULL;
                     break;
@@ -536,9 +576,12 @@ int orc_flow_load_param_rules(orc_flow *f, const orc_param_rule *rules, size_t n
             fr->prule[fr->nprule++] = keep;
             valid++;
         }
-        for (int k = 0; k < nold; k++) orc_prule_free(old[k]);
+        if (nold && !fr->nprule) thread_maps_clear(fr);
+        for (int k = 0; k < nold; k++) {
+            if (old[k] && fr->nprule) thread_map_remove(fr, old[k]->resolved ? old[k]->idx : old[k]->r.param_idx);
+            orc_prule_free(old[k]);
+        }
         free(old);
-        if (fr->nprule && !fr->pthreads) fr->pthreads = lru_new(PM_THREAD_COUNT_MAX_CAPACITY);
     }
     return valid;
 }
@@ -593,34 +636,116 @@ int orc_flow_load_degrade_rules(orc_flow *f, const orc_degrade_rule *rules, size
 void orc_flow_res_free_ext(flow_res *fr) {
     for (int k = 0; k < fr->nprule; k++) orc_prule_free(fr->prule[k]);
     free(fr->prule);
-    lru_free(fr->pthreads);
+    for (int k = 0; k < fr->npt; k++) lru_free(fr->pt_map[k]);
+    free(fr->pt_map);
+    free(fr->pt_idx);
     for (int k = 0; k < fr->ncb; k++) cb_free(fr->cb[k]);
     free(fr->cb);
 }
 
 /* ---------------------------------------------------------------- slot chain */
-/* ParameterMetric.addThreadCount / decreaseThreadCount (ParameterMetric.java:125-230): every element
- * of a Collection / array argument, else the single value; the thread map is a CacheMap of capacity
- * 4000 (THREAD_COUNT_MAX_CAPACITY, :37, :115-120), LRU as above. */
-static void param_thread_add(const orc_flow *f, flow_res *fr, int has_param, uint64_t param) {
-    if (!fr->pthreads || !has_param) return;
-    const uint64_t *v = f->plist ? f->plist : &param;
-    const uint32_t nv = f->plist ? f->plist_n : 1;
-    for (uint32_t i = 0; i < nv; i++) {
-        int64_t *c = lru_put_if_absent(fr->pthreads, v[i], 0); /* putIfAbsent(value, new AtomicInteger()) */
-        if (c) (*c)++;                                          /* oldValue.incrementAndGet() */
-        else lru_put(fr->pthreads, v[i], 1);                    /* put(value, new AtomicInteger(1)) */
+/* ---- the event's arguments ------------------------------------------------------------------
+ * args[k] of the current event: the argument vector (SGA_EV_ARGS), else the round-2 forms (args = [param]
+ * with has_param, a Collection / array args[0] with plist, or args = []). */
+enum { ARG_SCALAR = 0, ARG_NULL = 1, ARG_LIST = 2 };
+
+static uint32_t ev_nargs(const orc_flow *f, int has_param) { return f->args ? f->nargs : (has_param ? 1u : 0u); }
+
+static int ev_arg(const orc_flow *f, uint32_t k, uint64_t param, const uint64_t **vals, uint32_t *n) {
+    if (f->args) {
+        const uint64_t h = f->args[2 * k], w = f->args[2 * k + 1];
+        const int kind = (int)(h >> 62);
+        if (kind == ARG_LIST) {
+            *vals = f->args_pvals + w;
+            *n = (uint32_t)(h & 0xffffffffu);
+        } else {
+            *vals = &f->args[2 * k + 1];
+            *n = 1;
+        }
+        return kind;
     }
+    if (k == 0 && f->plist) {
+        *vals = f->plist;
+        *n = f->plist_n;
+        return ARG_LIST;
+    }
+    static uint64_t scratch; /* single-threaded oracle */
+    scratch = param;
+    *vals = &scratch;
+    *n = 1;
+    return ARG_SCALAR;
 }
 
-static void param_thread_dec(const orc_flow *f, flow_res *fr, int has_param, uint64_t param) {
-    if (!fr->pthreads || !has_param) return;
-    const uint64_t *v = f->plist ? f->plist : &param;
-    const uint32_t nv = f->plist ? f->plist_n : 1;
-    for (uint32_t i = 0; i < nv; i++) {
-        int64_t *c = lru_put_if_absent(fr->pthreads, v[i], 0); /* absent: stays as a 0 entry */
-        if (c && --(*c) <= 0) lru_remove(fr->pthreads, v[i]);
+/* ParameterMetric.threadCountMap.get(index), or NULL (ParameterMetric.java:53, 115-120) */
+static orc_lru *thread_map(const flow_res *fr, int32_t idx) {
+    for (int k = 0; k < fr->npt; k++)
+        if (fr->pt_idx[k] == idx) return fr->pt_map[k];
+    return NULL;
+}
+
+/* ParameterMetricStorage.initParamMetricsFor -> ParameterMetric.initialize(rule): the thread map of the
+ * rule's paramIdx is created once (:113-121) */
+static void thread_map_init(flow_res *fr, int32_t idx) {
+    if (thread_map(fr, idx)) return;
+    fr->pt_idx = (int32_t *)realloc(fr->pt_idx, sizeof(int32_t) * (size_t)(fr->npt + 1));
+    fr->pt_map = (orc_lru **)realloc(fr->pt_map, sizeof(orc_lru *) * (size_t)(fr->npt + 1));
+    fr->pt_idx[fr->npt] = idx;
+    fr->pt_map[fr->npt] = lru_new(PM_THREAD_COUNT_MAX_CAPACITY);
+    fr->npt++;
+}
+
+/* ParameterMetric.addThreadCount / decreaseThreadCount (ParameterMetric.java:125-230): for every argument
+ * index that has a thread map, every element of a Collection / array argument, else the value; null
+ * arguments are skipped.  Each map is a CacheMap of capacity 4000, LRU as above. */
+static void param_threads(const orc_flow *f, flow_res *fr, int has_param, uint64_t param, int delta) {
+    if (!fr->npt) return;
+    const uint32_t na = ev_nargs(f, has_param);
+    for (uint32_t k = 0; k < na; k++) {
+        orc_lru *m = thread_map(fr, (int32_t)k);
+        if (!m) continue;
+        const uint64_t *v;
+        uint32_t nv;
+        if (ev_arg(f, k, param, &v, &nv) == ARG_NULL) continue;
+        for (uint32_t i = 0; i < nv; i++) {
+            int64_t *c = lru_put_if_absent(m, v[i], 0); /* putIfAbsent(value, new AtomicInteger()) */
+            if (delta > 0) {
+                if (c) (*c)++;                 /* oldValue.incrementAndGet() */
+                else lru_put(m, v[i], 1);      /* put(value, new AtomicInteger(1)) */
+            } else if (c && --(*c) <= 0) {     /* absent: stays as a 0 entry */
+                lru_remove(m, v[i]);
+            }
+        }
     }
+}
+static void param_thread_add(const orc_flow *f, flow_res *fr, int has_param, uint64_t param) {
+    param_threads(f, fr, has_param, param, 1);
+}
+static void param_thread_dec(const orc_flow *f, flow_res *fr, int has_param, uint64_t param) {
+    param_threads(f, fr, has_param, param, -1);
+}
+
+/* ParamFlowChecker.passLocalCheck (ParamFlowChecker.java:79-106): every element of a Collection / array
+ * must pass, in order (the elements before a failing one keep their token updates) */
+static int param_local_check(flow_res *fr, orc_prule *p, const uint64_t *vals, uint32_t nv, int acquire,
+                             int64_t now, int64_t *total_wait) {
+    for (uint32_t q = 0; q < nv; q++) {
+        int64_t tc = 0;
+        if (p->r.grade == ORC_GRADE_THREAD) { /* getThreadCount(rule.getParamIdx(), value): CacheMap.get */
+            orc_lru *m = thread_map(fr, p->idx);
+            int64_t *c = m ? lru_get(m, vals[q]) : NULL;
+            tc = c ? *c : 0;
+        }
+        int64_t w = 0;
+        if (!orc_prule_pass_single(p, vals[q], acquire, now, tc, &w)) return 0;
+        *total_wait += w;
+    }
+    return 1;
+}
+
+int32_t orc_flow_param_idx(const orc_flow *f, uint32_t r, int k) {
+    if (r >= f->n || k >= f->res[r].nprule) return INT32_MIN;
+    const orc_prule *p = f->res[r].prule[k];
+    return p->resolved ? p->idx : INT32_MIN;
 }
 
 /* CtSph.entryWithPriority -> StatisticSlot.entry (StatisticSlot.java:64-145) around
@@ -634,30 +759,42 @@ int orc_flow_entry_p(orc_flow *f, uint32_t resource, int64_t now, int acquire, i
     if (resource >= f->n) return ORC_PASS;
     flow_res *fr = &f->res[resource];
     int64_t total_wait = 0;
-    /* ParamFlowSlot */
-    const int nargs = has_param ? 1 : 0;
+    /* ParamFlowSlot.checkFlow: args is never null here (SphU.entry passes an empty array) */
+    const uint32_t nargs = ev_nargs(f, has_param);
     for (int k = 0; k < fr->nprule; k++) {
         orc_prule *p = fr->prule[k];
-        int idx = p->r.param_idx;
-        if (idx < 0) idx = (-idx <= nargs) ? nargs + idx : -idx; /* applyRealParamIdx */
-        if (nargs <= idx) continue;                               /* args.length <= paramIdx -> pass */
-        /* passLocalCheck (ParamFlowChecker.java:79-106): a Collection / array argument passes when
-         * every element passes, checked in order (the elements before a failing one keep their
-         * token updates) */
-        const uint64_t *vals = f->plist ? f->plist : &param;
-        const uint32_t nv = f->plist ? f->plist_n : 1;
-        for (uint32_t q = 0; q < nv; q++) {
-            int64_t tc = 0;
-            if (idx == 0 && fr->pthreads && p->r.grade == ORC_GRADE_THREAD) {
-                int64_t *c = lru_get(fr->pthreads, vals[q]); /* getThreadCount: CacheMap.get */
-                tc = c ? *c : 0;
+        if (!p->resolved) { /* applyRealParamIdx: a negative index is rewritten on the rule, once */
+            int idx = p->r.param_idx;
+            if (idx < 0) idx = (-idx <= (int)nargs) ? (int)nargs + idx : -idx;
+            p->idx = idx;
+            p->resolved = 1;
+        }
+        thread_map_init(fr, p->idx); /* ParameterMetricStorage.initParamMetricsFor */
+        /* ParamFlowChecker.passCheck (:48-77): args.length <= paramIdx or a null value pass */
+        if ((int64_t)nargs <= (int64_t)p->idx) continue;
+        const uint64_t *vals;
+        uint32_t nv;
+        if (ev_arg(f, (uint32_t)p->idx, param, &vals, &nv) == ARG_NULL) continue;
+        int ok;
+        if (p->r.cluster_mode && p->r.grade == ORC_GRADE_QPS) {
+            /* passClusterCheck (:305-333): requestParamToken(flowId, count, toCollection(value)) to the
+             * embedded server; OK passes, BLOCKED blocks, anything else (or no service) falls back:
+             * fallbackToLocalOrPass (:335-343) checks the collection locally or passes */
+            int st = -1; /* TokenResultStatus.FAIL: no token service */
+            if (f->server && f->cluster_mode == 1) {
+                const orc_token_result r = orc_cluster_request_param_token(f->server, p->r.cluster_flow_id, acquire,
+                                                                           (const int64_t *)vals, nv, now);
+                st = r.status;
             }
-            int64_t w = 0;
-            if (!orc_prule_pass_single(p, vals[q], acquire, now, tc, &w)) {
-                orc_node_increase_block_qps(fr->node, now, acquire);
-                return ORC_BLOCK_PARAM;
-            }
-            total_wait += w;
+            if (st == 0) ok = 1;
+            else if (st == 1) ok = 0;
+            else ok = p->r.cluster_fallback ? param_local_check(fr, p, vals, nv, acquire, now, &total_wait) : 1;
+        } else {
+            ok = param_local_check(fr, p, vals, nv, acquire, now, &total_wait);
+        }
+        if (!ok) {
+            orc_node_increase_block_qps(fr->node, now, acquire);
+            return ORC_BLOCK_PARAM;
         }
     }
     /* FlowSlot */
@@ -844,13 +981,37 @@ void orc_flow_replay_pl(orc_flow *f, size_t n, const uint8_t *kind, const uint32
     }
 }
 
-/* flags: bit 0 prioritized, bit 1 error, bit 2 has_param, bit 3 inbound (EntryType.IN) */
+void orc_flow_replay_args(orc_flow *f, size_t n, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
+                          const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
+                          const uint64_t *pvals, int8_t *decision, int32_t *wait_ms) {
+    for (size_t i = 0; i < n; i++) {
+        const uint8_t fl = flags ? flags[i] : 0;
+        if (fl & 32) {
+            f->args = pvals + (param[i] >> 32);
+            f->args_pvals = pvals;
+            f->nargs = (uint32_t)(param[i] & 0xffffffffu);
+        } else if ((fl & 16) && (fl & 4)) {
+            f->plist = pvals + (param[i] >> 32);
+            f->plist_n = (uint32_t)(param[i] & 0xffffffffu);
+        }
+        orc_flow_replay_p(f, 1, kind ? kind + i : NULL, resource + i, ts + i, acquire + i, flags ? flags + i : NULL,
+                          rt ? rt + i : NULL, param ? param + i : NULL, decision ? decision + i : NULL,
+                          wait_ms ? wait_ms + i : NULL);
+        f->args = NULL;
+        f->args_pvals = NULL;
+        f->nargs = 0;
+        f->plist = NULL;
+        f->plist_n = 0;
+    }
+}
+
+/* flags: bit 0 prioritized, bit 1 error, bit 2 has_param, bit 3 inbound (EntryType.IN), bit 5 args */
 void orc_flow_replay_p(orc_flow *f, size_t n, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
                        const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
                        int8_t *decision, int32_t *wait_ms) {
     for (size_t i = 0; i < n; i++) {
         const uint8_t fl = flags ? flags[i] : 0;
-        const int hp = (fl & 4) != 0;
+        const int hp = (fl & 4) != 0 || (fl & 32) != 0;
         const int in = (fl & 8) != 0;
         const uint64_t pv = param ? param[i] : 0;
         if (kind && kind[i] == 1) {
@@ -878,7 +1039,7 @@ size_t orc_prule_map_keys(const orc_prule *p, int which, uint64_t *keys, int64_t
 size_t orc_flow_param_map_size(const orc_flow *f, uint32_t r, int k, int which) {
     if (r >= f->n) return 0;
     const flow_res *fr = &f->res[r];
-    if (which == 2) return orc_lru_size(fr->pthreads);
+    if (which == 2) return orc_lru_size(fr->npt ? fr->pt_map[0] : NULL);
     if (k >= fr->nprule) return 0;
     return orc_prule_map_size(fr->prule[k], which);
 }

@@ -33,6 +33,12 @@ typedef struct orc_param_rule {
     uint32_t n_hot;             /* parsed hot items (ParamFlowRuleUtil.parseHotItems) */
     const uint64_t *hot_values;
     const int32_t *hot_thresholds;
+    /* ParamFlowRule.clusterMode + ParamFlowClusterConfig (ParamFlowClusterConfig.java:32-44) */
+    int32_t cluster_mode;
+    int32_t cluster_fallback;   /* fallbackToLocalWhenFail, default false */
+    int64_t cluster_flow_id;
+    int32_t cluster_sample_count;
+    int32_t cluster_window_ms;
 } orc_param_rule;
 
 typedef struct orc_degrade_rule {
@@ -57,6 +63,16 @@ int orc_flow_entry_p(orc_flow *f, uint32_t resource, int64_t now, int acquire, i
 /* Entry.exit of a passed entry: stats, param thread counts, circuit breakers. */
 void orc_flow_exit_p(orc_flow *f, uint32_t resource, int64_t now, int64_t rt, int count, int error, int has_param,
                      uint64_t param);
+/* Argument vectors (SGA_EV_ARGS): events flagged 32 carry args[0 .. nargs) as word pairs in pvals:
+ * param = offset << 32 | nargs; pair k = pvals[offset + 2k] (kind << 62 | list length: kind 0 scalar,
+ * 1 null, 2 Collection / array) and pvals[offset + 2k + 1] (the scalar's key, or the offset of the
+ * list's elements in pvals).  Flags bit 4 (PARAM_LIST) keeps its round-2 meaning for args[0]. */
+void orc_flow_replay_args(orc_flow *f, size_t n, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
+                          const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
+                          const uint64_t *pvals, int8_t *decision, int32_t *wait_ms);
+/* the resolved parameter index of resource r's k-th parameter rule (ParamFlowSlot.applyRealParamIdx sets it
+ * on the rule at its first check), or INT32_MIN while unresolved */
+int32_t orc_flow_param_idx(const orc_flow *f, uint32_t r, int k);
 /* circuit breaker state of the k-th breaker of a resource: 0 CLOSED, 1 OPEN, 2 HALF_OPEN */
 int orc_flow_cb_state(orc_flow *f, uint32_t resource, int k);
 

@@ -63,7 +63,11 @@ typedef struct flow_res {
     int64_t *cflow;             /* per rule: ClusterFlowConfig.flowId */
     orc_prule **prule;  /* ParamFlowRuleManager rules of the resource, list order */
     int nprule;
-    orc_lru *pthreads;  /* ParameterMetric.threadCountMap[0] (LRU, capacity 4000) */
+    /* ParameterMetric.threadCountMap: paramIdx -> CacheMap (LRU, capacity 4000), created by
+     * ParameterMetric.initialize(rule) for the rule's (resolved) paramIdx */
+    int32_t *pt_idx;
+    orc_lru **pt_map;
+    int npt;
     orc_cb **cb;        /* DegradeRuleManager circuit breakers, list order */
     int ncb;
 } flow_res;
@@ -89,6 +93,10 @@ struct orc_flow {
      * checks every element): its values, or NULL for a single value */
     const uint64_t *plist;
     uint32_t plist_n;
+    /* the current event's argument vector (SGA_EV_ARGS), or NULL: word pairs, see oracle_ext.h */
+    const uint64_t *args;
+    const uint64_t *args_pvals;
+    uint32_t nargs;
 };
 
 /* helpers implemented in sentinel_oracle.c / oracle_ext.c */

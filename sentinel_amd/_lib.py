@@ -66,7 +66,9 @@ class SgaParamRule(C.Structure):
                 ("control_behavior", C.c_int32), ("max_queueing_time_ms", C.c_int32), ("burst_count", C.c_int32),
                 ("param_idx", C.c_int32), ("duration_in_sec", C.c_int64), ("n_hot", C.c_uint32),
                 ("reserved", C.c_uint32), ("hot_values", C.POINTER(C.c_uint64)),
-                ("hot_thresholds", C.POINTER(C.c_int32))]
+                ("hot_thresholds", C.POINTER(C.c_int32)), ("cluster_mode", C.c_int32),
+                ("cluster_fallback", C.c_int32), ("cluster_flow_id", C.c_int64),
+                ("cluster_sample_count", C.c_int32), ("cluster_window_ms", C.c_int32)]
 
 
 class SgaDegradeRule(C.Structure):

@@ -22,6 +22,7 @@
 //   5 results   : every event derives its TokenResult from its run record.
 #include "cluster.hpp"
 #include "cluster_exact.hpp"
+#include "cparam_exact.hpp"
 
 #include <cstdio>
 #include <cstdlib>
@@ -545,7 +546,17 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
     const int4 *v = reinterpret_cast<const int4 *>(R.r);
     const int4 *cv = reinterpret_cast<const int4 *>(R.r + 2 * P.S + kOccWords + 6 * cj);
     const int4 c01 = cv[0], c23 = cv[1], c45 = cv[2];
-    const SlotOcc occ_ld = R.occ();
+    SlotOcc occ_ld;  // two 16-byte loads (the occupy state is 16-byte aligned in the record)
+    int2 occ_hi;
+    {
+        const int4 *ov = reinterpret_cast<const int4 *>(&R.occ());
+        const int4 o0 = ov[0], o1 = ov[1];
+        occ_ld.occ_pass = i64_lo(o0);
+        occ_ld.occ_preq = i64_hi(o0);
+        occ_ld.has_occ = o1.x;
+        occ_ld.pad = o1.y;
+        occ_hi = make_int2(o1.z, o1.w);  // the record's spare occupy word, stored back unchanged
+    }
     int4 cur;  // the current bucket's pair: taken from the pair loads below (no load of its own)
     int64_t bp = 0, hstart = kAbsent, hpass = 0;
     {
@@ -626,10 +637,25 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
         // WAITING over the same valid buckets (only runs with prioritized blocked requests read it;
         // validity is re-tested per bucket, so any sampleCount works)
         int64_t w0 = c[CEV_WAITING];
+        if (P.S <= kMaxPairs) {
+            // the buckets' WAITING counters (one per 48-byte group), loaded together at clamped
+            // indices; a load under the validity branch would be waited for bucket by bucket
+            int64_t wv[kMaxPairs], st_[kMaxPairs];
+#pragma unroll
+            for (int jj = 0; jj < kMaxPairs; ++jj) {
+                const int j2 = min(jj, P.S - 1);
+                st_[jj] = R.start(j2);
+                wv[jj] = R.cnt(CEV_WAITING, j2);
+            }
+#pragma unroll
+            for (int jj = 0; jj < kMaxPairs; ++jj)
+                if (jj < P.S && jj != cj && st_[jj] != kAbsent && !(t0 - st_[jj] > (int64_t)P.interval)) w0 += wv[jj];
+        } else {
 #pragma nounroll
-        for (int jj = 0; jj < P.S; ++jj) {
-            const int64_t w = R.start(jj);
-            if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) w0 += R.cnt(CEV_WAITING, jj);
+            for (int jj = 0; jj < P.S; ++jj) {
+                const int64_t w = R.start(jj);
+                if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) w0 += R.cnt(CEV_WAITING, jj);
+            }
         }
         if (!occ_loaded) o = occ_ld;
         const double latest = (double)(s0 + (int64_t)f * a) / P.isec;
@@ -661,10 +687,24 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
     c[CEV_BLOCK] += (int64_t)nblk * a;
     c[CEV_BLOCK_REQUEST] += nblk;
     c[CEV_OCCUPIED_BLOCK] += (int64_t)(np_after - cw) * a;
-    if (rot) R.start(cj) = ws;
-#pragma unroll
-    for (int k = 0; k < CEV_N; ++k) R.cnt(k, cj) = c[k];
-    if (occ_dirty) R.occ() = o;
+    // 16-byte stores: the (start, PASS) pair, the six other counters (one 48-byte group), the occupy state
+    {
+        const int64_t stv = rot ? ws : old;
+        auto i4 = [](int64_t lo, int64_t hi) {
+            return make_int4((int)(uint32_t)lo, (int)(uint32_t)((uint64_t)lo >> 32), (int)(uint32_t)hi,
+                             (int)(uint32_t)((uint64_t)hi >> 32));
+        };
+        reinterpret_cast<int4 *>(R.r)[cj] = i4(stv, c[CEV_PASS]);
+        int4 *cg = reinterpret_cast<int4 *>(R.r + 2 * P.S + kOccWords + 6 * cj);
+        cg[0] = i4(c[CEV_WAITING], c[CEV_BLOCK]);
+        cg[1] = i4(c[CEV_PASS_REQUEST], c[CEV_BLOCK_REQUEST]);
+        cg[2] = i4(c[CEV_OCCUPIED_PASS], c[CEV_OCCUPIED_BLOCK]);
+        if (occ_dirty) {
+            int4 *ov = reinterpret_cast<int4 *>(&R.occ());
+            ov[0] = i4(o.occ_pass, o.occ_preq);
+            ov[1] = make_int4(o.has_occ, o.pad, occ_hi.x, occ_hi.y);
+        }
+    }
     ro.s0 = s0;
     ro.thr = thr;
     ro.isec = P.isec;
@@ -2537,86 +2577,7 @@ __global__ void k_lim_init(NsLimiterDev *L) {
 // call, LeapArray.isWindowDeprecated), so keys are independent and each (key, bucket) run is
 // solved in closed form like a ClusterFlowChecker run.  Otherwise the rule's requests are
 // replayed one by one against the rule-level starts (k_pslow).
-constexpr uint32_t kErrKeys = 1, kErrPool = 2;
-
-__device__ __forceinline__ uint32_t prule_lookup(const CParamState &st, int64_t fid) {
-    uint32_t h = (uint32_t)hash_flow_id(fid) & st.hmask;
-    for (uint32_t probe = 0; probe <= st.hmask; ++probe) {
-        const HashEntry e = st.htab[h];
-        if (e.key == fid) return e.slot;
-        if (e.key == 0) break;
-        h = (h + 1) & st.hmask;
-    }
-    return 0xFFFFFFFFu;
-}
-
-// ParamFlowRule.retrieveExclusiveItemCount + calcGlobalThreshold (ClusterParamFlowChecker.java:101-120)
-__device__ __forceinline__ double prule_threshold(const CParamState &st, const PRuleParam &P, int64_t value) {
-    double count = P.count;
-    uint32_t lo = 0, hi = P.n_hot;
-    while (lo < hi) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (st.hot_v[P.hot_off + m] < value) lo = m + 1;
-        else hi = m;
-    }
-    if (lo < P.n_hot && st.hot_v[P.hot_off + lo] == value) count = (double)st.hot_c[P.hot_off + lo];
-    if (P.threshold_type == 1) return count;  // FLOW_THRESHOLD_GLOBAL
-    return count * (double)(P.ns >= 0 ? st.ns_connected[P.ns] : 0);
-}
-
-// value -> vid (insert-only open addressing on the 64-bit value)
-__device__ __forceinline__ uint32_t vid_of(const CParamState &st, int64_t v, bool insert) {
-    if (v == kAbsent) return st.vmask + 1;
-    uint32_t h = (uint32_t)hash_flow_id(v) & st.vmask;
-    for (uint32_t probe = 0; probe <= st.vmask; ++probe) {
-        int64_t cur = st.vtab[h];
-        if (cur == v) return h;
-        if (cur == kAbsent) {
-            if (!insert) return 0xFFFFFFFFu;
-            const unsigned long long prev = atomicCAS((unsigned long long *)&st.vtab[h], (unsigned long long)kAbsent,
-                                                      (unsigned long long)v);
-            if ((int64_t)prev == kAbsent || (int64_t)prev == v) return h;
-        }
-        h = (h + 1) & st.vmask;
-    }
-    return 0xFFFFFFFFu;
-}
-
-// (slot, vid) -> kidx; the inserting lane allocates and initialises the key's record
-__device__ __forceinline__ uint32_t key_of(const CParamState &st, uint32_t slot, uint32_t vid, int64_t value,
-                                           bool insert) {
-    const uint64_t key = ((uint64_t)(slot + 1) << 32) | vid;
-    uint32_t h = (uint32_t)splitmix64(key) & st.kmask;
-    for (uint32_t probe = 0; probe <= st.kmask; ++probe) {
-        const uint64_t cur = st.ktab[h];
-        if (cur == key) return h;
-        if (cur == 0) {
-            if (!insert) return 0xFFFFFFFFu;
-            const unsigned long long prev = atomicCAS((unsigned long long *)&st.ktab[h], 0ull, key);
-            if (prev == 0) {
-                const int S = st.param[slot].S;
-                const uint32_t off = atomicAdd(&st.ctl[0], (uint32_t)(2 * S));
-                if ((uint64_t)off + 2 * S > st.krec_cap) {
-                    atomicOr(&st.ctl[1], kErrPool);
-                    st.koff[h] = 0;
-                } else {
-                    st.koff[h] = off;
-                    for (int j = 0; j < S; ++j) {
-                        st.krec[off + j] = kAbsent;
-                        st.krec[off + S + j] = 0;
-                    }
-                }
-                st.kslot[h] = slot;
-                st.kval[h] = value;
-                return h;
-            }
-            if (prev == key) return h;
-        }
-        h = (h + 1) & st.kmask;
-    }
-    atomicOr(&st.ctl[1], kErrKeys);
-    return 0xFFFFFFFFu;
-}
+// kErrKeys / kErrPool, prule_lookup, prule_threshold, vid_of, key_of: cparam_exact.hpp
 
 // Stage 1a: validation (DefaultTokenService.notValidRequest || params empty -> BAD_REQUEST,
 // :54-56), rule lookup (NO_RULE_EXISTS), sequential-path triggers.
@@ -2701,29 +2662,7 @@ __global__ __launch_bounds__(kThreads) void k_ppath(CParamState st, uint64_t *__
     els[i] = slow;
 }
 
-// ClusterParamMetric over the rule-level starts for one call at t (exact, any time order):
-// currentWindow(t) (LeapArray.java:121-222) then the key's sum over valid buckets.
-__device__ __forceinline__ int pm_window(const CParamState &st, const PRuleParam &P, int64_t t) {
-    const int idx = (int)((t / P.W) % P.S);
-    const int64_t ws = t - t % P.W;
-    int64_t &rs = st.rstart[P.boff + idx];
-    if (rs == kAbsent || ws > rs) {  // newEmptyBucket / resetWindowTo: the bucket's map is empty
-        rs = ws;
-        return idx;
-    }
-    return ws == rs ? idx : -1;  // -1: detached bucket (clock went backwards), adds lost
-}
-
-__device__ __forceinline__ int64_t pm_key_sum(const CParamState &st, const PRuleParam &P, const int64_t *rec,
-                                              int64_t t) {
-    int64_t s = 0;
-    for (int j = 0; j < P.S; ++j) {
-        const int64_t rs = st.rstart[P.boff + j];
-        if (rs == kAbsent || t - rs > (int64_t)P.interval) continue;
-        if (rec[j] == rs) s += rec[P.S + j];
-    }
-    return s;
-}
+// pm_window / pm_key_sum: cparam_exact.hpp
 
 // Sequential path: one lane per rule replays its requests in arrival order.
 __global__ __launch_bounds__(kThreads) void k_pslow(CParamState st, BatchScratch sc, const uint64_t *__restrict__ els,

@@ -70,7 +70,7 @@ struct LimiterPass {
 };
 
 // Per-run decision record written by k_flows, read by k_results (40 B).
-struct RunOut {
+struct alignas(16) RunOut {  // 48 B: three 16-byte stores / loads
     int64_t s0;     // window PASS sum before the run (closed form)
     double thr;     // threshold used
     double isec;    // intervalInSecond

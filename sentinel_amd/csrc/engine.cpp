@@ -1569,6 +1569,26 @@ int sga_load_degrade_rules(sga_engine *e, const sga_degrade_rule *rules, size_t 
     });
 }
 
+// Cluster-mode parameter rules of the local path (ParamFlowChecker.passClusterCheck): the embedded server's
+// parameter path state, refused (-ENOSYS) when a rule's flowId lives in a namespace with a request limiter
+// (the local path does not apply GlobalRequestLimiter)
+static int cluster_param_plumb(Engine &g) {
+    g.flow.cparam_st = sga::CParamState{};
+    if (!g.flow.has_cluster_prules || g.cluster_server != 1) return SGA_OK;
+    if (g.d_pctl.p) g.flow.cparam_st = g.pstate();
+    for (const sga_param_rule &r : g.flow.h_prule_src) {
+        if (!r.cluster_mode) continue;
+        auto it = g.pslot_of.find(r.cluster_flow_id);
+        if (it == g.pslot_of.end()) continue;
+        const sga::PSlotHost &h = g.pslots[it->second];
+        if (h.active && h.ns >= 0 && g.nss[h.ns].has_limit) {
+            g.err = "cluster-mode parameter rule: its namespace has a request limiter";
+            return SGA_ENOSYS;
+        }
+    }
+    return SGA_OK;
+}
+
 int sga_submit_events(sga_engine *e, const uint8_t *kind, const uint32_t *resource, const int64_t *ts,
                       const int32_t *acquire, const uint8_t *flags, const int64_t *rt, const uint64_t *param,
                       size_t n, int8_t *decision, int32_t *wait_ms) {
@@ -1583,6 +1603,7 @@ int sga_submit_events_ex(sga_engine *e, const uint8_t *kind, const uint32_t *res
     return guarded(e, [&](Engine &g) {
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
         g.flow.cluster_on = g.cluster_server == 1 ? 1 : 0;
+        if (const int rc = cluster_param_plumb(g); rc != SGA_OK) return rc;
         if (g.flow.has_cluster_rules) {
             g.flow.cluster_st = g.state();
             const int rc = g.flow.resolve_cluster(
@@ -1615,6 +1636,7 @@ int sga_submit_events_device(sga_engine *e, const uint8_t *d_kind, const uint32_
         if (n > g.cfg.max_batch) return SGA_ERANGE;
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
         g.flow.cluster_on = g.cluster_server == 1 ? 1 : 0;
+        if (const int rc = cluster_param_plumb(g); rc != SGA_OK) return rc;
         if (g.flow.has_cluster_rules) {
             g.flow.cluster_st = g.state();
             const int rc = g.flow.resolve_cluster(

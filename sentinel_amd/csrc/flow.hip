@@ -19,6 +19,7 @@
 // replayed event by event with a device restatement of the whole slot chain.
 #include "flow.hpp"
 #include "cluster_exact.hpp"
+#include "cparam_exact.hpp"
 
 #include <algorithm>
 #include <cstring>
@@ -567,25 +568,104 @@ __device__ __forceinline__ ResMem res_global(const Ctx &c, uint32_t r, const Res
     return ResMem{c.st.node + (size_t)r * kNodeWords, c.st.rules + R.rule_off, c.st.cbs + R.cb_off};
 }
 
-// args[0] of an event: one value, or the elements of a Collection / array (SGA_EV_PARAM_LIST)
+// The event's arguments (SphU.entry(..., Object... args)).  args = [param] (SGA_EV_HAS_PARAM), [] (none),
+// args[0] a Collection / array (SGA_EV_PARAM_LIST: v0 / n0), or a whole argument vector (SGA_EV_ARGS:
+// word pairs at args, kind << 62 | list length, then the key or the list's offset into pvals).
 struct PArgs {
-    const uint64_t *v;
+    const uint64_t *v;  // SGA_EV_PARAM_LIST: args[0]'s elements
     uint32_t n;
+    const uint64_t *args = nullptr;   // SGA_EV_ARGS
+    const uint64_t *pvals = nullptr;
+    uint32_t nargs = 0;
 };
+enum : int { ARG_SCALAR = 0, ARG_NULL = 1, ARG_LIST = 2 };
 
-// ParameterMetric.addThreadCount / decreaseThreadCount over every element (ParameterMetric.java:125-230)
-__device__ void param_threads(const Ctx &c, uint32_t r, const PArgs &pa, int delta) {
-    for (uint32_t q = 0; q < pa.n; ++q) {
-        PEntry *te = ptab_get(c.st.ttab, c.st.tmask, r + 1, pa.v[q], true, c.st.overflow);
-        if (!te) continue;
-        if (delta > 0) {
-            te->a = (te->a == kPAbsent ? 0 : te->a) + 1;
-        } else if (te->a == kPAbsent) {
-            te->a = 0;  // putIfAbsent(value, new AtomicInteger())
-        } else if (--te->a <= 0) {
-            te->a = kPAbsent;  // remove(value)
+__device__ __forceinline__ uint32_t ev_nargs(const PArgs &pa, bool has_param) {
+    return pa.args ? pa.nargs : (has_param ? 1u : 0u);
+}
+
+// args[k]: its kind and values (a scalar is one value); `one` holds a scalar for the legacy forms
+__device__ __forceinline__ int ev_arg(const PArgs &pa, uint32_t k, const uint64_t &param, const uint64_t **vals,
+                                      uint32_t *n) {
+    if (pa.args) {
+        const uint64_t h = pa.args[2 * k];
+        const int kind = (int)(h >> 62);
+        if (kind == ARG_LIST) {
+            *vals = pa.pvals + pa.args[2 * k + 1];
+            *n = (uint32_t)(h & 0xFFFFFFFFu);
+        } else {
+            *vals = &pa.args[2 * k + 1];
+            *n = 1;
+        }
+        return kind;
+    }
+    if (k == 0 && pa.v) {
+        *vals = pa.v;
+        *n = pa.n;
+        return ARG_LIST;
+    }
+    *vals = &param;
+    *n = 1;
+    return ARG_SCALAR;
+}
+
+// thread-count map owner of (resource r, argument index k): resource + 1 for index 0
+__device__ __forceinline__ uint32_t tmap_owner(uint32_t r, uint32_t k) { return (r + 1) | (k << 24); }
+
+// ParameterMetric.addThreadCount / decreaseThreadCount (ParameterMetric.java:125-230): every argument
+// index with a thread-count map, every element of a Collection / array, null arguments skipped
+__device__ void param_threads(const Ctx &c, uint32_t r, const PArgs &pa, bool has_param, const uint64_t &param,
+                              int delta) {
+    const uint64_t mask = c.st.tmapmask ? c.st.tmapmask[r] : 0ull;
+    if (!mask) return;
+    const uint32_t na = min(ev_nargs(pa, has_param), (uint32_t)kMaxParamIdx);
+    for (uint32_t k = 0; k < na; ++k) {
+        if (!((mask >> k) & 1ull)) continue;
+        const uint64_t *vals;
+        uint32_t nv;
+        if (ev_arg(pa, k, param, &vals, &nv) == ARG_NULL) continue;
+        for (uint32_t q = 0; q < nv; ++q) {
+            PEntry *te = ptab_get(c.st.ttab, c.st.tmask, tmap_owner(r, k), vals[q], true, c.st.overflow);
+            if (!te) continue;
+            if (delta > 0) {
+                te->a = (te->a == kPAbsent ? 0 : te->a) + 1;
+            } else if (te->a == kPAbsent) {
+                te->a = 0;  // putIfAbsent(value, new AtomicInteger())
+            } else if (--te->a <= 0) {
+                te->a = kPAbsent;  // remove(value)
+            }
         }
     }
+}
+
+// ParamFlowSlot.applyRealParamIdx (ParamFlowSlot.java:56-66): a negative index is rewritten on the rule
+// at its first check (the reference mutates the rule object), so the first event's arity fixes it
+__device__ __forceinline__ int32_t param_idx_of(ParamRuleDev &p, uint32_t nargs) {
+    if (p.idx_res == kIdxUnresolved) {
+        int32_t idx = p.param_idx;
+        if (idx < 0) idx = (-idx <= (int32_t)nargs) ? (int32_t)nargs + idx : -idx;
+        p.idx_res = idx;
+    }
+    return p.idx_res;
+}
+
+// ParamFlowChecker.passLocalCheck (ParamFlowChecker.java:79-106): every element must pass, in order
+// (elements before a failing one keep their token updates)
+__device__ bool param_local_check(const Ctx &c, uint32_t r, ParamRuleDev &p, int32_t idx, const uint64_t *vals,
+                                  uint32_t nv, int acquire, int64_t t, int64_t *total_wait) {
+    for (uint32_t q = 0; q < nv; ++q) {
+        const uint64_t v = vals[q];
+        int64_t tc = 0;
+        if (p.grade == 0 && idx < kMaxParamIdx) {  // getThreadCount(rule.getParamIdx(), value)
+            PEntry *te = ptab_get(c.st.ttab, c.st.tmask, tmap_owner(r, (uint32_t)idx), v, false, c.st.overflow);
+            tc = (te && te->a != kPAbsent) ? te->a : 0;
+        }
+        int64_t w = 0;
+        const bool ok = c.pre_param ? (w = c.pre_wait, c.pre_param == 1) : param_pass(c, p, v, acquire, t, tc, &w);
+        if (!ok) return false;
+        *total_wait += w;
+    }
+    return true;
 }
 
 __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t t, int acquire, bool prio,
@@ -594,30 +674,33 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
     int64_t *node = m.node;
     *wait_ms = 0;
     int64_t total_wait = 0;
-    if (!pa.v) pa = PArgs{&param, 1u};
-    // ParamFlowSlot (ParamFlowSlot.java:65-92): args = [param] or []
-    const int nargs = has_param ? 1 : 0;
+    // ParamFlowSlot.checkFlow (ParamFlowSlot.java:65-92): args is never null (SphU.entry passes [])
+    const uint32_t nargs = ev_nargs(pa, has_param);
     for (uint32_t k = 0; k < R.n_prules; ++k) {
-        const ParamRuleDev &p = c.st.prules[R.prule_off + k];
-        int idx = p.param_idx;
-        if (idx < 0) idx = (-idx <= nargs) ? nargs + idx : -idx;
-        if (nargs <= idx) continue;
-        // passLocalCheck (ParamFlowChecker.java:79-106): a Collection / array passes when every
-        // element passes, in order (elements before a failing one keep their token updates)
-        for (uint32_t q = 0; q < pa.n; ++q) {
-            const uint64_t v = pa.v[q];
-            int64_t tc = 0;
-            if (idx == 0 && (R.fast & 2u)) {
-                PEntry *te = ptab_get(c.st.ttab, c.st.tmask, r + 1, v, false, c.st.overflow);
-                tc = (te && te->a != kPAbsent) ? te->a : 0;
-            }
-            int64_t w = 0;
-            const bool ok = c.pre_param ? (w = c.pre_wait, c.pre_param == 1) : param_pass(c, p, v, acquire, t, tc, &w);
-            if (!ok) {
-                node_add(c, node, t, MB_BLOCK, acquire);
-                return D_BLOCK_PARAM;
-            }
-            total_wait += w;
+        ParamRuleDev &p = c.st.prules[R.prule_off + k];
+        const int32_t idx = param_idx_of(p, nargs);
+        // ParameterMetricStorage.initParamMetricsFor: the rule's thread-count map exists from now on
+        if (idx < kMaxParamIdx && c.st.tmapmask) c.st.tmapmask[r] |= 1ull << idx;
+        if ((int64_t)nargs <= (int64_t)idx) continue;  // ParamFlowChecker.passCheck: args.length <= paramIdx
+        const uint64_t *vals;
+        uint32_t nv;
+        if (ev_arg(pa, (uint32_t)idx, param, &vals, &nv) == ARG_NULL) continue;  // a null value passes
+        bool ok;
+        if (p.cluster && p.grade == 1) {
+            // passClusterCheck (ParamFlowChecker.java:305-333): requestParamToken(flowId, count,
+            // toCollection(value)) to the embedded server, in event order; OK passes, BLOCKED blocks,
+            // anything else -- or no token service -- falls back (fallbackToLocalOrPass, :335-343)
+            int8_t ts = TRS_FAIL;
+            if (c.st.cluster_on) ts = (int8_t)(cparam_request_exact(c.st.cpst, p.cflow, acquire, vals, nv, t) >> 48);
+            if (ts == TRS_OK) ok = true;
+            else if (ts == TRS_BLOCKED) ok = false;
+            else ok = p.cfallback ? param_local_check(c, r, p, idx, vals, nv, acquire, t, &total_wait) : true;
+        } else {
+            ok = param_local_check(c, r, p, idx, vals, nv, acquire, t, &total_wait);
+        }
+        if (!ok) {
+            node_add(c, node, t, MB_BLOCK, acquire);
+            return D_BLOCK_PARAM;
         }
     }
     // FlowSlot
@@ -658,7 +741,7 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
         }
         if (d == D_PASS_WAIT) {
             node[kNodeThreads] += 1;
-            if (has_param && (R.fast & 2u)) param_threads(c, r, pa, 1);
+            param_threads(c, r, pa, has_param, param, 1);
             *wait_ms = w;
             return D_PASS_WAIT;
         }
@@ -671,7 +754,7 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
     }
     node[kNodeThreads] += 1;
     node_add(c, node, t, MB_PASS, acquire);
-    if (has_param && (R.fast & 2u)) param_threads(c, r, pa, 1);
+    param_threads(c, r, pa, has_param, param, 1);
     *wait_ms = total_wait;
     return D_PASS;
 }
@@ -683,8 +766,7 @@ __device__ void chain_exit(const Ctx &c, uint32_t r, const ResMem &m, int64_t t,
     node_add_rt_success(c, node, t, rt, count);
     node[kNodeThreads] -= 1;
     if (error) node_add(c, node, t, MB_EXC, count);
-    if (!pa.v) pa = PArgs{&param, 1u};
-    if (has_param && (R.fast & 2u)) param_threads(c, r, pa, -1);  // ParameterMetric.decreaseThreadCount
+    param_threads(c, r, pa, has_param, param, -1);  // ParameterMetric.decreaseThreadCount
     for (uint32_t k = 0; k < R.n_cbs; ++k) cb_on_complete(m.cbs[k], t, rt, error);
 }
 
@@ -768,13 +850,26 @@ __device__ __forceinline__ bool gate_is(const uint32_t *g, uint32_t mask, uint32
 __global__ __launch_bounds__(kT) void k_lgate(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ resource,
                                               const int32_t *__restrict__ acquire, const uint8_t *__restrict__ flags,
                                               const uint64_t *__restrict__ param_in, uint32_t n, uint32_t nres,
-                                              int sys_check, uint64_t npvals, uint32_t *gate) {
+                                              int sys_check, uint64_t npvals, uint32_t *gate,
+                                              const uint64_t *__restrict__ pvals) {
     uint32_t g = 0;
     for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
         const uint8_t fl = flags ? flags[i] : 0;
         if (acquire[i] < 0 || kind[i] > 1) g |= kGateBad;
         if ((fl & SGA_EV_INBOUND) && resource[i] < nres) g |= sys_check ? (kGateIn | kGateSeq) : kGateIn;
-        if ((fl & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) {
+        if (fl & SGA_EV_ARGS) {  // the argument vector's word pairs and every list inside npvals
+            const uint64_t pv = param_in ? param_in[i] : 0;
+            const uint64_t off = pv >> 32, na = pv & 0xFFFFFFFFu;
+            if (!pvals || off + 2 * na > npvals) {
+                g |= kGateBad;
+            } else {
+                for (uint64_t k = 0; k < na; ++k) {
+                    const uint64_t h = pvals[off + 2 * k], w = pvals[off + 2 * k + 1];
+                    if ((h >> 62) > 2 || ((h >> 62) == ARG_LIST && w + (h & 0xFFFFFFFFu) > npvals)) g |= kGateBad;
+                }
+            }
+            g |= kGateSeq;
+        } else if ((fl & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) {
             const uint64_t pv = param_in ? param_in[i] : 0;
             if ((pv >> 32) + (pv & 0xFFFFFFFFu) > npvals) g |= kGateBad;
             g |= kGateSeq;
@@ -817,7 +912,13 @@ __global__ void k_lseq(FlowState st, int64_t max_rt, SysDev sys, const uint8_t *
         const bool in = (fl & SGA_EV_INBOUND) != 0, hp = (fl & SGA_EV_HAS_PARAM) != 0;
         const int a = (int)((uint32_t)acquire[i] & 0x7FFFFFFFu);
         PArgs pa{nullptr, 0};
-        if (hp && (fl & SGA_EV_PARAM_LIST) && pvals) pa = PArgs{pvals + (param_in[i] >> 32), (uint32_t)param_in[i]};
+        if ((fl & SGA_EV_ARGS) && pvals) {
+            pa.args = pvals + (param_in[i] >> 32);
+            pa.pvals = pvals;
+            pa.nargs = (uint32_t)param_in[i];
+        } else if (hp && (fl & SGA_EV_PARAM_LIST) && pvals) {
+            pa = PArgs{pvals + (param_in[i] >> 32), (uint32_t)param_in[i]};
+        }
         if (kind[i] == 1) {
             chain_exit(c, r, t, rt_in[i], a, (fl & SGA_EV_ERROR) != 0, hp, param_in[i], pa);
             if (in) entry_node_after_exit(c, t, rt_in[i], a, (fl & SGA_EV_ERROR) != 0);
@@ -1764,6 +1865,8 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
     __shared__ int64_t qrank_ws[kHeavyChunk];  // breaker-only resources: the breaker's stat window start
     __shared__ int64_t sbad[kHeavyChunk], stot[kHeavyChunk];  // CLOSED-breaker scan: window counts after each exit
     __shared__ int bulk_end;                  // breaker-only resources: where the next bulk part starts
+    __shared__ int32_t s_pidx;                // the parameter rule's index in force (applyRealParamIdx)
+    __shared__ uint64_t s_tmask;              // the resource's thread-count maps
     const Ctx c{st, max_rt, nullptr, 0, 0, nullptr};
     constexpr uint64_t kLEmpty = ~0ull;  // a value equal to it bypasses the cache (map path)
     constexpr uint32_t kGiNone = 0xFFFFFFFFu, kGiFail = 0xFFFFFFFEu;
@@ -1791,10 +1894,35 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
             (R.n_prules == 1 && st.prules[R.prule_off].grade == 1) ? &st.prules[R.prule_off] : nullptr;
         // parameter-only resource: per-value lanes own the rule map entry and the thread-count entry
         const bool par = cache_p && R.n_rules == 0 && R.n_cbs == 0;
-        int pidx = cache_p ? cache_p->param_idx : 0;  // ParamFlowSlot index with one argument
-        if (pidx < 0) pidx = (-pidx <= 1) ? 1 + pidx : -pidx;
-        const bool p_applies = pidx < 1;
         const uint32_t jb = sc.run_start[r0], je = sc.run_end[r1 - 1];
+        // ParamFlowSlot.applyRealParamIdx fixes a negative index at the rule's first check: the
+        // resource's first entry (events are in arrival order), with args = [param] or [].  The rule
+        // is checked by every entry, so its thread-count map exists from then on.
+        if (cache_p && threadIdx.x == 0) {
+            ParamRuleDev &pr = st.prules[R.prule_off];
+            int32_t idx = pr.idx_res;
+            uint64_t mask = st.tmapmask[res];
+            if (idx == kIdxUnresolved) {
+                for (uint32_t j = jb; j < je; ++j) {
+                    const Payload q = pay[j];
+                    if (q.idx & F_EXIT) continue;
+                    idx = param_idx_of(pr, (q.idx & F_PARAM) ? 1u : 0u);
+                    break;
+                }
+            }
+            bool any_entry = false;
+            for (uint32_t j = jb; j < je && !any_entry; ++j) any_entry = !(pay[j].idx & F_EXIT);
+            if (any_entry && idx >= 0 && idx < kMaxParamIdx) {
+                mask |= 1ull << idx;
+                st.tmapmask[res] = mask;
+            }
+            s_pidx = idx;
+            s_tmask = mask;
+        }
+        __syncthreads();
+        const int32_t pidx = s_pidx;             // kIdxUnresolved: no entry yet (the rule is not checked)
+        const bool p_applies = pidx == 0;        // events carry args = [param]: index 0 reads it
+        const bool tmap0 = (s_tmask & 1ull) != 0;  // the thread-count map of argument 0 exists
         uint64_t tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         uint64_t tprev = prof ? wall_clock64() : 0;
         auto tick = [&](int ph) {
@@ -2026,7 +2154,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     const uint32_t k = qord[i];
                     const Payload q = qpay[k];
                     PEntry &te = tent[qslot[k]];
-                    const bool tmap = (R.fast & 2u) != 0;  // ParameterMetric thread counts exist
+                    const bool tmap = tmap0;  // ParameterMetric thread counts exist
                     if (q.idx & F_EXIT) {  // ParameterMetric.decreaseThreadCount (chain_exit)
                         if (tmap) {
                             if (te.a == kPAbsent) te.a = 0;
@@ -2517,6 +2645,8 @@ FlowState FlowEngine::state() const {
     s.cst = cluster_st;
     s.cluster_on = cluster_on;
     s.gate = nullptr;
+    s.tmapmask = d_tmapmask.p;
+    s.cpst = cparam_st;
     return s;
 }
 
@@ -2565,7 +2695,10 @@ int FlowEngine::resolve_cluster(const std::function<int32_t(int64_t)> &slot_of_f
 int FlowEngine::set_resources(uint32_t n) {
     if (n == nres) return 0;
     if (nres != 0) return SGA_EINVAL;  // resource table is fixed once set
+    if (n >= (1u << 24)) return SGA_EINVAL;  // thread-count map owners: resource + 1 in 24 bits
     nres = n;
+    d_tmapmask.alloc((size_t)n + 1);
+    SGA_HIP_CHECK(hipMemsetAsync(d_tmapmask.p, 0, ((size_t)n + 1) * 8, stream));
     d_node.alloc(((size_t)n + 1) * kNodeWords);  // + Constants.ENTRY_NODE at index n
     hipLaunchKernelGGL(k_init_nodes, dim3((n + 1 + kT - 1) / kT), dim3(kT), 0, stream, d_node.p, n + 1,
                        (int64_t)cfg.statistic_max_rt);
@@ -2665,28 +2798,64 @@ int FlowEngine::load_flow_rules(const sga_flow_rule *rules, size_t n) {
     return valid;
 }
 
-static bool prule_equal(const sga_param_rule &a, const std::vector<uint64_t> &av, const std::vector<int32_t> &at,
-                        const sga_param_rule &b) {
+// ParamFlowRule.equals (ParamFlowRule.java:192-210) of a loaded rule -- whose paramIdx the slot may have
+// rewritten (applyRealParamIdx mutates the rule object): aidx is the index in force -- and a new rule
+static bool prule_equal(const sga_param_rule &a, int32_t aidx, const std::vector<uint64_t> &av,
+                        const std::vector<int32_t> &at, const sga_param_rule &b) {
     if (a.resource != b.resource || a.grade != b.grade || a.count != b.count || a.control_behavior != b.control_behavior ||
         a.max_queueing_time_ms != b.max_queueing_time_ms || a.burst_count != b.burst_count ||
-        a.param_idx != b.param_idx || a.duration_in_sec != b.duration_in_sec || a.n_hot != b.n_hot)
+        aidx != b.param_idx || a.duration_in_sec != b.duration_in_sec || a.n_hot != b.n_hot ||
+        a.cluster_mode != b.cluster_mode)
+        return false;
+    if (a.cluster_mode && (a.cluster_fallback != b.cluster_fallback || a.cluster_flow_id != b.cluster_flow_id ||
+                           a.cluster_sample_count != b.cluster_sample_count || a.cluster_window_ms != b.cluster_window_ms))
         return false;
     for (uint32_t i = 0; i < b.n_hot; ++i)
         if (av[i] != b.hot_values[i] || at[i] != b.hot_thresholds[i]) return false;
     return true;
 }
 
-// ParamFlowRuleManager.loadRules: rules grouped by resource in list order; ParameterMetric maps
-// are keyed by the rule, so an equal rule keeps its maps (ids), a new one starts empty.
+// ParamFlowRuleUtil.isValidRule + checkCluster (ParamFlowRuleUtil.java:46-69)
+static bool prule_valid(const sga_param_rule &r) {
+    if (!(r.count >= 0 && r.grade >= 0 && r.duration_in_sec > 0 && r.burst_count >= 0 && r.control_behavior >= 0 &&
+          r.max_queueing_time_ms >= 0))
+        return false;
+    if (r.param_idx < -kMaxParamIdx || r.param_idx >= kMaxParamIdx) return false;  // engine limit (header)
+    if (!r.cluster_mode) return true;
+    if (!(r.cluster_sample_count > 0 && r.cluster_window_ms > 0 && r.cluster_window_ms % r.cluster_sample_count == 0))
+        return false;
+    return r.cluster_flow_id > 0;
+}
+
+// ParameterMetric.clearForRule / ParameterMetricStorage.clearParamMetricForResource: the thread-count
+// entries of the cleared (resource, index) maps read as absent, and the maps no longer exist
+__global__ void k_tmap_clear(PEntry *ttab, uint32_t n, const uint64_t *clear, uint32_t nres, uint64_t *tmapmask) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nres) tmapmask[i] &= ~clear[i];
+    if (i >= n) return;
+    const uint32_t o = ttab[i].owner;
+    if (!o) return;
+    const uint32_t r = (o & 0xFFFFFFu) - 1u, k = o >> 24;
+    if (r < nres && ((clear[r] >> k) & 1ull)) ttab[i].a = kPAbsent;
+}
+
+// ParamFlowRuleManager.loadRules (ParamFlowRuleManager.java:101-150): rules grouped by resource in list
+// order; ParameterMetric maps are keyed by the rule, so an equal rule keeps its maps (ids), a new one
+// starts empty.  aggregateAndPrepareParamRules: no rules at all clears every metric; a resource left
+// without rules loses its metric; each removed rule clears its maps and the thread-count map of its index.
 int FlowEngine::load_param_rules(const sga_param_rule *rules, size_t n) {
     if (!nres) return SGA_EINVAL;
+    // the indices the slot resolved on the device (applyRealParamIdx) take part in the equality
+    std::vector<ParamRuleDev> cur(h_prules.size());
+    if (!cur.empty())
+        SGA_HIP_CHECK(hipMemcpyAsync(cur.data(), d_prules.p, cur.size() * sizeof(ParamRuleDev), hipMemcpyDeviceToHost,
+                                     stream));
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
     std::vector<std::vector<size_t>> per(nres);
     for (size_t i = 0; i < n; ++i) {
         const sga_param_rule &r = rules[i];
         if (r.resource >= nres) continue;
-        if (!(r.count >= 0 && r.grade >= 0 && r.duration_in_sec > 0 && r.burst_count >= 0 && r.control_behavior >= 0 &&
-              r.max_queueing_time_ms >= 0))
-            continue;  // ParamFlowRuleUtil.isValidParamRule
+        if (!prule_valid(r)) continue;
         if (r.n_hot && (!r.hot_values || !r.hot_thresholds)) continue;
         per[r.resource].push_back(i);
     }
@@ -2697,6 +2866,9 @@ int FlowEngine::load_param_rules(const sga_param_rule *rules, size_t n) {
     std::vector<uint64_t> hv;
     std::vector<int32_t> ht;
     std::vector<bool> used(h_prule_src.size(), false);
+    auto idx_in_force = [&](size_t k) {
+        return (k < cur.size() && cur[k].idx_res != kIdxUnresolved) ? cur[k].idx_res : h_prule_src[k].param_idx;
+    };
     int valid = 0;
     for (uint32_t res = 0; res < nres; ++res) {
         h_res[res].prule_off = (uint32_t)nr.size();
@@ -2704,10 +2876,12 @@ int FlowEngine::load_param_rules(const sga_param_rule *rules, size_t n) {
         for (size_t i : per[res]) {
             const sga_param_rule &r = rules[i];
             uint32_t id = 0xFFFFFFFFu;
+            int32_t idx_res = kIdxUnresolved;
             for (size_t k = 0; k < h_prule_src.size(); ++k)
-                if (!used[k] && prule_equal(h_prule_src[k], h_prule_hot_v[k], h_prule_hot_t[k], r)) {
+                if (!used[k] && prule_equal(h_prule_src[k], idx_in_force(k), h_prule_hot_v[k], h_prule_hot_t[k], r)) {
                     used[k] = true;
                     id = h_prules[k].id;
+                    if (k < cur.size()) idx_res = cur[k].idx_res;
                     break;
                 }
             if (id == 0xFFFFFFFFu) id = next_prule_id++;
@@ -2722,6 +2896,10 @@ int FlowEngine::load_param_rules(const sga_param_rule *rules, size_t n) {
             d.n_hot = (int32_t)r.n_hot;
             d.hot_off = (uint32_t)hv.size();
             d.id = id;
+            d.idx_res = idx_res;
+            d.cluster = r.cluster_mode ? 1 : 0;
+            d.cfallback = r.cluster_fallback ? 1 : 0;
+            d.cflow = r.cluster_flow_id;
             for (uint32_t h = 0; h < r.n_hot; ++h) {
                 hv.push_back(r.hot_values[h]);
                 ht.push_back(r.hot_thresholds[h]);
@@ -2736,13 +2914,33 @@ int FlowEngine::load_param_rules(const sga_param_rule *rules, size_t n) {
             valid++;
         }
     }
-    for (uint32_t res = 0; res < nres; ++res)
-        if (h_res[res].n_prules) h_res[res].fast |= 2u;  // ParameterMetric created on first rule load
+    // thread-count maps cleared by the reload
+    std::vector<uint64_t> clear(nres, 0);
+    bool any_clear = false;
+    for (size_t k = 0; k < h_prule_src.size(); ++k) {
+        const uint32_t res = h_prule_src[k].resource;
+        if (res >= nres) continue;
+        if (valid == 0 || per[res].empty()) {
+            clear[res] = ~0ull;  // clearParamMetricForResource / every metric cleared
+            any_clear = true;
+        } else if (!used[k]) {
+            const int32_t idx = idx_in_force(k);  // clearForRule: threadCountMap.remove(rule.getParamIdx())
+            if (idx >= 0 && idx < kMaxParamIdx) {
+                clear[res] |= 1ull << idx;
+                any_clear = true;
+            }
+        }
+    }
+    has_cluster_prules = false;
+    for (uint32_t res = 0; res < nres; ++res) {
+        if (h_res[res].n_prules) h_res[res].fast |= 2u;  // the resource has parameter rules
+        else h_res[res].fast &= ~2u;
+    }
+    for (const ParamRuleDev &d : nr) has_cluster_prules |= d.cluster != 0;
     h_prules = nr;
     h_prule_src = nsrc;
     h_prule_hot_v = nhv;
     h_prule_hot_t = nht;
-    SGA_HIP_CHECK(hipStreamSynchronize(stream));
     d_prules.alloc(std::max<size_t>(nr.size(), 1));
     d_hot_v.alloc(std::max<size_t>(hv.size(), 1));
     d_hot_t.alloc(std::max<size_t>(ht.size(), 1));
@@ -2751,6 +2949,16 @@ int FlowEngine::load_param_rules(const sga_param_rule *rules, size_t n) {
     if (!hv.empty()) {
         SGA_HIP_CHECK(hipMemcpyAsync(d_hot_v.p, hv.data(), hv.size() * 8, hipMemcpyHostToDevice, stream));
         SGA_HIP_CHECK(hipMemcpyAsync(d_hot_t.p, ht.data(), ht.size() * 4, hipMemcpyHostToDevice, stream));
+    }
+    if (any_clear) {
+        DevBuf<uint64_t> dc;
+        dc.alloc(nres);
+        SGA_HIP_CHECK(hipMemcpyAsync(dc.p, clear.data(), (size_t)nres * 8, hipMemcpyHostToDevice, stream));
+        const uint32_t tn = (uint32_t)d_ttab.n;
+        const uint32_t m = std::max(tn, nres);
+        hipLaunchKernelGGL(k_tmap_clear, dim3((m + kT - 1) / kT), dim3(kT), 0, stream, d_ttab.p, tn, dc.p, nres,
+                           d_tmapmask.p);
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
     }
     upload_res();
     SGA_HIP_CHECK(hipStreamSynchronize(stream));
@@ -3003,17 +3211,27 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
     if (n == 0) return 0;
     // Collection / array arguments (SGA_EV_PARAM_LIST): the value array goes to the device once;
     // chunks holding such events are replayed in arrival order by one lane (k_lseq)
-    bool any_list = false;
-    for (size_t i = 0; flags && param && i < n && !any_list; ++i) {
-        if ((flags[i] & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) {
-            if (!pvals || (param[i] >> 32) + (param[i] & 0xFFFFFFFFu) > npvals) return SGA_EINVAL;
-            any_list = true;
+    // and whole argument vectors (SGA_EV_ARGS: word pairs, lists inside param_values)
+    auto is_list = [&](size_t i) {
+        return (flags[i] & SGA_EV_ARGS) ||
+               (flags[i] & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM);
+    };
+    auto list_ok = [&](size_t i) {
+        const uint64_t off = param[i] >> 32, na = param[i] & 0xFFFFFFFFu;
+        if (!(flags[i] & SGA_EV_ARGS)) return off + na <= npvals;
+        if (off + 2 * na > npvals) return false;
+        for (uint64_t k = 0; k < na; ++k) {
+            const uint64_t h = pvals[off + 2 * k], w = pvals[off + 2 * k + 1];
+            if ((h >> 62) > 2 || ((h >> 62) == SGA_ARG_LIST && w + (h & 0xFFFFFFFFu) > npvals)) return false;
         }
+        return true;
+    };
+    bool any_list = false;
+    for (size_t i = 0; flags && param && i < n; ++i) {
+        if (!is_list(i)) continue;
+        if (!pvals || !list_ok(i)) return SGA_EINVAL;
+        any_list = true;
     }
-    for (size_t i = 0; any_list && i < n; ++i)
-        if ((flags[i] & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM) &&
-            (param[i] >> 32) + (param[i] & 0xFFFFFFFFu) > npvals)
-            return SGA_EINVAL;
     if (any_list) {
         if (d_pvals.n < std::max<size_t>(npvals, 1)) d_pvals.alloc(std::max<size_t>(npvals, 1));
         if (npvals) SGA_HIP_CHECK(hipMemcpyAsync(d_pvals.p, pvals, npvals * 8, hipMemcpyHostToDevice, stream));
@@ -3060,8 +3278,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         const uint32_t nb = (uint32_t)((m + kT - 1) / kT);
         bool has_in = false, has_list = false;
         for (size_t i = 0; flags && i < m && !has_in; ++i) has_in = (flags[b + i] & SGA_EV_INBOUND) && resource[b + i] < nres;
-        for (size_t i = 0; any_list && i < m && !has_list; ++i)
-            has_list = (flags[b + i] & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM);
+        for (size_t i = 0; any_list && i < m && !has_list; ++i) has_list = is_list(b + i);
         if ((has_in && sys.check) || has_list) {  // SystemSlot / collection arguments: one lane in arrival order
             hipLaunchKernelGGL(k_lseq, dim3(1), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sys, d_kind.p,
                                d_resid.p, d_ts.p, lo, d_acq.p, d_flags.p, d_rt.p, d_param.p, (uint32_t)m, d_dec.p,
@@ -3151,7 +3368,7 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
     const uint32_t nb = (m + kT - 1) / kT;
     const uint32_t gb = std::min<uint32_t>(nb, 1024);
     hipLaunchKernelGGL(k_lgate, dim3(gb), dim3(kT), 0, s, d_kind_in, d_resource, d_acquire, flags_p, param_p, m, nres,
-                       (int)sys.check, (uint64_t)(d_param_values ? n_values : 0), d_gate.p);
+                       (int)sys.check, (uint64_t)(d_param_values ? n_values : 0), d_gate.p, d_param_values);
     FlowState st = state();
     st.gate = d_gate.p;
     FlowScratch gsc = sc;

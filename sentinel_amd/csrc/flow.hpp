@@ -48,7 +48,16 @@ struct ParamRuleDev {
     int32_t param_idx, n_hot;
     int64_t duration;
     uint32_t hot_off, id;   // id: global param-rule id (hash-table key part)
+    // ParamFlowSlot.applyRealParamIdx (ParamFlowSlot.java:56-66) rewrites a negative index on the rule at
+    // its first check: the index in force (kIdxUnresolved until then), kept by equal rules on reload
+    int32_t idx_res;
+    // ParamFlowRule.clusterMode (QPS grade): decided by the embedded server's parameter path
+    int32_t cluster, cfallback;
+    int32_t cpad;
+    int64_t cflow;
 };
+constexpr int32_t kIdxUnresolved = INT32_MIN;
+constexpr int kMaxParamIdx = 64;  // thread-count maps exist for argument indices 0..63
 
 struct CbDev {
     int32_t grade, min_req;
@@ -104,6 +113,11 @@ struct FlowState {
     // device entry (sga_submit_events_device): the chunk's gate word, written by k_lgate; nullptr on
     // the host entry, which chooses the kernels itself
     const uint32_t *gate;
+    // per resource: bit k set once a parameter rule with (resolved) index k was checked -- the
+    // ParameterMetric thread-count map of argument k exists (ParameterMetric.initialize, :113-121)
+    uint64_t *tmapmask;
+    // embedded cluster server's parameter path for cluster-mode parameter rules (ctl null: no rules)
+    CParamState cpst;
 };
 
 struct FlowScratch {
@@ -144,6 +158,9 @@ struct FlowEngine {
     DevBuf<PEntry> d_ptab, d_ttab;
     DevBuf<uint32_t> d_overflow;
     DevBuf<uint32_t> d_keycount;
+    DevBuf<uint64_t> d_tmapmask;  // FlowState::tmapmask
+    CParamState cparam_st{};      // set before each batch (the engine's cluster parameter state)
+    bool has_cluster_prules = false;
     // upper bounds of the keys held by the parameter / thread-count maps (exact after a count);
     // the maps are rehashed into more room before a batch could fill them past a quarter
     size_t pkeys_ub = 0, tkeys_ub = 0;

@@ -42,6 +42,9 @@ EV_PRIORITIZED = 1
 EV_ERROR = 2
 EV_HAS_PARAM = 4
 EV_INBOUND = 8          # EntryType.IN
+EV_PARAM_LIST = 16      # args[0] is a Collection / array (param = offset << 32 | count into param_values)
+EV_ARGS = 32            # the whole argument vector (param = offset << 32 | nargs into param_values)
+ARG_SCALAR, ARG_NULL, ARG_LIST = 0, 1, 2
 ENTRY_NODE = 0xFFFFFFFF  # resource id of Constants.ENTRY_NODE
 TOTAL_IN_RESOURCE_NAME = "__total_inbound_traffic__"  # Constants.TOTAL_IN_RESOURCE_NAME
 KIND_ENTRY = 0
@@ -92,6 +95,28 @@ def param_value(x) -> int:
     raise TypeError(f"unsupported parameter type {type(x).__name__}")
 
 
+def encode_args(args, pvals: List[int]) -> int:
+    """SGA_EV_ARGS encoding of SphU.entry's `Object... args` appended to `pvals` (include/sentinel_amd.h):
+    two words per argument -- kind << 62 | list length, then the scalar's key or the offset of the
+    list's elements in pvals.  None is a null argument; a list / tuple is a Collection or array (its
+    elements in iteration order; ParamFlowChecker.passLocalCheck checks every one).  Returns the event's
+    param word, offset << 32 | nargs."""
+    off = len(pvals)
+    pvals.extend([0] * (2 * len(args)))
+    for k, a in enumerate(args):
+        if a is None:
+            pvals[off + 2 * k] = ARG_NULL << 62
+        elif isinstance(a, (list, tuple)):
+            vals = [param_value(x) for x in a]
+            pvals[off + 2 * k] = (ARG_LIST << 62) | len(vals)
+            pvals[off + 2 * k + 1] = len(pvals)
+            pvals.extend(vals)
+        else:
+            pvals[off + 2 * k] = ARG_SCALAR << 62
+            pvals[off + 2 * k + 1] = param_value(a)
+    return (off << 32) | len(args)
+
+
 @dataclass
 class NodeView:
     pass_qps: float
@@ -135,8 +160,9 @@ class Entry:
     """A passed entry; exit() records RT / success (StatisticSlot.exit) and breaker completion."""
 
     def __init__(self, owner: "LocalSentinel", rid: int, create_ts: int, count: int, param: Optional[int],
-                 wait_ms: int, inbound: bool = False):
+                 wait_ms: int, inbound: bool = False, args=()):
         self._owner = owner
+        self.args = tuple(args)
         self.inbound = inbound
         self.rid = rid
         self.create_timestamp = create_ts
@@ -153,10 +179,12 @@ class Entry:
         if self.exited:
             return
         self.exited = True
-        fl = (EV_ERROR if self.error else 0) | (EV_HAS_PARAM if self.param is not None else 0) | \
-            (EV_INBOUND if self.inbound else 0)
+        # Entry.exit(count, args): ParamFlowStatisticExitCallback decreases the thread counts of the args
+        pvals: List[int] = []
+        word = encode_args(self.args, pvals)
+        fl = (EV_ERROR if self.error else 0) | EV_ARGS | (EV_INBOUND if self.inbound else 0)
         self._owner.submit([KIND_EXIT], [self.rid], [now], [self.count], [fl], [now - self.create_timestamp],
-                           [self.param or 0])
+                           [word], pvals)
 
 
 class LocalSentinel:
@@ -242,14 +270,17 @@ class LocalSentinel:
         """SphU.entry(resource, entryType, batchCount, args); entry_type "IN" marks inbound traffic."""
         rid = self.ids[resource]
         inbound = entry_type == "IN"
-        param = param_value(args[0]) if len(args) > 0 else None
-        fl = (EV_PRIORITIZED if prioritized else 0) | (EV_HAS_PARAM if param is not None else 0) | \
-            (EV_INBOUND if inbound else 0)
-        dec, wait = self.submit([KIND_ENTRY], [rid], [now], [batch_count], [fl], None, [param or 0])
+        # the whole argument vector (SGA_EV_ARGS): ParamFlowSlot indexes args by each rule's paramIdx
+        pvals: List[int] = []
+        word = encode_args(tuple(args), pvals)
+        fl = (EV_PRIORITIZED if prioritized else 0) | EV_ARGS | (EV_INBOUND if inbound else 0)
+        dec, wait = self.submit([KIND_ENTRY], [rid], [now], [batch_count], [fl], None, [word], pvals)
         d = int(dec[0])
         if d in _EXC:
             raise _EXC[d](resource)
-        return Entry(self, rid, now, batch_count, param, int(wait[0]), inbound)
+        param = param_value(args[0]) if len(args) > 0 and args[0] is not None and \
+            not isinstance(args[0], (list, tuple)) else None
+        return Entry(self, rid, now, batch_count, param, int(wait[0]), inbound, args)
 
     def node(self, resource, now: int) -> NodeView:
         """ClusterNode views; resource ENTRY_NODE (or TOTAL_IN_RESOURCE_NAME) is Constants.ENTRY_NODE."""
@@ -350,6 +381,13 @@ class ParamFlowRuleManager:
             a.burst_count = r.burst_count
             a.param_idx = r.param_idx
             a.duration_in_sec = r.duration_in_sec
+            if r.cluster_mode:  # ParamFlowRule.clusterMode + ParamFlowClusterConfig
+                cc = r.cluster_config
+                a.cluster_mode = 1
+                a.cluster_flow_id = cc.flow_id if cc and cc.flow_id is not None else 0
+                a.cluster_fallback = 1 if cc and cc.fallback_to_local_when_fail else 0
+                a.cluster_sample_count = cc.sample_count if cc else 0
+                a.cluster_window_ms = cc.window_interval_ms if cc else 0
             # ParamFlowRuleUtil.parseHotItems: later items with the same value win
             hot: Dict[int, int] = {}
             for it in r.param_flow_item_list:

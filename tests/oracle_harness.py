@@ -52,7 +52,9 @@ class OrcParamRule(C.Structure):
     _fields_ = [("resource", C.c_uint32), ("grade", C.c_int32), ("count", C.c_double),
                 ("control_behavior", C.c_int32), ("max_queueing_time_ms", C.c_int32), ("burst_count", C.c_int32),
                 ("param_idx", C.c_int32), ("duration_in_sec", C.c_int64), ("n_hot", C.c_uint32),
-                ("hot_values", C.POINTER(C.c_uint64)), ("hot_thresholds", C.POINTER(C.c_int32))]
+                ("hot_values", C.POINTER(C.c_uint64)), ("hot_thresholds", C.POINTER(C.c_int32)),
+                ("cluster_mode", C.c_int32), ("cluster_fallback", C.c_int32), ("cluster_flow_id", C.c_int64),
+                ("cluster_sample_count", C.c_int32), ("cluster_window_ms", C.c_int32)]
 
 
 class OrcDegradeRule(C.Structure):
@@ -162,6 +164,8 @@ def lib():
         "orc_flow_cb_state": (C.c_int, [P, U32, C.c_int]),
         "orc_flow_replay_p": (None, [P, C.c_size_t, P, P, P, P, P, P, P, P, P]),
         "orc_flow_replay_pl": (None, [P, C.c_size_t, P, P, P, P, P, P, P, P, P, P]),
+        "orc_flow_replay_args": (None, [P, C.c_size_t, P, P, P, P, P, P, P, P, P, P]),
+        "orc_flow_param_idx": (I32, [P, U32, C.c_int]),
         "orc_prule_new": (P, [C.POINTER(OrcParamRule)]),
         "orc_prule_free": (None, [P]),
         "orc_prule_pass_single": (C.c_int, [P, C.c_uint64, C.c_int, I64, I64, C.POINTER(I64)]),
@@ -223,6 +227,11 @@ def param_rule_struct(r, keep):
     x.burst_count = r.get("burst_count", 0)
     x.param_idx = r.get("param_idx", 0)
     x.duration_in_sec = r.get("duration_in_sec", 1)
+    x.cluster_mode = 1 if r.get("cluster_mode") else 0
+    x.cluster_fallback = 1 if r.get("cluster_fallback") else 0
+    x.cluster_flow_id = r.get("cluster_flow_id", 0)
+    x.cluster_sample_count = r.get("cluster_sample_count", 10)
+    x.cluster_window_ms = r.get("cluster_window_ms", 1000)
     hot = r.get("hot", {})
     x.n_hot = len(hot)
     if hot:

