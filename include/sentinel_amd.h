@@ -336,13 +336,26 @@ int sga_rls_should_rate_limit_device(sga_engine *e, const uint32_t *d_desc_offse
  * (single default context, limitApp "default", strategy DIRECT).
  * ------------------------------------------------------------------------- */
 
-/* decision codes of sga_submit_events */
+/* decision codes of sga_submit_events.  wait_ms of an entry: the sleep of a pass (RateLimiter pacing,
+ * SHOULD_WAIT, parameter throttle) or of SGA_PASS_WAIT; for a block, the block detail the exception
+ * carries: SGA_BLOCK_FLOW the blocking FlowRule's index in the resource's rules (FlowRuleComparator
+ * order), SGA_BLOCK_PARAM the ParamFlowRule's index (list order), SGA_BLOCK_DEGRADE the breaker's
+ * index (DegradeRuleManager list order), SGA_BLOCK_SYSTEM the SystemRule check (SystemBlockException
+ * limitType: 0 qps, 1 thread, 2 rt, 3 load, 4 cpu). */
 #define SGA_PASS 0
 #define SGA_BLOCK_FLOW 1     /* FlowException */
 #define SGA_BLOCK_PARAM 2    /* ParamFlowException */
 #define SGA_BLOCK_DEGRADE 3  /* DegradeException */
 #define SGA_PASS_WAIT 4      /* PriorityWaitException: passed after wait_ms, not counted as pass */
 #define SGA_BLOCK_SYSTEM 5   /* SystemBlockException (SystemSlot, inbound entries only) */
+
+/* event kinds: 0 entry, 1 exit of a passed entry, 2 an entry blocked by a slot outside the engine
+ * (AuthoritySlot or a custom slot ahead of the checks): StatisticSlot's BlockException branch only --
+ * increaseBlockQps on the node and, inbound, on ENTRY_NODE (StatisticSlot.java:121-135).  Kind 2 events
+ * report SGA_PASS and are decided in arrival order by one lane. */
+#define SGA_KIND_ENTRY 0
+#define SGA_KIND_EXIT 1
+#define SGA_KIND_BLOCKED 2
 
 /* event flags */
 #define SGA_EV_PRIORITIZED 1u

@@ -6,6 +6,7 @@
  *      -o libsentinel_amd_jni.so */
 #include <jni.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "sga_jni_glue.h"
 
@@ -147,4 +148,193 @@ JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_loadFlowRules
     (void)cls;
     return sga_load_flow_rules(ENGINE(h), (const sga_flow_rule *)(*env)->GetDirectBufferAddress(env, packed),
                                (size_t)n);
+}
+
+/* ---- Java array access helpers (NULL arrays pass through as NULL) ----------------------------------- */
+#define GET_I(a) ((a) ? (*env)->GetIntArrayElements(env, (a), NULL) : NULL)
+#define GET_L(a) ((a) ? (*env)->GetLongArrayElements(env, (a), NULL) : NULL)
+#define GET_D(a) ((a) ? (*env)->GetDoubleArrayElements(env, (a), NULL) : NULL)
+#define REL_I(a, p) do { if (a) (*env)->ReleaseIntArrayElements(env, (a), (p), JNI_ABORT); } while (0)
+#define REL_L(a, p) do { if (a) (*env)->ReleaseLongArrayElements(env, (a), (p), JNI_ABORT); } while (0)
+#define REL_D(a, p) do { if (a) (*env)->ReleaseDoubleArrayElements(env, (a), (p), JNI_ABORT); } while (0)
+
+/* GpuStatisticSlot.entry with the whole args vector: words = GpuArgs encoding (SGA_EV_ARGS pairs + list
+ * elements), out = int[2] {decision, waitMs} */
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_entryArgs(JNIEnv *env, jclass cls, jlong h,
+                                                                            jint resource, jlong now_ms, jint count,
+                                                                            jint flags, jlongArray words, jint nargs,
+                                                                            jintArray out) {
+    (void)cls;
+    const jsize nw = (*env)->GetArrayLength(env, words);
+    jlong *w = GET_L(words);
+    int32_t o[2] = {0, 0};
+    const int rc = sgaj_entry_args(ENGINE(h), (uint32_t)resource, now_ms, count, (uint32_t)flags, (const uint64_t *)w,
+                                   (uint32_t)nargs, (uint32_t)nw, o);
+    REL_L(words, w);
+    if (rc == SGA_OK) (*env)->SetIntArrayRegion(env, out, 0, 2, (const jint *)o);
+    return rc;
+}
+
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_exitArgs(JNIEnv *env, jclass cls, jlong h,
+                                                                           jint resource, jlong now_ms, jint count,
+                                                                           jint flags, jlong rt_ms, jlongArray words,
+                                                                           jint nargs) {
+    (void)cls;
+    const jsize nw = (*env)->GetArrayLength(env, words);
+    jlong *w = GET_L(words);
+    const int rc = sgaj_exit_args(ENGINE(h), (uint32_t)resource, now_ms, count, (uint32_t)flags, rt_ms,
+                                  (const uint64_t *)w, (uint32_t)nargs, (uint32_t)nw);
+    REL_L(words, w);
+    return rc;
+}
+
+/* a BlockException thrown by a slot the engine does not run (AuthoritySlot): counted as a block */
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_blocked(JNIEnv *env, jclass cls, jlong h,
+                                                                          jint resource, jlong now_ms, jint count,
+                                                                          jint flags) {
+    (void)env;
+    (void)cls;
+    return sgaj_blocked(ENGINE(h), (uint32_t)resource, now_ms, count, (uint32_t)flags);
+}
+
+/* ParamFlowRuleManager.loadRules: parallel arrays (GpuRuleSync.pushParamRules) */
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_loadParamRules(
+    JNIEnv *env, jclass cls, jlong h, jintArray resource, jintArray grade, jdoubleArray count, jintArray behavior,
+    jintArray max_queue, jintArray burst, jintArray param_idx, jlongArray duration, jintArray hot_off,
+    jlongArray hot_values, jintArray hot_counts, jintArray cluster_mode, jintArray cluster_fallback,
+    jlongArray cluster_flow_id, jintArray cluster_sample, jintArray cluster_window) {
+    (void)cls;
+    const jsize n = (*env)->GetArrayLength(env, resource);
+    jint *r = GET_I(resource), *g = GET_I(grade), *b = GET_I(behavior), *mq = GET_I(max_queue), *bu = GET_I(burst);
+    jint *pi = GET_I(param_idx), *ho = GET_I(hot_off), *hc = GET_I(hot_counts), *cm = GET_I(cluster_mode);
+    jint *cf = GET_I(cluster_fallback), *cs = GET_I(cluster_sample), *cw = GET_I(cluster_window);
+    jdouble *c = GET_D(count);
+    jlong *du = GET_L(duration), *hv = GET_L(hot_values), *cid = GET_L(cluster_flow_id);
+    const int rc = sgaj_load_param_rules(ENGINE(h), (size_t)n, (const uint32_t *)r, (const int32_t *)g,
+                                         (const double *)c, (const int32_t *)b, (const int32_t *)mq,
+                                         (const int32_t *)bu, (const int32_t *)pi, (const int64_t *)du,
+                                         (const uint32_t *)ho, (const int64_t *)hv, (const int32_t *)hc,
+                                         (const int32_t *)cm, (const int32_t *)cf, (const int64_t *)cid,
+                                         (const int32_t *)cs, (const int32_t *)cw);
+    REL_I(resource, r); REL_I(grade, g); REL_I(behavior, b); REL_I(max_queue, mq); REL_I(burst, bu);
+    REL_I(param_idx, pi); REL_I(hot_off, ho); REL_I(hot_counts, hc); REL_I(cluster_mode, cm);
+    REL_I(cluster_fallback, cf); REL_I(cluster_sample, cs); REL_I(cluster_window, cw);
+    REL_D(count, c);
+    REL_L(duration, du); REL_L(hot_values, hv); REL_L(cluster_flow_id, cid);
+    return rc;
+}
+
+/* DegradeRuleManager.loadRules */
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_loadDegradeRules(
+    JNIEnv *env, jclass cls, jlong h, jintArray resource, jintArray grade, jdoubleArray count, jintArray time_window,
+    jintArray min_request, jdoubleArray slow_ratio, jintArray stat_interval) {
+    (void)cls;
+    const jsize n = (*env)->GetArrayLength(env, resource);
+    jint *r = GET_I(resource), *g = GET_I(grade), *tw = GET_I(time_window), *mr = GET_I(min_request);
+    jint *si = GET_I(stat_interval);
+    jdouble *c = GET_D(count), *sr = GET_D(slow_ratio);
+    const int rc = sgaj_load_degrade_rules(ENGINE(h), (size_t)n, (const uint32_t *)r, (const int32_t *)g,
+                                           (const double *)c, (const int32_t *)tw, (const int32_t *)mr,
+                                           (const double *)sr, (const int32_t *)si);
+    REL_I(resource, r); REL_I(grade, g); REL_I(time_window, tw); REL_I(min_request, mr); REL_I(stat_interval, si);
+    REL_D(count, c); REL_D(slow_ratio, sr);
+    return rc;
+}
+
+/* SystemRuleManager.loadRules */
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_loadSystemRules(
+    JNIEnv *env, jclass cls, jlong h, jdoubleArray load, jdoubleArray cpu, jdoubleArray qps, jlongArray avg_rt,
+    jlongArray max_thread) {
+    (void)cls;
+    const jsize n = (*env)->GetArrayLength(env, load);
+    jdouble *l = GET_D(load), *c = GET_D(cpu), *q = GET_D(qps);
+    jlong *a = GET_L(avg_rt), *m = GET_L(max_thread);
+    const int rc = sgaj_load_system_rules(ENGINE(h), (size_t)n, (const double *)l, (const double *)c,
+                                          (const double *)q, (const int64_t *)a, (const int64_t *)m);
+    REL_D(load, l); REL_D(cpu, c); REL_D(qps, q); REL_L(avg_rt, a); REL_L(max_thread, m);
+    return rc;
+}
+
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_setSystemStatus(JNIEnv *env, jclass cls,
+                                                                                  jlong h, jdouble load,
+                                                                                  jdouble cpu) {
+    (void)env;
+    (void)cls;
+    return sgaj_set_system_status(ENGINE(h), load, cpu);
+}
+
+/* ClusterParamFlowRuleManager.loadRules(namespace, rules) */
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_loadClusterParamRules(
+    JNIEnv *env, jclass cls, jlong h, jstring ns, jlongArray flow_id, jdoubleArray count, jintArray threshold_type,
+    jintArray sample_count, jintArray window_ms, jintArray hot_off, jlongArray hot_values, jintArray hot_counts) {
+    (void)cls;
+    const jsize n = (*env)->GetArrayLength(env, flow_id);
+    const char *nss = (*env)->GetStringUTFChars(env, ns, NULL);
+    jlong *f = GET_L(flow_id), *hv = GET_L(hot_values);
+    jdouble *c = GET_D(count);
+    jint *tt = GET_I(threshold_type), *sc = GET_I(sample_count), *w = GET_I(window_ms), *ho = GET_I(hot_off);
+    jint *hc = GET_I(hot_counts);
+    const int rc = sgaj_load_cluster_param_rules(ENGINE(h), nss, (size_t)n, (const int64_t *)f, (const double *)c,
+                                                 (const int32_t *)tt, (const int32_t *)sc, (const int32_t *)w,
+                                                 (const uint32_t *)ho, (const int64_t *)hv, (const int32_t *)hc);
+    REL_L(flow_id, f); REL_L(hot_values, hv); REL_D(count, c);
+    REL_I(threshold_type, tt); REL_I(sample_count, sc); REL_I(window_ms, w); REL_I(hot_off, ho); REL_I(hot_counts, hc);
+    (*env)->ReleaseStringUTFChars(env, ns, nss);
+    return rc;
+}
+
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_setConnectedCount(JNIEnv *env, jclass cls,
+                                                                                    jlong h, jstring ns, jint n) {
+    (void)cls;
+    const char *nss = (*env)->GetStringUTFChars(env, ns, NULL);
+    const int rc = sgaj_set_connected_count(ENGINE(h), nss, n);
+    (*env)->ReleaseStringUTFChars(env, ns, nss);
+    return rc;
+}
+
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_setNamespaceLimit(JNIEnv *env, jclass cls,
+                                                                                    jlong h, jstring ns,
+                                                                                    jdouble qps) {
+    (void)cls;
+    const char *nss = (*env)->GetStringUTFChars(env, ns, NULL);
+    const int rc = sgaj_set_namespace_limit(ENGINE(h), nss, qps);
+    (*env)->ReleaseStringUTFChars(env, ns, nss);
+    return rc;
+}
+
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_setClusterServer(JNIEnv *env, jclass cls,
+                                                                                   jlong h, jint mode) {
+    (void)env;
+    (void)cls;
+    return sgaj_set_cluster_server(ENGINE(h), mode);
+}
+
+/* GpuNode: d8 / l6 as sgaj_query_node */
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_queryNode(JNIEnv *env, jclass cls, jlong h,
+                                                                            jint resource, jlong now_ms,
+                                                                            jdoubleArray d8, jlongArray l6) {
+    (void)cls;
+    double d[8];
+    int64_t l[6];
+    const int rc = sgaj_query_node(ENGINE(h), (uint32_t)resource, now_ms, d, l);
+    if (rc == SGA_OK) {
+        (*env)->SetDoubleArrayRegion(env, d8, 0, 8, (const jdouble *)d);
+        (*env)->SetLongArrayRegion(env, l6, 0, 6, (const jlong *)l);
+    }
+    return rc;
+}
+
+/* GpuMetricTimerListener: rows of 8 longs into `rows` (length 8 * cap); returns the row count or an error */
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_metricsSnapshot(JNIEnv *env, jclass cls, jlong h,
+                                                                                  jlong now_ms, jlongArray rows) {
+    (void)cls;
+    const jsize len = (*env)->GetArrayLength(env, rows);
+    const size_t cap = (size_t)len / 8;
+    int64_t *buf = (int64_t *)malloc((cap ? cap : 1) * 8 * sizeof(int64_t));
+    if (!buf) return SGA_ENOMEM;
+    size_t n = 0;
+    const int rc = sgaj_metrics_snapshot(ENGINE(h), now_ms, buf, cap, &n);
+    if (n) (*env)->SetLongArrayRegion(env, rows, 0, (jsize)(8 * n), (const jlong *)buf);
+    free(buf);
+    return rc == SGA_OK ? (jint)n : rc;
 }

@@ -1,5 +1,7 @@
 package com.alibaba.csp.sentinel.gpu;
 
+import java.util.ArrayList;
+import java.util.List;
 import java.util.Map;
 import java.util.concurrent.ConcurrentHashMap;
 import java.util.concurrent.TimeUnit;
@@ -9,97 +11,136 @@ import com.alibaba.csp.sentinel.context.Context;
 import com.alibaba.csp.sentinel.node.DefaultNode;
 import com.alibaba.csp.sentinel.slotchain.AbstractLinkedProcessorSlot;
 import com.alibaba.csp.sentinel.slotchain.ResourceWrapper;
+import com.alibaba.csp.sentinel.slots.block.BlockException;
+import com.alibaba.csp.sentinel.slots.block.RuleConstant;
 import com.alibaba.csp.sentinel.slots.block.degrade.DegradeException;
+import com.alibaba.csp.sentinel.slots.block.degrade.DegradeRule;
 import com.alibaba.csp.sentinel.slots.block.flow.FlowException;
+import com.alibaba.csp.sentinel.slots.block.flow.FlowRule;
 import com.alibaba.csp.sentinel.slots.block.flow.param.ParamFlowException;
+import com.alibaba.csp.sentinel.slots.block.flow.param.ParamFlowRule;
 import com.alibaba.csp.sentinel.slots.system.SystemBlockException;
 import com.alibaba.csp.sentinel.util.TimeUtil;
 
 /**
- * One slot in place of StatisticSlot, ParamFlowSlot, FlowSlot, DegradeSlot and SystemSlot
- * (ProcessorSlot.java:41-76): entry and exit become events of the engine's local path
- * (sga_submit_events), which keeps the nodes' statistics, the controllers, the parameter maps and the
- * breakers on the GPU and answers the decision the reference's slots would have thrown.
+ * One slot in place of StatisticSlot, SystemSlot, ParamFlowSlot, FlowSlot and DegradeSlot (ProcessorSlot.java:41-76).
+ * As StatisticSlot (StatisticSlot.java:64-145) it first fires the rest of the chain -- AuthoritySlot and any
+ * custom slot -- and then decides: the engine's local path (sga_submit_events) runs SystemSlot, ParamFlowSlot,
+ * FlowSlot and DegradeSlot and the StatisticSlot accounting on the GPU in one event.  A BlockException from the
+ * fired slots is counted as a block (event kind 2) and rethrown; an engine block becomes the reference's
+ * exception with the blocking rule ({@link GpuRuleSync} keeps the per-resource lists in engine order), and its
+ * block error is set on the entry so that exit records nothing.  Passes sleep the engine's wait (RateLimiter
+ * pacing, cluster SHOULD_WAIT, parameter throttle) as the reference controllers do before returning.
  */
 public class GpuStatisticSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
 
-    /** sga_submit_events flags (include/sentinel_amd.h SGA_EV_*). */
-    static final int EV_PRIORITIZED = 1, EV_ERROR = 2, EV_HAS_PARAM = 4, EV_INBOUND = 8;
-
     private static final Map<String, Integer> RESOURCE_IDS = new ConcurrentHashMap<>();
+    private static final List<String> NAMES = new ArrayList<>();
     private final long engine = GpuEngine.get();
 
-    /** Dense resource id of a resource name (like CtSph's chain map); grows the engine's table. */
+    /** Dense resource id of a resource name (like CtSph's chain map); at most csp.sentinel.gpu.maxResources. */
     static int resourceId(String name) {
         Integer id = RESOURCE_IDS.get(name);
         if (id != null) {
             return id;
         }
-        synchronized (RESOURCE_IDS) {
+        synchronized (NAMES) {
             id = RESOURCE_IDS.get(name);
             if (id == null) {
-                id = RESOURCE_IDS.size();
+                if (NAMES.size() >= GpuEngine.MAX_RESOURCES) {
+                    throw new IllegalStateException("more than " + GpuEngine.MAX_RESOURCES + " resources "
+                                                    + "(csp.sentinel.gpu.maxResources)");
+                }
+                id = NAMES.size();
+                NAMES.add(name);
                 RESOURCE_IDS.put(name, id);
-                GpuEngine.setResources(GpuEngine.get(), RESOURCE_IDS.size());
             }
             return id;
         }
     }
 
-    @Override
-    public void entry(Context context, ResourceWrapper resourceWrapper, DefaultNode node, int count,
-                      boolean prioritized, Object... args) throws Throwable {
-        int flags = prioritized ? EV_PRIORITIZED : 0;
-        long param = 0;
-        if (args != null && args.length > 0 && args[0] != null) {  // ParamFlowRule.paramIdx 0
-            flags |= EV_HAS_PARAM;
-            param = GpuTokenService.paramKey(args[0]);
+    /** The name of a dense resource id (metric rows), or null. */
+    static String resourceName(int id) {
+        synchronized (NAMES) {
+            return id >= 0 && id < NAMES.size() ? NAMES.get(id) : null;
         }
-        if (resourceWrapper.getEntryType() == EntryType.IN) {
-            flags |= EV_INBOUND;
-        }
-        String name = resourceWrapper.getName();
-        int[] o = new int[2];
-        int rc = GpuEngine.entry(engine, resourceId(name), TimeUtil.currentTimeMillis(), count, flags, param, o);
-        if (rc != GpuEngine.OK) {
-            throw new IllegalStateException("sga_submit_events: " + rc + " " + GpuEngine.lastError(engine));
-        }
-        switch (o[0]) {
-            case 0:
-                break;
-            case 1:
-                throw new FlowException(context.getOrigin());
-            case 2:
-                throw new ParamFlowException(name, String.valueOf(args[0]));
-            case 3:
-                throw new DegradeException(context.getOrigin());
-            case 4:  // DefaultController.canPass slept and threw PriorityWaitException, which StatisticSlot
-                     // counts as passed (the engine has counted it); the slots after FlowSlot do not run
-                TimeUnit.MILLISECONDS.sleep(o[1]);
-                return;
-            case 5:
-                throw new SystemBlockException(name, "gpu");
-            default:
-                throw new IllegalStateException("unknown decision " + o[0]);
-        }
-        fireEntry(context, resourceWrapper, node, count, prioritized, args);
+    }
+
+    private static int flags(ResourceWrapper r, boolean prioritized) {
+        return (prioritized ? GpuEngine.EV_PRIORITIZED : 0) | (r.getEntryType() == EntryType.IN ? GpuEngine.EV_INBOUND : 0);
     }
 
     @Override
+    public void entry(Context context, ResourceWrapper resourceWrapper, DefaultNode node, int count,
+                      boolean prioritized, Object... args) throws Throwable {
+        final String name = resourceWrapper.getName();
+        final int rid = resourceId(name);
+        final int fl = flags(resourceWrapper, prioritized);
+        try {
+            // StatisticSlot.java:71: the slots after this one run first (AuthoritySlot, custom slots)
+            fireEntry(context, resourceWrapper, node, count, prioritized, args);
+        } catch (BlockException e) {
+            // StatisticSlot.java:121-135: the block is counted (node + ENTRY_NODE when inbound)
+            context.getCurEntry().setBlockError(e);
+            GpuEngine.blocked(engine, rid, TimeUtil.currentTimeMillis(), count, fl);
+            throw e;
+        }
+        long[] words = GpuArgs.encode(args);
+        int[] o = new int[2];
+        int rc = GpuEngine.entryArgs(engine, rid, TimeUtil.currentTimeMillis(), count, fl, words,
+                                     args == null ? 0 : args.length, o);
+        if (rc != GpuEngine.OK) {
+            throw new IllegalStateException("sga_submit_events: " + rc + " " + GpuEngine.lastError(engine));
+        }
+        BlockException block;
+        switch (o[0]) {
+            case 0:  // passed; RateLimiter / SHOULD_WAIT / throttle waits sleep like the controllers
+            case 4:  // PriorityWaitException: DefaultController slept; counted as a thread, not a pass
+                if (o[1] > 0) {
+                    TimeUnit.MILLISECONDS.sleep(o[1]);
+                }
+                return;
+            case 1: {
+                FlowRule r = GpuRuleSync.flowRule(name, o[1]);
+                block = new FlowException(r != null ? r.getLimitApp() : RuleConstant.LIMIT_APP_DEFAULT, r);
+                break;
+            }
+            case 2: {
+                ParamFlowRule r = GpuRuleSync.paramRule(name, o[1]);
+                Object v = null;
+                if (r != null && args != null && r.getParamIdx() != null && r.getParamIdx() >= 0
+                    && r.getParamIdx() < args.length) {
+                    v = args[r.getParamIdx()];
+                }
+                block = new ParamFlowException(name, v == null ? "" : String.valueOf(v), r);
+                break;
+            }
+            case 3: {
+                DegradeRule r = GpuRuleSync.degradeRule(name, o[1]);
+                block = new DegradeException(r != null ? r.getLimitApp() : RuleConstant.LIMIT_APP_DEFAULT, r);
+                break;
+            }
+            case 5:
+                block = new SystemBlockException(name, SYSTEM_LIMIT_TYPES[Math.min(Math.max(o[1], 0), 4)]);
+                break;
+            default:
+                throw new IllegalStateException("unknown decision " + o[0]);
+        }
+        context.getCurEntry().setBlockError(block);  // exit then records nothing (StatisticSlot.java:150)
+        throw block;
+    }
+
+    /** SystemRuleManager.checkSystem's limitType of each check (block detail 0..4). */
+    private static final String[] SYSTEM_LIMIT_TYPES = {"qps", "thread", "rt", "load", "cpu"};
+
+    @Override
     public void exit(Context context, ResourceWrapper resourceWrapper, int count, Object... args) {
-        long now = TimeUtil.currentTimeMillis();
-        long rt = now - context.getCurEntry().getCreateTimestamp();
-        int flags = context.getCurEntry().getError() != null ? EV_ERROR : 0;
-        long param = 0;
-        if (args != null && args.length > 0 && args[0] != null) {
-            flags |= EV_HAS_PARAM;
-            param = GpuTokenService.paramKey(args[0]);
-        }
-        if (resourceWrapper.getEntryType() == EntryType.IN) {
-            flags |= EV_INBOUND;
-        }
-        if (context.getCurEntry().getBlockError() == null) {  // only entries that passed exit
-            GpuEngine.exit(engine, resourceId(resourceWrapper.getName()), now, count, flags, rt, param);
+        if (context.getCurEntry().getBlockError() == null) {  // StatisticSlot.exit: only entries that passed
+            long now = TimeUtil.currentTimeMillis();
+            long rt = now - context.getCurEntry().getCreateTimestamp();
+            int fl = flags(resourceWrapper, false) | (context.getCurEntry().getError() != null ? GpuEngine.EV_ERROR : 0);
+            GpuEngine.exitArgs(engine, resourceId(resourceWrapper.getName()), now, count, fl, rt,
+                               GpuArgs.encode(args), args == null ? 0 : args.length);
         }
         fireExit(context, resourceWrapper, count, args);
     }

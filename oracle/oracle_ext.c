@@ -794,6 +794,7 @@ int orc_flow_entry_p(orc_flow *f, uint32_t resource, int64_t now, int acquire, i
         }
         if (!ok) {
             orc_node_increase_block_qps(fr->node, now, acquire);
+            *wait_ms = k; /* block detail: the ParamFlowRule's index in the resource's list */
             return ORC_BLOCK_PARAM;
         }
     }
@@ -802,6 +803,7 @@ int orc_flow_entry_p(orc_flow *f, uint32_t resource, int64_t now, int acquire, i
     int d = orc_flow_rule_check(f, resource, now, acquire, prioritized, &w);
     if (d == ORC_BLOCK_FLOW) {
         orc_node_increase_block_qps(fr->node, now, acquire);
+        *wait_ms = w; /* block detail: the blocking FlowRule's index */
         return ORC_BLOCK_FLOW;
     }
     if (d == ORC_PASS_WAIT) { /* PriorityWaitException: thread++ and entry callbacks only */
@@ -824,6 +826,7 @@ int orc_flow_entry_p(orc_flow *f, uint32_t resource, int64_t now, int acquire, i
             for (int q = 0; q < k && q < 64; q++)
                 if (half_open_here[q] && fr->cb[q]->state == CB_HALF_OPEN) fr->cb[q]->state = CB_OPEN;
             orc_node_increase_block_qps(fr->node, now, acquire);
+            *wait_ms = k; /* block detail: the breaker's index */
             return ORC_BLOCK_DEGRADE;
         }
     }
@@ -906,19 +909,20 @@ void orc_flow_set_system_status(orc_flow *f, double avg_load, double cpu_usage) 
     f->sys.cur_cpu = cpu_usage;
 }
 
-/* SystemRuleManager.checkSystem + checkBbr for an inbound entry, SystemRuleManager.java:298-353 */
-static int system_blocks(orc_flow *f, int64_t now, int count) {
-    if (!f->sys.check) return 0;
+/* SystemRuleManager.checkSystem + checkBbr for an inbound entry, SystemRuleManager.java:298-353: the check
+ * that throws (SystemBlockException limitType 0 "qps", 1 "thread", 2 "rt", 3 "load", 4 "cpu") or -1 */
+static int system_block_type(orc_flow *f, int64_t now, int count) {
+    if (!f->sys.check) return -1;
     orc_node *e = f->entry;
-    if (orc_node_pass_qps(e, now) + count > f->sys.qps) return 1;
+    if (orc_node_pass_qps(e, now) + count > f->sys.qps) return 0;
     const int32_t thr = orc_node_cur_thread_num(e);
     if ((int64_t)thr > f->sys.max_thread) return 1;
-    if (orc_node_avg_rt(e, now) > (double)f->sys.max_rt) return 1;
+    if (orc_node_avg_rt(e, now) > (double)f->sys.max_rt) return 2;
     if (f->sys.load_set && f->sys.cur_load > f->sys.load) {
-        if (thr > 1 && thr > orc_node_max_success_qps(e, now) * orc_node_min_rt(e, now) / 1000) return 1;
+        if (thr > 1 && thr > orc_node_max_success_qps(e, now) * orc_node_min_rt(e, now) / 1000) return 3;
     }
-    if (f->sys.cpu_set && f->sys.cur_cpu > f->sys.cpu) return 1;
-    return 0;
+    if (f->sys.cpu_set && f->sys.cur_cpu > f->sys.cpu) return 4;
+    return -1;
 }
 
 /* The slot chain for one entry with its EntryType: SystemSlot before ParamFlowSlot / FlowSlot /
@@ -930,9 +934,11 @@ int orc_flow_entry_x(orc_flow *f, uint32_t resource, int64_t now, int acquire, i
     *wait_ms = 0;
     if (resource >= f->n) return ORC_PASS;
     int d;
-    if (inbound && system_blocks(f, now, acquire)) {
+    const int sb = inbound ? system_block_type(f, now, acquire) : -1;
+    if (sb >= 0) {
         orc_node_increase_block_qps(f->res[resource].node, now, acquire);
         d = ORC_BLOCK_SYSTEM;
+        *wait_ms = sb; /* block detail: the SystemRule check */
     } else {
         d = orc_flow_entry_p(f, resource, now, acquire, prioritized, has_param, param, wait_ms);
     }
@@ -1014,6 +1020,15 @@ void orc_flow_replay_p(orc_flow *f, size_t n, const uint8_t *kind, const uint32_
         const int hp = (fl & 4) != 0 || (fl & 32) != 0;
         const int in = (fl & 8) != 0;
         const uint64_t pv = param ? param[i] : 0;
+        if (kind && kind[i] == 2) { /* StatisticSlot: a BlockException thrown by a slot outside the engine */
+            if (resource[i] < f->n) {
+                orc_node_increase_block_qps(f->res[resource[i]].node, ts[i], acquire[i]);
+                if (in) orc_node_increase_block_qps(f->entry, ts[i], acquire[i]);
+            }
+            if (decision) decision[i] = ORC_PASS;
+            if (wait_ms) wait_ms[i] = 0;
+            continue;
+        }
         if (kind && kind[i] == 1) {
             orc_flow_exit_x(f, resource[i], ts[i], rt ? rt[i] : 0, acquire[i], (fl & 2) != 0, hp, pv, in);
             if (decision) decision[i] = ORC_PASS;

@@ -694,12 +694,15 @@ int orc_flow_rule_check(orc_flow *f, uint32_t resource, int64_t now, int acquire
             }
             if (status == 0) continue;                      /* OK */
             if (status == 2) { total_wait += tw; continue; } /* SHOULD_WAIT: sleep, then pass */
-            if (status == 1) return ORC_BLOCK_FLOW;         /* BLOCKED */
-            if (status != 3 && status != -4 && status != -1 && status != -2) return ORC_BLOCK_FLOW; /* default */
+            if (status == 1) { *wait_ms = k; return ORC_BLOCK_FLOW; } /* BLOCKED (block detail: rule index) */
+            if (status != 3 && status != -4 && status != -1 && status != -2) { *wait_ms = k; return ORC_BLOCK_FLOW; }
             if (!fr->cfallback[k]) continue;                /* fallbackToLocalOrPass: pass */
         }
         int d = orc_ctrl_can_pass(fr->ctrl[k], fr->node, now, acquire, prioritized, &w);
-        if (d == ORC_BLOCK_FLOW) return ORC_BLOCK_FLOW;
+        if (d == ORC_BLOCK_FLOW) {
+            *wait_ms = k; /* block detail: the rule's index in FlowRuleComparator order */
+            return ORC_BLOCK_FLOW;
+        }
         if (d == ORC_PASS_WAIT) {
             *wait_ms = w;
             return ORC_PASS_WAIT;

@@ -484,7 +484,7 @@ __device__ void cb_stat_at(CbDev &b, int64_t ws) {  // LeapArray(1, statInterval
 
 // DegradeSlot.entry over the resource's breakers (DegradeSlot.java:52-66): tryPass of each in order;
 // a breaker moved to HALF_OPEN goes back to OPEN when a later one blocks (whenTerminate, blockError)
-__device__ bool degrade_pass(CbDev *cbs, uint32_t n, int64_t t) {
+__device__ int degrade_block_index(CbDev *cbs, uint32_t n, int64_t t) {  // -1: every breaker passes
     uint64_t half_mask = 0;
     for (uint32_t k = 0; k < n; ++k) {
         CbDev &b = cbs[k];
@@ -500,10 +500,13 @@ __device__ bool degrade_pass(CbDev *cbs, uint32_t n, int64_t t) {
                 CbDev &bq = cbs[q];
                 if (((half_mask >> q) & 1) && bq.state == 2) bq.state = 1;
             }
-            return false;
+            return (int)k;
         }
     }
-    return true;
+    return -1;
+}
+__device__ __forceinline__ bool degrade_pass(CbDev *cbs, uint32_t n, int64_t t) {
+    return degrade_block_index(cbs, n, t) < 0;
 }
 
 // handleStateChangeWhenThresholdExceeded of a CLOSED breaker over its current window's counts
@@ -700,6 +703,7 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
         }
         if (!ok) {
             node_add(c, node, t, MB_BLOCK, acquire);
+            *wait_ms = (int64_t)k;  // block detail: the ParamFlowRule's index in the resource's list
             return D_BLOCK_PARAM;
         }
     }
@@ -730,6 +734,7 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
             }
             if (ts == TRS_BLOCKED) {
                 node_add(c, node, t, MB_BLOCK, acquire);
+                *wait_ms = (int64_t)k;  // block detail: the FlowRule's index (FlowRuleComparator order)
                 return D_BLOCK_FLOW;
             }
             if (!fr.cfallback) continue;  // fallbackToLocalOrPass: the rule is not activated
@@ -737,6 +742,7 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
         const int8_t d = rater_can_pass(c, fr, node, t, acquire, prio, &w);
         if (d == D_BLOCK_FLOW) {
             node_add(c, node, t, MB_BLOCK, acquire);
+            *wait_ms = (int64_t)k;
             return D_BLOCK_FLOW;
         }
         if (d == D_PASS_WAIT) {
@@ -748,8 +754,9 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
         total_wait += w;
     }
     // DegradeSlot
-    if (!degrade_pass(m.cbs, R.n_cbs, t)) {
+    if (const int kb = degrade_block_index(m.cbs, R.n_cbs, t); kb >= 0) {
         node_add(c, node, t, MB_BLOCK, acquire);
+        *wait_ms = kb;  // block detail: the breaker's index (DegradeRuleManager list order)
         return D_BLOCK_DEGRADE;
     }
     node[kNodeThreads] += 1;
@@ -787,16 +794,18 @@ __device__ __forceinline__ void chain_exit(const Ctx &c, uint32_t r, int64_t t, 
 __device__ __forceinline__ int64_t *entry_node(const Ctx &c) { return c.st.node + (size_t)c.st.nres * kNodeWords; }
 
 // SystemRuleManager.checkSystem + checkBbr (SystemRuleManager.java:298-353) for an inbound entry
-__device__ bool system_blocks(const Ctx &c, const SysDev &s, int64_t t, int count) {
-    if (!s.check) return false;
+// returns the check that blocks (SystemBlockException's limitType: 0 "qps", 1 "thread", 2 "rt",
+// 3 "load", 4 "cpu") or -1
+__device__ int system_block_type(const Ctx &c, const SysDev &s, int64_t t, int count) {
+    if (!s.check) return -1;
     int64_t *e = entry_node(c);
-    if (node_pass_qps(c, e, t) + (double)count > s.qps) return true;  // ENTRY_NODE.passQps()
-    const int32_t thr = (int32_t)e[kNodeThreads];                    // curThreadNum()
-    if ((int64_t)thr > s.max_thread) return true;
+    if (node_pass_qps(c, e, t) + (double)count > s.qps) return 0;  // ENTRY_NODE.passQps()
+    const int32_t thr = (int32_t)e[kNodeThreads];                  // curThreadNum()
+    if ((int64_t)thr > s.max_thread) return 1;
     sec_current(e, t, c.max_rt);                                      // avgRt(): success(), rt()
     const int64_t succ = sec_sum(e, t, MB_SUCC);
     const double rt = succ == 0 ? 0.0 : (double)sec_sum(e, t, MB_RT) * 1.0 / (double)succ;
-    if (rt > (double)s.max_rt) return true;
+    if (rt > (double)s.max_rt) return 2;
     if (s.load_set && s.cur_load > s.load) {
         if (thr > 1) {
             // maxSuccessQps() = maxSuccess * sampleCount / intervalInSec; minRt() = max(1, min bucket minRt)
@@ -810,11 +819,11 @@ __device__ bool system_blocks(const Ctx &c, const SysDev &s, int64_t t, int coun
             if (ms < 1) ms = 1;
             if (mr < 1) mr = 1;
             const double cap = (double)ms * 2.0 / 1.0 * (double)mr / 1000;
-            if ((double)thr > cap) return true;
+            if ((double)thr > cap) return 3;
         }
     }
-    if (s.cpu_set && s.cur_cpu > s.cpu) return true;
-    return false;
+    if (s.cpu_set && s.cur_cpu > s.cpu) return 4;
+    return -1;
 }
 
 __device__ __forceinline__ void entry_node_after_entry(const Ctx &c, int64_t t, int a, int8_t d) {
@@ -855,7 +864,8 @@ __global__ __launch_bounds__(kT) void k_lgate(const uint8_t *__restrict__ kind, 
     uint32_t g = 0;
     for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
         const uint8_t fl = flags ? flags[i] : 0;
-        if (acquire[i] < 0 || kind[i] > 1) g |= kGateBad;
+        if (acquire[i] < 0 || kind[i] > 2) g |= kGateBad;
+        if (kind[i] == 2) g |= kGateSeq;  // a block counted for a slot outside the engine: arrival order
         if ((fl & SGA_EV_INBOUND) && resource[i] < nres) g |= sys_check ? (kGateIn | kGateSeq) : kGateIn;
         if (fl & SGA_EV_ARGS) {  // the argument vector's word pairs and every list inside npvals
             const uint64_t pv = param_in ? param_in[i] : 0;
@@ -924,11 +934,17 @@ __global__ void k_lseq(FlowState st, int64_t max_rt, SysDev sys, const uint8_t *
             if (in) entry_node_after_exit(c, t, rt_in[i], a, (fl & SGA_EV_ERROR) != 0);
             continue;
         }
+        if (kind[i] == 2) {  // StatisticSlot's BlockException branch for a block thrown outside the engine
+            node_add(c, st.node + (size_t)r * kNodeWords, t, MB_BLOCK, a);
+            if (in) node_add(c, entry_node(c), t, MB_BLOCK, a);
+            continue;
+        }
         int8_t d;
         int64_t w = 0;
-        if (in && system_blocks(c, sys, t, a)) {
+        if (const int sb = in ? system_block_type(c, sys, t, a) : -1; sb >= 0) {
             node_add(c, st.node + (size_t)r * kNodeWords, t, MB_BLOCK, a);  // StatisticSlot: increaseBlockQps
             d = D_BLOCK_SYSTEM;
+            w = sb;  // block detail: the SystemRule check
         } else {
             d = chain_entry(c, r, t, a, (fl & SGA_EV_PRIORITIZED) != 0, hp, param_in[i], &w, pa);
         }
@@ -2306,9 +2322,10 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                                     else
                                         for (uint32_t b = 0; b < R.n_cbs; ++b)
                                             cb_on_complete(lcbs[b], t, qrt[k], (q.idx & F_ERROR) != 0);
-                                } else {  // DegradeSlot
-                                    qd[k] = degrade_pass(lcbs, R.n_cbs, t) ? D_PASS : D_BLOCK_DEGRADE;
-                                    qw[k] = 0;
+                                } else {  // DegradeSlot (a block's wait_ms: the breaker's index)
+                                    const int kb = degrade_block_index(lcbs, R.n_cbs, t);
+                                    qd[k] = kb < 0 ? D_PASS : D_BLOCK_DEGRADE;
+                                    qw[k] = kb < 0 ? 0 : kb;
                                 }
                             };
                             uint32_t k = end;
@@ -3279,6 +3296,10 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         bool has_in = false, has_list = false;
         for (size_t i = 0; flags && i < m && !has_in; ++i) has_in = (flags[b + i] & SGA_EV_INBOUND) && resource[b + i] < nres;
         for (size_t i = 0; any_list && i < m && !has_list; ++i) has_list = is_list(b + i);
+        for (size_t i = 0; i < m && !has_list; ++i) {
+            if (kind[b + i] > 2) return SGA_EINVAL;
+            has_list = kind[b + i] == 2;
+        }
         if ((has_in && sys.check) || has_list) {  // SystemSlot / collection arguments: one lane in arrival order
             hipLaunchKernelGGL(k_lseq, dim3(1), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sys, d_kind.p,
                                d_resid.p, d_ts.p, lo, d_acq.p, d_flags.p, d_rt.p, d_param.p, (uint32_t)m, d_dec.p,
@@ -3400,10 +3421,11 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
     hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, s, gsc, pay, d_decision, wait_p);
     hipLaunchKernelGGL(k_entry_stats, dim3(1), dim3(kEnTile), 0, s, st, (int64_t)cfg.statistic_max_rt, d_kind_in,
                        d_resource, d_ts_off, ts_base, d_acquire, flags_p, rt_p, d_decision, m);
-    if (sys.check || d_param_values)
-        hipLaunchKernelGGL(k_lseq, dim3(1), dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, sys, d_kind_in,
-                           d_resource, d_ts_off, ts_base, d_acquire, flags_p, rt_p, param_p, m, d_decision, wait_p,
-                           d_param_values);
+    // arrival-order chunks (system rules, collection / argument vectors, kind 2 blocks): k_lseq acts only
+    // when the gate says so
+    hipLaunchKernelGGL(k_lseq, dim3(1), dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, sys, d_kind_in,
+                       d_resource, d_ts_off, ts_base, d_acquire, flags_p, rt_p, param_p, m, d_decision, wait_p,
+                       d_param_values);
     hipLaunchKernelGGL(k_lfail, dim3(gb), dim3(kT), 0, s, d_gate.p, d_overflow.p, d_gate.p + 1, m, d_decision, wait_p);
     SGA_HIP_CHECK(hipGetLastError());
     return 0;

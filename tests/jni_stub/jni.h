@@ -29,6 +29,7 @@ struct JNINativeInterface_ {
     void (*ReleaseIntArrayElements)(JNIEnv *, jintArray, jint *, jint);
     void (*SetIntArrayRegion)(JNIEnv *, jintArray, jsize, jsize, const jint *);
     void (*SetLongArrayRegion)(JNIEnv *, jlongArray, jsize, jsize, const jlong *);
+    void (*SetDoubleArrayRegion)(JNIEnv *, jdoubleArray, jsize, jsize, const jdouble *);
     void *(*GetDirectBufferAddress)(JNIEnv *, jobject);
 };
 #endif

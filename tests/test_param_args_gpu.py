@@ -158,3 +158,28 @@ def _load_cluster_params(s, rules):
                       cluster_config=ParamFlowClusterConfig(flow_id=r.get("cluster_flow_id"),
                                                             fallback_to_local_when_fail=bool(r.get("cluster_fallback"))))
         for r in rules])
+
+
+def test_blocked_entries_outside_the_engine():
+    """Event kind 2 (SGA_KIND_BLOCKED): an entry blocked by a slot outside the engine (AuthoritySlot ahead
+    of the checks) is counted by StatisticSlot's BlockException branch only (StatisticSlot.java:121-135) --
+    block QPS on the node and, inbound, on ENTRY_NODE; later decisions see those counts (block QPS feeds
+    no controller, the node views must match)."""
+    rng = np.random.default_rng(9)
+    n_res = 4
+    flow = [{"resource": r, "count": 5.0} for r in range(n_res)]
+    n = 3000
+    st = {"kind": (rng.random(n) < 0.2).astype(np.uint8) * 2, "resource": rng.integers(0, n_res, n).astype(np.uint32),
+          "ts": T0 + np.arange(n, dtype=np.int64) // 3, "acquire": rng.integers(1, 3, n).astype(np.int32),
+          "flags": np.where(rng.random(n) < 0.5, 8, 0).astype(np.uint8), "rt": np.zeros(n, np.int64),
+          "param": np.zeros(n, np.uint64)}
+    orc = lt.Oracle(n_res, flow)
+    exp = orc.replay(st)
+    eng, s = _sentinel(n_res, 1 << 14)
+    _load(s, flow)
+    got = s.submit(st["kind"], st["resource"], st["ts"], st["acquire"], st["flags"], st["rt"], st["param"])
+    _assert_same(st, got, exp, "kind-2 blocks")
+    _assert_nodes(s, orc, n_res, int(st["ts"].max()))
+    assert s.node(0xFFFFFFFF, int(st["ts"].max())).total_block == orc.node(0xFFFFFFFF, int(st["ts"].max()))[9]
+    orc.close()
+    eng.close()
