@@ -15,7 +15,6 @@ import com.alibaba.csp.sentinel.cluster.flow.rule.ClusterFlowRuleManager;
 import com.alibaba.csp.sentinel.cluster.flow.rule.ClusterParamFlowRuleManager;
 import com.alibaba.csp.sentinel.property.PropertyListener;
 import com.alibaba.csp.sentinel.property.SentinelProperty;
-import com.alibaba.csp.sentinel.slots.block.RuleConstant;
 import com.alibaba.csp.sentinel.slots.block.degrade.DegradeRule;
 import com.alibaba.csp.sentinel.slots.block.degrade.DegradeRuleManager;
 import com.alibaba.csp.sentinel.slots.block.flow.FlowRule;
@@ -356,9 +355,5 @@ public final class GpuRuleSync {
             check(GpuEngine.loadClusterParamRules(GpuEngine.get(), ns, id, count, tt, sc, w, off, hv, hc),
                   "ClusterParamFlowRuleManager.loadRules");
         }
-    }
-
-    static String defaultNamespace() {
-        return RuleConstant.LIMIT_APP_DEFAULT;
     }
 }

@@ -18,14 +18,18 @@ import com.alibaba.csp.sentinel.spi.SpiLoader;
 /**
  * {@link SlotChainBuilder} (SlotChainProvider.java:28-60 resolves the first SPI instance) that builds the
  * default SPI-sorted chain (DefaultSlotChainBuilder) but puts one {@link GpuStatisticSlot} where
- * StatisticSlot was and drops the slots it replaces: ParamFlowSlot, FlowSlot, DegradeSlot, SystemSlot.
- * NodeSelectorSlot, ClusterBuilderSlot, LogSlot and AuthoritySlot stay as they are.
+ * StatisticSlot was and drops the slots the engine runs: SystemSlot, ParamFlowSlot, FlowSlot, DegradeSlot.
+ * NodeSelectorSlot, ClusterBuilderSlot, LogSlot and AuthoritySlot stay; GpuStatisticSlot fires AuthoritySlot
+ * (and any custom slot) before the engine decides, as StatisticSlot fires the checks before accounting.
+ * The engine's rules arrive through {@link GpuRuleSync#install()}, called here, so no rule manager is left
+ * without a path into the engine; {@link GpuMetricTimerListener} writes the metric log from the engine.
  */
 @Spi(order = -100)
 public class GpuSlotChainBuilder implements SlotChainBuilder {
 
     @Override
     public ProcessorSlotChain build() {
+        GpuRuleSync.install();
         ProcessorSlotChain chain = new DefaultProcessorSlotChain();
         List<ProcessorSlot> sorted = SpiLoader.of(ProcessorSlot.class).loadInstanceListSorted();
         for (ProcessorSlot slot : sorted) {

@@ -1,9 +1,9 @@
 package com.alibaba.csp.sentinel.gpu;
 
-import java.nio.charset.StandardCharsets;
 import java.util.Collection;
 import java.util.Map;
 import java.util.concurrent.ConcurrentHashMap;
+import java.util.concurrent.atomic.AtomicInteger;
 
 import com.alibaba.csp.sentinel.cluster.TokenResult;
 import com.alibaba.csp.sentinel.cluster.TokenResultStatus;
@@ -24,6 +24,7 @@ public class GpuTokenService implements TokenService {
 
     private final long engine = GpuEngine.get();
     private final Map<String, Integer> clientIds = new ConcurrentHashMap<>();
+    private final AtomicInteger nextClientId = new AtomicInteger();
 
     private static TokenResult result(int rc, int[] o) {
         if (rc != GpuEngine.OK) {
@@ -50,7 +51,7 @@ public class GpuTokenService implements TokenService {
         long[] keys = new long[params.size()];
         int i = 0;
         for (Object p : params) {
-            keys[i++] = paramKey(p);
+            keys[i++] = GpuArgs.key(p);
         }
         int[] o = new int[3];
         int rc = GpuEngine.requestParamToken(engine, ruleId, acquireCount, keys, TimeUtil.currentTimeMillis(), o);
@@ -81,24 +82,7 @@ public class GpuTokenService implements TokenService {
         GpuEngine.concurrent(engine, 1, 0, tokenId, 0, TimeUtil.currentTimeMillis(), new long[2]);
     }
 
-    private int clientId(String address) {
-        return clientIds.computeIfAbsent(address, a -> clientIds.size());
-    }
-
-    /**
-     * A stable 64-bit key per parameter object: integral numbers by value, anything else by a
-     * 64-bit FNV-1a hash of its string form (the engine compares keys, as ParameterMetric compares
-     * objects with equals()).
-     */
-    static long paramKey(Object p) {
-        if (p instanceof Long || p instanceof Integer || p instanceof Short || p instanceof Byte) {
-            return ((Number) p).longValue();
-        }
-        long h = 0xcbf29ce484222325L;
-        for (byte b : String.valueOf(p).getBytes(StandardCharsets.UTF_8)) {
-            h ^= (b & 0xff);
-            h *= 0x100000001b3L;
-        }
-        return h;
+    private int clientId(String address) {  // dense, unique per address (an AtomicInteger, not size())
+        return clientIds.computeIfAbsent(address, a -> nextClientId.getAndIncrement());
     }
 }
