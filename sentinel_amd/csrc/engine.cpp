@@ -995,15 +995,30 @@ int sga_request_tokens(sga_engine *e, const int64_t *flow_id, const int32_t *acq
 }
 
 // ---- coalescing queue (TokenQueue above)
+static int combine_round(sga_engine *e);
+
 int sga_token_submit(sga_engine *e, int64_t flow_id, int32_t acquire, uint8_t prioritized, int64_t ts,
                      uint64_t *ticket) {
     if (!e || !ticket) return SGA_EINVAL;
+    // what would fail the whole coalesced batch is refused here, for this caller only (the engine
+    // answers an invalid flowId / acquireCount with BAD_REQUEST inside the batch)
+    if (ts < 0) return SGA_EINVAL;
     sga::TokenQueue &q = e->impl.tq;
     const uint64_t t = q.tail.fetch_add(1, std::memory_order_relaxed);
     sga::TokenQueue::Slot &sl = q.ring[t & (sga::TokenQueue::kCap - 1)];
-    // a full ring (the ticket kCap earlier not collected yet) waits for its poller
-    for (int spin = 0; sl.seq.load(std::memory_order_acquire) != t; ++spin)
-        if (spin > 64) std::this_thread::yield();
+    // The slot still holds ticket t - kCap.  Decided but never polled (its caller gave up): reclaim it --
+    // a later sga_poll of that ticket answers SGA_EINVAL.  Filled but not decided: decide it (this caller
+    // becomes the combiner if none is running).  Free but not yet filled by its producer: wait for it.
+    const uint64_t prev = t - sga::TokenQueue::kCap;
+    for (int spin = 0;; ++spin) {
+        uint64_t s = sl.seq.load(std::memory_order_acquire);
+        if (s == t) break;
+        if (t >= sga::TokenQueue::kCap && s == prev + 2 &&
+            sl.seq.compare_exchange_strong(s, t, std::memory_order_acq_rel))
+            break;
+        if (t >= sga::TokenQueue::kCap && s == prev + 1) (void)combine_round(e);
+        else if (spin > 64) std::this_thread::yield();
+    }
     sl.flow_id = flow_id;
     sl.acquire = acquire;
     sl.prio = prioritized ? 1 : 0;
@@ -1062,10 +1077,14 @@ int sga_poll(sga_engine *e, uint64_t ticket, sga_token_result *out) {
     sga::TokenQueue &q = e->impl.tq;
     sga::TokenQueue::Slot &sl = q.ring[ticket & (sga::TokenQueue::kCap - 1)];
     for (int pass = 0; pass < 2; ++pass) {
-        const uint64_t s = sl.seq.load(std::memory_order_acquire);
+        uint64_t s = sl.seq.load(std::memory_order_acquire);
         if (s == ticket + 2) {
-            std::memcpy(out, &sl.result, sizeof(*out));
-            sl.seq.store(ticket + sga::TokenQueue::kCap, std::memory_order_release);
+            sga_token_result r;
+            std::memcpy(&r, &sl.result, sizeof(r));
+            // a producer kCap tickets later may reclaim the slot at the same time (sga_token_submit)
+            if (!sl.seq.compare_exchange_strong(s, ticket + sga::TokenQueue::kCap, std::memory_order_acq_rel))
+                return SGA_EINVAL;
+            *out = r;
             return SGA_OK;
         }
         if (s != ticket + 1) return SGA_EINVAL;  // not a live ticket

@@ -166,6 +166,13 @@ class ClusterTokenServer:
                         # the decoder also stops when the batch's value or namespace buffer is full;
                         # a complete frame left undecoded means such a capacity stop, not a partial frame
                         full = self.batch.n >= self.batch.s.cap or _complete_frame_at(pending, used)
+                        # a frame that does not fit even an empty batch (more parameter values or a longer
+                        # namespace than the batch buffers hold) can never be decoded: drop the channel,
+                        # as for an over-long frame, instead of flushing empty batches forever
+                        stuck = full and used == 0 and before == 0 and self.batch.n == 0
+                    if stuck:
+                        writer.close()
+                        return
                     pending = pending[used:]
                     if full:
                         await self.flush()  # drain, then decode the rest

@@ -516,3 +516,33 @@ def test_coalescing_queue_threads_equal_ticket_order(eng_mod):
     one = svc.request_token(1, 1, False, T0 + 10_000)
     assert one.status in (0, 1)
     eng.close()
+
+
+def test_coalescing_queue_bad_request_and_abandoned_tickets(eng_mod):
+    """a request the batch would reject (ts < 0) is refused at submit for its caller only, the
+    other queued requests are decided; tickets whose callers never poll are reclaimed when the ring wraps
+    (a later poll of such a ticket answers EINVAL), so producers never spin forever."""
+    from sentinel_amd._lib import EngineError
+    c = eng_mod
+    rules = {"default": [{"flow_id": 1, "count": 1e9, "threshold_type": 1}]}
+    eng = make_engine(c, max_batch=1 << 12)
+    engine_rules(c, eng, rules)
+    svc = c.DefaultTokenService(eng)
+    good = [svc.submit(1, 1, False, T0 + i) for i in range(5)]
+    with pytest.raises(EngineError):
+        svc.submit(1, 1, False, -5)
+    res = [svc.poll(t) for t in good]
+    while any(r is None for r in res):
+        res = [r if r is not None else svc.poll(t) for r, t in zip(res, good)]
+    assert all(r.status == 0 for r in res)
+    # abandon a ticket, wrap the ring (65536 slots) with polled requests, then poll the abandoned one
+    lost = svc.submit(1, 1, False, T0 + 100)
+    cap = 1 << 16
+    for k in range(cap + 10):
+        t = svc.submit(1, 1, False, T0 + 200 + k // 1000)
+        r = None
+        while r is None:
+            r = svc.poll(t)
+    with pytest.raises(EngineError):
+        svc.poll(lost)
+    eng.close()
