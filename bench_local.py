@@ -160,38 +160,97 @@ def _state_bytes(cfg, b):
     return 2 * total
 
 
-def _cpu_local(cfg, b):
-    """One host thread: the C oracle replays the first `sample` entries, then their exits (masked by
-    the oracle's own decisions, as the GPU masks by its decisions)."""
-    from tests import local_trace as lt
-    m = min(cfg["sample"], b.n)
-    orc = lt.Oracle(cfg["n_res"], cfg.get("flow", []), cfg.get("param", []), cfg.get("degrade", []))
-    ent = {"kind": np.zeros(m, np.uint8), "resource": b.res[:m], "ts": b.ts[:m], "acquire": b.acq[:m],
-           "flags": b.flags[:m], "rt": np.zeros(m, np.int64), "param": b.param[:m]}
-    t0 = time.perf_counter()
-    dec, _ = orc.replay(ent)
-    dt = time.perf_counter() - t0
-    n_ev = m
-    if b.exit_of is not None:
-        sel = b.exit_of[b.exit_of < m]
-        ok = (dec[sel] == 0) | (dec[sel] == 4)
-        sel = sel[ok]
-        # exit times / rt / flags of the selected entries, in the batch's exit order
+def _threads():
+    import os
+    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+
+
+class _Shard:
+    """One oracle instance and its share of the sample: the entries (of the first m) whose resource is in
+    sel_res, then the exits of those that passed, masked by its own decisions.  Rules and streams are
+    built before any timing; entries() and exits() are the timed replays."""
+
+    def __init__(self, cfg, b, m, sel_res):
+        from tests import local_trace as lt
+        self.b, self.m = b, m
+        self.orc = lt.Oracle(cfg["n_res"], cfg.get("flow", []), cfg.get("param", []), cfg.get("degrade", []))
+        idx = np.nonzero(sel_res[b.res[:m]])[0] if sel_res is not None else np.arange(m)
+        self.idx = idx
+        self.ent = {k: np.ascontiguousarray(v) for k, v in
+                    {"kind": np.zeros(len(idx), np.uint8), "resource": b.res[idx], "ts": b.ts[idx],
+                     "acquire": b.acq[idx], "flags": b.flags[idx], "rt": np.zeros(len(idx), np.int64),
+                     "param": b.param[idx]}.items()}
+        self.ex = None
+        self.n_ev = len(idx)
+
+    def entries(self):
+        self.dec, _ = self.orc.replay(self.ent)
+
+    def build_exits(self):
+        b = self.b
+        if b.exit_of is None:
+            return
+        passed = np.zeros(b.n, bool)
+        passed[self.idx] = (self.dec == 0) | (self.dec == 4)
         pos = np.empty(b.n, np.int64)
         pos[b.exit_of] = np.arange(b.n)
-        order = np.sort(pos[sel])
-        ex = {"kind": np.ones(len(order), np.uint8), "resource": b.res[b.exit_of[order]], "ts": b.exit_ts[order],
-              "acquire": b.acq[b.exit_of[order]], "flags": b.exit_flags[order], "rt": b.exit_rt[order],
-              "param": b.param[b.exit_of[order]]}
-        t0 = time.perf_counter()
-        orc.replay(ex)
-        dt += time.perf_counter() - t0
-        n_ev += len(order)
-    orc.close()
-    return {"value": m / dt, "unit": "decisions/s", "cores": 1, "kind": "port",
-            "events_per_s": n_ev / dt,
-            "sample": f"the first {m} entries of the batch and the exits of those that passed ({n_ev} events), "
-                      f"replayed by the C oracle (oracle/sentinel_oracle.c slot-chain restatement), one thread"}
+        sel = b.exit_of[b.exit_of < self.m]
+        order = np.sort(pos[sel[passed[sel]]])
+        self.ex = {k: np.ascontiguousarray(v) for k, v in
+                   {"kind": np.ones(len(order), np.uint8), "resource": b.res[b.exit_of[order]],
+                    "ts": b.exit_ts[order], "acquire": b.acq[b.exit_of[order]], "flags": b.exit_flags[order],
+                    "rt": b.exit_rt[order], "param": b.param[b.exit_of[order]]}.items()}
+        self.n_ev += len(order)
+
+    def exits(self):
+        if self.ex is not None:
+            self.orc.replay(self.ex)
+
+    def close(self):
+        self.orc.close()
+
+
+def _timed(shards, fn):
+    import threading
+    ths = [threading.Thread(target=lambda s=s: getattr(s, fn)()) for s in shards]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    return time.perf_counter() - t0
+
+
+def _cpu_local(cfg, b):
+    """The C oracle on the host: one thread replaying the first `sample` entries (then their exits, masked by
+    its own decisions as the GPU masks by its decisions), and T threads over disjoint resource subsets
+    (resource mod T; resources are independent without SystemRules, as on the GPUs) -- the shard-parallel
+    analogue of the reference's multi-threaded path.  Only the replays are timed (rule loads and stream
+    building are not).  `value` is the larger of the two figures."""
+    m = min(cfg["sample"], b.n)
+    one = _Shard(cfg, b, m, None)
+    dt1 = _timed([one], "entries")
+    one.build_exits()
+    dt1 += _timed([one], "exits")
+    n1 = one.n_ev
+    one.close()
+    T = _threads()
+    res_of = np.arange(cfg["n_res"]) % T
+    shards = [_Shard(cfg, b, m, res_of == k) for k in range(T)]
+    dtn = _timed(shards, "entries")
+    for sh in shards:
+        sh.build_exits()
+    dtn += _timed(shards, "exits")
+    busy = sum(1 for sh in shards if len(sh.idx))
+    for sh in shards:
+        sh.close()
+    return {"value": max(m / dtn, m / dt1), "unit": "decisions/s", "cores": T, "kind": "port",
+            "value_1thread": m / dt1, "value_threads": m / dtn, "events_per_s_1thread": n1 / dt1,
+            "threads_with_work": busy,
+            "sample": f"the first {m} entries of the batch and the exits of those that passed ({n1} events), "
+                      f"replayed by the C oracle (oracle/ slot-chain restatement): {T} threads over disjoint "
+                      f"resource subsets (resource mod {T}; {busy} with events), value_1thread = one thread in "
+                      f"arrival order; value = the larger of the two"}
 
 
 def run_local(args, cfg_name):
@@ -347,9 +406,35 @@ def run_rls(args):
         L.orc_cluster_replay_simple(oh, m, f_s.ctypes.data, a_s.ctypes.data, dts.ctypes.data, res)
         dt = time.perf_counter() - t0
         L.orc_cluster_free(oh)
-        cpu = {"value": m / dt, "unit": "descriptors/s", "cores": 1, "kind": "port",
+        # T threads over disjoint flowId subsets (one oracle each, rules independent)
+        import threading
+        T = _threads()
+        part = (f_s % T).astype(np.int64)
+        shards = []
+        for k in range(T):
+            sel = part == k
+            ohk = L.orc_cluster_new(1.0, 1.0)
+            L.orc_cluster_load_rules(ohk, b"default", arr, n_rules)
+            shards.append((ohk, np.ascontiguousarray(f_s[sel]), np.ascontiguousarray(a_s[sel]),
+                           np.ascontiguousarray(dts[sel]), (H.OrcTokenResult * max(1, int(sel.sum())))()))
+
+        def work(k):
+            ohk, f, a, t, r = shards[k]
+            L.orc_cluster_replay_simple(ohk, len(f), f.ctypes.data, a.ctypes.data, t.ctypes.data, r)
+
+        ths = [threading.Thread(target=work, args=(k,)) for k in range(T)]
+        t0 = time.perf_counter()
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        dtn = time.perf_counter() - t0
+        for sh in shards:
+            L.orc_cluster_free(sh[0])
+        cpu = {"value": m / dtn, "unit": "descriptors/s", "cores": T, "kind": "port", "value_1thread": m / dt,
                "sample": f"the first {m} descriptors of the batch, replayed by the C oracle's "
-                         f"SimpleClusterFlowChecker restatement (oracle/sentinel_oracle.c), one thread"}
+                         f"SimpleClusterFlowChecker restatement (oracle/sentinel_oracle.c): {T} threads over "
+                         f"disjoint flowId subsets (flowId mod {T}); value_1thread = one thread in order"}
     return {
         "metric": "admission decisions/sec, config C5A (Envoy RLS descriptors, SURVEY.md 8(d)); % HBM peak",
         "value": nd * args.steps / wall, "unit": "descriptors/s", "n_gpus": 1, "steps": args.steps,

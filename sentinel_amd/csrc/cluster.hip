@@ -1073,7 +1073,22 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
                 s_cand[2 * k + 1] = r1 - r0;
             }
         }
-        const SlotParam P = st.param[s];
+        SlotParam P;
+        if (st.uni_S) {
+            // uniform geometry: the record address and the window geometry without the parameter
+            // load; only the threshold is loaded, beside the record's loads
+            P.S = st.uni_S;
+            P.W = st.uni_W;
+            P.interval = st.uni_iv;
+            P.isec = st.uni_iv / 1000.0;
+            P.boff = s * (uint32_t)(st.uni_S + 1);
+            P.thr = simple ? st.param[s].thr_simple : st.param[s].thr;
+            P.thr_simple = P.thr;
+            P.active = 1;
+            P.ns = 0;
+        } else {
+            P = st.param[s];
+        }
         const Rec R = rec_of(st, P);
         const double thr = simple ? P.thr_simple : P.thr;
         const int64_t qbase = div_pos(ts_base, P.W);
@@ -1898,7 +1913,20 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
     const uint32_t s_raw = sc.hot_slot[h];
     const uint32_t plo = sc.plo[h], phi = max(sc.phi[h], plo);
     const uint32_t s = s_raw < st.nslots ? s_raw : 0u;  // ids past the hot count hold stale slots
-    const SlotParam P = st.param[s];
+    SlotParam P;
+    if (st.uni_S) {  // uniform geometry (ClusterState::uni_S): the record loads need no parameter load
+        P.S = st.uni_S;
+        P.W = st.uni_W;
+        P.interval = st.uni_iv;
+        P.isec = st.uni_iv / 1000.0;
+        P.boff = s * (uint32_t)(st.uni_S + 1);
+        P.thr = st.param[s].thr;
+        P.thr_simple = P.thr;
+        P.active = 1;
+        P.ns = 0;
+    } else {
+        P = st.param[s];
+    }
     if (!mode || h >= nhot) return;
     const uint32_t nb = bd_hi >= bd_lo ? bd_hi - bd_lo + 1 : 0;
     const bool bl = (uint32_t)lane < nb && lane > 0;

@@ -54,6 +54,10 @@ struct ClusterState {
     uint32_t hmask;
     uint32_t nslots;
     double max_occupy_ratio;
+    // Uniform geometry (every allocated slot has sampleCount uni_S, windowLength uni_W, interval uni_iv and
+    // its record at slot * (uni_S + 1) 64-byte units, the layout of one load of equal rules): a slot's record
+    // address needs no parameter load, so the record loads do not wait for one.  uni_S = 0: not uniform.
+    int32_t uni_S, uni_W, uni_iv, uni_pad;
 };
 
 // GlobalRequestLimiter / RequestLimiter of one namespace over UnaryLeapArray(10, 1000)

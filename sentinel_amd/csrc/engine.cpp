@@ -365,6 +365,7 @@ struct Engine {
     // ---- local flow engine
     FlowEngine flow;
 
+    int32_t uni_S = 0, uni_W = 0, uni_iv = 0;  // ClusterState::uni_S (sync_device)
     ClusterState state() const {
         ClusterState st{};
         st.param = d_param.p;
@@ -378,6 +379,9 @@ struct Engine {
         st.hmask = hmask;
         st.nslots = (uint32_t)slots.size();
         st.max_occupy_ratio = cfg.max_occupy_ratio;
+        st.uni_S = uni_S;
+        st.uni_W = uni_W;
+        st.uni_iv = uni_iv;
         return st;
     }
 
@@ -481,6 +485,27 @@ struct Engine {
             p.ns = h.ns;
         }
         if (ns) SGA_HIP_CHECK(hipMemcpyAsync(d_param.p, hp.data(), ns * sizeof(SlotParam), hipMemcpyHostToDevice, stream));
+        // uniform geometry (ClusterState::uni_S): every allocated slot's record at slot * (S + 1) units
+        uni_S = 0;
+        {
+            int32_t S0 = 0, W0 = 0, I0 = 0;
+            bool uni = true;
+            for (size_t i = 0; i < ns && uni; ++i) {
+                const SlotParam &p = hp[i];
+                if (!slots[i].allocated) continue;
+                if (!S0) {
+                    S0 = p.S;
+                    W0 = p.W;
+                    I0 = p.interval;
+                }
+                uni = p.S == S0 && p.W == W0 && p.interval == I0 && (uint64_t)p.boff == (uint64_t)i * (uint64_t)(S0 + 1);
+            }
+            if (uni && S0 > 0 && S0 <= 64) {
+                uni_S = S0;
+                uni_W = W0;
+                uni_iv = I0;
+            }
+        }
         {  // concurrency: ConcurrentClusterFlowChecker.calcGlobalThreshold (no exceedCount), timeouts
             if (d_cparam.n < slot_cap) {
                 const size_t c = std::max<size_t>(slot_cap, d_cparam.n * 2);
