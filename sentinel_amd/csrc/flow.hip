@@ -3246,7 +3246,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
     bool any_list = false;
     for (size_t i = 0; flags && param && i < n; ++i) {
         if (!is_list(i)) continue;
-        if (!pvals || !list_ok(i)) return SGA_EINVAL;
+        if ((npvals && !pvals) || !list_ok(i)) return SGA_EINVAL;  // an empty args vector needs no values
         any_list = true;
     }
     if (any_list) {
