@@ -524,11 +524,23 @@ struct RunIn {
     uint32_t bd;  // bucket delta of the run (its bucket = ts_base / W + bd)
 };
 
+// A rule's record between its runs (cold flows): the (start, PASS) pairs and the occupy state as
+// the lane's last run left them, so the rule's later runs issue no record loads (one memory round
+// trip per rule instead of one per run).  have = false: load from the record.
+template <int kMaxPairs>
+struct RecCarry {
+    int4 sp[kMaxPairs > 0 ? kMaxPairs : 1];
+    int4 o0, o1;
+    bool have;
+};
+
 // prio_before(k): prioritized requests among the run's first k (asked only when some prioritized
-// request is past the passing prefix).
-template <class PrioBefore, int kMaxPairs = 16>
+// request is past the passing prefix).  kMaxPairs = 0: sampleCount above the register form, the
+// pairs are loaded one by one every run.
+template <class PrioBefore, int kMaxPairs>
 __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam &P, const Rec &R, double thr,
-                                         int64_t qbase, const RunIn &ri, PrioBefore prio_before, RunOut &ro) {
+                                         int64_t qbase, const RunIn &ri, PrioBefore prio_before, RunOut &ro,
+                                         RecCarry<kMaxPairs> &rc) {
     // Cluster rules have intervalInMs = sampleCount x windowLengthInMs (checkClusterField), so every
     // validity test below (isWindowDeprecated, getValidHead) gives the same answer for any time in
     // the run's bucket: the bucket start stands in for the first request's time.
@@ -539,30 +551,37 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
     const int64_t qs = div_pos(q, P.S);
     const int cj = (int)(q - qs * P.S);
     const int jh = cj + 1 == P.S ? 0 : cj + 1;  // LeapArray.getValidHead index ((t0 + W) / W) % S
-    // The record's loads are issued before any is used (one memory latency per run, not one per
-    // dependent step): the current bucket's (start, PASS) pair and its six other counters
-    // (WAITING, BLOCK, PASS_REQUEST, BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK), the occupy
-    // state (in the lines of the pairs), and below the (start, PASS) pairs of every bucket.
+    // First run of a rule: the record's loads are issued before any is used (one memory latency,
+    // not one per dependent step): the current bucket's six other counters (WAITING, BLOCK,
+    // PASS_REQUEST, BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK), the occupy state (in the lines of
+    // the pairs) and the (start, PASS) pair of every bucket, at clamped indices (a load under a
+    // branch is waited for before the branch closes, which would serialise them).  Later runs take
+    // the pairs and the occupy state from registers.
     const int4 *v = reinterpret_cast<const int4 *>(R.r);
     const int4 *cv = reinterpret_cast<const int4 *>(R.r + 2 * P.S + kOccWords + 6 * cj);
-    const int4 c01 = cv[0], c23 = cv[1], c45 = cv[2];
-    SlotOcc occ_ld;  // two 16-byte loads (the occupy state is 16-byte aligned in the record)
-    int2 occ_hi;
-    {
+    int4 c01 = make_int4(0, 0, 0, 0), c23 = c01, c45 = c01;
+    bool cnt_loaded = false;
+    if (!rc.have) {
+        c01 = cv[0];
+        c23 = cv[1];
+        c45 = cv[2];
+        cnt_loaded = true;
         const int4 *ov = reinterpret_cast<const int4 *>(&R.occ());
-        const int4 o0 = ov[0], o1 = ov[1];
-        occ_ld.occ_pass = i64_lo(o0);
-        occ_ld.occ_preq = i64_hi(o0);
-        occ_ld.has_occ = o1.x;
-        occ_ld.pad = o1.y;
-        occ_hi = make_int2(o1.z, o1.w);  // the record's spare occupy word, stored back unchanged
+        rc.o0 = ov[0];
+        rc.o1 = ov[1];
+        if constexpr (kMaxPairs > 0) {
+#pragma unroll
+            for (int jj = 0; jj < kMaxPairs; ++jj) rc.sp[jj] = v[min(jj, P.S - 1)];
+        }
     }
-    int4 cur;  // the current bucket's pair: taken from the pair loads below (no load of its own)
+    SlotOcc occ_ld;
+    occ_ld.occ_pass = i64_lo(rc.o0);
+    occ_ld.occ_preq = i64_hi(rc.o0);
+    occ_ld.has_occ = rc.o1.x;
+    occ_ld.pad = rc.o1.y;
+    int4 cur;  // the current bucket's pair
     int64_t bp = 0, hstart = kAbsent, hpass = 0;
     {
-        // (start, PASS) pairs: one 16-byte load per bucket.  Up to 16 buckets (sampleCount 10 is
-        // the default) the loads are issued together before any is used: a loop that waits for
-        // each bucket's load in turn pays S memory latencies per run.
         auto take = [&](int jj, const int4 &sp) {
             const int64_t w = i64_lo(sp), pv = i64_hi(sp);
             if (jj == jh) {
@@ -571,19 +590,14 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
             }
             if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) bp += pv;
         };
-        if (P.S <= kMaxPairs) {
-            // unconditional loads (a clamped index re-reads the last pair): a load under a branch
-            // is waited for before the branch closes, which serialises the S loads
-            int4 sp[kMaxPairs];
-#pragma unroll
-            for (int jj = 0; jj < kMaxPairs; ++jj) sp[jj] = v[min(jj, P.S - 1)];
-            cur = sp[0];
+        if constexpr (kMaxPairs > 0) {
+            cur = rc.sp[0];
 #pragma unroll
             for (int jj = 1; jj < kMaxPairs; ++jj)
-                if (jj == cj) cur = sp[jj];
+                if (jj == cj) cur = rc.sp[jj];
 #pragma unroll
             for (int jj = 0; jj < kMaxPairs; ++jj)
-                if (jj < P.S) take(jj, sp[jj]);
+                if (jj < P.S) take(jj, rc.sp[jj]);
         } else {
             cur = v[cj];
             for (int jj = 0; jj < P.S; ++jj) take(jj, v[jj]);
@@ -593,6 +607,11 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
     if (a <= 0 || (old != kAbsent && ws < old)) return false;
     if (ri.cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) return false;
     const bool rot = old == kAbsent || ws > old;
+    if (!rot && !cnt_loaded) {  // a later run in a bucket the record already holds (rare)
+        c01 = cv[0];
+        c23 = cv[1];
+        c45 = cv[2];
+    }
     int64_t c[CEV_N];
     SlotOcc o{0, 0, 0, 0};
     bool occ_loaded = false, occ_dirty = false;
@@ -637,25 +656,10 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
         // WAITING over the same valid buckets (only runs with prioritized blocked requests read it;
         // validity is re-tested per bucket, so any sampleCount works)
         int64_t w0 = c[CEV_WAITING];
-        if (P.S <= kMaxPairs) {
-            // the buckets' WAITING counters (one per 48-byte group), loaded together at clamped
-            // indices; a load under the validity branch would be waited for bucket by bucket
-            int64_t wv[kMaxPairs], st_[kMaxPairs];
-#pragma unroll
-            for (int jj = 0; jj < kMaxPairs; ++jj) {
-                const int j2 = min(jj, P.S - 1);
-                st_[jj] = R.start(j2);
-                wv[jj] = R.cnt(CEV_WAITING, j2);
-            }
-#pragma unroll
-            for (int jj = 0; jj < kMaxPairs; ++jj)
-                if (jj < P.S && jj != cj && st_[jj] != kAbsent && !(t0 - st_[jj] > (int64_t)P.interval)) w0 += wv[jj];
-        } else {
 #pragma nounroll
-            for (int jj = 0; jj < P.S; ++jj) {
-                const int64_t w = R.start(jj);
-                if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) w0 += R.cnt(CEV_WAITING, jj);
-            }
+        for (int jj = 0; jj < P.S; ++jj) {
+            const int64_t w = R.start(jj);
+            if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) w0 += R.cnt(CEV_WAITING, jj);
         }
         if (!occ_loaded) o = occ_ld;
         const double latest = (double)(s0 + (int64_t)f * a) / P.isec;
@@ -700,10 +704,19 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
         cg[1] = i4(c[CEV_PASS_REQUEST], c[CEV_BLOCK_REQUEST]);
         cg[2] = i4(c[CEV_OCCUPIED_PASS], c[CEV_OCCUPIED_BLOCK]);
         if (occ_dirty) {
+            rc.o0 = i4(o.occ_pass, o.occ_preq);
+            rc.o1 = make_int4(o.has_occ, o.pad, rc.o1.z, rc.o1.w);  // the spare word stored back unchanged
             int4 *ov = reinterpret_cast<int4 *>(&R.occ());
-            ov[0] = i4(o.occ_pass, o.occ_preq);
-            ov[1] = make_int4(o.has_occ, o.pad, occ_hi.x, occ_hi.y);
+            ov[0] = rc.o0;
+            ov[1] = rc.o1;
         }
+        if constexpr (kMaxPairs > 0) {
+            const int4 np = i4(stv, c[CEV_PASS]);
+#pragma unroll
+            for (int jj = 0; jj < kMaxPairs; ++jj)
+                if (jj == cj) rc.sp[jj] = np;
+        }
+        rc.have = kMaxPairs > 0;
     }
     ro.s0 = s0;
     ro.thr = thr;
@@ -914,7 +927,7 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
     __shared__ uint32_t rl_n[kFzChunk], rl_cp[kFzChunk], rl_p0[kFzChunk], rl_ab[kFzChunk];
     __shared__ FAgg wtot[kFzThreads / 64];
     __shared__ uint32_t s_h0, s_E, s_wcnt[kFzThreads / 64];
-    __shared__ uint32_t s_ncand, s_cbase, s_cand[2 * kFzThreads];
+    __shared__ uint32_t s_ncand, s_cbase, s_next, s_cand[2 * kFzThreads];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t n = dn ? min(nhost, *dn) : nhost;
     const uint32_t c0 = blockIdx.x * kFzChunk;
@@ -1055,25 +1068,38 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
         __syncthreads();
     }
     const uint32_t nf = nf_carry;
-    if (threadIdx.x == 0) s_ncand = 0;
+    if (threadIdx.x == 0) {
+        s_ncand = 0;
+        s_next = kFzThreads;  // rules [0, kFzThreads) go to the lanes of the same index
+    }
     __syncthreads();  // run records and plist (global, this workgroup) before the flows read them
     // next-hot-set candidates: counts of at least the floor (half the last pick threshold) are
     // gathered in LDS and published with one global reservation per workgroup
     const uint32_t cand_floor = max(hot_min, sc.hot_ctl[7] >> 1);
     fz_mark(dbg, 1, fzt);
-    // ---- 2 flows: one lane per owned rule
-    for (uint32_t f = threadIdx.x; f < ((dbg & 1) ? 0u : nf); f += kFzThreads) {
-        const uint32_t r0 = fheads[f];
-        const uint32_t r1 = f + 1 < nf ? fheads[f + 1] : E;
-        const uint32_t s = fslot[f];
-        if (r1 - r0 >= cand_floor) {  // next batch's hot-set candidate
+    // ---- 2 flows: every lane takes owned rules from a workgroup counter and walks each rule's runs
+    // in time order, the rule's record in registers between its runs.  A lane that finishes a rule
+    // takes the next one at once, so the wave's iterations follow the workgroup's total runs, not its
+    // slowest lane's share of statically assigned rules.
+    const uint32_t nfw = (dbg & 1) ? 0u : nf;
+    uint32_t f = threadIdx.x, r = 0, r1 = 0, s = 0;
+    SlotParam P;
+    Rec R{nullptr, 0};
+    double thr = 0;
+    int64_t qbase = 0;
+    RecCarry<10> rc;
+    rc.have = false;
+    auto take_rule = [&]() {
+        r = fheads[f];
+        r1 = f + 1 < nf ? fheads[f + 1] : E;
+        s = fslot[f];
+        if (r1 - r >= cand_floor) {  // next batch's hot-set candidate
             const uint32_t k = atomicAdd(&s_ncand, 1u);
             if (k < (uint32_t)kFzThreads) {
                 s_cand[2 * k] = s;
-                s_cand[2 * k + 1] = r1 - r0;
+                s_cand[2 * k + 1] = r1 - r;
             }
         }
-        SlotParam P;
         if (st.uni_S) {
             // uniform geometry: the record address and the window geometry without the parameter
             // load; only the threshold is loaded, beside the record's loads
@@ -1089,48 +1115,53 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
         } else {
             P = st.param[s];
         }
-        const Rec R = rec_of(st, P);
-        const double thr = simple ? P.thr_simple : P.thr;
-        const int64_t qbase = div_pos(ts_base, P.W);
-        for (uint32_t r = r0; r < r1;) {
-            RunIn ri;
-            ri.j0 = r;
-            if (r - h0 < (uint32_t)kFzChunk) {
-                ri.n = rl_n[r - h0];
-                ri.cp_tot = rl_cp[r - h0];
-                ri.p0 = rl_p0[r - h0];
-                const uint32_t ab = rl_ab[r - h0];
-                ri.a = (int32_t)(ab & 0xFFu);
-                ri.bd = ab >> 8;
-            } else {
-                ri.n = sc.run_start[r];
-                ri.cp_tot = sc.run_cp[r];
-                ri.p0 = sc.run_p0[r];
-                ri.a = sc.run_acq[r];
-                ri.bd = sc.run_bd[r];
+        R = rec_of(st, P);
+        thr = simple ? P.thr_simple : P.thr;
+        qbase = div_pos(ts_base, P.W);
+        rc.have = false;
+    };
+    bool live = f < nfw;
+    if (live) take_rule();
+    while (live) {
+        RunIn ri;
+        ri.j0 = r;
+        if (r - h0 < (uint32_t)kFzChunk) {
+            ri.n = rl_n[r - h0];
+            ri.cp_tot = rl_cp[r - h0];
+            ri.p0 = rl_p0[r - h0];
+            const uint32_t ab = rl_ab[r - h0];
+            ri.a = (int32_t)(ab & 0xFFu);
+            ri.bd = ab >> 8;
+        } else {
+            ri.n = sc.run_start[r];
+            ri.cp_tot = sc.run_cp[r];
+            ri.p0 = sc.run_p0[r];
+            ri.a = sc.run_acq[r];
+            ri.bd = sc.run_bd[r];
+        }
+        // prioritized requests among the run's first k: plist[p0 .. p0 + cp_tot) holds the
+        // run's prioritized positions (ascending)
+        auto prio_before = [&](uint32_t k) -> uint32_t {
+            uint32_t lo = 0, hi = ri.cp_tot;
+            while (lo < hi) {
+                const uint32_t m = (lo + hi) >> 1;
+                if (sc.plist[ri.p0 + m] < ri.j0 + k) lo = m + 1;
+                else hi = m;
             }
-            // prioritized requests among the run's first k: plist[p0 .. p0 + cp_tot) holds the
-            // run's prioritized positions (ascending)
-            auto prio_before = [&](uint32_t k) -> uint32_t {
-                uint32_t lo = 0, hi = ri.cp_tot;
-                while (lo < hi) {
-                    const uint32_t m = (lo + hi) >> 1;
-                    if (sc.plist[ri.p0 + m] < ri.j0 + k) lo = m + 1;
-                    else hi = m;
-                }
-                return lo;
-            };
-            RunOut ro;
-            // sampleCount <= 10 (the default, every C3 rule) issues exactly ten pair loads: the
-            // 16-pair form re-reads the last pair six times, and the flows phase is bound by the
-            // number of load requests in flight
-            const bool fast = P.S <= 10 ? run_fast<decltype(prio_before), 10>(st, P, R, thr, qbase, ri, prio_before, ro)
-                                        : run_fast(st, P, R, thr, qbase, ri, prio_before, ro);
-            if (fast) {
-                sc.run_out[r] = ro;
-                r += ri.n;
-                continue;
-            }
+            return lo;
+        };
+        RunOut ro;
+        // sampleCount <= 10 (the default, every C3 rule): ten pair registers carried between runs;
+        // larger sampleCounts load the pairs every run
+        bool fast;
+        if (P.S <= 10) {
+            fast = run_fast<decltype(prio_before), 10>(st, P, R, thr, qbase, ri, prio_before, ro, rc);
+        } else {
+            RecCarry<0> rc0;
+            rc0.have = false;
+            fast = run_fast<decltype(prio_before), 0>(st, P, R, thr, qbase, ri, prio_before, ro, rc0);
+        }
+        if (!fast) {
             for (uint32_t j = r; j < r + ri.n; ++j) {
                 const uint32_t i = el_idx(el[j]);
                 const int64_t t = ts_base + (int64_t)ts_off[i];
@@ -1138,8 +1169,14 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
                 out[i] = request_exact(st, s, t, acquire[i], p, simple);
             }
             ro.mode = RUN_DONE;
-            sc.run_out[r] = ro;
-            r += ri.n;
+            rc.have = false;  // the record changed in memory
+        }
+        sc.run_out[r] = ro;
+        r += ri.n;
+        if (r >= r1) {
+            f = atomicAdd(&s_next, 1u);
+            live = f < nfw;
+            if (live) take_rule();
         }
     }
     __syncthreads();  // run_out of every owned run
@@ -1699,7 +1736,9 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
         }
         __syncthreads();
         if (active) {
-            // codes: in-wave ranks -> in-segment ranks; prioritized hot requests join the sub's elements
+            // codes: in-wave ranks -> in-segment ranks; prioritized hot requests go to the sub's
+            // prioritized buffer (their own sort by hot id, beside the cold sort)
+            uint32_t npc = 0;
 #pragma unroll
             for (int r = 0; r < kSubRounds; ++r) {
                 const uint32_t i = ubase + (uint32_t)r * 64 + lane;
@@ -1710,14 +1749,15 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                 const bool pr = hot && (cd >> 31);
                 if (i < send) sc.hcode[i] = hot ? ((cd & ~(0x1FFFu << 12)) | (r_seg << 12)) : kNoCode;
                 const uint64_t em = __ballot(pr);
-                if (pr) {
-                    sc.el_tile[(size_t)ubase + nc + (uint32_t)__popcll(em & lt)] =
-                        el_pack(st.nslots + 1 + hid, r_seg >> 7, 1u, r_seg & 127u, i);
-                    if (d0) atomicAdd(&sh.hist0[wave >> 2][(st.nslots + 1 + hid) & dmask], 1u);
-                }
-                nc += (uint32_t)__popcll(em);
+                if (pr) sc.pel_tile[(size_t)ubase + npc + (uint32_t)__popcll(em & lt)] = el_pack(hid, r_seg >> 7, 1u, r_seg & 127u, i);
+                npc += (uint32_t)__popcll(em);
             }
+            if (lane == 0) sc.ptile_np[sub] = npc;
+        } else if (lane == 0) {
+            sc.ptile_np[sub] = 0u;
         }
+    } else if (lane == 0) {
+        sc.ptile_np[sub] = 0u;  // no hot set (or the re-classifying pass): nothing prioritized to sort
     }
     if (lane == 0) sc.tile_nc[sub] = active ? nc : 0u;  // totals: k_hot_mode
     if (d0) {  // the sort's first-pass histogram rows of this segment's two tiles
@@ -1780,9 +1820,9 @@ __global__ __launch_bounds__(1024) void k_hot_mode(BatchScratch sc, uint32_t nsu
             b += red[1][w];
             m = max(m, red[2][w]);
         }
-        sc.counters[CTL_NSORT] = a;
+        sc.counters[CTL_NSORT] = a;  // the compaction segments hold the cold elements only
         sc.counters[CTL_NPRIO] = b;
-        sc.counters[CTL_NCOLD] = a - b;
+        sc.counters[CTL_NCOLD] = a;
         sc.counters[CTL_BDHI] = m;
         sc.counters[CTL_MODE] = nhot ? 1u : 0u;
     }
@@ -1860,11 +1900,10 @@ __global__ __launch_bounds__(kThreads) void k_hot_pre(BatchScratch sc) {
 __global__ __launch_bounds__(kThreads) void k_prio_rank(ClusterState st, BatchScratch sc,
                                                         const uint64_t *__restrict__ el) {
     if (!sc.counters[CTL_MODE]) return;
-    const uint32_t np = sc.counters[CTL_NPRIO], base = sc.counters[CTL_NCOLD];
-    const uint32_t key0 = st.nslots + 1;
+    const uint32_t np = sc.counters[CTL_NPRIO], base = 0;
     for (uint32_t j = blockIdx.x * kThreads + threadIdx.x; j < np; j += gridDim.x * kThreads) {
         const uint64_t e = el[base + j];
-        const uint32_t h = el_slot(e) - key0;
+        const uint32_t h = el_slot(e);
         const uint32_t r_in = (((uint32_t)(e >> kBdShift) & kBdEsc) << 7) | (uint32_t)((e >> kAcqShift) & kAcqMax);
         const uint32_t seg = el_idx(e) / (uint32_t)kHotSeg;
         sc.prank[j] = sc.hbase[(size_t)seg * kHot + h] + r_in;
@@ -2069,12 +2108,12 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
 __device__ __forceinline__ void prio_results_range(const ClusterState &st, const BatchScratch &sc,
                                                    const uint64_t *__restrict__ el, uint64_t *__restrict__ out,
                                                    uint32_t j0, uint32_t stride) {
-    const uint32_t np = sc.counters[CTL_NPRIO], base = sc.counters[CTL_NCOLD];
+    const uint32_t np = sc.counters[CTL_NPRIO];
     const uint32_t bd_lo = sc.counters[CTL_BDLO];
     const uint32_t bd_hi = min(sc.counters[CTL_BDHI], (uint32_t)kHotBuckets - 1);
     for (uint32_t j = j0; j < np; j += stride) {
-        const uint64_t e = el[base + j];
-        const uint32_t h = el_slot(e) - (st.nslots + 1);
+        const uint64_t e = el[j];
+        const uint32_t h = el_slot(e);
         const uint32_t rank = sc.prank[j];
         uint32_t b = bd_lo;
         for (; b < bd_hi; ++b)
@@ -3015,6 +3054,10 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up((size_t)nslots_cap * 2) + 2 * align_up(kHot * 4) + align_up(kHotCtlWords * 4);  // hot_of/slot/next/ctl
     b += align_up(segs_alloc * kHotSeg * 8);                                       // el_tile
     b += align_up(segs_alloc * kSubPerSeg * 4);                                    // tile_nc
+    b += align_up(segs_alloc * kHotSeg * 8) + align_up(segs_alloc * kSubPerSeg * 4);  // pel_tile, ptile_np
+    b += 2 * align_up(cap * 8);                                                    // pel (double buffer)
+    b += 2 * align_up(hist * 4) + align_up(scan_partials_needed(hist) * 4 + 64);   // radix_p
+    b += align_up(kRadixGhistWords * 4) + align_up(64);                            // radix_p row totals, flag
     b += align_up(segs_alloc * kHotSeg * 4);                                       // hcode
     b += align_up(segs_alloc * kHot * 2) + align_up(segs_alloc * kHot * 4);        // hcnt, hbase
     b += align_up(hot_groups(cap) * kHot * 4);                                     // hgsum
@@ -3073,6 +3116,15 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.hot_ctl = (uint32_t *)take(kHotCtlWords * 4);
     sc.el_tile = (uint64_t *)take(segs_alloc * kHotSeg * 8);
     sc.tile_nc = (uint32_t *)take(segs_alloc * kSubPerSeg * 4);
+    sc.pel_tile = (uint64_t *)take(segs_alloc * kHotSeg * 8);
+    sc.ptile_np = (uint32_t *)take(segs_alloc * kSubPerSeg * 4);
+    sc.pel[0] = (uint64_t *)take(cap * 8);
+    sc.pel[1] = (uint64_t *)take(cap * 8);
+    sc.radix_p.hist = (uint32_t *)take(hist * 4);
+    sc.radix_p.hist_scan = (uint32_t *)take(hist * 4);
+    sc.radix_p.partial = (uint32_t *)take(scan_partials_needed(hist) * 4 + 64);
+    sc.radix_p.ghist = (uint32_t *)take(kRadixGhistWords * 4);  // the tiled sort's per-digit row totals
+    sc.radix_p.err = (uint32_t *)take(64);
     sc.hcode = (uint32_t *)take(segs_alloc * kHotSeg * 4);
     sc.hcnt = (uint16_t *)take(segs_alloc * kHot * 2);
     sc.hbase = (uint32_t *)take(segs_alloc * kHot * 4);
@@ -3209,24 +3261,23 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, hs, sc, ngroups);
     hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
     hipLaunchKernelGGL(k_hot_pre, dim3(kHotBuckets), dim3(kThreads), 0, hs, sc);
-    const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
-                                        kSlotShift, bits, sc.radix, s, d0 > 0);
-    const uint64_t *el = (np & 1) ? sc.el[0] : sc.el[1];
+    // the prioritized hot requests, sorted by hot id on their own (12-bit key), then the hot runs and
+    // results: the whole hot side runs beside the cold sort and the cold stage
+    const int npp = radix_sort_u64_tiled(sc.pel_tile, sc.ptile_np, sc.counters + CTL_NPRIO, sc.pel[0], sc.pel[1], n,
+                                         kSlotShift, 12, sc.radix_p, hs, false);
+    const uint64_t *pel = (npp & 1) ? sc.pel[0] : sc.pel[1];
     const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
-    // the hot runs and results once the sort is done (the prioritized hot requests are sorted with
-    // the cold ones), beside the cold stage
-    if (ovl) {
-        SGA_HIP_CHECK(hipEventRecord(sc.ev_fork, s));
-        SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork, 0));
-    }
-    hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, el);
+    hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, pel);
     hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, hs, st, sc, ts_base);
     if (ovl) {
         SGA_HIP_CHECK(hipEventRecord(sc.ev_mid, hs));  // the hot runs read hot_slot; the next hot set may start
-        hipLaunchKernelGGL(k_hot_final, dim3(nseg + kFinPrioWgs), dim3(kFinWgThreads), 0, hs, st, sc, n, el, out,
+        hipLaunchKernelGGL(k_hot_final, dim3(nseg + kFinPrioWgs), dim3(kFinWgThreads), 0, hs, st, sc, n, pel, out,
                            fin_cache());
         SGA_HIP_CHECK(hipEventRecord(sc.ev_join, hs));
     }
+    const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
+                                        kSlotShift, bits, sc.radix, s, d0 > 0);
+    const uint64_t *el = (np & 1) ? sc.el[0] : sc.el[1];
     cold_stage(st, sc, el, n, sc.counters + CTL_NCOLD, invalid_key, acquire, prio, ts_off, ts_base, 0,
                std::max<uint32_t>(sc.hot_min, 1), out, s);
     if (fz_debug() & 16) {  // profiling only: k_cold_fused phase cycles per workgroup
@@ -3240,7 +3291,7 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
                     ph[7], (double)ph[0] / ph[7], (double)ph[1] / ph[7], (double)ph[2] / ph[7]);
     }
     if (!ovl) {
-        hipLaunchKernelGGL(k_hot_final, dim3(nseg + kFinPrioWgs), dim3(kFinWgThreads), 0, s, st, sc, n, el, out,
+        hipLaunchKernelGGL(k_hot_final, dim3(nseg + kFinPrioWgs), dim3(kFinWgThreads), 0, s, st, sc, n, pel, out,
                            fin_cache());
     } else if (!tail_early()) {
         SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_join, 0));

@@ -126,9 +126,9 @@ constexpr int kHotCand = 1 << 16;   // next-hot-set candidates gathered per batc
 enum : int {
     CTL_NVALID = 0, CTL_NRUNS = 1, CTL_NFLOWS = 2, CTL_LIMITED = 4, CTL_LIMRUNS = 5, CTL_DEFERRED = 6,
     CTL_FLAGS = 16,      // hot-path fallback reasons (kFlag*)
-    CTL_NPRIO = 19,      // prioritized hot requests (pass 0)
-    CTL_NSORT = 20,      // elements to sort
-    CTL_NCOLD = 21,      // cold elements (the sorted prefix the run kernels read)
+    CTL_NPRIO = 19,      // prioritized hot requests (pass 0; sorted on their own)
+    CTL_NSORT = 20,      // elements to sort (the cold ones)
+    CTL_NCOLD = 21,      // cold elements (the sorted elements the run kernels read)
     CTL_NPRE = 22,       // hot buckets starting inside a rank segment (k_hot_pre rows)
     CTL_BDLO = 23,       // hot bucket delta of the batch's first request
     CTL_BDHI = 24,       // largest hot bucket delta
@@ -182,9 +182,12 @@ struct BatchScratch {
     uint32_t *hot_ctl;        // [0] hot ids in use [1] picks [2] hot window length [3] next window length
                               // [4..5] best (count << 32 | slot) [6] candidates [7] last pick threshold
                               // [8..40) log2 count bins
-    uint64_t *el_tile;        // classify output per 1024-request segment: cold elements + prioritized hot
-                              // requests (hot key), arrival order
+    uint64_t *el_tile;        // classify output per 1024-request segment: cold elements, arrival order
     uint32_t *tile_nc;        // per 1024-request segment: elements
+    uint64_t *pel_tile;       // per 1024-request segment: the prioritized hot requests (key = hot id), arrival order
+    uint32_t *ptile_np;       // per 1024-request segment: prioritized hot requests
+    uint64_t *pel[2];         // the prioritized hot requests sorted by hot id (double buffer of their own sort)
+    RadixScratch radix_p;     // the prioritized sort's scratch (it runs on the side stream beside the cold sort)
     uint32_t *hcode;          // per request: hot id | in-segment rank << 12 | bucket << 25 | prioritized << 31
                               // (~0: not a hot request)
     uint16_t *hcnt;           // [segment][kHot] hot requests per hot id
@@ -195,7 +198,7 @@ struct BatchScratch {
     HotRun *hrun;             // [kHotBuckets][kHot]
     uint4 *hfin;              // [kHotBuckets][kHot]: (s0, f, start) of each hot run, what k_hot_final caches
     double2 *hthr;            // [kHot] threshold and intervalInSecond of each hot rule (k_hot_flows)
-    uint32_t *prank;          // per prioritized hot request (sorted region order): its rank
+    uint32_t *prank;          // per prioritized hot request (order of pel): its rank among its rule's requests
     uint32_t *plo, *phi;      // per hot id: its range in the prioritized region
     uint32_t *hot_tot;        // per hot id: requests in the batch
     WConst *wconst;           // [256] per window-length code

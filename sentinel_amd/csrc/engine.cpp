@@ -500,7 +500,8 @@ struct Engine {
                 }
                 uni = p.S == S0 && p.W == W0 && p.interval == I0 && (uint64_t)p.boff == (uint64_t)i * (uint64_t)(S0 + 1);
             }
-            if (uni && S0 > 0 && S0 <= 64) {
+            static const bool no_uni = getenv("SGA_NO_UNI") && atoi(getenv("SGA_NO_UNI"));  // A/B knob
+            if (uni && !no_uni && S0 > 0 && S0 <= 64) {
                 uni_S = S0;
                 uni_W = W0;
                 uni_iv = I0;

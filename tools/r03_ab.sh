@@ -8,5 +8,5 @@ i=0
 for cfg in "$@"; do
   i=$((i+1))
   python3 tools/timeline.py gpurun_out/$tag/trace_$i.csv 4 | grep -v copyBuffer > gpurun_out/$tag/timeline_$i.txt
-  grep -h "fz phases" gpurun_out/$tag/run_$i.err | tail -2
+  grep -h "fz phases" gpurun_out/$tag/run_$i.err | tail -2 || true
 done
