@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 25, help="oracle replay sample (requests)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) batches")
-    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c5a", "c5b"],
+    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c4full", "c5a", "c5b"],
                     help="BASELINE.json configuration (SURVEY.md 8(d)); c3 = the headline, the others run on one "
                          "GPU through bench_local.py")
     return ap.parse_args()
@@ -74,7 +74,7 @@ def main():
     args = parse()
     if args.config != "c3":
         if args.gpus != 1:
-            raise SystemExit("bench.py: --config c1/c2/c4/c5a/c5b run on one GPU")
+            raise SystemExit("bench.py: --config c1/c2/c4/c4full/c5a/c5b run on one GPU")
         import bench_local
         bench_local.run(args)
         return

@@ -88,6 +88,10 @@ def _cfg_c2(rng):
 
 
 def _cfg_c4(rng):
+    return _cfg_c4_common(rng, fold=True)
+
+
+def _cfg_c4_common(rng, fold):
     n_res, n = 10_000, 1 << 22
     param = []
     for r in range(n_res):
@@ -96,12 +100,22 @@ def _cfg_c4(rng):
             p.update(control_behavior=2, max_queueing_time_ms=0)
         param.append(p)
     res = _zipf(rng, n_res, n)
-    vals = _zipf(rng, 10_000_000, n) % 4000  # pinned mode: <= 4000 keys per rule (no CacheMap eviction)
+    vals = _zipf(rng, 10_000_000, n)
+    if fold:
+        vals = vals % 4000  # pinned mode: <= 4000 keys per rule (no CacheMap eviction)
     ts = T0 + np.arange(n) // 10_000
     b = Batch(res, ts, flags=np.full(n, EV_HAS_PARAM), param=vals, exit_rt=rng.integers(1, 30, size=n))
     return dict(name="C4 10k ParamFlowRules (90% default / 10% throttle), Zipf(1.1) values over 10^7 folded to "
                      "<= 4000 per rule (pinned mode), 2^22 entries + exits per batch",
                 n_res=n_res, param=param, batch=b, sample=1 << 20)
+
+
+def _cfg_c4full(rng):
+    cfg = _cfg_c4_common(rng, fold=False)
+    cfg["name"] = ("C4 full mode: 10k ParamFlowRules (90% default / 10% throttle), Zipf(1.1) values over 10^7 "
+                   "unfolded (the CacheMaps hold their min(4000 * duration, 200000) most recently used values and "
+                   "evict: strict LRU), 2^22 entries + exits per batch")
+    return cfg
 
 
 def _cfg_c5b(rng):
@@ -257,8 +271,8 @@ def run_local(args, cfg_name):
     import torch
     from sentinel_amd.cluster import Engine
     from sentinel_amd.local import LocalSentinel
-    rng = np.random.default_rng({"c1": 101, "c2": 102, "c4": 104, "c5b": 105}[cfg_name])
-    cfg = {"c1": _cfg_c1, "c2": _cfg_c2, "c4": _cfg_c4, "c5b": _cfg_c5b}[cfg_name](rng)
+    rng = np.random.default_rng({"c1": 101, "c2": 102, "c4": 104, "c4full": 104, "c5b": 105}[cfg_name])
+    cfg = {"c1": _cfg_c1, "c2": _cfg_c2, "c4": _cfg_c4, "c4full": _cfg_c4full, "c5b": _cfg_c5b}[cfg_name](rng)
     b = cfg["batch"]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)

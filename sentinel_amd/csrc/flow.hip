@@ -51,6 +51,7 @@ struct Ctx {
     int8_t pre_param;   // k_lheavy: that rule's check already decided by the value's lane (1 pass, 2 block)
     int64_t pre_wait;   // its wait
     const ResDev *res;  // k_lheavy: the resource's record, held by the replaying lane (null: st.res)
+    uint64_t *pstamp_ref;  // k_lheavy: the LDS stamp of pentry (its last access)
 };
 
 // ------------------------------------------------------------------ MetricBucket windows
@@ -373,6 +374,113 @@ __device__ PEntry *ptab_insert_absent(PEntry *tab, uint32_t mask, uint32_t owner
 __device__ __forceinline__ int64_t lwrap_mul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
 __device__ __forceinline__ int64_t lwrap_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
 
+// thread-count map owner of (resource r, argument index k): resource + 1 for index 0
+__device__ __forceinline__ uint32_t tmap_owner(uint32_t r, uint32_t k) { return (r + 1) | (k << 24); }
+
+// ------------------------------------------------------------------ CacheMap capacity (strict LRU)
+// ParameterMetric's maps (ParameterMetric.java:37-39,95-121) are ConcurrentLinkedHashMapWrappers of a fixed
+// capacity (CLHM 1.4.2, not vendored: restated as strict LRU, oracle/oracle_ext.c lru_*).  flow.hpp LruRec
+// describes the free / LRU modes.  A key access = CacheMap.get / putIfAbsent / put of a present key; an
+// insert = putIfAbsent / put of an absent one; a remove = the thread-count map's remove at zero.
+__device__ __forceinline__ uint64_t lru_stamp(const FlowState &st, uint32_t eidx, uint32_t q) {
+    return ((st.seq_base + eidx) << 16) | (uint64_t)min(q, 0xFFFFu);
+}
+
+struct MapRef {  // one owner's map
+    PEntry *tab;
+    uint64_t *stamp;
+    uint32_t mask, owner;
+    uint32_t *size;
+    uint64_t *q;
+    uint32_t cap;
+    uint32_t *overflow;
+};
+__device__ __forceinline__ MapRef map_ref_p(const FlowState &st, const ParamRuleDev &p) {
+    return MapRef{st.ptab, st.pstamp, st.pmask, p.id + 1, st.psize + p.id, st.pq + p.id, p.cap, st.overflow};
+}
+__device__ __forceinline__ MapRef map_ref_t(const FlowState &st, uint32_t r, uint32_t k) {
+    const uint32_t j = st.tbase[r] + k;
+    return MapRef{st.ttab, st.tstamp, st.tmask, tmap_owner(r, k), st.tsize + j, st.tq + j, kThreadMapCap, st.overflow};
+}
+__device__ __forceinline__ bool lru_on_p(const FlowState &st) { return st.pstamp != nullptr; }
+__device__ __forceinline__ bool lru_on_t(const FlowState &st, uint32_t r) {
+    return st.tstamp != nullptr && st.tbase != nullptr && st.tbase[r] != kNoTBase;
+}
+
+// LRU-mode queues: the owner is decided by one lane, plain loads and stores.  The area is
+// [meta {head, tail}][2 cap + 2 records]; a record is live while its key is present with its stamp.
+__device__ __forceinline__ uint64_t lru_qcap(const MapRef &m) { return 2ull * m.cap + 2; }
+__device__ __forceinline__ bool lru_live(const MapRef &m, const LruRec &rec, PEntry **pe) {
+    PEntry *e = ptab_get(m.tab, m.mask, m.owner, rec.value, false, m.overflow);
+    if (!e || e->a == kPAbsent || m.stamp[e - m.tab] != rec.stamp) return false;
+    *pe = e;
+    return true;
+}
+__device__ void lru_compact(const MapRef &m, LruRec *area) {
+    const uint64_t qcap = lru_qcap(m);
+    uint64_t w = area[0].value;
+    for (uint64_t i = area[0].value; i < area[0].stamp; ++i) {
+        const LruRec rec = area[1 + i % qcap];
+        PEntry *e;
+        if (lru_live(m, rec, &e)) area[1 + (w++) % qcap] = rec;
+    }
+    area[0].stamp = w;
+}
+__device__ void lru_push(const FlowState &st, const MapRef &m, uint64_t value, uint64_t stamp) {
+    LruRec *area = st.lpool + *m.q;
+    const uint64_t qcap = lru_qcap(m);
+    if (area[0].stamp - area[0].value >= qcap) lru_compact(m, area);  // live records <= cap + 1
+    if (area[0].stamp - area[0].value >= qcap) {
+        atomicOr(&st.lru_ctl[1], 2u);
+        atomicOr(st.overflow, 1u);
+        return;
+    }
+    area[1 + area[0].stamp % qcap] = LruRec{value, stamp};
+    area[0].stamp += 1;
+}
+// a full map's least recently used key (CLHM evicts after the insert that overflows it)
+__device__ void lru_evict(const FlowState &st, const MapRef &m) {
+    LruRec *area = st.lpool + *m.q;
+    const uint64_t qcap = lru_qcap(m);
+    while (area[0].value < area[0].stamp) {
+        const LruRec rec = area[1 + area[0].value % qcap];
+        area[0].value += 1;
+        PEntry *e;
+        if (lru_live(m, rec, &e)) {
+            e->a = kPAbsent;
+            e->b = kPAbsent;
+            *m.size -= 1;
+            return;
+        }
+    }
+    atomicOr(&st.lru_ctl[1], 2u);  // a full map without a live record: never expected
+    atomicOr(st.overflow, 1u);
+}
+// kLru: the caller may hold owners in LRU mode (k_llru, k_lseq: one lane per owner); the parallel kernels
+// only ever see free-mode owners (the count pass routes the others away) and compile without the queues
+template <bool kLru>
+__device__ __forceinline__ void lru_touch(const FlowState &st, const MapRef &m, PEntry *e, uint64_t stamp) {
+    m.stamp[e - m.tab] = stamp;
+    if (kLru && *m.q != kNoQueue) lru_push(st, m, e->value, stamp);
+}
+// e absent (a == kPAbsent) and about to be set present by the caller
+template <bool kLru>
+__device__ __forceinline__ void lru_insert(const FlowState &st, const MapRef &m, PEntry *e, uint64_t stamp) {
+    m.stamp[e - m.tab] = stamp;
+    if (!kLru || *m.q == kNoQueue) {  // free mode: the count pass guarantees room; lanes of one owner may add together
+        atomicAdd(m.size, 1u);
+        return;
+    }
+    *m.size += 1;
+    lru_push(st, m, e->value, stamp);
+    if (*m.size > m.cap) lru_evict(st, m);
+}
+template <bool kLru>
+__device__ __forceinline__ void lru_remove(const MapRef &m) {
+    if (!kLru || *m.q == kNoQueue) atomicSub(m.size, 1u);
+    else *m.size -= 1;
+}
+
 __device__ bool hot_lookup(const Ctx &c, const ParamRuleDev &p, uint64_t v, int64_t *thr) {
     for (int i = 0; i < p.n_hot; ++i)
         if (c.st.hot_v[p.hot_off + i] == v) {
@@ -447,16 +555,36 @@ __device__ __forceinline__ bool param_pass_qps(const Ctx &c, const ParamRuleDev 
     }
 }
 
+// whether a QPS check of value v reaches the rule's maps: not for a zero threshold, nor (token bucket)
+// for acquireCount > maxCount (ParamFlowChecker.java:137-154, 230-234)
+__device__ __forceinline__ bool param_map_access(const Ctx &c, const ParamRuleDev &p, uint64_t v, int acquire) {
+    int64_t token_count = j_d2l(p.count), hot;
+    if (hot_lookup(c, p, v, &hot)) token_count = hot;
+    if (token_count == 0) return false;
+    return p.behavior == 2 || (int64_t)acquire <= lwrap_add(token_count, p.burst);
+}
+
+template <bool kLru>
 __device__ bool param_pass(const Ctx &c, const ParamRuleDev &p, uint64_t v, int acquire, int64_t t,
-                           int64_t thread_count, int64_t *wait_ms) {
+                           int64_t thread_count, int64_t *wait_ms, uint64_t stamp) {
     *wait_ms = 0;
     int64_t hot;
     if (p.grade == 1) {
         int64_t token_count = j_d2l(p.count);
         if (hot_lookup(c, p, v, &hot)) token_count = hot;
         if (token_count == 0) return false;  // before any map access, as the reference
-        PEntry *e = c.pentry ? c.pentry : ptab_get(c.st.ptab, c.st.pmask, p.id + 1, v, true, c.st.overflow);
+        const bool access = p.behavior == 2 || (int64_t)acquire <= lwrap_add(token_count, p.burst);
+        if (c.pentry) {  // k_lheavy's LDS copy (free mode): its stamp beside it, its count at the write-back
+            if (access && c.pstamp_ref) *c.pstamp_ref = stamp;
+            return param_pass_qps(c, p, *c.pentry, v, acquire, t, wait_ms);
+        }
+        PEntry *e = ptab_get(c.st.ptab, c.st.pmask, p.id + 1, v, true, c.st.overflow);
         if (!e) return false;
+        if (access && lru_on_p(c.st)) {  // time map then token map: the same key sequence, one recency order
+            const MapRef m = map_ref_p(c.st, p);
+            if (e->a == kPAbsent) lru_insert<kLru>(c.st, m, e, stamp);
+            else lru_touch<kLru>(c.st, m, e, stamp);
+        }
         return param_pass_qps(c, p, *e, v, acquire, t, wait_ms);
     }
     if (p.grade == 0) {
@@ -612,13 +740,11 @@ __device__ __forceinline__ int ev_arg(const PArgs &pa, uint32_t k, const uint64_
     return ARG_SCALAR;
 }
 
-// thread-count map owner of (resource r, argument index k): resource + 1 for index 0
-__device__ __forceinline__ uint32_t tmap_owner(uint32_t r, uint32_t k) { return (r + 1) | (k << 24); }
-
 // ParameterMetric.addThreadCount / decreaseThreadCount (ParameterMetric.java:125-230): every argument
 // index with a thread-count map, every element of a Collection / array, null arguments skipped
+template <bool kLru>
 __device__ void param_threads(const Ctx &c, uint32_t r, const PArgs &pa, bool has_param, const uint64_t &param,
-                              int delta) {
+                              int delta, uint32_t eidx) {
     const uint64_t mask = c.st.tmapmask ? c.st.tmapmask[r] : 0ull;
     if (!mask) return;
     const uint32_t na = min(ev_nargs(pa, has_param), (uint32_t)kMaxParamIdx);
@@ -630,12 +756,21 @@ __device__ void param_threads(const Ctx &c, uint32_t r, const PArgs &pa, bool ha
         for (uint32_t q = 0; q < nv; ++q) {
             PEntry *te = ptab_get(c.st.ttab, c.st.tmask, tmap_owner(r, k), vals[q], true, c.st.overflow);
             if (!te) continue;
-            if (delta > 0) {
-                te->a = (te->a == kPAbsent ? 0 : te->a) + 1;
-            } else if (te->a == kPAbsent) {
-                te->a = 0;  // putIfAbsent(value, new AtomicInteger())
-            } else if (--te->a <= 0) {
-                te->a = kPAbsent;  // remove(value)
+            const bool lru = lru_on_t(c.st, r);
+            MapRef m{};
+            if (lru) m = map_ref_t(c.st, r, k);
+            const uint64_t stamp = lru_stamp(c.st, eidx, q);
+            if (te->a == kPAbsent) {  // putIfAbsent(value, new AtomicInteger()) inserts
+                if (lru) lru_insert<kLru>(c.st, m, te, stamp);
+                te->a = delta > 0 ? 1 : 0;  // then put(value, new AtomicInteger(1)); a decrease leaves 0
+            } else {
+                if (lru) lru_touch<kLru>(c.st, m, te, stamp);
+                if (delta > 0) {
+                    te->a += 1;
+                } else if (--te->a <= 0) {
+                    te->a = kPAbsent;  // remove(value)
+                    if (lru) lru_remove<kLru>(m);
+                }
             }
         }
     }
@@ -654,25 +789,31 @@ __device__ __forceinline__ int32_t param_idx_of(ParamRuleDev &p, uint32_t nargs)
 
 // ParamFlowChecker.passLocalCheck (ParamFlowChecker.java:79-106): every element must pass, in order
 // (elements before a failing one keep their token updates)
+template <bool kLru>
 __device__ bool param_local_check(const Ctx &c, uint32_t r, ParamRuleDev &p, int32_t idx, const uint64_t *vals,
-                                  uint32_t nv, int acquire, int64_t t, int64_t *total_wait) {
+                                  uint32_t nv, int acquire, int64_t t, int64_t *total_wait, uint32_t eidx) {
     for (uint32_t q = 0; q < nv; ++q) {
         const uint64_t v = vals[q];
+        const uint64_t stamp = lru_stamp(c.st, eidx, q);
         int64_t tc = 0;
-        if (p.grade == 0 && idx < kMaxParamIdx) {  // getThreadCount(rule.getParamIdx(), value)
+        if (p.grade == 0 && idx < kMaxParamIdx) {  // getThreadCount(rule.getParamIdx(), value): CacheMap.get
             PEntry *te = ptab_get(c.st.ttab, c.st.tmask, tmap_owner(r, (uint32_t)idx), v, false, c.st.overflow);
-            tc = (te && te->a != kPAbsent) ? te->a : 0;
+            if (te && te->a != kPAbsent) {
+                tc = te->a;
+                if (lru_on_t(c.st, r)) lru_touch<kLru>(c.st, map_ref_t(c.st, r, (uint32_t)idx), te, stamp);
+            }
         }
         int64_t w = 0;
-        const bool ok = c.pre_param ? (w = c.pre_wait, c.pre_param == 1) : param_pass(c, p, v, acquire, t, tc, &w);
+        const bool ok = c.pre_param ? (w = c.pre_wait, c.pre_param == 1) : param_pass<kLru>(c, p, v, acquire, t, tc, &w, stamp);
         if (!ok) return false;
         *total_wait += w;
     }
     return true;
 }
 
+template <bool kLru = false>
 __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t t, int acquire, bool prio,
-                              bool has_param, uint64_t param, int64_t *wait_ms, PArgs pa = PArgs{nullptr, 0}) {
+                              bool has_param, uint64_t param, int64_t *wait_ms, PArgs pa, uint32_t eidx) {
     const ResDev R = c.res ? *c.res : c.st.res[r];
     int64_t *node = m.node;
     *wait_ms = 0;
@@ -697,9 +838,9 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
             if (c.st.cluster_on) ts = (int8_t)(cparam_request_exact(c.st.cpst, p.cflow, acquire, vals, nv, t) >> 48);
             if (ts == TRS_OK) ok = true;
             else if (ts == TRS_BLOCKED) ok = false;
-            else ok = p.cfallback ? param_local_check(c, r, p, idx, vals, nv, acquire, t, &total_wait) : true;
+            else ok = p.cfallback ? param_local_check<kLru>(c, r, p, idx, vals, nv, acquire, t, &total_wait, eidx) : true;
         } else {
-            ok = param_local_check(c, r, p, idx, vals, nv, acquire, t, &total_wait);
+            ok = param_local_check<kLru>(c, r, p, idx, vals, nv, acquire, t, &total_wait, eidx);
         }
         if (!ok) {
             node_add(c, node, t, MB_BLOCK, acquire);
@@ -747,7 +888,7 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
         }
         if (d == D_PASS_WAIT) {
             node[kNodeThreads] += 1;
-            param_threads(c, r, pa, has_param, param, 1);
+            param_threads<kLru>(c, r, pa, has_param, param, 1, eidx);
             *wait_ms = w;
             return D_PASS_WAIT;
         }
@@ -761,31 +902,36 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
     }
     node[kNodeThreads] += 1;
     node_add(c, node, t, MB_PASS, acquire);
-    param_threads(c, r, pa, has_param, param, 1);
+    param_threads<kLru>(c, r, pa, has_param, param, 1, eidx);
     *wait_ms = total_wait;
     return D_PASS;
 }
 
+template <bool kLru = false>
 __device__ void chain_exit(const Ctx &c, uint32_t r, const ResMem &m, int64_t t, int64_t rt, int count, bool error,
-                           bool has_param, uint64_t param, PArgs pa = PArgs{nullptr, 0}) {
+                           bool has_param, uint64_t param, PArgs pa, uint32_t eidx) {
     const ResDev R = c.res ? *c.res : c.st.res[r];
     int64_t *node = m.node;
     node_add_rt_success(c, node, t, rt, count);
     node[kNodeThreads] -= 1;
     if (error) node_add(c, node, t, MB_EXC, count);
-    param_threads(c, r, pa, has_param, param, -1);  // ParameterMetric.decreaseThreadCount
+    param_threads<kLru>(c, r, pa, has_param, param, -1, eidx);  // ParameterMetric.decreaseThreadCount
     for (uint32_t k = 0; k < R.n_cbs; ++k) cb_on_complete(m.cbs[k], t, rt, error);
 }
 
+// eidx: the event's index in the batch (CacheMap access stamps)
+template <bool kLru = false>
 __device__ __forceinline__ int8_t chain_entry(const Ctx &c, uint32_t r, int64_t t, int acquire, bool prio,
-                                              bool has_param, uint64_t param, int64_t *wait_ms,
-                                              PArgs pa = PArgs{nullptr, 0}) {
-    return chain_entry(c, r, res_global(c, r, c.st.res[r]), t, acquire, prio, has_param, param, wait_ms, pa);
+                                              bool has_param, uint64_t param, int64_t *wait_ms, PArgs pa,
+                                              uint32_t eidx) {
+    return chain_entry<kLru>(c, r, res_global(c, r, c.st.res[r]), t, acquire, prio, has_param, param, wait_ms, pa,
+                             eidx);
 }
 
+template <bool kLru = false>
 __device__ __forceinline__ void chain_exit(const Ctx &c, uint32_t r, int64_t t, int64_t rt, int count, bool error,
-                                           bool has_param, uint64_t param, PArgs pa = PArgs{nullptr, 0}) {
-    chain_exit(c, r, res_global(c, r, c.st.res[r]), t, rt, count, error, has_param, param, pa);
+                                           bool has_param, uint64_t param, PArgs pa, uint32_t eidx) {
+    chain_exit<kLru>(c, r, res_global(c, r, c.st.res[r]), t, rt, count, error, has_param, param, pa, eidx);
 }
 
 // ------------------------------------------------------------------ SystemSlot / ENTRY_NODE
@@ -930,7 +1076,7 @@ __global__ void k_lseq(FlowState st, int64_t max_rt, SysDev sys, const uint8_t *
             pa = PArgs{pvals + (param_in[i] >> 32), (uint32_t)param_in[i]};
         }
         if (kind[i] == 1) {
-            chain_exit(c, r, t, rt_in[i], a, (fl & SGA_EV_ERROR) != 0, hp, param_in[i], pa);
+            chain_exit<true>(c, r, t, rt_in[i], a, (fl & SGA_EV_ERROR) != 0, hp, param_in[i], pa, i);
             if (in) entry_node_after_exit(c, t, rt_in[i], a, (fl & SGA_EV_ERROR) != 0);
             continue;
         }
@@ -946,7 +1092,7 @@ __global__ void k_lseq(FlowState st, int64_t max_rt, SysDev sys, const uint8_t *
             d = D_BLOCK_SYSTEM;
             w = sb;  // block detail: the SystemRule check
         } else {
-            d = chain_entry(c, r, t, a, (fl & SGA_EV_PRIORITIZED) != 0, hp, param_in[i], &w, pa);
+            d = chain_entry<true>(c, r, t, a, (fl & SGA_EV_PRIORITIZED) != 0, hp, param_in[i], &w, pa, i);
         }
         if (in) entry_node_after_entry(c, t, a, d);
         decision[i] = d;
@@ -1479,11 +1625,12 @@ __device__ void lane_run(const Ctx &c, int64_t max_rt, FlowScratch &sc, const Pa
             const bool hp = (q.idx & F_PARAM) != 0;
             const uint64_t pv = hp ? param_in[idx] : 0;
             if (q.idx & F_EXIT) {
-                chain_exit(c, res, t, rt_in[idx], (int)(q.acq_prio & 0x7FFFFFFFu), (q.idx & F_ERROR) != 0, hp, pv);
+                chain_exit(c, res, t, rt_in[idx], (int)(q.acq_prio & 0x7FFFFFFFu), (q.idx & F_ERROR) != 0, hp, pv,
+                           PArgs{nullptr, 0}, idx);
             } else {
                 int64_t w = 0;
                 decision[idx] = chain_entry(c, res, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
-                                            hp, pv, &w);
+                                            hp, pv, &w, PArgs{nullptr, 0}, idx);
                 wait_ms[idx] = (int32_t)w;
             }
         }
@@ -1561,6 +1708,10 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
         {  // a long event-by-event replay goes to k_lheavy (its state in LDS)
             const uint32_t res = sc.run_slot[r0];
             const uint32_t nev = sc.run_end[r1 - 1] - sc.run_start[r0];
+            if (st.lru_res && st.lru_res[res]) {  // a CacheMap in LRU mode: arrival order, one lane (k_llru)
+                sc.lru[atomicAdd(&sc.counters[10], 1u)] = fl;
+                continue;
+            }
             if ((st.res[res].fast & 5u) == 0 && nev >= kHeavyEvents) {
                 sc.heavy[atomicAdd(&sc.counters[8], 1u)] = fl;
                 continue;
@@ -1868,6 +2019,10 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
     __shared__ uint32_t lgi[kHeavySlots];   // map index of the slot's entry
     __shared__ PEntry tent[kHeavySlots];    // per-value lanes: the value's thread-count entry (ParameterMetric)
     __shared__ uint32_t tgi[kHeavySlots];
+    // CacheMap bookkeeping (free mode: the count pass keeps these owners below capacity): the stamp of each
+    // slot's last access in the chunk (0: none) and whether its key was present when the chunk began
+    __shared__ uint64_t lst[kHeavySlots], tst[kHeavySlots];
+    __shared__ uint8_t lp0[kHeavySlots], tp0[kHeavySlots];
     __shared__ int nocache;                 // a parameter event of the chunk got no slot
     __shared__ uint16_t qslot[kHeavyChunk];
     // parameter-only resources: the rule check of each event is decided by the lane that owns the
@@ -1977,6 +2132,8 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                             if (old == kLEmpty) {
                                 lgi[h] = kGiNone;
                                 tgi[h] = kGiNone;
+                                lst[h] = 0;
+                                tst[h] = 0;
                             }
                             if (old == kLEmpty || old == v) {
                                 sl = (uint16_t)h;
@@ -2115,6 +2272,13 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
             }
             __syncthreads();
             tick(1);
+            if (cache_p)  // presence of the chunk's keys before it (found entries as read, inserted ones absent)
+                for (int k = threadIdx.x; k < kHeavySlots; k += 64)
+                    if (lval[k] != kLEmpty) {
+                        lp0[k] = lent[k].a != kPAbsent ? 1 : 0;
+                        tp0[k] = (pt && tgi[k] < kGiFail && tent[k].a != kPAbsent) ? 1 : 0;
+                    }
+            __syncthreads();
             const bool par_ok = pt && !nocache;
             if (par_ok) {
                 const int lane = threadIdx.x;
@@ -2171,10 +2335,12 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     const Payload q = qpay[k];
                     PEntry &te = tent[qslot[k]];
                     const bool tmap = tmap0;  // ParameterMetric thread counts exist
+                    const uint64_t stamp = lru_stamp(st, q.idx & F_IDX, 0);
                     if (q.idx & F_EXIT) {  // ParameterMetric.decreaseThreadCount (chain_exit)
                         if (tmap) {
                             if (te.a == kPAbsent) te.a = 0;
                             else if (--te.a <= 0) te.a = kPAbsent;
+                            tst[qslot[k]] = stamp;
                         }
                         continue;
                     }
@@ -2182,12 +2348,16 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     // a QPS rule does not read the thread count; the entry is read and written back
                     // through LDS directly (a generic pointer would turn every access into a flat op)
                     PEntry pe = lent[qslot[k]];
-                    const bool pass = param_pass_qps(cl, prule, pe, qpv[k], (int)(q.acq_prio & 0x7FFFFFFFu),
-                                                     ts_base + (int64_t)q.ts_off, &w);
+                    const int aq = (int)(q.acq_prio & 0x7FFFFFFFu);
+                    if (param_map_access(cl, prule, qpv[k], aq)) lst[qslot[k]] = stamp;
+                    const bool pass = param_pass_qps(cl, prule, pe, qpv[k], aq, ts_base + (int64_t)q.ts_off, &w);
                     lent[qslot[k]] = pe;
                     qpre[k] = pass ? 1 : 2;
                     qpw[k] = (int32_t)w;
-                    if (pass && tmap) te.a = (te.a == kPAbsent ? 0 : te.a) + 1;  // ParameterMetric.addThreadCount
+                    if (pass && tmap) {  // ParameterMetric.addThreadCount
+                        te.a = (te.a == kPAbsent ? 0 : te.a) + 1;
+                        tst[qslot[k]] = stamp;
+                    }
                 }
             }
             __syncthreads();
@@ -2440,14 +2610,15 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                     const bool hp = (q.idx & F_PARAM) != 0;
                     if (q.idx & F_EXIT) {
                         chain_exit(cc, res, m, t, qrt[k], (int)(q.acq_prio & 0x7FFFFFFFu), (q.idx & F_ERROR) != 0, hp,
-                                   qpv[k]);
+                                   qpv[k], PArgs{nullptr, 0}, q.idx & F_IDX);
                     } else {
                         int64_t w = 0;
                         cc.pentry = (cache_p && qslot[k] != 0xFFFF) ? &lent[qslot[k]] : nullptr;
+                        cc.pstamp_ref = cc.pentry ? &lst[qslot[k]] : nullptr;
                         cc.pre_param = 0;  // not aggregated: lane 0 decides everything
                         cc.pre_wait = 0;
                         qd[k] = chain_entry(cc, res, m, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
-                                            hp, qpv[k], &w);
+                                            hp, qpv[k], &w, PArgs{nullptr, 0}, q.idx & F_IDX);
                         qw[k] = (int32_t)w;
                     }
                 }
@@ -2455,16 +2626,33 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
             __syncthreads();
             tick(3);
             if (cache_p) {  // write the chunk's entries back, free the slots
+                // (with the keys' stamps and the owners' present counts: free mode, many lanes per owner)
+                int pd = 0, td = 0;
                 for (int k = threadIdx.x; k < kHeavySlots; k += 64) {
                     if (lval[k] != kLEmpty) {
                         if (lgi[k] < kGiFail) {
                             PEntry *e = st.ptab + lgi[k];
                             e->a = lent[k].a;
                             e->b = lent[k].b;
+                            pd += (lent[k].a != kPAbsent ? 1 : 0) - (int)lp0[k];
+                            if (lst[k] && st.pstamp) st.pstamp[lgi[k]] = lst[k];
                         }
-                        if (par_ok && tgi[k] < kGiFail) st.ttab[tgi[k]].a = tent[k].a;
+                        if (par_ok && tgi[k] < kGiFail) {
+                            st.ttab[tgi[k]].a = tent[k].a;
+                            td += (tent[k].a != kPAbsent ? 1 : 0) - (int)tp0[k];
+                            if (tst[k] && st.tstamp) st.tstamp[tgi[k]] = tst[k];
+                        }
                         lval[k] = kLEmpty;
                     }
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    pd += __shfl_xor(pd, o, 64);
+                    td += __shfl_xor(td, o, 64);
+                }
+                if (threadIdx.x == 0) {
+                    if (pd && st.psize) atomicAdd(&st.psize[cache_p->id], (uint32_t)pd);
+                    if (td && lru_on_t(st, res)) atomicAdd(&st.tsize[st.tbase[res]], (uint32_t)td);
                 }
             }
             for (uint32_t k = threadIdx.x; k < cnt; k += 64) {
@@ -2492,6 +2680,248 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
             for (uint32_t k = threadIdx.x; k < R.n_cbs; k += 64) g.cbs[k] = lcbs[k];
         __syncthreads();
     }
+}
+
+// Resources with a CacheMap in LRU mode (k_lflows lists them): one lane each replays the resource's events
+// in arrival order, every map access keeping its owner's recency queue (eviction at capacity).
+__global__ __launch_bounds__(64) void k_llru(FlowState st, int64_t max_rt, FlowScratch sc,
+                                             const Payload *__restrict__ pay, int64_t ts_base,
+                                             const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in,
+                                             int8_t *decision, int32_t *wait_ms) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    const Ctx c{st, max_rt};
+    const uint32_t nl = sc.counters[10], nflows = sc.counters[2], nruns = sc.counters[1];
+    for (uint32_t i = blockIdx.x * 64 + threadIdx.x; i < nl; i += gridDim.x * 64) {
+        const uint32_t fl = sc.lru[i];
+        const uint32_t r0 = sc.flow_first_run[fl];
+        const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        const uint32_t res = sc.run_slot[r0];
+        for (uint32_t j = sc.run_start[r0]; j < sc.run_end[r1 - 1]; ++j) {
+            const Payload q = pay[j];
+            const int64_t t = ts_base + (int64_t)q.ts_off;
+            const uint32_t idx = q.idx & F_IDX;
+            const bool hp = (q.idx & F_PARAM) != 0;
+            const uint64_t pv = hp ? param_in[idx] : 0;
+            if (q.idx & F_EXIT) {
+                chain_exit<true>(c, res, t, rt_in[idx], (int)(q.acq_prio & 0x7FFFFFFFu), (q.idx & F_ERROR) != 0, hp,
+                                 pv, PArgs{nullptr, 0}, idx);
+            } else {
+                int64_t w = 0;
+                decision[idx] = chain_entry<true>(c, res, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
+                                                  hp, pv, &w, PArgs{nullptr, 0}, idx);
+                wait_ms[idx] = (int32_t)w;
+            }
+        }
+        for (uint32_t r = r0; r < r1; ++r) sc.run_mode[r] = RUN_DONE;
+    }
+}
+
+// ---- CacheMap capacity: before each batch (flow.hpp LruRec)
+// 1. count pass: per owner in free mode, the distinct keys absent at the batch start that its events name
+//    (the keys it could insert).  Two launches: the first claims every such key's slot (lanes of one owner
+//    run together here, so two lanes may claim a slot each for the same key: the later one in the probe
+//    sequence is never found again), the second looks each key up -- its first slot in the probe sequence --
+//    and the first event to meet an absent one marks its stamp and counts it.
+template <bool kCount>
+__device__ __forceinline__ void lru_count_key(PEntry *tab, uint64_t *stamp, uint32_t mask, uint32_t owner, uint64_t v,
+                                              uint32_t *ctr, uint64_t mark, uint32_t *overflow) {
+    PEntry *e = ptab_get(tab, mask, owner, v, !kCount, overflow);
+    if (!kCount || !e || e->a != kPAbsent) return;
+    const unsigned long long old = atomicExch((unsigned long long *)&stamp[e - tab], (unsigned long long)mark);
+    if (old != mark) atomicAdd(ctr, 1u);
+}
+
+template <bool kCount>
+__global__ __launch_bounds__(kT) void k_lru_count(FlowState st, const uint8_t *__restrict__ kind,
+                                                  const uint32_t *__restrict__ resource,
+                                                  const uint8_t *__restrict__ flags,
+                                                  const uint64_t *__restrict__ param_in,
+                                                  const uint64_t *__restrict__ pvals, uint32_t n) {
+    const uint64_t mark = kStampMark | st.seq_base;
+    for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
+        const uint32_t r = resource[i];
+        if (r >= st.nres || kind[i] > 1) continue;
+        const ResDev R = st.res[r];
+        if (!R.n_prules) continue;
+        const uint8_t fl = flags ? flags[i] : 0;
+        const bool hp = (fl & SGA_EV_HAS_PARAM) != 0;
+        const uint64_t pv = param_in ? param_in[i] : 0;
+        PArgs pa{nullptr, 0};
+        if ((fl & SGA_EV_ARGS) && pvals) {
+            pa.args = pvals + (pv >> 32);
+            pa.pvals = pvals;
+            pa.nargs = (uint32_t)pv;
+        } else if (hp && (fl & SGA_EV_PARAM_LIST) && pvals) {
+            pa = PArgs{pvals + (pv >> 32), (uint32_t)pv};
+        }
+        const uint32_t nargs = ev_nargs(pa, hp);
+        uint64_t kmask = st.tmapmask ? st.tmapmask[r] : 0ull;  // thread-count maps the event may reach
+        for (uint32_t k = 0; k < R.n_prules; ++k) {
+            const ParamRuleDev &p = st.prules[R.prule_off + k];
+            int32_t idx = p.idx_res;
+            if (idx == kIdxUnresolved) {  // as applyRealParamIdx would resolve it for this event
+                idx = p.param_idx;
+                if (idx < 0) idx = (-idx <= (int32_t)nargs) ? (int32_t)nargs + idx : -idx;
+            }
+            if (idx >= 0 && idx < kMaxParamIdx) kmask |= 1ull << idx;
+            if (kind[i] != 0 || p.grade != 1 || st.pq[p.id] != kNoQueue || (int64_t)nargs <= (int64_t)idx) continue;
+            const uint64_t *vals;
+            uint32_t nv;
+            if (ev_arg(pa, (uint32_t)idx, pv, &vals, &nv) == ARG_NULL) continue;
+            for (uint32_t q = 0; q < nv; ++q)
+                lru_count_key<kCount>(st.ptab, st.pstamp, st.pmask, p.id + 1, vals[q], &st.pnew[p.id], mark,
+                                      st.overflow);
+        }
+        if (st.tbase[r] == kNoTBase) continue;
+        for (uint32_t k = 0; k < nargs && k < (uint32_t)kMaxParamIdx; ++k) {
+            if (!((kmask >> k) & 1ull)) continue;
+            const uint32_t j = st.tbase[r] + k;
+            if (st.tq[j] != kNoQueue) continue;
+            const uint64_t *vals;
+            uint32_t nv;
+            if (ev_arg(pa, k, pv, &vals, &nv) == ARG_NULL) continue;
+            for (uint32_t q = 0; q < nv; ++q)
+                lru_count_key<kCount>(st.ttab, st.tstamp, st.tmask, tmap_owner(r, k), vals[q], &st.tnew[j], mark,
+                                      st.overflow);
+        }
+    }
+}
+
+// 2. owners that could pass their capacity switch to LRU mode: a queue area from the pool, marked
+//    for the collect pass (head = kLruBuilding), their resource replayed in arrival order from now on
+constexpr uint64_t kLruBuilding = ~0ull;
+__global__ __launch_bounds__(kT) void k_lru_decide(FlowState st) {
+    const uint32_t i = blockIdx.x * kT + threadIdx.x;
+    if (i >= st.nprid + st.ntslot) return;
+    const bool th = i >= st.nprid;
+    const uint32_t j = th ? i - st.nprid : i;
+    uint32_t *ctr = th ? &st.tnew[j] : &st.pnew[j];
+    const uint32_t c = *ctr;
+    if (!c) return;
+    *ctr = 0;
+    uint64_t *q = th ? &st.tq[j] : &st.pq[j];
+    const uint32_t cap = th ? kThreadMapCap : st.pcap[j];
+    const uint32_t size = th ? st.tsize[j] : st.psize[j];
+    if (*q != kNoQueue || (uint64_t)size + c <= (uint64_t)cap) return;
+    const uint64_t need = 2ull * cap + 3;  // meta + 2 cap + 2 records
+    const unsigned long long off = atomicAdd(st.lcursor, (unsigned long long)need);
+    if (off + need > st.lpool_cap) {
+        atomicOr(&st.lru_ctl[1], 1u);
+        atomicOr(st.overflow, 1u);
+        return;
+    }
+    st.lpool[off] = LruRec{kLruBuilding, 0};
+    *q = off;
+    st.lru_list[atomicAdd(&st.lru_ctl[0], 1u)] = th ? (kLruThread | j) : j;
+    const uint32_t res = th ? st.tres[j / kMaxParamIdx] : st.pres[j];
+    if (res < st.nres) st.lru_res[res] = 1;
+}
+
+// 3. the switched owners' present keys into their queues (every map slot once)
+__global__ __launch_bounds__(kT) void k_lru_collect(FlowState st) {
+    if (st.lru_ctl[0] == 0) return;
+    const uint32_t np = st.pmask + 1, nt = st.tmask + 1;
+    for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < np + nt; i += gridDim.x * kT) {
+        const bool th = i >= np;
+        const uint32_t s = th ? i - np : i;
+        const PEntry e = th ? st.ttab[s] : st.ptab[s];
+        if (e.owner == 0 || e.a == kPAbsent) continue;
+        uint64_t qo;
+        if (!th) {
+            if (e.owner - 1 >= st.nprid) continue;
+            qo = st.pq[e.owner - 1];
+        } else {
+            const uint32_t r = (e.owner & 0xFFFFFFu) - 1u, k = e.owner >> 24;
+            if (r >= st.nres || st.tbase[r] == kNoTBase) continue;
+            qo = st.tq[st.tbase[r] + k];
+        }
+        if (qo == kNoQueue || st.lpool[qo].value != kLruBuilding) continue;
+        const unsigned long long pos = atomicAdd((unsigned long long *)&st.lpool[qo].stamp, 1ull);
+        st.lpool[qo + 1 + pos] = LruRec{e.value, th ? st.tstamp[s] : st.pstamp[s]};
+    }
+}
+
+// 4. each switched owner's records ordered by stamp (oldest first): one workgroup per owner, bitonic
+//    (in LDS up to kLruLds records, else in the queue area itself, which holds 2 cap + 2 >= the padding)
+constexpr int kLruSortThreads = 256, kLruLds = 4096;
+__global__ __launch_bounds__(kLruSortThreads) void k_lru_sort(FlowState st) {
+    __shared__ uint64_t ks[kLruLds], vs[kLruLds];
+    const uint32_t nsw = st.lru_ctl[0];
+    for (uint32_t w = blockIdx.x; w < nsw; w += gridDim.x) {
+        const uint32_t id = st.lru_list[w];
+        const bool th = (id & kLruThread) != 0;
+        const uint32_t j = id & ~kLruThread;
+        const uint64_t qo = th ? st.tq[j] : st.pq[j];
+        const uint32_t cap = th ? kThreadMapCap : st.pcap[j];
+        const uint32_t size = th ? st.tsize[j] : st.psize[j];
+        LruRec *rec = st.lpool + qo + 1;
+        const uint32_t n = (uint32_t)st.lpool[qo].stamp;
+        uint32_t np2 = 1;
+        while (np2 < n) np2 <<= 1;
+        if (threadIdx.x == 0 && (n != size || n > cap)) {  // the present counts were kept exactly
+            atomicOr(&st.lru_ctl[1], 4u);
+            atomicOr(st.overflow, 1u);
+        }
+        if (np2 <= (uint32_t)kLruLds) {
+            for (uint32_t k = threadIdx.x; k < np2; k += kLruSortThreads) {
+                ks[k] = k < n ? rec[k].stamp : ~0ull;
+                vs[k] = k < n ? rec[k].value : 0ull;
+            }
+            __syncthreads();
+            for (uint32_t kk = 2; kk <= np2; kk <<= 1)
+                for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+                    for (uint32_t a = threadIdx.x; a < np2; a += kLruSortThreads) {
+                        const uint32_t b = a ^ jj;
+                        if (b > a) {
+                            const bool up = (a & kk) == 0;
+                            if ((ks[a] > ks[b]) == up) {
+                                const uint64_t tk = ks[a], tv = vs[a];
+                                ks[a] = ks[b];
+                                vs[a] = vs[b];
+                                ks[b] = tk;
+                                vs[b] = tv;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            for (uint32_t k = threadIdx.x; k < n; k += kLruSortThreads) rec[k] = LruRec{vs[k], ks[k]};
+        } else {
+            for (uint32_t k = n + threadIdx.x; k < np2; k += kLruSortThreads) rec[k] = LruRec{0, ~0ull};
+            __syncthreads();
+            for (uint32_t kk = 2; kk <= np2; kk <<= 1)
+                for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+                    for (uint32_t a = threadIdx.x; a < np2; a += kLruSortThreads) {
+                        const uint32_t b = a ^ jj;
+                        if (b > a) {
+                            const bool up = (a & kk) == 0;
+                            const LruRec x = rec[a], y = rec[b];
+                            if ((x.stamp > y.stamp) == up) {
+                                rec[a] = y;
+                                rec[b] = x;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) st.lpool[qo] = LruRec{0, n};  // head 0, tail n
+        __syncthreads();
+    }
+}
+
+// after a parameter-rule load: a resource keeps arrival-order replay while one of its current owners
+// is in LRU mode
+__global__ __launch_bounds__(kT) void k_lru_res_refresh(FlowState st) {
+    const uint32_t r = blockIdx.x * kT + threadIdx.x;
+    if (r >= st.nres) return;
+    const ResDev R = st.res[r];
+    bool any = false;
+    for (uint32_t k = 0; k < R.n_prules; ++k) any |= st.pq[st.prules[R.prule_off + k].id] != kNoQueue;
+    if (st.tbase[r] != kNoTBase)
+        for (uint32_t k = 0; k < (uint32_t)kMaxParamIdx; ++k) any |= st.tq[st.tbase[r] + k] != kNoQueue;
+    st.lru_res[r] = any ? 1 : 0;
 }
 
 __global__ __launch_bounds__(kT) void k_lresults(FlowScratch sc, const Payload *__restrict__ pay, int8_t *decision,
@@ -2605,35 +3035,52 @@ __global__ void k_clear_ptab(PEntry *t, uint32_t n) {
     if (i < n) t[i] = PEntry{0, 0, 0, kPAbsent, kPAbsent};
 }
 
-// keys held by a map (one atomic per workgroup)
+// slots claimed by a map and keys present in it (one atomic pair per workgroup)
+__device__ __forceinline__ bool pentry_present(const PEntry &e) { return e.a != kPAbsent || e.b != kPAbsent; }
 __global__ void k_count_keys(const PEntry *__restrict__ t, uint32_t n, uint32_t *__restrict__ out) {
-    __shared__ uint32_t ws[kT / 64];
-    uint32_t c = 0;
-    for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) c += t[i].owner != 0 ? 1u : 0u;
+    __shared__ uint32_t ws[2][kT / 64];
+    uint32_t c = 0, p = 0;
+    for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
+        const PEntry e = t[i];
+        c += e.owner != 0 ? 1u : 0u;
+        p += (e.owner != 0 && pentry_present(e)) ? 1u : 0u;
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_down((int)c, o, 64);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    for (int o = 32; o > 0; o >>= 1) {
+        c += (uint32_t)__shfl_down((int)c, o, 64);
+        p += (uint32_t)__shfl_down((int)p, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        ws[0][threadIdx.x >> 6] = c;
+        ws[1][threadIdx.x >> 6] = p;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t t2 = 0;
-        for (int w = 0; w < kT / 64; ++w) t2 += ws[w];
+        uint32_t t2 = 0, p2 = 0;
+        for (int w = 0; w < kT / 64; ++w) {
+            t2 += ws[0][w];
+            p2 += ws[1][w];
+        }
         if (t2) atomicAdd(out, t2);
+        if (p2) atomicAdd(out + 1, p2);
     }
 }
 
-// every key of `old` into the empty table `nt` (same hash as ptab_get; entries keep their counters)
-__global__ void k_rehash(const PEntry *__restrict__ old, uint32_t oldn, PEntry *__restrict__ nt, uint32_t nmask,
-                         uint32_t *overflow) {
+// every present key of `old` (with its stamp) into the empty table `nt` (same hash as ptab_get; entries
+// keep their counters); claimed slots of absent keys are dropped
+__global__ void k_rehash(const PEntry *__restrict__ old, const uint64_t *__restrict__ ostamp, uint32_t oldn,
+                         PEntry *__restrict__ nt, uint64_t *__restrict__ nstamp, uint32_t nmask, uint32_t *overflow) {
     const uint32_t i = blockIdx.x * kT + threadIdx.x;
     if (i >= oldn) return;
     const PEntry e = old[i];
-    if (e.owner == 0) return;
+    if (e.owner == 0 || !pentry_present(e)) return;
     uint32_t h = (uint32_t)splitmix64(e.value ^ ((uint64_t)e.owner << 40) ^ 0xA5A5ULL) & nmask;
     for (uint32_t probe = 0; probe <= nmask; ++probe) {
         if (atomicCAS(&nt[h].owner, 0u, e.owner) == 0u) {
             nt[h].value = e.value;
             nt[h].a = e.a;
             nt[h].b = e.b;
+            if (nstamp) nstamp[h] = ostamp ? ostamp[i] : 0;
             return;
         }
         h = (h + 1) & nmask;
@@ -2664,7 +3111,155 @@ FlowState FlowEngine::state() const {
     s.gate = nullptr;
     s.tmapmask = d_tmapmask.p;
     s.cpst = cparam_st;
+    // CacheMap capacity (null until parameter rules are loaded)
+    const bool lru = d_psize.p != nullptr;
+    s.pstamp = lru ? d_pstamp.p : nullptr;
+    s.tstamp = lru ? d_tstamp.p : nullptr;
+    s.psize = d_psize.p;
+    s.pq = d_pq.p;
+    s.pcap = d_pcap.p;
+    s.pres = d_pres.p;
+    s.tbase = lru ? d_tbase.p : nullptr;
+    s.tres = d_tres.p;
+    s.tsize = d_tsize.p;
+    s.tq = d_tq.p;
+    s.lpool = d_lpool.p;
+    s.lpool_cap = d_lpool.n;
+    s.lcursor = d_lcursor.p;
+    s.pnew = d_pnew.p;
+    s.tnew = d_tnew.p;
+    s.lru_res = lru ? d_lru_res.p : nullptr;
+    s.lru_ctl = d_lru_ctl.p;
+    s.lru_list = d_lru_list.p;
+    s.nprid = lru ? (uint32_t)d_psize.n : 0;
+    s.ntslot = lru ? ntbase * (uint32_t)kMaxParamIdx : 0;
+    s.seq_base = seq;
     return s;
+}
+
+// Per-id and per-slot CacheMap arrays after a parameter-rule load: new rule ids start empty in free mode,
+// resources with rules get thread-map owner slots (kept for good), the queue pool covers every current
+// owner switching once.
+__global__ void k_fill_u32(uint32_t *p, uint32_t v, size_t n) {
+    const size_t i = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+__global__ void k_fill_u64(uint64_t *p, uint64_t v, size_t n) {
+    const size_t i = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+template <class T>
+static void grow_fill(DevBuf<T> &b, size_t n, T v, hipStream_t s) {
+    const size_t old = b.p ? b.n : 0;
+    if (n <= old) return;
+    b.grow(n, s);
+    const size_t m = n - old;
+    if (sizeof(T) == 8)
+        hipLaunchKernelGGL(k_fill_u64, dim3((unsigned)((m + kT - 1) / kT)), dim3(kT), 0, s, (uint64_t *)(b.p + old),
+                           (uint64_t)v, m);
+    else
+        hipLaunchKernelGGL(k_fill_u32, dim3((unsigned)((m + kT - 1) / kT)), dim3(kT), 0, s, (uint32_t *)(b.p + old),
+                           (uint32_t)v, m);
+}
+
+void FlowEngine::lru_sync_rules() {
+    const size_t nid = std::max<size_t>(next_prule_id, 1);
+    grow_fill<uint32_t>(d_psize, nid, 0u, stream);
+    grow_fill<uint32_t>(d_pnew, nid, 0u, stream);
+    grow_fill<uint64_t>(d_pq, nid, kNoQueue, stream);
+    std::vector<uint32_t> pcap(nid, 0), pres(nid, 0xFFFFFFFFu);
+    if (d_pcap.p && d_pcap.n) {  // ids of earlier rules keep their values
+        std::vector<uint32_t> o(d_pcap.n), r(d_pres.n);
+        SGA_HIP_CHECK(hipMemcpyAsync(o.data(), d_pcap.p, o.size() * 4, hipMemcpyDeviceToHost, stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(r.data(), d_pres.p, r.size() * 4, hipMemcpyDeviceToHost, stream));
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+        std::copy(o.begin(), o.end(), pcap.begin());
+        std::copy(r.begin(), r.end(), pres.begin());
+    }
+    uint64_t pool = 0;
+    for (size_t k = 0; k < h_prules.size(); ++k) {
+        const ParamRuleDev &d = h_prules[k];
+        pcap[d.id] = d.cap;
+        pres[d.id] = h_prule_src[k].resource;
+        pool += 2 * (2ull * d.cap + 3);  // its time/token map and one thread-count map
+    }
+    for (uint32_t r = 0; r < nres; ++r)
+        if (h_res[r].n_prules && h_tbase[r] == kNoTBase) h_tbase[r] = (ntbase++) * (uint32_t)kMaxParamIdx;
+    std::vector<uint32_t> tres(std::max<uint32_t>(ntbase, 1), 0xFFFFFFFFu);
+    for (uint32_t r = 0; r < nres; ++r)
+        if (h_tbase[r] != kNoTBase) tres[h_tbase[r] / kMaxParamIdx] = r;
+    d_pcap.alloc(nid);
+    d_pres.alloc(nid);
+    SGA_HIP_CHECK(hipMemcpyAsync(d_pcap.p, pcap.data(), nid * 4, hipMemcpyHostToDevice, stream));
+    SGA_HIP_CHECK(hipMemcpyAsync(d_pres.p, pres.data(), nid * 4, hipMemcpyHostToDevice, stream));
+    const size_t nts = std::max<size_t>((size_t)ntbase * kMaxParamIdx, 1);
+    grow_fill<uint32_t>(d_tsize, nts, 0u, stream);
+    grow_fill<uint32_t>(d_tnew, nts, 0u, stream);
+    grow_fill<uint64_t>(d_tq, nts, kNoQueue, stream);
+    d_tres.alloc(tres.size());
+    SGA_HIP_CHECK(hipMemcpyAsync(d_tres.p, tres.data(), tres.size() * 4, hipMemcpyHostToDevice, stream));
+    if (d_tbase.n < std::max<size_t>(nres, 1)) d_tbase.alloc(std::max<size_t>(nres, 1));
+    SGA_HIP_CHECK(hipMemcpyAsync(d_tbase.p, h_tbase.data(), (size_t)nres * 4, hipMemcpyHostToDevice, stream));
+    if (d_lru_list.n < nid + nts) d_lru_list.alloc(nid + nts);
+    if (!d_lru_ctl.p) {
+        d_lru_ctl.alloc(4);
+        SGA_HIP_CHECK(hipMemsetAsync(d_lru_ctl.p, 0, 16, stream));
+        d_lcursor.alloc(1);
+        SGA_HIP_CHECK(hipMemsetAsync(d_lcursor.p, 0, 8, stream));
+    }
+    if (!d_lru_res.p) {
+        d_lru_res.alloc(std::max<size_t>(nres, 1));
+        SGA_HIP_CHECK(hipMemsetAsync(d_lru_res.p, 0, std::max<size_t>(nres, 1), stream));
+    }
+    if (!d_pstamp.p) {
+        d_pstamp.alloc(d_ptab.n);
+        d_tstamp.alloc(d_ttab.n);
+        SGA_HIP_CHECK(hipMemsetAsync(d_pstamp.p, 0, d_ptab.n * 8, stream));
+        SGA_HIP_CHECK(hipMemsetAsync(d_tstamp.p, 0, d_ttab.n * 8, stream));
+    }
+    // the pool: what is in use plus every current owner switching once (queue areas are not reused)
+    unsigned long long used = 0;
+    SGA_HIP_CHECK(hipMemcpyAsync(&used, d_lcursor.p, 8, hipMemcpyDeviceToHost, stream));
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    if (d_lpool.n < used + pool) d_lpool.grow(used + pool + 1024, stream);
+    upload_res();
+    const FlowState st = state();
+    hipLaunchKernelGGL(k_lru_res_refresh, dim3((nres + kT - 1) / kT), dim3(kT), 0, stream, st);
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+void FlowEngine::lru_prepare(const uint8_t *kind, const uint32_t *resource, const uint8_t *flags, const uint64_t *param,
+                             const uint64_t *pvals, uint32_t n, hipStream_t s) {
+    if (!d_psize.p || h_prules.empty()) return;
+    const FlowState st = state();
+    const uint32_t nb = std::min<uint32_t>((n + kT - 1) / kT, 2048);
+    hipLaunchKernelGGL(k_lru_count<false>, dim3(std::max<uint32_t>(nb, 1)), dim3(kT), 0, s, st, kind, resource, flags,
+                       param, pvals, n);
+    hipLaunchKernelGGL(k_lru_count<true>, dim3(std::max<uint32_t>(nb, 1)), dim3(kT), 0, s, st, kind, resource, flags,
+                       param, pvals, n);
+    const uint32_t no = st.nprid + st.ntslot;
+    hipLaunchKernelGGL(k_lru_decide, dim3((no + kT - 1) / kT), dim3(kT), 0, s, st);
+    hipLaunchKernelGGL(k_lru_collect, dim3(2048), dim3(kT), 0, s, st);
+    hipLaunchKernelGGL(k_lru_sort, dim3(64), dim3(kLruSortThreads), 0, s, st);
+    static const int dbg = getenv("SGA_LRU_DEBUG") ? atoi(getenv("SGA_LRU_DEBUG")) : 0;  // diagnostics only
+    if (dbg) {
+        uint32_t ctl[4];
+        SGA_HIP_CHECK(hipMemcpyAsync(ctl, d_lru_ctl.p, 16, hipMemcpyDeviceToHost, s));
+        SGA_HIP_CHECK(hipStreamSynchronize(s));
+        std::vector<uint32_t> lst(std::min<uint32_t>(ctl[0], 8));
+        if (!lst.empty())
+            SGA_HIP_CHECK(hipMemcpy(lst.data(), d_lru_list.p, lst.size() * 4, hipMemcpyDeviceToHost));
+        fprintf(stderr, "lru_prepare seq=%llu n=%u switched=%u err=%u", (unsigned long long)seq, n, ctl[0], ctl[1]);
+        for (uint32_t x : lst) {
+            const bool th = x & kLruThread;
+            const uint32_t j = x & ~kLruThread;
+            uint32_t sz = 0;
+            SGA_HIP_CHECK(hipMemcpy(&sz, (th ? d_tsize.p : d_psize.p) + j, 4, hipMemcpyDeviceToHost));
+            fprintf(stderr, " %s%u(size %u)", th ? "t" : "p", j, sz);
+        }
+        fprintf(stderr, "\n");
+    }
+    SGA_HIP_CHECK(hipMemsetAsync(d_lru_ctl.p, 0, 4, s));  // switches of this batch done
 }
 
 __global__ void k_set_cslot(FlowRuleDev *rules, const uint32_t *idx, const int32_t *slot, uint32_t n) {
@@ -2720,6 +3315,7 @@ int FlowEngine::set_resources(uint32_t n) {
     hipLaunchKernelGGL(k_init_nodes, dim3((n + 1 + kT - 1) / kT), dim3(kT), 0, stream, d_node.p, n + 1,
                        (int64_t)cfg.statistic_max_rt);
     h_res.assign(n, ResDev{});
+    h_tbase.assign(n, kNoTBase);
     d_overflow.alloc(1);
     SGA_HIP_CHECK(hipMemsetAsync(d_overflow.p, 0, 4, stream));
     // parameter tables: power of two, sized for the batch capacity
@@ -2846,9 +3442,18 @@ static bool prule_valid(const sga_param_rule &r) {
 
 // ParameterMetric.clearForRule / ParameterMetricStorage.clearParamMetricForResource: the thread-count
 // entries of the cleared (resource, index) maps read as absent, and the maps no longer exist
-__global__ void k_tmap_clear(PEntry *ttab, uint32_t n, const uint64_t *clear, uint32_t nres, uint64_t *tmapmask) {
+__global__ void k_tmap_clear(PEntry *ttab, uint32_t n, const uint64_t *clear, uint32_t nres, uint64_t *tmapmask,
+                             const uint32_t *tbase, uint32_t *tsize, uint64_t *tq) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nres) tmapmask[i] &= ~clear[i];
+    if (i < nres) {
+        tmapmask[i] &= ~clear[i];
+        if (tbase && tbase[i] != kNoTBase)  // a new map: empty, free mode
+            for (int k = 0; k < kMaxParamIdx; ++k)
+                if ((clear[i] >> k) & 1ull) {
+                    tsize[tbase[i] + k] = 0;
+                    tq[tbase[i] + k] = kNoQueue;
+                }
+    }
     if (i >= n) return;
     const uint32_t o = ttab[i].owner;
     if (!o) return;
@@ -2917,6 +3522,8 @@ int FlowEngine::load_param_rules(const sga_param_rule *rules, size_t n) {
             d.cluster = r.cluster_mode ? 1 : 0;
             d.cfallback = r.cluster_fallback ? 1 : 0;
             d.cflow = r.cluster_flow_id;
+            // ParameterMetric.initialize: Math.min(BASE_PARAM_MAX_CAPACITY * durationInSec, TOTAL_MAX_CAPACITY)
+            d.cap = (uint32_t)std::min<int64_t>((int64_t)4000 * (int64_t)r.duration_in_sec, 200000);
             for (uint32_t h = 0; h < r.n_hot; ++h) {
                 hv.push_back(r.hot_values[h]);
                 ht.push_back(r.hot_thresholds[h]);
@@ -2974,11 +3581,10 @@ int FlowEngine::load_param_rules(const sga_param_rule *rules, size_t n) {
         const uint32_t tn = (uint32_t)d_ttab.n;
         const uint32_t m = std::max(tn, nres);
         hipLaunchKernelGGL(k_tmap_clear, dim3((m + kT - 1) / kT), dim3(kT), 0, stream, d_ttab.p, tn, dc.p, nres,
-                           d_tmapmask.p);
+                           d_tmapmask.p, d_tbase.p, d_tsize.p, d_tq.p);
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
     }
-    upload_res();
-    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    lru_sync_rules();  // uploads the resources too
     return valid;
 }
 
@@ -3055,27 +3661,32 @@ int FlowEngine::load_degrade_rules(const sga_degrade_rule *rules, size_t n) {
 
 static size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
-void FlowEngine::grow_map(DevBuf<PEntry> &tab, size_t &ub, size_t add) {
+void FlowEngine::grow_map(DevBuf<PEntry> &tab, DevBuf<uint64_t> &stamp, size_t &ub, size_t add) {
     if (ub + add <= tab.n / 4) {
         ub += add;
         return;
     }
-    if (!d_keycount.p) d_keycount.alloc(1);
-    SGA_HIP_CHECK(hipMemsetAsync(d_keycount.p, 0, 4, stream));
+    if (!d_keycount.p || d_keycount.n < 2) d_keycount.alloc(2);
+    SGA_HIP_CHECK(hipMemsetAsync(d_keycount.p, 0, 8, stream));
     hipLaunchKernelGGL(k_count_keys, dim3((unsigned)std::min<size_t>((tab.n + kT - 1) / kT, 2048)), dim3(kT), 0, stream,
                        tab.p, (uint32_t)tab.n, d_keycount.p);
-    uint32_t keys = 0;
-    SGA_HIP_CHECK(hipMemcpyAsync(&keys, d_keycount.p, 4, hipMemcpyDeviceToHost, stream));
+    uint32_t keys[2] = {0, 0};  // claimed slots, present keys
+    SGA_HIP_CHECK(hipMemcpyAsync(keys, d_keycount.p, 8, hipMemcpyDeviceToHost, stream));
     SGA_HIP_CHECK(hipStreamSynchronize(stream));
-    ub = keys;
-    if (ub + add > tab.n / 4) {  // rehash into a table that stays at most a quarter full after this batch
+    ub = keys[0];
+    if (ub + add > tab.n / 4) {
+        // rehash the present keys (claimed slots of absent keys -- evicted or removed ones -- are dropped)
+        // into a table that stays at most a quarter full after this batch
         size_t nn = tab.n;
-        while (ub + add > nn / 4) nn <<= 1;
+        while (keys[1] + add > nn / 4) nn <<= 1;
         DevBuf<PEntry> nt;
         nt.alloc(nn);
+        DevBuf<uint64_t> ns;
+        if (stamp.p) ns.alloc(nn);
         hipLaunchKernelGGL(k_clear_ptab, dim3((unsigned)((nn + kT - 1) / kT)), dim3(kT), 0, stream, nt.p, (uint32_t)nn);
-        hipLaunchKernelGGL(k_rehash, dim3((unsigned)((tab.n + kT - 1) / kT)), dim3(kT), 0, stream, tab.p,
-                           (uint32_t)tab.n, nt.p, (uint32_t)(nn - 1), d_overflow.p);
+        hipLaunchKernelGGL(k_rehash, dim3((unsigned)((tab.n + kT - 1) / kT)), dim3(kT), 0, stream, tab.p, stamp.p,
+                           (uint32_t)tab.n, nt.p, ns.p, (uint32_t)(nn - 1), d_overflow.p);
+        ub = keys[1];
         uint32_t ovf = 0;
         SGA_HIP_CHECK(hipMemcpyAsync(&ovf, d_overflow.p, 4, hipMemcpyDeviceToHost, stream));
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
@@ -3086,21 +3697,25 @@ void FlowEngine::grow_map(DevBuf<PEntry> &tab, size_t &ub, size_t add) {
         }
         std::swap(tab.p, nt.p);
         std::swap(tab.n, nt.n);
+        if (stamp.p) {
+            std::swap(stamp.p, ns.p);
+            std::swap(stamp.n, ns.n);
+        }
     }
     ub += add;
 }
 
-// ParameterMetric maps have no eviction here (parity is unpinned past the reference's
-// CacheMap capacity), so they grow: before a batch of m events the maps get room for every key
-// the batch could add (m per parameter rule of a resource for the rule maps, m for thread counts).
+// Before a batch of m events the maps get room for every key the batch could add (m per parameter rule of
+// a resource for the rule maps, m for thread counts); CacheMap capacity bounds the present keys, and a
+// rehash drops the claimed slots of evicted / removed ones.
 int FlowEngine::ensure_maps(size_t m) {
     uint32_t mpr = 0;
     for (const ResDev &r : h_res) mpr = std::max<uint32_t>(mpr, r.n_prules);
     if (!mpr) return 0;
     const size_t limit = (size_t)1 << 31;  // 32-bit map indices
     if ((pkeys_ub + m * mpr) * 4 > limit || (tkeys_ub + m) * 4 > limit) return SGA_ENOMEM;
-    grow_map(d_ptab, pkeys_ub, m * mpr);
-    grow_map(d_ttab, tkeys_ub, m);
+    grow_map(d_ptab, d_pstamp, pkeys_ub, m * mpr);
+    grow_map(d_ttab, d_tstamp, tkeys_ub, m);
     return 0;
 }
 
@@ -3165,7 +3780,7 @@ int FlowEngine::ensure_scratch() {
         size_t hist = 0;
         for (int b = 1; b <= 32; ++b) hist = std::max(hist, radix_hist_entries(cap, b));
         const size_t ntiles = (cap + kTileElems - 1) / kTileElems + 1;
-        size_t bytes = 2 * al(cap * 4) + 2 * al(cap * sizeof(Payload)) + 2 * al(cap * 4) + 10 * al(cap * 4) +
+        size_t bytes = 2 * al(cap * 4) + 2 * al(cap * sizeof(Payload)) + 2 * al(cap * 4) + 11 * al(cap * 4) +
                        4 * al(cap * 8) + al(cap) + 3 * al(cap * 4) + 2 * al(ntiles * sizeof(LAgg)) + al(ntiles * 4) +
                        al(64) + 2 * al(hist * 4) + al(scan_partials_needed(hist) * 4 + 64);
         d_scratch.alloc(bytes);
@@ -3199,6 +3814,7 @@ int FlowEngine::ensure_scratch() {
         sc.flow_first_run = (uint32_t *)take(cap * 4);
         sc.heavy = (uint32_t *)take(cap * 4);
         sc.pace = (uint32_t *)take(cap * 4);
+        sc.lru = (uint32_t *)take(cap * 4);
         sc.tile_agg = take(ntiles * sizeof(LAgg));
         sc.tile_carry = take(ntiles * sizeof(LAgg));
         sc.tile_valid = (uint32_t *)take(ntiles * 4);
@@ -3291,6 +3907,9 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         // every later one.  A failed batch has been partly applied (its node and breaker updates
         // stay); the call reports -ENOMEM.
         SGA_HIP_CHECK(hipMemsetAsync(d_overflow.p, 0, 4, stream));
+        // CacheMap capacity: owners that could pass theirs switch to LRU mode (both paths below)
+        lru_prepare(d_kind.p, d_resid.p, flags ? d_flags.p : nullptr, param ? d_param.p : nullptr,
+                    any_list ? d_pvals.p : nullptr, (uint32_t)m, stream);
         const FlowState st = state();
         const uint32_t nb = (uint32_t)((m + kT - 1) / kT);
         bool has_in = false, has_list = false;
@@ -3312,6 +3931,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
             SGA_HIP_CHECK(hipStreamSynchronize(stream));
             if (ovf) return SGA_ENOMEM;
             b += m;
+            seq += m;
             continue;
         }
         hipLaunchKernelGGL(k_lclassify, dim3(nb), dim3(kT), 0, stream, st, d_kind.p, d_resid.p, d_ts.p, lo, d_acq.p,
@@ -3330,6 +3950,9 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         const uint32_t fthreads = (uint32_t)std::min<size_t>(m, nres);
         hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, stream, st,
                            (int64_t)cfg.statistic_max_rt, sc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p);
+        if (st.lru_res)
+            hipLaunchKernelGGL(k_llru, dim3(64), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo,
+                               d_rt.p, d_param.p, d_dec.p, d_wait.p);
         hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
                            d_dec.p, d_wait.p, lwave_prof());
@@ -3350,6 +3973,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
         if (ovf) return SGA_ENOMEM;  // parameter maps full
         b += m;
+        seq += m;
     }
     return 0;
 }
@@ -3390,6 +4014,7 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
     const uint32_t gb = std::min<uint32_t>(nb, 1024);
     hipLaunchKernelGGL(k_lgate, dim3(gb), dim3(kT), 0, s, d_kind_in, d_resource, d_acquire, flags_p, param_p, m, nres,
                        (int)sys.check, (uint64_t)(d_param_values ? n_values : 0), d_gate.p, d_param_values);
+    lru_prepare(d_kind_in, d_resource, flags_p, param_p, d_param_values, m, s);  // CacheMap capacity
     FlowState st = state();
     st.gate = d_gate.p;
     FlowScratch gsc = sc;
@@ -3410,6 +4035,9 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
     const uint32_t fthreads = std::min<uint32_t>(m, nres);
     hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc,
                        pay, keys, ts_base, rt_p, param_p, d_decision, wait_p);
+    if (st.lru_res)
+        hipLaunchKernelGGL(k_llru, dim3(64), dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p,
+                           param_p, d_decision, wait_p);
     hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
                        st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
                        lwave_prof());
@@ -3428,6 +4056,7 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
                        d_param_values);
     hipLaunchKernelGGL(k_lfail, dim3(gb), dim3(kT), 0, s, d_gate.p, d_overflow.p, d_gate.p + 1, m, d_decision, wait_p);
     SGA_HIP_CHECK(hipGetLastError());
+    seq += n;
     return 0;
 }
 

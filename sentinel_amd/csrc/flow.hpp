@@ -55,6 +55,8 @@ struct ParamRuleDev {
     int32_t cluster, cfallback;
     int32_t cpad;
     int64_t cflow;
+    uint32_t cap;   // ParameterMetric: the rule's time / token CacheMap capacity, min(4000 * durationInSec, 200000)
+    uint32_t pad2;
 };
 constexpr int32_t kIdxUnresolved = INT32_MIN;
 constexpr int kMaxParamIdx = 64;  // thread-count maps exist for argument indices 0..63
@@ -85,6 +87,23 @@ struct alignas(32) PEntry {
     int64_t b;        // token counter
 };
 constexpr int64_t kPAbsent = INT64_MIN;
+
+// ParameterMetric's CacheMaps (ConcurrentLinkedHashMapWrapper, strict LRU; ParameterMetric.java:37-39,95-121).
+// Every key access stamps the key's map slot with ((event sequence) << 16 | element index): within an
+// owner (a rule's time/token map, or a resource's thread-count map of one argument index) stamps grow
+// with the access order.  An owner whose keys cannot exceed its capacity in a batch (count pass) stays in
+// free mode (any kernel, sizes kept exactly); one that could is switched to LRU mode for good: its
+// present keys go into a recency queue (records {value, stamp}, oldest first), its resource is decided
+// in arrival order by one lane, every access appends a record, and an insert into a full map evicts the
+// oldest record whose stamp still matches its key.
+struct LruRec {
+    uint64_t value;
+    uint64_t stamp;  // the queue area's first record holds {head, tail}
+};
+constexpr uint64_t kNoQueue = ~0ull;        // free mode
+constexpr uint32_t kNoTBase = 0xFFFFFFFFu;  // a resource without thread-count map owner slots
+constexpr uint32_t kThreadMapCap = 4000;    // ParameterMetric.THREAD_COUNT_MAX_CAPACITY
+constexpr uint64_t kStampMark = 1ull << 63;  // count pass: an absent key first met in this batch
 
 // SystemRuleManager thresholds (SystemRuleManager.java:62-74) + SystemStatusListener readings
 struct SysDev {
@@ -118,7 +137,26 @@ struct FlowState {
     uint64_t *tmapmask;
     // embedded cluster server's parameter path for cluster-mode parameter rules (ctl null: no rules)
     CParamState cpst;
+    // CacheMap capacity (LruRec above)
+    uint64_t *pstamp, *tstamp;   // per map slot: stamp of the key's last access
+    uint32_t *psize;             // per parameter-rule id: keys present in its time/token map
+    uint64_t *pq;                // per parameter-rule id: LRU queue area in lpool (kNoQueue: free mode)
+    const uint32_t *pcap, *pres; // per parameter-rule id: capacity, resource
+    const uint32_t *tbase;       // per resource: first of its kMaxParamIdx thread-map owner slots
+    const uint32_t *tres;        // per thread-slot base (tbase / kMaxParamIdx): its resource
+    uint32_t *tsize;             // per thread-map owner slot: keys present
+    uint64_t *tq;                // per thread-map owner slot: LRU queue area (kNoQueue: free mode)
+    LruRec *lpool;
+    uint64_t lpool_cap;
+    unsigned long long *lcursor; // next free record of lpool
+    uint32_t *pnew, *tnew;       // count pass: distinct absent keys the batch may insert, per owner
+    uint8_t *lru_res;            // per resource: an owner in LRU mode (its events replay in arrival order)
+    uint32_t *lru_ctl;           // [0] owners switched this batch [1] error bits (1 queue pool full, 2 queue check)
+    uint32_t *lru_list;          // owners switched this batch: param id, or kLruThread | thread slot
+    uint32_t nprid, ntslot;      // parameter-rule ids, thread-map owner slots
+    uint64_t seq_base;           // event sequence of the batch's first event
 };
+constexpr uint32_t kLruThread = 1u << 31;
 
 struct FlowScratch {
     uint32_t *keys[2];
@@ -134,6 +172,7 @@ struct FlowScratch {
     uint32_t *flow_first_run;
     uint32_t *heavy;  // flows replayed by k_lheavy (count in counters[8])
     uint32_t *pace;   // long single-rule fast-path flows decided by k_lwave (count in counters[9])
+    uint32_t *lru;    // flows of resources with a map in LRU mode, replayed by k_llru (count in counters[10])
     void *tile_agg, *tile_carry;
     uint32_t *tile_valid;
     uint32_t *counters;
@@ -159,13 +198,26 @@ struct FlowEngine {
     DevBuf<uint32_t> d_overflow;
     DevBuf<uint32_t> d_keycount;
     DevBuf<uint64_t> d_tmapmask;  // FlowState::tmapmask
+    // CacheMap capacity (FlowState: pstamp .. seq_base)
+    DevBuf<uint64_t> d_pstamp, d_tstamp, d_pq, d_tq;
+    DevBuf<uint32_t> d_psize, d_pcap, d_pres, d_pnew, d_tbase, d_tres, d_tsize, d_tnew, d_lru_ctl, d_lru_list;
+    DevBuf<uint8_t> d_lru_res;
+    DevBuf<LruRec> d_lpool;
+    DevBuf<unsigned long long> d_lcursor;
+    std::vector<uint32_t> h_tbase;  // per resource (kNoTBase until it gets parameter rules)
+    uint32_t ntbase = 0;            // resources given thread-map owner slots
+    uint64_t seq = 0;               // events submitted so far (stamps)
+    void lru_sync_rules();          // per-id / per-slot arrays after a parameter-rule load
+    void lru_prepare(const uint8_t *kind, const uint32_t *resource, const uint8_t *flags, const uint64_t *param,
+                     const uint64_t *pvals, uint32_t n, hipStream_t s);  // count pass + switches, before a batch
+    int lru_error(hipStream_t s);   // sticky queue errors (host wait)
     CParamState cparam_st{};      // set before each batch (the engine's cluster parameter state)
     bool has_cluster_prules = false;
     // upper bounds of the keys held by the parameter / thread-count maps (exact after a count);
     // the maps are rehashed into more room before a batch could fill them past a quarter
     size_t pkeys_ub = 0, tkeys_ub = 0;
     int ensure_maps(size_t m);
-    void grow_map(DevBuf<PEntry> &tab, size_t &ub, size_t add);
+    void grow_map(DevBuf<PEntry> &tab, DevBuf<uint64_t> &stamp, size_t &ub, size_t add);
     DevBuf<uint8_t> d_scratch;
     FlowScratch sc;
     size_t scratch_cap = 0;

@@ -12,4 +12,4 @@ if [ -n "$files" ]; then
   tail -3 gpurun_out/$tag/pytest.log
   [ $rc = 0 ] || { grep -E "Error|assert|FAIL" gpurun_out/$tag/pytest.log | head -30; exit 1; }
 fi
-[ $# -gt 0 ] && bash tools/r03_ab.sh ${tag}_ab "$@"
+if [ $# -gt 0 ]; then bash tools/r03_ab.sh ${tag}_ab "$@"; fi
