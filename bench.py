@@ -244,13 +244,21 @@ def main():
         hip.hipEventRecord(e1, C.c_void_p(side.cuda_stream))
         mev.append((e0, e1))
 
+    # one sga_request_tokens_device per batch; SGA_BENCH_PIPE=1 uses the pipelined device entry instead (a batch's
+    # key pass and sorts beside the previous batch's decisions: measured slower on MI355X, the two stages compete
+    # for the same CUs -- DESIGN.md 3); the timed region ends after sga_stream_wait + a device synchronize
+    pipe = os.environ.get("SGA_BENCH_PIPE", "0") == "1"
+    in_torch = torch.cuda.Stream(dev)  # the inputs are complete (made before the loop); a stream of their own
+    in_stream = C.c_void_p(in_torch.cuda_stream)
+    entry = L.sga_request_tokens_device_pipelined if pipe else L.sga_request_tokens_device
+
     def step(b, k=None):
         f, a, p, t, ts_base, n = batches[b]
         o = outs[b & 1]
         if k is not None:
             hip.hipEventRecord(bev[k][0], estream)
-        rc = L.sga_request_tokens_device(eng.handle, f.data_ptr(), a.data_ptr(), p.data_ptr(), ts_base, t.data_ptr(),
-                                         n, o.data_ptr(), None)
+        rc = entry(eng.handle, f.data_ptr(), a.data_ptr(), p.data_ptr(), ts_base, t.data_ptr(), n, o.data_ptr(),
+                   in_stream if pipe else None)
         if rc != 0:
             raise RuntimeError(f"sga_request_tokens_device rc={rc}: {L.sga_last_error(eng.handle)}")
         if k is not None:
@@ -260,6 +268,7 @@ def main():
 
     for b in range(args.warmup):
         step(b)
+    _lib.check(L.sga_stream_wait(eng.handle, in_stream), eng.handle, "stream_wait")
     if args.warmup > 0:
         # the snapshot path is warmed up like the batches (its first call pays one-time setup:
         # events, the kernel's first launch); the timed loop still runs it every metric_every steps
@@ -272,9 +281,15 @@ def main():
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     hip.hipEventRecord(ev0, estream)
+    tq = []
     for k, b in enumerate(range(args.warmup, nb)):
+        tq.append(time.perf_counter())
         step(b, k)
+    tq.append(time.perf_counter())
+    _lib.check(L.sga_stream_wait(eng.handle, in_stream), eng.handle, "stream_wait")
     hip.hipEventRecord(ev1, estream)
+    if os.environ.get("SGA_BENCH_DEBUG"):  # diagnostics: host time to queue each step (ms)
+        print("queue ms per step:", [round((tq[i + 1] - tq[i]) * 1e3, 3) for i in range(len(tq) - 1)], file=sys.stderr)
     torch.cuda.synchronize(dev)
     t_end = time.perf_counter()
     if world > 1:

@@ -184,6 +184,15 @@ int sga_request_tokens_device(sga_engine *e, const int64_t *d_flow_id, const int
 int sga_request_tokens_device_async(sga_engine *e, const int64_t *d_flow_id, const int32_t *d_acquire,
                                     const uint8_t *d_prio, int64_t ts_base, const uint32_t *d_ts_off, size_t n,
                                     sga_token_result *d_out, void *hip_stream);
+/* Pipelined form of sga_request_tokens_device for a stream of hot-path batches: the batch's classification
+ * (key pass, count scans, sorts) starts once the inputs are ready on hip_stream, beside the previous batch's
+ * decisions; decisions still run in submission order after every earlier engine call.  The outputs are
+ * ready on hip_stream only after sga_stream_wait(e, hip_stream) (or sga_sync).  A batch the hot path does
+ * not take runs as sga_request_tokens_device.  Same decisions as one sga_request_tokens_device per batch
+ * (DefaultTokenService.requestToken in arrival order, CS/flow/DefaultTokenService.java:39-50). */
+int sga_request_tokens_device_pipelined(sga_engine *e, const int64_t *d_flow_id, const int32_t *d_acquire,
+                                        const uint8_t *d_prioritized, int64_t ts_base, const uint32_t *d_ts_off,
+                                        size_t n, sga_token_result *d_out, void *hip_stream);
 /* Make `hip_stream` wait for every queued engine batch (no host wait). */
 int sga_stream_wait(sga_engine *e, void *hip_stream);
 /* Host wait for every queued batch. */

@@ -126,6 +126,8 @@ SIGNATURES = {
                                             C.c_size_t, C.c_void_p, C.c_void_p]),
     "sga_request_tokens_device_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
                                             C.c_size_t, C.c_void_p, C.c_void_p]),
+    "sga_request_tokens_device_pipelined": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                                                      C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
     "sga_stream_wait": (C.c_int, [C.c_void_p, C.c_void_p]),
     "sga_sync": (C.c_int, [C.c_void_p]),
     "sga_cluster_metric_sums": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.POINTER(C.c_int64)]),

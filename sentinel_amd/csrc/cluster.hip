@@ -1425,7 +1425,7 @@ __device__ __forceinline__ uint32_t bucket_delta(uint32_t t, uint32_t W, uint32_
 // submitted out of time order), as the closed form needs each run's bucket to be the newest.
 __global__ __launch_bounds__(kThreads) void k_hot_precheck(ClusterState st, BatchScratch sc,
                                                            const uint32_t *__restrict__ ts_off, int64_t ts_base,
-                                                           uint32_t n) {
+                                                           uint32_t n, int pipelined) {
     if (blockIdx.x == 0 && st.dense_n) {
         const uint32_t W = st.wtab[threadIdx.x];
         WConst wc;
@@ -1442,6 +1442,10 @@ __global__ __launch_bounds__(kThreads) void k_hot_precheck(ClusterState st, Batc
     if (h >= hot_count(sc) || n == 0) return;
     const int64_t W = (int64_t)sc.hot_ctl[2];
     const int64_t t0 = ts_base + (int64_t)ts_off[0];
+    // Pipelined batches: the window starts read here may still be written by the earlier batch being
+    // decided.  That batch writes buckets at its own times only, so the answer is the same either way
+    // when this batch starts no earlier than every earlier batch's latest time; otherwise no hot path.
+    if (pipelined && h == 0 && t0 < (int64_t)*sc.tmax_all) atomicOr(&sc.counters[CTL_FLAGS], kFlagState);
     const int64_t ws0 = t0 - t0 % W;
     const uint32_t s = sc.hot_slot[h];
     const SlotParam P = st.param[s];
@@ -1480,7 +1484,7 @@ static_assert(kKeyWaves == kSubPerSeg, "one wave per compaction segment");
 struct KeyShared {
     WConst wcs[256];
     uint16_t cnt[kKeyWaves][kHot];  // per wave: hot requests so far per hot id
-    uint32_t s_np[kKeyWaves], s_bd[kKeyWaves];
+    uint32_t s_np[kKeyWaves], s_bd[kKeyWaves], s_tm[kKeyWaves];
     uint32_t hist0[2][256];         // per sort tile of the segment: the first radix digit's counts
 };
 template <int kPass, bool kDense>
@@ -1514,7 +1518,7 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
     const uint32_t Wh = nhot ? sc.hot_ctl[2] : 1u;
     const uint32_t r0h = (uint32_t)(ts_base % (int64_t)Wh);
     const double invh = 1.0 / (double)Wh;
-    uint32_t wflags = 0, nc = 0, np = 0, bdmax = 0;
+    uint32_t wflags = 0, nc = 0, np = 0, bdmax = 0, tmax_l = 0;
     const uint32_t send = min(n, ubase + (uint32_t)kSubSeg);
     // the sub's request codes stay in registers through the rank and fix-up passes (written once)
     uint32_t hc[kSubRounds];
@@ -1574,6 +1578,7 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                 const uint32_t rbase = ubase + (uint32_t)(ch * kH1Chunk + u) * 64;
                 const uint32_t i = rbase + lane;
                 const bool valid = i < send;
+                if (valid) tmax_l = max(tmax_l, B.t[u]);
                 uint32_t d = B.d[u], hfv = B.hf[u];
                 const uint32_t m = B.m[u];
                 if (kDense) {
@@ -1731,8 +1736,8 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                 a += s_np[w];
                 m = max(m, s_bd[w]);
             }
-            sc.seg_stat[2 * seg] = a;
-            sc.seg_stat[2 * seg + 1] = m;
+            sc.seg_stat[kSegStat * seg] = a;
+            sc.seg_stat[kSegStat * seg + 1] = m;
         }
         __syncthreads();
         if (active) {
@@ -1758,6 +1763,17 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
         }
     } else if (lane == 0) {
         sc.ptile_np[sub] = 0u;  // no hot set (or the re-classifying pass): nothing prioritized to sort
+    }
+    {  // the segment's latest request time (offset from ts_base): k_hot_mode keeps the maximum over batches
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tmax_l = max(tmax_l, (uint32_t)__shfl_xor((int)tmax_l, o, 64));
+        if (lane == 0) sh.s_tm[wave] = tmax_l;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t m = 0;
+            for (int w = 0; w < kKeyWaves; ++w) m = max(m, sh.s_tm[w]);
+            sc.seg_stat[kSegStat * seg + 2] = m;
+        }
     }
     if (lane == 0) sc.tile_nc[sub] = active ? nc : 0u;  // totals: k_hot_mode
     if (d0) {  // the sort's first-pass histogram rows of this segment's two tiles
@@ -1790,36 +1806,43 @@ __global__ __launch_bounds__(kKeyThreads) void k_hot_key_hash(
 
 // The batch's path and element counts: sums over the compaction segments and the rank segments
 // (one workgroup).
-__global__ __launch_bounds__(1024) void k_hot_mode(BatchScratch sc, uint32_t nsub, uint32_t nseg) {
-    __shared__ uint32_t red[3][16];
+__global__ __launch_bounds__(1024) void k_hot_mode(BatchScratch sc, uint32_t nsub, uint32_t nseg, int64_t ts_base) {
+    __shared__ uint32_t red[4][16];
     const uint32_t f = sc.counters[CTL_FLAGS];
     const uint32_t nhot = (f & (kFlagRerun | kFlagState)) ? 0u : hot_count(sc);
-    uint32_t ns = 0, np = 0, bd = 0;
+    uint32_t ns = 0, np = 0, bd = 0, tm = 0;
     for (uint32_t k = threadIdx.x; k < nsub; k += 1024) ns += sc.tile_nc[k];
-    if (nhot)
-        for (uint32_t k = threadIdx.x; k < nseg; k += 1024) {
-            np += sc.seg_stat[2 * k];
-            bd = max(bd, sc.seg_stat[2 * k + 1]);
+    for (uint32_t k = threadIdx.x; k < nseg; k += 1024) {
+        if (nhot) {
+            np += sc.seg_stat[kSegStat * k];
+            bd = max(bd, sc.seg_stat[kSegStat * k + 1]);
         }
+        tm = max(tm, sc.seg_stat[kSegStat * k + 2]);
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         ns += (uint32_t)__shfl_xor((int)ns, o, 64);
         np += (uint32_t)__shfl_xor((int)np, o, 64);
         bd = max(bd, (uint32_t)__shfl_xor((int)bd, o, 64));
+        tm = max(tm, (uint32_t)__shfl_xor((int)tm, o, 64));
     }
     if ((threadIdx.x & 63) == 0) {
         red[0][threadIdx.x >> 6] = ns;
         red[1][threadIdx.x >> 6] = np;
         red[2][threadIdx.x >> 6] = bd;
+        red[3][threadIdx.x >> 6] = tm;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t a = 0, b = 0, m = 0;
+        uint32_t a = 0, b = 0, m = 0, t = 0;
         for (int w = 0; w < 16; ++w) {
             a += red[0][w];
             b += red[1][w];
             m = max(m, red[2][w]);
+            t = max(t, red[3][w]);
         }
+        // the latest request time of every batch classified so far (pipelined prechecks)
+        atomicMax(sc.tmax_all, (unsigned long long)(ts_base + (int64_t)t));
         sc.counters[CTL_NSORT] = a;  // the compaction segments hold the cold elements only
         sc.counters[CTL_NPRIO] = b;
         sc.counters[CTL_NCOLD] = a;
@@ -2422,6 +2445,7 @@ __global__ void k_hot_reset(ClusterState st, BatchScratch sc, uint32_t nslots_ca
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)kHot; i += gridDim.x * blockDim.x)
         sc.hot_next[i] = kNoSlot;
     if (blockIdx.x == 0 && threadIdx.x < kHotCtlWords) sc.hot_ctl[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.tmax_all = 0;  // no batch in flight (callers have joined)
 }
 
 __global__ void k_metric_sums(ClusterState st, uint32_t s, int64_t now, int64_t *out7) {
@@ -3068,7 +3092,8 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up(cap * 4);                                                        // prank
     b += 3 * align_up(kHot * 4);                                                   // plo, phi, hot_tot
     b += align_up(256 * sizeof(WConst));
-    b += align_up(segs_alloc * 2 * 4);                                             // seg_stat
+    b += align_up(segs_alloc * kSegStat * 4);                                      // seg_stat
+    b += align_up(64);                                                             // tmax_all
     b += align_up((size_t)kHotCand * 2 * 4);                                       // hot_cand
     return b;
 }
@@ -3139,7 +3164,8 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.phi = (uint32_t *)take(kHot * 4);
     sc.hot_tot = (uint32_t *)take(kHot * 4);
     sc.wconst = (WConst *)take(256 * sizeof(WConst));
-    sc.seg_stat = (uint32_t *)take(segs_alloc * 2 * 4);
+    sc.seg_stat = (uint32_t *)take(segs_alloc * kSegStat * 4);
+    sc.tmax_all = (unsigned long long *)take(64);
     sc.hot_cand = (uint32_t *)take((size_t)kHotCand * 2 * 4);
     sc.cap = cap;
 }
@@ -3211,16 +3237,42 @@ void hot_reset(const ClusterState &st, BatchScratch &sc, uint32_t nslots_cap, hi
 // scan -> sort of the cold (and prioritized hot) elements -> cold runs / flows / results -> hot
 // runs (k_hot_flows) -> hot results in input order -> prioritized hot results -> next hot set.
 // Every kernel reads the batch's path from the control words, so no host synchronisation.
-static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id,
-                             const int32_t *acquire, const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off,
-                             uint32_t n, uint64_t *out, hipStream_t s, bool clean) {
-    const uint32_t invalid_key = st.nslots;
+static void side_stream_init(BatchScratch &sc) {
+    if (sc.side) return;
+    static const int side_prio = getenv("SGA_SIDE_PRIO") ? atoi(getenv("SGA_SIDE_PRIO")) : 0;  // A/B knob
+    if (side_prio) {
+        int lo = 0, hi = 0;  // hi: the greatest priority (numerically lowest)
+        SGA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        SGA_HIP_CHECK(hipStreamCreateWithPriority(&sc.side, hipStreamNonBlocking, side_prio > 0 ? hi : lo));
+    } else {
+        SGA_HIP_CHECK(hipStreamCreateWithFlags(&sc.side, hipStreamNonBlocking));
+    }
+    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork0, hipEventDisableTiming));
+    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork, hipEventDisableTiming));
+    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_join, hipEventDisableTiming));
+    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_mid, hipEventDisableTiming));
+}
+
+static int hot_key_bits(const ClusterState &st) {
     int bits = 1;
-    while (((uint64_t)1 << bits) < (uint64_t)st.nslots + kHot + 2) ++bits;  // hot keys nslots + 1 + id
+    while (((uint64_t)1 << bits) < (uint64_t)st.nslots + kHot + 2) ++bits;
+    return bits;
+}
+
+// Stage 1 of a hot-path batch (reads only its inputs, the dense table and -- the precheck -- the hot
+// rules' window starts): the precheck, the key pass (in-segment ranks, cold elements), the count scans,
+// the prioritized sort and the cold sort.  The result is in sc (CTL words, el[], pel[], hcode, hbase).
+// pipelined: an earlier batch may still be deciding (sga_request_tokens_device_pipelined); the precheck
+// then also refuses the hot path to a batch that starts before the latest time of any earlier batch.
+static void classify_hot(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
+                         const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, uint64_t *out,
+                         hipStream_t s, bool clean, bool pipelined) {
+    const int bits = hot_key_bits(st);
     const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
     const uint32_t ngroups = (nseg + kHotGroupRows - 1) / kHotGroupRows;
     if (!clean) SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, CTL_WORDS * 4, s));
-    hipLaunchKernelGGL(k_hot_precheck, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc, ts_off, ts_base, n);
+    hipLaunchKernelGGL(k_hot_precheck, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc, ts_off, ts_base, n,
+                       pipelined ? 1 : 0);
     auto hka = st.dense_n ? k_hot_key_dense<0> : k_hot_key_hash<0>;
     auto hkb = st.dense_n ? k_hot_key_dense<1> : k_hot_key_hash<1>;
     // the key kernels count the sort's first digit per tile as they write the elements
@@ -3232,27 +3284,12 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
                        fz_debug(), d0, sc.radix.hist, ntiles_sort);
     hipLaunchKernelGGL(hkb, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out,
                        fz_debug(), d0, sc.radix.hist, ntiles_sort);
-    hipLaunchKernelGGL(k_hot_mode, dim3(1), dim3(1024), 0, s, sc, nseg * kKeyWaves, nseg);
-    // the hot side (disjoint rules, disjoint results) runs on a side stream: its count scans beside
-    // the sort, its runs and results beside the cold stage (the cold flows are bound by record-load
-    // latency at low occupancy, the hot results stream)
+    hipLaunchKernelGGL(k_hot_mode, dim3(1), dim3(1024), 0, s, sc, nseg * kKeyWaves, nseg, ts_base);
+    // the hot side's count scans and prioritized sort on the side stream, beside the cold sort
     const bool ovl = hot_overlap() && !(fz_debug() & 16);
     hipStream_t hs = s;
     if (ovl) {
-        if (!sc.side) {
-            static const int side_prio = getenv("SGA_SIDE_PRIO") ? atoi(getenv("SGA_SIDE_PRIO")) : 0;  // A/B knob
-            if (side_prio) {
-                int lo = 0, hi = 0;  // hi: the greatest priority (numerically lowest)
-                SGA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-                SGA_HIP_CHECK(hipStreamCreateWithPriority(&sc.side, hipStreamNonBlocking, side_prio > 0 ? hi : lo));
-            } else {
-                SGA_HIP_CHECK(hipStreamCreateWithFlags(&sc.side, hipStreamNonBlocking));
-            }
-            SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork0, hipEventDisableTiming));
-            SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork, hipEventDisableTiming));
-            SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_join, hipEventDisableTiming));
-            SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_mid, hipEventDisableTiming));
-        }
+        side_stream_init(sc);
         SGA_HIP_CHECK(hipEventRecord(sc.ev_fork0, s));
         SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork0, 0));
         hs = sc.side;
@@ -3261,11 +3298,34 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, hs, sc, ngroups);
     hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
     hipLaunchKernelGGL(k_hot_pre, dim3(kHotBuckets), dim3(kThreads), 0, hs, sc);
-    // the prioritized hot requests, sorted by hot id on their own (12-bit key), then the hot runs and
-    // results: the whole hot side runs beside the cold sort and the cold stage
+    // the prioritized hot requests, sorted by hot id on their own (12-bit key)
     const int npp = radix_sort_u64_tiled(sc.pel_tile, sc.ptile_np, sc.counters + CTL_NPRIO, sc.pel[0], sc.pel[1], n,
                                          kSlotShift, 12, sc.radix_p, hs, false);
-    const uint64_t *pel = (npp & 1) ? sc.pel[0] : sc.pel[1];
+    sc.pel_sorted = (npp & 1) ? sc.pel[0] : sc.pel[1];
+    const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
+                                        kSlotShift, bits, sc.radix, s, d0 > 0);
+    sc.el_sorted = (np & 1) ? sc.el[0] : sc.el[1];
+    if (ovl) {  // stage 1 ends on s
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_fork, hs));
+        SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_fork, 0));
+    }
+}
+
+// Stage 2 (the batch's decisions; batches' stage 2 run in order): the hot runs and results on the side
+// stream beside the cold stage, then the next hot set.
+static void decide_hot(const ClusterState &st, BatchScratch &sc, const int32_t *acquire, const uint8_t *prio,
+                       int64_t ts_base, const uint32_t *ts_off, uint32_t n, uint64_t *out, hipStream_t s) {
+    const uint32_t invalid_key = st.nslots;
+    const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
+    const uint64_t *el = sc.el_sorted, *pel = sc.pel_sorted;
+    const bool ovl = hot_overlap() && !(fz_debug() & 16);
+    hipStream_t hs = s;
+    if (ovl) {
+        side_stream_init(sc);
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_fork0, s));
+        SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork0, 0));
+        hs = sc.side;
+    }
     const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
     hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, pel);
     hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, hs, st, sc, ts_base);
@@ -3275,9 +3335,6 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
                            fin_cache());
         SGA_HIP_CHECK(hipEventRecord(sc.ev_join, hs));
     }
-    const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
-                                        kSlotShift, bits, sc.radix, s, d0 > 0);
-    const uint64_t *el = (np & 1) ? sc.el[0] : sc.el[1];
     cold_stage(st, sc, el, n, sc.counters + CTL_NCOLD, invalid_key, acquire, prio, ts_off, ts_base, 0,
                std::max<uint32_t>(sc.hot_min, 1), out, s);
     if (fz_debug() & 16) {  // profiling only: k_cold_fused phase cycles per workgroup
@@ -3308,6 +3365,26 @@ static void decide_batch_hot(const ClusterState &st, BatchScratch &sc, const int
     if (ovl && tail_early()) SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_join, 0));
     hipLaunchKernelGGL(k_hot_fin, dim3(1), dim3(kFinThreads), 0, s, st, sc);
     sc.counters_clean = 1;
+}
+
+bool cluster_hot_eligible(const ClusterState &st, const BatchScratch &sc, uint32_t n, int simple, int nlims) {
+    const bool limited = nlims > 0 && !simple;
+    if (n == 0 || (n <= std::min<uint32_t>(sc.small_max, kSmall) && !limited && !radix64_lookback())) return false;
+    return sc.hot_enabled && sc.hot_lane_order && !simple && !limited && !radix64_lookback() &&
+           st.nslots + (uint64_t)kHot + 2 < kMaxSlots;
+}
+
+void cluster_classify_hot(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
+                          const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, void *out,
+                          hipStream_t s) {
+    const bool clean = sc.counters_clean != 0;
+    sc.counters_clean = 0;
+    classify_hot(st, sc, flow_id, acquire, prio, ts_base, ts_off, n, (uint64_t *)out, s, clean, true);
+}
+
+void cluster_decide_hot(const ClusterState &st, BatchScratch &sc, const int32_t *acquire, const uint8_t *prio,
+                        int64_t ts_base, const uint32_t *ts_off, uint32_t n, void *out, hipStream_t s) {
+    decide_hot(st, sc, acquire, prio, ts_base, ts_off, n, (uint64_t *)out, s);
 }
 
 void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
@@ -3341,9 +3418,9 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
                            n, nullptr, invalid_key, acquire, prio, ts_off, ts_base, simple, 0xFFFFFFFFu, out, 0);
         return;
     }
-    if (sc.hot_enabled && sc.hot_lane_order && !simple && !limited && !lb &&
-        st.nslots + (uint64_t)kHot + 2 < kMaxSlots) {
-        decide_batch_hot(st, sc, flow_id, acquire, prio, ts_base, ts_off, n, out, s, clean);
+    if (cluster_hot_eligible(st, sc, n, simple, nlims)) {
+        classify_hot(st, sc, flow_id, acquire, prio, ts_base, ts_off, n, out, s, clean, false);
+        decide_hot(st, sc, acquire, prio, ts_base, ts_off, n, out, s);
         return;
     }
     SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, CTL_WORDS * 4, s));

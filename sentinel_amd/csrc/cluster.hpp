@@ -121,6 +121,7 @@ constexpr int kSubSeg = 1024;       // cold compaction segment = sort input segm
 constexpr int kHotBuckets = 64;     // window buckets a batch may span on the hot path (6 bits)
 constexpr int kHotGroupRows = 16;   // count rows per group of the column scan
 constexpr int kHotCand = 1 << 16;   // next-hot-set candidates gathered per batch
+constexpr int kSegStat = 4;         // seg_stat words per rank segment
 
 // Per-batch control words (BatchScratch::counters, zeroed per batch).
 enum : int {
@@ -202,7 +203,11 @@ struct BatchScratch {
     uint32_t *plo, *phi;      // per hot id: its range in the prioritized region
     uint32_t *hot_tot;        // per hot id: requests in the batch
     WConst *wconst;           // [256] per window-length code
-    uint32_t *seg_stat;       // per rank segment: prioritized hot requests, largest hot bucket delta
+    uint32_t *seg_stat;       // per rank segment (kSegStat words): prioritized hot requests, largest hot bucket
+                              // delta, latest request time (offset)
+    unsigned long long *tmax_all;  // latest request time of every hot-path batch classified so far (precheck of
+                                   // pipelined batches; shared by an engine's scratch sets)
+    const uint64_t *el_sorted = nullptr, *pel_sorted = nullptr;  // stage 1's sorted cold / prioritized elements
     uint32_t *hot_cand;       // [kHotCand] (slot, count) of cold rules with >= hot_min requests (hot_ctl[6])
     int hot_enabled = 1;      // host policy (sga_set_hot_rules)
     uint32_t small_max = 4096; // batches of at most this many requests take the one-workgroup path (sga_set_small_batch)
@@ -236,6 +241,18 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
                           const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, int simple,
                           void *out /* sga_token_result */, hipStream_t stream, const LimiterPass *lims = nullptr,
                           int nlims = 0);
+
+// Whether a batch takes the hot path (the small path and the limiter / RLS / look-back sort paths do not).
+bool cluster_hot_eligible(const ClusterState &st, const BatchScratch &sc, uint32_t n, int simple, int nlims);
+// The hot path in two stages for pipelined batches (sga_request_tokens_device_pipelined): stage 1 reads only the
+// batch's inputs, the dense flowId table and the hot rules' window starts (the precheck refuses a batch that
+// starts before an earlier batch's latest time); stage 2 decides.  A batch's stage 2 must follow its stage 1 and
+// every earlier batch's stage 2; the next batch on the same scratch may start stage 1 once this stage 2 is done.
+void cluster_classify_hot(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
+                          const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, void *out,
+                          hipStream_t stream);
+void cluster_decide_hot(const ClusterState &st, BatchScratch &sc, const int32_t *acquire, const uint8_t *prio,
+                        int64_t ts_base, const uint32_t *ts_off, uint32_t n, void *out, hipStream_t stream);
 
 // ---------------------------------------------------------------------------------------------
 // Cluster parameter flow (ClusterParamFlowChecker + ClusterParamMetric, CS/flow/ClusterParamFlowChecker.java:37-120,

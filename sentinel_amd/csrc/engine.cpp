@@ -114,6 +114,21 @@ struct Engine {
     DevBuf<uint8_t> d_scratch;
     BatchScratch scratch;
     uint32_t scratch_slots_cap = 0;
+    // ---- pipelined device batches (sga_request_tokens_device_pipelined): batch k + 1's stage 1 (key pass,
+    // count scans, sorts) runs on cls_stream while batch k's stage 2 (decisions) runs on the engine stream.
+    // Batches alternate between two scratch sets, each with its own hot set and its own copy of the dense
+    // flowId table (whose hot-id halfwords the hot set writes); a set is reused once its previous batch's
+    // stage 2 is done (ev_dec).  Every other engine call joins the pipeline first (join_pipeline).
+    DevBuf<uint8_t> d_scratch2;
+    BatchScratch scratch2;
+    DevBuf<uint64_t> d_dense2;
+    hipStream_t cls_stream = nullptr;
+    hipEvent_t ev_cls[2] = {nullptr, nullptr}, ev_dec[2] = {nullptr, nullptr}, ev_in = nullptr, ev_other = nullptr;
+    bool dec_recorded[2] = {false, false};
+    bool pipe_live = false;   // stage-1 work may be in flight on cls_stream
+    bool pipe_dirty = true;   // other engine work queued since the last pipelined batch
+    int parity = 0;
+    const BatchScratch *last_sc = &scratch;  // the scratch of the last batch (sga_cluster_batch_info)
     // host API staging
     DevBuf<int64_t> d_in_fid;
     DevBuf<int32_t> d_in_acq;
@@ -366,13 +381,15 @@ struct Engine {
     FlowEngine flow;
 
     int32_t uni_S = 0, uni_W = 0, uni_iv = 0;  // ClusterState::uni_S (sync_device)
-    ClusterState state() const {
+    // pset 1: the second pipelined scratch set's dense table
+    ClusterState state(int pset = 0) const {
         ClusterState st{};
         st.param = d_param.p;
         st.rec = d_rec.p;
         st.htab = d_htab.p;
-        st.dense = d_dense.p;
-        st.dense_hot = dense_n ? reinterpret_cast<uint16_t *>(d_dense.p) : nullptr;
+        uint64_t *dn = (pset && d_dense2.p) ? d_dense2.p : d_dense.p;
+        st.dense = dn;
+        st.dense_hot = dense_n ? reinterpret_cast<uint16_t *>(dn) : nullptr;
         st.slot_fid = d_slot_fid.p;
         st.wtab = d_wtab.p;
         st.dense_n = dense_n;
@@ -409,6 +426,54 @@ struct Engine {
         scratch.hot_lane_order = lds_lane_order_ok(stream) ? 1 : 0;
         scratch_slots_cap = p2;
         hot_reset(state(), scratch, p2, stream);
+        if (d_scratch2.p) {  // the pipelined set follows
+            d_scratch2.release();
+            ensure_pipeline();
+        }
+    }
+
+    // the second scratch set, the dense table copy, the classify stream and its events (first pipelined batch)
+    void ensure_pipeline() {
+        if (d_scratch2.p) return;
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+        d_scratch2.alloc(batch_scratch_bytes(cfg.max_batch, scratch_slots_cap));
+        batch_scratch_carve(scratch2, d_scratch2.p, cfg.max_batch, scratch_slots_cap);
+        scratch2.tmax_all = scratch.tmax_all;  // one latest time for both sets
+        scratch2.hot_lane_order = scratch.hot_lane_order;
+        scratch2.hot_enabled = scratch.hot_enabled;
+        scratch2.hot_min = scratch.hot_min;
+        scratch2.small_max = scratch.small_max;
+        sync_dense2();
+        hot_reset(state(1), scratch2, scratch_slots_cap, stream);
+        if (!cls_stream) {
+            SGA_HIP_CHECK(hipStreamCreateWithFlags(&cls_stream, hipStreamNonBlocking));
+            for (int k = 0; k < 2; ++k) {
+                SGA_HIP_CHECK(hipEventCreateWithFlags(&ev_cls[k], hipEventDisableTiming));
+                SGA_HIP_CHECK(hipEventCreateWithFlags(&ev_dec[k], hipEventDisableTiming));
+            }
+            SGA_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+            SGA_HIP_CHECK(hipEventCreateWithFlags(&ev_other, hipEventDisableTiming));
+        }
+        dec_recorded[0] = dec_recorded[1] = false;
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+
+    // the second dense table = the first one (slots and window codes), hot ids of its own set
+    void sync_dense2() {
+        if (!d_scratch2.p) return;
+        if (!dense_n) return;
+        if (d_dense2.n < d_dense.n) d_dense2.alloc(d_dense.n);
+        SGA_HIP_CHECK(hipMemcpyAsync(d_dense2.p, d_dense.p, (size_t)dense_n * 8, hipMemcpyDeviceToDevice, stream));
+    }
+
+    // every engine call but a pipelined batch: order it after the pipeline's in-flight stage-1 work (stage 2
+    // runs on the engine stream already), and the next pipelined stage 1 after it
+    void join_pipeline() {
+        pipe_dirty = true;
+        if (!pipe_live) return;
+        SGA_HIP_CHECK(hipEventRecord(ev_other, cls_stream));
+        SGA_HIP_CHECK(hipStreamWaitEvent(stream, ev_other, 0));
+        pipe_live = false;
     }
 
     // ---- caller streams (device entries).  Every device batch is ordered after all earlier
@@ -605,6 +670,10 @@ struct Engine {
         ensure_scratch();
         // slots may have been freed or reused: forget the hot-rule set (the next batch re-chooses it)
         hot_reset(state(), scratch, scratch_slots_cap, stream);
+        if (d_scratch2.p) {
+            sync_dense2();
+            hot_reset(state(1), scratch2, scratch_slots_cap, stream);
+        }
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
     }
 };
@@ -622,10 +691,11 @@ using sga::CEV_N;
 // No exception crosses the C ABI: HIP errors map to -EIO, host allocation failures to -ENOMEM and
 // anything else (a standard-library container throwing, say) to -EIO with its message.
 template <typename F>
-static int guarded(sga_engine *e, F &&f) {
+static int guarded(sga_engine *e, F &&f, bool join = true) {
     if (!e) return SGA_EINVAL;
     std::lock_guard<std::mutex> lk(e->impl.mu);
     try {
+        if (join) e->impl.join_pipeline();
         return f(e->impl);
     } catch (const sga::HipError &h) {
         e->impl.err = h.what;
@@ -703,6 +773,17 @@ int sga_destroy(sga_engine *e) {
             (void)hipStreamSynchronize(e->impl.stream);
             e->impl.release_events();
             batch_scratch_release(e->impl.scratch);
+            batch_scratch_release(e->impl.scratch2);
+            if (e->impl.cls_stream) {
+                (void)hipStreamSynchronize(e->impl.cls_stream);
+                for (int k = 0; k < 2; ++k) {
+                    (void)hipEventDestroy(e->impl.ev_cls[k]);
+                    (void)hipEventDestroy(e->impl.ev_dec[k]);
+                }
+                (void)hipEventDestroy(e->impl.ev_in);
+                (void)hipEventDestroy(e->impl.ev_other);
+                (void)hipStreamDestroy(e->impl.cls_stream);
+            }
             e->impl.flow.release();
             e->impl.h_stage.release();
             e->impl.h_res.release();
@@ -817,12 +898,13 @@ int sga_load_cluster_flow_rules(sga_engine *e, const char *ns, const sga_cluster
 int sga_set_hot_rules(sga_engine *e, int32_t enabled, uint32_t min_requests) {
     return guarded(e, [&](Engine &g) {
         SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
-        g.scratch.hot_enabled = enabled ? 1 : 0;
-        g.scratch.hot_min = min_requests ? min_requests : 1;
-        if (g.d_scratch.p) {
-            sga::hot_reset(g.state(), g.scratch, g.scratch_slots_cap, g.stream);
-            SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        for (sga::BatchScratch *sc : {&g.scratch, &g.scratch2}) {
+            sc->hot_enabled = enabled ? 1 : 0;
+            sc->hot_min = min_requests ? min_requests : 1;
         }
+        if (g.d_scratch.p) sga::hot_reset(g.state(), g.scratch, g.scratch_slots_cap, g.stream);
+        if (g.d_scratch2.p) sga::hot_reset(g.state(1), g.scratch2, g.scratch_slots_cap, g.stream);
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
         return SGA_OK;
     });
 }
@@ -832,7 +914,7 @@ int sga_set_hot_rules(sga_engine *e, int32_t enabled, uint32_t min_requests) {
 // the multi-launch pipeline -- the path a single requestToken takes.  Decisions do not depend on it.
 int sga_set_small_batch(sga_engine *e, uint32_t max_requests) {
     return guarded(e, [&](Engine &g) {
-        g.scratch.small_max = std::min<uint32_t>(max_requests, 4096u);
+        g.scratch.small_max = g.scratch2.small_max = std::min<uint32_t>(max_requests, 4096u);
         return SGA_OK;
     });
 }
@@ -887,10 +969,70 @@ int sga_request_tokens_device(sga_engine *e, const int64_t *d_flow_id, const int
         const auto lims = limiter_passes(g);
         sga::cluster_decide_batch(g.state(), g.scratch, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off, (uint32_t)n,
                                   0, d_out, s, lims.data(), (int)lims.size());
+        g.last_sc = &g.scratch;
         SGA_HIP_CHECK(hipGetLastError());
         g.leave_stream(s);
         return SGA_OK;
     });
+}
+
+// Pipelined device batches: stage 1 of this batch (sga::cluster_classify_hot) starts as soon as the inputs are
+// ready on hip_stream and its scratch set is free, beside the previous batch's decisions; stage 2 runs on the
+// engine stream after every earlier batch.  The outputs are on hip_stream after sga_stream_wait (or sga_sync).
+// Batches the hot path does not take (small, limited) join the pipeline and run as sga_request_tokens_device.
+int sga_request_tokens_device_pipelined(sga_engine *e, const int64_t *d_flow_id, const int32_t *d_acquire,
+                                        const uint8_t *d_prio, int64_t ts_base, const uint32_t *d_ts_off, size_t n,
+                                        sga_token_result *d_out, void *hip_stream) {
+    if (n && (!d_flow_id || !d_acquire || !d_ts_off || !d_out)) return SGA_EINVAL;
+    if (ts_base < 0) return SGA_EINVAL;
+    return guarded(
+        e,
+        [&](Engine &g) {
+            if (n > g.cfg.max_batch) return SGA_ERANGE;
+            SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+            const auto lims = limiter_passes(g);
+            if (!g.d_scratch.p || !sga::cluster_hot_eligible(g.state(), g.scratch, (uint32_t)n, 0, (int)lims.size())) {
+                g.join_pipeline();
+                hipStream_t s = g.enter_stream(hip_stream);
+                sga::cluster_decide_batch(g.state(), g.scratch, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off,
+                                          (uint32_t)n, 0, d_out, s, lims.data(), (int)lims.size());
+                g.last_sc = &g.scratch;
+                SGA_HIP_CHECK(hipGetLastError());
+                g.leave_stream(s);
+                return SGA_OK;
+            }
+            g.ensure_pipeline();
+            const int p = g.parity;
+            sga::BatchScratch &sc = p ? g.scratch2 : g.scratch;
+            hipStream_t cs = g.cls_stream;
+            // stage 1 after: the inputs, other engine work queued since the last pipelined batch, and the
+            // previous batch on this scratch set (its stage 2 leaves the hot set this batch reads)
+            if (hip_stream && (hipStream_t)hip_stream != g.stream) {
+                SGA_HIP_CHECK(hipEventRecord(g.ev_in, (hipStream_t)hip_stream));
+                SGA_HIP_CHECK(hipStreamWaitEvent(cs, g.ev_in, 0));
+            } else {
+                g.pipe_dirty = true;  // inputs made on the engine stream
+            }
+            if (g.pipe_dirty) {
+                SGA_HIP_CHECK(hipEventRecord(g.ev_other, g.stream));
+                SGA_HIP_CHECK(hipStreamWaitEvent(cs, g.ev_other, 0));
+                g.pipe_dirty = false;
+            }
+            if (g.dec_recorded[p]) SGA_HIP_CHECK(hipStreamWaitEvent(cs, g.ev_dec[p], 0));
+            const sga::ClusterState st = g.state(p);
+            sga::cluster_classify_hot(st, sc, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off, (uint32_t)n, d_out, cs);
+            SGA_HIP_CHECK(hipEventRecord(g.ev_cls[p], cs));
+            SGA_HIP_CHECK(hipStreamWaitEvent(g.stream, g.ev_cls[p], 0));
+            sga::cluster_decide_hot(st, sc, d_acquire, d_prio, ts_base, d_ts_off, (uint32_t)n, d_out, g.stream);
+            SGA_HIP_CHECK(hipEventRecord(g.ev_dec[p], g.stream));
+            g.dec_recorded[p] = true;
+            g.pipe_live = true;
+            g.parity ^= 1;
+            g.last_sc = &sc;
+            SGA_HIP_CHECK(hipGetLastError());
+            return SGA_OK;
+        },
+        false);
 }
 
 // Kept for callers of the round-1 ABI: the device entry already returns once the batch is queued,
@@ -1359,9 +1501,10 @@ int sga_cluster_batch_info(sga_engine *e, uint32_t *out, size_t n) {
         uint32_t c[sga::CTL_WORDS];
         uint32_t hc[8];
         // a hot-path batch leaves its words in counters_last (k_hot_fin clears the live ones)
-        const uint32_t *src = g.scratch.counters_clean ? g.scratch.counters_last : g.scratch.counters;
+        const sga::BatchScratch &ls = *g.last_sc;
+        const uint32_t *src = ls.counters_clean ? ls.counters_last : ls.counters;
         SGA_HIP_CHECK(hipMemcpyAsync(c, src, sizeof(c), hipMemcpyDeviceToHost, g.stream));
-        SGA_HIP_CHECK(hipMemcpyAsync(hc, g.scratch.hot_ctl, sizeof(hc), hipMemcpyDeviceToHost, g.stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(hc, ls.hot_ctl, sizeof(hc), hipMemcpyDeviceToHost, g.stream));
         SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
         const uint32_t v[11] = {c[sga::CTL_MODE],  c[sga::CTL_FLAGS], c[sga::CTL_NSORT], c[sga::CTL_NCOLD],
                                 c[sga::CTL_NPRIO], hc[0],             c[sga::CTL_BDLO],  c[sga::CTL_BDHI],

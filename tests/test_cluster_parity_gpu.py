@@ -472,6 +472,86 @@ def test_pipelined_device_batches_match_sync(eng_mod):
     H.lib().orc_cluster_free(oh)
 
 
+def _decode(r):
+    r = r.view(np.uint64)
+    return {"status": ((r >> np.uint64(48)) & np.uint64(0xFF)).astype(np.int8).astype(np.int32),
+            "remaining": (r & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32),
+            "wait_in_ms": ((r >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.uint16).view(np.int16).astype(np.int32)}
+
+
+@pytest.mark.parametrize("script", ["plain", "interleaved"])
+def test_pipelined_entry_matches_sync_and_oracle(eng_mod, script):
+    """sga_request_tokens_device_pipelined (batch b + 1's key pass and sorts beside batch b's decisions, two
+    scratch sets and dense tables) decides exactly like one sga_request_tokens_device per batch.  "interleaved"
+    puts engine calls between the batches -- metric reads (they rotate windows), a batch whose clock goes back
+    (the precheck keeps it off the hot path), a rule reload, a host-API batch -- each of which must join the
+    pipeline.  Every batch's TokenResults, the metric counters afterwards, and the sampled rules against the
+    oracle replaying the same calls."""
+    import torch
+    from sentinel_amd import _lib
+    from sentinel_amd.workload import ClusterTrace
+    c = eng_mod
+    L = _lib.load()
+    dev = torch.device("cuda", 0)
+    tr = ClusterTrace(n_rules=200_000, lam=20_000_000)
+    fid_r, cnt = tr.rules()
+    nb, m = 9, 1 << 19
+    host = [tr.events(b * m, m) for b in range(nb)]
+    if script == "interleaved":  # batch 5 replays batch 4's times shifted back by 300 ms
+        f5, a5, p5, t5 = host[5]
+        host[5] = (f5, a5, p5, host[4][3] - 300)
+    sample = np.unique(np.concatenate([tr.perm[:8] + 1, np.arange(1, 200_001, 997)])).astype(np.int64)
+    res = {}
+    for mode in ("sync", "pipe"):
+        eng = make_engine(c, hot="on", max_batch=m, max_rules=1 << 18)
+        mgr = c.ClusterFlowRuleManager(eng)
+        mgr.load_rule_arrays("default", fid_r, cnt)
+        svc = c.DefaultTokenService(eng)
+        fn = L.sga_request_tokens_device if mode == "sync" else L.sga_request_tokens_device_pipelined
+        inp = torch.cuda.Stream(dev)
+        keep, outs, extra = [], [], []
+        for b, (f, a, p, ts) in enumerate(host):
+            base = int(ts.min())
+            with torch.cuda.stream(inp):
+                d = (torch.from_numpy(f).to(dev), torch.from_numpy(a).to(dev), torch.from_numpy(p).to(dev),
+                     torch.from_numpy((ts - base).astype(np.int32)).to(dev))
+                o = torch.zeros(m, dtype=torch.int64, device=dev)
+            rc = fn(eng.handle, d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), base, d[3].data_ptr(), m,
+                    o.data_ptr(), C.c_void_p(inp.cuda_stream))
+            assert rc == 0, (mode, b, rc, L.sga_last_error(eng.handle))
+            keep.append(d)
+            outs.append(o)
+            if script == "interleaved":
+                if b == 2:  # metric reads rotate the sampled rules' windows at a later time
+                    extra.append([svc.metric_sums(int(x), int(ts.max()) + 150) for x in sample[:16]])
+                if b == 6:  # a reload: every rule kept, half the counts changed
+                    cnt2 = cnt.copy()
+                    cnt2[::2] = np.maximum(cnt2[::2] // 2, 1)
+                    mgr.load_rule_arrays("default", fid_r, cnt2)
+                if b == 7:  # a host-API batch between two pipelined ones
+                    g = svc.request_tokens(f[:5000], a[:5000], p[:5000], ts[:5000] + 1)
+                    extra.append(g["status"].tolist())
+        assert L.sga_stream_wait(eng.handle, C.c_void_p(inp.cuda_stream)) == 0
+        torch.cuda.synchronize()
+        res[mode] = [o.cpu().numpy() for o in outs]
+        res[mode + "_extra"] = extra
+        res[mode + "_metrics"] = [svc.metric_sums(int(x), int(host[-1][3].max())) for x in sample]
+        eng.close()
+    for b in range(nb):
+        assert np.array_equal(res["sync"][b], res["pipe"][b]), f"batch {b}"
+    assert res["sync_extra"] == res["pipe_extra"]
+    assert res["sync_metrics"] == res["pipe_metrics"]
+    if script == "plain":  # the sampled rules against the oracle
+        rules = [{"flow_id": int(x), "count": float(cnt[x - 1]), "threshold_type": 1} for x in sample]
+        oh = oracle_cluster({"default": rules})
+        for b, (f, a, p, ts) in enumerate(host):
+            sel = np.isin(f, sample)
+            o = oracle_replay(oh, f[sel], a[sel], p[sel], ts[sel])
+            assert_same({k: v[sel] for k, v in _decode(res["pipe"][b]).items()}, o, f[sel], ts[sel],
+                        f"pipelined batch {b}")
+        H.lib().orc_cluster_free(oh)
+
+
 def test_coalescing_queue_threads_equal_ticket_order(eng_mod):
     """sga_token_submit / sga_poll from 8 threads at once (the Netty worker pattern of
     FlowRequestProcessor.java:43): every request is decided once, and the decisions and the rules'
