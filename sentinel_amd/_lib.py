@@ -195,6 +195,8 @@ def load():
                           " (or `make -C sentinel_amd/csrc`)")
     L = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
+        if os.environ.get("SGA_LIB_VARIANT") and not hasattr(L, name):
+            continue  # an A/B build older than this symbol; the default build must export all of them
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

@@ -834,6 +834,7 @@ __global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const 
 // and read by the same workgroup.  Elements with a slot >= nkey (invalid requests, prioritized hot
 // requests) end the data.
 constexpr int kFzThreads = 256, kFzPer = 8, kFzChunk = kFzThreads * kFzPer;  // 2048
+constexpr int kFzShortRun = 4;  // closed-form runs of at most this many requests: results from the flows lane
 
 // Profiling only (SGA_FZ_DEBUG bit 16): per-phase cycles of k_cold_fused summed over workgroups.
 __device__ unsigned long long g_fz_phase[8];
@@ -925,6 +926,7 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
     // a rule that continues past the chunk, which use the global run arrays): length,
     // prioritized count, first prioritized index, acquire count | bucket delta << 8
     __shared__ uint32_t rl_n[kFzChunk], rl_cp[kFzChunk], rl_p0[kFzChunk], rl_ab[kFzChunk];
+    __shared__ uint8_t rl_done[kFzChunk];  // short closed-form runs answered by their flows lane
     __shared__ FAgg wtot[kFzThreads / 64];
     __shared__ uint32_t s_h0, s_E, s_wcnt[kFzThreads / 64];
     __shared__ uint32_t s_ncand, s_cbase, s_next, s_cand[2 * kFzThreads];
@@ -1054,6 +1056,7 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
                     rl_cp[head - h0] = run.np - run.hp;
                     rl_p0[head - h0] = h0 + run.hp;
                     rl_ab[head - h0] = (uint32_t)acq | (bd << 8);
+                    rl_done[head - h0] = 0;
                 } else {  // global run arrays, indexed by head position
                     sc.run_start[head] = p + 1 - head;
                     sc.run_cp[head] = run.np - run.hp;
@@ -1171,7 +1174,33 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
             ro.mode = RUN_DONE;
             rc.have = false;  // the record changed in memory
         }
-        sc.run_out[r] = ro;
+        if (fast && ri.n <= (uint32_t)kFzShortRun && r - h0 < (uint32_t)kFzChunk) {
+            // a short run's TokenResults from its flows lane (the results phase skips it): the run's elements
+            // loaded together at clamped positions, decided as the results phase would
+            uint64_t x[kFzShortRun];
+#pragma unroll
+            for (int u = 0; u < kFzShortRun; ++u) x[u] = el[r + min((uint32_t)u, ri.n - 1)];
+            uint32_t kp = 0;  // prioritized requests of the run before this one
+#pragma unroll
+            for (int u = 0; u < kFzShortRun; ++u) {
+                if ((uint32_t)u >= ri.n) break;
+                const uint32_t pr = el_prio(x[u]);
+                uint64_t res;
+                if ((uint32_t)u < ro.f) {
+                    const int64_t sum = ro.s0 + (int64_t)u * ri.a;
+                    res = pack_result(TRS_OK, j_d2i(ro.thr - (double)sum / ro.isec - (double)ri.a), 0);
+                } else if (pr && kp - ro.cpf < ro.cw) {
+                    res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)ro.wait);
+                } else {
+                    res = pack_result(TRS_BLOCKED, 0, 0);
+                }
+                out[el_idx(x[u])] = res;
+                kp += pr;
+            }
+            rl_done[r - h0] = 1;
+        } else {
+            sc.run_out[r] = ro;
+        }
         r += ri.n;
         if (r >= r1) {
             f = atomicAdd(&s_next, 1u);
@@ -1221,11 +1250,14 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
             head[k] = run.hpos - 1;
             kp[k] = run.np - pr - run.hp;  // prioritized requests of the run before this one
         }
-        // run records of the 8 elements loaded together (one per run change)
+        // run records of the 8 elements loaded together (one per run change; none for a short run its flows
+        // lane answered)
         RunOut ro[kFzPer];
 #pragma unroll
         for (int k = 0; k < kFzPer; ++k) {
-            if (e0 + k < E && (k == 0 || head[k] != head[k - 1])) ro[k] = sc.run_out[head[k]];
+            const bool done = head[k] - h0 < (uint32_t)kFzChunk && rl_done[head[k] - h0];
+            if (done) ro[k].mode = RUN_DONE;
+            else if (e0 + k < E && (k == 0 || head[k] != head[k - 1])) ro[k] = sc.run_out[head[k]];
             else if (k > 0) ro[k] = ro[k - 1];
         }
 #pragma unroll
@@ -3264,6 +3296,22 @@ static int hot_key_bits(const ClusterState &st) {
 // the prioritized sort and the cold sort.  The result is in sc (CTL words, el[], pel[], hcode, hbase).
 // pipelined: an earlier batch may still be deciding (sga_request_tokens_device_pipelined); the precheck
 // then also refuses the hot path to a batch that starts before the latest time of any earlier batch.
+// The hot side's runs and results (k_prio_rank, k_hot_flows, k_hot_final): once the count scans and the
+// prioritized sort are done, on hs; ev_mid after the hot runs (the next hot set may start), ev_join after all.
+static void hot_side(const ClusterState &st, BatchScratch &sc, int64_t ts_base, uint32_t n, uint64_t *out,
+                     hipStream_t hs, bool ovl) {
+    const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
+    const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
+    hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, sc.pel_sorted);
+    hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, hs, st, sc, ts_base);
+    if (ovl) {
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_mid, hs));  // the hot runs read hot_slot; the next hot set may start
+        hipLaunchKernelGGL(k_hot_final, dim3(nseg + kFinPrioWgs), dim3(kFinWgThreads), 0, hs, st, sc, n, sc.pel_sorted,
+                           out, fin_cache());
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_join, hs));
+    }
+}
+
 static void classify_hot(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
                          const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, uint64_t *out,
                          hipStream_t s, bool clean, bool pipelined) {
@@ -3302,10 +3350,15 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const int64_t
     const int npp = radix_sort_u64_tiled(sc.pel_tile, sc.ptile_np, sc.counters + CTL_NPRIO, sc.pel[0], sc.pel[1], n,
                                          kSlotShift, 12, sc.radix_p, hs, false);
     sc.pel_sorted = (npp & 1) ? sc.pel[0] : sc.pel[1];
+    // Not pipelined: the hot side needs nothing of the cold sort (disjoint rules, disjoint results), so its runs
+    // and results go on beside the sort and the cold stage waits for it only at the end of the batch.  Pipelined,
+    // the hot runs write rule state and wait for stage 2 (after the earlier batch's decisions).
+    sc.hot_early = ovl && !pipelined;
+    if (sc.hot_early) hot_side(st, sc, ts_base, n, out, hs, true);
     const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
                                         kSlotShift, bits, sc.radix, s, d0 > 0);
     sc.el_sorted = (np & 1) ? sc.el[0] : sc.el[1];
-    if (ovl) {  // stage 1 ends on s
+    if (ovl && !sc.hot_early) {  // stage 1 ends on s
         SGA_HIP_CHECK(hipEventRecord(sc.ev_fork, hs));
         SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_fork, 0));
     }
@@ -3319,21 +3372,15 @@ static void decide_hot(const ClusterState &st, BatchScratch &sc, const int32_t *
     const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
     const uint64_t *el = sc.el_sorted, *pel = sc.pel_sorted;
     const bool ovl = hot_overlap() && !(fz_debug() & 16);
-    hipStream_t hs = s;
-    if (ovl) {
-        side_stream_init(sc);
-        SGA_HIP_CHECK(hipEventRecord(sc.ev_fork0, s));
-        SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork0, 0));
-        hs = sc.side;
-    }
-    const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
-    hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, pel);
-    hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, hs, st, sc, ts_base);
-    if (ovl) {
-        SGA_HIP_CHECK(hipEventRecord(sc.ev_mid, hs));  // the hot runs read hot_slot; the next hot set may start
-        hipLaunchKernelGGL(k_hot_final, dim3(nseg + kFinPrioWgs), dim3(kFinWgThreads), 0, hs, st, sc, n, pel, out,
-                           fin_cache());
-        SGA_HIP_CHECK(hipEventRecord(sc.ev_join, hs));
+    if (!sc.hot_early) {  // the hot side beside the cold stage
+        hipStream_t hs = s;
+        if (ovl) {
+            side_stream_init(sc);
+            SGA_HIP_CHECK(hipEventRecord(sc.ev_fork0, s));
+            SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork0, 0));
+            hs = sc.side;
+        }
+        hot_side(st, sc, ts_base, n, out, hs, ovl);
     }
     cold_stage(st, sc, el, n, sc.counters + CTL_NCOLD, invalid_key, acquire, prio, ts_off, ts_base, 0,
                std::max<uint32_t>(sc.hot_min, 1), out, s);

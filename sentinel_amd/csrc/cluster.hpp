@@ -208,6 +208,7 @@ struct BatchScratch {
     unsigned long long *tmax_all;  // latest request time of every hot-path batch classified so far (precheck of
                                    // pipelined batches; shared by an engine's scratch sets)
     const uint64_t *el_sorted = nullptr, *pel_sorted = nullptr;  // stage 1's sorted cold / prioritized elements
+    bool hot_early = false;   // host: the batch's hot runs and results were queued in stage 1 (beside the cold sort)
     uint32_t *hot_cand;       // [kHotCand] (slot, count) of cold rules with >= hot_min requests (hot_ctl[6])
     int hot_enabled = 1;      // host policy (sga_set_hot_rules)
     uint32_t small_max = 4096; // batches of at most this many requests take the one-workgroup path (sga_set_small_batch)
