@@ -41,7 +41,8 @@ enum : uint32_t { F_EXIT = 1u << 30, F_ERROR = 1u << 29, F_PARAM = 1u << 28, F_I
 constexpr uint32_t kHeavyEvents = 1024;  // per batch: replayed by k_lheavy instead of one k_lflows lane
 // RUN_POS: k_lwave left each entry's decision and wait in ev_eidx (wait << 1 | blocked; ~0: written
 // already), k_lresults scatters them in parallel
-enum : uint8_t { RUN_FAST = 0, RUN_DONE = 1, RUN_POS = 2 };
+// RUN_PSEG: a parameter-only resource's run, decided per (rule, value) segment (k_pseg_*)
+enum : uint8_t { RUN_FAST = 0, RUN_DONE = 1, RUN_POS = 2, RUN_PSEG = 3 };
 
 struct Ctx {
     FlowState st;
@@ -1694,6 +1695,63 @@ __device__ void lane_run(const Ctx &c, int64_t max_rt, FlowScratch &sc, const Pa
     sc.run_mode[r] = RUN_FAST;
 }
 
+// A parameter-only resource (one QPS-grade ParamFlowRule of index 0, no FlowRule, no breaker, its maps in
+// free mode) is decided per (rule, value) segment (k_pseg_*): a value's token bucket / throttle time and its
+// thread count see only that value's events, and its node statistics never feed a decision.  Taken here,
+// in k_lflows, on the flow's lane: ParamFlowSlot.applyRealParamIdx fixes an unresolved index at the first
+// entry (as chain_entry would), and the first entry creates the thread-count map of index 0
+// (ParameterMetricStorage.initParamMetricsFor) -- a flow whose parameter exits come before that entry
+// while the map does not exist yet stays with the event-by-event replay.
+__device__ bool pseg_take(const FlowState &st, const FlowScratch &sc, const Payload *__restrict__ pay, uint32_t res,
+                          uint32_t r0, uint32_t r1) {
+    const ResDev R = st.res[res];
+    if (R.n_rules || R.n_cbs || R.n_prules != 1 || !st.tmapmask) return false;
+    ParamRuleDev &p = st.prules[R.prule_off];
+    if (p.grade != 1 || p.cluster) return false;
+    const uint32_t jb = sc.run_start[r0], je = sc.run_end[r1 - 1];
+    bool ent = false;
+    for (uint32_t r = r0; r < r1 && !ent; ++r) ent = sc.run_nent[r] != 0;
+    if (!ent) {  // exits only: nothing to resolve, the map exists or is never touched
+        return p.idx_res == 0;
+    }
+    uint32_t j = jb;
+    bool pexit = false;  // a parameter exit before the first entry
+    for (; j < je; ++j) {
+        const uint32_t f = pay[j].idx;
+        if (!(f & F_EXIT)) break;
+        pexit |= (f & F_PARAM) != 0;
+    }
+    int32_t idx = p.idx_res;
+    if (idx == kIdxUnresolved) {
+        if (j == je) return false;
+        idx = param_idx_of(p, (pay[j].idx & F_PARAM) ? 1u : 0u);
+    }
+    if (idx != 0) return false;
+    const uint64_t mask = st.tmapmask[res];
+    if (!(mask & 1ull) && j < je) {
+        if (pexit) return false;
+        st.tmapmask[res] = mask | 1ull;
+    }
+    return true;
+}
+
+// A breaker-only resource (one DegradeRule, no FlowRule, no ParamFlowRule) whose batch holds only entries or
+// only exits: its entries move the breaker only OPEN -> HALF_OPEN (the first entry at or after the retry
+// time, AbstractCircuitBreaker.tryPass), its exits only feed the breaker (onRequestComplete); k_cb_flows
+// decides it, the node statistics go in aggregate as for the parameter-only resources.  Returns 0 (not
+// taken), 1 (taken, no breaker work: a CLOSED breaker passes every entry) or 2 (taken, k_cb_flows).
+__device__ int cb_take(const FlowState &st, const FlowScratch &sc, uint32_t res, uint32_t r0, uint32_t r1) {
+    const ResDev R = st.res[res];
+    if (R.n_rules || R.n_prules || R.n_cbs != 1) return 0;
+    bool ent = false, ex = false;
+    for (uint32_t r = r0; r < r1; ++r) {
+        ent |= sc.run_nent[r] != 0;
+        ex |= sc.run_nexit[r] != 0;
+    }
+    if (ent && ex) return 0;
+    return (ent && st.cbs[R.cb_off].state == 0) ? 1 : 2;
+}
+
 __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, FlowScratch sc,
                                                const Payload *__restrict__ pay, const uint32_t *__restrict__ keys,
                                                int64_t ts_base, const int64_t *__restrict__ rt_in,
@@ -1710,6 +1768,19 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
             const uint32_t nev = sc.run_end[r1 - 1] - sc.run_start[r0];
             if (st.lru_res && st.lru_res[res]) {  // a CacheMap in LRU mode: arrival order, one lane (k_llru)
                 sc.lru[atomicAdd(&sc.counters[10], 1u)] = fl;
+                continue;
+            }
+            int cbk = 0;
+            if (sc.pseg && ((cbk = cb_take(st, sc, res, r0, r1)) != 0 ||
+                            pseg_take(st, sc, pay, res, r0, r1))) {
+                if (cbk == 2) sc.cbf[atomicAdd(&sc.counters[13], 1u)] = fl;
+                for (uint32_t r = r0; r < r1; ++r) {
+                    sc.run_mode[r] = RUN_PSEG;
+                    sc.run_pa[r] = 0;
+                    sc.run_ba[r] = 0;
+                    sc.run_np[r] = 0;
+                }
+                sc.pseg[atomicAdd(&sc.counters[11], 1u)] = fl;
                 continue;
             }
             if ((st.res[res].fast & 5u) == 0 && nev >= kHeavyEvents) {
@@ -2716,6 +2787,596 @@ __global__ __launch_bounds__(64) void k_llru(FlowState st, int64_t max_rt, FlowS
     }
 }
 
+// ---- parameter-only resources per (rule, value) segment (pseg_take routes their flows here)
+// 1. every parameter event of such a flow names its value's thread-count map entry (owner resource + 1,
+//    argument 0; the map exists for the whole batch, pseg_take).  kClaim: make sure the entries exist --
+//    the thread-count one for every parameter event, the rule's (time, tokens) one for every entry (two
+//    lanes may claim a slot each for one key; the later one in the probe sequence is never found again,
+//    its key absent, dropped at the next rehash).  !kClaim: the element (slot << 32 | sorted position),
+//    kPsegNone in the slot bits for every other event.
+template <bool kClaim>
+__global__ __launch_bounds__(kT) void k_pseg_key(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
+                                                 const uint32_t *__restrict__ keys,
+                                                 const uint64_t *__restrict__ param_in, uint32_t m, uint64_t none) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    const uint32_t nvalid = sc.counters[0];
+    const bool any = sc.counters[11] != 0;
+    if (kClaim && !any) return;
+    for (uint32_t j = blockIdx.x * kT + threadIdx.x; j < m; j += gridDim.x * kT) {
+        uint64_t el = none | j;
+        if (any && j < nvalid && sc.run_mode[sc.ev_run[j]] == RUN_PSEG) {
+            const Payload q = pay[j];
+            if (q.idx & F_PARAM) {
+                const uint32_t res = keys[j];
+                const uint64_t v = param_in[q.idx & F_IDX];
+                if (st.tmapmask[res] & 1ull) {  // else an exit-only flow without the map: the exit touches no map
+                    PEntry *te = ptab_get(st.ttab, st.tmask, tmap_owner(res, 0), v, kClaim, st.overflow);
+                    if (kClaim && !(q.idx & F_EXIT))
+                        ptab_get(st.ptab, st.pmask, st.prules[st.res[res].prule_off].id + 1, v, true, st.overflow);
+                    if (!kClaim && te) {
+                        el = ((uint64_t)(te - st.ttab) << 32) | j;
+                        if (te->b != 0) te->b = 0;  // the segment's flag word for this batch (k_pseg_heads)
+                    }
+                }
+            }
+        }
+        if (!kClaim) sc.pel[0][j] = el;
+    }
+}
+
+// SGA_PSEG_DEBUG=1 (diagnostics only): the sorted elements out of order, and pseg elements of resources in
+// LRU mode (never expected)
+__global__ __launch_bounds__(kT) void k_pseg_check(FlowState st, const uint32_t *__restrict__ keys,
+                                                   const uint64_t *__restrict__ el, uint32_t m, uint64_t none,
+                                                   uint32_t *out) {
+    for (uint32_t e = blockIdx.x * kT + threadIdx.x; e < m; e += gridDim.x * kT) {
+        const uint64_t k = el[e] >> 32;
+        if (e > 0 && k < (el[e - 1] >> 32)) atomicAdd(&out[0], 1u);
+        if (k == none >> 32) continue;
+        atomicAdd(&out[1], 1u);
+        const uint32_t res = keys[(uint32_t)el[e]];
+        if (st.lru_res && st.lru_res[res]) atomicAdd(&out[2], 1u);
+        if (st.ttab[k].owner != res + 1) atomicAdd(&out[3], 1u);
+    }
+}
+
+// 2. segment heads of the sorted elements
+//    and each segment's flag word (the b word of its thread-count entry, which a thread count never uses):
+//    kSegExit / kSegEntry when it holds exits / entries, kSegIrregular when an entry's acquire count differs
+//    from the previous entry's or its time goes back (the closed forms of k_pseg_solve / k_pseg_long need
+//    one acquire count and non-decreasing times)
+constexpr int64_t kSegExit = 1, kSegEntry = 2, kSegIrregular = 4;
+__global__ __launch_bounds__(kT) void k_pseg_heads(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
+                                                   const uint64_t *__restrict__ el, uint32_t m, uint64_t none) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0) || sc.counters[11] == 0) return;
+    for (uint32_t e = blockIdx.x * kT + threadIdx.x; e < m; e += gridDim.x * kT) {
+        const uint64_t x = el[e];
+        const uint64_t k = x >> 32;
+        if (k == none >> 32) continue;
+        const bool head = e == 0 || (el[e - 1] >> 32) != k;
+        if (head) sc.seg[atomicAdd(&sc.counters[12], 1u)] = e;
+        const Payload q = pay[(uint32_t)x];
+        int64_t f = (q.idx & F_EXIT) ? kSegExit : kSegEntry;
+        if (!head && !(q.idx & F_EXIT)) {
+            const Payload pq = pay[(uint32_t)el[e - 1]];
+            if (!(pq.idx & F_EXIT) && ((pq.acq_prio & 0x7FFFFFFFu) != (q.acq_prio & 0x7FFFFFFFu) || q.ts_off < pq.ts_off))
+                f |= kSegIrregular;
+        }
+        int64_t *w = &st.ttab[k].b;
+        if ((*w & f) != f) atomicOr((unsigned long long *)w, (unsigned long long)f);  // a read first: hot segments
+    }
+}
+
+// 3. one lane per segment: the value's events in arrival order against its entries held in registers
+//    (ParamFlowChecker.passDefaultLocalCheck / passThrottleLocalCheck via param_pass_qps, ParameterMetric
+//    add/decreaseThreadCount as param_threads), the entries, their access stamps and the owners' present
+//    counts written back once (free mode: the count pass keeps these owners below capacity)
+constexpr int kPsegG = 8;       // elements loaded ahead
+constexpr int kPsegLong = 512;  // regular entry segments this long go to k_pseg_long
+__global__ __launch_bounds__(kT) void k_pseg_solve(FlowState st, int64_t max_rt, FlowScratch sc,
+                                                   const Payload *__restrict__ pay, const uint32_t *__restrict__ keys,
+                                                   const uint64_t *__restrict__ el, uint32_t m, int64_t ts_base,
+                                                   const uint64_t *__restrict__ param_in, int8_t *decision,
+                                                   int32_t *wait_ms) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    const Ctx c{st, max_rt};
+    const uint32_t nseg = sc.counters[12];
+    for (uint32_t s = blockIdx.x * kT + threadIdx.x; s < nseg; s += gridDim.x * kT) {
+        const uint32_t e0 = sc.seg[s];
+        const uint64_t key = el[e0] >> 32;
+        const uint32_t j0 = (uint32_t)el[e0];
+        const uint32_t res = keys[j0];
+        const ParamRuleDev prule = st.prules[st.res[res].prule_off];
+        const uint64_t v = param_in[pay[j0].idx & F_IDX];
+        PEntry *const tp = st.ttab + key;
+        int64_t ta = tp->a;
+        const bool t0 = ta != kPAbsent;
+        PEntry *pp = nullptr;
+        PEntry pe{};
+        bool p0 = false;
+        uint64_t pst = 0, tst = 0;  // the last access stamps
+        bool more = true;
+        const int64_t flags = tp->b;
+        if (flags == kSegExit || flags == kSegEntry) {
+            // the segment's end: galloping search on the keys
+            uint32_t lo = e0 + 1, step = 1, hi = e0 + 1;
+            while (hi < m && (el[hi] >> 32) == key) {
+                lo = hi + 1;
+                hi = min(m, hi + step);
+                step <<= 1;
+            }
+            while (lo < hi) {  // first index in [lo, hi) with another key (hi: one, or m)
+                const uint32_t mid = (lo + hi) >> 1;
+                if ((el[mid] >> 32) == key) lo = mid + 1;
+                else hi = mid;
+            }
+            const uint32_t e1 = lo;
+            if (flags == kSegEntry && e1 - e0 >= (uint32_t)kPsegLong) {  // one wave decides it (k_pseg_long)
+                const uint32_t li = atomicAdd(&sc.counters[14], 1u);
+                sc.plong[2 * li] = e0;
+                sc.plong[2 * li + 1] = e1 - e0;
+                continue;
+            }
+            if (flags == kSegExit) {
+                // exits only: decreaseThreadCount n times (absent -> 0, 0 or 1 -> absent, c -> c - 1)
+                const int64_t n = e1 - e0;
+                int64_t st0 = ta;
+                int64_t rem = n;
+                if (ta != kPAbsent && ta >= 1) {
+                    if (n < ta) {
+                        st0 = ta - n;
+                        rem = 0;
+                    } else {
+                        st0 = kPAbsent;
+                        rem = n - ta;
+                    }
+                }
+                if (rem) st0 = ((rem & 1) ? (st0 == kPAbsent ? 0 : kPAbsent) : st0);
+                ta = st0;
+                tst = lru_stamp(st, pay[(uint32_t)el[e1 - 1]].idx & F_IDX, 0);
+                more = false;
+            }
+        }
+        for (uint32_t g = e0; more; g += kPsegG) {
+            uint64_t x[kPsegG];
+            Payload q[kPsegG];
+#pragma unroll
+            for (int u = 0; u < kPsegG; ++u) x[u] = el[min(g + u, m - 1)];
+#pragma unroll
+            for (int u = 0; u < kPsegG; ++u) q[u] = pay[(uint32_t)x[u]];
+#pragma unroll
+            for (int u = 0; u < kPsegG; ++u) {
+                if (!more || g + u >= m || (x[u] >> 32) != key) {
+                    more = false;
+                    continue;
+                }
+                const uint32_t idx = q[u].idx & F_IDX;
+                const uint64_t stamp = lru_stamp(st, idx, 0);
+                if (q[u].idx & F_EXIT) {  // decreaseThreadCount: an absent count is put as 0, a count reaching 0 removed
+                    ta = ta == kPAbsent ? 0 : (ta - 1 <= 0 ? kPAbsent : ta - 1);
+                    tst = stamp;
+                    continue;
+                }
+                if (!pp) {
+                    pp = ptab_get(st.ptab, st.pmask, prule.id + 1, v, false, st.overflow);
+                    if (!pp) {  // overflow: the batch fails (-ENOMEM)
+                        more = false;
+                        continue;
+                    }
+                    pe = *pp;
+                    p0 = pe.a != kPAbsent;
+                }
+                const int aq = (int)(q[u].acq_prio & 0x7FFFFFFFu);
+                if (param_map_access(c, prule, v, aq)) pst = stamp;
+                int64_t w = 0;
+                const bool pass = param_pass_qps(c, prule, pe, v, aq, ts_base + (int64_t)q[u].ts_off, &w);
+                decision[idx] = pass ? D_PASS : D_BLOCK_PARAM;
+                wait_ms[idx] = pass ? (int32_t)w : 0;  // a block's detail: the rule's index (0)
+                if (pass) {  // addThreadCount
+                    ta = (ta == kPAbsent ? 0 : ta) + 1;
+                    tst = stamp;
+                }
+            }
+        }
+        if (pp) {
+            pp->a = pe.a;
+            pp->b = pe.b;
+            if (pst && st.pstamp) st.pstamp[pp - st.ptab] = pst;
+            const int d = (pe.a != kPAbsent ? 1 : 0) - (p0 ? 1 : 0);
+            if (d && st.psize) atomicAdd(&st.psize[prule.id], (uint32_t)d);
+        }
+        tp->a = ta;
+        if (tst && st.tstamp) st.tstamp[key] = tst;
+        const int d = (ta != kPAbsent ? 1 : 0) - (t0 ? 1 : 0);
+        if (d && lru_on_t(st, res)) atomicAdd(&st.tsize[st.tbase[res]], (uint32_t)d);
+    }
+}
+
+// Breaker-only flows (cb_take): one wave each, the breaker in registers (uniform over the lanes).
+//   entries only: HALF_OPEN blocks every entry; OPEN blocks every entry but the first at or after the retry
+//     time, which passes and moves the breaker to HALF_OPEN (DegradeSlot.entry, AbstractCircuitBreaker.tryPass);
+//   exits only (onRequestComplete, cb_on_complete_ws): the stat window (LeapArray(1, statIntervalMs)) counts
+//     as a segmented scan over the exits in rounds of 64 x kCbI (segments = windows, non-decreasing); a CLOSED
+//     breaker opens at the first exit whose window counts trip it, and exits after that only count; a
+//     HALF_OPEN one is decided by its first exit, stepped alone; a window that goes back in time (a detached
+//     bucket) sends the rest of the flow to the step-by-step replay.
+constexpr int kCbI = 32;
+struct CbAgg {
+    int64_t ws, bad, tot;  // the last window's counts (ws == kCbNone: no exit)
+};
+constexpr int64_t kCbNone = INT64_MIN + 1;
+__device__ __forceinline__ CbAgg cb_combine(const CbAgg &p, const CbAgg &x) {
+    if (x.ws == kCbNone) return p;
+    if (x.ws == p.ws) return CbAgg{x.ws, p.bad + x.bad, p.tot + x.tot};
+    return x;
+}
+__device__ __forceinline__ int64_t shfl_up_i64(int64_t v, int o) {
+    const int lo = __shfl_up((int)(uint32_t)v, o, 64), hi = __shfl_up((int)(uint32_t)((uint64_t)v >> 32), o, 64);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__global__ __launch_bounds__(64) void k_cb_flows(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
+                                                 int64_t ts_base, const int64_t *__restrict__ rt_in, int8_t *decision,
+                                                 int32_t *wait_ms) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    const int lane = threadIdx.x;
+    const uint32_t ncb = sc.counters[13], nflows = sc.counters[2], nruns = sc.counters[1];
+    for (uint32_t h = blockIdx.x; h < ncb; h += gridDim.x) {
+        const uint32_t fl = sc.cbf[h];
+        const uint32_t r0 = sc.flow_first_run[fl];
+        const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        const uint32_t res = sc.run_slot[r0];
+        const uint32_t jb = sc.run_start[r0], je = sc.run_end[r1 - 1];
+        CbDev *gb = st.cbs + st.res[res].cb_off;
+        CbDev b = *gb;
+        if (!(pay[jb].idx & F_EXIT)) {  // entries only (the breaker is not CLOSED)
+            uint32_t probe = je;
+            if (b.state == 1) {
+                for (uint32_t base = jb; base < je && probe == je; base += 64 * kCbI) {
+                    uint32_t mine = je;
+                    for (int i = 0; i < kCbI; ++i) {
+                        const uint32_t j = base + (uint32_t)lane * kCbI + i;
+                        if (j < je && ts_base + (int64_t)pay[j].ts_off >= b.next_retry) {
+                            mine = j;
+                            break;
+                        }
+                    }
+                    const uint64_t has = __ballot(mine < je);
+                    if (has) probe = (uint32_t)__shfl((int)mine, __ffsll((unsigned long long)has) - 1, 64);
+                }
+                if (probe < je) b.state = 2;  // fromOpenToHalfOpen: the probe passes
+            }
+            for (uint32_t j = jb + lane; j < je; j += 64) {
+                const uint32_t idx = pay[j].idx & F_IDX;
+                decision[idx] = j == probe ? D_PASS : D_BLOCK_DEGRADE;
+                wait_ms[idx] = 0;  // a block's detail: the breaker's index
+            }
+        } else {  // exits only
+            const int64_t si = b.stat_interval;
+            CbAgg carry{b.st_start == kAbsent ? kCbNone : b.st_start, b.st_bad, b.st_total};
+            bool seq = false;
+            uint32_t base = jb;
+            while (base < je && !seq) {
+                if (b.state == 2) {  // the probe's completion decides HALF_OPEN alone
+                    const Payload q = pay[base];
+                    const int64_t t = ts_base + (int64_t)q.ts_off;
+                    b.st_start = carry.ws == kCbNone ? kAbsent : carry.ws;
+                    b.st_bad = carry.bad;
+                    b.st_total = carry.tot;
+                    cb_on_complete_ws(b, t, t - t % si, rt_in[q.idx & F_IDX], (q.idx & F_ERROR) != 0);
+                    carry = CbAgg{b.st_start == kAbsent ? kCbNone : b.st_start, b.st_bad, b.st_total};
+                    ++base;
+                    continue;
+                }
+                int64_t wsv[kCbI];
+                uint32_t badm = 0, valm = 0;
+                const uint32_t j0 = base + (uint32_t)lane * kCbI;
+#pragma unroll
+                for (int i = 0; i < kCbI; ++i) {
+                    const uint32_t j = j0 + i;
+                    wsv[i] = kCbNone;
+                    if (j < je) {
+                        const Payload q = pay[j];
+                        const int64_t t = ts_base + (int64_t)q.ts_off;
+                        wsv[i] = t - t % si;
+                        const bool bad = b.grade == 0 ? rt_in[q.idx & F_IDX] > b.max_allowed_rt : (q.idx & F_ERROR) != 0;
+                        badm |= (bad ? 1u : 0u) << i;
+                        valm |= 1u << i;
+                    }
+                }
+                // windows must not go back: inside the lane, across lanes, and against the carry
+                bool mono = true;
+                int64_t first = kCbNone, last = kCbNone;
+#pragma unroll
+                for (int i = 0; i < kCbI; ++i) {
+                    if (!((valm >> i) & 1u)) continue;
+                    if (first == kCbNone) first = wsv[i];
+                    else if (wsv[i] < last) mono = false;
+                    last = wsv[i];
+                }
+                const int64_t prev_last = wave_incl_max_i64(last == kCbNone ? INT64_MIN : last);
+                const int64_t before = shfl_up_i64(prev_last, 1);
+                const int64_t lim = lane == 0 ? (carry.ws == kCbNone ? INT64_MIN : carry.ws)
+                                              : max(before, carry.ws == kCbNone ? INT64_MIN : carry.ws);
+                if (first != kCbNone && first < lim) mono = false;
+                if (!__all(mono)) {
+                    seq = true;
+                    break;
+                }
+                CbAgg agg{kCbNone, 0, 0};
+#pragma unroll
+                for (int i = 0; i < kCbI; ++i)
+                    if ((valm >> i) & 1u) agg = cb_combine(agg, CbAgg{wsv[i], (int64_t)((badm >> i) & 1u), 1});
+                // exclusive scan of the lane aggregates (Hillis-Steele on shuffles), the carry in front
+                CbAgg inc = agg;
+                for (int o = 1; o < 64; o <<= 1) {
+                    CbAgg y{shfl_up_i64(inc.ws, o), shfl_up_i64(inc.bad, o), shfl_up_i64(inc.tot, o)};
+                    if (lane >= o) inc = cb_combine(y, inc);
+                }
+                CbAgg ex{shfl_up_i64(inc.ws, 1), shfl_up_i64(inc.bad, 1), shfl_up_i64(inc.tot, 1)};
+                if (lane == 0) ex = CbAgg{kCbNone, 0, 0};
+                CbAgg run = cb_combine(carry, ex);
+                uint32_t trip = je;
+                if (b.state == 0) {
+#pragma unroll
+                    for (int i = 0; i < kCbI; ++i) {
+                        if (!((valm >> i) & 1u)) continue;
+                        run = cb_combine(run, CbAgg{wsv[i], (int64_t)((badm >> i) & 1u), 1});
+                        if (trip == je && cb_trips(b, run.bad, run.tot)) trip = j0 + i;
+                    }
+                }
+                const uint64_t tb = __ballot(trip < je);
+                if (tb) {  // the first exit that trips a CLOSED breaker opens it (cb_to_open)
+                    const uint32_t k = (uint32_t)__shfl((int)trip, __ffsll((unsigned long long)tb) - 1, 64);
+                    cb_to_open(b, ts_base + (int64_t)pay[k].ts_off);
+                }
+                const CbAgg all = cb_combine(carry, cb_combine(ex, agg));
+                carry = CbAgg{readlane_i64(all.ws, 63), readlane_i64(all.bad, 63), readlane_i64(all.tot, 63)};
+                base += 64 * kCbI;
+            }
+            b.st_start = carry.ws == kCbNone ? kAbsent : carry.ws;
+            b.st_bad = carry.bad;
+            b.st_total = carry.tot;
+            if (seq)  // step by step (every lane the same steps)
+                for (uint32_t j = base; j < je; ++j) {
+                    const Payload q = pay[j];
+                    const int64_t t = ts_base + (int64_t)q.ts_off;
+                    cb_on_complete_ws(b, t, t - t % si, rt_in[q.idx & F_IDX], (q.idx & F_ERROR) != 0);
+                }
+        }
+        if (lane == 0) *gb = b;
+    }
+}
+
+// 3b. a long segment of entries with one acquire count and non-decreasing times: one wave, by stretches
+//    instead of events.  Token bucket (passDefaultLocalCheck): between two refills (pass_time > duration)
+//    the first floor(tokens / acquire) entries pass and the rest block, so a stretch is one search for the
+//    next refill time and two fills; the refill itself is one exact step.  Throttle (passThrottleLocalCheck):
+//    an entry passes iff expected - t < maxQueueingTimeMs or expected <= t, so the next pass is one search
+//    for the first t >= expected - max(maxQueueingTimeMs - 1, 0).  Searches are 64-ary (a probe per lane),
+//    fills write the decisions on all lanes.
+__device__ __forceinline__ int64_t pseg_time(const Payload *__restrict__ pay, const uint64_t *__restrict__ el,
+                                             int64_t ts_base, uint32_t e) {
+    return ts_base + (int64_t)pay[(uint32_t)el[e]].ts_off;
+}
+// first e in [lo, hi) with time > x (hi if none); times non-decreasing over [lo, hi)
+__device__ uint32_t pseg_upper(const Payload *__restrict__ pay, const uint64_t *__restrict__ el, int64_t ts_base,
+                               uint32_t lo, uint32_t hi, int64_t x) {
+    const int lane = threadIdx.x & 63;
+    while (hi - lo > 64) {
+        const uint32_t step = (hi - lo + 63) / 64;
+        const uint32_t p = lo + (uint32_t)lane * step;
+        const bool gt = p < hi && pseg_time(pay, el, ts_base, p) > x;
+        const uint64_t b = __ballot(gt);
+        if (!b) {
+            lo = min(hi, lo + 63 * step + 1);  // every probe <= x: past the last one (lane 63's, or hi)
+            continue;
+        }
+        const int f = __ffsll((unsigned long long)b) - 1;
+        if (f == 0) return lo;
+        hi = lo + (uint32_t)f * step;  // satisfies
+        lo = lo + (uint32_t)(f - 1) * step + 1;
+    }
+    const uint32_t p = lo + (uint32_t)lane;
+    const uint64_t b = __ballot(p < hi && pseg_time(pay, el, ts_base, p) > x);
+    return b ? lo + (uint32_t)(__ffsll((unsigned long long)b) - 1) : hi;
+}
+__global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, FlowScratch sc,
+                                                  const Payload *__restrict__ pay, const uint32_t *__restrict__ keys,
+                                                  const uint64_t *__restrict__ el, int64_t ts_base,
+                                                  const uint64_t *__restrict__ param_in, int8_t *decision,
+                                                  int32_t *wait_ms) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    const Ctx c{st, max_rt};
+    const int lane = threadIdx.x;
+    const uint32_t nl = sc.counters[14];
+    for (uint32_t h = blockIdx.x; h < nl; h += gridDim.x) {
+        const uint32_t e0 = sc.plong[2 * h], e1 = e0 + sc.plong[2 * h + 1];
+        const uint64_t key = el[e0] >> 32;
+        const Payload q0 = pay[(uint32_t)el[e0]];
+        const uint32_t res = keys[(uint32_t)el[e0]];
+        const ParamRuleDev prule = st.prules[st.res[res].prule_off];
+        const uint64_t v = param_in[q0.idx & F_IDX];
+        const int a = (int)(q0.acq_prio & 0x7FFFFFFFu);
+        PEntry *const tp = st.ttab + key;
+        PEntry *const pp = ptab_get(st.ptab, st.pmask, prule.id + 1, v, false, st.overflow);
+        if (!pp) continue;  // overflow: the batch fails
+        PEntry pe = *pp;
+        const bool p0 = pe.a != kPAbsent;
+        int64_t npass = 0;
+        uint32_t last_pass = e1;
+        // decisions of [lo, hi) on all lanes
+        auto fill = [&](uint32_t lo, uint32_t hi, bool pass) {
+            const int8_t d = pass ? D_PASS : D_BLOCK_PARAM;
+            for (uint32_t e = lo + lane; e < hi; e += 4 * 64) {
+                uint32_t ix[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) ix[u] = (uint32_t)el[min(e + 64 * u, hi - 1)];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) ix[u] = pay[ix[u]].idx & F_IDX;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (e + 64 * u < hi) {
+                        decision[ix[u]] = d;
+                        wait_ms[ix[u]] = 0;
+                    }
+            }
+            if (pass && hi > lo) {
+                npass += hi - lo;
+                last_pass = hi - 1;
+            }
+        };
+        auto one = [&](uint32_t e, bool pass, int64_t w) {
+            if (lane == 0) {
+                const uint32_t ix = pay[(uint32_t)el[e]].idx & F_IDX;
+                decision[ix] = pass ? D_PASS : D_BLOCK_PARAM;
+                wait_ms[ix] = pass ? (int32_t)w : 0;
+            }
+            if (pass) {
+                ++npass;
+                last_pass = e;
+            }
+        };
+        const bool access = param_map_access(c, prule, v, a);
+        if (!access) {
+            fill(e0, e1, false);  // a zero threshold, or acquire > maxCount: every entry blocks, no map access
+        } else {
+            int64_t token_count = j_d2l(prule.count), hot;
+            if (hot_lookup(c, prule, v, &hot)) token_count = hot;
+            uint32_t e = e0;
+            if (prule.behavior == 2) {
+                const int64_t cost =
+                    j_round(1.0 * 1000 * (double)a * (double)prule.duration / (double)token_count);
+                const int64_t slack = prule.max_queue > 0 ? prule.max_queue - 1 : 0;
+                while (e < e1) {
+                    if (pe.a == kPAbsent) {
+                        pe.a = pseg_time(pay, el, ts_base, e);
+                        one(e++, true, 0);
+                        continue;
+                    }
+                    const int64_t expected = pe.a + cost;
+                    const uint32_t r = pseg_upper(pay, el, ts_base, e, e1, expected - slack - 1);
+                    fill(e, r, false);
+                    if (r >= e1) break;
+                    const int64_t tr = pseg_time(pay, el, ts_base, r);
+                    const int64_t w = expected - tr;
+                    pe.a = w > 0 ? expected : tr;
+                    one(r, true, w > 0 ? w : 0);
+                    e = r + 1;
+                }
+            } else {
+                const int64_t max_count = lwrap_add(token_count, prule.burst);
+                const int64_t dur_ms = lwrap_mul(prule.duration, 1000);
+                while (e < e1) {
+                    if (pe.a == kPAbsent) {
+                        pe.a = pseg_time(pay, el, ts_base, e);
+                        if (pe.b == kPAbsent) pe.b = max_count - a;
+                        one(e++, true, 0);
+                        continue;
+                    }
+                    const uint32_t r = pseg_upper(pay, el, ts_base, e, e1, pe.a + dur_ms);  // the next refill
+                    int64_t k = 0;
+                    if (pe.b != kPAbsent && pe.b >= 0) k = a > 0 ? min((int64_t)(r - e), pe.b / a) : (int64_t)(r - e);
+                    fill(e, e + (uint32_t)k, true);
+                    fill(e + (uint32_t)k, r, false);
+                    if (pe.b != kPAbsent) pe.b -= k * a;
+                    e = r;
+                    if (e >= e1) break;
+                    int64_t w = 0;  // the refill: one exact step
+                    const bool ok = param_pass_qps(c, prule, pe, v, a, pseg_time(pay, el, ts_base, e), &w);
+                    one(e++, ok, w);
+                }
+            }
+        }
+        if (lane == 0) {
+            pp->a = pe.a;
+            pp->b = pe.b;
+            if (access && st.pstamp) st.pstamp[pp - st.ptab] = lru_stamp(st, pay[(uint32_t)el[e1 - 1]].idx & F_IDX, 0);
+            const int d = (pe.a != kPAbsent ? 1 : 0) - (p0 ? 1 : 0);
+            if (d && st.psize) atomicAdd(&st.psize[prule.id], (uint32_t)d);
+            if (npass) {  // addThreadCount per pass
+                const int64_t ta0 = tp->a;
+                tp->a = (ta0 == kPAbsent ? 0 : ta0) + npass;
+                if (st.tstamp) st.tstamp[key] = lru_stamp(st, pay[(uint32_t)el[last_pass]].idx & F_IDX, 0);
+                if (ta0 == kPAbsent && lru_on_t(st, res)) atomicAdd(&st.tsize[st.tbase[res]], 1u);
+            }
+        }
+    }
+}
+
+// 4. each run's pass / block acquire sums and passes (the decisions are in), pre-reduced over a thread's
+//    consecutive events
+__global__ __launch_bounds__(kT) void k_pseg_runs(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
+                                                  const int8_t *__restrict__ decision) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0) || sc.counters[11] == 0) return;
+    const uint32_t nvalid = sc.counters[0];
+    const uint32_t e0 = (blockIdx.x * kT + threadIdx.x) * kItems;
+    uint32_t cur = 0xFFFFFFFFu, np = 0;
+    int64_t pa = 0, ba = 0;
+    auto flush = [&]() {
+        if (cur == 0xFFFFFFFFu) return;
+        if (pa) atomicAdd((unsigned long long *)&sc.run_pa[cur], (unsigned long long)pa);
+        if (ba) atomicAdd((unsigned long long *)&sc.run_ba[cur], (unsigned long long)ba);
+        if (np) atomicAdd(&sc.run_np[cur], np);
+    };
+    for (int i = 0; i < kItems && e0 + i < nvalid; ++i) {
+        const uint32_t e = e0 + i;
+        const uint32_t r = sc.ev_run[e];
+        if (sc.run_mode[r] != RUN_PSEG) continue;
+        const Payload q = pay[e];
+        if (q.idx & F_EXIT) continue;
+        if (r != cur) {
+            flush();
+            cur = r;
+            pa = ba = 0;
+            np = 0;
+        }
+        const int64_t a = (int64_t)(q.acq_prio & 0x7FFFFFFFu);
+        const int8_t d = decision[q.idx & F_IDX];
+        if (d == D_PASS || d == D_PASS_WAIT) {
+            pa += a;
+            ++np;
+        } else {
+            ba += a;
+        }
+    }
+    flush();
+}
+
+// 5. one lane per flow: StatisticSlot in aggregate, run by run in order -- every event of a run (one 500 ms
+//    bucket, nested in one minute bucket) sees the same window rotation, applied at the run's first event
+//    (a detached bucket takes none of the run's adds, as it would take none of its events')
+__global__ __launch_bounds__(kT) void k_pseg_apply(FlowState st, int64_t max_rt, FlowScratch sc, int64_t ts_base) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    const uint32_t nf = sc.counters[11], nflows = sc.counters[2], nruns = sc.counters[1];
+    for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < nf; i += gridDim.x * kT) {
+        const uint32_t fl = sc.pseg[i];
+        const uint32_t r0 = sc.flow_first_run[fl];
+        const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        int64_t *node = st.node + (size_t)sc.run_slot[r0] * kNodeWords;
+        int64_t thr = 0;
+        for (uint32_t r = r0; r < r1; ++r) {
+            const int64_t tf = ts_base + (int64_t)sc.run_t0off[r];
+            int64_t *bs[2] = {sec_current(node, tf, max_rt), min_current(node, tf, max_rt)};
+            const int64_t pa = sc.run_pa[r], ba = sc.run_ba[r];
+            const int64_t exc = (int64_t)sc.run_exc[r], exerr = (int64_t)sc.run_exerr[r];
+            const int64_t exrt = sc.run_exrt[r], exmin = sc.run_exmin[r];
+            for (int k = 0; k < 2; ++k) {
+                int64_t *b = bs[k];
+                if (!b) continue;
+                b[MB_PASS] += pa;
+                b[MB_BLOCK] += ba;
+                b[MB_SUCC] += exc;
+                b[MB_RT] += exrt;
+                b[MB_EXC] += exerr;
+                if (exmin < b[MB_MINRT]) b[MB_MINRT] = exmin;
+            }
+            thr += (int64_t)sc.run_np[r] - (int64_t)sc.run_nexit[r];
+            sc.run_mode[r] = RUN_DONE;
+        }
+        node[kNodeThreads] += thr;
+    }
+}
+
 // ---- CacheMap capacity: before each batch (flow.hpp LruRec)
 // 1. count pass: per owner in free mode, the distinct keys absent at the batch start that its events name
 //    (the keys it could insert).  Two launches: the first claims every such key's slot (lanes of one owner
@@ -3719,6 +4380,63 @@ int FlowEngine::ensure_maps(size_t m) {
     return 0;
 }
 
+// SGA_NO_PSEG=1 (A/B knob): parameter-only resources keep the event-by-event replay
+static bool pseg_on() {
+    static const bool off = getenv("SGA_NO_PSEG") && atoi(getenv("SGA_NO_PSEG")) == 1;
+    return !off;
+}
+
+void FlowEngine::launch_pseg(const FlowState &st, const FlowScratch &g, const Payload *pay, const uint32_t *keys,
+                             int64_t ts_base, const int64_t *rt, const uint64_t *param, int8_t *decision,
+                             int32_t *wait_ms, uint32_t m, hipStream_t s) {
+    if (!g.pseg || m == 0) return;
+    FlowScratch gs = g;
+    const uint64_t none = ((uint64_t)st.tmask + 1) << 32;  // after every map slot
+    int sbits = 1;
+    while ((1ull << sbits) <= (uint64_t)st.tmask + 1) ++sbits;
+    const uint32_t nb = std::min<uint32_t>((m + kT - 1) / kT, 2048);
+    if (!h_prules.empty()) {
+        hipLaunchKernelGGL(k_pseg_key<true>, dim3(nb), dim3(kT), 0, s, st, gs, pay, keys, param, m, none);
+        hipLaunchKernelGGL(k_pseg_key<false>, dim3(nb), dim3(kT), 0, s, st, gs, pay, keys, param, m, none);
+        // the slot bits sorted in pieces of at most 24 bits (3 radix passes each), least significant first
+        uint64_t *el = gs.pel[0], *alt = gs.pel[1];
+        const int pieces = (sbits + 23) / 24, pb = (sbits + pieces - 1) / pieces;
+        int np = 0;
+        for (int lo = 0; lo < sbits; lo += pb) {
+            np = radix_sort_u64(el, alt, m, 32 + lo, std::min(pb, sbits - lo), gs.radix, s, false);
+            if (np < 0) {  // never expected (at most 24 bits per call)
+                fprintf(stderr, "sentinel_amd: parameter segment sort of %d bits refused\n", sbits);
+                abort();
+            }
+            if (np & 1) std::swap(el, alt);
+        }
+        hipLaunchKernelGGL(k_pseg_heads, dim3(nb), dim3(kT), 0, s, st, gs, pay, el, m, none);
+        static const bool dbg = getenv("SGA_PSEG_DEBUG") && atoi(getenv("SGA_PSEG_DEBUG")) == 1;
+        if (dbg) {
+            uint32_t h[4] = {0, 0, 0, 0}, *dd = gs.radix.err;  // the radix error words are free here
+            SGA_HIP_CHECK(hipMemsetAsync(dd, 0, 16, s));
+            hipLaunchKernelGGL(k_pseg_check, dim3(nb), dim3(kT), 0, s, st, keys, el, m, none, dd);
+            SGA_HIP_CHECK(hipMemcpyAsync(h, dd, 16, hipMemcpyDeviceToHost, s));
+            uint32_t c[16];
+            SGA_HIP_CHECK(hipMemcpyAsync(c, gs.counters, 64, hipMemcpyDeviceToHost, s));
+            SGA_HIP_CHECK(hipStreamSynchronize(s));
+            fprintf(stderr, "pseg m=%u flows=%u segs=%u elements=%u unsorted=%u lru=%u wrong_owner=%u sbits=%d np=%d\n", m,
+                    c[11], c[12], h[1], h[0], h[2], h[3], sbits, np);
+        }
+        hipLaunchKernelGGL(k_pseg_solve, dim3(std::min<uint32_t>((m + kT - 1) / kT, 4096)), dim3(kT), 0, s, st,
+                           (int64_t)cfg.statistic_max_rt, gs, pay, keys, el, m, ts_base, param, decision, wait_ms);
+        hipLaunchKernelGGL(k_pseg_long, dim3(std::min<uint32_t>(m / kPsegLong + 1, 2048)), dim3(64), 0, s, st,
+                           (int64_t)cfg.statistic_max_rt, gs, pay, keys, el, ts_base, param, decision, wait_ms);
+    }
+    if (!h_cbs.empty())
+        hipLaunchKernelGGL(k_cb_flows, dim3(std::min<uint32_t>(std::max<uint32_t>(1, m / 64), 4096)), dim3(64), 0, s,
+                           st, gs, pay, ts_base, rt, decision, wait_ms);
+    hipLaunchKernelGGL(k_pseg_runs, dim3((m + kTileElems - 1) / kTileElems), dim3(kT), 0, s, st, gs, pay, decision);
+    const uint32_t fthreads = std::min<uint32_t>(m, nres);
+    hipLaunchKernelGGL(k_pseg_apply, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, s, st, (int64_t)cfg.statistic_max_rt,
+                       gs, ts_base);
+}
+
 // SGA_HEAVY_PROF=1: k_lheavy phase timers (1024 workgroups x 8 counters), printed by
 // FlowEngine::print_heavy_prof at engine release.  Diagnostics only.
 static uint64_t *g_heavy_prof = nullptr;
@@ -3782,7 +4500,8 @@ int FlowEngine::ensure_scratch() {
         const size_t ntiles = (cap + kTileElems - 1) / kTileElems + 1;
         size_t bytes = 2 * al(cap * 4) + 2 * al(cap * sizeof(Payload)) + 2 * al(cap * 4) + 11 * al(cap * 4) +
                        4 * al(cap * 8) + al(cap) + 3 * al(cap * 4) + 2 * al(ntiles * sizeof(LAgg)) + al(ntiles * 4) +
-                       al(64) + 2 * al(hist * 4) + al(scan_partials_needed(hist) * 4 + 64);
+                       al(64) + 2 * al(hist * 4) + al(scan_partials_needed(hist) * 4 + 64) + al(cap * 4) +
+                       2 * al(cap * 8) + al(cap * 4) + 2 * al(cap * 8) + al(cap * 4) + al(kRadixGhistWords * 4) + al(64) + al(cap * 4) + al((cap / 256 + 16) * 8);
         d_scratch.alloc(bytes);
         char *p = (char *)d_scratch.p;
         auto take = [&](size_t b) {
@@ -3822,6 +4541,17 @@ int FlowEngine::ensure_scratch() {
         sc.radix.hist = (uint32_t *)take(hist * 4);
         sc.radix.hist_scan = (uint32_t *)take(hist * 4);
         sc.radix.partial = (uint32_t *)take(scan_partials_needed(hist) * 4 + 64);
+        sc.pseg = (uint32_t *)take(cap * 4);
+        sc.cbf = (uint32_t *)take(cap * 4);
+        sc.plong = (uint32_t *)take((cap / 256 + 16) * 8);
+        sc.pel[0] = (uint64_t *)take(cap * 8);
+        sc.pel[1] = (uint64_t *)take(cap * 8);
+        sc.seg = (uint32_t *)take(cap * 4);
+        sc.run_pa = (int64_t *)take(cap * 8);
+        sc.run_ba = (int64_t *)take(cap * 8);
+        sc.run_np = (uint32_t *)take(cap * 4);
+        sc.radix.ghist = (uint32_t *)take(kRadixGhistWords * 4);
+        sc.radix.err = (uint32_t *)take(64);
         sc.cap = cap;
         scratch_cap = cap;
         d_kind.alloc(cap);
@@ -3948,8 +4678,11 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
                            (const LAgg *)sc.tile_carry, sc);
         hipLaunchKernelGGL(k_lexits, dim3(ntiles), dim3(kT), 0, stream, pay, d_rt.p, sc);
         const uint32_t fthreads = (uint32_t)std::min<size_t>(m, nres);
+        FlowScratch fsc = sc;
+        if ((h_prules.empty() && h_cbs.empty()) || !pseg_on()) fsc.pseg = nullptr;
         hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, stream, st,
-                           (int64_t)cfg.statistic_max_rt, sc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p);
+                           (int64_t)cfg.statistic_max_rt, fsc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p);
+        launch_pseg(st, fsc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p, (uint32_t)m, stream);
         if (st.lru_res)
             hipLaunchKernelGGL(k_llru, dim3(64), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo,
                                d_rt.p, d_param.p, d_dec.p, d_wait.p);
@@ -3972,10 +4705,44 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         SGA_HIP_CHECK(hipMemcpyAsync(&ovf, d_overflow.p, 4, hipMemcpyDeviceToHost, stream));
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
         if (ovf) return SGA_ENOMEM;  // parameter maps full
+        debug_size_check();
         b += m;
         seq += m;
     }
     return 0;
+}
+
+// SGA_SIZE_CHECK=1 (diagnostics only): after each host batch, every free-mode owner's kept present count
+// against a count of its present map keys
+void FlowEngine::debug_size_check() {
+    static const bool on = getenv("SGA_SIZE_CHECK") && atoi(getenv("SGA_SIZE_CHECK")) == 1;
+    if (!on || !d_psize.p) return;
+    const FlowState st = state();
+    std::vector<PEntry> pt(st.pmask + 1), tt(st.tmask + 1);
+    SGA_HIP_CHECK(hipMemcpy(pt.data(), d_ptab.p, pt.size() * sizeof(PEntry), hipMemcpyDeviceToHost));
+    SGA_HIP_CHECK(hipMemcpy(tt.data(), d_ttab.p, tt.size() * sizeof(PEntry), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> ps(st.nprid), ts(st.ntslot);
+    std::vector<uint64_t> pq(st.nprid), tq(st.ntslot);
+    SGA_HIP_CHECK(hipMemcpy(ps.data(), d_psize.p, ps.size() * 4, hipMemcpyDeviceToHost));
+    SGA_HIP_CHECK(hipMemcpy(ts.data(), d_tsize.p, ts.size() * 4, hipMemcpyDeviceToHost));
+    SGA_HIP_CHECK(hipMemcpy(pq.data(), d_pq.p, pq.size() * 8, hipMemcpyDeviceToHost));
+    SGA_HIP_CHECK(hipMemcpy(tq.data(), d_tq.p, tq.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> pc(st.nprid), tc(st.ntslot);
+    for (const PEntry &e : pt)
+        if (e.owner && e.a != kPAbsent && e.owner - 1 < st.nprid) ++pc[e.owner - 1];
+    for (const PEntry &e : tt) {
+        if (!e.owner || e.a == kPAbsent) continue;
+        const uint32_t r = (e.owner & 0xFFFFFFu) - 1u, k = e.owner >> 24;
+        if (r < h_tbase.size() && h_tbase[r] != kNoTBase) ++tc[h_tbase[r] + k];
+    }
+    int shown = 0;
+    for (uint32_t i = 0; i < st.nprid && shown < 12; ++i)
+        if (pq[i] == kNoQueue && pc[i] != ps[i] && ++shown)
+            fprintf(stderr, "size check seq=%llu: rule id %u size %u present %u\n", (unsigned long long)seq, i, ps[i], pc[i]);
+    for (uint32_t j = 0; j < st.ntslot && shown < 24; ++j)
+        if (tq[j] == kNoQueue && tc[j] != ts[j] && ++shown)
+            fprintf(stderr, "size check seq=%llu: thread slot %u size %u present %u\n", (unsigned long long)seq, j, ts[j], tc[j]);
+    if (!shown) fprintf(stderr, "size check seq=%llu: ok\n", (unsigned long long)seq);
 }
 
 // Device entry: one chunk of events already in HBM, launched on s without a host wait.  What the host
@@ -4033,8 +4800,10 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
                        gsc);
     hipLaunchKernelGGL(k_lexits, dim3(ntiles), dim3(kT), 0, s, pay, rt_p, gsc);
     const uint32_t fthreads = std::min<uint32_t>(m, nres);
+    if ((h_prules.empty() && h_cbs.empty()) || !pseg_on()) gsc.pseg = nullptr;
     hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc,
                        pay, keys, ts_base, rt_p, param_p, d_decision, wait_p);
+    launch_pseg(st, gsc, pay, keys, ts_base, rt_p, param_p, d_decision, wait_p, m, s);
     if (st.lru_res)
         hipLaunchKernelGGL(k_llru, dim3(64), dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p,
                            param_p, d_decision, wait_p);

@@ -173,6 +173,16 @@ struct FlowScratch {
     uint32_t *heavy;  // flows replayed by k_lheavy (count in counters[8])
     uint32_t *pace;   // long single-rule fast-path flows decided by k_lwave (count in counters[9])
     uint32_t *lru;    // flows of resources with a map in LRU mode, replayed by k_llru (count in counters[10])
+    // parameter-only resources decided per (rule, value) segment (flow.hip k_pseg_*): their flows (count in
+    // counters[11]), the events as (thread-count map slot << 32 | sorted position), sorted by slot, the
+    // segments' first elements (count in counters[12]), and each run's pass / block acquire sums and passes
+    uint32_t *pseg;
+    uint32_t *plong;  // long regular entry segments (first element, length; count in counters[14], k_pseg_long)
+    uint32_t *cbf;  // the breaker-only flows among them that move their breaker (count in counters[13], k_cb_flows)
+    uint64_t *pel[2];
+    uint32_t *seg;
+    int64_t *run_pa, *run_ba;
+    uint32_t *run_np;
     void *tile_agg, *tile_carry;
     uint32_t *tile_valid;
     uint32_t *counters;
@@ -208,6 +218,11 @@ struct FlowEngine {
     uint32_t ntbase = 0;            // resources given thread-map owner slots
     uint64_t seq = 0;               // events submitted so far (stamps)
     void lru_sync_rules();          // per-id / per-slot arrays after a parameter-rule load
+    // parameter-only resources per (rule, value) segment, after k_lflows took their flows (flow.hip k_pseg_*)
+    void launch_pseg(const FlowState &st, const FlowScratch &g, const Payload *pay, const uint32_t *keys,
+                     int64_t ts_base, const int64_t *rt, const uint64_t *param, int8_t *decision, int32_t *wait_ms,
+                     uint32_t m, hipStream_t s);
+    void debug_size_check();  // SGA_SIZE_CHECK=1 diagnostics
     void lru_prepare(const uint8_t *kind, const uint32_t *resource, const uint8_t *flags, const uint64_t *param,
                      const uint64_t *pvals, uint32_t n, hipStream_t s);  // count pass + switches, before a batch
     int lru_error(hipStream_t s);   // sticky queue errors (host wait)
