@@ -1421,8 +1421,7 @@ __global__ __launch_bounds__(kT) void k_lruns_down(const uint32_t *__restrict__ 
 __global__ __launch_bounds__(kT) void k_lexits(const Payload *__restrict__ pay, const int64_t *__restrict__ rt_in,
                                                FlowScratch sc) {
     const uint32_t nvalid = sc.counters[0];
-    const uint32_t e0 = (blockIdx.x * kT + threadIdx.x) * kItems;
-    if (e0 >= nvalid) return;
+    const uint32_t e0 = (blockIdx.x * kT + threadIdx.x) * kItems;  // no early return: the wave reduction below
     uint32_t cur = 0xFFFFFFFFu;
     uint64_t c = 0, er = 0;
     int64_t rs = 0, mn = INT64_MAX;
@@ -1451,6 +1450,15 @@ __global__ __launch_bounds__(kT) void k_lexits(const Payload *__restrict__ pay, 
         if (q.idx & F_ERROR) er += cnt;
         rs += rt;
         if (rt < mn) mn = rt;
+    }
+    // a long run covers whole waves: one set of atomics per wave
+    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur);
+    if (__all(cur == c0) && c0 != 0xFFFFFFFFu) {
+        c = (uint64_t)readlane_i64(wave_incl_sum_i64((int64_t)c), 63);
+        er = (uint64_t)readlane_i64(wave_incl_sum_i64((int64_t)er), 63);
+        rs = readlane_i64(wave_incl_sum_i64(rs), 63);
+        mn = readlane_i64(wave_incl_min_i64(mn), 63);
+        if ((threadIdx.x & 63) != 0) cur = 0xFFFFFFFFu;
     }
     flush();
 }
@@ -2849,12 +2857,21 @@ constexpr int64_t kSegExit = 1, kSegEntry = 2, kSegIrregular = 4;
 __global__ __launch_bounds__(kT) void k_pseg_heads(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
                                                    const uint64_t *__restrict__ el, uint32_t m, uint64_t none) {
     if (!gate_is(st.gate, kGateSeq | kGateBad, 0) || sc.counters[11] == 0) return;
-    for (uint32_t e = blockIdx.x * kT + threadIdx.x; e < m; e += gridDim.x * kT) {
-        const uint64_t x = el[e];
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t e0 = blockIdx.x * kT; e0 < m; e0 += gridDim.x * kT) {  // whole waves in every iteration
+        const uint32_t e = e0 + threadIdx.x;
+        const uint64_t x = e < m ? el[e] : none;
         const uint64_t k = x >> 32;
+        const bool head = k != none >> 32 && (e == 0 || (el[e - 1] >> 32) != k);
+        const uint64_t hb = __ballot(head);  // one counter atomic per wave
+        if (hb) {
+            const int first = __ffsll((unsigned long long)hb) - 1;
+            uint32_t base = 0;
+            if ((int)lane == first) base = atomicAdd(&sc.counters[12], (uint32_t)__popcll(hb));
+            base = (uint32_t)__shfl((int)base, first, 64);
+            if (head) sc.seg[base + (uint32_t)__popcll(hb & ((1ull << lane) - 1ull))] = e;
+        }
         if (k == none >> 32) continue;
-        const bool head = e == 0 || (el[e - 1] >> 32) != k;
-        if (head) sc.seg[atomicAdd(&sc.counters[12], 1u)] = e;
         const Payload q = pay[(uint32_t)x];
         int64_t f = (q.idx & F_EXIT) ? kSegExit : kSegEntry;
         if (!head && !(q.idx & F_EXIT)) {
@@ -3000,7 +3017,7 @@ __global__ __launch_bounds__(kT) void k_pseg_solve(FlowState st, int64_t max_rt,
 //     breaker opens at the first exit whose window counts trip it, and exits after that only count; a
 //     HALF_OPEN one is decided by its first exit, stepped alone; a window that goes back in time (a detached
 //     bucket) sends the rest of the flow to the step-by-step replay.
-constexpr int kCbI = 32;
+constexpr int kCbI = 16;
 struct CbAgg {
     int64_t ws, bad, tot;  // the last window's counts (ws == kCbNone: no exit)
 };
@@ -3070,19 +3087,33 @@ __global__ __launch_bounds__(64) void k_cb_flows(FlowState st, FlowScratch sc, c
                 int64_t wsv[kCbI];
                 uint32_t badm = 0, valm = 0;
                 const uint32_t j0 = base + (uint32_t)lane * kCbI;
+                // loads first, unconditional at clamped indices (a load under a branch is waited for there)
+                uint32_t tso[kCbI], fx[kCbI];
 #pragma unroll
                 for (int i = 0; i < kCbI; ++i) {
-                    const uint32_t j = j0 + i;
-                    wsv[i] = kCbNone;
-                    if (j < je) {
-                        const Payload q = pay[j];
-                        const int64_t t = ts_base + (int64_t)q.ts_off;
-                        wsv[i] = t - t % si;
-                        const bool bad = b.grade == 0 ? rt_in[q.idx & F_IDX] > b.max_allowed_rt : (q.idx & F_ERROR) != 0;
-                        badm |= (bad ? 1u : 0u) << i;
-                        valm |= 1u << i;
-                    }
+                    const Payload q = pay[min(j0 + i, je - 1)];
+                    tso[i] = q.ts_off;
+                    fx[i] = q.idx;
                 }
+                if (b.grade == 0) {
+                    int64_t rtv[kCbI];
+#pragma unroll
+                    for (int i = 0; i < kCbI; ++i) rtv[i] = rt_in[fx[i] & F_IDX];
+#pragma unroll
+                    for (int i = 0; i < kCbI; ++i) badm |= (rtv[i] > b.max_allowed_rt ? 1u : 0u) << i;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < kCbI; ++i) badm |= ((fx[i] & F_ERROR) ? 1u : 0u) << i;
+                }
+                int64_t cw = kCbNone;  // the window of the previous item: most items share it (no division)
+#pragma unroll
+                for (int i = 0; i < kCbI; ++i) {
+                    const int64_t t = ts_base + (int64_t)tso[i];
+                    if (cw == kCbNone || t < cw || t - cw >= si) cw = t - t % si;
+                    wsv[i] = j0 + i < je ? cw : kCbNone;
+                    valm |= (j0 + i < je ? 1u : 0u) << i;
+                }
+                badm &= valm;
                 // windows must not go back: inside the lane, across lanes, and against the carry
                 bool mono = true;
                 int64_t first = kCbNone, last = kCbNone;
@@ -3167,8 +3198,8 @@ __device__ uint32_t pseg_upper(const Payload *__restrict__ pay, const uint64_t *
         const uint32_t p = lo + (uint32_t)lane * step;
         const bool gt = p < hi && pseg_time(pay, el, ts_base, p) > x;
         const uint64_t b = __ballot(gt);
-        if (!b) {
-            lo = min(hi, lo + 63 * step + 1);  // every probe <= x: past the last one (lane 63's, or hi)
+        if (!b) {  // every probe <= x: the answer is past the last probe inside [lo, hi)
+            lo = lo + ((hi - lo - 1) / step) * step + 1;
             continue;
         }
         const int f = __ffsll((unsigned long long)b) - 1;
@@ -3338,6 +3369,14 @@ __global__ __launch_bounds__(kT) void k_pseg_runs(FlowState st, FlowScratch sc, 
         } else {
             ba += a;
         }
+    }
+    // a long run covers whole waves: one atomic per wave instead of one per lane
+    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur);
+    if (__all(cur == c0) && c0 != 0xFFFFFFFFu) {
+        pa = readlane_i64(wave_incl_sum_i64(pa), 63);
+        ba = readlane_i64(wave_incl_sum_i64(ba), 63);
+        np = (uint32_t)readlane_i64(wave_incl_sum_i64((int64_t)np), 63);
+        if ((threadIdx.x & 63) != 0) cur = 0xFFFFFFFFu;
     }
     flush();
 }
