@@ -1446,6 +1446,7 @@ __global__ __launch_bounds__(kT) void k_lexits(const Payload *__restrict__ pay, 
         }
         const uint64_t cnt = q.acq_prio & 0x7FFFFFFFu;
         const int64_t rt = rt_in[q.idx & F_IDX];
+        sc.rt_sorted[e] = rt;
         c += cnt;
         if (q.idx & F_ERROR) er += cnt;
         rs += rt;
@@ -3031,11 +3032,15 @@ __device__ __forceinline__ int64_t shfl_up_i64(int64_t v, int o) {
     const int lo = __shfl_up((int)(uint32_t)v, o, 64), hi = __shfl_up((int)(uint32_t)((uint64_t)v >> 32), o, 64);
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
-__global__ __launch_bounds__(64) void k_cb_flows(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
-                                                 int64_t ts_base, const int64_t *__restrict__ rt_in, int8_t *decision,
-                                                 int32_t *wait_ms) {
+constexpr int kCbW = 4;  // waves per flow: a round covers kCbW x 64 x kCbI exits
+__global__ __launch_bounds__(64 * kCbW) void k_cb_flows(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
+                                                        int64_t ts_base, const int64_t *__restrict__ rt_in,
+                                                        int8_t *decision, int32_t *wait_ms) {
     if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
-    const int lane = threadIdx.x;
+    __shared__ int64_t s_w[kCbW][5];  // per wave: total {ws, bad, tot}, first and last window
+    __shared__ uint32_t s_min, s_bad;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr uint32_t kRound = 64u * kCbW * kCbI, kWaveItems = 64u * kCbI;
     const uint32_t ncb = sc.counters[13], nflows = sc.counters[2], nruns = sc.counters[1];
     for (uint32_t h = blockIdx.x; h < ncb; h += gridDim.x) {
         const uint32_t fl = sc.cbf[h];
@@ -3044,25 +3049,27 @@ __global__ __launch_bounds__(64) void k_cb_flows(FlowState st, FlowScratch sc, c
         const uint32_t res = sc.run_slot[r0];
         const uint32_t jb = sc.run_start[r0], je = sc.run_end[r1 - 1];
         CbDev *gb = st.cbs + st.res[res].cb_off;
-        CbDev b = *gb;
+        CbDev b = *gb;  // every thread holds the same copy and takes the same steps
         if (!(pay[jb].idx & F_EXIT)) {  // entries only (the breaker is not CLOSED)
             uint32_t probe = je;
             if (b.state == 1) {
-                for (uint32_t base = jb; base < je && probe == je; base += 64 * kCbI) {
-                    uint32_t mine = je;
+                for (uint32_t base = jb; base < je && probe == je; base += kRound) {
+                    if (threadIdx.x == 0) s_min = je;
+                    __syncthreads();
                     for (int i = 0; i < kCbI; ++i) {
-                        const uint32_t j = base + (uint32_t)lane * kCbI + i;
+                        const uint32_t j = base + threadIdx.x * kCbI + i;
                         if (j < je && ts_base + (int64_t)pay[j].ts_off >= b.next_retry) {
-                            mine = j;
+                            atomicMin(&s_min, j);
                             break;
                         }
                     }
-                    const uint64_t has = __ballot(mine < je);
-                    if (has) probe = (uint32_t)__shfl((int)mine, __ffsll((unsigned long long)has) - 1, 64);
+                    __syncthreads();
+                    probe = s_min;
+                    __syncthreads();
                 }
                 if (probe < je) b.state = 2;  // fromOpenToHalfOpen: the probe passes
             }
-            for (uint32_t j = jb + lane; j < je; j += 64) {
+            for (uint32_t j = jb + threadIdx.x; j < je; j += 64 * kCbW) {
                 const uint32_t idx = pay[j].idx & F_IDX;
                 decision[idx] = j == probe ? D_PASS : D_BLOCK_DEGRADE;
                 wait_ms[idx] = 0;  // a block's detail: the breaker's index
@@ -3086,7 +3093,7 @@ __global__ __launch_bounds__(64) void k_cb_flows(FlowState st, FlowScratch sc, c
                 }
                 int64_t wsv[kCbI];
                 uint32_t badm = 0, valm = 0;
-                const uint32_t j0 = base + (uint32_t)lane * kCbI;
+                const uint32_t j0 = base + (uint32_t)wave * kWaveItems + (uint32_t)lane * kCbI;
                 // loads first, unconditional at clamped indices (a load under a branch is waited for there)
                 uint32_t tso[kCbI], fx[kCbI];
 #pragma unroll
@@ -3096,9 +3103,9 @@ __global__ __launch_bounds__(64) void k_cb_flows(FlowState st, FlowScratch sc, c
                     fx[i] = q.idx;
                 }
                 if (b.grade == 0) {
-                    int64_t rtv[kCbI];
+                    int64_t rtv[kCbI];  // in sorted order (k_lexits): contiguous, not a gather
 #pragma unroll
-                    for (int i = 0; i < kCbI; ++i) rtv[i] = rt_in[fx[i] & F_IDX];
+                    for (int i = 0; i < kCbI; ++i) rtv[i] = sc.rt_sorted[min(j0 + i, je - 1)];
 #pragma unroll
                     for (int i = 0; i < kCbI; ++i) badm |= (rtv[i] > b.max_allowed_rt ? 1u : 0u) << i;
                 } else {
@@ -3114,8 +3121,7 @@ __global__ __launch_bounds__(64) void k_cb_flows(FlowState st, FlowScratch sc, c
                     valm |= (j0 + i < je ? 1u : 0u) << i;
                 }
                 badm &= valm;
-                // windows must not go back: inside the lane, across lanes, and against the carry
-                bool mono = true;
+                bool mono = true;  // inside the lane
                 int64_t first = kCbNone, last = kCbNone;
 #pragma unroll
                 for (int i = 0; i < kCbI; ++i) {
@@ -3124,57 +3130,90 @@ __global__ __launch_bounds__(64) void k_cb_flows(FlowState st, FlowScratch sc, c
                     else if (wsv[i] < last) mono = false;
                     last = wsv[i];
                 }
-                const int64_t prev_last = wave_incl_max_i64(last == kCbNone ? INT64_MIN : last);
-                const int64_t before = shfl_up_i64(prev_last, 1);
-                const int64_t lim = lane == 0 ? (carry.ws == kCbNone ? INT64_MIN : carry.ws)
-                                              : max(before, carry.ws == kCbNone ? INT64_MIN : carry.ws);
-                if (first != kCbNone && first < lim) mono = false;
-                if (!__all(mono)) {
-                    seq = true;
-                    break;
-                }
                 CbAgg agg{kCbNone, 0, 0};
 #pragma unroll
                 for (int i = 0; i < kCbI; ++i)
                     if ((valm >> i) & 1u) agg = cb_combine(agg, CbAgg{wsv[i], (int64_t)((badm >> i) & 1u), 1});
-                // exclusive scan of the lane aggregates (Hillis-Steele on shuffles), the carry in front
-                CbAgg inc = agg;
-                for (int o = 1; o < 64; o <<= 1) {
-                    CbAgg y{shfl_up_i64(inc.ws, o), shfl_up_i64(inc.bad, o), shfl_up_i64(inc.tot, o)};
-                    if (lane >= o) inc = cb_combine(y, inc);
+                // the lanes' tail-window counts as one DPP segmented scan: a lane starts a segment when its
+                // tail window starts inside it or differs from the windows before it (windows only grow, so
+                // the window of everything up to a lane is the prefix maximum)
+                const int64_t prev_last = wave_incl_max_i64(last == kCbNone ? INT64_MIN : last);
+                const int64_t before = wave_shr1_i64(prev_last, INT64_MIN);  // windows of the lanes before
+                const bool has = agg.ws != kCbNone;
+                int hd = (has && (first != agg.ws || (before != INT64_MIN && before != agg.ws))) ? 1 : 0;
+                int sb = (int)agg.bad, stt = (int)agg.tot;
+                wave_incl_segsum2(sb, stt, hd);
+                const int64_t iws = prev_last == INT64_MIN ? kCbNone : prev_last;  // window of lanes <= this one
+                // the waves' totals, first and last windows: each wave's carry is the round's carry and the
+                // totals of the waves before it
+                {
+                    const int64_t fmin = wave_incl_min_i64(first == kCbNone ? INT64_MAX : first);
+                    if (lane == 63) {
+                        s_w[wave][0] = iws;
+                        s_w[wave][1] = sb;
+                        s_w[wave][2] = stt;
+                        s_w[wave][3] = fmin;  // first window of the wave (INT64_MAX: none)
+                        s_w[wave][4] = prev_last;
+                    }
+                    if (threadIdx.x == 0) s_bad = 0;
                 }
-                CbAgg ex{shfl_up_i64(inc.ws, 1), shfl_up_i64(inc.bad, 1), shfl_up_i64(inc.tot, 1)};
-                if (lane == 0) ex = CbAgg{kCbNone, 0, 0};
-                CbAgg run = cb_combine(carry, ex);
-                uint32_t trip = je;
+                __syncthreads();
+                CbAgg cwv = carry;
+                int64_t wlim = carry.ws == kCbNone ? INT64_MIN : carry.ws;
+                for (int w = 0; w < wave; ++w) {
+                    cwv = cb_combine(cwv, CbAgg{s_w[w][0], s_w[w][1], s_w[w][2]});
+                    wlim = max(wlim, s_w[w][4]);
+                }
+                // windows must not go back: across lanes, across waves and against the carry
+                const int64_t lim = max(before, wlim);
+                if (first != kCbNone && first < lim) mono = false;
+                if (!mono) s_bad = 1;
+                CbAgg total = carry;
+                for (int w = 0; w < kCbW; ++w) total = cb_combine(total, CbAgg{s_w[w][0], s_w[w][1], s_w[w][2]});
+                __syncthreads();
+                if (s_bad) {
+                    seq = true;
+                    break;
+                }
+                CbAgg inc{iws, sb, stt};
+                if (!hd && iws != kCbNone && iws == cwv.ws) {
+                    inc.bad += cwv.bad;
+                    inc.tot += cwv.tot;
+                }
+                if (iws == kCbNone) inc = cwv;  // nothing up to this lane: the carry alone
+                CbAgg run{wave_shr1_i64(inc.ws, cwv.ws), wave_shr1_i64(inc.bad, cwv.bad), wave_shr1_i64(inc.tot, cwv.tot)};
+                if (threadIdx.x == 0) s_min = je;
+                __syncthreads();
                 if (b.state == 0) {
+                    uint32_t trip = je;
 #pragma unroll
                     for (int i = 0; i < kCbI; ++i) {
                         if (!((valm >> i) & 1u)) continue;
                         run = cb_combine(run, CbAgg{wsv[i], (int64_t)((badm >> i) & 1u), 1});
                         if (trip == je && cb_trips(b, run.bad, run.tot)) trip = j0 + i;
                     }
+                    if (trip < je) atomicMin(&s_min, trip);
                 }
-                const uint64_t tb = __ballot(trip < je);
-                if (tb) {  // the first exit that trips a CLOSED breaker opens it (cb_to_open)
-                    const uint32_t k = (uint32_t)__shfl((int)trip, __ffsll((unsigned long long)tb) - 1, 64);
-                    cb_to_open(b, ts_base + (int64_t)pay[k].ts_off);
-                }
-                const CbAgg all = cb_combine(carry, cb_combine(ex, agg));
-                carry = CbAgg{readlane_i64(all.ws, 63), readlane_i64(all.bad, 63), readlane_i64(all.tot, 63)};
-                base += 64 * kCbI;
+                __syncthreads();
+                const uint32_t k = s_min;
+                if (k < je) cb_to_open(b, ts_base + (int64_t)pay[k].ts_off);  // the first exit that trips it
+                carry = total;
+                base += kRound;
+                __syncthreads();
             }
             b.st_start = carry.ws == kCbNone ? kAbsent : carry.ws;
             b.st_bad = carry.bad;
             b.st_total = carry.tot;
-            if (seq)  // step by step (every lane the same steps)
+            if (seq)  // step by step (every thread the same steps)
                 for (uint32_t j = base; j < je; ++j) {
                     const Payload q = pay[j];
                     const int64_t t = ts_base + (int64_t)q.ts_off;
                     cb_on_complete_ws(b, t, t - t % si, rt_in[q.idx & F_IDX], (q.idx & F_ERROR) != 0);
                 }
         }
-        if (lane == 0) *gb = b;
+        __syncthreads();
+        if (threadIdx.x == 0) *gb = b;
+        __syncthreads();
     }
 }
 
@@ -4468,7 +4507,7 @@ void FlowEngine::launch_pseg(const FlowState &st, const FlowScratch &g, const Pa
                            (int64_t)cfg.statistic_max_rt, gs, pay, keys, el, ts_base, param, decision, wait_ms);
     }
     if (!h_cbs.empty())
-        hipLaunchKernelGGL(k_cb_flows, dim3(std::min<uint32_t>(std::max<uint32_t>(1, m / 64), 4096)), dim3(64), 0, s,
+        hipLaunchKernelGGL(k_cb_flows, dim3(std::min<uint32_t>(std::max<uint32_t>(1, m / 64), 4096)), dim3(64 * kCbW), 0, s,
                            st, gs, pay, ts_base, rt, decision, wait_ms);
     hipLaunchKernelGGL(k_pseg_runs, dim3((m + kTileElems - 1) / kTileElems), dim3(kT), 0, s, st, gs, pay, decision);
     const uint32_t fthreads = std::min<uint32_t>(m, nres);
@@ -4540,7 +4579,7 @@ int FlowEngine::ensure_scratch() {
         size_t bytes = 2 * al(cap * 4) + 2 * al(cap * sizeof(Payload)) + 2 * al(cap * 4) + 11 * al(cap * 4) +
                        4 * al(cap * 8) + al(cap) + 3 * al(cap * 4) + 2 * al(ntiles * sizeof(LAgg)) + al(ntiles * 4) +
                        al(64) + 2 * al(hist * 4) + al(scan_partials_needed(hist) * 4 + 64) + al(cap * 4) +
-                       2 * al(cap * 8) + al(cap * 4) + 2 * al(cap * 8) + al(cap * 4) + al(kRadixGhistWords * 4) + al(64) + al(cap * 4) + al((cap / 256 + 16) * 8);
+                       2 * al(cap * 8) + al(cap * 4) + 2 * al(cap * 8) + al(cap * 4) + al(kRadixGhistWords * 4) + al(64) + al(cap * 4) + al((cap / 256 + 16) * 8) + al(cap * 8);
         d_scratch.alloc(bytes);
         char *p = (char *)d_scratch.p;
         auto take = [&](size_t b) {
@@ -4583,6 +4622,7 @@ int FlowEngine::ensure_scratch() {
         sc.pseg = (uint32_t *)take(cap * 4);
         sc.cbf = (uint32_t *)take(cap * 4);
         sc.plong = (uint32_t *)take((cap / 256 + 16) * 8);
+        sc.rt_sorted = (int64_t *)take(cap * 8);
         sc.pel[0] = (uint64_t *)take(cap * 8);
         sc.pel[1] = (uint64_t *)take(cap * 8);
         sc.seg = (uint32_t *)take(cap * 4);

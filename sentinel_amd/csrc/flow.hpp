@@ -178,7 +178,8 @@ struct FlowScratch {
     // segments' first elements (count in counters[12]), and each run's pass / block acquire sums and passes
     uint32_t *pseg;
     uint32_t *plong;  // long regular entry segments (first element, length; count in counters[14], k_pseg_long)
-    uint32_t *cbf;  // the breaker-only flows among them that move their breaker (count in counters[13], k_cb_flows)
+    uint32_t *cbf;
+    int64_t *rt_sorted;  // each exit's response time at its sorted position (k_lexits; k_cb_flows reads it in order)  // the breaker-only flows among them that move their breaker (count in counters[13], k_cb_flows)
     uint64_t *pel[2];
     uint32_t *seg;
     int64_t *run_pa, *run_ba;
