@@ -3032,7 +3032,7 @@ __device__ __forceinline__ int64_t shfl_up_i64(int64_t v, int o) {
     const int lo = __shfl_up((int)(uint32_t)v, o, 64), hi = __shfl_up((int)(uint32_t)((uint64_t)v >> 32), o, 64);
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
-constexpr int kCbW = 4;  // waves per flow: a round covers kCbW x 64 x kCbI exits
+constexpr int kCbW = 8;  // waves per flow: a round covers kCbW x 64 x kCbI exits
 __global__ __launch_bounds__(64 * kCbW) void k_cb_flows(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
                                                         int64_t ts_base, const int64_t *__restrict__ rt_in,
                                                         int8_t *decision, int32_t *wait_ms) {
