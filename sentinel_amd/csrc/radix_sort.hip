@@ -985,7 +985,7 @@ int radix_sort_pairs(uint32_t *keys, Payload *pay, uint32_t *keys_alt, Payload *
 
 int radix64_digit_bits(int bits) {
     if (bits <= 0) return 1;
-    const int mb = max_digit_bits() > 10 ? 10 : max_digit_bits();
+    const int mb = max_digit_bits();  // 8 by default; SGA_RADIX_BITS up to 11 (two passes for 21-bit keys)
     const int npass = (bits + mb - 1) / mb;
     return (bits + npass - 1) / npass;
 }
@@ -1074,7 +1074,8 @@ int radix_sort_u64(uint64_t *a, uint64_t *alt, size_t n, int key_shift, int bits
     case 7: return sort64_passes<7>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
     case 8: return sort64_passes<8>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
     case 9: return sort64_passes<9>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
-    default: return sort64_passes<10>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    case 10: return sort64_passes<10>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
+    default: return sort64_passes<11>(a, alt, nn, key_shift, npass, sc, s, hist0_ready);
     }
 }
 
@@ -1100,7 +1101,8 @@ int radix_sort_u64_tiled(const uint64_t *src, const uint32_t *tile_n0, const uin
     case 7: return sort64_passes<7>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
     case 8: return sort64_passes<8>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
     case 9: return sort64_passes<9>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
-    default: return sort64_passes<10>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
+    case 10: return sort64_passes<10>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
+    default: return sort64_passes<11>(a, alt, nn, key_shift, npass, sc, s, hist0_ready, src, tile_n0, dn);
     }
 }
 

@@ -64,7 +64,7 @@ def alg_bytes(k, bl):
     n_cold = lp.get("n_cold", n)
     t_hot = min(lp.get("n_hot_next", 0), touched)
     b = base(k)
-    if b == "k_hot_key_dense" and k.endswith("<0>"):
+    if b == "k_hot_key_dense" and re.search(r"<0\s*[,>]", k):  # pass 0 (k_hot_key_dense<0> or <0, true>)
         return n * 12.0
     if b == "k_cold_fused":
         return n_cold * 8.0 + (touched - t_hot) * 2 * 704.0
