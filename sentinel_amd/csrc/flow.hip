@@ -324,6 +324,14 @@ __device__ __forceinline__ uint32_t ptab_home(uint32_t mask, uint32_t owner, uin
     return (uint32_t)splitmix64(value ^ ((uint64_t)owner << 40) ^ 0xA5A5ULL) & mask;
 }
 
+// Claimed-slot counters: kClaimHdr entries in front of each table's slot 0 (never probed), their `a` words
+// counting every slot claim (64 shards against same-address contention).  The host reads them to bound the
+// table's load without scanning it (FlowEngine::grow_map).
+constexpr uint32_t kClaimHdr = 64;
+__device__ __forceinline__ void claim_note(PEntry *tab, uint32_t h) {
+    atomicAdd(reinterpret_cast<unsigned long long *>(&tab[-1 - (int)(h & (kClaimHdr - 1))].a), 1ull);
+}
+
 __device__ PEntry *ptab_get(PEntry *tab, uint32_t mask, uint32_t owner, uint64_t value, bool create,
                             uint32_t *overflow) {
     uint32_t h = (uint32_t)splitmix64(value ^ ((uint64_t)owner << 40) ^ 0xA5A5ULL) & mask;
@@ -337,6 +345,7 @@ __device__ PEntry *ptab_get(PEntry *tab, uint32_t mask, uint32_t owner, uint64_t
             if (!create) return nullptr;
             const uint32_t prev = atomicCAS(&e->owner, 0u, owner);  // the claim publishes the owner
             if (prev == 0) {
+                claim_note(tab, h);
                 e->value = value;
                 e->a = kPAbsent;
                 e->b = kPAbsent;
@@ -361,6 +370,7 @@ __device__ PEntry *ptab_insert_absent(PEntry *tab, uint32_t mask, uint32_t owner
         PEntry *e = &tab[h];
         if (__hip_atomic_load(&e->owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
             atomicCAS(&e->owner, 0u, owner) == 0u) {
+            claim_note(tab, h);
             e->value = value;
             e->a = kPAbsent;
             e->b = kPAbsent;
@@ -2324,6 +2334,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                         if (lgi[h] == kGiNone) {
                             PEntry *e;
                             if (pc[u] == 0u) {  // claimed the home slot (the CAS publishes the owner)
+                                claim_note(st.ptab, ptab_home(st.pmask, pown, v));
                                 e = &st.ptab[ptab_home(st.pmask, pown, v)];
                                 e->value = v;
                                 e->a = kPAbsent;
@@ -2337,6 +2348,7 @@ __global__ __launch_bounds__(64) void k_lheavy(FlowState st, int64_t max_rt, Flo
                         if (pt && tgi[h] == kGiNone) {
                             PEntry *te;
                             if (tc[u] == 0u) {
+                                claim_note(st.ttab, ptab_home(st.tmask, town, v));
                                 te = &st.ttab[ptab_home(st.tmask, town, v)];
                                 te->value = v;
                                 te->a = kPAbsent;
@@ -2915,6 +2927,8 @@ __global__ __launch_bounds__(kT) void k_pseg_solve(FlowState st, int64_t max_rt,
         uint64_t pst = 0, tst = 0;  // the last access stamps
         bool more = true;
         const int64_t flags = tp->b;
+        tp->b = kPAbsent;  // the flag word back to the thread-count entry's unused value (a present-key count
+                           // and a rehash test a != absent || b != absent)
         if (flags == kSegExit || flags == kSegEntry) {
             // the segment's end: galloping search on the keys
             uint32_t lo = e0 + 1, step = 1, hi = e0 + 1;
@@ -3322,6 +3336,13 @@ __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, 
                         pe.a = pseg_time(pay, el, ts_base, e);
                         one(e++, true, 0);
                         continue;
+                    }
+                    if (cost == 0 && pseg_time(pay, el, ts_base, e) >= pe.a) {
+                        // a zero cost (token count above 2000 x acquire x duration): with times
+                        // non-decreasing every entry from here passes without a wait, the last one's time kept
+                        fill(e, e1, true);
+                        pe.a = pseg_time(pay, el, ts_base, e1 - 1);
+                        break;
                     }
                     const int64_t expected = pe.a + cost;
                     const uint32_t r = pseg_upper(pay, el, ts_base, e, e1, expected - slack - 1);
@@ -3816,6 +3837,7 @@ __global__ void k_rehash(const PEntry *__restrict__ old, const uint64_t *__restr
     uint32_t h = (uint32_t)splitmix64(e.value ^ ((uint64_t)e.owner << 40) ^ 0xA5A5ULL) & nmask;
     for (uint32_t probe = 0; probe <= nmask; ++probe) {
         if (atomicCAS(&nt[h].owner, 0u, e.owner) == 0u) {
+            claim_note(nt, h);
             nt[h].value = e.value;
             nt[h].a = e.a;
             nt[h].b = e.b;
@@ -3830,6 +3852,10 @@ __global__ void k_rehash(const PEntry *__restrict__ old, const uint64_t *__restr
 }  // namespace
 
 // ======================================================================== host side
+// a parameter map's slots start after its claim counters
+static PEntry *tab_data(const DevBuf<PEntry> &d) { return d.p ? d.p + kClaimHdr : nullptr; }
+static size_t tab_slots(const DevBuf<PEntry> &d) { return d.n > kClaimHdr ? d.n - kClaimHdr : 0; }
+
 FlowState FlowEngine::state() const {
     FlowState s{};
     s.node = d_node.p;
@@ -3839,10 +3865,10 @@ FlowState FlowEngine::state() const {
     s.hot_t = d_hot_t.p;
     s.cbs = d_cbs.p;
     s.res = d_res.p;
-    s.ptab = d_ptab.p;
-    s.ttab = d_ttab.p;
-    s.pmask = d_ptab.n ? (uint32_t)(d_ptab.n - 1) : 0;
-    s.tmask = d_ttab.n ? (uint32_t)(d_ttab.n - 1) : 0;
+    s.ptab = tab_data(d_ptab);
+    s.ttab = tab_data(d_ttab);
+    s.pmask = tab_slots(d_ptab) ? (uint32_t)(tab_slots(d_ptab) - 1) : 0;
+    s.tmask = tab_slots(d_ttab) ? (uint32_t)(tab_slots(d_ttab) - 1) : 0;
     s.nres = nres;
     s.overflow = d_overflow.p;
     s.cst = cluster_st;
@@ -3951,10 +3977,10 @@ void FlowEngine::lru_sync_rules() {
         SGA_HIP_CHECK(hipMemsetAsync(d_lru_res.p, 0, std::max<size_t>(nres, 1), stream));
     }
     if (!d_pstamp.p) {
-        d_pstamp.alloc(d_ptab.n);
-        d_tstamp.alloc(d_ttab.n);
-        SGA_HIP_CHECK(hipMemsetAsync(d_pstamp.p, 0, d_ptab.n * 8, stream));
-        SGA_HIP_CHECK(hipMemsetAsync(d_tstamp.p, 0, d_ttab.n * 8, stream));
+        d_pstamp.alloc(tab_slots(d_ptab));
+        d_tstamp.alloc(tab_slots(d_ttab));
+        SGA_HIP_CHECK(hipMemsetAsync(d_pstamp.p, 0, tab_slots(d_ptab) * 8, stream));
+        SGA_HIP_CHECK(hipMemsetAsync(d_tstamp.p, 0, tab_slots(d_ttab) * 8, stream));
     }
     // the pool: what is in use plus every current owner switching once (queue areas are not reused)
     unsigned long long used = 0;
@@ -4061,10 +4087,13 @@ int FlowEngine::set_resources(uint32_t n) {
     size_t pc = 1;
     while (pc < (size_t)cfg.max_batch * 2) pc <<= 1;
     pc = std::max<size_t>(pc, 1 << 16);
-    d_ptab.alloc(pc);
-    d_ttab.alloc(pc);
-    hipLaunchKernelGGL(k_clear_ptab, dim3((unsigned)((pc + kT - 1) / kT)), dim3(kT), 0, stream, d_ptab.p, (uint32_t)pc);
-    hipLaunchKernelGGL(k_clear_ptab, dim3((unsigned)((pc + kT - 1) / kT)), dim3(kT), 0, stream, d_ttab.p, (uint32_t)pc);
+    d_ptab.alloc(pc + kClaimHdr);
+    d_ttab.alloc(pc + kClaimHdr);
+    for (DevBuf<PEntry> *t : {&d_ptab, &d_ttab}) {
+        SGA_HIP_CHECK(hipMemsetAsync(t->p, 0, kClaimHdr * sizeof(PEntry), stream));  // claim counters
+        hipLaunchKernelGGL(k_clear_ptab, dim3((unsigned)((pc + kT - 1) / kT)), dim3(kT), 0, stream, tab_data(*t),
+                           (uint32_t)pc);
+    }
     upload_res();
     SGA_HIP_CHECK(hipStreamSynchronize(stream));
     return 0;
@@ -4317,9 +4346,9 @@ int FlowEngine::load_param_rules(const sga_param_rule *rules, size_t n) {
         DevBuf<uint64_t> dc;
         dc.alloc(nres);
         SGA_HIP_CHECK(hipMemcpyAsync(dc.p, clear.data(), (size_t)nres * 8, hipMemcpyHostToDevice, stream));
-        const uint32_t tn = (uint32_t)d_ttab.n;
+        const uint32_t tn = (uint32_t)tab_slots(d_ttab);
         const uint32_t m = std::max(tn, nres);
-        hipLaunchKernelGGL(k_tmap_clear, dim3((m + kT - 1) / kT), dim3(kT), 0, stream, d_ttab.p, tn, dc.p, nres,
+        hipLaunchKernelGGL(k_tmap_clear, dim3((m + kT - 1) / kT), dim3(kT), 0, stream, tab_data(d_ttab), tn, dc.p, nres,
                            d_tmapmask.p, d_tbase.p, d_tsize.p, d_tq.p);
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
     }
@@ -4400,31 +4429,42 @@ int FlowEngine::load_degrade_rules(const sga_degrade_rule *rules, size_t n) {
 
 static size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
+
 void FlowEngine::grow_map(DevBuf<PEntry> &tab, DevBuf<uint64_t> &stamp, size_t &ub, size_t add) {
-    if (ub + add <= tab.n / 4) {
+    const size_t n = tab_slots(tab);
+    if (ub + add <= n / 4) {
         ub += add;
         return;
     }
-    if (!d_keycount.p || d_keycount.n < 2) d_keycount.alloc(2);
-    SGA_HIP_CHECK(hipMemsetAsync(d_keycount.p, 0, 8, stream));
-    hipLaunchKernelGGL(k_count_keys, dim3((unsigned)std::min<size_t>((tab.n + kT - 1) / kT, 2048)), dim3(kT), 0, stream,
-                       tab.p, (uint32_t)tab.n, d_keycount.p);
-    uint32_t keys[2] = {0, 0};  // claimed slots, present keys
-    SGA_HIP_CHECK(hipMemcpyAsync(keys, d_keycount.p, 8, hipMemcpyDeviceToHost, stream));
+    // the exact count of claimed slots: the table's claim counters (a 2 KB read, not a table scan)
+    PEntry hdr[kClaimHdr];
+    SGA_HIP_CHECK(hipMemcpyAsync(hdr, tab.p, sizeof(hdr), hipMemcpyDeviceToHost, stream));
     SGA_HIP_CHECK(hipStreamSynchronize(stream));
-    ub = keys[0];
-    if (ub + add > tab.n / 4) {
+    uint64_t claimed = 0;
+    for (const PEntry &h : hdr) claimed += (uint64_t)h.a;
+    ub = claimed;
+    if (ub + add > n / 4) {
         // rehash the present keys (claimed slots of absent keys -- evicted or removed ones -- are dropped)
-        // into a table that stays at most a quarter full after this batch
-        size_t nn = tab.n;
-        while (keys[1] + add > nn / 4) nn <<= 1;
+        // into a table that stays at most a quarter full for two batches like this one (so the next batch
+        // needs no counter read either)
+        if (!d_keycount.p || d_keycount.n < 2) d_keycount.alloc(2);
+        SGA_HIP_CHECK(hipMemsetAsync(d_keycount.p, 0, 8, stream));
+        hipLaunchKernelGGL(k_count_keys, dim3((unsigned)std::min<size_t>((n + kT - 1) / kT, 2048)), dim3(kT), 0,
+                           stream, tab_data(tab), (uint32_t)n, d_keycount.p);
+        uint32_t keys[2] = {0, 0};  // claimed slots, present keys
+        SGA_HIP_CHECK(hipMemcpyAsync(keys, d_keycount.p, 8, hipMemcpyDeviceToHost, stream));
+        SGA_HIP_CHECK(hipStreamSynchronize(stream));
+        size_t nn = n;
+        while (keys[1] + 2 * add > nn / 4) nn <<= 1;
         DevBuf<PEntry> nt;
-        nt.alloc(nn);
+        nt.alloc(nn + kClaimHdr);
         DevBuf<uint64_t> ns;
         if (stamp.p) ns.alloc(nn);
-        hipLaunchKernelGGL(k_clear_ptab, dim3((unsigned)((nn + kT - 1) / kT)), dim3(kT), 0, stream, nt.p, (uint32_t)nn);
-        hipLaunchKernelGGL(k_rehash, dim3((unsigned)((tab.n + kT - 1) / kT)), dim3(kT), 0, stream, tab.p, stamp.p,
-                           (uint32_t)tab.n, nt.p, ns.p, (uint32_t)(nn - 1), d_overflow.p);
+        SGA_HIP_CHECK(hipMemsetAsync(nt.p, 0, kClaimHdr * sizeof(PEntry), stream));
+        hipLaunchKernelGGL(k_clear_ptab, dim3((unsigned)((nn + kT - 1) / kT)), dim3(kT), 0, stream, tab_data(nt),
+                           (uint32_t)nn);
+        hipLaunchKernelGGL(k_rehash, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, stream, tab_data(tab), stamp.p,
+                           (uint32_t)n, tab_data(nt), ns.p, (uint32_t)(nn - 1), d_overflow.p);
         ub = keys[1];
         uint32_t ovf = 0;
         SGA_HIP_CHECK(hipMemcpyAsync(&ovf, d_overflow.p, 4, hipMemcpyDeviceToHost, stream));
@@ -4474,7 +4514,9 @@ void FlowEngine::launch_pseg(const FlowState &st, const FlowScratch &g, const Pa
     while ((1ull << sbits) <= (uint64_t)st.tmask + 1) ++sbits;
     const uint32_t nb = std::min<uint32_t>((m + kT - 1) / kT, 2048);
     if (!h_prules.empty()) {
-        hipLaunchKernelGGL(k_pseg_key<true>, dim3(nb), dim3(kT), 0, s, st, gs, pay, keys, param, m, none);
+        // the count pass (lru_prepare, whenever parameter rules are loaded) has claimed every key these events
+        // name in free-mode maps already; the claim launch is for an engine without it
+        if (!d_psize.p) hipLaunchKernelGGL(k_pseg_key<true>, dim3(nb), dim3(kT), 0, s, st, gs, pay, keys, param, m, none);
         hipLaunchKernelGGL(k_pseg_key<false>, dim3(nb), dim3(kT), 0, s, st, gs, pay, keys, param, m, none);
         // the slot bits sorted in pieces of at most 24 bits (3 radix passes each), least significant first
         uint64_t *el = gs.pel[0], *alt = gs.pel[1];
@@ -4798,8 +4840,8 @@ void FlowEngine::debug_size_check() {
     if (!on || !d_psize.p) return;
     const FlowState st = state();
     std::vector<PEntry> pt(st.pmask + 1), tt(st.tmask + 1);
-    SGA_HIP_CHECK(hipMemcpy(pt.data(), d_ptab.p, pt.size() * sizeof(PEntry), hipMemcpyDeviceToHost));
-    SGA_HIP_CHECK(hipMemcpy(tt.data(), d_ttab.p, tt.size() * sizeof(PEntry), hipMemcpyDeviceToHost));
+    SGA_HIP_CHECK(hipMemcpy(pt.data(), tab_data(d_ptab), pt.size() * sizeof(PEntry), hipMemcpyDeviceToHost));
+    SGA_HIP_CHECK(hipMemcpy(tt.data(), tab_data(d_ttab), tt.size() * sizeof(PEntry), hipMemcpyDeviceToHost));
     std::vector<uint32_t> ps(st.nprid), ts(st.ntslot);
     std::vector<uint64_t> pq(st.nprid), tq(st.ntslot);
     SGA_HIP_CHECK(hipMemcpy(ps.data(), d_psize.p, ps.size() * 4, hipMemcpyDeviceToHost));
