@@ -1836,12 +1836,13 @@ constexpr int kWavePf = 8;  // k_lwave: windows loaded ahead
 __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, FlowScratch sc,
                                               const Payload *__restrict__ pay, int64_t ts_base,
                                               const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in,
-                                              int8_t *decision, int32_t *wait_ms, uint64_t *prof) {
+                                              int8_t *decision, int32_t *wait_ms, uint64_t *prof, int pace_mode) {
     if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
     const Ctx c{st, max_rt};
     const int lane = threadIdx.x;
     const uint32_t nwave = sc.counters[9], nflows = sc.counters[2], nruns = sc.counters[1];
     uint64_t pr_iter = 0, pr_lr = 0, pr_lrt = 0;  // profiling (SGA_LWAVE_PROF=1)
+    const bool pace_scan = pace_mode == 0;
     for (uint32_t h = blockIdx.x; h < nwave; h += gridDim.x) {
         const uint32_t fl = sc.pace[h];
         const uint32_t r0 = sc.flow_first_run[fl];
@@ -1925,7 +1926,46 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                 int8_t d = D_PASS;
                 int64_t w = 0;
                 uint64_t rem = __ballot(ent);
-                if (pace) {
+                if (pace && pace_scan) {
+                    // RateLimiterController (RateLimiterController.java:46-91) as a state map per entry:
+                    // an entry of cost c at time t passes iff latest <= t + maxQueueing - c, and then
+                    // latest' = max(latest + c, t) (a blocked entry leaves it).  A zero-cost entry (the
+                    // acquire-1 entries of a rule above 1000 QPS) is latest' = max(latest, t) either way,
+                    // so the zero-cost entries of the window are one prefix max; only the entries with a
+                    // cost step the state, in lane order, as scalar work, and every zero-cost entry reads
+                    // the state before it from the prefix max of the cost entries' results.
+                    const bool mv = ent && aq > 0 && rcount > 0;
+                    const bool zero = mv && cost == 0;
+                    const int64_t mz = wave_incl_max_i64(zero ? t : INT64_MIN);  // zero-cost times up to lane
+                    const int64_t mzx = wave_shr1_i64(mz, INT64_MIN);              // ... before lane
+                    uint64_t costly = __ballot(mv && cost > 0);
+                    int64_t L = latest, lp = INT64_MIN;  // lp: latest after this lane's step (cost lanes)
+                    while (costly) {
+                        const int k = __builtin_ctzll(costly);
+                        costly &= costly - 1;
+                        const int64_t tk = readlane_i64(t, k), ck = readlane_i64(cost, k);
+                        const int64_t Lb = max(L, readlane_i64(mzx, k));
+                        const bool ok = Lb + ck <= tk || Lb + ck - tk <= rqueue;
+                        L = ok ? max(Lb + ck, tk) : Lb;
+                        if (lane == k) {
+                            d = ok ? D_PASS : D_BLOCK_FLOW;
+                            w = ok ? L - tk : 0;
+                            lp = L;
+                        }
+                    }
+                    // the state after the last cost entry before each lane (a scan on every lane: DPP reads
+                    // of inactive lanes would return the bound value)
+                    const int64_t lpx = wave_shr1_i64(wave_incl_max_i64(lp), INT64_MIN);
+                    if (zero) {
+                        const int64_t Lb = max(max(latest, lpx), mzx);
+                        d = (Lb <= t || Lb - t <= rqueue) ? D_PASS : D_BLOCK_FLOW;
+                        w = (d == D_PASS && Lb > t) ? Lb - t : 0;
+                    }
+                    if (ent && aq > 0 && rcount <= 0) d = D_BLOCK_FLOW;
+                    latest = max(L, readlane_i64(mz, 63));
+                    rem = 0;
+                }
+                if (pace && !pace_scan) {
                     // RateLimiterController (RateLimiterController.java:46-91) by speculation: every open
                     // entry gets a predicted decision (acquireCount <= 0: pass; count <= 0: block;
                     // cost 0: pass; otherwise the last decision of a costly entry), latestPassedTime
@@ -4498,6 +4538,12 @@ int FlowEngine::ensure_maps(size_t m) {
     return 0;
 }
 
+// k_lwave's RateLimiter windows: 1 by speculation (round 2), 0 by the cost-entry scan (SGA_PACE_SCAN=1)
+static int pace_mode() {
+    static const int v = (getenv("SGA_PACE_SCAN") && atoi(getenv("SGA_PACE_SCAN")) == 1) ? 0 : 1;
+    return v;
+}
+
 // SGA_NO_PSEG=1 (A/B knob): parameter-only resources keep the event-by-event replay
 static bool pseg_on() {
     static const bool off = getenv("SGA_NO_PSEG") && atoi(getenv("SGA_NO_PSEG")) == 1;
@@ -4809,7 +4855,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
                                d_rt.p, d_param.p, d_dec.p, d_wait.p);
         hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
-                           d_dec.p, d_wait.p, lwave_prof());
+                           d_dec.p, d_wait.p, lwave_prof(), pace_mode());
         print_lwave_prof(stream);
         hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
@@ -4930,7 +4976,7 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
                            param_p, d_decision, wait_p);
     hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
                        st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
-                       lwave_prof());
+                       lwave_prof(), pace_mode());
     print_lwave_prof(s);
     hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
                        st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
