@@ -4495,7 +4495,8 @@ void FlowEngine::grow_map(DevBuf<PEntry> &tab, DevBuf<uint64_t> &stamp, size_t &
         SGA_HIP_CHECK(hipMemcpyAsync(keys, d_keycount.p, 8, hipMemcpyDeviceToHost, stream));
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
         size_t nn = n;
-        while (keys[1] + 2 * add > nn / 4) nn <<= 1;
+        const size_t room = (keys[1] + 2 * add) * 4 <= ((size_t)1 << 31) ? 2 * add : add;  // 32-bit slot indices
+        while (keys[1] + room > nn / 4) nn <<= 1;
         DevBuf<PEntry> nt;
         nt.alloc(nn + kClaimHdr);
         DevBuf<uint64_t> ns;
