@@ -1836,13 +1836,12 @@ constexpr int kWavePf = 8;  // k_lwave: windows loaded ahead
 __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, FlowScratch sc,
                                               const Payload *__restrict__ pay, int64_t ts_base,
                                               const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in,
-                                              int8_t *decision, int32_t *wait_ms, uint64_t *prof, int pace_mode) {
+                                              int8_t *decision, int32_t *wait_ms, uint64_t *prof) {
     if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
     const Ctx c{st, max_rt};
     const int lane = threadIdx.x;
     const uint32_t nwave = sc.counters[9], nflows = sc.counters[2], nruns = sc.counters[1];
     uint64_t pr_iter = 0, pr_lr = 0, pr_lrt = 0;  // profiling (SGA_LWAVE_PROF=1)
-    const bool pace_scan = pace_mode == 0;
     for (uint32_t h = blockIdx.x; h < nwave; h += gridDim.x) {
         const uint32_t fl = sc.pace[h];
         const uint32_t r0 = sc.flow_first_run[fl];
@@ -1926,46 +1925,7 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                 int8_t d = D_PASS;
                 int64_t w = 0;
                 uint64_t rem = __ballot(ent);
-                if (pace && pace_scan) {
-                    // RateLimiterController (RateLimiterController.java:46-91) as a state map per entry:
-                    // an entry of cost c at time t passes iff latest <= t + maxQueueing - c, and then
-                    // latest' = max(latest + c, t) (a blocked entry leaves it).  A zero-cost entry (the
-                    // acquire-1 entries of a rule above 1000 QPS) is latest' = max(latest, t) either way,
-                    // so the zero-cost entries of the window are one prefix max; only the entries with a
-                    // cost step the state, in lane order, as scalar work, and every zero-cost entry reads
-                    // the state before it from the prefix max of the cost entries' results.
-                    const bool mv = ent && aq > 0 && rcount > 0;
-                    const bool zero = mv && cost == 0;
-                    const int64_t mz = wave_incl_max_i64(zero ? t : INT64_MIN);  // zero-cost times up to lane
-                    const int64_t mzx = wave_shr1_i64(mz, INT64_MIN);              // ... before lane
-                    uint64_t costly = __ballot(mv && cost > 0);
-                    int64_t L = latest, lp = INT64_MIN;  // lp: latest after this lane's step (cost lanes)
-                    while (costly) {
-                        const int k = __builtin_ctzll(costly);
-                        costly &= costly - 1;
-                        const int64_t tk = readlane_i64(t, k), ck = readlane_i64(cost, k);
-                        const int64_t Lb = max(L, readlane_i64(mzx, k));
-                        const bool ok = Lb + ck <= tk || Lb + ck - tk <= rqueue;
-                        L = ok ? max(Lb + ck, tk) : Lb;
-                        if (lane == k) {
-                            d = ok ? D_PASS : D_BLOCK_FLOW;
-                            w = ok ? L - tk : 0;
-                            lp = L;
-                        }
-                    }
-                    // the state after the last cost entry before each lane (a scan on every lane: DPP reads
-                    // of inactive lanes would return the bound value)
-                    const int64_t lpx = wave_shr1_i64(wave_incl_max_i64(lp), INT64_MIN);
-                    if (zero) {
-                        const int64_t Lb = max(max(latest, lpx), mzx);
-                        d = (Lb <= t || Lb - t <= rqueue) ? D_PASS : D_BLOCK_FLOW;
-                        w = (d == D_PASS && Lb > t) ? Lb - t : 0;
-                    }
-                    if (ent && aq > 0 && rcount <= 0) d = D_BLOCK_FLOW;
-                    latest = max(L, readlane_i64(mz, 63));
-                    rem = 0;
-                }
-                if (pace && !pace_scan) {
+                if (pace) {
                     // RateLimiterController (RateLimiterController.java:46-91) by speculation: every open
                     // entry gets a predicted decision (acquireCount <= 0: pass; count <= 0: block;
                     // cost 0: pass; otherwise the last decision of a costly entry), latestPassedTime
@@ -2877,6 +2837,11 @@ __global__ __launch_bounds__(kT) void k_pseg_key(FlowState st, FlowScratch sc, c
                     if (!kClaim && te) {
                         el = ((uint64_t)(te - st.ttab) << 32) | j;
                         if (te->b != 0) te->b = 0;  // the segment's flag word for this batch (k_pseg_heads)
+                    } else if (!kClaim) {
+                        // every parameter event of a RUN_PSEG flow had its thread-count entry claimed (by the
+                        // claim launch, or by k_lru_count in LRU mode); a missing one would leave the event
+                        // undecided, so the batch fails as a map overflow does
+                        atomicOr(st.overflow, 1u);
                     }
                 }
             }
@@ -3835,15 +3800,20 @@ __global__ void k_clear_ptab(PEntry *t, uint32_t n) {
     if (i < n) t[i] = PEntry{0, 0, 0, kPAbsent, kPAbsent};
 }
 
-// slots claimed by a map and keys present in it (one atomic pair per workgroup)
-__device__ __forceinline__ bool pentry_present(const PEntry &e) { return e.a != kPAbsent || e.b != kPAbsent; }
-__global__ void k_count_keys(const PEntry *__restrict__ t, uint32_t n, uint32_t *__restrict__ out) {
+// slots claimed by a map and keys present in it (one atomic pair per workgroup).  A rule map's entry is
+// {time, tokens}; a thread-count entry (tt) keeps its count in a, and b is the per-segment flag word
+// k_pseg_heads ORs into it, which may be left off kPAbsent when a batch stops at a gate check, so only a
+// counts there.
+__device__ __forceinline__ bool pentry_present(const PEntry &e, bool tt) {
+    return e.a != kPAbsent || (!tt && e.b != kPAbsent);
+}
+__global__ void k_count_keys(const PEntry *__restrict__ t, uint32_t n, uint32_t *__restrict__ out, int tt) {
     __shared__ uint32_t ws[2][kT / 64];
     uint32_t c = 0, p = 0;
     for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
         const PEntry e = t[i];
         c += e.owner != 0 ? 1u : 0u;
-        p += (e.owner != 0 && pentry_present(e)) ? 1u : 0u;
+        p += (e.owner != 0 && pentry_present(e, tt)) ? 1u : 0u;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -3869,18 +3839,19 @@ __global__ void k_count_keys(const PEntry *__restrict__ t, uint32_t n, uint32_t 
 // every present key of `old` (with its stamp) into the empty table `nt` (same hash as ptab_get; entries
 // keep their counters); claimed slots of absent keys are dropped
 __global__ void k_rehash(const PEntry *__restrict__ old, const uint64_t *__restrict__ ostamp, uint32_t oldn,
-                         PEntry *__restrict__ nt, uint64_t *__restrict__ nstamp, uint32_t nmask, uint32_t *overflow) {
+                         PEntry *__restrict__ nt, uint64_t *__restrict__ nstamp, uint32_t nmask, uint32_t *overflow,
+                         int tt) {
     const uint32_t i = blockIdx.x * kT + threadIdx.x;
     if (i >= oldn) return;
     const PEntry e = old[i];
-    if (e.owner == 0 || !pentry_present(e)) return;
+    if (e.owner == 0 || !pentry_present(e, tt)) return;
     uint32_t h = (uint32_t)splitmix64(e.value ^ ((uint64_t)e.owner << 40) ^ 0xA5A5ULL) & nmask;
     for (uint32_t probe = 0; probe <= nmask; ++probe) {
         if (atomicCAS(&nt[h].owner, 0u, e.owner) == 0u) {
             claim_note(nt, h);
             nt[h].value = e.value;
             nt[h].a = e.a;
-            nt[h].b = e.b;
+            nt[h].b = tt ? kPAbsent : e.b;
             if (nstamp) nstamp[h] = ostamp ? ostamp[i] : 0;
             return;
         }
@@ -4471,6 +4442,7 @@ static size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
 
 void FlowEngine::grow_map(DevBuf<PEntry> &tab, DevBuf<uint64_t> &stamp, size_t &ub, size_t add) {
+    const bool tt = &tab == &d_ttab;  // the thread-count table
     const size_t n = tab_slots(tab);
     if (ub + add <= n / 4) {
         ub += add;
@@ -4490,7 +4462,7 @@ void FlowEngine::grow_map(DevBuf<PEntry> &tab, DevBuf<uint64_t> &stamp, size_t &
         if (!d_keycount.p || d_keycount.n < 2) d_keycount.alloc(2);
         SGA_HIP_CHECK(hipMemsetAsync(d_keycount.p, 0, 8, stream));
         hipLaunchKernelGGL(k_count_keys, dim3((unsigned)std::min<size_t>((n + kT - 1) / kT, 2048)), dim3(kT), 0,
-                           stream, tab_data(tab), (uint32_t)n, d_keycount.p);
+                           stream, tab_data(tab), (uint32_t)n, d_keycount.p, tt ? 1 : 0);
         uint32_t keys[2] = {0, 0};  // claimed slots, present keys
         SGA_HIP_CHECK(hipMemcpyAsync(keys, d_keycount.p, 8, hipMemcpyDeviceToHost, stream));
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
@@ -4505,7 +4477,7 @@ void FlowEngine::grow_map(DevBuf<PEntry> &tab, DevBuf<uint64_t> &stamp, size_t &
         hipLaunchKernelGGL(k_clear_ptab, dim3((unsigned)((nn + kT - 1) / kT)), dim3(kT), 0, stream, tab_data(nt),
                            (uint32_t)nn);
         hipLaunchKernelGGL(k_rehash, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, stream, tab_data(tab), stamp.p,
-                           (uint32_t)n, tab_data(nt), ns.p, (uint32_t)(nn - 1), d_overflow.p);
+                           (uint32_t)n, tab_data(nt), ns.p, (uint32_t)(nn - 1), d_overflow.p, tt ? 1 : 0);
         ub = keys[1];
         uint32_t ovf = 0;
         SGA_HIP_CHECK(hipMemcpyAsync(&ovf, d_overflow.p, 4, hipMemcpyDeviceToHost, stream));
@@ -4525,24 +4497,20 @@ void FlowEngine::grow_map(DevBuf<PEntry> &tab, DevBuf<uint64_t> &stamp, size_t &
     ub += add;
 }
 
-// Before a batch of m events the maps get room for every key the batch could add (m per parameter rule of
-// a resource for the rule maps, m for thread counts); CacheMap capacity bounds the present keys, and a
-// rehash drops the claimed slots of evicted / removed ones.
+// Before a batch of m events the maps get room for every key the batch could add: m per parameter rule of
+// a resource for the rule maps, and m per argument index with a rule for the thread counts (one event claims
+// a thread-count entry for each of its resource's rule indices, tmap_owner(r, k); the rule count bounds the
+// distinct indices).  CacheMap capacity bounds the present keys, and a rehash drops the claimed slots of
+// evicted / removed ones.
 int FlowEngine::ensure_maps(size_t m) {
     uint32_t mpr = 0;
     for (const ResDev &r : h_res) mpr = std::max<uint32_t>(mpr, r.n_prules);
     if (!mpr) return 0;
     const size_t limit = (size_t)1 << 31;  // 32-bit map indices
-    if ((pkeys_ub + m * mpr) * 4 > limit || (tkeys_ub + m) * 4 > limit) return SGA_ENOMEM;
+    if ((pkeys_ub + m * mpr) * 4 > limit || (tkeys_ub + m * mpr) * 4 > limit) return SGA_ENOMEM;
     grow_map(d_ptab, d_pstamp, pkeys_ub, m * mpr);
-    grow_map(d_ttab, d_tstamp, tkeys_ub, m);
+    grow_map(d_ttab, d_tstamp, tkeys_ub, m * mpr);
     return 0;
-}
-
-// k_lwave's RateLimiter windows: 1 by speculation (round 2), 0 by the cost-entry scan (SGA_PACE_SCAN=1)
-static int pace_mode() {
-    static const int v = (getenv("SGA_PACE_SCAN") && atoi(getenv("SGA_PACE_SCAN")) == 1) ? 0 : 1;
-    return v;
 }
 
 // SGA_NO_PSEG=1 (A/B knob): parameter-only resources keep the event-by-event replay
@@ -4856,7 +4824,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
                                d_rt.p, d_param.p, d_dec.p, d_wait.p);
         hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
-                           d_dec.p, d_wait.p, lwave_prof(), pace_mode());
+                           d_dec.p, d_wait.p, lwave_prof());
         print_lwave_prof(stream);
         hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
@@ -4977,7 +4945,7 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
                            param_p, d_decision, wait_p);
     hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
                        st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
-                       lwave_prof(), pace_mode());
+                       lwave_prof());
     print_lwave_prof(s);
     hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
                        st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,

@@ -100,7 +100,10 @@ def main():
         for line in open(a.steps_from):
             if line.startswith("{"):
                 d = json.loads(line)
-                sets = d["steps"] + d["warmup"]
+                # every batch the bench ran through the engine: warmup + timed steps, plus the host-buffer
+                # (end-to-end) batches that follow the timed loop unless the bench ran with --no-e2e
+                e2e = d.get("end_to_end_host_buffers") or {}
+                sets = d["steps"] + d["warmup"] + int(e2e.get("batches", 0))
                 bline = d
     rand_factor = 1.0
     if a.cal and os.path.exists(a.cal):
