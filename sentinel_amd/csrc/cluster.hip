@@ -524,23 +524,29 @@ struct RunIn {
     uint32_t bd;  // bucket delta of the run (its bucket = ts_base / W + bd)
 };
 
-// A rule's record between its runs (cold flows): the (start, PASS) pairs and the occupy state as
-// the lane's last run left them, so the rule's later runs issue no record loads (one memory round
-// trip per rule instead of one per run).  have = false: load from the record.
+// A rule's record between its runs (cold flows): the record header as the lane's last run left it
+// -- the (start, PASS) pairs, the occupy state, the cached counter group with its tag and the
+// threshold -- so the rule's later runs issue no record loads (one memory round trip per rule
+// instead of one per run).  have = false: load from the record.
 template <int kMaxPairs>
 struct RecCarry {
     int4 sp[kMaxPairs > 0 ? kMaxPairs : 1];
     int4 o0, o1;
+    int4 cg[3];  // cached group: (WAITING, BLOCK), (PASS_REQUEST, BLOCK_REQUEST), (OCCUPIED_PASS, OCCUPIED_BLOCK)
+    int4 meta;   // (tag, threshold)
     bool have;
 };
 
+__device__ __forceinline__ double f64_hi(const int4 &v) { return __longlong_as_double(i64_hi(v)); }
+
 // prio_before(k): prioritized requests among the run's first k (asked only when some prioritized
 // request is past the passing prefix).  kMaxPairs = 0: sampleCount above the register form, the
-// pairs are loaded one by one every run.
+// pairs are loaded one by one every run.  hdr_thr: the threshold is the record's copy (Rec::thr),
+// not thr_in (which the caller then did not load).
 template <class PrioBefore, int kMaxPairs>
-__device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam &P, const Rec &R, double thr,
-                                         int64_t qbase, const RunIn &ri, PrioBefore prio_before, RunOut &ro,
-                                         RecCarry<kMaxPairs> &rc) {
+__device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam &P, const Rec &R, double thr_in,
+                                         bool hdr_thr, int64_t qbase, const RunIn &ri, PrioBefore prio_before,
+                                         RunOut &ro, RecCarry<kMaxPairs> &rc) {
     // Cluster rules have intervalInMs = sampleCount x windowLengthInMs (checkClusterField), so every
     // validity test below (isWindowDeprecated, getValidHead) gives the same answer for any time in
     // the run's bucket: the bucket start stands in for the first request's time.
@@ -551,29 +557,27 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
     const int64_t qs = div_pos(q, P.S);
     const int cj = (int)(q - qs * P.S);
     const int jh = cj + 1 == P.S ? 0 : cj + 1;  // LeapArray.getValidHead index ((t0 + W) / W) % S
-    // First run of a rule: the record's loads are issued before any is used (one memory latency,
-    // not one per dependent step): the current bucket's six other counters (WAITING, BLOCK,
-    // PASS_REQUEST, BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK), the occupy state (in the lines of
-    // the pairs) and the (start, PASS) pair of every bucket, at clamped indices (a load under a
-    // branch is waited for before the branch closes, which would serialise them).  Later runs take
-    // the pairs and the occupy state from registers.
+    // First run of a rule: the header's loads are issued before any is used (one memory latency, not
+    // one per dependent step), at clamped indices (a load under a branch is waited for before the
+    // branch closes, which would serialise them): the (start, PASS) pair of every bucket, the occupy
+    // state, the cached counter group and (tag, threshold) -- for S = 10 exactly the header's two
+    // 128-byte lines.  Later runs take them from registers.
     const int4 *v = reinterpret_cast<const int4 *>(R.r);
-    const int4 *cv = reinterpret_cast<const int4 *>(R.r + 2 * P.S + kOccWords + 6 * cj);
-    int4 c01 = make_int4(0, 0, 0, 0), c23 = c01, c45 = c01;
-    bool cnt_loaded = false;
+    const int4 *hv = reinterpret_cast<const int4 *>(R.cache());
     if (!rc.have) {
-        c01 = cv[0];
-        c23 = cv[1];
-        c45 = cv[2];
-        cnt_loaded = true;
         const int4 *ov = reinterpret_cast<const int4 *>(&R.occ());
         rc.o0 = ov[0];
         rc.o1 = ov[1];
+        rc.cg[0] = hv[0];
+        rc.cg[1] = hv[1];
+        rc.cg[2] = hv[2];
+        rc.meta = hv[3];
         if constexpr (kMaxPairs > 0) {
 #pragma unroll
             for (int jj = 0; jj < kMaxPairs; ++jj) rc.sp[jj] = v[min(jj, P.S - 1)];
         }
     }
+    const double thr = hdr_thr ? f64_hi(rc.meta) : thr_in;
     SlotOcc occ_ld;
     occ_ld.occ_pass = i64_lo(rc.o0);
     occ_ld.occ_preq = i64_hi(rc.o0);
@@ -607,7 +611,9 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
     if (a <= 0 || (old != kAbsent && ws < old)) return false;
     if (ri.cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) return false;
     const bool rot = old == kAbsent || ws > old;
-    if (!rot && !cnt_loaded) {  // a later run in a bucket the record already holds (rare)
+    int4 c01 = rc.cg[0], c23 = rc.cg[1], c45 = rc.cg[2];
+    if (!rot && i64_lo(rc.meta) != old) {  // the current bucket's counters are not the cached group: the array
+        const int4 *cv = reinterpret_cast<const int4 *>(R.group(cj));
         c01 = cv[0];
         c23 = cv[1];
         c45 = cv[2];
@@ -656,10 +662,24 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
         // WAITING over the same valid buckets (only runs with prioritized blocked requests read it;
         // validity is re-tested per bucket, so any sampleCount works)
         int64_t w0 = c[CEV_WAITING];
+        if constexpr (kMaxPairs > 0) {
+            // the S WAITING counters loaded together at clamped indices (one memory latency; a load per
+            // bucket behind its validity test waited S latencies, and about every wave has a lane here),
+            // validity from the pairs in registers
+            int64_t wv[kMaxPairs];
+#pragma unroll
+            for (int jj = 0; jj < kMaxPairs; ++jj) wv[jj] = R.group(min(jj, P.S - 1))[0];
+#pragma unroll
+            for (int jj = 0; jj < kMaxPairs; ++jj) {
+                const int64_t w = i64_lo(rc.sp[jj]);
+                if (jj < P.S && jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) w0 += wv[jj];
+            }
+        } else {
 #pragma nounroll
-        for (int jj = 0; jj < P.S; ++jj) {
-            const int64_t w = R.start(jj);
-            if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) w0 += R.cnt(CEV_WAITING, jj);
+            for (int jj = 0; jj < P.S; ++jj) {
+                const int64_t w = R.start(jj);
+                if (jj != cj && w != kAbsent && !(t0 - w > (int64_t)P.interval)) w0 += R.cnt(CEV_WAITING, jj);
+            }
         }
         if (!occ_loaded) o = occ_ld;
         const double latest = (double)(s0 + (int64_t)f * a) / P.isec;
@@ -699,10 +719,20 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
                              (int)(uint32_t)((uint64_t)hi >> 32));
         };
         reinterpret_cast<int4 *>(R.r)[cj] = i4(stv, c[CEV_PASS]);
-        int4 *cg = reinterpret_cast<int4 *>(R.r + 2 * P.S + kOccWords + 6 * cj);
-        cg[0] = i4(c[CEV_WAITING], c[CEV_BLOCK]);
-        cg[1] = i4(c[CEV_PASS_REQUEST], c[CEV_BLOCK_REQUEST]);
-        cg[2] = i4(c[CEV_OCCUPIED_PASS], c[CEV_OCCUPIED_BLOCK]);
+        rc.cg[0] = i4(c[CEV_WAITING], c[CEV_BLOCK]);
+        rc.cg[1] = i4(c[CEV_PASS_REQUEST], c[CEV_BLOCK_REQUEST]);
+        rc.cg[2] = i4(c[CEV_OCCUPIED_PASS], c[CEV_OCCUPIED_BLOCK]);
+        rc.meta.x = (int)(uint32_t)stv;  // the cache now holds bucket cj (the threshold word is stored back as loaded)
+        rc.meta.y = (int)(uint32_t)((uint64_t)stv >> 32);
+        int4 *cg = reinterpret_cast<int4 *>(R.group(cj));  // the array (authoritative) and the header's cache
+        int4 *ch = reinterpret_cast<int4 *>(R.cache());
+        cg[0] = rc.cg[0];
+        cg[1] = rc.cg[1];
+        cg[2] = rc.cg[2];
+        ch[0] = rc.cg[0];
+        ch[1] = rc.cg[1];
+        ch[2] = rc.cg[2];
+        ch[3] = rc.meta;
         if (occ_dirty) {
             rc.o0 = i4(o.occ_pass, o.occ_preq);
             rc.o1 = make_int4(o.has_occ, o.pad, rc.o1.z, rc.o1.w);  // the spare word stored back unchanged
@@ -911,26 +941,157 @@ __device__ __forceinline__ FAgg fagg_block_excl(const FAgg &v, FAgg *total, FAgg
     return fagg_combine(pre, ex);
 }
 
-enum : int { kFzAll = 0 };
+// Bin mode's ordering (the cold partition): the workgroup's bin [B0, B1) of the partition output, in
+// arrival order, sorted stably by the slot bits below the bin (lb <= kPartMaxLow) into es[B0, B1).
+// Each wave takes a contiguous quarter; pass 1 counts its digits (ballot match: lanes with equal
+// digits, the lowest adds the group), the counts become absolute bases (digit starts + earlier
+// waves), pass 2 ranks every element (base + earlier lanes of its digit) and stores it.
+__device__ __forceinline__ uint64_t match_lanes(uint32_t d, int bits, bool valid) {
+    uint64_t peers = __ballot(valid);
+    for (int b = 0; b < bits; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        peers &= bit ? bb : ~bb;
+    }
+    return peers;
+}
+constexpr int kBinLds = 3072;  // k_cold_fused bin mode: bins of at most this many elements are ordered in LDS
+constexpr int kBoRounds = 12;  // bin_order: rounds of 64 elements a wave holds in registers (bins of ~3k in one go)
+// The ordered bin goes to es[pos - ebase] (es: the workgroup's LDS image of a bin that fits, ebase = B0, or
+// the global element buffer, ebase = 0).
+__device__ void bin_order(const uint64_t *__restrict__ in, uint64_t *es, uint32_t ebase, uint32_t B0, uint32_t B1,
+                          int lb, uint32_t *pc, uint32_t *wsum) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int kW = kFzThreads / 64;
+    const uint32_t nd = 1u << lb, dm = nd - 1u;
+    const uint64_t lt = lanemask_lt64(lane);
+    for (uint32_t k = threadIdx.x; k < kW * nd; k += kFzThreads) pc[k] = 0;
+    const uint32_t nb = B1 - B0;
+    const uint32_t q = (((nb + kW - 1) / kW) + 63u) & ~63u;
+    const uint32_t w0 = min(B1, B0 + (uint32_t)wave * q), w1 = min(B1, w0 + q);
+    uint32_t *mine = pc + (uint32_t)wave * nd;
+    // the wave's elements, kBoRounds rounds at a time, all loads in flight together (unconditional, at
+    // clamped positions); a wave of a bin that fits keeps them for pass 2
+    uint64_t x[kBoRounds];
+    auto load = [&](uint32_t c0) {
+#pragma unroll
+        for (int r = 0; r < kBoRounds; ++r) {
+            const uint32_t p = c0 + (uint32_t)r * 64 + lane;
+            x[r] = in[p < w1 ? p : (w0 < w1 ? w0 : B0)];
+        }
+    };
+    const bool one = w1 - w0 <= (uint32_t)(kBoRounds * 64);
+    __syncthreads();
+    for (uint32_t c0 = w0; c0 < w1; c0 += kBoRounds * 64) {
+        load(c0);
+#pragma unroll
+        for (int r = 0; r < kBoRounds; ++r) {
+            if (c0 + (uint32_t)r * 64 >= w1) break;  // wave-uniform
+            const bool valid = c0 + (uint32_t)r * 64 + lane < w1;
+            const uint32_t d = el_slot(x[r]) & dm;
+            const uint64_t peers = match_lanes(d, lb, valid);
+            if (valid && (peers & lt) == 0) mine[d] += (uint32_t)__popcll(peers);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __syncthreads();
+    // digit totals -> digit starts (block scan over digits, kFzThreads x up to 4 digits), then each
+    // wave's base per digit = B0 + digit start + the counts of the earlier waves
+    constexpr int kDpt = (1 << kPartMaxLow) / kFzThreads;
+    uint32_t tot[kDpt], ts = 0;
+#pragma unroll
+    for (int k = 0; k < kDpt; ++k) {
+        const uint32_t d = threadIdx.x * kDpt + k;
+        uint32_t t = 0;
+        if (d < nd)
+            for (int w = 0; w < kW; ++w) t += pc[w * nd + d];
+        tot[k] = t;
+        ts += t;
+    }
+    uint32_t y = ts;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t z = __shfl_up(y, o, 64);
+        if (lane >= o) y += z;
+    }
+    if (lane == 63) wsum[wave] = y;
+    __syncthreads();
+    uint32_t pre = B0 + y - ts;
+    for (int w = 0; w < wave; ++w) pre += wsum[w];
+#pragma unroll
+    for (int k = 0; k < kDpt; ++k) {
+        const uint32_t d = threadIdx.x * kDpt + k;
+        if (d < nd) {
+            uint32_t run = pre;
+            for (int w = 0; w < kW; ++w) {
+                const uint32_t c = pc[w * nd + d];
+                pc[w * nd + d] = run;
+                run += c;
+            }
+        }
+        pre += tot[k];
+    }
+    __syncthreads();
+    for (uint32_t c0 = w0; c0 < w1; c0 += kBoRounds * 64) {
+        if (!one) load(c0);
+#pragma unroll
+        for (int r = 0; r < kBoRounds; ++r) {
+            if (c0 + (uint32_t)r * 64 >= w1) break;
+            const bool valid = c0 + (uint32_t)r * 64 + lane < w1;
+            const uint32_t d = el_slot(x[r]) & dm;
+            const uint64_t peers = match_lanes(d, lb, valid);
+            if (valid) es[mine[d] + (uint32_t)__popcll(peers & lt) - ebase] = x[r];
+            __builtin_amdgcn_wave_barrier();
+            if (valid && (peers & lt) == 0) mine[d] += (uint32_t)__popcll(peers);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __syncthreads();  // the bin in order before the runs read it
+}
+
+enum : int { kFzAll = 0, kFzBin = 1 };
+// kFzAll: one workgroup per kFzChunk sorted elements (owning the rules whose first element lies in
+// it); kFzBin: one workgroup per partition bin (el = the partition output; the bin is ordered into
+// es first, and every rule of the bin is the workgroup's).
 template <int kMode>
 __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, BatchScratch sc,
-                                                             const uint64_t *__restrict__ el, uint32_t nhost,
+                                                             const uint64_t *__restrict__ el_in, uint32_t nhost,
                                                              const uint32_t *__restrict__ dn, uint32_t nkey,
                                                              const int32_t *__restrict__ acquire,
                                                              const uint8_t *__restrict__ prio,
                                                              const uint32_t *__restrict__ ts_off, int64_t ts_base,
                                                              int simple, uint32_t hot_min, uint64_t *__restrict__ out,
-                                                             int dbg) {
+                                                             int dbg, uint64_t *__restrict__ es, int lb) {
     __shared__ uint32_t fheads[kFzChunk + 1], fslot[kFzChunk + 1];  // owned rules: first position, slot
     // run records of the runs that start in [h0, h0 + kFzChunk) (every run but the later runs of
     // a rule that continues past the chunk, which use the global run arrays): length,
     // prioritized count, first prioritized index, acquire count | bucket delta << 8
-    __shared__ uint32_t rl_n[kFzChunk], rl_cp[kFzChunk], rl_p0[kFzChunk], rl_ab[kFzChunk];
+    __shared__ uint32_t rl_buf[4 * kFzChunk];
+    uint32_t *rl_n = rl_buf, *rl_cp = rl_buf + kFzChunk, *rl_p0 = rl_buf + 2 * kFzChunk, *rl_ab = rl_buf + 3 * kFzChunk;
     __shared__ uint8_t rl_done[kFzChunk];  // short closed-form runs answered by their flows lane
     __shared__ FAgg wtot[kFzThreads / 64];
     __shared__ uint32_t s_h0, s_E, s_wcnt[kFzThreads / 64];
     __shared__ uint32_t s_ncand, s_cbase, s_next, s_cand[2 * kFzThreads];
+    // bin mode: the ordered bin, when it fits, stays in LDS (every later element read is an LDS read
+    // through a flat pointer); a larger bin is ordered into the global buffer es
+    __shared__ uint64_t sel[kMode == kFzBin ? kBinLds : 1];
+    static_assert((kFzThreads / 64) << kPartMaxLow <= 4 * kFzChunk, "bin_order's digit counts fit the run records");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t *el = el_in;
+    uint32_t h0, E;
+    if constexpr (kMode == kFzBin) {
+        const uint32_t B0 = sc.pstart[blockIdx.x], B1 = sc.pstart[blockIdx.x + 1];
+        if (B0 >= B1) return;
+        unsigned long long ot = 0;
+        fz_mark(dbg, 0, ot);
+        const bool in_lds = B1 - B0 <= (uint32_t)kBinLds && !(dbg & 64);
+        bin_order(el_in, in_lds ? sel : es, in_lds ? B0 : 0u, B0, B1, lb, rl_buf, s_wcnt);
+        fz_mark(dbg, 4, ot);
+        // element p of the bin at el[p]: the LDS image shifted by the bin start (a flat address)
+        el = in_lds ? reinterpret_cast<const uint64_t *>(reinterpret_cast<uintptr_t>(&sel[0]) - (uintptr_t)B0 * 8u) : es;
+        h0 = B0;
+        E = B1;
+    } else {
     const uint32_t n = dn ? min(nhost, *dn) : nhost;
     const uint32_t c0 = blockIdx.x * kFzChunk;
     if (c0 >= n) return;
@@ -953,7 +1114,7 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
         if (first_inv < c1) atomicMin(&s_E, first_inv);
     }
     __syncthreads();
-    const uint32_t h0 = s_h0;
+    h0 = s_h0;
     if (h0 >= s_E) return;  // uniform: the chunk holds no rule head
     if (s_E == c1 && c1 < n) {  // the last owned rule may continue past the chunk
         const uint32_t ls = el_slot(el[c1 - 1]);
@@ -987,7 +1148,8 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
         }
     }
     __syncthreads();
-    const uint32_t E = s_E;
+    E = s_E;
+    }
     unsigned long long fzt = 0;
     fz_mark(dbg, 0, fzt);
     // ---- 1 runs (blocks of kFzChunk elements over [h0, E))
@@ -1092,6 +1254,7 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
     int64_t qbase = 0;
     RecCarry<10> rc;
     rc.have = false;
+    const bool hdr_thr = st.uni_S && !simple;  // the closed form takes the threshold from the record header
     auto take_rule = [&]() {
         r = fheads[f];
         r1 = f + 1 < nf ? fheads[f + 1] : E;
@@ -1105,13 +1268,14 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
         }
         if (st.uni_S) {
             // uniform geometry: the record address and the window geometry without the parameter
-            // load; only the threshold is loaded, beside the record's loads
+            // load; the threshold is the record header's copy (Rec::thr), which comes with the
+            // header's loads (simple mode's threshold is a parameter load beside them)
             P.S = st.uni_S;
             P.W = st.uni_W;
             P.interval = st.uni_iv;
             P.isec = st.uni_iv / 1000.0;
-            P.boff = s * (uint32_t)(st.uni_S + 1);
-            P.thr = simple ? st.param[s].thr_simple : st.param[s].thr;
+            P.boff = s * rec_units(st.uni_S);
+            P.thr = simple ? st.param[s].thr_simple : 0.0;
             P.thr_simple = P.thr;
             P.active = 1;
             P.ns = 0;
@@ -1145,6 +1309,15 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
         // prioritized requests among the run's first k: plist[p0 .. p0 + cp_tot) holds the
         // run's prioritized positions (ascending)
         auto prio_before = [&](uint32_t k) -> uint32_t {
+            if (ri.cp_tot <= 4) {  // the usual case: the positions loaded together, no dependent search
+                uint32_t pv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) pv[u] = sc.plist[ri.p0 + min((uint32_t)u, ri.cp_tot - 1)];
+                uint32_t c = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) c += ((uint32_t)u < ri.cp_tot && pv[u] < ri.j0 + k) ? 1u : 0u;
+                return c;
+            }
             uint32_t lo = 0, hi = ri.cp_tot;
             while (lo < hi) {
                 const uint32_t m = (lo + hi) >> 1;
@@ -1158,11 +1331,11 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
         // larger sampleCounts load the pairs every run
         bool fast;
         if (P.S <= 10) {
-            fast = run_fast<decltype(prio_before), 10>(st, P, R, thr, qbase, ri, prio_before, ro, rc);
+            fast = run_fast<decltype(prio_before), 10>(st, P, R, thr, hdr_thr, qbase, ri, prio_before, ro, rc);
         } else {
             RecCarry<0> rc0;
             rc0.have = false;
-            fast = run_fast<decltype(prio_before), 0>(st, P, R, thr, qbase, ri, prio_before, ro, rc0);
+            fast = run_fast<decltype(prio_before), 0>(st, P, R, thr, hdr_thr, qbase, ri, prio_before, ro, rc0);
         }
         if (!fast) {
             for (uint32_t j = r; j < r + ri.n; ++j) {
@@ -1517,7 +1690,10 @@ struct KeyShared {
     WConst wcs[256];
     uint16_t cnt[kKeyWaves][kHot];  // per wave: hot requests so far per hot id
     uint32_t s_np[kKeyWaves], s_bd[kKeyWaves], s_tm[kKeyWaves];
-    uint32_t hist0[2][256];         // per sort tile of the segment: the first radix digit's counts
+    union {
+        uint32_t hist0[2][256];      // per sort tile of the segment: the first radix digit's counts
+        uint32_t phist[kPartBins];   // partition mode: the segment's cold elements per slot bin
+    };
 };
 template <int kPass, bool kDense, bool kNT = false>
 __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, const BatchScratch &sc,
@@ -1525,7 +1701,11 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                                         const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off,
                                         int64_t ts_base, uint32_t n, uint64_t *__restrict__ out, int dbg,
                                         int d0, uint32_t *__restrict__ hist, uint32_t ntiles) {
+    // d0 > 0: the LSD sort's first digit (d0 bits) counted per sort tile; d0 < 0: partition mode, the
+    // cold elements counted per slot bin (slot >> -d0) into the segment's row of hist ([seg][kPartBins])
     WConst *wcs = sh.wcs;
+    const int pl = d0 < 0 ? -d0 : 0;
+    if (pl) d0 = 0;
     const uint32_t dmask = (1u << d0) - 1u;
     auto &cnt = sh.cnt;
     uint32_t *s_np = sh.s_np, *s_bd = sh.s_bd;
@@ -1536,7 +1716,7 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
     const uint64_t lt = lanemask_lt64(lane);
     if (kDense)
         for (int k = threadIdx.x; k < 256; k += kKeyThreads) wcs[k] = sc.wconst[k];  // window-length codes
-    for (int k = threadIdx.x; k < 2 * 256; k += kKeyThreads) (&sh.hist0[0][0])[k] = 0;
+    for (int k = threadIdx.x; k < (pl ? kPartBins : 2 * 256); k += kKeyThreads) sh.phist[k] = 0;
     if (nhot) {
         uint4 *cz = reinterpret_cast<uint4 *>(&cnt[0][0]);
         for (int k = threadIdx.x; k < (int)(sizeof(cnt) / 16); k += kKeyThreads) cz[k] = make_uint4(0, 0, 0, 0);
@@ -1713,6 +1893,7 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                     else
                         sc.el_tile[(size_t)ubase + nc + (uint32_t)__popcll(em & lt)] = el_pack(slot, bd6, p, a7, i);
                     if (d0) atomicAdd(&sh.hist0[wave >> 2][slot & dmask], 1u);
+                    if (pl) atomicAdd(&sh.phist[slot >> pl], 1u);
                 }
                 nc += (uint32_t)__popcll(em);
             }
@@ -1819,12 +2000,158 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
         }
     }
     if (lane == 0) sc.tile_nc[sub] = active ? nc : 0u;  // totals: k_hot_mode
+    if (pl) {  // the segment's bin counts (one contiguous row; k_part_colscan scans the columns)
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < (uint32_t)kPartBins; k += kKeyThreads)
+            hist[(size_t)seg * kPartBins + k] = sh.phist[k];
+    }
     if (d0) {  // the sort's first-pass histogram rows of this segment's two tiles
         __syncthreads();
         for (uint32_t k = threadIdx.x; k < (2u << d0); k += kKeyThreads) {
             const uint32_t t = k >> d0, d = k & dmask, tile = seg * 2 + t;
             if (tile < ntiles) hist[(size_t)d * ntiles + tile] = sh.hist0[t][d];
         }
+    }
+}
+
+// ---- cold partition (hot path; SURVEY hard part 4): the key kernels count each segment's cold elements
+// per slot bin ([segment][bin], one contiguous row per segment), k_part_colscan turns each group of
+// kPartGroup rows into exclusive prefixes down the columns (and the group sums), k_part_binscan scans
+// the group sums per bin and the bin totals into bin starts, and k_part_scatter moves every cold element
+// to bin start + its position among the bin's elements in arrival order: one pass over the elements
+// instead of the LSD sort's three.  k_cold_fused then orders each bin inside its workgroup (bin_order).
+__global__ __launch_bounds__(256) void k_part_colscan(BatchScratch sc, uint32_t nseg) {
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t t0 = blockIdx.y * kPartGroup, t1 = min(nseg, t0 + kPartGroup);
+    uint32_t acc = 0;
+    for (uint32_t t = t0; t < t1; t += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = t + k < t1 ? sc.phist[(size_t)(t + k) * kPartBins + b] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (t + k < t1) sc.phist[(size_t)(t + k) * kPartBins + b] = acc;
+            acc += v[k];
+        }
+    }
+    sc.pgrp[(size_t)blockIdx.y * kPartBins + b] = acc;
+}
+
+// per bin: exclusive prefix of the group sums and the bin total (kPartBins / 256 workgroups); the last
+// workgroup to finish turns the totals into the bin starts
+__global__ __launch_bounds__(256) void k_part_binscan(BatchScratch sc, uint32_t ngroups) {
+    __shared__ uint32_t ws[4];
+    __shared__ uint32_t s_last;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    uint32_t acc = 0;
+    for (uint32_t g = 0; g < ngroups; g += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = g + k < ngroups ? sc.pgrp[(size_t)(g + k) * kPartBins + b] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (g + k < ngroups) sc.pgrp[(size_t)(g + k) * kPartBins + b] = acc;
+            acc += v[k];
+        }
+    }
+    sc.pstart[b] = acc;  // the bin's total for now
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&sc.pstart[kPartBins + 1], 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    constexpr int kPer = kPartBins / 256;
+    uint32_t tot[kPer], ts = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        tot[k] = __hip_atomic_load(&sc.pstart[threadIdx.x * kPer + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ts += tot[k];
+    }
+    uint32_t x = ts;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) ws[wave] = x;
+    __syncthreads();
+    uint32_t pre = x - ts;
+    for (int w = 0; w < wave; ++w) pre += ws[w];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        sc.pstart[threadIdx.x * kPer + k] = pre;
+        pre += tot[k];
+    }
+    if (threadIdx.x == 255) {
+        sc.pstart[kPartBins] = pre;
+        sc.pstart[kPartBins + 1] = 0;  // the done counter, for the next batch
+    }
+}
+
+// One workgroup per key segment, one wave per compaction segment (sub): pass 1 counts each wave's
+// elements per bin (ballot match, the lowest lane of a group adds it), the counts become prefixes
+// over the waves, pass 2 places every element at its segment's base for the bin + the earlier waves'
+// + the earlier lanes' elements of the bin.  Arrival order holds inside every bin.
+__global__ __launch_bounds__(kKeyThreads) void k_part_scatter(BatchScratch sc, uint32_t nseg, int lb,
+                                                              uint64_t *__restrict__ out, int dbg) {
+    __shared__ uint32_t gb[kPartBins];               // this segment's first position in each bin
+    __shared__ uint16_t wc[kKeyWaves][kPartBins];    // per wave: counts, then prefixes over the waves
+    // XCD-aware: consecutive blocks round-robin over the 8 XCDs, so block b takes segment (b % 8) * per + b / 8:
+    // each XCD's workgroups take consecutive segments, whose elements of one bin are neighbours in the
+    // output, so a 128-byte line is completed in one XCD's L2 instead of written back in pieces from all 8
+    const uint32_t per = (nseg + 7) / 8;
+    const uint32_t seg = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    if (seg >= nseg) return;
+    const uint32_t g = seg / kPartGroup;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt = lanemask_lt64(lane);
+    for (uint32_t b = threadIdx.x; b < (uint32_t)kPartBins; b += kKeyThreads) {
+        gb[b] = sc.pstart[b] + sc.pgrp[(size_t)g * kPartBins + b] + sc.phist[(size_t)seg * kPartBins + b];
+#pragma unroll
+        for (int w = 0; w < kKeyWaves; ++w) wc[w][b] = 0;
+    }
+    const uint32_t sub = seg * kKeyWaves + wave;
+    const uint32_t nc = sc.tile_nc[sub];
+    const uint64_t *src = sc.el_tile + (size_t)sub * kSubSeg;
+    uint64_t x[kSubRounds];
+#pragma unroll
+    for (int r = 0; r < kSubRounds; ++r) {
+        const uint32_t i = (uint32_t)r * 64 + lane;
+        x[r] = src[i < nc ? i : 0u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSubRounds; ++r) {
+        if ((uint32_t)r * 64 >= nc) break;  // wave-uniform
+        const bool valid = (uint32_t)r * 64 + lane < nc;
+        const uint32_t b = el_slot(x[r]) >> lb;
+        const uint64_t peers = match_lanes(b, kPartBits, valid);
+        if (valid && (peers & lt) == 0) wc[wave][b] += (uint16_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < (uint32_t)kPartBins; b += kKeyThreads) {
+        uint32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < kKeyWaves; ++w) {
+            const uint32_t c = wc[w][b];
+            wc[w][b] = (uint16_t)run;
+            run += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSubRounds; ++r) {
+        if ((uint32_t)r * 64 >= nc) break;
+        const bool valid = (uint32_t)r * 64 + lane < nc;
+        const uint32_t b = el_slot(x[r]) >> lb;
+        const uint64_t peers = match_lanes(b, kPartBits, valid);
+        if (valid && !(dbg & 32)) out[gb[b] + wc[wave][b] + (uint32_t)__popcll(peers & lt)] = x[r];  // 32: profiling
+        __builtin_amdgcn_wave_barrier();
+        if (valid && (peers & lt) == 0) wc[wave][b] += (uint16_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -2024,7 +2351,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
         P.W = st.uni_W;
         P.interval = st.uni_iv;
         P.isec = st.uni_iv / 1000.0;
-        P.boff = s * (uint32_t)(st.uni_S + 1);
+        P.boff = s * rec_units(st.uni_S);
         P.thr = st.param[s].thr;
         P.thr_simple = P.thr;
         P.active = 1;
@@ -2143,9 +2470,12 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
         if (lane == CEV_OCCUPIED_BLOCK) cl += (int64_t)(np_after - cw);
         if (ok) {
             if (lane < CEV_N) R.cnt(lane, cj) = cl;
+            // the header's cached group follows (the cold closed form reads it when the rule turns cold)
+            if (lane > 0 && lane < CEV_N) R.cache()[lane == CEV_WAITING ? 0 : lane] = cl;
             if (lane == 0) {
                 if (rot) R.start(cj) = ws;
                 if (occ_dirty) R.occ() = o;
+                R.tag() = ws;
             }
         } else if (lane == 0) {
             atomicAdd(&sc.counters[CTL_HOTERR], 1u);
@@ -2310,6 +2640,59 @@ __global__ __launch_bounds__(kFinWgThreads) void k_hot_final(ClusterState st, Ba
             res = pack_result(TRS_BLOCKED, 0, 0);
         }
         out[wbase + u * 64 + lane] = res;
+    }
+}
+
+// k_hot_final without LDS (the default; SGA_FIN_LDS=1 selects the LDS form above): every hot request
+// gathers its rank base (hbase row of its segment) and its run record (hrun, a few hundred KB, L2-resident)
+// directly.  Beside the cold stage, whose two workgroups per CU hold nearly all of the LDS, a kernel that
+// needs no LDS still finds room on every CU.  Four waves of kFinChunk x 64 requests per workgroup; the
+// first kFinPrioWgsG workgroups answer the prioritized hot requests.
+constexpr uint32_t kFinPrioWgsG = 64;
+constexpr int kFinGThreads = 256;
+constexpr uint32_t kFinGSpan = kFinGThreads * kFinChunk;  // requests per workgroup
+__global__ __launch_bounds__(kFinGThreads) void k_hot_final_g(ClusterState st, BatchScratch sc, uint32_t n,
+                                                              const uint64_t *__restrict__ el,
+                                                              uint64_t *__restrict__ out) {
+    if (!sc.counters[CTL_MODE]) return;
+    if (blockIdx.x < kFinPrioWgsG) {
+        prio_results_range(st, sc, el, out, blockIdx.x * kFinGThreads + threadIdx.x, kFinPrioWgsG * kFinGThreads);
+        return;
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t wbase = (blockIdx.x - kFinPrioWgsG) * kFinGSpan + (uint32_t)wave * (kFinChunk * 64);
+    if (wbase >= n) return;
+    uint32_t code[kFinChunk], bs[kFinChunk];
+    uint4 ra[kFinChunk], rb[kFinChunk];
+#pragma unroll
+    for (int u = 0; u < kFinChunk; ++u) code[u] = sc.hcode[min(wbase + (uint32_t)u * 64 + lane, n - 1)];
+#pragma unroll
+    for (int u = 0; u < kFinChunk; ++u) {  // unconditional gathers (a non-hot lane reads hot id 0's entries)
+        const uint32_t i = min(wbase + (uint32_t)u * 64 + lane, n - 1);
+        const uint32_t cd = code[u];
+        const bool hot = cd != kNoCode && !(cd >> 31);
+        const uint32_t h = hot ? (cd & 0xFFFu) : 0u, b = hot ? (cd >> 25) : 0u;
+        bs[u] = sc.hbase[(size_t)(i / kHotSeg) * kHot + h];
+        const uint4 *hp = reinterpret_cast<const uint4 *>(hrun_at(sc, h, b));
+        ra[u] = hp[0];  // s0, thr
+        rb[u] = hp[1];  // isec, f, start
+    }
+#pragma unroll
+    for (int u = 0; u < kFinChunk; ++u) {
+        const uint32_t i = wbase + (uint32_t)u * 64 + lane;
+        const uint32_t cd = code[u];
+        if (i >= n || cd == kNoCode || (cd >> 31)) continue;  // cold, invalid or prioritized
+        const int64_t s0 = i64_of(ra[u].x, ra[u].y);
+        const double thr = f64_of(ra[u].z, ra[u].w), isec = f64_of(rb[u].x, rb[u].y);
+        const uint32_t local = bs[u] + ((cd >> 12) & 0x1FFFu) - rb[u].w;
+        uint64_t res;
+        if (local < rb[u].z) {
+            const int64_t sum = s0 + (int64_t)local;
+            res = pack_result(TRS_OK, j_d2i(thr - (double)sum / isec - 1.0), 0);
+        } else {
+            res = pack_result(TRS_BLOCKED, 0, 0);
+        }
+        out[i] = res;
     }
 }
 
@@ -2488,7 +2871,10 @@ __global__ void k_hot_reset(ClusterState st, BatchScratch sc, uint32_t nslots_ca
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)kHot; i += gridDim.x * blockDim.x)
         sc.hot_next[i] = kNoSlot;
     if (blockIdx.x == 0 && threadIdx.x < kHotCtlWords) sc.hot_ctl[threadIdx.x] = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.tmax_all = 0;  // no batch in flight (callers have joined)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *sc.tmax_all = 0;  // no batch in flight (callers have joined)
+        sc.pstart[kPartBins + 1] = 0;  // k_part_binscan's done counter
+    }
 }
 
 __global__ void k_metric_sums(ClusterState st, uint32_t s, int64_t now, int64_t *out7) {
@@ -2573,6 +2959,16 @@ __global__ void k_init_slots(ClusterState st, const uint32_t *slots, uint32_t n)
         bucket_zero(R, j);
     }
     R.occ() = SlotOcc{0, 0, 0, 0};
+    R.tag() = kAbsent;
+    R.thr() = P.thr;
+}
+
+__global__ void k_rec_thr(ClusterState st, uint32_t n) {
+    const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
+    if (s >= n) return;
+    const SlotParam P = st.param[s];
+    if (P.S <= 0) return;  // not allocated (its parameters are zero, its boff is no record)
+    rec_of(st, P).thr() = P.thr;
 }
 
 
@@ -3056,7 +3452,7 @@ static size_t max_hist_entries(size_t cap, uint32_t nslots_cap) {
 }
 
 // A/B knob for profiling only (results are wrong when set): 1 skips k_cold_fused's flows, 2 its results,
-// 4 k_hot_key's rank pass, 8 its code fix-up
+// 4 k_hot_key's rank pass, 8 its code fix-up, 32 k_part_scatter's stores (16: phase times, results exact)
 static int fz_debug() {
     static const int v = getenv("SGA_FZ_DEBUG") ? atoi(getenv("SGA_FZ_DEBUG")) : 0;
     return v;
@@ -3065,6 +3461,20 @@ static int fz_debug() {
 static uint32_t fin_cache() {  // profiling knob: SGA_FIN_CACHE=0 turns k_hot_final's LDS cache off
     static const uint32_t v = getenv("SGA_FIN_CACHE") ? std::min<uint32_t>(atoi(getenv("SGA_FIN_CACHE")), kFinCache) : kFinCache;
     return v;
+}
+
+// k_hot_final_g by default; SGA_FIN_LDS=1 (A/B knob) the LDS-cached k_hot_final
+static void launch_hot_final(const ClusterState &st, BatchScratch &sc, uint32_t n, const uint64_t *pel, uint64_t *out,
+                             hipStream_t s) {
+    static const bool lds = getenv("SGA_FIN_LDS") && atoi(getenv("SGA_FIN_LDS")) == 1;
+    if (lds) {
+        const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
+        hipLaunchKernelGGL(k_hot_final, dim3(nseg + kFinPrioWgs), dim3(kFinWgThreads), 0, s, st, sc, n, pel, out,
+                           fin_cache());
+    } else {
+        hipLaunchKernelGGL(k_hot_final_g, dim3((n + kFinGSpan - 1) / kFinGSpan + kFinPrioWgsG), dim3(kFinGThreads), 0, s,
+                           st, sc, n, pel, out);
+    }
 }
 
 static int hot_overlap() {  // A/B knob: SGA_HOT_OVERLAP=0 runs the hot side after the cold stage
@@ -3083,17 +3493,28 @@ void batch_scratch_release(BatchScratch &sc) {
     if (sc.ev_join) (void)hipEventDestroy(sc.ev_join);
     if (sc.ev_fork0) (void)hipEventDestroy(sc.ev_fork0);
     if (sc.ev_mid) (void)hipEventDestroy(sc.ev_mid);
-    sc.side = nullptr;
-    sc.ev_fork = sc.ev_join = sc.ev_fork0 = sc.ev_mid = nullptr;
+    if (sc.side2) (void)hipStreamDestroy(sc.side2);
+    if (sc.ev_prio) (void)hipEventDestroy(sc.ev_prio);
+    sc.side = sc.side2 = nullptr;
+    sc.ev_fork = sc.ev_join = sc.ev_fork0 = sc.ev_mid = sc.ev_prio = nullptr;
 }
 
 
 // Cold stage of a large batch over the sorted elements: runs, flows and results in one kernel.
+// Partitioned (sc.part_lb > 0, hot path): one workgroup per slot bin, el = the partition output, each bin
+// ordered into the other element buffer first.
 static void cold_stage(const ClusterState &st, BatchScratch &sc, const uint64_t *el, uint32_t n, const uint32_t *dn,
                        uint32_t invalid_key, const int32_t *acquire, const uint8_t *prio, const uint32_t *ts_off,
                        int64_t ts_base, int simple, uint32_t hot_min, uint64_t *out, hipStream_t s) {
+    if (sc.part_lb) {
+        uint64_t *es = el == sc.el[0] ? sc.el[1] : sc.el[0];
+        hipLaunchKernelGGL(k_cold_fused_t<kFzBin>, dim3(kPartBins), dim3(kFzThreads), 0, s, st, sc, el, n, dn,
+                           invalid_key, acquire, prio, ts_off, ts_base, simple, hot_min, out, fz_debug(), es,
+                           sc.part_lb);
+        return;
+    }
     hipLaunchKernelGGL(k_cold_fused, dim3((n + kFzChunk - 1) / kFzChunk), dim3(kFzThreads), 0, s, st, sc, el, n, dn,
-                       invalid_key, acquire, prio, ts_off, ts_base, simple, hot_min, out, fz_debug());
+                       invalid_key, acquire, prio, ts_off, ts_base, simple, hot_min, out, fz_debug(), nullptr, 0);
 }
 
 static size_t hot_rows(size_t cap) { return (cap + kHotSeg - 1) / kHotSeg; }
@@ -3138,6 +3559,9 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up(segs_alloc * kSegStat * 4);                                      // seg_stat
     b += align_up(64);                                                             // tmax_all
     b += align_up((size_t)kHotCand * 2 * 4);                                       // hot_cand
+    b += align_up(segs_alloc * kPartBins * 4);                                     // phist
+    b += align_up(((segs_alloc + kPartGroup - 1) / kPartGroup) * kPartBins * 4);   // pgrp
+    b += align_up((kPartBins + 2) * 4);                                            // pstart, done counter
     return b;
 }
 
@@ -3210,6 +3634,9 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.seg_stat = (uint32_t *)take(segs_alloc * kSegStat * 4);
     sc.tmax_all = (unsigned long long *)take(64);
     sc.hot_cand = (uint32_t *)take((size_t)kHotCand * 2 * 4);
+    sc.phist = (uint32_t *)take(segs_alloc * kPartBins * 4);
+    sc.pgrp = (uint32_t *)take(((segs_alloc + kPartGroup - 1) / kPartGroup) * kPartBins * 4);
+    sc.pstart = (uint32_t *)take((kPartBins + 2) * 4);
     sc.cap = cap;
 }
 
@@ -3294,6 +3721,16 @@ static void side_stream_init(BatchScratch &sc) {
     SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork, hipEventDisableTiming));
     SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_join, hipEventDisableTiming));
     SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_mid, hipEventDisableTiming));
+    SGA_HIP_CHECK(hipStreamCreateWithFlags(&sc.side2, hipStreamNonBlocking));
+    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_prio, hipEventDisableTiming));
+}
+
+// The cold partition's slot bits below the bin, or 0 (the LSD sort): bins of 2^lb slots need
+// 5 <= lb <= kPartMaxLow (rule slot counts from 2^15 to about 2^21).  SGA_COLD_PART=0 (A/B knob) turns it off.
+static int cold_part_lb(int bits) {
+    static const bool off = getenv("SGA_COLD_PART") && atoi(getenv("SGA_COLD_PART")) == 0;
+    const int lb = bits - kPartBits;
+    return (!off && lb >= 5 && lb <= kPartMaxLow) ? lb : 0;
 }
 
 static int hot_key_bits(const ClusterState &st) {
@@ -3311,14 +3748,12 @@ static int hot_key_bits(const ClusterState &st) {
 // prioritized sort are done, on hs; ev_mid after the hot runs (the next hot set may start), ev_join after all.
 static void hot_side(const ClusterState &st, BatchScratch &sc, int64_t ts_base, uint32_t n, uint64_t *out,
                      hipStream_t hs, bool ovl) {
-    const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
     const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
     hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, hs, st, sc, sc.pel_sorted);
     hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, hs, st, sc, ts_base);
     if (ovl) {
         SGA_HIP_CHECK(hipEventRecord(sc.ev_mid, hs));  // the hot runs read hot_slot; the next hot set may start
-        hipLaunchKernelGGL(k_hot_final, dim3(nseg + kFinPrioWgs), dim3(kFinWgThreads), 0, hs, st, sc, n, sc.pel_sorted,
-                           out, fin_cache());
+        launch_hot_final(st, sc, n, sc.pel_sorted, out, hs);
         SGA_HIP_CHECK(hipEventRecord(sc.ev_join, hs));
     }
 }
@@ -3338,14 +3773,17 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const int64_t
     auto hka = st.dense_n ? (key_nt ? k_hot_key_dense<0, true> : k_hot_key_dense<0, false>) : k_hot_key_hash<0>;
     auto hkb = st.dense_n ? k_hot_key_dense<1> : k_hot_key_hash<1>;
     // the key kernels count the sort's first digit per tile as they write the elements
-    // (their LDS counts hold 8-bit digits; a wider first digit is counted by the sort itself)
+    // (their LDS counts hold 8-bit digits; a wider first digit is counted by the sort itself), or, with
+    // the cold partition, each segment's elements per slot bin
     const int dsort = radix64_digit_bits(bits);
-    const int d0 = dsort <= 8 ? dsort : 0;
+    sc.part_lb = cold_part_lb(bits);
+    const int d0 = sc.part_lb ? -sc.part_lb : (dsort <= 8 ? dsort : 0);
     const uint32_t ntiles_sort = (uint32_t)radix64_tiles(n);
+    uint32_t *khist = sc.part_lb ? sc.phist : sc.radix.hist;
     hipLaunchKernelGGL(hka, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out,
-                       fz_debug(), d0, sc.radix.hist, ntiles_sort);
+                       fz_debug(), d0, khist, ntiles_sort);
     hipLaunchKernelGGL(hkb, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out,
-                       fz_debug(), d0, sc.radix.hist, ntiles_sort);
+                       fz_debug(), d0, khist, ntiles_sort);
     hipLaunchKernelGGL(k_hot_mode, dim3(1), dim3(1024), 0, s, sc, nseg * kKeyWaves, nseg, ts_base);
     // the hot side's count scans and prioritized sort on the side stream, beside the cold sort
     const bool ovl = hot_overlap() && !(fz_debug() & 16);
@@ -3356,22 +3794,41 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const int64_t
         SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork0, 0));
         hs = sc.side;
     }
+    // the prioritized hot requests, sorted by hot id on their own (12-bit key): on a third stream when the
+    // hot side overlaps, so it and the count scans both run beside the cold sort / partition
+    hipStream_t ps = hs;
+    if (ovl) {
+        SGA_HIP_CHECK(hipStreamWaitEvent(sc.side2, sc.ev_fork0, 0));
+        ps = sc.side2;
+    }
+    const int npp = radix_sort_u64_tiled(sc.pel_tile, sc.ptile_np, sc.counters + CTL_NPRIO, sc.pel[0], sc.pel[1], n,
+                                         kSlotShift, 12, sc.radix_p, ps, false);
+    sc.pel_sorted = (npp & 1) ? sc.pel[0] : sc.pel[1];
     hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
     hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, hs, sc, ngroups);
     hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
     hipLaunchKernelGGL(k_hot_pre, dim3(kHotBuckets), dim3(kThreads), 0, hs, sc);
-    // the prioritized hot requests, sorted by hot id on their own (12-bit key)
-    const int npp = radix_sort_u64_tiled(sc.pel_tile, sc.ptile_np, sc.counters + CTL_NPRIO, sc.pel[0], sc.pel[1], n,
-                                         kSlotShift, 12, sc.radix_p, hs, false);
-    sc.pel_sorted = (npp & 1) ? sc.pel[0] : sc.pel[1];
+    if (ovl) {  // the prioritized sort joins the side stream (k_prio_rank needs both)
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_prio, ps));
+        SGA_HIP_CHECK(hipStreamWaitEvent(hs, sc.ev_prio, 0));
+    }
     // Not pipelined: the hot side needs nothing of the cold sort (disjoint rules, disjoint results), so its runs
     // and results go on beside the sort and the cold stage waits for it only at the end of the batch.  Pipelined,
     // the hot runs write rule state and wait for stage 2 (after the earlier batch's decisions).
     sc.hot_early = ovl && !pipelined;
     if (sc.hot_early) hot_side(st, sc, ts_base, n, out, hs, true);
-    const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
-                                        kSlotShift, bits, sc.radix, s, d0 > 0);
-    sc.el_sorted = (np & 1) ? sc.el[0] : sc.el[1];
+    if (sc.part_lb) {  // the cold partition: one pass into slot bins, ordered per bin by k_cold_fused
+        const uint32_t ngroups = (nseg + kPartGroup - 1) / kPartGroup;
+        hipLaunchKernelGGL(k_part_colscan, dim3(kPartBins / 256, ngroups), dim3(256), 0, s, sc, nseg);
+        hipLaunchKernelGGL(k_part_binscan, dim3(kPartBins / 256), dim3(256), 0, s, sc, ngroups);
+        hipLaunchKernelGGL(k_part_scatter, dim3(8 * ((nseg + 7) / 8)), dim3(kKeyThreads), 0, s, sc, nseg, sc.part_lb,
+                           sc.el[0], fz_debug());
+        sc.el_sorted = sc.el[0];
+    } else {
+        const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
+                                            kSlotShift, bits, sc.radix, s, d0 > 0);
+        sc.el_sorted = (np & 1) ? sc.el[0] : sc.el[1];
+    }
     if (ovl && !sc.hot_early) {  // stage 1 ends on s
         SGA_HIP_CHECK(hipEventRecord(sc.ev_fork, hs));
         SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_fork, 0));
@@ -3383,7 +3840,6 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const int64_t
 static void decide_hot(const ClusterState &st, BatchScratch &sc, const int32_t *acquire, const uint8_t *prio,
                        int64_t ts_base, const uint32_t *ts_off, uint32_t n, uint64_t *out, hipStream_t s) {
     const uint32_t invalid_key = st.nslots;
-    const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
     const uint64_t *el = sc.el_sorted, *pel = sc.pel_sorted;
     const bool ovl = hot_overlap() && !(fz_debug() & 16);
     if (!sc.hot_early) {  // the hot side beside the cold stage
@@ -3405,12 +3861,11 @@ static void decide_hot(const ClusterState &st, BatchScratch &sc, const int32_t *
         const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         SGA_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fz_phase), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
         if (ph[7])
-            fprintf(stderr, "fz phases (wall_clock64 ticks per workgroup, %llu wgs): runs %.0f flows %.0f results %.0f\n",
-                    ph[7], (double)ph[0] / ph[7], (double)ph[1] / ph[7], (double)ph[2] / ph[7]);
+            fprintf(stderr, "fz phases (wall_clock64 ticks per workgroup, %llu wgs): order %.0f runs %.0f flows %.0f results %.0f\n",
+                    ph[7], (double)ph[3] / ph[7], (double)ph[0] / ph[7], (double)ph[1] / ph[7], (double)ph[2] / ph[7]);
     }
     if (!ovl) {
-        hipLaunchKernelGGL(k_hot_final, dim3(nseg + kFinPrioWgs), dim3(kFinWgThreads), 0, s, st, sc, n, pel, out,
-                           fin_cache());
+        launch_hot_final(st, sc, n, pel, out, s);
     } else if (!tail_early()) {
         SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_join, 0));
     } else {
@@ -3476,7 +3931,8 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
         hipLaunchKernelGGL(k_small_sort, dim3(1), dim3(kSmallThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base,
                            n, m, simple, invalid_key, sc.el[0], out);
         hipLaunchKernelGGL(k_cold_fused, dim3((n + kFzChunk - 1) / kFzChunk), dim3(kFzThreads), 0, s, st, sc, sc.el[0],
-                           n, nullptr, invalid_key, acquire, prio, ts_off, ts_base, simple, 0xFFFFFFFFu, out, 0);
+                           n, nullptr, invalid_key, acquire, prio, ts_off, ts_base, simple, 0xFFFFFFFFu, out, 0,
+                           nullptr, 0);
         return;
     }
     if (cluster_hot_eligible(st, sc, n, simple, nlims)) {
@@ -3660,6 +4116,10 @@ void cluster_metric_sums(const ClusterState &st, uint32_t slot, int64_t now, int
 void cluster_init_slots(const ClusterState &st, const uint32_t *d_slots, uint32_t n, hipStream_t s) {
     if (n == 0) return;
     hipLaunchKernelGGL(k_init_slots, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, st, d_slots, n);
+}
+
+void cluster_sync_rec_thr(const ClusterState &st, uint32_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_rec_thr, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, st, n);
 }
 
 }  // namespace sga

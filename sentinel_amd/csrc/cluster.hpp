@@ -122,6 +122,12 @@ constexpr int kHotBuckets = 64;     // window buckets a batch may span on the ho
 constexpr int kHotGroupRows = 16;   // count rows per group of the column scan
 constexpr int kHotCand = 1 << 16;   // next-hot-set candidates gathered per batch
 constexpr int kSegStat = 4;         // seg_stat words per rank segment
+// Cold partition (hot path): the cold elements are scattered once into kPartBins bins of consecutive
+// rule slots (slot >> part_lb), and k_cold_fused orders each bin in its workgroup (SURVEY hard part 4)
+constexpr int kPartBits = 11;
+constexpr int kPartBins = 1 << kPartBits;
+constexpr int kPartGroup = 64;      // key segments per group of the column scan
+constexpr int kPartMaxLow = 10;     // slot bits below the bin (the in-workgroup digit) at most
 
 // Per-batch control words (BatchScratch::counters, zeroed per batch).
 enum : int {
@@ -210,6 +216,10 @@ struct BatchScratch {
     const uint64_t *el_sorted = nullptr, *pel_sorted = nullptr;  // stage 1's sorted cold / prioritized elements
     bool hot_early = false;   // host: the batch's hot runs and results were queued in stage 1 (beside the cold sort)
     uint32_t *hot_cand;       // [kHotCand] (slot, count) of cold rules with >= hot_min requests (hot_ctl[6])
+    // cold partition: [segment][bin] counts (then in-group exclusive prefixes), [group][bin] group sums
+    // (then prefixes), [bin] bin starts (+ the total); part_lb: slot bits below the bin (host, 0 = LSD sort)
+    uint32_t *phist, *pgrp, *pstart;
+    int part_lb = 0;
     int hot_enabled = 1;      // host policy (sga_set_hot_rules)
     uint32_t small_max = 4096; // batches of at most this many requests take the one-workgroup path (sga_set_small_batch)
     int hot_lane_order = 0;   // lds_lane_order_ok() held on this device (set when the scratch is made)
@@ -218,6 +228,9 @@ struct BatchScratch {
     // beside the cold stage on the batch's stream (fork and join by events; made on first use)
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork0 = nullptr, ev_mid = nullptr;
+    // the prioritized hot requests' sort on a stream of its own (beside the hot count scans on `side`)
+    hipStream_t side2 = nullptr;
+    hipEvent_t ev_prio = nullptr;
 };
 
 // The hot path's in-order ranks come from LDS atomics whose same-word lanes are served in lane
@@ -336,5 +349,7 @@ void cluster_metric_sums(const ClusterState &st, uint32_t slot, int64_t now, int
 
 // Fresh metrics: every bucket of each listed slot absent, occupy counters zero.
 void cluster_init_slots(const ClusterState &st, const uint32_t *d_slots, uint32_t n, hipStream_t stream);
+// copy SlotParam::thr into the header of every allocated slot < n (Rec::thr, cluster_exact.hpp)
+void cluster_sync_rec_thr(const ClusterState &st, uint32_t n, hipStream_t stream);
 
 }  // namespace sga

@@ -19,23 +19,40 @@ __device__ __forceinline__ uint64_t pack_result(int8_t status, int32_t remaining
 }
 
 // ---------------------------------------------------------------- exact per-request replay (device)
-// Window state of a rule lives in one contiguous record of 8 x S + 4 int64 (S + 1 64-byte units):
-//   [per bucket j: start, PASS] [occupy state: occupyCounter PASS, PASS_REQUEST, hasOccupied]
-//   [per bucket j: WAITING, BLOCK, PASS_REQUEST, BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK]
-// so the window sums read one dense vector of 16-byte pairs whose two cache lines also hold the
-// occupy state (a 64-byte aligned record puts pairs + occupy, 16 S + 32 bytes, in the same two
-// 128-byte lines for S = 10), and a run's update writes one pair and one 48-byte group.
+// Window state of a rule lives in one contiguous record of 8 x S + 12 int64, padded to an even number
+// of 64-byte units (rec_units: 12 units = 768 bytes for S = 10, so every record starts on a 128-byte line):
+//   header  [per bucket j: start, PASS] [occupy state: occupyCounter PASS, PASS_REQUEST, hasOccupied]
+//           [cache: the six other counters of one bucket] [cache tag: that bucket's start] [threshold]
+//   array   [per bucket j: WAITING, BLOCK, PASS_REQUEST, BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK]
+// The window sums read the dense vector of 16-byte pairs; for S = 10 the header is exactly two
+// 128-byte lines, so a cold rule's closed form (k_cold_fused) reads two lines: the pairs, the occupy
+// state, the current bucket's counters (the cache, valid while its tag equals that bucket's start) and
+// the rule's threshold (a copy of SlotParam::thr, written at every rule load by k_rec_thr).  The array
+// is authoritative and always written; the cache is only read by the closed forms, and a writer that
+// changes a bucket's array counters without refreshing the cache clears the tag (metric_add).
 constexpr int kOccWords = 4;  // SlotOcc inside the record
 static_assert(sizeof(SlotOcc) <= kOccWords * 8, "occupy state fits its words");
+constexpr int kCacheWords = 6;  // the cached counter group (array order)
+__host__ __device__ constexpr int rec_hdr_words(int S) { return 2 * S + kOccWords + kCacheWords + 2; }
+__host__ __device__ constexpr uint32_t rec_units(int S) {
+    return ((uint32_t)(8 * S + 12 + 7) / 8 + 1u) & ~1u;  // 64-byte units, even (128-byte aligned records)
+}
+static_assert(rec_hdr_words(10) == 32 && rec_units(10) == 12, "S = 10: a two-line header, 768-byte record");
 struct Rec {
     int64_t *r;
     int S;
     __device__ __forceinline__ int64_t &start(int j) const { return r[2 * j]; }
     __device__ __forceinline__ SlotOcc &occ() const { return *reinterpret_cast<SlotOcc *>(r + 2 * S); }
+    __device__ __forceinline__ int64_t *cache() const { return r + 2 * S + kOccWords; }
+    __device__ __forceinline__ int64_t &tag() const { return r[2 * S + kOccWords + kCacheWords]; }
+    __device__ __forceinline__ double &thr() const {
+        return *reinterpret_cast<double *>(r + 2 * S + kOccWords + kCacheWords + 1);
+    }
+    __device__ __forceinline__ int64_t *group(int j) const { return r + rec_hdr_words(S) + 6 * j; }
     __device__ __forceinline__ int64_t &cnt(int ev, int j) const {
         if (ev == CEV_PASS) return r[2 * j + 1];
-        if (ev == CEV_WAITING) return r[2 * S + kOccWords + 6 * j];
-        return r[2 * S + kOccWords + 6 * j + ev];  // BLOCK..OCCUPIED_BLOCK = ordinals 1..5
+        if (ev == CEV_WAITING) return group(j)[0];
+        return group(j)[ev];  // BLOCK..OCCUPIED_BLOCK = ordinals 1..5
     }
 };
 
@@ -100,7 +117,10 @@ __device__ __forceinline__ double get_avg(const ClusterState &st, const SlotPara
 __device__ __forceinline__ void metric_add(const ClusterState &st, const SlotParam &P, uint32_t s, int64_t t, int ev,
                                            int64_t n) {
     const WinRef w = cur_window(st, P, s, t);
-    if (!w.detached) rec_of(st, P).cnt(ev, w.j) += n;
+    if (w.detached) return;
+    const Rec R = rec_of(st, P);
+    R.cnt(ev, w.j) += n;
+    if (ev != CEV_PASS && R.tag() == R.start(w.j)) R.tag() = kAbsent;  // the cached group is stale now
 }
 
 // ClusterMetricLeapArray.getFirstCountOfWindow(PASS) = getValidHead(now).value().get(PASS)

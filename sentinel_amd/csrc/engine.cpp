@@ -2,6 +2,7 @@
 // mirror), device state ownership and the extern "C" ABI of include/sentinel_amd.h.
 #include "../../include/sentinel_amd.h"
 #include "cluster.hpp"
+#include "cluster_exact.hpp"  // the window record layout (rec_units)
 #include "concurrent.hpp"
 #include "flow.hpp"
 
@@ -550,7 +551,7 @@ struct Engine {
             p.ns = h.ns;
         }
         if (ns) SGA_HIP_CHECK(hipMemcpyAsync(d_param.p, hp.data(), ns * sizeof(SlotParam), hipMemcpyHostToDevice, stream));
-        // uniform geometry (ClusterState::uni_S): every allocated slot's record at slot * (S + 1) units
+        // uniform geometry (ClusterState::uni_S): every allocated slot's record at slot * rec_units(S) units
         uni_S = 0;
         {
             int32_t S0 = 0, W0 = 0, I0 = 0;
@@ -563,7 +564,7 @@ struct Engine {
                     W0 = p.W;
                     I0 = p.interval;
                 }
-                uni = p.S == S0 && p.W == W0 && p.interval == I0 && (uint64_t)p.boff == (uint64_t)i * (uint64_t)(S0 + 1);
+                uni = p.S == S0 && p.W == W0 && p.interval == I0 && (uint64_t)p.boff == (uint64_t)i * (uint64_t)sga::rec_units(S0);
             }
             static const bool no_uni = getenv("SGA_NO_UNI") && atoi(getenv("SGA_NO_UNI"));  // A/B knob
             if (uni && !no_uni && S0 > 0 && S0 <= 64) {
@@ -666,6 +667,8 @@ struct Engine {
             SGA_HIP_CHECK(hipMemcpyAsync(d_fresh.p, fresh.data(), fresh.size() * 4, hipMemcpyHostToDevice, stream));
             cluster_init_slots(state(), d_fresh.p, (uint32_t)fresh.size(), stream);
         }
+        // every record's copy of its threshold (the closed forms read it from the record's header)
+        if (ns) cluster_sync_rec_thr(state(), (uint32_t)ns, stream);
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
         ensure_scratch();
         // slots may have been freed or reused: forget the hot-rule set (the next batch re-chooses it)
@@ -855,7 +858,7 @@ int sga_load_cluster_flow_rules(sga_engine *e, const char *ns, const sga_cluster
             if (it == g.slot_of.end()) {  // putMetricIfAbsent -> new ClusterMetric(sampleCount, windowIntervalMs)
                 s = g.alloc_slot();
                 SlotHost &h = g.slots[s];
-                const uint32_t need = (uint32_t)r.sample_count + 1;  // buckets + the occupy state (64-byte units)
+                const uint32_t need = sga::rec_units(r.sample_count);  // the window record (64-byte units, cluster_exact.hpp)
                 if (h.bcap < need) {
                     h.boff = g.bucket_used;
                     h.bcap = need;

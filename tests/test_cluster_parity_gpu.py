@@ -216,6 +216,47 @@ def test_avg_local_threshold_and_reload(eng_mod):
     eng.close()
 
 
+@pytest.mark.parametrize("geometry", ["uniform", "mixed"])
+@pytest.mark.parametrize("clock", ["sorted", "regress"])
+def test_cold_partition_bit_exact(eng_mod, geometry, clock):
+    """The hot path's cold partition (rule slots from 2^15 up: one scatter pass into slot bins, each bin
+    ordered inside k_cold_fused's workgroup): 40k rules, Zipf-skewed traffic whose hot ids sit next to
+    each other in the slot space (uneven bins), acquire counts and prioritized requests mixed, with
+    mixed window geometries (per-rule parameter loads) or the uniform layout (the threshold from the
+    record header); "regress" sends batches whose clock goes back inside the batch, so the key pass
+    re-classifies every request as cold (the fallback) and single bins hold tens of thousands."""
+    c = eng_mod
+    rng = np.random.default_rng(11 if geometry == "uniform" else 12)
+    nr = 40_000
+    rules = random_rules(rng, nr, mixed_geometry=geometry == "mixed")
+    for r in rules:
+        r["count"] = float(rng.integers(1, 400))
+    oh = oracle_cluster({"default": rules})
+    eng = make_engine(c, hot="on", max_batch=1 << 18, max_rules=1 << 16)
+    engine_rules(c, eng, {"default": rules})
+    svc = c.DefaultTokenService(eng)
+    n = 1 << 18
+    t = T0
+    for b in range(4):
+        rank = np.minimum(rng.zipf(1.2, size=n), nr)
+        fid = rank.astype(np.int64)                     # hot ids adjacent in flowId (and slot) order
+        cold = rng.random(n) < 0.3
+        fid[cold] = rng.integers(1, nr + 1, size=int(cold.sum()))
+        acq = np.where(rng.random(n) < 0.95, 1, rng.integers(1, 4, size=n)).astype(np.int64)
+        prio = (rng.random(n) < 0.05).astype(np.uint8)
+        ts = t + np.sort(rng.integers(0, 400, size=n))
+        if clock == "regress" and b % 2 == 1:
+            k = rng.integers(1000, n - 1000)
+            ts[k:k + 500] -= 30                         # back in time inside the batch
+        t = int(ts.max()) + 1
+        g = svc.request_tokens(fid, acq, prio, ts)
+        o = oracle_replay(oh, fid, acq, prio, ts)
+        assert_same(g, o, fid, ts, f"{geometry}/{clock} batch {b}")
+    assert_metrics(c, eng, oh, list(range(1, 200)) + list(rng.integers(1, nr + 1, size=300)), t)
+    H.lib().orc_cluster_free(oh)
+    eng.close()
+
+
 @pytest.mark.parametrize("hot", ["on", "all"])
 def test_time_regression_and_gaps(eng_mod, hot):
     """Clock going backwards (detached windows) and long idle gaps."""
