@@ -66,8 +66,8 @@ def _cfg_c1(rng):
                 n_res=1, flow=[dict(resource=0, count=20.0)], batch=b, sample=n)
 
 
-def _cfg_c2(rng):
-    n_res, n = 100_000, 1 << 24
+def _cfg_c2(rng, n=1 << 24):
+    n_res = 100_000
     flow = []
     beh = rng.random(n_res)
     cnt = rng.integers(5, 5001, size=n_res)
@@ -198,7 +198,7 @@ class _Shard:
         self.n_ev = len(idx)
 
     def entries(self):
-        self.dec, _ = self.orc.replay(self.ent)
+        self.dec, self.wait = self.orc.replay(self.ent)
 
     def build_exits(self):
         b = self.b
@@ -244,6 +244,7 @@ def _cpu_local(cfg, b):
     m = min(cfg["sample"], b.n)
     one = _Shard(cfg, b, m, None)
     dt1 = _timed([one], "entries")
+    one_dec, one_wait = one.dec.copy(), one.wait.copy()
     one.build_exits()
     dt1 += _timed([one], "exits")
     n1 = one.n_ev
@@ -258,7 +259,7 @@ def _cpu_local(cfg, b):
     busy = sum(1 for sh in shards if len(sh.idx))
     for sh in shards:
         sh.close()
-    return {"value": max(m / dtn, m / dt1), "unit": "decisions/s", "cores": T, "kind": "port",
+    return one_dec, one_wait, {"value": max(m / dtn, m / dt1), "unit": "decisions/s", "cores": T, "kind": "port",
             "value_1thread": m / dt1, "value_threads": m / dtn, "events_per_s_1thread": n1 / dt1,
             "threads_with_work": busy,
             "sample": f"the first {m} entries of the batch and the exits of those that passed ({n1} events), "
@@ -315,8 +316,19 @@ def run_local(args, cfg_name):
             s.submit_device(x_kind, x_res, base, x_off, x_acq, flags=x_flags, rt=x_rt, param=x_param,
                             decision=x_dec, wait=None, stream=stream)
 
+    # the first step runs on a fresh engine, as the oracle's one-thread replay of the sample does: its
+    # decisions and waits of the sample's entries are kept for the parity check below
+    first = {}
+
+    def keep_first():
+        torch.cuda.synchronize(dev)
+        m = min(cfg["sample"], b.n)
+        first["dec"], first["wait"] = dec[:m].cpu().numpy(), wait[:m].cpu().numpy()
+
     for k in range(args.warmup):
         step(k)
+        if k == 0:
+            keep_first()
     torch.cuda.synchronize(dev)
     s.device_status()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -329,6 +341,8 @@ def run_local(args, cfg_name):
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     s.device_status()  # raises if a chunk was rejected or a parameter map filled
+    if not first:  # no warmup step: the first timed step was the fresh one (its arrays were overwritten since)
+        first = None
     gpu_s = ev0.elapsed_time(ev1) / 1e3
     d = dec.cpu().numpy()
     n_ent = b.n * args.steps
@@ -336,7 +350,17 @@ def run_local(args, cfg_name):
     e_in = E_PARAM_ENTRY if cfg.get("param") else E_ENTRY
     bytes_alg = n_ent * (e_in + E_DEC) + n_exit * E_EXIT + _state_bytes(cfg, b) * args.steps
     achieved = bytes_alg / gpu_s / 1e9
-    cpu = None if args.no_cpu else _cpu_local(cfg, b)
+    cpu, parity = None, None
+    if not args.no_cpu:
+        o_dec, o_wait, cpu = _cpu_local(cfg, b)
+        if first:
+            bad_d = int((first["dec"] != o_dec).sum())
+            bad_w = int((first["wait"] != o_wait).sum())
+            parity = {"entries": int(len(o_dec)), "decision_mismatches": bad_d, "wait_mismatches": bad_w,
+                      "what": "the first (fresh-engine) step's decisions and waits of the sample's entries against "
+                              "the C oracle's one-thread replay of the same entries (cpu_baseline's replay)"}
+            if bad_d or bad_w:
+                raise AssertionError(f"bench sample differs from the oracle: {parity}")
     eng.close()
     return {
         "metric": f"admission decisions/sec, config {cfg_name.upper()} (SURVEY.md 8(d)); % HBM peak",
@@ -352,6 +376,7 @@ def run_local(args, cfg_name):
                      "bytes_alg_per_step": bytes_alg / args.steps, "gpu_ms_per_step": gpu_s / args.steps * 1e3,
                      "lower_bound_bytes_per_step": (n_ent * (e_in + E_DEC) + n_exit * E_EXIT) / args.steps},
         "cpu_baseline": cpu,
+        "parity_sample": parity,
         "pass_fraction": float(((d == 0) | (d == 4)).mean()),
     }
 
@@ -387,13 +412,19 @@ def run_rls(args):
     def step(k):
         out["r"] = svc.should_rate_limit_device(d_off, d_fid, d_hits, T0 + k * span, d_ts, stream=stream)
 
-    for k in range(args.warmup):
+    first = {}  # the fresh engine's first step, per descriptor: status and remaining (the parity check below)
+    for k in range(max(1, args.warmup)):
         step(k)
+        if k == 0:
+            torch.cuda.synchronize(dev)
+            first["st"] = out["r"][1].cpu().numpy().astype(np.int32)
+            first["rem"] = out["r"][2].cpu().numpy()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for k in range(args.warmup, args.warmup + args.steps):
+    w0 = max(1, args.warmup)
+    for k in range(w0, w0 + args.steps):
         step(k)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
@@ -404,7 +435,7 @@ def run_rls(args):
     bytes_alg = (nd * (E_RLS_IN + E_RLS_OUT) + 2 * touched * S_RLS) * args.steps
     achieved = bytes_alg / gpu_s / 1e9
     eng.close()
-    cpu = None
+    cpu, parity = None, None
     if not args.no_cpu:
         L = H.lib()
         oh = L.orc_cluster_new(1.0, 1.0)
@@ -420,6 +451,13 @@ def run_rls(args):
         L.orc_cluster_replay_simple(oh, m, f_s.ctypes.data, a_s.ctypes.data, dts.ctypes.data, res)
         dt = time.perf_counter() - t0
         L.orc_cluster_free(oh)
+        ores = np.frombuffer(res, dtype=np.int32).reshape(m, 3)
+        parity = {"descriptors": int(m), "status_mismatches": int((first["st"][:m] != ores[:, 0]).sum()),
+                  "remaining_mismatches": int((first["rem"][:m] != ores[:, 1]).sum()),
+                  "what": "the first (fresh-engine) step's status and remaining of the sample's descriptors against "
+                          "the C oracle's one-thread SimpleClusterFlowChecker replay (cpu_baseline's replay)"}
+        if parity["status_mismatches"] or parity["remaining_mismatches"]:
+            raise AssertionError(f"bench sample differs from the oracle: {parity}")
         # T threads over disjoint flowId subsets (one oracle each, rules independent)
         import threading
         T = _threads()
@@ -462,6 +500,7 @@ def run_rls(args):
                      "kernel": "sga_rls_should_rate_limit_device pipeline, torch events on its stream",
                      "bytes_alg_per_step": bytes_alg / args.steps, "gpu_ms_per_step": gpu_s / args.steps * 1e3},
         "cpu_baseline": cpu,
+        "parity_sample": parity,
         "over_limit_fraction": float((code == 2).mean()),
     }
 

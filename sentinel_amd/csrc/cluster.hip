@@ -28,6 +28,7 @@
 #include <cstdlib>
 
 #include <algorithm>
+#include <type_traits>
 
 namespace sga {
 
@@ -528,6 +529,12 @@ struct RunIn {
 // -- the (start, PASS) pairs, the occupy state, the cached counter group with its tag and the
 // threshold -- so the rule's later runs issue no record loads (one memory round trip per rule
 // instead of one per run).  have = false: load from the record.
+#ifndef SGA_CARRY_PAIRS
+#define SGA_CARRY_PAIRS 0
+#endif
+// 1: later runs of a rule take the pairs from registers (64 more VGPRs live across runs: two waves per
+// SIMD); 0: they reload the header (an L2 hit: the lane just wrote it), and the kernel fits three
+constexpr bool kCarryPairs = SGA_CARRY_PAIRS;
 template <int kMaxPairs>
 struct RecCarry {
     int4 sp[kMaxPairs > 0 ? kMaxPairs : 1];
@@ -543,6 +550,14 @@ __device__ __forceinline__ double f64_hi(const int4 &v) { return __longlong_as_d
 // request is past the passing prefix).  kMaxPairs = 0: sampleCount above the register form, the
 // pairs are loaded one by one every run.  hdr_thr: the threshold is the record's copy (Rec::thr),
 // not thr_in (which the caller then did not load).
+#ifndef SGA_SKIP_GROUP
+#define SGA_SKIP_GROUP 0
+#endif
+constexpr bool kSkipGroup = SGA_SKIP_GROUP;  // profiling builds only (the array group then goes stale)
+#ifndef SGA_HDR_CACHE_ALL
+#define SGA_HDR_CACHE_ALL 0
+#endif
+constexpr bool kHdrCacheAll = SGA_HDR_CACHE_ALL;  // 1: every cold run rewrites the header's counter cache
 template <class PrioBefore, int kMaxPairs>
 __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam &P, const Rec &R, double thr_in,
                                          bool hdr_thr, int64_t qbase, const RunIn &ri, PrioBefore prio_before,
@@ -612,7 +627,8 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
     if (ri.cp_tot > 0 && (P.S <= 1 || 1000 / P.S <= 0)) return false;
     const bool rot = old == kAbsent || ws > old;
     int4 c01 = rc.cg[0], c23 = rc.cg[1], c45 = rc.cg[2];
-    if (!rot && i64_lo(rc.meta) != old) {  // the current bucket's counters are not the cached group: the array
+    const bool tag_was_cur = i64_lo(rc.meta) == old;
+    if (!rot && !tag_was_cur) {  // the current bucket's counters are not the cached group: the array
         const int4 *cv = reinterpret_cast<const int4 *>(R.group(cj));
         c01 = cv[0];
         c23 = cv[1];
@@ -726,13 +742,20 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
         rc.meta.y = (int)(uint32_t)((uint64_t)stv >> 32);
         int4 *cg = reinterpret_cast<int4 *>(R.group(cj));  // the array (authoritative) and the header's cache
         int4 *ch = reinterpret_cast<int4 *>(R.cache());
-        cg[0] = rc.cg[0];
-        cg[1] = rc.cg[1];
-        cg[2] = rc.cg[2];
-        ch[0] = rc.cg[0];
-        ch[1] = rc.cg[1];
-        ch[2] = rc.cg[2];
-        ch[3] = rc.meta;
+        if (!kSkipGroup) {
+            cg[0] = rc.cg[0];
+            cg[1] = rc.cg[1];
+            cg[2] = rc.cg[2];
+        }
+        // the header's cache: written when it must stay coherent (it already held this bucket) or when it is
+        // the policy (kHdrCacheAll); otherwise left alone -- its tag then names another bucket, and the run
+        // saves the partial write of the header's second line
+        if (kHdrCacheAll || (!rot && tag_was_cur)) {
+            ch[0] = rc.cg[0];
+            ch[1] = rc.cg[1];
+            ch[2] = rc.cg[2];
+            ch[3] = rc.meta;
+        }
         if (occ_dirty) {
             rc.o0 = i4(o.occ_pass, o.occ_preq);
             rc.o1 = make_int4(o.has_occ, o.pad, rc.o1.z, rc.o1.w);  // the spare word stored back unchanged
@@ -746,7 +769,7 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
             for (int jj = 0; jj < kMaxPairs; ++jj)
                 if (jj == cj) rc.sp[jj] = np;
         }
-        rc.have = kMaxPairs > 0;
+        rc.have = kCarryPairs && kMaxPairs > 0;
     }
     ro.s0 = s0;
     ro.thr = thr;
@@ -863,7 +886,9 @@ __global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const 
 // that continues past the chunk use global run arrays), run decisions in global scratch written
 // and read by the same workgroup.  Elements with a slot >= nkey (invalid requests, prioritized hot
 // requests) end the data.
-constexpr int kFzThreads = 256, kFzPer = 8, kFzChunk = kFzThreads * kFzPer;  // 2048
+// kFzChunk: elements per workgroup in chunk mode (and the run records kept in LDS); the runs / results scans
+// walk blocks of kFzBlk elements, kFzPer per thread
+constexpr int kFzThreads = 256, kFzPer = 4, kFzBlk = kFzThreads * kFzPer, kFzChunk = 2048;
 constexpr int kFzShortRun = 4;  // closed-form runs of at most this many requests: results from the flows lane
 
 // Profiling only (SGA_FZ_DEBUG bit 16): per-phase cycles of k_cold_fused summed over workgroups.
@@ -955,7 +980,7 @@ __device__ __forceinline__ uint64_t match_lanes(uint32_t d, int bits, bool valid
     }
     return peers;
 }
-constexpr int kBinLds = 3072;  // k_cold_fused bin mode: bins of at most this many elements are ordered in LDS
+constexpr int kBinLds = 2560;  // k_cold_fused bin mode: bins of at most this many elements are ordered in LDS
 constexpr int kBoRounds = 12;  // bin_order: rounds of 64 elements a wave holds in registers (bins of ~3k in one go)
 // The ordered bin goes to es[pos - ebase] (es: the workgroup's LDS image of a bin that fits, ebase = B0, or
 // the global element buffer, ebase = 0).
@@ -1054,7 +1079,7 @@ enum : int { kFzAll = 0, kFzBin = 1 };
 // it); kFzBin: one workgroup per partition bin (el = the partition output; the bin is ordered into
 // es first, and every rule of the bin is the workgroup's).
 template <int kMode>
-__global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, BatchScratch sc,
+__global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_cold_fused_t(ClusterState st, BatchScratch sc,
                                                              const uint64_t *__restrict__ el_in, uint32_t nhost,
                                                              const uint32_t *__restrict__ dn, uint32_t nkey,
                                                              const int32_t *__restrict__ acquire,
@@ -1062,20 +1087,30 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
                                                              const uint32_t *__restrict__ ts_off, int64_t ts_base,
                                                              int simple, uint32_t hot_min, uint64_t *__restrict__ out,
                                                              int dbg, uint64_t *__restrict__ es, int lb) {
-    __shared__ uint32_t fheads[kFzChunk + 1], fslot[kFzChunk + 1];  // owned rules: first position, slot
-    // run records of the runs that start in [h0, h0 + kFzChunk) (every run but the later runs of
-    // a rule that continues past the chunk, which use the global run arrays): length,
-    // prioritized count, first prioritized index, acquire count | bucket delta << 8
-    __shared__ uint32_t rl_buf[4 * kFzChunk];
-    uint32_t *rl_n = rl_buf, *rl_cp = rl_buf + kFzChunk, *rl_p0 = rl_buf + 2 * kFzChunk, *rl_ab = rl_buf + 3 * kFzChunk;
-    __shared__ uint8_t rl_done[kFzChunk];  // short closed-form runs answered by their flows lane
+    // Chunk mode keeps u32 run records for kFzChunk head positions; bin mode, sized for three workgroups
+    // per CU (<= 53 KB of LDS each), keeps u16 records for the kBinLds positions of a bin that fits in
+    // LDS (lengths, counts and the plist offset relative to h0 are then below 2^16) and none for a larger
+    // bin (every run in the global run arrays).
+    constexpr bool kBin = kMode == kFzBin;
+    constexpr int kRl = kBin ? kBinLds : kFzChunk;           // run-record capacity (head positions)
+    constexpr int kRules = kBin ? (1 << kPartMaxLow) : kFzChunk;  // rules per workgroup at most
+    using RlT = typename std::conditional<kBin, uint16_t, uint32_t>::type;
+    __shared__ uint32_t fheads[kRules + 1], fslot[kRules + 1];  // owned rules: first position, slot
+    // run records of the runs that start in [h0, h0 + rl_cap): length, prioritized count, first
+    // prioritized index (relative to h0 in bin mode), acquire count | bucket delta << 8
+    __shared__ RlT rl_buf[4 * kRl];
+    RlT *rl_n = rl_buf, *rl_cp = rl_buf + kRl, *rl_p0 = rl_buf + 2 * kRl, *rl_ab = rl_buf + 3 * kRl;
+    __shared__ uint8_t rl_done[kRl];  // short closed-form runs answered by their flows lane
     __shared__ FAgg wtot[kFzThreads / 64];
     __shared__ uint32_t s_h0, s_E, s_wcnt[kFzThreads / 64];
     __shared__ uint32_t s_ncand, s_cbase, s_next, s_cand[2 * kFzThreads];
     // bin mode: the ordered bin, when it fits, stays in LDS (every later element read is an LDS read
     // through a flat pointer); a larger bin is ordered into the global buffer es
-    __shared__ uint64_t sel[kMode == kFzBin ? kBinLds : 1];
-    static_assert((kFzThreads / 64) << kPartMaxLow <= 4 * kFzChunk, "bin_order's digit counts fit the run records");
+    __shared__ uint64_t sel[kBin ? kBinLds : 1];
+    static_assert(!kBin || sizeof(rl_buf) >= (size_t)((kFzThreads / 64) << kPartMaxLow) * 4,
+                  "bin_order's digit counts fit the run records");
+    uint32_t rl_cap = kRl;  // head positions [h0, h0 + rl_cap) keep their run record in LDS
+    uint32_t p0_rel = 0;    // bin mode: rl_p0 holds plist index - h0
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t *el = el_in;
     uint32_t h0, E;
@@ -1085,7 +1120,9 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
         unsigned long long ot = 0;
         fz_mark(dbg, 0, ot);
         const bool in_lds = B1 - B0 <= (uint32_t)kBinLds && !(dbg & 64);
-        bin_order(el_in, in_lds ? sel : es, in_lds ? B0 : 0u, B0, B1, lb, rl_buf, s_wcnt);
+        bin_order(el_in, in_lds ? sel : es, in_lds ? B0 : 0u, B0, B1, lb, reinterpret_cast<uint32_t *>(rl_buf), s_wcnt);
+        rl_cap = in_lds ? (uint32_t)kBinLds : 0u;
+        p0_rel = B0;
         fz_mark(dbg, 4, ot);
         // element p of the bin at el[p]: the LDS image shifted by the bin start (a flat address)
         el = in_lds ? reinterpret_cast<const uint64_t *>(reinterpret_cast<uintptr_t>(&sel[0]) - (uintptr_t)B0 * 8u) : es;
@@ -1152,10 +1189,10 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
     }
     unsigned long long fzt = 0;
     fz_mark(dbg, 0, fzt);
-    // ---- 1 runs (blocks of kFzChunk elements over [h0, E))
+    // ---- 1 runs (blocks of kFzBlk elements over [h0, E))
     FAgg carry = fagg_id();
     uint32_t nf_carry = 0;
-    for (uint32_t b0 = h0; b0 < E; b0 += kFzChunk) {
+    for (uint32_t b0 = h0; b0 < E; b0 += kFzBlk) {
         const uint32_t e0 = b0 + threadIdx.x * kFzPer;
         uint64_t x[kFzPer];
 #pragma unroll
@@ -1213,11 +1250,11 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
                 const uint32_t head = run.hpos - 1;
                 const int32_t acq = run.mn == run.mx ? run.mn : 0;  // 0: mixed or escaped -> replay
                 const uint32_t bd = (uint32_t)((x[k] >> kBdShift) & kBdEsc);
-                if (head - h0 < (uint32_t)kFzChunk) {
-                    rl_n[head - h0] = p + 1 - head;
-                    rl_cp[head - h0] = run.np - run.hp;
-                    rl_p0[head - h0] = h0 + run.hp;
-                    rl_ab[head - h0] = (uint32_t)acq | (bd << 8);
+                if (head - h0 < rl_cap) {
+                    rl_n[head - h0] = (RlT)(p + 1 - head);
+                    rl_cp[head - h0] = (RlT)(run.np - run.hp);
+                    rl_p0[head - h0] = (RlT)(h0 + run.hp - p0_rel);
+                    rl_ab[head - h0] = (RlT)((uint32_t)acq | (bd << 8));
                     rl_done[head - h0] = 0;
                 } else {  // global run arrays, indexed by head position
                     sc.run_start[head] = p + 1 - head;
@@ -1292,10 +1329,10 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
     while (live) {
         RunIn ri;
         ri.j0 = r;
-        if (r - h0 < (uint32_t)kFzChunk) {
+        if (r - h0 < rl_cap) {
             ri.n = rl_n[r - h0];
             ri.cp_tot = rl_cp[r - h0];
-            ri.p0 = rl_p0[r - h0];
+            ri.p0 = (uint32_t)rl_p0[r - h0] + p0_rel;
             const uint32_t ab = rl_ab[r - h0];
             ri.a = (int32_t)(ab & 0xFFu);
             ri.bd = ab >> 8;
@@ -1347,7 +1384,7 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
             ro.mode = RUN_DONE;
             rc.have = false;  // the record changed in memory
         }
-        if (fast && ri.n <= (uint32_t)kFzShortRun && r - h0 < (uint32_t)kFzChunk) {
+        if (fast && ri.n <= (uint32_t)kFzShortRun && r - h0 < rl_cap) {
             // a short run's TokenResults from its flows lane (the results phase skips it): the run's elements
             // loaded together at clamped positions, decided as the results phase would
             uint64_t x[kFzShortRun];
@@ -1367,7 +1404,7 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
                 } else {
                     res = pack_result(TRS_BLOCKED, 0, 0);
                 }
-                out[el_idx(x[u])] = res;
+                if (!(dbg & 128)) out[el_idx(x[u])] = res;
                 kp += pr;
             }
             rl_done[r - h0] = 1;
@@ -1395,7 +1432,7 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
     }
     // ---- 3 results (the scan again)
     carry = fagg_id();
-    for (uint32_t b0 = h0; b0 < ((dbg & 2) ? h0 : E); b0 += kFzChunk) {
+    for (uint32_t b0 = h0; b0 < ((dbg & 2) ? h0 : E); b0 += kFzBlk) {
         const uint32_t e0 = b0 + threadIdx.x * kFzPer;
         uint64_t x[kFzPer];
 #pragma unroll
@@ -1428,7 +1465,7 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
         RunOut ro[kFzPer];
 #pragma unroll
         for (int k = 0; k < kFzPer; ++k) {
-            const bool done = head[k] - h0 < (uint32_t)kFzChunk && rl_done[head[k] - h0];
+            const bool done = head[k] - h0 < rl_cap && rl_done[head[k] - h0];
             if (done) ro[k].mode = RUN_DONE;
             else if (e0 + k < E && (k == 0 || head[k] != head[k - 1])) ro[k] = sc.run_out[head[k]];
             else if (k > 0) ro[k] = ro[k - 1];
@@ -1448,7 +1485,7 @@ __global__ __launch_bounds__(kFzThreads) void k_cold_fused_t(ClusterState st, Ba
             } else {
                 res = pack_result(TRS_BLOCKED, 0, 0);
             }
-            out[el_idx(x[k])] = res;
+            if (!(dbg & 128)) out[el_idx(x[k])] = res;
         }
         carry = fagg_combine(carry, tot);
         __syncthreads();

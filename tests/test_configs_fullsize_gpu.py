@@ -121,6 +121,50 @@ def test_c2_100k_mixed_controllers_zipf():
     assert (d[ent] == 0).any() and (d[ent] == 1).any() and (st["kind"] == 1).sum() > 100_000
 
 
+def test_c2_bench_mix_bit_exact():
+    """bench.py --config c2's own mix (bench_local._cfg_c2): count U{5..5000} -- RateLimiter rules above
+    2000 QPS pace acquire-1 entries at zero cost in k_lwave --, lambda 10^7 entries per virtual second,
+    WarmUp 10 s, maxQueueingTimeMs 500, 5 % acquiring 2..5, at 2^22 entries per batch.  As the bench does:
+    one batch of entries, then the exits of the entries that passed (exit time = entry time + a geometric
+    RT), on the engine and on the oracle; every decision and wait equal, then the metric rows and the
+    hottest nodes."""
+    import bench_local as bl
+    rng = np.random.default_rng(102)
+    cfg = bl._cfg_c2(rng, n=1 << 22)
+    b = cfg["batch"]
+    n_res, flow = cfg["n_res"], cfg["flow"]
+    ent = {"kind": np.zeros(b.n, np.uint8), "resource": b.res, "ts": b.ts, "acquire": b.acq, "flags": b.flags,
+           "rt": np.zeros(b.n, np.int64), "param": b.param}
+    orc = lt.Oracle(n_res, flow)
+    exp_d, exp_w = orc.replay({k: np.ascontiguousarray(v) for k, v in ent.items()})
+    eng, s = _local(n_res, flow, max_batch=b.n)
+    d, w = s.submit(ent["kind"], ent["resource"], ent["ts"], ent["acquire"], ent["flags"], ent["rt"], ent["param"])
+    bad = np.nonzero((d != exp_d) | (w != exp_w))[0]
+    assert len(bad) == 0, (f"{len(bad)} of {b.n} entries differ; first at {bad[0]}: res={b.res[bad[0]]} "
+                           f"gpu=({d[bad[0]]},{w[bad[0]]}) oracle=({exp_d[bad[0]]},{exp_w[bad[0]]})")
+    rl0 = [r["resource"] for r in flow if r.get("control_behavior") == 2 and r["count"] > 2000]
+    assert np.isin(b.res, rl0).sum() > 10_000  # the zero-cost pacing path saw real traffic
+    passed = (exp_d == 0) | (exp_d == 4)
+    k = np.nonzero(passed[b.exit_of])[0]  # exits in exit-time order, of the entries that passed
+    e = b.exit_of[k]
+    ex = {"kind": np.ones(len(k), np.uint8), "resource": b.res[e], "ts": b.exit_ts[k], "acquire": b.acq[e],
+          "flags": b.exit_flags[k], "rt": b.exit_rt[k], "param": b.param[e]}
+    ex = {k: np.ascontiguousarray(v) for k, v in ex.items()}
+    exp_xd, _ = orc.replay(ex)
+    xd, _ = s.submit(ex["kind"], ex["resource"], ex["ts"], ex["acquire"], ex["flags"], ex["rt"], ex["param"])
+    assert (xd == exp_xd).all()
+    now = int(max(b.ts.max(), ex["ts"].max())) + 1
+    got = [(m.timestamp, s.resource_id(m.resource), m.pass_qps, m.block_qps, m.success_qps, m.exception_qps, m.rt,
+            m.occupied_pass_qps) for m in s.metrics(now, cap=1 << 20)]
+    assert got == orc.metrics(now, cap=1 << 20)
+    hot = np.argsort(-np.bincount(b.res.astype(np.int64), minlength=n_res))[:64]
+    for rid in hot:
+        v = s.node(int(rid), now)
+        assert [getattr(v, g) for g in lt.NODE_GETTERS] == orc.node(int(rid), now), int(rid)
+    orc.close()
+    eng.close()
+
+
 def test_c4_10k_param_rules_pinned():
     rng = np.random.default_rng(104)
     n_res, n = 10_000, 1 << 22

@@ -240,13 +240,15 @@ def test_pacing_heavy_resources(seed, regress):
     """RateLimiterController-only resources with thousands of entries per batch go to k_lwave (one wave
     per resource, a ballot finds each window's next passing entry); acquire 1..3 (cost differs per
     entry), queues of 0 / 20 / 500 ms, a zero-count rule (every entry blocks), exits interleaved, and
-    clock regressions (those runs take the per-event chain)."""
+    clock regressions (those runs take the per-event chain).  Resource 5 is above 2000 QPS: its acquire-1
+    entries cost Math.round(1000 / 2500.0) = 0 ms, the zero-cost pacing of C2's bench mix."""
     n_res = 6
     flow = [{"resource": 0, "count": 50.0, "control_behavior": 2, "max_queueing_time_ms": 500},
             {"resource": 1, "count": 7.5, "control_behavior": 2, "max_queueing_time_ms": 20},
             {"resource": 2, "count": 200.0, "control_behavior": 2, "max_queueing_time_ms": 0},
             {"resource": 3, "count": 0.0, "control_behavior": 2, "max_queueing_time_ms": 100},
-            {"resource": 4, "count": 1000.0, "control_behavior": 2, "max_queueing_time_ms": 500}]
+            {"resource": 4, "count": 1000.0, "control_behavior": 2, "max_queueing_time_ms": 500},
+            {"resource": 5, "count": 2500.0, "control_behavior": 2, "max_queueing_time_ms": 500}]
     _run(n_res, flow=flow, max_batch=1 << 15, n_entries=40000, seed=seed, gap_mean=0.05, acq_max=3, rt_max=20,
          err_pct=0.05, regress_pct=regress)
 
