@@ -63,7 +63,7 @@ def _cfg_c1(rng):
     ts = T0 + np.arange(n) // 20  # lambda = 20 events / ms, 50 virtual s
     b = Batch(np.zeros(n), ts, exit_rt=rng.integers(0, 6, size=n))
     return dict(name="C1 HelloWorld: 1 FlowRule QPS 20 DefaultController, 1M entries + exits",
-                n_res=1, flow=[dict(resource=0, count=20.0)], batch=b, sample=n)
+                n_res=1, flow=[dict(resource=0, count=20.0)], batch=b, sample=n, contended=True)
 
 
 def _cfg_c2(rng, n=1 << 24):
@@ -235,6 +235,33 @@ def _timed(shards, fn):
     return time.perf_counter() - t0
 
 
+def _cpu_contended_hello(cfg, b, m, T, passed):
+    """C1 with T threads sharing the one resource (oracle/oracle_contended.c: StatisticNode over LongAdder cells,
+    LeapArray's CAS / updateLock rotation, DefaultController.canPass): the sample's entries and the exits of the
+    single-threaded replay's passes, event i on thread i mod T."""
+    import ctypes as C
+    from tests import oracle_harness as H
+    L = H.lib()
+    fn = L.orc_contended_hello
+    fn.restype = C.c_double
+    fn.argtypes = [C.c_int, C.c_double, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    kind = np.zeros(m, np.uint8)
+    ts, rt = np.ascontiguousarray(b.ts[:m], np.int64), np.zeros(m, np.int64)
+    if b.exit_of is not None:  # exits of the sample's passed entries (one-thread replay), merged in time order
+        sel = b.exit_of[b.exit_of < m]
+        sel = sel[passed[sel]]
+        pos = np.argsort(np.concatenate([b.ts[:m], b.ts[sel] + b.exit_rt[np.argsort(b.exit_of)][sel]]), kind="stable")
+        kind = np.concatenate([kind, np.ones(len(sel), np.uint8)])[pos]
+        rt = np.concatenate([rt, b.exit_rt[np.argsort(b.exit_of)][sel]])[pos]
+        ts = np.concatenate([ts, b.ts[sel] + b.exit_rt[np.argsort(b.exit_of)][sel]])[pos]
+    kind, ts, rt = (np.ascontiguousarray(x) for x in (kind, ts.astype(np.int64), rt.astype(np.int64)))
+    dt = fn(T, float(cfg["flow"][0]["count"]), len(kind), kind.ctypes.data, ts.ctypes.data, rt.ctypes.data, None)
+    return {"value_contended": m / dt, "events_contended": int(len(kind)),
+            "contended": f"{T} threads on the one resource (oracle/oracle_contended.c: LongAdder cells, CAS / "
+                         f"updateLock window rotation), the sample's {m} entries and their exits, event i on thread "
+                         f"i mod {T}; value_contended counts entries"}
+
+
 def _cpu_local(cfg, b):
     """The C oracle on the host: one thread replaying the first `sample` entries (then their exits, masked by
     its own decisions as the GPU masks by its decisions), and T threads over disjoint resource subsets
@@ -259,9 +286,13 @@ def _cpu_local(cfg, b):
     busy = sum(1 for sh in shards if len(sh.idx))
     for sh in shards:
         sh.close()
-    return one_dec, one_wait, {"value": max(m / dtn, m / dt1), "unit": "decisions/s", "cores": T, "kind": "port",
+    extra = {}
+    if cfg.get("contended"):  # C1: the reference's own concurrency design on one shared resource
+        extra = _cpu_contended_hello(cfg, b, m, T, (one_dec == 0) | (one_dec == 4))
+    return one_dec, one_wait, {"value": max(m / dtn, m / dt1, extra.get("value_contended", 0.0)),
+            "unit": "decisions/s", "cores": T, "kind": "port",
             "value_1thread": m / dt1, "value_threads": m / dtn, "events_per_s_1thread": n1 / dt1,
-            "threads_with_work": busy,
+            "threads_with_work": busy, **extra,
             "sample": f"the first {m} entries of the batch and the exits of those that passed ({n1} events), "
                       f"replayed by the C oracle (oracle/ slot-chain restatement): {T} threads over disjoint "
                       f"resource subsets (resource mod {T}; {busy} with events), value_1thread = one thread in "

@@ -455,6 +455,10 @@ typedef struct sga_node_view {
     int64_t total_pass, total_block, total_success, total_exception;  /* minute window */
     int64_t cur_thread_num;
     int64_t waiting;                                                /* borrowed (occupied) tokens */
+    double max_success_qps;     /* StatisticNode.maxSuccessQps (StatisticNode.java:225-230): max bucket success
+                                 * of the second window (>= 1) x sampleCount / intervalInSec */
+    double previous_block_qps;  /* StatisticNode.previousBlockQps (StatisticNode.java:180-182): the minute
+                                 * window's previous bucket's block count */
 } sga_node_view;
 
 int sga_flow_set_resources(sga_engine *e, uint32_t n_resources);

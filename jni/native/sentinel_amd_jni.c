@@ -312,13 +312,13 @@ JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_setClusterSer
 /* GpuNode: d8 / l6 as sgaj_query_node */
 JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_queryNode(JNIEnv *env, jclass cls, jlong h,
                                                                             jint resource, jlong now_ms,
-                                                                            jdoubleArray d8, jlongArray l6) {
+                                                                            jdoubleArray d10, jlongArray l6) {
     (void)cls;
-    double d[8];
+    double d[10];
     int64_t l[6];
     const int rc = sgaj_query_node(ENGINE(h), (uint32_t)resource, now_ms, d, l);
     if (rc == SGA_OK) {
-        (*env)->SetDoubleArrayRegion(env, d8, 0, 8, (const jdouble *)d);
+        (*env)->SetDoubleArrayRegion(env, d10, 0, 10, (const jdouble *)d);
         (*env)->SetLongArrayRegion(env, l6, 0, 6, (const jlong *)l);
     }
     return rc;

@@ -251,7 +251,7 @@ int sgaj_set_namespace_limit(sga_engine *e, const char *ns, double max_qps) {
 
 int sgaj_set_cluster_server(sga_engine *e, int32_t mode) { return sga_set_cluster_server(e, mode); }
 
-int sgaj_query_node(sga_engine *e, uint32_t resource, int64_t now_ms, double d8[8], int64_t l6[6]) {
+int sgaj_query_node(sga_engine *e, uint32_t resource, int64_t now_ms, double d8[10], int64_t l6[6]) {
     sga_node_view v;
     const int rc = sga_query_node(e, resource, now_ms, &v);
     if (rc != SGA_OK) return rc;
@@ -263,6 +263,8 @@ int sgaj_query_node(sga_engine *e, uint32_t resource, int64_t now_ms, double d8[
     d8[5] = v.avg_rt;
     d8[6] = v.min_rt;
     d8[7] = v.previous_pass_qps;
+    d8[8] = v.max_success_qps;
+    d8[9] = v.previous_block_qps;
     l6[0] = v.total_pass;
     l6[1] = v.total_block;
     l6[2] = v.total_success;

@@ -88,9 +88,10 @@ int sgaj_set_namespace_limit(sga_engine *e, const char *ns, double max_qps);
 /* ClusterStateManager: 1 embedded token server (cluster-mode rules decided by this engine), 0 none. */
 int sgaj_set_cluster_server(sga_engine *e, int32_t mode);
 /* Node getters (Node.java:40-203) of a resource's ClusterNode at now_ms (reads rotate windows):
- * d8 = {passQps, blockQps, successQps, exceptionQps, occupiedPassQps, avgRt, minRt, previousPassQps},
+ * d10 = {passQps, blockQps, successQps, exceptionQps, occupiedPassQps, avgRt, minRt, previousPassQps,
+ *        maxSuccessQps, previousBlockQps},
  * l6 = {totalPass, totalBlock, totalSuccess, totalException, curThreadNum, waiting}. */
-int sgaj_query_node(sga_engine *e, uint32_t resource, int64_t now_ms, double d8[8], int64_t l6[6]);
+int sgaj_query_node(sga_engine *e, uint32_t resource, int64_t now_ms, double d10[10], int64_t l6[6]);
 /* StatisticNode.metrics() of every resource (MetricTimerListener.run's input): up to cap rows of 8
  * longs {timestamp, resource, pass, block, success, exception, rt, occupiedPass}; *n rows written. */
 int sgaj_metrics_snapshot(sga_engine *e, int64_t now_ms, int64_t *rows8, size_t cap, size_t *n);

@@ -136,11 +136,11 @@ public final class GpuEngine {
     static native int setClusterServer(long engine, int mode);
 
     /**
-     * Node getters of a resource's ClusterNode at nowMs: d8 = {passQps, blockQps, successQps, exceptionQps,
-     * occupiedPassQps, avgRt, minRt, previousPassQps}, l6 = {totalPass, totalBlock, totalSuccess, totalException,
-     * curThreadNum, waiting}.
+     * Node getters of a resource's ClusterNode at nowMs: d10 = {passQps, blockQps, successQps, exceptionQps,
+     * occupiedPassQps, avgRt, minRt, previousPassQps, maxSuccessQps, previousBlockQps}, l6 = {totalPass, totalBlock,
+     * totalSuccess, totalException, curThreadNum, waiting}.
      */
-    static native int queryNode(long engine, int resource, long nowMs, double[] d8, long[] l6);
+    static native int queryNode(long engine, int resource, long nowMs, double[] d10, long[] l6);
 
     /**
      * StatisticNode.metrics() of every resource: rows of 8 longs {timestamp, resource, pass, block, success,

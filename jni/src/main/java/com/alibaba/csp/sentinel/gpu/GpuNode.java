@@ -35,7 +35,7 @@ public final class GpuNode implements Node {
     }
 
     private static final class View {
-        final double[] d = new double[8];
+        final double[] d = new double[10];
         final long[] l = new long[6];
     }
 
@@ -66,14 +66,10 @@ public final class GpuNode implements Node {
     @Override public long waiting() { return view().l[5]; }
 
     @Override
-    public double maxSuccessQps() {
-        throw new UnsupportedOperationException("maxSuccessQps: not in the engine's node view");
-    }
+    public double maxSuccessQps() { return view().d[8]; }
 
     @Override
-    public double previousBlockQps() {
-        throw new UnsupportedOperationException("previousBlockQps: not in the engine's node view");
-    }
+    public double previousBlockQps() { return view().d[9]; }
 
     /** StatisticNode.metrics() of this node: the engine's snapshot (it advances every node's lastFetchTime). */
     @Override

@@ -330,6 +330,13 @@ double orc_node_previous_pass_qps(orc_node *n, int64_t now) {
     obucket *w = leap_previous(n->minute, now, now);
     return w ? (double)w->c[ORC_EV_PASS] : 0.0;
 }
+/* StatisticNode.previousBlockQps -> ArrayMetric.previousWindowBlock, StatisticNode.java:180-182,
+ * ArrayMetric.java:273-280 */
+double orc_node_previous_block_qps(orc_node *n, int64_t now) {
+    leap_current(n->minute, now);
+    obucket *w = leap_previous(n->minute, now, now);
+    return w ? (double)w->c[ORC_EV_BLOCK] : 0.0;
+}
 /* StatisticNode.avgRt, StatisticNode.java:238-245 */
 double orc_node_avg_rt(orc_node *n, int64_t now) {
     int64_t success = am_sum(n->second, now, ORC_EV_SUCCESS);

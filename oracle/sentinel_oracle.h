@@ -172,6 +172,7 @@ size_t orc_node_metrics(orc_node *n, int64_t now, uint32_t resource, orc_metric_
 size_t orc_flow_metrics(orc_flow *f, int64_t now, orc_metric_node *out, size_t cap);
 #define ORC_ENTRY_NODE 0xFFFFFFFFu /* resource id of Constants.ENTRY_NODE in metric rows and node queries */
 double orc_node_max_success_qps(orc_node *n, int64_t now);
+double orc_node_previous_block_qps(orc_node *n, int64_t now);
 
 /* ---- cluster token server (CS/flow) ---------------------------------------- */
 typedef struct orc_cluster_rule {

@@ -93,7 +93,8 @@ class SgaNodeView(C.Structure):
                 ("exception_qps", C.c_double), ("occupied_pass_qps", C.c_double), ("avg_rt", C.c_double),
                 ("min_rt", C.c_double), ("previous_pass_qps", C.c_double), ("total_pass", C.c_int64),
                 ("total_block", C.c_int64), ("total_success", C.c_int64), ("total_exception", C.c_int64),
-                ("cur_thread_num", C.c_int64), ("waiting", C.c_int64)]
+                ("cur_thread_num", C.c_int64), ("waiting", C.c_int64), ("max_success_qps", C.c_double),
+                ("previous_block_qps", C.c_double)]
 
 
 class SgaWireBatch(C.Structure):  # include/sga_wire.h

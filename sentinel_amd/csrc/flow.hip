@@ -144,16 +144,18 @@ __device__ __forceinline__ double node_pass_qps(const Ctx &c, int64_t *node, int
     return (double)sec_sum(node, t, MB_PASS) / 1.0;
 }
 
-// minute.previousWindowPass(): currentWindow(now) then getPreviousWindow(now), LeapArray.java:230-248
-__device__ double node_prev_pass_qps(const Ctx &c, int64_t *node, int64_t t) {
+// minute.previousWindowPass() / previousWindowBlock(): currentWindow(now) then getPreviousWindow(now),
+// LeapArray.java:230-248, ArrayMetric.java:283-297
+__device__ double node_prev_qps(const Ctx &c, int64_t *node, int64_t t, int f) {
     min_current(node, t, c.max_rt);
     const int64_t tp = t - kMinW;
     if (t < 0) return 0;
     const int64_t *b = node + kNodeMin + kMB * (int)((tp / kMinW) % 60);
     if (b[0] == kAbsent || t - b[0] > kMinInterval) return 0;
     if (b[0] + kMinW < tp) return 0;
-    return (double)b[MB_PASS];
+    return (double)b[f];
 }
+__device__ double node_prev_pass_qps(const Ctx &c, int64_t *node, int64_t t) { return node_prev_qps(c, node, t, MB_PASS); }
 
 __device__ __forceinline__ void node_add(const Ctx &c, int64_t *node, int64_t t, int f, int64_t n) {
     int64_t *b = sec_current(node, t, c.max_rt);
@@ -3730,6 +3732,16 @@ __global__ void k_node_view(FlowState st, int64_t max_rt, uint32_t r, int64_t no
     }
     dv[6] = (double)(mr < 1 ? 1 : mr);
     dv[7] = node_prev_pass_qps(c, node, now);
+    {  // maxSuccessQps: ArrayMetric.maxSuccess() (currentWindow, max over values(), at least 1) x 2 / 1.0
+        sec_current(node, now, max_rt);
+        int64_t ms = 0;
+        for (int j = 0; j < 2; ++j) {
+            const int64_t *b = node + kNodeSec + kMB * j;
+            if (b[0] != kAbsent && !(now - b[0] > kSecInterval) && b[MB_SUCC] > ms) ms = b[MB_SUCC];
+        }
+        dv[8] = (double)(ms < 1 ? 1 : ms) * 2.0 / 1.0;
+    }
+    dv[9] = node_prev_qps(c, node, now, MB_BLOCK);
     min_current(node, now, max_rt);
     iv[0] = min_sum(node, now, MB_PASS);
     iv[1] = min_sum(node, now, MB_BLOCK);
@@ -4980,13 +4992,13 @@ int FlowEngine::query(uint32_t r, int64_t now, sga_node_view *out) {
     if (r == SGA_ENTRY_NODE && nres) r = nres;
     else if (r >= nres) return SGA_EINVAL;
     if (now < 0 || !out) return SGA_EINVAL;
-    if (!d_view.p) d_view.alloc(16);
+    if (!d_view.p || d_view.n < 24) d_view.alloc(24);
     hipLaunchKernelGGL(k_node_view, dim3(1), dim3(64), 0, stream, state(), (int64_t)cfg.statistic_max_rt, r, now,
-                       (double *)d_view.p, d_view.p + 8);
-    double dv[8];
+                       (double *)d_view.p, d_view.p + 16);
+    double dv[16];
     int64_t iv[8];
-    SGA_HIP_CHECK(hipMemcpyAsync(dv, d_view.p, 64, hipMemcpyDeviceToHost, stream));
-    SGA_HIP_CHECK(hipMemcpyAsync(iv, d_view.p + 8, 64, hipMemcpyDeviceToHost, stream));
+    SGA_HIP_CHECK(hipMemcpyAsync(dv, d_view.p, 128, hipMemcpyDeviceToHost, stream));
+    SGA_HIP_CHECK(hipMemcpyAsync(iv, d_view.p + 16, 64, hipMemcpyDeviceToHost, stream));
     SGA_HIP_CHECK(hipStreamSynchronize(stream));
     out->pass_qps = dv[0];
     out->block_qps = dv[1];
@@ -5002,6 +5014,8 @@ int FlowEngine::query(uint32_t r, int64_t now, sga_node_view *out) {
     out->total_exception = iv[3];
     out->cur_thread_num = iv[4];
     out->waiting = iv[5];
+    out->max_success_qps = dv[8];
+    out->previous_block_qps = dv[9];
     return 0;
 }
 

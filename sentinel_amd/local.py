@@ -133,6 +133,8 @@ class NodeView:
     total_exception: int
     cur_thread_num: int
     waiting: int
+    max_success_qps: float
+    previous_block_qps: float
 
 
 @dataclass

@@ -4,6 +4,7 @@ tests/jni_stub), and the glue reaches the engine: without a GPU, creating an eng
 SGA_ENODEV through it.  The Java side (jni/src) needs a JDK and is not compiled here."""
 import ctypes as C
 import os
+import struct
 import subprocess
 
 import pytest
@@ -75,7 +76,7 @@ def test_glue_calls_reach_the_engine_abi(glue):
         "sgaj_set_connected_count": ([P, C.c_char_p, I32], [None, b"default", 2]),
         "sgaj_set_namespace_limit": ([P, C.c_char_p, D], [None, b"default", 100.0]),
         "sgaj_set_cluster_server": ([P, I32], [None, 1]),
-        "sgaj_query_node": ([P, U32, I64, P, P], [None, 0, 1, (C.c_double * 8)(), (C.c_int64 * 6)()]),
+        "sgaj_query_node": ([P, U32, I64, P, P], [None, 0, 1, (C.c_double * 10)(), (C.c_int64 * 6)()]),
     }
     for name, (argt, args) in calls.items():
         fn = getattr(glue, name)
@@ -116,3 +117,12 @@ def test_java_sources_present():
     svc = os.path.join(ROOT, "jni", "src", "main", "resources", "META-INF", "services")
     assert open(os.path.join(svc, "com.alibaba.csp.sentinel.cluster.TokenService")).read().strip() == \
         "com.alibaba.csp.sentinel.gpu.GpuTokenService"
+
+
+def test_flow_record_layout_matches_the_c_struct():
+    """GpuRuleSync's 64-byte record has sga_flow_rule's size and field offsets (include/sentinel_amd.h)."""
+    from sentinel_amd._lib import SgaFlowRule
+    # GpuRuleSync.FlowListener: putInt x2, putDouble, putInt x6, putLong, putInt x4 (GpuRuleSync.java:141-154)
+    assert struct.calcsize("<iidiiiiiiqiiii") == 64 == C.sizeof(SgaFlowRule)
+    java_offsets = [0, 4, 8, 16, 20, 24, 28, 32, 36, 40, 48, 52, 56, 60]
+    assert [getattr(SgaFlowRule, f).offset for f, _ in SgaFlowRule._fields_] == java_offsets
