@@ -10,6 +10,8 @@ import com.alibaba.csp.sentinel.EntryType;
 import com.alibaba.csp.sentinel.context.Context;
 import com.alibaba.csp.sentinel.node.DefaultNode;
 import com.alibaba.csp.sentinel.slotchain.AbstractLinkedProcessorSlot;
+import com.alibaba.csp.sentinel.slotchain.DefaultProcessorSlotChain;
+import com.alibaba.csp.sentinel.slotchain.ProcessorSlotChain;
 import com.alibaba.csp.sentinel.slotchain.ResourceWrapper;
 import com.alibaba.csp.sentinel.slots.block.BlockException;
 import com.alibaba.csp.sentinel.slots.block.RuleConstant;
@@ -24,10 +26,13 @@ import com.alibaba.csp.sentinel.util.TimeUtil;
 
 /**
  * One slot in place of StatisticSlot, SystemSlot, ParamFlowSlot, FlowSlot and DegradeSlot (ProcessorSlot.java:41-76).
- * As StatisticSlot (StatisticSlot.java:64-145) it first fires the rest of the chain -- AuthoritySlot and any
- * custom slot -- and then decides: the engine's local path (sga_submit_events) runs SystemSlot, ParamFlowSlot,
- * FlowSlot and DegradeSlot and the StatisticSlot accounting on the GPU in one event.  A BlockException from the
- * fired slots is counted as a block (event kind 2) and rethrown; an engine block becomes the reference's
+ * As StatisticSlot (StatisticSlot.java:64-145) it first fires the checks that precede the engine's -- the "pre"
+ * chain (AuthoritySlot and the custom slots sorted before DegradeSlot, GpuSlotChainBuilder) -- and then decides:
+ * the engine's local path (sga_submit_events) runs SystemSlot, ParamFlowSlot, FlowSlot and DegradeSlot and the
+ * StatisticSlot accounting on the GPU in one event; the "post" chain (slots sorted after DegradeSlot) runs only
+ * for an entry the engine passed, as in the reference.  A BlockException from the pre chain is counted as a block
+ * (event kind 2) and rethrown; one from the post chain too, but the engine has then already counted the pass
+ * (its event is one step); an engine block becomes the reference's
  * exception with the blocking rule ({@link GpuRuleSync} keeps the per-resource lists in engine order), and its
  * block error is set on the entry so that exit records nothing.  Passes sleep the engine's wait (RateLimiter
  * pacing, cluster SHOULD_WAIT, parameter throttle) as the reference controllers do before returning.
@@ -37,6 +42,16 @@ public class GpuStatisticSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
     private static final Map<String, Integer> RESOURCE_IDS = new ConcurrentHashMap<>();
     private static final List<String> NAMES = new ArrayList<>();
     private final long engine = GpuEngine.get();
+    private final ProcessorSlotChain pre, post;
+
+    public GpuStatisticSlot() {
+        this(new DefaultProcessorSlotChain(), new DefaultProcessorSlotChain());
+    }
+
+    GpuStatisticSlot(ProcessorSlotChain pre, ProcessorSlotChain post) {
+        this.pre = pre;
+        this.post = post;
+    }
 
     /** Dense resource id of a resource name (like CtSph's chain map); at most csp.sentinel.gpu.maxResources. */
     static int resourceId(String name) {
@@ -77,8 +92,8 @@ public class GpuStatisticSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
         final int rid = resourceId(name);
         final int fl = flags(resourceWrapper, prioritized);
         try {
-            // StatisticSlot.java:71: the slots after this one run first (AuthoritySlot, custom slots)
-            fireEntry(context, resourceWrapper, node, count, prioritized, args);
+            // StatisticSlot.java:71: the checks before the engine's (AuthoritySlot, custom slots sorted before DegradeSlot)
+            pre.entry(context, resourceWrapper, node, count, prioritized, args);
         } catch (BlockException e) {
             // StatisticSlot.java:121-135: the block is counted (node + ENTRY_NODE when inbound)
             context.getCurEntry().setBlockError(e);
@@ -99,6 +114,14 @@ public class GpuStatisticSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
                 if (o[1] > 0) {
                     TimeUnit.MILLISECONDS.sleep(o[1]);
                 }
+                try {  // the slots sorted after DegradeSlot, which the reference reaches only on a pass
+                    post.entry(context, resourceWrapper, node, count, prioritized, args);
+                } catch (BlockException e) {
+                    context.getCurEntry().setBlockError(e);
+                    GpuEngine.blocked(engine, rid, TimeUtil.currentTimeMillis(), count, fl);
+                    throw e;
+                }
+                fireEntry(context, resourceWrapper, node, count, prioritized, args);
                 return;
             case 1: {
                 FlowRule r = GpuRuleSync.flowRule(name, o[1]);
@@ -142,6 +165,9 @@ public class GpuStatisticSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
             GpuEngine.exitArgs(engine, resourceId(resourceWrapper.getName()), now, count, fl, rt,
                                GpuArgs.encode(args), args == null ? 0 : args.length);
         }
+        // StatisticSlot.exit accounts first, then the later slots' exits in chain order
+        pre.exit(context, resourceWrapper, count, args);
+        post.exit(context, resourceWrapper, count, args);
         fireExit(context, resourceWrapper, count, args);
     }
 }
