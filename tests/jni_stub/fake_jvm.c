@@ -22,7 +22,9 @@ typedef struct {
 static jstring f_new_string(JNIEnv *env, const char *s) {
     (void)env;
     fake_str *x = (fake_str *)malloc(sizeof(*x));
-    x->s = strdup(s ? s : "");
+    const size_t n = strlen(s ? s : "") + 1;
+    x->s = (char *)malloc(n);
+    memcpy(x->s, s ? s : "", n);
     return (jstring)x;
 }
 static jsize f_len(JNIEnv *env, jarray a) {

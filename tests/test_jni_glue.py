@@ -19,6 +19,7 @@ def glue(tmp_path_factory):
            "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "jni", "native"),
            "-I", os.path.join(ROOT, "tests", "jni_stub"),
            os.path.join(ROOT, "jni", "native", "sga_jni_glue.c"), os.path.join(ROOT, "jni", "native", "sentinel_amd_jni.c"),
+           os.path.join(ROOT, "tests", "jni_stub", "fake_jvm.c"),
            "-L", os.path.join(ROOT, "sentinel_amd"), "-lsentinel_amd", "-Wl,-rpath," + os.path.join(ROOT, "sentinel_amd"),
            "-o", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -107,6 +108,26 @@ def test_glue_reaches_engine_without_gpu(glue):
     h = C.c_void_p()
     assert glue.sgaj_create(0, 1 << 16, 1 << 16, C.byref(h)) == -19  # SGA_ENODEV
     assert not h.value
+
+
+def test_java_entry_points_through_a_fake_jnienv_without_gpu(glue):
+    """The Java_* entry points themselves, called with tests/jni_stub/fake_jvm.c's JNIEnv (as
+    tests/test_jni_live_gpu.py drives them on a GPU): GpuEngine.create answers SGA_ENODEV here, and
+    lastError returns a Java string."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present: the no-device answer is not observable")
+    glue.fake_env.restype = C.c_void_p
+    env = C.c_void_p(glue.fake_env())
+    create = getattr(glue, "Java_com_alibaba_csp_sentinel_gpu_GpuEngine_create")
+    create.restype = C.c_int64
+    assert create(env, None, 0, 1 << 14, 1 << 12) == -19
+    last = getattr(glue, "Java_com_alibaba_csp_sentinel_gpu_GpuEngine_lastError")
+    last.restype = C.c_void_p
+    js = last(env, None, C.c_int64(0))
+    glue.fake_string_chars.restype = C.c_char_p
+    glue.fake_string_chars.argtypes = [C.c_void_p]
+    assert isinstance(glue.fake_string_chars(js), bytes)
 
 
 def test_java_sources_present():
