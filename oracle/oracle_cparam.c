@@ -12,10 +12,16 @@
  *                                                CS/flow/rule/ClusterParamFlowRuleManager.java:195-223,318-368
  *   ParamFlowRuleUtil.isValidRule / checkCluster PF/slots/block/flow/param/ParamFlowRuleUtil.java:46-70
  *
- * Each bucket's value map is the reference's per-bucket CacheMap (a ConcurrentLinkedHashMap of
- * capacity 4000, ClusterParamMetric.DEFAULT_CLUSTER_MAX_CAPACITY).  concurrentlinkedhashmap-lru
- * 1.4.2 is not vendored and no reference test exercises its eviction, so this restatement keeps
- * every value (no eviction): parity is pinned only while a bucket holds <= 4000 distinct values.
+ * Each bucket's value map is the reference's per-bucket CacheMap: a ConcurrentLinkedHashMapWrapper of
+ * capacity ClusterParamMetric.DEFAULT_CLUSTER_MAX_CAPACITY = 4000 (ClusterParamMetric.java:37,42,49;
+ * ClusterParameterLeapArray.java:40-41, a new map per new bucket, cleared on reset :45-47), restated as a
+ * strict LRU of that capacity (concurrentlinkedhashmap-lru 1.4.2 is not vendored; for one thread its
+ * published policy is LRU: reads -- getSum's bucket.get(value) on every valid bucket, :57-62 -- and
+ * putIfAbsent of a present key move the key to the most recent end, an insert into a full map evicts the
+ * least recent one, :79-88).  getTopValues' keySet(true) + get(o) walk each map from its least recent key,
+ * moving every key to the most recent end in that same order, so it leaves the order as it was
+ * (:90-133).  orc_cluster_set_param_capacity changes the capacity of metrics created afterwards (tests);
+ * parity against CLHM itself is unpinned (Oracle).
  */
 #include "oracle_internal.h"
 #include "java_semantics.h"
@@ -27,9 +33,10 @@
 enum { P_BAD_REQUEST = -4, P_TOO_MANY_REQUEST = -2, P_FAIL = -1, P_OK = 0, P_BLOCKED = 1, P_NO_RULE_EXISTS = 3 };
 static const int64_t P_ABSENT = INT64_MIN;
 
-/* value -> LongAdder sum, open addressing (one per bucket) */
+/* value -> LongAdder sum, open addressing (one per bucket); rec = the key's last access (LRU order) */
 typedef struct vmap {
     int64_t *key, *val;
+    uint64_t *rec;
     uint8_t *used;
     size_t cap, n;
 } vmap;
@@ -41,36 +48,71 @@ static uint64_t vmix(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-static int64_t *vmap_slot(vmap *m, int64_t k, int create) {
-    if (create && (m->cap == 0 || (m->n + 1) * 2 > m->cap)) {
-        size_t ncap = m->cap ? m->cap * 2 : 16;
-        vmap nm = {calloc(ncap, 8), calloc(ncap, 8), calloc(ncap, 1), ncap, 0};
-        for (size_t i = 0; i < m->cap; i++) {
-            if (!m->used[i]) continue;
-            size_t h = vmix((uint64_t)m->key[i]) & (ncap - 1);
-            while (nm.used[h]) h = (h + 1) & (ncap - 1);
-            nm.used[h] = 1;
-            nm.key[h] = m->key[i];
-            nm.val[h] = m->val[i];
-            nm.n++;
-        }
-        free(m->key);
-        free(m->val);
-        free(m->used);
-        *m = nm;
+static void vmap_grow(vmap *m) {
+    size_t ncap = m->cap ? m->cap * 2 : 16;
+    vmap nm = {calloc(ncap, 8), calloc(ncap, 8), calloc(ncap, 8), calloc(ncap, 1), ncap, 0};
+    for (size_t i = 0; i < m->cap; i++) {
+        if (!m->used[i]) continue;
+        size_t h = vmix((uint64_t)m->key[i]) & (ncap - 1);
+        while (nm.used[h]) h = (h + 1) & (ncap - 1);
+        nm.used[h] = 1;
+        nm.key[h] = m->key[i];
+        nm.val[h] = m->val[i];
+        nm.rec[h] = m->rec[i];
+        nm.n++;
     }
-    if (m->cap == 0) return NULL;
+    free(m->key);
+    free(m->val);
+    free(m->rec);
+    free(m->used);
+    *m = nm;
+}
+
+/* the key's table index, or -1 */
+static long vmap_find(const vmap *m, int64_t k) {
+    if (m->cap == 0) return -1;
     size_t h = vmix((uint64_t)k) & (m->cap - 1);
     while (m->used[h]) {
-        if (m->key[h] == k) return &m->val[h];
+        if (m->key[h] == k) return (long)h;
         h = (h + 1) & (m->cap - 1);
     }
+    return -1;
+}
+
+static int64_t *vmap_slot(vmap *m, int64_t k, int create) {
+    long f = vmap_find(m, k);
+    if (f >= 0) return &m->val[f];
     if (!create) return NULL;
+    if (m->cap == 0 || (m->n + 1) * 2 > m->cap) vmap_grow(m);
+    size_t h = vmix((uint64_t)k) & (m->cap - 1);
+    while (m->used[h]) h = (h + 1) & (m->cap - 1);
     m->used[h] = 1;
     m->key[h] = k;
     m->val[h] = 0;
+    m->rec[h] = 0;
     m->n++;
     return &m->val[h];
+}
+
+/* linear-probing removal (backward shift: later keys of the probe run move up) */
+static void vmap_erase(vmap *m, size_t i) {
+    m->used[i] = 0;
+    m->n--;
+    size_t j = i;
+    for (;;) {
+        j = (j + 1) & (m->cap - 1);
+        if (!m->used[j]) return;
+        size_t h = vmix((uint64_t)m->key[j]) & (m->cap - 1);
+        /* move j to the hole i when its home h is not within (i, j] cyclically */
+        if ((j > i && (h <= i || h > j)) || (j < i && (h <= i && h > j))) {
+            m->used[i] = 1;
+            m->key[i] = m->key[j];
+            m->val[i] = m->val[j];
+            m->rec[i] = m->rec[j];
+            m->used[j] = 0;
+            i = j;
+        }
+    }
 }
 
 static void vmap_clear(vmap *m) {
@@ -81,6 +123,7 @@ static void vmap_clear(vmap *m) {
 static void vmap_free(vmap *m) {
     free(m->key);
     free(m->val);
+    free(m->rec);
     free(m->used);
     memset(m, 0, sizeof(*m));
 }
@@ -91,10 +134,16 @@ typedef struct pmetric {
     double interval_sec;
     int64_t *start; /* P_ABSENT = array slot null */
     vmap *map;
+    size_t capacity; /* each bucket map's maxCapacity */
+    uint64_t clock;  /* access order (LRU) */
 } pmetric;
+
+static size_t g_param_capacity = 4000; /* ClusterParamMetric.DEFAULT_CLUSTER_MAX_CAPACITY */
+void orc_cluster_set_param_capacity(size_t cap) { g_param_capacity = cap ? cap : 4000; }
 
 static pmetric *pm_new(int S, int interval) {
     pmetric *m = calloc(1, sizeof(pmetric));
+    m->capacity = g_param_capacity;
     m->S = S;
     m->interval = interval;
     m->W = interval / S;
@@ -132,22 +181,45 @@ static int pm_current_window(pmetric *m, int64_t t) {
     return -1;
 }
 
-/* ClusterParamMetric.getSum(value): currentWindow() then sum over values() */
+/* ClusterParamMetric.getSum(value): currentWindow() then sum over values(); every bucket.get(value) that
+ * finds the value is an access (LRU order) */
 static int64_t pm_sum(pmetric *m, int64_t value, int64_t t) {
     pm_current_window(m, t);
     int64_t s = 0;
     for (int j = 0; j < m->S; j++) {
         if (m->start[j] == P_ABSENT || t - m->start[j] > m->interval) continue;  /* isWindowDeprecated */
-        const int64_t *v = vmap_slot(&m->map[j], value, 0);
-        if (v) s += *v;
+        const long f = vmap_find(&m->map[j], value);
+        if (f >= 0) {
+            s += m->map[j].val[f];
+            m->map[j].rec[f] = ++m->clock;
+        }
     }
     return s;
 }
 
+/* addValue: putIfAbsent into the current bucket's map (a present key is an access; a new key into a full
+ * map evicts the least recently accessed one, ClusterParamMetric.java:79-88) */
 static void pm_add(pmetric *m, int64_t value, int count, int64_t t) {
     int idx = pm_current_window(m, t);
     if (idx < 0) return;
-    *vmap_slot(&m->map[idx], value, 1) += count;
+    vmap *b = &m->map[idx];
+    long f = vmap_find(b, value);
+    if (f < 0) {
+        if (b->n >= m->capacity) { /* evict the least recent key */
+            size_t lru = 0;
+            uint64_t best = UINT64_MAX;
+            for (size_t i = 0; i < b->cap; i++)
+                if (b->used[i] && b->rec[i] < best) {
+                    best = b->rec[i];
+                    lru = i;
+                }
+            vmap_erase(b, lru);
+        }
+        vmap_slot(b, value, 1);
+        f = vmap_find(b, value);
+    }
+    b->val[f] += count;
+    b->rec[f] = ++m->clock;
 }
 
 typedef struct prule {

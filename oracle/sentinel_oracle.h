@@ -253,6 +253,8 @@ typedef struct orc_cparam_rule {
 
 /* ClusterParamFlowRuleManager.loadRules(namespace, rules); returns #applied */
 int orc_cluster_load_param_rules(orc_cluster *c, const char *ns, const orc_cparam_rule *rules, size_t n);
+/* per-bucket CacheMap capacity of the ClusterParamMetrics created afterwards (default 4000; tests) */
+void orc_cluster_set_param_capacity(size_t cap);
 /* DefaultTokenService.requestParamToken(flowId, acquire, values) at `now` */
 orc_token_result orc_cluster_request_param_token(orc_cluster *c, int64_t flow_id, int32_t acquire,
                                                  const int64_t *values, size_t nvalues, int64_t now);

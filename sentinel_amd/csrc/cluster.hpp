@@ -271,9 +271,10 @@ void cluster_decide_hot(const ClusterState &st, BatchScratch &sc, const int32_t 
 // ---------------------------------------------------------------------------------------------
 // Cluster parameter flow (ClusterParamFlowChecker + ClusterParamMetric, CS/flow/ClusterParamFlowChecker.java:37-120,
 // CS/flow/statistic/metric/ClusterParamMetric.java:41-88).  Per rule slot the rule-level LeapArray
-// starts; per (rule, value) key a record [stamp x S][count x S] where stamp = start of the
-// rule bucket the count belongs to (a count is live while its stamp equals the rule's start:
-// resetWindowTo clearing a bucket's map = the rule start moving past the stamp).
+// starts; per (rule, value) key a record [stamp x S][count x S][access x S] where stamp = start of the
+// rule bucket the count belongs to (a count is live -- the key is in that bucket's map -- while its
+// stamp equals the rule's start: resetWindowTo clearing a bucket's map = the rule start moving past the
+// stamp) and access = the key's last access in that bucket's map (LRU order, see cparam_exact.hpp).
 struct PRuleParam {
     double count;        // ParamFlowRule.count
     double isec;         // intervalInMs / 1000.0
@@ -281,7 +282,16 @@ struct PRuleParam {
     int32_t S, W, interval;
     int32_t active, ns, threshold_type;
     uint32_t hot_off, n_hot;  // hot items (ascending value) at hot_v/hot_c[hot_off ..)
+    uint32_t cap;        // each bucket map's capacity (ClusterParamMetric maxCapacity, default 4000)
 };
+
+// LRU-mode queue record (cparam_exact.hpp): the key and the access stamp it was pushed with
+struct PLruRec {
+    uint64_t kidx;
+    uint64_t stamp;
+};
+constexpr uint64_t kPNoQueue = ~0ull;
+constexpr uint64_t kPLruBuilding = ~0ull;  // meta.kidx of an area the switch is filling
 
 struct CParamState {
     const PRuleParam *param;
@@ -302,8 +312,16 @@ struct CParamState {
     int64_t *kval;            // per kidx: value
     int64_t *krec;
     uint64_t krec_cap;        // int64 units
-    uint32_t *ctl;            // [0] krec cursor  [1] error flags (1 key table full, 2 record pool full)
-                              // [2] slow requests  [3] global slow (timestamps not ascending)
+    uint32_t *ctl;            // [0] krec cursor  [1] error flags (1 key table full, 2 record pool full,
+                              //     4 LRU queue check)  [2] slow requests  [3] global slow (timestamps
+                              //     not ascending)  [4] rules switching to LRU mode (k_plru_decide)
+    // CacheMap capacity (strict LRU, cparam_exact.hpp)
+    uint32_t *nkeys;          // per rule slot: keys ever created (a bucket map can only overflow past cap keys)
+    uint64_t *pq;             // per rule bucket (boff + j): LRU queue area in lpool (kPNoQueue: free mode)
+    uint32_t *psize;          // per rule bucket, LRU mode: keys in the bucket's map
+    PLruRec *lpool;
+    uint32_t *sw_list;        // rules switching this batch
+    uint64_t seq;             // access stamp base of this batch / call
 };
 
 struct CParamScratch {
@@ -327,6 +345,12 @@ void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
 // ClusterParamMetric.getSum(value) at now (rotation side effect included); *d_out = -1 if no key
 void cparam_sum(const CParamState &st, uint32_t slot, int64_t value, int64_t now, int64_t *d_out, hipStream_t s);
 void cparam_init_rule(const CParamState &st, uint32_t slot, hipStream_t s);
+// CacheMap capacity: rules whose key count passed their capacity switch to LRU mode (the sequential
+// path from then on).  decide lists them (count in ctl[4]); the host assigns each an area of S x
+// (2 cap + 3) records (qoff, one per listed rule) and calls switch, which fills the areas from the
+// access stamps.
+void cparam_lru_decide(const CParamState &st, hipStream_t s);
+void cparam_lru_switch(const CParamState &st, const uint64_t *d_qoff, uint32_t nsw, hipStream_t s);
 // ClusterParamMetric.getTopValues(number) of one rule at now: d_list holds 2 x (kmask + 1) int64.
 void cparam_top_values(const CParamState &st, uint32_t slot, int64_t now, uint32_t number, int64_t *d_list,
                        uint32_t *d_count, int64_t *d_val, double *d_qps, uint32_t *d_n, hipStream_t s);
