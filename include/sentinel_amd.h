@@ -241,7 +241,14 @@ int sga_request_param_tokens(sga_engine *e, const int64_t *flow_id, const int32_
                              const uint32_t *value_offsets, const int64_t *values, const int64_t *ts, size_t n,
                              sga_token_result *out);
 
-/* ClusterParamMetric.getSum(value) of a flow at `now` (rotation side effect included). */
+/* Each bucket map's capacity of the ClusterParamMetrics created from now on (the maxCapacity argument of
+ * ClusterParamMetric(sampleCount, intervalInMs, maxCapacity), ClusterParamMetric.java:44-49; 0 restores
+ * DEFAULT_CLUSTER_MAX_CAPACITY = 4000).  Existing metrics keep theirs.  A map at capacity evicts its least
+ * recently accessed value (getSum's get and addValue's putIfAbsent are accesses). */
+int sga_cluster_set_param_capacity(sga_engine *e, uint32_t capacity);
+
+/* ClusterParamMetric.getSum(value) of a flow at `now` (rotation side effect included; the gets are
+ * accesses in LRU order). */
 int sga_cluster_param_sum(sga_engine *e, int64_t flow_id, int64_t value, int64_t now, int64_t *out);
 
 /* ClusterParamMetric.getTopValues(number) of a param flow at `now` (rotation side effect included):

@@ -258,6 +258,12 @@ class ClusterParamFlowRuleManager:
         rc = _lib.load().sga_load_cluster_param_rules(self.engine.handle, namespace.encode(), arr, len(rules))
         return check(rc, self.engine.handle, "loadRules")
 
+    def set_param_capacity(self, capacity: int = 0) -> None:
+        """maxCapacity of each bucket map of the ClusterParamMetrics created from now on (0: the default
+        ClusterParamMetric.DEFAULT_CLUSTER_MAX_CAPACITY = 4000); a full map evicts its least recently
+        accessed value."""
+        check(_lib.load().sga_cluster_set_param_capacity(self.engine.handle, capacity))
+
     def param_sum(self, flow_id: int, value, now: int) -> int:
         """ClusterParamMetric.getSum(value) of the flow's metric at `now`."""
         out = C.c_int64()

@@ -3143,7 +3143,9 @@ __global__ void k_lim_init(NsLimiterDev *L) {
 // changes a key's sum (a stamp the rule start has moved past is already deprecated at the later
 // call, LeapArray.isWindowDeprecated), so keys are independent and each (key, bucket) run is
 // solved in closed form like a ClusterFlowChecker run.  Otherwise the rule's requests are
-// replayed one by one against the rule-level starts (k_pslow).
+// replayed one by one against the rule-level starts (k_pslow), as are, from the batch their key count
+// passes the bucket maps' capacity on, the rules whose maps may have to evict (cparam_exact.hpp, LRU mode).
+// Both paths keep every key's last access stamp per bucket, which orders the maps when a rule switches.
 // kErrKeys / kErrPool, prule_lookup, prule_threshold, vid_of, key_of: cparam_exact.hpp
 
 // Stage 1a: validation (DefaultTokenService.notValidRequest || params empty -> BAD_REQUEST,
@@ -3208,7 +3210,8 @@ __global__ __launch_bounds__(kThreads) void k_ppath(CParamState st, uint64_t *__
     const uint32_t slot = el_slot(el[i]);
     uint64_t fast = (uint64_t)key_invalid << kSlotShift, slow = (uint64_t)invalid_key << kSlotShift;
     if (slot != invalid_key) {
-        if (st.ctl[3] || st.coupled[slot]) {
+        const PRuleParam &Ps = st.param[slot];
+        if (st.ctl[3] || st.coupled[slot] || st.pq[Ps.boff] != kPNoQueue || st.nkeys[slot] > Ps.cap) {
             slow = ((uint64_t)slot << kSlotShift) | i;
             atomicAdd(&st.ctl[2], 1u);
         } else {
@@ -3258,7 +3261,8 @@ __global__ __launch_bounds__(kThreads) void k_pslow(CParamState st, BatchScratch
             for (uint32_t v = v0; v < v1; ++v) {  // ClusterParamFlowChecker.java:61-71
                 const uint32_t kidx = vkey[v];
                 pm_window(st, P, t);
-                const int64_t sum = kidx == 0xFFFFFFFFu ? 0 : pm_key_sum(st, P, st.krec + st.koff[kidx], t);
+                const int64_t sum =
+                    kidx == 0xFFFFFFFFu ? 0 : pm_key_sum_access(st, P, kidx, t, pstamp(st, i, min(v - v0, 0x7FFFu)));
                 const double next = prule_threshold(st, P, values[v]) - (double)sum / P.isec - (double)a;
                 remaining = next;
                 if (next < 0) {
@@ -3271,13 +3275,7 @@ __global__ __launch_bounds__(kThreads) void k_pslow(CParamState st, BatchScratch
                     const int idx = pm_window(st, P, t);
                     const uint32_t kidx = vkey[v];
                     if (idx < 0 || kidx == 0xFFFFFFFFu) continue;
-                    int64_t *rec = st.krec + st.koff[kidx];
-                    const int64_t rs = st.rstart[P.boff + idx];
-                    if (rec[idx] != rs) {
-                        rec[idx] = rs;
-                        rec[P.S + idx] = 0;
-                    }
-                    rec[P.S + idx] += a;
+                    pm_key_add(st, P, kidx, idx, a, pstamp(st, i, kPAddLow | min(v - v0, 0x7FFFu)));
                 }
             }
             if (v1 - v0 > 1) remaining = -1;
@@ -3325,17 +3323,22 @@ __global__ __launch_bounds__(kThreads) void k_pflows(CParamState st, BatchScratc
                 if (j == cj && stp != ws) continue;  // the current bucket was reset
                 s0 += rec[P.S + j];
             }
-            const int64_t cur = (rec[cj] == ws) ? rec[P.S + cj] : 0;
+            const bool held = rec[cj] == ws;  // the key is in the current bucket's map
+            const int64_t cur = held ? rec[P.S + cj] : 0;
             uint32_t f = 0;
             int64_t added = 0;
+            bool last_pass;
             if (a > 0) {
                 f = pass_prefix(thr, P.isec, s0, a, n);
                 added = (int64_t)f * a;
+                last_pass = f == n;
             } else {  // mixed acquire counts: request by request on the same lazily rotated sum
+                last_pass = false;
                 for (uint32_t j = j0; j < j1; ++j) {
                     const uint32_t i = el_idx(el[j]);
                     const int32_t ai = acquire[i];
                     const double next = thr - (double)(s0 + added) / P.isec - (double)ai;
+                    last_pass = next >= 0;
                     if (next >= 0) {
                         added += ai;
                         out[i] = pack_result(TRS_OK, j_d2i(next), 0);
@@ -3344,10 +3347,32 @@ __global__ __launch_bounds__(kThreads) void k_pflows(CParamState st, BatchScratc
                     }
                 }
             }
-            rec[cj] = ws;
-            rec[P.S + cj] = cur + added;
+            // last access stamps: every request's getSum reads the valid buckets holding the key, a pass
+            // adds to the current one; per bucket the run's last such access
+            const uint32_t il = el_idx(el[j1 - 1]);
+            const int64_t tl = ts_base + (int64_t)ts_off[il];
+            for (int j = 0; j < P.S; ++j) {
+                if (j == cj) continue;
+                const int64_t stp = rec[j];
+                if (stp == kAbsent || t0 - stp > (int64_t)P.interval) continue;
+                uint32_t ia = il;
+                if (tl - stp > (int64_t)P.interval) {  // valid for a prefix of the run only
+                    uint32_t lo = j0, hi = j1 - 1;     // last request with t - stp <= interval
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi + 1) >> 1;
+                        if (ts_base + (int64_t)ts_off[el_idx(el[mid])] - stp <= (int64_t)P.interval) lo = mid;
+                        else hi = mid - 1;
+                    }
+                    ia = el_idx(el[lo]);
+                }
+                rec[2 * P.S + j] = (int64_t)pstamp(st, ia, 0);
+            }
+            if (held || added > 0) {
+                rec[cj] = ws;
+                rec[P.S + cj] = cur + added;
+                rec[2 * P.S + cj] = (int64_t)pstamp(st, il, last_pass ? kPAddLow : 0u);
+            }
             atomicMax((long long *)&st.rstart[P.boff + cj], (long long)ws);
-            const int64_t tl = ts_base + (int64_t)ts_off[el_idx(el[j1 - 1])];
             atomicMax((long long *)&st.tmax[slot], (long long)tl);
             ro.s0 = s0;
             ro.thr = thr;
@@ -3369,7 +3394,7 @@ __global__ void k_psum(CParamState st, uint32_t slot, int64_t value, int64_t now
     pm_window(st, P, now);
     const uint32_t vid = vid_of(st, value, false);
     const uint32_t kidx = vid == 0xFFFFFFFFu ? 0xFFFFFFFFu : key_of(st, slot, vid, value, false);
-    *out = kidx == 0xFFFFFFFFu ? 0 : pm_key_sum(st, P, st.krec + st.koff[kidx], now);
+    *out = kidx == 0xFFFFFFFFu ? 0 : pm_key_sum_access(st, P, kidx, now, pstamp(st, 0, 0));
 }
 
 // ClusterParamMetric.getTopValues(number), CS/flow/statistic/metric/ClusterParamMetric.java:90-133:
@@ -3442,10 +3467,118 @@ __global__ __launch_bounds__(1024) void k_ptop_select(CParamState st, uint32_t s
 
 __global__ void k_pinit_rule(CParamState st, uint32_t slot) {
     const PRuleParam P = st.param[slot];
-    for (int j = threadIdx.x; j < P.S; j += blockDim.x) st.rstart[P.boff + j] = kAbsent;
+    for (int j = threadIdx.x; j < P.S; j += blockDim.x) {
+        st.rstart[P.boff + j] = kAbsent;
+        st.pq[P.boff + j] = kPNoQueue;
+        st.psize[P.boff + j] = 0;
+    }
     if (threadIdx.x == 0) {
         st.tmax[slot] = INT64_MIN;
         st.coupled[slot] = 0;
+        st.nkeys[slot] = 0;
+    }
+}
+
+// ---- CacheMap capacity: the switch to LRU mode (cparam_exact.hpp)
+// 1. rules in free mode whose key count passed their capacity (only then can a bucket map overflow)
+__global__ __launch_bounds__(kThreads) void k_plru_decide(CParamState st) {
+    const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
+    if (s >= st.nslots) return;
+    const PRuleParam &P = st.param[s];
+    if (P.S <= 0 || st.pq[P.boff] != kPNoQueue || st.nkeys[s] <= P.cap) return;
+    st.sw_list[atomicAdd(&st.ctl[4], 1u)] = s;
+}
+
+// 2. the host's areas: bucket j of listed rule w at qoff[w] + j (2 cap + 3), marked as filling
+__global__ __launch_bounds__(kThreads) void k_plru_alloc(CParamState st, const uint64_t *qoff, uint32_t nsw) {
+    const uint32_t w = blockIdx.x;
+    if (w >= nsw) return;
+    const PRuleParam &P = st.param[st.sw_list[w]];
+    for (int j = threadIdx.x; j < P.S; j += kThreads) {
+        const uint64_t q = qoff[w] + (uint64_t)j * (plru_qcap(P) + 1);
+        st.pq[P.boff + j] = q;
+        st.lpool[q] = PLruRec{kPLruBuilding, 0};
+    }
+}
+
+// 3. every key of a switching rule held by a bucket's map -> (key, its access stamp there) into that
+//    bucket's area
+__global__ __launch_bounds__(kThreads) void k_plru_collect(CParamState st) {
+    for (uint32_t k = blockIdx.x * kThreads + threadIdx.x; k <= st.kmask; k += gridDim.x * kThreads) {
+        if (st.ktab[k] == 0) continue;
+        const PRuleParam &P = st.param[st.kslot[k]];
+        const uint64_t q0 = st.pq[P.boff];
+        if (q0 == kPNoQueue || st.lpool[q0].kidx != kPLruBuilding) continue;
+        const int64_t *rec = st.krec + st.koff[k];
+        for (int j = 0; j < P.S; ++j) {
+            const int64_t rs = st.rstart[P.boff + j];
+            if (rs == kAbsent || rec[j] != rs) continue;
+            const uint64_t q = st.pq[P.boff + j];
+            const unsigned long long pos = atomicAdd((unsigned long long *)&st.lpool[q].stamp, 1ull);
+            if (pos < plru_qcap(P)) st.lpool[q + 1 + pos] = PLruRec{k, (uint64_t)rec[2 * P.S + j]};
+            else atomicOr(&st.ctl[1], 4u);
+        }
+    }
+}
+
+// 4. each area ordered by stamp (oldest first), head 0, tail n, size n: one workgroup per (rule, bucket),
+//    bitonic in LDS up to kPLruLds records, else in the area (2 cap + 2 >= the padded count)
+constexpr int kPLruSortThreads = 256, kPLruLds = 4096;
+__global__ __launch_bounds__(kPLruSortThreads) void k_plru_sort(CParamState st, uint32_t nsw) {
+    __shared__ uint64_t ks[kPLruLds], vs[kPLruLds];
+    const uint32_t w = blockIdx.x, j = blockIdx.y;
+    if (w >= nsw) return;
+    const PRuleParam &P = st.param[st.sw_list[w]];
+    if ((int)j >= P.S) return;
+    const uint64_t q = st.pq[P.boff + j];
+    PLruRec *rec = st.lpool + q + 1;
+    const uint32_t n = (uint32_t)min<uint64_t>(st.lpool[q].stamp, plru_qcap(P));
+    if (n > P.cap && threadIdx.x == 0) atomicOr(&st.ctl[1], 4u);  // a free-mode map holds at most cap keys
+    uint32_t np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    if (np2 <= (uint32_t)kPLruLds) {
+        for (uint32_t k = threadIdx.x; k < np2; k += kPLruSortThreads) {
+            ks[k] = k < n ? rec[k].stamp : ~0ull;
+            vs[k] = k < n ? rec[k].kidx : 0ull;
+        }
+        __syncthreads();
+        for (uint32_t kk = 2; kk <= np2; kk <<= 1)
+            for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+                for (uint32_t a = threadIdx.x; a < np2; a += kPLruSortThreads) {
+                    const uint32_t b = a ^ jj;
+                    if (b > a && (ks[a] > ks[b]) == ((a & kk) == 0)) {
+                        const uint64_t tk = ks[a], tv = vs[a];
+                        ks[a] = ks[b];
+                        vs[a] = vs[b];
+                        ks[b] = tk;
+                        vs[b] = tv;
+                    }
+                }
+                __syncthreads();
+            }
+        for (uint32_t k = threadIdx.x; k < n; k += kPLruSortThreads) rec[k] = PLruRec{vs[k], ks[k]};
+    } else {
+        for (uint32_t k = n + threadIdx.x; k < np2; k += kPLruSortThreads) rec[k] = PLruRec{0, ~0ull};
+        __syncthreads();
+        for (uint32_t kk = 2; kk <= np2; kk <<= 1)
+            for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+                for (uint32_t a = threadIdx.x; a < np2; a += kPLruSortThreads) {
+                    const uint32_t b = a ^ jj;
+                    if (b > a) {
+                        const PLruRec x = rec[a], y = rec[b];
+                        if ((x.stamp > y.stamp) == ((a & kk) == 0)) {
+                            rec[a] = y;
+                            rec[b] = x;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        st.lpool[q] = PLruRec{0, n};
+        st.psize[P.boff + j] = n;
     }
 }
 
@@ -4020,6 +4153,22 @@ void cparam_stage1(const CParamState &st, BatchScratch &sc, CParamScratch &ps, c
     hipLaunchKernelGGL(k_pkeys, dim3(nb), dim3(kThreads), 0, s, st, sc.el[0], voff, values, n, invalid_key, ps.vkey);
     hipLaunchKernelGGL(k_ppath, dim3(nb), dim3(kThreads), 0, s, st, sc.el[0], ps.els[0], voff, ps.vkey, acquire,
                        ts_base, ts_off, n, invalid_key, st.kmask + 1);
+    cparam_lru_decide(st, s);
+}
+
+void cparam_lru_decide(const CParamState &st, hipStream_t s) {
+    if (st.nslots == 0) return;
+    SGA_HIP_CHECK(hipMemsetAsync(st.ctl + 4, 0, 4, s));
+    hipLaunchKernelGGL(k_plru_decide, dim3((st.nslots + kThreads - 1) / kThreads), dim3(kThreads), 0, s, st);
+}
+
+void cparam_lru_switch(const CParamState &st, const uint64_t *d_qoff, uint32_t nsw, uint32_t max_s, hipStream_t s) {
+    if (nsw == 0) return;
+    hipLaunchKernelGGL(k_plru_alloc, dim3(nsw), dim3(kThreads), 0, s, st, d_qoff, nsw);
+    const uint32_t nk = st.kmask + 1;
+    hipLaunchKernelGGL(k_plru_collect, dim3(std::min<uint32_t>((nk + kThreads - 1) / kThreads, 4096)), dim3(kThreads),
+                       0, s, st);
+    hipLaunchKernelGGL(k_plru_sort, dim3(nsw, max_s), dim3(kPLruSortThreads), 0, s, st, nsw);
 }
 
 void cparam_stage2(const CParamState &st, BatchScratch &sc, CParamScratch &ps, const int32_t *acquire,

@@ -347,10 +347,10 @@ void cparam_sum(const CParamState &st, uint32_t slot, int64_t value, int64_t now
 void cparam_init_rule(const CParamState &st, uint32_t slot, hipStream_t s);
 // CacheMap capacity: rules whose key count passed their capacity switch to LRU mode (the sequential
 // path from then on).  decide lists them (count in ctl[4]); the host assigns each an area of S x
-// (2 cap + 3) records (qoff, one per listed rule) and calls switch, which fills the areas from the
-// access stamps.
+// (2 cap + 3) records (qoff, one per listed rule; max_s = their largest S) and calls switch, which
+// fills the areas from the access stamps.
 void cparam_lru_decide(const CParamState &st, hipStream_t s);
-void cparam_lru_switch(const CParamState &st, const uint64_t *d_qoff, uint32_t nsw, hipStream_t s);
+void cparam_lru_switch(const CParamState &st, const uint64_t *d_qoff, uint32_t nsw, uint32_t max_s, hipStream_t s);
 // ClusterParamMetric.getTopValues(number) of one rule at now: d_list holds 2 x (kmask + 1) int64.
 void cparam_top_values(const CParamState &st, uint32_t slot, int64_t now, uint32_t number, int64_t *d_list,
                        uint32_t *d_count, int64_t *d_val, double *d_qps, uint32_t *d_n, hipStream_t s);

@@ -43,6 +43,7 @@ struct PSlotHost {
     int threshold_type = 0;
     int S = 0, interval = 0;  // metric geometry, fixed at creation
     uint32_t boff = 0;
+    uint32_t cap = 4000;     // each bucket map's maxCapacity, fixed at creation
     std::vector<std::pair<int64_t, int32_t>> hot;  // ascending value
 };
 
@@ -169,6 +170,12 @@ struct Engine {
     DevBuf<int64_t> d_top_list, d_top_val;
     DevBuf<double> d_top_qps;
     DevBuf<uint32_t> d_top_n;
+    // CacheMap capacity (cparam_exact.hpp): per slot key counts, per bucket LRU queue areas and sizes
+    uint32_t pcap_default = 4000;  // ClusterParamMetric.DEFAULT_CLUSTER_MAX_CAPACITY
+    DevBuf<uint32_t> d_pnkeys, d_ppsize, d_psw;
+    DevBuf<uint64_t> d_ppq, d_pqoff;
+    DevBuf<PLruRec> d_plpool;
+    uint64_t plpool_used = 0;
 
     // ---- cluster concurrency tokens
     DevBuf<ConcParam> d_cparam;   // per slot
@@ -269,7 +276,37 @@ struct Engine {
         st.krec = d_krec.p;
         st.krec_cap = d_krec.n;
         st.ctl = d_pctl.p;
+        st.nkeys = d_pnkeys.p;
+        st.pq = d_ppq.p;
+        st.psize = d_ppsize.p;
+        st.lpool = d_plpool.p;
+        st.sw_list = d_psw.p;
+        st.seq = flow.seq;  // one access order with the local path's embedded-server calls
         return st;
+    }
+
+    // Rules the last stage-1 / count pass listed (ctl[4] of them, nsw > 0) switch to LRU mode: each gets
+    // S queue areas of 2 cap + 3 records from the pool, filled from the keys' access stamps.
+    void cparam_lru_switch_host(uint32_t nsw, hipStream_t s) {
+        std::vector<uint32_t> lst(nsw);
+        SGA_HIP_CHECK(hipMemcpyAsync(lst.data(), d_psw.p, nsw * 4, hipMemcpyDeviceToHost, s));
+        SGA_HIP_CHECK(hipStreamSynchronize(s));
+        std::vector<uint64_t> qoff(nsw);
+        uint64_t need = 0;
+        uint32_t max_s = 1;
+        for (uint32_t w = 0; w < nsw; ++w) {
+            const PSlotHost &h = pslots[lst[w]];
+            max_s = std::max<uint32_t>(max_s, (uint32_t)h.S);
+            qoff[w] = plpool_used + need;
+            need += (uint64_t)h.S * (2ull * h.cap + 3);
+        }
+        if (d_plpool.n < plpool_used + need) d_plpool.grow(std::max<uint64_t>(plpool_used + need, 2 * d_plpool.n), s);
+        plpool_used += need;
+        if (d_pqoff.n < nsw) d_pqoff.alloc(std::max<size_t>(nsw, 2 * d_pqoff.n));
+        SGA_HIP_CHECK(hipMemcpyAsync(d_pqoff.p, qoff.data(), nsw * 8, hipMemcpyHostToDevice, s));
+        cparam_lru_switch(pstate(), d_pqoff.p, nsw, max_s, s);
+        SGA_HIP_CHECK(hipMemsetAsync(d_pctl.p + 4, 0, 4, s));
+        SGA_HIP_CHECK(hipStreamSynchronize(s));
     }
 
     // key store + batch scratch of the param path, created with the first param rules
@@ -283,7 +320,7 @@ struct Engine {
         d_koff.alloc(cap);
         d_kslot.alloc(cap);
         d_kval.alloc(cap);
-        d_krec.alloc((size_t)keys * 20);  // 2 x 10 buckets per key on average
+        d_krec.alloc((size_t)keys * 30);  // 3 x 10 buckets per key on average
         d_pctl.alloc(8);
         SGA_HIP_CHECK(hipMemsetAsync(d_vtab.p, 0x00, d_vtab.bytes(), stream));
         std::vector<int64_t> empty(d_vtab.n, INT64_MIN);  // kAbsent = empty value slot
@@ -308,8 +345,21 @@ struct Engine {
             d_ptmax.grow(c, stream);
             d_pcoupled.grow(c, stream);
         }
+        if (d_pnkeys.n < d_pparam.n) {  // new slots: no keys, free mode
+            const size_t o = d_pnkeys.n;
+            d_pnkeys.grow(d_pparam.n, stream);
+            SGA_HIP_CHECK(hipMemsetAsync(d_pnkeys.p + o, 0, (d_pnkeys.n - o) * 4, stream));
+            d_psw.alloc(d_pparam.n);
+        }
         if (d_prstart.n < std::max<uint32_t>(pbucket_used, 1))
             d_prstart.grow(std::max<size_t>(pbucket_used, d_prstart.n * 2), stream);
+        if (d_ppq.n < d_prstart.n) {
+            const size_t o = d_ppq.n;
+            d_ppq.grow(d_prstart.n, stream);
+            d_ppsize.grow(d_prstart.n, stream);
+            SGA_HIP_CHECK(hipMemsetAsync(d_ppq.p + o, 0xFF, (d_ppq.n - o) * 8, stream));  // kPNoQueue
+            SGA_HIP_CHECK(hipMemsetAsync(d_ppsize.p + o, 0, (d_ppsize.n - o) * 4, stream));
+        }
         std::vector<PRuleParam> hp(ns);
         std::vector<int64_t> hv;
         std::vector<int32_t> hc;
@@ -326,6 +376,7 @@ struct Engine {
             q.active = h.active ? 1 : 0;
             q.ns = h.ns;
             q.threshold_type = h.threshold_type;
+            q.cap = h.cap;
             q.hot_off = (uint32_t)hv.size();
             q.n_hot = (uint32_t)h.hot.size();
             for (auto &kv : h.hot) {
@@ -1349,6 +1400,7 @@ int sga_load_cluster_param_rules(sga_engine *e, const char *ns, const sga_cluste
                 h.S = geo.sample_count;
                 h.interval = geo.window_interval_ms;
                 h.boff = g.pbucket_used;
+                h.cap = g.pcap_default;
                 g.pbucket_used += (uint32_t)h.S;
                 g.pslot_of[fid] = sl;
                 fresh.push_back(sl);
@@ -1422,7 +1474,7 @@ int sga_request_param_tokens(sga_engine *e, const int64_t *flow_id, const int32_
             const sga::CParamState st = g.pstate();
             sga::cparam_stage1(st, g.scratch, g.pscratch, g.d_in_fid.p, g.d_in_acq.p, g.d_in_voff.p, g.d_in_vals.p, lo,
                                g.d_in_ts.p, (uint32_t)m, g.d_out.p, g.stream, lims.data(), (int)lims.size());
-            uint32_t ctl[4];
+            uint32_t ctl[5];
             SGA_HIP_CHECK(hipMemcpyAsync(ctl, g.d_pctl.p, sizeof(ctl), hipMemcpyDeviceToHost, g.stream));
             SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
             if (ctl[1]) {
@@ -1430,13 +1482,29 @@ int sga_request_param_tokens(sga_engine *e, const int64_t *flow_id, const int32_
                                      : "cluster parameter record pool full (raise sga_config.max_param_keys)";
                 return SGA_ENOMEM;
             }
+            if (ctl[4]) g.cparam_lru_switch_host(ctl[4], g.stream);
             sga::cparam_stage2(st, g.scratch, g.pscratch, g.d_in_acq.p, g.d_in_voff.p, g.d_in_vals.p, lo, g.d_in_ts.p,
                                (uint32_t)m, ctl[2], g.d_out.p, g.stream);
             SGA_HIP_CHECK(hipGetLastError());
             SGA_HIP_CHECK(hipMemcpyAsync(out + b, g.d_out.p, m * 8, hipMemcpyDeviceToHost, g.stream));
+            uint32_t err = 0;
+            SGA_HIP_CHECK(hipMemcpyAsync(&err, g.d_pctl.p + 1, 4, hipMemcpyDeviceToHost, g.stream));
             SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+            g.flow.seq += m;  // access stamps of the next call come after these
+            if (err & 4) {
+                g.err = "cluster parameter LRU queue check failed";
+                return SGA_ENOMEM;
+            }
             b += m;
         }
+        return SGA_OK;
+    });
+}
+
+int sga_cluster_set_param_capacity(sga_engine *e, uint32_t capacity) {
+    if (capacity > (1u << 24)) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        g.pcap_default = capacity ? capacity : 4000;
         return SGA_OK;
     });
 }
@@ -1450,6 +1518,7 @@ int sga_cluster_param_sum(sga_engine *e, int64_t flow_id, int64_t value, int64_t
         sga::cparam_sum(g.pstate(), it->second, value, now, g.d_tmp7.p, g.stream);
         SGA_HIP_CHECK(hipMemcpyAsync(out, g.d_tmp7.p, 8, hipMemcpyDeviceToHost, g.stream));
         SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        g.flow.seq += 1;  // getSum's gets are accesses
         return SGA_OK;
     });
 }
@@ -1765,8 +1834,19 @@ int sga_load_degrade_rules(sga_engine *e, const sga_degrade_rule *rules, size_t 
 // (the local path does not apply GlobalRequestLimiter)
 static int cluster_param_plumb(Engine &g) {
     g.flow.cparam_st = sga::CParamState{};
+    g.flow.cparam_hook = nullptr;
     if (!g.flow.has_cluster_prules || g.cluster_server != 1) return SGA_OK;
-    if (g.d_pctl.p) g.flow.cparam_st = g.pstate();
+    if (g.d_pctl.p) {
+        g.flow.cparam_st = g.pstate();
+        g.flow.cparam_hook = [&g](hipStream_t s) {  // after the local count pass created this batch's keys
+            sga::cparam_lru_decide(g.pstate(), s);
+            uint32_t ctl[5];
+            SGA_HIP_CHECK(hipMemcpyAsync(ctl, g.d_pctl.p, sizeof(ctl), hipMemcpyDeviceToHost, s));
+            SGA_HIP_CHECK(hipStreamSynchronize(s));
+            if (ctl[4]) g.cparam_lru_switch_host(ctl[4], s);
+            g.flow.cparam_st = g.pstate();  // the pool may have moved
+        };
+    }
     for (const sga_param_rule &r : g.flow.h_prule_src) {
         if (!r.cluster_mode) continue;
         auto it = g.pslot_of.find(r.cluster_flow_id);

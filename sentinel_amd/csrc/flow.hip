@@ -848,7 +848,8 @@ __device__ int8_t chain_entry(const Ctx &c, uint32_t r, const ResMem &m, int64_t
             // toCollection(value)) to the embedded server, in event order; OK passes, BLOCKED blocks,
             // anything else -- or no token service -- falls back (fallbackToLocalOrPass, :335-343)
             int8_t ts = TRS_FAIL;
-            if (c.st.cluster_on) ts = (int8_t)(cparam_request_exact(c.st.cpst, p.cflow, acquire, vals, nv, t) >> 48);
+            if (c.st.cluster_on)
+                ts = (int8_t)(cparam_request_exact(c.st.cpst, p.cflow, acquire, vals, nv, t, eidx) >> 48);
             if (ts == TRS_OK) ok = true;
             else if (ts == TRS_BLOCKED) ok = false;
             else ok = p.cfallback ? param_local_check<kLru>(c, r, p, idx, vals, nv, acquire, t, &total_wait, eidx) : true;
@@ -3531,6 +3532,18 @@ __global__ __launch_bounds__(kT) void k_lru_count(FlowState st, const uint8_t *_
                 if (idx < 0) idx = (-idx <= (int32_t)nargs) ? (int32_t)nargs + idx : -idx;
             }
             if (idx >= 0 && idx < kMaxParamIdx) kmask |= 1ull << idx;
+            if (!kCount && p.cluster && p.grade == 1 && st.cluster_on && st.cpst.ctl && kind[i] == 0 &&
+                (int64_t)nargs > (int64_t)idx) {
+                // the embedded server's keys of this call (their count decides the CacheMap switch)
+                const uint32_t slot = prule_lookup(st.cpst, p.cflow);
+                const uint64_t *vals;
+                uint32_t nv;
+                if (slot != 0xFFFFFFFFu && st.cpst.param[slot].active && ev_arg(pa, (uint32_t)idx, pv, &vals, &nv) != ARG_NULL)
+                    for (uint32_t q = 0; q < nv; ++q) {
+                        const uint32_t vid = vid_of(st.cpst, (int64_t)vals[q], true);
+                        if (vid != 0xFFFFFFFFu) key_of(st.cpst, slot, vid, (int64_t)vals[q], true);
+                    }
+            }
             if (kind[i] != 0 || p.grade != 1 || st.pq[p.id] != kNoQueue || (int64_t)nargs <= (int64_t)idx) continue;
             const uint64_t *vals;
             uint32_t nv;
@@ -3899,6 +3912,7 @@ FlowState FlowEngine::state() const {
     s.gate = nullptr;
     s.tmapmask = d_tmapmask.p;
     s.cpst = cparam_st;
+    s.cpst.seq = seq;  // access stamps of the embedded server's parameter maps: this batch's events
     // CacheMap capacity (null until parameter rules are loaded)
     const bool lru = d_psize.p != nullptr;
     s.pstamp = lru ? d_pstamp.p : nullptr;
@@ -4029,6 +4043,7 @@ void FlowEngine::lru_prepare(const uint8_t *kind, const uint32_t *resource, cons
     hipLaunchKernelGGL(k_lru_decide, dim3((no + kT - 1) / kT), dim3(kT), 0, s, st);
     hipLaunchKernelGGL(k_lru_collect, dim3(2048), dim3(kT), 0, s, st);
     hipLaunchKernelGGL(k_lru_sort, dim3(64), dim3(kLruSortThreads), 0, s, st);
+    if (cparam_hook && has_cluster_prules && cluster_on && cparam_st.ctl) cparam_hook(s);
     static const int dbg = getenv("SGA_LRU_DEBUG") ? atoi(getenv("SGA_LRU_DEBUG")) : 0;  // diagnostics only
     if (dbg) {
         uint32_t ctl[4];

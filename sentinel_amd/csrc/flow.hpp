@@ -229,6 +229,9 @@ struct FlowEngine {
     int lru_error(hipStream_t s);   // sticky queue errors (host wait)
     CParamState cparam_st{};      // set before each batch (the engine's cluster parameter state)
     bool has_cluster_prules = false;
+    // after the count pass (which creates the cluster-mode rules' keys): the engine switches cluster
+    // parameter rules past their CacheMap capacity to LRU mode and refreshes cparam_st (host wait)
+    std::function<void(hipStream_t)> cparam_hook;
     // upper bounds of the keys held by the parameter / thread-count maps (exact after a count);
     // the maps are rehashed into more room before a batch could fill them past a quarter
     size_t pkeys_ub = 0, tkeys_ub = 0;

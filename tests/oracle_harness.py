@@ -136,6 +136,7 @@ def lib():
         "orc_cluster_request_param_token": (OrcTokenResult, [P, I64, I32, P, C.c_size_t, I64]),
         "orc_cluster_param_replay": (None, [P, C.c_size_t, P, P, P, P, P, P]),
         "orc_cluster_param_sum": (I64, [P, I64, I64, I64]),
+        "orc_cluster_set_param_capacity": (None, [C.c_size_t]),
         "orc_flow_load_system_rules": (C.c_int, [P, C.POINTER(OrcSystemRule), C.c_size_t]),
         "orc_flow_set_system_status": (None, [P, D, D]),
         "orc_flow_entry_x": (C.c_int, [P, U32, I64, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, C.POINTER(I64)]),

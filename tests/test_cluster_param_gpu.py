@@ -2,8 +2,9 @@
 DefaultTokenService.requestParamToken -> ClusterParamFlowChecker over ClusterParamMetric,
 HIP engine (through the C-ABI) against the oracle's single-threaded replay on the same ordered
 trace under a mocked clock.  Decisions (status, remaining) and ClusterParamMetric sums must be
-bit-exact.  Parity is pinned while a bucket holds <= 4000 distinct values (no LRU eviction,
-SURVEY.md §8(c)); every trace here stays below that."""
+bit-exact.  Each bucket map is a strict LRU of capacity 4000 (ClusterParamMetric.java:37-88): the
+cparamlru_* vectors (tests/golden/make_cparam_lru_golden.py, an independent model; CLHM itself is not
+vendored) and the small-capacity traces below evict."""
 import ctypes as C
 
 import numpy as np
@@ -198,4 +199,69 @@ def test_mixed_paths_limiter_and_reload(cm):
     fid2 = np.where(fid[4000:] == 13, 16, fid[4000:])
     p.run(fid2, acq[4000:], params[4000:], ts[4000:], "after reload")
     p.check_sums([(f, v) for f in (1, 2, 10, 11, 16) for v in range(0, 30, 3)], int(ts[-1]))
+    p.close()
+
+
+@pytest.mark.parametrize("name", ["exhaust_then_evict", "exhaust_no_evict_at_capacity", "blocked_get_moves_to_mru",
+                                  "two_buckets", "random_stream"])
+def test_lru_golden_vectors(cm, name):
+    """More than 4000 values a bucket at the default capacity: the engine against the vectors and the oracle.
+    The first batches stay under 4000 keys (key-parallel path, access stamps only); the batch whose keys
+    pass the capacity switches the rule to LRU mode from those stamps."""
+    from tests.test_cluster_param_oracle import golden_rule, load_lru_golden
+    doc = load_lru_golden(name)
+    p = Pair(cm)
+    p.load("default", [golden_rule(doc)])
+    ev = doc["events"]
+    n = len(ev)
+    fid = np.full(n, doc["flow_id"], np.int64)
+    acq = np.full(n, doc["acquire"], np.int64)
+    ts = np.array([t for _, t in ev], np.int64)
+    params = [[v] for v, _ in ev]
+    exp = np.array(doc["expect"], np.int64)
+    cuts = [0, n // 8, n // 3, n]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        got = p.run(fid[a:b], acq[a:b], params[a:b], ts[a:b], f"{name} batch@{a}")
+        st = np.asarray(got["status"], np.int64)
+        rem = np.asarray(got["remaining"], np.int64)
+        bad = np.nonzero((st != exp[a:b, 0]) | (rem != exp[a:b, 1]))[0]
+        assert bad.size == 0, (name, a + int(bad[0]), st[bad[0]], rem[bad[0]], exp[a + bad[0]])
+    for v, t, sm in doc["sums"]:
+        assert p.mgr.param_sum(doc["flow_id"], v, t) == sm, (v, t, sm)
+    p.close()
+
+
+def test_lru_small_capacity_mixed(cm):
+    """Capacity 40 (the maxCapacity constructor argument): several rules and geometries, both paths, a
+    rule switching mid-stream, collections, time going backwards, acquire counts beyond the packed field,
+    getSum calls (accesses) and getTopValues between batches -- decisions, sums and top values bit-exact."""
+    rng = np.random.default_rng(29)
+    L = H.lib()
+    p = Pair(cm)
+    p.mgr.set_param_capacity(40)
+    L.orc_cluster_set_param_capacity(40)
+    try:
+        p.load("default", [{"flow_id": f, "count": float(rng.integers(2, 6)), "threshold_type": 1,
+                            "sample_count": [1, 2, 5, 10][f % 4], "window_interval_ms": 1000,
+                            "hot": {1: 9} if f % 3 == 0 else {}} for f in range(1, 9)])
+    finally:
+        L.orc_cluster_set_param_capacity(0)
+    p.mgr.set_param_capacity(0)
+    n = 24000
+    fid = rng.integers(1, 9, size=n)
+    dom = np.where(fid <= 2, 30, np.where(fid <= 5, 120, 600))  # rules 1-2 never pass their capacity
+    ts = T0 + np.cumsum(rng.integers(0, 2, size=n) * (rng.random(n) < 0.4))
+    acq = np.where(rng.random(n) < 0.97, 1, rng.integers(2, 200, size=n))
+    params = [[int(rng.integers(0, d))] for d in dom]
+    for lo in range(0, n, 3000):
+        sl = slice(lo, lo + 3000)
+        f, a, t, pr = fid[sl].copy(), acq[sl].copy(), ts[sl].copy(), params[sl]
+        if lo >= 12000:  # sequential path for everyone: collections and time going backwards
+            pr = [q if rng.random() < 0.8 else q + [int(rng.integers(0, 50))] for q in pr]
+            back = rng.random(len(t)) < 0.02
+            t[back] -= rng.integers(1, 700, size=int(back.sum()))
+        p.run(f, a, pr, t, f"batch@{lo}")
+        now = int(t.max())
+        p.check_sums([(ff, v) for ff in range(1, 9) for v in (0, 1, 7, 19)], now)
+        p.check_top(range(1, 9), now, number=8)
     p.close()

@@ -5,6 +5,7 @@ several values, AVG_LOCAL thresholds scaled by the connected count, validation c
 import ctypes as C
 
 import numpy as np
+import pytest
 
 from tests import oracle_harness as H
 
@@ -99,3 +100,64 @@ def test_top_values():
     assert L.orc_cluster_param_top_values(h, 11, T0 + 5000, 8, vals, qps) == 0
     assert L.orc_cluster_param_top_values(h, 99, T0, 8, vals, qps) == 0  # no metric
     L.orc_cluster_free(h)
+
+
+def test_bucket_map_lru_small_capacity():
+    """Each bucket map is a strict LRU (ClusterParamMetric.java:37-88): capacity 3, one bucket, count 2.
+    getSum's get and addValue's putIfAbsent are accesses; a new value into a full map evicts the least
+    recently accessed one, whose count is gone (hand-derived sequence)."""
+    L = H.lib()
+    L.orc_cluster_set_param_capacity(3)
+    try:
+        L2, h, _ = make([{"flow_id": 5, "count": 2, "threshold_type": 1, "sample_count": 1,
+                          "window_interval_ms": 1000}])
+    finally:
+        L.orc_cluster_set_param_capacity(0)
+    seq = [1, 2, 3, 1, 4, 2, 1, 5, 4, 3, 1]
+    got = [req(L, h, 5, 1, [v], T0 + i) for i, v in enumerate(seq)]
+    # t3: value 1 read+added (order 2,3,1); t4: 4 evicts 2; t5: 2 is new again (evicts 3);
+    # t6: value 1 at 2 -> blocked, but its get moves it to the MRU end; t7: 5 evicts 4; t8: 4 evicts 2;
+    # t9: 3 evicts 1; t10: value 1 is new again
+    assert got == [(0, 1), (0, 1), (0, 1), (0, 0), (0, 1), (0, 1), (1, 0), (0, 1), (0, 1), (0, 1), (0, 1)]
+    assert [L.orc_cluster_param_sum(h, 5, v, T0 + 20) for v in (1, 2, 3, 4, 5)] == [1, 0, 1, 1, 0]
+    L.orc_cluster_free(h)
+
+
+@pytest.mark.parametrize("name", ["exhaust_then_evict", "exhaust_no_evict_at_capacity", "blocked_get_moves_to_mru",
+                                  "two_buckets", "random_stream"])
+def test_lru_golden_vectors(name):
+    """The oracle's bucket maps (capacity 4000) against the independent strict-LRU model's vectors
+    (tests/golden/make_cparam_lru_golden.py)."""
+    doc = load_lru_golden(name)
+    L, h, _ = make([golden_rule(doc)])
+    ev = doc["events"]
+    n = len(ev)
+    fid = np.full(n, doc["flow_id"], np.int64)
+    acq = np.full(n, doc["acquire"], np.int32)
+    ts = np.array([t for _, t in ev], np.int64)
+    off = np.arange(n + 1, dtype=np.uint32)
+    vals = np.array([v for v, _ in ev], np.int64)
+    out = (H.OrcTokenResult * n)()
+    L.orc_cluster_param_replay(h, n, fid.ctypes.data, acq.ctypes.data, off.ctypes.data, vals.ctypes.data,
+                               ts.ctypes.data, out)
+    ref = np.frombuffer(out, dtype=np.int32).reshape(-1, 3)[:, :2]
+    exp = np.array(doc["expect"], np.int32)
+    bad = np.nonzero((ref != exp).any(axis=1))[0]
+    assert bad.size == 0, (name, bad[:5], ref[bad[:5]], exp[bad[:5]])
+    for v, t, s in doc["sums"]:
+        assert L.orc_cluster_param_sum(h, doc["flow_id"], v, t) == s, (v, t, s)
+    L.orc_cluster_free(h)
+
+
+def load_lru_golden(name):
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", f"cparamlru_{name}.json")) as fh:
+        return json.load(fh)
+
+
+def golden_rule(doc):
+    r = doc["rule"]
+    return {"flow_id": doc["flow_id"], "count": float(r["count"]), "threshold_type": 1,
+            "sample_count": r["sample_count"], "window_interval_ms": r["window_interval_ms"],
+            "hot": {int(k): v for k, v in r.get("hot", {}).items()}}

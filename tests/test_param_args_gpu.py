@@ -87,13 +87,14 @@ def test_sticky_index_on_parallel_paths():
     eng.close()
 
 
-@pytest.mark.parametrize("server", [1, 0])
-def test_cluster_mode_param_rules(server):
+@pytest.mark.parametrize("server,cap", [(1, None), (0, None), (1, 6)])
+def test_cluster_mode_param_rules(server, cap):
     """Cluster-mode QPS parameter rules (ParamFlowChecker.passClusterCheck, :305-333): with the embedded server
     the same engine's cluster parameter path (requestParamToken -> ClusterParamFlowChecker) decides in event
     order -- OK passes, BLOCKED blocks, NO_RULE_EXISTS (a flowId without a cluster rule) falls back to the
     local check or passes (fallbackToLocalOrPass, :335-343); without a server every rule falls back.
-    Decisions, node views and the cluster parameter metrics equal the oracle."""
+    Decisions, node views and the cluster parameter metrics equal the oracle.  cap: the embedded server's
+    bucket maps hold 6 values (ClusterParamMetric maxCapacity), so they evict in LRU order."""
     from sentinel_amd import cluster as CL
     from sentinel_amd.local import ClusterStateManager
     from tests.test_cluster_param_gpu import to_param_rules
@@ -114,17 +115,24 @@ def test_cluster_mode_param_rules(server):
     srv_g = L.orc_cluster_new(1.0, 1.0)
     srv = L.orc_cluster_new(1.0, 1.0)
     keep = []
-    for h in (srv_g, srv):
-        arr = H.cluster_param_rules_array(crules, keep)
-        L.orc_cluster_load_param_rules(h, b"default", arr, len(crules))
+    H.lib().orc_cluster_set_param_capacity(cap or 0)
+    try:
+        for h in (srv_g, srv):
+            arr = H.cluster_param_rules_array(crules, keep)
+            L.orc_cluster_load_param_rules(h, b"default", arr, len(crules))
+    finally:
+        H.lib().orc_cluster_set_param_capacity(0)
     gen = lt.Oracle(n_res, [], rules)
     L.orc_flow_set_cluster(gen.h, srv_g, server)
-    st = lt.generate_args(gen, n_res, 5000, seed=13 + server, t0=T0, gap_mean=0.5, max_args=2, domain=4)
+    domain = 4 if cap is None else 24
+    st = lt.generate_args(gen, n_res, 5000, seed=13 + server, t0=T0, gap_mean=0.5, max_args=2, domain=domain)
     gen.close()
     orc = lt.Oracle(n_res, [], rules)
     L.orc_flow_set_cluster(orc.h, srv, server)
     exp = orc.replay(st)
     eng, s = _sentinel(n_res, 1 << 14)
+    if cap is not None:
+        CL.ClusterParamFlowRuleManager(eng).set_param_capacity(cap)
     CL.ClusterParamFlowRuleManager(eng).load_rules("default", to_param_rules(CL, crules))  # embedded server's rules
     _load_cluster_params(s, rules)
     if server:
@@ -135,7 +143,7 @@ def test_cluster_mode_param_rules(server):
     _assert_nodes(s, orc, n_res, t_end)
     pm = CL.ClusterParamFlowRuleManager(eng)
     for c in crules:
-        for v in range(4):
+        for v in range(domain):
             assert pm.param_sum(c["flow_id"], v, t_end) == L.orc_cluster_param_sum(srv, c["flow_id"], v, t_end), (c, v)
     d = exp[0][st["kind"] == 0]
     assert (d == 0).any() and (d == 2).any()
