@@ -1471,7 +1471,7 @@ int sga_request_param_tokens(sga_engine *e, const int64_t *flow_id, const int32_
             if (nv)
                 SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_vals.p, values + value_offsets[b], (size_t)nv * 8,
                                              hipMemcpyHostToDevice, g.stream));
-            const sga::CParamState st = g.pstate();
+            sga::CParamState st = g.pstate();
             sga::cparam_stage1(st, g.scratch, g.pscratch, g.d_in_fid.p, g.d_in_acq.p, g.d_in_voff.p, g.d_in_vals.p, lo,
                                g.d_in_ts.p, (uint32_t)m, g.d_out.p, g.stream, lims.data(), (int)lims.size());
             uint32_t ctl[5];
@@ -1482,7 +1482,10 @@ int sga_request_param_tokens(sga_engine *e, const int64_t *flow_id, const int32_
                                      : "cluster parameter record pool full (raise sga_config.max_param_keys)";
                 return SGA_ENOMEM;
             }
-            if (ctl[4]) g.cparam_lru_switch_host(ctl[4], g.stream);
+            if (ctl[4]) {
+                g.cparam_lru_switch_host(ctl[4], g.stream);
+                st = g.pstate();  // the queue pool may have moved
+            }
             sga::cparam_stage2(st, g.scratch, g.pscratch, g.d_in_acq.p, g.d_in_voff.p, g.d_in_vals.p, lo, g.d_in_ts.p,
                                (uint32_t)m, ctl[2], g.d_out.p, g.stream);
             SGA_HIP_CHECK(hipGetLastError());
