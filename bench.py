@@ -422,9 +422,11 @@ def run_e2e(L, eng, bats, dev):
         total += n
     return {"value": total / secs, "unit": "decisions/s", "batches": len(hosts), "requests": total,
             "ms_per_batch": secs / len(hosts) * 1e3,
-            "bytes_pcie_per_request": 8 + 4 + 1 + 8 + 12,
+            "bytes_pcie_per_request": 8 + 4 + 1 + 8 + 8,
             "what": "sga_request_tokens over pageable host buffers (int64 flowId, int32 acquire, uint8 prio, "
-                    "int64 ts in; 12-B TokenResult out): H2D + pipeline + D2H per batch, synchronous, one GPU; "
+                    "int64 ts in; 8-B TokenResult out): host threads stage 2^20-request chunks through page-locked "
+                    "slots while the DMA engine moves the previous chunk, then the pipeline, then the results back "
+                    "the same way (engine.cpp run_host_batch_pipelined); one call per batch, synchronous, one GPU; "
                     "the batches that follow the timed ones in virtual time"}
 
 

@@ -4236,6 +4236,16 @@ void cluster_metric_nodes(const ClusterState &st, const int64_t *slot_fid, int64
                        slot_fid, now, (sga_cluster_metric_node *)out, cap, count);
 }
 
+__global__ __launch_bounds__(kThreads) void k_ts_offsets(const int64_t *__restrict__ ts, int64_t lo,
+                                                         uint32_t *__restrict__ off, uint32_t n) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i < n) off[i] = (uint32_t)(ts[i] - lo);
+}
+
+void cluster_ts_offsets(const int64_t *ts, int64_t lo, uint32_t *off, uint32_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_ts_offsets, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, ts, lo, off, n);
+}
+
 void cluster_init_limiter(NsLimiterDev *d, hipStream_t s) {
     hipLaunchKernelGGL(k_lim_init, dim3(1), dim3(64), 0, s, d);
 }

@@ -329,6 +329,9 @@ struct CParamScratch {
     uint32_t *vkey;           // per value of the batch: kidx
 };
 
+// off[i] = ts[i] - lo (the host checked that the span fits u32): host-buffer batches ship int64 times
+void cluster_ts_offsets(const int64_t *ts, int64_t lo, uint32_t *off, uint32_t n, hipStream_t s);
+
 size_t cparam_scratch_bytes(size_t cap);
 void cparam_scratch_carve(CParamScratch &ps, void *base, size_t cap);
 

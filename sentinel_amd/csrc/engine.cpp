@@ -8,6 +8,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <memory>
 #include <thread>
 #include <cstring>
@@ -34,6 +36,64 @@ struct SlotHost {
 
 // Cluster parameter rule slot (ClusterParamFlowRuleManager PARAM_RULES + ClusterParamMetricStatistics).
 // Slots are never reused: keys (rule slot, value) of a dropped metric can never match a new one.
+// A few persistent host threads for the page-locked staging copies of large host-buffer batches
+// (run_host_batch): run(f) calls f(t) for t in [0, size()) on them and returns when all are done.
+class HostPool {
+  public:
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    int size() {
+        if (th_.empty()) start();
+        return (int)th_.size();
+    }
+    void run(const std::function<void(int)> &f) {
+        if (th_.empty()) start();
+        std::unique_lock<std::mutex> l(mu_);
+        job_ = &f;
+        pending_ = (int)th_.size();
+        ++gen_;
+        cv_.notify_all();
+        done_.wait(l, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void start() {
+        int n = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+        if (const char *e = getenv("SGA_HOST_THREADS")) n = std::max(1, std::min(64, atoi(e)));
+        for (int t = 0; t < n; ++t)
+            th_.emplace_back([this, t] {
+                uint64_t seen = 0;
+                for (;;) {
+                    const std::function<void(int)> *f;
+                    {
+                        std::unique_lock<std::mutex> l(mu_);
+                        cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+                        if (stop_) return;
+                        seen = gen_;
+                        f = job_;
+                    }
+                    (*f)(t);
+                    std::lock_guard<std::mutex> l(mu_);
+                    if (--pending_ == 0) done_.notify_one();
+                }
+            });
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)> *job_ = nullptr;
+    uint64_t gen_ = 0;
+    int pending_ = 0;
+    bool stop_ = false;
+};
+
 struct PSlotHost {
     int64_t flow_id = 0;
     bool allocated = false;  // metric exists
@@ -141,6 +201,19 @@ struct Engine {
     // page-locked memory, one copy each way
     static constexpr size_t kSmallStage = 4096;
     PinnedBuf h_stage, h_res;
+    // large host batches: kPipeSlots page-locked chunks of kPipeChunk requests each way, the batch's
+    // int64 times on the device (offsets computed there), the copy threads
+    static constexpr size_t kPipeChunk = 1u << 20, kPipeSlots = 3;
+    PinnedBuf h_pin_in, h_pin_out;
+    DevBuf<int64_t> d_ts64;
+    hipEvent_t ev_pin_in[kPipeSlots] = {}, ev_pin_out[kPipeSlots] = {};
+    HostPool host_pool;
+    ~Engine() {
+        for (size_t s = 0; s < kPipeSlots; ++s) {
+            if (ev_pin_in[s]) (void)hipEventDestroy(ev_pin_in[s]);
+            if (ev_pin_out[s]) (void)hipEventDestroy(ev_pin_out[s]);
+        }
+    }
     DevBuf<uint8_t> d_stage;
     DevBuf<int64_t> d_tmp7;
     DevBuf<NsLimiterDev> d_lim;  // one per namespace index (used when the namespace has a limiter)
@@ -1112,6 +1185,103 @@ int sga_sync(sga_engine *e) {
     });
 }
 
+// One engine batch from host buffers at PCIe rate: the host threads copy chunk c of the inputs into a
+// page-locked slot (and take the times' min / max) while the DMA engine moves chunk c - 1 to the device;
+// the device turns the int64 times into u32 offsets from their minimum; after the pipeline the results
+// come back the same way, chunk by chunk through page-locked slots the threads copy out of.
+// Returns 1 (nothing decided) when the times span more than u32 offsets.
+static int run_host_batch_pipelined(Engine &g, const int64_t *flow_id, const int32_t *acquire, const uint8_t *prio,
+                                    const int64_t *ts, size_t n, uint64_t *out, int simple,
+                                    const std::vector<sga::LimiterPass> &lims) {
+    constexpr size_t C = Engine::kPipeChunk, K = Engine::kPipeSlots;
+    constexpr size_t kIn = 8 + 8 + 4 + 1;  // flowId, time, acquire, prio
+    if (!g.h_pin_in.p) {
+        g.h_pin_in.alloc(K * C * kIn);
+        g.h_pin_out.alloc(K * C * 8);
+        for (size_t s = 0; s < K; ++s) {
+            SGA_HIP_CHECK(hipEventCreateWithFlags(&g.ev_pin_in[s], hipEventDisableTiming));
+            SGA_HIP_CHECK(hipEventCreateWithFlags(&g.ev_pin_out[s], hipEventDisableTiming));
+        }
+    }
+    if (g.d_ts64.n < g.cfg.max_batch) g.d_ts64.alloc(g.cfg.max_batch);
+    sga::HostPool &pool = g.host_pool;
+    const int T = pool.size();
+    std::vector<int64_t> tmin(T), tmax(T);
+    std::vector<uint8_t> tneg(T);
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    bool neg = false;
+    const size_t nch = (n + C - 1) / C;
+    for (size_t c = 0; c < nch; ++c) {
+        const size_t s = c % K, c0 = c * C, m = std::min(C, n - c0);
+        if (c >= K) SGA_HIP_CHECK(hipEventSynchronize(g.ev_pin_in[s]));  // the slot's last copy is done
+        uint8_t *slot = g.h_pin_in.p + s * C * kIn;
+        int64_t *pf = reinterpret_cast<int64_t *>(slot), *pt = reinterpret_cast<int64_t *>(slot + 8 * C);
+        int32_t *pa = reinterpret_cast<int32_t *>(slot + 16 * C);
+        uint8_t *pp = slot + 20 * C;
+        pool.run([&](int t) {
+            const size_t a = m * t / T, b = m * (t + 1) / T;
+            int64_t mn = INT64_MAX, mx = INT64_MIN;
+            for (size_t i = a; i < b; ++i) {
+                const int64_t x = ts[c0 + i];
+                pt[i] = x;
+                mn = std::min(mn, x);
+                mx = std::max(mx, x);
+            }
+            tmin[t] = mn;
+            tmax[t] = mx;
+            tneg[t] = mn < 0;
+            std::memcpy(pf + a, flow_id + c0 + a, (b - a) * 8);
+            std::memcpy(pa + a, acquire + c0 + a, (b - a) * 4);
+            if (prio) std::memcpy(pp + a, prio + c0 + a, b - a);
+        });
+        for (int t = 0; t < T; ++t) {
+            lo = std::min(lo, tmin[t]);
+            hi = std::max(hi, tmax[t]);
+            neg |= tneg[t] != 0;
+        }
+        SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_fid.p + c0, pf, m * 8, hipMemcpyHostToDevice, g.stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(g.d_ts64.p + c0, pt, m * 8, hipMemcpyHostToDevice, g.stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_acq.p + c0, pa, m * 4, hipMemcpyHostToDevice, g.stream));
+        if (prio) SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_prio.p + c0, pp, m, hipMemcpyHostToDevice, g.stream));
+        SGA_HIP_CHECK(hipEventRecord(g.ev_pin_in[s], g.stream));
+    }
+    if (neg || hi - lo > (int64_t)0xFFFFFFFFLL) {
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+        return neg ? SGA_EINVAL : 1;  // LeapArray.currentWindow(t < 0) returns null
+    }
+    if (!prio) SGA_HIP_CHECK(hipMemsetAsync(g.d_in_prio.p, 0, n, g.stream));
+    sga::cluster_ts_offsets(g.d_ts64.p, lo, g.d_in_ts.p, (uint32_t)n, g.stream);
+    sga::cluster_decide_batch(g.state(), g.scratch, g.d_in_fid.p, g.d_in_acq.p, g.d_in_prio.p, lo, g.d_in_ts.p,
+                              (uint32_t)n, simple, g.d_out.p, g.stream, lims.data(), (int)lims.size());
+    SGA_HIP_CHECK(hipGetLastError());
+    auto d2h = [&](size_t c) {
+        const size_t s = c % K, c0 = c * C, m = std::min(C, n - c0);
+        SGA_HIP_CHECK(hipMemcpyAsync(g.h_pin_out.p + s * C * 8, g.d_out.p + c0, m * 8, hipMemcpyDeviceToHost,
+                                     g.stream));
+        SGA_HIP_CHECK(hipEventRecord(g.ev_pin_out[s], g.stream));
+    };
+    for (size_t c = 0; c < std::min(K, nch); ++c) d2h(c);
+    for (size_t c = 0; c < nch; ++c) {
+        const size_t s = c % K, c0 = c * C, m = std::min(C, n - c0);
+        SGA_HIP_CHECK(hipEventSynchronize(g.ev_pin_out[s]));
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(g.h_pin_out.p + s * C * 8);
+        pool.run([&](int t) {
+            const size_t a = m * t / T, b = m * (t + 1) / T;
+            std::memcpy(out + c0 + a, src + a, (b - a) * 8);
+        });
+        if (c + K < nch) d2h(c + K);
+    }
+    if (sga::radix64_lookback()) {
+        uint32_t err = 0;
+        SGA_HIP_CHECK(hipMemcpy(&err, g.scratch.radix.err, 4, hipMemcpyDeviceToHost));
+        if (err) {
+            g.err = "radix look-back timed out";
+            return SGA_EIO;
+        }
+    }
+    return SGA_OK;
+}
+
 static int run_host_batch(Engine &g, const int64_t *flow_id, const int32_t *acquire, const uint8_t *prio,
                           const int64_t *ts, size_t n, uint64_t *out, int simple) {
     SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
@@ -1166,6 +1336,10 @@ static int run_host_batch(Engine &g, const int64_t *flow_id, const int32_t *acqu
             }
             return SGA_OK;
         }
+    }
+    if (n >= Engine::kPipeChunk && n <= cap) {
+        const int rc = run_host_batch_pipelined(g, flow_id, acquire, prio, ts, n, out, simple, lims);
+        if (rc != 1) return rc;  // 1: the batch's times span more than u32 offsets: the chunked path below
     }
     for (size_t b = 0; b < n;) {
         // chunk: at most cap events and a timestamp span that fits u32 offsets

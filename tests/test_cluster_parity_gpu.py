@@ -304,6 +304,35 @@ def test_zipf_c3_slice_bit_exact(eng_mod, hot):
     eng.close()
 
 
+def test_host_batches_pipelined(eng_mod):
+    """Host-buffer batches of more than one staging chunk (2^20 requests) take the page-locked pipeline
+    (engine.cpp run_host_batch_pipelined: chunked H2D / D2H, device-side time offsets), a ragged last
+    chunk included; one whose times span more than u32 offsets takes the chunked path.  Bit-exact
+    against the oracle, metrics included."""
+    from sentinel_amd.workload import ClusterTrace
+    c = eng_mod
+    tr = ClusterTrace(n_rules=50_000, lam=10_000_000)
+    fid_r, cnt = tr.rules()
+    rules = [{"flow_id": int(f), "count": float(x), "threshold_type": 1} for f, x in zip(fid_r, cnt)]
+    oh = oracle_cluster({"default": rules})
+    eng = make_engine(c, hot="on", max_batch=1 << 22, max_rules=1 << 16)
+    c.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_r, cnt)
+    svc = c.DefaultTokenService(eng)
+    lo = 0
+    for k, n in enumerate([3 * (1 << 20) + 12345, 1 << 20, (1 << 20) + 7]):
+        fid, acq, prio, ts = tr.events(lo, n)
+        lo += n
+        if k == 2:  # a jump past the u32 span half way: the chunked path
+            ts = ts.copy()
+            ts[n // 2:] += 1 << 33
+        g = svc.request_tokens(fid, acq, prio, ts)
+        o = oracle_replay(oh, fid, acq, prio, ts)
+        assert_same(g, o, fid, ts, f"host batch {k} ({n} requests)")
+    assert_metrics(c, eng, oh, np.unique(fid)[:100], int(ts[-1]))
+    H.lib().orc_cluster_free(oh)
+    eng.close()
+
+
 def test_rls_descriptors(eng_mod):
     """Envoy RLS: SimpleClusterFlowChecker per descriptor, NO_RULE -> OK, no short-circuit."""
     from sentinel_amd.javautil import rls_key
