@@ -13,6 +13,7 @@ key, 2*S_k) / the GPU time of the steps (torch events on the one stream every ca
 cpu_baseline = the C oracle (oracle/, test infrastructure) replaying a bounded sample of the same
 batch on one host thread."""
 import json
+import os
 import time
 
 import numpy as np
@@ -393,6 +394,13 @@ def run_local(args, cfg_name):
             if bad_d or bad_w:
                 raise AssertionError(f"bench sample differs from the oracle: {parity}")
     eng.close()
+    # HBM traffic per step from the committed rocprofv3 PMC passes of this line (tools/r04_pmc.sh)
+    traffic, traffic_src = None, None
+    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", f"traffic_{cfg_name}.json")
+    if os.path.exists(tpath):
+        with open(tpath) as fh:
+            tj = json.load(fh)
+        traffic, traffic_src = tj["traffic_bytes_per_step"], f"profiles/traffic_{cfg_name}.json ({tj.get('run', '')})"
     return {
         "metric": f"admission decisions/sec, config {cfg_name.upper()} (SURVEY.md 8(d)); % HBM peak",
         "value": n_ent / wall, "unit": "decisions/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -401,7 +409,7 @@ def run_local(args, cfg_name):
         "config": {"workload": cfg["name"], "entries_per_step": b.n, "exits_per_step": n_exit // max(1, args.steps),
                    "resources": cfg["n_res"], "parallelism": "shard1"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "sga_submit_events_device pipeline (entries, then masked exits), torch events on "
                                "the stream every call runs on",
                      "bytes_alg_per_step": bytes_alg / args.steps, "gpu_ms_per_step": gpu_s / args.steps * 1e3,

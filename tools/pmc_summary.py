@@ -28,10 +28,10 @@ ONE_TIME = {"k_init_slots", "k_hot_reset", "k_lds_order_probe", "k_conc_reset", 
 # reads are coalesced streams (input arrays, sort tiles, codes, count rows)
 STREAMING = {"k_hot_key_dense<0>", "k_hot_key_dense<1>", "k_hot_final", "k_rs64_hist<7>", "k_rs64_sweep<7>",
              "k_row_scan", "k_hscan_group", "k_hscan_mid", "k_hscan_down", "k_hot_pre", "k_hot_mode",
-             "k_prio_rank", "k_prio_results"}
+             "k_prio_rank", "k_prio_results", "k_part_colscan", "k_part_binscan", "k_part_scatter"}
 # reads are dominated by random gathers of rule records / parameters
 RANDOM = {"k_cold_fused", "k_hot_flows", "k_hot_precheck", "k_hot_hist", "k_hot_pick", "k_hot_clear", "k_hot_fin",
-          "k_cluster_nodes"}
+          "k_cluster_nodes", "k_hot_final_g"}
 
 
 def base(k):
@@ -70,7 +70,7 @@ def alg_bytes(k, bl):
         return n_cold * 8.0 + (touched - t_hot) * 2 * 704.0
     if b == "k_hot_flows":
         return t_hot * 2 * 704.0
-    if b == "k_hot_final":
+    if b in ("k_hot_final", "k_hot_final_g"):
         return (n - n_cold) * 8.0
     return 0.0
 
@@ -87,6 +87,8 @@ def main():
     ap.add_argument("--cal", default=None, help="calibration JSON (tools/pmc_cal.py) with random-read factors")
     ap.add_argument("--trace", default=None, help="kernel_trace.csv of the same bench for durations")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--all-random", action="store_true",
+                    help="local-path lines: every engine kernel's FETCH_SIZE gets the measured random factor")
     a = ap.parse_args()
 
     agg = defaultdict(lambda: defaultdict(list))
@@ -133,7 +135,7 @@ def main():
         per_step = n_calls / sets
         fr = (sum(cs.get("FETCH_SIZE", [0.0])) / max(1, len(cs.get("FETCH_SIZE", [])))) * 1024.0
         wr = (sum(cs.get("WRITE_SIZE", [0.0])) / max(1, len(cs.get("WRITE_SIZE", [])))) * 1024.0
-        kind = kind_of(k)
+        kind = "random" if a.all_random else kind_of(k)
         fac = 2.0 if kind == "stream" else (rand_factor if kind == "random" else 1.0)
         us = None
         if durations.get(k):
