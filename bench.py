@@ -30,7 +30,8 @@ N_RULES = 1_000_000
 LAMBDA_PER_GPU = 100_000_000
 E_IN, E_OUT, S_FLOW = 12, 8, 704  # token request 12 B, token result 8 B, cluster flow 704 B
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: 8.0 TB/s spec
-E2E_BATCHES = 2                   # host-buffer batches timed after the timed loop (PCIe included)
+E2E_BATCHES = 6                   # host-buffer batches after the timed loop (PCIe included): 1 warmup + 2 timed
+                                  # through pageable buffers, then the same through registered ones
 
 
 class SgawParams(C.Structure):
@@ -401,9 +402,11 @@ def main():
 
 def run_e2e(L, eng, bats, dev):
     """SURVEY.md 8(d), last bullet: the same C3 batches through host buffers -- sga_request_tokens
-    (H2D of flowId/acquire/prio/ts, the pipeline, D2H of the 12-B TokenResults), PCIe included.
-    Batches follow the timed ones in virtual time; timed one by one, synchronous per call.
-    Never `value`: reported beside it."""
+    (H2D of flowId/acquire/prio/ts, the pipeline, D2H of the 8-B TokenResults), PCIe included.
+    Batches follow the timed ones in virtual time, one synchronous call each.  The first three go
+    through pageable buffers (engine-staged), the last three through buffers the caller registered
+    with sga_host_register beforehand (a front end's long-lived pool: DMA straight from / to them);
+    the first batch of each three is an untimed warmup.  Never `value`: reported beside it."""
     import torch
     from sentinel_amd import _lib
     hosts = []
@@ -411,23 +414,44 @@ def run_e2e(L, eng, bats, dev):
         ts = (t.to(torch.int64) + ts_base).cpu().numpy()
         hosts.append((f.cpu().numpy(), a.cpu().numpy(), p.cpu().numpy(), ts, n))
     torch.cuda.synchronize(dev)
-    total, secs = 0, 0.0
-    for f, a, p, ts, n in hosts:
-        out = np.empty(n * 3, dtype=np.int32)
-        t0 = time.perf_counter()
-        rc = L.sga_request_tokens(eng.handle, f.ctypes.data, a.ctypes.data, p.ctypes.data, ts.ctypes.data, n,
-                                  out.ctypes.data)
-        secs += time.perf_counter() - t0
-        _lib.check(rc, eng.handle, "requestTokens (host buffers)")
-        total += n
-    return {"value": total / secs, "unit": "decisions/s", "batches": len(hosts), "requests": total,
-            "ms_per_batch": secs / len(hosts) * 1e3,
+    outs = [np.zeros(n * 2, dtype=np.int32) for *_, n in hosts]  # the caller's result buffers, allocated up front
+    half = len(hosts) // 2
+    regs = []
+    for (f, a, p, ts, n), out in list(zip(hosts, outs))[half:]:
+        for arr in (f, a, p, ts, out):
+            _lib.check(L.sga_host_register(eng.handle, arr.ctypes.data, arr.nbytes), eng.handle, "host_register")
+            regs.append(arr)
+
+    def timed(pairs):
+        total, secs = 0, 0.0
+        for k, ((f, a, p, ts, n), out) in enumerate(pairs):
+            t0 = time.perf_counter()
+            rc = L.sga_request_tokens(eng.handle, f.ctypes.data, a.ctypes.data, p.ctypes.data, ts.ctypes.data, n,
+                                      out.ctypes.data)
+            dt = time.perf_counter() - t0
+            _lib.check(rc, eng.handle, "requestTokens (host buffers)")
+            if k > 0:  # the first is the warmup
+                secs += dt
+                total += n
+        return total, secs
+
+    tp, sp = timed(list(zip(hosts, outs))[:half])
+    tr, sr = timed(list(zip(hosts, outs))[half:])
+    for arr in regs:
+        L.sga_host_unregister(eng.handle, arr.ctypes.data)
+    return {"value": tr / sr, "unit": "decisions/s", "batches": half - 1, "requests": tr,
+            "ms_per_batch": sr / (half - 1) * 1e3,
             "bytes_pcie_per_request": 8 + 4 + 1 + 8 + 8,
-            "what": "sga_request_tokens over pageable host buffers (int64 flowId, int32 acquire, uint8 prio, "
-                    "int64 ts in; 8-B TokenResult out): host threads stage 2^20-request chunks through page-locked "
-                    "slots while the DMA engine moves the previous chunk, then the pipeline, then the results back "
-                    "the same way (engine.cpp run_host_batch_pipelined); one call per batch, synchronous, one GPU; "
-                    "the batches that follow the timed ones in virtual time"}
+            "pageable": {"value": tp / sp, "ms_per_batch": sp / (half - 1) * 1e3, "batches": half - 1,
+                         "bytes_pcie_per_request": 8 + 4 + 4 + 1 + 8,
+                         "what": "the same call over pageable buffers: host threads stage 2^20-request chunks "
+                                 "(times as int32 deltas) through page-locked slots while the DMA engine moves the "
+                                 "previous chunk, the results come back the same way (run_host_batch_pipelined)"},
+            "what": "sga_request_tokens over host buffers the caller registered once with sga_host_register "
+                    "(int64 flowId, int32 acquire, uint8 prio, int64 ts in; 8-B TokenResult out): H2D straight "
+                    "from them, the pipeline, D2H straight into the result buffer (run_host_batch_registered); one "
+                    "synchronous call per 2^24-request batch, one GPU, after one warmup batch; the batches follow "
+                    "the timed ones in virtual time"}
 
 
 def _time_router(f, n_shards, threads):

@@ -154,6 +154,14 @@ int sga_set_small_batch(sga_engine *e, uint32_t max_requests);
 int sga_request_tokens(sga_engine *e, const int64_t *flow_id, const int32_t *acquire, const uint8_t *prioritized,
                        const int64_t *ts, size_t n, sga_token_result *out);
 
+/* Engine tuning (no reference counterpart): page-lock a long-lived host buffer of the caller (a front
+ * end's request / result pool) for this engine's DMA.  sga_request_tokens batches of at least 2^20
+ * requests whose arrays all lie in registered buffers are copied straight from / to them; other large
+ * batches are staged through the engine's own page-locked slots by host threads.  Decisions are the
+ * same either way.  Unregister before freeing the memory. */
+int sga_host_register(sga_engine *e, void *ptr, size_t bytes);
+int sga_host_unregister(sga_engine *e, void *ptr);
+
 /* Coalescing queue for single requests.  TokenService.requestToken is called once per request from
  * many threads (FlowRequestProcessor.java:43 -> DefaultTokenService.requestToken,
  * CS/flow/DefaultTokenService.java:39-54); calling sga_request_tokens with n = 1 from each would

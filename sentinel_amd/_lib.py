@@ -140,6 +140,8 @@ SIGNATURES = {
                                            C.c_size_t, C.c_void_p]),
     "sga_cluster_param_sum": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.POINTER(C.c_int64)]),
     "sga_cluster_set_param_capacity": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "sga_host_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "sga_host_unregister": (C.c_int, [C.c_void_p, C.c_void_p]),
     "sga_rls_should_rate_limit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p, C.c_void_p, C.c_void_p]),
     "sga_cluster_param_top_values": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_uint32, C.c_void_p,

@@ -4236,14 +4236,55 @@ void cluster_metric_nodes(const ClusterState &st, const int64_t *slot_fid, int64
                        slot_fid, now, (sga_cluster_metric_node *)out, cap, count);
 }
 
-__global__ __launch_bounds__(kThreads) void k_ts_offsets(const int64_t *__restrict__ ts, int64_t lo,
+__global__ __launch_bounds__(kThreads) void k_ts_offsets(const int32_t *__restrict__ ts, int64_t lo,
                                                          uint32_t *__restrict__ off, uint32_t n) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i < n) off[i] = (uint32_t)((int64_t)ts[i] - lo);
+}
+
+void cluster_ts_offsets(const int32_t *ts, int64_t lo, uint32_t *off, uint32_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_ts_offsets, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, ts, lo, off, n);
+}
+
+__global__ __launch_bounds__(kThreads) void k_ts_minmax(const int64_t *__restrict__ ts, uint32_t n, int64_t *mm) {
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+        const int64_t t = ts[i];
+        lo = min(lo, t);
+        hi = max(hi, t);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, (int64_t)__shfl_xor((long long)lo, o, 64));
+        hi = max(hi, (int64_t)__shfl_xor((long long)hi, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin((long long *)&mm[0], (long long)lo);
+        atomicMax((long long *)&mm[1], (long long)hi);
+    }
+}
+
+__global__ void k_ts_minmax_init(int64_t *mm) {
+    if (threadIdx.x == 0) {
+        mm[0] = INT64_MAX;
+        mm[1] = INT64_MIN;
+    }
+}
+
+void cluster_ts_minmax(const int64_t *ts, uint32_t n, int64_t *minmax, hipStream_t s) {
+    hipLaunchKernelGGL(k_ts_minmax_init, dim3(1), dim3(64), 0, s, minmax);
+    if (n) hipLaunchKernelGGL(k_ts_minmax, dim3(std::min<uint32_t>((n + kThreads - 1) / kThreads, 2048)), dim3(kThreads), 0, s,
+                              ts, n, minmax);
+}
+
+__global__ __launch_bounds__(kThreads) void k_ts_offsets64(const int64_t *__restrict__ ts, int64_t lo,
+                                                           uint32_t *__restrict__ off, uint32_t n) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
     if (i < n) off[i] = (uint32_t)(ts[i] - lo);
 }
 
-void cluster_ts_offsets(const int64_t *ts, int64_t lo, uint32_t *off, uint32_t n, hipStream_t s) {
-    if (n) hipLaunchKernelGGL(k_ts_offsets, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, ts, lo, off, n);
+void cluster_ts_offsets64(const int64_t *ts, int64_t lo, uint32_t *off, uint32_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_ts_offsets64, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, ts, lo, off, n);
 }
 
 void cluster_init_limiter(NsLimiterDev *d, hipStream_t s) {

@@ -329,8 +329,11 @@ struct CParamScratch {
     uint32_t *vkey;           // per value of the batch: kidx
 };
 
-// off[i] = ts[i] - lo (the host checked that the span fits u32): host-buffer batches ship int64 times
-void cluster_ts_offsets(const int64_t *ts, int64_t lo, uint32_t *off, uint32_t n, hipStream_t s);
+// off[i] = ts[i] - lo, ts int32 deltas from the batch's first time (host-buffer batches ship those)
+void cluster_ts_offsets(const int32_t *ts, int64_t lo, uint32_t *off, uint32_t n, hipStream_t s);
+// registered host buffers: int64 times on the device; minmax[0..1] = their min / max; off = ts - lo
+void cluster_ts_minmax(const int64_t *ts, uint32_t n, int64_t *minmax, hipStream_t s);
+void cluster_ts_offsets64(const int64_t *ts, int64_t lo, uint32_t *off, uint32_t n, hipStream_t s);
 
 size_t cparam_scratch_bytes(size_t cap);
 void cparam_scratch_carve(CParamScratch &ps, void *base, size_t cap);

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -205,9 +206,40 @@ struct Engine {
     // int64 times on the device (offsets computed there), the copy threads
     static constexpr size_t kPipeChunk = 1u << 20, kPipeSlots = 3;
     PinnedBuf h_pin_in, h_pin_out;
-    DevBuf<int64_t> d_ts64;
+    DevBuf<int32_t> d_tsd;  // times as int32 deltas from the batch's first time
+    DevBuf<int64_t> d_ts64, d_tminmax;  // registered host buffers: the int64 times, their min / max
+    std::vector<std::pair<uintptr_t, uintptr_t>> host_regs;  // sga_host_register ranges [lo, hi)
+    bool registered(const void *p, size_t bytes) const {
+        const uintptr_t a = (uintptr_t)p, b = a + bytes;
+        for (auto &r : host_regs)
+            if (a >= r.first && b <= r.second) return true;
+        return false;
+    }
     hipEvent_t ev_pin_in[kPipeSlots] = {}, ev_pin_out[kPipeSlots] = {};
     HostPool host_pool;
+    static constexpr size_t kPipeIn = 8 + 4 + 4 + 1;  // flowId, time delta, acquire, prio
+    // page-locked slots (each DMA'd once at allocation: the first transfers from fresh page-locked pages
+    // run at half rate), events, the device delta buffer
+    void ensure_pipe_staging() {
+        if (!h_pin_in.p) {
+            h_pin_in.alloc(kPipeSlots * kPipeChunk * kPipeIn);
+            h_pin_out.alloc(kPipeSlots * kPipeChunk * 8);
+            std::memset(h_pin_in.p, 0, h_pin_in.n);
+            std::memset(h_pin_out.p, 0, h_pin_out.n);
+            for (size_t s = 0; s < kPipeSlots; ++s) {
+                SGA_HIP_CHECK(hipEventCreateWithFlags(&ev_pin_in[s], hipEventDisableTiming));
+                SGA_HIP_CHECK(hipEventCreateWithFlags(&ev_pin_out[s], hipEventDisableTiming));
+            }
+        }
+        if (d_tsd.n < cfg.max_batch) {
+            d_tsd.alloc(cfg.max_batch);
+            const size_t w = std::min(h_pin_in.n, d_tsd.bytes());
+            SGA_HIP_CHECK(hipMemcpyAsync(d_tsd.p, h_pin_in.p, w, hipMemcpyHostToDevice, stream));
+            SGA_HIP_CHECK(hipMemcpyAsync(h_pin_out.p, d_tsd.p, std::min(h_pin_out.n, d_tsd.bytes()),
+                                         hipMemcpyDeviceToHost, stream));
+            SGA_HIP_CHECK(hipStreamSynchronize(stream));
+        }
+    }
     ~Engine() {
         for (size_t s = 0; s < kPipeSlots; ++s) {
             if (ev_pin_in[s]) (void)hipEventDestroy(ev_pin_in[s]);
@@ -880,6 +912,10 @@ int sga_create(const sga_config *cfg, sga_engine **out) {
         g.d_tmp7.alloc(8);
         g.flow.init(c, g.stream);
         g.ensure_scratch();
+        if (c.max_batch >= 4 * Engine::kPipeChunk) {  // host-buffer batches this large: staging ready up front
+            g.ensure_pipe_staging();
+            (void)g.host_pool.size();
+        }
         std::random_device rd;  // token ids: a random start, then splitmix64 of a counter (bijective)
         g.token_base = ((uint64_t)rd() << 32) ^ (uint64_t)rd();
         return SGA_OK;
@@ -1186,72 +1222,75 @@ int sga_sync(sga_engine *e) {
 }
 
 // One engine batch from host buffers at PCIe rate: the host threads copy chunk c of the inputs into a
-// page-locked slot (and take the times' min / max) while the DMA engine moves chunk c - 1 to the device;
-// the device turns the int64 times into u32 offsets from their minimum; after the pipeline the results
-// come back the same way, chunk by chunk through page-locked slots the threads copy out of.
-// Returns 1 (nothing decided) when the times span more than u32 offsets.
+// page-locked slot -- the times as int32 deltas from the batch's first time, with their min / max -- while
+// the DMA engine moves chunk c - 1 to the device (17 B per request); the device turns the deltas into u32
+// offsets from the minimum; after the pipeline the results come back the same way, chunk by chunk through
+// page-locked slots the threads copy out of.  Returns 1 (nothing decided) when a time lies more than
+// 2^31 - 1 ms from the first one.
 static int run_host_batch_pipelined(Engine &g, const int64_t *flow_id, const int32_t *acquire, const uint8_t *prio,
                                     const int64_t *ts, size_t n, uint64_t *out, int simple,
                                     const std::vector<sga::LimiterPass> &lims) {
     constexpr size_t C = Engine::kPipeChunk, K = Engine::kPipeSlots;
-    constexpr size_t kIn = 8 + 8 + 4 + 1;  // flowId, time, acquire, prio
-    if (!g.h_pin_in.p) {
-        g.h_pin_in.alloc(K * C * kIn);
-        g.h_pin_out.alloc(K * C * 8);
-        for (size_t s = 0; s < K; ++s) {
-            SGA_HIP_CHECK(hipEventCreateWithFlags(&g.ev_pin_in[s], hipEventDisableTiming));
-            SGA_HIP_CHECK(hipEventCreateWithFlags(&g.ev_pin_out[s], hipEventDisableTiming));
-        }
-    }
-    if (g.d_ts64.n < g.cfg.max_batch) g.d_ts64.alloc(g.cfg.max_batch);
+    constexpr size_t kIn = Engine::kPipeIn;
+    g.ensure_pipe_staging();
     sga::HostPool &pool = g.host_pool;
     const int T = pool.size();
     std::vector<int64_t> tmin(T), tmax(T);
-    std::vector<uint8_t> tneg(T);
-    int64_t lo = INT64_MAX, hi = INT64_MIN;
-    bool neg = false;
+    std::vector<uint8_t> tbad(T);
+    const int64_t t0 = ts[0];
+    int64_t lo = INT64_MAX, hi = INT64_MIN;  // deltas
+    bool bad = false;
     const size_t nch = (n + C - 1) / C;
+    static const bool dbg = getenv("SGA_PIPE_DEBUG") != nullptr;  // diagnostics only: phase times on stderr
+    using clk = std::chrono::steady_clock;
+    double t_fill = 0, t_win = 0, t_wout = 0, t_copy = 0;
+    const auto t_start = clk::now();
+    auto since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     for (size_t c = 0; c < nch; ++c) {
         const size_t s = c % K, c0 = c * C, m = std::min(C, n - c0);
+        auto ta = clk::now();
         if (c >= K) SGA_HIP_CHECK(hipEventSynchronize(g.ev_pin_in[s]));  // the slot's last copy is done
+        t_win += since(ta);
+        ta = clk::now();
         uint8_t *slot = g.h_pin_in.p + s * C * kIn;
-        int64_t *pf = reinterpret_cast<int64_t *>(slot), *pt = reinterpret_cast<int64_t *>(slot + 8 * C);
-        int32_t *pa = reinterpret_cast<int32_t *>(slot + 16 * C);
-        uint8_t *pp = slot + 20 * C;
+        int64_t *pf = reinterpret_cast<int64_t *>(slot);
+        int32_t *pt = reinterpret_cast<int32_t *>(slot + 8 * C), *pa = reinterpret_cast<int32_t *>(slot + 12 * C);
+        uint8_t *pp = slot + 16 * C;
         pool.run([&](int t) {
             const size_t a = m * t / T, b = m * (t + 1) / T;
             int64_t mn = INT64_MAX, mx = INT64_MIN;
             for (size_t i = a; i < b; ++i) {
-                const int64_t x = ts[c0 + i];
-                pt[i] = x;
+                const int64_t x = ts[c0 + i] - t0;
+                pt[i] = (int32_t)x;
                 mn = std::min(mn, x);
                 mx = std::max(mx, x);
             }
             tmin[t] = mn;
             tmax[t] = mx;
-            tneg[t] = mn < 0;
+            tbad[t] = mn < INT32_MIN || mx > INT32_MAX || mn + t0 < 0;
             std::memcpy(pf + a, flow_id + c0 + a, (b - a) * 8);
             std::memcpy(pa + a, acquire + c0 + a, (b - a) * 4);
             if (prio) std::memcpy(pp + a, prio + c0 + a, b - a);
         });
+        t_fill += since(ta);
         for (int t = 0; t < T; ++t) {
             lo = std::min(lo, tmin[t]);
             hi = std::max(hi, tmax[t]);
-            neg |= tneg[t] != 0;
+            bad |= tbad[t] != 0;
         }
         SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_fid.p + c0, pf, m * 8, hipMemcpyHostToDevice, g.stream));
-        SGA_HIP_CHECK(hipMemcpyAsync(g.d_ts64.p + c0, pt, m * 8, hipMemcpyHostToDevice, g.stream));
+        SGA_HIP_CHECK(hipMemcpyAsync(g.d_tsd.p + c0, pt, m * 4, hipMemcpyHostToDevice, g.stream));
         SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_acq.p + c0, pa, m * 4, hipMemcpyHostToDevice, g.stream));
         if (prio) SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_prio.p + c0, pp, m, hipMemcpyHostToDevice, g.stream));
         SGA_HIP_CHECK(hipEventRecord(g.ev_pin_in[s], g.stream));
     }
-    if (neg || hi - lo > (int64_t)0xFFFFFFFFLL) {
-        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
-        return neg ? SGA_EINVAL : 1;  // LeapArray.currentWindow(t < 0) returns null
+    if (bad) {  // a negative time (LeapArray.currentWindow(t < 0) returns null: -EINVAL from the chunked path)
+        SGA_HIP_CHECK(hipStreamSynchronize(g.stream));  // or a delta past int32: the chunked path
+        return 1;
     }
     if (!prio) SGA_HIP_CHECK(hipMemsetAsync(g.d_in_prio.p, 0, n, g.stream));
-    sga::cluster_ts_offsets(g.d_ts64.p, lo, g.d_in_ts.p, (uint32_t)n, g.stream);
-    sga::cluster_decide_batch(g.state(), g.scratch, g.d_in_fid.p, g.d_in_acq.p, g.d_in_prio.p, lo, g.d_in_ts.p,
+    sga::cluster_ts_offsets(g.d_tsd.p, lo, g.d_in_ts.p, (uint32_t)n, g.stream);
+    sga::cluster_decide_batch(g.state(), g.scratch, g.d_in_fid.p, g.d_in_acq.p, g.d_in_prio.p, t0 + lo, g.d_in_ts.p,
                               (uint32_t)n, simple, g.d_out.p, g.stream, lims.data(), (int)lims.size());
     SGA_HIP_CHECK(hipGetLastError());
     auto d2h = [&](size_t c) {
@@ -1260,17 +1299,61 @@ static int run_host_batch_pipelined(Engine &g, const int64_t *flow_id, const int
                                      g.stream));
         SGA_HIP_CHECK(hipEventRecord(g.ev_pin_out[s], g.stream));
     };
+    const double t_queued = since(t_start);
     for (size_t c = 0; c < std::min(K, nch); ++c) d2h(c);
     for (size_t c = 0; c < nch; ++c) {
         const size_t s = c % K, c0 = c * C, m = std::min(C, n - c0);
+        auto ta = clk::now();
         SGA_HIP_CHECK(hipEventSynchronize(g.ev_pin_out[s]));
+        t_wout += since(ta);
+        ta = clk::now();
         const uint64_t *src = reinterpret_cast<const uint64_t *>(g.h_pin_out.p + s * C * 8);
         pool.run([&](int t) {
             const size_t a = m * t / T, b = m * (t + 1) / T;
             std::memcpy(out + c0 + a, src + a, (b - a) * 8);
         });
+        t_copy += since(ta);
         if (c + K < nch) d2h(c + K);
     }
+    if (dbg)
+        fprintf(stderr, "pipe n=%zu threads=%d: fill %.2f wait-in %.2f queued-at %.2f wait-out %.2f copy-out %.2f total %.2f ms\n",
+                n, T, t_fill, t_win, t_queued, t_wout, t_copy, since(t_start));
+    if (sga::radix64_lookback()) {
+        uint32_t err = 0;
+        SGA_HIP_CHECK(hipMemcpy(&err, g.scratch.radix.err, 4, hipMemcpyDeviceToHost));
+        if (err) {
+            g.err = "radix look-back timed out";
+            return SGA_EIO;
+        }
+    }
+    return SGA_OK;
+}
+
+// One engine batch whose arrays all lie in sga_host_register'ed buffers: DMA straight from and to them
+// (21 B in, 8 B out per request); the times' min / max come from a device reduction (one 16-byte read
+// back), the offsets from the minimum are computed on the device.  Returns 1 (nothing decided) when the
+// times span more than u32 offsets or one is negative.
+static int run_host_batch_registered(Engine &g, const int64_t *flow_id, const int32_t *acquire, const uint8_t *prio,
+                                     const int64_t *ts, size_t n, uint64_t *out, int simple,
+                                     const std::vector<sga::LimiterPass> &lims) {
+    if (g.d_ts64.n < g.cfg.max_batch) g.d_ts64.alloc(g.cfg.max_batch);
+    if (!g.d_tminmax.p) g.d_tminmax.alloc(2);
+    SGA_HIP_CHECK(hipMemcpyAsync(g.d_ts64.p, ts, n * 8, hipMemcpyHostToDevice, g.stream));
+    sga::cluster_ts_minmax(g.d_ts64.p, (uint32_t)n, g.d_tminmax.p, g.stream);
+    int64_t mm[2];
+    SGA_HIP_CHECK(hipMemcpyAsync(mm, g.d_tminmax.p, 16, hipMemcpyDeviceToHost, g.stream));
+    SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_fid.p, flow_id, n * 8, hipMemcpyHostToDevice, g.stream));
+    SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_acq.p, acquire, n * 4, hipMemcpyHostToDevice, g.stream));
+    if (prio) SGA_HIP_CHECK(hipMemcpyAsync(g.d_in_prio.p, prio, n, hipMemcpyHostToDevice, g.stream));
+    else SGA_HIP_CHECK(hipMemsetAsync(g.d_in_prio.p, 0, n, g.stream));
+    SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+    if (mm[0] < 0 || mm[1] - mm[0] > (int64_t)0xFFFFFFFFLL) return 1;
+    sga::cluster_ts_offsets64(g.d_ts64.p, mm[0], g.d_in_ts.p, (uint32_t)n, g.stream);
+    sga::cluster_decide_batch(g.state(), g.scratch, g.d_in_fid.p, g.d_in_acq.p, g.d_in_prio.p, mm[0], g.d_in_ts.p,
+                              (uint32_t)n, simple, g.d_out.p, g.stream, lims.data(), (int)lims.size());
+    SGA_HIP_CHECK(hipGetLastError());
+    SGA_HIP_CHECK(hipMemcpyAsync(out, g.d_out.p, n * 8, hipMemcpyDeviceToHost, g.stream));
+    SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
     if (sga::radix64_lookback()) {
         uint32_t err = 0;
         SGA_HIP_CHECK(hipMemcpy(&err, g.scratch.radix.err, 4, hipMemcpyDeviceToHost));
@@ -1338,7 +1421,10 @@ static int run_host_batch(Engine &g, const int64_t *flow_id, const int32_t *acqu
         }
     }
     if (n >= Engine::kPipeChunk && n <= cap) {
-        const int rc = run_host_batch_pipelined(g, flow_id, acquire, prio, ts, n, out, simple, lims);
+        const bool reg = !g.host_regs.empty() && g.registered(flow_id, n * 8) && g.registered(acquire, n * 4) &&
+                         g.registered(ts, n * 8) && g.registered(out, n * 8) && (!prio || g.registered(prio, n));
+        const int rc = reg ? run_host_batch_registered(g, flow_id, acquire, prio, ts, n, out, simple, lims)
+                           : run_host_batch_pipelined(g, flow_id, acquire, prio, ts, n, out, simple, lims);
         if (rc != 1) return rc;  // 1: the batch's times span more than u32 offsets: the chunked path below
     }
     for (size_t b = 0; b < n;) {
@@ -1379,6 +1465,34 @@ static int run_host_batch(Engine &g, const int64_t *flow_id, const int32_t *acqu
         b += m;
     }
     return SGA_OK;
+}
+
+int sga_host_register(sga_engine *e, void *ptr, size_t bytes) {
+    if (!ptr || bytes == 0) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        if (hipHostRegister(ptr, bytes, hipHostRegisterDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            g.err = "hipHostRegister failed";
+            return SGA_ENOMEM;
+        }
+        g.host_regs.emplace_back((uintptr_t)ptr, (uintptr_t)ptr + bytes);
+        return SGA_OK;
+    });
+}
+
+int sga_host_unregister(sga_engine *e, void *ptr) {
+    if (!ptr) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        for (size_t i = 0; i < g.host_regs.size(); ++i)
+            if (g.host_regs[i].first == (uintptr_t)ptr) {
+                SGA_HIP_CHECK(hipStreamSynchronize(g.stream));
+                (void)hipHostUnregister(ptr);
+                g.host_regs.erase(g.host_regs.begin() + (long)i);
+                return SGA_OK;
+            }
+        return SGA_EINVAL;
+    });
 }
 
 int sga_request_tokens(sga_engine *e, const int64_t *flow_id, const int32_t *acquire, const uint8_t *prio,

@@ -319,13 +319,29 @@ def test_host_batches_pipelined(eng_mod):
     c.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_r, cnt)
     svc = c.DefaultTokenService(eng)
     lo = 0
-    for k, n in enumerate([3 * (1 << 20) + 12345, 1 << 20, (1 << 20) + 7]):
+    from sentinel_amd import _lib
+    L = _lib.load()
+    for k, n in enumerate([3 * (1 << 20) + 12345, 1 << 20, (1 << 20) + 7, (1 << 21) + 3]):
         fid, acq, prio, ts = tr.events(lo, n)
         lo += n
         if k == 2:  # a jump past the u32 span half way: the chunked path
             ts = ts.copy()
             ts[n // 2:] += 1 << 33
-        g = svc.request_tokens(fid, acq, prio, ts)
+        if k == 3:  # registered buffers: DMA straight from / to them (run_host_batch_registered)
+            fid, acq, prio, ts = (np.ascontiguousarray(x, dt) for x, dt in
+                                  ((fid, np.int64), (acq, np.int32), (prio, np.uint8), (ts, np.int64)))
+            out = np.zeros(n, dtype=c.TOKEN_DTYPE)
+            arrs = (fid, acq, prio, ts, out)
+            for x in arrs:
+                assert L.sga_host_register(eng.handle, x.ctypes.data, x.nbytes) == 0
+            rc = L.sga_request_tokens(eng.handle, fid.ctypes.data, acq.ctypes.data, prio.ctypes.data, ts.ctypes.data,
+                                      n, out.ctypes.data)
+            for x in arrs:
+                assert L.sga_host_unregister(eng.handle, x.ctypes.data) == 0
+            assert rc == 0
+            g = out
+        else:
+            g = svc.request_tokens(fid, acq, prio, ts)
         o = oracle_replay(oh, fid, acq, prio, ts)
         assert_same(g, o, fid, ts, f"host batch {k} ({n} requests)")
     assert_metrics(c, eng, oh, np.unique(fid)[:100], int(ts[-1]))
