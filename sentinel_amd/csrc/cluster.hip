@@ -3971,13 +3971,20 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const int64_t
         SGA_HIP_CHECK(hipStreamWaitEvent(sc.side2, sc.ev_fork0, 0));
         ps = sc.side2;
     }
-    const int npp = radix_sort_u64_tiled(sc.pel_tile, sc.ptile_np, sc.counters + CTL_NPRIO, sc.pel[0], sc.pel[1], n,
-                                         kSlotShift, 12, sc.radix_p, ps, false);
-    sc.pel_sorted = (npp & 1) ? sc.pel[0] : sc.pel[1];
+    // SGA_PRIO_LATE=1 (A/B knob): the count scans are queued before the prioritized sort (the two side
+    // streams may share a hardware queue, where submission order is execution order)
+    static const bool prio_late = getenv("SGA_PRIO_LATE") && atoi(getenv("SGA_PRIO_LATE")) == 1;
+    auto prio_sort = [&] {
+        const int npp = radix_sort_u64_tiled(sc.pel_tile, sc.ptile_np, sc.counters + CTL_NPRIO, sc.pel[0], sc.pel[1],
+                                             n, kSlotShift, 12, sc.radix_p, ps, false);
+        sc.pel_sorted = (npp & 1) ? sc.pel[0] : sc.pel[1];
+    };
+    if (!prio_late) prio_sort();
     hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
     hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, hs, sc, ngroups);
     hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
     hipLaunchKernelGGL(k_hot_pre, dim3(kHotBuckets), dim3(kThreads), 0, hs, sc);
+    if (prio_late) prio_sort();
     if (ovl) {  // the prioritized sort joins the side stream (k_prio_rank needs both)
         SGA_HIP_CHECK(hipEventRecord(sc.ev_prio, ps));
         SGA_HIP_CHECK(hipStreamWaitEvent(hs, sc.ev_prio, 0));

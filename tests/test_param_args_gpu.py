@@ -191,3 +191,38 @@ def test_blocked_entries_outside_the_engine():
     assert s.node(0xFFFFFFFF, int(st["ts"].max())).total_block == orc.node(0xFFFFFFFF, int(st["ts"].max()))[9]
     orc.close()
     eng.close()
+
+
+def test_thread_maps_many_indices_distinct_values():
+    """One resource with parameter rules on five argument indices and a max_batch batch of entries whose
+    arguments are all distinct: every entry claims a thread-count map slot per index (ParameterMetric
+    .addThreadCount, ParameterMetric.java:184-230), 5 x 2^16 keys in one batch, so the thread table's
+    growth budget must count the indices (FlowEngine::ensure_maps).  Then the exits.  Decisions, waits and
+    node views equal the oracle, and the batch does not fail."""
+    n_res, n, k_idx = 1, 1 << 16, 5
+    rules = [{"resource": 0, "count": 3.0, "param_idx": k} for k in range(k_idx)]
+    pv, words = [], []
+    for i in range(n):
+        words.append(lt.encode_args([i * k_idx + k + 1 for k in range(k_idx)], pv))
+    ts = T0 + np.arange(n, dtype=np.int64) // 64
+    st = {"kind": np.zeros(n, np.uint8), "resource": np.zeros(n, np.uint32), "ts": ts,
+          "acquire": np.ones(n, np.int32), "flags": np.full(n, 32, np.uint8), "rt": np.zeros(n, np.int64),
+          "param": np.array(words, np.uint64), "param_values": np.array(pv, np.uint64)}
+    orc = lt.Oracle(n_res, [], rules)
+    exp = orc.replay(st)
+    ok = np.isin(exp[0], (0, 4))  # passed entries exit
+    assert ok.all()
+    ex = {k: v.copy() for k, v in st.items()}
+    ex["kind"] = np.ones(n, np.uint8)
+    ex["ts"] = ts + 5
+    ex["rt"] = np.full(n, 5, np.int64)
+    exp_x = orc.replay(ex)
+    eng, s = _sentinel(n_res, n)
+    _load(s, param=rules)
+    got = _submit_args(s, st)
+    _assert_same(st, got, exp, "distinct arguments on five indices (entries)")
+    got_x = _submit_args(s, ex)
+    _assert_same(ex, got_x, exp_x, "distinct arguments on five indices (exits)")
+    _assert_nodes(s, orc, n_res, int(ex["ts"].max()))
+    orc.close()
+    eng.close()

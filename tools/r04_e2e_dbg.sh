@@ -12,3 +12,6 @@ SGA_PIPE_DEBUG=1 timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cp
 grep "^pipe" $out/bench.err | tail -3
 python3 -c "
 import json; d=json.load(open('$out/bench.json')); e=d.get('end_to_end_host_buffers'); print('e2e', e['value'], e['ms_per_batch'])"
+timeout -k 10 300 python3 -u -m pytest tests/test_param_args_gpu.py -m gpu -x -q -k "many_indices" --timeout 250 \
+    --timeout-method thread > $out/pytest_idx.log 2>&1 || { tail -30 $out/pytest_idx.log; exit 1; }
+tail -1 $out/pytest_idx.log
