@@ -1305,18 +1305,44 @@ __device__ LAgg lblock_excl(const LAgg &v, LAgg *total) {
     return ex;
 }
 
+// The blocked arrangement (thread t: the tile's elements t * kItems .. + kItems) read through LDS: one
+// thread's consecutive elements are kItems x 16 bytes apart, so direct loads put every lane of a wave on
+// its own cache lines and the lines are fetched again for each element (10x the bytes, PMC).  The tile
+// and its neighbours ([base - 1, base + kTileElems + 1), kStage elements) are loaded with coalesced
+// (striped) loads instead; an LDS slot per kItems elements of padding keeps the strided reads of the
+// compute loops off one bank.
+constexpr int kStage = kTileElems + 2;
+constexpr int kStagePad = kStage + kStage / kItems + 1;
+__device__ __forceinline__ uint32_t spad(uint32_t i) { return i + i / kItems; }
+// LDS slot of element e of the tile at base (e in [base - 1, base + kTileElems + 1))
+__device__ __forceinline__ uint32_t sslot(uint32_t base, uint32_t e) { return spad(e + 1 - base); }
+template <class T>
+__device__ __forceinline__ void stage_tile(T *lds, const T *__restrict__ g, uint32_t base, uint32_t lim, T none) {
+#pragma unroll 4
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kStage; i += kT) {
+        const uint32_t e = base + i - 1;  // base 0: e wraps for i = 0, and lim excludes it
+        lds[spad(i)] = (base + i >= 1 && e < lim) ? g[e] : none;
+    }
+}
+
 __global__ __launch_bounds__(kT) void k_lruns_up(const uint32_t *__restrict__ keys, const Payload *__restrict__ pay,
                                                  uint32_t n, uint32_t invalid, LAgg *tile_agg, uint32_t *tile_valid) {
-    const uint32_t e0 = blockIdx.x * kTileElems + threadIdx.x * kItems;
+    __shared__ uint32_t skey[kStagePad];
+    __shared__ Payload spay[kStagePad];
+    const uint32_t base = blockIdx.x * kTileElems;
+    stage_tile(skey, keys, base, n, invalid);
+    stage_tile(spay, pay, base, n, Payload{0, 0, 0, 0});
+    __syncthreads();
+    const uint32_t e0 = base + threadIdx.x * kItems;
     LAgg acc = lagg_id();
     uint32_t nv = 0;
     if (e0 < n) {
-        uint32_t pk = e0 > 0 ? keys[e0 - 1] : invalid;
-        Payload pq = e0 > 0 ? pay[e0 - 1] : Payload{0, 0, 0, 0};
+        uint32_t pk = e0 > 0 ? skey[sslot(base, e0 - 1)] : invalid;
+        Payload pq = e0 > 0 ? spay[sslot(base, e0 - 1)] : Payload{0, 0, 0, 0};
         for (int i = 0; i < kItems && e0 + i < n; ++i) {
             const uint32_t e = e0 + i;
-            const uint32_t k = keys[e];
-            const Payload q = pay[e];
+            const uint32_t k = skey[sslot(base, e)];
+            const Payload q = spay[sslot(base, e)];
             const bool valid = k != invalid;
             acc = lagg_combine(acc, lagg_value(k, pk, q, pq, e > 0, valid));
             nv += valid ? 1 : 0;
@@ -1367,40 +1393,45 @@ __global__ __launch_bounds__(kT) void k_lruns_tiles(const LAgg *__restrict__ til
 __global__ __launch_bounds__(kT) void k_lruns_down(const uint32_t *__restrict__ keys, const Payload *__restrict__ pay,
                                                    const int64_t *__restrict__ rt_in, uint32_t invalid,
                                                    const LAgg *__restrict__ tile_carry, FlowScratch sc) {
+    __shared__ uint32_t skey[kStagePad];
+    __shared__ Payload spay[kStagePad];
+    __shared__ uint32_t srun[kTileElems], seidx[kTileElems];  // the per-event outputs, stored coalesced below
     const uint32_t nvalid = sc.counters[0];
     const uint32_t base = blockIdx.x * kTileElems;
     if (base >= nvalid) return;
+    stage_tile(skey, keys, base, nvalid, invalid);
+    stage_tile(spay, pay, base, nvalid, Payload{0, 0, 0, 0});
+    __syncthreads();
     const uint32_t e0 = base + threadIdx.x * kItems;
     LAgg acc = lagg_id();
-    uint32_t pk0 = e0 > 0 && e0 - 1 < nvalid ? keys[e0 - 1] : invalid;
-    Payload pq0 = e0 > 0 && e0 - 1 < nvalid ? pay[e0 - 1] : Payload{0, 0, 0, 0};
+    uint32_t pk0 = e0 > 0 && e0 - 1 < nvalid ? skey[sslot(base, e0 - 1)] : invalid;
+    Payload pq0 = e0 > 0 && e0 - 1 < nvalid ? spay[sslot(base, e0 - 1)] : Payload{0, 0, 0, 0};
     {
         uint32_t pk = pk0;
         Payload pq = pq0;
         for (int i = 0; i < kItems && e0 + i < nvalid; ++i) {
             const uint32_t e = e0 + i;
-            const uint32_t k = keys[e];
-            const Payload q = pay[e];
+            const uint32_t k = skey[sslot(base, e)];
+            const Payload q = spay[sslot(base, e)];
             acc = lagg_combine(acc, lagg_value(k, pk, q, pq, e > 0, true));
             pk = k;
             pq = q;
         }
     }
     const LAgg ex = lblock_excl<kT>(acc, nullptr);
-    if (e0 >= nvalid) return;
     LAgg run = lagg_combine(tile_carry[blockIdx.x], ex);
     uint32_t pk = pk0;
     Payload pq = pq0;
     for (int i = 0; i < kItems && e0 + i < nvalid; ++i) {
         const uint32_t e = e0 + i;
-        const uint32_t k = keys[e];
-        const Payload q = pay[e];
+        const uint32_t k = skey[sslot(base, e)];
+        const Payload q = spay[sslot(base, e)];
         const LAgg v = lagg_value(k, pk, q, pq, e > 0, true);
         run = lagg_combine(run, v);
         const uint32_t rid = run.nh - 1;
         const bool ex_ev = (q.idx & F_EXIT) != 0;
-        sc.ev_run[e] = rid;
-        sc.ev_eidx[e] = ex_ev ? 0xFFFFFFFFu : run.nent - 1;  // entry index within the run
+        srun[e - base] = rid;
+        seidx[e - base] = ex_ev ? 0xFFFFFFFFu : run.nent - 1;  // entry index within the run
         if (v.flag) {
             sc.run_start[rid] = e;
             sc.run_slot[rid] = k;
@@ -1413,8 +1444,8 @@ __global__ __launch_bounds__(kT) void k_lruns_down(const uint32_t *__restrict__ 
         if (v.nf) sc.flow_first_run[run.nf - 1] = rid;
         bool last = e + 1 >= nvalid;
         if (!last) {
-            const uint32_t nk = keys[e + 1];
-            last = nk != k || pay[e + 1].bucket != q.bucket;
+            const uint32_t nk = skey[sslot(base, e + 1)];
+            last = nk != k || spay[sslot(base, e + 1)].bucket != q.bucket;
         }
         if (last) {
             sc.run_end[rid] = e + 1;
@@ -1427,13 +1458,30 @@ __global__ __launch_bounds__(kT) void k_lruns_down(const uint32_t *__restrict__ 
         pk = k;
         pq = q;
     }
+    __syncthreads();
+#pragma unroll 4
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kTileElems; i += kT) {
+        if (base + i >= nvalid) break;
+        sc.ev_run[base + i] = srun[i];
+        sc.ev_eidx[base + i] = seidx[i];
+    }
 }
 
 // exit aggregates per run (SUCCESS count, exceptions, RT sum, min RT): atomics per run
 // pre-reduced inside each thread's consecutive events.
 __global__ __launch_bounds__(kT) void k_lexits(const Payload *__restrict__ pay, const int64_t *__restrict__ rt_in,
                                                FlowScratch sc) {
+    __shared__ uint32_t srun[kStagePad];
+    __shared__ Payload spay[kStagePad];
+    __shared__ int64_t srt[kTileElems];
+    __shared__ uint8_t sex[kTileElems];  // an exit's RT is in srt
     const uint32_t nvalid = sc.counters[0];
+    const uint32_t base = blockIdx.x * kTileElems;
+    if (base >= nvalid) return;  // the whole block
+    stage_tile(srun, sc.ev_run, base, nvalid, 0xFFFFFFFFu);
+    stage_tile(spay, pay, base, nvalid, Payload{0, 0, 0, 0});
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kTileElems; i += kT) sex[i] = 0;
+    __syncthreads();
     const uint32_t e0 = (blockIdx.x * kT + threadIdx.x) * kItems;  // no early return: the wave reduction below
     uint32_t cur = 0xFFFFFFFFu;
     uint64_t c = 0, er = 0;
@@ -1447,9 +1495,9 @@ __global__ __launch_bounds__(kT) void k_lexits(const Payload *__restrict__ pay, 
     };
     for (int i = 0; i < kItems && e0 + i < nvalid; ++i) {
         const uint32_t e = e0 + i;
-        const Payload q = pay[e];
+        const Payload q = spay[sslot(base, e)];
         if (!(q.idx & F_EXIT)) continue;
-        const uint32_t r = sc.ev_run[e];
+        const uint32_t r = srun[sslot(base, e)];
         if (r != cur) {
             flush();
             cur = r;
@@ -1459,7 +1507,8 @@ __global__ __launch_bounds__(kT) void k_lexits(const Payload *__restrict__ pay, 
         }
         const uint64_t cnt = q.acq_prio & 0x7FFFFFFFu;
         const int64_t rt = rt_in[q.idx & F_IDX];
-        sc.rt_sorted[e] = rt;
+        srt[e - base] = rt;
+        sex[e - base] = 1;
         c += cnt;
         if (q.idx & F_ERROR) er += cnt;
         rs += rt;
@@ -1475,6 +1524,11 @@ __global__ __launch_bounds__(kT) void k_lexits(const Payload *__restrict__ pay, 
         if ((threadIdx.x & 63) != 0) cur = 0xFFFFFFFFu;
     }
     flush();
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kTileElems; i += kT) {  // the exits' RTs, coalesced
+        if (base + i >= nvalid) break;
+        if (sex[i]) sc.rt_sorted[base + i] = srt[i];
+    }
 }
 
 // ------------------------------------------------------------------ per-resource resolve
@@ -3406,8 +3460,15 @@ __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, 
 //    consecutive events
 __global__ __launch_bounds__(kT) void k_pseg_runs(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
                                                   const int8_t *__restrict__ decision) {
+    __shared__ uint32_t srun[kStagePad];
+    __shared__ Payload spay[kStagePad];
     if (!gate_is(st.gate, kGateSeq | kGateBad, 0) || sc.counters[11] == 0) return;
     const uint32_t nvalid = sc.counters[0];
+    const uint32_t base = blockIdx.x * kTileElems;
+    if (base >= nvalid) return;  // the whole block
+    stage_tile(srun, sc.ev_run, base, nvalid, 0u);
+    stage_tile(spay, pay, base, nvalid, Payload{0, 0, 0, 0});
+    __syncthreads();
     const uint32_t e0 = (blockIdx.x * kT + threadIdx.x) * kItems;
     uint32_t cur = 0xFFFFFFFFu, np = 0;
     int64_t pa = 0, ba = 0;
@@ -3419,9 +3480,9 @@ __global__ __launch_bounds__(kT) void k_pseg_runs(FlowState st, FlowScratch sc, 
     };
     for (int i = 0; i < kItems && e0 + i < nvalid; ++i) {
         const uint32_t e = e0 + i;
-        const uint32_t r = sc.ev_run[e];
+        const uint32_t r = srun[sslot(base, e)];
         if (sc.run_mode[r] != RUN_PSEG) continue;
-        const Payload q = pay[e];
+        const Payload q = spay[sslot(base, e)];
         if (q.idx & F_EXIT) continue;
         if (r != cur) {
             flush();

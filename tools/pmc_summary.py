@@ -56,8 +56,8 @@ def alg_bytes(k, bl):
     + writes the cold touched rules, the hot runs read + write the hot rules, the hot results kernel
     writes the hot results (E_out = 8 B).  Everything else (the sort, scans, next hot set) is 0:
     traffic there is non-algorithmic.  Hot touched rules ~ the hot-set size of the last batch."""
-    if not bl:
-        return None
+    if not bl or "requests_per_step_per_gpu" not in bl.get("config", {}):
+        return None  # local-path lines: the algorithmic bytes are the bench line's own roofline figure
     n = bl["config"]["requests_per_step_per_gpu"]
     touched = bl["roofline"]["touched_rules_per_step_per_gpu"]
     lp = bl.get("last_batch_path") or {}
