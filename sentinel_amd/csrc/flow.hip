@@ -3115,6 +3115,11 @@ __global__ __launch_bounds__(64 * kCbW) void k_cb_flows(FlowState st, FlowScratc
     if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
     __shared__ int64_t s_w[kCbW][5];  // per wave: total {ws, bad, tot}, first and last window
     __shared__ uint32_t s_min, s_bad;
+    // a wave's 64 x kCbI exits of a round, loaded coalesced and read back per lane (kCbI consecutive each;
+    // one pad slot per kCbI items keeps those strided reads off one bank)
+    constexpr int kCbStage = 64 * kCbI + 64;
+    __shared__ uint32_t s_ts[kCbW][kCbStage], s_fx[kCbW][kCbStage];
+    __shared__ int64_t s_rt[kCbW][kCbStage];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr uint32_t kRound = 64u * kCbW * kCbI, kWaveItems = 64u * kCbI;
     const uint32_t ncb = sc.counters[13], nflows = sc.counters[2], nruns = sc.counters[1];
@@ -3132,8 +3137,8 @@ __global__ __launch_bounds__(64 * kCbW) void k_cb_flows(FlowState st, FlowScratc
                 for (uint32_t base = jb; base < je && probe == je; base += kRound) {
                     if (threadIdx.x == 0) s_min = je;
                     __syncthreads();
-                    for (int i = 0; i < kCbI; ++i) {
-                        const uint32_t j = base + threadIdx.x * kCbI + i;
+                    for (int i = 0; i < kCbI; ++i) {  // coalesced; a thread's later items are later entries
+                        const uint32_t j = base + (uint32_t)i * (64u * kCbW) + threadIdx.x;
                         if (j < je && ts_base + (int64_t)pay[j].ts_off >= b.next_retry) {
                             atomicMin(&s_min, j);
                             break;
@@ -3169,21 +3174,36 @@ __global__ __launch_bounds__(64 * kCbW) void k_cb_flows(FlowState st, FlowScratc
                 }
                 int64_t wsv[kCbI];
                 uint32_t badm = 0, valm = 0;
-                const uint32_t j0 = base + (uint32_t)wave * kWaveItems + (uint32_t)lane * kCbI;
-                // loads first, unconditional at clamped indices (a load under a branch is waited for there)
+                const uint32_t wb = base + (uint32_t)wave * kWaveItems;
+                const uint32_t j0 = wb + (uint32_t)lane * kCbI;
+                // the wave's items through LDS: coalesced loads at clamped indices, then each lane's run
+                {
+#pragma unroll
+                    for (int i = 0; i < kCbI; ++i) {
+                        const uint32_t k = (uint32_t)i * 64 + (uint32_t)lane;
+                        const uint32_t j = min(wb + k, je - 1);
+                        const Payload q = pay[j];
+                        s_ts[wave][k + k / kCbI] = q.ts_off;
+                        s_fx[wave][k + k / kCbI] = q.idx;
+                        if (b.grade == 0) s_rt[wave][k + k / kCbI] = sc.rt_sorted[j];  // sorted order (k_lexits)
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                }
                 uint32_t tso[kCbI], fx[kCbI];
 #pragma unroll
                 for (int i = 0; i < kCbI; ++i) {
-                    const Payload q = pay[min(j0 + i, je - 1)];
-                    tso[i] = q.ts_off;
-                    fx[i] = q.idx;
+                    const uint32_t k = (uint32_t)lane * kCbI + (uint32_t)i;
+                    tso[i] = s_ts[wave][k + k / kCbI];
+                    fx[i] = s_fx[wave][k + k / kCbI];
                 }
                 if (b.grade == 0) {
-                    int64_t rtv[kCbI];  // in sorted order (k_lexits): contiguous, not a gather
 #pragma unroll
-                    for (int i = 0; i < kCbI; ++i) rtv[i] = sc.rt_sorted[min(j0 + i, je - 1)];
-#pragma unroll
-                    for (int i = 0; i < kCbI; ++i) badm |= (rtv[i] > b.max_allowed_rt ? 1u : 0u) << i;
+                    for (int i = 0; i < kCbI; ++i) {
+                        const uint32_t k = (uint32_t)lane * kCbI + (uint32_t)i;
+                        badm |= (s_rt[wave][k + k / kCbI] > b.max_allowed_rt ? 1u : 0u) << i;
+                    }
                 } else {
 #pragma unroll
                     for (int i = 0; i < kCbI; ++i) badm |= ((fx[i] & F_ERROR) ? 1u : 0u) << i;
