@@ -429,13 +429,24 @@ __device__ __forceinline__ bool lru_live(const MapRef &m, const LruRec &rec, PEn
     *pe = e;
     return true;
 }
+// SGA_LRU_PROF=1 (diagnostics only): [0] pushes [1] compactions [2] records scanned by them [3] their ticks
+// [4] evictions [5] records popped [6] k_llru entry ticks [7] k_llru exit ticks
+__device__ unsigned long long g_lru_prof[8];
+__device__ int g_lru_prof_on;
 __device__ void lru_compact(const MapRef &m, LruRec *area) {
+    const bool prof = g_lru_prof_on != 0;
+    const uint64_t t0 = prof ? wall_clock64() : 0;
     const uint64_t qcap = lru_qcap(m);
     uint64_t w = area[0].value;
     for (uint64_t i = area[0].value; i < area[0].stamp; ++i) {
         const LruRec rec = area[1 + i % qcap];
         PEntry *e;
         if (lru_live(m, rec, &e)) area[1 + (w++) % qcap] = rec;
+    }
+    if (prof) {
+        atomicAdd(&g_lru_prof[1], 1ull);
+        atomicAdd(&g_lru_prof[2], (unsigned long long)(area[0].stamp - area[0].value));
+        atomicAdd(&g_lru_prof[3], (unsigned long long)(wall_clock64() - t0));
     }
     area[0].stamp = w;
 }
@@ -450,14 +461,17 @@ __device__ void lru_push(const FlowState &st, const MapRef &m, uint64_t value, u
     }
     area[1 + area[0].stamp % qcap] = LruRec{value, stamp};
     area[0].stamp += 1;
+    if (g_lru_prof_on) atomicAdd(&g_lru_prof[0], 1ull);
 }
 // a full map's least recently used key (CLHM evicts after the insert that overflows it)
 __device__ void lru_evict(const FlowState &st, const MapRef &m) {
     LruRec *area = st.lpool + *m.q;
     const uint64_t qcap = lru_qcap(m);
+    if (g_lru_prof_on) atomicAdd(&g_lru_prof[4], 1ull);
     while (area[0].value < area[0].stamp) {
         const LruRec rec = area[1 + area[0].value % qcap];
         area[0].value += 1;
+        if (g_lru_prof_on) atomicAdd(&g_lru_prof[5], 1ull);
         PEntry *e;
         if (lru_live(m, rec, &e)) {
             e->a = kPAbsent;
@@ -1828,6 +1842,23 @@ __device__ int cb_take(const FlowState &st, const FlowScratch &sc, uint32_t res,
     return (ent && st.cbs[R.cb_off].state == 0) ? 1 : 2;
 }
 
+// k_llru_ps (below): LRU-mode parameter-only resources, chunked through LDS
+constexpr uint32_t kLruPs = 0x80000000u;
+constexpr int kPsPre = 256;
+__device__ __forceinline__ int64_t ps_ld(const int64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ps_ldu(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ bool lru_ps_take(const FlowState &st, uint32_t res) {
+    const ResDev R = st.res[res];
+    if (R.n_rules || R.n_cbs || R.n_prules != 1 || !st.tmapmask || st.tmapmask[res] != 1ull) return false;
+    const ParamRuleDev &p = st.prules[R.prule_off];
+    return p.grade == 1 && !p.cluster && p.idx_res == 0 && st.pstamp && st.tstamp && st.tbase &&
+           st.tbase[res] != kNoTBase;
+}
+
 __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, FlowScratch sc,
                                                const Payload *__restrict__ pay, const uint32_t *__restrict__ keys,
                                                int64_t ts_base, const int64_t *__restrict__ rt_in,
@@ -1843,7 +1874,9 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
             const uint32_t res = sc.run_slot[r0];
             const uint32_t nev = sc.run_end[r1 - 1] - sc.run_start[r0];
             if (st.lru_res && st.lru_res[res]) {  // a CacheMap in LRU mode: arrival order, one lane (k_llru)
-                sc.lru[atomicAdd(&sc.counters[10], 1u)] = fl;
+                // parameter-only: the chunked replay (k_llru_ps, SGA_LRU_PS=0 turns it off: an A/B knob)
+                const bool ps = st.lru_ps && lru_ps_take(st, res);
+                sc.lru[atomicAdd(&sc.counters[10], 1u)] = fl | (ps ? 0x80000000u : 0u);
                 continue;
             }
             int cbk = 0;
@@ -2842,6 +2875,7 @@ __global__ __launch_bounds__(64) void k_llru(FlowState st, int64_t max_rt, FlowS
     const uint32_t nl = sc.counters[10], nflows = sc.counters[2], nruns = sc.counters[1];
     for (uint32_t i = blockIdx.x * 64 + threadIdx.x; i < nl; i += gridDim.x * 64) {
         const uint32_t fl = sc.lru[i];
+        if (fl & 0x80000000u) continue;  // k_llru_ps (parameter-only, chunked)
         const uint32_t r0 = sc.flow_first_run[fl];
         const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
         const uint32_t res = sc.run_slot[r0];
@@ -2851,17 +2885,426 @@ __global__ __launch_bounds__(64) void k_llru(FlowState st, int64_t max_rt, FlowS
             const uint32_t idx = q.idx & F_IDX;
             const bool hp = (q.idx & F_PARAM) != 0;
             const uint64_t pv = hp ? param_in[idx] : 0;
+            const uint64_t tp = g_lru_prof_on ? wall_clock64() : 0;
             if (q.idx & F_EXIT) {
                 chain_exit<true>(c, res, t, rt_in[idx], (int)(q.acq_prio & 0x7FFFFFFFu), (q.idx & F_ERROR) != 0, hp,
                                  pv, PArgs{nullptr, 0}, idx);
+                if (tp) atomicAdd(&g_lru_prof[7], (unsigned long long)(wall_clock64() - tp));
             } else {
                 int64_t w = 0;
                 decision[idx] = chain_entry<true>(c, res, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
                                                   hp, pv, &w, PArgs{nullptr, 0}, idx);
                 wait_ms[idx] = (int32_t)w;
+                if (tp) atomicAdd(&g_lru_prof[6], (unsigned long long)(wall_clock64() - tp));
             }
         }
         for (uint32_t r = r0; r < r1; ++r) sc.run_mode[r] = RUN_DONE;
+    }
+}
+
+// ---- LRU-mode parameter-only resources, chunked through LDS (k_llru_ps)
+// A parameter-only resource (pseg_take's conditions: one QPS-grade ParamFlowRule of argument index 0, no
+// FlowRule, no breaker, only the index-0 thread-count map) whose maps are in LRU mode replays its events in
+// arrival order exactly as k_llru does, but one global round trip per chunk instead of ~25 per event: per
+// chunk of 64 events the 64 lanes load the events, find (or create) each distinct value's entry in the
+// rule's time/token map and in the thread-count map and copy them to LDS, and load the next kPsPre records
+// of each LRU queue with the state of their keys; lane 0 replays the chunk against those copies (queue
+// pushes gathered in LDS, evictions popping the loaded records, a global pop only past them); the lanes
+// write the copies, the evictions and the pushes back.  Decisions never read the node (as for pseg), so the
+// node statistics go in aggregate, run by run.  k_lflows flags these flows in sc.lru (kLruPs).
+struct PsQueue {  // one map's LRU queue during a chunk (lane-uniform)
+    LruRec *area;   // nullptr: free mode
+    uint64_t qcap, head, tail, used;  // used: records consumed from head this chunk
+    uint32_t npre, npush;
+};
+
+__global__ __launch_bounds__(64) void k_llru_ps(FlowState st, int64_t max_rt, FlowScratch sc,
+                                                const Payload *__restrict__ pay, int64_t ts_base,
+                                                const uint64_t *__restrict__ param_in, int8_t *decision,
+                                                int32_t *wait_ms) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    // per leader lane (a chunk's distinct value): the map entries and their copies
+    __shared__ uint32_t s_mslot[64], s_tslot[64];
+    __shared__ int64_t s_ma[64], s_mb[64], s_ta[64];
+    __shared__ uint64_t s_mst[64], s_tst[64], s_val[64];
+    __shared__ uint8_t s_tev[64], s_hasent[64];
+    // per event
+    __shared__ uint32_t s_lead[64], s_idx[64], s_run[64];
+    __shared__ int64_t s_t[64];
+    __shared__ int32_t s_acq[64], s_w[64];
+    __shared__ uint8_t s_fl[64];
+    __shared__ int8_t s_d[64];
+    // per map: the loaded queue records and their keys' state; pushes; evictions of keys outside the chunk
+    __shared__ uint64_t s_pst[2][kPsPre], s_pgst[2][kPsPre];
+    __shared__ uint32_t s_pslot[2][kPsPre];
+    __shared__ int8_t s_plink[2][kPsPre];
+    __shared__ uint8_t s_pgpres[2][kPsPre];
+    __shared__ LruRec s_push[2][64];
+    __shared__ uint32_t s_ev[2][64], s_nev[2];
+    __shared__ PsQueue s_q[2];
+    const int lane = threadIdx.x;
+    const Ctx c{st, max_rt};
+    const uint32_t nl = sc.counters[10], nflows = sc.counters[2], nruns = sc.counters[1];
+    for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+        const uint32_t flx = sc.lru[i];
+        if (!(flx & kLruPs)) continue;
+        const uint32_t fl = flx & ~kLruPs;
+        const uint32_t r0 = sc.flow_first_run[fl];
+        const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        const uint32_t res = sc.run_slot[r0];
+        const ParamRuleDev p = st.prules[st.res[res].prule_off];
+        const uint32_t mown = p.id + 1, town = tmap_owner(res, 0);
+        const uint32_t tj = st.tbase[res];
+        const uint32_t jb = sc.run_start[r0], je = sc.run_end[r1 - 1];
+        int64_t *node = st.node + (size_t)res * kNodeWords;
+        if (lane == 0) {
+            for (int m = 0; m < 2; ++m) {
+                const uint64_t q = m == 0 ? st.pq[p.id] : st.tq[tj];
+                PsQueue &Q = s_q[m];
+                Q.area = q == kNoQueue ? nullptr : st.lpool + q;
+                Q.qcap = 2ull * (m == 0 ? p.cap : (uint32_t)kThreadMapCap) + 2;
+                Q.head = Q.area ? ps_ldu(&Q.area[0].value) : 0;
+                Q.tail = Q.area ? ps_ldu(&Q.area[0].stamp) : 0;
+            }
+        }
+        uint32_t msize = st.psize[p.id], tsize = st.tsize[tj];  // lane 0's (single owner: plain counts)
+        const uint32_t mcap = p.cap, tcap = (uint32_t)kThreadMapCap;
+        // lane 0: the run in progress and its aggregates
+        uint32_t cur_run = 0xFFFFFFFFu;
+        int64_t pa = 0, ba = 0, np = 0, thr = 0;
+        auto apply_run = [&](uint32_t r) {
+            const int64_t tf = ts_base + (int64_t)sc.run_t0off[r];
+            int64_t *bs[2] = {sec_current(node, tf, max_rt), min_current(node, tf, max_rt)};
+            const int64_t exc = (int64_t)sc.run_exc[r], exerr = (int64_t)sc.run_exerr[r];
+            const int64_t exrt = sc.run_exrt[r], exmin = sc.run_exmin[r];
+            for (int k = 0; k < 2; ++k) {
+                int64_t *b = bs[k];
+                if (!b) continue;
+                b[MB_PASS] += pa;
+                b[MB_BLOCK] += ba;
+                b[MB_SUCC] += exc;
+                b[MB_RT] += exrt;
+                b[MB_EXC] += exerr;
+                if (exmin < b[MB_MINRT]) b[MB_MINRT] = exmin;
+            }
+            thr += np - (int64_t)sc.run_nexit[r];
+            sc.run_mode[r] = RUN_DONE;
+        };
+        for (uint32_t c0 = jb; c0 < je; c0 += 64) {
+            const uint32_t nk = min(64u, je - c0);
+            __syncthreads();
+            // 1. the chunk's events
+            const bool act = (uint32_t)lane < nk;
+            const uint32_t j = c0 + (uint32_t)lane;
+            const Payload q = act ? pay[j] : Payload{0, 0, 0, 0};
+            const bool ex = (q.idx & F_EXIT) != 0, hp = act && (q.idx & F_PARAM) != 0;
+            const uint64_t v = hp ? param_in[q.idx & F_IDX] : 0;
+            if (act) {
+                s_idx[lane] = q.idx & F_IDX;
+                s_t[lane] = ts_base + (int64_t)q.ts_off;
+                s_acq[lane] = (int32_t)(q.acq_prio & 0x7FFFFFFFu);
+                s_fl[lane] = (ex ? 1 : 0) | (hp ? 2 : 0);
+                s_run[lane] = sc.ev_run[j];
+            }
+            // 2. distinct values: the lowest lane of each value leads it
+            uint32_t lead = 64;
+            for (int k = 0; k < 64; ++k) {
+                const uint64_t vk = (uint64_t)__shfl((long long)v, k, 64);
+                const bool hk = __shfl((int)hp, k, 64) != 0;
+                if (hp && hk && vk == v && (uint32_t)k < lead) lead = (uint32_t)k;
+            }
+            s_lead[lane] = lead;
+            const bool leader = hp && lead == (uint32_t)lane;
+            s_hasent[lane] = 0;
+            __syncthreads();
+            if (hp && !ex) s_hasent[lead] = 1;  // the value's time/token entry is needed only by entries
+            __syncthreads();
+            // 3. the leaders' entries (created here, as chain_entry's ptab_get would), copied to LDS
+            s_mslot[lane] = 0xFFFFFFFFu;
+            s_tslot[lane] = 0xFFFFFFFFu;
+            s_tev[lane] = 0;
+            if (leader) {
+                s_val[lane] = v;
+                PEntry *me = s_hasent[lane] ? ptab_get(st.ptab, st.pmask, mown, v, true, st.overflow) : nullptr;
+                PEntry *te = ptab_get(st.ttab, st.tmask, town, v, true, st.overflow);
+                if (me) {
+                    const uint32_t ms = (uint32_t)(me - st.ptab);
+                    s_mslot[lane] = ms;
+                    s_ma[lane] = ps_ld(&me->a);
+                    s_mb[lane] = ps_ld(&me->b);
+                    s_mst[lane] = ps_ldu(&st.pstamp[ms]);
+                }
+                if (te) {
+                    const uint32_t ts = (uint32_t)(te - st.ttab);
+                    s_tslot[lane] = ts;
+                    s_ta[lane] = ps_ld(&te->a);
+                    s_tst[lane] = ps_ldu(&st.tstamp[ts]);
+                }
+            }
+            __syncthreads();
+            // 4. the next records of each queue, their keys' state, and which of them are the chunk's keys
+            for (int m = 0; m < 2; ++m) {
+                const PsQueue Q = s_q[m];
+                const uint32_t npre = Q.area ? (uint32_t)min<uint64_t>(kPsPre, Q.tail - Q.head) : 0u;
+                for (uint32_t k = (uint32_t)lane; k < npre; k += 64) {
+                    const LruRec *rp = &Q.area[1 + (Q.head + k) % Q.qcap];
+                    const uint64_t rv = ps_ldu(&rp->value), rs = ps_ldu(&rp->stamp);
+                    PEntry *tab = m == 0 ? st.ptab : st.ttab;
+                    PEntry *e = ptab_get(tab, m == 0 ? st.pmask : st.tmask, m == 0 ? mown : town, rv, false, st.overflow);
+                    uint32_t slot = 0xFFFFFFFFu;
+                    int8_t link = -1;
+                    uint8_t gp = 0;
+                    uint64_t gs = 0;
+                    if (e) {
+                        slot = (uint32_t)(e - tab);
+                        gp = ps_ld(&e->a) != kPAbsent ? 1 : 0;
+                        gs = ps_ldu(&(m == 0 ? st.pstamp : st.tstamp)[slot]);
+                        for (int l = 0; l < 64; ++l)
+                            if ((m == 0 ? s_mslot[l] : s_tslot[l]) == slot) link = (int8_t)l;
+                    }
+                    s_pst[m][k] = rs;
+                    s_pslot[m][k] = slot;
+                    s_plink[m][k] = link;
+                    s_pgpres[m][k] = gp;
+                    s_pgst[m][k] = gs;
+                }
+                if (lane == 0) {
+                    s_q[m].npre = npre;
+                    s_q[m].used = 0;
+                    s_q[m].npush = 0;
+                    s_nev[m] = 0;
+                }
+            }
+            __syncthreads();
+            // 5. lane 0: the chunk in arrival order (k_llru's chain_entry / chain_exit for this resource)
+            if (lane == 0) {
+                // pop the least recently used live key of map m (lru_evict): the loaded records, then the ring
+                auto evict = [&](int m) {
+                    PsQueue &Q = s_q[m];
+                    for (;;) {
+                        uint64_t rs;
+                        uint32_t slot;
+                        int link;
+                        bool gp;
+                        uint64_t gs;
+                        if (Q.used < Q.npre) {
+                            const uint32_t k = (uint32_t)Q.used;
+                            rs = s_pst[m][k];
+                            slot = s_pslot[m][k];
+                            link = s_plink[m][k];
+                            gp = s_pgpres[m][k] != 0;
+                            gs = s_pgst[m][k];
+                        } else if (Q.head + Q.used < Q.tail) {
+                            const LruRec *rp = &Q.area[1 + (Q.head + Q.used) % Q.qcap];
+                            const uint64_t rv = ps_ldu(&rp->value);
+                            rs = ps_ldu(&rp->stamp);
+                            PEntry *tab = m == 0 ? st.ptab : st.ttab;
+                            PEntry *e = ptab_get(tab, m == 0 ? st.pmask : st.tmask, m == 0 ? mown : town, rv, false,
+                                                 st.overflow);
+                            slot = e ? (uint32_t)(e - tab) : 0xFFFFFFFFu;
+                            link = -1;
+                            gp = false;
+                            gs = 0;
+                            if (e) {
+                                gp = ps_ld(&e->a) != kPAbsent;
+                                gs = ps_ldu(&(m == 0 ? st.pstamp : st.tstamp)[slot]);
+                                for (int l = 0; l < 64; ++l)
+                                    if ((m == 0 ? s_mslot[l] : s_tslot[l]) == slot) link = l;
+                            }
+                        } else {
+                            atomicOr(&st.lru_ctl[1], 2u);  // a full map without a live record: never expected
+                            atomicOr(st.overflow, 1u);
+                            return;
+                        }
+                        Q.used += 1;
+                        if (link >= 0) {
+                            const bool live = m == 0 ? (s_ma[link] != kPAbsent && s_mst[link] == rs)
+                                                     : (s_ta[link] != kPAbsent && s_tst[link] == rs);
+                            if (!live) continue;
+                            if (m == 0) {
+                                s_ma[link] = kPAbsent;
+                                s_mb[link] = kPAbsent;
+                                msize -= 1;
+                            } else {
+                                s_ta[link] = kPAbsent;
+                                s_tev[link] = 1;
+                                tsize -= 1;
+                            }
+                            return;
+                        }
+                        if (slot == 0xFFFFFFFFu || !gp || gs != rs) continue;
+                        s_ev[m][s_nev[m]++] = slot;
+                        if (m == 0) msize -= 1;
+                        else tsize -= 1;
+                        return;
+                    }
+                };
+                auto push = [&](int m, uint64_t val, uint64_t stamp) {
+                    PsQueue &Q = s_q[m];
+                    s_push[m][Q.npush++] = LruRec{val, stamp};
+                };
+                for (uint32_t k = 0; k < nk; ++k) {
+                    const uint8_t fl = s_fl[k];
+                    const uint32_t L = s_lead[k];
+                    const uint64_t stamp = lru_stamp(st, s_idx[k], 0);
+                    const uint32_t r = s_run[k];
+                    if (r != cur_run) {
+                        if (cur_run != 0xFFFFFFFFu) apply_run(cur_run);
+                        cur_run = r;
+                        pa = ba = np = 0;
+                    }
+                    const int acq = s_acq[k];
+                    int8_t d = D_PASS;
+                    int64_t w = 0;
+                    int tdelta = 0;
+                    if (!(fl & 1)) {  // entry
+                        if (fl & 2) {
+                            const uint64_t val = s_val[L];
+                            if (s_mslot[L] == 0xFFFFFFFFu) {  // the map is full (the batch fails with overflow)
+                                s_d[k] = D_BLOCK_PARAM;
+                                s_w[k] = 0;
+                                continue;
+                            }
+                            if (param_map_access(c, p, val, acq)) {  // time map then token map, one recency order
+                                if (s_ma[L] == kPAbsent) {
+                                    s_mst[L] = stamp;
+                                    msize += 1;
+                                    if (s_q[0].area) {
+                                        push(0, val, stamp);
+                                        if (msize > mcap) evict(0);
+                                    }
+                                } else {
+                                    s_mst[L] = stamp;
+                                    if (s_q[0].area) push(0, val, stamp);
+                                }
+                            }
+                            struct { int64_t a, b; } e{s_ma[L], s_mb[L]};
+                            const bool pass = param_pass_qps(c, p, e, val, acq, s_t[k], &w);
+                            s_ma[L] = e.a;
+                            s_mb[L] = e.b;
+                            if (!pass) {
+                                d = D_BLOCK_PARAM;
+                                w = 0;  // a block's detail: the rule's index
+                            }
+                        }
+                        if (d == D_PASS) {
+                            pa += acq;
+                            np += 1;
+                            tdelta = (fl & 2) ? 1 : 0;
+                        } else {
+                            ba += acq;
+                        }
+                        s_d[k] = d;
+                        s_w[k] = (int32_t)w;
+                    } else if (fl & 2) {
+                        tdelta = -1;
+                    }
+                    if (tdelta) {  // ParameterMetric.add / decreaseThreadCount of index 0 (param_threads)
+                        const uint64_t val = s_val[L];
+                        s_tst[L] = stamp;
+                        if (s_ta[L] == kPAbsent) {
+                            tsize += 1;
+                            if (s_q[1].area) {
+                                push(1, val, stamp);
+                                if (tsize > tcap) evict(1);
+                            }
+                            s_ta[L] = tdelta > 0 ? 1 : 0;
+                        } else {
+                            if (s_q[1].area) push(1, val, stamp);
+                            if (tdelta > 0) {
+                                s_ta[L] += 1;
+                            } else if (--s_ta[L] <= 0) {
+                                s_ta[L] = kPAbsent;
+                                tsize -= 1;
+                            }
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            // 6. write back: decisions, the copies, the evictions, then each queue's pushes (after a compaction
+            //    when the ring would overflow: live records kept in order, the whole wave 64 at a time)
+            if (act && !ex) {
+                decision[s_idx[lane]] = s_d[lane];
+                wait_ms[s_idx[lane]] = s_w[lane];
+            }
+            if (leader) {
+                const uint32_t ms = s_mslot[lane], ts = s_tslot[lane];
+                if (ms != 0xFFFFFFFFu) {
+                    st.ptab[ms].a = s_ma[lane];
+                    st.ptab[ms].b = s_mb[lane];
+                    st.pstamp[ms] = s_mst[lane];
+                }
+                if (ts != 0xFFFFFFFFu) {
+                    st.ttab[ts].a = s_ta[lane];
+                    if (s_tev[lane]) st.ttab[ts].b = kPAbsent;
+                    st.tstamp[ts] = s_tst[lane];
+                }
+            }
+            for (int m = 0; m < 2; ++m)
+                for (uint32_t k = (uint32_t)lane; k < s_nev[m]; k += 64) {
+                    PEntry *e = (m == 0 ? st.ptab : st.ttab) + s_ev[m][k];
+                    e->a = kPAbsent;
+                    e->b = kPAbsent;
+                }
+            __threadfence();
+            __syncthreads();
+            for (int m = 0; m < 2; ++m) {
+                PsQueue Q = s_q[m];
+                if (!Q.area) continue;
+                uint64_t head = Q.head + Q.used, tail = Q.tail;
+                if (tail - head + Q.npush > Q.qcap) {  // lru_compact over [head, tail)
+                    uint64_t w = head;
+                    const MapRef mr = m == 0 ? map_ref_p(st, p) : map_ref_t(st, res, 0);
+                    for (uint64_t b0 = head; b0 < tail; b0 += 64) {
+                        const uint64_t ix = b0 + (uint64_t)lane;
+                        LruRec rec{0, 0};
+                        bool live = false;
+                        if (ix < tail) {
+                            const LruRec *rp = &Q.area[1 + ix % Q.qcap];
+                            rec = LruRec{ps_ldu(&rp->value), ps_ldu(&rp->stamp)};
+                            PEntry *e = ptab_get(mr.tab, mr.mask, mr.owner, rec.value, false, st.overflow);
+                            live = e && ps_ld(&e->a) != kPAbsent && ps_ldu(&mr.stamp[e - mr.tab]) == rec.stamp;
+                        }
+                        const uint64_t bl = __ballot(live);
+                        __syncthreads();  // every lane has read its record before any is overwritten
+                        if (live) Q.area[1 + (w + (uint64_t)__popcll(bl & ((1ull << lane) - 1ull))) % Q.qcap] = rec;
+                        w += (uint64_t)__popcll(bl);
+                        __threadfence();
+                        __syncthreads();
+                    }
+                    tail = w;
+                    if (tail - head + Q.npush > Q.qcap) {
+                        if (lane == 0) {
+                            atomicOr(&st.lru_ctl[1], 2u);
+                            atomicOr(st.overflow, 1u);
+                        }
+                        Q.npush = 0;
+                    }
+                }
+                for (uint32_t k = (uint32_t)lane; k < Q.npush; k += 64) Q.area[1 + (tail + k) % Q.qcap] = s_push[m][k];
+                __threadfence();
+                __syncthreads();
+                if (lane == 0) {
+                    s_q[m].head = head;
+                    s_q[m].tail = tail + Q.npush;
+                }
+            }
+        }
+        __syncthreads();
+        if (lane == 0) {
+            if (cur_run != 0xFFFFFFFFu) apply_run(cur_run);
+            for (uint32_t r = r0; r < r1; ++r) sc.run_mode[r] = RUN_DONE;
+            node[kNodeThreads] += thr;
+            st.psize[p.id] = msize;
+            st.tsize[tj] = tsize;
+            for (int m = 0; m < 2; ++m)
+                if (s_q[m].area) {
+                    s_q[m].area[0].value = s_q[m].head;
+                    s_q[m].area[0].stamp = s_q[m].tail;
+                }
+        }
+        __syncthreads();
     }
 }
 
@@ -4012,6 +4455,8 @@ FlowState FlowEngine::state() const {
     s.pnew = d_pnew.p;
     s.tnew = d_tnew.p;
     s.lru_res = lru ? d_lru_res.p : nullptr;
+    static const bool lru_ps = !(getenv("SGA_LRU_PS") && atoi(getenv("SGA_LRU_PS")) == 0);
+    s.lru_ps = lru_ps ? 1 : 0;
     s.lru_ctl = d_lru_ctl.p;
     s.lru_list = d_lru_list.p;
     s.nprid = lru ? (uint32_t)d_psize.n : 0;
@@ -4125,6 +4570,22 @@ void FlowEngine::lru_prepare(const uint8_t *kind, const uint32_t *resource, cons
     hipLaunchKernelGGL(k_lru_collect, dim3(2048), dim3(kT), 0, s, st);
     hipLaunchKernelGGL(k_lru_sort, dim3(64), dim3(kLruSortThreads), 0, s, st);
     if (cparam_hook && has_cluster_prules && cluster_on && cparam_st.ctl) cparam_hook(s);
+    static const int prof = getenv("SGA_LRU_PROF") ? atoi(getenv("SGA_LRU_PROF")) : 0;  // diagnostics only
+    if (prof) {
+        static bool on = false;
+        unsigned long long v[8];
+        if (on) {  // the previous batch's counters
+            SGA_HIP_CHECK(hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_lru_prof), sizeof(v), 0, hipMemcpyDeviceToHost, s));
+            SGA_HIP_CHECK(hipStreamSynchronize(s));
+            fprintf(stderr, "lru_prof pushes %llu compactions %llu scanned %llu compact_ticks %llu evictions %llu popped %llu "
+                    "entry_ticks %llu exit_ticks %llu\n", v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+        }
+        std::memset(v, 0, sizeof(v));
+        const int one = 1;
+        SGA_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lru_prof), v, sizeof(v), 0, hipMemcpyHostToDevice, s));
+        SGA_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lru_prof_on), &one, sizeof(one), 0, hipMemcpyHostToDevice, s));
+        on = true;
+    }
     static const int dbg = getenv("SGA_LRU_DEBUG") ? atoi(getenv("SGA_LRU_DEBUG")) : 0;  // diagnostics only
     if (dbg) {
         uint32_t ctl[4];
@@ -4927,9 +5388,12 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, stream, st,
                            (int64_t)cfg.statistic_max_rt, fsc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p);
         launch_pseg(st, fsc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p, (uint32_t)m, stream);
-        if (st.lru_res)
+        if (st.lru_res) {
             hipLaunchKernelGGL(k_llru, dim3(64), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo,
                                d_rt.p, d_param.p, d_dec.p, d_wait.p);
+            hipLaunchKernelGGL(k_llru_ps, dim3(256), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo,
+                               d_param.p, d_dec.p, d_wait.p);
+        }
         hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
                            d_dec.p, d_wait.p, lwave_prof());
@@ -5048,9 +5512,12 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
     hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc,
                        pay, keys, ts_base, rt_p, param_p, d_decision, wait_p);
     launch_pseg(st, gsc, pay, keys, ts_base, rt_p, param_p, d_decision, wait_p, m, s);
-    if (st.lru_res)
+    if (st.lru_res) {
         hipLaunchKernelGGL(k_llru, dim3(64), dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p,
                            param_p, d_decision, wait_p);
+        hipLaunchKernelGGL(k_llru_ps, dim3(256), dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base,
+                           param_p, d_decision, wait_p);
+    }
     hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
                        st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
                        lwave_prof());

@@ -129,6 +129,7 @@ struct FlowState {
     // embedded cluster token server for cluster-mode FlowRules (sga_set_cluster_server 1)
     ClusterState cst;
     int32_t cluster_on;
+    int32_t lru_ps;              // k_llru_ps takes LRU-mode parameter-only resources (SGA_LRU_PS=0: k_llru)
     // device entry (sga_submit_events_device): the chunk's gate word, written by k_lgate; nullptr on
     // the host entry, which chooses the kernels itself
     const uint32_t *gate;
