@@ -22,6 +22,7 @@
 #include "cparam_exact.hpp"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstring>
 #include <new>
 
@@ -1844,7 +1845,7 @@ __device__ int cb_take(const FlowState &st, const FlowScratch &sc, uint32_t res,
 
 // k_llru_ps (below): LRU-mode parameter-only resources, chunked through LDS
 constexpr uint32_t kLruPs = 0x80000000u;
-constexpr int kPsPre = 256;
+constexpr int kPsPre = 128;
 __device__ __forceinline__ int64_t ps_ld(const int64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -2912,39 +2913,85 @@ __global__ __launch_bounds__(64) void k_llru(FlowState st, int64_t max_rt, FlowS
 // pushes gathered in LDS, evictions popping the loaded records, a global pop only past them); the lanes
 // write the copies, the evictions and the pushes back.  Decisions never read the node (as for pseg), so the
 // node statistics go in aggregate, run by run.  k_lflows flags these flows in sc.lru (kLruPs).
-struct PsQueue {  // one map's LRU queue during a chunk (lane-uniform)
-    LruRec *area;   // nullptr: free mode
-    uint64_t qcap, head, tail, used;  // used: records consumed from head this chunk
-    uint32_t npre, npush;
-};
+// SGA_LRU_PROF=1 (diagnostics only): k_llru_ps ticks per phase, summed over chunks: [0] events [1] loads +
+// dedupe [2] leader entries [3] queue records [4] replay [5] write-back [6] compaction [7] chunks
+__device__ unsigned long long g_lps_prof[8];
+
+__device__ __forceinline__ uint32_t rl32(uint32_t x, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t x, uint32_t l) {
+    return (uint64_t)rl32((uint32_t)x, l) | ((uint64_t)rl32((uint32_t)(x >> 32), l) << 32);
+}
+// lane l's copy of reg becomes v (v and l wave-uniform)
+__device__ __forceinline__ uint32_t wl32(uint32_t reg, uint32_t v, uint32_t l) { return threadIdx.x == l ? v : reg; }
+__device__ __forceinline__ uint64_t wl64(uint64_t reg, uint64_t v, uint32_t l) { return threadIdx.x == l ? v : reg; }
+// the entry of (owner, value) if present in the table, its home slot loaded first (the tables stay a quarter
+// full, so most keys sit there); kN lookups of one lane issued together
+template <int kN>
+__device__ __forceinline__ void ptab_find_n(PEntry *tab, uint32_t mask, uint32_t owner, const uint64_t (&v)[kN],
+                                            const bool (&want)[kN], PEntry *(&out)[kN], uint32_t *overflow) {
+    uint32_t ow[kN];
+    uint64_t vv[kN];
+#pragma unroll
+    for (int i = 0; i < kN; ++i) {
+        const uint32_t h = ptab_home(mask, owner, v[i]);
+        ow[i] = want[i] ? __hip_atomic_load(&tab[h].owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        vv[i] = want[i] ? tab[h].value : 0ull;
+    }
+#pragma unroll
+    for (int i = 0; i < kN; ++i) {
+        if (!want[i] || ow[i] == 0) {
+            out[i] = nullptr;
+        } else if (ow[i] == owner && vv[i] == v[i]) {
+            out[i] = &tab[ptab_home(mask, owner, v[i])];
+        } else {
+            out[i] = ptab_get(tab, mask, owner, v[i], false, overflow);
+        }
+    }
+}
+
+// the chunk's leader slots, slot -> leader lane (open addressing in LDS)
+constexpr int kPsHash = 256;
+__device__ __forceinline__ void ps_hash_put(uint32_t *keys, uint8_t *vals, uint32_t slot, uint32_t lane) {
+    uint32_t h = (slot * 2654435761u) >> 24;
+    for (;;) {
+        const uint32_t prev = atomicCAS(&keys[h], 0xFFFFFFFFu, slot);
+        if (prev == 0xFFFFFFFFu || prev == slot) {
+            vals[h] = (uint8_t)lane;
+            return;
+        }
+        h = (h + 1) & (kPsHash - 1);
+    }
+}
+__device__ __forceinline__ int ps_hash_get(const uint32_t *keys, const uint8_t *vals, uint32_t slot) {
+    uint32_t h = (slot * 2654435761u) >> 24;
+    for (;;) {
+        const uint32_t k = keys[h];
+        if (k == slot) return vals[h];
+        if (k == 0xFFFFFFFFu) return -1;
+        h = (h + 1) & (kPsHash - 1);
+    }
+}
 
 __global__ __launch_bounds__(64) void k_llru_ps(FlowState st, int64_t max_rt, FlowScratch sc,
                                                 const Payload *__restrict__ pay, int64_t ts_base,
                                                 const uint64_t *__restrict__ param_in, int8_t *decision,
                                                 int32_t *wait_ms) {
     if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
-    // per leader lane (a chunk's distinct value): the map entries and their copies
-    __shared__ uint32_t s_mslot[64], s_tslot[64];
-    __shared__ int64_t s_ma[64], s_mb[64], s_ta[64];
-    __shared__ uint64_t s_mst[64], s_tst[64], s_val[64];
-    __shared__ uint8_t s_tev[64], s_hasent[64];
-    // per event
-    __shared__ uint32_t s_lead[64], s_idx[64], s_run[64];
-    __shared__ int64_t s_t[64];
-    __shared__ int32_t s_acq[64], s_w[64];
-    __shared__ uint8_t s_fl[64];
-    __shared__ int8_t s_d[64];
-    // per map: the loaded queue records and their keys' state; pushes; evictions of keys outside the chunk
-    __shared__ uint64_t s_pst[2][kPsPre], s_pgst[2][kPsPre];
+    __shared__ uint32_t s_hk[2][kPsHash];
+    __shared__ uint8_t s_hv[2][kPsHash];
+    __shared__ uint8_t s_hasent[64];
+    // the loaded queue records (record k of map m at [m][k]) and their keys' state
+    __shared__ uint64_t s_pst[2][kPsPre], s_pgs[2][kPsPre];
     __shared__ uint32_t s_pslot[2][kPsPre];
     __shared__ int8_t s_plink[2][kPsPre];
-    __shared__ uint8_t s_pgpres[2][kPsPre];
-    __shared__ LruRec s_push[2][64];
-    __shared__ uint32_t s_ev[2][64], s_nev[2];
-    __shared__ PsQueue s_q[2];
-    const int lane = threadIdx.x;
+    __shared__ uint8_t s_pgp[2][kPsPre];
+    constexpr int kPre = kPsPre / 64;  // queue records per lane and map
+    const uint32_t lane = threadIdx.x;
     const Ctx c{st, max_rt};
     const uint32_t nl = sc.counters[10], nflows = sc.counters[2], nruns = sc.counters[1];
+    const bool prof = g_lru_prof_on != 0;
     for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
         const uint32_t flx = sc.lru[i];
         if (!(flx & kLruPs)) continue;
@@ -2953,26 +3000,28 @@ __global__ __launch_bounds__(64) void k_llru_ps(FlowState st, int64_t max_rt, Fl
         const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
         const uint32_t res = sc.run_slot[r0];
         const ParamRuleDev p = st.prules[st.res[res].prule_off];
-        const uint32_t mown = p.id + 1, town = tmap_owner(res, 0);
+        const uint32_t own[2] = {p.id + 1, tmap_owner(res, 0)};
+        PEntry *const tab[2] = {st.ptab, st.ttab};
+        const uint32_t tmask[2] = {st.pmask, st.tmask};
+        uint64_t *const tstamp[2] = {st.pstamp, st.tstamp};
         const uint32_t tj = st.tbase[res];
         const uint32_t jb = sc.run_start[r0], je = sc.run_end[r1 - 1];
         int64_t *node = st.node + (size_t)res * kNodeWords;
-        if (lane == 0) {
-            for (int m = 0; m < 2; ++m) {
-                const uint64_t q = m == 0 ? st.pq[p.id] : st.tq[tj];
-                PsQueue &Q = s_q[m];
-                Q.area = q == kNoQueue ? nullptr : st.lpool + q;
-                Q.qcap = 2ull * (m == 0 ? p.cap : (uint32_t)kThreadMapCap) + 2;
-                Q.head = Q.area ? ps_ldu(&Q.area[0].value) : 0;
-                Q.tail = Q.area ? ps_ldu(&Q.area[0].stamp) : 0;
-            }
+        // the queues (wave-uniform)
+        LruRec *area[2];
+        uint64_t qcap[2], head[2], tail[2];
+        for (int m = 0; m < 2; ++m) {
+            const uint64_t q = m == 0 ? st.pq[p.id] : st.tq[tj];
+            area[m] = q == kNoQueue ? nullptr : st.lpool + q;
+            qcap[m] = 2ull * (m == 0 ? p.cap : (uint32_t)kThreadMapCap) + 2;
+            head[m] = area[m] ? ps_ldu(&area[m][0].value) : 0;
+            tail[m] = area[m] ? ps_ldu(&area[m][0].stamp) : 0;
         }
-        uint32_t msize = st.psize[p.id], tsize = st.tsize[tj];  // lane 0's (single owner: plain counts)
-        const uint32_t mcap = p.cap, tcap = (uint32_t)kThreadMapCap;
-        // lane 0: the run in progress and its aggregates
+        uint32_t size[2] = {st.psize[p.id], st.tsize[tj]};
+        const uint32_t cap[2] = {p.cap, (uint32_t)kThreadMapCap};
         uint32_t cur_run = 0xFFFFFFFFu;
         int64_t pa = 0, ba = 0, np = 0, thr = 0;
-        auto apply_run = [&](uint32_t r) {
+        auto apply_run = [&](uint32_t r) {  // lane 0
             const int64_t tf = ts_base + (int64_t)sc.run_t0off[r];
             int64_t *bs[2] = {sec_current(node, tf, max_rt), min_current(node, tf, max_rt)};
             const int64_t exc = (int64_t)sc.run_exc[r], exerr = (int64_t)sc.run_exerr[r];
@@ -2988,24 +3037,31 @@ __global__ __launch_bounds__(64) void k_llru_ps(FlowState st, int64_t max_rt, Fl
                 if (exmin < b[MB_MINRT]) b[MB_MINRT] = exmin;
             }
             thr += np - (int64_t)sc.run_nexit[r];
-            sc.run_mode[r] = RUN_DONE;
+        };
+        uint64_t tp = prof ? wall_clock64() : 0;
+        auto mark = [&](int ph) __attribute__((always_inline)) {
+            if (!prof) return;
+            const uint64_t now = wall_clock64();
+            if (lane == 0) atomicAdd(&g_lps_prof[ph], (unsigned long long)(now - tp));
+            tp = now;
         };
         for (uint32_t c0 = jb; c0 < je; c0 += 64) {
             const uint32_t nk = min(64u, je - c0);
-            __syncthreads();
-            // 1. the chunk's events
-            const bool act = (uint32_t)lane < nk;
-            const uint32_t j = c0 + (uint32_t)lane;
+            if (prof && lane == 0) {
+                atomicAdd(&g_lps_prof[0], (unsigned long long)nk);
+                atomicAdd(&g_lps_prof[7], 1ull);
+            }
+            tp = prof ? wall_clock64() : 0;
+            // 1. this lane's event
+            const bool act = lane < nk;
+            const uint32_t j = c0 + lane;
             const Payload q = act ? pay[j] : Payload{0, 0, 0, 0};
             const bool ex = (q.idx & F_EXIT) != 0, hp = act && (q.idx & F_PARAM) != 0;
             const uint64_t v = hp ? param_in[q.idx & F_IDX] : 0;
-            if (act) {
-                s_idx[lane] = q.idx & F_IDX;
-                s_t[lane] = ts_base + (int64_t)q.ts_off;
-                s_acq[lane] = (int32_t)(q.acq_prio & 0x7FFFFFFFu);
-                s_fl[lane] = (ex ? 1 : 0) | (hp ? 2 : 0);
-                s_run[lane] = sc.ev_run[j];
-            }
+            const uint32_t e_fl = (ex ? 1u : 0u) | (hp ? 2u : 0u);
+            const uint32_t e_idx = q.idx & F_IDX, e_run = act ? sc.ev_run[j] : 0u;
+            const int64_t e_t = ts_base + (int64_t)q.ts_off;
+            const int32_t e_acq = (int32_t)(q.acq_prio & 0x7FFFFFFFu);
             // 2. distinct values: the lowest lane of each value leads it
             uint32_t lead = 64;
             for (int k = 0; k < 64; ++k) {
@@ -3013,295 +3069,300 @@ __global__ __launch_bounds__(64) void k_llru_ps(FlowState st, int64_t max_rt, Fl
                 const bool hk = __shfl((int)hp, k, 64) != 0;
                 if (hp && hk && vk == v && (uint32_t)k < lead) lead = (uint32_t)k;
             }
-            s_lead[lane] = lead;
-            const bool leader = hp && lead == (uint32_t)lane;
+            const uint32_t e_lead = lead;
+            const bool leader = hp && lead == lane;
             s_hasent[lane] = 0;
+            for (int m = 0; m < 2; ++m)
+                for (uint32_t k = lane; k < (uint32_t)kPsHash; k += 64) s_hk[m][k] = 0xFFFFFFFFu;
             __syncthreads();
             if (hp && !ex) s_hasent[lead] = 1;  // the value's time/token entry is needed only by entries
             __syncthreads();
-            // 3. the leaders' entries (created here, as chain_entry's ptab_get would), copied to LDS
-            s_mslot[lane] = 0xFFFFFFFFu;
-            s_tslot[lane] = 0xFFFFFFFFu;
-            s_tev[lane] = 0;
+            mark(1);
+            // 3. the leaders' entries (created here, as chain_entry's ptab_get would), kept in their lanes
+            uint32_t c_slot[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+            uint64_t c_val = v, c_st[2] = {0, 0};
+            int64_t c_ma = kPAbsent, c_mb = kPAbsent, c_ta = kPAbsent;
+            uint32_t c_tev = 0;
             if (leader) {
-                s_val[lane] = v;
-                PEntry *me = s_hasent[lane] ? ptab_get(st.ptab, st.pmask, mown, v, true, st.overflow) : nullptr;
-                PEntry *te = ptab_get(st.ttab, st.tmask, town, v, true, st.overflow);
+                // both home slots first (most keys sit there), the probe loops only past them
+                const uint32_t hm = ptab_home(st.pmask, own[0], v), ht = ptab_home(st.tmask, own[1], v);
+                const uint32_t om = __hip_atomic_load(&st.ptab[hm].owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t ot = __hip_atomic_load(&st.ttab[ht].owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t vm = st.ptab[hm].value, vt = st.ttab[ht].value;
+                PEntry *me = !s_hasent[lane] ? nullptr
+                             : (om == own[0] && vm == v) ? &st.ptab[hm]
+                                                         : ptab_get(st.ptab, st.pmask, own[0], v, true, st.overflow);
+                PEntry *te = (ot == own[1] && vt == v) ? &st.ttab[ht] : ptab_get(st.ttab, st.tmask, own[1], v, true, st.overflow);
                 if (me) {
-                    const uint32_t ms = (uint32_t)(me - st.ptab);
-                    s_mslot[lane] = ms;
-                    s_ma[lane] = ps_ld(&me->a);
-                    s_mb[lane] = ps_ld(&me->b);
-                    s_mst[lane] = ps_ldu(&st.pstamp[ms]);
+                    c_slot[0] = (uint32_t)(me - st.ptab);
+                    c_ma = ps_ld(&me->a);
+                    c_mb = ps_ld(&me->b);
+                    c_st[0] = ps_ldu(&st.pstamp[c_slot[0]]);
+                    ps_hash_put(s_hk[0], s_hv[0], c_slot[0], lane);
                 }
                 if (te) {
-                    const uint32_t ts = (uint32_t)(te - st.ttab);
-                    s_tslot[lane] = ts;
-                    s_ta[lane] = ps_ld(&te->a);
-                    s_tst[lane] = ps_ldu(&st.tstamp[ts]);
+                    c_slot[1] = (uint32_t)(te - st.ttab);
+                    c_ta = ps_ld(&te->a);
+                    c_st[1] = ps_ldu(&st.tstamp[c_slot[1]]);
+                    ps_hash_put(s_hk[1], s_hv[1], c_slot[1], lane);
                 }
             }
             __syncthreads();
-            // 4. the next records of each queue, their keys' state, and which of them are the chunk's keys
+            mark(2);
+            // 4. the next kPsPre records of each queue (record k in lane k % 64, register k / 64) with their
+            //    keys' state, and which of them are the chunk's keys
+            uint32_t npre[2];
+#pragma unroll
             for (int m = 0; m < 2; ++m) {
-                const PsQueue Q = s_q[m];
-                const uint32_t npre = Q.area ? (uint32_t)min<uint64_t>(kPsPre, Q.tail - Q.head) : 0u;
-                for (uint32_t k = (uint32_t)lane; k < npre; k += 64) {
-                    const LruRec *rp = &Q.area[1 + (Q.head + k) % Q.qcap];
-                    const uint64_t rv = ps_ldu(&rp->value), rs = ps_ldu(&rp->stamp);
-                    PEntry *tab = m == 0 ? st.ptab : st.ttab;
-                    PEntry *e = ptab_get(tab, m == 0 ? st.pmask : st.tmask, m == 0 ? mown : town, rv, false, st.overflow);
-                    uint32_t slot = 0xFFFFFFFFu;
-                    int8_t link = -1;
-                    uint8_t gp = 0;
-                    uint64_t gs = 0;
-                    if (e) {
-                        slot = (uint32_t)(e - tab);
-                        gp = ps_ld(&e->a) != kPAbsent ? 1 : 0;
-                        gs = ps_ldu(&(m == 0 ? st.pstamp : st.tstamp)[slot]);
-                        for (int l = 0; l < 64; ++l)
-                            if ((m == 0 ? s_mslot[l] : s_tslot[l]) == slot) link = (int8_t)l;
-                    }
-                    s_pst[m][k] = rs;
-                    s_pslot[m][k] = slot;
-                    s_plink[m][k] = link;
-                    s_pgpres[m][k] = gp;
-                    s_pgst[m][k] = gs;
+                npre[m] = area[m] ? (uint32_t)min<uint64_t>(kPsPre, tail[m] - head[m]) : 0u;
+                uint64_t rv[kPre];
+                bool want[kPre];
+                uint64_t rs[kPre];
+#pragma unroll
+                for (int r = 0; r < kPre; ++r) {
+                    const uint32_t k = (uint32_t)r * 64 + lane;
+                    want[r] = k < npre[m];
+                    const LruRec *rp = want[r] ? &area[m][1 + (head[m] + k) % qcap[m]] : nullptr;
+                    rv[r] = want[r] ? ps_ldu(&rp->value) : 0ull;
+                    rs[r] = want[r] ? ps_ldu(&rp->stamp) : 0ull;
                 }
-                if (lane == 0) {
-                    s_q[m].npre = npre;
-                    s_q[m].used = 0;
-                    s_q[m].npush = 0;
-                    s_nev[m] = 0;
+                PEntry *e[kPre];
+                ptab_find_n<kPre>(tab[m], tmask[m], own[m], rv, want, e, st.overflow);
+#pragma unroll
+                for (int r = 0; r < kPre; ++r) {
+                    if (!want[r]) continue;
+                    const uint32_t k = (uint32_t)r * 64 + lane;
+                    const uint32_t slot = e[r] ? (uint32_t)(e[r] - tab[m]) : 0xFFFFFFFFu;
+                    s_pst[m][k] = rs[r];
+                    s_pslot[m][k] = slot;
+                    s_pgp[m][k] = e[r] && ps_ld(&e[r]->a) != kPAbsent ? 1 : 0;
+                    s_pgs[m][k] = e[r] ? ps_ldu(&tstamp[m][slot]) : 0ull;
+                    s_plink[m][k] = (int8_t)(e[r] ? ps_hash_get(s_hk[m], s_hv[m], slot) : -1);
                 }
             }
             __syncthreads();
-            // 5. lane 0: the chunk in arrival order (k_llru's chain_entry / chain_exit for this resource)
-            if (lane == 0) {
-                // pop the least recently used live key of map m (lru_evict): the loaded records, then the ring
-                auto evict = [&](int m) {
-                    PsQueue &Q = s_q[m];
-                    for (;;) {
-                        uint64_t rs;
-                        uint32_t slot;
-                        int link;
-                        bool gp;
-                        uint64_t gs;
-                        if (Q.used < Q.npre) {
-                            const uint32_t k = (uint32_t)Q.used;
-                            rs = s_pst[m][k];
-                            slot = s_pslot[m][k];
-                            link = s_plink[m][k];
-                            gp = s_pgpres[m][k] != 0;
-                            gs = s_pgst[m][k];
-                        } else if (Q.head + Q.used < Q.tail) {
-                            const LruRec *rp = &Q.area[1 + (Q.head + Q.used) % Q.qcap];
-                            const uint64_t rv = ps_ldu(&rp->value);
-                            rs = ps_ldu(&rp->stamp);
-                            PEntry *tab = m == 0 ? st.ptab : st.ttab;
-                            PEntry *e = ptab_get(tab, m == 0 ? st.pmask : st.tmask, m == 0 ? mown : town, rv, false,
-                                                 st.overflow);
-                            slot = e ? (uint32_t)(e - tab) : 0xFFFFFFFFu;
-                            link = -1;
-                            gp = false;
-                            gs = 0;
-                            if (e) {
-                                gp = ps_ld(&e->a) != kPAbsent;
-                                gs = ps_ldu(&(m == 0 ? st.pstamp : st.tstamp)[slot]);
-                                for (int l = 0; l < 64; ++l)
-                                    if ((m == 0 ? s_mslot[l] : s_tslot[l]) == slot) link = l;
-                            }
-                        } else {
+            mark(3);
+            // 5. the chunk in arrival order, wave-uniform: every lane takes the same steps on values read
+            //    out of the owning lanes (k_llru's chain_entry / chain_exit for this resource)
+            uint64_t used[2] = {0, 0};
+            uint32_t npush[2] = {0, 0}, nev[2] = {0, 0};
+            uint64_t q_pv[2] = {0, 0}, q_ps[2] = {0, 0};
+            uint32_t ev_slot[2] = {0, 0};
+            int32_t r_d = 0, r_w = 0;
+            auto evict = [&](auto mc) __attribute__((always_inline)) {  // mc: std::integral_constant<int, map>
+                constexpr int m = decltype(mc)::value;
+                for (;;) {
+                    uint64_t rs, gs;
+                    uint32_t slot, gp;
+                    int link;
+                    if (used[m] < npre[m]) {
+                        const uint32_t k = (uint32_t)used[m];
+                        rs = s_pst[m][k];
+                        gs = s_pgs[m][k];
+                        slot = s_pslot[m][k];
+                        gp = s_pgp[m][k];
+                        link = s_plink[m][k];
+                    } else if (head[m] + used[m] < tail[m]) {  // past the loaded records: one global pop
+                        const LruRec *rp = &area[m][1 + (head[m] + used[m]) % qcap[m]];
+                        const uint64_t rv = ps_ldu(&rp->value);
+                        rs = ps_ldu(&rp->stamp);
+                        PEntry *e = ptab_get(tab[m], tmask[m], own[m], rv, false, st.overflow);
+                        slot = e ? (uint32_t)(e - tab[m]) : 0xFFFFFFFFu;
+                        gp = e && ps_ld(&e->a) != kPAbsent ? 1u : 0u;
+                        gs = e ? ps_ldu(&tstamp[m][slot]) : 0ull;
+                        const uint64_t hit = __ballot(c_slot[m] == slot && slot != 0xFFFFFFFFu);
+                        link = hit ? __builtin_ctzll(hit) : -1;
+                    } else {
+                        if (lane == 0) {
                             atomicOr(&st.lru_ctl[1], 2u);  // a full map without a live record: never expected
                             atomicOr(st.overflow, 1u);
-                            return;
                         }
-                        Q.used += 1;
-                        if (link >= 0) {
-                            const bool live = m == 0 ? (s_ma[link] != kPAbsent && s_mst[link] == rs)
-                                                     : (s_ta[link] != kPAbsent && s_tst[link] == rs);
-                            if (!live) continue;
-                            if (m == 0) {
-                                s_ma[link] = kPAbsent;
-                                s_mb[link] = kPAbsent;
-                                msize -= 1;
-                            } else {
-                                s_ta[link] = kPAbsent;
-                                s_tev[link] = 1;
-                                tsize -= 1;
-                            }
-                            return;
-                        }
-                        if (slot == 0xFFFFFFFFu || !gp || gs != rs) continue;
-                        s_ev[m][s_nev[m]++] = slot;
-                        if (m == 0) msize -= 1;
-                        else tsize -= 1;
                         return;
                     }
-                };
-                auto push = [&](int m, uint64_t val, uint64_t stamp) {
-                    PsQueue &Q = s_q[m];
-                    s_push[m][Q.npush++] = LruRec{val, stamp};
-                };
-                for (uint32_t k = 0; k < nk; ++k) {
-                    const uint8_t fl = s_fl[k];
-                    const uint32_t L = s_lead[k];
-                    const uint64_t stamp = lru_stamp(st, s_idx[k], 0);
-                    const uint32_t r = s_run[k];
-                    if (r != cur_run) {
-                        if (cur_run != 0xFFFFFFFFu) apply_run(cur_run);
-                        cur_run = r;
-                        pa = ba = np = 0;
+                    used[m] += 1;
+                    if (link >= 0) {
+                        const uint32_t L = (uint32_t)link;
+                        const bool live = m == 0 ? ((int64_t)rl64((uint64_t)c_ma, L) != kPAbsent && rl64(c_st[0], L) == rs)
+                                                 : ((int64_t)rl64((uint64_t)c_ta, L) != kPAbsent && rl64(c_st[1], L) == rs);
+                        if (!live) continue;
+                        if (m == 0) {
+                            c_ma = (int64_t)wl64((uint64_t)c_ma, (uint64_t)kPAbsent, L);
+                            c_mb = (int64_t)wl64((uint64_t)c_mb, (uint64_t)kPAbsent, L);
+                        } else {
+                            c_ta = (int64_t)wl64((uint64_t)c_ta, (uint64_t)kPAbsent, L);
+                            c_tev = wl32(c_tev, 1u, L);
+                        }
+                        size[m] -= 1;
+                        return;
                     }
-                    const int acq = s_acq[k];
-                    int8_t d = D_PASS;
-                    int64_t w = 0;
-                    int tdelta = 0;
-                    if (!(fl & 1)) {  // entry
-                        if (fl & 2) {
-                            const uint64_t val = s_val[L];
-                            if (s_mslot[L] == 0xFFFFFFFFu) {  // the map is full (the batch fails with overflow)
-                                s_d[k] = D_BLOCK_PARAM;
-                                s_w[k] = 0;
-                                continue;
-                            }
+                    if (slot == 0xFFFFFFFFu || !gp || gs != rs) continue;
+                    ev_slot[m] = wl32(ev_slot[m], slot, nev[m]);
+                    nev[m] += 1;
+                    size[m] -= 1;
+                    return;
+                }
+            };
+            auto push = [&](auto mc, uint64_t val, uint64_t stamp) __attribute__((always_inline)) {
+                constexpr int m = decltype(mc)::value;
+                q_pv[m] = wl64(q_pv[m], val, npush[m]);
+                q_ps[m] = wl64(q_ps[m], stamp, npush[m]);
+                npush[m] += 1;
+            };
+            for (uint32_t k = 0; k < nk; ++k) {
+                const uint32_t fl = rl32(e_fl, k);
+                const uint32_t L = rl32(e_lead, k);
+                const uint64_t stamp = lru_stamp(st, rl32(e_idx, k), 0);
+                const uint32_t r = rl32(e_run, k);
+                if (r != cur_run) {
+                    if (cur_run != 0xFFFFFFFFu && lane == 0) apply_run(cur_run);
+                    cur_run = r;
+                    pa = ba = np = 0;
+                }
+                const int acq = (int)rl32((uint32_t)e_acq, k);
+                int d = D_PASS;
+                int64_t w = 0;
+                int tdelta = 0;
+                if (!(fl & 1)) {  // entry
+                    if (fl & 2) {
+                        const uint64_t val = rl64(c_val, L);
+                        if (rl32(c_slot[0], L) == 0xFFFFFFFFu) {  // the map is full: the batch fails (overflow)
+                            d = D_BLOCK_PARAM;
+                        } else {
+                            const int64_t t = (int64_t)rl64((uint64_t)e_t, k);
                             if (param_map_access(c, p, val, acq)) {  // time map then token map, one recency order
-                                if (s_ma[L] == kPAbsent) {
-                                    s_mst[L] = stamp;
-                                    msize += 1;
-                                    if (s_q[0].area) {
-                                        push(0, val, stamp);
-                                        if (msize > mcap) evict(0);
-                                    }
-                                } else {
-                                    s_mst[L] = stamp;
-                                    if (s_q[0].area) push(0, val, stamp);
+                                const bool absent = (int64_t)rl64((uint64_t)c_ma, L) == kPAbsent;
+                                c_st[0] = wl64(c_st[0], stamp, L);
+                                if (absent) size[0] += 1;
+                                if (area[0]) {
+                                    push(std::integral_constant<int, 0>{}, val, stamp);
+                                    if (absent && size[0] > cap[0]) evict(std::integral_constant<int, 0>{});
                                 }
                             }
-                            struct { int64_t a, b; } e{s_ma[L], s_mb[L]};
-                            const bool pass = param_pass_qps(c, p, e, val, acq, s_t[k], &w);
-                            s_ma[L] = e.a;
-                            s_mb[L] = e.b;
+                            struct { int64_t a, b; } e{(int64_t)rl64((uint64_t)c_ma, L), (int64_t)rl64((uint64_t)c_mb, L)};
+                            const bool pass = param_pass_qps(c, p, e, val, acq, t, &w);
+                            c_ma = (int64_t)wl64((uint64_t)c_ma, (uint64_t)e.a, L);
+                            c_mb = (int64_t)wl64((uint64_t)c_mb, (uint64_t)e.b, L);
                             if (!pass) {
                                 d = D_BLOCK_PARAM;
                                 w = 0;  // a block's detail: the rule's index
                             }
                         }
-                        if (d == D_PASS) {
-                            pa += acq;
-                            np += 1;
-                            tdelta = (fl & 2) ? 1 : 0;
-                        } else {
-                            ba += acq;
-                        }
-                        s_d[k] = d;
-                        s_w[k] = (int32_t)w;
-                    } else if (fl & 2) {
-                        tdelta = -1;
                     }
-                    if (tdelta) {  // ParameterMetric.add / decreaseThreadCount of index 0 (param_threads)
-                        const uint64_t val = s_val[L];
-                        s_tst[L] = stamp;
-                        if (s_ta[L] == kPAbsent) {
-                            tsize += 1;
-                            if (s_q[1].area) {
-                                push(1, val, stamp);
-                                if (tsize > tcap) evict(1);
-                            }
-                            s_ta[L] = tdelta > 0 ? 1 : 0;
-                        } else {
-                            if (s_q[1].area) push(1, val, stamp);
-                            if (tdelta > 0) {
-                                s_ta[L] += 1;
-                            } else if (--s_ta[L] <= 0) {
-                                s_ta[L] = kPAbsent;
-                                tsize -= 1;
-                            }
+                    if (d == D_PASS) {
+                        pa += acq;
+                        np += 1;
+                        tdelta = (fl & 2) ? 1 : 0;
+                    } else {
+                        ba += acq;
+                    }
+                    r_d = (int32_t)wl32((uint32_t)r_d, (uint32_t)d, k);
+                    r_w = (int32_t)wl32((uint32_t)r_w, (uint32_t)(int32_t)w, k);
+                } else if (fl & 2) {
+                    tdelta = -1;
+                }
+                if (tdelta && rl32(c_slot[1], L) != 0xFFFFFFFFu) {  // ParameterMetric.add / decreaseThreadCount
+                    const uint64_t val = rl64(c_val, L);
+                    const int64_t ta = (int64_t)rl64((uint64_t)c_ta, L);
+                    c_st[1] = wl64(c_st[1], stamp, L);
+                    int64_t nt;
+                    if (ta == kPAbsent) {
+                        size[1] += 1;
+                        if (area[1]) {
+                            push(std::integral_constant<int, 1>{}, val, stamp);
+                            if (size[1] > cap[1]) evict(std::integral_constant<int, 1>{});
+                        }
+                        nt = tdelta > 0 ? 1 : 0;
+                    } else {
+                        if (area[1]) push(std::integral_constant<int, 1>{}, val, stamp);
+                        nt = ta + (tdelta > 0 ? 1 : -1);
+                        if (tdelta < 0 && nt <= 0) {
+                            nt = kPAbsent;
+                            size[1] -= 1;
                         }
                     }
+                    c_ta = (int64_t)wl64((uint64_t)c_ta, (uint64_t)nt, L);
                 }
             }
-            __syncthreads();
+            mark(4);
             // 6. write back: decisions, the copies, the evictions, then each queue's pushes (after a compaction
-            //    when the ring would overflow: live records kept in order, the whole wave 64 at a time)
+            //    when the ring would overflow: live records kept in order, the wave 64 at a time)
             if (act && !ex) {
-                decision[s_idx[lane]] = s_d[lane];
-                wait_ms[s_idx[lane]] = s_w[lane];
+                decision[e_idx] = (int8_t)r_d;
+                wait_ms[e_idx] = r_w;
             }
             if (leader) {
-                const uint32_t ms = s_mslot[lane], ts = s_tslot[lane];
-                if (ms != 0xFFFFFFFFu) {
-                    st.ptab[ms].a = s_ma[lane];
-                    st.ptab[ms].b = s_mb[lane];
-                    st.pstamp[ms] = s_mst[lane];
+                if (c_slot[0] != 0xFFFFFFFFu) {
+                    st.ptab[c_slot[0]].a = c_ma;
+                    st.ptab[c_slot[0]].b = c_mb;
+                    st.pstamp[c_slot[0]] = c_st[0];
                 }
-                if (ts != 0xFFFFFFFFu) {
-                    st.ttab[ts].a = s_ta[lane];
-                    if (s_tev[lane]) st.ttab[ts].b = kPAbsent;
-                    st.tstamp[ts] = s_tst[lane];
+                if (c_slot[1] != 0xFFFFFFFFu) {
+                    st.ttab[c_slot[1]].a = c_ta;
+                    if (c_tev) st.ttab[c_slot[1]].b = kPAbsent;
+                    st.tstamp[c_slot[1]] = c_st[1];
                 }
             }
+#pragma unroll
             for (int m = 0; m < 2; ++m)
-                for (uint32_t k = (uint32_t)lane; k < s_nev[m]; k += 64) {
-                    PEntry *e = (m == 0 ? st.ptab : st.ttab) + s_ev[m][k];
+                if (lane < nev[m]) {
+                    PEntry *e = tab[m] + ev_slot[m];
                     e->a = kPAbsent;
                     e->b = kPAbsent;
                 }
             __threadfence();
             __syncthreads();
+            mark(5);
+#pragma unroll
             for (int m = 0; m < 2; ++m) {
-                PsQueue Q = s_q[m];
-                if (!Q.area) continue;
-                uint64_t head = Q.head + Q.used, tail = Q.tail;
-                if (tail - head + Q.npush > Q.qcap) {  // lru_compact over [head, tail)
-                    uint64_t w = head;
-                    const MapRef mr = m == 0 ? map_ref_p(st, p) : map_ref_t(st, res, 0);
-                    for (uint64_t b0 = head; b0 < tail; b0 += 64) {
+                if (!area[m]) continue;
+                uint64_t h = head[m] + used[m], t = tail[m];
+                uint32_t npm = npush[m];
+                if (t - h + npm > qcap[m]) {  // lru_compact over [h, t)
+                    uint64_t w = h;
+                    for (uint64_t b0 = h; b0 < t; b0 += 64) {
                         const uint64_t ix = b0 + (uint64_t)lane;
                         LruRec rec{0, 0};
                         bool live = false;
-                        if (ix < tail) {
-                            const LruRec *rp = &Q.area[1 + ix % Q.qcap];
+                        if (ix < t) {
+                            const LruRec *rp = &area[m][1 + ix % qcap[m]];
                             rec = LruRec{ps_ldu(&rp->value), ps_ldu(&rp->stamp)};
-                            PEntry *e = ptab_get(mr.tab, mr.mask, mr.owner, rec.value, false, st.overflow);
-                            live = e && ps_ld(&e->a) != kPAbsent && ps_ldu(&mr.stamp[e - mr.tab]) == rec.stamp;
+                            PEntry *e = ptab_get(tab[m], tmask[m], own[m], rec.value, false, st.overflow);
+                            live = e && ps_ld(&e->a) != kPAbsent && ps_ldu(&tstamp[m][e - tab[m]]) == rec.stamp;
                         }
                         const uint64_t bl = __ballot(live);
                         __syncthreads();  // every lane has read its record before any is overwritten
-                        if (live) Q.area[1 + (w + (uint64_t)__popcll(bl & ((1ull << lane) - 1ull))) % Q.qcap] = rec;
+                        if (live) area[m][1 + (w + (uint64_t)__popcll(bl & ((1ull << lane) - 1ull))) % qcap[m]] = rec;
                         w += (uint64_t)__popcll(bl);
                         __threadfence();
                         __syncthreads();
                     }
-                    tail = w;
-                    if (tail - head + Q.npush > Q.qcap) {
+                    t = w;
+                    if (t - h + npm > qcap[m]) {
                         if (lane == 0) {
                             atomicOr(&st.lru_ctl[1], 2u);
                             atomicOr(st.overflow, 1u);
                         }
-                        Q.npush = 0;
+                        npm = 0;
                     }
                 }
-                for (uint32_t k = (uint32_t)lane; k < Q.npush; k += 64) Q.area[1 + (tail + k) % Q.qcap] = s_push[m][k];
-                __threadfence();
-                __syncthreads();
-                if (lane == 0) {
-                    s_q[m].head = head;
-                    s_q[m].tail = tail + Q.npush;
-                }
+                if (lane < npm) area[m][1 + (t + lane) % qcap[m]] = LruRec{q_pv[m], q_ps[m]};
+                head[m] = h;
+                tail[m] = t + npm;
             }
+            __threadfence();
+            __syncthreads();
+            mark(6);
         }
-        __syncthreads();
         if (lane == 0) {
             if (cur_run != 0xFFFFFFFFu) apply_run(cur_run);
             for (uint32_t r = r0; r < r1; ++r) sc.run_mode[r] = RUN_DONE;
             node[kNodeThreads] += thr;
-            st.psize[p.id] = msize;
-            st.tsize[tj] = tsize;
+            st.psize[p.id] = size[0];
+            st.tsize[tj] = size[1];
             for (int m = 0; m < 2; ++m)
-                if (s_q[m].area) {
-                    s_q[m].area[0].value = s_q[m].head;
-                    s_q[m].area[0].stamp = s_q[m].tail;
+                if (area[m]) {
+                    area[m][0].value = head[m];
+                    area[m][0].stamp = tail[m];
                 }
         }
         __syncthreads();
@@ -4579,8 +4640,13 @@ void FlowEngine::lru_prepare(const uint8_t *kind, const uint32_t *resource, cons
             SGA_HIP_CHECK(hipStreamSynchronize(s));
             fprintf(stderr, "lru_prof pushes %llu compactions %llu scanned %llu compact_ticks %llu evictions %llu popped %llu "
                     "entry_ticks %llu exit_ticks %llu\n", v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+            SGA_HIP_CHECK(hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_lps_prof), sizeof(v), 0, hipMemcpyDeviceToHost, s));
+            SGA_HIP_CHECK(hipStreamSynchronize(s));
+            fprintf(stderr, "lps_prof events %llu chunks %llu ticks: loads %llu leaders %llu records %llu replay %llu "
+                    "writeback %llu compaction %llu\n", v[0], v[7], v[1], v[2], v[3], v[4], v[5], v[6]);
         }
         std::memset(v, 0, sizeof(v));
+        SGA_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lps_prof), v, sizeof(v), 0, hipMemcpyHostToDevice, s));
         const int one = 1;
         SGA_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lru_prof), v, sizeof(v), 0, hipMemcpyHostToDevice, s));
         SGA_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lru_prof_on), &one, sizeof(one), 0, hipMemcpyHostToDevice, s));
