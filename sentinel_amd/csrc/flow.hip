@@ -2924,8 +2924,8 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, uint32_t l) {
     return (uint64_t)rl32((uint32_t)x, l) | ((uint64_t)rl32((uint32_t)(x >> 32), l) << 32);
 }
 // lane l's copy of reg becomes v (v and l wave-uniform)
-__device__ __forceinline__ uint32_t wl32(uint32_t reg, uint32_t v, uint32_t l) { return threadIdx.x == l ? v : reg; }
-__device__ __forceinline__ uint64_t wl64(uint64_t reg, uint64_t v, uint32_t l) { return threadIdx.x == l ? v : reg; }
+__device__ __forceinline__ uint32_t wl32(uint32_t reg, uint32_t v, uint32_t l) { return __lane_id() == l ? v : reg; }
+__device__ __forceinline__ uint64_t wl64(uint64_t reg, uint64_t v, uint32_t l) { return __lane_id() == l ? v : reg; }
 // the entry of (owner, value) if present in the table, its home slot loaded first (the tables stay a quarter
 // full, so most keys sit there); kN lookups of one lane issued together
 template <int kN>
@@ -2974,21 +2974,38 @@ __device__ __forceinline__ int ps_hash_get(const uint32_t *keys, const uint8_t *
     }
 }
 
-__global__ __launch_bounds__(64) void k_llru_ps(FlowState st, int64_t max_rt, FlowScratch sc,
-                                                const Payload *__restrict__ pay, int64_t ts_base,
-                                                const uint64_t *__restrict__ param_in, int8_t *decision,
-                                                int32_t *wait_ms) {
+// wave-local barrier: LDS and global writes of the wave's lanes visible to its other lanes
+__device__ __forceinline__ void ps_wave_sync() {
+    __threadfence();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Two waves per resource, one chunk apart: wave 0 decides chunk c (the time/token map, the decisions, the node
+// statistics) while wave 1 applies chunk c - 1's thread counts (the thread-count map follows the decisions and
+// the exits only), each on its own map, queue and LDS; the chunk's events and decisions pass through a double
+// buffer.  The per-map work (leaders' entries, queue records, the wave-uniform replay, the write-back) is the
+// same for both maps.
+__global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, FlowScratch sc,
+                                                 const Payload *__restrict__ pay, int64_t ts_base,
+                                                 const uint64_t *__restrict__ param_in, int8_t *decision,
+                                                 int32_t *wait_ms) {
     if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
     __shared__ uint32_t s_hk[2][kPsHash];
     __shared__ uint8_t s_hv[2][kPsHash];
     __shared__ uint8_t s_hasent[64];
-    // the loaded queue records (record k of map m at [m][k]) and their keys' state
     __shared__ uint64_t s_pst[2][kPsPre], s_pgs[2][kPsPre];
     __shared__ uint32_t s_pslot[2][kPsPre];
     __shared__ int8_t s_plink[2][kPsPre];
     __shared__ uint8_t s_pgp[2][kPsPre];
-    constexpr int kPre = kPsPre / 64;  // queue records per lane and map
-    const uint32_t lane = threadIdx.x;
+    // chunk handoff (wave 0 -> wave 1): per event flags (bit0 exit, bit1 parameter, bit2 passed), leader,
+    // request index, value
+    __shared__ uint8_t s_bfl[2][64], s_blead[2][64];
+    __shared__ uint32_t s_bidx[2][64];
+    __shared__ uint64_t s_bval[2][64];
+    constexpr int kPre = kPsPre / 64;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const Ctx c{st, max_rt};
     const uint32_t nl = sc.counters[10], nflows = sc.counters[2], nruns = sc.counters[1];
     const bool prof = g_lru_prof_on != 0;
@@ -3000,32 +3017,31 @@ __global__ __launch_bounds__(64) void k_llru_ps(FlowState st, int64_t max_rt, Fl
         const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
         const uint32_t res = sc.run_slot[r0];
         const ParamRuleDev p = st.prules[st.res[res].prule_off];
-        const uint32_t own[2] = {p.id + 1, tmap_owner(res, 0)};
-        PEntry *const tab[2] = {st.ptab, st.ttab};
-        const uint32_t tmask[2] = {st.pmask, st.tmask};
-        uint64_t *const tstamp[2] = {st.pstamp, st.tstamp};
         const uint32_t tj = st.tbase[res];
         const uint32_t jb = sc.run_start[r0], je = sc.run_end[r1 - 1];
         int64_t *node = st.node + (size_t)res * kNodeWords;
-        // the queues (wave-uniform)
-        LruRec *area[2];
-        uint64_t qcap[2], head[2], tail[2];
-        for (int m = 0; m < 2; ++m) {
-            const uint64_t q = m == 0 ? st.pq[p.id] : st.tq[tj];
-            area[m] = q == kNoQueue ? nullptr : st.lpool + q;
-            qcap[m] = 2ull * (m == 0 ? p.cap : (uint32_t)kThreadMapCap) + 2;
-            head[m] = area[m] ? ps_ldu(&area[m][0].value) : 0;
-            tail[m] = area[m] ? ps_ldu(&area[m][0].stamp) : 0;
-        }
-        uint32_t size[2] = {st.psize[p.id], st.tsize[tj]};
-        const uint32_t cap[2] = {p.cap, (uint32_t)kThreadMapCap};
+        // this wave's map: 0 the rule's time/token map, 1 the index-0 thread-count map
+        const int m = (int)wave;
+        const uint32_t own = m == 0 ? p.id + 1 : tmap_owner(res, 0);
+        PEntry *const tab = m == 0 ? st.ptab : st.ttab;
+        const uint32_t tmask = m == 0 ? st.pmask : st.tmask;
+        uint64_t *const tstamp = m == 0 ? st.pstamp : st.tstamp;
+        const uint64_t qo = m == 0 ? st.pq[p.id] : st.tq[tj];
+        LruRec *const area = qo == kNoQueue ? nullptr : st.lpool + qo;
+        const uint64_t qcap = 2ull * (m == 0 ? p.cap : (uint32_t)kThreadMapCap) + 2;
+        uint64_t head = area ? ps_ldu(&area[0].value) : 0, tail = area ? ps_ldu(&area[0].stamp) : 0;
+        uint32_t size = m == 0 ? st.psize[p.id] : st.tsize[tj];
+        const uint32_t cap = m == 0 ? p.cap : (uint32_t)kThreadMapCap;
+        uint32_t *const hk = s_hk[m];
+        uint8_t *const hv = s_hv[m];
         uint32_t cur_run = 0xFFFFFFFFu;
         int64_t pa = 0, ba = 0, np = 0, thr = 0;
-        auto apply_run = [&](uint32_t r) {  // lane 0
+        auto apply_run = [&](uint32_t r) __attribute__((always_inline)) {  // wave 0, lane 0
             const int64_t tf = ts_base + (int64_t)sc.run_t0off[r];
             int64_t *bs[2] = {sec_current(node, tf, max_rt), min_current(node, tf, max_rt)};
             const int64_t exc = (int64_t)sc.run_exc[r], exerr = (int64_t)sc.run_exerr[r];
             const int64_t exrt = sc.run_exrt[r], exmin = sc.run_exmin[r];
+#pragma unroll
             for (int k = 0; k < 2; ++k) {
                 int64_t *b = bs[k];
                 if (!b) continue;
@@ -3042,328 +3058,323 @@ __global__ __launch_bounds__(64) void k_llru_ps(FlowState st, int64_t max_rt, Fl
         auto mark = [&](int ph) __attribute__((always_inline)) {
             if (!prof) return;
             const uint64_t now = wall_clock64();
-            if (lane == 0) atomicAdd(&g_lps_prof[ph], (unsigned long long)(now - tp));
+            if (lane == 0 && wave == 0) atomicAdd(&g_lps_prof[ph], (unsigned long long)(now - tp));
             tp = now;
         };
-        for (uint32_t c0 = jb; c0 < je; c0 += 64) {
-            const uint32_t nk = min(64u, je - c0);
-            if (prof && lane == 0) {
-                atomicAdd(&g_lps_prof[0], (unsigned long long)nk);
-                atomicAdd(&g_lps_prof[7], 1ull);
-            }
-            tp = prof ? wall_clock64() : 0;
-            // 1. this lane's event
-            const bool act = lane < nk;
-            const uint32_t j = c0 + lane;
-            const Payload q = act ? pay[j] : Payload{0, 0, 0, 0};
-            const bool ex = (q.idx & F_EXIT) != 0, hp = act && (q.idx & F_PARAM) != 0;
-            const uint64_t v = hp ? param_in[q.idx & F_IDX] : 0;
-            const uint32_t e_fl = (ex ? 1u : 0u) | (hp ? 2u : 0u);
-            const uint32_t e_idx = q.idx & F_IDX, e_run = act ? sc.ev_run[j] : 0u;
-            const int64_t e_t = ts_base + (int64_t)q.ts_off;
-            const int32_t e_acq = (int32_t)(q.acq_prio & 0x7FFFFFFFu);
-            // 2. distinct values: the lowest lane of each value leads it
-            uint32_t lead = 64;
-            for (int k = 0; k < 64; ++k) {
-                const uint64_t vk = (uint64_t)__shfl((long long)v, k, 64);
-                const bool hk = __shfl((int)hp, k, 64) != 0;
-                if (hp && hk && vk == v && (uint32_t)k < lead) lead = (uint32_t)k;
-            }
-            const uint32_t e_lead = lead;
-            const bool leader = hp && lead == lane;
-            s_hasent[lane] = 0;
-            for (int m = 0; m < 2; ++m)
-                for (uint32_t k = lane; k < (uint32_t)kPsHash; k += 64) s_hk[m][k] = 0xFFFFFFFFu;
-            __syncthreads();
-            if (hp && !ex) s_hasent[lead] = 1;  // the value's time/token entry is needed only by entries
-            __syncthreads();
-            mark(1);
-            // 3. the leaders' entries (created here, as chain_entry's ptab_get would), kept in their lanes
-            uint32_t c_slot[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
-            uint64_t c_val = v, c_st[2] = {0, 0};
-            int64_t c_ma = kPAbsent, c_mb = kPAbsent, c_ta = kPAbsent;
-            uint32_t c_tev = 0;
-            if (leader) {
-                // both home slots first (most keys sit there), the probe loops only past them
-                const uint32_t hm = ptab_home(st.pmask, own[0], v), ht = ptab_home(st.tmask, own[1], v);
-                const uint32_t om = __hip_atomic_load(&st.ptab[hm].owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t ot = __hip_atomic_load(&st.ttab[ht].owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t vm = st.ptab[hm].value, vt = st.ttab[ht].value;
-                PEntry *me = !s_hasent[lane] ? nullptr
-                             : (om == own[0] && vm == v) ? &st.ptab[hm]
-                                                         : ptab_get(st.ptab, st.pmask, own[0], v, true, st.overflow);
-                PEntry *te = (ot == own[1] && vt == v) ? &st.ttab[ht] : ptab_get(st.ttab, st.tmask, own[1], v, true, st.overflow);
-                if (me) {
-                    c_slot[0] = (uint32_t)(me - st.ptab);
-                    c_ma = ps_ld(&me->a);
-                    c_mb = ps_ld(&me->b);
-                    c_st[0] = ps_ldu(&st.pstamp[c_slot[0]]);
-                    ps_hash_put(s_hk[0], s_hv[0], c_slot[0], lane);
+        const uint32_t nch = (je - jb + 63) / 64;
+        for (uint32_t step = 0; step <= nch; ++step) {
+            // wave 0: chunk `step`; wave 1: chunk step - 1
+            const bool work = wave == 0 ? step < nch : step >= 1;
+            const uint32_t ch = wave == 0 ? step : step - 1, bsel = ch & 1;
+            if (work) {
+                const uint32_t c0 = jb + ch * 64, nk = min(64u, je - c0);
+                if (prof && lane == 0 && wave == 0) {
+                    atomicAdd(&g_lps_prof[0], (unsigned long long)nk);
+                    atomicAdd(&g_lps_prof[7], 1ull);
                 }
-                if (te) {
-                    c_slot[1] = (uint32_t)(te - st.ttab);
-                    c_ta = ps_ld(&te->a);
-                    c_st[1] = ps_ldu(&st.tstamp[c_slot[1]]);
-                    ps_hash_put(s_hk[1], s_hv[1], c_slot[1], lane);
+                tp = prof ? wall_clock64() : 0;
+                // 1. the chunk's events (lane k: event k); wave 0 loads them and hands them over
+                const bool act = lane < nk;
+                uint32_t e_fl, e_lead, e_idx;
+                uint64_t v;
+                uint32_t e_run = 0;
+                int64_t e_t = 0;
+                int32_t e_acq = 0;
+                if (wave == 0) {
+                    const uint32_t j = c0 + lane;
+                    const Payload q = act ? pay[j] : Payload{0, 0, 0, 0};
+                    const bool ex = (q.idx & F_EXIT) != 0, hp = act && (q.idx & F_PARAM) != 0;
+                    v = hp ? param_in[q.idx & F_IDX] : 0;
+                    e_fl = (ex ? 1u : 0u) | (hp ? 2u : 0u);
+                    e_idx = q.idx & F_IDX;
+                    e_run = act ? sc.ev_run[j] : 0u;
+                    e_t = ts_base + (int64_t)q.ts_off;
+                    e_acq = (int32_t)(q.acq_prio & 0x7FFFFFFFu);
+                    uint32_t lead = 64;
+                    for (int k = 0; k < 64; ++k) {  // distinct values: the lowest lane of each value leads it
+                        const uint64_t vk = (uint64_t)__shfl((long long)v, k, 64);
+                        const bool hk2 = __shfl((int)hp, k, 64) != 0;
+                        if (hp && hk2 && vk == v && (uint32_t)k < lead) lead = (uint32_t)k;
+                    }
+                    e_lead = lead;
+                    s_hasent[lane] = 0;
+                    ps_wave_sync();
+                    if (hp && !ex) s_hasent[lead] = 1;  // the value's time/token entry is needed only by entries
+                    s_bfl[bsel][lane] = (uint8_t)e_fl;
+                    s_blead[bsel][lane] = (uint8_t)e_lead;
+                    s_bidx[bsel][lane] = e_idx;
+                    s_bval[bsel][lane] = v;
+                } else {
+                    e_fl = s_bfl[bsel][lane];
+                    e_lead = s_blead[bsel][lane];
+                    e_idx = s_bidx[bsel][lane];
+                    v = s_bval[bsel][lane];
                 }
-            }
-            __syncthreads();
-            mark(2);
-            // 4. the next kPsPre records of each queue (record k in lane k % 64, register k / 64) with their
-            //    keys' state, and which of them are the chunk's keys
-            uint32_t npre[2];
+                for (uint32_t k = lane; k < (uint32_t)kPsHash; k += 64) hk[k] = 0xFFFFFFFFu;
+                ps_wave_sync();
+                const bool hp = (e_fl & 2u) != 0;
+                const bool leader = hp && e_lead == lane;
+                mark(1);
+                // 2. the leaders' entries of this wave's map (created, as chain_entry's ptab_get would), kept in
+                //    their lanes
+                uint32_t c_slot = 0xFFFFFFFFu;
+                uint64_t c_st = 0;
+                int64_t c_a = kPAbsent, c_b = kPAbsent;
+                uint32_t c_ev = 0;
+                const bool need = leader && (m == 1 || s_hasent[lane]);
+                if (need) {
+                    const uint32_t h = ptab_home(tmask, own, v);
+                    const uint32_t oh = __hip_atomic_load(&tab[h].owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    PEntry *e = (oh == own && tab[h].value == v) ? &tab[h] : ptab_get(tab, tmask, own, v, true, st.overflow);
+                    if (e) {
+                        c_slot = (uint32_t)(e - tab);
+                        c_a = ps_ld(&e->a);
+                        c_b = ps_ld(&e->b);
+                        c_st = ps_ldu(&tstamp[c_slot]);
+                        ps_hash_put(hk, hv, c_slot, lane);
+                    }
+                }
+                const bool any = __ballot(need) != 0ull;  // this map is touched in the chunk
+                ps_wave_sync();
+                mark(2);
+                // 3. the next kPsPre records of the queue with their keys' state, and which are the chunk's keys
+                const uint32_t npre = (area && any) ? (uint32_t)min<uint64_t>(kPsPre, tail - head) : 0u;
+                {
+                    uint64_t rv[kPre], rs[kPre];
+                    bool want[kPre];
 #pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                npre[m] = area[m] ? (uint32_t)min<uint64_t>(kPsPre, tail[m] - head[m]) : 0u;
-                uint64_t rv[kPre];
-                bool want[kPre];
-                uint64_t rs[kPre];
+                    for (int r = 0; r < kPre; ++r) {
+                        const uint32_t k = (uint32_t)r * 64 + lane;
+                        want[r] = k < npre;
+                        const LruRec *rp = want[r] ? &area[1 + (head + k) % qcap] : nullptr;
+                        rv[r] = want[r] ? ps_ldu(&rp->value) : 0ull;
+                        rs[r] = want[r] ? ps_ldu(&rp->stamp) : 0ull;
+                    }
+                    PEntry *e[kPre];
+                    ptab_find_n<kPre>(tab, tmask, own, rv, want, e, st.overflow);
 #pragma unroll
-                for (int r = 0; r < kPre; ++r) {
-                    const uint32_t k = (uint32_t)r * 64 + lane;
-                    want[r] = k < npre[m];
-                    const LruRec *rp = want[r] ? &area[m][1 + (head[m] + k) % qcap[m]] : nullptr;
-                    rv[r] = want[r] ? ps_ldu(&rp->value) : 0ull;
-                    rs[r] = want[r] ? ps_ldu(&rp->stamp) : 0ull;
+                    for (int r = 0; r < kPre; ++r) {
+                        if (!want[r]) continue;
+                        const uint32_t k = (uint32_t)r * 64 + lane;
+                        const uint32_t slot = e[r] ? (uint32_t)(e[r] - tab) : 0xFFFFFFFFu;
+                        s_pst[m][k] = rs[r];
+                        s_pslot[m][k] = slot;
+                        s_pgp[m][k] = e[r] && ps_ld(&e[r]->a) != kPAbsent ? 1 : 0;
+                        s_pgs[m][k] = e[r] ? ps_ldu(&tstamp[slot]) : 0ull;
+                        s_plink[m][k] = (int8_t)(e[r] ? ps_hash_get(hk, hv, slot) : -1);
+                    }
                 }
-                PEntry *e[kPre];
-                ptab_find_n<kPre>(tab[m], tmask[m], own[m], rv, want, e, st.overflow);
-#pragma unroll
-                for (int r = 0; r < kPre; ++r) {
-                    if (!want[r]) continue;
-                    const uint32_t k = (uint32_t)r * 64 + lane;
-                    const uint32_t slot = e[r] ? (uint32_t)(e[r] - tab[m]) : 0xFFFFFFFFu;
-                    s_pst[m][k] = rs[r];
-                    s_pslot[m][k] = slot;
-                    s_pgp[m][k] = e[r] && ps_ld(&e[r]->a) != kPAbsent ? 1 : 0;
-                    s_pgs[m][k] = e[r] ? ps_ldu(&tstamp[m][slot]) : 0ull;
-                    s_plink[m][k] = (int8_t)(e[r] ? ps_hash_get(s_hk[m], s_hv[m], slot) : -1);
-                }
-            }
-            __syncthreads();
-            mark(3);
-            // 5. the chunk in arrival order, wave-uniform: every lane takes the same steps on values read
-            //    out of the owning lanes (k_llru's chain_entry / chain_exit for this resource)
-            uint64_t used[2] = {0, 0};
-            uint32_t npush[2] = {0, 0}, nev[2] = {0, 0};
-            uint64_t q_pv[2] = {0, 0}, q_ps[2] = {0, 0};
-            uint32_t ev_slot[2] = {0, 0};
-            int32_t r_d = 0, r_w = 0;
-            auto evict = [&](auto mc) __attribute__((always_inline)) {  // mc: std::integral_constant<int, map>
-                constexpr int m = decltype(mc)::value;
-                for (;;) {
-                    uint64_t rs, gs;
-                    uint32_t slot, gp;
-                    int link;
-                    if (used[m] < npre[m]) {
-                        const uint32_t k = (uint32_t)used[m];
-                        rs = s_pst[m][k];
-                        gs = s_pgs[m][k];
-                        slot = s_pslot[m][k];
-                        gp = s_pgp[m][k];
-                        link = s_plink[m][k];
-                    } else if (head[m] + used[m] < tail[m]) {  // past the loaded records: one global pop
-                        const LruRec *rp = &area[m][1 + (head[m] + used[m]) % qcap[m]];
-                        const uint64_t rv = ps_ldu(&rp->value);
-                        rs = ps_ldu(&rp->stamp);
-                        PEntry *e = ptab_get(tab[m], tmask[m], own[m], rv, false, st.overflow);
-                        slot = e ? (uint32_t)(e - tab[m]) : 0xFFFFFFFFu;
-                        gp = e && ps_ld(&e->a) != kPAbsent ? 1u : 0u;
-                        gs = e ? ps_ldu(&tstamp[m][slot]) : 0ull;
-                        const uint64_t hit = __ballot(c_slot[m] == slot && slot != 0xFFFFFFFFu);
-                        link = hit ? __builtin_ctzll(hit) : -1;
-                    } else {
-                        if (lane == 0) {
-                            atomicOr(&st.lru_ctl[1], 2u);  // a full map without a live record: never expected
-                            atomicOr(st.overflow, 1u);
+                ps_wave_sync();
+                mark(3);
+                // 4. the chunk in arrival order, wave-uniform: every lane takes the same steps on values read out
+                //    of the owning lanes (k_llru's chain_entry / chain_exit, this wave's map)
+                uint64_t used = 0;
+                uint32_t npush = 0, nev = 0;
+                uint64_t q_pv = 0, q_ps = 0;
+                uint32_t ev_slot = 0;
+                int32_t r_d = 0, r_w = 0;
+                uint32_t r_pass = 0;
+                auto evict = [&]() __attribute__((always_inline)) {
+                    for (;;) {
+                        uint64_t rs, gs;
+                        uint32_t slot, gp;
+                        int link;
+                        if (used < npre) {
+                            const uint32_t k = (uint32_t)used;
+                            rs = s_pst[m][k];
+                            gs = s_pgs[m][k];
+                            slot = s_pslot[m][k];
+                            gp = s_pgp[m][k];
+                            link = s_plink[m][k];
+                        } else if (head + used < tail) {  // past the loaded records: one global pop
+                            const LruRec *rp = &area[1 + (head + used) % qcap];
+                            const uint64_t rv = ps_ldu(&rp->value);
+                            rs = ps_ldu(&rp->stamp);
+                            PEntry *e = ptab_get(tab, tmask, own, rv, false, st.overflow);
+                            slot = e ? (uint32_t)(e - tab) : 0xFFFFFFFFu;
+                            gp = e && ps_ld(&e->a) != kPAbsent ? 1u : 0u;
+                            gs = e ? ps_ldu(&tstamp[slot]) : 0ull;
+                            const uint64_t hit = __ballot(c_slot == slot && slot != 0xFFFFFFFFu);
+                            link = hit ? __builtin_ctzll(hit) : -1;
+                        } else {
+                            if (lane == 0) {
+                                atomicOr(&st.lru_ctl[1], 2u);  // a full map without a live record: never expected
+                                atomicOr(st.overflow, 1u);
+                            }
+                            return;
                         }
+                        used += 1;
+                        if (link >= 0) {
+                            const uint32_t L = (uint32_t)link;
+                            if ((int64_t)rl64((uint64_t)c_a, L) == kPAbsent || rl64(c_st, L) != rs) continue;
+                            c_a = (int64_t)wl64((uint64_t)c_a, (uint64_t)kPAbsent, L);
+                            c_b = (int64_t)wl64((uint64_t)c_b, (uint64_t)kPAbsent, L);
+                            c_ev = wl32(c_ev, 1u, L);
+                            size -= 1;
+                            return;
+                        }
+                        if (slot == 0xFFFFFFFFu || !gp || gs != rs) continue;
+                        ev_slot = wl32(ev_slot, slot, nev);
+                        nev += 1;
+                        size -= 1;
                         return;
                     }
-                    used[m] += 1;
-                    if (link >= 0) {
-                        const uint32_t L = (uint32_t)link;
-                        const bool live = m == 0 ? ((int64_t)rl64((uint64_t)c_ma, L) != kPAbsent && rl64(c_st[0], L) == rs)
-                                                 : ((int64_t)rl64((uint64_t)c_ta, L) != kPAbsent && rl64(c_st[1], L) == rs);
-                        if (!live) continue;
-                        if (m == 0) {
-                            c_ma = (int64_t)wl64((uint64_t)c_ma, (uint64_t)kPAbsent, L);
-                            c_mb = (int64_t)wl64((uint64_t)c_mb, (uint64_t)kPAbsent, L);
-                        } else {
-                            c_ta = (int64_t)wl64((uint64_t)c_ta, (uint64_t)kPAbsent, L);
-                            c_tev = wl32(c_tev, 1u, L);
+                };
+                auto push = [&](uint64_t val, uint64_t stamp) __attribute__((always_inline)) {
+                    q_pv = wl64(q_pv, val, npush);
+                    q_ps = wl64(q_ps, stamp, npush);
+                    npush += 1;
+                };
+                for (uint32_t k = 0; k < nk; ++k) {
+                    const uint32_t fl2 = rl32(e_fl, k);
+                    const uint32_t L = rl32(e_lead, k);
+                    const uint64_t stamp = lru_stamp(st, rl32(e_idx, k), 0);
+                    if (m == 0) {  // the time/token map, the decision, the node statistics
+                        const uint32_t r = rl32(e_run, k);
+                        if (r != cur_run) {
+                            if (cur_run != 0xFFFFFFFFu && lane == 0) apply_run(cur_run);
+                            cur_run = r;
+                            pa = ba = np = 0;
                         }
-                        size[m] -= 1;
-                        return;
-                    }
-                    if (slot == 0xFFFFFFFFu || !gp || gs != rs) continue;
-                    ev_slot[m] = wl32(ev_slot[m], slot, nev[m]);
-                    nev[m] += 1;
-                    size[m] -= 1;
-                    return;
-                }
-            };
-            auto push = [&](auto mc, uint64_t val, uint64_t stamp) __attribute__((always_inline)) {
-                constexpr int m = decltype(mc)::value;
-                q_pv[m] = wl64(q_pv[m], val, npush[m]);
-                q_ps[m] = wl64(q_ps[m], stamp, npush[m]);
-                npush[m] += 1;
-            };
-            for (uint32_t k = 0; k < nk; ++k) {
-                const uint32_t fl = rl32(e_fl, k);
-                const uint32_t L = rl32(e_lead, k);
-                const uint64_t stamp = lru_stamp(st, rl32(e_idx, k), 0);
-                const uint32_t r = rl32(e_run, k);
-                if (r != cur_run) {
-                    if (cur_run != 0xFFFFFFFFu && lane == 0) apply_run(cur_run);
-                    cur_run = r;
-                    pa = ba = np = 0;
-                }
-                const int acq = (int)rl32((uint32_t)e_acq, k);
-                int d = D_PASS;
-                int64_t w = 0;
-                int tdelta = 0;
-                if (!(fl & 1)) {  // entry
-                    if (fl & 2) {
-                        const uint64_t val = rl64(c_val, L);
-                        if (rl32(c_slot[0], L) == 0xFFFFFFFFu) {  // the map is full: the batch fails (overflow)
-                            d = D_BLOCK_PARAM;
-                        } else {
-                            const int64_t t = (int64_t)rl64((uint64_t)e_t, k);
-                            if (param_map_access(c, p, val, acq)) {  // time map then token map, one recency order
-                                const bool absent = (int64_t)rl64((uint64_t)c_ma, L) == kPAbsent;
-                                c_st[0] = wl64(c_st[0], stamp, L);
-                                if (absent) size[0] += 1;
-                                if (area[0]) {
-                                    push(std::integral_constant<int, 0>{}, val, stamp);
-                                    if (absent && size[0] > cap[0]) evict(std::integral_constant<int, 0>{});
+                        if (fl2 & 1u) continue;  // an exit: wave 1's thread count only
+                        const int acq = (int)rl32((uint32_t)e_acq, k);
+                        int d = D_PASS;
+                        int64_t w = 0;
+                        if (fl2 & 2u) {
+                            const uint64_t val = rl64(v, L);
+                            if (rl32(c_slot, L) == 0xFFFFFFFFu) {  // the map is full: the batch fails (overflow)
+                                d = D_BLOCK_PARAM;
+                            } else {
+                                const int64_t t = (int64_t)rl64((uint64_t)e_t, k);
+                                if (param_map_access(c, p, val, acq)) {  // time map then token map, one recency order
+                                    const bool absent = (int64_t)rl64((uint64_t)c_a, L) == kPAbsent;
+                                    c_st = wl64(c_st, stamp, L);
+                                    if (absent) size += 1;
+                                    if (area) {
+                                        push(val, stamp);
+                                        if (absent && size > cap) evict();
+                                    }
+                                }
+                                struct { int64_t a, b; } e{(int64_t)rl64((uint64_t)c_a, L), (int64_t)rl64((uint64_t)c_b, L)};
+                                const bool pass = param_pass_qps(c, p, e, val, acq, t, &w);
+                                c_a = (int64_t)wl64((uint64_t)c_a, (uint64_t)e.a, L);
+                                c_b = (int64_t)wl64((uint64_t)c_b, (uint64_t)e.b, L);
+                                if (!pass) {
+                                    d = D_BLOCK_PARAM;
+                                    w = 0;  // a block's detail: the rule's index
                                 }
                             }
-                            struct { int64_t a, b; } e{(int64_t)rl64((uint64_t)c_ma, L), (int64_t)rl64((uint64_t)c_mb, L)};
-                            const bool pass = param_pass_qps(c, p, e, val, acq, t, &w);
-                            c_ma = (int64_t)wl64((uint64_t)c_ma, (uint64_t)e.a, L);
-                            c_mb = (int64_t)wl64((uint64_t)c_mb, (uint64_t)e.b, L);
-                            if (!pass) {
-                                d = D_BLOCK_PARAM;
-                                w = 0;  // a block's detail: the rule's index
+                        }
+                        if (d == D_PASS) {
+                            pa += acq;
+                            np += 1;
+                            r_pass = wl32(r_pass, 1u, k);
+                        } else {
+                            ba += acq;
+                        }
+                        r_d = (int32_t)wl32((uint32_t)r_d, (uint32_t)d, k);
+                        r_w = (int32_t)wl32((uint32_t)r_w, (uint32_t)(int32_t)w, k);
+                    } else {  // ParameterMetric.add / decreaseThreadCount of index 0 (param_threads)
+                        if (!(fl2 & 2u)) continue;
+                        const int tdelta = (fl2 & 1u) ? -1 : ((fl2 & 4u) ? 1 : 0);
+                        if (!tdelta || rl32(c_slot, L) == 0xFFFFFFFFu) continue;
+                        const uint64_t val = rl64(v, L);
+                        const int64_t ta = (int64_t)rl64((uint64_t)c_a, L);
+                        c_st = wl64(c_st, stamp, L);
+                        int64_t nt;
+                        if (ta == kPAbsent) {
+                            size += 1;
+                            if (area) {
+                                push(val, stamp);
+                                if (size > cap) evict();
+                            }
+                            nt = tdelta > 0 ? 1 : 0;
+                        } else {
+                            if (area) push(val, stamp);
+                            nt = ta + (tdelta > 0 ? 1 : -1);
+                            if (tdelta < 0 && nt <= 0) {
+                                nt = kPAbsent;
+                                size -= 1;
                             }
                         }
+                        c_a = (int64_t)wl64((uint64_t)c_a, (uint64_t)nt, L);
                     }
-                    if (d == D_PASS) {
-                        pa += acq;
-                        np += 1;
-                        tdelta = (fl & 2) ? 1 : 0;
-                    } else {
-                        ba += acq;
-                    }
-                    r_d = (int32_t)wl32((uint32_t)r_d, (uint32_t)d, k);
-                    r_w = (int32_t)wl32((uint32_t)r_w, (uint32_t)(int32_t)w, k);
-                } else if (fl & 2) {
-                    tdelta = -1;
                 }
-                if (tdelta && rl32(c_slot[1], L) != 0xFFFFFFFFu) {  // ParameterMetric.add / decreaseThreadCount
-                    const uint64_t val = rl64(c_val, L);
-                    const int64_t ta = (int64_t)rl64((uint64_t)c_ta, L);
-                    c_st[1] = wl64(c_st[1], stamp, L);
-                    int64_t nt;
-                    if (ta == kPAbsent) {
-                        size[1] += 1;
-                        if (area[1]) {
-                            push(std::integral_constant<int, 1>{}, val, stamp);
-                            if (size[1] > cap[1]) evict(std::integral_constant<int, 1>{});
+                mark(4);
+                // 5. write back: the decisions and the passes (wave 0), the copies, the evictions, then the queue's
+                //    pushes (after a compaction when the ring would overflow: live records kept in order)
+                if (m == 0) {
+                    const bool ent = act && !(e_fl & 1u);
+                    if (ent) {
+                        decision[e_idx] = (int8_t)r_d;
+                        wait_ms[e_idx] = r_w;
+                    }
+                    s_bfl[bsel][lane] = (uint8_t)(e_fl | (r_pass ? 4u : 0u));
+                }
+                if (c_slot != 0xFFFFFFFFu) {
+                    tab[c_slot].a = c_a;
+                    if (m == 0) tab[c_slot].b = c_b;
+                    else if (c_ev) tab[c_slot].b = kPAbsent;
+                    tstamp[c_slot] = c_st;
+                }
+                if (lane < nev) {
+                    tab[ev_slot].a = kPAbsent;
+                    tab[ev_slot].b = kPAbsent;
+                }
+                ps_wave_sync();
+                mark(5);
+                if (area) {
+                    uint64_t h = head + used, t = tail;
+                    uint32_t npm = npush;
+                    if (t - h + npm > qcap) {  // lru_compact over [h, t)
+                        uint64_t w = h;
+                        for (uint64_t b0 = h; b0 < t; b0 += 64) {
+                            const uint64_t ix = b0 + (uint64_t)lane;
+                            LruRec rec{0, 0};
+                            bool live = false;
+                            if (ix < t) {
+                                const LruRec *rp = &area[1 + ix % qcap];
+                                rec = LruRec{ps_ldu(&rp->value), ps_ldu(&rp->stamp)};
+                                PEntry *e = ptab_get(tab, tmask, own, rec.value, false, st.overflow);
+                                live = e && ps_ld(&e->a) != kPAbsent && ps_ldu(&tstamp[e - tab]) == rec.stamp;
+                            }
+                            const uint64_t bl = __ballot(live);
+                            ps_wave_sync();  // every lane has read its record before any is overwritten
+                            if (live) area[1 + (w + (uint64_t)__popcll(bl & ((1ull << lane) - 1ull))) % qcap] = rec;
+                            w += (uint64_t)__popcll(bl);
+                            ps_wave_sync();
                         }
-                        nt = tdelta > 0 ? 1 : 0;
-                    } else {
-                        if (area[1]) push(std::integral_constant<int, 1>{}, val, stamp);
-                        nt = ta + (tdelta > 0 ? 1 : -1);
-                        if (tdelta < 0 && nt <= 0) {
-                            nt = kPAbsent;
-                            size[1] -= 1;
+                        t = w;
+                        if (t - h + npm > qcap) {
+                            if (lane == 0) {
+                                atomicOr(&st.lru_ctl[1], 2u);
+                                atomicOr(st.overflow, 1u);
+                            }
+                            npm = 0;
                         }
                     }
-                    c_ta = (int64_t)wl64((uint64_t)c_ta, (uint64_t)nt, L);
+                    if (lane < npm) area[1 + (t + lane) % qcap] = LruRec{q_pv, q_ps};
+                    head = h;
+                    tail = t + npm;
                 }
+                ps_wave_sync();
+                mark(6);
             }
-            mark(4);
-            // 6. write back: decisions, the copies, the evictions, then each queue's pushes (after a compaction
-            //    when the ring would overflow: live records kept in order, the wave 64 at a time)
-            if (act && !ex) {
-                decision[e_idx] = (int8_t)r_d;
-                wait_ms[e_idx] = r_w;
-            }
-            if (leader) {
-                if (c_slot[0] != 0xFFFFFFFFu) {
-                    st.ptab[c_slot[0]].a = c_ma;
-                    st.ptab[c_slot[0]].b = c_mb;
-                    st.pstamp[c_slot[0]] = c_st[0];
-                }
-                if (c_slot[1] != 0xFFFFFFFFu) {
-                    st.ttab[c_slot[1]].a = c_ta;
-                    if (c_tev) st.ttab[c_slot[1]].b = kPAbsent;
-                    st.tstamp[c_slot[1]] = c_st[1];
-                }
-            }
-#pragma unroll
-            for (int m = 0; m < 2; ++m)
-                if (lane < nev[m]) {
-                    PEntry *e = tab[m] + ev_slot[m];
-                    e->a = kPAbsent;
-                    e->b = kPAbsent;
-                }
-            __threadfence();
-            __syncthreads();
-            mark(5);
-#pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                if (!area[m]) continue;
-                uint64_t h = head[m] + used[m], t = tail[m];
-                uint32_t npm = npush[m];
-                if (t - h + npm > qcap[m]) {  // lru_compact over [h, t)
-                    uint64_t w = h;
-                    for (uint64_t b0 = h; b0 < t; b0 += 64) {
-                        const uint64_t ix = b0 + (uint64_t)lane;
-                        LruRec rec{0, 0};
-                        bool live = false;
-                        if (ix < t) {
-                            const LruRec *rp = &area[m][1 + ix % qcap[m]];
-                            rec = LruRec{ps_ldu(&rp->value), ps_ldu(&rp->stamp)};
-                            PEntry *e = ptab_get(tab[m], tmask[m], own[m], rec.value, false, st.overflow);
-                            live = e && ps_ld(&e->a) != kPAbsent && ps_ldu(&tstamp[m][e - tab[m]]) == rec.stamp;
-                        }
-                        const uint64_t bl = __ballot(live);
-                        __syncthreads();  // every lane has read its record before any is overwritten
-                        if (live) area[m][1 + (w + (uint64_t)__popcll(bl & ((1ull << lane) - 1ull))) % qcap[m]] = rec;
-                        w += (uint64_t)__popcll(bl);
-                        __threadfence();
-                        __syncthreads();
-                    }
-                    t = w;
-                    if (t - h + npm > qcap[m]) {
-                        if (lane == 0) {
-                            atomicOr(&st.lru_ctl[1], 2u);
-                            atomicOr(st.overflow, 1u);
-                        }
-                        npm = 0;
-                    }
-                }
-                if (lane < npm) area[m][1 + (t + lane) % qcap[m]] = LruRec{q_pv[m], q_ps[m]};
-                head[m] = h;
-                tail[m] = t + npm;
-            }
-            __threadfence();
-            __syncthreads();
-            mark(6);
+            __syncthreads();  // wave 0's chunk handed over, wave 1's buffer free
         }
         if (lane == 0) {
-            if (cur_run != 0xFFFFFFFFu) apply_run(cur_run);
-            for (uint32_t r = r0; r < r1; ++r) sc.run_mode[r] = RUN_DONE;
-            node[kNodeThreads] += thr;
-            st.psize[p.id] = size[0];
-            st.tsize[tj] = size[1];
-            for (int m = 0; m < 2; ++m)
-                if (area[m]) {
-                    area[m][0].value = head[m];
-                    area[m][0].stamp = tail[m];
-                }
+            if (wave == 0) {
+                if (cur_run != 0xFFFFFFFFu) apply_run(cur_run);
+                for (uint32_t r = r0; r < r1; ++r) sc.run_mode[r] = RUN_DONE;
+                node[kNodeThreads] += thr;
+                st.psize[p.id] = size;
+            } else {
+                st.tsize[tj] = size;
+            }
+            if (area) {
+                area[0].value = head;
+                area[0].stamp = tail;
+            }
         }
         __syncthreads();
     }
@@ -5457,7 +5468,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         if (st.lru_res) {
             hipLaunchKernelGGL(k_llru, dim3(64), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo,
                                d_rt.p, d_param.p, d_dec.p, d_wait.p);
-            hipLaunchKernelGGL(k_llru_ps, dim3(256), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo,
+            hipLaunchKernelGGL(k_llru_ps, dim3(256), dim3(128), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo,
                                d_param.p, d_dec.p, d_wait.p);
         }
         hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
@@ -5581,7 +5592,7 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
     if (st.lru_res) {
         hipLaunchKernelGGL(k_llru, dim3(64), dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p,
                            param_p, d_decision, wait_p);
-        hipLaunchKernelGGL(k_llru_ps, dim3(256), dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base,
+        hipLaunchKernelGGL(k_llru_ps, dim3(256), dim3(128), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base,
                            param_p, d_decision, wait_p);
     }
     hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
