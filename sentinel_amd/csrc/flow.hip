@@ -2915,7 +2915,7 @@ __global__ __launch_bounds__(64) void k_llru(FlowState st, int64_t max_rt, FlowS
 // node statistics go in aggregate, run by run.  k_lflows flags these flows in sc.lru (kLruPs).
 // SGA_LRU_PROF=1 (diagnostics only): k_llru_ps ticks per phase, summed over chunks: [0] events [1] loads +
 // dedupe [2] leader entries [3] queue records [4] replay [5] write-back [6] compaction [7] chunks
-__device__ unsigned long long g_lps_prof[8];
+__device__ unsigned long long g_lps_prof[16];
 
 __device__ __forceinline__ uint32_t rl32(uint32_t x, uint32_t l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
@@ -2974,38 +2974,57 @@ __device__ __forceinline__ int ps_hash_get(const uint32_t *keys, const uint8_t *
     }
 }
 
-// wave-local barrier: LDS and global writes of the wave's lanes visible to its other lanes
+// wave-local barrier: the wave's LDS and global writes visible to its other lanes (the workgroup shares
+// the CU's L1, so workgroup scope is enough: no other workgroup reads an owner's keys or queue)
 __device__ __forceinline__ void ps_wave_sync() {
-    __threadfence();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ int64_t ps_wave_sum(int64_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += (int64_t)__shfl_xor((long long)x, o, 64);
+    return x;
+}
+__device__ __forceinline__ uint32_t ps_wave_max(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+    return x;
 }
 
 // Two waves per resource, one chunk apart: wave 0 decides chunk c (the time/token map, the decisions, the node
 // statistics) while wave 1 applies chunk c - 1's thread counts (the thread-count map follows the decisions and
 // the exits only), each on its own map, queue and LDS; the chunk's events and decisions pass through a double
-// buffer.  The per-map work (leaders' entries, queue records, the wave-uniform replay, the write-back) is the
-// same for both maps.
+// buffer.  Per chunk and map:
+//  * the leaders' entries (one lane per distinct value) and the next kPsPre queue records with their keys'
+//    state go to registers; a record is a candidate for eviction when its key is outside the chunk and live
+//    (bit masks `live`), or is a chunk key whose pre-chunk stamp it carries (`link`: live while the key is
+//    present and not yet accessed in the chunk);
+//  * the LRU scan walks the chunk's accesses in arrival order on wave-uniform bit masks (present, accessed,
+//    inserted-absent, evicted): an insert into a full map pops the first candidate (k_llru's lru_evict);
+//  * wave 0 then runs the token-bucket / throttle checks lane-parallel in rounds (round r: each value's r-th
+//    event, its state in LDS, reset where the scan saw the value absent), wave 1 kept the thread counts in the
+//    scan (a count reaching zero removes the key);
+//  * the queue's pushes are the accesses in arrival order (one per accessing lane), the copies, the evictions
+//    and the last access stamps go back, and the node statistics go in aggregate, run by run.
 __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, FlowScratch sc,
                                                  const Payload *__restrict__ pay, int64_t ts_base,
                                                  const uint64_t *__restrict__ param_in, int8_t *decision,
                                                  int32_t *wait_ms) {
     if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    static_assert(kPsPre == 128, "two loaded queue records per lane");
     __shared__ uint32_t s_hk[2][kPsHash];
     __shared__ uint8_t s_hv[2][kPsHash];
     __shared__ uint8_t s_hasent[64];
-    __shared__ uint64_t s_pst[2][kPsPre], s_pgs[2][kPsPre];
-    __shared__ uint32_t s_pslot[2][kPsPre];
-    __shared__ int8_t s_plink[2][kPsPre];
-    __shared__ uint8_t s_pgp[2][kPsPre];
+    __shared__ uint32_t s_last[2][64];  // per leader lane: 1 + the lane of its value's last access in the chunk
+    __shared__ int64_t s_ra[64], s_rb[64];  // wave 0's rounds: each value's (a, b) at its leader's index
     // chunk handoff (wave 0 -> wave 1): per event flags (bit0 exit, bit1 parameter, bit2 passed), leader,
     // request index, value
     __shared__ uint8_t s_bfl[2][64], s_blead[2][64];
     __shared__ uint32_t s_bidx[2][64];
     __shared__ uint64_t s_bval[2][64];
-    constexpr int kPre = kPsPre / 64;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
     const Ctx c{st, max_rt};
     const uint32_t nl = sc.counters[10], nflows = sc.counters[2], nruns = sc.counters[1];
     const bool prof = g_lru_prof_on != 0;
@@ -3062,6 +3081,8 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
             tp = now;
         };
         const uint32_t nch = (je - jb + 63) / 64;
+        uint64_t n_pop = 0, n_gpop = 0, n_evict = 0, n_acc = 0;  // diagnostics (SGA_LRU_PROF)
+        const uint64_t t_res = prof ? wall_clock64() : 0;
         for (uint32_t step = 0; step <= nch; ++step) {
             // wave 0: chunk `step`; wave 1: chunk step - 1
             const bool work = wave == 0 ? step < nch : step >= 1;
@@ -3075,7 +3096,7 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                 tp = prof ? wall_clock64() : 0;
                 // 1. the chunk's events (lane k: event k); wave 0 loads them and hands them over
                 const bool act = lane < nk;
-                uint32_t e_fl, e_lead, e_idx;
+                uint32_t e_fl, e_lead, e_idx, e_occ = 0;
                 uint64_t v;
                 uint32_t e_run = 0;
                 int64_t e_t = 0;
@@ -3090,11 +3111,16 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                     e_run = act ? sc.ev_run[j] : 0u;
                     e_t = ts_base + (int64_t)q.ts_off;
                     e_acq = (int32_t)(q.acq_prio & 0x7FFFFFFFu);
+                    // distinct values: the lowest lane of each value leads it; e_occ = the event's rank among
+                    // its value's events in the chunk
                     uint32_t lead = 64;
-                    for (int k = 0; k < 64; ++k) {  // distinct values: the lowest lane of each value leads it
+                    for (int k = 0; k < 64; ++k) {
                         const uint64_t vk = (uint64_t)__shfl((long long)v, k, 64);
                         const bool hk2 = __shfl((int)hp, k, 64) != 0;
-                        if (hp && hk2 && vk == v && (uint32_t)k < lead) lead = (uint32_t)k;
+                        if (hp && hk2 && vk == v) {
+                            lead = min(lead, (uint32_t)k);
+                            e_occ += (uint32_t)k < lane ? 1u : 0u;
+                        }
                     }
                     e_lead = lead;
                     s_hasent[lane] = 0;
@@ -3111,16 +3137,17 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                     v = s_bval[bsel][lane];
                 }
                 for (uint32_t k = lane; k < (uint32_t)kPsHash; k += 64) hk[k] = 0xFFFFFFFFu;
+                s_last[m][lane] = 0;
                 ps_wave_sync();
                 const bool hp = (e_fl & 2u) != 0;
                 const bool leader = hp && e_lead == lane;
+                const uint64_t my_stamp = lru_stamp(st, e_idx, 0);
                 mark(1);
                 // 2. the leaders' entries of this wave's map (created, as chain_entry's ptab_get would), kept in
                 //    their lanes
                 uint32_t c_slot = 0xFFFFFFFFu;
                 uint64_t c_st = 0;
                 int64_t c_a = kPAbsent, c_b = kPAbsent;
-                uint32_t c_ev = 0;
                 const bool need = leader && (m == 1 || s_hasent[lane]);
                 if (need) {
                     const uint32_t h = ptab_home(tmask, own, v);
@@ -3135,67 +3162,119 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                     }
                 }
                 const bool any = __ballot(need) != 0ull;  // this map is touched in the chunk
+                // the slot of this event's value (valid only for a parameter event whose entry exists)
+                const uint32_t l_slot = (uint32_t)__shfl((int)c_slot, hp ? (int)e_lead : 0, 64);
+                const bool slot_ok = hp && l_slot != 0xFFFFFFFFu;
                 ps_wave_sync();
                 mark(2);
-                // 3. the next kPsPre records of the queue with their keys' state, and which are the chunk's keys
+                // 3. the next kPsPre records of the queue (record r * 64 + lane in this lane) with their keys'
+                //    state: candidates outside the chunk (live*) and chunk keys' pre-chunk records (link*)
                 const uint32_t npre = (area && any) ? (uint32_t)min<uint64_t>(kPsPre, tail - head) : 0u;
+                uint32_t rslot0 = 0xFFFFFFFFu, rslot1 = 0xFFFFFFFFu, rlink0 = 0, rlink1 = 0;
+                uint64_t live0 = 0, live1 = 0, link0 = 0, link1 = 0;
                 {
-                    uint64_t rv[kPre], rs[kPre];
-                    bool want[kPre];
+                    uint64_t rv[2], rs[2];
+                    bool want[2];
 #pragma unroll
-                    for (int r = 0; r < kPre; ++r) {
+                    for (int r = 0; r < 2; ++r) {
                         const uint32_t k = (uint32_t)r * 64 + lane;
                         want[r] = k < npre;
                         const LruRec *rp = want[r] ? &area[1 + (head + k) % qcap] : nullptr;
                         rv[r] = want[r] ? ps_ldu(&rp->value) : 0ull;
                         rs[r] = want[r] ? ps_ldu(&rp->stamp) : 0ull;
                     }
-                    PEntry *e[kPre];
-                    ptab_find_n<kPre>(tab, tmask, own, rv, want, e, st.overflow);
+                    PEntry *e[2];
+                    ptab_find_n<2>(tab, tmask, own, rv, want, e, st.overflow);
 #pragma unroll
-                    for (int r = 0; r < kPre; ++r) {
-                        if (!want[r]) continue;
-                        const uint32_t k = (uint32_t)r * 64 + lane;
+                    for (int r = 0; r < 2; ++r) {
                         const uint32_t slot = e[r] ? (uint32_t)(e[r] - tab) : 0xFFFFFFFFu;
-                        s_pst[m][k] = rs[r];
-                        s_pslot[m][k] = slot;
-                        s_pgp[m][k] = e[r] && ps_ld(&e[r]->a) != kPAbsent ? 1 : 0;
-                        s_pgs[m][k] = e[r] ? ps_ldu(&tstamp[slot]) : 0ull;
-                        s_plink[m][k] = (int8_t)(e[r] ? ps_hash_get(hk, hv, slot) : -1);
+                        const bool gp = e[r] && ps_ld(&e[r]->a) != kPAbsent;
+                        const uint64_t gs = e[r] ? ps_ldu(&tstamp[slot]) : 0ull;
+                        const int link = e[r] ? ps_hash_get(hk, hv, slot) : -1;
+                        const uint64_t lst = (uint64_t)__shfl((long long)c_st, link >= 0 ? link : 0, 64);
+                        const bool lv = want[r] && link < 0 && gp && gs == rs[r];
+                        const bool lk = want[r] && link >= 0 && lst == rs[r];
+                        if (r == 0) {
+                            rslot0 = slot;
+                            rlink0 = (uint32_t)max(link, 0);
+                            live0 = __ballot(lv);
+                            link0 = __ballot(lk);
+                        } else {
+                            rslot1 = slot;
+                            rlink1 = (uint32_t)max(link, 0);
+                            live1 = __ballot(lv);
+                            link1 = __ballot(lk);
+                        }
                     }
                 }
-                ps_wave_sync();
                 mark(3);
-                // 4. the chunk in arrival order, wave-uniform: every lane takes the same steps on values read out
-                //    of the owning lanes (k_llru's chain_entry / chain_exit, this wave's map)
-                uint64_t used = 0;
-                uint32_t npush = 0, nev = 0;
-                uint64_t q_pv = 0, q_ps = 0;
-                uint32_t ev_slot = 0;
-                int32_t r_d = 0, r_w = 0;
-                uint32_t r_pass = 0;
+                // 4. the LRU scan: the chunk's accesses in arrival order on wave-uniform masks (bit L: leader L)
+                int32_t tdel = 0;  // wave 1: this event's thread-count change
+                uint64_t acc;
+                if (m == 0) {
+                    acc = __ballot(act && !(e_fl & 1u) && slot_ok && param_map_access(c, p, v, e_acq));
+                } else {
+                    tdel = slot_ok ? ((e_fl & 1u) ? -1 : ((e_fl & 4u) ? 1 : 0)) : 0;
+                    acc = __ballot(act && tdel != 0);
+                }
+                uint64_t present = __ballot(c_slot != 0xFFFFFFFFu && c_a != kPAbsent);
+                uint64_t touched = 0, reset = 0, evl = 0, evnc0 = 0, evnc1 = 0;
+                uint32_t used = 0, nev = 0, ev_slot = 0;
                 auto evict = [&]() __attribute__((always_inline)) {
+                    n_evict += 1;
                     for (;;) {
-                        uint64_t rs, gs;
-                        uint32_t slot, gp;
-                        int link;
-                        if (used < npre) {
-                            const uint32_t k = (uint32_t)used;
-                            rs = s_pst[m][k];
-                            gs = s_pgs[m][k];
-                            slot = s_pslot[m][k];
-                            gp = s_pgp[m][k];
-                            link = s_plink[m][k];
+                        if (used < npre) {  // the first candidate at or past `used`
+                            const uint64_t c0m = used < 64 ? (live0 | link0) & (~0ull << used) : 0ull;
+                            const uint64_t c1m = (live1 | link1) & (used < 64 ? ~0ull : (~0ull << (used - 64)));
+                            if (!c0m && !c1m) {
+                                n_pop += npre - used;
+                                used = npre;
+                                continue;
+                            }
+                            const uint32_t idx = c0m ? (uint32_t)__builtin_ctzll(c0m) : 64u + (uint32_t)__builtin_ctzll(c1m);
+                            n_pop += idx + 1 - used;
+                            used = idx + 1;
+                            const uint64_t bit = 1ull << (idx & 63);
+                            if (idx < 64 ? (live0 & bit) : (live1 & bit)) {
+                                if (idx < 64) evnc0 |= bit;
+                                else evnc1 |= bit;
+                                size -= 1;
+                                return;
+                            }
+                            const uint32_t L = idx < 64 ? rl32(rlink0, idx) : rl32(rlink1, idx - 64);
+                            const uint64_t bL = 1ull << L;
+                            if (!(present & bL) || (touched & bL)) continue;
+                            present &= ~bL;
+                            evl |= bL;
+                            if (m == 1) c_a = (int64_t)wl64((uint64_t)c_a, (uint64_t)kPAbsent, L);
+                            size -= 1;
+                            return;
                         } else if (head + used < tail) {  // past the loaded records: one global pop
+                            n_gpop += 1;
+                            n_pop += 1;
                             const LruRec *rp = &area[1 + (head + used) % qcap];
-                            const uint64_t rv = ps_ldu(&rp->value);
-                            rs = ps_ldu(&rp->stamp);
+                            const uint64_t rv = ps_ldu(&rp->value), rs = ps_ldu(&rp->stamp);
                             PEntry *e = ptab_get(tab, tmask, own, rv, false, st.overflow);
-                            slot = e ? (uint32_t)(e - tab) : 0xFFFFFFFFu;
-                            gp = e && ps_ld(&e->a) != kPAbsent ? 1u : 0u;
-                            gs = e ? ps_ldu(&tstamp[slot]) : 0ull;
+                            const uint32_t slot = e ? (uint32_t)(e - tab) : 0xFFFFFFFFu;
+                            const bool gp = e && ps_ld(&e->a) != kPAbsent;
+                            const uint64_t gs = e ? ps_ldu(&tstamp[slot]) : 0ull;
                             const uint64_t hit = __ballot(c_slot == slot && slot != 0xFFFFFFFFu);
-                            link = hit ? __builtin_ctzll(hit) : -1;
+                            used += 1;
+                            if (hit) {
+                                const uint32_t L = (uint32_t)__builtin_ctzll(hit);
+                                const uint64_t bL = 1ull << L;
+                                if (!(present & bL) || (touched & bL) || rl64(c_st, L) != rs) continue;
+                                present &= ~bL;
+                                evl |= bL;
+                                if (m == 1) c_a = (int64_t)wl64((uint64_t)c_a, (uint64_t)kPAbsent, L);
+                                size -= 1;
+                                return;
+                            }
+                            if (slot == 0xFFFFFFFFu || !gp || gs != rs) continue;
+                            ev_slot = wl32(ev_slot, slot, nev);
+                            nev += 1;
+                            size -= 1;
+                            return;
                         } else {
                             if (lane == 0) {
                                 atomicOr(&st.lru_ctl[1], 2u);  // a full map without a live record: never expected
@@ -3203,131 +3282,131 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                             }
                             return;
                         }
-                        used += 1;
-                        if (link >= 0) {
-                            const uint32_t L = (uint32_t)link;
-                            if ((int64_t)rl64((uint64_t)c_a, L) == kPAbsent || rl64(c_st, L) != rs) continue;
-                            c_a = (int64_t)wl64((uint64_t)c_a, (uint64_t)kPAbsent, L);
-                            c_b = (int64_t)wl64((uint64_t)c_b, (uint64_t)kPAbsent, L);
-                            c_ev = wl32(c_ev, 1u, L);
-                            size -= 1;
-                            return;
-                        }
-                        if (slot == 0xFFFFFFFFu || !gp || gs != rs) continue;
-                        ev_slot = wl32(ev_slot, slot, nev);
-                        nev += 1;
-                        size -= 1;
-                        return;
                     }
                 };
-                auto push = [&](uint64_t val, uint64_t stamp) __attribute__((always_inline)) {
-                    q_pv = wl64(q_pv, val, npush);
-                    q_ps = wl64(q_ps, stamp, npush);
-                    npush += 1;
-                };
-                for (uint32_t k = 0; k < nk; ++k) {
-                    const uint32_t fl2 = rl32(e_fl, k);
+                for (uint64_t am = acc; am; am &= am - 1ull) {
+                    const uint32_t k = (uint32_t)__builtin_ctzll(am);
                     const uint32_t L = rl32(e_lead, k);
-                    const uint64_t stamp = lru_stamp(st, rl32(e_idx, k), 0);
-                    if (m == 0) {  // the time/token map, the decision, the node statistics
-                        const uint32_t r = rl32(e_run, k);
-                        if (r != cur_run) {
-                            if (cur_run != 0xFFFFFFFFu && lane == 0) apply_run(cur_run);
-                            cur_run = r;
-                            pa = ba = np = 0;
+                    const uint64_t bL = 1ull << L;
+                    touched |= bL;
+                    if (m == 0) {  // time map then token map, one recency order
+                        if (!(present & bL)) {
+                            present |= bL;
+                            reset |= 1ull << k;
+                            size += 1;
+                            if (area && size > cap) evict();
                         }
-                        if (fl2 & 1u) continue;  // an exit: wave 1's thread count only
-                        const int acq = (int)rl32((uint32_t)e_acq, k);
-                        int d = D_PASS;
-                        int64_t w = 0;
-                        if (fl2 & 2u) {
-                            const uint64_t val = rl64(v, L);
-                            if (rl32(c_slot, L) == 0xFFFFFFFFu) {  // the map is full: the batch fails (overflow)
-                                d = D_BLOCK_PARAM;
-                            } else {
-                                const int64_t t = (int64_t)rl64((uint64_t)e_t, k);
-                                if (param_map_access(c, p, val, acq)) {  // time map then token map, one recency order
-                                    const bool absent = (int64_t)rl64((uint64_t)c_a, L) == kPAbsent;
-                                    c_st = wl64(c_st, stamp, L);
-                                    if (absent) size += 1;
-                                    if (area) {
-                                        push(val, stamp);
-                                        if (absent && size > cap) evict();
-                                    }
-                                }
-                                struct { int64_t a, b; } e{(int64_t)rl64((uint64_t)c_a, L), (int64_t)rl64((uint64_t)c_b, L)};
-                                const bool pass = param_pass_qps(c, p, e, val, acq, t, &w);
-                                c_a = (int64_t)wl64((uint64_t)c_a, (uint64_t)e.a, L);
-                                c_b = (int64_t)wl64((uint64_t)c_b, (uint64_t)e.b, L);
-                                if (!pass) {
-                                    d = D_BLOCK_PARAM;
-                                    w = 0;  // a block's detail: the rule's index
-                                }
-                            }
-                        }
-                        if (d == D_PASS) {
-                            pa += acq;
-                            np += 1;
-                            r_pass = wl32(r_pass, 1u, k);
-                        } else {
-                            ba += acq;
-                        }
-                        r_d = (int32_t)wl32((uint32_t)r_d, (uint32_t)d, k);
-                        r_w = (int32_t)wl32((uint32_t)r_w, (uint32_t)(int32_t)w, k);
                     } else {  // ParameterMetric.add / decreaseThreadCount of index 0 (param_threads)
-                        if (!(fl2 & 2u)) continue;
-                        const int tdelta = (fl2 & 1u) ? -1 : ((fl2 & 4u) ? 1 : 0);
-                        if (!tdelta || rl32(c_slot, L) == 0xFFFFFFFFu) continue;
-                        const uint64_t val = rl64(v, L);
+                        const int64_t td = (int64_t)(int32_t)rl32((uint32_t)tdel, k);
                         const int64_t ta = (int64_t)rl64((uint64_t)c_a, L);
-                        c_st = wl64(c_st, stamp, L);
                         int64_t nt;
                         if (ta == kPAbsent) {
                             size += 1;
-                            if (area) {
-                                push(val, stamp);
-                                if (size > cap) evict();
-                            }
-                            nt = tdelta > 0 ? 1 : 0;
+                            if (area && size > cap) evict();
+                            nt = td > 0 ? 1 : 0;
+                            present |= bL;
                         } else {
-                            if (area) push(val, stamp);
-                            nt = ta + (tdelta > 0 ? 1 : -1);
-                            if (tdelta < 0 && nt <= 0) {
+                            nt = ta + td;
+                            if (td < 0 && nt <= 0) {
                                 nt = kPAbsent;
                                 size -= 1;
+                                present &= ~bL;
                             }
                         }
                         c_a = (int64_t)wl64((uint64_t)c_a, (uint64_t)nt, L);
                     }
                 }
+                n_acc += (uint64_t)__popcll(acc);
+                if ((acc >> lane) & 1ull) atomicMax(&s_last[m][e_lead], lane + 1);
+                ps_wave_sync();
                 mark(4);
-                // 5. write back: the decisions and the passes (wave 0), the copies, the evictions, then the queue's
-                //    pushes (after a compaction when the ring would overflow: live records kept in order)
+                // 5. wave 0: the checks, lane-parallel in rounds of each value's events, and the decisions
+                const bool ent = act && !(e_fl & 1u);
+                int d = D_PASS;
+                int64_t w = 0;
                 if (m == 0) {
-                    const bool ent = act && !(e_fl & 1u);
-                    if (ent) {
-                        decision[e_idx] = (int8_t)r_d;
-                        wait_ms[e_idx] = r_w;
+                    if (leader) {
+                        s_ra[lane] = c_a;
+                        s_rb[lane] = c_b;
                     }
-                    s_bfl[bsel][lane] = (uint8_t)(e_fl | (r_pass ? 4u : 0u));
+                    const bool tok = ent && slot_ok;
+                    if (ent && hp && !slot_ok) d = D_BLOCK_PARAM;  // the map is full: the batch fails (overflow)
+                    const uint32_t nr = ps_wave_max(tok ? e_occ + 1 : 0u);
+                    const bool rs_me = (reset >> lane) & 1ull;
+                    ps_wave_sync();
+                    for (uint32_t r = 0; r < nr; ++r) {
+                        if (tok && e_occ == r) {
+                            struct { int64_t a, b; } e{s_ra[e_lead], s_rb[e_lead]};
+                            if (rs_me) e.a = e.b = kPAbsent;
+                            if (!param_pass_qps(c, p, e, v, e_acq, e_t, &w)) {
+                                d = D_BLOCK_PARAM;
+                                w = 0;  // a block's detail: the rule's index
+                            }
+                            s_ra[e_lead] = e.a;
+                            s_rb[e_lead] = e.b;
+                        }
+                        ps_wave_sync();
+                    }
+                    if (ent) {
+                        decision[e_idx] = (int8_t)d;
+                        wait_ms[e_idx] = (int32_t)w;
+                    }
+                    s_bfl[bsel][lane] = (uint8_t)(e_fl | (ent && d == D_PASS ? 4u : 0u));
+                    // the node statistics, run by run (a chunk's runs are consecutive lanes)
+                    for (uint64_t rem = __ballot(act); rem;) {
+                        const uint32_t r = rl32(e_run, (uint32_t)__builtin_ctzll(rem));
+                        const bool inr = act && e_run == r;
+                        rem &= ~__ballot(inr);
+                        if (r != cur_run) {
+                            if (cur_run != 0xFFFFFFFFu && lane == 0) apply_run(cur_run);
+                            cur_run = r;
+                            pa = ba = np = 0;
+                        }
+                        const bool ps_ = inr && ent && d == D_PASS, bk_ = inr && ent && d != D_PASS;
+                        pa += ps_wave_sum(ps_ ? (int64_t)e_acq : 0);
+                        ba += ps_wave_sum(bk_ ? (int64_t)e_acq : 0);
+                        np += (int64_t)__popcll(__ballot(ps_));
+                    }
+                    if (leader) {
+                        c_a = s_ra[lane];
+                        c_b = s_rb[lane];
+                    }
                 }
+                mark(5);
+                // 6. write back: the copies (an evicted key not accessed since is absent), the evictions, then the
+                //    queue's pushes (after a compaction when the ring would overflow: live records kept in order)
+                const uint32_t last = s_last[m][lane];
+                const uint64_t lst = (uint64_t)__shfl((long long)my_stamp, last ? (int)last - 1 : 0, 64);
                 if (c_slot != 0xFFFFFFFFu) {
-                    tab[c_slot].a = c_a;
-                    if (m == 0) tab[c_slot].b = c_b;
-                    else if (c_ev) tab[c_slot].b = kPAbsent;
-                    tstamp[c_slot] = c_st;
+                    const uint64_t bme = 1ull << lane;
+                    if (m == 0) {
+                        const bool gone = (evl & bme) && !(touched & bme);
+                        tab[c_slot].a = gone ? kPAbsent : c_a;
+                        tab[c_slot].b = gone ? kPAbsent : c_b;
+                    } else {
+                        tab[c_slot].a = c_a;
+                        if (evl & bme) tab[c_slot].b = kPAbsent;
+                    }
+                    tstamp[c_slot] = last ? lst : c_st;
+                }
+                if ((evnc0 >> lane) & 1ull) {
+                    tab[rslot0].a = kPAbsent;
+                    tab[rslot0].b = kPAbsent;
+                }
+                if ((evnc1 >> lane) & 1ull) {
+                    tab[rslot1].a = kPAbsent;
+                    tab[rslot1].b = kPAbsent;
                 }
                 if (lane < nev) {
                     tab[ev_slot].a = kPAbsent;
                     tab[ev_slot].b = kPAbsent;
                 }
                 ps_wave_sync();
-                mark(5);
                 if (area) {
                     uint64_t h = head + used, t = tail;
-                    uint32_t npm = npush;
+                    uint32_t npm = (uint32_t)__popcll(acc);
                     if (t - h + npm > qcap) {  // lru_compact over [h, t)
-                        uint64_t w = h;
+                        uint64_t wpos = h;
                         for (uint64_t b0 = h; b0 < t; b0 += 64) {
                             const uint64_t ix = b0 + (uint64_t)lane;
                             LruRec rec{0, 0};
@@ -3340,11 +3419,11 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                             }
                             const uint64_t bl = __ballot(live);
                             ps_wave_sync();  // every lane has read its record before any is overwritten
-                            if (live) area[1 + (w + (uint64_t)__popcll(bl & ((1ull << lane) - 1ull))) % qcap] = rec;
-                            w += (uint64_t)__popcll(bl);
+                            if (live) area[1 + (wpos + (uint64_t)__popcll(bl & lt_mask)) % qcap] = rec;
+                            wpos += (uint64_t)__popcll(bl);
                             ps_wave_sync();
                         }
-                        t = w;
+                        t = wpos;
                         if (t - h + npm > qcap) {
                             if (lane == 0) {
                                 atomicOr(&st.lru_ctl[1], 2u);
@@ -3353,7 +3432,8 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                             npm = 0;
                         }
                     }
-                    if (lane < npm) area[1 + (t + lane) % qcap] = LruRec{q_pv, q_ps};
+                    if (npm && ((acc >> lane) & 1ull))
+                        area[1 + (t + (uint64_t)__popcll(acc & lt_mask)) % qcap] = LruRec{v, my_stamp};
                     head = h;
                     tail = t + npm;
                 }
@@ -3361,6 +3441,13 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                 mark(6);
             }
             __syncthreads();  // wave 0's chunk handed over, wave 1's buffer free
+        }
+        if (prof && lane == 0) {  // per wave: [8 + 4 * wave] pops, global pops, evictions, accesses
+            atomicAdd(&g_lps_prof[8 + 4 * wave], (unsigned long long)n_pop);
+            atomicAdd(&g_lps_prof[9 + 4 * wave], (unsigned long long)n_gpop);
+            atomicAdd(&g_lps_prof[10 + 4 * wave], (unsigned long long)n_evict);
+            atomicAdd(&g_lps_prof[11 + 4 * wave], (unsigned long long)n_acc);
+            if (wave == 0) atomicMax(&g_lps_prof[5], (unsigned long long)(wall_clock64() - t_res));
         }
         if (lane == 0) {
             if (wave == 0) {
@@ -4645,21 +4732,23 @@ void FlowEngine::lru_prepare(const uint8_t *kind, const uint32_t *resource, cons
     static const int prof = getenv("SGA_LRU_PROF") ? atoi(getenv("SGA_LRU_PROF")) : 0;  // diagnostics only
     if (prof) {
         static bool on = false;
-        unsigned long long v[8];
+        unsigned long long v[16];
         if (on) {  // the previous batch's counters
-            SGA_HIP_CHECK(hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_lru_prof), sizeof(v), 0, hipMemcpyDeviceToHost, s));
+            SGA_HIP_CHECK(hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_lru_prof), 8 * sizeof(v[0]), 0, hipMemcpyDeviceToHost, s));
             SGA_HIP_CHECK(hipStreamSynchronize(s));
             fprintf(stderr, "lru_prof pushes %llu compactions %llu scanned %llu compact_ticks %llu evictions %llu popped %llu "
                     "entry_ticks %llu exit_ticks %llu\n", v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
             SGA_HIP_CHECK(hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_lps_prof), sizeof(v), 0, hipMemcpyDeviceToHost, s));
             SGA_HIP_CHECK(hipStreamSynchronize(s));
-            fprintf(stderr, "lps_prof events %llu chunks %llu ticks: loads %llu leaders %llu records %llu replay %llu "
-                    "writeback %llu compaction %llu\n", v[0], v[7], v[1], v[2], v[3], v[4], v[5], v[6]);
+            fprintf(stderr, "lps_prof events %llu chunks %llu ticks: loads %llu leaders %llu records %llu replay+writeback "
+                    "%llu compaction %llu longest resource %llu; time map: pops %llu global %llu evictions %llu accesses "
+                    "%llu; thread map: pops %llu global %llu evictions %llu accesses %llu\n", v[0], v[7], v[1], v[2], v[3],
+                    v[4], v[6], v[5], v[8], v[9], v[10], v[11], v[12], v[13], v[14], v[15]);
         }
         std::memset(v, 0, sizeof(v));
         SGA_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lps_prof), v, sizeof(v), 0, hipMemcpyHostToDevice, s));
         const int one = 1;
-        SGA_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lru_prof), v, sizeof(v), 0, hipMemcpyHostToDevice, s));
+        SGA_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lru_prof), v, 8 * sizeof(v[0]), 0, hipMemcpyHostToDevice, s));
         SGA_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lru_prof_on), &one, sizeof(one), 0, hipMemcpyHostToDevice, s));
         on = true;
     }
