@@ -2906,16 +2906,16 @@ __global__ __launch_bounds__(64) void k_llru(FlowState st, int64_t max_rt, FlowS
 // ---- LRU-mode parameter-only resources, chunked through LDS (k_llru_ps)
 // A parameter-only resource (pseg_take's conditions: one QPS-grade ParamFlowRule of argument index 0, no
 // FlowRule, no breaker, only the index-0 thread-count map) whose maps are in LRU mode replays its events in
-// arrival order exactly as k_llru does, but one global round trip per chunk instead of ~25 per event: per
-// chunk of 64 events the 64 lanes load the events, find (or create) each distinct value's entry in the
-// rule's time/token map and in the thread-count map and copy them to LDS, and load the next kPsPre records
-// of each LRU queue with the state of their keys; lane 0 replays the chunk against those copies (queue
-// pushes gathered in LDS, evictions popping the loaded records, a global pop only past them); the lanes
-// write the copies, the evictions and the pushes back.  Decisions never read the node (as for pseg), so the
-// node statistics go in aggregate, run by run.  k_lflows flags these flows in sc.lru (kLruPs).
-// SGA_LRU_PROF=1 (diagnostics only): k_llru_ps ticks per phase, summed over chunks: [0] events [1] loads +
-// dedupe [2] leader entries [3] queue records [4] replay [5] write-back [6] compaction [7] chunks
-__device__ unsigned long long g_lps_prof[16];
+// arrival order with k_llru's results, but a few global round trips per chunk of 64 events instead of ~25
+// per event: the lanes load the events, find (or create) each distinct value's entry in the map and the next
+// kPsPre records of its LRU queue with their keys' state (registers), the LRU order is replayed on
+// wave-uniform bit masks, the token checks run lane-parallel (k_llru_ps below).  Decisions never read the
+// node (as for pseg), so the node statistics go in aggregate, run by run.  k_lflows flags these flows in
+// sc.lru (kLruPs).
+// SGA_LRU_PROF=1 (diagnostics only): k_llru_ps ticks per phase of wave 0, summed over chunks: [0] events [1]
+// loads + dedupe [2] leader entries [3] queue records [4] LRU scan [5] rounds [6] write-back [7] chunks; [8..15]
+// queue pops per map; [16 + wave] the longest resource, [18 + wave] its busiest wave's ticks
+__device__ unsigned long long g_lps_prof[22];
 
 __device__ __forceinline__ uint32_t rl32(uint32_t x, uint32_t l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
@@ -2981,6 +2981,11 @@ __device__ __forceinline__ void ps_wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
+// a wave-uniform value the compiler cannot prove uniform (an atomic load's result): readfirstlane
+__device__ __forceinline__ uint32_t ps_uni32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t ps_uni64(uint64_t x) {
+    return (uint64_t)ps_uni32((uint32_t)x) | ((uint64_t)ps_uni32((uint32_t)(x >> 32)) << 32);
+}
 __device__ __forceinline__ int64_t ps_wave_sum(int64_t x) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x += (int64_t)__shfl_xor((long long)x, o, 64);
@@ -3018,12 +3023,16 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
     __shared__ uint8_t s_hasent[64];
     __shared__ uint32_t s_last[2][64];  // per leader lane: 1 + the lane of its value's last access in the chunk
     __shared__ int64_t s_ra[64], s_rb[64];  // wave 0's rounds: each value's (a, b) at its leader's index
+    __shared__ int64_t s_tc[64];            // wave 1's rounds: each value's thread count
+    __shared__ uint32_t s_first[2][64];     // per leader lane: the lane of its value's first access (64: none)
     // chunk handoff (wave 0 -> wave 1): per event flags (bit0 exit, bit1 parameter, bit2 passed), leader,
-    // request index, value
-    __shared__ uint8_t s_bfl[2][64], s_blead[2][64];
+    // rank among its value's events, request index, value
+    __shared__ uint8_t s_bfl[2][64], s_blead[2][64], s_bocc[2][64];
     __shared__ uint32_t s_bidx[2][64];
     __shared__ uint64_t s_bval[2][64];
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // the wave index through readfirstlane: wave-uniform to the compiler, so every branch on the map (and on
+    // the masks and counters derived from it) is a scalar branch, not an exec-masked one
+    const uint32_t lane = threadIdx.x & 63, wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     const Ctx c{st, max_rt};
     const uint32_t nl = sc.counters[10], nflows = sc.counters[2], nruns = sc.counters[1];
@@ -3048,8 +3057,8 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
         const uint64_t qo = m == 0 ? st.pq[p.id] : st.tq[tj];
         LruRec *const area = qo == kNoQueue ? nullptr : st.lpool + qo;
         const uint64_t qcap = 2ull * (m == 0 ? p.cap : (uint32_t)kThreadMapCap) + 2;
-        uint64_t head = area ? ps_ldu(&area[0].value) : 0, tail = area ? ps_ldu(&area[0].stamp) : 0;
-        uint32_t size = m == 0 ? st.psize[p.id] : st.tsize[tj];
+        uint64_t head = ps_uni64(area ? ps_ldu(&area[0].value) : 0), tail = ps_uni64(area ? ps_ldu(&area[0].stamp) : 0);
+        uint32_t size = ps_uni32(m == 0 ? st.psize[p.id] : st.tsize[tj]);
         const uint32_t cap = m == 0 ? p.cap : (uint32_t)kThreadMapCap;
         uint32_t *const hk = s_hk[m];
         uint8_t *const hv = s_hv[m];
@@ -3081,7 +3090,7 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
             tp = now;
         };
         const uint32_t nch = (je - jb + 63) / 64;
-        uint64_t n_pop = 0, n_gpop = 0, n_evict = 0, n_acc = 0;  // diagnostics (SGA_LRU_PROF)
+        uint64_t n_pop = 0, n_gpop = 0, n_evict = 0, n_acc = 0, busy = 0;  // diagnostics (SGA_LRU_PROF)
         const uint64_t t_res = prof ? wall_clock64() : 0;
         for (uint32_t step = 0; step <= nch; ++step) {
             // wave 0: chunk `step`; wave 1: chunk step - 1
@@ -3094,6 +3103,7 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                     atomicAdd(&g_lps_prof[7], 1ull);
                 }
                 tp = prof ? wall_clock64() : 0;
+                const uint64_t t_step = tp;
                 // 1. the chunk's events (lane k: event k); wave 0 loads them and hands them over
                 const bool act = lane < nk;
                 uint32_t e_fl, e_lead, e_idx, e_occ = 0;
@@ -3128,16 +3138,19 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                     if (hp && !ex) s_hasent[lead] = 1;  // the value's time/token entry is needed only by entries
                     s_bfl[bsel][lane] = (uint8_t)e_fl;
                     s_blead[bsel][lane] = (uint8_t)e_lead;
+                    s_bocc[bsel][lane] = (uint8_t)e_occ;
                     s_bidx[bsel][lane] = e_idx;
                     s_bval[bsel][lane] = v;
                 } else {
                     e_fl = s_bfl[bsel][lane];
                     e_lead = s_blead[bsel][lane];
+                    e_occ = s_bocc[bsel][lane];
                     e_idx = s_bidx[bsel][lane];
                     v = s_bval[bsel][lane];
                 }
                 for (uint32_t k = lane; k < (uint32_t)kPsHash; k += 64) hk[k] = 0xFFFFFFFFu;
                 s_last[m][lane] = 0;
+                s_first[m][lane] = 64;
                 ps_wave_sync();
                 const bool hp = (e_fl & 2u) != 0;
                 const bool leader = hp && e_lead == lane;
@@ -3169,7 +3182,10 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                 mark(2);
                 // 3. the next kPsPre records of the queue (record r * 64 + lane in this lane) with their keys'
                 //    state: candidates outside the chunk (live*) and chunk keys' pre-chunk records (link*)
-                const uint32_t npre = (area && any) ? (uint32_t)min<uint64_t>(kPsPre, tail - head) : 0u;
+                head = ps_uni64(head);
+                tail = ps_uni64(tail);
+                size = ps_uni32(size);
+                const uint32_t npre = ps_uni32((area && any) ? (uint32_t)min<uint64_t>(kPsPre, tail - head) : 0u);
                 uint32_t rslot0 = 0xFFFFFFFFu, rslot1 = 0xFFFFFFFFu, rlink0 = 0, rlink1 = 0;
                 uint64_t live0 = 0, live1 = 0, link0 = 0, link1 = 0;
                 {
@@ -3253,11 +3269,11 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                             n_gpop += 1;
                             n_pop += 1;
                             const LruRec *rp = &area[1 + (head + used) % qcap];
-                            const uint64_t rv = ps_ldu(&rp->value), rs = ps_ldu(&rp->stamp);
+                            const uint64_t rv = ps_uni64(ps_ldu(&rp->value)), rs = ps_uni64(ps_ldu(&rp->stamp));
                             PEntry *e = ptab_get(tab, tmask, own, rv, false, st.overflow);
-                            const uint32_t slot = e ? (uint32_t)(e - tab) : 0xFFFFFFFFu;
-                            const bool gp = e && ps_ld(&e->a) != kPAbsent;
-                            const uint64_t gs = e ? ps_ldu(&tstamp[slot]) : 0ull;
+                            const uint32_t slot = ps_uni32(e ? (uint32_t)(e - tab) : 0xFFFFFFFFu);
+                            const bool gp = ps_uni32(e && ps_ld(&e->a) != kPAbsent ? 1u : 0u) != 0;
+                            const uint64_t gs = ps_uni64(e ? ps_ldu(&tstamp[slot]) : 0ull);
                             const uint64_t hit = __ballot(c_slot == slot && slot != 0xFFFFFFFFu);
                             used += 1;
                             if (hit) {
@@ -3284,7 +3300,94 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                         }
                     }
                 };
-                for (uint64_t am = acc; am; am &= am - 1ull) {
+                // The fast path: in steady state the map is full, each insert evicts the first candidate, and the
+                // chunk's keys sit near the queue's tail.  Inserts and removals come from each value's own events
+                // (wave 1: its thread counts, lane-parallel in rounds), the number of evictions E from their order;
+                // when the first E candidates are all outside the chunk, they are the evictions and no chunk key
+                // was evicted, which is the scan's result.  Otherwise the sequential scan below.
+                if ((acc >> lane) & 1ull) atomicMin(&s_first[m][e_lead], lane);
+                ps_wave_sync();
+                const bool first_acc = ((acc >> lane) & 1ull) && s_first[m][e_lead] == lane;
+                const uint64_t acc_lead = __ballot(s_first[m][lane] < 64u);  // leaders whose value is accessed
+                uint64_t ins;
+                uint32_t n_evf = 0, size_f = size;
+                int64_t t_cnt = c_a;
+                if (m == 0) {
+                    ins = __ballot(first_acc && !((present >> e_lead) & 1ull));
+                    const uint32_t ni = (uint32_t)__popcll(ins);
+                    n_evf = !area ? 0u : (size >= cap ? ni : (ni > cap - size ? ni - (cap - size) : 0u));
+                    size_f = size + ni - n_evf;
+                } else {
+                    if (leader) s_tc[lane] = c_a;
+                    const bool ta_me = (acc >> lane) & 1ull;
+                    const uint32_t nr = ps_wave_max(ta_me ? e_occ + 1 : 0u);
+                    bool my_ins = false, my_rem = false;
+                    ps_wave_sync();
+                    for (uint32_t r = 0; r < nr; ++r) {
+                        if (ta_me && e_occ == r) {
+                            int64_t cnt = s_tc[e_lead];
+                            if (cnt == kPAbsent) {
+                                my_ins = true;
+                                cnt = tdel > 0 ? 1 : 0;
+                            } else {
+                                cnt += tdel;
+                                if (tdel < 0 && cnt <= 0) {
+                                    my_rem = true;
+                                    cnt = kPAbsent;
+                                }
+                            }
+                            s_tc[e_lead] = cnt;
+                        }
+                        ps_wave_sync();
+                    }
+                    ins = __ballot(my_ins);
+                    const uint64_t rem = __ballot(my_rem);
+                    uint32_t sz = size;
+                    for (uint64_t am = ins | rem; am; am &= am - 1ull) {
+                        if ((ins >> __builtin_ctzll(am)) & 1ull) {
+                            sz += 1;
+                            if (area && sz > cap) {
+                                sz -= 1;
+                                n_evf += 1;
+                            }
+                        } else {
+                            sz -= 1;
+                        }
+                    }
+                    size_f = sz;
+                    t_cnt = s_tc[lane];
+                }
+                const uint64_t cand0 = live0 | link0, cand1 = live1 | link1;
+                const uint32_t pc0 = (uint32_t)__popcll(cand0), pc1 = (uint32_t)__popcll(cand1);
+                const uint64_t sel0 = __ballot(n_evf != 0 && n_evf <= pc0 && ((cand0 >> lane) & 1ull) &&
+                                               (uint32_t)__popcll(cand0 & lt_mask) == n_evf - 1);
+                const uint64_t sel1 = __ballot(n_evf > pc0 && n_evf - pc0 <= pc1 && ((cand1 >> lane) & 1ull) &&
+                                               (uint32_t)__popcll(cand1 & lt_mask) == n_evf - pc0 - 1);
+                uint64_t fm0 = 0, fm1 = 0;  // the consumed records: bits up to the n_evf-th candidate
+                bool fast = n_evf == 0;
+                if (sel0) {
+                    const uint32_t pos = (uint32_t)__builtin_ctzll(sel0);
+                    fm0 = pos == 63 ? ~0ull : (2ull << pos) - 1ull;
+                    fast = true;
+                } else if (sel1) {
+                    const uint32_t pos = (uint32_t)__builtin_ctzll(sel1);
+                    fm0 = ~0ull;
+                    fm1 = pos == 63 ? ~0ull : (2ull << pos) - 1ull;
+                    fast = true;
+                }
+                fast = fast && !(link0 & fm0) && !(link1 & fm1);
+                if (fast) {
+                    evnc0 = live0 & fm0;
+                    evnc1 = live1 & fm1;
+                    used = (uint32_t)(__popcll(fm0) + __popcll(fm1));
+                    size = size_f;
+                    touched = acc_lead;
+                    reset = ins;
+                    if (m == 1 && leader) c_a = t_cnt;
+                    n_evict += n_evf;
+                    n_pop += used;
+                }
+                for (uint64_t am = fast ? 0ull : acc; am; am &= am - 1ull) {
                     const uint32_t k = (uint32_t)__builtin_ctzll(am);
                     const uint32_t L = rl32(e_lead, k);
                     const uint64_t bL = 1ull << L;
@@ -3439,6 +3542,7 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                 }
                 ps_wave_sync();
                 mark(6);
+                if (prof) busy += wall_clock64() - t_step;
             }
             __syncthreads();  // wave 0's chunk handed over, wave 1's buffer free
         }
@@ -3447,7 +3551,8 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
             atomicAdd(&g_lps_prof[9 + 4 * wave], (unsigned long long)n_gpop);
             atomicAdd(&g_lps_prof[10 + 4 * wave], (unsigned long long)n_evict);
             atomicAdd(&g_lps_prof[11 + 4 * wave], (unsigned long long)n_acc);
-            if (wave == 0) atomicMax(&g_lps_prof[5], (unsigned long long)(wall_clock64() - t_res));
+            atomicMax(&g_lps_prof[16 + wave], (unsigned long long)(wall_clock64() - t_res));
+            atomicMax(&g_lps_prof[18 + wave], (unsigned long long)busy);
         }
         if (lane == 0) {
             if (wave == 0) {
@@ -4732,7 +4837,7 @@ void FlowEngine::lru_prepare(const uint8_t *kind, const uint32_t *resource, cons
     static const int prof = getenv("SGA_LRU_PROF") ? atoi(getenv("SGA_LRU_PROF")) : 0;  // diagnostics only
     if (prof) {
         static bool on = false;
-        unsigned long long v[16];
+        unsigned long long v[22];
         if (on) {  // the previous batch's counters
             SGA_HIP_CHECK(hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_lru_prof), 8 * sizeof(v[0]), 0, hipMemcpyDeviceToHost, s));
             SGA_HIP_CHECK(hipStreamSynchronize(s));
@@ -4740,10 +4845,11 @@ void FlowEngine::lru_prepare(const uint8_t *kind, const uint32_t *resource, cons
                     "entry_ticks %llu exit_ticks %llu\n", v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
             SGA_HIP_CHECK(hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_lps_prof), sizeof(v), 0, hipMemcpyDeviceToHost, s));
             SGA_HIP_CHECK(hipStreamSynchronize(s));
-            fprintf(stderr, "lps_prof events %llu chunks %llu ticks: loads %llu leaders %llu records %llu replay+writeback "
-                    "%llu compaction %llu longest resource %llu; time map: pops %llu global %llu evictions %llu accesses "
-                    "%llu; thread map: pops %llu global %llu evictions %llu accesses %llu\n", v[0], v[7], v[1], v[2], v[3],
-                    v[4], v[6], v[5], v[8], v[9], v[10], v[11], v[12], v[13], v[14], v[15]);
+            fprintf(stderr, "lps_prof events %llu chunks %llu ticks: loads %llu leaders %llu records %llu scan %llu rounds "
+                    "%llu write-back %llu; longest resource: wave 0 %llu wave 1 %llu, busy %llu / %llu; time map: pops "
+                    "%llu global %llu evictions %llu accesses %llu; thread map: pops %llu global %llu evictions %llu "
+                    "accesses %llu\n", v[0], v[7], v[1], v[2], v[3], v[4], v[5], v[6], v[16], v[17], v[18], v[19], v[8], v[9],
+                    v[10], v[11], v[12], v[13], v[14], v[15]);
         }
         std::memset(v, 0, sizeof(v));
         SGA_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lps_prof), v, sizeof(v), 0, hipMemcpyHostToDevice, s));
