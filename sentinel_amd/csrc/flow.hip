@@ -519,77 +519,92 @@ __device__ bool hot_lookup(const Ctx &c, const ParamRuleDev &p, uint64_t v, int6
 }
 
 // ParamFlowChecker.passSingleValueCheck / passDefaultLocalCheck / passThrottleLocalCheck
-// QPS grade against the value's (lastAddTokenTime, tokens) or throttle-time entry e
+// QPS grade against the value's (lastAddTokenTime, tokens) or throttle-time entry e.  The check's constants for
+// (rule, value, acquireCount) come first (param_pre: the token count with the value's hot item, then the
+// throttle cost or the bucket's maxCount), so a caller checking many events of one value computes them once.
+struct ParamPre {
+    int64_t tc;  // token count (0: every check fails)
+    int64_t k2;  // throttle: cost of the acquire in ms; token bucket: maxCount
+};
+__device__ __forceinline__ ParamPre param_pre(const Ctx &c, const ParamRuleDev &p, uint64_t v, int acquire) {
+    int64_t tc = j_d2l(p.count), hot;
+    if (hot_lookup(c, p, v, &hot)) tc = hot;
+    if (tc == 0) return {0, 0};
+    if (p.behavior == 2)  // ParamFlowChecker.java:224-281
+        return {tc, j_round(1.0 * 1000 * (double)acquire * (double)p.duration / (double)tc)};
+    return {tc, lwrap_add(tc, p.burst)};  // ParamFlowChecker.java:132-222
+}
 template <class E>
-__device__ __forceinline__ bool param_pass_qps(const Ctx &c, const ParamRuleDev &p, E &e, uint64_t v, int acquire,
-                                               int64_t t, int64_t *wait_ms) {
+__device__ __forceinline__ bool param_pass_pre(const ParamRuleDev &p, E &e, ParamPre q, int acquire, int64_t t,
+                                               int64_t *wait_ms) {
     *wait_ms = 0;
-    int64_t hot;
-    {
-        int64_t token_count = j_d2l(p.count);
-        if (hot_lookup(c, p, v, &hot)) token_count = hot;
-        if (token_count == 0) return false;
-        if (p.behavior == 2) {  // throttle, ParamFlowChecker.java:224-281
-            const int64_t cost = j_round(1.0 * 1000 * (double)acquire * (double)p.duration / (double)token_count);
-            if (e.a == kPAbsent) {
-                e.a = t;
-                return true;
-            }
-            const int64_t expected = e.a + cost;
-            if (expected <= t || expected - t < p.max_queue) {
-                e.a = t;
-                const int64_t wait = expected - t;
-                if (wait > 0) {
-                    e.a = expected;
-                    *wait_ms = wait;
-                }
-                return true;
-            }
-            return false;
-        }
-        // token bucket, ParamFlowChecker.java:132-222
-        const int64_t max_count = lwrap_add(token_count, p.burst);
-        if ((int64_t)acquire > max_count) return false;
+    const int64_t token_count = q.tc;
+    if (token_count == 0) return false;
+    if (p.behavior == 2) {  // throttle
+        const int64_t cost = q.k2;
         if (e.a == kPAbsent) {
             e.a = t;
-            if (e.b == kPAbsent) e.b = max_count - acquire;
             return true;
         }
-        const int64_t pass_time = t - e.a;
-        const int64_t dur_ms = lwrap_mul(p.duration, 1000);
-        if (pass_time > dur_ms) {
-            if (e.b == kPAbsent) {
-                e.b = max_count - acquire;
-                e.a = t;
-                return true;
-            }
-            const int64_t rest = e.b;
-            const int64_t to_add = lwrap_mul(pass_time, token_count) / dur_ms;
-            const int64_t nq = lwrap_add(to_add, rest) > max_count ? max_count - acquire
-                                                                   : lwrap_add(rest, to_add) - acquire;
-            if (nq < 0) return false;
-            e.b = nq;
+        const int64_t expected = e.a + cost;
+        if (expected <= t || expected - t < p.max_queue) {
             e.a = t;
-            return true;
-        }
-        if (e.b != kPAbsent) {
-            if (e.b - acquire >= 0) {
-                e.b -= acquire;
-                return true;
+            const int64_t wait = expected - t;
+            if (wait > 0) {
+                e.a = expected;
+                *wait_ms = wait;
             }
-            return false;
+            return true;
         }
         return false;
     }
+    // token bucket
+    const int64_t max_count = q.k2;
+    if ((int64_t)acquire > max_count) return false;
+    if (e.a == kPAbsent) {
+        e.a = t;
+        if (e.b == kPAbsent) e.b = max_count - acquire;
+        return true;
+    }
+    const int64_t pass_time = t - e.a;
+    const int64_t dur_ms = lwrap_mul(p.duration, 1000);
+    if (pass_time > dur_ms) {
+        if (e.b == kPAbsent) {
+            e.b = max_count - acquire;
+            e.a = t;
+            return true;
+        }
+        const int64_t rest = e.b;
+        const int64_t to_add = lwrap_mul(pass_time, token_count) / dur_ms;
+        const int64_t nq = lwrap_add(to_add, rest) > max_count ? max_count - acquire
+                                                               : lwrap_add(rest, to_add) - acquire;
+        if (nq < 0) return false;
+        e.b = nq;
+        e.a = t;
+        return true;
+    }
+    if (e.b != kPAbsent) {
+        if (e.b - acquire >= 0) {
+            e.b -= acquire;
+            return true;
+        }
+        return false;
+    }
+    return false;
+}
+template <class E>
+__device__ __forceinline__ bool param_pass_qps(const Ctx &c, const ParamRuleDev &p, E &e, uint64_t v, int acquire,
+                                               int64_t t, int64_t *wait_ms) {
+    return param_pass_pre(p, e, param_pre(c, p, v, acquire), acquire, t, wait_ms);
 }
 
 // whether a QPS check of value v reaches the rule's maps: not for a zero threshold, nor (token bucket)
 // for acquireCount > maxCount (ParamFlowChecker.java:137-154, 230-234)
+__device__ __forceinline__ bool param_pre_access(const ParamRuleDev &p, ParamPre q, int acquire) {
+    return q.tc != 0 && (p.behavior == 2 || (int64_t)acquire <= q.k2);
+}
 __device__ __forceinline__ bool param_map_access(const Ctx &c, const ParamRuleDev &p, uint64_t v, int acquire) {
-    int64_t token_count = j_d2l(p.count), hot;
-    if (hot_lookup(c, p, v, &hot)) token_count = hot;
-    if (token_count == 0) return false;
-    return p.behavior == 2 || (int64_t)acquire <= lwrap_add(token_count, p.burst);
+    return param_pre_access(p, param_pre(c, p, v, acquire), acquire);
 }
 
 template <bool kLru>
@@ -3058,6 +3073,9 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
         LruRec *const area = qo == kNoQueue ? nullptr : st.lpool + qo;
         const uint64_t qcap = 2ull * (m == 0 ? p.cap : (uint32_t)kThreadMapCap) + 2;
         uint64_t head = ps_uni64(area ? ps_ldu(&area[0].value) : 0), tail = ps_uni64(area ? ps_ldu(&area[0].stamp) : 0);
+        // the ring positions of head and tail, kept incrementally (no 64-bit division per lane)
+        uint32_t hq = area ? (uint32_t)(head % qcap) : 0u, tq = area ? (uint32_t)(tail % qcap) : 0u;
+        const uint32_t qc32 = (uint32_t)qcap;
         uint32_t size = ps_uni32(m == 0 ? st.psize[p.id] : st.tsize[tj]);
         const uint32_t cap = m == 0 ? p.cap : (uint32_t)kThreadMapCap;
         uint32_t *const hk = s_hk[m];
@@ -3195,7 +3213,8 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                     for (int r = 0; r < 2; ++r) {
                         const uint32_t k = (uint32_t)r * 64 + lane;
                         want[r] = k < npre;
-                        const LruRec *rp = want[r] ? &area[1 + (head + k) % qcap] : nullptr;
+                        const uint32_t ix = hq + k;  // k < npre <= tail - head <= qcap
+                        const LruRec *rp = want[r] ? &area[1 + (ix >= qc32 ? ix - qc32 : ix)] : nullptr;
                         rv[r] = want[r] ? ps_ldu(&rp->value) : 0ull;
                         rs[r] = want[r] ? ps_ldu(&rp->stamp) : 0ull;
                     }
@@ -3227,8 +3246,9 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                 // 4. the LRU scan: the chunk's accesses in arrival order on wave-uniform masks (bit L: leader L)
                 int32_t tdel = 0;  // wave 1: this event's thread-count change
                 uint64_t acc;
+                const ParamPre e_pre = m == 0 && hp ? param_pre(c, p, v, e_acq) : ParamPre{0, 0};
                 if (m == 0) {
-                    acc = __ballot(act && !(e_fl & 1u) && slot_ok && param_map_access(c, p, v, e_acq));
+                    acc = __ballot(act && !(e_fl & 1u) && slot_ok && param_pre_access(p, e_pre, e_acq));
                 } else {
                     tdel = slot_ok ? ((e_fl & 1u) ? -1 : ((e_fl & 4u) ? 1 : 0)) : 0;
                     acc = __ballot(act && tdel != 0);
@@ -3441,7 +3461,7 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                         if (tok && e_occ == r) {
                             struct { int64_t a, b; } e{s_ra[e_lead], s_rb[e_lead]};
                             if (rs_me) e.a = e.b = kPAbsent;
-                            if (!param_pass_qps(c, p, e, v, e_acq, e_t, &w)) {
+                            if (!param_pass_pre(p, e, e_pre, e_acq, e_t, &w)) {
                                 d = D_BLOCK_PARAM;
                                 w = 0;  // a block's detail: the rule's index
                             }
@@ -3508,6 +3528,7 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                 if (area) {
                     uint64_t h = head + used, t = tail;
                     uint32_t npm = (uint32_t)__popcll(acc);
+                    hq = ps_uni32(hq + used >= qc32 ? hq + used - qc32 : hq + used);  // used <= tail - head <= qcap
                     if (t - h + npm > qcap) {  // lru_compact over [h, t)
                         uint64_t wpos = h;
                         for (uint64_t b0 = h; b0 < t; b0 += 64) {
@@ -3527,6 +3548,7 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                             ps_wave_sync();
                         }
                         t = wpos;
+                        tq = ps_uni32(hq + (uint32_t)(t - h) >= qc32 ? hq + (uint32_t)(t - h) - qc32 : hq + (uint32_t)(t - h));
                         if (t - h + npm > qcap) {
                             if (lane == 0) {
                                 atomicOr(&st.lru_ctl[1], 2u);
@@ -3535,8 +3557,11 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                             npm = 0;
                         }
                     }
-                    if (npm && ((acc >> lane) & 1ull))
-                        area[1 + (t + (uint64_t)__popcll(acc & lt_mask)) % qcap] = LruRec{v, my_stamp};
+                    if (npm && ((acc >> lane) & 1ull)) {
+                        const uint32_t ix = tq + (uint32_t)__popcll(acc & lt_mask);  // t - h + npm <= qcap
+                        area[1 + (ix >= qc32 ? ix - qc32 : ix)] = LruRec{v, my_stamp};
+                    }
+                    tq = ps_uni32(tq + npm >= qc32 ? tq + npm - qc32 : tq + npm);
                     head = h;
                     tail = t + npm;
                 }
