@@ -3040,6 +3040,8 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
     __shared__ int64_t s_ra[64], s_rb[64];  // wave 0's rounds: each value's (a, b) at its leader's index
     __shared__ int64_t s_tc[64];            // wave 1's rounds: each value's thread count
     __shared__ uint32_t s_first[2][64];     // per leader lane: the lane of its value's first access (64: none)
+    __shared__ uint64_t s_dk[128], s_dm[128];  // wave 0's value hash: key, lane mask
+    __shared__ uint32_t s_dt[128];             // claim tags
     // chunk handoff (wave 0 -> wave 1): per event flags (bit0 exit, bit1 parameter, bit2 passed), leader,
     // rank among its value's events, request index, value
     __shared__ uint8_t s_bfl[2][64], s_blead[2][64], s_bocc[2][64];
@@ -3110,6 +3112,8 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
         const uint32_t nch = (je - jb + 63) / 64;
         uint64_t n_pop = 0, n_gpop = 0, n_evict = 0, n_acc = 0, busy = 0;  // diagnostics (SGA_LRU_PROF)
         const uint64_t t_res = prof ? wall_clock64() : 0;
+        Payload nq{0, 0, 0, 0};  // wave 0: the next chunk's events, loaded during this chunk's LRU scan
+        uint32_t nrun = 0;
         for (uint32_t step = 0; step <= nch; ++step) {
             // wave 0: chunk `step`; wave 1: chunk step - 1
             const bool work = wave == 0 ? step < nch : step >= 1;
@@ -3131,25 +3135,37 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                 int32_t e_acq = 0;
                 if (wave == 0) {
                     const uint32_t j = c0 + lane;
-                    const Payload q = act ? pay[j] : Payload{0, 0, 0, 0};
+                    const Payload q = ch == 0 ? (act ? pay[j] : Payload{0, 0, 0, 0}) : nq;
                     const bool ex = (q.idx & F_EXIT) != 0, hp = act && (q.idx & F_PARAM) != 0;
                     v = hp ? param_in[q.idx & F_IDX] : 0;
                     e_fl = (ex ? 1u : 0u) | (hp ? 2u : 0u);
                     e_idx = q.idx & F_IDX;
-                    e_run = act ? sc.ev_run[j] : 0u;
+                    e_run = ch == 0 ? (act ? sc.ev_run[j] : 0u) : nrun;
                     e_t = ts_base + (int64_t)q.ts_off;
                     e_acq = (int32_t)(q.acq_prio & 0x7FFFFFFFu);
                     // distinct values: the lowest lane of each value leads it; e_occ = the event's rank among
                     // its value's events in the chunk
-                    uint32_t lead = 64;
-                    for (int k = 0; k < 64; ++k) {
-                        const uint64_t vk = (uint64_t)__shfl((long long)v, k, 64);
-                        const bool hk2 = __shfl((int)hp, k, 64) != 0;
-                        if (hp && hk2 && vk == v) {
-                            lead = min(lead, (uint32_t)k);
-                            e_occ += (uint32_t)k < lane ? 1u : 0u;
+                    // (an LDS hash of the chunk's values: a claim per slot, then each value's lane mask)
+                    s_dt[lane] = 0;
+                    s_dt[lane + 64] = 0;
+                    s_dm[lane] = 0;
+                    s_dm[lane + 64] = 0;
+                    ps_wave_sync();
+                    uint32_t h = (uint32_t)((v * 0x9E3779B97F4A7C15ull) >> 57);
+                    bool done = !hp;
+                    while (__ballot(!done)) {
+                        if (!done && atomicCAS(&s_dt[h], 0u, lane + 1u) == 0u) s_dk[h] = v;
+                        ps_wave_sync();
+                        if (!done) {
+                            if (s_dk[h] == v) done = true;
+                            else h = (h + 1u) & 127u;
                         }
                     }
+                    if (hp) atomicOr(&s_dm[h], 1ull << lane);
+                    ps_wave_sync();
+                    const uint64_t same = hp ? s_dm[h] : 0ull;
+                    const uint32_t lead = hp ? (uint32_t)__builtin_ctzll(same) : 64u;
+                    e_occ = (uint32_t)__popcll(same & lt_mask);
                     e_lead = lead;
                     s_hasent[lane] = 0;
                     ps_wave_sync();
@@ -3241,6 +3257,11 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                             link1 = __ballot(lk);
                         }
                     }
+                }
+                if (wave == 0 && ch + 1 < nch) {  // the next chunk's events (in flight through steps 4-6)
+                    const uint32_t jn = c0 + 64 + lane;
+                    nq = jn < je ? pay[jn] : Payload{0, 0, 0, 0};
+                    nrun = jn < je ? sc.ev_run[jn] : 0u;
                 }
                 mark(3);
                 // 4. the LRU scan: the chunk's accesses in arrival order on wave-uniform masks (bit L: leader L)
