@@ -2928,7 +2928,8 @@ __global__ __launch_bounds__(64) void k_llru(FlowState st, int64_t max_rt, FlowS
 // node (as for pseg), so the node statistics go in aggregate, run by run.  k_lflows flags these flows in
 // sc.lru (kLruPs).
 // SGA_LRU_PROF=1 (diagnostics only): k_llru_ps ticks per phase of wave 0, summed over chunks: [0] events [1]
-// loads + dedupe [2] leader entries [3] queue records [4] LRU scan [5] rounds [6] write-back [7] chunks; [8..15]
+// loads + dedupe [2] leader entries [3] queue records [4] LRU scan [5] rounds [6] write-back [20] queue
+// compaction and pushes [7] chunks; [8..15]
 // queue pops per map; [16 + wave] the longest resource, [18 + wave] its busiest wave's ticks
 __device__ unsigned long long g_lps_prof[22];
 
@@ -2962,6 +2963,37 @@ __device__ __forceinline__ void ptab_find_n(PEntry *tab, uint32_t mask, uint32_t
             out[i] = &tab[ptab_home(mask, owner, v[i])];
         } else {
             out[i] = ptab_get(tab, mask, owner, v[i], false, overflow);
+        }
+    }
+}
+
+// ptab_find_n with the entry's `a` and its stamp: the home slot's words are loaded together with its owner and
+// value, so a key at its home slot costs one round trip
+template <int kN>
+__device__ __forceinline__ void ptab_peek_n(PEntry *tab, const uint64_t *tstamp, uint32_t mask, uint32_t owner,
+                                            const uint64_t (&v)[kN], const bool (&want)[kN], uint32_t (&slot)[kN],
+                                            int64_t (&a)[kN], uint64_t (&ts)[kN], uint32_t *overflow) {
+    uint32_t h[kN], ow[kN];
+    uint64_t vv[kN];
+#pragma unroll
+    for (int i = 0; i < kN; ++i) {
+        h[i] = ptab_home(mask, owner, v[i]);
+        ow[i] = want[i] ? __hip_atomic_load(&tab[h[i]].owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        vv[i] = want[i] ? tab[h[i]].value : 0ull;
+        a[i] = want[i] ? ps_ld(&tab[h[i]].a) : kPAbsent;
+        ts[i] = want[i] ? ps_ldu(&tstamp[h[i]]) : 0ull;
+    }
+#pragma unroll
+    for (int i = 0; i < kN; ++i) {
+        if (!want[i] || ow[i] == 0) {
+            slot[i] = 0xFFFFFFFFu;
+        } else if (ow[i] == owner && vv[i] == v[i]) {
+            slot[i] = h[i];
+        } else {
+            PEntry *e = ptab_get(tab, mask, owner, v[i], false, overflow);
+            slot[i] = e ? (uint32_t)(e - tab) : 0xFFFFFFFFu;
+            a[i] = e ? ps_ld(&e->a) : kPAbsent;
+            ts[i] = e ? ps_ldu(&tstamp[slot[i]]) : 0ull;
         }
     }
 }
@@ -3196,17 +3228,24 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                 uint64_t c_st = 0;
                 int64_t c_a = kPAbsent, c_b = kPAbsent;
                 const bool need = leader && (m == 1 || s_hasent[lane]);
-                if (need) {
+                if (need) {  // the home slot's words together (one round trip for a key at its home slot)
                     const uint32_t h = ptab_home(tmask, own, v);
                     const uint32_t oh = __hip_atomic_load(&tab[h].owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    PEntry *e = (oh == own && tab[h].value == v) ? &tab[h] : ptab_get(tab, tmask, own, v, true, st.overflow);
-                    if (e) {
+                    const uint64_t vh = tab[h].value;
+                    const int64_t ah = ps_ld(&tab[h].a), bh = ps_ld(&tab[h].b);
+                    const uint64_t sh = ps_ldu(&tstamp[h]);
+                    if (oh == own && vh == v) {
+                        c_slot = h;
+                        c_a = ah;
+                        c_b = bh;
+                        c_st = sh;
+                    } else if (PEntry *e = ptab_get(tab, tmask, own, v, true, st.overflow)) {
                         c_slot = (uint32_t)(e - tab);
                         c_a = ps_ld(&e->a);
                         c_b = ps_ld(&e->b);
                         c_st = ps_ldu(&tstamp[c_slot]);
-                        ps_hash_put(hk, hv, c_slot, lane);
                     }
+                    if (c_slot != 0xFFFFFFFFu) ps_hash_put(hk, hv, c_slot, lane);
                 }
                 const bool any = __ballot(need) != 0ull;  // this map is touched in the chunk
                 // the slot of this event's value (valid only for a parameter event whose entry exists)
@@ -3234,14 +3273,16 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                         rv[r] = want[r] ? ps_ldu(&rp->value) : 0ull;
                         rs[r] = want[r] ? ps_ldu(&rp->stamp) : 0ull;
                     }
-                    PEntry *e[2];
-                    ptab_find_n<2>(tab, tmask, own, rv, want, e, st.overflow);
+                    uint32_t eslot[2];
+                    int64_t ea[2];
+                    uint64_t ets[2];
+                    ptab_peek_n<2>(tab, tstamp, tmask, own, rv, want, eslot, ea, ets, st.overflow);
 #pragma unroll
                     for (int r = 0; r < 2; ++r) {
-                        const uint32_t slot = e[r] ? (uint32_t)(e[r] - tab) : 0xFFFFFFFFu;
-                        const bool gp = e[r] && ps_ld(&e[r]->a) != kPAbsent;
-                        const uint64_t gs = e[r] ? ps_ldu(&tstamp[slot]) : 0ull;
-                        const int link = e[r] ? ps_hash_get(hk, hv, slot) : -1;
+                        const uint32_t slot = eslot[r];
+                        const bool gp = slot != 0xFFFFFFFFu && ea[r] != kPAbsent;
+                        const uint64_t gs = ets[r];
+                        const int link = slot != 0xFFFFFFFFu ? ps_hash_get(hk, hv, slot) : -1;
                         const uint64_t lst = (uint64_t)__shfl((long long)c_st, link >= 0 ? link : 0, 64);
                         const bool lv = want[r] && link < 0 && gp && gs == rs[r];
                         const bool lk = want[r] && link >= 0 && lst == rs[r];
@@ -3546,26 +3587,43 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                     tab[ev_slot].b = kPAbsent;
                 }
                 ps_wave_sync();
+                mark(6);
                 if (area) {
                     uint64_t h = head + used, t = tail;
                     uint32_t npm = (uint32_t)__popcll(acc);
                     hq = ps_uni32(hq + used >= qc32 ? hq + used - qc32 : hq + used);  // used <= tail - head <= qcap
-                    if (t - h + npm > qcap) {  // lru_compact over [h, t)
+                    if (t - h + npm > qcap) {  // lru_compact over [h, t), 256 records per round (4 per lane)
+                        auto ring = [&](uint64_t x) {  // x in [h, h + qcap]: its ring slot
+                            const uint32_t r = hq + (uint32_t)(x - h);
+                            return 1u + (r >= qc32 ? r - qc32 : r);
+                        };
                         uint64_t wpos = h;
-                        for (uint64_t b0 = h; b0 < t; b0 += 64) {
-                            const uint64_t ix = b0 + (uint64_t)lane;
-                            LruRec rec{0, 0};
-                            bool live = false;
-                            if (ix < t) {
-                                const LruRec *rp = &area[1 + ix % qcap];
-                                rec = LruRec{ps_ldu(&rp->value), ps_ldu(&rp->stamp)};
-                                PEntry *e = ptab_get(tab, tmask, own, rec.value, false, st.overflow);
-                                live = e && ps_ld(&e->a) != kPAbsent && ps_ldu(&tstamp[e - tab]) == rec.stamp;
+                        for (uint64_t b0 = h; b0 < t; b0 += 256) {
+                            uint64_t rv[4], rs[4];
+                            bool want[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const uint64_t ix = b0 + (uint64_t)(u * 64) + lane;
+                                want[u] = ix < t;
+                                const LruRec *rp = want[u] ? &area[ring(ix)] : nullptr;
+                                rv[u] = want[u] ? ps_ldu(&rp->value) : 0ull;
+                                rs[u] = want[u] ? ps_ldu(&rp->stamp) : 0ull;
                             }
-                            const uint64_t bl = __ballot(live);
-                            ps_wave_sync();  // every lane has read its record before any is overwritten
-                            if (live) area[1 + (wpos + (uint64_t)__popcll(bl & lt_mask)) % qcap] = rec;
-                            wpos += (uint64_t)__popcll(bl);
+                            PEntry *e[4];
+                            ptab_find_n<4>(tab, tmask, own, rv, want, e, st.overflow);
+                            bool live[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u)
+                                live[u] = e[u] && ps_ld(&e[u]->a) != kPAbsent && ps_ldu(&tstamp[e[u] - tab]) == rs[u];
+                            uint64_t bl[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) bl[u] = __ballot(live[u]);
+                            ps_wave_sync();  // every lane has read its records before any is overwritten
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                if (live[u]) area[ring(wpos + (uint64_t)__popcll(bl[u] & lt_mask))] = LruRec{rv[u], rs[u]};
+                                wpos += (uint64_t)__popcll(bl[u]);
+                            }
                             ps_wave_sync();
                         }
                         t = wpos;
@@ -3587,7 +3645,7 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                     tail = t + npm;
                 }
                 ps_wave_sync();
-                mark(6);
+                mark(20);
                 if (prof) busy += wall_clock64() - t_step;
             }
             __syncthreads();  // wave 0's chunk handed over, wave 1's buffer free
@@ -4892,9 +4950,9 @@ void FlowEngine::lru_prepare(const uint8_t *kind, const uint32_t *resource, cons
             SGA_HIP_CHECK(hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_lps_prof), sizeof(v), 0, hipMemcpyDeviceToHost, s));
             SGA_HIP_CHECK(hipStreamSynchronize(s));
             fprintf(stderr, "lps_prof events %llu chunks %llu ticks: loads %llu leaders %llu records %llu scan %llu rounds "
-                    "%llu write-back %llu; longest resource: wave 0 %llu wave 1 %llu, busy %llu / %llu; time map: pops "
+                    "%llu write-back %llu queue %llu; longest resource: wave 0 %llu wave 1 %llu, busy %llu / %llu; time map: pops "
                     "%llu global %llu evictions %llu accesses %llu; thread map: pops %llu global %llu evictions %llu "
-                    "accesses %llu\n", v[0], v[7], v[1], v[2], v[3], v[4], v[5], v[6], v[16], v[17], v[18], v[19], v[8], v[9],
+                    "accesses %llu\n", v[0], v[7], v[1], v[2], v[3], v[4], v[5], v[6], v[20], v[16], v[17], v[18], v[19], v[8], v[9],
                     v[10], v[11], v[12], v[13], v[14], v[15]);
         }
         std::memset(v, 0, sizeof(v));
