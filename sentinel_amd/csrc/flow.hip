@@ -1867,12 +1867,30 @@ __device__ __forceinline__ int64_t ps_ld(const int64_t *p) {
 __device__ __forceinline__ uint64_t ps_ldu(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ bool lru_ps_take(const FlowState &st, uint32_t res) {
+// k_llru_ps's resources (called on the flow's lane in k_lflows): as pseg_take, the flow's first entry resolves
+// the rule's index (ParamFlowSlot.applyRealParamIdx) and creates the index-0 thread-count map when it does not
+// exist yet (the first batch of a fresh engine); a parameter exit before that entry stays with k_llru
+__device__ bool lru_ps_take(const FlowState &st, const FlowScratch &sc, const Payload *__restrict__ pay, uint32_t res,
+                            uint32_t r0, uint32_t r1) {
     const ResDev R = st.res[res];
-    if (R.n_rules || R.n_cbs || R.n_prules != 1 || !st.tmapmask || st.tmapmask[res] != 1ull) return false;
-    const ParamRuleDev &p = st.prules[R.prule_off];
-    return p.grade == 1 && !p.cluster && p.idx_res == 0 && st.pstamp && st.tstamp && st.tbase &&
-           st.tbase[res] != kNoTBase;
+    if (R.n_rules || R.n_cbs || R.n_prules != 1 || !st.tmapmask || (st.tmapmask[res] & ~1ull)) return false;
+    ParamRuleDev &p = st.prules[R.prule_off];
+    if (!(p.grade == 1 && !p.cluster && st.pstamp && st.tstamp && st.tbase && st.tbase[res] != kNoTBase))
+        return false;
+    const bool has_map = (st.tmapmask[res] & 1ull) != 0;
+    if (p.idx_res == 0 && has_map) return true;
+    if (p.idx_res != 0 && p.idx_res != kIdxUnresolved) return false;
+    const uint32_t je = sc.run_end[r1 - 1];
+    uint32_t j = sc.run_start[r0];
+    for (; j < je; ++j) {
+        const uint32_t f = pay[j].idx;
+        if (!(f & F_EXIT)) break;
+        if ((f & F_PARAM) && !has_map) return false;  // a parameter exit before the map exists
+    }
+    if (j == je) return p.idx_res == 0 && has_map;  // exits only
+    if (param_idx_of(p, (pay[j].idx & F_PARAM) ? 1u : 0u) != 0) return false;
+    st.tmapmask[res] = 1ull;  // the first entry creates the map
+    return true;
 }
 
 __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, FlowScratch sc,
@@ -1891,7 +1909,7 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
             const uint32_t nev = sc.run_end[r1 - 1] - sc.run_start[r0];
             if (st.lru_res && st.lru_res[res]) {  // a CacheMap in LRU mode: arrival order, one lane (k_llru)
                 // parameter-only: the chunked replay (k_llru_ps, SGA_LRU_PS=0 turns it off: an A/B knob)
-                const bool ps = st.lru_ps && lru_ps_take(st, res);
+                const bool ps = st.lru_ps && lru_ps_take(st, sc, pay, res, r0, r1);
                 sc.lru[atomicAdd(&sc.counters[10], 1u)] = fl | (ps ? 0x80000000u : 0u);
                 continue;
             }
