@@ -3610,35 +3610,38 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
                     uint64_t h = head + used, t = tail;
                     uint32_t npm = (uint32_t)__popcll(acc);
                     hq = ps_uni32(hq + used >= qc32 ? hq + used - qc32 : hq + used);  // used <= tail - head <= qcap
-                    if (t - h + npm > qcap) {  // lru_compact over [h, t), 256 records per round (4 per lane)
+                    if (t - h + npm > qcap) {  // lru_compact over [h, t), 512 records per round (8 per lane)
+                        constexpr int kC = 8;
                         auto ring = [&](uint64_t x) {  // x in [h, h + qcap]: its ring slot
                             const uint32_t r = hq + (uint32_t)(x - h);
                             return 1u + (r >= qc32 ? r - qc32 : r);
                         };
                         uint64_t wpos = h;
-                        for (uint64_t b0 = h; b0 < t; b0 += 256) {
-                            uint64_t rv[4], rs[4];
-                            bool want[4];
+                        for (uint64_t b0 = h; b0 < t; b0 += 64 * kC) {
+                            uint64_t rv[kC], rs[kC];
+                            bool want[kC];
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) {
+                            for (int u = 0; u < kC; ++u) {
                                 const uint64_t ix = b0 + (uint64_t)(u * 64) + lane;
                                 want[u] = ix < t;
                                 const LruRec *rp = want[u] ? &area[ring(ix)] : nullptr;
                                 rv[u] = want[u] ? ps_ldu(&rp->value) : 0ull;
                                 rs[u] = want[u] ? ps_ldu(&rp->stamp) : 0ull;
                             }
-                            PEntry *e[4];
-                            ptab_find_n<4>(tab, tmask, own, rv, want, e, st.overflow);
-                            bool live[4];
+                            uint32_t eslot[kC];
+                            int64_t ea[kC];
+                            uint64_t ets[kC];
+                            ptab_peek_n<kC>(tab, tstamp, tmask, own, rv, want, eslot, ea, ets, st.overflow);
+                            bool live[kC];
+                            uint64_t bl[kC];
 #pragma unroll
-                            for (int u = 0; u < 4; ++u)
-                                live[u] = e[u] && ps_ld(&e[u]->a) != kPAbsent && ps_ldu(&tstamp[e[u] - tab]) == rs[u];
-                            uint64_t bl[4];
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) bl[u] = __ballot(live[u]);
+                            for (int u = 0; u < kC; ++u) {
+                                live[u] = eslot[u] != 0xFFFFFFFFu && ea[u] != kPAbsent && ets[u] == rs[u];
+                                bl[u] = __ballot(live[u]);
+                            }
                             ps_wave_sync();  // every lane has read its records before any is overwritten
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) {
+                            for (int u = 0; u < kC; ++u) {
                                 if (live[u]) area[ring(wpos + (uint64_t)__popcll(bl[u] & lt_mask))] = LruRec{rv[u], rs[u]};
                                 wpos += (uint64_t)__popcll(bl[u]);
                             }
