@@ -34,12 +34,6 @@ E2E_BATCHES = 6                   # host-buffer batches after the timed loop (PC
                                   # through pageable buffers, then the same through registered ones
 
 
-class SgawParams(C.Structure):
-    _fields_ = [("seed", C.c_uint64), ("t0", C.c_int64), ("lambda_", C.c_int64), ("n_rules", C.c_int64),
-                ("zipf_s", C.c_double), ("prio_pct", C.c_int32), ("n_shards", C.c_int32), ("shard", C.c_int32),
-                ("reserved", C.c_int32)]
-
-
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -50,6 +44,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 25, help="oracle replay sample (requests)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) batches")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the first two timed batches")
     ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c4full", "c5a", "c5b"],
                     help="BASELINE.json configuration (SURVEY.md 8(d)); c3 = the headline, the others run on one "
                          "GPU through bench_local.py")
@@ -121,15 +116,7 @@ def main():
     torch.cuda.set_device(local)
 
     from sentinel_amd import _lib, cluster
-    from sentinel_amd.workload import MASTER_SEED, T0, ClusterTrace, permutation, shard_of
-
-    wl = C.CDLL(os.path.join(ROOT, "sentinel_amd", "libsga_workload.so"))
-    wl.sgaw_gen_cluster.restype = C.c_int
-    wl.sgaw_gen_cluster.argtypes = [C.POINTER(SgawParams), C.c_uint64, C.c_uint32, C.c_void_p, C.c_int64,
-                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                    C.c_void_p]
-    wl.sgaw_flow_histogram.restype = C.c_int
-    wl.sgaw_flow_histogram.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64, C.c_void_p]
+    from sentinel_amd.workload import ClusterTrace, DeviceClusterGen, pack_requests, shard_of
 
     lam = LAMBDA_PER_GPU * n_gpus
     glob_batch = args.batch * n_gpus
@@ -139,49 +126,33 @@ def main():
     tr = ClusterTrace(n_rules=args.rules, lam=lam)
     fid_all, cnt_all = tr.rules()
     mine = shard_of(fid_all, n_gpus) == rank
-    perm = torch.from_numpy(permutation(args.rules)).to(dev)
 
     # ---- pre-generate warmup+steps batches in HBM (untimed), plus the end-to-end batches that follow
-    # the timed ones in virtual time (host buffers through sga_request_tokens, after the timed loop)
+    # the timed ones in virtual time (host buffers through sga_request_tokens, after the timed loop).
+    # The timed entry takes the packed 12-byte records (sga_token_request, SURVEY.md 8(d) E_in);
+    # SGA_BENCH_UNPACKED=1 times the four-array entry instead (A/B).
+    unpacked = os.environ.get("SGA_BENCH_UNPACKED", "0") == "1"
     n_e2e = 0 if args.no_e2e else E2E_BATCHES
     nb = args.warmup + args.steps
     nb_all = nb + n_e2e
-    params = SgawParams(MASTER_SEED, T0, lam, args.rules, 1.1, 1, n_gpus, rank, 0)
-    tmp = torch.empty(4 * glob_batch + 4096, dtype=torch.int32, device=dev)
-    cnt_dev = torch.zeros(1, dtype=torch.int32, device=dev)
-    hist = torch.zeros(args.rules + 1, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    batches = []
+    gen = DeviceClusterGen(dev, n_rules=args.rules, lam=lam, n_shards=n_gpus, shard=rank)
+    batches, packed = [], []
     touched = []
     max_n = 0
     for b in range(nb_all):
-        start = b * glob_batch
-        ts_base = T0 + (start * 1000) // lam
-        cap = glob_batch  # worst case: every request of the global batch is ours
-        f = torch.empty(cap, dtype=torch.int64, device=dev)
-        a = torch.empty(cap, dtype=torch.int32, device=dev)
-        p = torch.empty(cap, dtype=torch.uint8, device=dev)
-        t = torch.empty(cap, dtype=torch.int32, device=dev)
-        rc = wl.sgaw_gen_cluster(C.byref(params), start, glob_batch, perm.data_ptr(), ts_base, f.data_ptr(),
-                                 a.data_ptr(), p.data_ptr(), t.data_ptr(), cnt_dev.data_ptr(), tmp.data_ptr(),
-                                 C.c_void_p(stream.cuda_stream))
-        assert rc == 0, rc
-        torch.cuda.synchronize(dev)
-        n = int(cnt_dev.item())
-        wl.sgaw_flow_histogram(f.data_ptr(), n, hist.data_ptr(), args.rules, C.c_void_p(stream.cuda_stream))
-        torch.cuda.synchronize(dev)
-        touched.append(int((hist > 0).sum().item()))
-        # shrink to the kept events
-        batches.append((f[:n].clone(), a[:n].clone(), p[:n].clone(), t[:n].clone(), ts_base, n))
-        del f, a, p, t
+        f, a, p, t, ts_base, n, nt = gen.batch(b * glob_batch, glob_batch, touched=True)
+        touched.append(nt)
+        batches.append((f, a, p, t, ts_base, n))
+        packed.append(pack_requests(f, a, p, t) if b < nb and not unpacked else None)
         max_n = max(max_n, n)
-    del tmp
+    gen.tmp = None
 
     eng = cluster.Engine(device=local, max_batch=max_n + 1024, max_rules=max(1 << 16, int(mine.sum()) + 1))
     cluster.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_all[mine], cnt_all[mine])
     L = _lib.load()
     estream = L.sga_engine_stream(eng.handle)
-    outs = [torch.empty(max_n + 1024, dtype=torch.int64, device=dev) for _ in range(2)]
+    # every batch its own result buffer (the first two timed batches are checked against the oracle afterwards)
+    outs = [torch.empty(max(batches[b][5], 1), dtype=torch.int64, device=dev) for b in range(nb)]
 
     # HIP events on the engine stream: around the whole timed region and around every batch
     hip = C.CDLL("libamdhip64.so.7")
@@ -255,11 +226,14 @@ def main():
 
     def step(b, k=None):
         f, a, p, t, ts_base, n = batches[b]
-        o = outs[b & 1]
+        o = outs[b]
         if k is not None:
             hip.hipEventRecord(bev[k][0], estream)
-        rc = entry(eng.handle, f.data_ptr(), a.data_ptr(), p.data_ptr(), ts_base, t.data_ptr(), n, o.data_ptr(),
-                   in_stream if pipe else None)
+        if packed[b] is not None and not pipe:
+            rc = L.sga_request_tokens_packed_device(eng.handle, packed[b].data_ptr(), ts_base, n, o.data_ptr(), None)
+        else:
+            rc = entry(eng.handle, f.data_ptr(), a.data_ptr(), p.data_ptr(), ts_base, t.data_ptr(), n, o.data_ptr(),
+                       in_stream if pipe else None)
         if rc != 0:
             raise RuntimeError(f"sga_request_tokens_device rc={rc}: {L.sga_last_error(eng.handle)}")
         if k is not None:
@@ -325,9 +299,15 @@ def main():
     path = eng.batch_info()  # which path the last timed batch took (hot path or plain sort)
 
     # correctness spot-check of the last batch's statuses (cheap invariants)
-    res = outs[(nb - 1) & 1][: batches[nb - 1][5]].cpu().numpy().view(np.uint64)
+    res = outs[nb - 1][: batches[nb - 1][5]].cpu().numpy().view(np.uint64)
     status = ((res >> np.uint64(48)) & np.uint64(0xFF)).astype(np.int8)
     frac_ok = float((status == 0).mean())
+
+    # the headline checks itself: the first two timed batches against the oracle (every request, the
+    # sharded replay of this rank's trace from batch 0), rank 0
+    parity = None
+    if rank == 0 and not args.no_parity and args.steps >= 1:
+        parity = check_parity(batches, outs, args.warmup, min(2, args.steps), fid_all[mine], cnt_all[mine])
 
     cpu_baseline, router = None, None
     if rank == 0 and not args.no_cpu:
@@ -392,12 +372,47 @@ def main():
             "host_router": router,
             "end_to_end_host_buffers": e2e,
             "ok_fraction_last_batch": frac_ok,
+            "parity_sample": parity,
+            "entry": "sga_request_tokens_device (four arrays)" if (unpacked or pipe) else
+                     "sga_request_tokens_packed_device (12-B sga_token_request records)",
             "last_batch_path": path,
         }
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def check_parity(batches, outs, first, count, rule_fid, rule_cnt):
+    """Oracle (oracle/sentinel_oracle.c, ClusterFlowChecker restatement) replay of this rank's trace from
+    batch 0 through the timed batches [first, first + count), sharded by flowId over 16 host threads; the
+    timed batches' TokenResults (status, remaining, waitInMs) compared request by request."""
+    import time as _t
+    try:
+        from tests import oracle_harness as H
+    except Exception as e:  # pragma: no cover
+        return {"error": str(e)}
+    t0 = _t.perf_counter()
+    host = []
+    for b in range(first + count):
+        f, a, p, t, ts_base, n = batches[b]
+        host.append((f.cpu().numpy(), a.cpu().numpy(), p.cpu().numpy(), t.cpu().numpy().astype(np.int64) + ts_base))
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    orc = H.cluster_replay_sharded(rule_fid, rule_cnt, host, threads=threads)
+    mism, total = 0, 0
+    for b in range(first, first + count):
+        r = outs[b][: batches[b][5]].cpu().numpy().view(np.uint64)
+        st = ((r >> np.uint64(48)) & np.uint64(0xFF)).astype(np.int8).astype(np.int32)
+        rem = (r & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
+        wait = ((r >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.uint16).view(np.int16).astype(np.int32)
+        o = orc[b]
+        mism += int(((st != o[0]) | (rem != o[1]) | (wait != o[2])).sum())
+        total += len(st)
+    return {"timed_batches": list(range(first, first + count)), "requests": total, "mismatches": mism,
+            "seconds": _t.perf_counter() - t0,
+            "what": "every TokenResult (status, remaining, waitInMs) of these timed batches vs the oracle replaying "
+                    "this rank's trace from batch 0 (tests/oracle_harness.py cluster_replay_sharded, %d threads)"
+                    % threads}
 
 
 def run_e2e(L, eng, bats, dev):

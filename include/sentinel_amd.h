@@ -187,6 +187,27 @@ int sga_request_tokens_device(sga_engine *e, const int64_t *d_flow_id, const int
                               const uint8_t *d_prioritized, int64_t ts_base, const uint32_t *d_ts_off, size_t n,
                               sga_token_result *d_out, void *hip_stream);
 
+/* One token request in the packed 12-byte form (SURVEY.md 8(d) E_in: flowId u32, ts offset u32,
+ * acquireCount u16, flags u16): what a front end that decodes Netty frames (FlowRequestData:
+ * flowId, count, priority -- CS/server/codec/data/FlowRequestDataDecoder.java:35-48) into a device
+ * batch writes, for engines whose flowIds fit 32 bits.  flow_id = 0 and acquire = 0 answer
+ * BAD_REQUEST as flowId <= 0 / acquireCount <= 0 do (DefaultTokenService.notValidRequest, :87-89);
+ * flags bit 0 = prioritized, the other bits must be 0. */
+typedef struct sga_token_request {
+    uint32_t flow_id;
+    uint32_t ts_off;   /* time = ts_base + ts_off (ms) */
+    uint16_t acquire;
+    uint16_t flags;
+} sga_token_request;
+#define SGA_REQ_PRIORITIZED 1u
+
+/* sga_request_tokens_device over packed requests (12 B each, 4-byte aligned): same decisions as the
+ * unpacked entry on the same requests (DefaultTokenService.requestToken in arrival order,
+ * CS/flow/DefaultTokenService.java:39-50); the hot path reads the records directly, every other path
+ * unpacks them on the device first. */
+int sga_request_tokens_packed_device(sga_engine *e, const sga_token_request *d_req, int64_t ts_base, size_t n,
+                                     sga_token_result *d_out, void *hip_stream);
+
 /* Round-1 name of sga_request_tokens_device (kept for its callers): the device entry already
  * returns once the batch is queued on the engine stream, and batches run in submission order. */
 int sga_request_tokens_device_async(sga_engine *e, const int64_t *d_flow_id, const int32_t *d_acquire,

@@ -125,6 +125,8 @@ SIGNATURES = {
                                      C.c_void_p]),
     "sga_request_tokens_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
                                             C.c_size_t, C.c_void_p, C.c_void_p]),
+    "sga_request_tokens_packed_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_size_t, C.c_void_p,
+                                                   C.c_void_p]),
     "sga_request_tokens_device_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
                                             C.c_size_t, C.c_void_p, C.c_void_p]),
     "sga_request_tokens_device_pipelined": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,

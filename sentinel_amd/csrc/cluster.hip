@@ -1082,9 +1082,7 @@ template <int kMode>
 __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_cold_fused_t(ClusterState st, BatchScratch sc,
                                                              const uint64_t *__restrict__ el_in, uint32_t nhost,
                                                              const uint32_t *__restrict__ dn, uint32_t nkey,
-                                                             const int32_t *__restrict__ acquire,
-                                                             const uint8_t *__restrict__ prio,
-                                                             const uint32_t *__restrict__ ts_off, int64_t ts_base,
+                                                             const ReqIn in, int64_t ts_base,
                                                              int simple, uint32_t hot_min, uint64_t *__restrict__ out,
                                                              int dbg, uint64_t *__restrict__ es, int lb) {
     // Chunk mode keeps u32 run records for kFzChunk head positions; bin mode, sized for three workgroups
@@ -1377,9 +1375,9 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
         if (!fast) {
             for (uint32_t j = r; j < r + ri.n; ++j) {
                 const uint32_t i = el_idx(el[j]);
-                const int64_t t = ts_base + (int64_t)ts_off[i];
-                const bool p = !simple && prio && prio[i];
-                out[i] = request_exact(st, s, t, acquire[i], p, simple);
+                const int64_t t = ts_base + (int64_t)in.ts_at(i);
+                const bool p = !simple && in.prio_at(i);
+                out[i] = request_exact(st, s, t, in.acq_at(i), p, simple);
             }
             ro.mode = RUN_DONE;
             rc.have = false;  // the record changed in memory
@@ -1665,9 +1663,8 @@ __device__ __forceinline__ uint32_t bucket_delta(uint32_t t, uint32_t W, uint32_
 // Per batch: r0 and 1/W of every window-length code (the dense flowId table's wcode), and the
 // precheck: no hot rule's window may hold a bucket newer than the batch's first request (batches
 // submitted out of time order), as the closed form needs each run's bucket to be the newest.
-__global__ __launch_bounds__(kThreads) void k_hot_precheck(ClusterState st, BatchScratch sc,
-                                                           const uint32_t *__restrict__ ts_off, int64_t ts_base,
-                                                           uint32_t n, int pipelined) {
+__global__ __launch_bounds__(kThreads) void k_hot_precheck(ClusterState st, BatchScratch sc, const ReqIn in,
+                                                           int64_t ts_base, uint32_t n, int pipelined) {
     if (blockIdx.x == 0 && st.dense_n) {
         const uint32_t W = st.wtab[threadIdx.x];
         WConst wc;
@@ -1683,7 +1680,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_precheck(ClusterState st, Batc
     }
     if (h >= hot_count(sc) || n == 0) return;
     const int64_t W = (int64_t)sc.hot_ctl[2];
-    const int64_t t0 = ts_base + (int64_t)ts_off[0];
+    const int64_t t0 = ts_base + (int64_t)in.ts_at(0);
     // Pipelined batches: the window starts read here may still be written by the earlier batch being
     // decided.  That batch writes buckets at its own times only, so the answer is the same either way
     // when this batch starts no earlier than every earlier batch's latest time; otherwise no hot path.
@@ -1732,12 +1729,16 @@ struct KeyShared {
         uint32_t phist[kPartBins];   // partition mode: the segment's cold elements per slot bin
     };
 };
-template <int kPass, bool kDense, bool kNT = false>
-__device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, const BatchScratch &sc,
-                                        const int64_t *__restrict__ flow_id, const int32_t *__restrict__ acquire,
-                                        const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off,
+// kPk: the requests are packed sga_token_request records (in.pk), else the four arrays of in.
+template <int kPass, bool kDense, bool kNT = false, bool kPk = false>
+__device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, const BatchScratch &sc, const ReqIn in,
                                         int64_t ts_base, uint32_t n, uint64_t *__restrict__ out, int dbg,
                                         int d0, uint32_t *__restrict__ hist, uint32_t ntiles) {
+    const int64_t *__restrict__ flow_id = in.flow;
+    const int32_t *__restrict__ acquire = in.acq;
+    const uint8_t *__restrict__ prio = in.prio;
+    const uint32_t *__restrict__ ts_off = in.ts;
+    const uint32_t *__restrict__ pk = in.pk;
     // d0 > 0: the LSD sort's first digit (d0 bits) counted per sort tile; d0 < 0: partition mode, the
     // cold elements counted per slot bin (slot >> -d0) into the segment's row of hist ([seg][kPartBins])
     WConst *wcs = sh.wcs;
@@ -1747,8 +1748,11 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
     auto &cnt = sh.cnt;
     uint32_t *s_np = sh.s_np, *s_bd = sh.s_bd;
     const uint32_t flags0 = sc.counters[CTL_FLAGS];
-    if (kPass == 1 && !(flags0 & kFlagRerun)) return;
-    const uint32_t nhot = (kPass == 0 && !(flags0 & kFlagState)) ? hot_count(sc) : 0u;
+    // pass 0 decides nothing when the precheck refused the hot path; pass 1 (re-classifying every request as
+    // cold) runs after a refusal or a fallback flag of pass 0
+    if (kPass == 0 && (flags0 & kFlagState)) return;
+    if (kPass == 1 && !(flags0 & (kFlagRerun | kFlagState))) return;
+    const uint32_t nhot = kPass == 0 ? hot_count(sc) : 0u;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lt = lanemask_lt64(lane);
     if (kDense)
@@ -1767,6 +1771,11 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
     const uint32_t Wh = nhot ? sc.hot_ctl[2] : 1u;
     const uint32_t r0h = (uint32_t)(ts_base % (int64_t)Wh);
     const double invh = 1.0 / (double)Wh;
+    // a key-table entry may name a hot rule while this pass decides every request as cold (no hot path for
+    // the batch, or the re-classifying pass): its slot from the hot set, its window length the hot rules' one
+    const uint32_t Wc = (kDense && sc.hot_ctl[0]) ? sc.hot_ctl[2] : 1u;
+    const uint32_t r0c = (uint32_t)(ts_base % (int64_t)Wc);
+    const double invc = 1.0 / (double)Wc;
     uint32_t wflags = 0, nc = 0, np = 0, bdmax = 0, tmax_l = 0;
     const uint32_t send = min(n, ubase + (uint32_t)kSubSeg);
     // the sub's request codes stay in registers through the rank and fix-up passes (written once)
@@ -1774,25 +1783,41 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
 #pragma unroll
     for (int r = 0; r < kSubRounds; ++r) hc[r] = kNoCode;
     if (active) {
-        uint32_t ptso = ubase > 0 ? ts_off[ubase - 1] : 0u;  // time order across the sub start
+        uint32_t ptso = ubase > 0 ? (kPk ? pk[3 * (size_t)(ubase - 1) + 1] : ts_off[ubase - 1]) : 0u;  // time order across the sub start
         // hot bucket of the previous request (bucket boundaries)
         uint32_t pbd = (nhot && ubase > 0) ? min(bucket_delta(ptso, Wh, r0h, invh), (uint32_t)kHotBuckets - 1) : 0u;
-        const bool use_prio = prio != nullptr;
+        const bool use_prio = kPk || prio != nullptr;
         constexpr int nchunks = kSubRounds / kH1Chunk;  // a short last sub runs masked rounds
         struct Buf {
             int64_t f[kH1Chunk];
             int32_t a[kH1Chunk];
-            uint32_t t[kH1Chunk], p[kH1Chunk], d[kH1Chunk], hf[kH1Chunk], m[kH1Chunk];
+            uint32_t t[kH1Chunk], p[kH1Chunk], d[kH1Chunk], m[kH1Chunk];
             HashEntry e[kH1Chunk];
         };
         Buf B0, B1, B2;
         // a missing prio array reads the acquire bytes instead, masked off when processed
-        const uint8_t *pr_src = use_prio ? prio : reinterpret_cast<const uint8_t *>(acquire);
+        const uint8_t *pr_src = kPk ? nullptr : (use_prio ? prio : reinterpret_cast<const uint8_t *>(acquire));
         auto load = [&](int ch, Buf &B) {
 #pragma unroll
             for (int u = 0; u < kH1Chunk; ++u) {
                 const uint32_t i = min(ubase + (uint32_t)(ch * kH1Chunk + u) * 64 + lane, n - 1);
-                if (kNT) {  // streamed once: non-temporal, so the dense table keeps more of L2
+                if (kPk) {  // one 12-byte record: flowId, time offset, acquireCount | flags << 16
+                    const uint32_t *r = pk + 3 * (size_t)i;
+                    uint32_t w0, w1, w2;
+                    if (kNT) {
+                        w0 = __builtin_nontemporal_load(r);
+                        w1 = __builtin_nontemporal_load(r + 1);
+                        w2 = __builtin_nontemporal_load(r + 2);
+                    } else {
+                        w0 = r[0];
+                        w1 = r[1];
+                        w2 = r[2];
+                    }
+                    B.f[u] = (int64_t)w0;
+                    B.t[u] = w1;
+                    B.a[u] = (int32_t)(w2 & 0xFFFFu);
+                    B.p[u] = (w2 >> 16) & 1u;
+                } else if (kNT) {  // streamed once: non-temporal, so the dense table keeps more of L2
                     B.f[u] = __builtin_nontemporal_load(&flow_id[i]);
                     B.a[u] = __builtin_nontemporal_load(&acquire[i]);
                     B.t[u] = __builtin_nontemporal_load(&ts_off[i]);
@@ -1815,16 +1840,13 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                 B.m[u] = ((use_prio && B.p[u]) ? 1u : 0u) | ((f <= 0 || a <= 0) ? 2u : 0u) |
                          ((uint64_t)(f - 1) < (uint64_t)st.dense_n ? 4u : 0u) | (a == 1 ? 8u : 0u) |
                          ((a >= 1 && a <= (int32_t)kAcqMax ? (uint32_t)a : 0u) << 8);
-                if (kDense) {
+                if (kDense) {  // the hot path's key table: slot | wcode << 24, or kDkHot | hot id
                     const uint64_t k = (uint64_t)(B.f[u] - 1);
                     const uint32_t kk = k < (uint64_t)st.dense_n ? (uint32_t)k : 0u;
-                    const uint64_t ev = st.dense[kk];
-                    B.d[u] = (uint32_t)ev;
-                    B.hf[u] = (uint32_t)(ev >> 32) & 0xFFFFu;
+                    B.d[u] = st.dkey[kk];
                 } else {
                     B.d[u] = (uint32_t)hash_flow_id(B.f[u]) & st.hmask;
                     B.e[u] = st.htab[B.d[u]];
-                    B.hf[u] = kColdId;
                 }
             }
         };
@@ -1835,13 +1857,9 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                 const uint32_t i = rbase + lane;
                 const bool valid = i < send;
                 if (valid) tmax_l = max(tmax_l, B.t[u]);
-                uint32_t d = B.d[u], hfv = B.hf[u];
+                uint32_t d = B.d[u];
                 const uint32_t m = B.m[u];
-                if (kDense) {
-                    const bool in = m & 4u;
-                    if (!in) d = ~0u;
-                    if (!in || !nhot) hfv = kColdId;
-                }
+                if (kDense && !(m & 4u)) d = kDkNone;
                 const uint32_t p = m & 1u;
                 uint32_t kind = 0, hid = kColdId, slot = 0, bd6 = 0, a7 = 0;
                 // hot bucket (window length of the hot rules) of every request: time order of the
@@ -1854,8 +1872,15 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                     if (m & 2u) {
                         status = TRS_BAD_REQUEST;
                     } else if (kDense) {
-                        if (d == ~0u) {
+                        if (d == kDkNone) {
                             status = TRS_NO_RULE_EXISTS;
+                        } else if (d & kDkHot) {  // a hot rule: its window length is the hot rules' one
+                            hid = d & 0xFFFu;
+                            W = Wc;
+                            r0 = r0c;
+                            inv = invc;
+                            if (kPass == 1) slot = sc.hot_slot[hid];  // decided as cold in this pass
+                            else if (hid >= nhot) wflags |= kFlagHotKey;
                         } else {
                             slot = d & 0xFFFFFFu;
                             const WConst wc = wcs[d >> 24];
@@ -1896,7 +1921,7 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                         }
                         kind = 1;
                         if (nhot) {
-                            hid = kDense ? hfv : sc.hot_of[slot];
+                            if (!kDense) hid = sc.hot_of[slot];
                             if (hid < nhot) {
                                 kind = 2;
                                 if (!(m & 8u)) wflags |= kFlagMixed;
@@ -2192,23 +2217,21 @@ __global__ __launch_bounds__(kKeyThreads) void k_part_scatter(BatchScratch sc, u
     }
 }
 
-// Dense flowId table (the production layout): 4 waves per SIMD, two workgroups per CU.
-template <int kPass, bool kNT = false>
+// Dense flowId table (the production layout): 4 waves per SIMD, two workgroups per CU.  kPk: packed requests.
+template <int kPass, bool kNT = false, bool kPk = false>
 __global__ __launch_bounds__(kKeyThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_hot_key_dense(
-    ClusterState st, BatchScratch sc, const int64_t *__restrict__ flow_id, const int32_t *__restrict__ acquire,
-    const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off, int64_t ts_base, uint32_t n,
-    uint64_t *__restrict__ out, int dbg, int d0, uint32_t *__restrict__ hist, uint32_t ntiles) {
+    ClusterState st, BatchScratch sc, ReqIn in, int64_t ts_base, uint32_t n, uint64_t *__restrict__ out, int dbg,
+    int d0, uint32_t *__restrict__ hist, uint32_t ntiles) {
     __shared__ KeyShared sh;
-    hot_key<kPass, true, kNT>(sh, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out, dbg, d0, hist, ntiles);
+    hot_key<kPass, true, kNT, kPk>(sh, st, sc, in, ts_base, n, out, dbg, d0, hist, ntiles);
 }
 // Hashed flowId table (sparse flowIds): the probe loop needs more registers.
-template <int kPass>
+template <int kPass, bool kPk = false>
 __global__ __launch_bounds__(kKeyThreads) void k_hot_key_hash(
-    ClusterState st, BatchScratch sc, const int64_t *__restrict__ flow_id, const int32_t *__restrict__ acquire,
-    const uint8_t *__restrict__ prio, const uint32_t *__restrict__ ts_off, int64_t ts_base, uint32_t n,
-    uint64_t *__restrict__ out, int dbg, int d0, uint32_t *__restrict__ hist, uint32_t ntiles) {
+    ClusterState st, BatchScratch sc, ReqIn in, int64_t ts_base, uint32_t n, uint64_t *__restrict__ out, int dbg,
+    int d0, uint32_t *__restrict__ hist, uint32_t ntiles) {
     __shared__ KeyShared sh;
-    hot_key<kPass, false>(sh, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out, dbg, d0, hist, ntiles);
+    hot_key<kPass, false, false, kPk>(sh, st, sc, in, ts_base, n, out, dbg, d0, hist, ntiles);
 }
 
 // The batch's path and element counts: sums over the compaction segments and the rank segments
@@ -2780,10 +2803,11 @@ __global__ __launch_bounds__(kThreads) void k_hot_hist(ClusterState st, BatchScr
     if (threadIdx.x == 0 && best) atomicMax(reinterpret_cast<unsigned long long *>(sc.hot_ctl + 4), best);
 }
 
+// the key table entry of a rule entering (v = hot id) or leaving (kColdId) the hot set
 __device__ __forceinline__ void hot_fid_set(const ClusterState &st, uint32_t slot, uint16_t v) {
-    if (!st.dense_n || !st.dense_hot) return;
+    if (!st.dense_n || !st.dkey) return;
     const int64_t f = st.slot_fid[slot];
-    if (f >= 1 && f <= (int64_t)st.dense_n) st.dense_hot[4 * (f - 1) + 2] = v;  // bits 32..47 of the entry
+    if (f >= 1 && f <= (int64_t)st.dense_n) st.dkey[f - 1] = v == kColdId ? st.dense[f - 1] : (kDkHot | v);
 }
 
 __global__ __launch_bounds__(kThreads) void k_hot_clear(ClusterState st, BatchScratch sc) {
@@ -2902,9 +2926,9 @@ __global__ __launch_bounds__(kFinThreads) void k_hot_fin(ClusterState st, BatchS
 __global__ void k_hot_reset(ClusterState st, BatchScratch sc, uint32_t nslots_cap) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nslots_cap; i += gridDim.x * blockDim.x)
         sc.hot_of[i] = kColdId;
-    if (st.dense_hot)
+    if (st.dkey)
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < st.dense_n; i += gridDim.x * blockDim.x)
-            st.dense_hot[4 * (size_t)i + 2] = kColdId;
+            st.dkey[i] = st.dense[i] == ~0u ? kDkNone : st.dense[i];
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)kHot; i += gridDim.x * blockDim.x)
         sc.hot_next[i] = kNoSlot;
     if (blockIdx.x == 0 && threadIdx.x < kHotCtlWords) sc.hot_ctl[threadIdx.x] = 0;
@@ -3674,17 +3698,16 @@ void batch_scratch_release(BatchScratch &sc) {
 // Partitioned (sc.part_lb > 0, hot path): one workgroup per slot bin, el = the partition output, each bin
 // ordered into the other element buffer first.
 static void cold_stage(const ClusterState &st, BatchScratch &sc, const uint64_t *el, uint32_t n, const uint32_t *dn,
-                       uint32_t invalid_key, const int32_t *acquire, const uint8_t *prio, const uint32_t *ts_off,
-                       int64_t ts_base, int simple, uint32_t hot_min, uint64_t *out, hipStream_t s) {
+                       uint32_t invalid_key, const ReqIn &in, int64_t ts_base, int simple, uint32_t hot_min,
+                       uint64_t *out, hipStream_t s) {
     if (sc.part_lb) {
         uint64_t *es = el == sc.el[0] ? sc.el[1] : sc.el[0];
         hipLaunchKernelGGL(k_cold_fused_t<kFzBin>, dim3(kPartBins), dim3(kFzThreads), 0, s, st, sc, el, n, dn,
-                           invalid_key, acquire, prio, ts_off, ts_base, simple, hot_min, out, fz_debug(), es,
-                           sc.part_lb);
+                           invalid_key, in, ts_base, simple, hot_min, out, fz_debug(), es, sc.part_lb);
         return;
     }
     hipLaunchKernelGGL(k_cold_fused, dim3((n + kFzChunk - 1) / kFzChunk), dim3(kFzThreads), 0, s, st, sc, el, n, dn,
-                       invalid_key, acquire, prio, ts_off, ts_base, simple, hot_min, out, fz_debug(), nullptr, 0);
+                       invalid_key, in, ts_base, simple, hot_min, out, fz_debug(), nullptr, 0);
 }
 
 static size_t hot_rows(size_t cap) { return (cap + kHotSeg - 1) / kHotSeg; }
@@ -3868,7 +3891,7 @@ bool lds_lane_order_ok(hipStream_t s) {
 }
 
 void hot_reset(const ClusterState &st, BatchScratch &sc, uint32_t nslots_cap, hipStream_t s) {
-    const uint32_t m = std::max(nslots_cap, st.dense_hot ? st.dense_n : 0u);
+    const uint32_t m = std::max(nslots_cap, st.dkey ? st.dense_n : 0u);
     hipLaunchKernelGGL(k_hot_reset, dim3(std::max<uint32_t>(1, std::min<uint32_t>((m + 255) / 256, 4096))),
                        dim3(256), 0, s, st, sc, nslots_cap);
 }
@@ -3928,20 +3951,23 @@ static void hot_side(const ClusterState &st, BatchScratch &sc, int64_t ts_base, 
     }
 }
 
-static void classify_hot(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
-                         const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, uint64_t *out,
-                         hipStream_t s, bool clean, bool pipelined) {
+static void classify_hot(const ClusterState &st, BatchScratch &sc, const ReqIn &in, int64_t ts_base, uint32_t n,
+                         uint64_t *out, hipStream_t s, bool clean, bool pipelined) {
     const int bits = hot_key_bits(st);
     const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
     const uint32_t ngroups = (nseg + kHotGroupRows - 1) / kHotGroupRows;
     if (!clean) SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, CTL_WORDS * 4, s));
-    hipLaunchKernelGGL(k_hot_precheck, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc, ts_off, ts_base, n,
+    hipLaunchKernelGGL(k_hot_precheck, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc, in, ts_base, n,
                        pipelined ? 1 : 0);
     // the key pass streams its inputs and cold elements non-temporally, so the dense table keeps more of L2
     // (158 against 166 us on MI355X; SGA_KEY_NT=0, an A/B knob, turns it off)
     static const bool key_nt = !(getenv("SGA_KEY_NT") && atoi(getenv("SGA_KEY_NT")) == 0);
-    auto hka = st.dense_n ? (key_nt ? k_hot_key_dense<0, true> : k_hot_key_dense<0, false>) : k_hot_key_hash<0>;
-    auto hkb = st.dense_n ? k_hot_key_dense<1> : k_hot_key_hash<1>;
+    const bool pk = in.pk != nullptr;
+    auto hka = st.dense_n ? (pk ? (key_nt ? k_hot_key_dense<0, true, true> : k_hot_key_dense<0, false, true>)
+                                : (key_nt ? k_hot_key_dense<0, true, false> : k_hot_key_dense<0, false, false>))
+                          : (pk ? k_hot_key_hash<0, true> : k_hot_key_hash<0, false>);
+    auto hkb = st.dense_n ? (pk ? k_hot_key_dense<1, false, true> : k_hot_key_dense<1, false, false>)
+                          : (pk ? k_hot_key_hash<1, true> : k_hot_key_hash<1, false>);
     // the key kernels count the sort's first digit per tile as they write the elements
     // (their LDS counts hold 8-bit digits; a wider first digit is counted by the sort itself), or, with
     // the cold partition, each segment's elements per slot bin
@@ -3950,10 +3976,10 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const int64_t
     const int d0 = sc.part_lb ? -sc.part_lb : (dsort <= 8 ? dsort : 0);
     const uint32_t ntiles_sort = (uint32_t)radix64_tiles(n);
     uint32_t *khist = sc.part_lb ? sc.phist : sc.radix.hist;
-    hipLaunchKernelGGL(hka, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out,
-                       fz_debug(), d0, khist, ntiles_sort);
-    hipLaunchKernelGGL(hkb, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, flow_id, acquire, prio, ts_off, ts_base, n, out,
-                       fz_debug(), d0, khist, ntiles_sort);
+    hipLaunchKernelGGL(hka, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, in, ts_base, n, out, fz_debug(), d0, khist,
+                       ntiles_sort);
+    hipLaunchKernelGGL(hkb, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, in, ts_base, n, out, fz_debug(), d0, khist,
+                       ntiles_sort);
     hipLaunchKernelGGL(k_hot_mode, dim3(1), dim3(1024), 0, s, sc, nseg * kKeyWaves, nseg, ts_base);
     // the hot side's count scans and prioritized sort on the side stream, beside the cold sort
     const bool ovl = hot_overlap() && !(fz_debug() & 16);
@@ -4014,8 +4040,8 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const int64_t
 
 // Stage 2 (the batch's decisions; batches' stage 2 run in order): the hot runs and results on the side
 // stream beside the cold stage, then the next hot set.
-static void decide_hot(const ClusterState &st, BatchScratch &sc, const int32_t *acquire, const uint8_t *prio,
-                       int64_t ts_base, const uint32_t *ts_off, uint32_t n, uint64_t *out, hipStream_t s) {
+static void decide_hot(const ClusterState &st, BatchScratch &sc, const ReqIn &in, int64_t ts_base, uint32_t n,
+                       uint64_t *out, hipStream_t s) {
     const uint32_t invalid_key = st.nslots;
     const uint64_t *el = sc.el_sorted, *pel = sc.pel_sorted;
     const bool ovl = hot_overlap() && !(fz_debug() & 16);
@@ -4029,8 +4055,8 @@ static void decide_hot(const ClusterState &st, BatchScratch &sc, const int32_t *
         }
         hot_side(st, sc, ts_base, n, out, hs, ovl);
     }
-    cold_stage(st, sc, el, n, sc.counters + CTL_NCOLD, invalid_key, acquire, prio, ts_off, ts_base, 0,
-               std::max<uint32_t>(sc.hot_min, 1), out, s);
+    cold_stage(st, sc, el, n, sc.counters + CTL_NCOLD, invalid_key, in, ts_base, 0, std::max<uint32_t>(sc.hot_min, 1),
+               out, s);
     if (fz_debug() & 16) {  // profiling only: k_cold_fused phase cycles per workgroup
         unsigned long long ph[8];
         SGA_HIP_CHECK(hipMemcpyFromSymbolAsync(ph, HIP_SYMBOL(g_fz_phase), sizeof(ph), 0, hipMemcpyDeviceToHost, s));
@@ -4072,18 +4098,32 @@ void cluster_classify_hot(const ClusterState &st, BatchScratch &sc, const int64_
                           hipStream_t s) {
     const bool clean = sc.counters_clean != 0;
     sc.counters_clean = 0;
-    classify_hot(st, sc, flow_id, acquire, prio, ts_base, ts_off, n, (uint64_t *)out, s, clean, true);
+    ReqIn in;
+    in.flow = flow_id;
+    in.acq = acquire;
+    in.prio = prio;
+    in.ts = ts_off;
+    classify_hot(st, sc, in, ts_base, n, (uint64_t *)out, s, clean, true);
 }
 
 void cluster_decide_hot(const ClusterState &st, BatchScratch &sc, const int32_t *acquire, const uint8_t *prio,
                         int64_t ts_base, const uint32_t *ts_off, uint32_t n, void *out, hipStream_t s) {
-    decide_hot(st, sc, acquire, prio, ts_base, ts_off, n, (uint64_t *)out, s);
+    ReqIn in;
+    in.acq = acquire;
+    in.prio = prio;
+    in.ts = ts_off;
+    decide_hot(st, sc, in, ts_base, n, (uint64_t *)out, s);
 }
 
 void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_t *flow_id, const int32_t *acquire,
                           const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, int simple,
                           void *out_v, hipStream_t s, const LimiterPass *lims, int nlims) {
     if (n == 0) return;
+    ReqIn in;
+    in.flow = flow_id;
+    in.acq = acquire;
+    in.prio = simple ? nullptr : prio;
+    in.ts = ts_off;
     const bool clean = sc.counters_clean != 0;
     sc.counters_clean = 0;
     uint64_t *out = (uint64_t *)out_v;
@@ -4108,13 +4148,12 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
         hipLaunchKernelGGL(k_small_sort, dim3(1), dim3(kSmallThreads), 0, s, st, flow_id, acquire, prio, ts_off, ts_base,
                            n, m, simple, invalid_key, sc.el[0], out);
         hipLaunchKernelGGL(k_cold_fused, dim3((n + kFzChunk - 1) / kFzChunk), dim3(kFzThreads), 0, s, st, sc, sc.el[0],
-                           n, nullptr, invalid_key, acquire, prio, ts_off, ts_base, simple, 0xFFFFFFFFu, out, 0,
-                           nullptr, 0);
+                           n, nullptr, invalid_key, in, ts_base, simple, 0xFFFFFFFFu, out, 0, nullptr, 0);
         return;
     }
     if (cluster_hot_eligible(st, sc, n, simple, nlims)) {
-        classify_hot(st, sc, flow_id, acquire, prio, ts_base, ts_off, n, out, s, clean, false);
-        decide_hot(st, sc, acquire, prio, ts_base, ts_off, n, out, s);
+        classify_hot(st, sc, in, ts_base, n, out, s, clean, false);
+        decide_hot(st, sc, in, ts_base, n, out, s);
         return;
     }
     SGA_HIP_CHECK(hipMemsetAsync(sc.counters, 0, CTL_WORDS * 4, s));
@@ -4128,7 +4167,44 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
     if (!simple) apply_limiters(st.param, sc, sc.el[0], n, invalid_key, ts_base, ts_off, out, lims, nlims, s);
     const int np = radix_sort_u64(sc.el[0], sc.el[1], n, kSlotShift, bits, sc.radix, s, !limited && !nofuse);
     if (np != npass) throw HipError("radix pass count mismatch", __FILE__, __LINE__);
-    cold_stage(st, sc, el, n, nullptr, invalid_key, acquire, prio, ts_off, ts_base, simple, 0xFFFFFFFFu, out, s);
+    cold_stage(st, sc, el, n, nullptr, invalid_key, in, ts_base, simple, 0xFFFFFFFFu, out, s);
+}
+
+// packed requests -> the four arrays (the paths other than the hot one read those)
+__global__ __launch_bounds__(kThreads) void k_unpack(const uint32_t *__restrict__ pk, uint32_t n, int64_t *__restrict__ f,
+                                                     int32_t *__restrict__ a, uint8_t *__restrict__ p,
+                                                     uint32_t *__restrict__ t) {
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+        const uint32_t *r = pk + 3 * (size_t)i;
+        f[i] = (int64_t)r[0];
+        t[i] = r[1];
+        a[i] = (int32_t)(r[2] & 0xFFFFu);
+        p[i] = (uint8_t)((r[2] >> 16) & 1u);
+    }
+}
+
+void cluster_decide_batch_packed(const ClusterState &st, BatchScratch &sc, const uint32_t *pk, int64_t ts_base,
+                                 uint32_t n, void *out_v, hipStream_t s, const LimiterPass *lims, int nlims) {
+    if (n == 0) return;
+    const bool small = n <= std::min<uint32_t>(sc.small_max, kSmall) && nlims == 0 && !radix64_lookback();
+    if (!small && cluster_hot_eligible(st, sc, n, 0, nlims)) {
+        const bool clean = sc.counters_clean != 0;
+        sc.counters_clean = 0;
+        ReqIn in;
+        in.pk = pk;
+        classify_hot(st, sc, in, ts_base, n, (uint64_t *)out_v, s, clean, false);
+        decide_hot(st, sc, in, ts_base, n, (uint64_t *)out_v, s);
+        return;
+    }
+    // the hot path's scratch holds the arrays: flowIds in pel[0], acquire counts and time offsets in pel[1],
+    // prioritized flags in prank (none of them is used off the hot path)
+    int64_t *f = reinterpret_cast<int64_t *>(sc.pel[0]);
+    int32_t *a = reinterpret_cast<int32_t *>(sc.pel[1]);
+    uint32_t *t = reinterpret_cast<uint32_t *>(sc.pel[1]) + sc.cap;
+    uint8_t *p = reinterpret_cast<uint8_t *>(sc.prank);
+    const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 4096));
+    hipLaunchKernelGGL(k_unpack, dim3(nb), dim3(kThreads), 0, s, pk, n, f, a, p, t);
+    cluster_decide_batch(st, sc, f, a, p, ts_base, t, n, 0, out_v, s, lims, nlims);
 }
 
 // ---------------------------------------------------------------- cluster parameter flow (host)

@@ -45,10 +45,11 @@ struct ClusterState {
     int64_t *rec;            // per slot: 8 fields x S buckets at rec[8*boff]; field 0 = window start
                              // (kAbsent = null), fields 1..7 = LongAdder sums per ClusterFlowEvent
     const HashEntry *htab;   // open-addressing flowId -> (slot, windowLengthInMs)
-    const uint64_t *dense;   // when flowIds are dense, per flowId - 1: bits 0..31 slot | wcode << 24 (all ones:
-                             // no rule), bits 32..47 hot id (kColdId: cold) -- one gather answers both
+    const uint32_t *dense;   // when flowIds are dense, per flowId - 1: slot | wcode << 24 (all ones: no rule)
+    uint32_t *dkey;          // the hot path's copy of `dense` (one per scratch set): a hot rule's entry is
+                             // kDkHot | hot id instead, so the key pass's one 4-byte gather answers both
+                             // (written when the hot set changes); no rule = kDkNone; wcode < 127 here
     const uint32_t *wtab;    // wcode -> windowLengthInMs
-    uint16_t *dense_hot;      // the hot-id halfwords of `dense` (written when the hot set changes)
     const int64_t *slot_fid; // flowId per slot
     uint32_t dense_n;        // dense table length (0: hash lookup)
     uint32_t hmask;
@@ -58,6 +59,27 @@ struct ClusterState {
     // its record at slot * (uni_S + 1) 64-byte units, the layout of one load of equal rules): a slot's record
     // address needs no parameter load, so the record loads do not wait for one.  uni_S = 0: not uniform.
     int32_t uni_S, uni_W, uni_iv, uni_pad;
+};
+
+constexpr uint32_t kDkHot = 0x80000000u, kDkNone = 0x7FFFFFFFu;
+
+// A batch's requests as the device entries receive them: four arrays (int64 flowId, int32
+// acquireCount, u8 prioritized or none, u32 time offset), or the packed 12-byte records of
+// sga_token_request (3 words: flowId, time offset, acquireCount | flags << 16).
+struct ReqIn {
+    const int64_t *flow = nullptr;
+    const int32_t *acq = nullptr;
+    const uint8_t *prio = nullptr;
+    const uint32_t *ts = nullptr;
+    const uint32_t *pk = nullptr;
+    __device__ __forceinline__ uint32_t ts_at(uint32_t i) const { return pk ? pk[3 * (size_t)i + 1] : ts[i]; }
+    __device__ __forceinline__ int32_t acq_at(uint32_t i) const {
+        return pk ? (int32_t)(pk[3 * (size_t)i + 2] & 0xFFFFu) : acq[i];
+    }
+    __device__ __forceinline__ bool prio_at(uint32_t i) const {
+        return pk ? ((pk[3 * (size_t)i + 2] >> 16) & 1u) != 0 : (prio && prio[i]);
+    }
+    __device__ __forceinline__ int64_t flow_at(uint32_t i) const { return pk ? (int64_t)pk[3 * (size_t)i] : flow[i]; }
 };
 
 // GlobalRequestLimiter / RequestLimiter of one namespace over UnaryLeapArray(10, 1000)
@@ -147,7 +169,8 @@ enum : uint32_t {
     kFlagUnsorted = 1,   // timestamps decrease somewhere: no bucket order to rank by
     kFlagMixed = 2,      // a hot request with acquireCount != 1
     kFlagBucket = 4,     // the batch spans more than kHotBuckets hot buckets
-    kFlagRerun = 7,      // any of the above: pass 1 re-classifies every request as cold
+    kFlagHotKey = 8,     // a key-table entry names a hot id outside the hot set (never expected)
+    kFlagRerun = 15,     // any of the above: pass 1 re-classifies every request as cold
     kFlagState = 16      // a hot rule's window holds a bucket newer than the batch (precheck)
 };
 
@@ -255,6 +278,11 @@ void cluster_decide_batch(const ClusterState &st, BatchScratch &sc, const int64_
                           const uint8_t *prio, int64_t ts_base, const uint32_t *ts_off, uint32_t n, int simple,
                           void *out /* sga_token_result */, hipStream_t stream, const LimiterPass *lims = nullptr,
                           int nlims = 0);
+// The same over packed requests (sga_token_request): the hot path reads them directly; the other paths
+// unpack them into the hot path's scratch (pel, prank) first.
+void cluster_decide_batch_packed(const ClusterState &st, BatchScratch &sc, const uint32_t *pk, int64_t ts_base,
+                                 uint32_t n, void *out, hipStream_t stream, const LimiterPass *lims = nullptr,
+                                 int nlims = 0);
 
 // Whether a batch takes the hot path (the small path and the limiter / RLS / look-back sort paths do not).
 bool cluster_hot_eligible(const ClusterState &st, const BatchScratch &sc, uint32_t n, int simple, int nlims);

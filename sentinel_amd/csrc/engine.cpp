@@ -169,7 +169,8 @@ struct Engine {
     DevBuf<int64_t> d_slot_fid;  // flowId per slot (metric snapshots)
     DevBuf<uint32_t> d_ncount;
     DevBuf<uint8_t> d_nodes;
-    DevBuf<uint64_t> d_dense;  // dense flowId table (see sync_device): slot entry + hot id per flowId
+    DevBuf<uint32_t> d_dense;  // dense flowId table (see sync_device): slot | wcode << 24 per flowId
+    DevBuf<uint32_t> d_dkey;   // the hot path's key table (ClusterState::dkey) of the first scratch set
     DevBuf<uint32_t> d_wtab;
     uint32_t dense_n = 0;
     DevBuf<uint32_t> d_fresh;
@@ -179,12 +180,12 @@ struct Engine {
     uint32_t scratch_slots_cap = 0;
     // ---- pipelined device batches (sga_request_tokens_device_pipelined): batch k + 1's stage 1 (key pass,
     // count scans, sorts) runs on cls_stream while batch k's stage 2 (decisions) runs on the engine stream.
-    // Batches alternate between two scratch sets, each with its own hot set and its own copy of the dense
-    // flowId table (whose hot-id halfwords the hot set writes); a set is reused once its previous batch's
+    // Batches alternate between two scratch sets, each with its own hot set and its own key table (whose
+    // entries the hot set writes); a set is reused once its previous batch's
     // stage 2 is done (ev_dec).  Every other engine call joins the pipeline first (join_pipeline).
     DevBuf<uint8_t> d_scratch2;
     BatchScratch scratch2;
-    DevBuf<uint64_t> d_dense2;
+    DevBuf<uint32_t> d_dkey2;
     hipStream_t cls_stream = nullptr;
     hipEvent_t ev_cls[2] = {nullptr, nullptr}, ev_dec[2] = {nullptr, nullptr}, ev_in = nullptr, ev_other = nullptr;
     bool dec_recorded[2] = {false, false};
@@ -544,9 +545,8 @@ struct Engine {
         st.param = d_param.p;
         st.rec = d_rec.p;
         st.htab = d_htab.p;
-        uint64_t *dn = (pset && d_dense2.p) ? d_dense2.p : d_dense.p;
-        st.dense = dn;
-        st.dense_hot = dense_n ? reinterpret_cast<uint16_t *>(dn) : nullptr;
+        st.dense = d_dense.p;
+        st.dkey = dense_n ? ((pset && d_dkey2.p) ? d_dkey2.p : d_dkey.p) : nullptr;
         st.slot_fid = d_slot_fid.p;
         st.wtab = d_wtab.p;
         st.dense_n = dense_n;
@@ -600,7 +600,7 @@ struct Engine {
         scratch2.hot_enabled = scratch.hot_enabled;
         scratch2.hot_min = scratch.hot_min;
         scratch2.small_max = scratch.small_max;
-        sync_dense2();
+        sync_dkey2();
         hot_reset(state(1), scratch2, scratch_slots_cap, stream);
         if (!cls_stream) {
             SGA_HIP_CHECK(hipStreamCreateWithFlags(&cls_stream, hipStreamNonBlocking));
@@ -615,12 +615,11 @@ struct Engine {
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
     }
 
-    // the second dense table = the first one (slots and window codes), hot ids of its own set
-    void sync_dense2() {
+    // the second scratch set's key table (hot_reset then fills it from the dense table)
+    void sync_dkey2() {
         if (!d_scratch2.p) return;
         if (!dense_n) return;
-        if (d_dense2.n < d_dense.n) d_dense2.alloc(d_dense.n);
-        SGA_HIP_CHECK(hipMemcpyAsync(d_dense2.p, d_dense.p, (size_t)dense_n * 8, hipMemcpyDeviceToDevice, stream));
+        if (d_dkey2.n < d_dense.n) d_dkey2.alloc(d_dense.n);
     }
 
     // every engine call but a pipelined batch: order it after the pipeline's in-flight stage-1 work (stage 2
@@ -777,8 +776,9 @@ struct Engine {
         SGA_HIP_CHECK(hipMemcpyAsync(d_htab.p, ht.data(), hcap * sizeof(HashEntry), hipMemcpyHostToDevice, stream));
         hmask = (uint32_t)(hcap - 1);
         // Dense flowIds (the usual 1..N assignment): a direct table of 4-byte entries replaces the
-        // probe sequence when it costs at most 16 B per active rule and the rules use <= 255
-        // distinct window lengths.  Same lookup result as FLOW_RULES.get(flowId).
+        // probe sequence when it costs at most 16 B per active rule and the rules use <= 126
+        // distinct window lengths (the key table's entries keep bit 31 for the hot set).  Same lookup
+        // result as FLOW_RULES.get(flowId).
         {
             int64_t maxid = 0;
             std::vector<uint32_t> wvals;
@@ -788,25 +788,26 @@ struct Engine {
                 maxid = std::max(maxid, slots[i].flow_id);
                 const uint32_t W = (uint32_t)(slots[i].interval / slots[i].S);
                 if (std::find(wvals.begin(), wvals.end(), W) == wvals.end()) wvals.push_back(W);
-                if (wvals.size() > 255) ok = false;
+                if (wvals.size() > 126) ok = false;
             }
             if (ok && maxid <= (int64_t)(4 * nact + 4096) && maxid < (int64_t)0xFFFFFFFF) {
-                // entry: slot | wcode << 24 in bits 0..31, hot id (cold until the hot set is picked) in 32..47
-                const uint64_t cold = (uint64_t)kColdId << 32;
-                std::vector<uint64_t> dt((size_t)maxid, cold | 0xFFFFFFFFull);
+                // entry: slot | wcode << 24 (the key tables are filled from it by hot_reset below)
+                std::vector<uint32_t> dt((size_t)maxid, 0xFFFFFFFFu);
                 for (size_t i = 0; i < ns; ++i) {
                     if (!slots[i].active) continue;
                     const uint32_t W = (uint32_t)(slots[i].interval / slots[i].S);
                     const uint32_t code = (uint32_t)(std::find(wvals.begin(), wvals.end(), W) - wvals.begin());
-                    dt[(size_t)slots[i].flow_id - 1] = cold | (uint32_t)i | (code << 24);
+                    dt[(size_t)slots[i].flow_id - 1] = (uint32_t)i | (code << 24);
                 }
                 wvals.resize(256, 1);
                 if (d_dense.n < dt.size()) {
                     SGA_HIP_CHECK(hipStreamSynchronize(stream));
                     d_dense.alloc(dt.size());
+                    d_dkey.alloc(dt.size());
+                    if (d_dkey2.p) d_dkey2.alloc(dt.size());
                 }
                 if (d_wtab.n < 256) d_wtab.alloc(256);
-                SGA_HIP_CHECK(hipMemcpyAsync(d_dense.p, dt.data(), dt.size() * 8, hipMemcpyHostToDevice, stream));
+                SGA_HIP_CHECK(hipMemcpyAsync(d_dense.p, dt.data(), dt.size() * 4, hipMemcpyHostToDevice, stream));
                 SGA_HIP_CHECK(hipMemcpyAsync(d_wtab.p, wvals.data(), 256 * 4, hipMemcpyHostToDevice, stream));
                 SGA_HIP_CHECK(hipStreamSynchronize(stream));
                 dense_n = (uint32_t)maxid;
@@ -830,7 +831,7 @@ struct Engine {
         // slots may have been freed or reused: forget the hot-rule set (the next batch re-chooses it)
         hot_reset(state(), scratch, scratch_slots_cap, stream);
         if (d_scratch2.p) {
-            sync_dense2();
+            sync_dkey2();
             hot_reset(state(1), scratch2, scratch_slots_cap, stream);
         }
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
@@ -1132,6 +1133,25 @@ int sga_request_tokens_device(sga_engine *e, const int64_t *d_flow_id, const int
         const auto lims = limiter_passes(g);
         sga::cluster_decide_batch(g.state(), g.scratch, d_flow_id, d_acquire, d_prio, ts_base, d_ts_off, (uint32_t)n,
                                   0, d_out, s, lims.data(), (int)lims.size());
+        g.last_sc = &g.scratch;
+        SGA_HIP_CHECK(hipGetLastError());
+        g.leave_stream(s);
+        return SGA_OK;
+    });
+}
+
+int sga_request_tokens_packed_device(sga_engine *e, const sga_token_request *d_req, int64_t ts_base, size_t n,
+                                     sga_token_result *d_out, void *hip_stream) {
+    static_assert(sizeof(sga_token_request) == 12, "packed request = three words");
+    if (n && (!d_req || !d_out)) return SGA_EINVAL;
+    if (ts_base < 0 || ((uintptr_t)d_req & 3u)) return SGA_EINVAL;
+    return guarded(e, [&](Engine &g) {
+        if (n > g.cfg.max_batch) return SGA_ERANGE;
+        SGA_HIP_CHECK(hipSetDevice(g.cfg.device));
+        hipStream_t s = g.enter_stream(hip_stream);
+        const auto lims = limiter_passes(g);
+        sga::cluster_decide_batch_packed(g.state(), g.scratch, reinterpret_cast<const uint32_t *>(d_req), ts_base,
+                                         (uint32_t)n, d_out, s, lims.data(), (int)lims.size());
         g.last_sc = &g.scratch;
         SGA_HIP_CHECK(hipGetLastError());
         g.leave_stream(s);

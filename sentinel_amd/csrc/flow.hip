@@ -1085,10 +1085,12 @@ __global__ __launch_bounds__(kT) void k_lfail(const uint32_t *gate, const uint32
                                               uint32_t n, int8_t *decision, int32_t *wait_ms) {
     const uint32_t g = *gate;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const uint32_t e = ((g & kGateBad) ? 1u : 0u) | (*overflow ? 2u : 0u);
+        const uint32_t o = *overflow;
+        const uint32_t e = ((g & kGateBad) ? 1u : 0u) | ((o & ~kOvfMissingEntry) ? 2u : 0u) |
+                           ((o & kOvfMissingEntry) ? 4u : 0u);
         if (e) atomicOr(sticky, e);
     }
-    if (!(g & kGateBad)) return;
+    if (!(g & kGateBad) && !(*overflow & kOvfMissingEntry)) return;  // else every decision answers -1
     for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
         decision[i] = -1;
         wait_ms[i] = 0;
@@ -3704,10 +3706,13 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
 //    lanes may claim a slot each for one key; the later one in the probe sequence is never found again,
 //    its key absent, dropped at the next rehash).  !kClaim: the element (slot << 32 | sorted position),
 //    kPsegNone in the slot bits for every other event.
+// force_miss (fault injection, SGA_PSEG_FORCE_MISS=1; tests only): the first parameter event's entry is
+// taken as missing, so the device check below fails the batch
 template <bool kClaim>
 __global__ __launch_bounds__(kT) void k_pseg_key(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
                                                  const uint32_t *__restrict__ keys,
-                                                 const uint64_t *__restrict__ param_in, uint32_t m, uint64_t none) {
+                                                 const uint64_t *__restrict__ param_in, uint32_t m, uint64_t none,
+                                                 int force_miss) {
     if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
     const uint32_t nvalid = sc.counters[0];
     const bool any = sc.counters[11] != 0;
@@ -3721,6 +3726,7 @@ __global__ __launch_bounds__(kT) void k_pseg_key(FlowState st, FlowScratch sc, c
                 const uint64_t v = param_in[q.idx & F_IDX];
                 if (st.tmapmask[res] & 1ull) {  // else an exit-only flow without the map: the exit touches no map
                     PEntry *te = ptab_get(st.ttab, st.tmask, tmap_owner(res, 0), v, kClaim, st.overflow);
+                    if (!kClaim && force_miss && j < 64) te = nullptr;
                     if (kClaim && !(q.idx & F_EXIT))
                         ptab_get(st.ptab, st.pmask, st.prules[st.res[res].prule_off].id + 1, v, true, st.overflow);
                     if (!kClaim && te) {
@@ -3729,8 +3735,8 @@ __global__ __launch_bounds__(kT) void k_pseg_key(FlowState st, FlowScratch sc, c
                     } else if (!kClaim) {
                         // every parameter event of a RUN_PSEG flow had its thread-count entry claimed (by the
                         // claim launch, or by k_lru_count in LRU mode); a missing one would leave the event
-                        // undecided, so the batch fails as a map overflow does
-                        atomicOr(st.overflow, 1u);
+                        // undecided, so the batch fails: the overflow word's device-error bit (SGA_EIO)
+                        atomicOr(st.overflow, kOvfMissingEntry);
                     }
                 }
             }
@@ -5497,8 +5503,10 @@ void FlowEngine::launch_pseg(const FlowState &st, const FlowScratch &g, const Pa
     if (!h_prules.empty()) {
         // the count pass (lru_prepare, whenever parameter rules are loaded) has claimed every key these events
         // name in free-mode maps already; the claim launch is for an engine without it
-        if (!d_psize.p) hipLaunchKernelGGL(k_pseg_key<true>, dim3(nb), dim3(kT), 0, s, st, gs, pay, keys, param, m, none);
-        hipLaunchKernelGGL(k_pseg_key<false>, dim3(nb), dim3(kT), 0, s, st, gs, pay, keys, param, m, none);
+        static const int force_miss = getenv("SGA_PSEG_FORCE_MISS") ? atoi(getenv("SGA_PSEG_FORCE_MISS")) : 0;
+        if (!d_psize.p)
+            hipLaunchKernelGGL(k_pseg_key<true>, dim3(nb), dim3(kT), 0, s, st, gs, pay, keys, param, m, none, 0);
+        hipLaunchKernelGGL(k_pseg_key<false>, dim3(nb), dim3(kT), 0, s, st, gs, pay, keys, param, m, none, force_miss);
         // the slot bits sorted in pieces of at most 24 bits (3 radix passes each), least significant first
         uint64_t *el = gs.pel[0], *alt = gs.pel[1];
         const int pieces = (sbits + 23) / 24, pb = (sbits + pieces - 1) / pieces;
@@ -5761,6 +5769,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
             uint32_t ovf = 0;
             SGA_HIP_CHECK(hipMemcpyAsync(&ovf, d_overflow.p, 4, hipMemcpyDeviceToHost, stream));
             SGA_HIP_CHECK(hipStreamSynchronize(stream));
+            if (ovf & kOvfMissingEntry) throw HipError(kMissingEntryText, __FILE__, __LINE__);  // SGA_EIO
             if (ovf) return SGA_ENOMEM;
             b += m;
             seq += m;
@@ -5809,6 +5818,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         uint32_t ovf = 0;
         SGA_HIP_CHECK(hipMemcpyAsync(&ovf, d_overflow.p, 4, hipMemcpyDeviceToHost, stream));
         SGA_HIP_CHECK(hipStreamSynchronize(stream));
+        if (ovf & kOvfMissingEntry) throw HipError(kMissingEntryText, __FILE__, __LINE__);  // SGA_EIO
         if (ovf) return SGA_ENOMEM;  // parameter maps full
         debug_size_check();
         b += m;
@@ -5944,6 +5954,7 @@ int FlowEngine::device_status() {
     SGA_HIP_CHECK(hipMemsetAsync(d_gate.p + 1, 0, 4, stream));
     SGA_HIP_CHECK(hipStreamSynchronize(stream));
     if (e & 1u) return SGA_EINVAL;
+    if (e & 4u) throw HipError(kMissingEntryText, __FILE__, __LINE__);  // SGA_EIO
     if (e & 2u) return SGA_ENOMEM;
     return 0;
 }

@@ -11,6 +11,14 @@
 
 namespace sga {
 
+// FlowState::overflow bits: any other bit = a parameter map filled (SGA_ENOMEM); kOvfMissingEntry = a
+// parameter event of a per-value segment flow found no thread-count entry, which every such event had
+// claimed before (never expected: the batch fails with SGA_EIO instead of leaving the event undecided)
+constexpr uint32_t kOvfMissingEntry = 0x80000000u;
+constexpr const char *kMissingEntryText =
+    "parameter event without its thread-count map entry (k_pseg_key device check); the batch failed";
+
+
 // ---- node record (one ClusterNode per resource), int64 words -------------------
 // second window: OccupiableBucketLeapArray(2, 1000)  (StatisticNode.java:99-100)
 // borrow window: FutureBucketLeapArray(2, 1000)      (OccupiableBucketLeapArray.java:33-37)
@@ -125,7 +133,7 @@ struct FlowState {
     PEntry *ttab;      // thread-count maps
     uint32_t pmask, tmask;
     uint32_t nres;
-    uint32_t *overflow;  // set when a param table is full
+    uint32_t *overflow;  // set when a param table is full (bit kOvfMissingEntry: a device check failed)
     // embedded cluster token server for cluster-mode FlowRules (sga_set_cluster_server 1)
     ClusterState cst;
     int32_t cluster_on;

@@ -147,3 +147,83 @@ class ClusterTrace:
 def shard_of(flow_id, n_shards):
     """Rules shard by flowId hash across GPUs: splitmix64(flowId) mod G."""
     return (splitmix64(np.asarray(flow_id, dtype=np.int64).astype(np.uint64)) % np.uint64(n_shards)).astype(np.int64)
+
+
+# ------------------------------------------------------------------ C3 on the device
+class DeviceClusterGen:
+    """The C3 trace generated in HBM by libsga_workload.so (sgaw_gen_cluster: the same Zipf(1.1)
+    flowIds, 1 % prioritized, acquire 1 at lambda requests per virtual second), one rank's share
+    (splitmix64(flowId) mod n_shards == shard) of each global batch.  Benchmark / test input only."""
+
+    def __init__(self, dev, n_rules=1_000_000, lam=100_000_000, n_shards=1, shard=0, seed=MASTER_SEED,
+                 prio_pct=1, s=1.1):
+        import ctypes as C
+        import os
+
+        import torch
+
+        class SgawParams(C.Structure):
+            _fields_ = [("seed", C.c_uint64), ("t0", C.c_int64), ("lambda_", C.c_int64), ("n_rules", C.c_int64),
+                        ("zipf_s", C.c_double), ("prio_pct", C.c_int32), ("n_shards", C.c_int32),
+                        ("shard", C.c_int32), ("reserved", C.c_int32)]
+
+        self.C, self.torch, self.dev = C, torch, dev
+        self.lam, self.n_rules = lam, n_rules
+        self.wl = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsga_workload.so"))
+        self.wl.sgaw_gen_cluster.restype = C.c_int
+        self.wl.sgaw_gen_cluster.argtypes = [C.POINTER(SgawParams), C.c_uint64, C.c_uint32, C.c_void_p, C.c_int64,
+                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                             C.c_void_p]
+        self.wl.sgaw_flow_histogram.restype = C.c_int
+        self.wl.sgaw_flow_histogram.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64, C.c_void_p]
+        self.params = SgawParams(seed, T0, lam, n_rules, s, prio_pct, n_shards, shard, 0)
+        self.perm = torch.from_numpy(permutation(n_rules, seed=seed)).to(dev)
+        self.cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.hist = None
+        self.tmp = None
+
+    def ts_base(self, start):
+        return T0 + (start * 1000) // self.lam
+
+    def batch(self, start, m, touched=False):
+        """Global requests [start, start + m): this shard's (flowId int64, acquire int32, prio u8, time offset
+        int32 from ts_base(start)) on the device, ts_base, n (and the number of distinct flowIds if touched)."""
+        torch, C = self.torch, self.C
+        if self.tmp is None or self.tmp.numel() < 4 * m + 4096:
+            self.tmp = torch.empty(4 * m + 4096, dtype=torch.int32, device=self.dev)
+        f = torch.empty(m, dtype=torch.int64, device=self.dev)
+        a = torch.empty(m, dtype=torch.int32, device=self.dev)
+        p = torch.empty(m, dtype=torch.uint8, device=self.dev)
+        t = torch.empty(m, dtype=torch.int32, device=self.dev)
+        stream = torch.cuda.current_stream(self.dev)
+        base = self.ts_base(start)
+        rc = self.wl.sgaw_gen_cluster(C.byref(self.params), start, m, self.perm.data_ptr(), base, f.data_ptr(),
+                                      a.data_ptr(), p.data_ptr(), t.data_ptr(), self.cnt.data_ptr(),
+                                      self.tmp.data_ptr(), C.c_void_p(stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"sgaw_gen_cluster rc={rc}")
+        torch.cuda.synchronize(self.dev)
+        n = int(self.cnt.item())
+        out = (f[:n].clone(), a[:n].clone(), p[:n].clone(), t[:n].clone(), base, n)
+        if touched:
+            if self.hist is None:
+                self.hist = torch.zeros(self.n_rules + 1, dtype=torch.int32, device=self.dev)
+            self.wl.sgaw_flow_histogram(f.data_ptr(), n, self.hist.data_ptr(), self.n_rules,
+                                        C.c_void_p(stream.cuda_stream))
+            torch.cuda.synchronize(self.dev)
+            out = out + (int((self.hist > 0).sum().item()),)
+        return out
+
+
+def pack_requests(f, a, p, t):
+    """sga_token_request records (include/sentinel_amd.h) from device arrays: int32 [n, 3] =
+    (flowId u32, time offset u32, acquire u16 | prioritized << 16).  Requires 0 <= flowId < 2^32 and
+    0 <= acquire < 2^16 (the packed entry's domain)."""
+    import torch
+    n = f.numel()
+    out = torch.empty((n, 3), dtype=torch.int32, device=f.device)
+    out[:, 0] = f.to(torch.int64).to(torch.int32)
+    out[:, 1] = t.to(torch.int32)
+    out[:, 2] = a.to(torch.int32) | (p.to(torch.int32) << 16)
+    torch.cuda.synchronize(f.device)  # the engine reads them on its own stream
+    return out

@@ -529,3 +529,61 @@ def run_scenario(sc, base):
     finally:
         for fn, h in reversed(frees):
             fn(h)
+
+
+def cluster_replay_sharded(rule_fid, rule_count, batches, threads=16, sample_count=10, interval_ms=1000):
+    """The oracle's ClusterFlowChecker replay of whole C3 batches (GLOBAL rules, no namespace limiter):
+    rules are independent, so each of `threads` oracle instances replays the requests of the flowIds
+    with flowId mod threads == k in arrival order (ctypes releases the GIL: the threads run in parallel).
+    batches: [(flowId int64, acquire int32, prio u8, time int64)] in order.  Returns per batch the
+    (status, remaining, waitInMs) int32 arrays in request order."""
+    import threading
+
+    import numpy as np
+    L = lib()
+    rule_fid = np.asarray(rule_fid, np.int64)
+    rule_count = np.asarray(rule_count, np.float64)
+    rdt = np.dtype([("flow_id", np.int64), ("count", np.float64), ("threshold_type", np.int32),
+                    ("sample_count", np.int32), ("window_interval_ms", np.int32), ("grade", np.int32),
+                    ("strategy", np.int32), ("reserved", np.int32), ("resource_timeout_ms", np.int64),
+                    ("client_offline_time_ms", np.int64)])
+    assert rdt.itemsize == C.sizeof(OrcClusterRule), "oracle rule layout"
+    hs = []
+    for k in range(threads):
+        sel = (rule_fid % threads) == k
+        arr = np.zeros(int(sel.sum()), dtype=rdt)
+        arr["flow_id"], arr["count"] = rule_fid[sel], rule_count[sel]
+        arr["threshold_type"], arr["sample_count"], arr["window_interval_ms"], arr["grade"] = 1, sample_count, \
+            interval_ms, 1
+        arr["resource_timeout_ms"], arr["client_offline_time_ms"] = 2000, 2000
+        h = L.orc_cluster_new(1.0, 1.0)
+        L.orc_cluster_load_rules(h, b"default", arr.ctypes.data_as(C.POINTER(OrcClusterRule)), len(arr))
+        hs.append(h)
+    results = []
+    for f, a, p, ts in batches:
+        f = np.ascontiguousarray(f, np.int64)
+        shard = np.mod(f, threads).astype(np.uint8 if threads <= 256 else np.int64)
+        order = np.argsort(shard, kind="stable")  # radix sort for small integer keys
+        bounds = np.concatenate([[0], np.cumsum(np.bincount(shard, minlength=threads))])
+        parts = [np.ascontiguousarray(x[order]) for x in (f, np.asarray(a, np.int32), np.asarray(p, np.uint8),
+                                                             np.asarray(ts, np.int64))]
+        out = np.zeros((len(f), 3), dtype=np.int32)
+
+        def run(k):
+            lo, hi = int(bounds[k]), int(bounds[k + 1])
+            if hi <= lo:
+                return
+            buf = (OrcTokenResult * (hi - lo))()
+            L.orc_cluster_replay(hs[k], hi - lo, parts[0][lo:].ctypes.data, parts[1][lo:].ctypes.data,
+                                 parts[2][lo:].ctypes.data, parts[3][lo:].ctypes.data, buf)
+            out[order[lo:hi]] = np.frombuffer(buf, dtype=np.int32).reshape(-1, 3)
+
+        ths = [threading.Thread(target=run, args=(k,)) for k in range(threads)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        results.append((out[:, 0].copy(), out[:, 1].copy(), out[:, 2].copy()))
+    for h in hs:
+        L.orc_cluster_free(h)
+    return results

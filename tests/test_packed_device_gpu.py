@@ -1,0 +1,184 @@
+"""The packed device entry (sga_request_tokens_packed_device, 12-byte sga_token_request records -- the
+SURVEY.md 8(d) E_in of a token request) against the four-array device entry and the oracle's
+ClusterFlowChecker replay (DefaultTokenService.requestToken in arrival order,
+CS/flow/DefaultTokenService.java:39-50, ClusterFlowChecker.java:55-112): identical TokenResults on every
+path the engine takes (hot, sort, small, namespace limiter), and at BASELINE C3's full size every
+request of four warm 2^24-request batches equal to the oracle."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from tests import oracle_harness as H
+
+T0 = 1_700_000_000_000
+
+
+def _decode(r):
+    r = np.asarray(r).view(np.uint64)
+    return {"status": ((r >> np.uint64(48)) & np.uint64(0xFF)).astype(np.int8).astype(np.int32),
+            "remaining": (r & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32),
+            "wait_in_ms": ((r >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.uint16).view(np.int16).astype(np.int32)}
+
+
+def _mismatch(got, orc, what):
+    st, rem, wait = orc
+    bad = np.nonzero((got["status"] != st) | (got["remaining"] != rem) | (got["wait_in_ms"] != wait))[0]
+    if bad.size:
+        i = bad[0]
+        raise AssertionError(f"{what}: {bad.size} mismatches; first at {i}: gpu=({got['status'][i]},"
+                             f"{got['remaining'][i]},{got['wait_in_ms'][i]}) oracle=({st[i]},{rem[i]},{wait[i]})")
+
+
+def test_sharded_oracle_replay_equals_one_instance():
+    """CPU: the sharded oracle replay the full-size tests and bench.py's parity sample use equals one oracle
+    instance replaying the whole trace (rules are independent)."""
+    from sentinel_amd.workload import ClusterTrace
+    tr = ClusterTrace(n_rules=5000, lam=2_000_000)
+    fid_r, cnt = tr.rules()
+    cnt = np.minimum(cnt, 300.0)
+    batches = [tr.events(b * 40_000, 40_000) for b in range(3)]
+    f0, a0, p0, t0 = batches[1]
+    f0 = f0.copy()
+    f0[::97] = 0        # BAD_REQUEST
+    f0[5::89] = 999_999  # NO_RULE_EXISTS
+    batches[1] = (f0, a0, p0, t0)
+    got = H.cluster_replay_sharded(fid_r, cnt, batches, threads=4)
+    L = H.lib()
+    h = L.orc_cluster_new(1.0, 1.0)
+    arr = H.cluster_rules_array([{"flow_id": int(f), "count": float(c), "threshold_type": 1} for f, c in zip(fid_r, cnt)])
+    L.orc_cluster_load_rules(h, b"default", arr, len(fid_r))
+    for b, (f, a, p, ts) in enumerate(batches):
+        n = len(f)
+        out = (H.OrcTokenResult * n)()
+        L.orc_cluster_replay(h, n, np.ascontiguousarray(f).ctypes.data, np.ascontiguousarray(a).ctypes.data,
+                             np.ascontiguousarray(p).ctypes.data, np.ascontiguousarray(ts).ctypes.data, out)
+        ref = np.frombuffer(out, dtype=np.int32).reshape(n, 3)
+        for k in range(3):
+            assert np.array_equal(got[b][k], ref[:, k]), (b, k)
+    L.orc_cluster_free(h)
+
+
+def _engine(cluster, hot, max_batch, max_rules=1 << 16):
+    kw = {"off": dict(hot_rules=False, small_batch=0), "on": dict(hot_rules=True, hot_min_requests=16, small_batch=0),
+          "small": dict(hot_rules=False, small_batch=4096)}[hot]
+    return cluster.Engine(max_batch=max_batch, max_rules=max_rules, **kw)
+
+
+def _run(L, eng, dev, f, a, p, ts, packed):
+    import torch
+    base = int(ts.min())
+    n = len(f)
+    o = torch.zeros(max(n, 1), dtype=torch.int64, device=dev)
+    if packed:
+        rec = np.zeros((n, 3), dtype=np.uint32)
+        rec[:, 0] = f.astype(np.uint32)
+        rec[:, 1] = (ts - base).astype(np.uint32)
+        rec[:, 2] = a.astype(np.uint32) | (p.astype(np.uint32) << 16)
+        d = torch.from_numpy(rec.view(np.int32)).to(dev)
+        rc = L.sga_request_tokens_packed_device(eng.handle, d.data_ptr(), base, n, o.data_ptr(), None)
+    else:
+        d = [torch.from_numpy(x).to(dev) for x in (f, a, p, (ts - base).astype(np.int32))]
+        rc = L.sga_request_tokens_device(eng.handle, d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), base,
+                                         d[3].data_ptr(), n, o.data_ptr(), None)
+    assert rc == 0, L.sga_last_error(eng.handle)
+    assert L.sga_sync(eng.handle) == 0
+    return o[:n].cpu().numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hot", ["on", "off", "small"])
+def test_packed_entry_matches_arrays_and_oracle(hot):
+    """Random Zipf traces over 3000 rules with invalid requests (flowId 0, unknown flowIds, acquire 0), large
+    acquire counts (escapes: 200, 65535) and 5 % prioritized requests, six batches each way: the packed entry's
+    TokenResults equal the array entry's and the oracle's, on the hot, sort and small paths."""
+    import torch
+    from sentinel_amd import _lib, cluster
+    from sentinel_amd.workload import ClusterTrace
+    L = _lib.load()
+    dev = torch.device("cuda", 0)
+    tr = ClusterTrace(n_rules=3000, lam=3_000_000, prio_pct=5)
+    fid_r, cnt = tr.rules()
+    cnt = np.minimum(cnt, 500.0)
+    m = 3000 if hot == "small" else 200_000
+    rng = np.random.default_rng(7)
+    batches = []
+    for b in range(6):
+        f, a, p, ts = tr.events(b * m, m)
+        f, a = f.copy(), a.copy()
+        k = rng.integers(0, m, size=m // 200)
+        f[k[: len(k) // 3]] = 0
+        f[k[len(k) // 3: 2 * len(k) // 3]] = 3000 + rng.integers(1, 1000, size=len(k[len(k) // 3: 2 * len(k) // 3]))
+        a[k[2 * len(k) // 3:]] = 0
+        j = rng.integers(0, m, size=m // 500)
+        a[j] = rng.choice([2, 3, 200, 65535], size=len(j))
+        batches.append((f, a, p, ts))
+    res = {}
+    for packed in (False, True):
+        eng = _engine(cluster, hot, max_batch=m)
+        cluster.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_r, cnt)
+        res[packed] = [_run(L, eng, dev, *bt, packed) for bt in batches]
+        eng.close()
+    orc = H.cluster_replay_sharded(fid_r, cnt, batches, threads=4)
+    for b in range(len(batches)):
+        assert np.array_equal(res[True][b], res[False][b]), f"{hot} batch {b}: packed != arrays"
+        _mismatch(_decode(res[True][b]), orc[b], f"{hot} batch {b}")
+
+
+@pytest.mark.gpu
+def test_packed_entry_namespace_limiter():
+    """With a namespace limiter (GlobalRequestLimiter, a K9 pre-pass) the packed batch is unpacked on the
+    device and takes the sort path: TokenResults equal the array entry's."""
+    import torch
+    from sentinel_amd import _lib, cluster
+    from sentinel_amd.workload import ClusterTrace
+    L = _lib.load()
+    dev = torch.device("cuda", 0)
+    tr = ClusterTrace(n_rules=2000, lam=1_000_000)
+    fid_r, cnt = tr.rules()
+    res = {}
+    for packed in (False, True):
+        eng = _engine(cluster, "on", max_batch=1 << 16)
+        cluster.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_r, np.minimum(cnt, 200.0))
+        cluster.GlobalRequestLimiter(eng).init_if_absent("default", 20_000.0)
+        res[packed] = [_run(L, eng, dev, *tr.events(b << 16, 1 << 16), packed) for b in range(4)]
+        eng.close()
+    for b in range(4):
+        assert np.array_equal(res[True][b], res[False][b]), f"batch {b}"
+    st = np.concatenate([_decode(r)["status"] for r in res[True]])
+    assert (st == -2).any() and (st == 0).any()  # TOO_MANY_REQUEST from the limiter, passes
+
+
+@pytest.mark.gpu
+def test_c3_full_size_packed_device_entry_all_requests():
+    """BASELINE C3 at full size through the entry bench.py times: 1M cluster rules, four warm batches of 2^24
+    requests (the device-generated trace bench.py uses), packed records in HBM.  Every request of all four
+    batches equals the oracle (sharded replay of the same trace from the start), and the hot path was taken."""
+    import torch
+    from sentinel_amd import _lib, cluster
+    from sentinel_amd.workload import ClusterTrace, DeviceClusterGen, pack_requests
+    L = _lib.load()
+    dev = torch.device("cuda", 0)
+    tr = ClusterTrace()
+    fid_r, cnt = tr.rules()
+    gen = DeviceClusterGen(dev)
+    m = 1 << 24
+    eng = cluster.Engine(device=0, max_batch=m + 1024, max_rules=1 << 20)
+    cluster.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_r, cnt)
+    host, outs = [], []
+    for b in range(4):
+        f, a, p, t, base, n = gen.batch(b * m, m)
+        rec = pack_requests(f, a, p, t)
+        o = torch.zeros(n, dtype=torch.int64, device=dev)
+        rc = L.sga_request_tokens_packed_device(eng.handle, rec.data_ptr(), base, n, o.data_ptr(), None)
+        assert rc == 0, L.sga_last_error(eng.handle)
+        assert L.sga_sync(eng.handle) == 0
+        host.append((f.cpu().numpy(), a.cpu().numpy(), p.cpu().numpy(), t.cpu().numpy().astype(np.int64) + base))
+        outs.append(o.cpu().numpy())
+        if b == 3:
+            info = eng.batch_info()
+            assert info["hot_mode"] == 1 and info["flags"] == 0, info
+    eng.close()
+    orc = H.cluster_replay_sharded(fid_r, cnt, host, threads=16)
+    for b in range(4):
+        _mismatch(_decode(outs[b]), orc[b], f"C3 batch {b}")

@@ -182,3 +182,40 @@ def test_breaker_flows_trip_probe_half_open(grade):
     b5 = _batch(1, rng.integers(0, n_res, size=1000), t5, rt=rng.integers(1, 30, size=1000))
     b6 = _batch(0, rng.integers(0, n_res, size=5000), T0 + 13_000 + np.arange(5000))
     _check_batches(n_res, [b1, b2, b3, b4, b5, b6], degrade=degrade)
+
+
+def test_missing_thread_count_entry_fails_the_batch():
+    """The device check of k_pseg_key: a parameter event of a per-value segment flow whose thread-count entry
+    is missing (fault-injected with SGA_PSEG_FORCE_MISS=1, never expected otherwise) fails the batch with
+    SGA_EIO and the check's message, instead of leaving the event undecided.  Run in a child process (the
+    knob is read once per process); the same batch without the knob succeeds."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = f"""
+import sys
+sys.path.insert(0, {root!r})
+import numpy as np
+from tests.test_pseg_gpu import _batch, _param_stream, EV_HAS_PARAM
+from tests.test_configs_fullsize_gpu import _local
+rng = np.random.default_rng(3)
+res, vals, ts, acq = _param_stream(rng, 20_000, 2, 20, 2_000)
+b = _batch(0, res, ts, acq=acq, flags=np.full(len(ts), EV_HAS_PARAM), param=vals)
+eng, s = _local(2, param=[{{"resource": r, "count": 30.0}} for r in range(2)], max_batch=1 << 15)
+try:
+    s.submit(b["kind"], b["resource"], b["ts"], b["acquire"], b["flags"], b["rt"], b["param"])
+except Exception as e:
+    print("ERROR", e)
+else:
+    print("OK")
+eng.close()
+"""
+    out = {}
+    for knob in ("0", "1"):
+        env = dict(os.environ, SGA_PSEG_FORCE_MISS=knob)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[knob] = r.stdout.strip().splitlines()[-1]
+    assert out["0"] == "OK", out
+    assert out["1"].startswith("ERROR") and "rc=-5" in out["1"] and "k_pseg_key device check" in out["1"], out
