@@ -889,7 +889,11 @@ __global__ __launch_bounds__(kRunThreads) void k_results(BatchScratch sc, const 
 // kFzChunk: elements per workgroup in chunk mode (and the run records kept in LDS); the runs / results scans
 // walk blocks of kFzBlk elements, kFzPer per thread
 constexpr int kFzThreads = 256, kFzPer = 4, kFzBlk = kFzThreads * kFzPer, kFzChunk = 2048;
-constexpr int kFzShortRun = 4;  // closed-form runs of at most this many requests: results from the flows lane
+constexpr int kFzShortRun = 4;  // SGA_FZ_DEBUG bit 256 (A/B): the round-4 form -- runs of at most this many
+                                // requests answered by their flows lane, every other one by the results scan
+constexpr int kFzDirect = 32;   // closed-form runs of at most this many requests: TokenResults from the flows lane
+constexpr int kFzLong = 512;    // longer runs listed for the results phase (one wave per run); a full list
+                                // sends further runs to their flows lane as well
 
 // Profiling only (SGA_FZ_DEBUG bit 16): per-phase cycles of k_cold_fused summed over workgroups.
 __device__ unsigned long long g_fz_phase[8];
@@ -1098,7 +1102,9 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
     // prioritized index (relative to h0 in bin mode), acquire count | bucket delta << 8
     __shared__ RlT rl_buf[4 * kRl];
     RlT *rl_n = rl_buf, *rl_cp = rl_buf + kRl, *rl_p0 = rl_buf + 2 * kRl, *rl_ab = rl_buf + 3 * kRl;
-    __shared__ uint8_t rl_done[kRl];  // short closed-form runs answered by their flows lane
+    __shared__ uint32_t s_long[kFzLong];  // closed-form runs the flows lanes left to the results phase (heads)
+    __shared__ uint32_t s_nlong;
+    const bool scan_results = (dbg & 256) != 0;  // A/B: the round-4 results scan over every element
     __shared__ FAgg wtot[kFzThreads / 64];
     __shared__ uint32_t s_h0, s_E, s_wcnt[kFzThreads / 64];
     __shared__ uint32_t s_ncand, s_cbase, s_next, s_cand[2 * kFzThreads];
@@ -1253,7 +1259,6 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
                     rl_cp[head - h0] = (RlT)(run.np - run.hp);
                     rl_p0[head - h0] = (RlT)(h0 + run.hp - p0_rel);
                     rl_ab[head - h0] = (RlT)((uint32_t)acq | (bd << 8));
-                    rl_done[head - h0] = 0;
                 } else {  // global run arrays, indexed by head position
                     sc.run_start[head] = p + 1 - head;
                     sc.run_cp[head] = run.np - run.hp;
@@ -1271,6 +1276,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
     if (threadIdx.x == 0) {
         s_ncand = 0;
         s_next = kFzThreads;  // rules [0, kFzThreads) go to the lanes of the same index
+        s_nlong = 0;
     }
     __syncthreads();  // run records and plist (global, this workgroup) before the flows read them
     // next-hot-set candidates: counts of at least the floor (half the last pick threshold) are
@@ -1382,33 +1388,43 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
             ro.mode = RUN_DONE;
             rc.have = false;  // the record changed in memory
         }
-        if (fast && ri.n <= (uint32_t)kFzShortRun && r - h0 < rl_cap) {
-            // a short run's TokenResults from its flows lane (the results phase skips it): the run's elements
-            // loaded together at clamped positions, decided as the results phase would
-            uint64_t x[kFzShortRun];
-#pragma unroll
-            for (int u = 0; u < kFzShortRun; ++u) x[u] = el[r + min((uint32_t)u, ri.n - 1)];
-            uint32_t kp = 0;  // prioritized requests of the run before this one
-#pragma unroll
-            for (int u = 0; u < kFzShortRun; ++u) {
-                if ((uint32_t)u >= ri.n) break;
-                const uint32_t pr = el_prio(x[u]);
-                uint64_t res;
-                if ((uint32_t)u < ro.f) {
-                    const int64_t sum = ro.s0 + (int64_t)u * ri.a;
-                    res = pack_result(TRS_OK, j_d2i(ro.thr - (double)sum / ro.isec - (double)ri.a), 0);
-                } else if (pr && kp - ro.cpf < ro.cw) {
-                    res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)ro.wait);
-                } else {
-                    res = pack_result(TRS_BLOCKED, 0, 0);
-                }
-                if (!(dbg & 128)) out[el_idx(x[u])] = res;
-                kp += pr;
-            }
-            rl_done[r - h0] = 1;
-        } else {
-            sc.run_out[r] = ro;
+        // a closed-form run's TokenResults: from its flows lane when it is short (or the long-run list is
+        // full), else from a whole wave in the results phase (s_long)
+        bool direct = fast && ri.n <= (scan_results ? (uint32_t)kFzShortRun : (uint32_t)kFzDirect);
+        if (fast && !direct && !scan_results) {
+            const uint32_t k = atomicAdd(&s_nlong, 1u);
+            if (k < (uint32_t)kFzLong) s_long[k] = r;
+            else direct = true;
         }
+        if (direct) {
+            // the run's elements in chunks of 8, loaded together at clamped positions, decided as the results
+            // phase would (kp: prioritized requests of the run before the element)
+            uint32_t kp = 0;
+            for (uint32_t c0 = 0; c0 < ri.n; c0 += 8) {
+                uint64_t x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = el[r + min(c0 + (uint32_t)u, ri.n - 1)];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t loc = c0 + (uint32_t)u;
+                    if (loc >= ri.n) break;
+                    const uint32_t pr = el_prio(x[u]);
+                    uint64_t res;
+                    if (loc < ro.f) {
+                        const int64_t sum = ro.s0 + (int64_t)loc * ri.a;
+                        res = pack_result(TRS_OK, j_d2i(ro.thr - (double)sum / ro.isec - (double)ri.a), 0);
+                    } else if (pr && kp - ro.cpf < ro.cw) {
+                        res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)ro.wait);
+                    } else {
+                        res = pack_result(TRS_BLOCKED, 0, 0);
+                    }
+                    if (!(dbg & 128)) out[el_idx(x[u])] = res;
+                    kp += pr;
+                }
+            }
+            ro.mode = RUN_DONE;
+        }
+        if (scan_results || (fast && !direct)) sc.run_out[r] = ro;  // read by the results phase
         r += ri.n;
         if (r >= r1) {
             f = atomicAdd(&s_next, 1u);
@@ -1428,7 +1444,42 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
             sc.hot_cand[2 * k + 1] = s_cand[2 * threadIdx.x + 1];
         }
     }
-    // ---- 3 results (the scan again)
+    // ---- 3 results
+    if (!scan_results) {
+        // the listed long runs, one wave per run: 64 elements per step, the prioritized requests before each
+        // element from a ballot prefix
+        const uint32_t nl = (dbg & 2) ? 0u : min(s_nlong, (uint32_t)kFzLong);
+        const uint64_t lt = lanemask_lt64(lane);
+        for (uint32_t k = (uint32_t)wave; k < nl; k += kFzThreads / 64) {
+            const uint32_t hp = s_long[k];
+            const RunOut ro = sc.run_out[hp];
+            const uint32_t n = (hp - h0 < rl_cap) ? (uint32_t)rl_n[hp - h0] : sc.run_start[hp];
+            uint32_t kp0 = 0;
+            for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+                const uint32_t loc = c0 + (uint32_t)lane;
+                const uint64_t x = el[hp + min(loc, n - 1)];
+                const bool pr = loc < n && el_prio(x);
+                const uint64_t pb = __ballot(pr);
+                const uint32_t kp = kp0 + (uint32_t)__popcll(pb & lt);
+                kp0 += (uint32_t)__popcll(pb);
+                if (loc >= n) continue;
+                const int32_t a = el_acq(x);
+                uint64_t res;
+                if (loc < ro.f) {
+                    const int64_t sum = ro.s0 + (int64_t)loc * a;
+                    res = pack_result(TRS_OK, j_d2i(ro.thr - (double)sum / ro.isec - (double)a), 0);
+                } else if (pr && kp - ro.cpf < ro.cw) {
+                    res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)ro.wait);
+                } else {
+                    res = pack_result(TRS_BLOCKED, 0, 0);
+                }
+                if (!(dbg & 128)) out[el_idx(x)] = res;
+            }
+        }
+        fz_mark(dbg, 3, fzt);
+        return;
+    }
+    // (A/B knob) the round-4 results scan over every element
     carry = fagg_id();
     for (uint32_t b0 = h0; b0 < ((dbg & 2) ? h0 : E); b0 += kFzBlk) {
         const uint32_t e0 = b0 + threadIdx.x * kFzPer;
@@ -1463,9 +1514,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
         RunOut ro[kFzPer];
 #pragma unroll
         for (int k = 0; k < kFzPer; ++k) {
-            const bool done = head[k] - h0 < rl_cap && rl_done[head[k] - h0];
-            if (done) ro[k].mode = RUN_DONE;
-            else if (e0 + k < E && (k == 0 || head[k] != head[k - 1])) ro[k] = sc.run_out[head[k]];
+            if (e0 + k < E && (k == 0 || head[k] != head[k - 1])) ro[k] = sc.run_out[head[k]];
             else if (k > 0) ro[k] = ro[k - 1];
         }
 #pragma unroll
