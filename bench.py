@@ -46,8 +46,8 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) batches")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the first two timed batches")
     ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c4full", "c5a", "c5b"],
-                    help="BASELINE.json configuration (SURVEY.md 8(d)); c3 = the headline, the others run on one "
-                         "GPU through bench_local.py")
+                    help="BASELINE.json configuration (SURVEY.md 8(d)); c3 = the headline, the others through "
+                         "bench_local.py (c2 / c4 / c4full / c5b shard by resource over --gpus N)")
     return ap.parse_args()
 
 
@@ -68,14 +68,12 @@ def launch_ranks(args):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     if args.config != "c3":
-        if args.gpus != 1:
-            raise SystemExit("bench.py: --config c1/c2/c4/c4full/c5a/c5b run on one GPU")
         import bench_local
         bench_local.run(args)
         return
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -1,5 +1,11 @@
-"""`python bench.py --config c1|c2|c4|c5a|c5b`: the other BASELINE.json configurations (SURVEY.md 8(d)
-table) through the device-resident entries, one JSON line each (bench.py's contract; one GPU).
+"""`python bench.py --config c1|c2|c4|c4full|c5a|c5b [--gpus N]`: the other BASELINE.json configurations
+ through the device-resident entries, one JSON line each (bench.py's contract).
+
+Multi-GPU (c2, c4, c4full, c5b): resources shard by splitmix64(resource id) mod G, one process
+per GPU (bench.py's launcher), each rank holding its shard's rules and deciding its shard's events -- resources
+are independent on the local path without SystemRules or RELATE / CHAIN strategies, so there is no exchange.
+Weak scaling: each rank's batch has the full per-GPU size, drawn from the configuration's distribution
+restricted to its own resources (the share of a G-times larger global batch routed to it).
 
 A step is one pass of the local slot chain over one pre-generated, HBM-resident batch: the batch's
 entries (sga_submit_events_device), then the exits of the entries that passed (their resource id is
@@ -29,8 +35,23 @@ S_NODE, S_WARMUP_EXTRA, S_RL, S_WU, S_WURL = 192, 64, 8, 16, 24
 S_PARAM, S_PARAM_THROTTLE, S_BREAKER = 24, 16, 32
 
 
-def _zipf(rng, n_items, size, s=1.1):
+SHARD = (0, 1)  # (rank, G) of this process (run_local sets it before building the configuration)
+
+
+def own_resources(n_res):
+    """The resource ids this rank owns: splitmix64(id) mod G == rank (all of them on one GPU)."""
+    from sentinel_amd.workload import shard_of
+    rank, g = SHARD
+    if g == 1:
+        return np.ones(n_res, bool)
+    return shard_of(np.arange(n_res, dtype=np.int64), g) == rank
+
+
+def _zipf(rng, n_items, size, s=1.1, mask=None):
+    """Zipf(s) over n_items; with `mask`, the distribution restricted to those items (a shard's events)."""
     p = 1.0 / np.arange(1, n_items + 1) ** s
+    if mask is not None:
+        p = np.where(mask, p, 0.0)
     p /= p.sum()
     return rng.choice(n_items, size=size, p=p)
 
@@ -72,15 +93,18 @@ def _cfg_c2(rng, n=1 << 24):
     flow = []
     beh = rng.random(n_res)
     cnt = rng.integers(5, 5001, size=n_res)
+    own = own_resources(n_res)
     for r in range(n_res):
+        if not own[r]:
+            continue
         if beh[r] < 0.4:
             flow.append(dict(resource=r, count=float(cnt[r])))
         elif beh[r] < 0.7:
             flow.append(dict(resource=r, count=float(cnt[r]), control_behavior=2, max_queueing_time_ms=500))
         else:
             flow.append(dict(resource=r, count=float(cnt[r]), control_behavior=1, warm_up_period_sec=10))
-    res = _zipf(rng, n_res, n)
-    ts = T0 + np.arange(n) // 10_000  # lambda = 1e7 / virtual s
+    res = _zipf(rng, n_res, n, mask=None if SHARD[1] == 1 else own)
+    ts = T0 + np.arange(n) // 10_000  # lambda = 1e7 / virtual s (per GPU)
     acq = np.where(rng.random(n) < 0.05, rng.integers(2, 6, size=n), 1)
     b = Batch(res, ts, acq=acq, exit_rt=rng.geometric(1.0 / 5.0, size=n))
     return dict(name="C2 100k FlowRules 40% Default / 30% RateLimiter(500 ms) / 30% WarmUp(10 s), Zipf(1.1), "
@@ -95,12 +119,14 @@ def _cfg_c4(rng):
 def _cfg_c4_common(rng, fold):
     n_res, n = 10_000, 1 << 22
     param = []
+    own = own_resources(n_res)
     for r in range(n_res):
         p = dict(resource=r, count=float(rng.integers(5, 101)))
         if rng.random() < 0.1:
             p.update(control_behavior=2, max_queueing_time_ms=0)
-        param.append(p)
-    res = _zipf(rng, n_res, n)
+        if own[r]:
+            param.append(p)
+    res = _zipf(rng, n_res, n, mask=None if SHARD[1] == 1 else own)
     vals = _zipf(rng, 10_000_000, n)
     if fold:
         vals = vals % 4000  # pinned mode: <= 4000 keys per rule (no CacheMap eviction)
@@ -122,14 +148,17 @@ def _cfg_c4full(rng):
 def _cfg_c5b(rng):
     n_res, n = 10_000, 1 << 22
     degrade = []
+    own = own_resources(n_res)
     for r in range(n_res):
+        if not own[r]:
+            continue
         if r % 2 == 0:
             degrade.append(dict(resource=r, grade=0, count=50.0, slow_ratio_threshold=0.5, min_request_amount=5,
                                 stat_interval_ms=1000, time_window=5))
         else:
             degrade.append(dict(resource=r, grade=1, count=0.2, min_request_amount=5, stat_interval_ms=1000,
                                 time_window=5))
-    res = _zipf(rng, n_res, n)
+    res = _zipf(rng, n_res, n, mask=None if SHARD[1] == 1 else own)
     ts = T0 + np.arange(n) // 10_000
     rt = np.clip(np.round(rng.lognormal(mean=np.log(20.0), sigma=1.0, size=n)), 1, 10_000)
     b = Batch(res, ts, exit_rt=rt, exit_err=rng.random(n) < 0.03)
@@ -301,15 +330,49 @@ def _cpu_local(cfg, b):
 
 
 def run_local(args, cfg_name):
+    global SHARD
     import torch
     from sentinel_amd.cluster import Engine
     from sentinel_amd.local import LocalSentinel
-    rng = np.random.default_rng({"c1": 101, "c2": 102, "c4": 104, "c4full": 104, "c5b": 105}[cfg_name])
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus={args.gpus}")
+    if world > 1 and cfg_name == "c1":
+        raise SystemExit("bench.py: C1 is one resource (nothing to shard); run it with --gpus 1")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")  # barriers and the max-over-ranks timing (CPU tensors)
+        if os.environ.get("SGA_BENCH_ONE_DEVICE") == "1":
+            local = 0  # rehearsal of the N-rank path on a one-GPU box
+    SHARD = (rank, world)
+    seed = {"c1": 101, "c2": 102, "c4": 104, "c4full": 104, "c5b": 105}[cfg_name]
+    rng = np.random.default_rng(seed if world == 1 else [seed, rank, world])
     cfg = {"c1": _cfg_c1, "c2": _cfg_c2, "c4": _cfg_c4, "c4full": _cfg_c4full, "c5b": _cfg_c5b}[cfg_name](rng)
     b = cfg["batch"]
-    dev = torch.device("cuda", 0)
+    if os.environ.get("SGA_BENCH_DRY") == "1":  # launch and routing check only (tests, CPU)
+        own = own_resources(cfg["n_res"])
+        line = {"dry": True, "rank": rank, "world": world, "config": cfg_name, "events": int(b.n),
+                "own_resources": int(own.sum()), "events_on_own": bool(own[b.res].all()),
+                "rules": len(cfg.get("flow", []) or cfg.get("param", []) or cfg.get("degrade", []))}
+        if dist is not None:
+            t = torch.tensor([float(b.n)], dtype=torch.float64)
+            dist.all_reduce(t)
+            line["events_all_ranks"] = float(t.item())
+        out_dir = os.environ.get("SGA_BENCH_DRY_OUT")
+        if out_dir:
+            with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as fh:
+                fh.write(json.dumps(line))
+        else:
+            print(json.dumps(line), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return None
+    dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    eng = Engine(device=0, max_batch=b.n)
+    eng = Engine(device=local, max_batch=b.n)
     s = LocalSentinel(eng, [f"r{i}" for i in range(cfg["n_res"])])
     _load_rules(s, cfg)
     stream = torch.cuda.Stream(dev)  # every call and the exit masking run on this one stream
@@ -364,6 +427,8 @@ def run_local(args, cfg_name):
     torch.cuda.synchronize(dev)
     s.device_status()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if dist is not None:
+        dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(stream)
@@ -372,18 +437,29 @@ def run_local(args, cfg_name):
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
     s.device_status()  # raises if a chunk was rejected or a parameter map filled
     if not first:  # no warmup step: the first timed step was the fresh one (its arrays were overwritten since)
         first = None
     gpu_s = ev0.elapsed_time(ev1) / 1e3
     d = dec.cpu().numpy()
-    n_ent = b.n * args.steps
+    n_ent_rank = b.n * args.steps
+    n_ent = n_ent_rank
+    if dist is not None:  # max of the ranks' times, sum of their entries
+        tmax = torch.tensor([wall, gpu_s], dtype=torch.float64)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = torch.tensor([float(n_ent_rank)], dtype=torch.float64)
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        wall, gpu_s = float(tmax[0]), float(tmax[1])
+        n_ent = int(tsum[0])
     n_exit = int(((d == 0) | (d == 4)).sum()) * args.steps if has_exit else 0
     e_in = E_PARAM_ENTRY if cfg.get("param") else E_ENTRY
-    bytes_alg = n_ent * (e_in + E_DEC) + n_exit * E_EXIT + _state_bytes(cfg, b) * args.steps
+    # per GPU (rank 0's shard): the roofline is a per-GPU figure
+    bytes_alg = n_ent_rank * (e_in + E_DEC) + n_exit * E_EXIT + _state_bytes(cfg, b) * args.steps
     achieved = bytes_alg / gpu_s / 1e9
     cpu, parity = None, None
-    if not args.no_cpu:
+    if not args.no_cpu and rank == 0:
         o_dec, o_wait, cpu = _cpu_local(cfg, b)
         if first:
             bad_d = int((first["dec"] != o_dec).sum())
@@ -394,6 +470,11 @@ def run_local(args, cfg_name):
             if bad_d or bad_w:
                 raise AssertionError(f"bench sample differs from the oracle: {parity}")
     eng.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank != 0:
+        return None
     # HBM traffic per step from the committed rocprofv3 PMC passes of this line (tools/r04_pmc.sh)
     traffic, traffic_src = None, None
     tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", f"traffic_{cfg_name}.json")
@@ -403,11 +484,13 @@ def run_local(args, cfg_name):
         traffic, traffic_src = tj["traffic_bytes_per_step"], f"profiles/traffic_{cfg_name}.json ({tj.get('run', '')})"
     return {
         "metric": f"admission decisions/sec, config {cfg_name.upper()} (SURVEY.md 8(d)); % HBM peak",
-        "value": n_ent / wall, "unit": "decisions/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "value": n_ent / wall, "unit": "decisions/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "int64", "data": "synthetic (numpy, seeded), staged in HBM before the timed region",
-        "config": {"workload": cfg["name"], "entries_per_step": b.n, "exits_per_step": n_exit // max(1, args.steps),
-                   "resources": cfg["n_res"], "parallelism": "shard1"},
+        "config": {"workload": cfg["name"], "entries_per_step_per_gpu": b.n,
+                   "exits_per_step": n_exit // max(1, args.steps), "resources": cfg["n_res"],
+                   "parallelism": f"shard{world}",
+                   "sharding": "resources by splitmix64(resource id) mod G, no exchange (weak scaling)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "sga_submit_events_device pipeline (entries, then masked exits), torch events on "
@@ -546,5 +629,8 @@ def run_rls(args):
 
 def run(args):
     name = args.config.lower()
+    if name == "c5a" and args.gpus != 1:
+        raise SystemExit("bench.py: --config c5a runs on one GPU")
     line = run_rls(args) if name == "c5a" else run_local(args, name)
-    print(json.dumps(line), flush=True)
+    if line is not None:
+        print(json.dumps(line), flush=True)

@@ -1117,19 +1117,26 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
     uint32_t p0_rel = 0;    // bin mode: rl_p0 holds plist index - h0
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t *el = el_in;
+    bool in_lds = false;    // bin mode: the ordered bin is the LDS image sel (element p at sel[p - lds_base])
+    uint32_t lds_base = 0;
+    // element p: an LDS read (ds_read) when the bin is in LDS -- a flat pointer into LDS would make every
+    // element read wait for all outstanding global stores as well
     uint32_t h0, E;
     if constexpr (kMode == kFzBin) {
         const uint32_t B0 = sc.pstart[blockIdx.x], B1 = sc.pstart[blockIdx.x + 1];
         if (B0 >= B1) return;
         unsigned long long ot = 0;
         fz_mark(dbg, 0, ot);
-        const bool in_lds = B1 - B0 <= (uint32_t)kBinLds && !(dbg & 64);
-        bin_order(el_in, in_lds ? sel : es, in_lds ? B0 : 0u, B0, B1, lb, reinterpret_cast<uint32_t *>(rl_buf), s_wcnt);
+        in_lds = B1 - B0 <= (uint32_t)kBinLds && !(dbg & 64);
+        // (two calls, so each inlined copy knows its store's address space: ds_write into the LDS image)
+        if (in_lds) bin_order(el_in, sel, B0, B0, B1, lb, reinterpret_cast<uint32_t *>(rl_buf), s_wcnt);
+        else bin_order(el_in, es, 0u, B0, B1, lb, reinterpret_cast<uint32_t *>(rl_buf), s_wcnt);
         rl_cap = in_lds ? (uint32_t)kBinLds : 0u;
         p0_rel = B0;
         fz_mark(dbg, 4, ot);
-        // element p of the bin at el[p]: the LDS image shifted by the bin start (a flat address)
-        el = in_lds ? reinterpret_cast<const uint64_t *>(reinterpret_cast<uintptr_t>(&sel[0]) - (uintptr_t)B0 * 8u) : es;
+        // element p of the bin: sel[p - B0] (LDS image) or es[p]
+        el = es;
+        lds_base = B0;
         h0 = B0;
         E = B1;
     } else {
@@ -1191,6 +1198,17 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
     __syncthreads();
     E = s_E;
     }
+    // element p of the sorted cold elements: a ds_read of the bin's LDS image, or a global load.  The two
+    // pointers keep their address spaces, so the choice stays a branch: one flat load for both would wait for
+    // every outstanding global store as well.
+    using LdsU64 = __attribute__((address_space(3))) uint64_t;
+    using GlbU64 = __attribute__((address_space(1))) const uint64_t;
+    const LdsU64 *lds_el = (const LdsU64 *)(sel) - lds_base;
+    const GlbU64 *glb_el = (const GlbU64 *)el;
+    auto EL = [&](uint32_t p) -> uint64_t {
+        if (kBin && in_lds) return lds_el[p];
+        return glb_el[p];
+    };
     unsigned long long fzt = 0;
     fz_mark(dbg, 0, fzt);
     // ---- 1 runs (blocks of kFzBlk elements over [h0, E))
@@ -1200,8 +1218,8 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
         const uint32_t e0 = b0 + threadIdx.x * kFzPer;
         uint64_t x[kFzPer];
 #pragma unroll
-        for (int k = 0; k < kFzPer; ++k) x[k] = e0 + k < E ? el[e0 + k] : 0ull;
-        uint64_t px = e0 > h0 && e0 - 1 < E ? el[e0 - 1] : 0ull;
+        for (int k = 0; k < kFzPer; ++k) x[k] = e0 + k < E ? EL(e0 + k) : 0ull;
+        uint64_t px = e0 > h0 && e0 - 1 < E ? EL(e0 - 1) : 0ull;
         FAgg acc = fagg_id();
         uint32_t nfl = 0;
         bool hd[kFzPer], fh[kFzPer];
@@ -1249,7 +1267,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
             }
             if (pr) sc.plist[h0 + np_before] = p;
             // run end: this is the last element of its run
-            const bool last = p + 1 >= E || (k + 1 < kFzPer ? hd[k + 1] : (p + 1 < E && el_runkey(el[p + 1]) != el_runkey(x[k])));
+            const bool last = p + 1 >= E || (k + 1 < kFzPer ? hd[k + 1] : (p + 1 < E && el_runkey(EL(p + 1)) != el_runkey(x[k])));
             if (last) {
                 const uint32_t head = run.hpos - 1;
                 const int32_t acq = run.mn == run.mx ? run.mn : 0;  // 0: mixed or escaped -> replay
@@ -1380,7 +1398,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
         }
         if (!fast) {
             for (uint32_t j = r; j < r + ri.n; ++j) {
-                const uint32_t i = el_idx(el[j]);
+                const uint32_t i = el_idx(EL(j));
                 const int64_t t = ts_base + (int64_t)in.ts_at(i);
                 const bool p = !simple && in.prio_at(i);
                 out[i] = request_exact(st, s, t, in.acq_at(i), p, simple);
@@ -1403,7 +1421,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
             for (uint32_t c0 = 0; c0 < ri.n; c0 += 8) {
                 uint64_t x[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) x[u] = el[r + min(c0 + (uint32_t)u, ri.n - 1)];
+                for (int u = 0; u < 8; ++u) x[u] = EL(r + min(c0 + (uint32_t)u, ri.n - 1));
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const uint32_t loc = c0 + (uint32_t)u;
@@ -1457,7 +1475,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
             uint32_t kp0 = 0;
             for (uint32_t c0 = 0; c0 < n; c0 += 64) {
                 const uint32_t loc = c0 + (uint32_t)lane;
-                const uint64_t x = el[hp + min(loc, n - 1)];
+                const uint64_t x = EL(hp + min(loc, n - 1));
                 const bool pr = loc < n && el_prio(x);
                 const uint64_t pb = __ballot(pr);
                 const uint32_t kp = kp0 + (uint32_t)__popcll(pb & lt);
@@ -1485,8 +1503,8 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
         const uint32_t e0 = b0 + threadIdx.x * kFzPer;
         uint64_t x[kFzPer];
 #pragma unroll
-        for (int k = 0; k < kFzPer; ++k) x[k] = e0 + k < E ? el[e0 + k] : 0ull;
-        uint64_t px = e0 > h0 && e0 - 1 < E ? el[e0 - 1] : 0ull;
+        for (int k = 0; k < kFzPer; ++k) x[k] = e0 + k < E ? EL(e0 + k) : 0ull;
+        uint64_t px = e0 > h0 && e0 - 1 < E ? EL(e0 - 1) : 0ull;
         FAgg acc = fagg_id();
         bool hd[kFzPer];
 #pragma unroll
@@ -2485,6 +2503,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
         z.start = stb;
         *hrun_at(sc, h, bd_lo + lane) = z;
         sc.hfin[(size_t)(bd_lo + lane) * kHot + h] = make_uint4(0u, 0u, 0u, stb);
+        sc.hfs[(size_t)(bd_lo + lane) * kHot + h] = make_uint2(0u, stb);
     }
     uint64_t rm = __ballot(nrun > 0);
     if (!rm) return;
@@ -2604,6 +2623,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
             r.ok = ok ? 1 : 0;
             *hrun_at(sc, h, b) = r;
             sc.hfin[(size_t)b * kHot + h] = make_uint4((uint32_t)s0, (uint32_t)((uint64_t)s0 >> 32), f, j0);
+            sc.hfs[(size_t)b * kHot + h] = make_uint2(f, j0);
         }
     }
 }
@@ -2805,6 +2825,107 @@ __global__ __launch_bounds__(kFinGThreads) void k_hot_final_g(ClusterState st, B
     }
 }
 
+// k_hot_final_p (A/B knob SGA_FIN_P=1; measured slower than k_hot_final_g beside the cold stage, 0.78 against
+// 0.74-0.76 ms per C3 batch): persistent workgroups over
+// consecutive rank segments.  A workgroup stages (f, start) of every hot id's run in its first segment's bucket
+// (hfs, 32 KB) once, and each segment's hbase row (16 KB) in LDS, so a hot request's fate -- pass (rank inside
+// the run's pass prefix) or block -- costs two LDS reads; only the passing requests (and any request of another
+// bucket) gather their run record, after the fate pass, all such gathers of a wave's 16 rounds in flight together.
+constexpr int kFinPThreads = 512;
+constexpr int kFinPRounds = kHotSeg / kFinPThreads;  // codes per thread per segment (16)
+constexpr uint32_t kFinPrioWgsP = 32;
+__global__ __launch_bounds__(kFinPThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_hot_final_p(ClusterState st, BatchScratch sc, uint32_t n,
+                                                             const uint64_t *__restrict__ el,
+                                                             uint64_t *__restrict__ out, uint32_t segs_per_wg) {
+    __shared__ uint2 fs[kHot];       // (f, start) of each hot id's run in bucket b0
+    __shared__ uint32_t base[kHot];  // the segment's rank base per hot id
+    if (!sc.counters[CTL_MODE]) return;
+    if (blockIdx.x < kFinPrioWgsP) {
+        prio_results_range(st, sc, el, out, blockIdx.x * kFinPThreads + threadIdx.x, kFinPrioWgsP * kFinPThreads);
+        return;
+    }
+    const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
+    const uint32_t seg0 = (blockIdx.x - kFinPrioWgsP) * segs_per_wg, seg1 = min(nseg, seg0 + segs_per_wg);
+    if (seg0 >= seg1) return;
+    const uint32_t nhot = hot_count(sc);
+    // b0: the bucket holding the first request of seg0 (bucket starts hbnd[b], b in (bd_lo, bd_hi])
+    const uint32_t bd_lo = sc.counters[CTL_BDLO];
+    const uint32_t bd_hi = min(sc.counters[CTL_BDHI], (uint32_t)kHotBuckets - 1);
+    uint32_t b0 = bd_lo;
+    for (uint32_t b = bd_lo + 1; b <= bd_hi; ++b)
+        if (sc.hbnd[b] <= seg0 * (uint32_t)kHotSeg) b0 = b;
+    for (uint32_t h = threadIdx.x; h < nhot; h += kFinPThreads) fs[h] = sc.hfs[(size_t)b0 * kHot + h];
+    uint32_t cn[kFinPRounds];
+    auto load_codes = [&](uint32_t seg) {
+#pragma unroll
+        for (int u = 0; u < kFinPRounds; ++u)
+            cn[u] = sc.hcode[min(seg * (uint32_t)kHotSeg + (uint32_t)u * kFinPThreads + threadIdx.x, n - 1)];
+    };
+    load_codes(seg0);
+    for (uint32_t seg = seg0; seg < seg1; ++seg) {
+        __syncthreads();  // the previous segment's base reads are done (and fs is in place)
+        for (uint32_t h = threadIdx.x; h < nhot; h += kFinPThreads) base[h] = sc.hbase[(size_t)seg * kHot + h];
+        __syncthreads();
+        uint32_t code[kFinPRounds];
+#pragma unroll
+        for (int u = 0; u < kFinPRounds; ++u) code[u] = cn[u];
+        if (seg + 1 < seg1) load_codes(seg + 1);  // the next segment's codes in flight during this one
+        // per half of the rounds: the fate pass (blocked requests answered from LDS), then the gathers of the
+        // passing requests (and of requests of another bucket), all in flight together, then their results
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            constexpr int kH = kFinPRounds / 2;
+            uint32_t need = 0, loc[kH];
+#pragma unroll
+            for (int v = 0; v < kH; ++v) {
+                const int u = hf * kH + v;
+                const uint32_t i = seg * (uint32_t)kHotSeg + (uint32_t)u * kFinPThreads + threadIdx.x;
+                const uint32_t cd = code[u];
+                loc[v] = 0;
+                if (i >= n || cd == kNoCode || (cd >> 31)) continue;  // cold, invalid, prioritized: answered elsewhere
+                const uint32_t h = cd & 0xFFFu;
+                const uint32_t r = base[h] + ((cd >> 12) & 0x1FFFu);
+                if ((cd >> 25) != b0) {
+                    need |= 1u << v;
+                    loc[v] = r;
+                    continue;
+                }
+                const uint2 w = fs[h];
+                loc[v] = r - w.y;
+                if (loc[v] < w.x) need |= 1u << v;
+                else out[i] = pack_result(TRS_BLOCKED, 0, 0);
+            }
+            if (!__ballot(need != 0)) continue;  // wave-uniform: every hot request of these rounds blocked
+            uint4 ra[kH], rb[kH];
+#pragma unroll
+            for (int v = 0; v < kH; ++v) {  // unconditional gathers (lanes without a need read one shared line)
+                const uint32_t cd = code[hf * kH + v];
+                const bool nd = (need >> v) & 1u;
+                const uint4 *hp = reinterpret_cast<const uint4 *>(nd ? hrun_at(sc, cd & 0xFFFu, cd >> 25) : sc.hrun);
+                ra[v] = hp[0];  // s0, thr
+                rb[v] = hp[1];  // isec, f, start
+            }
+#pragma unroll
+            for (int v = 0; v < kH; ++v) {
+                if (!((need >> v) & 1u)) continue;
+                const int u = hf * kH + v;
+                const uint32_t i = seg * (uint32_t)kHotSeg + (uint32_t)u * kFinPThreads + threadIdx.x;
+                const uint32_t cd = code[u];
+                const uint32_t local = (cd >> 25) != b0 ? loc[v] - rb[v].w : loc[v];
+                uint64_t res;
+                if (local < rb[v].z) {
+                    const int64_t sum = i64_of(ra[v].x, ra[v].y) + (int64_t)local;
+                    res = pack_result(TRS_OK, j_d2i(f64_of(ra[v].z, ra[v].w) - (double)sum / f64_of(rb[v].x, rb[v].y) - 1.0),
+                                      0);
+                } else {
+                    res = pack_result(TRS_BLOCKED, 0, 0);
+                }
+                out[i] = res;
+            }
+        }
+    }
+}
+
 // ---- next batch's hot set: rules with at least T requests in this batch, T the smallest power of
 // two (>= hot_min) that admits at most kHot rules; all of them with the window length of the
 // busiest one, 1 < sampleCount <= 64 (the occupy path needs 1000 / sampleCount > 0).  Candidates:
@@ -2831,7 +2952,7 @@ __device__ __forceinline__ bool hot_candidate(const ClusterState &st, const Batc
     return hot_eligible(st.param[slot]);
 }
 
-__global__ __launch_bounds__(kThreads) void k_hot_hist(ClusterState st, BatchScratch sc, uint32_t hot_min) {
+__device__ __forceinline__ void hot_hist_body(const ClusterState &st, const BatchScratch &sc, uint32_t hot_min) {
     __shared__ uint32_t bins[32];
     __shared__ unsigned long long best;
     if (threadIdx.x < 32) bins[threadIdx.x] = 0;
@@ -2850,6 +2971,10 @@ __global__ __launch_bounds__(kThreads) void k_hot_hist(ClusterState st, BatchScr
     __syncthreads();
     if (threadIdx.x < 32 && bins[threadIdx.x]) atomicAdd(&sc.hot_ctl[8 + threadIdx.x], bins[threadIdx.x]);
     if (threadIdx.x == 0 && best) atomicMax(reinterpret_cast<unsigned long long *>(sc.hot_ctl + 4), best);
+}
+
+__global__ __launch_bounds__(kThreads) void k_hot_hist(ClusterState st, BatchScratch sc, uint32_t hot_min) {
+    hot_hist_body(st, sc, hot_min);
 }
 
 // the key table entry of a rule entering (v = hot id) or leaving (kColdId) the hot set
@@ -2871,7 +2996,7 @@ __global__ __launch_bounds__(kThreads) void k_hot_clear(ClusterState st, BatchSc
 // Hot ids go out in descending count-bin order (bin b holds counts in [2^b, 2^(b+1))): each bin
 // owns a block of ids, so after k_hot_fin compacts the holes left by rules of another window
 // length, the hottest rules have the smallest ids (k_hot_final caches the first kFinCache of them).
-__global__ __launch_bounds__(kThreads) void k_hot_pick(ClusterState st, BatchScratch sc, uint32_t hot_min) {
+__device__ __forceinline__ void hot_pick_body(const ClusterState &st, const BatchScratch &sc, uint32_t hot_min) {
     __shared__ uint32_t thr, wbest, bcnt[32], bbase[32], lcnt[32], gbase[32];
     if (threadIdx.x < 32) bcnt[threadIdx.x] = sc.hot_ctl[8 + threadIdx.x];
     __syncthreads();
@@ -2915,12 +3040,17 @@ __global__ __launch_bounds__(kThreads) void k_hot_pick(ClusterState st, BatchScr
     }
 }
 
+__global__ __launch_bounds__(kThreads) void k_hot_pick(ClusterState st, BatchScratch sc, uint32_t hot_min) {
+    hot_pick_body(st, sc, hot_min);
+}
+
 // Compacts the picked ids (stable, so the count-bin order stays) and publishes them.  Holes are
 // left only by candidates of another window length; a rule whose id moves is renamed here.
 constexpr int kFinThreads = 1024;
-constexpr int kFinPer = kHot / kFinThreads;
-__global__ __launch_bounds__(kFinThreads) void k_hot_fin(ClusterState st, BatchScratch sc) {
-    __shared__ uint32_t wsum[kFinThreads / 64];
+template <int kNT>
+__device__ __forceinline__ void hot_fin_body(const ClusterState &st, const BatchScratch &sc, uint32_t *wsum) {
+    constexpr int kFinPer = kHot / kNT;
+    constexpr int kFinThreads = kNT;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t sl[kFinPer], cnt = 0;
 #pragma unroll
@@ -2970,6 +3100,40 @@ __global__ __launch_bounds__(kFinThreads) void k_hot_fin(ClusterState st, BatchS
         sc.counters_last[threadIdx.x] = sc.counters[threadIdx.x];
         sc.counters[threadIdx.x] = 0;
     }
+}
+
+__global__ __launch_bounds__(kFinThreads) void k_hot_fin(ClusterState st, BatchScratch sc) {
+    __shared__ uint32_t wsum[kFinThreads / 64];
+    hot_fin_body<kFinThreads>(st, sc, wsum);
+}
+
+// The next hot set in three launches (default: k_hot_next_a, k_hot_pick, k_hot_fin), or two (SGA_HOT_NEXT=2, an
+// A/B knob; 4 keeps the four kernels above):
+// k_hot_next_a = k_hot_hist + k_hot_clear (the clear only has to precede the picks); k_hot_next_b =
+// k_hot_pick, then the last workgroup to finish runs k_hot_fin (a done counter in hot_ctl).
+constexpr int kHotNextDone = 100;  // hot_ctl word: k_hot_next_b workgroups done
+__global__ __launch_bounds__(kThreads) void k_hot_next_a(ClusterState st, BatchScratch sc, uint32_t hot_min) {
+    const uint32_t nh = hot_count(sc);
+    for (uint32_t h = blockIdx.x * kThreads + threadIdx.x; h < nh; h += gridDim.x * kThreads) {
+        const uint32_t slot = sc.hot_slot[h];
+        sc.hot_of[slot] = kColdId;
+        hot_fid_set(st, slot, kColdId);
+    }
+    hot_hist_body(st, sc, hot_min);
+}
+
+__global__ __launch_bounds__(kThreads) void k_hot_next_b(ClusterState st, BatchScratch sc, uint32_t hot_min) {
+    __shared__ uint32_t wsum[kThreads / 64];
+    __shared__ uint32_t s_last;
+    hot_pick_body(st, sc, hot_min);
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&sc.hot_ctl[kHotNextDone], 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    hot_fin_body<kThreads>(st, sc, wsum);
+    if (threadIdx.x == 0) sc.hot_ctl[kHotNextDone] = 0;
 }
 
 __global__ void k_hot_reset(ClusterState st, BatchScratch sc, uint32_t nslots_cap) {
@@ -3606,7 +3770,10 @@ __global__ __launch_bounds__(kPLruSortThreads) void k_plru_sort(CParamState st, 
     const uint64_t q = st.pq[P.boff + j];
     PLruRec *rec = st.lpool + q + 1;
     const uint32_t n = (uint32_t)min<uint64_t>(st.lpool[q].stamp, plru_qcap(P));
-    if (n > P.cap && threadIdx.x == 0) atomicOr(&st.ctl[1], 4u);  // a free-mode map holds at most cap keys
+    if (n > P.cap) {  // a free-mode map holds at most cap keys: never expected; the host fails the call
+        if (threadIdx.x == 0) atomicOr(&st.ctl[1], 4u);
+        return;  // (padding n past cap to a power of two could run past the area's 2 cap + 2 records)
+    }
     uint32_t np2 = 1;
     while (np2 < n) np2 <<= 1;
     if (np2 <= (uint32_t)kPLruLds) {
@@ -3710,6 +3877,15 @@ static uint32_t fin_cache() {  // profiling knob: SGA_FIN_CACHE=0 turns k_hot_fi
 static void launch_hot_final(const ClusterState &st, BatchScratch &sc, uint32_t n, const uint64_t *pel, uint64_t *out,
                              hipStream_t s) {
     static const bool lds = getenv("SGA_FIN_LDS") && atoi(getenv("SGA_FIN_LDS")) == 1;
+    static const bool pers = getenv("SGA_FIN_P") && atoi(getenv("SGA_FIN_P")) == 1;
+    if (pers) {  // persistent: about two workgroups per CU, consecutive segments each
+        const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
+        const uint32_t wgs = std::min<uint32_t>(nseg, 512);
+        const uint32_t per = (nseg + wgs - 1) / wgs;
+        hipLaunchKernelGGL(k_hot_final_p, dim3((nseg + per - 1) / per + kFinPrioWgsP), dim3(kFinPThreads), 0, s, st, sc,
+                           n, pel, out, per);
+        return;
+    }
     if (lds) {
         const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
         hipLaunchKernelGGL(k_hot_final, dim3(nseg + kFinPrioWgs), dim3(kFinWgThreads), 0, s, st, sc, n, pel, out,
@@ -3722,6 +3898,16 @@ static void launch_hot_final(const ClusterState &st, BatchScratch &sc, uint32_t 
 
 static int hot_overlap() {  // A/B knob: SGA_HOT_OVERLAP=0 runs the hot side after the cold stage
     static const int v = getenv("SGA_HOT_OVERLAP") ? atoi(getenv("SGA_HOT_OVERLAP")) : 1;
+    return v;
+}
+
+// Stream schedule of a hot-path batch (A/B knob SGA_HOT_SCHED): 1 (default) -- the hot side (count scans,
+// prioritized sort, hot runs, hot results) on side streams beside the cold partition and the cold stage; 2 -- the
+// hot side's short kernels on the batch stream beside the cold partition (side stream), then the hot results (third
+// stream) beside the cold stage.  Measured (C3, MI355X): 2 is slower, 0.83 against 0.76-0.78 ms per batch -- the hot
+// results and the cold stage side by side slow each other down more than one after the other would.
+static int hot_sched() {
+    static const int v = getenv("SGA_HOT_SCHED") ? atoi(getenv("SGA_HOT_SCHED")) : 1;
     return v;
 }
 
@@ -3794,6 +3980,7 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up((size_t)kHotBuckets * kHot * 2) + align_up(kHotBuckets * 4);     // hpre, hbnd
     b += align_up((size_t)kHot * kHotBuckets * sizeof(HotRun));                   // hrun
     b += align_up((size_t)kHot * kHotBuckets * sizeof(uint4));                    // hfin
+    b += align_up((size_t)kHot * kHotBuckets * sizeof(uint2));                    // hfs
     b += align_up(kHot * sizeof(double2));                                        // hthr
     b += align_up(cap * 4);                                                        // prank
     b += 3 * align_up(kHot * 4);                                                   // plo, phi, hot_tot
@@ -3867,6 +4054,7 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.hbnd = (uint32_t *)take(kHotBuckets * 4);
     sc.hrun = (HotRun *)take((size_t)kHot * kHotBuckets * sizeof(HotRun));
     sc.hfin = (uint4 *)take((size_t)kHot * kHotBuckets * sizeof(uint4));
+    sc.hfs = (uint2 *)take((size_t)kHot * kHotBuckets * sizeof(uint2));
     sc.hthr = (double2 *)take(kHot * sizeof(double2));
     sc.prank = (uint32_t *)take(cap * 4);
     sc.plo = (uint32_t *)take(kHot * 4);
@@ -4030,8 +4218,46 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const ReqIn &
     hipLaunchKernelGGL(hkb, dim3(nseg), dim3(kKeyThreads), 0, s, st, sc, in, ts_base, n, out, fz_debug(), d0, khist,
                        ntiles_sort);
     hipLaunchKernelGGL(k_hot_mode, dim3(1), dim3(1024), 0, s, sc, nseg * kKeyWaves, nseg, ts_base);
-    // the hot side's count scans and prioritized sort on the side stream, beside the cold sort
     const bool ovl = hot_overlap() && !(fz_debug() & 16);
+    sc.sched2 = ovl && !pipelined && hot_sched() == 2;
+    if (sc.sched2) {
+        // the cold partition (or sort) on the side stream; the hot side's short kernels on the batch stream
+        // beside it; the hot results on the third stream once the hot runs are done (beside the cold stage,
+        // which decide_hot queues on the batch stream after the partition)
+        side_stream_init(sc);
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_fork0, s));
+        SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork0, 0));
+        if (sc.part_lb) {
+            const uint32_t pg = (nseg + kPartGroup - 1) / kPartGroup;
+            hipLaunchKernelGGL(k_part_colscan, dim3(kPartBins / 256, pg), dim3(256), 0, sc.side, sc, nseg);
+            hipLaunchKernelGGL(k_part_binscan, dim3(kPartBins / 256), dim3(256), 0, sc.side, sc, pg);
+            hipLaunchKernelGGL(k_part_scatter, dim3(8 * ((nseg + 7) / 8)), dim3(kKeyThreads), 0, sc.side, sc, nseg,
+                               sc.part_lb, sc.el[0], fz_debug());
+            sc.el_sorted = sc.el[0];
+        } else {
+            const int np = radix_sort_u64_tiled(sc.el_tile, sc.tile_nc, sc.counters + CTL_NSORT, sc.el[0], sc.el[1], n,
+                                                kSlotShift, bits, sc.radix, sc.side, d0 > 0);
+            sc.el_sorted = (np & 1) ? sc.el[0] : sc.el[1];
+        }
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_fork, sc.side));  // the cold elements ready (decide_hot waits)
+        const int npp = radix_sort_u64_tiled(sc.pel_tile, sc.ptile_np, sc.counters + CTL_NPRIO, sc.pel[0], sc.pel[1],
+                                             n, kSlotShift, 12, sc.radix_p, s, false);
+        sc.pel_sorted = (npp & 1) ? sc.pel[0] : sc.pel[1];
+        hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
+        hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, s, sc, ngroups);
+        hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
+        hipLaunchKernelGGL(k_hot_pre, dim3(kHotBuckets), dim3(kThreads), 0, s, sc);
+        const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
+        hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, s, st, sc, sc.pel_sorted);
+        hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, s, st, sc, ts_base);
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_mid, s));
+        SGA_HIP_CHECK(hipStreamWaitEvent(sc.side2, sc.ev_mid, 0));
+        launch_hot_final(st, sc, n, sc.pel_sorted, out, sc.side2);
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_join, sc.side2));
+        sc.hot_early = true;
+        return;
+    }
+    // the hot side's count scans and prioritized sort on the side stream, beside the cold sort
     hipStream_t hs = s;
     if (ovl) {
         side_stream_init(sc);
@@ -4094,6 +4320,7 @@ static void decide_hot(const ClusterState &st, BatchScratch &sc, const ReqIn &in
     const uint32_t invalid_key = st.nslots;
     const uint64_t *el = sc.el_sorted, *pel = sc.pel_sorted;
     const bool ovl = hot_overlap() && !(fz_debug() & 16);
+    if (sc.sched2) SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_fork, 0));  // the cold partition (side stream)
     if (!sc.hot_early) {  // the hot side beside the cold stage
         hipStream_t hs = s;
         if (ovl) {
@@ -4127,11 +4354,25 @@ static void decide_hot(const ClusterState &st, BatchScratch &sc, const ReqIn &in
         SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_mid, 0));
     }
     const uint32_t sb = 64;  // few workgroups: their bins meet in global atomics
-    hipLaunchKernelGGL(k_hot_hist, dim3(sb), dim3(kThreads), 0, s, st, sc, std::max<uint32_t>(sc.hot_min, 1));
-    hipLaunchKernelGGL(k_hot_clear, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc);
-    hipLaunchKernelGGL(k_hot_pick, dim3(sb), dim3(kThreads), 0, s, st, sc, sc.hot_min);
-    if (ovl && tail_early()) SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_join, 0));
-    hipLaunchKernelGGL(k_hot_fin, dim3(1), dim3(kFinThreads), 0, s, st, sc);
+    static const int next = getenv("SGA_HOT_NEXT") ? atoi(getenv("SGA_HOT_NEXT")) : 3;  // A/B knob: 4, 3 or 2 launches
+    if (next == 3) {  // the picks beside the hot results, k_hot_fin after both
+        hipLaunchKernelGGL(k_hot_next_a, dim3(sb), dim3(kThreads), 0, s, st, sc, std::max<uint32_t>(sc.hot_min, 1));
+        hipLaunchKernelGGL(k_hot_pick, dim3(sb), dim3(kThreads), 0, s, st, sc, sc.hot_min);
+        if (ovl && tail_early()) SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_join, 0));
+        hipLaunchKernelGGL(k_hot_fin, dim3(1), dim3(kFinThreads), 0, s, st, sc);
+    } else if (next == 4) {
+        hipLaunchKernelGGL(k_hot_hist, dim3(sb), dim3(kThreads), 0, s, st, sc, std::max<uint32_t>(sc.hot_min, 1));
+        hipLaunchKernelGGL(k_hot_clear, dim3(kHot / kThreads), dim3(kThreads), 0, s, st, sc);
+        hipLaunchKernelGGL(k_hot_pick, dim3(sb), dim3(kThreads), 0, s, st, sc, sc.hot_min);
+        if (ovl && tail_early()) SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_join, 0));
+        hipLaunchKernelGGL(k_hot_fin, dim3(1), dim3(kFinThreads), 0, s, st, sc);
+    } else {
+        // k_hot_fin clears the control words the hot results read: the pick launch (which ends in it) waits
+        // for them
+        hipLaunchKernelGGL(k_hot_next_a, dim3(sb), dim3(kThreads), 0, s, st, sc, std::max<uint32_t>(sc.hot_min, 1));
+        if (ovl && tail_early()) SGA_HIP_CHECK(hipStreamWaitEvent(s, sc.ev_join, 0));
+        hipLaunchKernelGGL(k_hot_next_b, dim3(sb), dim3(kThreads), 0, s, st, sc, sc.hot_min);
+    }
     sc.counters_clean = 1;
 }
 

@@ -56,7 +56,7 @@ struct ClusterState {
     uint32_t nslots;
     double max_occupy_ratio;
     // Uniform geometry (every allocated slot has sampleCount uni_S, windowLength uni_W, interval uni_iv and
-    // its record at slot * (uni_S + 1) 64-byte units, the layout of one load of equal rules): a slot's record
+    // its record at slot * rec_units(uni_S) 64-byte units, the layout of one load of equal rules): a slot's record
     // address needs no parameter load, so the record loads do not wait for one.  uni_S = 0: not uniform.
     int32_t uni_S, uni_W, uni_iv, uni_pad;
 };
@@ -227,6 +227,7 @@ struct BatchScratch {
     uint32_t *hbnd;           // [kHotBuckets] the bucket's first request
     HotRun *hrun;             // [kHotBuckets][kHot]
     uint4 *hfin;              // [kHotBuckets][kHot]: (s0, f, start) of each hot run, what k_hot_final caches
+    uint2 *hfs;               // [kHotBuckets][kHot]: (f, start) of each hot run, what k_hot_final_p stages
     double2 *hthr;            // [kHot] threshold and intervalInSecond of each hot rule (k_hot_flows)
     uint32_t *prank;          // per prioritized hot request (order of pel): its rank among its rule's requests
     uint32_t *plo, *phi;      // per hot id: its range in the prioritized region
@@ -238,6 +239,8 @@ struct BatchScratch {
                                    // pipelined batches; shared by an engine's scratch sets)
     const uint64_t *el_sorted = nullptr, *pel_sorted = nullptr;  // stage 1's sorted cold / prioritized elements
     bool hot_early = false;   // host: the batch's hot runs and results were queued in stage 1 (beside the cold sort)
+    bool sched2 = false;      // host: stream schedule 2 (cluster.hip hot_sched): the cold partition on `side`, the
+                              // hot results on `side2`; the cold stage waits for ev_fork
     uint32_t *hot_cand;       // [kHotCand] (slot, count) of cold rules with >= hot_min requests (hot_ctl[6])
     // cold partition: [segment][bin] counts (then in-group exclusive prefixes), [group][bin] group sums
     // (then prefixes), [bin] bin starts (+ the total); part_lb: slot bits below the bin (host, 0 = LSD sort)

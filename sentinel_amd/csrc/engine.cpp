@@ -106,6 +106,7 @@ struct PSlotHost {
     uint32_t boff = 0;
     uint32_t cap = 4000;     // each bucket map's maxCapacity, fixed at creation
     std::vector<std::pair<int64_t, int32_t>> hot;  // ascending value
+    uint64_t lru_off = 0, lru_words = 0;  // LRU mode: the metric's queue areas in the pool (lru_words = 0: none)
 };
 
 struct NamespaceHost {
@@ -282,6 +283,7 @@ struct Engine {
     DevBuf<uint64_t> d_ppq, d_pqoff;
     DevBuf<PLruRec> d_plpool;
     uint64_t plpool_used = 0;
+    std::unordered_map<uint64_t, std::vector<uint64_t>> plpool_free;  // area size -> offsets of dropped metrics' areas
 
     // ---- cluster concurrency tokens
     DevBuf<ConcParam> d_cparam;   // per slot
@@ -401,10 +403,19 @@ struct Engine {
         uint64_t need = 0;
         uint32_t max_s = 1;
         for (uint32_t w = 0; w < nsw; ++w) {
-            const PSlotHost &h = pslots[lst[w]];
+            PSlotHost &h = pslots[lst[w]];
             max_s = std::max<uint32_t>(max_s, (uint32_t)h.S);
-            qoff[w] = plpool_used + need;
-            need += (uint64_t)h.S * (2ull * h.cap + 3);
+            const uint64_t words = (uint64_t)h.S * (2ull * h.cap + 3);
+            auto fl = plpool_free.find(words);  // the areas of dropped metrics are reused first
+            if (fl != plpool_free.end() && !fl->second.empty()) {
+                qoff[w] = fl->second.back();
+                fl->second.pop_back();
+            } else {
+                qoff[w] = plpool_used + need;
+                need += words;
+            }
+            h.lru_off = qoff[w];
+            h.lru_words = words;
         }
         if (d_plpool.n < plpool_used + need) d_plpool.grow(std::max<uint64_t>(plpool_used + need, 2 * d_plpool.n), s);
         plpool_used += need;
@@ -1689,6 +1700,10 @@ int sga_load_cluster_param_rules(sga_engine *e, const char *ns, const sga_cluste
             h.active = false;
             h.allocated = false;
             g.pslot_of.erase(h.flow_id);
+            if (h.lru_words) {  // the metric's LRU queue areas go back to the pool
+                g.plpool_free[h.lru_words].push_back(h.lru_off);
+                h.lru_words = 0;
+            }
         }
         for (int64_t fid : order) {
             const sga_cluster_param_rule &r = *rule_map[fid];

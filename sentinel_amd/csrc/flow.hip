@@ -5475,13 +5475,25 @@ void FlowEngine::grow_map(DevBuf<PEntry> &tab, DevBuf<uint64_t> &stamp, size_t &
 // distinct indices).  CacheMap capacity bounds the present keys, and a rehash drops the claimed slots of
 // evicted / removed ones.
 int FlowEngine::ensure_maps(size_t m) {
-    uint32_t mpr = 0;
-    for (const ResDev &r : h_res) mpr = std::max<uint32_t>(mpr, r.n_prules);
+    // an event claims at most one (rule, value) entry per parameter rule of its resource, and one thread-count
+    // entry per distinct argument index those rules name (ParameterMetric's threadCountMap per index)
+    uint32_t mpr = 0, midx = 0;
+    for (const ResDev &r : h_res) {
+        mpr = std::max<uint32_t>(mpr, r.n_prules);
+        uint64_t seen = 0;  // argument indices 0..63 (kMaxParamIdx); a negative index (resolved on the device
+        uint32_t other = 0;  // against each call's argument count) or a larger one counts once per rule
+        for (uint32_t k = 0; k < r.n_prules; ++k) {
+            const int32_t ix = h_prules[r.prule_off + k].param_idx;
+            if (ix >= 0 && ix < kMaxParamIdx) seen |= 1ull << ix;
+            else ++other;
+        }
+        midx = std::max<uint32_t>(midx, (uint32_t)__builtin_popcountll(seen) + other);
+    }
     if (!mpr) return 0;
     const size_t limit = (size_t)1 << 31;  // 32-bit map indices
-    if ((pkeys_ub + m * mpr) * 4 > limit || (tkeys_ub + m * mpr) * 4 > limit) return SGA_ENOMEM;
+    if ((pkeys_ub + m * mpr) * 4 > limit || (tkeys_ub + m * midx) * 4 > limit) return SGA_ENOMEM;
     grow_map(d_ptab, d_pstamp, pkeys_ub, m * mpr);
-    grow_map(d_ttab, d_tstamp, tkeys_ub, m * mpr);
+    grow_map(d_ttab, d_tstamp, tkeys_ub, m * midx);
     return 0;
 }
 

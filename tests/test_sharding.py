@@ -165,3 +165,158 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus=2" in r.stderr
+
+
+# ---- the local path (SphU.entry / Entry.exit through the slot chain): resources shard by
+# splitmix64(resource id) mod G (bench_local.py).  Resources are independent without
+# SystemRules and RELATE / CHAIN strategies (FlowRuleChecker.java:96-116 reads another resource's node: such
+# resources must be co-located, which the engine leaves to the caller), so a shard's decisions equal one
+# engine's on the same events.
+L_RES, L_EVENTS = 2_000, 60_000
+
+
+def _local_stream():
+    """A C2-like mixed workload (Default / RateLimiter / WarmUp rules, Zipf resources, acquire 1-5), its entries
+    then the exits of the entries that passed (masked by the deciding replay's own decisions)."""
+    rng = np.random.default_rng(77)
+    flow = []
+    for r in range(L_RES):
+        b = rng.random()
+        c = float(rng.integers(5, 300))
+        if b < 0.4:
+            flow.append(dict(resource=r, count=c))
+        elif b < 0.7:
+            flow.append(dict(resource=r, count=c, control_behavior=2, max_queueing_time_ms=500))
+        else:
+            flow.append(dict(resource=r, count=c, control_behavior=1, warm_up_period_sec=10))
+    p = 1.0 / np.arange(1, L_RES + 1) ** 1.1
+    res = rng.choice(L_RES, size=L_EVENTS, p=p / p.sum())
+    ts = 1_700_000_000_000 + np.arange(L_EVENTS) // 20
+    acq = np.where(rng.random(L_EVENTS) < 0.05, rng.integers(2, 6, size=L_EVENTS), 1)
+    rt = rng.geometric(0.2, size=L_EVENTS)
+    return flow, res.astype(np.uint32), ts.astype(np.int64), acq.astype(np.int32), rt.astype(np.int64)
+
+
+def _local_events(res, ts, acq, sel):
+    n = len(sel)
+    return {"kind": np.zeros(n, np.uint8), "resource": res[sel], "ts": ts[sel], "acquire": acq[sel],
+            "flags": np.zeros(n, np.uint8), "rt": np.zeros(n, np.int64), "param": np.zeros(n, np.uint64)}
+
+
+def _local_exits(res, ts, acq, rt, sel, dec):
+    ok = sel[(dec == 0) | (dec == 4)]
+    order = ok[np.argsort(ts[ok] + rt[ok], kind="stable")]
+    n = len(order)
+    return {"kind": np.ones(n, np.uint8), "resource": res[order], "ts": ts[order] + rt[order], "acquire": acq[order],
+            "flags": np.zeros(n, np.uint8), "rt": rt[order], "param": np.zeros(n, np.uint64)}
+
+
+def _local_replay(flow, res, ts, acq, rt, sel):
+    from tests import local_trace as lt
+    orc = lt.Oracle(L_RES, flow)
+    dec, wait = orc.replay(_local_events(res, ts, acq, sel))
+    ex = _local_exits(res, ts, acq, rt, sel, dec)
+    orc.replay(ex)
+    now = int(ts.max()) + 10_000
+    nodes = {int(r): orc.node(int(r), now) for r in np.unique(res[sel])[:200]}
+    orc.close()
+    return dec, wait, nodes
+
+
+def _local_rank_main(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    flow, res, ts, acq, rt = _local_stream()
+    mine = shard_of(res.astype(np.int64), world) == rank
+    sel = np.nonzero(mine)[0]
+    own_rules = [r for r in flow if shard_of(np.array([r["resource"]]), world)[0] == rank]
+    dec, wait, nodes = _local_replay(own_rules, res, ts, acq, rt, sel)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (sel, dec, wait, nodes))
+    if rank == 0:
+        q.put(gathered)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_local_shards_equal_single_replay():
+    """world 2 (gloo, the bench's launch shape): each rank replays the local oracle over its resource shard
+    (its rules only, its events in arrival order, the exits of its passes); merged, every decision, wait and
+    node view equals one oracle holding every rule."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_local_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    gathered = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    flow, res, ts, acq, rt = _local_stream()
+    dec, wait, nodes = _local_replay(flow, res, ts, acq, rt, np.arange(L_EVENTS))
+    md, mw = np.full(L_EVENTS, 99, np.int8), np.zeros(L_EVENTS, np.int32)
+    for sel, d, w, nd in gathered:
+        md[sel] = d
+        mw[sel] = w
+        for r, v in nd.items():
+            if r in nodes:
+                assert v == nodes[r], r
+    assert np.array_equal(md, dec) and np.array_equal(mw, wait)
+    assert (dec == 0).any() and (dec == 1).any()
+
+
+def test_local_bench_gpus2_launches_and_routes():
+    """`bench.py --config c5b --gpus 2` run bare starts two ranks (torch.distributed.run, before any GPU call);
+    each builds its shard (SGA_BENCH_DRY stops it before the GPU): disjoint resource sets covering all 10k, every
+    event on an own resource, both ranks' full per-GPU batches."""
+    import json
+    import subprocess
+    import sys
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tempfile.mkdtemp()
+    env = dict(os.environ, SGA_BENCH_DRY="1", SGA_BENCH_DRY_OUT=out)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--config", "c5b", "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.load(open(os.path.join(out, f))) for f in sorted(os.listdir(out))]
+    assert sorted(d["rank"] for d in lines) == [0, 1]
+    assert all(d["events_on_own"] and d["world"] == 2 for d in lines)
+    assert sum(d["own_resources"] for d in lines) == 10_000
+    assert all(d["events_all_ranks"] == 2 * (1 << 22) for d in lines)
+
+
+@pytest.mark.gpu
+def test_local_engines_per_shard_equal_single_engine():
+    """The local path through the engine: G = 2 engines on one device, each holding one resource shard's rules
+    and deciding that shard's entries and exits, equal one engine holding every rule (decisions, waits)."""
+    from sentinel_amd.cluster import Engine
+    from sentinel_amd.local import FlowRuleManager, LocalSentinel
+    from sentinel_amd.rules import FlowRule
+    flow, res, ts, acq, rt = _local_stream()
+
+    def run(rules, sel):
+        eng = Engine(max_batch=1 << 17)
+        s = LocalSentinel(eng, [f"r{i}" for i in range(L_RES)])
+        FlowRuleManager(s).load_rules([FlowRule(resource=f"r{r['resource']}", **{k: v for k, v in r.items()
+                                                                                 if k != "resource"}) for r in rules])
+        e = _local_events(res, ts, acq, sel)
+        d, w = s.submit(e["kind"], e["resource"], e["ts"], e["acquire"], e["flags"], e["rt"], e["param"])
+        x = _local_exits(res, ts, acq, rt, sel, d)
+        s.submit(x["kind"], x["resource"], x["ts"], x["acquire"], x["flags"], x["rt"], x["param"])
+        now = int(ts.max()) + 10_000
+        views = {int(r): s.node(int(r), now) for r in np.unique(res[sel])[:100]}
+        eng.close()
+        return d, w, views
+
+    d1, w1, v1 = run(flow, np.arange(L_EVENTS))
+    for rank in range(2):
+        sel = np.nonzero(shard_of(res.astype(np.int64), 2) == rank)[0]
+        own = [r for r in flow if shard_of(np.array([r["resource"]]), 2)[0] == rank]
+        d, w, v = run(own, sel)
+        assert np.array_equal(d, d1[sel]) and np.array_equal(w, w1[sel]), rank
+        for r, view in v.items():
+            assert view == v1[r], (rank, r)

@@ -125,6 +125,29 @@ __global__ void k_coop(int4 *rec, const uint32_t *__restrict__ sl, uint32_t n) {
     }
 }
 
+// 4 lanes per rule: lane q of the quad loads pieces q, q + 4, q + 8, q + 12 (each instruction: 64 contiguous bytes
+// per quad, 16 rules per wave); the pass sum is a quad reduction, each lane stores a piece of the group
+__global__ void k_quad(int4 *rec, const uint32_t *__restrict__ sl, uint32_t n) {
+    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x);
+    const uint32_t i = g >> 2;
+    const int q = threadIdx.x & 3;
+    if (i >= n) return;
+    int4 *r = rec + (size_t)sl[i] * kRecI4;
+    int4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = r[4 * k + q];
+    long long s = hi64(v[0]) + hi64(v[1]) + (q < 2 ? hi64(v[2]) : 0);  // pairs q, q + 4, q + 8 (< 10)
+    for (int o = 1; o < 4; o <<= 1) {
+        const int lo = __shfl_xor((int)(unsigned)s, o, 4);
+        const int hi = __shfl_xor((int)(unsigned)((unsigned long long)s >> 32), o, 4);
+        s += (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+    }
+    const int cj = __shfl(v[2].x, (threadIdx.x & ~3) + 2, 64) & 7;  // piece 10 (lane 2, register 2)
+    if (q == (cj & 3)) r[cj] = make_int4((int)s, 0, v[cj >> 2].z + 1, v[cj >> 2].w);
+    int4 *gp = r + kHdrI4 + 3 * cj;
+    if (q < 3) gp[q] = v[3];
+}
+
 template <class F> float timeit(F f, int reps = 20) {
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     f(); CK(hipDeviceSynchronize());
@@ -161,6 +184,8 @@ int main(int argc, char **argv) {
         printf("{\"mode\":\"lane2\",\"order\":\"%s\",\"touched\":%u,\"wg\":%d,\"us\":%.2f,\"GBs\":%.1f}\n", on, touched, wg, t * 1e3, mb / t);
         t = timeit([&] { hipLaunchKernelGGL(k_trans, dim3(nb), dim3(wg), lds, 0, rec, s, touched); });
         printf("{\"mode\":\"trans\",\"order\":\"%s\",\"touched\":%u,\"wg\":%d,\"us\":%.2f,\"GBs\":%.1f}\n", on, touched, wg, t * 1e3, mb / t);
+        t = timeit([&] { hipLaunchKernelGGL(k_quad, dim3((4 * touched + wg - 1) / wg), dim3(wg), 0, 0, rec, s, touched); });
+        printf("{\"mode\":\"quad\",\"order\":\"%s\",\"touched\":%u,\"wg\":%d,\"us\":%.2f,\"GBs\":%.1f}\n", on, touched, wg, t * 1e3, mb / t);
         t = timeit([&] { hipLaunchKernelGGL(k_coop, dim3(nb), dim3(wg), 0, 0, rec, s, touched); });
         printf("{\"mode\":\"coop\",\"order\":\"%s\",\"touched\":%u,\"wg\":%d,\"us\":%.2f,\"GBs\":%.1f}\n", on, touched, wg, t * 1e3, mb / t);
     }
