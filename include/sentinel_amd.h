@@ -401,6 +401,12 @@ int sga_rls_should_rate_limit_device(sga_engine *e, const uint32_t *d_desc_offse
 #define SGA_KIND_ENTRY 0
 #define SGA_KIND_EXIT 1
 #define SGA_KIND_BLOCKED 2
+/* kind 3: an entry the engine passed (decision SGA_PASS) that a slot after the engine's checks then blocked
+ * (a custom slot sorted after DegradeSlot).  In the reference StatisticSlot fires those slots before its pass
+ * accounting (StatisticSlot.java:71-84), so such an entry only counts a block: the revoke undoes the entry's
+ * pass, thread count and parameter thread counts and counts the block (node and, inbound, ENTRY_NODE), at the
+ * entry's time, with the entry's flags and arguments.  Decided in arrival order by one lane; reports SGA_PASS. */
+#define SGA_KIND_REVOKE 3
 
 /* event flags */
 #define SGA_EV_PRIORITIZED 1u

@@ -188,6 +188,20 @@ JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_exitArgs(JNIE
     return rc;
 }
 
+/* GpuStatisticSlot: a slot sorted after DegradeSlot blocked an entry the engine passed (SGA_KIND_REVOKE) */
+JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_revokedArgs(JNIEnv *env, jclass cls, jlong h,
+                                                                              jint resource, jlong now_ms,
+                                                                              jint count, jint flags,
+                                                                              jlongArray words, jint nargs) {
+    (void)cls;
+    const jsize nw = (*env)->GetArrayLength(env, words);
+    jlong *w = GET_L(words);
+    const int rc = sgaj_revoke_args(ENGINE(h), (uint32_t)resource, now_ms, count, (uint32_t)flags,
+                                    (const uint64_t *)w, (uint32_t)nargs, (uint32_t)nw);
+    REL_L(words, w);
+    return rc;
+}
+
 /* a BlockException thrown by a slot the engine does not run (AuthoritySlot): counted as a block */
 JNIEXPORT jint JNICALL Java_com_alibaba_csp_sentinel_gpu_GpuEngine_blocked(JNIEnv *env, jclass cls, jlong h,
                                                                           jint resource, jlong now_ms, jint count,

@@ -131,6 +131,17 @@ int sgaj_exit_args(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t cou
                                 &wait);
 }
 
+int sgaj_revoke_args(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, uint32_t flags,
+                     const uint64_t *words, uint32_t nargs, uint32_t nwords) {
+    const uint8_t kind = SGA_KIND_REVOKE, fl = (uint8_t)(flags | SGA_EV_ARGS);
+    const int64_t rt = 0;
+    const uint64_t param = (uint64_t)nargs;
+    int8_t dec = 0;
+    int32_t wait = 0;
+    return sga_submit_events_ex(e, &kind, &resource, &now_ms, &count, &fl, &rt, &param, 1, words, nwords, &dec,
+                                &wait);
+}
+
 int sgaj_blocked(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, uint32_t flags) {
     const uint8_t kind = SGA_KIND_BLOCKED, fl = (uint8_t)flags;
     const int64_t rt = 0;

@@ -59,6 +59,9 @@ int sgaj_exit_args(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t cou
 /* StatisticSlot's BlockException branch for a block thrown by a slot outside the engine (AuthoritySlot):
  * event kind SGA_KIND_BLOCKED. */
 int sgaj_blocked(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, uint32_t flags);
+/* a passed entry that a slot after the engine's checks blocked (SGA_KIND_REVOKE): the entry's time, flags, args */
+int sgaj_revoke_args(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, uint32_t flags,
+                     const uint64_t *words, uint32_t nargs, uint32_t nwords);
 
 /* ParamFlowRuleManager.loadRules (ParamFlowRuleManager.java:52): parallel arrays; rule i's hot items are
  * hot_values / hot_counts [hot_off[i], hot_off[i + 1]); cluster_* may be NULL (local rules). */

@@ -104,6 +104,11 @@ public final class GpuEngine {
     /** StatisticSlot's BlockException branch for a block thrown outside the engine (AuthoritySlot). */
     static native int blocked(long engine, int resource, long nowMs, int count, int flags);
 
+    /** A passed entry blocked by a slot after the engine's checks (SGA_KIND_REVOKE, the entry's time,
+     * flags and arguments). */
+    static native int revokedArgs(long engine, int resource, long nowMs, int count, int flags, long[] words,
+                                  int nargs);
+
     /** Round-2 single-parameter forms (flags EV_HAS_PARAM = 4: args = [param]). */
     static native int entry(long engine, int resource, long nowMs, int count, int flags, long param, int[] out);
 

@@ -31,8 +31,8 @@ import com.alibaba.csp.sentinel.util.TimeUtil;
  * the engine's local path (sga_submit_events) runs SystemSlot, ParamFlowSlot, FlowSlot and DegradeSlot and the
  * StatisticSlot accounting on the GPU in one event; the "post" chain (slots sorted after DegradeSlot) runs only
  * for an entry the engine passed, as in the reference.  A BlockException from the pre chain is counted as a block
- * (event kind 2) and rethrown; one from the post chain too, but the engine has then already counted the pass
- * (its event is one step); an engine block becomes the reference's
+ * (event kind 2) and rethrown; one from the post chain revokes the engine's pass (event kind 3: pass, thread and
+ * parameter thread counts undone, the block counted) and is rethrown; an engine block becomes the reference's
  * exception with the blocking rule ({@link GpuRuleSync} keeps the per-resource lists in engine order), and its
  * block error is set on the entry so that exit records nothing.  Passes sleep the engine's wait (RateLimiter
  * pacing, cluster SHOULD_WAIT, parameter throttle) as the reference controllers do before returning.
@@ -102,26 +102,34 @@ public class GpuStatisticSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
         }
         long[] words = GpuArgs.encode(args);
         int[] o = new int[2];
-        int rc = GpuEngine.entryArgs(engine, rid, TimeUtil.currentTimeMillis(), count, fl, words,
-                                     args == null ? 0 : args.length, o);
+        final long now = TimeUtil.currentTimeMillis();
+        int rc = GpuEngine.entryArgs(engine, rid, now, count, fl, words, args == null ? 0 : args.length, o);
         if (rc != GpuEngine.OK) {
             throw new IllegalStateException("sga_submit_events: " + rc + " " + GpuEngine.lastError(engine));
         }
         BlockException block;
         switch (o[0]) {
             case 0:  // passed; RateLimiter / SHOULD_WAIT / throttle waits sleep like the controllers
-            case 4:  // PriorityWaitException: DefaultController slept; counted as a thread, not a pass
                 if (o[1] > 0) {
                     TimeUnit.MILLISECONDS.sleep(o[1]);
                 }
                 try {  // the slots sorted after DegradeSlot, which the reference reaches only on a pass
                     post.entry(context, resourceWrapper, node, count, prioritized, args);
                 } catch (BlockException e) {
+                    // the reference counts no pass and no thread for it (StatisticSlot.java:71-84 run after
+                    // fireEntry) but a block (:121-135): the revoke event undoes the engine's pass accounting
+                    // (node, ENTRY_NODE, parameter thread counts) and counts the block, at the entry's time
                     context.getCurEntry().setBlockError(e);
-                    GpuEngine.blocked(engine, rid, TimeUtil.currentTimeMillis(), count, fl);
+                    GpuEngine.revokedArgs(engine, rid, now, count, fl, words, args == null ? 0 : args.length);
                     throw e;
                 }
                 fireEntry(context, resourceWrapper, node, count, prioritized, args);
+                return;
+            case 4:  // PriorityWaitException (FlowSlot): DefaultController slept; StatisticSlot counted a thread
+                     // and returned -- no slot after FlowSlot sees the entry (StatisticSlot.java:86-100)
+                if (o[1] > 0) {
+                    TimeUnit.MILLISECONDS.sleep(o[1]);
+                }
                 return;
             case 1: {
                 FlowRule r = GpuRuleSync.flowRule(name, o[1]);

@@ -1029,6 +1029,24 @@ void orc_flow_replay_p(orc_flow *f, size_t n, const uint8_t *kind, const uint32_
             if (wait_ms) wait_ms[i] = 0;
             continue;
         }
+        if (kind && kind[i] == 3) { /* SGA_KIND_REVOKE: a later slot blocked a passed entry (StatisticSlot.java:71-84,
+                                     * 121-135: the pass accounting never ran, the block is counted) */
+            if (resource[i] < f->n) {
+                flow_res *fr = &f->res[resource[i]];
+                orc_node_decrease_thread_num(fr->node);
+                orc_node_add_pass_request(fr->node, ts[i], -acquire[i]);
+                orc_node_increase_block_qps(fr->node, ts[i], acquire[i]);
+                param_thread_dec(f, fr, hp, pv);
+                if (in) {
+                    orc_node_decrease_thread_num(f->entry);
+                    orc_node_add_pass_request(f->entry, ts[i], -acquire[i]);
+                    orc_node_increase_block_qps(f->entry, ts[i], acquire[i]);
+                }
+            }
+            if (decision) decision[i] = ORC_PASS;
+            if (wait_ms) wait_ms[i] = 0;
+            continue;
+        }
         if (kind && kind[i] == 1) {
             orc_flow_exit_x(f, resource[i], ts[i], rt ? rt[i] : 0, acquire[i], (fl & 2) != 0, hp, pv, in);
             if (decision) decision[i] = ORC_PASS;

@@ -2094,9 +2094,11 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
         }
         __syncthreads();
         if (active) {
-            // codes: in-wave ranks -> in-segment ranks; prioritized hot requests go to the sub's
-            // prioritized buffer (their own sort by hot id, beside the cold sort)
+            // codes: in-wave ranks -> in-segment ranks; prioritized hot requests go to the segment's
+            // prioritized buffer, compacted over the segment in arrival order (the waves' counts s_np give each
+            // wave its offset; k_psort_* sort them by hot id)
             uint32_t npc = 0;
+            for (int w = 0; w < wave; ++w) npc += s_np[w];
 #pragma unroll
             for (int r = 0; r < kSubRounds; ++r) {
                 const uint32_t i = ubase + (uint32_t)r * 64 + lane;
@@ -2107,15 +2109,10 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                 const bool pr = hot && (cd >> 31);
                 if (i < send) sc.hcode[i] = hot ? ((cd & ~(0x1FFFu << 12)) | (r_seg << 12)) : kNoCode;
                 const uint64_t em = __ballot(pr);
-                if (pr) sc.pel_tile[(size_t)ubase + npc + (uint32_t)__popcll(em & lt)] = el_pack(hid, r_seg >> 7, 1u, r_seg & 127u, i);
+                if (pr) sc.pel_tile[(size_t)seg * kHotSeg + npc + (uint32_t)__popcll(em & lt)] = el_pack(hid, r_seg >> 7, 1u, r_seg & 127u, i);
                 npc += (uint32_t)__popcll(em);
             }
-            if (lane == 0) sc.ptile_np[sub] = npc;
-        } else if (lane == 0) {
-            sc.ptile_np[sub] = 0u;
         }
-    } else if (lane == 0) {
-        sc.ptile_np[sub] = 0u;  // no hot set (or the re-classifying pass): nothing prioritized to sort
     }
     {  // the segment's latest request time (offset from ts_base): k_hot_mode keeps the maximum over batches
 #pragma unroll
@@ -2413,6 +2410,136 @@ __global__ __launch_bounds__(kThreads) void k_hot_pre(BatchScratch sc) {
     __syncthreads();
     const uint32_t nhot = hot_count(sc);
     for (uint32_t h = threadIdx.x; h < nhot; h += kThreads) sc.hpre[(size_t)b * kHot + h] = (uint16_t)cnt[h];
+}
+
+// ---- the prioritized hot requests sorted by hot id, arrival order kept (a counting sort over kHot keys in three
+// small launches: the elements are about 1 % of the hot requests).  Input: each rank segment's elements compacted
+// at pel_tile[seg * kHotSeg ..], seg_stat[kSegStat * seg] of them.  kPsWgs workgroups own consecutive segment ranges;
+// in each, a wave owns kPsSegs consecutive segments.
+constexpr int kPsWgs = 16, kPsThreads = 512, kPsWaves = kPsThreads / 64;
+// the wave's elements in arrival order, 64 per step: f(e, element index in the wave's stream) for each
+template <class F>
+__device__ __forceinline__ void ps_walk(const BatchScratch &sc, uint32_t sg0, uint32_t sg1, F f) {
+    const int lane = threadIdx.x & 63;
+    for (uint32_t k0 = sg0; k0 < sg1; k0 += 64) {
+        const uint32_t kn = min(64u, sg1 - k0);
+        const uint32_t c = (uint32_t)lane < kn ? sc.seg_stat[kSegStat * (k0 + lane)] : 0u;
+        uint32_t inc = c;  // inclusive prefix over the lanes (segment order)
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        const uint32_t tot = __builtin_amdgcn_readlane((int)inc, 63);
+        for (uint32_t j0 = 0; j0 < tot; j0 += 64) {
+            const uint32_t j = j0 + (uint32_t)lane;
+            // the element's segment: the lanes whose inclusive prefix is <= j are before it
+            uint32_t kk = 0, before = 0;
+            for (uint32_t t = 0; t < kn; ++t) {
+                const uint32_t it = (uint32_t)__builtin_amdgcn_readlane((int)inc, (int)t);
+                if (it <= j) {
+                    kk = t + 1;
+                    before = it;
+                }
+            }
+            const bool valid = j < tot;
+            const uint32_t sg = k0 + min(kk, kn - 1);
+            const uint64_t e = sc.pel_tile[(size_t)sg * kHotSeg + (valid ? j - before : 0u)];
+            f(e, valid);
+        }
+    }
+}
+
+__device__ __forceinline__ void ps_range(uint32_t nseg, uint32_t g, uint32_t w, uint32_t &s0, uint32_t &s1) {
+    const uint32_t per_wg = (nseg + kPsWgs - 1) / kPsWgs;
+    const uint32_t a = min(nseg, g * per_wg), b = min(nseg, a + per_wg);
+    const uint32_t per_w = (b - a + kPsWaves - 1) / kPsWaves;
+    s0 = min(b, a + w * per_w);
+    s1 = min(b, s0 + per_w);
+}
+
+// 1: per workgroup, its elements per hot id (row g of prow)
+__global__ __launch_bounds__(kPsThreads) void k_psort_count(BatchScratch sc, uint32_t nseg) {
+    __shared__ uint32_t cnt[kHot];
+    if (!sc.counters[CTL_MODE]) return;
+    for (uint32_t h = threadIdx.x; h < (uint32_t)kHot; h += kPsThreads) cnt[h] = 0;
+    __syncthreads();
+    uint32_t s0, s1;
+    ps_range(nseg, blockIdx.x, threadIdx.x >> 6, s0, s1);
+    ps_walk(sc, s0, s1, [&](uint64_t e, bool valid) {
+        if (valid) atomicAdd(&cnt[el_slot(e)], 1u);
+    });
+    __syncthreads();
+    for (uint32_t h = threadIdx.x; h < (uint32_t)kHot; h += kPsThreads) sc.prow[blockIdx.x * kHot + h] = cnt[h];
+}
+
+// 2: per hot id, the workgroups' rows -> absolute starts (column prefix + the id's start), and plo / phi
+__global__ __launch_bounds__(1024) void k_psort_scan(BatchScratch sc) {
+    __shared__ uint32_t ws[16];
+    if (!sc.counters[CTL_MODE]) return;
+    constexpr int kPer = kHot / 1024;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t tot[kPer], tsum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t h = threadIdx.x * kPer + k;
+        uint32_t acc = 0;
+        for (int g = 0; g < kPsWgs; ++g) {
+            const uint32_t v = sc.prow[g * kHot + h];
+            sc.prow[g * kHot + h] = acc;
+            acc += v;
+        }
+        tot[k] = acc;
+        tsum += acc;
+    }
+    uint32_t x = tsum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) ws[wave] = x;
+    __syncthreads();
+    uint32_t pre = x - tsum;
+    for (int w = 0; w < wave; ++w) pre += ws[w];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t h = threadIdx.x * kPer + k;
+        sc.plo[h] = pre;
+        sc.phi[h] = pre + tot[k];
+        for (int g = 0; g < kPsWgs; ++g) sc.prow[g * kHot + h] += pre;
+        pre += tot[k];
+    }
+}
+
+// 3: per workgroup, the waves' counts -> prefixes over the waves, then every element to its place: the id's start
+// for the workgroup + the earlier waves' + its rank among the wave's elements of the id so far (same-word LDS
+// atomics of one wave instruction return in lane order, lds_lane_order_ok)
+__global__ __launch_bounds__(kPsThreads) void k_psort_scatter(BatchScratch sc, uint32_t nseg, uint64_t *__restrict__ out) {
+    __shared__ uint32_t cnt[kPsWaves][kHot];
+    if (!sc.counters[CTL_MODE]) return;
+    const int wave = threadIdx.x >> 6;
+    for (uint32_t k = threadIdx.x; k < (uint32_t)(kPsWaves * kHot); k += kPsThreads) (&cnt[0][0])[k] = 0;
+    __syncthreads();
+    uint32_t s0, s1;
+    ps_range(nseg, blockIdx.x, wave, s0, s1);
+    ps_walk(sc, s0, s1, [&](uint64_t e, bool valid) {
+        if (valid) atomicAdd(&cnt[wave][el_slot(e)], 1u);
+    });
+    __syncthreads();
+    for (uint32_t h = threadIdx.x; h < (uint32_t)kHot; h += kPsThreads) {
+        uint32_t run = sc.prow[blockIdx.x * kHot + h];
+#pragma unroll
+        for (int w = 0; w < kPsWaves; ++w) {
+            const uint32_t c = cnt[w][h];
+            cnt[w][h] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    ps_walk(sc, s0, s1, [&](uint64_t e, bool valid) {
+        if (valid) out[atomicAdd(&cnt[wave][el_slot(e)], 1u)] = e;
+    });
 }
 
 // Rank of each prioritized hot request (sorted region: hot id major, arrival order within) and each
@@ -3970,7 +4097,7 @@ size_t batch_scratch_bytes(size_t cap, uint32_t nslots_cap) {
     b += align_up((size_t)nslots_cap * 2) + 2 * align_up(kHot * 4) + align_up(kHotCtlWords * 4);  // hot_of/slot/next/ctl
     b += align_up(segs_alloc * kHotSeg * 8);                                       // el_tile
     b += align_up(segs_alloc * kSubPerSeg * 4);                                    // tile_nc
-    b += align_up(segs_alloc * kHotSeg * 8) + align_up(segs_alloc * kSubPerSeg * 4);  // pel_tile, ptile_np
+    b += align_up(segs_alloc * kHotSeg * 8) + align_up((size_t)kPsWgs * kHot * 4);     // pel_tile, prow
     b += 2 * align_up(cap * 8);                                                    // pel (double buffer)
     b += 2 * align_up(hist * 4) + align_up(scan_partials_needed(hist) * 4 + 64);   // radix_p
     b += align_up(kRadixGhistWords * 4) + align_up(64);                            // radix_p row totals, flag
@@ -4038,7 +4165,7 @@ void batch_scratch_carve(BatchScratch &sc, void *base, size_t cap, uint32_t nslo
     sc.el_tile = (uint64_t *)take(segs_alloc * kHotSeg * 8);
     sc.tile_nc = (uint32_t *)take(segs_alloc * kSubPerSeg * 4);
     sc.pel_tile = (uint64_t *)take(segs_alloc * kHotSeg * 8);
-    sc.ptile_np = (uint32_t *)take(segs_alloc * kSubPerSeg * 4);
+    sc.prow = (uint32_t *)take((size_t)kPsWgs * kHot * 4);
     sc.pel[0] = (uint64_t *)take(cap * 8);
     sc.pel[1] = (uint64_t *)take(cap * 8);
     sc.radix_p.hist = (uint32_t *)take(hist * 4);
@@ -4188,6 +4315,14 @@ static void hot_side(const ClusterState &st, BatchScratch &sc, int64_t ts_base, 
     }
 }
 
+// the prioritized hot requests sorted by hot id into pel[0] (k_psort_*; plo / phi per hot id)
+static void prio_sort(BatchScratch &sc, uint32_t nseg, hipStream_t s) {
+    hipLaunchKernelGGL(k_psort_count, dim3(kPsWgs), dim3(kPsThreads), 0, s, sc, nseg);
+    hipLaunchKernelGGL(k_psort_scan, dim3(1), dim3(1024), 0, s, sc);
+    hipLaunchKernelGGL(k_psort_scatter, dim3(kPsWgs), dim3(kPsThreads), 0, s, sc, nseg, sc.pel[0]);
+    sc.pel_sorted = sc.pel[0];
+}
+
 static void classify_hot(const ClusterState &st, BatchScratch &sc, const ReqIn &in, int64_t ts_base, uint32_t n,
                          uint64_t *out, hipStream_t s, bool clean, bool pipelined) {
     const int bits = hot_key_bits(st);
@@ -4240,9 +4375,7 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const ReqIn &
             sc.el_sorted = (np & 1) ? sc.el[0] : sc.el[1];
         }
         SGA_HIP_CHECK(hipEventRecord(sc.ev_fork, sc.side));  // the cold elements ready (decide_hot waits)
-        const int npp = radix_sort_u64_tiled(sc.pel_tile, sc.ptile_np, sc.counters + CTL_NPRIO, sc.pel[0], sc.pel[1],
-                                             n, kSlotShift, 12, sc.radix_p, s, false);
-        sc.pel_sorted = (npp & 1) ? sc.pel[0] : sc.pel[1];
+        prio_sort(sc, nseg, s);
         hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
         hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, s, sc, ngroups);
         hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
@@ -4275,11 +4408,7 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const ReqIn &
     // SGA_PRIO_LATE=1 (A/B knob): the count scans are queued before the prioritized sort (the two side
     // streams may share a hardware queue, where submission order is execution order)
     static const bool prio_late = getenv("SGA_PRIO_LATE") && atoi(getenv("SGA_PRIO_LATE")) == 1;
-    auto prio_sort = [&] {
-        const int npp = radix_sort_u64_tiled(sc.pel_tile, sc.ptile_np, sc.counters + CTL_NPRIO, sc.pel[0], sc.pel[1],
-                                             n, kSlotShift, 12, sc.radix_p, ps, false);
-        sc.pel_sorted = (npp & 1) ? sc.pel[0] : sc.pel[1];
-    };
+    auto prio_sort = [&] { sga::prio_sort(sc, nseg, ps); };
     if (!prio_late) prio_sort();
     hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
     hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, hs, sc, ngroups);

@@ -214,8 +214,9 @@ struct BatchScratch {
                               // [8..40) log2 count bins
     uint64_t *el_tile;        // classify output per 1024-request segment: cold elements, arrival order
     uint32_t *tile_nc;        // per 1024-request segment: elements
-    uint64_t *pel_tile;       // per 1024-request segment: the prioritized hot requests (key = hot id), arrival order
-    uint32_t *ptile_np;       // per 1024-request segment: prioritized hot requests
+    uint64_t *pel_tile;       // per rank segment (kHotSeg requests): the prioritized hot requests (key = hot id),
+                              // compacted in arrival order; seg_stat holds their count
+    uint32_t *prow;           // [kPsWgs][kHot]: the prioritized sort's per-workgroup counts, then starts
     uint64_t *pel[2];         // the prioritized hot requests sorted by hot id (double buffer of their own sort)
     RadixScratch radix_p;     // the prioritized sort's scratch (it runs on the side stream beside the cold sort)
     uint32_t *hcode;          // per request: hot id | in-segment rank << 12 | bucket << 25 | prioritized << 31

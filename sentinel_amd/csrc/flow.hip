@@ -1054,8 +1054,8 @@ __global__ __launch_bounds__(kT) void k_lgate(const uint8_t *__restrict__ kind, 
     uint32_t g = 0;
     for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
         const uint8_t fl = flags ? flags[i] : 0;
-        if (acquire[i] < 0 || kind[i] > 2) g |= kGateBad;
-        if (kind[i] == 2) g |= kGateSeq;  // a block counted for a slot outside the engine: arrival order
+        if (acquire[i] < 0 || kind[i] > SGA_KIND_REVOKE) g |= kGateBad;
+        if (kind[i] >= SGA_KIND_BLOCKED) g |= kGateSeq;  // blocks by slots outside the engine: arrival order
         if ((fl & SGA_EV_INBOUND) && resource[i] < nres) g |= sys_check ? (kGateIn | kGateSeq) : kGateIn;
         if (fl & SGA_EV_ARGS) {  // the argument vector's word pairs and every list inside npvals
             const uint64_t pv = param_in ? param_in[i] : 0;
@@ -1126,9 +1126,25 @@ __global__ void k_lseq(FlowState st, int64_t max_rt, SysDev sys, const uint8_t *
             if (in) entry_node_after_exit(c, t, rt_in[i], a, (fl & SGA_EV_ERROR) != 0);
             continue;
         }
-        if (kind[i] == 2) {  // StatisticSlot's BlockException branch for a block thrown outside the engine
+        if (kind[i] == SGA_KIND_BLOCKED) {  // StatisticSlot's BlockException branch for a block thrown outside the engine
             node_add(c, st.node + (size_t)r * kNodeWords, t, MB_BLOCK, a);
             if (in) node_add(c, entry_node(c), t, MB_BLOCK, a);
+            continue;
+        }
+        if (kind[i] == SGA_KIND_REVOKE) {
+            // a slot after the engine's checks blocked an entry the engine passed: StatisticSlot never reached
+            // its pass accounting (StatisticSlot.java:77-84 follow fireEntry), only the block branch (:121-135)
+            int64_t *nd = st.node + (size_t)r * kNodeWords;
+            nd[kNodeThreads] -= 1;
+            node_add(c, nd, t, MB_PASS, -(int64_t)a);
+            node_add(c, nd, t, MB_BLOCK, a);
+            param_threads<true>(c, r, pa, hp, param_in[i], -1, i);
+            if (in) {
+                int64_t *e = entry_node(c);
+                e[kNodeThreads] -= 1;
+                node_add(c, e, t, MB_PASS, -(int64_t)a);
+                node_add(c, e, t, MB_BLOCK, a);
+            }
             continue;
         }
         int8_t d;
@@ -4427,7 +4443,7 @@ __global__ __launch_bounds__(kT) void k_lru_count(FlowState st, const uint8_t *_
     const uint64_t mark = kStampMark | st.seq_base;
     for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
         const uint32_t r = resource[i];
-        if (r >= st.nres || kind[i] > 1) continue;
+        if (r >= st.nres || kind[i] == SGA_KIND_BLOCKED) continue;  // a revoke touches the maps as an exit does
         const ResDev R = st.res[r];
         if (!R.n_prules) continue;
         const uint8_t fl = flags ? flags[i] : 0;
@@ -5767,9 +5783,9 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         bool has_in = false, has_list = false;
         for (size_t i = 0; flags && i < m && !has_in; ++i) has_in = (flags[b + i] & SGA_EV_INBOUND) && resource[b + i] < nres;
         for (size_t i = 0; any_list && i < m && !has_list; ++i) has_list = is_list(b + i);
-        for (size_t i = 0; i < m && !has_list; ++i) {
-            if (kind[b + i] > 2) return SGA_EINVAL;
-            has_list = kind[b + i] == 2;
+        for (size_t i = 0; i < m; ++i) {
+            if (kind[b + i] > SGA_KIND_REVOKE) return SGA_EINVAL;
+            has_list |= kind[b + i] >= SGA_KIND_BLOCKED;  // blocks outside the engine: arrival order
         }
         if ((has_in && sys.check) || has_list) {  // SystemSlot / collection arguments: one lane in arrival order
             hipLaunchKernelGGL(k_lseq, dim3(1), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sys, d_kind.p,

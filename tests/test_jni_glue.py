@@ -32,7 +32,7 @@ def test_jni_symbols_exported(glue):
         assert hasattr(glue, "Java_com_alibaba_csp_sentinel_gpu_GpuEngine_" + name), name
     for name in ("sgaj_create", "sgaj_request_token", "sgaj_submit", "sgaj_poll", "sgaj_entry", "sgaj_exit",
                  "sgaj_request_param_token", "sgaj_concurrent", "sgaj_load_cluster_flow_rules", "sgaj_entry_args",
-                 "sgaj_exit_args", "sgaj_blocked", "sgaj_load_param_rules", "sgaj_load_degrade_rules",
+                 "sgaj_exit_args", "sgaj_blocked", "sgaj_revoke_args", "sgaj_load_param_rules", "sgaj_load_degrade_rules",
                  "sgaj_load_system_rules", "sgaj_set_system_status", "sgaj_load_cluster_param_rules",
                  "sgaj_set_connected_count", "sgaj_set_namespace_limit", "sgaj_set_cluster_server",
                  "sgaj_query_node", "sgaj_metrics_snapshot"):
@@ -42,7 +42,7 @@ def test_jni_symbols_exported(glue):
 # every `static native` of GpuEngine.java (the Java half cannot be compiled here: no JDK)
 JAVA_NATIVES = ("create", "destroy", "lastError", "loadClusterFlowRules", "loadClusterParamRules", "setConnectedCount",
                 "setNamespaceLimit", "requestToken", "submit", "poll", "requestParamToken", "concurrent", "entryArgs",
-                "exitArgs", "blocked", "entry", "exit", "setResources", "loadFlowRules", "loadParamRules",
+                "exitArgs", "blocked", "revokedArgs", "entry", "exit", "setResources", "loadFlowRules", "loadParamRules",
                 "loadDegradeRules", "loadSystemRules", "setSystemStatus", "setClusterServer", "queryNode",
                 "metricsSnapshot")
 
@@ -70,6 +70,7 @@ def test_glue_calls_reach_the_engine_abi(glue):
         "sgaj_entry_args": ([P, U32, I64, I32, U32, P, U32, U32, P], [None, 0, 1, 1, 0, words, 1, 2, out2]),
         "sgaj_exit_args": ([P, U32, I64, I32, U32, I64, P, U32, U32], [None, 0, 1, 1, 0, 0, words, 1, 2]),
         "sgaj_blocked": ([P, U32, I64, I32, U32], [None, 0, 1, 1, 0]),
+        "sgaj_revoke_args": ([P, U32, I64, I32, U32, P, U32, U32], [None, 0, 1, 1, 0, words, 1, 2]),
         "sgaj_load_degrade_rules": ([P, C.c_size_t, P, P, P, P, P, P, P],
                                     [None, 1, one_u32, one_i32, one_d, one_i32, one_i32, one_d, one_i32]),
         "sgaj_load_system_rules": ([P, C.c_size_t, P, P, P, P, P], [None, 1, one_d, one_d, one_d, one_i64, one_i64]),

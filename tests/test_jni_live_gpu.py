@@ -240,3 +240,64 @@ def test_live_engine_through_the_jni_entry_points(jni):
         from tests import oracle_harness as OH
         OH.lib().orc_cluster_free(oh)
         OH.lib().orc_cluster_free(ohg)
+
+
+def test_post_chain_block_revokes_through_the_jni_entry_points(jni):
+    """GpuStatisticSlot's post-chain path (a custom slot sorted after DegradeSlot throws BlockException for an
+    entry the engine passed): entryArgs, then revokedArgs at the entry's time with its flags and argument
+    vector.  The node then holds what the reference's StatisticSlot records (StatisticSlot.java:71-84,121-135):
+    no pass, no thread -- node, ENTRY_NODE and the parameter thread map -- and the block; thread-grade flow and
+    parameter rules of 1 pass the next entry again.  Node views equal the oracle's (kind 3)."""
+    flow = [{"resource": 0, "grade": 0, "count": 1.0}]
+    param = [{"resource": 0, "grade": 0, "count": 1.0, "param_idx": 0}]
+    J = Jvm(jni)
+    h = J.call("create", C.c_int64, 0, 1 << 12, 1 << 10)
+    assert h > 0
+    H = C.c_int64(h)
+    I, D, Q = np.int32, np.float64, np.int64
+    orc = lt.Oracle(2, flow, param)
+    try:
+        assert J.call("setResources", C.c_int32, H, 2) == 0
+        rec = C.create_string_buffer(flow_records(flow))
+        buf = C.c_void_p(jni.fake_buffer(C.addressof(rec)))
+        J.objs.append(buf.value)
+        assert J.call("loadFlowRules", C.c_int32, H, buf, 1) >= 0
+        z = lambda dt: J.arr([0], dt)
+        assert J.call("loadParamRules", C.c_int32, H, J.arr([0], I), J.arr([0], I), J.arr([1.0], D), z(I), z(I), z(I),
+                      z(I), J.arr([1], Q), J.arr([0, 0], I), J.arr([], Q), J.arr([], I), z(I), z(I), z(Q), z(I),
+                      z(I)) >= 0
+        pv = []
+        word = lt.encode_args([7], pv)
+        w = J.arr(np.array(pv, np.uint64).view(np.int64), Q)
+        out2 = np.zeros(2, np.int32)
+        o2 = J.arr(out2, I)
+        fl = 8  # EntryType.IN
+        events = [(0, T0), (0, T0 + 1), (3, T0), (0, T0 + 3)]
+        got = []
+        for kind, t in events:
+            if kind == 0:
+                assert J.call("entryArgs", C.c_int32, H, 0, C.c_int64(t), 1, fl, w, 1, o2) == 0
+                got.append(int(out2[0]))
+            else:
+                assert J.call("revokedArgs", C.c_int32, H, 0, C.c_int64(t), 1, fl, w, 1) == 0
+        st = {"kind": np.array([k for k, _ in events], np.uint8), "resource": np.zeros(4, np.uint32),
+              "ts": np.array([t for _, t in events], np.int64), "acquire": np.ones(4, np.int32),
+              "flags": np.full(4, 8 | 32, np.uint8), "rt": np.zeros(4, np.int64),
+              "param": np.full(4, word, np.uint64), "param_values": np.array(pv, np.uint64)}
+        exp_d, _ = orc.replay(st)
+        assert got == [int(exp_d[i]) for i in (0, 1, 3)] and got[0] == 0 and got[1] != 0 and got[2] == 0
+        now = T0 + 4
+        for rid in (0, 0xFFFFFFFF):  # the resource, ENTRY_NODE
+            d10, l6 = np.zeros(10, D), np.zeros(6, Q)
+            assert J.call("queryNode", C.c_int32, H, C.c_int32(rid - (1 << 32) if rid >> 31 else rid), C.c_int64(now),
+                          J.arr(d10, D), J.arr(l6, Q)) == 0
+            v = dict(zip(["pass_qps", "block_qps", "success_qps", "exception_qps", "occupied_pass_qps", "avg_rt",
+                          "min_rt", "previous_pass_qps", "max_success_qps", "previous_block_qps"], d10.tolist()))
+            v.update(zip(["total_pass", "total_block", "total_success", "total_exception", "cur_thread_num",
+                          "waiting"], l6.tolist()))
+            assert [v[g] for g in lt.NODE_GETTERS] == orc.node(rid, now), rid
+            assert v["total_block"] == 2 and v["total_pass"] == 1 and v["cur_thread_num"] == 1, (rid, v)
+    finally:
+        J.call("destroy", None, H)
+        J.close()
+        orc.close()

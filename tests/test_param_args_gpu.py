@@ -226,3 +226,50 @@ def test_thread_maps_many_indices_distinct_values():
     _assert_nodes(s, orc, n_res, int(ex["ts"].max()))
     orc.close()
     eng.close()
+
+
+def test_revoked_entries_after_a_later_slot_block():
+    """Event kind 3 (SGA_KIND_REVOKE): an entry the engine passed that a slot sorted after DegradeSlot then
+    blocked.  The reference's StatisticSlot fires those slots before its pass accounting (StatisticSlot.java:
+    71-84), so the entry counts only a block (:121-135): the revoke undoes the pass, the thread counts (node,
+    ENTRY_NODE, parameter thread maps) and counts the block.  Rounds of entries, then revokes for some of the
+    passed ones and exits for the rest; thread-grade flow and parameter rules see the released threads.
+    Decisions, waits and node views equal the oracle's replay (oracle_ext.c kind 3)."""
+    rng = np.random.default_rng(17)
+    n_res = 4
+    flow = [{"resource": 0, "grade": 0, "count": 3}, {"resource": 1, "count": 40.0}]
+    param = [{"resource": 2, "grade": 0, "count": 2.0, "param_idx": 0}, {"resource": 3, "count": 5.0}]
+    orc = lt.Oracle(n_res, flow, param)
+    eng, s = _sentinel(n_res, 1 << 12)
+    _load(s, flow, param)
+    n_rev = n_pass = 0
+    for k in range(30):
+        n = 200
+        t0 = T0 + k * 1000
+        st = {"kind": np.zeros(n, np.uint8), "resource": rng.integers(0, n_res, n).astype(np.uint32),
+              "ts": t0 + np.sort(rng.integers(0, 100, n)).astype(np.int64), "acquire": rng.integers(1, 3, n).astype(np.int32),
+              "flags": (4 | np.where(rng.random(n) < 0.5, 8, 0)).astype(np.uint8), "rt": np.zeros(n, np.int64),
+              "param": rng.integers(0, 3, n).astype(np.uint64)}
+        exp = orc.replay(st)
+        got = s.submit(st["kind"], st["resource"], st["ts"], st["acquire"], st["flags"], st["rt"], st["param"])
+        _assert_same(st, got, exp, f"round {k} entries")
+        passed = np.nonzero(exp[0] == 0)[0]
+        rev = passed[rng.random(len(passed)) < 0.4]
+        ext = np.setdiff1d(passed, rev)
+        n_rev += len(rev)
+        n_pass += len(passed)
+        fx = {f: np.concatenate([st[f][rev], st[f][ext]]) for f in st}
+        fx["kind"] = np.concatenate([np.full(len(rev), 3, np.uint8), np.ones(len(ext), np.uint8)])
+        fx["rt"] = np.concatenate([np.zeros(len(rev), np.int64), rng.integers(1, 30, len(ext)).astype(np.int64)])
+        fx["ts"] = np.concatenate([st["ts"][rev], t0 + 200 + fx["rt"][len(rev):]])
+        order = np.argsort(fx["ts"], kind="stable")
+        fx = {f: v[order] for f, v in fx.items()}
+        exp_x = orc.replay(fx)
+        got_x = s.submit(fx["kind"], fx["resource"], fx["ts"], fx["acquire"], fx["flags"], fx["rt"], fx["param"])
+        _assert_same(fx, got_x, exp_x, f"round {k} revokes and exits")
+        _assert_nodes(s, orc, n_res, t0 + 300)
+    assert n_rev > 500 and n_pass > n_rev
+    end = T0 + 30 * 1000
+    assert s.node(0xFFFFFFFF, end).cur_thread_num == 0
+    orc.close()
+    eng.close()

@@ -120,3 +120,30 @@ def test_generated_argument_streams_replay_identically():
     assert (d[st["kind"] == 0] == 2).any() and (d[st["kind"] == 0] == 0).any()
     gen.close()
     orc.close()
+
+
+def test_revoke_undoes_the_pass_and_counts_the_block():
+    """Kind 3 (SGA_KIND_REVOKE) in the oracle: after a passed entry and its revoke, the node holds what the
+    reference's StatisticSlot records when a slot after the checks throws (StatisticSlot.java:71-84,121-135):
+    no pass, no thread (node, ENTRY_NODE for an inbound entry, the parameter thread map), one block of the
+    entry's count.  A thread-grade rule of 1 then passes the next entry again."""
+    T = 1_700_000_000_000
+    flow = [{"resource": 0, "grade": 0, "count": 1}]
+    param = [{"resource": 0, "grade": 0, "count": 1.0, "param_idx": 0}]
+    orc = lt.Oracle(1, flow, param)
+
+    def ev(kind, t, acq=1):
+        return {"kind": np.array([kind], np.uint8), "resource": np.zeros(1, np.uint32), "ts": np.array([t], np.int64),
+                "acquire": np.array([acq], np.int32), "flags": np.array([4 | 8], np.uint8),
+                "rt": np.zeros(1, np.int64), "param": np.array([7], np.uint64)}
+
+    assert orc.replay(ev(0, T))[0][0] == 0
+    assert orc.replay(ev(0, T + 1))[0][0] != 0  # the first entry holds the one thread
+    orc.replay(ev(3, T))
+    v = dict(zip(lt.NODE_GETTERS, orc.node(0, T + 2)))
+    e = dict(zip(lt.NODE_GETTERS, orc.node(0xFFFFFFFF, T + 2)))
+    assert v["cur_thread_num"] == 0 and e["cur_thread_num"] == 0
+    assert v["pass_qps"] == 0 and e["pass_qps"] == 0
+    assert v["block_qps"] == 2 and e["block_qps"] == 2  # the second entry's block + the revoked entry's
+    assert orc.replay(ev(0, T + 3))[0][0] == 0  # thread and parameter thread counts released
+    orc.close()

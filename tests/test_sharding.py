@@ -308,10 +308,12 @@ def test_local_engines_per_shard_equal_single_engine():
         x = _local_exits(res, ts, acq, rt, sel, d)
         s.submit(x["kind"], x["resource"], x["ts"], x["acquire"], x["flags"], x["rt"], x["param"])
         now = int(ts.max()) + 10_000
-        views = {int(r): s.node(int(r), now) for r in np.unique(res[sel])[:100]}
+        mine = set(np.unique(res[sel]).tolist())
+        views = {int(r): s.node(int(r), now) for r in probe if int(r) in mine}
         eng.close()
         return d, w, views
 
+    probe = np.unique(res)[:200]  # the resources whose node views are compared
     d1, w1, v1 = run(flow, np.arange(L_EVENTS))
     for rank in range(2):
         sel = np.nonzero(shard_of(res.astype(np.int64), 2) == rank)[0]
