@@ -50,14 +50,40 @@ def kind_of(k):
     return "stream" if b in STREAMING_BASE else ("random" if b in RANDOM_BASE else "other")
 
 
+E_DEC = 1  # bench_local.py: one decision byte per entry (the wait word is written only for waits)
+
+
+def alg_local(k, bl):
+    """Local-path lines (bench_local.py): SURVEY.md 8(d)'s bytes per step split over the kernels that move
+    them -- the event records in (entries E_in, exits E_exit) to k_lclassify, which reads every event; the
+    decisions out (E_DEC per entry) to k_lresults; the touched keys' state (2 * S_k each: node, rule,
+    breaker and parameter state) to the synthetic row "(state)", since it is read and written across the
+    per-resource kernels.  The three parts sum to the line's roofline.bytes_alg_per_step."""
+    rf = bl.get("roofline", {})
+    total = rf.get("bytes_alg_per_step")
+    io = rf.get("lower_bound_bytes_per_step")
+    if total is None or io is None:
+        return None
+    dec = E_DEC * bl["config"].get("entries_per_step", 0) / max(1, bl.get("n_gpus", 1))
+    if k == "k_lclassify":
+        return io - dec
+    if k == "k_lresults":
+        return dec
+    if k == "(state)":
+        return total - io
+    return 0.0
+
+
 def alg_bytes(k, bl):
     """Per-kernel share of SURVEY.md 8(d)'s algorithmic bytes per step, from the bench line `bl`:
     the key kernel reads every request (E_in = 12 B), the cold stage writes the cold results and reads
     + writes the cold touched rules, the hot runs read + write the hot rules, the hot results kernel
     writes the hot results (E_out = 8 B).  Everything else (the sort, scans, next hot set) is 0:
     traffic there is non-algorithmic.  Hot touched rules ~ the hot-set size of the last batch."""
+    if bl and "entries_per_step" in bl.get("config", {}):
+        return alg_local(k, bl)
     if not bl or "requests_per_step_per_gpu" not in bl.get("config", {}):
-        return None  # local-path lines: the algorithmic bytes are the bench line's own roofline figure
+        return None
     n = bl["config"]["requests_per_step_per_gpu"]
     touched = bl["roofline"]["touched_rules_per_step_per_gpu"]
     lp = bl.get("last_batch_path") or {}
@@ -89,7 +115,12 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--all-random", action="store_true",
                     help="local-path lines: every engine kernel's FETCH_SIZE gets the measured random factor")
+    ap.add_argument("--relabel", default=None, help="update an existing traffic JSON's alg columns from the "
+                    "bench line given by --steps-from (no counters needed)")
     a = ap.parse_args()
+    if a.relabel:
+        relabel(a.relabel, a.steps_from)
+        return
 
     agg = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(os.path.join(a.dir, "counters_*.csv"))):
@@ -146,14 +177,12 @@ def main():
                "fetch_factor": fac, "fetch_mb": fr * fac * per_step / 1e6, "write_mb": wr * per_step / 1e6,
                "us_per_step": us}
         row["traffic_mb"] = row["fetch_mb"] + row["write_mb"]
-        ab = alg_bytes(k, bline)
-        row["alg_mb"] = None if ab is None else ab / 1e6
-        row["traffic_over_alg"] = (row["traffic_mb"] / row["alg_mb"]) if row["alg_mb"] else None
         tot["fetch_raw"] += row["fetch_raw_mb"]
         tot["fetch"] += row["fetch_mb"]
         tot["write"] += row["write_mb"]
         table.append(row)
     table.sort(key=lambda r: -r["traffic_mb"])
+    alg_total = attach_alg(table, bline) if bline else None
     print(f"\nper step ({sets} dispatch sets; engine kernels only; FETCH x2 for streaming kernels, "
           f"x{rand_factor:.2f} for random-gather kernels)")
     print(f"{'kernel':24s} {'kind':7s} {'calls':>5s} {'fetch_raw':>10s} {'fetch':>10s} {'write':>10s} {'traffic':>10s} "
@@ -171,11 +200,43 @@ def main():
                    "fetch_bytes_per_step_raw": tot["fetch_raw"] * 1e6, "write_bytes_per_step": tot["write"] * 1e6,
                    "kernel_us_per_step": tot["us"], "dispatch_sets": sets, "random_fetch_factor": rand_factor,
                    "run": os.path.basename(os.path.normpath(a.dir)), "kernels": table,
-                   "alg_bytes_per_step": sum((r["alg_mb"] or 0.0) for r in table) * 1e6 if bline else None,
+                   "alg_bytes_per_step": alg_total,
                    "note": "engine kernels only (sga::, per batch); FETCH_SIZE x2 for coalesced streaming kernels, "
                            "x random16_fetch_factor (tools/calib/pmccal.hip) for random-gather kernels; WRITE_SIZE as "
                            "reported"},
                   open(a.json, "w"), indent=1)
+
+
+def bench_line(path):
+    for line in open(path):
+        if line.startswith("{"):
+            d = json.loads(line)
+    return d
+
+
+def attach_alg(table, bl):
+    """Per-kernel alg_mb / traffic_over_alg and the step total (local lines add the "(state)" row)."""
+    if bl and "entries_per_step" in bl.get("config", {}) and not any(r["kernel"] == "(state)" for r in table):
+        table.append({"kernel": "(state)", "kind": "-", "calls_per_step": 0.0, "fetch_raw_mb": 0.0, "fetch_factor": 0.0,
+                      "fetch_mb": 0.0, "write_mb": 0.0, "us_per_step": None, "traffic_mb": 0.0,
+                      "note": "2 * S_k per touched key, moved by the per-resource kernels (no single kernel)"})
+    for r in table:
+        ab = alg_bytes(r["kernel"], bl)
+        r["alg_mb"] = None if ab is None else ab / 1e6
+        r["traffic_over_alg"] = (r["traffic_mb"] / r["alg_mb"]) if r["alg_mb"] else None
+    return sum((r["alg_mb"] or 0.0) for r in table) * 1e6
+
+
+def relabel(path, steps_from):
+    d = json.load(open(path))
+    bl = bench_line(steps_from)
+    d["alg_bytes_per_step"] = attach_alg(d["kernels"], bl)
+    d["alg_source"] = os.path.basename(steps_from)
+    tr = d["traffic_bytes_per_step"]
+    d["traffic_over_alg"] = tr / d["alg_bytes_per_step"] if d["alg_bytes_per_step"] else None
+    json.dump(d, open(path, "w"), indent=1)
+    print(f"{path}: alg {d['alg_bytes_per_step'] / 1e6:.1f} MB/step, traffic {tr / 1e6:.1f} MB/step, "
+          f"ratio {d['traffic_over_alg']:.2f}")
 
 
 if __name__ == "__main__":
