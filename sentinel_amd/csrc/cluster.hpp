@@ -216,9 +216,10 @@ struct BatchScratch {
     uint32_t *tile_nc;        // per 1024-request segment: elements
     uint64_t *pel_tile;       // per rank segment (kHotSeg requests): the prioritized hot requests (key = hot id),
                               // compacted in arrival order; seg_stat holds their count
-    uint32_t *prow;           // [kPsWgs][kHot]: the prioritized sort's per-workgroup counts, then starts
+    uint32_t *prow;           // [kPsGroups][kHot]: the prioritized requests per group of segments and hot id
+    uint32_t *ppre;           // [kPsGroups][kHot]: the earlier groups' (k_psort_cols)
+    uint32_t *ptot;           // [kHot]: per hot id
     uint64_t *pel[2];         // the prioritized hot requests sorted by hot id (double buffer of their own sort)
-    RadixScratch radix_p;     // the prioritized sort's scratch (it runs on the side stream beside the cold sort)
     uint32_t *hcode;          // per request: hot id | in-segment rank << 12 | bucket << 25 | prioritized << 31
                               // (~0: not a hot request)
     uint16_t *hcnt;           // [segment][kHot] hot requests per hot id
