@@ -2981,6 +2981,83 @@ __global__ __launch_bounds__(kFinGThreads) void k_hot_final_g(ClusterState st, B
     }
 }
 
+// k_hot_final_h (A/B knob SGA_FIN_H=1): as k_hot_final_g, with the segment's rank base row staged in LDS (16 KB, one
+// coalesced fill per 2048 requests) and the fate of every hot request from its run's (f, start) alone (one 8-byte
+// gather): most hot requests are blocked.  Only the passing ones read the run's window sum and the rule's
+// threshold / interval, through buffer loads whose out-of-range offset (every other lane) returns 0 without a
+// memory access, all issued together.
+__global__ __launch_bounds__(kFinGThreads) void k_hot_final_h(ClusterState st, BatchScratch sc, uint32_t n,
+                                                              const uint64_t *__restrict__ el,
+                                                              uint64_t *__restrict__ out) {
+    __shared__ uint32_t base[kHot];
+    if (!sc.counters[CTL_MODE]) return;
+    if (blockIdx.x < kFinPrioWgsG) {
+        prio_results_range(st, sc, el, out, blockIdx.x * kFinGThreads + threadIdx.x, kFinPrioWgsG * kFinGThreads);
+        return;
+    }
+    static_assert(kHotSeg % kFinGSpan == 0, "a workgroup's span lies in one rank segment");
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t wg0 = (blockIdx.x - kFinPrioWgsG) * kFinGSpan;
+    if (wg0 >= n) return;
+    const uint32_t nhot = hot_count(sc);
+    {
+        const uint32_t *row = sc.hbase + (size_t)(wg0 / kHotSeg) * kHot;
+        for (uint32_t h = threadIdx.x; h < nhot; h += kFinGThreads) base[h] = row[h];
+    }
+    const uint32_t wbase = wg0 + (uint32_t)wave * (kFinChunk * 64);
+    uint32_t code[kFinChunk];
+#pragma unroll
+    for (int u = 0; u < kFinChunk; ++u) code[u] = sc.hcode[min(wbase + (uint32_t)u * 64 + lane, n - 1)];
+    uint2 fs[kFinChunk];
+#pragma unroll
+    for (int u = 0; u < kFinChunk; ++u) {  // unconditional gathers (a non-hot lane reads hot id 0's)
+        const uint32_t cd = code[u];
+        const bool hot = cd != kNoCode && !(cd >> 31);
+        fs[u] = sc.hfs[(size_t)(hot ? (cd >> 25) : 0u) * kHot + (hot ? (cd & 0xFFFu) : 0u)];
+    }
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        sc.hrun, 0, (int)((size_t)kHot * kHotBuckets * sizeof(HotRun)), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(sc.hthr, 0, (int)(kHot * sizeof(double2)),
+                                                                        0x00020000);
+    constexpr uint32_t kOob = 0x80000000u;  // past both buffers: the load returns 0, touches nothing
+    uint32_t local[kFinChunk];
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x2 s0v[kFinChunk];
+    u32x4 tiv[kFinChunk];
+#pragma unroll
+    for (int u = 0; u < kFinChunk; ++u) {
+        const uint32_t i = wbase + (uint32_t)u * 64 + lane;
+        const uint32_t cd = code[u];
+        const bool hot = i < n && cd != kNoCode && !(cd >> 31);
+        const uint32_t h = cd & 0xFFFu;
+        local[u] = base[hot ? h : 0u] + ((cd >> 12) & 0x1FFFu) - fs[u].y;
+        const bool pass = hot && local[u] < fs[u].x;
+        const uint32_t ro = pass ? (uint32_t)(((cd >> 25) * (uint32_t)kHot + h) * sizeof(HotRun)) : kOob;
+        const uint32_t to = pass ? h * (uint32_t)sizeof(double2) : kOob;
+        s0v[u] = __builtin_amdgcn_raw_buffer_load_b64(rr, ro, 0, 0);
+        tiv[u] = __builtin_amdgcn_raw_buffer_load_b128(rt, to, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kFinChunk; ++u) {
+        const uint32_t i = wbase + (uint32_t)u * 64 + lane;
+        const uint32_t cd = code[u];
+        if (i >= n || cd == kNoCode || (cd >> 31)) continue;  // cold, invalid or prioritized
+        uint64_t res;
+        if (local[u] < fs[u].x) {
+            const int64_t s0 = (int64_t)(((uint64_t)s0v[u].y << 32) | s0v[u].x);
+            const double thr = __longlong_as_double((long long)(((uint64_t)tiv[u].y << 32) | tiv[u].x));
+            const double isec = __longlong_as_double((long long)(((uint64_t)tiv[u].w << 32) | tiv[u].z));
+            const int64_t sum = s0 + (int64_t)local[u];
+            res = pack_result(TRS_OK, j_d2i(thr - (double)sum / isec - 1.0), 0);
+        } else {
+            res = pack_result(TRS_BLOCKED, 0, 0);
+        }
+        out[i] = res;
+    }
+}
+
 // k_hot_final_p (A/B knob SGA_FIN_P=1; measured slower than k_hot_final_g beside the cold stage, 0.78 against
 // 0.74-0.76 ms per C3 batch): persistent workgroups over
 // consecutive rank segments.  A workgroup stages (f, start) of every hot id's run in its first segment's bucket
@@ -4030,6 +4107,12 @@ static uint32_t fin_cache() {  // profiling knob: SGA_FIN_CACHE=0 turns k_hot_fi
 }
 
 // k_hot_final_g by default; SGA_FIN_LDS=1 (A/B knob) the LDS-cached k_hot_final
+static bool fin_g() {  // A/B knob: SGA_FIN_H=1 takes k_hot_final_h (measured equal: 0.698-0.706 against
+                       // 0.697-0.699 ms per C3 batch; the kernel is not bound by its gathers)
+    static const bool v = !(getenv("SGA_FIN_H") && atoi(getenv("SGA_FIN_H")) == 1);
+    return v;
+}
+
 static void launch_hot_final(const ClusterState &st, BatchScratch &sc, uint32_t n, const uint64_t *pel, uint64_t *out,
                              hipStream_t s) {
     static const bool lds = getenv("SGA_FIN_LDS") && atoi(getenv("SGA_FIN_LDS")) == 1;
@@ -4046,8 +4129,11 @@ static void launch_hot_final(const ClusterState &st, BatchScratch &sc, uint32_t 
         const uint32_t nseg = (n + kHotSeg - 1) / kHotSeg;
         hipLaunchKernelGGL(k_hot_final, dim3(nseg + kFinPrioWgs), dim3(kFinWgThreads), 0, s, st, sc, n, pel, out,
                            fin_cache());
-    } else {
+    } else if (fin_g()) {
         hipLaunchKernelGGL(k_hot_final_g, dim3((n + kFinGSpan - 1) / kFinGSpan + kFinPrioWgsG), dim3(kFinGThreads), 0, s,
+                           st, sc, n, pel, out);
+    } else {
+        hipLaunchKernelGGL(k_hot_final_h, dim3((n + kFinGSpan - 1) / kFinGSpan + kFinPrioWgsG), dim3(kFinGThreads), 0, s,
                            st, sc, n, pel, out);
     }
 }
