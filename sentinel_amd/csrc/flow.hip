@@ -1303,9 +1303,10 @@ struct LAgg {
     uint32_t nh, nf, flag;
     uint32_t nent, nexit, cp;   // entries, exits, prioritized entries since the run head
     int32_t mn, mx;             // entry acquire min / max
+    int64_t asum;               // entry acquire sum
 };
 
-__device__ __forceinline__ LAgg lagg_id() { return LAgg{0, 0, 0, 0, 0, 0, INT32_MAX, INT32_MIN}; }
+__device__ __forceinline__ LAgg lagg_id() { return LAgg{0, 0, 0, 0, 0, 0, INT32_MAX, INT32_MIN, 0}; }
 
 __device__ __forceinline__ LAgg lagg_combine(const LAgg &a, const LAgg &b) {
     LAgg r;
@@ -1317,6 +1318,7 @@ __device__ __forceinline__ LAgg lagg_combine(const LAgg &a, const LAgg &b) {
     r.cp = b.flag ? b.cp : a.cp + b.cp;
     r.mn = b.flag ? b.mn : min(a.mn, b.mn);
     r.mx = b.flag ? b.mx : max(a.mx, b.mx);
+    r.asum = b.flag ? b.asum : a.asum + b.asum;
     return r;
 }
 
@@ -1328,7 +1330,7 @@ __device__ __forceinline__ LAgg lagg_value(uint32_t key, uint32_t pkey, const Pa
     const bool ex = (q.idx & F_EXIT) != 0;
     const int32_t a = (int32_t)(q.acq_prio & 0x7FFFFFFFu);
     return LAgg{h ? 1u : 0u, fh ? 1u : 0u, h ? 1u : 0u, ex ? 0u : 1u, ex ? 1u : 0u,
-                ex ? 0u : (q.acq_prio >> 31), ex ? INT32_MAX : a, ex ? INT32_MIN : a};
+                ex ? 0u : (q.acq_prio >> 31), ex ? INT32_MAX : a, ex ? INT32_MIN : a, ex ? 0 : (int64_t)a};
 }
 
 // blocked arrangement per thread (kItems consecutive events), block scan of thread aggregates
@@ -1502,6 +1504,7 @@ __global__ __launch_bounds__(kT) void k_lruns_down(const uint32_t *__restrict__ 
             sc.run_cp[rid] = run.cp;
             sc.run_amin[rid] = run.mn;
             sc.run_amax[rid] = run.mx;
+            sc.run_asum[rid] = run.asum;
         }
         pk = k;
         pq = q;
@@ -2171,13 +2174,21 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                     }
                 }
             };
-            for (uint32_t g0 = j0; g0 < j1; g0 += 64 * kWavePf) {
+            // Default / WarmUp: once not even the run's smallest acquireCount fits (blocked entries leave
+            // the pass count alone), every later entry blocks -- the walk stops there (js) and k_lresults
+            // writes the tail's decisions over the whole GPU; the blocked acquire is the run's entry sum
+            // less the passes
+            uint32_t js = j1;
+            for (uint32_t g0 = j0; g0 < j1 && js == j1; g0 += 64 * kWavePf) {
 #pragma unroll
                 for (int k = 0; k < kWavePf; ++k) {
                     const uint32_t g = g0 + (uint32_t)k * 64;
                     const Payload q = ring[k];
                     ring[k] = pay[min(g + (uint32_t)(kWavePf * 64 + lane), j1 - 1)];
-                    if (g < j1) window(g, q);  // wave-uniform
+                    if (g < j1 && js == j1) {  // wave-uniform
+                        if (!pace && !passes(0, 0, amin)) js = g;
+                        else window(g, q);
+                    }
                 }
             }
             for (int o = 32; o >= 1; o >>= 1) {
@@ -2185,6 +2196,7 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                 ba += __shfl_xor(ba, o);
                 npass += __shfl_xor(npass, o);
             }
+            if (!pace) ba = sc.run_asum[r] - pa;
             if (lane == 0) {
                 if (pace) rule.latest_passed = latest;
                 int64_t *sb = sec_current(node, t0, max_rt);
@@ -2202,6 +2214,7 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                     if (exmin < b[MB_MINRT]) b[MB_MINRT] = exmin;
                 }
                 node[kNodeThreads] += npass - (int64_t)sc.run_nexit[r];
+                sc.run_f[r] = js;  // RUN_POS: entries from js on blocked, not in ev_eidx
                 sc.run_mode[r] = RUN_POS;
             }
             __syncthreads();
@@ -4653,6 +4666,11 @@ __global__ __launch_bounds__(kT) void k_lresults(FlowScratch sc, const Payload *
     if (mode == RUN_FAST) {
         decision[q.idx & F_IDX] = sc.ev_eidx[j] < sc.run_f[r] ? D_PASS : D_BLOCK_FLOW;
     } else {
+        if (mode == RUN_POS && j >= sc.run_f[r]) {  // k_lwave's saturated tail
+            decision[q.idx & F_IDX] = D_BLOCK_FLOW;
+            if (wait_ms) wait_ms[q.idx & F_IDX] = 0;
+            return;
+        }
         const uint32_t v = sc.ev_eidx[j];
         if (v == ~0u) return;
         decision[q.idx & F_IDX] = (v & 1u) ? D_BLOCK_FLOW : D_PASS;
@@ -5638,7 +5656,8 @@ int FlowEngine::ensure_scratch() {
         size_t bytes = 2 * al(cap * 4) + 2 * al(cap * sizeof(Payload)) + 2 * al(cap * 4) + 11 * al(cap * 4) +
                        4 * al(cap * 8) + al(cap) + 3 * al(cap * 4) + 2 * al(ntiles * sizeof(LAgg)) + al(ntiles * 4) +
                        al(64) + 2 * al(hist * 4) + al(scan_partials_needed(hist) * 4 + 64) + al(cap * 4) +
-                       2 * al(cap * 8) + al(cap * 4) + 2 * al(cap * 8) + al(cap * 4) + al(kRadixGhistWords * 4) + al(64) + al(cap * 4) + al((cap / 256 + 16) * 8) + al(cap * 8);
+                       2 * al(cap * 8) + al(cap * 4) + 2 * al(cap * 8) + al(cap * 4) + al(kRadixGhistWords * 4) + al(64) + al(cap * 4) + al((cap / 256 + 16) * 8) + al(cap * 8) +
+                       al(cap * 8);  // run_asum
         d_scratch.alloc(bytes);
         char *p = (char *)d_scratch.p;
         auto take = [&](size_t b) {
@@ -5660,6 +5679,7 @@ int FlowEngine::ensure_scratch() {
         sc.run_cp = (uint32_t *)take(cap * 4);
         sc.run_amin = (int32_t *)take(cap * 4);
         sc.run_amax = (int32_t *)take(cap * 4);
+        sc.run_asum = (int64_t *)take(cap * 8);
         sc.run_nexit = (uint32_t *)take(cap * 4);
         sc.run_f = (uint32_t *)take(cap * 4);
         sc.run_exc = (uint64_t *)take(cap * 8);

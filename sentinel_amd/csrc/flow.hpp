@@ -173,6 +173,7 @@ struct FlowScratch {
     uint32_t *ev_run, *ev_eidx;
     uint32_t *run_start, *run_end, *run_slot, *run_t0off, *run_nent, *run_cp;
     int32_t *run_amin, *run_amax;
+    int64_t *run_asum;            // entries' acquire counts per run (k_lwave's saturated tail: blocks = sum - passes)
     uint64_t *run_exc, *run_exerr;
     int64_t *run_exrt, *run_exmin;
     uint32_t *run_nexit;
