@@ -28,10 +28,11 @@ ONE_TIME = {"k_init_slots", "k_hot_reset", "k_lds_order_probe", "k_conc_reset", 
 # reads are coalesced streams (input arrays, sort tiles, codes, count rows)
 STREAMING = {"k_hot_key_dense<0>", "k_hot_key_dense<1>", "k_hot_final", "k_rs64_hist<7>", "k_rs64_sweep<7>",
              "k_row_scan", "k_hscan_group", "k_hscan_mid", "k_hscan_down", "k_hot_pre", "k_hot_mode",
-             "k_prio_rank", "k_prio_results", "k_part_colscan", "k_part_binscan", "k_part_scatter"}
+             "k_prio_rank", "k_prio_results", "k_part_colscan", "k_part_binscan", "k_part_scatter", "k_psort_cols",
+             "k_psort_scatter", "k_unpack"}
 # reads are dominated by random gathers of rule records / parameters
 RANDOM = {"k_cold_fused", "k_hot_flows", "k_hot_precheck", "k_hot_hist", "k_hot_pick", "k_hot_clear", "k_hot_fin",
-          "k_cluster_nodes", "k_hot_final_g"}
+          "k_cluster_nodes", "k_hot_final_g", "k_hot_final_h", "k_hot_next_a", "k_hot_next_b"}
 
 
 def base(k):
@@ -96,7 +97,7 @@ def alg_bytes(k, bl):
         return n_cold * 8.0 + (touched - t_hot) * 2 * 704.0
     if b == "k_hot_flows":
         return t_hot * 2 * 704.0
-    if b in ("k_hot_final", "k_hot_final_g"):
+    if b in ("k_hot_final", "k_hot_final_g", "k_hot_final_h"):
         return (n - n_cold) * 8.0
     return 0.0
 
