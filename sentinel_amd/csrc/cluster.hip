@@ -1706,11 +1706,6 @@ __device__ __forceinline__ uint32_t rank_hot(uint32_t *cw, uint32_t hid) {
     return (atomicAdd(&cw[hid >> 1], 1u << sh) >> sh) & 0xFFFFu;
 }
 
-__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
 
 __device__ __forceinline__ uint32_t hot_count(const BatchScratch &sc) {
     return min(sc.hot_ctl[0], (uint32_t)kHot);
@@ -2063,8 +2058,7 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
     }
     if (wflags) atomicOr(&sc.counters[CTL_FLAGS], wflags);
     if (nhot) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) bdmax = max(bdmax, (uint32_t)__shfl_xor((int)bdmax, o, 64));
+bdmax = wave_max_u32(bdmax);
         if (lane == 0) {
             s_np[wave] = np;
             s_bd[wave] = bdmax;
@@ -2120,8 +2114,7 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
         }
     }
     {  // the segment's latest request time (offset from ts_base): k_hot_mode keeps the maximum over batches
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) tmax_l = max(tmax_l, (uint32_t)__shfl_xor((int)tmax_l, o, 64));
+tmax_l = wave_max_u32(tmax_l);
         if (lane == 0) sh.s_tm[wave] = tmax_l;
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -2318,13 +2311,10 @@ __global__ __launch_bounds__(1024) void k_hot_mode(BatchScratch sc, uint32_t nsu
         }
         tm = max(tm, sc.seg_stat[kSegStat * k + 2]);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        ns += (uint32_t)__shfl_xor((int)ns, o, 64);
-        np += (uint32_t)__shfl_xor((int)np, o, 64);
-        bd = max(bd, (uint32_t)__shfl_xor((int)bd, o, 64));
-        tm = max(tm, (uint32_t)__shfl_xor((int)tm, o, 64));
-    }
+    ns = wave_sum_u32(ns);
+    np = wave_sum_u32(np);
+    bd = wave_max_u32(bd);
+    tm = wave_max_u32(tm);
     if ((threadIdx.x & 63) == 0) {
         red[0][threadIdx.x >> 6] = ns;
         red[1][threadIdx.x >> 6] = np;
@@ -2859,8 +2849,7 @@ __global__ __launch_bounds__(kFinWgThreads) void k_hot_final(ClusterState st, Ba
     for (int u = 0; u < kFinChunk; ++u) cn[u] = sc.hcode[min(wbase + (uint32_t)u * 64 + lane, n - 1)];
     if (wave == 0) {  // the segment's first bucket: the smallest among its first 64 codes
         uint32_t bk = (cn[0] >> 31) ? 0xFFu : (cn[0] >> 25);
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) bk = min(bk, (uint32_t)__shfl_xor((int)bk, d));
+        bk = wave_min_u32(bk);
         if (lane == 0) s_b0 = bk == 0xFFu ? sc.counters[CTL_BDLO] : bk;
     }
     for (uint32_t h = threadIdx.x; h < nhot; h += kFinWgThreads) base[h] = sc.hbase[(size_t)seg * kHot + h];
@@ -4885,11 +4874,8 @@ __global__ __launch_bounds__(kThreads) void k_ts_minmax(const int64_t *__restric
         lo = min(lo, t);
         hi = max(hi, t);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        lo = min(lo, (int64_t)__shfl_xor((long long)lo, o, 64));
-        hi = max(hi, (int64_t)__shfl_xor((long long)hi, o, 64));
-    }
+    lo = wave_min_i64(lo);
+    hi = wave_max_i64(hi);
     if ((threadIdx.x & 63) == 0) {
         atomicMin((long long *)&mm[0], (long long)lo);
         atomicMax((long long *)&mm[1], (long long)hi);

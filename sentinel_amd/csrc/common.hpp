@@ -196,6 +196,32 @@ __device__ __forceinline__ void wave_incl_segsum2(int &a, int &b, int &hd) {
     segsum2_step<0x143, 0xc>(a, b, hd);
 }
 
+// whole-wave reductions through DPP row shifts and row broadcasts (no LDS permutes): the inclusive scan's
+// lane 63, read as a wave-uniform value.  Every lane of the wave must be active.
+template <class Op>
+__device__ __forceinline__ uint32_t wave_reduce_u32(uint32_t v, uint32_t id, Op op) {
+    int x = (int)v;
+    x = (int)op((uint32_t)x, (uint32_t)dpp::mov32<0x111, 0xf>((int)id, x));
+    x = (int)op((uint32_t)x, (uint32_t)dpp::mov32<0x112, 0xf>((int)id, x));
+    x = (int)op((uint32_t)x, (uint32_t)dpp::mov32<0x114, 0xf>((int)id, x));
+    x = (int)op((uint32_t)x, (uint32_t)dpp::mov32<0x118, 0xf>((int)id, x));
+    x = (int)op((uint32_t)x, (uint32_t)dpp::mov32<0x142, 0xa>((int)id, x));
+    x = (int)op((uint32_t)x, (uint32_t)dpp::mov32<0x143, 0xc>((int)id, x));
+    return (uint32_t)__builtin_amdgcn_readlane(x, 63);
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    return wave_reduce_u32(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    return wave_reduce_u32(v, 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+}
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+    return wave_reduce_u32(v, 0u, [](uint32_t a, uint32_t b) { return a | b; });
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    return wave_reduce_u32(v, 0xFFFFFFFFu, [](uint32_t a, uint32_t b) { return a < b ? a : b; });
+}
+
 // inclusive prefix sum of an int64 over the wave (lane order)
 __device__ __forceinline__ int64_t wave_incl_sum_i64(int64_t v) {
     v += dpp::mov64<0x111, 0xf>(0, v);
@@ -234,4 +260,9 @@ __device__ __forceinline__ int64_t readlane_i64(int64_t v, int l) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
+
+// whole-wave int64 sum / max / min (DPP scan, lane 63); every lane of the wave must be active
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) { return readlane_i64(wave_incl_sum_i64(v), 63); }
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) { return readlane_i64(wave_incl_max_i64(v), 63); }
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) { return readlane_i64(wave_incl_min_i64(v), 63); }
 }  // namespace sga

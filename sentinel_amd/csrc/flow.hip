@@ -1075,7 +1075,7 @@ __global__ __launch_bounds__(kT) void k_lgate(const uint8_t *__restrict__ kind, 
             g |= kGateSeq;
         }
     }
-    for (int d = 32; d >= 1; d >>= 1) g |= (uint32_t)__shfl_xor((int)g, d);
+    g = wave_or_u32(g);
     if ((threadIdx.x & 63) == 0 && g) atomicOr(gate, g);
 }
 
@@ -2060,13 +2060,22 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
 #pragma unroll
             for (int k = 0; k < kWavePf; ++k) ring[k] = pay[min(j0 + (uint32_t)(k * 64 + lane), j1 - 1)];
             bool pred_c = true;  // pacing: the last decision of an entry with a nonzero cost
+            int64_t ctab[5] = {0, 0, 0, 0, 0};
+            if (pace && rcount > 0)
+#pragma unroll
+                for (int k = 0; k < 5; ++k) ctab[k] = j_round(1.0 * (k + 1) / rcount * 1000);
             auto window = [&](uint32_t g, Payload q) {
                 const uint32_t j = g + (uint32_t)lane;
                 if (j >= j1) q.idx = F_EXIT;
                 const bool ent = !(q.idx & F_EXIT);
                 const int64_t t = ts_base + (int64_t)q.ts_off;
                 const int aq = ent ? (int)(q.acq_prio & 0x7FFFFFFFu) : 0;
-                const int64_t cost = (pace && ent && aq > 0 && rcount > 0) ? j_round(1.0 * aq / rcount * 1000) : 0;
+                // costTime = Math.round(1.0 * acquireCount / count * 1000): acquire counts 1..5 from the run's
+                // table (the same expression, evaluated once per run), others divided here
+                int64_t cost = 0;
+                if (pace && ent && aq > 0 && rcount > 0)
+                    cost = aq == 1 ? ctab[0] : aq == 2 ? ctab[1] : aq == 3 ? ctab[2] : aq == 4 ? ctab[3] : aq == 5 ? ctab[4] : -1;
+                if (__ballot(cost < 0) && cost < 0) cost = j_round(1.0 * aq / rcount * 1000);
                 int8_t d = D_PASS;
                 int64_t w = 0;
                 uint64_t rem = __ballot(ent);
@@ -2191,11 +2200,9 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                     }
                 }
             }
-            for (int o = 32; o >= 1; o >>= 1) {
-                pa += __shfl_xor(pa, o);
-                ba += __shfl_xor(ba, o);
-                npass += __shfl_xor(npass, o);
-            }
+            pa = wave_sum_i64(pa);
+            ba = wave_sum_i64(ba);
+            npass = wave_sum_i64(npass);
             if (!pace) ba = sc.run_asum[r] - pa;
             if (lane == 0) {
                 if (pace) rule.latest_passed = latest;
@@ -3082,16 +3089,8 @@ __device__ __forceinline__ uint32_t ps_uni32(uint32_t x) { return (uint32_t)__bu
 __device__ __forceinline__ uint64_t ps_uni64(uint64_t x) {
     return (uint64_t)ps_uni32((uint32_t)x) | ((uint64_t)ps_uni32((uint32_t)(x >> 32)) << 32);
 }
-__device__ __forceinline__ int64_t ps_wave_sum(int64_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += (int64_t)__shfl_xor((long long)x, o, 64);
-    return x;
-}
-__device__ __forceinline__ uint32_t ps_wave_max(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
-    return x;
-}
+__device__ __forceinline__ int64_t ps_wave_sum(int64_t x) { return wave_sum_i64(x); }
+__device__ __forceinline__ uint32_t ps_wave_max(uint32_t x) { return wave_max_u32(x); }
 
 // Two waves per resource, one chunk apart: wave 0 decides chunk c (the time/token map, the decisions, the node
 // statistics) while wave 1 applies chunk c - 1's thread counts (the thread-count map follows the decisions and
