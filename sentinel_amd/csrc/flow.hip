@@ -2060,22 +2060,13 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
 #pragma unroll
             for (int k = 0; k < kWavePf; ++k) ring[k] = pay[min(j0 + (uint32_t)(k * 64 + lane), j1 - 1)];
             bool pred_c = true;  // pacing: the last decision of an entry with a nonzero cost
-            int64_t ctab[5] = {0, 0, 0, 0, 0};
-            if (pace && rcount > 0)
-#pragma unroll
-                for (int k = 0; k < 5; ++k) ctab[k] = j_round(1.0 * (k + 1) / rcount * 1000);
             auto window = [&](uint32_t g, Payload q) {
                 const uint32_t j = g + (uint32_t)lane;
                 if (j >= j1) q.idx = F_EXIT;
                 const bool ent = !(q.idx & F_EXIT);
                 const int64_t t = ts_base + (int64_t)q.ts_off;
                 const int aq = ent ? (int)(q.acq_prio & 0x7FFFFFFFu) : 0;
-                // costTime = Math.round(1.0 * acquireCount / count * 1000): acquire counts 1..5 from the run's
-                // table (the same expression, evaluated once per run), others divided here
-                int64_t cost = 0;
-                if (pace && ent && aq > 0 && rcount > 0)
-                    cost = aq == 1 ? ctab[0] : aq == 2 ? ctab[1] : aq == 3 ? ctab[2] : aq == 4 ? ctab[3] : aq == 5 ? ctab[4] : -1;
-                if (__ballot(cost < 0) && cost < 0) cost = j_round(1.0 * aq / rcount * 1000);
+                const int64_t cost = (pace && ent && aq > 0 && rcount > 0) ? j_round(1.0 * aq / rcount * 1000) : 0;
                 int8_t d = D_PASS;
                 int64_t w = 0;
                 uint64_t rem = __ballot(ent);
