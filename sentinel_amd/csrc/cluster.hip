@@ -894,6 +894,7 @@ constexpr int kFzShortRun = 4;  // SGA_FZ_DEBUG bit 256 (A/B): the round-4 form 
 constexpr int kFzDirect = 32;   // closed-form runs of at most this many requests: TokenResults from the flows lane
 constexpr int kFzLong = 512;    // longer runs listed for the results phase (one wave per run); a full list
                                 // sends further runs to their flows lane as well
+constexpr uint32_t kFzHuge = 2048;  // listed runs answered by the whole workgroup (no SHOULD_WAIT among them)
 
 // Profiling only (SGA_FZ_DEBUG bit 16): per-phase cycles of k_cold_fused summed over workgroups.
 __device__ unsigned long long g_fz_phase[8];
@@ -1103,7 +1104,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
     __shared__ RlT rl_buf[4 * kRl];
     RlT *rl_n = rl_buf, *rl_cp = rl_buf + kRl, *rl_p0 = rl_buf + 2 * kRl, *rl_ab = rl_buf + 3 * kRl;
     __shared__ uint32_t s_long[kFzLong];  // closed-form runs the flows lanes left to the results phase (heads)
-    __shared__ uint32_t s_nlong;
+    __shared__ uint32_t s_nlong, s_huge;
     const bool scan_results = (dbg & 256) != 0;  // A/B: the round-4 results scan over every element
     __shared__ FAgg wtot[kFzThreads / 64];
     __shared__ uint32_t s_h0, s_E, s_wcnt[kFzThreads / 64];
@@ -1295,6 +1296,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
         s_ncand = 0;
         s_next = kFzThreads;  // rules [0, kFzThreads) go to the lanes of the same index
         s_nlong = 0;
+        s_huge = 0;
     }
     __syncthreads();  // run records and plist (global, this workgroup) before the flows read them
     // next-hot-set candidates: counts of at least the floor (half the last pick threshold) are
@@ -1411,8 +1413,12 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
         bool direct = fast && ri.n <= (scan_results ? (uint32_t)kFzShortRun : (uint32_t)kFzDirect);
         if (fast && !direct && !scan_results) {
             const uint32_t k = atomicAdd(&s_nlong, 1u);
-            if (k < (uint32_t)kFzLong) s_long[k] = r;
-            else direct = true;
+            if (k < (uint32_t)kFzLong) {
+                s_long[k] = r;
+                if (ri.n >= kFzHuge && ro.cw == 0) s_huge = 1u;
+            } else {
+                direct = true;
+            }
         }
         if (direct) {
             // the run's elements in chunks of 8, loaded together at clamped positions, decided as the results
@@ -1468,9 +1474,41 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
         // element from a ballot prefix
         const uint32_t nl = (dbg & 2) ? 0u : min(s_nlong, (uint32_t)kFzLong);
         const uint64_t lt = lanemask_lt64(lane);
+        // huge runs without SHOULD_WAIT answers (no prioritized count needed): the whole workgroup over each
+        // run's elements, eight loads in flight per thread (the sort path's hottest rule would otherwise be one
+        // wave's serial walk: C5a 2.95 against 1.18 ms per step)
+        auto run_len = [&](uint32_t hp) { return (hp - h0 < rl_cap) ? (uint32_t)rl_n[hp - h0] : sc.run_start[hp]; };
+        for (uint32_t k = 0; k < (s_huge ? nl : 0u); ++k) {
+            const uint32_t hp = s_long[k];
+            const RunOut ro = sc.run_out[hp];
+            const uint32_t n = run_len(hp);
+            if (ro.cw != 0 || n < kFzHuge) continue;
+            constexpr uint32_t kStep = kFzThreads * 8;
+            for (uint32_t c0 = 0; c0 < n; c0 += kStep) {
+                uint64_t x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = EL(hp + min(c0 + (uint32_t)u * kFzThreads + threadIdx.x, n - 1));
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t loc = c0 + (uint32_t)u * kFzThreads + threadIdx.x;
+                    if (loc >= n) break;
+                    const int32_t a = el_acq(x[u]);
+                    uint64_t res;
+                    if (loc < ro.f) {
+                        const int64_t sum = ro.s0 + (int64_t)loc * a;
+                        res = pack_result(TRS_OK, j_d2i(ro.thr - (double)sum / ro.isec - (double)a), 0);
+                    } else {
+                        res = pack_result(TRS_BLOCKED, 0, 0);
+                    }
+                    if (!(dbg & 128)) out[el_idx(x[u])] = res;
+                }
+            }
+        }
+        // the other long runs: one wave per run, the prioritized requests before each element from a ballot prefix
         for (uint32_t k = (uint32_t)wave; k < nl; k += kFzThreads / 64) {
             const uint32_t hp = s_long[k];
             const RunOut ro = sc.run_out[hp];
+            if (ro.cw == 0 && run_len(hp) >= kFzHuge) continue;
             const uint32_t n = (hp - h0 < rl_cap) ? (uint32_t)rl_n[hp - h0] : sc.run_start[hp];
             uint32_t kp0 = 0;
             for (uint32_t c0 = 0; c0 < n; c0 += 64) {
