@@ -1977,7 +1977,7 @@ constexpr int kHeavyRules = 16, kHeavyCbs = 16, kHeavyChunk = 512, kHeavySlots =
 // A window costs one iteration per pass after its first block, instead of one dependent step per entry.
 // Runs with a uniform acquire keep the closed form, and runs that go back in time or hold prioritized
 // entries take lane_run on lane 0, exactly as in k_lflows.
-constexpr int kWavePf = 8;  // k_lwave: windows loaded ahead
+constexpr int kWavePf = 8;  // k_lwave: windows loaded ahead (even: RateLimiter runs take them in pairs)
 __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, FlowScratch sc,
                                               const Payload *__restrict__ pay, int64_t ts_base,
                                               const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in,
@@ -1987,6 +1987,7 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
     const int lane = threadIdx.x;
     const uint32_t nwave = sc.counters[9], nflows = sc.counters[2], nruns = sc.counters[1];
     uint64_t pr_iter = 0, pr_lr = 0, pr_lrt = 0;  // profiling (SGA_LWAVE_PROF=1)
+    constexpr bool pace_pairs = true;  // RateLimiter windows two at a time (pace2)
     for (uint32_t h = blockIdx.x; h < nwave; h += gridDim.x) {
         const uint32_t fl = sc.pace[h];
         const uint32_t r0 = sc.flow_first_run[fl];
@@ -2174,6 +2175,101 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                     }
                 }
             };
+            // the decided entry's store (sorted order, coalesced; k_lresults scatters it by request index) and
+            // this lane's share of the statistics
+            auto store_ev = [&](uint32_t j, const Payload &q, bool ent, int aq, int8_t d, int64_t w) {
+                if (!(ent && j < j1)) return;
+                if (w < ((int64_t)1 << 30)) {
+                    sc.ev_eidx[j] = ((uint32_t)w << 1) | (d != D_PASS ? 1u : 0u);
+                } else {
+                    const uint32_t idx = q.idx & F_IDX;
+                    decision[idx] = d;
+                    wait_ms[idx] = (int32_t)w;
+                    sc.ev_eidx[j] = ~0u;
+                }
+                if (d == D_PASS) {
+                    pa += aq;
+                    ++npass;
+                } else {
+                    ba += aq;
+                }
+            };
+            // RateLimiter, two windows (128 entries) per step: the same speculation as window(), the two
+            // halves' max-plus scans independent (the second composed with the first's total), so their
+            // dependent DPP chains interleave -- one wave's window walk is bound by that latency
+            auto pace2 = [&](uint32_t g, Payload q0, Payload q1) {
+                const uint32_t ja = g + (uint32_t)lane, jb = g + 64u + (uint32_t)lane;
+                if (ja >= j1) q0.idx = F_EXIT;
+                if (jb >= j1) q1.idx = F_EXIT;
+                const bool ea = !(q0.idx & F_EXIT), eb = !(q1.idx & F_EXIT);
+                const int64_t ta = ts_base + (int64_t)q0.ts_off, tb = ts_base + (int64_t)q1.ts_off;
+                const int aa = ea ? (int)(q0.acq_prio & 0x7FFFFFFFu) : 0, ab = eb ? (int)(q1.acq_prio & 0x7FFFFFFFu) : 0;
+                const int64_t ca = (ea && aa > 0 && rcount > 0) ? j_round(1.0 * aa / rcount * 1000) : 0;
+                const int64_t cb = (eb && ab > 0 && rcount > 0) ? j_round(1.0 * ab / rcount * 1000) : 0;
+                int8_t da = D_PASS, db = D_PASS;
+                int64_t wa = 0, wb = 0;
+                uint64_t ra = __ballot(ea), rb = __ballot(eb);
+                while (ra | rb) {
+                    if (prof) ++pr_iter;
+                    const bool oa = (ra >> lane) & 1ull, ob = (rb >> lane) & 1ull;
+                    const bool mva = oa && aa > 0 && rcount > 0, mvb = ob && ab > 0 && rcount > 0;
+                    const bool spa = aa <= 0 || (rcount > 0 && (ca == 0 || pred_c));
+                    const bool spb = ab <= 0 || (rcount > 0 && (cb == 0 || pred_c));
+                    int64_t Aa = (mva && spa) ? ca : 0, Ba = (mva && spa) ? ta : kMaxPlusNegInf;
+                    int64_t Ab = (mvb && spb) ? cb : 0, Bb = (mvb && spb) ? tb : kMaxPlusNegInf;
+                    wave_incl_maxplus(Aa, Ba);
+                    wave_incl_maxplus(Ab, Bb);
+                    const int64_t Lka = max(latest + Aa, Ba);
+                    const int64_t Lenda = readlane_i64(Lka, 63);
+                    const int64_t Lkb = max(Lenda + Ab, Bb);
+                    const int64_t Lpa = wave_shr1_i64(Lka, latest), Lpb = wave_shr1_i64(Lkb, Lenda);
+                    const bool aca = aa <= 0 || (rcount > 0 && (ca + Lpa <= ta || ca + Lpa - ta <= rqueue));
+                    const bool acb = ab <= 0 || (rcount > 0 && (cb + Lpb <= tb || cb + Lpb - tb <= rqueue));
+                    const uint64_t misa = __ballot(oa && aca != spa);
+                    // the first wrong prediction of a half: the lanes before it decided, its true decision
+                    auto fix = [&](const int m, const bool op, const bool sp, const bool mvv, const int64_t Lk,
+                                   const int64_t Lstart, const bool ac, const int av, const int64_t tv,
+                                   const int64_t cv, int8_t &d, int64_t &w, uint64_t &r) {
+                        if (op && lane < m) {
+                            d = sp ? D_PASS : D_BLOCK_FLOW;
+                            if (sp && mvv) w = Lk - tv;
+                        }
+                        latest = m > 0 ? readlane_i64(Lk, m - 1) : Lstart;
+                        const int am = __builtin_amdgcn_readlane(av, m);
+                        const int64_t tm = readlane_i64(tv, m), cm = readlane_i64(cv, m);
+                        const bool pm = (__ballot(ac) >> m) & 1ull;
+                        if (lane == m) d = pm ? D_PASS : D_BLOCK_FLOW;
+                        if (pm && am > 0) {
+                            const int64_t lm = max(latest + cm, tm);
+                            if (lane == m) w = lm - tm;
+                            latest = lm;
+                        }
+                        if (am > 0 && cm > 0) pred_c = pm;
+                        r &= (m == 63) ? 0ull : (~0ull << (m + 1));
+                    };
+                    if (misa) {
+                        fix(__builtin_ctzll(misa), oa, spa, mva, Lka, latest, aca, aa, ta, ca, da, wa, ra);
+                        continue;
+                    }
+                    if (oa) {  // every open prediction of the first half was right
+                        da = spa ? D_PASS : D_BLOCK_FLOW;
+                        if (spa && mva) wa = Lka - ta;
+                    }
+                    ra = 0;
+                    const uint64_t misb = __ballot(ob && acb != spb);
+                    if (!misb) {
+                        if (ob) {
+                            db = spb ? D_PASS : D_BLOCK_FLOW;
+                            if (spb && mvb) wb = Lkb - tb;
+                        }
+                        latest = readlane_i64(Lkb, 63);
+                        break;
+                    }
+                    fix(__builtin_ctzll(misb), ob, spb, mvb, Lkb, Lenda, acb, ab, tb, cb, db, wb, rb);
+                }
+                store_ev(ja, q0, ea, aa, da, wa);
+                store_ev(jb, q1, eb, ab, db, wb);
+            };
             // Default / WarmUp: once not even the run's smallest acquireCount fits (blocked entries leave
             // the pass count alone), every later entry blocks -- the walk stops there (js) and k_lresults
             // writes the tail's decisions over the whole GPU; the blocked acquire is the run's entry sum
@@ -2183,6 +2279,14 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
 #pragma unroll
                 for (int k = 0; k < kWavePf; ++k) {
                     const uint32_t g = g0 + (uint32_t)k * 64;
+                    if (pace && pace_pairs) {  // windows k, k + 1 together (kWavePf is even)
+                        if (k & 1) continue;
+                        const Payload q0 = ring[k], q1 = ring[k + 1];
+                        ring[k] = pay[min(g + (uint32_t)(kWavePf * 64 + lane), j1 - 1)];
+                        ring[k + 1] = pay[min(g + 64u + (uint32_t)(kWavePf * 64 + lane), j1 - 1)];
+                        if (g < j1) pace2(g, q0, q1);  // wave-uniform
+                        continue;
+                    }
                     const Payload q = ring[k];
                     ring[k] = pay[min(g + (uint32_t)(kWavePf * 64 + lane), j1 - 1)];
                     if (g < j1 && js == j1) {  // wave-uniform
