@@ -1977,7 +1977,10 @@ constexpr int kHeavyRules = 16, kHeavyCbs = 16, kHeavyChunk = 512, kHeavySlots =
 // A window costs one iteration per pass after its first block, instead of one dependent step per entry.
 // Runs with a uniform acquire keep the closed form, and runs that go back in time or hold prioritized
 // entries take lane_run on lane 0, exactly as in k_lflows.
-constexpr int kWavePf = 8;  // k_lwave: windows loaded ahead (even: RateLimiter runs take them in pairs)
+#ifndef SGA_WAVE_PF
+#define SGA_WAVE_PF 8
+#endif
+constexpr int kWavePf = SGA_WAVE_PF;  // k_lwave: windows loaded ahead (even: RateLimiter runs take them in pairs)
 __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, FlowScratch sc,
                                               const Payload *__restrict__ pay, int64_t ts_base,
                                               const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in,
