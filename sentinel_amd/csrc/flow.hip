@@ -1592,7 +1592,7 @@ __device__ __forceinline__ bool default_cond(double count, int64_t sum, int32_t 
 // One run of a resource decided by one lane (k_lflows; k_lwave's lane 0 for runs it cannot split):
 // RateLimiter pacing in registers, the per-event slot chain, or the closed form (RUN_FAST: k_lresults
 // writes the decisions from run_f).
-__device__ void lane_run(const Ctx &c, int64_t max_rt, FlowScratch &sc, const Payload *__restrict__ pay,
+__device__ __noinline__ void lane_run(const Ctx &c, int64_t max_rt, FlowScratch &sc, const Payload *__restrict__ pay,
                          int64_t ts_base, const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in,
                          int8_t *decision, int32_t *wait_ms, uint32_t r) {
     const FlowState &st = c.st;
@@ -1981,6 +1981,9 @@ constexpr int kHeavyRules = 16, kHeavyCbs = 16, kHeavyChunk = 512, kHeavySlots =
 #define SGA_WAVE_PF 8
 #endif
 constexpr int kWavePf = SGA_WAVE_PF;  // k_lwave: windows loaded ahead (even: RateLimiter runs take them in pairs)
+// kRl: 1 = the RateLimiter resources only, 0 = the others (two launches, each compiled without the other's
+// window code: one kernel holding both spilled registers and waited on its own stores)
+template <int kRl>
 __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, FlowScratch sc,
                                               const Payload *__restrict__ pay, int64_t ts_base,
                                               const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in,
@@ -1995,6 +1998,7 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
         const uint32_t fl = sc.pace[h];
         const uint32_t r0 = sc.flow_first_run[fl];
         const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        if (((st.res[sc.run_slot[r0]].fast & 4u) != 0) != (kRl != 0)) continue;  // the other launch's
         const uint64_t pt0 = prof ? wall_clock64() : 0;
         for (uint32_t r = r0; r < r1; ++r) {
             const uint32_t res = sc.run_slot[r];
@@ -2010,8 +2014,8 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                 const int64_t *mb = node + kNodeMin + kMB * (int)((t0 / kMinW) % 60);
                 regress = (sb[0] != kAbsent && t0 - t0 % kSecW < sb[0]) || (mb[0] != kAbsent && t0 - t0 % kMinW < mb[0]);
             }
-            const bool pace = (R.fast & 4u) && !regress;
-            bool greedy = (R.fast & 1u) && !regress && sc.run_cp[r] == 0 && amin >= 0 && nent > 0 && amin != amax;
+            const bool pace = kRl && (R.fast & 4u) && !regress;
+            bool greedy = !kRl && (R.fast & 1u) && !regress && sc.run_cp[r] == 0 && amin >= 0 && nent > 0 && amin != amax;
             FlowRuleDev &rule = st.rules[R.rule_off];
             int64_t s0 = 0;
             double lim = 0;
@@ -5945,9 +5949,11 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
             hipLaunchKernelGGL(k_llru_ps, dim3(256), dim3(128), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo,
                                d_param.p, d_dec.p, d_wait.p);
         }
-        hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
-                           dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
-                           d_dec.p, d_wait.p, lwave_prof());
+        for (int rl = 0; rl < 2; ++rl)
+            hipLaunchKernelGGL(rl ? k_lwave<1> : k_lwave<0>,
+                               dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
+                               dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
+                               d_dec.p, d_wait.p, lwave_prof());
         print_lwave_prof(stream);
         hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
@@ -6070,9 +6076,10 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
         hipLaunchKernelGGL(k_llru_ps, dim3(256), dim3(128), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base,
                            param_p, d_decision, wait_p);
     }
-    hipLaunchKernelGGL(k_lwave, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
-                       st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
-                       lwave_prof());
+    for (int rl = 0; rl < 2; ++rl)
+        hipLaunchKernelGGL(rl ? k_lwave<1> : k_lwave<0>, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))),
+                           dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision,
+                           wait_p, lwave_prof());
     print_lwave_prof(s);
     hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
                        st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
