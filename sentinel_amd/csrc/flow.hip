@@ -40,6 +40,12 @@ enum : int8_t { D_PASS = 0, D_BLOCK_FLOW = 1, D_BLOCK_PARAM = 2, D_BLOCK_DEGRADE
                 D_BLOCK_SYSTEM = 5 };
 enum : uint32_t { F_EXIT = 1u << 30, F_ERROR = 1u << 29, F_PARAM = 1u << 28, F_IDX = (1u << 28) - 1 };
 constexpr uint32_t kHeavyEvents = 1024;  // per batch: replayed by k_lheavy instead of one k_lflows lane
+#ifndef SGA_WAVE_EVENTS
+#define SGA_WAVE_EVENTS 256
+#endif
+// per batch: a single-rule fast-path resource decided by one k_lwave wave instead of one k_lflows lane
+// (1024 until round 5; C2's lanes of 256..1023 events were the k_lflows tail)
+constexpr uint32_t kWaveEvents = SGA_WAVE_EVENTS;
 // RUN_POS: k_lwave left each entry's decision and wait in ev_eidx (wait << 1 | blocked; ~0: written
 // already), k_lresults scatters them in parallel
 // RUN_PSEG: a parameter-only resource's run, decided per (rule, value) segment (k_pseg_*)
@@ -1951,7 +1957,7 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
                 sc.heavy[atomicAdd(&sc.counters[8], 1u)] = fl;
                 continue;
             }
-            if ((st.res[res].fast & 5u) && nev >= kHeavyEvents) {  // a long single-rule fast path: k_lwave
+            if ((st.res[res].fast & 5u) && nev >= kWaveEvents) {  // a long single-rule fast path: k_lwave
                 sc.pace[atomicAdd(&sc.counters[9], 1u)] = fl;
                 continue;
             }
@@ -5951,7 +5957,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         }
         for (int rl = 0; rl < 2; ++rl)
             hipLaunchKernelGGL(rl ? k_lwave<1> : k_lwave<0>,
-                               dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
+                               dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kWaveEvents)))),
                                dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
                                d_dec.p, d_wait.p, lwave_prof());
         print_lwave_prof(stream);
@@ -6077,7 +6083,7 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
                            param_p, d_decision, wait_p);
     }
     for (int rl = 0; rl < 2; ++rl)
-        hipLaunchKernelGGL(rl ? k_lwave<1> : k_lwave<0>, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))),
+        hipLaunchKernelGGL(rl ? k_lwave<1> : k_lwave<0>, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kWaveEvents))),
                            dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision,
                            wait_p, lwave_prof());
     print_lwave_prof(s);
