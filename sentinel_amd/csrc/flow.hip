@@ -50,7 +50,12 @@ constexpr uint32_t kWaveEvents = SGA_WAVE_EVENTS;
 // RUN_POS: k_lwave left each entry's decision and wait in ev_eidx (wait << 1 | blocked; ~0: written
 // already), k_lresults scatters them in parallel
 // RUN_PSEG: a parameter-only resource's run, decided per (rule, value) segment (k_pseg_*)
-enum : uint8_t { RUN_FAST = 0, RUN_DONE = 1, RUN_POS = 2, RUN_PSEG = 3 };
+// RUN_WRL: a RateLimiter run k_lflows sent to k_lwave (k_lwsum summarizes its windows); k_lwave turns it
+// into RUN_POS or RUN_WIN
+// RUN_WIN: as RUN_POS, except the run's interior windows k_lwave skipped (wstate: latestPassedTime - ts_base
+// while it held; kWinWalked: walked, in ev_eidx), whose entries k_lresults decides from that state
+enum : uint8_t { RUN_FAST = 0, RUN_DONE = 1, RUN_POS = 2, RUN_PSEG = 3, RUN_WIN = 4, RUN_WRL = 5 };
+constexpr int64_t kWinWalked = INT64_MIN;
 
 struct Ctx {
     FlowState st;
@@ -1959,6 +1964,8 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
                 continue;
             }
             if ((st.res[res].fast & 5u) && nev >= kWaveEvents) {  // a long single-rule fast path: k_lwave
+                if (st.res[res].fast & 4u)
+                    for (uint32_t r = r0; r < r1; ++r) sc.run_mode[r] = RUN_WRL;  // k_lwsum's windows
                 sc.pace[atomicAdd(&sc.counters[9], 1u)] = fl;
                 continue;
             }
@@ -1984,9 +1991,40 @@ constexpr int kHeavyRules = 16, kHeavyCbs = 16, kHeavyChunk = 512, kHeavySlots =
 // A window costs one iteration per pass after its first block, instead of one dependent step per entry.
 // Runs with a uniform acquire keep the closed form, and runs that go back in time or hold prioritized
 // entries take lane_run on lane 0, exactly as in k_lflows.
+// A RateLimiter run's windows (RUN_WRL): the summary of every 64-event window (j / 64) that lies inside one
+// such run, one wave each over the whole GPU, so that k_lwave<1> walks a saturated run by the summaries
+// alone.  Blocked entries and zero-cost passes behind the queue leave latestPassedTime alone
+// (RateLimiterController.java:56-89), so such a window's decisions follow from the state it starts at.
+__global__ __launch_bounds__(256) void k_lwsum(FlowState st, FlowScratch sc, const Payload *__restrict__ pay) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0) || sc.counters[9] == 0) return;
+    const uint32_t nvalid = sc.counters[0];
+    const int lane = threadIdx.x & 63;
+    const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t jb = w * 64;
+    if (jb + 64 > nvalid) return;  // wave-uniform
+    const uint32_t r = sc.ev_run[jb];
+    if (sc.ev_run[jb + 63] != r || sc.run_mode[r] != RUN_WRL) return;  // wave-uniform
+    const double rcount = st.rules[st.res[sc.run_slot[r]].rule_off].count;
+    const Payload q = pay[jb + lane];
+    const bool ent = !(q.idx & F_EXIT);
+    const int aq = ent ? (int)(q.acq_prio & 0x7FFFFFFFu) : 0;
+    const int64_t cost = (ent && aq > 0 && rcount > 0) ? j_round(1.0 * aq / rcount * 1000) : 0;
+    const bool zero = ent && cost == 0;
+    // a cost past 2^40 ms takes the exact walk (Java's long sums)
+    const int64_t key = cost == 0 ? INT64_MIN : cost > ((int64_t)1 << 40) ? INT64_MAX : (int64_t)q.ts_off - cost;
+    const bool zt = zero && aq > 0;
+    const int64_t kmax = wave_max_i64(key);
+    const int64_t a0 = wave_sum_i64(zero ? (int64_t)aq : 0);
+    const uint32_t t0min = wave_min_u32(zt ? q.ts_off : 0xFFFFFFFFu), t0max = wave_max_u32(zt ? q.ts_off : 0u);
+    const uint32_t n0 = (uint32_t)__builtin_popcountll(__ballot(zero));
+    const uint32_t has0 = (uint32_t)(__ballot(zt) != 0);
+    if (lane == 0) sc.wsum[w] = WinSum{kmax, a0, t0min, t0max, n0, has0};
+}
+
 #ifndef SGA_WAVE_PF
 #define SGA_WAVE_PF 8
 #endif
+constexpr uint32_t kWinMin = 512;  // k_lwave<1>: RateLimiter runs of this many events walk window summaries
 constexpr int kWavePf = SGA_WAVE_PF;  // k_lwave: windows loaded ahead (even: RateLimiter runs take them in pairs)
 // kRl: 1 = the RateLimiter resources only, 0 = the others (two launches, each compiled without the other's
 // window code: one kernel holding both spilled registers and waited on its own stores)
@@ -2077,7 +2115,7 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
             bool pred_c = true;  // pacing: the last decision of an entry with a nonzero cost
             auto window = [&](uint32_t g, Payload q) {
                 const uint32_t j = g + (uint32_t)lane;
-                if (j >= j1) q.idx = F_EXIT;
+                if (j >= j1 || j < j0) q.idx = F_EXIT;
                 const bool ent = !(q.idx & F_EXIT);
                 const int64_t t = ts_base + (int64_t)q.ts_off;
                 const int aq = ent ? (int)(q.acq_prio & 0x7FFFFFFFu) : 0;
@@ -2289,7 +2327,43 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
             // writes the tail's decisions over the whole GPU; the blocked acquire is the run's entry sum
             // less the passes
             uint32_t js = j1;
-            for (uint32_t g0 = j0; g0 < j1 && js == j1; g0 += 64 * kWavePf) {
+            // a long RateLimiter run walks k_lwsum's window summaries: a window whose decisions follow from
+            // the state it starts at (every costly entry blocks, zero-cost entries pass behind the queue) is
+            // skipped, its state left in wstate for k_lresults; the run's first and last windows and any
+            // other window are walked as above (RUN_WIN)
+            const bool winmode = pace && rcount > 0 && j1 - j0 >= kWinMin;
+            if (winmode) {
+                const uint32_t wf = j0 / 64, wl = (j1 - 1) / 64;
+                const int64_t qp = rqueue > 0 ? rqueue : 0;
+                for (uint32_t wb = wf; wb <= wl; wb += 64) {
+                    const uint32_t w = wb + (uint32_t)lane;
+                    const bool inner = w > wf && w < wl;
+                    WinSum s{INT64_MAX, 0, 0, 0, 0, 0};
+                    if (inner) s = sc.wsum[w];
+                    uint64_t todo = __ballot(w <= wl);
+                    while (todo) {
+                        const int64_t lo = latest - ts_base, thr = lo - qp;
+                        const bool inert = inner && s.kmax < thr &&
+                                           (!s.has0 || ((int64_t)s.t0max <= lo && (int64_t)s.t0min >= thr));
+                        const uint64_t walk = __ballot(!inert) & todo;
+                        const int first = walk ? __builtin_ctzll(walk) : 64;
+                        const bool skip = ((todo >> lane) & 1ull) && lane < first;
+                        if (skip) {
+                            sc.wstate[w] = lo;
+                            pa += s.a0;
+                            npass += s.n0;
+                        }
+                        if (__ballot(skip && s.kmax != INT64_MIN)) pred_c = false;  // they blocked
+                        if (first == 64) break;
+                        const uint32_t g = (wb + (uint32_t)first) * 64;
+                        const Payload q = pay[min(max(g + (uint32_t)lane, j0), j1 - 1)];
+                        if (lane == first && inner) sc.wstate[w] = kWinWalked;
+                        window(g, q);
+                        todo &= (first == 63) ? 0ull : (~0ull << (first + 1));
+                    }
+                }
+            }
+            for (uint32_t g0 = j0; g0 < j1 && js == j1 && !winmode; g0 += 64 * kWavePf) {
 #pragma unroll
                 for (int k = 0; k < kWavePf; ++k) {
                     const uint32_t g = g0 + (uint32_t)k * 64;
@@ -2312,7 +2386,7 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
             pa = wave_sum_i64(pa);
             ba = wave_sum_i64(ba);
             npass = wave_sum_i64(npass);
-            if (!pace) ba = sc.run_asum[r] - pa;
+            if (!pace || winmode) ba = sc.run_asum[r] - pa;
             if (lane == 0) {
                 if (pace) rule.latest_passed = latest;
                 int64_t *sb = sec_current(node, t0, max_rt);
@@ -2331,7 +2405,7 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                 }
                 node[kNodeThreads] += npass - (int64_t)sc.run_nexit[r];
                 sc.run_f[r] = js;  // RUN_POS: entries from js on blocked, not in ev_eidx
-                sc.run_mode[r] = RUN_POS;
+                sc.run_mode[r] = winmode ? RUN_WIN : RUN_POS;
             }
             __syncthreads();
         }
@@ -4760,8 +4834,8 @@ __global__ __launch_bounds__(kT) void k_lru_res_refresh(FlowState st) {
     st.lru_res[r] = any ? 1 : 0;
 }
 
-__global__ __launch_bounds__(kT) void k_lresults(FlowScratch sc, const Payload *__restrict__ pay, int8_t *decision,
-                                                 int32_t *wait_ms) {
+__global__ __launch_bounds__(kT) void k_lresults(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
+                                                 int8_t *decision, int32_t *wait_ms) {
     if (!gate_is(sc.gate, kGateSeq | kGateBad, 0)) return;
     const uint32_t nvalid = sc.counters[0];
     const uint32_t j = blockIdx.x * kT + threadIdx.x;
@@ -4778,6 +4852,18 @@ __global__ __launch_bounds__(kT) void k_lresults(FlowScratch sc, const Payload *
             decision[q.idx & F_IDX] = D_BLOCK_FLOW;
             if (wait_ms) wait_ms[q.idx & F_IDX] = 0;
             return;
+        }
+        if (mode == RUN_WIN) {  // an interior window k_lwave skipped: RateLimiterController.java:46-89 at its state
+            const uint32_t w = j / 64;
+            const int64_t lo = (w != sc.run_start[r] / 64 && w != (sc.run_end[r] - 1) / 64) ? sc.wstate[w] : kWinWalked;
+            if (lo != kWinWalked) {
+                const int aq = (int)(q.acq_prio & 0x7FFFFFFFu);
+                const double rcount = st.rules[st.res[sc.run_slot[r]].rule_off].count;
+                const int64_t cost = aq > 0 ? j_round(1.0 * aq / rcount * 1000) : 0;
+                decision[q.idx & F_IDX] = cost > 0 ? D_BLOCK_FLOW : D_PASS;
+                if (wait_ms) wait_ms[q.idx & F_IDX] = (cost == 0 && aq > 0) ? (int32_t)(lo - (int64_t)q.ts_off) : 0;
+                return;
+            }
         }
         const uint32_t v = sc.ev_eidx[j];
         if (v == ~0u) return;
@@ -5765,7 +5851,8 @@ int FlowEngine::ensure_scratch() {
                        4 * al(cap * 8) + al(cap) + 3 * al(cap * 4) + 2 * al(ntiles * sizeof(LAgg)) + al(ntiles * 4) +
                        al(64) + 2 * al(hist * 4) + al(scan_partials_needed(hist) * 4 + 64) + al(cap * 4) +
                        2 * al(cap * 8) + al(cap * 4) + 2 * al(cap * 8) + al(cap * 4) + al(kRadixGhistWords * 4) + al(64) + al(cap * 4) + al((cap / 256 + 16) * 8) + al(cap * 8) +
-                       al(cap * 8);  // run_asum
+                       al(cap * 8) +  // run_asum
+                       al((cap / 64 + 2) * sizeof(WinSum)) + al((cap / 64 + 2) * 8);  // wsum, wstate
         d_scratch.alloc(bytes);
         char *p = (char *)d_scratch.p;
         auto take = [&](size_t b) {
@@ -5818,6 +5905,8 @@ int FlowEngine::ensure_scratch() {
         sc.run_np = (uint32_t *)take(cap * 4);
         sc.radix.ghist = (uint32_t *)take(kRadixGhistWords * 4);
         sc.radix.err = (uint32_t *)take(64);
+        sc.wsum = (WinSum *)take((cap / 64 + 2) * sizeof(WinSum));
+        sc.wstate = (int64_t *)take((cap / 64 + 2) * 8);
         sc.cap = cap;
         scratch_cap = cap;
         d_kind.alloc(cap);
@@ -5956,6 +6045,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
             hipLaunchKernelGGL(k_llru_ps, dim3(256), dim3(128), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo,
                                d_param.p, d_dec.p, d_wait.p);
         }
+        hipLaunchKernelGGL(k_lwsum, dim3((unsigned)((m / 64 + 3) / 4 + 1)), dim3(256), 0, stream, st, sc, pay);
         for (int rl = 0; rl < 2; ++rl)
             hipLaunchKernelGGL(rl ? k_lwave<1> : k_lwave<0>,
                                dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kWaveEvents)))),
@@ -5966,7 +6056,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
                            dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
                            d_dec.p, d_wait.p, heavy_prof());
         if (heavy_prof()) print_heavy_prof();
-        hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, stream, sc, pay, d_dec.p, d_wait.p);
+        hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, stream, st, sc, pay, d_dec.p, d_wait.p);
         if (has_in)  // ENTRY_NODE statistics of the inbound events
             hipLaunchKernelGGL(k_entry_stats, dim3(1), dim3(kEnTile), 0, stream, st, (int64_t)cfg.statistic_max_rt,
                                d_kind.p, d_resid.p, d_ts.p, lo, d_acq.p, d_flags.p, d_rt.p, d_dec.p, (uint32_t)m);
@@ -6083,6 +6173,7 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
         hipLaunchKernelGGL(k_llru_ps, dim3(256), dim3(128), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base,
                            param_p, d_decision, wait_p);
     }
+    hipLaunchKernelGGL(k_lwsum, dim3((m / 64 + 3) / 4 + 1), dim3(256), 0, s, st, gsc, pay);
     for (int rl = 0; rl < 2; ++rl)
         hipLaunchKernelGGL(rl ? k_lwave<1> : k_lwave<0>, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kWaveEvents))),
                            dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision,
@@ -6092,7 +6183,7 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
                        st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
                        heavy_prof());
         if (heavy_prof()) print_heavy_prof();
-    hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, s, gsc, pay, d_decision, wait_p);
+    hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, s, st, gsc, pay, d_decision, wait_p);
     hipLaunchKernelGGL(k_entry_stats, dim3(1), dim3(kEnTile), 0, s, st, (int64_t)cfg.statistic_max_rt, d_kind_in,
                        d_resource, d_ts_off, ts_base, d_acquire, flags_p, rt_p, d_decision, m);
     // arrival-order chunks (system rules, collection / argument vectors, kind 2 blocks): k_lseq acts only

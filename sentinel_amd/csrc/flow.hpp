@@ -167,6 +167,17 @@ struct FlowState {
 };
 constexpr uint32_t kLruThread = 1u << 31;
 
+// A RateLimiter window's state-independent summary (flow.hip k_lwsum): its entries with a nonzero
+// cost block while latestPassedTime L is past kmax + maxQueueingTime (kmax: the largest ts_off - cost),
+// and its zero-cost entries pass with L unchanged while L - maxQueueingTime <= t0min and t0max <= L;
+// n0 / a0: the entries that then pass (zero cost or acquireCount 0), their count and acquire sum; has0: any
+// zero-cost entry with a positive acquireCount (t0min / t0max hold)
+struct WinSum {
+    int64_t kmax;
+    int64_t a0;
+    uint32_t t0min, t0max, n0, has0;
+};
+
 struct FlowScratch {
     uint32_t *keys[2];
     Payload *pay[2];
@@ -194,6 +205,8 @@ struct FlowScratch {
     uint32_t *seg;
     int64_t *run_pa, *run_ba;
     uint32_t *run_np;
+    WinSum *wsum;     // per 64-event window (j / 64) of a RateLimiter k_lwave run (k_lwsum)
+    int64_t *wstate;  // per window: the state k_lwave skipped it at, or kWinWalked (flow.hip RUN_WIN)
     void *tile_agg, *tile_carry;
     uint32_t *tile_valid;
     uint32_t *counters;

@@ -253,6 +253,40 @@ def test_pacing_heavy_resources(seed, regress):
          err_pct=0.05, regress_pct=regress)
 
 
+@pytest.mark.parametrize("seed", [41, 42])
+def test_pacing_saturated_windows(seed):
+    """Saturated RateLimiter resources with tens of thousands of entries per second-run: k_lwave<1> walks
+    k_lwsum's window summaries, skipping windows whose costly entries all block and whose zero-cost entries
+    pass behind the queue (their waits L - t from the skipped state, k_lresults RUN_WIN).  acquireCount 0
+    entries (pass, no state), 1 and 2..6 (cost per entry), rules whose acquire-1 entries cost 0 ms (count
+    2500, 4000), 1 ms, 20 ms and a 1 ms queue; arrival rates from 5 to 40 entries per ms; two batches."""
+    rng = np.random.default_rng(seed)
+    flow = [{"resource": 0, "count": 2500.0, "control_behavior": 2, "max_queueing_time_ms": 500},
+            {"resource": 1, "count": 999.0, "control_behavior": 2, "max_queueing_time_ms": 500},
+            {"resource": 2, "count": 50.0, "control_behavior": 2, "max_queueing_time_ms": 500},
+            {"resource": 3, "count": 4000.0, "control_behavior": 2, "max_queueing_time_ms": 1},
+            {"resource": 4, "count": 700.0, "control_behavior": 2, "max_queueing_time_ms": 37}]
+    n_res = len(flow)
+    n = 160_000
+    res = rng.choice(n_res, size=n, p=[0.35, 0.25, 0.15, 0.15, 0.10]).astype(np.uint32)
+    ts = T0 + np.sort(rng.integers(0, 4000, size=n)).astype(np.int64)
+    u = rng.random(n)
+    acq = np.where(u < 0.02, 0, np.where(u < 0.9, 1, rng.integers(2, 7, size=n))).astype(np.int32)
+    st = {"kind": np.zeros(n, np.uint8), "resource": res, "ts": ts, "acquire": acq, "flags": np.zeros(n, np.uint8),
+          "rt": np.zeros(n, np.int64), "param": np.zeros(n, np.uint64)}
+    orc = lt.Oracle(n_res, flow, (), ())
+    exp = orc.replay(st)
+    eng, s = _sentinel(n_res, 1 << 17)
+    _load(s, flow)
+    got = _submit(s, st)
+    _assert_same(st, got, exp, "decisions")
+    _assert_nodes(s, orc, n_res, int(ts.max()))
+    passed = exp[0] == 0
+    assert passed.sum() > 1000 and (~passed).sum() > 1000
+    orc.close()
+    eng.close()
+
+
 @pytest.mark.parametrize("seed,regress", [(33, 0.0), (34, 0.002)])
 def test_mixed_acquire_heavy_resources(seed, regress):
     """DefaultController / WarmUpController resources with thousands of entries per batch and mixed
