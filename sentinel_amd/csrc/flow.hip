@@ -2024,7 +2024,8 @@ __global__ __launch_bounds__(256) void k_lwsum(FlowState st, FlowScratch sc, con
 #ifndef SGA_WAVE_PF
 #define SGA_WAVE_PF 8
 #endif
-constexpr uint32_t kWinMin = 512;  // k_lwave<1>: RateLimiter runs of this many events walk window summaries
+constexpr uint32_t kWinMin = 512;
+constexpr int kWinSteps = 4;  // k_lwave<1> window(): movers of latestPassedTime stepped one by one, beyond that a scan  // k_lwave<1>: RateLimiter runs of this many events walk window summaries
 constexpr int kWavePf = SGA_WAVE_PF;  // k_lwave: windows loaded ahead (even: RateLimiter runs take them in pairs)
 // kRl: 1 = the RateLimiter resources only, 0 = the others (two launches, each compiled without the other's
 // window code: one kernel holding both spilled registers and waited on its own stores)
@@ -2131,9 +2132,34 @@ __global__ __launch_bounds__(64) void k_lwave(FlowState st, int64_t max_rt, Flow
                     // max(latest + cost, now)), and every prediction is checked against the state
                     // before it.  Lanes up to the first wrong prediction are decided; that lane takes
                     // its true decision, and the rest of the window goes round again.
+                    // When few open entries would move latestPassedTime at the current state (a saturated
+                    // queue: costly entries block, zero-cost ones pass behind it), the step is exact
+                    // without a scan: every entry before the first mover is decided at the current
+                    // state, the mover passes and moves it.
                     while (rem) {
                         if (prof) ++pr_iter;
                         const bool open = (rem >> lane) & 1ull;
+                        {
+                            const bool act = aq <= 0 || (rcount > 0 && (cost + latest <= t || cost + latest - t <= rqueue));
+                            const uint64_t mvm = __ballot(open && act && aq > 0 && (cost > 0 || t > latest));
+                            if (__builtin_popcountll(mvm) <= kWinSteps) {
+                                const int f = mvm ? __builtin_ctzll(mvm) : 64;
+                                if (open && lane < f) {
+                                    d = act ? D_PASS : D_BLOCK_FLOW;
+                                    if (act && aq > 0) w = latest - t;  // a zero-cost pass behind the queue
+                                }
+                                const uint64_t before = f == 64 ? rem : rem & ((1ull << f) - 1);
+                                if (__ballot(cost > 0) & before) pred_c = false;  // costly entries before f blocked
+                                if (f == 64) break;
+                                const int64_t tf = readlane_i64(t, f), cf = readlane_i64(cost, f);
+                                const int64_t lf = max(latest + cf, tf);
+                                if (lane == f) w = lf - tf;  // d: D_PASS
+                                latest = lf;
+                                if (cf > 0) pred_c = true;
+                                rem &= (f == 63) ? 0ull : (~0ull << (f + 1));
+                                continue;
+                            }
+                        }
                         const bool mv = open && aq > 0 && rcount > 0;
                         const bool spec = aq <= 0 || (rcount > 0 && (cost == 0 || pred_c));
                         int64_t A = (mv && spec) ? cost : 0, B = (mv && spec) ? t : kMaxPlusNegInf;
