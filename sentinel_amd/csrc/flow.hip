@@ -1334,15 +1334,17 @@ __device__ __forceinline__ LAgg lagg_combine(const LAgg &a, const LAgg &b) {
     return r;
 }
 
-__device__ __forceinline__ LAgg lagg_value(uint32_t key, uint32_t pkey, const Payload &q, const Payload &pq,
+// staged run-scan element: key with the exit flag in bit 31 (kKeyExit), bucket, acq_prio
+constexpr uint32_t kKeyExit = 0x80000000u;
+__device__ __forceinline__ LAgg lagg_value(uint32_t kx, uint32_t pkx, uint32_t b, uint32_t pb, uint32_t acq_prio,
                                            bool has_prev, bool valid) {
     if (!valid) return lagg_id();
-    const bool fh = !has_prev || key != pkey;
-    const bool h = fh || q.bucket != pq.bucket;
-    const bool ex = (q.idx & F_EXIT) != 0;
-    const int32_t a = (int32_t)(q.acq_prio & 0x7FFFFFFFu);
+    const bool fh = !has_prev || ((kx ^ pkx) & ~kKeyExit) != 0;
+    const bool h = fh || b != pb;
+    const bool ex = (kx & kKeyExit) != 0;
+    const int32_t a = (int32_t)(acq_prio & 0x7FFFFFFFu);
     return LAgg{h ? 1u : 0u, fh ? 1u : 0u, h ? 1u : 0u, ex ? 0u : 1u, ex ? 1u : 0u,
-                ex ? 0u : (q.acq_prio >> 31), ex ? INT32_MAX : a, ex ? INT32_MIN : a, ex ? 0 : (int64_t)a};
+                ex ? 0u : (acq_prio >> 31), ex ? INT32_MAX : a, ex ? INT32_MIN : a, ex ? 0 : (int64_t)a};
 }
 
 // blocked arrangement per thread (kItems consecutive events), block scan of thread aggregates
@@ -1387,29 +1389,47 @@ __device__ __forceinline__ void stage_tile(T *lds, const T *__restrict__ g, uint
     }
 }
 
+// the run scans stage only what they read of an element (12 of its 20 bytes: key + exit flag, bucket,
+// acquire): 52 KB of LDS per tile instead of 87, so that more than one tile is resident per CU
+__device__ __forceinline__ void stage_runs(uint32_t *skey, uint32_t *sbk, uint32_t *sacq, const uint32_t *__restrict__ keys,
+                                           const Payload *__restrict__ pay, uint32_t base, uint32_t lim,
+                                           uint32_t invalid) {
+#pragma unroll 4
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kStage; i += kT) {
+        const uint32_t e = base + i - 1;  // base 0: e wraps for i = 0, and lim excludes it
+        uint32_t k = invalid, b = 0, a = 0;
+        if (base + i >= 1 && e < lim) {
+            const Payload q = pay[e];
+            k = keys[e] | ((q.idx & F_EXIT) ? kKeyExit : 0u);
+            b = q.bucket;
+            a = q.acq_prio;
+        }
+        skey[spad(i)] = k;
+        sbk[spad(i)] = b;
+        sacq[spad(i)] = a;
+    }
+}
+
 __global__ __launch_bounds__(kT) void k_lruns_up(const uint32_t *__restrict__ keys, const Payload *__restrict__ pay,
                                                  uint32_t n, uint32_t invalid, LAgg *tile_agg, uint32_t *tile_valid) {
-    __shared__ uint32_t skey[kStagePad];
-    __shared__ Payload spay[kStagePad];
+    __shared__ uint32_t skey[kStagePad], sbk[kStagePad], sacq[kStagePad];
     const uint32_t base = blockIdx.x * kTileElems;
-    stage_tile(skey, keys, base, n, invalid);
-    stage_tile(spay, pay, base, n, Payload{0, 0, 0, 0});
+    stage_runs(skey, sbk, sacq, keys, pay, base, n, invalid);
     __syncthreads();
     const uint32_t e0 = base + threadIdx.x * kItems;
     LAgg acc = lagg_id();
     uint32_t nv = 0;
     if (e0 < n) {
         uint32_t pk = e0 > 0 ? skey[sslot(base, e0 - 1)] : invalid;
-        Payload pq = e0 > 0 ? spay[sslot(base, e0 - 1)] : Payload{0, 0, 0, 0};
+        uint32_t pb = e0 > 0 ? sbk[sslot(base, e0 - 1)] : 0u;
         for (int i = 0; i < kItems && e0 + i < n; ++i) {
             const uint32_t e = e0 + i;
-            const uint32_t k = skey[sslot(base, e)];
-            const Payload q = spay[sslot(base, e)];
-            const bool valid = k != invalid;
-            acc = lagg_combine(acc, lagg_value(k, pk, q, pq, e > 0, valid));
+            const uint32_t k = skey[sslot(base, e)], b = sbk[sslot(base, e)];
+            const bool valid = (k & ~kKeyExit) != invalid;
+            acc = lagg_combine(acc, lagg_value(k, pk, b, pb, sacq[sslot(base, e)], e > 0, valid));
             nv += valid ? 1 : 0;
             pk = k;
-            pq = q;
+            pb = b;
         }
     }
     LAgg total;
@@ -1455,49 +1475,49 @@ __global__ __launch_bounds__(kT) void k_lruns_tiles(const LAgg *__restrict__ til
 __global__ __launch_bounds__(kT) void k_lruns_down(const uint32_t *__restrict__ keys, const Payload *__restrict__ pay,
                                                    const int64_t *__restrict__ rt_in, uint32_t invalid,
                                                    const LAgg *__restrict__ tile_carry, FlowScratch sc) {
-    __shared__ uint32_t skey[kStagePad];
-    __shared__ Payload spay[kStagePad];
-    __shared__ uint32_t srun[kTileElems], seidx[kTileElems];  // the per-event outputs, stored coalesced below
+    __shared__ uint32_t skey[kStagePad], sbk[kStagePad], sacq[kStagePad];
+    // the per-event outputs, stored coalesced below: run ids less the tile's first (they fit 16 bits), and
+    // entry indices over the element's own acquire slot (each thread reads only its own elements' sacq, and
+    // reads each before it writes it)
+    __shared__ uint16_t srun[kTileElems];
     const uint32_t nvalid = sc.counters[0];
     const uint32_t base = blockIdx.x * kTileElems;
     if (base >= nvalid) return;
-    stage_tile(skey, keys, base, nvalid, invalid);
-    stage_tile(spay, pay, base, nvalid, Payload{0, 0, 0, 0});
+    stage_runs(skey, sbk, sacq, keys, pay, base, nvalid, invalid);
     __syncthreads();
     const uint32_t e0 = base + threadIdx.x * kItems;
     LAgg acc = lagg_id();
     uint32_t pk0 = e0 > 0 && e0 - 1 < nvalid ? skey[sslot(base, e0 - 1)] : invalid;
-    Payload pq0 = e0 > 0 && e0 - 1 < nvalid ? spay[sslot(base, e0 - 1)] : Payload{0, 0, 0, 0};
+    uint32_t pb0 = e0 > 0 && e0 - 1 < nvalid ? sbk[sslot(base, e0 - 1)] : 0u;
     {
-        uint32_t pk = pk0;
-        Payload pq = pq0;
+        uint32_t pk = pk0, pb = pb0;
         for (int i = 0; i < kItems && e0 + i < nvalid; ++i) {
             const uint32_t e = e0 + i;
-            const uint32_t k = skey[sslot(base, e)];
-            const Payload q = spay[sslot(base, e)];
-            acc = lagg_combine(acc, lagg_value(k, pk, q, pq, e > 0, true));
+            const uint32_t k = skey[sslot(base, e)], b = sbk[sslot(base, e)];
+            acc = lagg_combine(acc, lagg_value(k, pk, b, pb, sacq[sslot(base, e)], e > 0, true));
             pk = k;
-            pq = q;
+            pb = b;
         }
     }
     const LAgg ex = lblock_excl<kT>(acc, nullptr);
-    LAgg run = lagg_combine(tile_carry[blockIdx.x], ex);
-    uint32_t pk = pk0;
-    Payload pq = pq0;
+    const LAgg carry = tile_carry[blockIdx.x];
+    const uint32_t rid0 = carry.nh - 1;  // the run before the tile's first element (wraps for tile 0)
+    LAgg run = lagg_combine(carry, ex);
+    uint32_t pk = pk0, pb = pb0;
     for (int i = 0; i < kItems && e0 + i < nvalid; ++i) {
         const uint32_t e = e0 + i;
-        const uint32_t k = skey[sslot(base, e)];
-        const Payload q = spay[sslot(base, e)];
-        const LAgg v = lagg_value(k, pk, q, pq, e > 0, true);
+        const uint32_t kx = skey[sslot(base, e)], b = sbk[sslot(base, e)];
+        const LAgg v = lagg_value(kx, pk, b, pb, sacq[sslot(base, e)], e > 0, true);
         run = lagg_combine(run, v);
         const uint32_t rid = run.nh - 1;
-        const bool ex_ev = (q.idx & F_EXIT) != 0;
-        srun[e - base] = rid;
-        seidx[e - base] = ex_ev ? 0xFFFFFFFFu : run.nent - 1;  // entry index within the run
+        const bool ex_ev = (kx & kKeyExit) != 0;
+        const uint32_t k = kx & ~kKeyExit;
+        srun[e - base] = (uint16_t)(rid - rid0);
+        sacq[sslot(base, e)] = ex_ev ? 0xFFFFFFFFu : run.nent - 1;  // entry index within the run
         if (v.flag) {
             sc.run_start[rid] = e;
             sc.run_slot[rid] = k;
-            sc.run_t0off[rid] = q.ts_off;
+            sc.run_t0off[rid] = pay[e].ts_off;
             sc.run_exc[rid] = 0;
             sc.run_exerr[rid] = 0;
             sc.run_exrt[rid] = 0;
@@ -1505,10 +1525,7 @@ __global__ __launch_bounds__(kT) void k_lruns_down(const uint32_t *__restrict__ 
         }
         if (v.nf) sc.flow_first_run[run.nf - 1] = rid;
         bool last = e + 1 >= nvalid;
-        if (!last) {
-            const uint32_t nk = skey[sslot(base, e + 1)];
-            last = nk != k || spay[sslot(base, e + 1)].bucket != q.bucket;
-        }
+        if (!last) last = (skey[sslot(base, e + 1)] & ~kKeyExit) != k || sbk[sslot(base, e + 1)] != b;
         if (last) {
             sc.run_end[rid] = e + 1;
             sc.run_nent[rid] = run.nent;
@@ -1518,15 +1535,15 @@ __global__ __launch_bounds__(kT) void k_lruns_down(const uint32_t *__restrict__ 
             sc.run_amax[rid] = run.mx;
             sc.run_asum[rid] = run.asum;
         }
-        pk = k;
-        pq = q;
+        pk = kx;
+        pb = b;
     }
     __syncthreads();
 #pragma unroll 4
     for (uint32_t i = threadIdx.x; i < (uint32_t)kTileElems; i += kT) {
         if (base + i >= nvalid) break;
-        sc.ev_run[base + i] = srun[i];
-        sc.ev_eidx[base + i] = seidx[i];
+        sc.ev_run[base + i] = rid0 + (uint32_t)srun[i];
+        sc.ev_eidx[base + i] = sacq[spad(i + 1)];
     }
 }
 
@@ -2024,8 +2041,14 @@ __global__ __launch_bounds__(256) void k_lwsum(FlowState st, FlowScratch sc, con
 #ifndef SGA_WAVE_PF
 #define SGA_WAVE_PF 8
 #endif
-constexpr uint32_t kWinMin = 512;
-constexpr int kWinSteps = 4;  // k_lwave<1> window(): movers of latestPassedTime stepped one by one, beyond that a scan  // k_lwave<1>: RateLimiter runs of this many events walk window summaries
+#ifndef SGA_WIN_MIN
+#define SGA_WIN_MIN 512
+#endif
+#ifndef SGA_WIN_STEPS
+#define SGA_WIN_STEPS 4
+#endif
+constexpr uint32_t kWinMin = SGA_WIN_MIN;
+constexpr int kWinSteps = SGA_WIN_STEPS;  // k_lwave<1> window(): movers of latestPassedTime stepped one by one, beyond that a scan  // k_lwave<1>: RateLimiter runs of this many events walk window summaries
 constexpr int kWavePf = SGA_WAVE_PF;  // k_lwave: windows loaded ahead (even: RateLimiter runs take them in pairs)
 // kRl: 1 = the RateLimiter resources only, 0 = the others (two launches, each compiled without the other's
 // window code: one kernel holding both spilled registers and waited on its own stores)
