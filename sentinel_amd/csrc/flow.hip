@@ -1549,17 +1549,33 @@ __global__ __launch_bounds__(kT) void k_lruns_down(const uint32_t *__restrict__ 
 
 // exit aggregates per run (SUCCESS count, exceptions, RT sum, min RT): atomics per run
 // pre-reduced inside each thread's consecutive events.
+// a tile's (idx | acq_prio << 32) per element, staged like stage_tile (8 of a payload's 16 bytes)
+__device__ __forceinline__ void stage_idx_acq(uint64_t *sia, const Payload *__restrict__ pay, uint32_t base,
+                                              uint32_t lim) {
+#pragma unroll 4
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kStage; i += kT) {
+        const uint32_t e = base + i - 1;
+        uint64_t v = 0;
+        if (base + i >= 1 && e < lim) {
+            const Payload q = pay[e];
+            v = (uint64_t)q.idx | ((uint64_t)q.acq_prio << 32);
+        }
+        sia[spad(i)] = v;
+    }
+}
+
 __global__ __launch_bounds__(kT) void k_lexits(const Payload *__restrict__ pay, const int64_t *__restrict__ rt_in,
                                                FlowScratch sc) {
+    // staged: run ids, and (idx | acq_prio << 32) per element, whose slot an exit then overwrites with its RT
+    // (each thread reads and writes only its own elements): 56 KB of LDS, two tiles per CU
     __shared__ uint32_t srun[kStagePad];
-    __shared__ Payload spay[kStagePad];
-    __shared__ int64_t srt[kTileElems];
-    __shared__ uint8_t sex[kTileElems];  // an exit's RT is in srt
+    __shared__ uint64_t sia[kStagePad];
+    __shared__ uint8_t sex[kTileElems];  // an exit's RT is in sia
     const uint32_t nvalid = sc.counters[0];
     const uint32_t base = blockIdx.x * kTileElems;
     if (base >= nvalid) return;  // the whole block
     stage_tile(srun, sc.ev_run, base, nvalid, 0xFFFFFFFFu);
-    stage_tile(spay, pay, base, nvalid, Payload{0, 0, 0, 0});
+    stage_idx_acq(sia, pay, base, nvalid);
     for (uint32_t i = threadIdx.x; i < (uint32_t)kTileElems; i += kT) sex[i] = 0;
     __syncthreads();
     const uint32_t e0 = (blockIdx.x * kT + threadIdx.x) * kItems;  // no early return: the wave reduction below
@@ -1575,8 +1591,9 @@ __global__ __launch_bounds__(kT) void k_lexits(const Payload *__restrict__ pay, 
     };
     for (int i = 0; i < kItems && e0 + i < nvalid; ++i) {
         const uint32_t e = e0 + i;
-        const Payload q = spay[sslot(base, e)];
-        if (!(q.idx & F_EXIT)) continue;
+        const uint64_t qv = sia[sslot(base, e)];
+        const uint32_t qidx = (uint32_t)qv, qacq = (uint32_t)(qv >> 32);
+        if (!(qidx & F_EXIT)) continue;
         const uint32_t r = srun[sslot(base, e)];
         if (r != cur) {
             flush();
@@ -1585,12 +1602,12 @@ __global__ __launch_bounds__(kT) void k_lexits(const Payload *__restrict__ pay, 
             rs = 0;
             mn = INT64_MAX;
         }
-        const uint64_t cnt = q.acq_prio & 0x7FFFFFFFu;
-        const int64_t rt = rt_in[q.idx & F_IDX];
-        srt[e - base] = rt;
+        const uint64_t cnt = qacq & 0x7FFFFFFFu;
+        const int64_t rt = rt_in[qidx & F_IDX];
+        sia[sslot(base, e)] = (uint64_t)rt;
         sex[e - base] = 1;
         c += cnt;
-        if (q.idx & F_ERROR) er += cnt;
+        if (qidx & F_ERROR) er += cnt;
         rs += rt;
         if (rt < mn) mn = rt;
     }
@@ -1607,7 +1624,7 @@ __global__ __launch_bounds__(kT) void k_lexits(const Payload *__restrict__ pay, 
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < (uint32_t)kTileElems; i += kT) {  // the exits' RTs, coalesced
         if (base + i >= nvalid) break;
-        if (sex[i]) sc.rt_sorted[base + i] = srt[i];
+        if (sex[i]) sc.rt_sorted[base + i] = (int64_t)sia[spad(i + 1)];
     }
 }
 
@@ -4579,13 +4596,13 @@ __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, 
 __global__ __launch_bounds__(kT) void k_pseg_runs(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
                                                   const int8_t *__restrict__ decision) {
     __shared__ uint32_t srun[kStagePad];
-    __shared__ Payload spay[kStagePad];
+    __shared__ uint64_t sia[kStagePad];  // idx | acq_prio << 32 (stage_idx_acq)
     if (!gate_is(st.gate, kGateSeq | kGateBad, 0) || sc.counters[11] == 0) return;
     const uint32_t nvalid = sc.counters[0];
     const uint32_t base = blockIdx.x * kTileElems;
     if (base >= nvalid) return;  // the whole block
     stage_tile(srun, sc.ev_run, base, nvalid, 0u);
-    stage_tile(spay, pay, base, nvalid, Payload{0, 0, 0, 0});
+    stage_idx_acq(sia, pay, base, nvalid);
     __syncthreads();
     const uint32_t e0 = (blockIdx.x * kT + threadIdx.x) * kItems;
     uint32_t cur = 0xFFFFFFFFu, np = 0;
@@ -4600,16 +4617,16 @@ __global__ __launch_bounds__(kT) void k_pseg_runs(FlowState st, FlowScratch sc, 
         const uint32_t e = e0 + i;
         const uint32_t r = srun[sslot(base, e)];
         if (sc.run_mode[r] != RUN_PSEG) continue;
-        const Payload q = spay[sslot(base, e)];
-        if (q.idx & F_EXIT) continue;
+        const uint64_t qv = sia[sslot(base, e)];
+        if ((uint32_t)qv & F_EXIT) continue;
         if (r != cur) {
             flush();
             cur = r;
             pa = ba = 0;
             np = 0;
         }
-        const int64_t a = (int64_t)(q.acq_prio & 0x7FFFFFFFu);
-        const int8_t d = decision[q.idx & F_IDX];
+        const int64_t a = (int64_t)((uint32_t)(qv >> 32) & 0x7FFFFFFFu);
+        const int8_t d = decision[(uint32_t)qv & F_IDX];
         if (d == D_PASS || d == D_PASS_WAIT) {
             pa += a;
             ++np;
