@@ -6114,7 +6114,7 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         hipLaunchKernelGGL(k_lwsum, dim3((unsigned)((m / 64 + 3) / 4 + 1)), dim3(256), 0, stream, st, sc, pay);
         for (int rl = 0; rl < 2; ++rl)
             hipLaunchKernelGGL(rl ? k_lwave<1> : k_lwave<0>,
-                               dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kWaveEvents)))),
+                               dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (uint32_t)(m / 4096)))),
                                dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
                                d_dec.p, d_wait.p, lwave_prof());
         print_lwave_prof(stream);
@@ -6241,7 +6241,7 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
     }
     hipLaunchKernelGGL(k_lwsum, dim3((m / 64 + 3) / 4 + 1), dim3(256), 0, s, st, gsc, pay);
     for (int rl = 0; rl < 2; ++rl)
-        hipLaunchKernelGGL(rl ? k_lwave<1> : k_lwave<0>, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kWaveEvents))),
+        hipLaunchKernelGGL(rl ? k_lwave<1> : k_lwave<0>, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, m / 4096))),
                            dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision,
                            wait_p, lwave_prof());
     print_lwave_prof(s);
