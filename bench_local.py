@@ -80,15 +80,17 @@ class Batch:
         self.t_hi = int(max(self.ts.max(), self.exit_ts.max() if self.exit_of is not None else self.ts.max()))
 
 
-def _cfg_c1(rng):
+def _cfg_c1(rng, erng=None):
+    erng = erng or rng
     n = 1_000_000
     ts = T0 + np.arange(n) // 20  # lambda = 20 events / ms, 50 virtual s
-    b = Batch(np.zeros(n), ts, exit_rt=rng.integers(0, 6, size=n))
+    b = Batch(np.zeros(n), ts, exit_rt=erng.integers(0, 6, size=n))
     return dict(name="C1 HelloWorld: 1 FlowRule QPS 20 DefaultController, 1M entries + exits",
                 n_res=1, flow=[dict(resource=0, count=20.0)], batch=b, sample=n, contended=True)
 
 
-def _cfg_c2(rng, n=1 << 24):
+def _cfg_c2(rng, erng=None, n=1 << 24):
+    erng = erng or rng  # rng: the rules (the same on every rank), erng: this rank's events
     n_res = 100_000
     flow = []
     beh = rng.random(n_res)
@@ -103,20 +105,20 @@ def _cfg_c2(rng, n=1 << 24):
             flow.append(dict(resource=r, count=float(cnt[r]), control_behavior=2, max_queueing_time_ms=500))
         else:
             flow.append(dict(resource=r, count=float(cnt[r]), control_behavior=1, warm_up_period_sec=10))
-    res = _zipf(rng, n_res, n, mask=None if SHARD[1] == 1 else own)
+    res = _zipf(erng, n_res, n, mask=None if SHARD[1] == 1 else own)
     ts = T0 + np.arange(n) // 10_000  # lambda = 1e7 / virtual s (per GPU)
-    acq = np.where(rng.random(n) < 0.05, rng.integers(2, 6, size=n), 1)
-    b = Batch(res, ts, acq=acq, exit_rt=rng.geometric(1.0 / 5.0, size=n))
+    acq = np.where(erng.random(n) < 0.05, erng.integers(2, 6, size=n), 1)
+    b = Batch(res, ts, acq=acq, exit_rt=erng.geometric(1.0 / 5.0, size=n))
     return dict(name="C2 100k FlowRules 40% Default / 30% RateLimiter(500 ms) / 30% WarmUp(10 s), Zipf(1.1), "
                      "2^24 entries + exits per batch",
                 n_res=n_res, flow=flow, batch=b, sample=1 << 21)
 
 
-def _cfg_c4(rng):
-    return _cfg_c4_common(rng, fold=True)
+def _cfg_c4(rng, erng=None):
+    return _cfg_c4_common(rng, erng or rng, fold=True)
 
 
-def _cfg_c4_common(rng, fold):
+def _cfg_c4_common(rng, erng, fold):
     n_res, n = 10_000, 1 << 22
     param = []
     own = own_resources(n_res)
@@ -126,26 +128,27 @@ def _cfg_c4_common(rng, fold):
             p.update(control_behavior=2, max_queueing_time_ms=0)
         if own[r]:
             param.append(p)
-    res = _zipf(rng, n_res, n, mask=None if SHARD[1] == 1 else own)
-    vals = _zipf(rng, 10_000_000, n)
+    res = _zipf(erng, n_res, n, mask=None if SHARD[1] == 1 else own)
+    vals = _zipf(erng, 10_000_000, n)
     if fold:
         vals = vals % 4000  # pinned mode: <= 4000 keys per rule (no CacheMap eviction)
     ts = T0 + np.arange(n) // 10_000
-    b = Batch(res, ts, flags=np.full(n, EV_HAS_PARAM), param=vals, exit_rt=rng.integers(1, 30, size=n))
+    b = Batch(res, ts, flags=np.full(n, EV_HAS_PARAM), param=vals, exit_rt=erng.integers(1, 30, size=n))
     return dict(name="C4 10k ParamFlowRules (90% default / 10% throttle), Zipf(1.1) values over 10^7 folded to "
                      "<= 4000 per rule (pinned mode), 2^22 entries + exits per batch",
                 n_res=n_res, param=param, batch=b, sample=1 << 20)
 
 
-def _cfg_c4full(rng):
-    cfg = _cfg_c4_common(rng, fold=False)
+def _cfg_c4full(rng, erng=None):
+    cfg = _cfg_c4_common(rng, erng or rng, fold=False)
     cfg["name"] = ("C4 full mode: 10k ParamFlowRules (90% default / 10% throttle), Zipf(1.1) values over 10^7 "
                    "unfolded (the CacheMaps hold their min(4000 * duration, 200000) most recently used values and "
                    "evict: strict LRU), 2^22 entries + exits per batch")
     return cfg
 
 
-def _cfg_c5b(rng):
+def _cfg_c5b(rng, erng=None):
+    erng = erng or rng
     n_res, n = 10_000, 1 << 22
     degrade = []
     own = own_resources(n_res)
@@ -158,10 +161,10 @@ def _cfg_c5b(rng):
         else:
             degrade.append(dict(resource=r, grade=1, count=0.2, min_request_amount=5, stat_interval_ms=1000,
                                 time_window=5))
-    res = _zipf(rng, n_res, n, mask=None if SHARD[1] == 1 else own)
+    res = _zipf(erng, n_res, n, mask=None if SHARD[1] == 1 else own)
     ts = T0 + np.arange(n) // 10_000
-    rt = np.clip(np.round(rng.lognormal(mean=np.log(20.0), sigma=1.0, size=n)), 1, 10_000)
-    b = Batch(res, ts, exit_rt=rt, exit_err=rng.random(n) < 0.03)
+    rt = np.clip(np.round(erng.lognormal(mean=np.log(20.0), sigma=1.0, size=n)), 1, 10_000)
+    b = Batch(res, ts, exit_rt=rt, exit_err=erng.random(n) < 0.03)
     return dict(name="C5b DegradeSlot: 10k DegradeRules (50% slow-RT 50 ms / 50% exception ratio 0.2), lognormal "
                      "RT (median 20 ms), 3% errors, 2^22 entries + exits per batch",
                 n_res=n_res, degrade=degrade, batch=b, sample=1 << 20)
@@ -349,8 +352,12 @@ def run_local(args, cfg_name):
             local = 0  # rehearsal of the N-rank path on a one-GPU box
     SHARD = (rank, world)
     seed = {"c1": 101, "c2": 102, "c4": 104, "c4full": 104, "c5b": 105}[cfg_name]
-    rng = np.random.default_rng(seed if world == 1 else [seed, rank, world])
-    cfg = {"c1": _cfg_c1, "c2": _cfg_c2, "c4": _cfg_c4, "c4full": _cfg_c4full, "c5b": _cfg_c5b}[cfg_name](rng)
+    # the rules (count, controller, grade of each resource) come from the base seed on every rank, so a shard's
+    # rules are the single-GPU workload's restricted to the shard; only the event stream is drawn per rank (one
+    # rank: one generator for both, the same draws as before)
+    rng = np.random.default_rng(seed)
+    erng = rng if world == 1 else np.random.default_rng([seed, rank, world])
+    cfg = {"c1": _cfg_c1, "c2": _cfg_c2, "c4": _cfg_c4, "c4full": _cfg_c4full, "c5b": _cfg_c5b}[cfg_name](rng, erng)
     b = cfg["batch"]
     if os.environ.get("SGA_BENCH_DRY") == "1":  # launch and routing check only (tests, CPU)
         own = own_resources(cfg["n_res"])

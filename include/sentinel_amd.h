@@ -192,7 +192,8 @@ int sga_request_tokens_device(sga_engine *e, const int64_t *d_flow_id, const int
  * flowId, count, priority -- CS/server/codec/data/FlowRequestDataDecoder.java:35-48) into a device
  * batch writes, for engines whose flowIds fit 32 bits.  flow_id = 0 and acquire = 0 answer
  * BAD_REQUEST as flowId <= 0 / acquireCount <= 0 do (DefaultTokenService.notValidRequest, :87-89);
- * flags bit 0 = prioritized, the other bits must be 0. */
+ * flags bit 0 = prioritized, the other bits are reserved: a request with any of them set answers
+ * BAD_REQUEST. */
 typedef struct sga_token_request {
     uint32_t flow_id;
     uint32_t ts_off;   /* time = ts_base + ts_off (ms) */

@@ -417,6 +417,7 @@ struct orc_cb {
     int64_t next_retry;
     int64_t recovery_ms;      /* timeWindow * 1000, AbstractCircuitBreaker.java:54 */
     int64_t max_allowed_rt;   /* Math.round(count), ResponseTimeCircuitBreaker.java:52 */
+    int64_t probe_t;          /* time of the entry that moved it OPEN -> HALF_OPEN (its whenTerminate hook) */
     orc_leap *stat;           /* LeapArray(1, statIntervalMs) of {err|slow, total} */
 };
 
@@ -443,6 +444,7 @@ static int cb_try_pass(orc_cb *c, int64_t now, int *to_half_open) {
     if (c->state == CB_OPEN) {
         if (now >= c->next_retry) {
             c->state = CB_HALF_OPEN;
+            c->probe_t = now;
             *to_half_open = 1;
             return 1;
         }
@@ -1037,6 +1039,10 @@ void orc_flow_replay_p(orc_flow *f, size_t n, const uint8_t *kind, const uint32_
                 orc_node_add_pass_request(fr->node, ts[i], -acquire[i]);
                 orc_node_increase_block_qps(fr->node, ts[i], acquire[i]);
                 param_thread_dec(f, fr, hp, pv);
+                /* the probe's whenTerminate hook (AbstractCircuitBreaker.java:117-139): blockError set, so a
+                 * breaker this entry moved to HALF_OPEN falls back to OPEN; the revoke carries the entry's time */
+                for (int k = 0; k < fr->ncb; k++)
+                    if (fr->cb[k]->state == CB_HALF_OPEN && fr->cb[k]->probe_t == ts[i]) fr->cb[k]->state = CB_OPEN;
                 if (in) {
                     orc_node_decrease_thread_num(f->entry);
                     orc_node_add_pass_request(f->entry, ts[i], -acquire[i]);

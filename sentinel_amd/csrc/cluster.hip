@@ -485,9 +485,16 @@ __global__ __launch_bounds__(kRunThreads) void k_runs_down(const uint64_t *__res
 }
 
 // ---------------------------------------------------------------- flows: resolve runs per rule
+// x / intervalInSec, exact: the default 1 s window has intervalInSec = 1.0 and x / 1.0 == x, so a wave whose lanes
+// all divide by 1.0 skips the double division (a uniform branch on a ballot; ~10 VALU per division otherwise)
+__device__ __forceinline__ double div_isec(double x, double isec) {
+    if (__all(isec == 1.0)) return x;
+    return x / isec;
+}
+
 __device__ __forceinline__ bool pass_cond(double thr, double isec, int64_t sum, int32_t a) {
     // nextRemaining = globalThreshold - latestQps - acquireCount >= 0   ClusterFlowChecker.java:67-71
-    return thr - (double)sum / isec - (double)a >= 0;
+    return thr - div_isec((double)sum, isec) - (double)a >= 0;
 }
 
 // First k in [0, n] with !pass_cond(s0 + k*a): a closed-form guess corrected against the
@@ -495,7 +502,8 @@ __device__ __forceinline__ bool pass_cond(double thr, double isec, int64_t sum, 
 __device__ __forceinline__ uint32_t pass_prefix(double thr, double isec, int64_t s0, int32_t a, uint32_t n) {
     if (n == 0) return 0;
     if (a <= 0) return pass_cond(thr, isec, s0, a) ? n : 0u;
-    const double g = floor(((thr - (double)a) * isec - (double)s0) / (double)a) + 1.0;
+    // the guess only seeds the exact search below: an approximate reciprocal of a does
+    const double g = floor(((thr - (double)a) * isec - (double)s0) * __builtin_amdgcn_rcp((double)a)) + 1.0;
     uint32_t k = 0;
     if (g >= (double)n) k = n;
     else if (g > 0) k = (uint32_t)g;
@@ -698,7 +706,7 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
             }
         }
         if (!occ_loaded) o = occ_ld;
-        const double latest = (double)(s0 + (int64_t)f * a) / P.isec;
+        const double latest = div_isec((double)(s0 + (int64_t)f * a), P.isec);
         const double lim = st.max_occupy_ratio * thr;
         const int64_t occ0 = o.occ_pass;
         uint32_t l2 = 0, h2 = np_after;
@@ -706,7 +714,7 @@ __device__ __forceinline__ bool run_fast(const ClusterState &st, const SlotParam
         while (l2 < h2) {
             const uint32_t cc = l2 + ((h2 - l2) >> 1);
             const int64_t add = (int64_t)cc * a;
-            const bool ok = ((double)(w0 + add) / P.isec <= lim) &&
+            const bool ok = (div_isec((double)(w0 + add), P.isec) <= lim) &&
                             (latest + (double)((int64_t)a + occ0 + add) - (double)head <= thr);
             if (ok) l2 = cc + 1;
             else h2 = cc;
@@ -1436,7 +1444,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
                     uint64_t res;
                     if (loc < ro.f) {
                         const int64_t sum = ro.s0 + (int64_t)loc * ri.a;
-                        res = pack_result(TRS_OK, j_d2i(ro.thr - (double)sum / ro.isec - (double)ri.a), 0);
+                        res = pack_result(TRS_OK, j_d2i(ro.thr - div_isec((double)sum, ro.isec) - (double)ri.a), 0);
                     } else if (pr && kp - ro.cpf < ro.cw) {
                         res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)ro.wait);
                     } else {
@@ -1496,7 +1504,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
                     uint64_t res;
                     if (loc < ro.f) {
                         const int64_t sum = ro.s0 + (int64_t)loc * a;
-                        res = pack_result(TRS_OK, j_d2i(ro.thr - (double)sum / ro.isec - (double)a), 0);
+                        res = pack_result(TRS_OK, j_d2i(ro.thr - div_isec((double)sum, ro.isec) - (double)a), 0);
                     } else {
                         res = pack_result(TRS_BLOCKED, 0, 0);
                     }
@@ -1523,7 +1531,7 @@ __global__ __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(3)))
                 uint64_t res;
                 if (loc < ro.f) {
                     const int64_t sum = ro.s0 + (int64_t)loc * a;
-                    res = pack_result(TRS_OK, j_d2i(ro.thr - (double)sum / ro.isec - (double)a), 0);
+                    res = pack_result(TRS_OK, j_d2i(ro.thr - div_isec((double)sum, ro.isec) - (double)a), 0);
                 } else if (pr && kp - ro.cpf < ro.cw) {
                     res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)ro.wait);
                 } else {
@@ -1825,6 +1833,7 @@ struct KeyShared {
     WConst wcs[256];
     uint16_t cnt[kKeyWaves][kHot];  // per wave: hot requests so far per hot id
     uint32_t s_np[kKeyWaves], s_bd[kKeyWaves], s_tm[kKeyWaves];
+    uint32_t s_bmin, s_bmax;  // hot buckets whose first request lies inside the segment (not at its start)
     union {
         uint32_t hist0[2][256];      // per sort tile of the segment: the first radix digit's counts
         uint32_t phist[kPartBins];   // partition mode: the segment's cold elements per slot bin
@@ -1862,6 +1871,10 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
     if (nhot) {
         uint4 *cz = reinterpret_cast<uint4 *>(&cnt[0][0]);
         for (int k = threadIdx.x; k < (int)(sizeof(cnt) / 16); k += kKeyThreads) cz[k] = make_uint4(0, 0, 0, 0);
+    }
+    if (threadIdx.x == 0) {
+        sh.s_bmin = 0xFFFFFFFFu;
+        sh.s_bmax = 0u;
     }
     __syncthreads();
     const uint32_t seg = blockIdx.x;
@@ -1917,7 +1930,7 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                     B.f[u] = (int64_t)w0;
                     B.t[u] = w1;
                     B.a[u] = (int32_t)(w2 & 0xFFFFu);
-                    B.p[u] = (w2 >> 16) & 1u;
+                    B.p[u] = w2 >> 16;  // the flags: bit 0 prioritized, other bits reserved (BAD_REQUEST)
                 } else if (kNT) {  // streamed once: non-temporal, so the dense table keeps more of L2
                     B.f[u] = __builtin_nontemporal_load(&flow_id[i]);
                     B.a[u] = __builtin_nontemporal_load(&acquire[i]);
@@ -1938,7 +1951,9 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                 // (the 64-bit flowId and the acquire count are dead after this in the dense case)
                 const int64_t f = B.f[u];
                 const int32_t a = B.a[u];
-                B.m[u] = ((use_prio && B.p[u]) ? 1u : 0u) | ((f <= 0 || a <= 0) ? 2u : 0u) |
+                const bool pr = kPk ? (B.p[u] & 1u) != 0 : (use_prio && B.p[u]);
+                const bool resv = kPk && (B.p[u] >> 1) != 0;  // reserved flag bits set: not a valid request
+                B.m[u] = (pr ? 1u : 0u) | ((f <= 0 || a <= 0 || resv) ? 2u : 0u) |
                          ((uint64_t)(f - 1) < (uint64_t)st.dense_n ? 4u : 0u) | (a == 1 ? 8u : 0u) |
                          ((a >= 1 && a <= (int32_t)kAcqMax ? (uint32_t)a : 0u) << 8);
                 if (kDense) {  // the hot path's key table: slot | wcode << 24, or kDkHot | hot id
@@ -1980,8 +1995,19 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                             W = Wc;
                             r0 = r0c;
                             inv = invc;
-                            if (kPass == 1) slot = sc.hot_slot[hid];  // decided as cold in this pass
-                            else if (hid >= nhot) wflags |= kFlagHotKey;
+                            if (kPass == 1) {
+                                // decided as cold in this pass: the slot and window length from the authoritative
+                                // table (a key-table entry naming a hot id outside the hot set -- kFlagHotKey --
+                                // would find a stale hot_slot)
+                                const uint32_t dd = st.dense[(uint32_t)(B.f[u] - 1)];
+                                slot = dd & 0xFFFFFFu;
+                                const WConst wc = wcs[dd >> 24];
+                                W = wc.W;
+                                r0 = wc.r0;
+                                inv = wc.inv;
+                            } else if (hid >= nhot) {
+                                wflags |= kFlagHotKey;
+                            }
                         } else {
                             slot = d & 0xFFFFFFu;
                             const WConst wc = wcs[d >> 24];
@@ -2041,8 +2067,13 @@ __device__ __forceinline__ void hot_key(KeyShared &sh, const ClusterState &st, c
                     if (valid) bdmax = max(bdmax, bdh);
                     if (i == 0) sc.counters[CTL_BDLO] = bdh;
                     const uint32_t pbk = wave_shr1(bdh, pbd);
-                    if (valid && hp && bdh > pbk)  // the first request of buckets pbk + 1 .. bdh
+                    if (valid && hp && bdh > pbk) {  // the first request of buckets pbk + 1 .. bdh
                         for (uint32_t qq = pbk + 1; qq <= bdh; ++qq) sc.hbnd[qq] = i;
+                        if (i & (uint32_t)(kHotSeg - 1)) {  // inside the segment: its pre rows (below)
+                            atomicMin(&sh.s_bmin, pbk + 1);
+                            atomicMax(&sh.s_bmax, bdh);
+                        }
+                    }
                     pbd = lane_u32(bdh, 63);
                     if (valid) hc[ch * kH1Chunk + u] = (kind == 2 ? (kKeyHot | hid | (p << 12)) : 0u) | (bdh << 13);
                 }
@@ -2149,6 +2180,26 @@ bdmax = wave_max_u32(bdmax);
                 }
                 npc += (uint32_t)__popcll(em);
             }
+        }
+        // Per hot bucket whose first request P lies inside this segment (not at its start): the segment's hot
+        // requests of each hot id before P (k_hot_flows adds them to the segment's base rank).  On the hot path
+        // the times are sorted, so "before P" is "of an earlier bucket".  Rare (a few segments per batch).
+        __syncthreads();  // the fix-up's reads of the wave prefixes are done: cnt is free
+        const uint32_t b0 = sh.s_bmin, b1 = sh.s_bmax;
+        uint32_t *pc = reinterpret_cast<uint32_t *>(&cnt[0][0]);
+        for (uint32_t b = b0; b <= b1; ++b) {  // uniform; empty unless a boundary is inside
+            for (uint32_t k = threadIdx.x; k < nhot; k += kKeyThreads) pc[k] = 0;
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < kSubRounds; ++r) {
+                const uint32_t cd = hc[r];
+                if (ubase + (uint32_t)r * 64 + lane < send && cd != kNoCode && ((cd >> 25) & 63u) < b)
+                    atomicAdd(&pc[cd & 0xFFFu], 1u);
+            }
+            __syncthreads();
+            for (uint32_t k = threadIdx.x; k < nhot; k += kKeyThreads) sc.hpre[(size_t)b * kHot + k] = (uint16_t)pc[k];
+            if (threadIdx.x == 0) atomicAdd(&sc.counters[CTL_NPRE], 1u);
+            __syncthreads();
         }
     }
     {  // the segment's latest request time (offset from ts_base): k_hot_mode keeps the maximum over batches
@@ -2391,9 +2442,13 @@ __global__ __launch_bounds__(kThreads) void k_hscan_group(BatchScratch sc, uint3
     sc.hgsum[(size_t)blockIdx.x * kHot + h] = s;
 }
 
-__global__ __launch_bounds__(kThreads) void k_hscan_mid(BatchScratch sc, uint32_t ngroups) {
+__device__ __forceinline__ void psort_cols_one(const BatchScratch &sc, uint32_t h, uint32_t ngroups);
+// pgroups > 0: also the prioritized sort's column prefix (k_psort_cols) for hot id h, so the hot side's chain has
+// one launch fewer
+__global__ __launch_bounds__(kThreads) void k_hscan_mid(BatchScratch sc, uint32_t ngroups, uint32_t pgroups) {
     if (!sc.counters[CTL_MODE]) return;
     const uint32_t h = blockIdx.x * kThreads + threadIdx.x;
+    if (pgroups) psort_cols_one(sc, h, pgroups);
     if (h >= hot_count(sc)) return;
     uint32_t acc = 0;
 #pragma unroll 8
@@ -2421,30 +2476,6 @@ __global__ __launch_bounds__(kThreads) void k_hscan_down(BatchScratch sc, uint32
     }
 }
 
-// Per hot bucket starting inside a rank segment: the segment's hot requests before its first
-// request, per hot id (the bucket's first rank is the segment's base plus these).
-__global__ __launch_bounds__(kThreads) void k_hot_pre(BatchScratch sc) {
-    __shared__ uint32_t cnt[kHot];
-    if (!sc.counters[CTL_MODE]) return;
-    const uint32_t b = blockIdx.x;
-    const uint32_t bd_lo = sc.counters[CTL_BDLO];
-    const uint32_t bd_hi = min(sc.counters[CTL_BDHI], (uint32_t)kHotBuckets - 1);
-    if (b <= bd_lo || b > bd_hi) return;
-    const uint32_t P = sc.hbnd[b];
-    const uint32_t s0 = P & ~(uint32_t)(kHotSeg - 1);
-    if (P == s0) return;
-    if (threadIdx.x == 0) atomicAdd(&sc.counters[CTL_NPRE], 1u);
-    for (uint32_t h = threadIdx.x; h < (uint32_t)kHot; h += kThreads) cnt[h] = 0;
-    __syncthreads();
-    for (uint32_t i = s0 + threadIdx.x; i < P; i += kThreads) {
-        const uint32_t cd = sc.hcode[i];
-        if (cd != kNoCode) atomicAdd(&cnt[cd & 0xFFFu], 1u);
-    }
-    __syncthreads();
-    const uint32_t nhot = hot_count(sc);
-    for (uint32_t h = threadIdx.x; h < nhot; h += kThreads) sc.hpre[(size_t)b * kHot + h] = (uint16_t)cnt[h];
-}
-
 // ---- the prioritized hot requests sorted by hot id, arrival order kept: a counting sort over kHot keys (the
 // elements are about 1 % of the hot requests).  kPsGroups groups of consecutive rank segments, one wave each.
 //   counts  the key kernel adds each element to prow[group][hot id] as it writes it (no-return atomics);
@@ -2457,7 +2488,9 @@ __device__ __forceinline__ uint32_t ps_per_group(uint32_t nseg) { return (nseg +
 
 __global__ __launch_bounds__(256) void k_psort_cols(BatchScratch sc, uint32_t ngroups) {
     if (!sc.counters[CTL_MODE]) return;
-    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+    psort_cols_one(sc, blockIdx.x * 256 + threadIdx.x, ngroups);
+}
+__device__ __forceinline__ void psort_cols_one(const BatchScratch &sc, uint32_t h, uint32_t ngroups) {
     uint32_t acc = 0;
     constexpr int kChunk = 64;  // loads in flight per lane
     for (uint32_t g0 = 0; g0 < ngroups; g0 += kChunk) {
@@ -2752,14 +2785,14 @@ __global__ __launch_bounds__(kThreads) void k_hot_flows(ClusterState st, BatchSc
             const int64_t wt = (lane < P.S && valid_b) ? R.cnt(CEV_WAITING, lane) : 0;
             const int64_t w0 = lane_i64(cl, CEV_WAITING) + wave_sum_i64(wt);
             if (!(rot && old != kAbsent)) o = o_ld;  // not taken by the rotation above
-            const double latest = (double)(s0 + (int64_t)f) / P.isec;
+            const double latest = div_isec((double)(s0 + (int64_t)f), P.isec);
             const double lim = st.max_occupy_ratio * thr;
             const int64_t occ0 = o.occ_pass;
             uint32_t l2 = 0, h2 = np_after;
             while (l2 < h2) {
                 const uint32_t cc = l2 + ((h2 - l2) >> 1);
                 const int64_t add = (int64_t)cc;
-                const bool fits = ((double)(w0 + add) / P.isec <= lim) &&
+                const bool fits = (div_isec((double)(w0 + add), P.isec) <= lim) &&
                                   (latest + (double)(1 + occ0 + add) - (double)head <= thr);
                 if (fits) l2 = cc + 1;
                 else h2 = cc;
@@ -2832,7 +2865,7 @@ __device__ __forceinline__ void prio_results_range(const ClusterState &st, const
         uint64_t res;
         if (local < hr.f) {
             const int64_t sum = hr.s0 + (int64_t)local;
-            res = pack_result(TRS_OK, j_d2i(hr.thr - (double)sum / hr.isec - 1.0), 0);
+            res = pack_result(TRS_OK, j_d2i(hr.thr - div_isec((double)sum, hr.isec) - 1.0), 0);
         } else if (j - hr.p0 - hr.cpf < hr.cw) {
             res = pack_result(TRS_SHOULD_WAIT, 0, (int32_t)hr.wait);
         } else {
@@ -2947,7 +2980,7 @@ __global__ __launch_bounds__(kFinWgThreads) void k_hot_final(ClusterState st, Ba
         uint64_t res;
         if (local < f) {
             const int64_t sum = s0 + (int64_t)local;
-            res = pack_result(TRS_OK, j_d2i(thr - (double)sum / isec - 1.0), 0);
+            res = pack_result(TRS_OK, j_d2i(thr - div_isec((double)sum, isec) - 1.0), 0);
         } else {
             res = pack_result(TRS_BLOCKED, 0, 0);
         }
@@ -3000,7 +3033,7 @@ __global__ __launch_bounds__(kFinGThreads) void k_hot_final_g(ClusterState st, B
         uint64_t res;
         if (local < rb[u].z) {
             const int64_t sum = s0 + (int64_t)local;
-            res = pack_result(TRS_OK, j_d2i(thr - (double)sum / isec - 1.0), 0);
+            res = pack_result(TRS_OK, j_d2i(thr - div_isec((double)sum, isec) - 1.0), 0);
         } else {
             res = pack_result(TRS_BLOCKED, 0, 0);
         }
@@ -3077,7 +3110,7 @@ __global__ __launch_bounds__(kFinGThreads) void k_hot_final_h(ClusterState st, B
             const double thr = __longlong_as_double((long long)(((uint64_t)tiv[u].y << 32) | tiv[u].x));
             const double isec = __longlong_as_double((long long)(((uint64_t)tiv[u].w << 32) | tiv[u].z));
             const int64_t sum = s0 + (int64_t)local[u];
-            res = pack_result(TRS_OK, j_d2i(thr - (double)sum / isec - 1.0), 0);
+            res = pack_result(TRS_OK, j_d2i(thr - div_isec((double)sum, isec) - 1.0), 0);
         } else {
             res = pack_result(TRS_BLOCKED, 0, 0);
         }
@@ -3982,7 +4015,7 @@ __global__ __launch_bounds__(kThreads) void k_plru_decide(CParamState st) {
     const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
     if (s >= st.nslots) return;
     const PRuleParam &P = st.param[s];
-    if (P.S <= 0 || st.pq[P.boff] != kPNoQueue || st.nkeys[s] <= P.cap) return;
+    if (P.S <= 0 || !P.active || st.pq[P.boff] != kPNoQueue || st.nkeys[s] <= P.cap) return;
     st.sw_list[atomicAdd(&st.ctl[4], 1u)] = s;
 }
 
@@ -4004,6 +4037,7 @@ __global__ __launch_bounds__(kThreads) void k_plru_collect(CParamState st) {
     for (uint32_t k = blockIdx.x * kThreads + threadIdx.x; k <= st.kmask; k += gridDim.x * kThreads) {
         if (st.ktab[k] == 0) continue;
         const PRuleParam &P = st.param[st.kslot[k]];
+        if (!P.active) continue;  // a dropped rule's keys stay in ktab; they never join a queue
         const uint64_t q0 = st.pq[P.boff];
         if (q0 == kPNoQueue || st.lpool[q0].kidx != kPLruBuilding) continue;
         const int64_t *rec = st.krec + st.koff[k];
@@ -4460,10 +4494,12 @@ static void hot_side(const ClusterState &st, BatchScratch &sc, int64_t ts_base, 
 
 // the prioritized hot requests sorted by hot id into pel[0] (k_psort_*; plo / phi per hot id)
 static uint32_t ps_per_group_h(uint32_t nseg) { return std::max<uint32_t>(1, (nseg + kPsGroups - 1) / kPsGroups); }
-static void prio_sort(BatchScratch &sc, uint32_t nseg, hipStream_t s) {
-    const uint32_t ngroups = (nseg + ps_per_group_h(nseg) - 1) / ps_per_group_h(nseg);
+static uint32_t ps_groups_h(uint32_t nseg) { return (nseg + ps_per_group_h(nseg) - 1) / ps_per_group_h(nseg); }
+// cols_done: k_hscan_mid already made the column prefix (the one-stream hot side)
+static void prio_sort(BatchScratch &sc, uint32_t nseg, hipStream_t s, bool cols_done = false) {
+    const uint32_t ngroups = ps_groups_h(nseg);
     if (fz_debug() & 512) hipLaunchKernelGGL(k_psort_dbgcount, dim3(kPsGroups), dim3(64), 0, s, sc, nseg);
-    hipLaunchKernelGGL(k_psort_cols, dim3(kHot / 256), dim3(256), 0, s, sc, ngroups);
+    if (!cols_done) hipLaunchKernelGGL(k_psort_cols, dim3(kHot / 256), dim3(256), 0, s, sc, ngroups);
     hipLaunchKernelGGL(k_psort_scatter, dim3(kPsGroups), dim3(64), 0, s, sc, nseg, sc.pel[0], fz_debug());
     if (fz_debug() & 512) hipLaunchKernelGGL(k_psort_verify, dim3(4), dim3(256), 0, s, sc, sc.pel[0]);
     sc.pel_sorted = sc.pel[0];
@@ -4523,9 +4559,8 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const ReqIn &
         SGA_HIP_CHECK(hipEventRecord(sc.ev_fork, sc.side));  // the cold elements ready (decide_hot waits)
         prio_sort(sc, nseg, s);
         hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
-        hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, s, sc, ngroups);
+        hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, s, sc, ngroups, 0u);
         hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, s, sc, nseg);
-        hipLaunchKernelGGL(k_hot_pre, dim3(kHotBuckets), dim3(kThreads), 0, s, sc);
         const uint32_t pgrid = std::max<uint32_t>(1, std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024));
         hipLaunchKernelGGL(k_prio_rank, dim3(pgrid), dim3(kThreads), 0, s, st, sc, sc.pel_sorted);
         hipLaunchKernelGGL(k_hot_flows, dim3(kHot / kH1Waves), dim3(kThreads), 0, s, st, sc, ts_base);
@@ -4540,7 +4575,24 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const ReqIn &
     // (SGA_HOT_SCHED=3): the count scans on the batch stream first, so the hot runs and results start beside
     // the partition instead of waiting for the scans' slots beside the cold stage
     const bool scans_first = ovl && !pipelined && hot_sched() == 3;
+    // Round 6 (default, SGA_HOT_ONE=0 the round-5 form): the whole hot side on ONE side stream -- count scans
+    // (k_hscan_mid also makes the prioritized sort's column prefix), the prioritized scatter, the hot runs and
+    // results -- no second side stream and no cross-stream join inside the hot chain.  Beside the cold stage
+    // every launch of the chain waits for free slots, so fewer launches shorten the chain.
+    static const bool hot_one = !getenv("SGA_HOT_ONE") || atoi(getenv("SGA_HOT_ONE")) == 1;
     hipStream_t hs = s;
+    if (ovl && !pipelined && !scans_first && hot_one) {
+        side_stream_init(sc);
+        SGA_HIP_CHECK(hipEventRecord(sc.ev_fork0, s));
+        SGA_HIP_CHECK(hipStreamWaitEvent(sc.side, sc.ev_fork0, 0));
+        hipStream_t hs1 = hs = sc.side;
+        hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs1, sc, nseg);
+        hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, hs1, sc, ngroups, ps_groups_h(nseg));
+        hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs1, sc, nseg);
+        sga::prio_sort(sc, nseg, hs1, true);
+        sc.hot_early = true;
+        hot_side(st, sc, ts_base, n, out, hs1, true);
+    } else {
     if (ovl) {
         side_stream_init(sc);
         SGA_HIP_CHECK(hipEventRecord(sc.ev_fork0, s));
@@ -4563,9 +4615,8 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const ReqIn &
     auto prio_sort = [&] { sga::prio_sort(sc, nseg, ps); };
     if (!prio_late) prio_sort();
     hipLaunchKernelGGL(k_hscan_group, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
-    hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, hs, sc, ngroups);
+    hipLaunchKernelGGL(k_hscan_mid, dim3(kHot / kThreads), dim3(kThreads), 0, hs, sc, ngroups, 0u);
     hipLaunchKernelGGL(k_hscan_down, dim3(ngroups, kHot / kThreads), dim3(kThreads), 0, hs, sc, nseg);
-    hipLaunchKernelGGL(k_hot_pre, dim3(kHotBuckets), dim3(kThreads), 0, hs, sc);
     if (prio_late) prio_sort();
     if (scans_first) {  // the hot side forks after the scans and the prioritized sort
         SGA_HIP_CHECK(hipEventRecord(sc.ev_fork, s));
@@ -4581,6 +4632,7 @@ static void classify_hot(const ClusterState &st, BatchScratch &sc, const ReqIn &
     // the hot runs write rule state and wait for stage 2 (after the earlier batch's decisions).
     sc.hot_early = ovl && !pipelined;
     if (sc.hot_early) hot_side(st, sc, ts_base, n, out, hs, true);
+    }
     if (sc.part_lb) {  // the cold partition: one pass into slot bins, ordered per bin by k_cold_fused
         const uint32_t ngroups = (nseg + kPartGroup - 1) / kPartGroup;
         hipLaunchKernelGGL(k_part_colscan, dim3(kPartBins / 256, ngroups), dim3(256), 0, s, sc, nseg);
@@ -4754,7 +4806,8 @@ __global__ __launch_bounds__(kThreads) void k_unpack(const uint32_t *__restrict_
         const uint32_t *r = pk + 3 * (size_t)i;
         f[i] = (int64_t)r[0];
         t[i] = r[1];
-        a[i] = (int32_t)(r[2] & 0xFFFFu);
+        // reserved flag bits set: acquireCount 0, so the request answers BAD_REQUEST like the hot path's
+        a[i] = (r[2] >> 17) ? 0 : (int32_t)(r[2] & 0xFFFFu);
         p[i] = (uint8_t)((r[2] >> 16) & 1u);
     }
 }

@@ -1704,6 +1704,9 @@ int sga_load_cluster_param_rules(sga_engine *e, const char *ns, const sga_cluste
                 g.plpool_free[h.lru_words].push_back(h.lru_off);
                 h.lru_words = 0;
             }
+            // the dead slot's device state (queue pointers, starts, key count) is reset before its area can
+            // be handed to another rule: k_plru_collect must never see the dead rule's keys as queued
+            fresh.push_back((uint32_t)(&h - g.pslots.data()));
         }
         for (int64_t fid : order) {
             const sga_cluster_param_rule &r = *rule_map[fid];

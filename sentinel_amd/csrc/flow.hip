@@ -675,6 +675,7 @@ __device__ int degrade_block_index(CbDev *cbs, uint32_t n, int64_t t) {  // -1: 
         if (b.state == 0) ok = true;
         else if (b.state == 1 && t >= b.next_retry) {
             b.state = 2;
+            b.probe_t = t;
             if (k < 64) half_mask |= 1ULL << k;
             ok = true;
         }
@@ -1151,6 +1152,12 @@ __global__ void k_lseq(FlowState st, int64_t max_rt, SysDev sys, const uint8_t *
             node_add(c, nd, t, MB_PASS, -(int64_t)a);
             node_add(c, nd, t, MB_BLOCK, a);
             param_threads<true>(c, r, pa, hp, param_in[i], -1, i);
+            // the whenTerminate hook of fromOpenToHalfOpen (AbstractCircuitBreaker.java:117-139, issue 1638): a
+            // breaker this entry moved to HALF_OPEN sees the block error and falls back to OPEN (next retry kept).
+            // The entry is identified by its time: the revoke carries the entry's timestamp
+            CbDev *cbs = st.cbs + st.res[r].cb_off;
+            for (uint32_t k = 0; k < st.res[r].n_cbs; ++k)
+                if (cbs[k].state == 2 && cbs[k].probe_t == t) cbs[k].state = 1;
             if (in) {
                 int64_t *e = entry_node(c);
                 e[kNodeThreads] -= 1;
@@ -4263,7 +4270,10 @@ __global__ __launch_bounds__(64 * kCbW) void k_cb_flows(FlowState st, FlowScratc
                     probe = s_min;
                     __syncthreads();
                 }
-                if (probe < je) b.state = 2;  // fromOpenToHalfOpen: the probe passes
+                if (probe < je) {  // fromOpenToHalfOpen: the probe passes
+                    b.state = 2;
+                    b.probe_t = ts_base + (int64_t)pay[probe].ts_off;
+                }
             }
             for (uint32_t j = jb + threadIdx.x; j < je; j += 64 * kCbW) {
                 const uint32_t idx = pay[j].idx & F_IDX;

@@ -75,6 +75,7 @@ struct CbDev {
     int32_t stat_interval, state;   // state: 0 CLOSED, 1 OPEN, 2 HALF_OPEN
     int64_t recovery_ms, max_allowed_rt, next_retry;
     int64_t st_start, st_bad, st_total;  // LeapArray(1, statIntervalMs) bucket
+    int64_t probe_t;  // time of the entry that moved it OPEN -> HALF_OPEN (its revoke moves it back)
 };
 
 struct ResDev {

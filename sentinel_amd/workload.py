@@ -221,6 +221,13 @@ def pack_requests(f, a, p, t):
     0 <= acquire < 2^16 (the packed entry's domain)."""
     import torch
     n = f.numel()
+    if n:  # outside the domain a value would wrap into a different valid request
+        if int(f.min()) < 0 or int(f.max()) >= 1 << 32:
+            raise ValueError("pack_requests: flowId outside [0, 2^32)")
+        if int(a.min()) < 0 or int(a.max()) >= 1 << 16:
+            raise ValueError("pack_requests: acquireCount outside [0, 2^16)")
+        if int(p.min()) < 0 or int(p.max()) > 1:
+            raise ValueError("pack_requests: prioritized must be 0 or 1")
     out = torch.empty((n, 3), dtype=torch.int32, device=f.device)
     out[:, 0] = f.to(torch.int64).to(torch.int32)
     out[:, 1] = t.to(torch.int32)

@@ -265,3 +265,37 @@ def test_lru_small_capacity_mixed(cm):
         p.check_sums([(ff, v) for ff in range(1, 9) for v in (0, 1, 7, 19)], now)
         p.check_top(range(1, 9), now, number=8)
     p.close()
+
+
+def test_lru_area_of_dropped_rule_reused(cm):
+    """A rule in LRU mode is dropped by a reload; a new rule of the same geometry then switches to LRU and
+    gets the dropped rule's queue area from the pool. The dropped rule's keys stay in the key store: none
+    of them may join the new rule's queues (its evictions, decisions and sums must equal the oracle's)."""
+    rng = np.random.default_rng(41)
+    L = H.lib()
+    p = Pair(cm)
+    p.mgr.set_param_capacity(40)
+    L.orc_cluster_set_param_capacity(40)
+    geo = {"count": 3.0, "threshold_type": 1, "sample_count": 2, "window_interval_ms": 1000}
+    try:
+        p.load("default", [dict(geo, flow_id=1), dict(geo, flow_id=2)])
+        n = 3000
+        ts = T0 + np.arange(n) // 4
+        fid = np.where(rng.random(n) < 0.7, 1, 2)
+        params = [[int(rng.integers(0, 200 if f == 1 else 20))] for f in fid]
+        p.run(fid, np.ones(n, np.int64), params, ts, "rule 1 switches to LRU")
+        p.load("default", [dict(geo, flow_id=2)])            # rule 1 and its metric dropped
+        p.load("default", [dict(geo, flow_id=2), dict(geo, flow_id=3)])  # rule 3: same S and capacity
+    finally:
+        L.orc_cluster_set_param_capacity(0)
+    p.mgr.set_param_capacity(0)
+    t1 = int(ts[-1]) + 1
+    for b in range(3):
+        ts2 = t1 + b * 700 + np.arange(n) // 5
+        fid2 = np.where(rng.random(n) < 0.8, 3, 2)
+        params2 = [[int(rng.integers(0, 200 if f == 3 else 20))] for f in fid2]
+        p.run(fid2, np.ones(n, np.int64), params2, ts2, f"rule 3 batch {b}")
+        now = int(ts2[-1])
+        p.check_sums([(3, v) for v in range(0, 200, 7)] + [(2, v) for v in range(20)], now)
+        p.check_top([2, 3], now, number=10)
+    p.close()

@@ -65,7 +65,7 @@ def _engine(cluster, hot, max_batch, max_rules=1 << 16):
     return cluster.Engine(max_batch=max_batch, max_rules=max_rules, **kw)
 
 
-def _run(L, eng, dev, f, a, p, ts, packed):
+def _run(L, eng, dev, f, a, p, ts, packed, resv=None):
     import torch
     base = int(ts.min())
     n = len(f)
@@ -75,6 +75,9 @@ def _run(L, eng, dev, f, a, p, ts, packed):
         rec[:, 0] = f.astype(np.uint32)
         rec[:, 1] = (ts - base).astype(np.uint32)
         rec[:, 2] = a.astype(np.uint32) | (p.astype(np.uint32) << 16)
+        if resv is not None:  # reserved flag bits: the packed record answers BAD_REQUEST
+            rec[resv, 2] = (rec[resv, 2] & 0xFFFF) | (np.uint32(1) << 16) * (p[resv].astype(np.uint32) & 1) | \
+                (np.uint32(2) << 16) << (np.arange(len(resv), dtype=np.uint32) % 15)
         d = torch.from_numpy(rec.view(np.int32)).to(dev)
         rc = L.sga_request_tokens_packed_device(eng.handle, d.data_ptr(), base, n, o.data_ptr(), None)
     else:
@@ -91,7 +94,8 @@ def _run(L, eng, dev, f, a, p, ts, packed):
 def test_packed_entry_matches_arrays_and_oracle(hot):
     """Random Zipf traces over 3000 rules with invalid requests (flowId 0, unknown flowIds, acquire 0), large
     acquire counts (escapes: 200, 65535) and 5 % prioritized requests, six batches each way: the packed entry's
-    TokenResults equal the array entry's and the oracle's, on the hot, sort and small paths."""
+    TokenResults equal the array entry's and the oracle's, on the hot, sort and small paths.  Packed records with
+    reserved flag bits set answer BAD_REQUEST (the array entry and the oracle see acquireCount 0 there)."""
     import torch
     from sentinel_amd import _lib, cluster
     from sentinel_amd.workload import ClusterTrace
@@ -102,7 +106,7 @@ def test_packed_entry_matches_arrays_and_oracle(hot):
     cnt = np.minimum(cnt, 500.0)
     m = 3000 if hot == "small" else 200_000
     rng = np.random.default_rng(7)
-    batches = []
+    batches, resv = [], []
     for b in range(6):
         f, a, p, ts = tr.events(b * m, m)
         f, a = f.copy(), a.copy()
@@ -112,12 +116,17 @@ def test_packed_entry_matches_arrays_and_oracle(hot):
         a[k[2 * len(k) // 3:]] = 0
         j = rng.integers(0, m, size=m // 500)
         a[j] = rng.choice([2, 3, 200, 65535], size=len(j))
-        batches.append((f, a, p, ts))
+        r = rng.integers(0, m, size=m // 300)
+        a_arr = a.copy()
+        a_arr[r] = 0  # what the reserved bits mean: BAD_REQUEST
+        batches.append((f, a_arr, p, ts))
+        resv.append((a, r))
     res = {}
     for packed in (False, True):
         eng = _engine(cluster, hot, max_batch=m)
         cluster.ClusterFlowRuleManager(eng).load_rule_arrays("default", fid_r, cnt)
-        res[packed] = [_run(L, eng, dev, *bt, packed) for bt in batches]
+        res[packed] = [_run(L, eng, dev, bt[0], rv[0] if packed else bt[1], bt[2], bt[3], packed,
+                            rv[1] if packed else None) for bt, rv in zip(batches, resv)]
         eng.close()
     orc = H.cluster_replay_sharded(fid_r, cnt, batches, threads=4)
     for b in range(len(batches)):

@@ -7,7 +7,7 @@ import pytest
 
 from tests import local_trace as lt
 from tests import oracle_harness as H
-from tests.test_local_parity_gpu import T0, _assert_nodes, _assert_same, _load, _sentinel
+from tests.test_local_parity_gpu import T0, _assert_nodes, _assert_same, _load, _sentinel, _submit
 
 pytestmark = pytest.mark.gpu
 
@@ -271,5 +271,52 @@ def test_revoked_entries_after_a_later_slot_block():
     assert n_rev > 500 and n_pass > n_rev
     end = T0 + 30 * 1000
     assert s.node(0xFFFFFFFF, end).cur_thread_num == 0
+    orc.close()
+    eng.close()
+
+
+def test_revoked_probes_return_breakers_to_open():
+    """Revokes of entries that were circuit-breaker probes (AbstractCircuitBreaker.java:117-139: the
+    whenTerminate hook moves a breaker the blocked entry made HALF_OPEN back to OPEN, next retry kept).
+    Exception-count and slow-RT breakers trip on erroring / slow exits; after each retry time the first entry
+    probes, and revokes take some probes back. Decisions, waits and node views equal the oracle's replay."""
+    rng = np.random.default_rng(23)
+    n_res = 3
+    degrade = [{"resource": 0, "grade": 2, "count": 2, "min_request_amount": 3, "time_window": 1},
+               {"resource": 1, "grade": 0, "count": 20, "min_request_amount": 3, "time_window": 1,
+                "slow_ratio_threshold": 0.5},
+               {"resource": 2, "grade": 1, "count": 0.5, "min_request_amount": 3, "time_window": 1}]
+    flow = [{"resource": 2, "count": 50.0}]
+    orc = lt.Oracle(n_res, flow, [], degrade)
+    eng, s = _sentinel(n_res, 1 << 12)
+    _load(s, flow, None, degrade)
+    reopened = 0
+    for k in range(40):
+        n = 60
+        t0 = T0 + k * 700
+        st = {"kind": np.zeros(n, np.uint8), "resource": rng.integers(0, n_res, n).astype(np.uint32),
+              "ts": t0 + np.sort(rng.integers(0, 100, n)).astype(np.int64), "acquire": np.ones(n, np.int32),
+              "flags": np.where(rng.random(n) < 0.5, 8, 0).astype(np.uint8), "rt": np.zeros(n, np.int64),
+              "param": np.zeros(n, np.uint64)}
+        exp = orc.replay(st)
+        got = _submit(s, st)
+        _assert_same(st, got, exp, f"round {k} entries")
+        passed = np.nonzero(exp[0] == 0)[0]
+        rev = passed[rng.random(len(passed)) < 0.5]
+        ext = np.setdiff1d(passed, rev)
+        fx = {f: np.concatenate([st[f][rev], st[f][ext]]) for f in st}
+        fx["kind"] = np.concatenate([np.full(len(rev), 3, np.uint8), np.ones(len(ext), np.uint8)])
+        err = rng.random(len(ext)) < 0.6
+        fx["flags"] = fx["flags"] | np.concatenate([np.zeros(len(rev), np.uint8), np.where(err, 2, 0).astype(np.uint8)])
+        fx["rt"] = np.concatenate([np.zeros(len(rev), np.int64), rng.integers(1, 60, len(ext)).astype(np.int64)])
+        fx["ts"] = np.concatenate([st["ts"][rev], t0 + 150 + fx["rt"][len(rev):]])
+        order = np.argsort(fx["ts"], kind="stable")
+        fx = {f: v[order] for f, v in fx.items()}
+        exp_x = orc.replay(fx)
+        got_x = _submit(s, fx)
+        _assert_same(fx, got_x, exp_x, f"round {k} revokes and exits")
+        _assert_nodes(s, orc, n_res, t0 + 300)
+        reopened += int((exp[0] == 3).sum() > 0 and len(rev) > 0)
+    assert reopened > 5
     orc.close()
     eng.close()

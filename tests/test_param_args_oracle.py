@@ -147,3 +147,29 @@ def test_revoke_undoes_the_pass_and_counts_the_block():
     assert v["block_qps"] == 2 and e["block_qps"] == 2  # the second entry's block + the revoked entry's
     assert orc.replay(ev(0, T + 3))[0][0] == 0  # thread and parameter thread counts released
     orc.close()
+
+
+def test_revoked_probe_returns_its_breaker_to_open():
+    """A revoked entry that was a breaker's HALF_OPEN probe: the reference's whenTerminate hook
+    (AbstractCircuitBreaker.java:117-139, the issue-1638 workaround) sees the block error and moves the
+    breaker back to OPEN without a new retry time, so the next entry past the retry time probes again
+    (a breaker left HALF_OPEN would block every later entry)."""
+    T = 1_700_000_000_000
+    degrade = [{"resource": 0, "grade": 2, "count": 2, "min_request_amount": 3, "time_window": 1}]
+    orc = lt.Oracle(1, [], [], degrade)
+
+    def ev(kind, t, err=False):
+        return {"kind": np.array([kind], np.uint8), "resource": np.zeros(1, np.uint32), "ts": np.array([t], np.int64),
+                "acquire": np.ones(1, np.int32), "flags": np.array([2 if err else 0], np.uint8),
+                "rt": np.array([1], np.int64), "param": np.zeros(1, np.uint64)}
+
+    for _ in range(4):
+        assert orc.replay(ev(0, T))[0][0] == 0
+    for _ in range(4):
+        orc.replay(ev(1, T + 1, err=True))  # three errors trip it at T + 1: OPEN, retry at T + 1001
+    assert orc.replay(ev(0, T + 500))[0][0] == 3  # OPEN
+    assert orc.replay(ev(0, T + 1500))[0][0] == 0  # the probe: HALF_OPEN
+    assert orc.replay(ev(0, T + 1501))[0][0] == 3  # HALF_OPEN blocks
+    orc.replay(ev(3, T + 1500))  # the probe is revoked: back to OPEN, retry time kept
+    assert orc.replay(ev(0, T + 1600))[0][0] == 0  # a new probe
+    orc.close()

@@ -148,6 +148,26 @@ __global__ void k_quad(int4 *rec, const uint32_t *__restrict__ sl, uint32_t n) {
     if (q < 3) gp[q] = v[3];
 }
 
+// lane-interleaved records: int4 k of slot s at ((s / 64) * kRecI4 + k) * 64 + s % 64 (a wave over 64 near slots
+// loads each piece as a few contiguous kilobytes); one lane per touched rule as in k_lane
+__device__ __forceinline__ size_t ilv(uint32_t s, int k) { return ((size_t)(s >> 6) * kRecI4 + k) * 64 + (s & 63); }
+__global__ void k_ilv(int4 *rec, const uint32_t *__restrict__ sl, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s0 = sl[i];
+    int4 h[kHdrI4];
+#pragma unroll
+    for (int k = 0; k < kHdrI4; ++k) h[k] = rec[ilv(s0, k)];
+    long long s = 0;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) s += hi64(h[k]);
+    const int cj = (int)(lo64(h[10]) & 7);
+    rec[ilv(s0, cj)] = make_int4((int)s, 0, h[cj].z + 1, h[cj].w);
+    rec[ilv(s0, kHdrI4 + 3 * cj)] = h[11];
+    rec[ilv(s0, kHdrI4 + 3 * cj + 1)] = h[12];
+    rec[ilv(s0, kHdrI4 + 3 * cj + 2)] = h[13];
+}
+
 template <class F> float timeit(F f, int reps = 20) {
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     f(); CK(hipDeviceSynchronize());
@@ -180,6 +200,8 @@ int main(int argc, char **argv) {
         float t;
         t = timeit([&] { hipLaunchKernelGGL(k_lane, dim3(nb), dim3(wg), 0, 0, rec, s, touched); });
         printf("{\"mode\":\"lane\",\"order\":\"%s\",\"touched\":%u,\"wg\":%d,\"us\":%.2f,\"GBs\":%.1f}\n", on, touched, wg, t * 1e3, mb / t);
+        t = timeit([&] { hipLaunchKernelGGL(k_ilv, dim3(nb), dim3(wg), 0, 0, rec, s, touched); });
+        printf("{\"mode\":\"ilv\",\"order\":\"%s\",\"touched\":%u,\"wg\":%d,\"us\":%.2f,\"GBs\":%.1f}\n", on, touched, wg, t * 1e3, mb / t);
         t = timeit([&] { hipLaunchKernelGGL(k_lane2, dim3(nb), dim3(wg), 0, 0, rec, s, touched); });
         printf("{\"mode\":\"lane2\",\"order\":\"%s\",\"touched\":%u,\"wg\":%d,\"us\":%.2f,\"GBs\":%.1f}\n", on, touched, wg, t * 1e3, mb / t);
         t = timeit([&] { hipLaunchKernelGGL(k_trans, dim3(nb), dim3(wg), lds, 0, rec, s, touched); });
