@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) batches")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the first two timed batches")
-    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c4full", "c5a", "c5b"],
+    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c4args", "c4full", "c5a", "c5b"],
                     help="BASELINE.json configuration (SURVEY.md 8(d)); c3 = the headline, the others through "
                          "bench_local.py (c2 / c4 / c4full / c5b shard by resource over --gpus N)")
     return ap.parse_args()

@@ -27,7 +27,7 @@ import numpy as np
 T0 = 1_700_000_000_000
 HBM_PEAK_GBS = 8000.0
 KIND_ENTRY, KIND_EXIT = 0, 1
-EV_ERROR, EV_HAS_PARAM = 2, 4
+EV_ERROR, EV_HAS_PARAM, EV_ARGS = 2, 4, 32
 # E_in / E_out and per-key state bytes S_k
 E_ENTRY, E_PARAM_ENTRY, E_EXIT, E_DEC = 12, 20, 12, 1
 E_RLS_IN, E_RLS_OUT, S_RLS = 12, 8, 72
@@ -57,9 +57,13 @@ def _zipf(rng, n_items, size, s=1.1, mask=None):
 
 
 class Batch:
-    """One batch: entries, then exits (exit i belongs to entry exit_of[i]); host arrays."""
+    """One batch: entries, then exits (exit i belongs to entry exit_of[i]); host arrays.  kind: 0 entries, or 2 (a
+    block by a slot outside the engine: no exit follows); revoke: a passed entry that a slot after the engine's
+    checks blocked -- its exit is a kind 3 revoke at the entry's time; pvals: the argument vectors' words
+    (SGA_EV_ARGS entries; their exits carry the same vector)."""
 
-    def __init__(self, res, ts, acq=None, flags=None, param=None, exit_rt=None, exit_err=None):
+    def __init__(self, res, ts, acq=None, flags=None, param=None, exit_rt=None, exit_err=None, kind=None,
+                 revoke=None, pvals=None):
         n = len(res)
         self.n = n
         self.res = res.astype(np.uint32)
@@ -67,15 +71,25 @@ class Batch:
         self.acq = (np.ones(n) if acq is None else acq).astype(np.int32)
         self.flags = (np.zeros(n) if flags is None else flags).astype(np.uint8)
         self.param = (np.zeros(n) if param is None else param).astype(np.uint64)
+        self.kind = None if kind is None else kind.astype(np.uint8)
+        self.pvals = None if pvals is None else np.ascontiguousarray(pvals, np.uint64)
         self.exit_of = None
+        self.exit_kind = None
         if exit_rt is not None:
-            ets = self.ts + exit_rt.astype(np.int64)
+            exit_rt = exit_rt.astype(np.int64)
+            if revoke is not None:
+                exit_rt = np.where(revoke, 0, exit_rt)  # the revoke carries the entry's time
+            ets = self.ts + exit_rt
             order = np.argsort(ets, kind="stable")
             self.exit_of = order.astype(np.int64)
             self.exit_ts = ets[order]
-            self.exit_rt = exit_rt.astype(np.int64)[order]
-            self.exit_flags = (self.flags[order] & EV_HAS_PARAM) | \
+            self.exit_rt = exit_rt[order]
+            self.exit_flags = (self.flags[order] & (EV_HAS_PARAM | EV_ARGS)) | \
                 (np.zeros(n, np.uint8) if exit_err is None else (exit_err[order] * EV_ERROR).astype(np.uint8))
+            if revoke is not None:
+                self.exit_kind = np.where(revoke[order], 3, 1).astype(np.uint8)
+                self.exit_flags = np.where(revoke[order], self.exit_flags & (EV_HAS_PARAM | EV_ARGS),
+                                           self.exit_flags).astype(np.uint8)
         self.t_lo = int(min(self.ts.min(), self.exit_ts.min() if self.exit_of is not None else self.ts.min()))
         self.t_hi = int(max(self.ts.max(), self.exit_ts.max() if self.exit_of is not None else self.ts.max()))
 
@@ -137,6 +151,36 @@ def _cfg_c4_common(rng, erng, fold):
     return dict(name="C4 10k ParamFlowRules (90% default / 10% throttle), Zipf(1.1) values over 10^7 folded to "
                      "<= 4000 per rule (pinned mode), 2^22 entries + exits per batch",
                 n_res=n_res, param=param, batch=b, sample=1 << 20)
+
+
+def _cfg_c4args(rng, erng=None):
+    """C4 pinned with what a JVM feeding the engine through GpuStatisticSlot sends besides plain entries: 5 % of
+    the entries pass their whole argument vector (SphU.entry(res, v, extra): SGA_EV_ARGS, the exits the same),
+    0.1 % are blocks by a slot before the engine (kind 2), 0.2 % of the passed entries are revoked by a slot after
+    it (kind 3 at the entry's time instead of an exit)."""
+    erng = erng or rng
+    cfg = _cfg_c4_common(rng, erng, fold=True)
+    b = cfg["batch"]
+    n = b.n
+    args = erng.random(n) < 0.05
+    blocked = (erng.random(n) < 0.001) & ~args
+    revoke = (erng.random(n) < 0.002) & ~blocked
+    extra = erng.integers(0, 1000, size=n).astype(np.uint64)
+    ia = np.nonzero(args)[0]
+    pvals = np.zeros(4 * len(ia), np.uint64)  # per vector: (scalar, v), (scalar, extra)
+    pvals[1::4] = b.param[ia]
+    pvals[3::4] = extra[ia]
+    flags, param = b.flags.copy(), b.param.copy()
+    flags[ia] = EV_ARGS
+    param[ia] = (np.arange(len(ia), dtype=np.uint64) * np.uint64(4)) << np.uint64(32) | np.uint64(2)
+    kind = np.where(blocked, 2, 0).astype(np.uint8)
+    rt = np.zeros(n, np.int64)
+    rt[b.exit_of] = b.exit_rt  # each entry's RT back in entry order
+    cfg["batch"] = Batch(b.res, b.ts, flags=flags, param=param, exit_rt=rt, kind=kind, revoke=revoke, pvals=pvals)
+    cfg["name"] = ("C4 args: C4 pinned, 5% of the entries with a whole argument vector (SGA_EV_ARGS, exits the "
+                   "same), 0.1% blocks by a slot before the engine (kind 2), 0.2% of the passed entries revoked "
+                   "(kind 3), 2^22 entries + exits per batch")
+    return cfg
 
 
 def _cfg_c4full(rng, erng=None):
@@ -201,7 +245,12 @@ def _state_bytes(cfg, b):
         thr = np.zeros(cfg["n_res"], bool)
         for r in cfg["param"]:
             thr[r["resource"]] = r.get("control_behavior", 0) == 2
-        keys = np.unique(b.res.astype(np.uint64) << np.uint64(32) | b.param.astype(np.uint64))
+        val = b.param.astype(np.uint64)
+        if b.pvals is not None:  # an argument vector's value: its argument 0
+            av = (b.flags & EV_ARGS) != 0
+            val = val.copy()
+            val[av] = b.pvals[(val[av] >> np.uint64(32)).astype(np.int64) + 1]
+        keys = np.unique(b.res.astype(np.uint64) << np.uint64(32) | val)
         kr = (keys >> np.uint64(32)).astype(np.int64)
         total += int(np.where(thr[kr], S_PARAM_THROTTLE, S_PARAM).sum())
     return 2 * total
@@ -224,9 +273,12 @@ class _Shard:
         idx = np.nonzero(sel_res[b.res[:m]])[0] if sel_res is not None else np.arange(m)
         self.idx = idx
         self.ent = {k: np.ascontiguousarray(v) for k, v in
-                    {"kind": np.zeros(len(idx), np.uint8), "resource": b.res[idx], "ts": b.ts[idx],
+                    {"kind": np.zeros(len(idx), np.uint8) if b.kind is None else b.kind[idx],
+                     "resource": b.res[idx], "ts": b.ts[idx],
                      "acquire": b.acq[idx], "flags": b.flags[idx], "rt": np.zeros(len(idx), np.int64),
                      "param": b.param[idx]}.items()}
+        if b.pvals is not None:
+            self.ent["param_values"] = b.pvals
         self.ex = None
         self.n_ev = len(idx)
 
@@ -239,14 +291,19 @@ class _Shard:
             return
         passed = np.zeros(b.n, bool)
         passed[self.idx] = (self.dec == 0) | (self.dec == 4)
+        if b.kind is not None:
+            passed &= b.kind != 2
         pos = np.empty(b.n, np.int64)
         pos[b.exit_of] = np.arange(b.n)
         sel = b.exit_of[b.exit_of < self.m]
         order = np.sort(pos[sel[passed[sel]]])
         self.ex = {k: np.ascontiguousarray(v) for k, v in
-                   {"kind": np.ones(len(order), np.uint8), "resource": b.res[b.exit_of[order]],
+                   {"kind": np.ones(len(order), np.uint8) if b.exit_kind is None else b.exit_kind[order],
+                    "resource": b.res[b.exit_of[order]],
                     "ts": b.exit_ts[order], "acquire": b.acq[b.exit_of[order]], "flags": b.exit_flags[order],
                     "rt": b.exit_rt[order], "param": b.param[b.exit_of[order]]}.items()}
+        if b.pvals is not None:
+            self.ex["param_values"] = b.pvals
         self.n_ev += len(order)
 
     def exits(self):
@@ -351,13 +408,14 @@ def run_local(args, cfg_name):
         if os.environ.get("SGA_BENCH_ONE_DEVICE") == "1":
             local = 0  # rehearsal of the N-rank path on a one-GPU box
     SHARD = (rank, world)
-    seed = {"c1": 101, "c2": 102, "c4": 104, "c4full": 104, "c5b": 105}[cfg_name]
+    seed = {"c1": 101, "c2": 102, "c4": 104, "c4args": 104, "c4full": 104, "c5b": 105}[cfg_name]
     # the rules (count, controller, grade of each resource) come from the base seed on every rank, so a shard's
     # rules are the single-GPU workload's restricted to the shard; only the event stream is drawn per rank (one
     # rank: one generator for both, the same draws as before)
     rng = np.random.default_rng(seed)
     erng = rng if world == 1 else np.random.default_rng([seed, rank, world])
-    cfg = {"c1": _cfg_c1, "c2": _cfg_c2, "c4": _cfg_c4, "c4full": _cfg_c4full, "c5b": _cfg_c5b}[cfg_name](rng, erng)
+    cfg = {"c1": _cfg_c1, "c2": _cfg_c2, "c4": _cfg_c4, "c4args": _cfg_c4args, "c4full": _cfg_c4full,
+           "c5b": _cfg_c5b}[cfg_name](rng, erng)
     b = cfg["batch"]
     if os.environ.get("SGA_BENCH_DRY") == "1":  # launch and routing check only (tests, CPU)
         own = own_resources(cfg["n_res"])
@@ -389,7 +447,8 @@ def run_local(args, cfg_name):
         return torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(dev)
 
     span = b.t_hi - b.t_lo + 1000
-    e_kind = torch.zeros(b.n, dtype=torch.uint8, device=dev)
+    e_kind = up(b.kind, np.uint8) if b.kind is not None else torch.zeros(b.n, dtype=torch.uint8, device=dev)
+    pvals = up(b.pvals, np.int64) if b.pvals is not None else None
     e_res, e_acq = up(b.res, np.int32), up(b.acq, np.int32)
     e_flags, e_param = up(b.flags, np.uint8), up(b.param, np.int64)
     e_off = up((b.ts - b.t_lo).astype(np.uint32), np.int32)
@@ -397,8 +456,9 @@ def run_local(args, cfg_name):
     wait = torch.empty(b.n, dtype=torch.int32, device=dev)
     has_exit = b.exit_of is not None
     if has_exit:
-        x_kind = torch.ones(b.n, dtype=torch.uint8, device=dev)
+        x_kind = up(b.exit_kind, np.uint8) if b.exit_kind is not None else torch.ones(b.n, dtype=torch.uint8, device=dev)
         x_of = up(b.exit_of, np.int64)
+        x_blocked = (e_kind[x_of] == 2) if b.kind is not None else None  # a block outside the engine: no exit
         x_res_all = e_res[x_of]
         x_acq = e_acq[x_of].contiguous()
         x_param = e_param[x_of].contiguous()
@@ -410,13 +470,16 @@ def run_local(args, cfg_name):
 
     def step(k):
         base = b.t_lo + k * span
-        s.submit_device(e_kind, e_res, base, e_off, e_acq, flags=e_flags, param=e_param, decision=dec, wait=wait,
-                        stream=stream)
+        s.submit_device(e_kind, e_res, base, e_off, e_acq, flags=e_flags, param=e_param, param_values=pvals,
+                        decision=dec, wait=wait, stream=stream)
         if has_exit:
             d = dec[x_of]
-            x_res = torch.where((d == 0) | (d == 4), x_res_all, unknown)
+            ok = (d == 0) | (d == 4)
+            if x_blocked is not None:
+                ok &= ~x_blocked
+            x_res = torch.where(ok, x_res_all, unknown)
             s.submit_device(x_kind, x_res, base, x_off, x_acq, flags=x_flags, rt=x_rt, param=x_param,
-                            decision=x_dec, wait=None, stream=stream)
+                            param_values=pvals, decision=x_dec, wait=None, stream=stream)
 
     # the first step runs on a fresh engine, as the oracle's one-thread replay of the sample does: its
     # decisions and waits of the sample's entries are kept for the parity check below

@@ -382,6 +382,22 @@ int sga_rls_should_rate_limit_device(sga_engine *e, const uint32_t *d_desc_offse
  * (single default context, limitApp "default", strategy DIRECT).
  * ------------------------------------------------------------------------- */
 
+/* Coalescing queue of single local events (SphU.entry / Entry.exit from many application threads, one
+ * synchronous call each: CtSph.entryWithPriority, CORE/CtSph.java:117-168).  sga_event_submit enqueues one
+ * event (lock-free, any thread; kind, flags, param as in sga_submit_events_ex, param_values holding this
+ * event's argument words only, at most 64 of them -- SGA_ERANGE otherwise) and returns a ticket;
+ * sga_event_poll returns SGA_OK with its decision and wait once decided, SGA_EAGAIN before (a poller that
+ * finds no batch running decides every queued event as ONE batch, so concurrent callers share a launch);
+ * each ticket is polled to SGA_OK exactly once.  Decisions equal one sga_submit_events_ex call per event in
+ * ticket order.  A batch that fails answers decision -1 and SGA_EIO.  sga_event_one = submit + poll until
+ * decided (an event with more argument words than a slot holds is decided on its own). */
+int sga_event_submit(sga_engine *e, uint8_t kind, uint32_t resource, int64_t ts, int32_t acquire, uint8_t flags,
+                     int64_t rt, uint64_t param, const uint64_t *param_values, size_t n_values, uint64_t *ticket);
+int sga_event_poll(sga_engine *e, uint64_t ticket, int8_t *decision, int32_t *wait_ms);
+int sga_event_one(sga_engine *e, uint8_t kind, uint32_t resource, int64_t ts, int32_t acquire, uint8_t flags,
+                  int64_t rt, uint64_t param, const uint64_t *param_values, size_t n_values, int8_t *decision,
+                  int32_t *wait_ms);
+
 /* decision codes of sga_submit_events.  wait_ms of an entry: the sleep of a pass (RateLimiter pacing,
  * SHOULD_WAIT, parameter throttle) or of SGA_PASS_WAIT; for a block, the block detail the exception
  * carries: SGA_BLOCK_FLOW the blocking FlowRule's index in the resource's rules (FlowRuleComparator

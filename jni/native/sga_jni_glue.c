@@ -89,7 +89,8 @@ int sgaj_entry(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, 
     const int64_t rt = 0;
     int8_t dec = 0;
     int32_t wait = 0;
-    const int rc = sga_submit_events(e, &kind, &resource, &now_ms, &count, &fl, &rt, &param, 1, &dec, &wait);
+    /* through the coalescing queue: concurrent SphU.entry callers share one engine batch */
+    const int rc = sga_event_one(e, kind, resource, now_ms, count, fl, rt, param, NULL, 0, &dec, &wait);
     if (rc == SGA_OK) {
         dec_wait[0] = dec;
         dec_wait[1] = wait;
@@ -102,7 +103,7 @@ int sgaj_exit(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, u
     const uint8_t kind = 1, fl = (uint8_t)flags;
     int8_t dec = 0;
     int32_t wait = 0;
-    return sga_submit_events(e, &kind, &resource, &now_ms, &count, &fl, &rt_ms, &param, 1, &dec, &wait);
+    return sga_event_one(e, kind, resource, now_ms, count, fl, rt_ms, param, NULL, 0, &dec, &wait);
 }
 
 int sgaj_entry_args(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, uint32_t flags,
@@ -112,8 +113,7 @@ int sgaj_entry_args(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t co
     const uint64_t param = (uint64_t)nargs; /* the pairs start at offset 0 */
     int8_t dec = 0;
     int32_t wait = 0;
-    const int rc = sga_submit_events_ex(e, &kind, &resource, &now_ms, &count, &fl, &rt, &param, 1, words, nwords,
-                                        &dec, &wait);
+    const int rc = sga_event_one(e, kind, resource, now_ms, count, fl, rt, param, words, nwords, &dec, &wait);
     if (rc == SGA_OK) {
         dec_wait[0] = dec;
         dec_wait[1] = wait;
@@ -127,8 +127,7 @@ int sgaj_exit_args(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t cou
     const uint64_t param = (uint64_t)nargs;
     int8_t dec = 0;
     int32_t wait = 0;
-    return sga_submit_events_ex(e, &kind, &resource, &now_ms, &count, &fl, &rt_ms, &param, 1, words, nwords, &dec,
-                                &wait);
+    return sga_event_one(e, kind, resource, now_ms, count, fl, rt_ms, param, words, nwords, &dec, &wait);
 }
 
 int sgaj_revoke_args(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, uint32_t flags,
@@ -138,8 +137,7 @@ int sgaj_revoke_args(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t c
     const uint64_t param = (uint64_t)nargs;
     int8_t dec = 0;
     int32_t wait = 0;
-    return sga_submit_events_ex(e, &kind, &resource, &now_ms, &count, &fl, &rt, &param, 1, words, nwords, &dec,
-                                &wait);
+    return sga_event_one(e, kind, resource, now_ms, count, fl, rt, param, words, nwords, &dec, &wait);
 }
 
 int sgaj_blocked(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, uint32_t flags) {
@@ -148,7 +146,7 @@ int sgaj_blocked(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count
     const uint64_t param = 0;
     int8_t dec = 0;
     int32_t wait = 0;
-    return sga_submit_events(e, &kind, &resource, &now_ms, &count, &fl, &rt, &param, 1, &dec, &wait);
+    return sga_event_one(e, kind, resource, now_ms, count, fl, rt, param, NULL, 0, &dec, &wait);
 }
 
 int sgaj_load_param_rules(sga_engine *e, size_t n, const uint32_t *resource, const int32_t *grade,

@@ -120,6 +120,11 @@ SIGNATURES = {
     "sga_set_small_batch": (C.c_int, [C.c_void_p, C.c_uint32]),
     "sga_token_submit": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_uint8, C.c_int64, C.POINTER(C.c_uint64)]),
     "sga_poll": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p]),
+    "sga_event_submit": (C.c_int, [C.c_void_p, C.c_uint8, C.c_uint32, C.c_int64, C.c_int32, C.c_uint8, C.c_int64,
+                                   C.c_uint64, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64)]),
+    "sga_event_poll": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_int8), C.POINTER(C.c_int32)]),
+    "sga_event_one": (C.c_int, [C.c_void_p, C.c_uint8, C.c_uint32, C.c_int64, C.c_int32, C.c_uint8, C.c_int64,
+                                C.c_uint64, C.c_void_p, C.c_size_t, C.POINTER(C.c_int8), C.POINTER(C.c_int32)]),
     "sga_request_token_one": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_uint8, C.c_int64, C.c_void_p]),
     "sga_request_tokens": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
                                      C.c_void_p]),

@@ -145,12 +145,48 @@ struct TokenQueue {
     }
 };
 
+// The same coalescing queue for the local path's events (SphU.entry / Entry.exit through GpuStatisticSlot, one
+// synchronous call per entry from every application thread: CtSph.entryWithPriority, CtSph.java:117-168).  A
+// slot holds one event and a copy of its argument words (SGA_EV_ARGS pairs and list values, at most kWords);
+// the combiner concatenates the slots' words, rebases their offsets and decides every filled slot from the head
+// as ONE sga_submit_events_ex batch, in ticket order.
+struct EventQueue {
+    static constexpr uint64_t kCap = 1u << 14;
+    static constexpr uint32_t kWords = 64;
+    struct Slot {
+        std::atomic<uint64_t> seq{0};
+        int64_t ts = 0, rt = 0;
+        uint64_t param = 0;
+        uint32_t resource = 0;
+        int32_t acquire = 0;
+        uint8_t kind = 0, flags = 0;
+        uint32_t nwords = 0;
+        uint64_t words[kWords];
+        int8_t decision = 0;
+        int32_t wait = 0;
+    };
+    std::unique_ptr<Slot[]> ring{new Slot[kCap]};
+    std::atomic<uint64_t> tail{0};
+    uint64_t head = 0;  // combiner only
+    std::atomic<bool> combining{false};
+    std::vector<uint8_t> kind, flags;
+    std::vector<uint32_t> res;
+    std::vector<int64_t> ts, rt;
+    std::vector<int32_t> acq, wait;
+    std::vector<uint64_t> param, vals;
+    std::vector<int8_t> dec;
+    EventQueue() {
+        for (uint64_t i = 0; i < kCap; ++i) ring[i].seq.store(i, std::memory_order_relaxed);
+    }
+};
+
 struct Engine {
     sga_config cfg{};
     hipStream_t stream = nullptr;
     std::string err;
     std::mutex mu;
     TokenQueue tq;
+    EventQueue eq;
     // cluster-mode FlowRules of the local path: ClusterStateManager mode (sga_set_cluster_server) and
     // a generation of the cluster rule set their slots were resolved against
     int32_t cluster_server = 0;
@@ -1642,6 +1678,153 @@ int sga_request_token_one(sga_engine *e, int64_t flow_id, int32_t acquire, uint8
     if (rc != SGA_OK) return rc;
     for (int spin = 0;; ++spin) {
         rc = sga_poll(e, t, out);
+        if (rc != SGA_EAGAIN) return rc;
+        if (spin > 16) std::this_thread::yield();
+    }
+}
+
+// ---- coalescing queue of local events (EventQueue above)
+static int event_combine_round(sga_engine *e);
+
+int sga_event_submit(sga_engine *e, uint8_t kind, uint32_t resource, int64_t ts, int32_t acquire, uint8_t flags,
+                     int64_t rt, uint64_t param, const uint64_t *param_values, size_t n_values, uint64_t *ticket) {
+    if (!e || !ticket) return SGA_EINVAL;
+    // refused here, for this caller only, what would fail the whole coalesced batch
+    if (ts < 0 || acquire < 0 || kind > SGA_KIND_REVOKE) return SGA_EINVAL;
+    const bool args = (flags & SGA_EV_ARGS) != 0;
+    const bool list = !args && (flags & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM);
+    if (args || list) {
+        if (n_values > sga::EventQueue::kWords) return SGA_ERANGE;  // the caller submits it directly
+        if (n_values && !param_values) return SGA_EINVAL;
+        const uint64_t off = param >> 32, na = param & 0xFFFFFFFFu;
+        if (list && off + na > n_values) return SGA_EINVAL;
+        if (args) {
+            if (off + 2 * na > n_values) return SGA_EINVAL;
+            for (uint64_t k = 0; k < na; ++k) {
+                const uint64_t h = param_values[off + 2 * k], w = param_values[off + 2 * k + 1];
+                if ((h >> 62) > 2 || ((h >> 62) == SGA_ARG_LIST && w + (h & 0xFFFFFFFFu) > n_values)) return SGA_EINVAL;
+            }
+        }
+    }
+    sga::EventQueue &q = e->impl.eq;
+    const uint64_t t = q.tail.fetch_add(1, std::memory_order_relaxed);
+    sga::EventQueue::Slot &sl = q.ring[t & (sga::EventQueue::kCap - 1)];
+    const uint64_t prev = t - sga::EventQueue::kCap;  // as sga_token_submit: reclaim, decide or wait
+    for (int spin = 0;; ++spin) {
+        uint64_t s = sl.seq.load(std::memory_order_acquire);
+        if (s == t) break;
+        if (t >= sga::EventQueue::kCap && s == prev + 2 &&
+            sl.seq.compare_exchange_strong(s, t, std::memory_order_acq_rel))
+            break;
+        if (t >= sga::EventQueue::kCap && s == prev + 1) (void)event_combine_round(e);
+        else if (spin > 64) std::this_thread::yield();
+    }
+    sl.kind = kind;
+    sl.resource = resource;
+    sl.ts = ts;
+    sl.acquire = acquire;
+    sl.flags = flags;
+    sl.rt = rt;
+    sl.param = param;
+    sl.nwords = (args || list) ? (uint32_t)n_values : 0u;
+    if (sl.nwords) std::memcpy(sl.words, param_values, sl.nwords * 8);
+    sl.seq.store(t + 1, std::memory_order_release);
+    *ticket = t;
+    return SGA_OK;
+}
+
+// One combining round: every filled slot from the head as one sga_submit_events_ex batch (at most max_batch);
+// each slot's argument words appended to one value array, their offsets rebased.
+static int event_combine_round(sga_engine *e) {
+    sga::EventQueue &q = e->impl.eq;
+    bool expect = false;
+    if (!q.combining.compare_exchange_strong(expect, true, std::memory_order_acquire)) return SGA_OK;
+    const uint64_t h = q.head;
+    const uint64_t cap = std::min<uint64_t>(e->impl.cfg.max_batch, sga::EventQueue::kCap);
+    uint64_t k = 0;
+    q.kind.clear();
+    q.flags.clear();
+    q.res.clear();
+    q.ts.clear();
+    q.rt.clear();
+    q.acq.clear();
+    q.param.clear();
+    q.vals.clear();
+    while (k < cap) {
+        sga::EventQueue::Slot &sl = q.ring[(h + k) & (sga::EventQueue::kCap - 1)];
+        if (sl.seq.load(std::memory_order_acquire) != h + k + 1) break;  // not filled yet: next round
+        uint64_t pv = sl.param;
+        if (sl.nwords) {
+            const uint64_t base = q.vals.size();
+            q.vals.insert(q.vals.end(), sl.words, sl.words + sl.nwords);
+            if (sl.flags & SGA_EV_ARGS) {
+                const uint64_t off = pv >> 32, na = pv & 0xFFFFFFFFu;
+                for (uint64_t j = 0; j < na; ++j)
+                    if ((q.vals[base + off + 2 * j] >> 62) == SGA_ARG_LIST) q.vals[base + off + 2 * j + 1] += base;
+            }
+            pv = (((pv >> 32) + base) << 32) | (pv & 0xFFFFFFFFu);
+        }
+        q.kind.push_back(sl.kind);
+        q.flags.push_back(sl.flags);
+        q.res.push_back(sl.resource);
+        q.ts.push_back(sl.ts);
+        q.rt.push_back(sl.rt);
+        q.acq.push_back(sl.acquire);
+        q.param.push_back(pv);
+        ++k;
+    }
+    int rc = SGA_OK;
+    if (k) {
+        q.dec.assign(k, 0);
+        q.wait.assign(k, 0);
+        rc = sga_submit_events_ex(e, q.kind.data(), q.res.data(), q.ts.data(), q.acq.data(), q.flags.data(),
+                                  q.rt.data(), q.param.data(), k, q.vals.empty() ? nullptr : q.vals.data(),
+                                  q.vals.size(), q.dec.data(), q.wait.data());
+        for (uint64_t j = 0; j < k; ++j) {
+            sga::EventQueue::Slot &sl = q.ring[(h + j) & (sga::EventQueue::kCap - 1)];
+            sl.decision = rc == SGA_OK ? q.dec[j] : (int8_t)-1;  // a failed batch: -1 for every event
+            sl.wait = rc == SGA_OK ? q.wait[j] : 0;
+            sl.seq.store(h + j + 2, std::memory_order_release);
+        }
+        q.head = h + k;
+    }
+    q.combining.store(false, std::memory_order_release);
+    return rc;
+}
+
+int sga_event_poll(sga_engine *e, uint64_t ticket, int8_t *decision, int32_t *wait_ms) {
+    if (!e || !decision) return SGA_EINVAL;
+    sga::EventQueue &q = e->impl.eq;
+    sga::EventQueue::Slot &sl = q.ring[ticket & (sga::EventQueue::kCap - 1)];
+    for (int pass = 0; pass < 2; ++pass) {
+        uint64_t s = sl.seq.load(std::memory_order_acquire);
+        if (s == ticket + 2) {
+            const int8_t d = sl.decision;
+            const int32_t w = sl.wait;
+            if (!sl.seq.compare_exchange_strong(s, ticket + sga::EventQueue::kCap, std::memory_order_acq_rel))
+                return SGA_EINVAL;
+            *decision = d;
+            if (wait_ms) *wait_ms = w;
+            return d < 0 ? SGA_EIO : SGA_OK;
+        }
+        if (s != ticket + 1) return SGA_EINVAL;  // not a live ticket
+        if (pass == 0) (void)event_combine_round(e);
+    }
+    return SGA_EAGAIN;
+}
+
+int sga_event_one(sga_engine *e, uint8_t kind, uint32_t resource, int64_t ts, int32_t acquire, uint8_t flags,
+                  int64_t rt, uint64_t param, const uint64_t *param_values, size_t n_values, int8_t *decision,
+                  int32_t *wait_ms) {
+    if (!e || !decision) return SGA_EINVAL;
+    uint64_t t = 0;
+    int rc = sga_event_submit(e, kind, resource, ts, acquire, flags, rt, param, param_values, n_values, &t);
+    if (rc == SGA_ERANGE)  // more argument words than a queue slot holds: its own batch
+        return sga_submit_events_ex(e, &kind, &resource, &ts, &acquire, &flags, &rt, &param, 1, param_values,
+                                    n_values, decision, wait_ms);
+    if (rc != SGA_OK) return rc;
+    for (int spin = 0;; ++spin) {
+        rc = sga_event_poll(e, t, decision, wait_ms);
         if (rc != SGA_EAGAIN) return rc;
         if (spin > 16) std::this_thread::yield();
     }

@@ -38,7 +38,10 @@ constexpr int kMinW = 1000, kMinInterval = 60000;
 constexpr int kOccupyTimeout = 500;               // OccupyTimeoutProperty
 enum : int8_t { D_PASS = 0, D_BLOCK_FLOW = 1, D_BLOCK_PARAM = 2, D_BLOCK_DEGRADE = 3, D_PASS_WAIT = 4,
                 D_BLOCK_SYSTEM = 5 };
-enum : uint32_t { F_EXIT = 1u << 30, F_ERROR = 1u << 29, F_PARAM = 1u << 28, F_IDX = (1u << 28) - 1 };
+// F_SPECIAL: the event is replayed with its original kind, flags and arguments by the per-resource replay
+// (replay_event): a kind 2 / 3 event, or arguments k_lclassify could not restate as one value
+enum : uint32_t { F_SPECIAL = 1u << 31, F_EXIT = 1u << 30, F_ERROR = 1u << 29, F_PARAM = 1u << 28,
+                  F_IDX = (1u << 28) - 1 };
 constexpr uint32_t kHeavyEvents = 1024;  // per batch: replayed by k_lheavy instead of one k_lflows lane
 #ifndef SGA_WAVE_EVENTS
 #define SGA_WAVE_EVENTS 128
@@ -991,6 +994,31 @@ __device__ __forceinline__ void chain_exit(const Ctx &c, uint32_t r, int64_t t, 
     chain_exit<kLru>(c, r, res_global(c, r, c.st.res[r]), t, rt, count, error, has_param, param, pa, eidx);
 }
 
+// StatisticSlot's BlockException branch for a block thrown by a slot outside the engine (SGA_KIND_BLOCKED,
+// StatisticSlot.java:121-135): the resource's node counts the block (ENTRY_NODE: the caller)
+__device__ __forceinline__ void blocked_event(const Ctx &c, uint32_t r, int64_t t, int a) {
+    node_add(c, c.st.node + (size_t)r * kNodeWords, t, MB_BLOCK, a);
+}
+
+// SGA_KIND_REVOKE: a slot after the engine's checks blocked an entry the engine passed.  StatisticSlot never
+// reached its pass accounting (StatisticSlot.java:77-84 follow fireEntry), only the block branch (:121-135):
+// the pass and the thread are taken back, the block counted, the parameter thread counts released; a breaker
+// this entry moved to HALF_OPEN falls back to OPEN, next retry kept (the probe's whenTerminate hook,
+// AbstractCircuitBreaker.java:117-139, issue 1638) -- the entry is identified by its time, which the revoke
+// carries.  ENTRY_NODE: the caller.
+template <bool kLru = false>
+__device__ void revoke_event(const Ctx &c, uint32_t r, int64_t t, int a, const PArgs &pa, bool hp, const uint64_t &pv,
+                             uint32_t eidx) {
+    int64_t *nd = c.st.node + (size_t)r * kNodeWords;
+    nd[kNodeThreads] -= 1;
+    node_add(c, nd, t, MB_PASS, -(int64_t)a);
+    node_add(c, nd, t, MB_BLOCK, a);
+    param_threads<kLru>(c, r, pa, hp, pv, -1, eidx);
+    CbDev *cbs = c.st.cbs + c.st.res[r].cb_off;
+    for (uint32_t k = 0; k < c.st.res[r].n_cbs; ++k)
+        if (cbs[k].state == 2 && cbs[k].probe_t == t) cbs[k].state = 1;
+}
+
 // ------------------------------------------------------------------ SystemSlot / ENTRY_NODE
 // Constants.ENTRY_NODE is node record nres.  StatisticSlot (StatisticSlot.java:54-137) updates it
 // for inbound (EntryType.IN) entries and their exits.
@@ -1068,7 +1096,8 @@ __global__ __launch_bounds__(kT) void k_lgate(const uint8_t *__restrict__ kind, 
     for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
         const uint8_t fl = flags ? flags[i] : 0;
         if (acquire[i] < 0 || kind[i] > SGA_KIND_REVOKE) g |= kGateBad;
-        if (kind[i] >= SGA_KIND_BLOCKED) g |= kGateSeq;  // blocks by slots outside the engine: arrival order
+        // kind 2 / 3 events and argument lists take the parallel pipeline (their resources are replayed per
+        // resource, in arrival order); only SystemRules couple resources (one lane for the whole chunk)
         if ((fl & SGA_EV_INBOUND) && resource[i] < nres) g |= sys_check ? (kGateIn | kGateSeq) : kGateIn;
         if (fl & SGA_EV_ARGS) {  // the argument vector's word pairs and every list inside npvals
             const uint64_t pv = param_in ? param_in[i] : 0;
@@ -1081,11 +1110,9 @@ __global__ __launch_bounds__(kT) void k_lgate(const uint8_t *__restrict__ kind, 
                     if ((h >> 62) > 2 || ((h >> 62) == ARG_LIST && w + (h & 0xFFFFFFFFu) > npvals)) g |= kGateBad;
                 }
             }
-            g |= kGateSeq;
         } else if ((fl & (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) == (SGA_EV_PARAM_LIST | SGA_EV_HAS_PARAM)) {
             const uint64_t pv = param_in ? param_in[i] : 0;
             if ((pv >> 32) + (pv & 0xFFFFFFFFu) > npvals) g |= kGateBad;
-            g |= kGateSeq;
         }
     }
     g = wave_or_u32(g);
@@ -1140,24 +1167,12 @@ __global__ void k_lseq(FlowState st, int64_t max_rt, SysDev sys, const uint8_t *
             continue;
         }
         if (kind[i] == SGA_KIND_BLOCKED) {  // StatisticSlot's BlockException branch for a block thrown outside the engine
-            node_add(c, st.node + (size_t)r * kNodeWords, t, MB_BLOCK, a);
+            blocked_event(c, r, t, a);
             if (in) node_add(c, entry_node(c), t, MB_BLOCK, a);
             continue;
         }
         if (kind[i] == SGA_KIND_REVOKE) {
-            // a slot after the engine's checks blocked an entry the engine passed: StatisticSlot never reached
-            // its pass accounting (StatisticSlot.java:77-84 follow fireEntry), only the block branch (:121-135)
-            int64_t *nd = st.node + (size_t)r * kNodeWords;
-            nd[kNodeThreads] -= 1;
-            node_add(c, nd, t, MB_PASS, -(int64_t)a);
-            node_add(c, nd, t, MB_BLOCK, a);
-            param_threads<true>(c, r, pa, hp, param_in[i], -1, i);
-            // the whenTerminate hook of fromOpenToHalfOpen (AbstractCircuitBreaker.java:117-139, issue 1638): a
-            // breaker this entry moved to HALF_OPEN sees the block error and falls back to OPEN (next retry kept).
-            // The entry is identified by its time: the revoke carries the entry's timestamp
-            CbDev *cbs = st.cbs + st.res[r].cb_off;
-            for (uint32_t k = 0; k < st.res[r].n_cbs; ++k)
-                if (cbs[k].state == 2 && cbs[k].probe_t == t) cbs[k].state = 1;
+            revoke_event<true>(c, r, t, a, pa, hp, param_in[i], i);
             if (in) {
                 int64_t *e = entry_node(c);
                 e[kNodeThreads] -= 1;
@@ -1233,6 +1248,12 @@ __global__ __launch_bounds__(kEnTile) void k_entry_stats(FlowState st, int64_t m
                     if (flags[i] & SGA_EV_ERROR) atomicAdd(&bs[bk][4], (u64)a);
                     atomicMin(&bmin[bk], (long long)rt_in[i]);
                     atomicAdd(&thr_delta, ~0ull);  // -1
+                } else if (kind[i] == SGA_KIND_BLOCKED) {  // StatisticSlot's block branch on ENTRY_NODE
+                    atomicAdd(&bs[bk][1], (u64)a);
+                } else if (kind[i] == SGA_KIND_REVOKE) {  // the pass and the thread taken back, the block counted
+                    atomicAdd(&bs[bk][0], (u64)(-(int64_t)a));
+                    atomicAdd(&bs[bk][1], (u64)a);
+                    atomicAdd(&thr_delta, ~0ull);
                 } else {
                     const int8_t d = decision[i];
                     if (d == D_PASS) {
@@ -1276,8 +1297,18 @@ __global__ __launch_bounds__(kEnTile) void k_entry_stats(FlowState st, int64_t m
                 if (resource[j] >= st.nres || !(flags[j] & SGA_EV_INBOUND)) continue;
                 const int64_t tj = ts_base + (int64_t)ts_off[j];
                 const int a = (int)((uint32_t)acquire[j] & 0x7FFFFFFFu);
-                if (kind[j] == 1) entry_node_after_exit(c, tj, rt_in[j], a, (flags[j] & SGA_EV_ERROR) != 0);
-                else entry_node_after_entry(c, tj, a, decision[j]);
+                if (kind[j] == 1) {
+                    entry_node_after_exit(c, tj, rt_in[j], a, (flags[j] & SGA_EV_ERROR) != 0);
+                } else if (kind[j] == SGA_KIND_BLOCKED) {
+                    node_add(c, entry_node(c), tj, MB_BLOCK, a);
+                } else if (kind[j] == SGA_KIND_REVOKE) {
+                    int64_t *e = entry_node(c);
+                    e[kNodeThreads] -= 1;
+                    node_add(c, e, tj, MB_PASS, -(int64_t)a);
+                    node_add(c, e, tj, MB_BLOCK, a);
+                } else {
+                    entry_node_after_entry(c, tj, a, decision[j]);
+                }
             }
         }
         if (threadIdx.x == 0) prev_last = ts_base + (int64_t)ts_off[min(base + kEnTile, n) - 1];
@@ -1286,11 +1317,40 @@ __global__ __launch_bounds__(kEnTile) void k_entry_stats(FlowState st, int64_t m
 }
 
 // ------------------------------------------------------------------ classify
-__global__ __launch_bounds__(kT) void k_lclassify(FlowState st, const uint8_t *__restrict__ kind,
+// An argument vector (SGA_EV_ARGS) restated as the one-value form (args = [param] or []) when that decides
+// and counts the same: every parameter rule of the resource reads argument 0 (its index resolved, or fixed at
+// 0), no thread-count map of another index exists (only rules create them), and argument 0 is a scalar or
+// null (a null or absent argument passes every rule and counts no thread: the no-parameter form).  A
+// Collection at 0, or another index, keeps the vector (F_SPECIAL).
+__device__ __forceinline__ bool args_one_value(const FlowState &st, uint32_t r, uint64_t pv,
+                                               const uint64_t *__restrict__ pvals, bool *hp, uint64_t *v) {
+    const ResDev R = st.res[r];
+    for (uint32_t k = 0; k < R.n_prules; ++k) {
+        const ParamRuleDev &p = st.prules[R.prule_off + k];
+        const int32_t idx = p.idx_res != kIdxUnresolved ? p.idx_res : (p.param_idx >= 0 ? p.param_idx : -1);
+        if (idx != 0) return false;
+    }
+    if (st.tmapmask && (st.tmapmask[r] & ~1ull)) return false;
+    const uint32_t na = (uint32_t)pv;
+    if (na == 0) {
+        *hp = false;
+        *v = 0;
+        return true;
+    }
+    const uint64_t h = pvals[pv >> 32];
+    const int k0 = (int)(h >> 62);
+    if (k0 == ARG_LIST) return false;
+    *hp = k0 == ARG_SCALAR;
+    *v = *hp ? pvals[(pv >> 32) + 1] : 0;
+    return true;
+}
+
+__global__ __launch_bounds__(kT) void k_lclassify(FlowState st, FlowScratch sc, const uint8_t *__restrict__ kind,
                                                   const uint32_t *__restrict__ resource,
                                                   const uint32_t *__restrict__ ts_off, int64_t ts_base,
                                                   const int32_t *__restrict__ acquire,
-                                                  const uint8_t *__restrict__ flags, uint32_t n, uint32_t *keys,
+                                                  const uint8_t *__restrict__ flags,
+                                                  const uint64_t *__restrict__ param_in, uint32_t n, uint32_t *keys,
                                                   Payload *pay, int8_t *decision, int32_t *wait_ms) {
     const uint32_t i = blockIdx.x * kT + threadIdx.x;
     if (i >= n) return;
@@ -1301,7 +1361,8 @@ __global__ __launch_bounds__(kT) void k_lclassify(FlowState st, const uint8_t *_
     }
     const uint32_t r = resource[i];
     const uint8_t fl = flags ? flags[i] : 0;
-    const bool ex = kind[i] == 1;
+    const uint8_t kd = kind[i];
+    const bool ex = kd == 1;
     decision[i] = D_PASS;
     wait_ms[i] = 0;
     if (r >= st.nres) {  // unknown resource: no node, no rules (documented)
@@ -1312,9 +1373,31 @@ __global__ __launch_bounds__(kT) void k_lclassify(FlowState st, const uint8_t *_
     keys[i] = r;
     const uint32_t off = ts_off[i];
     const int64_t t = ts_base + (int64_t)off;
-    uint32_t idx = i | (ex ? F_EXIT : 0u) | ((fl & SGA_EV_ERROR) ? F_ERROR : 0u) | ((fl & SGA_EV_HAS_PARAM) ? F_PARAM : 0u);
+    // the parameter the parallel kernels read (ev_param): the event's own, or its argument vector's one value
+    bool hp = (fl & SGA_EV_HAS_PARAM) != 0, kept = false;  // kept: the arguments stay whole (the replay reads them)
+    uint64_t pv = param_in ? param_in[i] : 0;
+    if (fl & SGA_EV_ARGS) {
+        kept = !args_one_value(st, r, pv, sc.pvals, &hp, &pv);
+    } else if (hp && (fl & SGA_EV_PARAM_LIST)) {
+        kept = true;
+    }
+    const bool spec = kept || kd >= SGA_KIND_BLOCKED;
+    // the resource's level this chunk (res_special = epoch << 2 | level, the highest wins): 1 -- kind 2 / 3 events
+    // only, which the per-value segments of a parameter-only resource also take (a revoke is an exit there
+    // that takes its pass back); 2 -- arguments kept whole: the per-resource replay
+    const uint32_t lvl = kept ? 2u : (spec ? 1u : 0u);
+    if (spec && sc.res_special) {
+        const uint32_t mark = (sc.epoch << 2) | lvl;
+        if (sc.res_special[r] < mark) atomicMax(&sc.res_special[r], mark);
+    }
+    if (sc.ev_param) sc.ev_param[i] = pv;
+    // a revoke is an exit (thread counts) that takes its pass back; a block is neither entry nor exit
+    // (its parameter bit: a block outside the engine touches no parameter map)
+    uint32_t idx = i | ((ex || kd == SGA_KIND_REVOKE) ? F_EXIT : 0u) | ((fl & SGA_EV_ERROR) ? F_ERROR : 0u) |
+                   ((hp && kd != SGA_KIND_BLOCKED) ? F_PARAM : 0u) | (spec ? F_SPECIAL : 0u);
     const uint32_t a = (uint32_t)acquire[i] & 0x7FFFFFFFu;
-    pay[i] = Payload{idx, off, a | ((!ex && (fl & SGA_EV_PRIORITIZED)) ? 0x80000000u : 0u), (uint32_t)(t / kSecW)};
+    pay[i] = Payload{idx, off, a | ((!ex && !spec && (fl & SGA_EV_PRIORITIZED)) ? 0x80000000u : 0u),
+                     (uint32_t)(t / kSecW)};
 }
 
 // ------------------------------------------------------------------ runs (segmented scan)
@@ -1600,7 +1683,7 @@ __global__ __launch_bounds__(kT) void k_lexits(const Payload *__restrict__ pay, 
         const uint32_t e = e0 + i;
         const uint64_t qv = sia[sslot(base, e)];
         const uint32_t qidx = (uint32_t)qv, qacq = (uint32_t)(qv >> 32);
-        if (!(qidx & F_EXIT)) continue;
+        if (!(qidx & F_EXIT) || (qidx & F_SPECIAL)) continue;  // a revoke completes nothing (no success, no RT)
         const uint32_t r = srun[sslot(base, e)];
         if (r != cur) {
             flush();
@@ -1642,12 +1725,60 @@ __device__ __forceinline__ bool default_cond(double count, int64_t sum, int32_t 
     return !((double)(int32_t)((uint32_t)cur + (uint32_t)a) > count);
 }
 
+// One event of the per-resource replay in arrival order (lane_run's event-by-event runs, k_llru): the slot
+// chain, or -- F_SPECIAL -- the event's original kind and arguments, as k_lseq takes them (ENTRY_NODE is
+// k_entry_stats').
+template <bool kLru>
+__device__ __forceinline__ void replay_event(const Ctx &c, const FlowScratch &sc, uint32_t res, const Payload &q,
+                                             int64_t ts_base, const int64_t *__restrict__ rt_in,
+                                             const uint64_t *__restrict__ param_in, int8_t *decision,
+                                             int32_t *wait_ms) {
+    const int64_t t = ts_base + (int64_t)q.ts_off;
+    const uint32_t idx = q.idx & F_IDX;
+    const int a = (int)(q.acq_prio & 0x7FFFFFFFu);
+    if (q.idx & F_SPECIAL) {
+        const uint8_t kd = sc.in_kind[idx];
+        const uint8_t fl = sc.in_flags ? sc.in_flags[idx] : 0;
+        const uint64_t pv = sc.in_param ? sc.in_param[idx] : 0;
+        const bool hp = (fl & SGA_EV_HAS_PARAM) != 0;
+        PArgs pa{nullptr, 0};
+        if ((fl & SGA_EV_ARGS) && sc.pvals) {
+            pa.args = sc.pvals + (pv >> 32);
+            pa.pvals = sc.pvals;
+            pa.nargs = (uint32_t)pv;
+        } else if (hp && (fl & SGA_EV_PARAM_LIST) && sc.pvals) {
+            pa = PArgs{sc.pvals + (pv >> 32), (uint32_t)pv};
+        }
+        if (kd == SGA_KIND_BLOCKED) {
+            blocked_event(c, res, t, a);
+        } else if (kd == SGA_KIND_REVOKE) {
+            revoke_event<kLru>(c, res, t, a, pa, hp, pv, idx);
+        } else if (kd == 1) {
+            chain_exit<kLru>(c, res, t, rt_in[idx], a, (fl & SGA_EV_ERROR) != 0, hp, pv, pa, idx);
+        } else {
+            int64_t w = 0;
+            decision[idx] = chain_entry<kLru>(c, res, t, a, (fl & SGA_EV_PRIORITIZED) != 0, hp, pv, &w, pa, idx);
+            wait_ms[idx] = (int32_t)w;
+        }
+        return;
+    }
+    const bool hp = (q.idx & F_PARAM) != 0;
+    const uint64_t pv = hp ? param_in[idx] : 0;
+    if (q.idx & F_EXIT) {
+        chain_exit<kLru>(c, res, t, rt_in[idx], a, (q.idx & F_ERROR) != 0, hp, pv, PArgs{nullptr, 0}, idx);
+    } else {
+        int64_t w = 0;
+        decision[idx] = chain_entry<kLru>(c, res, t, a, (q.acq_prio >> 31) != 0, hp, pv, &w, PArgs{nullptr, 0}, idx);
+        wait_ms[idx] = (int32_t)w;
+    }
+}
+
 // One run of a resource decided by one lane (k_lflows; k_lwave's lane 0 for runs it cannot split):
 // RateLimiter pacing in registers, the per-event slot chain, or the closed form (RUN_FAST: k_lresults
 // writes the decisions from run_f).
 __device__ __noinline__ void lane_run(const Ctx &c, int64_t max_rt, FlowScratch &sc, const Payload *__restrict__ pay,
                          int64_t ts_base, const int64_t *__restrict__ rt_in, const uint64_t *__restrict__ param_in,
-                         int8_t *decision, int32_t *wait_ms, uint32_t r) {
+                         int8_t *decision, int32_t *wait_ms, uint32_t r, bool special = false) {
     const FlowState &st = c.st;
     const uint32_t res = sc.run_slot[r];
     const ResDev R = st.res[res];
@@ -1656,6 +1787,11 @@ __device__ __noinline__ void lane_run(const Ctx &c, int64_t max_rt, FlowScratch 
     const uint32_t nent = sc.run_nent[r];
     const int32_t a = sc.run_amin[r];
     const int64_t t0 = ts_base + (int64_t)sc.run_t0off[r];
+    if (special) {  // a resource with F_SPECIAL events this chunk: every run event by event
+        for (uint32_t j = j0; j < j1; ++j) replay_event<false>(c, sc, res, pay[j], ts_base, rt_in, param_in, decision, wait_ms);
+        sc.run_mode[r] = RUN_DONE;
+        return;
+    }
     if (nent == 0 && (R.fast & 5u)) {
         // An exit-only run of a single-rule resource (no parameter rules, no breakers: an exit only
         // adds to the node).  Its exits share one second bucket and one minute bucket, so each
@@ -1799,22 +1935,7 @@ __device__ __noinline__ void lane_run(const Ctx &c, int64_t max_rt, FlowScratch 
         if (s0 + (int64_t)nent * a + a >= (int64_t)INT32_MAX) fast = false;
     }
     if (!fast) {
-        for (uint32_t j = j0; j < j1; ++j) {
-            const Payload q = pay[j];
-            const int64_t t = ts_base + (int64_t)q.ts_off;
-            const uint32_t idx = q.idx & F_IDX;
-            const bool hp = (q.idx & F_PARAM) != 0;
-            const uint64_t pv = hp ? param_in[idx] : 0;
-            if (q.idx & F_EXIT) {
-                chain_exit(c, res, t, rt_in[idx], (int)(q.acq_prio & 0x7FFFFFFFu), (q.idx & F_ERROR) != 0, hp, pv,
-                           PArgs{nullptr, 0}, idx);
-            } else {
-                int64_t w = 0;
-                decision[idx] = chain_entry(c, res, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
-                                            hp, pv, &w, PArgs{nullptr, 0}, idx);
-                wait_ms[idx] = (int32_t)w;
-            }
-        }
+        for (uint32_t j = j0; j < j1; ++j) replay_event<false>(c, sc, res, pay[j], ts_base, rt_in, param_in, decision, wait_ms);
         sc.run_mode[r] = RUN_DONE;
         return;
     }
@@ -1895,10 +2016,13 @@ __device__ bool pseg_take(const FlowState &st, const FlowScratch &sc, const Payl
         return p.idx_res == 0;
     }
     uint32_t j = jb;
-    bool pexit = false;  // a parameter exit before the first entry
+    bool pexit = false;  // a parameter exit (or revoke) before the first entry
     for (; j < je; ++j) {
         const uint32_t f = pay[j].idx;
-        if (!(f & F_EXIT)) break;
+        if (!(f & F_EXIT)) {
+            if (f & F_SPECIAL) continue;  // a block outside the engine checks nothing (not the first entry)
+            break;
+        }
         pexit |= (f & F_PARAM) != 0;
     }
     int32_t idx = p.idx_res;
@@ -1981,10 +2105,31 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
         {  // a long event-by-event replay goes to k_lheavy (its state in LDS)
             const uint32_t res = sc.run_slot[r0];
             const uint32_t nev = sc.run_end[r1 - 1] - sc.run_start[r0];
+            // events replayed with their original kind / arguments (F_SPECIAL) this chunk: this resource's events
+            // in arrival order on this lane (k_llru in LRU mode); the other resources keep every parallel form
+            const uint32_t rs = sc.res_special ? sc.res_special[res] : 0u;
+            const uint32_t special = (rs >> 2) == sc.epoch ? (rs & 3u) : 0u;  // level (k_lclassify)
             if (st.lru_res && st.lru_res[res]) {  // a CacheMap in LRU mode: arrival order, one lane (k_llru)
                 // parameter-only: the chunked replay (k_llru_ps, SGA_LRU_PS=0 turns it off: an A/B knob)
-                const bool ps = st.lru_ps && lru_ps_take(st, sc, pay, res, r0, r1);
+                const bool ps = !special && st.lru_ps && lru_ps_take(st, sc, pay, res, r0, r1);
                 sc.lru[atomicAdd(&sc.counters[10], 1u)] = fl | (ps ? 0x80000000u : 0u);
+                continue;
+            }
+            if (special) {
+                // kind 2 / 3 events of a parameter-only resource: its per-value segments (the revokes are exits
+                // there, the node statistics in aggregate); anything else event by event on this lane
+                if (special == 1 && sc.pseg && pseg_take(st, sc, pay, res, r0, r1)) {
+                    for (uint32_t r = r0; r < r1; ++r) {
+                        sc.run_mode[r] = RUN_PSEG;
+                        sc.run_pa[r] = 0;
+                        sc.run_ba[r] = 0;
+                        sc.run_np[r] = 0;
+                    }
+                    sc.pseg[atomicAdd(&sc.counters[11], 1u)] = fl;
+                    continue;
+                }
+                for (uint32_t r = r0; r < r1; ++r)
+                    lane_run(c, max_rt, sc, pay, ts_base, rt_in, param_in, decision, wait_ms, r, true);
                 continue;
             }
             int cbk = 0;
@@ -3209,22 +3354,9 @@ __global__ __launch_bounds__(64) void k_llru(FlowState st, int64_t max_rt, FlowS
         const uint32_t res = sc.run_slot[r0];
         for (uint32_t j = sc.run_start[r0]; j < sc.run_end[r1 - 1]; ++j) {
             const Payload q = pay[j];
-            const int64_t t = ts_base + (int64_t)q.ts_off;
-            const uint32_t idx = q.idx & F_IDX;
-            const bool hp = (q.idx & F_PARAM) != 0;
-            const uint64_t pv = hp ? param_in[idx] : 0;
             const uint64_t tp = g_lru_prof_on ? wall_clock64() : 0;
-            if (q.idx & F_EXIT) {
-                chain_exit<true>(c, res, t, rt_in[idx], (int)(q.acq_prio & 0x7FFFFFFFu), (q.idx & F_ERROR) != 0, hp,
-                                 pv, PArgs{nullptr, 0}, idx);
-                if (tp) atomicAdd(&g_lru_prof[7], (unsigned long long)(wall_clock64() - tp));
-            } else {
-                int64_t w = 0;
-                decision[idx] = chain_entry<true>(c, res, t, (int)(q.acq_prio & 0x7FFFFFFFu), (q.acq_prio >> 31) != 0,
-                                                  hp, pv, &w, PArgs{nullptr, 0}, idx);
-                wait_ms[idx] = (int32_t)w;
-                if (tp) atomicAdd(&g_lru_prof[6], (unsigned long long)(wall_clock64() - tp));
-            }
+            replay_event<true>(c, sc, res, q, ts_base, rt_in, param_in, decision, wait_ms);
+            if (tp) atomicAdd(&g_lru_prof[(q.idx & F_EXIT) ? 7 : 6], (unsigned long long)(wall_clock64() - tp));
         }
         for (uint32_t r = r0; r < r1; ++r) sc.run_mode[r] = RUN_DONE;
     }
@@ -4628,7 +4760,8 @@ __global__ __launch_bounds__(kT) void k_pseg_runs(FlowState st, FlowScratch sc, 
         const uint32_t r = srun[sslot(base, e)];
         if (sc.run_mode[r] != RUN_PSEG) continue;
         const uint64_t qv = sia[sslot(base, e)];
-        if ((uint32_t)qv & F_EXIT) continue;
+        const uint32_t qf = (uint32_t)qv;
+        if ((qf & F_EXIT) && !(qf & F_SPECIAL)) continue;
         if (r != cur) {
             flush();
             cur = r;
@@ -4636,7 +4769,12 @@ __global__ __launch_bounds__(kT) void k_pseg_runs(FlowState st, FlowScratch sc, 
             np = 0;
         }
         const int64_t a = (int64_t)((uint32_t)(qv >> 32) & 0x7FFFFFFFu);
-        const int8_t d = decision[(uint32_t)qv & F_IDX];
+        if (qf & F_SPECIAL) {  // a revoke takes its pass back and counts a block; a block outside the engine counts
+            if (qf & F_EXIT) pa -= a;
+            ba += a;
+            continue;
+        }
+        const int8_t d = decision[qf & F_IDX];
         if (d == D_PASS || d == D_PASS_WAIT) {
             pa += a;
             ++np;
@@ -5928,7 +6066,8 @@ int FlowEngine::ensure_scratch() {
                        al(64) + 2 * al(hist * 4) + al(scan_partials_needed(hist) * 4 + 64) + al(cap * 4) +
                        2 * al(cap * 8) + al(cap * 4) + 2 * al(cap * 8) + al(cap * 4) + al(kRadixGhistWords * 4) + al(64) + al(cap * 4) + al((cap / 256 + 16) * 8) + al(cap * 8) +
                        al(cap * 8) +  // run_asum
-                       al((cap / 64 + 2) * sizeof(WinSum)) + al((cap / 64 + 2) * 8);  // wsum, wstate
+                       al((cap / 64 + 2) * sizeof(WinSum)) + al((cap / 64 + 2) * 8) +  // wsum, wstate
+                       al(cap * 8);  // ev_param
         d_scratch.alloc(bytes);
         char *p = (char *)d_scratch.p;
         auto take = [&](size_t b) {
@@ -5983,6 +6122,7 @@ int FlowEngine::ensure_scratch() {
         sc.radix.err = (uint32_t *)take(64);
         sc.wsum = (WinSum *)take((cap / 64 + 2) * sizeof(WinSum));
         sc.wstate = (int64_t *)take((cap / 64 + 2) * 8);
+        sc.ev_param = (uint64_t *)take(cap * 8);
         sc.cap = cap;
         scratch_cap = cap;
         d_kind.alloc(cap);
@@ -5996,6 +6136,29 @@ int FlowEngine::ensure_scratch() {
         d_wait.alloc(cap);
     }
     return 0;
+}
+
+// The chunk's view of the scratch for F_SPECIAL events: a new epoch marks their resources (res_special), the
+// original kind / flags / parameters / value lists are what the per-resource replay reads for them.
+FlowScratch FlowEngine::special_scratch(const FlowScratch &base, const uint8_t *d_kind_in, const uint8_t *d_flags_in,
+                                        const uint64_t *d_param_in, const uint64_t *d_pvals) {
+    if (d_res_special.n < (size_t)nres + 1) {
+        d_res_special.alloc((size_t)nres + 1);
+        SGA_HIP_CHECK(hipMemset(d_res_special.p, 0, d_res_special.bytes()));
+        epoch = 0;
+    }
+    if (++epoch >= (1u << 30)) {  // wrapped (res_special holds epoch << 2 | level): no resource may hold the new one
+        SGA_HIP_CHECK(hipMemsetAsync(d_res_special.p, 0, d_res_special.bytes(), stream));
+        epoch = 1;
+    }
+    FlowScratch f = base;
+    f.res_special = d_res_special.p;
+    f.epoch = epoch;
+    f.in_kind = d_kind_in;
+    f.in_flags = d_flags_in;
+    f.in_param = d_param_in;
+    f.pvals = d_pvals;
+    return f;
 }
 
 int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int64_t *ts, const int32_t *acquire,
@@ -6076,11 +6239,11 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         bool has_in = false, has_list = false;
         for (size_t i = 0; flags && i < m && !has_in; ++i) has_in = (flags[b + i] & SGA_EV_INBOUND) && resource[b + i] < nres;
         for (size_t i = 0; any_list && i < m && !has_list; ++i) has_list = is_list(b + i);
-        for (size_t i = 0; i < m; ++i) {
+        for (size_t i = 0; i < m; ++i)
             if (kind[b + i] > SGA_KIND_REVOKE) return SGA_EINVAL;
-            has_list |= kind[b + i] >= SGA_KIND_BLOCKED;  // blocks outside the engine: arrival order
-        }
-        if ((has_in && sys.check) || has_list) {  // SystemSlot / collection arguments: one lane in arrival order
+        // kind 2 / 3 events and argument lists stay on the parallel pipeline (their resources replay per resource,
+        // F_SPECIAL); SystemRules read ENTRY_NODE across resources: one lane in arrival order
+        if (has_in && sys.check) {
             hipLaunchKernelGGL(k_lseq, dim3(1), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sys, d_kind.p,
                                d_resid.p, d_ts.p, lo, d_acq.p, d_flags.p, d_rt.p, d_param.p, (uint32_t)m, d_dec.p,
                                d_wait.p, has_list ? d_pvals.p : nullptr);
@@ -6096,8 +6259,11 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
             seq += m;
             continue;
         }
-        hipLaunchKernelGGL(k_lclassify, dim3(nb), dim3(kT), 0, stream, st, d_kind.p, d_resid.p, d_ts.p, lo, d_acq.p,
-                           d_flags.p, (uint32_t)m, sc.keys[0], sc.pay[0], d_dec.p, d_wait.p);
+        FlowScratch fsc = special_scratch(sc, d_kind.p, flags ? d_flags.p : nullptr, param ? d_param.p : nullptr,
+                                          has_list ? d_pvals.p : nullptr);
+        const uint64_t *evp = fsc.ev_param;
+        hipLaunchKernelGGL(k_lclassify, dim3(nb), dim3(kT), 0, stream, st, fsc, d_kind.p, d_resid.p, d_ts.p, lo, d_acq.p,
+                           d_flags.p, param ? d_param.p : nullptr, (uint32_t)m, sc.keys[0], sc.pay[0], d_dec.p, d_wait.p);
         const int np = radix_sort_pairs(sc.keys[0], sc.pay[0], sc.keys[1], sc.pay[1], m, bits, sc.radix, stream);
         const uint32_t *keys = sc.keys[np & 1];
         const Payload *pay = sc.pay[np & 1];
@@ -6110,29 +6276,29 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
                            (const LAgg *)sc.tile_carry, sc);
         hipLaunchKernelGGL(k_lexits, dim3(ntiles), dim3(kT), 0, stream, pay, d_rt.p, sc);
         const uint32_t fthreads = (uint32_t)std::min<size_t>(m, nres);
-        FlowScratch fsc = sc;
-        if ((h_prules.empty() && h_cbs.empty()) || !pseg_on()) fsc.pseg = nullptr;
+        FlowScratch fsc_p = fsc;  // the flows and the per-value segments (pseg off: null)
+        if ((h_prules.empty() && h_cbs.empty()) || !pseg_on()) fsc_p.pseg = nullptr;
         hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, stream, st,
-                           (int64_t)cfg.statistic_max_rt, fsc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p);
-        launch_pseg(st, fsc, pay, keys, lo, d_rt.p, d_param.p, d_dec.p, d_wait.p, (uint32_t)m, stream);
+                           (int64_t)cfg.statistic_max_rt, fsc_p, pay, keys, lo, d_rt.p, evp, d_dec.p, d_wait.p);
+        launch_pseg(st, fsc_p, pay, keys, lo, d_rt.p, evp, d_dec.p, d_wait.p, (uint32_t)m, stream);
         if (st.lru_res) {
-            hipLaunchKernelGGL(k_llru, dim3(64), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo,
-                               d_rt.p, d_param.p, d_dec.p, d_wait.p);
-            hipLaunchKernelGGL(k_llru_ps, dim3(256), dim3(128), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo,
-                               d_param.p, d_dec.p, d_wait.p);
+            hipLaunchKernelGGL(k_llru, dim3(64), dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, fsc, pay, lo,
+                               d_rt.p, evp, d_dec.p, d_wait.p);
+            hipLaunchKernelGGL(k_llru_ps, dim3(256), dim3(128), 0, stream, st, (int64_t)cfg.statistic_max_rt, fsc, pay, lo,
+                               evp, d_dec.p, d_wait.p);
         }
-        hipLaunchKernelGGL(k_lwsum, dim3((unsigned)((m / 64 + 3) / 4 + 1)), dim3(256), 0, stream, st, sc, pay);
+        hipLaunchKernelGGL(k_lwsum, dim3((unsigned)((m / 64 + 3) / 4 + 1)), dim3(256), 0, stream, st, fsc, pay);
         for (int rl = 0; rl < 2; ++rl)
             hipLaunchKernelGGL(rl ? k_lwave<1> : k_lwave<0>,
                                dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (uint32_t)(m / 4096)))),
-                               dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
+                               dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, fsc, pay, lo, d_rt.p, evp,
                                d_dec.p, d_wait.p, lwave_prof());
         print_lwave_prof(stream);
         hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, (uint32_t)(m / kHeavyEvents)))),
-                           dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, sc, pay, lo, d_rt.p, d_param.p,
+                           dim3(64), 0, stream, st, (int64_t)cfg.statistic_max_rt, fsc, pay, lo, d_rt.p, evp,
                            d_dec.p, d_wait.p, heavy_prof());
         if (heavy_prof()) print_heavy_prof();
-        hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, stream, st, sc, pay, d_dec.p, d_wait.p);
+        hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, stream, st, fsc, pay, d_dec.p, d_wait.p);
         if (has_in)  // ENTRY_NODE statistics of the inbound events
             hipLaunchKernelGGL(k_entry_stats, dim3(1), dim3(kEnTile), 0, stream, st, (int64_t)cfg.statistic_max_rt,
                                d_kind.p, d_resid.p, d_ts.p, lo, d_acq.p, d_flags.p, d_rt.p, d_dec.p, (uint32_t)m);
@@ -6223,10 +6389,11 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
     lru_prepare(d_kind_in, d_resource, flags_p, param_p, d_param_values, m, s);  // CacheMap capacity
     FlowState st = state();
     st.gate = d_gate.p;
-    FlowScratch gsc = sc;
+    FlowScratch gsc = special_scratch(sc, d_kind_in, flags_p, param_p, d_param_values);
     gsc.gate = d_gate.p;
-    hipLaunchKernelGGL(k_lclassify, dim3(nb), dim3(kT), 0, s, st, d_kind_in, d_resource, d_ts_off, ts_base, d_acquire,
-                       flags_p, m, gsc.keys[0], gsc.pay[0], d_decision, wait_p);
+    hipLaunchKernelGGL(k_lclassify, dim3(nb), dim3(kT), 0, s, st, gsc, d_kind_in, d_resource, d_ts_off, ts_base, d_acquire,
+                       flags_p, param_p, m, gsc.keys[0], gsc.pay[0], d_decision, wait_p);
+    const uint64_t *evp = gsc.ev_param;  // what the parallel kernels read as the event's parameter
     const int np = radix_sort_pairs(gsc.keys[0], gsc.pay[0], gsc.keys[1], gsc.pay[1], m, bits, gsc.radix, s);
     const uint32_t *keys = gsc.keys[np & 1];
     const Payload *pay = gsc.pay[np & 1];
@@ -6241,29 +6408,28 @@ int FlowEngine::submit_device(const uint8_t *d_kind_in, const uint32_t *d_resour
     const uint32_t fthreads = std::min<uint32_t>(m, nres);
     if ((h_prules.empty() && h_cbs.empty()) || !pseg_on()) gsc.pseg = nullptr;
     hipLaunchKernelGGL(k_lflows, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc,
-                       pay, keys, ts_base, rt_p, param_p, d_decision, wait_p);
-    launch_pseg(st, gsc, pay, keys, ts_base, rt_p, param_p, d_decision, wait_p, m, s);
+                       pay, keys, ts_base, rt_p, evp, d_decision, wait_p);
+    launch_pseg(st, gsc, pay, keys, ts_base, rt_p, evp, d_decision, wait_p, m, s);
     if (st.lru_res) {
         hipLaunchKernelGGL(k_llru, dim3(64), dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p,
-                           param_p, d_decision, wait_p);
+                           evp, d_decision, wait_p);
         hipLaunchKernelGGL(k_llru_ps, dim3(256), dim3(128), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base,
-                           param_p, d_decision, wait_p);
+                           evp, d_decision, wait_p);
     }
     hipLaunchKernelGGL(k_lwsum, dim3((m / 64 + 3) / 4 + 1), dim3(256), 0, s, st, gsc, pay);
     for (int rl = 0; rl < 2; ++rl)
         hipLaunchKernelGGL(rl ? k_lwave<1> : k_lwave<0>, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, m / 4096))),
-                           dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision,
+                           dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, evp, d_decision,
                            wait_p, lwave_prof());
     print_lwave_prof(s);
     hipLaunchKernelGGL(k_lheavy, dim3(std::max<uint32_t>(1, std::min<uint32_t>(1024, m / kHeavyEvents))), dim3(64), 0, s,
-                       st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, param_p, d_decision, wait_p,
+                       st, (int64_t)cfg.statistic_max_rt, gsc, pay, ts_base, rt_p, evp, d_decision, wait_p,
                        heavy_prof());
         if (heavy_prof()) print_heavy_prof();
     hipLaunchKernelGGL(k_lresults, dim3(nb), dim3(kT), 0, s, st, gsc, pay, d_decision, wait_p);
     hipLaunchKernelGGL(k_entry_stats, dim3(1), dim3(kEnTile), 0, s, st, (int64_t)cfg.statistic_max_rt, d_kind_in,
                        d_resource, d_ts_off, ts_base, d_acquire, flags_p, rt_p, d_decision, m);
-    // arrival-order chunks (system rules, collection / argument vectors, kind 2 blocks): k_lseq acts only
-    // when the gate says so
+    // arrival-order chunks (inbound events under system rules): k_lseq acts only when the gate says so
     hipLaunchKernelGGL(k_lseq, dim3(1), dim3(64), 0, s, st, (int64_t)cfg.statistic_max_rt, sys, d_kind_in,
                        d_resource, d_ts_off, ts_base, d_acquire, flags_p, rt_p, param_p, m, d_decision, wait_p,
                        d_param_values);

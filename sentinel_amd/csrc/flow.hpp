@@ -214,6 +214,15 @@ struct FlowScratch {
     RadixScratch radix;
     size_t cap = 0;
     const uint32_t *gate = nullptr;  // as FlowState::gate
+    // Events the slot chain replays with their original arguments (F_SPECIAL: kind 2 / 3 events, argument
+    // vectors and Collection arguments k_lclassify could not restate as one value): their resources are
+    // marked res_special[r] == epoch for this chunk and go to the per-resource replay.  ev_param: every
+    // event's parameter after that restatement (what the parallel kernels read as param_in).
+    uint64_t *ev_param = nullptr;
+    uint32_t *res_special = nullptr;
+    uint32_t epoch = 0;
+    const uint8_t *in_kind = nullptr, *in_flags = nullptr;
+    const uint64_t *in_param = nullptr, *pvals = nullptr;
 };
 
 void print_heavy_prof();  // SGA_HEAVY_PROF=1 diagnostics (flow.hip)
@@ -233,6 +242,8 @@ struct FlowEngine {
     DevBuf<uint32_t> d_overflow;
     DevBuf<uint32_t> d_keycount;
     DevBuf<uint64_t> d_tmapmask;  // FlowState::tmapmask
+    DevBuf<uint32_t> d_res_special;  // FlowScratch::res_special (per resource, the chunk epoch that marked it)
+    uint32_t epoch = 0;
     // CacheMap capacity (FlowState: pstamp .. seq_base)
     DevBuf<uint64_t> d_pstamp, d_tstamp, d_pq, d_tq;
     DevBuf<uint32_t> d_psize, d_pcap, d_pres, d_pnew, d_tbase, d_tres, d_tsize, d_tnew, d_lru_ctl, d_lru_list;
@@ -306,6 +317,8 @@ struct FlowEngine {
     int submit(const uint8_t *kind, const uint32_t *resource, const int64_t *ts, const int32_t *acquire,
                const uint8_t *flags, const int64_t *rt, const uint64_t *param, size_t n, int8_t *decision,
                int32_t *wait_ms, const uint64_t *pvals = nullptr, size_t npvals = 0);
+    FlowScratch special_scratch(const FlowScratch &base, const uint8_t *d_kind_in, const uint8_t *d_flags_in,
+                                const uint64_t *d_param_in, const uint64_t *d_pvals);
     DevBuf<uint64_t> d_pvals;  // values of Collection / array arguments (SGA_EV_PARAM_LIST)
     // the same over device buffers, asynchronous on s: one chunk of n <= max_batch events
     int submit_device(const uint8_t *d_kind, const uint32_t *d_resource, int64_t ts_base, const uint32_t *d_ts_off,

@@ -232,6 +232,38 @@ class LocalSentinel:
         check(rc, self.engine.handle, "submitEvents")
         return dec, wait
 
+    # ---- one event at a time through the coalescing queue (sga_event_submit / sga_event_poll): what a
+    # synchronous SphU.entry / Entry.exit of one application thread calls; concurrent callers share a batch
+    def event_submit(self, kind, resource, ts, acquire, flags=0, rt=0, param=0, param_values=None) -> int:
+        """Enqueue one event (kind, flags, param as in submit; param_values: this event's argument words only).
+        Returns a ticket for event_poll."""
+        pv = None if param_values is None else np.ascontiguousarray(param_values, dtype=np.uint64)
+        t = C.c_uint64()
+        rc = _lib.load().sga_event_submit(self.engine.handle, int(kind), int(resource), int(ts), int(acquire),
+                                          int(flags), int(rt), int(param), pv.ctypes.data if pv is not None else None,
+                                          0 if pv is None else len(pv), C.byref(t))
+        check(rc, self.engine.handle, "eventSubmit")
+        return int(t.value)
+
+    def event_poll(self, ticket):
+        """(decision, wait_ms) once the ticket's event is decided (each ticket answers once), else None."""
+        d, w = C.c_int8(), C.c_int32()
+        rc = _lib.load().sga_event_poll(self.engine.handle, int(ticket), C.byref(d), C.byref(w))
+        if rc == -11:  # SGA_EAGAIN
+            return None
+        check(rc, self.engine.handle, "eventPoll")
+        return int(d.value), int(w.value)
+
+    def event_one(self, kind, resource, ts, acquire, flags=0, rt=0, param=0, param_values=None):
+        """event_submit + event_poll until decided: (decision, wait_ms)."""
+        pv = None if param_values is None else np.ascontiguousarray(param_values, dtype=np.uint64)
+        d, w = C.c_int8(), C.c_int32()
+        rc = _lib.load().sga_event_one(self.engine.handle, int(kind), int(resource), int(ts), int(acquire), int(flags),
+                                       int(rt), int(param), pv.ctypes.data if pv is not None else None,
+                                       0 if pv is None else len(pv), C.byref(d), C.byref(w))
+        check(rc, self.engine.handle, "eventOne")
+        return int(d.value), int(w.value)
+
     def submit_device(self, kind, resource, ts_base, ts_off, acquire, flags=None, rt=None, param=None,
                       param_values=None, decision=None, wait=None, stream=None):
         """submit over device tensors (torch, on the engine's GPU), asynchronous on `stream` (torch stream or

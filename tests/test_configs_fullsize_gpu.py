@@ -236,3 +236,53 @@ def test_c5a_rls_100k_descriptors():
     assert blocked.any() and (~blocked).any()
     L.orc_cluster_free(oh)
     eng.close()
+
+
+def test_c4args_vectors_blocks_revokes_full_batch():
+    """bench.py --config c4args at its benched size (2^22 entries): C4 pinned with 5 % whole argument vectors
+    (SGA_EV_ARGS, the exits the same), 0.1 % blocks by a slot before the engine (kind 2) and 0.2 % of the passed
+    entries revoked (kind 3 at the entry's time).  None of them sends the chunk to the one-lane replay: the vectors
+    are restated as their one value, the blocks and revokes join the per-value segments (ParamFlowChecker.java
+    :48-130, StatisticSlot.java:121-135).  Every decision and wait, the metric rows and the hottest nodes equal
+    the oracle's replay."""
+    import bench_local as bl
+    bl.SHARD = (0, 1)
+    rng = np.random.default_rng(104)
+    cfg = bl._cfg_c4args(rng)
+    b = cfg["batch"]
+    n_res, param = cfg["n_res"], cfg["param"]
+    ent = {"kind": b.kind, "resource": b.res, "ts": b.ts, "acquire": b.acq, "flags": b.flags,
+           "rt": np.zeros(b.n, np.int64), "param": b.param, "param_values": b.pvals}
+    ent = {k: np.ascontiguousarray(v) for k, v in ent.items()}
+    orc = lt.Oracle(n_res, [], param)
+    exp_d, exp_w = orc.replay(ent)
+    eng, s = _local(n_res, param=param, max_batch=b.n)
+    d, w = s.submit(ent["kind"], ent["resource"], ent["ts"], ent["acquire"], ent["flags"], ent["rt"], ent["param"],
+                    ent["param_values"])
+    bad = np.nonzero((d != exp_d) | (w != exp_w))[0]
+    assert len(bad) == 0, (f"{len(bad)} of {b.n} entries differ; first at {bad[0]}: res={b.res[bad[0]]} "
+                           f"kind={b.kind[bad[0]]} flags={b.flags[bad[0]]} gpu=({d[bad[0]]},{w[bad[0]]}) "
+                           f"oracle=({exp_d[bad[0]]},{exp_w[bad[0]]})")
+    passed = ((exp_d == 0) | (exp_d == 4)) & (b.kind != 2)
+    k = np.nonzero(passed[b.exit_of])[0]  # exits (and revokes) in time order, of the entries that passed
+    e = b.exit_of[k]
+    ex = {"kind": b.exit_kind[k], "resource": b.res[e], "ts": b.exit_ts[k], "acquire": b.acq[e],
+          "flags": b.exit_flags[k], "rt": b.exit_rt[k], "param": b.param[e], "param_values": b.pvals}
+    ex = {kk: np.ascontiguousarray(v) for kk, v in ex.items()}
+    assert (ex["kind"] == 3).sum() > 1000 and (b.kind == 2).sum() > 1000 and (b.flags & 32).any()
+    exp_xd, _ = orc.replay(ex)
+    xd, _ = s.submit(ex["kind"], ex["resource"], ex["ts"], ex["acquire"], ex["flags"], ex["rt"], ex["param"],
+                     ex["param_values"])
+    assert (xd == exp_xd).all()
+    now = int(max(b.ts.max(), ex["ts"].max())) + 1
+    got = [(m.timestamp, s.resource_id(m.resource), m.pass_qps, m.block_qps, m.success_qps, m.exception_qps, m.rt,
+            m.occupied_pass_qps) for m in s.metrics(now, cap=1 << 20)]
+    assert got == orc.metrics(now, cap=1 << 20)
+    hot = np.argsort(-np.bincount(b.res.astype(np.int64), minlength=n_res))[:64]
+    for rid in hot:
+        v = s.node(int(rid), now)
+        assert [getattr(v, g) for g in lt.NODE_GETTERS] == orc.node(int(rid), now), int(rid)
+    ent_d = exp_d[b.kind == 0]
+    assert (ent_d == 0).any() and (ent_d == 2).any()
+    orc.close()
+    eng.close()

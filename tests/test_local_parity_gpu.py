@@ -520,3 +520,75 @@ def test_collection_and_array_parameters():
     assert (d[lst] == 2).any() and (d[lst] == 0).any()
     orc.close()
     eng.close()
+
+
+def test_event_queue_threads_equal_ticket_order():
+    """sga_event_submit / sga_event_poll from 8 threads at once (SphU.entry / Entry.exit from application threads,
+    CtSph.java:117-168): each thread enters, waits for its decision, then exits what passed, with argument
+    vectors, blocks outside the engine and revokes among them.  Every event is decided once, and the decisions,
+    waits and node views equal the oracle replaying all events one by one in ticket order."""
+    import threading
+    n_res = 12
+    flow = [{"resource": r, "count": 8.0, **({"grade": 0, "count": 3} if r % 4 == 1 else {})} for r in range(0, n_res, 2)]
+    param = [{"resource": r, "count": 4.0, "param_idx": 0} for r in range(1, n_res, 3)]
+    degrade = [{"resource": 3, "grade": 2, "count": 3, "min_request_amount": 3, "time_window": 1}]
+    eng, s = _sentinel(n_res, 1 << 12)
+    _load(s, flow, param, degrade)
+    n_thr, per = 8, 300
+    got = [[] for _ in range(n_thr)]
+
+    def worker(k):
+        r = np.random.default_rng(500 + k)
+        for i in range(per):
+            res = int(r.integers(0, n_res))
+            now = T0 + 3 * i + int(r.integers(0, 3))
+            acq = int(r.integers(1, 3))
+            words, fl, pv = None, 8 if r.random() < 0.3 else 0, 0
+            u = r.random()
+            if u < 0.2:  # a whole argument vector: (scalar v, scalar x) or (list [v, w])
+                v = int(r.integers(0, 6))
+                args = [v, int(r.integers(0, 100))] if r.random() < 0.7 else [[v, int(r.integers(0, 6))]]
+                lw = []
+                pv = lt.encode_args(args, lw)
+                words, fl = np.array(lw, np.uint64), fl | 32
+            elif u < 0.6:
+                pv, fl = int(r.integers(0, 6)), fl | 4
+            kind = 2 if r.random() < 0.03 else 0
+            t = s.event_submit(kind, res, now, acq, fl, 0, pv, words)
+            d = None
+            while d is None:
+                d = s.event_poll(t)
+            got[k].append((t, kind, res, now, acq, fl, 0, pv, words, d))
+            if kind == 0 and d[0] in (0, 4):  # passed: exit later (or revoked by a later slot)
+                rev = r.random() < 0.1
+                xt = now if rev else now + int(r.integers(1, 20))
+                xfl = (fl & (4 | 8 | 32)) | (2 if (not rev and r.random() < 0.2) else 0)
+                xrt = 0 if rev else xt - now
+                t2 = s.event_submit(3 if rev else 1, res, xt, acq, xfl, xrt, pv, words)
+                d2 = None
+                while d2 is None:
+                    d2 = s.event_poll(t2)
+                got[k].append((t2, 3 if rev else 1, res, xt, acq, xfl, xrt, pv, words, d2))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(n_thr)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    allr = sorted((x for g in got for x in g), key=lambda x: x[0])
+    assert len({x[0] for x in allr}) == len(allr)
+    orc = lt.Oracle(n_res, flow, param, degrade)
+    for (t, kind, res, now, acq, fl, rt, pv, words, d) in allr:
+        ev = {"kind": np.array([kind], np.uint8), "resource": np.array([res], np.uint32),
+              "ts": np.array([now], np.int64), "acquire": np.array([acq], np.int32),
+              "flags": np.array([fl], np.uint8), "rt": np.array([rt], np.int64), "param": np.array([pv], np.uint64)}
+        if words is not None:
+            ev["param_values"] = words
+        ed, ew = orc.replay(ev)
+        assert (d[0], d[1]) == (int(ed[0]), int(ew[0])), (t, kind, res, now, fl, d, int(ed[0]), int(ew[0]))
+    end = max(x[3] for x in allr) + 1
+    _assert_nodes(s, orc, n_res, end)
+    kinds = [x[1] for x in allr]
+    assert kinds.count(3) > 20 and kinds.count(2) > 20
+    orc.close()
+    eng.close()

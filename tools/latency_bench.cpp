@@ -2,7 +2,9 @@
 //   requestToken  : sga_request_token_one (coalescing queue) from 1 thread and from T threads at once
 //                   (the Netty worker pattern of FlowRequestProcessor.java:43), 100k cluster rules;
 //   batch of one  : sga_request_tokens with n = 1 (no queue) for comparison;
-//   SphU.entry    : sga_submit_events with one entry event (the local slot chain per call), 10k rules.
+//   SphU.entry    : sga_submit_events with one entry event (the local slot chain per call), 10k rules;
+//                   and through the coalescing event queue (sga_event_one) from 1 and T threads, each passed
+//                   entry followed by its exit (calls_per_s counts entries).
 // Prints one JSON line per case: p50 / p99 / max in microseconds and calls per second.
 // Build: g++ -O2 -std=c++17 tools/latency_bench.cpp -Iinclude -Lsentinel_amd -lsentinel_amd -lpthread
 // Run (GPU box): LD_LIBRARY_PATH=sentinel_amd ./tools/latency_bench [threads] [calls]
@@ -140,6 +142,37 @@ int main(int argc, char **argv) {
             lat.push_back(us_since(t));
         }
         report("SphU.entry (sga_submit_events, one entry)", lat, us_since(w0) / 1e6, 1);
+        // SphU.entry + Entry.exit through the coalescing event queue (sga_event_one), 1 thread and T threads:
+        // what GpuStatisticSlot calls per entry (jni/native/sga_jni_glue.c sgaj_entry / sgaj_exit)
+        for (int nt : {1, threads}) {
+            std::vector<std::vector<double>> l2(nt);
+            std::vector<std::thread> th;
+            std::atomic<int> passed{0};
+            const auto w1 = clk::now();
+            for (int k = 0; k < nt; ++k)
+                th.emplace_back([&, k] {
+                    for (int i = 0; i < calls; ++i) {
+                        const uint32_t res = (uint32_t)((i * 7919 + k * 104729) % n_res);
+                        const int64_t ts = t0 + 20000 + (nt > 1 ? 50000 : 0) + i / 10;
+                        int8_t dec;
+                        int32_t wait;
+                        const auto t = clk::now();
+                        sga_event_one(e, 0, res, ts, 1, 0, 0, 0, nullptr, 0, &dec, &wait);
+                        l2[k].push_back(us_since(t));
+                        if (dec == 0) {
+                            passed.fetch_add(1);
+                            sga_event_one(e, 1, res, ts + 5, 1, 0, 5, 0, nullptr, 0, &dec, &wait);
+                        }
+                    }
+                });
+            for (auto &t : th) t.join();
+            const double wall = us_since(w1) / 1e6;
+            std::vector<double> all;
+            for (auto &v : l2) all.insert(all.end(), v.begin(), v.end());
+            report(nt == 1 ? "SphU.entry (sga_event_one; each passed entry also exits)"
+                           : "SphU.entry (sga_event_one, concurrent; each passed entry also exits)",
+                   all, wall, nt);
+        }
     }
     sga_destroy(e);
     return 0;
