@@ -545,7 +545,7 @@ def run_local(args, cfg_name):
         dist.destroy_process_group()
     if rank != 0:
         return None
-    # HBM traffic per step from the committed rocprofv3 PMC passes of this line (tools/r04_pmc.sh)
+    # HBM traffic per step from the committed rocprofv3 PMC passes of this line (tools/pmc_configs.sh)
     traffic, traffic_src = None, None
     tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", f"traffic_{cfg_name}.json")
     if os.path.exists(tpath):

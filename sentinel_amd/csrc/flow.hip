@@ -4122,7 +4122,7 @@ __global__ __launch_bounds__(128) void k_llru_ps(FlowState st, int64_t max_rt, F
 //    lanes may claim a slot each for one key; the later one in the probe sequence is never found again,
 //    its key absent, dropped at the next rehash).  !kClaim: the element (slot << 32 | sorted position),
 //    kPsegNone in the slot bits for every other event.
-// force_miss (fault injection, SGA_PSEG_FORCE_MISS=1; tests only): the first parameter event's entry is
+// force_miss (fault injection, SGA_PSEG_FORCE_MISS=1 in the test-only build SGA_TEST_HOOKS): the first parameter event's entry is
 // taken as missing, so the device check below fails the batch
 template <bool kClaim>
 __global__ __launch_bounds__(kT) void k_pseg_key(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
@@ -5957,7 +5957,11 @@ void FlowEngine::launch_pseg(const FlowState &st, const FlowScratch &g, const Pa
     if (!h_prules.empty()) {
         // the count pass (lru_prepare, whenever parameter rules are loaded) has claimed every key these events
         // name in free-mode maps already; the claim launch is for an engine without it
+#ifdef SGA_TEST_HOOKS  // the test-only build (libsentinel_amd_testhooks.so): fault injection
         static const int force_miss = getenv("SGA_PSEG_FORCE_MISS") ? atoi(getenv("SGA_PSEG_FORCE_MISS")) : 0;
+#else
+        constexpr int force_miss = 0;
+#endif
         if (!d_psize.p)
             hipLaunchKernelGGL(k_pseg_key<true>, dim3(nb), dim3(kT), 0, s, st, gs, pay, keys, param, m, none, 0);
         hipLaunchKernelGGL(k_pseg_key<false>, dim3(nb), dim3(kT), 0, s, st, gs, pay, keys, param, m, none, force_miss);

@@ -213,7 +213,8 @@ eng.close()
 """
     out = {}
     for knob in ("0", "1"):
-        env = dict(os.environ, SGA_PSEG_FORCE_MISS=knob)
+        # the fault-injection hook exists only in the test-only build (flow.hip SGA_TEST_HOOKS)
+        env = dict(os.environ, SGA_PSEG_FORCE_MISS=knob, SGA_LIB_VARIANT="testhooks")
         r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, r.stderr[-2000:]
         out[knob] = r.stdout.strip().splitlines()[-1]

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Usage (GPU box): bash tools/r03_ab.sh <tag> "ENV=a" "ENV=b" ...  -- C3 bench A/B under kernel traces + timelines
+# Usage (GPU box): bash tools/ab_c3.sh <tag> "ENV=a" "ENV=b" ...  -- C3 bench A/B under kernel traces + timelines
 set -o pipefail
 tag=${1:-r03ab}; shift
 export TMPDIR=/tmp

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Usage (GPU box): bash tools/r05_ab.sh <tag> <pytest files...> -- "ENV=a" "ENV=b" ...
+# Usage (GPU box): bash tools/ab_runner.sh <tag> <pytest files...> -- "ENV=a" "ENV=b" ...
 # The listed GPU tests, then the C3 bench line under each environment (2 runs each, interleaved), then a kernel
 # trace (one batch's timeline) of the first environment.
 set -o pipefail

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Usage (GPU box): bash tools/r04_pmc.sh <tag> [configs...] -- HBM traffic per step from rocprofv3 PMC passes
+# Usage (GPU box): bash tools/pmc_configs.sh <tag> [configs...] -- HBM traffic per step from rocprofv3 PMC passes
 # (FETCH_SIZE and WRITE_SIZE in passes of their own, kernel trace only, as MI355X_MICROARCH.md prescribes):
 # calibration (tools/calib/pmccal), then per configuration two counter passes and a kernel trace of the bench
 # line, summarised by tools/pmc_summary.py into gpurun_out/<tag>/traffic_<cfg>.json.
