@@ -177,6 +177,8 @@ def main():
     # (sga_cluster_metric_nodes_device) + the node-wide all-gather (RCCL over xGMI at N > 1)
     step_virtual_ms = glob_batch * 1000.0 / lam
     metric_every = max(1, int(round(1000.0 / step_virtual_ms)))
+    if os.environ.get("SGA_BENCH_METRIC_EVERY"):  # diagnostics only (A/B of the snapshot's cost); never in a reported line
+        metric_every = int(os.environ["SGA_BENCH_METRIC_EVERY"])
     act = C.c_uint64()
     _lib.check(L.sga_cluster_stats(eng.handle, C.byref(act), None), eng.handle, "stats")
     cap_rows = max(int(act.value), 1)

@@ -145,7 +145,9 @@ int sga_set_hot_rules(sga_engine *e, int32_t enabled, uint32_t min_requests);
 /* Engine tuning (no reference counterpart): token batches of at most max_requests requests (capped
  * at 4096, 0 = off; default 4096) are classified and ordered by one workgroup instead of the
  * multi-launch sort pipeline -- the latency path of a single requestToken.  Decisions are the same
- * either way. */
+ * either way.  The same setting (capped at 1024) sends host chunks of local events (sga_submit_events,
+ * the sga_event_* queue) of at most that many events, without inbound events under SystemRules, to one
+ * replay kernel instead of the local pipeline. */
 int sga_set_small_batch(sga_engine *e, uint32_t max_requests);
 
 /* Batched DefaultTokenService.requestToken over host buffers; synchronous.

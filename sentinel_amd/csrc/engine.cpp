@@ -1126,6 +1126,8 @@ int sga_set_hot_rules(sga_engine *e, int32_t enabled, uint32_t min_requests) {
 int sga_set_small_batch(sga_engine *e, uint32_t max_requests) {
     return guarded(e, [&](Engine &g) {
         g.scratch.small_max = g.scratch2.small_max = std::min<uint32_t>(max_requests, 4096u);
+        // the local path's one-workgroup replay of small host chunks (k_lsmall), at most kSmallEvents events
+        g.flow.small_max = std::min<uint32_t>(max_requests, sga::FlowEngine::kSmallEvents);
         return SGA_OK;
     });
 }

@@ -1773,6 +1773,62 @@ __device__ __forceinline__ void replay_event(const Ctx &c, const FlowScratch &sc
     }
 }
 
+// Small batches (the coalescing event queue's rounds, a single SphU.entry): one workgroup.  The first event of
+// each resource in the batch leads: its lane replays the resource's events in arrival order with the whole slot
+// chain (replay_event, as lane_run does for a resource with F_SPECIAL events), the resources side by side; then
+// one lane adds the inbound events to ENTRY_NODE in arrival order (no SystemRule check on this path).
+constexpr int kLSmall = 1024;
+__global__ __launch_bounds__(kLSmall) void k_lsmall(FlowState st, int64_t max_rt, FlowScratch fs,
+                                                    const uint32_t *__restrict__ resource,
+                                                    const uint32_t *__restrict__ ts_off, int64_t ts_base,
+                                                    const int32_t *__restrict__ acquire,
+                                                    const int64_t *__restrict__ rt_in, uint32_t n, int8_t *decision,
+                                                    int32_t *wait_ms, uint32_t *ovf_out) {
+    __shared__ uint32_t sres[kLSmall];
+    const uint32_t i = threadIdx.x;
+    const Ctx c{st, max_rt};
+    if (i < n) {
+        sres[i] = resource[i];
+        decision[i] = D_PASS;
+        wait_ms[i] = 0;
+    }
+    __syncthreads();
+    if (i < n) {
+        const uint32_t r = sres[i];
+        bool lead = r < st.nres;
+        for (uint32_t j = 0; j < i && lead; ++j) lead = sres[j] != r;
+        if (lead)
+            for (uint32_t j = i; j < n; ++j) {
+                if (sres[j] != r) continue;
+                const Payload q{j | F_SPECIAL, ts_off[j], (uint32_t)acquire[j] & 0x7FFFFFFFu, 0u};
+                replay_event<true>(c, fs, r, q, ts_base, rt_in, fs.in_param, decision, wait_ms);
+            }
+    }
+    __syncthreads();
+    if (i == 0) {
+        for (uint32_t j = 0; j < n; ++j) {
+            const uint8_t fl = fs.in_flags ? fs.in_flags[j] : 0;
+            if (sres[j] >= st.nres || !(fl & SGA_EV_INBOUND)) continue;
+            const int64_t t = ts_base + (int64_t)ts_off[j];
+            const int a = (int)((uint32_t)acquire[j] & 0x7FFFFFFFu);
+            const uint8_t kd = fs.in_kind[j];
+            if (kd == 1) {
+                entry_node_after_exit(c, t, rt_in[j], a, (fl & SGA_EV_ERROR) != 0);
+            } else if (kd == SGA_KIND_BLOCKED) {
+                node_add(c, entry_node(c), t, MB_BLOCK, a);
+            } else if (kd == SGA_KIND_REVOKE) {
+                int64_t *e = entry_node(c);
+                e[kNodeThreads] -= 1;
+                node_add(c, e, t, MB_PASS, -(int64_t)a);
+                node_add(c, e, t, MB_BLOCK, a);
+            } else {
+                entry_node_after_entry(c, t, a, decision[j]);
+            }
+        }
+        *ovf_out = *st.overflow;
+    }
+}
+
 // One run of a resource decided by one lane (k_lflows; k_lwave's lane 0 for runs it cannot split):
 // RateLimiter pacing in registers, the per-event slot chain, or the closed form (RUN_FAST: k_lresults
 // writes the decisions from run_f).
@@ -6142,6 +6198,63 @@ int FlowEngine::ensure_scratch() {
     return 0;
 }
 
+// One small chunk (FlowEngine::kSmallEvents): the events and their argument words packed into page-locked memory,
+// one copy to the device, the CacheMap bookkeeping (lru_prepare), k_lsmall, one copy back of the decisions,
+// waits and the overflow word.
+int FlowEngine::submit_small(const uint8_t *kind, const uint32_t *resource, const int32_t *acquire,
+                             const uint8_t *flags, const int64_t *rt, const uint64_t *param, const uint32_t *ts_off,
+                             int64_t lo, uint32_t m, int8_t *decision, int32_t *wait_ms, const uint64_t *pvals,
+                             size_t npvals) {
+    auto a8 = [](size_t x) { return (x + 7) & ~(size_t)7; };
+    const size_t o_kind = 0, o_flags = a8(o_kind + kSmallEvents), o_res = a8(o_flags + kSmallEvents),
+                 o_ts = o_res + 4 * kSmallEvents, o_acq = o_ts + 4 * kSmallEvents, o_rt = o_acq + 4 * kSmallEvents,
+                 o_param = o_rt + 8 * kSmallEvents, o_vals = o_param + 8 * kSmallEvents,
+                 in_bytes = o_vals + 8 * (size_t)kSmallWords;
+    const size_t o_dec = in_bytes, o_wait = a8(o_dec + kSmallEvents), o_ovf = o_wait + 4 * kSmallEvents,
+                 all_bytes = o_ovf + 8;
+    if (!h_small.p) h_small.alloc(all_bytes);
+    if (!d_small.p) d_small.alloc(all_bytes);
+    uint8_t *h = h_small.p, *d = d_small.p;
+    std::memcpy(h + o_kind, kind, m);
+    if (flags) std::memcpy(h + o_flags, flags, m);
+    else std::memset(h + o_flags, 0, m);
+    std::memcpy(h + o_res, resource, 4 * (size_t)m);
+    std::memcpy(h + o_ts, ts_off, 4 * (size_t)m);
+    std::memcpy(h + o_acq, acquire, 4 * (size_t)m);
+    if (rt) std::memcpy(h + o_rt, rt, 8 * (size_t)m);
+    else std::memset(h + o_rt, 0, 8 * (size_t)m);
+    if (param) std::memcpy(h + o_param, param, 8 * (size_t)m);
+    else std::memset(h + o_param, 0, 8 * (size_t)m);
+    if (npvals) std::memcpy(h + o_vals, pvals, 8 * npvals);
+    // one copy of what the chunk uses (the argument words sit at the end of the input region)
+    const size_t up = npvals ? o_vals + 8 * npvals : o_vals;
+    SGA_HIP_CHECK(hipMemcpyAsync(d, h, up, hipMemcpyHostToDevice, stream));
+    SGA_HIP_CHECK(hipMemsetAsync(d_overflow.p, 0, 4, stream));
+    const uint8_t *dk = d + o_kind, *dfl = d + o_flags;
+    const uint32_t *dres = (const uint32_t *)(d + o_res), *dts = (const uint32_t *)(d + o_ts);
+    const int32_t *dacq = (const int32_t *)(d + o_acq);
+    const int64_t *drt = (const int64_t *)(d + o_rt);
+    const uint64_t *dpar = (const uint64_t *)(d + o_param), *dvals = npvals ? (const uint64_t *)(d + o_vals) : nullptr;
+    lru_prepare(dk, dres, dfl, dpar, dvals, m, stream);  // CacheMap capacity
+    FlowScratch fs = sc;
+    fs.in_kind = dk;
+    fs.in_flags = dfl;
+    fs.in_param = dpar;
+    fs.pvals = dvals;
+    hipLaunchKernelGGL(k_lsmall, dim3(1), dim3(kLSmall), 0, stream, state(), (int64_t)cfg.statistic_max_rt, fs, dres,
+                       dts, lo, dacq, drt, m, (int8_t *)(d + o_dec), (int32_t *)(d + o_wait), (uint32_t *)(d + o_ovf));
+    SGA_HIP_CHECK(hipGetLastError());
+    SGA_HIP_CHECK(hipMemcpyAsync(h + o_dec, d + o_dec, all_bytes - o_dec, hipMemcpyDeviceToHost, stream));
+    SGA_HIP_CHECK(hipStreamSynchronize(stream));
+    std::memcpy(decision, h + o_dec, m);
+    if (wait_ms) std::memcpy(wait_ms, h + o_wait, 4 * (size_t)m);
+    uint32_t ovf;
+    std::memcpy(&ovf, h + o_ovf, 4);
+    if (ovf & kOvfMissingEntry) throw HipError(kMissingEntryText, __FILE__, __LINE__);  // SGA_EIO
+    if (ovf) return SGA_ENOMEM;  // parameter maps full
+    return 0;
+}
+
 // The chunk's view of the scratch for F_SPECIAL events: a new epoch marks their resources (res_special), the
 // original kind / flags / parameters / value lists are what the per-resource replay reads for them.
 FlowScratch FlowEngine::special_scratch(const FlowScratch &base, const uint8_t *d_kind_in, const uint8_t *d_flags_in,
@@ -6220,6 +6333,21 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
         off.resize(m);
         for (size_t i = 0; i < m; ++i) off[i] = (uint32_t)(ts[b + i] - lo);
         if (const int rc = ensure_maps(m + (any_list ? npvals : 0))) return rc;
+        bool has_in = false, has_list = false;
+        for (size_t i = 0; flags && i < m && !has_in; ++i) has_in = (flags[b + i] & SGA_EV_INBOUND) && resource[b + i] < nres;
+        for (size_t i = 0; any_list && i < m && !has_list; ++i) has_list = is_list(b + i);
+        for (size_t i = 0; i < m; ++i)
+            if (kind[b + i] > SGA_KIND_REVOKE) return SGA_EINVAL;
+        if (m <= small_max && !(has_in && sys.check) && (!has_list || npvals <= kSmallWords)) {
+            if (const int rc = submit_small(kind + b, resource + b, acquire + b, flags ? flags + b : nullptr,
+                                            rt ? rt + b : nullptr, param ? param + b : nullptr, off.data(), lo,
+                                            (uint32_t)m, decision + b, wait_ms ? wait_ms + b : nullptr,
+                                            has_list ? pvals : nullptr, has_list ? npvals : 0))
+                return rc;
+            b += m;
+            seq += m;
+            continue;
+        }
         SGA_HIP_CHECK(hipMemcpyAsync(d_kind.p, kind + b, m, hipMemcpyHostToDevice, stream));
         SGA_HIP_CHECK(hipMemcpyAsync(d_resid.p, resource + b, m * 4, hipMemcpyHostToDevice, stream));
         SGA_HIP_CHECK(hipMemcpyAsync(d_ts.p, off.data(), m * 4, hipMemcpyHostToDevice, stream));
@@ -6240,11 +6368,6 @@ int FlowEngine::submit(const uint8_t *kind, const uint32_t *resource, const int6
                     any_list ? d_pvals.p : nullptr, (uint32_t)m, stream);
         const FlowState st = state();
         const uint32_t nb = (uint32_t)((m + kT - 1) / kT);
-        bool has_in = false, has_list = false;
-        for (size_t i = 0; flags && i < m && !has_in; ++i) has_in = (flags[b + i] & SGA_EV_INBOUND) && resource[b + i] < nres;
-        for (size_t i = 0; any_list && i < m && !has_list; ++i) has_list = is_list(b + i);
-        for (size_t i = 0; i < m; ++i)
-            if (kind[b + i] > SGA_KIND_REVOKE) return SGA_EINVAL;
         // kind 2 / 3 events and argument lists stay on the parallel pipeline (their resources replay per resource,
         // F_SPECIAL); SystemRules read ENTRY_NODE across resources: one lane in arrival order
         if (has_in && sys.check) {

@@ -321,6 +321,15 @@ struct FlowEngine {
                                 const uint64_t *d_param_in, const uint64_t *d_pvals);
     DevBuf<uint64_t> d_pvals;  // values of Collection / array arguments (SGA_EV_PARAM_LIST)
     // the same over device buffers, asynchronous on s: one chunk of n <= max_batch events
+    // small host batches (<= kSmallEvents events, <= kSmallWords argument words, no SystemRule check): one
+    // packed page-locked copy each way and one replay kernel (k_lsmall) instead of the pipeline
+    static constexpr uint32_t kSmallEvents = 1024, kSmallWords = 16384;
+    uint32_t small_max = kSmallEvents;  // sga_set_small_batch (0: off)
+    PinnedBuf h_small;
+    DevBuf<uint8_t> d_small;
+    int submit_small(const uint8_t *kind, const uint32_t *resource, const int32_t *acquire, const uint8_t *flags,
+                     const int64_t *rt, const uint64_t *param, const uint32_t *ts_off, int64_t lo, uint32_t m,
+                     int8_t *decision, int32_t *wait_ms, const uint64_t *pvals, size_t npvals);
     int submit_device(const uint8_t *d_kind, const uint32_t *d_resource, int64_t ts_base, const uint32_t *d_ts_off,
                       const int32_t *d_acquire, const uint8_t *d_flags, const int64_t *d_rt_in,
                       const uint64_t *d_param_in, size_t n, const uint64_t *d_param_values, size_t n_values,

@@ -228,7 +228,8 @@ def test_thread_maps_many_indices_distinct_values():
     eng.close()
 
 
-def test_revoked_entries_after_a_later_slot_block():
+@pytest.mark.parametrize("small", [True, False])
+def test_revoked_entries_after_a_later_slot_block(small):
     """Event kind 3 (SGA_KIND_REVOKE): an entry the engine passed that a slot sorted after DegradeSlot then
     blocked.  The reference's StatisticSlot fires those slots before its pass accounting (StatisticSlot.java:
     71-84), so the entry counts only a block (:121-135): the revoke undoes the pass, the thread counts (node,
@@ -241,6 +242,8 @@ def test_revoked_entries_after_a_later_slot_block():
     param = [{"resource": 2, "grade": 0, "count": 2.0, "param_idx": 0}, {"resource": 3, "count": 5.0}]
     orc = lt.Oracle(n_res, flow, param)
     eng, s = _sentinel(n_res, 1 << 12)
+    if not small:  # the rounds through the pipeline instead of the one-workgroup replay (k_lsmall)
+        eng.set_small_batch(0)
     _load(s, flow, param)
     n_rev = n_pass = 0
     for k in range(30):
@@ -275,7 +278,8 @@ def test_revoked_entries_after_a_later_slot_block():
     eng.close()
 
 
-def test_revoked_probes_return_breakers_to_open():
+@pytest.mark.parametrize("small", [True, False])
+def test_revoked_probes_return_breakers_to_open(small):
     """Revokes of entries that were circuit-breaker probes (AbstractCircuitBreaker.java:117-139: the
     whenTerminate hook moves a breaker the blocked entry made HALF_OPEN back to OPEN, next retry kept).
     Exception-count and slow-RT breakers trip on erroring / slow exits; after each retry time the first entry
@@ -289,6 +293,8 @@ def test_revoked_probes_return_breakers_to_open():
     flow = [{"resource": 2, "count": 50.0}]
     orc = lt.Oracle(n_res, flow, [], degrade)
     eng, s = _sentinel(n_res, 1 << 12)
+    if not small:
+        eng.set_small_batch(0)
     _load(s, flow, None, degrade)
     reopened = 0
     for k in range(40):
