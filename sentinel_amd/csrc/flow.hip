@@ -1783,10 +1783,11 @@ __global__ __launch_bounds__(kLSmall) void k_lsmall(FlowState st, int64_t max_rt
                                                     const uint32_t *__restrict__ ts_off, int64_t ts_base,
                                                     const int32_t *__restrict__ acquire,
                                                     const int64_t *__restrict__ rt_in, uint32_t n, int8_t *decision,
-                                                    int32_t *wait_ms, uint32_t *ovf_out) {
+                                                    int32_t *wait_ms, uint32_t *ovf_out, int zero_ovf) {
     __shared__ uint32_t sres[kLSmall];
     const uint32_t i = threadIdx.x;
     const Ctx c{st, max_rt};
+    if (zero_ovf && i == 0) *st.overflow = 0;  // no lru_prepare ahead of this kernel: the batch's overflow word
     if (i < n) {
         sres[i] = resource[i];
         decision[i] = D_PASS;
@@ -6226,10 +6227,18 @@ int FlowEngine::submit_small(const uint8_t *kind, const uint32_t *resource, cons
     if (param) std::memcpy(h + o_param, param, 8 * (size_t)m);
     else std::memset(h + o_param, 0, 8 * (size_t)m);
     if (npvals) std::memcpy(h + o_vals, pvals, 8 * npvals);
-    // one copy of what the chunk uses (the argument words sit at the end of the input region)
-    const size_t up = npvals ? o_vals + 8 * npvals : o_vals;
-    SGA_HIP_CHECK(hipMemcpyAsync(d, h, up, hipMemcpyHostToDevice, stream));
-    SGA_HIP_CHECK(hipMemsetAsync(d_overflow.p, 0, 4, stream));
+    // The kernels read the page-locked buffer in place and write the results into it (it is mapped into the
+    // device's address space, coherent): no copy operation either way, one launch (plus the CacheMap
+    // bookkeeping when parameter rules exist).  SGA_SMALL_COPY=1 (A/B knob) copies to HBM first.
+    static const bool copy = getenv("SGA_SMALL_COPY") && atoi(getenv("SGA_SMALL_COPY")) == 1;
+    if (copy) {
+        const size_t up = npvals ? o_vals + 8 * npvals : o_vals;  // the argument words end the input region
+        SGA_HIP_CHECK(hipMemcpyAsync(d, h, up, hipMemcpyHostToDevice, stream));
+    } else {
+        d = h;
+    }
+    const bool maps = d_psize.p && !h_prules.empty();  // lru_prepare runs (and may flag the overflow word)
+    if (maps) SGA_HIP_CHECK(hipMemsetAsync(d_overflow.p, 0, 4, stream));
     const uint8_t *dk = d + o_kind, *dfl = d + o_flags;
     const uint32_t *dres = (const uint32_t *)(d + o_res), *dts = (const uint32_t *)(d + o_ts);
     const int32_t *dacq = (const int32_t *)(d + o_acq);
@@ -6242,9 +6251,10 @@ int FlowEngine::submit_small(const uint8_t *kind, const uint32_t *resource, cons
     fs.in_param = dpar;
     fs.pvals = dvals;
     hipLaunchKernelGGL(k_lsmall, dim3(1), dim3(kLSmall), 0, stream, state(), (int64_t)cfg.statistic_max_rt, fs, dres,
-                       dts, lo, dacq, drt, m, (int8_t *)(d + o_dec), (int32_t *)(d + o_wait), (uint32_t *)(d + o_ovf));
+                       dts, lo, dacq, drt, m, (int8_t *)(d + o_dec), (int32_t *)(d + o_wait), (uint32_t *)(d + o_ovf),
+                       maps ? 0 : 1);
     SGA_HIP_CHECK(hipGetLastError());
-    SGA_HIP_CHECK(hipMemcpyAsync(h + o_dec, d + o_dec, all_bytes - o_dec, hipMemcpyDeviceToHost, stream));
+    if (copy) SGA_HIP_CHECK(hipMemcpyAsync(h + o_dec, d + o_dec, all_bytes - o_dec, hipMemcpyDeviceToHost, stream));
     SGA_HIP_CHECK(hipStreamSynchronize(stream));
     std::memcpy(decision, h + o_dec, m);
     if (wait_ms) std::memcpy(wait_ms, h + o_wait, 4 * (size_t)m);
