@@ -486,6 +486,44 @@ def _time_router(f, n_shards, threads):
                     "(host-side event routing, SURVEY.md 8(e)), timed on a sample of the C3 trace"}
 
 
+def _time_wire_decode(f, n_shards):
+    """One host thread decoding FLOW frames (the token server's Netty frames) into engine batches: plain
+    (sga_wire_decode) and routed inside the decode into n_shards per-GPU batches (sga_wire_decode_sharded) --
+    the host-fed node's way around a separate routing pass."""
+    from sentinel_amd import token_server as ts
+    f = np.asarray(f[: 1 << 20], dtype=np.int64)
+    fr = np.zeros(len(f), dtype=[("len", ">u2"), ("xid", ">i4"), ("type", "u1"), ("fid", ">i8"), ("cnt", ">i4"),
+                                 ("prio", "u1")])
+    fr["len"], fr["xid"], fr["type"], fr["fid"], fr["cnt"] = 18, np.arange(len(f)), 1, f, 1
+    buf = fr.tobytes()
+    out = {"frames": int(len(f)), "shards": n_shards, "threads": 1}
+    def one_pass(name, bs):
+        at, t = 0, 0.0
+        while at < len(buf):
+            for b in bs:
+                b.reset()
+            chunk = buf[at:at + 18 * 65536 + 2]
+            t0 = time.perf_counter()
+            if name == "plain":
+                _, used = bs[0].decode(chunk)
+            else:
+                _, used = ts.decode_sharded(chunk, bs)
+            t += time.perf_counter() - t0
+            if used == 0:
+                break
+            at += used
+        return t
+
+    for name in ("plain", "sharded"):
+        bs = [ts.WireBatch(1 << 16, 1, 1) for _ in range(n_shards if name == "sharded" else 1)]
+        one_pass(name, bs)  # touches the batches' pages
+        out[f"{name}_frames_per_s"] = len(f) / min(one_pass(name, bs) for _ in range(3))
+    out["what"] = ("one thread decoding 2^20 FLOW frames of the C3 trace's flowIds into engine batches: plain "
+                   "(sga_wire_decode) and routed to 8 per-GPU batches inside the decode (sga_wire_decode_sharded); "
+                   "best of three passes after one untimed, per-call Python overhead included")
+    return out
+
+
 def run_cpu_baseline(args, n_gpus):
     """CPU restatement of the same path on this host (the reference's JMH harness needs a JDK,
     which the image lacks).  Bounded sample: the first `cpu_sample` requests of rank 0's shard
@@ -572,6 +610,7 @@ def run_cpu_baseline(args, n_gpus):
     dtc = fn(threads, len(rf), rf.ctypes.data, rc.ctypes.data, 10, 1000, len(fa), fa.ctypes.data, aa.ctypes.data,
              pa.ctypes.data, ta.ctypes.data, None)
     router = _time_router(np.concatenate([c[0] for c in chunks]), 8, threads)
+    router["wire_decode"] = _time_wire_decode(np.concatenate([c[0] for c in chunks]), 8)
     v_shard, v_cont = total / dtn, total / dtc
     return {"value": max(v_shard, v_cont), "unit": "decisions/s", "cores": threads, "kind": "port",
             "variant": "contended" if v_cont >= v_shard else "shard-parallel",

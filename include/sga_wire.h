@@ -72,6 +72,12 @@ int64_t sga_wire_string_key(const uint8_t *bytes, size_t len);
  * connection: TooLongFrameException). */
 int sga_wire_decode(const uint8_t *buf, size_t len, size_t *consumed, sga_wire_batch *out);
 
+/* sga_wire_decode into G per-shard batches (the multi-GPU token server, one engine per GPU): a FLOW /
+ * PARAM_FLOW frame goes to outs[splitmix64(flowId) mod G] -- the shard function of sga_route_shards --,
+ * PING and malformed frames to outs[0]; each batch keeps arrival order.  The routing happens inside the
+ * decode (no separate pass over the requests).  Stops when the batch a frame goes to is full. */
+int sga_wire_decode_sharded(const uint8_t *buf, size_t len, size_t *consumed, uint32_t G, sga_wire_batch *outs);
+
 /* Encodes one response frame per request i in [0, n): FLOW / PARAM from token results
  * (status = TokenResultStatus, remaining, waitInMs; PARAM responses carry waitInMs 0,
  * ParamFlowRequestProcessor.java:48-54), PING with `ping_count[i]`, BAD as status -1 without data,

@@ -183,6 +183,8 @@ SIGNATURES = {
     "sga_metrics_snapshot": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "sga_cluster_metric_nodes": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "sga_wire_decode": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(SgaWireBatch)]),
+    "sga_wire_decode_sharded": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.c_uint32,
+                                          C.POINTER(SgaWireBatch)]),
     "sga_wire_encode": (C.c_int, [C.c_void_p] * 7 + [C.c_size_t, C.c_void_p, C.c_size_t]),
     "sga_wire_string_key": (C.c_int64, [C.c_char_p, C.c_size_t]),
     "sga_cluster_metric_nodes_device": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_size_t, C.c_void_p,

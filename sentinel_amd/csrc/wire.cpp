@@ -3,6 +3,7 @@
 // sga_request_param_tokens take, so one decode call turns many connections' frames into one
 // engine launch.
 #include "../../include/sga_wire.h"
+#include "common.hpp"  // splitmix64 (the shard function of sga_route_shards)
 
 #include <cerrno>
 #include <cstring>
@@ -46,15 +47,24 @@ int64_t sga_wire_string_key(const uint8_t *b, size_t len) {
     return (int64_t)h;
 }
 
-int sga_wire_decode(const uint8_t *buf, size_t len, size_t *consumed, sga_wire_batch *o) {
-    if (!buf || !consumed || !o) return -EINVAL;
-    size_t at = 0;
-    int frames = 0;
+}  // extern "C"
+
+namespace {
+
+void batch_begin(sga_wire_batch *o) {  // a batch's first decode call
     if (o->n == 0) {
         o->nv = 0;
         o->ns_used = 0;
         if (o->voff) o->voff[0] = 0;
     }
+}
+
+// The frame loop of sga_wire_decode / sga_wire_decode_sharded: pick(frame, flen) names the batch a frame goes
+// to (from the frame's first bytes), the rest is one decoder.
+template <bool kPrefetch, class Pick>
+int decode_frames(const uint8_t *buf, size_t len, size_t *consumed, Pick pick) {
+    size_t at = 0;
+    int frames = 0;
     while (len - at >= 2) {
         const size_t flen = ((size_t)buf[at] << 8) | buf[at + 1];
         if (flen > SGA_WIRE_MAX_FRAME) {
@@ -62,9 +72,25 @@ int sga_wire_decode(const uint8_t *buf, size_t len, size_t *consumed, sga_wire_b
             return -EINVAL;
         }
         if (len - at - 2 < flen) break;  // partial frame
+        sga_wire_batch *o = pick(buf + at + 2, flen);
         if (o->n >= o->cap) break;
         Reader r{buf + at + 2, flen};
         const size_t i = o->n;
+        if (kPrefetch) {  // G interleaved output streams per array outrun the hardware prefetchers
+            if ((i & 7) == 0) {
+                __builtin_prefetch(o->flow_id + i + 64, 1);
+                __builtin_prefetch(o->xid + i + 64, 1);
+                __builtin_prefetch(o->count + i + 64, 1);
+                __builtin_prefetch(o->ns_off + i + 64, 1);
+                __builtin_prefetch(o->ns_len + i + 64, 1);
+                __builtin_prefetch(o->voff + i + 65, 1);
+            }
+            if ((i & 63) == 0) {
+                __builtin_prefetch(o->type + i + 256, 1);
+                __builtin_prefetch(o->kind + i + 256, 1);
+                __builtin_prefetch(o->prio + i + 256, 1);
+            }
+        }
         int8_t kind = SGA_WIRE_DROP;
         int32_t xid = 0;
         int8_t type = 0;
@@ -185,6 +211,35 @@ int sga_wire_decode(const uint8_t *buf, size_t len, size_t *consumed, sga_wire_b
     }
     *consumed = at;
     return frames;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sga_wire_decode(const uint8_t *buf, size_t len, size_t *consumed, sga_wire_batch *o) {
+    if (!buf || !consumed || !o) return -EINVAL;
+    batch_begin(o);
+    return decode_frames<false>(buf, len, consumed, [o](const uint8_t *, size_t) { return o; });
+}
+
+// Routing inside the decode (the multi-GPU token server): a FLOW / PARAM_FLOW frame goes to the
+// batch of shard splitmix64(flowId) mod G -- the flowId sits right after xid and type, so it is read before
+// anything of the frame is stored -- everything else (PING, malformed frames) to batch 0.  Each shard's batch
+// keeps arrival order, as sga_route_shards does; no separate pass over the decoded requests.
+int sga_wire_decode_sharded(const uint8_t *buf, size_t len, size_t *consumed, uint32_t G, sga_wire_batch *outs) {
+    if (!buf || !consumed || !outs || G == 0) return -EINVAL;
+    for (uint32_t g = 0; g < G; ++g) batch_begin(&outs[g]);
+    const uint64_t mask = (G & (G - 1)) == 0 ? G - 1 : 0;  // a power-of-two G: the modulo is a mask
+    return decode_frames<true>(buf, len, consumed, [outs, G, mask](const uint8_t *f, size_t flen) {
+        if (flen >= 13 && (f[4] == SGA_MSG_FLOW || f[4] == SGA_MSG_PARAM_FLOW)) {
+            uint64_t fid;
+            std::memcpy(&fid, f + 5, 8);
+            const uint64_t h = sga::splitmix64(__builtin_bswap64(fid));
+            return &outs[mask || G == 1 ? h & mask : h % G];
+        }
+        return &outs[0];
+    });
 }
 
 int sga_wire_encode(const int32_t *xid, const int8_t *type, const int8_t *kind, const int32_t *status,

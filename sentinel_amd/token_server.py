@@ -75,6 +75,22 @@ class WireBatch:
         return bytes(self.ns_bytes[o:o + n]).decode("utf-8", errors="replace")
 
 
+def decode_sharded(buf: bytes, batches):
+    """sga_wire_decode_sharded: FLOW / PARAM_FLOW frames into batches[splitmix64(flowId) mod G] (G = len(batches),
+    one engine per GPU), PING and malformed frames into batches[0], each in arrival order, routed inside the
+    decode.  Returns (frames, consumed bytes)."""
+    L = _bind()
+    used = C.c_size_t()
+    b = np.frombuffer(buf, np.uint8) if buf else np.zeros(1, np.uint8)
+    arr = (SgaWireBatch * len(batches))(*[x.s for x in batches])
+    rc = L.sga_wire_decode_sharded(b.ctypes.data, len(buf), C.byref(used), len(batches), arr)
+    for x, a in zip(batches, arr):  # the counters came back in the array's copies
+        x.s.n, x.s.nv, x.s.ns_used = a.n, a.nv, a.ns_used
+    if rc < 0:
+        raise ValueError("frame longer than 1024 bytes (TooLongFrameException)")
+    return rc, used.value
+
+
 def encode_responses(xid, type_, kind, status, remaining, wait_ms, ping_count) -> bytes:
     L = _bind()
     n = len(xid)

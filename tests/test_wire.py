@@ -77,3 +77,44 @@ def test_partial_frames_and_limits():
     assert frames == 2 and b.n == 2
     with pytest.raises(ValueError):       # LengthFieldBasedFrameDecoder(1024): TooLongFrameException
         _decode((1025).to_bytes(2, "big") + b"\x00" * 1025)
+
+
+def test_decode_sharded_equals_decode_then_route():
+    """sga_wire_decode_sharded (routing inside the decode): every shard's batch holds exactly
+    the FLOW / PARAM_FLOW frames whose flowId maps to it under sga_route_shards' function (splitmix64(flowId)
+    mod G), in arrival order, with their values; PING and malformed frames go to shard 0."""
+    from sentinel_amd.workload import shard_of
+    rng = np.random.default_rng(5)
+    frames, meta = [], []
+    for x in range(400):
+        u = rng.random()
+        if u < 0.1:
+            frames.append(ts.frame_ping(x, "ns%d" % (x % 3)))
+            meta.append(("ping", x, None))
+        elif u < 0.6:
+            f = int(rng.integers(1, 10_000))
+            frames.append(ts.frame_flow(x, f, int(rng.integers(1, 4)), bool(rng.random() < 0.2)))
+            meta.append(("flow", x, f))
+        else:
+            f = int(rng.integers(1, 10_000))
+            frames.append(ts.frame_param(x, f, 1, [int(v) for v in rng.integers(0, 50, size=int(rng.integers(1, 4)))]))
+            meta.append(("param", x, f))
+    buf = b"".join(frames)
+    whole = ts.WireBatch(1024, 4096, 4096)
+    nf, used = whole.decode(buf)
+    assert nf == len(frames) and used == len(buf)
+    for G in (1, 2, 8):
+        bs = [ts.WireBatch(1024, 4096, 4096) for _ in range(G)]
+        nfs, used_s = ts.decode_sharded(buf, bs)
+        assert nfs == len(frames) and used_s == len(buf)
+        shard = [0 if k == "ping" else int(shard_of(np.array([f], np.int64), G)[0]) for k, _, f in meta]
+        for g in range(G):
+            idx = [i for i in range(len(meta)) if shard[i] == g]
+            b = bs[g]
+            assert b.n == len(idx)
+            assert list(b.xid[:b.n]) == list(whole.xid[idx]) and list(b.kind[:b.n]) == list(whole.kind[idx])
+            assert list(b.flow_id[:b.n]) == list(whole.flow_id[idx]) and list(b.count[:b.n]) == list(whole.count[idx])
+            for j, i in enumerate(idx):
+                assert list(b.values[b.voff[j]:b.voff[j + 1]]) == list(whole.values[whole.voff[i]:whole.voff[i + 1]])
+                if meta[i][0] == "ping":
+                    assert b.namespace(j) == whole.namespace(i)
