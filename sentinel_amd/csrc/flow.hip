@@ -4207,7 +4207,7 @@ __global__ __launch_bounds__(kT) void k_pseg_key(FlowState st, FlowScratch sc, c
                         if (te->b != 0) te->b = 0;  // the segment's flag word for this batch (k_pseg_heads)
                     } else if (!kClaim) {
                         // every parameter event of a RUN_PSEG flow had its thread-count entry claimed (by the
-                        // claim launch, or by k_lru_count in LRU mode); a missing one would leave the event
+                        // claim launch, or by k_lru_claim in LRU mode); a missing one would leave the event
                         // undecided, so the batch fails: the overflow word's device-error bit (SGA_EIO)
                         atomicOr(st.overflow, kOvfMissingEntry);
                     }
@@ -4889,83 +4889,122 @@ __global__ __launch_bounds__(kT) void k_pseg_apply(FlowState st, int64_t max_rt,
 // 1. count pass: per owner in free mode, the distinct keys absent at the batch start that its events name
 //    (the keys it could insert).  Two launches: the first claims every such key's slot (lanes of one owner
 //    run together here, so two lanes may claim a slot each for the same key: the later one in the probe
-//    sequence is never found again), the second looks each key up -- its first slot in the probe sequence --
-//    and the first event to meet an absent one marks its stamp and counts it.
+//    sequence is never found again), marks each slot it gets back without a value (claimed now, or absent
+//    since an earlier claim) with the batch's stamp mark and lists the events that marked one first; the
+//    second walks only those, looks each of their keys up -- its first slot in the probe sequence -- and the
+//    first to meet an absent one marks it counted and counts it.  Every absent key's first slot was marked
+//    by its claimant or by an event that found it, so one listed event names it: the counts are those of a
+//    walk over every event, and the second launch's work is the batch's distinct absent keys, not its events.
+constexpr uint64_t kStampCounted = 1ull << 62;
 template <bool kCount>
-__device__ __forceinline__ void lru_count_key(PEntry *tab, uint64_t *stamp, uint32_t mask, uint32_t owner, uint64_t v,
+__device__ __forceinline__ bool lru_count_key(PEntry *tab, uint64_t *stamp, uint32_t mask, uint32_t owner, uint64_t v,
                                               uint32_t *ctr, uint64_t mark, uint32_t *overflow) {
     PEntry *e = ptab_get(tab, mask, owner, v, !kCount, overflow);
-    if (!kCount || !e || e->a != kPAbsent) return;
-    const unsigned long long old = atomicExch((unsigned long long *)&stamp[e - tab], (unsigned long long)mark);
-    if (old != mark) atomicAdd(ctr, 1u);
+    if (!e || e->a != kPAbsent) return false;  // a claimant always reads its own kPAbsent
+    uint64_t *sp = &stamp[e - tab];
+    const uint64_t m = kCount ? mark | kStampCounted : mark;
+    if (__hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == m) return false;
+    const bool first = atomicExch((unsigned long long *)sp, (unsigned long long)m) != m;
+    if (kCount && first) atomicAdd(ctr, 1u);
+    return first;
 }
 
 template <bool kCount>
-__global__ __launch_bounds__(kT) void k_lru_count(FlowState st, const uint8_t *__restrict__ kind,
+__device__ __forceinline__ bool lru_count_event(const FlowState &st, uint32_t i, const uint8_t *__restrict__ kind,
+                                                const uint32_t *__restrict__ resource, const uint8_t *__restrict__ flags,
+                                                const uint64_t *__restrict__ param_in,
+                                                const uint64_t *__restrict__ pvals, uint64_t mark) {
+    const uint32_t r = resource[i];
+    if (r >= st.nres || kind[i] == SGA_KIND_BLOCKED) return false;  // a revoke touches the maps as an exit does
+    const ResDev R = st.res[r];
+    if (!R.n_prules) return false;
+    bool need = false;
+    const uint8_t fl = flags ? flags[i] : 0;
+    const bool hp = (fl & SGA_EV_HAS_PARAM) != 0;
+    const uint64_t pv = param_in ? param_in[i] : 0;
+    PArgs pa{nullptr, 0};
+    if ((fl & SGA_EV_ARGS) && pvals) {
+        pa.args = pvals + (pv >> 32);
+        pa.pvals = pvals;
+        pa.nargs = (uint32_t)pv;
+    } else if (hp && (fl & SGA_EV_PARAM_LIST) && pvals) {
+        pa = PArgs{pvals + (pv >> 32), (uint32_t)pv};
+    }
+    const uint32_t nargs = ev_nargs(pa, hp);
+    uint64_t kmask = st.tmapmask ? st.tmapmask[r] : 0ull;  // thread-count maps the event may reach
+    for (uint32_t k = 0; k < R.n_prules; ++k) {
+        const ParamRuleDev &p = st.prules[R.prule_off + k];
+        int32_t idx = p.idx_res;
+        if (idx == kIdxUnresolved) {  // as applyRealParamIdx would resolve it for this event
+            idx = p.param_idx;
+            if (idx < 0) idx = (-idx <= (int32_t)nargs) ? (int32_t)nargs + idx : -idx;
+        }
+        if (idx >= 0 && idx < kMaxParamIdx) kmask |= 1ull << idx;
+        if (!kCount && p.cluster && p.grade == 1 && st.cluster_on && st.cpst.ctl && kind[i] == 0 &&
+            (int64_t)nargs > (int64_t)idx) {
+            // the embedded server's keys of this call (their count decides the CacheMap switch)
+            const uint32_t slot = prule_lookup(st.cpst, p.cflow);
+            const uint64_t *vals;
+            uint32_t nv;
+            if (slot != 0xFFFFFFFFu && st.cpst.param[slot].active && ev_arg(pa, (uint32_t)idx, pv, &vals, &nv) != ARG_NULL)
+                for (uint32_t q = 0; q < nv; ++q) {
+                    const uint32_t vid = vid_of(st.cpst, (int64_t)vals[q], true);
+                    if (vid != 0xFFFFFFFFu) key_of(st.cpst, slot, vid, (int64_t)vals[q], true);
+                }
+        }
+        if (kind[i] != 0 || p.grade != 1 || st.pq[p.id] != kNoQueue || (int64_t)nargs <= (int64_t)idx) continue;
+        const uint64_t *vals;
+        uint32_t nv;
+        if (ev_arg(pa, (uint32_t)idx, pv, &vals, &nv) == ARG_NULL) continue;
+        for (uint32_t q = 0; q < nv; ++q)
+            need |= lru_count_key<kCount>(st.ptab, st.pstamp, st.pmask, p.id + 1, vals[q], &st.pnew[p.id], mark,
+                                          st.overflow);
+    }
+    if (st.tbase[r] == kNoTBase) return need;
+    for (uint32_t k = 0; k < nargs && k < (uint32_t)kMaxParamIdx; ++k) {
+        if (!((kmask >> k) & 1ull)) continue;
+        const uint32_t j = st.tbase[r] + k;
+        if (st.tq[j] != kNoQueue) continue;
+        const uint64_t *vals;
+        uint32_t nv;
+        if (ev_arg(pa, k, pv, &vals, &nv) == ARG_NULL) continue;
+        for (uint32_t q = 0; q < nv; ++q)
+            need |= lru_count_key<kCount>(st.ttab, st.tstamp, st.tmask, tmap_owner(r, k), vals[q], &st.tnew[j], mark,
+                                          st.overflow);
+    }
+    return need;
+}
+
+// the claim launch (every event; those that marked a slot first into st.lneed, one atomic per wave)
+__global__ __launch_bounds__(kT) void k_lru_claim(FlowState st, const uint8_t *__restrict__ kind,
                                                   const uint32_t *__restrict__ resource,
                                                   const uint8_t *__restrict__ flags,
                                                   const uint64_t *__restrict__ param_in,
                                                   const uint64_t *__restrict__ pvals, uint32_t n) {
     const uint64_t mark = kStampMark | st.seq_base;
-    for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
-        const uint32_t r = resource[i];
-        if (r >= st.nres || kind[i] == SGA_KIND_BLOCKED) continue;  // a revoke touches the maps as an exit does
-        const ResDev R = st.res[r];
-        if (!R.n_prules) continue;
-        const uint8_t fl = flags ? flags[i] : 0;
-        const bool hp = (fl & SGA_EV_HAS_PARAM) != 0;
-        const uint64_t pv = param_in ? param_in[i] : 0;
-        PArgs pa{nullptr, 0};
-        if ((fl & SGA_EV_ARGS) && pvals) {
-            pa.args = pvals + (pv >> 32);
-            pa.pvals = pvals;
-            pa.nargs = (uint32_t)pv;
-        } else if (hp && (fl & SGA_EV_PARAM_LIST) && pvals) {
-            pa = PArgs{pvals + (pv >> 32), (uint32_t)pv};
-        }
-        const uint32_t nargs = ev_nargs(pa, hp);
-        uint64_t kmask = st.tmapmask ? st.tmapmask[r] : 0ull;  // thread-count maps the event may reach
-        for (uint32_t k = 0; k < R.n_prules; ++k) {
-            const ParamRuleDev &p = st.prules[R.prule_off + k];
-            int32_t idx = p.idx_res;
-            if (idx == kIdxUnresolved) {  // as applyRealParamIdx would resolve it for this event
-                idx = p.param_idx;
-                if (idx < 0) idx = (-idx <= (int32_t)nargs) ? (int32_t)nargs + idx : -idx;
-            }
-            if (idx >= 0 && idx < kMaxParamIdx) kmask |= 1ull << idx;
-            if (!kCount && p.cluster && p.grade == 1 && st.cluster_on && st.cpst.ctl && kind[i] == 0 &&
-                (int64_t)nargs > (int64_t)idx) {
-                // the embedded server's keys of this call (their count decides the CacheMap switch)
-                const uint32_t slot = prule_lookup(st.cpst, p.cflow);
-                const uint64_t *vals;
-                uint32_t nv;
-                if (slot != 0xFFFFFFFFu && st.cpst.param[slot].active && ev_arg(pa, (uint32_t)idx, pv, &vals, &nv) != ARG_NULL)
-                    for (uint32_t q = 0; q < nv; ++q) {
-                        const uint32_t vid = vid_of(st.cpst, (int64_t)vals[q], true);
-                        if (vid != 0xFFFFFFFFu) key_of(st.cpst, slot, vid, (int64_t)vals[q], true);
-                    }
-            }
-            if (kind[i] != 0 || p.grade != 1 || st.pq[p.id] != kNoQueue || (int64_t)nargs <= (int64_t)idx) continue;
-            const uint64_t *vals;
-            uint32_t nv;
-            if (ev_arg(pa, (uint32_t)idx, pv, &vals, &nv) == ARG_NULL) continue;
-            for (uint32_t q = 0; q < nv; ++q)
-                lru_count_key<kCount>(st.ptab, st.pstamp, st.pmask, p.id + 1, vals[q], &st.pnew[p.id], mark,
-                                      st.overflow);
-        }
-        if (st.tbase[r] == kNoTBase) continue;
-        for (uint32_t k = 0; k < nargs && k < (uint32_t)kMaxParamIdx; ++k) {
-            if (!((kmask >> k) & 1ull)) continue;
-            const uint32_t j = st.tbase[r] + k;
-            if (st.tq[j] != kNoQueue) continue;
-            const uint64_t *vals;
-            uint32_t nv;
-            if (ev_arg(pa, k, pv, &vals, &nv) == ARG_NULL) continue;
-            for (uint32_t q = 0; q < nv; ++q)
-                lru_count_key<kCount>(st.ttab, st.tstamp, st.tmask, tmap_owner(r, k), vals[q], &st.tnew[j], mark,
-                                      st.overflow);
-        }
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t n_up = (n + 63) & ~63u;  // whole waves go round the loop together (the ballot below)
+    for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n_up; i += gridDim.x * kT) {
+        const bool need = i < n && lru_count_event<false>(st, i, kind, resource, flags, param_in, pvals, mark);
+        const uint64_t bal = __ballot(need);
+        if (!bal) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&st.lru_ctl[2], (uint32_t)__popcll(bal));
+        base = __shfl(base, 0);
+        if (need) st.lneed[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = i;
     }
+}
+
+// the count launch over the listed events
+__global__ __launch_bounds__(kT) void k_lru_count(FlowState st, const uint8_t *__restrict__ kind,
+                                                  const uint32_t *__restrict__ resource,
+                                                  const uint8_t *__restrict__ flags,
+                                                  const uint64_t *__restrict__ param_in,
+                                                  const uint64_t *__restrict__ pvals) {
+    const uint64_t mark = kStampMark | st.seq_base;
+    const uint32_t m = st.lru_ctl[2];
+    for (uint32_t t = blockIdx.x * kT + threadIdx.x; t < m; t += gridDim.x * kT)
+        (void)lru_count_event<true>(st, st.lneed[t], kind, resource, flags, param_in, pvals, mark);
 }
 
 // 2. owners that could pass their capacity switch to LRU mode: a queue area from the pool, marked
@@ -4973,6 +5012,7 @@ __global__ __launch_bounds__(kT) void k_lru_count(FlowState st, const uint8_t *_
 constexpr uint64_t kLruBuilding = ~0ull;
 __global__ __launch_bounds__(kT) void k_lru_decide(FlowState st) {
     const uint32_t i = blockIdx.x * kT + threadIdx.x;
+    if (i == 0) st.lru_ctl[2] = 0;  // the count launch (ahead of this one) is done with the list
     if (i >= st.nprid + st.ntslot) return;
     const bool th = i >= st.nprid;
     const uint32_t j = th ? i - st.nprid : i;
@@ -5353,6 +5393,7 @@ FlowState FlowEngine::state() const {
     s.lru_ps = lru_ps ? 1 : 0;
     s.lru_ctl = d_lru_ctl.p;
     s.lru_list = d_lru_list.p;
+    s.lneed = d_lneed.p;
     s.nprid = lru ? (uint32_t)d_psize.n : 0;
     s.ntslot = lru ? ntbase * (uint32_t)kMaxParamIdx : 0;
     s.seq_base = seq;
@@ -5453,12 +5494,13 @@ void FlowEngine::lru_sync_rules() {
 void FlowEngine::lru_prepare(const uint8_t *kind, const uint32_t *resource, const uint8_t *flags, const uint64_t *param,
                              const uint64_t *pvals, uint32_t n, hipStream_t s) {
     if (!d_psize.p || h_prules.empty()) return;
+    if (d_lneed.n < n) d_lneed.grow(n, s);
     const FlowState st = state();
     const uint32_t nb = std::min<uint32_t>((n + kT - 1) / kT, 2048);
-    hipLaunchKernelGGL(k_lru_count<false>, dim3(std::max<uint32_t>(nb, 1)), dim3(kT), 0, s, st, kind, resource, flags,
+    hipLaunchKernelGGL(k_lru_claim, dim3(std::max<uint32_t>(nb, 1)), dim3(kT), 0, s, st, kind, resource, flags,
                        param, pvals, n);
-    hipLaunchKernelGGL(k_lru_count<true>, dim3(std::max<uint32_t>(nb, 1)), dim3(kT), 0, s, st, kind, resource, flags,
-                       param, pvals, n);
+    hipLaunchKernelGGL(k_lru_count, dim3(std::max<uint32_t>(nb, 1)), dim3(kT), 0, s, st, kind, resource, flags,
+                       param, pvals);
     const uint32_t no = st.nprid + st.ntslot;
     hipLaunchKernelGGL(k_lru_decide, dim3((no + kT - 1) / kT), dim3(kT), 0, s, st);
     hipLaunchKernelGGL(k_lru_collect, dim3(2048), dim3(kT), 0, s, st);

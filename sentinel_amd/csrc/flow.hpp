@@ -162,7 +162,9 @@ struct FlowState {
     uint32_t *pnew, *tnew;       // count pass: distinct absent keys the batch may insert, per owner
     uint8_t *lru_res;            // per resource: an owner in LRU mode (its events replay in arrival order)
     uint32_t *lru_ctl;           // [0] owners switched this batch [1] error bits (1 queue pool full, 2 queue check)
+                                 // [2] events in lneed
     uint32_t *lru_list;          // owners switched this batch: param id, or kLruThread | thread slot
+    uint32_t *lneed;             // count pass input: the batch's events with a key absent at its start ([2] of lru_ctl)
     uint32_t nprid, ntslot;      // parameter-rule ids, thread-map owner slots
     uint64_t seq_base;           // event sequence of the batch's first event
 };
@@ -246,7 +248,7 @@ struct FlowEngine {
     uint32_t epoch = 0;
     // CacheMap capacity (FlowState: pstamp .. seq_base)
     DevBuf<uint64_t> d_pstamp, d_tstamp, d_pq, d_tq;
-    DevBuf<uint32_t> d_psize, d_pcap, d_pres, d_pnew, d_tbase, d_tres, d_tsize, d_tnew, d_lru_ctl, d_lru_list;
+    DevBuf<uint32_t> d_psize, d_pcap, d_pres, d_pnew, d_tbase, d_tres, d_tsize, d_tnew, d_lru_ctl, d_lru_list, d_lneed;
     DevBuf<uint8_t> d_lru_res;
     DevBuf<LruRec> d_lpool;
     DevBuf<unsigned long long> d_lcursor;
