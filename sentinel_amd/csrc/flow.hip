@@ -4406,9 +4406,6 @@ __global__ __launch_bounds__(kT) void k_pseg_solve(FlowState st, int64_t max_rt,
 //     HALF_OPEN one is decided by its first exit, stepped alone; a window that goes back in time (a detached
 //     bucket) sends the rest of the flow to the step-by-step replay.
 constexpr int kCbI = 16;
-struct CbAgg {
-    int64_t ws, bad, tot;  // the last window's counts (ws == kCbNone: no exit)
-};
 constexpr int64_t kCbNone = INT64_MIN + 1;
 __device__ __forceinline__ CbAgg cb_combine(const CbAgg &p, const CbAgg &x) {
     if (x.ws == kCbNone) return p;
@@ -4420,43 +4417,200 @@ __device__ __forceinline__ int64_t shfl_up_i64(int64_t v, int o) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 constexpr int kCbW = 8;  // waves per flow: a round covers kCbW x 64 x kCbI exits
-__global__ __launch_bounds__(64 * kCbW) void k_cb_flows(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
-                                                        int64_t ts_base, const int64_t *__restrict__ rt_in,
-                                                        int8_t *decision, int32_t *wait_ms) {
-    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
-    __shared__ int64_t s_w[kCbW][5];  // per wave: total {ws, bad, tot}, first and last window
-    __shared__ uint32_t s_min, s_bad;
-    // a wave's 64 x kCbI exits of a round, loaded coalesced and read back per lane (kCbI consecutive each;
-    // one pad slot per kCbI items keeps those strided reads off one bank)
-    constexpr int kCbStage = 64 * kCbI + 64;
-    __shared__ uint32_t s_ts[kCbW][kCbStage], s_fx[kCbW][kCbStage];
-    __shared__ int64_t s_rt[kCbW][kCbStage];
+constexpr uint32_t kCbRound = 64u * kCbW * kCbI;
+constexpr uint32_t kCbTiled = 1u << 31;        // a cbf word's flow taken by the tile kernels (k_cbt_*)
+constexpr uint32_t kCbTileMin = 2 * kCbRound;  // exits of the shortest flow they take
+// a wave's 64 x kCbI exits of a round, loaded coalesced and read back per lane (kCbI consecutive each; one pad
+// slot per kCbI items keeps those strided reads off one bank)
+constexpr int kCbStage = 64 * kCbI + 64;
+template <int kW>
+struct CbLds {
+    int64_t w[kW][5];  // per wave: total {ws, bad, tot}, first and last window
+    uint32_t min, bad;
+    uint32_t ts[kW][kCbStage], fx[kW][kCbStage];
+    int64_t rt[kW][kCbStage];
+};
+struct CbRound {
+    CbAgg total;    // carry combined with the round's exits
+    uint32_t trip;  // the first exit whose counts trip a CLOSED breaker (je: none, or !want_trip)
+    bool bad;       // a window went back (inside the round or against the carry): the round is not taken
+    int64_t first, last;  // the round's first and last windows (INT64_MAX / INT64_MIN: no exit)
+};
+// One round of a flow's exits (kW waves x 64 lanes x kCbI consecutive exits from base, clipped at je) against
+// the carry: the stat window's counts as a segmented scan (segments = windows, non-decreasing) and, when
+// want_trip, the first exit whose window counts trip the breaker (cb_trips).  Every thread of the workgroup
+// calls it with the same arguments.
+template <int kW>
+__device__ CbRound cb_round(CbLds<kW> &L, const CbDev &b, const CbAgg &carry, uint32_t base, uint32_t je, bool want_trip,
+                            const Payload *__restrict__ pay, const int64_t *__restrict__ rt_sorted, int64_t ts_base) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr uint32_t kRound = 64u * kCbW * kCbI, kWaveItems = 64u * kCbI;
+    constexpr uint32_t kWaveItems = 64u * kCbI;
+    const int64_t si = b.stat_interval;
+    int64_t wsv[kCbI];
+    uint32_t badm = 0, valm = 0;
+    const uint32_t wb = base + (uint32_t)wave * kWaveItems;
+    const uint32_t j0 = wb + (uint32_t)lane * kCbI;
+    // the wave's items through LDS: coalesced loads at clamped indices, then each lane's run
+    {
+#pragma unroll
+        for (int i = 0; i < kCbI; ++i) {
+            const uint32_t k = (uint32_t)i * 64 + (uint32_t)lane;
+            const uint32_t j = min(wb + k, je - 1);
+            const Payload q = pay[j];
+            L.ts[wave][k + k / kCbI] = q.ts_off;
+            L.fx[wave][k + k / kCbI] = q.idx;
+            if (b.grade == 0) L.rt[wave][k + k / kCbI] = rt_sorted[j];  // sorted order (k_lexits)
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
+    uint32_t tso[kCbI], fx[kCbI];
+#pragma unroll
+    for (int i = 0; i < kCbI; ++i) {
+        const uint32_t k = (uint32_t)lane * kCbI + (uint32_t)i;
+        tso[i] = L.ts[wave][k + k / kCbI];
+        fx[i] = L.fx[wave][k + k / kCbI];
+    }
+    if (b.grade == 0) {
+#pragma unroll
+        for (int i = 0; i < kCbI; ++i) {
+            const uint32_t k = (uint32_t)lane * kCbI + (uint32_t)i;
+            badm |= (L.rt[wave][k + k / kCbI] > b.max_allowed_rt ? 1u : 0u) << i;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kCbI; ++i) badm |= ((fx[i] & F_ERROR) ? 1u : 0u) << i;
+    }
+    int64_t cw = kCbNone;  // the window of the previous item: most items share it (no division)
+#pragma unroll
+    for (int i = 0; i < kCbI; ++i) {
+        const int64_t t = ts_base + (int64_t)tso[i];
+        if (cw == kCbNone || t < cw || t - cw >= si) cw = t - t % si;
+        wsv[i] = j0 + i < je ? cw : kCbNone;
+        valm |= (j0 + i < je ? 1u : 0u) << i;
+    }
+    badm &= valm;
+    bool mono = true;  // inside the lane
+    int64_t first = kCbNone, last = kCbNone;
+#pragma unroll
+    for (int i = 0; i < kCbI; ++i) {
+        if (!((valm >> i) & 1u)) continue;
+        if (first == kCbNone) first = wsv[i];
+        else if (wsv[i] < last) mono = false;
+        last = wsv[i];
+    }
+    CbAgg agg{kCbNone, 0, 0};
+#pragma unroll
+    for (int i = 0; i < kCbI; ++i)
+        if ((valm >> i) & 1u) agg = cb_combine(agg, CbAgg{wsv[i], (int64_t)((badm >> i) & 1u), 1});
+    // the lanes' tail-window counts as one DPP segmented scan: a lane starts a segment when its
+    // tail window starts inside it or differs from the windows before it (windows only grow, so
+    // the window of everything up to a lane is the prefix maximum)
+    const int64_t prev_last = wave_incl_max_i64(last == kCbNone ? INT64_MIN : last);
+    const int64_t before = wave_shr1_i64(prev_last, INT64_MIN);  // windows of the lanes before
+    const bool has = agg.ws != kCbNone;
+    int hd = (has && (first != agg.ws || (before != INT64_MIN && before != agg.ws))) ? 1 : 0;
+    int sb = (int)agg.bad, stt = (int)agg.tot;
+    wave_incl_segsum2(sb, stt, hd);
+    const int64_t iws = prev_last == INT64_MIN ? kCbNone : prev_last;  // window of lanes <= this one
+    // the waves' totals, first and last windows: each wave's carry is the round's carry and the
+    // totals of the waves before it
+    {
+        const int64_t fmin = wave_incl_min_i64(first == kCbNone ? INT64_MAX : first);
+        if (lane == 63) {
+            L.w[wave][0] = iws;
+            L.w[wave][1] = sb;
+            L.w[wave][2] = stt;
+            L.w[wave][3] = fmin;  // first window of the wave (INT64_MAX: none)
+            L.w[wave][4] = prev_last;
+        }
+        if (threadIdx.x == 0) L.bad = 0;
+    }
+    __syncthreads();
+    CbAgg cwv = carry;
+    int64_t wlim = carry.ws == kCbNone ? INT64_MIN : carry.ws;
+    for (int w = 0; w < wave; ++w) {
+        cwv = cb_combine(cwv, CbAgg{L.w[w][0], L.w[w][1], L.w[w][2]});
+        wlim = max(wlim, L.w[w][4]);
+    }
+    // windows must not go back: across lanes, across waves and against the carry
+    const int64_t lim = max(before, wlim);
+    if (first != kCbNone && first < lim) mono = false;
+    if (!mono) L.bad = 1;
+    CbRound out{carry, je, false, INT64_MAX, INT64_MIN};
+    for (int w = 0; w < kW; ++w) {
+        out.total = cb_combine(out.total, CbAgg{L.w[w][0], L.w[w][1], L.w[w][2]});
+        out.first = min(out.first, L.w[w][3]);
+        out.last = max(out.last, L.w[w][4]);
+    }
+    __syncthreads();
+    if (L.bad) {
+        out.bad = true;
+        __syncthreads();
+        return out;
+    }
+    CbAgg inc{iws, sb, stt};
+    if (!hd && iws != kCbNone && iws == cwv.ws) {
+        inc.bad += cwv.bad;
+        inc.tot += cwv.tot;
+    }
+    if (iws == kCbNone) inc = cwv;  // nothing up to this lane: the carry alone
+    CbAgg run{wave_shr1_i64(inc.ws, cwv.ws), wave_shr1_i64(inc.bad, cwv.bad), wave_shr1_i64(inc.tot, cwv.tot)};
+    if (threadIdx.x == 0) L.min = je;
+    __syncthreads();
+    if (want_trip) {
+        uint32_t trip = je;
+#pragma unroll
+        for (int i = 0; i < kCbI; ++i) {
+            if (!((valm >> i) & 1u)) continue;
+            run = cb_combine(run, CbAgg{wsv[i], (int64_t)((badm >> i) & 1u), 1});
+            if (trip == je && cb_trips(b, run.bad, run.tot)) trip = j0 + i;
+        }
+        if (trip < je) atomicMin(&L.min, trip);
+    }
+    __syncthreads();
+    out.trip = L.min;
+    __syncthreads();
+    return out;
+}
+
+// kW waves per flow: k_cb_flows<kCbW> takes the flows of at least kCbShort events, k_cb_flows<1> the others (many
+// one-wave workgroups per CU: most flows are short)
+constexpr uint32_t kCbShort = 4096;
+template <int kW>
+__global__ __launch_bounds__(64 * kW) void k_cb_flows(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
+                                                      int64_t ts_base, const int64_t *__restrict__ rt_in,
+                                                      int8_t *decision, int32_t *wait_ms) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    __shared__ CbLds<kW> L;
+    constexpr uint32_t kRound = 64u * kW * kCbI;
     const uint32_t ncb = sc.counters[13], nflows = sc.counters[2], nruns = sc.counters[1];
     for (uint32_t h = blockIdx.x; h < ncb; h += gridDim.x) {
         const uint32_t fl = sc.cbf[h];
+        if (fl & kCbTiled) continue;  // decided by the tile kernels (k_cbt_*)
         const uint32_t r0 = sc.flow_first_run[fl];
         const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
         const uint32_t res = sc.run_slot[r0];
         const uint32_t jb = sc.run_start[r0], je = sc.run_end[r1 - 1];
+        if ((je - jb >= kCbShort) != (kW == kCbW)) continue;  // the other launch's
         CbDev *gb = st.cbs + st.res[res].cb_off;
         CbDev b = *gb;  // every thread holds the same copy and takes the same steps
         if (!(pay[jb].idx & F_EXIT)) {  // entries only (the breaker is not CLOSED)
             uint32_t probe = je;
             if (b.state == 1) {
                 for (uint32_t base = jb; base < je && probe == je; base += kRound) {
-                    if (threadIdx.x == 0) s_min = je;
+                    if (threadIdx.x == 0) L.min = je;
                     __syncthreads();
                     for (int i = 0; i < kCbI; ++i) {  // coalesced; a thread's later items are later entries
-                        const uint32_t j = base + (uint32_t)i * (64u * kCbW) + threadIdx.x;
+                        const uint32_t j = base + (uint32_t)i * (64u * kW) + threadIdx.x;
                         if (j < je && ts_base + (int64_t)pay[j].ts_off >= b.next_retry) {
-                            atomicMin(&s_min, j);
+                            atomicMin(&L.min, j);
                             break;
                         }
                     }
                     __syncthreads();
-                    probe = s_min;
+                    probe = L.min;
                     __syncthreads();
                 }
                 if (probe < je) {  // fromOpenToHalfOpen: the probe passes
@@ -4464,7 +4618,7 @@ __global__ __launch_bounds__(64 * kCbW) void k_cb_flows(FlowState st, FlowScratc
                     b.probe_t = ts_base + (int64_t)pay[probe].ts_off;
                 }
             }
-            for (uint32_t j = jb + threadIdx.x; j < je; j += 64 * kCbW) {
+            for (uint32_t j = jb + threadIdx.x; j < je; j += 64 * kW) {
                 const uint32_t idx = pay[j].idx & F_IDX;
                 decision[idx] = j == probe ? D_PASS : D_BLOCK_DEGRADE;
                 wait_ms[idx] = 0;  // a block's detail: the breaker's index
@@ -4486,130 +4640,14 @@ __global__ __launch_bounds__(64 * kCbW) void k_cb_flows(FlowState st, FlowScratc
                     ++base;
                     continue;
                 }
-                int64_t wsv[kCbI];
-                uint32_t badm = 0, valm = 0;
-                const uint32_t wb = base + (uint32_t)wave * kWaveItems;
-                const uint32_t j0 = wb + (uint32_t)lane * kCbI;
-                // the wave's items through LDS: coalesced loads at clamped indices, then each lane's run
-                {
-#pragma unroll
-                    for (int i = 0; i < kCbI; ++i) {
-                        const uint32_t k = (uint32_t)i * 64 + (uint32_t)lane;
-                        const uint32_t j = min(wb + k, je - 1);
-                        const Payload q = pay[j];
-                        s_ts[wave][k + k / kCbI] = q.ts_off;
-                        s_fx[wave][k + k / kCbI] = q.idx;
-                        if (b.grade == 0) s_rt[wave][k + k / kCbI] = sc.rt_sorted[j];  // sorted order (k_lexits)
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    __builtin_amdgcn_wave_barrier();
-                }
-                uint32_t tso[kCbI], fx[kCbI];
-#pragma unroll
-                for (int i = 0; i < kCbI; ++i) {
-                    const uint32_t k = (uint32_t)lane * kCbI + (uint32_t)i;
-                    tso[i] = s_ts[wave][k + k / kCbI];
-                    fx[i] = s_fx[wave][k + k / kCbI];
-                }
-                if (b.grade == 0) {
-#pragma unroll
-                    for (int i = 0; i < kCbI; ++i) {
-                        const uint32_t k = (uint32_t)lane * kCbI + (uint32_t)i;
-                        badm |= (s_rt[wave][k + k / kCbI] > b.max_allowed_rt ? 1u : 0u) << i;
-                    }
-                } else {
-#pragma unroll
-                    for (int i = 0; i < kCbI; ++i) badm |= ((fx[i] & F_ERROR) ? 1u : 0u) << i;
-                }
-                int64_t cw = kCbNone;  // the window of the previous item: most items share it (no division)
-#pragma unroll
-                for (int i = 0; i < kCbI; ++i) {
-                    const int64_t t = ts_base + (int64_t)tso[i];
-                    if (cw == kCbNone || t < cw || t - cw >= si) cw = t - t % si;
-                    wsv[i] = j0 + i < je ? cw : kCbNone;
-                    valm |= (j0 + i < je ? 1u : 0u) << i;
-                }
-                badm &= valm;
-                bool mono = true;  // inside the lane
-                int64_t first = kCbNone, last = kCbNone;
-#pragma unroll
-                for (int i = 0; i < kCbI; ++i) {
-                    if (!((valm >> i) & 1u)) continue;
-                    if (first == kCbNone) first = wsv[i];
-                    else if (wsv[i] < last) mono = false;
-                    last = wsv[i];
-                }
-                CbAgg agg{kCbNone, 0, 0};
-#pragma unroll
-                for (int i = 0; i < kCbI; ++i)
-                    if ((valm >> i) & 1u) agg = cb_combine(agg, CbAgg{wsv[i], (int64_t)((badm >> i) & 1u), 1});
-                // the lanes' tail-window counts as one DPP segmented scan: a lane starts a segment when its
-                // tail window starts inside it or differs from the windows before it (windows only grow, so
-                // the window of everything up to a lane is the prefix maximum)
-                const int64_t prev_last = wave_incl_max_i64(last == kCbNone ? INT64_MIN : last);
-                const int64_t before = wave_shr1_i64(prev_last, INT64_MIN);  // windows of the lanes before
-                const bool has = agg.ws != kCbNone;
-                int hd = (has && (first != agg.ws || (before != INT64_MIN && before != agg.ws))) ? 1 : 0;
-                int sb = (int)agg.bad, stt = (int)agg.tot;
-                wave_incl_segsum2(sb, stt, hd);
-                const int64_t iws = prev_last == INT64_MIN ? kCbNone : prev_last;  // window of lanes <= this one
-                // the waves' totals, first and last windows: each wave's carry is the round's carry and the
-                // totals of the waves before it
-                {
-                    const int64_t fmin = wave_incl_min_i64(first == kCbNone ? INT64_MAX : first);
-                    if (lane == 63) {
-                        s_w[wave][0] = iws;
-                        s_w[wave][1] = sb;
-                        s_w[wave][2] = stt;
-                        s_w[wave][3] = fmin;  // first window of the wave (INT64_MAX: none)
-                        s_w[wave][4] = prev_last;
-                    }
-                    if (threadIdx.x == 0) s_bad = 0;
-                }
-                __syncthreads();
-                CbAgg cwv = carry;
-                int64_t wlim = carry.ws == kCbNone ? INT64_MIN : carry.ws;
-                for (int w = 0; w < wave; ++w) {
-                    cwv = cb_combine(cwv, CbAgg{s_w[w][0], s_w[w][1], s_w[w][2]});
-                    wlim = max(wlim, s_w[w][4]);
-                }
-                // windows must not go back: across lanes, across waves and against the carry
-                const int64_t lim = max(before, wlim);
-                if (first != kCbNone && first < lim) mono = false;
-                if (!mono) s_bad = 1;
-                CbAgg total = carry;
-                for (int w = 0; w < kCbW; ++w) total = cb_combine(total, CbAgg{s_w[w][0], s_w[w][1], s_w[w][2]});
-                __syncthreads();
-                if (s_bad) {
+                const CbRound o = cb_round(L, b, carry, base, je, b.state == 0, pay, sc.rt_sorted, ts_base);
+                if (o.bad) {
                     seq = true;
                     break;
                 }
-                CbAgg inc{iws, sb, stt};
-                if (!hd && iws != kCbNone && iws == cwv.ws) {
-                    inc.bad += cwv.bad;
-                    inc.tot += cwv.tot;
-                }
-                if (iws == kCbNone) inc = cwv;  // nothing up to this lane: the carry alone
-                CbAgg run{wave_shr1_i64(inc.ws, cwv.ws), wave_shr1_i64(inc.bad, cwv.bad), wave_shr1_i64(inc.tot, cwv.tot)};
-                if (threadIdx.x == 0) s_min = je;
-                __syncthreads();
-                if (b.state == 0) {
-                    uint32_t trip = je;
-#pragma unroll
-                    for (int i = 0; i < kCbI; ++i) {
-                        if (!((valm >> i) & 1u)) continue;
-                        run = cb_combine(run, CbAgg{wsv[i], (int64_t)((badm >> i) & 1u), 1});
-                        if (trip == je && cb_trips(b, run.bad, run.tot)) trip = j0 + i;
-                    }
-                    if (trip < je) atomicMin(&s_min, trip);
-                }
-                __syncthreads();
-                const uint32_t k = s_min;
-                if (k < je) cb_to_open(b, ts_base + (int64_t)pay[k].ts_off);  // the first exit that trips it
-                carry = total;
+                if (o.trip < je) cb_to_open(b, ts_base + (int64_t)pay[o.trip].ts_off);  // the first exit that trips it
+                carry = o.total;
                 base += kRound;
-                __syncthreads();
             }
             b.st_start = carry.ws == kCbNone ? kAbsent : carry.ws;
             b.st_bad = carry.bad;
@@ -4624,6 +4662,169 @@ __global__ __launch_bounds__(64 * kCbW) void k_cb_flows(FlowState st, FlowScratc
         __syncthreads();
         if (threadIdx.x == 0) *gb = b;
         __syncthreads();
+    }
+}
+
+// Long breaker-only flows over the whole GPU: the flow in tiles of one round (kCbRound), one workgroup per tile.
+// Exit flows of a CLOSED or OPEN breaker: the stat window's counts combine associatively (cb_combine), so
+//   k_cbt_plan         lists the flows with at least kCbTileMin events and numbers their tiles;
+//   k_cbt_tiles<0>     each tile's counts from an empty carry, and its first and last windows;
+//   k_cbt_scan         per flow, each tile's carry in tile order -- a window that goes back anywhere (inside a
+//                      tile, between tiles, against the breaker's window) hands the whole flow back to k_cb_flows;
+//   k_cbt_tiles<1>     a CLOSED breaker's first tripping exit: each tile's against its carry, the flow's first by
+//                      atomicMin (nothing after the trip can change the breaker: OPEN exits only count, and only
+//                      an entry moves OPEN on);
+//   k_cbt_fin          the breaker's window = the flow's total, cb_to_open at the first trip.
+// Entry flows (OPEN or HALF_OPEN): k_cbt_tiles<0> finds an OPEN breaker's probe (the first entry at or after the
+// retry time, atomicMin over the tiles), k_cbt_tiles<1> writes every entry's decision, k_cbt_fin moves the
+// breaker to HALF_OPEN at the probe.
+// k_cb_flows skips the flows k_cbt_scan took (kCbTiled in their cbf word).
+__global__ __launch_bounds__(kT) void k_cbt_plan(FlowState st, FlowScratch sc, const Payload *__restrict__ pay) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    const uint32_t ncb = sc.counters[13], nflows = sc.counters[2], nruns = sc.counters[1];
+    for (uint32_t h = blockIdx.x * kT + threadIdx.x; h < ncb; h += gridDim.x * kT) {
+        const uint32_t fl = sc.cbf[h];
+        const uint32_t r0 = sc.flow_first_run[fl];
+        const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+        const uint32_t jb = sc.run_start[r0], je = sc.run_end[r1 - 1];
+        if (je - jb < kCbTileMin) continue;
+        // exits: CLOSED or OPEN at the start (HALF_OPEN: the first exit alone decides); entries: any
+        const CbDev &b = st.cbs[st.res[sc.run_slot[r0]].cb_off];
+        if ((pay[jb].idx & F_EXIT) && b.state == 2) continue;
+        const uint32_t ntile = (je - jb + kCbRound - 1) / kCbRound;
+        // the flows' and tiles' numbering is arbitrary (a tile names its flow)
+        const uint32_t k = atomicAdd(&sc.cbt_ctl[0], 1u), t0 = atomicAdd(&sc.cbt_ctl[1], ntile);
+        sc.cbt_flow[k] = h;
+        sc.cbt_off[k] = t0;
+        sc.cbt_trip[k] = 0xFFFFFFFFu;
+        sc.cbt_state[k] = 0;
+        for (uint32_t i = 0; i < ntile; ++i) sc.cbt_tile[t0 + i] = k;
+    }
+}
+
+// a tiled flow's exit range [jb, je) and breaker
+__device__ __forceinline__ void cbt_flow(const FlowState &st, const FlowScratch &sc, uint32_t k, uint32_t &h,
+                                         uint32_t &jb, uint32_t &je, CbDev *&gb) {
+    const uint32_t nflows = sc.counters[2], nruns = sc.counters[1];
+    h = sc.cbt_flow[k];
+    const uint32_t fl = sc.cbf[h] & ~kCbTiled;
+    const uint32_t r0 = sc.flow_first_run[fl];
+    const uint32_t r1 = fl + 1 < nflows ? sc.flow_first_run[fl + 1] : nruns;
+    jb = sc.run_start[r0];
+    je = sc.run_end[r1 - 1];
+    gb = st.cbs + st.res[sc.run_slot[r0]].cb_off;
+}
+
+template <bool kTrip>
+__global__ __launch_bounds__(64 * kCbW) void k_cbt_tiles(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
+                                                         int64_t ts_base, int8_t *decision, int32_t *wait_ms) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    __shared__ CbLds<kCbW> L;
+    const uint32_t ntiles = sc.cbt_ctl[1];
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t k = sc.cbt_tile[t];
+        uint32_t h, jb, je;
+        CbDev *gb;
+        cbt_flow(st, sc, k, h, jb, je, gb);
+        const uint32_t base = jb + (t - sc.cbt_off[k]) * kCbRound, end = min(base + kCbRound, je);
+        const CbDev b = *gb;
+        if (!(pay[jb].idx & F_EXIT)) {  // entries: an OPEN breaker's probe, then every entry's decision
+            if (!kTrip) {
+                if (b.state != 1) continue;
+                if (threadIdx.x == 0) L.min = je;
+                __syncthreads();
+                for (uint32_t j = base + threadIdx.x; j < end; j += 64 * kCbW)
+                    if (ts_base + (int64_t)pay[j].ts_off >= b.next_retry) {  // a thread's later items are later
+                        atomicMin(&L.min, j);
+                        break;
+                    }
+                __syncthreads();
+                if (threadIdx.x == 0 && L.min < je) atomicMin(&sc.cbt_trip[k], L.min);
+                __syncthreads();
+            } else {
+                const uint32_t probe = b.state == 1 ? sc.cbt_trip[k] : 0xFFFFFFFFu;
+                for (uint32_t j = base + threadIdx.x; j < end; j += 64 * kCbW) {
+                    const uint32_t idx = pay[j].idx & F_IDX;
+                    decision[idx] = j == probe ? D_PASS : D_BLOCK_DEGRADE;
+                    wait_ms[idx] = 0;  // a block's detail: the breaker's index
+                }
+            }
+        } else if (!kTrip) {
+            const CbRound o = cb_round(L, b, CbAgg{kCbNone, 0, 0}, base, je, false, pay, sc.rt_sorted, ts_base);
+            if (threadIdx.x == 0) {
+                CbTile &T = sc.cbt[t];
+                T.agg = o.total;
+                T.first = o.first;
+                T.last = o.last;
+                T.bad = o.bad ? 1 : 0;
+            }
+        } else {
+            if (sc.cbt_state[k] != 1 || b.state != 0) continue;  // taken, CLOSED
+            const CbRound o = cb_round(L, b, sc.cbt[t].carry, base, je, true, pay, sc.rt_sorted, ts_base);
+            if (threadIdx.x == 0 && o.trip < je) atomicMin(&sc.cbt_trip[k], o.trip);
+        }
+    }
+}
+
+// one lane per tiled flow: the tiles' carries in order, the windows checked; cbt_state 1 = taken, 2 = back
+// to k_cb_flows
+__global__ __launch_bounds__(kT) void k_cbt_scan(FlowState st, FlowScratch sc, const Payload *__restrict__ pay) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    const uint32_t nf = sc.cbt_ctl[0];
+    for (uint32_t k = blockIdx.x * kT + threadIdx.x; k < nf; k += gridDim.x * kT) {
+        uint32_t h, jb, je;
+        CbDev *gb;
+        cbt_flow(st, sc, k, h, jb, je, gb);
+        const CbDev b = *gb;
+        if (!(pay[jb].idx & F_EXIT)) {  // entries: always taken
+            sc.cbt_state[k] = 1;
+            sc.cbf[h] |= kCbTiled;
+            continue;
+        }
+        CbAgg carry{b.st_start == kAbsent ? kCbNone : b.st_start, b.st_bad, b.st_total};
+        int64_t lim = carry.ws == kCbNone ? INT64_MIN : carry.ws;
+        const uint32_t t0 = sc.cbt_off[k], t1 = t0 + (je - jb + kCbRound - 1) / kCbRound;
+        bool ok = true;
+        for (uint32_t t = t0; t < t1 && ok; ++t) {
+            const CbTile T = sc.cbt[t];
+            if (T.bad || (T.first != INT64_MAX && T.first < lim)) ok = false;
+            sc.cbt[t].carry = carry;
+            carry = cb_combine(carry, T.agg);
+            lim = max(lim, T.last);
+        }
+        sc.cbt_state[k] = ok ? 1u : 2u;
+        if (ok) {
+            sc.cbt_total[k] = carry;
+            sc.cbf[h] |= kCbTiled;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kT) void k_cbt_fin(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
+                                                int64_t ts_base) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    const uint32_t nf = sc.cbt_ctl[0];
+    for (uint32_t k = blockIdx.x * kT + threadIdx.x; k < nf; k += gridDim.x * kT) {
+        if (sc.cbt_state[k] != 1) continue;
+        uint32_t h, jb, je;
+        CbDev *gb;
+        cbt_flow(st, sc, k, h, jb, je, gb);
+        CbDev b = *gb;
+        const uint32_t trip = sc.cbt_trip[k];
+        if (!(pay[jb].idx & F_EXIT)) {  // entries: an OPEN breaker's probe passes (fromOpenToHalfOpen)
+            if (b.state == 1 && trip < je) {
+                b.state = 2;
+                b.probe_t = ts_base + (int64_t)pay[trip].ts_off;
+                *gb = b;
+            }
+            continue;
+        }
+        if (b.state == 0 && trip < je) cb_to_open(b, ts_base + (int64_t)pay[trip].ts_off);
+        const CbAgg c = sc.cbt_total[k];
+        b.st_start = c.ws == kCbNone ? kAbsent : c.ws;
+        b.st_bad = c.bad;
+        b.st_total = c.tot;
+        *gb = b;
     }
 }
 
@@ -6094,9 +6295,22 @@ void FlowEngine::launch_pseg(const FlowState &st, const FlowScratch &g, const Pa
         hipLaunchKernelGGL(k_pseg_long, dim3(std::min<uint32_t>(m / kPsegLong + 1, 2048)), dim3(64), 0, s, st,
                            (int64_t)cfg.statistic_max_rt, gs, pay, keys, el, ts_base, param, decision, wait_ms);
     }
-    if (!h_cbs.empty())
-        hipLaunchKernelGGL(k_cb_flows, dim3(std::min<uint32_t>(std::max<uint32_t>(1, m / 64), 4096)), dim3(64 * kCbW), 0, s,
-                           st, gs, pay, ts_base, rt, decision, wait_ms);
+    if (!h_cbs.empty() && m >= kCbTileMin) {  // long exit-only flows over the whole GPU
+        const uint32_t tg = std::min<uint32_t>(2 * (m / kCbRound) + 16, 4096);
+        SGA_HIP_CHECK(hipMemsetAsync(gs.cbt_ctl, 0, 8, s));
+        hipLaunchKernelGGL(k_cbt_plan, dim3(std::min<uint32_t>(m / kT + 1, 256)), dim3(kT), 0, s, st, gs, pay);
+        hipLaunchKernelGGL(k_cbt_tiles<false>, dim3(tg), dim3(64 * kCbW), 0, s, st, gs, pay, ts_base, decision, wait_ms);
+        hipLaunchKernelGGL(k_cbt_scan, dim3(m / kCbTileMin / kT + 1), dim3(kT), 0, s, st, gs, pay);
+        hipLaunchKernelGGL(k_cbt_tiles<true>, dim3(tg), dim3(64 * kCbW), 0, s, st, gs, pay, ts_base, decision, wait_ms);
+        hipLaunchKernelGGL(k_cbt_fin, dim3(m / kCbTileMin / kT + 1), dim3(kT), 0, s, st, gs, pay, ts_base);
+    }
+    if (!h_cbs.empty()) {
+        if (m >= kCbShort)
+            hipLaunchKernelGGL(k_cb_flows<kCbW>, dim3(std::min<uint32_t>(m / kCbShort, 1024)), dim3(64 * kCbW), 0, s, st,
+                               gs, pay, ts_base, rt, decision, wait_ms);
+        hipLaunchKernelGGL(k_cb_flows<1>, dim3(std::min<uint32_t>(std::max<uint32_t>(1, m / 64), 4096)), dim3(64), 0, s, st,
+                           gs, pay, ts_base, rt, decision, wait_ms);
+    }
     hipLaunchKernelGGL(k_pseg_runs, dim3((m + kTileElems - 1) / kTileElems), dim3(kT), 0, s, st, gs, pay, decision);
     const uint32_t fthreads = std::min<uint32_t>(m, nres);
     hipLaunchKernelGGL(k_pseg_apply, dim3((fthreads + kT - 1) / kT), dim3(kT), 0, s, st, (int64_t)cfg.statistic_max_rt,
@@ -6170,7 +6384,9 @@ int FlowEngine::ensure_scratch() {
                        2 * al(cap * 8) + al(cap * 4) + 2 * al(cap * 8) + al(cap * 4) + al(kRadixGhistWords * 4) + al(64) + al(cap * 4) + al((cap / 256 + 16) * 8) + al(cap * 8) +
                        al(cap * 8) +  // run_asum
                        al((cap / 64 + 2) * sizeof(WinSum)) + al((cap / 64 + 2) * 8) +  // wsum, wstate
-                       al(cap * 8);  // ev_param
+                       al(cap * 8) +  // ev_param
+                       4 * al((cap / kCbTileMin + 2) * 4) + al((cap / kCbTileMin + 2) * sizeof(CbAgg)) +  // cbt_*
+                       al((2 * (cap / kCbRound) + 16) * 4) + al((2 * (cap / kCbRound) + 16) * sizeof(CbTile)) + al(64);
         d_scratch.alloc(bytes);
         char *p = (char *)d_scratch.p;
         auto take = [&](size_t b) {
@@ -6226,6 +6442,17 @@ int FlowEngine::ensure_scratch() {
         sc.wsum = (WinSum *)take((cap / 64 + 2) * sizeof(WinSum));
         sc.wstate = (int64_t *)take((cap / 64 + 2) * 8);
         sc.ev_param = (uint64_t *)take(cap * 8);
+        {
+            const size_t nf = cap / kCbTileMin + 2, nt = 2 * (cap / kCbRound) + 16;
+            sc.cbt_flow = (uint32_t *)take(nf * 4);
+            sc.cbt_off = (uint32_t *)take(nf * 4);
+            sc.cbt_trip = (uint32_t *)take(nf * 4);
+            sc.cbt_state = (uint32_t *)take(nf * 4);
+            sc.cbt_total = (CbAgg *)take(nf * sizeof(CbAgg));
+            sc.cbt_tile = (uint32_t *)take(nt * 4);
+            sc.cbt = (CbTile *)take(nt * sizeof(CbTile));
+            sc.cbt_ctl = (uint32_t *)take(64);
+        }
         sc.cap = cap;
         scratch_cap = cap;
         d_kind.alloc(cap);

@@ -181,6 +181,15 @@ struct WinSum {
     uint32_t t0min, t0max, n0, has0;
 };
 
+struct CbAgg {
+    int64_t ws, bad, tot;  // a breaker stat window's counts: the last window's start (kCbNone: no exit), bad, total
+};
+struct CbTile {  // one tile of a long exit-only breaker flow (k_cbt_*)
+    CbAgg agg, carry;
+    int64_t first, last;  // windows
+    uint32_t bad;         // a window went back inside the tile
+};
+
 struct FlowScratch {
     uint32_t *keys[2];
     Payload *pay[2];
@@ -202,8 +211,13 @@ struct FlowScratch {
     // segments' first elements (count in counters[12]), and each run's pass / block acquire sums and passes
     uint32_t *pseg;
     uint32_t *plong;  // long regular entry segments (first element, length; count in counters[14], k_pseg_long)
-    uint32_t *cbf;
-    int64_t *rt_sorted;  // each exit's response time at its sorted position (k_lexits; k_cb_flows reads it in order)  // the breaker-only flows among them that move their breaker (count in counters[13], k_cb_flows)
+    uint32_t *cbf;       // the breaker-only flows that move their breaker (count in counters[13], k_cb_flows)
+    int64_t *rt_sorted;  // each exit's response time at its sorted position (k_lexits; k_cb_flows reads it in order)
+    // long exit-only breaker flows over the whole GPU (k_cbt_*): per taken flow its cbf index, first tile, first
+    // tripping exit, state and total; per tile its flow, counts and carry; [0] flows [1] tiles
+    uint32_t *cbt_flow, *cbt_off, *cbt_trip, *cbt_state, *cbt_tile, *cbt_ctl;
+    CbTile *cbt;
+    CbAgg *cbt_total;
     uint64_t *pel[2];
     uint32_t *seg;
     int64_t *run_pa, *run_ba;

@@ -201,6 +201,55 @@ def test_c5b_10k_degrade_rules_lognormal_rt():
     assert (d[ent] == 3).any() and (d[ent] == 0).any()  # breakers open and close
 
 
+def test_c5b_bench_config_full_batch_two_steps():
+    """bench.py --config c5b at its benched size: 2^22 entries, then the exits of the passed ones in time order,
+    for two steps (the second 2^22 later in time).  Most flows are breaker-only and one-sided per batch, so the
+    long ones go over the whole GPU in tiles (k_cbt_*) and the short ones to one-wave k_cb_flows<1>.  Every
+    decision and wait, the metric rows, the hottest nodes and every breaker's state equal the oracle's replay."""
+    import bench_local as bl
+    bl.SHARD = (0, 1)
+    rng = np.random.default_rng(107)
+    cfg = bl._cfg_c5b(rng)
+    b = cfg["batch"]
+    n_res, degrade = cfg["n_res"], cfg["degrade"]
+    orc = lt.Oracle(n_res, [], [], degrade)
+    eng, s = _local(n_res, degrade=degrade, max_batch=b.n)
+    span = b.t_hi - b.t_lo + 1
+    blocked = 0
+    for step in range(2):
+        off = step * span
+        ent = {"kind": np.zeros(b.n, np.uint8), "resource": b.res, "ts": b.ts + off, "acquire": b.acq,
+               "flags": b.flags, "rt": np.zeros(b.n, np.int64), "param": b.param}
+        ent = {k: np.ascontiguousarray(v) for k, v in ent.items()}
+        exp_d, exp_w = orc.replay(ent)
+        d, w = s.submit(ent["kind"], ent["resource"], ent["ts"], ent["acquire"], ent["flags"], ent["rt"], ent["param"])
+        bad = np.nonzero((d != exp_d) | (w != exp_w))[0]
+        assert len(bad) == 0, (f"step {step}: {len(bad)} of {b.n} entries differ; first at {bad[0]}: "
+                               f"res={b.res[bad[0]]} gpu=({d[bad[0]]},{w[bad[0]]}) oracle=({exp_d[bad[0]]},{exp_w[bad[0]]})")
+        blocked += int((exp_d == 3).sum())
+        k = np.nonzero(exp_d[b.exit_of] == 0)[0]  # the passed entries' exits, in time order
+        e = b.exit_of[k]
+        ex = {"kind": np.ones(len(k), np.uint8), "resource": b.res[e], "ts": b.exit_ts[k] + off, "acquire": b.acq[e],
+              "flags": b.exit_flags[k], "rt": b.exit_rt[k], "param": b.param[e]}
+        ex = {kk: np.ascontiguousarray(v) for kk, v in ex.items()}
+        exp_xd, _ = orc.replay(ex)
+        xd, _ = s.submit(ex["kind"], ex["resource"], ex["ts"], ex["acquire"], ex["flags"], ex["rt"], ex["param"])
+        assert (xd == exp_xd).all(), step
+    assert blocked > 0  # breakers open
+    now = int(b.t_hi + span) + 1
+    got = [(m.timestamp, s.resource_id(m.resource), m.pass_qps, m.block_qps, m.success_qps, m.exception_qps, m.rt,
+            m.occupied_pass_qps) for m in s.metrics(now, cap=1 << 20)]
+    assert got == orc.metrics(now, cap=1 << 20)
+    hot = np.argsort(-np.bincount(b.res.astype(np.int64), minlength=n_res))[:64]
+    for rid in hot:
+        v = s.node(int(rid), now)
+        assert [getattr(v, g) for g in lt.NODE_GETTERS] == orc.node(int(rid), now), int(rid)
+    for r in degrade:
+        assert s.circuit_breaker_state(r["resource"], 0) == orc.cb_state(r["resource"], 0), r["resource"]
+    orc.close()
+    eng.close()
+
+
 def test_c5a_rls_100k_descriptors():
     from sentinel_amd import cluster
     rng = np.random.default_rng(106)

@@ -184,6 +184,58 @@ def test_breaker_flows_trip_probe_half_open(grade):
     _check_batches(n_res, [b1, b2, b3, b4, b5, b6], degrade=degrade)
 
 
+@pytest.mark.parametrize("grade", [0, 1])
+def test_breaker_long_exit_flows_tiles(grade):
+    """Exit-only flows of >= 2 rounds (16384 exits) go over the whole GPU in tiles (k_cbt_*): a CLOSED breaker
+    tripped inside a tile of its third window, a long healthy flow (only the counts move), an OPEN breaker's
+    long flow (no trip, the counts carry on), a HALF_OPEN one (left to k_cb_flows), and windows that go back
+    between tiles, inside a tile and against the breaker's own window (the whole flow back to the step-by-step
+    walk).  Entries after each exit batch read the breakers' states and retry times."""
+    rng = np.random.default_rng(70 + grade)
+    n_res = 3
+    if grade == 0:
+        degrade = [{"resource": r, "grade": 0, "count": 50.0, "slow_ratio_threshold": 0.4, "min_request_amount": 20,
+                    "stat_interval_ms": 1000, "time_window": 2} for r in range(n_res)]
+    else:
+        degrade = [{"resource": r, "grade": 1, "count": 0.25, "min_request_amount": 20, "stat_interval_ms": 1000,
+                    "time_window": 2} for r in range(n_res)]
+
+    def exits(res, ts, bad):
+        ts = np.asarray(ts, np.int64)
+        bad = np.asarray(bad, bool)
+        n = len(ts)
+        rt = np.where(bad & (grade == 0), 200, rng.integers(1, 30, size=n))
+        fl = np.where(bad & (grade == 1), EV_ERROR, 0).astype(np.uint8)
+        return _batch(1, res, ts, flags=fl, rt=rt)
+
+    n = 60_000
+    res = rng.choice(n_res, size=n, p=[0.6, 0.3, 0.1])
+    t1 = T0 + np.sort(rng.integers(0, 3_000, size=n))
+    b1 = _batch(0, res, t1)
+    te = t1 + 4_000  # windows T0+4 s .. T0+7 s
+    bad = (rng.random(n) < 0.1) | ((res == 0) & (te >= T0 + 6_000) & (rng.random(n) < 0.6))
+    b2 = exits(res, te, bad)  # resource 0: ~36k exits, trips in its third window; 1: ~18k healthy; 2: ~6k
+    b3 = _batch(0, rng.choice(n_res, size=20_000), T0 + 7_500 + np.sort(rng.integers(0, 3_000, size=20_000)))
+    # the probes' exits (HALF_OPEN at the start: k_cb_flows), resource 0's bad so it opens again
+    k = 20_000
+    r4 = np.concatenate([[0, 1, 2], rng.choice(n_res, size=k, p=[0.9, 0.05, 0.05])])
+    t4 = T0 + 10_600 + np.arange(k + 3) // 20
+    b4 = exits(r4, t4, np.concatenate([[True, False, False], rng.random(k) < 0.05]))
+    # OPEN at the start: a long flow of resource 0 only counts
+    k = 30_000
+    b5 = exits(np.zeros(k), T0 + 11_800 + np.arange(k) // 20, rng.random(k) < 0.5)
+    # windows that go back: resource 1 between tiles, resource 0 inside a tile, resource 2 against its window
+    a = T0 + 13_500 + np.arange(10_000) // 10
+    r1 = exits(np.ones(20_000), np.concatenate([a, a - 1_000]), rng.random(20_000) < 0.05)
+    t0b = T0 + 13_000 + np.arange(20_000) // 10
+    t0b[3_000:3_100] -= 1_000
+    r0 = exits(np.zeros(20_000), t0b, rng.random(20_000) < 0.05)
+    b6 = {kk: np.concatenate([r1[kk], r0[kk]]) for kk in r1}
+    b7 = exits(np.full(20_000, 2), T0 + 10_000 + np.arange(20_000) // 40, rng.random(20_000) < 0.05)
+    b8 = _batch(0, rng.choice(n_res, size=5_000), T0 + 16_000 + np.arange(5_000))
+    _check_batches(n_res, [b1, b2, b3, b4, b5, b6, b7, b8], degrade=degrade)
+
+
 def test_missing_thread_count_entry_fails_the_batch():
     """The device check of k_pseg_key: a parameter event of a per-value segment flow whose thread-count entry
     is missing (fault-injected with SGA_PSEG_FORCE_MISS=1, never expected otherwise) fails the batch with
