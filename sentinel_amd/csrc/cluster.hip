@@ -4451,12 +4451,16 @@ static void side_stream_init(BatchScratch &sc) {
     } else {
         SGA_HIP_CHECK(hipStreamCreateWithFlags(&sc.side, hipStreamNonBlocking));
     }
-    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork0, hipEventDisableTiming));
-    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork, hipEventDisableTiming));
-    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_join, hipEventDisableTiming));
-    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_mid, hipEventDisableTiming));
+    // the fork / join events only order streams of this device: a device-scope release is enough (the default
+    // system-scope one writes the L2s back at every record).  SGA_EV_SYSTEM=1 (A/B knob) keeps the default.
+    static const bool ev_sys = getenv("SGA_EV_SYSTEM") && atoi(getenv("SGA_EV_SYSTEM")) == 1;
+    const unsigned evf = hipEventDisableTiming | (ev_sys ? 0u : (unsigned)hipEventReleaseToDevice);
+    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork0, evf));
+    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_fork, evf));
+    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_join, evf));
+    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_mid, evf));
     SGA_HIP_CHECK(hipStreamCreateWithFlags(&sc.side2, hipStreamNonBlocking));
-    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_prio, hipEventDisableTiming));
+    SGA_HIP_CHECK(hipEventCreateWithFlags(&sc.ev_prio, evf));
 }
 
 // The cold partition's slot bits below the bin, or 0 (the LSD sort): bins of 2^lb slots need

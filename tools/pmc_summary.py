@@ -65,7 +65,9 @@ def alg_local(k, bl):
     io = rf.get("lower_bound_bytes_per_step")
     if total is None or io is None:
         return None
-    dec = E_DEC * bl["config"].get("entries_per_step", 0) / max(1, bl.get("n_gpus", 1))
+    cfg = bl["config"]
+    dec = E_DEC * (cfg["entries_per_step_per_gpu"] if "entries_per_step_per_gpu" in cfg
+                   else cfg.get("entries_per_step", 0) / max(1, bl.get("n_gpus", 1)))
     if k == "k_lclassify":
         return io - dec
     if k == "k_lresults":
@@ -81,7 +83,7 @@ def alg_bytes(k, bl):
     + writes the cold touched rules, the hot runs read + write the hot rules, the hot results kernel
     writes the hot results (E_out = 8 B).  Everything else (the sort, scans, next hot set) is 0:
     traffic there is non-algorithmic.  Hot touched rules ~ the hot-set size of the last batch."""
-    if bl and "entries_per_step" in bl.get("config", {}):
+    if bl and ("entries_per_step" in bl.get("config", {}) or "entries_per_step_per_gpu" in bl.get("config", {})):
         return alg_local(k, bl)
     if not bl or "requests_per_step_per_gpu" not in bl.get("config", {}):
         return None
