@@ -219,7 +219,8 @@ def bench_line(path):
 
 def attach_alg(table, bl):
     """Per-kernel alg_mb / traffic_over_alg and the step total (local lines add the "(state)" row)."""
-    if bl and "entries_per_step" in bl.get("config", {}) and not any(r["kernel"] == "(state)" for r in table):
+    local = bl and ("entries_per_step" in bl.get("config", {}) or "entries_per_step_per_gpu" in bl.get("config", {}))
+    if local and not any(r["kernel"] == "(state)" for r in table):
         table.append({"kernel": "(state)", "kind": "-", "calls_per_step": 0.0, "fetch_raw_mb": 0.0, "fetch_factor": 0.0,
                       "fetch_mb": 0.0, "write_mb": 0.0, "us_per_step": None, "traffic_mb": 0.0,
                       "note": "2 * S_k per touched key, moved by the per-resource kernels (no single kernel)"})
