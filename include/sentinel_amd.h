@@ -399,6 +399,14 @@ int sga_event_poll(sga_engine *e, uint64_t ticket, int8_t *decision, int32_t *wa
 int sga_event_one(sga_engine *e, uint8_t kind, uint32_t resource, int64_t ts, int32_t acquire, uint8_t flags,
                   int64_t rt, uint64_t param, const uint64_t *param_values, size_t n_values, int8_t *decision,
                   int32_t *wait_ms);
+/* An event whose caller needs no decision -- Entry.exit, a block counted by a slot before the engine, a revoke
+ * (kinds 1-3; an entry is refused with SGA_EINVAL) -- queued like sga_event_submit and returned at once: nobody
+ * polls its ticket (written to *ticket when not NULL, ~0 for an event decided on its own), the combining round
+ * that decides it frees its slot.  Ticket order holds: it is decided before every event this thread queues later,
+ * and every other call on the engine (batches, queries, snapshots, rule loads) first waits for the events queued
+ * before it.  A round that failed holding posted events makes the next sga_event_post return SGA_EIO. */
+int sga_event_post(sga_engine *e, uint8_t kind, uint32_t resource, int64_t ts, int32_t acquire, uint8_t flags,
+                   int64_t rt, uint64_t param, const uint64_t *param_values, size_t n_values, uint64_t *ticket);
 
 /* decision codes of sga_submit_events.  wait_ms of an entry: the sleep of a pass (RateLimiter pacing,
  * SHOULD_WAIT, parameter throttle) or of SGA_PASS_WAIT; for a block, the block detail the exception

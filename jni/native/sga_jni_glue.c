@@ -101,9 +101,9 @@ int sgaj_entry(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, 
 int sgaj_exit(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, uint32_t flags, int64_t rt_ms,
               uint64_t param) {
     const uint8_t kind = 1, fl = (uint8_t)flags;
-    int8_t dec = 0;
-    int32_t wait = 0;
-    return sga_event_one(e, kind, resource, now_ms, count, fl, rt_ms, param, NULL, 0, &dec, &wait);
+    /* Entry.exit returns nothing: queued without waiting (decided in ticket order before anything this thread
+       queues or calls later) */
+    return sga_event_post(e, kind, resource, now_ms, count, fl, rt_ms, param, NULL, 0, NULL);
 }
 
 int sgaj_entry_args(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, uint32_t flags,
@@ -125,9 +125,7 @@ int sgaj_exit_args(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t cou
                    const uint64_t *words, uint32_t nargs, uint32_t nwords) {
     const uint8_t kind = SGA_KIND_EXIT, fl = (uint8_t)(flags | SGA_EV_ARGS);
     const uint64_t param = (uint64_t)nargs;
-    int8_t dec = 0;
-    int32_t wait = 0;
-    return sga_event_one(e, kind, resource, now_ms, count, fl, rt_ms, param, words, nwords, &dec, &wait);
+    return sga_event_post(e, kind, resource, now_ms, count, fl, rt_ms, param, words, nwords, NULL);
 }
 
 int sgaj_revoke_args(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, uint32_t flags,
@@ -135,18 +133,14 @@ int sgaj_revoke_args(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t c
     const uint8_t kind = SGA_KIND_REVOKE, fl = (uint8_t)(flags | SGA_EV_ARGS);
     const int64_t rt = 0;
     const uint64_t param = (uint64_t)nargs;
-    int8_t dec = 0;
-    int32_t wait = 0;
-    return sga_event_one(e, kind, resource, now_ms, count, fl, rt, param, words, nwords, &dec, &wait);
+    return sga_event_post(e, kind, resource, now_ms, count, fl, rt, param, words, nwords, NULL);
 }
 
 int sgaj_blocked(sga_engine *e, uint32_t resource, int64_t now_ms, int32_t count, uint32_t flags) {
     const uint8_t kind = SGA_KIND_BLOCKED, fl = (uint8_t)flags;
     const int64_t rt = 0;
     const uint64_t param = 0;
-    int8_t dec = 0;
-    int32_t wait = 0;
-    return sga_event_one(e, kind, resource, now_ms, count, fl, rt, param, NULL, 0, &dec, &wait);
+    return sga_event_post(e, kind, resource, now_ms, count, fl, rt, param, NULL, 0, NULL);
 }
 
 int sgaj_load_param_rules(sga_engine *e, size_t n, const uint32_t *resource, const int32_t *grade,

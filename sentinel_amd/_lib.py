@@ -123,6 +123,8 @@ SIGNATURES = {
     "sga_event_submit": (C.c_int, [C.c_void_p, C.c_uint8, C.c_uint32, C.c_int64, C.c_int32, C.c_uint8, C.c_int64,
                                    C.c_uint64, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64)]),
     "sga_event_poll": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_int8), C.POINTER(C.c_int32)]),
+    "sga_event_post": (C.c_int, [C.c_void_p, C.c_uint8, C.c_uint32, C.c_int64, C.c_int32, C.c_uint8, C.c_int64,
+                                 C.c_uint64, C.c_void_p, C.c_size_t, C.c_void_p]),
     "sga_event_one": (C.c_int, [C.c_void_p, C.c_uint8, C.c_uint32, C.c_int64, C.c_int32, C.c_uint8, C.c_int64,
                                 C.c_uint64, C.c_void_p, C.c_size_t, C.POINTER(C.c_int8), C.POINTER(C.c_int32)]),
     "sga_request_token_one": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_uint8, C.c_int64, C.c_void_p]),

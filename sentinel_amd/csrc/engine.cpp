@@ -161,14 +161,17 @@ struct EventQueue {
         int32_t acquire = 0;
         uint8_t kind = 0, flags = 0;
         uint32_t nwords = 0;
+        bool posted = false;  // sga_event_post: nobody polls it, the combiner frees the slot
         uint64_t words[kWords];
         int8_t decision = 0;
         int32_t wait = 0;
     };
     std::unique_ptr<Slot[]> ring{new Slot[kCap]};
     std::atomic<uint64_t> tail{0};
-    uint64_t head = 0;  // combiner only
+    uint64_t head = 0;                // combiner only
+    std::atomic<uint64_t> done{0};    // head as published after each round (event_flush)
     std::atomic<bool> combining{false};
+    std::atomic<bool> post_err{false};  // a round holding posted events failed: the next sga_event_post says so
     std::vector<uint8_t> kind, flags;
     std::vector<uint32_t> res;
     std::vector<int64_t> ts, rt;
@@ -897,9 +900,11 @@ using sga::CEV_N;
 
 // No exception crosses the C ABI: HIP errors map to -EIO, host allocation failures to -ENOMEM and
 // anything else (a standard-library container throwing, say) to -EIO with its message.
+static void event_flush(sga_engine *e);
 template <typename F>
 static int guarded(sga_engine *e, F &&f, bool join = true) {
     if (!e) return SGA_EINVAL;
+    event_flush(e);  // events queued before this call (posted exits included) take effect first
     std::lock_guard<std::mutex> lk(e->impl.mu);
     try {
         if (join) e->impl.join_pipeline();
@@ -1687,9 +1692,11 @@ int sga_request_token_one(sga_engine *e, int64_t flow_id, int32_t acquire, uint8
 
 // ---- coalescing queue of local events (EventQueue above)
 static int event_combine_round(sga_engine *e);
+static thread_local bool tl_in_combiner = false;
 
-int sga_event_submit(sga_engine *e, uint8_t kind, uint32_t resource, int64_t ts, int32_t acquire, uint8_t flags,
-                     int64_t rt, uint64_t param, const uint64_t *param_values, size_t n_values, uint64_t *ticket) {
+static int event_enqueue(sga_engine *e, uint8_t kind, uint32_t resource, int64_t ts, int32_t acquire, uint8_t flags,
+                         int64_t rt, uint64_t param, const uint64_t *param_values, size_t n_values, uint64_t *ticket,
+                         bool posted) {
     if (!e || !ticket) return SGA_EINVAL;
     // refused here, for this caller only, what would fail the whole coalesced batch
     if (ts < 0 || acquire < 0 || kind > SGA_KIND_REVOKE) return SGA_EINVAL;
@@ -1730,9 +1737,32 @@ int sga_event_submit(sga_engine *e, uint8_t kind, uint32_t resource, int64_t ts,
     sl.param = param;
     sl.nwords = (args || list) ? (uint32_t)n_values : 0u;
     if (sl.nwords) std::memcpy(sl.words, param_values, sl.nwords * 8);
+    sl.posted = posted;
     sl.seq.store(t + 1, std::memory_order_release);
     *ticket = t;
     return SGA_OK;
+}
+
+int sga_event_submit(sga_engine *e, uint8_t kind, uint32_t resource, int64_t ts, int32_t acquire, uint8_t flags,
+                     int64_t rt, uint64_t param, const uint64_t *param_values, size_t n_values, uint64_t *ticket) {
+    return event_enqueue(e, kind, resource, ts, acquire, flags, rt, param, param_values, n_values, ticket, false);
+}
+
+int sga_event_post(sga_engine *e, uint8_t kind, uint32_t resource, int64_t ts, int32_t acquire, uint8_t flags,
+                   int64_t rt, uint64_t param, const uint64_t *param_values, size_t n_values, uint64_t *ticket) {
+    if (!e || kind == SGA_KIND_ENTRY) return SGA_EINVAL;  // an entry's caller needs its decision
+    uint64_t t = 0;
+    const int rc = event_enqueue(e, kind, resource, ts, acquire, flags, rt, param, param_values, n_values, &t, true);
+    if (rc == SGA_ERANGE) {  // more argument words than a queue slot holds: its own batch, after the queued ones
+        int8_t d = 0;
+        int32_t w = 0;
+        if (ticket) *ticket = ~0ull;
+        return sga_submit_events_ex(e, &kind, &resource, &ts, &acquire, &flags, &rt, &param, 1, param_values,
+                                    n_values, &d, &w);
+    }
+    if (rc != SGA_OK) return rc;
+    if (ticket) *ticket = t;
+    return e->impl.eq.post_err.exchange(false) ? SGA_EIO : SGA_OK;
 }
 
 // One combining round: every filled slot from the head as one sga_submit_events_ex batch (at most max_batch);
@@ -1779,19 +1809,41 @@ static int event_combine_round(sga_engine *e) {
     if (k) {
         q.dec.assign(k, 0);
         q.wait.assign(k, 0);
+        tl_in_combiner = true;  // the batch's own call must not wait for the queue it is draining
         rc = sga_submit_events_ex(e, q.kind.data(), q.res.data(), q.ts.data(), q.acq.data(), q.flags.data(),
                                   q.rt.data(), q.param.data(), k, q.vals.empty() ? nullptr : q.vals.data(),
                                   q.vals.size(), q.dec.data(), q.wait.data());
+        tl_in_combiner = false;
+        bool posted_failed = false;
         for (uint64_t j = 0; j < k; ++j) {
             sga::EventQueue::Slot &sl = q.ring[(h + j) & (sga::EventQueue::kCap - 1)];
+            if (sl.posted) {  // nobody polls it: free the slot for the ticket kCap later
+                posted_failed |= rc != SGA_OK;
+                sl.seq.store(h + j + sga::EventQueue::kCap, std::memory_order_release);
+                continue;
+            }
             sl.decision = rc == SGA_OK ? q.dec[j] : (int8_t)-1;  // a failed batch: -1 for every event
             sl.wait = rc == SGA_OK ? q.wait[j] : 0;
             sl.seq.store(h + j + 2, std::memory_order_release);
         }
+        if (posted_failed) q.post_err.store(true, std::memory_order_release);
         q.head = h + k;
+        q.done.store(h + k, std::memory_order_release);
     }
     q.combining.store(false, std::memory_order_release);
     return rc;
+}
+
+// Every event queued before this call decided (rounds run by this thread or another).  Not inside a round's own
+// batch call (tl_in_combiner).
+static void event_flush(sga_engine *e) {
+    if (tl_in_combiner) return;
+    sga::EventQueue &q = e->impl.eq;
+    const uint64_t t = q.tail.load(std::memory_order_acquire);
+    for (int spin = 0; q.done.load(std::memory_order_acquire) < t; ++spin) {
+        (void)event_combine_round(e);
+        if (spin > 16) std::this_thread::yield();
+    }
 }
 
 int sga_event_poll(sga_engine *e, uint64_t ticket, int8_t *decision, int32_t *wait_ms) {

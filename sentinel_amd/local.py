@@ -254,6 +254,17 @@ class LocalSentinel:
         check(rc, self.engine.handle, "eventPoll")
         return int(d.value), int(w.value)
 
+    def event_post(self, kind, resource, ts, acquire, flags=0, rt=0, param=0, param_values=None) -> int:
+        """Queue an exit / block / revoke (kinds 1-3) without waiting (sga_event_post): decided in ticket order
+        before anything queued or called later.  Returns its ticket (~0: decided on its own)."""
+        pv = None if param_values is None else np.ascontiguousarray(param_values, dtype=np.uint64)
+        t = C.c_uint64()
+        rc = _lib.load().sga_event_post(self.engine.handle, int(kind), int(resource), int(ts), int(acquire), int(flags),
+                                        int(rt), int(param), pv.ctypes.data if pv is not None else None,
+                                        0 if pv is None else len(pv), C.byref(t))
+        check(rc, self.engine.handle, "eventPost")
+        return int(t.value)
+
     def event_one(self, kind, resource, ts, acquire, flags=0, rt=0, param=0, param_values=None):
         """event_submit + event_poll until decided: (decision, wait_ms)."""
         pv = None if param_values is None else np.ascontiguousarray(param_values, dtype=np.uint64)

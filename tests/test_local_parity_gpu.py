@@ -592,3 +592,78 @@ def test_event_queue_threads_equal_ticket_order():
     assert kinds.count(3) > 20 and kinds.count(2) > 20
     orc.close()
     eng.close()
+
+
+def test_event_post_exits_threads_equal_ticket_order():
+    """sga_event_post: 8 threads enter through sga_event_submit / sga_event_poll and post their exits, revokes
+    and blocks without waiting (what GpuStatisticSlot's exit path calls).  Every posted event is decided in
+    ticket order before the thread's later events; the node views read afterwards (a query waits for the queued
+    events) and every entry's decision equal the oracle replaying all events one by one in ticket order."""
+    import threading
+    n_res = 12
+    flow = [{"resource": r, "count": 8.0, **({"grade": 0, "count": 3} if r % 4 == 1 else {})} for r in range(0, n_res, 2)]
+    param = [{"resource": r, "count": 4.0, "param_idx": 0} for r in range(1, n_res, 3)]
+    degrade = [{"resource": 3, "grade": 2, "count": 3, "min_request_amount": 3, "time_window": 1}]
+    eng, s = _sentinel(n_res, 1 << 12)
+    _load(s, flow, param, degrade)
+    n_thr, per = 8, 300
+    got = [[] for _ in range(n_thr)]
+
+    def worker(k):
+        r = np.random.default_rng(700 + k)
+        for i in range(per):
+            res = int(r.integers(0, n_res))
+            now = T0 + 3 * i + int(r.integers(0, 3))
+            acq = int(r.integers(1, 3))
+            words, fl, pv = None, 8 if r.random() < 0.3 else 0, 0
+            u = r.random()
+            if u < 0.2:
+                v = int(r.integers(0, 6))
+                args = [v, int(r.integers(0, 100))] if r.random() < 0.7 else [[v, int(r.integers(0, 6))]]
+                lw = []
+                pv = lt.encode_args(args, lw)
+                words, fl = np.array(lw, np.uint64), fl | 32
+            elif u < 0.6:
+                pv, fl = int(r.integers(0, 6)), fl | 4
+            if r.random() < 0.03:  # blocked by a slot before the engine: posted
+                t = s.event_post(2, res, now, acq, fl, 0, pv, words)
+                got[k].append((t, 2, res, now, acq, fl, 0, pv, words, None))
+                continue
+            t = s.event_submit(0, res, now, acq, fl, 0, pv, words)
+            d = None
+            while d is None:
+                d = s.event_poll(t)
+            got[k].append((t, 0, res, now, acq, fl, 0, pv, words, d))
+            if d[0] in (0, 4):  # passed: exit (or revoke), posted
+                rev = r.random() < 0.1
+                xt = now if rev else now + int(r.integers(1, 20))
+                xfl = (fl & (4 | 8 | 32)) | (2 if (not rev and r.random() < 0.2) else 0)
+                xrt = 0 if rev else xt - now
+                t2 = s.event_post(3 if rev else 1, res, xt, acq, xfl, xrt, pv, words)
+                got[k].append((t2, 3 if rev else 1, res, xt, acq, xfl, xrt, pv, words, None))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(n_thr)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    allr = sorted((x for g in got for x in g), key=lambda x: x[0])
+    assert len({x[0] for x in allr}) == len(allr)
+    orc = lt.Oracle(n_res, flow, param, degrade)
+    for (t, kind, res, now, acq, fl, rt, pv, words, d) in allr:
+        ev = {"kind": np.array([kind], np.uint8), "resource": np.array([res], np.uint32),
+              "ts": np.array([now], np.int64), "acquire": np.array([acq], np.int32),
+              "flags": np.array([fl], np.uint8), "rt": np.array([rt], np.int64), "param": np.array([pv], np.uint64)}
+        if words is not None:
+            ev["param_values"] = words
+        ed, ew = orc.replay(ev)
+        if d is not None:
+            assert (d[0], d[1]) == (int(ed[0]), int(ew[0])), (t, kind, res, now, fl, d, int(ed[0]), int(ew[0]))
+    end = max(x[3] for x in allr) + 1
+    _assert_nodes(s, orc, n_res, end)  # the node queries wait for the posted events
+    kinds = [x[1] for x in allr]
+    assert kinds.count(1) > 500 and kinds.count(3) > 20 and kinds.count(2) > 20
+    with pytest.raises(Exception):
+        s.event_post(0, 0, T0, 1)  # an entry needs its decision
+    orc.close()
+    eng.close()

@@ -144,6 +144,7 @@ int main(int argc, char **argv) {
         report("SphU.entry (sga_submit_events, one entry)", lat, us_since(w0) / 1e6, 1);
         // SphU.entry + Entry.exit through the coalescing event queue (sga_event_one), 1 thread and T threads:
         // what GpuStatisticSlot calls per entry (jni/native/sga_jni_glue.c sgaj_entry / sgaj_exit)
+        for (int post = 0; post < 2; ++post)  // exits waited for (sga_event_one) or posted (sga_event_post)
         for (int nt : {1, threads}) {
             std::vector<std::vector<double>> l2(nt);
             std::vector<std::thread> th;
@@ -153,7 +154,7 @@ int main(int argc, char **argv) {
                 th.emplace_back([&, k] {
                     for (int i = 0; i < calls; ++i) {
                         const uint32_t res = (uint32_t)((i * 7919 + k * 104729) % n_res);
-                        const int64_t ts = t0 + 20000 + (nt > 1 ? 50000 : 0) + i / 10;
+                        const int64_t ts = t0 + 20000 + (nt > 1 ? 50000 : 0) + post * 100000 + i / 10;
                         int8_t dec;
                         int32_t wait;
                         const auto t = clk::now();
@@ -161,7 +162,8 @@ int main(int argc, char **argv) {
                         l2[k].push_back(us_since(t));
                         if (dec == 0) {
                             passed.fetch_add(1);
-                            sga_event_one(e, 1, res, ts + 5, 1, 0, 5, 0, nullptr, 0, &dec, &wait);
+                            if (post) sga_event_post(e, 1, res, ts + 5, 1, 0, 5, 0, nullptr, 0, nullptr);
+                            else sga_event_one(e, 1, res, ts + 5, 1, 0, 5, 0, nullptr, 0, &dec, &wait);
                         }
                     }
                 });
@@ -169,8 +171,10 @@ int main(int argc, char **argv) {
             const double wall = us_since(w1) / 1e6;
             std::vector<double> all;
             for (auto &v : l2) all.insert(all.end(), v.begin(), v.end());
-            report(nt == 1 ? "SphU.entry (sga_event_one; each passed entry also exits)"
-                           : "SphU.entry (sga_event_one, concurrent; each passed entry also exits)",
+            report(post ? (nt == 1 ? "SphU.entry (sga_event_one; each passed entry's exit posted, sga_event_post)"
+                                   : "SphU.entry (sga_event_one, concurrent; each passed entry's exit posted)")
+                        : (nt == 1 ? "SphU.entry (sga_event_one; each passed entry also exits)"
+                                   : "SphU.entry (sga_event_one, concurrent; each passed entry also exits)"),
                    all, wall, nt);
         }
     }
