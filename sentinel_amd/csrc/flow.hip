@@ -1777,29 +1777,34 @@ __device__ __forceinline__ void replay_event(const Ctx &c, const FlowScratch &sc
 // each resource in the batch leads: its lane replays the resource's events in arrival order with the whole slot
 // chain (replay_event, as lane_run does for a resource with F_SPECIAL events), the resources side by side; then
 // one lane adds the inbound events to ENTRY_NODE in arrival order (no SystemRule check on this path).
-constexpr int kLSmall = 1024;
+#ifndef SGA_LSMALL_THREADS
+#define SGA_LSMALL_THREADS 512
+#endif
+// threads of k_lsmall: fewer than the chunk's events, so each lane holds the slot chain in registers (at 1024
+// threads a lane gets 128 VGPRs and the chain spills to scratch, a memory round trip per spilled value)
+constexpr int kLSmall = SGA_LSMALL_THREADS;
 __global__ __launch_bounds__(kLSmall) void k_lsmall(FlowState st, int64_t max_rt, FlowScratch fs,
                                                     const uint32_t *__restrict__ resource,
                                                     const uint32_t *__restrict__ ts_off, int64_t ts_base,
                                                     const int32_t *__restrict__ acquire,
                                                     const int64_t *__restrict__ rt_in, uint32_t n, int8_t *decision,
                                                     int32_t *wait_ms, uint32_t *ovf_out, int zero_ovf) {
-    __shared__ uint32_t sres[kLSmall];
+    __shared__ uint32_t sres[FlowEngine::kSmallEvents];
     const uint32_t i = threadIdx.x;
     const Ctx c{st, max_rt};
     if (zero_ovf && i == 0) *st.overflow = 0;  // no lru_prepare ahead of this kernel: the batch's overflow word
-    if (i < n) {
-        sres[i] = resource[i];
-        decision[i] = D_PASS;
-        wait_ms[i] = 0;
+    for (uint32_t k = i; k < n; k += kLSmall) {
+        sres[k] = resource[k];
+        decision[k] = D_PASS;
+        wait_ms[k] = 0;
     }
     __syncthreads();
-    if (i < n) {
-        const uint32_t r = sres[i];
+    for (uint32_t k = i; k < n; k += kLSmall) {  // each resource's first event leads: its lane replays them in order
+        const uint32_t r = sres[k];
         bool lead = r < st.nres;
-        for (uint32_t j = 0; j < i && lead; ++j) lead = sres[j] != r;
+        for (uint32_t j = 0; j < k && lead; ++j) lead = sres[j] != r;
         if (lead)
-            for (uint32_t j = i; j < n; ++j) {
+            for (uint32_t j = k; j < n; ++j) {
                 if (sres[j] != r) continue;
                 const Payload q{j | F_SPECIAL, ts_off[j], (uint32_t)acquire[j] & 0x7FFFFFFFu, 0u};
                 replay_event<true>(c, fs, r, q, ts_base, rt_in, fs.in_param, decision, wait_ms);
