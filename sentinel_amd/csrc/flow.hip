@@ -4239,6 +4239,11 @@ __global__ __launch_bounds__(kT) void k_pseg_check(FlowState st, const uint32_t 
     }
 }
 
+__device__ __forceinline__ int64_t shfl_up_i64(int64_t v, int o) {
+    const int lo = __shfl_up((int)(uint32_t)v, o, 64), hi = __shfl_up((int)(uint32_t)((uint64_t)v >> 32), o, 64);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
 // 2. segment heads of the sorted elements
 //    and each segment's flag word (the b word of its thread-count entry, which a thread count never uses):
 //    kSegExit / kSegEntry when it holds exits / entries, kSegIrregular when an entry's acquire count differs
@@ -4253,7 +4258,22 @@ __global__ __launch_bounds__(kT) void k_pseg_heads(FlowState st, FlowScratch sc,
         const uint32_t e = e0 + threadIdx.x;
         const uint64_t x = e < m ? el[e] : none;
         const uint64_t k = x >> 32;
-        const bool head = k != none >> 32 && (e == 0 || (el[e - 1] >> 32) != k);
+        // the previous element and its payload from the lane before (lane 0 loads them): one payload gather
+        // per element instead of two
+        uint64_t xp = shfl_up_i64((int64_t)x, 1);
+        if (lane == 0) xp = (e > 0 && e - 1 < m) ? el[e - 1] : none;
+        const bool head = k != none >> 32 && (e == 0 || (xp >> 32) != k);
+        const Payload q = pay[(uint32_t)x];  // every lane (a padding lane reads element 0)
+        Payload pq;
+        pq.idx = (uint32_t)__shfl_up((int)q.idx, 1, 64);
+        pq.ts_off = (uint32_t)__shfl_up((int)q.ts_off, 1, 64);
+        pq.acq_prio = (uint32_t)__shfl_up((int)q.acq_prio, 1, 64);
+        if (lane == 0 && e > 0 && (xp >> 32) != none >> 32) {
+            const Payload p0 = pay[(uint32_t)xp];
+            pq.idx = p0.idx;
+            pq.ts_off = p0.ts_off;
+            pq.acq_prio = p0.acq_prio;
+        }
         const uint64_t hb = __ballot(head);  // one counter atomic per wave
         if (hb) {
             const int first = __ffsll((unsigned long long)hb) - 1;
@@ -4262,16 +4282,26 @@ __global__ __launch_bounds__(kT) void k_pseg_heads(FlowState st, FlowScratch sc,
             base = (uint32_t)__shfl((int)base, first, 64);
             if (head) sc.seg[base + (uint32_t)__popcll(hb & ((1ull << lane) - 1ull))] = e;
         }
-        if (k == none >> 32) continue;
-        const Payload q = pay[(uint32_t)x];
+        const bool valid = k != none >> 32;
         int64_t f = (q.idx & F_EXIT) ? kSegExit : kSegEntry;
-        if (!head && !(q.idx & F_EXIT)) {
-            const Payload pq = pay[(uint32_t)el[e - 1]];
+        if (valid && !head && !(q.idx & F_EXIT)) {
             if (!(pq.idx & F_EXIT) && ((pq.acq_prio & 0x7FFFFFFFu) != (q.acq_prio & 0x7FFFFFFFu) || q.ts_off < pq.ts_off))
                 f |= kSegIrregular;
         }
+        // one flag update per run of equal keys in the wave (the elements are sorted, so a key's lanes are
+        // contiguous): its first lane ORs the run's flags in -- a long segment's lanes would otherwise all meet
+        // at one address
+        const bool lead = valid && (lane == 0 || (xp >> 32) != k);
+        const uint64_t ld = __ballot(lead), vm = __ballot(valid);
+        const uint64_t mx = __ballot(valid && (f & kSegExit)), me = __ballot(valid && (f & kSegEntry)),
+                       mi = __ballot(valid && (f & kSegIrregular));
+        if (!lead) continue;
+        const uint64_t after = lane == 63 ? 0ull : (ld & (~0ull << (lane + 1)));
+        const int rend = after ? __builtin_ctzll(after) : 64;  // the run: lanes [lane, rend)
+        const uint64_t run = (rend == 64 ? ~0ull : ((1ull << rend) - 1ull)) & (~0ull << lane) & vm;
+        const int64_t fr = ((mx & run) ? kSegExit : 0) | ((me & run) ? kSegEntry : 0) | ((mi & run) ? kSegIrregular : 0);
         int64_t *w = &st.ttab[k].b;
-        if ((*w & f) != f) atomicOr((unsigned long long *)w, (unsigned long long)f);  // a read first: hot segments
+        if ((*w & fr) != fr) atomicOr((unsigned long long *)w, (unsigned long long)fr);  // a read first: hot segments
     }
 }
 
@@ -4416,10 +4446,6 @@ __device__ __forceinline__ CbAgg cb_combine(const CbAgg &p, const CbAgg &x) {
     if (x.ws == kCbNone) return p;
     if (x.ws == p.ws) return CbAgg{x.ws, p.bad + x.bad, p.tot + x.tot};
     return x;
-}
-__device__ __forceinline__ int64_t shfl_up_i64(int64_t v, int o) {
-    const int lo = __shfl_up((int)(uint32_t)v, o, 64), hi = __shfl_up((int)(uint32_t)((uint64_t)v >> 32), o, 64);
-    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 constexpr int kCbW = 8;  // waves per flow: a round covers kCbW x 64 x kCbI exits
 constexpr uint32_t kCbRound = 64u * kCbW * kCbI;
