@@ -2481,8 +2481,8 @@ __global__ __launch_bounds__(kThreads) void k_hscan_down(BatchScratch sc, uint32
 //   counts  the key kernel adds each element to prow[group][hot id] as it writes it (no-return atomics);
 //   cols    k_psort_cols: per hot id, the groups' exclusive prefix (pstart) and the total (ptot);
 //   scatter k_psort_scatter: per group, the hot ids' starts (prefix of ptot) + pstart; the group's elements in
-//           arrival order, each to start + its rank so far (same-word LDS atomics of one wave instruction
-//           return in lane order, lds_lane_order_ok); it zeroes its prow row for the next batch.
+//           arrival order, each to start + its rank so far (per round: the lanes of one hot id found by ballots,
+//           one LDS add by the lowest, ranks in lane order); it zeroes its prow row for the next batch.
 // Small workgroups (one wave, 16 KB LDS): they run beside the cold stage's wide workgroups.
 __device__ __forceinline__ uint32_t ps_per_group(uint32_t nseg) { return (nseg + kPsGroups - 1) / kPsGroups; }
 
@@ -2585,7 +2585,16 @@ __global__ __launch_bounds__(64) void k_psort_scatter(BatchScratch sc, uint32_t 
 #pragma unroll
             for (int q = 0; q < kPre; ++q) {
                 const uint32_t j = j0 + (uint32_t)(q * 64 + lane);
-                if (j < tot) out[atomicAdd(&base[el_slot(e[q])], 1u)] = e[q];
+                // one LDS add per distinct hot id of the instruction (its lowest lane), ranks in lane order by
+                // ballots: no reliance on the order same-address atomics of one instruction return in
+                const bool v = j < tot;
+                const uint32_t hid = v ? el_slot(e[q]) : 0u;
+                const uint64_t peers = match_lanes(hid, 12, v);
+                const int lead = peers ? __ffsll((unsigned long long)peers) - 1 : lane;
+                uint32_t old = 0;
+                if (v && lead == lane) old = atomicAdd(&base[hid], (uint32_t)__popcll(peers));
+                old = (uint32_t)__shfl((int)old, lead, 64);
+                if (v) out[old + (uint32_t)__popcll(peers & lanemask_lt64(lane))] = e[q];
             }
         }
     }

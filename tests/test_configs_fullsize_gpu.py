@@ -121,16 +121,18 @@ def test_c2_100k_mixed_controllers_zipf():
     assert (d[ent] == 0).any() and (d[ent] == 1).any() and (st["kind"] == 1).sum() > 100_000
 
 
-def test_c2_bench_mix_bit_exact():
+@pytest.mark.parametrize("log_n", [22, 24])
+def test_c2_bench_mix_bit_exact(log_n):
     """bench.py --config c2's own mix (bench_local._cfg_c2): count U{5..5000} -- RateLimiter rules above
     2000 QPS pace acquire-1 entries at zero cost in k_lwave --, lambda 10^7 entries per virtual second,
-    WarmUp 10 s, maxQueueingTimeMs 500, 5 % acquiring 2..5, at 2^22 entries per batch.  As the bench does:
+    WarmUp 10 s, maxQueueingTimeMs 500, 5 % acquiring 2..5, at 2^22 entries per batch and at the bench's own
+    2^24 (the hottest resources' later windows, k_lwave's grid at the benched batch size).  As the bench does:
     one batch of entries, then the exits of the entries that passed (exit time = entry time + a geometric
     RT), on the engine and on the oracle; every decision and wait equal, then the metric rows and the
     hottest nodes."""
     import bench_local as bl
     rng = np.random.default_rng(102)
-    cfg = bl._cfg_c2(rng, n=1 << 22)
+    cfg = bl._cfg_c2(rng, n=1 << log_n)
     b = cfg["batch"]
     n_res, flow = cfg["n_res"], cfg["flow"]
     ent = {"kind": np.zeros(b.n, np.uint8), "resource": b.res, "ts": b.ts, "acquire": b.acq, "flags": b.flags,
