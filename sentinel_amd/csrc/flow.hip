@@ -4310,7 +4310,10 @@ __global__ __launch_bounds__(kT) void k_pseg_heads(FlowState st, FlowScratch sc,
 //    add/decreaseThreadCount as param_threads), the entries, their access stamps and the owners' present
 //    counts written back once (free mode: the count pass keeps these owners below capacity)
 constexpr int kPsegG = 8;       // elements loaded ahead
-constexpr int kPsegLong = 512;  // regular entry segments this long go to k_pseg_long
+#ifndef SGA_PSEG_LONG
+#define SGA_PSEG_LONG 512
+#endif
+constexpr int kPsegLong = SGA_PSEG_LONG;  // regular entry segments this long go to k_pseg_long
 __global__ __launch_bounds__(kT) void k_pseg_solve(FlowState st, int64_t max_rt, FlowScratch sc,
                                                    const Payload *__restrict__ pay, const uint32_t *__restrict__ keys,
                                                    const uint64_t *__restrict__ el, uint32_t m, int64_t ts_base,
@@ -4892,6 +4895,23 @@ __device__ uint32_t pseg_upper(const Payload *__restrict__ pay, const uint64_t *
     const uint64_t b = __ballot(p < hi && pseg_time(pay, el, ts_base, p) > x);
     return b ? lo + (uint32_t)(__ffsll((unsigned long long)b) - 1) : hi;
 }
+// The long segments' blocks written over the whole GPU ahead of k_pseg_long, which then writes only its passes
+// (a throttle segment passes one entry per stretch: one wave writing every block was most of its time)
+__global__ __launch_bounds__(kT) void k_pseg_prefill(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
+                                                     const uint64_t *__restrict__ el, int8_t *decision,
+                                                     int32_t *wait_ms) {
+    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
+    const uint32_t nl = sc.counters[14];
+    for (uint32_t h = blockIdx.y; h < nl; h += gridDim.y) {
+        const uint32_t e0 = sc.plong[2 * h], e1 = e0 + sc.plong[2 * h + 1];
+        for (uint32_t e = e0 + blockIdx.x * kT + threadIdx.x; e < e1; e += gridDim.x * kT) {
+            const uint32_t ix = pay[(uint32_t)el[e]].idx & F_IDX;
+            decision[ix] = D_BLOCK_PARAM;
+            wait_ms[ix] = 0;
+        }
+    }
+}
+
 __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, FlowScratch sc,
                                                   const Payload *__restrict__ pay, const uint32_t *__restrict__ keys,
                                                   const uint64_t *__restrict__ el, int64_t ts_base,
@@ -4916,9 +4936,10 @@ __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, 
         const bool p0 = pe.a != kPAbsent;
         int64_t npass = 0;
         uint32_t last_pass = e1;
-        // decisions of [lo, hi) on all lanes
+        // decisions of [lo, hi) on all lanes (blocks: written already, k_pseg_prefill)
         auto fill = [&](uint32_t lo, uint32_t hi, bool pass) {
-            const int8_t d = pass ? D_PASS : D_BLOCK_PARAM;
+            if (!pass) return;
+            const int8_t d = D_PASS;
             for (uint32_t e = lo + lane; e < hi; e += 4 * 64) {
                 uint32_t ix[4];
 #pragma unroll
@@ -6323,6 +6344,8 @@ void FlowEngine::launch_pseg(const FlowState &st, const FlowScratch &g, const Pa
         }
         hipLaunchKernelGGL(k_pseg_solve, dim3(std::min<uint32_t>((m + kT - 1) / kT, 4096)), dim3(kT), 0, s, st,
                            (int64_t)cfg.statistic_max_rt, gs, pay, keys, el, m, ts_base, param, decision, wait_ms);
+        hipLaunchKernelGGL(k_pseg_prefill, dim3(64, std::min<uint32_t>(m / kPsegLong + 1, 64)), dim3(kT), 0, s, st, gs,
+                           pay, el, decision, wait_ms);
         hipLaunchKernelGGL(k_pseg_long, dim3(std::min<uint32_t>(m / kPsegLong + 1, 2048)), dim3(64), 0, s, st,
                            (int64_t)cfg.statistic_max_rt, gs, pay, keys, el, ts_base, param, decision, wait_ms);
     }
