@@ -4244,7 +4244,8 @@ __device__ __forceinline__ int64_t shfl_up_i64(int64_t v, int o) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-// 2. segment heads of the sorted elements
+// 2. segment heads of the sorted elements, the elements' payloads gathered once into sorted order (sc.spay:
+//    every later pass streams them)
 //    and each segment's flag word (the b word of its thread-count entry, which a thread count never uses):
 //    kSegExit / kSegEntry when it holds exits / entries, kSegIrregular when an entry's acquire count differs
 //    from the previous entry's or its time goes back (the closed forms of k_pseg_solve / k_pseg_long need
@@ -4259,21 +4260,17 @@ __global__ __launch_bounds__(kT) void k_pseg_heads(FlowState st, FlowScratch sc,
         const uint64_t x = e < m ? el[e] : none;
         const uint64_t k = x >> 32;
         // the previous element and its payload from the lane before (lane 0 loads them): one payload gather
-        // per element instead of two
+        // per element, stored in sorted order
         uint64_t xp = shfl_up_i64((int64_t)x, 1);
         if (lane == 0) xp = (e > 0 && e - 1 < m) ? el[e - 1] : none;
         const bool head = k != none >> 32 && (e == 0 || (xp >> 32) != k);
         const Payload q = pay[(uint32_t)x];  // every lane (a padding lane reads element 0)
+        if (k != none >> 32) sc.spay[e] = q;
         Payload pq;
         pq.idx = (uint32_t)__shfl_up((int)q.idx, 1, 64);
         pq.ts_off = (uint32_t)__shfl_up((int)q.ts_off, 1, 64);
         pq.acq_prio = (uint32_t)__shfl_up((int)q.acq_prio, 1, 64);
-        if (lane == 0 && e > 0 && (xp >> 32) != none >> 32) {
-            const Payload p0 = pay[(uint32_t)xp];
-            pq.idx = p0.idx;
-            pq.ts_off = p0.ts_off;
-            pq.acq_prio = p0.acq_prio;
-        }
+        if (lane == 0 && e > 0 && (xp >> 32) != none >> 32) pq = pay[(uint32_t)xp];
         const uint64_t hb = __ballot(head);  // one counter atomic per wave
         if (hb) {
             const int first = __ffsll((unsigned long long)hb) - 1;
@@ -4329,7 +4326,7 @@ __global__ __launch_bounds__(kT) void k_pseg_solve(FlowState st, int64_t max_rt,
         const uint32_t j0 = (uint32_t)el[e0];
         const uint32_t res = keys[j0];
         const ParamRuleDev prule = st.prules[st.res[res].prule_off];
-        const uint64_t v = param_in[pay[j0].idx & F_IDX];
+        const uint64_t v = param_in[sc.spay[e0].idx & F_IDX];
         PEntry *const tp = st.ttab + key;
         int64_t ta = tp->a;
         const bool t0 = ta != kPAbsent;
@@ -4377,7 +4374,7 @@ __global__ __launch_bounds__(kT) void k_pseg_solve(FlowState st, int64_t max_rt,
                 }
                 if (rem) st0 = ((rem & 1) ? (st0 == kPAbsent ? 0 : kPAbsent) : st0);
                 ta = st0;
-                tst = lru_stamp(st, pay[(uint32_t)el[e1 - 1]].idx & F_IDX, 0);
+                tst = lru_stamp(st, sc.spay[e1 - 1].idx & F_IDX, 0);
                 more = false;
             }
         }
@@ -4387,7 +4384,7 @@ __global__ __launch_bounds__(kT) void k_pseg_solve(FlowState st, int64_t max_rt,
 #pragma unroll
             for (int u = 0; u < kPsegG; ++u) x[u] = el[min(g + u, m - 1)];
 #pragma unroll
-            for (int u = 0; u < kPsegG; ++u) q[u] = pay[(uint32_t)x[u]];
+            for (int u = 0; u < kPsegG; ++u) q[u] = sc.spay[min(g + u, m - 1)];
 #pragma unroll
             for (int u = 0; u < kPsegG; ++u) {
                 if (!more || g + u >= m || (x[u] >> 32) != key) {
@@ -4870,18 +4867,16 @@ __global__ __launch_bounds__(kT) void k_cbt_fin(FlowState st, FlowScratch sc, co
 //    an entry passes iff expected - t < maxQueueingTimeMs or expected <= t, so the next pass is one search
 //    for the first t >= expected - max(maxQueueingTimeMs - 1, 0).  Searches are 64-ary (a probe per lane),
 //    fills write the decisions on all lanes.
-__device__ __forceinline__ int64_t pseg_time(const Payload *__restrict__ pay, const uint64_t *__restrict__ el,
-                                             int64_t ts_base, uint32_t e) {
-    return ts_base + (int64_t)pay[(uint32_t)el[e]].ts_off;
+__device__ __forceinline__ int64_t pseg_time(const Payload *__restrict__ spay, int64_t ts_base, uint32_t e) {
+    return ts_base + (int64_t)spay[e].ts_off;
 }
 // first e in [lo, hi) with time > x (hi if none); times non-decreasing over [lo, hi)
-__device__ uint32_t pseg_upper(const Payload *__restrict__ pay, const uint64_t *__restrict__ el, int64_t ts_base,
-                               uint32_t lo, uint32_t hi, int64_t x) {
+__device__ uint32_t pseg_upper(const Payload *__restrict__ sp, int64_t ts_base, uint32_t lo, uint32_t hi, int64_t x) {
     const int lane = threadIdx.x & 63;
     while (hi - lo > 64) {
         const uint32_t step = (hi - lo + 63) / 64;
         const uint32_t p = lo + (uint32_t)lane * step;
-        const bool gt = p < hi && pseg_time(pay, el, ts_base, p) > x;
+        const bool gt = p < hi && pseg_time(sp, ts_base, p) > x;
         const uint64_t b = __ballot(gt);
         if (!b) {  // every probe <= x: the answer is past the last probe inside [lo, hi)
             lo = lo + ((hi - lo - 1) / step) * step + 1;
@@ -4893,7 +4888,7 @@ __device__ uint32_t pseg_upper(const Payload *__restrict__ pay, const uint64_t *
         lo = lo + (uint32_t)(f - 1) * step + 1;
     }
     const uint32_t p = lo + (uint32_t)lane;
-    const uint64_t b = __ballot(p < hi && pseg_time(pay, el, ts_base, p) > x);
+    const uint64_t b = __ballot(p < hi && pseg_time(sp, ts_base, p) > x);
     return b ? lo + (uint32_t)(__ffsll((unsigned long long)b) - 1) : hi;
 }
 // The long segments' blocks written over the whole GPU ahead of k_pseg_long, which then writes only its passes
@@ -4906,7 +4901,7 @@ __global__ __launch_bounds__(kT) void k_pseg_prefill(FlowState st, FlowScratch s
     for (uint32_t h = blockIdx.y; h < nl; h += gridDim.y) {
         const uint32_t e0 = sc.plong[2 * h], e1 = e0 + sc.plong[2 * h + 1];
         for (uint32_t e = e0 + blockIdx.x * kT + threadIdx.x; e < e1; e += gridDim.x * kT) {
-            const uint32_t ix = pay[(uint32_t)el[e]].idx & F_IDX;
+            const uint32_t ix = sc.spay[e].idx & F_IDX;
             decision[ix] = D_BLOCK_PARAM;
             wait_ms[ix] = 0;
         }
@@ -4925,7 +4920,8 @@ __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, 
     for (uint32_t h = blockIdx.x; h < nl; h += gridDim.x) {
         const uint32_t e0 = sc.plong[2 * h], e1 = e0 + sc.plong[2 * h + 1];
         const uint64_t key = el[e0] >> 32;
-        const Payload q0 = pay[(uint32_t)el[e0]];
+        const Payload *__restrict__ sp = sc.spay;
+        const Payload q0 = sp[e0];
         const uint32_t res = keys[(uint32_t)el[e0]];
         const ParamRuleDev prule = st.prules[st.res[res].prule_off];
         const uint64_t v = param_in[q0.idx & F_IDX];
@@ -4944,9 +4940,7 @@ __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, 
             for (uint32_t e = lo + lane; e < hi; e += 4 * 64) {
                 uint32_t ix[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) ix[u] = (uint32_t)el[min(e + 64 * u, hi - 1)];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) ix[u] = pay[ix[u]].idx & F_IDX;
+                for (int u = 0; u < 4; ++u) ix[u] = sp[min(e + 64 * u, hi - 1)].idx & F_IDX;
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     if (e + 64 * u < hi) {
@@ -4961,7 +4955,7 @@ __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, 
         };
         auto one = [&](uint32_t e, bool pass, int64_t w) {
             if (lane == 0) {
-                const uint32_t ix = pay[(uint32_t)el[e]].idx & F_IDX;
+                const uint32_t ix = sp[e].idx & F_IDX;
                 decision[ix] = pass ? D_PASS : D_BLOCK_PARAM;
                 wait_ms[ix] = pass ? (int32_t)w : 0;
             }
@@ -4983,22 +4977,22 @@ __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, 
                 const int64_t slack = prule.max_queue > 0 ? prule.max_queue - 1 : 0;
                 while (e < e1) {
                     if (pe.a == kPAbsent) {
-                        pe.a = pseg_time(pay, el, ts_base, e);
+                        pe.a = pseg_time(sp, ts_base, e);
                         one(e++, true, 0);
                         continue;
                     }
-                    if (cost == 0 && pseg_time(pay, el, ts_base, e) >= pe.a) {
+                    if (cost == 0 && pseg_time(sp, ts_base, e) >= pe.a) {
                         // a zero cost (token count above 2000 x acquire x duration): with times
                         // non-decreasing every entry from here passes without a wait, the last one's time kept
                         fill(e, e1, true);
-                        pe.a = pseg_time(pay, el, ts_base, e1 - 1);
+                        pe.a = pseg_time(sp, ts_base, e1 - 1);
                         break;
                     }
                     const int64_t expected = pe.a + cost;
-                    const uint32_t r = pseg_upper(pay, el, ts_base, e, e1, expected - slack - 1);
+                    const uint32_t r = pseg_upper(sp, ts_base, e, e1, expected - slack - 1);
                     fill(e, r, false);
                     if (r >= e1) break;
-                    const int64_t tr = pseg_time(pay, el, ts_base, r);
+                    const int64_t tr = pseg_time(sp, ts_base, r);
                     const int64_t w = expected - tr;
                     pe.a = w > 0 ? expected : tr;
                     one(r, true, w > 0 ? w : 0);
@@ -5009,12 +5003,12 @@ __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, 
                 const int64_t dur_ms = lwrap_mul(prule.duration, 1000);
                 while (e < e1) {
                     if (pe.a == kPAbsent) {
-                        pe.a = pseg_time(pay, el, ts_base, e);
+                        pe.a = pseg_time(sp, ts_base, e);
                         if (pe.b == kPAbsent) pe.b = max_count - a;
                         one(e++, true, 0);
                         continue;
                     }
-                    const uint32_t r = pseg_upper(pay, el, ts_base, e, e1, pe.a + dur_ms);  // the next refill
+                    const uint32_t r = pseg_upper(sp, ts_base, e, e1, pe.a + dur_ms);  // the next refill
                     int64_t k = 0;
                     if (pe.b != kPAbsent && pe.b >= 0) k = a > 0 ? min((int64_t)(r - e), pe.b / a) : (int64_t)(r - e);
                     fill(e, e + (uint32_t)k, true);
@@ -5023,7 +5017,7 @@ __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, 
                     e = r;
                     if (e >= e1) break;
                     int64_t w = 0;  // the refill: one exact step
-                    const bool ok = param_pass_qps(c, prule, pe, v, a, pseg_time(pay, el, ts_base, e), &w);
+                    const bool ok = param_pass_qps(c, prule, pe, v, a, pseg_time(sp, ts_base, e), &w);
                     one(e++, ok, w);
                 }
             }
@@ -5031,13 +5025,13 @@ __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, 
         if (lane == 0) {
             pp->a = pe.a;
             pp->b = pe.b;
-            if (access && st.pstamp) st.pstamp[pp - st.ptab] = lru_stamp(st, pay[(uint32_t)el[e1 - 1]].idx & F_IDX, 0);
+            if (access && st.pstamp) st.pstamp[pp - st.ptab] = lru_stamp(st, sp[e1 - 1].idx & F_IDX, 0);
             const int d = (pe.a != kPAbsent ? 1 : 0) - (p0 ? 1 : 0);
             if (d && st.psize) atomicAdd(&st.psize[prule.id], (uint32_t)d);
             if (npass) {  // addThreadCount per pass
                 const int64_t ta0 = tp->a;
                 tp->a = (ta0 == kPAbsent ? 0 : ta0) + npass;
-                if (st.tstamp) st.tstamp[key] = lru_stamp(st, pay[(uint32_t)el[last_pass]].idx & F_IDX, 0);
+                if (st.tstamp) st.tstamp[key] = lru_stamp(st, sp[last_pass].idx & F_IDX, 0);
                 if (ta0 == kPAbsent && lru_on_t(st, res)) atomicAdd(&st.tsize[st.tbase[res]], 1u);
             }
         }
@@ -6440,6 +6434,7 @@ int FlowEngine::ensure_scratch() {
                        al(cap * 8) +  // run_asum
                        al((cap / 64 + 2) * sizeof(WinSum)) + al((cap / 64 + 2) * 8) +  // wsum, wstate
                        al(cap * 8) +  // ev_param
+                       al(cap * sizeof(Payload)) +  // spay
                        4 * al((cap / kCbTileMin + 2) * 4) + al((cap / kCbTileMin + 2) * sizeof(CbAgg)) +  // cbt_*
                        al((2 * (cap / kCbRound) + 16) * 4) + al((2 * (cap / kCbRound) + 16) * sizeof(CbTile)) + al(64);
         d_scratch.alloc(bytes);
@@ -6497,6 +6492,7 @@ int FlowEngine::ensure_scratch() {
         sc.wsum = (WinSum *)take((cap / 64 + 2) * sizeof(WinSum));
         sc.wstate = (int64_t *)take((cap / 64 + 2) * 8);
         sc.ev_param = (uint64_t *)take(cap * 8);
+        sc.spay = (Payload *)take(cap * sizeof(Payload));
         {
             const size_t nf = cap / kCbTileMin + 2, nt = 2 * (cap / kCbRound) + 16;
             sc.cbt_flow = (uint32_t *)take(nf * 4);

@@ -219,6 +219,7 @@ struct FlowScratch {
     CbTile *cbt;
     CbAgg *cbt_total;
     uint64_t *pel[2];
+    Payload *spay;  // the per-value segments' payloads in sorted order (k_pseg_gather): one gather, then streams
     uint32_t *seg;
     int64_t *run_pa, *run_ba;
     uint32_t *run_np;
