@@ -4250,12 +4250,20 @@ __device__ __forceinline__ int64_t shfl_up_i64(int64_t v, int o) {
 //    kSegExit / kSegEntry when it holds exits / entries, kSegIrregular when an entry's acquire count differs
 //    from the previous entry's or its time goes back (the closed forms of k_pseg_solve / k_pseg_long need
 //    one acquire count and non-decreasing times)
+//    Each workgroup takes kHeadsChunk consecutive elements and lists its heads in LDS first: one counter atomic
+//    per workgroup (one per wave had all waves of the GPU queue at one address)
 constexpr int64_t kSegExit = 1, kSegEntry = 2, kSegIrregular = 4;
+constexpr uint32_t kHeadsChunk = 4096;
 __global__ __launch_bounds__(kT) void k_pseg_heads(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
                                                    const uint64_t *__restrict__ el, uint32_t m, uint64_t none) {
     if (!gate_is(st.gate, kGateSeq | kGateBad, 0) || sc.counters[11] == 0) return;
+    __shared__ uint32_t hl[kHeadsChunk];
+    __shared__ uint32_t hn, hbase;
+    if (threadIdx.x == 0) hn = 0;
+    __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t e0 = blockIdx.x * kT; e0 < m; e0 += gridDim.x * kT) {  // whole waves in every iteration
+    const uint32_t c0 = blockIdx.x * kHeadsChunk, c1 = min(m, c0 + kHeadsChunk);
+    for (uint32_t e0 = c0; e0 < c1; e0 += kT) {  // whole waves in every iteration
         const uint32_t e = e0 + threadIdx.x;
         const uint64_t x = e < m ? el[e] : none;
         const uint64_t k = x >> 32;
@@ -4271,13 +4279,13 @@ __global__ __launch_bounds__(kT) void k_pseg_heads(FlowState st, FlowScratch sc,
         pq.ts_off = (uint32_t)__shfl_up((int)q.ts_off, 1, 64);
         pq.acq_prio = (uint32_t)__shfl_up((int)q.acq_prio, 1, 64);
         if (lane == 0 && e > 0 && (xp >> 32) != none >> 32) pq = pay[(uint32_t)xp];
-        const uint64_t hb = __ballot(head);  // one counter atomic per wave
+        const uint64_t hb = __ballot(head);  // one LDS atomic per wave
         if (hb) {
             const int first = __ffsll((unsigned long long)hb) - 1;
             uint32_t base = 0;
-            if ((int)lane == first) base = atomicAdd(&sc.counters[12], (uint32_t)__popcll(hb));
+            if ((int)lane == first) base = atomicAdd(&hn, (uint32_t)__popcll(hb));
             base = (uint32_t)__shfl((int)base, first, 64);
-            if (head) sc.seg[base + (uint32_t)__popcll(hb & ((1ull << lane) - 1ull))] = e;
+            if (head) hl[base + (uint32_t)__popcll(hb & ((1ull << lane) - 1ull))] = e;
         }
         const bool valid = k != none >> 32;
         int64_t f = (q.idx & F_EXIT) ? kSegExit : kSegEntry;
@@ -4300,6 +4308,11 @@ __global__ __launch_bounds__(kT) void k_pseg_heads(FlowState st, FlowScratch sc,
         int64_t *w = &st.ttab[k].b;
         if ((*w & fr) != fr) atomicOr((unsigned long long *)w, (unsigned long long)fr);  // a read first: hot segments
     }
+    __syncthreads();
+    const uint32_t n = hn;
+    if (threadIdx.x == 0 && n) hbase = atomicAdd(&sc.counters[12], n);
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < n; t += kT) sc.seg[hbase + t] = hl[t];
 }
 
 // 3. one lane per segment: the value's events in arrival order against its entries held in registers
@@ -6324,7 +6337,8 @@ void FlowEngine::launch_pseg(const FlowState &st, const FlowScratch &g, const Pa
             }
             if (np & 1) std::swap(el, alt);
         }
-        hipLaunchKernelGGL(k_pseg_heads, dim3(nb), dim3(kT), 0, s, st, gs, pay, el, m, none);
+        hipLaunchKernelGGL(k_pseg_heads, dim3((m + kHeadsChunk - 1) / kHeadsChunk), dim3(kT), 0, s, st, gs, pay, el, m,
+                           none);
         static const bool dbg = getenv("SGA_PSEG_DEBUG") && atoi(getenv("SGA_PSEG_DEBUG")) == 1;
         if (dbg) {
             uint32_t h[4] = {0, 0, 0, 0}, *dd = gs.radix.err;  // the radix error words are free here
