@@ -2153,6 +2153,16 @@ __device__ bool lru_ps_take(const FlowState &st, const FlowScratch &sc, const Pa
     return true;
 }
 
+// a list append from divergent lanes: one counter atomic per wave and list (its lowest active lane)
+__device__ __forceinline__ uint32_t wave_append(uint32_t *ctr) {
+    const uint64_t act = __ballot(1);
+    const int lane = (int)(threadIdx.x & 63), lead = __ffsll((unsigned long long)act) - 1;
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(ctr, (uint32_t)__popcll(act));
+    base = (uint32_t)__shfl((int)base, lead, 64);
+    return base + (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
+}
+
 __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, FlowScratch sc,
                                                const Payload *__restrict__ pay, const uint32_t *__restrict__ keys,
                                                int64_t ts_base, const int64_t *__restrict__ rt_in,
@@ -2174,7 +2184,7 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
             if (st.lru_res && st.lru_res[res]) {  // a CacheMap in LRU mode: arrival order, one lane (k_llru)
                 // parameter-only: the chunked replay (k_llru_ps, SGA_LRU_PS=0 turns it off: an A/B knob)
                 const bool ps = !special && st.lru_ps && lru_ps_take(st, sc, pay, res, r0, r1);
-                sc.lru[atomicAdd(&sc.counters[10], 1u)] = fl | (ps ? 0x80000000u : 0u);
+                sc.lru[wave_append(&sc.counters[10])] = fl | (ps ? 0x80000000u : 0u);
                 continue;
             }
             if (special) {
@@ -2187,7 +2197,7 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
                         sc.run_ba[r] = 0;
                         sc.run_np[r] = 0;
                     }
-                    sc.pseg[atomicAdd(&sc.counters[11], 1u)] = fl;
+                    sc.pseg[wave_append(&sc.counters[11])] = fl;
                     continue;
                 }
                 for (uint32_t r = r0; r < r1; ++r)
@@ -2197,24 +2207,24 @@ __global__ __launch_bounds__(kT) void k_lflows(FlowState st, int64_t max_rt, Flo
             int cbk = 0;
             if (sc.pseg && ((cbk = cb_take(st, sc, res, r0, r1)) != 0 ||
                             pseg_take(st, sc, pay, res, r0, r1))) {
-                if (cbk == 2) sc.cbf[atomicAdd(&sc.counters[13], 1u)] = fl;
+                if (cbk == 2) sc.cbf[wave_append(&sc.counters[13])] = fl;
                 for (uint32_t r = r0; r < r1; ++r) {
                     sc.run_mode[r] = RUN_PSEG;
                     sc.run_pa[r] = 0;
                     sc.run_ba[r] = 0;
                     sc.run_np[r] = 0;
                 }
-                sc.pseg[atomicAdd(&sc.counters[11], 1u)] = fl;
+                sc.pseg[wave_append(&sc.counters[11])] = fl;
                 continue;
             }
             if ((st.res[res].fast & 5u) == 0 && nev >= kHeavyEvents) {
-                sc.heavy[atomicAdd(&sc.counters[8], 1u)] = fl;
+                sc.heavy[wave_append(&sc.counters[8])] = fl;
                 continue;
             }
             if ((st.res[res].fast & 5u) && nev >= kWaveEvents) {  // a long single-rule fast path: k_lwave
                 if (st.res[res].fast & 4u)
                     for (uint32_t r = r0; r < r1; ++r) sc.run_mode[r] = RUN_WRL;  // k_lwsum's windows
-                sc.pace[atomicAdd(&sc.counters[9], 1u)] = fl;
+                sc.pace[wave_append(&sc.counters[9])] = fl;
                 continue;
             }
         }
@@ -5236,24 +5246,37 @@ __device__ __forceinline__ bool lru_count_event(const FlowState &st, uint32_t i,
     return need;
 }
 
-// the claim launch (every event; those that marked a slot first into st.lneed, one atomic per wave)
+// the claim launch (every event; those that marked a slot first into st.lneed).  Each workgroup takes kLruChunk
+// consecutive events and lists its own in LDS first: one list atomic per workgroup (one per wave queued the
+// waves of the whole GPU at one address)
+constexpr uint32_t kLruChunk = 4096;
 __global__ __launch_bounds__(kT) void k_lru_claim(FlowState st, const uint8_t *__restrict__ kind,
                                                   const uint32_t *__restrict__ resource,
                                                   const uint8_t *__restrict__ flags,
                                                   const uint64_t *__restrict__ param_in,
                                                   const uint64_t *__restrict__ pvals, uint32_t n) {
+    __shared__ uint32_t ll[kLruChunk];
+    __shared__ uint32_t ln, lbase;
+    if (threadIdx.x == 0) ln = 0;
+    __syncthreads();
     const uint64_t mark = kStampMark | st.seq_base;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t n_up = (n + 63) & ~63u;  // whole waves go round the loop together (the ballot below)
-    for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < n_up; i += gridDim.x * kT) {
-        const bool need = i < n && lru_count_event<false>(st, i, kind, resource, flags, param_in, pvals, mark);
+    const uint32_t c0 = blockIdx.x * kLruChunk, c1 = min(n, c0 + kLruChunk);
+    for (uint32_t i0 = c0; i0 < c1; i0 += kT) {  // whole waves go round the loop together (the ballot below)
+        const uint32_t i = i0 + threadIdx.x;
+        const bool need = i < c1 && lru_count_event<false>(st, i, kind, resource, flags, param_in, pvals, mark);
         const uint64_t bal = __ballot(need);
         if (!bal) continue;
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&st.lru_ctl[2], (uint32_t)__popcll(bal));
+        if (lane == 0) base = atomicAdd(&ln, (uint32_t)__popcll(bal));
         base = __shfl(base, 0);
-        if (need) st.lneed[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = i;
+        if (need) ll[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = i;
     }
+    __syncthreads();
+    const uint32_t cnt = ln;
+    if (threadIdx.x == 0 && cnt) lbase = atomicAdd(&st.lru_ctl[2], cnt);
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < cnt; t += kT) st.lneed[lbase + t] = ll[t];
 }
 
 // the count launch over the listed events
@@ -5758,8 +5781,8 @@ void FlowEngine::lru_prepare(const uint8_t *kind, const uint32_t *resource, cons
     if (d_lneed.n < n) d_lneed.grow(n, s);
     const FlowState st = state();
     const uint32_t nb = std::min<uint32_t>((n + kT - 1) / kT, 2048);
-    hipLaunchKernelGGL(k_lru_claim, dim3(std::max<uint32_t>(nb, 1)), dim3(kT), 0, s, st, kind, resource, flags,
-                       param, pvals, n);
+    hipLaunchKernelGGL(k_lru_claim, dim3(std::max<uint32_t>((n + kLruChunk - 1) / kLruChunk, 1)), dim3(kT), 0, s, st,
+                       kind, resource, flags, param, pvals, n);
     hipLaunchKernelGGL(k_lru_count, dim3(std::max<uint32_t>(nb, 1)), dim3(kT), 0, s, st, kind, resource, flags,
                        param, pvals);
     const uint32_t no = st.nprid + st.ntslot;
