@@ -4219,7 +4219,9 @@ __global__ __launch_bounds__(kT) void k_pseg_key(FlowState st, FlowScratch sc, c
                         ptab_get(st.ptab, st.pmask, st.prules[st.res[res].prule_off].id + 1, v, true, st.overflow);
                     if (!kClaim && te) {
                         el = ((uint64_t)(te - st.ttab) << 32) | j;
-                        if (te->b != 0) te->b = 0;  // the segment's flag word for this batch (k_pseg_heads)
+                        // the segment's flag word: kPAbsent at rest (k_pseg_solve puts it back), k_pseg_heads ORs
+                        // the flags in; only a batch that failed before k_pseg_solve leaves one to reset
+                        if (te->b != kPAbsent) te->b = kPAbsent;
                     } else if (!kClaim) {
                         // every parameter event of a RUN_PSEG flow had its thread-count entry claimed (by the
                         // claim launch, or by k_lru_claim in LRU mode); a missing one would leave the event
@@ -4256,7 +4258,8 @@ __device__ __forceinline__ int64_t shfl_up_i64(int64_t v, int o) {
 
 // 2. segment heads of the sorted elements, the elements' payloads gathered once into sorted order (sc.spay:
 //    every later pass streams them)
-//    and each segment's flag word (the b word of its thread-count entry, which a thread count never uses):
+//    and each segment's flag word (the b word of its thread-count entry, which a thread count never uses: kPAbsent
+//    at rest, the flags ORed into its low bits and k_pseg_solve putting kPAbsent back):
 //    kSegExit / kSegEntry when it holds exits / entries, kSegIrregular when an entry's acquire count differs
 //    from the previous entry's or its time goes back (the closed forms of k_pseg_solve / k_pseg_long need
 //    one acquire count and non-decreasing times)
@@ -4358,7 +4361,7 @@ __global__ __launch_bounds__(kT) void k_pseg_solve(FlowState st, int64_t max_rt,
         bool p0 = false;
         uint64_t pst = 0, tst = 0;  // the last access stamps
         bool more = true;
-        const int64_t flags = tp->b;
+        const int64_t flags = tp->b & (kSegExit | kSegEntry | kSegIrregular);
         tp->b = kPAbsent;  // the flag word back to the thread-count entry's unused value (a present-key count
                            // and a rehash test a != absent || b != absent)
         if (flags == kSegExit || flags == kSegEntry) {
