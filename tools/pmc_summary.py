@@ -202,7 +202,7 @@ def main():
         json.dump({"traffic_bytes_per_step": traffic, "fetch_bytes_per_step": tot["fetch"] * 1e6,
                    "fetch_bytes_per_step_raw": tot["fetch_raw"] * 1e6, "write_bytes_per_step": tot["write"] * 1e6,
                    "kernel_us_per_step": tot["us"], "dispatch_sets": sets, "random_fetch_factor": rand_factor,
-                   "run": os.path.basename(os.path.normpath(a.dir)), "kernels": table,
+                   "run": os.path.basename(os.path.dirname(os.path.normpath(a.dir))), "kernels": table,  # the pmc_configs tag
                    "alg_bytes_per_step": alg_total,
                    "note": "engine kernels only (sga::, per batch); FETCH_SIZE x2 for coalesced streaming kernels, "
                            "x random16_fetch_factor (tools/calib/pmccal.hip) for random-gather kernels; WRITE_SIZE as "
