@@ -48,7 +48,7 @@ constexpr uint32_t kHeavyEvents = 1024;  // per batch: replayed by k_lheavy inst
 #endif
 // per batch: a single-rule fast-path resource decided by one k_lwave wave instead of one k_lflows lane
 // (1024 until round 5; C2 28.0 / 23.0 / 22.3 ms per step at 1024 / 256 / 128: its lanes of 128..1023 events
-// were the k_lflows tail)
+// were the k_lflows tail; round 6: 8.59 / 9.22 ms at 64 / 32 against 8.65 at 128, C5b unchanged -- kept)
 constexpr uint32_t kWaveEvents = SGA_WAVE_EVENTS;
 // RUN_POS: k_lwave left each entry's decision and wait in ev_eidx (wait << 1 | blocked; ~0: written
 // already), k_lresults scatters them in parallel
