@@ -1363,9 +1363,9 @@ __global__ __launch_bounds__(kT) void k_lclassify(FlowState st, FlowScratch sc, 
     const uint8_t fl = flags ? flags[i] : 0;
     const uint8_t kd = kind[i];
     const bool ex = kd == 1;
-    decision[i] = D_PASS;
     wait_ms[i] = 0;
     if (r >= st.nres) {  // unknown resource: no node, no rules (documented)
+        decision[i] = D_PASS;
         keys[i] = st.nres;
         pay[i] = Payload{i, 0, 0, 0};
         return;
@@ -1398,6 +1398,11 @@ __global__ __launch_bounds__(kT) void k_lclassify(FlowState st, FlowScratch sc, 
     const uint32_t a = (uint32_t)acquire[i] & 0x7FFFFFFFu;
     pay[i] = Payload{idx, off, a | ((!ex && !spec && (fl & SGA_EV_PRIORITIZED)) ? 0x80000000u : 0u),
                      (uint32_t)(t / kSecW)};
+    // the default decision: PASS; a parameter entry of a resource with parameter rules starts as a parameter
+    // block, so k_pseg_long writes only its passes (coalesced here instead of a scattered fill of the long
+    // segments' blocks).  Every other path that decides such an entry writes its decision explicitly
+    // (lane_run / k_lheavy / k_llru_ps / k_lseq / k_pseg_solve).
+    decision[i] = (kd == 0 && hp && !spec && st.res[r].n_prules) ? (int8_t)D_BLOCK_PARAM : (int8_t)D_PASS;
 }
 
 // ------------------------------------------------------------------ runs (segmented scan)
@@ -4917,23 +4922,6 @@ __device__ uint32_t pseg_upper(const Payload *__restrict__ sp, int64_t ts_base, 
     const uint64_t b = __ballot(p < hi && pseg_time(sp, ts_base, p) > x);
     return b ? lo + (uint32_t)(__ffsll((unsigned long long)b) - 1) : hi;
 }
-// The long segments' blocks written over the whole GPU ahead of k_pseg_long, which then writes only its passes
-// (a throttle segment passes one entry per stretch: one wave writing every block was most of its time)
-__global__ __launch_bounds__(kT) void k_pseg_prefill(FlowState st, FlowScratch sc, const Payload *__restrict__ pay,
-                                                     const uint64_t *__restrict__ el, int8_t *decision,
-                                                     int32_t *wait_ms) {
-    if (!gate_is(st.gate, kGateSeq | kGateBad, 0)) return;
-    const uint32_t nl = sc.counters[14];
-    for (uint32_t h = blockIdx.y; h < nl; h += gridDim.y) {
-        const uint32_t e0 = sc.plong[2 * h], e1 = e0 + sc.plong[2 * h + 1];
-        for (uint32_t e = e0 + blockIdx.x * kT + threadIdx.x; e < e1; e += gridDim.x * kT) {
-            const uint32_t ix = sc.spay[e].idx & F_IDX;
-            decision[ix] = D_BLOCK_PARAM;
-            wait_ms[ix] = 0;
-        }
-    }
-}
-
 __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, FlowScratch sc,
                                                   const Payload *__restrict__ pay, const uint32_t *__restrict__ keys,
                                                   const uint64_t *__restrict__ el, int64_t ts_base,
@@ -4959,7 +4947,7 @@ __global__ __launch_bounds__(64) void k_pseg_long(FlowState st, int64_t max_rt, 
         const bool p0 = pe.a != kPAbsent;
         int64_t npass = 0;
         uint32_t last_pass = e1;
-        // decisions of [lo, hi) on all lanes (blocks: written already, k_pseg_prefill)
+        // decisions of [lo, hi) on all lanes (blocks: the default k_lclassify wrote)
         auto fill = [&](uint32_t lo, uint32_t hi, bool pass) {
             if (!pass) return;
             const int8_t d = D_PASS;
@@ -6379,8 +6367,6 @@ void FlowEngine::launch_pseg(const FlowState &st, const FlowScratch &g, const Pa
         }
         hipLaunchKernelGGL(k_pseg_solve, dim3(std::min<uint32_t>((m + kT - 1) / kT, 4096)), dim3(kT), 0, s, st,
                            (int64_t)cfg.statistic_max_rt, gs, pay, keys, el, m, ts_base, param, decision, wait_ms);
-        hipLaunchKernelGGL(k_pseg_prefill, dim3(64, std::min<uint32_t>(m / kPsegLong + 1, 64)), dim3(kT), 0, s, st, gs,
-                           pay, el, decision, wait_ms);
         hipLaunchKernelGGL(k_pseg_long, dim3(std::min<uint32_t>(m / kPsegLong + 1, 2048)), dim3(64), 0, s, st,
                            (int64_t)cfg.statistic_max_rt, gs, pay, keys, el, ts_base, param, decision, wait_ms);
     }
