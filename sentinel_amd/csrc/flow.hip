@@ -4339,10 +4339,11 @@ __global__ __launch_bounds__(kT) void k_pseg_heads(FlowState st, FlowScratch sc,
 //    counts written back once (free mode: the count pass keeps these owners below capacity)
 constexpr int kPsegG = 8;       // elements loaded ahead
 #ifndef SGA_PSEG_LONG
-#define SGA_PSEG_LONG 128
+#define SGA_PSEG_LONG 64
 #endif
 constexpr int kPsegLong = SGA_PSEG_LONG;  // regular entry segments this long go to k_pseg_long (C4: 6.17 / 6.04 / 6.21 / 6.45
-                                          // ms per step at 512 / 128 / 64 / 32)
+                                          // ms per step at 512 / 128 / 64 / 32 with the scattered block fill;
+                                          // without it, round-6 end: 3.82 / 3.86 / 4.00 ms at 64 / 128 / 256)
 __global__ __launch_bounds__(kT) void k_pseg_solve(FlowState st, int64_t max_rt, FlowScratch sc,
                                                    const Payload *__restrict__ pay, const uint32_t *__restrict__ keys,
                                                    const uint64_t *__restrict__ el, uint32_t m, int64_t ts_base,
